@@ -1,0 +1,251 @@
+// mxstream — pybind11 bindings of the native engine (_mxs_native).
+//
+// Buffers cross the boundary as integer addresses (torch tensor data_ptr()); the Python layer
+// (mxstream/ops/native.py) owns allocation and validates shapes before every launch, so a
+// kernel never sees an operand whose shape disagrees with its grid.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <stdexcept>
+#include <vector>
+
+#include "mxs_kernels.h"
+#include "mxs_runtime.h"
+
+namespace py = pybind11;
+using namespace mxs;
+
+namespace {
+
+template <class T>
+T* P(intptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+
+ExprProg make_prog(const std::vector<int32_t>& code, const std::vector<double>& consts) {
+  ExprProg p;
+  std::memset(&p, 0, sizeof(p));
+  if (code.size() % 2 != 0) throw std::invalid_argument("expr code must be (op,arg) pairs");
+  if (code.size() > (size_t)2 * kExprMaxCode) throw std::invalid_argument("expr program too long");
+  if (consts.size() > (size_t)kExprMaxConst) throw std::invalid_argument("too many expr consts");
+  // Validate stack discipline so a malformed program can never run off the device stack.
+  int sp = 0;
+  for (size_t i = 0; i < code.size(); i += 2) {
+    const int op = code[i], arg = code[i + 1];
+    if (op == OP_VAR) {
+      if (arg < 0 || arg >= kExprVars) throw std::invalid_argument("expr var out of range");
+      ++sp;
+    } else if (op == OP_CONST) {
+      if (arg < 0 || arg >= (int)consts.size()) throw std::invalid_argument("expr const out of range");
+      ++sp;
+    } else if (op == OP_NOT || op == OP_NEG || op == OP_ABS || op == OP_TOINT) {
+      if (sp < 1) throw std::invalid_argument("expr stack underflow");
+    } else if (op >= OP_ADD && op <= OP_MOD) {
+      if (sp < 2) throw std::invalid_argument("expr stack underflow");
+      --sp;
+    } else {
+      throw std::invalid_argument("unknown expr op");
+    }
+    if (sp > kExprStack) throw std::invalid_argument("expr stack overflow");
+  }
+  if (!code.empty() && sp != 1) throw std::invalid_argument("expr must leave exactly one value");
+  for (size_t i = 0; i < code.size(); ++i) p.code[i] = code[i];
+  for (size_t i = 0; i < consts.size(); ++i) p.consts[i] = consts[i];
+  p.ncode = (int32_t)(code.size() / 2);
+  return p;
+}
+
+PartPlan make_part(py::dict d) {
+  PartPlan p;
+  std::memset(&p, 0, sizeof(p));
+  p.max_parallelism = d["max_parallelism"].cast<int32_t>();
+  p.nsub_log2 = d["nsub_log2"].cast<int32_t>();
+  p.nranks = d["nranks"].cast<int32_t>();
+  p.window_mode = d["window_mode"].cast<int32_t>();
+  p.drop_late = d["drop_late"].cast<int32_t>();
+  p.hash_mode = d["hash_mode"].cast<int32_t>();
+  p.bucket_cap = d["bucket_cap"].cast<uint32_t>();
+  p.wm = d["wm"].cast<int64_t>();
+  p.pane_base = d["pane_base"].cast<int64_t>();
+  p.win.size = d["size"].cast<int64_t>();
+  p.win.slide = d["slide"].cast<int64_t>();
+  p.win.offset = d["offset"].cast<int64_t>();
+  p.win.pane = d["pane"].cast<int64_t>();
+  p.win.lateness = d["lateness"].cast<int64_t>();
+  if (p.window_mode && (p.win.pane <= 0 || p.win.size <= 0 || p.win.slide <= 0))
+    throw std::invalid_argument("window sizes must be positive");
+  if (p.max_parallelism <= 0 || p.nranks <= 0 || p.nsub_log2 < 0 || p.nsub_log2 > 20)
+    throw std::invalid_argument("bad partition plan");
+  return p;
+}
+
+AggPlan make_agg(py::dict d) {
+  AggPlan p;
+  std::memset(&p, 0, sizeof(p));
+  p.cap_log2 = d["cap_log2"].cast<int32_t>();
+  p.nsub = d["nsub"].cast<int32_t>();
+  p.ring = d["ring"].cast<int32_t>();
+  p.agg = d["agg"].cast<int32_t>();
+  p.nsrc = d["nsrc"].cast<int32_t>();
+  p.bucket_cap = d["bucket_cap"].cast<uint32_t>();
+  p.np_step = d["np_step"].cast<int32_t>();
+  p.pg = d["pg"].cast<int32_t>();
+  p.pane_base = d["pane_base"].cast<int64_t>();
+  p.p_lo = d["p_lo"].cast<int64_t>();
+  p.fired_hi = d["fired_hi"].cast<int64_t>();
+  if (p.ring <= 0 || (p.ring & (p.ring - 1))) throw std::invalid_argument("ring must be 2^k");
+  if (p.cap_log2 < 4 || p.cap_log2 > 14) throw std::invalid_argument("cap_log2 out of range");
+  if (p.pg <= 0) throw std::invalid_argument("pg must be positive");
+  return p;
+}
+
+FirePlan make_fire(py::dict d) {
+  FirePlan p;
+  std::memset(&p, 0, sizeof(p));
+  p.agg = d["agg"].cast<int32_t>();
+  p.npanes = d["npanes"].cast<int32_t>();
+  p.ring = d["ring"].cast<int32_t>();
+  p.only_dirty = d["only_dirty"].cast<int32_t>();
+  p.nslots = d["nslots"].cast<int64_t>();
+  p.p0 = d["p0"].cast<int64_t>();
+  p.wstart = d["wstart"].cast<double>();
+  p.wend = d["wend"].cast<double>();
+  p.out_cap = d["out_cap"].cast<uint32_t>();
+  py::tuple m = d["map"].cast<py::tuple>();
+  py::tuple f = d["filt"].cast<py::tuple>();
+  p.map = make_prog(m[0].cast<std::vector<int32_t>>(), m[1].cast<std::vector<double>>());
+  p.filt = make_prog(f[0].cast<std::vector<int32_t>>(), f[1].cast<std::vector<double>>());
+  if (p.npanes <= 0 || p.npanes > p.ring) throw std::invalid_argument("window panes exceed ring");
+  return p;
+}
+
+RollPlan make_roll(py::dict d) {
+  RollPlan p;
+  std::memset(&p, 0, sizeof(p));
+  p.cap_log2 = d["cap_log2"].cast<int32_t>();
+  p.nsub = d["nsub"].cast<int32_t>();
+  p.agg = d["agg"].cast<int32_t>();
+  p.nsrc = d["nsrc"].cast<int32_t>();
+  p.bucket_cap = d["bucket_cap"].cast<uint32_t>();
+  p.emit = d["emit"].cast<int32_t>();
+  return p;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_mxs_native, m) {
+  m.doc() = "mxstream native engine: gfx950 HIP kernels, C++ CPU twins and host runtime";
+  m.attr("REC_BYTES") = (int)sizeof(Rec);
+  m.attr("STAT_COUNT") = kStatCount;
+  m.attr("EXPR_MAX_CODE") = kExprMaxCode;
+  m.attr("EXPR_MAX_CONST") = kExprMaxConst;
+
+  // Pure functions (host) — used for dictionary keys and tests.
+  m.def("flink_murmur", &flink_murmur);
+  m.def("java_long_hash", &java_long_hash);
+  m.def("key_group", &key_group_of_hash);
+  m.def("operator_index", &operator_index);
+  m.def("mix64", &mix64);
+  m.def("window_start", &window_start);
+  m.def("expr_eval", [](std::vector<int32_t> code, std::vector<double> consts, std::vector<double> vars) {
+    ExprProg p = make_prog(code, consts);
+    double v[kExprVars] = {0};
+    for (size_t i = 0; i < vars.size() && i < (size_t)kExprVars; ++i) v[i] = vars[i];
+    return expr_eval(p, v);
+  });
+
+  // ---- GPU ----
+  m.def("gpu_device_count", &gpu::device_count);
+  m.def("gpu_gen_events", [](intptr_t keys, intptr_t ts, intptr_t vals, int64_t n, uint64_t seed,
+                             uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
+                             int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
+                             int32_t val_f64, intptr_t stream) {
+    gpu::gen_events(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), n, seed, stream_id, idx0,
+                    nkeys, ts_base, ts_span, disorder, val_lo, val_span, val_f64, stream);
+  });
+  m.def("gpu_partition", [](intptr_t keys, intptr_t ts, intptr_t vals, intptr_t jhash, int64_t n,
+                            py::dict plan, intptr_t kg_dest, intptr_t cursor, intptr_t out,
+                            intptr_t stats, intptr_t late_idx, uint32_t late_cap, intptr_t stream) {
+    gpu::partition(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), P<int32_t>(jhash), n,
+                   make_part(plan), P<int32_t>(kg_dest), P<uint32_t>(cursor), P<Rec>(out),
+                   P<int64_t>(stats), P<uint32_t>(late_idx), late_cap, stream);
+  });
+  m.def("gpu_window_agg", [](intptr_t recs, intptr_t counts, py::dict plan, intptr_t keys_g,
+                             intptr_t acc_g, intptr_t cnt_g, intptr_t dirty_g, intptr_t occ,
+                             intptr_t flags, intptr_t stream) {
+    gpu::window_agg(P<Rec>(recs), P<uint32_t>(counts), make_agg(plan), P<uint64_t>(keys_g),
+                    P<uint64_t>(acc_g), P<uint32_t>(cnt_g), P<uint8_t>(dirty_g), P<uint32_t>(occ),
+                    P<uint32_t>(flags), stream);
+  });
+  m.def("gpu_window_fire", [](intptr_t keys_g, intptr_t acc_g, intptr_t cnt_g, intptr_t dirty_g,
+                              py::dict plan, intptr_t ok, intptr_t ov, intptr_t oraw, intptr_t oc,
+                              intptr_t on, intptr_t stream) {
+    gpu::window_fire(P<uint64_t>(keys_g), P<uint64_t>(acc_g), P<uint32_t>(cnt_g),
+                     P<uint8_t>(dirty_g), make_fire(plan), P<uint64_t>(ok), P<double>(ov),
+                     P<uint64_t>(oraw), P<uint32_t>(oc), P<uint32_t>(on), stream);
+  });
+  m.def("gpu_rolling", [](intptr_t recs, intptr_t counts, py::dict plan, intptr_t keys_g,
+                          intptr_t acc_g, intptr_t cnt_g, intptr_t occ, intptr_t flags,
+                          intptr_t out_vals, intptr_t stream) {
+    gpu::rolling(P<Rec>(recs), P<uint32_t>(counts), make_roll(plan), P<uint64_t>(keys_g),
+                 P<uint64_t>(acc_g), P<uint32_t>(cnt_g), P<uint32_t>(occ), P<uint32_t>(flags),
+                 P<uint64_t>(out_vals), stream);
+  });
+  m.def("gpu_expr_filter", [](intptr_t x, int64_t n, std::vector<int32_t> code,
+                              std::vector<double> consts, intptr_t keep, intptr_t stream) {
+    gpu::expr_filter(P<double>(x), n, make_prog(code, consts), P<uint8_t>(keep), stream);
+  });
+
+  // ---- CPU twins ----
+  m.def("cpu_gen_events", [](intptr_t keys, intptr_t ts, intptr_t vals, int64_t n, uint64_t seed,
+                             uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
+                             int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
+                             int32_t val_f64) {
+    py::gil_scoped_release nogil;
+    cpu::gen_events(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), n, seed, stream_id, idx0,
+                    nkeys, ts_base, ts_span, disorder, val_lo, val_span, val_f64);
+  });
+  m.def("cpu_partition", [](intptr_t keys, intptr_t ts, intptr_t vals, intptr_t jhash, int64_t n,
+                            py::dict plan, intptr_t kg_dest, intptr_t cursor, intptr_t out,
+                            intptr_t stats, intptr_t late_idx, uint32_t late_cap) {
+    PartPlan pp = make_part(plan);
+    py::gil_scoped_release nogil;
+    cpu::partition(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), P<int32_t>(jhash), n, pp,
+                   P<int32_t>(kg_dest), P<uint32_t>(cursor), P<Rec>(out), P<int64_t>(stats),
+                   P<uint32_t>(late_idx), late_cap);
+  });
+  m.def("cpu_window_agg", [](intptr_t recs, intptr_t counts, py::dict plan, intptr_t keys_g,
+                             intptr_t acc_g, intptr_t cnt_g, intptr_t dirty_g, intptr_t occ,
+                             intptr_t flags) {
+    AggPlan ap = make_agg(plan);
+    py::gil_scoped_release nogil;
+    cpu::window_agg(P<Rec>(recs), P<uint32_t>(counts), ap, P<uint64_t>(keys_g), P<uint64_t>(acc_g),
+                    P<uint32_t>(cnt_g), P<uint8_t>(dirty_g), P<uint32_t>(occ), P<uint32_t>(flags));
+  });
+  m.def("cpu_window_fire", [](intptr_t keys_g, intptr_t acc_g, intptr_t cnt_g, intptr_t dirty_g,
+                              py::dict plan, intptr_t ok, intptr_t ov, intptr_t oraw, intptr_t oc,
+                              intptr_t on) {
+    FirePlan fp = make_fire(plan);
+    py::gil_scoped_release nogil;
+    cpu::window_fire(P<uint64_t>(keys_g), P<uint64_t>(acc_g), P<uint32_t>(cnt_g),
+                     P<uint8_t>(dirty_g), fp, P<uint64_t>(ok), P<double>(ov), P<uint64_t>(oraw),
+                     P<uint32_t>(oc), P<uint32_t>(on));
+  });
+  m.def("cpu_rolling", [](intptr_t recs, intptr_t counts, py::dict plan, intptr_t keys_g,
+                          intptr_t acc_g, intptr_t cnt_g, intptr_t occ, intptr_t flags,
+                          intptr_t out_vals) {
+    RollPlan rp = make_roll(plan);
+    py::gil_scoped_release nogil;
+    cpu::rolling(P<Rec>(recs), P<uint32_t>(counts), rp, P<uint64_t>(keys_g), P<uint64_t>(acc_g),
+                 P<uint32_t>(cnt_g), P<uint32_t>(occ), P<uint32_t>(flags), P<uint64_t>(out_vals));
+  });
+  m.def("cpu_expr_filter", [](intptr_t x, int64_t n, std::vector<int32_t> code,
+                              std::vector<double> consts, intptr_t keep) {
+    ExprProg p = make_prog(code, consts);
+    py::gil_scoped_release nogil;
+    cpu::expr_filter(P<double>(x), n, p, P<uint8_t>(keep));
+  });
+
+  bind_runtime(m);
+}

@@ -1,0 +1,217 @@
+// mxstream — host C++ twins of the gfx950 kernels (kernels_hip.hip).
+//
+// Same arguments, same state layout, same hashing: the CPU engine is the no-GPU execution path
+// (BASELINE config 1 runs here) and the reference the GPU kernels are tested against. Events are
+// processed in arrival order, so float accumulations match Flink's per-record order exactly.
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+#include "mxs_kernels.h"
+
+namespace mxs {
+namespace cpu {
+
+void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
+                uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
+                int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
+                int32_t val_f64) {
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t r = rng64(seed, stream_id, idx0 + (uint64_t)i);
+    const uint64_t r2 = mix64(r);
+    const uint64_t r3 = mix64(r2);
+    keys[i] = (uint64_t)(((unsigned __int128)r * nkeys) >> 64);
+    int64_t t = ts_base +
+                (int64_t)(((unsigned __int128)(uint64_t)i * (uint64_t)ts_span) / (uint64_t)n);
+    if (disorder > 0) t -= (int64_t)(r2 % (uint64_t)(disorder + 1));
+    ts[i] = t;
+    const int64_t v = val_lo + (val_span > 0 ? (int64_t)(r3 % (uint64_t)val_span) : 0);
+    vals[i] = val_f64 ? f64_bits((double)v) : (uint64_t)v;
+  }
+}
+
+void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
+               const int32_t* jhash_tab, int64_t n, const PartPlan& p, const int32_t* kg_dest,
+               uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap) {
+  int64_t tmax = stats[kStatMaxTs], pmin = stats[kStatMinPane], pmax = stats[kStatMaxPane];
+  int64_t nlate = 0, nacc = 0;
+  bool ovf = false;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t key = keys[i];
+    const int64_t t = ts[i];
+    tmax = std::max(tmax, t);
+    uint32_t rt = 0;
+    if (p.window_mode) {
+      if (p.drop_late && element_is_late(t, p.win, p.wm)) {
+        if (late_idx) {
+          const int64_t pos = stats[kStatLate] + nlate;
+          if (pos < (int64_t)late_cap) late_idx[pos] = (uint32_t)i;
+        }
+        ++nlate;
+        continue;
+      }
+      const int64_t pane = pane_of(t, p.win);
+      pmin = std::min(pmin, pane);
+      pmax = std::max(pmax, pane);
+      rt = (uint32_t)(pane - p.pane_base);
+    }
+    ++nacc;
+    const int32_t jh = p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
+    const uint32_t b = bucket_of(key, jh, p, kg_dest);
+    const uint32_t pos = cursor[b]++;
+    if (pos < p.bucket_cap) {
+      Rec& r = out[(size_t)b * p.bucket_cap + pos];
+      r.key = key;
+      r.val = vals[i];
+      r.t = rt;
+      r.aux = (uint32_t)i;
+    } else {
+      ovf = true;
+    }
+  }
+  stats[kStatMaxTs] = tmax;
+  stats[kStatMinPane] = pmin;
+  stats[kStatMaxPane] = pmax;
+  stats[kStatLate] += nlate;
+  stats[kStatAccepted] += nacc;
+  if (ovf) stats[kStatOverflow] |= 1;
+}
+
+static inline uint32_t probe_insert(uint64_t* keys, uint64_t key, uint32_t mask, bool* inserted) {
+  uint32_t s = (uint32_t)mix64(key) & mask;
+  for (uint32_t i = 0; i <= mask; ++i) {
+    const uint64_t k = keys[s];
+    if (k == key) return s;
+    if (k == kEmptyKey) {
+      keys[s] = key;
+      *inserted = true;
+      return s;
+    }
+    s = (s + 1) & mask;
+  }
+  return kNoSlot;
+}
+
+void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p, uint64_t* keys_g,
+                uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g, uint32_t* occupancy,
+                uint32_t* flags) {
+  const uint32_t cap = 1u << p.cap_log2, mask = cap - 1;
+  const size_t nslots = (size_t)p.nsub << p.cap_log2;
+  for (int sub = 0; sub < p.nsub; ++sub) {
+    uint64_t* keys = keys_g + ((size_t)sub << p.cap_log2);
+    bool inserted = false;
+    for (int src = 0; src < p.nsrc; ++src) {
+      uint32_t c = counts[(size_t)src * p.nsub + sub];
+      c = std::min(c, p.bucket_cap);
+      const Rec* seg = recs + ((size_t)src * p.nsub + sub) * p.bucket_cap;
+      for (uint32_t e = 0; e < c; ++e) {
+        const Rec& r = seg[e];
+        const int64_t q = (int64_t)r.t - p.p_lo;
+        if (q < 0 || q >= p.np_step) continue;
+        const uint32_t s = probe_insert(keys, r.key, mask, &inserted);
+        if (s == kNoSlot) {
+          flags[0] |= 1u;
+          continue;
+        }
+        const int64_t pane = p.pane_base + (int64_t)r.t;
+        const size_t gi = (size_t)(pane & (p.ring - 1)) * nslots + ((size_t)sub << p.cap_log2) + s;
+        const uint64_t v = agg_lift(p.agg, r.val);
+        if (p.agg != AGG_COUNT) acc_g[gi] = cnt_g[gi] ? agg_combine(p.agg, acc_g[gi], v) : v;
+        cnt_g[gi] += 1;
+        if (pane <= p.fired_hi) dirty_g[gi] = 1;
+      }
+    }
+    if (inserted) {
+      uint32_t occ = 0;
+      for (uint32_t i = 0; i < cap; ++i) occ += keys[i] != kEmptyKey;
+      occupancy[sub] = occ;
+    }
+  }
+}
+
+void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
+                 const uint8_t* dirty_g, const FirePlan& p, uint64_t* out_keys,
+                 double* out_vals, uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n) {
+  const int64_t nslots = p.nslots;
+  uint32_t n = *out_n;
+  for (int64_t s = 0; s < nslots; ++s) {
+    bool dirty = !p.only_dirty, have = false;
+    uint64_t acc = 0;
+    uint32_t cnt = 0;
+    for (int j = 0; j < p.npanes; ++j) {
+      const size_t gi = (size_t)((p.p0 + j) & (p.ring - 1)) * nslots + s;
+      const uint32_t c = cnt_g[gi];
+      if (c) {
+        acc = have ? agg_combine(p.agg, acc, acc_g[gi]) : acc_g[gi];
+        have = true;
+        cnt += c;
+        if (p.only_dirty && dirty_g[gi]) dirty = true;
+      }
+    }
+    if (!cnt || !dirty) continue;
+    const uint64_t key = keys_g[s];
+    double vars[kExprVars];
+    vars[0] = agg_result_f64(p.agg, acc, cnt);
+    vars[1] = (double)cnt;
+    vars[2] = p.wstart;
+    vars[3] = p.wend;
+    vars[4] = (double)key;
+    vars[5] = (double)(int64_t)acc;
+    vars[6] = p.map.ncode ? expr_eval(p.map, vars) : vars[0];
+    vars[7] = 0.0;
+    const bool emit = p.filt.ncode ? (expr_eval(p.filt, vars) != 0.0) : true;
+    if (!emit) continue;
+    if (n < p.out_cap) {
+      out_keys[n] = key;
+      out_vals[n] = vars[6];
+      out_raw[n] = acc;
+      out_cnt[n] = cnt;
+    }
+    ++n;
+  }
+  *out_n = n;
+}
+
+void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& p, uint64_t* keys_g,
+             uint64_t* acc_g, uint32_t* cnt_g, uint32_t* occupancy, uint32_t* flags,
+             uint64_t* out_vals) {
+  // Ordered per key: records of one sub-table are visited in (src, arrival) order, which is the
+  // order Flink's StreamGroupedReduce sees them on one channel.
+  const uint32_t cap = 1u << p.cap_log2, mask = cap - 1;
+  for (int sub = 0; sub < p.nsub; ++sub) {
+    uint64_t* keys = keys_g + ((size_t)sub << p.cap_log2);
+    bool inserted = false;
+    for (int src = 0; src < p.nsrc; ++src) {
+      uint32_t c = std::min(counts[(size_t)src * p.nsub + sub], p.bucket_cap);
+      const Rec* seg = recs + ((size_t)src * p.nsub + sub) * p.bucket_cap;
+      for (uint32_t e = 0; e < c; ++e) {
+        const Rec& r = seg[e];
+        const uint32_t s = probe_insert(keys, r.key, mask, &inserted);
+        if (s == kNoSlot) {
+          flags[0] |= 1u;
+          continue;
+        }
+        const size_t gi = ((size_t)sub << p.cap_log2) + s;
+        const uint64_t v = agg_lift(p.agg, r.val);
+        acc_g[gi] = cnt_g[gi] ? agg_combine(p.agg, acc_g[gi], v) : v;
+        cnt_g[gi] += 1;
+        if (p.emit && out_vals) out_vals[r.aux] = p.agg == AGG_COUNT ? cnt_g[gi] : acc_g[gi];
+      }
+    }
+    if (inserted) {
+      uint32_t occ = 0;
+      for (uint32_t i = 0; i < cap; ++i) occ += keys[i] != kEmptyKey;
+      occupancy[sub] = occ;
+    }
+  }
+}
+
+void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep) {
+  for (int64_t i = 0; i < n; ++i) {
+    double vars[kExprVars] = {x[i], 0, 0, 0, 0, 0, 0, 0};
+    keep[i] = expr_eval(prog, vars) != 0.0;
+  }
+}
+
+}  // namespace cpu
+}  // namespace mxs

@@ -1,0 +1,544 @@
+// mxstream — CDNA4 (gfx950) kernels for the keyed streaming engine.
+//
+// Design (MI355X-first, see docs/DESIGN.md):
+//   * partition  : keyBy + window assignment + late check in ONE pass. Each 512-thread workgroup
+//                  builds an LDS histogram over (dest rank, sub-table) buckets for its chunk,
+//                  reserves one run per bucket with a single global atomic, then scatters
+//                  24-byte records into fixed-capacity buckets. The send buffer is therefore
+//                  already dest-contiguous with equal splits: the RCCL all-to-all needs no
+//                  host-side count exchange.
+//   * window_agg : one 1024-thread workgroup OWNS one hash sub-table for the whole launch. The
+//                  sub-table's keys and the step's pane deltas live in LDS (ds_cmpst_b64 insert,
+//                  ds_add_u64 / ds_add_f64 / ds_max_i64 accumulation), so there is not a single
+//                  global atomic per event; the deltas are written back with plain coalesced
+//                  read-modify-writes (ownership makes them race-free).
+//   * window_fire: pane-major state => each firing sweeps contiguous slot ranges; the window
+//                  result, the traced map/filter epilogue (ExprProg) and wave-ballot compaction
+//                  are fused into the sweep.
+// Replaces the per-record Flink operators used by the reference: keyBy
+// (chapter2/.../ComputeCpuMax.java:26), WindowOperator + ReducingState
+// (chapter3/.../BandwidthMonitor.java:32-37, BandwidthMonitorWithEventTime.java:45-47),
+// AggregatingState (chapter2/.../ComputeCpuAvg.java:27-59).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <stdexcept>
+#include <string>
+
+#include "mxs_kernels.h"
+
+namespace mxs {
+namespace {
+
+#define HIP_CHECK(x)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ != hipSuccess)                                                                   \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                  \
+  } while (0)
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    int64_t w = __shfl_xor(v, o);
+    v = v > w ? v : w;
+  }
+  return v;
+}
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    int64_t w = __shfl_xor(v, o);
+    v = v < w ? v : w;
+  }
+  return v;
+}
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Order-preserving map double <-> int64 so f64 min/max use the native ds_min_i64/ds_max_i64.
+__device__ __forceinline__ int64_t f64_ord(uint64_t bits) {
+  return (int64_t)(bits ^ ((uint64_t)((int64_t)bits >> 63) & 0x7FFFFFFFFFFFFFFFull));
+}
+__device__ __forceinline__ uint64_t f64_unord(int64_t o) {
+  return (uint64_t)o ^ ((uint64_t)(o >> 63) & 0x7FFFFFFFFFFFFFFFull);
+}
+
+// ------------------------------------------------------------------------------------------
+// Synthetic source: SoA (key, ts, val) batch from a counter-based RNG (device-side so the
+// benchmark measures the engine, not PCIe).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gen_events_kernel(
+    uint64_t* __restrict__ keys, int64_t* __restrict__ ts, uint64_t* __restrict__ vals,
+    int64_t n, uint64_t seed, uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
+    int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span, int32_t val_f64) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t r = rng64(seed, stream_id, idx0 + (uint64_t)i);
+    const uint64_t r2 = mix64(r);
+    const uint64_t r3 = mix64(r2);
+    keys[i] = (uint64_t)(((unsigned __int128)r * nkeys) >> 64);
+    int64_t t = ts_base + (int64_t)(((unsigned __int128)(uint64_t)i * (uint64_t)ts_span) /
+                                    (uint64_t)n);
+    if (disorder > 0) t -= (int64_t)(r2 % (uint64_t)(disorder + 1));
+    ts[i] = t;
+    const int64_t v = val_lo + (val_span > 0 ? (int64_t)(r3 % (uint64_t)val_span) : 0);
+    vals[i] = val_f64 ? f64_bits((double)v) : (uint64_t)v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Partition: keyBy (Flink key groups -> dest rank) x sub-table, window assignment, late drop.
+// ------------------------------------------------------------------------------------------
+struct PartEval {
+  bool keep;
+  uint32_t bucket;
+  uint32_t t;
+};
+
+__device__ __forceinline__ PartEval part_eval(uint64_t key, int64_t t, const int32_t* jhash_tab,
+                                              const PartPlan& p, const int32_t* kg_dest,
+                                              int64_t* pane_out, bool* late_out) {
+  PartEval e;
+  e.keep = true;
+  e.t = 0;
+  *late_out = false;
+  if (p.window_mode) {
+    if (p.drop_late && element_is_late(t, p.win, p.wm)) {
+      e.keep = false;
+      *late_out = true;
+      e.bucket = 0;
+      return e;
+    }
+    const int64_t pane = pane_of(t, p.win);
+    *pane_out = pane;
+    e.t = (uint32_t)(pane - p.pane_base);
+  }
+  const int32_t jh = p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
+  e.bucket = bucket_of(key, jh, p, kg_dest);
+  return e;
+}
+
+__global__ __launch_bounds__(512) void partition_kernel(
+    const uint64_t* __restrict__ keys, const int64_t* __restrict__ ts,
+    const uint64_t* __restrict__ vals, const int32_t* __restrict__ jhash_tab, int64_t n,
+    int64_t chunk, PartPlan plan, const int32_t* __restrict__ kg_dest,
+    uint32_t* __restrict__ cursor, Rec* __restrict__ out, int64_t* __restrict__ stats,
+    uint32_t* __restrict__ late_idx, uint32_t late_cap) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lhist[];
+  const int nb = plan.nranks << plan.nsub_log2;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) lhist[b] = 0;
+  __syncthreads();
+
+  const int64_t start = (int64_t)blockIdx.x * chunk;
+  const int64_t end = start + chunk < n ? start + chunk : n;
+  int64_t tmax = INT64_MIN, pmin = INT64_MAX, pmax = INT64_MIN, nlate = 0, nacc = 0;
+
+  // Pass A: histogram + stats.
+  for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
+    const uint64_t key = keys[i];
+    const int64_t t = ts[i];
+    tmax = t > tmax ? t : tmax;
+    int64_t pane = 0;
+    bool late;
+    PartEval e = part_eval(key, t, jhash_tab, plan, kg_dest, &pane, &late);
+    if (!e.keep) {
+      ++nlate;
+      if (late_idx) {
+        const unsigned long long pos = atomicAdd((unsigned long long*)&stats[kStatLate], 1ull);
+        if (pos < late_cap) late_idx[pos] = (uint32_t)i;
+      }
+      continue;
+    }
+    ++nacc;
+    pmin = pane < pmin ? pane : pmin;
+    pmax = pane > pmax ? pane : pmax;
+    atomicAdd(&lhist[e.bucket], 1u);
+  }
+  __syncthreads();
+
+  // Reserve one run per bucket: a single global atomic per (block, non-empty bucket).
+  bool overflow = false;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    const uint32_t c = lhist[b];
+    if (c) {
+      const uint32_t base = atomicAdd(&cursor[b], c);
+      if (base + c > plan.bucket_cap) overflow = true;
+      lhist[b] = base;
+    }
+  }
+  __syncthreads();
+
+  // Pass B: scatter records into their bucket runs.
+  const uint32_t bcap = plan.bucket_cap;
+  for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
+    const uint64_t key = keys[i];
+    const int64_t t = ts[i];
+    int64_t pane = 0;
+    bool late;
+    PartEval e = part_eval(key, t, jhash_tab, plan, kg_dest, &pane, &late);
+    if (!e.keep) continue;
+    const uint32_t pos = atomicAdd(&lhist[e.bucket], 1u);
+    if (pos < bcap) {
+      Rec r;
+      r.key = key;
+      r.val = vals[i];
+      r.t = e.t;
+      r.aux = (uint32_t)i;
+      out[(size_t)e.bucket * bcap + pos] = r;
+    }
+  }
+
+  // Block stats -> one atomic per wave.
+  tmax = wave_max_i64(tmax);
+  pmin = wave_min_i64(pmin);
+  pmax = wave_max_i64(pmax);
+  nacc = wave_sum_i64(nacc);
+  if (!late_idx) nlate = wave_sum_i64(nlate);
+  const unsigned long long ovf = __ballot(overflow);
+  if (lane_id() == 0) {
+    atomicMax((long long*)&stats[kStatMaxTs], (long long)tmax);
+    if (nacc) {
+      atomicMin((long long*)&stats[kStatMinPane], (long long)pmin);
+      atomicMax((long long*)&stats[kStatMaxPane], (long long)pmax);
+      atomicAdd((unsigned long long*)&stats[kStatAccepted], (unsigned long long)nacc);
+    }
+    if (!late_idx && nlate) atomicAdd((unsigned long long*)&stats[kStatLate], (unsigned long long)nlate);
+    if (ovf) atomicOr((unsigned long long*)&stats[kStatOverflow], 1ull);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// LDS hash sub-table helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lds_probe_insert(uint64_t* skeys, uint64_t key, uint32_t mask,
+                                                     int* inserted) {
+  uint32_t s = (uint32_t)mix64(key) & mask;
+  for (uint32_t i = 0; i <= mask; ++i) {
+    const uint64_t k = *((volatile uint64_t*)&skeys[s]);
+    if (k == key) return s;
+    if (k == kEmptyKey) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&skeys[s], (unsigned long long)kEmptyKey,
+                                      (unsigned long long)key);
+      if (prev == kEmptyKey) {
+        *inserted = 1;
+        return s;
+      }
+      if (prev == key) return s;
+    }
+    s = (s + 1) & mask;
+  }
+  return kNoSlot;
+}
+
+template <int AGG>
+__device__ __forceinline__ int64_t lds_identity() {
+  if (AGG == AGG_MIN_I64 || AGG == AGG_MIN_F64) return INT64_MAX;
+  if (AGG == AGG_MAX_I64 || AGG == AGG_MAX_F64) return INT64_MIN;
+  return 0;
+}
+
+template <int AGG>
+__device__ __forceinline__ void lds_accumulate(uint64_t* a, uint64_t v) {
+  if (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) {
+    atomicAdd((unsigned long long*)a, (unsigned long long)v);
+  } else if (AGG == AGG_SUM_F64 || AGG == AGG_AVG_F64) {
+    atomicAdd((double*)a, as_f64(v));
+  } else if (AGG == AGG_MIN_I64) {
+    atomicMin((long long*)a, (long long)v);
+  } else if (AGG == AGG_MAX_I64) {
+    atomicMax((long long*)a, (long long)v);
+  } else if (AGG == AGG_MIN_F64) {
+    atomicMin((long long*)a, (long long)f64_ord(v));
+  } else if (AGG == AGG_MAX_F64) {
+    atomicMax((long long*)a, (long long)f64_ord(v));
+  }
+  // AGG_COUNT: the count array carries it.
+}
+
+template <int AGG>
+__device__ __forceinline__ uint64_t lds_export(uint64_t a) {
+  if (AGG == AGG_MIN_F64 || AGG == AGG_MAX_F64) return f64_unord((int64_t)a);
+  if (AGG == AGG_COUNT) return 0;
+  return a;
+}
+
+// ------------------------------------------------------------------------------------------
+// Keyed window aggregation: one workgroup per sub-table.
+// LDS image (dynamic, 16-B aligned): keys[cap] u64 | acc[pg][cap] u64 | cnt[pg][cap] u32 | flag
+// ------------------------------------------------------------------------------------------
+template <int AGG>
+__global__ __launch_bounds__(1024) void window_agg_kernel(
+    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
+    uint64_t* __restrict__ keys_g, uint64_t* __restrict__ acc_g, uint32_t* __restrict__ cnt_g,
+    uint8_t* __restrict__ dirty_g, uint32_t* __restrict__ occupancy, uint32_t* __restrict__ flags) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int sub = blockIdx.x;
+  const uint32_t cap = 1u << p.cap_log2;
+  const uint32_t mask = cap - 1;
+  uint64_t* skeys = (uint64_t*)smem;
+  uint64_t* sacc = skeys + cap;
+  uint32_t* scnt = (uint32_t*)(sacc + (size_t)p.pg * cap);
+  int* sflag = (int*)(scnt + (size_t)p.pg * cap);  // [0] inserted, [1] overflow, [2] occupancy
+
+  const size_t sbase = (size_t)sub << p.cap_log2;
+  const size_t nslots = (size_t)p.nsub << p.cap_log2;
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) skeys[i] = keys_g[sbase + i];
+  if (threadIdx.x < 4) sflag[threadIdx.x] = 0;
+
+  int inserted = 0;
+  bool ovf = false;
+  for (int pg0 = 0; pg0 < p.np_step; pg0 += p.pg) {
+    const int npg = (p.np_step - pg0) < p.pg ? (p.np_step - pg0) : p.pg;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)npg * cap; i += blockDim.x) {
+      sacc[i] = (uint64_t)lds_identity<AGG>();
+      scnt[i] = 0;
+    }
+    __syncthreads();
+    const int64_t q0 = p.p_lo + pg0;  // relative pane of LDS row 0
+    for (int src = 0; src < p.nsrc; ++src) {
+      uint32_t c = counts[(size_t)src * p.nsub + sub];
+      c = c < p.bucket_cap ? c : p.bucket_cap;
+      const Rec* seg = recs + ((size_t)src * p.nsub + sub) * p.bucket_cap;
+      for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
+        const Rec r = seg[e];
+        const int64_t q = (int64_t)r.t - q0;
+        if (q < 0 || q >= npg) continue;
+        const uint32_t s = lds_probe_insert(skeys, r.key, mask, &inserted);
+        if (s == kNoSlot) {
+          ovf = true;
+          continue;
+        }
+        const uint32_t li = (uint32_t)q * cap + s;
+        lds_accumulate<AGG>(&sacc[li], r.val);
+        atomicAdd(&scnt[li], 1u);
+      }
+    }
+    __syncthreads();
+    // Write back the deltas of touched slots (this workgroup owns these slots: plain RMW).
+    for (uint32_t i = threadIdx.x; i < (uint32_t)npg * cap; i += blockDim.x) {
+      const uint32_t dc = scnt[i];
+      if (!dc) continue;
+      const uint32_t q = i >> p.cap_log2;
+      const uint32_t s = i & mask;
+      const int64_t pane = p.pane_base + q0 + q;
+      const size_t gi = (size_t)(pane & (p.ring - 1)) * nslots + sbase + s;
+      const uint64_t d = lds_export<AGG>(sacc[i]);
+      const uint32_t oc = cnt_g[gi];
+      if (AGG != AGG_COUNT) acc_g[gi] = oc ? agg_combine(AGG, acc_g[gi], d) : d;
+      cnt_g[gi] = oc + dc;
+      if (pane <= p.fired_hi) dirty_g[gi] = 1;
+    }
+    __syncthreads();
+  }
+  if (inserted) sflag[0] = 1;
+  if (ovf) sflag[1] = 1;
+  __syncthreads();
+  if (sflag[0]) {
+    for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
+      const uint64_t k = skeys[i];
+      keys_g[sbase + i] = k;
+      if (k != kEmptyKey) atomicAdd(&sflag[2], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) occupancy[sub] = (uint32_t)sflag[2];
+  }
+  if (threadIdx.x == 0 && sflag[1]) atomicOr(&flags[0], 1u);
+}
+
+// ------------------------------------------------------------------------------------------
+// Window firing: sweep slots (pane-major => coalesced), combine the window's panes, evaluate
+// the fused map/filter epilogue and compact the emitted rows with one atomic per wave.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void window_fire_kernel(
+    const uint64_t* __restrict__ keys_g, const uint64_t* __restrict__ acc_g,
+    const uint32_t* __restrict__ cnt_g, const uint8_t* __restrict__ dirty_g, FirePlan p,
+    uint64_t* __restrict__ out_keys, double* __restrict__ out_vals, uint64_t* __restrict__ out_raw,
+    uint32_t* __restrict__ out_cnt, uint32_t* __restrict__ out_n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t nslots = p.nslots;
+  // Uniform trip count so every lane reaches the ballot.
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nslots; base += stride) {
+    const int64_t s = base + threadIdx.x;
+    bool emit = false;
+    uint64_t acc = 0, key = 0;
+    uint32_t cnt = 0;
+    double val = 0.0;
+    if (s < nslots) {
+      bool dirty = !p.only_dirty;
+      bool have = false;
+      for (int j = 0; j < p.npanes; ++j) {
+        const size_t gi = (size_t)((p.p0 + j) & (p.ring - 1)) * nslots + s;
+        const uint32_t c = cnt_g[gi];
+        if (c) {
+          const uint64_t a = acc_g[gi];
+          acc = have ? agg_combine(p.agg, acc, a) : a;
+          have = true;
+          cnt += c;
+          if (p.only_dirty && dirty_g[gi]) dirty = true;
+        }
+      }
+      if (cnt && dirty) {
+        key = keys_g[s];
+        double vars[kExprVars];
+        vars[0] = agg_result_f64(p.agg, acc, cnt);
+        vars[1] = (double)cnt;
+        vars[2] = p.wstart;
+        vars[3] = p.wend;
+        vars[4] = (double)key;
+        vars[5] = (double)(int64_t)acc;
+        vars[6] = p.map.ncode ? expr_eval(p.map, vars) : vars[0];
+        vars[7] = 0.0;
+        val = vars[6];
+        emit = p.filt.ncode ? (expr_eval(p.filt, vars) != 0.0) : true;
+      }
+    }
+    const unsigned long long m = __ballot(emit);
+    if (m) {
+      uint32_t wbase = 0;
+      if (lane_id() == 0) wbase = atomicAdd(out_n, (uint32_t)__popcll(m));
+      wbase = __shfl(wbase, 0);
+      if (emit) {
+        const uint32_t pos = wbase + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+        if (pos < p.out_cap) {
+          out_keys[pos] = key;
+          out_vals[pos] = val;
+          out_raw[pos] = acc;
+          out_cnt[pos] = cnt;
+        }
+      }
+    }
+  }
+}
+
+// Stateless predicate (chapter1 filter `usage > 90`, Main.java:31) over one f64 column.
+__global__ __launch_bounds__(256) void expr_filter_kernel(const double* __restrict__ x, int64_t n,
+                                                          ExprProg prog, uint8_t* __restrict__ keep) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    double vars[kExprVars] = {x[i], 0, 0, 0, 0, 0, 0, 0};
+    keep[i] = expr_eval(prog, vars) != 0.0;
+  }
+}
+
+int grid_for(int64_t n, int block, int max_blocks) {
+  int64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  return (int)(g < max_blocks ? g : max_blocks);
+}
+
+}  // namespace
+
+namespace gpu {
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
+                uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
+                int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
+                int32_t val_f64, intptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gen_events_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, keys, ts, vals, n, seed, stream_id, idx0, nkeys, ts_base,
+                     ts_span, disorder, val_lo, val_span, val_f64);
+  HIP_CHECK(hipGetLastError());
+}
+
+void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
+               const int32_t* jhash_tab, int64_t n, const PartPlan& plan, const int32_t* kg_dest,
+               uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap,
+               intptr_t stream) {
+  if (n <= 0) return;
+  const int nb = plan.nranks << plan.nsub_log2;
+  if (nb > 16384) throw std::runtime_error("partition: too many buckets (max 16384)");
+  // ~8K events per workgroup keeps runs per bucket long while filling 256 CUs x 4.
+  int blocks = grid_for(n, 8192, 2048);
+  if (blocks < 256 && n > 256 * 1024) blocks = 256;
+  const int64_t chunk = (n + blocks - 1) / blocks;
+  hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(512), (size_t)nb * 4,
+                     (hipStream_t)stream, keys, ts, vals, jhash_tab, n, chunk, plan, kg_dest,
+                     cursor, out, stats, late_idx, late_cap);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <int AGG>
+static void launch_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p,
+                       uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
+                       uint32_t* occ, uint32_t* flags, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL(window_agg_kernel<AGG>, dim3(p.nsub), dim3(1024), lds, s, recs, counts, p,
+                     keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+}
+
+void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& plan, uint64_t* keys_g,
+                uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g, uint32_t* occupancy,
+                uint32_t* flags, intptr_t stream) {
+  if (plan.np_step <= 0 || plan.nsub <= 0) return;
+  const size_t cap = (size_t)1 << plan.cap_log2;
+  const size_t lds = cap * 8 + (size_t)plan.pg * cap * 12 + 16;
+  if (lds > 160 * 1024) throw std::runtime_error("window_agg: LDS image exceeds 160 KiB");
+  static bool attr_set = false;
+  if (!attr_set) {
+    // Allow the full 160 KiB LDS for every instantiation.
+#define MXS_SET_ATTR(A)                                                                     \
+  HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<A>,                           \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    MXS_SET_ATTR(AGG_SUM_I64) MXS_SET_ATTR(AGG_SUM_F64) MXS_SET_ATTR(AGG_MIN_I64)
+    MXS_SET_ATTR(AGG_MAX_I64) MXS_SET_ATTR(AGG_MIN_F64) MXS_SET_ATTR(AGG_MAX_F64)
+    MXS_SET_ATTR(AGG_COUNT) MXS_SET_ATTR(AGG_AVG_F64) MXS_SET_ATTR(AGG_AVG_I64)
+#undef MXS_SET_ATTR
+    attr_set = true;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  switch (plan.agg) {
+    case AGG_SUM_I64: launch_agg<AGG_SUM_I64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
+    case AGG_SUM_F64: launch_agg<AGG_SUM_F64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
+    case AGG_MIN_I64: launch_agg<AGG_MIN_I64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
+    case AGG_MAX_I64: launch_agg<AGG_MAX_I64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
+    case AGG_MIN_F64: launch_agg<AGG_MIN_F64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
+    case AGG_MAX_F64: launch_agg<AGG_MAX_F64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
+    case AGG_COUNT: launch_agg<AGG_COUNT>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
+    case AGG_AVG_F64: launch_agg<AGG_AVG_F64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
+    case AGG_AVG_I64: launch_agg<AGG_AVG_I64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
+    default: throw std::runtime_error("window_agg: unknown aggregate");
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
+                 const uint8_t* dirty_g, const FirePlan& plan, uint64_t* out_keys,
+                 double* out_vals, uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n,
+                 intptr_t stream) {
+  if (plan.nslots <= 0) return;
+  hipLaunchKernelGGL(window_fire_kernel, dim3(grid_for(plan.nslots, 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, keys_g, acc_g, cnt_g, dirty_g, plan, out_keys, out_vals,
+                     out_raw, out_cnt, out_n);
+  HIP_CHECK(hipGetLastError());
+}
+
+void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep,
+                 intptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(expr_filter_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, x, n, prog, keep);
+  HIP_CHECK(hipGetLastError());
+}
+
+void rolling(const Rec*, const uint32_t*, const RollPlan&, uint64_t*, uint64_t*, uint32_t*,
+             uint32_t*, uint32_t*, uint64_t*, intptr_t) {
+  throw std::runtime_error("rolling: GPU kernel not built yet");
+}
+
+}  // namespace gpu
+}  // namespace mxs

@@ -1,0 +1,331 @@
+// mxstream — shared host/device definitions.
+//
+// Everything in this header is compiled twice: once into the gfx950 code object (HIP kernels in
+// kernels_hip.hip) and once into the host C++ twins (kernels_cpu.cpp), so the CPU engine and the
+// GPU engine compute bit-identical key groups, sub-table ids, pane ids and expression results.
+//
+// Flink parity notes:
+//   * key group   = murmur(javaHash(key)) % maxParallelism   (Flink KeyGroupRangeAssignment)
+//   * subtask     = kg * parallelism / maxParallelism          (operatorIndex)
+//   * window start= ts - (ts - offset + size) % size           (TimeWindow.getWindowStartWithOffset)
+//   * late        = lastWindow.maxTs + allowedLateness <= wm   (WindowOperator.isElementLate, all windows)
+// Reference call sites: chapter2/src/main/java/me/zjy/ComputeCpuMax.java:26 (keyBy),
+// chapter3/src/main/java/me/zjy/BandwidthMonitorWithEventTime.java:46 (sliding event-time window).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define MXS_HD __host__ __device__ __forceinline__
+#else
+#define MXS_HD inline
+#endif
+
+namespace mxs {
+
+// Empty slot marker of the keyed hash tables. User keys are 64-bit ids (integer keys, or string
+// dictionary ids assigned by the host); the all-ones id is reserved.
+constexpr uint64_t kEmptyKey = ~0ull;
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+
+// Shuffle / bucket record: 24 bytes, AoS so one all-to-all moves a whole bucket range.
+//   key : 64-bit key id
+//   val : 64-bit payload (int64 or float64 bit pattern)
+//   t   : pane id relative to the step's pane base (window ops) or ts relative to ts base
+//   aux : original index of the event inside its source batch (ordered operators) / user field
+struct alignas(8) Rec {
+  uint64_t key;
+  uint64_t val;
+  uint32_t t;
+  uint32_t aux;
+};
+static_assert(sizeof(Rec) == 24, "Rec must be 24 bytes");
+
+// ---------------------------------------------------------------------------------------------
+// Java / Flink hashing
+// ---------------------------------------------------------------------------------------------
+MXS_HD int32_t rotl32(int32_t x, int r) {
+  uint32_t u = (uint32_t)x;
+  return (int32_t)((u << r) | (u >> (32 - r)));
+}
+
+// Flink MathUtils.murmurHash(int) — returns a non-negative int.
+MXS_HD int32_t flink_murmur(int32_t code) {
+  uint32_t h = (uint32_t)code;
+  h *= 0xcc9e2d51u;
+  h = (uint32_t)rotl32((int32_t)h, 15);
+  h *= 0x1b873593u;
+  h = (uint32_t)rotl32((int32_t)h, 13);
+  h = h * 5u + 0xe6546b64u;
+  h ^= 4u;
+  // bitMix (fmix32)
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  int32_t c = (int32_t)h;
+  if (c >= 0) return c;
+  if (c != (int32_t)0x80000000) return -c;
+  return 0;
+}
+
+// java.lang.Long.hashCode
+MXS_HD int32_t java_long_hash(int64_t v) {
+  uint64_t u = (uint64_t)v;
+  return (int32_t)(uint32_t)(u ^ (u >> 32));
+}
+
+MXS_HD int32_t key_group_of_hash(int32_t java_hash, int32_t max_parallelism) {
+  return flink_murmur(java_hash) % max_parallelism;
+}
+
+MXS_HD int32_t operator_index(int32_t key_group, int32_t parallelism, int32_t max_parallelism) {
+  return (int32_t)(((int64_t)key_group * parallelism) / max_parallelism);
+}
+
+// splitmix64 finaliser: the engine-internal hash that picks the sub-table (top bits) and the
+// probe start (low bits) — independent of the Flink key-group hash so that every rank's
+// sub-tables stay balanced whatever key groups it owns.
+MXS_HD uint64_t mix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+
+// Counter-based RNG for the synthetic source (stateless, reproducible for any G / batch split).
+MXS_HD uint64_t rng64(uint64_t seed, uint64_t stream, uint64_t idx) {
+  return mix64(mix64(seed ^ (stream * 0xd1b54a32d192ed03ull)) + idx * 0x9e3779b97f4a7c15ull);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Window math (Flink 1.8 TimeWindow semantics, Java '%' = truncated remainder)
+// ---------------------------------------------------------------------------------------------
+MXS_HD int64_t window_start(int64_t ts, int64_t offset, int64_t size) {
+  return ts - (ts - offset + size) % size;
+}
+
+// Floor division for pane ids (panes are a partition of the time axis, also for ts < 0).
+MXS_HD int64_t floor_div(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+  return q;
+}
+
+// Window-assignment parameters shared by the partition pass and the fire pass.
+struct WinParams {
+  int64_t size;       // window size (ms)
+  int64_t slide;      // slide (ms); == size for tumbling
+  int64_t offset;     // window offset (ms)
+  int64_t pane;       // pane length = gcd(size, slide)
+  int64_t lateness;   // allowed lateness (ms)
+};
+
+// True iff every window the element belongs to is already past its cleanup time.
+MXS_HD bool element_is_late(int64_t ts, const WinParams& w, int64_t wm) {
+  const int64_t last_start = window_start(ts, w.offset, w.slide);
+  const int64_t cleanup = last_start + w.size - 1 + w.lateness;
+  return cleanup <= wm;
+}
+
+MXS_HD int64_t pane_of(int64_t ts, const WinParams& w) { return floor_div(ts - w.offset, w.pane); }
+
+// ---------------------------------------------------------------------------------------------
+// Aggregation kinds
+// ---------------------------------------------------------------------------------------------
+enum AggKind : int32_t {
+  AGG_SUM_I64 = 0,
+  AGG_SUM_F64 = 1,
+  AGG_MIN_I64 = 2,
+  AGG_MAX_I64 = 3,
+  AGG_MIN_F64 = 4,
+  AGG_MAX_F64 = 5,
+  AGG_COUNT = 6,  // value ignored, result = count
+  AGG_AVG_F64 = 7,  // acc = sum f64, result = sum / count (ComputeCpuAvg.java:47-50)
+  AGG_AVG_I64 = 8,  // acc = sum i64, result = (double)sum / count
+};
+
+MXS_HD bool agg_is_f64(int32_t k) {
+  return k == AGG_SUM_F64 || k == AGG_MIN_F64 || k == AGG_MAX_F64 || k == AGG_AVG_F64;
+}
+
+MXS_HD double as_f64(uint64_t bits) {
+  union { uint64_t u; double d; } c;
+  c.u = bits;
+  return c.d;
+}
+MXS_HD uint64_t f64_bits(double d) {
+  union { uint64_t u; double d; } c;
+  c.d = d;
+  return c.u;
+}
+
+// Combine two partial accumulators (host side and device write-back).
+MXS_HD uint64_t agg_combine(int32_t k, uint64_t a, uint64_t b) {
+  switch (k) {
+    case AGG_SUM_I64:
+    case AGG_AVG_I64:
+    case AGG_COUNT:
+      return (uint64_t)((int64_t)a + (int64_t)b);
+    case AGG_SUM_F64:
+    case AGG_AVG_F64:
+      return f64_bits(as_f64(a) + as_f64(b));
+    case AGG_MIN_I64:
+      return ((int64_t)a < (int64_t)b) ? a : b;
+    case AGG_MAX_I64:
+      return ((int64_t)a > (int64_t)b) ? a : b;
+    case AGG_MIN_F64:
+      return (as_f64(a) < as_f64(b)) ? a : b;
+    case AGG_MAX_F64:
+      return (as_f64(a) > as_f64(b)) ? a : b;
+  }
+  return a;
+}
+
+// The accumulator value a single element contributes.
+MXS_HD uint64_t agg_lift(int32_t k, uint64_t v) { return k == AGG_COUNT ? 1ull : v; }
+
+// Final window result as double (what getResult / the chained map sees).
+MXS_HD double agg_result_f64(int32_t k, uint64_t acc, uint32_t cnt) {
+  switch (k) {
+    case AGG_SUM_F64:
+    case AGG_MIN_F64:
+    case AGG_MAX_F64:
+      return as_f64(acc);
+    case AGG_AVG_F64:
+      return cnt == 0 ? 0.0 : as_f64(acc) / (double)cnt;
+    case AGG_AVG_I64:
+      return cnt == 0 ? 0.0 : (double)(int64_t)acc / (double)cnt;
+    case AGG_COUNT:
+      return (double)cnt;
+    default:
+      return (double)(int64_t)acc;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Expression VM — the planner traces user map/filter lambdas (e.g. the Mbps map + `< 100` filter
+// of BandwidthMonitorWithEventTime.java:48-55) into this bytecode; the fire kernel and the
+// stateless filter kernel evaluate it per row. Java double semantics: every op rounds once, no
+// contraction (kernels are built with -ffp-contract=off).
+// ---------------------------------------------------------------------------------------------
+enum ExprOp : int32_t {
+  OP_END = 0,
+  OP_VAR = 1,    // push vars[arg]
+  OP_CONST = 2,  // push consts[arg]
+  OP_ADD = 3,
+  OP_SUB = 4,
+  OP_MUL = 5,
+  OP_DIV = 6,
+  OP_LT = 7,
+  OP_LE = 8,
+  OP_GT = 9,
+  OP_GE = 10,
+  OP_EQ = 11,
+  OP_NE = 12,
+  OP_AND = 13,
+  OP_OR = 14,
+  OP_NOT = 15,
+  OP_NEG = 16,
+  OP_ABS = 17,
+  OP_MIN = 18,
+  OP_MAX = 19,
+  OP_MOD = 20,   // Java double %, fmod
+  OP_TOINT = 21, // (long) cast toward zero
+};
+
+constexpr int kExprMaxCode = 64;
+constexpr int kExprMaxConst = 16;
+constexpr int kExprStack = 16;
+
+// Variables visible to window epilogues:
+//   0 = aggregated result (double), 1 = count, 2 = window start, 3 = window end,
+//   4 = key (as double), 5 = raw accumulator as integer (double), 6 = previous program's output
+constexpr int kExprVars = 8;
+
+struct ExprProg {
+  int32_t code[kExprMaxCode];  // (op, arg) pairs
+  double consts[kExprMaxConst];
+  int32_t ncode;               // number of (op,arg) pairs; 0 = empty program
+  int32_t pad;
+};
+
+MXS_HD double expr_eval(const ExprProg& p, const double* vars) {
+  double st[kExprStack];
+  int sp = 0;
+  for (int i = 0; i < p.ncode; ++i) {
+    const int32_t op = p.code[2 * i];
+    const int32_t arg = p.code[2 * i + 1];
+    switch (op) {
+      case OP_VAR: st[sp++] = vars[arg]; break;
+      case OP_CONST: st[sp++] = p.consts[arg]; break;
+      case OP_NOT: st[sp - 1] = (st[sp - 1] == 0.0) ? 1.0 : 0.0; break;
+      case OP_NEG: st[sp - 1] = -st[sp - 1]; break;
+      case OP_ABS: st[sp - 1] = st[sp - 1] < 0 ? -st[sp - 1] : st[sp - 1]; break;
+      case OP_TOINT: st[sp - 1] = (double)(int64_t)st[sp - 1]; break;
+      default: {
+        const double b = st[--sp];
+        const double a = st[sp - 1];
+        double r = 0.0;
+        switch (op) {
+          case OP_ADD: r = a + b; break;
+          case OP_SUB: r = a - b; break;
+          case OP_MUL: r = a * b; break;
+          case OP_DIV: r = a / b; break;
+          case OP_LT: r = a < b; break;
+          case OP_LE: r = a <= b; break;
+          case OP_GT: r = a > b; break;
+          case OP_GE: r = a >= b; break;
+          case OP_EQ: r = a == b; break;
+          case OP_NE: r = a != b; break;
+          case OP_AND: r = (a != 0.0) && (b != 0.0); break;
+          case OP_OR: r = (a != 0.0) || (b != 0.0); break;
+          case OP_MIN: r = a < b ? a : b; break;
+          case OP_MAX: r = a > b ? a : b; break;
+#if defined(__HIP_DEVICE_COMPILE__)
+          case OP_MOD: r = fmod(a, b); break;
+#else
+          case OP_MOD: r = __builtin_fmod(a, b); break;
+#endif
+          default: break;
+        }
+        st[sp - 1] = r;
+      }
+    }
+  }
+  return sp > 0 ? st[sp - 1] : 0.0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Partition plan (keyBy + window assignment + late check) shared by CPU and GPU.
+// ---------------------------------------------------------------------------------------------
+struct PartPlan {
+  int32_t max_parallelism;   // Flink maxParallelism (128 by default)
+  int32_t nsub_log2;         // sub-tables per rank = 1 << nsub_log2
+  int32_t nranks;            // G (destination ranks)
+  int32_t window_mode;       // 0 = keyed (no window, t = 0), 1 = windowed (t = pane - pane_base)
+  int32_t drop_late;         // 1: late elements are dropped (and optionally side-output)
+  int32_t hash_mode;         // 0: Long.hashCode(key); 1: jhash table lookup (string dict ids)
+  uint32_t bucket_cap;       // fixed capacity of one (dest, sub) bucket in the send buffer
+  uint32_t pad0;
+  int64_t wm;                // current watermark (late check)
+  int64_t pane_base;         // records carry pane - pane_base
+  WinParams win;
+};
+
+MXS_HD uint32_t bucket_of(uint64_t key, int32_t jhash, const PartPlan& p, const int32_t* kg_dest) {
+  const int32_t kg = key_group_of_hash(jhash, p.max_parallelism);
+  const int32_t dest = kg_dest[kg];
+  const uint32_t sub = p.nsub_log2 == 0 ? 0u : (uint32_t)(mix64(key) >> (64 - p.nsub_log2));
+  return ((uint32_t)dest << p.nsub_log2) | sub;
+}
+
+// Stats block written by the partition pass (all int64):
+//   [0] max ts (all events, used for the watermark)    [1] min pane of non-late events
+//   [2] max pane of non-late events                     [3] late (dropped) events
+//   [4] overflow flag (bucket capacity exceeded)        [5] events accepted
+constexpr int kStatMaxTs = 0, kStatMinPane = 1, kStatMaxPane = 2, kStatLate = 3, kStatOverflow = 4,
+              kStatAccepted = 5, kStatCount = 8;
+
+}  // namespace mxs

@@ -1,0 +1,100 @@
+// mxstream — kernel launcher interface (GPU: kernels_hip.hip, CPU twins: kernels_cpu.cpp).
+//
+// All buffers are raw pointers owned by the caller (torch tensors on the Python side); `stream`
+// is a hipStream_t passed as an integer. The CPU twins take the same arguments (stream ignored)
+// and are bit-compatible with the GPU kernels for integer aggregates; float sums are exact on
+// CPU (arrival order) and order-independent up to rounding on GPU.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mxs_common.h"
+
+namespace mxs {
+
+// Plan of the keyed-window aggregation pass (one workgroup per sub-table on the GPU).
+struct AggPlan {
+  int32_t cap_log2;     // slots per sub-table = 1 << cap_log2
+  int32_t nsub;         // sub-tables on this rank
+  int32_t ring;         // pane ring length R (power of two)
+  int32_t agg;          // AggKind
+  int32_t nsrc;         // number of source segments per sub-table (G after the all-to-all)
+  uint32_t bucket_cap;  // capacity of one (src, sub) segment
+  int32_t np_step;      // panes touched by this step: [pane_base + p_lo, + np_step)
+  int32_t pg;           // panes staged in LDS per pass (GPU only)
+  int64_t pane_base;    // records carry pane - pane_base
+  int64_t p_lo;         // first pane (relative to pane_base) touched this step
+  int64_t fired_hi;     // absolute pane id: panes <= fired_hi are in an already-fired window
+};
+
+// Plan of one window firing.
+struct FirePlan {
+  int32_t agg;
+  int32_t npanes;       // panes combined by the window
+  int32_t ring;
+  int32_t only_dirty;   // 1: re-fire only slots touched by late data
+  int64_t nslots;       // nsub << cap_log2
+  int64_t p0;           // first absolute pane of the window
+  double wstart, wend;  // window bounds (ms) for the epilogue vars
+  uint32_t out_cap;
+  uint32_t pad;
+  ExprProg map;         // value epilogue (empty = identity)
+  ExprProg filt;        // predicate on the mapped value (empty = true)
+};
+
+// Rolling keyed state plan (ValueState / rolling reduce, no windows).
+struct RollPlan {
+  int32_t cap_log2;
+  int32_t nsub;
+  int32_t agg;
+  int32_t nsrc;
+  uint32_t bucket_cap;
+  int32_t emit;         // 1: write the post-update value of every record (ordered operators)
+};
+
+// ---- GPU launchers (kernels_hip.hip) --------------------------------------------------------
+namespace gpu {
+int device_count();
+void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
+                uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
+                int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
+                int32_t val_f64, intptr_t stream);
+void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
+               const int32_t* jhash_tab, int64_t n, const PartPlan& plan, const int32_t* kg_dest,
+               uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap,
+               intptr_t stream);
+void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& plan, uint64_t* keys_g,
+                uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g, uint32_t* occupancy,
+                uint32_t* flags, intptr_t stream);
+void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
+                 const uint8_t* dirty_g, const FirePlan& plan, uint64_t* out_keys,
+                 double* out_vals, uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n,
+                 intptr_t stream);
+void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& plan, uint64_t* keys_g,
+             uint64_t* acc_g, uint32_t* cnt_g, uint32_t* occupancy, uint32_t* flags,
+             uint64_t* out_vals, intptr_t stream);
+void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep, intptr_t stream);
+}  // namespace gpu
+
+// ---- CPU twins (kernels_cpu.cpp) ------------------------------------------------------------
+namespace cpu {
+void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
+                uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
+                int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
+                int32_t val_f64);
+void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
+               const int32_t* jhash_tab, int64_t n, const PartPlan& plan, const int32_t* kg_dest,
+               uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap);
+void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& plan, uint64_t* keys_g,
+                uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g, uint32_t* occupancy,
+                uint32_t* flags);
+void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
+                 const uint8_t* dirty_g, const FirePlan& plan, uint64_t* out_keys,
+                 double* out_vals, uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n);
+void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& plan, uint64_t* keys_g,
+             uint64_t* acc_g, uint32_t* cnt_g, uint32_t* occupancy, uint32_t* flags,
+             uint64_t* out_vals);
+void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep);
+}  // namespace cpu
+
+}  // namespace mxs

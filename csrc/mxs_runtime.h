@@ -1,0 +1,6 @@
+// mxstream — host runtime (C++): string dictionary, Java-compatible text parsing, socket
+// source, key-group-indexed checkpoint files.
+#pragma once
+#include <pybind11/pybind11.h>
+
+void bind_runtime(pybind11::module_& m);

@@ -1,0 +1,644 @@
+// mxstream — host runtime components (C++).
+//
+//  * StringDict      : interns string keys to dense 64-bit ids and records their Java
+//                      String.hashCode (UTF-16), so keyBy on a String field reproduces Flink's key
+//                      groups (ComputeCpuMax.java:26 keyBy(0) -> Tuple1<String>.hashCode()).
+//  * parse_lines     : vectorised, Java-compatible `line.split(" ")` + Double.parseDouble /
+//                      Long.parseLong / LocalDateTime.parse(..).toEpochSecond(+08:00)
+//                      (Main.java:21-24, BandwidthMonitor.java:28-30,
+//                      BandwidthMonitorWithEventTime.java:33,41).
+//  * SocketSource    : background reader thread with Flink SocketTextStreamFunction semantics
+//                      ('\n' delimiter, trailing '\r' stripped, remainder flushed at EOF).
+//  * write/read_kg_file : keyed-state snapshot files indexed by key group (restore at a
+//                      different parallelism re-reads only the owned key-group range).
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <cmath>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <fstream>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "mxs_common.h"
+#include "mxs_runtime.h"
+
+namespace py = pybind11;
+
+namespace mxs {
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// Java String.hashCode over the UTF-16 encoding of UTF-8 input (invalid bytes -> U+FFFD).
+// ------------------------------------------------------------------------------------------
+int32_t java_string_hash(std::string_view s) {
+  uint32_t h = 0;
+  auto add = [&](uint32_t unit) { h = 31u * h + unit; };
+  size_t i = 0;
+  const size_t n = s.size();
+  while (i < n) {
+    const unsigned char c = (unsigned char)s[i];
+    uint32_t cp;
+    size_t len;
+    if (c < 0x80) {
+      cp = c;
+      len = 1;
+    } else if ((c >> 5) == 0x6 && i + 1 < n && ((unsigned char)s[i + 1] >> 6) == 2) {
+      cp = ((c & 0x1Fu) << 6) | ((unsigned char)s[i + 1] & 0x3Fu);
+      len = 2;
+    } else if ((c >> 4) == 0xE && i + 2 < n && ((unsigned char)s[i + 1] >> 6) == 2 &&
+               ((unsigned char)s[i + 2] >> 6) == 2) {
+      cp = ((c & 0x0Fu) << 12) | (((unsigned char)s[i + 1] & 0x3Fu) << 6) |
+           ((unsigned char)s[i + 2] & 0x3Fu);
+      len = 3;
+    } else if ((c >> 3) == 0x1E && i + 3 < n && ((unsigned char)s[i + 1] >> 6) == 2 &&
+               ((unsigned char)s[i + 2] >> 6) == 2 && ((unsigned char)s[i + 3] >> 6) == 2) {
+      cp = ((c & 0x07u) << 18) | (((unsigned char)s[i + 1] & 0x3Fu) << 12) |
+           (((unsigned char)s[i + 2] & 0x3Fu) << 6) | ((unsigned char)s[i + 3] & 0x3Fu);
+      len = 4;
+    } else {
+      cp = 0xFFFD;
+      len = 1;
+    }
+    if (cp >= 0x10000) {
+      cp -= 0x10000;
+      add(0xD800u + (cp >> 10));
+      add(0xDC00u + (cp & 0x3FFu));
+    } else {
+      add(cp);
+    }
+    i += len;
+  }
+  return (int32_t)h;
+}
+
+class StringDict {
+ public:
+  uint64_t intern(std::string_view s) {
+    std::lock_guard<std::mutex> g(mu_);
+    return intern_locked(s);
+  }
+  uint64_t intern_locked(std::string_view s) {
+    auto it = ids_.find(std::string(s));
+    if (it != ids_.end()) return it->second;
+    const uint64_t id = strs_.size();
+    strs_.emplace_back(s);
+    jhash_.push_back(java_string_hash(s));
+    ids_.emplace(strs_.back(), id);
+    return id;
+  }
+  std::string get(uint64_t id) const {
+    if (id >= strs_.size()) throw std::out_of_range("StringDict id out of range");
+    return strs_[id];
+  }
+  size_t size() const { return strs_.size(); }
+  py::array_t<int32_t> jhash_table() const {
+    py::array_t<int32_t> a((py::ssize_t)jhash_.size());
+    if (!jhash_.empty()) std::memcpy(a.mutable_data(), jhash_.data(), jhash_.size() * 4);
+    return a;
+  }
+  std::vector<std::string> strings() const { return strs_; }
+  std::mutex& mu() { return mu_; }
+
+ private:
+  std::mutex mu_;
+  std::unordered_map<std::string, uint64_t> ids_;
+  std::vector<std::string> strs_;
+  std::vector<int32_t> jhash_;
+};
+
+// ------------------------------------------------------------------------------------------
+// Java parsing helpers
+// ------------------------------------------------------------------------------------------
+struct ParseError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+// java.lang.String.split(String) for a single non-regex-metachar separator: every occurrence
+// splits, trailing empty strings are removed, "" -> [""].
+void java_split(std::string_view line, char sep, std::vector<std::string_view>& out) {
+  out.clear();
+  if (line.empty()) {  // no match: the array holds the input itself
+    out.push_back(line);
+    return;
+  }
+  size_t start = 0;
+  for (size_t i = 0; i < line.size(); ++i) {
+    if (line[i] == sep) {
+      out.push_back(line.substr(start, i - start));
+      start = i + 1;
+    }
+  }
+  out.push_back(line.substr(start));
+  while (!out.empty() && out.back().empty()) out.pop_back();
+}
+
+std::string_view java_trim(std::string_view s) {
+  size_t a = 0, b = s.size();
+  while (a < b && (unsigned char)s[a] <= ' ') ++a;
+  while (b > a && (unsigned char)s[b - 1] <= ' ') --b;
+  return s.substr(a, b - a);
+}
+
+double java_parse_double(std::string_view raw) {
+  std::string_view s = java_trim(raw);
+  if (s.empty()) throw ParseError("NumberFormatException: empty String");
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    i = 1;
+  }
+  std::string_view body = s.substr(i);
+  if (body == "NaN") return std::nan("");
+  if (body == "Infinity") return neg ? -INFINITY : INFINITY;
+  // Strip a Java float-type suffix.
+  if (!body.empty()) {
+    const char c = body.back();
+    if (c == 'd' || c == 'D' || c == 'f' || c == 'F') body = body.substr(0, body.size() - 1);
+  }
+  if (body.empty()) throw ParseError("NumberFormatException: For input string: \"" + std::string(raw) + "\"");
+  bool hex = body.size() > 1 && body[0] == '0' && (body[1] == 'x' || body[1] == 'X');
+  if (!hex) {
+    // Decimal grammar: digits [. digits] [e|E [+-] digits], at least one digit in the mantissa.
+    size_t j = 0, nd = 0;
+    while (j < body.size() && isdigit((unsigned char)body[j])) ++j, ++nd;
+    if (j < body.size() && body[j] == '.') {
+      ++j;
+      while (j < body.size() && isdigit((unsigned char)body[j])) ++j, ++nd;
+    }
+    if (nd == 0) throw ParseError("NumberFormatException: For input string: \"" + std::string(raw) + "\"");
+    if (j < body.size() && (body[j] == 'e' || body[j] == 'E')) {
+      ++j;
+      if (j < body.size() && (body[j] == '+' || body[j] == '-')) ++j;
+      size_t ne = 0;
+      while (j < body.size() && isdigit((unsigned char)body[j])) ++j, ++ne;
+      if (ne == 0) throw ParseError("NumberFormatException: For input string: \"" + std::string(raw) + "\"");
+    }
+    if (j != body.size()) throw ParseError("NumberFormatException: For input string: \"" + std::string(raw) + "\"");
+  }
+  std::string tmp(body);
+  errno = 0;
+  char* end = nullptr;
+  double v = std::strtod(tmp.c_str(), &end);
+  if (end != tmp.c_str() + tmp.size())
+    throw ParseError("NumberFormatException: For input string: \"" + std::string(raw) + "\"");
+  return neg ? -v : v;
+}
+
+int64_t java_parse_long(std::string_view s, int64_t lo, int64_t hi, const char* what) {
+  if (s.empty()) throw ParseError(std::string("NumberFormatException: For input string: \"\""));
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    i = 1;
+    if (s.size() == 1) throw ParseError("NumberFormatException: For input string: \"" + std::string(s) + "\"");
+  }
+  __int128 v = 0;
+  for (; i < s.size(); ++i) {
+    const char c = s[i];
+    if (c < '0' || c > '9')
+      throw ParseError("NumberFormatException: For input string: \"" + std::string(s) + "\"");
+    v = v * 10 + (c - '0');
+    if (v > (__int128)hi + 1) throw ParseError(std::string("NumberFormatException: ") + what + " overflow \"" + std::string(s) + "\"");
+  }
+  if (neg) v = -v;
+  if (v < lo || v > hi) throw ParseError(std::string("NumberFormatException: ") + what + " overflow \"" + std::string(s) + "\"");
+  return (int64_t)v;
+}
+
+int64_t days_from_civil(int64_t y, unsigned m, unsigned d) {
+  y -= m <= 2;
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const unsigned yoe = (unsigned)(y - era * 400);
+  const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + (int64_t)doe - 719468;
+}
+
+// LocalDateTime.parse (ISO_LOCAL_DATE_TIME) -> epoch milliseconds at the given offset.
+// Returns seconds and the sub-second millis separately.
+void parse_iso_local_datetime(std::string_view s, int64_t offset_s, int64_t* epoch_s, int64_t* millis) {
+  auto bad = [&]() { throw ParseError("DateTimeParseException: Text '" + std::string(s) + "' could not be parsed"); };
+  auto num = [&](size_t pos, size_t len) -> int {
+    if (pos + len > s.size()) bad();
+    int v = 0;
+    for (size_t k = 0; k < len; ++k) {
+      const char c = s[pos + k];
+      if (c < '0' || c > '9') bad();
+      v = v * 10 + (c - '0');
+    }
+    return v;
+  };
+  if (s.size() < 16) bad();
+  const int y = num(0, 4);
+  if (s[4] != '-' || s[7] != '-' || s[10] != 'T' || s[13] != ':') bad();
+  const int mo = num(5, 2), d = num(8, 2), h = num(11, 2), mi = num(14, 2);
+  int sec = 0, ms = 0;
+  size_t pos = 16;
+  if (pos < s.size()) {
+    if (s[pos] != ':') bad();
+    sec = num(pos + 1, 2);
+    pos += 3;
+    if (pos < s.size()) {
+      if (s[pos] != '.') bad();
+      ++pos;
+      size_t nd = 0;
+      int frac = 0;
+      while (pos < s.size()) {
+        const char c = s[pos];
+        if (c < '0' || c > '9') bad();
+        if (nd < 3) frac = frac * 10 + (c - '0');
+        ++nd;
+        ++pos;
+      }
+      if (nd == 0 || nd > 9) bad();
+      for (size_t k = nd; k < 3; ++k) frac *= 10;
+      ms = frac;
+    }
+  }
+  static const int mdays[] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  if (mo < 1 || mo > 12 || d < 1) bad();
+  const bool leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+  const int maxd = mdays[mo - 1] + (mo == 2 && leap ? 1 : 0);
+  if (d > maxd || h > 23 || mi > 59 || sec > 59) bad();
+  *epoch_s = days_from_civil(y, (unsigned)mo, (unsigned)d) * 86400 + h * 3600 + mi * 60 + sec - offset_s;
+  *millis = ms;
+}
+
+enum FieldKind : int {
+  FK_STR = 0,        // dictionary id (u64)
+  FK_DOUBLE = 1,     // Double.parseDouble -> f64
+  FK_LONG = 2,       // Long.parseLong -> i64
+  FK_TS_INTSEC = 3,  // (int) LocalDateTime.parse(x).toEpochSecond(off) * 1000L  (reference quirk)
+  FK_TS_MS = 4,      // exact epoch millis of LocalDateTime.parse(x) at offset
+  FK_INT = 5,        // Integer.parseInt -> i64
+  FK_RAW_LONG = 6,   // epoch-ms integer field
+};
+
+// Parse newline-separated lines. Returns (columns, nparsed, error_index, error_message).
+py::tuple parse_lines(py::bytes data, std::vector<std::pair<int, int>> spec, std::string sep,
+                      StringDict& dict, int64_t offset_s) {
+  if (sep.size() != 1) throw std::invalid_argument("separator must be one character");
+  char* buf;
+  py::ssize_t len;
+  if (PYBIND11_BYTES_AS_STRING_AND_SIZE(data.ptr(), &buf, &len)) throw py::error_already_set();
+  std::string_view all(buf, (size_t)len);
+  // Count lines (a trailing newline does not start a new line).
+  std::vector<std::string_view> lines;
+  {
+    size_t start = 0;
+    for (size_t i = 0; i < all.size(); ++i) {
+      if (all[i] == '\n') {
+        std::string_view l = all.substr(start, i - start);
+        if (!l.empty() && l.back() == '\r') l.remove_suffix(1);
+        lines.push_back(l);
+        start = i + 1;
+      }
+    }
+    if (start < all.size()) {
+      std::string_view l = all.substr(start);
+      if (!l.empty() && l.back() == '\r') l.remove_suffix(1);
+      lines.push_back(l);
+    }
+  }
+  const size_t n = lines.size();
+  std::vector<py::array> cols;
+  std::vector<void*> ptrs;
+  for (auto& f : spec) {
+    if (f.second == FK_DOUBLE) {
+      cols.push_back(py::array_t<double>((py::ssize_t)n));
+    } else if (f.second == FK_STR) {
+      cols.push_back(py::array_t<uint64_t>((py::ssize_t)n));
+    } else {
+      cols.push_back(py::array_t<int64_t>((py::ssize_t)n));
+    }
+    ptrs.push_back(cols.back().mutable_data());
+  }
+  int64_t err_idx = -1;
+  std::string err_msg;
+  size_t done = 0;
+  {
+    py::gil_scoped_release nogil;
+    std::lock_guard<std::mutex> g(dict.mu());
+    std::vector<std::string_view> parts;
+    for (size_t li = 0; li < n; ++li) {
+      try {
+        java_split(lines[li], sep[0], parts);
+        for (size_t c = 0; c < spec.size(); ++c) {
+          const int fi = spec[c].first;
+          if (fi < 0 || (size_t)fi >= parts.size())
+            throw ParseError("ArrayIndexOutOfBoundsException: " + std::to_string(fi));
+          std::string_view v = parts[fi];
+          switch (spec[c].second) {
+            case FK_STR: ((uint64_t*)ptrs[c])[li] = dict.intern_locked(v); break;
+            case FK_DOUBLE: ((double*)ptrs[c])[li] = java_parse_double(v); break;
+            case FK_LONG: ((int64_t*)ptrs[c])[li] = java_parse_long(v, INT64_MIN, INT64_MAX, "long"); break;
+            case FK_INT: ((int64_t*)ptrs[c])[li] = java_parse_long(v, INT32_MIN, INT32_MAX, "int"); break;
+            case FK_RAW_LONG: ((int64_t*)ptrs[c])[li] = java_parse_long(v, INT64_MIN, INT64_MAX, "long"); break;
+            case FK_TS_INTSEC: {
+              int64_t es, ms;
+              parse_iso_local_datetime(v, offset_s, &es, &ms);
+              ((int64_t*)ptrs[c])[li] = (int64_t)(int32_t)(uint32_t)(uint64_t)es * 1000LL;
+              break;
+            }
+            case FK_TS_MS: {
+              int64_t es, ms;
+              parse_iso_local_datetime(v, offset_s, &es, &ms);
+              ((int64_t*)ptrs[c])[li] = es * 1000LL + ms;
+              break;
+            }
+            default: throw ParseError("unknown field kind");
+          }
+        }
+        ++done;
+      } catch (const ParseError& e) {
+        err_idx = (int64_t)li;
+        err_msg = e.what();
+        break;
+      }
+    }
+  }
+  py::list out;
+  for (auto& c : cols) out.append(c);
+  return py::make_tuple(out, (int64_t)done, err_idx, err_msg);
+}
+
+// ------------------------------------------------------------------------------------------
+// Socket source (SocketTextStreamFunction semantics, maxRetry = 0 by default)
+// ------------------------------------------------------------------------------------------
+class SocketSource {
+ public:
+  SocketSource(std::string host, int port, std::string delimiter, int max_retry, int64_t retry_ms)
+      : host_(std::move(host)), port_(port), delim_(std::move(delimiter)), max_retry_(max_retry),
+        retry_ms_(retry_ms) {
+    if (delim_.empty()) throw std::invalid_argument("empty delimiter");
+  }
+  ~SocketSource() { close(); }
+
+  void start() {
+    if (th_.joinable()) return;
+    th_ = std::thread([this] { run(); });
+  }
+
+  // Returns (joined_lines_bytes, nlines, eof, error).
+  py::tuple poll(size_t max_lines, int timeout_ms) {
+    std::string joined;
+    size_t n = 0;
+    bool eof;
+    std::string err;
+    {
+      py::gil_scoped_release nogil;
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return !q_.empty() || eof_; });
+      while (!q_.empty() && n < max_lines) {
+        joined += q_.front();
+        joined.push_back('\n');
+        q_.pop_front();
+        ++n;
+      }
+      eof = eof_ && q_.empty();
+      err = err_;
+    }
+    return py::make_tuple(py::bytes(joined), (int64_t)n, eof, err);
+  }
+
+  void close() {
+    stop_ = true;
+    const int fd = fd_.exchange(-1);
+    if (fd >= 0) {
+      ::shutdown(fd, SHUT_RDWR);
+      ::close(fd);
+    }
+    if (th_.joinable()) th_.join();
+  }
+
+ private:
+  void push(std::string line) {
+    std::lock_guard<std::mutex> g(mu_);
+    q_.push_back(std::move(line));
+    cv_.notify_one();
+  }
+  void finish(const std::string& err) {
+    std::lock_guard<std::mutex> g(mu_);
+    eof_ = true;
+    err_ = err;
+    cv_.notify_all();
+  }
+  int connect_once() {
+    addrinfo hints{}, *res = nullptr;
+    hints.ai_family = AF_UNSPEC;
+    hints.ai_socktype = SOCK_STREAM;
+    if (getaddrinfo(host_.c_str(), std::to_string(port_).c_str(), &hints, &res) != 0) return -1;
+    int fd = -1;
+    for (addrinfo* p = res; p; p = p->ai_next) {
+      fd = ::socket(p->ai_family, p->ai_socktype, p->ai_protocol);
+      if (fd < 0) continue;
+      if (::connect(fd, p->ai_addr, p->ai_addrlen) == 0) break;
+      ::close(fd);
+      fd = -1;
+    }
+    freeaddrinfo(res);
+    return fd;
+  }
+  void run() {
+    int attempt = 0;
+    std::string buffer;
+    while (!stop_) {
+      const int fd = connect_once();
+      if (fd < 0) {
+        if (max_retry_ >= 0 && attempt >= max_retry_) {
+          finish("ConnectException: could not connect to " + host_ + ":" + std::to_string(port_));
+          return;
+        }
+        ++attempt;
+        std::this_thread::sleep_for(std::chrono::milliseconds(retry_ms_));
+        continue;
+      }
+      fd_ = fd;
+      char chunk[8192];
+      while (!stop_) {
+        const ssize_t r = ::recv(fd, chunk, sizeof(chunk), 0);
+        if (r <= 0) break;
+        buffer.append(chunk, (size_t)r);
+        size_t pos;
+        while ((pos = buffer.find(delim_)) != std::string::npos) {
+          std::string line = buffer.substr(0, pos);
+          if (delim_ == "\n" && !line.empty() && line.back() == '\r') line.pop_back();
+          push(std::move(line));
+          buffer.erase(0, pos + delim_.size());
+        }
+      }
+      const int cur = fd_.exchange(-1);
+      if (cur >= 0) ::close(cur);
+      ++attempt;
+      if (stop_ || max_retry_ == 0 || (max_retry_ > 0 && attempt > max_retry_)) break;
+      std::this_thread::sleep_for(std::chrono::milliseconds(retry_ms_));
+    }
+    if (!buffer.empty()) push(buffer);
+    finish("");
+  }
+
+  std::string host_;
+  int port_;
+  std::string delim_;
+  int max_retry_;
+  int64_t retry_ms_;
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::string> q_;
+  bool eof_ = false;
+  std::string err_;
+  std::atomic<bool> stop_{false};
+  std::atomic<int> fd_{-1};
+};
+
+// ------------------------------------------------------------------------------------------
+// Key-group indexed state files.
+// Layout: "MXSKG001" | u64 header_len | header (UTF-8 JSON from Python) | u32 kg_lo | u32 kg_hi |
+//         u64 offsets[kg_hi - kg_lo + 2] (row offsets) | columns (each nrows * itemsize, kg-sorted)
+// ------------------------------------------------------------------------------------------
+void write_kg_file(const std::string& path, const std::string& header, uint32_t kg_lo,
+                   uint32_t kg_hi, py::array_t<int32_t, py::array::c_style> kg, py::list columns) {
+  const size_t n = (size_t)kg.size();
+  const int32_t* kgp = kg.data();
+  const uint32_t ngroups = kg_hi - kg_lo + 1;
+  std::vector<uint64_t> off(ngroups + 1, 0);
+  for (size_t i = 0; i < n; ++i) {
+    const int32_t g = kgp[i];
+    if (g < (int32_t)kg_lo || g > (int32_t)kg_hi) throw std::invalid_argument("row key group outside file range");
+    off[g - kg_lo + 1]++;
+  }
+  for (uint32_t g = 0; g < ngroups; ++g) off[g + 1] += off[g];
+  std::vector<uint64_t> perm(n);
+  {
+    std::vector<uint64_t> cur(off.begin(), off.end() - 1);
+    for (size_t i = 0; i < n; ++i) perm[cur[kgp[i] - kg_lo]++] = i;  // stable counting sort
+  }
+  const std::string tmp = path + ".inprogress";
+  std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+  if (!f) throw std::runtime_error("cannot open " + tmp);
+  f.write("MXSKG001", 8);
+  const uint64_t hl = header.size();
+  f.write((const char*)&hl, 8);
+  f.write(header.data(), (std::streamsize)hl);
+  f.write((const char*)&kg_lo, 4);
+  f.write((const char*)&kg_hi, 4);
+  f.write((const char*)off.data(), (std::streamsize)(off.size() * 8));
+  std::vector<char> tmpbuf;
+  for (auto h : columns) {
+    py::array a = py::reinterpret_borrow<py::array>(h);
+    if ((size_t)a.size() != n) throw std::invalid_argument("column length mismatch");
+    py::array ac = py::array::ensure(a, py::array::c_style);
+    const size_t isz = (size_t)ac.itemsize();
+    const char* src = (const char*)ac.data();
+    tmpbuf.resize(n * isz);
+    for (size_t i = 0; i < n; ++i) std::memcpy(&tmpbuf[i * isz], src + perm[i] * isz, isz);
+    f.write(tmpbuf.data(), (std::streamsize)tmpbuf.size());
+  }
+  f.flush();
+  if (!f) throw std::runtime_error("write failed: " + tmp);
+  f.close();
+  if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("rename failed: " + path);
+}
+
+// Returns (header, kg_lo, kg_hi, offsets(np.uint64), raw column bytes for rows in [lo, hi]).
+py::tuple read_kg_file(const std::string& path, py::list itemsizes, uint32_t want_lo, uint32_t want_hi) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot open " + path);
+  char magic[8];
+  f.read(magic, 8);
+  if (std::memcmp(magic, "MXSKG001", 8) != 0) throw std::runtime_error("bad magic in " + path);
+  uint64_t hl;
+  f.read((char*)&hl, 8);
+  std::string header(hl, '\0');
+  f.read(header.data(), (std::streamsize)hl);
+  uint32_t lo, hi;
+  f.read((char*)&lo, 4);
+  f.read((char*)&hi, 4);
+  const uint32_t ng = hi - lo + 1;
+  std::vector<uint64_t> off(ng + 1);
+  f.read((char*)off.data(), (std::streamsize)(off.size() * 8));
+  const uint64_t nrows = off[ng];
+  const std::streamoff data0 = f.tellg();
+  const uint32_t a = std::max(lo, want_lo), b = std::min(hi, want_hi);
+  uint64_t r0 = 0, r1 = 0;
+  if (a <= b) {
+    r0 = off[a - lo];
+    r1 = off[b - lo + 1];
+  }
+  py::list cols;
+  std::streamoff colbase = data0;
+  for (auto h : itemsizes) {
+    const size_t isz = h.cast<size_t>();
+    std::string bytes((size_t)(r1 - r0) * isz, '\0');
+    f.seekg(colbase + (std::streamoff)(r0 * isz));
+    f.read(bytes.data(), (std::streamsize)bytes.size());
+    cols.append(py::bytes(bytes));
+    colbase += (std::streamoff)(nrows * isz);
+  }
+  py::array_t<uint64_t> offs((py::ssize_t)off.size());
+  std::memcpy(offs.mutable_data(), off.data(), off.size() * 8);
+  return py::make_tuple(py::bytes(header), lo, hi, offs, cols, (int64_t)(r1 - r0));
+}
+
+}  // namespace
+}  // namespace mxs
+
+void bind_runtime(py::module_& m) {
+  using namespace mxs;
+  m.def("java_string_hash", [](const std::string& s) { return java_string_hash(s); });
+  m.def("java_parse_double", [](const std::string& s) { return java_parse_double(s); });
+  m.def("java_split", [](const std::string& s, const std::string& sep) {
+    std::vector<std::string_view> parts;
+    java_split(s, sep.at(0), parts);
+    std::vector<std::string> out(parts.begin(), parts.end());
+    return out;
+  });
+  m.def("iso_to_epoch_ms", [](const std::string& s, int64_t offset_s) {
+    int64_t es, ms;
+    parse_iso_local_datetime(s, offset_s, &es, &ms);
+    return es * 1000 + ms;
+  });
+  py::register_exception<ParseError>(m, "ParseError");
+
+  py::class_<StringDict>(m, "StringDict")
+      .def(py::init<>())
+      .def("intern", [](StringDict& d, const std::string& s) { return d.intern(s); })
+      .def("get", &StringDict::get)
+      .def("__len__", &StringDict::size)
+      .def("jhash_table", &StringDict::jhash_table)
+      .def("strings", &StringDict::strings);
+
+  m.def("parse_lines", &parse_lines, py::arg("data"), py::arg("spec"), py::arg("sep"),
+        py::arg("dict"), py::arg("offset_s") = 0);
+
+  py::class_<SocketSource>(m, "SocketSource")
+      .def(py::init<std::string, int, std::string, int, int64_t>(), py::arg("host"), py::arg("port"),
+           py::arg("delimiter") = "\n", py::arg("max_retry") = 0, py::arg("retry_ms") = 500)
+      .def("start", &SocketSource::start)
+      .def("poll", &SocketSource::poll, py::arg("max_lines") = 1 << 20, py::arg("timeout_ms") = 100)
+      .def("close", &SocketSource::close);
+
+  m.def("write_kg_file", &write_kg_file);
+  m.def("read_kg_file", &read_kg_file);
+}

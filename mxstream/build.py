@@ -1,0 +1,124 @@
+"""In-tree build of the native engine (`mxstream/_mxs_native*.so`).
+
+HIP sources are compiled with ``hipcc --offload-arch=gfx950`` (cross-compiles without a GPU),
+host-only C++ with ``g++``; everything links into one pybind11 module next to this file so the
+built object travels with the repository snapshot to the GPU box. Incremental: an object is
+rebuilt only when its source, a header or the flags change.
+
+Usage: ``python -m mxstream.build [--force] [-j N]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+BUILD = ROOT / "build" / "native"
+PKG = ROOT / "mxstream"
+ARCH = os.environ.get("MXS_OFFLOAD_ARCH", "gfx950")
+
+HIP_SOURCES = ["kernels_hip.hip"]
+CXX_SOURCES = ["kernels_cpu.cpp", "runtime.cpp", "bindings.cpp"]
+
+
+def _ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def target_path() -> Path:
+    return PKG / ("_mxs_native" + _ext_suffix())
+
+
+def _includes() -> list[str]:
+    import pybind11
+
+    return [
+        f"-I{CSRC}",
+        f"-I{pybind11.get_include()}",
+        f"-I{sysconfig.get_paths()['include']}",
+    ]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc"):
+        if cand and Path(cand).exists():
+            return cand
+    return "hipcc"
+
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fvisibility=hidden",
+          "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+
+
+def _cmd_for(src: Path, obj: Path) -> list[str]:
+    if src.suffix == ".hip":
+        return [_hipcc(), f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *COMMON, *_includes(),
+                "-c", str(src), "-o", str(obj)]
+    # Host-only translation units: g++, no -march (the .so runs on the GPU box's CPU too).
+    return ["g++", *COMMON, *_includes(), "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__",
+            "-c", str(src), "-o", str(obj)]
+
+
+def _digest(src: Path, cmd: list[str]) -> str:
+    h = hashlib.sha256()
+    h.update(" ".join(cmd).encode())
+    h.update(src.read_bytes())
+    for hdr in sorted(CSRC.glob("*.h")):
+        h.update(hdr.read_bytes())
+    return h.hexdigest()
+
+
+def _compile(src: Path, force: bool) -> Path:
+    obj = BUILD / (src.name + ".o")
+    cmd = _cmd_for(src, obj)
+    stamp = obj.with_suffix(".o.sha")
+    dig = _digest(src, cmd)
+    if not force and obj.exists() and stamp.exists() and stamp.read_text() == dig:
+        return obj
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+    stamp.write_text(dig)
+    return obj
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
+    """Compile every native source for gfx950 + host and link the extension module."""
+    BUILD.mkdir(parents=True, exist_ok=True)
+    srcs = [CSRC / s for s in HIP_SOURCES + CXX_SOURCES]
+    jobs = jobs or min(8, len(srcs))
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    out = target_path()
+    link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs],
+            "-o", str(out) + ".tmp"]
+    newest = max(o.stat().st_mtime for o in objs)
+    if force or not out.exists() or out.stat().st_mtime < newest:
+        res = subprocess.run(link, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(link)}\n{res.stdout}\n{res.stderr}")
+        os.replace(str(out) + ".tmp", out)
+        if verbose:
+            print(f"[mxstream.build] linked {out}")
+    return out
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    a = ap.parse_args(argv)
+    p = build(force=a.force, jobs=a.jobs, verbose=True)
+    print(p)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

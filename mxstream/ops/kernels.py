@@ -1,0 +1,242 @@
+"""Validated launch wrappers around the native kernels.
+
+Every wrapper checks dtype, device, contiguity and the sizes the kernel's grid assumes BEFORE
+launching (a mis-shaped operand must never reach a hand-written kernel), then dispatches to the
+gfx950 kernel for CUDA(HIP) tensors or to the C++ twin for CPU tensors. There is no Python
+fallback: a missing extension raises.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from . import expr as _expr
+from .native import load
+
+REC_WORDS = 3  # 24-byte record = 3 x int64 words
+STAT_COUNT = 8
+STAT_MAXTS, STAT_MINPANE, STAT_MAXPANE, STAT_LATE, STAT_OVERFLOW, STAT_ACCEPTED = range(6)
+
+I64_MIN = -(1 << 63)
+I64_MAX = (1 << 63) - 1
+
+# AggKind (csrc/mxs_common.h)
+AGG_SUM_I64, AGG_SUM_F64, AGG_MIN_I64, AGG_MAX_I64, AGG_MIN_F64, AGG_MAX_F64, AGG_COUNT, \
+    AGG_AVG_F64, AGG_AVG_I64 = range(9)
+AGG_IS_F64 = {AGG_SUM_F64, AGG_MIN_F64, AGG_MAX_F64, AGG_AVG_F64}
+
+
+def _is_gpu(t: torch.Tensor) -> bool:
+    return t.device.type == "cuda"
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _p(t: torch.Tensor | None) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def _check(t: torch.Tensor, dtype: torch.dtype, numel_min: int, name: str, dev: torch.device):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if t.numel() < numel_min:
+        raise ValueError(f"{name}: needs >= {numel_min} elements, has {t.numel()}")
+    if t.device != dev:
+        raise ValueError(f"{name}: on {t.device}, expected {dev}")
+
+
+def new_stats(device) -> torch.Tensor:
+    s = torch.zeros(STAT_COUNT, dtype=torch.int64, device=device)
+    s[STAT_MAXTS] = I64_MIN
+    s[STAT_MINPANE] = I64_MAX
+    s[STAT_MAXPANE] = I64_MIN
+    return s
+
+
+def reset_stats(s: torch.Tensor) -> None:
+    init = torch.tensor([I64_MIN, I64_MAX, I64_MIN, 0, 0, 0, 0, 0], dtype=torch.int64)
+    s.copy_(init, non_blocking=False)
+
+
+def gen_events(keys, ts, vals, *, seed: int, stream_id: int, idx0: int, nkeys: int,
+               ts_base: int, ts_span: int, disorder: int, val_lo: int, val_span: int,
+               val_f64: bool = False) -> None:
+    n = keys.numel()
+    dev = keys.device
+    _check(keys, torch.int64, n, "keys", dev)
+    _check(ts, torch.int64, n, "ts", dev)
+    _check(vals, torch.int64, n, "vals", dev)
+    if nkeys <= 0 or nkeys >= (1 << 63):
+        raise ValueError("nkeys out of range")
+    m = load()
+    args = (_p(keys), _p(ts), _p(vals), n, seed & (2**64 - 1), stream_id & (2**64 - 1), idx0,
+            nkeys, ts_base, ts_span, disorder, val_lo, val_span, int(val_f64))
+    if _is_gpu(keys):
+        m.gpu_gen_events(*args, _stream(keys))
+    else:
+        m.cpu_gen_events(*args)
+
+
+@dataclass
+class PartitionPlan:
+    max_parallelism: int
+    nsub_log2: int
+    nranks: int
+    window_mode: int
+    drop_late: int
+    hash_mode: int
+    bucket_cap: int
+    wm: int
+    pane_base: int
+    size: int = 1
+    slide: int = 1
+    offset: int = 0
+    pane: int = 1
+    lateness: int = 0
+
+    @property
+    def nbuckets(self) -> int:
+        return self.nranks << self.nsub_log2
+
+    def as_dict(self) -> dict:
+        return dict(self.__dict__)
+
+
+def partition(keys, ts, vals, plan: PartitionPlan, kg_dest, cursor, out, stats,
+              jhash=None, late_idx=None) -> None:
+    n = keys.numel()
+    dev = keys.device
+    nb = plan.nbuckets
+    _check(keys, torch.int64, n, "keys", dev)
+    _check(ts, torch.int64, n, "ts", dev)
+    _check(vals, torch.int64, n, "vals", dev)
+    _check(kg_dest, torch.int32, plan.max_parallelism, "kg_dest", dev)
+    _check(cursor, torch.int32, nb, "cursor", dev)
+    _check(out, torch.int64, nb * plan.bucket_cap * REC_WORDS, "out", dev)
+    _check(stats, torch.int64, STAT_COUNT, "stats", dev)
+    if plan.hash_mode:
+        if jhash is None:
+            raise ValueError("hash_mode=1 needs the dictionary jhash table")
+        _check(jhash, torch.int32, 1, "jhash", dev)
+    if nb > 16384:
+        raise ValueError("too many buckets (ranks x sub-tables > 16384)")
+    if n >= (1 << 32):
+        raise ValueError("batch too large (2^32 events)")
+    late_cap = 0 if late_idx is None else late_idx.numel()
+    if late_idx is not None:
+        _check(late_idx, torch.int32, 0, "late_idx", dev)
+    m = load()
+    args = (_p(keys), _p(ts), _p(vals), _p(jhash), n, plan.as_dict(), _p(kg_dest), _p(cursor),
+            _p(out), _p(stats), _p(late_idx), late_cap)
+    if _is_gpu(keys):
+        m.gpu_partition(*args, _stream(keys))
+    else:
+        m.cpu_partition(*args)
+
+
+@dataclass
+class AggPlan:
+    cap_log2: int
+    nsub: int
+    ring: int
+    agg: int
+    nsrc: int
+    bucket_cap: int
+    np_step: int
+    pg: int
+    pane_base: int
+    p_lo: int
+    fired_hi: int
+
+    def as_dict(self) -> dict:
+        return dict(self.__dict__)
+
+
+def window_agg(recs, counts, plan: AggPlan, keys_g, acc_g, cnt_g, dirty_g, occ, flags) -> None:
+    dev = keys_g.device
+    nslots = plan.nsub << plan.cap_log2
+    _check(recs, torch.int64, plan.nsrc * plan.nsub * plan.bucket_cap * REC_WORDS, "recs", dev)
+    _check(counts, torch.int32, plan.nsrc * plan.nsub, "counts", dev)
+    _check(keys_g, torch.int64, nslots, "keys_g", dev)
+    _check(acc_g, torch.int64, plan.ring * nslots, "acc_g", dev)
+    _check(cnt_g, torch.int32, plan.ring * nslots, "cnt_g", dev)
+    _check(dirty_g, torch.uint8, plan.ring * nslots, "dirty_g", dev)
+    _check(occ, torch.int32, plan.nsub, "occupancy", dev)
+    _check(flags, torch.int32, 1, "flags", dev)
+    if plan.np_step > plan.ring:
+        raise ValueError("step touches more panes than the ring holds")
+    m = load()
+    args = (_p(recs), _p(counts), plan.as_dict(), _p(keys_g), _p(acc_g), _p(cnt_g), _p(dirty_g),
+            _p(occ), _p(flags))
+    if _is_gpu(keys_g):
+        m.gpu_window_agg(*args, _stream(keys_g))
+    else:
+        m.cpu_window_agg(*args)
+
+
+def window_fire(keys_g, acc_g, cnt_g, dirty_g, *, agg: int, npanes: int, ring: int, p0: int,
+                wstart: int, wend: int, only_dirty: bool, map_prog: _expr.Program,
+                filt_prog: _expr.Program, out_keys, out_vals, out_raw, out_cnt, out_n) -> None:
+    dev = keys_g.device
+    nslots = keys_g.numel()
+    cap = out_keys.numel()
+    _check(acc_g, torch.int64, ring * nslots, "acc_g", dev)
+    _check(cnt_g, torch.int32, ring * nslots, "cnt_g", dev)
+    _check(dirty_g, torch.uint8, ring * nslots, "dirty_g", dev)
+    _check(out_vals, torch.float64, cap, "out_vals", dev)
+    _check(out_raw, torch.int64, cap, "out_raw", dev)
+    _check(out_cnt, torch.int32, cap, "out_cnt", dev)
+    _check(out_n, torch.int32, 1, "out_n", dev)
+    if npanes > ring:
+        raise ValueError("window spans more panes than the ring")
+    plan = dict(agg=agg, npanes=npanes, ring=ring, only_dirty=int(only_dirty), nslots=nslots,
+                p0=p0, wstart=float(wstart), wend=float(wend), out_cap=cap,
+                map=tuple(map_prog.as_args()), filt=tuple(filt_prog.as_args()))
+    m = load()
+    args = (_p(keys_g), _p(acc_g), _p(cnt_g), _p(dirty_g), plan, _p(out_keys), _p(out_vals),
+            _p(out_raw), _p(out_cnt), _p(out_n))
+    if _is_gpu(keys_g):
+        m.gpu_window_fire(*args, _stream(keys_g))
+    else:
+        m.cpu_window_fire(*args)
+
+
+def rolling(recs, counts, *, cap_log2: int, nsub: int, agg: int, nsrc: int, bucket_cap: int,
+            emit: bool, keys_g, acc_g, cnt_g, occ, flags, out_vals=None) -> None:
+    dev = keys_g.device
+    nslots = nsub << cap_log2
+    _check(recs, torch.int64, nsrc * nsub * bucket_cap * REC_WORDS, "recs", dev)
+    _check(counts, torch.int32, nsrc * nsub, "counts", dev)
+    _check(keys_g, torch.int64, nslots, "keys_g", dev)
+    _check(acc_g, torch.int64, nslots, "acc_g", dev)
+    _check(cnt_g, torch.int32, nslots, "cnt_g", dev)
+    _check(occ, torch.int32, nsub, "occupancy", dev)
+    if emit and out_vals is None:
+        raise ValueError("emit needs out_vals")
+    plan = dict(cap_log2=cap_log2, nsub=nsub, agg=agg, nsrc=nsrc, bucket_cap=bucket_cap,
+                emit=int(emit))
+    m = load()
+    args = (_p(recs), _p(counts), plan, _p(keys_g), _p(acc_g), _p(cnt_g), _p(occ), _p(flags),
+            _p(out_vals))
+    if _is_gpu(keys_g):
+        m.gpu_rolling(*args, _stream(keys_g))
+    else:
+        m.cpu_rolling(*args)
+
+
+def expr_filter(x: torch.Tensor, prog: _expr.Program) -> torch.Tensor:
+    """Evaluate a traced predicate over one f64 column; returns a bool mask."""
+    _check(x, torch.float64, x.numel(), "x", x.device)
+    keep = torch.empty(x.numel(), dtype=torch.uint8, device=x.device)
+    m = load()
+    code, consts = prog.as_args()
+    if _is_gpu(x):
+        m.gpu_expr_filter(_p(x), x.numel(), code, consts, _p(keep), _stream(x))
+    else:
+        m.cpu_expr_filter(_p(x), x.numel(), code, consts, _p(keep))
+    return keep.bool()

@@ -1,0 +1,430 @@
+"""Keyed window operator: keyBy shuffle + pane-ring window state + watermark-driven firing.
+
+One instance runs per rank (one process per GPU). Per micro-batch (``process``):
+
+ 1. ``partition`` kernel: key group -> destination rank (Flink's
+    ``murmur(hash) % maxParallelism * P / maxParallelism``), sub-table, pane id, late drop —
+    records land in fixed-capacity (dest, sub-table) buckets;
+ 2. one MIN all-reduce of [-max pane, min pane, local watermark, -overflow] (the watermark valve)
+    and the equal-split all-to-all of the bucket ranges + counts (RCCL over xGMI); ONE host sync;
+ 3. ``window_agg`` kernel: one workgroup per LDS-resident hash sub-table folds the step's
+    records into the pane ring (pane = gcd(size, slide); a sliding window is a run of panes);
+ 4. late-but-allowed data re-fires the touched windows (``only_dirty``); the advanced watermark
+    fires every window with ``end - 1 <= wm`` (fused map/filter epilogue + compaction);
+ 5. panes whose every window passed its cleanup time (``maxTs + allowedLateness <= wm``) are
+    zeroed for reuse.
+
+Flink semantics reproduced (reference: ``BandwidthMonitorWithEventTime.java:30-55``,
+``BandwidthMonitor.java:32-40``, ``ComputeCpuAvg.java:27-59``):
+window assignment, lateness test, per-key emission only for windows that hold data, watermark =
+min over source partitions of (max ts - bound), processing-time windows never fire at end of
+input. Micro-batch deviation (documented): several late elements of one (key, window) in the same
+micro-batch produce one re-firing carrying their combined effect (Flink fires once per element).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable
+
+import numpy as np
+import torch
+
+from ..ops import expr as E
+from ..ops import kernels as K
+from ..parallel.comm import Comm, LocalComm
+
+I64_MIN = K.I64_MIN
+I64_MAX = K.I64_MAX
+
+
+def _next_pow2(x: int) -> int:
+    return 1 << max(0, int(x - 1).bit_length())
+
+
+def java_rem(a: int, b: int) -> int:
+    """Java's `%` on long (truncated remainder, sign of the dividend)."""
+    r = abs(a) % abs(b)
+    return -r if a < 0 else r
+
+
+def java_window_start(ts: int, offset: int, size: int) -> int:
+    """TimeWindow.getWindowStartWithOffset with Java's truncated remainder."""
+    return ts - java_rem(ts - offset + size, size)
+
+
+@dataclass
+class FireResult:
+    window_start: int
+    window_end: int
+    keys: np.ndarray        # uint64 key ids (dictionary ids for string keys)
+    values: np.ndarray      # float64 (result after the fused map epilogue)
+    raw: np.ndarray         # int64 raw accumulator (exact integer sums / f64 bit pattern)
+    counts: np.ndarray      # int32 element counts
+    refire: bool = False
+
+
+@dataclass
+class OperatorMetrics:
+    num_records_in: int = 0
+    num_late_records_dropped: int = 0
+    num_records_out: int = 0
+    num_fires: int = 0
+    current_watermark: int = I64_MIN
+    steps: int = 0
+    bucket_regrows: int = 0
+    ring_regrows: int = 0
+    extra: dict = field(default_factory=dict)
+
+
+class KeyedWindowOperator:
+    """Per-rank keyed tumbling/sliding window aggregation on GPU (or the CPU twin)."""
+
+    def __init__(self, *, size: int, slide: int | None = None, offset: int = 0,
+                 lateness: int = 0, agg: int = K.AGG_SUM_I64, device="cpu",
+                 comm: Comm | None = None, max_keys: int = 1 << 20,
+                 parallelism: int | None = None, max_parallelism: int = 128,
+                 hash_mode: int = 0, jhash_table: torch.Tensor | None = None,
+                 map_prog: E.Program = E.EMPTY, filter_prog: E.Program = E.EMPTY,
+                 batch_capacity: int = 1 << 20, bucket_slack: float = 1.5,
+                 cap_log2: int = 11, time_mode: str = "event", ooo_bound: int = 0,
+                 side_output_late: bool = False, late_capacity: int = 1 << 16,
+                 clock: Callable[[], int] | None = None):
+        self.device = torch.device(device)
+        self.comm = comm or LocalComm()
+        self.world = self.comm.world
+        self.rank = self.comm.rank
+        slide = size if slide is None else slide
+        if size <= 0 or slide <= 0:
+            raise ValueError("window size and slide must be positive")
+        self.size, self.slide, self.offset, self.lateness = int(size), int(slide), int(offset), int(lateness)
+        self.pane = math.gcd(self.size, self.slide)
+        self.panes_per_window = self.size // self.pane
+        self.agg = agg
+        self.time_mode = time_mode
+        if time_mode not in ("event", "processing"):
+            raise ValueError("time_mode must be 'event' or 'processing'")
+        self.ooo_bound = int(ooo_bound)
+        self.clock = clock
+        self.parallelism = parallelism or self.world
+        self.max_parallelism = max_parallelism
+        self.hash_mode = hash_mode
+        self.jhash = jhash_table
+        self.map_prog, self.filter_prog = map_prog, filter_prog
+        self.side_output_late = side_output_late
+        self.metrics = OperatorMetrics()
+
+        # ---- state geometry ----
+        per_rank = int(max_keys / self.world * 1.3) + 1024
+        self.cap_log2 = cap_log2
+        cap = 1 << cap_log2
+        self.nsub = _next_pow2(max(1, math.ceil(per_rank / (cap * 0.5))))
+        self.nsub_log2 = self.nsub.bit_length() - 1
+        if self.nsub * self.world > 16384:
+            raise ValueError("key space too large for the bucket histogram; raise cap_log2")
+        self.nslots = self.nsub << cap_log2
+        self.ring = max(4, _next_pow2(self.panes_per_window + 2 + math.ceil(self.lateness / self.pane)
+                                     + math.ceil(max(self.ooo_bound, self.slide) / self.pane)))
+        dev = self.device
+        self.keys_g = torch.full((self.nslots,), -1, dtype=torch.int64, device=dev)
+        self.acc_g = torch.zeros(self.ring * self.nslots, dtype=torch.int64, device=dev)
+        self.cnt_g = torch.zeros(self.ring * self.nslots, dtype=torch.int32, device=dev)
+        self.dirty_g = torch.zeros(self.ring * self.nslots, dtype=torch.uint8, device=dev)
+        self.occ = torch.zeros(self.nsub, dtype=torch.int32, device=dev)
+        self.flags = torch.zeros(4, dtype=torch.int32, device=dev)
+
+        # ---- key group -> rank map (subtasks laid out in contiguous blocks over ranks) ----
+        kgd = [self._rank_of_kg(kg) for kg in range(max_parallelism)]
+        self.kg_dest = torch.tensor(kgd, dtype=torch.int32, device=dev)
+
+        # ---- per-step buffers ----
+        self.nbuckets = self.world << self.nsub_log2
+        self._alloc_buckets(batch_capacity, bucket_slack)
+        self.stats = K.new_stats(dev)
+        self._stats_init = K.new_stats(dev)
+        self.local_maxts = torch.full((1,), I64_MIN, dtype=torch.int64, device=dev)
+        self.out_keys = torch.empty(self.nslots, dtype=torch.int64, device=dev)
+        self.out_vals = torch.empty(self.nslots, dtype=torch.float64, device=dev)
+        self.out_raw = torch.empty(self.nslots, dtype=torch.int64, device=dev)
+        self.out_cnt = torch.empty(self.nslots, dtype=torch.int32, device=dev)
+        self.out_n = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.late_idx = (torch.empty(late_capacity, dtype=torch.int32, device=dev)
+                         if side_output_late else None)
+
+        # ---- watermark / firing bookkeeping (host, identical on every rank) ----
+        self.wm = I64_MIN
+        self.next_fire_start: int | None = None   # smallest window start not yet passed
+        self.min_live_pane: int | None = None      # oldest unpurged pane
+        self.max_seen_pane: int | None = None
+        self.late_side: list[np.ndarray] = []
+
+    # ------------------------------------------------------------------------------------
+    def _rank_of_kg(self, kg: int) -> int:
+        sub = kg * self.parallelism // self.max_parallelism
+        return sub * self.world // self.parallelism
+
+    def _alloc_buckets(self, batch_capacity: int, slack: float) -> None:
+        self.batch_capacity = int(batch_capacity)
+        self.bucket_slack = slack
+        per = self.batch_capacity / self.nbuckets
+        self.bucket_cap = int(per * slack + 6 * math.sqrt(max(per, 1.0)) + 64)
+        words = self.nbuckets * self.bucket_cap * K.REC_WORDS
+        self.send = torch.empty(words, dtype=torch.int64, device=self.device)
+        self.recv = torch.empty(words, dtype=torch.int64, device=self.device) if self.world > 1 else self.send
+        self.cursor = torch.zeros(self.nbuckets, dtype=torch.int32, device=self.device)
+        self.recv_counts = torch.zeros(self.nbuckets, dtype=torch.int32, device=self.device) \
+            if self.world > 1 else self.cursor
+
+    def _grow_ring(self, need: int) -> None:
+        """Re-lay the pane ring so `need` consecutive panes fit (rare; keeps absolute pane ids)."""
+        new_ring = _next_pow2(need)
+        old = self.ring
+        acc = torch.zeros(new_ring * self.nslots, dtype=torch.int64, device=self.device)
+        cnt = torch.zeros(new_ring * self.nslots, dtype=torch.int32, device=self.device)
+        dirty = torch.zeros(new_ring * self.nslots, dtype=torch.uint8, device=self.device)
+        if self.min_live_pane is not None and self.max_seen_pane is not None:
+            for p in range(self.min_live_pane, self.max_seen_pane + 1):
+                so = (p & (old - 1)) * self.nslots
+                sn = (p & (new_ring - 1)) * self.nslots
+                acc[sn:sn + self.nslots].copy_(self.acc_g[so:so + self.nslots])
+                cnt[sn:sn + self.nslots].copy_(self.cnt_g[so:so + self.nslots])
+                dirty[sn:sn + self.nslots].copy_(self.dirty_g[so:so + self.nslots])
+        self.acc_g, self.cnt_g, self.dirty_g, self.ring = acc, cnt, dirty, new_ring
+        self.metrics.ring_regrows += 1
+
+    # ---- window arithmetic -------------------------------------------------------------
+    def pane_of(self, t: int) -> int:
+        return (t - self.offset) // self.pane
+
+    def pane_start(self, p: int) -> int:
+        return self.offset + p * self.pane
+
+    def last_start(self, t: int) -> int:
+        return java_window_start(t, self.offset, self.slide)
+
+    def first_start_containing(self, t: int) -> int:
+        ls = self.last_start(t)
+        return ls - ((ls - (t - self.size + 1)) // self.slide) * self.slide
+
+    def _fired_hi(self) -> int:
+        if self.next_fire_start is None:
+            return I64_MIN
+        last_passed_end = self.next_fire_start - self.slide + self.size
+        return self.pane_of(last_passed_end - 1)
+
+    # ---- main entry points ---------------------------------------------------------------
+    def _pane_base(self, ts: torch.Tensor) -> int:
+        if self.wm > I64_MIN and self.time_mode == "event":
+            return self.pane_of(max(self.wm - self.size - self.lateness + 1, I64_MIN + 1))
+        # No watermark yet: take the batch minimum (one reduction; happens before the first WM).
+        base = self.min_live_pane if self.min_live_pane is not None else None
+        if ts.numel():
+            bmin = self.pane_of(int(ts.min().item()))
+            base = bmin if base is None else min(base, bmin)
+        return base if base is not None else 0
+
+    def current_processing_time(self) -> int:
+        import time
+        return int(self.clock() if self.clock else time.time() * 1000)
+
+    def process(self, keys: torch.Tensor, ts: torch.Tensor, vals: torch.Tensor) -> list[FireResult]:
+        """Fold one micro-batch of this rank's source partition and fire what the watermark allows."""
+        n = keys.numel()
+        if n > self.batch_capacity:
+            self._alloc_buckets(n, self.bucket_slack)
+        old_wm = self.wm
+        pane_base = self._pane_base(ts)
+        drop_late = self.time_mode == "event"
+        while True:
+            self.cursor.zero_()
+            self.stats.copy_(self._stats_init)
+            plan = K.PartitionPlan(
+                max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2, nranks=self.world,
+                window_mode=1, drop_late=int(drop_late), hash_mode=self.hash_mode,
+                bucket_cap=self.bucket_cap, wm=old_wm, pane_base=pane_base, size=self.size,
+                slide=self.slide, offset=self.offset, pane=self.pane, lateness=self.lateness)
+            if n:
+                K.partition(keys, ts, vals, plan, self.kg_dest, self.cursor, self.send, self.stats,
+                            jhash=self.jhash, late_idx=self.late_idx)
+            # Local watermark of this source partition (BoundedOutOfOrderness: max ts - bound).
+            torch.maximum(self.local_maxts, self.stats[K.STAT_MAXTS:K.STAT_MAXTS + 1],
+                           out=self.local_maxts)
+            if self.time_mode == "event":
+                wm_cand = torch.where(self.local_maxts == I64_MIN, self.local_maxts,
+                                      self.local_maxts - self.ooo_bound)
+            else:
+                wm_cand = torch.full((1,), self.current_processing_time(), dtype=torch.int64,
+                                     device=self.device)
+            red = torch.cat([-self.stats[K.STAT_MAXPANE:K.STAT_MAXPANE + 1].clamp(min=I64_MIN + 1),
+                             self.stats[K.STAT_MINPANE:K.STAT_MINPANE + 1], wm_cand,
+                             -self.stats[K.STAT_OVERFLOW:K.STAT_OVERFLOW + 1]])
+            self.comm.allreduce_min_(red)
+            if self.world > 1:
+                self.comm.all_to_all(self.recv, self.send)
+                self.comm.all_to_all(self.recv_counts, self.cursor)
+            host = torch.cat([red, self.stats]).cpu().tolist()  # the step's single host sync
+            if -host[3]:
+                # A bucket overflowed somewhere: grow the fixed bucket capacity and redo the step.
+                self.metrics.bucket_regrows += 1
+                self._alloc_buckets(self.batch_capacity, self.bucket_slack * 2)
+                continue
+            break
+        gmax, gmin, wm_global = -host[0], host[1], host[2]
+        st = host[4:]
+        self.metrics.num_records_in += n
+        self.metrics.num_late_records_dropped += int(st[K.STAT_LATE])
+        if self.side_output_late and st[K.STAT_LATE]:
+            nl = min(int(st[K.STAT_LATE]), self.late_idx.numel())
+            self.late_side.append(self.late_idx[:nl].cpu().numpy().copy())
+
+        out: list[FireResult] = []
+        if gmin <= gmax:
+            lo = gmin if self.min_live_pane is None else min(self.min_live_pane, gmin)
+            hi = gmax if self.max_seen_pane is None else max(self.max_seen_pane, gmax)
+            if hi - lo + 1 > self.ring:
+                self._grow_ring(hi - lo + 1)
+            self.min_live_pane, self.max_seen_pane = lo, hi
+            if self.next_fire_start is None:
+                self.next_fire_start = self.first_start_containing(self.pane_start(gmin))
+            fired_hi = self._fired_hi()
+            cap = 1 << self.cap_log2
+            lds_budget = 150 * 1024 - cap * 8
+            pg = max(1, min(gmax - gmin + 1, lds_budget // (cap * 12)))
+            aplan = K.AggPlan(cap_log2=self.cap_log2, nsub=self.nsub, ring=self.ring, agg=self.agg,
+                              nsrc=self.world, bucket_cap=self.bucket_cap,
+                              np_step=gmax - gmin + 1, pg=pg, pane_base=pane_base,
+                              p_lo=gmin - pane_base, fired_hi=fired_hi)
+            K.window_agg(self.recv, self.recv_counts, aplan, self.keys_g, self.acc_g, self.cnt_g,
+                         self.dirty_g, self.occ, self.flags)
+            # Late-but-allowed data: re-fire already-passed windows that are not cleaned yet.
+            if gmin <= fired_hi:
+                out.extend(self._refire(gmin, min(gmax, fired_hi), old_wm))
+        new_wm = max(old_wm, wm_global)
+        self.wm = new_wm
+        self.metrics.current_watermark = new_wm
+        out.extend(self._fire_ready(new_wm))
+        self._purge(new_wm)
+        self.metrics.steps += 1
+        return out
+
+    def advance_watermark(self, wm: int) -> list[FireResult]:
+        """Advance the watermark without data (idle step / processing-time timer / end of input)."""
+        wm = int(wm)
+        if wm <= self.wm:
+            return []
+        self.wm = wm
+        self.metrics.current_watermark = wm
+        out = self._fire_ready(wm)
+        self._purge(wm)
+        return out
+
+    def finish(self) -> list[FireResult]:
+        """End of input: event time emits Long.MAX_VALUE (fires everything); processing time does
+        not fire pending windows (Flink 1.8 SocketTextStreamFunction end-of-stream behaviour)."""
+        if self.time_mode == "event":
+            return self.advance_watermark(I64_MAX)
+        return []
+
+    # ---- firing ---------------------------------------------------------------------------
+    def _window_overlaps_live(self, s: int) -> bool:
+        if self.min_live_pane is None:
+            return False
+        p0 = self.pane_of(s)
+        p1 = p0 + self.panes_per_window - 1
+        return not (p1 < self.min_live_pane or p0 > self.max_seen_pane)
+
+    def _fire_window(self, s: int, only_dirty: bool) -> FireResult | None:
+        p0 = self.pane_of(s)
+        self.out_n.zero_()
+        K.window_fire(self.keys_g, self.acc_g, self.cnt_g, self.dirty_g, agg=self.agg,
+                      npanes=self.panes_per_window, ring=self.ring, p0=p0, wstart=s,
+                      wend=s + self.size, only_dirty=only_dirty, map_prog=self.map_prog,
+                      filt_prog=self.filter_prog, out_keys=self.out_keys, out_vals=self.out_vals,
+                      out_raw=self.out_raw, out_cnt=self.out_cnt, out_n=self.out_n)
+        n = int(self.out_n.item())
+        self.metrics.num_fires += 1
+        if n == 0:
+            return None
+        n = min(n, self.out_keys.numel())
+        self.metrics.num_records_out += n
+        # .cpu() is a no-op for CPU tensors: copy, the output buffers are reused by the next fire.
+        host = [t[:n].cpu().numpy().copy() for t in (self.out_keys, self.out_vals, self.out_raw,
+                                                      self.out_cnt)]
+        return FireResult(s, s + self.size, host[0].view(np.uint64), host[1], host[2], host[3],
+                          refire=only_dirty)
+
+    def _fire_ready(self, wm: int) -> list[FireResult]:
+        out: list[FireResult] = []
+        if self.next_fire_start is None or self.max_seen_pane is None:
+            return out
+        s = self.next_fire_start
+        # Skip windows that cannot hold data (before the oldest live pane).
+        first_live = self.first_start_containing(self.pane_start(self.min_live_pane))
+        if s < first_live:
+            s = first_live
+        last_data_start = self.last_start(self.pane_start(self.max_seen_pane + 1) - 1)
+        while s + self.size - 1 <= wm:
+            if s > last_data_start:
+                # No window beyond the newest pane holds data: jump to the first window that can.
+                s = max(s, self._align_up(wm - self.size + 2))
+                break
+            if self._window_overlaps_live(s):
+                r = self._fire_window(s, only_dirty=False)
+                if r is not None:
+                    out.append(r)
+            s += self.slide
+        self.next_fire_start = s
+        return out
+
+    def _align_up(self, t: int) -> int:
+        """Smallest window start >= t."""
+        ls = self.last_start(t)
+        return ls if ls >= t else ls + self.slide
+
+    def _refire(self, pmin: int, pmax: int, old_wm: int) -> list[FireResult]:
+        out: list[FireResult] = []
+        s = self.first_start_containing(self.pane_start(pmin))
+        end_s = min(self.next_fire_start - self.slide, self.last_start(self.pane_start(pmax)))
+        while s <= end_s:
+            if s + self.size - 1 + self.lateness > old_wm:
+                r = self._fire_window(s, only_dirty=True)
+                if r is not None:
+                    out.append(r)
+            s += self.slide
+        for p in range(pmin, pmax + 1):
+            so = (p & (self.ring - 1)) * self.nslots
+            self.dirty_g[so:so + self.nslots].zero_()
+        return out
+
+    def _purge(self, wm: int) -> None:
+        if self.min_live_pane is None:
+            return
+        if wm == I64_MAX:
+            keep_from = self.max_seen_pane + 1
+        else:
+            # Earliest window that is not cleaned: s + size - 1 + lateness > wm.
+            s = self._align_up(wm - self.size - self.lateness + 2)
+            keep_from = self.pane_of(s)
+        p = self.min_live_pane
+        stop = min(keep_from, self.max_seen_pane + 1)
+        if stop - p > self.ring:
+            p = stop - self.ring
+        while p < stop:
+            so = (p & (self.ring - 1)) * self.nslots
+            self.acc_g[so:so + self.nslots].zero_()
+            self.cnt_g[so:so + self.nslots].zero_()
+            self.dirty_g[so:so + self.nslots].zero_()
+            p += 1
+        if keep_from > self.min_live_pane:
+            self.min_live_pane = keep_from
+            if self.min_live_pane > self.max_seen_pane:
+                self.min_live_pane = None
+                self.max_seen_pane = None
+
+    # ---- introspection ---------------------------------------------------------------------
+    def state_bytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in (self.keys_g, self.acc_g, self.cnt_g,
+                                                          self.dirty_g))
+
+    def num_keys(self) -> int:
+        return int(self.occ.sum().item())

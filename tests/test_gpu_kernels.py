@@ -1,0 +1,145 @@
+"""gfx950 kernels vs the C++ twins and plain PyTorch references (needs an MI355X)."""
+import numpy as np
+import pytest
+import torch
+
+from mxstream.ops import expr as E
+from mxstream.ops import kernels as K
+from mxstream.runtime.window_operator import KeyedWindowOperator
+
+pytestmark = pytest.mark.gpu
+
+
+def _gen(dev, n, nkeys, span=10_000, disorder=300, seed=3, f64=False):
+    keys = torch.empty(n, dtype=torch.int64, device=dev)
+    ts = torch.empty_like(keys)
+    vals = torch.empty_like(keys)
+    K.gen_events(keys, ts, vals, seed=seed, stream_id=1, idx0=17, nkeys=nkeys, ts_base=1000,
+                 ts_span=span, disorder=disorder, val_lo=0, val_span=1000, val_f64=f64)
+    return keys, ts, vals
+
+
+def test_native_module_is_loaded(native, gpu_device):
+    assert native.gpu_device_count() >= 1
+    assert native.__file__.endswith(".so")
+
+
+def test_gen_events_bit_exact(gpu_device):
+    g = _gen(gpu_device, 100_003, 777)
+    c = _gen("cpu", 100_003, 777)
+    for a, b in zip(g, c):
+        assert torch.equal(a.cpu(), b)
+
+
+def test_partition_matches_cpu_as_multisets(gpu_device):
+    n = 200_000
+    g = _gen(gpu_device, n, 50_000)
+    c = _gen("cpu", n, 50_000)
+    outs = {}
+    for dev, (keys, ts, vals) in (("gpu", g), ("cpu", c)):
+        d = keys.device
+        plan = K.PartitionPlan(max_parallelism=128, nsub_log2=6, nranks=4, window_mode=1,
+                               drop_late=1, hash_mode=0, bucket_cap=2048, wm=3000, pane_base=0,
+                               size=1000, slide=500, offset=0, pane=500, lateness=100)
+        kg = torch.tensor([(k * 4) // 128 for k in range(128)], dtype=torch.int32, device=d)
+        cursor = torch.zeros(plan.nbuckets, dtype=torch.int32, device=d)
+        out = torch.zeros(plan.nbuckets * plan.bucket_cap * 3, dtype=torch.int64, device=d)
+        stats = K.new_stats(d)
+        K.partition(keys, ts, vals, plan, kg, cursor, out, stats)
+        outs[dev] = (cursor.cpu(), out.cpu().view(plan.nbuckets, plan.bucket_cap, 3), stats.cpu())
+    cg, og, sg = outs["gpu"]
+    cc, oc, sc = outs["cpu"]
+    assert torch.equal(cg, cc)
+    assert torch.equal(sg, sc)
+    assert sg[K.STAT_OVERFLOW] == 0
+    for b in range(cg.numel()):
+        m = int(cg[b])
+        a = og[b, :m].numpy()
+        e = oc[b, :m].numpy()
+        assert np.array_equal(a[np.lexsort(a.T[::-1])], e[np.lexsort(e.T[::-1])])
+
+
+def _results(out):
+    return {(r.window_start, int(k)): (int(a), int(c))
+            for r in out for k, a, c in zip(r.keys, r.raw, r.counts)}
+
+
+@pytest.mark.parametrize("size,slide,lateness", [(2000, 2000, 0), (3000, 1000, 0), (2000, 500, 700)])
+def test_window_operator_gpu_equals_cpu(gpu_device, size, slide, lateness):
+    res = {}
+    for d in (gpu_device, torch.device("cpu")):
+        op = KeyedWindowOperator(size=size, slide=slide, lateness=lateness, agg=K.AGG_SUM_I64,
+                                 device=d, max_keys=20_000, batch_capacity=1 << 16,
+                                 ooo_bound=300, cap_log2=9)
+        out = []
+        for step in range(6):
+            keys, ts, vals = _gen(d, 1 << 16, 20_000, span=2500, disorder=1500, seed=step)
+            ts += step * 2500
+            out += op.process(keys, ts, vals)
+        out += op.finish()
+        res[d.type] = (_results(out), op.metrics.num_late_records_dropped)
+    assert res["cuda"] == res["cpu"]
+
+
+def test_window_sum_vs_torch_reference(gpu_device):
+    """Tumbling window sums vs a plain PyTorch (index_add) reference of the same op."""
+    n = 1 << 20
+    keys, ts, vals = _gen(gpu_device, n, 100_000, span=4000, disorder=0)
+    op = KeyedWindowOperator(size=1000, agg=K.AGG_SUM_I64, device=gpu_device, max_keys=100_000,
+                             batch_capacity=n)
+    out = op.process(keys, ts, vals) + op.finish()
+    got = _results(out)
+    win = torch.div(ts, 1000, rounding_mode="floor")
+    comp = win * 1_000_000 + keys
+    uniq, inv = torch.unique(comp, return_inverse=True)
+    sums = torch.zeros(uniq.numel(), dtype=torch.int64, device=gpu_device).index_add_(0, inv, vals)
+    cnts = torch.zeros(uniq.numel(), dtype=torch.int64, device=gpu_device).index_add_(
+        0, inv, torch.ones_like(vals))
+    exp = {(int(u) // 1_000_000 * 1000, int(u) % 1_000_000): (int(s), int(c))
+           for u, s, c in zip(uniq.cpu(), sums.cpu(), cnts.cpu())}
+    assert got == exp
+
+
+@pytest.mark.parametrize("agg", [K.AGG_SUM_F64, K.AGG_MIN_F64, K.AGG_MAX_F64, K.AGG_AVG_F64])
+def test_float_aggregates_vs_torch(gpu_device, agg):
+    n = 1 << 18
+    keys, ts, vals = _gen(gpu_device, n, 3000, span=1000, disorder=0, f64=True)
+    op = KeyedWindowOperator(size=10_000, agg=agg, device=gpu_device, max_keys=3000,
+                             batch_capacity=n)
+    out = op.process(keys, ts, vals) + op.finish()
+    v = vals.view(torch.float64)
+    uniq, inv = torch.unique(keys, return_inverse=True)
+    if agg in (K.AGG_SUM_F64, K.AGG_AVG_F64):
+        ref = torch.zeros(uniq.numel(), dtype=torch.float64, device=gpu_device).index_add_(0, inv, v)
+        if agg == K.AGG_AVG_F64:
+            ref = ref / torch.bincount(inv).double()
+    else:
+        red = "amin" if agg == K.AGG_MIN_F64 else "amax"
+        ref = torch.zeros(uniq.numel(), dtype=torch.float64, device=gpu_device).scatter_reduce_(
+            0, inv, v, red, include_self=False)
+    exp = dict(zip(uniq.cpu().tolist(), ref.cpu().tolist()))
+    got = {int(k): float(x) for r in out for k, x in zip(r.keys, r.values)}
+    assert set(got) == set(exp)
+    for k, x in exp.items():
+        assert got[k] == pytest.approx(x, rel=1e-12)
+
+
+def test_fire_epilogue_bit_exact(gpu_device):
+    n = 1 << 18
+    m = E.compile_expr(E.var(E.VAR_RESULT) * 8.0 / 60 / 1024 / 1024)
+    f = E.compile_expr(E.var(E.VAR_MAPPED) < 1.5)
+    res = {}
+    for d in (gpu_device, torch.device("cpu")):
+        keys, ts, vals = _gen(d, n, 4000, span=3000, disorder=0)
+        op = KeyedWindowOperator(size=1000, agg=K.AGG_SUM_I64, device=d, max_keys=4000,
+                                 batch_capacity=n, map_prog=m, filter_prog=f)
+        out = op.process(keys, ts, vals) + op.finish()
+        res[d.type] = {(r.window_start, int(k)): float(v) for r in out for k, v in zip(r.keys, r.values)}
+    assert res["cuda"] == res["cpu"] and len(res["cpu"]) > 0
+
+
+def test_expr_filter_gpu(gpu_device):
+    x = torch.linspace(0, 100, 10_001, dtype=torch.float64, device=gpu_device)
+    prog = E.compile_expr(E.var(0) > 90)
+    keep = K.expr_filter(x, prog)
+    assert torch.equal(keep, x > 90)

@@ -1,0 +1,123 @@
+"""KeyedWindowOperator (C++ twin path) vs the Flink-semantics oracle on random streams."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from mxstream.ops import kernels as K
+from mxstream.oracle.flink import BoundedOutOfOrderness, WindowOracle
+from mxstream.runtime.window_operator import KeyedWindowOperator
+
+
+def _run_engine(batches, *, size, slide, lateness, bound, agg, max_keys=4096, cap_log2=8):
+    op = KeyedWindowOperator(size=size, slide=slide, lateness=lateness, agg=agg, device="cpu",
+                             max_keys=max_keys, batch_capacity=256, cap_log2=cap_log2,
+                             ooo_bound=bound)
+    out = []
+    for keys, ts, vals in batches:
+        out += op.process(torch.tensor(keys, dtype=torch.int64), torch.tensor(ts, dtype=torch.int64),
+                          torch.tensor(vals, dtype=torch.int64))
+    out += op.finish()
+    last = {}
+    for r in out:
+        for k, v, raw, c in zip(r.keys.tolist(), r.values.tolist(), r.raw.tolist(), r.counts.tolist()):
+            last[((r.window_start, r.window_end), k)] = (raw, c, v)
+    return last, op
+
+
+def _run_oracle(batches, *, size, slide, lateness, bound):
+    orc = WindowOracle(size=size, slide=slide, lateness=lateness,
+                       add=lambda acc, v: (v, 1) if acc is None else (acc[0] + v, acc[1] + 1))
+    wm = BoundedOutOfOrderness(bound)
+    last = {}
+
+    def rec(ems):
+        for e in ems:
+            last[(e.window, e.key)] = e.value
+
+    for keys, ts, vals in batches:
+        for k, t, v in zip(keys, ts, vals):
+            rec(orc.element(k, t, v))
+            wm.observe(t)
+        rec(orc.watermark(wm.current_watermark()))
+    rec(orc.watermark((1 << 63) - 1))
+    return last, orc
+
+
+def _random_batches(seed, nbatches, per, nkeys, t0, dt, disorder, late_frac=0.0):
+    rnd = random.Random(seed)
+    t = t0
+    out = []
+    for _ in range(nbatches):
+        keys, ts, vals = [], [], []
+        for _ in range(per):
+            t += rnd.randint(0, dt)
+            tt = t - rnd.randint(0, disorder)
+            if rnd.random() < late_frac:
+                tt -= rnd.randint(0, 5 * disorder + 1)
+            keys.append(rnd.randrange(nkeys))
+            ts.append(tt)
+            vals.append(rnd.randint(0, 1000))
+        out.append((keys, ts, vals))
+    return out
+
+
+@pytest.mark.parametrize("size,slide,lateness,bound", [
+    (1000, 1000, 0, 200),     # tumbling
+    (1000, 250, 0, 300),      # sliding
+    (3000, 1000, 500, 400),   # sliding + allowed lateness
+    (600, 600, 1200, 100),    # tumbling + lateness larger than the window
+])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_window_sum_matches_oracle(size, slide, lateness, bound, seed):
+    batches = _random_batches(seed, 12, 80, 37, 10_000, 40, 300, late_frac=0.1)
+    got, op = _run_engine(batches, size=size, slide=slide, lateness=lateness, bound=bound,
+                          agg=K.AGG_SUM_I64)
+    exp, orc = _run_oracle(batches, size=size, slide=slide, lateness=lateness, bound=bound)
+    assert set(got) == set(exp)
+    for kw, (s, c) in exp.items():
+        raw, cnt, _ = got[kw]
+        assert (raw, cnt) == (s, c), kw
+    assert op.metrics.num_late_records_dropped == orc.late_dropped
+
+
+def test_window_count_and_avg():
+    batches = _random_batches(5, 6, 50, 9, 0, 30, 100)
+    got, _ = _run_engine(batches, size=500, slide=500, lateness=0, bound=100, agg=K.AGG_AVG_I64)
+    exp, _ = _run_oracle(batches, size=500, slide=500, lateness=0, bound=100)
+    for kw, (s, c) in exp.items():
+        raw, cnt, val = got[kw]
+        assert cnt == c and raw == s
+        assert val == pytest.approx(s / c)
+
+
+def test_epilogue_map_filter():
+    from mxstream.ops import expr as E
+
+    batches = _random_batches(7, 5, 60, 11, 0, 20, 50)
+    m = E.compile_expr(E.var(E.VAR_RESULT) * 8.0 / 60 / 1024 / 1024)
+    f = E.compile_expr(E.var(E.VAR_MAPPED) < 0.004)
+    op = KeyedWindowOperator(size=400, agg=K.AGG_SUM_I64, device="cpu", max_keys=128,
+                             batch_capacity=128, cap_log2=6, ooo_bound=50, map_prog=m,
+                             filter_prog=f)
+    out = []
+    for keys, ts, vals in batches:
+        out += op.process(torch.tensor(keys), torch.tensor(ts), torch.tensor(vals))
+    out += op.finish()
+    exp, _ = _run_oracle(batches, size=400, slide=400, lateness=0, bound=50)
+    want = {kw: s * 8.0 / 60 / 1024 / 1024 for kw, (s, c) in exp.items()
+            if s * 8.0 / 60 / 1024 / 1024 < 0.004}
+    got = {}
+    for r in out:
+        for k, v in zip(r.keys.tolist(), r.values.tolist()):
+            got[((r.window_start, r.window_end), k)] = v
+    assert got == want  # bit-exact Java double semantics
+
+
+def test_ring_growth_on_event_time_jump():
+    batches = [([1, 2], [0, 10], [1, 1]), ([1], [10_000_000], [5]), ([2], [10_000_050], [7])]
+    got, op = _run_engine(batches, size=100, slide=100, lateness=0, bound=0, agg=K.AGG_SUM_I64)
+    assert got[((0, 100), 1)][:2] == (1, 1)
+    assert got[((10_000_000, 10_000_100), 1)][:2] == (5, 1)
+    assert got[((10_000_000, 10_000_100), 2)][:2] == (7, 1)
