@@ -30,7 +30,7 @@ ExprProg make_prog(const std::vector<int32_t>& code, const std::vector<double>& 
   if (code.size() > (size_t)2 * kExprMaxCode) throw std::invalid_argument("expr program too long");
   if (consts.size() > (size_t)kExprMaxConst) throw std::invalid_argument("too many expr consts");
   // Validate stack discipline so a malformed program can never run off the device stack.
-  int sp = 0;
+  int sp = 0, depth = 0;
   for (size_t i = 0; i < code.size(); i += 2) {
     const int op = code[i], arg = code[i + 1];
     if (op == OP_VAR) {
@@ -48,11 +48,13 @@ ExprProg make_prog(const std::vector<int32_t>& code, const std::vector<double>& 
       throw std::invalid_argument("unknown expr op");
     }
     if (sp > kExprStack) throw std::invalid_argument("expr stack overflow");
+    depth = sp > depth ? sp : depth;
   }
   if (!code.empty() && sp != 1) throw std::invalid_argument("expr must leave exactly one value");
   for (size_t i = 0; i < code.size(); ++i) p.code[i] = code[i];
   for (size_t i = 0; i < consts.size(); ++i) p.consts[i] = consts[i];
   p.ncode = (int32_t)(code.size() / 2);
+  p.depth = depth;
   return p;
 }
 
@@ -66,15 +68,11 @@ PartPlan make_part(py::dict d) {
   p.drop_late = d["drop_late"].cast<int32_t>();
   p.hash_mode = d["hash_mode"].cast<int32_t>();
   p.bucket_cap = d["bucket_cap"].cast<uint32_t>();
-  p.wm = d["wm"].cast<int64_t>();
-  p.pane_base = d["pane_base"].cast<int64_t>();
-  p.win.size = d["size"].cast<int64_t>();
-  p.win.slide = d["slide"].cast<int64_t>();
-  p.win.offset = d["offset"].cast<int64_t>();
-  p.win.pane = d["pane"].cast<int64_t>();
-  p.win.lateness = d["lateness"].cast<int64_t>();
-  if (p.window_mode && (p.win.pane <= 0 || p.win.size <= 0 || p.win.slide <= 0))
-    throw std::invalid_argument("window sizes must be positive");
+  p.late_ts = d["late_ts"].cast<int64_t>();
+  p.tbase = d["tbase"].cast<int64_t>();
+  p.pane = d["pane"].cast<int64_t>();
+  if (p.window_mode && p.pane <= 0) throw std::invalid_argument("pane length must be positive");
+  p.inv_pane = p.pane > 0 ? 1.0 / (double)p.pane : 0.0;
   if (p.max_parallelism <= 0 || p.nranks <= 0 || p.nsub_log2 < 0 || p.nsub_log2 > 20)
     throw std::invalid_argument("bad partition plan");
   return p;
@@ -192,6 +190,13 @@ PYBIND11_MODULE(_mxs_native, m) {
                  P<uint64_t>(acc_g), P<uint32_t>(cnt_g), P<uint32_t>(occ), P<uint32_t>(flags),
                  P<uint64_t>(out_vals), stream);
   });
+  m.def("gpu_step_begin", [](intptr_t cursor, int nb, intptr_t stats, intptr_t stream) {
+    gpu::step_begin(P<uint32_t>(cursor), nb, P<int64_t>(stats), stream);
+  });
+  m.def("gpu_step_finish", [](intptr_t stats, intptr_t lm, int64_t bound, int32_t ev,
+                              int64_t now, intptr_t red, intptr_t stream) {
+    gpu::step_finish(P<int64_t>(stats), P<int64_t>(lm), bound, ev, now, P<int64_t>(red), stream);
+  });
   m.def("gpu_expr_filter", [](intptr_t x, int64_t n, std::vector<int32_t> code,
                               std::vector<double> consts, intptr_t keep, intptr_t stream) {
     gpu::expr_filter(P<double>(x), n, make_prog(code, consts), P<uint8_t>(keep), stream);
@@ -239,6 +244,13 @@ PYBIND11_MODULE(_mxs_native, m) {
     py::gil_scoped_release nogil;
     cpu::rolling(P<Rec>(recs), P<uint32_t>(counts), rp, P<uint64_t>(keys_g), P<uint64_t>(acc_g),
                  P<uint32_t>(cnt_g), P<uint32_t>(occ), P<uint32_t>(flags), P<uint64_t>(out_vals));
+  });
+  m.def("cpu_step_begin", [](intptr_t cursor, int nb, intptr_t stats) {
+    cpu::step_begin(P<uint32_t>(cursor), nb, P<int64_t>(stats));
+  });
+  m.def("cpu_step_finish", [](intptr_t stats, intptr_t lm, int64_t bound, int32_t ev, int64_t now,
+                              intptr_t red) {
+    cpu::step_finish(P<int64_t>(stats), P<int64_t>(lm), bound, ev, now, P<int64_t>(red));
   });
   m.def("cpu_expr_filter", [](intptr_t x, int64_t n, std::vector<int32_t> code,
                               std::vector<double> consts, intptr_t keep) {

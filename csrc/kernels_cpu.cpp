@@ -16,16 +16,18 @@ void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
                 int32_t val_f64) {
+  auto mulhi = [](uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); };
+  const double span_per_event = (double)ts_span / (double)n;
+  const uint64_t disorder_p1 = (uint64_t)(disorder + 1);
   for (int64_t i = 0; i < n; ++i) {
     const uint64_t r = rng64(seed, stream_id, idx0 + (uint64_t)i);
     const uint64_t r2 = mix64(r);
     const uint64_t r3 = mix64(r2);
-    keys[i] = (uint64_t)(((unsigned __int128)r * nkeys) >> 64);
-    int64_t t = ts_base +
-                (int64_t)(((unsigned __int128)(uint64_t)i * (uint64_t)ts_span) / (uint64_t)n);
-    if (disorder > 0) t -= (int64_t)(r2 % (uint64_t)(disorder + 1));
+    keys[i] = mulhi(r, nkeys);
+    int64_t t = ts_base + (int64_t)((double)i * span_per_event);
+    if (disorder_p1 > 1) t -= (int64_t)mulhi(r2, disorder_p1);
     ts[i] = t;
-    const int64_t v = val_lo + (val_span > 0 ? (int64_t)(r3 % (uint64_t)val_span) : 0);
+    const int64_t v = val_lo + (val_span > 0 ? (int64_t)mulhi(r3, (uint64_t)val_span) : 0);
     vals[i] = val_f64 ? f64_bits((double)v) : (uint64_t)v;
   }
 }
@@ -33,16 +35,16 @@ void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t
 void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                const int32_t* jhash_tab, int64_t n, const PartPlan& p, const int32_t* kg_dest,
                uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap) {
-  int64_t tmax = stats[kStatMaxTs], pmin = stats[kStatMinPane], pmax = stats[kStatMaxPane];
+  int64_t tmax = stats[kStatMaxTs], qmin = stats[kStatMinPane], qmax = stats[kStatMaxPane];
   int64_t nlate = 0, nacc = 0;
-  bool ovf = false;
+  int64_t ovf = 0;
   for (int64_t i = 0; i < n; ++i) {
     const uint64_t key = keys[i];
     const int64_t t = ts[i];
     tmax = std::max(tmax, t);
     uint32_t rt = 0;
     if (p.window_mode) {
-      if (p.drop_late && element_is_late(t, p.win, p.wm)) {
+      if (p.drop_late && t < p.late_ts) {
         if (late_idx) {
           const int64_t pos = stats[kStatLate] + nlate;
           if (pos < (int64_t)late_cap) late_idx[pos] = (uint32_t)i;
@@ -50,10 +52,13 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
         ++nlate;
         continue;
       }
-      const int64_t pane = pane_of(t, p.win);
-      pmin = std::min(pmin, pane);
-      pmax = std::max(pmax, pane);
-      rt = (uint32_t)(pane - p.pane_base);
+      int64_t q;
+      if (!rel_pane(t, p, &rt, &q)) {
+        ovf |= 2;
+        continue;
+      }
+      qmin = std::min(qmin, q);
+      qmax = std::max(qmax, q);
     }
     ++nacc;
     const int32_t jh = p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
@@ -66,15 +71,37 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
       r.t = rt;
       r.aux = (uint32_t)i;
     } else {
-      ovf = true;
+      ovf |= 1;
     }
   }
   stats[kStatMaxTs] = tmax;
-  stats[kStatMinPane] = pmin;
-  stats[kStatMaxPane] = pmax;
+  stats[kStatMinPane] = qmin;
+  stats[kStatMaxPane] = qmax;
   stats[kStatLate] += nlate;
   stats[kStatAccepted] += nacc;
-  if (ovf) stats[kStatOverflow] |= 1;
+  stats[kStatOverflow] |= ovf;
+}
+
+void step_begin(uint32_t* cursor, int nb, int64_t* stats) {
+  std::memset(cursor, 0, sizeof(uint32_t) * (size_t)nb);
+  for (int j = 0; j < kStatCount; ++j)
+    stats[j] = j == kStatMaxTs ? INT64_MIN : j == kStatMinPane ? INT64_MAX
+             : j == kStatMaxPane ? INT64_MIN : 0;
+}
+
+void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
+                 int64_t proc_now, int64_t* red) {
+  int64_t lm = std::max(local_maxts[0], stats[kStatMaxTs]);
+  local_maxts[0] = lm;
+  const int64_t wm = event_mode ? (lm == INT64_MIN ? INT64_MIN : lm - bound) : proc_now;
+  const int64_t qmax = stats[kStatMaxPane];
+  red[0] = qmax == INT64_MIN ? INT64_MAX : -qmax;
+  red[1] = stats[kStatMinPane];
+  red[2] = wm;
+  red[3] = -(stats[kStatOverflow] & 1);
+  red[4] = -((stats[kStatOverflow] >> 1) & 1);
+  red[5] = red[6] = red[7] = 0;
+  for (int j = 0; j < kStatCount; ++j) red[8 + j] = stats[j];
 }
 
 static inline uint32_t probe_insert(uint64_t* keys, uint64_t key, uint32_t mask, bool* inserted) {

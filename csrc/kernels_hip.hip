@@ -79,18 +79,18 @@ __device__ __forceinline__ uint64_t f64_unord(int64_t o) {
 __global__ __launch_bounds__(256) void gen_events_kernel(
     uint64_t* __restrict__ keys, int64_t* __restrict__ ts, uint64_t* __restrict__ vals,
     int64_t n, uint64_t seed, uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
-    int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span, int32_t val_f64) {
+    double span_per_event, uint64_t disorder_p1, int64_t val_lo, uint64_t val_span,
+    int32_t val_f64) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint64_t r = rng64(seed, stream_id, idx0 + (uint64_t)i);
     const uint64_t r2 = mix64(r);
     const uint64_t r3 = mix64(r2);
-    keys[i] = (uint64_t)(((unsigned __int128)r * nkeys) >> 64);
-    int64_t t = ts_base + (int64_t)(((unsigned __int128)(uint64_t)i * (uint64_t)ts_span) /
-                                    (uint64_t)n);
-    if (disorder > 0) t -= (int64_t)(r2 % (uint64_t)(disorder + 1));
+    keys[i] = __umul64hi(r, nkeys);  // multiply-shift: uniform in [0, nkeys), no division
+    int64_t t = ts_base + (int64_t)((double)i * span_per_event);
+    if (disorder_p1 > 1) t -= (int64_t)__umul64hi(r2, disorder_p1);
     ts[i] = t;
-    const int64_t v = val_lo + (val_span > 0 ? (int64_t)(r3 % (uint64_t)val_span) : 0);
+    const int64_t v = val_lo + (val_span ? (int64_t)__umul64hi(r3, val_span) : 0);
     vals[i] = val_f64 ? f64_bits((double)v) : (uint64_t)v;
   }
 }
@@ -98,36 +98,38 @@ __global__ __launch_bounds__(256) void gen_events_kernel(
 // ------------------------------------------------------------------------------------------
 // Partition: keyBy (Flink key groups -> dest rank) x sub-table, window assignment, late drop.
 // ------------------------------------------------------------------------------------------
+// Per-element partition decision; identical code runs in pass A (histogram) and pass B
+// (scatter) so both passes agree without storing per-element bucket ids.
+// kind: 0 = keep, 1 = late (dropped), 2 = unrepresentable pane (overflow)
 struct PartEval {
-  bool keep;
+  int kind;
   uint32_t bucket;
   uint32_t t;
 };
 
-__device__ __forceinline__ PartEval part_eval(uint64_t key, int64_t t, const int32_t* jhash_tab,
-                                              const PartPlan& p, const int32_t* kg_dest,
-                                              int64_t* pane_out, bool* late_out) {
+__device__ __forceinline__ PartEval part_eval(uint64_t key, int64_t ts, const int32_t* jhash_tab,
+                                              const PartPlan& p, const int32_t* kg_dest) {
   PartEval e;
-  e.keep = true;
+  e.kind = 0;
   e.t = 0;
-  *late_out = false;
+  e.bucket = 0;
   if (p.window_mode) {
-    if (p.drop_late && element_is_late(t, p.win, p.wm)) {
-      e.keep = false;
-      *late_out = true;
-      e.bucket = 0;
+    if (p.drop_late && ts < p.late_ts) {
+      e.kind = 1;
       return e;
     }
-    const int64_t pane = pane_of(t, p.win);
-    *pane_out = pane;
-    e.t = (uint32_t)(pane - p.pane_base);
+    int64_t q;
+    if (!rel_pane(ts, p, &e.t, &q)) {
+      e.kind = 2;
+      return e;
+    }
   }
   const int32_t jh = p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
   e.bucket = bucket_of(key, jh, p, kg_dest);
   return e;
 }
 
-__global__ __launch_bounds__(512) void partition_kernel(
+__global__ __launch_bounds__(1024) void partition_kernel(
     const uint64_t* __restrict__ keys, const int64_t* __restrict__ ts,
     const uint64_t* __restrict__ vals, const int32_t* __restrict__ jhash_tab, int64_t n,
     int64_t chunk, PartPlan plan, const int32_t* __restrict__ kg_dest,
@@ -140,17 +142,20 @@ __global__ __launch_bounds__(512) void partition_kernel(
 
   const int64_t start = (int64_t)blockIdx.x * chunk;
   const int64_t end = start + chunk < n ? start + chunk : n;
-  int64_t tmax = INT64_MIN, pmin = INT64_MAX, pmax = INT64_MIN, nlate = 0, nacc = 0;
+  int64_t tmax = INT64_MIN, qmin = INT64_MAX, qmax = INT64_MIN, nlate = 0, nacc = 0;
+  bool bad = false;
 
   // Pass A: histogram + stats.
   for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
     const uint64_t key = keys[i];
     const int64_t t = ts[i];
     tmax = t > tmax ? t : tmax;
-    int64_t pane = 0;
-    bool late;
-    PartEval e = part_eval(key, t, jhash_tab, plan, kg_dest, &pane, &late);
-    if (!e.keep) {
+    const PartEval e = part_eval(key, t, jhash_tab, plan, kg_dest);
+    if (e.kind) {
+      if (e.kind == 2) {
+        bad = true;
+        continue;
+      }
       ++nlate;
       if (late_idx) {
         const unsigned long long pos = atomicAdd((unsigned long long*)&stats[kStatLate], 1ull);
@@ -159,13 +164,14 @@ __global__ __launch_bounds__(512) void partition_kernel(
       continue;
     }
     ++nacc;
-    pmin = pane < pmin ? pane : pmin;
-    pmax = pane > pmax ? pane : pmax;
+    qmin = (int64_t)e.t < qmin ? (int64_t)e.t : qmin;
+    qmax = (int64_t)e.t > qmax ? (int64_t)e.t : qmax;
     atomicAdd(&lhist[e.bucket], 1u);
   }
   __syncthreads();
 
-  // Reserve one run per bucket: a single global atomic per (block, non-empty bucket).
+  // Reserve one run per bucket: one global atomic per (workgroup, non-empty bucket). With
+  // 64K events per workgroup a run averages >= 32 records, so the scatter below writes runs.
   bool overflow = false;
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
     const uint32_t c = lhist[b];
@@ -181,11 +187,8 @@ __global__ __launch_bounds__(512) void partition_kernel(
   const uint32_t bcap = plan.bucket_cap;
   for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
     const uint64_t key = keys[i];
-    const int64_t t = ts[i];
-    int64_t pane = 0;
-    bool late;
-    PartEval e = part_eval(key, t, jhash_tab, plan, kg_dest, &pane, &late);
-    if (!e.keep) continue;
+    const PartEval e = part_eval(key, ts[i], jhash_tab, plan, kg_dest);
+    if (e.kind) continue;
     const uint32_t pos = atomicAdd(&lhist[e.bucket], 1u);
     if (pos < bcap) {
       Rec r;
@@ -199,21 +202,58 @@ __global__ __launch_bounds__(512) void partition_kernel(
 
   // Block stats -> one atomic per wave.
   tmax = wave_max_i64(tmax);
-  pmin = wave_min_i64(pmin);
-  pmax = wave_max_i64(pmax);
+  qmin = wave_min_i64(qmin);
+  qmax = wave_max_i64(qmax);
   nacc = wave_sum_i64(nacc);
   if (!late_idx) nlate = wave_sum_i64(nlate);
   const unsigned long long ovf = __ballot(overflow);
+  const unsigned long long badm = __ballot(bad);
   if (lane_id() == 0) {
     atomicMax((long long*)&stats[kStatMaxTs], (long long)tmax);
     if (nacc) {
-      atomicMin((long long*)&stats[kStatMinPane], (long long)pmin);
-      atomicMax((long long*)&stats[kStatMaxPane], (long long)pmax);
+      atomicMin((long long*)&stats[kStatMinPane], (long long)qmin);
+      atomicMax((long long*)&stats[kStatMaxPane], (long long)qmax);
       atomicAdd((unsigned long long*)&stats[kStatAccepted], (unsigned long long)nacc);
     }
     if (!late_idx && nlate) atomicAdd((unsigned long long*)&stats[kStatLate], (unsigned long long)nlate);
     if (ovf) atomicOr((unsigned long long*)&stats[kStatOverflow], 1ull);
+    if (badm) atomicOr((unsigned long long*)&stats[kStatOverflow], 2ull);
   }
+}
+
+// Step prologue: zero the bucket cursors and reset the stats block (one launch instead of two
+// memsets + a host copy).
+__global__ __launch_bounds__(256) void step_begin_kernel(uint32_t* __restrict__ cursor, int nb,
+                                                         int64_t* __restrict__ stats) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x)
+    cursor[i] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < kStatCount) {
+    const int j = threadIdx.x;
+    stats[j] = j == kStatMaxTs ? INT64_MIN : j == kStatMinPane ? INT64_MAX
+             : j == kStatMaxPane ? INT64_MIN : 0;
+  }
+}
+
+// Step epilogue: fold this batch into the source partition's watermark and build the vector
+// the watermark valve all-reduces (MIN): [-max pane, min pane, wm, -bucket ovf, -pane ovf] plus
+// a copy of the raw stats for the host (red[8..15]).
+__global__ void step_finish_kernel(const int64_t* __restrict__ stats, int64_t* __restrict__ local_maxts,
+                                   int64_t bound, int32_t event_mode, int64_t proc_now,
+                                   int64_t* __restrict__ red) {
+  if (threadIdx.x != 0) return;
+  int64_t lm = local_maxts[0];
+  const int64_t bm = stats[kStatMaxTs];
+  lm = bm > lm ? bm : lm;
+  local_maxts[0] = lm;
+  const int64_t wm = event_mode ? (lm == INT64_MIN ? INT64_MIN : lm - bound) : proc_now;
+  const int64_t qmax = stats[kStatMaxPane];
+  red[0] = qmax == INT64_MIN ? INT64_MAX : -qmax;
+  red[1] = stats[kStatMinPane];
+  red[2] = wm;
+  red[3] = -(stats[kStatOverflow] & 1);
+  red[4] = -((stats[kStatOverflow] >> 1) & 1);
+  red[5] = red[6] = red[7] = 0;
+  for (int j = 0; j < kStatCount; ++j) red[8 + j] = stats[j];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -357,12 +397,23 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
 // ------------------------------------------------------------------------------------------
 // Window firing: sweep slots (pane-major => coalesced), combine the window's panes, evaluate
 // the fused map/filter epilogue and compact the emitted rows with one atomic per wave.
+// The epilogue VM keeps its operand stack and variables in per-lane LDS columns (a runtime-
+// indexed private array would live in scratch memory).
 // ------------------------------------------------------------------------------------------
+struct LdsCol {
+  double* base;
+  __device__ __forceinline__ double get(int i) const { return base[i * 256]; }
+  __device__ __forceinline__ void set(int i, double x) { base[i * 256] = x; }
+};
+
 __global__ __launch_bounds__(256) void window_fire_kernel(
     const uint64_t* __restrict__ keys_g, const uint64_t* __restrict__ acc_g,
     const uint32_t* __restrict__ cnt_g, const uint8_t* __restrict__ dirty_g, FirePlan p,
     uint64_t* __restrict__ out_keys, double* __restrict__ out_vals, uint64_t* __restrict__ out_raw,
     uint32_t* __restrict__ out_cnt, uint32_t* __restrict__ out_n) {
+  extern __shared__ __attribute__((aligned(16))) double fsm[];  // [kExprVars + depth][256]
+  LdsCol vars{fsm + threadIdx.x};
+  LdsCol stack{fsm + kExprVars * 256 + threadIdx.x};
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t nslots = p.nslots;
   // Uniform trip count so every lane reaches the ballot.
@@ -388,17 +439,20 @@ __global__ __launch_bounds__(256) void window_fire_kernel(
       }
       if (cnt && dirty) {
         key = keys_g[s];
-        double vars[kExprVars];
-        vars[0] = agg_result_f64(p.agg, acc, cnt);
-        vars[1] = (double)cnt;
-        vars[2] = p.wstart;
-        vars[3] = p.wend;
-        vars[4] = (double)key;
-        vars[5] = (double)(int64_t)acc;
-        vars[6] = p.map.ncode ? expr_eval(p.map, vars) : vars[0];
-        vars[7] = 0.0;
-        val = vars[6];
-        emit = p.filt.ncode ? (expr_eval(p.filt, vars) != 0.0) : true;
+        const double v0 = agg_result_f64(p.agg, acc, cnt);
+        val = v0;
+        emit = true;
+        if (p.map.ncode || p.filt.ncode) {
+          vars.set(0, v0);
+          vars.set(1, (double)cnt);
+          vars.set(2, p.wstart);
+          vars.set(3, p.wend);
+          vars.set(4, (double)key);
+          vars.set(5, (double)(int64_t)acc);
+          if (p.map.ncode) val = expr_eval_t(p.map, stack, vars);
+          vars.set(6, val);
+          if (p.filt.ncode) emit = expr_eval_t(p.filt, stack, vars) != 0.0;
+        }
       }
     }
     const unsigned long long m = __ballot(emit);
@@ -422,10 +476,13 @@ __global__ __launch_bounds__(256) void window_fire_kernel(
 // Stateless predicate (chapter1 filter `usage > 90`, Main.java:31) over one f64 column.
 __global__ __launch_bounds__(256) void expr_filter_kernel(const double* __restrict__ x, int64_t n,
                                                           ExprProg prog, uint8_t* __restrict__ keep) {
+  extern __shared__ __attribute__((aligned(16))) double fsm[];
+  LdsCol vars{fsm + threadIdx.x};
+  LdsCol stack{fsm + kExprVars * 256 + threadIdx.x};
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    double vars[kExprVars] = {x[i], 0, 0, 0, 0, 0, 0, 0};
-    keep[i] = expr_eval(prog, vars) != 0.0;
+    vars.set(0, x[i]);
+    keep[i] = expr_eval_t(prog, stack, vars) != 0.0;
   }
 }
 
@@ -452,7 +509,21 @@ void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t
   if (n <= 0) return;
   hipLaunchKernelGGL(gen_events_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, keys, ts, vals, n, seed, stream_id, idx0, nkeys, ts_base,
-                     ts_span, disorder, val_lo, val_span, val_f64);
+                     (double)ts_span / (double)n, (uint64_t)(disorder + 1), val_lo,
+                     (uint64_t)val_span, val_f64);
+  HIP_CHECK(hipGetLastError());
+}
+
+void step_begin(uint32_t* cursor, int nb, int64_t* stats, intptr_t stream) {
+  hipLaunchKernelGGL(step_begin_kernel, dim3(grid_for(nb, 256, 64)), dim3(256), 0,
+                     (hipStream_t)stream, cursor, nb, stats);
+  HIP_CHECK(hipGetLastError());
+}
+
+void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
+                 int64_t proc_now, int64_t* red, intptr_t stream) {
+  hipLaunchKernelGGL(step_finish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, stats,
+                     local_maxts, bound, event_mode, proc_now, red);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -463,11 +534,17 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
   if (n <= 0) return;
   const int nb = plan.nranks << plan.nsub_log2;
   if (nb > 16384) throw std::runtime_error("partition: too many buckets (max 16384)");
-  // ~8K events per workgroup keeps runs per bucket long while filling 256 CUs x 4.
-  int blocks = grid_for(n, 8192, 2048);
-  if (blocks < 256 && n > 256 * 1024) blocks = 256;
+  // 64K events per 1024-thread workgroup: one workgroup per CU at 16M events, bucket runs of
+  // >= 32 records, and nb global reservations per workgroup instead of per 8K events.
+  int blocks = grid_for(n, 65536, 1024);
   const int64_t chunk = (n + blocks - 1) / blocks;
-  hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(512), (size_t)nb * 4,
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)partition_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(1024), (size_t)nb * 4,
                      (hipStream_t)stream, keys, ts, vals, jhash_tab, n, chunk, plan, kg_dest,
                      cursor, out, stats, late_idx, late_cap);
   HIP_CHECK(hipGetLastError());
@@ -521,7 +598,10 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
                  double* out_vals, uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n,
                  intptr_t stream) {
   if (plan.nslots <= 0) return;
-  hipLaunchKernelGGL(window_fire_kernel, dim3(grid_for(plan.nslots, 256, 4096)), dim3(256), 0,
+  const size_t lds = (size_t)(kExprVars + (plan.map.depth > plan.filt.depth ? plan.map.depth
+                                                                             : plan.filt.depth)) *
+                     256 * sizeof(double);
+  hipLaunchKernelGGL(window_fire_kernel, dim3(grid_for(plan.nslots, 256, 4096)), dim3(256), lds,
                      (hipStream_t)stream, keys_g, acc_g, cnt_g, dirty_g, plan, out_keys, out_vals,
                      out_raw, out_cnt, out_n);
   HIP_CHECK(hipGetLastError());
@@ -530,7 +610,8 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
 void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep,
                  intptr_t stream) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(expr_filter_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+  const size_t lds = (size_t)(kExprVars + prog.depth) * 256 * sizeof(double);
+  hipLaunchKernelGGL(expr_filter_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), lds,
                      (hipStream_t)stream, x, n, prog, keep);
   HIP_CHECK(hipGetLastError());
 }

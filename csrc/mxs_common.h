@@ -248,25 +248,33 @@ struct ExprProg {
   int32_t code[kExprMaxCode];  // (op, arg) pairs
   double consts[kExprMaxConst];
   int32_t ncode;               // number of (op,arg) pairs; 0 = empty program
-  int32_t pad;
+  int32_t depth;               // max stack depth (validated on the host)
 };
 
-MXS_HD double expr_eval(const ExprProg& p, const double* vars) {
-  double st[kExprStack];
+// The VM is templated on where its stack lives: a local array on the host, a per-lane LDS
+// column on the GPU (a runtime-indexed private array would be spilled to scratch memory).
+struct LocalStack {
+  double v[kExprStack];
+  MXS_HD double get(int i) const { return v[i]; }
+  MXS_HD void set(int i, double x) { v[i] = x; }
+};
+
+template <class Stack, class Vars>
+MXS_HD double expr_eval_t(const ExprProg& p, Stack& st, const Vars& vars) {
   int sp = 0;
   for (int i = 0; i < p.ncode; ++i) {
     const int32_t op = p.code[2 * i];
     const int32_t arg = p.code[2 * i + 1];
     switch (op) {
-      case OP_VAR: st[sp++] = vars[arg]; break;
-      case OP_CONST: st[sp++] = p.consts[arg]; break;
-      case OP_NOT: st[sp - 1] = (st[sp - 1] == 0.0) ? 1.0 : 0.0; break;
-      case OP_NEG: st[sp - 1] = -st[sp - 1]; break;
-      case OP_ABS: st[sp - 1] = st[sp - 1] < 0 ? -st[sp - 1] : st[sp - 1]; break;
-      case OP_TOINT: st[sp - 1] = (double)(int64_t)st[sp - 1]; break;
+      case OP_VAR: st.set(sp++, vars.get(arg)); break;
+      case OP_CONST: st.set(sp++, p.consts[arg]); break;
+      case OP_NOT: st.set(sp - 1, st.get(sp - 1) == 0.0 ? 1.0 : 0.0); break;
+      case OP_NEG: st.set(sp - 1, -st.get(sp - 1)); break;
+      case OP_ABS: { const double a = st.get(sp - 1); st.set(sp - 1, a < 0 ? -a : a); break; }
+      case OP_TOINT: st.set(sp - 1, (double)(int64_t)st.get(sp - 1)); break;
       default: {
-        const double b = st[--sp];
-        const double a = st[sp - 1];
+        const double b = st.get(--sp);
+        const double a = st.get(sp - 1);
         double r = 0.0;
         switch (op) {
           case OP_ADD: r = a + b; break;
@@ -290,11 +298,36 @@ MXS_HD double expr_eval(const ExprProg& p, const double* vars) {
 #endif
           default: break;
         }
-        st[sp - 1] = r;
+        st.set(sp - 1, r);
       }
     }
   }
-  return sp > 0 ? st[sp - 1] : 0.0;
+  return sp > 0 ? st.get(sp - 1) : 0.0;
+}
+
+struct ArrayVars {
+  const double* v;
+  MXS_HD double get(int i) const { return v[i]; }
+};
+
+MXS_HD double expr_eval(const ExprProg& p, const double* vars) {
+  LocalStack st;
+  ArrayVars va{vars};
+  return expr_eval_t(p, st, va);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Division-free pane arithmetic. CDNA has no integer divider: a 64-bit `/` or `%` is a software
+// routine of ~100 instructions. Pane ids are floor(t_rel / pane) with t_rel >= 0 relative to the
+// step's base; the quotient comes from one f64 multiply by the host-computed reciprocal and is
+// corrected by at most one (exact for t_rel < 2^52).
+// ---------------------------------------------------------------------------------------------
+MXS_HD int64_t fast_floor_div_pos(int64_t t_rel, int64_t d, double inv_d) {
+  int64_t q = (int64_t)((double)t_rel * inv_d);
+  const int64_t r = t_rel - q * d;
+  if (r < 0) --q;
+  else if (r >= d) ++q;
+  return q;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -305,13 +338,16 @@ struct PartPlan {
   int32_t nsub_log2;         // sub-tables per rank = 1 << nsub_log2
   int32_t nranks;            // G (destination ranks)
   int32_t window_mode;       // 0 = keyed (no window, t = 0), 1 = windowed (t = pane - pane_base)
-  int32_t drop_late;         // 1: late elements are dropped (and optionally side-output)
+  int32_t drop_late;         // 1: elements with ts < late_ts are dropped (and optionally side-output)
   int32_t hash_mode;         // 0: Long.hashCode(key); 1: jhash table lookup (string dict ids)
   uint32_t bucket_cap;       // fixed capacity of one (dest, sub) bucket in the send buffer
   uint32_t pad0;
-  int64_t wm;                // current watermark (late check)
-  int64_t pane_base;         // records carry pane - pane_base
-  WinParams win;
+  // ts < late_ts  <=>  every window of the element is past cleanup (maxTs + lateness <= wm):
+  // late_ts is the smallest window start whose cleanup time is still ahead of the watermark.
+  int64_t late_ts;
+  int64_t tbase;             // pane_start(pane_base): records carry floor((ts - tbase) / pane)
+  int64_t pane;              // pane length (ms)
+  double inv_pane;           // 1.0 / pane
 };
 
 MXS_HD uint32_t bucket_of(uint64_t key, int32_t jhash, const PartPlan& p, const int32_t* kg_dest) {
@@ -321,10 +357,24 @@ MXS_HD uint32_t bucket_of(uint64_t key, int32_t jhash, const PartPlan& p, const 
   return ((uint32_t)dest << p.nsub_log2) | sub;
 }
 
+// Relative pane of a (non-late) element; returns false when it cannot be represented
+// (ts before the step base, or more than 2^32 panes ahead) — reported as an overflow.
+MXS_HD bool rel_pane(int64_t ts, const PartPlan& p, uint32_t* t_out, int64_t* pane_abs_rel) {
+  const int64_t d = ts - p.tbase;
+  if (d < 0 || d >= (int64_t)1 << 52) return false;
+  const int64_t q = fast_floor_div_pos(d, p.pane, p.inv_pane);
+  if (q >= ((int64_t)1 << 32)) return false;
+  *t_out = (uint32_t)q;
+  *pane_abs_rel = q;
+  return true;
+}
+
 // Stats block written by the partition pass (all int64):
 //   [0] max ts (all events, used for the watermark)    [1] min pane of non-late events
 //   [2] max pane of non-late events                     [3] late (dropped) events
-//   [4] overflow flag (bucket capacity exceeded)        [5] events accepted
+//   [4] overflow flags: bit0 bucket capacity exceeded,  [5] events accepted
+//       bit1 an element's pane is not representable
+// Panes in [1]/[2] are relative to the step's pane base.
 constexpr int kStatMaxTs = 0, kStatMinPane = 1, kStatMaxPane = 2, kStatLate = 3, kStatOverflow = 4,
               kStatAccepted = 5, kStatCount = 8;
 

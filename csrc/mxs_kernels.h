@@ -74,6 +74,9 @@ void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& plan, uint
              uint64_t* acc_g, uint32_t* cnt_g, uint32_t* occupancy, uint32_t* flags,
              uint64_t* out_vals, intptr_t stream);
 void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep, intptr_t stream);
+void step_begin(uint32_t* cursor, int nb, int64_t* stats, intptr_t stream);
+void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
+                 int64_t proc_now, int64_t* red, intptr_t stream);
 }  // namespace gpu
 
 // ---- CPU twins (kernels_cpu.cpp) ------------------------------------------------------------
@@ -95,6 +98,9 @@ void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& plan, uint
              uint64_t* acc_g, uint32_t* cnt_g, uint32_t* occupancy, uint32_t* flags,
              uint64_t* out_vals);
 void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep);
+void step_begin(uint32_t* cursor, int nb, int64_t* stats);
+void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
+                 int64_t proc_now, int64_t* red);
 }  // namespace cpu
 
 }  // namespace mxs

@@ -84,6 +84,8 @@ def gen_events(keys, ts, vals, *, seed: int, stream_id: int, idx0: int, nkeys: i
 
 @dataclass
 class PartitionPlan:
+    """keyBy + window assignment plan of one step (csrc/mxs_common.h PartPlan)."""
+
     max_parallelism: int
     nsub_log2: int
     nranks: int
@@ -91,13 +93,9 @@ class PartitionPlan:
     drop_late: int
     hash_mode: int
     bucket_cap: int
-    wm: int
-    pane_base: int
-    size: int = 1
-    slide: int = 1
-    offset: int = 0
-    pane: int = 1
-    lateness: int = 0
+    late_ts: int = I64_MIN   # elements with ts < late_ts are late (all windows cleaned)
+    tbase: int = 0           # start of the step's base pane
+    pane: int = 1            # pane length (ms)
 
     @property
     def nbuckets(self) -> int:
@@ -227,6 +225,33 @@ def rolling(recs, counts, *, cap_log2: int, nsub: int, agg: int, nsrc: int, buck
         m.gpu_rolling(*args, _stream(keys_g))
     else:
         m.cpu_rolling(*args)
+
+
+def step_begin(cursor: torch.Tensor, stats: torch.Tensor) -> None:
+    _check(stats, torch.int64, STAT_COUNT, "stats", cursor.device)
+    _check(cursor, torch.int32, cursor.numel(), "cursor", cursor.device)
+    m = load()
+    if _is_gpu(cursor):
+        m.gpu_step_begin(_p(cursor), cursor.numel(), _p(stats), _stream(cursor))
+    else:
+        m.cpu_step_begin(_p(cursor), cursor.numel(), _p(stats))
+
+
+RED_WORDS = 16  # [-qmax, qmin, wm, -bucket_ovf, -pane_ovf, 0, 0, 0, stats[8]]
+
+
+def step_finish(stats: torch.Tensor, local_maxts: torch.Tensor, red: torch.Tensor, *,
+                bound: int, event_mode: bool, proc_now: int) -> None:
+    dev = stats.device
+    _check(stats, torch.int64, STAT_COUNT, "stats", dev)
+    _check(local_maxts, torch.int64, 1, "local_maxts", dev)
+    _check(red, torch.int64, RED_WORDS, "red", dev)
+    m = load()
+    args = (_p(stats), _p(local_maxts), int(bound), int(event_mode), int(proc_now), _p(red))
+    if _is_gpu(stats):
+        m.gpu_step_finish(*args, _stream(stats))
+    else:
+        m.cpu_step_finish(*args)
 
 
 def expr_filter(x: torch.Tensor, prog: _expr.Program) -> torch.Tensor:

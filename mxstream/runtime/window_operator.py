@@ -141,7 +141,7 @@ class KeyedWindowOperator:
         self.nbuckets = self.world << self.nsub_log2
         self._alloc_buckets(batch_capacity, bucket_slack)
         self.stats = K.new_stats(dev)
-        self._stats_init = K.new_stats(dev)
+        self.red = torch.zeros(K.RED_WORDS, dtype=torch.int64, device=dev)
         self.local_maxts = torch.full((1,), I64_MIN, dtype=torch.int64, device=dev)
         self.out_keys = torch.empty(self.nslots, dtype=torch.int64, device=dev)
         self.out_vals = torch.empty(self.nslots, dtype=torch.float64, device=dev)
@@ -214,14 +214,25 @@ class KeyedWindowOperator:
 
     # ---- main entry points ---------------------------------------------------------------
     def _pane_base(self, ts: torch.Tensor) -> int:
-        if self.wm > I64_MIN and self.time_mode == "event":
-            return self.pane_of(max(self.wm - self.size - self.lateness + 1, I64_MIN + 1))
-        # No watermark yet: take the batch minimum (one reduction; happens before the first WM).
-        base = self.min_live_pane if self.min_live_pane is not None else None
-        if ts.numel():
-            bmin = self.pane_of(int(ts.min().item()))
-            base = bmin if base is None else min(base, bmin)
-        return base if base is not None else 0
+        """Base pane of the step, identical on every rank (records carry pane - base)."""
+        if self.wm > I64_MIN:
+            # Every non-late element has ts >= wm - size - lateness + 1.
+            return self.pane_of(self.wm - self.size - self.lateness + 1)
+        # No watermark yet: the global minimum timestamp (one MIN all-reduce, first steps only).
+        t = ts.min().reshape(1) if ts.numel() else torch.full((1,), I64_MAX, dtype=torch.int64,
+                                                                device=ts.device)
+        self.comm.allreduce_min_(t)
+        m = int(t.item())
+        base = self.pane_of(m) if m != I64_MAX else 0
+        if self.min_live_pane is not None:
+            base = min(base, self.min_live_pane)
+        return base
+
+    def _late_ts(self, wm: int) -> int:
+        """Smallest window start whose cleanup time (maxTs + lateness) is after `wm`."""
+        if wm == I64_MIN or self.time_mode != "event":
+            return I64_MIN
+        return self._align_up(wm - self.size - self.lateness + 2)
 
     def current_processing_time(self) -> int:
         import time
@@ -234,43 +245,37 @@ class KeyedWindowOperator:
             self._alloc_buckets(n, self.bucket_slack)
         old_wm = self.wm
         pane_base = self._pane_base(ts)
-        drop_late = self.time_mode == "event"
+        event_mode = self.time_mode == "event"
+        proc_now = 0 if event_mode else self.current_processing_time()
         while True:
-            self.cursor.zero_()
-            self.stats.copy_(self._stats_init)
+            K.step_begin(self.cursor, self.stats)
             plan = K.PartitionPlan(
                 max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2, nranks=self.world,
-                window_mode=1, drop_late=int(drop_late), hash_mode=self.hash_mode,
-                bucket_cap=self.bucket_cap, wm=old_wm, pane_base=pane_base, size=self.size,
-                slide=self.slide, offset=self.offset, pane=self.pane, lateness=self.lateness)
+                window_mode=1, drop_late=int(event_mode), hash_mode=self.hash_mode,
+                bucket_cap=self.bucket_cap, late_ts=self._late_ts(old_wm),
+                tbase=self.pane_start(pane_base), pane=self.pane)
             if n:
                 K.partition(keys, ts, vals, plan, self.kg_dest, self.cursor, self.send, self.stats,
                             jhash=self.jhash, late_idx=self.late_idx)
-            # Local watermark of this source partition (BoundedOutOfOrderness: max ts - bound).
-            torch.maximum(self.local_maxts, self.stats[K.STAT_MAXTS:K.STAT_MAXTS + 1],
-                           out=self.local_maxts)
-            if self.time_mode == "event":
-                wm_cand = torch.where(self.local_maxts == I64_MIN, self.local_maxts,
-                                      self.local_maxts - self.ooo_bound)
-            else:
-                wm_cand = torch.full((1,), self.current_processing_time(), dtype=torch.int64,
-                                     device=self.device)
-            red = torch.cat([-self.stats[K.STAT_MAXPANE:K.STAT_MAXPANE + 1].clamp(min=I64_MIN + 1),
-                             self.stats[K.STAT_MINPANE:K.STAT_MINPANE + 1], wm_cand,
-                             -self.stats[K.STAT_OVERFLOW:K.STAT_OVERFLOW + 1]])
-            self.comm.allreduce_min_(red)
+            K.step_finish(self.stats, self.local_maxts, self.red, bound=self.ooo_bound,
+                          event_mode=event_mode, proc_now=proc_now)
+            # Watermark valve + pane range + overflow flags: one MIN all-reduce.
+            self.comm.allreduce_min_(self.red[:5])
             if self.world > 1:
                 self.comm.all_to_all(self.recv, self.send)
                 self.comm.all_to_all(self.recv_counts, self.cursor)
-            host = torch.cat([red, self.stats]).cpu().tolist()  # the step's single host sync
-            if -host[3]:
+            host = self.red.cpu().tolist()  # the step's single host sync
+            if host[4]:
+                raise RuntimeError("event timestamp outside the representable pane range "
+                                   "(more than 2^32 panes ahead of the watermark)")
+            if host[3]:
                 # A bucket overflowed somewhere: grow the fixed bucket capacity and redo the step.
                 self.metrics.bucket_regrows += 1
                 self._alloc_buckets(self.batch_capacity, self.bucket_slack * 2)
                 continue
             break
-        gmax, gmin, wm_global = -host[0], host[1], host[2]
-        st = host[4:]
+        qmax, qmin, wm_global = -host[0], host[1], host[2]
+        st = host[8:]
         self.metrics.num_records_in += n
         self.metrics.num_late_records_dropped += int(st[K.STAT_LATE])
         if self.side_output_late and st[K.STAT_LATE]:
@@ -278,7 +283,8 @@ class KeyedWindowOperator:
             self.late_side.append(self.late_idx[:nl].cpu().numpy().copy())
 
         out: list[FireResult] = []
-        if gmin <= gmax:
+        if qmin <= qmax:
+            gmin, gmax = pane_base + qmin, pane_base + qmax
             lo = gmin if self.min_live_pane is None else min(self.min_live_pane, gmin)
             hi = gmax if self.max_seen_pane is None else max(self.max_seen_pane, gmax)
             if hi - lo + 1 > self.ring:
@@ -293,7 +299,7 @@ class KeyedWindowOperator:
             aplan = K.AggPlan(cap_log2=self.cap_log2, nsub=self.nsub, ring=self.ring, agg=self.agg,
                               nsrc=self.world, bucket_cap=self.bucket_cap,
                               np_step=gmax - gmin + 1, pg=pg, pane_base=pane_base,
-                              p_lo=gmin - pane_base, fired_hi=fired_hi)
+                              p_lo=qmin, fired_hi=fired_hi)
             K.window_agg(self.recv, self.recv_counts, aplan, self.keys_g, self.acc_g, self.cnt_g,
                          self.dirty_g, self.occ, self.flags)
             # Late-but-allowed data: re-fire already-passed windows that are not cleaned yet.

@@ -39,8 +39,8 @@ def test_partition_matches_cpu_as_multisets(gpu_device):
     for dev, (keys, ts, vals) in (("gpu", g), ("cpu", c)):
         d = keys.device
         plan = K.PartitionPlan(max_parallelism=128, nsub_log2=6, nranks=4, window_mode=1,
-                               drop_late=1, hash_mode=0, bucket_cap=2048, wm=3000, pane_base=0,
-                               size=1000, slide=500, offset=0, pane=500, lateness=100)
+                               drop_late=1, hash_mode=0, bucket_cap=2048, late_ts=3000,
+                               tbase=500, pane=500)
         kg = torch.tensor([(k * 4) // 128 for k in range(128)], dtype=torch.int32, device=d)
         cursor = torch.zeros(plan.nbuckets, dtype=torch.int32, device=d)
         out = torch.zeros(plan.nbuckets * plan.bucket_cap * 3, dtype=torch.int64, device=d)
