@@ -68,6 +68,7 @@ PartPlan make_part(py::dict d) {
   p.drop_late = d["drop_late"].cast<int32_t>();
   p.hash_mode = d["hash_mode"].cast<int32_t>();
   p.bucket_cap = d["bucket_cap"].cast<uint32_t>();
+  p.ablate = d.contains("ablate") ? d["ablate"].cast<uint32_t>() : 0u;
   p.late_ts = d["late_ts"].cast<int64_t>();
   p.tbase = d["tbase"].cast<int64_t>();
   p.pane = d["pane"].cast<int64_t>();
@@ -110,6 +111,7 @@ FirePlan make_fire(py::dict d) {
   p.wstart = d["wstart"].cast<double>();
   p.wend = d["wend"].cast<double>();
   p.out_cap = d["out_cap"].cast<uint32_t>();
+  p.ablate = d.contains("ablate") ? d["ablate"].cast<uint32_t>() : 0u;
   py::tuple m = d["map"].cast<py::tuple>();
   py::tuple f = d["filt"].cast<py::tuple>();
   p.map = make_prog(m[0].cast<std::vector<int32_t>>(), m[1].cast<std::vector<double>>());

@@ -129,44 +129,82 @@ __device__ __forceinline__ PartEval part_eval(uint64_t key, int64_t ts, const in
   return e;
 }
 
+// Block-wide reduction helpers (one global atomic per workgroup instead of one per wave).
+__device__ __forceinline__ int64_t block_reduce_i64(int64_t v, int64_t* red, int op) {
+  // op: 0 = max, 1 = min, 2 = sum. `red` = kMaxWaves int64 of LDS.
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t w = __shfl_xor(v, o);
+    v = op == 0 ? (v > w ? v : w) : op == 1 ? (v < w ? v : w) : v + w;
+  }
+  const int wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane_id() == 0) red[wid] = v;
+  __syncthreads();
+  v = red[0];
+  for (int i = 1; i < nw; ++i) {
+    const int64_t w = red[i];
+    v = op == 0 ? (v > w ? v : w) : op == 1 ? (v < w ? v : w) : v + w;
+  }
+  return v;
+}
+
+// ILP factor: each thread issues kPartU independent loads before it consumes any, so 16 waves
+// per CU keep ~16 x 64 x kPartU loads in flight (the loop was latency-bound at one chain).
+constexpr int kPartU = 8;
+
 __global__ __launch_bounds__(1024) void partition_kernel(
     const uint64_t* __restrict__ keys, const int64_t* __restrict__ ts,
     const uint64_t* __restrict__ vals, const int32_t* __restrict__ jhash_tab, int64_t n,
     int64_t chunk, PartPlan plan, const int32_t* __restrict__ kg_dest,
     uint32_t* __restrict__ cursor, Rec* __restrict__ out, int64_t* __restrict__ stats,
     uint32_t* __restrict__ late_idx, uint32_t late_cap) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lhist[];
+  extern __shared__ __attribute__((aligned(16))) uint32_t lhist[];  // nb u32 | 16 x i64 scratch
   const int nb = plan.nranks << plan.nsub_log2;
+  int64_t* lred = (int64_t*)(lhist + ((nb + 3) & ~3));
   for (int b = threadIdx.x; b < nb; b += blockDim.x) lhist[b] = 0;
   __syncthreads();
 
   const int64_t start = (int64_t)blockIdx.x * chunk;
   const int64_t end = start + chunk < n ? start + chunk : n;
+  const int64_t bstep = (int64_t)blockDim.x * kPartU;
   int64_t tmax = INT64_MIN, qmin = INT64_MAX, qmax = INT64_MIN, nlate = 0, nacc = 0;
   bool bad = false;
 
   // Pass A: histogram + stats.
-  for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
-    const uint64_t key = keys[i];
-    const int64_t t = ts[i];
-    tmax = t > tmax ? t : tmax;
-    const PartEval e = part_eval(key, t, jhash_tab, plan, kg_dest);
-    if (e.kind) {
-      if (e.kind == 2) {
-        bad = true;
+  for (int64_t i0 = start + threadIdx.x; i0 < end; i0 += bstep) {
+    uint64_t k[kPartU];
+    int64_t t[kPartU];
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i < end) {
+        k[u] = keys[i];
+        t[u] = ts[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i >= end) break;
+      tmax = t[u] > tmax ? t[u] : tmax;
+      const PartEval e = part_eval(k[u], t[u], jhash_tab, plan, kg_dest);
+      if (e.kind) {
+        if (e.kind == 2) {
+          bad = true;
+          continue;
+        }
+        ++nlate;
+        if (late_idx) {
+          const unsigned long long pos = atomicAdd((unsigned long long*)&stats[kStatLate], 1ull);
+          if (pos < late_cap) late_idx[pos] = (uint32_t)i;
+        }
         continue;
       }
-      ++nlate;
-      if (late_idx) {
-        const unsigned long long pos = atomicAdd((unsigned long long*)&stats[kStatLate], 1ull);
-        if (pos < late_cap) late_idx[pos] = (uint32_t)i;
-      }
-      continue;
+      ++nacc;
+      qmin = (int64_t)e.t < qmin ? (int64_t)e.t : qmin;
+      qmax = (int64_t)e.t > qmax ? (int64_t)e.t : qmax;
+      atomicAdd(&lhist[e.bucket], 1u);
     }
-    ++nacc;
-    qmin = (int64_t)e.t < qmin ? (int64_t)e.t : qmin;
-    qmax = (int64_t)e.t > qmax ? (int64_t)e.t : qmax;
-    atomicAdd(&lhist[e.bucket], 1u);
   }
   __syncthreads();
 
@@ -185,30 +223,45 @@ __global__ __launch_bounds__(1024) void partition_kernel(
 
   // Pass B: scatter records into their bucket runs.
   const uint32_t bcap = plan.bucket_cap;
-  for (int64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
-    const uint64_t key = keys[i];
-    const PartEval e = part_eval(key, ts[i], jhash_tab, plan, kg_dest);
-    if (e.kind) continue;
-    const uint32_t pos = atomicAdd(&lhist[e.bucket], 1u);
-    if (pos < bcap) {
-      Rec r;
-      r.key = key;
-      r.val = vals[i];
-      r.t = e.t;
-      r.aux = (uint32_t)i;
-      out[(size_t)e.bucket * bcap + pos] = r;
+  for (int64_t i0 = start + threadIdx.x; i0 < end; i0 += bstep) {
+    uint64_t k[kPartU], v[kPartU];
+    int64_t t[kPartU];
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i < end) {
+        k[u] = keys[i];
+        t[u] = ts[i];
+        v[u] = vals[i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i >= end) break;
+      const PartEval e = part_eval(k[u], t[u], jhash_tab, plan, kg_dest);
+      if (e.kind) continue;
+      const uint32_t pos = atomicAdd(&lhist[e.bucket], 1u);
+      if (pos < bcap && !(plan.ablate & 1u)) {
+        Rec r;
+        r.key = k[u];
+        r.val = v[u];
+        r.t = e.t;
+        r.aux = (uint32_t)i;
+        out[(size_t)e.bucket * bcap + pos] = r;
+      }
     }
   }
 
-  // Block stats -> one atomic per wave.
-  tmax = wave_max_i64(tmax);
-  qmin = wave_min_i64(qmin);
-  qmax = wave_max_i64(qmax);
-  nacc = wave_sum_i64(nacc);
-  if (!late_idx) nlate = wave_sum_i64(nlate);
-  const unsigned long long ovf = __ballot(overflow);
-  const unsigned long long badm = __ballot(bad);
-  if (lane_id() == 0) {
+  // Block stats -> one global atomic per workgroup and statistic.
+  tmax = block_reduce_i64(tmax, lred, 0);
+  qmin = block_reduce_i64(qmin, lred, 1);
+  qmax = block_reduce_i64(qmax, lred, 0);
+  nacc = block_reduce_i64(nacc, lred, 2);
+  if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
+  const int64_t flags = block_reduce_i64(overflow ? 1 : 0, lred, 0) |
+                        (block_reduce_i64(bad ? 2 : 0, lred, 0));
+  if (threadIdx.x == 0) {
     atomicMax((long long*)&stats[kStatMaxTs], (long long)tmax);
     if (nacc) {
       atomicMin((long long*)&stats[kStatMinPane], (long long)qmin);
@@ -216,8 +269,7 @@ __global__ __launch_bounds__(1024) void partition_kernel(
       atomicAdd((unsigned long long*)&stats[kStatAccepted], (unsigned long long)nacc);
     }
     if (!late_idx && nlate) atomicAdd((unsigned long long*)&stats[kStatLate], (unsigned long long)nlate);
-    if (ovf) atomicOr((unsigned long long*)&stats[kStatOverflow], 1ull);
-    if (badm) atomicOr((unsigned long long*)&stats[kStatOverflow], 2ull);
+    if (flags) atomicOr((unsigned long long*)&stats[kStatOverflow], (unsigned long long)flags);
   }
 }
 
@@ -315,6 +367,8 @@ __device__ __forceinline__ uint64_t lds_export(uint64_t a) {
 // Keyed window aggregation: one workgroup per sub-table.
 // LDS image (dynamic, 16-B aligned): keys[cap] u64 | acc[pg][cap] u64 | cnt[pg][cap] u32 | flag
 // ------------------------------------------------------------------------------------------
+constexpr int kAggU = 4;
+
 template <int AGG>
 __global__ __launch_bounds__(1024) void window_agg_kernel(
     const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
@@ -348,18 +402,30 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
       uint32_t c = counts[(size_t)src * p.nsub + sub];
       c = c < p.bucket_cap ? c : p.bucket_cap;
       const Rec* seg = recs + ((size_t)src * p.nsub + sub) * p.bucket_cap;
-      for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
-        const Rec r = seg[e];
-        const int64_t q = (int64_t)r.t - q0;
-        if (q < 0 || q >= npg) continue;
-        const uint32_t s = lds_probe_insert(skeys, r.key, mask, &inserted);
-        if (s == kNoSlot) {
-          ovf = true;
-          continue;
+      // kAggU independent record loads in flight per thread before the LDS work.
+      for (uint32_t e0 = threadIdx.x; e0 < c; e0 += blockDim.x * kAggU) {
+        Rec rr[kAggU];
+#pragma unroll
+        for (int u = 0; u < kAggU; ++u) {
+          const uint32_t e = e0 + u * blockDim.x;
+          if (e < c) rr[u] = seg[e];
         }
-        const uint32_t li = (uint32_t)q * cap + s;
-        lds_accumulate<AGG>(&sacc[li], r.val);
-        atomicAdd(&scnt[li], 1u);
+#pragma unroll
+        for (int u = 0; u < kAggU; ++u) {
+          const uint32_t e = e0 + u * blockDim.x;
+          if (e >= c) break;
+          const Rec& r = rr[u];
+          const int64_t q = (int64_t)r.t - q0;
+          if (q < 0 || q >= npg) continue;
+          const uint32_t s = lds_probe_insert(skeys, r.key, mask, &inserted);
+          if (s == kNoSlot) {
+            ovf = true;
+            continue;
+          }
+          const uint32_t li = (uint32_t)q * cap + s;
+          lds_accumulate<AGG>(&sacc[li], r.val);
+          atomicAdd(&scnt[li], 1u);
+        }
       }
     }
     __syncthreads();
@@ -402,73 +468,112 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
 // ------------------------------------------------------------------------------------------
 struct LdsCol {
   double* base;
-  __device__ __forceinline__ double get(int i) const { return base[i * 256]; }
-  __device__ __forceinline__ void set(int i, double x) { base[i * 256] = x; }
+  int stride;
+  __device__ __forceinline__ double get(int i) const { return base[i * stride]; }
+  __device__ __forceinline__ void set(int i, double x) { base[i * stride] = x; }
 };
 
-__global__ __launch_bounds__(256) void window_fire_kernel(
+constexpr int kFireThreads = 1024;
+constexpr int kFireU = 4;  // slots per thread per round (ILP)
+
+__global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
     const uint64_t* __restrict__ keys_g, const uint64_t* __restrict__ acc_g,
     const uint32_t* __restrict__ cnt_g, const uint8_t* __restrict__ dirty_g, FirePlan p,
     uint64_t* __restrict__ out_keys, double* __restrict__ out_vals, uint64_t* __restrict__ out_raw,
     uint32_t* __restrict__ out_cnt, uint32_t* __restrict__ out_n) {
-  extern __shared__ __attribute__((aligned(16))) double fsm[];  // [kExprVars + depth][256]
-  LdsCol vars{fsm + threadIdx.x};
-  LdsCol stack{fsm + kExprVars * 256 + threadIdx.x};
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // LDS: [kExprVars + depth][kFireThreads] f64 VM columns | 16 wave counts | block base
+  extern __shared__ __attribute__((aligned(16))) double fsm[];
+  LdsCol vars{fsm + threadIdx.x, kFireThreads};
+  LdsCol stack{fsm + kExprVars * kFireThreads + threadIdx.x, kFireThreads};
+  const int depth = p.map.depth > p.filt.depth ? p.map.depth : p.filt.depth;
+  uint32_t* wcnt = (uint32_t*)(fsm + (size_t)(kExprVars + depth) * kFireThreads);
+  const int wid = threadIdx.x >> 6, nw = kFireThreads >> 6;
   const int64_t nslots = p.nslots;
-  // Uniform trip count so every lane reaches the ballot.
-  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < nslots; base += stride) {
-    const int64_t s = base + threadIdx.x;
-    bool emit = false;
-    uint64_t acc = 0, key = 0;
-    uint32_t cnt = 0;
-    double val = 0.0;
-    if (s < nslots) {
-      bool dirty = !p.only_dirty;
-      bool have = false;
-      for (int j = 0; j < p.npanes; ++j) {
-        const size_t gi = (size_t)((p.p0 + j) & (p.ring - 1)) * nslots + s;
-        const uint32_t c = cnt_g[gi];
-        if (c) {
-          const uint64_t a = acc_g[gi];
-          acc = have ? agg_combine(p.agg, acc, a) : a;
-          have = true;
-          cnt += c;
-          if (p.only_dirty && dirty_g[gi]) dirty = true;
+  const int64_t per_round = (int64_t)kFireThreads * kFireU;
+  // Rounds are block-uniform, so every lane reaches the barriers and the ballots.
+  for (int64_t base = (int64_t)blockIdx.x * per_round; base < nslots;
+       base += (int64_t)gridDim.x * per_round) {
+    bool emit[kFireU];
+    uint64_t acc[kFireU], key[kFireU];
+    uint32_t cnt[kFireU];
+    double val[kFireU];
+#pragma unroll
+    for (int u = 0; u < kFireU; ++u) {
+      const int64_t s = base + (int64_t)u * kFireThreads + threadIdx.x;
+      emit[u] = false;
+      acc[u] = 0;
+      key[u] = 0;
+      cnt[u] = 0;
+      val[u] = 0.0;
+      if (s < nslots) {
+        bool dirty = !p.only_dirty;
+        bool have = false;
+        for (int j = 0; j < p.npanes; ++j) {
+          const size_t gi = (size_t)((p.p0 + j) & (p.ring - 1)) * nslots + s;
+          const uint32_t c = cnt_g[gi];
+          if (c) {
+            const uint64_t a = acc_g[gi];
+            acc[u] = have ? agg_combine(p.agg, acc[u], a) : a;
+            have = true;
+            cnt[u] += c;
+            if (p.only_dirty && dirty_g[gi]) dirty = true;
+          }
         }
-      }
-      if (cnt && dirty) {
-        key = keys_g[s];
-        const double v0 = agg_result_f64(p.agg, acc, cnt);
-        val = v0;
-        emit = true;
-        if (p.map.ncode || p.filt.ncode) {
-          vars.set(0, v0);
-          vars.set(1, (double)cnt);
-          vars.set(2, p.wstart);
-          vars.set(3, p.wend);
-          vars.set(4, (double)key);
-          vars.set(5, (double)(int64_t)acc);
-          if (p.map.ncode) val = expr_eval_t(p.map, stack, vars);
-          vars.set(6, val);
-          if (p.filt.ncode) emit = expr_eval_t(p.filt, stack, vars) != 0.0;
+        if (cnt[u] && dirty) {
+          key[u] = keys_g[s];
+          const double v0 = agg_result_f64(p.agg, acc[u], cnt[u]);
+          val[u] = v0;
+          emit[u] = true;
+          if ((p.map.ncode || p.filt.ncode) && !(p.ablate & 1u)) {
+            vars.set(0, v0);
+            vars.set(1, (double)cnt[u]);
+            vars.set(2, p.wstart);
+            vars.set(3, p.wend);
+            vars.set(4, (double)key[u]);
+            vars.set(5, (double)(int64_t)acc[u]);
+            if (p.map.ncode) val[u] = expr_eval_t(p.map, stack, vars);
+            vars.set(6, val[u]);
+            if (p.filt.ncode) emit[u] = expr_eval_t(p.filt, stack, vars) != 0.0;
+          }
         }
       }
     }
-    const unsigned long long m = __ballot(emit);
-    if (m) {
-      uint32_t wbase = 0;
-      if (lane_id() == 0) wbase = atomicAdd(out_n, (uint32_t)__popcll(m));
-      wbase = __shfl(wbase, 0);
-      if (emit) {
-        const uint32_t pos = wbase + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
-        if (pos < p.out_cap) {
-          out_keys[pos] = key;
-          out_vals[pos] = val;
-          out_raw[pos] = acc;
-          out_cnt[pos] = cnt;
+    // Block-level compaction: wave ballots -> LDS prefix over waves -> ONE global atomic per
+    // round of 4096 slots (a per-wave atomic on one counter serialises ~65K times at 4M slots).
+    uint32_t mine = 0;
+    unsigned long long masks[kFireU];
+#pragma unroll
+    for (int u = 0; u < kFireU; ++u) {
+      masks[u] = __ballot(emit[u]);
+      mine += (uint32_t)__popcll(masks[u]);
+    }
+    __syncthreads();
+    if (lane_id() == 0) wcnt[wid] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t tot = 0;
+      for (int w = 0; w < nw; ++w) {
+        const uint32_t c = wcnt[w];
+        wcnt[w] = tot;
+        tot += c;
+      }
+      wcnt[nw] = tot ? atomicAdd(out_n, tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t pos = wcnt[nw] + wcnt[wid];
+    const unsigned long long lt = (1ull << lane_id()) - 1ull;
+#pragma unroll
+    for (int u = 0; u < kFireU; ++u) {
+      if (emit[u]) {
+        const uint32_t q = pos + (uint32_t)__popcll(masks[u] & lt);
+        if (q < p.out_cap) {
+          out_keys[q] = key[u];
+          out_vals[q] = val[u];
+          out_raw[q] = acc[u];
+          out_cnt[q] = cnt[u];
         }
       }
+      pos += (uint32_t)__popcll(masks[u]);
     }
   }
 }
@@ -477,8 +582,8 @@ __global__ __launch_bounds__(256) void window_fire_kernel(
 __global__ __launch_bounds__(256) void expr_filter_kernel(const double* __restrict__ x, int64_t n,
                                                           ExprProg prog, uint8_t* __restrict__ keep) {
   extern __shared__ __attribute__((aligned(16))) double fsm[];
-  LdsCol vars{fsm + threadIdx.x};
-  LdsCol stack{fsm + kExprVars * 256 + threadIdx.x};
+  LdsCol vars{fsm + threadIdx.x, 256};
+  LdsCol stack{fsm + kExprVars * 256 + threadIdx.x, 256};
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     vars.set(0, x[i]);
@@ -544,7 +649,7 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
     attr = true;
   }
-  hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(1024), (size_t)nb * 4,
+  hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(1024), (size_t)((nb + 3) & ~3) * 4 + 16 * 8,
                      (hipStream_t)stream, keys, ts, vals, jhash_tab, n, chunk, plan, kg_dest,
                      cursor, out, stats, late_idx, late_cap);
   HIP_CHECK(hipGetLastError());
@@ -598,10 +703,17 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
                  double* out_vals, uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n,
                  intptr_t stream) {
   if (plan.nslots <= 0) return;
-  const size_t lds = (size_t)(kExprVars + (plan.map.depth > plan.filt.depth ? plan.map.depth
-                                                                             : plan.filt.depth)) *
-                     256 * sizeof(double);
-  hipLaunchKernelGGL(window_fire_kernel, dim3(grid_for(plan.nslots, 256, 4096)), dim3(256), lds,
+  const int depth = plan.map.depth > plan.filt.depth ? plan.map.depth : plan.filt.depth;
+  const size_t lds = (size_t)(kExprVars + depth) * kFireThreads * sizeof(double) + 17 * 4;
+  if (lds > 160 * 1024) throw std::runtime_error("window_fire: epilogue stack too deep for LDS");
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)window_fire_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL(window_fire_kernel, dim3(grid_for(plan.nslots, kFireThreads * kFireU, 1024)),
+                     dim3(kFireThreads), lds,
                      (hipStream_t)stream, keys_g, acc_g, cnt_g, dirty_g, plan, out_keys, out_vals,
                      out_raw, out_cnt, out_n);
   HIP_CHECK(hipGetLastError());

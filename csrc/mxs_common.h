@@ -341,7 +341,7 @@ struct PartPlan {
   int32_t drop_late;         // 1: elements with ts < late_ts are dropped (and optionally side-output)
   int32_t hash_mode;         // 0: Long.hashCode(key); 1: jhash table lookup (string dict ids)
   uint32_t bucket_cap;       // fixed capacity of one (dest, sub) bucket in the send buffer
-  uint32_t pad0;
+  uint32_t ablate;           // profiling-only ablation bits (0 in production): 1 = skip scatter stores
   // ts < late_ts  <=>  every window of the element is past cleanup (maxTs + lateness <= wm):
   // late_ts is the smallest window start whose cleanup time is still ahead of the watermark.
   int64_t late_ts;

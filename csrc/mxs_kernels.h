@@ -37,7 +37,7 @@ struct FirePlan {
   int64_t p0;           // first absolute pane of the window
   double wstart, wend;  // window bounds (ms) for the epilogue vars
   uint32_t out_cap;
-  uint32_t pad;
+  uint32_t ablate;      // profiling-only ablation bits (0 in production): 1 = skip the epilogue VM
   ExprProg map;         // value epilogue (empty = identity)
   ExprProg filt;        // predicate on the mapped value (empty = true)
 };

@@ -96,6 +96,7 @@ class PartitionPlan:
     late_ts: int = I64_MIN   # elements with ts < late_ts are late (all windows cleaned)
     tbase: int = 0           # start of the step's base pane
     pane: int = 1            # pane length (ms)
+    ablate: int = 0          # profiling-only ablation bits
 
     @property
     def nbuckets(self) -> int:
@@ -179,7 +180,8 @@ def window_agg(recs, counts, plan: AggPlan, keys_g, acc_g, cnt_g, dirty_g, occ, 
 
 def window_fire(keys_g, acc_g, cnt_g, dirty_g, *, agg: int, npanes: int, ring: int, p0: int,
                 wstart: int, wend: int, only_dirty: bool, map_prog: _expr.Program,
-                filt_prog: _expr.Program, out_keys, out_vals, out_raw, out_cnt, out_n) -> None:
+                filt_prog: _expr.Program, out_keys, out_vals, out_raw, out_cnt, out_n,
+                ablate: int = 0) -> None:
     dev = keys_g.device
     nslots = keys_g.numel()
     cap = out_keys.numel()
@@ -194,7 +196,7 @@ def window_fire(keys_g, acc_g, cnt_g, dirty_g, *, agg: int, npanes: int, ring: i
         raise ValueError("window spans more panes than the ring")
     plan = dict(agg=agg, npanes=npanes, ring=ring, only_dirty=int(only_dirty), nslots=nslots,
                 p0=p0, wstart=float(wstart), wend=float(wend), out_cap=cap,
-                map=tuple(map_prog.as_args()), filt=tuple(filt_prog.as_args()))
+                map=tuple(map_prog.as_args()), filt=tuple(filt_prog.as_args()), ablate=ablate)
     m = load()
     args = (_p(keys_g), _p(acc_g), _p(cnt_g), _p(dirty_g), plan, _p(out_keys), _p(out_vals),
             _p(out_raw), _p(out_cnt), _p(out_n))
