@@ -171,6 +171,13 @@ PYBIND11_MODULE(_mxs_native, m) {
                    make_part(plan), P<int32_t>(kg_dest), P<uint32_t>(cursor), P<Rec>(out),
                    P<int64_t>(stats), P<uint32_t>(late_idx), late_cap, stream);
   });
+  m.def("gpu_partition_variant", [](intptr_t keys, intptr_t ts, intptr_t vals, intptr_t jhash,
+                                    int64_t n, py::dict plan, intptr_t kg_dest, intptr_t cursor,
+                                    intptr_t out, intptr_t stats, intptr_t stream, int variant) {
+    gpu::partition_variant(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), P<int32_t>(jhash),
+                           n, make_part(plan), P<int32_t>(kg_dest), P<uint32_t>(cursor),
+                           P<Rec>(out), P<int64_t>(stats), nullptr, 0, stream, variant);
+  });
   m.def("gpu_window_agg", [](intptr_t recs, intptr_t counts, py::dict plan, intptr_t keys_g,
                              intptr_t acc_g, intptr_t cnt_g, intptr_t dirty_g, intptr_t occ,
                              intptr_t flags, intptr_t stream) {

@@ -39,6 +39,9 @@ namespace {
   } while (0)
 
 constexpr int kWave = 64;
+// Partition variants (scripts/kbench.py A/B, profiles/): 0 plain scatter, 1 + non-temporal
+// input loads, 2/3 + non-temporal stores (3x slower: rejected), 4/5 staged write-combined
+// scatter (5 = with non-temporal loads; production when nb <= 512).
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 
@@ -152,6 +155,14 @@ __device__ __forceinline__ int64_t block_reduce_i64(int64_t v, int64_t* red, int
 // per CU keep ~16 x 64 x kPartU loads in flight (the loop was latency-bound at one chain).
 constexpr int kPartU = 8;
 
+// Input-stream loads: V&1 = non-temporal (streamed once; keep L2 for the scatter's open lines).
+template <int V, class T>
+__device__ __forceinline__ T ldin(const T* p) {
+  if (V & 1) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
+template <int V>
 __global__ __launch_bounds__(1024) void partition_kernel(
     const uint64_t* __restrict__ keys, const int64_t* __restrict__ ts,
     const uint64_t* __restrict__ vals, const int32_t* __restrict__ jhash_tab, int64_t n,
@@ -178,8 +189,8 @@ __global__ __launch_bounds__(1024) void partition_kernel(
     for (int u = 0; u < kPartU; ++u) {
       const int64_t i = i0 + (int64_t)u * blockDim.x;
       if (i < end) {
-        k[u] = keys[i];
-        t[u] = ts[i];
+        k[u] = ldin<V>(&keys[i]);
+        t[u] = ldin<V>(&ts[i]);
       }
     }
 #pragma unroll
@@ -230,9 +241,9 @@ __global__ __launch_bounds__(1024) void partition_kernel(
     for (int u = 0; u < kPartU; ++u) {
       const int64_t i = i0 + (int64_t)u * blockDim.x;
       if (i < end) {
-        k[u] = keys[i];
-        t[u] = ts[i];
-        v[u] = vals[i];
+        k[u] = ldin<V>(&keys[i]);
+        t[u] = ldin<V>(&ts[i]);
+        v[u] = ldin<V>(&vals[i]);
       }
     }
 #pragma unroll
@@ -243,12 +254,19 @@ __global__ __launch_bounds__(1024) void partition_kernel(
       if (e.kind) continue;
       const uint32_t pos = atomicAdd(&lhist[e.bucket], 1u);
       if (pos < bcap && !(plan.ablate & 1u)) {
-        Rec r;
-        r.key = k[u];
-        r.val = v[u];
-        r.t = e.t;
-        r.aux = (uint32_t)i;
-        out[(size_t)e.bucket * bcap + pos] = r;
+        Rec* dst = &out[(size_t)e.bucket * bcap + pos];
+        if (V & 2) {
+          __builtin_nontemporal_store(k[u], &dst->key);
+          __builtin_nontemporal_store(v[u], &dst->val);
+          __builtin_nontemporal_store(((uint64_t)(uint32_t)i << 32) | e.t, (uint64_t*)&dst->t);
+        } else {
+          Rec r;
+          r.key = k[u];
+          r.val = v[u];
+          r.t = e.t;
+          r.aux = (uint32_t)i;
+          *dst = r;
+        }
       }
     }
   }
@@ -272,6 +290,270 @@ __global__ __launch_bounds__(1024) void partition_kernel(
     if (flags) atomicOr((unsigned long long*)&stats[kStatOverflow], (unsigned long long)flags);
   }
 }
+
+// ------------------------------------------------------------------------------------------
+// Staged partition (nb <= 512): write-combined scatter.
+//
+// The plain scatter writes 24-byte records into nb open runs per workgroup; on gfx950 the
+// partially written 128-B lines are evicted by the input stream long before they fill
+// (measured: 4.6x HBM write amplification). Here every round of kStageR records is counting-
+// sorted by bucket in LDS; each bucket keeps its partial tail group (< 8 records) in an LDS
+// carry buffer and only complete 8-record groups (192 B = three aligned 64-B sectors) are
+// written. Per-workgroup runs are reserved in multiples of 8 and the final partial group is
+// padded with hole records (t = kHoleT), which window_agg skips.
+// ------------------------------------------------------------------------------------------
+constexpr int kStageU = 2;                  // events per thread per round
+constexpr int kStageR = 1024 * kStageU;     // records per round
+constexpr int kStageMaxNb = 512;
+constexpr uint32_t kHoleT = 0xFFFFFFFFu;
+
+__device__ __forceinline__ void lds_store_rec(Rec* dst, const Rec& r) {
+  uint64_t* d = (uint64_t*)dst;
+  d[0] = r.key;
+  d[1] = r.val;
+  d[2] = ((uint64_t)r.aux << 32) | r.t;
+}
+
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* wsum) {
+  // 1024-thread exclusive scan; wsum = 17 u32 of LDS. Returns this thread's exclusive prefix.
+  const int lane = lane_id(), wid = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (int w = 0; w < 16; ++w) {
+      const uint32_t t = wsum[w];
+      wsum[w] = acc;
+      acc += t;
+    }
+    wsum[16] = acc;
+  }
+  __syncthreads();
+  return wsum[wid] + x - v;
+}
+
+template <int V>
+__global__ __launch_bounds__(1024) void partition_staged_kernel(
+    const uint64_t* __restrict__ keys, const int64_t* __restrict__ ts,
+    const uint64_t* __restrict__ vals, const int32_t* __restrict__ jhash_tab, int64_t n,
+    int64_t chunk, PartPlan plan, const int32_t* __restrict__ kg_dest,
+    uint32_t* __restrict__ cursor, Rec* __restrict__ out, int64_t* __restrict__ stats,
+    uint32_t* __restrict__ late_idx, uint32_t late_cap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char psm[];
+  const int nb = plan.nranks << plan.nsub_log2;
+  Rec* carry = (Rec*)psm;                                   // [kStageMaxNb][8]
+  Rec* rbuf = carry + kStageMaxNb * 8;                      // [kStageR]
+  uint32_t* run_base = (uint32_t*)(rbuf + kStageR);          // [kStageMaxNb]
+  uint32_t* lcnt = run_base + kStageMaxNb;                   // records appended per bucket
+  uint32_t* rcnt = lcnt + kStageMaxNb;                       // this round's count per bucket
+  uint32_t* roff = rcnt + kStageMaxNb;                       // this round's offsets
+  uint32_t* wsum = roff + kStageMaxNb;                       // 17 scan words (+pad)
+  int64_t* lred = (int64_t*)(wsum + 20);                     // 16 x i64
+
+  for (int b = threadIdx.x; b < kStageMaxNb; b += blockDim.x) {
+    run_base[b] = 0;
+    lcnt[b] = 0;
+    rcnt[b] = 0;
+  }
+  __syncthreads();
+
+  const int64_t start = (int64_t)blockIdx.x * chunk;
+  const int64_t end = start + chunk < n ? start + chunk : n;
+  int64_t tmax = INT64_MIN, qmin = INT64_MAX, qmax = INT64_MIN, nlate = 0, nacc = 0;
+  bool bad = false;
+
+  // Pass A: histogram (into run_base) + stats.
+  for (int64_t i0 = start + threadIdx.x; i0 < end; i0 += (int64_t)blockDim.x * kPartU) {
+    uint64_t k[kPartU];
+    int64_t t[kPartU];
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i < end) {
+        k[u] = ldin<V>(&keys[i]);
+        t[u] = ldin<V>(&ts[i]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i >= end) break;
+      tmax = t[u] > tmax ? t[u] : tmax;
+      const PartEval e = part_eval(k[u], t[u], jhash_tab, plan, kg_dest);
+      if (e.kind) {
+        if (e.kind == 2) {
+          bad = true;
+          continue;
+        }
+        ++nlate;
+        if (late_idx) {
+          const unsigned long long pos = atomicAdd((unsigned long long*)&stats[kStatLate], 1ull);
+          if (pos < late_cap) late_idx[pos] = (uint32_t)i;
+        }
+        continue;
+      }
+      ++nacc;
+      qmin = (int64_t)e.t < qmin ? (int64_t)e.t : qmin;
+      qmax = (int64_t)e.t > qmax ? (int64_t)e.t : qmax;
+      atomicAdd(&run_base[e.bucket], 1u);
+    }
+  }
+  __syncthreads();
+
+  // Reserve this workgroup's run per bucket, rounded up to whole 8-record groups so every
+  // group written below covers aligned 64-B sectors (bucket_cap is a multiple of 8).
+  bool overflow = false;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    const uint32_t c = (run_base[b] + 7u) & ~7u;
+    uint32_t base = 0;
+    if (c) {
+      base = atomicAdd(&cursor[b], c);
+      if (base + c > plan.bucket_cap) overflow = true;
+    }
+    run_base[b] = base;
+  }
+  const uint32_t bcap = plan.bucket_cap;
+  if (threadIdx.x == 0) wsum[18] = 0;
+  __syncthreads();
+  if (overflow) wsum[18] = 1;
+  __syncthreads();
+  const bool any_ovf = wsum[18] != 0;
+
+  // Pass B: rounds of kStageR records -> LDS sort by bucket -> whole-group writes.
+  for (int64_t r0 = start; r0 < end; r0 += kStageR) {
+    uint32_t bk[kStageU], rk[kStageU];
+    Rec rec[kStageU];
+    bool keep[kStageU];
+#pragma unroll
+    for (int u = 0; u < kStageU; ++u) {
+      const int64_t i = r0 + (int64_t)u * blockDim.x + threadIdx.x;
+      keep[u] = false;
+      if (i < end) {
+        const uint64_t k = ldin<V>(&keys[i]);
+        const int64_t t = ldin<V>(&ts[i]);
+        const uint64_t v = ldin<V>(&vals[i]);
+        const PartEval e = part_eval(k, t, jhash_tab, plan, kg_dest);
+        if (!e.kind) {
+          keep[u] = true;
+          bk[u] = e.bucket;
+          rec[u].key = k;
+          rec[u].val = v;
+          rec[u].t = e.t;
+          rec[u].aux = (uint32_t)i;
+          rk[u] = atomicAdd(&rcnt[e.bucket], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t myc = threadIdx.x < (unsigned)nb ? rcnt[threadIdx.x] : 0u;
+    const uint32_t off = block_exclusive_scan(myc, wsum);
+    if (threadIdx.x < (unsigned)nb) roff[threadIdx.x] = off;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kStageU; ++u)
+      if (keep[u]) lds_store_rec(&rbuf[roff[bk[u]] + rk[u]], rec[u]);
+    __syncthreads();
+    // Flush: one thread per bucket writes its complete groups (carry first, then this round).
+    if (threadIdx.x < (unsigned)nb && !any_ovf) {
+      const int b = threadIdx.x;
+      const uint32_t nc = lcnt[b] & 7u;      // records waiting in carry[b]
+      const uint32_t nr = rcnt[b];
+      const uint32_t tot = nc + nr;
+      const uint32_t groups = tot >> 3;
+      const uint32_t first = lcnt[b] - nc;   // run offset of carry[b][0]
+      Rec* dstb = out + (size_t)b * bcap + run_base[b] + first;
+      const Rec* src_r = rbuf + roff[b];
+      for (uint32_t g = 0; g < groups; ++g) {
+        uint4* d = (uint4*)(dstb + g * 8);   // 192 B = 12 x 16 B
+#pragma unroll
+        for (int q = 0; q < 12; ++q) {
+          // 16-B chunk q of the group: records are 24 B, chunk spans record idx = q*16/24.
+          const uint32_t byte = q * 16;
+          const uint32_t j = g * 8 + byte / 24;  // record index within (carry ++ round)
+          const uint32_t ob = byte % 24;         // 0, 16 or 8
+          const Rec* ra = j < nc ? &carry[b * 8 + j] : &src_r[j - nc];
+          const uint64_t* rw = (const uint64_t*)ra;
+          uint4 v;
+          if (ob == 0) {
+            v = make_uint4((uint32_t)rw[0], (uint32_t)(rw[0] >> 32), (uint32_t)rw[1], (uint32_t)(rw[1] >> 32));
+          } else if (ob == 16) {
+            const uint32_t j2 = j + 1;
+            const Rec* rb = j2 < nc ? &carry[b * 8 + j2] : &src_r[j2 - nc];
+            const uint64_t* rw2 = (const uint64_t*)rb;
+            v = make_uint4((uint32_t)rw[2], (uint32_t)(rw[2] >> 32), (uint32_t)rw2[0], (uint32_t)(rw2[0] >> 32));
+          } else {  // ob == 8
+            v = make_uint4((uint32_t)rw[1], (uint32_t)(rw[1] >> 32), (uint32_t)rw[2], (uint32_t)(rw[2] >> 32));
+          }
+          d[q] = v;
+        }
+      }
+      // Keep the remainder (< 8 records) in the carry buffer. When no group was written the
+      // carried records stay in place; otherwise every remaining record comes from rbuf, so
+      // the copy never reads a carry slot it has already overwritten.
+      const uint32_t rem = tot - groups * 8;
+      for (uint32_t j = 0; j < rem; ++j) {
+        const uint32_t jj = groups * 8 + j;
+        if (jj < nc) continue;  // groups == 0: already at carry[b * 8 + jj] with jj == j
+        const uint64_t* rw = (const uint64_t*)&src_r[jj - nc];
+        uint64_t* cw = (uint64_t*)&carry[b * 8 + j];
+        cw[0] = rw[0];
+        cw[1] = rw[1];
+        cw[2] = rw[2];
+      }
+      lcnt[b] += nr;
+      rcnt[b] = 0;
+    }
+    __syncthreads();
+  }
+  // Final partial groups, padded with holes.
+  if (threadIdx.x < (unsigned)nb && !any_ovf) {
+    const int b = threadIdx.x;
+    const uint32_t nc = lcnt[b] & 7u;
+    if (nc) {
+      Rec* dst = out + (size_t)b * bcap + run_base[b] + (lcnt[b] - nc);
+      for (uint32_t j = 0; j < 8; ++j) {
+        Rec r;
+        if (j < nc) {
+          r = carry[b * 8 + j];
+        } else {
+          r.key = kEmptyKey;
+          r.val = 0;
+          r.t = kHoleT;
+          r.aux = kHoleT;
+        }
+        dst[j] = r;
+      }
+    }
+  }
+
+  // Block stats -> one global atomic per workgroup and statistic.
+  tmax = block_reduce_i64(tmax, lred, 0);
+  qmin = block_reduce_i64(qmin, lred, 1);
+  qmax = block_reduce_i64(qmax, lred, 0);
+  nacc = block_reduce_i64(nacc, lred, 2);
+  if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
+  const int64_t flags = (any_ovf ? 1 : 0) | block_reduce_i64(bad ? 2 : 0, lred, 0);
+  if (threadIdx.x == 0) {
+    atomicMax((long long*)&stats[kStatMaxTs], (long long)tmax);
+    if (nacc) {
+      atomicMin((long long*)&stats[kStatMinPane], (long long)qmin);
+      atomicMax((long long*)&stats[kStatMaxPane], (long long)qmax);
+      atomicAdd((unsigned long long*)&stats[kStatAccepted], (unsigned long long)nacc);
+    }
+    if (!late_idx && nlate) atomicAdd((unsigned long long*)&stats[kStatLate], (unsigned long long)nlate);
+    if (flags) atomicOr((unsigned long long*)&stats[kStatOverflow], (unsigned long long)flags);
+  }
+}
+
+constexpr size_t kStagedLds = (size_t)kStageMaxNb * 8 * sizeof(Rec) + (size_t)kStageR * sizeof(Rec) +
+                              (size_t)kStageMaxNb * 4 * 4 + 20 * 4 + 16 * 8;
+static_assert(kStagedLds <= 160 * 1024, "staged partition LDS image exceeds 160 KiB");
 
 // Step prologue: zero the bucket cursors and reset the stats block (one launch instead of two
 // memsets + a host copy).
@@ -415,6 +697,7 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
           const uint32_t e = e0 + u * blockDim.x;
           if (e >= c) break;
           const Rec& r = rr[u];
+          if (r.t == 0xFFFFFFFFu) continue;  // hole record (staged partition padding)
           const int64_t q = (int64_t)r.t - q0;
           if (q < 0 || q >= npg) continue;
           const uint32_t s = lds_probe_insert(skeys, r.key, mask, &inserted);
@@ -636,6 +919,17 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                const int32_t* jhash_tab, int64_t n, const PartPlan& plan, const int32_t* kg_dest,
                uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap,
                intptr_t stream) {
+  const int nb = plan.nranks << plan.nsub_log2;
+  // Write-combined staged scatter when the LDS carry buffers fit (<= 512 buckets); otherwise
+  // the plain scatter. Both stream their inputs with non-temporal loads (kbench A/B).
+  partition_variant(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats, late_idx,
+                    late_cap, stream, nb <= kStageMaxNb ? 5 : 1);
+}
+
+void partition_variant(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
+                       const int32_t* jhash_tab, int64_t n, const PartPlan& plan,
+                       const int32_t* kg_dest, uint32_t* cursor, Rec* out, int64_t* stats,
+                       uint32_t* late_idx, uint32_t late_cap, intptr_t stream, int variant) {
   if (n <= 0) return;
   const int nb = plan.nranks << plan.nsub_log2;
   if (nb > 16384) throw std::runtime_error("partition: too many buckets (max 16384)");
@@ -643,15 +937,42 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
   // >= 32 records, and nb global reservations per workgroup instead of per 8K events.
   int blocks = grid_for(n, 65536, 1024);
   const int64_t chunk = (n + blocks - 1) / blocks;
-  static bool attr = false;
-  if (!attr) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)partition_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));
-    attr = true;
+  const size_t lds = (size_t)((nb + 3) & ~3) * 4 + 16 * 8;
+  hipStream_t st = (hipStream_t)stream;
+#define MXS_PART(VV)                                                                          \
+  case VV: {                                                                                  \
+    static bool attr = false;                                                                 \
+    if (!attr) {                                                                              \
+      HIP_CHECK(hipFuncSetAttribute((const void*)partition_kernel<VV>,                         \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024));   \
+      attr = true;                                                                            \
+    }                                                                                         \
+    hipLaunchKernelGGL(partition_kernel<VV>, dim3(blocks), dim3(1024), lds, st, keys, ts, vals, \
+                       jhash_tab, n, chunk, plan, kg_dest, cursor, out, stats, late_idx,       \
+                       late_cap);                                                              \
+    break;                                                                                    \
   }
-  hipLaunchKernelGGL(partition_kernel, dim3(blocks), dim3(1024), (size_t)((nb + 3) & ~3) * 4 + 16 * 8,
-                     (hipStream_t)stream, keys, ts, vals, jhash_tab, n, chunk, plan, kg_dest,
-                     cursor, out, stats, late_idx, late_cap);
+#define MXS_PART_STAGED(VV, TV)                                                               \
+  case VV: {                                                                                  \
+    if (nb > kStageMaxNb) throw std::runtime_error("staged partition needs <= 512 buckets");  \
+    static bool attr = false;                                                                 \
+    if (!attr) {                                                                              \
+      HIP_CHECK(hipFuncSetAttribute((const void*)partition_staged_kernel<TV>,                  \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kStagedLds)); \
+      attr = true;                                                                            \
+    }                                                                                         \
+    hipLaunchKernelGGL(partition_staged_kernel<TV>, dim3(blocks), dim3(1024), kStagedLds, st,   \
+                       keys, ts, vals, jhash_tab, n, chunk, plan, kg_dest, cursor, out, stats, \
+                       late_idx, late_cap);                                                    \
+    break;                                                                                    \
+  }
+  switch (variant) {
+    MXS_PART(0) MXS_PART(1) MXS_PART(2) MXS_PART(3)
+    MXS_PART_STAGED(4, 0) MXS_PART_STAGED(5, 1)
+    default: throw std::runtime_error("partition: unknown variant");
+  }
+#undef MXS_PART
+#undef MXS_PART_STAGED
   HIP_CHECK(hipGetLastError());
 }
 

@@ -63,6 +63,10 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                const int32_t* jhash_tab, int64_t n, const PartPlan& plan, const int32_t* kg_dest,
                uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap,
                intptr_t stream);
+void partition_variant(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
+                       const int32_t* jhash_tab, int64_t n, const PartPlan& plan,
+                       const int32_t* kg_dest, uint32_t* cursor, Rec* out, int64_t* stats,
+                       uint32_t* late_idx, uint32_t late_cap, intptr_t stream, int variant);
 void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& plan, uint64_t* keys_g,
                 uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g, uint32_t* occupancy,
                 uint32_t* flags, intptr_t stream);

@@ -87,7 +87,7 @@ class KeyedWindowOperator:
                  hash_mode: int = 0, jhash_table: torch.Tensor | None = None,
                  map_prog: E.Program = E.EMPTY, filter_prog: E.Program = E.EMPTY,
                  batch_capacity: int = 1 << 20, bucket_slack: float = 1.5,
-                 cap_log2: int = 11, time_mode: str = "event", ooo_bound: int = 0,
+                 cap_log2: int = 12, time_mode: str = "event", ooo_bound: int = 0,
                  side_output_late: bool = False, late_capacity: int = 1 << 16,
                  clock: Callable[[], int] | None = None):
         self.device = torch.device(device)
@@ -115,10 +115,14 @@ class KeyedWindowOperator:
         self.metrics = OperatorMetrics()
 
         # ---- state geometry ----
-        per_rank = int(max_keys / self.world * 1.3) + 1024
+        # Keys per rank: key groups spread keys unevenly over ranks, so leave 30 % headroom.
+        per_rank = int(max_keys / self.world * (1.3 if self.world > 1 else 1.0)) + 1024
         self.cap_log2 = cap_log2
         cap = 1 << cap_log2
-        self.nsub = _next_pow2(max(1, math.ceil(per_rank / (cap * 0.5))))
+        # Linear probing in LDS stays cheap up to ~0.7 load (2.2 probes per hit); small tables
+        # keep 0.5 for headroom against binomial imbalance between sub-tables.
+        load = 0.7 if cap_log2 >= 12 else 0.5
+        self.nsub = _next_pow2(max(1, math.ceil(per_rank / (cap * load))))
         self.nsub_log2 = self.nsub.bit_length() - 1
         if self.nsub * self.world > 16384:
             raise ValueError("key space too large for the bucket histogram; raise cap_log2")
@@ -167,7 +171,11 @@ class KeyedWindowOperator:
         self.batch_capacity = int(batch_capacity)
         self.bucket_slack = slack
         per = self.batch_capacity / self.nbuckets
-        self.bucket_cap = int(per * slack + 6 * math.sqrt(max(per, 1.0)) + 64)
+        # The GPU partition pads every workgroup's run to whole 8-record groups (<= 7 holes per
+        # bucket and workgroup, <= 1024 workgroups): capacity is a multiple of 8 with that slack.
+        nblk = min(1024, max(1, -(-self.batch_capacity // 65536)))
+        cap = int(per * slack + 6 * math.sqrt(max(per, 1.0)) + 64) + 8 * nblk
+        self.bucket_cap = (cap + 7) & ~7
         words = self.nbuckets * self.bucket_cap * K.REC_WORDS
         self.send = torch.empty(words, dtype=torch.int64, device=self.device)
         self.recv = torch.empty(words, dtype=torch.int64, device=self.device) if self.world > 1 else self.send

@@ -43,21 +43,27 @@ def main():
     kg = torch.zeros(128, dtype=torch.int32, device=dev)
     results = {}
     variants = {}
-    for nsub_log2 in (9, 10, 11):
+    for nsub_log2 in (9,):
         nb = 1 << nsub_log2
-        bcap = int(n / nb * 1.5) + 1024
+        bcap = (int(n / nb * 1.5) + 8 * 1024 + 7) & ~7
         cursor = torch.zeros(nb, dtype=torch.int32, device=dev)
         out = torch.empty(nb * bcap * 3, dtype=torch.int64, device=dev)
         stats = K.new_stats(dev)
-        for ablate in (0, 1):
-            plan = K.PartitionPlan(max_parallelism=128, nsub_log2=nsub_log2, nranks=1,
-                                   window_mode=1, drop_late=1, hash_mode=0, bucket_cap=bcap,
-                                   late_ts=-5000, tbase=-60000, pane=60000, ablate=ablate)
+        from mxstream.ops.native import load
+        m = load()
+        for ablate in [int(x) for x in os.environ.get("KB_ABLATE", "0,1").split(",")]:
+            for var in [int(x) for x in os.environ.get("KB_VARIANTS", "0,1,4,5").split(",")]:
+                plan = K.PartitionPlan(max_parallelism=128, nsub_log2=nsub_log2, nranks=1,
+                                       window_mode=1, drop_late=1, hash_mode=0, bucket_cap=bcap,
+                                       late_ts=-5000, tbase=-60000, pane=60000, ablate=ablate)
 
-            def f(plan=plan, cursor=cursor, out=out, stats=stats):
-                K.step_begin(cursor, stats)
-                K.partition(keys, ts, vals, plan, kg, cursor, out, stats)
-            variants[f"partition nb={nb} ablate={ablate}"] = f
+                def f(plan=plan, cursor=cursor, out=out, stats=stats, var=var):
+                    K.step_begin(cursor, stats)
+                    m.gpu_partition_variant(keys.data_ptr(), ts.data_ptr(), vals.data_ptr(), 0, n,
+                                            plan.as_dict(), kg.data_ptr(), cursor.data_ptr(),
+                                            out.data_ptr(), stats.data_ptr(),
+                                            torch.cuda.current_stream().cuda_stream, var)
+                variants[f"partition nb={nb} ablate={ablate} v={var}"] = f
     # fire: a populated 1M-key state
     op = KeyedWindowOperator(size=60000, agg=K.AGG_SUM_I64, device=dev, max_keys=nkeys,
                              batch_capacity=n, ooo_bound=2000,
@@ -75,6 +81,9 @@ def main():
                           map_prog=mp, filt_prog=fp, out_keys=op.out_keys, out_vals=op.out_vals,
                           out_raw=op.out_raw, out_cnt=op.out_cnt, out_n=op.out_n, ablate=ab)
         variants[f"fire {ablate}"] = g
+    flt = os.environ.get("KB_FILTER")
+    if flt:
+        variants = {k: v for k, v in variants.items() if flt in k}
     for name, f in variants.items():
         f()
     torch.cuda.synchronize()

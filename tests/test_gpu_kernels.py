@@ -143,3 +143,39 @@ def test_expr_filter_gpu(gpu_device):
     prog = E.compile_expr(E.var(0) > 90)
     keep = K.expr_filter(x, prog)
     assert torch.equal(keep, x > 90)
+
+
+@pytest.mark.parametrize("nsub_log2,nranks", [(9, 1), (6, 8), (3, 2)])
+def test_partition_staged_variant_matches_plain(native, gpu_device, nsub_log2, nranks):
+    """The write-combined partition (variant 4) holds the same records per bucket as the plain
+    scatter (variant 0); its padding holes carry t == 0xFFFFFFFF."""
+    n = 300_001
+    keys, ts, vals = _gen(gpu_device, n, 70_000)
+    nb = nranks << nsub_log2
+    bcap = (int(n / nb * 1.5) + 8 * 1024 + 7) & ~7
+    kg = torch.tensor([(k * nranks) // 128 for k in range(128)], dtype=torch.int32,
+                      device=gpu_device)
+    plan = K.PartitionPlan(max_parallelism=128, nsub_log2=nsub_log2, nranks=nranks, window_mode=1,
+                           drop_late=1, hash_mode=0, bucket_cap=bcap, late_ts=2000, tbase=500,
+                           pane=500)
+    res = {}
+    for var in (0, 4):
+        cursor = torch.zeros(nb, dtype=torch.int32, device=gpu_device)
+        out = torch.zeros(nb * bcap * 3, dtype=torch.int64, device=gpu_device)
+        stats = K.new_stats(gpu_device)
+        native.gpu_partition_variant(keys.data_ptr(), ts.data_ptr(), vals.data_ptr(), 0, n,
+                                     plan.as_dict(), kg.data_ptr(), cursor.data_ptr(),
+                                     out.data_ptr(), stats.data_ptr(),
+                                     torch.cuda.current_stream().cuda_stream, var)
+        res[var] = (cursor.cpu(), out.cpu().view(nb, bcap, 3), stats.cpu())
+    c0, o0, s0 = res[0]
+    c4, o4, s4 = res[4]
+    assert torch.equal(s0, s4)
+    hole = (0xFFFFFFFF << 32) | 0xFFFFFFFF
+    for b in range(nb):
+        a = o0[b, :int(c0[b])].numpy()
+        e = o4[b, :int(c4[b])].numpy()
+        e = e[e[:, 2] != np.int64(hole - (1 << 64))]
+        assert len(a) == len(e)
+        assert np.array_equal(a[np.lexsort(a.T[::-1])], e[np.lexsort(e.T[::-1])])
+        assert int(c4[b]) % 8 == 0
