@@ -1,0 +1,204 @@
+"""Native-backed DataStream operators.
+
+``NativeWindowOp`` runs a keyed tumbling/sliding window with a field-wise aggregate (reduce that
+sums one numeric field, ``sum/min/max(pos)``, builtin aggregate functions) on the native
+``KeyedWindowOperator`` — the C++ twin on CPU or the gfx950 kernels on GPU — instead of the
+per-record host WindowOperator. Semantics are identical (differential tests in
+tests/test_api_native.py); the planner (api/planner.py) only selects it for shapes it can prove.
+
+Records are columnarised per micro-batch: the key field becomes a 64-bit id (string keys via the
+C++ StringDict), the aggregated field an int64 / float64 column, the timestamp an int64 column;
+window results come back as (key id, value, count) rows and are rebuilt into tuples.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from ..ops import kernels as K
+from ..utils.hashing import java_hash
+from .operators import LONG_MAX, LONG_MIN, Operator, Rec, WM, WindowOp
+from .window_operator import KeyedWindowOperator
+
+
+class NativeWindowOp(Operator):
+    name = "Window(native)"
+
+    def __init__(self, *, key_fn, key_pos: int, val_pos: int, kind: str, assigner, lateness: int,
+                 late_tag, device: str, fallback_factory, map_prog=None, filter_prog=None,
+                 result_builder=None, max_keys: int = 1 << 16, ok_arities=None):
+        self.key_fn = key_fn
+        self.key_pos = key_pos
+        self.val_pos = val_pos
+        self.kind = kind                      # sum | min | max | count | avg
+        self.assigner = assigner
+        self.lateness = lateness
+        self.late_tag = late_tag
+        self.device = device
+        self.fallback_factory = fallback_factory
+        self.result_builder = result_builder
+        self.max_keys = max_keys
+        self.ok_arities = ok_arities
+        self.op: KeyedWindowOperator | None = None
+        self.fallback: WindowOp | None = None
+        self.wm = LONG_MIN
+        self.pending: list = []
+        self.templates: dict = {}             # key id -> first record (keep-first fields)
+        self.num_late_records_dropped = 0
+
+    def open(self, ctx):
+        super().open(ctx)
+        from ..ops.native import load
+
+        self.dict = load().StringDict()
+        self.str_keys = None
+
+    # -- lazy construction on the first records (value type decides the aggregate kind) --
+    def _build(self, sample_val) -> bool:
+        is_float = isinstance(sample_val, float)
+        if not isinstance(sample_val, (int, float)) or isinstance(sample_val, bool):
+            return False
+        agg = {("sum", False): K.AGG_SUM_I64, ("sum", True): K.AGG_SUM_F64,
+               ("min", False): K.AGG_MIN_I64, ("min", True): K.AGG_MIN_F64,
+               ("max", False): K.AGG_MAX_I64, ("max", True): K.AGG_MAX_F64,
+               ("count", False): K.AGG_COUNT, ("count", True): K.AGG_COUNT,
+               ("avg", False): K.AGG_AVG_I64, ("avg", True): K.AGG_AVG_F64}[(self.kind, is_float)]
+        self.is_float = is_float
+        a = self.assigner
+        event = a.is_event_time()
+        dev = torch.device(self.device)
+        cap_log2 = 12 if self.max_keys > 100_000 else 9
+        self.op = KeyedWindowOperator(
+            size=a.size, slide=a.slide, offset=a.offset, lateness=self.lateness if event else 0,
+            agg=agg, device=dev, max_keys=self.max_keys, parallelism=1,
+            batch_capacity=max(1024, self.ctx.parallelism), cap_log2=cap_log2,
+            time_mode="event" if event else "processing", external_watermark=True,
+            side_output_late=self.late_tag is not None, clock=self.ctx.clock)
+        return True
+
+    def _to_fallback(self):
+        self.fallback = self.fallback_factory()
+        self.fallback.open(self.ctx)
+
+    def _key_id(self, k) -> int:
+        if isinstance(k, str):
+            if self.str_keys is False:
+                raise TypeError("mixed key types")
+            self.str_keys = True
+            return self.dict.intern(k)
+        if isinstance(k, int) and not isinstance(k, bool) and 0 <= k < (1 << 63) - 1:
+            if self.str_keys is True:
+                raise TypeError("mixed key types")
+            self.str_keys = False
+            return k
+        raise TypeError("unsupported key type for the native path")
+
+    def _flush(self) -> list:
+        recs = self.pending
+        self.pending = []
+        if not recs:
+            return []
+        if self.op is None:
+            v0 = recs[0].value
+            if (not isinstance(v0, tuple) or (self.ok_arities and len(v0) not in self.ok_arities)
+                    or not self._build(v0[self.val_pos])):
+                self._to_fallback()
+                return self.fallback.process(recs)
+        n = len(recs)
+        try:
+            kid = np.empty(n, dtype=np.int64)
+            tsa = np.empty(n, dtype=np.int64)
+            vv = np.empty(n, dtype=np.float64 if self.is_float else np.int64)
+            now = self.ctx.clock()
+            event = self.assigner.is_event_time()
+            for i, r in enumerate(recs):
+                v = r.value
+                k = self._key_id(v[self.key_pos])
+                kid[i] = k
+                if k not in self.templates:
+                    self.templates[k] = v
+                tsa[i] = r.ts if event else now
+                x = v[self.val_pos]
+                if isinstance(x, float) != self.is_float:
+                    raise TypeError("mixed value types")
+                vv[i] = x
+        except TypeError:
+            # Unsupported data for the native path: switch to the exact host operator.
+            self._to_fallback()
+            return self.fallback.process(recs)
+        dev = self.op.device
+        kt = torch.from_numpy(kid).to(dev)
+        tt = torch.from_numpy(tsa).to(dev)
+        vt = torch.from_numpy(vv.view(np.int64)).to(dev)
+        late_before = self.op.metrics.num_late_records_dropped
+        fired = self.op.process(kt, tt, vt)
+        if self.op.late_side:
+            for idx in np.concatenate(self.op.late_side).tolist():
+                r = recs[idx]
+                self.side.setdefault(self.late_tag.tag_id, []).append(Rec(r.value, r.ts, r.subtask))
+            self.op.late_side.clear()
+        elif self.late_tag is None:
+            self.num_late_records_dropped += self.op.metrics.num_late_records_dropped - late_before
+        return self._emit(fired)
+
+    def _emit(self, fired) -> list:
+        out = []
+        P, MP = self.ctx.parallelism, self.ctx.max_parallelism
+        for fr in fired:
+            ts = fr.window_end - 1
+            for k, val, raw, cnt in zip(fr.keys.tolist(), fr.values.tolist(), fr.raw.tolist(),
+                                        fr.counts.tolist()):
+                key_obj = self.dict.get(k) if self.str_keys else k
+                if self.kind in ("sum", "min", "max"):
+                    res = float(np.int64(raw).view(np.float64)) if self.is_float else int(raw)
+                elif self.kind == "count":
+                    res = int(cnt)
+                else:
+                    res = float(val)
+                value = self.result_builder(self.templates[k], res, key_obj)
+                sub = java_hash(key_obj)
+                from ..utils.hashing import flink_murmur
+
+                sub = (flink_murmur(sub) % MP) * P // MP
+                out.append(Rec(value, ts, sub))
+        return out
+
+    def process(self, items):
+        if self.fallback is not None:
+            return self.fallback.process(items)
+        out = []
+        for it in items:
+            if isinstance(it, WM):
+                out.extend(self._flush())
+                if self.fallback is not None:
+                    out.extend(self.fallback.process([it]))
+                    continue
+                self.wm = it.ts
+                if self.op is not None and self.assigner.is_event_time():
+                    out.extend(self._emit(self.op.advance_watermark(it.ts)))
+                out.append(it)
+            else:
+                self.pending.append(it)
+        out.extend(self._flush())
+        return out
+
+    def on_processing_time(self, now):
+        if self.fallback is not None:
+            return self.fallback.on_processing_time(now)
+        out = self._flush()
+        if self.op is not None and not self.assigner.is_event_time():
+            out.extend(self._emit(self.op.advance_watermark(now)))
+        return out
+
+    def finish(self):
+        if self.fallback is not None:
+            return self.fallback.finish()
+        return self._flush()
+
+    def take_side(self, tag_id):
+        if self.fallback is not None:
+            return self.fallback.take_side(tag_id)
+        return super().take_side(tag_id)
+
+
+_ = LONG_MAX

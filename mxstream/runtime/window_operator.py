@@ -89,7 +89,7 @@ class KeyedWindowOperator:
                  batch_capacity: int = 1 << 20, bucket_slack: float = 1.5,
                  cap_log2: int = 12, time_mode: str = "event", ooo_bound: int = 0,
                  side_output_late: bool = False, late_capacity: int = 1 << 16,
-                 clock: Callable[[], int] | None = None):
+                 clock: Callable[[], int] | None = None, external_watermark: bool = False):
         self.device = torch.device(device)
         self.comm = comm or LocalComm()
         self.world = self.comm.world
@@ -106,6 +106,9 @@ class KeyedWindowOperator:
             raise ValueError("time_mode must be 'event' or 'processing'")
         self.ooo_bound = int(ooo_bound)
         self.clock = clock
+        # external_watermark: the caller drives time with advance_watermark() (DataStream API:
+        # watermarks come from the upstream assigner); process() then never advances it.
+        self.external_watermark = external_watermark
         self.parallelism = parallelism or self.world
         self.max_parallelism = max_parallelism
         self.hash_mode = hash_mode
@@ -298,8 +301,14 @@ class KeyedWindowOperator:
             if hi - lo + 1 > self.ring:
                 self._grow_ring(hi - lo + 1)
             self.min_live_pane, self.max_seen_pane = lo, hi
-            if self.next_fire_start is None:
-                self.next_fire_start = self.first_start_containing(self.pane_start(gmin))
+            # Invariant: every window starting before next_fire_start is due (maxTs <= wm) and
+            # has been evaluated. New data can belong to not-yet-due windows before the current
+            # cursor (older but not late): lower the cursor to the first such window. Windows
+            # that are already due and receive data (allowed lateness) go through _refire.
+            cand = self.first_start_containing(self.pane_start(gmin))
+            if old_wm > I64_MIN:
+                cand = max(cand, self._align_up(old_wm - self.size + 2))
+            self.next_fire_start = cand if self.next_fire_start is None else min(self.next_fire_start, cand)
             fired_hi = self._fired_hi()
             cap = 1 << self.cap_log2
             lds_budget = 150 * 1024 - cap * 8
@@ -313,12 +322,14 @@ class KeyedWindowOperator:
             # Late-but-allowed data: re-fire already-passed windows that are not cleaned yet.
             if gmin <= fired_hi:
                 out.extend(self._refire(gmin, min(gmax, fired_hi), old_wm))
+        self.metrics.steps += 1
+        if self.external_watermark:
+            return out
         new_wm = max(old_wm, wm_global)
         self.wm = new_wm
         self.metrics.current_watermark = new_wm
         out.extend(self._fire_ready(new_wm))
         self._purge(new_wm)
-        self.metrics.steps += 1
         return out
 
     def advance_watermark(self, wm: int) -> list[FireResult]:
@@ -348,10 +359,15 @@ class KeyedWindowOperator:
         return not (p1 < self.min_live_pane or p0 > self.max_seen_pane)
 
     def _fire_window(self, s: int, only_dirty: bool) -> FireResult | None:
-        p0 = self.pane_of(s)
+        # Only panes inside the live span exist in the ring; older/newer panes of the window
+        # never held data and their ring slots belong to other panes (aliasing).
+        p0 = max(self.pane_of(s), self.min_live_pane)
+        p1 = min(self.pane_of(s) + self.panes_per_window - 1, self.max_seen_pane)
+        if p1 < p0:
+            return None
         self.out_n.zero_()
         K.window_fire(self.keys_g, self.acc_g, self.cnt_g, self.dirty_g, agg=self.agg,
-                      npanes=self.panes_per_window, ring=self.ring, p0=p0, wstart=s,
+                      npanes=p1 - p0 + 1, ring=self.ring, p0=p0, wstart=s,
                       wend=s + self.size, only_dirty=only_dirty, map_prog=self.map_prog,
                       filt_prog=self.filter_prog, out_keys=self.out_keys, out_vals=self.out_vals,
                       out_raw=self.out_raw, out_cnt=self.out_cnt, out_n=self.out_n)
