@@ -1,0 +1,94 @@
+"""Multi-process keyBy shuffle over torch.distributed (gloo): results are invariant to G.
+
+Each rank ingests its own source partition; the keyed window operator routes records by Flink
+key group to the owning rank (equal-split all-to-all), the watermark is the MIN over ranks.
+The union of what all ranks fire must equal a single-rank run over the concatenated input.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mxstream.ops import kernels as K
+from mxstream.parallel.comm import TorchComm
+from mxstream.runtime.window_operator import KeyedWindowOperator
+
+STEPS, PER = 6, 3000
+
+
+def _batch(rank, step):
+    keys = torch.empty(PER, dtype=torch.int64)
+    ts = torch.empty_like(keys)
+    vals = torch.empty_like(keys)
+    K.gen_events(keys, ts, vals, seed=11, stream_id=rank, idx0=step * PER, nkeys=5000,
+                 ts_base=step * 2000, ts_span=2000, disorder=700, val_lo=0, val_span=1000)
+    return keys, ts, vals
+
+
+def _collect(out):
+    return {(r.window_start, int(k)): (int(a), int(c), r.refire)
+            for r in out for k, a, c in zip(r.keys, r.raw, r.counts)}
+
+
+def _worker(rank, world, port, size, slide, lateness, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = TorchComm()
+    op = KeyedWindowOperator(size=size, slide=slide, lateness=lateness, agg=K.AGG_SUM_I64,
+                             device="cpu", comm=comm, max_keys=5000, batch_capacity=PER,
+                             ooo_bound=500, cap_log2=8)
+    out = []
+    for step in range(STEPS):
+        out += op.process(*_batch(rank, step))
+    out += op.finish()
+    q.put((rank, _collect(out), op.metrics.num_late_records_dropped))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("size,slide,lateness", [(3000, 3000, 0), (4000, 1000, 1500)])
+def test_results_invariant_to_world_size(world, size, slide, lateness):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, size, slide, lateness, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    merged, late = {}, 0
+    owners = {}
+    for rank, d, nl in res:
+        late += nl
+        for k, v in d.items():
+            assert k not in owners, "a (window, key) fired on two ranks"
+            owners[k] = rank
+            merged[k] = v
+    # Single-rank reference: one operator sees every rank's batches, step by step.
+    op = KeyedWindowOperator(size=size, slide=slide, lateness=lateness, agg=K.AGG_SUM_I64,
+                             device="cpu", max_keys=5000, batch_capacity=PER * world,
+                             ooo_bound=500, cap_log2=8)
+    out = []
+    for step in range(STEPS):
+        parts = [_batch(r, step) for r in range(world)]
+        out += op.process(*[torch.cat([p[i] for p in parts]) for i in range(3)])
+    out += op.finish()
+    ref = _collect(out)
+    strip = lambda d: {k: v[:2] for k, v in d.items()}
+    assert strip(merged) == strip(ref)
+    assert late == op.metrics.num_late_records_dropped
