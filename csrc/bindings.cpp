@@ -206,6 +206,30 @@ PYBIND11_MODULE(_mxs_native, m) {
                               int64_t now, intptr_t red, intptr_t stream) {
     gpu::step_finish(P<int64_t>(stats), P<int64_t>(lm), bound, ev, now, P<int64_t>(red), stream);
   });
+  m.def("gpu_rolling_lookup", [](intptr_t recs, intptr_t counts, int nsrc, int nsub, uint32_t bcap,
+                                 int cap_log2, intptr_t keys_g, intptr_t sk, intptr_t vals,
+                                 intptr_t n_out, intptr_t flags, intptr_t stream) {
+    gpu::rolling_lookup(P<Rec>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2,
+                        P<uint64_t>(keys_g), P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_out),
+                        P<uint32_t>(flags), stream);
+  });
+  m.def("gpu_rolling_heads", [](intptr_t sk, intptr_t n_in, int64_t n_cap, intptr_t heads,
+                                intptr_t n_heads, intptr_t stream) {
+    gpu::rolling_heads(P<int64_t>(sk), P<uint32_t>(n_in), n_cap, P<uint32_t>(heads),
+                       P<uint32_t>(n_heads), stream);
+  });
+  m.def("gpu_rolling_scan", [](int agg, intptr_t sk, intptr_t perm, intptr_t vals, intptr_t n_in,
+                               intptr_t heads, intptr_t n_heads, int64_t max_segments,
+                               intptr_t acc_g, intptr_t cnt_g, intptr_t keys_g,
+                               std::vector<int32_t> code, std::vector<double> consts,
+                               intptr_t ok, intptr_t ov, intptr_t ot, intptr_t on,
+                               uint32_t out_cap, intptr_t stream) {
+    gpu::rolling_scan(agg, P<int64_t>(sk), P<int64_t>(perm), P<uint64_t>(vals), P<uint32_t>(n_in),
+                      P<uint32_t>(heads), P<uint32_t>(n_heads), max_segments, P<uint64_t>(acc_g),
+                      P<uint32_t>(cnt_g), P<uint64_t>(keys_g), make_prog(code, consts),
+                      P<uint64_t>(ok), P<uint64_t>(ov), P<int64_t>(ot), P<uint32_t>(on), out_cap,
+                      stream);
+  });
   m.def("gpu_expr_filter", [](intptr_t x, int64_t n, std::vector<int32_t> code,
                               std::vector<double> consts, intptr_t keep, intptr_t stream) {
     gpu::expr_filter(P<double>(x), n, make_prog(code, consts), P<uint8_t>(keep), stream);
@@ -260,6 +284,18 @@ PYBIND11_MODULE(_mxs_native, m) {
   m.def("cpu_step_finish", [](intptr_t stats, intptr_t lm, int64_t bound, int32_t ev, int64_t now,
                               intptr_t red) {
     cpu::step_finish(P<int64_t>(stats), P<int64_t>(lm), bound, ev, now, P<int64_t>(red));
+  });
+  m.def("cpu_rolling_rows", [](intptr_t recs, intptr_t counts, int nsrc, int nsub, uint32_t bcap,
+                               int cap_log2, int agg, intptr_t keys_g, intptr_t acc_g,
+                               intptr_t cnt_g, intptr_t flags, std::vector<int32_t> code,
+                               std::vector<double> consts, intptr_t ok, intptr_t ov, intptr_t ot,
+                               intptr_t on, uint32_t out_cap) {
+    ExprProg f = make_prog(code, consts);
+    py::gil_scoped_release nogil;
+    cpu::rolling_rows(P<Rec>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2, agg,
+                      P<uint64_t>(keys_g), P<uint64_t>(acc_g), P<uint32_t>(cnt_g),
+                      P<uint32_t>(flags), f, P<uint64_t>(ok), P<uint64_t>(ov), P<int64_t>(ot),
+                      P<uint32_t>(on), out_cap);
   });
   m.def("cpu_expr_filter", [](intptr_t x, int64_t n, std::vector<int32_t> code,
                               std::vector<double> consts, intptr_t keep) {

@@ -233,6 +233,56 @@ void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& p, uint64_
   }
 }
 
+// Rolling keyed state with per-record rows (key, post-update value, src<<32|arrival) in
+// per-key arrival order: the twin of rolling_lookup + sort + rolling_scan on the GPU.
+void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bucket_cap,
+                  int cap_log2, int agg, uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g,
+                  uint32_t* flags, const ExprProg& filt, uint64_t* out_key, uint64_t* out_val,
+                  int64_t* out_tag, uint32_t* out_n, uint32_t out_cap) {
+  const uint32_t mask = (1u << cap_log2) - 1;
+  uint32_t n = *out_n;
+  for (int sub = 0; sub < nsub; ++sub) {
+    uint64_t* keys = keys_g + ((size_t)sub << cap_log2);
+    bool inserted = false;
+    for (int src = 0; src < nsrc; ++src) {
+      const uint32_t c = std::min(counts[(size_t)src * nsub + sub], bucket_cap);
+      const Rec* seg = recs + ((size_t)src * nsub + sub) * bucket_cap;
+      for (uint32_t e = 0; e < c; ++e) {
+        const Rec& r = seg[e];
+        if (r.t == 0xFFFFFFFFu) continue;
+        const uint32_t s = probe_insert(keys, r.key, mask, &inserted);
+        if (s == kNoSlot) {
+          flags[0] |= 1u;
+          continue;
+        }
+        const size_t gi = ((size_t)sub << cap_log2) + s;
+        const uint64_t v = agg_lift(agg, r.val);
+        acc_g[gi] = cnt_g[gi] ? agg_combine(agg, acc_g[gi], v) : v;
+        cnt_g[gi] += 1;
+        bool emit = true;
+        if (filt.ncode) {
+          double vars[kExprVars] = {0};
+          vars[0] = agg_result_f64(agg, acc_g[gi], cnt_g[gi]);
+          vars[1] = (double)cnt_g[gi];
+          vars[4] = (double)r.key;
+          vars[5] = (double)(int64_t)acc_g[gi];
+          vars[6] = vars[0];
+          emit = expr_eval(filt, vars) != 0.0;
+        }
+        if (emit) {
+          if (n < out_cap) {
+            out_key[n] = r.key;
+            out_val[n] = agg == AGG_COUNT ? (uint64_t)cnt_g[gi] : acc_g[gi];
+            out_tag[n] = ((int64_t)src << 32) | r.aux;
+          }
+          ++n;
+        }
+      }
+    }
+  }
+  *out_n = n;
+}
+
 void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep) {
   for (int64_t i = 0; i < n; ++i) {
     double vars[kExprVars] = {x[i], 0, 0, 0, 0, 0, 0, 0};

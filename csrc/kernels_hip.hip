@@ -874,6 +874,169 @@ __global__ __launch_bounds__(256) void expr_filter_kernel(const double* __restri
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Rolling keyed state (StreamGroupedReduce / keyed ValueState): per-record post-update values
+// in arrival order per key (ComputeCpuMax.java:26 `keyBy(0).max(2)` emits on every record).
+//   1. rolling_lookup : one workgroup per received (src, sub) bucket; find/insert the key in the
+//                       HBM hash table (global CAS), write sort key (slot<<40 | src<<32 | aux)
+//                       and the value, compacted.
+//   2. sort (one radix sort of the 64-bit keys: key-major, then channel, then arrival)
+//   3. rolling_heads  : segment starts (first record of every key) compacted.
+//   4. rolling_scan   : one wave per key segment: ordered inclusive scan with shuffles, seeded
+//                       by the stored state, traced filter epilogue, ballot-compacted output,
+//                       state written back once per key.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t global_probe_insert(uint64_t* keys, uint64_t key, uint32_t mask) {
+  uint32_t s = (uint32_t)mix64(key) & mask;
+  for (uint32_t i = 0; i <= mask; ++i) {
+    const uint64_t k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == key) return s;
+    if (k == kEmptyKey) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&keys[s], (unsigned long long)kEmptyKey,
+                                      (unsigned long long)key);
+      if (prev == kEmptyKey || prev == key) return s;
+    }
+    s = (s + 1) & mask;
+  }
+  return kNoSlot;
+}
+
+__global__ __launch_bounds__(256) void rolling_lookup_kernel(
+    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
+    uint32_t bucket_cap, int cap_log2, uint64_t* __restrict__ keys_g,
+    int64_t* __restrict__ sort_key, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
+    uint32_t* __restrict__ flags) {
+  const int b = blockIdx.x;  // = src * nsub + sub
+  const int src = b / nsub, sub = b % nsub;
+  uint32_t c = counts[b];
+  c = c < bucket_cap ? c : bucket_cap;
+  const Rec* seg = recs + (size_t)b * bucket_cap;
+  __shared__ uint32_t base;
+  if (threadIdx.x == 0) base = c ? atomicAdd(n_out, c) : 0u;
+  __syncthreads();
+  uint64_t* keys = keys_g + ((size_t)sub << cap_log2);
+  const uint32_t mask = (1u << cap_log2) - 1;
+  for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
+    const Rec r = seg[e];
+    int64_t sk = INT64_MAX;  // holes and overflow sort last and are ignored
+    if (r.t != 0xFFFFFFFFu) {
+      const uint32_t s = global_probe_insert(keys, r.key, mask);
+      if (s == kNoSlot) {
+        atomicOr(&flags[0], 1u);
+      } else {
+        const uint64_t slot = ((uint64_t)sub << cap_log2) | s;
+        sk = (int64_t)((slot << 40) | ((uint64_t)src << 32) | r.aux);
+      }
+    }
+    sort_key[base + e] = sk;
+    vals_out[base + e] = r.val;
+  }
+}
+
+__global__ __launch_bounds__(256) void rolling_heads_kernel(const int64_t* __restrict__ sk,
+                                                            const uint32_t* __restrict__ n_in,
+                                                            uint32_t* __restrict__ heads,
+                                                            uint32_t* __restrict__ n_heads) {
+  const uint32_t n = *n_in;
+  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    const uint32_t i = base + threadIdx.x;
+    bool h = false;
+    if (i < n) {
+      const int64_t k = sk[i];
+      h = k != INT64_MAX && (i == 0 || (sk[i - 1] >> 40) != (k >> 40));
+    }
+    const unsigned long long m = __ballot(h);
+    uint32_t wb = 0;
+    if (lane_id() == 0 && m) wb = atomicAdd(n_heads, (uint32_t)__popcll(m));
+    wb = __shfl(wb, 0);
+    if (h) heads[wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = i;
+  }
+}
+
+template <int AGG>
+__device__ __forceinline__ uint64_t roll_combine(uint64_t a, uint64_t b) {
+  return agg_combine(AGG, a, b);
+}
+
+template <int AGG>
+__global__ __launch_bounds__(256) void rolling_scan_kernel(
+    const int64_t* __restrict__ sk, const int64_t* __restrict__ perm,
+    const uint64_t* __restrict__ vals, const uint32_t* __restrict__ n_in,
+    const uint32_t* __restrict__ heads, const uint32_t* __restrict__ n_heads,
+    uint64_t* __restrict__ acc_g, uint32_t* __restrict__ cnt_g, const uint64_t* __restrict__ keys_g,
+    ExprProg filt, uint64_t* __restrict__ out_key, uint64_t* __restrict__ out_val,
+    int64_t* __restrict__ out_tag, uint32_t* __restrict__ out_n, uint32_t out_cap) {
+  extern __shared__ __attribute__((aligned(16))) double rsm[];  // VM columns [8 + depth][256]
+  LdsCol vars{rsm + threadIdx.x, 256};
+  LdsCol stack{rsm + kExprVars * 256 + threadIdx.x, 256};
+  const uint32_t n = *n_in, nh = *n_heads;
+  const int lane = lane_id();
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (uint32_t h = wave; h < nh; h += nwaves) {  // wave-uniform loop
+    const uint32_t start = heads[h];
+    const uint64_t slot = (uint64_t)(sk[start] >> 40);
+    uint32_t end = start + 1;
+    // Segment end: next record with a different slot (scan forward a wave at a time).
+    for (;;) {
+      const uint32_t i = end + lane;
+      const bool same = i < n && (uint64_t)(sk[i] >> 40) == slot && sk[i] != INT64_MAX;
+      const unsigned long long m = __ballot(!same);
+      if (m) {
+        end += (uint32_t)__ffsll((long long)m) - 1;
+        break;
+      }
+      end += 64;
+    }
+    const uint32_t c0 = cnt_g[slot];
+    uint64_t carry = c0 ? acc_g[slot] : 0;
+    bool have = c0 != 0;
+    const uint64_t key = keys_g[slot];
+    uint32_t cnt = c0;
+    for (uint32_t b0 = start; b0 < end; b0 += 64) {
+      const uint32_t i = b0 + lane;
+      const bool in = i < end;
+      uint64_t v = in ? agg_lift(AGG, vals[perm[i]]) : 0;
+      // Inclusive wave scan (Hillis-Steele) over the ordered chunk.
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(v, o);
+        if (lane >= o && in) v = roll_combine<AGG>(y, v);
+      }
+      const uint64_t post = have ? roll_combine<AGG>(carry, v) : v;
+      const uint32_t pcount = cnt + (uint32_t)(lane + 1);
+      const uint32_t nin = (end - b0) < 64 ? (end - b0) : 64;
+      bool emit = in;
+      if (in && filt.ncode) {
+        vars.set(0, agg_result_f64(AGG, post, pcount));
+        vars.set(1, (double)pcount);
+        vars.set(4, (double)key);
+        vars.set(5, (double)(int64_t)post);
+        vars.set(6, agg_result_f64(AGG, post, pcount));
+        emit = expr_eval_t(filt, stack, vars) != 0.0;
+      }
+      const unsigned long long m = __ballot(emit);
+      uint32_t wb = 0;
+      if (lane == 0 && m) wb = atomicAdd(out_n, (uint32_t)__popcll(m));
+      wb = __shfl(wb, 0);
+      if (emit) {
+        const uint32_t q = wb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (q < out_cap) {
+          out_key[q] = key;
+          out_val[q] = AGG == AGG_COUNT ? (uint64_t)pcount : post;
+          out_tag[q] = sk[i] & 0xFFFFFFFFFFll;  // src << 32 | arrival index
+        }
+      }
+      carry = __shfl(post, (int)nin - 1);
+      have = true;
+      cnt += nin;
+    }
+    if (lane == 0) {
+      if (AGG != AGG_COUNT) acc_g[slot] = carry;
+      cnt_g[slot] = cnt;
+    }
+  }
+}
+
 int grid_for(int64_t n, int block, int max_blocks) {
   int64_t g = (n + block - 1) / block;
   if (g < 1) g = 1;
@@ -1051,7 +1214,52 @@ void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep
 
 void rolling(const Rec*, const uint32_t*, const RollPlan&, uint64_t*, uint64_t*, uint32_t*,
              uint32_t*, uint32_t*, uint64_t*, intptr_t) {
-  throw std::runtime_error("rolling: GPU kernel not built yet");
+  throw std::runtime_error("gpu::rolling: use rolling_lookup / rolling_heads / rolling_scan");
+}
+
+void rolling_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
+                    uint32_t bucket_cap, int cap_log2, uint64_t* keys_g, int64_t* sort_key,
+                    uint64_t* vals_out, uint32_t* n_out, uint32_t* flags, intptr_t stream) {
+  if (nsrc * nsub <= 0) return;
+  hipLaunchKernelGGL(rolling_lookup_kernel, dim3(nsrc * nsub), dim3(256), 0, (hipStream_t)stream,
+                     recs, counts, nsrc, nsub, bucket_cap, cap_log2, keys_g, sort_key, vals_out,
+                     n_out, flags);
+  HIP_CHECK(hipGetLastError());
+}
+
+void rolling_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
+                   uint32_t* n_heads, intptr_t stream) {
+  hipLaunchKernelGGL(rolling_heads_kernel, dim3(grid_for(n_cap, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, sk, n_in, heads, n_heads);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <int AGG>
+static void launch_roll(const int64_t* sk, const int64_t* perm, const uint64_t* vals,
+                        const uint32_t* n_in, const uint32_t* heads, const uint32_t* n_heads,
+                        uint64_t* acc_g, uint32_t* cnt_g, const uint64_t* keys_g,
+                        const ExprProg& filt, uint64_t* ok, uint64_t* ov, int64_t* ot,
+                        uint32_t* on, uint32_t cap, int grid, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL(rolling_scan_kernel<AGG>, dim3(grid), dim3(256), lds, s, sk, perm, vals, n_in,
+                     heads, n_heads, acc_g, cnt_g, keys_g, filt, ok, ov, ot, on, cap);
+}
+
+void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_t* vals,
+                  const uint32_t* n_in, const uint32_t* heads, const uint32_t* n_heads,
+                  int64_t max_segments, uint64_t* acc_g, uint32_t* cnt_g, const uint64_t* keys_g,
+                  const ExprProg& filt, uint64_t* out_key, uint64_t* out_val, int64_t* out_tag,
+                  uint32_t* out_n, uint32_t out_cap, intptr_t stream) {
+  const int grid = grid_for(max_segments * 64, 256, 4096);
+  const size_t lds = (size_t)(kExprVars + filt.depth) * 256 * sizeof(double);
+  hipStream_t s = (hipStream_t)stream;
+  switch (agg) {
+#define MXS_R(A) case A: launch_roll<A>(sk, perm, vals, n_in, heads, n_heads, acc_g, cnt_g, keys_g, filt, out_key, out_val, out_tag, out_n, out_cap, grid, lds, s); break;
+    MXS_R(AGG_SUM_I64) MXS_R(AGG_SUM_F64) MXS_R(AGG_MIN_I64) MXS_R(AGG_MAX_I64)
+    MXS_R(AGG_MIN_F64) MXS_R(AGG_MAX_F64) MXS_R(AGG_COUNT)
+#undef MXS_R
+    default: throw std::runtime_error("rolling_scan: unsupported aggregate");
+  }
+  HIP_CHECK(hipGetLastError());
 }
 
 }  // namespace gpu

@@ -79,6 +79,16 @@ void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& plan, uint
              uint64_t* out_vals, intptr_t stream);
 void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep, intptr_t stream);
 void step_begin(uint32_t* cursor, int nb, int64_t* stats, intptr_t stream);
+void rolling_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
+                    uint32_t bucket_cap, int cap_log2, uint64_t* keys_g, int64_t* sort_key,
+                    uint64_t* vals_out, uint32_t* n_out, uint32_t* flags, intptr_t stream);
+void rolling_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
+                   uint32_t* n_heads, intptr_t stream);
+void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_t* vals,
+                  const uint32_t* n_in, const uint32_t* heads, const uint32_t* n_heads,
+                  int64_t max_segments, uint64_t* acc_g, uint32_t* cnt_g, const uint64_t* keys_g,
+                  const ExprProg& filt, uint64_t* out_key, uint64_t* out_val, int64_t* out_tag,
+                  uint32_t* out_n, uint32_t out_cap, intptr_t stream);
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
                  int64_t proc_now, int64_t* red, intptr_t stream);
 }  // namespace gpu
@@ -103,6 +113,10 @@ void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& plan, uint
              uint64_t* out_vals);
 void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep);
 void step_begin(uint32_t* cursor, int nb, int64_t* stats);
+void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bucket_cap,
+                  int cap_log2, int agg, uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g,
+                  uint32_t* flags, const ExprProg& filt, uint64_t* out_key, uint64_t* out_val,
+                  int64_t* out_tag, uint32_t* out_n, uint32_t out_cap);
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
                  int64_t proc_now, int64_t* red);
 }  // namespace cpu

@@ -1,0 +1,167 @@
+"""Benchmarks for the other BASELINE.json configs (bench.py runs config 3, the headline).
+
+  python -m mxstream.models.bench_configs --config 1   # chapter1 threshold alert on CPU
+  python -m mxstream.models.bench_configs --config 2   # keyed ValueState counter, 10k keys, 1 GPU
+  python -m mxstream.models.bench_configs --config 4   # sliding 1 min / 10 s + lateness, 10M keys
+
+Each prints one JSON line: events/s and the step time (and p50 alert latency where alerts fire).
+Config 1 runs the reference's exact text path: Java-semantics split + Double.parseDouble in the
+C++ runtime (csrc/runtime.cpp) and the traced `usage > 90` predicate in the C++ twin of the
+filter kernel (Main.java:21-31).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import time
+
+import numpy as np
+import torch
+
+from ..ops import expr as E
+from ..ops import kernels as K
+from ..ops.native import load
+from ..runtime.rolling_operator import KeyedRollingOperator
+from ..runtime.window_operator import KeyedWindowOperator
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def config1(steps: int, warmup: int, lines_per_step: int = 1 << 20) -> dict:
+    """CPU: text lines "ts ip cpuN usage" -> parse -> filter usage > 90 -> alerts."""
+    m = load()
+    rng = np.random.default_rng(1)
+    hosts = [f"10.8.{i // 256}.{i % 256}" for i in range(1024)]
+    usage = rng.uniform(0, 100, lines_per_step)
+    h = rng.integers(0, len(hosts), lines_per_step)
+    cpu = rng.integers(0, 64, lines_per_step)
+    text = "\n".join(f"1563452056 {hosts[a]} cpu{b} {u:.1f}" for a, b, u in zip(h, cpu, usage)).encode()
+    d = m.StringDict()
+    prog = E.compile_expr(E.var(0) > 90)
+    spec = [(1, 0), (2, 0), (3, 1)]  # host (dict id), cpu (dict id), usage (double)
+
+    def step():
+        cols, n, err_idx, err = m.parse_lines(text, spec, " ", d, 0)
+        x = torch.from_numpy(cols[2])
+        keep = K.expr_filter(x, prog)
+        return int(keep.sum())
+
+    for _ in range(warmup):
+        step()
+    t0 = time.perf_counter()
+    alerts = 0
+    for _ in range(steps):
+        alerts += step()
+    dt = time.perf_counter() - t0
+    ev = lines_per_step * steps
+    return {"config": 1, "metric": "events/sec (CPU threshold alert)", "value": ev / dt,
+            "unit": "events/s", "ms_per_step": dt / steps * 1e3, "alerts": alerts,
+            "lines_per_step": lines_per_step, "device": "cpu (1 thread)"}
+
+
+def config2(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000,
+            device: str = "cuda") -> dict:
+    """Keyed ValueState counter: count += 1 per record, per-record post-update value; alerts
+    (rows copied to the host) when a key's count crosses a multiple of 100k."""
+    dev = torch.device(device)
+    op = KeyedRollingOperator(agg=K.AGG_COUNT, device=dev, max_keys=keys, batch_capacity=batch,
+                              filter_prog=E.compile_expr(E.var(E.VAR_COUNT) % 100_000 == 0),
+                              emit_capacity=1 << 20)
+    kt = torch.empty(batch, dtype=torch.int64, device=dev)
+    tt = torch.empty_like(kt)
+    vt = torch.empty_like(kt)
+    step_i = [0]
+
+    def step():
+        K.gen_events(kt, tt, vt, seed=2, stream_id=0, idx0=step_i[0] * batch, nkeys=keys,
+                     ts_base=0, ts_span=1000, disorder=0, val_lo=0, val_span=100)
+        rows = op.process(kt, vt)
+        step_i[0] += 1
+        return len(rows.keys)
+
+    for _ in range(warmup):
+        step()
+    _sync(dev)
+    t0 = time.perf_counter()
+    alerts = 0
+    for _ in range(steps):
+        alerts += step()
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    return {"config": 2, "metric": "events/sec (keyed ValueState counter, 10k keys)",
+            "value": batch * steps / dt, "unit": "events/s", "ms_per_step": dt / steps * 1e3,
+            "alerts": alerts, "keys": keys, "events_per_step": batch, "device": str(dev)}
+
+
+def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_000,
+            device: str = "cuda") -> dict:
+    """Sliding 1 min / 10 s event-time window sum + 30 s allowed lateness, 10M keys; 5 % of
+    events arrive up to 40 s late (within lateness -> re-firings)."""
+    dev = torch.device(device)
+    span = 2_000
+    mbps = E.var(E.VAR_RESULT) * 8.0 / 60 / 1024 / 1024
+    op = KeyedWindowOperator(size=60_000, slide=10_000, lateness=30_000, agg=K.AGG_SUM_I64,
+                             device=dev, max_keys=keys, batch_capacity=batch, ooo_bound=5_000,
+                             map_prog=E.compile_expr(mbps),
+                             filter_prog=E.compile_expr(E.var(E.VAR_MAPPED) < 1e-4))
+    kt = torch.empty(batch, dtype=torch.int64, device=dev)
+    tt = torch.empty_like(kt)
+    vt = torch.empty_like(kt)
+    late_n = batch // 20
+    step_i = [0]
+    lat = []
+
+    def step():
+        t_in = time.perf_counter()
+        i = step_i[0]
+        K.gen_events(kt, tt, vt, seed=4, stream_id=0, idx0=i * batch, nkeys=keys,
+                     ts_base=i * span, ts_span=span, disorder=5_000, val_lo=0, val_span=20_000)
+        if i > 20:
+            tt[:late_n] -= 40_000  # late but (mostly) within the allowed lateness
+        fired = op.process(kt, tt, vt)
+        step_i[0] += 1
+        if fired:
+            lat.append((time.perf_counter() - t_in) * 1e3)
+        return sum(len(r.keys) for r in fired)
+
+    for _ in range(warmup):
+        step()
+    _sync(dev)
+    lat.clear()
+    t0 = time.perf_counter()
+    alerts = 0
+    for _ in range(steps):
+        alerts += step()
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    return {"config": 4, "metric": "events/sec (sliding 1min/10s + lateness, 10M keys)",
+            "value": batch * steps / dt, "unit": "events/s", "ms_per_step": dt / steps * 1e3,
+            "p50_alert_latency_ms": statistics.median(lat) if lat else None, "alerts": alerts,
+            "late_dropped": op.metrics.num_late_records_dropped, "keys": keys,
+            "events_per_step": batch, "state_bytes": op.state_bytes(), "device": str(dev)}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 4])
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--device", default="cuda")
+    a = ap.parse_args(argv)
+    if a.config == 1:
+        r = config1(a.steps, a.warmup, a.batch or (1 << 20))
+    elif a.config == 2:
+        r = config2(a.steps, a.warmup, a.batch or (1 << 24), device=a.device)
+    else:
+        r = config4(a.steps, a.warmup, a.batch or (1 << 24), device=a.device)
+    print(json.dumps(r), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

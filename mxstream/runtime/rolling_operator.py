@@ -1,0 +1,182 @@
+"""Keyed rolling state operator: ``keyBy(..).max/min/sum/reduce`` and keyed ValueState counters
+with a per-record emission of the post-update value (StreamGroupedReduce semantics,
+ComputeCpuMax.java:26; BASELINE config 2 "keyed ValueState counter").
+
+Per micro-batch and rank: partition by key group (window_mode 0) -> RCCL all-to-all ->
+rolling pass. GPU: rolling_lookup (HBM hash table insert/find, 64-bit sort keys
+slot|src|arrival) -> one radix sort -> rolling_heads -> rolling_scan (one wave per key,
+ordered shuffle scan seeded by the stored state, fused filter, compacted rows). CPU: the
+sequential twin ``rolling_rows``. Output rows are in per-key arrival order.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from ..ops import expr as E
+from ..ops import kernels as K
+from ..ops.native import load
+from ..parallel.comm import Comm, LocalComm
+
+I64_MIN, I64_MAX = K.I64_MIN, K.I64_MAX
+
+
+def _next_pow2(x: int) -> int:
+    return 1 << max(0, int(x - 1).bit_length())
+
+
+@dataclass
+class RollingRows:
+    keys: np.ndarray   # uint64
+    values: np.ndarray  # int64 raw (f64 bit pattern for float aggregates; count for COUNT)
+    tags: np.ndarray   # int64: src rank << 32 | index in that rank's batch
+
+
+class KeyedRollingOperator:
+    def __init__(self, *, agg: int, device="cpu", comm: Comm | None = None,
+                 max_keys: int = 1 << 16, parallelism: int | None = None,
+                 max_parallelism: int = 128, batch_capacity: int = 1 << 20,
+                 cap_log2: int = 12, filter_prog: E.Program = E.EMPTY, emit_capacity: int | None = None):
+        self.device = torch.device(device)
+        self.comm = comm or LocalComm()
+        self.world, self.rank = self.comm.world, self.comm.rank
+        self.agg = agg
+        if agg in (K.AGG_AVG_F64, K.AGG_AVG_I64):
+            raise ValueError("rolling avg is not a Flink rolling aggregate")
+        self.parallelism = parallelism or self.world
+        self.max_parallelism = max_parallelism
+        self.filter_prog = filter_prog
+        per_rank = int(max_keys / self.world * (1.3 if self.world > 1 else 1.0)) + 1024
+        self.cap_log2 = cap_log2
+        cap = 1 << cap_log2
+        load_f = 0.7 if cap_log2 >= 12 else 0.5
+        self.nsub = _next_pow2(max(1, math.ceil(per_rank / (cap * load_f))))
+        self.nsub_log2 = self.nsub.bit_length() - 1
+        self.nslots = self.nsub << cap_log2
+        dev = self.device
+        self.keys_g = torch.full((self.nslots,), -1, dtype=torch.int64, device=dev)
+        self.acc_g = torch.zeros(self.nslots, dtype=torch.int64, device=dev)
+        self.cnt_g = torch.zeros(self.nslots, dtype=torch.int32, device=dev)
+        self.flags = torch.zeros(4, dtype=torch.int32, device=dev)
+        kgd = [(kg * self.parallelism // max_parallelism) * self.world // self.parallelism
+               for kg in range(max_parallelism)]
+        self.kg_dest = torch.tensor(kgd, dtype=torch.int32, device=dev)
+        self.nbuckets = self.world << self.nsub_log2
+        self.stats = K.new_stats(dev)
+        self.local_maxts = torch.full((1,), I64_MIN, dtype=torch.int64, device=dev)
+        self.red = torch.zeros(K.RED_WORDS, dtype=torch.int64, device=dev)
+        self.emit_capacity = emit_capacity
+        self._alloc(batch_capacity)
+        self.steps = 0
+        self.records_in = 0
+
+    def _alloc(self, batch_capacity: int, slack: float = 1.5):
+        self.batch_capacity = int(batch_capacity)
+        self.slack = slack
+        per = self.batch_capacity / self.nbuckets
+        nblk = min(1024, max(1, -(-self.batch_capacity // 65536)))
+        cap = int(per * slack + 6 * math.sqrt(max(per, 1.0)) + 64) + 8 * nblk
+        self.bucket_cap = (cap + 7) & ~7
+        words = self.nbuckets * self.bucket_cap * K.REC_WORDS
+        dev = self.device
+        self.send = torch.empty(words, dtype=torch.int64, device=dev)
+        self.recv = torch.empty(words, dtype=torch.int64, device=dev) if self.world > 1 else self.send
+        self.cursor = torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
+        self.recv_counts = (torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
+                            if self.world > 1 else self.cursor)
+        total = self.nbuckets * self.bucket_cap
+        self.sort_key = torch.empty(total, dtype=torch.int64, device=dev)
+        self.vals_buf = torch.empty(total, dtype=torch.int64, device=dev)
+        self.heads = torch.empty(total, dtype=torch.int32, device=dev)
+        self.n_buf = torch.zeros(2, dtype=torch.int32, device=dev)
+        ocap = self.emit_capacity or total
+        self.out_key = torch.empty(ocap, dtype=torch.int64, device=dev)
+        self.out_val = torch.empty(ocap, dtype=torch.int64, device=dev)
+        self.out_tag = torch.empty(ocap, dtype=torch.int64, device=dev)
+        self.out_n = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def process(self, keys: torch.Tensor, vals: torch.Tensor, to_host: bool = True):
+        """Update state with one micro-batch; returns the emitted rows (host) or the device count."""
+        n = keys.numel()
+        if n > self.batch_capacity:
+            self._alloc(n, self.slack)
+        dummy_ts = self._dummy_ts(n)  # keyed (non-windowed) records carry no timestamp
+        while True:
+            K.step_begin(self.cursor, self.stats)
+            plan = K.PartitionPlan(max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2,
+                                   nranks=self.world, window_mode=0, drop_late=0, hash_mode=0,
+                                   bucket_cap=self.bucket_cap, pane=1)
+            if n:
+                K.partition(keys, dummy_ts, vals, plan, self.kg_dest, self.cursor, self.send,
+                            self.stats)
+            K.step_finish(self.stats, self.local_maxts, self.red, bound=0, event_mode=True,
+                          proc_now=0)
+            self.comm.allreduce_min_(self.red[3:4])
+            if self.world > 1:
+                self.comm.all_to_all(self.recv, self.send)
+                self.comm.all_to_all(self.recv_counts, self.cursor)
+            if int(self.red[3].item()):
+                self._alloc(self.batch_capacity, self.slack * 2)
+                continue
+            break
+        self.records_in += n
+        self.steps += 1
+        self.out_n.zero_()
+        m = load()
+        code, consts = self.filter_prog.as_args()
+        cap = self.out_key.numel()
+        if self.device.type == "cuda":
+            st = torch.cuda.current_stream(self.device).cuda_stream
+            self.n_buf.zero_()
+            m.gpu_rolling_lookup(self.recv.data_ptr(), self.recv_counts.data_ptr(), self.world,
+                                 self.nsub, self.bucket_cap, self.cap_log2, self.keys_g.data_ptr(),
+                                 self.sort_key.data_ptr(), self.vals_buf.data_ptr(),
+                                 self.n_buf.data_ptr(), self.flags.data_ptr(), st)
+            total = int(self.n_buf[0].item())
+            if total:
+                sk, perm = torch.sort(self.sort_key[:total])
+                sk = sk.contiguous()
+                perm = perm.contiguous()
+                n_in = self.n_buf[0:1]
+                m.gpu_rolling_heads(sk.data_ptr(), n_in.data_ptr(), total,
+                                    self.heads.data_ptr(), self.n_buf[1:2].data_ptr(), st)
+                m.gpu_rolling_scan(self.agg, sk.data_ptr(), perm.data_ptr(),
+                                   self.vals_buf.data_ptr(), n_in.data_ptr(), self.heads.data_ptr(),
+                                   self.n_buf[1:2].data_ptr(), min(total, self.nslots),
+                                   self.acc_g.data_ptr(), self.cnt_g.data_ptr(),
+                                   self.keys_g.data_ptr(), code, consts, self.out_key.data_ptr(),
+                                   self.out_val.data_ptr(), self.out_tag.data_ptr(),
+                                   self.out_n.data_ptr(), cap, st)
+        else:
+            m.cpu_rolling_rows(self.recv.data_ptr(), self.recv_counts.data_ptr(), self.world,
+                               self.nsub, self.bucket_cap, self.cap_log2, self.agg,
+                               self.keys_g.data_ptr(), self.acc_g.data_ptr(),
+                               self.cnt_g.data_ptr(), self.flags.data_ptr(), code, consts,
+                               self.out_key.data_ptr(), self.out_val.data_ptr(),
+                               self.out_tag.data_ptr(), self.out_n.data_ptr(), cap)
+        if not to_host:
+            return self.out_n
+        k = int(self.out_n.item())
+        k = min(k, cap)
+        return RollingRows(self.out_key[:k].cpu().numpy().copy().view(np.uint64),
+                           self.out_val[:k].cpu().numpy().copy(),
+                           self.out_tag[:k].cpu().numpy().copy())
+
+    def _dummy_ts(self, n: int) -> torch.Tensor:
+        t = getattr(self, "_ts0", None)
+        if t is None or t.numel() < n:
+            t = torch.zeros(max(n, 1), dtype=torch.int64, device=self.device)
+            self._ts0 = t
+        return t[:n]
+
+    def state_of(self, key: int):
+        """Current (value, count) of a key (host lookup, tests/inspection)."""
+        keys = self.keys_g.cpu().numpy()
+        idx = np.nonzero(keys == np.int64(key))[0]
+        if not len(idx):
+            return None
+        i = int(idx[0])
+        return int(self.acc_g[i].item()), int(self.cnt_g[i].item())
