@@ -901,22 +901,27 @@ __device__ __forceinline__ uint32_t global_probe_insert(uint64_t* keys, uint64_t
   return kNoSlot;
 }
 
+constexpr uint32_t kLookupChunk = 8192;  // records per workgroup (grid = buckets x chunks)
+
 __global__ __launch_bounds__(256) void rolling_lookup_kernel(
     const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
     uint32_t bucket_cap, int cap_log2, uint64_t* __restrict__ keys_g,
     int64_t* __restrict__ sort_key, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
     uint32_t* __restrict__ flags) {
-  const int b = blockIdx.x;  // = src * nsub + sub
+  const int b = blockIdx.y;  // = src * nsub + sub
   const int src = b / nsub, sub = b % nsub;
   uint32_t c = counts[b];
   c = c < bucket_cap ? c : bucket_cap;
+  const uint32_t lo = blockIdx.x * kLookupChunk;
+  if (lo >= c) return;  // whole workgroup exits together
+  const uint32_t hi = lo + kLookupChunk < c ? lo + kLookupChunk : c;
   const Rec* seg = recs + (size_t)b * bucket_cap;
   __shared__ uint32_t base;
-  if (threadIdx.x == 0) base = c ? atomicAdd(n_out, c) : 0u;
+  if (threadIdx.x == 0) base = atomicAdd(n_out, hi - lo);
   __syncthreads();
   uint64_t* keys = keys_g + ((size_t)sub << cap_log2);
   const uint32_t mask = (1u << cap_log2) - 1;
-  for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
+  for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
     const Rec r = seg[e];
     int64_t sk = INT64_MAX;  // holes and overflow sort last and are ignored
     if (r.t != 0xFFFFFFFFu) {
@@ -928,8 +933,8 @@ __global__ __launch_bounds__(256) void rolling_lookup_kernel(
         sk = (int64_t)((slot << 40) | ((uint64_t)src << 32) | r.aux);
       }
     }
-    sort_key[base + e] = sk;
-    vals_out[base + e] = r.val;
+    sort_key[base + (e - lo)] = sk;
+    vals_out[base + (e - lo)] = r.val;
   }
 }
 
@@ -1221,7 +1226,9 @@ void rolling_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
                     uint32_t bucket_cap, int cap_log2, uint64_t* keys_g, int64_t* sort_key,
                     uint64_t* vals_out, uint32_t* n_out, uint32_t* flags, intptr_t stream) {
   if (nsrc * nsub <= 0) return;
-  hipLaunchKernelGGL(rolling_lookup_kernel, dim3(nsrc * nsub), dim3(256), 0, (hipStream_t)stream,
+  const uint32_t chunks = (bucket_cap + kLookupChunk - 1) / kLookupChunk;
+  hipLaunchKernelGGL(rolling_lookup_kernel, dim3(chunks, nsrc * nsub), dim3(256), 0,
+                     (hipStream_t)stream,
                      recs, counts, nsrc, nsub, bucket_cap, cap_log2, keys_g, sort_key, vals_out,
                      n_out, flags);
   HIP_CHECK(hipGetLastError());

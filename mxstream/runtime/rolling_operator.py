@@ -39,7 +39,7 @@ class KeyedRollingOperator:
     def __init__(self, *, agg: int, device="cpu", comm: Comm | None = None,
                  max_keys: int = 1 << 16, parallelism: int | None = None,
                  max_parallelism: int = 128, batch_capacity: int = 1 << 20,
-                 cap_log2: int = 12, filter_prog: E.Program = E.EMPTY, emit_capacity: int | None = None):
+                 cap_log2: int | None = None, filter_prog: E.Program = E.EMPTY, emit_capacity: int | None = None):
         self.device = torch.device(device)
         self.comm = comm or LocalComm()
         self.world, self.rank = self.comm.world, self.comm.rank
@@ -49,11 +49,10 @@ class KeyedRollingOperator:
         self.parallelism = parallelism or self.world
         self.max_parallelism = max_parallelism
         self.filter_prog = filter_prog
-        per_rank = int(max_keys / self.world * (1.3 if self.world > 1 else 1.0)) + 1024
-        self.cap_log2 = cap_log2
-        cap = 1 << cap_log2
-        load_f = 0.7 if cap_log2 >= 12 else 0.5
-        self.nsub = _next_pow2(max(1, math.ceil(per_rank / (cap * load_f))))
+        from .geometry import state_geometry
+
+        self.nsub, self.cap_log2 = state_geometry(max_keys, self.world, cap_log2)
+        cap_log2 = self.cap_log2
         self.nsub_log2 = self.nsub.bit_length() - 1
         self.nslots = self.nsub << cap_log2
         dev = self.device

@@ -87,7 +87,7 @@ class KeyedWindowOperator:
                  hash_mode: int = 0, jhash_table: torch.Tensor | None = None,
                  map_prog: E.Program = E.EMPTY, filter_prog: E.Program = E.EMPTY,
                  batch_capacity: int = 1 << 20, bucket_slack: float = 1.5,
-                 cap_log2: int = 12, time_mode: str = "event", ooo_bound: int = 0,
+                 cap_log2: int | None = None, time_mode: str = "event", ooo_bound: int = 0,
                  side_output_late: bool = False, late_capacity: int = 1 << 16,
                  clock: Callable[[], int] | None = None, external_watermark: bool = False):
         self.device = torch.device(device)
@@ -118,14 +118,10 @@ class KeyedWindowOperator:
         self.metrics = OperatorMetrics()
 
         # ---- state geometry ----
-        # Keys per rank: key groups spread keys unevenly over ranks, so leave 30 % headroom.
-        per_rank = int(max_keys / self.world * (1.3 if self.world > 1 else 1.0)) + 1024
-        self.cap_log2 = cap_log2
-        cap = 1 << cap_log2
-        # Linear probing in LDS stays cheap up to ~0.7 load (2.2 probes per hit); small tables
-        # keep 0.5 for headroom against binomial imbalance between sub-tables.
-        load = 0.7 if cap_log2 >= 12 else 0.5
-        self.nsub = _next_pow2(max(1, math.ceil(per_rank / (cap * load))))
+        from .geometry import state_geometry
+
+        self.nsub, self.cap_log2 = state_geometry(max_keys, self.world, cap_log2)
+        cap_log2 = self.cap_log2
         self.nsub_log2 = self.nsub.bit_length() - 1
         if self.nsub * self.world > 16384:
             raise ValueError("key space too large for the bucket histogram; raise cap_log2")
