@@ -230,6 +230,78 @@ PYBIND11_MODULE(_mxs_native, m) {
                       P<uint64_t>(ok), P<uint64_t>(ov), P<int64_t>(ot), P<uint32_t>(on), out_cap,
                       stream);
   });
+  m.def("gpu_session_lookup", [](intptr_t recs, intptr_t counts, int nsrc, int nsub, uint32_t bcap,
+                                 int cap_log2, intptr_t keys_g, intptr_t spill_set,
+                                 uint32_t spill_mask, int spill_any, intptr_t sk, intptr_t vals,
+                                 intptr_t n_out, intptr_t host_recs, intptr_t n_host,
+                                 uint32_t host_cap, intptr_t n_ins, intptr_t stream) {
+    gpu::session_lookup(P<Rec>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2,
+                        P<uint64_t>(keys_g), P<uint64_t>(spill_set), spill_mask, spill_any,
+                        P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_out), P<Rec>(host_recs),
+                        P<uint32_t>(n_host), host_cap, P<uint32_t>(n_ins), stream);
+  });
+  m.def("gpu_session_heads", [](intptr_t sk, intptr_t n_in, int64_t n_cap, intptr_t heads,
+                                intptr_t n_heads, intptr_t stream) {
+    gpu::session_heads(P<int64_t>(sk), P<uint32_t>(n_in), n_cap, P<uint32_t>(heads),
+                       P<uint32_t>(n_heads), stream);
+  });
+  m.def("gpu_session_merge", [](intptr_t sk, intptr_t perm, intptr_t vals, intptr_t n_in,
+                                intptr_t heads, intptr_t n_heads, int64_t max_segments, int64_t gap,
+                                int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
+                                int64_t nslots, intptr_t s_start, intptr_t s_end, intptr_t s_acc,
+                                intptr_t s_cnt, intptr_t s_flags, intptr_t slot_due,
+                                intptr_t slot_last, intptr_t late_cnt, intptr_t ovf_slots,
+                                intptr_t n_ovf, intptr_t ovf_rows, intptr_t n_ovf_runs,
+                                uint32_t ovf_cap, intptr_t stream) {
+    gpu::session_merge(P<int64_t>(sk), P<int64_t>(perm), P<uint64_t>(vals), P<uint32_t>(n_in),
+                       P<uint32_t>(heads), P<uint32_t>(n_heads), max_segments, gap, lateness, wm,
+                       tbase, agg, cap_log2, nslots, P<int64_t>(s_start), P<int64_t>(s_end),
+                       P<uint64_t>(s_acc), P<uint32_t>(s_cnt), P<uint32_t>(s_flags),
+                       P<int64_t>(slot_due), P<int64_t>(slot_last), P<uint64_t>(late_cnt),
+                       P<int64_t>(ovf_slots), P<uint32_t>(n_ovf), P<int64_t>(ovf_rows),
+                       P<uint32_t>(n_ovf_runs), ovf_cap, stream);
+  });
+  m.def("gpu_session_fire", [](int64_t gap, int64_t lateness, int64_t wm, int agg, int cap_log2,
+                               int64_t nslots, intptr_t keys_g, intptr_t s_start, intptr_t s_end,
+                               intptr_t s_acc, intptr_t s_cnt, intptr_t s_flags, intptr_t slot_due,
+                               std::vector<int32_t> mc, std::vector<double> mk,
+                               std::vector<int32_t> fc, std::vector<double> fk, intptr_t ok,
+                               intptr_t os, intptr_t oe, intptr_t ov, intptr_t oraw, intptr_t oc,
+                               intptr_t on, uint32_t out_cap, intptr_t stream) {
+    gpu::session_fire(gap, lateness, wm, agg, cap_log2, nslots, P<uint64_t>(keys_g),
+                      P<int64_t>(s_start), P<int64_t>(s_end), P<uint64_t>(s_acc),
+                      P<uint32_t>(s_cnt), P<uint32_t>(s_flags), P<int64_t>(slot_due),
+                      make_prog(mc, mk), make_prog(fc, fk), P<uint64_t>(ok), P<int64_t>(os),
+                      P<int64_t>(oe), P<double>(ov), P<uint64_t>(oraw), P<uint32_t>(oc),
+                      P<uint32_t>(on), out_cap, stream);
+  });
+  m.def("gpu_session_evict", [](int64_t nslots, int cap_log2, intptr_t keys_g, intptr_t s_start,
+                                intptr_t s_end, intptr_t s_acc, intptr_t s_cnt, intptr_t s_flags,
+                                intptr_t slot_due, intptr_t slot_last, int64_t idle_before,
+                                intptr_t slots, uint32_t nslots_list, intptr_t spill_set,
+                                uint32_t spill_mask, intptr_t st_key, intptr_t st_start,
+                                intptr_t st_end, intptr_t st_acc, intptr_t st_cnt,
+                                intptr_t st_flags, intptr_t n_rows, uint32_t row_cap,
+                                intptr_t n_evicted, intptr_t stream) {
+    gpu::session_evict(nslots, cap_log2, P<uint64_t>(keys_g), P<int64_t>(s_start),
+                       P<int64_t>(s_end), P<uint64_t>(s_acc), P<uint32_t>(s_cnt),
+                       P<uint32_t>(s_flags), P<int64_t>(slot_due), P<int64_t>(slot_last),
+                       idle_before, P<int64_t>(slots), nslots_list, P<uint64_t>(spill_set),
+                       spill_mask, P<int64_t>(st_key), P<int64_t>(st_start), P<int64_t>(st_end),
+                       P<int64_t>(st_acc), P<int64_t>(st_cnt), P<int64_t>(st_flags),
+                       P<uint32_t>(n_rows), row_cap, P<uint32_t>(n_evicted), stream);
+  });
+  m.def("gpu_session_rehash", [](int64_t nslots, int cap_log2, intptr_t ko, intptr_t so,
+                                 intptr_t eo, intptr_t ao, intptr_t co, intptr_t fo, intptr_t dout,
+                                 intptr_t lo, intptr_t kn, intptr_t sn, intptr_t en, intptr_t an,
+                                 intptr_t cn, intptr_t fn, intptr_t dn, intptr_t ln, intptr_t ins,
+                                 intptr_t stream) {
+    gpu::session_rehash(nslots, cap_log2, P<uint64_t>(ko), P<int64_t>(so), P<int64_t>(eo),
+                        P<uint64_t>(ao), P<uint32_t>(co), P<uint32_t>(fo), P<int64_t>(dout),
+                        P<int64_t>(lo), P<uint64_t>(kn), P<int64_t>(sn), P<int64_t>(en),
+                        P<uint64_t>(an), P<uint32_t>(cn), P<uint32_t>(fn), P<int64_t>(dn),
+                        P<int64_t>(ln), P<uint32_t>(ins), stream);
+  });
   m.def("gpu_expr_filter", [](intptr_t x, int64_t n, std::vector<int32_t> code,
                               std::vector<double> consts, intptr_t keep, intptr_t stream) {
     gpu::expr_filter(P<double>(x), n, make_prog(code, consts), P<uint8_t>(keep), stream);
@@ -305,4 +377,5 @@ PYBIND11_MODULE(_mxs_native, m) {
   });
 
   bind_runtime(m);
+  bind_sessions(m);
 }

@@ -1042,6 +1042,529 @@ __global__ __launch_bounds__(256) void rolling_scan_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Session windows on the GPU (BASELINE config 5). Per key slot: up to kSess sessions (SoA:
+// start, end, acc, cnt, flags) + due time (min over sessions of maxTs, or cleanup time once
+// fired) + last activity (LRU for the host-DRAM spill). Keys evicted to host DRAM are recorded
+// in a device spill set; their records are diverted to the host SessionStore (csrc/sessions.cpp).
+// ------------------------------------------------------------------------------------------
+constexpr int kSess = 4;
+constexpr uint64_t kTombKey = ~1ull;  // evicted slot (probing continues past it)
+
+struct SessArgs {
+  int64_t gap, lateness, wm, tbase;
+  int32_t agg, cap_log2;
+  int64_t nslots;
+};
+
+__device__ __forceinline__ bool set_contains(const uint64_t* set, uint32_t mask, uint64_t key) {
+  uint32_t s = (uint32_t)(mix64(key) >> 32) & mask;
+  for (uint32_t i = 0; i <= mask; ++i) {
+    const uint64_t k = set[s];
+    if (k == key) return true;
+    if (k == kEmptyKey) return false;
+    s = (s + 1) & mask;
+  }
+  return false;
+}
+
+__device__ __forceinline__ void set_insert(uint64_t* set, uint32_t mask, uint64_t key) {
+  uint32_t s = (uint32_t)(mix64(key) >> 32) & mask;
+  for (uint32_t i = 0; i <= mask; ++i) {
+    const uint64_t prev = atomicCAS((unsigned long long*)&set[s], (unsigned long long)kEmptyKey,
+                                    (unsigned long long)key);
+    if (prev == kEmptyKey || prev == key) return;
+    s = (s + 1) & mask;
+  }
+}
+
+// Insert-or-find with tombstone reuse. Linear-probing invariant: a key sits before the first
+// empty slot of its chain, so the probe runs to the key or the first empty slot and claims the
+// first tombstone seen on the way (else that empty slot). A lost CAS means another key was
+// inserted there: restart (each restart is someone else's progress). `inserted` counts claimed
+// empty slots only (tombstone reuse does not shorten the empty-slot budget).
+__device__ __forceinline__ uint32_t sess_probe_insert(uint64_t* keys, uint64_t key, uint32_t mask,
+                                                      uint32_t* inserted) {
+  const uint32_t s0 = (uint32_t)mix64(key) & mask;
+  for (;;) {
+    uint32_t s = s0, tomb = kNoSlot, target = kNoSlot;
+    for (uint32_t i = 0; i <= mask; ++i) {
+      const uint64_t k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (k == key) return s;
+      if (k == kTombKey) {
+        if (tomb == kNoSlot) tomb = s;
+      } else if (k == kEmptyKey) {
+        target = s;
+        break;
+      }
+      s = (s + 1) & mask;
+    }
+    const bool use_tomb = tomb != kNoSlot;
+    if (use_tomb) target = tomb;
+    if (target == kNoSlot) return kNoSlot;  // full: no empty slot, no tombstone
+    const uint64_t expect = use_tomb ? kTombKey : kEmptyKey;
+    const uint64_t prev = atomicCAS((unsigned long long*)&keys[target], (unsigned long long)expect,
+                                    (unsigned long long)key);
+    if (prev == expect) {
+      if (!use_tomb) atomicAdd(inserted, 1u);
+      return target;
+    }
+    if (prev == key) return target;
+  }
+}
+
+__global__ __launch_bounds__(256) void session_lookup_kernel(
+    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
+    uint32_t bucket_cap, int cap_log2, uint64_t* __restrict__ keys_g,
+    uint64_t* __restrict__ spill_set, uint32_t spill_mask, int32_t spill_any,
+    int64_t* __restrict__ sort_key, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
+    Rec* __restrict__ host_recs, uint32_t* __restrict__ n_host, uint32_t host_cap,
+    uint32_t* __restrict__ n_inserted) {
+  const int b = blockIdx.y;
+  const int sub = b % nsub;
+  uint32_t c = counts[b];
+  c = c < bucket_cap ? c : bucket_cap;
+  const uint32_t lo = blockIdx.x * kLookupChunk;
+  if (lo >= c) return;
+  const uint32_t hi = lo + kLookupChunk < c ? lo + kLookupChunk : c;
+  const Rec* seg = recs + (size_t)b * bucket_cap;
+  __shared__ uint32_t base;
+  if (threadIdx.x == 0) base = atomicAdd(n_out, hi - lo);
+  __syncthreads();
+  uint64_t* keys = keys_g + ((size_t)sub << cap_log2);
+  const uint32_t mask = (1u << cap_log2) - 1;
+  for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
+    const Rec r = seg[e];
+    int64_t sk = INT64_MAX;
+    if (r.t != 0xFFFFFFFFu) {
+      bool to_host = spill_any && set_contains(spill_set, spill_mask, r.key);
+      uint32_t s = kNoSlot;
+      if (!to_host) {
+        s = sess_probe_insert(keys, r.key, mask, n_inserted);
+        if (s == kNoSlot) {  // sub-table full: the key lives in host DRAM from now on
+          to_host = true;
+          set_insert(spill_set, spill_mask, r.key);
+        }
+      }
+      if (to_host) {
+        const uint32_t q = atomicAdd(n_host, 1u);
+        if (q < host_cap) host_recs[q] = r;
+      } else {
+        const uint64_t slot = ((uint64_t)sub << cap_log2) | s;
+        sk = (int64_t)((slot << 32) | r.t);
+      }
+    }
+    sort_key[base + (e - lo)] = sk;
+    vals_out[base + (e - lo)] = r.val;
+  }
+}
+
+__global__ __launch_bounds__(256) void session_heads_kernel(const int64_t* __restrict__ sk,
+                                                            const uint32_t* __restrict__ n_in,
+                                                            uint32_t* __restrict__ heads,
+                                                            uint32_t* __restrict__ n_heads) {
+  const uint32_t n = *n_in;
+  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    const uint32_t i = base + threadIdx.x;
+    bool h = false;
+    if (i < n) {
+      const int64_t k = sk[i];
+      h = k != INT64_MAX && (i == 0 || (sk[i - 1] >> 32) != (k >> 32));
+    }
+    const unsigned long long m = __ballot(h);
+    uint32_t wb = 0;
+    if (lane_id() == 0 && m) wb = atomicAdd(n_heads, (uint32_t)__popcll(m));
+    wb = __shfl(wb, 0);
+    if (h) heads[wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = i;
+  }
+}
+
+struct SessState {
+  int64_t start[kSess], end[kSess];
+  uint64_t acc[kSess];
+  uint32_t cnt[kSess], flags[kSess];
+  int n;
+};
+
+// Merge candidate run (cs, ce, ca, cc) into the slot's sessions (lane-local, kSess unrolled).
+// Returns: 0 merged/inserted, 1 late-dropped, 2 overflow (more than kSess sessions).
+__device__ __forceinline__ int sess_merge(SessState& st, int64_t cs, int64_t ce, uint64_t ca,
+                                          uint32_t cc, const SessArgs& a) {
+  int64_t ms = cs, me = ce;
+  uint64_t macc = ca;
+  uint32_t mcnt = cc, mflags = 0;
+  bool touched = false;
+  SessState rest;
+  rest.n = 0;
+#pragma unroll
+  for (int j = 0; j < kSess; ++j) {
+    if (j >= st.n) break;
+    if (ms <= st.end[j] && me >= st.start[j]) {
+      ms = ms < st.start[j] ? ms : st.start[j];
+      me = me > st.end[j] ? me : st.end[j];
+      macc = agg_combine(a.agg, st.acc[j], macc);
+      mcnt += st.cnt[j];
+      mflags |= st.flags[j];
+      touched = true;
+    } else {
+      const int q = rest.n++;
+      rest.start[q] = st.start[j];
+      rest.end[q] = st.end[j];
+      rest.acc[q] = st.acc[j];
+      rest.cnt[q] = st.cnt[j];
+      rest.flags[q] = st.flags[j];
+    }
+  }
+  if (!touched && (me - 1) + a.lateness <= a.wm) return 1;
+  if (rest.n >= kSess) return 2;
+  if (mflags & 1u) mflags |= 2u;
+  const int q = rest.n++;
+  rest.start[q] = ms;
+  rest.end[q] = me;
+  rest.acc[q] = macc;
+  rest.cnt[q] = mcnt;
+  rest.flags[q] = mflags;
+  st = rest;
+  return 0;
+}
+
+__device__ __forceinline__ int64_t sess_due(const SessState& st, int64_t lateness) {
+  int64_t t = INT64_MAX;
+#pragma unroll
+  for (int j = 0; j < kSess; ++j) {
+    if (j >= st.n) break;
+    const int64_t maxts = st.end[j] - 1;
+    const int64_t due = ((st.flags[j] & 1u) && !(st.flags[j] & 2u)) ? maxts + lateness : maxts;
+    t = due < t ? due : t;
+  }
+  return t;
+}
+
+__device__ __forceinline__ void sess_load(SessState& st, int64_t slot, int64_t nslots,
+                                          const int64_t* s_start, const int64_t* s_end,
+                                          const uint64_t* s_acc, const uint32_t* s_cnt,
+                                          const uint32_t* s_flags) {
+  st.n = 0;
+#pragma unroll
+  for (int j = 0; j < kSess; ++j) {
+    const size_t gi = (size_t)j * nslots + slot;
+    const uint32_t c = s_cnt[gi];
+    if (c) {
+      const int q = st.n++;
+      st.start[q] = s_start[gi];
+      st.end[q] = s_end[gi];
+      st.acc[q] = s_acc[gi];
+      st.cnt[q] = c;
+      st.flags[q] = s_flags[gi];
+    }
+  }
+}
+
+__device__ __forceinline__ void sess_store(const SessState& st, int64_t slot, int64_t nslots,
+                                           int64_t* s_start, int64_t* s_end, uint64_t* s_acc,
+                                           uint32_t* s_cnt, uint32_t* s_flags) {
+#pragma unroll
+  for (int j = 0; j < kSess; ++j) {
+    const size_t gi = (size_t)j * nslots + slot;
+    if (j < st.n) {
+      s_start[gi] = st.start[j];
+      s_end[gi] = st.end[j];
+      s_acc[gi] = st.acc[j];
+      s_cnt[gi] = st.cnt[j];
+      s_flags[gi] = st.flags[j];
+    } else {
+      s_cnt[gi] = 0;
+    }
+  }
+}
+
+// One wave per key segment (sorted by slot, then ts): lanes find the runs of their 64-record
+// chunk (ts gaps > gap split runs) and their accumulators with shuffles; lane 0 merges the runs
+// into the slot's sessions in ts order.
+__global__ __launch_bounds__(256) void session_merge_kernel(
+    const int64_t* __restrict__ sk, const int64_t* __restrict__ perm,
+    const uint64_t* __restrict__ vals, const uint32_t* __restrict__ n_in,
+    const uint32_t* __restrict__ heads, const uint32_t* __restrict__ n_heads, SessArgs a,
+    int64_t* __restrict__ s_start, int64_t* __restrict__ s_end, uint64_t* __restrict__ s_acc,
+    uint32_t* __restrict__ s_cnt, uint32_t* __restrict__ s_flags, int64_t* __restrict__ slot_due,
+    int64_t* __restrict__ slot_last, uint64_t* __restrict__ late_cnt,
+    int64_t* __restrict__ ovf_slots, uint32_t* __restrict__ n_ovf, int64_t* __restrict__ ovf_rows,
+    uint32_t* __restrict__ n_ovf_runs, uint32_t ovf_cap) {
+  const uint32_t n = *n_in, nh = *n_heads;
+  const int lane = lane_id();
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  for (uint32_t h = wave; h < nh; h += nwaves) {
+    const uint32_t start = heads[h];
+    const int64_t slot = sk[start] >> 32;
+    SessState st;
+    sess_load(st, slot, a.nslots, s_start, s_end, s_acc, s_cnt, s_flags);
+    uint64_t late = 0;
+    bool overflow = false;
+    int64_t last_ts = INT64_MIN;
+    // Lane 0's pending run: a run ending on a chunk's last lane may continue in the next chunk,
+    // so runs are committed only once the following run starts more than `gap` later.
+    bool pv = false;
+    int64_t ps = 0, pe = 0;
+    uint64_t pa = 0;
+    uint32_t pc = 0;
+    auto commit = [&]() {
+      const int res = overflow ? 2 : sess_merge(st, ps, pe, pa, pc, a);
+      if (res == 1) {
+        late += pc;
+      } else if (res == 2) {
+        // More than kSess live sessions: this run (and every later run of the key) goes to
+        // the host store, which takes the key over after the step.
+        overflow = true;
+        const uint32_t q = atomicAdd(n_ovf_runs, 1u);
+        if (q < ovf_cap) {
+          ovf_rows[q] = slot;
+          ovf_rows[ovf_cap + q] = ps;
+          ovf_rows[2 * (size_t)ovf_cap + q] = pe;
+          ovf_rows[3 * (size_t)ovf_cap + q] = (int64_t)pa;
+          ovf_rows[4 * (size_t)ovf_cap + q] = pc;
+        }
+      }
+    };
+    for (uint32_t b0 = start;; b0 += 64) {
+      const uint32_t i = b0 + lane;
+      const bool in = i < n && sk[i] != INT64_MAX && (sk[i] >> 32) == slot;
+      const unsigned long long inm = __ballot(in);
+      if (!inm) break;
+      const int64_t ts = in ? a.tbase + (int64_t)(uint32_t)(sk[i] & 0xFFFFFFFF) : 0;
+      const uint64_t v = in ? agg_lift(a.agg, vals[perm[i]]) : 0;
+      const int64_t prev_ts = __shfl_up(ts, 1);
+      const bool head = in && (lane == 0 || ts > prev_ts + a.gap);
+      // Segmented inclusive scan of (acc, cnt) over runs.
+      uint64_t acc = v;
+      uint32_t cnt = in ? 1u : 0u;
+      const unsigned long long hm = __ballot(head);
+      const unsigned long long below = hm & ((lane == 63) ? ~0ull : ((1ull << (lane + 1)) - 1ull));
+      const int run0 = 63 - __clzll(below);
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t ya = __shfl_up(acc, o);
+        const uint32_t yc = __shfl_up(cnt, o);
+        if (in && lane - o >= run0) {
+          acc = agg_combine(a.agg, ya, acc);
+          cnt += yc;
+        }
+      }
+      // Run ends: next lane is a head or out of range.
+      const bool next_head = __shfl_down(head ? 1 : 0, 1) != 0;
+      const bool next_in = __shfl_down(in ? 1 : 0, 1) != 0;
+      const bool run_end = in && (lane == 63 || !next_in || next_head);
+      const unsigned long long em = __ballot(run_end);
+      const int64_t chunk_last = __shfl(ts, 63 - __clzll(inm));
+      last_ts = chunk_last > last_ts ? chunk_last : last_ts;
+      // Lane 0 folds the chunk's runs in ts order (run ends ascending).
+      unsigned long long rem = em;
+      while (rem) {
+        const int e = __ffsll((long long)rem) - 1;
+        rem &= rem - 1;
+        const unsigned long long hb = hm & ((e == 63) ? ~0ull : ((1ull << (e + 1)) - 1ull));
+        const int r0 = 63 - __clzll(hb);
+        const int64_t cs = __shfl(ts, r0);
+        const int64_t ce = __shfl(ts, e) + a.gap;
+        const uint64_t ca = __shfl(acc, e);
+        const uint32_t cc = __shfl(cnt, e);
+        if (lane == 0) {
+          if (pv && cs <= pe) {  // continues the pending run across the chunk boundary
+            pe = ce > pe ? ce : pe;
+            pa = agg_combine(a.agg, pa, ca);
+            pc += cc;
+          } else {
+            if (pv) commit();
+            ps = cs;
+            pe = ce;
+            pa = ca;
+            pc = cc;
+            pv = true;
+          }
+        }
+      }
+      if (__popcll(inm) < 64) break;
+    }
+    if (lane == 0 && pv) commit();
+    if (lane == 0) {
+      sess_store(st, slot, a.nslots, s_start, s_end, s_acc, s_cnt, s_flags);
+      slot_due[slot] = sess_due(st, a.lateness);
+      if (last_ts > slot_last[slot]) slot_last[slot] = last_ts;
+      if (late) atomicAdd((unsigned long long*)late_cnt, (unsigned long long)late);
+      if (overflow) {
+        const uint32_t q = atomicAdd(n_ovf, 1u);
+        ovf_slots[q] = slot;  // host evicts these keys and re-merges their overflow runs
+      }
+    }
+  }
+}
+
+// Fire due sessions: one lane per slot whose due time has passed.
+__global__ __launch_bounds__(256) void session_fire_kernel(
+    SessArgs a, const uint64_t* __restrict__ keys_g, int64_t* __restrict__ s_start,
+    int64_t* __restrict__ s_end, uint64_t* __restrict__ s_acc, uint32_t* __restrict__ s_cnt,
+    uint32_t* __restrict__ s_flags, int64_t* __restrict__ slot_due, ExprProg map, ExprProg filt,
+    uint64_t* __restrict__ out_key, int64_t* __restrict__ out_start, int64_t* __restrict__ out_end,
+    double* __restrict__ out_val, uint64_t* __restrict__ out_raw, uint32_t* __restrict__ out_cnt,
+    uint32_t* __restrict__ out_n, uint32_t out_cap) {
+  extern __shared__ __attribute__((aligned(16))) double ssm[];
+  LdsCol vars{ssm + threadIdx.x, 256};
+  LdsCol stack{ssm + kExprVars * 256 + threadIdx.x, 256};
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < a.nslots;
+       base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t slot = base + threadIdx.x;
+    const bool due = slot < a.nslots && slot_due[slot] <= a.wm;
+    if (!__ballot(due)) continue;
+    SessState st;
+    st.n = 0;
+    if (due) sess_load(st, slot, a.nslots, s_start, s_end, s_acc, s_cnt, s_flags);
+    const uint64_t key = due ? keys_g[slot] : 0;
+#pragma unroll
+    for (int j = 0; j < kSess; ++j) {
+      bool emit = false;
+      double val = 0.0;
+      if (due && j < st.n) {
+        const int64_t maxts = st.end[j] - 1;
+        if (maxts <= a.wm && (!(st.flags[j] & 1u) || (st.flags[j] & 2u))) {
+          const double v0 = agg_result_f64(a.agg, st.acc[j], st.cnt[j]);
+          val = v0;
+          emit = true;
+          if (map.ncode || filt.ncode) {
+            vars.set(0, v0);
+            vars.set(1, (double)st.cnt[j]);
+            vars.set(2, (double)st.start[j]);
+            vars.set(3, (double)st.end[j]);
+            vars.set(4, (double)key);
+            vars.set(5, (double)(int64_t)st.acc[j]);
+            if (map.ncode) val = expr_eval_t(map, stack, vars);
+            vars.set(6, val);
+            if (filt.ncode) emit = expr_eval_t(filt, stack, vars) != 0.0;
+          }
+          st.flags[j] = 1u;
+        }
+      }
+      const unsigned long long m = __ballot(emit);
+      if (m) {
+        uint32_t wb = 0;
+        if (lane_id() == 0) wb = atomicAdd(out_n, (uint32_t)__popcll(m));
+        wb = __shfl(wb, 0);
+        if (emit) {
+          const uint32_t q = wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+          if (q < out_cap) {
+            out_key[q] = key;
+            out_start[q] = st.start[j];
+            out_end[q] = st.end[j];
+            out_val[q] = val;
+            out_raw[q] = st.acc[j];
+            out_cnt[q] = st.cnt[j];
+          }
+        }
+      }
+    }
+    if (due) {
+      // Drop sessions past cleanup (maxTs + lateness <= wm).
+      SessState keep;
+      keep.n = 0;
+#pragma unroll
+      for (int j = 0; j < kSess; ++j) {
+        if (j < st.n && (st.end[j] - 1) + a.lateness > a.wm) {
+          const int q = keep.n++;
+          keep.start[q] = st.start[j];
+          keep.end[q] = st.end[j];
+          keep.acc[q] = st.acc[j];
+          keep.cnt[q] = st.cnt[j];
+          keep.flags[q] = st.flags[j];
+        }
+      }
+      sess_store(keep, slot, a.nslots, s_start, s_end, s_acc, s_cnt, s_flags);
+      slot_due[slot] = sess_due(keep, a.lateness);
+    }
+  }
+}
+
+// Evict (spill) slots idle since before `idle_before` (or listed in `slots`): pack their key and
+// sessions into staging rows, tombstone the slot and insert the key into the spill set.
+__global__ __launch_bounds__(256) void session_evict_kernel(
+    SessArgs a, uint64_t* __restrict__ keys_g, int64_t* __restrict__ s_start,
+    int64_t* __restrict__ s_end, uint64_t* __restrict__ s_acc, uint32_t* __restrict__ s_cnt,
+    uint32_t* __restrict__ s_flags, int64_t* __restrict__ slot_due,
+    int64_t* __restrict__ slot_last, int64_t idle_before, const int64_t* __restrict__ slots,
+    uint32_t nslots_list, uint64_t* __restrict__ spill_set, uint32_t spill_mask,
+    int64_t* __restrict__ st_key, int64_t* __restrict__ st_start, int64_t* __restrict__ st_end,
+    int64_t* __restrict__ st_acc, int64_t* __restrict__ st_cnt, int64_t* __restrict__ st_flags,
+    uint32_t* __restrict__ n_rows, uint32_t row_cap, uint32_t* __restrict__ n_evicted) {
+  const int64_t total = slots ? (int64_t)nslots_list : a.nslots;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t slot = slots ? slots[i] : i;
+    const uint64_t key = keys_g[slot];
+    if (key == kEmptyKey || key == kTombKey) continue;
+    if (!slots && slot_last[slot] >= idle_before) continue;
+    SessState st;
+    sess_load(st, slot, a.nslots, s_start, s_end, s_acc, s_cnt, s_flags);
+    if (st.n == 0) {  // no live session: free the slot, the key is not spilled
+      slot_due[slot] = INT64_MAX;
+      slot_last[slot] = INT64_MIN;
+      keys_g[slot] = kTombKey;
+      atomicAdd(n_evicted, 1u);
+      continue;
+    }
+    const uint32_t q = atomicAdd(n_rows, (uint32_t)st.n);
+    if (q + st.n > row_cap) continue;  // staging full: keep resident this round
+#pragma unroll
+    for (int j = 0; j < kSess; ++j) {
+      if (j < st.n) {
+        st_key[q + j] = (int64_t)key;
+        st_start[q + j] = st.start[j];
+        st_end[q + j] = st.end[j];
+        st_acc[q + j] = (int64_t)st.acc[j];
+        st_cnt[q + j] = st.cnt[j];
+        st_flags[q + j] = st.flags[j];
+      }
+    }
+    SessState empty;
+    empty.n = 0;
+    sess_store(empty, slot, a.nslots, s_start, s_end, s_acc, s_cnt, s_flags);
+    slot_due[slot] = INT64_MAX;
+    slot_last[slot] = INT64_MIN;
+    set_insert(spill_set, spill_mask, key);
+    keys_g[slot] = kTombKey;
+    atomicAdd(n_evicted, 1u);
+  }
+}
+
+// Rebuild the slot table without tombstones: every live slot is re-inserted into fresh arrays
+// (same sub-table, new position) with its sessions, due time and last activity.
+__global__ __launch_bounds__(256) void session_rehash_kernel(
+    SessArgs a, const uint64_t* __restrict__ keys_o, const int64_t* __restrict__ start_o,
+    const int64_t* __restrict__ end_o, const uint64_t* __restrict__ acc_o,
+    const uint32_t* __restrict__ cnt_o, const uint32_t* __restrict__ flags_o,
+    const int64_t* __restrict__ due_o, const int64_t* __restrict__ last_o,
+    uint64_t* __restrict__ keys_n, int64_t* __restrict__ start_n, int64_t* __restrict__ end_n,
+    uint64_t* __restrict__ acc_n, uint32_t* __restrict__ cnt_n, uint32_t* __restrict__ flags_n,
+    int64_t* __restrict__ due_n, int64_t* __restrict__ last_n, uint32_t* __restrict__ inserted) {
+  const uint32_t mask = (1u << a.cap_log2) - 1;
+  for (int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; slot < a.nslots;
+       slot += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys_o[slot];
+    if (key == kEmptyKey || key == kTombKey) continue;
+    const int64_t sub = slot >> a.cap_log2;
+    uint64_t* keys = keys_n + (sub << a.cap_log2);
+    const uint32_t s = sess_probe_insert(keys, key, mask, inserted);
+    const int64_t ns = (sub << a.cap_log2) | s;  // never kNoSlot: the old table held the key
+#pragma unroll
+    for (int j = 0; j < kSess; ++j) {
+      const size_t go = (size_t)j * a.nslots + slot, gn = (size_t)j * a.nslots + ns;
+      start_n[gn] = start_o[go];
+      end_n[gn] = end_o[go];
+      acc_n[gn] = acc_o[go];
+      cnt_n[gn] = cnt_o[go];
+      flags_n[gn] = flags_o[go];
+    }
+    due_n[ns] = due_o[slot];
+    last_n[ns] = last_o[slot];
+  }
+}
+
 int grid_for(int64_t n, int block, int max_blocks) {
   int64_t g = (n + block - 1) / block;
   if (g < 1) g = 1;
@@ -1266,6 +1789,103 @@ void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_
 #undef MXS_R
     default: throw std::runtime_error("rolling_scan: unsupported aggregate");
   }
+  HIP_CHECK(hipGetLastError());
+}
+
+
+static SessArgs make_sess_args(int64_t gap, int64_t lateness, int64_t wm, int64_t tbase, int agg,
+                               int cap_log2, int64_t nslots) {
+  SessArgs a;
+  a.gap = gap;
+  a.lateness = lateness;
+  a.wm = wm;
+  a.tbase = tbase;
+  a.agg = agg;
+  a.cap_log2 = cap_log2;
+  a.nslots = nslots;
+  return a;
+}
+
+void session_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bcap,
+                    int cap_log2, uint64_t* keys_g, uint64_t* spill_set, uint32_t spill_mask,
+                    int spill_any, int64_t* sk, uint64_t* vals, uint32_t* n_out, Rec* host_recs,
+                    uint32_t* n_host, uint32_t host_cap, uint32_t* n_inserted, intptr_t stream) {
+  if (nsrc * nsub <= 0) return;
+  const uint32_t chunks = (bcap + kLookupChunk - 1) / kLookupChunk;
+  hipLaunchKernelGGL(session_lookup_kernel, dim3(chunks, nsrc * nsub), dim3(256), 0,
+                     (hipStream_t)stream, recs, counts, nsrc, nsub, bcap, cap_log2, keys_g,
+                     spill_set, spill_mask, spill_any, sk, vals, n_out, host_recs, n_host,
+                     host_cap, n_inserted);
+  HIP_CHECK(hipGetLastError());
+}
+
+void session_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
+                   uint32_t* n_heads, intptr_t stream) {
+  hipLaunchKernelGGL(session_heads_kernel, dim3(grid_for(n_cap, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, sk, n_in, heads, n_heads);
+  HIP_CHECK(hipGetLastError());
+}
+
+void session_merge(const int64_t* sk, const int64_t* perm, const uint64_t* vals,
+                   const uint32_t* n_in, const uint32_t* heads, const uint32_t* n_heads,
+                   int64_t max_segments, int64_t gap, int64_t lateness, int64_t wm, int64_t tbase,
+                   int agg, int cap_log2, int64_t nslots, int64_t* s_start, int64_t* s_end,
+                   uint64_t* s_acc, uint32_t* s_cnt, uint32_t* s_flags, int64_t* slot_due,
+                   int64_t* slot_last, uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf,
+                   int64_t* ovf_rows, uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream) {
+  const SessArgs a = make_sess_args(gap, lateness, wm, tbase, agg, cap_log2, nslots);
+  hipLaunchKernelGGL(session_merge_kernel, dim3(grid_for(max_segments * 64, 256, 8192)), dim3(256),
+                     0, (hipStream_t)stream, sk, perm, vals, n_in, heads, n_heads, a, s_start,
+                     s_end, s_acc, s_cnt, s_flags, slot_due, slot_last, late_cnt, ovf_slots, n_ovf,
+                     ovf_rows, n_ovf_runs, ovf_cap);
+  HIP_CHECK(hipGetLastError());
+}
+
+void session_fire(int64_t gap, int64_t lateness, int64_t wm, int agg, int cap_log2,
+                  int64_t nslots, const uint64_t* keys_g, int64_t* s_start, int64_t* s_end,
+                  uint64_t* s_acc, uint32_t* s_cnt, uint32_t* s_flags, int64_t* slot_due,
+                  const ExprProg& map, const ExprProg& filt, uint64_t* out_key, int64_t* out_start,
+                  int64_t* out_end, double* out_val, uint64_t* out_raw, uint32_t* out_cnt,
+                  uint32_t* out_n, uint32_t out_cap, intptr_t stream) {
+  const SessArgs a = make_sess_args(gap, lateness, wm, 0, agg, cap_log2, nslots);
+  const int depth = map.depth > filt.depth ? map.depth : filt.depth;
+  const size_t lds = (size_t)(kExprVars + depth) * 256 * sizeof(double);
+  hipLaunchKernelGGL(session_fire_kernel, dim3(grid_for(nslots, 256, 8192)), dim3(256), lds,
+                     (hipStream_t)stream, a, keys_g, s_start, s_end, s_acc, s_cnt, s_flags,
+                     slot_due, map, filt, out_key, out_start, out_end, out_val, out_raw, out_cnt,
+                     out_n, out_cap);
+  HIP_CHECK(hipGetLastError());
+}
+
+void session_evict(int64_t nslots, int cap_log2, uint64_t* keys_g, int64_t* s_start,
+                   int64_t* s_end, uint64_t* s_acc, uint32_t* s_cnt, uint32_t* s_flags,
+                   int64_t* slot_due, int64_t* slot_last, int64_t idle_before, const int64_t* slots,
+                   uint32_t nslots_list, uint64_t* spill_set, uint32_t spill_mask, int64_t* st_key,
+                   int64_t* st_start, int64_t* st_end, int64_t* st_acc, int64_t* st_cnt,
+                   int64_t* st_flags, uint32_t* n_rows, uint32_t row_cap, uint32_t* n_evicted,
+                   intptr_t stream) {
+  const SessArgs a = make_sess_args(0, 0, 0, 0, 0, cap_log2, nslots);
+  const int64_t total = slots ? (int64_t)nslots_list : nslots;
+  if (total <= 0) return;
+  hipLaunchKernelGGL(session_evict_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, a, keys_g, s_start, s_end, s_acc, s_cnt, s_flags,
+                     slot_due, slot_last, idle_before, slots, nslots_list, spill_set, spill_mask,
+                     st_key, st_start, st_end, st_acc, st_cnt, st_flags, n_rows, row_cap,
+                     n_evicted);
+  HIP_CHECK(hipGetLastError());
+}
+
+void session_rehash(int64_t nslots, int cap_log2, const uint64_t* keys_o, const int64_t* start_o,
+                    const int64_t* end_o, const uint64_t* acc_o, const uint32_t* cnt_o,
+                    const uint32_t* flags_o, const int64_t* due_o, const int64_t* last_o,
+                    uint64_t* keys_n, int64_t* start_n, int64_t* end_n, uint64_t* acc_n,
+                    uint32_t* cnt_n, uint32_t* flags_n, int64_t* due_n, int64_t* last_n,
+                    uint32_t* inserted, intptr_t stream) {
+  const SessArgs a = make_sess_args(0, 0, 0, 0, 0, cap_log2, nslots);
+  hipLaunchKernelGGL(session_rehash_kernel, dim3(grid_for(nslots, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, a, keys_o, start_o, end_o, acc_o, cnt_o, flags_o, due_o,
+                     last_o, keys_n, start_n, end_n, acc_n, cnt_n, flags_n, due_n, last_n,
+                     inserted);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -4,3 +4,4 @@
 #include <pybind11/pybind11.h>
 
 void bind_runtime(pybind11::module_& m);
+void bind_sessions(pybind11::module_& m);

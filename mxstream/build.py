@@ -25,7 +25,7 @@ PKG = ROOT / "mxstream"
 ARCH = os.environ.get("MXS_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["kernels_hip.hip"]
-CXX_SOURCES = ["kernels_cpu.cpp", "runtime.cpp", "bindings.cpp"]
+CXX_SOURCES = ["kernels_cpu.cpp", "runtime.cpp", "sessions.cpp", "bindings.cpp"]
 
 
 def _ext_suffix() -> str:

@@ -3,6 +3,7 @@
   python -m mxstream.models.bench_configs --config 1   # chapter1 threshold alert on CPU
   python -m mxstream.models.bench_configs --config 2   # keyed ValueState counter, 10k keys, 1 GPU
   python -m mxstream.models.bench_configs --config 4   # sliding 1 min / 10 s + lateness, 10M keys
+  python -m mxstream.models.bench_configs --config 5   # session alert + host-DRAM spill
 
 Each prints one JSON line: events/s and the step time (and p50 alert latency where alerts fire).
 Config 1 runs the reference's exact text path: Java-semantics split + Double.parseDouble in the
@@ -23,6 +24,7 @@ from ..ops import expr as E
 from ..ops import kernels as K
 from ..ops.native import load
 from ..runtime.rolling_operator import KeyedRollingOperator
+from ..runtime.session_operator import KeyedSessionOperator
 from ..runtime.window_operator import KeyedWindowOperator
 
 
@@ -148,9 +150,67 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
             "events_per_step": batch, "state_bytes": op.state_bytes(), "device": str(dev)}
 
 
+def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_000,
+            drift: int = 400_000, table_keys: int = 4_000_000, device: str = "cuda") -> dict:
+    """Session windows (gap 5 s, 30 s allowed lateness) over a drifting active key set: each step
+    draws events from `active` consecutive key ids whose window advances by `drift` ids, so keys
+    go idle and their sessions close. The HBM slot table holds `table_keys` keys; idle keys whose
+    fired sessions are still inside the allowed lateness are spilled to the host-DRAM store.
+    Alert: sessions whose volume exceeds 1.5x the expected mean (fused map/filter epilogue)."""
+    dev = torch.device(device)
+    span, gap = 2_000, 5_000
+    per_key_step = batch / active
+    # A key is active for active/drift steps; its session spans that time.
+    exp_sum = per_key_step * (active / drift) * 5_000
+    op = KeyedSessionOperator(gap=gap, lateness=30_000, agg=K.AGG_SUM_I64, device=dev,
+                              max_keys=table_keys, batch_capacity=batch, ooo_bound=1_000,
+                              idle_spill_ms=gap + 2 * span, spill_rows=1 << 22,
+                              filter_prog=E.compile_expr(E.var(E.VAR_RESULT) > 1.5 * exp_sum))
+    kt = torch.empty(batch, dtype=torch.int64, device=dev)
+    tt = torch.empty_like(kt)
+    vt = torch.empty_like(kt)
+    step_i = [0]
+    lat = []
+
+    def step():
+        t_in = time.perf_counter()
+        i = step_i[0]
+        K.gen_events(kt, tt, vt, seed=5, stream_id=0, idx0=i * batch, nkeys=active,
+                     ts_base=i * span, ts_span=span, disorder=1_000, val_lo=0, val_span=10_000)
+        kt.add_(i * drift)
+        rows = op.process(kt, tt, vt)
+        step_i[0] += 1
+        if len(rows):
+            lat.append((time.perf_counter() - t_in) * 1e3)
+        return len(rows)
+
+    for _ in range(warmup):
+        step()
+    _sync(dev)
+    lat.clear()
+    m0 = dict(op.metrics.__dict__)
+    t0 = time.perf_counter()
+    alerts = 0
+    for _ in range(steps):
+        alerts += step()
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    mt = op.metrics
+    return {"config": 5, "metric": "events/sec (session-window alert + host-DRAM spill)",
+            "value": batch * steps / dt, "unit": "events/s", "ms_per_step": dt / steps * 1e3,
+            "p50_alert_latency_ms": statistics.median(lat) if lat else None, "alerts": alerts,
+            "late_dropped": mt.num_late_records_dropped - m0["num_late_records_dropped"],
+            "spilled_keys": mt.spilled_keys - m0["spilled_keys"],
+            "records_to_host": mt.records_to_host - m0["records_to_host"],
+            "overflow_keys": mt.overflow_keys - m0["overflow_keys"],
+            "host_store_bytes": op.host_bytes(), "resident_keys": op.resident_keys() if op.gpu else 0,
+            "hbm_state_bytes": op.state_bytes() - op.host_bytes(), "events_per_step": batch,
+            "active_keys": active, "table_keys": table_keys, "device": str(dev)}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 4])
+    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 4, 5])
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None)
@@ -160,8 +220,10 @@ def main(argv=None) -> int:
         r = config1(a.steps, a.warmup, a.batch or (1 << 20))
     elif a.config == 2:
         r = config2(a.steps, a.warmup, a.batch or (1 << 24), device=a.device)
-    else:
+    elif a.config == 4:
         r = config4(a.steps, a.warmup, a.batch or (1 << 24), device=a.device)
+    else:
+        r = config5(a.steps, a.warmup, a.batch or (1 << 24), device=a.device)
     print(json.dumps(r), flush=True)
     return 0
 

@@ -1,0 +1,468 @@
+"""Keyed event-time session windows with a host-DRAM spill tier (BASELINE config 5).
+
+Semantics follow ``EventTimeSessionWindows.withGap(gap)`` + ``allowedLateness`` + an
+aggregate (chapter3/README.md:412-428, chapter2/README.md:145 for ``AggregateFunction.merge``):
+each element opens ``[ts, ts + gap)``; intersecting (or touching) sessions merge; a session fires
+when the watermark reaches ``end - 1``, stays until ``end - 1 + lateness`` and fires again when a
+late element extends it. Micro-batch rule (shared by every tier): a batch's elements of one key
+are folded in timestamp order, a run of elements closer than ``gap`` is one candidate session,
+and a candidate is dropped as late only when it is late on its own and merges with no live
+session (csrc/sessions.cpp).
+
+Per step and rank:
+
+1. the batch's global minimum timestamp (one MIN all-reduce) is the step's time base;
+2. keyBy partition (pane = 1 ms, so records carry ``ts - tbase``) + RCCL all-to-all, watermark
+   valve and overflow flags in the step's one MIN all-reduce (same pass as the window operator);
+3. GPU: ``session_lookup`` (HBM open-addressing slot table, tombstone reuse; keys in the device
+   spill set -- or hitting a full sub-table -- are diverted to a host staging buffer) -> one
+   radix sort of ``slot << 32 | ts - tbase`` -> ``session_heads`` -> ``session_merge`` (one wave
+   per key, run detection + segmented scan with shuffles, up to ``kSess`` = 4 resident sessions
+   per key; keys with more overflow to the host tier);
+4. diverted records and overflow runs are merged by the host ``SessionStore`` (C++);
+5. the advanced watermark fires due sessions on both tiers (``session_fire``: fused map/filter
+   epilogue, compacted rows) and purges cleaned ones;
+6. spill: when the slot table passes its load budget, slots idle for ``idle_spill_ms`` are packed
+   by ``session_evict`` into staging rows, copied to host DRAM and inserted into the store; their
+   keys join the device spill set (rebuilt from the store as spilled keys expire).
+
+On CPU (``device="cpu"``) the store is the whole engine.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..ops import expr as E
+from ..ops import kernels as K
+from ..ops.native import load
+from ..parallel.comm import Comm, LocalComm
+
+I64_MIN, I64_MAX = K.I64_MIN, K.I64_MAX
+K_SESS = 4                # resident sessions per key slot (csrc/kernels_hip.hip kSess)
+EMPTY_KEY = -1            # ~0ull
+TOMB_KEY = -2             # ~1ull
+
+
+def _next_pow2(x: int) -> int:
+    return 1 << max(0, int(x - 1).bit_length())
+
+
+@dataclass
+class SessionRows:
+    keys: np.ndarray      # uint64
+    start: np.ndarray     # int64 session start
+    end: np.ndarray       # int64 session end (exclusive; window maxTimestamp = end - 1)
+    values: np.ndarray    # float64 result after the map epilogue
+    raw: np.ndarray       # int64 raw accumulator
+    counts: np.ndarray    # int64 element counts
+
+    def __len__(self) -> int:
+        return len(self.keys)
+
+    @staticmethod
+    def concat(parts: list["SessionRows"]) -> "SessionRows":
+        parts = [p for p in parts if len(p)]
+        if not parts:
+            return SessionRows(np.zeros(0, np.uint64), *(np.zeros(0, np.int64) for _ in range(2)),
+                               np.zeros(0, np.float64), np.zeros(0, np.int64), np.zeros(0, np.int64))
+        return SessionRows(*(np.concatenate([getattr(p, f) for p in parts])
+                             for f in ("keys", "start", "end", "values", "raw", "counts")))
+
+
+@dataclass
+class SessionMetrics:
+    num_records_in: int = 0
+    num_late_records_dropped: int = 0
+    num_records_out: int = 0
+    records_to_host: int = 0
+    overflow_keys: int = 0
+    spilled_keys: int = 0
+    freed_slots: int = 0
+    rehashes: int = 0
+    current_watermark: int = I64_MIN
+    steps: int = 0
+    extra: dict = field(default_factory=dict)
+
+
+class KeyedSessionOperator:
+    """Per-rank keyed session-window aggregation: HBM slot table + host-DRAM store."""
+
+    def __init__(self, *, gap: int, lateness: int = 0, agg: int = K.AGG_SUM_I64, device="cpu",
+                 comm: Comm | None = None, max_keys: int = 1 << 20,
+                 parallelism: int | None = None, max_parallelism: int = 128,
+                 batch_capacity: int = 1 << 20, cap_log2: int | None = None,
+                 map_prog: E.Program = E.EMPTY, filter_prog: E.Program = E.EMPTY,
+                 ooo_bound: int = 0, max_load: float = 0.7, idle_spill_ms: int | None = None,
+                 spill_rows: int = 1 << 20, emit_capacity: int | None = None,
+                 external_watermark: bool = False):
+        if gap <= 0:
+            raise ValueError("session gap must be positive")
+        self.device = torch.device(device)
+        self.comm = comm or LocalComm()
+        self.world, self.rank = self.comm.world, self.comm.rank
+        self.gap, self.lateness, self.agg = int(gap), int(lateness), agg
+        self.parallelism = parallelism or self.world
+        self.max_parallelism = max_parallelism
+        self.map_prog, self.filter_prog = map_prog, filter_prog
+        self.ooo_bound = int(ooo_bound)
+        self.external_watermark = external_watermark
+        self.max_load = max_load
+        self.idle_spill_ms = int(idle_spill_ms if idle_spill_ms is not None else 4 * gap)
+        self.metrics = SessionMetrics()
+        self.native = load()
+        self.store = self.native.SessionStore(self.gap, self.lateness, agg)
+        self.wm = I64_MIN
+        self.gpu = self.device.type == "cuda"
+
+        from .geometry import state_geometry
+
+        self.nsub, self.cap_log2 = state_geometry(max_keys, self.world, cap_log2)
+        self.nsub_log2 = self.nsub.bit_length() - 1
+        self.nslots = self.nsub << self.cap_log2
+        dev = self.device
+        kgd = [(kg * self.parallelism // max_parallelism) * self.world // self.parallelism
+               for kg in range(max_parallelism)]
+        self.kg_dest = torch.tensor(kgd, dtype=torch.int32, device=dev)
+        self.nbuckets = self.world << self.nsub_log2
+        self.stats = K.new_stats(dev)
+        self.local_maxts = torch.full((1,), I64_MIN, dtype=torch.int64, device=dev)
+        self.red = torch.zeros(K.RED_WORDS, dtype=torch.int64, device=dev)
+        self._alloc(batch_capacity)
+        if self.gpu:
+            self._alloc_state()
+            self.spill_rows = int(spill_rows)
+            self.st_rows = torch.empty(6 * self.spill_rows, dtype=torch.int64, device=dev)
+            self.ocap = int(emit_capacity or max(self.nslots, 1 << 16))
+            self.out_key = torch.empty(self.ocap, dtype=torch.int64, device=dev)
+            self.out_start = torch.empty(self.ocap, dtype=torch.int64, device=dev)
+            self.out_end = torch.empty(self.ocap, dtype=torch.int64, device=dev)
+            self.out_val = torch.empty(self.ocap, dtype=torch.float64, device=dev)
+            self.out_raw = torch.empty(self.ocap, dtype=torch.int64, device=dev)
+            self.out_cnt = torch.empty(self.ocap, dtype=torch.int32, device=dev)
+            # counters: [0] n_out [1] n_heads [2] n_host [3] n_inserted(step) [4] n_ovf
+            #           [5] n_ovf_runs [6] fire n_out [7] evict rows [8] evicted [9] rehash ins
+            self.ctr = torch.zeros(16, dtype=torch.int32, device=dev)
+            self.late_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+            self.spill_log2 = 16
+            self.spill_set = torch.full((1 << self.spill_log2,), EMPTY_KEY, dtype=torch.int64,
+                                        device=dev)
+            self.spill_keys_at_build = 0
+            self.spill_any = False
+
+    # ---- buffers ----------------------------------------------------------------------------
+    def _alloc(self, batch_capacity: int, slack: float = 1.5) -> None:
+        self.batch_capacity = int(batch_capacity)
+        self.slack = slack
+        per = self.batch_capacity / self.nbuckets
+        nblk = min(1024, max(1, -(-self.batch_capacity // 65536)))
+        cap = int(per * slack + 6 * math.sqrt(max(per, 1.0)) + 64) + 8 * nblk
+        self.bucket_cap = (cap + 7) & ~7
+        dev = self.device
+        words = self.nbuckets * self.bucket_cap * K.REC_WORDS
+        self.send = torch.empty(words, dtype=torch.int64, device=dev)
+        self.recv = torch.empty(words, dtype=torch.int64, device=dev) if self.world > 1 else self.send
+        self.cursor = torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
+        self.recv_counts = (torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
+                            if self.world > 1 else self.cursor)
+        if self.gpu:
+            total = self.nbuckets * self.bucket_cap
+            self.sort_key = torch.empty(total, dtype=torch.int64, device=dev)
+            self.vals_buf = torch.empty(total, dtype=torch.int64, device=dev)
+            self.heads = torch.empty(total, dtype=torch.int32, device=dev)
+            self.host_cap = total
+            self.host_recs = torch.empty(total * K.REC_WORDS, dtype=torch.int64, device=dev)
+            self.ovf_cap = max(1 << 12, total // 16)
+            self.ovf_rows = torch.empty(5 * self.ovf_cap, dtype=torch.int64, device=dev)
+            self.ovf_slots = torch.empty(total, dtype=torch.int64, device=dev)
+
+    def _alloc_state(self) -> None:
+        dev, n = self.device, self.nslots
+        self.keys_g = torch.full((n,), EMPTY_KEY, dtype=torch.int64, device=dev)
+        self.s_start = torch.zeros(K_SESS * n, dtype=torch.int64, device=dev)
+        self.s_end = torch.zeros(K_SESS * n, dtype=torch.int64, device=dev)
+        self.s_acc = torch.zeros(K_SESS * n, dtype=torch.int64, device=dev)
+        self.s_cnt = torch.zeros(K_SESS * n, dtype=torch.int32, device=dev)
+        self.s_flags = torch.zeros(K_SESS * n, dtype=torch.int32, device=dev)
+        self.slot_due = torch.full((n,), I64_MAX, dtype=torch.int64, device=dev)
+        self.slot_last = torch.full((n,), I64_MIN, dtype=torch.int64, device=dev)
+
+    def state_bytes(self) -> int:
+        hbm = 0
+        if self.gpu:
+            hbm = self.nslots * (8 + K_SESS * (8 + 8 + 8 + 4 + 4) + 16)
+        return hbm + int(self.store.bytes())
+
+    def host_bytes(self) -> int:
+        return int(self.store.bytes())
+
+    # ---- main entry -------------------------------------------------------------------------
+    def process(self, keys: torch.Tensor, ts: torch.Tensor, vals: torch.Tensor) -> SessionRows:
+        n = keys.numel()
+        if n > self.batch_capacity:
+            self._alloc(n, self.slack)
+        old_wm = self.wm
+        t = ts.min().reshape(1) if n else torch.full((1,), I64_MAX, dtype=torch.int64,
+                                                    device=ts.device)
+        self.comm.allreduce_min_(t)
+        tbase = int(t.item())
+        if tbase == I64_MAX:
+            tbase = 0
+        while True:
+            K.step_begin(self.cursor, self.stats)
+            plan = K.PartitionPlan(max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2,
+                                   nranks=self.world, window_mode=1, drop_late=0, hash_mode=0,
+                                   bucket_cap=self.bucket_cap, late_ts=I64_MIN, tbase=tbase, pane=1)
+            if n:
+                K.partition(keys, ts, vals, plan, self.kg_dest, self.cursor, self.send, self.stats)
+            K.step_finish(self.stats, self.local_maxts, self.red, bound=self.ooo_bound,
+                          event_mode=True, proc_now=0)
+            self.comm.allreduce_min_(self.red[:5])
+            if self.world > 1:
+                self.comm.all_to_all(self.recv, self.send)
+                self.comm.all_to_all(self.recv_counts, self.cursor)
+            host = self.red.cpu().tolist()
+            if host[4]:
+                raise RuntimeError("session batch spans more than 2^32 ms")
+            if host[3]:
+                self._alloc(self.batch_capacity, self.slack * 2)
+                continue
+            break
+        wm_global = host[2]
+        self.metrics.num_records_in += n
+        self.metrics.steps += 1
+        if self.gpu:
+            self._fold_gpu(tbase, old_wm)
+        else:
+            self._fold_cpu(tbase, old_wm)
+        # Sessions that late data re-opened fire even when the watermark did not move
+        # (EventTimeTrigger.onElement: maxTimestamp <= currentWatermark -> FIRE).
+        wm = old_wm if self.external_watermark else max(old_wm, wm_global)
+        return self._fire_at(wm)
+
+    def advance_watermark(self, wm: int) -> SessionRows:
+        wm = int(wm)
+        if wm <= self.wm:
+            return SessionRows.concat([])
+        return self._fire_at(wm)
+
+    def _fire_at(self, wm: int) -> SessionRows:
+        self.wm = wm
+        self.metrics.current_watermark = wm
+        if wm == I64_MIN:
+            return SessionRows.concat([])
+        parts = []
+        if self.gpu:
+            parts.append(self._fire_gpu(wm))
+        parts.append(self._fire_host(wm))
+        out = SessionRows.concat(parts)
+        self.metrics.num_records_out += len(out)
+        if self.gpu:
+            self._maybe_spill(wm)
+        return out
+
+    def finish(self) -> SessionRows:
+        return self.advance_watermark(I64_MAX)
+
+    # ---- CPU tier ---------------------------------------------------------------------------
+    def _received(self, tbase: int):
+        """Decode the received bucket records (host arrays key, ts, val)."""
+        recs = self.recv.view(-1, K.REC_WORDS).cpu().numpy()
+        counts = self.recv_counts.cpu().numpy().astype(np.int64)
+        idx = np.arange(self.bucket_cap, dtype=np.int64)
+        valid = (idx[None, :] < counts[:, None]).reshape(-1)
+        r = recs[: self.nbuckets * self.bucket_cap][valid]
+        t = (r[:, 2] & 0xFFFFFFFF)
+        keep = t != 0xFFFFFFFF
+        r, t = r[keep], t[keep]
+        return r[:, 0].copy(), t + tbase, r[:, 1].copy()
+
+    def _fold_cpu(self, tbase: int, wm: int) -> None:
+        k, t, v = self._received(tbase)
+        if len(k):
+            self.metrics.num_late_records_dropped += int(self.store.process(k, t, v, wm))
+
+    def _fire_host(self, wm: int) -> SessionRows:
+        mc, mk = self.map_prog.as_args()
+        fc, fk = self.filter_prog.as_args()
+        d = self.store.fire(wm, mc, mk, fc, fk)
+        return SessionRows(d["keys"].view(np.uint64), d["start"], d["end"], d["values"], d["raw"],
+                           d["counts"])
+
+    # ---- GPU tier ---------------------------------------------------------------------------
+    def _st(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _fold_gpu(self, tbase: int, wm: int) -> None:
+        m, st, c = self.native, self._st(), self.ctr
+        c.zero_()
+        self.late_cnt.zero_()
+        m.gpu_session_lookup(self.recv.data_ptr(), self.recv_counts.data_ptr(), self.world,
+                             self.nsub, self.bucket_cap, self.cap_log2, self.keys_g.data_ptr(),
+                             self.spill_set.data_ptr(), self.spill_set.numel() - 1,
+                             int(self.spill_any), self.sort_key.data_ptr(), self.vals_buf.data_ptr(),
+                             c[0:1].data_ptr(), self.host_recs.data_ptr(), c[2:3].data_ptr(),
+                             self.host_cap, c[3:4].data_ptr(), st)
+        total = int(c[0].item())
+        if total:
+            sk, perm = torch.sort(self.sort_key[:total])
+            m.gpu_session_heads(sk.data_ptr(), c[0:1].data_ptr(), total, self.heads.data_ptr(),
+                                c[1:2].data_ptr(), st)
+            m.gpu_session_merge(sk.data_ptr(), perm.data_ptr(), self.vals_buf.data_ptr(),
+                                c[0:1].data_ptr(), self.heads.data_ptr(), c[1:2].data_ptr(),
+                                min(total, self.nslots), self.gap, self.lateness, wm, tbase,
+                                self.agg, self.cap_log2, self.nslots, self.s_start.data_ptr(),
+                                self.s_end.data_ptr(), self.s_acc.data_ptr(), self.s_cnt.data_ptr(),
+                                self.s_flags.data_ptr(), self.slot_due.data_ptr(),
+                                self.slot_last.data_ptr(), self.late_cnt.data_ptr(),
+                                self.ovf_slots.data_ptr(), c[4:5].data_ptr(),
+                                self.ovf_rows.data_ptr(), c[5:6].data_ptr(), self.ovf_cap, st)
+        h = c[:6].cpu().tolist()
+        n_host, n_ins, n_ovf, n_runs = h[2], h[3], h[4], h[5]
+        late = int(self.late_cnt.item()) if total else 0
+        if n_host:
+            if n_host > self.host_cap:
+                raise RuntimeError("host diversion buffer overflow")
+            r = self.host_recs[: n_host * K.REC_WORDS].view(-1, K.REC_WORDS).cpu().numpy()
+            t = (r[:, 2] & 0xFFFFFFFF) + tbase
+            late += int(self.store.process(r[:, 0].copy(), t, r[:, 1].copy(), wm))
+            self.metrics.records_to_host += n_host
+            self.spill_any = True
+        if n_ovf:
+            if n_runs > self.ovf_cap:
+                raise RuntimeError("session overflow-run buffer too small")
+            slots = self.ovf_slots[:n_ovf]
+            okeys = self.keys_g[slots].cpu().numpy()
+            slot_key = dict(zip(slots.cpu().tolist(), okeys.tolist()))
+            self._evict(slots=slots)
+            rows = self.ovf_rows.view(5, self.ovf_cap)[:, :n_runs].cpu().numpy()
+            rk = np.array([slot_key[s] for s in rows[0].tolist()], dtype=np.int64)
+            late += int(self.store.merge_runs(rk, rows[1].copy(), rows[2].copy(), rows[3].copy(),
+                                              rows[4].copy(), wm))
+            self.metrics.overflow_keys += n_ovf
+        self.metrics.num_late_records_dropped += late
+
+    def _fire_gpu(self, wm: int) -> SessionRows:
+        m, st, c = self.native, self._st(), self.ctr
+        mc, mk = self.map_prog.as_args()
+        fc, fk = self.filter_prog.as_args()
+        c[6:7].zero_()
+        m.gpu_session_fire(self.gap, self.lateness, wm, self.agg, self.cap_log2, self.nslots,
+                           self.keys_g.data_ptr(), self.s_start.data_ptr(), self.s_end.data_ptr(),
+                           self.s_acc.data_ptr(), self.s_cnt.data_ptr(), self.s_flags.data_ptr(),
+                           self.slot_due.data_ptr(), mc, mk, fc, fk, self.out_key.data_ptr(),
+                           self.out_start.data_ptr(), self.out_end.data_ptr(),
+                           self.out_val.data_ptr(), self.out_raw.data_ptr(),
+                           self.out_cnt.data_ptr(), c[6:7].data_ptr(), self.ocap, st)
+        k = int(c[6].item())
+        if k > self.ocap:
+            raise RuntimeError(f"session emit buffer overflow ({k} > {self.ocap})")
+        return SessionRows(self.out_key[:k].cpu().numpy().view(np.uint64),
+                           self.out_start[:k].cpu().numpy(), self.out_end[:k].cpu().numpy(),
+                           self.out_val[:k].cpu().numpy(), self.out_raw[:k].cpu().numpy(),
+                           self.out_cnt[:k].cpu().numpy().astype(np.int64))
+
+    # ---- spill tier -------------------------------------------------------------------------
+    def _evict(self, *, slots: torch.Tensor | None = None, idle_before: int = I64_MIN) -> int:
+        """Pack slots (listed, or idle since before `idle_before`) into staging rows, move them
+        to the host store and tombstone them; returns the number of freed slots."""
+        m, st, c = self.native, self._st(), self.ctr
+        self._ensure_spill_capacity(self.store.num_keys() + (slots.numel() if slots is not None
+                                                              else self.nslots))
+        R = self.spill_rows
+        rows = self.st_rows.view(6, R)
+        rows[4].zero_()
+        c[7:9].zero_()
+        m.gpu_session_evict(self.nslots, self.cap_log2, self.keys_g.data_ptr(),
+                            self.s_start.data_ptr(), self.s_end.data_ptr(), self.s_acc.data_ptr(),
+                            self.s_cnt.data_ptr(), self.s_flags.data_ptr(),
+                            self.slot_due.data_ptr(), self.slot_last.data_ptr(), idle_before,
+                            slots.data_ptr() if slots is not None else 0,
+                            slots.numel() if slots is not None else 0,
+                            self.spill_set.data_ptr(), self.spill_set.numel() - 1,
+                            rows[0].data_ptr(), rows[1].data_ptr(), rows[2].data_ptr(),
+                            rows[3].data_ptr(), rows[4].data_ptr(), rows[5].data_ptr(),
+                            c[7:8].data_ptr(), R, c[8:9].data_ptr(), st)
+        nr, ne = c[7:9].cpu().tolist()
+        nr = min(nr, R)
+        if nr:
+            h = rows[:, :nr].cpu().numpy()
+            ok = h[4] > 0  # rows of slots skipped for lack of staging room stay zero
+            h = h[:, ok]
+            self.store.insert(h[0].copy(), h[1].copy(), h[2].copy(), h[3].copy(), h[4].copy(),
+                              h[5].copy())
+            self.spill_any = True
+            self.metrics.spilled_keys += int(len(np.unique(h[0])))
+        self.metrics.freed_slots += ne
+        return ne
+
+    def _ensure_spill_capacity(self, nkeys: int) -> None:
+        need = max(16, _next_pow2(max(1, 2 * nkeys)).bit_length() - 1)
+        if need > self.spill_log2:
+            self._rebuild_spill_set(need)
+
+    def _rebuild_spill_set(self, log2: int | None = None) -> None:
+        log2 = log2 or self.spill_log2
+        log2 = max(log2, max(16, _next_pow2(max(1, 2 * self.store.num_keys())).bit_length() - 1))
+        arr = self.store.spill_set(log2)
+        self.spill_log2 = log2
+        self.spill_set = torch.from_numpy(arr).to(self.device)
+        self.spill_keys_at_build = self.store.num_keys()
+        self.spill_any = self.spill_keys_at_build > 0
+
+    def _rehash(self) -> None:
+        m, st = self.native, self._st()
+        old = (self.keys_g, self.s_start, self.s_end, self.s_acc, self.s_cnt, self.s_flags,
+               self.slot_due, self.slot_last)
+        self._alloc_state()
+        self.ctr[9:10].zero_()
+        m.gpu_session_rehash(self.nslots, self.cap_log2, *(t.data_ptr() for t in old),
+                             self.keys_g.data_ptr(), self.s_start.data_ptr(), self.s_end.data_ptr(),
+                             self.s_acc.data_ptr(), self.s_cnt.data_ptr(), self.s_flags.data_ptr(),
+                             self.slot_due.data_ptr(), self.slot_last.data_ptr(),
+                             self.ctr[9:10].data_ptr(), st)
+        self.metrics.rehashes += 1
+
+    def _maybe_spill(self, wm: int) -> None:
+        k = self.keys_g
+        live, occupied = torch.stack([((k != EMPTY_KEY) & (k != TOMB_KEY)).sum(),
+                                      (k != EMPTY_KEY).sum()]).tolist()
+        if live > self.max_load * self.nslots and wm > I64_MIN:
+            # LRU by last event time: keys idle for idle_spill_ms move to host DRAM (keys with no
+            # live session are simply freed).
+            live -= self._evict(idle_before=wm - self.idle_spill_ms)
+        if occupied > 0.85 * self.nslots and live < 0.6 * self.nslots:
+            self._rehash()
+        # Spilled keys whose sessions expired leave the store: drop them from the device set.
+        nk = self.store.num_keys()
+        if self.spill_any and (nk == 0 or nk * 2 < self.spill_keys_at_build):
+            self._rebuild_spill_set()
+
+    # ---- inspection -------------------------------------------------------------------------
+    def resident_keys(self) -> int:
+        if not self.gpu:
+            return 0
+        k = self.keys_g
+        return int(((k != EMPTY_KEY) & (k != TOMB_KEY)).sum().item())
+
+    def snapshot(self) -> dict:
+        """All live sessions (both tiers) as host columns key/start/end/acc/cnt/flags."""
+        parts = [self.store.snapshot()]
+        if self.gpu:
+            n = self.nslots
+            keys = self.keys_g.cpu().numpy()
+            cnt = self.s_cnt.view(K_SESS, n).cpu().numpy()
+            live = (keys != EMPTY_KEY) & (keys != TOMB_KEY)
+            for j in range(K_SESS):
+                sel = live & (cnt[j] > 0)
+                parts.append({
+                    "key": keys[sel], "start": self.s_start.view(K_SESS, n)[j].cpu().numpy()[sel],
+                    "end": self.s_end.view(K_SESS, n)[j].cpu().numpy()[sel],
+                    "acc": self.s_acc.view(K_SESS, n)[j].cpu().numpy()[sel],
+                    "cnt": cnt[j][sel].astype(np.int64),
+                    "flags": self.s_flags.view(K_SESS, n)[j].cpu().numpy()[sel].astype(np.int64)})
+        return {f: np.concatenate([p[f] for p in parts]) for f in
+                ("key", "start", "end", "acc", "cnt", "flags")}

@@ -92,3 +92,57 @@ def test_results_invariant_to_world_size(world, size, slide, lateness):
     strip = lambda d: {k: v[:2] for k, v in d.items()}
     assert strip(merged) == strip(ref)
     assert late == op.metrics.num_late_records_dropped
+
+
+# ---- session windows: same invariance ----------------------------------------------------
+def _collect_sessions(rows):
+    return {(int(k), int(s)): (int(e), int(a), int(c))
+            for k, s, e, a, c in zip(rows.keys, rows.start, rows.end, rows.raw, rows.counts)}
+
+
+def _session_worker(rank, world, port, q):
+    from mxstream.runtime.session_operator import KeyedSessionOperator
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    op = KeyedSessionOperator(gap=40, lateness=300, agg=K.AGG_SUM_I64, device="cpu",
+                              comm=TorchComm(), max_keys=5000, batch_capacity=PER, ooo_bound=500,
+                              cap_log2=8)
+    got = {}
+    for step in range(STEPS):
+        got.update(_collect_sessions(op.process(*_batch(rank, step))))
+    got.update(_collect_sessions(op.finish()))
+    q.put((rank, got, op.metrics.num_late_records_dropped))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sessions_invariant_to_world_size():
+    from mxstream.runtime.session_operator import KeyedSessionOperator
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_session_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    merged, late = {}, 0
+    for _rank, d, nl in res:
+        late += nl
+        assert not (set(d) & set(merged)), "a session fired on two ranks"
+        merged.update(d)
+    op = KeyedSessionOperator(gap=40, lateness=300, agg=K.AGG_SUM_I64, device="cpu",
+                              max_keys=5000, batch_capacity=PER * world, ooo_bound=500, cap_log2=8)
+    ref = {}
+    for step in range(STEPS):
+        parts = [_batch(r, step) for r in range(world)]
+        ref.update(_collect_sessions(op.process(*[torch.cat([p[i] for p in parts])
+                                                  for i in range(3)])))
+    ref.update(_collect_sessions(op.finish()))
+    assert merged == ref
+    assert late == op.metrics.num_late_records_dropped

@@ -1,0 +1,169 @@
+"""Session windows (BASELINE config 5): native store / GPU operator vs the exact host
+WindowOperator with EventTimeSessionWindows (Flink MergingWindowSet semantics).
+
+Oracle: the DataStream API on the host path (native off), punctuated watermark max_ts - bound
+after every element. Engine: KeyedSessionOperator fed one element per micro-batch (then outputs
+must be identical, late handling included) or in larger batches without late data (then the
+sessions formed are identical because session merging is associative).
+"""
+from collections import Counter
+
+import numpy as np
+import pytest
+import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from mxstream.api.environment import StreamExecutionEnvironment
+from mxstream.api.time import Time, TimeCharacteristic
+from mxstream.api.watermarks import AssignerWithPunctuatedWatermarks, Watermark
+from mxstream.api.windowing import EventTimeSessionWindows
+from mxstream.ops import expr as E
+from mxstream.ops import kernels as K
+from mxstream.runtime.session_operator import KeyedSessionOperator
+
+LONG_MIN = -(1 << 63)
+
+
+class _Punct(AssignerWithPunctuatedWatermarks):
+    periodic = False
+
+    def __init__(self, bound):
+        self.bound = bound
+        self.max = LONG_MIN
+
+    def extract_timestamp(self, e, prev):
+        self.max = max(self.max, e[1])
+        return e[1]
+
+    def check_and_get_next_watermark(self, last, ts):
+        return Watermark(self.max - self.bound)
+
+
+def oracle(events, gap, bound, lateness):
+    out = []
+    env = StreamExecutionEnvironment(1)
+    env.set_stream_time_characteristic(TimeCharacteristic.EventTime)
+    env.config.native = "off"
+    (env.from_collection([(k, t, v, 1) for k, t, v in events])
+     .assign_timestamps_and_watermarks(_Punct(bound))
+     .key_by(lambda e: e[0])
+     .window(EventTimeSessionWindows.with_gap(Time.milliseconds(gap)))
+     .allowed_lateness(Time.milliseconds(lateness))
+     .reduce(lambda a, b: (a[0], a[1], a[2] + b[2], a[3] + b[3]),
+             lambda key, w, els, col: [col.collect((key, w.start, w.end, e[2], e[3])) for e in els])
+     .collect(out))
+    env.execute("session-oracle")
+    return Counter(out)
+
+
+def engine(events, gap, bound, lateness, device="cpu", batch=1, **kw):
+    op = KeyedSessionOperator(gap=gap, lateness=lateness, agg=K.AGG_SUM_I64, device=device,
+                              max_keys=1 << 10, batch_capacity=max(batch, 64), ooo_bound=bound,
+                              **kw)
+    out = Counter()
+
+    def take(rows):
+        for k, s, e, r, c in zip(rows.keys, rows.start, rows.end, rows.raw, rows.counts):
+            out[(int(k), int(s), int(e), int(r), int(c))] += 1
+
+    for i in range(0, len(events), batch):
+        chunk = events[i:i + batch]
+        k = torch.tensor([e[0] for e in chunk], dtype=torch.int64, device=device)
+        t = torch.tensor([e[1] for e in chunk], dtype=torch.int64, device=device)
+        v = torch.tensor([e[2] for e in chunk], dtype=torch.int64, device=device)
+        take(op.process(k, t, v))
+    take(op.finish())
+    return out, op
+
+
+events_st = st.lists(st.tuples(st.integers(0, 5), st.integers(0, 5_000), st.integers(0, 100)),
+                     min_size=1, max_size=50)
+
+
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(events=events_st, gap=st.sampled_from([1, 50, 300, 1000]),
+       bound=st.sampled_from([0, 200, 2000]), lateness=st.sampled_from([0, 500]))
+def test_store_equals_flink_per_element(events, gap, bound, lateness):
+    got, _ = engine(events, gap, bound, lateness)
+    assert got == oracle(events, gap, bound, lateness)
+
+
+@settings(max_examples=30, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(seed=st.integers(0, 10_000), gap=st.sampled_from([10, 100, 400]),
+       batch=st.sampled_from([7, 64, 500]))
+def test_store_batched_no_late_data(seed, gap, batch):
+    rng = np.random.default_rng(seed)
+    n = 600
+    ts = np.sort(rng.integers(0, 20_000, n))
+    ts = ts + rng.integers(-50, 50, n)  # disorder < bound: nothing is late
+    events = [(int(k), int(t), int(v)) for k, t, v in
+              zip(rng.integers(0, 20, n), ts, rng.integers(0, 100, n))]
+    got, op = engine(events, gap, 100, 0, batch=batch)
+    assert op.metrics.num_late_records_dropped == 0
+    assert got == oracle(events, gap, 100, 0)
+
+
+def test_session_late_refire_and_drop():
+    # gap 10: a=[0,10) fires at wm>=9; a late element inside lateness re-fires the merged session;
+    # an element past cleanup is dropped.
+    ev = [(1, 0, 5), (1, 3, 1), (1, 40, 2), (1, 5, 10), (1, 100, 1), (1, 2, 7)]
+    got, op = engine(ev, 10, 0, 40)
+    assert got == oracle(ev, 10, 0, 40)
+    assert op.metrics.num_late_records_dropped == 1
+
+
+def test_session_map_filter_epilogue():
+    op = KeyedSessionOperator(gap=100, agg=K.AGG_SUM_I64, max_keys=64, batch_capacity=64,
+                              map_prog=E.compile_expr(E.var(E.VAR_RESULT) * 2.0),
+                              filter_prog=E.compile_expr(E.var(E.VAR_COUNT) >= 2))
+    k = torch.tensor([1, 1, 2, 3, 3, 3])
+    t = torch.tensor([0, 50, 10, 0, 90, 180])
+    v = torch.tensor([1, 2, 5, 1, 1, 1])
+    got = []
+    for rows in (op.process(k, t, v), op.finish()):
+        got += zip(rows.keys.tolist(), rows.values.tolist(), rows.counts.tolist())
+    got.sort()
+    assert got == [(1, 6.0, 2), (3, 6.0, 3)]
+
+
+def test_spill_set_builder():
+    from mxstream.ops.native import load
+
+    s = load().SessionStore(10, 0, K.AGG_SUM_I64)
+    s.process(np.array([5, 9, 12], np.int64), np.array([0, 0, 0], np.int64),
+              np.array([1, 1, 1], np.int64), LONG_MIN)
+    arr = s.spill_set(4)
+    assert sorted(int(x) for x in arr if x != -1) == [5, 9, 12]
+
+
+# ----------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@settings(max_examples=15, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(seed=st.integers(0, 10_000), gap=st.sampled_from([5, 100, 400]),
+       batch=st.sampled_from([1, 64, 1000]), lateness=st.sampled_from([0, 300]))
+def test_gpu_sessions_equal_cpu(seed, gap, batch, lateness):
+    rng = np.random.default_rng(seed)
+    n = 1500
+    ts = np.sort(rng.integers(0, 30_000, n)) + rng.integers(-400, 400, n)
+    events = [(int(k), int(t), int(v)) for k, t, v in
+              zip(rng.integers(0, 50, n), ts, rng.integers(0, 100, n))]
+    a, _ = engine(events, gap, 100, lateness, device="cpu", batch=batch)
+    b, op = engine(events, gap, 100, lateness, device="cuda", batch=batch)
+    assert a == b
+
+
+@pytest.mark.gpu
+def test_gpu_sessions_overflow_and_spill():
+    # > 4 live sessions per key (overflow to the host tier) and a tiny slot table with an
+    # aggressive idle threshold (spill of cold keys), against the CPU store.
+    rng = np.random.default_rng(3)
+    n = 20_000
+    ts = np.sort(rng.integers(0, 200_000, n))
+    keys = rng.integers(0, 3000, n)
+    events = [(int(k), int(t), int(v)) for k, t, v in zip(keys, ts, rng.integers(0, 9, n))]
+    b, op = engine(events, 50, 30_000, 0, device="cuda", batch=2000, max_load=0.05,
+                   idle_spill_ms=2_000, cap_log2=6)
+    a2, _ = engine(events, 50, 30_000, 0, device="cpu", batch=2000)
+    assert a2 == b
+    assert op.metrics.spilled_keys > 0 or op.metrics.overflow_keys > 0
