@@ -246,61 +246,55 @@ PYBIND11_MODULE(_mxs_native, m) {
                        P<uint32_t>(n_heads), stream);
   });
   m.def("gpu_session_merge", [](intptr_t sk, intptr_t perm, intptr_t vals, intptr_t n_in,
-                                intptr_t heads, intptr_t n_heads, int64_t max_segments, int64_t gap,
+                                intptr_t long_heads, intptr_t n_long, int64_t n_cap, int64_t gap,
                                 int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
-                                int64_t nslots, intptr_t s_start, intptr_t s_end, intptr_t s_acc,
-                                intptr_t s_cnt, intptr_t s_flags, intptr_t slot_due,
+                                int64_t nslots, intptr_t sess, intptr_t slot_due,
                                 intptr_t slot_last, intptr_t late_cnt, intptr_t ovf_slots,
                                 intptr_t n_ovf, intptr_t ovf_rows, intptr_t n_ovf_runs,
                                 uint32_t ovf_cap, intptr_t stream) {
     gpu::session_merge(P<int64_t>(sk), P<int64_t>(perm), P<uint64_t>(vals), P<uint32_t>(n_in),
-                       P<uint32_t>(heads), P<uint32_t>(n_heads), max_segments, gap, lateness, wm,
-                       tbase, agg, cap_log2, nslots, P<int64_t>(s_start), P<int64_t>(s_end),
-                       P<uint64_t>(s_acc), P<uint32_t>(s_cnt), P<uint32_t>(s_flags),
-                       P<int64_t>(slot_due), P<int64_t>(slot_last), P<uint64_t>(late_cnt),
-                       P<int64_t>(ovf_slots), P<uint32_t>(n_ovf), P<int64_t>(ovf_rows),
-                       P<uint32_t>(n_ovf_runs), ovf_cap, stream);
+                       P<uint32_t>(long_heads), P<uint32_t>(n_long), n_cap, gap, lateness, wm,
+                       tbase, agg, cap_log2, nslots, P<int64_t>(sess), P<int64_t>(slot_due),
+                       P<int64_t>(slot_last), P<uint64_t>(late_cnt), P<int64_t>(ovf_slots),
+                       P<uint32_t>(n_ovf), P<int64_t>(ovf_rows), P<uint32_t>(n_ovf_runs), ovf_cap,
+                       stream);
   });
   m.def("gpu_session_fire", [](int64_t gap, int64_t lateness, int64_t wm, int agg, int cap_log2,
-                               int64_t nslots, intptr_t keys_g, intptr_t s_start, intptr_t s_end,
-                               intptr_t s_acc, intptr_t s_cnt, intptr_t s_flags, intptr_t slot_due,
+                               int64_t nslots, intptr_t keys_g, intptr_t sess, intptr_t slot_due,
                                std::vector<int32_t> mc, std::vector<double> mk,
                                std::vector<int32_t> fc, std::vector<double> fk, intptr_t ok,
                                intptr_t os, intptr_t oe, intptr_t ov, intptr_t oraw, intptr_t oc,
                                intptr_t on, uint32_t out_cap, intptr_t stream) {
     gpu::session_fire(gap, lateness, wm, agg, cap_log2, nslots, P<uint64_t>(keys_g),
-                      P<int64_t>(s_start), P<int64_t>(s_end), P<uint64_t>(s_acc),
-                      P<uint32_t>(s_cnt), P<uint32_t>(s_flags), P<int64_t>(slot_due),
-                      make_prog(mc, mk), make_prog(fc, fk), P<uint64_t>(ok), P<int64_t>(os),
-                      P<int64_t>(oe), P<double>(ov), P<uint64_t>(oraw), P<uint32_t>(oc),
-                      P<uint32_t>(on), out_cap, stream);
+                      P<int64_t>(sess), P<int64_t>(slot_due), make_prog(mc, mk), make_prog(fc, fk),
+                      P<uint64_t>(ok), P<int64_t>(os), P<int64_t>(oe), P<double>(ov),
+                      P<uint64_t>(oraw), P<uint32_t>(oc), P<uint32_t>(on), out_cap, stream);
   });
-  m.def("gpu_session_evict", [](int64_t nslots, int cap_log2, intptr_t keys_g, intptr_t s_start,
-                                intptr_t s_end, intptr_t s_acc, intptr_t s_cnt, intptr_t s_flags,
+  m.def("gpu_session_evict", [](int64_t nslots, int cap_log2, intptr_t keys_g, intptr_t sess,
                                 intptr_t slot_due, intptr_t slot_last, int64_t idle_before,
                                 intptr_t slots, uint32_t nslots_list, intptr_t spill_set,
                                 uint32_t spill_mask, intptr_t st_key, intptr_t st_start,
                                 intptr_t st_end, intptr_t st_acc, intptr_t st_cnt,
                                 intptr_t st_flags, intptr_t n_rows, uint32_t row_cap,
                                 intptr_t n_evicted, intptr_t stream) {
-    gpu::session_evict(nslots, cap_log2, P<uint64_t>(keys_g), P<int64_t>(s_start),
-                       P<int64_t>(s_end), P<uint64_t>(s_acc), P<uint32_t>(s_cnt),
-                       P<uint32_t>(s_flags), P<int64_t>(slot_due), P<int64_t>(slot_last),
-                       idle_before, P<int64_t>(slots), nslots_list, P<uint64_t>(spill_set),
-                       spill_mask, P<int64_t>(st_key), P<int64_t>(st_start), P<int64_t>(st_end),
-                       P<int64_t>(st_acc), P<int64_t>(st_cnt), P<int64_t>(st_flags),
-                       P<uint32_t>(n_rows), row_cap, P<uint32_t>(n_evicted), stream);
+    gpu::session_evict(nslots, cap_log2, P<uint64_t>(keys_g), P<int64_t>(sess),
+                       P<int64_t>(slot_due), P<int64_t>(slot_last), idle_before, P<int64_t>(slots),
+                       nslots_list, P<uint64_t>(spill_set), spill_mask, P<int64_t>(st_key),
+                       P<int64_t>(st_start), P<int64_t>(st_end), P<int64_t>(st_acc),
+                       P<int64_t>(st_cnt), P<int64_t>(st_flags), P<uint32_t>(n_rows), row_cap,
+                       P<uint32_t>(n_evicted), stream);
   });
-  m.def("gpu_session_rehash", [](int64_t nslots, int cap_log2, intptr_t ko, intptr_t so,
-                                 intptr_t eo, intptr_t ao, intptr_t co, intptr_t fo, intptr_t dout,
-                                 intptr_t lo, intptr_t kn, intptr_t sn, intptr_t en, intptr_t an,
-                                 intptr_t cn, intptr_t fn, intptr_t dn, intptr_t ln, intptr_t ins,
-                                 intptr_t stream) {
-    gpu::session_rehash(nslots, cap_log2, P<uint64_t>(ko), P<int64_t>(so), P<int64_t>(eo),
-                        P<uint64_t>(ao), P<uint32_t>(co), P<uint32_t>(fo), P<int64_t>(dout),
-                        P<int64_t>(lo), P<uint64_t>(kn), P<int64_t>(sn), P<int64_t>(en),
-                        P<uint64_t>(an), P<uint32_t>(cn), P<uint32_t>(fn), P<int64_t>(dn),
-                        P<int64_t>(ln), P<uint32_t>(ins), stream);
+  m.def("gpu_set_erase", [](intptr_t set, uint32_t mask, intptr_t keys, int64_t n,
+                            intptr_t stream) {
+    gpu::set_erase(P<uint64_t>(set), mask, P<int64_t>(keys), n, stream);
+  });
+  m.def("gpu_session_rehash", [](int64_t nslots, int cap_log2, intptr_t keys_o, intptr_t sess_o,
+                                 intptr_t due_o, intptr_t last_o, intptr_t keys_n, intptr_t sess_n,
+                                 intptr_t due_n, intptr_t last_n, intptr_t ins, intptr_t stream) {
+    gpu::session_rehash(nslots, cap_log2, P<uint64_t>(keys_o), P<int64_t>(sess_o),
+                        P<int64_t>(due_o), P<int64_t>(last_o), P<uint64_t>(keys_n),
+                        P<int64_t>(sess_n), P<int64_t>(due_n), P<int64_t>(last_n),
+                        P<uint32_t>(ins), stream);
   });
   m.def("gpu_expr_filter", [](intptr_t x, int64_t n, std::vector<int32_t> code,
                               std::vector<double> consts, intptr_t keep, intptr_t stream) {

@@ -1106,7 +1106,7 @@ __device__ __forceinline__ uint32_t sess_probe_insert(uint64_t* keys, uint64_t k
     const uint64_t prev = atomicCAS((unsigned long long*)&keys[target], (unsigned long long)expect,
                                     (unsigned long long)key);
     if (prev == expect) {
-      if (!use_tomb) atomicAdd(inserted, 1u);
+      if (!use_tomb && inserted) atomicAdd(inserted, 1u);
       return target;
     }
     if (prev == key) return target;
@@ -1179,6 +1179,14 @@ __global__ __launch_bounds__(256) void session_heads_kernel(const int64_t* __res
   }
 }
 
+struct __attribute__((aligned(32))) SessRec {
+  int64_t start, end;  // [start, end)
+  uint64_t acc;
+  uint32_t cnt;        // 0 = free
+  uint32_t flags;      // bit0 fired, bit1 modified since firing
+};
+static_assert(sizeof(SessRec) == 32, "SessRec layout");
+
 struct SessState {
   int64_t start[kSess], end[kSess];
   uint64_t acc[kSess];
@@ -1240,56 +1248,154 @@ __device__ __forceinline__ int64_t sess_due(const SessState& st, int64_t latenes
   return t;
 }
 
-__device__ __forceinline__ void sess_load(SessState& st, int64_t slot, int64_t nslots,
-                                          const int64_t* s_start, const int64_t* s_end,
-                                          const uint64_t* s_acc, const uint32_t* s_cnt,
-                                          const uint32_t* s_flags) {
+// A slot's kSess sessions are one 128-byte AoS record (one cache line): loads and stores are
+// four 32-byte accesses instead of 20 scattered ones.
+__device__ __forceinline__ void sess_load(SessState& st, const SessRec* r) {
   st.n = 0;
 #pragma unroll
   for (int j = 0; j < kSess; ++j) {
-    const size_t gi = (size_t)j * nslots + slot;
-    const uint32_t c = s_cnt[gi];
-    if (c) {
+    const SessRec x = r[j];
+    if (x.cnt) {
       const int q = st.n++;
-      st.start[q] = s_start[gi];
-      st.end[q] = s_end[gi];
-      st.acc[q] = s_acc[gi];
-      st.cnt[q] = c;
-      st.flags[q] = s_flags[gi];
+      st.start[q] = x.start;
+      st.end[q] = x.end;
+      st.acc[q] = x.acc;
+      st.cnt[q] = x.cnt;
+      st.flags[q] = x.flags;
     }
   }
 }
 
-__device__ __forceinline__ void sess_store(const SessState& st, int64_t slot, int64_t nslots,
-                                           int64_t* s_start, int64_t* s_end, uint64_t* s_acc,
-                                           uint32_t* s_cnt, uint32_t* s_flags) {
+__device__ __forceinline__ void sess_store(const SessState& st, SessRec* r) {
 #pragma unroll
   for (int j = 0; j < kSess; ++j) {
-    const size_t gi = (size_t)j * nslots + slot;
+    SessRec x;
     if (j < st.n) {
-      s_start[gi] = st.start[j];
-      s_end[gi] = st.end[j];
-      s_acc[gi] = st.acc[j];
-      s_cnt[gi] = st.cnt[j];
-      s_flags[gi] = st.flags[j];
+      x.start = st.start[j];
+      x.end = st.end[j];
+      x.acc = st.acc[j];
+      x.cnt = st.cnt[j];
+      x.flags = st.flags[j];
     } else {
-      s_cnt[gi] = 0;
+      x.start = x.end = 0;
+      x.acc = 0;
+      x.cnt = x.flags = 0;
+    }
+    r[j] = x;
+  }
+}
+
+// Per-key fold state shared by the thread-per-segment and wave-per-segment merge kernels.
+struct SessOut {
+  SessRec* sess;
+  int64_t* slot_due;
+  int64_t* slot_last;
+  uint64_t* late_cnt;
+  int64_t* ovf_slots;
+  uint32_t* n_ovf;
+  int64_t* ovf_rows;
+  uint32_t* n_ovf_runs;
+  uint32_t ovf_cap;
+};
+
+// Merge one candidate run into the key's sessions (or route it to the host tier on overflow).
+__device__ __forceinline__ void sess_commit(SessState& st, bool& overflow, uint64_t& late,
+                                            int64_t slot, int64_t ps, int64_t pe, uint64_t pa,
+                                            uint32_t pc, const SessArgs& a, const SessOut& o) {
+  const int res = overflow ? 2 : sess_merge(st, ps, pe, pa, pc, a);
+  if (res == 1) {
+    late += pc;
+  } else if (res == 2) {
+    // More than kSess live sessions: this run (and every later run of the key) goes to the
+    // host store, which takes the key over after the step.
+    overflow = true;
+    const uint32_t q = atomicAdd(o.n_ovf_runs, 1u);
+    if (q < o.ovf_cap) {
+      o.ovf_rows[q] = slot;
+      o.ovf_rows[o.ovf_cap + q] = ps;
+      o.ovf_rows[2 * (size_t)o.ovf_cap + q] = pe;
+      o.ovf_rows[3 * (size_t)o.ovf_cap + q] = (int64_t)pa;
+      o.ovf_rows[4 * (size_t)o.ovf_cap + q] = pc;
     }
   }
 }
 
-// One wave per key segment (sorted by slot, then ts): lanes find the runs of their 64-record
-// chunk (ts gaps > gap split runs) and their accumulators with shuffles; lane 0 merges the runs
-// into the slot's sessions in ts order.
-__global__ __launch_bounds__(256) void session_merge_kernel(
+__device__ __forceinline__ void sess_finish(const SessState& st, int64_t slot, int64_t last_ts,
+                                            uint64_t late, bool overflow, const SessArgs& a,
+                                            const SessOut& o) {
+  sess_store(st, o.sess + slot * kSess);
+  o.slot_due[slot] = sess_due(st, a.lateness);
+  if (last_ts > o.slot_last[slot]) o.slot_last[slot] = last_ts;
+  if (late) atomicAdd((unsigned long long*)o.late_cnt, (unsigned long long)late);
+  if (overflow) {
+    const uint32_t q = atomicAdd(o.n_ovf, 1u);
+    o.ovf_slots[q] = slot;  // host evicts these keys and re-merges their overflow runs
+  }
+}
+
+constexpr uint32_t kSessLongSeg = 96;  // segments longer than this go to the wave kernel
+
+// Thread per key segment (sorted by slot, then ts): the thread at a segment head walks its
+// records serially, splitting runs at ts gaps > gap. Typical session workloads have a few records
+// per key and step, where a wave per key would idle most lanes. Long segments are queued for
+// session_merge_long_kernel.
+__global__ __launch_bounds__(256) void session_merge_small_kernel(
+    const int64_t* __restrict__ sk, const int64_t* __restrict__ perm,
+    const uint64_t* __restrict__ vals, const uint32_t* __restrict__ n_in, SessArgs a, SessOut o,
+    uint32_t* __restrict__ long_heads, uint32_t* __restrict__ n_long) {
+  const uint32_t n = *n_in;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int64_t k = sk[i];
+    if (k == INT64_MAX) continue;
+    const int64_t slot = k >> 32;
+    if (i > 0 && (sk[i - 1] >> 32) == slot) continue;  // not a segment head
+    uint32_t j = i + 1;
+    while (j < n && j - i <= kSessLongSeg) {
+      const int64_t kj = sk[j];
+      if (kj == INT64_MAX || (kj >> 32) != slot) break;
+      ++j;
+    }
+    if (j - i > kSessLongSeg) {
+      long_heads[atomicAdd(n_long, 1u)] = i;
+      continue;
+    }
+    SessState st;
+    sess_load(st, o.sess + slot * kSess);
+    uint64_t late = 0;
+    bool overflow = false;
+    bool pv = false;
+    int64_t ps = 0, pe = 0;
+    uint64_t pa = 0;
+    uint32_t pc = 0;
+    int64_t ts = 0;
+    for (uint32_t r = i; r < j; ++r) {
+      ts = a.tbase + (int64_t)(uint32_t)(sk[r] & 0xFFFFFFFF);
+      const uint64_t v = agg_lift(a.agg, vals[perm[r]]);
+      if (pv && ts <= pe) {
+        pe = ts + a.gap;
+        pa = agg_combine(a.agg, pa, v);
+        pc += 1;
+      } else {
+        if (pv) sess_commit(st, overflow, late, slot, ps, pe, pa, pc, a, o);
+        ps = ts;
+        pe = ts + a.gap;
+        pa = v;
+        pc = 1;
+        pv = true;
+      }
+    }
+    sess_commit(st, overflow, late, slot, ps, pe, pa, pc, a, o);
+    sess_finish(st, slot, ts, late, overflow, a, o);
+  }
+}
+
+// One wave per long key segment: lanes find the runs of their 64-record chunk (ts gaps > gap
+// split runs) and their accumulators with shuffles; lane 0 folds the runs in ts order.
+__global__ __launch_bounds__(256) void session_merge_long_kernel(
     const int64_t* __restrict__ sk, const int64_t* __restrict__ perm,
     const uint64_t* __restrict__ vals, const uint32_t* __restrict__ n_in,
     const uint32_t* __restrict__ heads, const uint32_t* __restrict__ n_heads, SessArgs a,
-    int64_t* __restrict__ s_start, int64_t* __restrict__ s_end, uint64_t* __restrict__ s_acc,
-    uint32_t* __restrict__ s_cnt, uint32_t* __restrict__ s_flags, int64_t* __restrict__ slot_due,
-    int64_t* __restrict__ slot_last, uint64_t* __restrict__ late_cnt,
-    int64_t* __restrict__ ovf_slots, uint32_t* __restrict__ n_ovf, int64_t* __restrict__ ovf_rows,
-    uint32_t* __restrict__ n_ovf_runs, uint32_t ovf_cap) {
+    SessOut o) {
   const uint32_t n = *n_in, nh = *n_heads;
   const int lane = lane_id();
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -1298,7 +1404,7 @@ __global__ __launch_bounds__(256) void session_merge_kernel(
     const uint32_t start = heads[h];
     const int64_t slot = sk[start] >> 32;
     SessState st;
-    sess_load(st, slot, a.nslots, s_start, s_end, s_acc, s_cnt, s_flags);
+    sess_load(st, o.sess + slot * kSess);
     uint64_t late = 0;
     bool overflow = false;
     int64_t last_ts = INT64_MIN;
@@ -1308,24 +1414,6 @@ __global__ __launch_bounds__(256) void session_merge_kernel(
     int64_t ps = 0, pe = 0;
     uint64_t pa = 0;
     uint32_t pc = 0;
-    auto commit = [&]() {
-      const int res = overflow ? 2 : sess_merge(st, ps, pe, pa, pc, a);
-      if (res == 1) {
-        late += pc;
-      } else if (res == 2) {
-        // More than kSess live sessions: this run (and every later run of the key) goes to
-        // the host store, which takes the key over after the step.
-        overflow = true;
-        const uint32_t q = atomicAdd(n_ovf_runs, 1u);
-        if (q < ovf_cap) {
-          ovf_rows[q] = slot;
-          ovf_rows[ovf_cap + q] = ps;
-          ovf_rows[2 * (size_t)ovf_cap + q] = pe;
-          ovf_rows[3 * (size_t)ovf_cap + q] = (int64_t)pa;
-          ovf_rows[4 * (size_t)ovf_cap + q] = pc;
-        }
-      }
-    };
     for (uint32_t b0 = start;; b0 += 64) {
       const uint32_t i = b0 + lane;
       const bool in = i < n && sk[i] != INT64_MAX && (sk[i] >> 32) == slot;
@@ -1341,10 +1429,10 @@ __global__ __launch_bounds__(256) void session_merge_kernel(
       const unsigned long long hm = __ballot(head);
       const unsigned long long below = hm & ((lane == 63) ? ~0ull : ((1ull << (lane + 1)) - 1ull));
       const int run0 = 63 - __clzll(below);
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint64_t ya = __shfl_up(acc, o);
-        const uint32_t yc = __shfl_up(cnt, o);
-        if (in && lane - o >= run0) {
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t ya = __shfl_up(acc, off);
+        const uint32_t yc = __shfl_up(cnt, off);
+        if (in && lane - off >= run0) {
           acc = agg_combine(a.agg, ya, acc);
           cnt += yc;
         }
@@ -1356,7 +1444,6 @@ __global__ __launch_bounds__(256) void session_merge_kernel(
       const unsigned long long em = __ballot(run_end);
       const int64_t chunk_last = __shfl(ts, 63 - __clzll(inm));
       last_ts = chunk_last > last_ts ? chunk_last : last_ts;
-      // Lane 0 folds the chunk's runs in ts order (run ends ascending).
       unsigned long long rem = em;
       while (rem) {
         const int e = __ffsll((long long)rem) - 1;
@@ -1373,7 +1460,7 @@ __global__ __launch_bounds__(256) void session_merge_kernel(
             pa = agg_combine(a.agg, pa, ca);
             pc += cc;
           } else {
-            if (pv) commit();
+            if (pv) sess_commit(st, overflow, late, slot, ps, pe, pa, pc, a, o);
             ps = cs;
             pe = ce;
             pa = ca;
@@ -1384,25 +1471,16 @@ __global__ __launch_bounds__(256) void session_merge_kernel(
       }
       if (__popcll(inm) < 64) break;
     }
-    if (lane == 0 && pv) commit();
     if (lane == 0) {
-      sess_store(st, slot, a.nslots, s_start, s_end, s_acc, s_cnt, s_flags);
-      slot_due[slot] = sess_due(st, a.lateness);
-      if (last_ts > slot_last[slot]) slot_last[slot] = last_ts;
-      if (late) atomicAdd((unsigned long long*)late_cnt, (unsigned long long)late);
-      if (overflow) {
-        const uint32_t q = atomicAdd(n_ovf, 1u);
-        ovf_slots[q] = slot;  // host evicts these keys and re-merges their overflow runs
-      }
+      if (pv) sess_commit(st, overflow, late, slot, ps, pe, pa, pc, a, o);
+      sess_finish(st, slot, last_ts, late, overflow, a, o);
     }
   }
 }
 
 // Fire due sessions: one lane per slot whose due time has passed.
 __global__ __launch_bounds__(256) void session_fire_kernel(
-    SessArgs a, const uint64_t* __restrict__ keys_g, int64_t* __restrict__ s_start,
-    int64_t* __restrict__ s_end, uint64_t* __restrict__ s_acc, uint32_t* __restrict__ s_cnt,
-    uint32_t* __restrict__ s_flags, int64_t* __restrict__ slot_due, ExprProg map, ExprProg filt,
+    SessArgs a, const uint64_t* __restrict__ keys_g, SessRec* __restrict__ sess, int64_t* __restrict__ slot_due, ExprProg map, ExprProg filt,
     uint64_t* __restrict__ out_key, int64_t* __restrict__ out_start, int64_t* __restrict__ out_end,
     double* __restrict__ out_val, uint64_t* __restrict__ out_raw, uint32_t* __restrict__ out_cnt,
     uint32_t* __restrict__ out_n, uint32_t out_cap) {
@@ -1416,7 +1494,7 @@ __global__ __launch_bounds__(256) void session_fire_kernel(
     if (!__ballot(due)) continue;
     SessState st;
     st.n = 0;
-    if (due) sess_load(st, slot, a.nslots, s_start, s_end, s_acc, s_cnt, s_flags);
+    if (due) sess_load(st, sess + slot * kSess);
     const uint64_t key = due ? keys_g[slot] : 0;
 #pragma unroll
     for (int j = 0; j < kSess; ++j) {
@@ -1475,7 +1553,7 @@ __global__ __launch_bounds__(256) void session_fire_kernel(
           keep.flags[q] = st.flags[j];
         }
       }
-      sess_store(keep, slot, a.nslots, s_start, s_end, s_acc, s_cnt, s_flags);
+      sess_store(keep, sess + slot * kSess);
       slot_due[slot] = sess_due(keep, a.lateness);
     }
   }
@@ -1484,64 +1562,98 @@ __global__ __launch_bounds__(256) void session_fire_kernel(
 // Evict (spill) slots idle since before `idle_before` (or listed in `slots`): pack their key and
 // sessions into staging rows, tombstone the slot and insert the key into the spill set.
 __global__ __launch_bounds__(256) void session_evict_kernel(
-    SessArgs a, uint64_t* __restrict__ keys_g, int64_t* __restrict__ s_start,
-    int64_t* __restrict__ s_end, uint64_t* __restrict__ s_acc, uint32_t* __restrict__ s_cnt,
-    uint32_t* __restrict__ s_flags, int64_t* __restrict__ slot_due,
+    SessArgs a, uint64_t* __restrict__ keys_g, SessRec* __restrict__ sess, int64_t* __restrict__ slot_due,
     int64_t* __restrict__ slot_last, int64_t idle_before, const int64_t* __restrict__ slots,
     uint32_t nslots_list, uint64_t* __restrict__ spill_set, uint32_t spill_mask,
     int64_t* __restrict__ st_key, int64_t* __restrict__ st_start, int64_t* __restrict__ st_end,
     int64_t* __restrict__ st_acc, int64_t* __restrict__ st_cnt, int64_t* __restrict__ st_flags,
     uint32_t* __restrict__ n_rows, uint32_t row_cap, uint32_t* __restrict__ n_evicted) {
   const int64_t total = slots ? (int64_t)nslots_list : a.nslots;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t slot = slots ? slots[i] : i;
-    const uint64_t key = keys_g[slot];
-    if (key == kEmptyKey || key == kTombKey) continue;
-    if (!slots && slot_last[slot] >= idle_before) continue;
+  const int lane = lane_id();
+  for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < total;
+       base += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = base + threadIdx.x;
+    int64_t slot = -1;
+    uint64_t key = kEmptyKey;
+    bool take = false;
+    if (i < total) {
+      slot = slots ? slots[i] : i;
+      key = keys_g[slot];
+      take = key != kEmptyKey && key != kTombKey && (slots || slot_last[slot] < idle_before);
+    }
     SessState st;
-    sess_load(st, slot, a.nslots, s_start, s_end, s_acc, s_cnt, s_flags);
-    if (st.n == 0) {  // no live session: free the slot, the key is not spilled
+    st.n = 0;
+    if (take) sess_load(st, sess + slot * kSess);
+    // Wave-aggregated row allocation (one atomic per wave): exclusive scan of st.n.
+    uint32_t x = take ? (uint32_t)st.n : 0u;
+    uint32_t incl = x;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_up(incl, off);
+      if (lane >= off) incl += y;
+    }
+    const uint32_t wave_total = __shfl(incl, 63);
+    uint32_t wb = 0;
+    if (lane == 0 && wave_total) wb = atomicAdd(n_rows, wave_total);
+    wb = __shfl(wb, 0);
+    const uint32_t q = wb + incl - x;
+    bool done = false;
+    if (take && st.n == 0) {  // no live session: free the slot, the key is not spilled
+      done = true;
+    } else if (take && q + st.n <= row_cap) {
+#pragma unroll
+      for (int j = 0; j < kSess; ++j) {
+        if (j < st.n) {
+          st_key[q + j] = (int64_t)key;
+          st_start[q + j] = st.start[j];
+          st_end[q + j] = st.end[j];
+          st_acc[q + j] = (int64_t)st.acc[j];
+          st_cnt[q + j] = st.cnt[j];
+          st_flags[q + j] = st.flags[j];
+        }
+      }
+      SessState empty;
+      empty.n = 0;
+      sess_store(empty, sess + slot * kSess);
+      set_insert(spill_set, spill_mask, key);
+      done = true;
+    }  // else: staging full, the key stays resident this round
+    if (done) {
       slot_due[slot] = INT64_MAX;
       slot_last[slot] = INT64_MIN;
       keys_g[slot] = kTombKey;
-      atomicAdd(n_evicted, 1u);
-      continue;
     }
-    const uint32_t q = atomicAdd(n_rows, (uint32_t)st.n);
-    if (q + st.n > row_cap) continue;  // staging full: keep resident this round
-#pragma unroll
-    for (int j = 0; j < kSess; ++j) {
-      if (j < st.n) {
-        st_key[q + j] = (int64_t)key;
-        st_start[q + j] = st.start[j];
-        st_end[q + j] = st.end[j];
-        st_acc[q + j] = (int64_t)st.acc[j];
-        st_cnt[q + j] = st.cnt[j];
-        st_flags[q + j] = st.flags[j];
+    const unsigned long long dm = __ballot(done);
+    if (lane == 0 && dm) atomicAdd(n_evicted, (uint32_t)__popcll(dm));
+  }
+}
+
+// Forget keys that left the host store (tombstones: probing continues past them).
+__global__ __launch_bounds__(256) void set_erase_kernel(uint64_t* __restrict__ set, uint32_t mask,
+                                                        const int64_t* __restrict__ keys,
+                                                        int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = (uint64_t)keys[i];
+    uint32_t s = (uint32_t)(mix64(key) >> 32) & mask;
+    for (uint32_t p = 0; p <= mask; ++p) {
+      const uint64_t k = set[s];
+      if (k == key) {
+        set[s] = kTombKey;
+        break;
       }
+      if (k == kEmptyKey) break;
+      s = (s + 1) & mask;
     }
-    SessState empty;
-    empty.n = 0;
-    sess_store(empty, slot, a.nslots, s_start, s_end, s_acc, s_cnt, s_flags);
-    slot_due[slot] = INT64_MAX;
-    slot_last[slot] = INT64_MIN;
-    set_insert(spill_set, spill_mask, key);
-    keys_g[slot] = kTombKey;
-    atomicAdd(n_evicted, 1u);
   }
 }
 
 // Rebuild the slot table without tombstones: every live slot is re-inserted into fresh arrays
 // (same sub-table, new position) with its sessions, due time and last activity.
 __global__ __launch_bounds__(256) void session_rehash_kernel(
-    SessArgs a, const uint64_t* __restrict__ keys_o, const int64_t* __restrict__ start_o,
-    const int64_t* __restrict__ end_o, const uint64_t* __restrict__ acc_o,
-    const uint32_t* __restrict__ cnt_o, const uint32_t* __restrict__ flags_o,
+    SessArgs a, const uint64_t* __restrict__ keys_o, const SessRec* __restrict__ sess_o,
     const int64_t* __restrict__ due_o, const int64_t* __restrict__ last_o,
-    uint64_t* __restrict__ keys_n, int64_t* __restrict__ start_n, int64_t* __restrict__ end_n,
-    uint64_t* __restrict__ acc_n, uint32_t* __restrict__ cnt_n, uint32_t* __restrict__ flags_n,
-    int64_t* __restrict__ due_n, int64_t* __restrict__ last_n, uint32_t* __restrict__ inserted) {
+    uint64_t* __restrict__ keys_n, SessRec* __restrict__ sess_n, int64_t* __restrict__ due_n,
+    int64_t* __restrict__ last_n, uint32_t* __restrict__ inserted) {
   const uint32_t mask = (1u << a.cap_log2) - 1;
   for (int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; slot < a.nslots;
        slot += (int64_t)gridDim.x * blockDim.x) {
@@ -1552,14 +1664,7 @@ __global__ __launch_bounds__(256) void session_rehash_kernel(
     const uint32_t s = sess_probe_insert(keys, key, mask, inserted);
     const int64_t ns = (sub << a.cap_log2) | s;  // never kNoSlot: the old table held the key
 #pragma unroll
-    for (int j = 0; j < kSess; ++j) {
-      const size_t go = (size_t)j * a.nslots + slot, gn = (size_t)j * a.nslots + ns;
-      start_n[gn] = start_o[go];
-      end_n[gn] = end_o[go];
-      acc_n[gn] = acc_o[go];
-      cnt_n[gn] = cnt_o[go];
-      flags_n[gn] = flags_o[go];
-    }
+    for (int j = 0; j < kSess; ++j) sess_n[ns * kSess + j] = sess_o[slot * kSess + j];
     due_n[ns] = due_o[slot];
     last_n[ns] = last_o[slot];
   }
@@ -1827,23 +1932,25 @@ void session_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint3
 }
 
 void session_merge(const int64_t* sk, const int64_t* perm, const uint64_t* vals,
-                   const uint32_t* n_in, const uint32_t* heads, const uint32_t* n_heads,
-                   int64_t max_segments, int64_t gap, int64_t lateness, int64_t wm, int64_t tbase,
-                   int agg, int cap_log2, int64_t nslots, int64_t* s_start, int64_t* s_end,
-                   uint64_t* s_acc, uint32_t* s_cnt, uint32_t* s_flags, int64_t* slot_due,
+                   const uint32_t* n_in, uint32_t* long_heads, uint32_t* n_long,
+                   int64_t n_cap, int64_t gap, int64_t lateness, int64_t wm, int64_t tbase,
+                   int agg, int cap_log2, int64_t nslots, int64_t* sess, int64_t* slot_due,
                    int64_t* slot_last, uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf,
                    int64_t* ovf_rows, uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream) {
   const SessArgs a = make_sess_args(gap, lateness, wm, tbase, agg, cap_log2, nslots);
-  hipLaunchKernelGGL(session_merge_kernel, dim3(grid_for(max_segments * 64, 256, 8192)), dim3(256),
-                     0, (hipStream_t)stream, sk, perm, vals, n_in, heads, n_heads, a, s_start,
-                     s_end, s_acc, s_cnt, s_flags, slot_due, slot_last, late_cnt, ovf_slots, n_ovf,
-                     ovf_rows, n_ovf_runs, ovf_cap);
+  const SessOut o{reinterpret_cast<SessRec*>(sess), slot_due, slot_last, late_cnt,
+                  ovf_slots, n_ovf, ovf_rows, n_ovf_runs, ovf_cap};
+  hipLaunchKernelGGL(session_merge_small_kernel, dim3(grid_for(n_cap, 256, 16384)), dim3(256), 0,
+                     (hipStream_t)stream, sk, perm, vals, n_in, a, o, long_heads, n_long);
+  HIP_CHECK(hipGetLastError());
+  // Long segments (hot keys): a wave each; the count stays on the device (grid-stride waves).
+  hipLaunchKernelGGL(session_merge_long_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, sk,
+                     perm, vals, n_in, long_heads, n_long, a, o);
   HIP_CHECK(hipGetLastError());
 }
 
 void session_fire(int64_t gap, int64_t lateness, int64_t wm, int agg, int cap_log2,
-                  int64_t nslots, const uint64_t* keys_g, int64_t* s_start, int64_t* s_end,
-                  uint64_t* s_acc, uint32_t* s_cnt, uint32_t* s_flags, int64_t* slot_due,
+                  int64_t nslots, const uint64_t* keys_g, int64_t* sess, int64_t* slot_due,
                   const ExprProg& map, const ExprProg& filt, uint64_t* out_key, int64_t* out_start,
                   int64_t* out_end, double* out_val, uint64_t* out_raw, uint32_t* out_cnt,
                   uint32_t* out_n, uint32_t out_cap, intptr_t stream) {
@@ -1851,14 +1958,13 @@ void session_fire(int64_t gap, int64_t lateness, int64_t wm, int agg, int cap_lo
   const int depth = map.depth > filt.depth ? map.depth : filt.depth;
   const size_t lds = (size_t)(kExprVars + depth) * 256 * sizeof(double);
   hipLaunchKernelGGL(session_fire_kernel, dim3(grid_for(nslots, 256, 8192)), dim3(256), lds,
-                     (hipStream_t)stream, a, keys_g, s_start, s_end, s_acc, s_cnt, s_flags,
+                     (hipStream_t)stream, a, keys_g, reinterpret_cast<SessRec*>(sess),
                      slot_due, map, filt, out_key, out_start, out_end, out_val, out_raw, out_cnt,
                      out_n, out_cap);
   HIP_CHECK(hipGetLastError());
 }
 
-void session_evict(int64_t nslots, int cap_log2, uint64_t* keys_g, int64_t* s_start,
-                   int64_t* s_end, uint64_t* s_acc, uint32_t* s_cnt, uint32_t* s_flags,
+void session_evict(int64_t nslots, int cap_log2, uint64_t* keys_g, int64_t* sess,
                    int64_t* slot_due, int64_t* slot_last, int64_t idle_before, const int64_t* slots,
                    uint32_t nslots_list, uint64_t* spill_set, uint32_t spill_mask, int64_t* st_key,
                    int64_t* st_start, int64_t* st_end, int64_t* st_acc, int64_t* st_cnt,
@@ -1868,24 +1974,27 @@ void session_evict(int64_t nslots, int cap_log2, uint64_t* keys_g, int64_t* s_st
   const int64_t total = slots ? (int64_t)nslots_list : nslots;
   if (total <= 0) return;
   hipLaunchKernelGGL(session_evict_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0,
-                     (hipStream_t)stream, a, keys_g, s_start, s_end, s_acc, s_cnt, s_flags,
+                     (hipStream_t)stream, a, keys_g, reinterpret_cast<SessRec*>(sess),
                      slot_due, slot_last, idle_before, slots, nslots_list, spill_set, spill_mask,
                      st_key, st_start, st_end, st_acc, st_cnt, st_flags, n_rows, row_cap,
                      n_evicted);
   HIP_CHECK(hipGetLastError());
 }
 
-void session_rehash(int64_t nslots, int cap_log2, const uint64_t* keys_o, const int64_t* start_o,
-                    const int64_t* end_o, const uint64_t* acc_o, const uint32_t* cnt_o,
-                    const uint32_t* flags_o, const int64_t* due_o, const int64_t* last_o,
-                    uint64_t* keys_n, int64_t* start_n, int64_t* end_n, uint64_t* acc_n,
-                    uint32_t* cnt_n, uint32_t* flags_n, int64_t* due_n, int64_t* last_n,
-                    uint32_t* inserted, intptr_t stream) {
+void session_rehash(int64_t nslots, int cap_log2, const uint64_t* keys_o, const int64_t* sess_o,
+                    const int64_t* due_o, const int64_t* last_o, uint64_t* keys_n, int64_t* sess_n,
+                    int64_t* due_n, int64_t* last_n, uint32_t* inserted, intptr_t stream) {
   const SessArgs a = make_sess_args(0, 0, 0, 0, 0, cap_log2, nslots);
   hipLaunchKernelGGL(session_rehash_kernel, dim3(grid_for(nslots, 256, 8192)), dim3(256), 0,
-                     (hipStream_t)stream, a, keys_o, start_o, end_o, acc_o, cnt_o, flags_o, due_o,
-                     last_o, keys_n, start_n, end_n, acc_n, cnt_n, flags_n, due_n, last_n,
-                     inserted);
+                     (hipStream_t)stream, a, keys_o, reinterpret_cast<const SessRec*>(sess_o), due_o,
+                     last_o, keys_n, reinterpret_cast<SessRec*>(sess_n), due_n, last_n, inserted);
+  HIP_CHECK(hipGetLastError());
+}
+
+void set_erase(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, intptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(set_erase_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, set, mask, keys, n);
   HIP_CHECK(hipGetLastError());
 }
 

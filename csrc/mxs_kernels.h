@@ -91,31 +91,26 @@ void session_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
 void session_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
                    uint32_t* n_heads, intptr_t stream);
 void session_merge(const int64_t* sk, const int64_t* perm, const uint64_t* vals,
-                   const uint32_t* n_in, const uint32_t* heads, const uint32_t* n_heads,
-                   int64_t max_segments, int64_t gap, int64_t lateness, int64_t wm, int64_t tbase,
-                   int agg, int cap_log2, int64_t nslots, int64_t* s_start, int64_t* s_end,
-                   uint64_t* s_acc, uint32_t* s_cnt, uint32_t* s_flags, int64_t* slot_due,
+                   const uint32_t* n_in, uint32_t* long_heads, uint32_t* n_long,
+                   int64_t n_cap, int64_t gap, int64_t lateness, int64_t wm, int64_t tbase,
+                   int agg, int cap_log2, int64_t nslots, int64_t* sess, int64_t* slot_due,
                    int64_t* slot_last, uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf,
                    int64_t* ovf_rows, uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream);
 void session_fire(int64_t gap, int64_t lateness, int64_t wm, int agg, int cap_log2,
-                  int64_t nslots, const uint64_t* keys_g, int64_t* s_start, int64_t* s_end,
-                  uint64_t* s_acc, uint32_t* s_cnt, uint32_t* s_flags, int64_t* slot_due,
+                  int64_t nslots, const uint64_t* keys_g, int64_t* sess, int64_t* slot_due,
                   const ExprProg& map, const ExprProg& filt, uint64_t* out_key, int64_t* out_start,
                   int64_t* out_end, double* out_val, uint64_t* out_raw, uint32_t* out_cnt,
                   uint32_t* out_n, uint32_t out_cap, intptr_t stream);
-void session_evict(int64_t nslots, int cap_log2, uint64_t* keys_g, int64_t* s_start,
-                   int64_t* s_end, uint64_t* s_acc, uint32_t* s_cnt, uint32_t* s_flags,
+void session_evict(int64_t nslots, int cap_log2, uint64_t* keys_g, int64_t* sess,
                    int64_t* slot_due, int64_t* slot_last, int64_t idle_before, const int64_t* slots,
                    uint32_t nslots_list, uint64_t* spill_set, uint32_t spill_mask, int64_t* st_key,
                    int64_t* st_start, int64_t* st_end, int64_t* st_acc, int64_t* st_cnt,
                    int64_t* st_flags, uint32_t* n_rows, uint32_t row_cap, uint32_t* n_evicted,
                    intptr_t stream);
-void session_rehash(int64_t nslots, int cap_log2, const uint64_t* keys_o, const int64_t* start_o,
-                    const int64_t* end_o, const uint64_t* acc_o, const uint32_t* cnt_o,
-                    const uint32_t* flags_o, const int64_t* due_o, const int64_t* last_o,
-                    uint64_t* keys_n, int64_t* start_n, int64_t* end_n, uint64_t* acc_n,
-                    uint32_t* cnt_n, uint32_t* flags_n, int64_t* due_n, int64_t* last_n,
-                    uint32_t* inserted, intptr_t stream);
+void set_erase(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, intptr_t stream);
+void session_rehash(int64_t nslots, int cap_log2, const uint64_t* keys_o, const int64_t* sess_o,
+                    const int64_t* due_o, const int64_t* last_o, uint64_t* keys_n, int64_t* sess_n,
+                    int64_t* due_n, int64_t* last_n, uint32_t* inserted, intptr_t stream);
 void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_t* vals,
                   const uint32_t* n_in, const uint32_t* heads, const uint32_t* n_heads,
                   int64_t max_segments, uint64_t* acc_g, uint32_t* cnt_g, const uint64_t* keys_g,

@@ -11,6 +11,15 @@
 //  * the host-DRAM spill tier of the GPU session operator: keys evicted from HBM live here and
 //    their records are diverted here (BASELINE config 5, "host-DRAM state spill").
 //
+// Two tiers inside the store:
+//  * hot: key -> sessions map with a due-time heap (elements, merging, firing);
+//  * cold: columnar chunks of spilled sessions that already fired and were not modified since
+//    (the common case for idle keys: they only wait for their cleanup time). A chunk is one
+//    eviction batch; it is dropped as a whole once every row is past cleanup. A record that
+//    arrives for a key with cold rows promotes them into the hot map first (rows already past
+//    cleanup at that point are discarded, exactly as if they had been cleaned on time).
+// Keys that leave the store are reported by fire() so the device spill set can forget them.
+//
 // Micro-batch semantics (shared with the GPU kernels): a batch's elements of one key are merged
 // in timestamp order; a run of elements closer than `gap` becomes one candidate session, which
 // is dropped as late only if it is late on its own and merges with no live session.
@@ -20,8 +29,10 @@
 
 #include <algorithm>
 #include <cstring>
+#include <deque>
 #include <queue>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "mxs_common.h"
@@ -38,6 +49,20 @@ struct Session {
   uint32_t flags;      // bit0: fired, bit1: modified since firing
 };
 
+struct ColdChunk {
+  std::vector<uint64_t> key;
+  std::vector<int64_t> start, end;
+  std::vector<uint64_t> acc;
+  std::vector<uint32_t> cnt;  // 0 = row gone (promoted or discarded)
+  int64_t max_due = INT64_MIN;
+  size_t live = 0;
+};
+
+template <class T>
+py::array_t<T> to_np(const std::vector<T>& v) {
+  return py::array_t<T>((py::ssize_t)v.size(), v.data());
+}
+
 class SessionStore {
  public:
   SessionStore(int64_t gap, int64_t lateness, int agg) : gap_(gap), late_(lateness), agg_(agg) {
@@ -53,6 +78,7 @@ class SessionStore {
     const int64_t* k = keys.data();
     const int64_t* t = ts.data();
     const int64_t* v = vals.data();
+    promote(k, n, wm);
     std::vector<int64_t> idx(n);
     for (int64_t i = 0; i < n; ++i) idx[i] = i;
     std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
@@ -64,7 +90,6 @@ class SessionStore {
       const uint64_t key = (uint64_t)k[idx[i]];
       int64_t j = i;
       while (j < n && (uint64_t)k[idx[j]] == key) ++j;
-      // runs of this key
       int64_t r = i;
       while (r < j) {
         Session c{t[idx[r]], t[idx[r]] + gap_, agg_lift(agg_, (uint64_t)v[idx[r]]), 1u, 0u};
@@ -84,10 +109,13 @@ class SessionStore {
   }
 
   // Merge pre-built runs (GPU overflow path): each is a candidate session.
-  int64_t merge_runs(py::array_t<int64_t, py::array::c_style> keys, py::array_t<int64_t> starts,
-                     py::array_t<int64_t> ends, py::array_t<int64_t> accs,
-                     py::array_t<int64_t> cnts, int64_t wm) {
+  int64_t merge_runs(py::array_t<int64_t, py::array::c_style> keys,
+                     py::array_t<int64_t, py::array::c_style> starts,
+                     py::array_t<int64_t, py::array::c_style> ends,
+                     py::array_t<int64_t, py::array::c_style> accs,
+                     py::array_t<int64_t, py::array::c_style> cnts, int64_t wm) {
     const int64_t n = keys.size();
+    promote(keys.data(), n, wm);
     int64_t late = 0;
     for (int64_t i = 0; i < n; ++i) {
       Session c{starts.data()[i], ends.data()[i], (uint64_t)accs.data()[i],
@@ -97,10 +125,13 @@ class SessionStore {
     return late;
   }
 
-  // Insert sessions evicted from HBM (spill). Arrays: key, start, end, acc, cnt, flags.
-  void insert(py::array_t<int64_t, py::array::c_style> keys, py::array_t<int64_t> starts,
-              py::array_t<int64_t> ends, py::array_t<int64_t> accs, py::array_t<int64_t> cnts,
-              py::array_t<int64_t> flags) {
+  // Insert sessions evicted from HBM. Arrays: key, start, end, acc, cnt, flags. With `cold`,
+  // fired-and-unmodified sessions of keys without hot state go to one new cold chunk.
+  // Arguments by const reference: the call runs without the GIL, so no Python object may be
+  // created or released inside it.
+  using I64Array = py::array_t<int64_t, py::array::c_style>;
+  void insert(const I64Array& keys, const I64Array& starts, const I64Array& ends,
+              const I64Array& accs, const I64Array& cnts, const I64Array& flags, bool cold) {
     const int64_t n = keys.size();
     auto K = keys.data();
     auto S = starts.data();
@@ -108,18 +139,34 @@ class SessionStore {
     auto A = accs.data();
     auto C = cnts.data();
     auto F = flags.data();
+    ColdChunk ch;
     for (int64_t i = 0; i < n; ++i) {
-      auto& vec = m_[(uint64_t)K[i]];
-      vec.push_back(Session{S[i], E[i], (uint64_t)A[i], (uint32_t)C[i], (uint32_t)F[i]});
-      schedule((uint64_t)K[i]);
+      const uint64_t key = (uint64_t)K[i];
+      if (cold && F[i] == 1 && m_.find(key) == m_.end()) {
+        ch.key.push_back(key);
+        ch.start.push_back(S[i]);
+        ch.end.push_back(E[i]);
+        ch.acc.push_back((uint64_t)A[i]);
+        ch.cnt.push_back((uint32_t)C[i]);
+        ch.max_due = std::max(ch.max_due, cleanup_time(E[i] - 1));
+        continue;
+      }
+      m_[key].push_back(Session{S[i], E[i], (uint64_t)A[i], (uint32_t)C[i], (uint32_t)F[i]});
+      schedule(key);
+    }
+    if (!ch.key.empty()) {
+      ch.live = ch.key.size();
+      cold_rows_ += ch.live;
+      cold_.push_back(std::move(ch));
     }
   }
 
-  // Fire / clean up everything the watermark allows. Returns columns of emitted rows.
+  // Fire / clean up everything the watermark allows. Returns columns of emitted rows plus the
+  // keys that left the store ("released").
   py::dict fire(int64_t wm, std::vector<int32_t> map_code, std::vector<double> map_consts,
                 std::vector<int32_t> f_code, std::vector<double> f_consts) {
     ExprProg mp = prog(map_code, map_consts), fp = prog(f_code, f_consts);
-    std::vector<int64_t> okey, ostart, oend, oraw, ocnt, oref;
+    std::vector<int64_t> okey, ostart, oend, oraw, ocnt, oref, released;
     std::vector<double> oval;
     while (!heap_.empty() && heap_.top().first <= wm) {
       const uint64_t key = heap_.top().second;
@@ -150,23 +197,40 @@ class SessionStore {
           }
           s.flags = 1u;
         }
-        if (maxts + late_ > wm || maxts + late_ < maxts) keep.push_back(s);  // not cleaned yet
+        if (cleanup_time(maxts) > wm) keep.push_back(s);  // not cleaned yet
       }
       if (keep.empty()) {
         m_.erase(it);
+        released.push_back((int64_t)key);
       } else {
         vec.swap(keep);
         schedule(key);
       }
     }
+    for (uint64_t key : pending_released_)
+      if (m_.find(key) == m_.end()) released.push_back((int64_t)key);
+    pending_released_.clear();
+    // Cold chunks: dropped as a whole once every row is past cleanup.
+    for (auto it = cold_.begin(); it != cold_.end();) {
+      if (it->max_due <= wm) {
+        for (size_t r = 0; r < it->key.size(); ++r)
+          if (it->cnt[r] && m_.find(it->key[r]) == m_.end())
+            released.push_back((int64_t)it->key[r]);
+        cold_rows_ -= it->live;
+        it = cold_.erase(it);
+      } else {
+        ++it;
+      }
+    }
     py::dict d;
-    d["keys"] = py::array_t<int64_t>((py::ssize_t)okey.size(), okey.data());
-    d["start"] = py::array_t<int64_t>((py::ssize_t)ostart.size(), ostart.data());
-    d["end"] = py::array_t<int64_t>((py::ssize_t)oend.size(), oend.data());
-    d["values"] = py::array_t<double>((py::ssize_t)oval.size(), oval.data());
-    d["raw"] = py::array_t<int64_t>((py::ssize_t)oraw.size(), oraw.data());
-    d["counts"] = py::array_t<int64_t>((py::ssize_t)ocnt.size(), ocnt.data());
-    d["refire"] = py::array_t<int64_t>((py::ssize_t)oref.size(), oref.data());
+    d["keys"] = to_np(okey);
+    d["start"] = to_np(ostart);
+    d["end"] = to_np(oend);
+    d["values"] = to_np(oval);
+    d["raw"] = to_np(oraw);
+    d["counts"] = to_np(ocnt);
+    d["refire"] = to_np(oref);
+    d["released"] = to_np(released);
     return d;
   }
 
@@ -174,54 +238,83 @@ class SessionStore {
   // every key of this store: records of these keys are diverted from HBM to the host tier.
   py::array_t<int64_t> spill_set(int cap_log2) const {
     const size_t cap = (size_t)1 << cap_log2;
-    if (m_.size() * 2 > cap) throw std::invalid_argument("spill set too small");
+    if (num_keys() * 2 > cap) throw std::invalid_argument("spill set too small");
     py::array_t<int64_t> out((py::ssize_t)cap);
     int64_t* d = out.mutable_data();
     std::fill(d, d + cap, (int64_t)kEmptyKey);
     const uint32_t mask = (uint32_t)(cap - 1);
-    for (auto& kv : m_) {
-      uint32_t s = (uint32_t)(mix64(kv.first) >> 32) & mask;
-      while ((uint64_t)d[s] != kEmptyKey) s = (s + 1) & mask;
-      d[s] = (int64_t)kv.first;
-    }
+    auto put = [&](uint64_t key) {
+      uint32_t s = (uint32_t)(mix64(key) >> 32) & mask;
+      while ((uint64_t)d[s] != kEmptyKey) {
+        if ((uint64_t)d[s] == key) return;
+        s = (s + 1) & mask;
+      }
+      d[s] = (int64_t)key;
+    };
+    for (auto& kv : m_) put(kv.first);
+    for (auto& ch : cold_)
+      for (size_t r = 0; r < ch.key.size(); ++r)
+        if (ch.cnt[r]) put(ch.key[r]);
     return out;
   }
 
-  bool contains(uint64_t key) const { return m_.count(key) != 0; }
-  size_t num_keys() const { return m_.size(); }
+  bool contains(uint64_t key) const {
+    if (m_.count(key)) return true;
+    for (auto& ch : cold_)
+      for (size_t r = 0; r < ch.key.size(); ++r)
+        if (ch.cnt[r] && ch.key[r] == key) return true;
+    return false;
+  }
+  // Keys (cold rows are one session per key in practice: an upper bound otherwise).
+  size_t num_keys() const { return m_.size() + cold_rows_; }
   size_t num_sessions() const {
-    size_t s = 0;
+    size_t s = cold_rows_;
     for (auto& kv : m_) s += kv.second.size();
     return s;
   }
-  size_t bytes() const { return num_sessions() * sizeof(Session) + m_.size() * 48; }
-
-  py::array_t<int64_t> key_list() const {
-    std::vector<int64_t> k;
-    k.reserve(m_.size());
-    for (auto& kv : m_) k.push_back((int64_t)kv.first);
-    return py::array_t<int64_t>((py::ssize_t)k.size(), k.data());
+  size_t num_cold_rows() const { return cold_rows_; }
+  size_t bytes() const {
+    size_t hot = 0;
+    for (auto& kv : m_) hot += kv.second.capacity() * sizeof(Session) + 48;
+    size_t cold = 0;
+    for (auto& ch : cold_) cold += ch.key.size() * (8 + 8 + 8 + 8 + 4);
+    return hot + cold;
   }
 
-  // Snapshot: flat columns (key, start, end, acc, cnt, flags).
+  py::array_t<int64_t> key_list() const {
+    std::unordered_set<uint64_t> ks;
+    for (auto& kv : m_) ks.insert(kv.first);
+    for (auto& ch : cold_)
+      for (size_t r = 0; r < ch.key.size(); ++r)
+        if (ch.cnt[r]) ks.insert(ch.key[r]);
+    std::vector<int64_t> k(ks.begin(), ks.end());
+    std::sort(k.begin(), k.end());
+    return to_np(k);
+  }
+
+  // Snapshot: flat columns (key, start, end, acc, cnt, flags) of both tiers.
   py::dict snapshot() const {
     std::vector<int64_t> k, s, e, a, c, f;
+    auto add = [&](uint64_t key, int64_t st, int64_t en, uint64_t ac, uint32_t cn, uint32_t fl) {
+      k.push_back((int64_t)key);
+      s.push_back(st);
+      e.push_back(en);
+      a.push_back((int64_t)ac);
+      c.push_back(cn);
+      f.push_back(fl);
+    };
     for (auto& kv : m_)
-      for (auto& x : kv.second) {
-        k.push_back((int64_t)kv.first);
-        s.push_back(x.start);
-        e.push_back(x.end);
-        a.push_back((int64_t)x.acc);
-        c.push_back(x.cnt);
-        f.push_back(x.flags);
-      }
+      for (auto& x : kv.second) add(kv.first, x.start, x.end, x.acc, x.cnt, x.flags);
+    for (auto& ch : cold_)
+      for (size_t r = 0; r < ch.key.size(); ++r)
+        if (ch.cnt[r]) add(ch.key[r], ch.start[r], ch.end[r], ch.acc[r], ch.cnt[r], 1u);
     py::dict d;
-    d["key"] = py::array_t<int64_t>((py::ssize_t)k.size(), k.data());
-    d["start"] = py::array_t<int64_t>((py::ssize_t)s.size(), s.data());
-    d["end"] = py::array_t<int64_t>((py::ssize_t)e.size(), e.data());
-    d["acc"] = py::array_t<int64_t>((py::ssize_t)a.size(), a.data());
-    d["cnt"] = py::array_t<int64_t>((py::ssize_t)c.size(), c.data());
-    d["flags"] = py::array_t<int64_t>((py::ssize_t)f.size(), f.data());
+    d["key"] = to_np(k);
+    d["start"] = to_np(s);
+    d["end"] = to_np(e);
+    d["acc"] = to_np(a);
+    d["cnt"] = to_np(c);
+    d["flags"] = to_np(f);
     return d;
   }
 
@@ -235,6 +328,33 @@ class SessionStore {
     for (size_t i = 0; i < consts.size(); ++i) p.consts[i] = consts[i];
     p.ncode = (int32_t)(code.size() / 2);
     return p;
+  }
+
+  int64_t cleanup_time(int64_t maxts) const {
+    const int64_t c = maxts + late_;
+    return c < maxts ? INT64_MAX : c;  // overflow: never cleaned before end of input
+  }
+
+  // Move cold rows of `keys` into the hot map (rows past cleanup at `wm` are discarded).
+  void promote(const int64_t* keys, int64_t n, int64_t wm) {
+    if (cold_rows_ == 0 || n == 0) return;
+    std::unordered_set<uint64_t> want;
+    want.reserve((size_t)n * 2);
+    for (int64_t i = 0; i < n; ++i) want.insert((uint64_t)keys[i]);
+    for (auto& ch : cold_) {
+      for (size_t r = 0; r < ch.key.size(); ++r) {
+        if (!ch.cnt[r] || !want.count(ch.key[r])) continue;
+        if (cleanup_time(ch.end[r] - 1) > wm) {
+          m_[ch.key[r]].push_back(Session{ch.start[r], ch.end[r], ch.acc[r], ch.cnt[r], 1u});
+          schedule(ch.key[r]);
+        }
+        else
+          pending_released_.push_back(ch.key[r]);  // reported by fire() unless it turns hot
+        ch.cnt[r] = 0;
+        ch.live -= 1;
+        cold_rows_ -= 1;
+      }
+    }
   }
 
   // Merge candidate c into key's sessions; returns the number of late-dropped elements.
@@ -255,8 +375,7 @@ class SessionStore {
         rest.push_back(s);
       }
     }
-    const int64_t maxts = merged.end - 1;
-    if (!touched_existing && maxts + late_ <= wm) {
+    if (!touched_existing && cleanup_time(merged.end - 1) <= wm) {
       if (vec.empty()) m_.erase(key);
       return c.cnt;  // late: every window of these elements is already cleaned
     }
@@ -275,7 +394,7 @@ class SessionStore {
     int64_t t = INT64_MAX;
     for (auto& s : it->second) {
       const int64_t maxts = s.end - 1;
-      const int64_t due = ((s.flags & 1u) && !(s.flags & 2u)) ? maxts + late_ : maxts;
+      const int64_t due = ((s.flags & 1u) && !(s.flags & 2u)) ? cleanup_time(maxts) : maxts;
       t = std::min(t, due);
     }
     heap_.push({t, key});
@@ -287,6 +406,9 @@ class SessionStore {
   std::priority_queue<std::pair<int64_t, uint64_t>, std::vector<std::pair<int64_t, uint64_t>>,
                       std::greater<>>
       heap_;
+  std::deque<ColdChunk> cold_;
+  size_t cold_rows_ = 0;
+  std::vector<uint64_t> pending_released_;
 };
 
 }  // namespace
@@ -297,13 +419,18 @@ void bind_sessions(py::module_& m) {
   py::class_<SessionStore>(m, "SessionStore")
       .def(py::init<int64_t, int64_t, int>(), py::arg("gap"), py::arg("lateness"), py::arg("agg"))
       .def("process", &SessionStore::process)
-      .def("insert", &SessionStore::insert)
+      // GIL released: the operator inserts spilled rows from a worker thread while the main
+      // thread keeps launching the next step's kernels (the store is not touched concurrently).
+      .def("insert", &SessionStore::insert, py::arg("keys"), py::arg("starts"), py::arg("ends"),
+           py::arg("accs"), py::arg("cnts"), py::arg("flags"), py::arg("cold") = false,
+           py::call_guard<py::gil_scoped_release>())
       .def("merge_runs", &SessionStore::merge_runs)
       .def("fire", &SessionStore::fire)
       .def("spill_set", &SessionStore::spill_set)
       .def("contains", &SessionStore::contains)
       .def("num_keys", &SessionStore::num_keys)
       .def("num_sessions", &SessionStore::num_sessions)
+      .def("num_cold_rows", &SessionStore::num_cold_rows)
       .def("bytes", &SessionStore::bytes)
       .def("key_list", &SessionStore::key_list)
       .def("snapshot", &SessionStore::snapshot);

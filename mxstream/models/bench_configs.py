@@ -205,7 +205,9 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
             "overflow_keys": mt.overflow_keys - m0["overflow_keys"],
             "host_store_bytes": op.host_bytes(), "resident_keys": op.resident_keys() if op.gpu else 0,
             "hbm_state_bytes": op.state_bytes() - op.host_bytes(), "events_per_step": batch,
-            "active_keys": active, "table_keys": table_keys, "device": str(dev)}
+            "active_keys": active, "table_keys": table_keys, "device": str(dev),
+            "host_phase_ms_per_step": {k: round(v * 1e3 / max(1, mt.steps), 2)
+                                       for k, v in op.phase_s.items()}}
 
 
 def main(argv=None) -> int:

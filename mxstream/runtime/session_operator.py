@@ -30,7 +30,11 @@ On CPU (``device="cpu"``) the store is the whole engine.
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import threading
+import time
+from collections import defaultdict
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -113,6 +117,7 @@ class KeyedSessionOperator:
         self.max_load = max_load
         self.idle_spill_ms = int(idle_spill_ms if idle_spill_ms is not None else 4 * gap)
         self.metrics = SessionMetrics()
+        self.phase_s: dict[str, float] = defaultdict(float)  # host wall time per phase
         self.native = load()
         self.store = self.native.SessionStore(self.gap, self.lateness, agg)
         self.wm = I64_MIN
@@ -136,6 +141,8 @@ class KeyedSessionOperator:
             self._alloc_state()
             self.spill_rows = int(spill_rows)
             self.st_rows = torch.empty(6 * self.spill_rows, dtype=torch.int64, device=dev)
+            self._pin_rows = torch.empty((6, self.spill_rows), dtype=torch.int64).pin_memory()
+            self._spill_thread = None
             self.ocap = int(emit_capacity or max(self.nslots, 1 << 16))
             self.out_key = torch.empty(self.ocap, dtype=torch.int64, device=dev)
             self.out_start = torch.empty(self.ocap, dtype=torch.int64, device=dev)
@@ -150,7 +157,8 @@ class KeyedSessionOperator:
             self.spill_log2 = 16
             self.spill_set = torch.full((1 << self.spill_log2,), EMPTY_KEY, dtype=torch.int64,
                                         device=dev)
-            self.spill_keys_at_build = 0
+            self.set_used = 0  # occupied spill-set entries (keys + tombstones)
+            self._live_estimate = 0
             self.spill_any = False
 
     # ---- buffers ----------------------------------------------------------------------------
@@ -182,22 +190,31 @@ class KeyedSessionOperator:
     def _alloc_state(self) -> None:
         dev, n = self.device, self.nslots
         self.keys_g = torch.full((n,), EMPTY_KEY, dtype=torch.int64, device=dev)
-        self.s_start = torch.zeros(K_SESS * n, dtype=torch.int64, device=dev)
-        self.s_end = torch.zeros(K_SESS * n, dtype=torch.int64, device=dev)
-        self.s_acc = torch.zeros(K_SESS * n, dtype=torch.int64, device=dev)
-        self.s_cnt = torch.zeros(K_SESS * n, dtype=torch.int32, device=dev)
-        self.s_flags = torch.zeros(K_SESS * n, dtype=torch.int32, device=dev)
+        # [slot][kSess] x {start, end, acc, cnt | flags << 32}: one 128-byte record per slot.
+        self.sess = torch.zeros(n * K_SESS * 4, dtype=torch.int64, device=dev)
         self.slot_due = torch.full((n,), I64_MAX, dtype=torch.int64, device=dev)
         self.slot_last = torch.full((n,), I64_MIN, dtype=torch.int64, device=dev)
 
     def state_bytes(self) -> int:
+        if self.gpu:
+            self._join_spill()
         hbm = 0
         if self.gpu:
-            hbm = self.nslots * (8 + K_SESS * (8 + 8 + 8 + 4 + 4) + 16)
+            hbm = self.nslots * (8 + K_SESS * 32 + 16)
         return hbm + int(self.store.bytes())
 
     def host_bytes(self) -> int:
+        if self.gpu:
+            self._join_spill()
         return int(self.store.bytes())
+
+    @contextlib.contextmanager
+    def _phase(self, name: str):
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            self.phase_s[name] += time.perf_counter() - t0
 
     # ---- main entry -------------------------------------------------------------------------
     def process(self, keys: torch.Tensor, ts: torch.Tensor, vals: torch.Tensor) -> SessionRows:
@@ -235,7 +252,8 @@ class KeyedSessionOperator:
         self.metrics.num_records_in += n
         self.metrics.steps += 1
         if self.gpu:
-            self._fold_gpu(tbase, old_wm)
+            with self._phase("fold_gpu"):
+                self._fold_gpu(tbase, old_wm)
         else:
             self._fold_cpu(tbase, old_wm)
         # Sessions that late data re-opened fire even when the watermark did not move
@@ -256,12 +274,17 @@ class KeyedSessionOperator:
             return SessionRows.concat([])
         parts = []
         if self.gpu:
-            parts.append(self._fire_gpu(wm))
-        parts.append(self._fire_host(wm))
+            with self._phase("fire_gpu"):
+                parts.append(self._fire_gpu(wm))
+        with self._phase("fire_host"):
+            if self.gpu:
+                self._join_spill()
+            parts.append(self._fire_host(wm))
         out = SessionRows.concat(parts)
         self.metrics.num_records_out += len(out)
         if self.gpu:
-            self._maybe_spill(wm)
+            with self._phase("spill"):
+                self._maybe_spill(wm)
         return out
 
     def finish(self) -> SessionRows:
@@ -289,6 +312,12 @@ class KeyedSessionOperator:
         mc, mk = self.map_prog.as_args()
         fc, fk = self.filter_prog.as_args()
         d = self.store.fire(wm, mc, mk, fc, fk)
+        rel = d["released"]
+        if self.gpu and len(rel) and self.spill_any:
+            # Keys that left the host store leave the device spill set (tombstoned).
+            kt = torch.from_numpy(rel).to(self.device)
+            self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
+                                      kt.data_ptr(), kt.numel(), self._st())
         return SessionRows(d["keys"].view(np.uint64), d["start"], d["end"], d["values"], d["raw"],
                            d["counts"])
 
@@ -298,30 +327,33 @@ class KeyedSessionOperator:
 
     def _fold_gpu(self, tbase: int, wm: int) -> None:
         m, st, c = self.native, self._st(), self.ctr
-        c.zero_()
+        if self._live_estimate > 0.9 * self.nslots:
+            self._join_spill()
+            # Sub-tables may fill up: room in the spill set for every key the lookup may divert.
+            self._ensure_spill_capacity(self.batch_capacity)
+        c[:7].zero_()  # c[7:9] may still be read by the spill worker
         self.late_cnt.zero_()
         m.gpu_session_lookup(self.recv.data_ptr(), self.recv_counts.data_ptr(), self.world,
                              self.nsub, self.bucket_cap, self.cap_log2, self.keys_g.data_ptr(),
                              self.spill_set.data_ptr(), self.spill_set.numel() - 1,
                              int(self.spill_any), self.sort_key.data_ptr(), self.vals_buf.data_ptr(),
                              c[0:1].data_ptr(), self.host_recs.data_ptr(), c[2:3].data_ptr(),
-                             self.host_cap, c[3:4].data_ptr(), st)
+                             self.host_cap, 0, st)
         total = int(c[0].item())
         if total:
             sk, perm = torch.sort(self.sort_key[:total])
-            m.gpu_session_heads(sk.data_ptr(), c[0:1].data_ptr(), total, self.heads.data_ptr(),
-                                c[1:2].data_ptr(), st)
             m.gpu_session_merge(sk.data_ptr(), perm.data_ptr(), self.vals_buf.data_ptr(),
                                 c[0:1].data_ptr(), self.heads.data_ptr(), c[1:2].data_ptr(),
-                                min(total, self.nslots), self.gap, self.lateness, wm, tbase,
-                                self.agg, self.cap_log2, self.nslots, self.s_start.data_ptr(),
-                                self.s_end.data_ptr(), self.s_acc.data_ptr(), self.s_cnt.data_ptr(),
-                                self.s_flags.data_ptr(), self.slot_due.data_ptr(),
+                                total, self.gap, self.lateness, wm, tbase,
+                                self.agg, self.cap_log2, self.nslots, self.sess.data_ptr(),
+                                self.slot_due.data_ptr(),
                                 self.slot_last.data_ptr(), self.late_cnt.data_ptr(),
                                 self.ovf_slots.data_ptr(), c[4:5].data_ptr(),
                                 self.ovf_rows.data_ptr(), c[5:6].data_ptr(), self.ovf_cap, st)
-        h = c[:6].cpu().tolist()
-        n_host, n_ins, n_ovf, n_runs = h[2], h[3], h[4], h[5]
+        with self._phase("fold_gpu.sync"):
+            h = c[:6].cpu().tolist()
+        self._join_spill()  # the host store must hold last step's spilled rows
+        n_host, n_ovf, n_runs = h[2], h[4], h[5]
         late = int(self.late_cnt.item()) if total else 0
         if n_host:
             if n_host > self.host_cap:
@@ -330,7 +362,9 @@ class KeyedSessionOperator:
             t = (r[:, 2] & 0xFFFFFFFF) + tbase
             late += int(self.store.process(r[:, 0].copy(), t, r[:, 1].copy(), wm))
             self.metrics.records_to_host += n_host
+            self.set_used += n_host  # upper bound on keys the lookup added (full sub-tables)
             self.spill_any = True
+            self._ensure_spill_capacity(0)
         if n_ovf:
             if n_runs > self.ovf_cap:
                 raise RuntimeError("session overflow-run buffer too small")
@@ -351,9 +385,7 @@ class KeyedSessionOperator:
         fc, fk = self.filter_prog.as_args()
         c[6:7].zero_()
         m.gpu_session_fire(self.gap, self.lateness, wm, self.agg, self.cap_log2, self.nslots,
-                           self.keys_g.data_ptr(), self.s_start.data_ptr(), self.s_end.data_ptr(),
-                           self.s_acc.data_ptr(), self.s_cnt.data_ptr(), self.s_flags.data_ptr(),
-                           self.slot_due.data_ptr(), mc, mk, fc, fk, self.out_key.data_ptr(),
+                           self.keys_g.data_ptr(), self.sess.data_ptr(), self.slot_due.data_ptr(), mc, mk, fc, fk, self.out_key.data_ptr(),
                            self.out_start.data_ptr(), self.out_end.data_ptr(),
                            self.out_val.data_ptr(), self.out_raw.data_ptr(),
                            self.out_cnt.data_ptr(), c[6:7].data_ptr(), self.ocap, st)
@@ -366,62 +398,102 @@ class KeyedSessionOperator:
                            self.out_cnt[:k].cpu().numpy().astype(np.int64))
 
     # ---- spill tier -------------------------------------------------------------------------
-    def _evict(self, *, slots: torch.Tensor | None = None, idle_before: int = I64_MIN) -> int:
-        """Pack slots (listed, or idle since before `idle_before`) into staging rows, move them
-        to the host store and tombstone them; returns the number of freed slots."""
+    def _evict(self, *, slots: torch.Tensor | None = None, idle_before: int = I64_MIN) -> None:
+        """Pack slots (listed, or idle since before `idle_before`) into staging rows and
+        tombstone them; the rows go to the host store. For idle evictions the host-store insert
+        runs on a worker thread while the next step's kernels run."""
+        self._join_spill()
         m, st, c = self.native, self._st(), self.ctr
-        self._ensure_spill_capacity(self.store.num_keys() + (slots.numel() if slots is not None
-                                                              else self.nslots))
+        self._ensure_spill_capacity(slots.numel() if slots is not None else self._live_estimate)
         R = self.spill_rows
         rows = self.st_rows.view(6, R)
         rows[4].zero_()
         c[7:9].zero_()
         m.gpu_session_evict(self.nslots, self.cap_log2, self.keys_g.data_ptr(),
-                            self.s_start.data_ptr(), self.s_end.data_ptr(), self.s_acc.data_ptr(),
-                            self.s_cnt.data_ptr(), self.s_flags.data_ptr(),
-                            self.slot_due.data_ptr(), self.slot_last.data_ptr(), idle_before,
+                            self.sess.data_ptr(), self.slot_due.data_ptr(),
+                            self.slot_last.data_ptr(), idle_before,
                             slots.data_ptr() if slots is not None else 0,
                             slots.numel() if slots is not None else 0,
                             self.spill_set.data_ptr(), self.spill_set.numel() - 1,
                             rows[0].data_ptr(), rows[1].data_ptr(), rows[2].data_ptr(),
                             rows[3].data_ptr(), rows[4].data_ptr(), rows[5].data_ptr(),
                             c[7:8].data_ptr(), R, c[8:9].data_ptr(), st)
-        nr, ne = c[7:9].cpu().tolist()
+        self.spill_any = True
+        with self._phase("spill.evict_kernel"):
+            nr, ne = self.ctr[7:9].cpu().tolist()
         nr = min(nr, R)
+        h = None
         if nr:
-            h = rows[:, :nr].cpu().numpy()
-            ok = h[4] > 0  # rows of slots skipped for lack of staging room stay zero
-            h = h[:, ok]
-            self.store.insert(h[0].copy(), h[1].copy(), h[2].copy(), h[3].copy(), h[4].copy(),
-                              h[5].copy())
-            self.spill_any = True
-            self.metrics.spilled_keys += int(len(np.unique(h[0])))
+            # Six contiguous DMA copies into pinned host memory.
+            for j in range(6):
+                self._pin_rows[j, :nr].copy_(rows[j, :nr], non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            h = self._pin_rows[:, :nr].numpy()
+            h = np.ascontiguousarray(h[:, h[4] > 0])  # skipped rows (no staging room) stay zero
+        nk = int((h[0][1:] != h[0][:-1]).sum()) + 1 if h is not None and h.shape[1] else 0
+        self._apply_spill((nk, ne))
+        if h is None or not h.shape[1]:
+            return
+        cold = slots is None  # idle keys: fired-and-unmodified sessions go to a cold chunk
+        if not cold:
+            self.store.insert(h[0], h[1], h[2], h[3], h[4], h[5], False)
+            return
+        # The host-store insert (C++, GIL released) overlaps the next step's GPU work; joined
+        # before the store is used again.
+        self._spill_err = None
+
+        def work():
+            try:
+                t0 = time.perf_counter()
+                self.store.insert(h[0], h[1], h[2], h[3], h[4], h[5], True)
+                self.phase_s["spill.host_insert"] += time.perf_counter() - t0
+            except BaseException as e:  # re-raised by _join_spill
+                self._spill_err = e
+
+        self._spill_thread = threading.Thread(target=work, name="mxs-spill", daemon=True)
+        self._spill_thread.start()
+
+    def _apply_spill(self, res: tuple[int, int]) -> None:
+        nk, ne = res
+        self.set_used += nk
+        self.metrics.spilled_keys += nk
         self.metrics.freed_slots += ne
-        return ne
 
-    def _ensure_spill_capacity(self, nkeys: int) -> None:
-        need = max(16, _next_pow2(max(1, 2 * nkeys)).bit_length() - 1)
-        if need > self.spill_log2:
-            self._rebuild_spill_set(need)
+    def _join_spill(self) -> None:
+        t = getattr(self, "_spill_thread", None)
+        if t is None:
+            return
+        with self._phase("spill.join"):
+            t.join()
+        self._spill_thread = None
+        if self._spill_err is not None:
+            raise self._spill_err
 
-    def _rebuild_spill_set(self, log2: int | None = None) -> None:
-        log2 = log2 or self.spill_log2
-        log2 = max(log2, max(16, _next_pow2(max(1, 2 * self.store.num_keys())).bit_length() - 1))
+    def _ensure_spill_capacity(self, extra: int) -> None:
+        """Keep the device spill set (live keys + tombstones) at most half full after `extra`
+        more insertions; otherwise rebuild it from the store's keys at a larger size."""
+        cap = self.spill_set.numel()
+        if self.set_used + extra <= cap // 2:
+            return
+        want = 4 * (self.store.num_keys() + extra)
+        self._rebuild_spill_set(max(16, _next_pow2(max(1, want)).bit_length() - 1))
+
+    def _rebuild_spill_set(self, log2: int) -> None:
+        t0 = time.perf_counter()
         arr = self.store.spill_set(log2)
         self.spill_log2 = log2
         self.spill_set = torch.from_numpy(arr).to(self.device)
-        self.spill_keys_at_build = self.store.num_keys()
-        self.spill_any = self.spill_keys_at_build > 0
+        self.set_used = self.store.num_keys()
+        self.spill_any = self.set_used > 0
+        self.phase_s["spill.set_rebuild"] += time.perf_counter() - t0
 
     def _rehash(self) -> None:
         m, st = self.native, self._st()
-        old = (self.keys_g, self.s_start, self.s_end, self.s_acc, self.s_cnt, self.s_flags,
-               self.slot_due, self.slot_last)
+        old = (self.keys_g, self.sess, self.slot_due, self.slot_last)
         self._alloc_state()
         self.ctr[9:10].zero_()
         m.gpu_session_rehash(self.nslots, self.cap_log2, *(t.data_ptr() for t in old),
-                             self.keys_g.data_ptr(), self.s_start.data_ptr(), self.s_end.data_ptr(),
-                             self.s_acc.data_ptr(), self.s_cnt.data_ptr(), self.s_flags.data_ptr(),
+                             self.keys_g.data_ptr(), self.sess.data_ptr(),
                              self.slot_due.data_ptr(), self.slot_last.data_ptr(),
                              self.ctr[9:10].data_ptr(), st)
         self.metrics.rehashes += 1
@@ -430,16 +502,18 @@ class KeyedSessionOperator:
         k = self.keys_g
         live, occupied = torch.stack([((k != EMPTY_KEY) & (k != TOMB_KEY)).sum(),
                                       (k != EMPTY_KEY).sum()]).tolist()
+        self._live_estimate = int(live)
+        if occupied > 0.85 * self.nslots and live < 0.6 * self.nslots:
+            self._rehash()
         if live > self.max_load * self.nslots and wm > I64_MIN:
             # LRU by last event time: keys idle for idle_spill_ms move to host DRAM (keys with no
             # live session are simply freed).
-            live -= self._evict(idle_before=wm - self.idle_spill_ms)
-        if occupied > 0.85 * self.nslots and live < 0.6 * self.nslots:
-            self._rehash()
-        # Spilled keys whose sessions expired leave the store: drop them from the device set.
-        nk = self.store.num_keys()
-        if self.spill_any and (nk == 0 or nk * 2 < self.spill_keys_at_build):
-            self._rebuild_spill_set()
+            self._evict(idle_before=wm - self.idle_spill_ms)
+        # Store empty again: clear the device set (drops its tombstones) and skip set probes.
+        if self.spill_any and self._spill_thread is None and self.store.num_keys() == 0:
+            self.spill_set.fill_(EMPTY_KEY)
+            self.set_used = 0
+            self.spill_any = False
 
     # ---- inspection -------------------------------------------------------------------------
     def resident_keys(self) -> int:
@@ -450,19 +524,18 @@ class KeyedSessionOperator:
 
     def snapshot(self) -> dict:
         """All live sessions (both tiers) as host columns key/start/end/acc/cnt/flags."""
+        if self.gpu:
+            self._join_spill()
         parts = [self.store.snapshot()]
         if self.gpu:
-            n = self.nslots
             keys = self.keys_g.cpu().numpy()
-            cnt = self.s_cnt.view(K_SESS, n).cpu().numpy()
+            rec = self.sess.view(self.nslots, K_SESS, 4).cpu().numpy()
+            cnt = rec[:, :, 3] & 0xFFFFFFFF
             live = (keys != EMPTY_KEY) & (keys != TOMB_KEY)
             for j in range(K_SESS):
-                sel = live & (cnt[j] > 0)
-                parts.append({
-                    "key": keys[sel], "start": self.s_start.view(K_SESS, n)[j].cpu().numpy()[sel],
-                    "end": self.s_end.view(K_SESS, n)[j].cpu().numpy()[sel],
-                    "acc": self.s_acc.view(K_SESS, n)[j].cpu().numpy()[sel],
-                    "cnt": cnt[j][sel].astype(np.int64),
-                    "flags": self.s_flags.view(K_SESS, n)[j].cpu().numpy()[sel].astype(np.int64)})
+                sel = live & (cnt[:, j] > 0)
+                parts.append({"key": keys[sel], "start": rec[sel, j, 0], "end": rec[sel, j, 1],
+                              "acc": rec[sel, j, 2], "cnt": cnt[sel, j],
+                              "flags": rec[sel, j, 3] >> 32})
         return {f: np.concatenate([p[f] for p in parts]) for f in
                 ("key", "start", "end", "acc", "cnt", "flags")}

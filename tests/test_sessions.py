@@ -137,17 +137,57 @@ def test_spill_set_builder():
     assert sorted(int(x) for x in arr if x != -1) == [5, 9, 12]
 
 
+def test_store_cold_tier_promotion_equals_hot():
+    """Sessions inserted as cold rows (spilled, fired, waiting for cleanup) behave exactly like
+    hot ones: late records promote them (or find them cleaned), cleanup releases the keys."""
+    from mxstream.ops.native import load
+
+    m = load()
+    rng = np.random.default_rng(7)
+    hot = m.SessionStore(100, 1000, K.AGG_SUM_I64)
+    cold = m.SessionStore(100, 1000, K.AGG_SUM_I64)
+    n = 400
+    keys = rng.integers(0, 300, n)
+    starts = rng.integers(0, 5000, n)
+    rows = [np.unique(keys)]
+    k = rows[0].astype(np.int64)
+    s = (k * 17) % 5000
+    e = s + 100
+    acc = k * 3
+    cnt = np.ones_like(k)
+    flags = np.ones_like(k)
+    hot.insert(k, s, e, acc, cnt, flags, False)
+    cold.insert(k, s, e, acc, cnt, flags, True)
+    assert cold.num_cold_rows() == len(k)
+    outs = []
+    for st_ in (hot, cold):
+        d0 = st_.fire(3000, [], [], [], [])  # the operator fires every step before new data
+        late = st_.process(keys.astype(np.int64), starts.astype(np.int64), np.ones(n, np.int64),
+                           3000)
+        fired, released = [], set(d0["released"].tolist())
+        for w in (3500, 5000, 7000, (1 << 63) - 1):
+            d = st_.fire(w, [], [], [], [])
+            fired.append(sorted(zip(d["keys"].tolist(), d["start"].tolist(), d["raw"].tolist())))
+            released |= set(d["released"].tolist())
+        outs.append((late, fired, released))
+    assert outs[0] == outs[1]
+    assert outs[0][2] == set(k.tolist()) | set(keys.tolist())
+    assert cold.num_keys() == 0 and hot.num_keys() == 0
+
+
 # ----------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
 @settings(max_examples=15, deadline=None, suppress_health_check=[HealthCheck.too_slow])
 @given(seed=st.integers(0, 10_000), gap=st.sampled_from([5, 100, 400]),
-       batch=st.sampled_from([1, 64, 1000]), lateness=st.sampled_from([0, 300]))
-def test_gpu_sessions_equal_cpu(seed, gap, batch, lateness):
+       batch=st.sampled_from([1, 64, 1000]), lateness=st.sampled_from([0, 300]),
+       nkeys=st.sampled_from([2, 50]))
+def test_gpu_sessions_equal_cpu(seed, gap, batch, lateness, nkeys):
+    # nkeys=2 with batch 1000: ~500 records per key and step (wave-per-key merge path).
     rng = np.random.default_rng(seed)
-    n = 1500
+    n = 1500 if batch > 1 else 300
     ts = np.sort(rng.integers(0, 30_000, n)) + rng.integers(-400, 400, n)
     events = [(int(k), int(t), int(v)) for k, t, v in
-              zip(rng.integers(0, 50, n), ts, rng.integers(0, 100, n))]
+              zip(rng.integers(0, nkeys, n), ts, rng.integers(0, 100, n))]
     a, _ = engine(events, gap, 100, lateness, device="cpu", batch=batch)
     b, op = engine(events, gap, 100, lateness, device="cuda", batch=batch)
     assert a == b
@@ -162,8 +202,8 @@ def test_gpu_sessions_overflow_and_spill():
     ts = np.sort(rng.integers(0, 200_000, n))
     keys = rng.integers(0, 3000, n)
     events = [(int(k), int(t), int(v)) for k, t, v in zip(keys, ts, rng.integers(0, 9, n))]
-    b, op = engine(events, 50, 30_000, 0, device="cuda", batch=2000, max_load=0.05,
+    b, op = engine(events, 50, 30_000, 5_000, device="cuda", batch=2000, max_load=0.05,
                    idle_spill_ms=2_000, cap_log2=6)
-    a2, _ = engine(events, 50, 30_000, 0, device="cpu", batch=2000)
+    a2, _ = engine(events, 50, 30_000, 5_000, device="cpu", batch=2000)
     assert a2 == b
     assert op.metrics.spilled_keys > 0 or op.metrics.overflow_keys > 0
