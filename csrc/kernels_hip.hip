@@ -1187,52 +1187,60 @@ struct __attribute__((aligned(32))) SessRec {
 };
 static_assert(sizeof(SessRec) == 32, "SessRec layout");
 
+// A slot's sessions in registers: fixed positions, valid iff cnt != 0. Every index below is a
+// compile-time constant (unrolled loops), so the state never spills to scratch.
 struct SessState {
   int64_t start[kSess], end[kSess];
   uint64_t acc[kSess];
   uint32_t cnt[kSess], flags[kSess];
-  int n;
 };
 
-// Merge candidate run (cs, ce, ca, cc) into the slot's sessions (lane-local, kSess unrolled).
-// Returns: 0 merged/inserted, 1 late-dropped, 2 overflow (more than kSess sessions).
+__device__ __forceinline__ int sess_count(const SessState& st) {
+  int n = 0;
+#pragma unroll
+  for (int j = 0; j < kSess; ++j) n += st.cnt[j] != 0;
+  return n;
+}
+
+// Merge candidate run (cs, ce, ca, cc) into the slot's sessions.
+// Returns: 0 merged/inserted, 1 late-dropped, 2 overflow (all kSess positions hold sessions
+// that do not intersect the candidate; the state is unchanged).
 __device__ __forceinline__ int sess_merge(SessState& st, int64_t cs, int64_t ce, uint64_t ca,
                                           uint32_t cc, const SessArgs& a) {
   int64_t ms = cs, me = ce;
   uint64_t macc = ca;
   uint32_t mcnt = cc, mflags = 0;
-  bool touched = false;
-  SessState rest;
-  rest.n = 0;
+  bool touched = false, any_free = false;
 #pragma unroll
   for (int j = 0; j < kSess; ++j) {
-    if (j >= st.n) break;
-    if (ms <= st.end[j] && me >= st.start[j]) {
+    if (st.cnt[j] && ms <= st.end[j] && me >= st.start[j]) {
       ms = ms < st.start[j] ? ms : st.start[j];
       me = me > st.end[j] ? me : st.end[j];
       macc = agg_combine(a.agg, st.acc[j], macc);
       mcnt += st.cnt[j];
       mflags |= st.flags[j];
       touched = true;
-    } else {
-      const int q = rest.n++;
-      rest.start[q] = st.start[j];
-      rest.end[q] = st.end[j];
-      rest.acc[q] = st.acc[j];
-      rest.cnt[q] = st.cnt[j];
-      rest.flags[q] = st.flags[j];
     }
+    any_free |= st.cnt[j] == 0;
   }
   if (!touched && (me - 1) + a.lateness <= a.wm) return 1;
-  if (rest.n >= kSess) return 2;
+  if (!touched && !any_free) return 2;
   if (mflags & 1u) mflags |= 2u;
-  const int q = rest.n++;
-  rest.start[q] = ms;
-  rest.end[q] = me;
-  rest.acc[q] = macc;
-  rest.cnt[q] = mcnt;
-  rest.flags[q] = mflags;
-  st = rest;
+  // Sessions absorbed into the merged one leave; the merged one takes the first free position.
+  bool placed = false;
+#pragma unroll
+  for (int j = 0; j < kSess; ++j) {
+    const bool absorbed = st.cnt[j] && ms <= st.end[j] && me >= st.start[j];
+    if (absorbed) st.cnt[j] = 0;
+    if (!placed && st.cnt[j] == 0) {
+      st.start[j] = ms;
+      st.end[j] = me;
+      st.acc[j] = macc;
+      st.cnt[j] = mcnt;
+      st.flags[j] = mflags;
+      placed = true;
+    }
+  }
   return 0;
 }
 
@@ -1240,7 +1248,7 @@ __device__ __forceinline__ int64_t sess_due(const SessState& st, int64_t latenes
   int64_t t = INT64_MAX;
 #pragma unroll
   for (int j = 0; j < kSess; ++j) {
-    if (j >= st.n) break;
+    if (!st.cnt[j]) continue;
     const int64_t maxts = st.end[j] - 1;
     const int64_t due = ((st.flags[j] & 1u) && !(st.flags[j] & 2u)) ? maxts + lateness : maxts;
     t = due < t ? due : t;
@@ -1251,18 +1259,23 @@ __device__ __forceinline__ int64_t sess_due(const SessState& st, int64_t latenes
 // A slot's kSess sessions are one 128-byte AoS record (one cache line): loads and stores are
 // four 32-byte accesses instead of 20 scattered ones.
 __device__ __forceinline__ void sess_load(SessState& st, const SessRec* r) {
-  st.n = 0;
 #pragma unroll
   for (int j = 0; j < kSess; ++j) {
     const SessRec x = r[j];
-    if (x.cnt) {
-      const int q = st.n++;
-      st.start[q] = x.start;
-      st.end[q] = x.end;
-      st.acc[q] = x.acc;
-      st.cnt[q] = x.cnt;
-      st.flags[q] = x.flags;
-    }
+    st.start[j] = x.start;
+    st.end[j] = x.end;
+    st.acc[j] = x.acc;
+    st.cnt[j] = x.cnt;
+    st.flags[j] = x.flags;
+  }
+}
+
+__device__ __forceinline__ void sess_clear(SessState& st) {
+#pragma unroll
+  for (int j = 0; j < kSess; ++j) {
+    st.start[j] = st.end[j] = 0;
+    st.acc[j] = 0;
+    st.cnt[j] = st.flags[j] = 0;
   }
 }
 
@@ -1270,17 +1283,11 @@ __device__ __forceinline__ void sess_store(const SessState& st, SessRec* r) {
 #pragma unroll
   for (int j = 0; j < kSess; ++j) {
     SessRec x;
-    if (j < st.n) {
-      x.start = st.start[j];
-      x.end = st.end[j];
-      x.acc = st.acc[j];
-      x.cnt = st.cnt[j];
-      x.flags = st.flags[j];
-    } else {
-      x.start = x.end = 0;
-      x.acc = 0;
-      x.cnt = x.flags = 0;
-    }
+    x.start = st.start[j];
+    x.end = st.end[j];
+    x.acc = st.acc[j];
+    x.cnt = st.cnt[j];
+    x.flags = st.cnt[j] ? st.flags[j] : 0u;
     r[j] = x;
   }
 }
@@ -1493,14 +1500,14 @@ __global__ __launch_bounds__(256) void session_fire_kernel(
     const bool due = slot < a.nslots && slot_due[slot] <= a.wm;
     if (!__ballot(due)) continue;
     SessState st;
-    st.n = 0;
+    sess_clear(st);
     if (due) sess_load(st, sess + slot * kSess);
     const uint64_t key = due ? keys_g[slot] : 0;
 #pragma unroll
     for (int j = 0; j < kSess; ++j) {
       bool emit = false;
       double val = 0.0;
-      if (due && j < st.n) {
+      if (due && st.cnt[j]) {
         const int64_t maxts = st.end[j] - 1;
         if (maxts <= a.wm && (!(st.flags[j] & 1u) || (st.flags[j] & 2u))) {
           const double v0 = agg_result_f64(a.agg, st.acc[j], st.cnt[j]);
@@ -1540,28 +1547,20 @@ __global__ __launch_bounds__(256) void session_fire_kernel(
     }
     if (due) {
       // Drop sessions past cleanup (maxTs + lateness <= wm).
-      SessState keep;
-      keep.n = 0;
 #pragma unroll
-      for (int j = 0; j < kSess; ++j) {
-        if (j < st.n && (st.end[j] - 1) + a.lateness > a.wm) {
-          const int q = keep.n++;
-          keep.start[q] = st.start[j];
-          keep.end[q] = st.end[j];
-          keep.acc[q] = st.acc[j];
-          keep.cnt[q] = st.cnt[j];
-          keep.flags[q] = st.flags[j];
-        }
-      }
-      sess_store(keep, sess + slot * kSess);
-      slot_due[slot] = sess_due(keep, a.lateness);
+      for (int j = 0; j < kSess; ++j)
+        if (st.cnt[j] && (st.end[j] - 1) + a.lateness <= a.wm) st.cnt[j] = 0;
+      sess_store(st, sess + slot * kSess);
+      slot_due[slot] = sess_due(st, a.lateness);
     }
   }
 }
 
 // Evict (spill) slots idle since before `idle_before` (or listed in `slots`): pack their key and
 // sessions into staging rows, tombstone the slot and insert the key into the spill set.
-__global__ __launch_bounds__(256) void session_evict_kernel(
+constexpr int kEvictBlock = 1024;
+
+__global__ __launch_bounds__(kEvictBlock) void session_evict_kernel(
     SessArgs a, uint64_t* __restrict__ keys_g, SessRec* __restrict__ sess, int64_t* __restrict__ slot_due,
     int64_t* __restrict__ slot_last, int64_t idle_before, const int64_t* __restrict__ slots,
     uint32_t nslots_list, uint64_t* __restrict__ spill_set, uint32_t spill_mask,
@@ -1582,37 +1581,54 @@ __global__ __launch_bounds__(256) void session_evict_kernel(
       take = key != kEmptyKey && key != kTombKey && (slots || slot_last[slot] < idle_before);
     }
     SessState st;
-    st.n = 0;
+    sess_clear(st);
     if (take) sess_load(st, sess + slot * kSess);
-    // Wave-aggregated row allocation (one atomic per wave): exclusive scan of st.n.
-    uint32_t x = take ? (uint32_t)st.n : 0u;
+    const int nst = sess_count(st);
+    // Block-aggregated row allocation: one global atomic per block iteration (same-address
+    // atomics serialize at L2; per-wave atomics made this kernel atomic-bound).
+    __shared__ uint32_t wsum[kEvictBlock / 64];
+    __shared__ uint32_t bdone;
+    const int wid = threadIdx.x >> 6;
+    uint32_t x = take ? (uint32_t)nst : 0u;
     uint32_t incl = x;
     for (int off = 1; off < 64; off <<= 1) {
       const uint32_t y = __shfl_up(incl, off);
       if (lane >= off) incl += y;
     }
-    const uint32_t wave_total = __shfl(incl, 63);
-    uint32_t wb = 0;
-    if (lane == 0 && wave_total) wb = atomicAdd(n_rows, wave_total);
-    wb = __shfl(wb, 0);
-    const uint32_t q = wb + incl - x;
+    if (lane == 63) wsum[wid] = incl;
+    if (threadIdx.x == 0) bdone = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t run = 0;
+      for (int w = 0; w < kEvictBlock / 64; ++w) {
+        const uint32_t t = wsum[w];
+        wsum[w] = run;
+        run += t;
+      }
+      const uint32_t base = run ? atomicAdd(n_rows, run) : 0u;
+      for (int w = 0; w < kEvictBlock / 64; ++w) wsum[w] += base;
+    }
+    __syncthreads();
+    const uint32_t q = wsum[wid] + incl - x;
     bool done = false;
-    if (take && st.n == 0) {  // no live session: free the slot, the key is not spilled
+    if (take && nst == 0) {  // no live session: free the slot, the key is not spilled
       done = true;
-    } else if (take && q + st.n <= row_cap) {
+    } else if (take && q + nst <= row_cap) {
+      uint32_t r = q;
 #pragma unroll
       for (int j = 0; j < kSess; ++j) {
-        if (j < st.n) {
-          st_key[q + j] = (int64_t)key;
-          st_start[q + j] = st.start[j];
-          st_end[q + j] = st.end[j];
-          st_acc[q + j] = (int64_t)st.acc[j];
-          st_cnt[q + j] = st.cnt[j];
-          st_flags[q + j] = st.flags[j];
+        if (st.cnt[j]) {
+          st_key[r] = (int64_t)key;
+          st_start[r] = st.start[j];
+          st_end[r] = st.end[j];
+          st_acc[r] = (int64_t)st.acc[j];
+          st_cnt[r] = st.cnt[j];
+          st_flags[r] = st.flags[j];
+          ++r;
         }
       }
       SessState empty;
-      empty.n = 0;
+      sess_clear(empty);
       sess_store(empty, sess + slot * kSess);
       set_insert(spill_set, spill_mask, key);
       done = true;
@@ -1623,7 +1639,10 @@ __global__ __launch_bounds__(256) void session_evict_kernel(
       keys_g[slot] = kTombKey;
     }
     const unsigned long long dm = __ballot(done);
-    if (lane == 0 && dm) atomicAdd(n_evicted, (uint32_t)__popcll(dm));
+    if (lane == 0 && dm) atomicAdd(&bdone, (uint32_t)__popcll(dm));
+    __syncthreads();
+    if (threadIdx.x == 0 && bdone) atomicAdd(n_evicted, bdone);
+    __syncthreads();  // wsum / bdone are rewritten by the next iteration
   }
 }
 
@@ -1973,7 +1992,8 @@ void session_evict(int64_t nslots, int cap_log2, uint64_t* keys_g, int64_t* sess
   const SessArgs a = make_sess_args(0, 0, 0, 0, 0, cap_log2, nslots);
   const int64_t total = slots ? (int64_t)nslots_list : nslots;
   if (total <= 0) return;
-  hipLaunchKernelGGL(session_evict_kernel, dim3(grid_for(total, 256, 8192)), dim3(256), 0,
+  hipLaunchKernelGGL(session_evict_kernel, dim3(grid_for(total, kEvictBlock, 2048)),
+                     dim3(kEvictBlock), 0,
                      (hipStream_t)stream, a, keys_g, reinterpret_cast<SessRec*>(sess),
                      slot_due, slot_last, idle_before, slots, nslots_list, spill_set, spill_mask,
                      st_key, st_start, st_end, st_acc, st_cnt, st_flags, n_rows, row_cap,
