@@ -234,27 +234,27 @@ PYBIND11_MODULE(_mxs_native, m) {
                                  int cap_log2, intptr_t keys_g, intptr_t spill_set,
                                  uint32_t spill_mask, int spill_any, intptr_t sk, intptr_t vals,
                                  intptr_t n_out, intptr_t host_recs, intptr_t n_host,
-                                 uint32_t host_cap, intptr_t n_ins, intptr_t stream) {
+                                 uint32_t host_cap, intptr_t n_ins, int tbits, intptr_t stream) {
     gpu::session_lookup(P<Rec>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2,
                         P<uint64_t>(keys_g), P<uint64_t>(spill_set), spill_mask, spill_any,
                         P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_out), P<Rec>(host_recs),
-                        P<uint32_t>(n_host), host_cap, P<uint32_t>(n_ins), stream);
+                        P<uint32_t>(n_host), host_cap, P<uint32_t>(n_ins), tbits, stream);
   });
   m.def("gpu_session_heads", [](intptr_t sk, intptr_t n_in, int64_t n_cap, intptr_t heads,
                                 intptr_t n_heads, intptr_t stream) {
     gpu::session_heads(P<int64_t>(sk), P<uint32_t>(n_in), n_cap, P<uint32_t>(heads),
                        P<uint32_t>(n_heads), stream);
   });
-  m.def("gpu_session_merge", [](intptr_t sk, intptr_t perm, intptr_t vals, intptr_t n_in,
-                                intptr_t long_heads, intptr_t n_long, int64_t n_cap, int64_t gap,
+  m.def("gpu_session_merge", [](intptr_t sk, intptr_t vals, intptr_t n_in, intptr_t long_heads,
+                                intptr_t n_long, int64_t n_cap, int tbits, int64_t gap,
                                 int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
                                 int64_t nslots, intptr_t sess, intptr_t slot_due,
                                 intptr_t slot_last, intptr_t late_cnt, intptr_t ovf_slots,
                                 intptr_t n_ovf, intptr_t ovf_rows, intptr_t n_ovf_runs,
                                 uint32_t ovf_cap, intptr_t stream) {
-    gpu::session_merge(P<int64_t>(sk), P<int64_t>(perm), P<uint64_t>(vals), P<uint32_t>(n_in),
-                       P<uint32_t>(long_heads), P<uint32_t>(n_long), n_cap, gap, lateness, wm,
-                       tbase, agg, cap_log2, nslots, P<int64_t>(sess), P<int64_t>(slot_due),
+    gpu::session_merge(P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_in),
+                       P<uint32_t>(long_heads), P<uint32_t>(n_long), n_cap, tbits, gap, lateness,
+                       wm, tbase, agg, cap_log2, nslots, P<int64_t>(sess), P<int64_t>(slot_due),
                        P<int64_t>(slot_last), P<uint64_t>(late_cnt), P<int64_t>(ovf_slots),
                        P<uint32_t>(n_ovf), P<int64_t>(ovf_rows), P<uint32_t>(n_ovf_runs), ovf_cap,
                        stream);
@@ -283,6 +283,13 @@ PYBIND11_MODULE(_mxs_native, m) {
                        P<int64_t>(st_start), P<int64_t>(st_end), P<int64_t>(st_acc),
                        P<int64_t>(st_cnt), P<int64_t>(st_flags), P<uint32_t>(n_rows), row_cap,
                        P<uint32_t>(n_evicted), stream);
+  });
+  m.def("gpu_sort_pairs_temp_bytes", &gpu::sort_pairs_temp_bytes);
+  m.def("gpu_sort_pairs", [](intptr_t temp, size_t temp_bytes, intptr_t kin, intptr_t kout,
+                             intptr_t vin, intptr_t vout, int64_t n, int begin_bit, int end_bit,
+                             intptr_t stream) {
+    gpu::sort_pairs(reinterpret_cast<void*>(temp), temp_bytes, P<uint64_t>(kin), P<uint64_t>(kout),
+                    P<uint64_t>(vin), P<uint64_t>(vout), n, begin_bit, end_bit, stream);
   });
   m.def("gpu_set_erase", [](intptr_t set, uint32_t mask, intptr_t keys, int64_t n,
                             intptr_t stream) {

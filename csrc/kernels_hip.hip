@@ -154,6 +154,9 @@ __device__ __forceinline__ int64_t block_reduce_i64(int64_t v, int64_t* red, int
 // ILP factor: each thread issues kPartU independent loads before it consumes any, so 16 waves
 // per CU keep ~16 x 64 x kPartU loads in flight (the loop was latency-bound at one chain).
 constexpr int kPartU = 8;
+// The plain-scatter kernel keeps key, ts and value of every unrolled element live across
+// part_eval: at 1024 threads (<= 128 VGPRs) 8 elements spilled to scratch, 4 do not.
+constexpr int kPlainU = 4;
 
 // Input-stream loads: V&1 = non-temporal (streamed once; keep L2 for the scatter's open lines).
 template <int V, class T>
@@ -177,16 +180,16 @@ __global__ __launch_bounds__(1024) void partition_kernel(
 
   const int64_t start = (int64_t)blockIdx.x * chunk;
   const int64_t end = start + chunk < n ? start + chunk : n;
-  const int64_t bstep = (int64_t)blockDim.x * kPartU;
+  const int64_t bstep = (int64_t)blockDim.x * kPlainU;
   int64_t tmax = INT64_MIN, qmin = INT64_MAX, qmax = INT64_MIN, nlate = 0, nacc = 0;
   bool bad = false;
 
   // Pass A: histogram + stats.
   for (int64_t i0 = start + threadIdx.x; i0 < end; i0 += bstep) {
-    uint64_t k[kPartU];
-    int64_t t[kPartU];
+    uint64_t k[kPlainU];
+    int64_t t[kPlainU];
 #pragma unroll
-    for (int u = 0; u < kPartU; ++u) {
+    for (int u = 0; u < kPlainU; ++u) {
       const int64_t i = i0 + (int64_t)u * blockDim.x;
       if (i < end) {
         k[u] = ldin<V>(&keys[i]);
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(1024) void partition_kernel(
       }
     }
 #pragma unroll
-    for (int u = 0; u < kPartU; ++u) {
+    for (int u = 0; u < kPlainU; ++u) {
       const int64_t i = i0 + (int64_t)u * blockDim.x;
       if (i >= end) break;
       tmax = t[u] > tmax ? t[u] : tmax;
@@ -235,10 +238,10 @@ __global__ __launch_bounds__(1024) void partition_kernel(
   // Pass B: scatter records into their bucket runs.
   const uint32_t bcap = plan.bucket_cap;
   for (int64_t i0 = start + threadIdx.x; i0 < end; i0 += bstep) {
-    uint64_t k[kPartU], v[kPartU];
-    int64_t t[kPartU];
+    uint64_t k[kPlainU], v[kPlainU];
+    int64_t t[kPlainU];
 #pragma unroll
-    for (int u = 0; u < kPartU; ++u) {
+    for (int u = 0; u < kPlainU; ++u) {
       const int64_t i = i0 + (int64_t)u * blockDim.x;
       if (i < end) {
         k[u] = ldin<V>(&keys[i]);
@@ -247,7 +250,7 @@ __global__ __launch_bounds__(1024) void partition_kernel(
       }
     }
 #pragma unroll
-    for (int u = 0; u < kPartU; ++u) {
+    for (int u = 0; u < kPlainU; ++u) {
       const int64_t i = i0 + (int64_t)u * blockDim.x;
       if (i >= end) break;
       const PartEval e = part_eval(k[u], t[u], jhash_tab, plan, kg_dest);
@@ -1055,6 +1058,7 @@ struct SessArgs {
   int64_t gap, lateness, wm, tbase;
   int32_t agg, cap_log2;
   int64_t nslots;
+  int32_t tbits;  // sort key = slot << tbits | (ts - tbase)
 };
 
 __device__ __forceinline__ bool set_contains(const uint64_t* set, uint32_t mask, uint64_t key) {
@@ -1083,13 +1087,16 @@ __device__ __forceinline__ void set_insert(uint64_t* set, uint32_t mask, uint64_
 // first tombstone seen on the way (else that empty slot). A lost CAS means another key was
 // inserted there: restart (each restart is someone else's progress). `inserted` counts claimed
 // empty slots only (tombstone reuse does not shorten the empty-slot budget).
+// kScope: __HIP_MEMORY_SCOPE_AGENT for a table in global memory, _WORKGROUP for one staged in
+// LDS (the same code then compiles to ds_read / ds_cmpst).
+template <int kScope = __HIP_MEMORY_SCOPE_AGENT>
 __device__ __forceinline__ uint32_t sess_probe_insert(uint64_t* keys, uint64_t key, uint32_t mask,
                                                       uint32_t* inserted) {
   const uint32_t s0 = (uint32_t)mix64(key) & mask;
   for (;;) {
     uint32_t s = s0, tomb = kNoSlot, target = kNoSlot;
     for (uint32_t i = 0; i <= mask; ++i) {
-      const uint64_t k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, kScope);
       if (k == key) return s;
       if (k == kTombKey) {
         if (tomb == kNoSlot) tomb = s;
@@ -1113,13 +1120,26 @@ __device__ __forceinline__ uint32_t sess_probe_insert(uint64_t* keys, uint64_t k
   }
 }
 
+// Read-only probe: the key's slot, or kNoSlot (first empty slot reached / table scanned).
+template <int kScope = __HIP_MEMORY_SCOPE_AGENT>
+__device__ __forceinline__ uint32_t sess_find(const uint64_t* keys, uint64_t key, uint32_t mask) {
+  uint32_t s = (uint32_t)mix64(key) & mask;
+  for (uint32_t i = 0; i <= mask; ++i) {
+    const uint64_t k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, kScope);
+    if (k == key) return s;
+    if (k == kEmptyKey) return kNoSlot;
+    s = (s + 1) & mask;
+  }
+  return kNoSlot;
+}
+
 __global__ __launch_bounds__(256) void session_lookup_kernel(
     const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
     uint32_t bucket_cap, int cap_log2, uint64_t* __restrict__ keys_g,
     uint64_t* __restrict__ spill_set, uint32_t spill_mask, int32_t spill_any,
     int64_t* __restrict__ sort_key, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
     Rec* __restrict__ host_recs, uint32_t* __restrict__ n_host, uint32_t host_cap,
-    uint32_t* __restrict__ n_inserted) {
+    uint32_t* __restrict__ n_inserted, int tbits) {
   const int b = blockIdx.y;
   const int sub = b % nsub;
   uint32_t c = counts[b];
@@ -1137,9 +1157,11 @@ __global__ __launch_bounds__(256) void session_lookup_kernel(
     const Rec r = seg[e];
     int64_t sk = INT64_MAX;
     if (r.t != 0xFFFFFFFFu) {
-      bool to_host = spill_any && set_contains(spill_set, spill_mask, r.key);
-      uint32_t s = kNoSlot;
-      if (!to_host) {
+      // Resident keys are found in the slot table (a key is never resident and spilled at once),
+      // so only keys missing from it pay the spill-set probe.
+      uint32_t s = sess_find(keys, r.key, mask);
+      bool to_host = s == kNoSlot && spill_any && set_contains(spill_set, spill_mask, r.key);
+      if (!to_host && s == kNoSlot) {
         s = sess_probe_insert(keys, r.key, mask, n_inserted);
         if (s == kNoSlot) {  // sub-table full: the key lives in host DRAM from now on
           to_host = true;
@@ -1151,12 +1173,78 @@ __global__ __launch_bounds__(256) void session_lookup_kernel(
         if (q < host_cap) host_recs[q] = r;
       } else {
         const uint64_t slot = ((uint64_t)sub << cap_log2) | s;
-        sk = (int64_t)((slot << 32) | r.t);
+        sk = (int64_t)((slot << tbits) | r.t);
       }
     }
     sort_key[base + (e - lo)] = sk;
     vals_out[base + (e - lo)] = r.val;
   }
+}
+
+// LDS variant (sub-tables of <= 8192 slots): one workgroup owns one sub-table for the whole
+// step -- its keys are staged in LDS, probed/inserted with ds_read/ds_cmpst, written back once.
+// Records of every source rank for that sub-table are handled by the same workgroup.
+constexpr int kSessLookupBlock = 512;
+constexpr int kSessLookupLdsMaxLog2 = 12;  // 32 KB of keys
+
+__global__ __launch_bounds__(kSessLookupBlock) void session_lookup_lds_kernel(
+    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
+    uint32_t bucket_cap, int cap_log2, uint64_t* __restrict__ keys_g,
+    uint64_t* __restrict__ spill_set, uint32_t spill_mask, int32_t spill_any,
+    int64_t* __restrict__ sort_key, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
+    Rec* __restrict__ host_recs, uint32_t* __restrict__ n_host, uint32_t host_cap,
+    uint32_t* __restrict__ n_inserted, int tbits) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t lkeys[];
+  __shared__ uint32_t base, lins;
+  const int sub = blockIdx.x;
+  const uint32_t cap = 1u << cap_log2, mask = cap - 1;
+  uint64_t* gkeys = keys_g + ((size_t)sub << cap_log2);
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) lkeys[i] = gkeys[i];
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int src = 0; src < nsrc; ++src) {
+      const uint32_t c = counts[src * nsub + sub];
+      tot += c < bucket_cap ? c : bucket_cap;
+    }
+    base = tot ? atomicAdd(n_out, tot) : 0u;
+    lins = 0;
+  }
+  __syncthreads();
+  uint32_t off = base;
+  for (int src = 0; src < nsrc; ++src) {
+    const int b = src * nsub + sub;
+    uint32_t c = counts[b];
+    c = c < bucket_cap ? c : bucket_cap;
+    const Rec* seg = recs + (size_t)b * bucket_cap;
+    for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
+      const Rec r = seg[e];
+      int64_t sk = INT64_MAX;
+      if (r.t != 0xFFFFFFFFu) {
+        uint32_t s = sess_find<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask);
+        bool to_host = s == kNoSlot && spill_any && set_contains(spill_set, spill_mask, r.key);
+        if (!to_host && s == kNoSlot) {
+          s = sess_probe_insert<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask, &lins);
+          if (s == kNoSlot) {  // sub-table full: the key lives in host DRAM from now on
+            to_host = true;
+            set_insert(spill_set, spill_mask, r.key);
+          }
+        }
+        if (to_host) {
+          const uint32_t q = atomicAdd(n_host, 1u);
+          if (q < host_cap) host_recs[q] = r;
+        } else {
+          const uint64_t slot = ((uint64_t)sub << cap_log2) | s;
+          sk = (int64_t)((slot << tbits) | r.t);
+        }
+      }
+      sort_key[off + e] = sk;
+      vals_out[off + e] = r.val;
+    }
+    off += c;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) gkeys[i] = lkeys[i];
+  if (threadIdx.x == 0 && n_inserted && lins) atomicAdd(n_inserted, lins);
 }
 
 __global__ __launch_bounds__(256) void session_heads_kernel(const int64_t* __restrict__ sk,
@@ -1347,19 +1435,20 @@ constexpr uint32_t kSessLongSeg = 96;  // segments longer than this go to the wa
 // per key and step, where a wave per key would idle most lanes. Long segments are queued for
 // session_merge_long_kernel.
 __global__ __launch_bounds__(256) void session_merge_small_kernel(
-    const int64_t* __restrict__ sk, const int64_t* __restrict__ perm,
+    const int64_t* __restrict__ sk,
     const uint64_t* __restrict__ vals, const uint32_t* __restrict__ n_in, SessArgs a, SessOut o,
     uint32_t* __restrict__ long_heads, uint32_t* __restrict__ n_long) {
   const uint32_t n = *n_in;
+  const int64_t tmask = ((int64_t)1 << a.tbits) - 1;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int64_t k = sk[i];
     if (k == INT64_MAX) continue;
-    const int64_t slot = k >> 32;
-    if (i > 0 && (sk[i - 1] >> 32) == slot) continue;  // not a segment head
+    const int64_t slot = k >> a.tbits;
+    if (i > 0 && (sk[i - 1] >> a.tbits) == slot) continue;  // not a segment head
     uint32_t j = i + 1;
     while (j < n && j - i <= kSessLongSeg) {
       const int64_t kj = sk[j];
-      if (kj == INT64_MAX || (kj >> 32) != slot) break;
+      if (kj == INT64_MAX || (kj >> a.tbits) != slot) break;
       ++j;
     }
     if (j - i > kSessLongSeg) {
@@ -1376,8 +1465,8 @@ __global__ __launch_bounds__(256) void session_merge_small_kernel(
     uint32_t pc = 0;
     int64_t ts = 0;
     for (uint32_t r = i; r < j; ++r) {
-      ts = a.tbase + (int64_t)(uint32_t)(sk[r] & 0xFFFFFFFF);
-      const uint64_t v = agg_lift(a.agg, vals[perm[r]]);
+      ts = a.tbase + (sk[r] & tmask);
+      const uint64_t v = agg_lift(a.agg, vals[r]);
       if (pv && ts <= pe) {
         pe = ts + a.gap;
         pa = agg_combine(a.agg, pa, v);
@@ -1399,7 +1488,7 @@ __global__ __launch_bounds__(256) void session_merge_small_kernel(
 // One wave per long key segment: lanes find the runs of their 64-record chunk (ts gaps > gap
 // split runs) and their accumulators with shuffles; lane 0 folds the runs in ts order.
 __global__ __launch_bounds__(256) void session_merge_long_kernel(
-    const int64_t* __restrict__ sk, const int64_t* __restrict__ perm,
+    const int64_t* __restrict__ sk,
     const uint64_t* __restrict__ vals, const uint32_t* __restrict__ n_in,
     const uint32_t* __restrict__ heads, const uint32_t* __restrict__ n_heads, SessArgs a,
     SessOut o) {
@@ -1409,7 +1498,8 @@ __global__ __launch_bounds__(256) void session_merge_long_kernel(
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   for (uint32_t h = wave; h < nh; h += nwaves) {
     const uint32_t start = heads[h];
-    const int64_t slot = sk[start] >> 32;
+    const int64_t slot = sk[start] >> a.tbits;
+    const int64_t tmask = ((int64_t)1 << a.tbits) - 1;
     SessState st;
     sess_load(st, o.sess + slot * kSess);
     uint64_t late = 0;
@@ -1423,11 +1513,11 @@ __global__ __launch_bounds__(256) void session_merge_long_kernel(
     uint32_t pc = 0;
     for (uint32_t b0 = start;; b0 += 64) {
       const uint32_t i = b0 + lane;
-      const bool in = i < n && sk[i] != INT64_MAX && (sk[i] >> 32) == slot;
+      const bool in = i < n && sk[i] != INT64_MAX && (sk[i] >> a.tbits) == slot;
       const unsigned long long inm = __ballot(in);
       if (!inm) break;
-      const int64_t ts = in ? a.tbase + (int64_t)(uint32_t)(sk[i] & 0xFFFFFFFF) : 0;
-      const uint64_t v = in ? agg_lift(a.agg, vals[perm[i]]) : 0;
+      const int64_t ts = in ? a.tbase + (sk[i] & tmask) : 0;
+      const uint64_t v = in ? agg_lift(a.agg, vals[i]) : 0;
       const int64_t prev_ts = __shfl_up(ts, 1);
       const bool head = in && (lane == 0 || ts > prev_ts + a.gap);
       // Segmented inclusive scan of (acc, cnt) over runs.
@@ -1918,8 +2008,9 @@ void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_
 
 
 static SessArgs make_sess_args(int64_t gap, int64_t lateness, int64_t wm, int64_t tbase, int agg,
-                               int cap_log2, int64_t nslots) {
+                               int cap_log2, int64_t nslots, int tbits = 32) {
   SessArgs a;
+  a.tbits = tbits;
   a.gap = gap;
   a.lateness = lateness;
   a.wm = wm;
@@ -1933,13 +2024,23 @@ static SessArgs make_sess_args(int64_t gap, int64_t lateness, int64_t wm, int64_
 void session_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bcap,
                     int cap_log2, uint64_t* keys_g, uint64_t* spill_set, uint32_t spill_mask,
                     int spill_any, int64_t* sk, uint64_t* vals, uint32_t* n_out, Rec* host_recs,
-                    uint32_t* n_host, uint32_t host_cap, uint32_t* n_inserted, intptr_t stream) {
+                    uint32_t* n_host, uint32_t host_cap, uint32_t* n_inserted, int tbits,
+                    intptr_t stream) {
   if (nsrc * nsub <= 0) return;
-  const uint32_t chunks = (bcap + kLookupChunk - 1) / kLookupChunk;
-  hipLaunchKernelGGL(session_lookup_kernel, dim3(chunks, nsrc * nsub), dim3(256), 0,
-                     (hipStream_t)stream, recs, counts, nsrc, nsub, bcap, cap_log2, keys_g,
-                     spill_set, spill_mask, spill_any, sk, vals, n_out, host_recs, n_host,
-                     host_cap, n_inserted);
+  if (tbits < 1 || tbits > 32) throw std::invalid_argument("session_lookup: tbits out of range");
+  if (cap_log2 <= kSessLookupLdsMaxLog2) {
+    const size_t lds = (size_t)sizeof(uint64_t) << cap_log2;
+    hipLaunchKernelGGL(session_lookup_lds_kernel, dim3(nsub), dim3(kSessLookupBlock), lds,
+                       (hipStream_t)stream, recs, counts, nsrc, nsub, bcap, cap_log2, keys_g,
+                       spill_set, spill_mask, spill_any, sk, vals, n_out, host_recs, n_host,
+                       host_cap, n_inserted, tbits);
+  } else {
+    const uint32_t chunks = (bcap + kLookupChunk - 1) / kLookupChunk;
+    hipLaunchKernelGGL(session_lookup_kernel, dim3(chunks, nsrc * nsub), dim3(256), 0,
+                       (hipStream_t)stream, recs, counts, nsrc, nsub, bcap, cap_log2, keys_g,
+                       spill_set, spill_mask, spill_any, sk, vals, n_out, host_recs, n_host,
+                       host_cap, n_inserted, tbits);
+  }
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1950,21 +2051,21 @@ void session_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint3
   HIP_CHECK(hipGetLastError());
 }
 
-void session_merge(const int64_t* sk, const int64_t* perm, const uint64_t* vals,
-                   const uint32_t* n_in, uint32_t* long_heads, uint32_t* n_long,
-                   int64_t n_cap, int64_t gap, int64_t lateness, int64_t wm, int64_t tbase,
-                   int agg, int cap_log2, int64_t nslots, int64_t* sess, int64_t* slot_due,
-                   int64_t* slot_last, uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf,
-                   int64_t* ovf_rows, uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream) {
-  const SessArgs a = make_sess_args(gap, lateness, wm, tbase, agg, cap_log2, nslots);
+void session_merge(const int64_t* sk, const uint64_t* vals, const uint32_t* n_in,
+                   uint32_t* long_heads, uint32_t* n_long, int64_t n_cap, int tbits, int64_t gap,
+                   int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
+                   int64_t nslots, int64_t* sess, int64_t* slot_due, int64_t* slot_last,
+                   uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf, int64_t* ovf_rows,
+                   uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream) {
+  const SessArgs a = make_sess_args(gap, lateness, wm, tbase, agg, cap_log2, nslots, tbits);
   const SessOut o{reinterpret_cast<SessRec*>(sess), slot_due, slot_last, late_cnt,
                   ovf_slots, n_ovf, ovf_rows, n_ovf_runs, ovf_cap};
   hipLaunchKernelGGL(session_merge_small_kernel, dim3(grid_for(n_cap, 256, 16384)), dim3(256), 0,
-                     (hipStream_t)stream, sk, perm, vals, n_in, a, o, long_heads, n_long);
+                     (hipStream_t)stream, sk, vals, n_in, a, o, long_heads, n_long);
   HIP_CHECK(hipGetLastError());
   // Long segments (hot keys): a wave each; the count stays on the device (grid-stride waves).
   hipLaunchKernelGGL(session_merge_long_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, sk,
-                     perm, vals, n_in, long_heads, n_long, a, o);
+                     vals, n_in, long_heads, n_long, a, o);
   HIP_CHECK(hipGetLastError());
 }
 

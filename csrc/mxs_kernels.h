@@ -87,15 +87,16 @@ void rolling_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint3
 void session_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bcap,
                     int cap_log2, uint64_t* keys_g, uint64_t* spill_set, uint32_t spill_mask,
                     int spill_any, int64_t* sk, uint64_t* vals, uint32_t* n_out, Rec* host_recs,
-                    uint32_t* n_host, uint32_t host_cap, uint32_t* n_inserted, intptr_t stream);
+                    uint32_t* n_host, uint32_t host_cap, uint32_t* n_inserted, int tbits,
+                    intptr_t stream);
 void session_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
                    uint32_t* n_heads, intptr_t stream);
-void session_merge(const int64_t* sk, const int64_t* perm, const uint64_t* vals,
-                   const uint32_t* n_in, uint32_t* long_heads, uint32_t* n_long,
-                   int64_t n_cap, int64_t gap, int64_t lateness, int64_t wm, int64_t tbase,
-                   int agg, int cap_log2, int64_t nslots, int64_t* sess, int64_t* slot_due,
-                   int64_t* slot_last, uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf,
-                   int64_t* ovf_rows, uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream);
+void session_merge(const int64_t* sk, const uint64_t* vals, const uint32_t* n_in,
+                   uint32_t* long_heads, uint32_t* n_long, int64_t n_cap, int tbits, int64_t gap,
+                   int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
+                   int64_t nslots, int64_t* sess, int64_t* slot_due, int64_t* slot_last,
+                   uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf, int64_t* ovf_rows,
+                   uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream);
 void session_fire(int64_t gap, int64_t lateness, int64_t wm, int agg, int cap_log2,
                   int64_t nslots, const uint64_t* keys_g, int64_t* sess, int64_t* slot_due,
                   const ExprProg& map, const ExprProg& filt, uint64_t* out_key, int64_t* out_start,
@@ -107,6 +108,10 @@ void session_evict(int64_t nslots, int cap_log2, uint64_t* keys_g, int64_t* sess
                    int64_t* st_start, int64_t* st_end, int64_t* st_acc, int64_t* st_cnt,
                    int64_t* st_flags, uint32_t* n_rows, uint32_t row_cap, uint32_t* n_evicted,
                    intptr_t stream);
+size_t sort_pairs_temp_bytes(int64_t n, int begin_bit, int end_bit);
+void sort_pairs(void* temp, size_t temp_bytes, const uint64_t* keys_in, uint64_t* keys_out,
+                const uint64_t* vals_in, uint64_t* vals_out, int64_t n, int begin_bit, int end_bit,
+                intptr_t stream);
 void set_erase(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, intptr_t stream);
 void session_rehash(int64_t nslots, int cap_log2, const uint64_t* keys_o, const int64_t* sess_o,
                     const int64_t* due_o, const int64_t* last_o, uint64_t* keys_n, int64_t* sess_n,

@@ -140,9 +140,17 @@ class SessionStore {
     auto C = cnts.data();
     auto F = flags.data();
     ColdChunk ch;
+    if (cold) {
+      ch.key.reserve(n);
+      ch.start.reserve(n);
+      ch.end.reserve(n);
+      ch.acc.reserve(n);
+      ch.cnt.reserve(n);
+    }
+    const bool no_hot = m_.empty();
     for (int64_t i = 0; i < n; ++i) {
       const uint64_t key = (uint64_t)K[i];
-      if (cold && F[i] == 1 && m_.find(key) == m_.end()) {
+      if (cold && F[i] == 1 && (no_hot || m_.find(key) == m_.end())) {
         ch.key.push_back(key);
         ch.start.push_back(S[i]);
         ch.end.push_back(E[i]);

@@ -188,6 +188,7 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
         step()
     _sync(dev)
     lat.clear()
+    op.phase_s.clear()
     m0 = dict(op.metrics.__dict__)
     t0 = time.perf_counter()
     alerts = 0
@@ -206,8 +207,8 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
             "host_store_bytes": op.host_bytes(), "resident_keys": op.resident_keys() if op.gpu else 0,
             "hbm_state_bytes": op.state_bytes() - op.host_bytes(), "events_per_step": batch,
             "active_keys": active, "table_keys": table_keys, "device": str(dev),
-            "host_phase_ms_per_step": {k: round(v * 1e3 / max(1, mt.steps), 2)
-                                       for k, v in op.phase_s.items()}}
+            "host_phase_ms_per_step": {k: round(v * 1e3 / steps, 2)
+                                       for k, v in sorted(op.phase_s.items())}}
 
 
 def main(argv=None) -> int:

@@ -180,6 +180,9 @@ class KeyedSessionOperator:
             total = self.nbuckets * self.bucket_cap
             self.sort_key = torch.empty(total, dtype=torch.int64, device=dev)
             self.vals_buf = torch.empty(total, dtype=torch.int64, device=dev)
+            self.sort_out = torch.empty(total, dtype=torch.int64, device=dev)
+            self.vals_out = torch.empty(total, dtype=torch.int64, device=dev)
+            self._sort_tmp = None
             self.heads = torch.empty(total, dtype=torch.int32, device=dev)
             self.host_cap = total
             self.host_recs = torch.empty(total * K.REC_WORDS, dtype=torch.int64, device=dev)
@@ -253,7 +256,7 @@ class KeyedSessionOperator:
         self.metrics.steps += 1
         if self.gpu:
             with self._phase("fold_gpu"):
-                self._fold_gpu(tbase, old_wm)
+                self._fold_gpu(tbase, old_wm, max(0, -host[0]))
         else:
             self._fold_cpu(tbase, old_wm)
         # Sessions that late data re-opened fire even when the watermark did not move
@@ -325,8 +328,11 @@ class KeyedSessionOperator:
     def _st(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
-    def _fold_gpu(self, tbase: int, wm: int) -> None:
+    def _fold_gpu(self, tbase: int, wm: int, tspan: int) -> None:
+        """tspan: the step's largest ts - tbase over all ranks (sizes the sort key's time bits)."""
         m, st, c = self.native, self._st(), self.ctr
+        tbits = min(32, max(1, int(tspan).bit_length()))  # (no records: tspan is meaningless)
+        sbits = self.nslots.bit_length()  # one spare bit: valid keys stay below the sentinel
         if self._live_estimate > 0.9 * self.nslots:
             self._join_spill()
             # Sub-tables may fill up: room in the spill set for every key the lookup may divert.
@@ -338,13 +344,20 @@ class KeyedSessionOperator:
                              self.spill_set.data_ptr(), self.spill_set.numel() - 1,
                              int(self.spill_any), self.sort_key.data_ptr(), self.vals_buf.data_ptr(),
                              c[0:1].data_ptr(), self.host_recs.data_ptr(), c[2:3].data_ptr(),
-                             self.host_cap, 0, st)
+                             self.host_cap, 0, tbits, st)
         total = int(c[0].item())
         if total:
-            sk, perm = torch.sort(self.sort_key[:total])
-            m.gpu_session_merge(sk.data_ptr(), perm.data_ptr(), self.vals_buf.data_ptr(),
+            # Key-value radix sort over the used bits only (slot | ts - tbase); values ride along.
+            nbits = tbits + sbits
+            need = m.gpu_sort_pairs_temp_bytes(total, 0, nbits)
+            if self._sort_tmp is None or self._sort_tmp.numel() < need:
+                self._sort_tmp = torch.empty(need, dtype=torch.uint8, device=self.device)
+            m.gpu_sort_pairs(self._sort_tmp.data_ptr(), self._sort_tmp.numel(),
+                             self.sort_key.data_ptr(), self.sort_out.data_ptr(),
+                             self.vals_buf.data_ptr(), self.vals_out.data_ptr(), total, 0, nbits, st)
+            m.gpu_session_merge(self.sort_out.data_ptr(), self.vals_out.data_ptr(),
                                 c[0:1].data_ptr(), self.heads.data_ptr(), c[1:2].data_ptr(),
-                                total, self.gap, self.lateness, wm, tbase,
+                                total, tbits, self.gap, self.lateness, wm, tbase,
                                 self.agg, self.cap_log2, self.nslots, self.sess.data_ptr(),
                                 self.slot_due.data_ptr(),
                                 self.slot_last.data_ptr(), self.late_cnt.data_ptr(),
@@ -420,19 +433,25 @@ class KeyedSessionOperator:
                             c[7:8].data_ptr(), R, c[8:9].data_ptr(), st)
         self.spill_any = True
         with self._phase("spill.evict_kernel"):
-            nr, ne = self.ctr[7:9].cpu().tolist()
-        nr = min(nr, R)
+            nr_all, ne = self.ctr[7:9].cpu().tolist()
+        nr = min(nr_all, R)
         h = None
         if nr:
-            # Six contiguous DMA copies into pinned host memory.
+            t0 = time.perf_counter()
+            # Six contiguous DMA copies into pinned host memory; the host store reads the pinned
+            # rows in place (the buffer is reused only after the insert has been joined).
             for j in range(6):
                 self._pin_rows[j, :nr].copy_(rows[j, :nr], non_blocking=True)
             torch.cuda.current_stream(self.device).synchronize()
-            h = self._pin_rows[:, :nr].numpy()
-            h = np.ascontiguousarray(h[:, h[4] > 0])  # skipped rows (no staging room) stay zero
-        nk = int((h[0][1:] != h[0][:-1]).sum()) + 1 if h is not None and h.shape[1] else 0
+            pin = self._pin_rows.numpy()
+            h = [pin[j, :nr] for j in range(6)]
+            if nr_all > R:  # staging overflowed: rows of skipped slots stay zero (cnt == 0)
+                ok = h[4] > 0
+                h = [np.ascontiguousarray(x[ok]) for x in h]
+            self.phase_s["spill.d2h"] += time.perf_counter() - t0
+        nk = int(np.count_nonzero(h[0][1:] != h[0][:-1])) + 1 if h is not None and len(h[0]) else 0
         self._apply_spill((nk, ne))
-        if h is None or not h.shape[1]:
+        if h is None or not len(h[0]):
             return
         cold = slots is None  # idle keys: fired-and-unmodified sessions go to a cold chunk
         if not cold:
@@ -500,8 +519,9 @@ class KeyedSessionOperator:
 
     def _maybe_spill(self, wm: int) -> None:
         k = self.keys_g
-        live, occupied = torch.stack([((k != EMPTY_KEY) & (k != TOMB_KEY)).sum(),
-                                      (k != EMPTY_KEY).sum()]).tolist()
+        with self._phase("spill.occupancy"):
+            live, occupied = torch.stack([((k != EMPTY_KEY) & (k != TOMB_KEY)).sum(),
+                                          (k != EMPTY_KEY).sum()]).tolist()
         self._live_estimate = int(live)
         if occupied > 0.85 * self.nslots and live < 0.6 * self.nslots:
             self._rehash()
