@@ -208,27 +208,28 @@ PYBIND11_MODULE(_mxs_native, m) {
   });
   m.def("gpu_rolling_lookup", [](intptr_t recs, intptr_t counts, int nsrc, int nsub, uint32_t bcap,
                                  int cap_log2, intptr_t keys_g, intptr_t sk, intptr_t vals,
-                                 intptr_t n_out, intptr_t flags, intptr_t stream) {
+                                 intptr_t n_out, intptr_t flags, int abits, int shift,
+                                 intptr_t stream) {
     gpu::rolling_lookup(P<Rec>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2,
                         P<uint64_t>(keys_g), P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_out),
-                        P<uint32_t>(flags), stream);
+                        P<uint32_t>(flags), abits, shift, stream);
   });
   m.def("gpu_rolling_heads", [](intptr_t sk, intptr_t n_in, int64_t n_cap, intptr_t heads,
-                                intptr_t n_heads, intptr_t stream) {
+                                intptr_t n_heads, int shift, intptr_t stream) {
     gpu::rolling_heads(P<int64_t>(sk), P<uint32_t>(n_in), n_cap, P<uint32_t>(heads),
-                       P<uint32_t>(n_heads), stream);
+                       P<uint32_t>(n_heads), shift, stream);
   });
   m.def("gpu_rolling_scan", [](int agg, intptr_t sk, intptr_t perm, intptr_t vals, intptr_t n_in,
                                intptr_t heads, intptr_t n_heads, int64_t max_segments,
                                intptr_t acc_g, intptr_t cnt_g, intptr_t keys_g,
                                std::vector<int32_t> code, std::vector<double> consts,
                                intptr_t ok, intptr_t ov, intptr_t ot, intptr_t on,
-                               uint32_t out_cap, intptr_t stream) {
+                               uint32_t out_cap, int abits, int shift, intptr_t stream) {
     gpu::rolling_scan(agg, P<int64_t>(sk), P<int64_t>(perm), P<uint64_t>(vals), P<uint32_t>(n_in),
                       P<uint32_t>(heads), P<uint32_t>(n_heads), max_segments, P<uint64_t>(acc_g),
                       P<uint32_t>(cnt_g), P<uint64_t>(keys_g), make_prog(code, consts),
                       P<uint64_t>(ok), P<uint64_t>(ov), P<int64_t>(ot), P<uint32_t>(on), out_cap,
-                      stream);
+                      abits, shift, stream);
   });
   m.def("gpu_session_lookup", [](intptr_t recs, intptr_t counts, int nsrc, int nsub, uint32_t bcap,
                                  int cap_log2, intptr_t keys_g, intptr_t spill_set,

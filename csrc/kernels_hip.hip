@@ -910,7 +910,7 @@ __global__ __launch_bounds__(256) void rolling_lookup_kernel(
     const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
     uint32_t bucket_cap, int cap_log2, uint64_t* __restrict__ keys_g,
     int64_t* __restrict__ sort_key, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
-    uint32_t* __restrict__ flags) {
+    uint32_t* __restrict__ flags, int abits, int shift) {
   const int b = blockIdx.y;  // = src * nsub + sub
   const int src = b / nsub, sub = b % nsub;
   uint32_t c = counts[b];
@@ -933,7 +933,7 @@ __global__ __launch_bounds__(256) void rolling_lookup_kernel(
         atomicOr(&flags[0], 1u);
       } else {
         const uint64_t slot = ((uint64_t)sub << cap_log2) | s;
-        sk = (int64_t)((slot << 40) | ((uint64_t)src << 32) | r.aux);
+        sk = (int64_t)((slot << shift) | ((uint64_t)src << abits) | r.aux);
       }
     }
     sort_key[base + (e - lo)] = sk;
@@ -944,14 +944,15 @@ __global__ __launch_bounds__(256) void rolling_lookup_kernel(
 __global__ __launch_bounds__(256) void rolling_heads_kernel(const int64_t* __restrict__ sk,
                                                             const uint32_t* __restrict__ n_in,
                                                             uint32_t* __restrict__ heads,
-                                                            uint32_t* __restrict__ n_heads) {
+                                                            uint32_t* __restrict__ n_heads,
+                                                            int shift) {
   const uint32_t n = *n_in;
   for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
     const uint32_t i = base + threadIdx.x;
     bool h = false;
     if (i < n) {
       const int64_t k = sk[i];
-      h = k != INT64_MAX && (i == 0 || (sk[i - 1] >> 40) != (k >> 40));
+      h = k != INT64_MAX && (i == 0 || (sk[i - 1] >> shift) != (k >> shift));
     }
     const unsigned long long m = __ballot(h);
     uint32_t wb = 0;
@@ -973,7 +974,8 @@ __global__ __launch_bounds__(256) void rolling_scan_kernel(
     const uint32_t* __restrict__ heads, const uint32_t* __restrict__ n_heads,
     uint64_t* __restrict__ acc_g, uint32_t* __restrict__ cnt_g, const uint64_t* __restrict__ keys_g,
     ExprProg filt, uint64_t* __restrict__ out_key, uint64_t* __restrict__ out_val,
-    int64_t* __restrict__ out_tag, uint32_t* __restrict__ out_n, uint32_t out_cap) {
+    int64_t* __restrict__ out_tag, uint32_t* __restrict__ out_n, uint32_t out_cap, int abits,
+    int shift) {
   extern __shared__ __attribute__((aligned(16))) double rsm[];  // VM columns [8 + depth][256]
   LdsCol vars{rsm + threadIdx.x, 256};
   LdsCol stack{rsm + kExprVars * 256 + threadIdx.x, 256};
@@ -983,12 +985,12 @@ __global__ __launch_bounds__(256) void rolling_scan_kernel(
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   for (uint32_t h = wave; h < nh; h += nwaves) {  // wave-uniform loop
     const uint32_t start = heads[h];
-    const uint64_t slot = (uint64_t)(sk[start] >> 40);
+    const uint64_t slot = (uint64_t)(sk[start] >> shift);
     uint32_t end = start + 1;
     // Segment end: next record with a different slot (scan forward a wave at a time).
     for (;;) {
       const uint32_t i = end + lane;
-      const bool same = i < n && (uint64_t)(sk[i] >> 40) == slot && sk[i] != INT64_MAX;
+      const bool same = i < n && (uint64_t)(sk[i] >> shift) == slot && sk[i] != INT64_MAX;
       const unsigned long long m = __ballot(!same);
       if (m) {
         end += (uint32_t)__ffsll((long long)m) - 1;
@@ -1004,7 +1006,8 @@ __global__ __launch_bounds__(256) void rolling_scan_kernel(
     for (uint32_t b0 = start; b0 < end; b0 += 64) {
       const uint32_t i = b0 + lane;
       const bool in = i < end;
-      uint64_t v = in ? agg_lift(AGG, vals[perm[i]]) : 0;
+      // perm == nullptr: values were sorted along with the keys.
+      uint64_t v = in ? agg_lift(AGG, vals[perm ? perm[i] : i]) : 0;
       // Inclusive wave scan (Hillis-Steele) over the ordered chunk.
       for (int o = 1; o < 64; o <<= 1) {
         const uint64_t y = __shfl_up(v, o);
@@ -1031,7 +1034,9 @@ __global__ __launch_bounds__(256) void rolling_scan_kernel(
         if (q < out_cap) {
           out_key[q] = key;
           out_val[q] = AGG == AGG_COUNT ? (uint64_t)pcount : post;
-          out_tag[q] = sk[i] & 0xFFFFFFFFFFll;  // src << 32 | arrival index
+          const int64_t k = sk[i];
+          const int64_t srcv = (k >> abits) & (((int64_t)1 << (shift - abits)) - 1);
+          out_tag[q] = (srcv << 32) | (k & (((int64_t)1 << abits) - 1));  // src << 32 | arrival
         }
       }
       carry = __shfl(post, (int)nin - 1);
@@ -1959,22 +1964,29 @@ void rolling(const Rec*, const uint32_t*, const RollPlan&, uint64_t*, uint64_t*,
   throw std::runtime_error("gpu::rolling: use rolling_lookup / rolling_heads / rolling_scan");
 }
 
+static void check_roll_layout(int abits, int shift) {
+  if (abits < 1 || abits > 32 || shift < abits || shift > 40)
+    throw std::invalid_argument("rolling sort-key layout out of range");
+}
+
 void rolling_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
                     uint32_t bucket_cap, int cap_log2, uint64_t* keys_g, int64_t* sort_key,
-                    uint64_t* vals_out, uint32_t* n_out, uint32_t* flags, intptr_t stream) {
+                    uint64_t* vals_out, uint32_t* n_out, uint32_t* flags, int abits, int shift,
+                    intptr_t stream) {
   if (nsrc * nsub <= 0) return;
+  check_roll_layout(abits, shift);
   const uint32_t chunks = (bucket_cap + kLookupChunk - 1) / kLookupChunk;
   hipLaunchKernelGGL(rolling_lookup_kernel, dim3(chunks, nsrc * nsub), dim3(256), 0,
                      (hipStream_t)stream,
                      recs, counts, nsrc, nsub, bucket_cap, cap_log2, keys_g, sort_key, vals_out,
-                     n_out, flags);
+                     n_out, flags, abits, shift);
   HIP_CHECK(hipGetLastError());
 }
 
 void rolling_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
-                   uint32_t* n_heads, intptr_t stream) {
+                   uint32_t* n_heads, int shift, intptr_t stream) {
   hipLaunchKernelGGL(rolling_heads_kernel, dim3(grid_for(n_cap, 256, 8192)), dim3(256), 0,
-                     (hipStream_t)stream, sk, n_in, heads, n_heads);
+                     (hipStream_t)stream, sk, n_in, heads, n_heads, shift);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1983,21 +1995,23 @@ static void launch_roll(const int64_t* sk, const int64_t* perm, const uint64_t* 
                         const uint32_t* n_in, const uint32_t* heads, const uint32_t* n_heads,
                         uint64_t* acc_g, uint32_t* cnt_g, const uint64_t* keys_g,
                         const ExprProg& filt, uint64_t* ok, uint64_t* ov, int64_t* ot,
-                        uint32_t* on, uint32_t cap, int grid, size_t lds, hipStream_t s) {
+                        uint32_t* on, uint32_t cap, int grid, size_t lds, int abits, int shift,
+                        hipStream_t s) {
   hipLaunchKernelGGL(rolling_scan_kernel<AGG>, dim3(grid), dim3(256), lds, s, sk, perm, vals, n_in,
-                     heads, n_heads, acc_g, cnt_g, keys_g, filt, ok, ov, ot, on, cap);
+                     heads, n_heads, acc_g, cnt_g, keys_g, filt, ok, ov, ot, on, cap, abits, shift);
 }
 
 void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_t* vals,
                   const uint32_t* n_in, const uint32_t* heads, const uint32_t* n_heads,
                   int64_t max_segments, uint64_t* acc_g, uint32_t* cnt_g, const uint64_t* keys_g,
                   const ExprProg& filt, uint64_t* out_key, uint64_t* out_val, int64_t* out_tag,
-                  uint32_t* out_n, uint32_t out_cap, intptr_t stream) {
+                  uint32_t* out_n, uint32_t out_cap, int abits, int shift, intptr_t stream) {
+  check_roll_layout(abits, shift);
   const int grid = grid_for(max_segments * 64, 256, 4096);
   const size_t lds = (size_t)(kExprVars + filt.depth) * 256 * sizeof(double);
   hipStream_t s = (hipStream_t)stream;
   switch (agg) {
-#define MXS_R(A) case A: launch_roll<A>(sk, perm, vals, n_in, heads, n_heads, acc_g, cnt_g, keys_g, filt, out_key, out_val, out_tag, out_n, out_cap, grid, lds, s); break;
+#define MXS_R(A) case A: launch_roll<A>(sk, perm, vals, n_in, heads, n_heads, acc_g, cnt_g, keys_g, filt, out_key, out_val, out_tag, out_n, out_cap, grid, lds, abits, shift, s); break;
     MXS_R(AGG_SUM_I64) MXS_R(AGG_SUM_F64) MXS_R(AGG_MIN_I64) MXS_R(AGG_MAX_I64)
     MXS_R(AGG_MIN_F64) MXS_R(AGG_MAX_F64) MXS_R(AGG_COUNT)
 #undef MXS_R

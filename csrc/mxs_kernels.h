@@ -81,9 +81,10 @@ void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep
 void step_begin(uint32_t* cursor, int nb, int64_t* stats, intptr_t stream);
 void rolling_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
                     uint32_t bucket_cap, int cap_log2, uint64_t* keys_g, int64_t* sort_key,
-                    uint64_t* vals_out, uint32_t* n_out, uint32_t* flags, intptr_t stream);
+                    uint64_t* vals_out, uint32_t* n_out, uint32_t* flags, int abits, int shift,
+                    intptr_t stream);
 void rolling_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
-                   uint32_t* n_heads, intptr_t stream);
+                   uint32_t* n_heads, int shift, intptr_t stream);
 void session_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bcap,
                     int cap_log2, uint64_t* keys_g, uint64_t* spill_set, uint32_t spill_mask,
                     int spill_any, int64_t* sk, uint64_t* vals, uint32_t* n_out, Rec* host_recs,
@@ -120,7 +121,7 @@ void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_
                   const uint32_t* n_in, const uint32_t* heads, const uint32_t* n_heads,
                   int64_t max_segments, uint64_t* acc_g, uint32_t* cnt_g, const uint64_t* keys_g,
                   const ExprProg& filt, uint64_t* out_key, uint64_t* out_val, int64_t* out_tag,
-                  uint32_t* out_n, uint32_t out_cap, intptr_t stream);
+                  uint32_t* out_n, uint32_t out_cap, int abits, int shift, intptr_t stream);
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
                  int64_t proc_now, int64_t* red, intptr_t stream);
 }  // namespace gpu

@@ -89,6 +89,9 @@ class KeyedRollingOperator:
         total = self.nbuckets * self.bucket_cap
         self.sort_key = torch.empty(total, dtype=torch.int64, device=dev)
         self.vals_buf = torch.empty(total, dtype=torch.int64, device=dev)
+        self.sort_out = torch.empty(total, dtype=torch.int64, device=dev)
+        self.vals_out = torch.empty(total, dtype=torch.int64, device=dev)
+        self._sort_tmp = None
         self.heads = torch.empty(total, dtype=torch.int32, device=dev)
         self.n_buf = torch.zeros(2, dtype=torch.int32, device=dev)
         ocap = self.emit_capacity or total
@@ -113,11 +116,13 @@ class KeyedRollingOperator:
                             self.stats)
             K.step_finish(self.stats, self.local_maxts, self.red, bound=0, event_mode=True,
                           proc_now=0)
-            self.comm.allreduce_min_(self.red[3:4])
+            self.red[5] = -n  # the largest batch over ranks sizes the arrival bits of the sort key
+            self.comm.allreduce_min_(self.red[3:6])
             if self.world > 1:
                 self.comm.all_to_all(self.recv, self.send)
                 self.comm.all_to_all(self.recv_counts, self.cursor)
-            if int(self.red[3].item()):
+            red = self.red[3:6].tolist()
+            if red[0]:
                 self._alloc(self.batch_capacity, self.slack * 2)
                 continue
             break
@@ -130,25 +135,35 @@ class KeyedRollingOperator:
         if self.device.type == "cuda":
             st = torch.cuda.current_stream(self.device).cuda_stream
             self.n_buf.zero_()
+            abits = max(1, int(-red[2] - 1).bit_length())
+            shift = abits + max(0, (self.world - 1).bit_length())
             m.gpu_rolling_lookup(self.recv.data_ptr(), self.recv_counts.data_ptr(), self.world,
                                  self.nsub, self.bucket_cap, self.cap_log2, self.keys_g.data_ptr(),
                                  self.sort_key.data_ptr(), self.vals_buf.data_ptr(),
-                                 self.n_buf.data_ptr(), self.flags.data_ptr(), st)
+                                 self.n_buf.data_ptr(), self.flags.data_ptr(), abits, shift, st)
             total = int(self.n_buf[0].item())
             if total:
-                sk, perm = torch.sort(self.sort_key[:total])
-                sk = sk.contiguous()
-                perm = perm.contiguous()
+                # Key-value radix sort over the used bits (slot | src | arrival): the values ride
+                # along, so the scan reads them in order (no permutation gather).
+                nbits = shift + self.nslots.bit_length()
+                need = m.gpu_sort_pairs_temp_bytes(total, 0, nbits)
+                if self._sort_tmp is None or self._sort_tmp.numel() < need:
+                    self._sort_tmp = torch.empty(need, dtype=torch.uint8, device=self.device)
+                m.gpu_sort_pairs(self._sort_tmp.data_ptr(), self._sort_tmp.numel(),
+                                 self.sort_key.data_ptr(), self.sort_out.data_ptr(),
+                                 self.vals_buf.data_ptr(), self.vals_out.data_ptr(), total, 0,
+                                 nbits, st)
+                sk = self.sort_out
                 n_in = self.n_buf[0:1]
                 m.gpu_rolling_heads(sk.data_ptr(), n_in.data_ptr(), total,
-                                    self.heads.data_ptr(), self.n_buf[1:2].data_ptr(), st)
-                m.gpu_rolling_scan(self.agg, sk.data_ptr(), perm.data_ptr(),
-                                   self.vals_buf.data_ptr(), n_in.data_ptr(), self.heads.data_ptr(),
+                                    self.heads.data_ptr(), self.n_buf[1:2].data_ptr(), shift, st)
+                m.gpu_rolling_scan(self.agg, sk.data_ptr(), 0,
+                                   self.vals_out.data_ptr(), n_in.data_ptr(), self.heads.data_ptr(),
                                    self.n_buf[1:2].data_ptr(), min(total, self.nslots),
                                    self.acc_g.data_ptr(), self.cnt_g.data_ptr(),
                                    self.keys_g.data_ptr(), code, consts, self.out_key.data_ptr(),
                                    self.out_val.data_ptr(), self.out_tag.data_ptr(),
-                                   self.out_n.data_ptr(), cap, st)
+                                   self.out_n.data_ptr(), cap, abits, shift, st)
         else:
             m.cpu_rolling_rows(self.recv.data_ptr(), self.recv_counts.data_ptr(), self.world,
                                self.nsub, self.bucket_cap, self.cap_log2, self.agg,
