@@ -292,6 +292,25 @@ PYBIND11_MODULE(_mxs_native, m) {
     gpu::sort_pairs(reinterpret_cast<void*>(temp), temp_bytes, P<uint64_t>(kin), P<uint64_t>(kout),
                     P<uint64_t>(vin), P<uint64_t>(vout), n, begin_bit, end_bit, stream);
   });
+  m.def("gpu_keygroups", [](intptr_t keys, int64_t n, int hash_mode, intptr_t jhash, int max_par,
+                            intptr_t kg, intptr_t stream) {
+    gpu::keygroups(P<uint64_t>(keys), n, hash_mode, P<int32_t>(jhash), max_par, P<int32_t>(kg),
+                   stream);
+  });
+  m.def("cpu_keygroups", [](intptr_t keys, int64_t n, int hash_mode, intptr_t jhash, int max_par,
+                            intptr_t kg) {
+    cpu::keygroups(P<uint64_t>(keys), n, hash_mode, P<int32_t>(jhash), max_par, P<int32_t>(kg));
+  });
+  m.def("gpu_table_insert", [](intptr_t keys, int64_t n, int nsub_log2, int cap_log2,
+                               intptr_t keys_g, intptr_t slots, intptr_t stream) {
+    gpu::table_insert(P<uint64_t>(keys), n, nsub_log2, cap_log2, P<uint64_t>(keys_g),
+                      P<int64_t>(slots), stream);
+  });
+  m.def("cpu_table_insert", [](intptr_t keys, int64_t n, int nsub_log2, int cap_log2,
+                               intptr_t keys_g, intptr_t slots) {
+    cpu::table_insert(P<uint64_t>(keys), n, nsub_log2, cap_log2, P<uint64_t>(keys_g),
+                      P<int64_t>(slots));
+  });
   m.def("gpu_set_erase", [](intptr_t set, uint32_t mask, intptr_t keys, int64_t n,
                             intptr_t stream) {
     gpu::set_erase(P<uint64_t>(set), mask, P<int64_t>(keys), n, stream);

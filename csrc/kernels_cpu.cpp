@@ -290,5 +290,38 @@ void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep
   }
 }
 
+void keygroups(const uint64_t* keys, int64_t n, int hash_mode, const int32_t* jhash, int max_par,
+               int32_t* kg) {
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t h = hash_mode ? jhash[keys[i]] : java_long_hash((int64_t)keys[i]);
+    kg[i] = key_group_of_hash(h, max_par);
+  }
+}
+
+void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,
+                  int64_t* slots) {
+  const uint32_t mask = (1u << cap_log2) - 1;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t key = keys[i];
+    const uint64_t sub = nsub_log2 == 0 ? 0 : (mix64(key) >> (64 - nsub_log2));
+    uint64_t* t = keys_g + (sub << cap_log2);
+    uint32_t s = (uint32_t)mix64(key) & mask;
+    int64_t found = -1;
+    for (uint32_t p = 0; p <= mask; ++p) {
+      if (t[s] == key) {
+        found = s;
+        break;
+      }
+      if (t[s] == kEmptyKey) {
+        t[s] = key;
+        found = s;
+        break;
+      }
+      s = (s + 1) & mask;
+    }
+    slots[i] = found < 0 ? -1 : (int64_t)((sub << cap_log2) | (uint64_t)found);
+  }
+}
+
 }  // namespace cpu
 }  // namespace mxs

@@ -1784,6 +1784,38 @@ __global__ __launch_bounds__(256) void session_rehash_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Checkpoint support (K17): key group of every exported key, and re-insertion of restored keys.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void keygroup_kernel(const uint64_t* __restrict__ keys, int64_t n,
+                                                       int hash_mode,
+                                                       const int32_t* __restrict__ jhash,
+                                                       int max_par, int32_t* __restrict__ kg) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = keys[i];
+    const int32_t h = hash_mode ? jhash[k] : java_long_hash((int64_t)k);
+    kg[i] = key_group_of_hash(h, max_par);
+  }
+}
+
+// Insert keys into a fresh sub-table layout (sub = top nsub_log2 bits of mix64, linear probing on
+// the low bits -- the same placement window_agg / the lookups use). slot = -1 if the sub-table is
+// full.
+__global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t* __restrict__ keys,
+                                                           int64_t n, int nsub_log2, int cap_log2,
+                                                           uint64_t* __restrict__ keys_g,
+                                                           int64_t* __restrict__ slots) {
+  const uint32_t mask = (1u << cap_log2) - 1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys[i];
+    const uint64_t sub = nsub_log2 == 0 ? 0 : (mix64(key) >> (64 - nsub_log2));
+    const uint32_t s = global_probe_insert(keys_g + (sub << cap_log2), key, mask);
+    slots[i] = s == kNoSlot ? -1 : (int64_t)((sub << cap_log2) | s);
+  }
+}
+
 int grid_for(int64_t n, int block, int max_blocks) {
   int64_t g = (n + block - 1) / block;
   if (g < 1) g = 1;
@@ -2130,6 +2162,22 @@ void set_erase(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, int
   if (n <= 0) return;
   hipLaunchKernelGGL(set_erase_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0,
                      (hipStream_t)stream, set, mask, keys, n);
+  HIP_CHECK(hipGetLastError());
+}
+
+void keygroups(const uint64_t* keys, int64_t n, int hash_mode, const int32_t* jhash, int max_par,
+               int32_t* kg, intptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(keygroup_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, keys, n, hash_mode, jhash, max_par, kg);
+  HIP_CHECK(hipGetLastError());
+}
+
+void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,
+                  int64_t* slots, intptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(table_insert_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, keys, n, nsub_log2, cap_log2, keys_g, slots);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -113,6 +113,10 @@ size_t sort_pairs_temp_bytes(int64_t n, int begin_bit, int end_bit);
 void sort_pairs(void* temp, size_t temp_bytes, const uint64_t* keys_in, uint64_t* keys_out,
                 const uint64_t* vals_in, uint64_t* vals_out, int64_t n, int begin_bit, int end_bit,
                 intptr_t stream);
+void keygroups(const uint64_t* keys, int64_t n, int hash_mode, const int32_t* jhash, int max_par,
+               int32_t* kg, intptr_t stream);
+void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,
+                  int64_t* slots, intptr_t stream);
 void set_erase(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, intptr_t stream);
 void session_rehash(int64_t nslots, int cap_log2, const uint64_t* keys_o, const int64_t* sess_o,
                     const int64_t* due_o, const int64_t* last_o, uint64_t* keys_n, int64_t* sess_n,
@@ -152,6 +156,10 @@ void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, u
                   int64_t* out_tag, uint32_t* out_n, uint32_t out_cap);
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
                  int64_t proc_now, int64_t* red);
+void keygroups(const uint64_t* keys, int64_t n, int hash_mode, const int32_t* jhash, int max_par,
+               int32_t* kg);
+void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,
+                  int64_t* slots);
 }  // namespace cpu
 
 }  // namespace mxs

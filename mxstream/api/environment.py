@@ -27,6 +27,8 @@ class ExecutionConfig:
     device: str = "cpu"                     # cpu | cuda  (where native operators run)
     batch_size: int = 1 << 16
     global_job_parameters: dict = field(default_factory=dict)
+    # "<operator name>:<records>[:<attempts>]" (tests / chaos runs); default from MXS_FAULT.
+    fault_injection: str | None = field(default_factory=lambda: os.environ.get("MXS_FAULT"))
 
     def set_auto_watermark_interval(self, ms: int) -> "ExecutionConfig":
         self.auto_watermark_interval = int(ms)
@@ -52,6 +54,31 @@ class CheckpointConfig:
 
     def is_checkpointing_enabled(self) -> bool:
         return self.interval_ms > 0
+
+
+class MemoryStateBackend:
+    """Flink's default: keyed state on the heap (host operators) / in HBM (native operators);
+    checkpoints need a directory set on the CheckpointConfig."""
+
+    checkpoint_path: str | None = None
+
+
+class FsStateBackend(MemoryStateBackend):
+    """Checkpoints to `<checkpoint_path>/<jobId>/chk-<n>/` (Flink FsStateBackend layout)."""
+
+    def __init__(self, checkpoint_path: str):
+        self.checkpoint_path = str(checkpoint_path)
+
+
+class HbmStateBackend(FsStateBackend):
+    """MI355X engine backend: keyed state in HBM hash tables, cold state spilled to host DRAM
+    (up to `host_budget_bytes`), checkpoints under `checkpoint_path`."""
+
+    def __init__(self, checkpoint_path: str, spill_dir: str | None = None,
+                 host_budget_bytes: int | None = None):
+        super().__init__(checkpoint_path)
+        self.spill_dir = spill_dir
+        self.host_budget_bytes = host_budget_bytes
 
 
 class RestartStrategies:
@@ -203,11 +230,16 @@ class StreamExecutionEnvironment:
             raise RuntimeError("No operators defined in streaming topology. Cannot execute.")
         from .planner import plan
 
+        import secrets
+
         sinks = plan(self, list(self._sinks))
+        job_id = secrets.token_hex(16)
         attempts = 0
+        restore = None
         while True:
             try:
-                result = Executor(self, sinks, job_name).run()
+                result = Executor(self, sinks, job_name, job_id=job_id, restore_from=restore,
+                                  attempt=attempts).run()
                 break
             except Exception:
                 kind = self.restart_strategy[0]
@@ -216,8 +248,27 @@ class StreamExecutionEnvironment:
                     import time as _t
 
                     _t.sleep(self.restart_strategy[2] / 1000.0)
+                    # Restart from the latest completed checkpoint (replayable sources rewind to
+                    # their checkpointed offsets); without checkpoints the job starts over.
+                    restore = None
+                    if self.checkpoint_config.is_checkpointing_enabled():
+                        from ..runtime.checkpoint import CheckpointStorage
+
+                        root = (self.checkpoint_config.checkpoint_dir
+                                or getattr(self.state_backend, "checkpoint_path", None))
+                        restore = CheckpointStorage(root, job_id).latest()
                     continue
                 raise
+        result.metrics["numRestarts"] = attempts
+        self._sinks = []
+        return result
+
+    def execute_from_savepoint(self, path: str, job_name: str = "Flink Streaming Job"):
+        """Run the job graph starting from a checkpoint/savepoint directory (`flink run -s`)."""
+        from .planner import plan
+
+        sinks = plan(self, list(self._sinks))
+        result = Executor(self, sinks, job_name, restore_from=path).run()
         self._sinks = []
         return result
 

@@ -267,3 +267,42 @@ def expr_filter(x: torch.Tensor, prog: _expr.Program) -> torch.Tensor:
     else:
         m.cpu_expr_filter(_p(x), x.numel(), code, consts, _p(keep))
     return keep.bool()
+
+
+def keygroups(keys: torch.Tensor, *, max_parallelism: int, hash_mode: int = 0,
+              jhash: torch.Tensor | None = None) -> torch.Tensor:
+    """Flink key group of every key (murmur(javaHash) % maxParallelism), int32."""
+    dev = keys.device
+    _check(keys, torch.int64, keys.numel(), "keys", dev)
+    if hash_mode:
+        if jhash is None:
+            raise ValueError("hash_mode=1 needs the dictionary jhash table")
+        _check(jhash, torch.int32, 1, "jhash", dev)
+        if keys.numel() and int(keys.max().item()) >= jhash.numel():
+            raise ValueError("dictionary id outside the jhash table")
+    kg = torch.empty(keys.numel(), dtype=torch.int32, device=dev)
+    m = load()
+    args = (_p(keys), keys.numel(), int(hash_mode), _p(jhash), int(max_parallelism), _p(kg))
+    if _is_gpu(keys):
+        m.gpu_keygroups(*args, _stream(keys))
+    else:
+        m.cpu_keygroups(*args)
+    return kg
+
+
+def table_insert(keys: torch.Tensor, keys_g: torch.Tensor, *, nsub_log2: int,
+                 cap_log2: int) -> torch.Tensor:
+    """Insert keys into the sub-table hash layout; returns their global slots (-1: table full)."""
+    dev = keys.device
+    _check(keys, torch.int64, keys.numel(), "keys", dev)
+    _check(keys_g, torch.int64, (1 << nsub_log2) << cap_log2, "keys_g", dev)
+    if bool(((keys == -1) | (keys == -2)).any()):
+        raise ValueError("keys -1 / -2 are reserved (empty / tombstone)")
+    slots = torch.empty(keys.numel(), dtype=torch.int64, device=dev)
+    m = load()
+    args = (_p(keys), keys.numel(), int(nsub_log2), int(cap_log2), _p(keys_g), _p(slots))
+    if _is_gpu(keys):
+        m.gpu_table_insert(*args, _stream(keys))
+    else:
+        m.cpu_table_insert(*args)
+    return slots

@@ -1,0 +1,315 @@
+"""Checkpoints and savepoints with Flink's FsStateBackend directory layout.
+
+Flink 1.8 (promised but not implemented by the reference,
+chapter3/README.md:454-456) stores
+
+  <checkpoint dir>/<jobId>/chk-<n>/_metadata        (+ <jobId>/shared/, <jobId>/taskowned/)
+  <savepoint dir>/savepoint-<jobId[:6]>-<12 hex>/_metadata
+
+with keyed state partitioned by *key group* so that a job can be restored at another parallelism.
+This module mirrors that layout; the file contents are mxstream's own (documented below), not
+Flink's binary MetadataV2.
+
+* One state file per (operator uid, rank): ``<uid>-<rank>.kg`` written by the C++ runtime
+  (csrc/runtime.cpp ``write_kg_file``): magic ``MXSKG001`` | JSON header | key-group range |
+  per-key-group row offsets | columns sorted by key group. A reader asks for a key-group range and
+  gets exactly those rows (restore at a different world size reads the slices it now owns from
+  every old rank's file).
+* ``_metadata`` (JSON) is written last, atomically (write + rename), by rank 0 after every rank
+  finished its files (barrier): checkpoint id, job id, world size, max parallelism, per-operator
+  file list and scalar metadata (watermark, fire cursor, ...), source offsets, user extras.
+  A directory without ``_metadata`` is an incomplete checkpoint and is never restored.
+
+Snapshots are step-aligned: between two micro-batches every rank is at the same step, so the
+checkpoint barrier needs no alignment buffering (the engine's analogue of Flink's aligned
+barriers). The device tables are exported by ``keygroups`` + gathers on the GPU and copied to the
+host once per checkpoint.
+"""
+from __future__ import annotations
+
+import json
+import os
+import secrets
+import shutil
+import time
+from dataclasses import dataclass, field
+from pathlib import Path
+
+import numpy as np
+
+from ..ops.native import load
+
+META = "_metadata"
+FORMAT = "mxstream-checkpoint-v1"
+
+
+@dataclass
+class OperatorSnapshot:
+    """What an operator hands to the coordinator: key-grouped rows + scalar metadata."""
+    kg: np.ndarray                         # int32 key group per row
+    columns: dict[str, np.ndarray]         # equal-length columns (fixed-width dtypes)
+    meta: dict = field(default_factory=dict)
+
+
+def _dtype_str(a: np.ndarray) -> str:
+    return np.dtype(a.dtype).str
+
+
+class CheckpointStorage:
+    """Directory layout of one job's checkpoints (and of savepoints)."""
+
+    def __init__(self, root: str | os.PathLike, job_id: str | None = None):
+        self.root = Path(root)
+        self.job_id = job_id or secrets.token_hex(16)
+
+    @property
+    def job_dir(self) -> Path:
+        return self.root / self.job_id
+
+    def checkpoint_dir(self, n: int) -> Path:
+        return self.job_dir / f"chk-{n}"
+
+    def init_job_dirs(self) -> None:
+        for d in (self.job_dir, self.job_dir / "shared", self.job_dir / "taskowned"):
+            d.mkdir(parents=True, exist_ok=True)
+
+    def new_savepoint_dir(self, target: str | os.PathLike | None = None) -> Path:
+        base = Path(target) if target is not None else self.root
+        return base / f"savepoint-{self.job_id[:6]}-{secrets.token_hex(6)}"
+
+    def completed_checkpoints(self) -> list[Path]:
+        if not self.job_dir.exists():
+            return []
+        out = []
+        for d in self.job_dir.iterdir():
+            if d.name.startswith("chk-") and (d / META).exists():
+                out.append(d)
+        return sorted(out, key=lambda d: int(d.name[4:]))
+
+    def latest(self) -> Path | None:
+        done = self.completed_checkpoints()
+        return done[-1] if done else None
+
+
+def write_operator_file(directory: Path, uid: str, rank: int, snap: OperatorSnapshot,
+                        max_parallelism: int) -> str:
+    """Write one operator's key-grouped rows for this rank; returns the file name."""
+    m = load()
+    name = f"{uid}-{rank}.kg"
+    cols = list(snap.columns.items())
+    n = len(snap.kg)
+    for k, v in cols:
+        if len(v) != n:
+            raise ValueError(f"column {k}: {len(v)} rows, expected {n}")
+    header = json.dumps({"uid": uid, "rank": rank,
+                         "columns": [[k, _dtype_str(v)] for k, v in cols]})
+    m.write_kg_file(str(directory / name), header, 0, max_parallelism - 1,
+                    np.ascontiguousarray(snap.kg, dtype=np.int32),
+                    [np.ascontiguousarray(v) for _, v in cols])
+    return name
+
+
+def read_operator_rows(directory: Path, files: list[str], kg_lo: int, kg_hi: int) -> dict:
+    """Rows of key groups [kg_lo, kg_hi] from every listed file, concatenated per column."""
+    m = load()
+    parts: dict[str, list[np.ndarray]] = {}
+    order: list[tuple[str, str]] = []
+    for fname in files:
+        path = directory / fname
+        head, _lo, _hi, _offs, _c, _n = m.read_kg_file(str(path), [], 0, 0)
+        cols = json.loads(bytes(head).decode())["columns"]
+        if not order:
+            order = [tuple(c) for c in cols]
+        sizes = [np.dtype(dt).itemsize for _, dt in cols]
+        head, _lo, _hi, _offs, raw, nrows = m.read_kg_file(str(path), sizes, kg_lo, kg_hi)
+        for (cname, dt), buf in zip(cols, raw):
+            parts.setdefault(cname, []).append(np.frombuffer(bytes(buf), dtype=np.dtype(dt)))
+    return {c: (np.concatenate(parts[c]) if parts.get(c) else np.zeros(0, np.dtype(dt)))
+            for c, dt in order}
+
+
+def _atomic_write_json(path: Path, obj: dict) -> None:
+    tmp = path.with_name(path.name + ".inprogress")
+    with open(tmp, "w") as f:
+        json.dump(obj, f, indent=1, sort_keys=True)
+        f.flush()
+        os.fsync(f.fileno())
+    os.replace(tmp, path)
+
+
+def read_metadata(path: str | os.PathLike) -> dict:
+    d = Path(path)
+    with open(d / META) as f:
+        meta = json.load(f)
+    if meta.get("format") != FORMAT:
+        raise ValueError(f"{d}: not an mxstream checkpoint ({meta.get('format')})")
+    return meta
+
+
+class CheckpointCoordinator:
+    """Triggers step-aligned checkpoints of a set of engine operators across ranks.
+
+    ``operators``: {uid: operator} where each operator implements ``snapshot_state() ->
+    OperatorSnapshot`` and ``restore_state(rows: dict, meta: dict)`` and exposes ``comm`` (all
+    operators of a job share one communicator) and ``max_parallelism``.
+    """
+
+    def __init__(self, storage: CheckpointStorage, operators: dict, *, comm=None,
+                 interval_steps: int | None = None, retain: int = 1):
+        self.storage = storage
+        self.ops = operators
+        first = next(iter(operators.values()))
+        self.comm = comm if comm is not None else first.comm
+        self.world, self.rank = self.comm.world, self.comm.rank
+        self.max_parallelism = first.max_parallelism
+        self.interval_steps = interval_steps
+        self.retain = max(1, retain)
+        self.next_id = 1
+        done = storage.completed_checkpoints()
+        if done:
+            self.next_id = int(done[-1].name[4:]) + 1
+        self.stats: list[dict] = []
+
+    # ---- triggering --------------------------------------------------------------------
+    def maybe_trigger(self, step: int, sources: dict | None = None) -> Path | None:
+        if self.interval_steps and step > 0 and step % self.interval_steps == 0:
+            return self.trigger(step, sources)
+        return None
+
+    def trigger(self, step: int, sources: dict | None = None, extra: dict | None = None) -> Path:
+        """Checkpoint chk-<next id> (all ranks call this at the same step)."""
+        if self.rank == 0:
+            self.storage.init_job_dirs()
+        d = self.storage.checkpoint_dir(self.next_id)
+        self._write(d, "checkpoint", step, sources, extra)
+        self.next_id += 1
+        if self.rank == 0:
+            self._prune()
+        return d
+
+    def savepoint(self, step: int, target: str | None = None, sources: dict | None = None,
+                  extra: dict | None = None) -> Path:
+        """Savepoint (all ranks must pass the same `target`; rank 0's directory name wins)."""
+        d = self.storage.new_savepoint_dir(target)
+        name = [d.name]
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.broadcast_object_list(name, src=0)
+            d = d.parent / name[0]
+        self._write(d, "savepoint", step, sources, extra)
+        return d
+
+    def _write(self, d: Path, kind: str, step: int, sources, extra) -> dict | None:
+        t0 = time.perf_counter()
+        d.mkdir(parents=True, exist_ok=True)
+        op_meta, nbytes = {}, 0
+        for uid, op in self.ops.items():
+            snap = op.snapshot_state()
+            fname = write_operator_file(d, uid, self.rank, snap, self.max_parallelism)
+            nbytes += sum(v.nbytes for v in snap.columns.values())
+            op_meta[uid] = {"meta": snap.meta, "rows": int(len(snap.kg)), "file": fname}
+        gathered = self._gather({"rank": self.rank, "ops": op_meta, "sources": sources or {},
+                                 "bytes": nbytes})
+        meta = None
+        if self.rank == 0:
+            ops_all = {}
+            for uid in self.ops:
+                ops_all[uid] = {
+                    "files": [g["ops"][uid]["file"] for g in gathered],
+                    "rows": [g["ops"][uid]["rows"] for g in gathered],
+                    "meta": gathered[0]["ops"][uid]["meta"],
+                }
+            meta = {"format": FORMAT, "type": kind, "job_id": self.storage.job_id,
+                    "checkpoint_id": self.next_id if kind == "checkpoint" else None,
+                    "step": int(step), "timestamp_ms": int(time.time() * 1000),
+                    "world": self.world, "max_parallelism": self.max_parallelism,
+                    "operators": ops_all, "sources": [g["sources"] for g in gathered],
+                    "extra": extra or {}}
+            _atomic_write_json(d / META, meta)
+        self.comm.barrier()
+        self.stats.append({"dir": str(d), "type": kind, "step": step,
+                           "ms": (time.perf_counter() - t0) * 1e3, "bytes": nbytes})
+        return meta
+
+    def _gather(self, obj: dict) -> list[dict]:
+        if self.world == 1:
+            return [obj]
+        import torch.distributed as dist
+
+        out = [None] * self.world
+        dist.all_gather_object(out, obj)
+        return out
+
+    def _prune(self) -> None:
+        done = self.storage.completed_checkpoints()
+        for old in done[:-self.retain]:
+            shutil.rmtree(old, ignore_errors=True)
+
+    # ---- restore -----------------------------------------------------------------------
+    def restore(self, path: str | os.PathLike | None = None) -> dict:
+        """Restore every operator from a completed checkpoint/savepoint (default: latest).
+
+        Works at any world size: each rank reads the key groups it now owns from all old files.
+        Returns the metadata (source offsets etc. are the caller's to apply)."""
+        d = Path(path) if path is not None else self.storage.latest()
+        if d is None:
+            raise FileNotFoundError("no completed checkpoint")
+        meta = read_metadata(d)
+        if meta["max_parallelism"] != self.max_parallelism:
+            raise ValueError("max parallelism changed: key groups cannot be remapped")
+        for uid, op in self.ops.items():
+            om = meta["operators"].get(uid)
+            if om is None:
+                raise KeyError(f"operator {uid!r} not in checkpoint {d}")
+            lo, hi = op.owned_key_groups()
+            rows = read_operator_rows(d, om["files"], lo, hi)
+            op.restore_state(rows, om["meta"])
+        if meta.get("checkpoint_id") is not None and d.parent == self.storage.job_dir:
+            self.next_id = max(self.next_id, int(meta["checkpoint_id"]) + 1)
+        return meta
+
+
+def owned_key_groups(rank: int, world: int, parallelism: int, max_parallelism: int) -> tuple[int, int]:
+    """Contiguous key-group range of a rank (subtasks laid out in blocks over ranks):
+    kg -> subtask = kg * P // maxP -> rank = subtask * G // P."""
+    kgs = [kg for kg in range(max_parallelism)
+           if (kg * parallelism // max_parallelism) * world // parallelism == rank]
+    if not kgs:
+        return 1, 0  # empty range
+    return kgs[0], kgs[-1]
+
+
+# ---- host executor checkpoints (DataStream API jobs) ------------------------------------------
+# Host operators hold arbitrary Python values (user tuples, accumulators, timers), so their state
+# files are pickles written and read only by this engine (never files from elsewhere); keyed
+# state inside them is already partitioned by key group (HeapKeyedStateBackend.snapshot).
+def write_host_checkpoint(d: Path, *, job_id: str, checkpoint_id: int, states: dict[str, dict],
+                          extra: dict, kind: str = "checkpoint") -> None:
+    import pickle
+
+    d.mkdir(parents=True, exist_ok=True)
+    files = {}
+    for i, (node_id, st) in enumerate(states.items()):
+        name = f"op{i:03d}-0.state"  # uid -> file map lives in _metadata
+        tmp = d / (name + ".inprogress")
+        with open(tmp, "wb") as f:
+            pickle.dump(st, f, protocol=pickle.HIGHEST_PROTOCOL)
+        os.replace(tmp, d / name)
+        files[node_id] = name
+    _atomic_write_json(d / META, {"format": FORMAT, "type": kind, "job_id": job_id,
+                                  "checkpoint_id": checkpoint_id,
+                                  "timestamp_ms": int(time.time() * 1000), "host_operators": files,
+                                  "extra": extra})
+
+
+def read_host_checkpoint(path: str | os.PathLike) -> tuple[dict, dict[str, dict]]:
+    import pickle
+
+    d = Path(path)
+    meta = read_metadata(d)
+    states = {}
+    for node_id, name in meta["host_operators"].items():
+        with open(d / name, "rb") as f:
+            states[node_id] = pickle.load(f)  # written by write_host_checkpoint above
+    return meta, states

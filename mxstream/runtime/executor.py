@@ -70,10 +70,38 @@ class JobExecutionException(RuntimeError):
     """Job failed (no restart strategy): wraps the user/operator exception."""
 
 
+class InjectedFault(RuntimeError):
+    """Raised by the fault injector (``MXS_FAULT`` / ExecutionConfig.fault_injection)."""
+
+
+def parse_fault(spec: str | None):
+    """"<operator name substring>:<records>[:<attempts>]" -> (name, n, attempts) or None.
+    The fault fires when the operator has received `records` records, on the first `attempts`
+    executions of the job (default 1: the restarted job runs clean)."""
+    if not spec:
+        return None
+    parts = spec.split(":")
+    if len(parts) not in (2, 3):
+        raise ValueError(f"bad fault spec {spec!r} (name:records[:attempts])")
+    return parts[0], int(parts[1]), int(parts[2]) if len(parts) == 3 else 1
+
+
 class Executor:
-    def __init__(self, env, sinks: list[Transformation], job_name: str):
+    """Micro-batch DAG executor. Checkpoints are step-aligned: taken between two passes over the
+    DAG, when no record is in flight (every pass drains the inboxes to the sinks), so operator
+    snapshots plus source positions form a consistent cut -- Flink's aligned barrier without
+    alignment buffering. Layout: runtime/checkpoint.py (chk-<n>/_metadata + one state file per
+    operator)."""
+
+    def __init__(self, env, sinks: list[Transformation], job_name: str, *, job_id: str | None = None,
+                 restore_from=None, attempt: int = 0):
         self.env = env
         self.job_name = job_name
+        self.job_id = job_id
+        self.restore_from = restore_from
+        self.attempt = attempt
+        self.fault = parse_fault(getattr(env.config, "fault_injection", None))
+        self._fault_count = 0
         self.nodes = self._topo(sinks)
         self.children: dict[int, list[Transformation]] = {n.id: [] for n in self.nodes}
         for n in self.nodes:
@@ -138,6 +166,8 @@ class Executor:
                 for p in n.parents:
                     items.extend(inbox.pop((n.id, p.id), []))
                 op = self.ops[n.id]
+                if self.fault is not None and items:
+                    self._maybe_fault(n, items)
                 out = op.process(items) if items else []
                 if now is not None:
                     out.extend(op.on_processing_time(now))
@@ -150,12 +180,97 @@ class Executor:
                 else:
                     inbox.setdefault((c.id, n.id), []).extend(out)
 
+    # ---- checkpoints ---------------------------------------------------------------------
+    def _storage(self):
+        from .checkpoint import CheckpointStorage
+
+        cfg = self.env.checkpoint_config
+        root = cfg.checkpoint_dir or getattr(self.env.state_backend, "checkpoint_path", None)
+        if root is None:
+            raise ValueError("checkpointing needs a directory: set_state_backend(FsStateBackend(path))"
+                             " or get_checkpoint_config().checkpoint_dir")
+        return CheckpointStorage(root, self.job_id)
+
+    def _checkpoint(self, finished: dict) -> None:
+        from .checkpoint import write_host_checkpoint
+
+        t0 = time.perf_counter()
+        storage = self._storage()
+        storage.init_job_dirs()
+        n = self._next_ckpt
+        states = {self._uid(nd): self.ops[nd.id].snapshot() for nd in self.nodes if nd.id in self.ops}
+        write_host_checkpoint(storage.checkpoint_dir(n), job_id=storage.job_id, checkpoint_id=n,
+                              states=states, extra={
+                                  "clock": self.clock() if isinstance(self.clock, ManualClock) else None,
+                                  "rr": [[self._uid(self._node[a]), self._uid(self._node[b]), v]
+                                         for (a, b), v in self._rr.items()],
+                                  "finished": {self._uid(nd): finished[nd.id] for nd in self.nodes
+                                               if nd.id in finished},
+                                  "nodes": {self._uid(nd): nd.name for nd in self.nodes}})
+        for old in storage.completed_checkpoints()[:-max(1, self.env.checkpoint_config.max_retained)]:
+            import shutil
+
+            shutil.rmtree(old, ignore_errors=True)
+        self._next_ckpt += 1
+        self.metrics["numberOfCompletedCheckpoints"] = self.metrics.get("numberOfCompletedCheckpoints", 0) + 1
+        self.metrics["lastCheckpointDuration"] = (time.perf_counter() - t0) * 1e3
+        self.metrics["lastCheckpointPath"] = str(storage.checkpoint_dir(n))
+
+    def _restore(self, path, finished: dict) -> None:
+        from .checkpoint import read_host_checkpoint
+
+        meta, states = read_host_checkpoint(path)
+        names = meta["extra"]["nodes"]
+        for nd in self.nodes:
+            key = self._uid(nd)
+            if key not in states or names.get(key) != nd.name:
+                raise ValueError(f"checkpoint {path} does not match the job graph ({nd.name})")
+            self.ops[nd.id].restore(states[key])
+        ex = meta["extra"]
+        if ex.get("clock") is not None and isinstance(self.clock, ManualClock):
+            self.clock.advance_to(ex["clock"])
+        by_uid = {self._uid(nd): nd.id for nd in self.nodes}
+        self._rr = {(by_uid[a], by_uid[b]): v for a, b, v in ex.get("rr", [])}
+        for k, v in ex.get("finished", {}).items():
+            finished[by_uid[k]] = v
+        self._next_ckpt = int(meta["checkpoint_id"]) + 1
+        self.metrics["restoredCheckpointId"] = int(meta["checkpoint_id"])
+
+    def _uid(self, nd) -> str:
+        """Stable operator id across job submissions: the user's .uid(), else the position in
+        the topological order + name (Flink hashes the graph structure the same way)."""
+        if nd.uid:
+            return nd.uid
+        if not hasattr(self, "_pos"):
+            self._pos = {n.id: i for i, n in enumerate(self.nodes)}
+            self._node = {n.id: n for n in self.nodes}
+        return f"{self._pos[nd.id]}-{nd.name}"
+
+    def _maybe_fault(self, node, items) -> None:
+        f = self.fault
+        if f is None or self.attempt >= f[2] or f[0] not in node.name:
+            return
+        self._fault_count += sum(1 for it in items if isinstance(it, Rec))
+        if self._fault_count >= f[1]:
+            raise InjectedFault(f"injected fault in {node.name} after {self._fault_count} records"
+                                f" (attempt {self.attempt})")
+
     def run(self) -> JobExecutionResult:
         t0 = time.perf_counter()
         self._open()
         sources = [n for n in self.nodes if n.kind == "source"]
         finished = {n.id: False for n in sources}
         manual = isinstance(self.clock, ManualClock)
+        cfg = self.env.checkpoint_config
+        self._next_ckpt = 1
+        self._uid(self.nodes[0])  # builds the position / node maps
+        if self.restore_from is not None:
+            self._restore(self.restore_from, finished)
+        elif cfg.is_checkpointing_enabled():
+            done = self._storage().completed_checkpoints()
+            if done:
+                self._next_ckpt = int(done[-1].name[4:]) + 1
+        last_ckpt = self.clock()
         try:
             while not all(finished.values()):
                 if manual:
@@ -173,6 +288,9 @@ class Executor:
                     for c in self.children[n.id]:
                         inbox.setdefault((c.id, n.id), []).extend(self._rebalance(n, c, items))
                 self._push(inbox, now)
+                if cfg.is_checkpointing_enabled() and self.clock() - last_ckpt >= cfg.interval_ms:
+                    self._checkpoint(finished)
+                    last_ckpt = self.clock()
             # End of input: MAX watermark (event time), then operators' finish hooks.
             inbox = {}
             for n in sources:
@@ -180,7 +298,7 @@ class Executor:
                     inbox.setdefault((c.id, n.id), []).append(WM(LONG_MAX))
             self._push(inbox, None)
             self._finish()
-        except JobExecutionException:
+        except (JobExecutionException, InjectedFault):
             raise
         except Exception as e:
             raise JobExecutionException(f"Job '{self.job_name}' failed: {type(e).__name__}: {e}") from e

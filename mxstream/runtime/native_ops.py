@@ -195,6 +195,36 @@ class NativeWindowOp(Operator):
             return self.fallback.finish()
         return self._flush()
 
+    def snapshot(self) -> dict:
+        """Engine state (key-grouped rows of the pane tables) + the host-side key dictionary and
+        keep-first templates; or the exact host operator's state after a fallback."""
+        if self.pending:
+            raise RuntimeError("snapshot between micro-batches only (records pending)")
+        if self.fallback is not None:
+            return {"fallback": self.fallback.snapshot()}
+        snap = {"wm": self.wm, "late": self.num_late_records_dropped, "str_keys": self.str_keys,
+                "templates": dict(self.templates), "strings": list(self.dict.strings())}
+        if self.op is not None:
+            es = self.op.snapshot_state()
+            snap["engine"] = {"columns": es.columns, "meta": es.meta, "is_float": self.is_float}
+        return snap
+
+    def restore(self, snap: dict) -> None:
+        if "fallback" in snap:
+            self._to_fallback()
+            self.fallback.restore(snap["fallback"])
+            return
+        self.wm = snap["wm"]
+        self.num_late_records_dropped = snap["late"]
+        self.str_keys = snap["str_keys"]
+        self.templates = dict(snap["templates"])
+        for st in snap["strings"]:
+            self.dict.intern(st)
+        eng = snap.get("engine")
+        if eng is not None:
+            self._build(1.0 if eng["is_float"] else 1)
+            self.op.restore_state(eng["columns"], eng["meta"])
+
     def take_side(self, tag_id):
         if self.fallback is not None:
             return self.fallback.take_side(tag_id)

@@ -15,6 +15,8 @@ Flink 1.8 behaviour reproduced (class names are Flink's):
 """
 from __future__ import annotations
 
+import copy
+
 import heapq
 import itertools
 from dataclasses import dataclass
@@ -215,7 +217,9 @@ class TimestampsAndWatermarksOp(Operator):
     name = "Timestamps/Watermarks"
 
     def __init__(self, assigner):
-        self.assigner = assigner
+        # Each (re)started task gets its own copy of the user assigner, as Flink deserializes one
+        # per task: a restarted job must not inherit the failed attempt's max timestamp.
+        self.assigner = copy.deepcopy(assigner)
         self.current = LONG_MIN
 
     def process(self, items):

@@ -194,3 +194,39 @@ class KeyedRollingOperator:
             return None
         i = int(idx[0])
         return int(self.acc_g[i].item()), int(self.cnt_g[i].item())
+
+    # ---- checkpoint / restore (runtime/checkpoint.py) --------------------------------------
+    def owned_key_groups(self) -> tuple[int, int]:
+        from .checkpoint import owned_key_groups
+
+        return owned_key_groups(self.rank, self.world, self.parallelism, self.max_parallelism)
+
+    def snapshot_state(self):
+        """Per-key ValueState (accumulator, count) grouped by key group."""
+        from .checkpoint import OperatorSnapshot
+
+        live = torch.nonzero(self.keys_g != -1).flatten()
+        keys = self.keys_g[live].contiguous()
+        kg = K.keygroups(keys, max_parallelism=self.max_parallelism).cpu().numpy()
+        cols = {"key": keys.cpu().numpy(), "acc": self.acc_g[live].cpu().numpy(),
+                "cnt": self.cnt_g[live].cpu().numpy()}
+        meta = {"kind": "rolling", "agg": self.agg, "records_in": self.records_in,
+                "steps": self.steps}
+        return OperatorSnapshot(kg, cols, meta)
+
+    def restore_state(self, rows: dict, meta: dict) -> None:
+        if meta["agg"] != self.agg:
+            raise ValueError("checkpoint aggregate does not match the operator")
+        self.records_in, self.steps = meta["records_in"], meta["steps"]
+        self.keys_g.fill_(-1)
+        self.acc_g.zero_()
+        self.cnt_g.zero_()
+        if not len(rows["key"]):
+            return
+        dev = self.device
+        keys = torch.from_numpy(np.ascontiguousarray(rows["key"])).to(dev)
+        slots = K.table_insert(keys, self.keys_g, nsub_log2=self.nsub_log2, cap_log2=self.cap_log2)
+        if bool((slots < 0).any()):
+            raise RuntimeError("restore: keyed state does not fit the table (raise max_keys)")
+        self.acc_g[slots] = torch.from_numpy(np.ascontiguousarray(rows["acc"])).to(dev)
+        self.cnt_g[slots] = torch.from_numpy(np.ascontiguousarray(rows["cnt"])).to(dev)

@@ -559,3 +559,75 @@ class KeyedSessionOperator:
                               "flags": rec[sel, j, 3] >> 32})
         return {f: np.concatenate([p[f] for p in parts]) for f in
                 ("key", "start", "end", "acc", "cnt", "flags")}
+
+    # ---- checkpoint / restore (runtime/checkpoint.py) --------------------------------------
+    def owned_key_groups(self) -> tuple[int, int]:
+        from .checkpoint import owned_key_groups
+
+        return owned_key_groups(self.rank, self.world, self.parallelism, self.max_parallelism)
+
+    def snapshot_state(self):
+        """Every live session of both tiers (HBM slots and the host store), by key group."""
+        from .checkpoint import OperatorSnapshot
+
+        snap = self.snapshot()
+        keys = torch.from_numpy(np.ascontiguousarray(snap["key"], dtype=np.int64))
+        kg = K.keygroups(keys, max_parallelism=self.max_parallelism).numpy()
+        cols = {k: np.ascontiguousarray(snap[k], dtype=np.int64)
+                for k in ("key", "start", "end", "acc", "cnt", "flags")}
+        meta = {"kind": "session", "gap": self.gap, "lateness": self.lateness, "agg": self.agg,
+                "wm": self.wm, "metrics": {k: v for k, v in self.metrics.__dict__.items()
+                                           if isinstance(v, int)}}
+        return OperatorSnapshot(kg, cols, meta)
+
+    def restore_state(self, rows: dict, meta: dict) -> None:
+        """Restored sessions go to the HBM slot table (keys with <= kSess sessions) or to the
+        host store (the rest), exactly like state that overflowed during processing."""
+        for k in ("gap", "agg"):
+            if meta[k] != getattr(self, k):
+                raise ValueError(f"checkpoint {k} does not match the operator")
+        self.wm = meta["wm"]
+        for k, v in meta.get("metrics", {}).items():
+            setattr(self.metrics, k, v)
+        self.store = self.native.SessionStore(self.gap, self.lateness, self.agg)
+        cols = [np.ascontiguousarray(rows[k], dtype=np.int64)
+                for k in ("key", "start", "end", "acc", "cnt", "flags")]
+        if not self.gpu:
+            if len(cols[0]):
+                self.store.insert(*cols, False)
+            return
+        self._join_spill()
+        self._alloc_state()
+        self.spill_set.fill_(EMPTY_KEY)
+        self.set_used, self.spill_any = 0, False
+        if not len(cols[0]):
+            return
+        key = cols[0]
+        order = np.argsort(key, kind="stable")
+        cols = [c[order] for c in cols]
+        key = cols[0]
+        uniq, first, counts = np.unique(key, return_index=True, return_counts=True)
+        pos = np.arange(len(key)) - np.repeat(first, counts)  # session index within its key
+        many = np.repeat(counts > K_SESS, counts)
+        if many.any():  # more sessions than an HBM slot holds: host tier
+            self.store.insert(*[c[many] for c in cols], False)
+        dev = self.device
+        fit_keys = uniq[counts <= K_SESS]
+        if len(fit_keys):
+            slots_u = K.table_insert(torch.from_numpy(fit_keys).to(dev), self.keys_g,
+                                     nsub_log2=self.nsub_log2, cap_log2=self.cap_log2)
+            if bool((slots_u < 0).any()):
+                raise RuntimeError("restore: session keys do not fit the slot table")
+            sel = ~many
+            slot_of = dict(zip(fit_keys.tolist(), slots_u.cpu().tolist()))
+            slot = np.array([slot_of[k] for k in key[sel].tolist()], dtype=np.int64)
+            rec = np.zeros((len(slot), 4), dtype=np.int64)
+            rec[:, 0], rec[:, 1], rec[:, 2] = cols[1][sel], cols[2][sel], cols[3][sel]
+            rec[:, 3] = (cols[4][sel] & 0xFFFFFFFF) | (cols[5][sel] << 32)
+            view = self.sess.view(self.nslots * K_SESS, 4)
+            dst = torch.from_numpy(slot * K_SESS + pos[sel]).to(dev)
+            view[dst] = torch.from_numpy(rec).to(dev)
+            # Due times: recomputed by one fire sweep at the restored watermark; mark all due now.
+            self.slot_due[torch.from_numpy(np.unique(slot)).to(dev)] = I64_MIN
+        if len(self.store.key_list()):
+            self._rebuild_spill_set(max(16, _next_pow2(4 * self.store.num_keys()).bit_length() - 1))

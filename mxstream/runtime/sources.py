@@ -37,6 +37,16 @@ class Source:
     def close(self) -> None:
         pass
 
+    # Replayable sources report their read position in checkpoints and seek back to it on
+    # restore (Flink's source offsets). Non-replayable ones (socket) return {}.
+    def snapshot(self) -> dict:
+        pos = getattr(self, "pos", None)
+        return {} if pos is None else {"pos": pos}
+
+    def restore(self, snap: dict) -> None:
+        if "pos" in snap:
+            self.pos = snap["pos"]
+
 
 class CollectionSource(Source):
     name = "Collection Source"
@@ -132,6 +142,12 @@ class SequenceSource(Source):
         super().open(rank, world, clock)
         self.cur = self.start + rank
         self.step = world
+
+    def snapshot(self) -> dict:
+        return {"cur": self.cur}
+
+    def restore(self, snap: dict) -> None:
+        self.cur = snap.get("cur", self.cur)
 
     def poll(self, now):
         out = []

@@ -454,3 +454,84 @@ class KeyedWindowOperator:
 
     def num_keys(self) -> int:
         return int(self.occ.sum().item())
+
+    # ---- checkpoint / restore (runtime/checkpoint.py) --------------------------------------
+    def owned_key_groups(self) -> tuple[int, int]:
+        from .checkpoint import owned_key_groups
+
+        return owned_key_groups(self.rank, self.world, self.parallelism, self.max_parallelism)
+
+    def _check_ckpt_meta(self, meta: dict) -> None:
+        for k in ("size", "slide", "offset", "agg", "time_mode"):
+            if meta[k] != getattr(self, k):
+                raise ValueError(f"checkpoint {k}={meta[k]!r} does not match operator "
+                                 f"{getattr(self, k)!r}")
+
+    def snapshot_state(self):
+        """Live (key, pane) accumulators grouped by key group, plus the firing bookkeeping."""
+        from .checkpoint import OperatorSnapshot
+
+        live = torch.nonzero(self.keys_g != -1).flatten()
+        cols = {"key": np.zeros(0, np.int64), "pane": np.zeros(0, np.int64),
+                "acc": np.zeros(0, np.int64), "cnt": np.zeros(0, np.int32),
+                "dirty": np.zeros(0, np.uint8)}
+        kg = np.zeros(0, np.int32)
+        if self.min_live_pane is not None and live.numel():
+            panes = torch.arange(self.min_live_pane, self.max_seen_pane + 1, device=self.device)
+            idx = ((panes & (self.ring - 1)) * self.nslots)[:, None] + live[None, :]
+            cnt = self.cnt_g[idx]
+            sel = cnt > 0
+            keys = self.keys_g[live][None, :].expand_as(idx)[sel].contiguous()
+            kg = K.keygroups(keys, max_parallelism=self.max_parallelism, hash_mode=self.hash_mode,
+                             jhash=self.jhash).cpu().numpy()
+            cols = {"key": keys.cpu().numpy(),
+                    "pane": panes[:, None].expand_as(idx)[sel].cpu().numpy(),
+                    "acc": self.acc_g[idx][sel].cpu().numpy(),
+                    "cnt": cnt[sel].cpu().numpy(),
+                    "dirty": self.dirty_g[idx][sel].cpu().numpy()}
+        meta = {"kind": "window", "size": self.size, "slide": self.slide, "offset": self.offset,
+                "lateness": self.lateness, "agg": self.agg, "time_mode": self.time_mode,
+                "wm": self.wm, "next_fire_start": self.next_fire_start,
+                "min_live_pane": self.min_live_pane, "max_seen_pane": self.max_seen_pane,
+                "metrics": {"num_records_in": self.metrics.num_records_in,
+                            "num_late_records_dropped": self.metrics.num_late_records_dropped,
+                            "num_records_out": self.metrics.num_records_out,
+                            "num_fires": self.metrics.num_fires, "steps": self.metrics.steps}}
+        return OperatorSnapshot(kg, cols, meta)
+
+    def restore_state(self, rows: dict, meta: dict) -> None:
+        """Rebuild the tables from checkpoint rows (this rank's key groups only)."""
+        self._check_ckpt_meta(meta)
+        dev = self.device
+        self.wm = meta["wm"]
+        self.metrics.current_watermark = self.wm
+        self.next_fire_start = meta["next_fire_start"]
+        self.min_live_pane, self.max_seen_pane = meta["min_live_pane"], meta["max_seen_pane"]
+        for k, v in meta.get("metrics", {}).items():
+            setattr(self.metrics, k, v)
+        if self.min_live_pane is not None and self.max_seen_pane - self.min_live_pane + 1 > self.ring:
+            self.ring = _next_pow2(self.max_seen_pane - self.min_live_pane + 1)
+            self.acc_g = torch.zeros(self.ring * self.nslots, dtype=torch.int64, device=dev)
+            self.cnt_g = torch.zeros(self.ring * self.nslots, dtype=torch.int32, device=dev)
+            self.dirty_g = torch.zeros(self.ring * self.nslots, dtype=torch.uint8, device=dev)
+        self.keys_g.fill_(-1)
+        self.acc_g.zero_()
+        self.cnt_g.zero_()
+        self.dirty_g.zero_()
+        self.occ.zero_()
+        if not len(rows["key"]):
+            return
+        keys = torch.from_numpy(np.ascontiguousarray(rows["key"])).to(dev)
+        uniq, inv = torch.unique(keys, return_inverse=True)
+        slots_u = K.table_insert(uniq.contiguous(), self.keys_g, nsub_log2=self.nsub_log2,
+                                 cap_log2=self.cap_log2)
+        if bool((slots_u < 0).any()):
+            raise RuntimeError("restore: keyed state does not fit the table (raise max_keys)")
+        slot = slots_u[inv]
+        pane = torch.from_numpy(np.ascontiguousarray(rows["pane"])).to(dev)
+        idx = (pane & (self.ring - 1)) * self.nslots + slot
+        self.acc_g[idx] = torch.from_numpy(np.ascontiguousarray(rows["acc"])).to(dev)
+        self.cnt_g[idx] = torch.from_numpy(np.ascontiguousarray(rows["cnt"])).to(dev)
+        self.dirty_g[idx] = torch.from_numpy(np.ascontiguousarray(rows["dirty"])).to(dev)
+        self.occ.copy_(torch.bincount(slots_u >> self.cap_log2, minlength=self.nsub)
+                       .to(torch.int32))

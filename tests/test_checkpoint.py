@@ -1,0 +1,289 @@
+"""Checkpoint / savepoint layout and restore: a run that checkpoints at step k
+and a fresh operator restored from that checkpoint must produce identical results afterwards,
+including at a different world size (key-group re-partitioning) and across devices."""
+import os
+import re
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from mxstream.ops import kernels as K
+from mxstream.parallel.comm import TorchComm
+from mxstream.runtime.checkpoint import (CheckpointCoordinator, CheckpointStorage, read_metadata,
+                                         owned_key_groups)
+from mxstream.runtime.rolling_operator import KeyedRollingOperator
+from mxstream.runtime.session_operator import KeyedSessionOperator
+from mxstream.runtime.window_operator import KeyedWindowOperator
+
+STEPS, CUT, PER = 8, 4, 3000
+
+
+def _batch(step, src=0, n=PER, device="cpu"):
+    k = torch.empty(n, dtype=torch.int64, device=device)
+    t = torch.empty_like(k)
+    v = torch.empty_like(k)
+    K.gen_events(k, t, v, seed=21, stream_id=src, idx0=step * n, nkeys=4000, ts_base=step * 2000,
+                 ts_span=2000, disorder=600, val_lo=0, val_span=1000)
+    return k, t, v
+
+
+def _win(device="cpu", comm=None, **kw):
+    args = dict(size=3000, slide=1000, lateness=1500, agg=K.AGG_SUM_I64, device=device,
+                max_keys=8000, batch_capacity=PER * 2, ooo_bound=500, cap_log2=8)
+    args.update(kw)
+    return KeyedWindowOperator(comm=comm, **args)
+
+
+def _fires(out):
+    return sorted((r.window_start, int(k), int(a), int(c), r.refire)
+                  for r in out for k, a, c in zip(r.keys, r.raw, r.counts))
+
+
+def test_window_checkpoint_restore_equals_uninterrupted(tmp_path):
+    op = _win()
+    storage = CheckpointStorage(tmp_path, job_id="a" * 32)
+    coord = CheckpointCoordinator(storage, {"window": op})
+    tail = []
+    for s in range(STEPS):
+        out = op.process(*_batch(s))
+        if s == CUT:
+            path = coord.trigger(s, sources={"next_step": s + 1})
+        if s > CUT:
+            tail += out
+    tail += op.finish()
+    # Flink layout
+    assert path == tmp_path / ("a" * 32) / f"chk-1"
+    assert (path / "_metadata").exists() and (tmp_path / ("a" * 32) / "shared").is_dir()
+    assert (tmp_path / ("a" * 32) / "taskowned").is_dir()
+    meta = read_metadata(path)
+    assert meta["sources"][0]["next_step"] == CUT + 1 and meta["operators"]["window"]["rows"][0] > 0
+
+    op2 = _win()
+    CheckpointCoordinator(storage, {"window": op2}).restore()
+    tail2 = []
+    for s in range(CUT + 1, STEPS):
+        tail2 += op2.process(*_batch(s))
+    tail2 += op2.finish()
+    assert _fires(tail) == _fires(tail2)
+
+
+def test_retention_savepoint_and_incomplete(tmp_path):
+    op = KeyedRollingOperator(agg=K.AGG_COUNT, device="cpu", max_keys=5000, batch_capacity=PER)
+    storage = CheckpointStorage(tmp_path, job_id="0123456789abcdef" * 2)
+    coord = CheckpointCoordinator(storage, {"count": op}, interval_steps=2, retain=2)
+    for s in range(1, 8):
+        k, _t, v = _batch(s)
+        op.process(k, v)
+        coord.maybe_trigger(s)
+    done = [p.name for p in storage.completed_checkpoints()]
+    assert done == ["chk-2", "chk-3"]  # steps 2,4,6 -> ids 1,2,3; retain 2
+    (storage.job_dir / "chk-9").mkdir()  # no _metadata: incomplete, never restored
+    assert storage.latest().name == "chk-3"
+    sp = coord.savepoint(8, target=str(tmp_path / "sp"))
+    assert re.fullmatch(r"savepoint-012345-[0-9a-f]{12}", sp.name)
+    assert read_metadata(sp)["type"] == "savepoint"
+    op2 = KeyedRollingOperator(agg=K.AGG_COUNT, device="cpu", max_keys=5000, batch_capacity=PER)
+    CheckpointCoordinator(storage, {"count": op2}).restore(sp)
+    for key in (1, 17, 333):
+        assert op.state_of(key) == op2.state_of(key)
+
+
+def test_rolling_restore_continues_counts(tmp_path):
+    a = KeyedRollingOperator(agg=K.AGG_COUNT, device="cpu", max_keys=5000, batch_capacity=PER)
+    storage = CheckpointStorage(tmp_path)
+    coord = CheckpointCoordinator(storage, {"c": a})
+    rows_a = []
+    for s in range(6):
+        k, _t, v = _batch(s)
+        r = a.process(k, v)
+        if s == 2:
+            coord.trigger(s)
+        if s > 2:
+            rows_a.append(sorted(zip(r.keys.tolist(), r.values.tolist(), r.tags.tolist())))
+    b = KeyedRollingOperator(agg=K.AGG_COUNT, device="cpu", max_keys=5000, batch_capacity=PER)
+    CheckpointCoordinator(storage, {"c": b}).restore()
+    rows_b = []
+    for s in range(3, 6):
+        k, _t, v = _batch(s)
+        r = b.process(k, v)
+        rows_b.append(sorted(zip(r.keys.tolist(), r.values.tolist(), r.tags.tolist())))
+    assert rows_a == rows_b
+
+
+def test_session_restore(tmp_path):
+    mk = lambda: KeyedSessionOperator(gap=150, lateness=400, agg=K.AGG_SUM_I64, device="cpu",
+                                      max_keys=8000, batch_capacity=PER, ooo_bound=500)
+    a = mk()
+    storage = CheckpointStorage(tmp_path)
+    coord = CheckpointCoordinator(storage, {"s": a})
+    got_a = []
+    for s in range(STEPS):
+        r = a.process(*_batch(s))
+        if s == CUT:
+            coord.trigger(s)
+        if s > CUT:
+            got_a += list(zip(r.keys.tolist(), r.start.tolist(), r.raw.tolist(), r.counts.tolist()))
+    r = a.finish()
+    got_a += list(zip(r.keys.tolist(), r.start.tolist(), r.raw.tolist(), r.counts.tolist()))
+    b = mk()
+    CheckpointCoordinator(storage, {"s": b}).restore()
+    got_b = []
+    for s in range(CUT + 1, STEPS):
+        r = b.process(*_batch(s))
+        got_b += list(zip(r.keys.tolist(), r.start.tolist(), r.raw.tolist(), r.counts.tolist()))
+    r = b.finish()
+    got_b += list(zip(r.keys.tolist(), r.start.tolist(), r.raw.tolist(), r.counts.tolist()))
+    assert sorted(got_a) == sorted(got_b)
+
+
+def test_owned_key_groups_partition_all():
+    for world, par in ((1, 1), (2, 2), (2, 4), (4, 4), (3, 6)):
+        seen = []
+        for r in range(world):
+            lo, hi = owned_key_groups(r, world, par, 128)
+            seen += list(range(lo, hi + 1))
+        assert seen == list(range(128))
+
+
+# ---- rescale: checkpoint at world 2 (gloo), restore at world 1 and vice versa -------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, root, mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    op = _win(comm=TorchComm(), batch_capacity=PER * 2)
+    storage = CheckpointStorage(root, job_id="b" * 32)
+    coord = CheckpointCoordinator(storage, {"window": op})
+    out = []
+    if mode == "write":
+        for s in range(CUT + 1):
+            op.process(*_batch(s, src=rank))
+        coord.trigger(CUT)
+    else:
+        coord.restore()
+        for s in range(CUT + 1, STEPS):
+            out += op.process(*_batch(s, src=rank))
+        out += op.finish()
+    q.put((rank, _fires(out)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _spawn(world, root, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, root, mode, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(x for _r, f in res for x in f)
+
+
+def _single_run_tail(world_sources):
+    op = _win(batch_capacity=PER * world_sources)
+    out = []
+    for s in range(STEPS):
+        parts = [_batch(s, src=r) for r in range(world_sources)]
+        o = op.process(*[torch.cat([p[i] for p in parts]) for i in range(3)])
+        if s > CUT:
+            out += o
+    out += op.finish()
+    return _fires(out)
+
+
+def test_rescale_2_to_1_and_1_to_2(tmp_path):
+    strip = lambda f: sorted(x[:4] for x in f)
+    ref = strip(_single_run_tail(2))
+    # world 2 writes, world 1 restores (reads both old ranks' files)
+    root = tmp_path / "a"
+    _spawn(2, root, "write")
+    op = _win(batch_capacity=PER * 2)
+    CheckpointCoordinator(CheckpointStorage(root, job_id="b" * 32), {"window": op}).restore()
+    out = []
+    for s in range(CUT + 1, STEPS):
+        parts = [_batch(s, src=r) for r in range(2)]
+        out += op.process(*[torch.cat([p[i] for p in parts]) for i in range(3)])
+    out += op.finish()
+    assert strip(_fires(out)) == ref
+    # world 1 writes, world 2 restores (each rank reads its key groups)
+    root = tmp_path / "b"
+    op = _win(batch_capacity=PER * 2)
+    coord = CheckpointCoordinator(CheckpointStorage(root, job_id="b" * 32), {"window": op})
+    for s in range(CUT + 1):
+        parts = [_batch(s, src=r) for r in range(2)]
+        op.process(*[torch.cat([p[i] for p in parts]) for i in range(3)])
+    coord.trigger(CUT)
+    assert strip(_spawn(2, root, "read")) == ref
+
+
+# ---- GPU -------------------------------------------------------------------------------------
+@pytest.mark.gpu
+def test_gpu_window_checkpoint_restores_on_cpu_and_gpu(tmp_path):
+    op = _win(device="cuda")
+    storage = CheckpointStorage(tmp_path)
+    coord = CheckpointCoordinator(storage, {"window": op})
+    tail = []
+    for s in range(STEPS):
+        out = op.process(*_batch(s, device="cuda"))
+        if s == CUT:
+            coord.trigger(s)
+        if s > CUT:
+            tail += out
+    tail += op.finish()
+    for dev in ("cuda", "cpu"):
+        op2 = _win(device=dev)
+        CheckpointCoordinator(storage, {"window": op2}).restore()
+        t2 = []
+        for s in range(CUT + 1, STEPS):
+            t2 += op2.process(*_batch(s, device=dev))
+        t2 += op2.finish()
+        assert _fires(tail) == _fires(t2), dev
+
+
+@pytest.mark.gpu
+def test_gpu_session_and_rolling_restore(tmp_path):
+    s_op = KeyedSessionOperator(gap=150, lateness=400, agg=K.AGG_SUM_I64, device="cuda",
+                                max_keys=8000, batch_capacity=PER, ooo_bound=500)
+    r_op = KeyedRollingOperator(agg=K.AGG_COUNT, device="cuda", max_keys=5000, batch_capacity=PER)
+    storage = CheckpointStorage(tmp_path)
+    coord = CheckpointCoordinator(storage, {"s": s_op, "r": r_op})
+    tail = []
+    for s in range(STEPS):
+        k, t, v = _batch(s, device="cuda")
+        rs = s_op.process(k, t, v)
+        r_op.process(k, v)
+        if s == CUT:
+            coord.trigger(s)
+        if s > CUT:
+            tail += list(zip(rs.keys.tolist(), rs.start.tolist(), rs.raw.tolist()))
+    rs = s_op.finish()
+    tail += list(zip(rs.keys.tolist(), rs.start.tolist(), rs.raw.tolist()))
+    s2 = KeyedSessionOperator(gap=150, lateness=400, agg=K.AGG_SUM_I64, device="cuda",
+                              max_keys=8000, batch_capacity=PER, ooo_bound=500)
+    r2 = KeyedRollingOperator(agg=K.AGG_COUNT, device="cuda", max_keys=5000, batch_capacity=PER)
+    CheckpointCoordinator(storage, {"s": s2, "r": r2}).restore()
+    t2 = []
+    for s in range(CUT + 1, STEPS):
+        k, t, v = _batch(s, device="cuda")
+        rs = s2.process(k, t, v)
+        r2.process(k, v)
+        t2 += list(zip(rs.keys.tolist(), rs.start.tolist(), rs.raw.tolist()))
+    rs = s2.finish()
+    t2 += list(zip(rs.keys.tolist(), rs.start.tolist(), rs.raw.tolist()))
+    assert sorted(tail) == sorted(t2)
+    for key in (3, 99, 2048):
+        assert r_op.state_of(key) == r2.state_of(key)
