@@ -93,6 +93,7 @@ AggPlan make_agg(py::dict d) {
   p.pane_base = d["pane_base"].cast<int64_t>();
   p.p_lo = d["p_lo"].cast<int64_t>();
   p.fired_hi = d["fired_hi"].cast<int64_t>();
+  p.combined = d.contains("combined") ? d["combined"].cast<int32_t>() : 0;
   if (p.ring <= 0 || (p.ring & (p.ring - 1))) throw std::invalid_argument("ring must be 2^k");
   if (p.cap_log2 < 4 || p.cap_log2 > 14) throw std::invalid_argument("cap_log2 out of range");
   if (p.pg <= 0) throw std::invalid_argument("pg must be positive");
@@ -310,6 +311,17 @@ PYBIND11_MODULE(_mxs_native, m) {
                                intptr_t keys_g, intptr_t slots) {
     cpu::table_insert(P<uint64_t>(keys), n, nsub_log2, cap_log2, P<uint64_t>(keys_g),
                       P<int64_t>(slots));
+  });
+  m.def("gpu_window_combine", [](intptr_t recs, intptr_t counts, int nbuckets, py::dict plan,
+                                 intptr_t out, uint32_t ccap, intptr_t out_counts, intptr_t flags,
+                                 intptr_t stream) {
+    gpu::window_combine(P<Rec>(recs), P<uint32_t>(counts), nbuckets, make_agg(plan), P<Rec>(out),
+                        ccap, P<uint32_t>(out_counts), P<uint32_t>(flags), stream);
+  });
+  m.def("cpu_window_combine", [](intptr_t recs, intptr_t counts, int nbuckets, py::dict plan,
+                                 intptr_t out, uint32_t ccap, intptr_t out_counts, intptr_t flags) {
+    cpu::window_combine(P<Rec>(recs), P<uint32_t>(counts), nbuckets, make_agg(plan), P<Rec>(out),
+                        ccap, P<uint32_t>(out_counts), P<uint32_t>(flags));
   });
   m.def("gpu_set_erase", [](intptr_t set, uint32_t mask, intptr_t keys, int64_t n,
                             intptr_t stream) {

@@ -144,7 +144,7 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p, uint6
         const size_t gi = (size_t)(pane & (p.ring - 1)) * nslots + ((size_t)sub << p.cap_log2) + s;
         const uint64_t v = agg_lift(p.agg, r.val);
         if (p.agg != AGG_COUNT) acc_g[gi] = cnt_g[gi] ? agg_combine(p.agg, acc_g[gi], v) : v;
-        cnt_g[gi] += 1;
+        cnt_g[gi] += p.combined ? r.aux : 1u;
         if (pane <= p.fired_hi) dirty_g[gi] = 1;
       }
     }
@@ -320,6 +320,49 @@ void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
       s = (s + 1) & mask;
     }
     slots[i] = found < 0 ? -1 : (int64_t)((sub << cap_log2) | (uint64_t)found);
+  }
+}
+
+void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const AggPlan& p,
+                    Rec* out, uint32_t ccap, uint32_t* out_counts, uint32_t* flags) {
+  const uint32_t cap = 1u << p.cap_log2, mask = cap - 1;
+  std::vector<uint64_t> keys(cap), acc((size_t)cap * p.np_step);
+  std::vector<uint32_t> cnt((size_t)cap * p.np_step);
+  for (int b = 0; b < nbuckets; ++b) {
+    std::fill(keys.begin(), keys.end(), kEmptyKey);
+    std::fill(cnt.begin(), cnt.end(), 0u);
+    bool inserted = false, ovf = false;
+    const uint32_t c = std::min(counts[b], p.bucket_cap);
+    const Rec* seg = recs + (size_t)b * p.bucket_cap;
+    for (uint32_t e = 0; e < c; ++e) {
+      const Rec& r = seg[e];
+      const int64_t q = (int64_t)r.t - p.p_lo;
+      if (q < 0 || q >= p.np_step) continue;
+      const uint32_t s = probe_insert(keys.data(), r.key, mask, &inserted);
+      if (s == kNoSlot) {
+        ovf = true;
+        continue;
+      }
+      const size_t li = (size_t)q * cap + s;
+      const uint64_t v = agg_lift(p.agg, r.val);
+      acc[li] = cnt[li] ? agg_combine(p.agg, acc[li], v) : v;
+      cnt[li] += 1;
+    }
+    uint32_t n = 0;
+    for (size_t li = 0; li < cnt.size(); ++li) {
+      if (!cnt[li]) continue;
+      if (n >= ccap) {
+        ovf = true;
+        break;
+      }
+      Rec& o = out[(size_t)b * ccap + n++];
+      o.key = keys[li & mask];
+      o.val = p.agg == AGG_COUNT ? 0 : acc[li];
+      o.t = (uint32_t)(p.p_lo + (int64_t)(li >> p.cap_log2));
+      o.aux = cnt[li];
+    }
+    out_counts[b] = n;
+    if (ovf) flags[0] |= 2u;
   }
 }
 

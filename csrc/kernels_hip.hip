@@ -710,7 +710,7 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
           }
           const uint32_t li = (uint32_t)q * cap + s;
           lds_accumulate<AGG>(&sacc[li], r.val);
-          atomicAdd(&scnt[li], 1u);
+          atomicAdd(&scnt[li], p.combined ? r.aux : 1u);
         }
       }
     }
@@ -744,6 +744,101 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
     if (threadIdx.x == 0) occupancy[sub] = (uint32_t)sflag[2];
   }
   if (threadIdx.x == 0 && sflag[1]) atomicOr(&flags[0], 1u);
+}
+
+// ------------------------------------------------------------------------------------------
+// Sender-side combiner (G > 1): one workgroup per send bucket (dest rank, sub-table) folds its raw
+// records into a fresh LDS table of that sub-table's geometry and writes one pre-aggregated
+// record per (key, pane): val = exported accumulator, aux = element count. The all-to-all then
+// moves ~#distinct (key, pane) records instead of every event (sum/min/max/count/avg are all
+// associative, so the receiver's window_agg result is unchanged).
+// ------------------------------------------------------------------------------------------
+template <int AGG>
+__global__ __launch_bounds__(1024) void window_combine_kernel(
+    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
+    Rec* __restrict__ out, uint32_t ccap, uint32_t* __restrict__ out_counts,
+    uint32_t* __restrict__ flags) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int b = blockIdx.x;
+  const uint32_t cap = 1u << p.cap_log2;
+  const uint32_t mask = cap - 1;
+  uint64_t* skeys = (uint64_t*)smem;
+  uint64_t* sacc = skeys + cap;
+  uint32_t* scnt = (uint32_t*)(sacc + (size_t)p.pg * cap);
+  uint32_t* sflag = scnt + (size_t)p.pg * cap;  // [0] records written, [1] overflow
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) skeys[i] = kEmptyKey;
+  if (threadIdx.x < 2) sflag[threadIdx.x] = 0;
+  uint32_t c = counts[b];
+  c = c < p.bucket_cap ? c : p.bucket_cap;
+  const Rec* seg = recs + (size_t)b * p.bucket_cap;
+  Rec* dst = out + (size_t)b * ccap;
+  int inserted = 0;
+  bool ovf = false;
+  for (int pg0 = 0; pg0 < p.np_step; pg0 += p.pg) {
+    const int npg = (p.np_step - pg0) < p.pg ? (p.np_step - pg0) : p.pg;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)npg * cap; i += blockDim.x) {
+      sacc[i] = (uint64_t)lds_identity<AGG>();
+      scnt[i] = 0;
+    }
+    __syncthreads();
+    const int64_t q0 = p.p_lo + pg0;
+    for (uint32_t e0 = threadIdx.x; e0 < c; e0 += blockDim.x * kAggU) {
+      Rec rr[kAggU];
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) {
+        const uint32_t e = e0 + u * blockDim.x;
+        if (e < c) rr[u] = seg[e];
+      }
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) {
+        const uint32_t e = e0 + u * blockDim.x;
+        if (e >= c) break;
+        const Rec& r = rr[u];
+        if (r.t == 0xFFFFFFFFu) continue;  // hole record (staged partition padding)
+        const int64_t q = (int64_t)r.t - q0;
+        if (q < 0 || q >= npg) continue;
+        const uint32_t s = lds_probe_insert(skeys, r.key, mask, &inserted);
+        if (s == kNoSlot) {
+          ovf = true;
+          continue;
+        }
+        const uint32_t li = (uint32_t)q * cap + s;
+        lds_accumulate<AGG>(&sacc[li], r.val);
+        atomicAdd(&scnt[li], 1u);
+      }
+    }
+    __syncthreads();
+    // Compact the touched (slot, pane) cells into the bucket's output run (one LDS atomic per
+    // wave).
+    for (uint32_t i0 = 0; i0 < (uint32_t)npg * cap; i0 += blockDim.x) {
+      const uint32_t i = i0 + threadIdx.x;
+      const bool have = i < (uint32_t)npg * cap && scnt[i] != 0;
+      const unsigned long long m = __ballot(have);
+      uint32_t wb = 0;
+      if (lane_id() == 0 && m) wb = atomicAdd(&sflag[0], (uint32_t)__popcll(m));
+      wb = __shfl(wb, 0);
+      if (have) {
+        const uint32_t pos = wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+        if (pos < ccap) {
+          Rec o;
+          o.key = skeys[i & mask];
+          o.val = lds_export<AGG>(sacc[i]);
+          o.t = (uint32_t)(q0 + (int64_t)(i >> p.cap_log2));
+          o.aux = scnt[i];
+          dst[pos] = o;
+        } else {
+          ovf = true;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (ovf) sflag[1] = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out_counts[b] = sflag[0] < ccap ? sflag[0] : ccap;
+    if (sflag[1]) atomicOr(&flags[0], 2u);  // bit1: combiner overflow (send raw this step)
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2178,6 +2273,43 @@ void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
   if (n <= 0) return;
   hipLaunchKernelGGL(table_insert_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, keys, n, nsub_log2, cap_log2, keys_g, slots);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <int AGG>
+static void launch_combine(const Rec* recs, const uint32_t* counts, int nbuckets,
+                           const AggPlan& p, Rec* out, uint32_t ccap, uint32_t* out_counts,
+                           uint32_t* flags, size_t lds, hipStream_t s) {
+  hipLaunchKernelGGL(window_combine_kernel<AGG>, dim3(nbuckets), dim3(1024), lds, s, recs, counts,
+                     p, out, ccap, out_counts, flags);
+}
+
+void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const AggPlan& p,
+                    Rec* out, uint32_t ccap, uint32_t* out_counts, uint32_t* flags,
+                    intptr_t stream) {
+  if (nbuckets <= 0) return;
+  const size_t cap = (size_t)1 << p.cap_log2;
+  const size_t lds = cap * 8 + (size_t)p.pg * cap * 12 + 16;
+  if (lds > 160 * 1024) throw std::invalid_argument("window_combine: LDS image exceeds 160 KiB");
+  static bool attr_set = false;
+  if (!attr_set) {
+#define MXS_SET_ATTR(A)                                                                     \
+  HIP_CHECK(hipFuncSetAttribute((const void*)window_combine_kernel<A>,                       \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    MXS_SET_ATTR(AGG_SUM_I64) MXS_SET_ATTR(AGG_SUM_F64) MXS_SET_ATTR(AGG_MIN_I64)
+    MXS_SET_ATTR(AGG_MAX_I64) MXS_SET_ATTR(AGG_MIN_F64) MXS_SET_ATTR(AGG_MAX_F64)
+    MXS_SET_ATTR(AGG_COUNT) MXS_SET_ATTR(AGG_AVG_F64) MXS_SET_ATTR(AGG_AVG_I64)
+#undef MXS_SET_ATTR
+    attr_set = true;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  switch (p.agg) {
+#define MXS_C(A) case A: launch_combine<A>(recs, counts, nbuckets, p, out, ccap, out_counts, flags, lds, s); break;
+    MXS_C(AGG_SUM_I64) MXS_C(AGG_SUM_F64) MXS_C(AGG_MIN_I64) MXS_C(AGG_MAX_I64)
+    MXS_C(AGG_MIN_F64) MXS_C(AGG_MAX_F64) MXS_C(AGG_COUNT) MXS_C(AGG_AVG_F64) MXS_C(AGG_AVG_I64)
+#undef MXS_C
+    default: throw std::runtime_error("window_combine: unsupported aggregate");
+  }
   HIP_CHECK(hipGetLastError());
 }
 

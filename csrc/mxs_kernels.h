@@ -25,6 +25,7 @@ struct AggPlan {
   int64_t pane_base;    // records carry pane - pane_base
   int64_t p_lo;         // first pane (relative to pane_base) touched this step
   int64_t fired_hi;     // absolute pane id: panes <= fired_hi are in an already-fired window
+  int32_t combined;     // records are pre-aggregated (aux = element count, val = exported acc)
 };
 
 // Plan of one window firing.
@@ -117,6 +118,9 @@ void keygroups(const uint64_t* keys, int64_t n, int hash_mode, const int32_t* jh
                int32_t* kg, intptr_t stream);
 void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,
                   int64_t* slots, intptr_t stream);
+void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const AggPlan& plan,
+                    Rec* out, uint32_t ccap, uint32_t* out_counts, uint32_t* flags,
+                    intptr_t stream);
 void set_erase(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, intptr_t stream);
 void session_rehash(int64_t nslots, int cap_log2, const uint64_t* keys_o, const int64_t* sess_o,
                     const int64_t* due_o, const int64_t* last_o, uint64_t* keys_n, int64_t* sess_n,
@@ -160,6 +164,8 @@ void keygroups(const uint64_t* keys, int64_t n, int hash_mode, const int32_t* jh
                int32_t* kg);
 void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,
                   int64_t* slots);
+void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const AggPlan& plan,
+                    Rec* out, uint32_t ccap, uint32_t* out_counts, uint32_t* flags);
 }  // namespace cpu
 
 }  // namespace mxs

@@ -151,9 +151,30 @@ class AggPlan:
     pane_base: int
     p_lo: int
     fired_hi: int
+    combined: int = 0    # records are pre-aggregated by window_combine (aux = element count)
 
     def as_dict(self) -> dict:
         return dict(self.__dict__)
+
+
+def window_combine(recs, counts, plan: AggPlan, out, ccap: int, out_counts, flags) -> None:
+    """Sender-side combiner: one pre-aggregated record per (key, pane) of every send bucket.
+    `plan.nsub` here is the number of send buckets (ranks x sub-tables)."""
+    dev = recs.device
+    nb = plan.nsub
+    _check(recs, torch.int64, nb * plan.bucket_cap * REC_WORDS, "recs", dev)
+    _check(counts, torch.int32, nb, "counts", dev)
+    _check(out, torch.int64, nb * ccap * REC_WORDS, "out", dev)
+    _check(out_counts, torch.int32, nb, "out_counts", dev)
+    _check(flags, torch.int32, 1, "flags", dev)
+    if (1 << plan.cap_log2) * 8 + plan.pg * (1 << plan.cap_log2) * 12 + 16 > 160 * 1024:
+        raise ValueError("window_combine: LDS plan too large")
+    m = load()
+    args = (_p(recs), _p(counts), nb, plan.as_dict(), _p(out), int(ccap), _p(out_counts), _p(flags))
+    if _is_gpu(recs):
+        m.gpu_window_combine(*args, _stream(recs))
+    else:
+        m.cpu_window_combine(*args)
 
 
 def window_agg(recs, counts, plan: AggPlan, keys_g, acc_g, cnt_g, dirty_g, occ, flags) -> None:

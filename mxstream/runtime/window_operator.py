@@ -89,7 +89,8 @@ class KeyedWindowOperator:
                  batch_capacity: int = 1 << 20, bucket_slack: float = 1.5,
                  cap_log2: int | None = None, time_mode: str = "event", ooo_bound: int = 0,
                  side_output_late: bool = False, late_capacity: int = 1 << 16,
-                 clock: Callable[[], int] | None = None, external_watermark: bool = False):
+                 clock: Callable[[], int] | None = None, external_watermark: bool = False,
+                 combine: bool | None = None):
         self.device = torch.device(device)
         self.comm = comm or LocalComm()
         self.world = self.comm.world
@@ -153,6 +154,11 @@ class KeyedWindowOperator:
         self.out_n = torch.zeros(1, dtype=torch.int32, device=dev)
         self.late_idx = (torch.empty(late_capacity, dtype=torch.int32, device=dev)
                          if side_output_late else None)
+        # G > 1: sender-side combiner before the all-to-all (all aggregates are associative).
+        self.combine = self.world > 1 if combine is None else bool(combine and self.world > 1)
+        self.comb_send = self.comb_recv = None
+        self.comb_counts = torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
+        self._ccap_hint = 1 << self.cap_log2
 
         # ---- watermark / firing bookkeeping (host, identical on every rank) ----
         self.wm = I64_MIN
@@ -181,6 +187,46 @@ class KeyedWindowOperator:
         self.cursor = torch.zeros(self.nbuckets, dtype=torch.int32, device=self.device)
         self.recv_counts = torch.zeros(self.nbuckets, dtype=torch.int32, device=self.device) \
             if self.world > 1 else self.cursor
+
+    def _combine_and_exchange(self, p_lo: int, np_step: int, pg: int):
+        """G > 1: pre-aggregate every send bucket to one record per (key, pane), then exchange
+        only those (the all-to-all volume drops from ~all events to ~distinct keys x panes).
+        The per-bucket capacity adapts to the largest combined bucket seen (doubling on
+        overflow, which re-runs only the combiner)."""
+        cap = 1 << self.cap_log2
+        nb = self.nbuckets
+        hard = min(self.bucket_cap, cap * np_step)  # distinct (key, pane) per bucket bound
+        while True:
+            ccap = min(hard, max(64, (self._ccap_hint + 7) & ~7))
+            if self.comb_send is None or self.comb_send.numel() < nb * ccap * K.REC_WORDS:
+                words = nb * ccap * K.REC_WORDS
+                self.comb_send = torch.empty(words, dtype=torch.int64, device=self.device)
+                self.comb_recv = torch.empty(words, dtype=torch.int64, device=self.device)
+            self.flags[1:2].zero_()
+            cplan = K.AggPlan(cap_log2=self.cap_log2, nsub=nb, ring=self.ring, agg=self.agg,
+                              nsrc=1, bucket_cap=self.bucket_cap, np_step=np_step, pg=pg,
+                              pane_base=0, p_lo=p_lo, fired_hi=0)
+            K.window_combine(self.send, self.cursor, cplan, self.comb_send, ccap,
+                             self.comb_counts, self.flags[1:2])
+            # One small sync: overflow flag (global, so every rank retries together) + max fill.
+            chk = torch.stack([-(self.flags[1].to(torch.int64) & 2),
+                               -self.comb_counts.max().to(torch.int64)])
+            self.comm.allreduce_min_(chk)
+            ovf, fill = [-x for x in chk.tolist()]
+            if ovf and ccap < hard:
+                self._ccap_hint = ccap * 2
+                self.metrics.extra["combine_regrows"] = self.metrics.extra.get("combine_regrows", 0) + 1
+                continue
+            if ovf:
+                raise RuntimeError("window_combine: a send bucket exceeds its sub-table capacity")
+            self._ccap_hint = max(64, int(fill * 1.25) + 8)
+            break
+        send = self.comb_send[: nb * ccap * K.REC_WORDS]
+        recv = self.comb_recv[: nb * ccap * K.REC_WORDS]
+        self.comm.all_to_all(recv, send)
+        self.comm.all_to_all(self.recv_counts, self.comb_counts)
+        self.metrics.extra["a2a_bytes"] = self.metrics.extra.get("a2a_bytes", 0) + send.numel() * 8
+        return recv, self.recv_counts, ccap
 
     def _grow_ring(self, need: int) -> None:
         """Re-lay the pane ring so `need` consecutive panes fit (rare; keeps absolute pane ids)."""
@@ -268,7 +314,7 @@ class KeyedWindowOperator:
                           event_mode=event_mode, proc_now=proc_now)
             # Watermark valve + pane range + overflow flags: one MIN all-reduce.
             self.comm.allreduce_min_(self.red[:5])
-            if self.world > 1:
+            if self.world > 1 and not self.combine:
                 self.comm.all_to_all(self.recv, self.send)
                 self.comm.all_to_all(self.recv_counts, self.cursor)
             host = self.red.cpu().tolist()  # the step's single host sync
@@ -309,11 +355,15 @@ class KeyedWindowOperator:
             cap = 1 << self.cap_log2
             lds_budget = 150 * 1024 - cap * 8
             pg = max(1, min(gmax - gmin + 1, lds_budget // (cap * 12)))
+            recs, counts, bcap, combined = self.recv, self.recv_counts, self.bucket_cap, 0
+            if self.combine:
+                recs, counts, bcap = self._combine_and_exchange(qmin, gmax - gmin + 1, pg)
+                combined = 1
             aplan = K.AggPlan(cap_log2=self.cap_log2, nsub=self.nsub, ring=self.ring, agg=self.agg,
-                              nsrc=self.world, bucket_cap=self.bucket_cap,
+                              nsrc=self.world, bucket_cap=bcap,
                               np_step=gmax - gmin + 1, pg=pg, pane_base=pane_base,
-                              p_lo=qmin, fired_hi=fired_hi)
-            K.window_agg(self.recv, self.recv_counts, aplan, self.keys_g, self.acc_g, self.cnt_g,
+                              p_lo=qmin, fired_hi=fired_hi, combined=combined)
+            K.window_agg(recs, counts, aplan, self.keys_g, self.acc_g, self.cnt_g,
                          self.dirty_g, self.occ, self.flags)
             # Late-but-allowed data: re-fire already-passed windows that are not cleaned yet.
             if gmin <= fired_hi:

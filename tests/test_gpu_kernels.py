@@ -179,3 +179,42 @@ def test_partition_staged_variant_matches_plain(native, gpu_device, nsub_log2, n
         assert len(a) == len(e)
         assert np.array_equal(a[np.lexsort(a.T[::-1])], e[np.lexsort(e.T[::-1])])
         assert int(c4[b]) % 8 == 0
+
+
+@pytest.mark.parametrize("agg", [K.AGG_SUM_I64, K.AGG_MAX_I64, K.AGG_COUNT, K.AGG_AVG_F64])
+def test_window_combine_matches_cpu(gpu_device, agg):
+    """Sender-side combiner (G > 1 path) on the GPU vs its C++ twin on the same send buckets."""
+    n = 200_000
+    outs = {}
+    for dev in (gpu_device, "cpu"):
+        keys, ts, vals = _gen(dev, n, 20_000, f64=agg in K.AGG_IS_F64)
+        plan = K.PartitionPlan(max_parallelism=128, nsub_log2=4, nranks=2, window_mode=1,
+                               drop_late=0, hash_mode=0, bucket_cap=16384, tbase=1000, pane=500)
+        kg = torch.tensor([(k * 2) // 128 for k in range(128)], dtype=torch.int32, device=dev)
+        cursor = torch.zeros(plan.nbuckets, dtype=torch.int32, device=dev)
+        send = torch.zeros(plan.nbuckets * plan.bucket_cap * 3, dtype=torch.int64, device=dev)
+        stats = K.new_stats(dev)
+        K.partition(keys, ts, vals, plan, kg, cursor, send, stats)
+        qmin, qmax = int(stats[K.STAT_MINPANE]), int(stats[K.STAT_MAXPANE])
+        ccap = 2048 * (qmax - qmin + 1)
+        out = torch.zeros(plan.nbuckets * ccap * 3, dtype=torch.int64, device=dev)
+        oc = torch.zeros(plan.nbuckets, dtype=torch.int32, device=dev)
+        flags = torch.zeros(1, dtype=torch.int32, device=dev)
+        cp = K.AggPlan(cap_log2=11, nsub=plan.nbuckets, ring=1, agg=agg, nsrc=1,
+                       bucket_cap=plan.bucket_cap, np_step=qmax - qmin + 1, pg=2, pane_base=0,
+                       p_lo=qmin, fired_hi=0)
+        K.window_combine(send, cursor, cp, out, ccap, oc, flags)
+        assert int(flags[0]) == 0
+        outs[str(dev)] = (oc.cpu(), out.cpu().view(plan.nbuckets, ccap, 3))
+    (cg, og), (cc, occ) = outs[str(gpu_device)], outs["cpu"]
+    assert torch.equal(cg, cc)
+    for b in range(cg.numel()):
+        a = og[b, :int(cg[b])].numpy()
+        e = occ[b, :int(cc[b])].numpy()
+        sa = a[np.lexsort((a[:, 2], a[:, 0]))]
+        se = e[np.lexsort((e[:, 2], e[:, 0]))]
+        assert np.array_equal(sa[:, [0, 2]], se[:, [0, 2]])  # key, (t | count << 32)
+        if agg == K.AGG_AVG_F64:  # f64 sums: order-dependent rounding
+            assert np.allclose(sa[:, 1].view(np.float64), se[:, 1].view(np.float64), rtol=1e-12)
+        else:
+            assert np.array_equal(sa[:, 1], se[:, 1])
