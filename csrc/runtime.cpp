@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <deque>
 #include <fstream>
 #include <mutex>
@@ -44,6 +45,42 @@ namespace py = pybind11;
 
 namespace mxs {
 namespace {
+
+// ------------------------------------------------------------------------------------------
+// Minimal leveled logger for the native runtime (threads without the GIL): level from
+// MXS_LOG_LEVEL (DEBUG/INFO/WARN/ERROR, default WARN), log4j-like layout on stderr.
+// ------------------------------------------------------------------------------------------
+enum LogLevel { kDebug = 0, kInfo = 1, kWarn = 2, kError = 3 };
+
+int log_threshold() {
+  static const int lvl = [] {
+    const char* e = std::getenv("MXS_LOG_LEVEL");
+    if (!e) return (int)kWarn;
+    const std::string v(e);
+    if (v == "DEBUG" || v == "debug" || v == "TRACE") return (int)kDebug;
+    if (v == "INFO" || v == "info") return (int)kInfo;
+    if (v == "ERROR" || v == "error") return (int)kError;
+    return (int)kWarn;
+  }();
+  return lvl;
+}
+
+void mxs_log(LogLevel level, const std::string& logger, const std::string& msg) {
+  if ((int)level < log_threshold()) return;
+  static std::mutex mu;
+  static const char* names[] = {"DEBUG", "INFO", "WARN", "ERROR"};
+  const auto now = std::chrono::system_clock::now();
+  const std::time_t tt = std::chrono::system_clock::to_time_t(now);
+  const int ms = (int)(std::chrono::duration_cast<std::chrono::milliseconds>(
+                           now.time_since_epoch()).count() % 1000);
+  std::tm tm{};
+  localtime_r(&tt, &tm);
+  char ts[32];
+  std::strftime(ts, sizeof(ts), "%Y-%m-%d %H:%M:%S", &tm);
+  std::lock_guard<std::mutex> g(mu);
+  std::fprintf(stderr, "%s,%03d %-5s mxstream.native.%-25s - %s\n", ts, ms, names[level],
+               logger.c_str(), msg.c_str());
+}
 
 // ------------------------------------------------------------------------------------------
 // Java String.hashCode over the UTF-16 encoding of UTF-8 input (invalid bytes -> U+FFFD).
@@ -466,14 +503,18 @@ class SocketSource {
       const int fd = connect_once();
       if (fd < 0) {
         if (max_retry_ >= 0 && attempt >= max_retry_) {
+          mxs_log(kError, "socket", "could not connect to " + host_ + ":" + std::to_string(port_));
           finish("ConnectException: could not connect to " + host_ + ":" + std::to_string(port_));
           return;
         }
         ++attempt;
+        mxs_log(kWarn, "socket", "connect to " + host_ + ":" + std::to_string(port_) +
+                                     " failed, retry " + std::to_string(attempt));
         std::this_thread::sleep_for(std::chrono::milliseconds(retry_ms_));
         continue;
       }
       fd_ = fd;
+      mxs_log(kInfo, "socket", "connected to " + host_ + ":" + std::to_string(port_));
       char chunk[8192];
       while (!stop_) {
         const ssize_t r = ::recv(fd, chunk, sizeof(chunk), 0);

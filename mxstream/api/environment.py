@@ -29,6 +29,10 @@ class ExecutionConfig:
     global_job_parameters: dict = field(default_factory=dict)
     # "<operator name>:<records>[:<attempts>]" (tests / chaos runs); default from MXS_FAULT.
     fault_injection: str | None = field(default_factory=lambda: os.environ.get("MXS_FAULT"))
+    metrics_json: str | None = field(default_factory=lambda: os.environ.get("MXS_METRICS_JSON"))
+    metrics_prometheus: str | None = field(
+        default_factory=lambda: os.environ.get("MXS_METRICS_PROMETHEUS"))
+    metrics_interval_ms: int = 1000
 
     def set_auto_watermark_interval(self, ms: int) -> "ExecutionConfig":
         self.auto_watermark_interval = int(ms)
@@ -241,10 +245,15 @@ class StreamExecutionEnvironment:
                 result = Executor(self, sinks, job_name, job_id=job_id, restore_from=restore,
                                   attempt=attempts).run()
                 break
-            except Exception:
+            except Exception as e:
                 kind = self.restart_strategy[0]
                 if kind == "fixed_delay" and attempts < self.restart_strategy[1]:
                     attempts += 1
+                    from ..utils.log import get_logger
+
+                    get_logger("api.environment").warning(
+                        "Job %s failed (%s: %s); restart %d of %d", job_name, type(e).__name__, e,
+                        attempts, self.restart_strategy[1])
                     import time as _t
 
                     _t.sleep(self.restart_strategy[2] / 1000.0)

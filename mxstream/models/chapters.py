@@ -175,15 +175,22 @@ JOBS = {
 
 
 def main(argv=None) -> int:
-    """python -m mxstream.models.chapters <Job> [host] [port]  (defaults: localhost 8080)."""
+    """python -m mxstream.models.chapters <Job> [host] [port] [--conf k=v ...]
+    (defaults: localhost 8080; engine keys: mxstream/utils/config.py)."""
+    from ..utils.config import apply_to_env, load_config, strip_conf_args
+
     argv = sys.argv[1:] if argv is None else argv
+    cfg = load_config(argv)
+    argv = strip_conf_args(argv)
     if not argv or argv[0] not in JOBS:
-        print(f"usage: python -m mxstream.models.chapters {{{'|'.join(JOBS)}}} [host] [port]")
+        print(f"usage: python -m mxstream.models.chapters {{{'|'.join(JOBS)}}} [host] [port]"
+              " [--conf key=value ...]")
         return 2
     build, name = JOBS[argv[0]]
     host = argv[1] if len(argv) > 1 else "localhost"
     port = int(argv[2]) if len(argv) > 2 else 8080
     env = StreamExecutionEnvironment.get_execution_environment()
+    apply_to_env(cfg, env)
     build(env, env.socket_text_stream(host, port))
     env.execute(name)
     return 0

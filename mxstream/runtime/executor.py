@@ -16,8 +16,11 @@ import time
 from dataclasses import dataclass, field
 from typing import Any, Callable
 
+from ..utils.log import get_logger
 from .operators import LONG_MAX, OpContext, Operator, Rec, UnionOp, WM
 from .sources import Source
+
+log = get_logger("runtime.executor")
 
 
 class ManualClock:
@@ -102,6 +105,7 @@ class Executor:
         self.attempt = attempt
         self.fault = parse_fault(getattr(env.config, "fault_injection", None))
         self._fault_count = 0
+        self._counts: dict[int, dict[str, int]] = {}
         self.nodes = self._topo(sinks)
         self.children: dict[int, list[Transformation]] = {n.id: [] for n in self.nodes}
         for n in self.nodes:
@@ -171,6 +175,10 @@ class Executor:
                 out = op.process(items) if items else []
                 if now is not None:
                     out.extend(op.on_processing_time(now))
+                if items or out:
+                    c = self._counts.setdefault(n.id, {"numRecordsIn": 0, "numRecordsOut": 0})
+                    c["numRecordsIn"] += sum(1 for it in items if isinstance(it, Rec))
+                    c["numRecordsOut"] += sum(1 for it in out if isinstance(it, Rec))
             for c in self.children[n.id]:
                 if c.kind == "side":
                     side = [it for it in self.ops[n.id].take_side(c.side_tag.tag_id)] \
@@ -215,6 +223,8 @@ class Executor:
         self.metrics["numberOfCompletedCheckpoints"] = self.metrics.get("numberOfCompletedCheckpoints", 0) + 1
         self.metrics["lastCheckpointDuration"] = (time.perf_counter() - t0) * 1e3
         self.metrics["lastCheckpointPath"] = str(storage.checkpoint_dir(n))
+        log.info("Completed checkpoint %d for job %s (%.1f ms)", n, storage.job_id,
+                 self.metrics["lastCheckpointDuration"])
 
     def _restore(self, path, finished: dict) -> None:
         from .checkpoint import read_host_checkpoint
@@ -235,6 +245,27 @@ class Executor:
             finished[by_uid[k]] = v
         self._next_ckpt = int(meta["checkpoint_id"]) + 1
         self.metrics["restoredCheckpointId"] = int(meta["checkpoint_id"])
+        log.info("Restored job %s from %s", self.job_name, path)
+
+    def _reporter(self):
+        c = self.env.config
+        if not (getattr(c, "metrics_json", None) or getattr(c, "metrics_prometheus", None)):
+            return None
+        from ..utils.metrics import REGISTRY, Reporter
+
+        for n in self.nodes:
+            cnt = self._counts.setdefault(n.id, {"numRecordsIn": 0, "numRecordsOut": 0})
+            scope = f"{self.job_name}.{self._uid(n)}"
+            for k in ("numRecordsIn", "numRecordsOut"):
+                REGISTRY.gauge(f"{scope}.{k}", lambda d=cnt, k=k: d[k])
+            op = self.ops.get(n.id)
+            if op is not None and hasattr(op, "num_late_records_dropped"):
+                REGISTRY.gauge(f"{scope}.numLateRecordsDropped",
+                               lambda o=op: o.num_late_records_dropped)
+            if op is not None and hasattr(op, "wm"):
+                REGISTRY.gauge(f"{scope}.currentInputWatermark", lambda o=op: o.wm)
+        return Reporter(json_path=c.metrics_json, prom_path=c.metrics_prometheus,
+                        interval_ms=c.metrics_interval_ms)
 
     def _uid(self, nd) -> str:
         """Stable operator id across job submissions: the user's .uid(), else the position in
@@ -271,6 +302,7 @@ class Executor:
             if done:
                 self._next_ckpt = int(done[-1].name[4:]) + 1
         last_ckpt = self.clock()
+        reporter = self._reporter()
         try:
             while not all(finished.values()):
                 if manual:
@@ -291,6 +323,8 @@ class Executor:
                 if cfg.is_checkpointing_enabled() and self.clock() - last_ckpt >= cfg.interval_ms:
                     self._checkpoint(finished)
                     last_ckpt = self.clock()
+                if reporter is not None:
+                    reporter.maybe_report(job=self.job_name)
             # End of input: MAX watermark (event time), then operators' finish hooks.
             inbox = {}
             for n in sources:
@@ -314,6 +348,11 @@ class Executor:
             op = self.ops.get(n.id)
             if op is not None and hasattr(op, "num_late_records_dropped"):
                 self.metrics[f"{n.name}.numLateRecordsDropped"] = op.num_late_records_dropped
+        for n in self.nodes:
+            for k, v in self._counts.get(n.id, {}).items():
+                self.metrics[f"{n.name}.{k}"] = v
+        if reporter is not None:
+            reporter.maybe_report(force=True, job=self.job_name, final=True)
         return JobExecutionResult(self.job_name, (time.perf_counter() - t0) * 1e3, self.metrics)
 
     def _rebalance(self, src: Transformation, child: Transformation, items: list) -> list:

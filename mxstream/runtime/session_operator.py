@@ -102,7 +102,7 @@ class KeyedSessionOperator:
                  map_prog: E.Program = E.EMPTY, filter_prog: E.Program = E.EMPTY,
                  ooo_bound: int = 0, max_load: float = 0.7, idle_spill_ms: int | None = None,
                  spill_rows: int = 1 << 20, emit_capacity: int | None = None,
-                 external_watermark: bool = False):
+                 external_watermark: bool = False, host_budget_bytes: int | None = None):
         if gap <= 0:
             raise ValueError("session gap must be positive")
         self.device = torch.device(device)
@@ -115,6 +115,7 @@ class KeyedSessionOperator:
         self.ooo_bound = int(ooo_bound)
         self.external_watermark = external_watermark
         self.max_load = max_load
+        self.host_budget_bytes = host_budget_bytes
         self.idle_spill_ms = int(idle_spill_ms if idle_spill_ms is not None else 4 * gap)
         self.metrics = SessionMetrics()
         self.phase_s: dict[str, float] = defaultdict(float)  # host wall time per phase
@@ -288,7 +289,15 @@ class KeyedSessionOperator:
         if self.gpu:
             with self._phase("spill"):
                 self._maybe_spill(wm)
+        if self.host_budget_bytes is not None and self.steps_since_budget_check() and \
+                self.host_bytes() > self.host_budget_bytes:
+            raise MemoryError(f"host-DRAM session state {self.host_bytes()} B exceeds the budget "
+                              f"{self.host_budget_bytes} B")
         return out
+
+    def steps_since_budget_check(self, every: int = 16) -> bool:
+        """The store's byte count walks the hot map: check the budget every `every` steps."""
+        return self.metrics.steps % every == 0
 
     def finish(self) -> SessionRows:
         return self.advance_watermark(I64_MAX)

@@ -159,6 +159,7 @@ class KeyedWindowOperator:
         self.comb_send = self.comb_recv = None
         self.comb_counts = torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
         self._ccap_hint = 1 << self.cap_log2
+        self.timer = None  # utils.metrics.StageTimer: per-stage step_ms histograms when attached
 
         # ---- watermark / firing bookkeeping (host, identical on every rank) ----
         self.wm = I64_MIN
@@ -307,16 +308,18 @@ class KeyedWindowOperator:
                 window_mode=1, drop_late=int(event_mode), hash_mode=self.hash_mode,
                 bucket_cap=self.bucket_cap, late_ts=self._late_ts(old_wm),
                 tbase=self.pane_start(pane_base), pane=self.pane)
-            if n:
-                K.partition(keys, ts, vals, plan, self.kg_dest, self.cursor, self.send, self.stats,
-                            jhash=self.jhash, late_idx=self.late_idx)
+            with self._stage("partition"):
+                if n:
+                    K.partition(keys, ts, vals, plan, self.kg_dest, self.cursor, self.send,
+                                self.stats, jhash=self.jhash, late_idx=self.late_idx)
             K.step_finish(self.stats, self.local_maxts, self.red, bound=self.ooo_bound,
                           event_mode=event_mode, proc_now=proc_now)
             # Watermark valve + pane range + overflow flags: one MIN all-reduce.
             self.comm.allreduce_min_(self.red[:5])
             if self.world > 1 and not self.combine:
-                self.comm.all_to_all(self.recv, self.send)
-                self.comm.all_to_all(self.recv_counts, self.cursor)
+                with self._stage("all_to_all"):
+                    self.comm.all_to_all(self.recv, self.send)
+                    self.comm.all_to_all(self.recv_counts, self.cursor)
             host = self.red.cpu().tolist()  # the step's single host sync
             if host[4]:
                 raise RuntimeError("event timestamp outside the representable pane range "
@@ -324,6 +327,10 @@ class KeyedWindowOperator:
             if host[3]:
                 # A bucket overflowed somewhere: grow the fixed bucket capacity and redo the step.
                 self.metrics.bucket_regrows += 1
+                from ..utils.log import get_logger
+
+                get_logger("runtime.window").warning(
+                    "bucket capacity %d exceeded: regrowing and redoing the step", self.bucket_cap)
                 self._alloc_buckets(self.batch_capacity, self.bucket_slack * 2)
                 continue
             break
@@ -357,14 +364,16 @@ class KeyedWindowOperator:
             pg = max(1, min(gmax - gmin + 1, lds_budget // (cap * 12)))
             recs, counts, bcap, combined = self.recv, self.recv_counts, self.bucket_cap, 0
             if self.combine:
-                recs, counts, bcap = self._combine_and_exchange(qmin, gmax - gmin + 1, pg)
+                with self._stage("combine_all_to_all"):
+                    recs, counts, bcap = self._combine_and_exchange(qmin, gmax - gmin + 1, pg)
                 combined = 1
             aplan = K.AggPlan(cap_log2=self.cap_log2, nsub=self.nsub, ring=self.ring, agg=self.agg,
                               nsrc=self.world, bucket_cap=bcap,
                               np_step=gmax - gmin + 1, pg=pg, pane_base=pane_base,
                               p_lo=qmin, fired_hi=fired_hi, combined=combined)
-            K.window_agg(recs, counts, aplan, self.keys_g, self.acc_g, self.cnt_g,
-                         self.dirty_g, self.occ, self.flags)
+            with self._stage("window_agg"):
+                K.window_agg(recs, counts, aplan, self.keys_g, self.acc_g, self.cnt_g,
+                             self.dirty_g, self.occ, self.flags)
             # Late-but-allowed data: re-fire already-passed windows that are not cleaned yet.
             if gmin <= fired_hi:
                 out.extend(self._refire(gmin, min(gmax, fired_hi), old_wm))
@@ -374,9 +383,17 @@ class KeyedWindowOperator:
         new_wm = max(old_wm, wm_global)
         self.wm = new_wm
         self.metrics.current_watermark = new_wm
-        out.extend(self._fire_ready(new_wm))
-        self._purge(new_wm)
+        with self._stage("fire"):
+            out.extend(self._fire_ready(new_wm))
+            self._purge(new_wm)
+        if self.timer is not None:
+            self.timer.flush()
         return out
+
+    def _stage(self, name: str):
+        import contextlib
+
+        return self.timer.stage(name) if self.timer is not None else contextlib.nullcontext()
 
     def advance_watermark(self, wm: int) -> list[FireResult]:
         """Advance the watermark without data (idle step / processing-time timer / end of input)."""
