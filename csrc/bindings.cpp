@@ -323,6 +323,16 @@ PYBIND11_MODULE(_mxs_native, m) {
     cpu::window_combine(P<Rec>(recs), P<uint32_t>(counts), nbuckets, make_agg(plan), P<Rec>(out),
                         ccap, P<uint32_t>(out_counts), P<uint32_t>(flags));
   });
+  m.def("gpu_parse_text", [](intptr_t text, int64_t text_len, intptr_t starts, int64_t nlines,
+                             std::vector<int32_t> fields, std::vector<int32_t> kinds,
+                             std::string sep, int64_t offset_s, intptr_t cols, intptr_t jhash,
+                             intptr_t status, intptr_t stream) {
+    if (fields.size() != kinds.size() || sep.size() != 1)
+      throw std::invalid_argument("parse_text: spec / separator");
+    gpu::parse_text(reinterpret_cast<const char*>(text), text_len, P<int64_t>(starts), nlines,
+                    fields.data(), kinds.data(), (int)fields.size(), sep[0], offset_s,
+                    P<int64_t>(cols), P<int32_t>(jhash), P<uint8_t>(status), stream);
+  });
   m.def("gpu_set_erase", [](intptr_t set, uint32_t mask, intptr_t keys, int64_t n,
                             intptr_t stream) {
     gpu::set_erase(P<uint64_t>(set), mask, P<int64_t>(keys), n, stream);

@@ -378,4 +378,95 @@ MXS_HD bool rel_pane(int64_t ts, const PartPlan& p, uint32_t* t_out, int64_t* pa
 constexpr int kStatMaxTs = 0, kStatMinPane = 1, kStatMaxPane = 2, kStatLate = 3, kStatOverflow = 4,
               kStatAccepted = 5, kStatCount = 8;
 
+
+// ------------------------------------------------------------------------------------------
+// Text field parsing shared by the C++ runtime (csrc/runtime.cpp, throws Java exceptions) and the
+// GPU parse kernel (csrc/parse_hip.hip, flags the line): one source of truth for semantics.
+// ------------------------------------------------------------------------------------------
+// Long.parseLong / Integer.parseInt grammar: [+-]digits. Returns 0 ok, 1 format error, 2 overflow.
+MXS_HD int parse_long_ascii(const char* s, int64_t len, int64_t lo, int64_t hi, int64_t* out) {
+  if (len <= 0) return 1;
+  int64_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    i = 1;
+    if (len == 1) return 1;
+  }
+  // Java's Long.parseLong: accumulate negatively (covers INT64_MIN), check before each step.
+  int64_t v = 0;
+  const int64_t limit = neg ? lo : -hi;
+  const int64_t multmin = limit / 10;
+  for (; i < len; ++i) {
+    const char c = s[i];
+    if (c < '0' || c > '9') return 1;
+    const int d = c - '0';
+    if (v < multmin) return 2;
+    v *= 10;
+    if (v < limit + d) return 2;
+    v -= d;
+  }
+  *out = neg ? v : -v;
+  return 0;
+}
+
+MXS_HD int64_t days_from_civil_hd(int64_t y, unsigned m, unsigned d) {
+  y -= m <= 2;
+  const int64_t era = (y >= 0 ? y : y - 399) / 400;
+  const unsigned yoe = (unsigned)(y - era * 400);
+  const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + (int64_t)doe - 719468;
+}
+
+// LocalDateTime.parse (ISO_LOCAL_DATE_TIME: yyyy-MM-ddTHH:mm[:ss[.f{1,9}]]) at a fixed offset.
+// Returns false on a DateTimeParseException.
+MXS_HD bool iso_local_datetime(const char* s, int64_t len, int64_t offset_s, int64_t* epoch_s,
+                               int64_t* millis) {
+  if (len < 16) return false;
+  int v[5] = {0, 0, 0, 0, 0};
+  const int pos[5] = {0, 5, 8, 11, 14}, w[5] = {4, 2, 2, 2, 2};
+  for (int f = 0; f < 5; ++f)
+    for (int k = 0; k < w[f]; ++k) {
+      const char c = s[pos[f] + k];
+      if (c < '0' || c > '9') return false;
+      v[f] = v[f] * 10 + (c - '0');
+    }
+  if (s[4] != '-' || s[7] != '-' || s[10] != 'T' || s[13] != ':') return false;
+  int sec = 0, ms = 0;
+  int64_t p = 16;
+  if (p < len) {
+    if (s[p] != ':' || p + 3 > len) return false;
+    for (int k = 1; k <= 2; ++k) {
+      const char c = s[p + k];
+      if (c < '0' || c > '9') return false;
+      sec = sec * 10 + (c - '0');
+    }
+    p += 3;
+    if (p < len) {
+      if (s[p] != '.') return false;
+      ++p;
+      int nd = 0, frac = 0;
+      for (; p < len; ++p) {
+        const char c = s[p];
+        if (c < '0' || c > '9') return false;
+        if (nd < 3) frac = frac * 10 + (c - '0');
+        ++nd;
+      }
+      if (nd == 0 || nd > 9) return false;
+      for (int k = nd; k < 3; ++k) frac *= 10;
+      ms = frac;
+    }
+  }
+  const int y = v[0], mo = v[1], d = v[2], h = v[3], mi = v[4];
+  if (mo < 1 || mo > 12 || d < 1) return false;
+  const bool leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+  const int mdays = mo == 2 ? (leap ? 29 : 28) : (mo == 4 || mo == 6 || mo == 9 || mo == 11) ? 30 : 31;
+  if (d > mdays || h > 23 || mi > 59 || sec > 59) return false;
+  *epoch_s = days_from_civil_hd(y, (unsigned)mo, (unsigned)d) * 86400 + h * 3600 + mi * 60 + sec -
+             offset_s;
+  *millis = ms;
+  return true;
+}
+
 }  // namespace mxs

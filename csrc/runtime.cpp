@@ -241,84 +241,18 @@ double java_parse_double(std::string_view raw) {
 }
 
 int64_t java_parse_long(std::string_view s, int64_t lo, int64_t hi, const char* what) {
-  if (s.empty()) throw ParseError(std::string("NumberFormatException: For input string: \"\""));
-  size_t i = 0;
-  bool neg = false;
-  if (s[0] == '+' || s[0] == '-') {
-    neg = s[0] == '-';
-    i = 1;
-    if (s.size() == 1) throw ParseError("NumberFormatException: For input string: \"" + std::string(s) + "\"");
-  }
-  __int128 v = 0;
-  for (; i < s.size(); ++i) {
-    const char c = s[i];
-    if (c < '0' || c > '9')
-      throw ParseError("NumberFormatException: For input string: \"" + std::string(s) + "\"");
-    v = v * 10 + (c - '0');
-    if (v > (__int128)hi + 1) throw ParseError(std::string("NumberFormatException: ") + what + " overflow \"" + std::string(s) + "\"");
-  }
-  if (neg) v = -v;
-  if (v < lo || v > hi) throw ParseError(std::string("NumberFormatException: ") + what + " overflow \"" + std::string(s) + "\"");
-  return (int64_t)v;
+  int64_t v = 0;
+  const int rc = parse_long_ascii(s.data(), (int64_t)s.size(), lo, hi, &v);
+  if (rc == 1) throw ParseError("NumberFormatException: For input string: \"" + std::string(s) + "\"");
+  if (rc == 2)
+    throw ParseError(std::string("NumberFormatException: ") + what + " overflow \"" + std::string(s) + "\"");
+  return v;
 }
 
-int64_t days_from_civil(int64_t y, unsigned m, unsigned d) {
-  y -= m <= 2;
-  const int64_t era = (y >= 0 ? y : y - 399) / 400;
-  const unsigned yoe = (unsigned)(y - era * 400);
-  const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
-  const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
-  return era * 146097 + (int64_t)doe - 719468;
-}
-
-// LocalDateTime.parse (ISO_LOCAL_DATE_TIME) -> epoch milliseconds at the given offset.
-// Returns seconds and the sub-second millis separately.
+// LocalDateTime.parse (ISO_LOCAL_DATE_TIME) -> epoch seconds + sub-second millis at an offset.
 void parse_iso_local_datetime(std::string_view s, int64_t offset_s, int64_t* epoch_s, int64_t* millis) {
-  auto bad = [&]() { throw ParseError("DateTimeParseException: Text '" + std::string(s) + "' could not be parsed"); };
-  auto num = [&](size_t pos, size_t len) -> int {
-    if (pos + len > s.size()) bad();
-    int v = 0;
-    for (size_t k = 0; k < len; ++k) {
-      const char c = s[pos + k];
-      if (c < '0' || c > '9') bad();
-      v = v * 10 + (c - '0');
-    }
-    return v;
-  };
-  if (s.size() < 16) bad();
-  const int y = num(0, 4);
-  if (s[4] != '-' || s[7] != '-' || s[10] != 'T' || s[13] != ':') bad();
-  const int mo = num(5, 2), d = num(8, 2), h = num(11, 2), mi = num(14, 2);
-  int sec = 0, ms = 0;
-  size_t pos = 16;
-  if (pos < s.size()) {
-    if (s[pos] != ':') bad();
-    sec = num(pos + 1, 2);
-    pos += 3;
-    if (pos < s.size()) {
-      if (s[pos] != '.') bad();
-      ++pos;
-      size_t nd = 0;
-      int frac = 0;
-      while (pos < s.size()) {
-        const char c = s[pos];
-        if (c < '0' || c > '9') bad();
-        if (nd < 3) frac = frac * 10 + (c - '0');
-        ++nd;
-        ++pos;
-      }
-      if (nd == 0 || nd > 9) bad();
-      for (size_t k = nd; k < 3; ++k) frac *= 10;
-      ms = frac;
-    }
-  }
-  static const int mdays[] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
-  if (mo < 1 || mo > 12 || d < 1) bad();
-  const bool leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
-  const int maxd = mdays[mo - 1] + (mo == 2 && leap ? 1 : 0);
-  if (d > maxd || h > 23 || mi > 59 || sec > 59) bad();
-  *epoch_s = days_from_civil(y, (unsigned)mo, (unsigned)d) * 86400 + h * 3600 + mi * 60 + sec - offset_s;
-  *millis = ms;
+  if (!iso_local_datetime(s.data(), (int64_t)s.size(), offset_s, epoch_s, millis))
+    throw ParseError("DateTimeParseException: Text '" + std::string(s) + "' could not be parsed");
 }
 
 enum FieldKind : int {

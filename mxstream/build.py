@@ -24,7 +24,7 @@ BUILD = ROOT / "build" / "native"
 PKG = ROOT / "mxstream"
 ARCH = os.environ.get("MXS_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["kernels_hip.hip", "sort_hip.hip"]
+HIP_SOURCES = ["kernels_hip.hip", "sort_hip.hip", "parse_hip.hip"]
 CXX_SOURCES = ["kernels_cpu.cpp", "runtime.cpp", "sessions.cpp", "bindings.cpp"]
 
 
