@@ -18,7 +18,7 @@ def test_parse_cpu_metrics_lines_bit_exact(gpu_device):
     n = 50_000
     hosts = [f"10.0.{i // 256}.{i % 256}" for i in range(500)] + ["主机-1", "srv"]
     usage = rng.uniform(0, 100, n)
-    fmts = ["{:.1f}", "{:.3f}", "{}", "{:.0f}", "{:.2e}", "  {:.4f} "]
+    fmts = ["{:.1f}", "{:.3f}", "{}", "{:.0f}", "{:.2e}", "{:.4f}\t"]
     lines = []
     for i in range(n):
         u = fmts[i % len(fmts)].format(usage[i])
