@@ -278,6 +278,8 @@ class KeyedStream(DataStream):
         key_fn = self.key_fn
         op = self._one_input("Keyed Aggregation", lambda: O.RollingReduceOp(key_fn, wrapped))
         op._rolling_spec = (kind, p, self.key_pos)
+        op.t.meta = {"kind": "rolling", "agg": kind, "pos": p, "key_pos": self.key_pos,
+                     "key_fn": key_fn}
         return op
 
     def sum(self, pos) -> SingleOutputStreamOperator:

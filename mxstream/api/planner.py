@@ -118,12 +118,20 @@ def plan(env, sinks):
     nodes, children = _consumers(sinks)
     for t in nodes:
         meta = getattr(t, "meta", None) or {}
+        if meta.get("kind") == "rolling" and meta["agg"] in ("sum", "min", "max") \
+                and meta["key_pos"] is not None:
+            _install_native_rolling(env, t, meta)
+            continue
         if meta.get("kind") != "window":
             continue
         ws = meta["stream"]
         spec = meta["spec"]
         a = ws.assigner
-        if not isinstance(a, (W.TumblingEventTimeWindows, W.SlidingEventTimeWindows)):
+        session = type(a) is W.EventTimeSessionWindows
+        if session and ws._late_tag is not None:
+            continue  # late side output of merging windows: host operator
+        if not session and not isinstance(a, (W.TumblingEventTimeWindows,
+                                              W.SlidingEventTimeWindows)):
             continue
         if ws._trigger is not None or ws._evictor is not None or ws.keyed is None:
             continue
@@ -154,13 +162,15 @@ def plan(env, sinks):
                     ok_arities.add(ar)
         if kind is None or not ok_arities:
             continue
-        _install_native(env, t, ws, spec, key_pos, val_pos, kind, result, ok_arities)
+        _install_native(env, t, ws, spec, key_pos, val_pos, kind, result, ok_arities,
+                        session=session)
     return sinks
 
 
-def _install_native(env, t, ws, spec, key_pos, val_pos, kind, result, ok_arities):
+def _install_native(env, t, ws, spec, key_pos, val_pos, kind, result, ok_arities,
+                    session: bool = False):
     from ..runtime import operators as O
-    from ..runtime.native_ops import NativeWindowOp
+    from ..runtime.native_ops import NativeSessionOp, NativeWindowOp
     from .tuples import Tuple
 
     fallback = t.factory
@@ -178,12 +188,29 @@ def _install_native(env, t, ws, spec, key_pos, val_pos, kind, result, ok_arities
 
     device = env.config.device
 
+    cls = NativeSessionOp if session else NativeWindowOp
+
     def factory():
-        return NativeWindowOp(key_fn=key_fn, key_pos=key_pos, val_pos=val_pos, kind=kind,
-                              assigner=assigner, lateness=late, late_tag=tag, device=device,
-                              fallback_factory=fallback, result_builder=builder,
-                              ok_arities=ok_arities)
+        return cls(key_fn=key_fn, key_pos=key_pos, val_pos=val_pos, kind=kind,
+                   assigner=assigner, lateness=late, late_tag=tag, device=device,
+                   fallback_factory=fallback, result_builder=builder, ok_arities=ok_arities)
 
     t.factory = factory
     t.meta = dict(t.meta, native=True)
     _ = O
+
+
+def _install_native_rolling(env, t, meta):
+    """keyBy(<int field>).sum/min/max(p) -> NativeRollingOp (ComputeCpuMax.java:26)."""
+    from ..runtime.native_ops import NativeRollingOp
+
+    fallback = t.factory
+    device = env.config.device
+    key_fn, key_pos, pos, kind = meta["key_fn"], meta["key_pos"], meta["pos"], meta["agg"]
+
+    def factory():
+        return NativeRollingOp(key_fn=key_fn, key_pos=key_pos, val_pos=pos, kind=kind,
+                               device=device, fallback_factory=fallback)
+
+    t.factory = factory
+    t.meta = dict(t.meta, native=True)

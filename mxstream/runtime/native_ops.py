@@ -232,3 +232,201 @@ class NativeWindowOp(Operator):
 
 
 _ = LONG_MAX
+
+
+class NativeRollingOp(Operator):
+    """``keyBy(k).sum/min/max(p)`` (StreamGroupedReduce + ComparableAggregator,
+    ComputeCpuMax.java:26) on the native ``KeyedRollingOperator``: per micro-batch the records
+    are columnarised, the GPU (or C++ twin) returns the post-update value of every record in
+    per-key arrival order, and the output tuples are rebuilt from each key's first record with
+    field p replaced (Flink's ``max(p)`` keeps the other fields of the first record). Output order
+    equals input order. Unsupported data (non-numeric field, mixed types, non-tuple records)
+    switches to the exact host RollingReduceOp."""
+
+    name = "Keyed Aggregation"
+
+    def __init__(self, *, key_fn, key_pos: int, val_pos: int, kind: str, device: str,
+                 fallback_factory, max_keys: int = 1 << 20):
+        self.key_fn, self.key_pos, self.val_pos, self.kind = key_fn, key_pos, val_pos, kind
+        self.device = device
+        self.fallback_factory = fallback_factory
+        self.max_keys = max_keys
+        self.op = None
+        self.fallback = None
+        self.templates: dict = {}
+        self.is_float = None
+        self.str_keys = None
+
+    def open(self, ctx):
+        super().open(ctx)
+        from ..ops.native import load
+
+        self.dict = load().StringDict()
+
+    def _to_fallback(self):
+        self.fallback = self.fallback_factory()
+        self.fallback.open(self.ctx)
+        if self.templates:
+            raise RuntimeError("native rolling state cannot be handed to the host operator")
+
+    def _build(self, v) -> bool:
+        from .rolling_operator import KeyedRollingOperator
+
+        if isinstance(v, bool) or not isinstance(v, (int, float)):
+            return False
+        self.is_float = isinstance(v, float)
+        agg = {("sum", False): K.AGG_SUM_I64, ("sum", True): K.AGG_SUM_F64,
+               ("max", False): K.AGG_MAX_I64, ("max", True): K.AGG_MAX_F64,
+               ("min", False): K.AGG_MIN_I64, ("min", True): K.AGG_MIN_F64}[(self.kind, self.is_float)]
+        self.op = KeyedRollingOperator(agg=agg, device=torch.device(self.device),
+                                       max_keys=self.max_keys, parallelism=1,
+                                       batch_capacity=1024)
+        return True
+
+    def _key_id(self, k) -> int:
+        if isinstance(k, str):
+            if self.str_keys is False:
+                raise TypeError("mixed key types")
+            self.str_keys = True
+            return self.dict.intern(k)
+        if isinstance(k, int) and not isinstance(k, bool) and 0 <= k < (1 << 63) - 2:
+            if self.str_keys is True:
+                raise TypeError("mixed key types")
+            self.str_keys = False
+            return k
+        raise TypeError("unsupported key type for the native path")
+
+    def _run(self, recs: list) -> list:
+        if not recs:
+            return []
+        if self.op is None:
+            v0 = recs[0].value
+            if not isinstance(v0, tuple) or len(v0) <= max(self.key_pos, self.val_pos) \
+                    or not self._build(v0[self.val_pos]):
+                self._to_fallback()
+                return self.fallback.process(recs)
+        n = len(recs)
+        try:
+            kid = np.empty(n, dtype=np.int64)
+            vv = np.empty(n, dtype=np.float64 if self.is_float else np.int64)
+            ar = len(recs[0].value)
+            for i, r in enumerate(recs):
+                v = r.value
+                if not isinstance(v, tuple) or len(v) != ar:
+                    raise TypeError("record shape")
+                k = self._key_id(v[self.key_pos])
+                kid[i] = k
+                if k not in self.templates:
+                    self.templates[k] = v
+                x = v[self.val_pos]
+                if isinstance(x, bool) or isinstance(x, float) != self.is_float or \
+                        not isinstance(x, (int, float)):
+                    raise TypeError("mixed value types")
+                vv[i] = x
+        except TypeError:
+            if self.templates:
+                raise
+            self._to_fallback()
+            return self.fallback.process(recs)
+        dev = self.op.device
+        rows = self.op.process(torch.from_numpy(kid).to(dev),
+                               torch.from_numpy(vv.view(np.int64)).to(dev))
+        order = np.argsort(rows.tags & 0xFFFFFFFF, kind="stable")  # back to input order
+        from ..api.tuples import Tuple
+        from ..utils.hashing import flink_murmur
+
+        P, MP = self.ctx.parallelism, self.ctx.max_parallelism
+        out = []
+        for j in order.tolist():
+            k = int(rows.keys[j])
+            raw = int(rows.values[j])
+            res = float(np.int64(raw).view(np.float64)) if self.is_float else raw
+            row = list(self.templates[k])
+            row[self.val_pos] = res
+            key_obj = self.dict.get(k) if self.str_keys else k
+            sub = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
+            idx = int(rows.tags[j]) & 0xFFFFFFFF
+            out.append(Rec(Tuple(row), recs[idx].ts, sub))
+        return out
+
+    def process(self, items):
+        if self.fallback is not None:
+            return self.fallback.process(items)
+        out, pending = [], []
+        for it in items:
+            if isinstance(it, WM):
+                out.extend(self._run(pending))
+                pending = []
+                out.append(it)
+            else:
+                pending.append(it)
+        out.extend(self._run(pending))
+        return out
+
+    def snapshot(self) -> dict:
+        if self.fallback is not None:
+            return {"fallback": self.fallback.snapshot()}
+        snap = {"templates": dict(self.templates), "strings": list(self.dict.strings()),
+                "str_keys": self.str_keys, "is_float": self.is_float}
+        if self.op is not None:
+            es = self.op.snapshot_state()
+            snap["engine"] = {"columns": es.columns, "meta": es.meta}
+        return snap
+
+    def restore(self, snap: dict) -> None:
+        if "fallback" in snap:
+            self.fallback = self.fallback_factory()
+            self.fallback.open(self.ctx)
+            self.fallback.restore(snap["fallback"])
+            return
+        self.templates = dict(snap["templates"])
+        self.str_keys = snap["str_keys"]
+        for st in snap["strings"]:
+            self.dict.intern(st)
+        if "engine" in snap:
+            self._build(1.0 if snap["is_float"] else 1)
+            self.op.restore_state(snap["engine"]["columns"], snap["engine"]["meta"])
+
+
+class NativeSessionOp(NativeWindowOp):
+    """``window(EventTimeSessionWindows.withGap(g))`` with a field-wise aggregate on the native
+    ``KeyedSessionOperator`` (GPU slot table + host store, or the C++ store on CPU). Results are
+    emitted at the session's maxTimestamp like Flink's WindowOperator."""
+
+    def _build(self, sample_val) -> bool:
+        from .session_operator import KeyedSessionOperator
+
+        is_float = isinstance(sample_val, float)
+        if not isinstance(sample_val, (int, float)) or isinstance(sample_val, bool):
+            return False
+        agg = {("sum", False): K.AGG_SUM_I64, ("sum", True): K.AGG_SUM_F64,
+               ("min", False): K.AGG_MIN_I64, ("min", True): K.AGG_MIN_F64,
+               ("max", False): K.AGG_MAX_I64, ("max", True): K.AGG_MAX_F64,
+               ("count", False): K.AGG_COUNT, ("count", True): K.AGG_COUNT,
+               ("avg", False): K.AGG_AVG_I64, ("avg", True): K.AGG_AVG_F64}[(self.kind, is_float)]
+        self.is_float = is_float
+        self.op = KeyedSessionOperator(gap=self.assigner.gap, lateness=self.lateness, agg=agg,
+                                       device=torch.device(self.device), max_keys=self.max_keys,
+                                       parallelism=1, batch_capacity=max(1024, self.ctx.parallelism),
+                                       external_watermark=True)
+        return True
+
+    def _emit(self, rows) -> list:
+        out = []
+        P, MP = self.ctx.parallelism, self.ctx.max_parallelism
+        from ..utils.hashing import flink_murmur
+
+        for k, end, val, raw, cnt in zip(rows.keys.tolist(), rows.end.tolist(),
+                                         rows.values.tolist(), rows.raw.tolist(),
+                                         rows.counts.tolist()):
+            key_obj = self.dict.get(k) if self.str_keys else k
+            if self.kind in ("sum", "min", "max"):
+                res = float(np.int64(raw).view(np.float64)) if self.is_float else int(raw)
+            elif self.kind == "count":
+                res = int(cnt)
+            else:
+                res = float(val)
+            value = self.result_builder(self.templates[k], res, key_obj)
+            sub = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
+            out.append(Rec(value, end - 1, sub))
+        return out

@@ -118,6 +118,7 @@ class KeyedSessionOperator:
         self.host_budget_bytes = host_budget_bytes
         self.idle_spill_ms = int(idle_spill_ms if idle_spill_ms is not None else 4 * gap)
         self.metrics = SessionMetrics()
+        self.late_side: list = []  # late records are dropped (no side output on this path)
         self.phase_s: dict[str, float] = defaultdict(float)  # host wall time per phase
         self.native = load()
         self.store = self.native.SessionStore(self.gap, self.lateness, agg)

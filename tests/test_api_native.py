@@ -6,7 +6,7 @@ from hypothesis import strategies as st
 
 from mxstream.api.environment import StreamExecutionEnvironment
 from mxstream.api.time import Time, TimeCharacteristic
-from mxstream.api.tuples import Tuple2
+from mxstream.api.tuples import Tuple2, Tuple3
 from mxstream.api.watermarks import BoundedOutOfOrdernessTimestampExtractor
 from mxstream.runtime.executor import ManualClock
 
@@ -80,3 +80,70 @@ def test_native_path_is_selected():
 
     ops = [n.factory() for n in Executor._topo(sinks) if n.kind == "op"]
     assert any(isinstance(o, NativeWindowOp) for o in ops)
+
+
+# ---- keyed rolling aggregations: NativeRollingOp vs the host RollingReduceOp ------------------
+def _run_rolling(events, kind, native, pos=1):
+    out = []
+    env = StreamExecutionEnvironment(4).set_output(out.append)
+    env.config.native = native
+    ks = env.from_collection(events).map(lambda e: Tuple3(e[0], e[1], e[2])).key_by(0)
+    getattr(ks, kind)(pos).print()
+    env.execute("rolling")
+    return out
+
+
+roll_st = st.lists(st.tuples(st.sampled_from(["h1", "h2", "h3", "www.163.com"]),
+                             st.integers(-50, 1000), st.sampled_from(["cpu0", "cpu1"])),
+                   min_size=1, max_size=60)
+
+
+@settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(events=roll_st, kind=st.sampled_from(["max", "min", "sum"]))
+def test_native_rolling_equals_host(events, kind):
+    assert _run_rolling(events, kind, "auto") == _run_rolling(events, kind, "off")
+
+
+def test_native_rolling_floats_and_selection():
+    from mxstream.api import planner
+    from mxstream.runtime.executor import Executor
+    from mxstream.runtime.native_ops import NativeRollingOp
+
+    ev = [("a", 1.5, "x"), ("b", 0.25, "y"), ("a", 3.75, "z"), ("a", -2.0, "w")]
+    assert _run_rolling(ev, "max", "auto") == _run_rolling(ev, "max", "off")
+    env = StreamExecutionEnvironment(4)
+    env.from_collection([("a", 1, "c")]).map(lambda e: Tuple3(*e)).key_by(0).max(1).print()
+    sinks = planner.plan(env, list(env._sinks))
+    ops = [n.factory() for n in Executor._topo(sinks) if n.kind == "op"]
+    assert any(isinstance(o, NativeRollingOp) for o in ops)
+
+
+# ---- session windows: NativeSessionOp vs the host merging WindowOperator ----------------------
+def _run_sessions(events, gap, bound, lateness, native):
+    from mxstream.api.windowing import EventTimeSessionWindows
+
+    out = []
+    env = StreamExecutionEnvironment(4, clock=ManualClock(0)).set_output(out.append)
+    env.config.native = native
+    env.set_stream_time_characteristic(TimeCharacteristic.EventTime)
+    timed = [(i + 1, e) for i, e in enumerate(events)]
+    (env.from_timed_collection(timed)
+     .assign_timestamps_and_watermarks(
+         BoundedOutOfOrdernessTimestampExtractor(Time.milliseconds(bound), extractor=lambda e: e[2]))
+     .map(lambda e: Tuple2(e[0], e[1]))
+     .key_by(0)
+     .window(EventTimeSessionWindows.with_gap(Time.milliseconds(gap)))
+     .allowed_lateness(Time.milliseconds(lateness))
+     .reduce(lambda a, b: Tuple2(a.f0, a.f1 + b.f1))
+     .print())
+    env.execute("sessions")
+    return out
+
+
+@settings(max_examples=50, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(events=events_st, gap=st.sampled_from([100, 1500, 6000]),
+       bound=st.sampled_from([0, 500, 3000]), lateness=st.sampled_from([0, 2000]))
+def test_native_sessions_equal_host(events, gap, bound, lateness):
+    a = _run_sessions(events, gap, bound, lateness, "off")
+    b = _run_sessions(events, gap, bound, lateness, "auto")
+    assert Counter(a) == Counter(b)
