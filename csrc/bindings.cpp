@@ -333,6 +333,20 @@ PYBIND11_MODULE(_mxs_native, m) {
                     fields.data(), kinds.data(), (int)fields.size(), sep[0], offset_s,
                     P<int64_t>(cols), P<int32_t>(jhash), P<uint8_t>(status), stream);
   });
+  m.def("gpu_f64_order_bits", [](intptr_t v, int64_t n, intptr_t o, intptr_t stream) {
+    gpu::f64_order_bits(P<uint64_t>(v), n, P<uint64_t>(o), stream);
+  });
+  m.def("cpu_f64_order_bits", [](intptr_t v, int64_t n, intptr_t o) {
+    cpu::f64_order_bits(P<uint64_t>(v), n, P<uint64_t>(o));
+  });
+  m.def("gpu_segment_median", [](intptr_t heads, int64_t nseg, int64_t total, intptr_t ord,
+                                 intptr_t out, intptr_t stream) {
+    gpu::segment_median(P<int64_t>(heads), nseg, total, P<uint64_t>(ord), P<double>(out), stream);
+  });
+  m.def("cpu_segment_median", [](intptr_t heads, int64_t nseg, int64_t total, intptr_t ord,
+                                 intptr_t out) {
+    cpu::segment_median(P<int64_t>(heads), nseg, total, P<uint64_t>(ord), P<double>(out));
+  });
   m.def("gpu_set_erase", [](intptr_t set, uint32_t mask, intptr_t keys, int64_t n,
                             intptr_t stream) {
     gpu::set_erase(P<uint64_t>(set), mask, P<int64_t>(keys), n, stream);

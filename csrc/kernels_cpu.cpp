@@ -366,5 +366,22 @@ void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const
   }
 }
 
+void f64_order_bits(const uint64_t* v, int64_t n, uint64_t* o) {
+  for (int64_t i = 0; i < n; ++i) o[i] = mxs::f64_order_bits(v[i]);
+}
+
+void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uint64_t* ord,
+                    double* out) {
+  for (int64_t s = 0; s < nseg; ++s) {
+    const int64_t a = heads[s], b = s + 1 < nseg ? heads[s + 1] : total, n = b - a;
+    double m = 0.0;
+    if (n > 0) {
+      const double hi = as_f64(f64_from_order_bits(ord[a + n / 2]));
+      m = (n & 1) ? hi : (hi + as_f64(f64_from_order_bits(ord[a + n / 2 - 1]))) / 2.0;
+    }
+    out[s] = m;
+  }
+}
+
 }  // namespace cpu
 }  // namespace mxs

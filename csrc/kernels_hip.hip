@@ -1911,6 +1911,35 @@ __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t* __res
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Median of `process` windows (ComputeCpuMiddle.java:36-47): elements are radix-
+// sorted by (key, order-preserving value bits); one thread per key segment reads the middle
+// element(s). Java Collections.sort order on Double: -0.0 < 0.0, NaN last (all NaN equal).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void f64_order_bits_kernel(const uint64_t* __restrict__ v,
+                                                             int64_t n, uint64_t* __restrict__ o) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    o[i] = f64_order_bits(v[i]);
+}
+
+__global__ __launch_bounds__(256) void segment_median_kernel(const int64_t* __restrict__ heads,
+                                                             int64_t nseg, int64_t total,
+                                                             const uint64_t* __restrict__ ord,
+                                                             double* __restrict__ out) {
+  for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nseg;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = heads[s], b = s + 1 < nseg ? heads[s + 1] : total;
+    const int64_t n = b - a;
+    double m = 0.0;
+    if (n > 0) {
+      const double hi = as_f64(f64_from_order_bits(ord[a + n / 2]));
+      m = (n & 1) ? hi : (hi + as_f64(f64_from_order_bits(ord[a + n / 2 - 1]))) / 2.0;
+    }
+    out[s] = m;
+  }
+}
+
 int grid_for(int64_t n, int block, int max_blocks) {
   int64_t g = (n + block - 1) / block;
   if (g < 1) g = 1;
@@ -2310,6 +2339,21 @@ void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const
 #undef MXS_C
     default: throw std::runtime_error("window_combine: unsupported aggregate");
   }
+  HIP_CHECK(hipGetLastError());
+}
+
+void f64_order_bits(const uint64_t* v, int64_t n, uint64_t* o, intptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(f64_order_bits_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, v, n, o);
+  HIP_CHECK(hipGetLastError());
+}
+
+void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uint64_t* ord,
+                    double* out, intptr_t stream) {
+  if (nseg <= 0) return;
+  hipLaunchKernelGGL(segment_median_kernel, dim3(grid_for(nseg, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, heads, nseg, total, ord, out);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -469,4 +469,15 @@ MXS_HD bool iso_local_datetime(const char* s, int64_t len, int64_t offset_s, int
   return true;
 }
 
+// Order-preserving map of an f64 bit pattern to u64 (ascending = Java Double.compareTo order:
+// -0.0 < 0.0, every NaN canonical and largest) and its inverse.
+MXS_HD uint64_t f64_order_bits(uint64_t b) {
+  if ((b & 0x7FF0000000000000ull) == 0x7FF0000000000000ull && (b & 0x000FFFFFFFFFFFFFull))
+    b = 0x7FF8000000000000ull;  // NaN
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+MXS_HD uint64_t f64_from_order_bits(uint64_t o) {
+  return (o >> 63) ? (o & 0x7FFFFFFFFFFFFFFFull) : ~o;
+}
+
 }  // namespace mxs

@@ -125,6 +125,9 @@ void parse_text(const char* text, int64_t text_len, const int64_t* starts, int64
                 const int32_t* fields, const int32_t* kinds, int nfields, char sep,
                 int64_t offset_s, int64_t* cols, int32_t* jhash, uint8_t* status,
                 intptr_t stream);
+void f64_order_bits(const uint64_t* v, int64_t n, uint64_t* o, intptr_t stream);
+void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uint64_t* ord,
+                    double* out, intptr_t stream);
 void set_erase(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, intptr_t stream);
 void session_rehash(int64_t nslots, int cap_log2, const uint64_t* keys_o, const int64_t* sess_o,
                     const int64_t* due_o, const int64_t* last_o, uint64_t* keys_n, int64_t* sess_n,
@@ -170,6 +173,9 @@ void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
                   int64_t* slots);
 void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const AggPlan& plan,
                     Rec* out, uint32_t ccap, uint32_t* out_counts, uint32_t* flags);
+void f64_order_bits(const uint64_t* v, int64_t n, uint64_t* o);
+void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uint64_t* ord,
+                    double* out);
 }  // namespace cpu
 
 }  // namespace mxs

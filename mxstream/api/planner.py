@@ -149,6 +149,11 @@ def plan(env, sinks):
             kind, val_pos = spec.fn.native
             result = "value"
             ok_arities = set(range(max(key_pos, val_pos) + 1, 64))
+        elif spec.kind == "process" and getattr(spec.fn, "native", (None,))[0] == "median" \
+                and not session:
+            kind, val_pos = "median", spec.fn.native[1]
+            result = "value"
+            ok_arities = set(range(max(key_pos, val_pos) + 1, 64))
         elif spec.kind == "reduce" and spec.window_fn is None:
             result = "tuple"
             for ar in range(2, 9):
@@ -188,7 +193,9 @@ def _install_native(env, t, ws, spec, key_pos, val_pos, kind, result, ok_arities
 
     device = env.config.device
 
-    cls = NativeSessionOp if session else NativeWindowOp
+    from ..runtime.native_ops import NativeMedianOp
+
+    cls = NativeSessionOp if session else (NativeMedianOp if kind == "median" else NativeWindowOp)
 
     def factory():
         return cls(key_fn=key_fn, key_pos=key_pos, val_pos=val_pos, kind=kind,

@@ -94,7 +94,13 @@ def build_compute_cpu_avg(env, text, aggregate=None):
 
 
 class MedianUsage(ProcessWindowFunction):
-    """ComputeCpuMiddle.java:34-48: buffer, sort, median (0.0 when empty)."""
+    """ComputeCpuMiddle.java:34-48: buffer, sort, median (0.0 when empty).
+
+    ``native`` tells the planner this is the median of field 1, so the window can run on the
+    device list-window operator (sort + segment-median kernels); this method is the exact host
+    implementation used otherwise."""
+
+    native = ("median", 1)
 
     def process(self, key, context, elements, out):
         values = sorted(t.f1 for t in elements)

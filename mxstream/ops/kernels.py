@@ -327,3 +327,58 @@ def table_insert(keys: torch.Tensor, keys_g: torch.Tensor, *, nsub_log2: int,
     else:
         m.cpu_table_insert(*args)
     return slots
+
+
+def sort_pairs(keys: torch.Tensor, vals: torch.Tensor, *, bits: int = 64):
+    """Stable ascending sort of (uint64 key bits, int64 value) pairs over the low `bits` key bits.
+    GPU: rocPRIM onesweep radix sort (csrc/sort_hip.hip); CPU: torch stable sort."""
+    n = keys.numel()
+    dev = keys.device
+    _check(keys, torch.int64, n, "keys", dev)
+    _check(vals, torch.int64, n, "vals", dev)
+    if not 1 <= bits <= 64:
+        raise ValueError("bits must be in [1, 64]")
+    if _is_gpu(keys):
+        m = load()
+        ko = torch.empty_like(keys)
+        vo = torch.empty_like(vals)
+        if n:
+            need = m.gpu_sort_pairs_temp_bytes(n, 0, bits)
+            tmp = torch.empty(max(1, need), dtype=torch.uint8, device=dev)
+            m.gpu_sort_pairs(tmp.data_ptr(), tmp.numel(), keys.data_ptr(), ko.data_ptr(),
+                             vals.data_ptr(), vo.data_ptr(), n, 0, bits, _stream(keys))
+        return ko, vo
+    k = keys if bits == 64 else keys & ((1 << bits) - 1)
+    # Unsigned order of the 64-bit patterns: flip the sign bit for a signed sort.
+    ks = k ^ I64_MIN if bits == 64 else k
+    order = torch.sort(ks, stable=True).indices
+    return keys[order], vals[order]
+
+
+def f64_order_bits(v: torch.Tensor) -> torch.Tensor:
+    """f64 bit patterns (int64 view) -> u64 bits whose unsigned order is Double.compareTo order."""
+    _check(v, torch.int64, v.numel(), "v", v.device)
+    o = torch.empty_like(v)
+    m = load()
+    if _is_gpu(v):
+        m.gpu_f64_order_bits(v.data_ptr(), v.numel(), o.data_ptr(), _stream(v))
+    else:
+        m.cpu_f64_order_bits(v.data_ptr(), v.numel(), o.data_ptr())
+    return o
+
+
+def segment_median(heads: torch.Tensor, ord_bits: torch.Tensor) -> torch.Tensor:
+    """Median (Java ComputeCpuMiddle semantics) of every sorted segment starting at `heads`."""
+    dev = ord_bits.device
+    _check(heads, torch.int64, heads.numel(), "heads", dev)
+    _check(ord_bits, torch.int64, ord_bits.numel(), "ord", dev)
+    if heads.numel() and (int(heads[0]) != 0 or int(heads[-1]) >= max(1, ord_bits.numel())):
+        raise ValueError("segment heads out of range")
+    out = torch.empty(heads.numel(), dtype=torch.float64, device=dev)
+    m = load()
+    args = (heads.data_ptr(), heads.numel(), ord_bits.numel(), ord_bits.data_ptr(), out.data_ptr())
+    if _is_gpu(ord_bits):
+        m.gpu_segment_median(*args, _stream(ord_bits))
+    else:
+        m.cpu_segment_median(*args)
+    return out

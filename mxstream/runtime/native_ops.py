@@ -430,3 +430,39 @@ class NativeSessionOp(NativeWindowOp):
             sub = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
             out.append(Rec(value, end - 1, sub))
         return out
+
+
+class NativeMedianOp(NativeWindowOp):
+    """``process(<median>)`` windows (ComputeCpuMiddle.java:34-48) on the device list-window
+    operator: elements stay on the device per pane, the fire sorts (key, value) with two radix
+    passes and a kernel takes the per-key median."""
+
+    def _build(self, sample_val) -> bool:
+        from .list_window_operator import KeyedListWindowOperator
+
+        if not isinstance(sample_val, float):
+            return False  # the reference's values are Double; anything else: host operator
+        self.is_float = True
+        a = self.assigner
+        self.op = KeyedListWindowOperator(
+            size=a.size, slide=a.slide, offset=a.offset,
+            lateness=self.lateness if a.is_event_time() else 0, device=torch.device(self.device),
+            time_mode="event" if a.is_event_time() else "processing")
+        return True
+
+    def _emit(self, fired) -> list:
+        out = []
+        P, MP = self.ctx.parallelism, self.ctx.max_parallelism
+        from ..utils.hashing import flink_murmur
+
+        for s, e, keys, med in fired:
+            for k, v in zip(keys.tolist(), med.tolist()):
+                key_obj = self.dict.get(k) if self.str_keys else k
+                value = self.result_builder(self.templates[k], float(v), key_obj)
+                sub = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
+                out.append(Rec(value, e - 1, sub))
+        return out
+
+    def snapshot(self) -> dict:
+        raise NotImplementedError("checkpointing of native process windows is not supported; "
+                                  "run with native='off' for checkpointed process windows")

@@ -147,3 +147,35 @@ def test_native_sessions_equal_host(events, gap, bound, lateness):
     a = _run_sessions(events, gap, bound, lateness, "off")
     b = _run_sessions(events, gap, bound, lateness, "auto")
     assert Counter(a) == Counter(b)
+
+
+# ---- process-window median: NativeMedianOp vs the host WindowOperator ------------------------
+def _run_median(events, size, slide, bound, lateness, native):
+    from mxstream.models.chapters import MedianUsage
+
+    out = []
+    env = StreamExecutionEnvironment(4, clock=ManualClock(0)).set_output(out.append)
+    env.config.native = native
+    env.set_stream_time_characteristic(TimeCharacteristic.EventTime)
+    timed = [(i + 1, e) for i, e in enumerate(events)]
+    (env.from_timed_collection(timed)
+     .assign_timestamps_and_watermarks(
+         BoundedOutOfOrdernessTimestampExtractor(Time.milliseconds(bound), extractor=lambda e: e[2]))
+     .map(lambda e: Tuple2(e[0], float(e[1]) / 4))
+     .key_by(0)
+     .time_window(Time.milliseconds(size), Time.milliseconds(slide))
+     .allowed_lateness(Time.milliseconds(lateness))
+     .process(MedianUsage())
+     .print())
+    env.execute("median")
+    return out
+
+
+@settings(max_examples=40, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(events=events_st, size_k=st.integers(1, 4), slide_div=st.sampled_from([1, 2]),
+       bound=st.sampled_from([0, 1000]), lateness=st.sampled_from([0, 3000]))
+def test_native_median_equals_host(events, size_k, slide_div, bound, lateness):
+    size = size_k * 2000
+    a = _run_median(events, size, size // slide_div, bound, lateness, "off")
+    b = _run_median(events, size, size // slide_div, bound, lateness, "auto")
+    assert Counter(a) == Counter(b)

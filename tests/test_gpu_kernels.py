@@ -218,3 +218,28 @@ def test_window_combine_matches_cpu(gpu_device, agg):
             assert np.allclose(sa[:, 1].view(np.float64), se[:, 1].view(np.float64), rtol=1e-12)
         else:
             assert np.array_equal(sa[:, 1], se[:, 1])
+
+
+def test_segment_median_vs_numpy(gpu_device):
+    rng = np.random.default_rng(9)
+    n = 300_000
+    keys = rng.integers(0, 5000, n)
+    vals = rng.normal(0, 100, n)
+    vals[::977] = -0.0
+    vals[::1301] = 0.0
+    kt = torch.from_numpy(keys).to(gpu_device)
+    vt = torch.from_numpy(vals).to(gpu_device).view(torch.int64)
+    uniq, ids = torch.unique(kt, return_inverse=True)
+    ordv = K.f64_order_bits(vt.contiguous())
+    ordv, ids = K.sort_pairs(ordv, ids.contiguous(), bits=64)
+    ids, ordv = K.sort_pairs(ids.contiguous(), ordv, bits=13)
+    heads = torch.nonzero(torch.cat([torch.ones(1, dtype=torch.bool, device=gpu_device),
+                                     ids[1:] != ids[:-1]])).flatten()
+    med = K.segment_median(heads.contiguous(), ordv).cpu().numpy()
+    got = dict(zip(uniq[ids[heads]].cpu().tolist(), med.tolist()))
+    for k in range(0, 5000, 97):
+        v = np.sort(vals[keys == k])
+        if not len(v):
+            continue
+        exp = v[len(v) // 2] if len(v) % 2 else (v[len(v) // 2] + v[len(v) // 2 - 1]) / 2
+        assert got[k] == exp
