@@ -24,7 +24,8 @@ class ExecutionConfig:
     auto_watermark_interval: int = 0        # ms; set to 200 by EventTime (Flink default)
     rebalance_start: int = 0                # first channel of round-robin rebalance
     native: str = "auto"                    # auto | off | force  (native keyed operators)
-    device: str = "cpu"                     # cpu | cuda  (where native operators run)
+    # cpu | cuda: where native operators run (MXS_DEVICE overrides the default)
+    device: str = field(default_factory=lambda: os.environ.get("MXS_DEVICE", "cpu"))
     batch_size: int = 1 << 16
     global_job_parameters: dict = field(default_factory=dict)
     # "<operator name>:<records>[:<attempts>]" (tests / chaos runs); default from MXS_FAULT.
