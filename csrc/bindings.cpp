@@ -74,6 +74,10 @@ PartPlan make_part(py::dict d) {
   p.pane = d["pane"].cast<int64_t>();
   if (p.window_mode && p.pane <= 0) throw std::invalid_argument("pane length must be positive");
   p.inv_pane = p.pane > 0 ? 1.0 / (double)p.pane : 0.0;
+  p.rec_words = d.contains("rec_words") ? d["rec_words"].cast<int32_t>() : 3;
+  if (p.rec_words != 2 && p.rec_words != 3) throw std::invalid_argument("rec_words must be 2 or 3");
+  if (p.rec_words == 2 && !p.window_mode)
+    throw std::invalid_argument("compact records are for the window path");
   if (p.max_parallelism <= 0 || p.nranks <= 0 || p.nsub_log2 < 0 || p.nsub_log2 > 20)
     throw std::invalid_argument("bad partition plan");
   return p;
@@ -94,6 +98,8 @@ AggPlan make_agg(py::dict d) {
   p.p_lo = d["p_lo"].cast<int64_t>();
   p.fired_hi = d["fired_hi"].cast<int64_t>();
   p.combined = d.contains("combined") ? d["combined"].cast<int32_t>() : 0;
+  p.rec_words = d.contains("rec_words") ? d["rec_words"].cast<int32_t>() : 3;
+  if (p.rec_words != 2 && p.rec_words != 3) throw std::invalid_argument("rec_words must be 2 or 3");
   if (p.ring <= 0 || (p.ring & (p.ring - 1))) throw std::invalid_argument("ring must be 2^k");
   if (p.cap_log2 < 4 || p.cap_log2 > 14) throw std::invalid_argument("cap_log2 out of range");
   if (p.pg <= 0) throw std::invalid_argument("pg must be positive");

@@ -12,6 +12,18 @@
 namespace mxs {
 namespace cpu {
 
+// Record at index `idx` of a bucket buffer in either layout (24-byte Rec / 16-byte RecC).
+static Rec load_any(const Rec* base, size_t idx, int rec_words) {
+  if (rec_words == 3) return base[idx];
+  const RecC& c = reinterpret_cast<const RecC*>(base)[idx];
+  Rec r;
+  r.key = c.key;
+  r.val = (uint64_t)(int64_t)(int32_t)c.val;
+  r.t = c.t;
+  r.aux = 0;
+  return r;
+}
+
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
@@ -64,14 +76,20 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
     const int32_t jh = p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
     const uint32_t b = bucket_of(key, jh, p, kg_dest);
     const uint32_t pos = cursor[b]++;
-    if (pos < p.bucket_cap) {
+    if (pos >= p.bucket_cap) {
+      ovf |= 1;
+    } else if (p.rec_words == 2) {  // compact 16-byte record (int32 value)
+      RecC& r = reinterpret_cast<RecC*>(out)[(size_t)b * p.bucket_cap + pos];
+      if ((int64_t)(int32_t)vals[i] != (int64_t)vals[i]) ovf |= 4;
+      r.key = key;
+      r.val = (uint32_t)vals[i];
+      r.t = rt;
+    } else {
       Rec& r = out[(size_t)b * p.bucket_cap + pos];
       r.key = key;
       r.val = vals[i];
       r.t = rt;
       r.aux = (uint32_t)i;
-    } else {
-      ovf |= 1;
     }
   }
   stats[kStatMaxTs] = tmax;
@@ -100,7 +118,8 @@ void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int3
   red[2] = wm;
   red[3] = -(stats[kStatOverflow] & 1);
   red[4] = -((stats[kStatOverflow] >> 1) & 1);
-  red[5] = red[6] = red[7] = 0;
+  red[5] = -((stats[kStatOverflow] >> 2) & 1);  // compact records cannot hold a value
+  red[6] = red[7] = 0;
   for (int j = 0; j < kStatCount; ++j) red[8 + j] = stats[j];
 }
 
@@ -130,9 +149,9 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p, uint6
     for (int src = 0; src < p.nsrc; ++src) {
       uint32_t c = counts[(size_t)src * p.nsub + sub];
       c = std::min(c, p.bucket_cap);
-      const Rec* seg = recs + ((size_t)src * p.nsub + sub) * p.bucket_cap;
+      const size_t seg0 = ((size_t)src * p.nsub + sub) * p.bucket_cap;
       for (uint32_t e = 0; e < c; ++e) {
-        const Rec& r = seg[e];
+        const Rec r = load_any(recs, seg0 + e, p.rec_words);
         const int64_t q = (int64_t)r.t - p.p_lo;
         if (q < 0 || q >= p.np_step) continue;
         const uint32_t s = probe_insert(keys, r.key, mask, &inserted);
@@ -333,9 +352,8 @@ void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const
     std::fill(cnt.begin(), cnt.end(), 0u);
     bool inserted = false, ovf = false;
     const uint32_t c = std::min(counts[b], p.bucket_cap);
-    const Rec* seg = recs + (size_t)b * p.bucket_cap;
     for (uint32_t e = 0; e < c; ++e) {
-      const Rec& r = seg[e];
+      const Rec r = load_any(recs, (size_t)b * p.bucket_cap + e, p.rec_words);
       const int64_t q = (int64_t)r.t - p.p_lo;
       if (q < 0 || q >= p.np_step) continue;
       const uint32_t s = probe_insert(keys.data(), r.key, mask, &inserted);

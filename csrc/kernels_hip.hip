@@ -558,6 +558,195 @@ constexpr size_t kStagedLds = (size_t)kStageMaxNb * 8 * sizeof(Rec) + (size_t)kS
                               (size_t)kStageMaxNb * 4 * 4 + 20 * 4 + 16 * 8;
 static_assert(kStagedLds <= 160 * 1024, "staged partition LDS image exceeds 160 KiB");
 
+// ------------------------------------------------------------------------------------------
+// Compact staged partition (16-byte RecC, integer window aggregates). Same structure as the
+// staged kernel with three differences that the counters pointed at (profiles/r1_bench_pmc.md):
+//  * pass A reads only the keys (the bucket is a function of the key); late / unrepresentable
+//    records are counted into the reservation and their slots filled with holes at the end,
+//    so pass B alone reads ts/val (32 B of input per event instead of 40 B);
+//  * a record is one 16-byte vector: a write group is 4 records = one 64-byte sector, the LDS
+//    image halves (~72 KB) and two workgroups fit per CU (twice the waves to hide latency);
+//  * records move LDS -> HBM as uint4 copies (no 24-byte splicing).
+// A value outside int32 sets stats overflow bit 2: the host redoes the step with 24-byte records.
+// ------------------------------------------------------------------------------------------
+constexpr int kCU = 2;                   // events per thread per round
+constexpr int kCR = 1024 * kCU;          // records per round
+constexpr int kCG = 4;                   // records per write group (64 B)
+constexpr int kCMaxNb = 512;
+constexpr size_t kCompactLds = (size_t)kCMaxNb * kCG * sizeof(RecC) + (size_t)kCR * sizeof(RecC) +
+                               (size_t)kCMaxNb * 5 * 4 + 20 * 4 + 16 * 8;
+static_assert(kCompactLds <= 80 * 1024, "compact partition must fit two workgroups per CU");
+
+template <int V>
+__global__ __launch_bounds__(1024) void partition_compact_kernel(
+    const uint64_t* __restrict__ keys, const int64_t* __restrict__ ts,
+    const uint64_t* __restrict__ vals, const int32_t* __restrict__ jhash_tab, int64_t n,
+    int64_t chunk, PartPlan plan, const int32_t* __restrict__ kg_dest,
+    uint32_t* __restrict__ cursor, RecC* __restrict__ out, int64_t* __restrict__ stats,
+    uint32_t* __restrict__ late_idx, uint32_t late_cap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char csm[];
+  const int nb = plan.nranks << plan.nsub_log2;
+  uint4* carry = (uint4*)csm;                                  // [kCMaxNb][kCG]
+  uint4* rbuf = carry + kCMaxNb * kCG;                         // [kCR]
+  uint32_t* run_base = (uint32_t*)(rbuf + kCR);                // [kCMaxNb]
+  uint32_t* resv = run_base + kCMaxNb;                         // reserved records per bucket
+  uint32_t* lcnt = resv + kCMaxNb;                             // records appended per bucket
+  uint32_t* rcnt = lcnt + kCMaxNb;                             // this round's count per bucket
+  uint32_t* roff = rcnt + kCMaxNb;                             // this round's offsets
+  uint32_t* wsum = roff + kCMaxNb;                             // 17 scan words (+pad)
+  int64_t* lred = (int64_t*)(wsum + 20);                       // 16 x i64
+
+  for (int b = threadIdx.x; b < kCMaxNb; b += blockDim.x) {
+    run_base[b] = 0;
+    lcnt[b] = 0;
+    rcnt[b] = 0;
+  }
+  __syncthreads();
+  const int64_t start = (int64_t)blockIdx.x * chunk;
+  const int64_t end = start + chunk < n ? start + chunk : n;
+
+  // Pass A: bucket histogram from the keys alone.
+  for (int64_t i0 = start + threadIdx.x; i0 < end; i0 += (int64_t)blockDim.x * kPartU) {
+    uint64_t k[kPartU];
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i < end) k[u] = ldin<V>(&keys[i]);
+    }
+#pragma unroll
+    for (int u = 0; u < kPartU; ++u) {
+      const int64_t i = i0 + (int64_t)u * blockDim.x;
+      if (i >= end) break;
+      const int32_t jh = plan.hash_mode ? jhash_tab[k[u]] : java_long_hash((int64_t)k[u]);
+      atomicAdd(&run_base[bucket_of(k[u], jh, plan, kg_dest)], 1u);
+    }
+  }
+  __syncthreads();
+  bool overflow = false;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    const uint32_t c = (run_base[b] + (kCG - 1)) & ~(uint32_t)(kCG - 1);
+    uint32_t base = 0;
+    if (c) {
+      base = atomicAdd(&cursor[b], c);
+      if (base + c > plan.bucket_cap) overflow = true;
+    }
+    run_base[b] = base;
+    resv[b] = c;
+  }
+  if (threadIdx.x == 0) wsum[18] = 0;
+  __syncthreads();
+  if (overflow) wsum[18] = 1;
+  __syncthreads();
+  const bool any_ovf = wsum[18] != 0;
+  const uint32_t bcap = plan.bucket_cap;
+
+  int64_t tmax = INT64_MIN, qmin = INT64_MAX, qmax = INT64_MIN, nlate = 0, nacc = 0;
+  int64_t flags = 0;
+  // Pass B: rounds of kCR records -> LDS sort by bucket -> whole 64-byte groups.
+  for (int64_t r0 = start; r0 < end; r0 += kCR) {
+    uint32_t bk[kCU], rk[kCU];
+    uint4 rec[kCU];
+    bool keep[kCU];
+#pragma unroll
+    for (int u = 0; u < kCU; ++u) {
+      const int64_t i = r0 + (int64_t)u * blockDim.x + threadIdx.x;
+      keep[u] = false;
+      if (i < end) {
+        const uint64_t k = ldin<V>(&keys[i]);
+        const int64_t t = ldin<V>(&ts[i]);
+        const uint64_t v = ldin<V>(&vals[i]);
+        tmax = t > tmax ? t : tmax;
+        const PartEval e = part_eval(k, t, jhash_tab, plan, kg_dest);
+        if (e.kind == 1) {
+          ++nlate;
+          if (late_idx) {
+            const unsigned long long pos = atomicAdd((unsigned long long*)&stats[kStatLate], 1ull);
+            if (pos < late_cap) late_idx[pos] = (uint32_t)i;
+          }
+        } else if (e.kind == 2) {
+          flags |= 2;
+        } else {
+          if ((int64_t)(int32_t)v != (int64_t)v) flags |= 4;  // needs 24-byte records
+          ++nacc;
+          qmin = (int64_t)e.t < qmin ? (int64_t)e.t : qmin;
+          qmax = (int64_t)e.t > qmax ? (int64_t)e.t : qmax;
+          keep[u] = true;
+          bk[u] = e.bucket;
+          rec[u] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), (uint32_t)v, e.t);
+          rk[u] = atomicAdd(&rcnt[e.bucket], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t myc = threadIdx.x < (unsigned)nb ? rcnt[threadIdx.x] : 0u;
+    const uint32_t off = block_exclusive_scan(myc, wsum);
+    if (threadIdx.x < (unsigned)nb) roff[threadIdx.x] = off;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kCU; ++u)
+      if (keep[u]) rbuf[roff[bk[u]] + rk[u]] = rec[u];
+    __syncthreads();
+    if (threadIdx.x < (unsigned)nb && !any_ovf) {
+      const int b = threadIdx.x;
+      const uint32_t nc = lcnt[b] & (kCG - 1);
+      const uint32_t nr = rcnt[b];
+      const uint32_t tot = nc + nr;
+      const uint32_t groups = tot / kCG;
+      uint4* dstb = (uint4*)(out + (size_t)b * bcap + run_base[b] + (lcnt[b] - nc));
+      const uint4* src_r = rbuf + roff[b];
+      for (uint32_t g = 0; g < groups; ++g) {
+#pragma unroll
+        for (int q = 0; q < kCG; ++q) {
+          const uint32_t j = g * kCG + q;
+          dstb[j] = j < nc ? carry[b * kCG + j] : src_r[j - nc];
+        }
+      }
+      const uint32_t rem = tot - groups * kCG;
+      for (uint32_t j = 0; j < rem; ++j) {
+        const uint32_t jj = groups * kCG + j;
+        if (jj < nc) continue;  // no group written: the carried record is already in place
+        carry[b * kCG + j] = src_r[jj - nc];
+      }
+      lcnt[b] += nr;
+      rcnt[b] = 0;
+    }
+    __syncthreads();
+  }
+  // Tail: pad the last partial group and fill the rest of the reservation (slots reserved for
+  // late / dropped records) with holes, whole groups at a time.
+  if (threadIdx.x < (unsigned)nb && !any_ovf) {
+    const int b = threadIdx.x;
+    const uint32_t nc = lcnt[b] & (kCG - 1);
+    uint4* dst = (uint4*)(out + (size_t)b * bcap + run_base[b]);
+    const uint4 hole = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, kHoleT);
+    uint32_t w = lcnt[b] - nc;
+    if (nc) {
+#pragma unroll
+      for (int j = 0; j < kCG; ++j) dst[w + j] = j < (int)nc ? carry[b * kCG + j] : hole;
+      w += kCG;
+    }
+    for (; w < resv[b]; ++w) dst[w] = hole;
+  }
+
+  tmax = block_reduce_i64(tmax, lred, 0);
+  qmin = block_reduce_i64(qmin, lred, 1);
+  qmax = block_reduce_i64(qmax, lred, 0);
+  nacc = block_reduce_i64(nacc, lred, 2);
+  if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
+  flags = (any_ovf ? 1 : 0) | block_reduce_i64(flags & 2, lred, 0) |
+          block_reduce_i64(flags & 4, lred, 0);
+  if (threadIdx.x == 0) {
+    atomicMax((long long*)&stats[kStatMaxTs], (long long)tmax);
+    if (nacc) {
+      atomicMin((long long*)&stats[kStatMinPane], (long long)qmin);
+      atomicMax((long long*)&stats[kStatMaxPane], (long long)qmax);
+      atomicAdd((unsigned long long*)&stats[kStatAccepted], (unsigned long long)nacc);
+    }
+    if (!late_idx && nlate) atomicAdd((unsigned long long*)&stats[kStatLate], (unsigned long long)nlate);
+    if (flags) atomicOr((unsigned long long*)&stats[kStatOverflow], (unsigned long long)flags);
+  }
+}
+
 // Step prologue: zero the bucket cursors and reset the stats block (one launch instead of two
 // memsets + a host copy).
 __global__ __launch_bounds__(256) void step_begin_kernel(uint32_t* __restrict__ cursor, int nb,
@@ -589,7 +778,8 @@ __global__ void step_finish_kernel(const int64_t* __restrict__ stats, int64_t* _
   red[2] = wm;
   red[3] = -(stats[kStatOverflow] & 1);
   red[4] = -((stats[kStatOverflow] >> 1) & 1);
-  red[5] = red[6] = red[7] = 0;
+  red[5] = -((stats[kStatOverflow] >> 2) & 1);  // compact records cannot hold a value
+  red[6] = red[7] = 0;
   for (int j = 0; j < kStatCount; ++j) red[8 + j] = stats[j];
 }
 
@@ -654,9 +844,22 @@ __device__ __forceinline__ uint64_t lds_export(uint64_t a) {
 // ------------------------------------------------------------------------------------------
 constexpr int kAggU = 4;
 
-template <int AGG>
+// Record load for both layouts: RW = 3 (24-byte Rec) or 2 (16-byte RecC, int32 value).
+template <int RW>
+__device__ __forceinline__ Rec load_rec(const void* base, size_t idx) {
+  if (RW == 3) return ((const Rec*)base)[idx];
+  const uint4 c = ((const uint4*)base)[idx];
+  Rec r;
+  r.key = (uint64_t)c.x | ((uint64_t)c.y << 32);
+  r.val = (uint64_t)(int64_t)(int32_t)c.z;
+  r.t = c.w;
+  r.aux = 0;
+  return r;
+}
+
+template <int AGG, int RW>
 __global__ __launch_bounds__(1024) void window_agg_kernel(
-    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
+    const void* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
     uint64_t* __restrict__ keys_g, uint64_t* __restrict__ acc_g, uint32_t* __restrict__ cnt_g,
     uint8_t* __restrict__ dirty_g, uint32_t* __restrict__ occupancy, uint32_t* __restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -686,14 +889,14 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
     for (int src = 0; src < p.nsrc; ++src) {
       uint32_t c = counts[(size_t)src * p.nsub + sub];
       c = c < p.bucket_cap ? c : p.bucket_cap;
-      const Rec* seg = recs + ((size_t)src * p.nsub + sub) * p.bucket_cap;
+      const size_t seg0 = ((size_t)src * p.nsub + sub) * p.bucket_cap;
       // kAggU independent record loads in flight per thread before the LDS work.
       for (uint32_t e0 = threadIdx.x; e0 < c; e0 += blockDim.x * kAggU) {
         Rec rr[kAggU];
 #pragma unroll
         for (int u = 0; u < kAggU; ++u) {
           const uint32_t e = e0 + u * blockDim.x;
-          if (e < c) rr[u] = seg[e];
+          if (e < c) rr[u] = load_rec<RW>(recs, seg0 + e);
         }
 #pragma unroll
         for (int u = 0; u < kAggU; ++u) {
@@ -753,9 +956,9 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
 // moves ~#distinct (key, pane) records instead of every event (sum/min/max/count/avg are all
 // associative, so the receiver's window_agg result is unchanged).
 // ------------------------------------------------------------------------------------------
-template <int AGG>
+template <int AGG, int RW>
 __global__ __launch_bounds__(1024) void window_combine_kernel(
-    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
+    const void* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
     Rec* __restrict__ out, uint32_t ccap, uint32_t* __restrict__ out_counts,
     uint32_t* __restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -770,7 +973,7 @@ __global__ __launch_bounds__(1024) void window_combine_kernel(
   if (threadIdx.x < 2) sflag[threadIdx.x] = 0;
   uint32_t c = counts[b];
   c = c < p.bucket_cap ? c : p.bucket_cap;
-  const Rec* seg = recs + (size_t)b * p.bucket_cap;
+  const size_t seg0 = (size_t)b * p.bucket_cap;
   Rec* dst = out + (size_t)b * ccap;
   int inserted = 0;
   bool ovf = false;
@@ -787,7 +990,7 @@ __global__ __launch_bounds__(1024) void window_combine_kernel(
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
         const uint32_t e = e0 + u * blockDim.x;
-        if (e < c) rr[u] = seg[e];
+        if (e < c) rr[u] = load_rec<RW>(recs, seg0 + e);
       }
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
@@ -1986,6 +2189,24 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap,
                intptr_t stream) {
   const int nb = plan.nranks << plan.nsub_log2;
+  if (plan.rec_words == 2) {
+    if (n <= 0) return;
+    if (nb > kCMaxNb) throw std::invalid_argument("compact partition needs <= 512 buckets");
+    // 32K events per workgroup: two workgroups per CU (LDS ~72 KB each) at 16M events.
+    const int blocks = grid_for(n, 32768, 2048);
+    const int64_t chunk = (n + blocks - 1) / blocks;
+    static bool attr = false;
+    if (!attr) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)partition_compact_kernel<1>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCompactLds));
+      attr = true;
+    }
+    hipLaunchKernelGGL(partition_compact_kernel<1>, dim3(blocks), dim3(1024), kCompactLds,
+                       (hipStream_t)stream, keys, ts, vals, jhash_tab, n, chunk, plan, kg_dest,
+                       cursor, reinterpret_cast<RecC*>(out), stats, late_idx, late_cap);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   // Write-combined staged scatter when the LDS carry buffers fit (<= 512 buckets); otherwise
   // the plain scatter. Both stream their inputs with non-temporal loads (kbench A/B).
   partition_variant(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats, late_idx,
@@ -2046,8 +2267,20 @@ template <int AGG>
 static void launch_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p,
                        uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
                        uint32_t* occ, uint32_t* flags, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(window_agg_kernel<AGG>, dim3(p.nsub), dim3(1024), lds, s, recs, counts, p,
-                     keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+  static bool attr = false;
+  if (!attr) {  // allow the full 160 KiB LDS for both record layouts
+    HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 3>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 2>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  if (p.rec_words == 2)
+    hipLaunchKernelGGL((window_agg_kernel<AGG, 2>), dim3(p.nsub), dim3(1024), lds, s,
+                       (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+  else
+    hipLaunchKernelGGL((window_agg_kernel<AGG, 3>), dim3(p.nsub), dim3(1024), lds, s,
+                       (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
 }
 
 void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& plan, uint64_t* keys_g,
@@ -2057,29 +2290,14 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& plan, ui
   const size_t cap = (size_t)1 << plan.cap_log2;
   const size_t lds = cap * 8 + (size_t)plan.pg * cap * 12 + 16;
   if (lds > 160 * 1024) throw std::runtime_error("window_agg: LDS image exceeds 160 KiB");
-  static bool attr_set = false;
-  if (!attr_set) {
-    // Allow the full 160 KiB LDS for every instantiation.
-#define MXS_SET_ATTR(A)                                                                     \
-  HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<A>,                           \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    MXS_SET_ATTR(AGG_SUM_I64) MXS_SET_ATTR(AGG_SUM_F64) MXS_SET_ATTR(AGG_MIN_I64)
-    MXS_SET_ATTR(AGG_MAX_I64) MXS_SET_ATTR(AGG_MIN_F64) MXS_SET_ATTR(AGG_MAX_F64)
-    MXS_SET_ATTR(AGG_COUNT) MXS_SET_ATTR(AGG_AVG_F64) MXS_SET_ATTR(AGG_AVG_I64)
-#undef MXS_SET_ATTR
-    attr_set = true;
-  }
+  if (plan.rec_words == 2 && plan.combined)
+    throw std::invalid_argument("window_agg: combined records are 24-byte records");
   hipStream_t s = (hipStream_t)stream;
   switch (plan.agg) {
-    case AGG_SUM_I64: launch_agg<AGG_SUM_I64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
-    case AGG_SUM_F64: launch_agg<AGG_SUM_F64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
-    case AGG_MIN_I64: launch_agg<AGG_MIN_I64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
-    case AGG_MAX_I64: launch_agg<AGG_MAX_I64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
-    case AGG_MIN_F64: launch_agg<AGG_MIN_F64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
-    case AGG_MAX_F64: launch_agg<AGG_MAX_F64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
-    case AGG_COUNT: launch_agg<AGG_COUNT>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
-    case AGG_AVG_F64: launch_agg<AGG_AVG_F64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
-    case AGG_AVG_I64: launch_agg<AGG_AVG_I64>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
+#define MXS_A(A) case A: launch_agg<A>(recs, counts, plan, keys_g, acc_g, cnt_g, dirty_g, occupancy, flags, lds, s); break;
+    MXS_A(AGG_SUM_I64) MXS_A(AGG_SUM_F64) MXS_A(AGG_MIN_I64) MXS_A(AGG_MAX_I64)
+    MXS_A(AGG_MIN_F64) MXS_A(AGG_MAX_F64) MXS_A(AGG_COUNT) MXS_A(AGG_AVG_F64) MXS_A(AGG_AVG_I64)
+#undef MXS_A
     default: throw std::runtime_error("window_agg: unknown aggregate");
   }
   HIP_CHECK(hipGetLastError());
@@ -2309,8 +2527,20 @@ template <int AGG>
 static void launch_combine(const Rec* recs, const uint32_t* counts, int nbuckets,
                            const AggPlan& p, Rec* out, uint32_t ccap, uint32_t* out_counts,
                            uint32_t* flags, size_t lds, hipStream_t s) {
-  hipLaunchKernelGGL(window_combine_kernel<AGG>, dim3(nbuckets), dim3(1024), lds, s, recs, counts,
-                     p, out, ccap, out_counts, flags);
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)window_combine_kernel<AGG, 3>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_CHECK(hipFuncSetAttribute((const void*)window_combine_kernel<AGG, 2>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  if (p.rec_words == 2)
+    hipLaunchKernelGGL((window_combine_kernel<AGG, 2>), dim3(nbuckets), dim3(1024), lds, s,
+                       (const void*)recs, counts, p, out, ccap, out_counts, flags);
+  else
+    hipLaunchKernelGGL((window_combine_kernel<AGG, 3>), dim3(nbuckets), dim3(1024), lds, s,
+                       (const void*)recs, counts, p, out, ccap, out_counts, flags);
 }
 
 void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const AggPlan& p,
@@ -2320,17 +2550,6 @@ void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const
   const size_t cap = (size_t)1 << p.cap_log2;
   const size_t lds = cap * 8 + (size_t)p.pg * cap * 12 + 16;
   if (lds > 160 * 1024) throw std::invalid_argument("window_combine: LDS image exceeds 160 KiB");
-  static bool attr_set = false;
-  if (!attr_set) {
-#define MXS_SET_ATTR(A)                                                                     \
-  HIP_CHECK(hipFuncSetAttribute((const void*)window_combine_kernel<A>,                       \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    MXS_SET_ATTR(AGG_SUM_I64) MXS_SET_ATTR(AGG_SUM_F64) MXS_SET_ATTR(AGG_MIN_I64)
-    MXS_SET_ATTR(AGG_MAX_I64) MXS_SET_ATTR(AGG_MIN_F64) MXS_SET_ATTR(AGG_MAX_F64)
-    MXS_SET_ATTR(AGG_COUNT) MXS_SET_ATTR(AGG_AVG_F64) MXS_SET_ATTR(AGG_AVG_I64)
-#undef MXS_SET_ATTR
-    attr_set = true;
-  }
   hipStream_t s = (hipStream_t)stream;
   switch (p.agg) {
 #define MXS_C(A) case A: launch_combine<A>(recs, counts, nbuckets, p, out, ccap, out_counts, flags, lds, s); break;

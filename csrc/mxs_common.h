@@ -41,6 +41,15 @@ struct alignas(8) Rec {
 };
 static_assert(sizeof(Rec) == 24, "Rec must be 24 bytes");
 
+// Compact 16-byte record (window path with integer aggregates whose values fit int32): one
+// 16-byte vector per record, 4 records per 64-byte sector.
+struct alignas(16) RecC {
+  uint64_t key;
+  uint32_t val;  // int32 value (sign-extended on load)
+  uint32_t t;    // relative pane; 0xFFFFFFFF = hole
+};
+static_assert(sizeof(RecC) == 16, "RecC must be 16 bytes");
+
 // ---------------------------------------------------------------------------------------------
 // Java / Flink hashing
 // ---------------------------------------------------------------------------------------------
@@ -348,6 +357,7 @@ struct PartPlan {
   int64_t tbase;             // pane_start(pane_base): records carry floor((ts - tbase) / pane)
   int64_t pane;              // pane length (ms)
   double inv_pane;           // 1.0 / pane
+  int32_t rec_words;         // 3: 24-byte Rec; 2: 16-byte RecC (int32 values, GPU window path)
 };
 
 MXS_HD uint32_t bucket_of(uint64_t key, int32_t jhash, const PartPlan& p, const int32_t* kg_dest) {

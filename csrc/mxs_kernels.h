@@ -26,6 +26,7 @@ struct AggPlan {
   int64_t p_lo;         // first pane (relative to pane_base) touched this step
   int64_t fired_hi;     // absolute pane id: panes <= fired_hi are in an already-fired window
   int32_t combined;     // records are pre-aggregated (aux = element count, val = exported acc)
+  int32_t rec_words;    // 3: Rec (24 B); 2: RecC (16 B)
 };
 
 // Plan of one window firing.

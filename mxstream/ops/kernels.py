@@ -97,6 +97,7 @@ class PartitionPlan:
     tbase: int = 0           # start of the step's base pane
     pane: int = 1            # pane length (ms)
     ablate: int = 0          # profiling-only ablation bits
+    rec_words: int = 3       # 3: 24-byte records; 2: 16-byte records (int32 values, window path)
 
     @property
     def nbuckets(self) -> int:
@@ -152,6 +153,7 @@ class AggPlan:
     p_lo: int
     fired_hi: int
     combined: int = 0    # records are pre-aggregated by window_combine (aux = element count)
+    rec_words: int = 3   # layout of the input records (3: Rec, 2: RecC)
 
     def as_dict(self) -> dict:
         return dict(self.__dict__)

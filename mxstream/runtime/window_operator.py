@@ -90,7 +90,7 @@ class KeyedWindowOperator:
                  cap_log2: int | None = None, time_mode: str = "event", ooo_bound: int = 0,
                  side_output_late: bool = False, late_capacity: int = 1 << 16,
                  clock: Callable[[], int] | None = None, external_watermark: bool = False,
-                 combine: bool | None = None):
+                 combine: bool | None = None, compact: bool | None = None):
         self.device = torch.device(device)
         self.comm = comm or LocalComm()
         self.world = self.comm.world
@@ -159,6 +159,12 @@ class KeyedWindowOperator:
         self.comb_send = self.comb_recv = None
         self.comb_counts = torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
         self._ccap_hint = 1 << self.cap_log2
+        # 16-byte records (int32 values) for integer aggregates on the GPU staged path; a value
+        # outside int32 switches the operator to 24-byte records for good (step redone).
+        int_agg = agg in (K.AGG_SUM_I64, K.AGG_MIN_I64, K.AGG_MAX_I64, K.AGG_COUNT, K.AGG_AVG_I64)
+        if compact is None:
+            compact = self.device.type == "cuda" and int_agg and self.nbuckets <= 512
+        self.compact = bool(compact and int_agg and self.nbuckets <= 512)
         self.timer = None  # utils.metrics.StageTimer: per-stage step_ms histograms when attached
 
         # ---- watermark / firing bookkeeping (host, identical on every rank) ----
@@ -206,7 +212,8 @@ class KeyedWindowOperator:
             self.flags[1:2].zero_()
             cplan = K.AggPlan(cap_log2=self.cap_log2, nsub=nb, ring=self.ring, agg=self.agg,
                               nsrc=1, bucket_cap=self.bucket_cap, np_step=np_step, pg=pg,
-                              pane_base=0, p_lo=p_lo, fired_hi=0)
+                              pane_base=0, p_lo=p_lo, fired_hi=0,
+                              rec_words=2 if self.compact else 3)
             K.window_combine(self.send, self.cursor, cplan, self.comb_send, ccap,
                              self.comb_counts, self.flags[1:2])
             # One small sync: overflow flag (global, so every rank retries together) + max fill.
@@ -307,7 +314,8 @@ class KeyedWindowOperator:
                 max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2, nranks=self.world,
                 window_mode=1, drop_late=int(event_mode), hash_mode=self.hash_mode,
                 bucket_cap=self.bucket_cap, late_ts=self._late_ts(old_wm),
-                tbase=self.pane_start(pane_base), pane=self.pane)
+                tbase=self.pane_start(pane_base), pane=self.pane,
+                rec_words=2 if self.compact else 3)
             with self._stage("partition"):
                 if n:
                     K.partition(keys, ts, vals, plan, self.kg_dest, self.cursor, self.send,
@@ -324,6 +332,11 @@ class KeyedWindowOperator:
             if host[4]:
                 raise RuntimeError("event timestamp outside the representable pane range "
                                    "(more than 2^32 panes ahead of the watermark)")
+            if host[5]:
+                # A value does not fit the 16-byte record: 24-byte records from now on.
+                self.compact = False
+                self.metrics.extra["compact_fallbacks"] = self.metrics.extra.get("compact_fallbacks", 0) + 1
+                continue
             if host[3]:
                 # A bucket overflowed somewhere: grow the fixed bucket capacity and redo the step.
                 self.metrics.bucket_regrows += 1
@@ -370,7 +383,8 @@ class KeyedWindowOperator:
             aplan = K.AggPlan(cap_log2=self.cap_log2, nsub=self.nsub, ring=self.ring, agg=self.agg,
                               nsrc=self.world, bucket_cap=bcap,
                               np_step=gmax - gmin + 1, pg=pg, pane_base=pane_base,
-                              p_lo=qmin, fired_hi=fired_hi, combined=combined)
+                              p_lo=qmin, fired_hi=fired_hi, combined=combined,
+                              rec_words=3 if combined else (2 if self.compact else 3))
             with self._stage("window_agg"):
                 K.window_agg(recs, counts, aplan, self.keys_g, self.acc_g, self.cnt_g,
                              self.dirty_g, self.occ, self.flags)

@@ -243,3 +243,29 @@ def test_segment_median_vs_numpy(gpu_device):
             continue
         exp = v[len(v) // 2] if len(v) % 2 else (v[len(v) // 2] + v[len(v) // 2 - 1]) / 2
         assert got[k] == exp
+
+
+def test_compact_partition_matches_cpu(gpu_device):
+    """16-byte record partition (keys-only histogram pass, hole-filled reservations) vs the C++
+    twin, including late records (their reserved slots become holes)."""
+    n = 300_000
+    outs = {}
+    for dev in (gpu_device, "cpu"):
+        keys, ts, vals = _gen(dev, n, 40_000, span=6000, disorder=2000)
+        plan = K.PartitionPlan(max_parallelism=128, nsub_log2=7, nranks=2, window_mode=1,
+                               drop_late=1, hash_mode=0, bucket_cap=4096, late_ts=2500,
+                               tbase=1000, pane=500, rec_words=2)
+        kg = torch.tensor([(k * 2) // 128 for k in range(128)], dtype=torch.int32, device=dev)
+        cursor = torch.zeros(plan.nbuckets, dtype=torch.int32, device=dev)
+        out = torch.zeros(plan.nbuckets * plan.bucket_cap * 3, dtype=torch.int64, device=dev)
+        stats = K.new_stats(dev)
+        K.partition(keys, ts, vals, plan, kg, cursor, out, stats)
+        outs[str(dev)] = (cursor.cpu(), out.cpu()[: plan.nbuckets * plan.bucket_cap * 2]
+                          .view(plan.nbuckets, plan.bucket_cap, 2), stats.cpu())
+    (cg, og, sg), (cc, oc, sc) = outs[str(gpu_device)], outs["cpu"]
+    assert torch.equal(sg, sc) and int(sg[K.STAT_LATE]) > 0 and int(sg[K.STAT_OVERFLOW]) == 0
+    for b in range(cg.numel()):
+        a = og[b, :int(cg[b])].numpy()
+        a = a[(a[:, 1] >> 32) != -1]  # drop holes (t = 0xFFFFFFFF)
+        e = oc[b, :int(cc[b])].numpy()
+        assert np.array_equal(a[np.lexsort(a.T[::-1])], e[np.lexsort(e.T[::-1])])

@@ -121,3 +121,36 @@ def test_ring_growth_on_event_time_jump():
     assert got[((0, 100), 1)][:2] == (1, 1)
     assert got[((10_000_000, 10_000_100), 1)][:2] == (5, 1)
     assert got[((10_000_000, 10_000_100), 2)][:2] == (7, 1)
+
+
+@pytest.mark.parametrize("agg", [K.AGG_SUM_I64, K.AGG_MAX_I64, K.AGG_COUNT, K.AGG_AVG_I64])
+def test_compact_records_equal_wide(agg):
+    """16-byte records (int32 values) give the same windows as 24-byte records; a value outside
+    int32 switches the operator to 24-byte records and redoes the step."""
+    rng = np.random.default_rng(2)
+    res = {}
+    for compact in (False, True):
+        op = KeyedWindowOperator(size=2000, slide=1000, lateness=500, agg=agg, device="cpu",
+                                 max_keys=4096, batch_capacity=4096, cap_log2=8, ooo_bound=300,
+                                 compact=compact)
+        out = []
+        for step in range(6):
+            k = torch.from_numpy(rng.integers(0, 500, 2000) if compact else
+                                 np.random.default_rng(10 + step).integers(0, 500, 2000))
+            t = torch.from_numpy(np.random.default_rng(20 + step).integers(step * 900,
+                                                                          step * 900 + 1500, 2000))
+            v = torch.from_numpy(np.random.default_rng(30 + step).integers(-5000, 5000, 2000))
+            k = torch.from_numpy(np.random.default_rng(10 + step).integers(0, 500, 2000))
+            out += op.process(k, t, v)
+        out += op.finish()
+        res[compact] = sorted((r.window_start, int(kk), int(a), int(c), r.refire)
+                              for r in out for kk, a, c in zip(r.keys, r.raw, r.counts))
+        assert op.compact == compact
+    assert res[True] == res[False]
+    op = KeyedWindowOperator(size=2000, agg=K.AGG_SUM_I64, device="cpu", max_keys=64,
+                             batch_capacity=64, cap_log2=6, compact=True)
+    op.process(torch.tensor([1, 2]), torch.tensor([10, 20]), torch.tensor([5, 1 << 40]))
+    assert op.compact is False and op.metrics.extra["compact_fallbacks"] == 1
+    fired = op.finish()
+    got = {int(k): int(a) for r in fired for k, a in zip(r.keys, r.raw)}
+    assert got == {1: 5, 2: 1 << 40}
