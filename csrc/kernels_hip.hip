@@ -559,22 +559,24 @@ constexpr size_t kStagedLds = (size_t)kStageMaxNb * 8 * sizeof(Rec) + (size_t)kS
 static_assert(kStagedLds <= 160 * 1024, "staged partition LDS image exceeds 160 KiB");
 
 // ------------------------------------------------------------------------------------------
-// Compact staged partition (16-byte RecC, integer window aggregates). Same structure as the
-// staged kernel with three differences that the counters pointed at (profiles/r1_bench_pmc.md):
+// Compact staged partition (16-byte RecC, integer window aggregates). Differences from the
+// 24-byte staged kernel, each measured (profiles/README.md):
 //  * pass A reads only the keys (the bucket is a function of the key); late / unrepresentable
-//    records are counted into the reservation and their slots filled with holes at the end,
-//    so pass B alone reads ts/val (32 B of input per event instead of 40 B);
-//  * a record is one 16-byte vector: a write group is 4 records = one 64-byte sector, the LDS
-//    image halves (~72 KB) and two workgroups fit per CU (twice the waves to hide latency);
-//  * records move LDS -> HBM as uint4 copies (no 24-byte splicing).
+//    records are counted into the reservation and their slots filled with holes at the end, so
+//    pass B alone reads ts/val (32 B of input per event instead of 40 B);
+//  * a record is one 16-byte vector; the LDS image (~42 KB) lets two workgroups share a CU;
+//  * cooperative flush: after the per-round LDS counting sort every thread writes one sorted
+//    record to its bucket run (runs are contiguous, so a wave's stores coalesce and the partial
+//    sectors at run ends are completed by the next round while still in L2). This beat the
+//    carry/whole-group flush of the 24-byte kernel by ~3 % end to end.
 // A value outside int32 sets stats overflow bit 2: the host redoes the step with 24-byte records.
 // ------------------------------------------------------------------------------------------
 constexpr int kCU = 2;                   // events per thread per round
 constexpr int kCR = 1024 * kCU;          // records per round
-constexpr int kCG = 4;                   // records per write group (64 B)
+constexpr int kCG = 4;                   // reservation granularity (records per 64-byte sector)
 constexpr int kCMaxNb = 512;
-constexpr size_t kCompactLds = (size_t)kCMaxNb * kCG * sizeof(RecC) + (size_t)kCR * sizeof(RecC) +
-                               (size_t)kCMaxNb * 5 * 4 + 20 * 4 + 16 * 8;
+constexpr size_t kCompactLds = (size_t)kCR * sizeof(RecC) + (size_t)kCMaxNb * 5 * 4 + 20 * 4 +
+                               16 * 8 + (size_t)kCR * 2;
 static_assert(kCompactLds <= 80 * 1024, "compact partition must fit two workgroups per CU");
 
 template <int V>
@@ -586,15 +588,15 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
     uint32_t* __restrict__ late_idx, uint32_t late_cap) {
   extern __shared__ __attribute__((aligned(16))) unsigned char csm[];
   const int nb = plan.nranks << plan.nsub_log2;
-  uint4* carry = (uint4*)csm;                                  // [kCMaxNb][kCG]
-  uint4* rbuf = carry + kCMaxNb * kCG;                         // [kCR]
+  uint4* rbuf = (uint4*)csm;                                   // [kCR] sorted round
   uint32_t* run_base = (uint32_t*)(rbuf + kCR);                // [kCMaxNb]
   uint32_t* resv = run_base + kCMaxNb;                         // reserved records per bucket
-  uint32_t* lcnt = resv + kCMaxNb;                             // records appended per bucket
+  uint32_t* lcnt = resv + kCMaxNb;                             // records written per bucket
   uint32_t* rcnt = lcnt + kCMaxNb;                             // this round's count per bucket
   uint32_t* roff = rcnt + kCMaxNb;                             // this round's offsets
   uint32_t* wsum = roff + kCMaxNb;                             // 17 scan words (+pad)
   int64_t* lred = (int64_t*)(wsum + 20);                       // 16 x i64
+  uint16_t* sbk = (uint16_t*)(lred + 16);                      // [kCR] bucket of rbuf[j]
 
   for (int b = threadIdx.x; b < kCMaxNb; b += blockDim.x) {
     run_base[b] = 0;
@@ -642,7 +644,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
 
   int64_t tmax = INT64_MIN, qmin = INT64_MAX, qmax = INT64_MIN, nlate = 0, nacc = 0;
   int64_t flags = 0;
-  // Pass B: rounds of kCR records -> LDS sort by bucket -> whole 64-byte groups.
+  // Pass B: rounds of kCR records -> LDS counting sort by bucket -> cooperative run writes.
   for (int64_t r0 = start; r0 < end; r0 += kCR) {
     uint32_t bk[kCU], rk[kCU];
     uint4 rec[kCU];
@@ -684,48 +686,34 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < kCU; ++u)
-      if (keep[u]) rbuf[roff[bk[u]] + rk[u]] = rec[u];
+      if (keep[u]) {
+        const uint32_t j = roff[bk[u]] + rk[u];
+        rbuf[j] = rec[u];
+        sbk[j] = (uint16_t)bk[u];
+      }
     __syncthreads();
-    if (threadIdx.x < (unsigned)nb && !any_ovf) {
-      const int b = threadIdx.x;
-      const uint32_t nc = lcnt[b] & (kCG - 1);
-      const uint32_t nr = rcnt[b];
-      const uint32_t tot = nc + nr;
-      const uint32_t groups = tot / kCG;
-      uint4* dstb = (uint4*)(out + (size_t)b * bcap + run_base[b] + (lcnt[b] - nc));
-      const uint4* src_r = rbuf + roff[b];
-      for (uint32_t g = 0; g < groups; ++g) {
-#pragma unroll
-        for (int q = 0; q < kCG; ++q) {
-          const uint32_t j = g * kCG + q;
-          dstb[j] = j < nc ? carry[b * kCG + j] : src_r[j - nc];
-        }
+    const uint32_t nrec = wsum[16];
+    if (!any_ovf) {
+      for (uint32_t j = threadIdx.x; j < nrec; j += blockDim.x) {
+        const uint32_t b = sbk[j];
+        const uint32_t pos = lcnt[b] + (j - roff[b]);
+        ((uint4*)(out + (size_t)b * bcap + run_base[b]))[pos] = rbuf[j];
       }
-      const uint32_t rem = tot - groups * kCG;
-      for (uint32_t j = 0; j < rem; ++j) {
-        const uint32_t jj = groups * kCG + j;
-        if (jj < nc) continue;  // no group written: the carried record is already in place
-        carry[b * kCG + j] = src_r[jj - nc];
-      }
-      lcnt[b] += nr;
-      rcnt[b] = 0;
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)nb) {
+      lcnt[threadIdx.x] += rcnt[threadIdx.x];
+      rcnt[threadIdx.x] = 0;
     }
     __syncthreads();
   }
-  // Tail: pad the last partial group and fill the rest of the reservation (slots reserved for
-  // late / dropped records) with holes, whole groups at a time.
+  // Tail: holes in the reserved slots that no record filled (padding to a whole sector, and the
+  // slots counted for late / dropped records in pass A).
   if (threadIdx.x < (unsigned)nb && !any_ovf) {
     const int b = threadIdx.x;
-    const uint32_t nc = lcnt[b] & (kCG - 1);
     uint4* dst = (uint4*)(out + (size_t)b * bcap + run_base[b]);
     const uint4 hole = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, kHoleT);
-    uint32_t w = lcnt[b] - nc;
-    if (nc) {
-#pragma unroll
-      for (int j = 0; j < kCG; ++j) dst[w + j] = j < (int)nc ? carry[b * kCG + j] : hole;
-      w += kCG;
-    }
-    for (; w < resv[b]; ++w) dst[w] = hole;
+    for (uint32_t w = lcnt[b]; w < resv[b]; ++w) dst[w] = hole;
   }
 
   tmax = block_reduce_i64(tmax, lred, 0);
@@ -2195,12 +2183,6 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
     // 32K events per workgroup: two workgroups per CU (LDS ~72 KB each) at 16M events.
     const int blocks = grid_for(n, 32768, 2048);
     const int64_t chunk = (n + blocks - 1) / blocks;
-    static bool attr = false;
-    if (!attr) {
-      HIP_CHECK(hipFuncSetAttribute((const void*)partition_compact_kernel<1>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)kCompactLds));
-      attr = true;
-    }
     hipLaunchKernelGGL(partition_compact_kernel<1>, dim3(blocks), dim3(1024), kCompactLds,
                        (hipStream_t)stream, keys, ts, vals, jhash_tab, n, chunk, plan, kg_dest,
                        cursor, reinterpret_cast<RecC*>(out), stats, late_idx, late_cap);
