@@ -235,6 +235,7 @@ __global__ __launch_bounds__(1024) void partition_kernel(
   }
   __syncthreads();
 
+  bool wide = false;  // a value does not fit a 16-byte record
   // Pass B: scatter records into their bucket runs.
   const uint32_t bcap = plan.bucket_cap;
   for (int64_t i0 = start + threadIdx.x; i0 < end; i0 += bstep) {
@@ -256,7 +257,12 @@ __global__ __launch_bounds__(1024) void partition_kernel(
       const PartEval e = part_eval(k[u], t[u], jhash_tab, plan, kg_dest);
       if (e.kind) continue;
       const uint32_t pos = atomicAdd(&lhist[e.bucket], 1u);
-      if (pos < bcap && !(plan.ablate & 1u)) {
+      if (pos < bcap && !(plan.ablate & 1u) && plan.rec_words == 2) {
+        // 16-byte record: one vector store (int32 value; wider values flag bit 2).
+        if ((int64_t)(int32_t)v[u] != (int64_t)v[u]) wide = true;
+        ((uint4*)out)[(size_t)e.bucket * bcap + pos] =
+            make_uint4((uint32_t)k[u], (uint32_t)(k[u] >> 32), (uint32_t)v[u], e.t);
+      } else if (pos < bcap && !(plan.ablate & 1u)) {
         Rec* dst = &out[(size_t)e.bucket * bcap + pos];
         if (V & 2) {
           __builtin_nontemporal_store(k[u], &dst->key);
@@ -281,7 +287,8 @@ __global__ __launch_bounds__(1024) void partition_kernel(
   nacc = block_reduce_i64(nacc, lred, 2);
   if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
   const int64_t flags = block_reduce_i64(overflow ? 1 : 0, lred, 0) |
-                        (block_reduce_i64(bad ? 2 : 0, lred, 0));
+                        block_reduce_i64(bad ? 2 : 0, lred, 0) |
+                        block_reduce_i64(wide ? 4 : 0, lred, 0);
   if (threadIdx.x == 0) {
     atomicMax((long long*)&stats[kStatMaxTs], (long long)tmax);
     if (nacc) {
@@ -2177,9 +2184,8 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap,
                intptr_t stream) {
   const int nb = plan.nranks << plan.nsub_log2;
-  if (plan.rec_words == 2) {
+  if (plan.rec_words == 2 && nb <= kCMaxNb) {
     if (n <= 0) return;
-    if (nb > kCMaxNb) throw std::invalid_argument("compact partition needs <= 512 buckets");
     // 32K events per workgroup: two workgroups per CU (LDS ~72 KB each) at 16M events.
     const int blocks = grid_for(n, 32768, 2048);
     const int64_t chunk = (n + blocks - 1) / blocks;

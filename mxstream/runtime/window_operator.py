@@ -163,8 +163,8 @@ class KeyedWindowOperator:
         # outside int32 switches the operator to 24-byte records for good (step redone).
         int_agg = agg in (K.AGG_SUM_I64, K.AGG_MIN_I64, K.AGG_MAX_I64, K.AGG_COUNT, K.AGG_AVG_I64)
         if compact is None:
-            compact = self.device.type == "cuda" and int_agg and self.nbuckets <= 512
-        self.compact = bool(compact and int_agg and self.nbuckets <= 512)
+            compact = self.device.type == "cuda" and int_agg
+        self.compact = bool(compact and int_agg)
         self.timer = None  # utils.metrics.StageTimer: per-stage step_ms histograms when attached
 
         # ---- watermark / firing bookkeeping (host, identical on every rank) ----
