@@ -24,8 +24,9 @@ BUILD = ROOT / "build" / "native"
 PKG = ROOT / "mxstream"
 ARCH = os.environ.get("MXS_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["kernels_hip.hip", "sort_hip.hip", "parse_hip.hip"]
-CXX_SOURCES = ["kernels_cpu.cpp", "runtime.cpp", "sessions.cpp", "bindings.cpp"]
+HIP_SOURCES = ["kernels_hip.hip", "sort_hip.hip", "parse_hip.hip", "vector_hip.hip"]
+CXX_SOURCES = ["kernels_cpu.cpp", "runtime.cpp", "sessions.cpp", "vector_cpu.cpp",
+               "vector_bindings.cpp", "bindings.cpp"]
 
 
 def _ext_suffix() -> str:

@@ -4,6 +4,7 @@
   python -m mxstream.models.bench_configs --config 2   # keyed ValueState counter, 10k keys, 1 GPU
   python -m mxstream.models.bench_configs --config 4   # sliding 1 min / 10 s + lateness, 10M keys
   python -m mxstream.models.bench_configs --config 5   # session alert + host-DRAM spill
+  python -m mxstream.models.bench_configs --config 6   # vector-metric window avg (MFMA reduce)
 
 Each prints one JSON line: events/s and the step time (and p50 alert latency where alerts fire).
 Config 1 runs the reference's exact text path: Java-semantics split + Double.parseDouble in the
@@ -14,6 +15,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import statistics
 import time
 
@@ -225,9 +227,70 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
                                        for k, v in sorted(op.phase_s.items())}}
 
 
+def config6(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 1_000_000,
+            dim: int = 32, device: str = "cuda", mfma: bool = True) -> dict:
+    """Vector-metric window: 1-min tumbling event-time AVERAGE of a D-float metric vector per
+    host (per-core CPU usage; ComputeCpuAvg.java:27-59 with the scalar generalised to a vector),
+    1M keys, alert when any core's window average exceeds a threshold. The per-(key, pane)
+    vector sums run on the MFMA segmented-sum kernel (mfma=False: the VALU variant)."""
+    from ..ops import vector as V
+    from ..runtime.vector_window_operator import VectorWindowOperator
+
+    dev = torch.device("cuda", 0) if device != "cpu" and torch.cuda.is_available() \
+        else torch.device("cpu")
+    step_ms, disorder = 5_000, 2_000
+    # Alert when some core's 1-min average usage is 4.4 sigma above the mean (U[0, 100) usage,
+    # ~events_per_window samples per key): ~0.1 % of the (key, window) pairs.
+    per_window = batch * (60_000 / step_ms) / keys
+    thr = 50.0 + 4.4 * (100.0 / math.sqrt(12.0)) / math.sqrt(max(per_window, 1.0))
+    op = VectorWindowOperator(dim=dim, size=60_000, device=dev, max_keys=keys,
+                              batch_capacity=batch, ooo_bound=disorder, avg=True,
+                              threshold=thr, mfma=mfma)
+    k = torch.empty(batch, dtype=torch.int64, device=dev)
+    ts = torch.empty_like(k)
+    vals = torch.empty_like(k)
+    vec = torch.empty(batch, dim, dtype=torch.float32, device=dev)
+    t0_event = 1_566_957_600_000
+    state = {"i": 0}
+    lat: list[float] = []
+
+    def step():
+        i = state["i"]
+        t_in = time.perf_counter()
+        K.gen_events(k, ts, vals, seed=11, stream_id=0, idx0=i * batch, nkeys=keys,
+                     ts_base=t0_event + i * step_ms, ts_span=step_ms, disorder=disorder,
+                     val_lo=0, val_span=1)
+        V.gen_vectors(vec, seed=11, stream_id=0, idx0=i * batch, lo=0.0, span=100.0)
+        fired = op.process(k, ts, vec)
+        n = sum(len(r.keys) for r in fired)
+        if fired:
+            lat.append((time.perf_counter() - t_in) * 1e3)
+        state["i"] = i + 1
+        return n
+
+    for _ in range(warmup):
+        step()
+    _sync(dev)
+    lat.clear()
+    t0 = time.perf_counter()
+    alerts = 0
+    for _ in range(steps):
+        alerts += step()
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    return {"config": 6, "metric": "events/sec (vector-metric tumbling window avg, MFMA reduce)",
+            "value": batch * steps / dt, "unit": "events/s", "ms_per_step": dt / steps * 1e3,
+            "metric_values_per_sec": batch * steps * dim / dt,
+            "p50_alert_latency_ms": statistics.median(lat) if lat else None, "alerts": alerts,
+            "keys": keys, "dim": dim, "events_per_step": batch, "mode": "mfma" if mfma else "valu",
+            "state_bytes": op.state_bytes(), "device": str(dev)}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 4, 5])
+    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 4, 5, 6])
+    ap.add_argument("--dim", type=int, default=32, help="config 6: metric vector width")
+    ap.add_argument("--valu", action="store_true", help="config 6: VALU instead of MFMA reduce")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None)
@@ -241,6 +304,9 @@ def main(argv=None) -> int:
         r = config2(a.steps, a.warmup, a.batch or (1 << 24), device=a.device)
     elif a.config == 4:
         r = config4(a.steps, a.warmup, a.batch or (1 << 24), device=a.device)
+    elif a.config == 6:
+        r = config6(a.steps, a.warmup, a.batch or (1 << 24), dim=a.dim, device=a.device,
+                    mfma=not a.valu)
     else:
         r = config5(a.steps, a.warmup, a.batch or (1 << 24), device=a.device)
     print(json.dumps(r), flush=True)

@@ -80,6 +80,8 @@ class OperatorMetrics:
 class KeyedWindowOperator:
     """Per-rank keyed tumbling/sliding window aggregation on GPU (or the CPU twin)."""
 
+    _geometry = None  # subclasses: (max_keys, cap_log2) -> (nsub, cap_log2)
+
     def __init__(self, *, size: int, slide: int | None = None, offset: int = 0,
                  lateness: int = 0, agg: int = K.AGG_SUM_I64, device="cpu",
                  comm: Comm | None = None, max_keys: int = 1 << 20,
@@ -121,7 +123,8 @@ class KeyedWindowOperator:
         # ---- state geometry ----
         from .geometry import state_geometry
 
-        self.nsub, self.cap_log2 = state_geometry(max_keys, self.world, cap_log2)
+        self.nsub, self.cap_log2 = (self._geometry(max_keys, cap_log2) if self._geometry
+                                    else state_geometry(max_keys, self.world, cap_log2))
         cap_log2 = self.cap_log2
         self.nsub_log2 = self.nsub.bit_length() - 1
         if self.nsub * self.world > 16384:
@@ -326,8 +329,7 @@ class KeyedWindowOperator:
             self.comm.allreduce_min_(self.red[:5])
             if self.world > 1 and not self.combine:
                 with self._stage("all_to_all"):
-                    self.comm.all_to_all(self.recv, self.send)
-                    self.comm.all_to_all(self.recv_counts, self.cursor)
+                    self._exchange()
             host = self.red.cpu().tolist()  # the step's single host sync
             if host[4]:
                 raise RuntimeError("event timestamp outside the representable pane range "
@@ -386,8 +388,7 @@ class KeyedWindowOperator:
                               p_lo=qmin, fired_hi=fired_hi, combined=combined,
                               rec_words=3 if combined else (2 if self.compact else 3))
             with self._stage("window_agg"):
-                K.window_agg(recs, counts, aplan, self.keys_g, self.acc_g, self.cnt_g,
-                             self.dirty_g, self.occ, self.flags)
+                self._aggregate(recs, counts, aplan)
             # Late-but-allowed data: re-fire already-passed windows that are not cleaned yet.
             if gmin <= fired_hi:
                 out.extend(self._refire(gmin, min(gmax, fired_hi), old_wm))
@@ -403,6 +404,22 @@ class KeyedWindowOperator:
         if self.timer is not None:
             self.timer.flush()
         return out
+
+    # ---- hooks (overridden by the vector-metric operator) ---------------------------------
+    def _exchange(self) -> None:
+        """G > 1 without the combiner: the equal-split all-to-all of the bucket ranges."""
+        self.comm.all_to_all(self.recv, self.send)
+        self.comm.all_to_all(self.recv_counts, self.cursor)
+
+    def _aggregate(self, recs, counts, aplan: K.AggPlan) -> None:
+        K.window_agg(recs, counts, aplan, self.keys_g, self.acc_g, self.cnt_g, self.dirty_g,
+                     self.occ, self.flags)
+
+    def _zero_pane(self, so: int) -> None:
+        """Reset the pane slab starting at slot index `so` (pane-major state)."""
+        self.acc_g[so:so + self.nslots].zero_()
+        self.cnt_g[so:so + self.nslots].zero_()
+        self.dirty_g[so:so + self.nslots].zero_()
 
     def _stage(self, name: str):
         import contextlib
@@ -517,10 +534,7 @@ class KeyedWindowOperator:
         if stop - p > self.ring:
             p = stop - self.ring
         while p < stop:
-            so = (p & (self.ring - 1)) * self.nslots
-            self.acc_g[so:so + self.nslots].zero_()
-            self.cnt_g[so:so + self.nslots].zero_()
-            self.dirty_g[so:so + self.nslots].zero_()
+            self._zero_pane((p & (self.ring - 1)) * self.nslots)
             p += 1
         if keep_from > self.min_live_pane:
             self.min_live_pane = keep_from

@@ -7,7 +7,7 @@ ROOT=$(pwd)
 mkdir -p gpurun_out
 STEPS=${STEPS:-24}
 BATCH=${BATCH:-16777216}
-python -m mxstream.build > gpurun_out/build.log 2>&1 &&
+test -f mxstream/_mxs_native*.so &&
 timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 &&
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
 timeout -k 10 300 python bench.py --steps $STEPS --warmup 6 --batch $BATCH > gpurun_out/bench.log 2>&1 &&
