@@ -415,6 +415,7 @@ __global__ __launch_bounds__(kVFThreads) void vec_window_fire_kernel(
       if (ok && p.use_thr) ok = vf_result(p, acc_g, cnt_g, s0 + j, cnt, r, res) > p.thr;
       if (r == 0) live[j] = ok ? 1u : 0u;
     }
+    __syncthreads();
     // Block exclusive scan of the 256 flags (one per thread) + one cursor atomic.
     const uint32_t f = live[threadIdx.x];
     uint32_t x = f;
