@@ -107,3 +107,48 @@ class MaxAggregate(MinAggregate):
         if b is None:
             return a
         return a if a >= b else b
+
+
+class VectorSumAggregate(BuiltinAggregate):
+    """Element-wise sum of a metric-vector field (list/tuple of floats, e.g. one usage value
+    per CPU core). Host path: a list accumulator; native path: the MFMA vector-window kernel
+    (runtime/vector_window_operator.py). The result is a list of floats."""
+
+    kind = "vsum"
+
+    def __init__(self, field: int):
+        self.field = field
+        self.native = (self.kind, field)
+
+    def create_accumulator(self):
+        return (0, None)
+
+    def add(self, value, acc):
+        x = [float(v) for v in value[self.field]]
+        n, s = acc
+        if s is None:
+            return (n + 1, x)
+        if len(x) != len(s):
+            raise ValueError("metric vectors of one key must have the same length")
+        return (n + 1, [a + b for a, b in zip(s, x)])
+
+    def get_result(self, acc):
+        return [] if acc[1] is None else list(acc[1])
+
+    def merge(self, a, b):
+        if a[1] is None:
+            return b
+        if b[1] is None:
+            return a
+        return (a[0] + b[0], [x + y for x, y in zip(a[1], b[1])])
+
+
+class VectorAvgAggregate(VectorSumAggregate):
+    """Element-wise average of a metric-vector field (ComputeCpuAvg.java:31-58 per vector
+    component: accumulator (count, sums), result sums / count)."""
+
+    kind = "vavg"
+
+    def get_result(self, acc):
+        n, s = acc
+        return [] if s is None else [v / n for v in s]

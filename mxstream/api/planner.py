@@ -195,7 +195,13 @@ def _install_native(env, t, ws, spec, key_pos, val_pos, kind, result, ok_arities
 
     from ..runtime.native_ops import NativeMedianOp
 
-    cls = NativeSessionOp if session else (NativeMedianOp if kind == "median" else NativeWindowOp)
+    from ..runtime.native_ops import NativeVectorWindowOp
+
+    if session and kind in ("vsum", "vavg"):
+        return  # merging windows over vectors: exact host operator
+    cls = NativeSessionOp if session else (
+        NativeMedianOp if kind == "median" else
+        NativeVectorWindowOp if kind in ("vsum", "vavg") else NativeWindowOp)
 
     def factory():
         return cls(key_fn=key_fn, key_pos=key_pos, val_pos=val_pos, kind=kind,

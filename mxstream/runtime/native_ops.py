@@ -466,3 +466,112 @@ class NativeMedianOp(NativeWindowOp):
     def snapshot(self) -> dict:
         raise NotImplementedError("checkpointing of native process windows is not supported; "
                                   "run with native='off' for checkpointed process windows")
+
+
+class NativeVectorWindowOp(NativeWindowOp):
+    """``timeWindow(..).aggregate(VectorSumAggregate / VectorAvgAggregate(field))``: per-key
+    element-wise sum / average of a metric-vector field on the native vector-window operator
+    (runtime/vector_window_operator.py: MFMA segmented sums on the GPU, C++ twin on the CPU).
+    Vectors are zero-padded to the kernel width (a multiple of 32); results are cut back to the
+    input length. Windows and watermarks behave exactly as in NativeWindowOp."""
+
+    name = "VectorWindow(native)"
+
+    def _build(self, sample_val) -> bool:
+        if not isinstance(sample_val, (list, tuple)) or not sample_val \
+                or not all(isinstance(x, (int, float)) and not isinstance(x, bool)
+                           for x in sample_val):
+            return False
+        from .vector_window_operator import VectorWindowOperator
+
+        self.vlen = len(sample_val)
+        self.is_float = True
+        dim = max(32, -(-self.vlen // 32) * 32)
+        if dim > 256:
+            return False
+        a = self.assigner
+        event = a.is_event_time()
+        self.op = VectorWindowOperator(
+            dim=dim, avg=self.kind == "vavg", size=a.size, slide=a.slide, offset=a.offset,
+            lateness=self.lateness if event else 0, device=torch.device(self.device),
+            max_keys=self.max_keys, parallelism=1, batch_capacity=max(1024, self.ctx.parallelism),
+            cap_log2=9, time_mode="event" if event else "processing", external_watermark=True,
+            side_output_late=self.late_tag is not None, clock=self.ctx.clock)
+        return True
+
+    def _flush(self) -> list:
+        recs = self.pending
+        self.pending = []
+        if not recs:
+            return []
+        if self.op is None:
+            v0 = recs[0].value
+            if (not isinstance(v0, tuple) or (self.ok_arities and len(v0) not in self.ok_arities)
+                    or not self._build(v0[self.val_pos])):
+                self._to_fallback()
+                return self.fallback.process(recs)
+        n = len(recs)
+        dim = self.op.dim
+        try:
+            kid = np.empty(n, dtype=np.int64)
+            tsa = np.empty(n, dtype=np.int64)
+            vv = np.zeros((n, dim), dtype=np.float32)
+            now = self.ctx.clock()
+            event = self.assigner.is_event_time()
+            for i, r in enumerate(recs):
+                v = r.value
+                k = self._key_id(v[self.key_pos])
+                kid[i] = k
+                if k not in self.templates:
+                    self.templates[k] = v
+                tsa[i] = r.ts if event else now
+                x = v[self.val_pos]
+                if not isinstance(x, (list, tuple)) or len(x) != self.vlen:
+                    raise TypeError("metric vectors must all have the first vector's length")
+                vv[i, :self.vlen] = x
+        except (TypeError, ValueError):
+            self._to_fallback()
+            return self.fallback.process(recs)
+        dev = self.op.device
+        fired = self.op.process(torch.from_numpy(kid).to(dev), torch.from_numpy(tsa).to(dev),
+                                torch.from_numpy(vv).to(dev))
+        if self.op.late_side:
+            for idx in np.concatenate(self.op.late_side).tolist():
+                r = recs[idx]
+                self.side.setdefault(self.late_tag.tag_id, []).append(Rec(r.value, r.ts, r.subtask))
+            self.op.late_side.clear()
+        return self._emit(fired)
+
+    def _emit(self, fired) -> list:
+        from ..utils.hashing import flink_murmur
+
+        out = []
+        P, MP = self.ctx.parallelism, self.ctx.max_parallelism
+        for fr in fired:
+            ts = fr.window_end - 1
+            for k, vec in zip(fr.keys.tolist(), fr.values):
+                key_obj = self.dict.get(k) if self.str_keys else k
+                res = [float(x) for x in vec[:self.vlen]]
+                value = self.result_builder(self.templates[k], res, key_obj)
+                sub = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
+                out.append(Rec(value, ts, sub))
+        return out
+
+    def snapshot(self) -> dict:
+        snap = super().snapshot()
+        if "engine" in snap:
+            snap["engine"]["vlen"] = self.vlen
+        return snap
+
+    def restore(self, snap: dict) -> None:
+        eng = snap.get("engine")
+        if eng is None or "fallback" in snap:
+            return super().restore(snap)
+        self.wm = snap["wm"]
+        self.num_late_records_dropped = snap["late"]
+        self.str_keys = snap["str_keys"]
+        self.templates = dict(snap["templates"])
+        for st in snap["strings"]:
+            self.dict.intern(st)
+        self._build([0.0] * eng["vlen"])
+        self.op.restore_state(eng["columns"], eng["meta"])
