@@ -38,6 +38,10 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=1 << 24, help="events per GPU per step")
     ap.add_argument("--keys", type=int, default=1_000_000)
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--trace", default=None,
+                    help="write a Chrome trace of the timed steps (stage spans; roctx with MXS_ROCTX=1)")
+    ap.add_argument("--step-timeout-ms", type=int, default=0,
+                    help="watchdog: abort the run if one step makes no progress for this long")
     a = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -55,6 +59,17 @@ def main() -> int:
 
     cfg = TumblingBenchConfig(keys=a.keys, batch=a.batch)
     bench = TumblingWindowBench(cfg, comm, device)
+    if a.trace:
+        from mxstream.utils import trace
+        from mxstream.utils.metrics import StageTimer
+
+        trace.enable(True)
+        bench.op.timer = StageTimer(f"rank{comm.rank}", device)
+    wd = None
+    if a.step_timeout_ms > 0:
+        from mxstream.runtime.health import Watchdog
+
+        wd = Watchdog(a.step_timeout_ms, name=f"bench-rank{comm.rank}", action="abort").start()
 
     def sync():
         if device.type == "cuda":
@@ -70,6 +85,8 @@ def main() -> int:
     t0 = time.perf_counter()
     for _ in range(a.steps):
         bench.step()
+        if wd is not None:
+            wd.beat()
     sync()
     comm.barrier()
     sync()
@@ -117,6 +134,15 @@ def main() -> int:
             },
         }
         print(json.dumps(out), flush=True)
+    if wd is not None:
+        wd.stop()
+    if a.trace:
+        from mxstream.utils import trace
+
+        if bench.op.timer is not None:
+            bench.op.timer.flush()
+        path = a.trace if comm.world == 1 else f"{a.trace}.rank{comm.rank}"
+        trace.dump(path, comm.rank)
     return 0
 
 

@@ -442,4 +442,5 @@ PYBIND11_MODULE(_mxs_native, m) {
   bind_runtime(m);
   bind_sessions(m);
   bind_vector(m);
+  bind_trace(m);
 }

@@ -34,6 +34,12 @@ class ExecutionConfig:
     metrics_prometheus: str | None = field(
         default_factory=lambda: os.environ.get("MXS_METRICS_PROMETHEUS"))
     metrics_interval_ms: int = 1000
+    # Chrome-trace JSON of the job's stage spans (utils/trace.py); MXS_TRACE_PATH.
+    trace_path: str | None = field(default_factory=lambda: os.environ.get("MXS_TRACE_PATH"))
+    # Failure detection (runtime/health.py): a pass over the DAG taking longer than this fails
+    # the job with StepTimeout (restartable like any failure); <= 0 disables. MXS_STEP_TIMEOUT_MS.
+    step_timeout_ms: int = field(
+        default_factory=lambda: int(os.environ.get("MXS_STEP_TIMEOUT_MS", "0")))
 
     def set_auto_watermark_interval(self, ms: int) -> "ExecutionConfig":
         self.auto_watermark_interval = int(ms)

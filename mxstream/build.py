@@ -26,7 +26,9 @@ ARCH = os.environ.get("MXS_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["kernels_hip.hip", "sort_hip.hip", "parse_hip.hip", "vector_hip.hip"]
 CXX_SOURCES = ["kernels_cpu.cpp", "runtime.cpp", "sessions.cpp", "vector_cpu.cpp",
-               "vector_bindings.cpp", "bindings.cpp"]
+               "vector_bindings.cpp", "trace.cpp", "bindings.cpp"]
+# roctx ranges (csrc/trace.cpp) come from the ROCm profiler SDK's marker library.
+LINK_LIBS = ["-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def _ext_suffix() -> str:
@@ -99,7 +101,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
     out = target_path()
     link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs],
-            "-o", str(out) + ".tmp"]
+            *LINK_LIBS, "-o", str(out) + ".tmp"]
     newest = max(o.stat().st_mtime for o in objs)
     if force or not out.exists() or out.stat().st_mtime < newest:
         res = subprocess.run(link, capture_output=True, text=True)

@@ -122,6 +122,10 @@ def init_distributed(device: str = "auto", timeout_s: int = 600) -> Comm:
         device = "cuda" if torch.cuda.is_available() else "cpu"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     backend = "nccl" if device == "cuda" else "gloo"
+    if backend == "nccl":
+        from ..runtime.health import configure_collective_errors
+
+        configure_collective_errors()
     if not dist.is_initialized():
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":

@@ -16,7 +16,9 @@ import time
 from dataclasses import dataclass, field
 from typing import Any, Callable
 
+from ..utils import trace
 from ..utils.log import get_logger
+from .health import StepTimeout, Watchdog
 from .operators import LONG_MAX, OpContext, Operator, Rec, UnionOp, WM
 from .sources import Source
 
@@ -115,6 +117,7 @@ class Executor:
         self.ops: dict[int, Any] = {}
         self.metrics: dict[str, int] = {}
         self._rr: dict = {}
+        self._trace = False
 
     @staticmethod
     def _topo(sinks):
@@ -172,7 +175,11 @@ class Executor:
                 op = self.ops[n.id]
                 if self.fault is not None and items:
                     self._maybe_fault(n, items)
-                out = op.process(items) if items else []
+                if items and self._trace:
+                    with trace.span(n.name, "operator"):
+                        out = op.process(items)
+                else:
+                    out = op.process(items) if items else []
                 if now is not None:
                     out.extend(op.on_processing_time(now))
                 if items or out:
@@ -303,6 +310,14 @@ class Executor:
                 self._next_ckpt = int(done[-1].name[4:]) + 1
         last_ckpt = self.clock()
         reporter = self._reporter()
+        cfg_x = self.env.config
+        trace_path = getattr(cfg_x, "trace_path", None)
+        if trace_path:
+            trace.enable(True)
+        self._trace = trace.active()
+        wd = None
+        if getattr(cfg_x, "step_timeout_ms", 0) and cfg_x.step_timeout_ms > 0:
+            wd = Watchdog(cfg_x.step_timeout_ms, name=self.job_name).start()
         try:
             while not all(finished.values()):
                 if manual:
@@ -320,6 +335,8 @@ class Executor:
                     for c in self.children[n.id]:
                         inbox.setdefault((c.id, n.id), []).extend(self._rebalance(n, c, items))
                 self._push(inbox, now)
+                if wd is not None:
+                    wd.beat()
                 if cfg.is_checkpointing_enabled() and self.clock() - last_ckpt >= cfg.interval_ms:
                     self._checkpoint(finished)
                     last_ckpt = self.clock()
@@ -334,9 +351,19 @@ class Executor:
             self._finish()
         except (JobExecutionException, InjectedFault):
             raise
+        except KeyboardInterrupt:
+            if wd is not None and wd.expired:
+                raise JobExecutionException(f"Job '{self.job_name}' failed: StepTimeout: no "
+                                            f"progress for {cfg_x.step_timeout_ms} ms") \
+                    from StepTimeout(self.job_name)
+            raise
         except Exception as e:
             raise JobExecutionException(f"Job '{self.job_name}' failed: {type(e).__name__}: {e}") from e
         finally:
+            if wd is not None:
+                wd.stop()
+            if trace_path:
+                trace.dump(trace_path, self.env.rank)
             for n in self.nodes:
                 op = self.ops.get(n.id)
                 if op is not None:

@@ -23,6 +23,8 @@ Keys (all optional):
 | metrics_interval_ms | reporter period | 1000 |
 | fault | fault injection spec "op:records[:attempts]" | none |
 | host_budget_bytes | host-DRAM budget of spilled session state (exceeding it fails the job) | unlimited |
+| trace_path | Chrome-trace JSON of the job's stage spans (utils/trace.py) | none |
+| step_timeout_ms | watchdog: a DAG pass slower than this fails the job (runtime/health.py) | off |
 """
 from __future__ import annotations
 
@@ -46,6 +48,8 @@ class EngineConfig:
     metrics_interval_ms: int = 1000
     fault: str | None = None
     host_budget_bytes: int | None = None
+    trace_path: str | None = None
+    step_timeout_ms: int = 0
 
     def resolved_device(self) -> str:
         if self.device != "auto":
@@ -133,6 +137,10 @@ def apply_to_env(cfg: EngineConfig, env) -> None:
     env.config.metrics_json = cfg.metrics_json
     env.config.metrics_prometheus = cfg.metrics_prometheus
     env.config.metrics_interval_ms = cfg.metrics_interval_ms
+    if cfg.trace_path:
+        env.config.trace_path = cfg.trace_path
+    if cfg.step_timeout_ms:
+        env.config.step_timeout_ms = cfg.step_timeout_ms
     if cfg.checkpoint_interval_ms and cfg.checkpoint_interval_ms > 0:
         env.enable_checkpointing(cfg.checkpoint_interval_ms)
         env.checkpoint_config.checkpoint_dir = cfg.checkpoint_dir

@@ -229,6 +229,11 @@ class StageTimer:
 
         class _Ctx:
             def __enter__(self_inner):
+                from . import trace
+
+                self_inner.tr = trace.active()
+                if self_inner.tr:
+                    trace.load().trace_push(f"{timer.scope}.{name}", "stage")
                 if not timer.enabled:
                     return self_inner
                 if timer.gpu:
@@ -239,6 +244,10 @@ class StageTimer:
                 return self_inner
 
             def __exit__(self_inner, *exc):
+                if self_inner.tr:
+                    from . import trace
+
+                    trace.load().trace_pop()
                 if not timer.enabled:
                     return False
                 if timer.gpu:
@@ -254,10 +263,15 @@ class StageTimer:
 
     def flush(self) -> None:
         """Resolve recorded GPU events (call after a sync point)."""
+        from . import trace
+
+        tr = self.gpu and trace.enabled()
         keep = []
         for name, a, b in self._pending:
             if b.query():
                 self.registry.histogram(f"{self.scope}.step_ms.{name}").update(a.elapsed_time(b))
+                if tr:
+                    trace.gpu_span(f"{self.scope}.{name}", a, b)
             else:
                 keep.append((name, a, b))
         self._pending = keep
