@@ -443,4 +443,5 @@ PYBIND11_MODULE(_mxs_native, m) {
   bind_sessions(m);
   bind_vector(m);
   bind_trace(m);
+  bind_check(m);
 }

@@ -7,3 +7,4 @@ void bind_runtime(pybind11::module_& m);
 void bind_sessions(pybind11::module_& m);
 void bind_vector(pybind11::module_& m);
 void bind_trace(pybind11::module_& m);
+void bind_check(pybind11::module_& m);

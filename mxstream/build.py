@@ -24,9 +24,10 @@ BUILD = ROOT / "build" / "native"
 PKG = ROOT / "mxstream"
 ARCH = os.environ.get("MXS_OFFLOAD_ARCH", "gfx950")
 
-HIP_SOURCES = ["kernels_hip.hip", "sort_hip.hip", "parse_hip.hip", "vector_hip.hip"]
+HIP_SOURCES = ["kernels_hip.hip", "sort_hip.hip", "parse_hip.hip", "vector_hip.hip",
+               "check_hip.hip"]
 CXX_SOURCES = ["kernels_cpu.cpp", "runtime.cpp", "sessions.cpp", "vector_cpu.cpp",
-               "vector_bindings.cpp", "trace.cpp", "bindings.cpp"]
+               "vector_bindings.cpp", "trace.cpp", "check_cpu.cpp", "bindings.cpp"]
 # roctx ranges (csrc/trace.cpp) come from the ROCm profiler SDK's marker library.
 LINK_LIBS = ["-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
 
@@ -113,11 +114,41 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     return out
 
 
+SANITIZE_SOURCES = ["kernels_cpu.cpp", "vector_cpu.cpp", "tests/sanitize_main.cpp"]
+SANITIZE_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+                  "-fno-sanitize-recover=all"]
+
+
+def build_sanitize(verbose: bool = False) -> Path:
+    """Host sanitizer harness: the C++ twins + csrc/tests/sanitize_main.cpp
+    under AddressSanitizer + UndefinedBehaviorSanitizer (host code only; GPU sanitizers are not
+    available on the target pool). Returns the executable's path."""
+    out_dir = ROOT / "build" / "sanitize"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    exe = out_dir / "mxs_sanitize"
+    srcs = [CSRC / s for s in SANITIZE_SOURCES]
+    cmd = ["g++", "-std=c++17", *SANITIZE_FLAGS, f"-I{CSRC}", "-I/opt/rocm/include",
+           "-D__HIP_PLATFORM_AMD__", *[str(s) for s in srcs], "-o", str(exe)]
+    newest = max(s.stat().st_mtime for s in srcs + sorted(CSRC.glob("*.h")))
+    if not exe.exists() or exe.stat().st_mtime < newest:
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"sanitize build failed: {' '.join(cmd)}\n{res.stderr}")
+        if verbose:
+            print(f"[mxstream.build] built {exe}")
+    return exe
+
+
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--sanitize", action="store_true",
+                    help="build the ASan/UBSan host harness (build/sanitize/mxs_sanitize)")
     a = ap.parse_args(argv)
+    if a.sanitize:
+        print(build_sanitize(verbose=True))
+        return 0
     p = build(force=a.force, jobs=a.jobs, verbose=True)
     print(p)
     return 0

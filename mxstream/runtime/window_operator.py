@@ -169,6 +169,9 @@ class KeyedWindowOperator:
             compact = self.device.type == "cuda" and int_agg
         self.compact = bool(compact and int_agg)
         self.timer = None  # utils.metrics.StageTimer: per-stage step_ms histograms when attached
+        from ..ops.debug import debug_enabled
+
+        self._debug = debug_enabled()  # MXS_DEBUG: table invariant check after every step
 
         # ---- watermark / firing bookkeeping (host, identical on every rank) ----
         self.wm = I64_MIN
@@ -389,6 +392,11 @@ class KeyedWindowOperator:
                               rec_words=3 if combined else (2 if self.compact else 3))
             with self._stage("window_agg"):
                 self._aggregate(recs, counts, aplan)
+            if self._debug:
+                from ..ops.debug import assert_table_ok
+
+                assert_table_ok(self.keys_g, nsub=self.nsub, nsub_log2=self.nsub_log2,
+                                cap_log2=self.cap_log2, where=f"after step {self.metrics.steps}")
             # Late-but-allowed data: re-fire already-passed windows that are not cleaned yet.
             if gmin <= fired_hi:
                 out.extend(self._refire(gmin, min(gmax, fired_hi), old_wm))

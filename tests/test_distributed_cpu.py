@@ -146,3 +146,70 @@ def test_sessions_invariant_to_world_size():
     ref.update(_collect_sessions(op.finish()))
     assert merged == ref
     assert late == op.metrics.num_late_records_dropped
+
+
+# ---- vector-metric windows: vectors travel with their records --------------------------------
+def _vec_batch(rank, step, dim=32):
+    from mxstream.ops import vector as V
+
+    keys, ts, _ = _batch(rank, step)
+    vec = torch.empty(PER, dim, dtype=torch.float32)
+    V.gen_vectors(vec, seed=3, stream_id=rank, idx0=step * PER)
+    return keys, ts, vec
+
+
+def _collect_vec(out):
+    return {(r.window_start, int(k)): (v.tolist(), int(c))
+            for r in out for k, v, c in zip(r.keys, r.values, r.counts)}
+
+
+def _vector_worker(rank, world, port, q):
+    from mxstream.runtime.vector_window_operator import VectorWindowOperator
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    op = VectorWindowOperator(dim=32, size=3000, slide=1000, device="cpu", comm=TorchComm(),
+                              max_keys=5000, batch_capacity=PER, ooo_bound=500)
+    out = []
+    for step in range(STEPS):
+        out += op.process(*_vec_batch(rank, step))
+    out += op.finish()
+    q.put((rank, _collect_vec(out), op.metrics.num_late_records_dropped))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_vector_windows_invariant_to_world_size():
+    import numpy as np
+
+    from mxstream.runtime.vector_window_operator import VectorWindowOperator
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_vector_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    merged, late = {}, 0
+    for _rank, d, nl in res:
+        late += nl
+        assert not (set(d) & set(merged)), "a (window, key) fired on two ranks"
+        merged.update(d)
+    op = VectorWindowOperator(dim=32, size=3000, slide=1000, device="cpu", max_keys=5000,
+                              batch_capacity=PER * world, ooo_bound=500)
+    out = []
+    for step in range(STEPS):
+        parts = [_vec_batch(r, step) for r in range(world)]
+        out += op.process(*[torch.cat([p[i] for p in parts]) for i in range(3)])
+    out += op.finish()
+    ref = _collect_vec(out)
+    assert merged.keys() == ref.keys()
+    for k, (v, c) in ref.items():
+        assert merged[k][1] == c
+        np.testing.assert_allclose(merged[k][0], v, rtol=1e-5, atol=1e-4)
+    assert late == op.metrics.num_late_records_dropped
