@@ -38,9 +38,38 @@ __global__ __launch_bounds__(256) void check_table_kernel(const uint64_t* __rest
   if (threadIdx.x < kChkN && red[threadIdx.x]) atomicAdd(&stats[threadIdx.x], red[threadIdx.x]);
 }
 
+__global__ __launch_bounds__(256) void min_i64_kernel(const int64_t* __restrict__ x, int64_t n,
+                                                      long long* __restrict__ out) {
+  __shared__ long long red[4];
+  long long m = INT64_MAX;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    m = x[i] < m ? x[i] : m;
+  for (int o = 32; o > 0; o >>= 1) {
+    const long long w = __shfl_xor(m, o);
+    m = w < m ? w : m;
+  }
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) m = red[w] < m ? red[w] : m;
+    if (m != INT64_MAX) atomicMin(out, m);
+  }
+}
+
 }  // namespace
 
 namespace gpu {
+void min_i64(const int64_t* x, int64_t n, int64_t* out, intptr_t stream) {
+  if (n <= 0) return;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(min_i64_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, x,
+                     n, (long long*)out);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e));
+}
+
 void check_table(const uint64_t* keys_g, int nsub, int nsub_log2, int cap_log2, uint64_t* stats,
                  intptr_t stream) {
   if (nsub <= 0) return;

@@ -1,0 +1,78 @@
+/* mxstream — C ABI of the native keyed-window pipeline (csrc/pipeline.cpp).
+ *
+ * The surface a non-Python host binds to (a JNI layer for the DataStream-style Java API of
+ * BASELINE.json, or a C/C++ service): one pipeline = one rank's keyed event-time tumbling /
+ * sliding window with allowed lateness and a bounded-out-of-orderness watermark — the
+ * reference's BandwidthMonitorWithEventTime shape (chapter3/src/main/java/me/zjy/
+ * BandwidthMonitorWithEventTime.java:30-55) — running the gfx950 kernels (device = 1) or their
+ * C++ twins (device = 0). Built as build/lib/libmxstream.so by `python -m mxstream.build --capi`.
+ *
+ * Threading: a pipeline is single-threaded (one caller at a time); distinct pipelines are
+ * independent. Errors: functions return < 0 and mxs_last_error() describes the failure.
+ */
+#ifndef MXS_C_H_
+#define MXS_C_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MXS_API __attribute__((visibility("default")))
+
+/* Aggregates (same numbering as the engine's AggKind). */
+enum { MXS_AGG_SUM_I64 = 0, MXS_AGG_SUM_F64 = 1, MXS_AGG_MIN_I64 = 2, MXS_AGG_MAX_I64 = 3,
+       MXS_AGG_MIN_F64 = 4, MXS_AGG_MAX_F64 = 5, MXS_AGG_COUNT = 6, MXS_AGG_AVG_F64 = 7,
+       MXS_AGG_AVG_I64 = 8 };
+
+typedef struct mxs_window_config {
+  int64_t size_ms;          /* window size */
+  int64_t slide_ms;         /* == size_ms for tumbling windows */
+  int64_t offset_ms;        /* window offset (0 = epoch aligned) */
+  int64_t lateness_ms;      /* allowed lateness (late-but-allowed data re-fires) */
+  int64_t ooo_bound_ms;     /* BoundedOutOfOrdernessTimestampExtractor bound */
+  int32_t agg;              /* MXS_AGG_* */
+  int32_t device;           /* 0 = C++ twins on the host, 1 = HIP device */
+  int32_t device_index;     /* HIP device ordinal when device == 1 */
+  int32_t max_parallelism;  /* Flink key groups (128) */
+  int64_t max_keys;         /* keyed state sizing */
+  int64_t batch_capacity;   /* events per process() call (grows on demand) */
+} mxs_window_config;
+
+typedef struct mxs_window_result {
+  int64_t window_start;
+  int64_t window_end;
+  uint64_t key;
+  double value;             /* aggregate result (avg = sum / count; f64 aggregates as double) */
+  int64_t raw;              /* raw accumulator: exact integer sum / f64 bit pattern */
+  uint32_t count;           /* elements in the window */
+  int32_t refire;           /* 1: re-firing caused by late-but-allowed data */
+} mxs_window_result;
+
+typedef struct mxs_pipeline mxs_pipeline;
+
+MXS_API void mxs_window_config_default(mxs_window_config* cfg);
+MXS_API mxs_pipeline* mxs_pipeline_create(const mxs_window_config* cfg);
+MXS_API void mxs_pipeline_destroy(mxs_pipeline* p);
+/* One micro-batch of host arrays (keys, event timestamps in ms, int64 values / f64 bit
+ * patterns). Fires every window the advanced watermark allows; results queue up until taken. */
+MXS_API int mxs_pipeline_process(mxs_pipeline* p, const uint64_t* keys, const int64_t* ts,
+                                 const int64_t* vals, int64_t n);
+/* End of input: Long.MAX_VALUE watermark fires every remaining window. */
+MXS_API int mxs_pipeline_finish(mxs_pipeline* p);
+MXS_API int64_t mxs_pipeline_num_results(const mxs_pipeline* p);
+/* Moves up to `cap` queued results into `out`; returns how many were written. */
+MXS_API int64_t mxs_pipeline_take_results(mxs_pipeline* p, mxs_window_result* out, int64_t cap);
+MXS_API int64_t mxs_pipeline_watermark(const mxs_pipeline* p);
+MXS_API int64_t mxs_pipeline_late_dropped(const mxs_pipeline* p);
+MXS_API int64_t mxs_pipeline_records_in(const mxs_pipeline* p);
+MXS_API const char* mxs_last_error(void);
+MXS_API const char* mxs_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MXS_C_H_ */

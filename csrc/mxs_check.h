@@ -45,6 +45,9 @@ MXS_HD uint32_t check_slot(const uint64_t* keys, uint32_t s, uint32_t mask, int 
 namespace gpu {
 void check_table(const uint64_t* keys_g, int nsub, int nsub_log2, int cap_log2, uint64_t* stats,
                  intptr_t stream);
+// out[0] = min(out[0], min(x[0..n))) (caller initialises out[0]); used by the native pipeline
+// for the first step's pane base.
+void min_i64(const int64_t* x, int64_t n, int64_t* out, intptr_t stream);
 }
 namespace cpu {
 // C++ twin (header-only so the sanitizer harness links it without the Python bindings).

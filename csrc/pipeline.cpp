@@ -1,0 +1,576 @@
+// mxstream — native keyed event-time window pipeline + C ABI (mxs_c.h).
+//
+// The per-rank micro-batch control loop of runtime/window_operator.py (KeyedWindowOperator,
+// G = 1) in C++, so a host without Python (a JNI binding of the Java DataStream API, a C/C++
+// service) can run the reference's BandwidthMonitorWithEventTime shape
+// (chapter3/src/main/java/me/zjy/BandwidthMonitorWithEventTime.java:30-55): Flink window
+// assignment (TimeWindow.getWindowStartWithOffset), bounded-out-of-orderness watermark, late drop
+// (maxTs + allowedLateness <= wm), re-firing of late-but-allowed data, purge after cleanup time,
+// Long.MAX_VALUE watermark at end of input. Same kernels as the Python operator: gfx950
+// (device = 1) or the C++ twins (device = 0); tests/test_capi.py checks the two agree and
+// replays the chapter3 README golden stream through the C ABI.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "mxs_c.h"
+#include "mxs_check.h"
+#include "mxs_kernels.h"
+
+namespace mxs {
+namespace {
+
+using i128 = __int128;
+constexpr int64_t kMin = INT64_MIN, kMax = INT64_MAX;
+
+thread_local std::string g_err;
+
+void hip_ok(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+i128 fdiv128(i128 a, i128 b) {
+  i128 q = a / b;
+  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+  return q;
+}
+i128 java_rem(i128 a, i128 b) {  // Java's % on long: sign of the dividend
+  const i128 r = (a < 0 ? -a : a) % (b < 0 ? -b : b);
+  return a < 0 ? -r : r;
+}
+int64_t clamp64(i128 v) { return v > kMax ? kMax : v < kMin ? kMin : (int64_t)v; }
+int64_t next_pow2(int64_t x) {
+  int64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// Device-or-host buffers of one pipeline.
+struct Mem {
+  bool gpu = false;
+  hipStream_t stream = nullptr;
+  std::vector<void*> owned;
+
+  void* alloc(size_t bytes) {
+    void* p = nullptr;
+    if (bytes == 0) bytes = 8;
+    if (gpu) {
+      hip_ok(hipMalloc(&p, bytes), "hipMalloc");
+    } else {
+      p = std::calloc(1, bytes);
+      if (!p) throw std::bad_alloc();
+    }
+    owned.push_back(p);
+    return p;
+  }
+  void release(void* p) {
+    if (!p) return;
+    owned.erase(std::remove(owned.begin(), owned.end(), p), owned.end());
+    if (gpu) (void)hipFree(p);
+    else std::free(p);
+  }
+  void fill(void* p, int byte, size_t bytes) {
+    if (gpu) hip_ok(hipMemsetAsync(p, byte, bytes, stream), "hipMemsetAsync");
+    else std::memset(p, byte, bytes);
+  }
+  void to_dev(void* dst, const void* src, size_t bytes) {
+    if (gpu) hip_ok(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream), "H2D");
+    else std::memcpy(dst, src, bytes);
+  }
+  void to_host(void* dst, const void* src, size_t bytes) {
+    if (gpu) {
+      hip_ok(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream), "D2H");
+      hip_ok(hipStreamSynchronize(stream), "hipStreamSynchronize");
+    } else {
+      std::memcpy(dst, src, bytes);
+    }
+  }
+  void dev_copy(void* dst, const void* src, size_t bytes) {
+    if (gpu) hip_ok(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream), "D2D");
+    else std::memmove(dst, src, bytes);
+  }
+  ~Mem() {
+    for (void* p : owned) {
+      if (gpu) (void)hipFree(p);
+      else std::free(p);
+    }
+  }
+};
+
+// runtime/geometry.py state_geometry(max_keys, world = 1)
+void state_geometry(int64_t max_keys, int* nsub_out, int* cap_log2_out) {
+  const double per_rank = (double)max_keys + 64;
+  const double load = 0.7;
+  int64_t nsub = next_pow2(std::max<int64_t>(1, (int64_t)std::ceil(per_rank / (4096 * load))));
+  nsub = std::max<int64_t>(nsub, 256);
+  const double need = per_rank / (double)nsub / load;
+  int cl = (int)std::ceil(std::log2(std::max(need, 2.0)));
+  cl = std::max(6, std::min(12, cl));
+  const double mean = per_rank / (double)nsub;
+  while (cl < 12 && mean + 4 * std::sqrt(mean) + 8 > (double)(1 << cl) * 0.85) ++cl;
+  *nsub_out = (int)nsub;
+  *cap_log2_out = cl;
+}
+
+}  // namespace
+
+class WindowPipeline {
+ public:
+  explicit WindowPipeline(const mxs_window_config& c) : cfg_(c) {
+    if (c.size_ms <= 0 || c.slide_ms <= 0) throw std::invalid_argument("window size and slide must be positive");
+    if (c.agg < AGG_SUM_I64 || c.agg > AGG_AVG_I64) throw std::invalid_argument("unknown aggregate");
+    if (c.lateness_ms < 0 || c.ooo_bound_ms < 0) throw std::invalid_argument("negative lateness / bound");
+    mem_.gpu = c.device != 0;
+    if (mem_.gpu) {
+      hip_ok(hipSetDevice(c.device_index), "hipSetDevice");
+      hip_ok(hipStreamCreateWithFlags(&mem_.stream, hipStreamNonBlocking), "hipStreamCreate");
+    }
+    size_ = c.size_ms;
+    slide_ = c.slide_ms;
+    offset_ = c.offset_ms;
+    lateness_ = c.lateness_ms;
+    ooo_ = c.ooo_bound_ms;
+    max_par_ = c.max_parallelism > 0 ? c.max_parallelism : 128;
+    pane_ = std::gcd(size_, slide_);
+    ppw_ = size_ / pane_;
+    state_geometry(std::max<int64_t>(c.max_keys, 1), &nsub_, &cap_log2_);
+    nsub_log2_ = 0;
+    while ((1 << nsub_log2_) < nsub_) ++nsub_log2_;
+    nslots_ = (int64_t)nsub_ << cap_log2_;
+    ring_ = std::max<int64_t>(4, next_pow2(ppw_ + 2 + (lateness_ + pane_ - 1) / pane_ +
+                                           (std::max(ooo_, slide_) + pane_ - 1) / pane_));
+    const bool int_agg = c.agg == AGG_SUM_I64 || c.agg == AGG_MIN_I64 || c.agg == AGG_MAX_I64 ||
+                         c.agg == AGG_COUNT || c.agg == AGG_AVG_I64;
+    compact_ = mem_.gpu && int_agg;
+    keys_g_ = (uint64_t*)mem_.alloc(nslots_ * 8);
+    mem_.fill(keys_g_, 0xFF, nslots_ * 8);
+    alloc_state(ring_);
+    occ_ = (uint32_t*)mem_.alloc(nsub_ * 4);
+    flags_ = (uint32_t*)mem_.alloc(16);
+    kg_dest_ = (int32_t*)mem_.alloc(max_par_ * 4);  // all key groups on this rank (zeros)
+    stats_ = (int64_t*)mem_.alloc(kStatCount * 8);
+    red_ = (int64_t*)mem_.alloc(16 * 8);
+    local_maxts_ = (int64_t*)mem_.alloc(8);
+    mem_.to_dev(local_maxts_, &kMin, 8);
+    minbuf_ = (int64_t*)mem_.alloc(8);
+    out_keys_ = (uint64_t*)mem_.alloc(nslots_ * 8);
+    out_vals_ = (double*)mem_.alloc(nslots_ * 8);
+    out_raw_ = (uint64_t*)mem_.alloc(nslots_ * 8);
+    out_cnt_ = (uint32_t*)mem_.alloc(nslots_ * 4);
+    out_n_ = (uint32_t*)mem_.alloc(4);
+    alloc_buckets(std::max<int64_t>(c.batch_capacity, 1024), 1.5);
+  }
+
+  ~WindowPipeline() {
+    if (mem_.gpu && mem_.stream) {
+      (void)hipStreamSynchronize(mem_.stream);
+      (void)hipStreamDestroy(mem_.stream);
+    }
+  }
+
+  void process(const uint64_t* keys_h, const int64_t* ts_h, const int64_t* vals_h, int64_t n) {
+    if (n < 0) throw std::invalid_argument("negative batch size");
+    if (n > batch_capacity_) alloc_buckets(n, slack_);
+    if (n > in_cap_) {
+      mem_.release(in_keys_);
+      mem_.release(in_ts_);
+      mem_.release(in_vals_);
+      in_cap_ = n;
+      in_keys_ = (uint64_t*)mem_.alloc(n * 8);
+      in_ts_ = (int64_t*)mem_.alloc(n * 8);
+      in_vals_ = (uint64_t*)mem_.alloc(n * 8);
+    }
+    if (n) {
+      mem_.to_dev(in_keys_, keys_h, n * 8);
+      mem_.to_dev(in_ts_, ts_h, n * 8);
+      mem_.to_dev(in_vals_, vals_h, n * 8);
+    }
+    const int64_t old_wm = wm_;
+    const int64_t pane_base = pane_base_of(n);
+    int64_t host[16];
+    for (;;) {
+      if (mem_.gpu) gpu::step_begin(cursor_, nb(), stats_, (intptr_t)mem_.stream);
+      else cpu::step_begin(cursor_, nb(), stats_);
+      PartPlan pp;
+      std::memset(&pp, 0, sizeof(pp));
+      pp.max_parallelism = max_par_;
+      pp.nsub_log2 = nsub_log2_;
+      pp.nranks = 1;
+      pp.window_mode = 1;
+      pp.drop_late = 1;
+      pp.hash_mode = 0;
+      pp.bucket_cap = (uint32_t)bucket_cap_;
+      pp.late_ts = late_ts(old_wm);
+      pp.tbase = pane_start(pane_base);
+      pp.pane = pane_;
+      pp.inv_pane = 1.0 / (double)pane_;
+      pp.rec_words = compact_ ? 2 : 3;
+      if (n) {
+        if (mem_.gpu)
+          gpu::partition(in_keys_, in_ts_, in_vals_, nullptr, n, pp, kg_dest_, cursor_, send_,
+                         stats_, nullptr, 0, (intptr_t)mem_.stream);
+        else
+          cpu::partition(in_keys_, in_ts_, in_vals_, nullptr, n, pp, kg_dest_, cursor_, send_,
+                         stats_, nullptr, 0);
+      }
+      if (mem_.gpu)
+        gpu::step_finish(stats_, local_maxts_, ooo_, 1, 0, red_, (intptr_t)mem_.stream);
+      else
+        cpu::step_finish(stats_, local_maxts_, ooo_, 1, 0, red_);
+      mem_.to_host(host, red_, sizeof(host));  // the step's single host sync
+      if (host[4]) throw std::runtime_error("event timestamp outside the representable pane range");
+      if (host[5]) {
+        compact_ = false;  // a value does not fit the 16-byte record
+        continue;
+      }
+      if (host[3]) {
+        alloc_buckets(batch_capacity_, slack_ * 2);
+        continue;
+      }
+      break;
+    }
+    const int64_t qmax = -host[0], qmin = host[1], wm_global = host[2];
+    records_in_ += n;
+    late_dropped_ += host[8 + kStatLate];
+    if (qmin <= qmax) {
+      const int64_t gmin = pane_base + qmin, gmax = pane_base + qmax;
+      const int64_t lo = has_live_ ? std::min(min_live_, gmin) : gmin;
+      const int64_t hi = has_live_ ? std::max(max_seen_, gmax) : gmax;
+      if (hi - lo + 1 > ring_) grow_ring(hi - lo + 1);
+      min_live_ = lo;
+      max_seen_ = hi;
+      has_live_ = true;
+      int64_t cand = first_start_containing(pane_start(gmin));
+      if (old_wm > kMin) cand = std::max(cand, align_up((i128)old_wm - size_ + 2));
+      nfs_ = has_nfs_ ? std::min(nfs_, cand) : cand;
+      has_nfs_ = true;
+      const int64_t fhi = fired_hi();
+      const int64_t cap = (int64_t)1 << cap_log2_;
+      const int64_t np = gmax - gmin + 1;
+      const int64_t pg = std::max<int64_t>(1, std::min<int64_t>(np, (150 * 1024 - cap * 8) / (cap * 12)));
+      AggPlan ap;
+      std::memset(&ap, 0, sizeof(ap));
+      ap.cap_log2 = cap_log2_;
+      ap.nsub = nsub_;
+      ap.ring = (int32_t)ring_;
+      ap.agg = cfg_.agg;
+      ap.nsrc = 1;
+      ap.bucket_cap = (uint32_t)bucket_cap_;
+      ap.np_step = (int32_t)np;
+      ap.pg = (int32_t)pg;
+      ap.pane_base = pane_base;
+      ap.p_lo = qmin;
+      ap.fired_hi = fhi;
+      ap.rec_words = compact_ ? 2 : 3;
+      if (mem_.gpu)
+        gpu::window_agg(send_, cursor_, ap, keys_g_, acc_g_, cnt_g_, dirty_g_, occ_, flags_,
+                        (intptr_t)mem_.stream);
+      else
+        cpu::window_agg(send_, cursor_, ap, keys_g_, acc_g_, cnt_g_, dirty_g_, occ_, flags_);
+      if (gmin <= fhi) refire(gmin, std::min(gmax, fhi), old_wm);
+    }
+    ++steps_;
+    const int64_t new_wm = std::max(old_wm, wm_global);
+    wm_ = new_wm;
+    fire_ready(new_wm);
+    purge(new_wm);
+  }
+
+  void finish() {
+    if (wm_ >= kMax) return;
+    wm_ = kMax;
+    fire_ready(kMax);
+    purge(kMax);
+  }
+
+  int64_t watermark() const { return wm_; }
+  int64_t late_dropped() const { return late_dropped_; }
+  int64_t records_in() const { return records_in_; }
+  std::deque<mxs_window_result> results;
+
+ private:
+  int nb() const { return 1 << nsub_log2_; }
+
+  void alloc_state(int64_t ring) {
+    acc_g_ = (uint64_t*)mem_.alloc(ring * nslots_ * 8);
+    cnt_g_ = (uint32_t*)mem_.alloc(ring * nslots_ * 4);
+    dirty_g_ = (uint8_t*)mem_.alloc(ring * nslots_);
+    mem_.fill(acc_g_, 0, ring * nslots_ * 8);
+    mem_.fill(cnt_g_, 0, ring * nslots_ * 4);
+    mem_.fill(dirty_g_, 0, ring * nslots_);
+  }
+
+  void alloc_buckets(int64_t capacity, double slack) {
+    batch_capacity_ = capacity;
+    slack_ = slack;
+    const double per = (double)capacity / nb();
+    const int64_t nblk = std::min<int64_t>(1024, std::max<int64_t>(1, (capacity + 65535) / 65536));
+    int64_t cap = (int64_t)(per * slack + 6 * std::sqrt(std::max(per, 1.0)) + 64) + 8 * nblk;
+    bucket_cap_ = (cap + 7) & ~(int64_t)7;
+    mem_.release(send_);
+    mem_.release(cursor_);
+    send_ = (Rec*)mem_.alloc((size_t)nb() * bucket_cap_ * sizeof(Rec));
+    cursor_ = (uint32_t*)mem_.alloc(nb() * 4);
+  }
+
+  void grow_ring(int64_t need) {
+    const int64_t nr = next_pow2(need), old = ring_;
+    uint64_t* oacc = acc_g_;
+    uint32_t* ocnt = cnt_g_;
+    uint8_t* odirty = dirty_g_;
+    alloc_state(nr);
+    if (has_live_)
+      for (int64_t p = min_live_; p <= max_seen_; ++p) {
+        const int64_t so = (p & (old - 1)) * nslots_, sn = (p & (nr - 1)) * nslots_;
+        mem_.dev_copy(acc_g_ + sn, oacc + so, nslots_ * 8);
+        mem_.dev_copy(cnt_g_ + sn, ocnt + so, nslots_ * 4);
+        mem_.dev_copy(dirty_g_ + sn, odirty + so, nslots_);
+      }
+    if (mem_.gpu) hip_ok(hipStreamSynchronize(mem_.stream), "sync");
+    mem_.release(oacc);
+    mem_.release(ocnt);
+    mem_.release(odirty);
+    ring_ = nr;
+  }
+
+  // ---- window arithmetic (Flink 1.8 TimeWindow / SlidingEventTimeWindows) ----
+  int64_t pane_of(i128 t) const { return clamp64(fdiv128(t - offset_, pane_)); }
+  int64_t pane_start(i128 p) const { return clamp64((i128)offset_ + p * pane_); }
+  i128 last_start(i128 t) const { return t - java_rem(t - offset_ + slide_, slide_); }
+  int64_t first_start_containing(i128 t) const {
+    const i128 ls = last_start(t);
+    return clamp64(ls - fdiv128(ls - (t - size_ + 1), slide_) * slide_);
+  }
+  int64_t align_up(i128 t) const {
+    const i128 ls = last_start(t);
+    return clamp64(ls >= t ? ls : ls + slide_);
+  }
+  int64_t fired_hi() const {
+    if (!has_nfs_) return kMin;
+    return pane_of((i128)nfs_ - slide_ + size_ - 1);
+  }
+  int64_t late_ts(int64_t wm) const {
+    if (wm == kMin) return kMin;
+    return align_up((i128)wm - size_ - lateness_ + 2);
+  }
+  int64_t pane_base_of(int64_t n) {
+    if (wm_ > kMin) return pane_of((i128)wm_ - size_ - lateness_ + 1);
+    int64_t m = kMax;
+    if (n) {
+      if (mem_.gpu) {
+        mem_.to_dev(minbuf_, &kMax, 8);
+        gpu::min_i64(in_ts_, n, minbuf_, (intptr_t)mem_.stream);
+        mem_.to_host(&m, minbuf_, 8);
+      } else {
+        for (int64_t i = 0; i < n; ++i) m = std::min(m, in_ts_[i]);
+      }
+    }
+    int64_t base = m != kMax ? pane_of(m) : 0;
+    if (has_live_) base = std::min(base, min_live_);
+    return base;
+  }
+  bool overlaps_live(int64_t s) const {
+    if (!has_live_) return false;
+    const int64_t p0 = pane_of(s), p1 = p0 + ppw_ - 1;
+    return !(p1 < min_live_ || p0 > max_seen_);
+  }
+
+  void fire_window(int64_t s, bool only_dirty) {
+    const int64_t p0 = std::max(pane_of(s), min_live_);
+    const int64_t p1 = std::min(pane_of(s) + ppw_ - 1, max_seen_);
+    if (p1 < p0) return;
+    const uint32_t zero = 0;
+    mem_.to_dev(out_n_, &zero, 4);
+    FirePlan fp;
+    std::memset(&fp, 0, sizeof(fp));
+    fp.agg = cfg_.agg;
+    fp.npanes = (int32_t)(p1 - p0 + 1);
+    fp.ring = (int32_t)ring_;
+    fp.only_dirty = only_dirty ? 1 : 0;
+    fp.nslots = nslots_;
+    fp.p0 = p0;
+    fp.wstart = (double)s;
+    fp.wend = (double)s + (double)size_;
+    fp.out_cap = (uint32_t)nslots_;
+    if (mem_.gpu)
+      gpu::window_fire(keys_g_, acc_g_, cnt_g_, dirty_g_, fp, out_keys_, out_vals_, out_raw_,
+                       out_cnt_, out_n_, (intptr_t)mem_.stream);
+    else
+      cpu::window_fire(keys_g_, acc_g_, cnt_g_, dirty_g_, fp, out_keys_, out_vals_, out_raw_,
+                       out_cnt_, out_n_);
+    uint32_t n = 0;
+    mem_.to_host(&n, out_n_, 4);
+    n = (uint32_t)std::min<int64_t>(n, nslots_);
+    if (!n) return;
+    std::vector<uint64_t> k(n), raw(n);
+    std::vector<double> v(n);
+    std::vector<uint32_t> c(n);
+    mem_.to_host(k.data(), out_keys_, n * 8);
+    mem_.to_host(v.data(), out_vals_, n * 8);
+    mem_.to_host(raw.data(), out_raw_, n * 8);
+    mem_.to_host(c.data(), out_cnt_, n * 4);
+    for (uint32_t i = 0; i < n; ++i)
+      results.push_back({s, clamp64((i128)s + size_), k[i], v[i], (int64_t)raw[i], c[i],
+                         only_dirty ? 1 : 0});
+  }
+
+  void fire_ready(int64_t wm) {
+    if (!has_nfs_ || !has_live_) return;
+    int64_t s = nfs_;
+    const int64_t first_live = first_start_containing(pane_start(min_live_));
+    if (s < first_live) s = first_live;
+    const int64_t last_data_start = clamp64(last_start((i128)pane_start((i128)max_seen_ + 1) - 1));
+    while ((i128)s + size_ - 1 <= wm) {
+      if (s > last_data_start) {
+        s = std::max(s, align_up((i128)wm - size_ + 2));
+        break;
+      }
+      if (overlaps_live(s)) fire_window(s, false);
+      s += slide_;
+    }
+    nfs_ = s;
+  }
+
+  void refire(int64_t pmin, int64_t pmax, int64_t old_wm) {
+    int64_t s = first_start_containing(pane_start(pmin));
+    const int64_t end_s = std::min<int64_t>(nfs_ - slide_, clamp64(last_start(pane_start(pmax))));
+    for (; s <= end_s; s += slide_)
+      if ((i128)s + size_ - 1 + lateness_ > old_wm) fire_window(s, true);
+    for (int64_t p = pmin; p <= pmax; ++p)
+      mem_.fill(dirty_g_ + (p & (ring_ - 1)) * nslots_, 0, nslots_);
+  }
+
+  void purge(int64_t wm) {
+    if (!has_live_) return;
+    int64_t keep_from;
+    if (wm == kMax) keep_from = max_seen_ + 1;
+    else keep_from = pane_of(align_up((i128)wm - size_ - lateness_ + 2));
+    int64_t p = min_live_;
+    const int64_t stop = std::min(keep_from, max_seen_ + 1);
+    if (stop - p > ring_) p = stop - ring_;
+    for (; p < stop; ++p) {
+      const int64_t so = (p & (ring_ - 1)) * nslots_;
+      mem_.fill(acc_g_ + so, 0, nslots_ * 8);
+      mem_.fill(cnt_g_ + so, 0, nslots_ * 4);
+      mem_.fill(dirty_g_ + so, 0, nslots_);
+    }
+    if (keep_from > min_live_) {
+      min_live_ = keep_from;
+      if (min_live_ > max_seen_) has_live_ = false;
+    }
+  }
+
+  mxs_window_config cfg_;
+  Mem mem_;
+  int64_t size_, slide_, offset_, lateness_, ooo_, pane_, ppw_, ring_, nslots_;
+  int max_par_, nsub_, cap_log2_, nsub_log2_;
+  bool compact_ = false;
+  int64_t batch_capacity_ = 0, bucket_cap_ = 0, in_cap_ = 0;
+  double slack_ = 1.5;
+  uint64_t *keys_g_ = nullptr, *acc_g_ = nullptr, *out_keys_ = nullptr, *out_raw_ = nullptr;
+  uint64_t *in_keys_ = nullptr, *in_vals_ = nullptr;
+  int64_t *in_ts_ = nullptr, *stats_ = nullptr, *red_ = nullptr, *local_maxts_ = nullptr,
+          *minbuf_ = nullptr;
+  uint32_t *cnt_g_ = nullptr, *occ_ = nullptr, *flags_ = nullptr, *cursor_ = nullptr,
+           *out_cnt_ = nullptr, *out_n_ = nullptr;
+  uint8_t* dirty_g_ = nullptr;
+  int32_t* kg_dest_ = nullptr;
+  double* out_vals_ = nullptr;
+  Rec* send_ = nullptr;
+  // firing bookkeeping (identical to KeyedWindowOperator)
+  int64_t wm_ = kMin, nfs_ = 0, min_live_ = 0, max_seen_ = 0;
+  bool has_nfs_ = false, has_live_ = false;
+  int64_t records_in_ = 0, late_dropped_ = 0, steps_ = 0;
+};
+
+}  // namespace mxs
+
+// ---- C ABI ----------------------------------------------------------------------------------
+struct mxs_pipeline {
+  mxs::WindowPipeline impl;
+  explicit mxs_pipeline(const mxs_window_config& c) : impl(c) {}
+};
+
+namespace {
+template <class F>
+int guard(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    mxs::g_err = e.what();
+  } catch (...) {
+    mxs::g_err = "unknown error";
+  }
+  return -1;
+}
+}  // namespace
+
+extern "C" {
+
+void mxs_window_config_default(mxs_window_config* c) {
+  if (!c) return;
+  std::memset(c, 0, sizeof(*c));
+  c->size_ms = 60000;
+  c->slide_ms = 60000;
+  c->agg = MXS_AGG_SUM_I64;
+  c->max_parallelism = 128;
+  c->max_keys = 1 << 16;
+  c->batch_capacity = 1 << 16;
+}
+
+mxs_pipeline* mxs_pipeline_create(const mxs_window_config* cfg) {
+  if (!cfg) {
+    mxs::g_err = "null config";
+    return nullptr;
+  }
+  mxs_pipeline* p = nullptr;
+  if (guard([&] { p = new mxs_pipeline(*cfg); }) != 0) return nullptr;
+  return p;
+}
+
+void mxs_pipeline_destroy(mxs_pipeline* p) { delete p; }
+
+int mxs_pipeline_process(mxs_pipeline* p, const uint64_t* keys, const int64_t* ts,
+                         const int64_t* vals, int64_t n) {
+  if (!p || (n > 0 && (!keys || !ts || !vals))) {
+    mxs::g_err = "null argument";
+    return -1;
+  }
+  return guard([&] { p->impl.process(keys, ts, vals, n); });
+}
+
+int mxs_pipeline_finish(mxs_pipeline* p) {
+  if (!p) return -1;
+  return guard([&] { p->impl.finish(); });
+}
+
+int64_t mxs_pipeline_num_results(const mxs_pipeline* p) {
+  return p ? (int64_t)p->impl.results.size() : -1;
+}
+
+int64_t mxs_pipeline_take_results(mxs_pipeline* p, mxs_window_result* out, int64_t cap) {
+  if (!p || (cap > 0 && !out)) return -1;
+  int64_t n = 0;
+  while (n < cap && !p->impl.results.empty()) {
+    out[n++] = p->impl.results.front();
+    p->impl.results.pop_front();
+  }
+  return n;
+}
+
+int64_t mxs_pipeline_watermark(const mxs_pipeline* p) { return p ? p->impl.watermark() : INT64_MIN; }
+int64_t mxs_pipeline_late_dropped(const mxs_pipeline* p) { return p ? p->impl.late_dropped() : -1; }
+int64_t mxs_pipeline_records_in(const mxs_pipeline* p) { return p ? p->impl.records_in() : -1; }
+const char* mxs_last_error(void) { return mxs::g_err.c_str(); }
+const char* mxs_version(void) { return "mxstream-native 0.1 (gfx950)"; }
+
+}  // extern "C"

@@ -139,13 +139,47 @@ def build_sanitize(verbose: bool = False) -> Path:
     return exe
 
 
+CAPI_SOURCES = ["kernels_hip.hip", "check_hip.hip", "kernels_cpu.cpp", "pipeline.cpp"]
+
+
+def capi_path() -> Path:
+    # Next to the Python module (travels with the tree like the module; build/ does not).
+    return PKG / "lib" / "libmxstream.so"
+
+
+def build_capi(verbose: bool = False) -> Path:
+    """The C ABI library (csrc/mxs_c.h): the native window pipeline + kernels, no Python."""
+    out = capi_path()
+    srcs = [CSRC / s for s in CAPI_SOURCES] + sorted(CSRC.glob("*.h"))
+    if out.exists() and out.stat().st_mtime >= max(s.stat().st_mtime for s in srcs):
+        return out  # up to date (also on a GPU box that received the built tree)
+    BUILD.mkdir(parents=True, exist_ok=True)
+    objs = [_compile(CSRC / s, False) for s in CAPI_SOURCES]
+    out.parent.mkdir(parents=True, exist_ok=True)
+    if not out.exists() or out.stat().st_mtime < max(o.stat().st_mtime for o in objs):
+        link = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs],
+                "-o", str(out) + ".tmp"]
+        res = subprocess.run(link, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(link)}\n{res.stdout}\n{res.stderr}")
+        os.replace(str(out) + ".tmp", out)
+        if verbose:
+            print(f"[mxstream.build] linked {out}")
+    return out
+
+
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--sanitize", action="store_true",
                     help="build the ASan/UBSan host harness (build/sanitize/mxs_sanitize)")
+    ap.add_argument("--capi", action="store_true",
+                    help="build the C ABI library build/lib/libmxstream.so (csrc/mxs_c.h)")
     a = ap.parse_args(argv)
+    if a.capi:
+        print(build_capi(verbose=True))
+        return 0
     if a.sanitize:
         print(build_sanitize(verbose=True))
         return 0
