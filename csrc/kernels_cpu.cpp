@@ -73,7 +73,7 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
       qmax = std::max(qmax, q);
     }
     ++nacc;
-    const int32_t jh = p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
+    const int32_t jh = p.nranks == 1 ? 0 : p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
     const uint32_t b = bucket_of(key, jh, p, kg_dest);
     const uint32_t pos = cursor[b]++;
     if (pos >= p.bucket_cap) {

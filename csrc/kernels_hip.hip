@@ -127,7 +127,7 @@ __device__ __forceinline__ PartEval part_eval(uint64_t key, int64_t ts, const in
       return e;
     }
   }
-  const int32_t jh = p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
+  const int32_t jh = p.nranks == 1 ? 0 : p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
   e.bucket = bucket_of(key, jh, p, kg_dest);
   return e;
 }
@@ -626,7 +626,8 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
     for (int u = 0; u < kPartU; ++u) {
       const int64_t i = i0 + (int64_t)u * blockDim.x;
       if (i >= end) break;
-      const int32_t jh = plan.hash_mode ? jhash_tab[k[u]] : java_long_hash((int64_t)k[u]);
+      const int32_t jh = plan.nranks == 1 ? 0
+                         : plan.hash_mode ? jhash_tab[k[u]] : java_long_hash((int64_t)k[u]);
       atomicAdd(&run_base[bucket_of(k[u], jh, plan, kg_dest)], 1u);
     }
   }

@@ -361,9 +361,10 @@ struct PartPlan {
 };
 
 MXS_HD uint32_t bucket_of(uint64_t key, int32_t jhash, const PartPlan& p, const int32_t* kg_dest) {
+  const uint32_t sub = p.nsub_log2 == 0 ? 0u : (uint32_t)(mix64(key) >> (64 - p.nsub_log2));
+  if (p.nranks == 1) return sub;  // one rank owns every key group: no Java hash / murmur needed
   const int32_t kg = key_group_of_hash(jhash, p.max_parallelism);
   const int32_t dest = kg_dest[kg];
-  const uint32_t sub = p.nsub_log2 == 0 ? 0u : (uint32_t)(mix64(key) >> (64 - p.nsub_log2));
   return ((uint32_t)dest << p.nsub_log2) | sub;
 }
 
