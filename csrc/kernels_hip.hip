@@ -915,18 +915,38 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
     }
     __syncthreads();
     // Write back the deltas of touched slots (this workgroup owns these slots: plain RMW).
-    for (uint32_t i = threadIdx.x; i < (uint32_t)npg * cap; i += blockDim.x) {
-      const uint32_t dc = scnt[i];
-      if (!dc) continue;
-      const uint32_t q = i >> p.cap_log2;
-      const uint32_t s = i & mask;
-      const int64_t pane = p.pane_base + q0 + q;
-      const size_t gi = (size_t)(pane & (p.ring - 1)) * nslots + sbase + s;
-      const uint64_t d = lds_export<AGG>(sacc[i]);
-      const uint32_t oc = cnt_g[gi];
-      if (AGG != AGG_COUNT) acc_g[gi] = oc ? agg_combine(AGG, acc_g[gi], d) : d;
-      cnt_g[gi] = oc + dc;
-      if (pane <= p.fired_hi) dirty_g[gi] = 1;
+    // kWB slots per thread per batch: all their state loads are issued before the first
+    // combine, so the read-modify-write costs one memory latency per batch instead of one per
+    // slot (a slot-at-a-time loop serialised 8 dependent HBM round trips per thread).
+    constexpr int kWB = 8;
+    const uint32_t nrow = (uint32_t)npg * cap;
+    for (uint32_t i0 = threadIdx.x; i0 < nrow; i0 += blockDim.x * kWB) {
+      uint32_t dc[kWB], oc[kWB];
+      uint64_t oa[kWB];
+      size_t gi[kWB];
+#pragma unroll
+      for (int w = 0; w < kWB; ++w) {
+        const uint32_t i = i0 + (uint32_t)w * blockDim.x;
+        dc[w] = i < nrow ? scnt[i] : 0u;
+        oc[w] = 0;
+        oa[w] = 0;
+        gi[w] = 0;
+        if (dc[w]) {
+          const int64_t pane = p.pane_base + q0 + (i >> p.cap_log2);
+          gi[w] = (size_t)(pane & (p.ring - 1)) * nslots + sbase + (i & mask);
+          oc[w] = cnt_g[gi[w]];
+          if (AGG != AGG_COUNT) oa[w] = acc_g[gi[w]];
+        }
+      }
+#pragma unroll
+      for (int w = 0; w < kWB; ++w) {
+        if (!dc[w]) continue;
+        const uint32_t i = i0 + (uint32_t)w * blockDim.x;
+        const uint64_t d = lds_export<AGG>(sacc[i]);
+        if (AGG != AGG_COUNT) acc_g[gi[w]] = oc[w] ? agg_combine(AGG, oa[w], d) : d;
+        cnt_g[gi[w]] = oc[w] + dc[w];
+        if (p.pane_base + q0 + (int64_t)(i >> p.cap_log2) <= p.fired_hi) dirty_g[gi[w]] = 1;
+      }
     }
     __syncthreads();
   }

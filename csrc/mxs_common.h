@@ -373,6 +373,19 @@ MXS_HD uint32_t bucket_of(uint64_t key, int32_t jhash, const PartPlan& p, const 
 MXS_HD bool rel_pane(int64_t ts, const PartPlan& p, uint32_t* t_out, int64_t* pane_abs_rel) {
   const int64_t d = ts - p.tbase;
   if (d < 0 || d >= (int64_t)1 << 52) return false;
+  if (d < ((int64_t)1 << 31) && p.pane < ((int64_t)1 << 31)) {
+    // 32-bit fast path (the common case: a step spans < 24 days of event time): u32 -> f64
+    // conversion, one f64 multiply, f64 -> u32, one 32-bit multiply for the +-1 correction —
+    // instead of the 64-bit integer <-> f64 conversion sequences (the partition is VALU-bound).
+    const uint32_t du = (uint32_t)d, pu = (uint32_t)p.pane;
+    uint32_t q = (uint32_t)((double)du * p.inv_pane);
+    const uint32_t qp = q * pu;  // <= du + pu < 2^32
+    if (qp > du) --q;
+    else if (du - qp >= pu) ++q;
+    *t_out = q;
+    *pane_abs_rel = q;
+    return true;
+  }
   const int64_t q = fast_floor_div_pos(d, p.pane, p.inv_pane);
   if (q >= ((int64_t)1 << 32)) return false;
   *t_out = (uint32_t)q;
