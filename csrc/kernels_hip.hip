@@ -582,7 +582,7 @@ constexpr int kCU = 2;                   // events per thread per round
 constexpr int kCR = 1024 * kCU;          // records per round
 constexpr int kCG = 4;                   // reservation granularity (records per 64-byte sector)
 constexpr int kCMaxNb = 512;
-constexpr size_t kCompactLds = (size_t)kCR * sizeof(RecC) + (size_t)kCMaxNb * 5 * 4 + 20 * 4 +
+constexpr size_t kCompactLds = (size_t)kCR * sizeof(RecC) + (size_t)kCMaxNb * 6 * 4 + 20 * 4 +
                                16 * 8 + (size_t)kCR * 2;
 static_assert(kCompactLds <= 80 * 1024, "compact partition must fit two workgroups per CU");
 
@@ -604,6 +604,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   uint32_t* wsum = roff + kCMaxNb;                             // 17 scan words (+pad)
   int64_t* lred = (int64_t*)(wsum + 20);                       // 16 x i64
   uint16_t* sbk = (uint16_t*)(lred + 16);                      // [kCR] bucket of rbuf[j]
+  uint32_t* dbase = (uint32_t*)(sbk + kCR);                    // [kCMaxNb] round's dest - offset
 
   for (int b = threadIdx.x; b < kCMaxNb; b += blockDim.x) {
     run_base[b] = 0;
@@ -650,7 +651,8 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   const bool any_ovf = wsum[18] != 0;
   const uint32_t bcap = plan.bucket_cap;
 
-  int64_t tmax = INT64_MIN, qmin = INT64_MAX, qmax = INT64_MIN, nlate = 0, nacc = 0;
+  int64_t tmax = INT64_MIN, nlate = 0, nacc = 0;
+  uint32_t qmin32 = 0xFFFFFFFFu, qmax32 = 0;  // relative panes are u32: 32-bit min/max per event
   int64_t flags = 0;
   // Pass B: rounds of kCR records -> LDS counting sort by bucket -> cooperative run writes.
   for (int64_t r0 = start; r0 < end; r0 += kCR) {
@@ -677,9 +679,8 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
           flags |= 2;
         } else {
           if ((int64_t)(int32_t)v != (int64_t)v) flags |= 4;  // needs 24-byte records
-          ++nacc;
-          qmin = (int64_t)e.t < qmin ? (int64_t)e.t : qmin;
-          qmax = (int64_t)e.t > qmax ? (int64_t)e.t : qmax;
+          qmin32 = e.t < qmin32 ? e.t : qmin32;
+          qmax32 = e.t > qmax32 ? e.t : qmax32;
           keep[u] = true;
           bk[u] = e.bucket;
           rec[u] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), (uint32_t)v, e.t);
@@ -690,7 +691,12 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
     __syncthreads();
     const uint32_t myc = threadIdx.x < (unsigned)nb ? rcnt[threadIdx.x] : 0u;
     const uint32_t off = block_exclusive_scan(myc, wsum);
-    if (threadIdx.x < (unsigned)nb) roff[threadIdx.x] = off;
+    if (threadIdx.x < (unsigned)nb) {
+      roff[threadIdx.x] = off;
+      // Record j of this round (bucket b) goes to out[b * bcap + run_base[b] + lcnt[b] + j -
+      // roff[b]]: one per-bucket base (mod 2^32) so the flush does one LDS lookup per record.
+      dbase[threadIdx.x] = threadIdx.x * bcap + run_base[threadIdx.x] + lcnt[threadIdx.x] - off;
+    }
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < kCU; ++u)
@@ -701,12 +707,10 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
       }
     __syncthreads();
     const uint32_t nrec = wsum[16];
+    nacc += threadIdx.x == 0 ? nrec : 0u;
     if (!any_ovf) {
-      for (uint32_t j = threadIdx.x; j < nrec; j += blockDim.x) {
-        const uint32_t b = sbk[j];
-        const uint32_t pos = lcnt[b] + (j - roff[b]);
-        ((uint4*)(out + (size_t)b * bcap + run_base[b]))[pos] = rbuf[j];
-      }
+      uint4* out4 = (uint4*)out;
+      for (uint32_t j = threadIdx.x; j < nrec; j += blockDim.x) out4[dbase[sbk[j]] + j] = rbuf[j];
     }
     __syncthreads();
     if (threadIdx.x < (unsigned)nb) {
@@ -724,10 +728,11 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
     for (uint32_t w = lcnt[b]; w < resv[b]; ++w) dst[w] = hole;
   }
 
+  int64_t qmin = qmin32 == 0xFFFFFFFFu && qmax32 == 0 ? INT64_MAX : (int64_t)qmin32;
+  int64_t qmax = qmin == INT64_MAX ? INT64_MIN : (int64_t)qmax32;
   tmax = block_reduce_i64(tmax, lred, 0);
   qmin = block_reduce_i64(qmin, lred, 1);
   qmax = block_reduce_i64(qmax, lred, 0);
-  nacc = block_reduce_i64(nacc, lred, 2);
   if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
   flags = (any_ovf ? 1 : 0) | block_reduce_i64(flags & 2, lred, 0) |
           block_reduce_i64(flags & 4, lred, 0);
@@ -2205,7 +2210,7 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap,
                intptr_t stream) {
   const int nb = plan.nranks << plan.nsub_log2;
-  if (plan.rec_words == 2 && nb <= kCMaxNb) {
+  if (plan.rec_words == 2 && nb <= kCMaxNb && (uint64_t)nb * plan.bucket_cap < (1ull << 32)) {
     if (n <= 0) return;
     // 32K events per workgroup: two workgroups per CU (LDS ~72 KB each) at 16M events.
     const int blocks = grid_for(n, 32768, 2048);
