@@ -322,7 +322,7 @@ void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
   const uint32_t mask = (1u << cap_log2) - 1;
   for (int64_t i = 0; i < n; ++i) {
     const uint64_t key = keys[i];
-    const uint64_t sub = nsub_log2 == 0 ? 0 : (mix64(key) >> (64 - nsub_log2));
+    const uint64_t sub = sub_table_of(key, nsub_log2);
     uint64_t* t = keys_g + (sub << cap_log2);
     uint32_t s = (uint32_t)mix64(key) & mask;
     int64_t found = -1;

@@ -655,18 +655,45 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   uint32_t qmin32 = 0xFFFFFFFFu, qmax32 = 0;  // relative panes are u32: 32-bit min/max per event
   int64_t flags = 0;
   // Pass B: rounds of kCR records -> LDS counting sort by bucket -> cooperative run writes.
+  // Software-pipelined: the next round's (key, ts, value) loads are issued before this round's
+  // LDS sort and flush, so the HBM latency is not exposed once per round (16 rounds/group).
+  uint64_t nk[kCU], nv[kCU];
+  int64_t nt[kCU];
+#pragma unroll
+  for (int u = 0; u < kCU; ++u) {
+    const int64_t i = start + (int64_t)u * blockDim.x + threadIdx.x;
+    if (i < end) {
+      nk[u] = ldin<V>(&keys[i]);
+      nt[u] = ldin<V>(&ts[i]);
+      nv[u] = ldin<V>(&vals[i]);
+    }
+  }
   for (int64_t r0 = start; r0 < end; r0 += kCR) {
     uint32_t bk[kCU], rk[kCU];
     uint4 rec[kCU];
     bool keep[kCU];
+    uint64_t ck[kCU], cv[kCU];
+    int64_t ct[kCU];
+#pragma unroll
+    for (int u = 0; u < kCU; ++u) {
+      ck[u] = nk[u];
+      ct[u] = nt[u];
+      cv[u] = nv[u];
+      const int64_t i = r0 + kCR + (int64_t)u * blockDim.x + threadIdx.x;
+      if (i < end) {
+        nk[u] = ldin<V>(&keys[i]);
+        nt[u] = ldin<V>(&ts[i]);
+        nv[u] = ldin<V>(&vals[i]);
+      }
+    }
 #pragma unroll
     for (int u = 0; u < kCU; ++u) {
       const int64_t i = r0 + (int64_t)u * blockDim.x + threadIdx.x;
       keep[u] = false;
       if (i < end) {
-        const uint64_t k = ldin<V>(&keys[i]);
-        const int64_t t = ldin<V>(&ts[i]);
-        const uint64_t v = ldin<V>(&vals[i]);
+        const uint64_t k = ck[u];
+        const int64_t t = ct[u];
+        const uint64_t v = cv[u];
         tmax = t > tmax ? t : tmax;
         const PartEval e = part_eval(k, t, jhash_tab, plan, kg_dest);
         if (e.kind == 1) {
@@ -2129,7 +2156,7 @@ __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t* __res
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t key = keys[i];
-    const uint64_t sub = nsub_log2 == 0 ? 0 : (mix64(key) >> (64 - nsub_log2));
+    const uint64_t sub = sub_table_of(key, nsub_log2);
     const uint32_t s = global_probe_insert(keys_g + (sub << cap_log2), key, mask);
     slots[i] = s == kNoSlot ? -1 : (int64_t)((sub << cap_log2) | s);
   }

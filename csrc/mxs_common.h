@@ -93,9 +93,9 @@ MXS_HD int32_t operator_index(int32_t key_group, int32_t parallelism, int32_t ma
   return (int32_t)(((int64_t)key_group * parallelism) / max_parallelism);
 }
 
-// splitmix64 finaliser: the engine-internal hash that picks the sub-table (top bits) and the
-// probe start (low bits) — independent of the Flink key-group hash so that every rank's
-// sub-tables stay balanced whatever key groups it owns.
+// splitmix64 finaliser: the engine-internal hash that picks a key's probe start in its sub-table
+// (low bits; the sub-table itself comes from sub_table_of) — independent of the Flink key-group
+// hash so that every rank's sub-tables stay balanced whatever key groups it owns.
 MXS_HD uint64_t mix64(uint64_t x) {
   x += 0x9e3779b97f4a7c15ull;
   x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -360,8 +360,20 @@ struct PartPlan {
   int32_t rec_words;         // 3: 24-byte Rec; 2: 16-byte RecC (int32 values, GPU window path)
 };
 
+// Sub-table of a key: a 32-bit multiplicative hash of both key halves (3 32-bit multiplies).
+// Independent of the slot hash (low bits of mix64) and about half the VALU of a second mix64 —
+// the partition pass evaluates it twice per event and is VALU-bound.
+MXS_HD uint32_t sub_table_of(uint64_t key, int nsub_log2) {
+  if (nsub_log2 == 0) return 0u;
+  uint32_t h = (uint32_t)key * 0x9E3779B1u ^ (uint32_t)(key >> 32) * 0x85EBCA77u;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 13;
+  return h >> (32 - nsub_log2);
+}
+
 MXS_HD uint32_t bucket_of(uint64_t key, int32_t jhash, const PartPlan& p, const int32_t* kg_dest) {
-  const uint32_t sub = p.nsub_log2 == 0 ? 0u : (uint32_t)(mix64(key) >> (64 - p.nsub_log2));
+  const uint32_t sub = sub_table_of(key, p.nsub_log2);
   if (p.nranks == 1) return sub;  // one rank owns every key group: no Java hash / murmur needed
   const int32_t kg = key_group_of_hash(jhash, p.max_parallelism);
   const int32_t dest = kg_dest[kg];
