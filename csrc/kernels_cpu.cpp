@@ -124,7 +124,7 @@ void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int3
 }
 
 static inline uint32_t probe_insert(uint64_t* keys, uint64_t key, uint32_t mask, bool* inserted) {
-  uint32_t s = (uint32_t)mix64(key) & mask;
+  uint32_t s = slot_hash(key) & mask;
   for (uint32_t i = 0; i <= mask; ++i) {
     const uint64_t k = keys[s];
     if (k == key) return s;
@@ -324,7 +324,7 @@ void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
     const uint64_t key = keys[i];
     const uint64_t sub = sub_table_of(key, nsub_log2);
     uint64_t* t = keys_g + (sub << cap_log2);
-    uint32_t s = (uint32_t)mix64(key) & mask;
+    uint32_t s = slot_hash(key) & mask;
     int64_t found = -1;
     for (uint32_t p = 0; p <= mask; ++p) {
       if (t[s] == key) {

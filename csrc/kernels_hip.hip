@@ -816,7 +816,7 @@ __global__ void step_finish_kernel(const int64_t* __restrict__ stats, int64_t* _
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t lds_probe_insert(uint64_t* skeys, uint64_t key, uint32_t mask,
                                                      int* inserted) {
-  uint32_t s = (uint32_t)mix64(key) & mask;
+  uint32_t s = slot_hash(key) & mask;
   for (uint32_t i = 0; i <= mask; ++i) {
     const uint64_t k = *((volatile uint64_t*)&skeys[s]);
     if (k == key) return s;
@@ -1236,7 +1236,7 @@ __global__ __launch_bounds__(256) void expr_filter_kernel(const double* __restri
 //                       state written back once per key.
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t global_probe_insert(uint64_t* keys, uint64_t key, uint32_t mask) {
-  uint32_t s = (uint32_t)mix64(key) & mask;
+  uint32_t s = slot_hash(key) & mask;
   for (uint32_t i = 0; i <= mask; ++i) {
     const uint64_t k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (k == key) return s;
@@ -1443,7 +1443,7 @@ __device__ __forceinline__ void set_insert(uint64_t* set, uint32_t mask, uint64_
 template <int kScope = __HIP_MEMORY_SCOPE_AGENT>
 __device__ __forceinline__ uint32_t sess_probe_insert(uint64_t* keys, uint64_t key, uint32_t mask,
                                                       uint32_t* inserted) {
-  const uint32_t s0 = (uint32_t)mix64(key) & mask;
+  const uint32_t s0 = slot_hash(key) & mask;
   for (;;) {
     uint32_t s = s0, tomb = kNoSlot, target = kNoSlot;
     for (uint32_t i = 0; i <= mask; ++i) {
@@ -1474,7 +1474,7 @@ __device__ __forceinline__ uint32_t sess_probe_insert(uint64_t* keys, uint64_t k
 // Read-only probe: the key's slot, or kNoSlot (first empty slot reached / table scanned).
 template <int kScope = __HIP_MEMORY_SCOPE_AGENT>
 __device__ __forceinline__ uint32_t sess_find(const uint64_t* keys, uint64_t key, uint32_t mask) {
-  uint32_t s = (uint32_t)mix64(key) & mask;
+  uint32_t s = slot_hash(key) & mask;
   for (uint32_t i = 0; i <= mask; ++i) {
     const uint64_t k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, kScope);
     if (k == key) return s;

@@ -3,7 +3,7 @@
 //
 // For every live slot s of sub-table `sub` holding key k:
 //   * placement : k belongs to this sub-table (sub_table_of(k) == sub; partition rule);
-//   * chain     : linear probing from k's home slot (mix64(k) & mask) reaches s without passing
+//   * chain     : linear probing from k's home slot (slot_hash(k) & mask) reaches s without passing
 //                 an empty slot (otherwise lookups of k would stop early and re-insert it);
 //   * unique    : no slot between the home slot and s holds k (a duplicate live key).
 // Tombstones (session tables) count as occupied for the chain rule, as in the probe loops.
@@ -24,9 +24,8 @@ MXS_HD uint32_t check_slot(const uint64_t* keys, uint32_t s, uint32_t mask, int 
                            uint32_t sub) {
   const uint64_t k = keys[s];
   uint32_t bad = 0;
-  const uint64_t h = mix64(k);
   if (nsub_log2 > 0 && sub_table_of(k, nsub_log2) != sub) bad |= 1u;
-  uint32_t i = (uint32_t)h & mask;
+  uint32_t i = slot_hash(k) & mask;
   for (uint32_t step = 0; step <= mask && i != s; ++step) {
     const uint64_t x = keys[i];
     if (x == kEmptyKey) {

@@ -372,6 +372,17 @@ MXS_HD uint32_t sub_table_of(uint64_t key, int nsub_log2) {
   return h >> (32 - nsub_log2);
 }
 
+// Home slot of a key inside its sub-table (low bits; linear probing from there): a second,
+// independent 32-bit hash (murmur3-style mix of both halves). Every keyed table kernel, its C++
+// twin and the invariant checker probe from this slot.
+MXS_HD uint32_t slot_hash(uint64_t key) {
+  uint32_t h = (uint32_t)key * 0xCC9E2D51u ^ (uint32_t)(key >> 32) * 0x1B873593u;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  return h;
+}
+
 MXS_HD uint32_t bucket_of(uint64_t key, int32_t jhash, const PartPlan& p, const int32_t* kg_dest) {
   const uint32_t sub = sub_table_of(key, p.nsub_log2);
   if (p.nranks == 1) return sub;  // one rank owns every key group: no Java hash / murmur needed

@@ -28,7 +28,7 @@ inline void load_vrec(const void* base, size_t idx, int rec_words, uint64_t& key
 }
 
 inline uint32_t vprobe(uint64_t* keys, uint64_t key, uint32_t mask, bool* inserted) {
-  uint32_t s = (uint32_t)mix64(key) & mask;
+  uint32_t s = slot_hash(key) & mask;
   for (uint32_t i = 0; i <= mask; ++i) {
     const uint64_t k = keys[s];
     if (k == key) return s;

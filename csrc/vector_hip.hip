@@ -50,7 +50,7 @@ constexpr uint32_t kHole = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint32_t vprobe_insert(uint64_t* skeys, uint64_t key, uint32_t mask,
                                                   int* inserted) {
-  uint32_t s = (uint32_t)mix64(key) & mask;
+  uint32_t s = slot_hash(key) & mask;
   for (uint32_t i = 0; i <= mask; ++i) {
     const uint64_t k = *((volatile uint64_t*)&skeys[s]);
     if (k == key) return s;
