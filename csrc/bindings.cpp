@@ -55,6 +55,7 @@ ExprProg make_prog(const std::vector<int32_t>& code, const std::vector<double>& 
   for (size_t i = 0; i < consts.size(); ++i) p.consts[i] = consts[i];
   p.ncode = (int32_t)(code.size() / 2);
   p.depth = depth;
+  p.chain = expr_is_chain(p) ? 1 : 0;
   return p;
 }
 
@@ -160,6 +161,18 @@ PYBIND11_MODULE(_mxs_native, m) {
     double v[kExprVars] = {0};
     for (size_t i = 0; i < vars.size() && i < (size_t)kExprVars; ++i) v[i] = vars[i];
     return expr_eval(p, v);
+  });
+  m.def("expr_is_chain", [](std::vector<int32_t> code, std::vector<double> consts) {
+    return make_prog(code, consts).chain != 0;
+  });
+  m.def("expr_eval_chain", [](std::vector<int32_t> code, std::vector<double> consts,
+                              std::vector<double> vars) {
+    ExprProg p = make_prog(code, consts);
+    if (!p.chain) throw std::invalid_argument("not a chain program");
+    double v[kExprVars] = {0};
+    for (size_t i = 0; i < vars.size() && i < (size_t)kExprVars; ++i) v[i] = vars[i];
+    ArrayVars va{v};
+    return expr_eval_chain(p, va);
   });
 
   // ---- GPU ----

@@ -1105,6 +1105,22 @@ struct LdsCol {
   __device__ __forceinline__ void set(int i, double x) { base[i * stride] = x; }
 };
 
+// Epilogue variables in registers (a switch over named values: no runtime-indexed array).
+struct RegVars {
+  double v0, v1, v2, v3, v4, v5, v6;
+  __device__ __forceinline__ double get(int i) const {
+    switch (i) {
+      case 0: return v0;
+      case 1: return v1;
+      case 2: return v2;
+      case 3: return v3;
+      case 4: return v4;
+      case 5: return v5;
+      default: return v6;
+    }
+  }
+};
+
 constexpr int kFireThreads = 1024;
 constexpr int kFireU = 4;  // slots per thread per round (ILP)
 
@@ -1122,6 +1138,7 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
   const int wid = threadIdx.x >> 6, nw = kFireThreads >> 6;
   const int64_t nslots = p.nslots;
   const int64_t per_round = (int64_t)kFireThreads * kFireU;
+  const bool chain_only = (!p.map.ncode || p.map.chain) && (!p.filt.ncode || p.filt.chain);
   // Rounds are block-uniform, so every lane reaches the barriers and the ballots.
   for (int64_t base = (int64_t)blockIdx.x * per_round; base < nslots;
        base += (int64_t)gridDim.x * per_round) {
@@ -1156,7 +1173,17 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
           const double v0 = agg_result_f64(p.agg, acc[u], cnt[u]);
           val[u] = v0;
           emit[u] = true;
-          if ((p.map.ncode || p.filt.ncode) && !(p.ablate & 1u)) {
+          if ((p.map.ncode || p.filt.ncode) && !(p.ablate & 1u) && chain_only) {
+            // Register-only epilogue (plan-uniform branch): no LDS stack / variable columns.
+            const RegVars rv{v0, (double)cnt[u], p.wstart, p.wend, (double)key[u],
+                             (double)(int64_t)acc[u], 0.0};
+            if (p.map.ncode) val[u] = expr_eval_chain(p.map, rv);
+            if (p.filt.ncode) {
+              RegVars rf = rv;
+              rf.v6 = val[u];
+              emit[u] = expr_eval_chain(p.filt, rf) != 0.0;
+            }
+          } else if ((p.map.ncode || p.filt.ncode) && !(p.ablate & 1u)) {
             vars.set(0, v0);
             vars.set(1, (double)cnt[u]);
             vars.set(2, p.wstart);

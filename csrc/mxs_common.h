@@ -258,6 +258,7 @@ struct ExprProg {
   double consts[kExprMaxConst];
   int32_t ncode;               // number of (op,arg) pairs; 0 = empty program
   int32_t depth;               // max stack depth (validated on the host)
+  int32_t chain;               // 1: "VAR, (CONST|VAR, binop)*" — evaluated without a stack
 };
 
 // The VM is templated on where its stack lives: a local array on the host, a per-lane LDS
@@ -312,6 +313,58 @@ MXS_HD double expr_eval_t(const ExprProg& p, Stack& st, const Vars& vars) {
     }
   }
   return sp > 0 ? st.get(sp - 1) : 0.0;
+}
+
+// Binary op of the VM (shared by the stack VM's semantics and the chain evaluator).
+MXS_HD double expr_binop(int32_t op, double a, double b) {
+  switch (op) {
+    case OP_ADD: return a + b;
+    case OP_SUB: return a - b;
+    case OP_MUL: return a * b;
+    case OP_DIV: return a / b;
+    case OP_LT: return a < b;
+    case OP_LE: return a <= b;
+    case OP_GT: return a > b;
+    case OP_GE: return a >= b;
+    case OP_EQ: return a == b;
+    case OP_NE: return a != b;
+    case OP_AND: return (a != 0.0) && (b != 0.0);
+    case OP_OR: return (a != 0.0) || (b != 0.0);
+    case OP_MIN: return a < b ? a : b;
+    case OP_MAX: return a > b ? a : b;
+#if defined(__HIP_DEVICE_COMPILE__)
+    case OP_MOD: return fmod(a, b);
+#else
+    case OP_MOD: return __builtin_fmod(a, b);
+#endif
+    default: return 0.0;
+  }
+}
+
+// Stack-free evaluation of chain programs (the traced epilogues of the reference jobs:
+// `sum * 8.0 / 60 / 1024 / 1024`, `mbps < 100.0`): the running value is the left operand of
+// every binop, so it stays in a register — the same double ops in the same order as the VM
+// (bit-identical results), without the VM's per-op LDS stack traffic.
+template <class Vars>
+MXS_HD double expr_eval_chain(const ExprProg& p, const Vars& vars) {
+  double x = vars.get(p.code[1]);
+  for (int i = 1; i + 1 < p.ncode; i += 2) {
+    const int32_t pop = p.code[2 * i], parg = p.code[2 * i + 1];
+    const double b = pop == OP_CONST ? p.consts[parg] : vars.get(parg);
+    x = expr_binop(p.code[2 * (i + 1)], x, b);
+  }
+  return x;
+}
+
+// Host-side classification (bindings: make_prog).
+inline bool expr_is_chain(const ExprProg& p) {
+  if (p.ncode < 1 || p.code[0] != OP_VAR || (p.ncode - 1) % 2 != 0) return false;
+  for (int i = 1; i < p.ncode; i += 2) {
+    const int32_t pop = p.code[2 * i], op = p.code[2 * (i + 1)];
+    if (pop != OP_CONST && pop != OP_VAR) return false;
+    if (op < OP_ADD || op > OP_MOD || op == OP_NOT || op == OP_NEG || op == OP_ABS) return false;
+  }
+  return true;
 }
 
 struct ArrayVars {

@@ -22,7 +22,7 @@ import torch
 
 from ..ops import kernels as K
 from ..ops import vector as V
-from .window_operator import FireResult, KeyedWindowOperator, _next_pow2
+from .window_operator import FireResult, KeyedWindowOperator, _next_pow2, to_host_arrays
 
 I64_MIN = K.I64_MIN
 
@@ -130,9 +130,8 @@ class VectorWindowOperator(KeyedWindowOperator):
             return None
         n = min(n, self.out_keys.numel())
         self.metrics.num_records_out += n
-        keys = self.out_keys[:n].cpu().numpy().copy()
-        vecs = self.out_vec[:n * self.dim].cpu().numpy().reshape(n, self.dim).copy()
-        cnts = self.out_cnt[:n].cpu().numpy().copy()
+        keys, cnts = to_host_arrays([self.out_keys, self.out_cnt], n)
+        vecs = to_host_arrays([self.out_vec], n * self.dim)[0].reshape(n, self.dim)
         return FireResult(s, s + self.size, keys.view(np.uint64), vecs,
                           np.zeros(n, dtype=np.int64), cnts, refire=only_dirty)
 
