@@ -496,6 +496,18 @@ void write_kg_file(const std::string& path, const std::string& header, uint32_t 
                    uint32_t kg_hi, py::array_t<int32_t, py::array::c_style> kg, py::list columns) {
   const size_t n = (size_t)kg.size();
   const int32_t* kgp = kg.data();
+  // Pin every column (contiguous views kept alive here) while holding the GIL, then do the
+  // counting sort, the row permutation and the file I/O without it: an asynchronous checkpoint
+  // writes from a worker thread while the step loop keeps running Python.
+  std::vector<py::array> keep;
+  std::vector<std::pair<const char*, size_t>> cols;
+  for (auto h : columns) {
+    py::array a = py::reinterpret_borrow<py::array>(h);
+    if ((size_t)a.size() != n) throw std::invalid_argument("column length mismatch");
+    keep.push_back(py::array::ensure(a, py::array::c_style));
+    cols.emplace_back((const char*)keep.back().data(), (size_t)keep.back().itemsize());
+  }
+  py::gil_scoped_release nogil;
   const uint32_t ngroups = kg_hi - kg_lo + 1;
   std::vector<uint64_t> off(ngroups + 1, 0);
   for (size_t i = 0; i < n; ++i) {
@@ -520,12 +532,7 @@ void write_kg_file(const std::string& path, const std::string& header, uint32_t 
   f.write((const char*)&kg_hi, 4);
   f.write((const char*)off.data(), (std::streamsize)(off.size() * 8));
   std::vector<char> tmpbuf;
-  for (auto h : columns) {
-    py::array a = py::reinterpret_borrow<py::array>(h);
-    if ((size_t)a.size() != n) throw std::invalid_argument("column length mismatch");
-    py::array ac = py::array::ensure(a, py::array::c_style);
-    const size_t isz = (size_t)ac.itemsize();
-    const char* src = (const char*)ac.data();
+  for (const auto& [src, isz] : cols) {
     tmpbuf.resize(n * isz);
     for (size_t i = 0; i < n; ++i) std::memcpy(&tmpbuf[i * isz], src + perm[i] * isz, isz);
     f.write(tmpbuf.data(), (std::streamsize)tmpbuf.size());

@@ -51,6 +51,34 @@ class OperatorSnapshot:
     meta: dict = field(default_factory=dict)
 
 
+def freeze_operator(op, tensor_names: tuple[str, ...]):
+    """Synchronous phase of an async snapshot: a shallow copy of ``op`` whose state tensors are
+    device-side clones (HBM-speed copies enqueued on the current stream, ordered after every
+    kernel that wrote the state) and whose metrics are copied. Returns a thunk that runs the
+    operator's ordinary ``snapshot_state`` on the frozen copy — safe to call from another thread
+    on another stream while ``op`` keeps processing micro-batches."""
+    import copy
+
+    import torch
+
+    frozen = copy.copy(op)
+    frozen.metrics = copy.copy(op.metrics)
+    for name in tensor_names:
+        setattr(frozen, name, getattr(op, name).clone())
+    ev = None
+    dev = getattr(op, "device", None)
+    if dev is not None and torch.device(dev).type == "cuda":
+        ev = torch.cuda.Event()
+        ev.record()
+
+    def run():
+        if ev is not None:
+            torch.cuda.current_stream().wait_event(ev)
+        return type(op).snapshot_state(frozen)
+
+    return run
+
+
 def _dtype_str(a: np.ndarray) -> str:
     return np.dtype(a.dtype).str
 
@@ -169,6 +197,7 @@ class CheckpointCoordinator:
         if done:
             self.next_id = int(done[-1].name[4:]) + 1
         self.stats: list[dict] = []
+        self._pending: dict | None = None
 
     # ---- triggering --------------------------------------------------------------------
     def maybe_trigger(self, step: int, sources: dict | None = None) -> Path | None:
@@ -178,6 +207,7 @@ class CheckpointCoordinator:
 
     def trigger(self, step: int, sources: dict | None = None, extra: dict | None = None) -> Path:
         """Checkpoint chk-<next id> (all ranks call this at the same step)."""
+        self.complete_pending()
         if self.rank == 0:
             self.storage.init_job_dirs()
         d = self.storage.checkpoint_dir(self.next_id)
@@ -190,6 +220,7 @@ class CheckpointCoordinator:
     def savepoint(self, step: int, target: str | None = None, sources: dict | None = None,
                   extra: dict | None = None) -> Path:
         """Savepoint (all ranks must pass the same `target`; rank 0's directory name wins)."""
+        self.complete_pending()
         d = self.storage.new_savepoint_dir(target)
         name = [d.name]
         if self.world > 1:
@@ -232,6 +263,112 @@ class CheckpointCoordinator:
                            "ms": (time.perf_counter() - t0) * 1e3, "bytes": nbytes})
         return meta
 
+    # ---- asynchronous checkpoints (SURVEY.md §5.4 "async mode") -----------------------------
+    def trigger_async(self, step: int, sources: dict | None = None,
+                      extra: dict | None = None) -> None:
+        """Start chk-<next id> without stalling the step loop.
+
+        Synchronous part (this call, between two micro-batches): every operator freezes its
+        state (``snapshot_state_async``: device-to-device copies of the tables at HBM speed, plus
+        the host bookkeeping). Asynchronous part (a worker thread, on its own HIP stream): the
+        key-group export, the D2H copies and the state files, overlapped with the next steps.
+        ``complete_pending()`` (called by the next trigger, or explicitly at a step boundary /
+        end of job) joins the worker and runs the cross-rank acknowledgement — metadata gather,
+        ``_metadata`` written atomically by rank 0, barrier — on the calling thread, so the
+        process group is never used from two threads. Until then the checkpoint has no
+        ``_metadata`` and is not restorable (Flink's pending checkpoint)."""
+        import threading
+
+        self.complete_pending()
+        t0 = time.perf_counter()
+        if self.rank == 0:
+            self.storage.init_job_dirs()
+        d = self.storage.checkpoint_dir(self.next_id)
+        d.mkdir(parents=True, exist_ok=True)
+        frozen = {uid: (op.snapshot_state_async() if hasattr(op, "snapshot_state_async")
+                        else (lambda s=op.snapshot_state(): s))
+                  for uid, op in self.ops.items()}
+        result: dict = {}
+        cuda_dev = next((op.device for op in self.ops.values()
+                         if getattr(getattr(op, "device", None), "type", "cpu") == "cuda"), None)
+
+        def work():
+            import contextlib
+
+            try:
+                op_meta, nbytes = {}, 0
+                ctx = contextlib.ExitStack()
+                if cuda_dev is not None:
+                    import torch
+
+                    # The current device is per thread: pin it, then export on a side stream.
+                    ctx.enter_context(torch.cuda.device(cuda_dev))
+                    ctx.enter_context(torch.cuda.stream(torch.cuda.Stream(cuda_dev)))
+                with ctx:
+                    for uid, fn in frozen.items():
+                        snap = fn()
+                        fname = write_operator_file(d, uid, self.rank, snap, self.max_parallelism)
+                        # make the data durable here, off the step loop, so the _metadata
+                        # fsync in complete_pending() does not flush it on the caller's thread
+                        fd = os.open(d / fname, os.O_RDONLY)
+                        try:
+                            os.fsync(fd)
+                        finally:
+                            os.close(fd)
+                        nbytes += sum(v.nbytes for v in snap.columns.values())
+                        op_meta[uid] = {"meta": snap.meta, "rows": int(len(snap.kg)),
+                                        "file": fname}
+                result.update(op_meta=op_meta, nbytes=nbytes, t_done=time.perf_counter())
+            except BaseException as e:  # surfaced by complete_pending()
+                result["error"] = e
+
+        th = threading.Thread(target=work, name=f"mxs-ckpt-{self.next_id}", daemon=True)
+        th.start()
+        self._pending = {"thread": th, "result": result, "dir": d, "step": step,
+                         "sources": sources, "extra": extra, "id": self.next_id, "t0": t0,
+                         "sync_ms": (time.perf_counter() - t0) * 1e3}
+        self.next_id += 1
+
+    def pending_done(self) -> bool:
+        """True when this rank's export of the pending checkpoint has finished (local only:
+        ranks must still agree on the step at which they call ``complete_pending``)."""
+        return self._pending is not None and not self._pending["thread"].is_alive()
+
+    def complete_pending(self) -> Path | None:
+        """Finish the pending async checkpoint (if any); returns its directory."""
+        import threading
+
+        p = getattr(self, "_pending", None)
+        if p is None:
+            return None
+        self._pending = None
+        p["thread"].join()
+        res = p["result"]
+        if "error" in res:
+            raise RuntimeError(f"async checkpoint {p['id']} failed") from res["error"]
+        d = p["dir"]
+        gathered = self._gather({"rank": self.rank, "ops": res["op_meta"],
+                                 "sources": p["sources"] or {}, "bytes": res["nbytes"]})
+        if self.rank == 0:
+            ops_all = {uid: {"files": [g["ops"][uid]["file"] for g in gathered],
+                             "rows": [g["ops"][uid]["rows"] for g in gathered],
+                             "meta": gathered[0]["ops"][uid]["meta"]} for uid in self.ops}
+            meta = {"format": FORMAT, "type": "checkpoint", "job_id": self.storage.job_id,
+                    "checkpoint_id": p["id"], "step": int(p["step"]),
+                    "timestamp_ms": int(time.time() * 1000), "world": self.world,
+                    "max_parallelism": self.max_parallelism, "operators": ops_all,
+                    "sources": [g["sources"] for g in gathered], "extra": p["extra"] or {},
+                    "async": True}
+            _atomic_write_json(d / META, meta)
+        self.comm.barrier()
+        if self.rank == 0:
+            threading.Thread(target=self._prune, name="mxs-ckpt-prune", daemon=True).start()
+        self.stats.append({"dir": str(d), "type": "checkpoint-async", "step": p["step"],
+                           "ms": (time.perf_counter() - p["t0"]) * 1e3,
+                           "sync_ms": p["sync_ms"], "bytes": res["nbytes"],
+                           "export_ms": (res["t_done"] - p["t0"]) * 1e3})
+        return d
+
     def _gather(self, obj: dict) -> list[dict]:
         if self.world == 1:
             return [obj]
@@ -252,6 +389,7 @@ class CheckpointCoordinator:
 
         Works at any world size: each rank reads the key groups it now owns from all old files.
         Returns the metadata (source offsets etc. are the caller's to apply)."""
+        self.complete_pending()
         d = Path(path) if path is not None else self.storage.latest()
         if d is None:
             raise FileNotFoundError("no completed checkpoint")

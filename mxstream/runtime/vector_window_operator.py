@@ -146,6 +146,8 @@ class VectorWindowOperator(KeyedWindowOperator):
                 raise ValueError(f"checkpoint {k}={meta[k]!r} does not match operator "
                                  f"{getattr(self, k)!r}")
 
+    _state_tensors = ("keys_g", "vacc_g", "cnt_g", "dirty_g")
+
     def snapshot_state(self):
         """Live (key, pane) vectors grouped by key group; the vector column is stored as one
         fixed-width binary field per row (dtype V<4*dim>)."""

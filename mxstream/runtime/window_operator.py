@@ -583,6 +583,14 @@ class KeyedWindowOperator:
                 raise ValueError(f"checkpoint {k}={meta[k]!r} does not match operator "
                                  f"{getattr(self, k)!r}")
 
+    _state_tensors = ("keys_g", "acc_g", "cnt_g", "dirty_g")
+
+    def snapshot_state_async(self):
+        """Freeze the state now (D2D copies), export it later: see checkpoint.freeze_operator."""
+        from .checkpoint import freeze_operator
+
+        return freeze_operator(self, self._state_tensors)
+
     def snapshot_state(self):
         """Live (key, pane) accumulators grouped by key group, plus the firing bookkeeping."""
         from .checkpoint import OperatorSnapshot

@@ -71,6 +71,66 @@ def test_window_checkpoint_restore_equals_uninterrupted(tmp_path):
     assert _fires(tail) == _fires(tail2)
 
 
+def _async_roundtrip(tmp_path, device):
+    """Async checkpoint at CUT while the next steps run: pending until complete_pending(), then
+    byte-identical rows to a synchronous checkpoint of the same step, and a restore from it
+    continues exactly like the uninterrupted run."""
+    op = _win(device=device)
+    storage = CheckpointStorage(tmp_path / "async", job_id="c" * 32)
+    coord = CheckpointCoordinator(storage, {"window": op})
+    ref = _win(device=device)
+    ref_coord = CheckpointCoordinator(CheckpointStorage(tmp_path / "sync", job_id="d" * 32),
+                                      {"window": ref})
+    tail = []
+    for s in range(STEPS):
+        out = op.process(*_batch(s, device=device))
+        ref.process(*_batch(s, device=device))
+        if s == CUT:
+            coord.trigger_async(s, sources={"next_step": s + 1})
+            sync_path = ref_coord.trigger(s)
+        if s == CUT + 1:
+            assert storage.latest() is None or coord._pending is None  # not restorable yet
+        if s == CUT + 2:
+            path = coord.complete_pending()
+            assert storage.latest() == path
+        if s > CUT:
+            tail += out
+    tail += op.finish()
+    meta = read_metadata(path)
+    assert meta["async"] and meta["step"] == CUT and meta["checkpoint_id"] == 1
+    a = (path / "window-0.kg").read_bytes()
+    b = (sync_path / "window-0.kg").read_bytes()
+    assert a == b
+    op2 = _win(device=device)
+    CheckpointCoordinator(storage, {"window": op2}).restore()
+    tail2 = []
+    for s in range(CUT + 1, STEPS):
+        tail2 += op2.process(*_batch(s, device=device))
+    tail2 += op2.finish()
+    assert _fires(tail) == _fires(tail2)
+    st = coord.stats[-1]
+    assert st["type"] == "checkpoint-async" and st["sync_ms"] <= st["ms"]
+
+
+def test_async_checkpoint_matches_sync(tmp_path):
+    _async_roundtrip(tmp_path, "cpu")
+
+
+def test_async_checkpoint_error_surfaces(tmp_path):
+    op = _win()
+    coord = CheckpointCoordinator(CheckpointStorage(tmp_path), {"window": op})
+    op.process(*_batch(0))
+
+    def boom():
+        raise OSError("disk full")
+
+    op.snapshot_state_async = lambda: boom
+    coord.trigger_async(0)
+    with pytest.raises(RuntimeError, match="async checkpoint 1 failed"):
+        coord.complete_pending()
+    assert coord.storage.latest() is None
+
+
 def test_retention_savepoint_and_incomplete(tmp_path):
     op = KeyedRollingOperator(agg=K.AGG_COUNT, device="cpu", max_keys=5000, batch_capacity=PER)
     storage = CheckpointStorage(tmp_path, job_id="0123456789abcdef" * 2)
@@ -252,6 +312,11 @@ def test_gpu_window_checkpoint_restores_on_cpu_and_gpu(tmp_path):
             t2 += op2.process(*_batch(s, device=dev))
         t2 += op2.finish()
         assert _fires(tail) == _fires(t2), dev
+
+
+@pytest.mark.gpu
+def test_gpu_async_checkpoint_matches_sync(tmp_path):
+    _async_roundtrip(tmp_path, "cuda")
 
 
 @pytest.mark.gpu

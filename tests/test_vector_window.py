@@ -113,6 +113,15 @@ def test_checkpoint_roundtrip_cpu(tmp_path):
                               batch_capacity=6000, ooo_bound=400)
     op.process(*batches[0])
     snap = op.snapshot_state()
+    # the async freeze (D2D clones of the vector state) exports the same rows
+    frozen = op.snapshot_state_async()
+    op.process(*batches[1])  # mutate the live state after the freeze
+    snap_a = frozen()
+    for c in snap.columns:
+        assert snap.columns[c].tobytes() == snap_a.columns[c].tobytes(), c
+    op = VectorWindowOperator(dim=32, size=3000, device="cpu", max_keys=5000,
+                              batch_capacity=6000, ooo_bound=400)
+    op.process(*batches[0])
     name = write_operator_file(tmp_path, "vec", 0, snap, 128)
     rows = read_operator_rows(tmp_path, [name], 0, 127)
     op2 = VectorWindowOperator(dim=32, size=3000, device="cpu", max_keys=5000,
