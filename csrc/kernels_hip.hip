@@ -578,15 +578,19 @@ static_assert(kStagedLds <= 160 * 1024, "staged partition LDS image exceeds 160 
 //    carry/whole-group flush of the 24-byte kernel by ~3 % end to end.
 // A value outside int32 sets stats overflow bit 2: the host redoes the step with 24-byte records.
 // ------------------------------------------------------------------------------------------
-constexpr int kCU = 2;                   // events per thread per round
-constexpr int kCR = 1024 * kCU;          // records per round
+constexpr int kCU = 2;                   // events per thread per round (production)
 constexpr int kCG = 4;                   // reservation granularity (records per 64-byte sector)
 constexpr int kCMaxNb = 512;
-constexpr size_t kCompactLds = (size_t)kCR * sizeof(RecC) + (size_t)kCMaxNb * 6 * 4 + 20 * 4 +
-                               16 * 8 + (size_t)kCR * 2;
+constexpr size_t compact_lds(int cu) {
+  return (size_t)1024 * cu * sizeof(RecC) + (size_t)kCMaxNb * 6 * 4 + 20 * 4 + 16 * 8 +
+         (size_t)1024 * cu * 2;
+}
+constexpr size_t kCompactLds = compact_lds(kCU);
 static_assert(kCompactLds <= 80 * 1024, "compact partition must fit two workgroups per CU");
+constexpr int kCUProd = 4;               // production round: 4096 records, one group per CU
+static_assert(compact_lds(kCUProd) <= 160 * 1024, "compact partition LDS exceeds 160 KiB");
 
-template <int V>
+template <int V, int CU = kCU>
 __global__ __launch_bounds__(1024) void partition_compact_kernel(
     const uint64_t* __restrict__ keys, const int64_t* __restrict__ ts,
     const uint64_t* __restrict__ vals, const int32_t* __restrict__ jhash_tab, int64_t n,
@@ -595,16 +599,16 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
     uint32_t* __restrict__ late_idx, uint32_t late_cap) {
   extern __shared__ __attribute__((aligned(16))) unsigned char csm[];
   const int nb = plan.nranks << plan.nsub_log2;
-  uint4* rbuf = (uint4*)csm;                                   // [kCR] sorted round
-  uint32_t* run_base = (uint32_t*)(rbuf + kCR);                // [kCMaxNb]
+  uint4* rbuf = (uint4*)csm;                                   // [(1024 * CU)] sorted round
+  uint32_t* run_base = (uint32_t*)(rbuf + (1024 * CU));                // [kCMaxNb]
   uint32_t* resv = run_base + kCMaxNb;                         // reserved records per bucket
   uint32_t* lcnt = resv + kCMaxNb;                             // records written per bucket
   uint32_t* rcnt = lcnt + kCMaxNb;                             // this round's count per bucket
   uint32_t* roff = rcnt + kCMaxNb;                             // this round's offsets
   uint32_t* wsum = roff + kCMaxNb;                             // 17 scan words (+pad)
   int64_t* lred = (int64_t*)(wsum + 20);                       // 16 x i64
-  uint16_t* sbk = (uint16_t*)(lred + 16);                      // [kCR] bucket of rbuf[j]
-  uint32_t* dbase = (uint32_t*)(sbk + kCR);                    // [kCMaxNb] round's dest - offset
+  uint16_t* sbk = (uint16_t*)(lred + 16);                      // [(1024 * CU)] bucket of rbuf[j]
+  uint32_t* dbase = (uint32_t*)(sbk + (1024 * CU));                    // [kCMaxNb] round's dest - offset
 
   for (int b = threadIdx.x; b < kCMaxNb; b += blockDim.x) {
     run_base[b] = 0;
@@ -654,13 +658,13 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   int64_t tmax = INT64_MIN, nlate = 0, nacc = 0;
   uint32_t qmin32 = 0xFFFFFFFFu, qmax32 = 0;  // relative panes are u32: 32-bit min/max per event
   int64_t flags = 0;
-  // Pass B: rounds of kCR records -> LDS counting sort by bucket -> cooperative run writes.
+  // Pass B: rounds of (1024 * CU) records -> LDS counting sort by bucket -> cooperative run writes.
   // Software-pipelined: the next round's (key, ts, value) loads are issued before this round's
   // LDS sort and flush, so the HBM latency is not exposed once per round (16 rounds/group).
-  uint64_t nk[kCU], nv[kCU];
-  int64_t nt[kCU];
+  uint64_t nk[CU], nv[CU];
+  int64_t nt[CU];
 #pragma unroll
-  for (int u = 0; u < kCU; ++u) {
+  for (int u = 0; u < CU; ++u) {
     const int64_t i = start + (int64_t)u * blockDim.x + threadIdx.x;
     if (i < end) {
       nk[u] = ldin<V>(&keys[i]);
@@ -668,18 +672,18 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
       nv[u] = ldin<V>(&vals[i]);
     }
   }
-  for (int64_t r0 = start; r0 < end; r0 += kCR) {
-    uint32_t bk[kCU], rk[kCU];
-    uint4 rec[kCU];
-    bool keep[kCU];
-    uint64_t ck[kCU], cv[kCU];
-    int64_t ct[kCU];
+  for (int64_t r0 = start; r0 < end; r0 += (1024 * CU)) {
+    uint32_t bk[CU], rk[CU];
+    uint4 rec[CU];
+    bool keep[CU];
+    uint64_t ck[CU], cv[CU];
+    int64_t ct[CU];
 #pragma unroll
-    for (int u = 0; u < kCU; ++u) {
+    for (int u = 0; u < CU; ++u) {
       ck[u] = nk[u];
       ct[u] = nt[u];
       cv[u] = nv[u];
-      const int64_t i = r0 + kCR + (int64_t)u * blockDim.x + threadIdx.x;
+      const int64_t i = r0 + (1024 * CU) + (int64_t)u * blockDim.x + threadIdx.x;
       if (i < end) {
         nk[u] = ldin<V>(&keys[i]);
         nt[u] = ldin<V>(&ts[i]);
@@ -687,7 +691,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
       }
     }
 #pragma unroll
-    for (int u = 0; u < kCU; ++u) {
+    for (int u = 0; u < CU; ++u) {
       const int64_t i = r0 + (int64_t)u * blockDim.x + threadIdx.x;
       keep[u] = false;
       if (i < end) {
@@ -726,7 +730,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
     }
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < kCU; ++u)
+    for (int u = 0; u < CU; ++u)
       if (keep[u]) {
         const uint32_t j = roff[bk[u]] + rk[u];
         rbuf[j] = rec[u];
@@ -2266,12 +2270,25 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
   const int nb = plan.nranks << plan.nsub_log2;
   if (plan.rec_words == 2 && nb <= kCMaxNb && (uint64_t)nb * plan.bucket_cap < (1ull << 32)) {
     if (n <= 0) return;
-    // 32K events per workgroup: two workgroups per CU (LDS ~72 KB each) at 16M events.
-    const int blocks = grid_for(n, 32768, 2048);
+    // 4096-record rounds, up to 64K events per workgroup (one group per CU: 86 KB of LDS),
+    // i.e. one workgroup per CU at 16M events. Against 2048-record rounds / 32K events at two
+    // groups per CU (kbench, profiles/r1_partition_rounds.md): 227 -> 198 us. Longer bucket
+    // runs per group and bigger rounds cut the partial-sector writes and the per-group
+    // reservation work; fewer, larger groups beat the higher occupancy.
+    static bool attr = false;
+    if (!attr) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)partition_compact_kernel<1, kCUProd>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)compact_lds(kCUProd)));
+      attr = true;
+    }
+    const int64_t per = std::min<int64_t>(65536, std::max<int64_t>(4096, (n + 255) / 256));
+    const int blocks = grid_for(n, per, 4096);
     const int64_t chunk = (n + blocks - 1) / blocks;
-    hipLaunchKernelGGL(partition_compact_kernel<1>, dim3(blocks), dim3(1024), kCompactLds,
-                       (hipStream_t)stream, keys, ts, vals, jhash_tab, n, chunk, plan, kg_dest,
-                       cursor, reinterpret_cast<RecC*>(out), stats, late_idx, late_cap);
+    hipLaunchKernelGGL((partition_compact_kernel<1, kCUProd>), dim3(blocks), dim3(1024),
+                       compact_lds(kCUProd), (hipStream_t)stream, keys, ts, vals, jhash_tab, n,
+                       chunk, plan, kg_dest, cursor, reinterpret_cast<RecC*>(out), stats,
+                       late_idx, late_cap);
     HIP_CHECK(hipGetLastError());
     return;
   }
@@ -2321,13 +2338,36 @@ void partition_variant(const uint64_t* keys, const int64_t* ts, const uint64_t* 
                        late_idx, late_cap);                                                    \
     break;                                                                                    \
   }
+#define MXS_PART_COMPACT(VV, CUV, EPB)                                                         \
+  case VV: {                                                                                  \
+    if (plan.rec_words != 2 || nb > kCMaxNb) throw std::runtime_error("compact variant: plan"); \
+    static bool attr = false;                                                                 \
+    if (!attr) {                                                                              \
+      HIP_CHECK(hipFuncSetAttribute((const void*)partition_compact_kernel<1, CUV>,             \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,                \
+                                    (int)compact_lds(CUV)));                                   \
+      attr = true;                                                                            \
+    }                                                                                         \
+    const int cb = grid_for(n, EPB, 2048);                                                    \
+    const int64_t cchunk = (n + cb - 1) / cb;                                                 \
+    hipLaunchKernelGGL((partition_compact_kernel<1, CUV>), dim3(cb), dim3(1024),               \
+                       compact_lds(CUV), st, keys, ts, vals, jhash_tab, n, cchunk, plan,       \
+                       kg_dest, cursor, reinterpret_cast<RecC*>(out), stats, late_idx,         \
+                       late_cap);                                                              \
+    break;                                                                                    \
+  }
   switch (variant) {
     MXS_PART(0) MXS_PART(1) MXS_PART(2) MXS_PART(3)
     MXS_PART_STAGED(4, 0) MXS_PART_STAGED(5, 1)
+    MXS_PART_COMPACT(10, 2, 32768) MXS_PART_COMPACT(11, 3, 32768) MXS_PART_COMPACT(12, 4, 32768)
+    MXS_PART_COMPACT(13, 3, 49152) MXS_PART_COMPACT(14, 4, 65536)
+    MXS_PART_COMPACT(15, 2, 65536) MXS_PART_COMPACT(16, 3, 65536)
+    MXS_PART_COMPACT(17, 4, 131072)
     default: throw std::runtime_error("partition: unknown variant");
   }
 #undef MXS_PART
 #undef MXS_PART_STAGED
+#undef MXS_PART_COMPACT
   HIP_CHECK(hipGetLastError());
 }
 

@@ -55,7 +55,8 @@ def main():
             for var in [int(x) for x in os.environ.get("KB_VARIANTS", "0,1,4,5").split(",")]:
                 plan = K.PartitionPlan(max_parallelism=128, nsub_log2=nsub_log2, nranks=1,
                                        window_mode=1, drop_late=1, hash_mode=0, bucket_cap=bcap,
-                                       late_ts=-5000, tbase=-60000, pane=60000, ablate=ablate)
+                                       late_ts=-5000, tbase=-60000, pane=60000, ablate=ablate,
+                                       rec_words=int(os.environ.get("KB_RECW", 3)))
 
                 def f(plan=plan, cursor=cursor, out=out, stats=stats, var=var):
                     K.step_begin(cursor, stats)
