@@ -21,6 +21,8 @@
 // AggregatingState (chapter2/.../ComputeCpuAvg.java:27-59).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <stdexcept>
 #include <string>
@@ -110,6 +112,8 @@ struct PartEval {
   uint32_t t;
 };
 
+// ONE = true: compiled for a single rank (no key-group hashing at all; bucket = sub-table).
+template <bool ONE = false>
 __device__ __forceinline__ PartEval part_eval(uint64_t key, int64_t ts, const int32_t* jhash_tab,
                                               const PartPlan& p, const int32_t* kg_dest) {
   PartEval e;
@@ -127,8 +131,12 @@ __device__ __forceinline__ PartEval part_eval(uint64_t key, int64_t ts, const in
       return e;
     }
   }
-  const int32_t jh = p.nranks == 1 ? 0 : p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
-  e.bucket = bucket_of(key, jh, p, kg_dest);
+  if constexpr (ONE) {
+    e.bucket = sub_table_of(key, p.nsub_log2);
+  } else {
+    const int32_t jh = p.nranks == 1 ? 0 : p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
+    e.bucket = bucket_of(key, jh, p, kg_dest);
+  }
   return e;
 }
 
@@ -581,16 +589,17 @@ static_assert(kStagedLds <= 160 * 1024, "staged partition LDS image exceeds 160 
 constexpr int kCU = 2;                   // events per thread per round (production)
 constexpr int kCG = 4;                   // reservation granularity (records per 64-byte sector)
 constexpr int kCMaxNb = 512;
+constexpr int kKgLdsMax = 4096;          // max parallelism whose kg -> rank table goes to LDS
 constexpr size_t compact_lds(int cu) {
   return (size_t)1024 * cu * sizeof(RecC) + (size_t)kCMaxNb * 6 * 4 + 20 * 4 + 16 * 8 +
-         (size_t)1024 * cu * 2;
+         (size_t)1024 * cu * 2 + (size_t)kKgLdsMax * 4;
 }
 constexpr size_t kCompactLds = compact_lds(kCU);
 static_assert(kCompactLds <= 80 * 1024, "compact partition must fit two workgroups per CU");
 constexpr int kCUProd = 4;               // production round: 4096 records, one group per CU
 static_assert(compact_lds(kCUProd) <= 160 * 1024, "compact partition LDS exceeds 160 KiB");
 
-template <int V, int CU = kCU>
+template <int V, int CU = kCU, bool ONE = false>
 __global__ __launch_bounds__(1024) void partition_compact_kernel(
     const uint64_t* __restrict__ keys, const int64_t* __restrict__ ts,
     const uint64_t* __restrict__ vals, const int32_t* __restrict__ jhash_tab, int64_t n,
@@ -609,12 +618,18 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   int64_t* lred = (int64_t*)(wsum + 20);                       // 16 x i64
   uint16_t* sbk = (uint16_t*)(lred + 16);                      // [(1024 * CU)] bucket of rbuf[j]
   uint32_t* dbase = (uint32_t*)(sbk + (1024 * CU));                    // [kCMaxNb] round's dest - offset
+  int32_t* skg = (int32_t*)(dbase + kCMaxNb);                  // [kKgLdsMax] key group -> rank
 
   for (int b = threadIdx.x; b < kCMaxNb; b += blockDim.x) {
     run_base[b] = 0;
     lcnt[b] = 0;
     rcnt[b] = 0;
   }
+  // G > 1: the key-group -> rank table lives in LDS. A global load per record inside the round
+  // made the in-order vmcnt wait for the next round's prefetched (key, ts, value) loads too.
+  const bool kg_lds = !ONE && plan.nranks > 1 && plan.max_parallelism <= kKgLdsMax;
+  if (kg_lds)
+    for (int g = threadIdx.x; g < plan.max_parallelism; g += blockDim.x) skg[g] = kg_dest[g];
   __syncthreads();
   const int64_t start = (int64_t)blockIdx.x * chunk;
   const int64_t end = start + chunk < n ? start + chunk : n;
@@ -631,9 +646,15 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
     for (int u = 0; u < kPartU; ++u) {
       const int64_t i = i0 + (int64_t)u * blockDim.x;
       if (i >= end) break;
-      const int32_t jh = plan.nranks == 1 ? 0
-                         : plan.hash_mode ? jhash_tab[k[u]] : java_long_hash((int64_t)k[u]);
-      atomicAdd(&run_base[bucket_of(k[u], jh, plan, kg_dest)], 1u);
+      uint32_t b;
+      if constexpr (ONE) {
+        b = sub_table_of(k[u], plan.nsub_log2);
+      } else {
+        const int32_t jh = plan.nranks == 1 ? 0
+                           : plan.hash_mode ? jhash_tab[k[u]] : java_long_hash((int64_t)k[u]);
+        b = kg_lds ? bucket_of(k[u], jh, plan, skg) : bucket_of(k[u], jh, plan, kg_dest);
+      }
+      atomicAdd(&run_base[b], 1u);
     }
   }
   __syncthreads();
@@ -699,7 +720,9 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
         const int64_t t = ct[u];
         const uint64_t v = cv[u];
         tmax = t > tmax ? t : tmax;
-        const PartEval e = part_eval(k, t, jhash_tab, plan, kg_dest);
+        const PartEval e = ONE      ? part_eval<true>(k, t, jhash_tab, plan, kg_dest)
+                           : kg_lds ? part_eval(k, t, jhash_tab, plan, skg)
+                                    : part_eval(k, t, jhash_tab, plan, kg_dest);
         if (e.kind == 1) {
           ++nlate;
           if (late_idx) {
@@ -822,7 +845,10 @@ __device__ __forceinline__ uint32_t lds_probe_insert(uint64_t* skeys, uint64_t k
                                                      int* inserted) {
   uint32_t s = slot_hash(key) & mask;
   for (uint32_t i = 0; i <= mask; ++i) {
-    const uint64_t k = *((volatile uint64_t*)&skeys[s]);
+    // Relaxed workgroup-scope atomic load, not a volatile read: the volatile cast made the
+    // access generic (flat_load ... sc0 sc1 + s_waitcnt vmcnt(0)), which waited for every
+    // record load in flight before each probe.
+    const uint64_t k = __hip_atomic_load(&skeys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (k == key) return s;
     if (k == kEmptyKey) {
       const uint64_t prev = atomicCAS((unsigned long long*)&skeys[s], (unsigned long long)kEmptyKey,
@@ -889,19 +915,42 @@ __device__ __forceinline__ Rec load_rec(const void* base, size_t idx) {
   return r;
 }
 
-template <int AGG, int RW>
+// Materialise a loaded record in registers at this point (empty asm that "modifies" every
+// field). Without it LLVM narrowed the 16-byte record load and sank the key half into the
+// per-record branch, where its s_waitcnt vmcnt(0) also waited for the other records in flight.
+template <int RW>
+__device__ __forceinline__ void pin_rec(Rec& r) {
+  asm volatile("" : "+v"(r.key), "+v"(r.val), "+v"(r.t), "+v"(r.aux));
+}
+
+// Packed (sum, count) accumulator for integer sums of int32 values (PK = true): one LDS word
+// P = sum_i (v_i + 2^48) mod 2^64 holds both the 48-bit signed sum and the 16-bit count, so a
+// record costs one LDS atomic instead of two and a pane row 8 bytes instead of 12. Exact while
+// |sum| < 2^47 and count < 2^16, guaranteed by the host (int32 values, < 65536 records per
+// sub-table and step). An untouched slot stays 0 (a touched one cannot be 0: |sum| < 2^47).
+constexpr uint64_t kPkOne = 1ull << 48;
+__device__ __forceinline__ int64_t pk_sum(uint64_t p) {
+  return (int64_t)(p << 16) >> 16;
+}
+__device__ __forceinline__ uint32_t pk_cnt(uint64_t p) {
+  return (uint32_t)((p - (uint64_t)pk_sum(p)) >> 48);
+}
+
+template <int AGG, int RW, bool PK = false>
 __global__ __launch_bounds__(1024) void window_agg_kernel(
     const void* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
     uint64_t* __restrict__ keys_g, uint64_t* __restrict__ acc_g, uint32_t* __restrict__ cnt_g,
     uint8_t* __restrict__ dirty_g, uint32_t* __restrict__ occupancy, uint32_t* __restrict__ flags) {
+  static_assert(!PK || ((AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) && RW == 2),
+                "packed accumulators: integer sum/avg of 16-byte records only");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int sub = blockIdx.x;
   const uint32_t cap = 1u << p.cap_log2;
   const uint32_t mask = cap - 1;
   uint64_t* skeys = (uint64_t*)smem;
   uint64_t* sacc = skeys + cap;
-  uint32_t* scnt = (uint32_t*)(sacc + (size_t)p.pg * cap);
-  int* sflag = (int*)(scnt + (size_t)p.pg * cap);  // [0] inserted, [1] overflow, [2] occupancy
+  uint32_t* scnt = (uint32_t*)(sacc + (size_t)p.pg * cap);           // unused when PK
+  int* sflag = (int*)(scnt + (PK ? 0 : (size_t)p.pg * cap));  // [0] inserted, [1] ovf, [2] occ
 
   const size_t sbase = (size_t)sub << p.cap_log2;
   const size_t nslots = (size_t)p.nsub << p.cap_log2;
@@ -913,8 +962,8 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
   for (int pg0 = 0; pg0 < p.np_step; pg0 += p.pg) {
     const int npg = (p.np_step - pg0) < p.pg ? (p.np_step - pg0) : p.pg;
     for (uint32_t i = threadIdx.x; i < (uint32_t)npg * cap; i += blockDim.x) {
-      sacc[i] = (uint64_t)lds_identity<AGG>();
-      scnt[i] = 0;
+      sacc[i] = PK ? 0ull : (uint64_t)lds_identity<AGG>();
+      if (!PK) scnt[i] = 0;
     }
     __syncthreads();
     const int64_t q0 = p.p_lo + pg0;  // relative pane of LDS row 0
@@ -928,8 +977,13 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
 #pragma unroll
         for (int u = 0; u < kAggU; ++u) {
           const uint32_t e = e0 + u * blockDim.x;
-          if (e < c) rr[u] = load_rec<RW>(recs, seg0 + e);
+          // Branch-free: a load under `if (e < c)` made the compiler wait for each load at the
+          // branch join (s_waitcnt vmcnt(0) after every load: no loads in flight at all).
+          // Lanes past the end re-read the last record and skip it below.
+          rr[u] = load_rec<RW>(recs, seg0 + (e < c ? e : c - 1));
         }
+#pragma unroll
+        for (int u = 0; u < kAggU; ++u) pin_rec<RW>(rr[u]);
 #pragma unroll
         for (int u = 0; u < kAggU; ++u) {
           const uint32_t e = e0 + u * blockDim.x;
@@ -944,8 +998,12 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
             continue;
           }
           const uint32_t li = (uint32_t)q * cap + s;
-          lds_accumulate<AGG>(&sacc[li], r.val);
-          atomicAdd(&scnt[li], p.combined ? r.aux : 1u);
+          if (PK) {
+            atomicAdd((unsigned long long*)&sacc[li], (unsigned long long)(r.val + kPkOne));
+          } else {
+            lds_accumulate<AGG>(&sacc[li], r.val);
+            atomicAdd(&scnt[li], p.combined ? r.aux : 1u);
+          }
         }
       }
     }
@@ -963,7 +1021,7 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
 #pragma unroll
       for (int w = 0; w < kWB; ++w) {
         const uint32_t i = i0 + (uint32_t)w * blockDim.x;
-        dc[w] = i < nrow ? scnt[i] : 0u;
+        dc[w] = i < nrow ? (PK ? pk_cnt(sacc[i]) : scnt[i]) : 0u;
         oc[w] = 0;
         oa[w] = 0;
         gi[w] = 0;
@@ -978,7 +1036,7 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
       for (int w = 0; w < kWB; ++w) {
         if (!dc[w]) continue;
         const uint32_t i = i0 + (uint32_t)w * blockDim.x;
-        const uint64_t d = lds_export<AGG>(sacc[i]);
+        const uint64_t d = PK ? (uint64_t)pk_sum(sacc[i]) : lds_export<AGG>(sacc[i]);
         if (AGG != AGG_COUNT) acc_g[gi[w]] = oc[w] ? agg_combine(AGG, oa[w], d) : d;
         cnt_g[gi[w]] = oc[w] + dc[w];
         if (p.pane_base + q0 + (int64_t)(i >> p.cap_log2) <= p.fired_hi) dirty_g[gi[w]] = 1;
@@ -1042,8 +1100,10 @@ __global__ __launch_bounds__(1024) void window_combine_kernel(
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
         const uint32_t e = e0 + u * blockDim.x;
-        if (e < c) rr[u] = load_rec<RW>(recs, seg0 + e);
+        rr[u] = load_rec<RW>(recs, seg0 + (e < c ? e : c - 1));  // branch-free (see window_agg)
       }
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) pin_rec<RW>(rr[u]);
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
         const uint32_t e = e0 + u * blockDim.x;
@@ -2277,7 +2337,10 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
     // reservation work; fewer, larger groups beat the higher occupancy.
     static bool attr = false;
     if (!attr) {
-      HIP_CHECK(hipFuncSetAttribute((const void*)partition_compact_kernel<1, kCUProd>,
+      HIP_CHECK(hipFuncSetAttribute((const void*)partition_compact_kernel<1, kCUProd, false>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)compact_lds(kCUProd)));
+      HIP_CHECK(hipFuncSetAttribute((const void*)partition_compact_kernel<1, kCUProd, true>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)compact_lds(kCUProd)));
       attr = true;
@@ -2285,10 +2348,17 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
     const int64_t per = std::min<int64_t>(65536, std::max<int64_t>(4096, (n + 255) / 256));
     const int blocks = grid_for(n, per, 4096);
     const int64_t chunk = (n + blocks - 1) / blocks;
-    hipLaunchKernelGGL((partition_compact_kernel<1, kCUProd>), dim3(blocks), dim3(1024),
-                       compact_lds(kCUProd), (hipStream_t)stream, keys, ts, vals, jhash_tab, n,
-                       chunk, plan, kg_dest, cursor, reinterpret_cast<RecC*>(out), stats,
-                       late_idx, late_cap);
+    // One rank: the kernel specialised without key-group hashing (and without the LDS kg table).
+    if (plan.nranks == 1)
+      hipLaunchKernelGGL((partition_compact_kernel<1, kCUProd, true>), dim3(blocks), dim3(1024),
+                         compact_lds(kCUProd) - (size_t)kKgLdsMax * 4, (hipStream_t)stream, keys,
+                         ts, vals, jhash_tab, n, chunk, plan, kg_dest, cursor,
+                         reinterpret_cast<RecC*>(out), stats, late_idx, late_cap);
+    else
+      hipLaunchKernelGGL((partition_compact_kernel<1, kCUProd, false>), dim3(blocks), dim3(1024),
+                         compact_lds(kCUProd), (hipStream_t)stream, keys, ts, vals, jhash_tab, n,
+                         chunk, plan, kg_dest, cursor, reinterpret_cast<RecC*>(out), stats,
+                         late_idx, late_cap);
     HIP_CHECK(hipGetLastError());
     return;
   }
@@ -2371,6 +2441,18 @@ void partition_variant(const uint64_t* keys, const int64_t* ts, const uint64_t* 
   HIP_CHECK(hipGetLastError());
 }
 
+// Packed (sum, count) accumulators apply: integer sum/avg over 16-byte records, raw events
+// (not combiner output) and fewer than 2^16 records per sub-table and step. MXS_AGG_PACK=0
+// turns them off (A/B switch).
+static bool agg_pack_ok(const AggPlan& p) {
+  static const bool enabled = [] {
+    const char* e = std::getenv("MXS_AGG_PACK");
+    return !(e && e[0] == '0');
+  }();
+  return enabled && (p.agg == AGG_SUM_I64 || p.agg == AGG_AVG_I64) && p.rec_words == 2 &&
+         !p.combined && (uint64_t)p.nsrc * p.bucket_cap < 65536;
+}
+
 template <int AGG>
 static void launch_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p,
                        uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
@@ -2381,7 +2463,19 @@ static void launch_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 2>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    if constexpr (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64)
+      HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 2, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
+  }
+  if constexpr (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) {
+    if (agg_pack_ok(p)) {
+      const size_t cap = (size_t)1 << p.cap_log2;
+      const size_t lds_pk = cap * 8 + (size_t)p.pg * cap * 8 + 16;
+      hipLaunchKernelGGL((window_agg_kernel<AGG, 2, true>), dim3(p.nsub), dim3(1024), lds_pk, s,
+                         (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+      return;
+    }
   }
   if (p.rec_words == 2)
     hipLaunchKernelGGL((window_agg_kernel<AGG, 2>), dim3(p.nsub), dim3(1024), lds, s,

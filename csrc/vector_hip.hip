@@ -52,7 +52,9 @@ __device__ __forceinline__ uint32_t vprobe_insert(uint64_t* skeys, uint64_t key,
                                                   int* inserted) {
   uint32_t s = slot_hash(key) & mask;
   for (uint32_t i = 0; i <= mask; ++i) {
-    const uint64_t k = *((volatile uint64_t*)&skeys[s]);
+    // Relaxed workgroup-scope atomic load (a volatile read compiles to a generic flat load that
+    // waits for all outstanding global loads; see lds_probe_insert in kernels_hip.hip).
+    const uint64_t k = __hip_atomic_load(&skeys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (k == key) return s;
     if (k == kEmptyKey) {
       const uint64_t prev = atomicCAS((unsigned long long*)&skeys[s], (unsigned long long)kEmptyKey,

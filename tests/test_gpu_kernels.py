@@ -101,6 +101,31 @@ def test_window_sum_vs_torch_reference(gpu_device):
     assert got == exp
 
 
+@pytest.mark.parametrize("agg", [K.AGG_SUM_I64, K.AGG_AVG_I64])
+def test_packed_int_sums_extreme_values(gpu_device, agg):
+    """Packed (48-bit sum, 16-bit count) LDS accumulators: int32 extremes of both signs and hot
+    keys with thousands of records per slot per step, vs a PyTorch int64 reference."""
+    n = 1 << 18
+    g = torch.Generator(device="cpu").manual_seed(7)
+    keys = torch.randint(0, 64, (n,), generator=g, dtype=torch.int64)  # ~4K records per key
+    keys[: n // 2] = torch.randint(0, 50_000, (n // 2,), generator=g, dtype=torch.int64)
+    ts = torch.randint(0, 3000, (n,), generator=g, dtype=torch.int64)
+    vals = torch.randint(-(2**31), 2**31, (n,), generator=g, dtype=torch.int64)
+    vals[::7] = 2**31 - 1
+    vals[::11] = -(2**31)
+    op = KeyedWindowOperator(size=1000, agg=agg, device=gpu_device, max_keys=60_000,
+                             batch_capacity=n)
+    out = op.process(keys.to(gpu_device), ts.to(gpu_device), vals.to(gpu_device)) + op.finish()
+    got = _results(out)
+    comp = torch.div(ts, 1000, rounding_mode="floor") * 1_000_000 + keys
+    uniq, inv = torch.unique(comp, return_inverse=True)
+    sums = torch.zeros(uniq.numel(), dtype=torch.int64).index_add_(0, inv, vals)
+    cnts = torch.zeros(uniq.numel(), dtype=torch.int64).index_add_(0, inv, torch.ones_like(vals))
+    exp = {(int(u) // 1_000_000 * 1000, int(u) % 1_000_000): (int(s), int(c))
+           for u, s, c in zip(uniq, sums, cnts)}
+    assert got == exp
+
+
 @pytest.mark.parametrize("agg", [K.AGG_SUM_F64, K.AGG_MIN_F64, K.AGG_MAX_F64, K.AGG_AVG_F64])
 def test_float_aggregates_vs_torch(gpu_device, agg):
     n = 1 << 18
