@@ -900,7 +900,7 @@ __device__ __forceinline__ uint64_t lds_export(uint64_t a) {
 // Keyed window aggregation: one workgroup per sub-table.
 // LDS image (dynamic, 16-B aligned): keys[cap] u64 | acc[pg][cap] u64 | cnt[pg][cap] u32 | flag
 // ------------------------------------------------------------------------------------------
-constexpr int kAggU = 4;
+constexpr int kAggU = 4;  // 8 measured equal (162.7 vs 162.1 us, profiles/r1_window_agg_ab.md)
 
 // Record load for both layouts: RW = 3 (24-byte Rec) or 2 (16-byte RecC, int32 value).
 template <int RW>

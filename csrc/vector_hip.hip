@@ -44,6 +44,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kVThreads = 1024;              // 16 waves per workgroup, one workgroup per CU
 constexpr int kVWaves = kVThreads / 64;
 constexpr int kVPer = 16;                    // records per thread per round
+constexpr int kVLoad = 4;                    // record loads in flight per thread
 constexpr int kVRound = kVThreads * kVPer;   // 16 Ki records per LDS round
 constexpr int kVHist = 4096;                 // (pane, slot) histogram entries per pane group
 constexpr uint32_t kHole = 0xFFFFFFFFu;
@@ -172,15 +173,27 @@ __global__ __launch_bounds__(kVThreads) void vec_window_agg_kernel(
         __syncthreads();
         // 1. slot lookup + (pane, slot) histogram; the rank inside a bin comes from the atomic.
         uint32_t ck[kVPer], rowk[kVPer];
+        uint64_t kk[kVLoad];
+        uint32_t vv[kVLoad], tt[kVLoad];
 #pragma unroll
         for (int u = 0; u < kVPer; ++u) {
+          if (u % kVLoad == 0) {
+            // kVLoad branch-free record loads in flight, pinned in registers before the probes
+            // (a load per record under `if (e < c)` waited on vmcnt(0) each time).
+#pragma unroll
+            for (int j = 0; j < kVLoad; ++j) {
+              const uint32_t e = r0 + (uint32_t)(u + j) * kVThreads + threadIdx.x;
+              vload_rec<RW>(recs, seg0 + (e < c ? e : c - 1), kk[j], vv[j], tt[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < kVLoad; ++j) asm volatile("" : "+v"(kk[j]), "+v"(vv[j]), "+v"(tt[j]));
+          }
           ck[u] = kHole;
           rowk[u] = 0;
           const uint32_t e = r0 + (uint32_t)u * kVThreads + threadIdx.x;
           if (e >= c) continue;
-          uint64_t key;
-          uint32_t val, t;
-          vload_rec<RW>(recs, seg0 + e, key, val, t);
+          const uint64_t key = kk[u % kVLoad];
+          const uint32_t val = vv[u % kVLoad], t = tt[u % kVLoad];
           if (t == kHole) continue;
           const int64_t q = (int64_t)t - q0;
           if (q < 0 || q >= npg) continue;

@@ -38,19 +38,71 @@ I64_MIN = K.I64_MIN
 I64_MAX = K.I64_MAX
 
 
-def to_host_arrays(cols: list[torch.Tensor], n: int) -> list[np.ndarray]:
-    """The first n rows of each output column as fresh host arrays. On a GPU: non-blocking
-    copies into pinned buffers (PyTorch's caching host allocator, reused once the arrays are
-    dropped) and one stream sync — a pageable .cpu() stages every column through a bounce
-    buffer at a fraction of the PCIe rate. On the CPU: copies (the device buffers are reused by
-    the next fire)."""
+class PinnedSlabPool:
+    """Pinned host slabs for fired rows, reused once every array handed out of a slab is gone.
+
+    `torch.empty(..., pin_memory=True)` per fire cost ~1.5 ms of host time per firing in the
+    rocprofv3 timeline of the headline bench (profiles/r1_fire_pinned_pool.md): the GPU idled
+    between the fire kernel and the D2H copies. A slab is one pinned byte tensor plus its numpy
+    view; every column handed out is a numpy view of that array, so the array's refcount says
+    whether any caller still holds rows of the slab."""
+
+    def __init__(self, pin: bool = True, max_slabs: int = 8):
+        self.pin = pin
+        self.max_slabs = max_slabs
+        self.slabs: list[tuple[torch.Tensor, np.ndarray]] = []
+        self.allocs = 0
+
+    def _free(self, i: int) -> bool:
+        # References to a free slab's array: the pool's tuple + getrefcount's own argument.
+        import sys
+
+        return sys.getrefcount(self.slabs[i][1]) <= 2
+
+    def take(self, nbytes: int) -> tuple[torch.Tensor, np.ndarray]:
+        for i in range(len(self.slabs)):
+            if self.slabs[i][0].numel() >= nbytes and self._free(i):
+                return self.slabs[i]
+        if len(self.slabs) >= self.max_slabs:
+            # Drop the smallest free slab so a long-lived caller cannot grow the pool unbounded.
+            free = [i for i in range(len(self.slabs)) if self._free(i)]
+            if free:
+                self.slabs.pop(min(free, key=lambda i: self.slabs[i][0].numel()))
+        t = torch.empty(_next_pow2(max(nbytes, 1 << 16)), dtype=torch.uint8, pin_memory=self.pin)
+        self.allocs += 1
+        slab = (t, t.numpy())
+        self.slabs.append(slab)
+        return slab
+
+
+_PINNED = PinnedSlabPool()
+
+
+def to_host_arrays(cols: list[torch.Tensor], n: int, pool: PinnedSlabPool | None = None) -> list[np.ndarray]:
+    """The first n rows of each output column as host arrays. On a GPU: non-blocking copies into
+    one pinned slab (reused from `pool` once the caller dropped the previous arrays) and one
+    stream sync — a pageable .cpu() stages every column through a bounce buffer at a fraction of
+    the PCIe rate. On the CPU: copies (the device buffers are reused by the next fire)."""
     if not cols or cols[0].device.type != "cuda":
         return [c[:n].numpy().copy() for c in cols]
-    host = [torch.empty(n, dtype=c.dtype, pin_memory=True) for c in cols]
-    for h, c in zip(host, cols):
-        h.copy_(c[:n], non_blocking=True)
+    pool = _PINNED if pool is None else pool
+    offs, nbytes = [], 0
+    for c in cols:
+        offs.append(nbytes)
+        nbytes += (n * c.element_size() + 255) & ~255
+    t, arr = pool.take(nbytes)
+    out = []
+    for o, c in zip(offs, cols):
+        nb = n * c.element_size()
+        t[o:o + nb].view(c.dtype).copy_(c[:n], non_blocking=True)
+        out.append(arr[o:o + nb].view(_NP_DTYPE[c.dtype]))
     torch.cuda.current_stream(cols[0].device).synchronize()
-    return [h.numpy() for h in host]
+    return out
+
+
+_NP_DTYPE = {torch.int64: np.int64, torch.int32: np.int32, torch.float64: np.float64,
+             torch.float32: np.float32, torch.uint8: np.uint8, torch.int16: np.int16,
+             torch.bfloat16: np.uint16, torch.float16: np.float16}
 
 
 def _next_pow2(x: int) -> int:

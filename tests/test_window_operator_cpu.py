@@ -154,3 +154,24 @@ def test_compact_records_equal_wide(agg):
     fired = op.finish()
     got = {int(k): int(a) for r in fired for k, a in zip(r.keys, r.raw)}
     assert got == {1: 5, 2: 1 << 40}
+
+
+def test_pinned_slab_pool_reuses_only_released_slabs():
+    """The fire D2H slab pool (window_operator.PinnedSlabPool) never hands out a slab whose rows a
+    caller still holds, and reuses it once they are dropped (pin=False: same logic on CPU)."""
+    import numpy as np
+
+    from mxstream.runtime.window_operator import PinnedSlabPool
+
+    pool = PinnedSlabPool(pin=False, max_slabs=2)
+    t1, a1 = pool.take(1000)
+    held = a1[0:64].view(np.int64)
+    del t1, a1
+    t2, a2 = pool.take(1000)
+    assert pool.allocs == 2  # first slab still referenced through `held`
+    del t2, a2
+    del held
+    pool.take(1000)
+    assert pool.allocs == 2  # released slab reused
+    big = pool.take(1 << 20)
+    assert big[0].numel() >= 1 << 20 and pool.allocs == 3 and len(pool.slabs) <= 2
