@@ -234,6 +234,14 @@ PYBIND11_MODULE(_mxs_native, m) {
                         P<uint64_t>(keys_g), P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_out),
                         P<uint32_t>(flags), abits, shift, stream);
   });
+  m.def("gpu_rolling_lookup_direct", [](intptr_t keys, intptr_t vals, uint32_t n, int nsub_log2,
+                                        int cap_log2, intptr_t keys_g, intptr_t sk, intptr_t vout,
+                                        intptr_t n_out, intptr_t flags, int shift,
+                                        intptr_t stream) {
+    gpu::rolling_lookup_direct(P<uint64_t>(keys), P<uint64_t>(vals), n, nsub_log2, cap_log2,
+                               P<uint64_t>(keys_g), P<int64_t>(sk), P<uint64_t>(vout),
+                               P<uint32_t>(n_out), P<uint32_t>(flags), shift, stream);
+  });
   m.def("gpu_rolling_heads", [](intptr_t sk, intptr_t n_in, int64_t n_cap, intptr_t heads,
                                 intptr_t n_heads, int shift, intptr_t stream) {
     gpu::rolling_heads(P<int64_t>(sk), P<uint32_t>(n_in), n_cap, P<uint32_t>(heads),

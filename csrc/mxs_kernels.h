@@ -81,6 +81,9 @@ void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& plan, uint
              uint64_t* out_vals, intptr_t stream);
 void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep, intptr_t stream);
 void step_begin(uint32_t* cursor, int nb, int64_t* stats, intptr_t stream);
+void rolling_lookup_direct(const uint64_t* keys, const uint64_t* vals, uint32_t n, int nsub_log2,
+                           int cap_log2, uint64_t* keys_g, int64_t* sort_key, uint64_t* vals_out,
+                           uint32_t* n_out, uint32_t* flags, int shift, intptr_t stream);
 void rolling_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
                     uint32_t bucket_cap, int cap_log2, uint64_t* keys_g, int64_t* sort_key,
                     uint64_t* vals_out, uint32_t* n_out, uint32_t* flags, int abits, int shift,

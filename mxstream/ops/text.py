@@ -35,18 +35,40 @@ def fnv1a64(b: bytes) -> int:
     return h - (1 << 64) if h >= 1 << 63 else h
 
 
-def parse_text_gpu(data: bytes, spec: list[tuple[int, int]], sep: str = " ", offset_s: int = 0,
+def pinned_text_batch(data: bytes) -> torch.Tensor:
+    """Stage a text batch in page-locked host memory, as the socket reader's ring slots are
+    (SURVEY.md F-src): ``parse_text_gpu`` then uploads it with one DMA instead of a pageable
+    copy through the driver's bounce buffer."""
+    t = torch.empty(len(data), dtype=torch.uint8, pin_memory=torch.cuda.is_available())
+    if len(data):
+        t.numpy()[:] = np.frombuffer(data, dtype=np.uint8)
+    return t
+
+
+def parse_text_gpu(data, spec: list[tuple[int, int]], sep: str = " ", offset_s: int = 0,
                    device="cuda") -> list:
     """Returns one entry per spec field: a float64/int64 device tensor, or for FK_STR a
-    (key int64, java_hash int32) pair of device tensors."""
+    (key int64, java_hash int32) pair of device tensors.
+
+    ``data`` is ``bytes`` or a 1-D uint8 tensor (a pinned host batch from ``pinned_text_batch``
+    or a batch already on the device); a pinned batch is uploaded asynchronously."""
     if not spec or len(spec) > 8:
         raise ValueError("1..8 fields")
     dev = torch.device(device)
     m = load()
-    raw = np.frombuffer(data, dtype=np.uint8)
-    n_bytes = raw.size
-    buf = torch.from_numpy(raw.copy()).to(dev) if n_bytes else torch.zeros(1, dtype=torch.uint8,
-                                                                              device=dev)
+    if isinstance(data, torch.Tensor):
+        if data.dtype != torch.uint8 or data.dim() != 1:
+            raise ValueError("text batch tensor must be 1-D uint8")
+        n_bytes = data.numel()
+        buf = (data.to(dev, non_blocking=data.is_pinned()) if n_bytes
+               else torch.zeros(1, dtype=torch.uint8, device=dev))
+        host = data
+    else:
+        raw = np.frombuffer(data, dtype=np.uint8)
+        n_bytes = raw.size
+        buf = torch.from_numpy(raw.copy()).to(dev) if n_bytes else torch.zeros(
+            1, dtype=torch.uint8, device=dev)
+        host = None
     nl = torch.nonzero(buf[:n_bytes] == 10).flatten()
     starts = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), nl + 1])
     if starts.numel() and int(starts[-1]) >= n_bytes:
@@ -63,6 +85,8 @@ def parse_text_gpu(data: bytes, spec: list[tuple[int, int]], sep: str = " ", off
                          torch.cuda.current_stream(dev).cuda_stream)
         bad = torch.nonzero(status[:n]).flatten()
         if bad.numel():
+            if host is not None:
+                data = host.cpu().numpy().tobytes()
             _host_patch(m, data, starts.cpu().numpy(), bad.cpu().numpy(), spec, sep, offset_s,
                         cols, jh, n)
     out = []

@@ -71,6 +71,7 @@ class KeyedRollingOperator:
         self._alloc(batch_capacity)
         self.steps = 0
         self.records_in = 0
+        self.direct_single_rank = True  # world 1 on the GPU: no partition pass (_process_direct)
 
     def _alloc(self, batch_capacity: int, slack: float = 1.5):
         self.batch_capacity = int(batch_capacity)
@@ -100,11 +101,52 @@ class KeyedRollingOperator:
         self.out_tag = torch.empty(ocap, dtype=torch.int64, device=dev)
         self.out_n = torch.zeros(1, dtype=torch.int32, device=dev)
 
+    def _process_direct(self, keys: torch.Tensor, vals: torch.Tensor, n: int, to_host: bool):
+        """Single-rank GPU path: every key group is local, so the table lookup reads the source
+        columns directly (no partition pass) and writes record i at position i. The batch is then
+        in arrival order and a stable radix sort over the slot bits alone gives the (slot,
+        arrival) order the scan needs -- the same keys and rows as the partitioned path."""
+        m = load()
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        keys = keys.contiguous()
+        vals = vals.contiguous()
+        self.records_in += n
+        self.steps += 1
+        self.out_n.zero_()
+        code, consts = self.filter_prog.as_args()
+        cap = self.out_key.numel()
+        self.n_buf.zero_()
+        shift = max(1, int(n - 1).bit_length())
+        m.gpu_rolling_lookup_direct(keys.data_ptr(), vals.data_ptr(), n, self.nsub_log2,
+                                    self.cap_log2, self.keys_g.data_ptr(),
+                                    self.sort_key.data_ptr(), self.vals_buf.data_ptr(),
+                                    self.n_buf.data_ptr(), self.flags.data_ptr(), shift, st)
+        nbits = shift + self.nslots.bit_length()
+        need = m.gpu_sort_pairs_temp_bytes(n, shift, nbits)
+        if self._sort_tmp is None or self._sort_tmp.numel() < need:
+            self._sort_tmp = torch.empty(need, dtype=torch.uint8, device=self.device)
+        m.gpu_sort_pairs(self._sort_tmp.data_ptr(), self._sort_tmp.numel(),
+                         self.sort_key.data_ptr(), self.sort_out.data_ptr(),
+                         self.vals_buf.data_ptr(), self.vals_out.data_ptr(), n, shift, nbits, st)
+        sk = self.sort_out
+        n_in = self.n_buf[0:1]
+        m.gpu_rolling_heads(sk.data_ptr(), n_in.data_ptr(), n, self.heads.data_ptr(),
+                            self.n_buf[1:2].data_ptr(), shift, st)
+        m.gpu_rolling_scan(self.agg, sk.data_ptr(), 0, self.vals_out.data_ptr(), n_in.data_ptr(),
+                           self.heads.data_ptr(), self.n_buf[1:2].data_ptr(),
+                           min(n, self.nslots), self.acc_g.data_ptr(), self.cnt_g.data_ptr(),
+                           self.keys_g.data_ptr(), code, consts, self.out_key.data_ptr(),
+                           self.out_val.data_ptr(), self.out_tag.data_ptr(),
+                           self.out_n.data_ptr(), cap, shift, shift, st)
+        return self._emit(to_host)
+
     def process(self, keys: torch.Tensor, vals: torch.Tensor, to_host: bool = True):
         """Update state with one micro-batch; returns the emitted rows (host) or the device count."""
         n = keys.numel()
         if n > self.batch_capacity:
             self._alloc(n, self.slack)
+        if self.direct_single_rank and self.world == 1 and self.device.type == "cuda" and n:
+            return self._process_direct(keys, vals, n, to_host)
         dummy_ts = self._dummy_ts(n)  # keyed (non-windowed) records carry no timestamp
         while True:
             K.step_begin(self.cursor, self.stats)
@@ -171,10 +213,12 @@ class KeyedRollingOperator:
                                self.cnt_g.data_ptr(), self.flags.data_ptr(), code, consts,
                                self.out_key.data_ptr(), self.out_val.data_ptr(),
                                self.out_tag.data_ptr(), self.out_n.data_ptr(), cap)
+        return self._emit(to_host)
+
+    def _emit(self, to_host: bool):
         if not to_host:
             return self.out_n
-        k = int(self.out_n.item())
-        k = min(k, cap)
+        k = min(int(self.out_n.item()), self.out_key.numel())
         return RollingRows(self.out_key[:k].cpu().numpy().copy().view(np.uint64),
                            self.out_val[:k].cpu().numpy().copy(),
                            self.out_tag[:k].cpu().numpy().copy())

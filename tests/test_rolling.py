@@ -70,14 +70,21 @@ def test_rolling_filter_epilogue_cpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("agg", [K.AGG_SUM_I64, K.AGG_MAX_I64, K.AGG_COUNT])
 @pytest.mark.parametrize("nkeys", [10, 10_000])
-def test_rolling_gpu_equals_cpu(gpu_device, agg, nkeys):
+@pytest.mark.parametrize("direct", [True, False])
+def test_rolling_gpu_equals_cpu(gpu_device, agg, nkeys, direct):
+    """direct=True: single-rank lookup from the source columns + slot-bits sort;
+    direct=False: the partitioned path every rank takes at world size > 1."""
     res = {}
     for d in (gpu_device, torch.device("cpu")):
         op = KeyedRollingOperator(agg=agg, device=d, max_keys=nkeys, batch_capacity=1 << 16)
+        op.direct_single_rank = direct
         got = {}
         for s in range(3):
             keys, vals = _gen(d, 1 << 16, nkeys, s)
             for k, v in _per_key(op.process(keys, vals)).items():
                 got.setdefault(k, []).extend(v)
         res[d.type] = got
+        if d.type == "cuda":
+            tags = op.process(*_gen(d, 1 << 16, nkeys, 9)).tags
+            assert len(tags) == 1 << 16 and len(np.unique(tags)) == 1 << 16
     assert res["cuda"] == res["cpu"]

@@ -64,3 +64,20 @@ def test_parse_error_has_java_text(gpu_device):
         T.parse_text_gpu(data, [(3, T.FK_DOUBLE)], " ", 0, gpu_device)
     with pytest.raises(T.ParseError, match="ArrayIndexOutOfBounds"):
         T.parse_text_gpu(b"1 h\n", [(3, T.FK_DOUBLE)], " ", 0, gpu_device)
+
+
+@pytest.mark.gpu
+def test_pinned_batch_matches_bytes(gpu_device):
+    """A pinned host batch (the socket ring's slot) parses identically to the bytes path,
+    including lines the kernel hands back to the host runtime."""
+    lines = [f"{1563452056 + i} 10.8.{i % 7}.{i % 251} cpu{i % 64} {(i * 7.31) % 100:.2f}"
+             for i in range(5000)]
+    lines[17] = "1 h cpu1 87.5d"  # Java suffix: host patch path
+    data = ("\n".join(lines) + "\n").encode()
+    spec = [(0, T.FK_LONG), (1, T.FK_STR), (3, T.FK_DOUBLE)]
+    a = T.parse_text_gpu(data, spec, " ", 0, gpu_device)
+    pinned = T.pinned_text_batch(data)
+    assert pinned.is_pinned()
+    b = T.parse_text_gpu(pinned, spec, " ", 0, gpu_device)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[2], b[2])
+    assert torch.equal(a[1][0], b[1][0]) and torch.equal(a[1][1], b[1][1])
