@@ -1389,19 +1389,47 @@ __global__ __launch_bounds__(256) void rolling_lookup_direct_kernel(
     int shift) {
   if (blockIdx.x == 0 && threadIdx.x == 0) n_out[0] = n;
   const uint32_t mask = (1u << cap_log2) - 1;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint64_t key = keys[i];
-    const uint64_t v = vals[i];
-    const uint64_t sub = sub_table_of(key, nsub_log2);
-    const uint32_t s = global_probe_insert(keys_g + (sub << cap_log2), key, mask);
-    int64_t sk = INT64_MAX;
-    if (s == kNoSlot) {
-      atomicOr(&flags[0], 1u);
-    } else {
-      sk = (int64_t)((((sub << cap_log2) | s) << shift) | i);
+  // Four records per thread per round: their column loads and first-probe table reads are all
+  // issued before any is consumed (the table read is the long-latency step; most records hit
+  // their home slot, the rest fall back to the full insert-or-find probe).
+  constexpr int U = 4;
+  for (uint32_t base = blockIdx.x * blockDim.x * U; base < n; base += gridDim.x * blockDim.x * U) {
+    uint64_t key[U], v[U], home[U], k0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = base + u * blockDim.x + threadIdx.x;
+      key[u] = i < n ? keys[i] : 0;
+      v[u] = i < n ? vals[i] : 0;
     }
-    sort_key[i] = sk;
-    vals_out[i] = v;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = base + u * blockDim.x + threadIdx.x;
+      home[u] = (sub_table_of(key[u], nsub_log2) << cap_log2) | (slot_hash(key[u]) & mask);
+      k0[u] = i < n ? __hip_atomic_load(&keys_g[home[u]], __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT)
+                    : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = base + u * blockDim.x + threadIdx.x;
+      if (i >= n) continue;
+      uint64_t slot;
+      if (k0[u] == key[u]) {
+        slot = home[u];
+      } else {
+        const uint64_t sub = sub_table_of(key[u], nsub_log2);
+        const uint32_t s = global_probe_insert(keys_g + (sub << cap_log2), key[u], mask);
+        slot = s == kNoSlot ? ~0ull : ((sub << cap_log2) | s);
+      }
+      int64_t sk = INT64_MAX;
+      if (slot == ~0ull) {
+        atomicOr(&flags[0], 1u);
+      } else {
+        sk = (int64_t)((slot << shift) | i);
+      }
+      sort_key[i] = sk;
+      vals_out[i] = v[u];
+    }
   }
 }
 
@@ -1411,18 +1439,26 @@ __global__ __launch_bounds__(256) void rolling_heads_kernel(const int64_t* __res
                                                             uint32_t* __restrict__ n_heads,
                                                             int shift) {
   const uint32_t n = *n_in;
-  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-    const uint32_t i = base + threadIdx.x;
-    bool h = false;
-    if (i < n) {
-      const int64_t k = sk[i];
-      h = k != INT64_MAX && (i == 0 || (sk[i - 1] >> shift) != (k >> shift));
+  // Four elements per thread per round, loads issued together (the kernel is load-latency bound).
+  constexpr int U = 4;
+  for (uint32_t base = blockIdx.x * blockDim.x * U; base < n; base += gridDim.x * blockDim.x * U) {
+    int64_t k[U], p[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = base + u * blockDim.x + threadIdx.x;
+      k[u] = i < n ? sk[i] : INT64_MAX;
+      p[u] = (i < n && i > 0) ? sk[i - 1] : 0;
     }
-    const unsigned long long m = __ballot(h);
-    uint32_t wb = 0;
-    if (lane_id() == 0 && m) wb = atomicAdd(n_heads, (uint32_t)__popcll(m));
-    wb = __shfl(wb, 0);
-    if (h) heads[wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = i;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = base + u * blockDim.x + threadIdx.x;
+      const bool h = i < n && k[u] != INT64_MAX && (i == 0 || (p[u] >> shift) != (k[u] >> shift));
+      const unsigned long long m = __ballot(h);
+      uint32_t wb = 0;
+      if (lane_id() == 0 && m) wb = atomicAdd(n_heads, (uint32_t)__popcll(m));
+      wb = __shfl(wb, 0);
+      if (h) heads[wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = i;
+    }
   }
 }
 
@@ -2592,7 +2628,7 @@ void rolling_lookup_direct(const uint64_t* keys, const uint64_t* vals, uint32_t 
   check_roll_layout(shift, shift);
   if ((uint64_t)n > (1ull << shift))
     throw std::invalid_argument("rolling_lookup_direct: arrival index does not fit the shift");
-  hipLaunchKernelGGL(rolling_lookup_direct_kernel, dim3(grid_for(n > 0 ? n : 1, 256, 8192)),
+  hipLaunchKernelGGL(rolling_lookup_direct_kernel, dim3(grid_for(n > 0 ? (n + 3) / 4 : 1, 256, 8192)),
                      dim3(256), 0, (hipStream_t)stream, keys, vals, n, nsub_log2, cap_log2, keys_g,
                      sort_key, vals_out, n_out, flags, shift);
   HIP_CHECK(hipGetLastError());
@@ -2600,7 +2636,7 @@ void rolling_lookup_direct(const uint64_t* keys, const uint64_t* vals, uint32_t 
 
 void rolling_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
                    uint32_t* n_heads, int shift, intptr_t stream) {
-  hipLaunchKernelGGL(rolling_heads_kernel, dim3(grid_for(n_cap, 256, 8192)), dim3(256), 0,
+  hipLaunchKernelGGL(rolling_heads_kernel, dim3(grid_for((n_cap + 3) / 4, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, sk, n_in, heads, n_heads, shift);
   HIP_CHECK(hipGetLastError());
 }
