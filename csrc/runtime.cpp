@@ -133,7 +133,7 @@ class StringDict {
     return intern_locked(s);
   }
   uint64_t intern_locked(std::string_view s) {
-    auto it = ids_.find(std::string(s));
+    auto it = ids_.find(s);  // no temporary std::string per lookup
     if (it != ids_.end()) return it->second;
     const uint64_t id = strs_.size();
     strs_.emplace_back(s);
@@ -151,13 +151,14 @@ class StringDict {
     if (!jhash_.empty()) std::memcpy(a.mutable_data(), jhash_.data(), jhash_.size() * 4);
     return a;
   }
-  std::vector<std::string> strings() const { return strs_; }
+  std::vector<std::string> strings() const { return {strs_.begin(), strs_.end()}; }
   std::mutex& mu() { return mu_; }
 
  private:
   std::mutex mu_;
-  std::unordered_map<std::string, uint64_t> ids_;
-  std::vector<std::string> strs_;
+  // Keys view the interned strings; a deque never relocates its elements, so the views stay valid.
+  std::deque<std::string> strs_;
+  std::unordered_map<std::string_view, uint64_t> ids_;
   std::vector<int32_t> jhash_;
 };
 

@@ -71,6 +71,10 @@ def config1(steps: int, warmup: int, lines_per_step: int = 1 << 20, device: str 
         return int(keep.sum())
 
     step = step_gpu if device != "cpu" else step_cpu
+    if device == "cpu":
+        # The CPU path is the single-threaded C++ runtime; torch's intra-op pool only adds
+        # fork/join overhead to the two tiny tensor ops per step (measured 150 ms vs 9 ms).
+        torch.set_num_threads(1)
 
     for _ in range(warmup):
         step()
