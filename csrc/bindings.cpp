@@ -223,8 +223,9 @@ PYBIND11_MODULE(_mxs_native, m) {
     gpu::step_begin(P<uint32_t>(cursor), nb, P<int64_t>(stats), stream);
   });
   m.def("gpu_step_finish", [](intptr_t stats, intptr_t lm, int64_t bound, int32_t ev,
-                              int64_t now, intptr_t red, intptr_t stream) {
-    gpu::step_finish(P<int64_t>(stats), P<int64_t>(lm), bound, ev, now, P<int64_t>(red), stream);
+                              int64_t now, intptr_t red, intptr_t flags, intptr_t stream) {
+    gpu::step_finish(P<int64_t>(stats), P<int64_t>(lm), bound, ev, now, P<int64_t>(red),
+                     P<uint32_t>(flags), stream);
   });
   m.def("gpu_rolling_lookup", [](intptr_t recs, intptr_t counts, int nsrc, int nsub, uint32_t bcap,
                                  int cap_log2, intptr_t keys_g, intptr_t sk, intptr_t vals,
@@ -438,8 +439,9 @@ PYBIND11_MODULE(_mxs_native, m) {
     cpu::step_begin(P<uint32_t>(cursor), nb, P<int64_t>(stats));
   });
   m.def("cpu_step_finish", [](intptr_t stats, intptr_t lm, int64_t bound, int32_t ev, int64_t now,
-                              intptr_t red) {
-    cpu::step_finish(P<int64_t>(stats), P<int64_t>(lm), bound, ev, now, P<int64_t>(red));
+                              intptr_t red, intptr_t flags) {
+    cpu::step_finish(P<int64_t>(stats), P<int64_t>(lm), bound, ev, now, P<int64_t>(red),
+                     P<uint32_t>(flags));
   });
   m.def("cpu_rolling_rows", [](intptr_t recs, intptr_t counts, int nsrc, int nsub, uint32_t bcap,
                                int cap_log2, int agg, intptr_t keys_g, intptr_t acc_g,

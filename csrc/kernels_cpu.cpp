@@ -55,6 +55,10 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
     const int64_t t = ts[i];
     tmax = std::max(tmax, t);
     uint32_t rt = 0;
+    if (key >= kTombKey) {  // reserved ids (tombstone / empty-slot / hole markers): reported
+      ovf |= 8;
+      continue;
+    }
     if (p.window_mode) {
       if (p.drop_late && t < p.late_ts) {
         if (late_idx) {
@@ -108,7 +112,7 @@ void step_begin(uint32_t* cursor, int nb, int64_t* stats) {
 }
 
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
-                 int64_t proc_now, int64_t* red) {
+                 int64_t proc_now, int64_t* red, const uint32_t* flags) {
   int64_t lm = std::max(local_maxts[0], stats[kStatMaxTs]);
   local_maxts[0] = lm;
   const int64_t wm = event_mode ? (lm == INT64_MIN ? INT64_MIN : lm - bound) : proc_now;
@@ -119,7 +123,8 @@ void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int3
   red[3] = -(stats[kStatOverflow] & 1);
   red[4] = -((stats[kStatOverflow] >> 1) & 1);
   red[5] = -((stats[kStatOverflow] >> 2) & 1);  // compact records cannot hold a value
-  red[6] = red[7] = 0;
+  red[6] = flags ? -(int64_t)(flags[0] & 1u) : 0;  // a key found no slot (table full), sticky
+  red[7] = -((stats[kStatOverflow] >> 3) & 1);  // the reserved key id ~0 occurred
   for (int j = 0; j < kStatCount; ++j) red[8 + j] = stats[j];
 }
 

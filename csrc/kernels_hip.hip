@@ -105,7 +105,8 @@ __global__ __launch_bounds__(256) void gen_events_kernel(
 // ------------------------------------------------------------------------------------------
 // Per-element partition decision; identical code runs in pass A (histogram) and pass B
 // (scatter) so both passes agree without storing per-element bucket ids.
-// kind: 0 = keep, 1 = late (dropped), 2 = unrepresentable pane (overflow)
+// kind: 0 = keep, 1 = late (dropped), 2 = unrepresentable pane (overflow), 3 = reserved key id
+// (~0 is the tables' empty-slot marker and the partition's hole marker: reported, never stored)
 struct PartEval {
   int kind;
   uint32_t bucket;
@@ -120,6 +121,10 @@ __device__ __forceinline__ PartEval part_eval(uint64_t key, int64_t ts, const in
   e.kind = 0;
   e.t = 0;
   e.bucket = 0;
+  if (key >= kTombKey) {  // ~1 / ~0: tombstone and empty-slot markers of the tables
+    e.kind = 3;
+    return e;
+  }
   if (p.window_mode) {
     if (p.drop_late && ts < p.late_ts) {
       e.kind = 1;
@@ -190,7 +195,7 @@ __global__ __launch_bounds__(1024) void partition_kernel(
   const int64_t end = start + chunk < n ? start + chunk : n;
   const int64_t bstep = (int64_t)blockDim.x * kPlainU;
   int64_t tmax = INT64_MIN, qmin = INT64_MAX, qmax = INT64_MIN, nlate = 0, nacc = 0;
-  bool bad = false;
+  int bad = 0;  // stats overflow bits: 2 unrepresentable pane, 8 reserved key
 
   // Pass A: histogram + stats.
   for (int64_t i0 = start + threadIdx.x; i0 < end; i0 += bstep) {
@@ -211,8 +216,8 @@ __global__ __launch_bounds__(1024) void partition_kernel(
       tmax = t[u] > tmax ? t[u] : tmax;
       const PartEval e = part_eval(k[u], t[u], jhash_tab, plan, kg_dest);
       if (e.kind) {
-        if (e.kind == 2) {
-          bad = true;
+        if (e.kind >= 2) {
+          bad |= e.kind == 2 ? 2 : 8;
           continue;
         }
         ++nlate;
@@ -295,7 +300,7 @@ __global__ __launch_bounds__(1024) void partition_kernel(
   nacc = block_reduce_i64(nacc, lred, 2);
   if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
   const int64_t flags = block_reduce_i64(overflow ? 1 : 0, lred, 0) |
-                        block_reduce_i64(bad ? 2 : 0, lred, 0) |
+                        block_reduce_i64(bad & 2, lred, 0) | block_reduce_i64(bad & 8, lred, 0) |
                         block_reduce_i64(wide ? 4 : 0, lred, 0);
   if (threadIdx.x == 0) {
     atomicMax((long long*)&stats[kStatMaxTs], (long long)tmax);
@@ -384,7 +389,7 @@ __global__ __launch_bounds__(1024) void partition_staged_kernel(
   const int64_t start = (int64_t)blockIdx.x * chunk;
   const int64_t end = start + chunk < n ? start + chunk : n;
   int64_t tmax = INT64_MIN, qmin = INT64_MAX, qmax = INT64_MIN, nlate = 0, nacc = 0;
-  bool bad = false;
+  int bad = 0;  // stats overflow bits: 2 unrepresentable pane, 8 reserved key
 
   // Pass A: histogram (into run_base) + stats.
   for (int64_t i0 = start + threadIdx.x; i0 < end; i0 += (int64_t)blockDim.x * kPartU) {
@@ -405,8 +410,8 @@ __global__ __launch_bounds__(1024) void partition_staged_kernel(
       tmax = t[u] > tmax ? t[u] : tmax;
       const PartEval e = part_eval(k[u], t[u], jhash_tab, plan, kg_dest);
       if (e.kind) {
-        if (e.kind == 2) {
-          bad = true;
+        if (e.kind >= 2) {
+          bad |= e.kind == 2 ? 2 : 8;
           continue;
         }
         ++nlate;
@@ -556,7 +561,8 @@ __global__ __launch_bounds__(1024) void partition_staged_kernel(
   qmax = block_reduce_i64(qmax, lred, 0);
   nacc = block_reduce_i64(nacc, lred, 2);
   if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
-  const int64_t flags = (any_ovf ? 1 : 0) | block_reduce_i64(bad ? 2 : 0, lred, 0);
+  const int64_t flags = (any_ovf ? 1 : 0) | block_reduce_i64(bad & 2, lred, 0) |
+                        block_reduce_i64(bad & 8, lred, 0);
   if (threadIdx.x == 0) {
     atomicMax((long long*)&stats[kStatMaxTs], (long long)tmax);
     if (nacc) {
@@ -729,8 +735,8 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
             const unsigned long long pos = atomicAdd((unsigned long long*)&stats[kStatLate], 1ull);
             if (pos < late_cap) late_idx[pos] = (uint32_t)i;
           }
-        } else if (e.kind == 2) {
-          flags |= 2;
+        } else if (e.kind >= 2) {
+          flags |= e.kind == 2 ? 2 : 8;
         } else {
           if ((int64_t)(int32_t)v != (int64_t)v) flags |= 4;  // needs 24-byte records
           qmin32 = e.t < qmin32 ? e.t : qmin32;
@@ -789,7 +795,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   qmax = block_reduce_i64(qmax, lred, 0);
   if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
   flags = (any_ovf ? 1 : 0) | block_reduce_i64(flags & 2, lred, 0) |
-          block_reduce_i64(flags & 4, lred, 0);
+          block_reduce_i64(flags & 4, lred, 0) | block_reduce_i64(flags & 8, lred, 0);
   if (threadIdx.x == 0) {
     atomicMax((long long*)&stats[kStatMaxTs], (long long)tmax);
     if (nacc) {
@@ -820,7 +826,7 @@ __global__ __launch_bounds__(256) void step_begin_kernel(uint32_t* __restrict__ 
 // a copy of the raw stats for the host (red[8..15]).
 __global__ void step_finish_kernel(const int64_t* __restrict__ stats, int64_t* __restrict__ local_maxts,
                                    int64_t bound, int32_t event_mode, int64_t proc_now,
-                                   int64_t* __restrict__ red) {
+                                   int64_t* __restrict__ red, const uint32_t* __restrict__ flags) {
   if (threadIdx.x != 0) return;
   int64_t lm = local_maxts[0];
   const int64_t bm = stats[kStatMaxTs];
@@ -834,7 +840,8 @@ __global__ void step_finish_kernel(const int64_t* __restrict__ stats, int64_t* _
   red[3] = -(stats[kStatOverflow] & 1);
   red[4] = -((stats[kStatOverflow] >> 1) & 1);
   red[5] = -((stats[kStatOverflow] >> 2) & 1);  // compact records cannot hold a value
-  red[6] = red[7] = 0;
+  red[6] = flags ? -(int64_t)(flags[0] & 1u) : 0;  // a key found no slot (table full), sticky
+  red[7] = -((stats[kStatOverflow] >> 3) & 1);  // the reserved key id ~0 occurred
   for (int j = 0; j < kStatCount; ++j) red[8 + j] = stats[j];
 }
 
@@ -1413,6 +1420,12 @@ __global__ __launch_bounds__(256) void rolling_lookup_direct_kernel(
     for (int u = 0; u < U; ++u) {
       const uint32_t i = base + u * blockDim.x + threadIdx.x;
       if (i >= n) continue;
+      if (key[u] >= kTombKey) {  // reserved ids (table markers): flagged, never stored
+        atomicOr(&flags[0], 4u);
+        sort_key[i] = INT64_MAX;
+        vals_out[i] = v[u];
+        continue;
+      }
       uint64_t slot;
       if (k0[u] == key[u]) {
         slot = home[u];
@@ -1557,7 +1570,7 @@ __global__ __launch_bounds__(256) void rolling_scan_kernel(
 // in a device spill set; their records are diverted to the host SessionStore (csrc/sessions.cpp).
 // ------------------------------------------------------------------------------------------
 constexpr int kSess = 4;
-constexpr uint64_t kTombKey = ~1ull;  // evicted slot (probing continues past it)
+// kTombKey (mxs_common.h): evicted slot, probing continues past it
 
 struct SessArgs {
   int64_t gap, lateness, wm, tbase;
@@ -2380,9 +2393,9 @@ void step_begin(uint32_t* cursor, int nb, int64_t* stats, intptr_t stream) {
 }
 
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
-                 int64_t proc_now, int64_t* red, intptr_t stream) {
+                 int64_t proc_now, int64_t* red, const uint32_t* flags, intptr_t stream) {
   hipLaunchKernelGGL(step_finish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, stats,
-                     local_maxts, bound, event_mode, proc_now, red);
+                     local_maxts, bound, event_mode, proc_now, red, flags);
   HIP_CHECK(hipGetLastError());
 }
 

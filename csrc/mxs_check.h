@@ -15,7 +15,7 @@
 
 namespace mxs {
 
-constexpr uint64_t kTombKey = ~0ull - 1;  // session tables' deleted-slot marker
+// kTombKey (mxs_common.h): session tables' deleted-slot marker
 
 enum CheckStat { kChkLive = 0, kChkMisplaced = 1, kChkBrokenChain = 2, kChkDuplicate = 3, kChkN = 4 };
 

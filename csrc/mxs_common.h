@@ -26,6 +26,9 @@ namespace mxs {
 // Empty slot marker of the keyed hash tables. User keys are 64-bit ids (integer keys, or string
 // dictionary ids assigned by the host); the all-ones id is reserved.
 constexpr uint64_t kEmptyKey = ~0ull;
+// Tombstone marker of tables with deletion (sessions). Keys >= kTombKey (ids -1 and -2) are
+// reserved: the partition pass reports them instead of routing them.
+constexpr uint64_t kTombKey = ~1ull;
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 
 // Shuffle / bucket record: 24 bytes, AoS so one all-to-all moves a whole bucket range.

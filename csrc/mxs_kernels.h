@@ -142,7 +142,7 @@ void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_
                   const ExprProg& filt, uint64_t* out_key, uint64_t* out_val, int64_t* out_tag,
                   uint32_t* out_n, uint32_t out_cap, int abits, int shift, intptr_t stream);
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
-                 int64_t proc_now, int64_t* red, intptr_t stream);
+                 int64_t proc_now, int64_t* red, const uint32_t* flags, intptr_t stream);
 }  // namespace gpu
 
 // ---- CPU twins (kernels_cpu.cpp) ------------------------------------------------------------
@@ -170,7 +170,7 @@ void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, u
                   uint32_t* flags, const ExprProg& filt, uint64_t* out_key, uint64_t* out_val,
                   int64_t* out_tag, uint32_t* out_n, uint32_t out_cap);
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
-                 int64_t proc_now, int64_t* red);
+                 int64_t proc_now, int64_t* red, const uint32_t* flags);
 void keygroups(const uint64_t* keys, int64_t n, int hash_mode, const int32_t* jhash, int max_par,
                int32_t* kg);
 void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,

@@ -222,9 +222,9 @@ class WindowPipeline {
                          stats_, nullptr, 0);
       }
       if (mem_.gpu)
-        gpu::step_finish(stats_, local_maxts_, ooo_, 1, 0, red_, (intptr_t)mem_.stream);
+        gpu::step_finish(stats_, local_maxts_, ooo_, 1, 0, red_, nullptr, (intptr_t)mem_.stream);
       else
-        cpu::step_finish(stats_, local_maxts_, ooo_, 1, 0, red_);
+        cpu::step_finish(stats_, local_maxts_, ooo_, 1, 0, red_, nullptr);
       mem_.to_host(host, red_, sizeof(host));  // the step's single host sync
       if (host[4]) throw std::runtime_error("event timestamp outside the representable pane range");
       if (host[5]) {

@@ -69,7 +69,7 @@ int main() {
     cpu::partition(keys.data(), ts.data(), vals.data(), nullptr, m, pp, kg_dest.data(),
                    cursor.data(), recs.data(), stats.data(), late_idx.data(),
                    (uint32_t)late_idx.size());
-    cpu::step_finish(stats.data(), local_maxts.data(), 400, 1, 0, red.data());
+    cpu::step_finish(stats.data(), local_maxts.data(), 400, 1, 0, red.data(), nullptr);
     if (stats[kStatOverflow]) return fail("bucket overflow");
     const int64_t qmin = stats[kStatMinPane], qmax = stats[kStatMaxPane];
     if (qmin > qmax) continue;

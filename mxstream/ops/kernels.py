@@ -262,17 +262,24 @@ def step_begin(cursor: torch.Tensor, stats: torch.Tensor) -> None:
         m.cpu_step_begin(_p(cursor), cursor.numel(), _p(stats))
 
 
-RED_WORDS = 16  # [-qmax, qmin, wm, -bucket_ovf, -pane_ovf, 0, 0, 0, stats[8]]
+RED_WORDS = 16  # [-qmax, qmin, wm, -bucket_ovf, -pane_ovf, -compact_ovf, -table_full, 0, stats[8]]
 
 
 def step_finish(stats: torch.Tensor, local_maxts: torch.Tensor, red: torch.Tensor, *,
-                bound: int, event_mode: bool, proc_now: int) -> None:
+                bound: int, event_mode: bool, proc_now: int,
+                flags: torch.Tensor | None = None) -> None:
+    """Reduce the partition stats into the step's all-reduce vector (RED_WORDS). With the
+    operator's `flags`, red[6] = -(table full): a key that found no slot in a previous
+    aggregation surfaces in the step's one host sync."""
     dev = stats.device
     _check(stats, torch.int64, STAT_COUNT, "stats", dev)
     _check(local_maxts, torch.int64, 1, "local_maxts", dev)
     _check(red, torch.int64, RED_WORDS, "red", dev)
+    if flags is not None:
+        _check(flags, torch.int32, 1, "flags", dev)
     m = load()
-    args = (_p(stats), _p(local_maxts), int(bound), int(event_mode), int(proc_now), _p(red))
+    args = (_p(stats), _p(local_maxts), int(bound), int(event_mode), int(proc_now), _p(red),
+            _p(flags))
     if _is_gpu(stats):
         m.gpu_step_finish(*args, _stream(stats))
     else:

@@ -63,6 +63,193 @@ class LocalComm(Comm):
         return None
 
 
+class LoopbackGroup:
+    """G virtual ranks inside ONE process (SURVEY.md §2.5 "testing": LoopbackComm).
+
+    Every virtual rank is a thread that owns its operator instances and calls the collectives in
+    the same order a real rank would. The exchange has exactly ``all_to_all_single``'s layout
+    (equal split, chunk j of rank i lands in chunk i of rank j); on a GPU the chunks move with
+    device-to-device copies on the reading rank's current stream, ordered against the producing
+    rank's stream with HIP events (deposit event -> reader waits; reader-done events -> the
+    producer waits before it may overwrite its buffer). So the whole G>1 GPU path -- key-group
+    partition, combiner, combined-record aggregation, overflow regrow, watermark valve -- runs on
+    one MI355X (or on the CPU twins) with RCCL's data layout, without RCCL.
+    """
+
+    def __init__(self, world: int, timeout_s: float = 600.0):
+        import threading
+
+        if world < 1:
+            raise ValueError("world must be >= 1")
+        self.world = world
+        self.timeout_s = timeout_s
+        self._barrier = threading.Barrier(world, timeout=timeout_s)
+        self._slots: list = [None] * world
+        self._events: list = [None] * world
+        self._done: list = [[None] * world for _ in range(world)]
+        self.a2a_bytes = 0
+
+    def comm(self, rank: int) -> "LoopbackComm":
+        return LoopbackComm(self, rank)
+
+    def abort(self) -> None:
+        self._barrier.abort()
+
+    def wait(self) -> None:
+        self._barrier.wait()
+
+
+def _record_event(t: torch.Tensor):
+    if t.device.type != "cuda":
+        return None
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(t.device))
+    return ev
+
+
+def _wait_event(t: torch.Tensor, ev) -> None:
+    if ev is not None:
+        torch.cuda.current_stream(t.device).wait_event(ev)
+
+
+class LoopbackComm(Comm):
+    """One virtual rank of a LoopbackGroup (same interface as TorchComm)."""
+
+    def __init__(self, group: LoopbackGroup, rank: int):
+        self.group_obj = group
+        self.group = None
+        self.rank = rank
+        self.world = group.world
+        self.backend = "loopback"
+
+    # Collective skeleton: deposit -> barrier -> read peers -> barrier (peers done reading) ->
+    # the owner's stream waits for the readers' events before it reuses its buffer.
+    def _deposit(self, t) -> None:
+        g = self.group_obj
+        g._slots[self.rank] = t
+        g._events[self.rank] = _record_event(t) if isinstance(t, torch.Tensor) else None
+        g.wait()
+
+    def _finish(self, t) -> None:
+        g = self.group_obj
+        g.wait()
+        if isinstance(t, torch.Tensor) and t.device.type == "cuda":
+            for src in range(self.world):
+                _wait_event(t, g._done[src][self.rank])
+        g.wait()  # every rank consumed its done events before the next collective reuses them
+
+    def _read(self, src: int, like: torch.Tensor) -> torch.Tensor:
+        g = self.group_obj
+        _wait_event(like, g._events[src])
+        return g._slots[src]
+
+    def _mark_read(self, src: int, like: torch.Tensor) -> None:
+        self.group_obj._done[self.rank][src] = _record_event(like)
+
+    def all_to_all(self, out, inp):
+        if out.numel() != inp.numel() or inp.numel() % self.world:
+            raise ValueError("all_to_all: equal split needs numel divisible by world")
+        if self.world == 1:
+            LocalComm.all_to_all(self, out, inp)
+            return
+        self._deposit(inp)
+        c = inp.numel() // self.world
+        for src in range(self.world):
+            peer = self._read(src, out)
+            out[src * c:(src + 1) * c].copy_(peer[self.rank * c:(self.rank + 1) * c],
+                                             non_blocking=True)
+            self._mark_read(src, out)
+        if self.rank == 0:
+            self.group_obj.a2a_bytes += inp.numel() * inp.element_size() * self.world
+        self._finish(inp)
+
+    def _allreduce(self, t, op) -> None:
+        if self.world == 1:
+            return
+        self._deposit(t)
+        acc = t.clone()
+        for src in range(self.world):
+            if src == self.rank:
+                self._mark_read(src, t)
+                continue
+            peer = self._read(src, t)
+            acc = op(acc, peer)
+            self._mark_read(src, t)
+        # Nobody may overwrite its own input before every peer has read it.
+        g = self.group_obj
+        g.wait()
+        if t.device.type == "cuda":
+            for src in range(self.world):
+                _wait_event(t, g._done[src][self.rank])
+        t.copy_(acc)
+        g.wait()
+
+    def allreduce_min_(self, t):
+        self._allreduce(t, torch.minimum)
+
+    def allreduce_max_(self, t):
+        self._allreduce(t, torch.maximum)
+
+    def allreduce_sum_(self, t):
+        self._allreduce(t, torch.add)
+
+    def barrier(self):
+        if self.world > 1:
+            self.group_obj.wait()
+
+    def broadcast_object(self, obj, src: int = 0):
+        if self.world == 1:
+            return obj
+        g = self.group_obj
+        g._slots[self.rank] = obj
+        g.wait()
+        v = g._slots[src]
+        g.wait()
+        return v
+
+    def all_gather_object(self, obj):
+        if self.world == 1:
+            return [obj]
+        g = self.group_obj
+        g._slots[self.rank] = obj
+        g.wait()
+        v = list(g._slots)
+        g.wait()
+        return v
+
+
+def run_loopback(world: int, fn, *args, device: torch.device | None = None,
+                 timeout_s: float = 600.0) -> list:
+    """Run ``fn(comm, *args)`` on `world` virtual ranks (threads) of one LoopbackGroup and return
+    the per-rank results in rank order. An exception on any rank aborts the group (the others
+    leave their barrier with BrokenBarrierError) and is re-raised here."""
+    import threading
+
+    group = LoopbackGroup(world, timeout_s=timeout_s)
+    res: list = [None] * world
+    errs: list = [None] * world
+
+    def body(r):
+        try:
+            if device is not None and device.type == "cuda":
+                torch.cuda.set_device(device)
+            res[r] = fn(group.comm(r), *args)
+        except BaseException as e:  # noqa: BLE001 - re-raised on the caller's thread
+            errs[r] = e
+            group.abort()
+
+    ths = [threading.Thread(target=body, args=(r,), name=f"mxs-loopback-{r}") for r in range(world)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    first = next((e for e in errs if e is not None and not isinstance(e, threading.BrokenBarrierError)),
+                 next((e for e in errs if e is not None), None))
+    if first is not None:
+        raise first
+    return res
+
+
 class TorchComm(Comm):
     """torch.distributed process group: backend 'nccl' (= RCCL over xGMI) or 'gloo' (CPU)."""
 
@@ -74,11 +261,23 @@ class TorchComm(Comm):
         self.world = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
 
+    def _data_group(self):
+        """The keyBy payload travels on its own communicator: RCCL runs each communicator's
+        collectives on its own internal stream, so the all-to-all of step i (issued on the
+        operator's state stream) does not queue behind the watermark all-reduce of step i+1,
+        which waits for that step's partition kernel. Created on the first all-to-all, which
+        every rank reaches in the same order."""
+        g = getattr(self, "_dgroup", None)
+        if g is None:
+            ranks = dist.get_process_group_ranks(self.group) if self.group is not None else None
+            g = self._dgroup = dist.new_group(ranks=ranks, backend=self.backend)
+        return g
+
     def all_to_all(self, out, inp):
         if self.world == 1:
             LocalComm.all_to_all(self, out, inp)
             return
-        dist.all_to_all_single(out, inp, group=self.group)
+        dist.all_to_all_single(out, inp, group=self._data_group())
 
     def allreduce_min_(self, t):
         if self.world > 1:

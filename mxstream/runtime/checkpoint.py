@@ -222,12 +222,9 @@ class CheckpointCoordinator:
         """Savepoint (all ranks must pass the same `target`; rank 0's directory name wins)."""
         self.complete_pending()
         d = self.storage.new_savepoint_dir(target)
-        name = [d.name]
         if self.world > 1:
-            import torch.distributed as dist
-
-            dist.broadcast_object_list(name, src=0)
-            d = d.parent / name[0]
+            # the communicator's group (not the default one): operators may run on a subgroup
+            d = d.parent / self.comm.broadcast_object(d.name, src=0)
         self._write(d, "savepoint", step, sources, extra)
         return d
 
@@ -344,11 +341,21 @@ class CheckpointCoordinator:
         self._pending = None
         p["thread"].join()
         res = p["result"]
-        if "error" in res:
-            raise RuntimeError(f"async checkpoint {p['id']} failed") from res["error"]
         d = p["dir"]
-        gathered = self._gather({"rank": self.rank, "ops": res["op_meta"],
-                                 "sources": p["sources"] or {}, "bytes": res["nbytes"]})
+        # Every rank joins the acknowledgement, failed or not, so a rank whose export failed
+        # (disk error, ...) does not leave the others blocked in the collective until its
+        # timeout: all ranks learn the failure together, nobody writes _metadata, all raise.
+        err = res.get("error")
+        gathered = self._gather({"rank": self.rank, "error": repr(err) if err else None,
+                                 "ops": res.get("op_meta"), "sources": p["sources"] or {},
+                                 "bytes": res.get("nbytes", 0)})
+        failed = [(g["rank"], g["error"]) for g in gathered if g.get("error")]
+        if failed:
+            self.comm.barrier()
+            msg = f"async checkpoint {p['id']} failed on rank(s) {failed}"
+            if err is not None:
+                raise RuntimeError(msg) from err
+            raise RuntimeError(msg)
         if self.rank == 0:
             ops_all = {uid: {"files": [g["ops"][uid]["file"] for g in gathered],
                              "rows": [g["ops"][uid]["rows"] for g in gathered],
@@ -372,11 +379,7 @@ class CheckpointCoordinator:
     def _gather(self, obj: dict) -> list[dict]:
         if self.world == 1:
             return [obj]
-        import torch.distributed as dist
-
-        out = [None] * self.world
-        dist.all_gather_object(out, obj)
-        return out
+        return self.comm.all_gather_object(obj)
 
     def _prune(self) -> None:
         done = self.storage.completed_checkpoints()

@@ -99,7 +99,9 @@ class KeyedRollingOperator:
         self.out_key = torch.empty(ocap, dtype=torch.int64, device=dev)
         self.out_val = torch.empty(ocap, dtype=torch.int64, device=dev)
         self.out_tag = torch.empty(ocap, dtype=torch.int64, device=dev)
-        self.out_n = torch.zeros(1, dtype=torch.int32, device=dev)
+        # flags[2] is the emitted-row cursor: one D2H returns the row count with the table-full
+        # (bit0) and reserved-key (bit2) flags of flags[0].
+        self.out_n = self.flags[2:3]
 
     def _process_direct(self, keys: torch.Tensor, vals: torch.Tensor, n: int, to_host: bool):
         """Single-rank GPU path: every key group is local, so the table lookup reads the source
@@ -110,6 +112,11 @@ class KeyedRollingOperator:
         st = torch.cuda.current_stream(self.device).cuda_stream
         keys = keys.contiguous()
         vals = vals.contiguous()
+        # The kernel reads both columns straight from these pointers: validate like K.partition.
+        K._check(keys, torch.int64, n, "keys", self.device)
+        K._check(vals, torch.int64, n, "vals", self.device)
+        if n >= (1 << 32) or n > self.sort_key.numel():
+            raise ValueError("batch larger than the operator's buffers")
         self.records_in += n
         self.steps += 1
         self.out_n.zero_()
@@ -157,13 +164,17 @@ class KeyedRollingOperator:
                 K.partition(keys, dummy_ts, vals, plan, self.kg_dest, self.cursor, self.send,
                             self.stats)
             K.step_finish(self.stats, self.local_maxts, self.red, bound=0, event_mode=True,
-                          proc_now=0)
+                          proc_now=0, flags=self.flags)
             self.red[5] = -n  # the largest batch over ranks sizes the arrival bits of the sort key
-            self.comm.allreduce_min_(self.red[3:6])
+            self.comm.allreduce_min_(self.red[3:8])
             if self.world > 1:
                 self.comm.all_to_all(self.recv, self.send)
                 self.comm.all_to_all(self.recv_counts, self.cursor)
-            red = self.red[3:6].tolist()
+            red = self.red[3:8].tolist()
+            if red[3]:
+                raise RuntimeError("keyed state table full: a key found no free slot (raise max_keys)")
+            if red[4]:
+                raise ValueError("key ids -1 and -2 are reserved (the state tables' markers)")
             if red[0]:
                 self._alloc(self.batch_capacity, self.slack * 2)
                 continue
@@ -215,10 +226,20 @@ class KeyedRollingOperator:
                                self.out_tag.data_ptr(), self.out_n.data_ptr(), cap)
         return self._emit(to_host)
 
+    def check(self) -> int:
+        """Host check of the sticky flags (table full, reserved key); returns the last step's
+        emitted row count. to_host=False callers (benchmarks) call it at the end."""
+        hf = self.flags.tolist()
+        if hf[0] & 1:
+            raise RuntimeError("keyed state table full: a key found no free slot (raise max_keys)")
+        if hf[0] & 4:
+            raise ValueError("key ids -1 and -2 are reserved (the state tables' markers)")
+        return hf[2]
+
     def _emit(self, to_host: bool):
         if not to_host:
             return self.out_n
-        k = min(int(self.out_n.item()), self.out_key.numel())
+        k = min(self.check(), self.out_key.numel())
         return RollingRows(self.out_key[:k].cpu().numpy().copy().view(np.uint64),
                            self.out_val[:k].cpu().numpy().copy(),
                            self.out_tag[:k].cpu().numpy().copy())

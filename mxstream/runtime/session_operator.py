@@ -242,13 +242,15 @@ class KeyedSessionOperator:
                 K.partition(keys, ts, vals, plan, self.kg_dest, self.cursor, self.send, self.stats)
             K.step_finish(self.stats, self.local_maxts, self.red, bound=self.ooo_bound,
                           event_mode=True, proc_now=0)
-            self.comm.allreduce_min_(self.red[:5])
+            self.comm.allreduce_min_(self.red[:8])
             if self.world > 1:
                 self.comm.all_to_all(self.recv, self.send)
                 self.comm.all_to_all(self.recv_counts, self.cursor)
             host = self.red.cpu().tolist()
             if host[4]:
                 raise RuntimeError("session batch spans more than 2^32 ms")
+            if host[7]:
+                raise ValueError("key ids -1 and -2 are reserved (the state tables' markers)")
             if host[3]:
                 self._alloc(self.batch_capacity, self.slack * 2)
                 continue

@@ -38,7 +38,9 @@ class VectorWindowOperator(KeyedWindowOperator):
                 raise TypeError(f"VectorWindowOperator does not take {k!r}")
         self.dim = int(dim)
         # Records carry the event's row index as an int32 value: compact 16-byte records on GPU.
-        super().__init__(agg=K.AGG_SUM_I64, combine=False, cap_log2=cap_log2, **kw)
+        # Not pipelined: the vectors of a batch are gathered into the send layout during its own
+        # call (the caller may reuse `vecs` right after process() returns).
+        super().__init__(agg=K.AGG_SUM_I64, combine=False, cap_log2=cap_log2, pipeline=False, **kw)
         self.avg = bool(avg)
         self.threshold = threshold
         self.mode = V.MODE_MFMA if mfma else V.MODE_VALU
@@ -124,7 +126,7 @@ class VectorWindowOperator(KeyedWindowOperator):
                           npanes=p1 - p0 + 1, ring=self.ring, p0=p0, only_dirty=only_dirty,
                           avg=self.avg, threshold=self.threshold, out_keys=self.out_keys,
                           out_vec=self.out_vec, out_cnt=self.out_cnt, out_n=self.out_n)
-        n = int(self.out_n.item())
+        n = self._fired_count()
         self.metrics.num_fires += 1
         if n == 0:
             return None

@@ -75,7 +75,16 @@ class PinnedSlabPool:
         return slab
 
 
-_PINNED = PinnedSlabPool()
+_TLS = __import__("threading").local()
+
+
+def _thread_pool() -> PinnedSlabPool:
+    """One pool per host thread: virtual ranks of a LoopbackGroup (threads) must never be handed
+    the same free slab at once."""
+    pool = getattr(_TLS, "pool", None)
+    if pool is None:
+        pool = _TLS.pool = PinnedSlabPool()
+    return pool
 
 
 def to_host_arrays(cols: list[torch.Tensor], n: int, pool: PinnedSlabPool | None = None) -> list[np.ndarray]:
@@ -85,7 +94,7 @@ def to_host_arrays(cols: list[torch.Tensor], n: int, pool: PinnedSlabPool | None
     the PCIe rate. On the CPU: copies (the device buffers are reused by the next fire)."""
     if not cols or cols[0].device.type != "cuda":
         return [c[:n].numpy().copy() for c in cols]
-    pool = _PINNED if pool is None else pool
+    pool = _thread_pool() if pool is None else pool
     offs, nbytes = [], 0
     for c in cols:
         offs.append(nbytes)
@@ -132,6 +141,43 @@ class FireResult:
 
 
 @dataclass
+class _Front:
+    """One batch whose partition has been enqueued (S0) and whose reduced vector is on its way
+    to pinned host memory."""
+    keys: torch.Tensor
+    ts: torch.Tensor
+    vals: torch.Tensor
+    n: int
+    par: int
+    old_wm: int
+    pane_base: int
+    proc_now: int
+    compact: bool = True
+    ev: object = None
+
+
+@dataclass
+class _Back:
+    """The state half of one step, planned on the host after its sync."""
+    par: int
+    n: int
+    old_wm: int
+    compact: bool
+    pane_base: int
+    has_data: bool = False
+    qmin: int = 0
+    np_step: int = 0
+    pg: int = 1
+    gmin: int = 0
+    gmax: int = -1
+    fired_hi: int = I64_MIN
+    new_wm: int | None = None
+    ccap: int = 0
+    hard: int = 0
+    chk_ev: object = None
+
+
+@dataclass
 class OperatorMetrics:
     num_records_in: int = 0
     num_late_records_dropped: int = 0
@@ -159,7 +205,8 @@ class KeyedWindowOperator:
                  cap_log2: int | None = None, time_mode: str = "event", ooo_bound: int = 0,
                  side_output_late: bool = False, late_capacity: int = 1 << 16,
                  clock: Callable[[], int] | None = None, external_watermark: bool = False,
-                 combine: bool | None = None, compact: bool | None = None):
+                 combine: bool | None = None, compact: bool | None = None,
+                 pipeline: bool | None = None):
         self.device = torch.device(device)
         self.comm = comm or LocalComm()
         self.world = self.comm.world
@@ -213,19 +260,40 @@ class KeyedWindowOperator:
 
         # ---- per-step buffers ----
         self.nbuckets = self.world << self.nsub_log2
+        # G > 1: sender-side combiner before the all-to-all (all aggregates are associative).
+        self.combine = self.world > 1 if combine is None else bool(combine and self.world > 1)
+        # Pipelining: the partition of batch i+1 overlaps the state half of batch i (process()
+        # then returns the windows fired by the previous batch; flush() drains). Opt-in: the
+        # engine's hot loops (bench, configs) enable it; callers that need each batch's fires
+        # from its own call (DataStream API, external watermarks) keep the default.
+        self.pipeline = bool(pipeline) and not external_watermark
+        self.s1 = (torch.cuda.Stream(dev) if self.pipeline and self.device.type == "cuda"
+                   else None)
+        self._par = 0
+        self._pending: _Back | None = None
+        self._carry: list[FireResult] = []  # fired by a flush a state reader forced
+        nbuf = 2 if self.pipeline else 1
+        self._ev_consumed: list = [None] * nbuf
+        self._ev_part: list = [None] * nbuf
         self._alloc_buckets(batch_capacity, bucket_slack)
-        self.stats = K.new_stats(dev)
-        self.red = torch.zeros(K.RED_WORDS, dtype=torch.int64, device=dev)
+        self._stats = [K.new_stats(dev) for _ in range(nbuf)]
+        self._red = [torch.zeros(K.RED_WORDS, dtype=torch.int64, device=dev) for _ in range(nbuf)]
+        pin = self.device.type == "cuda"
+        self._hred = [torch.zeros(K.RED_WORDS, dtype=torch.int64, pin_memory=pin)
+                      for _ in range(nbuf)]
+        self._hchk = torch.zeros(2, dtype=torch.int64, pin_memory=pin)
+        self._hflags = torch.zeros(4, dtype=torch.int32, pin_memory=pin)
+        self.stats, self.red = self._stats[0], self._red[0]
         self.local_maxts = torch.full((1,), I64_MIN, dtype=torch.int64, device=dev)
         self.out_keys = torch.empty(self.nslots, dtype=torch.int64, device=dev)
         self.out_vals = torch.empty(self.nslots, dtype=torch.float64, device=dev)
         self.out_raw = torch.empty(self.nslots, dtype=torch.int64, device=dev)
         self.out_cnt = torch.empty(self.nslots, dtype=torch.int32, device=dev)
-        self.out_n = torch.zeros(1, dtype=torch.int32, device=dev)
+        # flags: [0] table full (bit0) / [1] combiner overflow / [2] fired-row cursor (out_n), so
+        # one 16-byte D2H after a fire returns the row count and the table-full bit together.
+        self.out_n = self.flags[2:3]
         self.late_idx = (torch.empty(late_capacity, dtype=torch.int32, device=dev)
                          if side_output_late else None)
-        # G > 1: sender-side combiner before the all-to-all (all aggregates are associative).
-        self.combine = self.world > 1 if combine is None else bool(combine and self.world > 1)
         self.comb_send = self.comb_recv = None
         self.comb_counts = torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
         self._ccap_hint = 1 << self.cap_log2
@@ -253,6 +321,7 @@ class KeyedWindowOperator:
         return sub * self.world // self.parallelism
 
     def _alloc_buckets(self, batch_capacity: int, slack: float) -> None:
+        self._drain()
         self.batch_capacity = int(batch_capacity)
         self.bucket_slack = slack
         per = self.batch_capacity / self.nbuckets
@@ -262,46 +331,93 @@ class KeyedWindowOperator:
         cap = int(per * slack + 6 * math.sqrt(max(per, 1.0)) + 64) + 8 * nblk
         self.bucket_cap = (cap + 7) & ~7
         words = self.nbuckets * self.bucket_cap * K.REC_WORDS
-        self.send = torch.empty(words, dtype=torch.int64, device=self.device)
-        self.recv = torch.empty(words, dtype=torch.int64, device=self.device) if self.world > 1 else self.send
-        self.cursor = torch.zeros(self.nbuckets, dtype=torch.int32, device=self.device)
-        self.recv_counts = torch.zeros(self.nbuckets, dtype=torch.int32, device=self.device) \
-            if self.world > 1 else self.cursor
+        dev = self.device
+        # Pipelined: step i+1's partition writes the other send buffer while step i's combiner /
+        # all-to-all / aggregation still read theirs (double buffering).
+        nbuf = 2 if self.pipeline else 1
+        self._send_bufs = [torch.empty(words, dtype=torch.int64, device=dev) for _ in range(nbuf)]
+        self._cursor_bufs = [torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
+                             for _ in range(nbuf)]
+        # The plain exchange lands in `recv`; with the combiner only combined records travel.
+        self.recv = (torch.empty(words, dtype=torch.int64, device=dev)
+                     if self.world > 1 and not self.combine else None)
+        self._recv_counts = (torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
+                             if self.world > 1 else None)
+        self._use_par(0)
 
-    def _combine_and_exchange(self, p_lo: int, np_step: int, pg: int):
-        """G > 1: pre-aggregate every send bucket to one record per (key, pane), then exchange
-        only those (the all-to-all volume drops from ~all events to ~distinct keys x panes).
-        The per-bucket capacity adapts to the largest combined bucket seen (doubling on
-        overflow, which re-runs only the combiner)."""
+    def _use_par(self, p: int) -> None:
+        """Point send/cursor (and, at G = 1, recv/recv_counts) at buffer set `p`."""
+        self.send, self.cursor = self._send_bufs[p], self._cursor_bufs[p]
+        if self.world == 1:
+            self.recv, self.recv_counts = self.send, self.cursor
+        else:
+            self.recv_counts = self._recv_counts
+
+    # ---- streams / host sync helpers (GPU pipelining) ----------------------------------------
+    def _s1(self):
+        """Context running the state half of a step (combiner, all-to-all, aggregation, firing,
+        purge) on the operator's state stream; the partition of the next step keeps the
+        caller's stream (S0)."""
+        import contextlib
+
+        return torch.cuda.stream(self.s1) if self.s1 is not None else contextlib.nullcontext()
+
+    def _drain(self) -> None:
+        """Wait for every queued kernel of this operator (before buffers are reallocated)."""
+        if self.device.type == "cuda" and getattr(self, "s1", None) is not None:
+            self.s1.synchronize()
+            torch.cuda.current_stream(self.device).synchronize()
+
+    def _event(self):
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return ev
+
+    def _combine_begin(self, b: "_Back") -> None:
+        """G > 1: pre-aggregate every send bucket to one record per (key, pane); the global
+        overflow flag and largest fill go through one small MIN all-reduce into pinned memory
+        (read in _combine_finish, while the next step's partition runs on S0)."""
         cap = 1 << self.cap_log2
         nb = self.nbuckets
-        hard = min(self.bucket_cap, cap * np_step)  # distinct (key, pane) per bucket bound
+        hard = min(self.bucket_cap, cap * b.np_step)  # distinct (key, pane) per bucket bound
+        ccap = min(hard, max(64, (self._ccap_hint + 7) & ~7))
+        if self.comb_send is None or self.comb_send.numel() < nb * ccap * K.REC_WORDS:
+            self._drain()
+            words = nb * ccap * K.REC_WORDS
+            self.comb_send = torch.empty(words, dtype=torch.int64, device=self.device)
+            self.comb_recv = torch.empty(words, dtype=torch.int64, device=self.device)
+        self.flags[1:2].zero_()
+        cplan = K.AggPlan(cap_log2=self.cap_log2, nsub=nb, ring=self.ring, agg=self.agg,
+                          nsrc=1, bucket_cap=self.bucket_cap, np_step=b.np_step, pg=b.pg,
+                          pane_base=0, p_lo=b.qmin, fired_hi=0,
+                          rec_words=2 if b.compact else 3)
+        K.window_combine(self.send, self.cursor, cplan, self.comb_send, ccap,
+                         self.comb_counts, self.flags[1:2])
+        chk = torch.stack([-(self.flags[1].to(torch.int64) & 2),
+                           -self.comb_counts.max().to(torch.int64)])
+        self.comm.allreduce_min_(chk)
+        b.ccap, b.hard = ccap, hard
+        if self.device.type == "cuda":
+            self._hchk.copy_(chk, non_blocking=True)
+            b.chk_ev = self._event()
+        else:
+            self._hchk.copy_(chk)
+            b.chk_ev = None
+
+    def _combine_finish(self, b: "_Back"):
         while True:
-            ccap = min(hard, max(64, (self._ccap_hint + 7) & ~7))
-            if self.comb_send is None or self.comb_send.numel() < nb * ccap * K.REC_WORDS:
-                words = nb * ccap * K.REC_WORDS
-                self.comb_send = torch.empty(words, dtype=torch.int64, device=self.device)
-                self.comb_recv = torch.empty(words, dtype=torch.int64, device=self.device)
-            self.flags[1:2].zero_()
-            cplan = K.AggPlan(cap_log2=self.cap_log2, nsub=nb, ring=self.ring, agg=self.agg,
-                              nsrc=1, bucket_cap=self.bucket_cap, np_step=np_step, pg=pg,
-                              pane_base=0, p_lo=p_lo, fired_hi=0,
-                              rec_words=2 if self.compact else 3)
-            K.window_combine(self.send, self.cursor, cplan, self.comb_send, ccap,
-                             self.comb_counts, self.flags[1:2])
-            # One small sync: overflow flag (global, so every rank retries together) + max fill.
-            chk = torch.stack([-(self.flags[1].to(torch.int64) & 2),
-                               -self.comb_counts.max().to(torch.int64)])
-            self.comm.allreduce_min_(chk)
-            ovf, fill = [-x for x in chk.tolist()]
-            if ovf and ccap < hard:
-                self._ccap_hint = ccap * 2
-                self.metrics.extra["combine_regrows"] = self.metrics.extra.get("combine_regrows", 0) + 1
-                continue
-            if ovf:
+            if b.chk_ev is not None:
+                b.chk_ev.synchronize()
+            ovf, fill = (-int(x) for x in self._hchk.tolist())
+            if not ovf:
+                break
+            if b.ccap >= b.hard:
                 raise RuntimeError("window_combine: a send bucket exceeds its sub-table capacity")
-            self._ccap_hint = max(64, int(fill * 1.25) + 8)
-            break
+            self._ccap_hint = b.ccap * 2
+            self.metrics.extra["combine_regrows"] = self.metrics.extra.get("combine_regrows", 0) + 1
+            self._combine_begin(b)
+        self._ccap_hint = max(64, int(fill * 1.25) + 8)
+        ccap, nb = b.ccap, self.nbuckets
         send = self.comb_send[: nb * ccap * K.REC_WORDS]
         recv = self.comb_recv[: nb * ccap * K.REC_WORDS]
         self.comm.all_to_all(recv, send)
@@ -373,43 +489,109 @@ class KeyedWindowOperator:
         return int(self.clock() if self.clock else time.time() * 1000)
 
     def process(self, keys: torch.Tensor, ts: torch.Tensor, vals: torch.Tensor) -> list[FireResult]:
-        """Fold one micro-batch of this rank's source partition and fire what the watermark allows."""
+        """Fold one micro-batch of this rank's source partition and fire what the watermark allows.
+
+        Unpipelined (CPU, DataStream API): partition -> one host sync -> aggregation -> fire, all
+        for this batch. Pipelined (GPU default): the call enqueues this batch's partition on the
+        caller's stream (S0) and the state half of the PREVIOUS batch (combiner, all-to-all,
+        aggregation, firing, purge) on the state stream (S1), so the two overlap; it returns the
+        windows fired by the previous batch (``flush()`` / ``finish()`` drain the last one). One
+        host sync per step, on this batch's reduced vector, while S1 still works."""
+        out, self._carry = self._carry, []
+        if not self.pipeline:
+            b = self._settle(self._front(keys, ts, vals))
+            self._back_begin(b)
+            return out + self._back_finish(b)
+        prev, self._pending = self._pending, None
+        if prev is not None:
+            with self._s1():
+                self._back_begin(prev)      # combiner + its tiny all-reduce, before S0's
+        f = self._front(keys, ts, vals)     # partition of this batch (S0)
+        if prev is not None:
+            out += self._back_finish(prev)
+        self._pending = self._settle(f)     # the step's one host sync (S1 keeps working)
+        return out
+
+    def flush(self) -> list[FireResult]:
+        """Complete the pending state half of the last batch (pipelined mode); returns what it
+        fired. Every entry point that reads or replaces state calls it first."""
+        out, self._carry = self._carry, []
+        prev, self._pending = self._pending, None
+        if prev is None:
+            return out
+        with self._s1():
+            self._back_begin(prev)
+        return out + self._back_finish(prev)
+
+    # ---- step phases ------------------------------------------------------------------------
+    def _front(self, keys, ts, vals) -> "_Front":
         n = keys.numel()
         if n > self.batch_capacity:
+            self.flush()
             self._alloc_buckets(n, self.bucket_slack)
-        old_wm = self.wm
-        pane_base = self._pane_base(ts)
+        p = self._par
+        if self.pipeline:
+            self._par ^= 1
         event_mode = self.time_mode == "event"
-        proc_now = 0 if event_mode else self.current_processing_time()
+        f = _Front(keys=keys, ts=ts, vals=vals, n=n, par=p, old_wm=self.wm,
+                   pane_base=self._pane_base(ts),
+                   proc_now=0 if event_mode else self.current_processing_time())
+        self._launch_front(f)
+        return f
+
+    def _launch_front(self, f: "_Front") -> None:
+        p = f.par
+        self._use_par(p)
+        cuda = self.device.type == "cuda"
+        if cuda and self._ev_consumed[p] is not None:
+            # send[p] / cursor[p] are still read by the state half of the step before last
+            torch.cuda.current_stream(self.device).wait_event(self._ev_consumed[p])
+        event_mode = self.time_mode == "event"
+        stats, red = self._stats[p], self._red[p]
+        K.step_begin(self.cursor, stats)
+        plan = K.PartitionPlan(
+            max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2, nranks=self.world,
+            window_mode=1, drop_late=int(event_mode), hash_mode=self.hash_mode,
+            bucket_cap=self.bucket_cap, late_ts=self._late_ts(f.old_wm),
+            tbase=self.pane_start(f.pane_base), pane=self.pane,
+            rec_words=2 if self.compact else 3)
+        f.compact = self.compact
+        with self._stage("partition"):
+            if f.n:
+                K.partition(f.keys, f.ts, f.vals, plan, self.kg_dest, self.cursor, self.send,
+                            stats, jhash=self.jhash, late_idx=self.late_idx)
+        K.step_finish(stats, self.local_maxts, red, bound=self.ooo_bound, event_mode=event_mode,
+                      proc_now=f.proc_now, flags=self.flags)
+        # Watermark valve + pane range + every overflow flag: ONE MIN all-reduce per step.
+        self.comm.allreduce_min_(red[:8])
+        if cuda:
+            self._hred[p].copy_(red, non_blocking=True)
+            f.ev = self._event()
+        else:
+            self._hred[p].copy_(red)
+            f.ev = None
+        if cuda:
+            self._ev_part[p] = f.ev
+
+    def _settle(self, f: "_Front") -> "_Back":
+        """The step's host sync: overflow handling (redo), watermark and pane bookkeeping."""
         while True:
-            K.step_begin(self.cursor, self.stats)
-            plan = K.PartitionPlan(
-                max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2, nranks=self.world,
-                window_mode=1, drop_late=int(event_mode), hash_mode=self.hash_mode,
-                bucket_cap=self.bucket_cap, late_ts=self._late_ts(old_wm),
-                tbase=self.pane_start(pane_base), pane=self.pane,
-                rec_words=2 if self.compact else 3)
-            with self._stage("partition"):
-                if n:
-                    K.partition(keys, ts, vals, plan, self.kg_dest, self.cursor, self.send,
-                                self.stats, jhash=self.jhash, late_idx=self.late_idx)
-            K.step_finish(self.stats, self.local_maxts, self.red, bound=self.ooo_bound,
-                          event_mode=event_mode, proc_now=proc_now)
-            # Watermark valve + pane range + overflow flags: one MIN all-reduce.
-            self.comm.allreduce_min_(self.red[:5])
-            if self.world > 1 and not self.combine:
-                with self._stage("all_to_all"):
-                    self._exchange()
-            host = self.red.cpu().tolist()  # the step's single host sync
+            if f.ev is not None:
+                f.ev.synchronize()
+            host = self._hred[f.par].tolist()
             if host[4]:
                 raise RuntimeError("event timestamp outside the representable pane range "
                                    "(more than 2^32 panes ahead of the watermark)")
+            if host[6]:
+                raise RuntimeError("keyed state table full: a key found no free slot "
+                                   "(raise max_keys)")
+            if host[7]:
+                raise ValueError("key ids -1 and -2 are reserved (the state tables' markers)")
             if host[5]:
                 # A value does not fit the 16-byte record: 24-byte records from now on.
                 self.compact = False
                 self.metrics.extra["compact_fallbacks"] = self.metrics.extra.get("compact_fallbacks", 0) + 1
-                continue
-            if host[3]:
+            elif host[3]:
                 # A bucket overflowed somewhere: grow the fixed bucket capacity and redo the step.
                 self.metrics.bucket_regrows += 1
                 from ..utils.log import get_logger
@@ -417,22 +599,24 @@ class KeyedWindowOperator:
                 get_logger("runtime.window").warning(
                     "bucket capacity %d exceeded: regrowing and redoing the step", self.bucket_cap)
                 self._alloc_buckets(self.batch_capacity, self.bucket_slack * 2)
-                continue
-            break
+            else:
+                break
+            self._drain()
+            self._launch_front(f)
         qmax, qmin, wm_global = -host[0], host[1], host[2]
         st = host[8:]
-        self.metrics.num_records_in += n
+        self.metrics.num_records_in += f.n
         self.metrics.num_late_records_dropped += int(st[K.STAT_LATE])
         if self.side_output_late and st[K.STAT_LATE]:
             nl = min(int(st[K.STAT_LATE]), self.late_idx.numel())
             self.late_side.append(self.late_idx[:nl].cpu().numpy().copy())
-
-        out: list[FireResult] = []
+        b = _Back(par=f.par, n=f.n, old_wm=f.old_wm, compact=f.compact, pane_base=f.pane_base)
         if qmin <= qmax:
-            gmin, gmax = pane_base + qmin, pane_base + qmax
+            gmin, gmax = f.pane_base + qmin, f.pane_base + qmax
             lo = gmin if self.min_live_pane is None else min(self.min_live_pane, gmin)
             hi = gmax if self.max_seen_pane is None else max(self.max_seen_pane, gmax)
             if hi - lo + 1 > self.ring:
+                self._drain()
                 self._grow_ring(hi - lo + 1)
             self.min_live_pane, self.max_seen_pane = lo, hi
             # Invariant: every window starting before next_fire_start is due (maxTs <= wm) and
@@ -440,42 +624,70 @@ class KeyedWindowOperator:
             # cursor (older but not late): lower the cursor to the first such window. Windows
             # that are already due and receive data (allowed lateness) go through _refire.
             cand = self.first_start_containing(self.pane_start(gmin))
-            if old_wm > I64_MIN:
-                cand = max(cand, self._align_up(old_wm - self.size + 2))
+            if f.old_wm > I64_MIN:
+                cand = max(cand, self._align_up(f.old_wm - self.size + 2))
             self.next_fire_start = cand if self.next_fire_start is None else min(self.next_fire_start, cand)
-            fired_hi = self._fired_hi()
+            b.fired_hi = self._fired_hi()
             cap = 1 << self.cap_log2
             lds_budget = 150 * 1024 - cap * 8
-            pg = max(1, min(gmax - gmin + 1, lds_budget // (cap * 12)))
-            recs, counts, bcap, combined = self.recv, self.recv_counts, self.bucket_cap, 0
-            if self.combine:
-                with self._stage("combine_all_to_all"):
-                    recs, counts, bcap = self._combine_and_exchange(qmin, gmax - gmin + 1, pg)
-                combined = 1
-            aplan = K.AggPlan(cap_log2=self.cap_log2, nsub=self.nsub, ring=self.ring, agg=self.agg,
-                              nsrc=self.world, bucket_cap=bcap,
-                              np_step=gmax - gmin + 1, pg=pg, pane_base=pane_base,
-                              p_lo=qmin, fired_hi=fired_hi, combined=combined,
-                              rec_words=3 if combined else (2 if self.compact else 3))
-            with self._stage("window_agg"):
-                self._aggregate(recs, counts, aplan)
-            if self._debug:
-                from ..ops.debug import assert_table_ok
-
-                assert_table_ok(self.keys_g, nsub=self.nsub, nsub_log2=self.nsub_log2,
-                                cap_log2=self.cap_log2, where=f"after step {self.metrics.steps}")
-            # Late-but-allowed data: re-fire already-passed windows that are not cleaned yet.
-            if gmin <= fired_hi:
-                out.extend(self._refire(gmin, min(gmax, fired_hi), old_wm))
+            b.has_data = True
+            b.qmin, b.np_step = qmin, gmax - gmin + 1
+            b.pg = max(1, min(b.np_step, lds_budget // (cap * 12)))
+            b.gmin, b.gmax = gmin, gmax
         self.metrics.steps += 1
-        if self.external_watermark:
-            return out
-        new_wm = max(old_wm, wm_global)
-        self.wm = new_wm
-        self.metrics.current_watermark = new_wm
-        with self._stage("fire"):
-            out.extend(self._fire_ready(new_wm))
-            self._purge(new_wm)
+        if not self.external_watermark:
+            b.new_wm = max(f.old_wm, wm_global)
+            self.wm = b.new_wm
+            self.metrics.current_watermark = b.new_wm
+        return b
+
+    def _back_begin(self, b: "_Back") -> None:
+        if not b.has_data:
+            return
+        self._use_par(b.par)
+        if self.device.type == "cuda" and self._ev_part[b.par] is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._ev_part[b.par])
+        if self.combine:
+            with self._stage("combine"):
+                self._combine_begin(b)
+
+    def _back_finish(self, b: "_Back") -> list[FireResult]:
+        out: list[FireResult] = []
+        cuda = self.device.type == "cuda"
+        with self._s1():
+            if b.has_data:
+                self._use_par(b.par)
+                recs, counts, bcap, combined = self.recv, self.recv_counts, self.bucket_cap, 0
+                if self.combine:
+                    with self._stage("all_to_all"):
+                        recs, counts, bcap = self._combine_finish(b)
+                    combined = 1
+                elif self.world > 1:
+                    with self._stage("all_to_all"):
+                        self._exchange()
+                if cuda and self.world > 1:
+                    self._ev_consumed[b.par] = self._event()
+                aplan = K.AggPlan(cap_log2=self.cap_log2, nsub=self.nsub, ring=self.ring,
+                                  agg=self.agg, nsrc=self.world, bucket_cap=bcap,
+                                  np_step=b.np_step, pg=b.pg, pane_base=b.pane_base,
+                                  p_lo=b.qmin, fired_hi=b.fired_hi, combined=combined,
+                                  rec_words=3 if combined else (2 if b.compact else 3))
+                with self._stage("window_agg"):
+                    self._aggregate(recs, counts, aplan)
+                if cuda and self.world == 1:
+                    self._ev_consumed[b.par] = self._event()
+                if self._debug:
+                    from ..ops.debug import assert_table_ok
+
+                    assert_table_ok(self.keys_g, nsub=self.nsub, nsub_log2=self.nsub_log2,
+                                    cap_log2=self.cap_log2, where=f"after step {self.metrics.steps}")
+                # Late-but-allowed data: re-fire already-passed windows that are not cleaned yet.
+                if b.gmin <= b.fired_hi:
+                    out.extend(self._refire(b.gmin, min(b.gmax, b.fired_hi), b.old_wm))
+            if b.new_wm is not None:
+                with self._stage("fire"):
+                    out.extend(self._fire_ready(b.new_wm))
+                    self._purge(b.new_wm)
         if self.timer is not None:
             self.timer.flush()
         return out
@@ -504,12 +716,14 @@ class KeyedWindowOperator:
     def advance_watermark(self, wm: int) -> list[FireResult]:
         """Advance the watermark without data (idle step / processing-time timer / end of input)."""
         wm = int(wm)
+        out = self.flush()
         if wm <= self.wm:
-            return []
+            return out
         self.wm = wm
         self.metrics.current_watermark = wm
-        out = self._fire_ready(wm)
-        self._purge(wm)
+        with self._s1():
+            out.extend(self._fire_ready(wm))
+            self._purge(wm)
         return out
 
     def finish(self) -> list[FireResult]:
@@ -517,7 +731,7 @@ class KeyedWindowOperator:
         not fire pending windows (Flink 1.8 SocketTextStreamFunction end-of-stream behaviour)."""
         if self.time_mode == "event":
             return self.advance_watermark(I64_MAX)
-        return []
+        return self.flush()
 
     # ---- firing ---------------------------------------------------------------------------
     def _window_overlaps_live(self, s: int) -> bool:
@@ -540,7 +754,7 @@ class KeyedWindowOperator:
                       wend=s + self.size, only_dirty=only_dirty, map_prog=self.map_prog,
                       filt_prog=self.filter_prog, out_keys=self.out_keys, out_vals=self.out_vals,
                       out_raw=self.out_raw, out_cnt=self.out_cnt, out_n=self.out_n)
-        n = int(self.out_n.item())
+        n = self._fired_count()
         self.metrics.num_fires += 1
         if n == 0:
             return None
@@ -549,6 +763,19 @@ class KeyedWindowOperator:
         host = to_host_arrays([self.out_keys, self.out_vals, self.out_raw, self.out_cnt], n)
         return FireResult(s, s + self.size, host[0].view(np.uint64), host[1], host[2], host[3],
                           refire=only_dirty)
+
+    def _fired_count(self) -> int:
+        """Rows the last fire produced; raises if any aggregation found its table full (a key
+        without a slot would otherwise be missing from the fired windows)."""
+        if self.device.type == "cuda":
+            self._hflags.copy_(self.flags, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            hf = self._hflags.tolist()
+        else:
+            hf = self.flags.tolist()
+        if hf[0] & 1:
+            raise RuntimeError("keyed state table full: a key found no free slot (raise max_keys)")
+        return hf[2]
 
     def _fire_ready(self, wm: int) -> list[FireResult]:
         out: list[FireResult] = []
@@ -621,7 +848,15 @@ class KeyedWindowOperator:
                                                           self.dirty_g))
 
     def num_keys(self) -> int:
+        self._sync_state()
         return int(self.occ.sum().item())
+
+    def _sync_state(self) -> None:
+        """Make the state tables current for a host reader: the pending step must be applied
+        (its fired rows are kept for the next process()/flush() caller) and S1 drained."""
+        if self._pending is not None:
+            self._carry.extend(self.flush())
+        self._drain()
 
     # ---- checkpoint / restore (runtime/checkpoint.py) --------------------------------------
     def owned_key_groups(self) -> tuple[int, int]:
@@ -641,12 +876,14 @@ class KeyedWindowOperator:
         """Freeze the state now (D2D copies), export it later: see checkpoint.freeze_operator."""
         from .checkpoint import freeze_operator
 
+        self._sync_state()
         return freeze_operator(self, self._state_tensors)
 
     def snapshot_state(self):
         """Live (key, pane) accumulators grouped by key group, plus the firing bookkeeping."""
         from .checkpoint import OperatorSnapshot
 
+        self._sync_state()
         live = torch.nonzero(self.keys_g != -1).flatten()
         cols = {"key": np.zeros(0, np.int64), "pane": np.zeros(0, np.int64),
                 "acc": np.zeros(0, np.int64), "cnt": np.zeros(0, np.int32),
@@ -678,6 +915,8 @@ class KeyedWindowOperator:
     def restore_state(self, rows: dict, meta: dict) -> None:
         """Rebuild the tables from checkpoint rows (this rank's key groups only)."""
         self._check_ckpt_meta(meta)
+        self._pending, self._carry = None, []
+        self._drain()
         dev = self.device
         self.wm = meta["wm"]
         self.metrics.current_watermark = self.wm

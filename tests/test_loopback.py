@@ -1,0 +1,332 @@
+"""G virtual ranks on one device (LoopbackComm): every keyed operator's results are invariant to G.
+
+The loopback group runs the complete G>1 path -- Flink key-group partition into G x sub-table
+buckets, the sender-side combiner, the equal-split all-to-all layout, combined-record
+aggregation, the MIN watermark valve, overflow regrow -- in one process, so the same test runs
+on the C++ twins (CPU) and on one MI355X (``-m gpu``). The reference for every G is a single
+rank that sees every rank's batch of a step concatenated in rank order; integer sums must be
+bit-exact. (Flink parity: keyBy at ``ComputeCpuMax.java:26``, ``BandwidthMonitorWithEventTime
+.java:45``.)
+"""
+import numpy as np
+import pytest
+import torch
+
+from mxstream.ops import kernels as K
+from mxstream.parallel.comm import LoopbackGroup, run_loopback
+from mxstream.runtime.window_operator import KeyedWindowOperator
+
+STEPS = 6
+
+
+def _devices():
+    return [pytest.param("cpu", id="cpu"),
+            pytest.param("cuda", id="gpu", marks=pytest.mark.gpu)]
+
+
+def _sizes(dev):
+    # The GPU run uses batches large enough for many partition workgroups per rank.
+    return (3000, 5000, 8) if dev == "cpu" else (150_000, 60_000, None)
+
+
+def _batch(dev, rank, step, per, nkeys, span=2000, disorder=700):
+    d = torch.device(dev)
+    keys = torch.empty(per, dtype=torch.int64, device=d)
+    ts = torch.empty_like(keys)
+    vals = torch.empty_like(keys)
+    K.gen_events(keys, ts, vals, seed=11, stream_id=rank, idx0=step * per, nkeys=nkeys,
+                 ts_base=step * span, ts_span=span, disorder=disorder, val_lo=0, val_span=1000)
+    # Every source partition ends its batch at the same event time, so the G-rank watermark
+    # (MIN over ranks of max ts - bound) equals the single-rank reference's (max over all).
+    ts[-1] = step * span + span
+    return keys, ts, vals
+
+
+def _concat(dev, world, step, per, nkeys):
+    parts = [_batch(dev, r, step, per, nkeys) for r in range(world)]
+    return [torch.cat([p[i] for p in parts]) for i in range(3)]
+
+
+def _collect(out):
+    return {(r.window_start, int(k)): (int(a), int(c))
+            for r in out for k, a, c in zip(r.keys, r.raw, r.counts)}
+
+
+def _skip_no_gpu(dev):
+    if dev == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.mark.parametrize("dev", _devices())
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+@pytest.mark.parametrize("size,slide,lateness", [(3000, 3000, 0), (4000, 1000, 1500)])
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_window_invariant_to_world(dev, world, size, slide, lateness, pipeline):
+    """pipeline=True: the partition of batch i+1 overlaps the combiner / all-to-all /
+    aggregation / firing of batch i on a second stream (GPU); on the CPU twins the same
+    one-step-deferred control flow runs synchronously."""
+    _skip_no_gpu(dev)
+    per, nkeys, cap_log2 = _sizes(dev)
+
+    def make(comm, batch_capacity, pipe=pipeline):
+        return KeyedWindowOperator(size=size, slide=slide, lateness=lateness, agg=K.AGG_SUM_I64,
+                                   device=dev, comm=comm, max_keys=nkeys,
+                                   batch_capacity=batch_capacity, ooo_bound=500, cap_log2=cap_log2,
+                                   pipeline=pipe)
+
+    def rank_fn(comm):
+        op = make(comm, per)
+        out = []
+        for step in range(STEPS):
+            out += op.process(*_batch(dev, comm.rank, step, per, nkeys))
+        out += op.finish()
+        return _collect(out), op.metrics.num_late_records_dropped, op.metrics.extra
+
+    res = run_loopback(world, rank_fn, device=torch.device(dev))
+    merged, late = {}, 0
+    for d, nl, _ in res:
+        assert not (set(d) & set(merged)), "a (window, key) fired on two ranks"
+        merged.update(d)
+        late += nl
+    ref_op = make(None, per * world, pipe=False)  # unpipelined single rank: the reference
+    out = []
+    for step in range(STEPS):
+        out += ref_op.process(*_concat(dev, world, step, per, nkeys))
+    out += ref_op.finish()
+    ref = _collect(out)
+    assert len(ref) > 0
+    assert merged == ref
+    assert late == ref_op.metrics.num_late_records_dropped
+
+
+@pytest.mark.parametrize("dev", _devices())
+def test_window_loopback_without_combiner(dev):
+    """The plain exchange (every record crosses the all-to-all) gives the same result."""
+    _skip_no_gpu(dev)
+    per, nkeys, cap_log2 = _sizes(dev)
+    world = 4
+
+    def rank_fn(comm):
+        op = KeyedWindowOperator(size=3000, agg=K.AGG_SUM_I64, device=dev, comm=comm,
+                                 max_keys=nkeys, batch_capacity=per, ooo_bound=500,
+                                 cap_log2=cap_log2, combine=False)
+        out = []
+        for step in range(STEPS):
+            out += op.process(*_batch(dev, comm.rank, step, per, nkeys))
+        return _collect(out + op.finish())
+
+    merged = {}
+    for d in run_loopback(world, rank_fn, device=torch.device(dev)):
+        merged.update(d)
+    ref_op = KeyedWindowOperator(size=3000, agg=K.AGG_SUM_I64, device=dev, max_keys=nkeys,
+                                 batch_capacity=per * world, ooo_bound=500, cap_log2=cap_log2)
+    out = []
+    for step in range(STEPS):
+        out += ref_op.process(*_concat(dev, world, step, per, nkeys))
+    assert merged == _collect(out + ref_op.finish())
+
+
+@pytest.mark.parametrize("dev", _devices())
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_window_loopback_bucket_regrow(dev, pipeline):
+    """A skewed rank overflows its fixed-capacity buckets: every rank regrows and redoes the
+    step together (the flag travels in the step's MIN all-reduce), results unchanged."""
+    _skip_no_gpu(dev)
+    per, nkeys, cap_log2 = _sizes(dev)
+    world = 2
+
+    def batch(rank, step):
+        k, t, v = _batch(dev, rank, step, per, nkeys)
+        if rank == 1:
+            k = k % 7  # a handful of hot keys: a few buckets receive everything
+        return k, t, v
+
+    def rank_fn(comm):
+        op = KeyedWindowOperator(size=3000, agg=K.AGG_SUM_I64, device=dev, comm=comm,
+                                 max_keys=nkeys, batch_capacity=per, ooo_bound=500,
+                                 cap_log2=cap_log2, bucket_slack=1.0, pipeline=pipeline)
+        out = []
+        for step in range(STEPS):
+            out += op.process(*batch(comm.rank, step))
+        return _collect(out + op.finish()), op.metrics.bucket_regrows
+
+    res = run_loopback(world, rank_fn, device=torch.device(dev))
+    assert all(r[1] >= 1 for r in res)
+    merged = {}
+    for d, _ in res:
+        merged.update(d)
+    ref_op = KeyedWindowOperator(size=3000, agg=K.AGG_SUM_I64, device=dev, max_keys=nkeys,
+                                 batch_capacity=per * world, ooo_bound=500, cap_log2=cap_log2)
+    out = []
+    for step in range(STEPS):
+        parts = [batch(r, step) for r in range(world)]
+        out += ref_op.process(*[torch.cat([p[i] for p in parts]) for i in range(3)])
+    assert merged == _collect(out + ref_op.finish())
+
+
+# ---- keyed rolling state (ComputeCpuMax.java:26) --------------------------------------------
+@pytest.mark.parametrize("dev", _devices())
+@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("agg", [K.AGG_SUM_I64, K.AGG_MAX_I64, K.AGG_COUNT])
+def test_rolling_invariant_to_world(dev, world, agg):
+    from mxstream.runtime.rolling_operator import KeyedRollingOperator
+
+    _skip_no_gpu(dev)
+    per = 2000 if dev == "cpu" else 100_000
+    nkeys = 300 if dev == "cpu" else 10_000
+
+    def rank_fn(comm):
+        op = KeyedRollingOperator(agg=agg, device=dev, comm=comm, max_keys=nkeys,
+                                  batch_capacity=per, cap_log2=8 if dev == "cpu" else None)
+        rows = {}
+        for step in range(4):
+            k, _, v = _batch(dev, comm.rank, step, per, nkeys)
+            r = op.process(k, v)
+            for key, val, tag in zip(r.keys.tolist(), r.values.tolist(), r.tags.tolist()):
+                rows[(step, tag >> 32, tag & 0xFFFFFFFF)] = (key, val)
+        return rows
+
+    merged = {}
+    for d in run_loopback(world, rank_fn, device=torch.device(dev)):
+        assert not (set(d) & set(merged))
+        merged.update(d)
+    ref_op = KeyedRollingOperator(agg=agg, device=dev, max_keys=nkeys, batch_capacity=per * world,
+                                  cap_log2=8 if dev == "cpu" else None)
+    ref = {}
+    for step in range(4):
+        k, _, v = _concat(dev, world, step, per, nkeys)
+        r = ref_op.process(k, v)
+        for key, val, tag in zip(r.keys.tolist(), r.values.tolist(), r.tags.tolist()):
+            i = tag & 0xFFFFFFFF  # single rank: the index in the concatenated batch
+            ref[(step, i // per, i % per)] = (key, val)
+    assert len(ref) == per * world * 4
+    assert merged == ref
+
+
+# ---- session windows (chapter3/README.md:412-428, BASELINE config 5) -----------------------
+def _collect_sessions(rows):
+    return {(int(k), int(s)): (int(e), int(a), int(c))
+            for k, s, e, a, c in zip(rows.keys, rows.start, rows.end, rows.raw, rows.counts)}
+
+
+@pytest.mark.parametrize("dev", _devices())
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sessions_invariant_to_world(dev, world):
+    from mxstream.runtime.session_operator import KeyedSessionOperator
+
+    _skip_no_gpu(dev)
+    per = 3000 if dev == "cpu" else 60_000
+    nkeys = 5000 if dev == "cpu" else 40_000
+
+    def make(comm, cap):
+        return KeyedSessionOperator(gap=40, lateness=300, agg=K.AGG_SUM_I64, device=dev,
+                                    comm=comm, max_keys=nkeys, batch_capacity=cap, ooo_bound=500,
+                                    cap_log2=8 if dev == "cpu" else None)
+
+    def rank_fn(comm):
+        op = make(comm, per)
+        got = {}
+        for step in range(STEPS):
+            got.update(_collect_sessions(op.process(*_batch(dev, comm.rank, step, per, nkeys))))
+        got.update(_collect_sessions(op.finish()))
+        return got, op.metrics.num_late_records_dropped
+
+    merged, late = {}, 0
+    for d, nl in run_loopback(world, rank_fn, device=torch.device(dev)):
+        assert not (set(d) & set(merged)), "a session fired on two ranks"
+        merged.update(d)
+        late += nl
+    op = make(None, per * world)
+    ref = {}
+    for step in range(STEPS):
+        ref.update(_collect_sessions(op.process(*_concat(dev, world, step, per, nkeys))))
+    ref.update(_collect_sessions(op.finish()))
+    assert len(ref) > 0
+    assert merged == ref
+    assert late == op.metrics.num_late_records_dropped
+
+
+# ---- vector-metric windows (MFMA path on the GPU) ------------------------------------------
+@pytest.mark.parametrize("dev", _devices())
+@pytest.mark.parametrize("world", [2, 8])
+def test_vector_windows_invariant_to_world(dev, world):
+    from mxstream.ops import vector as V
+    from mxstream.runtime.vector_window_operator import VectorWindowOperator
+
+    _skip_no_gpu(dev)
+    per = 2000 if dev == "cpu" else 40_000
+    nkeys = 3000 if dev == "cpu" else 20_000
+
+    def vb(rank, step):
+        keys, ts, _ = _batch(dev, rank, step, per, nkeys)
+        vec = torch.empty(per, 32, dtype=torch.float32, device=torch.device(dev))
+        V.gen_vectors(vec, seed=3, stream_id=rank, idx0=step * per)
+        return keys, ts, vec
+
+    def collect(out):
+        return {(r.window_start, int(k)): (np.asarray(v), int(c))
+                for r in out for k, v, c in zip(r.keys, r.values, r.counts)}
+
+    def rank_fn(comm):
+        op = VectorWindowOperator(dim=32, size=3000, slide=1000, device=dev, comm=comm,
+                                  max_keys=nkeys, batch_capacity=per, ooo_bound=500)
+        out = []
+        for step in range(4):
+            out += op.process(*vb(comm.rank, step))
+        return collect(out + op.finish())
+
+    merged = {}
+    for d in run_loopback(world, rank_fn, device=torch.device(dev)):
+        assert not (set(d) & set(merged))
+        merged.update(d)
+    op = VectorWindowOperator(dim=32, size=3000, slide=1000, device=dev, max_keys=nkeys,
+                              batch_capacity=per * world, ooo_bound=500)
+    out = []
+    for step in range(4):
+        parts = [vb(r, step) for r in range(world)]
+        out += op.process(*[torch.cat([p[i] for p in parts]) for i in range(3)])
+    ref = collect(out + op.finish())
+    assert merged.keys() == ref.keys()
+    for k, (v, c) in ref.items():
+        assert merged[k][1] == c
+        np.testing.assert_allclose(merged[k][0], v, rtol=1e-5, atol=1e-4)
+
+
+# ---- the communicator itself ------------------------------------------------------------------
+@pytest.mark.parametrize("dev", _devices())
+def test_loopback_collectives_match_all_to_all_single_layout(dev):
+    _skip_no_gpu(dev)
+    world = 4
+    d = torch.device(dev)
+
+    def rank_fn(comm):
+        inp = torch.arange(world * 3, dtype=torch.int64, device=d) + 100 * comm.rank
+        out = torch.empty_like(inp)
+        comm.all_to_all(out, inp)
+        t = torch.tensor([comm.rank + 5, -comm.rank], dtype=torch.int64, device=d)
+        comm.allreduce_min_(t)
+        s = torch.tensor([comm.rank + 1], dtype=torch.int64, device=d)
+        comm.allreduce_sum_(s)
+        objs = comm.all_gather_object({"r": comm.rank})
+        b = comm.broadcast_object("x" if comm.rank == 2 else None, src=2)
+        return out.cpu().tolist(), t.cpu().tolist(), int(s.item()), objs, b
+
+    res = run_loopback(world, rank_fn, device=d)
+    for r, (out, t, s, objs, b) in enumerate(res):
+        assert out == [100 * src + r * 3 + j for src in range(world) for j in range(3)]
+        assert t == [5, -(world - 1)]
+        assert s == sum(range(1, world + 1))
+        assert objs == [{"r": i} for i in range(world)]
+        assert b == "x"
+
+
+def test_loopback_error_on_one_rank_propagates():
+    def rank_fn(comm):
+        if comm.rank == 1:
+            raise ValueError("boom")
+        comm.barrier()
+        return comm.rank
+
+    with pytest.raises(ValueError, match="boom"):
+        run_loopback(3, rank_fn, timeout_s=30)
+    assert LoopbackGroup(2).world == 2
