@@ -34,7 +34,11 @@ class TumblingBenchConfig:
     val_max: int = 20_000            # bytes per event ~ U[0, val_max)
     seed: int = 1234
     alert_fraction: float = 0.92     # alert when Mbps < fraction * expected Mbps
-    pipeline: bool = True            # partition of step i+1 overlaps the state half of step i
+    # Partition of step i+1 overlaps the state half (combiner, all-to-all, aggregation, firing)
+    # of step i. None = on when there is an exchange to hide (G > 1). At G = 1 the two halves
+    # are both HBM-bound and overlapping them measured slower (0.45 -> 0.75 ms/step,
+    # profiles/r2_pipeline_g1.md).
+    pipeline: bool | None = None
 
 
 class TumblingWindowBench:
@@ -51,7 +55,7 @@ class TumblingWindowBench:
             max_keys=cfg.keys, parallelism=world, batch_capacity=cfg.batch,
             ooo_bound=cfg.disorder_ms, map_prog=E.compile_expr(mbps),
             filter_prog=E.compile_expr(E.var(E.VAR_MAPPED) < self.threshold_mbps),
-            pipeline=cfg.pipeline)
+            pipeline=(world > 1) if cfg.pipeline is None else cfg.pipeline)
         self.keys = torch.empty(cfg.batch, dtype=torch.int64, device=device)
         self.ts = torch.empty(cfg.batch, dtype=torch.int64, device=device)
         self.vals = torch.empty(cfg.batch, dtype=torch.int64, device=device)

@@ -39,6 +39,15 @@ def _p(t: torch.Tensor | None) -> int:
     return 0 if t is None else t.data_ptr()
 
 
+def resolve_device(d) -> torch.device:
+    """torch.device with an explicit index: a bare 'cuda' means the current device (operators
+    compare tensor devices against theirs, and tensors always carry the index)."""
+    d = torch.device(d)
+    if d.type == "cuda" and d.index is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
 def _check(t: torch.Tensor, dtype: torch.dtype, numel_min: int, name: str, dev: torch.device):
     if t.dtype != dtype:
         raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
@@ -46,7 +55,7 @@ def _check(t: torch.Tensor, dtype: torch.dtype, numel_min: int, name: str, dev: 
         raise ValueError(f"{name}: must be contiguous")
     if t.numel() < numel_min:
         raise ValueError(f"{name}: needs >= {numel_min} elements, has {t.numel()}")
-    if t.device != dev:
+    if t.device != dev and t.device != resolve_device(dev):
         raise ValueError(f"{name}: on {t.device}, expected {dev}")
 
 

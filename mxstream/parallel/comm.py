@@ -225,6 +225,8 @@ def run_loopback(world: int, fn, *args, device: torch.device | None = None,
     leave their barrier with BrokenBarrierError) and is re-raised here."""
     import threading
 
+    if device is not None and device.type == "cuda" and device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
     group = LoopbackGroup(world, timeout_s=timeout_s)
     res: list = [None] * world
     errs: list = [None] * world

@@ -31,7 +31,7 @@ class KeyedListWindowOperator:
             raise ValueError("supported list-window functions: median")
         self.size, self.slide, self.offset, self.lateness = int(size), int(slide), int(offset), int(lateness)
         self.pane = math.gcd(self.size, self.slide)
-        self.device = torch.device(device)
+        self.device = K.resolve_device(device)
         self.time_mode = time_mode
         self.wm = I64_MIN
         self.panes: dict[int, list[tuple[torch.Tensor, torch.Tensor]]] = {}

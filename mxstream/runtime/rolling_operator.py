@@ -40,7 +40,7 @@ class KeyedRollingOperator:
                  max_keys: int = 1 << 16, parallelism: int | None = None,
                  max_parallelism: int = 128, batch_capacity: int = 1 << 20,
                  cap_log2: int | None = None, filter_prog: E.Program = E.EMPTY, emit_capacity: int | None = None):
-        self.device = torch.device(device)
+        self.device = K.resolve_device(device)
         self.comm = comm or LocalComm()
         self.world, self.rank = self.comm.world, self.comm.rank
         self.agg = agg

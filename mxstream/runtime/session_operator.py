@@ -105,7 +105,7 @@ class KeyedSessionOperator:
                  external_watermark: bool = False, host_budget_bytes: int | None = None):
         if gap <= 0:
             raise ValueError("session gap must be positive")
-        self.device = torch.device(device)
+        self.device = K.resolve_device(device)
         self.comm = comm or LocalComm()
         self.world, self.rank = self.comm.world, self.comm.rank
         self.gap, self.lateness, self.agg = int(gap), int(lateness), agg
@@ -145,7 +145,8 @@ class KeyedSessionOperator:
             self.st_rows = torch.empty(6 * self.spill_rows, dtype=torch.int64, device=dev)
             self._pin_rows = torch.empty((6, self.spill_rows), dtype=torch.int64).pin_memory()
             self._spill_thread = None
-            self.ocap = int(emit_capacity or max(self.nslots, 1 << 16))
+            # A fire can close every resident session of every slot (end of input: all kSess).
+            self.ocap = int(emit_capacity or max(self.nslots * K_SESS, 1 << 16))
             self.out_key = torch.empty(self.ocap, dtype=torch.int64, device=dev)
             self.out_start = torch.empty(self.ocap, dtype=torch.int64, device=dev)
             self.out_end = torch.empty(self.ocap, dtype=torch.int64, device=dev)
@@ -188,7 +189,9 @@ class KeyedSessionOperator:
             self.heads = torch.empty(total, dtype=torch.int32, device=dev)
             self.host_cap = total
             self.host_recs = torch.empty(total * K.REC_WORDS, dtype=torch.int64, device=dev)
-            self.ovf_cap = max(1 << 12, total // 16)
+            # The merge folds runs into the state as it goes (no redo), so the overflow-run buffer
+            # holds the worst case: every received record a run of its own.
+            self.ovf_cap = max(1 << 12, total)
             self.ovf_rows = torch.empty(5 * self.ovf_cap, dtype=torch.int64, device=dev)
             self.ovf_slots = torch.empty(total, dtype=torch.int64, device=dev)
 

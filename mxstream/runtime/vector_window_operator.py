@@ -72,19 +72,19 @@ class VectorWindowOperator(KeyedWindowOperator):
     def _rec_words(self) -> int:
         return 2 if self.compact else 3
 
-    def _exchange(self) -> None:
+    def _exchange(self, rw: int) -> None:
         nb, bcap = self.nbuckets, self.bucket_cap
         need = nb * bcap * self.dim
         if self.send_vec is None or self.send_vec.numel() < need:
             self.send_vec = torch.zeros(need, dtype=torch.float32, device=self.device)
             self.recv_vec = torch.zeros(need, dtype=torch.float32, device=self.device)
-        V.vec_gather(self.send, self._rec_words(), self.cursor, nb, bcap, self._vec,
-                     self.send_vec[:need])
-        self.comm.all_to_all(self.recv, self.send)
+        V.vec_gather(self.send, rw, self.cursor, nb, bcap, self._vec, self.send_vec[:need])
+        words = nb * bcap * rw  # records of rw words: each rank's chunk is a prefix share
+        self.comm.all_to_all(self.recv[:words], self.send[:words])
         self.comm.all_to_all(self.recv_counts, self.cursor)
         self.comm.all_to_all(self.recv_vec[:need], self.send_vec[:need])
         self.metrics.extra["a2a_bytes"] = self.metrics.extra.get("a2a_bytes", 0) + \
-            (self.send.numel() * 8 + need * 4)
+            (words * 8 + need * 4)
 
     def _aggregate(self, recs, counts, aplan: K.AggPlan) -> None:
         positional = int(self.world > 1)

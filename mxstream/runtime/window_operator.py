@@ -207,7 +207,7 @@ class KeyedWindowOperator:
                  clock: Callable[[], int] | None = None, external_watermark: bool = False,
                  combine: bool | None = None, compact: bool | None = None,
                  pipeline: bool | None = None):
-        self.device = torch.device(device)
+        self.device = K.resolve_device(device)
         self.comm = comm or LocalComm()
         self.world = self.comm.world
         self.rank = self.comm.rank
@@ -664,7 +664,7 @@ class KeyedWindowOperator:
                     combined = 1
                 elif self.world > 1:
                     with self._stage("all_to_all"):
-                        self._exchange()
+                        self._exchange(2 if b.compact else 3)
                 if cuda and self.world > 1:
                     self._ev_consumed[b.par] = self._event()
                 aplan = K.AggPlan(cap_log2=self.cap_log2, nsub=self.nsub, ring=self.ring,
@@ -693,9 +693,12 @@ class KeyedWindowOperator:
         return out
 
     # ---- hooks (overridden by the vector-metric operator) ---------------------------------
-    def _exchange(self) -> None:
-        """G > 1 without the combiner: the equal-split all-to-all of the bucket ranges."""
-        self.comm.all_to_all(self.recv, self.send)
+    def _exchange(self, rw: int) -> None:
+        """G > 1 without the combiner: the equal-split all-to-all of the bucket ranges. The
+        buckets are laid out in records of `rw` words (16-byte compact or 24-byte), so the
+        per-rank chunks are nsub * bucket_cap records of that size: the prefix of the buffers."""
+        words = self.nbuckets * self.bucket_cap * rw
+        self.comm.all_to_all(self.recv[:words], self.send[:words])
         self.comm.all_to_all(self.recv_counts, self.cursor)
 
     def _aggregate(self, recs, counts, aplan: K.AggPlan) -> None:

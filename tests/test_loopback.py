@@ -100,8 +100,11 @@ def test_window_invariant_to_world(dev, world, size, slide, lateness, pipeline):
 
 
 @pytest.mark.parametrize("dev", _devices())
-def test_window_loopback_without_combiner(dev):
-    """The plain exchange (every record crosses the all-to-all) gives the same result."""
+@pytest.mark.parametrize("compact", [False, True])
+def test_window_loopback_without_combiner(dev, compact):
+    """The plain exchange (every record crosses the all-to-all) gives the same result, with
+    24-byte and with 16-byte (compact, the GPU default for integer aggregates) records: each
+    rank's chunk of the equal split is nsub * bucket_cap records of the layout in use."""
     _skip_no_gpu(dev)
     per, nkeys, cap_log2 = _sizes(dev)
     world = 4
@@ -109,7 +112,7 @@ def test_window_loopback_without_combiner(dev):
     def rank_fn(comm):
         op = KeyedWindowOperator(size=3000, agg=K.AGG_SUM_I64, device=dev, comm=comm,
                                  max_keys=nkeys, batch_capacity=per, ooo_bound=500,
-                                 cap_log2=cap_log2, combine=False)
+                                 cap_log2=cap_log2, combine=False, compact=compact)
         out = []
         for step in range(STEPS):
             out += op.process(*_batch(dev, comm.rank, step, per, nkeys))
