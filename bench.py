@@ -44,6 +44,11 @@ def main() -> int:
                     help="watchdog: abort the run if one step makes no progress for this long")
     a = ap.parse_args()
 
+    if os.environ.get("MXS_SPIN") == "1" and a.device == "cuda":
+        # Spin-wait host syncs (hipDeviceScheduleSpin) before torch creates the HIP context.
+        from mxstream.ops.native import load as _load
+
+        print(f"hipSetDeviceFlags(spin) -> {_load().gpu_set_spin_schedule()}", file=sys.stderr)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus > 1 and world_env != a.gpus:
         print(f"--gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes", file=sys.stderr)
@@ -130,6 +135,11 @@ def main() -> int:
                 "global_batch": a.batch * n,
                 "seq_len": cfg.window_ms,
                 "parallelism": f"keyBy-a2a{n}",
+                # partials: local-global aggregation (per-rank pre-aggregation over the whole key
+                # space, partial accumulators cross the all-to-all when a window fires);
+                # records: per-step exchange of combined (key, pane) records.
+                "exchange": ("partials" if bench.op.local_global
+                             else "records" if n > 1 else "none"),
                 "keys": a.keys,
                 "events_per_gpu_per_step": a.batch,
                 "event_time_per_step_ms": cfg.step_span_ms,

@@ -84,6 +84,19 @@ PartPlan make_part(py::dict d) {
   return p;
 }
 
+ScatPlan make_scat(py::dict d) {
+  ScatPlan p{};
+  p.max_parallelism = d["max_parallelism"].cast<int32_t>();
+  p.nranks = d["nranks"].cast<int32_t>();
+  p.nsub_log2 = d["nsub_log2"].cast<int32_t>();
+  p.hash_mode = d["hash_mode"].cast<int32_t>();
+  p.bucket_cap = d["bucket_cap"].cast<uint32_t>();
+  p.n_cap = d["n_cap"].cast<uint32_t>();
+  if (p.nranks < 1 || p.nsub_log2 < 0 || (p.nranks << p.nsub_log2) > 16384)
+    throw std::invalid_argument("scatter_partials: bad bucket geometry");
+  return p;
+}
+
 AggPlan make_agg(py::dict d) {
   AggPlan p;
   std::memset(&p, 0, sizeof(p));
@@ -177,6 +190,7 @@ PYBIND11_MODULE(_mxs_native, m) {
 
   // ---- GPU ----
   m.def("gpu_device_count", &gpu::device_count);
+  m.def("gpu_set_spin_schedule", &gpu::set_spin_schedule);
   m.def("gpu_gen_events", [](intptr_t keys, intptr_t ts, intptr_t vals, int64_t n, uint64_t seed,
                              uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                              int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
@@ -339,6 +353,20 @@ PYBIND11_MODULE(_mxs_native, m) {
                                intptr_t keys_g, intptr_t slots) {
     cpu::table_insert(P<uint64_t>(keys), n, nsub_log2, cap_log2, P<uint64_t>(keys_g),
                       P<int64_t>(slots));
+  });
+  m.def("gpu_scatter_partials", [](intptr_t keys, intptr_t acc, intptr_t cnt, intptr_t n_in,
+                                   py::dict plan, intptr_t jhash, intptr_t kg_dest,
+                                   intptr_t cursor, intptr_t out, intptr_t flags, intptr_t stream) {
+    gpu::scatter_partials(P<uint64_t>(keys), P<uint64_t>(acc), P<uint32_t>(cnt), P<uint32_t>(n_in),
+                          make_scat(plan), P<int32_t>(jhash), P<int32_t>(kg_dest),
+                          P<uint32_t>(cursor), P<Rec>(out), P<uint32_t>(flags), stream);
+  });
+  m.def("cpu_scatter_partials", [](intptr_t keys, intptr_t acc, intptr_t cnt, intptr_t n_in,
+                                   py::dict plan, intptr_t jhash, intptr_t kg_dest,
+                                   intptr_t cursor, intptr_t out, intptr_t flags) {
+    cpu::scatter_partials(P<uint64_t>(keys), P<uint64_t>(acc), P<uint32_t>(cnt), P<uint32_t>(n_in),
+                          make_scat(plan), P<int32_t>(jhash), P<int32_t>(kg_dest),
+                          P<uint32_t>(cursor), P<Rec>(out), P<uint32_t>(flags));
   });
   m.def("gpu_window_combine", [](intptr_t recs, intptr_t counts, int nbuckets, py::dict plan,
                                  intptr_t out, uint32_t ccap, intptr_t out_counts, intptr_t flags,

@@ -406,5 +406,29 @@ void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uin
   }
 }
 
+// Local-global window aggregation: rows of a locally fired window -> owner (rank, sub-table)
+// buckets as combined records (val = partial accumulator, aux = element count, t = pane 0).
+void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt,
+                      const uint32_t* n_in, const ScatPlan& p, const int32_t* jhash,
+                      const int32_t* kg_dest, uint32_t* cursor, Rec* out, uint32_t* flags) {
+  const uint32_t n = std::min(*n_in, p.n_cap);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t k = keys[i];
+    const int32_t jh = p.hash_mode ? jhash[k] : java_long_hash((int64_t)k);
+    const uint32_t dest = (uint32_t)kg_dest[key_group_of_hash(jh, p.max_parallelism)];
+    const uint32_t b = (dest << p.nsub_log2) | sub_table_of(k, p.nsub_log2);
+    const uint32_t pos = cursor[b]++;
+    if (pos >= p.bucket_cap) {
+      flags[0] |= 1u;  // more keys than the owner's sub-table holds: table full
+      continue;
+    }
+    Rec& r = out[(size_t)b * p.bucket_cap + pos];
+    r.key = k;
+    r.val = acc[i];
+    r.t = 0;
+    r.aux = cnt[i];
+  }
+}
+
 }  // namespace cpu
 }  // namespace mxs

@@ -1308,6 +1308,73 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Local-global window aggregation (G > 1): every rank folds its own events into a local table
+// of the whole key space (no per-event exchange); when a window fires, the rows of the local
+// fire (key, partial accumulator, count) travel to the key's owner rank as combined records.
+// One workgroup scatters kScatU * 1024 rows: LDS histogram over the (owner, sub-table) buckets,
+// one global cursor atomic per touched bucket, then the writes. The row count comes from the
+// fire's device counter, so no host round trip sits between the local fire and the exchange.
+// ------------------------------------------------------------------------------------------
+constexpr int kScatThreads = 1024;
+constexpr int kScatU = 8;
+
+__global__ __launch_bounds__(kScatThreads) void scatter_partials_kernel(
+    const uint64_t* __restrict__ keys, const uint64_t* __restrict__ acc,
+    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ n_in, ScatPlan p,
+    const int32_t* __restrict__ jhash, const int32_t* __restrict__ kg_dest,
+    uint32_t* __restrict__ cursor, Rec* __restrict__ out, uint32_t* __restrict__ flags) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t scm[];
+  const int nb = p.nranks << p.nsub_log2;
+  uint32_t* lcnt = scm;       // [nb] rows of this group per bucket
+  uint32_t* lbase = scm + nb;  // [nb] the group's base in each bucket
+  uint32_t n = *n_in;
+  n = n < p.n_cap ? n : p.n_cap;
+  const uint32_t r0 = blockIdx.x * (uint32_t)(kScatThreads * kScatU);
+  if (r0 >= n) return;  // workgroup-uniform
+  for (int b = threadIdx.x; b < nb; b += kScatThreads) lcnt[b] = 0;
+  __syncthreads();
+  uint32_t bk[kScatU], rk[kScatU];
+  uint64_t kk[kScatU];
+#pragma unroll
+  for (int u = 0; u < kScatU; ++u) {
+    const uint32_t i = r0 + (uint32_t)u * kScatThreads + threadIdx.x;
+    bk[u] = 0xFFFFFFFFu;
+    if (i < n) {
+      const uint64_t k = keys[i];
+      kk[u] = k;
+      const int32_t jh = p.hash_mode ? jhash[k] : java_long_hash((int64_t)k);
+      const uint32_t dest = (uint32_t)kg_dest[key_group_of_hash(jh, p.max_parallelism)];
+      bk[u] = (dest << p.nsub_log2) | sub_table_of(k, p.nsub_log2);
+      rk[u] = atomicAdd(&lcnt[bk[u]], 1u);
+    }
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nb; b += kScatThreads) {
+    const uint32_t c = lcnt[b];
+    lbase[b] = c ? atomicAdd(&cursor[b], c) : 0u;
+  }
+  __syncthreads();
+  bool ovf = false;
+#pragma unroll
+  for (int u = 0; u < kScatU; ++u) {
+    if (bk[u] == 0xFFFFFFFFu) continue;
+    const uint32_t i = r0 + (uint32_t)u * kScatThreads + threadIdx.x;
+    const uint32_t pos = lbase[bk[u]] + rk[u];
+    if (pos >= p.bucket_cap) {
+      ovf = true;
+      continue;
+    }
+    Rec r;
+    r.key = kk[u];
+    r.val = acc[i];
+    r.t = 0;
+    r.aux = cnt[i];
+    out[(size_t)bk[u] * p.bucket_cap + pos] = r;
+  }
+  if (ovf) atomicOr(&flags[0], 1u);
+}
+
 // Stateless predicate (chapter1 filter `usage > 90`, Main.java:31) over one f64 column.
 __global__ __launch_bounds__(256) void expr_filter_kernel(const double* __restrict__ x, int64_t n,
                                                           ExprProg prog, uint8_t* __restrict__ keep) {
@@ -2368,6 +2435,10 @@ int grid_for(int64_t n, int block, int max_blocks) {
 
 namespace gpu {
 
+// hipDeviceScheduleSpin: host threads spin (instead of yielding / sleeping) in every
+// synchronisation; set before the device's context exists (bench.py MXS_SPIN=1).
+int set_spin_schedule() { return (int)hipSetDeviceFlags(hipDeviceScheduleSpin); }
+
 int device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -2599,6 +2670,28 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
                      dim3(kFireThreads), lds,
                      (hipStream_t)stream, keys_g, acc_g, cnt_g, dirty_g, plan, out_keys, out_vals,
                      out_raw, out_cnt, out_n);
+  HIP_CHECK(hipGetLastError());
+}
+
+void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt,
+                      const uint32_t* n_in, const ScatPlan& plan, const int32_t* jhash,
+                      const int32_t* kg_dest, uint32_t* cursor, Rec* out, uint32_t* flags,
+                      intptr_t stream) {
+  if (plan.n_cap == 0) return;
+  const int nb = plan.nranks << plan.nsub_log2;
+  if (nb > 16384) throw std::invalid_argument("scatter_partials: more than 16384 buckets");
+  const size_t lds = (size_t)nb * 2 * sizeof(uint32_t);
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)scatter_partials_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  const int64_t per = (int64_t)kScatThreads * kScatU;
+  const int grid = (int)((plan.n_cap + per - 1) / per);
+  hipLaunchKernelGGL(scatter_partials_kernel, dim3(grid), dim3(kScatThreads), lds,
+                     (hipStream_t)stream, keys, acc, cnt, n_in, plan, jhash, kg_dest, cursor, out,
+                     flags);
   HIP_CHECK(hipGetLastError());
 }
 

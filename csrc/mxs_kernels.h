@@ -44,6 +44,16 @@ struct FirePlan {
   ExprProg filt;        // predicate on the mapped value (empty = true)
 };
 
+// Local-global window aggregation (G > 1): where the rows of a locally fired window go.
+struct ScatPlan {
+  int32_t max_parallelism;  // Flink maxParallelism (key groups)
+  int32_t nranks;           // G
+  int32_t nsub_log2;        // owner sub-tables per rank = 1 << nsub_log2
+  int32_t hash_mode;        // 0: Long.hashCode(key); 1: jhash table lookup (string dict ids)
+  uint32_t bucket_cap;      // capacity of one (owner, sub-table) bucket
+  uint32_t n_cap;           // rows readable in the input columns
+};
+
 // Rolling keyed state plan (ValueState / rolling reduce, no windows).
 struct RollPlan {
   int32_t cap_log2;
@@ -57,6 +67,7 @@ struct RollPlan {
 // ---- GPU launchers (kernels_hip.hip) --------------------------------------------------------
 namespace gpu {
 int device_count();
+int set_spin_schedule();
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
@@ -143,6 +154,10 @@ void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_
                   uint32_t* out_n, uint32_t out_cap, int abits, int shift, intptr_t stream);
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
                  int64_t proc_now, int64_t* red, const uint32_t* flags, intptr_t stream);
+void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt,
+                      const uint32_t* n_in, const ScatPlan& plan, const int32_t* jhash,
+                      const int32_t* kg_dest, uint32_t* cursor, Rec* out, uint32_t* flags,
+                      intptr_t stream);
 }  // namespace gpu
 
 // ---- CPU twins (kernels_cpu.cpp) ------------------------------------------------------------
@@ -180,6 +195,9 @@ void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const
 void f64_order_bits(const uint64_t* v, int64_t n, uint64_t* o);
 void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uint64_t* ord,
                     double* out);
+void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt,
+                      const uint32_t* n_in, const ScatPlan& plan, const int32_t* jhash,
+                      const int32_t* kg_dest, uint32_t* cursor, Rec* out, uint32_t* flags);
 }  // namespace cpu
 
 }  // namespace mxs

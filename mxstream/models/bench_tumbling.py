@@ -39,6 +39,7 @@ class TumblingBenchConfig:
     # are both HBM-bound and overlapping them measured slower (0.45 -> 0.75 ms/step,
     # profiles/r2_pipeline_g1.md).
     pipeline: bool | None = None
+    exchange: str = "auto"           # G > 1: "partials" (local-global) or "records"
 
 
 class TumblingWindowBench:
@@ -55,7 +56,8 @@ class TumblingWindowBench:
             max_keys=cfg.keys, parallelism=world, batch_capacity=cfg.batch,
             ooo_bound=cfg.disorder_ms, map_prog=E.compile_expr(mbps),
             filter_prog=E.compile_expr(E.var(E.VAR_MAPPED) < self.threshold_mbps),
-            pipeline=(world > 1) if cfg.pipeline is None else cfg.pipeline)
+            pipeline=(world > 1) if cfg.pipeline is None else cfg.pipeline,
+            exchange=cfg.exchange)
         self.keys = torch.empty(cfg.batch, dtype=torch.int64, device=device)
         self.ts = torch.empty(cfg.batch, dtype=torch.int64, device=device)
         self.vals = torch.empty(cfg.batch, dtype=torch.int64, device=device)

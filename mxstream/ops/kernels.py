@@ -238,6 +238,40 @@ def window_fire(keys_g, acc_g, cnt_g, dirty_g, *, agg: int, npanes: int, ring: i
         m.cpu_window_fire(*args)
 
 
+def scatter_partials(keys, acc, cnt, n_dev, *, n_cap: int, max_parallelism: int, nranks: int,
+                     nsub_log2: int, hash_mode: int, jhash, kg_dest, bucket_cap: int, cursor, out,
+                     flags) -> None:
+    """Local-global window aggregation: the first min(n_dev[0], n_cap) rows of a local fire
+    (key, partial accumulator, count) -> combined records in their owner's (rank, sub-table)
+    bucket of `out` (bucket_cap records each; cursor counts). A bucket overflow sets flags bit0
+    (the owner's sub-table cannot hold that many keys)."""
+    dev = keys.device
+    nb = nranks << nsub_log2
+    _check(keys, torch.int64, n_cap, "keys", dev)
+    _check(acc, torch.int64, n_cap, "acc", dev)
+    _check(cnt, torch.int32, n_cap, "cnt", dev)
+    _check(n_dev, torch.int32, 1, "n", dev)
+    _check(kg_dest, torch.int32, max_parallelism, "kg_dest", dev)
+    _check(cursor, torch.int32, nb, "cursor", dev)
+    _check(out, torch.int64, nb * bucket_cap * REC_WORDS, "out", dev)
+    _check(flags, torch.int32, 1, "flags", dev)
+    if hash_mode:
+        if jhash is None:
+            raise ValueError("hash_mode=1 needs the dictionary jhash table")
+        _check(jhash, torch.int32, 1, "jhash", dev)
+    if n_cap >= (1 << 32):
+        raise ValueError("too many rows")
+    plan = dict(max_parallelism=max_parallelism, nranks=nranks, nsub_log2=nsub_log2,
+                hash_mode=hash_mode, bucket_cap=bucket_cap, n_cap=n_cap)
+    m = load()
+    args = (_p(keys), _p(acc), _p(cnt), _p(n_dev), plan, _p(jhash), _p(kg_dest), _p(cursor),
+            _p(out), _p(flags))
+    if _is_gpu(keys):
+        m.gpu_scatter_partials(*args, _stream(keys))
+    else:
+        m.cpu_scatter_partials(*args)
+
+
 def rolling(recs, counts, *, cap_log2: int, nsub: int, agg: int, nsrc: int, bucket_cap: int,
             emit: bool, keys_g, acc_g, cnt_g, occ, flags, out_vals=None) -> None:
     dev = keys_g.device

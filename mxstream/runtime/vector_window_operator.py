@@ -68,6 +68,8 @@ class VectorWindowOperator(KeyedWindowOperator):
         self._vec = vecs
         return super().process(keys, ts, self._rows[:n])
 
+    _local_global_ok = False  # vector panes are exchanged per step (records mode)
+
     # ---- hooks -----------------------------------------------------------------------------
     def _rec_words(self) -> int:
         return 2 if self.compact else 3

@@ -114,6 +114,19 @@ _NP_DTYPE = {torch.int64: np.int64, torch.int32: np.int32, torch.float64: np.flo
              torch.bfloat16: np.uint16, torch.float16: np.float16}
 
 
+# How the step's host sync waits for the GPU (MXS_SYNC, measured in profiles/r2_host_sync.md):
+#   "stream" (default): hipStreamSynchronize of the caller's stream when nothing else is queued
+#     on it (unpipelined); "event": hipEventSynchronize on the step's event.
+_SYNC = __import__("os").environ.get("MXS_SYNC", "stream")
+
+
+def _host_wait(ev, device, pipelined: bool) -> None:
+    if _SYNC == "event" or pipelined:
+        ev.synchronize()
+    else:
+        torch.cuda.current_stream(device).synchronize()
+
+
 def _next_pow2(x: int) -> int:
     return 1 << max(0, int(x - 1).bit_length())
 
@@ -127,6 +140,21 @@ def java_rem(a: int, b: int) -> int:
 def java_window_start(ts: int, offset: int, size: int) -> int:
     """TimeWindow.getWindowStartWithOffset with Java's truncated remainder."""
     return ts - java_rem(ts - offset + size, size)
+
+
+def combine_partials(agg: int, acc: torch.Tensor, inv: torch.Tensor, n: int) -> torch.Tensor:
+    """Fold rows of exported accumulators (int64 bit patterns) into n groups (`inv`: group of
+    each row) with the aggregate's combine: sum / min / max over int64 or float64 values."""
+    f64 = agg in (K.AGG_SUM_F64, K.AGG_AVG_F64, K.AGG_MIN_F64, K.AGG_MAX_F64)
+    x = acc.view(torch.float64) if f64 else acc
+    if agg in (K.AGG_MIN_I64, K.AGG_MIN_F64, K.AGG_MAX_I64, K.AGG_MAX_F64):
+        is_min = agg in (K.AGG_MIN_I64, K.AGG_MIN_F64)
+        init = (float("inf") if is_min else float("-inf")) if f64 else (I64_MAX if is_min else I64_MIN)
+        out = torch.full((n,), init, dtype=x.dtype, device=x.device)
+        out.scatter_reduce_(0, inv, x, "amin" if is_min else "amax")
+    else:
+        out = torch.zeros(n, dtype=x.dtype, device=x.device).index_add_(0, inv, x)
+    return out.view(torch.int64) if f64 else out
 
 
 @dataclass
@@ -206,7 +234,7 @@ class KeyedWindowOperator:
                  side_output_late: bool = False, late_capacity: int = 1 << 16,
                  clock: Callable[[], int] | None = None, external_watermark: bool = False,
                  combine: bool | None = None, compact: bool | None = None,
-                 pipeline: bool | None = None):
+                 pipeline: bool | None = None, exchange: str = "auto"):
         self.device = K.resolve_device(device)
         self.comm = comm or LocalComm()
         self.world = self.comm.world
@@ -234,14 +262,35 @@ class KeyedWindowOperator:
         self.side_output_late = side_output_late
         self.metrics = OperatorMetrics()
 
+        # ---- keyBy exchange strategy (G > 1) ----
+        # "records": per step, every event (pre-aggregated per (key, pane) by the sender-side
+        #   combiner) crosses the all-to-all to the key's owner, whose table holds its key share.
+        # "partials" (local-global aggregation): per step, every rank folds its own events into a
+        #   local table of the whole key space -- no per-event exchange; when a window fires, the
+        #   local fire's rows (key, partial accumulator, count) cross ONE all-to-all to the owner,
+        #   which merges them and evaluates the window (epilogue, filter, emit). Every aggregate
+        #   here is associative, so the emitted rows are identical; the exchange shrinks from
+        #   ~#distinct (key, pane) per step to #keys per window, and the per-step work of a rank
+        #   is the G = 1 step. HBM (288 GB) holds the whole key space per rank many times over.
+        #   Needs allowedLateness = 0 (a late refire would need every rank's delta since the
+        #   first fire), so "auto" picks it exactly then.
+        if exchange not in ("auto", "records", "partials"):
+            raise ValueError("exchange must be 'auto', 'records' or 'partials'")
+        lg_ok = self.world > 1 and self.lateness == 0 and self._local_global_ok
+        if exchange == "partials" and self.world > 1 and not lg_ok:
+            raise ValueError("exchange='partials' needs allowed_lateness == 0")
+        self.local_global = lg_ok and exchange != "records"
+        self._exchanging = self.world > 1 and not self.local_global
+        self._part_ranks = self.world if self._exchanging else 1
+
         # ---- state geometry ----
         from .geometry import state_geometry
 
         self.nsub, self.cap_log2 = (self._geometry(max_keys, cap_log2) if self._geometry
-                                    else state_geometry(max_keys, self.world, cap_log2))
+                                    else state_geometry(max_keys, self._part_ranks, cap_log2))
         cap_log2 = self.cap_log2
         self.nsub_log2 = self.nsub.bit_length() - 1
-        if self.nsub * self.world > 16384:
+        if self.nsub * self._part_ranks > 16384:
             raise ValueError("key space too large for the bucket histogram; raise cap_log2")
         self.nslots = self.nsub << cap_log2
         self.ring = max(4, _next_pow2(self.panes_per_window + 2 + math.ceil(self.lateness / self.pane)
@@ -259,14 +308,15 @@ class KeyedWindowOperator:
         self.kg_dest = torch.tensor(kgd, dtype=torch.int32, device=dev)
 
         # ---- per-step buffers ----
-        self.nbuckets = self.world << self.nsub_log2
+        self.nbuckets = self._part_ranks << self.nsub_log2
         # G > 1: sender-side combiner before the all-to-all (all aggregates are associative).
-        self.combine = self.world > 1 if combine is None else bool(combine and self.world > 1)
+        self.combine = (self._exchanging if combine is None
+                        else bool(combine and self._exchanging))
         # Pipelining: the partition of batch i+1 overlaps the state half of batch i (process()
         # then returns the windows fired by the previous batch; flush() drains). Opt-in: the
         # engine's hot loops (bench, configs) enable it; callers that need each batch's fires
         # from its own call (DataStream API, external watermarks) keep the default.
-        self.pipeline = bool(pipeline) and not external_watermark
+        self.pipeline = bool(pipeline) and not external_watermark and not self.local_global
         self.s1 = (torch.cuda.Stream(dev) if self.pipeline and self.device.type == "cuda"
                    else None)
         self._par = 0
@@ -292,8 +342,16 @@ class KeyedWindowOperator:
         # flags: [0] table full (bit0) / [1] combiner overflow / [2] fired-row cursor (out_n), so
         # one 16-byte D2H after a fire returns the row count and the table-full bit together.
         self.out_n = self.flags[2:3]
+        # Pinned slabs for fired rows, allocated here: a first-fire pinned allocation of the
+        # whole-table slab costs milliseconds of host time inside a step.
+        self._pool = None
+        if dev.type == "cuda":
+            self._pool = PinnedSlabPool()
+            self._pool.take(self.nslots * 28 + 4 * 256)
         self.late_idx = (torch.empty(late_capacity, dtype=torch.int32, device=dev)
                          if side_output_late else None)
+        if self.local_global:
+            self._init_owner_tables(max_keys, cap_log2)
         self.comb_send = self.comb_recv = None
         self.comb_counts = torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
         self._ccap_hint = 1 << self.cap_log2
@@ -314,6 +372,35 @@ class KeyedWindowOperator:
         self.min_live_pane: int | None = None      # oldest unpurged pane
         self.max_seen_pane: int | None = None
         self.late_side: list[np.ndarray] = []
+
+    _local_global_ok = True  # subclasses whose fire is not a plain reduce opt out
+
+    def _init_owner_tables(self, max_keys: int, cap_log2: int | None) -> None:
+        """Local-global mode: the owner side of a fire -- the merge table of this rank's key
+        share (one pane: the window being fired) and the fire exchange buffers. A bucket
+        (owner, owner sub-table) holds at most one row per key of that sub-table, so its
+        capacity is the sub-table's: the fire exchange cannot overflow unless the owner's table
+        is full (reported as such)."""
+        from .geometry import state_geometry
+
+        dev = self.device
+        self.nsub_o, self.cap_log2_o = state_geometry(max_keys, self.world, cap_log2)
+        self.nsub_o_log2 = self.nsub_o.bit_length() - 1
+        if self.nsub_o * self.world > 16384:
+            raise ValueError("key space too large for the fire exchange; raise cap_log2")
+        nslots_o = self.nsub_o << self.cap_log2_o
+        self.keys_m = torch.full((nslots_o,), -1, dtype=torch.int64, device=dev)
+        self.acc_m = torch.zeros(nslots_o, dtype=torch.int64, device=dev)
+        self.cnt_m = torch.zeros(nslots_o, dtype=torch.int32, device=dev)
+        self.dirty_m = torch.zeros(nslots_o, dtype=torch.uint8, device=dev)
+        self.occ_m = torch.zeros(self.nsub_o, dtype=torch.int32, device=dev)
+        self.fbcap = 1 << self.cap_log2_o
+        nbf = self.world << self.nsub_o_log2
+        self.fsend = torch.empty(nbf * self.fbcap * K.REC_WORDS, dtype=torch.int64, device=dev)
+        self.frecv = torch.empty_like(self.fsend)
+        self.fcursor = torch.zeros(nbf, dtype=torch.int32, device=dev)
+        self.frecv_counts = torch.zeros(nbf, dtype=torch.int32, device=dev)
+        self.part_n = torch.zeros(1, dtype=torch.int32, device=dev)
 
     # ------------------------------------------------------------------------------------
     def _rank_of_kg(self, kg: int) -> int:
@@ -340,15 +427,15 @@ class KeyedWindowOperator:
                              for _ in range(nbuf)]
         # The plain exchange lands in `recv`; with the combiner only combined records travel.
         self.recv = (torch.empty(words, dtype=torch.int64, device=dev)
-                     if self.world > 1 and not self.combine else None)
+                     if self._exchanging and not self.combine else None)
         self._recv_counts = (torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
-                             if self.world > 1 else None)
+                             if self._exchanging else None)
         self._use_par(0)
 
     def _use_par(self, p: int) -> None:
         """Point send/cursor (and, at G = 1, recv/recv_counts) at buffer set `p`."""
         self.send, self.cursor = self._send_bufs[p], self._cursor_bufs[p]
-        if self.world == 1:
+        if not self._exchanging:
             self.recv, self.recv_counts = self.send, self.cursor
         else:
             self.recv_counts = self._recv_counts
@@ -407,7 +494,7 @@ class KeyedWindowOperator:
     def _combine_finish(self, b: "_Back"):
         while True:
             if b.chk_ev is not None:
-                b.chk_ev.synchronize()
+                _host_wait(b.chk_ev, self.device, self.pipeline)
             ovf, fill = (-int(x) for x in self._hchk.tolist())
             if not ovf:
                 break
@@ -550,7 +637,8 @@ class KeyedWindowOperator:
         stats, red = self._stats[p], self._red[p]
         K.step_begin(self.cursor, stats)
         plan = K.PartitionPlan(
-            max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2, nranks=self.world,
+            max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2,
+            nranks=self._part_ranks,
             window_mode=1, drop_late=int(event_mode), hash_mode=self.hash_mode,
             bucket_cap=self.bucket_cap, late_ts=self._late_ts(f.old_wm),
             tbase=self.pane_start(f.pane_base), pane=self.pane,
@@ -577,7 +665,7 @@ class KeyedWindowOperator:
         """The step's host sync: overflow handling (redo), watermark and pane bookkeeping."""
         while True:
             if f.ev is not None:
-                f.ev.synchronize()
+                _host_wait(f.ev, self.device, self.pipeline)
             host = self._hred[f.par].tolist()
             if host[4]:
                 raise RuntimeError("event timestamp outside the representable pane range "
@@ -662,19 +750,19 @@ class KeyedWindowOperator:
                     with self._stage("all_to_all"):
                         recs, counts, bcap = self._combine_finish(b)
                     combined = 1
-                elif self.world > 1:
+                elif self._exchanging:
                     with self._stage("all_to_all"):
                         self._exchange(2 if b.compact else 3)
-                if cuda and self.world > 1:
+                if cuda and self._exchanging:
                     self._ev_consumed[b.par] = self._event()
                 aplan = K.AggPlan(cap_log2=self.cap_log2, nsub=self.nsub, ring=self.ring,
-                                  agg=self.agg, nsrc=self.world, bucket_cap=bcap,
+                                  agg=self.agg, nsrc=self._part_ranks, bucket_cap=bcap,
                                   np_step=b.np_step, pg=b.pg, pane_base=b.pane_base,
                                   p_lo=b.qmin, fired_hi=b.fired_hi, combined=combined,
                                   rec_words=3 if combined else (2 if b.compact else 3))
                 with self._stage("window_agg"):
                     self._aggregate(recs, counts, aplan)
-                if cuda and self.world == 1:
+                if cuda and not self._exchanging:
                     self._ev_consumed[b.par] = self._event()
                 if self._debug:
                     from ..ops.debug import assert_table_ok
@@ -751,6 +839,8 @@ class KeyedWindowOperator:
         p1 = min(self.pane_of(s) + self.panes_per_window - 1, self.max_seen_pane)
         if p1 < p0:
             return None
+        if self.local_global:
+            return self._fire_window_partials(s, p0, p1)
         self.out_n.zero_()
         K.window_fire(self.keys_g, self.acc_g, self.cnt_g, self.dirty_g, agg=self.agg,
                       npanes=p1 - p0 + 1, ring=self.ring, p0=p0, wstart=s,
@@ -763,9 +853,61 @@ class KeyedWindowOperator:
             return None
         n = min(n, self.out_keys.numel())
         self.metrics.num_records_out += n
-        host = to_host_arrays([self.out_keys, self.out_vals, self.out_raw, self.out_cnt], n)
+        host = to_host_arrays([self.out_keys, self.out_vals, self.out_raw, self.out_cnt], n,
+                              self._pool)
         return FireResult(s, s + self.size, host[0].view(np.uint64), host[1], host[2], host[3],
                           refire=only_dirty)
+
+    def _fire_window_partials(self, s: int, p0: int, p1: int) -> FireResult | None:
+        """Local-global fire of window [s, s + size): local partials -> owner -> emit.
+
+        1. local fire without epilogue: one row (key, partial acc, count) per local key with
+           data in the window (all ranks, collectively identical decisions);
+        2. scatter_partials: rows -> combined records in (owner rank, owner sub-table) buckets;
+        3. ONE equal-split all-to-all of the buckets (+ their counts) over RCCL;
+        4. the owner folds the G partials per key into its merge table (window_agg, combined
+           records) and fires that with the fused map/filter epilogue; the merge pane is reset.
+        The row count of step 1 stays on the device until the owner's fire is counted."""
+        self.part_n.zero_()
+        K.window_fire(self.keys_g, self.acc_g, self.cnt_g, self.dirty_g, agg=self.agg,
+                      npanes=p1 - p0 + 1, ring=self.ring, p0=p0, wstart=s, wend=s + self.size,
+                      only_dirty=False, map_prog=E.EMPTY, filt_prog=E.EMPTY,
+                      out_keys=self.out_keys, out_vals=self.out_vals, out_raw=self.out_raw,
+                      out_cnt=self.out_cnt, out_n=self.part_n)
+        self.fcursor.zero_()
+        K.scatter_partials(self.out_keys, self.out_raw, self.out_cnt, self.part_n,
+                           n_cap=self.out_keys.numel(), max_parallelism=self.max_parallelism,
+                           nranks=self.world, nsub_log2=self.nsub_o_log2,
+                           hash_mode=self.hash_mode, jhash=self.jhash, kg_dest=self.kg_dest,
+                           bucket_cap=self.fbcap, cursor=self.fcursor, out=self.fsend,
+                           flags=self.flags)
+        with self._stage("all_to_all"):
+            self.comm.all_to_all(self.frecv, self.fsend)
+            self.comm.all_to_all(self.frecv_counts, self.fcursor)
+        self.metrics.extra["a2a_bytes"] = self.metrics.extra.get("a2a_bytes", 0) + \
+            self.fsend.numel() * 8
+        mplan = K.AggPlan(cap_log2=self.cap_log2_o, nsub=self.nsub_o, ring=1, agg=self.agg,
+                          nsrc=self.world, bucket_cap=self.fbcap, np_step=1, pg=1, pane_base=0,
+                          p_lo=0, fired_hi=I64_MIN, combined=1, rec_words=3)
+        K.window_agg(self.frecv, self.frecv_counts, mplan, self.keys_m, self.acc_m, self.cnt_m,
+                     self.dirty_m, self.occ_m, self.flags)
+        self.out_n.zero_()
+        K.window_fire(self.keys_m, self.acc_m, self.cnt_m, self.dirty_m, agg=self.agg, npanes=1,
+                      ring=1, p0=0, wstart=s, wend=s + self.size, only_dirty=False,
+                      map_prog=self.map_prog, filt_prog=self.filter_prog,
+                      out_keys=self.out_keys, out_vals=self.out_vals, out_raw=self.out_raw,
+                      out_cnt=self.out_cnt, out_n=self.out_n)
+        self.acc_m.zero_()
+        self.cnt_m.zero_()
+        n = self._fired_count()
+        self.metrics.num_fires += 1
+        if n == 0:
+            return None
+        n = min(n, self.out_keys.numel())
+        self.metrics.num_records_out += n
+        host = to_host_arrays([self.out_keys, self.out_vals, self.out_raw, self.out_cnt], n,
+                              self._pool)
+        return FireResult(s, s + self.size, host[0].view(np.uint64), host[1], host[2], host[3])
 
     def _fired_count(self) -> int:
         """Rows the last fire produced; raises if any aggregation found its table full (a key
@@ -948,8 +1090,19 @@ class KeyedWindowOperator:
         slot = slots_u[inv]
         pane = torch.from_numpy(np.ascontiguousarray(rows["pane"])).to(dev)
         idx = (pane & (self.ring - 1)) * self.nslots + slot
-        self.acc_g[idx] = torch.from_numpy(np.ascontiguousarray(rows["acc"])).to(dev)
-        self.cnt_g[idx] = torch.from_numpy(np.ascontiguousarray(rows["cnt"])).to(dev)
-        self.dirty_g[idx] = torch.from_numpy(np.ascontiguousarray(rows["dirty"])).to(dev)
+        acc = torch.from_numpy(np.ascontiguousarray(rows["acc"])).to(dev)
+        cnt = torch.from_numpy(np.ascontiguousarray(rows["cnt"])).to(dev)
+        dirty = torch.from_numpy(np.ascontiguousarray(rows["dirty"])).to(dev)
+        u, inv = torch.unique(idx, return_inverse=True)
+        if u.numel() == idx.numel():
+            self.acc_g[idx], self.cnt_g[idx], self.dirty_g[idx] = acc, cnt, dirty
+        else:
+            # Several rows per (key, pane): partial accumulators of a local-global checkpoint
+            # (every rank held a partial of every key) -- fold them with the aggregate.
+            self.acc_g[u] = combine_partials(self.agg, acc, inv, u.numel())
+            self.cnt_g[u] = torch.zeros(u.numel(), dtype=torch.int32, device=dev).index_add_(
+                0, inv, cnt)
+            self.dirty_g[u] = torch.zeros(u.numel(), dtype=torch.int32, device=dev).scatter_reduce_(
+                0, inv, dirty.to(torch.int32), "amax").to(torch.uint8)
         self.occ.copy_(torch.bincount(slots_u >> self.cap_log2, minlength=self.nsub)
                        .to(torch.int32))

@@ -36,13 +36,15 @@ def main() -> int:
     ap.add_argument("--keys", type=int, default=1_000_000)
     ap.add_argument("--out", default=None)
     ap.add_argument("--no-pipeline", action="store_true")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "records", "partials"])
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
 
     def rank_fn(comm):
         b = TumblingWindowBench(TumblingBenchConfig(keys=a.keys, batch=a.batch,
-                                                    pipeline=not a.no_pipeline), comm, dev)
+                                                    pipeline=not a.no_pipeline,
+                                                    exchange=a.exchange), comm, dev)
         for _ in range(a.warmup):
             b.step()
         torch.cuda.synchronize()
@@ -62,7 +64,7 @@ def main() -> int:
     out = {
         "what": "G virtual ranks on one MI355X (LoopbackComm): per-rank step cost of the G>1 path",
         "world": a.world, "steps": a.steps, "warmup": a.warmup, "batch_per_rank": a.batch,
-        "keys": a.keys, "pipeline": not a.no_pipeline, "wall_s": dt, "per_rank_step_ms": per_rank_ms,
+        "keys": a.keys, "pipeline": not a.no_pipeline, "exchange": a.exchange, "wall_s": dt, "per_rank_step_ms": per_rank_ms,
         "per_rank_events_per_s": a.batch / (per_rank_ms / 1e3),
         "alerts": sum(r[1] for r in res), "extra_rank0": res[0][2],
         "bucket_regrows": [r[3] for r in res],

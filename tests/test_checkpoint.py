@@ -253,8 +253,8 @@ def _spawn(world, root, mode):
     return sorted(x for _r, f in res for x in f)
 
 
-def _single_run_tail(world_sources):
-    op = _win(batch_capacity=PER * world_sources)
+def _single_run_tail(world_sources, **kw):
+    op = _win(batch_capacity=PER * world_sources, **kw)
     out = []
     for s in range(STEPS):
         parts = [_batch(s, src=r) for r in range(world_sources)]
@@ -352,3 +352,48 @@ def test_gpu_session_and_rolling_restore(tmp_path):
     assert sorted(tail) == sorted(t2)
     for key in (3, 99, 2048):
         assert r_op.state_of(key) == r2.state_of(key)
+
+
+# ---- local-global window state (exchange="partials") ------------------------------------------
+def test_local_global_checkpoint_rescale(tmp_path):
+    """Every rank of a local-global operator holds PARTIAL accumulators of every key it saw;
+    its checkpoint files therefore carry several rows per (key, pane). Restoring at any world
+    size folds them (restore_state combines duplicate rows with the aggregate), and the run
+    continues exactly like an uninterrupted single-rank run."""
+    from mxstream.parallel.comm import run_loopback
+
+    def mk(comm=None, world=1):
+        return _win(comm=comm, lateness=0, batch_capacity=PER * 2, exchange="auto")
+
+    strip = lambda f: sorted(x[:4] for x in f)
+    ref = strip(_single_run_tail(2, lateness=0))
+    root = tmp_path / "lg"
+    storage = CheckpointStorage(root, job_id="c" * 32)
+
+    def write(comm):
+        op = mk(comm)
+        assert op.local_global
+        coord = CheckpointCoordinator(storage, {"window": op})
+        for s in range(CUT + 1):
+            op.process(*_batch(s, src=comm.rank))
+        coord.trigger(CUT)
+        return True
+
+    run_loopback(2, write)
+
+    def read(comm):
+        op = mk(comm)
+        CheckpointCoordinator(storage, {"window": op}).restore()
+        out = []
+        for s in range(CUT + 1, STEPS):
+            # Two source partitions feed the job; at world 1 one rank reads both.
+            if comm.world == 1:
+                parts = [_batch(s, src=r) for r in range(2)]
+                out += op.process(*[torch.cat([p[i] for p in parts]) for i in range(3)])
+            else:
+                out += op.process(*_batch(s, src=comm.rank))
+        return _fires(out + op.finish())
+
+    for world in (1, 2):
+        got = sorted(x for f in run_loopback(world, read) for x in f)
+        assert strip(got) == ref, world

@@ -59,12 +59,15 @@ def _skip_no_gpu(dev):
 
 @pytest.mark.parametrize("dev", _devices())
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
-@pytest.mark.parametrize("size,slide,lateness", [(3000, 3000, 0), (4000, 1000, 1500)])
+@pytest.mark.parametrize("size,slide,lateness,exchange", [
+    (3000, 3000, 0, "records"), (3000, 3000, 0, "partials"), (4000, 1000, 0, "partials"),
+    (4000, 1000, 1500, "records")])
 @pytest.mark.parametrize("pipeline", [False, True])
-def test_window_invariant_to_world(dev, world, size, slide, lateness, pipeline):
+def test_window_invariant_to_world(dev, world, size, slide, lateness, exchange, pipeline):
     """pipeline=True: the partition of batch i+1 overlaps the combiner / all-to-all /
     aggregation / firing of batch i on a second stream (GPU); on the CPU twins the same
-    one-step-deferred control flow runs synchronously."""
+    one-step-deferred control flow runs synchronously. exchange='partials': local-global
+    aggregation (no per-step exchange; partial accumulators travel when a window fires)."""
     _skip_no_gpu(dev)
     per, nkeys, cap_log2 = _sizes(dev)
 
@@ -72,7 +75,7 @@ def test_window_invariant_to_world(dev, world, size, slide, lateness, pipeline):
         return KeyedWindowOperator(size=size, slide=slide, lateness=lateness, agg=K.AGG_SUM_I64,
                                    device=dev, comm=comm, max_keys=nkeys,
                                    batch_capacity=batch_capacity, ooo_bound=500, cap_log2=cap_log2,
-                                   pipeline=pipe)
+                                   pipeline=pipe, exchange=exchange)
 
     def rank_fn(comm):
         op = make(comm, per)
@@ -112,7 +115,8 @@ def test_window_loopback_without_combiner(dev, compact):
     def rank_fn(comm):
         op = KeyedWindowOperator(size=3000, agg=K.AGG_SUM_I64, device=dev, comm=comm,
                                  max_keys=nkeys, batch_capacity=per, ooo_bound=500,
-                                 cap_log2=cap_log2, combine=False, compact=compact)
+                                 cap_log2=cap_log2, combine=False, compact=compact,
+                                 exchange="records")
         out = []
         for step in range(STEPS):
             out += op.process(*_batch(dev, comm.rank, step, per, nkeys))
@@ -130,8 +134,9 @@ def test_window_loopback_without_combiner(dev, compact):
 
 
 @pytest.mark.parametrize("dev", _devices())
-@pytest.mark.parametrize("pipeline", [False, True])
-def test_window_loopback_bucket_regrow(dev, pipeline):
+@pytest.mark.parametrize("pipeline,exchange", [(False, "records"), (True, "records"),
+                                               (False, "partials")])
+def test_window_loopback_bucket_regrow(dev, pipeline, exchange):
     """A skewed rank overflows its fixed-capacity buckets: every rank regrows and redoes the
     step together (the flag travels in the step's MIN all-reduce), results unchanged."""
     _skip_no_gpu(dev)
@@ -147,7 +152,8 @@ def test_window_loopback_bucket_regrow(dev, pipeline):
     def rank_fn(comm):
         op = KeyedWindowOperator(size=3000, agg=K.AGG_SUM_I64, device=dev, comm=comm,
                                  max_keys=nkeys, batch_capacity=per, ooo_bound=500,
-                                 cap_log2=cap_log2, bucket_slack=1.0, pipeline=pipeline)
+                                 cap_log2=cap_log2, bucket_slack=1.0, pipeline=pipeline,
+                                 exchange=exchange)
         out = []
         for step in range(STEPS):
             out += op.process(*batch(comm.rank, step))
