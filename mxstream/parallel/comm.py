@@ -262,13 +262,21 @@ class TorchComm(Comm):
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
+        if self.world > 1:
+            # Create (and, on RCCL, connect) the payload communicator now: every rank constructs
+            # its TorchComm at the same point, while a lazy creation would sit inside the first
+            # all-to-all -- a window firing in the middle of a timed run.
+            g = self._data_group()
+            dev = (torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl"
+                   else torch.device("cpu"))
+            t = torch.zeros(self.world, dtype=torch.int32, device=dev)
+            dist.all_to_all_single(torch.empty_like(t), t, group=g)
 
     def _data_group(self):
         """The keyBy payload travels on its own communicator: RCCL runs each communicator's
         collectives on its own internal stream, so the all-to-all of step i (issued on the
         operator's state stream) does not queue behind the watermark all-reduce of step i+1,
-        which waits for that step's partition kernel. Created on the first all-to-all, which
-        every rank reaches in the same order."""
+        which waits for that step's partition kernel. Created in __init__."""
         g = getattr(self, "_dgroup", None)
         if g is None:
             ranks = dist.get_process_group_ranks(self.group) if self.group is not None else None
