@@ -102,7 +102,8 @@ class KeyedSessionOperator:
                  map_prog: E.Program = E.EMPTY, filter_prog: E.Program = E.EMPTY,
                  ooo_bound: int = 0, max_load: float = 0.7, idle_spill_ms: int | None = None,
                  spill_rows: int = 1 << 20, emit_capacity: int | None = None,
-                 external_watermark: bool = False, host_budget_bytes: int | None = None):
+                 external_watermark: bool = False, host_budget_bytes: int | None = None,
+                 idle_timeout_steps: int | None = None):
         if gap <= 0:
             raise ValueError("session gap must be positive")
         self.device = K.resolve_device(device)
@@ -114,6 +115,10 @@ class KeyedSessionOperator:
         self.map_prog, self.filter_prog = map_prog, filter_prog
         self.ooo_bound = int(ooo_bound)
         self.external_watermark = external_watermark
+        # Idle partitions are left out of the MIN watermark valve (see KeyedWindowOperator).
+        self.idle_timeout_steps = idle_timeout_steps
+        self._idle_marked = False
+        self._empty_steps = 0
         self.max_load = max_load
         self.host_budget_bytes = host_budget_bytes
         self.idle_spill_ms = int(idle_spill_ms if idle_spill_ms is not None else 4 * gap)
@@ -230,6 +235,9 @@ class KeyedSessionOperator:
         if n > self.batch_capacity:
             self._alloc(n, self.slack)
         old_wm = self.wm
+        self._empty_steps = self._empty_steps + 1 if n == 0 else 0
+        idle = self._idle_marked or (self.idle_timeout_steps is not None
+                                     and self._empty_steps >= self.idle_timeout_steps)
         t = ts.min().reshape(1) if n else torch.full((1,), I64_MAX, dtype=torch.int64,
                                                     device=ts.device)
         self.comm.allreduce_min_(t)
@@ -245,6 +253,8 @@ class KeyedSessionOperator:
                 K.partition(keys, ts, vals, plan, self.kg_dest, self.cursor, self.send, self.stats)
             K.step_finish(self.stats, self.local_maxts, self.red, bound=self.ooo_bound,
                           event_mode=True, proc_now=0)
+            if idle:
+                self.red[2:3].fill_(I64_MAX)
             self.comm.allreduce_min_(self.red[:8])
             if self.world > 1:
                 self.comm.all_to_all(self.recv, self.send)
@@ -259,6 +269,8 @@ class KeyedSessionOperator:
                 continue
             break
         wm_global = host[2]
+        if wm_global == I64_MAX:
+            wm_global = old_wm  # every partition idle: the watermark holds
         self.metrics.num_records_in += n
         self.metrics.steps += 1
         if self.gpu:
@@ -270,6 +282,9 @@ class KeyedSessionOperator:
         # (EventTimeTrigger.onElement: maxTimestamp <= currentWatermark -> FIRE).
         wm = old_wm if self.external_watermark else max(old_wm, wm_global)
         return self._fire_at(wm)
+
+    def mark_idle(self, idle: bool = True) -> None:
+        self._idle_marked = bool(idle)
 
     def advance_watermark(self, wm: int) -> SessionRows:
         wm = int(wm)

@@ -182,6 +182,7 @@ class _Front:
     proc_now: int
     compact: bool = True
     ev: object = None
+    idle: bool = False
 
 
 @dataclass
@@ -234,7 +235,8 @@ class KeyedWindowOperator:
                  side_output_late: bool = False, late_capacity: int = 1 << 16,
                  clock: Callable[[], int] | None = None, external_watermark: bool = False,
                  combine: bool | None = None, compact: bool | None = None,
-                 pipeline: bool | None = None, exchange: str = "auto"):
+                 pipeline: bool | None = None, exchange: str = "auto",
+                 idle_timeout_steps: int | None = None):
         self.device = K.resolve_device(device)
         self.comm = comm or LocalComm()
         self.world = self.comm.world
@@ -254,6 +256,13 @@ class KeyedWindowOperator:
         # external_watermark: the caller drives time with advance_watermark() (DataStream API:
         # watermarks come from the upstream assigner); process() then never advances it.
         self.external_watermark = external_watermark
+        # Idle source partitions (Flink StreamStatus IDLE, StatusWatermarkValve): a rank whose
+        # source is idle -- marked with mark_idle(), or empty for `idle_timeout_steps`
+        # consecutive batches -- sends +inf as its watermark, so the MIN over ranks is taken over
+        # the active partitions only; if every partition is idle the watermark holds.
+        self.idle_timeout_steps = idle_timeout_steps
+        self._idle_marked = False
+        self._empty_steps = 0
         self.parallelism = parallelism or self.world
         self.max_parallelism = max_parallelism
         self.hash_mode = hash_mode
@@ -620,11 +629,22 @@ class KeyedWindowOperator:
         if self.pipeline:
             self._par ^= 1
         event_mode = self.time_mode == "event"
-        f = _Front(keys=keys, ts=ts, vals=vals, n=n, par=p, old_wm=self.wm,
+        self._empty_steps = self._empty_steps + 1 if n == 0 else 0
+        f = _Front(keys=keys, ts=ts, vals=vals, n=n, par=p, old_wm=self.wm, idle=self.idle,
                    pane_base=self._pane_base(ts),
                    proc_now=0 if event_mode else self.current_processing_time())
         self._launch_front(f)
         return f
+
+    def mark_idle(self, idle: bool = True) -> None:
+        """SourceContext.markAsTemporarilyIdle(): exclude this partition from the valve until it
+        is marked active again (or sends data, with an idle timeout)."""
+        self._idle_marked = bool(idle)
+
+    @property
+    def idle(self) -> bool:
+        return self._idle_marked or (self.idle_timeout_steps is not None
+                                     and self._empty_steps >= self.idle_timeout_steps)
 
     def _launch_front(self, f: "_Front") -> None:
         p = f.par
@@ -650,6 +670,8 @@ class KeyedWindowOperator:
                             stats, jhash=self.jhash, late_idx=self.late_idx)
         K.step_finish(stats, self.local_maxts, red, bound=self.ooo_bound, event_mode=event_mode,
                       proc_now=f.proc_now, flags=self.flags)
+        if f.idle:
+            red[2:3].fill_(I64_MAX)  # idle partition: no say in the MIN watermark
         # Watermark valve + pane range + every overflow flag: ONE MIN all-reduce per step.
         self.comm.allreduce_min_(red[:8])
         if cuda:
@@ -692,6 +714,8 @@ class KeyedWindowOperator:
             self._drain()
             self._launch_front(f)
         qmax, qmin, wm_global = -host[0], host[1], host[2]
+        if wm_global == I64_MAX:
+            wm_global = f.old_wm  # every partition idle: the watermark holds
         st = host[8:]
         self.metrics.num_records_in += f.n
         self.metrics.num_late_records_dropped += int(st[K.STAT_LATE])

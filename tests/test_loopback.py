@@ -339,3 +339,55 @@ def test_loopback_error_on_one_rank_propagates():
     with pytest.raises(ValueError, match="boom"):
         run_loopback(3, rank_fn, timeout_s=30)
     assert LoopbackGroup(2).world == 2
+
+
+# ---- idle source partitions (StatusWatermarkValve, SURVEY.md F-valve) --------------------------
+@pytest.mark.parametrize("dev", _devices())
+@pytest.mark.parametrize("exchange", ["records", "partials"])
+def test_idle_partition_does_not_hold_the_watermark(dev, exchange):
+    """Rank 1's source goes quiet after step 1. Without idleness its stale watermark holds the
+    MIN valve back: no window fires until end of input. With idle_timeout_steps=1 the valve
+    takes the MIN over active partitions and the windows fire on time, with the same results
+    as one rank fed every batch."""
+    _skip_no_gpu(dev)
+    per, nkeys, cap_log2 = _sizes(dev)
+    world, quiet_from = 2, 2
+
+    def batch(rank, step):
+        k, t, v = _batch(dev, rank, step, per, nkeys)
+        if rank == 1 and step >= quiet_from:
+            return k[:0], t[:0], v[:0]
+        return k, t, v
+
+    def run(idle_steps):
+        def rank_fn(comm):
+            op = KeyedWindowOperator(size=3000, agg=K.AGG_SUM_I64, device=dev, comm=comm,
+                                     max_keys=nkeys, batch_capacity=per, ooo_bound=500,
+                                     cap_log2=cap_log2, exchange=exchange,
+                                     idle_timeout_steps=idle_steps)
+            during = []
+            for step in range(STEPS):
+                during += op.process(*batch(comm.rank, step))
+            return _collect(during), _collect(op.finish())
+        res = run_loopback(world, rank_fn, device=torch.device(dev))
+        during, total = {}, {}
+        for d, f in res:
+            during.update(d)
+            total.update(d)
+            total.update(f)
+        return during, total
+
+    ref_op = KeyedWindowOperator(size=3000, agg=K.AGG_SUM_I64, device=dev, max_keys=nkeys,
+                                 batch_capacity=per * world, ooo_bound=500, cap_log2=cap_log2)
+    ref_during = []
+    for step in range(STEPS):
+        parts = [batch(r, step) for r in range(world)]
+        ref_during += ref_op.process(*[torch.cat([p[i] for p in parts]) for i in range(3)])
+    ref_total = _collect(ref_during + ref_op.finish())
+    ref_during = _collect(ref_during)
+
+    held_during, held_total = run(None)
+    live_during, live_total = run(1)
+    assert len(ref_during) > len(_collect([])) and live_during == ref_during
+    assert live_total == ref_total == held_total
+    assert len(held_during) < len(ref_during)  # the quiet partition held the valve back
