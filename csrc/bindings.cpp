@@ -112,6 +112,12 @@ AggPlan make_agg(py::dict d) {
   p.p_lo = d["p_lo"].cast<int64_t>();
   p.fired_hi = d["fired_hi"].cast<int64_t>();
   p.combined = d.contains("combined") ? d["combined"].cast<int32_t>() : 0;
+  if (d.contains("dlist") && d["dlist"].cast<intptr_t>()) {
+    p.dlist = reinterpret_cast<uint32_t*>(d["dlist"].cast<intptr_t>());
+    p.dlist_n = reinterpret_cast<uint32_t*>(d["dlist_n"].cast<intptr_t>());
+    p.slot_mark = reinterpret_cast<uint32_t*>(d["slot_mark"].cast<intptr_t>());
+    if (!p.dlist_n || !p.slot_mark) throw std::invalid_argument("dirty list needs dlist_n and slot_mark");
+  }
   p.rec_words = d.contains("rec_words") ? d["rec_words"].cast<int32_t>() : 3;
   if (p.rec_words != 2 && p.rec_words != 3) throw std::invalid_argument("rec_words must be 2 or 3");
   if (p.ring <= 0 || (p.ring & (p.ring - 1))) throw std::invalid_argument("ring must be 2^k");
@@ -133,6 +139,11 @@ FirePlan make_fire(py::dict d) {
   p.wend = d["wend"].cast<double>();
   p.out_cap = d["out_cap"].cast<uint32_t>();
   p.ablate = d.contains("ablate") ? d["ablate"].cast<uint32_t>() : 0u;
+  if (d.contains("list") && d["list"].cast<intptr_t>()) {
+    p.list = reinterpret_cast<const uint32_t*>(d["list"].cast<intptr_t>());
+    p.list_n = reinterpret_cast<const uint32_t*>(d["list_n"].cast<intptr_t>());
+    if (!p.list_n) throw std::invalid_argument("slot list needs list_n");
+  }
   py::tuple m = d["map"].cast<py::tuple>();
   py::tuple f = d["filt"].cast<py::tuple>();
   p.map = make_prog(m[0].cast<std::vector<int32_t>>(), m[1].cast<std::vector<double>>());
@@ -353,6 +364,16 @@ PYBIND11_MODULE(_mxs_native, m) {
                                intptr_t keys_g, intptr_t slots) {
     cpu::table_insert(P<uint64_t>(keys), n, nsub_log2, cap_log2, P<uint64_t>(keys_g),
                       P<int64_t>(slots));
+  });
+  m.def("gpu_dirty_clear", [](intptr_t list, intptr_t list_n, uint32_t cap, int ring,
+                              int64_t nslots, intptr_t dirty_g, intptr_t mark, intptr_t stream) {
+    gpu::dirty_clear(P<uint32_t>(list), P<uint32_t>(list_n), cap, ring, nslots, P<uint8_t>(dirty_g),
+                     P<uint32_t>(mark), stream);
+  });
+  m.def("cpu_dirty_clear", [](intptr_t list, intptr_t list_n, uint32_t cap, int ring,
+                              int64_t nslots, intptr_t dirty_g, intptr_t mark) {
+    cpu::dirty_clear(P<uint32_t>(list), P<uint32_t>(list_n), cap, ring, nslots, P<uint8_t>(dirty_g),
+                     P<uint32_t>(mark));
   });
   m.def("gpu_scatter_partials", [](intptr_t keys, intptr_t acc, intptr_t cnt, intptr_t n_in,
                                    py::dict plan, intptr_t jhash, intptr_t kg_dest,

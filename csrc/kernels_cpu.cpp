@@ -169,7 +169,14 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p, uint6
         const uint64_t v = agg_lift(p.agg, r.val);
         if (p.agg != AGG_COUNT) acc_g[gi] = cnt_g[gi] ? agg_combine(p.agg, acc_g[gi], v) : v;
         cnt_g[gi] += p.combined ? r.aux : 1u;
-        if (pane <= p.fired_hi) dirty_g[gi] = 1;
+        if (pane <= p.fired_hi) {
+          dirty_g[gi] = 1;
+          const size_t slot = ((size_t)sub << p.cap_log2) + s;
+          if (p.dlist && !p.slot_mark[slot]) {
+            p.slot_mark[slot] = 1;
+            p.dlist[(*p.dlist_n)++] = (uint32_t)slot;
+          }
+        }
       }
     }
     if (inserted) {
@@ -185,7 +192,9 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
                  double* out_vals, uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n) {
   const int64_t nslots = p.nslots;
   uint32_t n = *out_n;
-  for (int64_t s = 0; s < nslots; ++s) {
+  const int64_t nvisit = p.list ? (int64_t)*p.list_n : nslots;
+  for (int64_t v = 0; v < nvisit; ++v) {
+    const int64_t s = p.list ? (int64_t)p.list[v] : v;
     bool dirty = !p.only_dirty, have = false;
     uint64_t acc = 0;
     uint32_t cnt = 0;
@@ -403,6 +412,16 @@ void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uin
       m = (n & 1) ? hi : (hi + as_f64(f64_from_order_bits(ord[a + n / 2 - 1]))) / 2.0;
     }
     out[s] = m;
+  }
+}
+
+void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
+                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark) {
+  const uint32_t n = std::min(*list_n, list_cap);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t s = list[i];
+    slot_mark[s] = 0;
+    for (int r = 0; r < ring; ++r) dirty_g[(size_t)r * nslots + s] = 0;
   }
 }
 

@@ -1039,14 +1039,34 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
           if (AGG != AGG_COUNT) oa[w] = acc_g[gi[w]];
         }
       }
+      bool late[kWB];
 #pragma unroll
       for (int w = 0; w < kWB; ++w) {
+        late[w] = false;
         if (!dc[w]) continue;
         const uint32_t i = i0 + (uint32_t)w * blockDim.x;
         const uint64_t d = PK ? (uint64_t)pk_sum(sacc[i]) : lds_export<AGG>(sacc[i]);
         if (AGG != AGG_COUNT) acc_g[gi[w]] = oc[w] ? agg_combine(AGG, oa[w], d) : d;
         cnt_g[gi[w]] = oc[w] + dc[w];
-        if (p.pane_base + q0 + (int64_t)(i >> p.cap_log2) <= p.fired_hi) dirty_g[gi[w]] = 1;
+        if (p.pane_base + q0 + (int64_t)(i >> p.cap_log2) <= p.fired_hi) {
+          dirty_g[gi[w]] = 1;
+          late[w] = true;
+        }
+      }
+      if (p.dlist) {
+        // Touched-slot list: a slot's first late update appends it (one atomic per wave).
+#pragma unroll
+        for (int w = 0; w < kWB; ++w) {
+          const uint32_t i = i0 + (uint32_t)w * blockDim.x;
+          const size_t slot = sbase + (i & mask);
+          const bool app = late[w] && atomicOr(&p.slot_mark[slot], 1u) == 0u;
+          const unsigned long long m = __ballot(app);
+          if (!m) continue;
+          uint32_t wb = 0;
+          if (lane_id() == 0) wb = atomicAdd(p.dlist_n, (uint32_t)__popcll(m));
+          wb = __shfl(wb, 0);
+          if (app) p.dlist[wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = (uint32_t)slot;
+        }
       }
     }
     __syncthreads();
@@ -1210,8 +1230,10 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
   const int64_t nslots = p.nslots;
   const int64_t per_round = (int64_t)kFireThreads * kFireU;
   const bool chain_only = (!p.map.ncode || p.map.chain) && (!p.filt.ncode || p.filt.chain);
+  // Slot-list mode (re-firings): visit only the listed slots.
+  const int64_t nvisit = p.list ? (int64_t)*p.list_n : nslots;
   // Rounds are block-uniform, so every lane reaches the barriers and the ballots.
-  for (int64_t base = (int64_t)blockIdx.x * per_round; base < nslots;
+  for (int64_t base = (int64_t)blockIdx.x * per_round; base < nvisit;
        base += (int64_t)gridDim.x * per_round) {
     bool emit[kFireU];
     uint64_t acc[kFireU], key[kFireU];
@@ -1219,13 +1241,14 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
     double val[kFireU];
 #pragma unroll
     for (int u = 0; u < kFireU; ++u) {
-      const int64_t s = base + (int64_t)u * kFireThreads + threadIdx.x;
+      const int64_t v = base + (int64_t)u * kFireThreads + threadIdx.x;
       emit[u] = false;
       acc[u] = 0;
       key[u] = 0;
       cnt[u] = 0;
       val[u] = 0.0;
-      if (s < nslots) {
+      if (v < nvisit) {
+        const int64_t s = p.list ? (int64_t)p.list[v] : v;
         bool dirty = !p.only_dirty;
         bool have = false;
         for (int j = 0; j < p.npanes; ++j) {
@@ -1316,6 +1339,22 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
 // one global cursor atomic per touched bucket, then the writes. The row count comes from the
 // fire's device counter, so no host round trip sits between the local fire and the exchange.
 // ------------------------------------------------------------------------------------------
+// Reset the touched-slot list after a step's re-firings: every listed slot's dirty bytes (all
+// ring panes) and its mark.
+__global__ __launch_bounds__(256) void dirty_clear_kernel(const uint32_t* __restrict__ list,
+                                                          const uint32_t* __restrict__ list_n,
+                                                          uint32_t list_cap, int ring, int64_t nslots,
+                                                          uint8_t* __restrict__ dirty_g,
+                                                          uint32_t* __restrict__ slot_mark) {
+  uint32_t n = *list_n;
+  n = n < list_cap ? n : list_cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t s = list[i];
+    slot_mark[s] = 0u;
+    for (int r = 0; r < ring; ++r) dirty_g[(size_t)r * nslots + s] = 0;
+  }
+}
+
 constexpr int kScatThreads = 1024;
 constexpr int kScatU = 8;
 
@@ -2670,6 +2709,14 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
                      dim3(kFireThreads), lds,
                      (hipStream_t)stream, keys_g, acc_g, cnt_g, dirty_g, plan, out_keys, out_vals,
                      out_raw, out_cnt, out_n);
+  HIP_CHECK(hipGetLastError());
+}
+
+void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
+                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, intptr_t stream) {
+  if (list_cap == 0) return;
+  hipLaunchKernelGGL(dirty_clear_kernel, dim3(grid_for(list_cap, 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, list, list_n, list_cap, ring, nslots, dirty_g, slot_mark);
   HIP_CHECK(hipGetLastError());
 }
 

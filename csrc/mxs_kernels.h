@@ -27,6 +27,12 @@ struct AggPlan {
   int64_t fired_hi;     // absolute pane id: panes <= fired_hi are in an already-fired window
   int32_t combined;     // records are pre-aggregated (aux = element count, val = exported acc)
   int32_t rec_words;    // 3: Rec (24 B); 2: RecC (16 B)
+  // Touched-slot list of late-but-allowed data (optional, all three or none): the first time a
+  // slot receives data for an already-fired pane it is marked and appended, so re-firings visit
+  // only those slots instead of sweeping the table.
+  uint32_t* dlist;      // [nslots] slot ids
+  uint32_t* dlist_n;    // list length
+  uint32_t* slot_mark;  // [nslots] 1 = listed
 };
 
 // Plan of one window firing.
@@ -42,6 +48,8 @@ struct FirePlan {
   uint32_t ablate;      // profiling-only ablation bits (0 in production): 1 = skip the epilogue VM
   ExprProg map;         // value epilogue (empty = identity)
   ExprProg filt;        // predicate on the mapped value (empty = true)
+  const uint32_t* list;    // optional: visit only these slots (touched-slot list) ...
+  const uint32_t* list_n;  // ... of this length (device counter)
 };
 
 // Local-global window aggregation (G > 1): where the rows of a locally fired window go.
@@ -158,6 +166,8 @@ void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t*
                       const uint32_t* n_in, const ScatPlan& plan, const int32_t* jhash,
                       const int32_t* kg_dest, uint32_t* cursor, Rec* out, uint32_t* flags,
                       intptr_t stream);
+void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
+                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, intptr_t stream);
 }  // namespace gpu
 
 // ---- CPU twins (kernels_cpu.cpp) ------------------------------------------------------------
@@ -198,6 +208,8 @@ void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uin
 void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt,
                       const uint32_t* n_in, const ScatPlan& plan, const int32_t* jhash,
                       const int32_t* kg_dest, uint32_t* cursor, Rec* out, uint32_t* flags);
+void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
+                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark);
 }  // namespace cpu
 
 }  // namespace mxs

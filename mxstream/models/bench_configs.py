@@ -158,6 +158,11 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
             lat.append((time.perf_counter() - t_in) * 1e3)
         return sum(len(r.keys) for r in fired)
 
+    # Steady state: the first windows (started before the stream) hold a partial minute of
+    # data and nearly every key of them is below the alert threshold -- an artefact of the
+    # stream start, not the workload. The untimed warmup covers the first full window (60 s of
+    # event time = 30 steps) and the onset of late data (step 21).
+    warmup = max(warmup, 32)
     for _ in range(warmup):
         step()
     _sync(dev)
@@ -168,7 +173,7 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
         alerts += step()
     _sync(dev)
     dt = time.perf_counter() - t0
-    return {"config": 4, "metric": "events/sec (sliding 1min/10s + lateness, 10M keys)",
+    return {"config": 4, "warmup": warmup, "metric": "events/sec (sliding 1min/10s + lateness, 10M keys)",
             "value": batch * steps / dt, "unit": "events/s", "ms_per_step": dt / steps * 1e3,
             "p50_alert_latency_ms": statistics.median(lat) if lat else None, "alerts": alerts,
             "late_dropped": op.metrics.num_late_records_dropped, "keys": keys,

@@ -163,6 +163,9 @@ class AggPlan:
     fired_hi: int
     combined: int = 0    # records are pre-aggregated by window_combine (aux = element count)
     rec_words: int = 3   # layout of the input records (3: Rec, 2: RecC)
+    dlist: int = 0       # touched-slot list (data pointers, 0 = off): slot ids ...
+    dlist_n: int = 0     # ... its length ...
+    slot_mark: int = 0   # ... and the per-slot listed marks
 
     def as_dict(self) -> dict:
         return dict(self.__dict__)
@@ -213,7 +216,9 @@ def window_agg(recs, counts, plan: AggPlan, keys_g, acc_g, cnt_g, dirty_g, occ, 
 def window_fire(keys_g, acc_g, cnt_g, dirty_g, *, agg: int, npanes: int, ring: int, p0: int,
                 wstart: int, wend: int, only_dirty: bool, map_prog: _expr.Program,
                 filt_prog: _expr.Program, out_keys, out_vals, out_raw, out_cnt, out_n,
-                ablate: int = 0) -> None:
+                ablate: int = 0, slot_list=None, slot_list_n=None) -> None:
+    """slot_list/slot_list_n (int32 device tensors): visit only the listed slots (re-firings of
+    late-but-allowed data) instead of sweeping the table."""
     dev = keys_g.device
     nslots = keys_g.numel()
     cap = out_keys.numel()
@@ -229,6 +234,10 @@ def window_fire(keys_g, acc_g, cnt_g, dirty_g, *, agg: int, npanes: int, ring: i
     plan = dict(agg=agg, npanes=npanes, ring=ring, only_dirty=int(only_dirty), nslots=nslots,
                 p0=p0, wstart=float(wstart), wend=float(wend), out_cap=cap,
                 map=tuple(map_prog.as_args()), filt=tuple(filt_prog.as_args()), ablate=ablate)
+    if slot_list is not None:
+        _check(slot_list, torch.int32, 0, "slot_list", dev)
+        _check(slot_list_n, torch.int32, 1, "slot_list_n", dev)
+        plan.update(list=_p(slot_list), list_n=_p(slot_list_n))
     m = load()
     args = (_p(keys_g), _p(acc_g), _p(cnt_g), _p(dirty_g), plan, _p(out_keys), _p(out_vals),
             _p(out_raw), _p(out_cnt), _p(out_n))
@@ -270,6 +279,23 @@ def scatter_partials(keys, acc, cnt, n_dev, *, n_cap: int, max_parallelism: int,
         m.gpu_scatter_partials(*args, _stream(keys))
     else:
         m.cpu_scatter_partials(*args)
+
+
+def dirty_clear(slot_list, slot_list_n, *, ring: int, nslots: int, dirty_g, slot_mark) -> None:
+    """Reset the touched-slot list's dirty bytes (every ring pane) and marks; the caller zeroes
+    the list length afterwards."""
+    dev = dirty_g.device
+    _check(slot_list, torch.int32, 0, "slot_list", dev)
+    _check(slot_list_n, torch.int32, 1, "slot_list_n", dev)
+    _check(dirty_g, torch.uint8, ring * nslots, "dirty_g", dev)
+    _check(slot_mark, torch.int32, nslots, "slot_mark", dev)
+    m = load()
+    args = (_p(slot_list), _p(slot_list_n), slot_list.numel(), ring, nslots, _p(dirty_g),
+            _p(slot_mark))
+    if _is_gpu(dirty_g):
+        m.gpu_dirty_clear(*args, _stream(dirty_g))
+    else:
+        m.cpu_dirty_clear(*args)
 
 
 def rolling(recs, counts, *, cap_log2: int, nsub: int, agg: int, nsrc: int, bucket_cap: int,

@@ -69,6 +69,7 @@ class VectorWindowOperator(KeyedWindowOperator):
         return super().process(keys, ts, self._rows[:n])
 
     _local_global_ok = False  # vector panes are exchanged per step (records mode)
+    _use_dlist = False        # its own fire kernel sweeps the table
 
     # ---- hooks -----------------------------------------------------------------------------
     def _rec_words(self) -> int:

@@ -359,6 +359,13 @@ class KeyedWindowOperator:
             self._pool.take(self.nslots * 28 + 4 * 256)
         self.late_idx = (torch.empty(late_capacity, dtype=torch.int32, device=dev)
                          if side_output_late else None)
+        # Touched-slot list (allowed lateness): window_agg appends every slot that receives
+        # late-but-allowed data, re-firings visit only those slots (not the whole table).
+        self.dlist = self.dlist_n = self.slot_mark = None
+        if self.lateness > 0 and self._use_dlist:
+            self.dlist = torch.empty(self.nslots, dtype=torch.int32, device=dev)
+            self.dlist_n = torch.zeros(1, dtype=torch.int32, device=dev)
+            self.slot_mark = torch.zeros(self.nslots, dtype=torch.int32, device=dev)
         if self.local_global:
             self._init_owner_tables(max_keys, cap_log2)
         self.comb_send = self.comb_recv = None
@@ -383,6 +390,7 @@ class KeyedWindowOperator:
         self.late_side: list[np.ndarray] = []
 
     _local_global_ok = True  # subclasses whose fire is not a plain reduce opt out
+    _use_dlist = True        # subclasses with their own fire kernel opt out of slot lists
 
     def _init_owner_tables(self, max_keys: int, cap_log2: int | None) -> None:
         """Local-global mode: the owner side of a fire -- the merge table of this rank's key
@@ -784,6 +792,9 @@ class KeyedWindowOperator:
                                   np_step=b.np_step, pg=b.pg, pane_base=b.pane_base,
                                   p_lo=b.qmin, fired_hi=b.fired_hi, combined=combined,
                                   rec_words=3 if combined else (2 if b.compact else 3))
+                if self.dlist is not None:
+                    aplan.dlist, aplan.dlist_n = self.dlist.data_ptr(), self.dlist_n.data_ptr()
+                    aplan.slot_mark = self.slot_mark.data_ptr()
                 with self._stage("window_agg"):
                     self._aggregate(recs, counts, aplan)
                 if cuda and not self._exchanging:
@@ -870,7 +881,9 @@ class KeyedWindowOperator:
                       npanes=p1 - p0 + 1, ring=self.ring, p0=p0, wstart=s,
                       wend=s + self.size, only_dirty=only_dirty, map_prog=self.map_prog,
                       filt_prog=self.filter_prog, out_keys=self.out_keys, out_vals=self.out_vals,
-                      out_raw=self.out_raw, out_cnt=self.out_cnt, out_n=self.out_n)
+                      out_raw=self.out_raw, out_cnt=self.out_cnt, out_n=self.out_n,
+                      slot_list=self.dlist if only_dirty else None,
+                      slot_list_n=self.dlist_n if only_dirty else None)
         n = self._fired_count()
         self.metrics.num_fires += 1
         if n == 0:
@@ -984,9 +997,14 @@ class KeyedWindowOperator:
                 if r is not None:
                     out.append(r)
             s += self.slide
-        for p in range(pmin, pmax + 1):
-            so = (p & (self.ring - 1)) * self.nslots
-            self.dirty_g[so:so + self.nslots].zero_()
+        if self.dlist is not None:
+            K.dirty_clear(self.dlist, self.dlist_n, ring=self.ring, nslots=self.nslots,
+                          dirty_g=self.dirty_g, slot_mark=self.slot_mark)
+            self.dlist_n.zero_()
+        else:
+            for p in range(pmin, pmax + 1):
+                so = (p & (self.ring - 1)) * self.nslots
+                self.dirty_g[so:so + self.nslots].zero_()
         return out
 
     def _purge(self, wm: int) -> None:
@@ -1099,6 +1117,9 @@ class KeyedWindowOperator:
             self.cnt_g = torch.zeros(self.ring * self.nslots, dtype=torch.int32, device=dev)
             self.dirty_g = torch.zeros(self.ring * self.nslots, dtype=torch.uint8, device=dev)
         self.keys_g.fill_(-1)
+        if self.dlist is not None:
+            self.dlist_n.zero_()
+            self.slot_mark.zero_()
         self.acc_g.zero_()
         self.cnt_g.zero_()
         self.dirty_g.zero_()
@@ -1128,5 +1149,12 @@ class KeyedWindowOperator:
                 0, inv, cnt)
             self.dirty_g[u] = torch.zeros(u.numel(), dtype=torch.int32, device=dev).scatter_reduce_(
                 0, inv, dirty.to(torch.int32), "amax").to(torch.uint8)
+        if self.dlist is not None:
+            # Rebuild the touched-slot list from the restored dirty bytes.
+            self.slot_mark.zero_()
+            ds = torch.unique(slot[dirty != 0]).to(torch.int32)
+            self.dlist[:ds.numel()] = ds
+            self.dlist_n.fill_(ds.numel())
+            self.slot_mark[ds.long()] = 1
         self.occ.copy_(torch.bincount(slots_u >> self.cap_log2, minlength=self.nsub)
                        .to(torch.int32))

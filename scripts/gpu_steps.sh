@@ -1,0 +1,36 @@
+#!/bin/bash
+# One gpurun call = a list of named steps, each under its own time limit; output under
+# gpurun_out/<tag>/. Stops at the first failing step (never retries a GPU step).
+#   gpurun -- 'bash scripts/gpu_steps.sh r2x tests bench cfg4 prof_cfg4'
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+tag=$1; shift
+out=gpurun_out/$tag
+mkdir -p "$out"
+export PYTHONPATH=$PWD
+test -f mxstream/_mxs_native*.so || { echo "native module missing"; exit 3; }
+prof() {  # prof <name> <cmd...>: rocprofv3 kernel trace + stats of one python command
+  local name=$1; shift
+  (cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" &&
+   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/prof_$name" -o "$name" -- "$@" \
+     > "$out/prof_$name.log" 2>&1)
+}
+for step in "$@"; do
+  echo "== $step"
+  case $step in
+    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$out/pytest_gpu.log" 2>&1
+           st=$?; tail -3 "$out/pytest_gpu.log"; [ $st -eq 0 ] || [ $st -eq 1 ] || exit $st ;;
+    smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 || exit $? ;;
+    bench) timeout -k 10 300 python bench.py --steps 48 --warmup 8 > "$out/bench.log" 2>&1 || exit $? ;;
+    bench20) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "$out/bench20.log" 2>&1 || exit $? ;;
+    cfg1) timeout -k 10 300 python -m mxstream.models.bench_configs --config 1 --steps 20 --warmup 3 > "$out/cfg1.json" 2>&1 || exit $? ;;
+    cfg1gpu) timeout -k 10 300 python -m mxstream.models.bench_configs --config 1 --gpu-parse --steps 20 --warmup 3 > "$out/cfg1_gpu.json" 2>&1 || exit $? ;;
+    cfg2|cfg4|cfg5|cfg6) timeout -k 10 300 python -m mxstream.models.bench_configs --config ${step#cfg} --steps 20 --warmup 5 > "$out/$step.json" 2>&1 || exit $? ;;
+    loop8) timeout -k 10 300 python scripts/loopback_bench.py --world 8 --steps 24 --warmup 4 --out "$out/loop8.json" > "$out/loop8.log" 2>&1 || exit $? ;;
+    prof_bench) prof bench python3 bench.py --steps 24 --warmup 6 || exit $? ;;
+    prof_cfg2|prof_cfg4|prof_cfg5|prof_cfg6) c=${step#prof_cfg}; prof cfg$c python3 -m mxstream.models.bench_configs --config $c --steps 12 --warmup 4 || exit $? ;;
+    prof_loop8) prof loop8 python3 scripts/loopback_bench.py --world 8 --steps 24 --warmup 4 || exit $? ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "all steps done"
