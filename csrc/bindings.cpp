@@ -366,14 +366,15 @@ PYBIND11_MODULE(_mxs_native, m) {
                       P<int64_t>(slots));
   });
   m.def("gpu_dirty_clear", [](intptr_t list, intptr_t list_n, uint32_t cap, int ring,
-                              int64_t nslots, intptr_t dirty_g, intptr_t mark, intptr_t stream) {
+                              int64_t nslots, intptr_t dirty_g, intptr_t mark, int64_t p_lo, int np,
+                              intptr_t stream) {
     gpu::dirty_clear(P<uint32_t>(list), P<uint32_t>(list_n), cap, ring, nslots, P<uint8_t>(dirty_g),
-                     P<uint32_t>(mark), stream);
+                     P<uint32_t>(mark), p_lo, np, stream);
   });
   m.def("cpu_dirty_clear", [](intptr_t list, intptr_t list_n, uint32_t cap, int ring,
-                              int64_t nslots, intptr_t dirty_g, intptr_t mark) {
+                              int64_t nslots, intptr_t dirty_g, intptr_t mark, int64_t p_lo, int np) {
     cpu::dirty_clear(P<uint32_t>(list), P<uint32_t>(list_n), cap, ring, nslots, P<uint8_t>(dirty_g),
-                     P<uint32_t>(mark));
+                     P<uint32_t>(mark), p_lo, np);
   });
   m.def("gpu_scatter_partials", [](intptr_t keys, intptr_t acc, intptr_t cnt, intptr_t n_in,
                                    py::dict plan, intptr_t jhash, intptr_t kg_dest,

@@ -416,12 +416,13 @@ void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uin
 }
 
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
-                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark) {
+                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np) {
   const uint32_t n = std::min(*list_n, list_cap);
+  np = std::min(np, ring);
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t s = list[i];
     slot_mark[s] = 0;
-    for (int r = 0; r < ring; ++r) dirty_g[(size_t)r * nslots + s] = 0;
+    for (int j = 0; j < np; ++j) dirty_g[(size_t)((p_lo + j) & (ring - 1)) * nslots + s] = 0;
   }
 }
 

@@ -963,6 +963,17 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
   const size_t nslots = (size_t)p.nsub << p.cap_log2;
   for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) skeys[i] = keys_g[sbase + i];
   if (threadIdx.x < 4) sflag[threadIdx.x] = 0;
+  // Touched-slot list (late-but-allowed data): an LDS bitmap dedupes the sub-table's slots
+  // across pane passes and an LDS buffer collects them; one global atomic per workgroup at the
+  // end reserves the run in the list (a per-wave atomic on one global counter and a returning
+  // global atomic per late row made the late steps of config 4 4.7x slower).
+  uint32_t* sdl_hdr = (uint32_t*)(sflag + 4);  // [0] listed slots, [1] list base
+  uint32_t* sbit = sdl_hdr + 4;                // [cap / 32] listed bits
+  uint32_t* sdl = sbit + (cap >> 5);           // [cap] listed slot offsets
+  if (p.dlist) {
+    if (threadIdx.x < 4) sdl_hdr[threadIdx.x] = 0;
+    for (uint32_t i = threadIdx.x; i < (cap >> 5); i += blockDim.x) sbit[i] = 0;
+  }
 
   int inserted = 0;
   bool ovf = false;
@@ -1054,18 +1065,12 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
         }
       }
       if (p.dlist) {
-        // Touched-slot list: a slot's first late update appends it (one atomic per wave).
 #pragma unroll
         for (int w = 0; w < kWB; ++w) {
-          const uint32_t i = i0 + (uint32_t)w * blockDim.x;
-          const size_t slot = sbase + (i & mask);
-          const bool app = late[w] && atomicOr(&p.slot_mark[slot], 1u) == 0u;
-          const unsigned long long m = __ballot(app);
-          if (!m) continue;
-          uint32_t wb = 0;
-          if (lane_id() == 0) wb = atomicAdd(p.dlist_n, (uint32_t)__popcll(m));
-          wb = __shfl(wb, 0);
-          if (app) p.dlist[wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = (uint32_t)slot;
+          if (!late[w]) continue;
+          const uint32_t s = (i0 + (uint32_t)w * blockDim.x) & mask;
+          const uint32_t bit = 1u << (s & 31u);
+          if (!(atomicOr(&sbit[s >> 5], bit) & bit)) sdl[atomicAdd(&sdl_hdr[0], 1u)] = s;
         }
       }
     }
@@ -1074,6 +1079,12 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
   if (inserted) sflag[0] = 1;
   if (ovf) sflag[1] = 1;
   __syncthreads();
+  if (p.dlist && sdl_hdr[0]) {
+    if (threadIdx.x == 0) sdl_hdr[1] = atomicAdd(p.dlist_n, sdl_hdr[0]);
+    __syncthreads();
+    const uint32_t nl = sdl_hdr[0], base = sdl_hdr[1];
+    for (uint32_t j = threadIdx.x; j < nl; j += blockDim.x) p.dlist[base + j] = (uint32_t)(sbase + sdl[j]);
+  }
   if (sflag[0]) {
     for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
       const uint64_t k = skeys[i];
@@ -1345,13 +1356,14 @@ __global__ __launch_bounds__(256) void dirty_clear_kernel(const uint32_t* __rest
                                                           const uint32_t* __restrict__ list_n,
                                                           uint32_t list_cap, int ring, int64_t nslots,
                                                           uint8_t* __restrict__ dirty_g,
-                                                          uint32_t* __restrict__ slot_mark) {
+                                                          uint32_t* __restrict__ slot_mark,
+                                                          int64_t p_lo, int np) {
   uint32_t n = *list_n;
   n = n < list_cap ? n : list_cap;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t s = list[i];
     slot_mark[s] = 0u;
-    for (int r = 0; r < ring; ++r) dirty_g[(size_t)r * nslots + s] = 0;
+    for (int j = 0; j < np; ++j) dirty_g[(size_t)((p_lo + j) & (ring - 1)) * nslots + s] = 0;
   }
 }
 
@@ -2676,7 +2688,8 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& plan, ui
                 uint32_t* flags, intptr_t stream) {
   if (plan.np_step <= 0 || plan.nsub <= 0) return;
   const size_t cap = (size_t)1 << plan.cap_log2;
-  const size_t lds = cap * 8 + (size_t)plan.pg * cap * 12 + 16;
+  const size_t lds = cap * 8 + (size_t)plan.pg * cap * 12 + 16 +
+                     (plan.dlist ? 16 + cap / 8 + cap * 4 : 0);  // touched-slot bitmap + buffer
   if (lds > 160 * 1024) throw std::runtime_error("window_agg: LDS image exceeds 160 KiB");
   if (plan.rec_words == 2 && plan.combined)
     throw std::invalid_argument("window_agg: combined records are 24-byte records");
@@ -2713,10 +2726,13 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
 }
 
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
-                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, intptr_t stream) {
+                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np,
+                 intptr_t stream) {
   if (list_cap == 0) return;
+  np = np < ring ? np : ring;
   hipLaunchKernelGGL(dirty_clear_kernel, dim3(grid_for(list_cap, 256, 4096)), dim3(256), 0,
-                     (hipStream_t)stream, list, list_n, list_cap, ring, nslots, dirty_g, slot_mark);
+                     (hipStream_t)stream, list, list_n, list_cap, ring, nslots, dirty_g, slot_mark,
+                     p_lo, np);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -167,7 +167,8 @@ void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t*
                       const int32_t* kg_dest, uint32_t* cursor, Rec* out, uint32_t* flags,
                       intptr_t stream);
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
-                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, intptr_t stream);
+                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np,
+                 intptr_t stream);
 }  // namespace gpu
 
 // ---- CPU twins (kernels_cpu.cpp) ------------------------------------------------------------
@@ -209,7 +210,7 @@ void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t*
                       const uint32_t* n_in, const ScatPlan& plan, const int32_t* jhash,
                       const int32_t* kg_dest, uint32_t* cursor, Rec* out, uint32_t* flags);
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
-                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark);
+                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np);
 }  // namespace cpu
 
 }  // namespace mxs

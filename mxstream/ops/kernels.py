@@ -281,17 +281,19 @@ def scatter_partials(keys, acc, cnt, n_dev, *, n_cap: int, max_parallelism: int,
         m.cpu_scatter_partials(*args)
 
 
-def dirty_clear(slot_list, slot_list_n, *, ring: int, nslots: int, dirty_g, slot_mark) -> None:
-    """Reset the touched-slot list's dirty bytes (every ring pane) and marks; the caller zeroes
-    the list length afterwards."""
+def dirty_clear(slot_list, slot_list_n, *, ring: int, nslots: int, dirty_g, slot_mark,
+                p_lo: int = 0, np_: int | None = None) -> None:
+    """Reset the touched-slot list's dirty bytes (panes p_lo .. p_lo + np_ - 1; default every
+    ring pane) and marks; the caller zeroes the list length afterwards."""
     dev = dirty_g.device
     _check(slot_list, torch.int32, 0, "slot_list", dev)
     _check(slot_list_n, torch.int32, 1, "slot_list_n", dev)
     _check(dirty_g, torch.uint8, ring * nslots, "dirty_g", dev)
     _check(slot_mark, torch.int32, nslots, "slot_mark", dev)
     m = load()
+    np_ = ring if np_ is None else max(0, min(int(np_), ring))
     args = (_p(slot_list), _p(slot_list_n), slot_list.numel(), ring, nslots, _p(dirty_g),
-            _p(slot_mark))
+            _p(slot_mark), int(p_lo), np_)
     if _is_gpu(dirty_g):
         m.gpu_dirty_clear(*args, _stream(dirty_g))
     else:

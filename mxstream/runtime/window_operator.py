@@ -749,7 +749,8 @@ class KeyedWindowOperator:
             self.next_fire_start = cand if self.next_fire_start is None else min(self.next_fire_start, cand)
             b.fired_hi = self._fired_hi()
             cap = 1 << self.cap_log2
-            lds_budget = 150 * 1024 - cap * 8
+            lds_budget = 150 * 1024 - cap * 8 - (cap * 4 + cap // 8 + 16
+                                                 if self.dlist is not None else 0)
             b.has_data = True
             b.qmin, b.np_step = qmin, gmax - gmin + 1
             b.pg = max(1, min(b.np_step, lds_budget // (cap * 12)))
@@ -999,7 +1000,8 @@ class KeyedWindowOperator:
             s += self.slide
         if self.dlist is not None:
             K.dirty_clear(self.dlist, self.dlist_n, ring=self.ring, nslots=self.nslots,
-                          dirty_g=self.dirty_g, slot_mark=self.slot_mark)
+                          dirty_g=self.dirty_g, slot_mark=self.slot_mark, p_lo=pmin,
+                          np_=pmax - pmin + 1)
             self.dlist_n.zero_()
         else:
             for p in range(pmin, pmax + 1):
