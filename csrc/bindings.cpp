@@ -201,6 +201,8 @@ PYBIND11_MODULE(_mxs_native, m) {
 
   // ---- GPU ----
   m.def("gpu_device_count", &gpu::device_count);
+  m.def("cpu_set_threads", &cpu::set_threads);
+  m.def("cpu_get_threads", &cpu::get_threads);
   m.def("gpu_set_spin_schedule", &gpu::set_spin_schedule);
   m.def("gpu_gen_events", [](intptr_t keys, intptr_t ts, intptr_t vals, int64_t n, uint64_t seed,
                              uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,

@@ -4,8 +4,11 @@
 // (BASELINE config 1 runs here) and the reference the GPU kernels are tested against. Events are
 // processed in arrival order, so float accumulations match Flink's per-record order exactly.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <stdexcept>
+#include <thread>
+#include <vector>
 
 #include "mxs_kernels.h"
 
@@ -316,11 +319,31 @@ void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, u
   *out_n = n;
 }
 
-void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep) {
-  for (int64_t i = 0; i < n; ++i) {
-    double vars[kExprVars] = {x[i], 0, 0, 0, 0, 0, 0, 0};
-    keep[i] = expr_eval(prog, vars) != 0.0;
+// Worker threads of the CPU twins' embarrassingly parallel loops (set_threads; 1 = serial).
+static std::atomic<int> g_threads{1};
+void set_threads(int n) { g_threads = std::max(1, std::min(n, 256)); }
+int get_threads() { return g_threads; }
+
+template <class F>
+static void parallel_for(int64_t n, int64_t min_per_thread, F&& body) {
+  const int64_t t = std::min<int64_t>(g_threads, std::max<int64_t>(1, n / min_per_thread));
+  if (t <= 1) {
+    body(0, n);
+    return;
   }
+  std::vector<std::thread> th;
+  for (int64_t k = 0; k < t; ++k)
+    th.emplace_back([&, k] { body(n * k / t, n * (k + 1) / t); });
+  for (auto& x : th) x.join();
+}
+
+void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep) {
+  parallel_for(n, 1 << 16, [&](int64_t a, int64_t b) {
+    for (int64_t i = a; i < b; ++i) {
+      double vars[kExprVars] = {x[i], 0, 0, 0, 0, 0, 0, 0};
+      keep[i] = expr_eval(prog, vars) != 0.0;
+    }
+  });
 }
 
 void keygroups(const uint64_t* keys, int64_t n, int hash_mode, const int32_t* jhash, int max_par,

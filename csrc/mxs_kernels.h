@@ -173,6 +173,8 @@ void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap
 
 // ---- CPU twins (kernels_cpu.cpp) ------------------------------------------------------------
 namespace cpu {
+void set_threads(int n);  // worker threads of the parallel CPU twins (expr_filter, ...)
+int get_threads();
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,

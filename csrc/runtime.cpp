@@ -232,6 +232,41 @@ double java_parse_double(std::string_view raw) {
     }
     if (j != body.size()) throw ParseError("NumberFormatException: For input string: \"" + std::string(raw) + "\"");
   }
+  if (!hex) {
+    // Clinger's fast path: a decimal with <= 15 significant digits and no exponent is an exact
+    // integer mantissa over an exact power of ten (<= 10^22); one IEEE division of two exact
+    // values is correctly rounded, i.e. identical to strtod / Double.parseDouble.
+    static const double kPow10[] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,
+                                    1e8,  1e9,  1e10, 1e11, 1e12, 1e13, 1e14, 1e15,
+                                    1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+    uint64_t mant = 0;
+    int nd = 0, frac = -1;
+    bool simple = true;
+    for (size_t j = 0; j < body.size(); ++j) {
+      const char c = body[j];
+      if (c >= '0' && c <= '9') {
+        if (mant == 0 && c == '0') {  // leading zeros are not significant
+          if (frac >= 0) ++frac;
+          continue;
+        }
+        if (++nd > 15) {
+          simple = false;
+          break;
+        }
+        mant = mant * 10 + (uint64_t)(c - '0');
+        if (frac >= 0) ++frac;
+      } else if (c == '.' && frac < 0) {
+        frac = 0;
+      } else {
+        simple = false;  // exponent: the general path
+        break;
+      }
+    }
+    if (simple && (frac < 0 ? 0 : frac) <= 22) {
+      const double v = (double)mant / kPow10[frac < 0 ? 0 : frac];
+      return neg ? -v : v;
+    }
+  }
   std::string tmp(body);
   errno = 0;
   char* end = nullptr;
@@ -266,33 +301,112 @@ enum FieldKind : int {
   FK_RAW_LONG = 6,   // epoch-ms integer field
 };
 
+// Parse one line's fields into row `li` of the columns. String fields get a thread-local id
+// (remapped to the dictionary's ids afterwards). Throws ParseError.
+struct LocalDict {
+  std::unordered_map<std::string_view, uint32_t> ids;
+  std::vector<std::string_view> strs;
+  uint32_t intern(std::string_view v) {
+    auto it = ids.find(v);
+    if (it != ids.end()) return it->second;
+    const uint32_t id = (uint32_t)strs.size();
+    strs.push_back(v);
+    ids.emplace(v, id);
+    return id;
+  }
+};
+
+static void parse_line_into(std::string_view line, char sep,
+                            const std::vector<std::pair<int, int>>& spec,
+                            const std::vector<void*>& ptrs, size_t li, int64_t offset_s,
+                            std::vector<std::string_view>& parts, LocalDict& ld) {
+  java_split(line, sep, parts);
+  for (size_t c = 0; c < spec.size(); ++c) {
+    const int fi = spec[c].first;
+    if (fi < 0 || (size_t)fi >= parts.size())
+      throw ParseError("ArrayIndexOutOfBoundsException: " + std::to_string(fi));
+    std::string_view v = parts[fi];
+    switch (spec[c].second) {
+      case FK_STR: ((uint64_t*)ptrs[c])[li] = ld.intern(v); break;
+      case FK_DOUBLE: ((double*)ptrs[c])[li] = java_parse_double(v); break;
+      case FK_LONG: ((int64_t*)ptrs[c])[li] = java_parse_long(v, INT64_MIN, INT64_MAX, "long"); break;
+      case FK_INT: ((int64_t*)ptrs[c])[li] = java_parse_long(v, INT32_MIN, INT32_MAX, "int"); break;
+      case FK_RAW_LONG: ((int64_t*)ptrs[c])[li] = java_parse_long(v, INT64_MIN, INT64_MAX, "long"); break;
+      case FK_TS_INTSEC: {
+        int64_t es, ms;
+        parse_iso_local_datetime(v, offset_s, &es, &ms);
+        ((int64_t*)ptrs[c])[li] = (int64_t)(int32_t)(uint32_t)(uint64_t)es * 1000LL;
+        break;
+      }
+      case FK_TS_MS: {
+        int64_t es, ms;
+        parse_iso_local_datetime(v, offset_s, &es, &ms);
+        ((int64_t*)ptrs[c])[li] = es * 1000LL + ms;
+        break;
+      }
+      default: throw ParseError("unknown field kind");
+    }
+  }
+}
+
+// Lines of [a, b) of `all` (a starts a line): '\n'-separated, trailing '\r' stripped, a trailing
+// newline does not start a line.
+static void find_lines(std::string_view all, size_t a, size_t b, std::vector<std::string_view>& out) {
+  size_t start = a;
+  for (size_t i = a; i < b; ++i) {
+    if (all[i] == '\n') {
+      std::string_view l = all.substr(start, i - start);
+      if (!l.empty() && l.back() == '\r') l.remove_suffix(1);
+      out.push_back(l);
+      start = i + 1;
+    }
+  }
+  if (start < b) {
+    std::string_view l = all.substr(start, b - start);
+    if (!l.empty() && l.back() == '\r') l.remove_suffix(1);
+    out.push_back(l);
+  }
+}
+
 // Parse newline-separated lines. Returns (columns, nparsed, error_index, error_message).
+//
+// threads > 1: the byte buffer is cut into `threads` newline-aligned chunks; each thread finds
+// its lines and parses them into its row range, interning string fields into a thread-local
+// dictionary. The local dictionaries are then merged into `dict` in chunk order (first
+// appearance order over the whole batch) and the string columns remapped -- ids, like every
+// column, are identical to the single-threaded parse. An error stops at the lowest failing
+// line (nparsed = its index); rows after it are not part of the result.
 py::tuple parse_lines(py::bytes data, std::vector<std::pair<int, int>> spec, std::string sep,
-                      StringDict& dict, int64_t offset_s) {
+                      StringDict& dict, int64_t offset_s, int threads) {
   if (sep.size() != 1) throw std::invalid_argument("separator must be one character");
   char* buf;
   py::ssize_t len;
   if (PYBIND11_BYTES_AS_STRING_AND_SIZE(data.ptr(), &buf, &len)) throw py::error_already_set();
   std::string_view all(buf, (size_t)len);
-  // Count lines (a trailing newline does not start a new line).
-  std::vector<std::string_view> lines;
+  const int T = std::max(1, std::min(threads, 64));
+  // Newline-aligned chunk bounds.
+  std::vector<size_t> cut(T + 1, all.size());
+  cut[0] = 0;
+  for (int t = 1; t < T; ++t) {
+    size_t c = std::max(cut[t - 1], all.size() * (size_t)t / (size_t)T);
+    while (c < all.size() && c > 0 && all[c - 1] != '\n') ++c;
+    cut[t] = c;
+  }
+  std::vector<std::vector<std::string_view>> lines(T);
   {
-    size_t start = 0;
-    for (size_t i = 0; i < all.size(); ++i) {
-      if (all[i] == '\n') {
-        std::string_view l = all.substr(start, i - start);
-        if (!l.empty() && l.back() == '\r') l.remove_suffix(1);
-        lines.push_back(l);
-        start = i + 1;
-      }
-    }
-    if (start < all.size()) {
-      std::string_view l = all.substr(start);
-      if (!l.empty() && l.back() == '\r') l.remove_suffix(1);
-      lines.push_back(l);
+    py::gil_scoped_release nogil;
+    if (T == 1) {
+      find_lines(all, 0, all.size(), lines[0]);
+    } else {
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] { find_lines(all, cut[t], cut[t + 1], lines[t]); });
+      for (auto& x : th) x.join();
     }
   }
-  const size_t n = lines.size();
+  std::vector<size_t> row0(T + 1, 0);
+  for (int t = 0; t < T; ++t) row0[t + 1] = row0[t] + lines[t].size();
+  const size_t n = row0[T];
   std::vector<py::array> cols;
   std::vector<void*> ptrs;
   for (auto& f : spec) {
@@ -305,53 +419,81 @@ py::tuple parse_lines(py::bytes data, std::vector<std::pair<int, int>> spec, std
     }
     ptrs.push_back(cols.back().mutable_data());
   }
+  std::vector<LocalDict> ld(T);
+  std::vector<int64_t> terr(T, -1);
+  std::vector<std::string> tmsg(T);
   int64_t err_idx = -1;
   std::string err_msg;
-  size_t done = 0;
   {
     py::gil_scoped_release nogil;
-    std::lock_guard<std::mutex> g(dict.mu());
-    std::vector<std::string_view> parts;
-    for (size_t li = 0; li < n; ++li) {
-      try {
-        java_split(lines[li], sep[0], parts);
-        for (size_t c = 0; c < spec.size(); ++c) {
-          const int fi = spec[c].first;
-          if (fi < 0 || (size_t)fi >= parts.size())
-            throw ParseError("ArrayIndexOutOfBoundsException: " + std::to_string(fi));
-          std::string_view v = parts[fi];
-          switch (spec[c].second) {
-            case FK_STR: ((uint64_t*)ptrs[c])[li] = dict.intern_locked(v); break;
-            case FK_DOUBLE: ((double*)ptrs[c])[li] = java_parse_double(v); break;
-            case FK_LONG: ((int64_t*)ptrs[c])[li] = java_parse_long(v, INT64_MIN, INT64_MAX, "long"); break;
-            case FK_INT: ((int64_t*)ptrs[c])[li] = java_parse_long(v, INT32_MIN, INT32_MAX, "int"); break;
-            case FK_RAW_LONG: ((int64_t*)ptrs[c])[li] = java_parse_long(v, INT64_MIN, INT64_MAX, "long"); break;
-            case FK_TS_INTSEC: {
-              int64_t es, ms;
-              parse_iso_local_datetime(v, offset_s, &es, &ms);
-              ((int64_t*)ptrs[c])[li] = (int64_t)(int32_t)(uint32_t)(uint64_t)es * 1000LL;
-              break;
-            }
-            case FK_TS_MS: {
-              int64_t es, ms;
-              parse_iso_local_datetime(v, offset_s, &es, &ms);
-              ((int64_t*)ptrs[c])[li] = es * 1000LL + ms;
-              break;
-            }
-            default: throw ParseError("unknown field kind");
-          }
+    auto work = [&](int t) {
+      std::vector<std::string_view> parts;
+      for (size_t k = 0; k < lines[t].size(); ++k) {
+        try {
+          parse_line_into(lines[t][k], sep[0], spec, ptrs, row0[t] + k, offset_s, parts, ld[t]);
+        } catch (const ParseError& e) {
+          terr[t] = (int64_t)(row0[t] + k);
+          tmsg[t] = e.what();
+          return;
         }
-        ++done;
-      } catch (const ParseError& e) {
-        err_idx = (int64_t)li;
-        err_msg = e.what();
+      }
+    };
+    if (T == 1) {
+      work(0);
+    } else {
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; ++t) th.emplace_back(work, t);
+      for (auto& x : th) x.join();
+    }
+    for (int t = 0; t < T; ++t)
+      if (terr[t] >= 0) {
+        err_idx = terr[t];
+        err_msg = tmsg[t];
         break;
       }
+    const size_t done = err_idx >= 0 ? (size_t)err_idx : n;
+    // Merge the local dictionaries in chunk order, then remap the string columns.
+    std::vector<std::vector<uint64_t>> gid(T);
+    {
+      std::lock_guard<std::mutex> g(dict.mu());
+      for (int t = 0; t < T && row0[t] < done; ++t) {
+        // Only strings of rows before the error enter the dictionary (as in a serial parse).
+        const size_t lim = std::min(done, row0[t + 1]) - row0[t];
+        if (lim == lines[t].size()) {
+          gid[t].reserve(ld[t].strs.size());
+          for (auto v : ld[t].strs) gid[t].push_back(dict.intern_locked(v));
+        } else {
+          // Partial chunk: intern in first-appearance order over the kept rows only.
+          gid[t].assign(ld[t].strs.size(), ~0ull);
+          for (size_t k = 0; k < lim; ++k)
+            for (size_t c = 0; c < spec.size(); ++c)
+              if (spec[c].second == FK_STR) {
+                const uint64_t l = ((uint64_t*)ptrs[c])[row0[t] + k];
+                if (gid[t][l] == ~0ull) gid[t][l] = dict.intern_locked(ld[t].strs[l]);
+              }
+        }
+      }
+    }
+    auto remap = [&](int t) {
+      const size_t lim = row0[t] < done ? std::min(done, row0[t + 1]) - row0[t] : 0;
+      for (size_t c = 0; c < spec.size(); ++c) {
+        if (spec[c].second != FK_STR) continue;
+        uint64_t* col = (uint64_t*)ptrs[c] + row0[t];
+        for (size_t k = 0; k < lim; ++k) col[k] = gid[t][col[k]];
+      }
+    };
+    if (T == 1) {
+      remap(0);
+    } else {
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; ++t) th.emplace_back(remap, t);
+      for (auto& x : th) x.join();
     }
   }
   py::list out;
   for (auto& c : cols) out.append(c);
-  return py::make_tuple(out, (int64_t)done, err_idx, err_msg);
+  const int64_t done = err_idx >= 0 ? err_idx : (int64_t)n;
+  return py::make_tuple(out, done, err_idx, err_msg);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -613,7 +755,7 @@ void bind_runtime(py::module_& m) {
       .def("strings", &StringDict::strings);
 
   m.def("parse_lines", &parse_lines, py::arg("data"), py::arg("spec"), py::arg("sep"),
-        py::arg("dict"), py::arg("offset_s") = 0);
+        py::arg("dict"), py::arg("offset_s") = 0, py::arg("threads") = 1);
 
   py::class_<SocketSource>(m, "SocketSource")
       .def(py::init<std::string, int, std::string, int, int64_t>(), py::arg("host"), py::arg("port"),

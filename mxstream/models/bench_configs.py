@@ -35,9 +35,11 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
-def config1(steps: int, warmup: int, lines_per_step: int = 1 << 20, device: str = "cpu") -> dict:
+def config1(steps: int, warmup: int, lines_per_step: int = 1 << 20, device: str = "cpu",
+            threads: int = 4) -> dict:
     """Text lines "ts ip cpuN usage" -> parse -> filter usage > 90 -> alerts. BASELINE config 1
-    is the CPU path (C++ runtime, one thread); device="cuda" runs the same job through the GPU
+    is the CPU path (C++ runtime, `threads` parse threads over newline-aligned chunks; the
+    reference job runs at parallelism 4); device="cuda" runs the same job through the GPU
     parse kernel (csrc/parse_hip.hip) and the fused filter kernel."""
     m = load()
     rng = np.random.default_rng(1)
@@ -51,7 +53,7 @@ def config1(steps: int, warmup: int, lines_per_step: int = 1 << 20, device: str 
     spec = [(1, 0), (2, 0), (3, 1)]  # host (dict id), cpu (dict id), usage (double)
 
     def step_cpu():
-        cols, n, err_idx, err = m.parse_lines(text, spec, " ", d, 0)
+        cols, n, err_idx, err = m.parse_lines(text, spec, " ", d, 0, threads)
         x = torch.from_numpy(cols[2])
         keep = K.expr_filter(x, prog)
         return int(keep.sum())
@@ -72,9 +74,10 @@ def config1(steps: int, warmup: int, lines_per_step: int = 1 << 20, device: str 
 
     step = step_gpu if device != "cpu" else step_cpu
     if device == "cpu":
-        # The CPU path is the single-threaded C++ runtime; torch's intra-op pool only adds
-        # fork/join overhead to the two tiny tensor ops per step (measured 150 ms vs 9 ms).
+        # The CPU path is the C++ runtime: `threads` parse threads and as many filter threads;
+        # torch's intra-op pool only adds fork/join overhead to the tiny tensor ops per step.
         torch.set_num_threads(1)
+        m.cpu_set_threads(threads)
 
     for _ in range(warmup):
         step()
@@ -87,7 +90,8 @@ def config1(steps: int, warmup: int, lines_per_step: int = 1 << 20, device: str 
     return {"config": 1, "metric": "events/sec (threshold alert: parse + filter)", "value": ev / dt,
             "unit": "events/s", "ms_per_step": dt / steps * 1e3, "alerts": alerts,
             "lines_per_step": lines_per_step,
-            "device": "cpu (1 thread)" if device == "cpu" else f"{device} (pinned H2D text + GPU parse)"}
+            "threads": threads if device == "cpu" else None,
+            "device": f"cpu ({threads} threads)" if device == "cpu" else f"{device} (pinned H2D text + GPU parse)"}
 
 
 def config2(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000,
@@ -310,10 +314,13 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--gpu-parse", action="store_true", help="config 1 on the GPU parse path")
+    ap.add_argument("--threads", type=int, default=4,
+                    help="config 1 CPU path: parse threads (the reference job runs at P = 4)")
     a = ap.parse_args(argv)
     if a.config == 1:
         r = config1(a.steps, a.warmup, a.batch or (1 << 20),
-                    device="cpu" if a.device == "cuda" and not a.gpu_parse else a.device)
+                    device="cpu" if a.device == "cuda" and not a.gpu_parse else a.device,
+                    threads=a.threads)
     elif a.config == 2:
         r = config2(a.steps, a.warmup, a.batch or (1 << 24), device=a.device)
     elif a.config == 4:
