@@ -76,9 +76,11 @@ PartPlan make_part(py::dict d) {
   if (p.window_mode && p.pane <= 0) throw std::invalid_argument("pane length must be positive");
   p.inv_pane = p.pane > 0 ? 1.0 / (double)p.pane : 0.0;
   p.rec_words = d.contains("rec_words") ? d["rec_words"].cast<int32_t>() : 3;
-  if (p.rec_words != 2 && p.rec_words != 3) throw std::invalid_argument("rec_words must be 2 or 3");
-  if (p.rec_words == 2 && !p.window_mode)
+  if (p.rec_words < 1 || p.rec_words > 3) throw std::invalid_argument("rec_words must be 1, 2 or 3");
+  if (p.rec_words < 3 && !p.window_mode)
     throw std::invalid_argument("compact records are for the window path");
+  if (p.rec_words == 1 && p.nranks != 1)
+    throw std::invalid_argument("8-byte records need a single destination");
   if (p.max_parallelism <= 0 || p.nranks <= 0 || p.nsub_log2 < 0 || p.nsub_log2 > 20)
     throw std::invalid_argument("bad partition plan");
   return p;
@@ -119,7 +121,7 @@ AggPlan make_agg(py::dict d) {
     if (!p.dlist_n || !p.slot_mark) throw std::invalid_argument("dirty list needs dlist_n and slot_mark");
   }
   p.rec_words = d.contains("rec_words") ? d["rec_words"].cast<int32_t>() : 3;
-  if (p.rec_words != 2 && p.rec_words != 3) throw std::invalid_argument("rec_words must be 2 or 3");
+  if (p.rec_words < 1 || p.rec_words > 3) throw std::invalid_argument("rec_words must be 1, 2 or 3");
   if (p.ring <= 0 || (p.ring & (p.ring - 1))) throw std::invalid_argument("ring must be 2^k");
   if (p.cap_log2 < 4 || p.cap_log2 > 14) throw std::invalid_argument("cap_log2 out of range");
   if (p.pg <= 0) throw std::invalid_argument("pg must be positive");

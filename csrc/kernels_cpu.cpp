@@ -18,6 +18,15 @@ namespace cpu {
 // Record at index `idx` of a bucket buffer in either layout (24-byte Rec / 16-byte RecC).
 static Rec load_any(const Rec* base, size_t idx, int rec_words) {
   if (rec_words == 3) return base[idx];
+  if (rec_words == 1) {
+    const RecN& c = reinterpret_cast<const RecN*>(base)[idx];
+    Rec r;
+    r.key = c.key;
+    r.val = (uint64_t)(int64_t)((int32_t)c.vt >> 4);
+    r.t = (c.vt & 15u) == kNarrowHoleT ? 0xFFFFFFFFu : (c.vt & 15u);
+    r.aux = 0;
+    return r;
+  }
   const RecC& c = reinterpret_cast<const RecC*>(base)[idx];
   Rec r;
   r.key = c.key;
@@ -85,6 +94,12 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
     const uint32_t pos = cursor[b]++;
     if (pos >= p.bucket_cap) {
       ovf |= 1;
+    } else if (p.rec_words == 1) {  // narrow 8-byte record
+      RecN& r = reinterpret_cast<RecN*>(out)[(size_t)b * p.bucket_cap + pos];
+      if ((int64_t)(int32_t)vals[i] != (int64_t)vals[i]) ovf |= 4;
+      if (!narrow_fits(key, (int64_t)vals[i], rt)) ovf |= 16;
+      r.key = (uint32_t)key;
+      r.vt = ((uint32_t)vals[i] << 4) | (rt & 15u);
     } else if (p.rec_words == 2) {  // compact 16-byte record (int32 value)
       RecC& r = reinterpret_cast<RecC*>(out)[(size_t)b * p.bucket_cap + pos];
       if ((int64_t)(int32_t)vals[i] != (int64_t)vals[i]) ovf |= 4;
@@ -125,7 +140,8 @@ void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int3
   red[2] = wm;
   red[3] = -(stats[kStatOverflow] & 1);
   red[4] = -((stats[kStatOverflow] >> 1) & 1);
-  red[5] = -((stats[kStatOverflow] >> 2) & 1);  // compact records cannot hold a value
+  // Record width a value needs: -2 = 24-byte records, -1 = 16-byte records, 0 = as planned.
+  red[5] = (stats[kStatOverflow] & 4) ? -2 : (stats[kStatOverflow] & 16) ? -1 : 0;
   red[6] = flags ? -(int64_t)(flags[0] & 1u) : 0;  // a key found no slot (table full), sticky
   red[7] = -((stats[kStatOverflow] >> 3) & 1);  // the reserved key id ~0 occurred
   for (int j = 0; j < kStatCount; ++j) red[8 + j] = stats[j];

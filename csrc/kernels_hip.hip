@@ -605,7 +605,8 @@ static_assert(kCompactLds <= 80 * 1024, "compact partition must fit two workgrou
 constexpr int kCUProd = 4;               // production round: 4096 records, one group per CU
 static_assert(compact_lds(kCUProd) <= 160 * 1024, "compact partition LDS exceeds 160 KiB");
 
-template <int V, int CU = kCU, bool ONE = false>
+// RB = 16: RecC records; RB = 8: RecN records (one destination, see RecN).
+template <int V, int CU = kCU, bool ONE = false, int RB = 16>
 __global__ __launch_bounds__(1024) void partition_compact_kernel(
     const uint64_t* __restrict__ keys, const int64_t* __restrict__ ts,
     const uint64_t* __restrict__ vals, const int32_t* __restrict__ jhash_tab, int64_t n,
@@ -614,7 +615,8 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
     uint32_t* __restrict__ late_idx, uint32_t late_cap) {
   extern __shared__ __attribute__((aligned(16))) unsigned char csm[];
   const int nb = plan.nranks << plan.nsub_log2;
-  uint4* rbuf = (uint4*)csm;                                   // [(1024 * CU)] sorted round
+  using RT = typename std::conditional<RB == 8, uint2, uint4>::type;
+  RT* rbuf = (RT*)csm;                                         // [(1024 * CU)] sorted round
   uint32_t* run_base = (uint32_t*)(rbuf + (1024 * CU));                // [kCMaxNb]
   uint32_t* resv = run_base + kCMaxNb;                         // reserved records per bucket
   uint32_t* lcnt = resv + kCMaxNb;                             // records written per bucket
@@ -701,7 +703,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   }
   for (int64_t r0 = start; r0 < end; r0 += (1024 * CU)) {
     uint32_t bk[CU], rk[CU];
-    uint4 rec[CU];
+    RT rec[CU];
     bool keep[CU];
     uint64_t ck[CU], cv[CU];
     int64_t ct[CU];
@@ -743,7 +745,12 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
           qmax32 = e.t > qmax32 ? e.t : qmax32;
           keep[u] = true;
           bk[u] = e.bucket;
-          rec[u] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), (uint32_t)v, e.t);
+          if constexpr (RB == 8) {
+            if (!narrow_fits(k, (int64_t)v, e.t)) flags |= 16;  // needs 16-byte records
+            rec[u] = make_uint2((uint32_t)k, ((uint32_t)v << 4) | (e.t & 15u));
+          } else {
+            rec[u] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), (uint32_t)v, e.t);
+          }
           rk[u] = atomicAdd(&rcnt[e.bucket], 1u);
         }
       }
@@ -769,8 +776,8 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
     const uint32_t nrec = wsum[16];
     nacc += threadIdx.x == 0 ? nrec : 0u;
     if (!any_ovf) {
-      uint4* out4 = (uint4*)out;
-      for (uint32_t j = threadIdx.x; j < nrec; j += blockDim.x) out4[dbase[sbk[j]] + j] = rbuf[j];
+      RT* outr = (RT*)out;
+      for (uint32_t j = threadIdx.x; j < nrec; j += blockDim.x) outr[dbase[sbk[j]] + j] = rbuf[j];
     }
     __syncthreads();
     if (threadIdx.x < (unsigned)nb) {
@@ -783,8 +790,10 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   // slots counted for late / dropped records in pass A).
   if (threadIdx.x < (unsigned)nb && !any_ovf) {
     const int b = threadIdx.x;
-    uint4* dst = (uint4*)(out + (size_t)b * bcap + run_base[b]);
-    const uint4 hole = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, kHoleT);
+    RT* dst = (RT*)out + (size_t)b * bcap + run_base[b];
+    RT hole;
+    if constexpr (RB == 8) hole = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+    else hole = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, kHoleT);
     for (uint32_t w = lcnt[b]; w < resv[b]; ++w) dst[w] = hole;
   }
 
@@ -795,7 +804,8 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   qmax = block_reduce_i64(qmax, lred, 0);
   if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
   flags = (any_ovf ? 1 : 0) | block_reduce_i64(flags & 2, lred, 0) |
-          block_reduce_i64(flags & 4, lred, 0) | block_reduce_i64(flags & 8, lred, 0);
+          block_reduce_i64(flags & 4, lred, 0) | block_reduce_i64(flags & 8, lred, 0) |
+          (RB == 8 ? block_reduce_i64(flags & 16, lred, 0) : 0);
   if (threadIdx.x == 0) {
     atomicMax((long long*)&stats[kStatMaxTs], (long long)tmax);
     if (nacc) {
@@ -839,7 +849,8 @@ __global__ void step_finish_kernel(const int64_t* __restrict__ stats, int64_t* _
   red[2] = wm;
   red[3] = -(stats[kStatOverflow] & 1);
   red[4] = -((stats[kStatOverflow] >> 1) & 1);
-  red[5] = -((stats[kStatOverflow] >> 2) & 1);  // compact records cannot hold a value
+  // Record width a value needs: -2 = 24-byte records, -1 = 16-byte records, 0 = as planned.
+  red[5] = (stats[kStatOverflow] & 4) ? -2 : (stats[kStatOverflow] & 16) ? -1 : 0;
   red[6] = flags ? -(int64_t)(flags[0] & 1u) : 0;  // a key found no slot (table full), sticky
   red[7] = -((stats[kStatOverflow] >> 3) & 1);  // the reserved key id ~0 occurred
   for (int j = 0; j < kStatCount; ++j) red[8 + j] = stats[j];
@@ -913,6 +924,15 @@ constexpr int kAggU = 4;  // 8 measured equal (162.7 vs 162.1 us, profiles/r1_wi
 template <int RW>
 __device__ __forceinline__ Rec load_rec(const void* base, size_t idx) {
   if (RW == 3) return ((const Rec*)base)[idx];
+  if (RW == 1) {  // narrow 8-byte record
+    const uint2 c = ((const uint2*)base)[idx];
+    Rec r;
+    r.key = c.x;
+    r.val = (uint64_t)(int64_t)((int32_t)c.y >> 4);
+    r.t = (c.y & 15u) == kNarrowHoleT ? 0xFFFFFFFFu : (c.y & 15u);
+    r.aux = 0;
+    return r;
+  }
   const uint4 c = ((const uint4*)base)[idx];
   Rec r;
   r.key = (uint64_t)c.x | ((uint64_t)c.y << 32);
@@ -948,8 +968,8 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
     const void* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
     uint64_t* __restrict__ keys_g, uint64_t* __restrict__ acc_g, uint32_t* __restrict__ cnt_g,
     uint8_t* __restrict__ dirty_g, uint32_t* __restrict__ occupancy, uint32_t* __restrict__ flags) {
-  static_assert(!PK || ((AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) && RW == 2),
-                "packed accumulators: integer sum/avg of 16-byte records only");
+  static_assert(!PK || ((AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) && RW <= 2),
+                "packed accumulators: integer sum/avg of 8/16-byte records only");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int sub = blockIdx.x;
   const uint32_t cap = 1u << p.cap_log2;
@@ -2526,6 +2546,28 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap,
                intptr_t stream) {
   const int nb = plan.nranks << plan.nsub_log2;
+  if (plan.rec_words == 1) {
+    // Narrow 8-byte records: only the single-destination compact kernel writes them.
+    if (plan.nranks != 1 || nb > kCMaxNb || (uint64_t)nb * plan.bucket_cap >= (1ull << 32))
+      throw std::invalid_argument("partition: 8-byte records need one destination, <= 512 buckets");
+    if (n <= 0) return;
+    static bool attr8 = false;
+    if (!attr8) {
+      HIP_CHECK(hipFuncSetAttribute((const void*)partition_compact_kernel<1, kCUProd, true, 8>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)compact_lds(kCUProd)));
+      attr8 = true;
+    }
+    const int64_t per = std::min<int64_t>(65536, std::max<int64_t>(4096, (n + 255) / 256));
+    const int blocks = grid_for(n, per, 4096);
+    const int64_t chunk = (n + blocks - 1) / blocks;
+    hipLaunchKernelGGL((partition_compact_kernel<1, kCUProd, true, 8>), dim3(blocks), dim3(1024),
+                       compact_lds(kCUProd) - (size_t)kKgLdsMax * 4, (hipStream_t)stream, keys,
+                       ts, vals, jhash_tab, n, chunk, plan, kg_dest, cursor,
+                       reinterpret_cast<RecC*>(out), stats, late_idx, late_cap);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (plan.rec_words == 2 && nb <= kCMaxNb && (uint64_t)nb * plan.bucket_cap < (1ull << 32)) {
     if (n <= 0) return;
     // 4096-record rounds, up to 64K events per workgroup (one group per CU: 86 KB of LDS),
@@ -2647,7 +2689,7 @@ static bool agg_pack_ok(const AggPlan& p) {
     const char* e = std::getenv("MXS_AGG_PACK");
     return !(e && e[0] == '0');
   }();
-  return enabled && (p.agg == AGG_SUM_I64 || p.agg == AGG_AVG_I64) && p.rec_words == 2 &&
+  return enabled && (p.agg == AGG_SUM_I64 || p.agg == AGG_AVG_I64) && p.rec_words <= 2 &&
          !p.combined && (uint64_t)p.nsrc * p.bucket_cap < 65536;
 }
 
@@ -2661,21 +2703,34 @@ static void launch_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 2>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    if constexpr (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64)
+    HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 1>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    if constexpr (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) {
       HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 2, true>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 1, true>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    }
     attr = true;
   }
   if constexpr (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) {
     if (agg_pack_ok(p)) {
       const size_t cap = (size_t)1 << p.cap_log2;
-      const size_t lds_pk = cap * 8 + (size_t)p.pg * cap * 8 + 16;
-      hipLaunchKernelGGL((window_agg_kernel<AGG, 2, true>), dim3(p.nsub), dim3(1024), lds_pk, s,
-                         (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+      const size_t lds_pk = cap * 8 + (size_t)p.pg * cap * 8 + 16 +
+                            (p.dlist ? 16 + cap / 8 + cap * 4 : 0);
+      if (p.rec_words == 1)
+        hipLaunchKernelGGL((window_agg_kernel<AGG, 1, true>), dim3(p.nsub), dim3(1024), lds_pk, s,
+                           (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+      else
+        hipLaunchKernelGGL((window_agg_kernel<AGG, 2, true>), dim3(p.nsub), dim3(1024), lds_pk, s,
+                           (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
       return;
     }
   }
-  if (p.rec_words == 2)
+  if (p.rec_words == 1)
+    hipLaunchKernelGGL((window_agg_kernel<AGG, 1>), dim3(p.nsub), dim3(1024), lds, s,
+                       (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+  else if (p.rec_words == 2)
     hipLaunchKernelGGL((window_agg_kernel<AGG, 2>), dim3(p.nsub), dim3(1024), lds, s,
                        (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
   else
@@ -2691,7 +2746,7 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& plan, ui
   const size_t lds = cap * 8 + (size_t)plan.pg * cap * 12 + 16 +
                      (plan.dlist ? 16 + cap / 8 + cap * 4 : 0);  // touched-slot bitmap + buffer
   if (lds > 160 * 1024) throw std::runtime_error("window_agg: LDS image exceeds 160 KiB");
-  if (plan.rec_words == 2 && plan.combined)
+  if (plan.rec_words < 3 && plan.combined)
     throw std::invalid_argument("window_agg: combined records are 24-byte records");
   hipStream_t s = (hipStream_t)stream;
   switch (plan.agg) {

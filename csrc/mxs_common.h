@@ -53,6 +53,21 @@ struct alignas(16) RecC {
 };
 static_assert(sizeof(RecC) == 16, "RecC must be 16 bytes");
 
+// Narrow 8-byte record (window path with integer aggregates when one destination owns every
+// key: G = 1 or local-global aggregation): 32-bit key id, value in 28 bits (signed), relative
+// pane in 4 bits; vt = value << 4 | t, t = 15 marks a hole. A record that does not fit sets
+// overflow bit 16 and the step is redone with 16-byte records (sticky).
+struct RecN {
+  uint32_t key;
+  uint32_t vt;
+};
+static_assert(sizeof(RecN) == 8, "RecN must be 8 bytes");
+constexpr uint32_t kNarrowHoleT = 15u;
+MXS_HD bool narrow_fits(uint64_t key, int64_t v, uint32_t t) {
+  return key < 0xFFFFFFFFull && v >= -(int64_t(1) << 27) && v < (int64_t(1) << 27) &&
+         t < kNarrowHoleT;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Java / Flink hashing
 // ---------------------------------------------------------------------------------------------

@@ -70,6 +70,7 @@ class VectorWindowOperator(KeyedWindowOperator):
 
     _local_global_ok = False  # vector panes are exchanged per step (records mode)
     _use_dlist = False        # its own fire kernel sweeps the table
+    _narrow_ok = False        # records carry a row index into the vector batch
 
     # ---- hooks -----------------------------------------------------------------------------
     def _rec_words(self) -> int:

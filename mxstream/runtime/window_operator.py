@@ -180,7 +180,7 @@ class _Front:
     old_wm: int
     pane_base: int
     proc_now: int
-    compact: bool = True
+    rw: int = 3
     ev: object = None
     idle: bool = False
 
@@ -191,7 +191,7 @@ class _Back:
     par: int
     n: int
     old_wm: int
-    compact: bool
+    rw: int
     pane_base: int
     has_data: bool = False
     qmin: int = 0
@@ -235,6 +235,7 @@ class KeyedWindowOperator:
                  side_output_late: bool = False, late_capacity: int = 1 << 16,
                  clock: Callable[[], int] | None = None, external_watermark: bool = False,
                  combine: bool | None = None, compact: bool | None = None,
+                 narrow: bool | None = None,
                  pipeline: bool | None = None, exchange: str = "auto",
                  idle_timeout_steps: int | None = None):
         self.device = K.resolve_device(device)
@@ -376,7 +377,16 @@ class KeyedWindowOperator:
         int_agg = agg in (K.AGG_SUM_I64, K.AGG_MIN_I64, K.AGG_MAX_I64, K.AGG_COUNT, K.AGG_AVG_I64)
         if compact is None:
             compact = self.device.type == "cuda" and int_agg
-        self.compact = bool(compact and int_agg)
+        compact = bool(compact and int_agg)
+        # 8-byte records (32-bit key id, 28-bit value, 4-bit pane) when one destination owns
+        # every key (G = 1 or local-global) and the partition uses its LDS-sorted kernel; a
+        # record that does not fit widens the format for good (step redone).
+        if narrow is None:
+            narrow = compact and self.device.type == "cuda"
+        narrow = bool(narrow and compact and not self._exchanging and self.nbuckets <= 512
+                      and type(self)._narrow_ok)
+        # Record words: 1 = 8-byte RecN, 2 = 16-byte RecC (int32 values), 3 = 24-byte Rec.
+        self.rec_w = 1 if narrow else 2 if compact else 3
         self.timer = None  # utils.metrics.StageTimer: per-stage step_ms histograms when attached
         from ..ops.debug import debug_enabled
 
@@ -390,6 +400,12 @@ class KeyedWindowOperator:
         self.late_side: list[np.ndarray] = []
 
     _local_global_ok = True  # subclasses whose fire is not a plain reduce opt out
+    _narrow_ok = True        # subclasses whose records carry more than (key, value) opt out
+
+    @property
+    def compact(self) -> bool:
+        """Records narrower than 24 bytes (integer values)."""
+        return self.rec_w < 3
     _use_dlist = True        # subclasses with their own fire kernel opt out of slot lists
 
     def _init_owner_tables(self, max_keys: int, cap_log2: int | None) -> None:
@@ -494,7 +510,7 @@ class KeyedWindowOperator:
         cplan = K.AggPlan(cap_log2=self.cap_log2, nsub=nb, ring=self.ring, agg=self.agg,
                           nsrc=1, bucket_cap=self.bucket_cap, np_step=b.np_step, pg=b.pg,
                           pane_base=0, p_lo=b.qmin, fired_hi=0,
-                          rec_words=2 if b.compact else 3)
+                          rec_words=b.rw)
         K.window_combine(self.send, self.cursor, cplan, self.comb_send, ccap,
                          self.comb_counts, self.flags[1:2])
         chk = torch.stack([-(self.flags[1].to(torch.int64) & 2),
@@ -670,8 +686,8 @@ class KeyedWindowOperator:
             window_mode=1, drop_late=int(event_mode), hash_mode=self.hash_mode,
             bucket_cap=self.bucket_cap, late_ts=self._late_ts(f.old_wm),
             tbase=self.pane_start(f.pane_base), pane=self.pane,
-            rec_words=2 if self.compact else 3)
-        f.compact = self.compact
+            rec_words=self.rec_w)
+        f.rw = self.rec_w
         with self._stage("partition"):
             if f.n:
                 K.partition(f.keys, f.ts, f.vals, plan, self.kg_dest, self.cursor, self.send,
@@ -705,9 +721,11 @@ class KeyedWindowOperator:
                                    "(raise max_keys)")
             if host[7]:
                 raise ValueError("key ids -1 and -2 are reserved (the state tables' markers)")
-            if host[5]:
-                # A value does not fit the 16-byte record: 24-byte records from now on.
-                self.compact = False
+            need_rw = {1: 2, 2: 3}.get(-host[5], self.rec_w)
+            if need_rw > self.rec_w:
+                # A record does not fit the format: wider records from now on (2: a key or value
+                # outside the 8-byte record, 3: a value outside int32).
+                self.rec_w = need_rw
                 self.metrics.extra["compact_fallbacks"] = self.metrics.extra.get("compact_fallbacks", 0) + 1
             elif host[3]:
                 # A bucket overflowed somewhere: grow the fixed bucket capacity and redo the step.
@@ -730,7 +748,7 @@ class KeyedWindowOperator:
         if self.side_output_late and st[K.STAT_LATE]:
             nl = min(int(st[K.STAT_LATE]), self.late_idx.numel())
             self.late_side.append(self.late_idx[:nl].cpu().numpy().copy())
-        b = _Back(par=f.par, n=f.n, old_wm=f.old_wm, compact=f.compact, pane_base=f.pane_base)
+        b = _Back(par=f.par, n=f.n, old_wm=f.old_wm, rw=f.rw, pane_base=f.pane_base)
         if qmin <= qmax:
             gmin, gmax = f.pane_base + qmin, f.pane_base + qmax
             lo = gmin if self.min_live_pane is None else min(self.min_live_pane, gmin)
@@ -785,14 +803,14 @@ class KeyedWindowOperator:
                     combined = 1
                 elif self._exchanging:
                     with self._stage("all_to_all"):
-                        self._exchange(2 if b.compact else 3)
+                        self._exchange(b.rw)
                 if cuda and self._exchanging:
                     self._ev_consumed[b.par] = self._event()
                 aplan = K.AggPlan(cap_log2=self.cap_log2, nsub=self.nsub, ring=self.ring,
                                   agg=self.agg, nsrc=self._part_ranks, bucket_cap=bcap,
                                   np_step=b.np_step, pg=b.pg, pane_base=b.pane_base,
                                   p_lo=b.qmin, fired_hi=b.fired_hi, combined=combined,
-                                  rec_words=3 if combined else (2 if b.compact else 3))
+                                  rec_words=3 if combined else b.rw)
                 if self.dlist is not None:
                     aplan.dlist, aplan.dlist_n = self.dlist.data_ptr(), self.dlist_n.data_ptr()
                     aplan.slot_mark = self.slot_mark.data_ptr()

@@ -175,3 +175,43 @@ def test_pinned_slab_pool_reuses_only_released_slabs():
     assert pool.allocs == 2  # released slab reused
     big = pool.take(1 << 20)
     assert big[0].numel() >= 1 << 20 and pool.allocs == 3 and len(pool.slabs) <= 2
+
+
+@pytest.mark.parametrize("big", ["none", "value", "key", "int32"])
+def test_narrow_records_match_wide(big):
+    """8-byte records (32-bit key, 28-bit value, 4-bit pane) on the C++ twin give the same
+    windows as 24-byte records; a key or value that does not fit widens the format (16-byte,
+    or 24-byte for a value outside int32) and redoes the step."""
+    import torch
+
+    from mxstream.ops import kernels as K
+    from mxstream.runtime.window_operator import KeyedWindowOperator
+
+    def run(narrow):
+        op = KeyedWindowOperator(size=2000, slide=1000, agg=K.AGG_SUM_I64, device="cpu",
+                                 max_keys=4000, batch_capacity=5000, ooo_bound=300, cap_log2=8,
+                                 compact=narrow, narrow=narrow)
+        out = []
+        for step in range(6):
+            k = torch.empty(5000, dtype=torch.int64)
+            t = torch.empty_like(k)
+            v = torch.empty_like(k)
+            K.gen_events(k, t, v, seed=9, stream_id=0, idx0=step * 5000, nkeys=3000,
+                         ts_base=step * 1000, ts_span=1000, disorder=300, val_lo=-500,
+                         val_span=1000)
+            if step == 3 and big == "value":
+                v[7] = 1 << 29
+            if step == 3 and big == "key":
+                k[7] = (1 << 32) + 5
+            if step == 3 and big == "int32":
+                v[7] = 1 << 40
+            out += op.process(k, t, v)
+        out += op.finish()
+        return ({(r.window_start, int(a), int(b), int(c))
+                 for r in out for a, b, c in zip(r.keys, r.raw, r.counts)}, op.rec_w)
+
+    wide, rw_wide = run(False)
+    nar, rw_nar = run(True)
+    assert rw_wide == 3
+    assert rw_nar == {"none": 1, "value": 2, "key": 2, "int32": 3}[big]
+    assert nar == wide
