@@ -38,6 +38,7 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=1 << 24, help="events per GPU per step")
     ap.add_argument("--keys", type=int, default=1_000_000)
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--cap-log2", type=int, default=None, help="sub-table size (experiments)")
     ap.add_argument("--trace", default=None,
                     help="write a Chrome trace of the timed steps (stage spans; roctx with MXS_ROCTX=1)")
     ap.add_argument("--step-timeout-ms", type=int, default=0,
@@ -62,7 +63,7 @@ def main() -> int:
     else:
         device = torch.device("cpu")
 
-    cfg = TumblingBenchConfig(keys=a.keys, batch=a.batch)
+    cfg = TumblingBenchConfig(keys=a.keys, batch=a.batch, cap_log2=a.cap_log2)
     bench = TumblingWindowBench(cfg, comm, device)
     if a.trace:
         from mxstream.utils import trace

@@ -40,6 +40,7 @@ class TumblingBenchConfig:
     # profiles/r2_pipeline_g1.md).
     pipeline: bool | None = None
     exchange: str = "auto"           # G > 1: "partials" (local-global) or "records"
+    cap_log2: int | None = None      # sub-table size override (experiments)
 
 
 class TumblingWindowBench:
@@ -57,7 +58,7 @@ class TumblingWindowBench:
             ooo_bound=cfg.disorder_ms, map_prog=E.compile_expr(mbps),
             filter_prog=E.compile_expr(E.var(E.VAR_MAPPED) < self.threshold_mbps),
             pipeline=(world > 1) if cfg.pipeline is None else cfg.pipeline,
-            exchange=cfg.exchange)
+            exchange=cfg.exchange, cap_log2=cfg.cap_log2)
         self.keys = torch.empty(cfg.batch, dtype=torch.int64, device=device)
         self.ts = torch.empty(cfg.batch, dtype=torch.int64, device=device)
         self.vals = torch.empty(cfg.batch, dtype=torch.int64, device=device)
