@@ -29,6 +29,16 @@ for step in "$@"; do
     cfg2|cfg4|cfg5|cfg6) timeout -k 10 300 python -m mxstream.models.bench_configs --config ${step#cfg} --steps 20 --warmup 5 > "$out/$step.json" 2>&1 || exit $? ;;
     loop8) timeout -k 10 300 python scripts/loopback_bench.py --world 8 --steps 24 --warmup 4 --out "$out/loop8.json" > "$out/loop8.log" 2>&1 || exit $? ;;
     prof_bench) prof bench python3 bench.py --steps 24 --warmup 6 || exit $? ;;
+    prof_bench_cap*) c=${step#prof_bench_cap}; prof bench_cap$c python3 bench.py --steps 24 --warmup 6 --cap-log2 $c || exit $? ;;
+    pmc_bench*) # pmc_bench<k>: one counter pass over the headline (window_agg / partition)
+      k=${step#pmc_bench}
+      case $k in
+        1) set="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS" ;;
+        2) set="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INST_LEVEL_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY" ;;
+        3) set="TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum" ;;
+      esac
+      (cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" &&
+       timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --pmc $set -d "$out/pmc_bench$k" -o run -- python3 bench.py --steps 6 --warmup 3 > "$out/pmc_bench$k.log" 2>&1) || exit $? ;;
     prof_cfg2|prof_cfg4|prof_cfg5|prof_cfg6) c=${step#prof_cfg}; prof cfg$c python3 -m mxstream.models.bench_configs --config $c --steps 12 --warmup 4 || exit $? ;;
     prof_loop8) prof loop8 python3 scripts/loopback_bench.py --world 8 --steps 24 --warmup 4 || exit $? ;;
     *) echo "unknown step $step"; exit 2 ;;
