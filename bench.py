@@ -39,6 +39,8 @@ def main() -> int:
     ap.add_argument("--keys", type=int, default=1_000_000)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--cap-log2", type=int, default=None, help="sub-table size (experiments)")
+    ap.add_argument("--hashed-keys", action="store_true",
+                    help="hash-table state for arbitrary int64 keys instead of dense dictionary ids")
     ap.add_argument("--trace", default=None,
                     help="write a Chrome trace of the timed steps (stage spans; roctx with MXS_ROCTX=1)")
     ap.add_argument("--step-timeout-ms", type=int, default=0,
@@ -63,7 +65,8 @@ def main() -> int:
     else:
         device = torch.device("cpu")
 
-    cfg = TumblingBenchConfig(keys=a.keys, batch=a.batch, cap_log2=a.cap_log2)
+    cfg = TumblingBenchConfig(keys=a.keys, batch=a.batch, cap_log2=a.cap_log2,
+                              dense_keys=not a.hashed_keys)
     bench = TumblingWindowBench(cfg, comm, device)
     if a.trace:
         from mxstream.utils import trace
@@ -127,7 +130,8 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64",
-            "data": "synthetic (device-generated metric events, uniform keys, 2 s bounded disorder)",
+            "data": "synthetic (device-generated metric events, uniform keys = dictionary ids of "
+                    "1M channels, 2 s bounded disorder)",
             "p50_alert_latency_ms": (lt.item() if lt.item() >= 0 else None),
             "alerts": int(al.item()),
             "late_dropped": bench.op.metrics.num_late_records_dropped,
@@ -141,6 +145,8 @@ def main() -> int:
                 # records: per-step exchange of combined (key, pane) records.
                 "exchange": ("partials" if bench.op.local_global
                              else "records" if n > 1 else "none"),
+                "keyed_state": "dense" if bench.op.dense_bits else "hashed",
+                "record_bytes": {1: 8, 2: 16, 3: 24}[bench.op.rec_w],
                 "keys": a.keys,
                 "events_per_gpu_per_step": a.batch,
                 "event_time_per_step_ms": cfg.step_span_ms,

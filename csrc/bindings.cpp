@@ -75,6 +75,11 @@ PartPlan make_part(py::dict d) {
   p.pane = d["pane"].cast<int64_t>();
   if (p.window_mode && p.pane <= 0) throw std::invalid_argument("pane length must be positive");
   p.inv_pane = p.pane > 0 ? 1.0 / (double)p.pane : 0.0;
+  p.dense_bits = d.contains("dense_bits") ? d["dense_bits"].cast<int32_t>() : 0;
+  p.dense_mul = d.contains("dense_mul") ? d["dense_mul"].cast<uint32_t>() : 0u;
+  if (p.dense_bits < 0 || p.dense_bits > 32 || (p.dense_bits && (p.nranks != 1 ||
+      p.nsub_log2 > p.dense_bits || !(p.dense_mul & 1u))))
+    throw std::invalid_argument("dense keys: one destination, nsub <= 2^bits, odd multiplier");
   p.rec_words = d.contains("rec_words") ? d["rec_words"].cast<int32_t>() : 3;
   if (p.rec_words < 1 || p.rec_words > 3) throw std::invalid_argument("rec_words must be 1, 2 or 3");
   if (p.rec_words < 3 && !p.window_mode)
@@ -114,6 +119,11 @@ AggPlan make_agg(py::dict d) {
   p.p_lo = d["p_lo"].cast<int64_t>();
   p.fired_hi = d["fired_hi"].cast<int64_t>();
   p.combined = d.contains("combined") ? d["combined"].cast<int32_t>() : 0;
+  p.dense_bits = d.contains("dense_bits") ? d["dense_bits"].cast<int32_t>() : 0;
+  p.dense_mul = d.contains("dense_mul") ? d["dense_mul"].cast<uint32_t>() : 0u;
+  if (p.dense_bits && (p.dense_bits > 32 || !(p.dense_mul & 1u) || p.combined ||
+      ((int64_t)p.nsub << p.cap_log2) != ((int64_t)1 << p.dense_bits)))
+    throw std::invalid_argument("dense keys: nsub << cap_log2 == 2^bits, odd multiplier, raw records");
   if (d.contains("dlist") && d["dlist"].cast<intptr_t>()) {
     p.dlist = reinterpret_cast<uint32_t*>(d["dlist"].cast<intptr_t>());
     p.dlist_n = reinterpret_cast<uint32_t*>(d["dlist_n"].cast<intptr_t>());

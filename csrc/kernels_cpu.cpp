@@ -178,7 +178,16 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p, uint6
         const Rec r = load_any(recs, seg0 + e, p.rec_words);
         const int64_t q = (int64_t)r.t - p.p_lo;
         if (q < 0 || q >= p.np_step) continue;
-        const uint32_t s = probe_insert(keys, r.key, mask, &inserted);
+        uint32_t s;
+        if (p.dense_bits) {
+          if (p.dense_bits < 64 && (r.key >> p.dense_bits)) {  // id outside the dense space
+            flags[0] |= 1u;
+            continue;
+          }
+          s = dense_slot(r.key, p.dense_mul, p.dense_bits) & mask;
+        } else {
+          s = probe_insert(keys, r.key, mask, &inserted);
+        }
         if (s == kNoSlot) {
           flags[0] |= 1u;
           continue;

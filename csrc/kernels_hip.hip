@@ -137,7 +137,7 @@ __device__ __forceinline__ PartEval part_eval(uint64_t key, int64_t ts, const in
     }
   }
   if constexpr (ONE) {
-    e.bucket = sub_table_of(key, p.nsub_log2);
+    e.bucket = sub_of(key, p);
   } else {
     const int32_t jh = p.nranks == 1 ? 0 : p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
     e.bucket = bucket_of(key, jh, p, kg_dest);
@@ -656,7 +656,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
       if (i >= end) break;
       uint32_t b;
       if constexpr (ONE) {
-        b = sub_table_of(k[u], plan.nsub_log2);
+        b = sub_of(k[u], plan);
       } else {
         const int32_t jh = plan.nranks == 1 ? 0
                            : plan.hash_mode ? jhash_tab[k[u]] : java_long_hash((int64_t)k[u]);
@@ -963,7 +963,8 @@ __device__ __forceinline__ uint32_t pk_cnt(uint64_t p) {
   return (uint32_t)((p - (uint64_t)pk_sum(p)) >> 48);
 }
 
-template <int AGG, int RW, bool PK = false>
+// DENSE: directly addressed dense key ids (AggPlan.dense_bits): no LDS key table, no probe.
+template <int AGG, int RW, bool PK = false, bool DENSE = false>
 __global__ __launch_bounds__(1024) void window_agg_kernel(
     const void* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
     uint64_t* __restrict__ keys_g, uint64_t* __restrict__ acc_g, uint32_t* __restrict__ cnt_g,
@@ -974,14 +975,15 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
   const int sub = blockIdx.x;
   const uint32_t cap = 1u << p.cap_log2;
   const uint32_t mask = cap - 1;
-  uint64_t* skeys = (uint64_t*)smem;
-  uint64_t* sacc = skeys + cap;
+  uint64_t* skeys = (uint64_t*)smem;                   // unused when DENSE
+  uint64_t* sacc = DENSE ? (uint64_t*)smem : skeys + cap;
   uint32_t* scnt = (uint32_t*)(sacc + (size_t)p.pg * cap);           // unused when PK
   int* sflag = (int*)(scnt + (PK ? 0 : (size_t)p.pg * cap));  // [0] inserted, [1] ovf, [2] occ
 
   const size_t sbase = (size_t)sub << p.cap_log2;
   const size_t nslots = (size_t)p.nsub << p.cap_log2;
-  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) skeys[i] = keys_g[sbase + i];
+  if constexpr (!DENSE)
+    for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) skeys[i] = keys_g[sbase + i];
   if (threadIdx.x < 4) sflag[threadIdx.x] = 0;
   // Touched-slot list (late-but-allowed data): an LDS bitmap dedupes the sub-table's slots
   // across pane passes and an LDS buffer collects them; one global atomic per workgroup at the
@@ -1030,10 +1032,19 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
           if (r.t == 0xFFFFFFFFu) continue;  // hole record (staged partition padding)
           const int64_t q = (int64_t)r.t - q0;
           if (q < 0 || q >= npg) continue;
-          const uint32_t s = lds_probe_insert(skeys, r.key, mask, &inserted);
-          if (s == kNoSlot) {
-            ovf = true;
-            continue;
+          uint32_t s;
+          if constexpr (DENSE) {
+            if (r.key >> p.dense_bits) {  // id outside the dense key space: table full
+              ovf = true;
+              continue;
+            }
+            s = dense_slot(r.key, p.dense_mul, p.dense_bits) & mask;
+          } else {
+            s = lds_probe_insert(skeys, r.key, mask, &inserted);
+            if (s == kNoSlot) {
+              ovf = true;
+              continue;
+            }
           }
           const uint32_t li = (uint32_t)q * cap + s;
           if (PK) {
@@ -2693,49 +2704,59 @@ static bool agg_pack_ok(const AggPlan& p) {
          !p.combined && (uint64_t)p.nsrc * p.bucket_cap < 65536;
 }
 
-template <int AGG>
-static void launch_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p,
-                       uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
-                       uint32_t* occ, uint32_t* flags, size_t lds, hipStream_t s) {
+template <int AGG, int RW, bool PK, bool DENSE>
+static void launch_agg_v(const Rec* recs, const uint32_t* counts, const AggPlan& p,
+                         uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
+                         uint32_t* occ, uint32_t* flags, size_t lds, hipStream_t s) {
   static bool attr = false;
-  if (!attr) {  // allow the full 160 KiB LDS for both record layouts
-    HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 3>,
+  if (!attr) {  // allow the full 160 KiB LDS
+    HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, RW, PK, DENSE>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 2>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 1>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    if constexpr (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) {
-      HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 2, true>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, 1, true>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    }
     attr = true;
   }
+  hipLaunchKernelGGL((window_agg_kernel<AGG, RW, PK, DENSE>), dim3(p.nsub), dim3(1024), lds, s,
+                     (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+}
+
+template <int AGG, bool DENSE>
+static void launch_agg_d(const Rec* recs, const uint32_t* counts, const AggPlan& p,
+                         uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
+                         uint32_t* occ, uint32_t* flags, hipStream_t s) {
+  const size_t cap = (size_t)1 << p.cap_log2;
+  const size_t keys_lds = DENSE ? 0 : cap * 8;  // dense ids need no LDS key table
+  const size_t list_lds = p.dlist ? 16 + cap / 8 + cap * 4 : 0;
   if constexpr (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) {
     if (agg_pack_ok(p)) {
-      const size_t cap = (size_t)1 << p.cap_log2;
-      const size_t lds_pk = cap * 8 + (size_t)p.pg * cap * 8 + 16 +
-                            (p.dlist ? 16 + cap / 8 + cap * 4 : 0);
+      const size_t lds_pk = keys_lds + (size_t)p.pg * cap * 8 + 16 + list_lds;
       if (p.rec_words == 1)
-        hipLaunchKernelGGL((window_agg_kernel<AGG, 1, true>), dim3(p.nsub), dim3(1024), lds_pk, s,
-                           (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+        launch_agg_v<AGG, 1, true, DENSE>(recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ,
+                                          flags, lds_pk, s);
       else
-        hipLaunchKernelGGL((window_agg_kernel<AGG, 2, true>), dim3(p.nsub), dim3(1024), lds_pk, s,
-                           (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+        launch_agg_v<AGG, 2, true, DENSE>(recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ,
+                                          flags, lds_pk, s);
       return;
     }
   }
+  const size_t lds = keys_lds + (size_t)p.pg * cap * 12 + 16 + list_lds;
   if (p.rec_words == 1)
-    hipLaunchKernelGGL((window_agg_kernel<AGG, 1>), dim3(p.nsub), dim3(1024), lds, s,
-                       (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+    launch_agg_v<AGG, 1, false, DENSE>(recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags,
+                                       lds, s);
   else if (p.rec_words == 2)
-    hipLaunchKernelGGL((window_agg_kernel<AGG, 2>), dim3(p.nsub), dim3(1024), lds, s,
-                       (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+    launch_agg_v<AGG, 2, false, DENSE>(recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags,
+                                       lds, s);
   else
-    hipLaunchKernelGGL((window_agg_kernel<AGG, 3>), dim3(p.nsub), dim3(1024), lds, s,
-                       (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+    launch_agg_v<AGG, 3, false, DENSE>(recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags,
+                                       lds, s);
+}
+
+template <int AGG>
+static void launch_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p,
+                       uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
+                       uint32_t* occ, uint32_t* flags, size_t, hipStream_t s) {
+  if (p.dense_bits)
+    launch_agg_d<AGG, true>(recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags, s);
+  else
+    launch_agg_d<AGG, false>(recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags, s);
 }
 
 void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& plan, uint64_t* keys_g,

@@ -429,6 +429,8 @@ struct PartPlan {
   int64_t pane;              // pane length (ms)
   double inv_pane;           // 1.0 / pane
   int32_t rec_words;         // 3: 24-byte Rec; 2: 16-byte RecC (int32 values, GPU window path)
+  int32_t dense_bits;        // > 0: dense key ids < 2^dense_bits, directly addressed (dense_slot)
+  uint32_t dense_mul;        // odd multiplier of the dense slot bijection
 };
 
 // Sub-table of a key: a 32-bit multiplicative hash of both key halves (3 32-bit multiplies).
@@ -454,8 +456,25 @@ MXS_HD uint32_t slot_hash(uint64_t key) {
   return h;
 }
 
+// Dense key ids (dictionary ids of string keys, or any id space [0, 2^bits)): the state is
+// directly addressed, no hash-table probe. A bijection on [0, 2^bits) -- multiplication by an
+// odd constant mod 2^bits -- spreads consecutive ids over the sub-tables (high bits) and gives
+// each id its own slot; the host keeps the inverse to name the key of a slot.
+MXS_HD uint32_t dense_slot(uint64_t key, uint32_t mul, int bits) {
+  const uint32_t m = bits >= 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u);
+  return ((uint32_t)key * mul) & m;
+}
+
+// Sub-table of a key on a single-destination plan (hashed, or dense high bits).
+MXS_HD uint32_t sub_of(uint64_t key, const PartPlan& p) {
+  if (p.dense_bits > 0)
+    return p.nsub_log2 ? dense_slot(key, p.dense_mul, p.dense_bits) >> (p.dense_bits - p.nsub_log2)
+                       : 0u;
+  return sub_table_of(key, p.nsub_log2);
+}
+
 MXS_HD uint32_t bucket_of(uint64_t key, int32_t jhash, const PartPlan& p, const int32_t* kg_dest) {
-  const uint32_t sub = sub_table_of(key, p.nsub_log2);
+  const uint32_t sub = sub_of(key, p);
   if (p.nranks == 1) return sub;  // one rank owns every key group: no Java hash / murmur needed
   const int32_t kg = key_group_of_hash(jhash, p.max_parallelism);
   const int32_t dest = kg_dest[kg];

@@ -33,6 +33,8 @@ struct AggPlan {
   uint32_t* dlist;      // [nslots] slot ids
   uint32_t* dlist_n;    // list length
   uint32_t* slot_mark;  // [nslots] 1 = listed
+  int32_t dense_bits;   // > 0: directly addressed dense key ids (slot = dense_slot(key))
+  uint32_t dense_mul;
 };
 
 // Plan of one window firing.

@@ -41,6 +41,9 @@ class TumblingBenchConfig:
     pipeline: bool | None = None
     exchange: str = "auto"           # G > 1: "partials" (local-global) or "records"
     cap_log2: int | None = None      # sub-table size override (experiments)
+    # Channel keys arrive as dictionary ids (the source interns strings, SURVEY.md F-ser), i.e.
+    # dense ids < keys: directly addressed state. False: the hashed tables (arbitrary int64 keys).
+    dense_keys: bool = True
 
 
 class TumblingWindowBench:
@@ -58,7 +61,7 @@ class TumblingWindowBench:
             ooo_bound=cfg.disorder_ms, map_prog=E.compile_expr(mbps),
             filter_prog=E.compile_expr(E.var(E.VAR_MAPPED) < self.threshold_mbps),
             pipeline=(world > 1) if cfg.pipeline is None else cfg.pipeline,
-            exchange=cfg.exchange, cap_log2=cfg.cap_log2)
+            exchange=cfg.exchange, cap_log2=cfg.cap_log2, dense_keys=cfg.dense_keys)
         self.keys = torch.empty(cfg.batch, dtype=torch.int64, device=device)
         self.ts = torch.empty(cfg.batch, dtype=torch.int64, device=device)
         self.vals = torch.empty(cfg.batch, dtype=torch.int64, device=device)

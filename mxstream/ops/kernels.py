@@ -107,6 +107,8 @@ class PartitionPlan:
     pane: int = 1            # pane length (ms)
     ablate: int = 0          # profiling-only ablation bits
     rec_words: int = 3       # 3: 24-byte records; 2: 16-byte records (int32 values, window path)
+    dense_bits: int = 0      # > 0: dense key ids < 2^dense_bits, directly addressed
+    dense_mul: int = 0       # odd multiplier of the dense slot bijection
 
     @property
     def nbuckets(self) -> int:
@@ -166,6 +168,8 @@ class AggPlan:
     dlist: int = 0       # touched-slot list (data pointers, 0 = off): slot ids ...
     dlist_n: int = 0     # ... its length ...
     slot_mark: int = 0   # ... and the per-slot listed marks
+    dense_bits: int = 0  # > 0: directly addressed dense key ids (see PartitionPlan)
+    dense_mul: int = 0
 
     def as_dict(self) -> dict:
         return dict(self.__dict__)

@@ -71,6 +71,7 @@ class VectorWindowOperator(KeyedWindowOperator):
     _local_global_ok = False  # vector panes are exchanged per step (records mode)
     _use_dlist = False        # its own fire kernel sweeps the table
     _narrow_ok = False        # records carry a row index into the vector batch
+    _dense_ok = False         # its own aggregation kernel
 
     # ---- hooks -----------------------------------------------------------------------------
     def _rec_words(self) -> int:

@@ -235,7 +235,7 @@ class KeyedWindowOperator:
                  side_output_late: bool = False, late_capacity: int = 1 << 16,
                  clock: Callable[[], int] | None = None, external_watermark: bool = False,
                  combine: bool | None = None, compact: bool | None = None,
-                 narrow: bool | None = None,
+                 narrow: bool | None = None, dense_keys: bool = False,
                  pipeline: bool | None = None, exchange: str = "auto",
                  idle_timeout_steps: int | None = None):
         self.device = K.resolve_device(device)
@@ -296,8 +296,23 @@ class KeyedWindowOperator:
         # ---- state geometry ----
         from .geometry import state_geometry
 
-        self.nsub, self.cap_log2 = (self._geometry(max_keys, cap_log2) if self._geometry
-                                    else state_geometry(max_keys, self._part_ranks, cap_log2))
+        # Dense keys: ids < max_keys (dictionary ids of string keys) are directly addressed --
+        # 2^bits slots, slot = id * mul mod 2^bits (a bijection), no hash-table probe, no LDS key
+        # table. Needs one destination per event (G = 1 or local-global aggregation).
+        self.dense_bits = self.dense_mul = 0
+        if dense_keys:
+            if self._exchanging or not self._dense_ok:
+                raise ValueError("dense_keys needs one destination (G = 1 or exchange='partials')")
+            bits = max(4, int(max_keys - 1).bit_length())
+            if bits > 32:
+                raise ValueError("dense_keys: ids must fit 32 bits")
+            cl = min(12, bits) if cap_log2 is None else min(int(cap_log2), bits)
+            self.nsub, self.cap_log2 = 1 << (bits - cl), cl
+            self.dense_bits = bits
+            self.dense_mul = (0x9E3779B1 & ((1 << bits) - 1)) | 1
+        else:
+            self.nsub, self.cap_log2 = (self._geometry(max_keys, cap_log2) if self._geometry
+                                        else state_geometry(max_keys, self._part_ranks, cap_log2))
         cap_log2 = self.cap_log2
         self.nsub_log2 = self.nsub.bit_length() - 1
         if self.nsub * self._part_ranks > 16384:
@@ -306,7 +321,13 @@ class KeyedWindowOperator:
         self.ring = max(4, _next_pow2(self.panes_per_window + 2 + math.ceil(self.lateness / self.pane)
                                      + math.ceil(max(self.ooo_bound, self.slide) / self.pane)))
         dev = self.device
-        self.keys_g = torch.full((self.nslots,), -1, dtype=torch.int64, device=dev)
+        if self.dense_bits:
+            # The key of every slot: the inverse bijection (slots are never "inserted").
+            inv = pow(self.dense_mul, -1, 1 << self.dense_bits)
+            self.keys_g = (torch.arange(self.nslots, dtype=torch.int64, device=dev) * inv) & \
+                ((1 << self.dense_bits) - 1)
+        else:
+            self.keys_g = torch.full((self.nslots,), -1, dtype=torch.int64, device=dev)
         self.acc_g = torch.zeros(self.ring * self.nslots, dtype=torch.int64, device=dev)
         self.cnt_g = torch.zeros(self.ring * self.nslots, dtype=torch.int32, device=dev)
         self.dirty_g = torch.zeros(self.ring * self.nslots, dtype=torch.uint8, device=dev)
@@ -401,6 +422,7 @@ class KeyedWindowOperator:
 
     _local_global_ok = True  # subclasses whose fire is not a plain reduce opt out
     _narrow_ok = True        # subclasses whose records carry more than (key, value) opt out
+    _dense_ok = True         # subclasses with their own aggregation kernel opt out
 
     @property
     def compact(self) -> bool:
@@ -686,7 +708,7 @@ class KeyedWindowOperator:
             window_mode=1, drop_late=int(event_mode), hash_mode=self.hash_mode,
             bucket_cap=self.bucket_cap, late_ts=self._late_ts(f.old_wm),
             tbase=self.pane_start(f.pane_base), pane=self.pane,
-            rec_words=self.rec_w)
+            rec_words=self.rec_w, dense_bits=self.dense_bits, dense_mul=self.dense_mul)
         f.rw = self.rec_w
         with self._stage("partition"):
             if f.n:
@@ -811,6 +833,7 @@ class KeyedWindowOperator:
                                   np_step=b.np_step, pg=b.pg, pane_base=b.pane_base,
                                   p_lo=b.qmin, fired_hi=b.fired_hi, combined=combined,
                                   rec_words=3 if combined else b.rw)
+                aplan.dense_bits, aplan.dense_mul = self.dense_bits, self.dense_mul
                 if self.dlist is not None:
                     aplan.dlist, aplan.dlist_n = self.dlist.data_ptr(), self.dlist_n.data_ptr()
                     aplan.slot_mark = self.slot_mark.data_ptr()
@@ -1056,6 +1079,8 @@ class KeyedWindowOperator:
 
     def num_keys(self) -> int:
         self._sync_state()
+        if self.dense_bits:  # no insertion: keys with data in a live pane
+            return int((self.cnt_g.view(self.ring, self.nslots) > 0).any(0).sum().item())
         return int(self.occ.sum().item())
 
     def _sync_state(self) -> None:
@@ -1136,7 +1161,8 @@ class KeyedWindowOperator:
             self.acc_g = torch.zeros(self.ring * self.nslots, dtype=torch.int64, device=dev)
             self.cnt_g = torch.zeros(self.ring * self.nslots, dtype=torch.int32, device=dev)
             self.dirty_g = torch.zeros(self.ring * self.nslots, dtype=torch.uint8, device=dev)
-        self.keys_g.fill_(-1)
+        if not self.dense_bits:
+            self.keys_g.fill_(-1)
         if self.dlist is not None:
             self.dlist_n.zero_()
             self.slot_mark.zero_()
@@ -1148,8 +1174,13 @@ class KeyedWindowOperator:
             return
         keys = torch.from_numpy(np.ascontiguousarray(rows["key"])).to(dev)
         uniq, inv = torch.unique(keys, return_inverse=True)
-        slots_u = K.table_insert(uniq.contiguous(), self.keys_g, nsub_log2=self.nsub_log2,
-                                 cap_log2=self.cap_log2)
+        if self.dense_bits:
+            if bool((uniq >> self.dense_bits).any()):
+                raise RuntimeError("restore: key id outside the dense key space (raise max_keys)")
+            slots_u = (uniq * self.dense_mul) & ((1 << self.dense_bits) - 1)
+        else:
+            slots_u = K.table_insert(uniq.contiguous(), self.keys_g, nsub_log2=self.nsub_log2,
+                                     cap_log2=self.cap_log2)
         if bool((slots_u < 0).any()):
             raise RuntimeError("restore: keyed state does not fit the table (raise max_keys)")
         slot = slots_u[inv]

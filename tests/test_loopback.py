@@ -391,3 +391,32 @@ def test_idle_partition_does_not_hold_the_watermark(dev, exchange):
     assert len(ref_during) > len(_collect([])) and live_during == ref_during
     assert live_total == ref_total == held_total
     assert len(held_during) < len(ref_during)  # the quiet partition held the valve back
+
+
+@pytest.mark.parametrize("dev", _devices())
+@pytest.mark.parametrize("world", [1, 4])
+def test_dense_keys_local_global_invariant(dev, world):
+    """Dense key ids (directly addressed local tables) under local-global aggregation: the
+    per-window results at G ranks equal one hashed-table rank's."""
+    _skip_no_gpu(dev)
+    per, nkeys, cap_log2 = _sizes(dev)
+
+    def rank_fn(comm):
+        op = KeyedWindowOperator(size=3000, slide=1000, agg=K.AGG_SUM_I64, device=dev, comm=comm,
+                                 max_keys=nkeys, batch_capacity=per, ooo_bound=500,
+                                 dense_keys=True, exchange="partials")
+        out = []
+        for step in range(STEPS):
+            out += op.process(*_batch(dev, comm.rank, step, per, nkeys))
+        return _collect(out + op.finish())
+
+    merged = {}
+    for d in run_loopback(world, rank_fn, device=torch.device(dev)):
+        merged.update(d)
+    ref_op = KeyedWindowOperator(size=3000, slide=1000, agg=K.AGG_SUM_I64, device=dev,
+                                 max_keys=nkeys, batch_capacity=per * world, ooo_bound=500,
+                                 cap_log2=cap_log2)
+    out = []
+    for step in range(STEPS):
+        out += ref_op.process(*_concat(dev, world, step, per, nkeys))
+    assert merged == _collect(out + ref_op.finish())

@@ -215,3 +215,39 @@ def test_narrow_records_match_wide(big):
     assert rw_wide == 3
     assert rw_nar == {"none": 1, "value": 2, "key": 2, "int32": 3}[big]
     assert nar == wide
+
+
+@pytest.mark.parametrize("size,slide,lateness", [(2000, 2000, 0), (3000, 1000, 1500)])
+def test_dense_keys_match_hashed(size, slide, lateness):
+    """dense_keys=True (ids < max_keys directly addressed through a bijective slot map, no
+    hash-table probe) fires exactly the windows of the hashed tables; an id outside the dense
+    key space reports a full table."""
+    import torch
+
+    from mxstream.ops import kernels as K
+    from mxstream.runtime.window_operator import KeyedWindowOperator
+
+    def run(dense, bad=False):
+        op = KeyedWindowOperator(size=size, slide=slide, lateness=lateness, agg=K.AGG_SUM_I64,
+                                 device="cpu", max_keys=3000, batch_capacity=5000, ooo_bound=300,
+                                 dense_keys=dense, cap_log2=8)
+        out = []
+        for step in range(7):
+            k = torch.empty(5000, dtype=torch.int64)
+            t = torch.empty_like(k)
+            v = torch.empty_like(k)
+            K.gen_events(k, t, v, seed=13, stream_id=0, idx0=step * 5000, nkeys=3000,
+                         ts_base=step * 1000, ts_span=1000, disorder=400, val_lo=0, val_span=1000)
+            if step > 3:
+                t[:200] -= 1200
+            if bad and step == 2:
+                k[3] = 1 << 20
+            out += op.process(k, t, v)
+        out += op.finish()
+        assert not dense or op.num_keys() >= 0
+        return sorted((r.window_start, r.refire, int(a), int(b), int(c))
+                      for r in out for a, b, c in zip(r.keys, r.raw, r.counts))
+
+    assert run(True) == run(False)
+    with pytest.raises(RuntimeError, match="table full"):
+        run(True, bad=True)
