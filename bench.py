@@ -39,6 +39,8 @@ def main() -> int:
     ap.add_argument("--keys", type=int, default=1_000_000)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--cap-log2", type=int, default=None, help="sub-table size (experiments)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="unpipelined step (host sync between the partition and the aggregation)")
     ap.add_argument("--hashed-keys", action="store_true",
                     help="hash-table state for arbitrary int64 keys instead of dense dictionary ids")
     ap.add_argument("--trace", default=None,
@@ -66,7 +68,8 @@ def main() -> int:
         device = torch.device("cpu")
 
     cfg = TumblingBenchConfig(keys=a.keys, batch=a.batch, cap_log2=a.cap_log2,
-                              dense_keys=not a.hashed_keys)
+                              dense_keys=not a.hashed_keys,
+                              pipeline=False if a.no_pipeline else None)
     bench = TumblingWindowBench(cfg, comm, device)
     if a.trace:
         from mxstream.utils import trace

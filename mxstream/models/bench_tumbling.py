@@ -34,11 +34,11 @@ class TumblingBenchConfig:
     val_max: int = 20_000            # bytes per event ~ U[0, val_max)
     seed: int = 1234
     alert_fraction: float = 0.92     # alert when Mbps < fraction * expected Mbps
-    # Partition of step i+1 overlaps the state half (combiner, all-to-all, aggregation, firing)
-    # of step i. None = on when there is an exchange to hide (G > 1). At G = 1 the two halves
-    # are both HBM-bound and overlapping them measured slower (0.45 -> 0.75 ms/step,
-    # profiles/r2_pipeline_g1.md).
-    pipeline: bool | None = None
+    # Step pipelining (KeyedWindowOperator): "stream" = partition of step i+1 enqueued ahead of
+    # the state half of step i on one stream (hides the host's per-step sync); True = state
+    # half on a second stream (hides a per-step exchange; measured slower at G = 1 with the
+    # hashed tables, profiles/r2_pipeline_g1.md). None = "stream".
+    pipeline: bool | str | None = None
     exchange: str = "auto"           # G > 1: "partials" (local-global) or "records"
     cap_log2: int | None = None      # sub-table size override (experiments)
     # Channel keys arrive as dictionary ids (the source interns strings, SURVEY.md F-ser), i.e.
@@ -60,7 +60,7 @@ class TumblingWindowBench:
             max_keys=cfg.keys, parallelism=world, batch_capacity=cfg.batch,
             ooo_bound=cfg.disorder_ms, map_prog=E.compile_expr(mbps),
             filter_prog=E.compile_expr(E.var(E.VAR_MAPPED) < self.threshold_mbps),
-            pipeline=(world > 1) if cfg.pipeline is None else cfg.pipeline,
+            pipeline="stream" if cfg.pipeline is None else cfg.pipeline,
             exchange=cfg.exchange, cap_log2=cfg.cap_log2, dense_keys=cfg.dense_keys)
         self.keys = torch.empty(cfg.batch, dtype=torch.int64, device=device)
         self.ts = torch.empty(cfg.batch, dtype=torch.int64, device=device)

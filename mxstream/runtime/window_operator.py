@@ -236,7 +236,7 @@ class KeyedWindowOperator:
                  clock: Callable[[], int] | None = None, external_watermark: bool = False,
                  combine: bool | None = None, compact: bool | None = None,
                  narrow: bool | None = None, dense_keys: bool = False,
-                 pipeline: bool | None = None, exchange: str = "auto",
+                 pipeline: bool | str | None = None, exchange: str = "auto",
                  idle_timeout_steps: int | None = None):
         self.device = K.resolve_device(device)
         self.comm = comm or LocalComm()
@@ -343,13 +343,21 @@ class KeyedWindowOperator:
         # G > 1: sender-side combiner before the all-to-all (all aggregates are associative).
         self.combine = (self._exchanging if combine is None
                         else bool(combine and self._exchanging))
-        # Pipelining: the partition of batch i+1 overlaps the state half of batch i (process()
-        # then returns the windows fired by the previous batch; flush() drains). Opt-in: the
-        # engine's hot loops (bench, configs) enable it; callers that need each batch's fires
-        # from its own call (DataStream API, external watermarks) keep the default.
-        self.pipeline = bool(pipeline) and not external_watermark and not self.local_global
-        self.s1 = (torch.cuda.Stream(dev) if self.pipeline and self.device.type == "cuda"
-                   else None)
+        # Pipelining: the partition of batch i+1 is enqueued before the state half of batch i
+        # (process() then returns the windows fired by the previous batch; flush() drains).
+        #   True:     the state half runs on a second stream, overlapping the partition (hides
+        #             the per-step exchange at G > 1);
+        #   "stream": one stream, deferred order  partition(i+1) | state half(i): the step's host
+        #             sync waits on partition(i+1)'s reduced vector while the GPU still works on
+        #             the state half of batch i, so the host's planning and launches never leave
+        #             the GPU idle (no second stream: no HBM contention between the halves).
+        # Opt-in: the engine's hot loops (bench, configs) enable it; callers that need each
+        # batch's fires from its own call (DataStream API, external watermarks) keep the default.
+        stream_mode = pipeline == "stream"
+        self.pipeline = (bool(pipeline) and not external_watermark
+                         and (stream_mode or not self.local_global))
+        self.s1 = (torch.cuda.Stream(dev) if self.pipeline and not stream_mode
+                   and self.device.type == "cuda" else None)
         self._par = 0
         self._pending: _Back | None = None
         self._carry: list[FireResult] = []  # fired by a flush a state reader forced

@@ -22,6 +22,7 @@ for step in "$@"; do
            st=$?; tail -3 "$out/pytest_gpu.log"; [ $st -eq 0 ] || [ $st -eq 1 ] || exit $st ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 || exit $? ;;
     bench) timeout -k 10 300 python bench.py --steps 48 --warmup 8 > "$out/bench.log" 2>&1 || exit $? ;;
+    bench_nopipe) timeout -k 10 300 python bench.py --steps 48 --warmup 8 --no-pipeline > "$out/bench_nopipe.log" 2>&1 || exit $? ;;
     bench_hashed) timeout -k 10 300 python bench.py --steps 48 --warmup 8 --hashed-keys > "$out/bench_hashed.log" 2>&1 || exit $? ;;
     prof_bench_hashed) prof bench_hashed python3 bench.py --steps 24 --warmup 6 --hashed-keys || exit $? ;;
     bench20) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "$out/bench20.log" 2>&1 || exit $? ;;

@@ -43,7 +43,7 @@ def main() -> int:
 
     def rank_fn(comm):
         b = TumblingWindowBench(TumblingBenchConfig(keys=a.keys, batch=a.batch,
-                                                    pipeline=not a.no_pipeline,
+                                                    pipeline=False if a.no_pipeline else "stream",
                                                     exchange=a.exchange), comm, dev)
         for _ in range(a.warmup):
             b.step()

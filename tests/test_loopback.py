@@ -62,7 +62,7 @@ def _skip_no_gpu(dev):
 @pytest.mark.parametrize("size,slide,lateness,exchange", [
     (3000, 3000, 0, "records"), (3000, 3000, 0, "partials"), (4000, 1000, 0, "partials"),
     (4000, 1000, 1500, "records")])
-@pytest.mark.parametrize("pipeline", [False, True])
+@pytest.mark.parametrize("pipeline", [False, True, "stream"])
 def test_window_invariant_to_world(dev, world, size, slide, lateness, exchange, pipeline):
     """pipeline=True: the partition of batch i+1 overlaps the combiner / all-to-all /
     aggregation / firing of batch i on a second stream (GPU); on the CPU twins the same
