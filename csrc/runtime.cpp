@@ -299,6 +299,7 @@ enum FieldKind : int {
   FK_TS_MS = 4,      // exact epoch millis of LocalDateTime.parse(x) at offset
   FK_INT = 5,        // Integer.parseInt -> i64
   FK_RAW_LONG = 6,   // epoch-ms integer field
+  FK_ISO_SEC = 7,    // (int) LocalDateTime.parse(x).toEpochSecond(off): int32 seconds
 };
 
 // Parse one line's fields into row `li` of the columns. String fields get a thread-local id
@@ -342,6 +343,12 @@ static void parse_line_into(std::string_view line, char sep,
         int64_t es, ms;
         parse_iso_local_datetime(v, offset_s, &es, &ms);
         ((int64_t*)ptrs[c])[li] = es * 1000LL + ms;
+        break;
+      }
+      case FK_ISO_SEC: {
+        int64_t es, ms;
+        parse_iso_local_datetime(v, offset_s, &es, &ms);
+        ((int64_t*)ptrs[c])[li] = (int64_t)(int32_t)(uint32_t)(uint64_t)es;
         break;
       }
       default: throw ParseError("unknown field kind");

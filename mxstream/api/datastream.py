@@ -78,7 +78,9 @@ class DataStream:
         return op
 
     def filter(self, fn) -> "SingleOutputStreamOperator":
-        return self._one_input("Filter", lambda: O.FilterOp(fn))
+        op = self._one_input("Filter", lambda: O.FilterOp(fn))
+        op.t.meta = {"kind": "filter", "fn": fn}
+        return op
 
     def flat_map(self, fn) -> "SingleOutputStreamOperator":
         return self._one_input("Flat Map", lambda: O.FlatMapOp(fn))
@@ -101,7 +103,9 @@ class DataStream:
 
     # -- time --
     def assign_timestamps_and_watermarks(self, assigner) -> "SingleOutputStreamOperator":
-        return self._one_input("Timestamps/Watermarks", lambda: O.TimestampsAndWatermarksOp(assigner))
+        op = self._one_input("Timestamps/Watermarks", lambda: O.TimestampsAndWatermarksOp(assigner))
+        op.t.meta = {"kind": "timestamps", "assigner": assigner}
+        return op
 
     # -- keyed --
     def key_by(self, *fields) -> "KeyedStream":

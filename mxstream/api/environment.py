@@ -194,18 +194,23 @@ class StreamExecutionEnvironment:
         return self
 
     # ---- sources ----
-    def _source(self, name: str, factory) -> DataStream:
+    def _source(self, name: str, factory, text: bool = False) -> DataStream:
         t = Transformation(next(_ids), name, "source", [], factory, 1)
+        # text: the source can emit raw line batches (planner: columnar text ingest)
+        t.meta = {"kind": "source", "text": text}
         return DataStream(self, t)
 
     def socket_text_stream(self, hostname: str, port: int, delimiter: str = "\n",
                            max_retry: int = 0) -> DataStream:
         return self._source("Socket Stream",
-                            lambda: S.SocketTextSource(hostname, port, delimiter, max_retry))
+                            lambda: S.SocketTextSource(hostname, port, delimiter, max_retry),
+                            text=delimiter == "\n")
 
     def from_collection(self, values, batch_size: int | None = None) -> DataStream:
         vals = list(values)
-        return self._source("Collection Source", lambda: S.CollectionSource(vals, batch_size))
+        return self._source("Collection Source", lambda: S.CollectionSource(vals, batch_size),
+                            text=bool(vals) and all(isinstance(v, str) and "\n" not in v
+                                                    for v in vals))
 
     def from_elements(self, *values) -> DataStream:
         return self.from_collection(values)
@@ -213,10 +218,13 @@ class StreamExecutionEnvironment:
     def from_timed_collection(self, timed, end_time: int | None = None) -> DataStream:
         """[(processing_time_ms, value), ...] arriving one per micro-batch at those times."""
         items = list(timed)
-        return self._source("Timed Source", lambda: S.TimedCollectionSource(items, end_time))
+        return self._source("Timed Source", lambda: S.TimedCollectionSource(items, end_time),
+                            text=bool(items) and all(isinstance(v, str) and "\n" not in v
+                                                     for _, v in items))
 
     def read_text_file(self, path: str) -> DataStream:
-        return self._source("Text File Source", lambda: S.TextFileSource(path, self.config.batch_size))
+        return self._source("Text File Source", lambda: S.TextFileSource(path, self.config.batch_size),
+                            text=True)
 
     def generate_sequence(self, start: int, end: int) -> DataStream:
         return self._source("Sequence Source", lambda: S.SequenceSource(start, end))

@@ -79,6 +79,63 @@ def trace_fieldwise_reduce(fn, arity: int) -> int | None:
     return summed
 
 
+def trace_avg_aggregate(fn, arity: int) -> int | None:
+    """Recognise a user AggregateFunction computing the average of one numeric field with a
+    (count, sum) accumulator (ComputeCpuAvg.java:31-58): `add` traced symbolically must be
+    "count + 1, sum + value.f<p>" (in either accumulator order), and `get_result` / `merge`
+    checked on concrete accumulators (get_result branches on count == 0, which no trace
+    expresses). Returns p, or None."""
+    from .functions import AggregateFunction
+
+    if not isinstance(fn, AggregateFunction):
+        return None
+    try:
+        acc0 = fn.create_accumulator()
+        if not isinstance(acc0, tuple) or len(acc0) != 2 or any(x != 0 for x in acc0):
+            return None
+
+        class Row(tuple):
+            def __getattr__(self, name):
+                if name.startswith("f") and name[1:].isdigit():
+                    return self[int(name[1:])]
+                raise AttributeError(name)
+
+        out = fn.add(Row([E.var(i) for i in range(arity)]), Row([E.var(100), E.var(101)]))
+        if not isinstance(out, tuple) or len(out) != 2:
+            return None
+        cnt_i = sum_i = field = None
+        for i, f in enumerate(out):
+            if not isinstance(f, E.Expr) or f.op != "+" or len(f.args) != 2:
+                return None
+            a, b = f.args
+            names = {x.value for x in (a, b) if x.op == "var"}
+            consts = [x.value for x in (a, b) if x.op == "const"]
+            if names == {100 + i} and consts == [1.0]:
+                cnt_i = i
+            elif len(names) == 2 and 100 + i in names and all(x.op == "var" for x in (a, b)):
+                sum_i, field = i, (names - {100 + i}).pop()
+            else:
+                return None
+        if cnt_i is None or sum_i is None or not 0 <= field < arity:
+            return None
+        T = type(acc0)
+
+        def mk(c, sm):
+            v = [0, 0]
+            v[cnt_i], v[sum_i] = c, sm
+            return T(v)
+        for c, sm in ((0, 0.0), (3, 6.0), (7, 10.5), (2, -3.0), (5, 1e300)):
+            want = 0.0 if c == 0 else sm / c
+            if fn.get_result(mk(c, sm)) != want:
+                return None
+        m = fn.merge(mk(2, 1.5), mk(3, 4.0))
+        if tuple(m) != tuple(mk(5, 5.5)):
+            return None
+        return field
+    except Exception:
+        return None
+
+
 def _consumers(sinks):
     from ..runtime.executor import Executor
 
@@ -112,9 +169,66 @@ def _dead_fields_ok(t: Transformation, children, key_pos: int, val_pos: int, ari
     return not (probe.used & keep)
 
 
+def _lower_text(env, sinks) -> None:
+    """Columnar text ingest: source(text) -> [timestamps] -> map(parse) -> [filter] becomes one
+    TextParseOp fed by raw line batches, when the map (and extractor / filter) trace
+    (api/textplan.py). The filter node stays in the graph as a pass-through."""
+    from ..runtime.columnar import PassThroughOp, TextParseOp
+    from . import textplan as T
+
+    nodes, children = _consumers(sinks)
+    for t in nodes:
+        meta = getattr(t, "meta", None) or {}
+        if meta.get("kind") != "map" or meta.get("columnar") or len(t.parents) != 1:
+            continue
+        parent, ts_node = t.parents[0], None
+        pmeta = getattr(parent, "meta", None) or {}
+        if pmeta.get("kind") == "timestamps" and len(parent.parents) == 1:
+            ts_node, parent = parent, parent.parents[0]
+            pmeta = getattr(parent, "meta", None) or {}
+        if parent.kind != "source" or not pmeta.get("text"):
+            continue
+        if len(children[parent.id]) != 1 or (ts_node is not None and len(children[ts_node.id]) != 1):
+            continue
+        try:
+            spec = T.trace_text_map(meta["fn"])
+            ts_spec, bound = None, 0
+            if ts_node is not None:
+                a = ts_node.meta["assigner"]
+                ts_spec = T.trace_extractor(a)
+                bound = a.get_max_out_of_orderness_in_millis()
+        except T.TraceError:
+            continue
+        filt, fnode = None, None
+        kids = children[t.id]
+        if len(kids) == 1 and (getattr(kids[0], "meta", None) or {}).get("kind") == "filter" \
+                and (kids[0].parallelism or env.parallelism) == (t.parallelism or env.parallelism):
+            try:
+                filt = T.trace_tuple_filter(kids[0].meta["fn"], tuple(k for _, k in spec.fields))
+                fnode = kids[0]
+            except T.TraceError:
+                filt = None
+        t.factory = (lambda spec=spec, ts_spec=ts_spec, bound=bound, filt=filt:
+                     TextParseOp(spec, ts_spec=ts_spec, bound=bound, filter_prog=filt))
+        t.parents = [parent]
+        if fnode is not None:
+            fnode.factory = PassThroughOp
+            fnode.meta = dict(fnode.meta, fused=True)
+        src_factory = parent.factory
+
+        def columnar_source(f=src_factory):
+            s = f()
+            s.columnar = True
+            return s
+
+        parent.factory = columnar_source
+        t.meta = dict(meta, columnar=True, text_spec=spec)
+
+
 def plan(env, sinks):
     if env.config.native == "off":
         return sinks
+    _lower_text(env, sinks)
     nodes, children = _consumers(sinks)
     for t in nodes:
         meta = getattr(t, "meta", None) or {}
@@ -149,6 +263,15 @@ def plan(env, sinks):
             kind, val_pos = spec.fn.native
             result = "value"
             ok_arities = set(range(max(key_pos, val_pos) + 1, 64))
+        elif spec.kind == "aggregate" and spec.window_fn is None and not session:
+            # A user AggregateFunction: the (count, sum) average of one field?
+            for ar in range(2, 9):
+                if ar <= key_pos:
+                    continue
+                p = trace_avg_aggregate(spec.fn, ar)
+                if p is not None and p != key_pos:
+                    kind, val_pos, result = "avg", p, "value"
+                    ok_arities.add(ar)
         elif spec.kind == "process" and getattr(spec.fn, "native", (None,))[0] == "median" \
                 and not session:
             kind, val_pos = "median", spec.fn.native[1]
@@ -169,7 +292,115 @@ def plan(env, sinks):
             continue
         _install_native(env, t, ws, spec, key_pos, val_pos, kind, result, ok_arities,
                         session=session)
+        if not session and kind in ("sum", "min", "max") and result == "tuple":
+            _fuse_window_epilogue(env, t, children, key_pos, val_pos, ok_arities)
     return sinks
+
+
+def _expr_vars(e) -> set:
+    if e.op == "var":
+        return {e.value}
+    return set().union(*(_expr_vars(a) for a in e.args)) if e.args else set()
+
+
+def _fuse_window_epilogue(env, t, children, key_pos: int, val_pos: int, ok_arities) -> None:
+    """window(reduce/sum/min/max) -> map -> [filter] (BandwidthMonitorWithEventTime.java:46-55):
+    the map and filter are traced over the window's output tuple (the aggregate as
+    VAR_RESULT, other fields passed through by name) and run inside the fire kernel's epilogue;
+    only the rows that pass leave the device. The map / filter nodes become pass-throughs."""
+    from ..runtime.columnar import PassThroughOp
+    from .functions import FilterFunction, MapFunction
+
+    par = lambda n: n.parallelism or env.parallelism  # noqa: E731
+    kids = children.get(t.id, [])
+    if len(kids) != 1:
+        return
+    m = kids[0]
+    mmeta = getattr(m, "meta", None) or {}
+    spec = None
+    for p in t.parents:
+        spec = (getattr(p, "meta", None) or {}).get("text_spec") or spec
+    arity = spec.arity if spec is not None else (next(iter(ok_arities)) if len(ok_arities) == 1 else None)
+    if arity is None or arity not in ok_arities or par(m) != par(t):
+        return
+    if mmeta.get("kind") == "filter" and not mmeta.get("fused"):
+        # window -> filter (BandwidthMonitor.java:37-39): the predicate over the aggregate runs
+        # in the fire kernel.
+        ff = mmeta["fn"]
+        try:
+            row = [E.var(E.VAR_RESULT) if i == val_pos else E.FieldRef(f"f{i}") for i in range(arity)]
+            r = E.trace_row_fn(ff.filter if isinstance(ff, FilterFunction) else ff, row)
+        except E.TraceError:
+            return
+        if not isinstance(r, E.Expr) or not _expr_vars(r) <= {E.VAR_RESULT}:
+            return
+        inner, prog = t.factory, E.compile_expr(r)
+
+        def ffactory(inner=inner, prog=prog):
+            op = inner()
+            op.filter_prog = prog
+            return op
+
+        t.factory = ffactory
+        m.factory = PassThroughOp
+        m.meta = dict(mmeta, fused=True)
+        return
+    if mmeta.get("kind") != "map" or mmeta.get("columnar"):
+        return
+    fn = mmeta["fn"]
+    try:
+        row = [E.var(E.VAR_RESULT) if i == val_pos else E.FieldRef(f"f{i}") for i in range(arity)]
+        out = E.trace_row_fn(fn.map if isinstance(fn, MapFunction) else fn, row)
+        from .tuples import Tuple
+
+        comps = list(out) if isinstance(out, Tuple) else [out]
+        layout, exprs = [], []
+        for c in comps:
+            if isinstance(c, E.FieldRef):
+                layout.append(int(c.name[1:]))
+            elif isinstance(c, E.Expr):
+                if not _expr_vars(c) <= {E.VAR_RESULT}:
+                    return
+                layout.append(-1)
+                exprs.append(c)
+            else:
+                return
+        if len(exprs) > 1:
+            return
+        map_prog = E.compile_expr(exprs[0]) if exprs else E.EMPTY
+        filt_prog, fnode = E.EMPTY, None
+        mk = children.get(m.id, [])
+        if len(mk) == 1 and (getattr(mk[0], "meta", None) or {}).get("kind") == "filter" \
+                and par(mk[0]) == par(m):
+            ff = mk[0].meta["fn"]
+            row2 = [E.var(E.VAR_MAPPED) if j < 0 else E.FieldRef(f"f{j}") for j in layout]
+            try:
+                r2 = E.trace_row_fn(ff.filter if isinstance(ff, FilterFunction) else ff,
+                                    row2 if isinstance(out, Tuple) else [E.var(E.VAR_MAPPED)])
+                if not isinstance(out, Tuple):
+                    r2 = ff.filter(E.var(E.VAR_MAPPED)) if isinstance(ff, FilterFunction) else ff(E.var(E.VAR_MAPPED))
+                if isinstance(r2, E.Expr) and _expr_vars(r2) <= {E.VAR_MAPPED, E.VAR_RESULT}:
+                    filt_prog, fnode = E.compile_expr(r2), mk[0]
+            except E.TraceError:
+                pass
+    except E.TraceError:
+        return
+    inner = t.factory
+    scalar = not isinstance(out, Tuple)
+
+    def factory(inner=inner, map_prog=map_prog, filt_prog=filt_prog, layout=tuple(layout)):
+        op = inner()
+        op.map_prog, op.filter_prog = map_prog, filt_prog
+        op.fused_layout = None if scalar else layout
+        op.fused_scalar = scalar
+        return op
+
+    t.factory = factory
+    m.factory = PassThroughOp
+    m.meta = dict(mmeta, fused=True)
+    if fnode is not None:
+        fnode.factory = PassThroughOp
+        fnode.meta = dict(fnode.meta, fused=True)
 
 
 def _install_native(env, t, ws, spec, key_pos, val_pos, kind, result, ok_arities,

@@ -160,6 +160,8 @@ class Executor:
 
     def _push(self, inbox: dict[int, list], now: int | None) -> None:
         """One pass over the DAG in topological order."""
+        from .columnar import expand_columns, rows_in
+
         for n in self.nodes:
             if n.kind == "source":
                 out = inbox.pop(n.id, [])
@@ -173,6 +175,8 @@ class Executor:
                 for p in n.parents:
                     items.extend(inbox.pop((n.id, p.id), []))
                 op = self.ops[n.id]
+                if not getattr(op, "accepts_columns", False):
+                    items = expand_columns(items)
                 if self.fault is not None and items:
                     self._maybe_fault(n, items)
                 if items and self._trace:
@@ -184,8 +188,8 @@ class Executor:
                     out.extend(op.on_processing_time(now))
                 if items or out:
                     c = self._counts.setdefault(n.id, {"numRecordsIn": 0, "numRecordsOut": 0})
-                    c["numRecordsIn"] += sum(1 for it in items if isinstance(it, Rec))
-                    c["numRecordsOut"] += sum(1 for it in out if isinstance(it, Rec))
+                    c["numRecordsIn"] += rows_in(items)
+                    c["numRecordsOut"] += rows_in(out)
             for c in self.children[n.id]:
                 if c.kind == "side":
                     side = [it for it in self.ops[n.id].take_side(c.side_tag.tag_id)] \
@@ -288,7 +292,9 @@ class Executor:
         f = self.fault
         if f is None or self.attempt >= f[2] or f[0] not in node.name:
             return
-        self._fault_count += sum(1 for it in items if isinstance(it, Rec))
+        from .columnar import rows_in
+
+        self._fault_count += rows_in(items)
         if self._fault_count >= f[1]:
             raise InjectedFault(f"injected fault in {node.name} after {self._fault_count} records"
                                 f" (attempt {self.attempt})")
@@ -387,11 +393,16 @@ class Executor:
         p = child.parallelism or self.env.parallelism
         key = (src.id, child.id)
         nxt = self._rr.get(key, self.env.config.rebalance_start)
+        from .columnar import TextBatch
+
         out = []
         for it in items:
             if isinstance(it, Rec):
                 out.append(Rec(it.value, it.ts, nxt % p))
                 nxt += 1
+            elif isinstance(it, TextBatch):
+                out.append(TextBatch(it.data, it.n, nxt % p, p))
+                nxt += it.n
             else:
                 out.append(it)
         self._rr[key] = nxt
@@ -410,6 +421,10 @@ class Executor:
                 for p in n.parents:
                     items.extend(inbox.pop((n.id, p.id), []))
                 op = self.ops[n.id]
+                if not getattr(op, "accepts_columns", False):
+                    from .columnar import expand_columns
+
+                    items = expand_columns(items)
                 out = op.process(items) if items else []
                 out.extend(op.finish())
             for c in self.children[n.id]:

@@ -15,14 +15,76 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from ..api.tuples import Tuple
+from ..ops import expr as E
 from ..ops import kernels as K
+from ..ops.text import FK_DOUBLE, FK_STR
 from ..utils.hashing import java_hash
+from .columnar import ColumnBatch, expand_columns
 from .operators import LONG_MAX, LONG_MIN, Operator, Rec, WM, WindowOp
 from .window_operator import KeyedWindowOperator
 
 
-class NativeWindowOp(Operator):
+class _ColumnInput:
+    """Columnar input for the native keyed operators: a ColumnBatch's key column (dense
+    dictionary ids of string keys, or integer keys) and value column go to the engine as they
+    are; only keys seen for the first time build a keep-first template tuple."""
+
+    def _cb_keys(self, cb: ColumnBatch) -> np.ndarray:
+        kp = self.key_pos
+        kk = cb.kinds[kp]
+        col = cb.cols[kp]
+        if kk == FK_STR:
+            if self.str_keys is False:
+                raise TypeError("mixed key types")
+            self.str_keys = True
+            if cb.strings is not self.dict:
+                if len(self.dict) == 0 and not self.templates:
+                    self.dict = cb.strings  # adopt the parser's dictionary: ids are shared
+                else:
+                    u, inv = np.unique(col, return_inverse=True)
+                    names = cb.strings.strings()
+                    ids = np.array([self.dict.intern(names[x]) for x in u.tolist()], dtype=np.int64)
+                    return ids[inv]
+            return col.astype(np.int64, copy=False)
+        if kk == FK_DOUBLE:
+            raise TypeError("double keys on the native path")
+        if self.str_keys is True:
+            raise TypeError("mixed key types")
+        self.str_keys = False
+        if col.size and (int(col.min()) < 0 or int(col.max()) >= (1 << 63) - 2):
+            raise TypeError("negative / reserved integer keys on the native path")
+        return col.astype(np.int64, copy=False)
+
+    def _cb_templates(self, cb: ColumnBatch, kid: np.ndarray) -> None:
+        u, first = np.unique(kid, return_index=True)
+        known = getattr(self, "_known", None)
+        if known is not None and known.size:
+            new = ~np.isin(u, known)
+            u, first = u[new], first[new]
+        if u.size:
+            for k, i in zip(u.tolist(), first.tolist()):
+                if k not in self.templates:
+                    self.templates[k] = cb.value(i)
+            self._known = u if known is None else np.union1d(known, u)
+
+    @staticmethod
+    def _cb_concat(batches: list) -> ColumnBatch:
+        if len(batches) == 1:
+            return batches[0]
+        b0 = batches[0]
+        if any(b.kinds != b0.kinds or b.strings is not b0.strings for b in batches):
+            raise TypeError("incompatible column batches")
+        cat = lambda xs: None if xs[0] is None else np.concatenate(xs)  # noqa: E731
+        return ColumnBatch(sum(b.n for b in batches),
+                           [np.concatenate([b.cols[j] for b in batches]) for j in range(len(b0.cols))],
+                           b0.kinds, b0.strings, cat([b.ts for b in batches]),
+                           cat([b.sub for b in batches]))
+
+
+class NativeWindowOp(_ColumnInput, Operator):
     name = "Window(native)"
+    accepts_columns = True
 
     def __init__(self, *, key_fn, key_pos: int, val_pos: int, kind: str, assigner, lateness: int,
                  late_tag, device: str, fallback_factory, map_prog=None, filter_prog=None,
@@ -39,6 +101,12 @@ class NativeWindowOp(Operator):
         self.result_builder = result_builder
         self.max_keys = max_keys
         self.ok_arities = ok_arities
+        # Fused post-window map/filter (planner._fuse_window_epilogue): evaluated in the fire
+        # kernel; fused_layout gives the output tuple (field index, or -1 = the mapped value).
+        self.map_prog, self.filter_prog = map_prog, filter_prog
+        self.fused_layout = None
+        self.fused_scalar = False
+        self._subs: dict = {}                 # key id -> output subtask
         self.op: KeyedWindowOperator | None = None
         self.fallback: WindowOp | None = None
         self.wm = LONG_MIN
@@ -54,7 +122,7 @@ class NativeWindowOp(Operator):
         self.str_keys = None
 
     # -- lazy construction on the first records (value type decides the aggregate kind) --
-    def _build(self, sample_val) -> bool:
+    def _build(self, sample_val, dense: bool = False) -> bool:
         is_float = isinstance(sample_val, float)
         if not isinstance(sample_val, (int, float)) or isinstance(sample_val, bool):
             return False
@@ -73,7 +141,9 @@ class NativeWindowOp(Operator):
             agg=agg, device=dev, max_keys=self.max_keys, parallelism=1,
             batch_capacity=max(1024, self.ctx.parallelism), cap_log2=cap_log2,
             time_mode="event" if event else "processing", external_watermark=True,
-            side_output_late=self.late_tag is not None, clock=self.ctx.clock)
+            side_output_late=self.late_tag is not None, clock=self.ctx.clock,
+            dense_keys=dense, map_prog=self.map_prog or E.EMPTY,
+            filter_prog=self.filter_prog or E.EMPTY)
         return True
 
     def _to_fallback(self):
@@ -93,15 +163,62 @@ class NativeWindowOp(Operator):
             return k
         raise TypeError("unsupported key type for the native path")
 
+    def _flush_columns(self, batches: list) -> list:
+        """All pending items are ColumnBatches: no per-record Python on the input side."""
+        try:
+            cb = self._cb_concat(batches)
+            vk = cb.kinds[self.val_pos]
+            if vk == FK_STR or (self.ok_arities and len(cb.kinds) not in self.ok_arities):
+                raise TypeError("value column not numeric")
+            if self.op is None:
+                dense = cb.kinds[self.key_pos] == FK_STR
+                if not self._build(1.0 if vk == FK_DOUBLE else 1, dense=dense):
+                    raise TypeError("unsupported value")
+            elif (vk == FK_DOUBLE) != self.is_float:
+                raise TypeError("mixed value types")
+            kid = self._cb_keys(cb)
+        except TypeError:
+            if self.templates:
+                raise
+            recs = expand_columns(batches)
+            self._to_fallback()
+            return self.fallback.process(recs)
+        self._cb_templates(cb, kid)
+        event = self.assigner.is_event_time()
+        if event:
+            tsa = cb.ts if cb.ts is not None else np.full(cb.n, LONG_MIN, dtype=np.int64)
+        else:
+            tsa = np.full(cb.n, self.ctx.clock(), dtype=np.int64)
+        vv = cb.cols[self.val_pos].astype(np.float64 if self.is_float else np.int64, copy=False)
+        dev = self.op.device
+        late_before = self.op.metrics.num_late_records_dropped
+        fired = self.op.process(torch.from_numpy(np.ascontiguousarray(kid)).to(dev),
+                                torch.from_numpy(np.ascontiguousarray(tsa, dtype=np.int64)).to(dev),
+                                torch.from_numpy(np.ascontiguousarray(vv).view(np.int64)).to(dev))
+        if getattr(self.op, "late_side", None):
+            for idx in np.concatenate(self.op.late_side).tolist():
+                sub = int(cb.sub[idx]) if cb.sub is not None else 0
+                ts = int(cb.ts[idx]) if cb.ts is not None else LONG_MIN
+                self.side.setdefault(self.late_tag.tag_id, []).append(Rec(cb.value(idx), ts, sub))
+            self.op.late_side.clear()
+        elif self.late_tag is None:
+            self.num_late_records_dropped += self.op.metrics.num_late_records_dropped - late_before
+        return self._emit(fired)
+
     def _flush(self) -> list:
         recs = self.pending
         self.pending = []
         if not recs:
             return []
+        if all(isinstance(r, ColumnBatch) for r in recs):
+            return self._flush_columns(recs)
+        recs = expand_columns(recs)
         if self.op is None:
             v0 = recs[0].value
+            dense = (isinstance(v0, tuple) and len(v0) > self.key_pos
+                     and isinstance(v0[self.key_pos], str))
             if (not isinstance(v0, tuple) or (self.ok_arities and len(v0) not in self.ok_arities)
-                    or not self._build(v0[self.val_pos])):
+                    or not self._build(v0[self.val_pos], dense=dense)):
                 self._to_fallback()
                 return self.fallback.process(recs)
         n = len(recs)
@@ -155,17 +272,25 @@ class NativeWindowOp(Operator):
                     res = int(cnt)
                 else:
                     res = float(val)
-                value = self.result_builder(self.templates[k], res, key_obj)
-                sub = java_hash(key_obj)
-                from ..utils.hashing import flink_murmur
+                if self.fused_scalar:
+                    value = float(val)
+                elif self.fused_layout is not None:
+                    tpl = self.templates[k]
+                    value = Tuple([float(val) if j < 0 else (res if j == self.val_pos else tpl[j])
+                                   for j in self.fused_layout])
+                else:
+                    value = self.result_builder(self.templates[k], res, key_obj)
+                sub = self._subs.get(k)
+                if sub is None:  # subtask of the key (Java hash + murmur): once per key
+                    from ..utils.hashing import flink_murmur
 
-                sub = (flink_murmur(sub) % MP) * P // MP
+                    sub = self._subs[k] = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
                 out.append(Rec(value, ts, sub))
         return out
 
     def process(self, items):
         if self.fallback is not None:
-            return self.fallback.process(items)
+            return self.fallback.process(expand_columns(items))
         out = []
         for it in items:
             if isinstance(it, WM):
@@ -222,7 +347,7 @@ class NativeWindowOp(Operator):
             self.dict.intern(st)
         eng = snap.get("engine")
         if eng is not None:
-            self._build(1.0 if eng["is_float"] else 1)
+            self._build(1.0 if eng["is_float"] else 1, dense=bool(self.str_keys))
             self.op.restore_state(eng["columns"], eng["meta"])
 
     def take_side(self, tag_id):
@@ -234,7 +359,7 @@ class NativeWindowOp(Operator):
 _ = LONG_MAX
 
 
-class NativeRollingOp(Operator):
+class NativeRollingOp(_ColumnInput, Operator):
     """``keyBy(k).sum/min/max(p)`` (StreamGroupedReduce + ComparableAggregator,
     ComputeCpuMax.java:26) on the native ``KeyedRollingOperator``: per micro-batch the records
     are columnarised, the GPU (or C++ twin) returns the post-update value of every record in
@@ -244,6 +369,7 @@ class NativeRollingOp(Operator):
     switches to the exact host RollingReduceOp."""
 
     name = "Keyed Aggregation"
+    accepts_columns = True
 
     def __init__(self, *, key_fn, key_pos: int, val_pos: int, kind: str, device: str,
                  fallback_factory, max_keys: int = 1 << 20):
@@ -296,9 +422,59 @@ class NativeRollingOp(Operator):
             return k
         raise TypeError("unsupported key type for the native path")
 
+    def _run_columns(self, batches: list) -> list:
+        """ColumnBatch input: key/value columns straight to the engine; the output (one row per
+        input record, Flink's rolling emit) is built per row only for the host sink."""
+        try:
+            cb = self._cb_concat(batches)
+            vk = cb.kinds[self.val_pos]
+            if vk == FK_STR or len(cb.kinds) <= max(self.key_pos, self.val_pos):
+                raise TypeError("value column not numeric")
+            if self.op is None:
+                if not self._build(1.0 if vk == FK_DOUBLE else 1):
+                    raise TypeError("unsupported value")
+            elif (vk == FK_DOUBLE) != self.is_float:
+                raise TypeError("mixed value types")
+            kid = self._cb_keys(cb)
+        except TypeError:
+            if self.templates:
+                raise
+            recs = expand_columns(batches)
+            self._to_fallback()
+            return self.fallback.process(recs)
+        self._cb_templates(cb, kid)
+        vv = cb.cols[self.val_pos].astype(np.float64 if self.is_float else np.int64, copy=False)
+        dev = self.op.device
+        rows = self.op.process(torch.from_numpy(np.ascontiguousarray(kid)).to(dev),
+                               torch.from_numpy(np.ascontiguousarray(vv).view(np.int64)).to(dev))
+        order = np.argsort(rows.tags & 0xFFFFFFFF, kind="stable")  # back to input order
+        from ..api.tuples import Tuple
+        from ..utils.hashing import flink_murmur
+
+        P, MP = self.ctx.parallelism, self.ctx.max_parallelism
+        keys = rows.keys[order].tolist()
+        vals = rows.values[order]
+        res = (vals.view(np.float64) if self.is_float else vals).tolist()
+        idx = (rows.tags[order] & 0xFFFFFFFF).tolist()
+        ts = cb.ts.tolist() if cb.ts is not None else None
+        subs: dict = {}
+        out = []
+        for k, r, i in zip(keys, res, idx):
+            row = list(self.templates[k])
+            row[self.val_pos] = r
+            sub = subs.get(k)
+            if sub is None:
+                key_obj = self.dict.get(k) if self.str_keys else k
+                sub = subs[k] = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
+            out.append(Rec(Tuple(row), ts[i] if ts is not None else LONG_MIN, sub))
+        return out
+
     def _run(self, recs: list) -> list:
         if not recs:
             return []
+        if all(isinstance(r, ColumnBatch) for r in recs):
+            return self._run_columns(recs)
+        recs = expand_columns(recs)
         if self.op is None:
             v0 = recs[0].value
             if not isinstance(v0, tuple) or len(v0) <= max(self.key_pos, self.val_pos) \
@@ -351,7 +527,7 @@ class NativeRollingOp(Operator):
 
     def process(self, items):
         if self.fallback is not None:
-            return self.fallback.process(items)
+            return self.fallback.process(expand_columns(items))
         out, pending = [], []
         for it in items:
             if isinstance(it, WM):
@@ -393,7 +569,7 @@ class NativeSessionOp(NativeWindowOp):
     ``KeyedSessionOperator`` (GPU slot table + host store, or the C++ store on CPU). Results are
     emitted at the session's maxTimestamp like Flink's WindowOperator."""
 
-    def _build(self, sample_val) -> bool:
+    def _build(self, sample_val, dense: bool = False) -> bool:
         from .session_operator import KeyedSessionOperator
 
         is_float = isinstance(sample_val, float)
@@ -437,7 +613,7 @@ class NativeMedianOp(NativeWindowOp):
     operator: elements stay on the device per pane, the fire sorts (key, value) with two radix
     passes and a kernel takes the per-key median."""
 
-    def _build(self, sample_val) -> bool:
+    def _build(self, sample_val, dense: bool = False) -> bool:
         from .list_window_operator import KeyedListWindowOperator
 
         if not isinstance(sample_val, float):
@@ -477,7 +653,7 @@ class NativeVectorWindowOp(NativeWindowOp):
 
     name = "VectorWindow(native)"
 
-    def _build(self, sample_val) -> bool:
+    def _build(self, sample_val, dense: bool = False) -> bool:
         if not isinstance(sample_val, (list, tuple)) or not sample_val \
                 or not all(isinstance(x, (int, float)) and not isinstance(x, bool)
                            for x in sample_val):
@@ -500,7 +676,7 @@ class NativeVectorWindowOp(NativeWindowOp):
         return True
 
     def _flush(self) -> list:
-        recs = self.pending
+        recs = expand_columns(self.pending)
         self.pending = []
         if not recs:
             return []

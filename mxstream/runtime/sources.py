@@ -23,6 +23,9 @@ from .operators import LONG_MIN, Rec, WM
 class Source:
     parallelism = 1
     name = "Source"
+    # Set by the planner when the consumer chain parses text columnar (runtime/columnar.py):
+    # text sources then emit one TextBatch of raw lines per poll instead of a Rec per line.
+    columnar = False
 
     def open(self, rank: int, world: int, clock) -> None:
         self.rank, self.world, self.clock = rank, world, clock
@@ -70,6 +73,12 @@ class CollectionSource(Source):
         if self.pos >= len(self.values):
             return [], True
         end = min(len(self.values), self.pos + self.batch)
+        if self.columnar and self.timestamps is None:
+            from .columnar import TextBatch
+
+            lines = self.values[self.pos:end]
+            self.pos = end
+            return [TextBatch("\n".join(lines).encode(), len(lines))], self.pos >= len(self.values)
         out = [Rec(v, self.timestamps[i] if self.timestamps else LONG_MIN)
                for i, v in zip(range(self.pos, end), self.values[self.pos:end])]
         self.pos = end
@@ -101,7 +110,13 @@ class TimedCollectionSource(Source):
     def poll(self, now):
         out = []
         while self.pos < len(self.timed) and self.timed[self.pos][0] <= now:
-            out.append(Rec(self.timed[self.pos][1]))
+            v = self.timed[self.pos][1]
+            if self.columnar:
+                from .columnar import TextBatch
+
+                out.append(TextBatch(v.encode(), 1))
+            else:
+                out.append(Rec(v))
             self.pos += 1
             break  # one line per micro-batch: a human typing into `nc`
         done = self.pos >= len(self.timed) and now >= self.end_time
@@ -119,13 +134,56 @@ class TextFileSource(Source):
 
     def open(self, rank, world, clock):
         super().open(rank, world, clock)
+        if self.columnar:
+            # K18: the file is split into one contiguous newline-aligned byte range per rank,
+            # read in batches of ~batch lines without building Python strings.
+            with open(self.path, "rb") as f:
+                data = f.read()
+            lo, hi = (len(data) * rank) // world, (len(data) * (rank + 1)) // world
+            if rank:
+                j = data.find(b"\n", lo - 1) if lo else 0
+                lo = len(data) if j < 0 else j + 1
+            if rank + 1 < world:
+                j = data.find(b"\n", hi - 1)
+                hi = len(data) if j < 0 else j + 1
+            self.data = memoryview(data)[lo:max(lo, hi)]
+            self.bpos = 0
+            return
         with open(self.path, "r", encoding="utf-8") as f:
             lines = f.read().split("\n")
         if lines and lines[-1] == "":
             lines.pop()
         self.lines = [l[:-1] if l.endswith("\r") else l for l in lines][rank::world]
 
+    def snapshot(self) -> dict:
+        return {"bpos": self.bpos} if self.columnar else super().snapshot()
+
+    def restore(self, snap: dict) -> None:
+        if self.columnar and "bpos" in snap:
+            self.bpos = snap["bpos"]
+        else:
+            super().restore(snap)
+
     def poll(self, now):
+        if self.columnar:
+            from .columnar import TextBatch
+
+            d = self.data
+            if self.bpos >= len(d):
+                return [], True
+            end = min(len(d), self.bpos + self.batch * 48)  # ~batch lines of a metric log
+            if end < len(d):
+                j = bytes(d[end - 1:end]) == b"\n"
+                if not j:
+                    k = bytes(d[end:min(len(d), end + 4096)]).find(b"\n")
+                    while k < 0 and end < len(d):
+                        end = min(len(d), end + 4096)
+                        k = bytes(d[end:min(len(d), end + 4096)]).find(b"\n")
+                    end = len(d) if k < 0 else end + k + 1
+            chunk = bytes(d[self.bpos:end])
+            self.bpos = end
+            n = chunk.count(b"\n") + (0 if chunk.endswith(b"\n") else 1)
+            return [TextBatch(chunk, n)], self.bpos >= len(d)
         end = min(len(self.lines), self.pos + self.batch)
         out = [Rec(l) for l in self.lines[self.pos:end]]
         self.pos = end
@@ -183,6 +241,10 @@ class SocketTextSource(Source):
         if err:
             raise ConnectionError(err)
         out = []
+        if n and self.columnar:
+            from .columnar import TextBatch
+
+            return [TextBatch(bytes(data), int(n))], bool(eof)
         if n:
             text = data.decode("utf-8", errors="replace")
             parts = text.split("\n")[:n]
