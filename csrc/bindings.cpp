@@ -211,6 +211,68 @@ PYBIND11_MODULE(_mxs_native, m) {
     return expr_eval_chain(p, va);
   });
 
+  // ---- Hot path of the keyed window operator --------------------------------------------
+  // Plans as native objects (built once from the dict form, mutated per step: no per-call dict
+  // parsing) and one call per step half: step_begin + partition + step_finish, and the
+  // aggregation. `gpu` selects the HIP launchers or the C++ twins. Buffers are the operator's
+  // own (validated when allocated); the caller checks the batch columns.
+  py::class_<PartPlan>(m, "PartPlanObj")
+      .def(py::init(&make_part))
+      .def_readwrite("late_ts", &PartPlan::late_ts)
+      .def_readwrite("tbase", &PartPlan::tbase)
+      .def_readwrite("rec_words", &PartPlan::rec_words)
+      .def_readwrite("bucket_cap", &PartPlan::bucket_cap)
+      .def_readwrite("drop_late", &PartPlan::drop_late);
+  py::class_<AggPlan>(m, "AggPlanObj")
+      .def(py::init(&make_agg))
+      .def_readwrite("bucket_cap", &AggPlan::bucket_cap)
+      .def_readwrite("np_step", &AggPlan::np_step)
+      .def_readwrite("pg", &AggPlan::pg)
+      .def_readwrite("pane_base", &AggPlan::pane_base)
+      .def_readwrite("p_lo", &AggPlan::p_lo)
+      .def_readwrite("fired_hi", &AggPlan::fired_hi)
+      .def_readwrite("rec_words", &AggPlan::rec_words)
+      .def_readwrite("ring", &AggPlan::ring)
+      .def_readwrite("nsrc", &AggPlan::nsrc)
+      .def_readwrite("combined", &AggPlan::combined);
+  m.def("window_front", [](bool gpu, intptr_t keys, intptr_t ts, intptr_t vals, intptr_t jhash,
+                           int64_t n, const PartPlan& p, intptr_t kg_dest, intptr_t cursor,
+                           intptr_t out, intptr_t stats, intptr_t late_idx, uint32_t late_cap,
+                           intptr_t local_maxts, int64_t bound, int32_t event_mode,
+                           int64_t proc_now, intptr_t red, intptr_t flags, intptr_t stream) {
+    const int nb = p.nranks << p.nsub_log2;
+    py::gil_scoped_release nogil;  // loopback ranks are threads of one process
+    if (gpu) {
+      gpu::step_begin(P<uint32_t>(cursor), nb, P<int64_t>(stats), stream);
+      if (n)
+        gpu::partition(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), P<int32_t>(jhash), n,
+                       p, P<int32_t>(kg_dest), P<uint32_t>(cursor), P<Rec>(out), P<int64_t>(stats),
+                       P<uint32_t>(late_idx), late_cap, stream);
+      gpu::step_finish(P<int64_t>(stats), P<int64_t>(local_maxts), bound, event_mode, proc_now,
+                       P<int64_t>(red), P<uint32_t>(flags), stream);
+    } else {
+      cpu::step_begin(P<uint32_t>(cursor), nb, P<int64_t>(stats));
+      if (n)
+        cpu::partition(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), P<int32_t>(jhash), n,
+                       p, P<int32_t>(kg_dest), P<uint32_t>(cursor), P<Rec>(out), P<int64_t>(stats),
+                       P<uint32_t>(late_idx), late_cap);
+      cpu::step_finish(P<int64_t>(stats), P<int64_t>(local_maxts), bound, event_mode, proc_now,
+                       P<int64_t>(red), P<uint32_t>(flags));
+    }
+  });
+  m.def("window_agg_obj", [](bool gpu, intptr_t recs, intptr_t counts, const AggPlan& p,
+                             intptr_t keys_g, intptr_t acc_g, intptr_t cnt_g, intptr_t dirty_g,
+                             intptr_t occ, intptr_t flags, intptr_t stream) {
+    py::gil_scoped_release nogil;
+    if (gpu)
+      gpu::window_agg(P<Rec>(recs), P<uint32_t>(counts), p, P<uint64_t>(keys_g), P<uint64_t>(acc_g),
+                      P<uint32_t>(cnt_g), P<uint8_t>(dirty_g), P<uint32_t>(occ), P<uint32_t>(flags),
+                      stream);
+    else
+      cpu::window_agg(P<Rec>(recs), P<uint32_t>(counts), p, P<uint64_t>(keys_g), P<uint64_t>(acc_g),
+                      P<uint32_t>(cnt_g), P<uint8_t>(dirty_g), P<uint32_t>(occ), P<uint32_t>(flags));
+  });
+
   // ---- GPU ----
   m.def("gpu_device_count", &gpu::device_count);
   m.def("cpu_set_threads", &cpu::set_threads);

@@ -417,6 +417,11 @@ class KeyedWindowOperator:
         # Record words: 1 = 8-byte RecN, 2 = 16-byte RecC (int32 values), 3 = 24-byte Rec.
         self.rec_w = 1 if narrow else 2 if compact else 3
         self.timer = None  # utils.metrics.StageTimer: per-stage step_ms histograms when attached
+        from ..ops.native import load as _load
+
+        self._m = _load()
+        self._pplan = self._aplan = None
+        self._pplan_key = self._aplan_key = None
         from ..ops.debug import debug_enabled
 
         self._debug = debug_enabled()  # MXS_DEBUG: table invariant check after every step
@@ -709,21 +714,40 @@ class KeyedWindowOperator:
             torch.cuda.current_stream(self.device).wait_event(self._ev_consumed[p])
         event_mode = self.time_mode == "event"
         stats, red = self._stats[p], self._red[p]
-        K.step_begin(self.cursor, stats)
-        plan = K.PartitionPlan(
-            max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2,
-            nranks=self._part_ranks,
-            window_mode=1, drop_late=int(event_mode), hash_mode=self.hash_mode,
-            bucket_cap=self.bucket_cap, late_ts=self._late_ts(f.old_wm),
-            tbase=self.pane_start(f.pane_base), pane=self.pane,
-            rec_words=self.rec_w, dense_bits=self.dense_bits, dense_mul=self.dense_mul)
         f.rw = self.rec_w
+        # Native plan object, rebuilt only when its structure changes; per step only the late
+        # bound and the pane base move. One native call launches step_begin + partition +
+        # step_finish (per-call dict parsing and argument checks cost ~100 us of host time per
+        # step, which the pipelined step cannot always hide).
+        key = (self.bucket_cap, self.rec_w, int(event_mode))
+        if self._pplan_key != key:
+            self._pplan = self._m.PartPlanObj(K.PartitionPlan(
+                max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2,
+                nranks=self._part_ranks, window_mode=1, drop_late=int(event_mode),
+                hash_mode=self.hash_mode, bucket_cap=self.bucket_cap, pane=self.pane,
+                rec_words=self.rec_w, dense_bits=self.dense_bits,
+                dense_mul=self.dense_mul).as_dict())
+            self._pplan_key = key
+        pp = self._pplan
+        pp.late_ts = self._late_ts(f.old_wm)
+        pp.tbase = self.pane_start(f.pane_base)
+        if f.n:
+            for t, name in ((f.keys, "keys"), (f.ts, "ts"), (f.vals, "vals")):
+                if t.dtype != torch.int64 or not t.is_contiguous() or t.numel() < f.n \
+                        or t.device != self.device:
+                    K._check(t, torch.int64, f.n, name, self.device)
+            if f.n >= (1 << 32):
+                raise ValueError("batch too large (2^32 events)")
+        li = self.late_idx
         with self._stage("partition"):
-            if f.n:
-                K.partition(f.keys, f.ts, f.vals, plan, self.kg_dest, self.cursor, self.send,
-                            stats, jhash=self.jhash, late_idx=self.late_idx)
-        K.step_finish(stats, self.local_maxts, red, bound=self.ooo_bound, event_mode=event_mode,
-                      proc_now=f.proc_now, flags=self.flags)
+            self._m.window_front(
+                cuda, f.keys.data_ptr(), f.ts.data_ptr(), f.vals.data_ptr(),
+                0 if self.jhash is None else self.jhash.data_ptr(), f.n, pp,
+                self.kg_dest.data_ptr(), self.cursor.data_ptr(), self.send.data_ptr(),
+                stats.data_ptr(), 0 if li is None else li.data_ptr(),
+                0 if li is None else li.numel(), self.local_maxts.data_ptr(), self.ooo_bound,
+                int(event_mode), f.proc_now, red.data_ptr(), self.flags.data_ptr(),
+                torch.cuda.current_stream(self.device).cuda_stream if cuda else 0)
         if f.idle:
             red[2:3].fill_(I64_MAX)  # idle partition: no say in the MIN watermark
         # Watermark valve + pane range + every overflow flag: ONE MIN all-reduce per step.
@@ -875,8 +899,22 @@ class KeyedWindowOperator:
         self.comm.all_to_all(self.recv_counts, self.cursor)
 
     def _aggregate(self, recs, counts, aplan: K.AggPlan) -> None:
-        K.window_agg(recs, counts, aplan, self.keys_g, self.acc_g, self.cnt_g, self.dirty_g,
-                     self.occ, self.flags)
+        if aplan.np_step > aplan.ring:
+            raise ValueError("step touches more panes than the ring holds")
+        key = (aplan.bucket_cap, aplan.rec_words, aplan.ring, aplan.nsrc, aplan.combined,
+               aplan.pg, aplan.dlist)
+        if self._aplan_key != key:
+            self._aplan = self._m.AggPlanObj(aplan.as_dict())
+            self._aplan_key = key
+        ap = self._aplan
+        ap.np_step, ap.pane_base, ap.p_lo, ap.fired_hi = (aplan.np_step, aplan.pane_base,
+                                                          aplan.p_lo, aplan.fired_hi)
+        cuda = self.device.type == "cuda"
+        self._m.window_agg_obj(cuda, recs.data_ptr(), counts.data_ptr(), ap,
+                               self.keys_g.data_ptr(), self.acc_g.data_ptr(),
+                               self.cnt_g.data_ptr(), self.dirty_g.data_ptr(),
+                               self.occ.data_ptr(), self.flags.data_ptr(),
+                               torch.cuda.current_stream(self.device).cuda_stream if cuda else 0)
 
     def _zero_pane(self, so: int) -> None:
         """Reset the pane slab starting at slot index `so` (pane-major state)."""
