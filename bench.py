@@ -94,15 +94,43 @@ def main() -> int:
     sync()
     bench.latencies_ms.clear()
     alerts0 = bench.alerts
+    step_t = [] if os.environ.get("MXS_STEP_TIMES") == "1" else None
     t0 = time.perf_counter()
+    prof_steps = os.environ.get("MXS_STEP_PROFILE") == "1"
+    worst = (0.0, None)
     for _ in range(a.steps):
+        if prof_steps:
+            import cProfile
+
+            pr = cProfile.Profile()
+            ts_ = time.perf_counter()
+            pr.enable()
         bench.step()
+        if prof_steps:
+            pr.disable()
+            if time.perf_counter() - ts_ > worst[0]:
+                worst = (time.perf_counter() - ts_, pr)
+        if step_t is not None:
+            step_t.append(time.perf_counter())
         if wd is not None:
             wd.beat()
     # Pipelined: the last step's state half (aggregation, firing) runs inside the timed region
     # too, so K timed steps = K partitions + K+1 state halves (never less work than K steps).
     bench.drain()
+    if step_t is not None:
+        step_t.append(time.perf_counter())
     sync()
+    if step_t is not None:
+        step_t.append(time.perf_counter())
+        d = [round((b - a_) * 1e3, 3) for a_, b in zip([t0] + step_t[:-1], step_t)]
+        print(f"step host ms (last two: drain, final sync): {d}", file=sys.stderr)
+        if worst[1] is not None:
+            import pstats
+
+            pstats.Stats(worst[1], stream=sys.stderr).sort_stats("tottime").print_stats(25)
+        m = bench.op.metrics
+        print(f"ring_regrows={m.ring_regrows} bucket_regrows={m.bucket_regrows} "
+              f"extra={m.extra} ring={bench.op.ring}", file=sys.stderr)
     comm.barrier()
     sync()
     dt = time.perf_counter() - t0

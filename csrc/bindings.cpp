@@ -8,6 +8,8 @@
 
 #include <cstring>
 #include <stdexcept>
+#include <string>
+#include <tuple>
 #include <vector>
 
 #include "mxs_kernels.h"
@@ -440,6 +442,16 @@ PYBIND11_MODULE(_mxs_native, m) {
                                intptr_t keys_g, intptr_t slots) {
     cpu::table_insert(P<uint64_t>(keys), n, nsub_log2, cap_log2, P<uint64_t>(keys_g),
                       P<int64_t>(slots));
+  });
+  // Fired rows -> one pinned host slab: one hipMemcpyAsync per column on `stream`, no sync
+  // (window_operator.to_host_arrays syncs once). copies = [(src, nbytes, dst_offset)].
+  m.def("gpu_d2h_many", [](intptr_t dst, const std::vector<std::tuple<intptr_t, int64_t, int64_t>>& copies,
+                           intptr_t stream) {
+    for (const auto& c : copies) {
+      const int e = gpu::d2h_async((char*)dst + std::get<2>(c), (const void*)std::get<0>(c),
+                                   (size_t)std::get<1>(c), stream);
+      if (e != 0) throw std::runtime_error("hipMemcpyAsync D2H failed: " + std::to_string(e));
+    }
   });
   m.def("gpu_dirty_clear", [](intptr_t list, intptr_t list_n, uint32_t cap, int ring,
                               int64_t nslots, intptr_t dirty_g, intptr_t mark, int64_t p_lo, int np,

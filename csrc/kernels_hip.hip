@@ -2521,6 +2521,10 @@ namespace gpu {
 // synchronisation; set before the device's context exists (bench.py MXS_SPIN=1).
 int set_spin_schedule() { return (int)hipSetDeviceFlags(hipDeviceScheduleSpin); }
 
+int d2h_async(void* dst, const void* src, size_t bytes, intptr_t stream) {
+  return (int)hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream);
+}
+
 int device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

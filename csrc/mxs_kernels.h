@@ -78,6 +78,8 @@ struct RollPlan {
 namespace gpu {
 int device_count();
 int set_spin_schedule();
+// Async device->host copy on `stream` (hipMemcpyAsync); returns the hipError_t code.
+int d2h_async(void* dst, const void* src, size_t bytes, intptr_t stream);
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,

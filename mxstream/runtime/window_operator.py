@@ -100,12 +100,21 @@ def to_host_arrays(cols: list[torch.Tensor], n: int, pool: PinnedSlabPool | None
         offs.append(nbytes)
         nbytes += (n * c.element_size() + 255) & ~255
     t, arr = pool.take(nbytes)
-    out = []
+    out, copies = [], []
     for o, c in zip(offs, cols):
         nb = n * c.element_size()
-        t[o:o + nb].view(c.dtype).copy_(c[:n], non_blocking=True)
+        if not c.is_contiguous() or n > c.numel():
+            raise ValueError("to_host_arrays: columns must be contiguous with at least n rows")
+        copies.append((c.data_ptr(), nb, o))
         out.append(arr[o:o + nb].view(_NP_DTYPE[c.dtype]))
-    torch.cuda.current_stream(cols[0].device).synchronize()
+    # One native call issuing a hipMemcpyAsync per column: torch's copy_ into a pinned slice
+    # occasionally blocked for 7-9 ms (one firing per run in the headline bench, cProfile:
+    # profiles/r2_fire_d2h.md).
+    from ..ops.native import load
+
+    stream = torch.cuda.current_stream(cols[0].device)
+    load().gpu_d2h_many(t.data_ptr(), copies, stream.cuda_stream)
+    stream.synchronize()
     return out
 
 
@@ -115,13 +124,19 @@ _NP_DTYPE = {torch.int64: np.int64, torch.int32: np.int32, torch.float64: np.flo
 
 
 # How the step's host sync waits for the GPU (MXS_SYNC, measured in profiles/r2_host_sync.md):
-#   "stream" (default): hipStreamSynchronize of the caller's stream when nothing else is queued
-#     on it (unpipelined); "event": hipEventSynchronize on the step's event.
-_SYNC = __import__("os").environ.get("MXS_SYNC", "stream")
+#   "query" (default): poll hipEventQuery on the step's event -- the host resumes within a
+#     microsecond of the partition finishing, where a blocking wait (hipEventSynchronize /
+#     hipStreamSynchronize) sleeps in the driver and wakes tens of microseconds late, time
+#     the pipelined step cannot hide; "event": hipEventSynchronize; "stream":
+#     hipStreamSynchronize (unpipelined only).
+_SYNC = __import__("os").environ.get("MXS_SYNC", "query")
 
 
 def _host_wait(ev, device, pipelined: bool) -> None:
-    if _SYNC == "event" or pipelined:
+    if _SYNC == "query":
+        while not ev.query():
+            pass
+    elif _SYNC == "event" or pipelined:
         ev.synchronize()
     else:
         torch.cuda.current_stream(device).synchronize()
@@ -425,6 +440,7 @@ class KeyedWindowOperator:
         from ..ops.debug import debug_enabled
 
         self._debug = debug_enabled()  # MXS_DEBUG: table invariant check after every step
+        self._warm = self.device.type == "cuda"  # first-fire warm-up pending (see _warm_fire)
 
         # ---- watermark / firing bookkeeping (host, identical on every rank) ----
         self.wm = I64_MIN
@@ -679,7 +695,22 @@ class KeyedWindowOperator:
         return out + self._back_finish(prev)
 
     # ---- step phases ------------------------------------------------------------------------
+    def _warm_fire(self) -> None:
+        """Launch the fire kernel once over the still-empty table before the first step. Its
+        first launch costs ~7 ms of one-time runtime set-up (measured: the first firing step of
+        the headline bench took 7.3 ms against ~0.5 ms for every later one), which would
+        otherwise land on the first window's alert latency. Emits nothing: no slot has data."""
+        self._warm = False
+        K.window_fire(self.keys_g, self.acc_g, self.cnt_g, self.dirty_g, agg=self.agg, npanes=1,
+                      ring=self.ring, p0=0, wstart=0, wend=self.size, only_dirty=False,
+                      map_prog=self.map_prog, filt_prog=self.filter_prog, out_keys=self.out_keys,
+                      out_vals=self.out_vals, out_raw=self.out_raw, out_cnt=self.out_cnt,
+                      out_n=self.out_n)
+        self.out_n.zero_()
+
     def _front(self, keys, ts, vals) -> "_Front":
+        if self._warm:
+            self._warm_fire()
         n = keys.numel()
         if n > self.batch_capacity:
             self.flush()

@@ -25,6 +25,9 @@ for step in "$@"; do
     bench_nopipe) timeout -k 10 300 python bench.py --steps 48 --warmup 8 --no-pipeline > "$out/bench_nopipe.log" 2>&1 || exit $? ;;
     bench_hashed) timeout -k 10 300 python bench.py --steps 48 --warmup 8 --hashed-keys > "$out/bench_hashed.log" 2>&1 || exit $? ;;
     prof_bench_hashed) prof bench_hashed python3 bench.py --steps 24 --warmup 6 --hashed-keys || exit $? ;;
+    bench_sync_*) m=${step#bench_sync_}; MXS_SYNC=$m timeout -k 10 300 python bench.py --steps 48 --warmup 8 > "$out/bench_sync_$m.log" 2>&1 || exit $? ;;
+    bench_times) MXS_STEP_TIMES=1 timeout -k 10 300 python bench.py --steps 48 --warmup 8 > "$out/bench_times.log" 2>&1 || exit $? ;;
+    bench_sprof) MXS_STEP_TIMES=1 MXS_STEP_PROFILE=1 timeout -k 10 300 python bench.py --steps 48 --warmup 8 > "$out/bench_sprof.log" 2>&1 || exit $? ;;
     bench20) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "$out/bench20.log" 2>&1 || exit $? ;;
     cfg1) timeout -k 10 300 python -m mxstream.models.bench_configs --config 1 --steps 20 --warmup 3 > "$out/cfg1.json" 2>&1 || exit $? ;;
     cfg1t*) t=${step#cfg1t}; timeout -k 10 300 python -m mxstream.models.bench_configs --config 1 --threads $t --steps 20 --warmup 3 > "$out/cfg1_t$t.json" 2>&1 || exit $? ;;
