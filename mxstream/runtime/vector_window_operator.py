@@ -74,9 +74,6 @@ class VectorWindowOperator(KeyedWindowOperator):
     _dense_ok = False         # its own aggregation kernel
 
     # ---- hooks -----------------------------------------------------------------------------
-    def _warm_fire(self) -> None:
-        self._warm = False  # vec_window_fire has no expression epilogue to set up
-
     def _rec_words(self) -> int:
         return 2 if self.compact else 3
 

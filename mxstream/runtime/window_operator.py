@@ -440,7 +440,6 @@ class KeyedWindowOperator:
         from ..ops.debug import debug_enabled
 
         self._debug = debug_enabled()  # MXS_DEBUG: table invariant check after every step
-        self._warm = self.device.type == "cuda"  # first-fire warm-up pending (see _warm_fire)
 
         # ---- watermark / firing bookkeeping (host, identical on every rank) ----
         self.wm = I64_MIN
@@ -695,22 +694,7 @@ class KeyedWindowOperator:
         return out + self._back_finish(prev)
 
     # ---- step phases ------------------------------------------------------------------------
-    def _warm_fire(self) -> None:
-        """Launch the fire kernel once over the still-empty table before the first step. Its
-        first launch costs ~7 ms of one-time runtime set-up (measured: the first firing step of
-        the headline bench took 7.3 ms against ~0.5 ms for every later one), which would
-        otherwise land on the first window's alert latency. Emits nothing: no slot has data."""
-        self._warm = False
-        K.window_fire(self.keys_g, self.acc_g, self.cnt_g, self.dirty_g, agg=self.agg, npanes=1,
-                      ring=self.ring, p0=0, wstart=0, wend=self.size, only_dirty=False,
-                      map_prog=self.map_prog, filt_prog=self.filter_prog, out_keys=self.out_keys,
-                      out_vals=self.out_vals, out_raw=self.out_raw, out_cnt=self.out_cnt,
-                      out_n=self.out_n)
-        self.out_n.zero_()
-
     def _front(self, keys, ts, vals) -> "_Front":
-        if self._warm:
-            self._warm_fire()
         n = keys.numel()
         if n > self.batch_capacity:
             self.flush()
