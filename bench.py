@@ -43,6 +43,8 @@ def main() -> int:
                     help="unpipelined step (host sync between the partition and the aggregation)")
     ap.add_argument("--hashed-keys", action="store_true",
                     help="hash-table state for arbitrary int64 keys instead of dense dictionary ids")
+    ap.add_argument("--int32-keys", action="store_true",
+                    help="dense key ids as an int32 column instead of int64 (experiments)")
     ap.add_argument("--trace", default=None,
                     help="write a Chrome trace of the timed steps (stage spans; roctx with MXS_ROCTX=1)")
     ap.add_argument("--step-timeout-ms", type=int, default=0,
@@ -68,7 +70,7 @@ def main() -> int:
         device = torch.device("cpu")
 
     cfg = TumblingBenchConfig(keys=a.keys, batch=a.batch, cap_log2=a.cap_log2,
-                              dense_keys=not a.hashed_keys,
+                              dense_keys=not a.hashed_keys, key32=a.int32_keys,
                               pipeline=False if a.no_pipeline else None)
     bench = TumblingWindowBench(cfg, comm, device)
     if a.trace:

@@ -79,6 +79,7 @@ PartPlan make_part(py::dict d) {
   p.inv_pane = p.pane > 0 ? 1.0 / (double)p.pane : 0.0;
   p.dense_bits = d.contains("dense_bits") ? d["dense_bits"].cast<int32_t>() : 0;
   p.dense_mul = d.contains("dense_mul") ? d["dense_mul"].cast<uint32_t>() : 0u;
+  p.key32 = d.contains("key32") ? d["key32"].cast<int32_t>() : 0;
   if (p.dense_bits < 0 || p.dense_bits > 32 || (p.dense_bits && (p.nranks != 1 ||
       p.nsub_log2 > p.dense_bits || !(p.dense_mul & 1u))))
     throw std::invalid_argument("dense keys: one destination, nsub <= 2^bits, odd multiplier");
@@ -254,6 +255,13 @@ PYBIND11_MODULE(_mxs_native, m) {
                        P<int64_t>(red), P<uint32_t>(flags), stream);
     } else {
       cpu::step_begin(P<uint32_t>(cursor), nb, P<int64_t>(stats));
+      std::vector<uint64_t> wide;
+      if (n && p.key32) {  // int32 key ids: sign-extended copy for the CPU kernel
+        wide.resize((size_t)n);
+        const int32_t* k32 = P<int32_t>(keys);
+        for (int64_t i = 0; i < n; ++i) wide[(size_t)i] = (uint64_t)(int64_t)k32[i];
+        keys = (intptr_t)wide.data();
+      }
       if (n)
         cpu::partition(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), P<int32_t>(jhash), n,
                        p, P<int32_t>(kg_dest), P<uint32_t>(cursor), P<Rec>(out), P<int64_t>(stats),

@@ -47,12 +47,13 @@ void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t
     const uint64_t r = rng64(seed, stream_id, idx0 + (uint64_t)i);
     const uint64_t r2 = mix64(r);
     const uint64_t r3 = mix64(r2);
-    keys[i] = mulhi(r, nkeys);
+    if (val_f64 & 2) reinterpret_cast<int32_t*>(keys)[i] = (int32_t)mulhi(r, nkeys);
+    else keys[i] = mulhi(r, nkeys);
     int64_t t = ts_base + (int64_t)((double)i * span_per_event);
     if (disorder_p1 > 1) t -= (int64_t)mulhi(r2, disorder_p1);
     ts[i] = t;
     const int64_t v = val_lo + (val_span > 0 ? (int64_t)mulhi(r3, (uint64_t)val_span) : 0);
-    vals[i] = val_f64 ? f64_bits((double)v) : (uint64_t)v;
+    vals[i] = (val_f64 & 1) ? f64_bits((double)v) : (uint64_t)v;
   }
 }
 

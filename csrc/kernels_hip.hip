@@ -85,18 +85,21 @@ __global__ __launch_bounds__(256) void gen_events_kernel(
     uint64_t* __restrict__ keys, int64_t* __restrict__ ts, uint64_t* __restrict__ vals,
     int64_t n, uint64_t seed, uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
     double span_per_event, uint64_t disorder_p1, int64_t val_lo, uint64_t val_span,
-    int32_t val_f64) {
+    int32_t mode) {
+  // mode bit 0: values as f64 bits; bit 1: int32 key ids (the columnar sources' dictionary ids)
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint64_t r = rng64(seed, stream_id, idx0 + (uint64_t)i);
     const uint64_t r2 = mix64(r);
     const uint64_t r3 = mix64(r2);
-    keys[i] = __umul64hi(r, nkeys);  // multiply-shift: uniform in [0, nkeys), no division
+    const uint64_t key = __umul64hi(r, nkeys);  // multiply-shift: uniform in [0, nkeys)
+    if (mode & 2) reinterpret_cast<int32_t*>(keys)[i] = (int32_t)key;
+    else keys[i] = key;
     int64_t t = ts_base + (int64_t)((double)i * span_per_event);
     if (disorder_p1 > 1) t -= (int64_t)__umul64hi(r2, disorder_p1);
     ts[i] = t;
     const int64_t v = val_lo + (val_span ? (int64_t)__umul64hi(r3, val_span) : 0);
-    vals[i] = val_f64 ? f64_bits((double)v) : (uint64_t)v;
+    vals[i] = (mode & 1) ? f64_bits((double)v) : (uint64_t)v;
   }
 }
 
@@ -176,6 +179,43 @@ template <int V, class T>
 __device__ __forceinline__ T ldin(const T* p) {
   if (V & 1) return __builtin_nontemporal_load(p);
   return *p;
+}
+
+// Key column load: 64-bit keys, or int32 dictionary ids (PartPlan.key32) sign-extended so the
+// reserved markers -1 / -2 stay detectable.
+template <int V, bool K32>
+__device__ __forceinline__ uint64_t ldkey(const uint64_t* keys, int64_t i) {
+  if constexpr (K32) return (uint64_t)(int64_t)ldin<V>(&reinterpret_cast<const int32_t*>(keys)[i]);
+  else return ldin<V>(&keys[i]);
+}
+
+// Two consecutive events per lane (PAIR partition variant): keys as one 8-byte (int32 ids) or
+// 16-byte load, ts and values as one 16-byte load each -- half the load instructions of the
+// one-event-per-lane form and 1 KB of contiguous bytes per wave-wide ts / value load.
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+template <int V, typename T>
+__device__ __forceinline__ T ldvec(const T* p) {
+  if (V & 1) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <int V, bool K32>
+__device__ __forceinline__ void ldkey2(const uint64_t* keys, int64_t i, uint64_t& k0, uint64_t& k1) {
+  if constexpr (K32) {
+    const u32x2_t w = ldvec<V>(reinterpret_cast<const u32x2_t*>(reinterpret_cast<const int32_t*>(keys) + i));
+    k0 = (uint64_t)(int64_t)(int32_t)w.x;
+    k1 = (uint64_t)(int64_t)(int32_t)w.y;
+  } else {
+    const u32x4_t w = ldvec<V>(reinterpret_cast<const u32x4_t*>(keys + i));
+    k0 = (uint64_t)w.x | ((uint64_t)w.y << 32);
+    k1 = (uint64_t)w.z | ((uint64_t)w.w << 32);
+  }
+}
+template <int V>
+__device__ __forceinline__ void ld64x2(const void* base, int64_t i, uint64_t& a, uint64_t& b) {
+  const u32x4_t w = ldvec<V>(reinterpret_cast<const u32x4_t*>(reinterpret_cast<const uint64_t*>(base) + i));
+  a = (uint64_t)w.x | ((uint64_t)w.y << 32);
+  b = (uint64_t)w.z | ((uint64_t)w.w << 32);
 }
 
 template <int V>
@@ -606,7 +646,7 @@ constexpr int kCUProd = 4;               // production round: 4096 records, one 
 static_assert(compact_lds(kCUProd) <= 160 * 1024, "compact partition LDS exceeds 160 KiB");
 
 // RB = 16: RecC records; RB = 8: RecN records (one destination, see RecN).
-template <int V, int CU = kCU, bool ONE = false, int RB = 16>
+template <int V, int CU = kCU, bool ONE = false, int RB = 16, bool K32 = false, bool PAIR = false>
 __global__ __launch_bounds__(1024) void partition_compact_kernel(
     const uint64_t* __restrict__ keys, const int64_t* __restrict__ ts,
     const uint64_t* __restrict__ vals, const int32_t* __restrict__ jhash_tab, int64_t n,
@@ -642,18 +682,34 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   const int64_t start = (int64_t)blockIdx.x * chunk;
   const int64_t end = start + chunk < n ? start + chunk : n;
 
+  // Event u of a thread's group: lane-strided, or (PAIR) two consecutive events per lane.
+  auto ev_at = [&](int64_t base, int u) -> int64_t {
+    if constexpr (PAIR)
+      return base + (int64_t)(u >> 1) * 2 * blockDim.x + 2 * (int64_t)threadIdx.x + (u & 1);
+    else
+      return base + (int64_t)u * blockDim.x + threadIdx.x;
+  };
   // Pass A: bucket histogram from the keys alone.
-  for (int64_t i0 = start + threadIdx.x; i0 < end; i0 += (int64_t)blockDim.x * kPartU) {
+  for (int64_t i0 = start; i0 < end; i0 += (int64_t)blockDim.x * kPartU) {
     uint64_t k[kPartU];
+    if constexpr (PAIR) {
 #pragma unroll
-    for (int u = 0; u < kPartU; ++u) {
-      const int64_t i = i0 + (int64_t)u * blockDim.x;
-      if (i < end) k[u] = ldin<V>(&keys[i]);
+      for (int u = 0; u < kPartU; u += 2) {
+        const int64_t i = ev_at(i0, u);
+        if (i + 1 < end) ldkey2<V, K32>(keys, i, k[u], k[u + 1]);
+        else if (i < end) k[u] = ldkey<V, K32>(keys, i);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kPartU; ++u) {
+        const int64_t i = ev_at(i0, u);
+        if (i < end) k[u] = ldkey<V, K32>(keys, i);
+      }
     }
 #pragma unroll
     for (int u = 0; u < kPartU; ++u) {
-      const int64_t i = i0 + (int64_t)u * blockDim.x;
-      if (i >= end) break;
+      const int64_t i = ev_at(i0, u);
+      if (i >= end) continue;
       uint32_t b;
       if constexpr (ONE) {
         b = sub_of(k[u], plan);
@@ -692,15 +748,37 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   // LDS sort and flush, so the HBM latency is not exposed once per round (16 rounds/group).
   uint64_t nk[CU], nv[CU];
   int64_t nt[CU];
+  auto load_round = [&](int64_t base) {
+    if constexpr (PAIR) {
 #pragma unroll
-  for (int u = 0; u < CU; ++u) {
-    const int64_t i = start + (int64_t)u * blockDim.x + threadIdx.x;
-    if (i < end) {
-      nk[u] = ldin<V>(&keys[i]);
-      nt[u] = ldin<V>(&ts[i]);
-      nv[u] = ldin<V>(&vals[i]);
+      for (int u = 0; u < CU; u += 2) {
+        const int64_t i = ev_at(base, u);
+        if (i + 1 < end) {
+          ldkey2<V, K32>(keys, i, nk[u], nk[u + 1]);
+          uint64_t t0, t1;
+          ld64x2<V>(ts, i, t0, t1);
+          nt[u] = (int64_t)t0;
+          nt[u + 1] = (int64_t)t1;
+          ld64x2<V>(vals, i, nv[u], nv[u + 1]);
+        } else if (i < end) {
+          nk[u] = ldkey<V, K32>(keys, i);
+          nt[u] = ldin<V>(&ts[i]);
+          nv[u] = ldin<V>(&vals[i]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < CU; ++u) {
+        const int64_t i = ev_at(base, u);
+        if (i < end) {
+          nk[u] = ldkey<V, K32>(keys, i);
+          nt[u] = ldin<V>(&ts[i]);
+          nv[u] = ldin<V>(&vals[i]);
+        }
+      }
     }
-  }
+  };
+  load_round(start);
   for (int64_t r0 = start; r0 < end; r0 += (1024 * CU)) {
     uint32_t bk[CU], rk[CU];
     RT rec[CU];
@@ -712,16 +790,11 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
       ck[u] = nk[u];
       ct[u] = nt[u];
       cv[u] = nv[u];
-      const int64_t i = r0 + (1024 * CU) + (int64_t)u * blockDim.x + threadIdx.x;
-      if (i < end) {
-        nk[u] = ldin<V>(&keys[i]);
-        nt[u] = ldin<V>(&ts[i]);
-        nv[u] = ldin<V>(&vals[i]);
-      }
     }
+    load_round(r0 + (1024 * CU));
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
-      const int64_t i = r0 + (int64_t)u * blockDim.x + threadIdx.x;
+      const int64_t i = ev_at(r0, u);
       keep[u] = false;
       if (i < end) {
         const uint64_t k = ck[u];
@@ -2556,6 +2629,66 @@ void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int3
   HIP_CHECK(hipGetLastError());
 }
 
+int getenv_int(const char* name, int def) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : def;
+}
+
+// One compact-partition instantiation: LDS attribute set once, one group per 64K events.
+template <bool ONE, int RB, bool K32, bool PAIR>
+void launch_compact(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
+                    const int32_t* jhash_tab, int64_t n, int64_t chunk, int blocks,
+                    const PartPlan& plan, const int32_t* kg_dest, uint32_t* cursor, Rec* out,
+                    int64_t* stats, uint32_t* late_idx, uint32_t late_cap, intptr_t stream) {
+  auto kfn = partition_compact_kernel<1, kCUProd, ONE, RB, K32, PAIR>;
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)compact_lds(kCUProd)));
+    attr = true;
+  }
+  // One rank: no key-group hashing and no LDS kg table.
+  const size_t lds = compact_lds(kCUProd) - (ONE ? (size_t)kKgLdsMax * 4 : 0);
+  hipLaunchKernelGGL(kfn, dim3(blocks), dim3(1024), lds, (hipStream_t)stream, keys, ts, vals,
+                     jhash_tab, n, chunk, plan, kg_dest, cursor, reinterpret_cast<RecC*>(out),
+                     stats, late_idx, late_cap);
+  HIP_CHECK(hipGetLastError());
+}
+
+static const bool kPairEnv = getenv_int("MXS_PAIR", 1) != 0;  // A/B knob (profiles)
+
+template <bool ONE, int RB>
+void dispatch_compact(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
+                      const int32_t* jhash_tab, int64_t n, const PartPlan& plan,
+                      const int32_t* kg_dest, uint32_t* cursor, Rec* out, int64_t* stats,
+                      uint32_t* late_idx, uint32_t late_cap, intptr_t stream) {
+  // 4096-record rounds, up to 64K events per workgroup (one group per CU: 86 KB of LDS),
+  // i.e. one workgroup per CU at 16M events. Against 2048-record rounds / 32K events at two
+  // groups per CU (kbench, profiles/r1_partition_rounds.md): 227 -> 198 us. Longer bucket
+  // runs per group and bigger rounds cut the partial-sector writes and the per-group
+  // reservation work; fewer, larger groups beat the higher occupancy.
+  const int64_t per = std::min<int64_t>(65536, std::max<int64_t>(4096, (n + 255) / 256));
+  const int blocks = grid_for(n, per, 4096);
+  int64_t chunk = (n + blocks - 1) / blocks;
+  // PAIR loads (two events per lane, 16-byte ts / value loads) need even group boundaries and
+  // 16-byte aligned columns (8-byte for int32 keys); a misaligned view takes the lane-strided
+  // kernel.
+  const bool pair = ((uintptr_t)ts % 16 == 0) && ((uintptr_t)vals % 16 == 0) &&
+                    ((uintptr_t)keys % (plan.key32 ? 8 : 16) == 0) && kPairEnv;
+  if (pair) chunk = (chunk + 1) & ~(int64_t)1;
+#define MXS_COMPACT(K32_, PAIR_)                                                                \
+  launch_compact<ONE, RB, K32_, PAIR_>(keys, ts, vals, jhash_tab, n, chunk, blocks, plan,        \
+                                       kg_dest, cursor, out, stats, late_idx, late_cap, stream)
+  if (plan.key32) {
+    if (pair) MXS_COMPACT(true, true);
+    else MXS_COMPACT(true, false);
+  } else {
+    if (pair) MXS_COMPACT(false, true);
+    else MXS_COMPACT(false, false);
+  }
+#undef MXS_COMPACT
+}
+
 void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                const int32_t* jhash_tab, int64_t n, const PartPlan& plan, const int32_t* kg_dest,
                uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap,
@@ -2566,57 +2699,22 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
     if (plan.nranks != 1 || nb > kCMaxNb || (uint64_t)nb * plan.bucket_cap >= (1ull << 32))
       throw std::invalid_argument("partition: 8-byte records need one destination, <= 512 buckets");
     if (n <= 0) return;
-    static bool attr8 = false;
-    if (!attr8) {
-      HIP_CHECK(hipFuncSetAttribute((const void*)partition_compact_kernel<1, kCUProd, true, 8>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)compact_lds(kCUProd)));
-      attr8 = true;
-    }
-    const int64_t per = std::min<int64_t>(65536, std::max<int64_t>(4096, (n + 255) / 256));
-    const int blocks = grid_for(n, per, 4096);
-    const int64_t chunk = (n + blocks - 1) / blocks;
-    hipLaunchKernelGGL((partition_compact_kernel<1, kCUProd, true, 8>), dim3(blocks), dim3(1024),
-                       compact_lds(kCUProd) - (size_t)kKgLdsMax * 4, (hipStream_t)stream, keys,
-                       ts, vals, jhash_tab, n, chunk, plan, kg_dest, cursor,
-                       reinterpret_cast<RecC*>(out), stats, late_idx, late_cap);
-    HIP_CHECK(hipGetLastError());
+    dispatch_compact<true, 8>(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats,
+                              late_idx, late_cap, stream);
     return;
   }
   if (plan.rec_words == 2 && nb <= kCMaxNb && (uint64_t)nb * plan.bucket_cap < (1ull << 32)) {
     if (n <= 0) return;
-    // 4096-record rounds, up to 64K events per workgroup (one group per CU: 86 KB of LDS),
-    // i.e. one workgroup per CU at 16M events. Against 2048-record rounds / 32K events at two
-    // groups per CU (kbench, profiles/r1_partition_rounds.md): 227 -> 198 us. Longer bucket
-    // runs per group and bigger rounds cut the partial-sector writes and the per-group
-    // reservation work; fewer, larger groups beat the higher occupancy.
-    static bool attr = false;
-    if (!attr) {
-      HIP_CHECK(hipFuncSetAttribute((const void*)partition_compact_kernel<1, kCUProd, false>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)compact_lds(kCUProd)));
-      HIP_CHECK(hipFuncSetAttribute((const void*)partition_compact_kernel<1, kCUProd, true>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)compact_lds(kCUProd)));
-      attr = true;
-    }
-    const int64_t per = std::min<int64_t>(65536, std::max<int64_t>(4096, (n + 255) / 256));
-    const int blocks = grid_for(n, per, 4096);
-    const int64_t chunk = (n + blocks - 1) / blocks;
-    // One rank: the kernel specialised without key-group hashing (and without the LDS kg table).
     if (plan.nranks == 1)
-      hipLaunchKernelGGL((partition_compact_kernel<1, kCUProd, true>), dim3(blocks), dim3(1024),
-                         compact_lds(kCUProd) - (size_t)kKgLdsMax * 4, (hipStream_t)stream, keys,
-                         ts, vals, jhash_tab, n, chunk, plan, kg_dest, cursor,
-                         reinterpret_cast<RecC*>(out), stats, late_idx, late_cap);
+      dispatch_compact<true, 16>(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats,
+                                 late_idx, late_cap, stream);
     else
-      hipLaunchKernelGGL((partition_compact_kernel<1, kCUProd, false>), dim3(blocks), dim3(1024),
-                         compact_lds(kCUProd), (hipStream_t)stream, keys, ts, vals, jhash_tab, n,
-                         chunk, plan, kg_dest, cursor, reinterpret_cast<RecC*>(out), stats,
-                         late_idx, late_cap);
-    HIP_CHECK(hipGetLastError());
+      dispatch_compact<false, 16>(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats,
+                                  late_idx, late_cap, stream);
     return;
   }
+  if (plan.key32)
+    throw std::invalid_argument("partition: int32 keys need compact records (<= 512 buckets)");
   // Write-combined staged scatter when the LDS carry buffers fit (<= 512 buckets); otherwise
   // the plain scatter. Both stream their inputs with non-temporal loads (kbench A/B).
   partition_variant(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats, late_idx,

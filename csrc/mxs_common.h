@@ -431,6 +431,7 @@ struct PartPlan {
   int32_t rec_words;         // 3: 24-byte Rec; 2: 16-byte RecC (int32 values, GPU window path)
   int32_t dense_bits;        // > 0: dense key ids < 2^dense_bits, directly addressed (dense_slot)
   uint32_t dense_mul;        // odd multiplier of the dense slot bijection
+  int32_t key32;             // 1: the key column is int32 (dictionary ids), sign-extended on load
 };
 
 // Sub-table of a key: a 32-bit multiplicative hash of both key halves (3 32-bit multiplies).

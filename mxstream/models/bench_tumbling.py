@@ -44,6 +44,9 @@ class TumblingBenchConfig:
     # Channel keys arrive as dictionary ids (the source interns strings, SURVEY.md F-ser), i.e.
     # dense ids < keys: directly addressed state. False: the hashed tables (arbitrary int64 keys).
     dense_keys: bool = True
+    # Key ids as an int32 column (the columnar sources' dictionary ids) instead of int64: fewer
+    # bytes, yet the partition measured slower on the same box (profiles/r2_partition_pairs.md).
+    key32: bool = False
 
 
 class TumblingWindowBench:
@@ -62,7 +65,8 @@ class TumblingWindowBench:
             filter_prog=E.compile_expr(E.var(E.VAR_MAPPED) < self.threshold_mbps),
             pipeline="stream" if cfg.pipeline is None else cfg.pipeline,
             exchange=cfg.exchange, cap_log2=cfg.cap_log2, dense_keys=cfg.dense_keys)
-        self.keys = torch.empty(cfg.batch, dtype=torch.int64, device=device)
+        self.keys = torch.empty(cfg.batch, dtype=torch.int32 if cfg.dense_keys and cfg.key32
+                                else torch.int64, device=device)
         self.ts = torch.empty(cfg.batch, dtype=torch.int64, device=device)
         self.vals = torch.empty(cfg.batch, dtype=torch.int64, device=device)
         self.step_idx = 0

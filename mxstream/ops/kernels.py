@@ -75,16 +75,18 @@ def reset_stats(s: torch.Tensor) -> None:
 def gen_events(keys, ts, vals, *, seed: int, stream_id: int, idx0: int, nkeys: int,
                ts_base: int, ts_span: int, disorder: int, val_lo: int, val_span: int,
                val_f64: bool = False) -> None:
+    """keys: int64, or int32 (dictionary ids, nkeys < 2^31)."""
     n = keys.numel()
     dev = keys.device
-    _check(keys, torch.int64, n, "keys", dev)
+    key32 = keys.dtype == torch.int32
+    _check(keys, torch.int32 if key32 else torch.int64, n, "keys", dev)
     _check(ts, torch.int64, n, "ts", dev)
     _check(vals, torch.int64, n, "vals", dev)
-    if nkeys <= 0 or nkeys >= (1 << 63):
+    if nkeys <= 0 or nkeys >= (1 << (31 if key32 else 63)):
         raise ValueError("nkeys out of range")
     m = load()
     args = (_p(keys), _p(ts), _p(vals), n, seed & (2**64 - 1), stream_id & (2**64 - 1), idx0,
-            nkeys, ts_base, ts_span, disorder, val_lo, val_span, int(val_f64))
+            nkeys, ts_base, ts_span, disorder, val_lo, val_span, int(val_f64) | (2 if key32 else 0))
     if _is_gpu(keys):
         m.gpu_gen_events(*args, _stream(keys))
     else:
@@ -109,6 +111,7 @@ class PartitionPlan:
     rec_words: int = 3       # 3: 24-byte records; 2: 16-byte records (int32 values, window path)
     dense_bits: int = 0      # > 0: dense key ids < 2^dense_bits, directly addressed
     dense_mul: int = 0       # odd multiplier of the dense slot bijection
+    key32: int = 0           # 1: int32 key column (compact-record GPU partition only)
 
     @property
     def nbuckets(self) -> int:

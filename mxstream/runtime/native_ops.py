@@ -44,9 +44,10 @@ class _ColumnInput:
                 else:
                     u, inv = np.unique(col, return_inverse=True)
                     names = cb.strings.strings()
-                    ids = np.array([self.dict.intern(names[x]) for x in u.tolist()], dtype=np.int64)
+                    ids = np.array([self.dict.intern(names[x]) for x in u.tolist()], dtype=np.int32)
                     return ids[inv]
-            return col.astype(np.int64, copy=False)
+            # Dictionary ids stay int32: the window operator's partition reads them as they are.
+            return col.astype(np.int32, copy=False)
         if kk == FK_DOUBLE:
             raise TypeError("double keys on the native path")
         if self.str_keys is True:
@@ -445,7 +446,7 @@ class NativeRollingOp(_ColumnInput, Operator):
         self._cb_templates(cb, kid)
         vv = cb.cols[self.val_pos].astype(np.float64 if self.is_float else np.int64, copy=False)
         dev = self.op.device
-        rows = self.op.process(torch.from_numpy(np.ascontiguousarray(kid)).to(dev),
+        rows = self.op.process(torch.from_numpy(np.ascontiguousarray(kid, dtype=np.int64)).to(dev),
                                torch.from_numpy(np.ascontiguousarray(vv).view(np.int64)).to(dev))
         order = np.argsort(rows.tags & 0xFFFFFFFF, kind="stable")  # back to input order
         from ..api.tuples import Tuple

@@ -325,3 +325,29 @@ def test_late_refires_at_scale_equal_cpu(gpu_device, narrow):
     g, c = run(gpu_device), run("cpu")
     assert sum(1 for x in c if x[1]) > 10_000  # many re-fired rows
     assert g == c
+
+
+@pytest.mark.parametrize("narrow,compact", [(True, True), (False, True), (False, False)])
+def test_int32_keys_gpu_match_cpu(gpu_device, narrow, compact):
+    """int32 key ids through the GPU partition (read as 4-byte keys by the 8- and 16-byte record
+    kernels, widened for the 24-byte path) fire exactly the C++ twin's rows from int64 keys."""
+
+    def run(dev, dtype):
+        op = KeyedWindowOperator(size=3000, slide=1000, agg=K.AGG_SUM_I64, device=dev,
+                                 max_keys=100_000, batch_capacity=300_000, ooo_bound=400,
+                                 dense_keys=True, narrow=narrow if dev != "cpu" else False,
+                                 compact=compact if dev != "cpu" else None)
+        rows = []
+        for step in range(8):
+            k = torch.empty(300_000, dtype=dtype, device=dev)
+            t = torch.empty(300_000, dtype=torch.int64, device=dev)
+            v = torch.empty_like(t)
+            K.gen_events(k, t, v, seed=11, stream_id=0, idx0=step * 300_000, nkeys=90_000,
+                         ts_base=step * 1000, ts_span=1000, disorder=400, val_lo=0,
+                         val_span=5000)
+            rows += op.process(k, t, v)
+        rows += op.finish()
+        return sorted((r.window_start, int(a), int(b), int(c))
+                      for r in rows for a, b, c in zip(r.keys, r.raw, r.counts))
+
+    assert run(gpu_device, torch.int32) == run("cpu", torch.int64)

@@ -251,3 +251,35 @@ def test_dense_keys_match_hashed(size, slide, lateness):
     assert run(True) == run(False)
     with pytest.raises(RuntimeError, match="table full"):
         run(True, bad=True)
+
+
+@pytest.mark.parametrize("dense", [True, False])
+def test_int32_key_ids_match_int64(dense):
+    """An int32 key column (dictionary ids, as the columnar sources produce) fires exactly what
+    the same ids as int64 fire; -1 stays a reserved id after the sign extension."""
+    import torch
+
+    from mxstream.ops import kernels as K
+    from mxstream.runtime.window_operator import KeyedWindowOperator
+
+    def run(dtype, bad=False):
+        op = KeyedWindowOperator(size=2000, slide=1000, lateness=500, agg=K.AGG_SUM_I64,
+                                 device="cpu", max_keys=3000, batch_capacity=5000, ooo_bound=300,
+                                 dense_keys=dense, cap_log2=8)
+        out = []
+        for step in range(6):
+            k = torch.empty(5000, dtype=dtype)
+            t = torch.empty(5000, dtype=torch.int64)
+            v = torch.empty_like(t)
+            K.gen_events(k, t, v, seed=3, stream_id=0, idx0=step * 5000, nkeys=3000,
+                         ts_base=step * 1000, ts_span=1000, disorder=400, val_lo=0, val_span=1000)
+            if bad and step == 2:
+                k[7] = -1
+            out += op.process(k, t, v)
+        out += op.finish()
+        return sorted((r.window_start, r.refire, int(a), int(b), int(c))
+                      for r in out for a, b, c in zip(r.keys, r.raw, r.counts))
+
+    assert run(torch.int32) == run(torch.int64)
+    with pytest.raises(ValueError, match="reserved"):
+        run(torch.int32, bad=True)
