@@ -690,8 +690,29 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
       return base + (int64_t)u * blockDim.x + threadIdx.x;
   };
   // Pass A: bucket histogram from the keys alone.
+  auto bucket_a = [&](uint64_t key) -> uint32_t {
+    if constexpr (ONE) {
+      return sub_of(key, plan);
+    } else {
+      key = key < kTombKey ? key : 0;  // reserved ids: any bucket (their slot becomes a hole)
+      const int32_t jh = plan.nranks == 1 ? 0
+                         : plan.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
+      return kg_lds ? bucket_of(key, jh, plan, skg) : bucket_of(key, jh, plan, kg_dest);
+    }
+  };
   for (int64_t i0 = start; i0 < end; i0 += (int64_t)blockDim.x * kPartU) {
     uint64_t k[kPartU];
+    if (i0 + (int64_t)blockDim.x * kPartU <= end) {
+      // Full iteration (all but a group's last): no per-lane bounds checks.
+#pragma unroll
+      for (int u = 0; u < kPartU; u += (PAIR ? 2 : 1)) {
+        if constexpr (PAIR) ldkey2<V, K32>(keys, ev_at(i0, u), k[u], k[u + 1]);
+        else k[u] = ldkey<V, K32>(keys, ev_at(i0, u));
+      }
+#pragma unroll
+      for (int u = 0; u < kPartU; ++u) atomicAdd(&run_base[bucket_a(k[u])], 1u);
+      continue;
+    }
     if constexpr (PAIR) {
 #pragma unroll
       for (int u = 0; u < kPartU; u += 2) {
@@ -710,15 +731,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
     for (int u = 0; u < kPartU; ++u) {
       const int64_t i = ev_at(i0, u);
       if (i >= end) continue;
-      uint32_t b;
-      if constexpr (ONE) {
-        b = sub_of(k[u], plan);
-      } else {
-        const int32_t jh = plan.nranks == 1 ? 0
-                           : plan.hash_mode ? jhash_tab[k[u]] : java_long_hash((int64_t)k[u]);
-        b = kg_lds ? bucket_of(k[u], jh, plan, skg) : bucket_of(k[u], jh, plan, kg_dest);
-      }
-      atomicAdd(&run_base[b], 1u);
+      atomicAdd(&run_base[bucket_a(k[u])], 1u);
     }
   }
   __syncthreads();
@@ -743,6 +756,8 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   int64_t tmax = INT64_MIN, nlate = 0, nacc = 0;
   uint32_t qmin32 = 0xFFFFFFFFu, qmax32 = 0;  // relative panes are u32: 32-bit min/max per event
   int64_t flags = 0;
+  const bool pane32 = plan.window_mode && plan.pane > 0 && plan.pane < ((int64_t)1 << 31);
+  const uint32_t pane_u = (uint32_t)plan.pane;
   // Pass B: rounds of (1024 * CU) records -> LDS counting sort by bucket -> cooperative run writes.
   // Software-pipelined: the next round's (key, ts, value) loads are issued before this round's
   // LDS sort and flush, so the HBM latency is not exposed once per round (16 rounds/group).
@@ -792,6 +807,55 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
       cv[u] = nv[u];
     }
     load_round(r0 + (1024 * CU));
+    // Fast path: a full round whose events in this wave are all ordinary (valid key, not late,
+    // relative pane in 32 bits) -- decided by one wave vote, then evaluated without per-lane
+    // branches (PMC: the general path spent as many SALU as VALU instructions on exec-mask
+    // bookkeeping). Record-width misfits only set flag bits (the host redoes the step).
+    // (8-byte records only: the 16-byte kernels spill with both paths compiled in.)
+    bool simple = RB == 8 && r0 + (1024 * CU) <= end && pane32 && !(plan.ablate & 8u);
+    if (simple) {
+      bool ok = true;
+#pragma unroll
+      for (int u = 0; u < CU; ++u) {
+        const int64_t d = ct[u] - plan.tbase;
+        ok = ok && ck[u] < kTombKey && !(plan.drop_late && ct[u] < plan.late_ts) && d >= 0 &&
+             d < ((int64_t)1 << 31);
+      }
+      simple = __all(ok);
+    }
+    if (RB == 8 && simple) {
+#pragma unroll
+      for (int u = 0; u < CU; ++u) {
+        const uint64_t k = ck[u];
+        const int64_t t = ct[u];
+        const uint64_t v = cv[u];
+        tmax = t > tmax ? t : tmax;
+        const uint32_t du = (uint32_t)(t - plan.tbase);
+        uint32_t q = (uint32_t)((double)du * plan.inv_pane);
+        const uint32_t qp = q * pane_u;
+        q = qp > du ? q - 1u : (du - qp >= pane_u ? q + 1u : q);
+        qmin32 = q < qmin32 ? q : qmin32;
+        qmax32 = q > qmax32 ? q : qmax32;
+        flags |= (int64_t)(int32_t)v != (int64_t)v ? 4 : 0;  // needs 24-byte records
+        uint32_t b;
+        if constexpr (ONE) {
+          b = sub_of(k, plan);
+        } else {
+          const int32_t jh = plan.nranks == 1 ? 0
+                             : plan.hash_mode ? jhash_tab[k] : java_long_hash((int64_t)k);
+          b = kg_lds ? bucket_of(k, jh, plan, skg) : bucket_of(k, jh, plan, kg_dest);
+        }
+        keep[u] = true;
+        bk[u] = b;
+        if constexpr (RB == 8) {
+          flags |= narrow_fits(k, (int64_t)v, q) ? 0 : 16;  // needs 16-byte records
+          rec[u] = make_uint2((uint32_t)k, ((uint32_t)v << 4) | (q & 15u));
+        } else {
+          rec[u] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), (uint32_t)v, q);
+        }
+        rk[u] = atomicAdd(&rcnt[b], 1u);
+      }
+    } else
 #pragma unroll
     for (int u = 0; u < CU; ++u) {
       const int64_t i = ev_at(r0, u);
@@ -2655,7 +2719,8 @@ void launch_compact(const uint64_t* keys, const int64_t* ts, const uint64_t* val
   HIP_CHECK(hipGetLastError());
 }
 
-static const bool kPairEnv = getenv_int("MXS_PAIR", 1) != 0;  // A/B knob (profiles)
+static const bool kPairEnv = getenv_int("MXS_PAIR", 1) != 0;  // A/B knobs (profiles)
+static const bool kFastEnv = getenv_int("MXS_PART_FAST", 1) != 0;
 
 template <bool ONE, int RB>
 void dispatch_compact(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
@@ -2676,8 +2741,10 @@ void dispatch_compact(const uint64_t* keys, const int64_t* ts, const uint64_t* v
   const bool pair = ((uintptr_t)ts % 16 == 0) && ((uintptr_t)vals % 16 == 0) &&
                     ((uintptr_t)keys % (plan.key32 ? 8 : 16) == 0) && kPairEnv;
   if (pair) chunk = (chunk + 1) & ~(int64_t)1;
+  PartPlan pl = plan;
+  if (!kFastEnv) pl.ablate |= 8u;  // wave-vote fast path off
 #define MXS_COMPACT(K32_, PAIR_)                                                                \
-  launch_compact<ONE, RB, K32_, PAIR_>(keys, ts, vals, jhash_tab, n, chunk, blocks, plan,        \
+  launch_compact<ONE, RB, K32_, PAIR_>(keys, ts, vals, jhash_tab, n, chunk, blocks, pl,          \
                                        kg_dest, cursor, out, stats, late_idx, late_cap, stream)
   if (plan.key32) {
     if (pair) MXS_COMPACT(true, true);

@@ -3,7 +3,10 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
-mkdir -p gpurun_out
+TAG=${1:-pmc}
+shift || true
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
@@ -11,6 +14,6 @@ for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LD
            "TCC_EA0_WRREQ_sum TCC_EA0_RDREQ_sum TCC_HIT_sum TCC_MISS_sum" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_INT64 SQ_INSTS_SALU TCC_EA0_WRREQ_64B_sum"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv --pmc $set \
-    -d "$ROOT/gpurun_out/pmc_bench_$i" -o run -- python3 "$ROOT/bench.py" --steps 6 --warmup 3 > "$ROOT/gpurun_out/pmc_bench_$i.log" 2>&1 || exit $?
+  timeout -s KILL 150 rocprofv3 --kernel-trace --output-format csv --pmc $set \
+    -d "$OUT/pass_$i" -o run -- python3 "$ROOT/bench.py" --steps 6 --warmup 3 "$@" > "$OUT/pass_$i.log" 2>&1 || exit $?
 done
