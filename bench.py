@@ -43,6 +43,8 @@ def main() -> int:
                     help="unpipelined step (host sync between the partition and the aggregation)")
     ap.add_argument("--hashed-keys", action="store_true",
                     help="hash-table state for arbitrary int64 keys instead of dense dictionary ids")
+    ap.add_argument("--zipf", type=float, default=0.0,
+                    help="power-law key skew exponent (0 = uniform keys, the BASELINE config)")
     ap.add_argument("--int32-keys", action="store_true",
                     help="dense key ids as an int32 column instead of int64 (experiments)")
     ap.add_argument("--trace", default=None,
@@ -70,7 +72,7 @@ def main() -> int:
         device = torch.device("cpu")
 
     cfg = TumblingBenchConfig(keys=a.keys, batch=a.batch, cap_log2=a.cap_log2,
-                              dense_keys=not a.hashed_keys, key32=a.int32_keys,
+                              dense_keys=not a.hashed_keys, key32=a.int32_keys, zipf=a.zipf,
                               pipeline=False if a.no_pipeline else None)
     bench = TumblingWindowBench(cfg, comm, device)
     if a.trace:
@@ -163,8 +165,9 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64",
-            "data": "synthetic (device-generated metric events, uniform keys = dictionary ids of "
-                    "1M channels, 2 s bounded disorder)",
+            "data": "synthetic (device-generated metric events, "
+                    + (f"zipf({a.zipf:g})" if a.zipf > 0 else "uniform")
+                    + f" keys = dictionary ids of {a.keys} channels, 2 s bounded disorder)",
             "p50_alert_latency_ms": (lt.item() if lt.item() >= 0 else None),
             "alerts": int(al.item()),
             "late_dropped": bench.op.metrics.num_late_records_dropped,
@@ -181,6 +184,7 @@ def main() -> int:
                 "keyed_state": "dense" if bench.op.dense_bits else "hashed",
                 "record_bytes": {1: 8, 2: 16, 3: 24}[bench.op.rec_w],
                 "keys": a.keys,
+                "key_distribution": f"zipf({a.zipf:g})" if a.zipf > 0 else "uniform",
                 "events_per_gpu_per_step": a.batch,
                 "event_time_per_step_ms": cfg.step_span_ms,
                 "device": str(device),

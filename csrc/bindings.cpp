@@ -291,9 +291,9 @@ PYBIND11_MODULE(_mxs_native, m) {
   m.def("gpu_gen_events", [](intptr_t keys, intptr_t ts, intptr_t vals, int64_t n, uint64_t seed,
                              uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                              int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
-                             int32_t val_f64, intptr_t stream) {
+                             int32_t val_f64, double zipf_s, intptr_t stream) {
     gpu::gen_events(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), n, seed, stream_id, idx0,
-                    nkeys, ts_base, ts_span, disorder, val_lo, val_span, val_f64, stream);
+                    nkeys, ts_base, ts_span, disorder, val_lo, val_span, val_f64, zipf_s, stream);
   });
   m.def("gpu_partition", [](intptr_t keys, intptr_t ts, intptr_t vals, intptr_t jhash, int64_t n,
                             py::dict plan, intptr_t kg_dest, intptr_t cursor, intptr_t out,
@@ -364,12 +364,13 @@ PYBIND11_MODULE(_mxs_native, m) {
                                intptr_t acc_g, intptr_t cnt_g, intptr_t keys_g,
                                std::vector<int32_t> code, std::vector<double> consts,
                                intptr_t ok, intptr_t ov, intptr_t ot, intptr_t on,
-                               uint32_t out_cap, int abits, int shift, intptr_t stream) {
+                               uint32_t out_cap, int abits, int shift, intptr_t stream,
+                               uint32_t count_n) {
     gpu::rolling_scan(agg, P<int64_t>(sk), P<int64_t>(perm), P<uint64_t>(vals), P<uint32_t>(n_in),
                       P<uint32_t>(heads), P<uint32_t>(n_heads), max_segments, P<uint64_t>(acc_g),
                       P<uint32_t>(cnt_g), P<uint64_t>(keys_g), make_prog(code, consts),
                       P<uint64_t>(ok), P<uint64_t>(ov), P<int64_t>(ot), P<uint32_t>(on), out_cap,
-                      abits, shift, stream);
+                      abits, shift, stream, count_n);
   });
   m.def("gpu_session_lookup", [](intptr_t recs, intptr_t counts, int nsrc, int nsub, uint32_t bcap,
                                  int cap_log2, intptr_t keys_g, intptr_t spill_set,
@@ -542,10 +543,10 @@ PYBIND11_MODULE(_mxs_native, m) {
   m.def("cpu_gen_events", [](intptr_t keys, intptr_t ts, intptr_t vals, int64_t n, uint64_t seed,
                              uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                              int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
-                             int32_t val_f64) {
+                             int32_t val_f64, double zipf_s) {
     py::gil_scoped_release nogil;
     cpu::gen_events(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), n, seed, stream_id, idx0,
-                    nkeys, ts_base, ts_span, disorder, val_lo, val_span, val_f64);
+                    nkeys, ts_base, ts_span, disorder, val_lo, val_span, val_f64, zipf_s);
   });
   m.def("cpu_partition", [](intptr_t keys, intptr_t ts, intptr_t vals, intptr_t jhash, int64_t n,
                             py::dict plan, intptr_t kg_dest, intptr_t cursor, intptr_t out,
@@ -593,13 +594,13 @@ PYBIND11_MODULE(_mxs_native, m) {
                                int cap_log2, int agg, intptr_t keys_g, intptr_t acc_g,
                                intptr_t cnt_g, intptr_t flags, std::vector<int32_t> code,
                                std::vector<double> consts, intptr_t ok, intptr_t ov, intptr_t ot,
-                               intptr_t on, uint32_t out_cap) {
+                               intptr_t on, uint32_t out_cap, uint32_t count_n) {
     ExprProg f = make_prog(code, consts);
     py::gil_scoped_release nogil;
     cpu::rolling_rows(P<Rec>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2, agg,
                       P<uint64_t>(keys_g), P<uint64_t>(acc_g), P<uint32_t>(cnt_g),
                       P<uint32_t>(flags), f, P<uint64_t>(ok), P<uint64_t>(ov), P<int64_t>(ot),
-                      P<uint32_t>(on), out_cap);
+                      P<uint32_t>(on), out_cap, count_n);
   });
   m.def("cpu_expr_filter", [](intptr_t x, int64_t n, std::vector<int32_t> code,
                               std::vector<double> consts, intptr_t keep) {

@@ -39,7 +39,7 @@ static Rec load_any(const Rec* base, size_t idx, int rec_words) {
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
-                int32_t val_f64) {
+                int32_t val_f64, double zipf_s) {
   auto mulhi = [](uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); };
   const double span_per_event = (double)ts_span / (double)n;
   const uint64_t disorder_p1 = (uint64_t)(disorder + 1);
@@ -47,8 +47,9 @@ void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t
     const uint64_t r = rng64(seed, stream_id, idx0 + (uint64_t)i);
     const uint64_t r2 = mix64(r);
     const uint64_t r3 = mix64(r2);
-    if (val_f64 & 2) reinterpret_cast<int32_t*>(keys)[i] = (int32_t)mulhi(r, nkeys);
-    else keys[i] = mulhi(r, nkeys);
+    const uint64_t key = zipf_s > 0.0 ? zipf_key(r, nkeys, zipf_s) : mulhi(r, nkeys);
+    if (val_f64 & 2) reinterpret_cast<int32_t*>(keys)[i] = (int32_t)key;
+    else keys[i] = key;
     int64_t t = ts_base + (int64_t)((double)i * span_per_event);
     if (disorder_p1 > 1) t -= (int64_t)mulhi(r2, disorder_p1);
     ts[i] = t;
@@ -300,7 +301,9 @@ void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& p, uint64_
 void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bucket_cap,
                   int cap_log2, int agg, uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g,
                   uint32_t* flags, const ExprProg& filt, uint64_t* out_key, uint64_t* out_val,
-                  int64_t* out_tag, uint32_t* out_n, uint32_t out_cap) {
+                  int64_t* out_tag, uint32_t* out_n, uint32_t out_cap, uint32_t count_n) {
+  // count_n > 0: tumbling count windows -- emit when a key's open window reaches count_n
+  // elements, then start a new one (the GPU rolling_scan's segmented mode).
   const uint32_t mask = (1u << cap_log2) - 1;
   uint32_t n = *out_n;
   for (int sub = 0; sub < nsub; ++sub) {
@@ -321,7 +324,7 @@ void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, u
         const uint64_t v = agg_lift(agg, r.val);
         acc_g[gi] = cnt_g[gi] ? agg_combine(agg, acc_g[gi], v) : v;
         cnt_g[gi] += 1;
-        bool emit = true;
+        bool emit = !count_n || cnt_g[gi] == count_n;
         if (filt.ncode) {
           double vars[kExprVars] = {0};
           vars[0] = agg_result_f64(agg, acc_g[gi], cnt_g[gi]);
@@ -339,6 +342,7 @@ void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, u
           }
           ++n;
         }
+        if (count_n && cnt_g[gi] == count_n) cnt_g[gi] = 0;  // window purged
       }
     }
   }

@@ -85,14 +85,16 @@ __global__ __launch_bounds__(256) void gen_events_kernel(
     uint64_t* __restrict__ keys, int64_t* __restrict__ ts, uint64_t* __restrict__ vals,
     int64_t n, uint64_t seed, uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
     double span_per_event, uint64_t disorder_p1, int64_t val_lo, uint64_t val_span,
-    int32_t mode) {
+    int32_t mode, double zipf_s) {
   // mode bit 0: values as f64 bits; bit 1: int32 key ids (the columnar sources' dictionary ids)
+  // zipf_s > 0: skewed keys (key_of_draw: power law, rank 0 hottest); 0: uniform.
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint64_t r = rng64(seed, stream_id, idx0 + (uint64_t)i);
     const uint64_t r2 = mix64(r);
     const uint64_t r3 = mix64(r2);
-    const uint64_t key = __umul64hi(r, nkeys);  // multiply-shift: uniform in [0, nkeys)
+    const uint64_t key = zipf_s > 0.0 ? zipf_key(r, nkeys, zipf_s)
+                                      : __umul64hi(r, nkeys);  // multiply-shift: uniform
     if (mode & 2) reinterpret_cast<int32_t*>(keys)[i] = (int32_t)key;
     else keys[i] = key;
     int64_t t = ts_base + (int64_t)((double)i * span_per_event);
@@ -1774,7 +1776,10 @@ __global__ __launch_bounds__(256) void rolling_scan_kernel(
     uint64_t* __restrict__ acc_g, uint32_t* __restrict__ cnt_g, const uint64_t* __restrict__ keys_g,
     ExprProg filt, uint64_t* __restrict__ out_key, uint64_t* __restrict__ out_val,
     int64_t* __restrict__ out_tag, uint32_t* __restrict__ out_n, uint32_t out_cap, int abits,
-    int shift) {
+    int shift, uint32_t count_n) {
+  // count_n > 0: tumbling count windows (countWindow(n), PurgingTrigger(CountTrigger(n))): the
+  // scan is segmented at every n-th element of a key (per-key ordinal % n == 0 starts a window),
+  // only the element completing a window emits, and the state keeps the open window.
   extern __shared__ __attribute__((aligned(16))) double rsm[];  // VM columns [8 + depth][256]
   LdsCol vars{rsm + threadIdx.x, 256};
   LdsCol stack{rsm + kExprVars * 256 + threadIdx.x, 256};
@@ -1807,15 +1812,21 @@ __global__ __launch_bounds__(256) void rolling_scan_kernel(
       const bool in = i < end;
       // perm == nullptr: values were sorted along with the keys.
       uint64_t v = in ? agg_lift(AGG, vals[perm ? perm[i] : i]) : 0;
-      // Inclusive wave scan (Hillis-Steele) over the ordered chunk.
+      // Inclusive wave scan (Hillis-Steele) over the ordered chunk; with count windows a
+      // segmented scan (f: a window starts at or before this lane within the chunk).
+      int f = count_n && (cnt + (uint32_t)lane) % count_n == 0;
       for (int o = 1; o < 64; o <<= 1) {
         const uint64_t y = __shfl_up(v, o);
-        if (lane >= o && in) v = roll_combine<AGG>(y, v);
+        const int g = __shfl_up(f, o);
+        if (lane >= o && in && !f) {
+          v = roll_combine<AGG>(y, v);
+          f = g;
+        }
       }
-      const uint64_t post = have ? roll_combine<AGG>(carry, v) : v;
-      const uint32_t pcount = cnt + (uint32_t)(lane + 1);
+      const uint64_t post = have && !f ? roll_combine<AGG>(carry, v) : v;
+      const uint32_t pcount = count_n ? count_n : cnt + (uint32_t)(lane + 1);
       const uint32_t nin = (end - b0) < 64 ? (end - b0) : 64;
-      bool emit = in;
+      bool emit = in && (!count_n || (cnt + (uint32_t)lane + 1) % count_n == 0);
       if (in && filt.ncode) {
         vars.set(0, agg_result_f64(AGG, post, pcount));
         vars.set(1, (double)pcount);
@@ -1844,7 +1855,7 @@ __global__ __launch_bounds__(256) void rolling_scan_kernel(
     }
     if (lane == 0) {
       if (AGG != AGG_COUNT) acc_g[slot] = carry;
-      cnt_g[slot] = cnt;
+      cnt_g[slot] = count_n ? cnt % count_n : cnt;
     }
   }
 }
@@ -2671,12 +2682,12 @@ int device_count() {
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
-                int32_t val_f64, intptr_t stream) {
+                int32_t val_f64, double zipf_s, intptr_t stream) {
   if (n <= 0) return;
   hipLaunchKernelGGL(gen_events_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, keys, ts, vals, n, seed, stream_id, idx0, nkeys, ts_base,
                      (double)ts_span / (double)n, (uint64_t)(disorder + 1), val_lo,
-                     (uint64_t)val_span, val_f64);
+                     (uint64_t)val_span, val_f64, zipf_s);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -3061,24 +3072,27 @@ static void launch_roll(const int64_t* sk, const int64_t* perm, const uint64_t* 
                         uint64_t* acc_g, uint32_t* cnt_g, const uint64_t* keys_g,
                         const ExprProg& filt, uint64_t* ok, uint64_t* ov, int64_t* ot,
                         uint32_t* on, uint32_t cap, int grid, size_t lds, int abits, int shift,
-                        hipStream_t s) {
+                        uint32_t count_n, hipStream_t s) {
   hipLaunchKernelGGL(rolling_scan_kernel<AGG>, dim3(grid), dim3(256), lds, s, sk, perm, vals, n_in,
-                     heads, n_heads, acc_g, cnt_g, keys_g, filt, ok, ov, ot, on, cap, abits, shift);
+                     heads, n_heads, acc_g, cnt_g, keys_g, filt, ok, ov, ot, on, cap, abits, shift,
+                     count_n);
 }
 
 void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_t* vals,
                   const uint32_t* n_in, const uint32_t* heads, const uint32_t* n_heads,
                   int64_t max_segments, uint64_t* acc_g, uint32_t* cnt_g, const uint64_t* keys_g,
                   const ExprProg& filt, uint64_t* out_key, uint64_t* out_val, int64_t* out_tag,
-                  uint32_t* out_n, uint32_t out_cap, int abits, int shift, intptr_t stream) {
+                  uint32_t* out_n, uint32_t out_cap, int abits, int shift, intptr_t stream,
+                  uint32_t count_n) {
   check_roll_layout(abits, shift);
   const int grid = grid_for(max_segments * 64, 256, 4096);
   const size_t lds = (size_t)(kExprVars + filt.depth) * 256 * sizeof(double);
   hipStream_t s = (hipStream_t)stream;
   switch (agg) {
-#define MXS_R(A) case A: launch_roll<A>(sk, perm, vals, n_in, heads, n_heads, acc_g, cnt_g, keys_g, filt, out_key, out_val, out_tag, out_n, out_cap, grid, lds, abits, shift, s); break;
+#define MXS_R(A) case A: launch_roll<A>(sk, perm, vals, n_in, heads, n_heads, acc_g, cnt_g, keys_g, filt, out_key, out_val, out_tag, out_n, out_cap, grid, lds, abits, shift, count_n, s); break;
     MXS_R(AGG_SUM_I64) MXS_R(AGG_SUM_F64) MXS_R(AGG_MIN_I64) MXS_R(AGG_MAX_I64)
     MXS_R(AGG_MIN_F64) MXS_R(AGG_MAX_F64) MXS_R(AGG_COUNT)
+    MXS_R(AGG_AVG_I64) MXS_R(AGG_AVG_F64)
 #undef MXS_R
     default: throw std::runtime_error("rolling_scan: unsupported aggregate");
   }

@@ -12,6 +12,7 @@
 // Reference call sites: chapter2/src/main/java/me/zjy/ComputeCpuMax.java:26 (keyBy),
 // chapter3/src/main/java/me/zjy/BandwidthMonitorWithEventTime.java:46 (sliding event-time window).
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #if defined(__HIPCC__)
@@ -63,6 +64,23 @@ struct RecN {
 };
 static_assert(sizeof(RecN) == 8, "RecN must be 8 bytes");
 constexpr uint32_t kNarrowHoleT = 15u;
+// Skewed synthetic keys: a power law with exponent s over ranks [0, nkeys) (rank 0 hottest),
+// by inverting the continuous CDF of x^-s on [1, nkeys + 1] at u = the top 53 bits of r.
+// A Zipf-like workload for hot-key benchmarks; not bit-identical between CPU and GPU.
+MXS_HD uint64_t zipf_key(uint64_t r, uint64_t nkeys, double s) {
+  const double u = (double)((r >> 11) + 1) * (1.0 / 9007199254740992.0);  // (0, 1]
+  const double top = (double)nkeys + 1.0;
+  double x;
+  if (s > 0.999999 && s < 1.000001) {
+    x = exp(u * log(top));
+  } else {
+    const double a = 1.0 - s;
+    x = pow(1.0 + u * (pow(top, a) - 1.0), 1.0 / a);
+  }
+  const double k = floor(x) - 1.0;
+  return k < 0.0 ? 0ull : k >= (double)nkeys ? nkeys - 1 : (uint64_t)k;
+}
+
 MXS_HD bool narrow_fits(uint64_t key, int64_t v, uint32_t t) {
   return key < 0xFFFFFFFFull && v >= -(int64_t(1) << 27) && v < (int64_t(1) << 27) &&
          t < kNarrowHoleT;

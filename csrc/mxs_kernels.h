@@ -83,7 +83,7 @@ int d2h_async(void* dst, const void* src, size_t bytes, intptr_t stream);
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
-                int32_t val_f64, intptr_t stream);
+                int32_t val_f64, double zipf_s, intptr_t stream);
 void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                const int32_t* jhash_tab, int64_t n, const PartPlan& plan, const int32_t* kg_dest,
                uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap,
@@ -163,7 +163,8 @@ void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_
                   const uint32_t* n_in, const uint32_t* heads, const uint32_t* n_heads,
                   int64_t max_segments, uint64_t* acc_g, uint32_t* cnt_g, const uint64_t* keys_g,
                   const ExprProg& filt, uint64_t* out_key, uint64_t* out_val, int64_t* out_tag,
-                  uint32_t* out_n, uint32_t out_cap, int abits, int shift, intptr_t stream);
+                  uint32_t* out_n, uint32_t out_cap, int abits, int shift, intptr_t stream,
+                  uint32_t count_n = 0);
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
                  int64_t proc_now, int64_t* red, const uint32_t* flags, intptr_t stream);
 void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt,
@@ -182,7 +183,7 @@ int get_threads();
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
-                int32_t val_f64);
+                int32_t val_f64, double zipf_s);
 void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                const int32_t* jhash_tab, int64_t n, const PartPlan& plan, const int32_t* kg_dest,
                uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap);
@@ -200,7 +201,7 @@ void step_begin(uint32_t* cursor, int nb, int64_t* stats);
 void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bucket_cap,
                   int cap_log2, int agg, uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g,
                   uint32_t* flags, const ExprProg& filt, uint64_t* out_key, uint64_t* out_val,
-                  int64_t* out_tag, uint32_t* out_n, uint32_t out_cap);
+                  int64_t* out_tag, uint32_t* out_n, uint32_t out_cap, uint32_t count_n = 0);
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
                  int64_t proc_now, int64_t* red, const uint32_t* flags);
 void keygroups(const uint64_t* keys, int64_t n, int hash_mode, const int32_t* jhash, int max_par,

@@ -46,7 +46,7 @@ int main() {
   for (int step = 0; step < 6; ++step) {
     const int64_t m = step == 3 ? 0 : n;  // one empty batch
     cpu::gen_events(keys.data(), ts.data(), vals.data(), m, 7, 0, (uint64_t)step * n, 1500,
-                    step * 1000, 1000, 400, 0, 1000, 0);
+                    step * 1000, 1000, 400, 0, 1000, 0, 0.0);
     if (step == 5)
       for (int64_t i = 0; i < m; i += 50) ts[i] -= 4000;  // late data
     cpu::gen_vectors(vec.data(), m, dim, 7, 0, (uint64_t)step * n, -10.0f, 100.0f);

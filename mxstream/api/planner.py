@@ -241,6 +241,9 @@ def plan(env, sinks):
         ws = meta["stream"]
         spec = meta["spec"]
         a = ws.assigner
+        if type(a) is W.GlobalWindows:
+            _lower_count_window(env, t, ws, spec, meta, children)
+            continue
         session = type(a) is W.EventTimeSessionWindows
         if session and ws._late_tag is not None:
             continue  # late side output of merging windows: host operator
@@ -295,6 +298,81 @@ def plan(env, sinks):
         if not session and kind in ("sum", "min", "max") and result == "tuple":
             _fuse_window_epilogue(env, t, children, key_pos, val_pos, ok_arities)
     return sinks
+
+
+def _count_window_size(ws) -> int | None:
+    """n of a tumbling count window: GlobalWindows + PurgingTrigger(CountTrigger(n)), no evictor
+    (KeyedStream.countWindow(n)); None for anything else (sliding count windows use an evictor)."""
+    tr = ws._trigger
+    if ws._evictor is not None or not isinstance(tr, W.PurgingTrigger):
+        return None
+    inner = tr.nested
+    if type(inner) is not W.CountTrigger or not isinstance(inner.count, int) or inner.count < 1:
+        return None
+    return inner.count
+
+
+def _lower_count_window(env, t, ws, spec, meta, children) -> None:
+    """keyBy(k).countWindow(n).sum/min/max(p) | reduce(field-wise sum) | aggregate(avg) ->
+    NativeCountWindowOp (segmented-scan count windows on the GPU / C++ twin)."""
+    n = _count_window_size(ws)
+    if n is None or ws.keyed is None or ws.keyed.key_pos is None or ws._late_tag is not None:
+        return
+    key_pos = ws.keyed.key_pos
+    kind = val_pos = None
+    ok: set[int] = set()
+    result = "tuple"
+    if meta.get("native_hint") and meta["native_hint"][0] in ("sum", "min", "max"):
+        kind, val_pos = meta["native_hint"]
+        ok = {ar for ar in range(2, 9) if ar > max(key_pos, val_pos)
+              and _dead_fields_ok(t, children, key_pos, val_pos, ar)}
+    elif spec.kind == "aggregate" and spec.window_fn is None and hasattr(spec.fn, "native"):
+        kind, val_pos = spec.fn.native
+        result = "value"
+        ok = set(range(max(key_pos, val_pos) + 1, 64))
+    elif spec.kind == "aggregate" and spec.window_fn is None:
+        for ar in range(2, 9):
+            if ar <= key_pos:
+                continue
+            p = trace_avg_aggregate(spec.fn, ar)
+            if p is not None and p != key_pos:
+                kind, val_pos, result = "avg", p, "value"
+                ok.add(ar)
+    elif spec.kind == "reduce" and spec.window_fn is None:
+        for ar in range(2, 9):
+            p = trace_fieldwise_reduce(spec.fn, ar)
+            if p is None or p == key_pos or ar <= key_pos:
+                continue
+            if val_pos is not None and p != val_pos:
+                continue
+            if _dead_fields_ok(t, children, key_pos, p, ar):
+                kind, val_pos = "sum", p
+                ok.add(ar)
+    if kind not in ("sum", "min", "max", "count", "avg") or not ok:
+        return
+    from ..runtime.native_ops import NativeCountWindowOp
+    from .tuples import Tuple
+
+    if result == "value":
+        def builder(template, res, key):
+            return res
+    else:
+        def builder(template, res, key, vp=val_pos):
+            row = list(template)
+            row[vp] = res
+            return Tuple(row)
+
+    fallback = t.factory
+    device = env.config.device
+    key_fn = ws.keyed.key_fn
+
+    def factory():
+        return NativeCountWindowOp(count=n, result_builder=builder, ok_arities=ok, key_fn=key_fn,
+                                   key_pos=key_pos, val_pos=val_pos, kind=kind, device=device,
+                                   fallback_factory=fallback)
+
+    t.factory = factory
+    t.meta = dict(t.meta, native=True)
 
 
 def _expr_vars(e) -> set:

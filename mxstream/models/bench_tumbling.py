@@ -47,6 +47,9 @@ class TumblingBenchConfig:
     # Key ids as an int32 column (the columnar sources' dictionary ids) instead of int64: fewer
     # bytes, yet the partition measured slower on the same box (profiles/r2_partition_pairs.md).
     key32: bool = False
+    # > 0: power-law skewed keys with this exponent (hot-key contention);
+    # 0: uniform keys (the BASELINE config).
+    zipf: float = 0.0
 
 
 class TumblingWindowBench:
@@ -91,7 +94,7 @@ class TumblingWindowBench:
                      idx0=self.step_idx * cfg.batch, nkeys=cfg.keys,
                      ts_base=self.t0_event + self.step_idx * cfg.step_span_ms,
                      ts_span=cfg.step_span_ms, disorder=cfg.disorder_ms, val_lo=0,
-                     val_span=cfg.val_max)
+                     val_span=cfg.val_max, zipf=cfg.zipf)
         self._ingest.append(t_ingest)
         fired = self.op.process(self.keys, self.ts, self.vals)
         src = self._ingest.pop(0) if self.op.pipeline and len(self._ingest) > 1 else t_ingest

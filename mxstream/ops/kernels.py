@@ -74,8 +74,9 @@ def reset_stats(s: torch.Tensor) -> None:
 
 def gen_events(keys, ts, vals, *, seed: int, stream_id: int, idx0: int, nkeys: int,
                ts_base: int, ts_span: int, disorder: int, val_lo: int, val_span: int,
-               val_f64: bool = False) -> None:
-    """keys: int64, or int32 (dictionary ids, nkeys < 2^31)."""
+               val_f64: bool = False, zipf: float = 0.0) -> None:
+    """keys: int64, or int32 (dictionary ids, nkeys < 2^31). zipf > 0: power-law skewed keys
+    with that exponent (key 0 hottest; csrc/mxs_common.h zipf_key), 0: uniform."""
     n = keys.numel()
     dev = keys.device
     key32 = keys.dtype == torch.int32
@@ -86,7 +87,10 @@ def gen_events(keys, ts, vals, *, seed: int, stream_id: int, idx0: int, nkeys: i
         raise ValueError("nkeys out of range")
     m = load()
     args = (_p(keys), _p(ts), _p(vals), n, seed & (2**64 - 1), stream_id & (2**64 - 1), idx0,
-            nkeys, ts_base, ts_span, disorder, val_lo, val_span, int(val_f64) | (2 if key32 else 0))
+            nkeys, ts_base, ts_span, disorder, val_lo, val_span, int(val_f64) | (2 if key32 else 0),
+            float(zipf))
+    if zipf < 0:
+        raise ValueError("zipf exponent must be >= 0")
     if _is_gpu(keys):
         m.gpu_gen_events(*args, _stream(keys))
     else:

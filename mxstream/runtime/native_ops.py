@@ -448,26 +448,39 @@ class NativeRollingOp(_ColumnInput, Operator):
         dev = self.op.device
         rows = self.op.process(torch.from_numpy(np.ascontiguousarray(kid, dtype=np.int64)).to(dev),
                                torch.from_numpy(np.ascontiguousarray(vv).view(np.int64)).to(dev))
-        order = np.argsort(rows.tags & 0xFFFFFFFF, kind="stable")  # back to input order
+        ts = cb.ts.tolist() if cb.ts is not None else None
+        return self._rows_out(rows, (lambda i: ts[i]) if ts is not None else (lambda i: LONG_MIN))
+
+    def _result(self, raw: int):
+        return float(np.int64(raw).view(np.float64)) if self.is_float else raw
+
+    def _value(self, k: int, res):
         from ..api.tuples import Tuple
+
+        row = list(self.templates[k])
+        row[self.val_pos] = res
+        return Tuple(row)
+
+    def _out_ts(self, ts: int) -> int:
+        return ts
+
+    def _rows_out(self, rows, ts_of) -> list:
+        """Engine rows -> output records in input order (by arrival tag)."""
         from ..utils.hashing import flink_murmur
 
+        order = np.argsort(rows.tags & 0xFFFFFFFF, kind="stable")  # back to input order
         P, MP = self.ctx.parallelism, self.ctx.max_parallelism
         keys = rows.keys[order].tolist()
-        vals = rows.values[order]
-        res = (vals.view(np.float64) if self.is_float else vals).tolist()
+        raws = rows.values[order].tolist()
         idx = (rows.tags[order] & 0xFFFFFFFF).tolist()
-        ts = cb.ts.tolist() if cb.ts is not None else None
         subs: dict = {}
         out = []
-        for k, r, i in zip(keys, res, idx):
-            row = list(self.templates[k])
-            row[self.val_pos] = r
+        for k, raw, i in zip(keys, raws, idx):
             sub = subs.get(k)
             if sub is None:
                 key_obj = self.dict.get(k) if self.str_keys else k
                 sub = subs[k] = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
-            out.append(Rec(Tuple(row), ts[i] if ts is not None else LONG_MIN, sub))
+            out.append(Rec(self._value(k, self._result(raw)), self._out_ts(ts_of(i)), sub))
         return out
 
     def _run(self, recs: list) -> list:
@@ -508,23 +521,7 @@ class NativeRollingOp(_ColumnInput, Operator):
         dev = self.op.device
         rows = self.op.process(torch.from_numpy(kid).to(dev),
                                torch.from_numpy(vv.view(np.int64)).to(dev))
-        order = np.argsort(rows.tags & 0xFFFFFFFF, kind="stable")  # back to input order
-        from ..api.tuples import Tuple
-        from ..utils.hashing import flink_murmur
-
-        P, MP = self.ctx.parallelism, self.ctx.max_parallelism
-        out = []
-        for j in order.tolist():
-            k = int(rows.keys[j])
-            raw = int(rows.values[j])
-            res = float(np.int64(raw).view(np.float64)) if self.is_float else raw
-            row = list(self.templates[k])
-            row[self.val_pos] = res
-            key_obj = self.dict.get(k) if self.str_keys else k
-            sub = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
-            idx = int(rows.tags[j]) & 0xFFFFFFFF
-            out.append(Rec(Tuple(row), recs[idx].ts, sub))
-        return out
+        return self._rows_out(rows, lambda i: recs[i].ts)
 
     def process(self, items):
         if self.fallback is not None:
@@ -563,6 +560,68 @@ class NativeRollingOp(_ColumnInput, Operator):
         if "engine" in snap:
             self._build(1.0 if snap["is_float"] else 1)
             self.op.restore_state(snap["engine"]["columns"], snap["engine"]["meta"])
+
+
+class NativeCountWindowOp(NativeRollingOp):
+    """``keyBy(k).countWindow(n)`` with an incremental sum/min/max/reduce or (count, sum) average
+    (GlobalWindows + PurgingTrigger(CountTrigger(n)); countWindow in chapter2/README.md:78 and
+    chapter3/README.md:4) on the native ``KeyedRollingOperator`` in count-window mode: the
+    segmented wave scan emits one row per completed window, in input order of the completing
+    elements, with the GlobalWindow's timestamp (Long.MAX_VALUE). Only lowered when the fields
+    other than key and value are dead downstream (planner), like the time windows."""
+
+    name = "Window(native count)"
+
+    def __init__(self, *, count: int, result_builder, ok_arities=None, **kw):
+        super().__init__(**kw)
+        self.count = int(count)
+        self.result_builder = result_builder
+        self.ok_arities = ok_arities
+
+    def _build(self, v) -> bool:
+        from .rolling_operator import KeyedRollingOperator
+
+        if isinstance(v, bool) or not isinstance(v, (int, float)):
+            return False
+        self.is_float = isinstance(v, float)
+        agg = {("sum", False): K.AGG_SUM_I64, ("sum", True): K.AGG_SUM_F64,
+               ("max", False): K.AGG_MAX_I64, ("max", True): K.AGG_MAX_F64,
+               ("min", False): K.AGG_MIN_I64, ("min", True): K.AGG_MIN_F64,
+               ("count", False): K.AGG_COUNT, ("count", True): K.AGG_COUNT,
+               ("avg", False): K.AGG_AVG_I64, ("avg", True): K.AGG_AVG_F64}[(self.kind, self.is_float)]
+        self.op = KeyedRollingOperator(agg=agg, device=torch.device(self.device),
+                                       max_keys=self.max_keys, parallelism=1,
+                                       batch_capacity=1024, count_window=self.count)
+        return True
+
+    def _result(self, raw: int):
+        if self.kind == "count":
+            return int(raw)
+        if self.kind == "avg":
+            s = float(np.int64(raw).view(np.float64)) if self.is_float else float(raw)
+            return s / self.count
+        return super()._result(raw)
+
+    def _value(self, k: int, res):
+        key_obj = self.dict.get(k) if self.str_keys else k
+        return self.result_builder(self.templates[k], res, key_obj)
+
+    def _out_ts(self, ts: int) -> int:
+        return LONG_MAX  # GlobalWindow.maxTimestamp()
+
+    def _run_columns(self, batches: list) -> list:
+        if self.ok_arities and self.op is None and len(batches[0].kinds) not in self.ok_arities:
+            self._to_fallback()
+            return self.fallback.process(expand_columns(batches))
+        return super()._run_columns(batches)
+
+    def _run(self, recs: list) -> list:
+        if recs and self.ok_arities and self.op is None:
+            v0 = expand_columns(recs[:1])[0].value if not isinstance(recs[0], ColumnBatch) else None
+            if v0 is not None and (not isinstance(v0, tuple) or len(v0) not in self.ok_arities):
+                self._to_fallback()
+                return self.fallback.process(expand_columns(recs))
+        return super()._run(recs)
 
 
 class NativeSessionOp(NativeWindowOp):

@@ -39,12 +39,21 @@ class KeyedRollingOperator:
     def __init__(self, *, agg: int, device="cpu", comm: Comm | None = None,
                  max_keys: int = 1 << 16, parallelism: int | None = None,
                  max_parallelism: int = 128, batch_capacity: int = 1 << 20,
-                 cap_log2: int | None = None, filter_prog: E.Program = E.EMPTY, emit_capacity: int | None = None):
+                 cap_log2: int | None = None, filter_prog: E.Program = E.EMPTY, emit_capacity: int | None = None,
+                 count_window: int = 0):
+        """count_window = n > 0: tumbling count windows instead of a rolling aggregate
+        (``keyBy(..).countWindow(n)`` with an incremental reduce/aggregate: GlobalWindows +
+        PurgingTrigger(CountTrigger(n)), chapter2/README.md:78) -- a row is emitted when a key's
+        open window reaches n elements (value = the window's aggregate; for avg the sum, the
+        count is n), and the state keeps each key's open window."""
         self.device = K.resolve_device(device)
         self.comm = comm or LocalComm()
         self.world, self.rank = self.comm.world, self.comm.rank
         self.agg = agg
-        if agg in (K.AGG_AVG_F64, K.AGG_AVG_I64):
+        self.count_window = int(count_window)
+        if self.count_window < 0 or self.count_window >= (1 << 31):
+            raise ValueError("count window size out of range")
+        if agg in (K.AGG_AVG_F64, K.AGG_AVG_I64) and not self.count_window:
             raise ValueError("rolling avg is not a Flink rolling aggregate")
         self.parallelism = parallelism or self.world
         self.max_parallelism = max_parallelism
@@ -144,7 +153,7 @@ class KeyedRollingOperator:
                            min(n, self.nslots), self.acc_g.data_ptr(), self.cnt_g.data_ptr(),
                            self.keys_g.data_ptr(), code, consts, self.out_key.data_ptr(),
                            self.out_val.data_ptr(), self.out_tag.data_ptr(),
-                           self.out_n.data_ptr(), cap, shift, shift, st)
+                           self.out_n.data_ptr(), cap, shift, shift, st, self.count_window)
         return self._emit(to_host)
 
     def process(self, keys: torch.Tensor, vals: torch.Tensor, to_host: bool = True):
@@ -216,14 +225,16 @@ class KeyedRollingOperator:
                                    self.acc_g.data_ptr(), self.cnt_g.data_ptr(),
                                    self.keys_g.data_ptr(), code, consts, self.out_key.data_ptr(),
                                    self.out_val.data_ptr(), self.out_tag.data_ptr(),
-                                   self.out_n.data_ptr(), cap, abits, shift, st)
+                                   self.out_n.data_ptr(), cap, abits, shift, st,
+                                   self.count_window)
         else:
             m.cpu_rolling_rows(self.recv.data_ptr(), self.recv_counts.data_ptr(), self.world,
                                self.nsub, self.bucket_cap, self.cap_log2, self.agg,
                                self.keys_g.data_ptr(), self.acc_g.data_ptr(),
                                self.cnt_g.data_ptr(), self.flags.data_ptr(), code, consts,
                                self.out_key.data_ptr(), self.out_val.data_ptr(),
-                               self.out_tag.data_ptr(), self.out_n.data_ptr(), cap)
+                               self.out_tag.data_ptr(), self.out_n.data_ptr(), cap,
+                               self.count_window)
         return self._emit(to_host)
 
     def check(self) -> int:
@@ -276,12 +287,12 @@ class KeyedRollingOperator:
         cols = {"key": keys.cpu().numpy(), "acc": self.acc_g[live].cpu().numpy(),
                 "cnt": self.cnt_g[live].cpu().numpy()}
         meta = {"kind": "rolling", "agg": self.agg, "records_in": self.records_in,
-                "steps": self.steps}
+                "steps": self.steps, "count_window": self.count_window}
         return OperatorSnapshot(kg, cols, meta)
 
     def restore_state(self, rows: dict, meta: dict) -> None:
-        if meta["agg"] != self.agg:
-            raise ValueError("checkpoint aggregate does not match the operator")
+        if meta["agg"] != self.agg or meta.get("count_window", 0) != self.count_window:
+            raise ValueError("checkpoint aggregate / count window does not match the operator")
         self.records_in, self.steps = meta["records_in"], meta["steps"]
         self.keys_g.fill_(-1)
         self.acc_g.zero_()

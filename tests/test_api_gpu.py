@@ -41,3 +41,21 @@ def test_native_operators_match_host_on_gpu():
             Counter(N._run_sessions(ev, 1500, 500, 2000, "off"))
         assert Counter(N._run_median(ev, 4000, 2000, 1000, 3000, "auto")) == \
             Counter(N._run_median(ev, 4000, 2000, 1000, 3000, "off"))
+
+
+def test_native_count_windows_match_host_on_gpu():
+    from collections import Counter
+
+    import numpy as np
+
+    import test_api_native as N
+
+    rng = np.random.default_rng(7)
+    keys = ["a", "b", "c", "10.8.22.1"]
+    for trial in range(8):
+        ev = [(keys[int(rng.integers(0, 4))], int(rng.integers(0, 1000)))
+              for _ in range(int(rng.integers(5, 80)))]
+        n = int(rng.integers(1, 7))
+        for agg in ("reduce", "max", "sum", "avg"):
+            assert Counter(N._run_count(ev, n, "auto", agg)) == \
+                Counter(N._run_count(ev, n, "off", agg))

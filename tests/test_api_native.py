@@ -179,3 +179,61 @@ def test_native_median_equals_host(events, size_k, slide_div, bound, lateness):
     a = _run_median(events, size, size // slide_div, bound, lateness, "off")
     b = _run_median(events, size, size // slide_div, bound, lateness, "auto")
     assert Counter(a) == Counter(b)
+
+
+def _run_count(events, n, native, agg):
+    from mxstream.api.functions import AggregateFunction
+
+    class Avg(AggregateFunction):
+        def create_accumulator(self):
+            return Tuple2(0, 0)
+
+        def add(self, v, acc):
+            return Tuple2(acc.f0 + 1, acc.f1 + v.f1)
+
+        def get_result(self, acc):
+            return acc.f1 / acc.f0
+
+        def merge(self, a, b):
+            return Tuple2(a.f0 + b.f0, a.f1 + b.f1)
+
+    out = []
+    env = StreamExecutionEnvironment(4, clock=ManualClock(0)).set_output(out.append)
+    env.config.native = native
+    ws = (env.from_collection(events).map(lambda e: Tuple2(e[0], e[1])).key_by(0)
+          .count_window(n))
+    if agg == "reduce":
+        s = ws.reduce(lambda a, b: Tuple2(a.f0, a.f1 + b.f1))
+    elif agg == "avg":
+        s = ws.aggregate(Avg())
+    else:
+        s = getattr(ws, agg)(1)
+    s.print()
+    env.execute("count")
+    return out
+
+
+@settings(max_examples=50, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(events=st.lists(st.tuples(st.sampled_from(["a", "b", "c", "10.8.22.1"]),
+                                 st.integers(0, 1000)), min_size=1, max_size=60),
+       n=st.integers(1, 6), agg=st.sampled_from(["reduce", "max", "min", "sum", "avg"]))
+def test_native_count_window_equals_host(events, n, agg):
+    """keyBy(0).countWindow(n) (GlobalWindows + PurgingTrigger(CountTrigger(n))): the native
+    segmented-scan path emits exactly the host WindowOperator's lines."""
+    a = _run_count(events, n, "off", agg)
+    b = _run_count(events, n, "auto", agg)
+    assert Counter(a) == Counter(b)
+
+
+def test_native_count_window_is_selected():
+    from mxstream.api import planner
+    from mxstream.runtime.native_ops import NativeCountWindowOp
+
+    env = StreamExecutionEnvironment(4)
+    (env.from_collection([("a", 1)]).key_by(0).count_window(3)
+     .reduce(lambda a, b: Tuple2(a.f0, a.f1 + b.f1)).print())
+    sinks = planner.plan(env, list(env._sinks))
+    from mxstream.runtime.executor import Executor
+
+    ops = [n.factory() for n in Executor._topo(sinks) if n.kind == "op"]
+    assert any(isinstance(o, NativeCountWindowOp) for o in ops)

@@ -351,3 +351,35 @@ def test_int32_keys_gpu_match_cpu(gpu_device, narrow, compact):
                       for r in rows for a, b, c in zip(r.keys, r.raw, r.counts))
 
     assert run(gpu_device, torch.int32) == run("cpu", torch.int64)
+
+
+@pytest.mark.parametrize("zipf,narrow", [(1.2, True), (1.2, False), (0.9, True)])
+def test_hot_keys_gpu_match_cpu(gpu_device, zipf, narrow):
+    """Power-law keys (key 0 carries ~14 % of the events at s = 1.2): LDS atomics on one hot
+    slot, one bucket far above the mean (bucket regrow + step redo) -- the fired rows equal the
+    C++ twin's. The batches are generated once on the CPU and copied to the device."""
+    batches = []
+    for step in range(6):
+        k = torch.empty(400_000, dtype=torch.int64)
+        t = torch.empty_like(k)
+        v = torch.empty_like(k)
+        K.gen_events(k, t, v, seed=21, stream_id=0, idx0=step * 400_000, nkeys=200_000,
+                     ts_base=step * 1000, ts_span=1000, disorder=300, val_lo=0, val_span=3000,
+                     zipf=zipf)
+        batches.append((k, t, v))
+
+    def run(dev):
+        op = KeyedWindowOperator(size=2000, slide=1000, agg=K.AGG_SUM_I64, device=dev,
+                                 max_keys=200_000, batch_capacity=400_000, ooo_bound=300,
+                                 dense_keys=True, narrow=narrow if dev != "cpu" else False)
+        rows = []
+        for k, t, v in batches:
+            rows += op.process(k.to(dev), t.to(dev), v.to(dev))
+        rows += op.finish()
+        return sorted((r.window_start, int(a), int(b), int(c))
+                      for r in rows for a, b, c in zip(r.keys, r.raw, r.counts)), op
+
+    (g, gop), (c, _) = run(gpu_device), run("cpu")
+    assert g == c
+    top = max(x[3] for x in c)
+    assert top > 20_000  # the hot key really is hot (mean count per key and window: ~4)

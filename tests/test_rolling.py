@@ -88,3 +88,56 @@ def test_rolling_gpu_equals_cpu(gpu_device, agg, nkeys, direct):
             tags = op.process(*_gen(d, 1 << 16, nkeys, 9)).tags
             assert len(tags) == 1 << 16 and len(np.unique(tags)) == 1 << 16
     assert res["cuda"] == res["cpu"]
+
+
+def _count_oracle(batches, agg, n):
+    """Tumbling count windows per key (countWindow(n)): one row per n elements."""
+    win, out = {}, {}
+    for keys, vals in batches:
+        for k, v in zip(keys.tolist(), vals.tolist()):
+            w = win.setdefault(k, [])
+            w.append(v)
+            if len(w) == n:
+                r = {K.AGG_SUM_I64: sum(w), K.AGG_MAX_I64: max(w), K.AGG_MIN_I64: min(w),
+                     K.AGG_COUNT: n, K.AGG_AVG_I64: sum(w)}[agg]
+                out.setdefault(k, []).append(r)
+                win[k] = []
+    return out
+
+
+@pytest.mark.parametrize("agg", [K.AGG_SUM_I64, K.AGG_MAX_I64, K.AGG_MIN_I64, K.AGG_COUNT,
+                                 K.AGG_AVG_I64])
+@pytest.mark.parametrize("n", [1, 7, 64, 150])
+def test_count_window_cpu_matches_oracle(agg, n):
+    batches = [_gen("cpu", 3000, 97, s) for s in range(4)]
+    op = KeyedRollingOperator(agg=agg, device="cpu", max_keys=200, batch_capacity=3000,
+                              cap_log2=8, count_window=n)
+    got = {}
+    for keys, vals in batches:
+        for k, v in _per_key(op.process(keys, vals)).items():
+            got.setdefault(k, []).extend(v)
+    assert got == _count_oracle(batches, agg, n)
+    with pytest.raises(ValueError):
+        KeyedRollingOperator(agg=K.AGG_AVG_I64, device="cpu")  # avg only with count windows
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", [K.AGG_SUM_I64, K.AGG_MAX_I64, K.AGG_COUNT, K.AGG_AVG_I64])
+@pytest.mark.parametrize("n", [1, 5, 64, 100, 1000])
+@pytest.mark.parametrize("direct", [True, False])
+def test_count_window_gpu_equals_cpu(gpu_device, agg, n, direct):
+    """The segmented wave scan (window boundaries inside and across 64-element chunks and
+    batches) emits exactly the C++ twin's windows."""
+    res = {}
+    for d in (gpu_device, torch.device("cpu")):
+        op = KeyedRollingOperator(agg=agg, device=d, max_keys=300, batch_capacity=1 << 15,
+                                  count_window=n)
+        op.direct_single_rank = direct
+        got = {}
+        for s in range(3):
+            keys, vals = _gen(d, 1 << 15, 300, s)
+            for k, v in _per_key(op.process(keys, vals)).items():
+                got.setdefault(k, []).extend(v)
+        res[d.type] = got
+    assert res["cuda"] == res["cpu"]
+    assert sum(len(v) for v in res["cpu"].values()) > 0
