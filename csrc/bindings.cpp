@@ -138,6 +138,8 @@ AggPlan make_agg(py::dict d) {
   if (p.ring <= 0 || (p.ring & (p.ring - 1))) throw std::invalid_argument("ring must be 2^k");
   if (p.cap_log2 < 4 || p.cap_log2 > 14) throw std::invalid_argument("cap_log2 out of range");
   if (p.pg <= 0) throw std::invalid_argument("pg must be positive");
+  p.split = d.contains("split") ? d["split"].cast<int32_t>() : 1;
+  if (p.split < 1 || p.split > 1024) throw std::invalid_argument("agg split out of range");
   return p;
 }
 
@@ -228,6 +230,7 @@ PYBIND11_MODULE(_mxs_native, m) {
       .def_readwrite("drop_late", &PartPlan::drop_late);
   py::class_<AggPlan>(m, "AggPlanObj")
       .def(py::init(&make_agg))
+      .def_readwrite("split", &AggPlan::split)
       .def_readwrite("bucket_cap", &AggPlan::bucket_cap)
       .def_readwrite("np_step", &AggPlan::np_step)
       .def_readwrite("pg", &AggPlan::pg)

@@ -738,21 +738,31 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   }
   __syncthreads();
   bool overflow = false;
+  uint32_t mb = 0;  // largest bucket fill seen by this group (the last reserver sees the total)
   for (int b = threadIdx.x; b < nb; b += blockDim.x) {
     const uint32_t c = (run_base[b] + (kCG - 1)) & ~(uint32_t)(kCG - 1);
     uint32_t base = 0;
     if (c) {
       base = atomicAdd(&cursor[b], c);
       if (base + c > plan.bucket_cap) overflow = true;
+      mb = base + c > mb ? base + c : mb;
     }
     run_base[b] = base;
     resv[b] = c;
   }
-  if (threadIdx.x == 0) wsum[18] = 0;
+  if (threadIdx.x == 0) {
+    wsum[18] = 0;
+    wsum[19] = 0;
+  }
   __syncthreads();
   if (overflow) wsum[18] = 1;
+  if (mb) atomicMax(&wsum[19], mb);
   __syncthreads();
   const bool any_ovf = wsum[18] != 0;
+  // Max bucket fill of the step (stats): the host splits an oversized sub-table's aggregation
+  // over several workgroups (hot keys, AggPlan.split).
+  if (threadIdx.x == 0 && wsum[19])
+    atomicMax((unsigned long long*)&stats[kStatMaxBucket], (unsigned long long)wsum[19]);
   const uint32_t bcap = plan.bucket_cap;
 
   int64_t tmax = INT64_MIN, nlate = 0, nacc = 0;
@@ -1103,6 +1113,8 @@ __device__ __forceinline__ uint32_t pk_cnt(uint64_t p) {
 }
 
 // DENSE: directly addressed dense key ids (AggPlan.dense_bits): no LDS key table, no probe.
+constexpr uint32_t kAggSliceMin = 131072;  // records per workgroup of a split sub-table
+
 template <int AGG, int RW, bool PK = false, bool DENSE = false>
 __global__ __launch_bounds__(1024) void window_agg_kernel(
     const void* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
@@ -1111,7 +1123,20 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
   static_assert(!PK || ((AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) && RW <= 2),
                 "packed accumulators: integer sum/avg of 8/16-byte records only");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int sub = blockIdx.x;
+  // Split sub-tables (AggPlan.split, hot keys): workgroup `slice` of `split` takes an equal
+  // share of the sub-table's records; the shares merge into the state with atomic adds.
+  const int split = p.split;  // launcher guarantees 1 unless the layout/aggregate allows it
+  const int sub = split > 1 ? (int)blockIdx.x / split : (int)blockIdx.x;
+  const int slice = split > 1 ? (int)blockIdx.x % split : 0;
+  int nact = 1;
+  if (split > 1) {
+    uint32_t ca = counts[sub];
+    ca = ca < p.bucket_cap ? ca : p.bucket_cap;
+    nact = (int)((ca + kAggSliceMin - 1) / kAggSliceMin);
+    nact = nact < 1 ? 1 : nact > split ? split : nact;
+    if (slice >= nact) return;  // workgroup-uniform: before any barrier
+  }
+  const bool shared_sub = nact > 1;
   const uint32_t cap = 1u << p.cap_log2;
   const uint32_t mask = cap - 1;
   uint64_t* skeys = (uint64_t*)smem;                   // unused when DENSE
@@ -1150,8 +1175,11 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
       uint32_t c = counts[(size_t)src * p.nsub + sub];
       c = c < p.bucket_cap ? c : p.bucket_cap;
       const size_t seg0 = ((size_t)src * p.nsub + sub) * p.bucket_cap;
+      // This workgroup's share [e_lo, c) of the segment (all of it unless split).
+      const uint32_t e_lo = shared_sub ? (uint32_t)((uint64_t)c * slice / nact) : 0u;
+      if (shared_sub) c = (uint32_t)((uint64_t)c * (slice + 1) / nact);
       // kAggU independent record loads in flight per thread before the LDS work.
-      for (uint32_t e0 = threadIdx.x; e0 < c; e0 += blockDim.x * kAggU) {
+      for (uint32_t e0 = e_lo + threadIdx.x; e0 < c; e0 += blockDim.x * kAggU) {
         Rec rr[kAggU];
 #pragma unroll
         for (int u = 0; u < kAggU; ++u) {
@@ -1216,8 +1244,10 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
         if (dc[w]) {
           const int64_t pane = p.pane_base + q0 + (i >> p.cap_log2);
           gi[w] = (size_t)(pane & (p.ring - 1)) * nslots + sbase + (i & mask);
-          oc[w] = cnt_g[gi[w]];
-          if (AGG != AGG_COUNT) oa[w] = acc_g[gi[w]];
+          if (!shared_sub) {
+            oc[w] = cnt_g[gi[w]];
+            if (AGG != AGG_COUNT) oa[w] = acc_g[gi[w]];
+          }
         }
       }
       bool late[kWB];
@@ -1227,8 +1257,14 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
         if (!dc[w]) continue;
         const uint32_t i = i0 + (uint32_t)w * blockDim.x;
         const uint64_t d = PK ? (uint64_t)pk_sum(sacc[i]) : lds_export<AGG>(sacc[i]);
-        if (AGG != AGG_COUNT) acc_g[gi[w]] = oc[w] ? agg_combine(AGG, oa[w], d) : d;
-        cnt_g[gi[w]] = oc[w] + dc[w];
+        if (shared_sub) {
+          // Additive aggregates only (launcher): an empty slot's accumulator is 0.
+          if (AGG != AGG_COUNT) atomicAdd((unsigned long long*)&acc_g[gi[w]], (unsigned long long)d);
+          atomicAdd(&cnt_g[gi[w]], dc[w]);
+        } else {
+          if (AGG != AGG_COUNT) acc_g[gi[w]] = oc[w] ? agg_combine(AGG, oa[w], d) : d;
+          cnt_g[gi[w]] = oc[w] + dc[w];
+        }
         if (p.pane_base + q0 + (int64_t)(i >> p.cap_log2) <= p.fired_hi) {
           dirty_g[gi[w]] = 1;
           late[w] = true;
@@ -2894,8 +2930,15 @@ static void launch_agg_v(const Rec* recs, const uint32_t* counts, const AggPlan&
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  hipLaunchKernelGGL((window_agg_kernel<AGG, RW, PK, DENSE>), dim3(p.nsub), dim3(1024), lds, s,
-                     (const void*)recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ, flags);
+  // Split only what the kernel's atomic merge supports: dense ids (no LDS key table to share),
+  // one source segment, additive integer aggregates, no touched-slot list.
+  AggPlan q = p;
+  const bool split_ok = DENSE && p.nsrc == 1 && !p.dlist &&
+                        (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64 || AGG == AGG_COUNT);
+  q.split = split_ok && p.split > 1 ? p.split : 1;
+  hipLaunchKernelGGL((window_agg_kernel<AGG, RW, PK, DENSE>), dim3(p.nsub * q.split), dim3(1024),
+                     lds, s, (const void*)recs, counts, q, keys_g, acc_g, cnt_g, dirty_g, occ,
+                     flags);
 }
 
 template <int AGG, bool DENSE>

@@ -532,7 +532,7 @@ MXS_HD bool rel_pane(int64_t ts, const PartPlan& p, uint32_t* t_out, int64_t* pa
 //       bit1 an element's pane is not representable
 // Panes in [1]/[2] are relative to the step's pane base.
 constexpr int kStatMaxTs = 0, kStatMinPane = 1, kStatMaxPane = 2, kStatLate = 3, kStatOverflow = 4,
-              kStatAccepted = 5, kStatCount = 8;
+              kStatAccepted = 5, kStatMaxBucket = 6, kStatCount = 8;
 
 
 // ------------------------------------------------------------------------------------------

@@ -35,6 +35,10 @@ struct AggPlan {
   uint32_t* slot_mark;  // [nslots] 1 = listed
   int32_t dense_bits;   // > 0: directly addressed dense key ids (slot = dense_slot(key))
   uint32_t dense_mul;
+  // Hot sub-tables (dense ids, one source, additive aggregates, no touched-slot list): up to
+  // `split` workgroups share one sub-table's records (>= kAggSliceMin each) and merge into the
+  // state with atomic adds; 1 = one workgroup per sub-table.
+  int32_t split;
 };
 
 // Plan of one window firing.

@@ -16,7 +16,8 @@ from .native import load
 
 REC_WORDS = 3  # 24-byte record = 3 x int64 words
 STAT_COUNT = 8
-STAT_MAXTS, STAT_MINPANE, STAT_MAXPANE, STAT_LATE, STAT_OVERFLOW, STAT_ACCEPTED = range(6)
+STAT_MAXTS, STAT_MINPANE, STAT_MAXPANE, STAT_LATE, STAT_OVERFLOW, STAT_ACCEPTED, STAT_MAXBUCKET = range(7)
+AGG_SLICE = 131072  # records per workgroup of a split sub-table (csrc kAggSliceMin)
 
 I64_MIN = -(1 << 63)
 I64_MAX = (1 << 63) - 1
@@ -177,6 +178,7 @@ class AggPlan:
     slot_mark: int = 0   # ... and the per-slot listed marks
     dense_bits: int = 0  # > 0: directly addressed dense key ids (see PartitionPlan)
     dense_mul: int = 0
+    split: int = 1       # workgroups sharing an oversized sub-table (hot keys; GPU, see AGG_SLICE)
 
     def as_dict(self) -> dict:
         return dict(self.__dict__)

@@ -219,6 +219,7 @@ class _Back:
     ccap: int = 0
     hard: int = 0
     chk_ev: object = None
+    maxb: int = 0  # largest bucket fill of the step's partition (0: not reported)
 
 
 @dataclass
@@ -825,7 +826,8 @@ class KeyedWindowOperator:
         if self.side_output_late and st[K.STAT_LATE]:
             nl = min(int(st[K.STAT_LATE]), self.late_idx.numel())
             self.late_side.append(self.late_idx[:nl].cpu().numpy().copy())
-        b = _Back(par=f.par, n=f.n, old_wm=f.old_wm, rw=f.rw, pane_base=f.pane_base)
+        b = _Back(par=f.par, n=f.n, old_wm=f.old_wm, rw=f.rw, pane_base=f.pane_base,
+                  maxb=int(st[K.STAT_MAXBUCKET]))
         if qmin <= qmax:
             gmin, gmax = f.pane_base + qmin, f.pane_base + qmax
             lo = gmin if self.min_live_pane is None else min(self.min_live_pane, gmin)
@@ -889,6 +891,9 @@ class KeyedWindowOperator:
                                   p_lo=b.qmin, fired_hi=b.fired_hi, combined=combined,
                                   rec_words=3 if combined else b.rw)
                 aplan.dense_bits, aplan.dense_mul = self.dense_bits, self.dense_mul
+                # Hot keys: a sub-table holding more than AGG_SLICE records is shared by several
+                # workgroups (the launcher applies it where the atomic merge is exact).
+                aplan.split = min(64, max(1, -(-b.maxb // K.AGG_SLICE))) if not combined else 1
                 if self.dlist is not None:
                     aplan.dlist, aplan.dlist_n = self.dlist.data_ptr(), self.dlist_n.data_ptr()
                     aplan.slot_mark = self.slot_mark.data_ptr()
@@ -932,6 +937,7 @@ class KeyedWindowOperator:
         ap = self._aplan
         ap.np_step, ap.pane_base, ap.p_lo, ap.fired_hi = (aplan.np_step, aplan.pane_base,
                                                           aplan.p_lo, aplan.fired_hi)
+        ap.split = aplan.split
         cuda = self.device.type == "cuda"
         self._m.window_agg_obj(cuda, recs.data_ptr(), counts.data_ptr(), ap,
                                self.keys_g.data_ptr(), self.acc_g.data_ptr(),
