@@ -420,3 +420,45 @@ def test_dense_keys_local_global_invariant(dev, world):
     for step in range(STEPS):
         out += ref_op.process(*_concat(dev, world, step, per, nkeys))
     assert merged == _collect(out + ref_op.finish())
+
+
+@pytest.mark.parametrize("dev", _devices())
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("count_window", [0, 5])
+def test_rolling_and_count_windows_invariant_to_world(dev, world, count_window):
+    """Keyed rolling sums (ComputeCpuMax.java:26 shape) and tumbling count windows at G ranks:
+    the owner sees a key's records ordered (source rank, arrival), i.e. the rank-ordered
+    concatenation, so every key's emitted sequence equals the single-rank reference's."""
+    _skip_no_gpu(dev)
+    from mxstream.runtime.rolling_operator import KeyedRollingOperator
+
+    per, nkeys = (4000, 700) if dev == "cpu" else (60_000, 20_000)
+
+    def rows_by_key(rows, acc):
+        order = np.argsort(rows.tags, kind="stable")  # (src << 32 | arrival): rank-major
+        for i in order:
+            acc.setdefault(int(rows.keys[i]), []).append(int(rows.values[i]))
+
+    def rank_fn(comm):
+        op = KeyedRollingOperator(agg=K.AGG_SUM_I64, device=dev, comm=comm, max_keys=nkeys,
+                                  parallelism=comm.world, batch_capacity=per,
+                                  count_window=count_window)
+        got = {}
+        for step in range(4):
+            k, _, v = _batch(dev, comm.rank, step, per, nkeys)
+            rows_by_key(op.process(k, v), got)
+        return got
+
+    ranks = run_loopback(world, rank_fn, device=torch.device(dev))
+    merged = {}
+    for g in ranks:
+        for k, seq in g.items():
+            assert k not in merged  # one owner per key
+            merged[k] = seq
+    ref_op = KeyedRollingOperator(agg=K.AGG_SUM_I64, device=dev, max_keys=nkeys,
+                                  batch_capacity=per * world, count_window=count_window)
+    ref = {}
+    for step in range(4):
+        k, _, v = _concat(dev, world, step, per, nkeys)
+        rows_by_key(ref_op.process(k, v), ref)
+    assert merged == ref and len(ref) > 0
