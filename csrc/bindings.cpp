@@ -465,6 +465,15 @@ PYBIND11_MODULE(_mxs_native, m) {
       if (e != 0) throw std::runtime_error("hipMemcpyAsync D2H failed: " + std::to_string(e));
     }
   });
+  // Kernel variant of gpu_d2h_many (16-byte granules); returns the hipError_t code (0 = ok).
+  m.def("gpu_d2h_kernel", [](intptr_t dst, const std::vector<std::tuple<intptr_t, int64_t, int64_t>>& copies,
+                             intptr_t stream) {
+    if (copies.size() > (size_t)kD2HMax) throw std::invalid_argument("gpu_d2h_kernel: too many columns");
+    D2HCopy c[kD2HMax];
+    for (size_t i = 0; i < copies.size(); ++i)
+      c[i] = D2HCopy{(const void*)std::get<0>(copies[i]), std::get<1>(copies[i]), std::get<2>(copies[i])};
+    return gpu::d2h_kernel((void*)dst, c, (int)copies.size(), stream);
+  });
   m.def("gpu_dirty_clear", [](intptr_t list, intptr_t list_n, uint32_t cap, int ring,
                               int64_t nslots, intptr_t dirty_g, intptr_t mark, int64_t p_lo, int np,
                               intptr_t stream) {

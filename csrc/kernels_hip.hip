@@ -106,6 +106,23 @@ __global__ __launch_bounds__(256) void gen_events_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// Fired rows -> pinned host slab by a kernel (16-byte vector stores into mapped host memory):
+// the DMA path (hipMemcpyAsync D2H) stalled the host for 7-9 ms at one firing in some runs
+// (profiles/r2_fire_d2h.md); a kernel copy has no lazily initialised engine behind it.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void d2h_copy_kernel(unsigned char* __restrict__ dst, D2HBatch b) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int k = 0; k < b.n; ++k) {
+    const v4u* __restrict__ s = reinterpret_cast<const v4u*>(b.c[k].src);
+    v4u* __restrict__ d = reinterpret_cast<v4u*>(dst + b.c[k].dst_off);
+    const int64_t n16 = b.c[k].bytes >> 4;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+      d[i] = __builtin_nontemporal_load(&s[i]);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Partition: keyBy (Flink key groups -> dest rank) x sub-table, window assignment, late drop.
 // ------------------------------------------------------------------------------------------
 // Per-element partition decision; identical code runs in pass A (histogram) and pass B
@@ -2707,6 +2724,27 @@ int set_spin_schedule() { return (int)hipSetDeviceFlags(hipDeviceScheduleSpin); 
 
 int d2h_async(void* dst, const void* src, size_t bytes, intptr_t stream) {
   return (int)hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream);
+}
+
+int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream) {
+  // Device-side address of the pinned host slab (mapped host memory).
+  void* dd = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&dd, dst_host, 0);
+  if (e != hipSuccess || !dd) return (int)(e != hipSuccess ? e : hipErrorInvalidValue);
+  D2HBatch b{};
+  if (n < 1 || n > kD2HMax) return (int)hipErrorInvalidValue;
+  b.n = n;
+  int64_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    b.c[i] = copies[i];
+    if ((copies[i].bytes & 15) || (copies[i].dst_off & 15) || ((uintptr_t)copies[i].src & 15))
+      return (int)hipErrorInvalidValue;  // 16-byte granules only (the caller pads)
+    total += copies[i].bytes;
+  }
+  const int grid = grid_for(total / 16, 256 * 4, 1024);
+  hipLaunchKernelGGL(d2h_copy_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                     (unsigned char*)dd, b);
+  return (int)hipGetLastError();
 }
 
 int device_count() {

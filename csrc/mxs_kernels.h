@@ -79,11 +79,25 @@ struct RollPlan {
 };
 
 // ---- GPU launchers (kernels_hip.hip) --------------------------------------------------------
+constexpr int kD2HMax = 8;
+struct D2HCopy {
+  const void* src;
+  int64_t bytes;
+  int64_t dst_off;
+};
+struct D2HBatch {
+  D2HCopy c[kD2HMax];
+  int n;
+};
+
 namespace gpu {
 int device_count();
 int set_spin_schedule();
 // Async device->host copy on `stream` (hipMemcpyAsync); returns the hipError_t code.
 int d2h_async(void* dst, const void* src, size_t bytes, intptr_t stream);
+// Up to kD2HMax device buffers -> one pinned (mapped) host slab by a copy kernel on `stream`;
+// every size, source address and slab offset a multiple of 16 bytes. Returns hipError_t.
+int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream);
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,

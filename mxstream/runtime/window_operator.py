@@ -24,6 +24,7 @@ micro-batch produce one re-firing carrying their combined effect (Flink fires on
 from __future__ import annotations
 
 import math
+import os as _os
 from dataclasses import dataclass, field
 from typing import Callable
 
@@ -101,21 +102,30 @@ def to_host_arrays(cols: list[torch.Tensor], n: int, pool: PinnedSlabPool | None
         nbytes += (n * c.element_size() + 255) & ~255
     t, arr = pool.take(nbytes)
     out, copies = [], []
+    kernel_ok = _D2H != "dma"
     for o, c in zip(offs, cols):
         nb = n * c.element_size()
         if not c.is_contiguous() or n > c.numel():
             raise ValueError("to_host_arrays: columns must be contiguous with at least n rows")
-        copies.append((c.data_ptr(), nb, o))
+        nb16 = (nb + 15) & ~15
+        kernel_ok = kernel_ok and nb16 <= c.numel() * c.element_size() and c.data_ptr() % 16 == 0
+        copies.append((c.data_ptr(), nb16, o))
         out.append(arr[o:o + nb].view(_NP_DTYPE[c.dtype]))
-    # One native call issuing a hipMemcpyAsync per column: torch's copy_ into a pinned slice
-    # occasionally blocked for 7-9 ms (one firing per run in the headline bench, cProfile:
-    # profiles/r2_fire_d2h.md).
+    # The DMA path (hipMemcpyAsync, and torch's copy_ before it) stalled the host for 7-9 ms at
+    # one firing in some runs (profiles/r2_fire_d2h.md): a copy kernel storing into the mapped
+    # pinned slab by default, one native call either way.
     from ..ops.native import load
 
     stream = torch.cuda.current_stream(cols[0].device)
-    load().gpu_d2h_many(t.data_ptr(), copies, stream.cuda_stream)
+    m = load()
+    if not kernel_ok or m.gpu_d2h_kernel(t.data_ptr(), copies, stream.cuda_stream) != 0:
+        m.gpu_d2h_many(t.data_ptr(), [(p, min(b, n * c.element_size()), o)
+                                      for (p, b, o), c in zip(copies, cols)], stream.cuda_stream)
     stream.synchronize()
     return out
+
+
+_D2H = _os.environ.get("MXS_D2H", "kernel")  # "dma": hipMemcpyAsync (A/B)
 
 
 _NP_DTYPE = {torch.int64: np.int64, torch.int32: np.int32, torch.float64: np.float64,

@@ -27,7 +27,7 @@ for step in "$@"; do
     prof_bench_hashed) prof bench_hashed python3 bench.py --steps 24 --warmup 6 --hashed-keys || exit $? ;;
     bench_sync_*) m=${step#bench_sync_}; MXS_SYNC=$m timeout -k 10 300 python bench.py --steps 48 --warmup 8 > "$out/bench_sync_$m.log" 2>&1 || exit $? ;;
     bench_times) MXS_STEP_TIMES=1 timeout -k 10 300 python bench.py --steps 48 --warmup 8 > "$out/bench_times.log" 2>&1 || exit $? ;;
-    bench_sprof) MXS_STEP_TIMES=1 MXS_STEP_PROFILE=1 timeout -k 10 300 python bench.py --steps 48 --warmup 8 > "$out/bench_sprof.log" 2>&1 || exit $? ;;
+    bench_sprof*) MXS_STEP_TIMES=1 MXS_STEP_PROFILE=1 timeout -k 10 300 python bench.py --steps 48 --warmup 8 > "$out/$step.log" 2>&1 || exit $? ;;
     bench_k32) MXS_STEP_TIMES=1 timeout -k 10 300 python bench.py --steps 48 --warmup 8 --int32-keys > "$out/bench_k32.log" 2>&1 || exit $? ;;
     prof_k32) prof k32 python3 bench.py --steps 24 --warmup 6 --int32-keys || exit $? ;;
     bench_nopair) MXS_PAIR=0 MXS_STEP_TIMES=1 timeout -k 10 300 python bench.py --steps 48 --warmup 8 > "$out/bench_nopair.log" 2>&1 || exit $? ;;
