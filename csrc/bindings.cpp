@@ -139,6 +139,7 @@ AggPlan make_agg(py::dict d) {
   if (p.cap_log2 < 4 || p.cap_log2 > 14) throw std::invalid_argument("cap_log2 out of range");
   if (p.pg <= 0) throw std::invalid_argument("pg must be positive");
   p.split = d.contains("split") ? d["split"].cast<int32_t>() : 1;
+  p.det = d.contains("det") ? d["det"].cast<int32_t>() : 0;
   if (p.split < 1 || p.split > 1024) throw std::invalid_argument("agg split out of range");
   return p;
 }

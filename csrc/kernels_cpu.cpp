@@ -169,6 +169,15 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p, uint6
                 uint32_t* flags) {
   const uint32_t cap = 1u << p.cap_log2, mask = cap - 1;
   const size_t nslots = (size_t)p.nsub << p.cap_log2;
+  // Deterministic f64 sums: per-step slot sums in 128-bit fixed point, folded once per slot
+  // (the GPU kernel's LDS accumulation + write-back, bit for bit).
+  const bool det = p.det && (p.agg == AGG_SUM_F64 || p.agg == AGG_AVG_F64);
+  std::vector<unsigned __int128> dsum;
+  std::vector<uint32_t> dcnt;
+  if (det) {
+    dsum.assign((size_t)p.np_step * cap, 0);
+    dcnt.assign((size_t)p.np_step * cap, 0);
+  }
   for (int sub = 0; sub < p.nsub; ++sub) {
     uint64_t* keys = keys_g + ((size_t)sub << p.cap_log2);
     bool inserted = false;
@@ -196,9 +205,20 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p, uint6
         }
         const int64_t pane = p.pane_base + (int64_t)r.t;
         const size_t gi = (size_t)(pane & (p.ring - 1)) * nslots + ((size_t)sub << p.cap_log2) + s;
-        const uint64_t v = agg_lift(p.agg, r.val);
-        if (p.agg != AGG_COUNT) acc_g[gi] = cnt_g[gi] ? agg_combine(p.agg, acc_g[gi], v) : v;
-        cnt_g[gi] += p.combined ? r.aux : 1u;
+        if (det) {
+          uint64_t lo, hi;
+          if (!f64_to_fx(as_f64(r.val), &lo, &hi)) {
+            flags[0] |= 8u;
+            continue;
+          }
+          const size_t li = (size_t)q * cap + s;
+          dsum[li] += ((unsigned __int128)hi << 64) | lo;
+          dcnt[li] += p.combined ? r.aux : 1u;
+        } else {
+          const uint64_t v = agg_lift(p.agg, r.val);
+          if (p.agg != AGG_COUNT) acc_g[gi] = cnt_g[gi] ? agg_combine(p.agg, acc_g[gi], v) : v;
+          cnt_g[gi] += p.combined ? r.aux : 1u;
+        }
         if (pane <= p.fired_hi) {
           dirty_g[gi] = 1;
           const size_t slot = ((size_t)sub << p.cap_log2) + s;
@@ -208,6 +228,20 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p, uint6
           }
         }
       }
+    }
+    if (det) {
+      for (int q = 0; q < p.np_step; ++q)
+        for (uint32_t s = 0; s < cap; ++s) {
+          const size_t li = (size_t)q * cap + s;
+          if (!dcnt[li]) continue;
+          const int64_t pane = p.pane_base + p.p_lo + q;
+          const size_t gi = (size_t)(pane & (p.ring - 1)) * nslots + ((size_t)sub << p.cap_log2) + s;
+          const double d = fx_to_f64((uint64_t)dsum[li], (uint64_t)(dsum[li] >> 64));
+          acc_g[gi] = cnt_g[gi] ? f64_bits(as_f64(acc_g[gi]) + d) : f64_bits(d);
+          cnt_g[gi] += dcnt[li];
+          dsum[li] = 0;
+          dcnt[li] = 0;
+        }
     }
     if (inserted) {
       uint32_t occ = 0;

@@ -1132,7 +1132,7 @@ __device__ __forceinline__ uint32_t pk_cnt(uint64_t p) {
 // DENSE: directly addressed dense key ids (AggPlan.dense_bits): no LDS key table, no probe.
 constexpr uint32_t kAggSliceMin = 131072;  // records per workgroup of a split sub-table
 
-template <int AGG, int RW, bool PK = false, bool DENSE = false>
+template <int AGG, int RW, bool PK = false, bool DENSE = false, bool DET = false>
 __global__ __launch_bounds__(1024) void window_agg_kernel(
     const void* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
     uint64_t* __restrict__ keys_g, uint64_t* __restrict__ acc_g, uint32_t* __restrict__ cnt_g,
@@ -1158,7 +1158,8 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
   const uint32_t mask = cap - 1;
   uint64_t* skeys = (uint64_t*)smem;                   // unused when DENSE
   uint64_t* sacc = DENSE ? (uint64_t*)smem : skeys + cap;
-  uint32_t* scnt = (uint32_t*)(sacc + (size_t)p.pg * cap);           // unused when PK
+  // DET: two words per slot (128-bit fixed-point sum, f64_to_fx), see AggPlan.det.
+  uint32_t* scnt = (uint32_t*)(sacc + (size_t)p.pg * cap * (DET ? 2 : 1));  // unused when PK
   int* sflag = (int*)(scnt + (PK ? 0 : (size_t)p.pg * cap));  // [0] inserted, [1] ovf, [2] occ
 
   const size_t sbase = (size_t)sub << p.cap_log2;
@@ -1179,11 +1180,16 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
   }
 
   int inserted = 0;
-  bool ovf = false;
+  bool ovf = false, fxbad = false;
   for (int pg0 = 0; pg0 < p.np_step; pg0 += p.pg) {
     const int npg = (p.np_step - pg0) < p.pg ? (p.np_step - pg0) : p.pg;
     for (uint32_t i = threadIdx.x; i < (uint32_t)npg * cap; i += blockDim.x) {
-      sacc[i] = PK ? 0ull : (uint64_t)lds_identity<AGG>();
+      if (DET) {
+        sacc[2 * i] = 0;
+        sacc[2 * i + 1] = 0;
+      } else {
+        sacc[i] = PK ? 0ull : (uint64_t)lds_identity<AGG>();
+      }
       if (!PK) scnt[i] = 0;
     }
     __syncthreads();
@@ -1231,7 +1237,19 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
             }
           }
           const uint32_t li = (uint32_t)q * cap + s;
-          if (PK) {
+          if (DET) {
+            uint64_t lo, hi;
+            if (!f64_to_fx(as_f64(r.val), &lo, &hi)) {
+              fxbad = true;
+              continue;
+            }
+            // 128-bit add from two 64-bit LDS atomics: the carry out of the low word goes into
+            // the high word (two's complement, so the final sum is order-independent).
+            const uint64_t old = atomicAdd((unsigned long long*)&sacc[2 * li], (unsigned long long)lo);
+            atomicAdd((unsigned long long*)&sacc[2 * li + 1],
+                      (unsigned long long)(hi + (old + lo < old ? 1ull : 0ull)));
+            atomicAdd(&scnt[li], p.combined ? r.aux : 1u);
+          } else if (PK) {
             atomicAdd((unsigned long long*)&sacc[li], (unsigned long long)(r.val + kPkOne));
           } else {
             lds_accumulate<AGG>(&sacc[li], r.val);
@@ -1273,7 +1291,8 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
         late[w] = false;
         if (!dc[w]) continue;
         const uint32_t i = i0 + (uint32_t)w * blockDim.x;
-        const uint64_t d = PK ? (uint64_t)pk_sum(sacc[i]) : lds_export<AGG>(sacc[i]);
+        const uint64_t d = DET ? f64_bits(fx_to_f64(sacc[2 * i], sacc[2 * i + 1]))
+                           : PK ? (uint64_t)pk_sum(sacc[i]) : lds_export<AGG>(sacc[i]);
         if (shared_sub) {
           // Additive aggregates only (launcher): an empty slot's accumulator is 0.
           if (AGG != AGG_COUNT) atomicAdd((unsigned long long*)&acc_g[gi[w]], (unsigned long long)d);
@@ -1301,7 +1320,9 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
   }
   if (inserted) sflag[0] = 1;
   if (ovf) sflag[1] = 1;
+  if (fxbad) sflag[3] = 1;
   __syncthreads();
+  if (threadIdx.x == 0 && sflag[3]) atomicOr(&flags[0], 8u);  // DET: value outside fixed point
   if (p.dlist && sdl_hdr[0]) {
     if (threadIdx.x == 0) sdl_hdr[1] = atomicAdd(p.dlist_n, sdl_hdr[0]);
     __syncthreads();
@@ -2958,13 +2979,13 @@ static bool agg_pack_ok(const AggPlan& p) {
          !p.combined && (uint64_t)p.nsrc * p.bucket_cap < 65536;
 }
 
-template <int AGG, int RW, bool PK, bool DENSE>
+template <int AGG, int RW, bool PK, bool DENSE, bool DET = false>
 static void launch_agg_v(const Rec* recs, const uint32_t* counts, const AggPlan& p,
                          uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
                          uint32_t* occ, uint32_t* flags, size_t lds, hipStream_t s) {
   static bool attr = false;
   if (!attr) {  // allow the full 160 KiB LDS
-    HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, RW, PK, DENSE>,
+    HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, RW, PK, DENSE, DET>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
@@ -2974,7 +2995,7 @@ static void launch_agg_v(const Rec* recs, const uint32_t* counts, const AggPlan&
   const bool split_ok = DENSE && p.nsrc == 1 && !p.dlist &&
                         (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64 || AGG == AGG_COUNT);
   q.split = split_ok && p.split > 1 ? p.split : 1;
-  hipLaunchKernelGGL((window_agg_kernel<AGG, RW, PK, DENSE>), dim3(p.nsub * q.split), dim3(1024),
+  hipLaunchKernelGGL((window_agg_kernel<AGG, RW, PK, DENSE, DET>), dim3(p.nsub * q.split), dim3(1024),
                      lds, s, (const void*)recs, counts, q, keys_g, acc_g, cnt_g, dirty_g, occ,
                      flags);
 }
@@ -2986,6 +3007,15 @@ static void launch_agg_d(const Rec* recs, const uint32_t* counts, const AggPlan&
   const size_t cap = (size_t)1 << p.cap_log2;
   const size_t keys_lds = DENSE ? 0 : cap * 8;  // dense ids need no LDS key table
   const size_t list_lds = p.dlist ? 16 + cap / 8 + cap * 4 : 0;
+  if constexpr (AGG == AGG_SUM_F64 || AGG == AGG_AVG_F64) {
+    if (p.det) {  // deterministic sums: 16-byte fixed-point accumulators, 24-byte records
+      if (p.rec_words != 3) throw std::invalid_argument("window_agg: deterministic sums need 24-byte records");
+      const size_t lds_det = keys_lds + (size_t)p.pg * cap * 20 + 16 + list_lds;
+      launch_agg_v<AGG, 3, false, DENSE, true>(recs, counts, p, keys_g, acc_g, cnt_g, dirty_g,
+                                               occ, flags, lds_det, s);
+      return;
+    }
+  }
   if constexpr (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) {
     if (agg_pack_ok(p)) {
       const size_t lds_pk = keys_lds + (size_t)p.pg * cap * 8 + 16 + list_lds;
@@ -3025,7 +3055,7 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& plan, ui
                 uint32_t* flags, intptr_t stream) {
   if (plan.np_step <= 0 || plan.nsub <= 0) return;
   const size_t cap = (size_t)1 << plan.cap_log2;
-  const size_t lds = cap * 8 + (size_t)plan.pg * cap * 12 + 16 +
+  const size_t lds = cap * 8 + (size_t)plan.pg * cap * (plan.det ? 20 : 12) + 16 +
                      (plan.dlist ? 16 + cap / 8 + cap * 4 : 0);  // touched-slot bitmap + buffer
   if (lds > 160 * 1024) throw std::runtime_error("window_agg: LDS image exceeds 160 KiB");
   if (plan.rec_words < 3 && plan.combined)

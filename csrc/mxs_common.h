@@ -206,6 +206,54 @@ MXS_HD uint64_t f64_bits(double d) {
   return c.u;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Deterministic f64 sums (AggPlan.det): a step's per-slot sum is accumulated as a 128-bit
+// two's-complement fixed-point number with 64 fraction bits. Integer addition is associative and
+// commutative, so the result does not depend on the order in which LDS atomics (or the C++
+// twin's loop) add the values; it is converted to a double once. Values are truncated to
+// multiples of 2^-64 (|x| < 2^-64 adds 0) and must satisfy |x| < 2^63; NaN/Inf are rejected.
+// ---------------------------------------------------------------------------------------------
+MXS_HD bool f64_to_fx(double x, uint64_t* lo, uint64_t* hi) {
+  const uint64_t bits = f64_bits(x);
+  const int ex = (int)((bits >> 52) & 0x7FF);
+  *lo = 0;
+  *hi = 0;
+  if (ex == 0x7FF) return false;  // Inf / NaN
+  if (ex == 0) return true;       // zero / subnormal: below the fixed-point resolution
+  const uint64_t m = (bits & ((1ull << 52) - 1)) | (1ull << 52);
+  const int sh = ex - 1011;       // x = m * 2^(ex - 1075); fixed = x * 2^64 = m * 2^sh
+  if (sh > 74) return false;      // |x| >= 2^63
+  unsigned __int128 mag;
+  if (sh >= 0) mag = (unsigned __int128)m << sh;
+  else mag = -sh >= 64 ? 0 : (unsigned __int128)(m >> -sh);
+  if (bits >> 63) mag = (unsigned __int128)0 - mag;
+  *lo = (uint64_t)mag;
+  *hi = (uint64_t)(mag >> 64);
+  return true;
+}
+
+MXS_HD int clz64(uint64_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return v ? __clzll((long long)v) : 64;
+#else
+  return v ? __builtin_clzll(v) : 64;
+#endif
+}
+
+MXS_HD double fx_to_f64(uint64_t lo, uint64_t hi) {
+  unsigned __int128 v = ((unsigned __int128)hi << 64) | lo;
+  const bool neg = (int64_t)hi < 0;
+  if (neg) v = (unsigned __int128)0 - v;
+  const uint64_t vh = (uint64_t)(v >> 64), vl = (uint64_t)v;
+  if (!vh && !vl) return 0.0;
+  // Top 64 significant bits -> double (one u64 -> f64 rounding), times 2^(shift - 64).
+  const int shift = vh ? 64 - clz64(vh) : 0;
+  const uint64_t top = shift ? (uint64_t)(v >> shift) : vl;
+  const double scale = as_f64((uint64_t)(1023 + shift - 64) << 52);
+  const double d = (double)top * scale;
+  return neg ? -d : d;
+}
+
 // Combine two partial accumulators (host side and device write-back).
 MXS_HD uint64_t agg_combine(int32_t k, uint64_t a, uint64_t b) {
   switch (k) {

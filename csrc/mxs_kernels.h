@@ -39,6 +39,10 @@ struct AggPlan {
   // `split` workgroups share one sub-table's records (>= kAggSliceMin each) and merge into the
   // state with atomic adds; 1 = one workgroup per sub-table.
   int32_t split;
+  // 1: deterministic f64 sums (AGG_SUM_F64 / AGG_AVG_F64): per-step slot sums in 128-bit fixed
+  // point (mxs_common.h f64_to_fx), bit-identical between runs and between the GPU and the C++
+  // twin. A value outside the fixed-point range sets flags[0] bit 3.
+  int32_t det;
 };
 
 // Plan of one window firing.

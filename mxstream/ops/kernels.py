@@ -179,6 +179,7 @@ class AggPlan:
     dense_bits: int = 0  # > 0: directly addressed dense key ids (see PartitionPlan)
     dense_mul: int = 0
     split: int = 1       # workgroups sharing an oversized sub-table (hot keys; GPU, see AGG_SLICE)
+    det: int = 0         # 1: deterministic f64 sums (128-bit fixed-point per-step slot sums)
 
     def as_dict(self) -> dict:
         return dict(self.__dict__)

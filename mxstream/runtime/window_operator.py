@@ -263,8 +263,15 @@ class KeyedWindowOperator:
                  combine: bool | None = None, compact: bool | None = None,
                  narrow: bool | None = None, dense_keys: bool = False,
                  pipeline: bool | str | None = None, exchange: str = "auto",
-                 idle_timeout_steps: int | None = None):
+                 idle_timeout_steps: int | None = None, deterministic: bool = False):
+        """deterministic: f64 sums/averages accumulate each step's per-slot sum in 128-bit fixed
+        point (order-independent integer adds, one rounding per slot and step), so results are
+        bit-identical between runs, between the GPU and the C++ twin, and independent of the
+        number of virtual ranks' exchange order; values must satisfy |x| < 2^63 and are
+        truncated to multiples of 2^-64. The sender-side combiner is off in
+        this mode (raw records are exchanged). Integer aggregates are always exact."""
         self.device = K.resolve_device(device)
+        self.deterministic = bool(deterministic) and agg in (K.AGG_SUM_F64, K.AGG_AVG_F64)
         self.comm = comm or LocalComm()
         self.world = self.comm.world
         self.rank = self.comm.rank
@@ -312,9 +319,13 @@ class KeyedWindowOperator:
         #   first fire), so "auto" picks it exactly then.
         if exchange not in ("auto", "records", "partials"):
             raise ValueError("exchange must be 'auto', 'records' or 'partials'")
-        lg_ok = self.world > 1 and self.lateness == 0 and self._local_global_ok
+        # Deterministic f64 sums keep records exchange: a rank's partial would be rounded to a
+        # double before the merge, so the result would depend on G.
+        lg_ok = (self.world > 1 and self.lateness == 0 and self._local_global_ok
+                 and not self.deterministic)
         if exchange == "partials" and self.world > 1 and not lg_ok:
-            raise ValueError("exchange='partials' needs allowed_lateness == 0")
+            raise ValueError("exchange='partials' needs allowed_lateness == 0 and "
+                             "deterministic=False")
         self.local_global = lg_ok and exchange != "records"
         self._exchanging = self.world > 1 and not self.local_global
         self._part_ranks = self.world if self._exchanging else 1
@@ -368,7 +379,7 @@ class KeyedWindowOperator:
         self.nbuckets = self._part_ranks << self.nsub_log2
         # G > 1: sender-side combiner before the all-to-all (all aggregates are associative).
         self.combine = (self._exchanging if combine is None
-                        else bool(combine and self._exchanging))
+                        else bool(combine and self._exchanging)) and not self.deterministic
         # Pipelining: the partition of batch i+1 is enqueued before the state half of batch i
         # (process() then returns the windows fired by the previous batch; flush() drains).
         #   True:     the state half runs on a second stream, overlapping the partition (hides
@@ -860,7 +871,7 @@ class KeyedWindowOperator:
                                                  if self.dlist is not None else 0)
             b.has_data = True
             b.qmin, b.np_step = qmin, gmax - gmin + 1
-            b.pg = max(1, min(b.np_step, lds_budget // (cap * 12)))
+            b.pg = max(1, min(b.np_step, lds_budget // (cap * (20 if self.deterministic else 12))))
             b.gmin, b.gmax = gmin, gmax
         self.metrics.steps += 1
         if not self.external_watermark:
@@ -901,6 +912,7 @@ class KeyedWindowOperator:
                                   p_lo=b.qmin, fired_hi=b.fired_hi, combined=combined,
                                   rec_words=3 if combined else b.rw)
                 aplan.dense_bits, aplan.dense_mul = self.dense_bits, self.dense_mul
+                aplan.det = int(self.deterministic)
                 # Hot keys: a sub-table holding more than AGG_SLICE records is shared by several
                 # workgroups (the launcher applies it where the atomic merge is exact).
                 aplan.split = min(64, max(1, -(-b.maxb // K.AGG_SLICE))) if not combined else 1
@@ -940,7 +952,7 @@ class KeyedWindowOperator:
         if aplan.np_step > aplan.ring:
             raise ValueError("step touches more panes than the ring holds")
         key = (aplan.bucket_cap, aplan.rec_words, aplan.ring, aplan.nsrc, aplan.combined,
-               aplan.pg, aplan.dlist)
+               aplan.pg, aplan.dlist, aplan.det)
         if self._aplan_key != key:
             self._aplan = self._m.AggPlanObj(aplan.as_dict())
             self._aplan_key = key
@@ -1052,7 +1064,8 @@ class KeyedWindowOperator:
             self.fsend.numel() * 8
         mplan = K.AggPlan(cap_log2=self.cap_log2_o, nsub=self.nsub_o, ring=1, agg=self.agg,
                           nsrc=self.world, bucket_cap=self.fbcap, np_step=1, pg=1, pane_base=0,
-                          p_lo=0, fired_hi=I64_MIN, combined=1, rec_words=3)
+                          p_lo=0, fired_hi=I64_MIN, combined=1, rec_words=3,
+                          det=int(self.deterministic))
         K.window_agg(self.frecv, self.frecv_counts, mplan, self.keys_m, self.acc_m, self.cnt_m,
                      self.dirty_m, self.occ_m, self.flags)
         self.out_n.zero_()
@@ -1084,6 +1097,8 @@ class KeyedWindowOperator:
             hf = self.flags.tolist()
         if hf[0] & 1:
             raise RuntimeError("keyed state table full: a key found no free slot (raise max_keys)")
+        if hf[0] & 8:
+            raise ValueError("deterministic f64 sum: a value is NaN, infinite or |x| >= 2^63")
         return hf[2]
 
     def _fire_ready(self, wm: int) -> list[FireResult]:

@@ -386,3 +386,29 @@ def test_hot_keys_gpu_match_cpu(gpu_device, zipf, narrow):
     assert g == c
     top = max(x[3] for x in c)
     assert top > 20_000  # the hot key really is hot (mean count per key and window: ~4)
+
+
+@pytest.mark.parametrize("dense", [False, True])
+def test_deterministic_f64_sums_gpu_bit_exact(gpu_device, dense):
+    """deterministic=True: the GPU's LDS fixed-point accumulation (two 64-bit atomics per add)
+    gives f64 window sums bit-identical to the C++ twin's, run after run."""
+    import sys
+
+    sys.path.insert(0, __import__("os").path.dirname(__file__))
+    from test_window_operator_cpu import _f64_batches
+
+    batches = _f64_batches(200_000, 5, 11)
+
+    def run(dev):
+        op = KeyedWindowOperator(size=2000, agg=K.AGG_SUM_F64, device=dev, max_keys=600,
+                                 batch_capacity=200_000, deterministic=True, dense_keys=dense)
+        rows = {}
+        for k, t, v in batches:
+            for r in op.process(k.to(dev), t.to(dev), v.to(dev)) + []:
+                rows.update({(r.window_start, a): b for a, b in zip(r.keys.tolist(), r.raw.tolist())})
+        for r in op.finish():
+            rows.update({(r.window_start, a): b for a, b in zip(r.keys.tolist(), r.raw.tolist())})
+        return rows
+
+    g1, g2, c = run(gpu_device), run(gpu_device), run("cpu")
+    assert g1 == c and g2 == c and len(c) > 1000

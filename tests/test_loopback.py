@@ -462,3 +462,50 @@ def test_rolling_and_count_windows_invariant_to_world(dev, world, count_window):
         k, _, v = _concat(dev, world, step, per, nkeys)
         rows_by_key(ref_op.process(k, v), ref)
     assert merged == ref and len(ref) > 0
+
+
+@pytest.mark.parametrize("dev", _devices())
+@pytest.mark.parametrize("world", [2, 3])
+def test_deterministic_f64_sums_invariant_to_world(dev, world):
+    """deterministic f64 sums at G virtual ranks (records exchange, and local-global partials)
+    are bit-identical to the single-rank result on the rank-concatenated batches."""
+    _skip_no_gpu(dev)
+    per, nkeys = (3000, 400) if dev == "cpu" else (60_000, 20_000)
+    rng = np.random.default_rng(5)
+    vals = {(r, s): torch.from_numpy(rng.standard_normal(per) * 10.0 ** rng.integers(-5, 8, per))
+            for r in range(world) for s in range(STEPS)}
+
+    def batch(rank, step):
+        k, t, _ = _batch("cpu", rank, step, per, nkeys)
+        return k.to(dev), t.to(dev), vals[(rank, step)].view(torch.int64).to(dev)
+
+    def collect(out, acc):
+        for r in out:
+            acc.update({(r.window_start, int(k)): int(a) for k, a in zip(r.keys, r.raw)})
+
+    for exchange in ("records", "auto"):  # "auto" picks records exchange in this mode
+        def rank_fn(comm):
+            op = KeyedWindowOperator(size=3000, agg=K.AGG_SUM_F64, device=dev, comm=comm,
+                                     max_keys=nkeys, parallelism=comm.world, batch_capacity=per,
+                                     ooo_bound=700, deterministic=True, exchange=exchange)
+            got = {}
+            for step in range(STEPS):
+                collect(op.process(*batch(comm.rank, step)), got)
+            collect(op.finish(), got)
+            return got
+
+        merged = {}
+        for g in run_loopback(world, rank_fn, device=torch.device(dev)):
+            merged.update(g)
+        ref_op = KeyedWindowOperator(size=3000, agg=K.AGG_SUM_F64, device=dev, max_keys=nkeys,
+                                     batch_capacity=per * world, ooo_bound=700, deterministic=True)
+        ref = {}
+        for step in range(STEPS):
+            parts = [batch(r, step) for r in range(world)]
+            collect(ref_op.process(*[torch.cat([p[i] for p in parts]) for i in range(3)]), ref)
+        collect(ref_op.finish(), ref)
+        assert merged == ref and len(ref) > 100, exchange
+    with pytest.raises(ValueError, match="deterministic"):
+        run_loopback(2, lambda comm: KeyedWindowOperator(
+            size=3000, agg=K.AGG_SUM_F64, device=dev, comm=comm, max_keys=nkeys,
+            parallelism=2, deterministic=True, exchange="partials"), device=torch.device(dev))

@@ -283,3 +283,59 @@ def test_int32_key_ids_match_int64(dense):
     assert run(torch.int32) == run(torch.int64)
     with pytest.raises(ValueError, match="reserved"):
         run(torch.int32, bad=True)
+
+
+def _f64_batches(n, steps, seed):
+    import torch
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for step in range(steps):
+        k = torch.from_numpy(rng.integers(0, 500, n).astype(np.int64))
+        t = torch.from_numpy((step * 1000 + rng.integers(0, 1000, n)).astype(np.int64))
+        # wide dynamic range: rounding order matters for plain f64 sums
+        v = rng.standard_normal(n) * 10.0 ** rng.integers(-6, 9, n)
+        out.append((k, t, torch.from_numpy(v).view(torch.int64)))
+    return out
+
+
+@pytest.mark.parametrize("agg_name", ["sum", "avg"])
+def test_deterministic_f64_sums_order_independent(agg_name):
+    """deterministic=True: permuting the records of every batch leaves every fired f64 sum
+    bit-identical (128-bit fixed-point slot sums), and the sums equal math.fsum up to the final
+    conversion."""
+    import math
+
+    import torch
+
+    from mxstream.ops import kernels as K
+    from mxstream.runtime.window_operator import KeyedWindowOperator
+
+    agg = K.AGG_SUM_F64 if agg_name == "sum" else K.AGG_AVG_F64
+    batches = _f64_batches(4000, 5, 3)
+
+    def run(perm_seed):
+        op = KeyedWindowOperator(size=2000, agg=agg, device="cpu", max_keys=600,
+                                 batch_capacity=4000, ooo_bound=0, deterministic=True, cap_log2=8)
+        rows = {}
+        rng = np.random.default_rng(perm_seed)
+        for k, t, v in batches:
+            p = torch.from_numpy(rng.permutation(k.numel())) if perm_seed else torch.arange(k.numel())
+            for r in op.process(k[p], t[p], v[p]):
+                for key, raw in zip(r.keys.tolist(), r.raw.tolist()):
+                    rows[(r.window_start, key)] = raw
+        for r in op.finish():
+            for key, raw in zip(r.keys.tolist(), r.raw.tolist()):
+                rows[(r.window_start, key)] = raw
+        return rows
+
+    a, b = run(0), run(7)
+    assert a == b and len(a) > 100
+    # spot-check against an exact sum of one window/key
+    (ws, key), raw = next(iter(sorted(a.items())))
+    vals = []
+    for k, t, v in batches:
+        sel = (k == key) & (t >= ws) & (t < ws + 2000)
+        vals += v[sel].view(torch.float64).tolist()
+    got = float(np.int64(raw).view(np.float64))
+    assert abs(got - math.fsum(vals)) <= 1e-9 * max(1.0, abs(math.fsum(vals)))
