@@ -475,6 +475,31 @@ PYBIND11_MODULE(_mxs_native, m) {
       c[i] = D2HCopy{(const void*)std::get<0>(copies[i]), std::get<1>(copies[i]), std::get<2>(copies[i])};
     return gpu::d2h_kernel((void*)dst, c, (int)copies.size(), stream);
   });
+  // Keyed-window compaction / eviction (host-DRAM spill tier). out = (key, pane, acc, cnt, dirty,
+  // n, cap, counters) pointers.
+  auto compact_out = [](const std::vector<intptr_t>& o, uint32_t cap) {
+    if (o.size() != 7) throw std::invalid_argument("window_compact: 7 output pointers");
+    return CompactOut{P<uint64_t>(o[0]), P<int64_t>(o[1]), P<uint64_t>(o[2]), P<uint32_t>(o[3]),
+                      P<uint8_t>(o[4]), P<uint32_t>(o[5]), cap, P<uint32_t>(o[6])};
+  };
+  m.def("gpu_window_compact", [compact_out](intptr_t keys_g, intptr_t acc_g, intptr_t cnt_g,
+                                            intptr_t dirty_g, int nsub, int cap_log2, int ring,
+                                            int64_t p_lo, int np, int64_t cutoff,
+                                            std::vector<intptr_t> o, uint32_t cap, intptr_t occ,
+                                            intptr_t stream) {
+    gpu::window_compact(P<uint64_t>(keys_g), P<uint64_t>(acc_g), P<uint32_t>(cnt_g),
+                        P<uint8_t>(dirty_g), nsub, cap_log2, ring, p_lo, np, cutoff,
+                        compact_out(o, cap), P<uint32_t>(occ), stream);
+  });
+  m.def("cpu_window_compact", [compact_out](intptr_t keys_g, intptr_t acc_g, intptr_t cnt_g,
+                                            intptr_t dirty_g, int nsub, int cap_log2, int ring,
+                                            int64_t p_lo, int np, int64_t cutoff,
+                                            std::vector<intptr_t> o, uint32_t cap, intptr_t occ) {
+    py::gil_scoped_release nogil;
+    cpu::window_compact(P<uint64_t>(keys_g), P<uint64_t>(acc_g), P<uint32_t>(cnt_g),
+                        P<uint8_t>(dirty_g), nsub, cap_log2, ring, p_lo, np, cutoff,
+                        compact_out(o, cap), P<uint32_t>(occ));
+  });
   m.def("gpu_dirty_clear", [](intptr_t list, intptr_t list_n, uint32_t cap, int ring,
                               int64_t nslots, intptr_t dirty_g, intptr_t mark, int64_t p_lo, int np,
                               intptr_t stream) {

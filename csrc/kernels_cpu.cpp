@@ -502,6 +502,78 @@ void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uin
   }
 }
 
+void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
+                    int nsub, int cap_log2, int ring, int64_t p_lo, int np, int64_t cutoff,
+                    const CompactOut& out, uint32_t* occupancy) {
+  const uint32_t cap = 1u << cap_log2, mask = cap - 1;
+  const size_t nslots = (size_t)nsub << cap_log2;
+  std::vector<uint64_t> nk(cap), ta(cap);
+  std::vector<uint32_t> from(cap), tc(cap);
+  std::vector<uint8_t> td(cap);
+  for (int sub = 0; sub < nsub; ++sub) {
+    const size_t sbase = (size_t)sub << cap_log2;
+    std::fill(nk.begin(), nk.end(), kEmptyKey);
+    std::fill(from.begin(), from.end(), kNoSlot);
+    uint32_t kept = 0;
+    for (uint32_t s = 0; s < cap; ++s) {
+      const uint64_t k = keys_g[sbase + s];
+      if (k == kEmptyKey || k == kTombKey) continue;
+      int64_t newest = INT64_MIN;
+      for (int j = 0; j < np; ++j) {
+        const int64_t p = p_lo + j;
+        if (cnt_g[(size_t)(p & (ring - 1)) * nslots + sbase + s]) newest = p;
+      }
+      if (newest == INT64_MIN) {
+        ++out.counters[0];
+        continue;
+      }
+      if (newest <= cutoff) {
+        ++out.counters[1];
+        for (int j = 0; j < np; ++j) {
+          const int64_t p = p_lo + j;
+          const size_t gi = (size_t)(p & (ring - 1)) * nslots + sbase + s;
+          if (!cnt_g[gi]) continue;
+          const uint32_t q = (*out.n)++;
+          if (q < out.cap) {
+            out.key[q] = k;
+            out.pane[q] = p;
+            out.acc[q] = acc_g[gi];
+            out.cnt[q] = cnt_g[gi];
+            out.dirty[q] = dirty_g[gi];
+          } else {
+            out.counters[2] |= 1u;
+          }
+        }
+        continue;
+      }
+      bool ins = false;
+      const uint32_t t = probe_insert(nk.data(), k, mask, &ins);
+      if (t == kNoSlot) {
+        out.counters[2] |= 1u;
+        continue;
+      }
+      from[t] = s;
+      ++kept;
+    }
+    for (uint32_t i = 0; i < cap; ++i) keys_g[sbase + i] = nk[i];
+    for (int j = 0; j < np; ++j) {
+      const size_t pb = (size_t)((p_lo + j) & (ring - 1)) * nslots + sbase;
+      for (uint32_t i = 0; i < cap; ++i) {
+        ta[i] = acc_g[pb + i];
+        tc[i] = cnt_g[pb + i];
+        td[i] = dirty_g[pb + i];
+      }
+      for (uint32_t i = 0; i < cap; ++i) {
+        const uint32_t f = from[i];
+        acc_g[pb + i] = f == kNoSlot ? 0 : ta[f];
+        cnt_g[pb + i] = f == kNoSlot ? 0 : tc[f];
+        dirty_g[pb + i] = f == kNoSlot ? 0 : td[f];
+      }
+    }
+    occupancy[sub] = kept;
+  }
+}
+
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
                  int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np) {
   const uint32_t n = std::min(*list_n, list_cap);

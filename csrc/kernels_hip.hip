@@ -1342,6 +1342,104 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// Keyed-window table maintenance for the host-DRAM spill tier (hashed keys): one workgroup per
+// sub-table. A key with no data in the live panes is dropped (the tables never delete keys
+// otherwise); a key whose newest data pane is <= cutoff is evicted: its live (pane, acc, cnt,
+// dirty) rows go to the host tier. The kept keys are re-inserted into a fresh LDS table (no
+// tombstones: window_agg's probe stays a plain linear probe) and each live pane's slice is
+// permuted through LDS to the new positions.
+// LDS: old keys | new keys | pane acc [cap] u64, then from-slot | pane cnt [cap] u32, dirty [cap].
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void window_compact_kernel(
+    uint64_t* __restrict__ keys_g, uint64_t* __restrict__ acc_g, uint32_t* __restrict__ cnt_g,
+    uint8_t* __restrict__ dirty_g, int cap_log2, int ring, int64_t nslots, int64_t p_lo, int np,
+    int64_t cutoff, CompactOut out, uint32_t* __restrict__ occupancy) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const uint32_t cap = 1u << cap_log2, mask = cap - 1;
+  const size_t sbase = (size_t)blockIdx.x << cap_log2;
+  uint64_t* sold = (uint64_t*)smem;
+  uint64_t* snew = sold + cap;
+  uint64_t* sacc = snew + cap;
+  uint32_t* sfrom = (uint32_t*)(sacc + cap);
+  uint32_t* scnt = sfrom + cap;
+  uint8_t* sdirty = (uint8_t*)(scnt + cap);
+  uint32_t* sc = (uint32_t*)(sdirty + cap);  // [0] dropped, [1] evicted, [2] overflow, [3] kept
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
+    sold[i] = keys_g[sbase + i];
+    snew[i] = kEmptyKey;
+    sfrom[i] = kNoSlot;
+  }
+  if (threadIdx.x < 4) sc[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t s = threadIdx.x; s < cap; s += blockDim.x) {
+    const uint64_t k = sold[s];
+    if (k == kEmptyKey || k == kTombKey) continue;
+    int64_t newest = INT64_MIN;
+    for (int j = 0; j < np; ++j) {
+      const int64_t p = p_lo + j;
+      if (cnt_g[(size_t)(p & (ring - 1)) * nslots + sbase + s]) newest = p;
+    }
+    if (newest == INT64_MIN) {
+      atomicAdd(&sc[0], 1u);
+      continue;
+    }
+    if (newest <= cutoff) {
+      atomicAdd(&sc[1], 1u);
+      for (int j = 0; j < np; ++j) {
+        const int64_t p = p_lo + j;
+        const size_t gi = (size_t)(p & (ring - 1)) * nslots + sbase + s;
+        const uint32_t c = cnt_g[gi];
+        if (!c) continue;
+        const uint32_t q = atomicAdd(out.n, 1u);
+        if (q < out.cap) {
+          out.key[q] = k;
+          out.pane[q] = p;
+          out.acc[q] = acc_g[gi];
+          out.cnt[q] = c;
+          out.dirty[q] = dirty_g[gi];
+        } else {
+          atomicOr(&sc[2], 1u);
+        }
+      }
+      continue;
+    }
+    int ins = 0;
+    const uint32_t t = lds_probe_insert(snew, k, mask, &ins);
+    if (t == kNoSlot) {
+      atomicOr(&sc[2], 1u);
+      continue;
+    }
+    sfrom[t] = s;
+    atomicAdd(&sc[3], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) keys_g[sbase + i] = snew[i];
+  for (int j = 0; j < np; ++j) {
+    const size_t pb = (size_t)((p_lo + j) & (ring - 1)) * nslots + sbase;
+    for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
+      sacc[i] = acc_g[pb + i];
+      scnt[i] = cnt_g[pb + i];
+      sdirty[i] = dirty_g[pb + i];
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
+      const uint32_t f = sfrom[i];
+      const bool has = f != kNoSlot;
+      acc_g[pb + i] = has ? sacc[f] : 0ull;
+      cnt_g[pb + i] = has ? scnt[f] : 0u;
+      dirty_g[pb + i] = has ? sdirty[f] : (uint8_t)0;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    occupancy[blockIdx.x] = sc[3];
+    atomicAdd(&out.counters[0], sc[0]);
+    atomicAdd(&out.counters[1], sc[1]);
+    if (sc[2]) atomicOr(&out.counters[2], 1u);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Sender-side combiner (G > 1): one workgroup per send bucket (dest rank, sub-table) folds its raw
 // records into a fresh LDS table of that sub-table's geometry and writes one pre-aggregated
 // record per (key, pane): val = exported accumulator, aux = element count. The all-to-all then
@@ -3089,6 +3187,27 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
                      dim3(kFireThreads), lds,
                      (hipStream_t)stream, keys_g, acc_g, cnt_g, dirty_g, plan, out_keys, out_vals,
                      out_raw, out_cnt, out_n);
+  HIP_CHECK(hipGetLastError());
+}
+
+void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
+                    int nsub, int cap_log2, int ring, int64_t p_lo, int np, int64_t cutoff,
+                    const CompactOut& out, uint32_t* occupancy, intptr_t stream) {
+  if (nsub <= 0) return;
+  if (cap_log2 > 12 || np > ring || np < 0)
+    throw std::invalid_argument("window_compact: sub-table > 4096 slots or bad pane range");
+  const size_t cap = (size_t)1 << cap_log2;
+  const size_t lds = cap * (8 * 3 + 4 * 2 + 1) + 16;
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)window_compact_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  const int64_t nslots = (int64_t)nsub << cap_log2;
+  hipLaunchKernelGGL(window_compact_kernel, dim3(nsub), dim3(1024), lds, (hipStream_t)stream,
+                     keys_g, acc_g, cnt_g, dirty_g, cap_log2, ring, nslots, p_lo, np, cutoff, out,
+                     occupancy);
   HIP_CHECK(hipGetLastError());
 }
 

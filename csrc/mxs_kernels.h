@@ -83,6 +83,18 @@ struct RollPlan {
 };
 
 // ---- GPU launchers (kernels_hip.hip) --------------------------------------------------------
+// Keyed-window table maintenance (host-DRAM spill tier): rows of evicted (key, pane) state.
+struct CompactOut {
+  uint64_t* key;
+  int64_t* pane;
+  uint64_t* acc;
+  uint32_t* cnt;
+  uint8_t* dirty;
+  uint32_t* n;        // rows written (device counter)
+  uint32_t cap;       // row capacity (>= occupied slots x live panes)
+  uint32_t* counters; // [0] keys dropped (no live data), [1] keys evicted, [2] overflow flag
+};
+
 constexpr int kD2HMax = 8;
 struct D2HCopy {
   const void* src;
@@ -193,6 +205,12 @@ void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t*
                       const uint32_t* n_in, const ScatPlan& plan, const int32_t* jhash,
                       const int32_t* kg_dest, uint32_t* cursor, Rec* out, uint32_t* flags,
                       intptr_t stream);
+// Per sub-table: drop keys without live data, move keys whose newest data pane <= cutoff out
+// (rows), rehash the kept keys into a tombstone-free table carrying their pane state along
+// (live panes [p_lo, p_lo + np) of the ring). occupancy[sub] = kept keys.
+void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
+                    int nsub, int cap_log2, int ring, int64_t p_lo, int np, int64_t cutoff,
+                    const CompactOut& out, uint32_t* occupancy, intptr_t stream);
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
                  int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np,
                  intptr_t stream);
@@ -238,6 +256,12 @@ void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uin
 void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt,
                       const uint32_t* n_in, const ScatPlan& plan, const int32_t* jhash,
                       const int32_t* kg_dest, uint32_t* cursor, Rec* out, uint32_t* flags);
+// Per sub-table: drop keys without live data, move keys whose newest data pane <= cutoff out
+// (rows), rehash the kept keys into a tombstone-free table carrying their pane state along
+// (live panes [p_lo, p_lo + np) of the ring). occupancy[sub] = kept keys.
+void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
+                    int nsub, int cap_log2, int ring, int64_t p_lo, int np, int64_t cutoff,
+                    const CompactOut& out, uint32_t* occupancy);
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
                  int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np);
 }  // namespace cpu

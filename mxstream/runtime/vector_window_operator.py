@@ -68,7 +68,8 @@ class VectorWindowOperator(KeyedWindowOperator):
         self._vec = vecs
         return super().process(keys, ts, self._rows[:n])
 
-    _local_global_ok = False  # vector panes are exchanged per step (records mode)
+    _local_global_ok = False
+    _spill_ok = False  # vector panes are exchanged per step (records mode)
     _use_dlist = False        # its own fire kernel sweeps the table
     _narrow_ok = False        # records carry a row index into the vector batch
     _dense_ok = False         # its own aggregation kernel

@@ -263,7 +263,9 @@ class KeyedWindowOperator:
                  combine: bool | None = None, compact: bool | None = None,
                  narrow: bool | None = None, dense_keys: bool = False,
                  pipeline: bool | str | None = None, exchange: str = "auto",
-                 idle_timeout_steps: int | None = None, deterministic: bool = False):
+                 idle_timeout_steps: int | None = None, deterministic: bool = False,
+                 spill: bool = False, spill_load: float = 0.8, spill_check_steps: int = 8,
+                 spill_keep_panes: int | None = None):
         """deterministic: f64 sums/averages accumulate each step's per-slot sum in 128-bit fixed
         point (order-independent integer adds, one rounding per slot and step), so results are
         bit-identical between runs, between the GPU and the C++ twin, and independent of the
@@ -272,6 +274,10 @@ class KeyedWindowOperator:
         this mode (raw records are exchanged). Integer aggregates are always exact."""
         self.device = K.resolve_device(device)
         self.deterministic = bool(deterministic) and agg in (K.AGG_SUM_F64, K.AGG_AVG_F64)
+        # spill: host-DRAM tier for hashed keys (runtime/window_spill.py). Every
+        # `spill_check_steps` steps, a sub-table above `spill_load` of its slots triggers
+        # window_compact: keys without live data are dropped, keys whose newest data pane is
+        # older than the newest `spill_keep_panes` panes (default: one window) move to the tier.
         self.comm = comm or LocalComm()
         self.world = self.comm.world
         self.rank = self.comm.rank
@@ -462,6 +468,16 @@ class KeyedWindowOperator:
         from ..ops.debug import debug_enabled
 
         self._debug = debug_enabled()  # MXS_DEBUG: table invariant check after every step
+        self.host_tier = None
+        if spill:
+            if self.dense_bits or self.local_global or not type(self)._spill_ok:
+                raise ValueError("spill needs hashed keys, records exchange and a plain reduce")
+            from .window_spill import HostWindowTier
+
+            self.host_tier = HostWindowTier(agg)
+        self.spill_load, self.spill_check_steps = float(spill_load), max(1, int(spill_check_steps))
+        self.spill_keep_panes = spill_keep_panes
+        self._spill_out = None
 
         # ---- watermark / firing bookkeeping (host, identical on every rank) ----
         self.wm = I64_MIN
@@ -471,6 +487,7 @@ class KeyedWindowOperator:
         self.late_side: list[np.ndarray] = []
 
     _local_global_ok = True  # subclasses whose fire is not a plain reduce opt out
+    _spill_ok = True         # subclasses whose state is not (acc, cnt) per slot opt out
     _narrow_ok = True        # subclasses whose records carry more than (key, value) opt out
     _dense_ok = True         # subclasses with their own aggregation kernel opt out
 
@@ -935,9 +952,71 @@ class KeyedWindowOperator:
                 with self._stage("fire"):
                     out.extend(self._fire_ready(b.new_wm))
                     self._purge(b.new_wm)
+            if self.host_tier is not None and self.metrics.steps % self.spill_check_steps == 0:
+                self._maybe_spill()
         if self.timer is not None:
             self.timer.flush()
         return out
+
+    # ---- host-DRAM spill tier (runtime/window_spill.py) -----------------------------------
+    def _maybe_spill(self) -> None:
+        cap = 1 << self.cap_log2
+        if int(self.occ.max()) <= self.spill_load * cap or self.max_seen_pane is None:
+            return
+        keep = self.spill_keep_panes or self.panes_per_window
+        self.compact_state(self.max_seen_pane - keep)
+
+    def compact_state(self, cutoff_pane: int | None = None) -> dict:
+        """Table maintenance at a step boundary: drop keys without live data and (with the spill
+        tier) move keys whose newest data pane is <= cutoff_pane to host DRAM. Returns counts."""
+        if self.dense_bits:
+            return {"dropped": 0, "evicted": 0, "rows": 0}
+        if cutoff_pane is not None and self.host_tier is None:
+            raise ValueError("evicting keys needs the spill tier (spill=True)")
+        self._drain()
+        dev = self.device
+        cuda = dev.type == "cuda"
+        if self.min_live_pane is None:
+            p_lo, np_ = 0, 0
+        else:
+            p_lo, np_ = self.min_live_pane, min(self.ring, self.max_seen_pane - self.min_live_pane + 1)
+        cutoff = I64_MIN if cutoff_pane is None else int(cutoff_pane)
+        rows_cap = max(1, int(self.occ.sum()) * max(np_, 1)) if cutoff != I64_MIN else 1
+        o = self._spill_out
+        if o is None or o["key"].numel() < rows_cap:
+            o = self._spill_out = {
+                "key": torch.empty(rows_cap, dtype=torch.int64, device=dev),
+                "pane": torch.empty(rows_cap, dtype=torch.int64, device=dev),
+                "acc": torch.empty(rows_cap, dtype=torch.int64, device=dev),
+                "cnt": torch.empty(rows_cap, dtype=torch.int32, device=dev),
+                "dirty": torch.empty(rows_cap, dtype=torch.uint8, device=dev),
+                "ctr": torch.zeros(4, dtype=torch.int32, device=dev)}
+        o["ctr"].zero_()
+        ptrs = [o["key"].data_ptr(), o["pane"].data_ptr(), o["acc"].data_ptr(),
+                o["cnt"].data_ptr(), o["dirty"].data_ptr(), o["ctr"][3:4].data_ptr(),
+                o["ctr"].data_ptr()]
+        args = (self.keys_g.data_ptr(), self.acc_g.data_ptr(), self.cnt_g.data_ptr(),
+                self.dirty_g.data_ptr(), self.nsub, self.cap_log2, self.ring, p_lo, np_, cutoff,
+                ptrs, o["key"].numel(), self.occ.data_ptr())
+        if cuda:
+            self._m.gpu_window_compact(*args, torch.cuda.current_stream(dev).cuda_stream)
+        else:
+            self._m.cpu_window_compact(*args)
+        ctr = o["ctr"].tolist()
+        if ctr[2]:
+            raise RuntimeError("window_compact: eviction rows overflowed (internal error)")
+        n = ctr[3]
+        if n and self.host_tier is not None:
+            self.host_tier.absorb(o["key"][:n].cpu().numpy().view(np.uint64),
+                                  o["pane"][:n].cpu().numpy(), o["acc"][:n].cpu().numpy(),
+                                  o["cnt"][:n].cpu().numpy(), o["dirty"][:n].cpu().numpy())
+        # (Touched-slot lists and dirty bytes are empty here: every step's re-firings cleared
+        # them before this step boundary, so no slot id survives the rehash.)
+        ex = self.metrics.extra
+        ex["dropped_keys"] = ex.get("dropped_keys", 0) + ctr[0]
+        ex["spilled_keys"] = ex.get("spilled_keys", 0) + ctr[1]
+        ex["spilled_rows"] = ex.get("spilled_rows", 0) + n
+        return {"dropped": ctr[0], "evicted": ctr[1], "rows": n}
 
     # ---- hooks (overridden by the vector-metric operator) ---------------------------------
     def _exchange(self, rw: int) -> None:
@@ -1015,6 +1094,8 @@ class KeyedWindowOperator:
             return None
         if self.local_global:
             return self._fire_window_partials(s, p0, p1)
+        if self.host_tier is not None and self.host_tier.overlaps(p0, p1):
+            return self._fire_window_tiered(s, p0, p1, only_dirty)
         self.out_n.zero_()
         K.window_fire(self.keys_g, self.acc_g, self.cnt_g, self.dirty_g, agg=self.agg,
                       npanes=p1 - p0 + 1, ring=self.ring, p0=p0, wstart=s,
@@ -1033,6 +1114,32 @@ class KeyedWindowOperator:
                               self._pool)
         return FireResult(s, s + self.size, host[0].view(np.uint64), host[1], host[2], host[3],
                           refire=only_dirty)
+
+    def _fire_window_tiered(self, s: int, p0: int, p1: int, only_dirty: bool) -> FireResult | None:
+        """Window [s, s + size) with part of its state in the host tier: the device fires
+        without its epilogue, the tier's share is combined per key, the epilogue runs here."""
+        from .window_spill import merge_fire
+
+        self.out_n.zero_()
+        K.window_fire(self.keys_g, self.acc_g, self.cnt_g, self.dirty_g, agg=self.agg,
+                      npanes=p1 - p0 + 1, ring=self.ring, p0=p0, wstart=s, wend=s + self.size,
+                      only_dirty=only_dirty, map_prog=E.EMPTY, filt_prog=E.EMPTY,
+                      out_keys=self.out_keys, out_vals=self.out_vals, out_raw=self.out_raw,
+                      out_cnt=self.out_cnt, out_n=self.out_n,
+                      slot_list=self.dlist if only_dirty else None,
+                      slot_list_n=self.dlist_n if only_dirty else None)
+        n = min(self._fired_count(), self.out_keys.numel())
+        self.metrics.num_fires += 1
+        dk, dr, dc = (t[:n].cpu().numpy() for t in (self.out_keys, self.out_raw, self.out_cnt))
+        if only_dirty and n == 0:
+            return None
+        keys, vals, raw, cnt = merge_fire(self.agg, dk.view(np.uint64), dr, dc,
+                                          self.host_tier.part(p0, p1), only_dirty,
+                                          self.map_prog, self.filter_prog, s, s + self.size)
+        if not keys.size:
+            return None
+        self.metrics.num_records_out += int(keys.size)
+        return FireResult(s, s + self.size, keys, vals, raw, cnt, refire=only_dirty)
 
     def _fire_window_partials(self, s: int, p0: int, p1: int) -> FireResult | None:
         """Local-global fire of window [s, s + size): local partials -> owner -> emit.
@@ -1159,6 +1266,8 @@ class KeyedWindowOperator:
             # Earliest window that is not cleaned: s + size - 1 + lateness > wm.
             s = self._align_up(wm - self.size - self.lateness + 2)
             keep_from = self.pane_of(s)
+        if self.host_tier is not None:
+            self.host_tier.purge(keep_from)
         p = self.min_live_pane
         stop = min(keep_from, self.max_seen_pane + 1)
         if stop - p > self.ring:
@@ -1176,6 +1285,10 @@ class KeyedWindowOperator:
     def state_bytes(self) -> int:
         return sum(t.numel() * t.element_size() for t in (self.keys_g, self.acc_g, self.cnt_g,
                                                           self.dirty_g))
+
+    def host_state_bytes(self) -> int:
+        """Bytes of keyed state in the host-DRAM tier (0 without spill)."""
+        return 0 if self.host_tier is None else self.host_tier.nbytes
 
     def num_keys(self) -> int:
         self._sync_state()
@@ -1234,6 +1347,19 @@ class KeyedWindowOperator:
                     "acc": self.acc_g[idx][sel].cpu().numpy(),
                     "cnt": cnt[sel].cpu().numpy(),
                     "dirty": self.dirty_g[idx][sel].cpu().numpy()}
+        if self.host_tier is not None and self.host_tier.nrows:
+            # Spilled state travels in the same rows (restore folds duplicate (key, pane) rows).
+            h = self.host_tier.rows()
+            hk = torch.from_numpy(h["key"].view(np.int64))
+            kg = np.concatenate([kg, K.keygroups(hk, max_parallelism=self.max_parallelism,
+                                                 hash_mode=self.hash_mode,
+                                                 jhash=None if self.jhash is None else self.jhash.cpu()
+                                                 ).numpy()]).astype(np.int32)
+            cols = {"key": np.concatenate([cols["key"], h["key"].view(np.int64)]),
+                    "pane": np.concatenate([cols["pane"], h["pane"]]),
+                    "acc": np.concatenate([cols["acc"], h["acc"]]),
+                    "cnt": np.concatenate([cols["cnt"], h["cnt"].astype(np.int32)]),
+                    "dirty": np.concatenate([cols["dirty"], h["dirty"]])}
         meta = {"kind": "window", "size": self.size, "slide": self.slide, "offset": self.offset,
                 "lateness": self.lateness, "agg": self.agg, "time_mode": self.time_mode,
                 "wm": self.wm, "next_fire_start": self.next_fire_start,
@@ -1247,6 +1373,8 @@ class KeyedWindowOperator:
     def restore_state(self, rows: dict, meta: dict) -> None:
         """Rebuild the tables from checkpoint rows (this rank's key groups only)."""
         self._check_ckpt_meta(meta)
+        if self.host_tier is not None:
+            self.host_tier.clear()
         self._pending, self._carry = None, []
         self._drain()
         dev = self.device

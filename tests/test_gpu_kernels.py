@@ -412,3 +412,19 @@ def test_deterministic_f64_sums_gpu_bit_exact(gpu_device, dense):
 
     g1, g2, c = run(gpu_device), run(gpu_device), run("cpu")
     assert g1 == c and g2 == c and len(c) > 1000
+
+
+def test_spill_tier_gpu_matches_unbounded_cpu(gpu_device):
+    """window_compact on the GPU (LDS rehash of every sub-table, eviction rows to the host
+    tier) + tiered firings == an unbounded C++-twin table."""
+    import sys
+
+    sys.path.insert(0, __import__("os").path.dirname(__file__))
+    from test_window_operator_cpu import _drift_batches, _run_windows
+
+    batches = _drift_batches(26, 6000)
+    ref, _ = _run_windows(batches, max_keys=80_000)
+    got, op = _run_windows(batches, device=gpu_device, max_keys=3000, spill=True,
+                           spill_check_steps=1, spill_load=0.5, cap_log2=7, spill_keep_panes=1)
+    assert op.metrics.extra.get("spilled_keys", 0) > 0
+    assert got == ref

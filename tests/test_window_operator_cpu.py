@@ -339,3 +339,120 @@ def test_deterministic_f64_sums_order_independent(agg_name):
         vals += v[sel].view(torch.float64).tolist()
     got = float(np.int64(raw).view(np.float64))
     assert abs(got - math.fsum(vals)) <= 1e-9 * max(1.0, abs(math.fsum(vals)))
+
+
+def _drift_batches(steps, n, seed=9):
+    """Keys drift over time (1500 new ids per step) plus 50 hot ids: many more distinct keys
+    than the table holds, most of them cold after a few steps."""
+    import torch
+
+    rng = np.random.default_rng(seed)
+    out = []
+    for step in range(steps):
+        k = np.where(rng.random(n) < 0.1, rng.integers(0, 50, n),
+                     1000 + step * 1500 + rng.integers(0, 2000, n)).astype(np.int64)
+        t = (step * 1000 + rng.integers(0, 1000, n)).astype(np.int64)
+        t[rng.random(n) < 0.03] -= 2500  # late, within the allowed lateness
+        v = rng.integers(0, 1000, n).astype(np.int64)
+        out.append((torch.from_numpy(k), torch.from_numpy(t), torch.from_numpy(v)))
+    return out
+
+
+def _run_windows(batches, **kw):
+    from mxstream.ops import expr as E
+    from mxstream.ops import kernels as K
+    from mxstream.runtime.window_operator import KeyedWindowOperator
+
+    op = KeyedWindowOperator(size=6000, slide=2000, lateness=3000, agg=K.AGG_SUM_I64,
+                             device=kw.pop("device", "cpu"), batch_capacity=6000, ooo_bound=500,
+                             map_prog=E.compile_expr(E.var(E.VAR_RESULT) * 0.5),
+                             filter_prog=E.compile_expr(E.var(E.VAR_COUNT) > 1), **kw)
+    rows = []
+    for k, t, v in batches:
+        rows += op.process(k.to(op.device), t.to(op.device), v.to(op.device))
+    rows += op.finish()
+    got = sorted((r.window_start, r.refire, int(a), int(b), int(c), float(x))
+                 for r in rows for a, b, c, x in zip(r.keys, r.raw, r.counts, r.values))
+    return got, op
+
+
+def test_spill_tier_matches_unbounded_table():
+    """A hashed-key table far smaller than the key space: window_compact drops keys without
+    live data and moves cold keys' live panes to the host tier; every firing and late re-firing
+    (device part + host part, epilogue on the host) equals a table that holds every key."""
+    batches = _drift_batches(26, 6000)  # ~40K distinct keys over a 32K-slot table
+    ref, _ = _run_windows(batches, max_keys=80_000)
+    got, op = _run_windows(batches, max_keys=3000, spill=True, spill_check_steps=1,
+                           spill_load=0.5, cap_log2=7, spill_keep_panes=1)
+    ex = op.metrics.extra
+    assert ex.get("spilled_keys", 0) > 0 and ex.get("spilled_rows", 0) > 0
+    assert got == ref
+    import pytest as _pt
+
+    with _pt.raises(RuntimeError, match="table full"):
+        _run_windows(batches, max_keys=3000, cap_log2=7)
+
+
+def test_spill_tier_checkpoint_roundtrip():
+    """Spilled state is part of the snapshot; a restored operator fires the same windows."""
+    batches = _drift_batches(12, 6000, seed=4)
+    ref, _ = _run_windows(batches, max_keys=60_000)
+    from mxstream.ops import expr as E
+    from mxstream.ops import kernels as K
+    from mxstream.runtime.window_operator import KeyedWindowOperator
+
+    def make():
+        return KeyedWindowOperator(size=6000, slide=2000, lateness=3000, agg=K.AGG_SUM_I64,
+                                   device="cpu", batch_capacity=6000, ooo_bound=500,
+                                   map_prog=E.compile_expr(E.var(E.VAR_RESULT) * 0.5),
+                                   filter_prog=E.compile_expr(E.var(E.VAR_COUNT) > 1),
+                                   max_keys=3000, spill=True, spill_check_steps=1,
+                                   spill_load=0.5, cap_log2=7, spill_keep_panes=1)
+
+    op = make()
+    rows = []
+    for k, t, v in batches[:7]:
+        rows += op.process(k, t, v)
+    rows += op.flush()
+    assert op.host_state_bytes() > 0
+    snap = op.snapshot_state()
+    op2 = KeyedWindowOperator(size=6000, slide=2000, lateness=3000, agg=K.AGG_SUM_I64,
+                              device="cpu", batch_capacity=6000, ooo_bound=500,
+                              map_prog=E.compile_expr(E.var(E.VAR_RESULT) * 0.5),
+                              filter_prog=E.compile_expr(E.var(E.VAR_COUNT) > 1),
+                              max_keys=60_000)
+    op2.restore_state(snap.columns, snap.meta)
+    for k, t, v in batches[7:]:
+        rows += op2.process(k, t, v)
+    rows += op2.finish()
+    got = sorted((r.window_start, r.refire, int(a), int(b), int(c), float(x))
+                 for r in rows for a, b, c, x in zip(r.keys, r.raw, r.counts, r.values))
+    assert got == ref
+
+
+def test_compact_state_drops_dead_keys():
+    """compact_state() without a cutoff (no spill tier): keys with no data in the live panes are
+    dropped and the kept keys rehashed; later firings are unchanged."""
+    batches = _drift_batches(10, 6000, seed=2)
+    ref, _ = _run_windows(batches, max_keys=60_000)
+    from mxstream.ops import expr as E
+    from mxstream.ops import kernels as K
+    from mxstream.runtime.window_operator import KeyedWindowOperator
+
+    op = KeyedWindowOperator(size=6000, slide=2000, lateness=3000, agg=K.AGG_SUM_I64,
+                             device="cpu", batch_capacity=6000, ooo_bound=500,
+                             map_prog=E.compile_expr(E.var(E.VAR_RESULT) * 0.5),
+                             filter_prog=E.compile_expr(E.var(E.VAR_COUNT) > 1), max_keys=60_000)
+    rows = []
+    dropped = 0
+    for i, (k, t, v) in enumerate(batches):
+        rows += op.process(k, t, v)
+        if i % 3 == 2:
+            rows += op.flush()
+            before = int((op.keys_g != -1).sum())
+            dropped += op.compact_state()["dropped"]
+            assert int((op.keys_g != -1).sum()) <= before
+    rows += op.finish()
+    got = sorted((r.window_start, r.refire, int(a), int(b), int(c), float(x))
+                 for r in rows for a, b, c, x in zip(r.keys, r.raw, r.counts, r.values))
+    assert dropped > 0 and got == ref
