@@ -68,6 +68,39 @@ MXS_API int64_t mxs_pipeline_take_results(mxs_pipeline* p, mxs_window_result* ou
 MXS_API int64_t mxs_pipeline_watermark(const mxs_pipeline* p);
 MXS_API int64_t mxs_pipeline_late_dropped(const mxs_pipeline* p);
 MXS_API int64_t mxs_pipeline_records_in(const mxs_pipeline* p);
+/* ---- keyed rolling aggregates and tumbling count windows ------------------------------------
+ * keyBy(k).sum/min/max(v) with one output row per input record (StreamGroupedReduce,
+ * chapter2/src/main/java/me/zjy/ComputeCpuMax.java:26), or keyBy(k).countWindow(n) with an
+ * incremental aggregate (one row per completed window; count_window = n > 0). One rank; the
+ * gfx950 kernels (device = 1: table lookup -> radix sort -> per-key ordered / segmented wave
+ * scan) or their C++ twins (device = 0). Rows come out in input order of the emitting records. */
+typedef struct mxs_rolling_config {
+  int32_t agg;              /* MXS_AGG_* (avg only with count windows) */
+  int32_t device;           /* 0 = C++ twins, 1 = HIP device */
+  int32_t device_index;
+  int32_t reserved;
+  int64_t max_keys;         /* keyed state sizing */
+  int64_t batch_capacity;   /* events per process() call (grows on demand) */
+  int64_t count_window;     /* 0: rolling aggregate; n > 0: tumbling count windows of n */
+} mxs_rolling_config;
+
+typedef struct mxs_rolling_row {
+  uint64_t key;
+  int64_t raw;              /* aggregate: integer / f64 bit pattern (avg: the sum); count: n */
+  int64_t index;            /* position of the emitting record in its process() batch */
+} mxs_rolling_row;
+
+typedef struct mxs_rolling mxs_rolling;
+
+MXS_API void mxs_rolling_config_default(mxs_rolling_config* cfg);
+MXS_API mxs_rolling* mxs_rolling_create(const mxs_rolling_config* cfg);
+MXS_API void mxs_rolling_destroy(mxs_rolling* r);
+/* One micro-batch (host arrays: keys, int64 values / f64 bit patterns); rows queue up. */
+MXS_API int mxs_rolling_process(mxs_rolling* r, const uint64_t* keys, const int64_t* vals,
+                                int64_t n);
+MXS_API int64_t mxs_rolling_num_rows(const mxs_rolling* r);
+MXS_API int64_t mxs_rolling_take_rows(mxs_rolling* r, mxs_rolling_row* out, int64_t cap);
+
 MXS_API const char* mxs_last_error(void);
 MXS_API const char* mxs_version(void);
 

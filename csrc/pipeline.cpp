@@ -494,9 +494,180 @@ class WindowPipeline {
 }  // namespace mxs
 
 // ---- C ABI ----------------------------------------------------------------------------------
+namespace mxs {
+// The single-rank control loop of runtime/rolling_operator.py (KeyedRollingOperator) in C++:
+// GPU = _process_direct (rolling_lookup_direct -> sort_pairs over the slot bits -> rolling_heads
+// -> rolling_scan, count_n for count windows); CPU = partition (window_mode 0) -> rolling_rows.
+class RollingPipeline {
+ public:
+  explicit RollingPipeline(const mxs_rolling_config& c) : cfg_(c) {
+    if (c.agg < AGG_SUM_I64 || c.agg > AGG_AVG_I64) throw std::invalid_argument("unknown aggregate");
+    if ((c.agg == AGG_AVG_F64 || c.agg == AGG_AVG_I64) && c.count_window <= 0)
+      throw std::invalid_argument("rolling avg is not a Flink rolling aggregate (count windows only)");
+    if (c.count_window < 0 || c.count_window >= ((int64_t)1 << 31))
+      throw std::invalid_argument("count window size out of range");
+    mem_.gpu = c.device != 0;
+    if (mem_.gpu) {
+      hip_ok(hipSetDevice(c.device_index), "hipSetDevice");
+      hip_ok(hipStreamCreateWithFlags(&mem_.stream, hipStreamNonBlocking), "hipStreamCreate");
+    }
+    state_geometry(std::max<int64_t>(c.max_keys, 1), &nsub_, &cap_log2_);
+    nsub_log2_ = 0;
+    while ((1 << nsub_log2_) < nsub_) ++nsub_log2_;
+    nslots_ = (int64_t)nsub_ << cap_log2_;
+    keys_g_ = (uint64_t*)mem_.alloc(nslots_ * 8);
+    mem_.fill(keys_g_, 0xFF, nslots_ * 8);
+    acc_g_ = (uint64_t*)mem_.alloc(nslots_ * 8);
+    mem_.fill(acc_g_, 0, nslots_ * 8);
+    cnt_g_ = (uint32_t*)mem_.alloc(nslots_ * 4);
+    mem_.fill(cnt_g_, 0, nslots_ * 4);
+    flags_ = (uint32_t*)mem_.alloc(16);
+    mem_.fill(flags_, 0, 16);
+    nbuf_ = (uint32_t*)mem_.alloc(16);
+    kg_dest_ = (int32_t*)mem_.alloc(128 * 4);
+    mem_.fill(kg_dest_, 0, 128 * 4);
+    stats_ = (int64_t*)mem_.alloc(kStatCount * 8);
+    grow(std::max<int64_t>(c.batch_capacity, 1024));
+  }
+  ~RollingPipeline() {
+    if (mem_.gpu && mem_.stream) {
+      (void)hipStreamSynchronize(mem_.stream);
+      (void)hipStreamDestroy(mem_.stream);
+    }
+  }
+
+  void process(const uint64_t* keys_h, const int64_t* vals_h, int64_t n) {
+    if (n < 0) throw std::invalid_argument("negative batch size");
+    if (n == 0) return;
+    if (n >= ((int64_t)1 << 31)) throw std::invalid_argument("batch too large");
+    if (n > cap_) grow(n);
+    mem_.to_dev(in_keys_, keys_h, n * 8);
+    mem_.to_dev(in_vals_, vals_h, n * 8);
+    const ExprProg none{};
+    uint32_t hn[4];
+    if (mem_.gpu) {
+      const intptr_t st = (intptr_t)mem_.stream;
+      mem_.fill(nbuf_, 0, 16);
+      int shift = 1;
+      while (((int64_t)1 << shift) < n) ++shift;
+      int nb = 0;
+      while (((int64_t)1 << nb) <= nslots_) ++nb;  // bit length of nslots
+      gpu::rolling_lookup_direct(in_keys_, in_vals_, (uint32_t)n, nsub_log2_, cap_log2_, keys_g_,
+                                 sort_key_, vals_buf_, nbuf_, flags_, shift, st);
+      const int nbits = shift + nb;
+      const size_t need = gpu::sort_pairs_temp_bytes(n, shift, nbits);
+      if (need > temp_bytes_) {
+        mem_.release(temp_);
+        temp_ = mem_.alloc(need);
+        temp_bytes_ = need;
+      }
+      gpu::sort_pairs(temp_, temp_bytes_, (const uint64_t*)sort_key_, (uint64_t*)sort_out_,
+                      vals_buf_, vals_out_, n, shift, nbits, st);
+      gpu::rolling_heads(sort_out_, nbuf_, n, heads_, nbuf_ + 1, shift, st);
+      mem_.fill(flags_ + 2, 0, 4);  // emitted-row cursor
+      gpu::rolling_scan(cfg_.agg, sort_out_, nullptr, vals_out_, nbuf_, heads_, nbuf_ + 1,
+                        std::min<int64_t>(n, nslots_), acc_g_, cnt_g_, keys_g_, none, out_key_,
+                        out_val_, out_tag_, flags_ + 2, (uint32_t)cap_, shift, shift, st,
+                        (uint32_t)cfg_.count_window);
+    } else {
+      // Keyed (non-window) partition into sub-table buckets, then the sequential twin.
+      PartPlan pp;
+      std::memset(&pp, 0, sizeof(pp));
+      pp.max_parallelism = 128;
+      pp.nsub_log2 = nsub_log2_;
+      pp.nranks = 1;
+      pp.bucket_cap = bcap_;
+      pp.pane = 1;
+      pp.inv_pane = 1.0;
+      pp.rec_words = 3;
+      std::vector<int64_t> ts0((size_t)n, 0);
+      uint32_t* counts = (uint32_t*)heads_;  // nsub counters (host memory on the CPU path)
+      for (;;) {
+        cpu::step_begin(counts, nsub_, stats_);
+        cpu::partition(in_keys_, ts0.data(), in_vals_, nullptr, n, pp, kg_dest_, counts,
+                       (Rec*)sort_key_, stats_, nullptr, 0);
+        if (!(stats_[kStatOverflow] & 1)) break;
+        bcap_ *= 2;  // a bucket overflowed: larger buckets, same batch again
+        alloc_buckets();
+        pp.bucket_cap = bcap_;
+      }
+      flags_[2] = 0;
+      cpu::rolling_rows((const Rec*)sort_key_, counts, 1, nsub_, bcap_, cap_log2_, cfg_.agg,
+                        keys_g_, acc_g_, cnt_g_, flags_, none, out_key_, out_val_, out_tag_,
+                        flags_ + 2, (uint32_t)cap_, (uint32_t)cfg_.count_window);
+    }
+    mem_.to_host(hn, flags_, 16);
+    if (hn[0] & 1) throw std::runtime_error("keyed state table full: a key found no free slot (raise max_keys)");
+    if (hn[0] & 4) throw std::invalid_argument("key ids -1 and -2 are reserved");
+    const int64_t rows = std::min<int64_t>(hn[2], cap_);
+    if (!rows) return;
+    std::vector<uint64_t> k((size_t)rows), v((size_t)rows);
+    std::vector<int64_t> t((size_t)rows);
+    mem_.to_host(k.data(), out_key_, rows * 8);
+    mem_.to_host(v.data(), out_val_, rows * 8);
+    mem_.to_host(t.data(), out_tag_, rows * 8);
+    std::vector<int64_t> order((size_t)rows);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+      return (t[a] & 0xFFFFFFFF) < (t[b] & 0xFFFFFFFF);
+    });
+    for (int64_t j : order)
+      rows_.push_back(mxs_rolling_row{k[j], (int64_t)v[j], t[j] & 0xFFFFFFFF});
+    records_in_ += n;
+  }
+
+  std::deque<mxs_rolling_row> rows_;
+
+ private:
+  // sort_key_ doubles as the CPU path's bucketed Rec buffer (nsub x bcap records).
+  void alloc_buckets() {
+    mem_.release(sort_key_);
+    const int64_t recs = mem_.gpu ? cap_ : std::max<int64_t>((int64_t)nsub_ * bcap_, cap_);
+    sort_key_ = (int64_t*)mem_.alloc(recs * (mem_.gpu ? 8 : 24));
+  }
+
+  void grow(int64_t n) {
+    cap_ = std::max<int64_t>(n, cap_);
+    bcap_ = std::max<uint32_t>(bcap_, (uint32_t)std::max<int64_t>(64, (int64_t)(1.5 * (double)cap_ / nsub_ + 64)));
+    for (void* q : {(void*)in_keys_, (void*)in_vals_, (void*)sort_out_,
+                    (void*)vals_buf_, (void*)vals_out_, (void*)heads_, (void*)out_key_,
+                    (void*)out_val_, (void*)out_tag_})
+      mem_.release(q);
+    in_keys_ = (uint64_t*)mem_.alloc(cap_ * 8);
+    in_vals_ = (uint64_t*)mem_.alloc(cap_ * 8);
+    alloc_buckets();
+    sort_out_ = (int64_t*)mem_.alloc(cap_ * 8);
+    vals_buf_ = (uint64_t*)mem_.alloc(cap_ * 8);
+    vals_out_ = (uint64_t*)mem_.alloc(cap_ * 8);
+    heads_ = (uint32_t*)mem_.alloc(std::max<int64_t>(cap_, nsub_) * 4);
+    out_key_ = (uint64_t*)mem_.alloc(cap_ * 8);
+    out_val_ = (uint64_t*)mem_.alloc(cap_ * 8);
+    out_tag_ = (int64_t*)mem_.alloc(cap_ * 8);
+  }
+
+  mxs_rolling_config cfg_;
+  Mem mem_;
+  int nsub_ = 0, cap_log2_ = 0, nsub_log2_ = 0;
+  int64_t nslots_ = 0, cap_ = 0, records_in_ = 0;
+  uint32_t bcap_ = 0;
+  size_t temp_bytes_ = 0;
+  void* temp_ = nullptr;
+  uint64_t *keys_g_ = nullptr, *acc_g_ = nullptr, *in_keys_ = nullptr, *in_vals_ = nullptr;
+  uint64_t *vals_buf_ = nullptr, *vals_out_ = nullptr, *out_key_ = nullptr, *out_val_ = nullptr;
+  int64_t *sort_key_ = nullptr, *sort_out_ = nullptr, *out_tag_ = nullptr, *stats_ = nullptr;
+  uint32_t *cnt_g_ = nullptr, *flags_ = nullptr, *nbuf_ = nullptr, *heads_ = nullptr;
+  int32_t* kg_dest_ = nullptr;
+};
+}  // namespace mxs
+
 struct mxs_pipeline {
   mxs::WindowPipeline impl;
   explicit mxs_pipeline(const mxs_window_config& c) : impl(c) {}
+};
+
+struct mxs_rolling {
+  mxs::RollingPipeline impl;
+  explicit mxs_rolling(const mxs_rolling_config& c) : impl(c) {}
 };
 
 namespace {
@@ -570,6 +741,46 @@ int64_t mxs_pipeline_take_results(mxs_pipeline* p, mxs_window_result* out, int64
 int64_t mxs_pipeline_watermark(const mxs_pipeline* p) { return p ? p->impl.watermark() : INT64_MIN; }
 int64_t mxs_pipeline_late_dropped(const mxs_pipeline* p) { return p ? p->impl.late_dropped() : -1; }
 int64_t mxs_pipeline_records_in(const mxs_pipeline* p) { return p ? p->impl.records_in() : -1; }
+void mxs_rolling_config_default(mxs_rolling_config* c) {
+  if (!c) return;
+  std::memset(c, 0, sizeof(*c));
+  c->agg = MXS_AGG_SUM_I64;
+  c->max_keys = 1 << 16;
+  c->batch_capacity = 1 << 16;
+}
+
+mxs_rolling* mxs_rolling_create(const mxs_rolling_config* cfg) {
+  if (!cfg) {
+    mxs::g_err = "null config";
+    return nullptr;
+  }
+  mxs_rolling* r = nullptr;
+  if (guard([&] { r = new mxs_rolling(*cfg); }) != 0) return nullptr;
+  return r;
+}
+
+void mxs_rolling_destroy(mxs_rolling* r) { delete r; }
+
+int mxs_rolling_process(mxs_rolling* r, const uint64_t* keys, const int64_t* vals, int64_t n) {
+  if (!r || (n > 0 && (!keys || !vals))) {
+    mxs::g_err = "null argument";
+    return -1;
+  }
+  return guard([&] { r->impl.process(keys, vals, n); });
+}
+
+int64_t mxs_rolling_num_rows(const mxs_rolling* r) { return r ? (int64_t)r->impl.rows_.size() : -1; }
+
+int64_t mxs_rolling_take_rows(mxs_rolling* r, mxs_rolling_row* out, int64_t cap) {
+  if (!r || (cap > 0 && !out)) return -1;
+  int64_t n = 0;
+  while (n < cap && !r->impl.rows_.empty()) {
+    out[n++] = r->impl.rows_.front();
+    r->impl.rows_.pop_front();
+  }
+  return n;
+}
+
 const char* mxs_last_error(void) { return mxs::g_err.c_str(); }
 const char* mxs_version(void) { return "mxstream-native 0.1 (gfx950)"; }
 

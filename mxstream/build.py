@@ -139,7 +139,8 @@ def build_sanitize(verbose: bool = False) -> Path:
     return exe
 
 
-CAPI_SOURCES = ["kernels_hip.hip", "check_hip.hip", "kernels_cpu.cpp", "pipeline.cpp"]
+CAPI_SOURCES = ["kernels_hip.hip", "check_hip.hip", "sort_hip.hip", "kernels_cpu.cpp",
+                "pipeline.cpp"]
 
 
 def capi_path() -> Path:

@@ -141,3 +141,93 @@ def test_capi_gpu_equals_host(lib, gpu_device):
     a, la = _run_capi(lib, stream, 0, 3000, 1000, 2000)
     b, lb = _run_capi(lib, stream, 1, 3000, 1000, 2000)
     assert a == b and la == lb
+
+
+class RCfg(ctypes.Structure):
+    _fields_ = [("agg", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("device_index", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("max_keys", ctypes.c_int64), ("batch_capacity", ctypes.c_int64),
+                ("count_window", ctypes.c_int64)]
+
+
+class RRow(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_uint64), ("raw", ctypes.c_int64), ("index", ctypes.c_int64)]
+
+
+def _rolling_lib(L):
+    L.mxs_rolling_create.restype = ctypes.c_void_p
+    L.mxs_rolling_create.argtypes = [ctypes.POINTER(RCfg)]
+    L.mxs_rolling_destroy.argtypes = [ctypes.c_void_p]
+    L.mxs_rolling_process.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_int64]
+    L.mxs_rolling_take_rows.restype = ctypes.c_int64
+    L.mxs_rolling_take_rows.argtypes = [ctypes.c_void_p, ctypes.POINTER(RRow), ctypes.c_int64]
+    L.mxs_rolling_config_default.argtypes = [ctypes.POINTER(RCfg)]
+    return L
+
+
+def _run_rolling_capi(L, batches, device, agg, count_window):
+    L = _rolling_lib(L)
+    cfg = RCfg()
+    L.mxs_rolling_config_default(ctypes.byref(cfg))
+    cfg.agg, cfg.device, cfg.max_keys, cfg.batch_capacity = agg, device, 2000, 1024
+    cfg.count_window = count_window
+    r = L.mxs_rolling_create(ctypes.byref(cfg))
+    assert r, L.mxs_last_error()
+    out = []
+    buf = (RRow * 8192)()
+    try:
+        for step, (keys, vals) in enumerate(batches):
+            k, v = (np.ascontiguousarray(x.numpy()) for x in (keys, vals))
+            assert L.mxs_rolling_process(r, k.ctypes.data, v.ctypes.data, len(k)) == 0, L.mxs_last_error()
+            while True:
+                n = L.mxs_rolling_take_rows(r, buf, 8192)
+                if n <= 0:
+                    break
+                out += [(step, x.index, x.key, x.raw) for x in buf[:n]]
+    finally:
+        L.mxs_rolling_destroy(r)
+    return out
+
+
+@pytest.mark.parametrize("agg,count_window", [(K.AGG_SUM_I64, 0), (K.AGG_MAX_I64, 0),
+                                              (K.AGG_COUNT, 0), (K.AGG_SUM_I64, 7),
+                                              (K.AGG_AVG_I64, 16)])
+def test_capi_rolling_equals_python_operator(lib, agg, count_window):
+    """mxs_rolling_* (C++ control loop over the C++ twins) emits exactly the Python
+    KeyedRollingOperator's rows, in input order (keyed rolling state and count windows)."""
+    from mxstream.runtime.rolling_operator import KeyedRollingOperator
+
+    batches = []
+    for s in range(4):
+        keys = torch.empty(5000, dtype=torch.int64)
+        ts = torch.empty_like(keys)
+        vals = torch.empty_like(keys)
+        K.gen_events(keys, ts, vals, seed=3, stream_id=0, idx0=s * 5000, nkeys=1200,
+                     ts_base=0, ts_span=1000, disorder=0, val_lo=-300, val_span=1000)
+        batches.append((keys, vals))
+    got = _run_rolling_capi(lib, batches, 0, agg, count_window)
+    op = KeyedRollingOperator(agg=agg, device="cpu", max_keys=2000, batch_capacity=1024,
+                              count_window=count_window)
+    ref = []
+    for step, (keys, vals) in enumerate(batches):
+        rows = op.process(keys, vals)
+        order = np.argsort(rows.tags & 0xFFFFFFFF, kind="stable")
+        ref += [(step, int(rows.tags[i]) & 0xFFFFFFFF, int(rows.keys[i]), int(rows.values[i]))
+                for i in order]
+    assert got == ref and len(ref) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg,count_window", [(K.AGG_SUM_I64, 0), (K.AGG_AVG_I64, 16)])
+def test_capi_rolling_gpu_equals_host(lib, gpu_device, agg, count_window):
+    batches = []
+    for s in range(3):
+        keys = torch.empty(40_000, dtype=torch.int64)
+        ts = torch.empty_like(keys)
+        vals = torch.empty_like(keys)
+        K.gen_events(keys, ts, vals, seed=5, stream_id=0, idx0=s * 40_000, nkeys=1500,
+                     ts_base=0, ts_span=1000, disorder=0, val_lo=0, val_span=1000)
+        batches.append((keys, vals))
+    assert _run_rolling_capi(lib, batches, 1, agg, count_window) == \
+        _run_rolling_capi(lib, batches, 0, agg, count_window)
