@@ -187,12 +187,15 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
 
 
 def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_000,
-            drift: int = 400_000, table_keys: int = 4_000_000, device: str = "cuda") -> dict:
+            drift: int = 400_000, table_keys: int = 4_000_000, device: str = "cuda",
+            revisit: float = 0.0) -> dict:
     """Session windows (gap 5 s, 30 s allowed lateness) over a drifting active key set: each step
     draws events from `active` consecutive key ids whose window advances by `drift` ids, so keys
     go idle and their sessions close. The HBM slot table holds `table_keys` keys; idle keys whose
     fired sessions are still inside the allowed lateness are spilled to the host-DRAM store.
-    Alert: sessions whose volume exceeds 1.5x the expected mean (fused map/filter epilogue)."""
+    Alert: sessions whose volume exceeds 1.5x the expected mean (fused map/filter epilogue).
+    revisit > 0: that fraction of events (every round(1/revisit)-th) goes to keys that went idle
+    ~10 drift windows ago -- spilled keys whose records take the host-DRAM store path."""
     dev = torch.device(device)
     span, gap = 2_000, 5_000
     per_key_step = batch / active
@@ -214,6 +217,10 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
         K.gen_events(kt, tt, vt, seed=5, stream_id=0, idx0=i * batch, nkeys=active,
                      ts_base=i * span, ts_span=span, disorder=1_000, val_lo=0, val_span=10_000)
         kt.add_(i * drift)
+        if revisit > 0 and i >= 12:
+            stride = max(2, round(1.0 / revisit))
+            old = kt[::stride]
+            old.sub_(10 * drift + i * drift).remainder_(drift).add_((i - 10) * drift)
         rows = op.process(kt, tt, vt)
         step_i[0] += 1
         if len(rows):
@@ -248,7 +255,7 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
 
 
 def config6(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 1_000_000,
-            dim: int = 32, device: str = "cuda", mfma: bool = True) -> dict:
+            dim: int = 32, device: str = "cuda", mfma: bool = True, zipf: float = 0.0) -> dict:
     """Vector-metric window: 1-min tumbling event-time AVERAGE of a D-float metric vector per
     host (per-core CPU usage; ComputeCpuAvg.java:27-59 with the scalar generalised to a vector),
     1M keys, alert when any core's window average exceeds a threshold. The per-(key, pane)
@@ -279,7 +286,7 @@ def config6(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 1_000_000
         t_in = time.perf_counter()
         K.gen_events(k, ts, vals, seed=11, stream_id=0, idx0=i * batch, nkeys=keys,
                      ts_base=t0_event + i * step_ms, ts_span=step_ms, disorder=disorder,
-                     val_lo=0, val_span=1)
+                     val_lo=0, val_span=1, zipf=zipf)
         V.gen_vectors(vec, seed=11, stream_id=0, idx0=i * batch, lo=0.0, span=100.0)
         fired = op.process(k, ts, vec)
         n = sum(len(r.keys) for r in fired)
@@ -303,6 +310,7 @@ def config6(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 1_000_000
             "metric_values_per_sec": batch * steps * dim / dt,
             "p50_alert_latency_ms": statistics.median(lat) if lat else None, "alerts": alerts,
             "keys": keys, "dim": dim, "events_per_step": batch, "mode": "mfma" if mfma else "valu",
+            "key_distribution": f"zipf({zipf:g})" if zipf > 0 else "uniform",
             "state_bytes": op.state_bytes(), "device": str(dev)}
 
 
@@ -372,6 +380,9 @@ def main(argv=None) -> int:
     ap.add_argument("--config", type=int, required=True, choices=[1, 2, 4, 5, 6, 7])
     ap.add_argument("--dim", type=int, default=32, help="config 6: metric vector width")
     ap.add_argument("--valu", action="store_true", help="config 6: VALU instead of MFMA reduce")
+    ap.add_argument("--zipf", type=float, default=0.0, help="config 6: power-law key skew")
+    ap.add_argument("--revisit", type=float, default=0.0,
+                    help="config 5: fraction of events for spilled (long idle) keys")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None)
@@ -394,9 +405,9 @@ def main(argv=None) -> int:
         r = config7(device=a.device)
     elif a.config == 6:
         r = config6(a.steps, a.warmup, a.batch or (1 << 24), dim=a.dim, device=a.device,
-                    mfma=not a.valu)
+                    mfma=not a.valu, zipf=a.zipf)
     else:
-        r = config5(a.steps, a.warmup, a.batch or (1 << 24), device=a.device)
+        r = config5(a.steps, a.warmup, a.batch or (1 << 24), device=a.device, revisit=a.revisit)
     print(json.dumps(r), flush=True)
     return 0
 

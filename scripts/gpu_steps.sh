@@ -39,6 +39,8 @@ for step in "$@"; do
     prof_nofin) MXS_FUSED_FIN=0 prof nofin python3 bench.py --steps 24 --warmup 6 || exit $? ;;
     bench_zipf_*) z=${step#bench_zipf_}; MXS_STEP_TIMES=1 timeout -k 10 300 python bench.py --steps 48 --warmup 8 --zipf "$z" > "$out/bench_zipf_$z.log" 2>&1 || exit $? ;;
     prof_zipf_*) z=${step#prof_zipf_}; prof "zipf_$z" python3 bench.py --steps 24 --warmup 6 --zipf "$z" || exit $? ;;
+    cfg6z_*) z=${step#cfg6z_}; z=${z%_*}; m=${step##*_}; extra=""; [ "$m" = valu ] && extra=--valu; timeout -k 10 300 python -m mxstream.models.bench_configs --config 6 --steps 20 --warmup 5 --zipf "$z" $extra > "$out/$step.json" 2>&1 || exit $? ;;
+    cfg5r) timeout -k 10 300 python -m mxstream.models.bench_configs --config 5 --steps 20 --warmup 14 --revisit 0.01 > "$out/cfg5r.json" 2>&1 || exit $? ;;
     bench20) timeout -k 10 300 python bench.py --steps 20 --warmup 5 > "$out/bench20.log" 2>&1 || exit $? ;;
     cfg1) timeout -k 10 300 python -m mxstream.models.bench_configs --config 1 --steps 20 --warmup 3 > "$out/cfg1.json" 2>&1 || exit $? ;;
     cfg1t*) t=${step#cfg1t}; timeout -k 10 300 python -m mxstream.models.bench_configs --config 1 --threads $t --steps 20 --warmup 3 > "$out/cfg1_t$t.json" 2>&1 || exit $? ;;
