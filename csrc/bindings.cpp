@@ -552,6 +552,16 @@ PYBIND11_MODULE(_mxs_native, m) {
   m.def("cpu_f64_order_bits", [](intptr_t v, int64_t n, intptr_t o) {
     cpu::f64_order_bits(P<uint64_t>(v), n, P<uint64_t>(o));
   });
+  m.def("gpu_segment_median_select", [](intptr_t heads, int64_t nseg, int64_t total, intptr_t ord,
+                                        intptr_t out, intptr_t stream) {
+    gpu::segment_median_select(P<int64_t>(heads), nseg, total, P<uint64_t>(ord), P<double>(out),
+                               stream);
+  });
+  m.def("cpu_segment_median_select", [](intptr_t heads, int64_t nseg, int64_t total, intptr_t ord,
+                                        intptr_t out) {
+    py::gil_scoped_release nogil;
+    cpu::segment_median_select(P<int64_t>(heads), nseg, total, P<uint64_t>(ord), P<double>(out));
+  });
   m.def("gpu_segment_median", [](intptr_t heads, int64_t nseg, int64_t total, intptr_t ord,
                                  intptr_t out, intptr_t stream) {
     gpu::segment_median(P<int64_t>(heads), nseg, total, P<uint64_t>(ord), P<double>(out), stream);

@@ -489,6 +489,27 @@ void f64_order_bits(const uint64_t* v, int64_t n, uint64_t* o) {
   for (int64_t i = 0; i < n; ++i) o[i] = mxs::f64_order_bits(v[i]);
 }
 
+void segment_median_select(const int64_t* heads, int64_t nseg, int64_t total,
+                           const uint64_t* ord, double* out) {
+  std::vector<uint64_t> v;
+  for (int64_t sg = 0; sg < nseg; ++sg) {
+    const int64_t a = heads[sg], e = sg + 1 < nseg ? heads[sg + 1] : total, n = e - a;
+    if (n <= 0) {
+      out[sg] = 0.0;
+      continue;
+    }
+    v.assign(ord + a, ord + e);
+    std::nth_element(v.begin(), v.begin() + n / 2, v.end());
+    const double hi = as_f64(f64_from_order_bits(v[n / 2]));
+    if (n & 1) {
+      out[sg] = hi;
+    } else {
+      const uint64_t lo = *std::max_element(v.begin(), v.begin() + n / 2);
+      out[sg] = (hi + as_f64(f64_from_order_bits(lo))) / 2.0;
+    }
+  }
+}
+
 void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uint64_t* ord,
                     double* out) {
   for (int64_t s = 0; s < nseg; ++s) {

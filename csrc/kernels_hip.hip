@@ -2827,6 +2827,115 @@ __global__ __launch_bounds__(256) void segment_median_kernel(const int64_t* __re
   }
 }
 
+// Median of every segment of *unsorted* order-preserving f64 bits (segments = runs of equal key
+// after a radix sort by key only; the values ride along unsorted). One wave per segment: a
+// segment of up to kMedLds values is bitonic-sorted in the wave's LDS slice; a longer one is
+// resolved by two radix selects (8 byte passes each over the segment, 256-bin LDS histograms).
+// Replaces the second, 64-bit radix sort over every value of the window (8 of the 11 passes).
+constexpr int kMedLds = 2048;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+__device__ uint64_t wave_radix_select(const uint64_t* __restrict__ v, int64_t n, int64_t k,
+                                      uint32_t* hist, int lane) {
+  uint64_t prefix = 0, mask = 0;
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int i = lane; i < 256; i += 64) hist[i] = 0;
+    wave_lds_sync();
+    for (int64_t i = lane; i < n; i += 64) {
+      const uint64_t x = v[i];
+      if ((x & mask) == prefix) atomicAdd(&hist[(x >> shift) & 255u], 1u);
+    }
+    wave_lds_sync();
+    // Lane l owns bins 4l..4l+3: find the bin holding the k-th candidate.
+    uint32_t c[4], tot = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      c[j] = hist[lane * 4 + j];
+      tot += c[j];
+    }
+    uint32_t incl = tot;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    const uint32_t excl = incl - tot;
+    int found = -1;
+    int64_t kk = k - excl;
+    if (k >= excl && k < incl) {
+      for (int j = 0; j < 4; ++j) {
+        if (kk < c[j]) {
+          found = lane * 4 + j;
+          break;
+        }
+        kk -= c[j];
+      }
+    }
+    const unsigned long long who = __ballot(found >= 0);
+    const int src = who ? __ffsll((long long)who) - 1 : 0;
+    const int bin = __shfl(found, src);
+    k = __shfl(kk, src);
+    prefix |= (uint64_t)bin << shift;
+    mask |= (uint64_t)255 << shift;
+    wave_lds_sync();
+  }
+  return prefix;
+}
+
+__global__ __launch_bounds__(256) void segment_median_select_kernel(
+    const int64_t* __restrict__ heads, int64_t nseg, int64_t total, const uint64_t* __restrict__ ord,
+    double* __restrict__ out) {
+  __shared__ uint64_t buf[4][kMedLds];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint64_t* b = buf[w];
+  for (int64_t s = (int64_t)blockIdx.x * 4 + w; s < nseg; s += (int64_t)gridDim.x * 4) {
+    const int64_t a = heads[s], e = s + 1 < nseg ? heads[s + 1] : total;
+    const int64_t n = e - a;
+    uint64_t hi_bits = 0, lo_bits = 0;
+    if (n <= 0) {
+      if (lane == 0) out[s] = 0.0;
+      continue;
+    }
+    if (n <= kMedLds) {
+      int P = 64;
+      while (P < n) P <<= 1;
+      for (int i = lane; i < P; i += 64) b[i] = i < n ? ord[a + i] : ~0ull;
+      wave_lds_sync();
+      for (int k = 2; k <= P; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = lane; i < P; i += 64) {
+            const int ixj = i ^ j;
+            if (ixj > i) {
+              const uint64_t x = b[i], y = b[ixj];
+              const bool up = (i & k) == 0;
+              if ((x > y) == up) {
+                b[i] = y;
+                b[ixj] = x;
+              }
+            }
+          }
+          wave_lds_sync();
+        }
+      }
+      hi_bits = b[n / 2];
+      lo_bits = b[(n - 1) / 2];
+      wave_lds_sync();
+    } else {
+      uint32_t* hist = reinterpret_cast<uint32_t*>(b);
+      hi_bits = wave_radix_select(ord + a, n, n / 2, hist, lane);
+      lo_bits = (n & 1) ? hi_bits : wave_radix_select(ord + a, n, n / 2 - 1, hist, lane);
+    }
+    if (lane == 0) {
+      const double hi = as_f64(f64_from_order_bits(hi_bits));
+      out[s] = (n & 1) ? hi : (hi + as_f64(f64_from_order_bits(lo_bits))) / 2.0;
+    }
+  }
+}
+
 int grid_for(int64_t n, int block, int max_blocks) {
   int64_t g = (n + block - 1) / block;
   if (g < 1) g = 1;
@@ -3500,6 +3609,14 @@ void f64_order_bits(const uint64_t* v, int64_t n, uint64_t* o, intptr_t stream) 
   if (n <= 0) return;
   hipLaunchKernelGGL(f64_order_bits_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, v, n, o);
+  HIP_CHECK(hipGetLastError());
+}
+
+void segment_median_select(const int64_t* heads, int64_t nseg, int64_t total, const uint64_t* ord,
+                           double* out, intptr_t stream) {
+  if (nseg <= 0) return;
+  hipLaunchKernelGGL(segment_median_select_kernel, dim3(grid_for(nseg, 4, 16384)), dim3(256), 0,
+                     (hipStream_t)stream, heads, nseg, total, ord, out);
   HIP_CHECK(hipGetLastError());
 }
 

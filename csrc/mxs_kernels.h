@@ -189,6 +189,9 @@ void parse_text(const char* text, int64_t text_len, const int64_t* starts, int64
 void f64_order_bits(const uint64_t* v, int64_t n, uint64_t* o, intptr_t stream);
 void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uint64_t* ord,
                     double* out, intptr_t stream);
+// The same medians over segments whose values are NOT sorted (selection per segment).
+void segment_median_select(const int64_t* heads, int64_t nseg, int64_t total,
+                           const uint64_t* ord, double* out, intptr_t stream);
 void set_erase(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, intptr_t stream);
 void session_rehash(int64_t nslots, int cap_log2, const uint64_t* keys_o, const int64_t* sess_o,
                     const int64_t* due_o, const int64_t* last_o, uint64_t* keys_n, int64_t* sess_n,
@@ -253,6 +256,8 @@ void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const
 void f64_order_bits(const uint64_t* v, int64_t n, uint64_t* o);
 void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uint64_t* ord,
                     double* out);
+void segment_median_select(const int64_t* heads, int64_t nseg, int64_t total,
+                           const uint64_t* ord, double* out);
 void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt,
                       const uint32_t* n_in, const ScatPlan& plan, const int32_t* jhash,
                       const int32_t* kg_dest, uint32_t* cursor, Rec* out, uint32_t* flags);

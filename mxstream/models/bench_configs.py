@@ -314,6 +314,57 @@ def config6(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 1_000_000
             "state_bytes": op.state_bytes(), "device": str(dev)}
 
 
+def config8(steps: int, warmup: int, batch: int = 1 << 22, keys: int = 100_000,
+            device: str = "cuda") -> dict:
+    """Process-window median at scale (ComputeCpuMiddle.java:34-48 shape): per host, the median
+    CPU usage of every 1-min tumbling event-time window over `keys` hosts; every element is kept
+    (ListState analogue, runtime/list_window_operator.py) and each firing sorts the window's
+    values by host (one radix sort over the host-id bits) and selects each host's median
+    (segment_median_select: LDS bitonic sort / radix select per segment)."""
+    from ..runtime.list_window_operator import KeyedListWindowOperator
+
+    dev = torch.device(device)
+    step_ms, disorder = 5_000, 1_000
+    op = KeyedListWindowOperator(size=60_000, device=dev)
+    kt = torch.empty(batch, dtype=torch.int64, device=dev)
+    tt = torch.empty_like(kt)
+    vt = torch.empty_like(kt)
+    t0_event = 1_566_957_600_000
+    state = {"i": 0}
+    lat: list[float] = []
+
+    def step():
+        i = state["i"]
+        t_in = time.perf_counter()
+        K.gen_events(kt, tt, vt, seed=8, stream_id=0, idx0=i * batch, nkeys=keys,
+                     ts_base=t0_event + i * step_ms, ts_span=step_ms, disorder=disorder,
+                     val_lo=0, val_span=10_000, val_f64=True)
+        fired = op.process(kt, tt, vt)
+        wm = t0_event + (i + 1) * step_ms - disorder - 1
+        fired += op.advance_watermark(wm)
+        n = sum(len(r[2]) for r in fired)
+        if fired:
+            lat.append((time.perf_counter() - t_in) * 1e3)
+        state["i"] = i + 1
+        return n
+
+    for _ in range(warmup):
+        step()
+    _sync(dev)
+    lat.clear()
+    t0 = time.perf_counter()
+    rows = 0
+    for _ in range(steps):
+        rows += step()
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    return {"config": 8, "metric": "events/sec (process-window median per key, ListState)",
+            "value": batch * steps / dt, "unit": "events/s", "ms_per_step": dt / steps * 1e3,
+            "p50_fire_step_ms": statistics.median(lat) if lat else None, "medians": rows,
+            "keys": keys, "events_per_step": batch, "window_values": batch * 12,
+            "device": str(dev)}
+
+
 def config7(lines: int = 4_000_000, channels: int = 1_000, device: str = "cuda",
             batch_lines: int = 1 << 18, threads: int = 16) -> dict:
     """Host ingest through the DataStream API: the reference's BandwidthMonitorWithEventTime job
@@ -377,7 +428,7 @@ def config7(lines: int = 4_000_000, channels: int = 1_000, device: str = "cuda",
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 4, 5, 6, 7])
+    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 4, 5, 6, 7, 8])
     ap.add_argument("--dim", type=int, default=32, help="config 6: metric vector width")
     ap.add_argument("--valu", action="store_true", help="config 6: VALU instead of MFMA reduce")
     ap.add_argument("--zipf", type=float, default=0.0, help="config 6: power-law key skew")
@@ -403,6 +454,8 @@ def main(argv=None) -> int:
                     dense_keys=not a.hashed_keys)
     elif a.config == 7:
         r = config7(device=a.device)
+    elif a.config == 8:
+        r = config8(a.steps, a.warmup, a.batch or (1 << 22), device=a.device)
     elif a.config == 6:
         r = config6(a.steps, a.warmup, a.batch or (1 << 24), dim=a.dim, device=a.device,
                     mfma=not a.valu, zipf=a.zipf)

@@ -461,8 +461,11 @@ def f64_order_bits(v: torch.Tensor) -> torch.Tensor:
     return o
 
 
-def segment_median(heads: torch.Tensor, ord_bits: torch.Tensor) -> torch.Tensor:
-    """Median (Java ComputeCpuMiddle semantics) of every sorted segment starting at `heads`."""
+def segment_median(heads: torch.Tensor, ord_bits: torch.Tensor, *, sorted_values: bool = True
+                   ) -> torch.Tensor:
+    """Median (Java ComputeCpuMiddle semantics) of every segment starting at `heads`.
+    sorted_values=False: the values inside a segment are in any order (per-segment selection:
+    LDS bitonic sort or radix select, csrc segment_median_select)."""
     dev = ord_bits.device
     _check(heads, torch.int64, heads.numel(), "heads", dev)
     _check(ord_bits, torch.int64, ord_bits.numel(), "ord", dev)
@@ -471,8 +474,9 @@ def segment_median(heads: torch.Tensor, ord_bits: torch.Tensor) -> torch.Tensor:
     out = torch.empty(heads.numel(), dtype=torch.float64, device=dev)
     m = load()
     args = (heads.data_ptr(), heads.numel(), ord_bits.numel(), ord_bits.data_ptr(), out.data_ptr())
+    name = "segment_median" if sorted_values else "segment_median_select"
     if _is_gpu(ord_bits):
-        m.gpu_segment_median(*args, _stream(ord_bits))
+        getattr(m, "gpu_" + name)(*args, _stream(ord_bits))
     else:
-        m.cpu_segment_median(*args)
+        getattr(m, "cpu_" + name)(*args)
     return out

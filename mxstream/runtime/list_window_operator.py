@@ -53,8 +53,10 @@ class KeyedListWindowOperator:
         return ls if ls >= t else ls + self.slide
 
     def process(self, keys: torch.Tensor, ts: torch.Tensor, vals_f64: torch.Tensor) -> list:
-        """keys int64, ts int64, vals: f64 bit patterns (int64). Returns fired rows."""
+        """keys int64 (or int32 dictionary ids), ts int64, vals: f64 bit patterns (int64).
+        Returns fired rows."""
         out = []
+        keys = keys.to(torch.int64)
         if keys.numel():
             late_ts = self._late_ts()
             keep = ts >= late_ts
@@ -125,13 +127,21 @@ class KeyedListWindowOperator:
             keys, vals = keys[sel], vals[sel]
             if not keys.numel():
                 return []
-        uniq, ids = torch.unique(keys, return_inverse=True)
-        kbits = max(1, int(uniq.numel() - 1).bit_length())
         ordv = K.f64_order_bits(vals.contiguous())
-        # Two stable radix passes: by value, then by key id -> (key, value) order.
-        ordv, ids = K.sort_pairs(ordv, ids.contiguous(), bits=64)
+        # One radix sort by key over the used key bits (dictionary ids / small ints sort as they
+        # are; anything else through dense ids), the values ride along unsorted; the median of
+        # each key segment is then selected per segment (LDS bitonic sort / radix select) -- no
+        # 64-bit sort of every value of the window.
+        kmin, kmax = (int(x) for x in torch.aminmax(keys))
+        if kmin >= 0 and kmax < (1 << 40):
+            uniq, ids = None, keys.contiguous()
+            kbits = max(1, kmax.bit_length())
+        else:
+            uniq, ids = torch.unique(keys, return_inverse=True)
+            kbits = max(1, int(uniq.numel() - 1).bit_length())
         ids, ordv = K.sort_pairs(ids.contiguous(), ordv, bits=kbits)
         heads = torch.nonzero(torch.cat([torch.ones(1, dtype=torch.bool, device=ids.device),
                                          ids[1:] != ids[:-1]])).flatten()
-        med = K.segment_median(heads.contiguous(), ordv)
-        return [(s, s + self.size, uniq[ids[heads]].cpu().numpy(), med.cpu().numpy())]
+        med = K.segment_median(heads.contiguous(), ordv, sorted_values=False)
+        out_keys = ids[heads] if uniq is None else uniq[ids[heads]]
+        return [(s, s + self.size, out_keys.cpu().numpy(), med.cpu().numpy())]

@@ -47,6 +47,7 @@ for step in "$@"; do
     cfg1gpu) timeout -k 10 300 python -m mxstream.models.bench_configs --config 1 --gpu-parse --steps 20 --warmup 3 > "$out/cfg1_gpu.json" 2>&1 || exit $? ;;
     cfg4_hashed) timeout -k 10 300 python -m mxstream.models.bench_configs --config 4 --hashed-keys --steps 20 --warmup 5 > "$out/cfg4_hashed.json" 2>&1 || exit $? ;;
     cfg7) timeout -k 10 600 python -m mxstream.models.bench_configs --config 7 > "$out/cfg7.json" 2>&1 || exit $? ;;
+    cfg8) timeout -k 10 300 python -m mxstream.models.bench_configs --config 8 --steps 24 --warmup 13 > "$out/cfg8.json" 2>&1 || exit $? ;;
     cfg2|cfg4|cfg5|cfg6) timeout -k 10 300 python -m mxstream.models.bench_configs --config ${step#cfg} --steps 20 --warmup 5 > "$out/$step.json" 2>&1 || exit $? ;;
     loop8) timeout -k 10 300 python scripts/loopback_bench.py --world 8 --steps 24 --warmup 4 --out "$out/loop8.json" > "$out/loop8.log" 2>&1 || exit $? ;;
     prof_bench) prof bench python3 bench.py --steps 24 --warmup 6 || exit $? ;;

@@ -428,3 +428,18 @@ def test_spill_tier_gpu_matches_unbounded_cpu(gpu_device):
                            spill_check_steps=1, spill_load=0.5, cap_log2=7, spill_keep_panes=1)
     assert op.metrics.extra.get("spilled_keys", 0) > 0
     assert got == ref
+
+
+def test_segment_median_select_gpu_matches_cpu(gpu_device):
+    """Median of unsorted segments: LDS bitonic path (<= 2048 values) and radix-select path
+    (longer segments, odd and even lengths) equal numpy's median and the C++ twin."""
+    rng = np.random.default_rng(1)
+    lens = [1, 2, 3, 63, 64, 65, 1000, 2047, 2048, 2049, 5000, 10_001, 7]
+    vals = rng.standard_normal(sum(lens)) * 1e3
+    vals[:20] = 5.0  # ties
+    heads = torch.tensor(np.r_[0, np.cumsum(lens)[:-1]], dtype=torch.int64)
+    ordb = K.f64_order_bits(torch.from_numpy(vals).view(torch.int64))
+    g = K.segment_median(heads.to(gpu_device), ordb.to(gpu_device), sorted_values=False).cpu()
+    c = K.segment_median(heads, ordb, sorted_values=False)
+    ref = [np.median(vals[a:a + n]) for a, n in zip(heads.tolist(), lens)]
+    assert torch.equal(g, c) and np.allclose(c.numpy(), ref, rtol=0, atol=0)
