@@ -56,6 +56,29 @@ struct ColdChunk {
   std::vector<uint32_t> cnt;  // 0 = row gone (promoted or discarded)
   int64_t max_due = INT64_MIN;
   size_t live = 0;
+  // Rows by key: promote() looks keys up by binary search or a merge join instead of probing a
+  // hash set with every cold row of the store.
+  std::vector<uint32_t> by_key;
+  uint64_t kmin = ~0ull, kmax = 0;
+
+  // Key range at sealing (O(n)); the sorted row index is built on the first promote() that
+  // reaches this chunk, so chunks that are never revisited never pay for it.
+  void seal() {
+    for (uint64_t k : key) {
+      kmin = k < kmin ? k : kmin;
+      kmax = k > kmax ? k : kmax;
+    }
+  }
+  void ensure_index() {
+    if (by_key.size() == key.size()) return;
+    // (key, row) pairs sorted contiguously: an index sort with key[] lookups in the comparator
+    // was 5x slower (random reads).
+    std::vector<std::pair<uint64_t, uint32_t>> kr(key.size());
+    for (size_t i = 0; i < kr.size(); ++i) kr[i] = {key[i], (uint32_t)i};
+    std::sort(kr.begin(), kr.end());
+    by_key.resize(kr.size());
+    for (size_t i = 0; i < kr.size(); ++i) by_key[i] = kr[i].second;
+  }
 };
 
 template <class T>
@@ -164,6 +187,7 @@ class SessionStore {
     }
     if (!ch.key.empty()) {
       ch.live = ch.key.size();
+      ch.seal();
       cold_rows_ += ch.live;
       cold_.push_back(std::move(ch));
     }
@@ -346,21 +370,41 @@ class SessionStore {
   // Move cold rows of `keys` into the hot map (rows past cleanup at `wm` are discarded).
   void promote(const int64_t* keys, int64_t n, int64_t wm) {
     if (cold_rows_ == 0 || n == 0) return;
-    std::unordered_set<uint64_t> want;
-    want.reserve((size_t)n * 2);
-    for (int64_t i = 0; i < n; ++i) want.insert((uint64_t)keys[i]);
+    std::vector<uint64_t> want((const uint64_t*)keys, (const uint64_t*)keys + n);
+    std::sort(want.begin(), want.end());
+    want.erase(std::unique(want.begin(), want.end()), want.end());
+    auto take = [&](ColdChunk& ch, uint32_t r) {
+      if (!ch.cnt[r]) return;
+      if (cleanup_time(ch.end[r] - 1) > wm) {
+        m_[ch.key[r]].push_back(Session{ch.start[r], ch.end[r], ch.acc[r], ch.cnt[r], 1u});
+        schedule(ch.key[r]);
+      } else {
+        pending_released_.push_back(ch.key[r]);  // reported by fire() unless it turns hot
+      }
+      ch.cnt[r] = 0;
+      ch.live -= 1;
+      cold_rows_ -= 1;
+    };
     for (auto& ch : cold_) {
-      for (size_t r = 0; r < ch.key.size(); ++r) {
-        if (!ch.cnt[r] || !want.count(ch.key[r])) continue;
-        if (cleanup_time(ch.end[r] - 1) > wm) {
-          m_[ch.key[r]].push_back(Session{ch.start[r], ch.end[r], ch.acc[r], ch.cnt[r], 1u});
-          schedule(ch.key[r]);
+      if (!ch.live || want.back() < ch.kmin || want.front() > ch.kmax) continue;
+      auto lo = std::lower_bound(want.begin(), want.end(), ch.kmin);
+      auto hi = std::upper_bound(lo, want.end(), ch.kmax);
+      if (lo == hi) continue;
+      ch.ensure_index();
+      const size_t nw = (size_t)(hi - lo), nc = ch.by_key.size();
+      auto ckey = [&](uint32_t r) { return ch.key[r]; };
+      if (nw * 20 < nc) {  // few wanted keys: binary search each in the chunk's key order
+        for (auto it = lo; it != hi; ++it) {
+          auto p = std::lower_bound(ch.by_key.begin(), ch.by_key.end(), *it,
+                                    [&](uint32_t r, uint64_t k) { return ckey(r) < k; });
+          for (; p != ch.by_key.end() && ckey(*p) == *it; ++p) take(ch, *p);
         }
-        else
-          pending_released_.push_back(ch.key[r]);  // reported by fire() unless it turns hot
-        ch.cnt[r] = 0;
-        ch.live -= 1;
-        cold_rows_ -= 1;
+      } else {  // merge join of two sorted sequences
+        size_t i = 0;
+        for (auto it = lo; it != hi && i < nc; ++it) {
+          while (i < nc && ckey(ch.by_key[i]) < *it) ++i;
+          for (; i < nc && ckey(ch.by_key[i]) == *it; ++i) take(ch, ch.by_key[i]);
+        }
       }
     }
   }
