@@ -500,6 +500,15 @@ PYBIND11_MODULE(_mxs_native, m) {
                         P<uint8_t>(dirty_g), nsub, cap_log2, ring, p_lo, np, cutoff,
                         compact_out(o, cap), P<uint32_t>(occ));
   });
+  m.def("gpu_direct_agg_probe", [](intptr_t keys, intptr_t ts, intptr_t vals, int64_t n,
+                                   int64_t tbase, int64_t pane, int ring, int64_t nslots,
+                                   uint32_t mul, int bits, int64_t pane_base, intptr_t acc,
+                                   intptr_t cnt, int mode, intptr_t sink, int grid,
+                                   intptr_t stream) {
+    gpu::direct_agg_probe(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), n, tbase, pane,
+                          ring, nslots, mul, bits, pane_base, P<uint64_t>(acc), P<uint32_t>(cnt),
+                          mode, P<uint64_t>(sink), grid, stream);
+  });
   m.def("gpu_dirty_clear", [](intptr_t list, intptr_t list_n, uint32_t cap, int ring,
                               int64_t nslots, intptr_t dirty_g, intptr_t mark, int64_t p_lo, int np,
                               intptr_t stream) {

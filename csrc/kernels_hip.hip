@@ -1342,6 +1342,38 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// Experiment (profiles/r2_direct_atomics.md): pane accumulation by global atomics straight from
+// the source columns (dense ids, one rank), no partition. mode 0: sum + count atomics; 1: sum
+// atomic only; 2: no atomics (loads + pane/slot math only, a checksum keeps it alive).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void direct_agg_probe_kernel(
+    const uint64_t* __restrict__ keys, const int64_t* __restrict__ ts,
+    const uint64_t* __restrict__ vals, int64_t n, int64_t tbase, int64_t pane, int ring,
+    int64_t nslots, uint32_t mul, int bits, int64_t pane_base, uint64_t* __restrict__ acc_g,
+    uint32_t* __restrict__ cnt_g, int mode, uint64_t* __restrict__ sink) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  uint64_t chk = 0;
+  const double inv = 1.0 / (double)pane;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t k = __builtin_nontemporal_load(&keys[i]);
+    const int64_t t = __builtin_nontemporal_load(&ts[i]);
+    const uint64_t v = __builtin_nontemporal_load(&vals[i]);
+    const int64_t q = (int64_t)((double)(t - tbase) * inv);
+    const int64_t p = pane_base + q;
+    const size_t gi = (size_t)(p & (ring - 1)) * nslots + dense_slot(k, mul, bits);
+    if (mode == 0) {
+      atomicAdd((unsigned long long*)&acc_g[gi], (unsigned long long)v);
+      atomicAdd(&cnt_g[gi], 1u);
+    } else if (mode == 1) {
+      atomicAdd((unsigned long long*)&acc_g[gi], (unsigned long long)v);
+    } else {
+      chk += gi ^ v;
+    }
+  }
+  if (mode == 2 && chk == 0x1234567) sink[0] = chk;
+}
+
+// ------------------------------------------------------------------------------------------
 // Keyed-window table maintenance for the host-DRAM spill tier (hashed keys): one workgroup per
 // sub-table. A key with no data in the live panes is dropped (the tables never delete keys
 // otherwise); a key whose newest data pane is <= cutoff is evicted: its live (pane, acc, cnt,
@@ -3296,6 +3328,16 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
                      dim3(kFireThreads), lds,
                      (hipStream_t)stream, keys_g, acc_g, cnt_g, dirty_g, plan, out_keys, out_vals,
                      out_raw, out_cnt, out_n);
+  HIP_CHECK(hipGetLastError());
+}
+
+void direct_agg_probe(const uint64_t* keys, const int64_t* ts, const uint64_t* vals, int64_t n,
+                      int64_t tbase, int64_t pane, int ring, int64_t nslots, uint32_t mul,
+                      int bits, int64_t pane_base, uint64_t* acc_g, uint32_t* cnt_g, int mode,
+                      uint64_t* sink, int grid, intptr_t stream) {
+  hipLaunchKernelGGL(direct_agg_probe_kernel, dim3(grid > 0 ? grid : grid_for(n, 256 * 4, 16384)),
+                     dim3(256), 0, (hipStream_t)stream, keys, ts, vals, n, tbase, pane, ring,
+                     nslots, mul, bits, pane_base, acc_g, cnt_g, mode, sink);
   HIP_CHECK(hipGetLastError());
 }
 

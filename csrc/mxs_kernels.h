@@ -114,6 +114,11 @@ int d2h_async(void* dst, const void* src, size_t bytes, intptr_t stream);
 // Up to kD2HMax device buffers -> one pinned (mapped) host slab by a copy kernel on `stream`;
 // every size, source address and slab offset a multiple of 16 bytes. Returns hipError_t.
 int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream);
+// Experiment: pane accumulation by global atomics from the source columns (see kernels_hip).
+void direct_agg_probe(const uint64_t* keys, const int64_t* ts, const uint64_t* vals, int64_t n,
+                      int64_t tbase, int64_t pane, int ring, int64_t nslots, uint32_t mul,
+                      int bits, int64_t pane_base, uint64_t* acc_g, uint32_t* cnt_g, int mode,
+                      uint64_t* sink, int grid, intptr_t stream);
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
