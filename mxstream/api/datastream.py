@@ -254,6 +254,11 @@ class KeyedStream(DataStream):
     def get_key_selector(self):
         return self.key_fn
 
+    def _one_input(self, name: str, factory, parallelism: int | None = None):
+        op = super()._one_input(name, factory, parallelism)
+        op.t.key_fn_in = self.key_fn  # hash-partitioned edge (multi-rank record exchange)
+        return op
+
     # -- rolling aggregations (StreamGroupedReduce: emit per element) --
     def reduce(self, fn) -> SingleOutputStreamOperator:
         key_fn = self.key_fn

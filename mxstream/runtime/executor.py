@@ -7,8 +7,15 @@ items (records and watermarks in stream order), and processing-time timers up to
 ``now`` fire. After the last tick, event-time jobs see ``Long.MAX_VALUE`` (end of input fires all
 event-time windows); processing-time windows are not fired at end of input (Flink 1.8).
 
-Multi-rank: every rank runs the same graph on its source partition; keyed native operators
-shuffle through RCCL/gloo (mxstream.parallel.comm).
+Multi-rank (``torchrun`` with WORLD_SIZE > 1, one process per GPU): every rank runs the same
+graph on its source partition. Every tick is step-synchronous across ranks: a keyed edge
+(an operator built on a KeyedStream) exchanges its records so that each key group's records
+reach the rank that owns it. Subtask s of P lives on rank s * world // P, like the engine
+operators' key-group map. Watermarks crossing a keyed edge are merged to the minimum over the
+ranks, like Flink's minimum over input channels. A parallelism-1 operator (windowAll) gathers
+its input on rank 0. The job ends when every rank's sources are finished. The record exchange
+runs over the gloo process group with pickled records; it is the host-level data path. The
+engines' GPU-scale exchange is the RCCL all-to-all inside the keyed operators (bench path).
 """
 from __future__ import annotations
 
@@ -54,6 +61,7 @@ class Transformation:
     side_tag: Any = None
     uid: str | None = None
     meta: dict = field(default_factory=dict)   # planner hints (op kind, user fn, window spec)
+    key_fn_in: Any = None              # set when the input is a KeyedStream (hash-partitioned edge)
 
     def __hash__(self):
         return self.id
@@ -118,6 +126,18 @@ class Executor:
         self.metrics: dict[str, int] = {}
         self._rr: dict = {}
         self._trace = False
+        self.comm = None
+        self._wm_in: dict = {}  # keyed node -> latest watermark received from every rank
+        if getattr(env, "world", 1) > 1:
+            import os
+
+            import torch
+
+            from ..parallel.comm import init_distributed
+
+            if str(env.config.device).startswith("cuda") and torch.cuda.is_available():
+                torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))  # one GPU per rank
+            self.comm = init_distributed("cpu")
 
     @staticmethod
     def _topo(sinks):
@@ -175,6 +195,8 @@ class Executor:
                 for p in n.parents:
                     items.extend(inbox.pop((n.id, p.id), []))
                 op = self.ops[n.id]
+                if self.comm is not None:
+                    items = self._exchange(n, items)
                 if not getattr(op, "accepts_columns", False):
                     items = expand_columns(items)
                 if self.fault is not None and items:
@@ -198,6 +220,57 @@ class Executor:
                     inbox.setdefault((c.id, n.id), []).extend(side)
                 else:
                     inbox.setdefault((c.id, n.id), []).extend(out)
+
+    # ---- multi-rank exchange ---------------------------------------------------------------
+    def _exchange(self, n: Transformation, items: list) -> list:
+        """Route this rank's input items of node n to their owner ranks (keyed edge: the key's
+        subtask; parallelism 1: rank 0; anything else stays). Collective: every rank calls it for
+        every node in the same order, with or without items."""
+        from ..utils.hashing import flink_murmur, java_hash
+        from .columnar import expand_columns
+
+        world, rank = self.comm.world, self.comm.rank
+        p = n.parallelism or self.env.parallelism
+        keyed = n.key_fn_in is not None
+        if not keyed and p != 1:
+            return items
+        mp = self.env.max_parallelism
+        outs: list[list] = [[] for _ in range(world)]
+        last_wm = None
+        for it in expand_columns(items):
+            if isinstance(it, WM):
+                last_wm = it.ts
+                continue
+            if not isinstance(it, Rec):
+                outs[rank].append(it)
+                continue
+            if keyed:
+                sub = (flink_murmur(java_hash(n.key_fn_in(it.value))) % mp) * p // mp
+                outs[sub * world // p].append(it)
+            else:
+                outs[0].append(it)
+        got = self.comm.all_gather_object((outs, last_wm))
+        recv: list = []
+        for r_outs, _ in got:
+            recv.extend(r_outs[rank])
+        # Watermarks: the minimum over the ranks of the latest watermark each one has sent.
+        seen = self._wm_in.setdefault(n.id, [None] * world)
+        for r, (_, w) in enumerate(got):
+            if w is not None:
+                seen[r] = w if seen[r] is None else max(seen[r], w)
+        if all(w is not None for w in seen):
+            wm = min(seen)
+            prev = self._wm_in.get((n.id, "emitted"))
+            if prev is None or wm > prev:
+                self._wm_in[(n.id, "emitted")] = wm
+                recv.append(WM(wm))
+        return recv
+
+    def _all_done(self, finished: dict) -> bool:
+        done = all(finished.values())
+        if self.comm is None:
+            return done
+        return all(self.comm.all_gather_object(done))
 
     # ---- checkpoints ---------------------------------------------------------------------
     def _storage(self):
@@ -325,7 +398,7 @@ class Executor:
         if getattr(cfg_x, "step_timeout_ms", 0) and cfg_x.step_timeout_ms > 0:
             wd = Watchdog(cfg_x.step_timeout_ms, name=self.job_name).start()
         try:
-            while not all(finished.values()):
+            while not self._all_done(finished):
                 if manual:
                     nxt = [self.ops[n.id].next_event_time() for n in sources if not finished[n.id]]
                     nxt = [t for t in nxt if t is not None]
@@ -421,6 +494,8 @@ class Executor:
                 for p in n.parents:
                     items.extend(inbox.pop((n.id, p.id), []))
                 op = self.ops[n.id]
+                if self.comm is not None:
+                    items = self._exchange(n, items)
                 if not getattr(op, "accepts_columns", False):
                     from .columnar import expand_columns
 
