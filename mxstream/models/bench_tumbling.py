@@ -111,16 +111,19 @@ class TumblingWindowBench:
         return self._account(self.op.flush(), t)
 
     def p50_latency_ms(self) -> float | None:
+        return self.latency_quantile_ms(0.5)
+
+    def latency_quantile_ms(self, q: float) -> float | None:
+        """Quantile over alerts (each alert of a firing carries that firing's latency)."""
         if not self.latencies_ms:
             return None
-        # Median over alerts (each alert of a firing carries that firing's latency).
         pts = sorted(self.latencies_ms)
         total = sum(c for _, c in pts)
         if total == 0:
-            return statistics.median(l for l, _ in pts)
+            return statistics.median(l for l, _ in pts) if q == 0.5 else pts[-1][0]
         acc = 0
         for lat, c in pts:
             acc += c
-            if acc * 2 >= total:
+            if acc >= q * total:
                 return lat
         return pts[-1][0]
