@@ -358,6 +358,21 @@ PYBIND11_MODULE(_mxs_native, m) {
                                P<uint64_t>(keys_g), P<int64_t>(sk), P<uint64_t>(vout),
                                P<uint32_t>(n_out), P<uint32_t>(flags), shift, stream);
   });
+  m.def("rolling_hist_scratch_bytes", &gpu::rolling_hist_scratch_bytes);
+  m.def("rolling_hist_supported", [](int agg, uint32_t count_n, int64_t nslots,
+                                     std::vector<int32_t> code, std::vector<double> consts) {
+    return gpu::rolling_hist_supported(agg, count_n, nslots, make_prog(code, consts));
+  });
+  m.def("gpu_rolling_hist", [](intptr_t keys, int64_t n, int nsub_log2, int cap_log2,
+                               intptr_t keys_g, intptr_t cnt_g, intptr_t scratch,
+                               size_t scratch_bytes, std::vector<int32_t> code,
+                               std::vector<double> consts, intptr_t ok, intptr_t ov, intptr_t ot,
+                               intptr_t on, uint32_t out_cap, intptr_t flags, intptr_t stream) {
+    gpu::rolling_hist(P<uint64_t>(keys), n, nsub_log2, cap_log2, P<uint64_t>(keys_g),
+                      P<uint32_t>(cnt_g), P<void>(scratch), scratch_bytes, make_prog(code, consts),
+                      P<uint64_t>(ok), P<uint64_t>(ov), P<int64_t>(ot), P<uint32_t>(on), out_cap,
+                      P<uint32_t>(flags), stream);
+  });
   m.def("gpu_rolling_heads", [](intptr_t sk, intptr_t n_in, int64_t n_cap, intptr_t heads,
                                 intptr_t n_heads, int shift, intptr_t stream) {
     gpu::rolling_heads(P<int64_t>(sk), P<uint32_t>(n_in), n_cap, P<uint32_t>(heads),

@@ -106,6 +106,8 @@ struct D2HBatch {
   int n;
 };
 
+constexpr int64_t kRollHistMaxSlots = 16384;  // LDS running-count table of the emit pass
+
 namespace gpu {
 int device_count();
 int set_spin_schedule();
@@ -152,6 +154,14 @@ void rolling_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
                     intptr_t stream);
 void rolling_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
                    uint32_t* n_heads, int shift, intptr_t stream);
+// Sort-free rolling COUNT for state tables of <= kRollHistMaxSlots slots (rolling_hist_hip.hip):
+// hist -> cross-chunk prefix -> tile-ranked emit; the same rows as lookup_direct + sort + scan.
+size_t rolling_hist_scratch_bytes(int64_t n, int64_t nslots);
+bool rolling_hist_supported(int agg, uint32_t count_n, int64_t nslots, const ExprProg& filt);
+void rolling_hist(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,
+                  uint32_t* cnt_g, void* scratch, size_t scratch_bytes, const ExprProg& filt,
+                  uint64_t* out_key, uint64_t* out_val, int64_t* out_tag, uint32_t* out_n,
+                  uint32_t out_cap, uint32_t* flags, intptr_t stream);
 void session_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bcap,
                     int cap_log2, uint64_t* keys_g, uint64_t* spill_set, uint32_t spill_mask,
                     int spill_any, int64_t* sk, uint64_t* vals, uint32_t* n_out, Rec* host_recs,

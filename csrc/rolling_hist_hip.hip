@@ -1,0 +1,411 @@
+// mxstream — sort-free keyed rolling COUNT for small key spaces (gfx950).
+//
+// BASELINE config 2 ("keyed ValueState counter", 10k keys) and any `keyBy(..)` counter whose
+// state table fits in LDS: every record emits its key's post-update count in arrival order
+// (StreamGroupedReduce / ValueState semantics, chapter2/src/main/java/me/zjy/ComputeCpuMax.java:26,
+// golden chapter2/README.md:62-66). The general path (kernels_hip.hip rolling_lookup_direct ->
+// radix sort -> rolling_heads -> rolling_scan) sorts the whole batch by slot; with <= 16K slots a
+// counting formulation needs no sort at all:
+//
+//   1. hist   (one 1024-thread workgroup per chunk of <= 64K records): find/insert every key in
+//             the HBM hash table, write its slot as u16, LDS histogram of the chunk's slots,
+//             histogram written out (part[chunk][slot]).
+//   2. group + prefix: per slot, an exclusive scan over the chunks seeded by the stored count
+//             (two launches: 16-chunk group totals, then the per-chunk prefixes); the final count
+//             is written back to the state table here.
+//   3. emit   (one 512-thread workgroup per chunk): the chunk's running counts start from its
+//             exclusive prefix in LDS; records are ranked a 512-record tile at a time. Within a
+//             tile, each distinct slot gets a tile-local id through an LDS hash table and every
+//             record ORs its lane bit into that id's per-wave 64-bit lane mask; a record's rank is
+//             then popcount(masks of earlier waves) + popcount(own wave's mask below its lane) --
+//             arrival order without a sort or a serial chain between waves. The last record of a
+//             slot in the tile advances the running count (applied after the next tile's first
+//             barrier; two table buffers alternate, so a tile costs two barriers). The traced
+//             filter epilogue and the wave-ballot row compaction are fused.
+//
+// Per record: 8 B key read + 2 B slot write (hist), 2 B slot read (emit) instead of the sort
+// path's 32 B in / 32 B out per pass. Output rows are unordered (the host restores arrival order
+// by tag, exactly as for the sort path); values are bit-identical to the C++ twin rolling_rows.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
+
+#include "mxs_kernels.h"
+
+namespace mxs {
+namespace {
+
+#define HIP_CHECK(x)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (x);                                                                    \
+    if (e_ != hipSuccess)                                                                   \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));                  \
+  } while (0)
+
+constexpr int kHistThreads = 1024;
+constexpr int kTileWaves = 8;
+constexpr int kTile = kTileWaves * 64;  // records per tile = threads of the emit workgroup
+constexpr int kHt = 1024;               // tile hash entries per buffer (<= 512 keys: load <= 0.5)
+constexpr uint32_t kHtEmpty = 0xFFFFFFFFu;
+constexpr uint16_t kNoSlot16 = 0xFFFF;
+constexpr uint32_t kChunkMin = kTile, kChunkMax = 65536;
+constexpr int kGroup = 16;  // chunks per group in the cross-chunk scan
+
+struct Geo {
+  uint32_t chunk, nb, ngroups;
+};
+
+Geo geometry(uint32_t n) {
+  // >= 256 chunks when the batch allows it (one workgroup per CU), tiles of whole 512 records.
+  uint64_t c = ((uint64_t)n + 255) / 256;
+  c = (c + kTile - 1) / kTile * kTile;
+  if (c < kChunkMin) c = kChunkMin;
+  if (c > kChunkMax) c = kChunkMax;
+  Geo g;
+  g.chunk = (uint32_t)c;
+  g.nb = n ? (uint32_t)(((uint64_t)n + c - 1) / c) : 0;
+  g.ngroups = (g.nb + kGroup - 1) / kGroup;
+  return g;
+}
+
+struct RollVars {  // filter variables of the rolling epilogue (rolling_scan's numbering)
+  double v0, v1, v4, v5;
+  __device__ __forceinline__ double get(int i) const {
+    switch (i) {
+      case 0: return v0;
+      case 1: return v1;
+      case 4: return v4;
+      case 5: return v5;
+      case 6: return v0;
+      default: return 0.0;
+    }
+  }
+};
+
+// Insert-or-find by linear probing, eight slots per round trip: the chain is contiguous, so one
+// batch of independent loads covers what would otherwise be up to eight dependent L2 reads (the
+// tail of the probe-length distribution, not its mean, sets a wave's latency).
+__device__ __forceinline__ uint32_t probe_insert(uint64_t* keys, uint64_t key, uint32_t mask) {
+  constexpr uint32_t W = 8;
+  uint32_t s = slot_hash(key) & mask;
+  for (uint32_t done = 0; done <= mask;) {
+    uint64_t k[W];
+#pragma unroll
+    for (uint32_t j = 0; j < W; ++j)
+      k[j] = __hip_atomic_load(&keys[(s + j) & mask], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t j = 0;
+    for (; j < W; ++j) {
+      if (k[j] == key) return (s + j) & mask;
+      if (k[j] == kEmptyKey) break;
+    }
+    if (j < W) {  // first empty slot of the chain: claim it (or meet a racing insert of key)
+      const uint32_t t = (s + j) & mask;
+      const uint64_t prev = atomicCAS((unsigned long long*)&keys[t], (unsigned long long)kEmptyKey,
+                                      (unsigned long long)key);
+      if (prev == kEmptyKey || prev == key) return t;
+      s = (t + 1) & mask;  // another key took it: continue after it
+      done += j + 1;
+    } else {
+      s = (s + W) & mask;
+      done += W;
+    }
+  }
+  return kNoSlot;
+}
+
+__global__ __launch_bounds__(kHistThreads) void rolling_hist_count_kernel(
+    const uint64_t* __restrict__ keys, uint32_t n, uint32_t chunk, int nsub_log2, int cap_log2,
+    uint64_t* __restrict__ keys_g, uint16_t* __restrict__ slot16, uint32_t* __restrict__ part,
+    uint32_t nslots, uint32_t* __restrict__ flags, uint32_t ablate) {
+  extern __shared__ uint32_t hcnt[];
+  for (uint32_t s = threadIdx.x; s < nslots; s += kHistThreads) hcnt[s] = 0;
+  __syncthreads();
+  const uint32_t lo = blockIdx.x * chunk;
+  const uint32_t hi = n - lo < chunk ? n : lo + chunk;
+  const uint32_t mask = (1u << cap_log2) - 1;
+  // Eight records per thread per round: the key loads and first-probe table reads are all in
+  // flight before any is consumed (most records hit their home slot).
+  constexpr int U = 8;
+  for (uint32_t base = lo; base < hi; base += kHistThreads * U) {
+    uint64_t key[U], k0[U];
+    uint32_t home[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = base + u * kHistThreads + threadIdx.x;
+      key[u] = i < hi ? keys[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = base + u * kHistThreads + threadIdx.x;
+      home[u] = (sub_table_of(key[u], nsub_log2) << cap_log2) | (slot_hash(key[u]) & mask);
+      k0[u] = i < hi ? __hip_atomic_load(&keys_g[home[u]], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT)
+                     : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t i = base + u * kHistThreads + threadIdx.x;
+      if (i >= hi) continue;
+      uint32_t slot;
+      if (key[u] >= kTombKey) {  // reserved ids (table markers): flagged, never stored
+        atomicOr(&flags[0], 4u);
+        slot = kNoSlot;
+      } else if (k0[u] == key[u] || (ablate & 1u)) {
+        slot = home[u];
+      } else {
+        const uint32_t sub = sub_table_of(key[u], nsub_log2);
+        const uint32_t s = probe_insert(keys_g + ((size_t)sub << cap_log2), key[u], mask);
+        slot = s == kNoSlot ? kNoSlot : ((sub << cap_log2) | s);
+        if (s == kNoSlot) atomicOr(&flags[0], 1u);
+      }
+      slot16[i] = slot == kNoSlot ? kNoSlot16 : (uint16_t)slot;
+      if (slot != kNoSlot && !(ablate & 2u)) atomicAdd(&hcnt[slot], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* out = part + (size_t)blockIdx.x * nslots;
+  for (uint32_t s = threadIdx.x; s < nslots; s += kHistThreads) out[s] = hcnt[s];
+}
+
+// tot row 0 = the stored counts, row g+1 = group g's total (chunks [16g, 16g+16)).
+__global__ __launch_bounds__(256) void rolling_hist_group_kernel(const uint32_t* __restrict__ part,
+                                                                 uint32_t nb, uint32_t nslots,
+                                                                 const uint32_t* __restrict__ cnt_g,
+                                                                 uint32_t* __restrict__ tot) {
+  const uint32_t s = blockIdx.x * 256 + threadIdx.x, g = blockIdx.y;
+  if (s >= nslots) return;
+  const uint32_t b0 = g * kGroup, b1 = b0 + kGroup < nb ? b0 + kGroup : nb;
+  uint32_t t = 0;
+#pragma unroll 4
+  for (uint32_t b = b0; b < b1; ++b) t += part[(size_t)b * nslots + s];
+  tot[(size_t)(g + 1) * nslots + s] = t;
+  if (g == 0) tot[s] = cnt_g[s];
+}
+
+// part[b][s] <- stored count + everything of chunks < b (exclusive); the last group writes the
+// final counts (it reads tot, not cnt_g, so no other thread's read races the write).
+__global__ __launch_bounds__(256) void rolling_hist_prefix_kernel(uint32_t* __restrict__ part,
+                                                                  uint32_t nb, uint32_t nslots,
+                                                                  const uint32_t* __restrict__ tot,
+                                                                  uint32_t* __restrict__ cnt_g) {
+  const uint32_t s = blockIdx.x * 256 + threadIdx.x, g = blockIdx.y;
+  if (s >= nslots) return;
+  uint32_t base = 0;
+  for (uint32_t r = 0; r <= g; ++r) base += tot[(size_t)r * nslots + s];
+  const uint32_t b0 = g * kGroup, b1 = b0 + kGroup < nb ? b0 + kGroup : nb;
+  uint32_t p[kGroup];
+#pragma unroll
+  for (int j = 0; j < kGroup; ++j) p[j] = b0 + j < b1 ? part[(size_t)(b0 + j) * nslots + s] : 0;
+#pragma unroll
+  for (int j = 0; j < kGroup; ++j) {
+    if (b0 + j < b1) part[(size_t)(b0 + j) * nslots + s] = base;
+    base += p[j];
+  }
+  if (g == gridDim.y - 1) cnt_g[s] = base;
+}
+
+__device__ __forceinline__ uint32_t tile_hash(uint32_t slot) {
+  return (slot * 2654435761u) >> (32 - 10);  // kHt = 1024
+}
+
+__global__ __launch_bounds__(kTile) void rolling_hist_emit_kernel(
+    const uint16_t* __restrict__ slot16, uint32_t n, uint32_t chunk,
+    const uint32_t* __restrict__ part, uint32_t nslots, const uint64_t* __restrict__ keys_g,
+    ExprProg filt, int need_key, uint64_t* __restrict__ out_key, uint64_t* __restrict__ out_val,
+    int64_t* __restrict__ out_tag, uint32_t* __restrict__ out_n, uint32_t out_cap,
+    uint32_t ablate) {
+  // LDS: run[nslots] u32 | ht[2][kHt] u32 (slot << 16 | tile id) | nid[2] (+2 pad)
+  //      | lane masks m64[2][kTile ids][kTileWaves] u64 (16-byte aligned: nslots % 4 == 0)
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* run = lds;
+  uint32_t* ht = lds + nslots;
+  uint32_t* nid = ht + 2 * kHt;
+  uint64_t* m64 = (uint64_t*)(nid + 4);
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t lo = blockIdx.x * chunk;
+  const uint32_t hi = n - lo < chunk ? n : lo + chunk;
+  const uint32_t* pre = part + (size_t)blockIdx.x * nslots;
+  for (uint32_t s = tid; s < nslots; s += kTile) run[s] = pre[s];
+  for (uint32_t e = tid; e < 2 * kHt; e += kTile) ht[e] = kHtEmpty;
+  for (uint32_t e = tid; e < 2 * kTile * kTileWaves; e += kTile) m64[e] = 0;
+  if (tid < 2) nid[tid] = 0;
+  __syncthreads();
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t pend_slot = kNoSlot, pend_cnt = 0;  // running-count update of the previous tile
+  int prev_h = -1;                               // ht entry this thread created last tile
+  uint32_t prev_id = 0;
+  uint32_t buf = 0;
+  // One tile: rank the records of [t0, t0 + kTile) (block-uniform call: every thread reaches
+  // the barriers). `slot` was loaded a tile earlier.
+  auto tile = [&](uint32_t t0, uint32_t slot) {
+    const uint32_t i = t0 + tid;
+    const bool valid = i < hi && slot != kNoSlot16;
+    uint32_t* H = ht + buf * kHt;
+    uint64_t* M = m64 + (size_t)buf * kTile * kTileWaves;
+    uint32_t h = 0;
+    bool winner = false;
+    if (valid && (ablate & 4u)) {
+      h = slot & (kTile - 1);
+    } else if (valid) {
+      h = tile_hash(slot);
+      for (;;) {
+        uint32_t e = __hip_atomic_load(&H[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (e == kHtEmpty) {
+          e = atomicCAS(&H[h], kHtEmpty, (slot << 16) | 0xFFFFu);
+          if (e == kHtEmpty) {
+            winner = true;
+            break;
+          }
+        }
+        if ((e >> 16) == slot) break;
+        h = (h + 1) & (kHt - 1);
+      }
+      if (winner) H[h] = (slot << 16) | atomicAdd(&nid[buf], 1u);
+    }
+    __syncthreads();  // A: ids assigned; the previous tile's readers are done
+    if (pend_slot != kNoSlot) run[pend_slot] = pend_cnt;
+    pend_slot = kNoSlot;
+    if (prev_h >= 0) {  // recycle the previous tile's buffer for the tile after this one
+      ht[(buf ^ 1) * kHt + prev_h] = kHtEmpty;
+      uint64_t* row = m64 + (size_t)(buf ^ 1) * kTile * kTileWaves + (size_t)prev_id * kTileWaves;
+#pragma unroll
+      for (int j = 0; j < kTileWaves; ++j) row[j] = 0;
+      prev_h = -1;
+    }
+    if (tid == 0) nid[buf ^ 1] = 0;
+    uint32_t id = 0;
+    if (valid) {
+      id = (ablate & 4u) ? h : H[h] & 0xFFFFu;
+      if (!(ablate & 8u)) atomicOr((unsigned long long*)&M[(size_t)id * kTileWaves + w], 1ull << lane);
+    }
+    __syncthreads();  // B: lane masks complete
+    bool emit = false;
+    uint32_t pcount = 0;
+    if (valid) {
+      const uint64_t* row = M + (size_t)id * kTileWaves;
+      uint64_t r[kTileWaves];
+#pragma unroll
+      for (int j = 0; j < kTileWaves; ++j) r[j] = row[j];
+      uint32_t before = 0;
+      uint64_t later = 0;
+#pragma unroll
+      for (int j = 0; j < kTileWaves; ++j) {  // compile-time indices only (no scratch array)
+        if ((uint32_t)j < w) before += (uint32_t)__popcll(r[j]);
+        if ((uint32_t)j == w) {
+          before += (uint32_t)__popcll(r[j] & below);
+          later |= (r[j] >> lane) >> 1;
+        }
+        if ((uint32_t)j > w) later |= r[j];
+      }
+      pcount = run[slot] + before + 1;
+      if (!later) {  // last record of this slot in the tile
+        pend_slot = slot;
+        pend_cnt = pcount;
+      }
+      emit = true;
+      if (filt.ncode && !(ablate & 16u)) {
+        const double key = need_key ? (double)keys_g[slot] : 0.0;
+        const RollVars rv{(double)pcount, (double)pcount, key, (double)pcount};
+        emit = expr_eval_chain(filt, rv) != 0.0;
+      }
+    }
+    if (winner) {
+      prev_h = (int)h;
+      prev_id = id;
+    }
+    const unsigned long long m = __ballot(emit);
+    if (m) {  // wave-uniform
+      uint32_t wb = 0;
+      if (lane == 0) wb = atomicAdd(out_n, (uint32_t)__popcll(m));
+      wb = __shfl(wb, 0);
+      if (emit) {
+        const uint32_t q = wb + (uint32_t)__popcll(m & below);
+        if (q < out_cap) {
+          out_key[q] = keys_g[slot];
+          out_val[q] = pcount;
+          out_tag[q] = (int64_t)i;  // src 0 << 32 | arrival index
+        }
+      }
+    }
+    buf ^= 1;
+  };
+  auto load = [&](uint32_t t0) { return t0 + tid < hi ? (uint32_t)slot16[t0 + tid] : kNoSlot16; };
+  // Two tiles per iteration with two prefetch registers: each tile's slots were loaded one tile
+  // of work earlier (a single register would be copied at the back-edge, exposing the load).
+  uint32_t sa = load(lo), sb = load(lo + kTile);
+  for (uint32_t t0 = lo; t0 < hi; t0 += 2 * kTile) {  // block-uniform bounds
+    tile(t0, sa);
+    sa = load(t0 + 2 * kTile);
+    if (t0 + kTile < hi) tile(t0 + kTile, sb);
+    sb = load(t0 + 3 * kTile);
+  }
+}
+
+}  // namespace
+
+namespace gpu {
+
+size_t rolling_hist_scratch_bytes(int64_t n, int64_t nslots) {
+  const Geo g = geometry((uint32_t)n);
+  const size_t words = (size_t)g.nb * nslots + (size_t)(g.ngroups + 1) * nslots;
+  return words * 4 + (((size_t)n * 2 + 15) & ~(size_t)15) + 16;
+}
+
+bool rolling_hist_supported(int agg, uint32_t count_n, int64_t nslots, const ExprProg& filt) {
+  return agg == AGG_COUNT && count_n == 0 && nslots >= 64 && nslots <= kRollHistMaxSlots &&
+         (filt.ncode == 0 || filt.chain);
+}
+
+void rolling_hist(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,
+                  uint32_t* cnt_g, void* scratch, size_t scratch_bytes, const ExprProg& filt,
+                  uint64_t* out_key, uint64_t* out_val, int64_t* out_tag, uint32_t* out_n,
+                  uint32_t out_cap, uint32_t* flags, intptr_t stream) {
+  const int64_t nslots = (int64_t)1 << (nsub_log2 + cap_log2);
+  if (!rolling_hist_supported(AGG_COUNT, 0, nslots, filt))
+    throw std::invalid_argument("rolling_hist: state table too large or filter not a chain");
+  if (n < 0 || n >= (int64_t)1 << 32) throw std::invalid_argument("rolling_hist: batch size");
+  if (n == 0) return;
+  if (scratch_bytes < rolling_hist_scratch_bytes(n, nslots))
+    throw std::invalid_argument("rolling_hist: scratch buffer too small");
+  const Geo g = geometry((uint32_t)n);
+  uint32_t* part = (uint32_t*)scratch;
+  uint32_t* tot = part + (size_t)g.nb * nslots;
+  uint16_t* slot16 = (uint16_t*)(tot + (size_t)(g.ngroups + 1) * nslots);
+  int need_key = 0;
+  for (int i = 0; i < filt.ncode; ++i)
+    if (filt.code[2 * i] == OP_VAR && filt.code[2 * i + 1] == 4) need_key = 1;
+  hipStream_t s = (hipStream_t)stream;
+  // MXS_RH_ABLATE (timing experiments only; results are wrong when set): 1 no probe past the
+  // home slot, 2 no histogram atomics, 4 no tile hash (id = slot % 512), 8 no lane-mask ORs,
+  // 16 no filter evaluation.
+  static const uint32_t ablate = [] {
+    const char* e = std::getenv("MXS_RH_ABLATE");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
+  }();
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)rolling_hist_count_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_CHECK(hipFuncSetAttribute((const void*)rolling_hist_emit_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  const uint32_t ns = (uint32_t)nslots;
+  hipLaunchKernelGGL(rolling_hist_count_kernel, dim3(g.nb), dim3(kHistThreads), ns * 4, s, keys,
+                     (uint32_t)n, g.chunk, nsub_log2, cap_log2, keys_g, slot16, part, ns, flags,
+                     ablate);
+  const dim3 sg((ns + 255) / 256, g.ngroups);
+  hipLaunchKernelGGL(rolling_hist_group_kernel, sg, dim3(256), 0, s, part, g.nb, ns, cnt_g, tot);
+  hipLaunchKernelGGL(rolling_hist_prefix_kernel, sg, dim3(256), 0, s, part, g.nb, ns, tot, cnt_g);
+  const size_t lds = (size_t)ns * 4 + 2 * kHt * 4 + 16 + (size_t)2 * kTile * kTileWaves * 8;
+  hipLaunchKernelGGL(rolling_hist_emit_kernel, dim3(g.nb), dim3(kTile), lds, s, slot16,
+                     (uint32_t)n, g.chunk, part, ns, keys_g, filt, need_key, out_key, out_val,
+                     out_tag, out_n, out_cap, ablate);
+  HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace gpu
+}  // namespace mxs

@@ -25,7 +25,7 @@ PKG = ROOT / "mxstream"
 ARCH = os.environ.get("MXS_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["kernels_hip.hip", "sort_hip.hip", "parse_hip.hip", "vector_hip.hip",
-               "check_hip.hip"]
+               "check_hip.hip", "rolling_hist_hip.hip"]
 CXX_SOURCES = ["kernels_cpu.cpp", "runtime.cpp", "sessions.cpp", "vector_cpu.cpp",
                "vector_bindings.cpp", "trace.cpp", "check_cpu.cpp", "bindings.cpp"]
 # roctx ranges (csrc/trace.cpp) come from the ROCm profiler SDK's marker library.
@@ -139,8 +139,8 @@ def build_sanitize(verbose: bool = False) -> Path:
     return exe
 
 
-CAPI_SOURCES = ["kernels_hip.hip", "check_hip.hip", "sort_hip.hip", "kernels_cpu.cpp",
-                "pipeline.cpp"]
+CAPI_SOURCES = ["kernels_hip.hip", "check_hip.hip", "sort_hip.hip", "rolling_hist_hip.hip",
+                "kernels_cpu.cpp", "pipeline.cpp"]
 
 
 def capi_path() -> Path:

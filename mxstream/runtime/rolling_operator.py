@@ -60,7 +60,13 @@ class KeyedRollingOperator:
         self.filter_prog = filter_prog
         from .geometry import state_geometry
 
-        self.nsub, self.cap_log2 = state_geometry(max_keys, self.world, cap_log2)
+        if self.world == 1 and cap_log2 is None:
+            # One rank: no keyBy buckets or LDS sub-tables to size for (the direct GPU path reads
+            # the source columns), so a single table at <= 0.7 load keeps small key spaces small
+            # enough for the sort-free LDS counter (rolling_hist: <= 16K slots ~ 11K keys).
+            self.nsub, self.cap_log2 = 1, max(6, math.ceil(math.log2((max_keys + 64) / 0.7)))
+        else:
+            self.nsub, self.cap_log2 = state_geometry(max_keys, self.world, cap_log2)
         cap_log2 = self.cap_log2
         self.nsub_log2 = self.nsub.bit_length() - 1
         self.nslots = self.nsub << cap_log2
@@ -81,6 +87,10 @@ class KeyedRollingOperator:
         self.steps = 0
         self.records_in = 0
         self.direct_single_rank = True  # world 1 on the GPU: no partition pass (_process_direct)
+        # Sort-free COUNT path (rolling_hist) when the table fits its LDS counter; False forces
+        # the sort path (A/B, tests).
+        self.sort_free = True
+        self._hist_tmp = None
 
     def _alloc(self, batch_capacity: int, slack: float = 1.5):
         self.batch_capacity = int(batch_capacity)
@@ -131,6 +141,20 @@ class KeyedRollingOperator:
         self.out_n.zero_()
         code, consts = self.filter_prog.as_args()
         cap = self.out_key.numel()
+        if self.sort_free and m.rolling_hist_supported(self.agg, self.count_window, self.nslots,
+                                                       code, consts):
+            # Counting formulation: per-chunk LDS histograms, a cross-chunk prefix seeded by the
+            # stored counts, then tile-ranked emission (csrc/rolling_hist_hip.hip) -- no sort.
+            need = m.rolling_hist_scratch_bytes(n, self.nslots)
+            if self._hist_tmp is None or self._hist_tmp.numel() < need:
+                self._hist_tmp = torch.empty(need, dtype=torch.uint8, device=self.device)
+            m.gpu_rolling_hist(keys.data_ptr(), n, self.nsub_log2, self.cap_log2,
+                               self.keys_g.data_ptr(), self.cnt_g.data_ptr(),
+                               self._hist_tmp.data_ptr(), self._hist_tmp.numel(), code, consts,
+                               self.out_key.data_ptr(), self.out_val.data_ptr(),
+                               self.out_tag.data_ptr(), self.out_n.data_ptr(), cap,
+                               self.flags.data_ptr(), st)
+            return self._emit(to_host)
         self.n_buf.zero_()
         shift = max(1, int(n - 1).bit_length())
         m.gpu_rolling_lookup_direct(keys.data_ptr(), vals.data_ptr(), n, self.nsub_log2,

@@ -20,6 +20,8 @@ for step in "$@"; do
   case $step in
     tests) timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$out/pytest_gpu.log" 2>&1
            st=$?; tail -3 "$out/pytest_gpu.log"; [ $st -eq 0 ] || [ $st -eq 1 ] || exit $st ;;
+    t_*) f=${step#t_}; timeout -k 10 600 python -u -m pytest tests/test_$f.py -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$out/pytest_$f.log" 2>&1
+         st=$?; tail -3 "$out/pytest_$f.log"; [ $st -eq 0 ] || exit $st ;;
     smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 || exit $? ;;
     bench) timeout -k 10 300 python bench.py --steps 48 --warmup 8 > "$out/bench.log" 2>&1 || exit $? ;;
     bench_nopipe) timeout -k 10 300 python bench.py --steps 48 --warmup 8 --no-pipeline > "$out/bench_nopipe.log" 2>&1 || exit $? ;;

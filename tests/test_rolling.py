@@ -90,6 +90,45 @@ def test_rolling_gpu_equals_cpu(gpu_device, agg, nkeys, direct):
     assert res["cuda"] == res["cpu"]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,nkeys,zipf", [(1, 10, 0.0), (777, 50, 0.0), (70_001, 10_000, 0.0),
+                                          (3_000_000, 10_000, 0.0), (1 << 20, 5_000, 1.2),
+                                          (1 << 18, 11_000, 0.0)])
+@pytest.mark.parametrize("filt", ["none", "count", "key", "stack"])
+def test_rolling_sort_free_count(gpu_device, n, nkeys, zipf, filt):
+    """Sort-free COUNT (csrc/rolling_hist_hip.hip: chunk histograms, cross-chunk prefix, tile
+    ranking by lane masks) == the sort path on the GPU == the C++ twin, per record, over several
+    batches (state carried), chunk counts > 16 (two-level prefix) and a Zipf hot key."""
+    fp = {"none": E.EMPTY, "count": E.compile_expr(E.var(E.VAR_COUNT) % 7 == 0),
+          "key": E.compile_expr(E.var(E.VAR_KEY) % 3 == 1),
+          # not a chain program: the operator falls back to the sort path
+          "stack": E.compile_expr((E.var(E.VAR_KEY) % 3 == 1) & (E.var(E.VAR_COUNT) > 2))}[filt]
+    res = {}
+    for d, sort_free in ((gpu_device, True), (gpu_device, False), (torch.device("cpu"), False)):
+        op = KeyedRollingOperator(agg=K.AGG_COUNT, device=d, max_keys=nkeys, batch_capacity=n,
+                                  filter_prog=fp)
+        op.sort_free = sort_free
+        if d.type == "cuda":
+            assert op.nslots <= 16384
+        got = {}
+        for s in range(3):
+            keys = torch.empty(n, dtype=torch.int64, device=d)
+            K.gen_events(keys, torch.empty_like(keys), torch.empty_like(keys), seed=s, stream_id=0,
+                         idx0=s * n, nkeys=nkeys, ts_base=0, ts_span=1000, disorder=0, val_lo=0,
+                         val_span=10, zipf=zipf)
+            rows = op.process(keys, keys)
+            order = np.lexsort((rows.tags, rows.keys))
+            got[s] = (rows.keys[order].tolist(), rows.values[order].tolist(),
+                      rows.tags[order].tolist())
+        res[(d.type, sort_free)] = got
+        res[(d.type, sort_free, "state")] = sorted(
+            (int(k), int(c)) for k, c in zip(op.keys_g.cpu().tolist(), op.cnt_g.cpu().tolist())
+            if k != -1)
+    assert res[("cuda", True)] == res[("cpu", False)]
+    assert res[("cuda", False)] == res[("cpu", False)]
+    assert res[("cuda", True, "state")] == res[("cpu", False, "state")]
+
+
 def _count_oracle(batches, agg, n):
     """Tumbling count windows per key (countWindow(n)): one row per n elements."""
     win, out = {}, {}
