@@ -367,11 +367,12 @@ PYBIND11_MODULE(_mxs_native, m) {
                                intptr_t keys_g, intptr_t cnt_g, intptr_t scratch,
                                size_t scratch_bytes, std::vector<int32_t> code,
                                std::vector<double> consts, intptr_t ok, intptr_t ov, intptr_t ot,
-                               intptr_t on, uint32_t out_cap, intptr_t flags, intptr_t stream) {
+                               intptr_t on, uint32_t out_cap, intptr_t flags, int dense,
+                               intptr_t stream) {
     gpu::rolling_hist(P<uint64_t>(keys), n, nsub_log2, cap_log2, P<uint64_t>(keys_g),
                       P<uint32_t>(cnt_g), P<void>(scratch), scratch_bytes, make_prog(code, consts),
                       P<uint64_t>(ok), P<uint64_t>(ov), P<int64_t>(ot), P<uint32_t>(on), out_cap,
-                      P<uint32_t>(flags), stream);
+                      P<uint32_t>(flags), dense, stream);
   });
   m.def("gpu_rolling_heads", [](intptr_t sk, intptr_t n_in, int64_t n_cap, intptr_t heads,
                                 intptr_t n_heads, int shift, intptr_t stream) {

@@ -161,7 +161,7 @@ bool rolling_hist_supported(int agg, uint32_t count_n, int64_t nslots, const Exp
 void rolling_hist(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,
                   uint32_t* cnt_g, void* scratch, size_t scratch_bytes, const ExprProg& filt,
                   uint64_t* out_key, uint64_t* out_val, int64_t* out_tag, uint32_t* out_n,
-                  uint32_t out_cap, uint32_t* flags, intptr_t stream);
+                  uint32_t out_cap, uint32_t* flags, int dense, intptr_t stream);
 void session_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bcap,
                     int cap_log2, uint64_t* keys_g, uint64_t* spill_set, uint32_t spill_mask,
                     int spill_any, int64_t* sk, uint64_t* vals, uint32_t* n_out, Rec* host_recs,

@@ -15,12 +15,13 @@
 //             is written back to the state table here.
 //   3. emit   (one 512-thread workgroup per chunk): the chunk's running counts start from its
 //             exclusive prefix in LDS; records are ranked a 512-record tile at a time. Within a
-//             tile, each distinct slot gets a tile-local id through an LDS hash table and every
-//             record ORs its lane bit into that id's per-wave 64-bit lane mask; a record's rank is
-//             then popcount(masks of earlier waves) + popcount(own wave's mask below its lane) --
+//             tile, every record writes its thread id to owner[slot]; the write that lands names
+//             the slot for the tile (no atomics, no hash table). Every record ORs its lane bit
+//             into its owner's per-wave 64-bit lane mask; a record's rank is then
+//             popcount(masks of earlier waves) + popcount(own wave's mask below its lane) --
 //             arrival order without a sort or a serial chain between waves. The last record of a
 //             slot in the tile advances the running count (applied after the next tile's first
-//             barrier; two table buffers alternate, so a tile costs two barriers). The traced
+//             barrier; two mask buffers alternate, so a tile costs two barriers). The traced
 //             filter epilogue and the wave-ballot row compaction are fused.
 //
 // Per record: 8 B key read + 2 B slot write (hist), 2 B slot read (emit) instead of the sort
@@ -48,8 +49,6 @@ namespace {
 constexpr int kHistThreads = 1024;
 constexpr int kTileWaves = 8;
 constexpr int kTile = kTileWaves * 64;  // records per tile = threads of the emit workgroup
-constexpr int kHt = 1024;               // tile hash entries per buffer (<= 512 keys: load <= 0.5)
-constexpr uint32_t kHtEmpty = 0xFFFFFFFFu;
 constexpr uint16_t kNoSlot16 = 0xFFFF;
 constexpr uint32_t kChunkMin = kTile, kChunkMax = 65536;
 constexpr int kGroup = 16;  // chunks per group in the cross-chunk scan
@@ -88,14 +87,18 @@ struct RollVars {  // filter variables of the rolling epilogue (rolling_scan's n
 // Insert-or-find by linear probing, eight slots per round trip: the chain is contiguous, so one
 // batch of independent loads covers what would otherwise be up to eight dependent L2 reads (the
 // tail of the probe-length distribution, not its mean, sets a wave's latency).
+// The probe reads are plain (L2-cacheable) loads, not device-scope atomic loads: the table is
+// insert-only (a slot goes EMPTY -> key once), so a stale line can only show EMPTY where a key
+// now sits, and the device-scope CAS on that slot returns the real occupant (our key: found;
+// another key: probing continues after it). Device-scope loads of a 128 KB table hammered by
+// every CU are served past the per-XCD L2s.
 __device__ __forceinline__ uint32_t probe_insert(uint64_t* keys, uint64_t key, uint32_t mask) {
   constexpr uint32_t W = 8;
   uint32_t s = slot_hash(key) & mask;
   for (uint32_t done = 0; done <= mask;) {
     uint64_t k[W];
 #pragma unroll
-    for (uint32_t j = 0; j < W; ++j)
-      k[j] = __hip_atomic_load(&keys[(s + j) & mask], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t j = 0; j < W; ++j) k[j] = keys[(s + j) & mask];  // plain: see below
     uint32_t j = 0;
     for (; j < W; ++j) {
       if (k[j] == key) return (s + j) & mask;
@@ -119,7 +122,7 @@ __device__ __forceinline__ uint32_t probe_insert(uint64_t* keys, uint64_t key, u
 __global__ __launch_bounds__(kHistThreads) void rolling_hist_count_kernel(
     const uint64_t* __restrict__ keys, uint32_t n, uint32_t chunk, int nsub_log2, int cap_log2,
     uint64_t* __restrict__ keys_g, uint16_t* __restrict__ slot16, uint32_t* __restrict__ part,
-    uint32_t nslots, uint32_t* __restrict__ flags, uint32_t ablate) {
+    uint32_t nslots, uint32_t* __restrict__ flags, int dense, uint32_t ablate) {
   extern __shared__ uint32_t hcnt[];
   for (uint32_t s = threadIdx.x; s < nslots; s += kHistThreads) hcnt[s] = 0;
   __syncthreads();
@@ -128,41 +131,81 @@ __global__ __launch_bounds__(kHistThreads) void rolling_hist_count_kernel(
   const uint32_t mask = (1u << cap_log2) - 1;
   // Eight records per thread per round: the key loads and first-probe table reads are all in
   // flight before any is consumed (most records hit their home slot).
-  constexpr int U = 8;
-  for (uint32_t base = lo; base < hi; base += kHistThreads * U) {
-    uint64_t key[U], k0[U];
-    uint32_t home[U];
+  constexpr int U = 8, W = 4;
+  auto finish = [&](uint32_t i, uint32_t slot) {
+    slot16[i] = slot == kNoSlot ? kNoSlot16 : (uint16_t)slot;
+    if (slot != kNoSlot && !(ablate & 2u)) atomicAdd(&hcnt[slot], 1u);
+  };
+  if (dense) {  // dictionary ids: slot = key, no table probe (keys_g is filled by the prefix pass)
+    for (uint32_t base = lo; base < hi; base += kHistThreads * U) {
+      uint64_t key[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = base + u * kHistThreads + threadIdx.x;
+        key[u] = i < hi ? keys[i] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t i = base + u * kHistThreads + threadIdx.x;
+        if (i >= hi) continue;
+        const bool ok = key[u] < nslots;
+        if (!ok) atomicOr(&flags[0], 16u);
+        finish(i, ok ? (uint32_t)key[u] : kNoSlot);
+      }
+    }
+  }
+  for (uint32_t base = dense ? hi : lo; base < hi; base += kHistThreads * U) {
+    uint64_t key[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = base + u * kHistThreads + threadIdx.x;
       key[u] = i < hi ? keys[i] : 0;
     }
+    // Round 1: a 4-slot window from every record's home slot, all 32 loads in flight at once
+    // (plain loads: a stale EMPTY only sends the record to the CAS path below).
+    uint64_t k[U][W];
+    uint32_t home[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = base + u * kHistThreads + threadIdx.x;
-      home[u] = (sub_table_of(key[u], nsub_log2) << cap_log2) | (slot_hash(key[u]) & mask);
-      k0[u] = i < hi ? __hip_atomic_load(&keys_g[home[u]], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT)
-                     : 0;
+      home[u] = slot_hash(key[u]) & mask;
+      const uint64_t* tab = keys_g + ((size_t)sub_table_of(key[u], nsub_log2) << cap_log2);
+#pragma unroll
+      for (int j = 0; j < W; ++j) k[u][j] = i < hi ? tab[(home[u] + j) & mask] : 0;
     }
+    uint32_t pend = 0;  // records whose key was not met in the window (insert or long chain)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const uint32_t i = base + u * kHistThreads + threadIdx.x;
       if (i >= hi) continue;
-      uint32_t slot;
       if (key[u] >= kTombKey) {  // reserved ids (table markers): flagged, never stored
         atomicOr(&flags[0], 4u);
-        slot = kNoSlot;
-      } else if (k0[u] == key[u] || (ablate & 1u)) {
-        slot = home[u];
-      } else {
-        const uint32_t sub = sub_table_of(key[u], nsub_log2);
-        const uint32_t s = probe_insert(keys_g + ((size_t)sub << cap_log2), key[u], mask);
-        slot = s == kNoSlot ? kNoSlot : ((sub << cap_log2) | s);
-        if (s == kNoSlot) atomicOr(&flags[0], 1u);
+        finish(i, kNoSlot);
+        continue;
       }
-      slot16[i] = slot == kNoSlot ? kNoSlot16 : (uint16_t)slot;
-      if (slot != kNoSlot && !(ablate & 2u)) atomicAdd(&hcnt[slot], 1u);
+      uint32_t hit = kNoSlot;
+#pragma unroll
+      for (int j = W - 1; j >= 0; --j)
+        if (k[u][j] == key[u]) hit = (home[u] + j) & mask;
+      if (hit == kNoSlot && (ablate & 1u)) hit = home[u];
+      if (hit != kNoSlot)
+        finish(i, (sub_table_of(key[u], nsub_log2) << cap_log2) | hit);
+      else
+        pend |= 1u << u;
+    }
+    // Round 2: the lane's pending records one at a time -- the wave iterates max-over-lanes
+    // times (usually once) instead of once per unrolled record.
+    while (pend) {
+      const int u = __ffs(pend) - 1;
+      pend &= pend - 1;
+      uint64_t kk = 0;
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (j == u) kk = key[j];
+      const uint32_t sub = sub_table_of(kk, nsub_log2);
+      const uint32_t sl = probe_insert(keys_g + ((size_t)sub << cap_log2), kk, mask);
+      if (sl == kNoSlot) atomicOr(&flags[0], 1u);
+      finish(base + u * kHistThreads + threadIdx.x, sl == kNoSlot ? kNoSlot : (sub << cap_log2) | sl);
     }
   }
   __syncthreads();
@@ -190,7 +233,9 @@ __global__ __launch_bounds__(256) void rolling_hist_group_kernel(const uint32_t*
 __global__ __launch_bounds__(256) void rolling_hist_prefix_kernel(uint32_t* __restrict__ part,
                                                                   uint32_t nb, uint32_t nslots,
                                                                   const uint32_t* __restrict__ tot,
-                                                                  uint32_t* __restrict__ cnt_g) {
+                                                                  uint32_t* __restrict__ cnt_g,
+                                                                  uint64_t* __restrict__ keys_g,
+                                                                  int dense) {
   const uint32_t s = blockIdx.x * 256 + threadIdx.x, g = blockIdx.y;
   if (s >= nslots) return;
   uint32_t base = 0;
@@ -204,91 +249,70 @@ __global__ __launch_bounds__(256) void rolling_hist_prefix_kernel(uint32_t* __re
     if (b0 + j < b1) part[(size_t)(b0 + j) * nslots + s] = base;
     base += p[j];
   }
-  if (g == gridDim.y - 1) cnt_g[s] = base;
-}
-
-__device__ __forceinline__ uint32_t tile_hash(uint32_t slot) {
-  return (slot * 2654435761u) >> (32 - 10);  // kHt = 1024
+  if (g == gridDim.y - 1) {
+    cnt_g[s] = base;
+    if (dense && base) keys_g[s] = s;  // dense slots hold their own key id
+  }
 }
 
 __global__ __launch_bounds__(kTile) void rolling_hist_emit_kernel(
     const uint16_t* __restrict__ slot16, uint32_t n, uint32_t chunk,
     const uint32_t* __restrict__ part, uint32_t nslots, const uint64_t* __restrict__ keys_g,
-    ExprProg filt, int need_key, uint64_t* __restrict__ out_key, uint64_t* __restrict__ out_val,
-    int64_t* __restrict__ out_tag, uint32_t* __restrict__ out_n, uint32_t out_cap,
-    uint32_t ablate) {
-  // LDS: run[nslots] u32 | ht[2][kHt] u32 (slot << 16 | tile id) | nid[2] (+2 pad)
-  //      | lane masks m64[2][kTile ids][kTileWaves] u64 (16-byte aligned: nslots % 4 == 0)
+    ExprProg filt, int need_key, int dense, uint64_t* __restrict__ out_key,
+    uint64_t* __restrict__ out_val, int64_t* __restrict__ out_tag, uint32_t* __restrict__ out_n,
+    uint32_t out_cap, uint32_t ablate) {
+  // LDS (<= 160 KB at 16K slots): run[nslots] u32 | owner[nslots] u16 | lane masks
+  // m64[2][kTileWaves][kTile] u64, wave-major so a wave's 64 lanes touch 64 different owners'
+  // words (owner-major rows would put every owner on the same 4 of the 64 banks).
+  // A tile's distinct slots are named without atomics: every record writes its thread id to
+  // owner[slot] and, after the barrier, reads back the one write that landed -- the same id for
+  // all records of that slot in the tile. Stale owner entries are never read (a slot's entry is
+  // written in every tile that reads it), so the array is never cleared.
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* run = lds;
-  uint32_t* ht = lds + nslots;
-  uint32_t* nid = ht + 2 * kHt;
-  uint64_t* m64 = (uint64_t*)(nid + 4);
+  uint16_t* owner = (uint16_t*)(lds + nslots);
+  uint64_t* m64 = (uint64_t*)(lds + nslots + nslots / 2);
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t lo = blockIdx.x * chunk;
   const uint32_t hi = n - lo < chunk ? n : lo + chunk;
   const uint32_t* pre = part + (size_t)blockIdx.x * nslots;
   for (uint32_t s = tid; s < nslots; s += kTile) run[s] = pre[s];
-  for (uint32_t e = tid; e < 2 * kHt; e += kTile) ht[e] = kHtEmpty;
   for (uint32_t e = tid; e < 2 * kTile * kTileWaves; e += kTile) m64[e] = 0;
-  if (tid < 2) nid[tid] = 0;
+  if (!filt.ncode && blockIdx.x == 0 && tid == 0) atomicAdd(out_n, n);  // rows = records
   __syncthreads();
   const uint64_t below = (1ull << lane) - 1ull;
   uint32_t pend_slot = kNoSlot, pend_cnt = 0;  // running-count update of the previous tile
-  int prev_h = -1;                               // ht entry this thread created last tile
-  uint32_t prev_id = 0;
+  bool was_owner = false;                        // this thread's masks of the previous tile
   uint32_t buf = 0;
   // One tile: rank the records of [t0, t0 + kTile) (block-uniform call: every thread reaches
   // the barriers). `slot` was loaded a tile earlier.
   auto tile = [&](uint32_t t0, uint32_t slot) {
     const uint32_t i = t0 + tid;
     const bool valid = i < hi && slot != kNoSlot16;
-    uint32_t* H = ht + buf * kHt;
     uint64_t* M = m64 + (size_t)buf * kTile * kTileWaves;
-    uint32_t h = 0;
-    bool winner = false;
-    if (valid && (ablate & 4u)) {
-      h = slot & (kTile - 1);
-    } else if (valid) {
-      h = tile_hash(slot);
-      for (;;) {
-        uint32_t e = __hip_atomic_load(&H[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (e == kHtEmpty) {
-          e = atomicCAS(&H[h], kHtEmpty, (slot << 16) | 0xFFFFu);
-          if (e == kHtEmpty) {
-            winner = true;
-            break;
-          }
-        }
-        if ((e >> 16) == slot) break;
-        h = (h + 1) & (kHt - 1);
-      }
-      if (winner) H[h] = (slot << 16) | atomicAdd(&nid[buf], 1u);
-    }
-    __syncthreads();  // A: ids assigned; the previous tile's readers are done
+    if (valid) owner[slot] = (uint16_t)((ablate & 4u) ? (slot & (kTile - 1)) : tid);
+    __syncthreads();  // A: owners settled; the previous tile's readers are done
     if (pend_slot != kNoSlot) run[pend_slot] = pend_cnt;
     pend_slot = kNoSlot;
-    if (prev_h >= 0) {  // recycle the previous tile's buffer for the tile after this one
-      ht[(buf ^ 1) * kHt + prev_h] = kHtEmpty;
-      uint64_t* row = m64 + (size_t)(buf ^ 1) * kTile * kTileWaves + (size_t)prev_id * kTileWaves;
+    if (was_owner) {  // recycle the previous tile's mask buffer for the tile after this one
+      uint64_t* col = m64 + (size_t)(buf ^ 1) * kTile * kTileWaves + tid;
 #pragma unroll
-      for (int j = 0; j < kTileWaves; ++j) row[j] = 0;
-      prev_h = -1;
+      for (int j = 0; j < kTileWaves; ++j) col[j * kTile] = 0;
     }
-    if (tid == 0) nid[buf ^ 1] = 0;
     uint32_t id = 0;
     if (valid) {
-      id = (ablate & 4u) ? h : H[h] & 0xFFFFu;
-      if (!(ablate & 8u)) atomicOr((unsigned long long*)&M[(size_t)id * kTileWaves + w], 1ull << lane);
+      id = owner[slot];
+      if (!(ablate & 8u)) atomicOr((unsigned long long*)&M[(size_t)w * kTile + id], 1ull << lane);
     }
+    was_owner = valid && id == tid;
     __syncthreads();  // B: lane masks complete
     bool emit = false;
     uint32_t pcount = 0;
     if (valid) {
-      const uint64_t* row = M + (size_t)id * kTileWaves;
+      const uint64_t* col = M + id;
       uint64_t r[kTileWaves];
 #pragma unroll
-      for (int j = 0; j < kTileWaves; ++j) r[j] = row[j];
+      for (int j = 0; j < kTileWaves; ++j) r[j] = col[j * kTile];
       uint32_t before = 0;
       uint64_t later = 0;
 #pragma unroll
@@ -307,14 +331,19 @@ __global__ __launch_bounds__(kTile) void rolling_hist_emit_kernel(
       }
       emit = true;
       if (filt.ncode && !(ablate & 16u)) {
-        const double key = need_key ? (double)keys_g[slot] : 0.0;
+        const double key = !need_key ? 0.0 : dense ? (double)slot : (double)keys_g[slot];
         const RollVars rv{(double)pcount, (double)pcount, key, (double)pcount};
         emit = expr_eval_chain(filt, rv) != 0.0;
       }
     }
-    if (winner) {
-      prev_h = (int)h;
-      prev_id = id;
+    buf ^= 1;
+    if (!filt.ncode) {  // every record emits: its row index is its arrival index (no atomics)
+      if (valid && i < out_cap) {
+        out_key[i] = dense ? slot : keys_g[slot];
+        out_val[i] = pcount;
+        out_tag[i] = (int64_t)i;
+      }
+      return;
     }
     const unsigned long long m = __ballot(emit);
     if (m) {  // wave-uniform
@@ -324,23 +353,32 @@ __global__ __launch_bounds__(kTile) void rolling_hist_emit_kernel(
       if (emit) {
         const uint32_t q = wb + (uint32_t)__popcll(m & below);
         if (q < out_cap) {
-          out_key[q] = keys_g[slot];
+          out_key[q] = dense ? slot : keys_g[slot];
           out_val[q] = pcount;
           out_tag[q] = (int64_t)i;  // src 0 << 32 | arrival index
         }
       }
     }
-    buf ^= 1;
   };
   auto load = [&](uint32_t t0) { return t0 + tid < hi ? (uint32_t)slot16[t0 + tid] : kNoSlot16; };
-  // Two tiles per iteration with two prefetch registers: each tile's slots were loaded one tile
-  // of work earlier (a single register would be copied at the back-edge, exposing the load).
-  uint32_t sa = load(lo), sb = load(lo + kTile);
-  for (uint32_t t0 = lo; t0 < hi; t0 += 2 * kTile) {  // block-uniform bounds
-    tile(t0, sa);
-    sa = load(t0 + 2 * kTile);
-    if (t0 + kTile < hi) tile(t0 + kTile, sb);
-    sb = load(t0 + 3 * kTile);
+  // Four tiles per iteration: the next group's slots are loaded before this group's four tiles
+  // run, and only the back-edge copy waits for them (four tiles of work later).
+  constexpr int G = 4;
+  uint32_t cur[G];
+#pragma unroll
+  for (int j = 0; j < G; ++j) cur[j] = load(lo + j * kTile);
+  // Retire the prologue loads here: with them pending on the loop's entry edge the wait-count
+  // pass merges that state into the header and waits for every in-flight load each iteration.
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  for (uint32_t t0 = lo; t0 < hi; t0 += G * kTile) {  // block-uniform bounds
+    uint32_t nxt[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) nxt[j] = load(t0 + (G + j) * kTile);
+#pragma unroll
+    for (int j = 0; j < G; ++j)
+      if (t0 + j * kTile < hi) tile(t0 + j * kTile, cur[j]);
+#pragma unroll
+    for (int j = 0; j < G; ++j) cur[j] = nxt[j];
   }
 }
 
@@ -362,7 +400,7 @@ bool rolling_hist_supported(int agg, uint32_t count_n, int64_t nslots, const Exp
 void rolling_hist(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,
                   uint32_t* cnt_g, void* scratch, size_t scratch_bytes, const ExprProg& filt,
                   uint64_t* out_key, uint64_t* out_val, int64_t* out_tag, uint32_t* out_n,
-                  uint32_t out_cap, uint32_t* flags, intptr_t stream) {
+                  uint32_t out_cap, uint32_t* flags, int dense, intptr_t stream) {
   const int64_t nslots = (int64_t)1 << (nsub_log2 + cap_log2);
   if (!rolling_hist_supported(AGG_COUNT, 0, nslots, filt))
     throw std::invalid_argument("rolling_hist: state table too large or filter not a chain");
@@ -379,8 +417,8 @@ void rolling_hist(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
     if (filt.code[2 * i] == OP_VAR && filt.code[2 * i + 1] == 4) need_key = 1;
   hipStream_t s = (hipStream_t)stream;
   // MXS_RH_ABLATE (timing experiments only; results are wrong when set): 1 no probe past the
-  // home slot, 2 no histogram atomics, 4 no tile hash (id = slot % 512), 8 no lane-mask ORs,
-  // 16 no filter evaluation.
+  // home window, 2 no histogram atomics, 4 owner = slot % 512, 8 no lane-mask ORs, 16 no filter
+  // evaluation.
   static const uint32_t ablate = [] {
     const char* e = std::getenv("MXS_RH_ABLATE");
     return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
@@ -396,14 +434,15 @@ void rolling_hist(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
   const uint32_t ns = (uint32_t)nslots;
   hipLaunchKernelGGL(rolling_hist_count_kernel, dim3(g.nb), dim3(kHistThreads), ns * 4, s, keys,
                      (uint32_t)n, g.chunk, nsub_log2, cap_log2, keys_g, slot16, part, ns, flags,
-                     ablate);
+                     dense, ablate);
   const dim3 sg((ns + 255) / 256, g.ngroups);
   hipLaunchKernelGGL(rolling_hist_group_kernel, sg, dim3(256), 0, s, part, g.nb, ns, cnt_g, tot);
-  hipLaunchKernelGGL(rolling_hist_prefix_kernel, sg, dim3(256), 0, s, part, g.nb, ns, tot, cnt_g);
-  const size_t lds = (size_t)ns * 4 + 2 * kHt * 4 + 16 + (size_t)2 * kTile * kTileWaves * 8;
+  hipLaunchKernelGGL(rolling_hist_prefix_kernel, sg, dim3(256), 0, s, part, g.nb, ns, tot, cnt_g,
+                     keys_g, dense);
+  const size_t lds = (size_t)ns * 6 + (size_t)2 * kTile * kTileWaves * 8;  // 160 KB at 16K
   hipLaunchKernelGGL(rolling_hist_emit_kernel, dim3(g.nb), dim3(kTile), lds, s, slot16,
-                     (uint32_t)n, g.chunk, part, ns, keys_g, filt, need_key, out_key, out_val,
-                     out_tag, out_n, out_cap, ablate);
+                     (uint32_t)n, g.chunk, part, ns, keys_g, filt, need_key, dense, out_key,
+                     out_val, out_tag, out_n, out_cap, ablate);
   HIP_CHECK(hipGetLastError());
 }
 

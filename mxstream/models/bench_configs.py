@@ -95,13 +95,16 @@ def config1(steps: int, warmup: int, lines_per_step: int = 1 << 20, device: str 
 
 
 def config2(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000,
-            device: str = "cuda") -> dict:
+            device: str = "cuda", dense_keys: bool = True, sort_free: bool = True) -> dict:
     """Keyed ValueState counter: count += 1 per record, per-record post-update value; alerts
-    (rows copied to the host) when a key's count crosses a multiple of 100k."""
+    (rows copied to the host) when a key's count crosses a multiple of 100k. dense_keys: the
+    keys are dictionary ids (as columnar ingest produces), slot = id; else hashed state."""
     dev = torch.device(device)
+    dense_keys = dense_keys and dev.type == "cuda" and sort_free
     op = KeyedRollingOperator(agg=K.AGG_COUNT, device=dev, max_keys=keys, batch_capacity=batch,
                               filter_prog=E.compile_expr(E.var(E.VAR_COUNT) % 100_000 == 0),
-                              emit_capacity=1 << 20)
+                              emit_capacity=1 << 20, dense_keys=dense_keys)
+    op.sort_free = sort_free
     kt = torch.empty(batch, dtype=torch.int64, device=dev)
     tt = torch.empty_like(kt)
     vt = torch.empty_like(kt)
@@ -123,7 +126,9 @@ def config2(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000,
         alerts += step()
     _sync(dev)
     dt = time.perf_counter() - t0
-    return {"config": 2, "metric": "events/sec (keyed ValueState counter, 10k keys)",
+    return {"config": 2, "keyed_state": "dense" if dense_keys else "hashed",
+            "path": "sort-free" if sort_free else "radix-sort",
+            "metric": "events/sec (keyed ValueState counter, 10k keys)",
             "value": batch * steps / dt, "unit": "events/s", "ms_per_step": dt / steps * 1e3,
             "alerts": alerts, "keys": keys, "events_per_step": batch, "device": str(dev)}
 
@@ -439,7 +444,10 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--gpu-parse", action="store_true", help="config 1 on the GPU parse path")
-    ap.add_argument("--hashed-keys", action="store_true", help="config 4: hashed keyed state")
+    ap.add_argument("--hashed-keys", action="store_true",
+                    help="configs 2/4: hashed keyed state instead of dictionary-id slots")
+    ap.add_argument("--sort-path", action="store_true",
+                    help="config 2: the radix-sort rolling path instead of the sort-free one")
     ap.add_argument("--threads", type=int, default=4,
                     help="config 1 CPU path: parse threads (the reference job runs at P = 4)")
     a = ap.parse_args(argv)
@@ -448,7 +456,8 @@ def main(argv=None) -> int:
                     device="cpu" if a.device == "cuda" and not a.gpu_parse else a.device,
                     threads=a.threads)
     elif a.config == 2:
-        r = config2(a.steps, a.warmup, a.batch or (1 << 24), device=a.device)
+        r = config2(a.steps, a.warmup, a.batch or (1 << 24), device=a.device,
+                    dense_keys=not a.hashed_keys, sort_free=not a.sort_path)
     elif a.config == 4:
         r = config4(a.steps, a.warmup, a.batch or (1 << 24), device=a.device,
                     dense_keys=not a.hashed_keys)

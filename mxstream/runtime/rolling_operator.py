@@ -40,12 +40,15 @@ class KeyedRollingOperator:
                  max_keys: int = 1 << 16, parallelism: int | None = None,
                  max_parallelism: int = 128, batch_capacity: int = 1 << 20,
                  cap_log2: int | None = None, filter_prog: E.Program = E.EMPTY, emit_capacity: int | None = None,
-                 count_window: int = 0):
+                 count_window: int = 0, dense_keys: bool = False):
         """count_window = n > 0: tumbling count windows instead of a rolling aggregate
         (``keyBy(..).countWindow(n)`` with an incremental reduce/aggregate: GlobalWindows +
         PurgingTrigger(CountTrigger(n)), chapter2/README.md:78) -- a row is emitted when a key's
         open window reaches n elements (value = the window's aggregate; for avg the sum, the
-        count is n), and the state keeps each key's open window."""
+        count is n), and the state keeps each key's open window.
+
+        dense_keys: keys are dictionary ids in [0, max_keys) (columnar ingest, device-generated
+        ids): the slot IS the key id -- no hash probe. Single-rank GPU sort-free COUNT only."""
         self.device = K.resolve_device(device)
         self.comm = comm or LocalComm()
         self.world, self.rank = self.comm.world, self.comm.rank
@@ -60,7 +63,12 @@ class KeyedRollingOperator:
         self.filter_prog = filter_prog
         from .geometry import state_geometry
 
-        if self.world == 1 and cap_log2 is None:
+        self.dense = bool(dense_keys)
+        if self.dense:
+            if self.world != 1 or self.device.type != "cuda" or cap_log2 is not None:
+                raise ValueError("dense_keys: single-rank GPU rolling state only")
+            self.nsub, self.cap_log2 = 1, max(6, int(max_keys - 1).bit_length())
+        elif self.world == 1 and cap_log2 is None:
             # One rank: no keyBy buckets or LDS sub-tables to size for (the direct GPU path reads
             # the source columns), so a single table at <= 0.7 load keeps small key spaces small
             # enough for the sort-free LDS counter (rolling_hist: <= 16K slots ~ 11K keys).
@@ -91,6 +99,11 @@ class KeyedRollingOperator:
         # the sort path (A/B, tests).
         self.sort_free = True
         self._hist_tmp = None
+        if self.dense:
+            code, consts = filter_prog.as_args()
+            if not load().rolling_hist_supported(agg, self.count_window, self.nslots, code, consts):
+                raise ValueError("dense_keys: needs the sort-free path (COUNT, no count window, "
+                                 "a chain filter, <= 16K keys)")
 
     def _alloc(self, batch_capacity: int, slack: float = 1.5):
         self.batch_capacity = int(batch_capacity)
@@ -141,8 +154,8 @@ class KeyedRollingOperator:
         self.out_n.zero_()
         code, consts = self.filter_prog.as_args()
         cap = self.out_key.numel()
-        if self.sort_free and m.rolling_hist_supported(self.agg, self.count_window, self.nslots,
-                                                       code, consts):
+        if self.dense or (self.sort_free and m.rolling_hist_supported(
+                self.agg, self.count_window, self.nslots, code, consts)):
             # Counting formulation: per-chunk LDS histograms, a cross-chunk prefix seeded by the
             # stored counts, then tile-ranked emission (csrc/rolling_hist_hip.hip) -- no sort.
             need = m.rolling_hist_scratch_bytes(n, self.nslots)
@@ -153,7 +166,7 @@ class KeyedRollingOperator:
                                self._hist_tmp.data_ptr(), self._hist_tmp.numel(), code, consts,
                                self.out_key.data_ptr(), self.out_val.data_ptr(),
                                self.out_tag.data_ptr(), self.out_n.data_ptr(), cap,
-                               self.flags.data_ptr(), st)
+                               self.flags.data_ptr(), int(self.dense), st)
             return self._emit(to_host)
         self.n_buf.zero_()
         shift = max(1, int(n - 1).bit_length())
@@ -185,7 +198,8 @@ class KeyedRollingOperator:
         n = keys.numel()
         if n > self.batch_capacity:
             self._alloc(n, self.slack)
-        if self.direct_single_rank and self.world == 1 and self.device.type == "cuda" and n:
+        if ((self.direct_single_rank or self.dense) and self.world == 1
+                and self.device.type == "cuda" and n):
             return self._process_direct(keys, vals, n, to_host)
         dummy_ts = self._dummy_ts(n)  # keyed (non-windowed) records carry no timestamp
         while True:
@@ -269,6 +283,8 @@ class KeyedRollingOperator:
             raise RuntimeError("keyed state table full: a key found no free slot (raise max_keys)")
         if hf[0] & 4:
             raise ValueError("key ids -1 and -2 are reserved (the state tables' markers)")
+        if hf[0] & 16:
+            raise ValueError("dense keyed state: a key id is outside [0, max_keys)")
         return hf[2]
 
     def _emit(self, to_host: bool):
@@ -325,7 +341,14 @@ class KeyedRollingOperator:
             return
         dev = self.device
         keys = torch.from_numpy(np.ascontiguousarray(rows["key"])).to(dev)
-        slots = K.table_insert(keys, self.keys_g, nsub_log2=self.nsub_log2, cap_log2=self.cap_log2)
+        if self.dense:
+            if bool(((keys < 0) | (keys >= self.nslots)).any()):
+                raise RuntimeError("restore: a key id does not fit the dense table (raise max_keys)")
+            self.keys_g[keys] = keys
+            slots = keys
+        else:
+            slots = K.table_insert(keys, self.keys_g, nsub_log2=self.nsub_log2,
+                                   cap_log2=self.cap_log2)
         if bool((slots < 0).any()):
             raise RuntimeError("restore: keyed state does not fit the table (raise max_keys)")
         self.acc_g[slots] = torch.from_numpy(np.ascontiguousarray(rows["acc"])).to(dev)

@@ -129,6 +129,42 @@ def test_rolling_sort_free_count(gpu_device, n, nkeys, zipf, filt):
     assert res[("cuda", True, "state")] == res[("cpu", False, "state")]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("zipf", [0.0, 1.1])
+def test_rolling_dense_keys(gpu_device, zipf):
+    """Dictionary-id keys (slot = id, no probe) give the hashed CPU twin's rows and state; a
+    snapshot restores into a fresh dense operator; an id >= max_keys raises."""
+    n, nkeys = 200_003, 9_000
+    fp = E.compile_expr(E.var(E.VAR_COUNT) % 5 == 0)
+    ops = {"dense": KeyedRollingOperator(agg=K.AGG_COUNT, device=gpu_device, max_keys=nkeys,
+                                         batch_capacity=n, filter_prog=fp, dense_keys=True),
+           "cpu": KeyedRollingOperator(agg=K.AGG_COUNT, device="cpu", max_keys=nkeys,
+                                       batch_capacity=n, filter_prog=fp)}
+    res = {}
+    for name, op in ops.items():
+        d = op.device
+        got = []
+        for s in range(3):
+            keys = torch.empty(n, dtype=torch.int64, device=d)
+            K.gen_events(keys, torch.empty_like(keys), torch.empty_like(keys), seed=s, stream_id=0,
+                         idx0=s * n, nkeys=nkeys, ts_base=0, ts_span=1000, disorder=0, val_lo=0,
+                         val_span=10, zipf=zipf)
+            rows = op.process(keys, keys)
+            order = np.lexsort((rows.tags, rows.keys))
+            got.append((rows.keys[order].tolist(), rows.values[order].tolist()))
+        res[name] = got
+    assert res["dense"] == res["cpu"]
+    snap = ops["dense"].snapshot_state()
+    fresh = KeyedRollingOperator(agg=K.AGG_COUNT, device=gpu_device, max_keys=nkeys,
+                                 batch_capacity=n, filter_prog=fp, dense_keys=True)
+    fresh.restore_state(snap.columns, snap.meta)
+    for k in (0, 17, nkeys - 1):
+        assert fresh.state_of(k)[1] == ops["cpu"].state_of(k)[1]  # counts (COUNT keeps no acc)
+    bad = torch.full((10,), 1 << 20, dtype=torch.int64, device=gpu_device)
+    with pytest.raises(ValueError, match="dense"):
+        fresh.process(bad, bad)
+
+
 def _count_oracle(batches, agg, n):
     """Tumbling count windows per key (countWindow(n)): one row per n elements."""
     win, out = {}, {}
