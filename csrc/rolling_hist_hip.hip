@@ -92,6 +92,52 @@ struct RollVars {  // filter variables of the rolling epilogue (rolling_scan's n
 // now sits, and the device-scope CAS on that slot returns the real occupant (our key: found;
 // another key: probing continues after it). Device-scope loads of a 128 KB table hammered by
 // every CU are served past the per-XCD L2s.
+// A chain filter decoded once per workgroup into registers: the per-record evaluation is then an
+// unrolled sequence of uniform branches with hoisted operands, instead of re-reading the program
+// (op, arg) pairs from kernel-argument memory and branching on them for every record.
+constexpr int kChainOps = 8;
+struct ChainRegs {
+  int n;  // binops; -1 = longer than kChainOps (use expr_eval_chain)
+  int v0;
+  int op[kChainOps], src[kChainOps];  // src < 0: constant c[k]
+  double c[kChainOps];
+};
+
+__device__ __forceinline__ ChainRegs decode_chain(const ExprProg& p) {
+  ChainRegs r;
+  r.n = (p.ncode - 1) / 2;
+  r.v0 = p.code[1];
+  if (r.n > kChainOps) {
+    r.n = -1;
+    return r;
+  }
+#pragma unroll
+  for (int k = 0; k < kChainOps; ++k) {
+    const int i = 1 + 2 * k;  // operand pair i, binop pair i + 1
+    const bool on = k < r.n;
+    const int pop = on ? p.code[2 * i] : OP_CONST;
+    const int parg = on ? p.code[2 * i + 1] : 0;
+    r.op[k] = on ? p.code[2 * (i + 1)] : OP_ADD;
+    r.src[k] = pop == OP_CONST ? -1 : parg;
+    r.c[k] = pop == OP_CONST && on ? p.consts[parg] : 0.0;
+  }
+  return r;
+}
+
+template <class Vars>
+__device__ __forceinline__ double eval_chain_regs(const ChainRegs& r, const ExprProg& p,
+                                                  const Vars& vars) {
+  if (r.n < 0) return expr_eval_chain(p, vars);
+  double x = vars.get(r.v0);
+#pragma unroll
+  for (int k = 0; k < kChainOps; ++k) {
+    if (k >= r.n) break;
+    const double b = r.src[k] < 0 ? r.c[k] : vars.get(r.src[k]);
+    x = expr_binop(r.op[k], x, b);
+  }
+  return x;
+}
+
 __device__ __forceinline__ uint32_t probe_insert(uint64_t* keys, uint64_t key, uint32_t mask) {
   constexpr uint32_t W = 8;
   uint32_t s = slot_hash(key) & mask;
@@ -281,6 +327,7 @@ __global__ __launch_bounds__(kTile) void rolling_hist_emit_kernel(
   if (!filt.ncode && blockIdx.x == 0 && tid == 0) atomicAdd(out_n, n);  // rows = records
   __syncthreads();
   const uint64_t below = (1ull << lane) - 1ull;
+  const ChainRegs chain = decode_chain(filt);
   uint32_t pend_slot = kNoSlot, pend_cnt = 0;  // running-count update of the previous tile
   bool was_owner = false;                        // this thread's masks of the previous tile
   uint32_t buf = 0;
@@ -312,7 +359,7 @@ __global__ __launch_bounds__(kTile) void rolling_hist_emit_kernel(
       const uint64_t* col = M + id;
       uint64_t r[kTileWaves];
 #pragma unroll
-      for (int j = 0; j < kTileWaves; ++j) r[j] = col[j * kTile];
+      for (int j = 0; j < kTileWaves; ++j) r[j] = (ablate & 32u) ? 0 : col[j * kTile];
       uint32_t before = 0;
       uint64_t later = 0;
 #pragma unroll
@@ -329,11 +376,16 @@ __global__ __launch_bounds__(kTile) void rolling_hist_emit_kernel(
         pend_slot = slot;
         pend_cnt = pcount;
       }
-      emit = true;
+      emit = !(ablate & 16u);
       if (filt.ncode && !(ablate & 16u)) {
         const double key = !need_key ? 0.0 : dense ? (double)slot : (double)keys_g[slot];
         const RollVars rv{(double)pcount, (double)pcount, key, (double)pcount};
-        emit = expr_eval_chain(filt, rv) != 0.0;
+        if (ablate & 64u)
+          emit = pcount % 100000u == 0;  // timing reference only
+        else if (ablate & 128u)
+          emit = expr_eval_chain(filt, rv) != 0.0;
+        else
+          emit = eval_chain_regs(chain, filt, rv) != 0.0;
       }
     }
     buf ^= 1;
@@ -418,7 +470,8 @@ void rolling_hist(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
   hipStream_t s = (hipStream_t)stream;
   // MXS_RH_ABLATE (timing experiments only; results are wrong when set): 1 no probe past the
   // home window, 2 no histogram atomics, 4 owner = slot % 512, 8 no lane-mask ORs, 16 no filter
-  // evaluation.
+  // evaluation and no rows, 32 no lane-mask reads, 64 filter hard-coded as count % 100000 == 0,
+  // 128 interpretive chain evaluation (the pre-decode evaluator).
   static const uint32_t ablate = [] {
     const char* e = std::getenv("MXS_RH_ABLATE");
     return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;

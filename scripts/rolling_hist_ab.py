@@ -17,7 +17,8 @@ dev = torch.device("cuda", 0)
 filt = E.compile_expr(E.var(E.VAR_COUNT) % 100_000 == 0) if os.environ.get("FILT", "1") == "1" \
     else E.EMPTY
 op = KeyedRollingOperator(agg=K.AGG_COUNT, device=dev, max_keys=keys_n, batch_capacity=n,
-                          filter_prog=filt, emit_capacity=1 << 20)
+                          filter_prog=filt, emit_capacity=1 << 20,
+                          dense_keys=os.environ.get("DENSE", "0") == "1")
 op.sort_free = os.environ.get("SORT_FREE", "1") == "1"
 kt = torch.empty(n, dtype=torch.int64, device=dev)
 K.gen_events(kt, torch.empty_like(kt), torch.empty_like(kt), seed=2, stream_id=0, idx0=0,
@@ -32,5 +33,6 @@ for _ in range(steps):
 torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / steps
 print(json.dumps({"ablate": os.environ.get("MXS_RH_ABLATE", "0"), "sort_free": op.sort_free,
+                  "dense": op.dense, "filter": bool(filt.as_args()[0]),
                   "keys": keys_n, "nslots": op.nslots, "ms_per_step": dt * 1e3,
                   "events_per_s": n / dt}))

@@ -213,3 +213,69 @@ def test_vector_windows_invariant_to_world_size():
         assert merged[k][1] == c
         np.testing.assert_allclose(merged[k][0], v, rtol=1e-5, atol=1e-4)
     assert late == op.metrics.num_late_records_dropped
+
+
+# ---- keyed rolling state over gloo (ComputeCpuMax.java:26 keyBy(0).max(2), config 2) ---------
+def _rolling_batch(rank, step, per=2500, nkeys=400):
+    keys = torch.empty(per, dtype=torch.int64)
+    K.gen_events(keys, torch.empty_like(keys), torch.empty_like(keys), seed=23, stream_id=rank,
+                 idx0=step * per, nkeys=nkeys, ts_base=0, ts_span=1000, disorder=0, val_lo=-50,
+                 val_span=1000)
+    vals = torch.empty_like(keys)
+    K.gen_events(torch.empty_like(keys), torch.empty_like(keys), vals, seed=29, stream_id=rank,
+                 idx0=step * per, nkeys=nkeys, ts_base=0, ts_span=1000, disorder=0, val_lo=-50,
+                 val_span=1000)
+    return keys, vals
+
+
+def _rolling_worker(rank, world, port, agg, q):
+    from mxstream.runtime.rolling_operator import KeyedRollingOperator
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    op = KeyedRollingOperator(agg=agg, device="cpu", comm=TorchComm(), max_keys=400,
+                              batch_capacity=2500, cap_log2=8)
+    rows = {}
+    for step in range(STEPS):
+        r = op.process(*_rolling_batch(rank, step))
+        for key, val, tag in zip(r.keys.tolist(), r.values.tolist(), r.tags.tolist()):
+            rows[(step, tag >> 32, tag & 0xFFFFFFFF)] = (key, val)
+    q.put((rank, rows))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("agg", [K.AGG_MAX_I64, K.AGG_COUNT])
+def test_rolling_invariant_to_world_size(world, agg):
+    """Every record's post-update value over a real gloo all-to-all equals a single-rank run
+    over the step-wise concatenation (per key: step, then source rank, then arrival)."""
+    from mxstream.runtime.rolling_operator import KeyedRollingOperator
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rolling_worker, args=(r, world, port, agg, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    merged = {}
+    for _ in range(world):
+        _, rows = q.get(timeout=120)
+        assert not (set(rows) & set(merged))
+        merged.update(rows)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    per = 2500
+    ref_op = KeyedRollingOperator(agg=agg, device="cpu", max_keys=400, batch_capacity=per * world,
+                                  cap_log2=8)
+    ref = {}
+    for step in range(STEPS):
+        parts = [_rolling_batch(r, step) for r in range(world)]
+        r = ref_op.process(torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts]))
+        for key, val, tag in zip(r.keys.tolist(), r.values.tolist(), r.tags.tolist()):
+            i = tag & 0xFFFFFFFF
+            ref[(step, i // per, i % per)] = (key, val)
+    assert len(ref) == per * world * STEPS
+    assert merged == ref
