@@ -101,16 +101,28 @@ struct ChainRegs {
   int v0;
   int op[kChainOps], src[kChainOps];  // src < 0: constant c[k]
   double c[kChainOps];
+  // `x % c` by an integer constant 2 <= c < 2^32: round-up magic multiplier (m, l) for an exact
+  // u32 remainder when x is an integer in [0, 2^32) -- counts and key ids always are -- in 7
+  // integer ops instead of the library f64 fmod (frexp/ldexp/division: ~80 us per 16.7M rows).
+  uint32_t mag[kChainOps], dc[kChainOps];
+  int ml[kChainOps];
+  // Integer mode: the chain starts from a count variable and only takes remainders by those
+  // constants and compares with integer constants (`count % N == 0`, `count >= 1000`): the
+  // running value stays an exact u32/0-1 integer, so no f64 op is needed at all.
+  bool intmode;
+  int64_t ci[kChainOps];
 };
 
 __device__ __forceinline__ ChainRegs decode_chain(const ExprProg& p) {
   ChainRegs r;
   r.n = (p.ncode - 1) / 2;
   r.v0 = p.code[1];
+  r.intmode = false;
   if (r.n > kChainOps) {
     r.n = -1;
     return r;
   }
+  bool im_all = r.v0 == 0 || r.v0 == 1 || r.v0 == 5 || r.v0 == 6;  // count-valued for COUNT
 #pragma unroll
   for (int k = 0; k < kChainOps; ++k) {
     const int i = 1 + 2 * k;  // operand pair i, binop pair i + 1
@@ -120,8 +132,45 @@ __device__ __forceinline__ ChainRegs decode_chain(const ExprProg& p) {
     r.op[k] = on ? p.code[2 * (i + 1)] : OP_ADD;
     r.src[k] = pop == OP_CONST ? -1 : parg;
     r.c[k] = pop == OP_CONST && on ? p.consts[parg] : 0.0;
+    const double c = r.c[k];
+    const bool im = on && r.op[k] == OP_MOD && pop == OP_CONST && c >= 2.0 && c < 4294967296.0 &&
+                    c == trunc(c);
+    r.dc[k] = im ? (uint32_t)c : 0u;  // 0 = no integer fast path
+    r.ml[k] = im ? 32 - __clz((int)(r.dc[k] - 1)) : 1;
+    r.mag[k] = im ? (uint32_t)(((uint64_t)((1ull << r.ml[k]) - r.dc[k]) << 32) / r.dc[k] + 1) : 0u;
+    const bool cmp = r.op[k] >= OP_LT && r.op[k] <= OP_NE && pop == OP_CONST && c == trunc(c) &&
+                     fabs(c) < 9007199254740992.0;
+    r.ci[k] = cmp ? (int64_t)c : 0;
+    if (on && !im && !cmp) im_all = false;
   }
+  r.intmode = im_all;
   return r;
+}
+
+// Integer-mode chain (ChainRegs::intmode) on a count.
+__device__ __forceinline__ bool eval_chain_int(const ChainRegs& r, uint32_t count) {
+  int64_t x = count;  // stays in [0, 2^32): remainders of a u32 or 0/1 compare results
+#pragma unroll
+  for (int k = 0; k < kChainOps; ++k) {
+    if (k >= r.n) break;
+    const int64_t c = r.ci[k];
+    switch (r.op[k]) {
+      case OP_MOD: {
+        const uint32_t u = (uint32_t)x;
+        const uint32_t t = __umulhi(r.mag[k], u);
+        const uint32_t q = (t + ((u - t) >> 1)) >> (r.ml[k] - 1);
+        x = u - q * r.dc[k];
+        break;
+      }
+      case OP_LT: x = x < c; break;
+      case OP_LE: x = x <= c; break;
+      case OP_GT: x = x > c; break;
+      case OP_GE: x = x >= c; break;
+      case OP_EQ: x = x == c; break;
+      default: x = x != c; break;  // OP_NE
+    }
+  }
+  return x != 0;
 }
 
 template <class Vars>
@@ -132,6 +181,14 @@ __device__ __forceinline__ double eval_chain_regs(const ChainRegs& r, const Expr
 #pragma unroll
   for (int k = 0; k < kChainOps; ++k) {
     if (k >= r.n) break;
+    if (r.dc[k] && x >= 0.0 && x < 4294967296.0 && x == trunc(x)) {
+      // fmod(x, c) for integers is the integer remainder, +0 included (x >= 0).
+      const uint32_t u = (uint32_t)x;
+      const uint32_t t = __umulhi(r.mag[k], u);
+      const uint32_t q = (t + ((u - t) >> 1)) >> (r.ml[k] - 1);
+      x = (double)(u - q * r.dc[k]);
+      continue;
+    }
     const double b = r.src[k] < 0 ? r.c[k] : vars.get(r.src[k]);
     x = expr_binop(r.op[k], x, b);
   }
@@ -378,14 +435,15 @@ __global__ __launch_bounds__(kTile) void rolling_hist_emit_kernel(
       }
       emit = !(ablate & 16u);
       if (filt.ncode && !(ablate & 16u)) {
-        const double key = !need_key ? 0.0 : dense ? (double)slot : (double)keys_g[slot];
-        const RollVars rv{(double)pcount, (double)pcount, key, (double)pcount};
-        if (ablate & 64u)
+        if (ablate & 64u) {
           emit = pcount % 100000u == 0;  // timing reference only
-        else if (ablate & 128u)
-          emit = expr_eval_chain(filt, rv) != 0.0;
-        else
+        } else if (chain.intmode && !(ablate & 128u)) {
+          emit = eval_chain_int(chain, pcount);
+        } else {
+          const double key = !need_key ? 0.0 : dense ? (double)slot : (double)keys_g[slot];
+          const RollVars rv{(double)pcount, (double)pcount, key, (double)pcount};
           emit = eval_chain_regs(chain, filt, rv) != 0.0;
+        }
       }
     }
     buf ^= 1;
@@ -471,7 +529,7 @@ void rolling_hist(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
   // MXS_RH_ABLATE (timing experiments only; results are wrong when set): 1 no probe past the
   // home window, 2 no histogram atomics, 4 owner = slot % 512, 8 no lane-mask ORs, 16 no filter
   // evaluation and no rows, 32 no lane-mask reads, 64 filter hard-coded as count % 100000 == 0,
-  // 128 interpretive chain evaluation (the pre-decode evaluator).
+  // 128 no integer-mode chain (f64 evaluation of the decoded chain).
   static const uint32_t ablate = [] {
     const char* e = std::getenv("MXS_RH_ABLATE");
     return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
