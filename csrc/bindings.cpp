@@ -595,6 +595,10 @@ PYBIND11_MODULE(_mxs_native, m) {
                                  intptr_t out) {
     cpu::segment_median(P<int64_t>(heads), nseg, total, P<uint64_t>(ord), P<double>(out));
   });
+  m.def("gpu_set_rehash", [](intptr_t old, int64_t n_old, intptr_t neu, uint32_t new_mask,
+                             intptr_t stream) {
+    gpu::set_rehash(P<uint64_t>(old), n_old, P<uint64_t>(neu), new_mask, stream);
+  });
   m.def("gpu_set_erase", [](intptr_t set, uint32_t mask, intptr_t keys, int64_t n,
                             intptr_t stream) {
     gpu::set_erase(P<uint64_t>(set), mask, P<int64_t>(keys), n, stream);

@@ -2775,6 +2775,20 @@ __global__ __launch_bounds__(256) void set_erase_kernel(uint64_t* __restrict__ s
   }
 }
 
+// Grow / compact the device spill set without a host round trip: every live key of the old
+// set (not empty, not a tombstone) is re-inserted into the fresh, larger set. The old set holds
+// exactly the host store's keys (inserted by the lookup/evict kernels, erased on release), so
+// the result equals a rebuild from the store, including keys whose host insert is still queued.
+__global__ __launch_bounds__(256) void set_rehash_kernel(const uint64_t* __restrict__ old,
+                                                         int64_t n_old, uint64_t* __restrict__ neu,
+                                                         uint32_t new_mask) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_old;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = old[i];
+    if (k < kTombKey) set_insert(neu, new_mask, k);
+  }
+}
+
 // Rebuild the slot table without tombstones: every live slot is re-inserted into fresh arrays
 // (same sub-table, new position) with its sessions, due time and last activity.
 __global__ __launch_bounds__(256) void session_rehash_kernel(
@@ -3583,6 +3597,14 @@ void session_rehash(int64_t nslots, int cap_log2, const uint64_t* keys_o, const 
   hipLaunchKernelGGL(session_rehash_kernel, dim3(grid_for(nslots, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, a, keys_o, reinterpret_cast<const SessRec*>(sess_o), due_o,
                      last_o, keys_n, reinterpret_cast<SessRec*>(sess_n), due_n, last_n, inserted);
+  HIP_CHECK(hipGetLastError());
+}
+
+void set_rehash(const uint64_t* old, int64_t n_old, uint64_t* neu, uint32_t new_mask,
+                intptr_t stream) {
+  if (n_old <= 0) return;
+  hipLaunchKernelGGL(set_rehash_kernel, dim3(grid_for(n_old, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, old, n_old, neu, new_mask);
   HIP_CHECK(hipGetLastError());
 }
 

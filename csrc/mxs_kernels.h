@@ -208,6 +208,9 @@ void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uin
 void segment_median_select(const int64_t* heads, int64_t nseg, int64_t total,
                            const uint64_t* ord, double* out, intptr_t stream);
 void set_erase(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, intptr_t stream);
+// Re-insert the live keys of a spill set into a fresh (empty-filled) set of new_mask + 1 entries.
+void set_rehash(const uint64_t* old, int64_t n_old, uint64_t* neu, uint32_t new_mask,
+                intptr_t stream);
 void session_rehash(int64_t nslots, int cap_log2, const uint64_t* keys_o, const int64_t* sess_o,
                     const int64_t* due_o, const int64_t* last_o, uint64_t* keys_n, int64_t* sess_n,
                     int64_t* due_n, int64_t* last_n, uint32_t* inserted, intptr_t stream);

@@ -102,29 +102,34 @@ class SessionStore {
     const int64_t* t = ts.data();
     const int64_t* v = vals.data();
     promote(k, n, wm);
-    std::vector<int64_t> idx(n);
-    for (int64_t i = 0; i < n; ++i) idx[i] = i;
-    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
-      return k[a] != k[b] ? k[a] < k[b] : t[a] < t[b];
-    });
+    // Sort the records themselves by (key, ts) (contiguous, no indirect compares): every
+    // aggregate is a commutative monoid, so the order of equal (key, ts) records is free.
+    struct KTV {
+      uint64_t k;
+      int64_t t, v;
+    };
+    std::vector<KTV> r(n);
+    for (int64_t i = 0; i < n; ++i) r[i] = KTV{(uint64_t)k[i], t[i], v[i]};
+    std::sort(r.begin(), r.end(),
+              [](const KTV& a, const KTV& b) { return a.k != b.k ? a.k < b.k : a.t < b.t; });
     int64_t late = 0;
     int64_t i = 0;
     while (i < n) {
-      const uint64_t key = (uint64_t)k[idx[i]];
+      const uint64_t key = r[i].k;
       int64_t j = i;
-      while (j < n && (uint64_t)k[idx[j]] == key) ++j;
-      int64_t r = i;
-      while (r < j) {
-        Session c{t[idx[r]], t[idx[r]] + gap_, agg_lift(agg_, (uint64_t)v[idx[r]]), 1u, 0u};
-        int64_t q = r + 1;
-        while (q < j && t[idx[q]] <= c.end) {  // intersects (touching merges)
-          c.end = std::max(c.end, t[idx[q]] + gap_);
-          c.acc = agg_combine(agg_, c.acc, agg_lift(agg_, (uint64_t)v[idx[q]]));
+      while (j < n && r[j].k == key) ++j;
+      int64_t q0 = i;
+      while (q0 < j) {
+        Session c{r[q0].t, r[q0].t + gap_, agg_lift(agg_, (uint64_t)r[q0].v), 1u, 0u};
+        int64_t q = q0 + 1;
+        while (q < j && r[q].t <= c.end) {  // intersects (touching merges)
+          c.end = std::max(c.end, r[q].t + gap_);
+          c.acc = agg_combine(agg_, c.acc, agg_lift(agg_, (uint64_t)r[q].v));
           c.cnt += 1;
           ++q;
         }
         late += merge_candidate(key, c, wm);
-        r = q;
+        q0 = q;
       }
       i = j;
     }
@@ -201,10 +206,12 @@ class SessionStore {
     std::vector<int64_t> okey, ostart, oend, oraw, ocnt, oref, released;
     std::vector<double> oval;
     while (!heap_.empty() && heap_.top().first <= wm) {
+      const int64_t due = heap_.top().first;
       const uint64_t key = heap_.top().second;
       heap_.pop();
       auto it = m_.find(key);
-      if (it == m_.end()) continue;
+      if (it == m_.end() || it->second.due != due) continue;  // stale entry
+      it->second.due = INT64_MAX;  // this entry is consumed
       auto& vec = it->second;
       std::vector<Session> keep;
       for (auto& s : vec) {
@@ -411,31 +418,37 @@ class SessionStore {
 
   // Merge candidate c into key's sessions; returns the number of late-dropped elements.
   int64_t merge_candidate(uint64_t key, Session c, int64_t wm) {
-    auto& vec = m_[key];
+    auto found = m_.find(key);
     Session merged = c;
     bool touched_existing = false;
-    std::vector<Session> rest;
-    for (auto& s : vec) {
-      if (merged.start <= s.end && merged.end >= s.start) {
-        merged.start = std::min(merged.start, s.start);
-        merged.end = std::max(merged.end, s.end);
-        merged.acc = agg_combine(agg_, s.acc, merged.acc);
-        merged.cnt += s.cnt;
-        merged.flags |= s.flags;
-        touched_existing = true;
-      } else {
-        rest.push_back(s);
+    if (found != m_.end()) {
+      // In-place compaction: sessions intersecting the candidate fold into it, the rest stay.
+      auto& vec = found->second;
+      size_t w = 0;
+      for (size_t r = 0; r < vec.size(); ++r) {
+        const Session& s = vec[r];
+        if (merged.start <= s.end && merged.end >= s.start) {
+          merged.start = std::min(merged.start, s.start);
+          merged.end = std::max(merged.end, s.end);
+          merged.acc = agg_combine(agg_, s.acc, merged.acc);
+          merged.cnt += s.cnt;
+          merged.flags |= s.flags;
+          touched_existing = true;
+        } else {
+          vec[w++] = s;
+        }
       }
+      vec.resize(w);
     }
     if (!touched_existing && cleanup_time(merged.end - 1) <= wm) {
-      if (vec.empty()) m_.erase(key);
+      if (found != m_.end() && found->second.empty()) m_.erase(found);
       return c.cnt;  // late: every window of these elements is already cleaned
     }
     // A fired session that grows (or a new session already past its end within lateness)
     // fires again at the next fire() with the watermark (EventTimeTrigger.onElement).
     if (merged.flags & 1u) merged.flags |= 2u;
-    rest.push_back(merged);
-    vec.swap(rest);
+    if (found == m_.end()) found = m_.emplace(key, Hot()).first;
+    found->second.push_back(merged);
     schedule(key);
     return 0;
   }
@@ -449,12 +462,19 @@ class SessionStore {
       const int64_t due = ((s.flags & 1u) && !(s.flags & 2u)) ? cleanup_time(maxts) : maxts;
       t = std::min(t, due);
     }
+    if (t == it->second.due) return;  // the key's heap entry already says t
+    it->second.due = t;
     heap_.push({t, key});
   }
 
   int64_t gap_, late_;
   int agg_;
-  std::unordered_map<uint64_t, std::vector<Session>> m_;
+  // A key's live sessions plus the due time of its one valid heap entry (schedule() pushes only
+  // when the due time changes; fire() skips popped entries whose time is not the key's due).
+  struct Hot : std::vector<Session> {
+    int64_t due = INT64_MAX;
+  };
+  std::unordered_map<uint64_t, Hot> m_;
   std::priority_queue<std::pair<int64_t, uint64_t>, std::vector<std::pair<int64_t, uint64_t>>,
                       std::greater<>>
       heap_;

@@ -103,7 +103,7 @@ class KeyedSessionOperator:
                  ooo_bound: int = 0, max_load: float = 0.7, idle_spill_ms: int | None = None,
                  spill_rows: int = 1 << 20, emit_capacity: int | None = None,
                  external_watermark: bool = False, host_budget_bytes: int | None = None,
-                 idle_timeout_steps: int | None = None):
+                 idle_timeout_steps: int | None = None, spill_set_log2: int = 16):
         if gap <= 0:
             raise ValueError("session gap must be positive")
         self.device = K.resolve_device(device)
@@ -162,7 +162,7 @@ class KeyedSessionOperator:
             #           [5] n_ovf_runs [6] fire n_out [7] evict rows [8] evicted [9] rehash ins
             self.ctr = torch.zeros(16, dtype=torch.int32, device=dev)
             self.late_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
-            self.spill_log2 = 16
+            self.spill_log2 = int(spill_set_log2)  # grows on the GPU (_rehash_spill_set)
             self.spill_set = torch.full((1 << self.spill_log2,), EMPTY_KEY, dtype=torch.int64,
                                         device=dev)
             self.set_used = 0  # occupied spill-set entries (keys + tombstones)
@@ -525,9 +525,25 @@ class KeyedSessionOperator:
         if self.set_used + extra <= cap // 2:
             return
         want = 4 * (self.store.num_keys() + extra)
-        self._rebuild_spill_set(max(16, _next_pow2(max(1, want)).bit_length() - 1))
+        self._rehash_spill_set(max(16, _next_pow2(max(1, want)).bit_length() - 1))
+
+    def _rehash_spill_set(self, log2: int) -> None:
+        """Grow the device spill set (dropping its tombstones) on the GPU: the live keys of the
+        old set are re-inserted into a fresh one (no host walk of the store, no H2D copy)."""
+        t0 = time.perf_counter()
+        old = self.spill_set
+        self.spill_log2 = log2
+        self.spill_set = torch.full((1 << log2,), EMPTY_KEY, dtype=torch.int64, device=self.device)
+        self.native.gpu_set_rehash(old.data_ptr(), old.numel(), self.spill_set.data_ptr(),
+                                   (1 << log2) - 1, self._st())
+        # Live keys of the set = the store's keys (+ keys evicted by a still-queued insert,
+        # which the worker adds to the store; num_keys() is an upper bound after the join).
+        self.set_used = self.store.num_keys()
+        self.spill_any = self.spill_any or self.set_used > 0
+        self.phase_s["spill.set_rebuild"] += time.perf_counter() - t0
 
     def _rebuild_spill_set(self, log2: int) -> None:
+        """Rebuild the device spill set from the host store's keys (restore)."""
         t0 = time.perf_counter()
         arr = self.store.spill_set(log2)
         self.spill_log2 = log2

@@ -207,3 +207,19 @@ def test_gpu_sessions_overflow_and_spill():
     a2, _ = engine(events, 50, 30_000, 5_000, device="cpu", batch=2000)
     assert a2 == b
     assert op.metrics.spilled_keys > 0 or op.metrics.overflow_keys > 0
+
+
+@pytest.mark.gpu
+def test_gpu_sessions_spill_set_grows_on_device():
+    # A 16-entry device spill set must grow (GPU rehash of its live keys, no host rebuild) while
+    # keys keep spilling and coming back; results equal the CPU store.
+    rng = np.random.default_rng(11)
+    n = 20_000
+    ts = np.sort(rng.integers(0, 200_000, n))
+    keys = rng.integers(0, 3000, n)
+    events = [(int(k), int(t), int(v)) for k, t, v in zip(keys, ts, rng.integers(0, 9, n))]
+    b, op = engine(events, 50, 30_000, 5_000, device="cuda", batch=2000, max_load=0.05,
+                   idle_spill_ms=2_000, cap_log2=6, spill_set_log2=4)
+    a2, _ = engine(events, 50, 30_000, 5_000, device="cpu", batch=2000)
+    assert a2 == b
+    assert op.metrics.spilled_keys > 8 and op.spill_log2 > 4
