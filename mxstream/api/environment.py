@@ -253,6 +253,11 @@ class StreamExecutionEnvironment:
 
         sinks = plan(self, list(self._sinks))
         job_id = secrets.token_hex(16)
+        if getattr(self, "world", 1) > 1:
+            # All ranks of a multi-process job share one job id (checkpoint directory).
+            from ..parallel.comm import init_distributed
+
+            job_id = init_distributed("cpu").broadcast_object(job_id, src=0)
         attempts = 0
         restore = None
         while True:

@@ -425,32 +425,57 @@ def owned_key_groups(rank: int, world: int, parallelism: int, max_parallelism: i
 # Host operators hold arbitrary Python values (user tuples, accumulators, timers), so their state
 # files are pickles written and read only by this engine (never files from elsewhere); keyed
 # state inside them is already partitioned by key group (HeapKeyedStateBackend.snapshot).
-def write_host_checkpoint(d: Path, *, job_id: str, checkpoint_id: int, states: dict[str, dict],
-                          extra: dict, kind: str = "checkpoint") -> None:
+def write_host_states(d: Path, states: dict[str, dict], rank: int = 0) -> dict[str, str]:
+    """One state file per operator of this rank (``op<i>-<rank>.state``); returns uid -> file."""
     import pickle
 
     d.mkdir(parents=True, exist_ok=True)
     files = {}
     for i, (node_id, st) in enumerate(states.items()):
-        name = f"op{i:03d}-0.state"  # uid -> file map lives in _metadata
+        name = f"op{i:03d}-{rank}.state"  # uid -> file map lives in _metadata
         tmp = d / (name + ".inprogress")
         with open(tmp, "wb") as f:
             pickle.dump(st, f, protocol=pickle.HIGHEST_PROTOCOL)
         os.replace(tmp, d / name)
         files[node_id] = name
-    _atomic_write_json(d / META, {"format": FORMAT, "type": kind, "job_id": job_id,
-                                  "checkpoint_id": checkpoint_id,
-                                  "timestamp_ms": int(time.time() * 1000), "host_operators": files,
-                                  "extra": extra})
+    return files
 
 
-def read_host_checkpoint(path: str | os.PathLike) -> tuple[dict, dict[str, dict]]:
+def write_host_checkpoint(d: Path, *, job_id: str, checkpoint_id: int, states: dict[str, dict],
+                          extra: dict, kind: str = "checkpoint",
+                          ranks: list[dict] | None = None) -> None:
+    """Single-process host checkpoint, or (``ranks``: every rank's ``{"host_operators",
+    "extra"}``, files already written by write_host_states) the metadata of a multi-rank one."""
+    files = write_host_states(d, states) if ranks is None else ranks[0]["host_operators"]
+    meta = {"format": FORMAT, "type": kind, "job_id": job_id, "checkpoint_id": checkpoint_id,
+            "timestamp_ms": int(time.time() * 1000), "host_operators": files,
+            "extra": extra if ranks is None else ranks[0]["extra"]}
+    if ranks is not None:
+        meta["world"] = len(ranks)
+        meta["ranks"] = ranks
+    _atomic_write_json(d / META, meta)
+
+
+def read_host_checkpoint(path: str | os.PathLike, rank: int = 0,
+                         world: int = 1) -> tuple[dict, dict[str, dict]]:
+    """Metadata (with this rank's ``extra``) and this rank's operator states. A multi-rank host
+    checkpoint restores at the world size that wrote it (host operator state is per subtask
+    set, not re-split by key group)."""
     import pickle
 
     d = Path(path)
     meta = read_metadata(d)
+    files = meta["host_operators"]
+    if "ranks" in meta or world > 1:
+        w = int(meta.get("world", 1))
+        if w != world:
+            raise ValueError(f"checkpoint {d} was written by {w} rank(s); restoring it needs the "
+                             f"same world size (got {world})")
+        if "ranks" in meta:
+            files = meta["ranks"][rank]["host_operators"]
+            meta = dict(meta, extra=meta["ranks"][rank]["extra"])
     states = {}
-    for node_id, name in meta["host_operators"].items():
+    for node_id, name in files.items():
         with open(d / name, "rb") as f:
-            states[node_id] = pickle.load(f)  # written by write_host_checkpoint above
+            states[node_id] = pickle.load(f)  # written by write_host_states above
     return meta, states

@@ -128,6 +128,7 @@ class Executor:
         self._trace = False
         self.comm = None
         self._wm_in: dict = {}  # keyed node -> latest watermark received from every rank
+        self._failure: Exception | None = None  # multi-rank: first operator failure of this rank
         if getattr(env, "world", 1) > 1:
             import os
 
@@ -197,17 +198,20 @@ class Executor:
                 op = self.ops[n.id]
                 if self.comm is not None:
                     items = self._exchange(n, items)
-                if not getattr(op, "accepts_columns", False):
-                    items = expand_columns(items)
-                if self.fault is not None and items:
-                    self._maybe_fault(n, items)
-                if items and self._trace:
-                    with trace.span(n.name, "operator"):
-                        out = op.process(items)
+                if self.comm is not None:
+                    # Multi-rank: a failing operator must not leave the other ranks blocked in
+                    # this pass's exchanges. The rank records the failure, keeps joining the
+                    # collectives with no work, and every rank learns it at the step's control
+                    # gather (_control) and fails together -> coordinated restart.
+                    if self._failure is not None:
+                        items = []
+                    try:
+                        out = self._run_op(n, op, items, now)
+                    except Exception as e:  # noqa: BLE001 -- re-raised by _control
+                        self._failure = e
+                        out = []
                 else:
-                    out = op.process(items) if items else []
-                if now is not None:
-                    out.extend(op.on_processing_time(now))
+                    out = self._run_op(n, op, items, now)
                 if items or out:
                     c = self._counts.setdefault(n.id, {"numRecordsIn": 0, "numRecordsOut": 0})
                     c["numRecordsIn"] += rows_in(items)
@@ -220,6 +224,39 @@ class Executor:
                     inbox.setdefault((c.id, n.id), []).extend(side)
                 else:
                     inbox.setdefault((c.id, n.id), []).extend(out)
+
+    def _run_op(self, n: Transformation, op, items: list, now: int | None) -> list:
+        from .columnar import expand_columns
+
+        if not getattr(op, "accepts_columns", False):
+            items = expand_columns(items)
+        if self.fault is not None and items:
+            self._maybe_fault(n, items)
+        if items and self._trace:
+            with trace.span(n.name, "operator"):
+                out = op.process(items)
+        else:
+            out = op.process(items) if items else []
+        if now is not None:
+            out.extend(op.on_processing_time(now))
+        return out
+
+    def _control(self, want_ckpt: bool) -> bool:
+        """End-of-step agreement between ranks: a failure anywhere fails every rank (the
+        restart strategy then restarts all of them from the same checkpoint), and a checkpoint
+        is taken when any rank's interval elapsed (ranks' clocks need not agree)."""
+        if self.comm is None:
+            return want_ckpt
+        got = self.comm.all_gather_object(
+            (bool(want_ckpt), None if self._failure is None else
+             f"{type(self._failure).__name__}: {self._failure}"))
+        failed = [(r, f) for r, (_, f) in enumerate(got) if f is not None]
+        if failed:
+            if self._failure is not None:
+                raise self._failure
+            raise JobExecutionException(f"Job '{self.job_name}' failed on rank(s) "
+                                        f"{[r for r, _ in failed]}: {failed[0][1]}")
+        return any(w for w, _ in got)
 
     # ---- multi-rank exchange ---------------------------------------------------------------
     def _exchange(self, n: Transformation, items: list) -> list:
@@ -284,25 +321,37 @@ class Executor:
         return CheckpointStorage(root, self.job_id)
 
     def _checkpoint(self, finished: dict) -> None:
-        from .checkpoint import write_host_checkpoint
+        from .checkpoint import write_host_checkpoint, write_host_states
 
         t0 = time.perf_counter()
         storage = self._storage()
         storage.init_job_dirs()
         n = self._next_ckpt
         states = {self._uid(nd): self.ops[nd.id].snapshot() for nd in self.nodes if nd.id in self.ops}
-        write_host_checkpoint(storage.checkpoint_dir(n), job_id=storage.job_id, checkpoint_id=n,
-                              states=states, extra={
-                                  "clock": self.clock() if isinstance(self.clock, ManualClock) else None,
-                                  "rr": [[self._uid(self._node[a]), self._uid(self._node[b]), v]
-                                         for (a, b), v in self._rr.items()],
-                                  "finished": {self._uid(nd): finished[nd.id] for nd in self.nodes
-                                               if nd.id in finished},
-                                  "nodes": {self._uid(nd): nd.name for nd in self.nodes}})
-        for old in storage.completed_checkpoints()[:-max(1, self.env.checkpoint_config.max_retained)]:
-            import shutil
+        extra = {
+            "clock": self.clock() if isinstance(self.clock, ManualClock) else None,
+            "rr": [[self._uid(self._node[a]), self._uid(self._node[b]), v]
+                   for (a, b), v in self._rr.items()],
+            "finished": {self._uid(nd): finished[nd.id] for nd in self.nodes if nd.id in finished},
+            "nodes": {self._uid(nd): nd.name for nd in self.nodes}}
+        d = storage.checkpoint_dir(n)
+        if self.comm is None:
+            write_host_checkpoint(d, job_id=storage.job_id, checkpoint_id=n, states=states,
+                                  extra=extra)
+        else:
+            # Every rank writes its own state files; rank 0 completes the checkpoint (_metadata)
+            # once all of them have, so a crash mid-write leaves no completed checkpoint.
+            files = write_host_states(d, states, self.comm.rank)
+            ranks = self.comm.all_gather_object({"host_operators": files, "extra": extra})
+            if self.comm.rank == 0:
+                write_host_checkpoint(d, job_id=storage.job_id, checkpoint_id=n, states={},
+                                      extra=extra, ranks=ranks)
+            self.comm.barrier()
+        if self.comm is None or self.comm.rank == 0:
+            for old in storage.completed_checkpoints()[:-max(1, self.env.checkpoint_config.max_retained)]:
+                import shutil
 
-            shutil.rmtree(old, ignore_errors=True)
+                shutil.rmtree(old, ignore_errors=True)
         self._next_ckpt += 1
         self.metrics["numberOfCompletedCheckpoints"] = self.metrics.get("numberOfCompletedCheckpoints", 0) + 1
         self.metrics["lastCheckpointDuration"] = (time.perf_counter() - t0) * 1e3
@@ -313,7 +362,8 @@ class Executor:
     def _restore(self, path, finished: dict) -> None:
         from .checkpoint import read_host_checkpoint
 
-        meta, states = read_host_checkpoint(path)
+        rank, world = (self.comm.rank, self.comm.world) if self.comm is not None else (0, 1)
+        meta, states = read_host_checkpoint(path, rank, world)
         names = meta["extra"]["nodes"]
         for nd in self.nodes:
             key = self._uid(nd)
@@ -416,7 +466,8 @@ class Executor:
                 self._push(inbox, now)
                 if wd is not None:
                     wd.beat()
-                if cfg.is_checkpointing_enabled() and self.clock() - last_ckpt >= cfg.interval_ms:
+                want = cfg.is_checkpointing_enabled() and self.clock() - last_ckpt >= cfg.interval_ms
+                if self._control(want):
                     self._checkpoint(finished)
                     last_ckpt = self.clock()
                 if reporter is not None:

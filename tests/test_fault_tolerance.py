@@ -98,3 +98,78 @@ def test_execute_from_savepoint(tmp_path):
     env.config.native = "off"
     env.execute_from_savepoint(path)
     assert out and set(map(str, out)) <= set(map(str, full))
+
+
+# ---- multi-rank: one rank fails, every rank restarts from the same checkpoint ------------------
+def _mr_worker(rank, world, port, root, fault_rank, q):
+    import os
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        out = []
+        env = StreamExecutionEnvironment(4, clock=ManualClock(0))
+        env.config.native = "off"
+        env.config.fault_injection = "Window:60" if rank == fault_rank else None
+        env.set_stream_time_characteristic(TimeCharacteristic.EventTime)
+        if root is not None:
+            env.enable_checkpointing(500)
+            env.set_state_backend(FsStateBackend(root))
+            env.set_restart_strategy(RestartStrategies.fixed_delay_restart(2, 0))
+        (env.from_timed_collection(_events())
+         .assign_timestamps_and_watermarks(
+             BoundedOutOfOrdernessTimestampExtractor(Time.milliseconds(100), extractor=lambda e: e[2]))
+         .map(lambda e: Tuple2(e[0], e[1]))
+         .key_by(0)
+         .time_window(Time.milliseconds(1000))
+         .reduce(lambda a, b: Tuple2(a.f0, a.f1 + b.f1))
+         .collect(out))
+        res = env.execute("ft-multirank")
+        q.put((rank, [str(x) for x in out], dict(res.metrics), None))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, [], {}, repr(e)))
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def _run_ranks(world, root, fault_rank):
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_mr_worker, args=(r, world, port, root, fault_rank, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    errs = [e for *_, e in res if e]
+    assert not errs, errs
+    return res
+
+
+def test_multirank_failure_restarts_every_rank_from_checkpoint(tmp_path):
+    import os
+
+    for k in ("RANK", "WORLD_SIZE"):
+        os.environ.pop(k, None)
+    clean = _run_ranks(2, None, None)
+    got = _run_ranks(2, str(tmp_path), 1)  # rank 1's window operator fails mid-stream
+    for _, _, m, _ in got:
+        assert m["numRestarts"] == 1  # the healthy rank restarted too
+        assert m["restoredCheckpointId"] >= 1
+    c_clean = Counter(x for _, out, _, _ in clean for x in out)
+    c_got = Counter(x for _, out, _, _ in got for x in out)
+    assert len(c_clean) > 10 and set(c_got) == set(c_clean)
+    assert all(c_got[k] >= v for k, v in c_clean.items())  # at-least-once sink
+    meta = read_metadata(got[0][2]["lastCheckpointPath"])
+    assert meta["world"] == 2 and len(meta["ranks"]) == 2
