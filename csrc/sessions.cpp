@@ -198,6 +198,47 @@ class SessionStore {
     }
   }
 
+  // Hand keys back to the HBM tier: every listed key with at most `max_sess` live sessions
+  // leaves the store (hot sessions and cold rows; rows past cleanup at `wm` are dropped).
+  // Returns its sessions as columns grouped by key (keys ascending) plus "moved": every listed
+  // key that is no longer in the store (its spill-set entry can go). Keys with more sessions
+  // than an HBM slot holds stay here.
+  py::dict extract(py::array_t<int64_t, py::array::c_style> keys, int64_t wm, int64_t max_sess) {
+    const int64_t n = keys.size();
+    promote(keys.data(), n, wm);
+    std::vector<uint64_t> want((const uint64_t*)keys.data(), (const uint64_t*)keys.data() + n);
+    std::sort(want.begin(), want.end());
+    want.erase(std::unique(want.begin(), want.end()), want.end());
+    std::vector<int64_t> k, st, en, ac, cn, fl, moved;
+    for (uint64_t key : want) {
+      auto it = m_.find(key);
+      if (it == m_.end()) {
+        moved.push_back((int64_t)key);
+        continue;
+      }
+      if ((int64_t)it->second.size() > max_sess) continue;
+      for (const Session& x : it->second) {
+        k.push_back((int64_t)key);
+        st.push_back(x.start);
+        en.push_back(x.end);
+        ac.push_back((int64_t)x.acc);
+        cn.push_back(x.cnt);
+        fl.push_back(x.flags);
+      }
+      m_.erase(it);  // its heap entries turn stale
+      moved.push_back((int64_t)key);
+    }
+    py::dict d;
+    d["key"] = to_np(k);
+    d["start"] = to_np(st);
+    d["end"] = to_np(en);
+    d["acc"] = to_np(ac);
+    d["cnt"] = to_np(cn);
+    d["flags"] = to_np(fl);
+    d["moved"] = to_np(moved);
+    return d;
+  }
+
   // Fire / clean up everything the watermark allows. Returns columns of emitted rows plus the
   // keys that left the store ("released").
   py::dict fire(int64_t wm, std::vector<int32_t> map_code, std::vector<double> map_consts,
@@ -497,6 +538,7 @@ void bind_sessions(py::module_& m) {
            py::arg("accs"), py::arg("cnts"), py::arg("flags"), py::arg("cold") = false,
            py::call_guard<py::gil_scoped_release>())
       .def("merge_runs", &SessionStore::merge_runs)
+      .def("extract", &SessionStore::extract)
       .def("fire", &SessionStore::fire)
       .def("spill_set", &SessionStore::spill_set)
       .def("contains", &SessionStore::contains)

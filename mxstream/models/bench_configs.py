@@ -193,7 +193,7 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
 
 def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_000,
             drift: int = 400_000, table_keys: int = 4_000_000, device: str = "cuda",
-            revisit: float = 0.0) -> dict:
+            revisit: float = 0.0, promote: bool = True) -> dict:
     """Session windows (gap 5 s, 30 s allowed lateness) over a drifting active key set: each step
     draws events from `active` consecutive key ids whose window advances by `drift` ids, so keys
     go idle and their sessions close. The HBM slot table holds `table_keys` keys; idle keys whose
@@ -210,6 +210,7 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
                               max_keys=table_keys, batch_capacity=batch, ooo_bound=1_000,
                               idle_spill_ms=gap + 2 * span, spill_rows=1 << 22,
                               filter_prog=E.compile_expr(E.var(E.VAR_RESULT) > 1.5 * exp_sum))
+    op.promote_spilled = promote
     kt = torch.empty(batch, dtype=torch.int64, device=dev)
     tt = torch.empty_like(kt)
     vt = torch.empty_like(kt)
@@ -251,6 +252,8 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
             "late_dropped": mt.num_late_records_dropped - m0["num_late_records_dropped"],
             "spilled_keys": mt.spilled_keys - m0["spilled_keys"],
             "records_to_host": mt.records_to_host - m0["records_to_host"],
+            "records_promoted": mt.records_promoted - m0["records_promoted"],
+            "promoted_keys": mt.promoted_keys - m0["promoted_keys"],
             "overflow_keys": mt.overflow_keys - m0["overflow_keys"],
             "host_store_bytes": op.host_bytes(), "resident_keys": op.resident_keys() if op.gpu else 0,
             "hbm_state_bytes": op.state_bytes() - op.host_bytes(), "events_per_step": batch,
@@ -437,6 +440,8 @@ def main(argv=None) -> int:
     ap.add_argument("--dim", type=int, default=32, help="config 6: metric vector width")
     ap.add_argument("--valu", action="store_true", help="config 6: VALU instead of MFMA reduce")
     ap.add_argument("--zipf", type=float, default=0.0, help="config 6: power-law key skew")
+    ap.add_argument("--host-fold", action="store_true",
+                    help="config 5: fold records of spilled keys in host DRAM (no promotion to HBM)")
     ap.add_argument("--revisit", type=float, default=0.0,
                     help="config 5: fraction of events for spilled (long idle) keys")
     ap.add_argument("--steps", type=int, default=20)
@@ -469,7 +474,8 @@ def main(argv=None) -> int:
         r = config6(a.steps, a.warmup, a.batch or (1 << 24), dim=a.dim, device=a.device,
                     mfma=not a.valu, zipf=a.zipf)
     else:
-        r = config5(a.steps, a.warmup, a.batch or (1 << 24), device=a.device, revisit=a.revisit)
+        r = config5(a.steps, a.warmup, a.batch or (1 << 24), device=a.device, revisit=a.revisit,
+                    promote=not a.host_fold)
     print(json.dumps(r), flush=True)
     return 0
 

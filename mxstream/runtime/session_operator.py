@@ -87,6 +87,8 @@ class SessionMetrics:
     spilled_keys: int = 0
     freed_slots: int = 0
     rehashes: int = 0
+    promoted_keys: int = 0      # spilled keys handed back to HBM (records arrived for them)
+    records_promoted: int = 0   # records of those keys folded on the GPU instead of the host
     current_watermark: int = I64_MIN
     steps: int = 0
     extra: dict = field(default_factory=dict)
@@ -141,6 +143,9 @@ class KeyedSessionOperator:
         self.kg_dest = torch.tensor(kgd, dtype=torch.int32, device=dev)
         self.nbuckets = self.world << self.nsub_log2
         self.stats = K.new_stats(dev)
+        self.kg_zero = torch.zeros(max_parallelism, dtype=torch.int32, device=dev)  # refold: local
+        # Spilled keys that receive records return to HBM (False: fold them in host DRAM).
+        self.promote_spilled = True
         self.local_maxts = torch.full((1,), I64_MIN, dtype=torch.int64, device=dev)
         self.red = torch.zeros(K.RED_WORDS, dtype=torch.int64, device=dev)
         self._alloc(batch_capacity)
@@ -360,17 +365,35 @@ class KeyedSessionOperator:
 
     def _fold_gpu(self, tbase: int, wm: int, tspan: int) -> None:
         """tspan: the step's largest ts - tbase over all ranks (sizes the sort key's time bits)."""
-        m, st, c = self.native, self._st(), self.ctr
         tbits = min(32, max(1, int(tspan).bit_length()))  # (no records: tspan is meaningless)
-        sbits = self.nslots.bit_length()  # one spare bit: valid keys stay below the sentinel
         if self._live_estimate > 0.9 * self.nslots:
             self._join_spill()
             # Sub-tables may fill up: room in the spill set for every key the lookup may divert.
             self._ensure_spill_capacity(self.batch_capacity)
-        c[:7].zero_()  # c[7:9] may still be read by the spill worker
+        h, total = self._fold_recs(self.recv, self.recv_counts, self.world, tbase, wm, tbits,
+                                   self.bucket_cap)
+        self._join_spill()  # the host store must hold last step's spilled rows
+        late = int(self.late_cnt.item()) if total else 0
+        n_host = h[2]
+        # Overflow runs first: the refold below reuses the overflow buffers.
+        late += self._overflow_runs(h, wm)
+        if n_host and self.promote_spilled:
+            n_host, late2 = self._promote_and_refold(n_host, tbase, wm, tbits)
+            late += late2
+        if n_host:
+            self._host_fold(n_host, tbase, wm)
+        self.metrics.num_late_records_dropped += late
+
+    def _fold_recs(self, recs, counts, nsrc: int, tbase: int, wm: int, tbits: int,
+                   bucket_cap: int):
+        """Lookup -> (slot | ts) radix sort -> ordered session merge of bucketed records.
+        Returns the host counters c[:6] and the number of looked-up records."""
+        m, st, c = self.native, self._st(), self.ctr
+        sbits = self.nslots.bit_length()  # one spare bit: valid keys stay below the sentinel
+        c[:7].zero_()
         self.late_cnt.zero_()
-        m.gpu_session_lookup(self.recv.data_ptr(), self.recv_counts.data_ptr(), self.world,
-                             self.nsub, self.bucket_cap, self.cap_log2, self.keys_g.data_ptr(),
+        m.gpu_session_lookup(recs.data_ptr(), counts.data_ptr(), nsrc,
+                             self.nsub, bucket_cap, self.cap_log2, self.keys_g.data_ptr(),
                              self.spill_set.data_ptr(), self.spill_set.numel() - 1,
                              int(self.spill_any), self.sort_key.data_ptr(), self.vals_buf.data_ptr(),
                              c[0:1].data_ptr(), self.host_recs.data_ptr(), c[2:3].data_ptr(),
@@ -395,32 +418,114 @@ class KeyedSessionOperator:
                                 self.ovf_rows.data_ptr(), c[5:6].data_ptr(), self.ovf_cap, st)
         with self._phase("fold_gpu.sync"):
             h = c[:6].cpu().tolist()
-        self._join_spill()  # the host store must hold last step's spilled rows
-        n_host, n_ovf, n_runs = h[2], h[4], h[5]
-        late = int(self.late_cnt.item()) if total else 0
-        if n_host:
-            if n_host > self.host_cap:
-                raise RuntimeError("host diversion buffer overflow")
-            r = self.host_recs[: n_host * K.REC_WORDS].view(-1, K.REC_WORDS).cpu().numpy()
-            t = (r[:, 2] & 0xFFFFFFFF) + tbase
-            late += int(self.store.process(r[:, 0].copy(), t, r[:, 1].copy(), wm))
-            self.metrics.records_to_host += n_host
-            self.set_used += n_host  # upper bound on keys the lookup added (full sub-tables)
-            self.spill_any = True
-            self._ensure_spill_capacity(0)
-        if n_ovf:
-            if n_runs > self.ovf_cap:
-                raise RuntimeError("session overflow-run buffer too small")
-            slots = self.ovf_slots[:n_ovf]
-            okeys = self.keys_g[slots].cpu().numpy()
-            slot_key = dict(zip(slots.cpu().tolist(), okeys.tolist()))
-            self._evict(slots=slots)
-            rows = self.ovf_rows.view(5, self.ovf_cap)[:, :n_runs].cpu().numpy()
-            rk = np.array([slot_key[s] for s in rows[0].tolist()], dtype=np.int64)
-            late += int(self.store.merge_runs(rk, rows[1].copy(), rows[2].copy(), rows[3].copy(),
-                                              rows[4].copy(), wm))
-            self.metrics.overflow_keys += n_ovf
-        self.metrics.num_late_records_dropped += late
+        if h[2] > self.host_cap:
+            raise RuntimeError("host diversion buffer overflow")
+        return h, total
+
+    def _diverted(self, n_host: int, tbase: int):
+        r = self.host_recs[: n_host * K.REC_WORDS].view(-1, K.REC_WORDS)
+        return r[:, 0], (r[:, 2] & 0xFFFFFFFF) + tbase, r[:, 1]
+
+    def _host_fold(self, n_host: int, tbase: int, wm: int) -> None:
+        """Records of keys that live in host DRAM: folded by the host store."""
+        k, t, v = (x.cpu().numpy() for x in self._diverted(n_host, tbase))
+        self.metrics.num_late_records_dropped += int(self.store.process(k.copy(), t, v.copy(), wm))
+        self.metrics.records_to_host += n_host
+        self.set_used += n_host  # upper bound on keys the lookup added (full sub-tables)
+        self.spill_any = True
+        self._ensure_spill_capacity(0)
+
+    def _promote_and_refold(self, n_host: int, tbase: int, wm: int, tbits: int):
+        """Spilled keys that received records come back to HBM: their sessions leave the host
+        store (store.extract), are written into freshly inserted slots, the keys leave the
+        device spill set, and their records are re-partitioned and folded by the same GPU
+        lookup/sort/merge as resident keys (instead of a per-record host fold). Keys with more
+        sessions than a slot holds, or whose sub-table is full, stay on the host path.
+        Returns (records still for the host tier, late-dropped)."""
+        with self._phase("promote"):
+            dk, dt, dv = (x.clone(memory_format=torch.contiguous_format)
+                          for x in self._diverted(n_host, tbase))
+            ex = self.store.extract(torch.unique(dk).cpu().numpy(), wm, K_SESS)
+            moved = ex["moved"]
+            keys = ex["key"]
+            dev = self.device
+            if len(keys):
+                uniq, first, counts = np.unique(keys, return_index=True, return_counts=True)
+                slots = K.table_insert(torch.from_numpy(uniq).to(dev), self.keys_g,
+                                       nsub_log2=self.nsub_log2, cap_log2=self.cap_log2).cpu().numpy()
+                bad = slots < 0
+                if bad.any():  # sub-table full: those keys' sessions go back to the store
+                    rb = np.repeat(bad, counts)
+                    self.store.insert(*(np.ascontiguousarray(ex[f][rb], dtype=np.int64) for f in
+                                        ("key", "start", "end", "acc", "cnt", "flags")), False)
+                    moved = np.setdiff1d(moved, uniq[bad])
+                ok = ~bad
+                if ok.any():
+                    ro = np.repeat(ok, counts)
+                    pos = (np.arange(len(keys)) - np.repeat(first, counts))[ro]
+                    srow = np.repeat(np.arange(len(uniq)), counts)[ro]
+                    nk = int(ok.sum())
+                    remap = np.cumsum(ok) - 1  # index among the inserted keys
+                    rec = np.zeros((nk, K_SESS, 4), dtype=np.int64)
+                    ri = remap[srow]
+                    rec[ri, pos, 0] = ex["start"][ro]
+                    rec[ri, pos, 1] = ex["end"][ro]
+                    rec[ri, pos, 2] = ex["acc"][ro]
+                    rec[ri, pos, 3] = (ex["cnt"][ro] & 0xFFFFFFFF) | (ex["flags"][ro] << 32)
+                    last = np.full(len(uniq), I64_MIN, dtype=np.int64)
+                    np.maximum.at(last, srow, ex["end"][ro] - self.gap)
+                    sl = torch.from_numpy(slots[ok]).to(dev)
+                    self.sess.view(self.nslots, K_SESS * 4)[sl] = \
+                        torch.from_numpy(rec.reshape(nk, K_SESS * 4)).to(dev)
+                    self.slot_due[sl] = I64_MIN  # the next fire sweep recomputes due times
+                    self.slot_last[sl] = torch.from_numpy(last[ok]).to(dev)
+            if len(moved):
+                mt = torch.from_numpy(np.ascontiguousarray(moved, dtype=np.int64)).to(dev)
+                self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
+                                          mt.data_ptr(), mt.numel(), self._st())
+            self.metrics.promoted_keys += len(moved)
+            # Re-partition the diverted records (local sub-tables only) and fold them.
+            # Private bucket buffers sized for these records (the exchange buffers must keep the
+            # same size on every rank, so they are never regrown locally).
+            per = n_host / self.nsub
+            cap = (int(per * 1.5 + 6 * math.sqrt(max(per, 1.0)) + 64) + 8 * 16 + 7) & ~7
+            while True:
+                words = self.nsub * cap * K.REC_WORDS
+                if getattr(self, "_rf_send", None) is None or self._rf_send.numel() < words:
+                    self._rf_send = torch.empty(words, dtype=torch.int64, device=dev)
+                    self._rf_cursor = torch.zeros(self.nsub, dtype=torch.int32, device=dev)
+                K.step_begin(self._rf_cursor, self.stats)
+                plan = K.PartitionPlan(max_parallelism=self.max_parallelism,
+                                       nsub_log2=self.nsub_log2, nranks=1, window_mode=1,
+                                       drop_late=0, hash_mode=0, bucket_cap=cap,
+                                       late_ts=I64_MIN, tbase=tbase, pane=1)
+                K.partition(dk, dt, dv, plan, self.kg_zero, self._rf_cursor, self._rf_send,
+                            self.stats)
+                if int(self._rf_cursor.max()) <= cap:
+                    break
+                cap *= 2  # a bucket overflowed (skewed keys): larger buckets, partition again
+            h, total = self._fold_recs(self._rf_send, self._rf_cursor, 1, tbase, wm, tbits, cap)
+            self.metrics.records_promoted += n_host - h[2]
+            late = int(self.late_cnt.item()) if total else 0
+            late += self._overflow_runs(h, wm)
+            return h[2], late
+
+    def _overflow_runs(self, h, wm: int) -> int:
+        """Keys whose merge produced more than kSess sessions move to the host tier."""
+        n_ovf, n_runs = h[4], h[5]
+        if not n_ovf:
+            return 0
+        if n_runs > self.ovf_cap:
+            raise RuntimeError("session overflow-run buffer too small")
+        slots = self.ovf_slots[:n_ovf]
+        okeys = self.keys_g[slots].cpu().numpy()
+        slot_key = dict(zip(slots.cpu().tolist(), okeys.tolist()))
+        self._evict(slots=slots)
+        rows = self.ovf_rows.view(5, self.ovf_cap)[:, :n_runs].cpu().numpy()
+        rk = np.array([slot_key[s] for s in rows[0].tolist()], dtype=np.int64)
+        self.metrics.overflow_keys += n_ovf
+        return int(self.store.merge_runs(rk, rows[1].copy(), rows[2].copy(), rows[3].copy(),
+                                         rows[4].copy(), wm))
 
     def _fire_gpu(self, wm: int) -> SessionRows:
         m, st, c = self.native, self._st(), self.ctr

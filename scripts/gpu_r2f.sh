@@ -12,4 +12,6 @@ timeout -k 10 300 python bench.py --zipf 1.2 > gpurun_out/bench_zipf.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python bench.py --steps 24 --warmup 6 > gpurun_out/bench_prof.log 2>&1 &&
 timeout -k 10 300 python -m mxstream.models.bench_configs --config 2 --steps 20 --warmup 5 > gpurun_out/cfg2.log 2>&1 &&
 timeout -k 10 300 python scripts/loopback_bench.py --world 8 > gpurun_out/loop8.log 2>&1
-echo "exit $?"
+rc=$?
+echo "exit $rc"
+exit $rc

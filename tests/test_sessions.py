@@ -223,3 +223,48 @@ def test_gpu_sessions_spill_set_grows_on_device():
     a2, _ = engine(events, 50, 30_000, 5_000, device="cpu", batch=2000)
     assert a2 == b
     assert op.metrics.spilled_keys > 8 and op.spill_log2 > 4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("promote", [True, False])
+def test_gpu_spilled_keys_return_to_hbm(promote):
+    # Keys go idle (spilled to host DRAM with fired sessions inside the lateness), then receive
+    # records again: with promotion their sessions come back to HBM slots and the records are
+    # folded on the GPU; without it the host store folds them. Both equal the CPU store.
+    rng = np.random.default_rng(5)
+    events = []
+    for rnd in range(6):  # each round: 300 keys active for 20 s, then idle
+        base = rnd * 20_000
+        for k in range(300):
+            for t in rng.integers(base, base + 20_000, 6):
+                events.append((k + 300 * (rnd % 2), int(t), int(rng.integers(0, 9))))
+    events.sort(key=lambda e: e[1])
+    kw = dict(max_load=0.05, idle_spill_ms=3_000, cap_log2=7)
+    b, op = engine_with(events, 5_000, 2_000, 30_000, promote=promote, device="cuda", batch=600, **kw)
+    a2, _ = engine(events, 5_000, 2_000, 30_000, device="cpu", batch=600)
+    assert a2 == b
+    assert op.metrics.spilled_keys > 0
+    if promote:
+        assert op.metrics.promoted_keys > 0 and op.metrics.records_promoted > 0
+    else:
+        assert op.metrics.records_to_host > 0
+
+
+def engine_with(events, gap, bound, lateness, *, promote, device, batch, **kw):
+    op = KeyedSessionOperator(gap=gap, lateness=lateness, agg=K.AGG_SUM_I64, device=device,
+                              max_keys=1 << 10, batch_capacity=max(batch, 64), ooo_bound=bound,
+                              **kw)
+    op.promote_spilled = promote
+    out = Counter()
+    for i in range(0, len(events), batch):
+        chunk = events[i:i + batch]
+        k = torch.tensor([e[0] for e in chunk], dtype=torch.int64, device=device)
+        t = torch.tensor([e[1] for e in chunk], dtype=torch.int64, device=device)
+        v = torch.tensor([e[2] for e in chunk], dtype=torch.int64, device=device)
+        for r in (op.process(k, t, v),):
+            for kk, s_, e_, rr, c in zip(r.keys, r.start, r.end, r.raw, r.counts):
+                out[(int(kk), int(s_), int(e_), int(rr), int(c))] += 1
+    r = op.finish()
+    for kk, s_, e_, rr, c in zip(r.keys, r.start, r.end, r.raw, r.counts):
+        out[(int(kk), int(s_), int(e_), int(rr), int(c))] += 1
+    return out, op
