@@ -595,6 +595,12 @@ PYBIND11_MODULE(_mxs_native, m) {
                                  intptr_t out) {
     cpu::segment_median(P<int64_t>(heads), nseg, total, P<uint64_t>(ord), P<double>(out));
   });
+  m.def("gpu_session_slot_insert", [](intptr_t keys, int64_t n, int nsub_log2, int cap_log2,
+                                      intptr_t keys_g, intptr_t slots, intptr_t ins,
+                                      intptr_t stream) {
+    gpu::session_slot_insert(P<uint64_t>(keys), n, nsub_log2, cap_log2, P<uint64_t>(keys_g),
+                             P<int64_t>(slots), P<uint32_t>(ins), stream);
+  });
   m.def("gpu_set_rehash", [](intptr_t old, int64_t n_old, intptr_t neu, uint32_t new_mask,
                              intptr_t stream) {
     gpu::set_rehash(P<uint64_t>(old), n_old, P<uint64_t>(neu), new_mask, stream);

@@ -2844,6 +2844,22 @@ __global__ __launch_bounds__(256) void table_insert_kernel(const uint64_t* __res
   }
 }
 
+// Session slot table insert for keys promoted back from host DRAM: the same tombstone-reusing
+// probe as the session lookup (sess_probe_insert), so a sub-table whose free slots are all
+// tombstones still takes the key. slot = -1 only if the sub-table has neither.
+__global__ __launch_bounds__(256) void session_slot_insert_kernel(
+    const uint64_t* __restrict__ keys, int64_t n, int nsub_log2, int cap_log2,
+    uint64_t* __restrict__ keys_g, int64_t* __restrict__ slots, uint32_t* __restrict__ inserted) {
+  const uint32_t mask = (1u << cap_log2) - 1;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t key = keys[i];
+    const uint64_t sub = sub_table_of(key, nsub_log2);
+    const uint32_t s = sess_probe_insert(keys_g + (sub << cap_log2), key, mask, inserted);
+    slots[i] = s == kNoSlot ? -1 : (int64_t)((sub << cap_log2) | s);
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Median of `process` windows (ComputeCpuMiddle.java:36-47): elements are radix-
 // sorted by (key, order-preserving value bits); one thread per key segment reads the middle
@@ -3628,6 +3644,14 @@ void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
   if (n <= 0) return;
   hipLaunchKernelGGL(table_insert_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, keys, n, nsub_log2, cap_log2, keys_g, slots);
+  HIP_CHECK(hipGetLastError());
+}
+
+void session_slot_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2,
+                         uint64_t* keys_g, int64_t* slots, uint32_t* inserted, intptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(session_slot_insert_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, keys, n, nsub_log2, cap_log2, keys_g, slots, inserted);
   HIP_CHECK(hipGetLastError());
 }
 

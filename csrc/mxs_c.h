@@ -101,6 +101,45 @@ MXS_API int mxs_rolling_process(mxs_rolling* r, const uint64_t* keys, const int6
 MXS_API int64_t mxs_rolling_num_rows(const mxs_rolling* r);
 MXS_API int64_t mxs_rolling_take_rows(mxs_rolling* r, mxs_rolling_row* out, int64_t cap);
 
+/* ---- keyed event-time session windows --------------------------------------------------------
+ * keyBy(k).window(EventTimeSessionWindows.withGap(gap)) with an incremental aggregate, allowed
+ * lateness (late-but-allowed elements merge into fired sessions and re-fire them) and a
+ * bounded-out-of-orderness watermark (chapter3/README.md:412-428). Host C++ session store (the
+ * CPU engine and host-DRAM tier of the GPU session operator, csrc/session_store.h). */
+typedef struct mxs_session_config {
+  int64_t gap_ms;           /* session gap */
+  int64_t lateness_ms;      /* allowed lateness */
+  int64_t ooo_bound_ms;     /* BoundedOutOfOrdernessTimestampExtractor bound */
+  int32_t agg;              /* MXS_AGG_* */
+  int32_t reserved;
+} mxs_session_config;
+
+typedef struct mxs_session_result {
+  uint64_t key;
+  int64_t start;            /* session [start, end) */
+  int64_t end;
+  double value;             /* aggregate result */
+  int64_t raw;              /* raw accumulator */
+  uint32_t count;           /* elements in the session */
+  int32_t refire;           /* 1: re-firing caused by late-but-allowed data */
+} mxs_session_result;
+
+typedef struct mxs_session mxs_session;
+
+MXS_API void mxs_session_config_default(mxs_session_config* cfg);
+MXS_API mxs_session* mxs_session_create(const mxs_session_config* cfg);
+MXS_API void mxs_session_destroy(mxs_session* s);
+/* One micro-batch (keys, event timestamps in ms, int64 values / f64 bit patterns). Elements are
+ * checked for lateness against the watermark before the batch; then the watermark advances
+ * (max ts - bound) and every session it passes fires. Results queue up until taken. */
+MXS_API int mxs_session_process(mxs_session* s, const uint64_t* keys, const int64_t* ts,
+                                const int64_t* vals, int64_t n);
+MXS_API int mxs_session_finish(mxs_session* s);
+MXS_API int64_t mxs_session_num_results(const mxs_session* s);
+MXS_API int64_t mxs_session_take_results(mxs_session* s, mxs_session_result* out, int64_t cap);
+MXS_API int64_t mxs_session_watermark(const mxs_session* s);
+MXS_API int64_t mxs_session_late_dropped(const mxs_session* s);
+
 MXS_API const char* mxs_last_error(void);
 MXS_API const char* mxs_version(void);
 

@@ -24,6 +24,7 @@
 #include "mxs_c.h"
 #include "mxs_check.h"
 #include "mxs_kernels.h"
+#include "session_store.h"
 
 namespace mxs {
 namespace {
@@ -780,6 +781,85 @@ int64_t mxs_rolling_take_rows(mxs_rolling* r, mxs_rolling_row* out, int64_t cap)
   }
   return n;
 }
+
+// ---- sessions ---------------------------------------------------------------------------------
+struct mxs_session {
+  explicit mxs_session(const mxs_session_config& c)
+      : store(c.gap_ms, c.lateness_ms, c.agg), bound(c.ooo_bound_ms), agg(c.agg) {
+    if (c.lateness_ms < 0 || c.ooo_bound_ms < 0) throw std::invalid_argument("negative lateness / bound");
+    if (c.agg < 0 || c.agg > MXS_AGG_AVG_I64) throw std::invalid_argument("unknown aggregate");
+  }
+  void fire_at(int64_t w) {
+    wm = w;
+    if (wm == INT64_MIN) return;
+    mxs::sess::SessionCore::FireOut o;
+    const mxs::ExprProg none = mxs::sess::SessionCore::prog(nullptr, 0, nullptr, 0);
+    store.fire(wm, none, none, o);
+    for (size_t i = 0; i < o.okey.size(); ++i)
+      results.push_back(mxs_session_result{(uint64_t)o.okey[i], o.ostart[i], o.oend[i], o.oval[i],
+                                           o.oraw[i], (uint32_t)o.ocnt[i], (int32_t)o.oref[i]});
+  }
+  void process(const uint64_t* k, const int64_t* t, const int64_t* v, int64_t n) {
+    // Same micro-batch order as the Python operator: fold against the old watermark, then fire
+    // at the advanced one (late data may re-open fired sessions without moving it).
+    late += store.process((const int64_t*)k, t, v, n, wm);
+    for (int64_t i = 0; i < n; ++i) maxts = std::max(maxts, t[i]);
+    const int64_t w = maxts == INT64_MIN ? INT64_MIN : maxts - bound;
+    fire_at(std::max(wm, w));
+  }
+  mxs::sess::SessionCore store;
+  int64_t bound, wm = INT64_MIN, maxts = INT64_MIN, late = 0;
+  int32_t agg;
+  std::deque<mxs_session_result> results;
+};
+
+void mxs_session_config_default(mxs_session_config* cfg) {
+  if (!cfg) return;
+  std::memset(cfg, 0, sizeof(*cfg));
+  cfg->gap_ms = 5000;
+  cfg->agg = MXS_AGG_SUM_I64;
+}
+
+mxs_session* mxs_session_create(const mxs_session_config* cfg) {
+  if (!cfg) {
+    mxs::g_err = "null config";
+    return nullptr;
+  }
+  mxs_session* s = nullptr;
+  if (guard([&] { s = new mxs_session(*cfg); }) != 0) return nullptr;
+  return s;
+}
+
+void mxs_session_destroy(mxs_session* s) { delete s; }
+
+int mxs_session_process(mxs_session* s, const uint64_t* keys, const int64_t* ts,
+                        const int64_t* vals, int64_t n) {
+  if (!s || (n > 0 && (!keys || !ts || !vals))) {
+    mxs::g_err = "null argument";
+    return -1;
+  }
+  return guard([&] { s->process(keys, ts, vals, n); });
+}
+
+int mxs_session_finish(mxs_session* s) {
+  if (!s) return -1;
+  return guard([&] { s->fire_at(INT64_MAX); });
+}
+
+int64_t mxs_session_num_results(const mxs_session* s) { return s ? (int64_t)s->results.size() : -1; }
+
+int64_t mxs_session_take_results(mxs_session* s, mxs_session_result* out, int64_t cap) {
+  if (!s || (cap > 0 && !out)) return -1;
+  int64_t n = 0;
+  while (n < cap && !s->results.empty()) {
+    out[n++] = s->results.front();
+    s->results.pop_front();
+  }
+  return n;
+}
+
+int64_t mxs_session_watermark(const mxs_session* s) { return s ? s->wm : INT64_MIN; }
+int64_t mxs_session_late_dropped(const mxs_session* s) { return s ? s->late : -1; }
 
 const char* mxs_last_error(void) { return mxs::g_err.c_str(); }
 const char* mxs_version(void) { return "mxstream-native 0.1 (gfx950)"; }

@@ -1,0 +1,498 @@
+// mxstream — host session-window store core (C++, no Python): shared by the pybind module
+// (csrc/sessions.cpp: CPU engine + spill tier of the GPU session operator) and the C ABI
+// (csrc/pipeline.cpp: mxs_session_*). Semantics: see csrc/sessions.cpp.
+#ifndef MXS_SESSION_STORE_H_
+#define MXS_SESSION_STORE_H_
+
+#include <algorithm>
+#include <cstring>
+#include <deque>
+#include <queue>
+#include <stdexcept>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+#include "mxs_common.h"
+
+namespace mxs {
+namespace sess {
+
+struct Session {
+  int64_t start, end;  // [start, end)
+  uint64_t acc;
+  uint32_t cnt;
+  uint32_t flags;      // bit0: fired, bit1: modified since firing
+};
+
+struct ColdChunk {
+  std::vector<uint64_t> key;
+  std::vector<int64_t> start, end;
+  std::vector<uint64_t> acc;
+  std::vector<uint32_t> cnt;  // 0 = row gone (promoted or discarded)
+  int64_t max_due = INT64_MIN;
+  size_t live = 0;
+  // Rows by key: promote() looks keys up by binary search or a merge join instead of probing a
+  // hash set with every cold row of the store.
+  std::vector<uint32_t> by_key;
+  uint64_t kmin = ~0ull, kmax = 0;
+
+  // Key range at sealing (O(n)); the sorted row index is built on the first promote() that
+  // reaches this chunk, so chunks that are never revisited never pay for it.
+  void seal() {
+    for (uint64_t k : key) {
+      kmin = k < kmin ? k : kmin;
+      kmax = k > kmax ? k : kmax;
+    }
+  }
+  void ensure_index() {
+    if (by_key.size() == key.size()) return;
+    // (key, row) pairs sorted contiguously: an index sort with key[] lookups in the comparator
+    // was 5x slower (random reads).
+    std::vector<std::pair<uint64_t, uint32_t>> kr(key.size());
+    for (size_t i = 0; i < kr.size(); ++i) kr[i] = {key[i], (uint32_t)i};
+    std::sort(kr.begin(), kr.end());
+    by_key.resize(kr.size());
+    for (size_t i = 0; i < kr.size(); ++i) by_key[i] = kr[i].second;
+  }
+};
+
+// Session rows as flat columns (key, start, end, acc, cnt, flags).
+struct Columns {
+  std::vector<int64_t> key, start, end, acc, cnt, flags;
+  void add(uint64_t k, int64_t s, int64_t e, uint64_t a, uint32_t c, uint32_t f) {
+    key.push_back((int64_t)k);
+    start.push_back(s);
+    end.push_back(e);
+    acc.push_back((int64_t)a);
+    cnt.push_back(c);
+    flags.push_back(f);
+  }
+};
+
+class SessionCore {
+ public:
+  SessionCore(int64_t gap, int64_t lateness, int agg) : gap_(gap), late_(lateness), agg_(agg) {
+    if (gap <= 0) throw std::invalid_argument("session gap must be > 0");
+  }
+
+  // Fold a batch (keys, ts, vals) with the current watermark `wm`; returns late-dropped count.
+  int64_t process(const int64_t* k, const int64_t* t, const int64_t* v, int64_t n, int64_t wm) {
+    promote(k, n, wm);
+    // Sort the records themselves by (key, ts) (contiguous, no indirect compares): every
+    // aggregate is a commutative monoid, so the order of equal (key, ts) records is free.
+    struct KTV {
+      uint64_t k;
+      int64_t t, v;
+    };
+    std::vector<KTV> r(n);
+    for (int64_t i = 0; i < n; ++i) r[i] = KTV{(uint64_t)k[i], t[i], v[i]};
+    std::sort(r.begin(), r.end(),
+              [](const KTV& a, const KTV& b) { return a.k != b.k ? a.k < b.k : a.t < b.t; });
+    int64_t late = 0;
+    int64_t i = 0;
+    while (i < n) {
+      const uint64_t key = r[i].k;
+      int64_t j = i;
+      while (j < n && r[j].k == key) ++j;
+      int64_t q0 = i;
+      while (q0 < j) {
+        Session c{r[q0].t, r[q0].t + gap_, agg_lift(agg_, (uint64_t)r[q0].v), 1u, 0u};
+        int64_t q = q0 + 1;
+        while (q < j && r[q].t <= c.end) {  // intersects (touching merges)
+          c.end = std::max(c.end, r[q].t + gap_);
+          c.acc = agg_combine(agg_, c.acc, agg_lift(agg_, (uint64_t)r[q].v));
+          c.cnt += 1;
+          ++q;
+        }
+        late += merge_candidate(key, c, wm);
+        q0 = q;
+      }
+      i = j;
+    }
+    return late;
+  }
+
+  // Merge pre-built runs (GPU overflow path): each is a candidate session.
+  int64_t merge_runs(const int64_t* keys, const int64_t* starts, const int64_t* ends,
+                     const int64_t* accs, const int64_t* cnts, int64_t n, int64_t wm) {
+    promote(keys, n, wm);
+    int64_t late = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      Session c{starts[i], ends[i], (uint64_t)accs[i], (uint32_t)cnts[i], 0u};
+      late += merge_candidate((uint64_t)keys[i], c, wm);
+    }
+    return late;
+  }
+
+  // Insert sessions evicted from HBM. Arrays: key, start, end, acc, cnt, flags. With `cold`,
+  // fired-and-unmodified sessions of keys without hot state go to one new cold chunk.
+  void insert(const int64_t* K, const int64_t* S, const int64_t* E, const int64_t* A,
+              const int64_t* C, const int64_t* F, int64_t n, bool cold) {
+    ColdChunk ch;
+    if (cold) {
+      ch.key.reserve(n);
+      ch.start.reserve(n);
+      ch.end.reserve(n);
+      ch.acc.reserve(n);
+      ch.cnt.reserve(n);
+    }
+    const bool no_hot = m_.empty();
+    for (int64_t i = 0; i < n; ++i) {
+      const uint64_t key = (uint64_t)K[i];
+      if (cold && F[i] == 1 && (no_hot || m_.find(key) == m_.end())) {
+        ch.key.push_back(key);
+        ch.start.push_back(S[i]);
+        ch.end.push_back(E[i]);
+        ch.acc.push_back((uint64_t)A[i]);
+        ch.cnt.push_back((uint32_t)C[i]);
+        ch.max_due = std::max(ch.max_due, cleanup_time(E[i] - 1));
+        continue;
+      }
+      m_[key].push_back(Session{S[i], E[i], (uint64_t)A[i], (uint32_t)C[i], (uint32_t)F[i]});
+      schedule(key);
+    }
+    if (!ch.key.empty()) {
+      ch.live = ch.key.size();
+      ch.seal();
+      cold_rows_ += ch.live;
+      cold_.push_back(std::move(ch));
+    }
+  }
+
+  // Hand keys back to the HBM tier: every listed key with at most `max_sess` live sessions
+  // leaves the store (hot sessions and cold rows; rows past cleanup at `wm` are dropped).
+  // Returns its sessions as columns grouped by key (keys ascending) plus "moved": every listed
+  // key that is no longer in the store (its spill-set entry can go). Keys with more sessions
+  // than an HBM slot holds stay here.
+  Columns extract(const int64_t* keys, int64_t n, int64_t wm, int64_t max_sess,
+                  std::vector<int64_t>* moved) {
+    std::vector<uint64_t> want((const uint64_t*)keys, (const uint64_t*)keys + n);
+    std::sort(want.begin(), want.end());
+    want.erase(std::unique(want.begin(), want.end()), want.end());
+    // Cold rows of the wanted keys come straight out of their chunks (no detour through the hot
+    // map); rows already past cleanup at `wm` are dropped, as a promote would.
+    std::vector<std::pair<uint64_t, Session>> cold;
+    if (cold_rows_ && !want.empty()) {
+      for (auto& ch : cold_) {
+        if (!ch.live || want.back() < ch.kmin || want.front() > ch.kmax) continue;
+        auto lo = std::lower_bound(want.begin(), want.end(), ch.kmin);
+        auto hi = std::upper_bound(lo, want.end(), ch.kmax);
+        if (lo == hi) continue;
+        ch.ensure_index();
+        auto take = [&](uint32_t r) {
+          if (!ch.cnt[r]) return;
+          if (cleanup_time(ch.end[r] - 1) > wm)
+            cold.push_back({ch.key[r], Session{ch.start[r], ch.end[r], ch.acc[r], ch.cnt[r], 1u}});
+          ch.cnt[r] = 0;
+          ch.live -= 1;
+          cold_rows_ -= 1;
+        };
+        for (auto it = lo; it != hi; ++it) {
+          auto p = std::lower_bound(ch.by_key.begin(), ch.by_key.end(), *it,
+                                    [&](uint32_t r, uint64_t k) { return ch.key[r] < k; });
+          for (; p != ch.by_key.end() && ch.key[*p] == *it; ++p) take(*p);
+        }
+      }
+      std::stable_sort(cold.begin(), cold.end(),
+                       [](const auto& a, const auto& b) { return a.first < b.first; });
+    }
+    Columns out;
+    size_t c = 0;
+    for (uint64_t key : want) {
+      const size_t c0 = c;
+      while (c < cold.size() && cold[c].first < key) ++c;  // (cannot happen: keys are wanted)
+      const size_t cb = c;
+      while (c < cold.size() && cold[c].first == key) ++c;
+      (void)c0;
+      auto it = m_.find(key);
+      const int64_t nhot = it == m_.end() ? 0 : (int64_t)it->second.size();
+      if (nhot + (int64_t)(c - cb) > max_sess) {  // stays on the host: cold rows turn hot
+        auto& vec = m_[key];
+        for (size_t q = cb; q < c; ++q) vec.push_back(cold[q].second);
+        schedule(key);
+        continue;
+      }
+      if (it != m_.end()) {
+        for (const Session& x : it->second) out.add(key, x.start, x.end, x.acc, x.cnt, x.flags);
+        m_.erase(it);  // its heap entries turn stale
+      }
+      for (size_t q = cb; q < c; ++q) {
+        const Session& x = cold[q].second;
+        out.add(key, x.start, x.end, x.acc, x.cnt, x.flags);
+      }
+      moved->push_back((int64_t)key);
+    }
+    return out;
+  }
+
+  // Fire / clean up everything the watermark allows. Returns columns of emitted rows plus the
+  // keys that left the store ("released").
+  struct FireOut {
+    std::vector<int64_t> okey, ostart, oend, oraw, ocnt, oref, released;
+    std::vector<double> oval;
+  };
+  void fire(int64_t wm, const ExprProg& mp, const ExprProg& fp, FireOut& o) {
+    auto& okey = o.okey;
+    auto& ostart = o.ostart;
+    auto& oend = o.oend;
+    auto& oraw = o.oraw;
+    auto& ocnt = o.ocnt;
+    auto& oref = o.oref;
+    auto& released = o.released;
+    auto& oval = o.oval;
+    while (!heap_.empty() && heap_.top().first <= wm) {
+      const int64_t due = heap_.top().first;
+      const uint64_t key = heap_.top().second;
+      heap_.pop();
+      auto it = m_.find(key);
+      if (it == m_.end() || it->second.due != due) continue;  // stale entry
+      it->second.due = INT64_MAX;  // this entry is consumed
+      auto& vec = it->second;
+      std::vector<Session> keep;
+      for (auto& s : vec) {
+        const int64_t maxts = s.end - 1;
+        if (maxts <= wm && (!(s.flags & 1u) || (s.flags & 2u))) {
+          double vars[kExprVars] = {0};
+          vars[0] = agg_result_f64(agg_, s.acc, s.cnt);
+          vars[1] = (double)s.cnt;
+          vars[2] = (double)s.start;
+          vars[3] = (double)s.end;
+          vars[4] = (double)key;
+          vars[5] = (double)(int64_t)s.acc;
+          vars[6] = mp.ncode ? expr_eval(mp, vars) : vars[0];
+          if (!fp.ncode || expr_eval(fp, vars) != 0.0) {
+            okey.push_back((int64_t)key);
+            ostart.push_back(s.start);
+            oend.push_back(s.end);
+            oval.push_back(vars[6]);
+            oraw.push_back((int64_t)s.acc);
+            ocnt.push_back(s.cnt);
+            oref.push_back((s.flags & 1u) ? 1 : 0);
+          }
+          s.flags = 1u;
+        }
+        if (cleanup_time(maxts) > wm) keep.push_back(s);  // not cleaned yet
+      }
+      if (keep.empty()) {
+        m_.erase(it);
+        released.push_back((int64_t)key);
+      } else {
+        vec.swap(keep);
+        schedule(key);
+      }
+    }
+    for (uint64_t key : pending_released_)
+      if (m_.find(key) == m_.end()) released.push_back((int64_t)key);
+    pending_released_.clear();
+    // Cold chunks: dropped as a whole once every row is past cleanup.
+    for (auto it = cold_.begin(); it != cold_.end();) {
+      if (it->max_due <= wm) {
+        for (size_t r = 0; r < it->key.size(); ++r)
+          if (it->cnt[r] && m_.find(it->key[r]) == m_.end())
+            released.push_back((int64_t)it->key[r]);
+        cold_rows_ -= it->live;
+        it = cold_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+
+  // Device spill set (open addressing on mix64(key) >> 32, linear probing, empty = ~0) holding
+  // every key of this store: records of these keys are diverted from HBM to the host tier.
+  // `d`: 2^cap_log2 entries.
+  void spill_set(int cap_log2, int64_t* d) const {
+    const size_t cap = (size_t)1 << cap_log2;
+    if (num_keys() * 2 > cap) throw std::invalid_argument("spill set too small");
+    std::fill(d, d + cap, (int64_t)kEmptyKey);
+    const uint32_t mask = (uint32_t)(cap - 1);
+    auto put = [&](uint64_t key) {
+      uint32_t s = (uint32_t)(mix64(key) >> 32) & mask;
+      while ((uint64_t)d[s] != kEmptyKey) {
+        if ((uint64_t)d[s] == key) return;
+        s = (s + 1) & mask;
+      }
+      d[s] = (int64_t)key;
+    };
+    for (auto& kv : m_) put(kv.first);
+    for (auto& ch : cold_)
+      for (size_t r = 0; r < ch.key.size(); ++r)
+        if (ch.cnt[r]) put(ch.key[r]);
+  }
+
+  bool contains(uint64_t key) const {
+    if (m_.count(key)) return true;
+    for (auto& ch : cold_)
+      for (size_t r = 0; r < ch.key.size(); ++r)
+        if (ch.cnt[r] && ch.key[r] == key) return true;
+    return false;
+  }
+  // Keys (cold rows are one session per key in practice: an upper bound otherwise).
+  size_t num_keys() const { return m_.size() + cold_rows_; }
+  size_t num_sessions() const {
+    size_t s = cold_rows_;
+    for (auto& kv : m_) s += kv.second.size();
+    return s;
+  }
+  size_t num_cold_rows() const { return cold_rows_; }
+  size_t bytes() const {
+    size_t hot = 0;
+    for (auto& kv : m_) hot += kv.second.capacity() * sizeof(Session) + 48;
+    size_t cold = 0;
+    for (auto& ch : cold_) cold += ch.key.size() * (8 + 8 + 8 + 8 + 4);
+    return hot + cold;
+  }
+
+  std::vector<int64_t> key_list() const {
+    std::unordered_set<uint64_t> ks;
+    for (auto& kv : m_) ks.insert(kv.first);
+    for (auto& ch : cold_)
+      for (size_t r = 0; r < ch.key.size(); ++r)
+        if (ch.cnt[r]) ks.insert(ch.key[r]);
+    std::vector<int64_t> k(ks.begin(), ks.end());
+    std::sort(k.begin(), k.end());
+    return k;
+  }
+
+  // Snapshot: flat columns (key, start, end, acc, cnt, flags) of both tiers.
+  Columns snapshot() const {
+    Columns out;
+    for (auto& kv : m_)
+      for (auto& x : kv.second) out.add(kv.first, x.start, x.end, x.acc, x.cnt, x.flags);
+    for (auto& ch : cold_)
+      for (size_t r = 0; r < ch.key.size(); ++r)
+        if (ch.cnt[r]) out.add(ch.key[r], ch.start[r], ch.end[r], ch.acc[r], ch.cnt[r], 1u);
+    return out;
+  }
+
+  static ExprProg prog(const int32_t* code, size_t ncode, const double* consts, size_t nconst) {
+    ExprProg p;
+    std::memset(&p, 0, sizeof(p));
+    if (ncode > (size_t)2 * kExprMaxCode || nconst > (size_t)kExprMaxConst)
+      throw std::invalid_argument("expr program too large");
+    for (size_t i = 0; i < ncode; ++i) p.code[i] = code[i];
+    for (size_t i = 0; i < nconst; ++i) p.consts[i] = consts[i];
+    p.ncode = (int32_t)(ncode / 2);
+    return p;
+  }
+
+ private:
+  int64_t cleanup_time(int64_t maxts) const {
+    const int64_t c = maxts + late_;
+    return c < maxts ? INT64_MAX : c;  // overflow: never cleaned before end of input
+  }
+
+  // Move cold rows of `keys` into the hot map (rows past cleanup at `wm` are discarded).
+  void promote(const int64_t* keys, int64_t n, int64_t wm) {
+    if (cold_rows_ == 0 || n == 0) return;
+    std::vector<uint64_t> want((const uint64_t*)keys, (const uint64_t*)keys + n);
+    std::sort(want.begin(), want.end());
+    want.erase(std::unique(want.begin(), want.end()), want.end());
+    auto take = [&](ColdChunk& ch, uint32_t r) {
+      if (!ch.cnt[r]) return;
+      if (cleanup_time(ch.end[r] - 1) > wm) {
+        m_[ch.key[r]].push_back(Session{ch.start[r], ch.end[r], ch.acc[r], ch.cnt[r], 1u});
+        schedule(ch.key[r]);
+      } else {
+        pending_released_.push_back(ch.key[r]);  // reported by fire() unless it turns hot
+      }
+      ch.cnt[r] = 0;
+      ch.live -= 1;
+      cold_rows_ -= 1;
+    };
+    for (auto& ch : cold_) {
+      if (!ch.live || want.back() < ch.kmin || want.front() > ch.kmax) continue;
+      auto lo = std::lower_bound(want.begin(), want.end(), ch.kmin);
+      auto hi = std::upper_bound(lo, want.end(), ch.kmax);
+      if (lo == hi) continue;
+      ch.ensure_index();
+      const size_t nw = (size_t)(hi - lo), nc = ch.by_key.size();
+      auto ckey = [&](uint32_t r) { return ch.key[r]; };
+      if (nw * 20 < nc) {  // few wanted keys: binary search each in the chunk's key order
+        for (auto it = lo; it != hi; ++it) {
+          auto p = std::lower_bound(ch.by_key.begin(), ch.by_key.end(), *it,
+                                    [&](uint32_t r, uint64_t k) { return ckey(r) < k; });
+          for (; p != ch.by_key.end() && ckey(*p) == *it; ++p) take(ch, *p);
+        }
+      } else {  // merge join of two sorted sequences
+        size_t i = 0;
+        for (auto it = lo; it != hi && i < nc; ++it) {
+          while (i < nc && ckey(ch.by_key[i]) < *it) ++i;
+          for (; i < nc && ckey(ch.by_key[i]) == *it; ++i) take(ch, ch.by_key[i]);
+        }
+      }
+    }
+  }
+
+  // Merge candidate c into key's sessions; returns the number of late-dropped elements.
+  int64_t merge_candidate(uint64_t key, Session c, int64_t wm) {
+    auto found = m_.find(key);
+    Session merged = c;
+    bool touched_existing = false;
+    if (found != m_.end()) {
+      // In-place compaction: sessions intersecting the candidate fold into it, the rest stay.
+      auto& vec = found->second;
+      size_t w = 0;
+      for (size_t r = 0; r < vec.size(); ++r) {
+        const Session& s = vec[r];
+        if (merged.start <= s.end && merged.end >= s.start) {
+          merged.start = std::min(merged.start, s.start);
+          merged.end = std::max(merged.end, s.end);
+          merged.acc = agg_combine(agg_, s.acc, merged.acc);
+          merged.cnt += s.cnt;
+          merged.flags |= s.flags;
+          touched_existing = true;
+        } else {
+          vec[w++] = s;
+        }
+      }
+      vec.resize(w);
+    }
+    if (!touched_existing && cleanup_time(merged.end - 1) <= wm) {
+      if (found != m_.end() && found->second.empty()) m_.erase(found);
+      return c.cnt;  // late: every window of these elements is already cleaned
+    }
+    // A fired session that grows (or a new session already past its end within lateness)
+    // fires again at the next fire() with the watermark (EventTimeTrigger.onElement).
+    if (merged.flags & 1u) merged.flags |= 2u;
+    if (found == m_.end()) found = m_.emplace(key, Hot()).first;
+    found->second.push_back(merged);
+    schedule(key);
+    return 0;
+  }
+
+  void schedule(uint64_t key) {
+    auto it = m_.find(key);
+    if (it == m_.end()) return;
+    int64_t t = INT64_MAX;
+    for (auto& s : it->second) {
+      const int64_t maxts = s.end - 1;
+      const int64_t due = ((s.flags & 1u) && !(s.flags & 2u)) ? cleanup_time(maxts) : maxts;
+      t = std::min(t, due);
+    }
+    if (t == it->second.due) return;  // the key's heap entry already says t
+    it->second.due = t;
+    heap_.push({t, key});
+  }
+
+  int64_t gap_, late_;
+  int agg_;
+  // A key's live sessions plus the due time of its one valid heap entry (schedule() pushes only
+  // when the due time changes; fire() skips popped entries whose time is not the key's due).
+  struct Hot : std::vector<Session> {
+    int64_t due = INT64_MAX;
+  };
+  std::unordered_map<uint64_t, Hot> m_;
+  std::priority_queue<std::pair<int64_t, uint64_t>, std::vector<std::pair<int64_t, uint64_t>>,
+                      std::greater<>>
+      heap_;
+  std::deque<ColdChunk> cold_;
+  size_t cold_rows_ = 0;
+  std::vector<uint64_t> pending_released_;
+};
+
+}  // namespace sess
+}  // namespace mxs
+
+#endif  // MXS_SESSION_STORE_H_

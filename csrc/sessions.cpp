@@ -27,501 +27,92 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
-#include <algorithm>
-#include <cstring>
-#include <deque>
-#include <queue>
-#include <unordered_map>
-#include <unordered_set>
-#include <vector>
-
-#include "mxs_common.h"
+#include "session_store.h"
 
 namespace py = pybind11;
 
 namespace mxs {
 namespace {
 
-struct Session {
-  int64_t start, end;  // [start, end)
-  uint64_t acc;
-  uint32_t cnt;
-  uint32_t flags;      // bit0: fired, bit1: modified since firing
-};
-
-struct ColdChunk {
-  std::vector<uint64_t> key;
-  std::vector<int64_t> start, end;
-  std::vector<uint64_t> acc;
-  std::vector<uint32_t> cnt;  // 0 = row gone (promoted or discarded)
-  int64_t max_due = INT64_MIN;
-  size_t live = 0;
-  // Rows by key: promote() looks keys up by binary search or a merge join instead of probing a
-  // hash set with every cold row of the store.
-  std::vector<uint32_t> by_key;
-  uint64_t kmin = ~0ull, kmax = 0;
-
-  // Key range at sealing (O(n)); the sorted row index is built on the first promote() that
-  // reaches this chunk, so chunks that are never revisited never pay for it.
-  void seal() {
-    for (uint64_t k : key) {
-      kmin = k < kmin ? k : kmin;
-      kmax = k > kmax ? k : kmax;
-    }
-  }
-  void ensure_index() {
-    if (by_key.size() == key.size()) return;
-    // (key, row) pairs sorted contiguously: an index sort with key[] lookups in the comparator
-    // was 5x slower (random reads).
-    std::vector<std::pair<uint64_t, uint32_t>> kr(key.size());
-    for (size_t i = 0; i < kr.size(); ++i) kr[i] = {key[i], (uint32_t)i};
-    std::sort(kr.begin(), kr.end());
-    by_key.resize(kr.size());
-    for (size_t i = 0; i < kr.size(); ++i) by_key[i] = kr[i].second;
-  }
-};
+using I64Array = py::array_t<int64_t, py::array::c_style>;
 
 template <class T>
 py::array_t<T> to_np(const std::vector<T>& v) {
   return py::array_t<T>((py::ssize_t)v.size(), v.data());
 }
 
-class SessionStore {
+py::dict columns_dict(const sess::Columns& c) {
+  py::dict d;
+  d["key"] = to_np(c.key);
+  d["start"] = to_np(c.start);
+  d["end"] = to_np(c.end);
+  d["acc"] = to_np(c.acc);
+  d["cnt"] = to_np(c.cnt);
+  d["flags"] = to_np(c.flags);
+  return d;
+}
+
+void same_len(int64_t n, std::initializer_list<int64_t> sizes) {
+  for (int64_t s : sizes)
+    if (s != n) throw std::invalid_argument("length mismatch");
+}
+
+// NumPy adapter of the store core (csrc/session_store.h).
+class SessionStore : public sess::SessionCore {
  public:
-  SessionStore(int64_t gap, int64_t lateness, int agg) : gap_(gap), late_(lateness), agg_(agg) {
-    if (gap <= 0) throw std::invalid_argument("session gap must be > 0");
-  }
+  using SessionCore::SessionCore;
 
   // Fold a batch (keys, ts, vals) with the current watermark `wm`; returns late-dropped count.
-  int64_t process(py::array_t<int64_t, py::array::c_style> keys,
-                  py::array_t<int64_t, py::array::c_style> ts,
-                  py::array_t<int64_t, py::array::c_style> vals, int64_t wm) {
-    const int64_t n = keys.size();
-    if (ts.size() != n || vals.size() != n) throw std::invalid_argument("length mismatch");
-    const int64_t* k = keys.data();
-    const int64_t* t = ts.data();
-    const int64_t* v = vals.data();
-    promote(k, n, wm);
-    // Sort the records themselves by (key, ts) (contiguous, no indirect compares): every
-    // aggregate is a commutative monoid, so the order of equal (key, ts) records is free.
-    struct KTV {
-      uint64_t k;
-      int64_t t, v;
-    };
-    std::vector<KTV> r(n);
-    for (int64_t i = 0; i < n; ++i) r[i] = KTV{(uint64_t)k[i], t[i], v[i]};
-    std::sort(r.begin(), r.end(),
-              [](const KTV& a, const KTV& b) { return a.k != b.k ? a.k < b.k : a.t < b.t; });
-    int64_t late = 0;
-    int64_t i = 0;
-    while (i < n) {
-      const uint64_t key = r[i].k;
-      int64_t j = i;
-      while (j < n && r[j].k == key) ++j;
-      int64_t q0 = i;
-      while (q0 < j) {
-        Session c{r[q0].t, r[q0].t + gap_, agg_lift(agg_, (uint64_t)r[q0].v), 1u, 0u};
-        int64_t q = q0 + 1;
-        while (q < j && r[q].t <= c.end) {  // intersects (touching merges)
-          c.end = std::max(c.end, r[q].t + gap_);
-          c.acc = agg_combine(agg_, c.acc, agg_lift(agg_, (uint64_t)r[q].v));
-          c.cnt += 1;
-          ++q;
-        }
-        late += merge_candidate(key, c, wm);
-        q0 = q;
-      }
-      i = j;
-    }
-    return late;
+  int64_t process_np(const I64Array& keys, const I64Array& ts, const I64Array& vals, int64_t wm) {
+    same_len(keys.size(), {ts.size(), vals.size()});
+    return process(keys.data(), ts.data(), vals.data(), keys.size(), wm);
   }
-
   // Merge pre-built runs (GPU overflow path): each is a candidate session.
-  int64_t merge_runs(py::array_t<int64_t, py::array::c_style> keys,
-                     py::array_t<int64_t, py::array::c_style> starts,
-                     py::array_t<int64_t, py::array::c_style> ends,
-                     py::array_t<int64_t, py::array::c_style> accs,
-                     py::array_t<int64_t, py::array::c_style> cnts, int64_t wm) {
-    const int64_t n = keys.size();
-    promote(keys.data(), n, wm);
-    int64_t late = 0;
-    for (int64_t i = 0; i < n; ++i) {
-      Session c{starts.data()[i], ends.data()[i], (uint64_t)accs.data()[i],
-                (uint32_t)cnts.data()[i], 0u};
-      late += merge_candidate((uint64_t)keys.data()[i], c, wm);
-    }
-    return late;
+  int64_t merge_runs_np(const I64Array& keys, const I64Array& starts, const I64Array& ends,
+                        const I64Array& accs, const I64Array& cnts, int64_t wm) {
+    same_len(keys.size(), {starts.size(), ends.size(), accs.size(), cnts.size()});
+    return merge_runs(keys.data(), starts.data(), ends.data(), accs.data(), cnts.data(),
+                      keys.size(), wm);
   }
-
-  // Insert sessions evicted from HBM. Arrays: key, start, end, acc, cnt, flags. With `cold`,
-  // fired-and-unmodified sessions of keys without hot state go to one new cold chunk.
   // Arguments by const reference: the call runs without the GIL, so no Python object may be
   // created or released inside it.
-  using I64Array = py::array_t<int64_t, py::array::c_style>;
-  void insert(const I64Array& keys, const I64Array& starts, const I64Array& ends,
-              const I64Array& accs, const I64Array& cnts, const I64Array& flags, bool cold) {
-    const int64_t n = keys.size();
-    auto K = keys.data();
-    auto S = starts.data();
-    auto E = ends.data();
-    auto A = accs.data();
-    auto C = cnts.data();
-    auto F = flags.data();
-    ColdChunk ch;
-    if (cold) {
-      ch.key.reserve(n);
-      ch.start.reserve(n);
-      ch.end.reserve(n);
-      ch.acc.reserve(n);
-      ch.cnt.reserve(n);
-    }
-    const bool no_hot = m_.empty();
-    for (int64_t i = 0; i < n; ++i) {
-      const uint64_t key = (uint64_t)K[i];
-      if (cold && F[i] == 1 && (no_hot || m_.find(key) == m_.end())) {
-        ch.key.push_back(key);
-        ch.start.push_back(S[i]);
-        ch.end.push_back(E[i]);
-        ch.acc.push_back((uint64_t)A[i]);
-        ch.cnt.push_back((uint32_t)C[i]);
-        ch.max_due = std::max(ch.max_due, cleanup_time(E[i] - 1));
-        continue;
-      }
-      m_[key].push_back(Session{S[i], E[i], (uint64_t)A[i], (uint32_t)C[i], (uint32_t)F[i]});
-      schedule(key);
-    }
-    if (!ch.key.empty()) {
-      ch.live = ch.key.size();
-      ch.seal();
-      cold_rows_ += ch.live;
-      cold_.push_back(std::move(ch));
-    }
+  void insert_np(const I64Array& keys, const I64Array& starts, const I64Array& ends,
+                 const I64Array& accs, const I64Array& cnts, const I64Array& flags, bool cold) {
+    same_len(keys.size(), {starts.size(), ends.size(), accs.size(), cnts.size(), flags.size()});
+    insert(keys.data(), starts.data(), ends.data(), accs.data(), cnts.data(), flags.data(),
+           keys.size(), cold);
   }
-
-  // Hand keys back to the HBM tier: every listed key with at most `max_sess` live sessions
-  // leaves the store (hot sessions and cold rows; rows past cleanup at `wm` are dropped).
-  // Returns its sessions as columns grouped by key (keys ascending) plus "moved": every listed
-  // key that is no longer in the store (its spill-set entry can go). Keys with more sessions
-  // than an HBM slot holds stay here.
-  py::dict extract(py::array_t<int64_t, py::array::c_style> keys, int64_t wm, int64_t max_sess) {
-    const int64_t n = keys.size();
-    promote(keys.data(), n, wm);
-    std::vector<uint64_t> want((const uint64_t*)keys.data(), (const uint64_t*)keys.data() + n);
-    std::sort(want.begin(), want.end());
-    want.erase(std::unique(want.begin(), want.end()), want.end());
-    std::vector<int64_t> k, st, en, ac, cn, fl, moved;
-    for (uint64_t key : want) {
-      auto it = m_.find(key);
-      if (it == m_.end()) {
-        moved.push_back((int64_t)key);
-        continue;
-      }
-      if ((int64_t)it->second.size() > max_sess) continue;
-      for (const Session& x : it->second) {
-        k.push_back((int64_t)key);
-        st.push_back(x.start);
-        en.push_back(x.end);
-        ac.push_back((int64_t)x.acc);
-        cn.push_back(x.cnt);
-        fl.push_back(x.flags);
-      }
-      m_.erase(it);  // its heap entries turn stale
-      moved.push_back((int64_t)key);
-    }
-    py::dict d;
-    d["key"] = to_np(k);
-    d["start"] = to_np(st);
-    d["end"] = to_np(en);
-    d["acc"] = to_np(ac);
-    d["cnt"] = to_np(cn);
-    d["flags"] = to_np(fl);
+  py::dict extract_np(const I64Array& keys, int64_t wm, int64_t max_sess) {
+    std::vector<int64_t> moved;
+    py::dict d = columns_dict(extract(keys.data(), keys.size(), wm, max_sess, &moved));
     d["moved"] = to_np(moved);
     return d;
   }
-
   // Fire / clean up everything the watermark allows. Returns columns of emitted rows plus the
   // keys that left the store ("released").
-  py::dict fire(int64_t wm, std::vector<int32_t> map_code, std::vector<double> map_consts,
-                std::vector<int32_t> f_code, std::vector<double> f_consts) {
-    ExprProg mp = prog(map_code, map_consts), fp = prog(f_code, f_consts);
-    std::vector<int64_t> okey, ostart, oend, oraw, ocnt, oref, released;
-    std::vector<double> oval;
-    while (!heap_.empty() && heap_.top().first <= wm) {
-      const int64_t due = heap_.top().first;
-      const uint64_t key = heap_.top().second;
-      heap_.pop();
-      auto it = m_.find(key);
-      if (it == m_.end() || it->second.due != due) continue;  // stale entry
-      it->second.due = INT64_MAX;  // this entry is consumed
-      auto& vec = it->second;
-      std::vector<Session> keep;
-      for (auto& s : vec) {
-        const int64_t maxts = s.end - 1;
-        if (maxts <= wm && (!(s.flags & 1u) || (s.flags & 2u))) {
-          double vars[kExprVars] = {0};
-          vars[0] = agg_result_f64(agg_, s.acc, s.cnt);
-          vars[1] = (double)s.cnt;
-          vars[2] = (double)s.start;
-          vars[3] = (double)s.end;
-          vars[4] = (double)key;
-          vars[5] = (double)(int64_t)s.acc;
-          vars[6] = mp.ncode ? expr_eval(mp, vars) : vars[0];
-          if (!fp.ncode || expr_eval(fp, vars) != 0.0) {
-            okey.push_back((int64_t)key);
-            ostart.push_back(s.start);
-            oend.push_back(s.end);
-            oval.push_back(vars[6]);
-            oraw.push_back((int64_t)s.acc);
-            ocnt.push_back(s.cnt);
-            oref.push_back((s.flags & 1u) ? 1 : 0);
-          }
-          s.flags = 1u;
-        }
-        if (cleanup_time(maxts) > wm) keep.push_back(s);  // not cleaned yet
-      }
-      if (keep.empty()) {
-        m_.erase(it);
-        released.push_back((int64_t)key);
-      } else {
-        vec.swap(keep);
-        schedule(key);
-      }
-    }
-    for (uint64_t key : pending_released_)
-      if (m_.find(key) == m_.end()) released.push_back((int64_t)key);
-    pending_released_.clear();
-    // Cold chunks: dropped as a whole once every row is past cleanup.
-    for (auto it = cold_.begin(); it != cold_.end();) {
-      if (it->max_due <= wm) {
-        for (size_t r = 0; r < it->key.size(); ++r)
-          if (it->cnt[r] && m_.find(it->key[r]) == m_.end())
-            released.push_back((int64_t)it->key[r]);
-        cold_rows_ -= it->live;
-        it = cold_.erase(it);
-      } else {
-        ++it;
-      }
-    }
+  py::dict fire_np(int64_t wm, std::vector<int32_t> map_code, std::vector<double> map_consts,
+                   std::vector<int32_t> f_code, std::vector<double> f_consts) {
+    FireOut o;
+    fire(wm, prog(map_code.data(), map_code.size(), map_consts.data(), map_consts.size()),
+         prog(f_code.data(), f_code.size(), f_consts.data(), f_consts.size()), o);
     py::dict d;
-    d["keys"] = to_np(okey);
-    d["start"] = to_np(ostart);
-    d["end"] = to_np(oend);
-    d["values"] = to_np(oval);
-    d["raw"] = to_np(oraw);
-    d["counts"] = to_np(ocnt);
-    d["refire"] = to_np(oref);
-    d["released"] = to_np(released);
+    d["keys"] = to_np(o.okey);
+    d["start"] = to_np(o.ostart);
+    d["end"] = to_np(o.oend);
+    d["values"] = to_np(o.oval);
+    d["raw"] = to_np(o.oraw);
+    d["counts"] = to_np(o.ocnt);
+    d["refire"] = to_np(o.oref);
+    d["released"] = to_np(o.released);
     return d;
   }
-
-  // Device spill set (open addressing on mix64(key) >> 32, linear probing, empty = ~0) holding
-  // every key of this store: records of these keys are diverted from HBM to the host tier.
-  py::array_t<int64_t> spill_set(int cap_log2) const {
-    const size_t cap = (size_t)1 << cap_log2;
-    if (num_keys() * 2 > cap) throw std::invalid_argument("spill set too small");
-    py::array_t<int64_t> out((py::ssize_t)cap);
-    int64_t* d = out.mutable_data();
-    std::fill(d, d + cap, (int64_t)kEmptyKey);
-    const uint32_t mask = (uint32_t)(cap - 1);
-    auto put = [&](uint64_t key) {
-      uint32_t s = (uint32_t)(mix64(key) >> 32) & mask;
-      while ((uint64_t)d[s] != kEmptyKey) {
-        if ((uint64_t)d[s] == key) return;
-        s = (s + 1) & mask;
-      }
-      d[s] = (int64_t)key;
-    };
-    for (auto& kv : m_) put(kv.first);
-    for (auto& ch : cold_)
-      for (size_t r = 0; r < ch.key.size(); ++r)
-        if (ch.cnt[r]) put(ch.key[r]);
+  py::array_t<int64_t> spill_set_np(int cap_log2) const {
+    py::array_t<int64_t> out((py::ssize_t)1 << cap_log2);
+    spill_set(cap_log2, out.mutable_data());
     return out;
   }
-
-  bool contains(uint64_t key) const {
-    if (m_.count(key)) return true;
-    for (auto& ch : cold_)
-      for (size_t r = 0; r < ch.key.size(); ++r)
-        if (ch.cnt[r] && ch.key[r] == key) return true;
-    return false;
-  }
-  // Keys (cold rows are one session per key in practice: an upper bound otherwise).
-  size_t num_keys() const { return m_.size() + cold_rows_; }
-  size_t num_sessions() const {
-    size_t s = cold_rows_;
-    for (auto& kv : m_) s += kv.second.size();
-    return s;
-  }
-  size_t num_cold_rows() const { return cold_rows_; }
-  size_t bytes() const {
-    size_t hot = 0;
-    for (auto& kv : m_) hot += kv.second.capacity() * sizeof(Session) + 48;
-    size_t cold = 0;
-    for (auto& ch : cold_) cold += ch.key.size() * (8 + 8 + 8 + 8 + 4);
-    return hot + cold;
-  }
-
-  py::array_t<int64_t> key_list() const {
-    std::unordered_set<uint64_t> ks;
-    for (auto& kv : m_) ks.insert(kv.first);
-    for (auto& ch : cold_)
-      for (size_t r = 0; r < ch.key.size(); ++r)
-        if (ch.cnt[r]) ks.insert(ch.key[r]);
-    std::vector<int64_t> k(ks.begin(), ks.end());
-    std::sort(k.begin(), k.end());
-    return to_np(k);
-  }
-
-  // Snapshot: flat columns (key, start, end, acc, cnt, flags) of both tiers.
-  py::dict snapshot() const {
-    std::vector<int64_t> k, s, e, a, c, f;
-    auto add = [&](uint64_t key, int64_t st, int64_t en, uint64_t ac, uint32_t cn, uint32_t fl) {
-      k.push_back((int64_t)key);
-      s.push_back(st);
-      e.push_back(en);
-      a.push_back((int64_t)ac);
-      c.push_back(cn);
-      f.push_back(fl);
-    };
-    for (auto& kv : m_)
-      for (auto& x : kv.second) add(kv.first, x.start, x.end, x.acc, x.cnt, x.flags);
-    for (auto& ch : cold_)
-      for (size_t r = 0; r < ch.key.size(); ++r)
-        if (ch.cnt[r]) add(ch.key[r], ch.start[r], ch.end[r], ch.acc[r], ch.cnt[r], 1u);
-    py::dict d;
-    d["key"] = to_np(k);
-    d["start"] = to_np(s);
-    d["end"] = to_np(e);
-    d["acc"] = to_np(a);
-    d["cnt"] = to_np(c);
-    d["flags"] = to_np(f);
-    return d;
-  }
-
- private:
-  static ExprProg prog(const std::vector<int32_t>& code, const std::vector<double>& consts) {
-    ExprProg p;
-    std::memset(&p, 0, sizeof(p));
-    if (code.size() > (size_t)2 * kExprMaxCode || consts.size() > (size_t)kExprMaxConst)
-      throw std::invalid_argument("expr program too large");
-    for (size_t i = 0; i < code.size(); ++i) p.code[i] = code[i];
-    for (size_t i = 0; i < consts.size(); ++i) p.consts[i] = consts[i];
-    p.ncode = (int32_t)(code.size() / 2);
-    return p;
-  }
-
-  int64_t cleanup_time(int64_t maxts) const {
-    const int64_t c = maxts + late_;
-    return c < maxts ? INT64_MAX : c;  // overflow: never cleaned before end of input
-  }
-
-  // Move cold rows of `keys` into the hot map (rows past cleanup at `wm` are discarded).
-  void promote(const int64_t* keys, int64_t n, int64_t wm) {
-    if (cold_rows_ == 0 || n == 0) return;
-    std::vector<uint64_t> want((const uint64_t*)keys, (const uint64_t*)keys + n);
-    std::sort(want.begin(), want.end());
-    want.erase(std::unique(want.begin(), want.end()), want.end());
-    auto take = [&](ColdChunk& ch, uint32_t r) {
-      if (!ch.cnt[r]) return;
-      if (cleanup_time(ch.end[r] - 1) > wm) {
-        m_[ch.key[r]].push_back(Session{ch.start[r], ch.end[r], ch.acc[r], ch.cnt[r], 1u});
-        schedule(ch.key[r]);
-      } else {
-        pending_released_.push_back(ch.key[r]);  // reported by fire() unless it turns hot
-      }
-      ch.cnt[r] = 0;
-      ch.live -= 1;
-      cold_rows_ -= 1;
-    };
-    for (auto& ch : cold_) {
-      if (!ch.live || want.back() < ch.kmin || want.front() > ch.kmax) continue;
-      auto lo = std::lower_bound(want.begin(), want.end(), ch.kmin);
-      auto hi = std::upper_bound(lo, want.end(), ch.kmax);
-      if (lo == hi) continue;
-      ch.ensure_index();
-      const size_t nw = (size_t)(hi - lo), nc = ch.by_key.size();
-      auto ckey = [&](uint32_t r) { return ch.key[r]; };
-      if (nw * 20 < nc) {  // few wanted keys: binary search each in the chunk's key order
-        for (auto it = lo; it != hi; ++it) {
-          auto p = std::lower_bound(ch.by_key.begin(), ch.by_key.end(), *it,
-                                    [&](uint32_t r, uint64_t k) { return ckey(r) < k; });
-          for (; p != ch.by_key.end() && ckey(*p) == *it; ++p) take(ch, *p);
-        }
-      } else {  // merge join of two sorted sequences
-        size_t i = 0;
-        for (auto it = lo; it != hi && i < nc; ++it) {
-          while (i < nc && ckey(ch.by_key[i]) < *it) ++i;
-          for (; i < nc && ckey(ch.by_key[i]) == *it; ++i) take(ch, ch.by_key[i]);
-        }
-      }
-    }
-  }
-
-  // Merge candidate c into key's sessions; returns the number of late-dropped elements.
-  int64_t merge_candidate(uint64_t key, Session c, int64_t wm) {
-    auto found = m_.find(key);
-    Session merged = c;
-    bool touched_existing = false;
-    if (found != m_.end()) {
-      // In-place compaction: sessions intersecting the candidate fold into it, the rest stay.
-      auto& vec = found->second;
-      size_t w = 0;
-      for (size_t r = 0; r < vec.size(); ++r) {
-        const Session& s = vec[r];
-        if (merged.start <= s.end && merged.end >= s.start) {
-          merged.start = std::min(merged.start, s.start);
-          merged.end = std::max(merged.end, s.end);
-          merged.acc = agg_combine(agg_, s.acc, merged.acc);
-          merged.cnt += s.cnt;
-          merged.flags |= s.flags;
-          touched_existing = true;
-        } else {
-          vec[w++] = s;
-        }
-      }
-      vec.resize(w);
-    }
-    if (!touched_existing && cleanup_time(merged.end - 1) <= wm) {
-      if (found != m_.end() && found->second.empty()) m_.erase(found);
-      return c.cnt;  // late: every window of these elements is already cleaned
-    }
-    // A fired session that grows (or a new session already past its end within lateness)
-    // fires again at the next fire() with the watermark (EventTimeTrigger.onElement).
-    if (merged.flags & 1u) merged.flags |= 2u;
-    if (found == m_.end()) found = m_.emplace(key, Hot()).first;
-    found->second.push_back(merged);
-    schedule(key);
-    return 0;
-  }
-
-  void schedule(uint64_t key) {
-    auto it = m_.find(key);
-    if (it == m_.end()) return;
-    int64_t t = INT64_MAX;
-    for (auto& s : it->second) {
-      const int64_t maxts = s.end - 1;
-      const int64_t due = ((s.flags & 1u) && !(s.flags & 2u)) ? cleanup_time(maxts) : maxts;
-      t = std::min(t, due);
-    }
-    if (t == it->second.due) return;  // the key's heap entry already says t
-    it->second.due = t;
-    heap_.push({t, key});
-  }
-
-  int64_t gap_, late_;
-  int agg_;
-  // A key's live sessions plus the due time of its one valid heap entry (schedule() pushes only
-  // when the due time changes; fire() skips popped entries whose time is not the key's due).
-  struct Hot : std::vector<Session> {
-    int64_t due = INT64_MAX;
-  };
-  std::unordered_map<uint64_t, Hot> m_;
-  std::priority_queue<std::pair<int64_t, uint64_t>, std::vector<std::pair<int64_t, uint64_t>>,
-                      std::greater<>>
-      heap_;
-  std::deque<ColdChunk> cold_;
-  size_t cold_rows_ = 0;
-  std::vector<uint64_t> pending_released_;
+  py::array_t<int64_t> key_list_np() const { return to_np(key_list()); }
+  py::dict snapshot_np() const { return columns_dict(snapshot()); }
 };
 
 }  // namespace
@@ -531,21 +122,21 @@ void bind_sessions(py::module_& m) {
   using mxs::SessionStore;
   py::class_<SessionStore>(m, "SessionStore")
       .def(py::init<int64_t, int64_t, int>(), py::arg("gap"), py::arg("lateness"), py::arg("agg"))
-      .def("process", &SessionStore::process)
+      .def("process", &SessionStore::process_np)
       // GIL released: the operator inserts spilled rows from a worker thread while the main
       // thread keeps launching the next step's kernels (the store is not touched concurrently).
-      .def("insert", &SessionStore::insert, py::arg("keys"), py::arg("starts"), py::arg("ends"),
-           py::arg("accs"), py::arg("cnts"), py::arg("flags"), py::arg("cold") = false,
-           py::call_guard<py::gil_scoped_release>())
-      .def("merge_runs", &SessionStore::merge_runs)
-      .def("extract", &SessionStore::extract)
-      .def("fire", &SessionStore::fire)
-      .def("spill_set", &SessionStore::spill_set)
+      .def("insert", &SessionStore::insert_np, py::arg("keys"), py::arg("starts"),
+           py::arg("ends"), py::arg("accs"), py::arg("cnts"), py::arg("flags"),
+           py::arg("cold") = false, py::call_guard<py::gil_scoped_release>())
+      .def("merge_runs", &SessionStore::merge_runs_np)
+      .def("extract", &SessionStore::extract_np)
+      .def("fire", &SessionStore::fire_np)
+      .def("spill_set", &SessionStore::spill_set_np)
       .def("contains", &SessionStore::contains)
       .def("num_keys", &SessionStore::num_keys)
       .def("num_sessions", &SessionStore::num_sessions)
       .def("num_cold_rows", &SessionStore::num_cold_rows)
       .def("bytes", &SessionStore::bytes)
-      .def("key_list", &SessionStore::key_list)
-      .def("snapshot", &SessionStore::snapshot);
+      .def("key_list", &SessionStore::key_list_np)
+      .def("snapshot", &SessionStore::snapshot_np);
 }

@@ -451,8 +451,14 @@ class KeyedSessionOperator:
             dev = self.device
             if len(keys):
                 uniq, first, counts = np.unique(keys, return_index=True, return_counts=True)
-                slots = K.table_insert(torch.from_numpy(uniq).to(dev), self.keys_g,
-                                       nsub_log2=self.nsub_log2, cap_log2=self.cap_log2).cpu().numpy()
+                ukeys = torch.from_numpy(uniq).to(dev)
+                slots_t = torch.empty_like(ukeys)
+                self.ctr[3:4].zero_()
+                self.native.gpu_session_slot_insert(ukeys.data_ptr(), ukeys.numel(),
+                                                    self.nsub_log2, self.cap_log2,
+                                                    self.keys_g.data_ptr(), slots_t.data_ptr(),
+                                                    self.ctr[3:4].data_ptr(), self._st())
+                slots = slots_t.cpu().numpy()
                 bad = slots < 0
                 if bad.any():  # sub-table full: those keys' sessions go back to the store
                     rb = np.repeat(bad, counts)

@@ -231,3 +231,77 @@ def test_capi_rolling_gpu_equals_host(lib, gpu_device, agg, count_window):
         batches.append((keys, vals))
     assert _run_rolling_capi(lib, batches, 1, agg, count_window) == \
         _run_rolling_capi(lib, batches, 0, agg, count_window)
+
+
+class SCfg(ctypes.Structure):
+    _fields_ = [("gap_ms", ctypes.c_int64), ("lateness_ms", ctypes.c_int64),
+                ("ooo_bound_ms", ctypes.c_int64), ("agg", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
+
+
+class SRes(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_uint64), ("start", ctypes.c_int64), ("end", ctypes.c_int64),
+                ("value", ctypes.c_double), ("raw", ctypes.c_int64), ("count", ctypes.c_uint32),
+                ("refire", ctypes.c_int32)]
+
+
+@pytest.mark.parametrize("agg", [K.AGG_SUM_I64, K.AGG_MAX_I64, K.AGG_COUNT])
+@pytest.mark.parametrize("lateness", [0, 3_000])
+def test_capi_sessions_equal_python_operator(lib, agg, lateness):
+    """mxs_session_* (C ABI over the C++ session store core) emits exactly the Python
+    KeyedSessionOperator's sessions (EventTimeSessionWindows, chapter3/README.md:412-428),
+    including late-but-allowed re-firings."""
+    from mxstream.runtime.session_operator import KeyedSessionOperator
+
+    L = lib
+    L.mxs_session_create.restype = ctypes.c_void_p
+    L.mxs_session_create.argtypes = [ctypes.POINTER(SCfg)]
+    L.mxs_session_destroy.argtypes = [ctypes.c_void_p]
+    L.mxs_session_process.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int64]
+    L.mxs_session_finish.argtypes = [ctypes.c_void_p]
+    L.mxs_session_take_results.restype = ctypes.c_int64
+    L.mxs_session_take_results.argtypes = [ctypes.c_void_p, ctypes.POINTER(SRes), ctypes.c_int64]
+    L.mxs_session_late_dropped.restype = ctypes.c_int64
+    L.mxs_session_late_dropped.argtypes = [ctypes.c_void_p]
+    L.mxs_session_config_default.argtypes = [ctypes.POINTER(SCfg)]
+    rng = np.random.default_rng(agg + lateness)
+    n = 6000
+    ts = np.sort(rng.integers(0, 120_000, n)) + rng.integers(-2_500, 2_500, n)  # disorder
+    keys = rng.integers(0, 40, n)
+    vals = rng.integers(0, 100, n)
+    cfg = SCfg()
+    L.mxs_session_config_default(ctypes.byref(cfg))
+    cfg.gap_ms, cfg.lateness_ms, cfg.ooo_bound_ms, cfg.agg = 1_500, lateness, 1_000, agg
+    s = L.mxs_session_create(ctypes.byref(cfg))
+    assert s, L.mxs_last_error()
+    op = KeyedSessionOperator(gap=1_500, lateness=lateness, agg=agg, device="cpu",
+                              max_keys=64, batch_capacity=512, ooo_bound=1_000)
+    got, want = [], []
+    buf = (SRes * 4096)()
+
+    def take():
+        while True:
+            m = L.mxs_session_take_results(s, buf, 4096)
+            if m <= 0:
+                break
+            got.extend((x.key, x.start, x.end, x.raw, x.count) for x in buf[:m])
+
+    def rows(r):
+        want.extend((int(k), int(a), int(b), int(w), int(c))
+                    for k, a, b, w, c in zip(r.keys, r.start, r.end, r.raw, r.counts))
+
+    try:
+        for i in range(0, n, 500):
+            k, t, v = (np.ascontiguousarray(x[i:i + 500], dtype=np.int64) for x in (keys, ts, vals))
+            assert L.mxs_session_process(s, k.ctypes.data, t.ctypes.data, v.ctypes.data,
+                                         len(k)) == 0, L.mxs_last_error()
+            take()
+            rows(op.process(torch.from_numpy(k), torch.from_numpy(t), torch.from_numpy(v)))
+        assert L.mxs_session_finish(s) == 0
+        take()
+        rows(op.finish())
+        assert L.mxs_session_late_dropped(s) == op.metrics.num_late_records_dropped
+    finally:
+        L.mxs_session_destroy(s)
+    assert len(want) > 100 and sorted(got) == sorted(want)

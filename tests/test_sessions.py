@@ -268,3 +268,25 @@ def engine_with(events, gap, bound, lateness, *, promote, device, batch, **kw):
     for kk, s_, e_, rr, c in zip(r.keys, r.start, r.end, r.raw, r.counts):
         out[(int(kk), int(s_), int(e_), int(rr), int(c))] += 1
     return out, op
+
+
+def test_store_extract_hands_back_sessions():
+    # Promotion back to HBM (GPU operator) takes keys out of the host store: cold rows and hot
+    # sessions of keys with <= max_sess sessions; rows past cleanup are dropped; keys with more
+    # sessions stay (their cold rows turn hot).
+    from mxstream.ops.native import load
+
+    st = load().SessionStore(100, 1_000, K.AGG_SUM_I64)
+    a = lambda *x: np.array(x, dtype=np.int64)  # noqa: E731
+    # cold rows (fired, unmodified): key 1 live, key 2 past cleanup at wm=5000, key 3 x3 rows
+    st.insert(a(1, 2, 3, 3, 3), a(4000, 0, 4000, 4200, 4400), a(4100, 100, 4100, 4300, 4500),
+              a(7, 8, 1, 2, 3), a(1, 1, 1, 1, 1), a(1, 1, 1, 1, 1), True)
+    st.process(a(4, 3), a(4800, 4700), a(5, 6), 4000)  # key 4 hot only; key 3 gets a hot session
+    assert st.num_keys() >= 4
+    ex = st.extract(a(1, 2, 3, 4, 9), 5_000, 2)
+    assert ex["key"].tolist() == [1, 4]
+    assert ex["acc"].tolist() == [7, 5] and ex["flags"].tolist() == [1, 0]
+    assert sorted(ex["moved"].tolist()) == [1, 2, 4, 9]  # 3 has 4 sessions > 2: stays
+    assert st.contains(3) and not st.contains(1) and not st.contains(4)
+    snap = st.snapshot()
+    assert sorted(snap["key"].tolist()) == [3, 3, 3, 3]
