@@ -173,13 +173,14 @@ class SessionCore {
     // Cold rows of the wanted keys come straight out of their chunks (no detour through the hot
     // map); rows already past cleanup at `wm` are dropped, as a promote would.
     std::vector<std::pair<uint64_t, Session>> cold;
+    std::vector<uint64_t> wset;  // hash set of `want`, built on first use
+    size_t wmask = 0;
     if (cold_rows_ && !want.empty()) {
       for (auto& ch : cold_) {
         if (!ch.live || want.back() < ch.kmin || want.front() > ch.kmax) continue;
         auto lo = std::lower_bound(want.begin(), want.end(), ch.kmin);
         auto hi = std::upper_bound(lo, want.end(), ch.kmax);
         if (lo == hi) continue;
-        ch.ensure_index();
         auto take = [&](uint32_t r) {
           if (!ch.cnt[r]) return;
           if (cleanup_time(ch.end[r] - 1) > wm)
@@ -188,6 +189,31 @@ class SessionCore {
           ch.live -= 1;
           cold_rows_ -= 1;
         };
+        const size_t nw = (size_t)(hi - lo), nc = ch.key.size();
+        if (ch.by_key.size() != nc && nw * 20 >= nc) {
+          // Many wanted keys and no row index yet: one pass over the chunk probing a hash set
+          // of the wanted keys (sorting the chunk's 10^5-10^6 rows for an index costs more).
+          if (wset.empty()) {
+            size_t cap = 16;
+            while (cap < 2 * want.size()) cap <<= 1;
+            wset.assign(cap, kEmptyKey);
+            wmask = cap - 1;
+            for (uint64_t k : want) {
+              size_t h = (size_t)(mix64(k) >> 32) & wmask;
+              while (wset[h] != kEmptyKey && wset[h] != k) h = (h + 1) & wmask;
+              wset[h] = k;
+            }
+          }
+          for (uint32_t r = 0; r < (uint32_t)nc; ++r) {
+            const uint64_t k = ch.key[r];
+            if (!ch.cnt[r] || k < *lo || k > *(hi - 1)) continue;
+            size_t h = (size_t)(mix64(k) >> 32) & wmask;
+            while (wset[h] != kEmptyKey && wset[h] != k) h = (h + 1) & wmask;
+            if (wset[h] == k) take(r);
+          }
+          continue;
+        }
+        ch.ensure_index();
         for (auto it = lo; it != hi; ++it) {
           auto p = std::lower_bound(ch.by_key.begin(), ch.by_key.end(), *it,
                                     [&](uint32_t r, uint64_t k) { return ch.key[r] < k; });
