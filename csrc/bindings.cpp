@@ -617,6 +617,13 @@ PYBIND11_MODULE(_mxs_native, m) {
                         P<int64_t>(sess_n), P<int64_t>(due_n), P<int64_t>(last_n),
                         P<uint32_t>(ins), stream);
   });
+  m.def("gpu_filter_compact_scratch_bytes", &gpu::filter_compact_scratch_bytes);
+  m.def("gpu_expr_filter_compact", [](intptr_t x, int64_t n, std::vector<int32_t> code,
+                                      std::vector<double> consts, intptr_t scratch, intptr_t idx,
+                                      intptr_t total, intptr_t stream) {
+    gpu::expr_filter_compact(P<double>(x), n, make_prog(code, consts), P<void>(scratch),
+                             P<int64_t>(idx), P<int64_t>(total), stream);
+  });
   m.def("gpu_expr_filter", [](intptr_t x, int64_t n, std::vector<int32_t> code,
                               std::vector<double> consts, intptr_t keep, intptr_t stream) {
     gpu::expr_filter(P<double>(x), n, make_prog(code, consts), P<uint8_t>(keep), stream);
@@ -684,6 +691,12 @@ PYBIND11_MODULE(_mxs_native, m) {
                       P<uint64_t>(keys_g), P<uint64_t>(acc_g), P<uint32_t>(cnt_g),
                       P<uint32_t>(flags), f, P<uint64_t>(ok), P<uint64_t>(ov), P<int64_t>(ot),
                       P<uint32_t>(on), out_cap, count_n);
+  });
+  m.def("cpu_expr_filter_compact", [](intptr_t x, int64_t n, std::vector<int32_t> code,
+                                      std::vector<double> consts, intptr_t idx, intptr_t total) {
+    ExprProg p = make_prog(code, consts);
+    py::gil_scoped_release nogil;
+    cpu::expr_filter_compact(P<double>(x), n, p, P<int64_t>(idx), P<int64_t>(total));
   });
   m.def("cpu_expr_filter", [](intptr_t x, int64_t n, std::vector<int32_t> code,
                               std::vector<double> consts, intptr_t keep) {

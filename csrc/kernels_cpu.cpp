@@ -410,6 +410,16 @@ void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep
   });
 }
 
+void expr_filter_compact(const double* x, int64_t n, const ExprProg& prog, int64_t* idx,
+                         int64_t* total) {
+  int64_t c = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    double vars[kExprVars] = {x[i], 0, 0, 0, 0, 0, 0, 0};
+    if (expr_eval(prog, vars) != 0.0) idx[c++] = i;
+  }
+  total[0] = c;
+}
+
 void keygroups(const uint64_t* keys, int64_t n, int hash_mode, const int32_t* jhash, int max_par,
                int32_t* kg) {
   for (int64_t i = 0; i < n; ++i) {

@@ -1813,6 +1813,102 @@ __global__ __launch_bounds__(256) void expr_filter_kernel(const double* __restri
   }
 }
 
+// Order-preserving filter compaction (chapter1 `filter(usage > 90)`, Main.java:31):
+// the indices of the rows that pass, in input order. Three launches, no atomics on the data path:
+//   1. filter_mask  : a workgroup owns a tile of kFcItems x 256 rows (row = tile + j*256 + tid);
+//                     each wave ballots its lanes' predicates into one 64-bit word per item j
+//                     (words in row order: j-major, wave-minor) and the tile count is written;
+//   2. filter_scan  : one workgroup turns the tile counts into exclusive offsets (+ the total);
+//   3. filter_write : each kept row's position = tile offset + popcount of the tile's earlier
+//                     words + popcount of its own word's lower lanes.
+constexpr int kFcItems = 4;
+constexpr int kFcWords = kFcItems * 4;  // 64-bit words per 256-thread tile
+constexpr int kFcTile = kFcItems * 256;
+
+__global__ __launch_bounds__(256) void filter_mask_kernel(const double* __restrict__ x, int64_t n,
+                                                          ExprProg prog,
+                                                          uint64_t* __restrict__ masks,
+                                                          uint32_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) double fsm[];
+  LdsCol vars{fsm + threadIdx.x, 256};
+  LdsCol stack{fsm + kExprVars * 256 + threadIdx.x, 256};
+  __shared__ uint32_t wcnt[kFcWords];
+  const int64_t tile = (int64_t)blockIdx.x * kFcTile;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < kFcItems; ++j) {
+    const int64_t i = tile + j * 256 + threadIdx.x;
+    bool keep = false;
+    if (i < n) {
+      vars.set(0, x[i]);
+      keep = expr_eval_t(prog, stack, vars) != 0.0;
+    }
+    const uint64_t m = __ballot(keep);
+    if (lane == 0) {
+      masks[(size_t)blockIdx.x * kFcWords + j * 4 + wave] = m;
+      wcnt[j * 4 + wave] = (uint32_t)__popcll(m);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    for (int w = 0; w < kFcWords; ++w) c += wcnt[w];
+    counts[blockIdx.x] = c;
+  }
+}
+
+// Exclusive scan of `nt` tile counts by one 1024-thread workgroup (chunks of 1024, carried).
+__global__ __launch_bounds__(1024) void filter_scan_kernel(const uint32_t* __restrict__ counts,
+                                                           int64_t nt, int64_t* __restrict__ offs,
+                                                           int64_t* __restrict__ total) {
+  __shared__ int64_t part[1024];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < nt; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t v = i < nt ? (int64_t)counts[i] : 0;
+    part[threadIdx.x] = v;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan in LDS
+      const int64_t add = threadIdx.x >= (unsigned)d ? part[threadIdx.x - d] : 0;
+      __syncthreads();
+      part[threadIdx.x] += add;
+      __syncthreads();
+    }
+    if (i < nt) offs[i] = carry + part[threadIdx.x] - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += part[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) total[0] = carry;
+}
+
+__global__ __launch_bounds__(256) void filter_write_kernel(const uint64_t* __restrict__ masks,
+                                                           const int64_t* __restrict__ offs,
+                                                           int64_t n, int64_t* __restrict__ idx) {
+  __shared__ uint32_t wpre[kFcWords];
+  const uint64_t* tm = masks + (size_t)blockIdx.x * kFcWords;
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    for (int w = 0; w < kFcWords; ++w) {
+      wpre[w] = c;
+      c += (uint32_t)__popcll(tm[w]);
+    }
+  }
+  __syncthreads();
+  const int64_t tile = (int64_t)blockIdx.x * kFcTile, off = offs[blockIdx.x];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+  for (int j = 0; j < kFcItems; ++j) {
+    const int w = j * 4 + wave;
+    const uint64_t m = tm[w];
+    const int64_t i = tile + j * 256 + threadIdx.x;
+    if (((m >> lane) & 1ull) && i < n) idx[off + wpre[w] + __popcll(m & below)] = i;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Rolling keyed state (StreamGroupedReduce / keyed ValueState): per-record post-update values
 // in arrival order per key (ComputeCpuMax.java:26 `keyBy(0).max(2)` emits on every record).
@@ -3431,6 +3527,33 @@ void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep
   const size_t lds = (size_t)(kExprVars + prog.depth) * 256 * sizeof(double);
   hipLaunchKernelGGL(expr_filter_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), lds,
                      (hipStream_t)stream, x, n, prog, keep);
+  HIP_CHECK(hipGetLastError());
+}
+
+int64_t filter_compact_scratch_bytes(int64_t n) {
+  const int64_t nt = (n + kFcTile - 1) / kFcTile;
+  return nt * (kFcWords * 8 + 4 + 8);
+}
+
+void expr_filter_compact(const double* x, int64_t n, const ExprProg& prog, void* scratch,
+                         int64_t* idx, int64_t* total, intptr_t stream) {
+  if (n <= 0) {
+    HIP_CHECK(hipMemsetAsync(total, 0, 8, (hipStream_t)stream));
+    return;
+  }
+  const int64_t nt = (n + kFcTile - 1) / kFcTile;
+  uint64_t* masks = (uint64_t*)scratch;
+  int64_t* offs = (int64_t*)(masks + nt * kFcWords);
+  uint32_t* counts = (uint32_t*)(offs + nt);
+  const size_t lds = (size_t)(kExprVars + prog.depth) * 256 * sizeof(double);
+  hipLaunchKernelGGL(filter_mask_kernel, dim3((uint32_t)nt), dim3(256), lds, (hipStream_t)stream,
+                     x, n, prog, masks, counts);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(filter_scan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, counts, nt,
+                     offs, total);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(filter_write_kernel, dim3((uint32_t)nt), dim3(256), 0, (hipStream_t)stream,
+                     masks, offs, n, idx);
   HIP_CHECK(hipGetLastError());
 }
 

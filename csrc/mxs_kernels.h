@@ -144,6 +144,10 @@ void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& plan, uint
              uint64_t* acc_g, uint32_t* cnt_g, uint32_t* occupancy, uint32_t* flags,
              uint64_t* out_vals, intptr_t stream);
 void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep, intptr_t stream);
+// Indices of the rows that pass (input order) and their number; scratch: filter_compact_scratch_bytes.
+int64_t filter_compact_scratch_bytes(int64_t n);
+void expr_filter_compact(const double* x, int64_t n, const ExprProg& prog, void* scratch,
+                         int64_t* idx, int64_t* total, intptr_t stream);
 void step_begin(uint32_t* cursor, int nb, int64_t* stats, intptr_t stream);
 void rolling_lookup_direct(const uint64_t* keys, const uint64_t* vals, uint32_t n, int nsub_log2,
                            int cap_log2, uint64_t* keys_g, int64_t* sort_key, uint64_t* vals_out,
@@ -261,6 +265,8 @@ void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& plan, uint
              uint64_t* acc_g, uint32_t* cnt_g, uint32_t* occupancy, uint32_t* flags,
              uint64_t* out_vals);
 void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep);
+void expr_filter_compact(const double* x, int64_t n, const ExprProg& prog, int64_t* idx,
+                         int64_t* total);
 void step_begin(uint32_t* cursor, int nb, int64_t* stats);
 void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bucket_cap,
                   int cap_log2, int agg, uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g,

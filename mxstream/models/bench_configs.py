@@ -69,8 +69,12 @@ def config1(steps: int, warmup: int, lines_per_step: int = 1 << 20, device: str 
 
     def step_gpu():
         cols = parse_text_gpu(pinned, gspec, " ", 0, device)
-        keep = K.expr_filter(cols[2], prog)
-        return int(keep.sum())
+        # Order-preserving compaction of the alerting rows (mask/scan/write kernels), then the
+        # alert rows (host, cpu, usage) gathered on the device in input order.
+        idx, total = K.expr_filter_compact(cols[2], prog)
+        c = int(total.item())
+        alerts = [col[idx[:c]] for col in cols]
+        return int(alerts[2].numel())
 
     step = step_gpu if device != "cpu" else step_cpu
     if device == "cpu":

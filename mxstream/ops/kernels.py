@@ -371,6 +371,26 @@ def step_finish(stats: torch.Tensor, local_maxts: torch.Tensor, red: torch.Tenso
         m.cpu_step_finish(*args)
 
 
+def expr_filter_compact(x: torch.Tensor, prog: _expr.Program) -> tuple[torch.Tensor, torch.Tensor]:
+    """Indices (int64, input order) of the rows of one f64 column that pass a traced predicate,
+    and their number as a 1-element device tensor (the index buffer has x.numel() entries;
+    entries past the count are unspecified). No host sync."""
+    _check(x, torch.float64, x.numel(), "x", x.device)
+    n = x.numel()
+    idx = torch.empty(max(n, 1), dtype=torch.int64, device=x.device)
+    total = torch.zeros(1, dtype=torch.int64, device=x.device)
+    m = load()
+    code, consts = prog.as_args()
+    if _is_gpu(x):
+        scratch = torch.empty(max(1, m.gpu_filter_compact_scratch_bytes(n)), dtype=torch.uint8,
+                              device=x.device)
+        m.gpu_expr_filter_compact(_p(x), n, code, consts, _p(scratch), _p(idx), _p(total),
+                                  _stream(x))
+    else:
+        m.cpu_expr_filter_compact(_p(x), n, code, consts, _p(idx), _p(total))
+    return idx, total
+
+
 def expr_filter(x: torch.Tensor, prog: _expr.Program) -> torch.Tensor:
     """Evaluate a traced predicate over one f64 column; returns a bool mask."""
     _check(x, torch.float64, x.numel(), "x", x.device)
