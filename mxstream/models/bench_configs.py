@@ -73,7 +73,8 @@ def config1(steps: int, warmup: int, lines_per_step: int = 1 << 20, device: str 
         # alert rows (host, cpu, usage) gathered on the device in input order.
         idx, total = K.expr_filter_compact(cols[2], prog)
         c = int(total.item())
-        alerts = [col[idx[:c]] for col in cols]
+        # string fields are (dictionary ids, Java hashes): the alert carries the ids
+        alerts = [(col[0] if isinstance(col, tuple) else col)[idx[:c]] for col in cols]
         return int(alerts[2].numel())
 
     step = step_gpu if device != "cpu" else step_cpu
