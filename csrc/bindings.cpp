@@ -618,6 +618,11 @@ PYBIND11_MODULE(_mxs_native, m) {
                         P<uint32_t>(ins), stream);
   });
   m.def("gpu_filter_compact_scratch_bytes", &gpu::filter_compact_scratch_bytes);
+  m.def("gpu_line_starts", [](intptr_t buf, int64_t n, intptr_t scratch, intptr_t idx,
+                              intptr_t total, intptr_t stream) {
+    gpu::line_starts(P<uint8_t>(buf), n, P<void>(scratch), P<int64_t>(idx), P<int64_t>(total),
+                     stream);
+  });
   m.def("gpu_expr_filter_compact", [](intptr_t x, int64_t n, std::vector<int32_t> code,
                                       std::vector<double> consts, intptr_t scratch, intptr_t idx,
                                       intptr_t total, intptr_t stream) {

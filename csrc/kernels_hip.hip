@@ -1857,6 +1857,33 @@ __global__ __launch_bounds__(256) void filter_mask_kernel(const double* __restri
   }
 }
 
+// Line starts of a text batch (GPU ingest): positions i < n with i == 0 or buf[i-1] == '\n', in
+// order -- the same tile ballots as filter_mask_kernel, then filter_scan / filter_write.
+__global__ __launch_bounds__(256) void line_start_mask_kernel(const uint8_t* __restrict__ buf,
+                                                              int64_t n,
+                                                              uint64_t* __restrict__ masks,
+                                                              uint32_t* __restrict__ counts) {
+  __shared__ uint32_t wcnt[kFcWords];
+  const int64_t tile = (int64_t)blockIdx.x * kFcTile;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < kFcItems; ++j) {
+    const int64_t i = tile + j * 256 + threadIdx.x;
+    const bool start = i < n && (i == 0 || buf[i - 1] == (uint8_t)'\n');
+    const uint64_t m = __ballot(start);
+    if (lane == 0) {
+      masks[(size_t)blockIdx.x * kFcWords + j * 4 + wave] = m;
+      wcnt[j * 4 + wave] = (uint32_t)__popcll(m);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t c = 0;
+    for (int w = 0; w < kFcWords; ++w) c += wcnt[w];
+    counts[blockIdx.x] = c;
+  }
+}
+
 // Exclusive scan of `nt` tile counts by one 1024-thread workgroup (chunks of 1024, carried).
 __global__ __launch_bounds__(1024) void filter_scan_kernel(const uint32_t* __restrict__ counts,
                                                            int64_t nt, int64_t* __restrict__ offs,
@@ -3527,6 +3554,27 @@ void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep
   const size_t lds = (size_t)(kExprVars + prog.depth) * 256 * sizeof(double);
   hipLaunchKernelGGL(expr_filter_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), lds,
                      (hipStream_t)stream, x, n, prog, keep);
+  HIP_CHECK(hipGetLastError());
+}
+
+void line_starts(const uint8_t* buf, int64_t n, void* scratch, int64_t* idx, int64_t* total,
+                 intptr_t stream) {
+  if (n <= 0) {
+    HIP_CHECK(hipMemsetAsync(total, 0, 8, (hipStream_t)stream));
+    return;
+  }
+  const int64_t nt = (n + kFcTile - 1) / kFcTile;
+  uint64_t* masks = (uint64_t*)scratch;
+  int64_t* offs = (int64_t*)(masks + nt * kFcWords);
+  uint32_t* counts = (uint32_t*)(offs + nt);
+  hipLaunchKernelGGL(line_start_mask_kernel, dim3((uint32_t)nt), dim3(256), 0,
+                     (hipStream_t)stream, buf, n, masks, counts);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(filter_scan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, counts, nt,
+                     offs, total);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(filter_write_kernel, dim3((uint32_t)nt), dim3(256), 0, (hipStream_t)stream,
+                     masks, offs, n, idx);
   HIP_CHECK(hipGetLastError());
 }
 

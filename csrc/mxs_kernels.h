@@ -146,6 +146,9 @@ void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& plan, uint
 void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep, intptr_t stream);
 // Indices of the rows that pass (input order) and their number; scratch: filter_compact_scratch_bytes.
 int64_t filter_compact_scratch_bytes(int64_t n);
+// Line-start offsets of a text batch, in order (scratch: filter_compact_scratch_bytes(n)).
+void line_starts(const uint8_t* buf, int64_t n, void* scratch, int64_t* idx, int64_t* total,
+                 intptr_t stream);
 void expr_filter_compact(const double* x, int64_t n, const ExprProg& prog, void* scratch,
                          int64_t* idx, int64_t* total, intptr_t stream);
 void step_begin(uint32_t* cursor, int nb, int64_t* stats, intptr_t stream);

@@ -1,7 +1,7 @@
 """Text ingestion on the GPU: delimited lines -> typed columns.
 
-``parse_text_gpu`` uploads a batch of text once, finds the line starts (a select over the
-newline mask), and runs the gfx950 ``parse_text`` kernel (csrc/parse_hip.hip): one thread per
+``parse_text_gpu`` uploads a batch of text once, finds the line starts (order-preserving
+wave-ballot / tile-scan / write kernels over the bytes, csrc/kernels_hip.hip `line_starts`), and runs the gfx950 ``parse_text`` kernel (csrc/parse_hip.hip): one thread per
 line, Java field semantics shared with the host runtime. Lines the kernel flags (inputs outside
 its exact fast paths, or real errors) are re-parsed by the C++ runtime on the host and patched
 into the device columns, so results are bit-identical to ``parse_lines`` on the CPU; a genuine
@@ -69,11 +69,16 @@ def parse_text_gpu(data, spec: list[tuple[int, int]], sep: str = " ", offset_s: 
         buf = torch.from_numpy(raw.copy()).to(dev) if n_bytes else torch.zeros(
             1, dtype=torch.uint8, device=dev)
         host = None
-    nl = torch.nonzero(buf[:n_bytes] == 10).flatten()
-    starts = torch.cat([torch.zeros(1, dtype=torch.int64, device=dev), nl + 1])
-    if starts.numel() and int(starts[-1]) >= n_bytes:
-        starts = starts[:-1]  # a trailing newline does not start a line
-    n = starts.numel() if n_bytes else 0
+    # Line starts (0 and every byte after a newline, below n_bytes: a trailing newline starts no
+    # line) by the order-preserving ballot/scan/write kernels; one host sync for the count.
+    starts_buf = torch.empty(max(n_bytes, 1), dtype=torch.int64, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    scratch = torch.empty(max(1, m.gpu_filter_compact_scratch_bytes(n_bytes)), dtype=torch.uint8,
+                          device=dev)
+    m.gpu_line_starts(buf.data_ptr(), n_bytes, scratch.data_ptr(), starts_buf.data_ptr(),
+                      total.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    n = int(total.item()) if n_bytes else 0
+    starts = starts_buf[:n]
     nf = len(spec)
     cols = torch.empty(nf * max(n, 1), dtype=torch.int64, device=dev)
     jh = torch.zeros(nf * max(n, 1), dtype=torch.int32, device=dev)
