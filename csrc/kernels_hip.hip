@@ -1821,7 +1821,7 @@ __global__ __launch_bounds__(256) void expr_filter_kernel(const double* __restri
 //   2. filter_scan  : one workgroup turns the tile counts into exclusive offsets (+ the total);
 //   3. filter_write : each kept row's position = tile offset + popcount of the tile's earlier
 //                     words + popcount of its own word's lower lanes.
-constexpr int kFcItems = 4;
+constexpr int kFcItems = 16;  // 4096 rows per tile: few enough tiles for the one-workgroup scan
 constexpr int kFcWords = kFcItems * 4;  // 64-bit words per 256-thread tile
 constexpr int kFcTile = kFcItems * 256;
 
