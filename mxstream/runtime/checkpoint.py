@@ -51,7 +51,7 @@ class OperatorSnapshot:
     meta: dict = field(default_factory=dict)
 
 
-def freeze_operator(op, tensor_names: tuple[str, ...]):
+def freeze_operator(op, tensor_names: tuple[str, ...], post=None):
     """Synchronous phase of an async snapshot: a shallow copy of ``op`` whose state tensors are
     device-side clones (HBM-speed copies enqueued on the current stream, ordered after every
     kernel that wrote the state) and whose metrics are copied. Returns a thunk that runs the
@@ -65,6 +65,8 @@ def freeze_operator(op, tensor_names: tuple[str, ...]):
     frozen.metrics = copy.copy(op.metrics)
     for name in tensor_names:
         setattr(frozen, name, getattr(op, name).clone())
+    if post is not None:
+        post(frozen)  # host-side state the export reads (e.g. the spill tier): private copies
     ev = None
     dev = getattr(op, "device", None)
     if dev is not None and torch.device(dev).type == "cuda":

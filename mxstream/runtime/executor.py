@@ -208,7 +208,7 @@ class Executor:
                     try:
                         out = self._run_op(n, op, items, now)
                     except Exception as e:  # noqa: BLE001 -- re-raised by _control
-                        self._failure = e
+                        self._record_failure(e)
                         out = []
                 else:
                     out = self._run_op(n, op, items, now)
@@ -240,6 +240,14 @@ class Executor:
         if now is not None:
             out.extend(op.on_processing_time(now))
         return out
+
+    def _record_failure(self, e: Exception) -> None:
+        """Multi-rank: keep the first failure of this rank for the next _control (which raises
+        it on every rank); single rank: raise right away."""
+        if self.comm is None:
+            raise e
+        if self._failure is None:
+            self._failure = e
 
     def _control(self, want_ckpt: bool) -> bool:
         """End-of-step agreement between ranks: a failure anywhere fails every rank (the
@@ -274,18 +282,22 @@ class Executor:
         mp = self.env.max_parallelism
         outs: list[list] = [[] for _ in range(world)]
         last_wm = None
-        for it in expand_columns(items):
-            if isinstance(it, WM):
-                last_wm = it.ts
-                continue
-            if not isinstance(it, Rec):
-                outs[rank].append(it)
-                continue
-            if keyed:
-                sub = (flink_murmur(java_hash(n.key_fn_in(it.value))) % mp) * p // mp
-                outs[sub * world // p].append(it)
-            else:
-                outs[0].append(it)
+        try:
+            for it in expand_columns(items):
+                if isinstance(it, WM):
+                    last_wm = it.ts
+                    continue
+                if not isinstance(it, Rec):
+                    outs[rank].append(it)
+                    continue
+                if keyed:
+                    sub = (flink_murmur(java_hash(n.key_fn_in(it.value))) % mp) * p // mp
+                    outs[sub * world // p].append(it)
+                else:
+                    outs[0].append(it)
+        except Exception as e:  # noqa: BLE001 -- a user key selector failed: agreed in _control
+            self._record_failure(e)
+            outs, last_wm = [[] for _ in range(world)], None
         got = self.comm.all_gather_object((outs, last_wm))
         recv: list = []
         for r_outs, _ in got:
@@ -327,7 +339,11 @@ class Executor:
         storage = self._storage()
         storage.init_job_dirs()
         n = self._next_ckpt
-        states = {self._uid(nd): self.ops[nd.id].snapshot() for nd in self.nodes if nd.id in self.ops}
+
+        def snap_all():
+            return {self._uid(nd): self.ops[nd.id].snapshot() for nd in self.nodes
+                    if nd.id in self.ops}
+
         extra = {
             "clock": self.clock() if isinstance(self.clock, ManualClock) else None,
             "rr": [[self._uid(self._node[a]), self._uid(self._node[b]), v]
@@ -336,13 +352,21 @@ class Executor:
             "nodes": {self._uid(nd): nd.name for nd in self.nodes}}
         d = storage.checkpoint_dir(n)
         if self.comm is None:
-            write_host_checkpoint(d, job_id=storage.job_id, checkpoint_id=n, states=states,
+            write_host_checkpoint(d, job_id=storage.job_id, checkpoint_id=n, states=snap_all(),
                                   extra=extra)
         else:
             # Every rank writes its own state files; rank 0 completes the checkpoint (_metadata)
             # once all of them have, so a crash mid-write leaves no completed checkpoint.
-            files = write_host_states(d, states, self.comm.rank)
-            ranks = self.comm.all_gather_object({"host_operators": files, "extra": extra})
+            try:
+                files, err = write_host_states(d, snap_all(), self.comm.rank), None
+            except Exception as e:  # noqa: BLE001 -- agreed on below, raised on every rank
+                files, err = None, f"{type(e).__name__}: {e}"
+            ranks = self.comm.all_gather_object({"host_operators": files, "extra": extra,
+                                                 "error": err})
+            bad = [(r, x["error"]) for r, x in enumerate(ranks) if x.get("error")]
+            if bad:
+                raise JobExecutionException(f"Job '{self.job_name}': checkpoint {n} failed on "
+                                            f"rank(s) {[r for r, _ in bad]}: {bad[0][1]}")
             if self.comm.rank == 0:
                 write_host_checkpoint(d, job_id=storage.job_id, checkpoint_id=n, states={},
                                       extra=extra, ranks=ranks)
@@ -459,10 +483,13 @@ class Executor:
                 for n in sources:
                     if finished[n.id]:
                         continue
-                    items, done = self.ops[n.id].poll(now)
-                    finished[n.id] = done
-                    for c in self.children[n.id]:
-                        inbox.setdefault((c.id, n.id), []).extend(self._rebalance(n, c, items))
+                    try:
+                        items, done = self.ops[n.id].poll(now)
+                        finished[n.id] = done
+                        for c in self.children[n.id]:
+                            inbox.setdefault((c.id, n.id), []).extend(self._rebalance(n, c, items))
+                    except Exception as e:  # noqa: BLE001 -- multi-rank: re-raised by _control
+                        self._record_failure(e)
                 self._push(inbox, now)
                 if wd is not None:
                     wd.beat()
@@ -478,7 +505,12 @@ class Executor:
                 for c in self.children[n.id]:
                     inbox.setdefault((c.id, n.id), []).append(WM(LONG_MAX))
             self._push(inbox, None)
+            # Multi-rank: the end-of-input firing (MAX watermark) and the finish hooks run under
+            # the same record-then-agree protocol as every step, so a failure in either fails
+            # every rank instead of being swallowed or leaving the peers in a collective.
+            self._control(False)
             self._finish()
+            self._control(False)
         except (JobExecutionException, InjectedFault):
             raise
         except KeyboardInterrupt:
@@ -547,12 +579,20 @@ class Executor:
                 op = self.ops[n.id]
                 if self.comm is not None:
                     items = self._exchange(n, items)
+                    if self._failure is not None:
+                        items = []
                 if not getattr(op, "accepts_columns", False):
                     from .columnar import expand_columns
 
                     items = expand_columns(items)
-                out = op.process(items) if items else []
-                out.extend(op.finish())
+                try:
+                    out = op.process(items) if items else []
+                    out.extend(op.finish())
+                except Exception as e:  # noqa: BLE001 -- multi-rank: re-raised by _control
+                    if self.comm is None:
+                        raise
+                    self._record_failure(e)
+                    out = []
             for c in self.children[n.id]:
                 inbox.setdefault((c.id, n.id), []).extend(out)
 

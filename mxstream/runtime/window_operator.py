@@ -1322,7 +1322,15 @@ class KeyedWindowOperator:
         from .checkpoint import freeze_operator
 
         self._sync_state()
-        return freeze_operator(self, self._state_tensors)
+
+        def private_tier(frozen):
+            # The export reads the spill tier from a worker thread while the step loop keeps
+            # absorbing / purging the live one: the frozen copy gets its own tier as of now, so
+            # keys evicted after the freeze are neither lost nor exported twice.
+            if self.host_tier is not None:
+                frozen.host_tier = self.host_tier.copy()
+
+        return freeze_operator(self, self._state_tensors, post=private_tier)
 
     def snapshot_state(self):
         """Live (key, pane) accumulators grouped by key group, plus the firing bookkeeping."""
@@ -1401,22 +1409,49 @@ class KeyedWindowOperator:
         if not len(rows["key"]):
             return
         keys = torch.from_numpy(np.ascontiguousarray(rows["key"])).to(dev)
+        pane = torch.from_numpy(np.ascontiguousarray(rows["pane"])).to(dev)
+        acc = torch.from_numpy(np.ascontiguousarray(rows["acc"])).to(dev)
+        cnt = torch.from_numpy(np.ascontiguousarray(rows["cnt"])).to(dev)
+        dirty = torch.from_numpy(np.ascontiguousarray(rows["dirty"])).to(dev)
         uniq, inv = torch.unique(keys, return_inverse=True)
+        occ_slots = None
         if self.dense_bits:
             if bool((uniq >> self.dense_bits).any()):
                 raise RuntimeError("restore: key id outside the dense key space (raise max_keys)")
             slots_u = (uniq * self.dense_mul) & ((1 << self.dense_bits) - 1)
+        elif self.host_tier is not None:
+            # With the spill tier the checkpoint may hold more keys than the table: keys without
+            # data in the newest spill_keep_panes panes go back to the tier (as compact_state
+            # would have put them), the others are inserted; any that find no slot join the tier.
+            to_tier = torch.zeros(uniq.numel(), dtype=torch.bool, device=dev)
+            if self.max_seen_pane is not None:
+                newest = torch.full((uniq.numel(),), I64_MIN, dtype=torch.int64, device=dev)
+                newest.scatter_reduce_(0, inv, pane, "amax")
+                keep = self.spill_keep_panes or self.panes_per_window
+                to_tier = newest <= self.max_seen_pane - keep
+            slots_u = torch.full((uniq.numel(),), -1, dtype=torch.int64, device=dev)
+            hot = torch.nonzero(~to_tier).flatten()
+            if hot.numel():
+                slots_u[hot] = K.table_insert(uniq[hot].contiguous(), self.keys_g,
+                                              nsub_log2=self.nsub_log2, cap_log2=self.cap_log2)
+            row_tier = (slots_u < 0)[inv]
+            occ_slots = slots_u[slots_u >= 0]
+            if bool(row_tier.any()):
+                sel = torch.nonzero(row_tier).flatten()
+                self.host_tier.absorb(keys[sel].cpu().numpy().view(np.uint64),
+                                      pane[sel].cpu().numpy(), acc[sel].cpu().numpy(),
+                                      cnt[sel].cpu().numpy(), dirty[sel].cpu().numpy())
+                sel = torch.nonzero(~row_tier).flatten()
+                keys, pane, acc, cnt, dirty = keys[sel], pane[sel], acc[sel], cnt[sel], dirty[sel]
+                inv = inv[sel]
+                slots_u = torch.where(slots_u < 0, torch.zeros_like(slots_u), slots_u)
         else:
             slots_u = K.table_insert(uniq.contiguous(), self.keys_g, nsub_log2=self.nsub_log2,
                                      cap_log2=self.cap_log2)
         if bool((slots_u < 0).any()):
             raise RuntimeError("restore: keyed state does not fit the table (raise max_keys)")
         slot = slots_u[inv]
-        pane = torch.from_numpy(np.ascontiguousarray(rows["pane"])).to(dev)
         idx = (pane & (self.ring - 1)) * self.nslots + slot
-        acc = torch.from_numpy(np.ascontiguousarray(rows["acc"])).to(dev)
-        cnt = torch.from_numpy(np.ascontiguousarray(rows["cnt"])).to(dev)
-        dirty = torch.from_numpy(np.ascontiguousarray(rows["dirty"])).to(dev)
         u, inv = torch.unique(idx, return_inverse=True)
         if u.numel() == idx.numel():
             self.acc_g[idx], self.cnt_g[idx], self.dirty_g[idx] = acc, cnt, dirty
@@ -1435,5 +1470,6 @@ class KeyedWindowOperator:
             self.dlist[:ds.numel()] = ds
             self.dlist_n.fill_(ds.numel())
             self.slot_mark[ds.long()] = 1
-        self.occ.copy_(torch.bincount(slots_u >> self.cap_log2, minlength=self.nsub)
+        occ_slots = slots_u if occ_slots is None else occ_slots
+        self.occ.copy_(torch.bincount(occ_slots >> self.cap_log2, minlength=self.nsub)
                        .to(torch.int32))

@@ -136,6 +136,13 @@ class HostWindowTier:
         self._cols = self._empty()
         self._merged = 0
 
+    def copy(self) -> "HostWindowTier":
+        """An independent copy (the frozen tier of an asynchronous snapshot)."""
+        t = HostWindowTier(self.agg)
+        t._cols = {k: v.copy() for k, v in self._cols.items()}
+        t._merged, t.rows_in = self._merged, self.rows_in
+        return t
+
 
 def merge_fire(agg: int, dev_keys, dev_raw, dev_cnt, host_part, only_dirty: bool,
                map_prog: E.Program, filter_prog: E.Program, wstart: int, wend: int):

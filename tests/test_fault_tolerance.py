@@ -173,3 +173,61 @@ def test_multirank_failure_restarts_every_rank_from_checkpoint(tmp_path):
     assert all(c_got[k] >= v for k, v in c_clean.items())  # at-least-once sink
     meta = read_metadata(got[0][2]["lastCheckpointPath"])
     assert meta["world"] == 2 and len(meta["ranks"]) == 2
+
+
+# ---- multi-rank: a failure in the end-of-input firing fails every rank -------------------------
+def _eoi_worker(rank, world, port, fault, q):
+    import os
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        out = []
+        env = StreamExecutionEnvironment(4, clock=ManualClock(0))
+        env.config.native = "off"
+        env.config.fault_injection = fault if rank == 1 else None
+        env.set_stream_time_characteristic(TimeCharacteristic.EventTime)
+        # One window per key that only the end-of-input MAX watermark fires: the map after the
+        # window first receives records in the final firing, where the fault is injected.
+        (env.from_timed_collection(_events(40))
+         .assign_timestamps_and_watermarks(
+             BoundedOutOfOrdernessTimestampExtractor(Time.milliseconds(100), extractor=lambda e: e[2]))
+         .map(lambda e: Tuple2(e[0], e[1]))
+         .key_by(0)
+         .time_window(Time.milliseconds(10_000_000))
+         .reduce(lambda a, b: Tuple2(a.f0, a.f1 + b.f1))
+         .map(lambda t: t).name("EoiMap")
+         .collect(out))
+        env.execute("ft-eoi")
+        q.put((rank, "ok"))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, type(e).__name__ + ": " + str(e)))
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def test_multirank_failure_in_end_of_input_firing_fails_every_rank():
+    import os
+    import socket
+
+    import torch.multiprocessing as mp
+
+    for k in ("RANK", "WORLD_SIZE"):
+        os.environ.pop(k, None)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_eoi_worker, args=(r, 2, port, "EoiMap:1", q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    # Neither rank may report success (the failure was swallowed before) or hang.
+    assert all(r != "ok" for _, r in res), res
+    assert any("injected fault" in r for _, r in res), res

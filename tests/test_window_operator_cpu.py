@@ -456,3 +456,71 @@ def test_compact_state_drops_dead_keys():
     got = sorted((r.window_start, r.refire, int(a), int(b), int(c), float(x))
                  for r in rows for a, b, c, x in zip(r.keys, r.raw, r.counts, r.values))
     assert dropped > 0 and got == ref
+
+
+def _spill_op(**kw):
+    from mxstream.ops import expr as E
+    from mxstream.ops import kernels as K
+    from mxstream.runtime.window_operator import KeyedWindowOperator
+
+    args = dict(size=6000, slide=2000, lateness=3000, agg=K.AGG_SUM_I64, device="cpu",
+                batch_capacity=6000, ooo_bound=500,
+                map_prog=E.compile_expr(E.var(E.VAR_RESULT) * 0.5),
+                filter_prog=E.compile_expr(E.var(E.VAR_COUNT) > 1))
+    args.update(kw)
+    return KeyedWindowOperator(**args)
+
+
+def _rows_key(rows):
+    return sorted((r.window_start, r.refire, int(a), int(b), int(c), float(x))
+                  for r in rows for a, b, c, x in zip(r.keys, r.raw, r.counts, r.values))
+
+
+def test_spill_checkpoint_restores_into_the_small_table():
+    """A checkpoint taken with more keys than the table holds restores into an operator with the
+    same small table: cold keys return to the host tier, the rest are inserted."""
+    batches = _drift_batches(12, 6000, seed=4)
+    ref, _ = _run_windows(batches, max_keys=60_000)
+    small = dict(max_keys=3000, spill=True, spill_check_steps=1, spill_load=0.5, cap_log2=7,
+                 spill_keep_panes=1)
+    op = _spill_op(**small)
+    rows = []
+    for k, t, v in batches[:7]:
+        rows += op.process(k, t, v)
+    rows += op.flush()
+    snap = op.snapshot_state()
+    assert len(np.unique(snap.columns["key"])) > op.nslots  # more keys than slots
+    op2 = _spill_op(**small)
+    op2.restore_state(snap.columns, snap.meta)
+    assert op2.host_state_bytes() > 0
+    for k, t, v in batches[7:]:
+        rows += op2.process(k, t, v)
+    rows += op2.finish()
+    assert _rows_key(rows) == ref
+
+
+def test_async_snapshot_with_spill_is_isolated_from_later_evictions():
+    """The async export reads a private copy of the spill tier: evictions between the freeze and
+    the export neither lose rows nor export them twice (restore equals a synchronous snapshot)."""
+    batches = _drift_batches(10, 6000, seed=5)
+    small = dict(max_keys=3000, spill=True, spill_check_steps=1, spill_load=0.5, cap_log2=7,
+                 spill_keep_panes=1)
+    op = _spill_op(**small)
+    for k, t, v in batches[:6]:
+        op.process(k, t, v)
+    op.flush()
+    sync = op.snapshot_state()
+    run = op.snapshot_state_async()
+    op.compact_state(op.max_seen_pane - 1)  # evicts more keys into the live tier
+    frozen = run()
+
+    def canon(snap):
+        c = snap.columns
+        df = {}
+        for key, pane, acc, cnt in zip(c["key"].tolist(), c["pane"].tolist(), c["acc"].tolist(),
+                                       c["cnt"].tolist()):
+            a0, c0 = df.get((key, pane), (0, 0))
+            df[(key, pane)] = (a0 + acc, c0 + cnt)
+        return df
+
+    assert canon(frozen) == canon(sync)
