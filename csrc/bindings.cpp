@@ -12,6 +12,7 @@
 #include <tuple>
 #include <vector>
 
+#include "ingest.h"
 #include "mxs_kernels.h"
 #include "mxs_runtime.h"
 
@@ -180,6 +181,67 @@ RollPlan make_roll(py::dict d) {
   p.bucket_cap = d["bucket_cap"].cast<uint32_t>();
   p.emit = d["emit"].cast<int32_t>();
   return p;
+}
+
+IngestSpec make_ingest_spec(py::dict d) {
+  IngestSpec sp;
+  std::memset(&sp, 0, sizeof(sp));
+  auto fields = d["fields"].cast<std::vector<int32_t>>();
+  auto kinds = d["kinds"].cast<std::vector<int32_t>>();
+  if (fields.empty() || fields.size() > (size_t)kIngestMaxFields || fields.size() != kinds.size())
+    throw std::invalid_argument("ingest: 1..8 fields with one kind each");
+  sp.nfields = (int32_t)fields.size();
+  sp.nstr = 0;
+  for (int f = 0; f < sp.nfields; ++f) {
+    if (fields[f] < 0 || kinds[f] < IK_STR || kinds[f] > IK_ISO_SEC)
+      throw std::invalid_argument("ingest: bad field spec");
+    sp.field[f] = fields[f];
+    sp.kind[f] = kinds[f];
+    sp.sidx[f] = kinds[f] == IK_STR ? sp.nstr++ : -1;
+  }
+  for (int f = sp.nfields; f < kIngestMaxFields; ++f) sp.sidx[f] = -1;
+  sp.ts_col = d["ts_col"].cast<int32_t>();
+  if (sp.ts_col >= sp.nfields || (sp.ts_col >= 0 && kinds[sp.ts_col] == IK_STR))
+    throw std::invalid_argument("ingest: bad timestamp column");
+  sp.offset_s = d["offset_s"].cast<int64_t>();
+  const auto sep = d["sep"].cast<std::string>();
+  if (sep.size() != 1) throw std::invalid_argument("ingest: separator must be one byte");
+  sp.sep = (unsigned char)sep[0];
+  return sp;
+}
+
+IngestOut make_ingest_out(py::dict d) {
+  IngestOut o;
+  o.cols = P<int64_t>(d["cols"].cast<intptr_t>());
+  o.ids = P<int32_t>(d["ids"].cast<intptr_t>());
+  o.status = P<uint8_t>(d["status"].cast<intptr_t>());
+  o.spos = P<int64_t>(d["spos"].cast<intptr_t>());
+  o.slen = P<int32_t>(d["slen"].cast<intptr_t>());
+  o.sjh = P<int32_t>(d["sjh"].cast<intptr_t>());
+  o.sslot = P<int32_t>(d["sslot"].cast<intptr_t>());
+  o.shash = P<uint64_t>(d["shash"].cast<intptr_t>());
+  o.nflag = P<uint32_t>(d["nflag"].cast<intptr_t>());
+  o.maxts = P<int64_t>(d["maxts"].cast<intptr_t>());
+  return o;
+}
+
+DictState make_dict(py::dict d) {
+  DictState s;
+  s.tab_h = P<uint64_t>(d["tab_h"].cast<intptr_t>());
+  s.tab_id = P<int32_t>(d["tab_id"].cast<intptr_t>());
+  s.tab_first = P<int64_t>(d["tab_first"].cast<intptr_t>());
+  const int64_t cap = d["cap"].cast<int64_t>();
+  if (cap < 2 || (cap & (cap - 1)) || cap > (int64_t)1 << 32)
+    throw std::invalid_argument("dictionary table capacity must be a power of two <= 2^32");
+  s.mask = (uint32_t)(cap - 1);
+  s.id_off = P<int64_t>(d["id_off"].cast<intptr_t>());
+  s.id_len = P<int32_t>(d["id_len"].cast<intptr_t>());
+  s.id_jh = P<int32_t>(d["id_jh"].cast<intptr_t>());
+  s.arena = P<uint8_t>(d["arena"].cast<intptr_t>());
+  s.arena_cap = d["arena_cap"].cast<int64_t>();
+  s.id_cap = d["id_cap"].cast<int64_t>();
+  s.ctr = P<int64_t>(d["ctr"].cast<intptr_t>());
+  return s;
 }
 
 }  // namespace
@@ -618,6 +680,68 @@ PYBIND11_MODULE(_mxs_native, m) {
                         P<uint32_t>(ins), stream);
   });
   m.def("gpu_filter_compact_scratch_bytes", &gpu::filter_compact_scratch_bytes);
+  // ---- device text ingest + string dictionary (csrc/ingest*.{h,hip,cpp}) ----
+  m.def("ingest_parse", [](bool cuda, intptr_t text, int64_t text_len, intptr_t starts, int64_t n,
+                           py::dict spec, py::dict out, py::dict dict, intptr_t stream) {
+    const IngestSpec sp = make_ingest_spec(spec);
+    const IngestOut o = make_ingest_out(out);
+    const DictState d = make_dict(dict);
+    if (cuda) {
+      gpu::ingest_parse(P<char>(text), text_len, P<int64_t>(starts), n, sp, o, d, stream);
+    } else {
+      py::gil_scoped_release nogil;
+      cpu::ingest_parse(P<char>(text), text_len, P<int64_t>(starts), n, sp, o, d);
+    }
+  });
+  m.def("dict_assign_new", [](bool cuda, intptr_t text, int64_t n, int32_t nstr, py::dict out,
+                              py::dict dict, intptr_t scratch, intptr_t newpos, intptr_t stream) {
+    const IngestOut o = make_ingest_out(out);
+    const DictState d = make_dict(dict);
+    if (cuda) {
+      gpu::dict_assign_new(P<char>(text), n, nstr, o, d, P<void>(scratch), P<int64_t>(newpos),
+                           stream);
+    } else {
+      py::gil_scoped_release nogil;
+      cpu::dict_assign_new(P<char>(text), n, nstr, o, d, P<int64_t>(newpos));
+    }
+  });
+  m.def("dict_rehash", [](bool cuda, intptr_t old_h, intptr_t old_id, int64_t old_cap,
+                          py::dict dict, intptr_t stream) {
+    const DictState d = make_dict(dict);
+    if (cuda) gpu::dict_rehash(P<uint64_t>(old_h), P<int32_t>(old_id), old_cap, d, stream);
+    else cpu::dict_rehash(P<uint64_t>(old_h), P<int32_t>(old_id), old_cap, d);
+  });
+  m.def("ingest_filter_compact", [](bool cuda, intptr_t cols, int64_t n, int32_t nf,
+                                    int32_t dbl_mask, std::vector<int32_t> code,
+                                    std::vector<double> consts, intptr_t scratch, intptr_t idx,
+                                    intptr_t total, intptr_t stream) {
+    if (nf < 1 || nf > kIngestMaxFields) throw std::invalid_argument("ingest filter: 1..8 columns");
+    const ExprProg p = make_prog(code, consts);
+    if (cuda) {
+      gpu::ingest_filter_compact(P<int64_t>(cols), n, nf, dbl_mask, p, P<void>(scratch),
+                                 P<int64_t>(idx), P<int64_t>(total), stream);
+    } else {
+      py::gil_scoped_release nogil;
+      cpu::ingest_filter_compact(P<int64_t>(cols), n, nf, dbl_mask, p, P<int64_t>(idx),
+                                 P<int64_t>(total));
+    }
+  });
+  m.def("ingest_gather", [](bool cuda, intptr_t cols, int64_t n, int32_t nf, intptr_t ids,
+                            int32_t nstr, intptr_t idx, intptr_t total, intptr_t out_cols,
+                            intptr_t out_ids, int64_t out_stride, intptr_t stream) {
+    if (cuda) {
+      gpu::ingest_gather(P<int64_t>(cols), n, nf, P<int32_t>(ids), nstr, P<int64_t>(idx),
+                         P<int64_t>(total), P<int64_t>(out_cols), P<int32_t>(out_ids), out_stride,
+                         stream);
+    } else {
+      cpu::ingest_gather(P<int64_t>(cols), n, nf, P<int32_t>(ids), nstr, P<int64_t>(idx),
+                         P<int64_t>(total), P<int64_t>(out_cols), P<int32_t>(out_ids), out_stride);
+    }
+  });
+  m.def("cpu_line_starts", [](intptr_t buf, int64_t n, intptr_t idx, intptr_t total) {
+    py::gil_scoped_release nogil;
+    cpu::line_starts(P<uint8_t>(buf), n, P<int64_t>(idx), P<int64_t>(total));
+  });
   m.def("gpu_line_starts", [](intptr_t buf, int64_t n, intptr_t scratch, intptr_t idx,
                               intptr_t total, intptr_t stream) {
     gpu::line_starts(P<uint8_t>(buf), n, P<void>(scratch), P<int64_t>(idx), P<int64_t>(total),

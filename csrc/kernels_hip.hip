@@ -1821,9 +1821,7 @@ __global__ __launch_bounds__(256) void expr_filter_kernel(const double* __restri
 //   2. filter_scan  : one workgroup turns the tile counts into exclusive offsets (+ the total);
 //   3. filter_write : each kept row's position = tile offset + popcount of the tile's earlier
 //                     words + popcount of its own word's lower lanes.
-constexpr int kFcItems = 16;  // 4096 rows per tile: few enough tiles for the one-workgroup scan
-constexpr int kFcWords = kFcItems * 4;  // 64-bit words per 256-thread tile
-constexpr int kFcTile = kFcItems * 256;
+// Tile constants kFcItems / kFcWords / kFcTile: mxs_kernels.h (shared with csrc/ingest_hip.hip).
 
 __global__ __launch_bounds__(256) void filter_mask_kernel(const double* __restrict__ x, int64_t n,
                                                           ExprProg prog,
@@ -3570,6 +3568,16 @@ void line_starts(const uint8_t* buf, int64_t n, void* scratch, int64_t* idx, int
   hipLaunchKernelGGL(line_start_mask_kernel, dim3((uint32_t)nt), dim3(256), 0,
                      (hipStream_t)stream, buf, n, masks, counts);
   HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(filter_scan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, counts, nt,
+                     offs, total);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(filter_write_kernel, dim3((uint32_t)nt), dim3(256), 0, (hipStream_t)stream,
+                     masks, offs, n, idx);
+  HIP_CHECK(hipGetLastError());
+}
+
+void compact_from_masks(const uint64_t* masks, const uint32_t* counts, int64_t nt, int64_t n,
+                        int64_t* offs, int64_t* idx, int64_t* total, intptr_t stream) {
   hipLaunchKernelGGL(filter_scan_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, counts, nt,
                      offs, total);
   HIP_CHECK(hipGetLastError());

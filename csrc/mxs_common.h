@@ -673,6 +673,45 @@ MXS_HD bool iso_local_datetime(const char* s, int64_t len, int64_t offset_s, int
   return true;
 }
 
+// java.lang.String.hashCode() of UTF-8 text, over its UTF-16 code units (invalid bytes decode
+// to U+FFFD, supplementary code points to surrogate pairs): keyBy on a String field hashes the
+// Java string (ComputeCpuMax.java:26 keyBy(0) -> Tuple1<String>.hashCode()). Shared by the host
+// StringDict (csrc/runtime.cpp) and the GPU dictionary (csrc/ingest_hip.hip).
+MXS_HD int32_t java_hash_utf8(const char* s, int64_t n) {
+  uint32_t h = 0;
+  int64_t i = 0;
+  while (i < n) {
+    const uint32_t c = (unsigned char)s[i];
+    uint32_t cp = 0xFFFDu;
+    int64_t len = 1;
+    if (c < 0x80u) {
+      cp = c;
+    } else if ((c >> 5) == 0x6u && i + 1 < n && ((unsigned char)s[i + 1] >> 6) == 2u) {
+      cp = ((c & 0x1Fu) << 6) | ((unsigned char)s[i + 1] & 0x3Fu);
+      len = 2;
+    } else if ((c >> 4) == 0xEu && i + 2 < n && ((unsigned char)s[i + 1] >> 6) == 2u &&
+               ((unsigned char)s[i + 2] >> 6) == 2u) {
+      cp = ((c & 0x0Fu) << 12) | (((unsigned char)s[i + 1] & 0x3Fu) << 6) |
+           ((unsigned char)s[i + 2] & 0x3Fu);
+      len = 3;
+    } else if ((c >> 3) == 0x1Eu && i + 3 < n && ((unsigned char)s[i + 1] >> 6) == 2u &&
+               ((unsigned char)s[i + 2] >> 6) == 2u && ((unsigned char)s[i + 3] >> 6) == 2u) {
+      cp = ((c & 0x07u) << 18) | (((unsigned char)s[i + 1] & 0x3Fu) << 12) |
+           (((unsigned char)s[i + 2] & 0x3Fu) << 6) | ((unsigned char)s[i + 3] & 0x3Fu);
+      len = 4;
+    }
+    if (cp >= 0x10000u) {
+      cp -= 0x10000u;
+      h = 31u * h + (0xD800u + (cp >> 10));
+      h = 31u * h + (0xDC00u + (cp & 0x3FFu));
+    } else {
+      h = 31u * h + cp;
+    }
+    i += len;
+  }
+  return (int32_t)h;
+}
+
 // Order-preserving map of an f64 bit pattern to u64 (ascending = Java Double.compareTo order:
 // -0.0 < 0.0, every NaN canonical and largest) and its inverse.
 MXS_HD uint64_t f64_order_bits(uint64_t b) {

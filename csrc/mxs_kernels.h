@@ -108,6 +108,16 @@ struct D2HBatch {
 
 constexpr int64_t kRollHistMaxSlots = 16384;  // LDS running-count table of the emit pass
 
+// Order-preserving compaction tiles (filter_mask / line_starts / ingest masks): a 256-thread
+// workgroup owns kFcTile rows, one 64-bit ballot word per wave and item.
+constexpr int kFcItems = 16;  // 4096 rows per tile: few enough tiles for the one-workgroup scan
+constexpr int kFcWords = kFcItems * 4;  // 64-bit words per 256-thread tile
+constexpr int kFcTile = kFcItems * 256;
+
+struct IngestSpec;
+struct IngestOut;
+struct DictState;
+
 namespace gpu {
 int device_count();
 int set_spin_schedule();
@@ -151,6 +161,22 @@ void line_starts(const uint8_t* buf, int64_t n, void* scratch, int64_t* idx, int
                  intptr_t stream);
 void expr_filter_compact(const double* x, int64_t n, const ExprProg& prog, void* scratch,
                          int64_t* idx, int64_t* total, intptr_t stream);
+// Scan + write half of the compaction over tile masks/counts made by any mask kernel.
+void compact_from_masks(const uint64_t* masks, const uint32_t* counts, int64_t nt, int64_t n,
+                        int64_t* offs, int64_t* idx, int64_t* total, intptr_t stream);
+// Device text ingest + string dictionary (csrc/ingest_hip.hip, csrc/ingest.h).
+void ingest_parse(const char* text, int64_t text_len, const int64_t* starts, int64_t n,
+                  const IngestSpec& sp, const IngestOut& o, const DictState& d, intptr_t stream);
+void dict_assign_new(const char* text, int64_t n, int32_t nstr, const IngestOut& o,
+                     const DictState& d, void* scratch, int64_t* newpos, intptr_t stream);
+void dict_rehash(const uint64_t* old_h, const int32_t* old_id, int64_t old_cap, const DictState& d,
+                 intptr_t stream);
+void ingest_filter_compact(const int64_t* cols, int64_t n, int32_t nf, int32_t dbl_mask,
+                           const ExprProg& prog, void* scratch, int64_t* idx, int64_t* total,
+                           intptr_t stream);
+void ingest_gather(const int64_t* cols, int64_t n, int32_t nf, const int32_t* ids, int32_t nstr,
+                   const int64_t* idx, const int64_t* total, int64_t* out_cols, int32_t* out_ids,
+                   int64_t out_stride, intptr_t stream);
 void step_begin(uint32_t* cursor, int nb, int64_t* stats, intptr_t stream);
 void rolling_lookup_direct(const uint64_t* keys, const uint64_t* vals, uint32_t n, int nsub_log2,
                            int cap_log2, uint64_t* keys_g, int64_t* sort_key, uint64_t* vals_out,
@@ -271,6 +297,18 @@ void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep
 void expr_filter_compact(const double* x, int64_t n, const ExprProg& prog, int64_t* idx,
                          int64_t* total);
 void step_begin(uint32_t* cursor, int nb, int64_t* stats);
+// C++ twins of the device text ingest (csrc/ingest_cpu.cpp): identical outputs and ids.
+void line_starts(const uint8_t* buf, int64_t n, int64_t* idx, int64_t* total);
+void ingest_parse(const char* text, int64_t text_len, const int64_t* starts, int64_t n,
+                  const IngestSpec& sp, const IngestOut& o, const DictState& d);
+void dict_assign_new(const char* text, int64_t n, int32_t nstr, const IngestOut& o,
+                     const DictState& d, int64_t* newpos);
+void dict_rehash(const uint64_t* old_h, const int32_t* old_id, int64_t old_cap, const DictState& d);
+void ingest_filter_compact(const int64_t* cols, int64_t n, int32_t nf, int32_t dbl_mask,
+                           const ExprProg& prog, int64_t* idx, int64_t* total);
+void ingest_gather(const int64_t* cols, int64_t n, int32_t nf, const int32_t* ids, int32_t nstr,
+                   const int64_t* idx, const int64_t* total, int64_t* out_cols, int32_t* out_ids,
+                   int64_t out_stride);
 void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bucket_cap,
                   int cap_log2, int agg, uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g,
                   uint32_t* flags, const ExprProg& filt, uint64_t* out_key, uint64_t* out_val,

@@ -86,44 +86,7 @@ void mxs_log(LogLevel level, const std::string& logger, const std::string& msg) 
 // Java String.hashCode over the UTF-16 encoding of UTF-8 input (invalid bytes -> U+FFFD).
 // ------------------------------------------------------------------------------------------
 int32_t java_string_hash(std::string_view s) {
-  uint32_t h = 0;
-  auto add = [&](uint32_t unit) { h = 31u * h + unit; };
-  size_t i = 0;
-  const size_t n = s.size();
-  while (i < n) {
-    const unsigned char c = (unsigned char)s[i];
-    uint32_t cp;
-    size_t len;
-    if (c < 0x80) {
-      cp = c;
-      len = 1;
-    } else if ((c >> 5) == 0x6 && i + 1 < n && ((unsigned char)s[i + 1] >> 6) == 2) {
-      cp = ((c & 0x1Fu) << 6) | ((unsigned char)s[i + 1] & 0x3Fu);
-      len = 2;
-    } else if ((c >> 4) == 0xE && i + 2 < n && ((unsigned char)s[i + 1] >> 6) == 2 &&
-               ((unsigned char)s[i + 2] >> 6) == 2) {
-      cp = ((c & 0x0Fu) << 12) | (((unsigned char)s[i + 1] & 0x3Fu) << 6) |
-           ((unsigned char)s[i + 2] & 0x3Fu);
-      len = 3;
-    } else if ((c >> 3) == 0x1E && i + 3 < n && ((unsigned char)s[i + 1] >> 6) == 2 &&
-               ((unsigned char)s[i + 2] >> 6) == 2 && ((unsigned char)s[i + 3] >> 6) == 2) {
-      cp = ((c & 0x07u) << 18) | (((unsigned char)s[i + 1] & 0x3Fu) << 12) |
-           (((unsigned char)s[i + 2] & 0x3Fu) << 6) | ((unsigned char)s[i + 3] & 0x3Fu);
-      len = 4;
-    } else {
-      cp = 0xFFFD;
-      len = 1;
-    }
-    if (cp >= 0x10000) {
-      cp -= 0x10000;
-      add(0xD800u + (cp >> 10));
-      add(0xDC00u + (cp & 0x3FFu));
-    } else {
-      add(cp);
-    }
-    i += len;
-  }
-  return (int32_t)h;
+  return java_hash_utf8(s.data(), (int64_t)s.size());  // mxs_common.h (shared with the GPU)
 }
 
 class StringDict {

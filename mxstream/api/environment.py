@@ -27,6 +27,10 @@ class ExecutionConfig:
     # cpu | cuda: where native operators run (MXS_DEVICE overrides the default)
     device: str = field(default_factory=lambda: os.environ.get("MXS_DEVICE", "cpu"))
     batch_size: int = 1 << 16
+    # Text jobs whose parse map traces (api/textplan.py): "device" parses on `device` with the
+    # device string dictionary (ops/ingest.py; the C++ twins when device is "cpu"), "host" with
+    # the multi-threaded host parser, "auto" = device on a GPU. MXS_TEXT_INGEST overrides.
+    text_ingest: str = field(default_factory=lambda: os.environ.get("MXS_TEXT_INGEST", "auto"))
     global_job_parameters: dict = field(default_factory=dict)
     # "<operator name>:<records>[:<attempts>]" (tests / chaos runs); default from MXS_FAULT.
     fault_injection: str | None = field(default_factory=lambda: os.environ.get("MXS_FAULT"))

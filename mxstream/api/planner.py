@@ -208,8 +208,12 @@ def _lower_text(env, sinks) -> None:
                 fnode = kids[0]
             except T.TraceError:
                 filt = None
-        t.factory = (lambda spec=spec, ts_spec=ts_spec, bound=bound, filt=filt:
-                     TextParseOp(spec, ts_spec=ts_spec, bound=bound, filter_prog=filt))
+        mode = getattr(env.config, "text_ingest", "auto")
+        dev = str(env.config.device)
+        ingest_dev = dev if (mode == "device" or (mode == "auto" and dev.startswith("cuda"))) \
+            else None
+        t.factory = (lambda spec=spec, ts_spec=ts_spec, bound=bound, filt=filt, d=ingest_dev:
+                     TextParseOp(spec, ts_spec=ts_spec, bound=bound, filter_prog=filt, device=d))
         t.parents = [parent]
         if fnode is not None:
             fnode.factory = PassThroughOp

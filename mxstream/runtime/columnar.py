@@ -85,6 +85,74 @@ class ColumnBatch:
                            None if self.sub is None else self.sub[idx])
 
 
+class DeviceColumnBatch(ColumnBatch):
+    """A ColumnBatch whose columns live on the device (the device text ingest,
+    ops/ingest.py): string columns hold int32 ids of a DeviceDict, ``ts`` is a device int64
+    column. Native operators read the columns in place; anything that needs host values
+    (host operators, print sinks, late side outputs) materialises ``host()`` once."""
+
+    def __init__(self, n: int, cols: list, kinds: tuple, strings, ts, *, sub0: int = 0,
+                 parallelism: int = 1, line_idx=None, max_ts: int | None = None):
+        self.n, self.cols, self.kinds, self.strings, self.ts = n, cols, kinds, strings, ts
+        self.sub0, self.parallelism, self.line_idx, self.max_ts = sub0, parallelism, line_idx, max_ts
+        self._cache = {}
+        self._host = None
+
+    @property
+    def sub(self):
+        return self.host().sub
+
+    def host(self) -> ColumnBatch:
+        if self._host is None:
+            cols = []
+            for c, k in zip(self.cols, self.kinds):
+                a = c[:self.n].cpu().numpy()
+                cols.append(a.astype(np.int64) if k == FK_STR else a)
+            line = (self.line_idx[:self.n].cpu().numpy() if self.line_idx is not None
+                    else np.arange(self.n, dtype=np.int64))
+            sub = ((self.sub0 + line) % max(1, self.parallelism)).astype(np.int32)
+            ts = None if self.ts is None else self.ts[:self.n].cpu().numpy()
+            self._host = ColumnBatch(self.n, cols, self.kinds, self.strings, ts, sub)
+        return self._host
+
+    def field_value(self, j: int, i: int):
+        return self.host().field_value(j, i)
+
+    def value(self, i: int) -> Tuple:
+        return self.host().value(i)
+
+    def to_recs(self) -> list[Rec]:
+        return self.host().to_recs()
+
+    def take(self, mask: np.ndarray) -> ColumnBatch:
+        return self.host().take(mask)
+
+
+def concat_device(batches: list) -> DeviceColumnBatch:
+    """Concatenate device batches of one layout and one dictionary."""
+    if len(batches) == 1:
+        return batches[0]
+    import torch
+
+    b0 = batches[0]
+    if any(b.kinds != b0.kinds or b.strings is not b0.strings for b in batches):
+        raise TypeError("incompatible column batches")
+    cols = [torch.cat([b.cols[j][:b.n] for b in batches]) for j in range(len(b0.cols))]
+    ts = None if b0.ts is None else torch.cat([b.ts[:b.n] for b in batches])
+    out = DeviceColumnBatch(sum(b.n for b in batches), cols, b0.kinds, b0.strings, ts)
+    out._host = _concat_host([b.host() for b in batches])  # sub / late rows, if ever needed
+    return out
+
+
+def _concat_host(batches: list) -> ColumnBatch:
+    b0 = batches[0]
+    cat = lambda xs: None if xs[0] is None else np.concatenate(xs)  # noqa: E731
+    return ColumnBatch(sum(b.n for b in batches),
+                       [np.concatenate([b.cols[j] for b in batches]) for j in range(len(b0.cols))],
+                       b0.kinds, b0.strings, cat([b.ts for b in batches]),
+                       cat([b.sub for b in batches]))
+
+
 def expand_columns(items: list) -> list:
     """ColumnBatch items -> Recs, for operators without columnar input."""
     if not any(isinstance(it, ColumnBatch) for it in items):
@@ -117,12 +185,15 @@ class TextParseOp(Operator):
     name = "Map"
 
     def __init__(self, spec, *, ts_spec=None, bound: int = 0, filter_prog=None,
-                 threads: int | None = None):
+                 threads: int | None = None, device: str | None = None):
         self.spec = spec
         self.ts_spec = ts_spec
         self.bound = int(bound)
         self.filter_prog = filter_prog
         self.threads = threads or min(16, os.cpu_count() or 1)
+        # device: parse on this device (ops/ingest.py: device parse kernels + device string
+        # dictionary, C++ twins on "cpu"); None: the host C++ parser (parse_lines).
+        self.device = device
         self.cur_max = LONG_MIN + self.bound  # BoundedOutOfOrdernessTimestampExtractor state
         self.cur_wm = LONG_MIN
 
@@ -131,7 +202,6 @@ class TextParseOp(Operator):
         from ..ops.native import load
 
         self.m = load()
-        self.strings = self.m.StringDict()
         fields = list(self.spec.fields)
         if self.ts_spec is not None:
             if self.ts_spec.sep != self.spec.sep:
@@ -140,6 +210,36 @@ class TextParseOp(Operator):
         self.pspec = fields
         self.offset_s = self.spec.offset_s if self.ts_spec is None else (
             self.ts_spec.offset_s or self.spec.offset_s)
+        self.ingest = None
+        if self.device is not None:
+            from ..ops.ingest import DeviceDict, TextIngest
+
+            self.strings = DeviceDict(self.device)
+            self.ingest = TextIngest(fields, sep=self.spec.sep, offset_s=self.offset_s,
+                                     ts_field=len(self.spec.fields) if self.ts_spec is not None else -1,
+                                     device=self.device, dictionary=self.strings,
+                                     filter_prog=self.filter_prog)
+        else:
+            self.strings = self.m.StringDict()
+
+    def _parse_device(self, tb: TextBatch) -> DeviceColumnBatch:
+        res = self.ingest.parse(tb.data, tb.n)
+        nf = len(self.spec.fields)
+        return DeviceColumnBatch(res.n, res.cols[:nf], tuple(k for _, k in self.spec.fields),
+                                 self.strings, res.ts, sub0=tb.sub0,
+                                 parallelism=max(1, self.ctx.parallelism), line_idx=res.line_idx,
+                                 max_ts=res.max_ts)
+
+    def _advance(self, max_ts) -> list:
+        if self.ts_spec is None or max_ts is None:
+            return []
+        if max_ts > self.cur_max:
+            self.cur_max = max_ts
+        wm = self.cur_max - self.bound
+        if wm > self.cur_wm:
+            self.cur_wm = wm
+            return [WM(wm)]
+        return []
 
     def _parse(self, tb: TextBatch) -> ColumnBatch | None:
         cols, done, err_idx, err = self.m.parse_lines(tb.data, self.pspec, self.spec.sep,
@@ -182,6 +282,15 @@ class TextParseOp(Operator):
                 continue
             if not isinstance(it, TextBatch):
                 raise TypeError(f"TextParseOp got {type(it).__name__}")
+            if self.ingest is not None:
+                # Device ingest: the traced filter already ran on the device; the watermark
+                # comes from the batch maximum over every parsed line (before the filter).
+                dcb = self._parse_device(it)
+                wm = self._advance(dcb.max_ts)
+                if dcb.n:
+                    out.append(dcb)
+                out.extend(wm)
+                continue
             cb = self._parse(it)
             wm = self._watermark(cb)
             if self.filter_prog is not None and cb.n:
@@ -198,5 +307,9 @@ class TextParseOp(Operator):
 
     def restore(self, snap: dict) -> None:
         self.cur_max, self.cur_wm = snap["cur_max"], snap["cur_wm"]
-        for s in snap.get("strings", []):
+        strings = snap.get("strings", [])
+        if self.ingest is not None:
+            self.strings.intern_many(list(strings))
+            return
+        for s in strings:
             self.strings.intern(s)

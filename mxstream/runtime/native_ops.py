@@ -20,7 +20,7 @@ from ..ops import expr as E
 from ..ops import kernels as K
 from ..ops.text import FK_DOUBLE, FK_STR
 from ..utils.hashing import java_hash
-from .columnar import ColumnBatch, expand_columns
+from .columnar import ColumnBatch, DeviceColumnBatch, concat_device, expand_columns
 from .operators import LONG_MAX, LONG_MIN, Operator, Rec, WM, WindowOp
 from .window_operator import KeyedWindowOperator
 
@@ -68,6 +68,50 @@ class _ColumnInput:
                 if k not in self.templates:
                     self.templates[k] = cb.value(i)
             self._known = u if known is None else np.union1d(known, u)
+
+    def _template(self, k: int):
+        """Keep-first template of key id k. Device batches never bring host rows: their
+        template holds the key (its dictionary name) and leaves the other fields empty -- the
+        planner only lowers a window whose other fields are dead downstream."""
+        t = self.templates.get(k)
+        if t is not None:
+            return t
+        lazy = getattr(self, "_lazy_tpl", None)
+        if lazy is None:
+            raise KeyError(k)
+        t = lazy.get(k)
+        if t is None:
+            row = [None] * self._lazy_arity
+            row[self.key_pos] = self.dict.get(k) if self.str_keys else k
+            t = lazy[k] = Tuple(row)
+        return t
+
+    def _device_keys(self, cb: DeviceColumnBatch):
+        """Key column of a device batch: dictionary ids (the batch's DeviceDict becomes this
+        operator's dictionary) or non-negative integer keys."""
+        kp = self.key_pos
+        kk = cb.kinds[kp]
+        col = cb.cols[kp][:cb.n]
+        if kk == FK_STR:
+            if self.str_keys is False:
+                raise TypeError("mixed key types")
+            if cb.strings is not self.dict:
+                known = self.dict.strings() if len(self.dict) else []
+                if not self.templates and cb.strings.strings()[:len(known)] == known:
+                    # the parser's dictionary (after a restore: the same strings, same ids)
+                    self.dict = cb.strings
+                else:
+                    raise TypeError("keys from a second dictionary")
+            self.str_keys = True
+            return col
+        if kk == FK_DOUBLE:
+            raise TypeError("double keys on the native path")
+        if self.str_keys is True:
+            raise TypeError("mixed key types")
+        self.str_keys = False
+        if cb.n and int(col.min()) < 0:
+            raise TypeError("negative integer keys on the native path")
+        return col
 
     @staticmethod
     def _cb_concat(batches: list) -> ColumnBatch:
@@ -164,8 +208,60 @@ class NativeWindowOp(_ColumnInput, Operator):
             return k
         raise TypeError("unsupported key type for the native path")
 
+    def _flush_device(self, batches: list) -> list:
+        """Device batches (device text ingest): key, timestamp and value columns go to the
+        engine operator in place -- no host copy, no per-record Python."""
+        try:
+            cb = concat_device(batches)
+            vk = cb.kinds[self.val_pos]
+            if vk == FK_STR or (self.ok_arities and len(cb.kinds) not in self.ok_arities):
+                raise TypeError("value column not numeric")
+            if self.op is None:
+                dense = cb.kinds[self.key_pos] == FK_STR
+                if not self._build(1.0 if vk == FK_DOUBLE else 1, dense=dense):
+                    raise TypeError("unsupported value")
+            elif (vk == FK_DOUBLE) != self.is_float:
+                raise TypeError("mixed value types")
+            kid = self._device_keys(cb)
+        except TypeError:
+            if self.templates or getattr(self, "_lazy_tpl", None):
+                raise
+            recs = expand_columns(batches)
+            self._to_fallback()
+            return self.fallback.process(recs)
+        if getattr(self, "_lazy_tpl", None) is None:
+            self._lazy_tpl, self._lazy_arity = {}, len(cb.kinds)
+        dev = self.op.device
+        n = cb.n
+        if self.assigner.is_event_time():
+            ts = cb.ts[:n] if cb.ts is not None else torch.full((n,), LONG_MIN, dtype=torch.int64,
+                                                                 device=dev)
+        else:
+            ts = torch.full((n,), self.ctx.clock(), dtype=torch.int64, device=dev)
+        vals = cb.cols[self.val_pos][:n]
+        vals = vals.view(torch.int64) if vals.dtype == torch.float64 else vals.to(torch.int64)
+        if kid.dtype == torch.int32 and not self._key32_ok:
+            kid = kid.to(torch.int64)
+        late_before = self.op.metrics.num_late_records_dropped
+        fired = self.op.process(kid.contiguous(), ts.contiguous(), vals.contiguous())
+        if getattr(self.op, "late_side", None):
+            host = cb.host()
+            for idx in np.concatenate(self.op.late_side).tolist():
+                self.side.setdefault(self.late_tag.tag_id, []).append(
+                    Rec(host.value(idx), int(host.ts[idx]) if host.ts is not None else LONG_MIN,
+                        int(host.sub[idx])))
+            self.op.late_side.clear()
+        elif self.late_tag is None:
+            self.num_late_records_dropped += self.op.metrics.num_late_records_dropped - late_before
+        return self._emit(fired)
+
+    _key32_ok = True  # KeyedWindowOperator reads int32 dictionary ids as they are
+
     def _flush_columns(self, batches: list) -> list:
         """All pending items are ColumnBatches: no per-record Python on the input side."""
+        if all(isinstance(b, DeviceColumnBatch) for b in batches):
+            return self._flush_device(batches)
+        batches = [b.host() if isinstance(b, DeviceColumnBatch) else b for b in batches]
         try:
             cb = self._cb_concat(batches)
             vk = cb.kinds[self.val_pos]
@@ -276,11 +372,11 @@ class NativeWindowOp(_ColumnInput, Operator):
                 if self.fused_scalar:
                     value = float(val)
                 elif self.fused_layout is not None:
-                    tpl = self.templates[k]
+                    tpl = self._template(k)
                     value = Tuple([float(val) if j < 0 else (res if j == self.val_pos else tpl[j])
                                    for j in self.fused_layout])
                 else:
-                    value = self.result_builder(self.templates[k], res, key_obj)
+                    value = self.result_builder(self._template(k), res, key_obj)
                 sub = self._subs.get(k)
                 if sub is None:  # subtask of the key (Java hash + murmur): once per key
                     from ..utils.hashing import flink_murmur
@@ -329,7 +425,9 @@ class NativeWindowOp(_ColumnInput, Operator):
         if self.fallback is not None:
             return {"fallback": self.fallback.snapshot()}
         snap = {"wm": self.wm, "late": self.num_late_records_dropped, "str_keys": self.str_keys,
-                "templates": dict(self.templates), "strings": list(self.dict.strings())}
+                "templates": dict(self.templates), "strings": list(self.dict.strings()),
+                "lazy_arity": getattr(self, "_lazy_arity", None)
+                if getattr(self, "_lazy_tpl", None) is not None else None}
         if self.op is not None:
             es = self.op.snapshot_state()
             snap["engine"] = {"columns": es.columns, "meta": es.meta, "is_float": self.is_float}
@@ -346,6 +444,8 @@ class NativeWindowOp(_ColumnInput, Operator):
         self.templates = dict(snap["templates"])
         for st in snap["strings"]:
             self.dict.intern(st)
+        if snap.get("lazy_arity") is not None:
+            self._lazy_tpl, self._lazy_arity = {}, snap["lazy_arity"]
         eng = snap.get("engine")
         if eng is not None:
             self._build(1.0 if eng["is_float"] else 1, dense=bool(self.str_keys))
@@ -426,6 +526,8 @@ class NativeRollingOp(_ColumnInput, Operator):
     def _run_columns(self, batches: list) -> list:
         """ColumnBatch input: key/value columns straight to the engine; the output (one row per
         input record, Flink's rolling emit) is built per row only for the host sink."""
+        # One output row per input record goes to a host sink anyway: device batches come over.
+        batches = [b.host() if isinstance(b, DeviceColumnBatch) else b for b in batches]
         try:
             cb = self._cb_concat(batches)
             vk = cb.kinds[self.val_pos]
@@ -629,6 +731,8 @@ class NativeSessionOp(NativeWindowOp):
     ``KeyedSessionOperator`` (GPU slot table + host store, or the C++ store on CPU). Results are
     emitted at the session's maxTimestamp like Flink's WindowOperator."""
 
+    _key32_ok = False
+
     def _build(self, sample_val, dense: bool = False) -> bool:
         from .session_operator import KeyedSessionOperator
 
@@ -662,7 +766,7 @@ class NativeSessionOp(NativeWindowOp):
                 res = int(cnt)
             else:
                 res = float(val)
-            value = self.result_builder(self.templates[k], res, key_obj)
+            value = self.result_builder(self._template(k), res, key_obj)
             sub = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
             out.append(Rec(value, end - 1, sub))
         return out
@@ -672,6 +776,8 @@ class NativeMedianOp(NativeWindowOp):
     """``process(<median>)`` windows (ComputeCpuMiddle.java:34-48) on the device list-window
     operator: elements stay on the device per pane, the fire sorts (key, value) with two radix
     passes and a kernel takes the per-key median."""
+
+    _key32_ok = False
 
     def _build(self, sample_val, dense: bool = False) -> bool:
         from .list_window_operator import KeyedListWindowOperator
@@ -694,7 +800,7 @@ class NativeMedianOp(NativeWindowOp):
         for s, e, keys, med in fired:
             for k, v in zip(keys.tolist(), med.tolist()):
                 key_obj = self.dict.get(k) if self.str_keys else k
-                value = self.result_builder(self.templates[k], float(v), key_obj)
+                value = self.result_builder(self._template(k), float(v), key_obj)
                 sub = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
                 out.append(Rec(value, e - 1, sub))
         return out
@@ -788,7 +894,7 @@ class NativeVectorWindowOp(NativeWindowOp):
             for k, vec in zip(fr.keys.tolist(), fr.values):
                 key_obj = self.dict.get(k) if self.str_keys else k
                 res = [float(x) for x in vec[:self.vlen]]
-                value = self.result_builder(self.templates[k], res, key_obj)
+                value = self.result_builder(self._template(k), res, key_obj)
                 sub = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
                 out.append(Rec(value, ts, sub))
         return out
