@@ -389,6 +389,41 @@ PYBIND11_MODULE(_mxs_native, m) {
                      P<uint8_t>(dirty_g), make_fire(plan), P<uint64_t>(ok), P<double>(ov),
                      P<uint64_t>(oraw), P<uint32_t>(oc), P<uint32_t>(on), stream);
   });
+  m.def("window_fire_many", [](bool cuda, intptr_t keys_g, intptr_t acc_g, intptr_t cnt_g,
+                               intptr_t dirty_g, py::dict plan,
+                               std::vector<std::tuple<int64_t, int32_t, double, double>> wins,
+                               intptr_t ok, intptr_t ov, intptr_t oraw, intptr_t oc, intptr_t on,
+                               intptr_t bounds, intptr_t stream) {
+    const FirePlan base = make_fire(plan);
+    std::vector<FireWin> w(wins.size());
+    for (size_t i = 0; i < wins.size(); ++i) {
+      w[i].p0 = std::get<0>(wins[i]);
+      w[i].npanes = std::get<1>(wins[i]);
+      w[i].wstart = std::get<2>(wins[i]);
+      w[i].wend = std::get<3>(wins[i]);
+      if (w[i].npanes <= 0 || w[i].npanes > base.ring)
+        throw std::invalid_argument("window_fire_many: window panes exceed the ring");
+    }
+    if (cuda) {
+      gpu::window_fire_many(P<uint64_t>(keys_g), P<uint64_t>(acc_g), P<uint32_t>(cnt_g),
+                            P<uint8_t>(dirty_g), base, w.data(), (int)w.size(), P<uint64_t>(ok),
+                            P<double>(ov), P<uint64_t>(oraw), P<uint32_t>(oc), P<uint32_t>(on),
+                            P<uint32_t>(bounds), stream);
+      return;
+    }
+    py::gil_scoped_release nogil;
+    for (size_t i = 0; i < w.size(); ++i) {
+      FirePlan p = base;
+      p.p0 = w[i].p0;
+      p.npanes = w[i].npanes;
+      p.wstart = w[i].wstart;
+      p.wend = w[i].wend;
+      cpu::window_fire(P<uint64_t>(keys_g), P<uint64_t>(acc_g), P<uint32_t>(cnt_g),
+                       P<uint8_t>(dirty_g), p, P<uint64_t>(ok), P<double>(ov), P<uint64_t>(oraw),
+                       P<uint32_t>(oc), P<uint32_t>(on));
+      P<uint32_t>(bounds)[i] = *P<uint32_t>(on);
+    }
+  });
   m.def("gpu_rolling", [](intptr_t recs, intptr_t counts, py::dict plan, intptr_t keys_g,
                           intptr_t acc_g, intptr_t cnt_g, intptr_t occ, intptr_t flags,
                           intptr_t out_vals, intptr_t stream) {
@@ -839,4 +874,5 @@ PYBIND11_MODULE(_mxs_native, m) {
   bind_vector(m);
   bind_trace(m);
   bind_check(m);
+  bind_reader(m);
 }

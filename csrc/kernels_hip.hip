@@ -1597,6 +1597,10 @@ struct RegVars {
   }
 };
 
+__global__ void copy_u32_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst) {
+  if (threadIdx.x == 0) *dst = *src;
+}
+
 constexpr int kFireThreads = 1024;
 constexpr int kFireU = 4;  // slots per thread per round (ILP)
 
@@ -3480,6 +3484,25 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
                      (hipStream_t)stream, keys_g, acc_g, cnt_g, dirty_g, plan, out_keys, out_vals,
                      out_raw, out_cnt, out_n);
   HIP_CHECK(hipGetLastError());
+}
+
+void window_fire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
+                      const uint8_t* dirty_g, const FirePlan& base, const FireWin* wins, int k,
+                      uint64_t* out_keys, double* out_vals, uint64_t* out_raw, uint32_t* out_cnt,
+                      uint32_t* out_n, uint32_t* bounds, intptr_t stream) {
+  for (int i = 0; i < k; ++i) {
+    FirePlan p = base;
+    p.p0 = wins[i].p0;
+    p.npanes = wins[i].npanes;
+    p.wstart = wins[i].wstart;
+    p.wend = wins[i].wend;
+    window_fire(keys_g, acc_g, cnt_g, dirty_g, p, out_keys, out_vals, out_raw, out_cnt, out_n,
+                stream);
+    // rows of windows 0..i = the cursor after window i (stream order)
+    hipLaunchKernelGGL(copy_u32_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, out_n,
+                       bounds + i);
+    HIP_CHECK(hipGetLastError());
+  }
 }
 
 void direct_agg_probe(const uint64_t* keys, const int64_t* ts, const uint64_t* vals, int64_t n,

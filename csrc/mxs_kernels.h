@@ -62,6 +62,13 @@ struct FirePlan {
   const uint32_t* list_n;  // ... of this length (device counter)
 };
 
+// One window of a batched firing (window_fire_many): the per-window fields of FirePlan.
+struct FireWin {
+  int64_t p0;
+  int32_t npanes;
+  double wstart, wend;
+};
+
 // Local-global window aggregation (G > 1): where the rows of a locally fired window go.
 struct ScatPlan {
   int32_t max_parallelism;  // Flink maxParallelism (key groups)
@@ -150,6 +157,12 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
                  const uint8_t* dirty_g, const FirePlan& plan, uint64_t* out_keys,
                  double* out_vals, uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n,
                  intptr_t stream);
+// Several windows in one call: each window's rows follow the previous ones at the shared
+// cursor out_n; bounds[i] = rows of windows 0..i (device).
+void window_fire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
+                      const uint8_t* dirty_g, const FirePlan& base, const FireWin* wins, int k,
+                      uint64_t* out_keys, double* out_vals, uint64_t* out_raw, uint32_t* out_cnt,
+                      uint32_t* out_n, uint32_t* bounds, intptr_t stream);
 void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& plan, uint64_t* keys_g,
              uint64_t* acc_g, uint32_t* cnt_g, uint32_t* occupancy, uint32_t* flags,
              uint64_t* out_vals, intptr_t stream);

@@ -8,3 +8,4 @@ void bind_sessions(pybind11::module_& m);
 void bind_vector(pybind11::module_& m);
 void bind_trace(pybind11::module_& m);
 void bind_check(pybind11::module_& m);
+void bind_reader(pybind11::module_& m);

@@ -220,9 +220,11 @@ def _lower_text(env, sinks) -> None:
             fnode.meta = dict(fnode.meta, fused=True)
         src_factory = parent.factory
 
-        def columnar_source(f=src_factory):
+        def columnar_source(f=src_factory, ring=ingest_dev is not None):
             s = f()
             s.columnar = True
+            if ring and hasattr(type(s), "ring"):
+                s.ring = True  # file -> pinned ring slots (C++ reader) -> device ingest
             return s
 
         parent.factory = columnar_source

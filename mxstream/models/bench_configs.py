@@ -378,65 +378,101 @@ def config8(steps: int, warmup: int, batch: int = 1 << 22, keys: int = 100_000,
             "device": str(dev)}
 
 
-def config7(lines: int = 4_000_000, channels: int = 1_000, device: str = "cuda",
-            batch_lines: int = 1 << 18, threads: int = 16) -> dict:
-    """Host ingest through the DataStream API: the reference's BandwidthMonitorWithEventTime job
-    (BandwidthMonitorWithEventTime.java:25-57) over a text file replay -- file -> columnar
-    text batches -> C++ parse (threads) -> event-time sliding 5 min / 5 s window on the native
-    operator (device) -> Mbps map -> filter -> sink. Lines per second end to end (wall clock of
-    env.execute, the file already in the page cache), next to the device-generated headline."""
+def bandwidth_text(lines: int, channels: int = 1_000, seed: int = 7) -> np.ndarray:
+    """Synthetic chapter3 input (chapter3/README.md:286 format, ``BandwidthMonitorWithEventTime``)
+    as fixed-width lines ``yyyy-MM-ddTHH:mm:ss chNNN.example.com VVVVVVVVV`` over one hour of
+    event time, built with numpy (a Python f-string per line would dominate a 10^8-line file).
+    Healthy channels move 150-300 MB per line; 1 % of the channels are starved (a few KB per
+    line) and alert in every 5-min window -- a small alert stream, as in a monitoring system.
+    The byte count is zero-padded (Long.parseLong accepts leading zeros)."""
+    import datetime as _dt
+
+    rng = np.random.default_rng(seed)
+    t0s = 1_566_957_600  # 2019-08-28T10:00:00+08:00
+    secs = (np.arange(lines, dtype=np.int64) * 3600) // max(lines, 1)
+    tz = _dt.timezone(_dt.timedelta(hours=8))
+    stamps = np.frombuffer("".join(_dt.datetime.fromtimestamp(t0s + i, tz).strftime("%Y-%m-%dT%H:%M:%S")
+                                   for i in range(3600)).encode(), np.uint8).reshape(3600, 19)
+    width = max(3, len(str(channels - 1)))
+    names = np.frombuffer("".join(f"ch{c:0{width}d}.example.com" for c in range(channels)).encode(),
+                          np.uint8).reshape(channels, width + 14)
+    ch = rng.integers(0, channels, lines)
+    vals = rng.integers(150_000_000, 300_000_000, lines)
+    starved = ch % 100 == 0
+    vals[starved] = rng.integers(1, 1000, int(starved.sum()))
+    w = 19 + 1 + names.shape[1] + 1 + 9 + 1
+    out = np.empty((lines, w), np.uint8)
+    out[:, :19] = stamps[secs]
+    out[:, 19] = 32
+    out[:, 20:20 + names.shape[1]] = names[ch]
+    o = 20 + names.shape[1]
+    out[:, o] = 32
+    v = vals.copy()
+    for k in range(8, -1, -1):
+        out[:, o + 1 + k] = 48 + (v % 10)
+        v //= 10
+    out[:, w - 1] = 10
+    return out.reshape(-1)
+
+
+def config7(lines: int = 16_000_000, channels: int = 1_000, device: str = "cuda",
+            batch_lines: int = 1 << 20, profile: bool = False) -> dict:
+    """The reference's BandwidthMonitorWithEventTime job (BandwidthMonitorWithEventTime.java:25-57)
+    through the DataStream API over a text file replay: env.readTextFile -> assigner -> map(parse)
+    -> keyBy -> 5 min / 5 s sliding event-time window reduce -> Mbps map -> filter -> sink.
+    On a GPU the planner runs it on the device ingest: the C++ reader fills pinned ring slots,
+    the batch is parsed on the device with channel names interned in the HBM dictionary, the
+    native window operator reads the device columns, the Mbps map + filter run in the fire
+    kernel. Lines per second end to end (wall clock of env.execute, the file in the page cache)."""
     import os
     import tempfile
 
     from ..api.environment import StreamExecutionEnvironment
     from . import chapters as C
 
-    rng = np.random.default_rng(7)
-    t0s = 1_566_957_600  # 2019-08-28T10:00:00+08:00 (chapter3/README.md:286)
-    secs = t0s + np.arange(lines) * 3600 // lines  # one hour of event time
-    import datetime as _dt
-
-    tz = _dt.timezone(_dt.timedelta(hours=8))
-    stamp = {s: _dt.datetime.fromtimestamp(int(s), tz).strftime("%Y-%m-%dT%H:%M:%S")
-             for s in np.unique(secs).tolist()}
-    ch = rng.integers(0, channels, lines)
-    # Healthy channels move 150-300 MB per line (every 5-min window, even the first 5 s of the
-    # stream, stays above the job's 100 Mbps); 1 % of the channels are starved (a few KB per line)
-    # and alert in every window -- the alert stream is small, as in a monitoring system.
-    vals = rng.integers(150_000_000, 300_000_000, lines)
-    starved = ch % 100 == 0
-    vals[starved] = rng.integers(1, 1000, int(starved.sum()))
-    text = "\n".join(f"{stamp[int(s)]} ch{c}.example.com {v}"
-                      for s, c, v in zip(secs.tolist(), ch.tolist(), vals.tolist())) + "\n"
+    text = bandwidth_text(lines, channels)
     fd, path = tempfile.mkstemp(suffix=".txt")
-    with os.fdopen(fd, "w") as f:
-        f.write(text)
+    with os.fdopen(fd, "wb") as f:
+        f.write(text.tobytes())
+    head_lines = 50_000
+    line_w = text.size // max(lines, 1)
+    fd, head = tempfile.mkstemp(suffix=".txt")
+    with os.fdopen(fd, "wb") as f:
+        f.write(text[:head_lines * line_w].tobytes())
+    del text
 
-    def run(n_lines_file):
+    def run(file, batch):
         alerts = [0]
         env = StreamExecutionEnvironment(4).set_output(lambda s: alerts.__setitem__(0, alerts[0] + 1))
         env.config.native = "auto"
         env.config.device = device
-        env.config.batch_size = batch_lines
-        C.build_bandwidth_event_time(env, env.read_text_file(n_lines_file))
+        env.config.batch_size = batch
+        C.build_bandwidth_event_time(env, env.read_text_file(file))
         t = time.perf_counter()
-        env.execute("BandwidthMonitorWithEventTime")
-        return time.perf_counter() - t, alerts[0]
+        res = env.execute("BandwidthMonitorWithEventTime")
+        return time.perf_counter() - t, alerts[0], res
 
     try:
-        head = tempfile.mkstemp(suffix=".txt")[1]
-        with open(head, "w") as f:
-            f.write("".join(text.splitlines(True)[:50_000]))
-        run(head)  # warm-up: module loads, device buffers
-        os.unlink(head)
-        dt, alerts = run(path)
+        run(head, 1 << 14)  # warm-up: module loads, kernels, pinned pools
+        if profile:
+            import cProfile
+            import pstats
+
+            pr = cProfile.Profile()
+            pr.enable()
+        dt, alerts, res = run(path, batch_lines)
+        if profile:
+            pr.disable()
+            pstats.Stats(pr).sort_stats("cumulative").print_stats(40)
     finally:
         os.unlink(path)
-    return {"config": 7, "metric": "lines/sec through the DataStream API (host ingest, file replay)",
+        os.unlink(head)
+    return {"config": 7, "metric": "lines/sec through the DataStream API (file replay)",
             "value": lines / dt, "unit": "lines/s", "seconds": dt, "alerts": alerts,
-            "lines": lines, "channels": channels, "batch_lines": batch_lines,
+            "lines": lines, "bytes_per_line": line_w, "channels": channels,
+            "batch_lines": batch_lines,
             "job": "BandwidthMonitorWithEventTime (5 min / 5 s sliding, 1 min bound)",
-            "device": device}
+            "ingest": "device" if str(device).startswith("cuda") else "host", "device": device}
 
 
 def main(argv=None) -> int:
@@ -452,6 +488,8 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--lines", type=int, default=None, help="config 7: lines in the file")
+    ap.add_argument("--profile", action="store_true", help="config 7: cProfile the job")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--gpu-parse", action="store_true", help="config 1 on the GPU parse path")
     ap.add_argument("--hashed-keys", action="store_true",
@@ -472,7 +510,8 @@ def main(argv=None) -> int:
         r = config4(a.steps, a.warmup, a.batch or (1 << 24), device=a.device,
                     dense_keys=not a.hashed_keys)
     elif a.config == 7:
-        r = config7(device=a.device)
+        r = config7(lines=a.lines or 16_000_000, device=a.device,
+                    batch_lines=a.batch or (1 << 20), profile=a.profile)
     elif a.config == 8:
         r = config8(a.steps, a.warmup, a.batch or (1 << 22), device=a.device)
     elif a.config == 6:

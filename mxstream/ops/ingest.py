@@ -258,7 +258,9 @@ class TextIngest:
         return dev, slot[0]
 
     # ---- parse ----------------------------------------------------------------------------------
-    def parse(self, data, nlines: int | None = None) -> IngestResult:
+    def parse(self, data, nlines: int | None = None, on_upload=None) -> IngestResult:
+        """on_upload(event): called with a device event recorded after the H2D copy of a host
+        tensor input (its pinned slot may be reused once the event completed)."""
         m = self._m
         n = count_lines(data) if nlines is None else int(nlines)
         nbytes = len(data) if not isinstance(data, torch.Tensor) else data.numel()
@@ -272,6 +274,12 @@ class TextIngest:
             return IngestResult(0, empty, None if self.ts_field < 0 else empty[self.ts_field],
                                 None, None, 0)
         buf, keep_alive = self._upload(data)
+        if on_upload is not None:
+            ev = None
+            if self.cuda:
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.device))
+            on_upload(ev)
         dev, st = self.device, self._stream()
         nf, S = self.nf, self.nstr
         ctl = self._buf("ctl", 8, torch.int64)[:8]

@@ -32,11 +32,22 @@ from .operators import LONG_MAX, LONG_MIN, Operator, Rec, WM
 
 @dataclass
 class TextBatch:
-    """A micro-batch of raw lines ('\\n'-separated, trailing '\\r' allowed)."""
-    data: bytes
+    """A micro-batch of raw lines ('\\n'-separated, trailing '\\r' allowed). `data` is bytes,
+    or a 1-D uint8 tensor in a pinned slot of the source's ring (`token` returns the slot once
+    the consumer's H2D copy has completed)."""
+    data: object
     n: int
     sub0: int = 0        # subtask of the first line (round-robin from the source edge)
     parallelism: int = 1
+    token: object = None
+
+    def host_bytes(self) -> bytes:
+        if isinstance(self.data, (bytes, bytearray)):
+            return bytes(self.data)
+        b = self.data.numpy().tobytes()
+        if self.token is not None:
+            self.token.consumed()
+        return b
 
 
 @dataclass
@@ -223,7 +234,8 @@ class TextParseOp(Operator):
             self.strings = self.m.StringDict()
 
     def _parse_device(self, tb: TextBatch) -> DeviceColumnBatch:
-        res = self.ingest.parse(tb.data, tb.n)
+        res = self.ingest.parse(tb.data, tb.n, on_upload=None if tb.token is None
+                                else tb.token.uploaded)
         nf = len(self.spec.fields)
         return DeviceColumnBatch(res.n, res.cols[:nf], tuple(k for _, k in self.spec.fields),
                                  self.strings, res.ts, sub0=tb.sub0,
@@ -242,7 +254,7 @@ class TextParseOp(Operator):
         return []
 
     def _parse(self, tb: TextBatch) -> ColumnBatch | None:
-        cols, done, err_idx, err = self.m.parse_lines(tb.data, self.pspec, self.spec.sep,
+        cols, done, err_idx, err = self.m.parse_lines(tb.host_bytes(), self.pspec, self.spec.sep,
                                                       self.strings, self.offset_s, self.threads)
         if err_idx >= 0:
             from ..api import java as J

@@ -123,17 +123,93 @@ class TimedCollectionSource(Source):
         return out, done
 
 
+class SlotToken:
+    """A pinned ring slot lent to one TextBatch: returned to the reader once the consumer's H2D
+    copy has completed (event) or the consumer copied the bytes out (consumed)."""
+
+    __slots__ = ("slot", "event", "done")
+
+    def __init__(self, slot: int):
+        self.slot, self.event, self.done = slot, None, False
+
+    def uploaded(self, event) -> None:
+        self.event = event
+        if event is None:
+            self.done = True
+
+    def consumed(self) -> None:
+        self.done = True
+
+    def ready(self, wait: bool = False) -> bool:
+        if self.done:
+            return True
+        if self.event is None:
+            return False
+        if wait:
+            self.event.synchronize()
+            return True
+        return bool(self.event.query())
+
+
+def _aligned_range(path: str, rank: int, world: int) -> tuple[int, int]:
+    """K18: this rank's newline-aligned byte range of the file."""
+    import os as _os
+
+    size = _os.path.getsize(path)
+    lo, hi = (size * rank) // world, (size * (rank + 1)) // world
+
+    def next_line(pos):
+        if pos <= 0:
+            return 0
+        with open(path, "rb") as f:
+            f.seek(pos - 1)
+            while True:
+                blk = f.read(1 << 16)
+                if not blk:
+                    return size
+                j = blk.find(b"\n")
+                if j >= 0:
+                    return pos - 1 + j + 1
+                pos += len(blk)
+
+    return next_line(lo) if rank else 0, next_line(hi) if rank + 1 < world else size
+
+
 class TextFileSource(Source):
     name = "Text File Source"
+    # Set by the planner with the device ingest: batches are read by the C++ reader
+    # (csrc/reader.cpp) into pinned ring slots and handed over without a host copy.
+    ring = False
 
     def __init__(self, path: str, batch_size: int = 65536):
         self.path = path
         self.batch = batch_size
         self.lines: list[str] | None = None
         self.pos = 0
+        self._ring = None
+
+    def _open_ring(self, start: int) -> None:
+        import torch
+
+        from ..ops.native import load
+
+        chunk = max(1 << 20, self.batch * 48)
+        pin = torch.cuda.is_available()
+        self._slots = [torch.empty(chunk, dtype=torch.uint8, pin_memory=pin) for _ in range(4)]
+        self._ring = load().TextFileRing(self.path, self.lo + start, self.hi,
+                                         [(t.data_ptr(), t.numel()) for t in self._slots], chunk,
+                                         min(16, max(1, __import__("os").cpu_count() or 1)))
+        self._ring.start()
+        self._held: list = []
+        self.bpos = start
+        self._ring_done = self.lo + start >= self.hi
 
     def open(self, rank, world, clock):
         super().open(rank, world, clock)
+        if self.columnar and self.ring:
+            self.lo, self.hi = _aligned_range(self.path, rank, world)
+            self._open_ring(0)
+            return
         if self.columnar:
             # K18: the file is split into one contiguous newline-aligned byte range per rank,
             # read in batches of ~batch lines without building Python strings.
@@ -160,11 +236,49 @@ class TextFileSource(Source):
 
     def restore(self, snap: dict) -> None:
         if self.columnar and "bpos" in snap:
-            self.bpos = snap["bpos"]
+            if self._ring is not None:
+                self._ring.close()
+                self._open_ring(int(snap["bpos"]))
+            else:
+                self.bpos = snap["bpos"]
         else:
             super().restore(snap)
 
+    def close(self):
+        if self._ring is not None:
+            for t in self._held:
+                t.ready(wait=True)
+            self._ring.close()
+            self._ring = None
+
+    def _poll_ring(self):
+        from .columnar import TextBatch
+
+        # Slots whose upload completed go back to the reader.
+        keep = []
+        for t in self._held:
+            if t.ready(wait=len(self._held) >= len(self._slots) - 1 and t is self._held[0]):
+                self._ring.release(t.slot)
+            else:
+                keep.append(t)
+        self._held = keep
+        if self._ring_done:
+            return [], True
+        slot, nbytes, nlines, end, eof = self._ring.next(1000)
+        if slot < 0:
+            self._ring_done = bool(eof)
+            return [], self._ring_done
+        tok = SlotToken(slot)
+        self._held.append(tok)
+        self.bpos = end
+        self._ring_done = self.lo + end >= self.hi
+        return [TextBatch(self._slots[slot][:nbytes], int(nlines), token=tok)], self._ring_done
+
     def poll(self, now):
+        if self.columnar and self._ring is not None:
+            return self._poll_ring()
+        if self.columnar and self.ring:
+            return [], True
         if self.columnar:
             from .columnar import TextBatch
 

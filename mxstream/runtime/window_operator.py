@@ -417,10 +417,18 @@ class KeyedWindowOperator:
         self._hflags = torch.zeros(4, dtype=torch.int32, pin_memory=pin)
         self.stats, self.red = self._stats[0], self._red[0]
         self.local_maxts = torch.full((1,), I64_MIN, dtype=torch.int64, device=dev)
-        self.out_keys = torch.empty(self.nslots, dtype=torch.int64, device=dev)
-        self.out_vals = torch.empty(self.nslots, dtype=torch.float64, device=dev)
-        self.out_raw = torch.empty(self.nslots, dtype=torch.int64, device=dev)
-        self.out_cnt = torch.empty(self.nslots, dtype=torch.int32, device=dev)
+        # Batched firing: up to `_fire_group` due windows per native call and host sync (one
+        # window's rows never exceed nslots, so the output holds the group's rows).
+        self._fire_group = (max(1, min(64, (1 << 21) // self.nslots))
+                            if type(self)._fire_window is KeyedWindowOperator._fire_window else 1)
+        orows = self.nslots * self._fire_group
+        self.out_keys = torch.empty(orows, dtype=torch.int64, device=dev)
+        self.out_vals = torch.empty(orows, dtype=torch.float64, device=dev)
+        self.out_raw = torch.empty(orows, dtype=torch.int64, device=dev)
+        self.out_cnt = torch.empty(orows, dtype=torch.int32, device=dev)
+        self.fire_bounds = torch.zeros(self._fire_group, dtype=torch.int32, device=dev)
+        self._hbounds = torch.zeros(self._fire_group, dtype=torch.int32,
+                                    pin_memory=dev.type == "cuda")
         # flags: [0] table full (bit0) / [1] combiner overflow / [2] fired-row cursor (out_n), so
         # one 16-byte D2H after a fire returns the row count and the table-full bit together.
         self.out_n = self.flags[2:3]
@@ -429,7 +437,7 @@ class KeyedWindowOperator:
         self._pool = None
         if dev.type == "cuda":
             self._pool = PinnedSlabPool()
-            self._pool.take(self.nslots * 28 + 4 * 256)
+            self._pool.take(orows * 28 + 4 * 256)
         self.late_idx = (torch.empty(late_capacity, dtype=torch.int32, device=dev)
                          if side_output_late else None)
         # Touched-slot list (allowed lateness): window_agg appends every slot that receives
@@ -1202,11 +1210,91 @@ class KeyedWindowOperator:
             hf = self._hflags.tolist()
         else:
             hf = self.flags.tolist()
+        return self._check_fire_flags(hf)
+
+    def _fired_bounds(self, k: int) -> list[int]:
+        """Cumulative row counts of a batched firing's k windows (one host sync)."""
+        if self.device.type == "cuda":
+            self._hflags.copy_(self.flags, non_blocking=True)
+            self._hbounds[:k].copy_(self.fire_bounds[:k], non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            hf = self._hflags.tolist()
+            b = self._hbounds[:k].tolist()
+        else:
+            hf = self.flags.tolist()
+            b = self.fire_bounds[:k].tolist()
+        self._check_fire_flags(hf)
+        return b
+
+    def _check_fire_flags(self, hf) -> int:
         if hf[0] & 1:
             raise RuntimeError("keyed state table full: a key found no free slot (raise max_keys)")
         if hf[0] & 8:
             raise ValueError("deterministic f64 sum: a value is NaN, infinite or |x| >= 2^63")
         return hf[2]
+
+    def _batched_fire_ok(self) -> bool:
+        return (not self.local_global and self.host_tier is None
+                and type(self)._fire_window is KeyedWindowOperator._fire_window)
+
+    def _fire_list(self, starts: list[int], only_dirty: bool) -> list[FireResult]:
+        """Fire the windows starting at `starts` (in order)."""
+        if len(starts) > 1 and self._batched_fire_ok():
+            return self._fire_many(starts, only_dirty)
+        out = []
+        for s in starts:
+            r = self._fire_window(s, only_dirty)
+            if r is not None:
+                out.append(r)
+        return out
+
+    def _fire_many(self, starts: list[int], only_dirty: bool) -> list[FireResult]:
+        """Batched firing: a group of due windows is evaluated by one native call (one fire
+        launch per window, rows appended at a shared cursor, the cursor recorded after each
+        window), then ONE host sync and ONE copy to the pinned slab for the whole group -- a
+        watermark jump over many slides (5 min / 5 s windows: 60 per element) no longer costs two
+        host round trips per window."""
+        out: list[FireResult] = []
+        cuda = self.device.type == "cuda"
+        plan = dict(agg=self.agg, npanes=1, ring=self.ring, only_dirty=int(only_dirty),
+                    nslots=self.nslots, p0=0, wstart=0.0, wend=0.0, out_cap=self.out_keys.numel(),
+                    map=tuple(self.map_prog.as_args()), filt=tuple(self.filter_prog.as_args()))
+        if only_dirty and self.dlist is not None:
+            plan.update(list=self.dlist.data_ptr(), list_n=self.dlist_n.data_ptr())
+        wins = []
+        for s in starts:
+            p0 = max(self.pane_of(s), self.min_live_pane)
+            p1 = min(self.pane_of(s) + self.panes_per_window - 1, self.max_seen_pane)
+            if p1 >= p0:
+                wins.append((s, (p0, p1 - p0 + 1, float(s), float(s + self.size))))
+        stream = torch.cuda.current_stream(self.device).cuda_stream if cuda else 0
+        g = self._fire_group
+        for i in range(0, len(wins), g):
+            chunk = wins[i:i + g]
+            self.out_n.zero_()
+            self._m.window_fire_many(cuda, self.keys_g.data_ptr(), self.acc_g.data_ptr(),
+                                     self.cnt_g.data_ptr(), self.dirty_g.data_ptr(), plan,
+                                     [w for _, w in chunk], self.out_keys.data_ptr(),
+                                     self.out_vals.data_ptr(), self.out_raw.data_ptr(),
+                                     self.out_cnt.data_ptr(), self.out_n.data_ptr(),
+                                     self.fire_bounds.data_ptr(), stream)
+            bounds = self._fired_bounds(len(chunk))
+            self.metrics.num_fires += len(chunk)
+            n = min(bounds[-1], self.out_keys.numel())
+            if n == 0:
+                continue
+            self.metrics.num_records_out += n
+            host = to_host_arrays([self.out_keys, self.out_vals, self.out_raw, self.out_cnt], n,
+                                  self._pool)
+            keys = host[0].view(np.uint64)
+            lo = 0
+            for (s, _), hi in zip(chunk, bounds):
+                hi = min(hi, n)
+                if hi > lo:
+                    out.append(FireResult(s, s + self.size, keys[lo:hi], host[1][lo:hi],
+                                          host[2][lo:hi], host[3][lo:hi], refire=only_dirty))
+                lo = hi
+        return out
 
     def _fire_ready(self, wm: int) -> list[FireResult]:
         out: list[FireResult] = []
@@ -1218,16 +1306,16 @@ class KeyedWindowOperator:
         if s < first_live:
             s = first_live
         last_data_start = self.last_start(self.pane_start(self.max_seen_pane + 1) - 1)
+        due = []
         while s + self.size - 1 <= wm:
             if s > last_data_start:
                 # No window beyond the newest pane holds data: jump to the first window that can.
                 s = max(s, self._align_up(wm - self.size + 2))
                 break
             if self._window_overlaps_live(s):
-                r = self._fire_window(s, only_dirty=False)
-                if r is not None:
-                    out.append(r)
+                due.append(s)
             s += self.slide
+        out.extend(self._fire_list(due, only_dirty=False))
         self.next_fire_start = s
         return out
 
@@ -1240,12 +1328,12 @@ class KeyedWindowOperator:
         out: list[FireResult] = []
         s = self.first_start_containing(self.pane_start(pmin))
         end_s = min(self.next_fire_start - self.slide, self.last_start(self.pane_start(pmax)))
+        due = []
         while s <= end_s:
             if s + self.size - 1 + self.lateness > old_wm:
-                r = self._fire_window(s, only_dirty=True)
-                if r is not None:
-                    out.append(r)
+                due.append(s)
             s += self.slide
+        out.extend(self._fire_list(due, only_dirty=True))
         if self.dlist is not None:
             K.dirty_clear(self.dlist, self.dlist_n, ring=self.ring, nslots=self.nslots,
                           dirty_g=self.dirty_g, slot_mark=self.slot_mark, p_lo=pmin,
