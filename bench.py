@@ -51,6 +51,11 @@ def main() -> int:
                     help="write a Chrome trace of the timed steps (stage spans; roctx with MXS_ROCTX=1)")
     ap.add_argument("--step-timeout-ms", type=int, default=0,
                     help="watchdog: abort the run if one step makes no progress for this long")
+    ap.add_argument("--latency-firings", type=int, default=12,
+                    help="after the timed steps: run untimed steps until this many firings "
+                         "for the p50/p99 alert latency (0: timed firings only)")
+    ap.add_argument("--no-hashed-figure", action="store_true",
+                    help="skip the untimed-in-headline hashed-key run reported next to it")
     a = ap.parse_args()
 
     if os.environ.get("MXS_SPIN") == "1" and a.device == "cuda":
@@ -143,13 +148,55 @@ def main() -> int:
     t = torch.tensor([dt], dtype=torch.float64, device=device)
     comm.allreduce_max_(t)
     dt = float(t.item())
-    lat = bench.p50_latency_ms()
-    lat99 = bench.latency_quantile_ms(0.99)
-    lt = torch.tensor([lat if lat is not None else -1.0, lat99 if lat99 is not None else -1.0],
-                      dtype=torch.float64, device=device)
-    comm.allreduce_max_(lt)
     al = torch.tensor([bench.alerts - alerts0], dtype=torch.int64, device=device)
     comm.allreduce_sum_(al)
+    op_metrics = bench.op.metrics
+    op_info = {"local_global": bench.op.local_global, "dense": bool(bench.op.dense_bits),
+               "rec_w": bench.op.rec_w}
+
+    # ---- after the timed region (not part of `value`) ----
+    # Latency phase: the timed steps cover few firings (5 s of event time per step, 1-min
+    # windows: one firing per 12 steps), so the alert-latency quantiles come from further,
+    # untimed steps until `--latency-firings` firings were observed.
+    timed_firings = len(bench.latencies_ms)
+    lat_steps = 0
+    while a.latency_firings > 0 and len(bench.latencies_ms) < a.latency_firings \
+            and lat_steps < 40 * a.latency_firings:
+        bench.step()
+        lat_steps += 1
+    bench.drain()
+    sync()
+    lat = bench.p50_latency_ms()
+    lat99 = bench.latency_quantile_ms(0.99)
+    lt = torch.tensor([lat if lat is not None else -1.0, lat99 if lat99 is not None else -1.0,
+                       float(len(bench.latencies_ms))], dtype=torch.float64, device=device)
+    comm.allreduce_max_(lt)
+    # The same step on hashed keyed state (arbitrary int64 keys: open-addressing sub-tables
+    # instead of the dense dictionary-id bijection), timed the same way, reported next to it.
+    hashed = None
+    if not a.no_hashed_figure and not a.hashed_keys:
+        hcfg = TumblingBenchConfig(keys=a.keys, batch=a.batch, cap_log2=a.cap_log2,
+                                   dense_keys=False, zipf=a.zipf,
+                                   pipeline=False if a.no_pipeline else None)
+        del bench
+        hb = TumblingWindowBench(hcfg, comm, device)
+        for _ in range(a.warmup):
+            hb.step()
+        sync()
+        comm.barrier()
+        sync()
+        th = time.perf_counter()
+        for _ in range(a.steps):
+            hb.step()
+        hb.drain()
+        sync()
+        comm.barrier()
+        sync()
+        tt = torch.tensor([time.perf_counter() - th], dtype=torch.float64, device=device)
+        comm.allreduce_max_(tt)
+        hashed = {"hashed_events_per_s": a.batch * a.steps * comm.world / float(tt.item()),
+                  "hashed_ms_per_step": float(tt.item()) / a.steps * 1e3}
+        bench = hb
 
     n = comm.world
     events = a.batch * a.steps * n
@@ -170,11 +217,15 @@ def main() -> int:
             "data": "synthetic (device-generated metric events, "
                     + (f"zipf({a.zipf:g})" if a.zipf > 0 else "uniform")
                     + f" keys = dictionary ids of {a.keys} channels, 2 s bounded disorder)",
+            # over the timed firings plus the untimed latency phase (>= --latency-firings)
             "p50_alert_latency_ms": (lt[0].item() if lt[0].item() >= 0 else None),
             "p99_alert_latency_ms": (lt[1].item() if lt[1].item() >= 0 else None),
-            "firings_timed": len(bench.latencies_ms),
+            "firings_timed": timed_firings,
+            "firings_for_latency": int(lt[2].item()),
             "alerts": int(al.item()),
-            "late_dropped": bench.op.metrics.num_late_records_dropped,
+            "late_dropped": op_metrics.num_late_records_dropped,
+            # untimed extra run, NOT the headline: the same job on hashed keyed state
+            **(hashed or {}),
             "config": {
                 "model": "chapter3 1-min tumbling event-time window sum (BandwidthMonitorWithEventTime shape), 1M keys",
                 "global_batch": a.batch * n,
@@ -183,10 +234,10 @@ def main() -> int:
                 # partials: local-global aggregation (per-rank pre-aggregation over the whole key
                 # space, partial accumulators cross the all-to-all when a window fires);
                 # records: per-step exchange of combined (key, pane) records.
-                "exchange": ("partials" if bench.op.local_global
+                "exchange": ("partials" if op_info["local_global"]
                              else "records" if n > 1 else "none"),
-                "keyed_state": "dense" if bench.op.dense_bits else "hashed",
-                "record_bytes": {1: 8, 2: 16, 3: 24}[bench.op.rec_w],
+                "keyed_state": "dense" if op_info["dense"] else "hashed",
+                "record_bytes": {1: 8, 2: 16, 3: 24}[op_info["rec_w"]],
                 "keys": a.keys,
                 "key_distribution": f"zipf({a.zipf:g})" if a.zipf > 0 else "uniform",
                 "events_per_gpu_per_step": a.batch,
