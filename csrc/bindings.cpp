@@ -141,6 +141,11 @@ AggPlan make_agg(py::dict d) {
   if (p.pg <= 0) throw std::invalid_argument("pg must be positive");
   p.split = d.contains("split") ? d["split"].cast<int32_t>() : 1;
   p.det = d.contains("det") ? d["det"].cast<int32_t>() : 0;
+  if (d.contains("dacc") && d["dacc"].cast<intptr_t>()) {
+    p.dacc = reinterpret_cast<uint64_t*>(d["dacc"].cast<intptr_t>());
+    p.dcnt = reinterpret_cast<uint32_t*>(d["dcnt"].cast<intptr_t>());
+    if (!p.dcnt || !p.dlist) throw std::invalid_argument("delta ring needs dcnt and the slot list");
+  }
   if (p.split < 1 || p.split > 1024) throw std::invalid_argument("agg split out of range");
   return p;
 }
@@ -624,15 +629,20 @@ PYBIND11_MODULE(_mxs_native, m) {
   });
   m.def("gpu_dirty_clear", [](intptr_t list, intptr_t list_n, uint32_t cap, int ring,
                               int64_t nslots, intptr_t dirty_g, intptr_t mark, int64_t p_lo, int np,
-                              intptr_t stream) {
+                              intptr_t stream, intptr_t dacc, intptr_t dcnt) {
     gpu::dirty_clear(P<uint32_t>(list), P<uint32_t>(list_n), cap, ring, nslots, P<uint8_t>(dirty_g),
-                     P<uint32_t>(mark), p_lo, np, stream);
-  });
+                     P<uint32_t>(mark), p_lo, np, stream, P<uint64_t>(dacc), P<uint32_t>(dcnt));
+  }, py::arg("list"), py::arg("list_n"), py::arg("cap"), py::arg("ring"), py::arg("nslots"),
+     py::arg("dirty_g"), py::arg("mark"), py::arg("p_lo"), py::arg("np"), py::arg("stream"),
+     py::arg("dacc") = 0, py::arg("dcnt") = 0);
   m.def("cpu_dirty_clear", [](intptr_t list, intptr_t list_n, uint32_t cap, int ring,
-                              int64_t nslots, intptr_t dirty_g, intptr_t mark, int64_t p_lo, int np) {
+                              int64_t nslots, intptr_t dirty_g, intptr_t mark, int64_t p_lo, int np,
+                              intptr_t dacc, intptr_t dcnt) {
     cpu::dirty_clear(P<uint32_t>(list), P<uint32_t>(list_n), cap, ring, nslots, P<uint8_t>(dirty_g),
-                     P<uint32_t>(mark), p_lo, np);
-  });
+                     P<uint32_t>(mark), p_lo, np, P<uint64_t>(dacc), P<uint32_t>(dcnt));
+  }, py::arg("list"), py::arg("list_n"), py::arg("cap"), py::arg("ring"), py::arg("nslots"),
+     py::arg("dirty_g"), py::arg("mark"), py::arg("p_lo"), py::arg("np"), py::arg("dacc") = 0,
+     py::arg("dcnt") = 0);
   m.def("gpu_scatter_partials", [](intptr_t keys, intptr_t acc, intptr_t cnt, intptr_t n_in,
                                    py::dict plan, intptr_t jhash, intptr_t kg_dest,
                                    intptr_t cursor, intptr_t out, intptr_t flags, intptr_t stream) {

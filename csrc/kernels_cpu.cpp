@@ -221,6 +221,11 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p, uint6
         }
         if (pane <= p.fired_hi) {
           dirty_g[gi] = 1;
+          if (p.dacc && !det) {  // local-global delta ring of late-but-allowed data
+            const uint64_t v = agg_lift(p.agg, r.val);
+            if (p.agg != AGG_COUNT) p.dacc[gi] = p.dcnt[gi] ? agg_combine(p.agg, p.dacc[gi], v) : v;
+            p.dcnt[gi] += p.combined ? r.aux : 1u;
+          }
           const size_t slot = ((size_t)sub << p.cap_log2) + s;
           if (p.dlist && !p.slot_mark[slot]) {
             p.slot_mark[slot] = 1;
@@ -606,13 +611,21 @@ void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t*
 }
 
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
-                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np) {
+                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np,
+                 uint64_t* dacc, uint32_t* dcnt) {
   const uint32_t n = std::min(*list_n, list_cap);
   np = std::min(np, ring);
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t s = list[i];
     slot_mark[s] = 0;
-    for (int j = 0; j < np; ++j) dirty_g[(size_t)((p_lo + j) & (ring - 1)) * nslots + s] = 0;
+    for (int j = 0; j < np; ++j) {
+      const size_t gi = (size_t)((p_lo + j) & (ring - 1)) * nslots + s;
+      dirty_g[gi] = 0;
+      if (dcnt) {
+        dcnt[gi] = 0;
+        dacc[gi] = 0;
+      }
+    }
   }
 }
 

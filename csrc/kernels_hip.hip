@@ -1304,6 +1304,11 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
         if (p.pane_base + q0 + (int64_t)(i >> p.cap_log2) <= p.fired_hi) {
           dirty_g[gi[w]] = 1;
           late[w] = true;
+          if (p.dacc) {  // local-global delta ring (this workgroup owns the slot: plain RMW)
+            const uint32_t odc = p.dcnt[gi[w]];
+            if (AGG != AGG_COUNT) p.dacc[gi[w]] = odc ? agg_combine(AGG, p.dacc[gi[w]], d) : d;
+            p.dcnt[gi[w]] = odc + dc[w];
+          }
         }
       }
       if (p.dlist) {
@@ -1735,13 +1740,22 @@ __global__ __launch_bounds__(256) void dirty_clear_kernel(const uint32_t* __rest
                                                           uint32_t list_cap, int ring, int64_t nslots,
                                                           uint8_t* __restrict__ dirty_g,
                                                           uint32_t* __restrict__ slot_mark,
-                                                          int64_t p_lo, int np) {
+                                                          int64_t p_lo, int np,
+                                                          uint64_t* __restrict__ dacc,
+                                                          uint32_t* __restrict__ dcnt) {
   uint32_t n = *list_n;
   n = n < list_cap ? n : list_cap;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t s = list[i];
     slot_mark[s] = 0u;
-    for (int j = 0; j < np; ++j) dirty_g[(size_t)((p_lo + j) & (ring - 1)) * nslots + s] = 0;
+    for (int j = 0; j < np; ++j) {
+      const size_t gi = (size_t)((p_lo + j) & (ring - 1)) * nslots + s;
+      dirty_g[gi] = 0;
+      if (dcnt) {
+        dcnt[gi] = 0u;
+        dacc[gi] = 0ull;
+      }
+    }
   }
 }
 
@@ -3538,12 +3552,12 @@ void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t*
 
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
                  int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np,
-                 intptr_t stream) {
+                 intptr_t stream, uint64_t* dacc, uint32_t* dcnt) {
   if (list_cap == 0) return;
   np = np < ring ? np : ring;
   hipLaunchKernelGGL(dirty_clear_kernel, dim3(grid_for(list_cap, 256, 4096)), dim3(256), 0,
                      (hipStream_t)stream, list, list_n, list_cap, ring, nslots, dirty_g, slot_mark,
-                     p_lo, np);
+                     p_lo, np, dacc, dcnt);
   HIP_CHECK(hipGetLastError());
 }
 

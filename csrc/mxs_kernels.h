@@ -43,6 +43,11 @@ struct AggPlan {
   // point (mxs_common.h f64_to_fx), bit-identical between runs and between the GPU and the C++
   // twin. A value outside the fixed-point range sets flags[0] bit 3.
   int32_t det;
+  // Local-global aggregation with allowed lateness: the contributions of late-but-allowed data
+  // (panes <= fired_hi) are also accumulated into this delta ring (same layout as acc_g/cnt_g),
+  // so a re-firing ships only the deltas to the window's owner. Needs the touched-slot list.
+  uint64_t* dacc;
+  uint32_t* dcnt;
 };
 
 // Plan of one window firing.
@@ -281,9 +286,10 @@ void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t*
 void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
                     int nsub, int cap_log2, int ring, int64_t p_lo, int np, int64_t cutoff,
                     const CompactOut& out, uint32_t* occupancy, intptr_t stream);
+// (dacc/dcnt: the delta ring of local-global aggregation, zeroed for the same slots and panes.)
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
                  int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np,
-                 intptr_t stream);
+                 intptr_t stream, uint64_t* dacc = nullptr, uint32_t* dcnt = nullptr);
 }  // namespace gpu
 
 // ---- CPU twins (kernels_cpu.cpp) ------------------------------------------------------------
@@ -349,7 +355,8 @@ void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t*
                     int nsub, int cap_log2, int ring, int64_t p_lo, int np, int64_t cutoff,
                     const CompactOut& out, uint32_t* occupancy);
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
-                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np);
+                 int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np,
+                 uint64_t* dacc = nullptr, uint32_t* dcnt = nullptr);
 }  // namespace cpu
 
 }  // namespace mxs

@@ -180,6 +180,8 @@ class AggPlan:
     dense_mul: int = 0
     split: int = 1       # workgroups sharing an oversized sub-table (hot keys; GPU, see AGG_SLICE)
     det: int = 0         # 1: deterministic f64 sums (128-bit fixed-point per-step slot sums)
+    dacc: int = 0        # local-global delta ring of late data (data pointers, 0 = off) ...
+    dcnt: int = 0        # ... and its counts
 
     def as_dict(self) -> dict:
         return dict(self.__dict__)
@@ -296,22 +298,27 @@ def scatter_partials(keys, acc, cnt, n_dev, *, n_cap: int, max_parallelism: int,
 
 
 def dirty_clear(slot_list, slot_list_n, *, ring: int, nslots: int, dirty_g, slot_mark,
-                p_lo: int = 0, np_: int | None = None) -> None:
+                p_lo: int = 0, np_: int | None = None, dacc=None, dcnt=None) -> None:
     """Reset the touched-slot list's dirty bytes (panes p_lo .. p_lo + np_ - 1; default every
-    ring pane) and marks; the caller zeroes the list length afterwards."""
+    ring pane) and marks -- and the delta ring (dacc/dcnt) of the same slots and panes; the
+    caller zeroes the list length afterwards."""
     dev = dirty_g.device
     _check(slot_list, torch.int32, 0, "slot_list", dev)
     _check(slot_list_n, torch.int32, 1, "slot_list_n", dev)
     _check(dirty_g, torch.uint8, ring * nslots, "dirty_g", dev)
     _check(slot_mark, torch.int32, nslots, "slot_mark", dev)
+    if dacc is not None:
+        _check(dacc, torch.int64, ring * nslots, "dacc", dev)
+        _check(dcnt, torch.int32, ring * nslots, "dcnt", dev)
     m = load()
     np_ = ring if np_ is None else max(0, min(int(np_), ring))
     args = (_p(slot_list), _p(slot_list_n), slot_list.numel(), ring, nslots, _p(dirty_g),
             _p(slot_mark), int(p_lo), np_)
+    extra = (0, 0) if dacc is None else (_p(dacc), _p(dcnt))
     if _is_gpu(dirty_g):
-        m.gpu_dirty_clear(*args, _stream(dirty_g))
+        m.gpu_dirty_clear(*args, _stream(dirty_g), *extra)
     else:
-        m.cpu_dirty_clear(*args)
+        m.cpu_dirty_clear(*args, *extra)
 
 
 def rolling(recs, counts, *, cap_log2: int, nsub: int, agg: int, nsrc: int, bucket_cap: int,

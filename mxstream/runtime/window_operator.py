@@ -321,17 +321,16 @@ class KeyedWindowOperator:
         #   here is associative, so the emitted rows are identical; the exchange shrinks from
         #   ~#distinct (key, pane) per step to #keys per window, and the per-step work of a rank
         #   is the G = 1 step. HBM (288 GB) holds the whole key space per rank many times over.
-        #   Needs allowedLateness = 0 (a late refire would need every rank's delta since the
-        #   first fire), so "auto" picks it exactly then.
+        #   With allowed lateness the owner keeps every fired window's merged value until its
+        #   cleanup time, each rank accumulates its late-but-allowed data into a delta ring as
+        #   well, and a re-firing ships only those deltas (every aggregate merges deltas exactly).
         if exchange not in ("auto", "records", "partials"):
             raise ValueError("exchange must be 'auto', 'records' or 'partials'")
         # Deterministic f64 sums keep records exchange: a rank's partial would be rounded to a
         # double before the merge, so the result would depend on G.
-        lg_ok = (self.world > 1 and self.lateness == 0 and self._local_global_ok
-                 and not self.deterministic)
+        lg_ok = self.world > 1 and self._local_global_ok and not self.deterministic
         if exchange == "partials" and self.world > 1 and not lg_ok:
-            raise ValueError("exchange='partials' needs allowed_lateness == 0 and "
-                             "deterministic=False")
+            raise ValueError("exchange='partials' needs deterministic=False and a plain reduce")
         self.local_global = lg_ok and exchange != "records"
         self._exchanging = self.world > 1 and not self.local_global
         self._part_ranks = self.world if self._exchanging else 1
@@ -374,6 +373,11 @@ class KeyedWindowOperator:
         self.acc_g = torch.zeros(self.ring * self.nslots, dtype=torch.int64, device=dev)
         self.cnt_g = torch.zeros(self.ring * self.nslots, dtype=torch.int32, device=dev)
         self.dirty_g = torch.zeros(self.ring * self.nslots, dtype=torch.uint8, device=dev)
+        # Local-global with allowed lateness: the delta ring of late-but-allowed data.
+        self.dacc_g = self.dcnt_g = None
+        if self.local_global and self.lateness > 0:
+            self.dacc_g = torch.zeros(self.ring * self.nslots, dtype=torch.int64, device=dev)
+            self.dcnt_g = torch.zeros(self.ring * self.nslots, dtype=torch.int32, device=dev)
         self.occ = torch.zeros(self.nsub, dtype=torch.int32, device=dev)
         self.flags = torch.zeros(4, dtype=torch.int32, device=dev)
 
@@ -519,10 +523,14 @@ class KeyedWindowOperator:
         if self.nsub_o * self.world > 16384:
             raise ValueError("key space too large for the fire exchange; raise cap_log2")
         nslots_o = self.nsub_o << self.cap_log2_o
+        self.nslots_o = nslots_o
+        # One merge slice per window that fired but is not cleaned yet (allowed lateness), so a
+        # re-firing adds the ranks' deltas to the window's merged value.
+        self.ring_m = _next_pow2(math.ceil(self.lateness / self.slide) + 2)
         self.keys_m = torch.full((nslots_o,), -1, dtype=torch.int64, device=dev)
-        self.acc_m = torch.zeros(nslots_o, dtype=torch.int64, device=dev)
-        self.cnt_m = torch.zeros(nslots_o, dtype=torch.int32, device=dev)
-        self.dirty_m = torch.zeros(nslots_o, dtype=torch.uint8, device=dev)
+        self.acc_m = torch.zeros(self.ring_m * nslots_o, dtype=torch.int64, device=dev)
+        self.cnt_m = torch.zeros(self.ring_m * nslots_o, dtype=torch.int32, device=dev)
+        self.dirty_m = torch.zeros(self.ring_m * nslots_o, dtype=torch.uint8, device=dev)
         self.occ_m = torch.zeros(self.nsub_o, dtype=torch.int32, device=dev)
         self.fbcap = 1 << self.cap_log2_o
         nbf = self.world << self.nsub_o_log2
@@ -656,6 +664,16 @@ class KeyedWindowOperator:
                 acc[sn:sn + self.nslots].copy_(self.acc_g[so:so + self.nslots])
                 cnt[sn:sn + self.nslots].copy_(self.cnt_g[so:so + self.nslots])
                 dirty[sn:sn + self.nslots].copy_(self.dirty_g[so:so + self.nslots])
+        if self.dacc_g is not None:
+            dacc = torch.zeros(new_ring * self.nslots, dtype=torch.int64, device=self.device)
+            dcnt = torch.zeros(new_ring * self.nslots, dtype=torch.int32, device=self.device)
+            if self.min_live_pane is not None and self.max_seen_pane is not None:
+                for p in range(self.min_live_pane, self.max_seen_pane + 1):
+                    so = (p & (old - 1)) * self.nslots
+                    sn = (p & (new_ring - 1)) * self.nslots
+                    dacc[sn:sn + self.nslots].copy_(self.dacc_g[so:so + self.nslots])
+                    dcnt[sn:sn + self.nslots].copy_(self.dcnt_g[so:so + self.nslots])
+            self.dacc_g, self.dcnt_g = dacc, dcnt
         self.acc_g, self.cnt_g, self.dirty_g, self.ring = acc, cnt, dirty, new_ring
         self.metrics.ring_regrows += 1
 
@@ -944,6 +962,8 @@ class KeyedWindowOperator:
                 if self.dlist is not None:
                     aplan.dlist, aplan.dlist_n = self.dlist.data_ptr(), self.dlist_n.data_ptr()
                     aplan.slot_mark = self.slot_mark.data_ptr()
+                if self.dacc_g is not None:
+                    aplan.dacc, aplan.dcnt = self.dacc_g.data_ptr(), self.dcnt_g.data_ptr()
                 with self._stage("window_agg"):
                     self._aggregate(recs, counts, aplan)
                 if cuda and not self._exchanging:
@@ -1039,7 +1059,7 @@ class KeyedWindowOperator:
         if aplan.np_step > aplan.ring:
             raise ValueError("step touches more panes than the ring holds")
         key = (aplan.bucket_cap, aplan.rec_words, aplan.ring, aplan.nsrc, aplan.combined,
-               aplan.pg, aplan.dlist, aplan.det)
+               aplan.pg, aplan.dlist, aplan.det, aplan.dacc)
         if self._aplan_key != key:
             self._aplan = self._m.AggPlanObj(aplan.as_dict())
             self._aplan_key = key
@@ -1101,7 +1121,7 @@ class KeyedWindowOperator:
         if p1 < p0:
             return None
         if self.local_global:
-            return self._fire_window_partials(s, p0, p1)
+            return self._fire_window_partials(s, p0, p1, only_dirty)
         if self.host_tier is not None and self.host_tier.overlaps(p0, p1):
             return self._fire_window_tiered(s, p0, p1, only_dirty)
         self.out_n.zero_()
@@ -1149,22 +1169,31 @@ class KeyedWindowOperator:
         self.metrics.num_records_out += int(keys.size)
         return FireResult(s, s + self.size, keys, vals, raw, cnt, refire=only_dirty)
 
-    def _fire_window_partials(self, s: int, p0: int, p1: int) -> FireResult | None:
+    def _fire_window_partials(self, s: int, p0: int, p1: int, only_dirty: bool = False,
+                              emit: bool = True) -> FireResult | None:
         """Local-global fire of window [s, s + size): local partials -> owner -> emit.
 
         1. local fire without epilogue: one row (key, partial acc, count) per local key with
-           data in the window (all ranks, collectively identical decisions);
+           data in the window (all ranks, collectively identical decisions); a re-firing
+           (allowed lateness) reads the delta ring of the late data instead, only the listed
+           touched slots;
         2. scatter_partials: rows -> combined records in (owner rank, owner sub-table) buckets;
         3. ONE equal-split all-to-all of the buckets (+ their counts) over RCCL;
-        4. the owner folds the G partials per key into its merge table (window_agg, combined
-           records) and fires that with the fused map/filter epilogue; the merge pane is reset.
+        4. the owner folds the G partials per key into the window's merge slice (window_agg,
+           combined records; a first fire resets the slice, a re-firing adds the deltas to the
+           merged value and marks the keys) and fires it with the fused map/filter epilogue
+           (a re-firing: only the marked keys). The slice lives until the window is cleaned.
         The row count of step 1 stays on the device until the owner's fire is counted."""
         self.part_n.zero_()
-        K.window_fire(self.keys_g, self.acc_g, self.cnt_g, self.dirty_g, agg=self.agg,
+        delta = only_dirty and self.dacc_g is not None
+        K.window_fire(self.keys_g, self.dacc_g if delta else self.acc_g,
+                      self.dcnt_g if delta else self.cnt_g, self.dirty_g, agg=self.agg,
                       npanes=p1 - p0 + 1, ring=self.ring, p0=p0, wstart=s, wend=s + self.size,
-                      only_dirty=False, map_prog=E.EMPTY, filt_prog=E.EMPTY,
+                      only_dirty=only_dirty, map_prog=E.EMPTY, filt_prog=E.EMPTY,
                       out_keys=self.out_keys, out_vals=self.out_vals, out_raw=self.out_raw,
-                      out_cnt=self.out_cnt, out_n=self.part_n)
+                      out_cnt=self.out_cnt, out_n=self.part_n,
+                      slot_list=self.dlist if only_dirty else None,
+                      slot_list_n=self.dlist_n if only_dirty else None)
         self.fcursor.zero_()
         K.scatter_partials(self.out_keys, self.out_raw, self.out_cnt, self.part_n,
                            n_cap=self.out_keys.numel(), max_parallelism=self.max_parallelism,
@@ -1177,20 +1206,28 @@ class KeyedWindowOperator:
             self.comm.all_to_all(self.frecv_counts, self.fcursor)
         self.metrics.extra["a2a_bytes"] = self.metrics.extra.get("a2a_bytes", 0) + \
             self.fsend.numel() * 8
-        mplan = K.AggPlan(cap_log2=self.cap_log2_o, nsub=self.nsub_o, ring=1, agg=self.agg,
-                          nsrc=self.world, bucket_cap=self.fbcap, np_step=1, pg=1, pane_base=0,
-                          p_lo=0, fired_hi=I64_MIN, combined=1, rec_words=3,
-                          det=int(self.deterministic))
+        widx = (s - self.offset) // self.slide
+        so = (widx & (self.ring_m - 1)) * self.nslots_o
+        if not only_dirty:  # the slice's previous window is cleaned: reuse it
+            self.acc_m[so:so + self.nslots_o].zero_()
+            self.cnt_m[so:so + self.nslots_o].zero_()
+            self.dirty_m[so:so + self.nslots_o].zero_()
+        mplan = K.AggPlan(cap_log2=self.cap_log2_o, nsub=self.nsub_o, ring=self.ring_m,
+                          agg=self.agg, nsrc=self.world, bucket_cap=self.fbcap, np_step=1, pg=1,
+                          pane_base=widx, p_lo=0, fired_hi=widx if only_dirty else I64_MIN,
+                          combined=1, rec_words=3, det=int(self.deterministic))
         K.window_agg(self.frecv, self.frecv_counts, mplan, self.keys_m, self.acc_m, self.cnt_m,
                      self.dirty_m, self.occ_m, self.flags)
+        if not emit:  # restore: rebuild the merged value of an already fired window
+            return None
         self.out_n.zero_()
         K.window_fire(self.keys_m, self.acc_m, self.cnt_m, self.dirty_m, agg=self.agg, npanes=1,
-                      ring=1, p0=0, wstart=s, wend=s + self.size, only_dirty=False,
-                      map_prog=self.map_prog, filt_prog=self.filter_prog,
+                      ring=self.ring_m, p0=widx, wstart=s, wend=s + self.size,
+                      only_dirty=only_dirty, map_prog=self.map_prog, filt_prog=self.filter_prog,
                       out_keys=self.out_keys, out_vals=self.out_vals, out_raw=self.out_raw,
                       out_cnt=self.out_cnt, out_n=self.out_n)
-        self.acc_m.zero_()
-        self.cnt_m.zero_()
+        if only_dirty:
+            self.dirty_m[so:so + self.nslots_o].zero_()
         n = self._fired_count()
         self.metrics.num_fires += 1
         if n == 0:
@@ -1199,7 +1236,8 @@ class KeyedWindowOperator:
         self.metrics.num_records_out += n
         host = to_host_arrays([self.out_keys, self.out_vals, self.out_raw, self.out_cnt], n,
                               self._pool)
-        return FireResult(s, s + self.size, host[0].view(np.uint64), host[1], host[2], host[3])
+        return FireResult(s, s + self.size, host[0].view(np.uint64), host[1], host[2], host[3],
+                          refire=only_dirty)
 
     def _fired_count(self) -> int:
         """Rows the last fire produced; raises if any aggregation found its table full (a key
@@ -1337,7 +1375,7 @@ class KeyedWindowOperator:
         if self.dlist is not None:
             K.dirty_clear(self.dlist, self.dlist_n, ring=self.ring, nslots=self.nslots,
                           dirty_g=self.dirty_g, slot_mark=self.slot_mark, p_lo=pmin,
-                          np_=pmax - pmin + 1)
+                          np_=pmax - pmin + 1, dacc=self.dacc_g, dcnt=self.dcnt_g)
             self.dlist_n.zero_()
         else:
             for p in range(pmin, pmax + 1):
@@ -1494,7 +1532,12 @@ class KeyedWindowOperator:
         self.cnt_g.zero_()
         self.dirty_g.zero_()
         self.occ.zero_()
+        if self.local_global and self.lateness > 0:
+            self.dacc_g = torch.zeros(self.ring * self.nslots, dtype=torch.int64, device=dev)
+            self.dcnt_g = torch.zeros(self.ring * self.nslots, dtype=torch.int32, device=dev)
         if not len(rows["key"]):
+            if self.local_global:
+                self._rebuild_merge_ring()
             return
         keys = torch.from_numpy(np.ascontiguousarray(rows["key"])).to(dev)
         pane = torch.from_numpy(np.ascontiguousarray(rows["pane"])).to(dev)
@@ -1561,3 +1604,27 @@ class KeyedWindowOperator:
         occ_slots = slots_u if occ_slots is None else occ_slots
         self.occ.copy_(torch.bincount(occ_slots >> self.cap_log2, minlength=self.nsub)
                        .to(torch.int32))
+        if self.local_global:
+            self._rebuild_merge_ring()
+
+    def _rebuild_merge_ring(self) -> None:
+        """Local-global with allowed lateness, after a restore: the owners' merged values of the
+        windows that fired but are not cleaned (a late re-firing adds deltas to them) are
+        recomputed from the restored state -- the same collective exchange as a fire, without
+        the emit. Every rank runs the same window sequence (identical restored bookkeeping)."""
+        self.keys_m.fill_(-1)
+        self.acc_m.zero_()
+        self.cnt_m.zero_()
+        self.dirty_m.zero_()
+        self.occ_m.zero_()
+        if (self.lateness <= 0 or self.next_fire_start is None or self.min_live_pane is None
+                or self.wm == I64_MIN):
+            return
+        s = max(self._align_up(self.wm - self.size - self.lateness + 2),
+                self.first_start_containing(self.pane_start(self.min_live_pane)))
+        while s < self.next_fire_start:
+            p0 = max(self.pane_of(s), self.min_live_pane)
+            p1 = min(self.pane_of(s) + self.panes_per_window - 1, self.max_seen_pane)
+            if p1 >= p0:
+                self._fire_window_partials(s, p0, p1, only_dirty=False, emit=False)
+            s += self.slide

@@ -29,27 +29,37 @@ def _sizes(dev):
     return (3000, 5000, 8) if dev == "cpu" else (150_000, 60_000, None)
 
 
-def _batch(dev, rank, step, per, nkeys, span=2000, disorder=700):
+def _batch(dev, rank, step, per, nkeys, span=2000, disorder=700, late=0):
     d = torch.device(dev)
     keys = torch.empty(per, dtype=torch.int64, device=d)
     ts = torch.empty_like(keys)
     vals = torch.empty_like(keys)
     K.gen_events(keys, ts, vals, seed=11, stream_id=rank, idx0=step * per, nkeys=nkeys,
                  ts_base=step * span, ts_span=span, disorder=disorder, val_lo=0, val_span=1000)
+    if late and step >= 2:
+        ts[::37] -= late  # behind the watermark: late, mostly within the allowed lateness
     # Every source partition ends its batch at the same event time, so the G-rank watermark
     # (MIN over ranks of max ts - bound) equals the single-rank reference's (max over all).
     ts[-1] = step * span + span
     return keys, ts, vals
 
 
-def _concat(dev, world, step, per, nkeys):
-    parts = [_batch(dev, r, step, per, nkeys) for r in range(world)]
+def _concat(dev, world, step, per, nkeys, late=0):
+    parts = [_batch(dev, r, step, per, nkeys, late=late) for r in range(world)]
     return [torch.cat([p[i] for p in parts]) for i in range(3)]
 
 
 def _collect(out):
     return {(r.window_start, int(k)): (int(a), int(c))
             for r in out for k, a, c in zip(r.keys, r.raw, r.counts)}
+
+
+def _collect_seq(out):
+    seq = {}
+    for r in out:
+        for k, a, c in zip(r.keys, r.raw, r.counts):
+            seq.setdefault((r.window_start, int(k)), []).append((bool(r.refire), int(a), int(c)))
+    return seq
 
 
 def _skip_no_gpu(dev):
@@ -61,7 +71,8 @@ def _skip_no_gpu(dev):
 @pytest.mark.parametrize("world", [1, 2, 4, 8])
 @pytest.mark.parametrize("size,slide,lateness,exchange", [
     (3000, 3000, 0, "records"), (3000, 3000, 0, "partials"), (4000, 1000, 0, "partials"),
-    (4000, 1000, 1500, "records")])
+    (4000, 1000, 1500, "records"), (4000, 1000, 1500, "partials"),
+    (3000, 3000, 2500, "partials")])
 @pytest.mark.parametrize("pipeline", [False, True, "stream"])
 def test_window_invariant_to_world(dev, world, size, slide, lateness, exchange, pipeline):
     """pipeline=True: the partition of batch i+1 overlaps the combiner / all-to-all /
@@ -70,6 +81,7 @@ def test_window_invariant_to_world(dev, world, size, slide, lateness, exchange, 
     aggregation (no per-step exchange; partial accumulators travel when a window fires)."""
     _skip_no_gpu(dev)
     per, nkeys, cap_log2 = _sizes(dev)
+    late_shift = lateness * 9 // 10 + 700 if lateness else 0
 
     def make(comm, batch_capacity, pipe=pipeline):
         return KeyedWindowOperator(size=size, slide=slide, lateness=lateness, agg=K.AGG_SUM_I64,
@@ -81,25 +93,32 @@ def test_window_invariant_to_world(dev, world, size, slide, lateness, exchange, 
         op = make(comm, per)
         out = []
         for step in range(STEPS):
-            out += op.process(*_batch(dev, comm.rank, step, per, nkeys))
+            out += op.process(*_batch(dev, comm.rank, step, per, nkeys, late=late_shift))
         out += op.finish()
-        return _collect(out), op.metrics.num_late_records_dropped, op.metrics.extra
+        return _collect(out), op.metrics.num_late_records_dropped, op.metrics.extra, \
+            _collect_seq(out)
 
     res = run_loopback(world, rank_fn, device=torch.device(dev))
-    merged, late = {}, 0
-    for d, nl, _ in res:
+    merged, late, seqs = {}, 0, {}
+    for d, nl, _, sq in res:
         assert not (set(d) & set(merged)), "a (window, key) fired on two ranks"
         merged.update(d)
+        seqs.update(sq)
         late += nl
     ref_op = make(None, per * world, pipe=False)  # unpipelined single rank: the reference
     out = []
     for step in range(STEPS):
-        out += ref_op.process(*_concat(dev, world, step, per, nkeys))
+        out += ref_op.process(*_concat(dev, world, step, per, nkeys, late=late_shift))
     out += ref_op.finish()
     ref = _collect(out)
     assert len(ref) > 0
     assert merged == ref
     assert late == ref_op.metrics.num_late_records_dropped
+    if lateness:
+        # every firing and re-firing of every (window, key), in order, with its value
+        ref_seq = _collect_seq(out)
+        assert sum(len(v) for v in ref_seq.values()) > len(ref_seq)  # re-firings happened
+        assert seqs == ref_seq
 
 
 @pytest.mark.parametrize("dev", _devices())
