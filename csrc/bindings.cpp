@@ -750,6 +750,29 @@ PYBIND11_MODULE(_mxs_native, m) {
       cpu::dict_assign_new(P<char>(text), n, nstr, o, d, P<int64_t>(newpos));
     }
   });
+  m.def("dict_find_new", [](bool cuda, int64_t n, int32_t nstr, py::dict out, py::dict dict,
+                            intptr_t scratch, intptr_t newpos, intptr_t stream) {
+    const IngestOut o = make_ingest_out(out);
+    const DictState d = make_dict(dict);
+    if (cuda) gpu::dict_find_new(n, nstr, o, d, P<void>(scratch), P<int64_t>(newpos), stream);
+    else cpu::dict_find_new(n, nstr, o, d, P<int64_t>(newpos));
+  });
+  m.def("dict_insert_ids", [](bool cuda, intptr_t buf, intptr_t offs, intptr_t lens, int64_t k,
+                              int64_t id0, py::dict dict, intptr_t stream) {
+    const DictState d = make_dict(dict);
+    if (cuda) {
+      gpu::dict_insert_ids(P<uint8_t>(buf), P<int64_t>(offs), P<int32_t>(lens), k, id0, d, stream);
+    } else {
+      cpu::dict_insert_ids(P<uint8_t>(buf), P<int64_t>(offs), P<int32_t>(lens), k, id0, d);
+    }
+  });
+  m.def("dict_resolve", [](bool cuda, intptr_t text, int64_t n, int32_t nstr, py::dict out,
+                           py::dict dict, intptr_t stream) {
+    const IngestOut o = make_ingest_out(out);
+    const DictState d = make_dict(dict);
+    if (cuda) gpu::dict_resolve(P<char>(text), n, nstr, o, d, stream);
+    else cpu::dict_resolve(P<char>(text), n, nstr, o, d);
+  });
   m.def("dict_rehash", [](bool cuda, intptr_t old_h, intptr_t old_id, int64_t old_cap,
                           py::dict dict, intptr_t stream) {
     const DictState d = make_dict(dict);

@@ -58,8 +58,8 @@ void ingest_parse(const char* text, int64_t text_len, const int64_t* starts, int
   }
 }
 
-void dict_assign_new(const char* text, int64_t n, int32_t nstr, const IngestOut& o,
-                     const DictState& d, int64_t* newpos) {
+void dict_find_new(int64_t n, int32_t nstr, const IngestOut& o, const DictState& d,
+                   int64_t* newpos) {
   const int64_t np = n * nstr;
   int64_t k = 0;
   for (int64_t p = 0; p < np; ++p) {
@@ -67,6 +67,56 @@ void dict_assign_new(const char* text, int64_t n, int32_t nstr, const IngestOut&
     if (s >= 0 && d.tab_id[s] < 0 && d.tab_first[s] == p) newpos[k++] = p;
   }
   d.ctr[3] = k;
+}
+
+void dict_resolve(const char* text, int64_t n, int32_t nstr, const IngestOut& o,
+                  const DictState& d) {
+  const int64_t np = n * nstr;
+  for (int64_t p = 0; p < np; ++p) {
+    const int32_t s = o.sslot[p];
+    int32_t id = -1;
+    if (s >= 0) {
+      id = d.tab_id[s];
+      const bool same = id >= 0 && d.id_len[id] == o.slen[p] &&
+                        std::memcmp(text + o.spos[p], d.arena + d.id_off[id], (size_t)o.slen[p]) == 0;
+      if (!same) {
+        d.ctr[2] |= kDictErrCollision;
+        id = -1;
+      }
+    }
+    const int64_t li = p / nstr, si = p - li * nstr;
+    o.ids[si * n + li] = id;
+  }
+}
+
+void dict_insert_ids(const uint8_t* buf, const int64_t* offs, const int32_t* lens, int64_t k,
+                     int64_t id0, const DictState& d) {
+  d.ctr[0] = id0 + k;
+  for (int64_t i = 0; i < k; ++i) {
+    const char* str = (const char*)buf + offs[i];
+    const int32_t len = lens[i];
+    const int32_t slot = probe_insert(d, text_hash64(str, len));
+    const int64_t id = id0 + i;
+    if (slot < 0 || id >= d.id_cap || d.ctr[1] + len > d.arena_cap) {
+      d.ctr[2] |= slot < 0 ? kDictErrFull : kDictErrCapacity;
+      continue;
+    }
+    const int64_t off = d.ctr[1];
+    d.ctr[1] += len;
+    std::memcpy(d.arena + off, str, (size_t)len);
+    d.id_off[id] = off;
+    d.id_len[id] = len;
+    d.id_jh[id] = java_hash_utf8(str, len);
+    d.tab_first[slot] = INT64_MAX;
+    d.tab_id[slot] = (int32_t)id;
+  }
+}
+
+void dict_assign_new(const char* text, int64_t n, int32_t nstr, const IngestOut& o,
+                     const DictState& d, int64_t* newpos) {
+  const int64_t np = n * nstr;
+  dict_find_new(n, nstr, o, d, newpos);
+  const int64_t k = d.ctr[3];
   const int64_t n_ids = d.ctr[0];
   for (int64_t j = 0; j < k; ++j) {
     const int64_t p = newpos[j];
@@ -87,21 +137,8 @@ void dict_assign_new(const char* text, int64_t n, int32_t nstr, const IngestOut&
     d.tab_id[s] = (int32_t)id;
   }
   d.ctr[0] += k;
-  for (int64_t p = 0; p < np; ++p) {
-    const int32_t s = o.sslot[p];
-    int32_t id = -1;
-    if (s >= 0) {
-      id = d.tab_id[s];
-      const bool same = id >= 0 && d.id_len[id] == o.slen[p] &&
-                        std::memcmp(text + o.spos[p], d.arena + d.id_off[id], (size_t)o.slen[p]) == 0;
-      if (!same) {
-        d.ctr[2] |= kDictErrCollision;
-        id = -1;
-      }
-    }
-    const int64_t li = p / nstr, si = p - li * nstr;
-    o.ids[si * n + li] = id;
-  }
+  (void)np;
+  dict_resolve(text, n, nstr, o, d);
 }
 
 void dict_rehash(const uint64_t* old_h, const int32_t* old_id, int64_t old_cap, const DictState& d) {

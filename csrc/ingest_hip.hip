@@ -199,6 +199,48 @@ __global__ __launch_bounds__(256) void dict_resolve_kernel(const char* __restric
   }
 }
 
+// Agreed ids (several ranks, csrc/ingest.h): string i of a packed list gets id id0 + i -- in the
+// slot this batch's parse claimed for it, or in a fresh slot (a string new on another rank).
+__global__ __launch_bounds__(256) void dict_insert_ids_kernel(const uint8_t* __restrict__ buf,
+                                                              const int64_t* __restrict__ offs,
+                                                              const int32_t* __restrict__ lens,
+                                                              int64_t k, int64_t id0, DictState d) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.ctr[0] = id0 + k;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < k; i += stride) {
+    const char* str = (const char*)buf + offs[i];
+    const int32_t len = lens[i];
+    const uint64_t h = text_hash64(str, len);
+    uint32_t q = dict_home(h, d.mask);
+    int32_t slot = -1;
+    for (uint32_t t = 0; t <= d.mask; ++t) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&d.tab_h[q], 0ull, (unsigned long long)h);
+      if (prev == 0 || prev == h) {
+        slot = (int32_t)q;
+        break;
+      }
+      q = (q + 1) & d.mask;
+    }
+    const int64_t id = id0 + i;
+    if (slot < 0 || id >= d.id_cap) {
+      atomicOr((unsigned long long*)&d.ctr[2], (unsigned long long)(slot < 0 ? kDictErrFull
+                                                                             : kDictErrCapacity));
+      continue;
+    }
+    const int64_t off = (int64_t)atomicAdd((unsigned long long*)&d.ctr[1], (unsigned long long)len);
+    if (off + len > d.arena_cap) {
+      atomicOr((unsigned long long*)&d.ctr[2], (unsigned long long)kDictErrCapacity);
+      continue;
+    }
+    for (int32_t c = 0; c < len; ++c) d.arena[off + c] = (uint8_t)str[c];
+    d.id_off[id] = off;
+    d.id_len[id] = len;
+    d.id_jh[id] = java_hash_utf8(str, len);
+    d.tab_first[slot] = INT64_MAX;
+    d.tab_id[slot] = (int32_t)id;
+  }
+}
+
 // Grow: re-insert the assigned entries of the old table into an empty one.
 __global__ __launch_bounds__(256) void dict_rehash_kernel(const uint64_t* __restrict__ old_h,
                                                           const int32_t* __restrict__ old_id,
@@ -308,10 +350,13 @@ void ingest_parse(const char* text, int64_t text_len, const int64_t* starts, int
   ING_CHECK(hipGetLastError());
 }
 
-void dict_assign_new(const char* text, int64_t n, int32_t nstr, const IngestOut& o,
-                     const DictState& d, void* scratch, int64_t* newpos, intptr_t stream) {
+void dict_find_new(int64_t n, int32_t nstr, const IngestOut& o, const DictState& d,
+                   void* scratch, int64_t* newpos, intptr_t stream) {
   const int64_t np = n * nstr;
-  if (np <= 0) return;
+  if (np <= 0) {
+    ING_CHECK(hipMemsetAsync(&d.ctr[3], 0, 8, (hipStream_t)stream));
+    return;
+  }
   const int64_t nt = (np + kFcTile - 1) / kFcTile;
   uint64_t* masks = (uint64_t*)scratch;
   int64_t* offs = (int64_t*)(masks + nt * kFcWords);
@@ -320,13 +365,35 @@ void dict_assign_new(const char* text, int64_t n, int32_t nstr, const IngestOut&
                      o.sslot, np, d, masks, counts);
   ING_CHECK(hipGetLastError());
   compact_from_masks(masks, counts, nt, np, offs, newpos, &d.ctr[3], stream);
+}
+
+void dict_resolve(const char* text, int64_t n, int32_t nstr, const IngestOut& o,
+                  const DictState& d, intptr_t stream) {
+  const int64_t np = n * nstr;
+  if (np <= 0) return;
+  hipLaunchKernelGGL(dict_resolve_kernel, dim3(ing_grid(np, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, text, n, nstr, o, d);
+  ING_CHECK(hipGetLastError());
+}
+
+void dict_assign_new(const char* text, int64_t n, int32_t nstr, const IngestOut& o,
+                     const DictState& d, void* scratch, int64_t* newpos, intptr_t stream) {
+  const int64_t np = n * nstr;
+  if (np <= 0) return;
+  dict_find_new(n, nstr, o, d, scratch, newpos, stream);
   hipLaunchKernelGGL(dict_assign_kernel, dim3(ing_grid(np, 256, 2048)), dim3(256), 0,
                      (hipStream_t)stream, text, newpos, np, o, d);
   ING_CHECK(hipGetLastError());
   hipLaunchKernelGGL(dict_commit_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d);
   ING_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(dict_resolve_kernel, dim3(ing_grid(np, 256, 8192)), dim3(256), 0,
-                     (hipStream_t)stream, text, n, nstr, o, d);
+  dict_resolve(text, n, nstr, o, d, stream);
+}
+
+void dict_insert_ids(const uint8_t* buf, const int64_t* offs, const int32_t* lens, int64_t k,
+                     int64_t id0, const DictState& d, intptr_t stream) {
+  if (k <= 0) return;
+  hipLaunchKernelGGL(dict_insert_ids_kernel, dim3(ing_grid(k, 256, 2048)), dim3(256), 0,
+                     (hipStream_t)stream, buf, offs, lens, k, id0, d);
   ING_CHECK(hipGetLastError());
 }
 

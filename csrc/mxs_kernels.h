@@ -189,6 +189,15 @@ void dict_assign_new(const char* text, int64_t n, int32_t nstr, const IngestOut&
                      const DictState& d, void* scratch, int64_t* newpos, intptr_t stream);
 void dict_rehash(const uint64_t* old_h, const int32_t* old_id, int64_t old_cap, const DictState& d,
                  intptr_t stream);
+// Several ranks agree on ids: find this batch's new strings (no ids yet) ...
+void dict_find_new(int64_t n, int32_t nstr, const IngestOut& o, const DictState& d,
+                   void* scratch, int64_t* newpos, intptr_t stream);
+// ... insert the agreed list (string i -> id id0 + i) ...
+void dict_insert_ids(const uint8_t* buf, const int64_t* offs, const int32_t* lens, int64_t k,
+                     int64_t id0, const DictState& d, intptr_t stream);
+// ... and resolve the batch's string fields to ids.
+void dict_resolve(const char* text, int64_t n, int32_t nstr, const IngestOut& o,
+                  const DictState& d, intptr_t stream);
 void ingest_filter_compact(const int64_t* cols, int64_t n, int32_t nf, int32_t dbl_mask,
                            const ExprProg& prog, void* scratch, int64_t* idx, int64_t* total,
                            intptr_t stream);
@@ -323,6 +332,12 @@ void ingest_parse(const char* text, int64_t text_len, const int64_t* starts, int
 void dict_assign_new(const char* text, int64_t n, int32_t nstr, const IngestOut& o,
                      const DictState& d, int64_t* newpos);
 void dict_rehash(const uint64_t* old_h, const int32_t* old_id, int64_t old_cap, const DictState& d);
+void dict_find_new(int64_t n, int32_t nstr, const IngestOut& o, const DictState& d,
+                   int64_t* newpos);
+void dict_insert_ids(const uint8_t* buf, const int64_t* offs, const int32_t* lens, int64_t k,
+                     int64_t id0, const DictState& d);
+void dict_resolve(const char* text, int64_t n, int32_t nstr, const IngestOut& o,
+                  const DictState& d);
 void ingest_filter_compact(const int64_t* cols, int64_t n, int32_t nf, int32_t dbl_mask,
                            const ExprProg& prog, int64_t* idx, int64_t* total);
 void ingest_gather(const int64_t* cols, int64_t n, int32_t nf, const int32_t* ids, int32_t nstr,

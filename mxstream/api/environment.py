@@ -257,7 +257,11 @@ class StreamExecutionEnvironment:
 
         sinks = plan(self, list(self._sinks))
         job_id = secrets.token_hex(16)
-        if getattr(self, "world", 1) > 1:
+        comm = getattr(self, "_comm", None)  # injected (LoopbackComm: virtual ranks in tests)
+        if comm is not None:
+            self.rank, self.world = comm.rank, comm.world
+            job_id = comm.broadcast_object(job_id, src=0)
+        elif getattr(self, "world", 1) > 1:
             # All ranks of a multi-process job share one job id (checkpoint directory).
             from ..parallel.comm import init_distributed
 
@@ -267,7 +271,7 @@ class StreamExecutionEnvironment:
         while True:
             try:
                 result = Executor(self, sinks, job_name, job_id=job_id, restore_from=restore,
-                                  attempt=attempts).run()
+                                  attempt=attempts, comm=comm).run()
                 break
             except Exception as e:
                 kind = self.restart_strategy[0]

@@ -212,8 +212,12 @@ def _lower_text(env, sinks) -> None:
         dev = str(env.config.device)
         ingest_dev = dev if (mode == "device" or (mode == "auto" and dev.startswith("cuda"))) \
             else None
-        t.factory = (lambda spec=spec, ts_spec=ts_spec, bound=bound, filt=filt, d=ingest_dev:
-                     TextParseOp(spec, ts_spec=ts_spec, bound=bound, filter_prog=filt, device=d))
+        # The device ingest's dictionary is shared with the keyed native operators downstream
+        # (names of fired keys, Java hashes of key groups at G > 1).
+        shared: dict = {}
+        t.factory = (lambda spec=spec, ts_spec=ts_spec, bound=bound, filt=filt, d=ingest_dev,
+                     sh=shared: TextParseOp(spec, ts_spec=ts_spec, bound=bound, filter_prog=filt,
+                                            device=d, shared=sh))
         t.parents = [parent]
         if fnode is not None:
             fnode.factory = PassThroughOp
@@ -228,7 +232,8 @@ def _lower_text(env, sinks) -> None:
             return s
 
         parent.factory = columnar_source
-        t.meta = dict(meta, columnar=True, text_spec=spec)
+        t.meta = dict(meta, columnar=True, text_spec=spec,
+                      device_ingest=shared if ingest_dev is not None else None)
 
 
 def plan(env, sinks):
@@ -517,11 +522,20 @@ def _install_native(env, t, ws, spec, key_pos, val_pos, kind, result, ok_arities
     cls = NativeSessionOp if session else (
         NativeMedianOp if kind == "median" else
         NativeVectorWindowOp if kind in ("vsum", "vavg") else NativeWindowOp)
+    # Input straight from the device ingest: the operator knows its column kinds up front and
+    # shares the ingest's dictionary (the G > 1 device exchange needs both before any data).
+    device_input = None
+    for p in t.parents:
+        pm = getattr(p, "meta", None) or {}
+        if pm.get("device_ingest") is not None and pm.get("text_spec") is not None:
+            device_input = (tuple(k for _, k in pm["text_spec"].fields), pm["device_ingest"])
 
     def factory():
-        return cls(key_fn=key_fn, key_pos=key_pos, val_pos=val_pos, kind=kind,
-                   assigner=assigner, lateness=late, late_tag=tag, device=device,
-                   fallback_factory=fallback, result_builder=builder, ok_arities=ok_arities)
+        op = cls(key_fn=key_fn, key_pos=key_pos, val_pos=val_pos, kind=kind,
+                 assigner=assigner, lateness=late, late_tag=tag, device=device,
+                 fallback_factory=fallback, result_builder=builder, ok_arities=ok_arities)
+        op.device_input = device_input
+        return op
 
     t.factory = factory
     t.meta = dict(t.meta, native=True)

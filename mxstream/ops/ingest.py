@@ -96,20 +96,43 @@ class DeviceDict:
         out[:t.numel()].copy_(t)
         return out
 
-    def reserve(self, new_strings: int, new_bytes: int) -> None:
+    def reserve(self, new_strings: int, new_bytes: int) -> bool:
         """Capacity for up to `new_strings` more ids / `new_bytes` more arena bytes: the table stays
         at most half full, so probes are short and an insert always finds a slot. Growth is
-        stream-ordered (no host sync)."""
+        stream-ordered (no host sync). Returns True when the table was rehashed (slots moved)."""
         need = self.n_ids + int(new_strings)
+        moved = False
         if 2 * need > self.cap:
             old_h, old_id, old_cap = self.tab_h, self.tab_id, self.cap
             self._alloc_table(_pow2(2 * need))
             self._m.dict_rehash(self.cuda, old_h.data_ptr(), old_id.data_ptr(), old_cap,
                                 self.state(), self._stream())
+            moved = True
         self.id_off = self._grow(self.id_off, need)
         self.id_len = self._grow(self.id_len, need)
         self.id_jh = self._grow(self.id_jh, need)
         self.arena = self._grow(self.arena, self.arena_used + int(new_bytes))
+        return moved
+
+    def add_agreed(self, strings: list[bytes]) -> None:
+        """Append an agreed list of new strings (several ranks: every rank adds the same list
+        in the same order, so ids agree): string i gets id n_ids + i."""
+        if not strings:
+            return
+        self.reserve(len(strings), sum(len(b) for b in strings))
+        buf = b"".join(strings)
+        lens = np.fromiter((len(b) for b in strings), dtype=np.int32, count=len(strings))
+        offs = np.zeros(len(strings), dtype=np.int64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.int64)
+        dev = self.device
+        tb = torch.from_numpy(np.frombuffer(buf, dtype=np.uint8).copy() if buf else
+                              np.zeros(1, np.uint8)).to(dev)
+        to = torch.from_numpy(offs).to(dev)
+        tl = torch.from_numpy(lens).to(dev)
+        self._m.dict_insert_ids(self.cuda, tb.data_ptr(), to.data_ptr(), tl.data_ptr(),
+                                len(strings), self.n_ids, self.state(), self._stream())
+        self.n_ids += len(strings)
+        self.arena_used += len(buf)
 
     def note_counters(self, ctr: list[int]) -> None:
         """Host view of the device counters after a batch (read back with the batch's other
@@ -258,9 +281,14 @@ class TextIngest:
         return dev, slot[0]
 
     # ---- parse ----------------------------------------------------------------------------------
-    def parse(self, data, nlines: int | None = None, on_upload=None) -> IngestResult:
+    def parse(self, data, nlines: int | None = None, on_upload=None, agree=None) -> IngestResult:
         """on_upload(event): called with a device event recorded after the H2D copy of a host
-        tensor input (its pinned slot may be reused once the event completed)."""
+        tensor input (its pinned slot may be reused once the event completed).
+
+        agree(list[bytes]) -> list[bytes]: several ranks share one id space (keyBy across GPUs
+        needs the same id for the same string everywhere): the batch's new strings go to `agree`
+        (a collective: every rank's new strings, in rank order, deduplicated), every rank appends
+        the agreed list to its dictionary, and the batch is resolved against it."""
         m = self._m
         n = count_lines(data) if nlines is None else int(nlines)
         nbytes = len(data) if not isinstance(data, torch.Tensor) else data.numel()
@@ -268,6 +296,8 @@ class TextIngest:
         self.stats["lines"] += n
         self.stats["bytes"] += nbytes
         if n == 0:
+            if agree is not None:
+                self.dict.add_agreed(agree([]))
             empty = [torch.empty(0, dtype=torch.int32 if k == FK_STR else
                                  (torch.float64 if k == FK_DOUBLE else torch.int64), device=self.device)
                      for k in self.kinds]
@@ -311,10 +341,12 @@ class TextIngest:
         ds = self.dict.state()
         m.ingest_parse(self.cuda, buf.data_ptr(), nbytes, starts.data_ptr(), n, self._spec, out,
                        ds, st)
-        if S:
+        if S and agree is None:
             newpos = self._buf("newpos", np_, torch.int64)
             m.dict_assign_new(self.cuda, buf.data_ptr(), n, S, out, ds, scratch.data_ptr(),
                               newpos.data_ptr(), st)
+        elif agree is not None:
+            self._agree_ids(agree, data, keep_alive, buf, nbytes, starts, n, out, scratch)
         fidx = None
         if self.filter_prog is not None:
             fidx = self._buf("fidx", n, torch.int64)
@@ -350,6 +382,44 @@ class TextIngest:
             line_idx = fidx[:k].clone()
             return self._result(ocols, oids, max(k, 1), k, max_ts, line_idx, n)
         return self._result(cols, ids, n, n, max_ts, None, n)
+
+    def _agree_ids(self, agree, data, keep_alive, buf, nbytes, starts, n, out, scratch) -> None:
+        """Several ranks: this batch's new strings -> agree() -> the agreed list appended on every
+        rank -> resolve. One extra host round trip per batch (the new strings' positions)."""
+        m, S, st = self._m, self.nstr, self._stream()
+        local: list[bytes] = []
+        if S:
+            np_ = n * S
+            newpos = self._buf("newpos", np_, torch.int64)
+            m.dict_find_new(self.cuda, n, S, out, self.dict.state(), scratch.data_ptr(),
+                            newpos.data_ptr(), st)
+            k = int(self.dict.ctr[3].item())
+            if k:
+                pos = newpos[:k]
+                spos = self._ws["spos"][pos].cpu().numpy()
+                slen = self._ws["slen"].index_select(0, pos).cpu().numpy()
+                if isinstance(data, torch.Tensor):
+                    raw = (data if data.device.type == "cpu" else data.cpu()).numpy()
+                    local = [raw[a:a + b].tobytes() for a, b in zip(spos.tolist(), slen.tolist())]
+                else:
+                    mv = bytes(data)
+                    local = [mv[a:a + b] for a, b in zip(spos.tolist(), slen.tolist())]
+        agreed = agree(local)
+        if agreed:
+            moved = self.dict.reserve(len(agreed), sum(len(b) for b in agreed))
+            if moved:
+                # The rehash dropped this batch's claimed-but-unassigned slots: insert the agreed
+                # list into the new table, then probe the batch again (every string now has an id).
+                self.dict.add_agreed(agreed)
+                ctl = self._ws["ctl"][:8]
+                m.ingest_parse(self.cuda, buf.data_ptr(), nbytes, starts.data_ptr(), n,
+                               self._spec, dict(out, nflag=ctl[6:7].data_ptr(),
+                                                maxts=ctl[7:8].data_ptr()),
+                               self.dict.state(), st)
+            else:
+                self.dict.add_agreed(agreed)
+        if S:
+            m.dict_resolve(self.cuda, buf.data_ptr(), n, S, out, self.dict.state(), st)
 
     def _result(self, cols, ids, stride, k, max_ts, line_idx, n_lines) -> IngestResult:
         out = []

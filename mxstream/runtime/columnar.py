@@ -196,7 +196,7 @@ class TextParseOp(Operator):
     name = "Map"
 
     def __init__(self, spec, *, ts_spec=None, bound: int = 0, filter_prog=None,
-                 threads: int | None = None, device: str | None = None):
+                 threads: int | None = None, device: str | None = None, shared=None):
         self.spec = spec
         self.ts_spec = ts_spec
         self.bound = int(bound)
@@ -205,6 +205,8 @@ class TextParseOp(Operator):
         # device: parse on this device (ops/ingest.py: device parse kernels + device string
         # dictionary, C++ twins on "cpu"); None: the host C++ parser (parse_lines).
         self.device = device
+        self.shared = shared if shared is not None else {}
+        self.agree = None
         self.cur_max = LONG_MIN + self.bound  # BoundedOutOfOrdernessTimestampExtractor state
         self.cur_wm = LONG_MIN
 
@@ -226,16 +228,33 @@ class TextParseOp(Operator):
             from ..ops.ingest import DeviceDict, TextIngest
 
             self.strings = DeviceDict(self.device)
+            self.shared["dict"] = self.strings
             self.ingest = TextIngest(fields, sep=self.spec.sep, offset_s=self.offset_s,
                                      ts_field=len(self.spec.fields) if self.ts_spec is not None else -1,
                                      device=self.device, dictionary=self.strings,
                                      filter_prog=self.filter_prog)
+            ctrl = getattr(ctx, "ctrl", None)
+            if ctrl is not None and ctrl.world > 1:
+                # Several ranks: one id space for every rank (keyBy across GPUs). Each pass parses
+                # this rank's batch and agrees on the new strings with every rank (collective).
+                self.collective = True
+
+                def agree(local, ctrl=ctrl):
+                    seen, out = set(), []
+                    for lst in ctrl.all_gather_object(local):
+                        for b in lst:
+                            if b not in seen:
+                                seen.add(b)
+                                out.append(b)
+                    return out
+
+                self.agree = agree
         else:
             self.strings = self.m.StringDict()
 
     def _parse_device(self, tb: TextBatch) -> DeviceColumnBatch:
         res = self.ingest.parse(tb.data, tb.n, on_upload=None if tb.token is None
-                                else tb.token.uploaded)
+                                else tb.token.uploaded, agree=self.agree)
         nf = len(self.spec.fields)
         return DeviceColumnBatch(res.n, res.cols[:nf], tuple(k for _, k in self.spec.fields),
                                  self.strings, res.ts, sub0=tb.sub0,
@@ -283,7 +302,25 @@ class TextParseOp(Operator):
             return [WM(wm)]
         return []
 
+    @staticmethod
+    def _one_batch(batches: list) -> TextBatch:
+        """A pass's text batches as one (one dictionary agreement per pass on every rank)."""
+        if len(batches) == 1:
+            return batches[0]
+        parts = []
+        for b in batches:
+            d = b.host_bytes()
+            parts.append(d if not d or d.endswith(b"\n") else d + b"\n")
+        return TextBatch(b"".join(parts), sum(b.n for b in batches), batches[0].sub0,
+                         batches[0].parallelism)
+
     def process(self, items):
+        if self.agree is not None:
+            # Multi-rank device ingest: exactly one parse (and dictionary agreement) per pass.
+            tbs = [it for it in items if isinstance(it, TextBatch)]
+            tb = self._one_batch(tbs) if tbs else TextBatch(b"", 0)
+            rest = [it for it in items if not isinstance(it, TextBatch)]
+            items = rest[:0] + [tb] + rest
         out = []
         for it in items:
             if isinstance(it, WM):

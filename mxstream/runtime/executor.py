@@ -107,7 +107,7 @@ class Executor:
     operator)."""
 
     def __init__(self, env, sinks: list[Transformation], job_name: str, *, job_id: str | None = None,
-                 restore_from=None, attempt: int = 0):
+                 restore_from=None, attempt: int = 0, comm=None):
         self.env = env
         self.job_name = job_name
         self.job_id = job_id
@@ -129,16 +129,29 @@ class Executor:
         self.comm = None
         self._wm_in: dict = {}  # keyed node -> latest watermark received from every rank
         self._failure: Exception | None = None  # multi-rank: first operator failure of this rank
-        if getattr(env, "world", 1) > 1:
+        self.dev_comm = None  # device collectives of the native operators (G > 1)
+        if comm is not None and comm.world > 1:
+            # Injected communicator (LoopbackComm: G virtual ranks in one process, tests).
+            self.comm = self.dev_comm = comm
+        elif getattr(env, "world", 1) > 1:
             import os
 
             import torch
 
-            from ..parallel.comm import init_distributed
+            from ..parallel.comm import TorchComm, init_distributed
 
-            if str(env.config.device).startswith("cuda") and torch.cuda.is_available():
+            cuda = str(env.config.device).startswith("cuda") and torch.cuda.is_available()
+            if cuda:
                 torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))  # one GPU per rank
             self.comm = init_distributed("cpu")
+            if cuda:
+                # Device tensors of the native operators travel over RCCL (xGMI); host objects
+                # (records, control) over the gloo group.
+                import torch.distributed as dist
+
+                self.dev_comm = TorchComm(dist.new_group(backend="nccl"))
+            else:
+                self.dev_comm = self.comm
 
     @staticmethod
     def _topo(sinks):
@@ -164,6 +177,8 @@ class Executor:
             p = n.parallelism or env.parallelism
             if n.kind == "source":
                 src: Source = n.factory()
+                if self.comm is not None and hasattr(type(src), "comm"):
+                    src.comm = self.comm  # K18: the source spreads its batches over the ranks
                 src.open(env.rank, env.world, self.clock)
                 self.ops[n.id] = src
             elif n.kind == "union":
@@ -176,7 +191,8 @@ class Executor:
                 self.ops[n.id] = op
             else:
                 op = n.factory()
-                op.open(OpContext(n.name, p, env.max_parallelism, self.clock, tc))
+                op.open(OpContext(n.name, p, env.max_parallelism, self.clock, tc,
+                                  comm=self.dev_comm, ctrl=self.comm))
                 self.ops[n.id] = op
 
     def _push(self, inbox: dict[int, list], now: int | None) -> None:
@@ -232,11 +248,14 @@ class Executor:
             items = expand_columns(items)
         if self.fault is not None and items:
             self._maybe_fault(n, items)
-        if items and self._trace:
+        # Collective operators (multi-rank device exchange) run every pass, with or without
+        # input: each call is one step of their collectives on every rank.
+        run = bool(items) or getattr(op, "collective", False)
+        if run and self._trace:
             with trace.span(n.name, "operator"):
                 out = op.process(items)
         else:
-            out = op.process(items) if items else []
+            out = op.process(items) if run else []
         if now is not None:
             out.extend(op.on_processing_time(now))
         return out
@@ -279,6 +298,12 @@ class Executor:
         keyed = n.key_fn_in is not None
         if not keyed and p != 1:
             return items
+        if keyed and getattr(self.ops.get(n.id), "device_exchange", False):
+            # The operator exchanges its keys itself (RCCL all-to-all inside the native keyed
+            # operator): its data stays on this rank; only the watermarks are merged here.
+            data = [it for it in items if not isinstance(it, WM)]
+            wms = [it.ts for it in items if isinstance(it, WM)]
+            return data + self._merge_watermarks(n, wms[-1] if wms else None)
         mp = self.env.max_parallelism
         outs: list[list] = [[] for _ in range(world)]
         last_wm = None
@@ -302,9 +327,17 @@ class Executor:
         recv: list = []
         for r_outs, _ in got:
             recv.extend(r_outs[rank])
-        # Watermarks: the minimum over the ranks of the latest watermark each one has sent.
+        return recv + self._merge_watermarks(n, last_wm, [w for _, w in got])
+
+    def _merge_watermarks(self, n: Transformation, last_wm, got_wms=None) -> list:
+        """Watermarks across a keyed edge: the minimum over the ranks of the latest watermark
+        each one has sent (Flink's StatusWatermarkValve over the input channels). Collective when
+        `got_wms` is not given."""
+        world = self.comm.world
+        if got_wms is None:
+            got_wms = self.comm.all_gather_object(last_wm)
         seen = self._wm_in.setdefault(n.id, [None] * world)
-        for r, (_, w) in enumerate(got):
+        for r, w in enumerate(got_wms):
             if w is not None:
                 seen[r] = w if seen[r] is None else max(seen[r], w)
         if all(w is not None for w in seen):
@@ -312,8 +345,8 @@ class Executor:
             prev = self._wm_in.get((n.id, "emitted"))
             if prev is None or wm > prev:
                 self._wm_in[(n.id, "emitted")] = wm
-                recv.append(WM(wm))
-        return recv
+                return [WM(wm)]
+        return []
 
     def _all_done(self, finished: dict) -> bool:
         done = all(finished.values())
@@ -586,7 +619,7 @@ class Executor:
 
                     items = expand_columns(items)
                 try:
-                    out = op.process(items) if items else []
+                    out = op.process(items) if (items or getattr(op, "collective", False)) else []
                     out.extend(op.finish())
                 except Exception as e:  # noqa: BLE001 -- multi-rank: re-raised by _control
                     if self.comm is None:

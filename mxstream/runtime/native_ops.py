@@ -159,12 +159,84 @@ class NativeWindowOp(_ColumnInput, Operator):
         self.templates: dict = {}             # key id -> first record (keep-first fields)
         self.num_late_records_dropped = 0
 
+    device_input = None  # planner: (column kinds, shared ingest state) for device-ingest input
+
     def open(self, ctx):
         super().open(ctx)
         from ..ops.native import load
 
         self.dict = load().StringDict()
         self.str_keys = None
+        self.device_exchange = self.collective = False
+        comm = getattr(ctx, "comm", None)
+        if (comm is not None and comm.world > 1 and self.device_input is not None
+                and type(self) is NativeWindowOp and self.assigner.is_event_time()):
+            # Multi-rank with device-ingest input: the operator exchanges keys itself (local-
+            # global partials over RCCL, key groups from the shared dictionary's Java hashes)
+            # and runs one collective step per pass -- built now, identically on every rank.
+            kinds, shared = self.device_input
+            vk = kinds[self.val_pos]
+            if vk == FK_STR or (self.ok_arities and len(kinds) not in self.ok_arities):
+                return
+            self.dict = shared["dict"]
+            self.str_keys = kinds[self.key_pos] == FK_STR
+            if kinds[self.key_pos] == FK_DOUBLE:
+                return
+            self.comm = comm
+            self.device_exchange = self.collective = True
+            self._lazy_tpl, self._lazy_arity = {}, len(kinds)
+            self._build(1.0 if vk == FK_DOUBLE else 1, dense=self.str_keys)
+
+    def _jhash(self):
+        """Java hashes of the dictionary ids (key groups of string keys at G > 1)."""
+        jh = getattr(self.dict, "id_jh", None)
+        return jh if jh is not None else torch.zeros(1, dtype=torch.int32,
+                                                     device=torch.device(self.device))
+
+    def _ensure_capacity(self) -> None:
+        """Dense state covers dictionary ids < max_keys: a growing dictionary regrows the state
+        (snapshot -> larger operator -> restore). At G > 1 every rank sees the same dictionary
+        size, so every rank regrows in the same pass (the restore is collective)."""
+        if not (self.str_keys and self.op is not None and getattr(self.op, "dense_bits", 0)):
+            return
+        need = len(self.dict)
+        if need <= (1 << self.op.dense_bits):
+            return
+        es = self.op.snapshot_state()
+        self.max_keys = 1 << max(need - 1, 1).bit_length()
+        self._build(1.0 if self.is_float else 1, dense=True)
+        self.op.restore_state(es.columns, es.meta)
+
+    def _process_exchange(self, items) -> list:
+        """G > 1 device exchange: one engine step per pass (an empty batch if this rank got no
+        rows), then the merged watermark (identical on every rank) advances every rank."""
+        data = [it for it in items if not isinstance(it, WM)]
+        wms = [it.ts for it in items if isinstance(it, WM)]
+        dev = self.op.device
+        if any(not isinstance(b, DeviceColumnBatch) for b in data):
+            raise TypeError("multi-rank native window: device-ingest batches expected")
+        self._ensure_capacity()
+        self.op.jhash = self._jhash()
+        if data:
+            cb = concat_device(data)
+            n = cb.n
+            kid = cb.cols[self.key_pos][:n]
+            ts = cb.ts[:n] if cb.ts is not None else torch.full((n,), LONG_MIN, dtype=torch.int64,
+                                                                 device=dev)
+            vals = cb.cols[self.val_pos][:n]
+            vals = vals.view(torch.int64) if vals.dtype == torch.float64 else vals.to(torch.int64)
+        else:
+            kid = torch.empty(0, dtype=torch.int32 if self.str_keys else torch.int64, device=dev)
+            ts = torch.empty(0, dtype=torch.int64, device=dev)
+            vals = torch.empty(0, dtype=torch.int64, device=dev)
+        late_before = self.op.metrics.num_late_records_dropped
+        out = self._emit(self.op.process(kid.contiguous(), ts.contiguous(), vals.contiguous()))
+        self.num_late_records_dropped += self.op.metrics.num_late_records_dropped - late_before
+        for w in wms:
+            self.wm = w
+            out.extend(self._emit(self.op.advance_watermark(w)))
+            out.append(WM(w))
+        return out
 
     # -- lazy construction on the first records (value type decides the aggregate kind) --
     def _build(self, sample_val, dense: bool = False) -> bool:
@@ -181,9 +253,16 @@ class NativeWindowOp(_ColumnInput, Operator):
         event = a.is_event_time()
         dev = torch.device(self.device)
         cap_log2 = 12 if self.max_keys > 100_000 else 9
+        comm = getattr(self, "comm", None)
+        multi = comm is not None and comm.world > 1
         self.op = KeyedWindowOperator(
             size=a.size, slide=a.slide, offset=a.offset, lateness=self.lateness if event else 0,
-            agg=agg, device=dev, max_keys=self.max_keys, parallelism=1,
+            agg=agg, device=dev, max_keys=self.max_keys,
+            parallelism=self.ctx.parallelism if multi else 1, comm=comm if multi else None,
+            max_parallelism=self.ctx.max_parallelism if multi else 128,
+            hash_mode=1 if (multi and dense) else 0,
+            jhash_table=self._jhash() if (multi and dense) else None,
+            exchange="partials" if multi else "auto",
             batch_capacity=max(1024, self.ctx.parallelism), cap_log2=cap_log2,
             time_mode="event" if event else "processing", external_watermark=True,
             side_output_late=self.late_tag is not None, clock=self.ctx.clock,
@@ -231,6 +310,7 @@ class NativeWindowOp(_ColumnInput, Operator):
             return self.fallback.process(recs)
         if getattr(self, "_lazy_tpl", None) is None:
             self._lazy_tpl, self._lazy_arity = {}, len(cb.kinds)
+        self._ensure_capacity()
         dev = self.op.device
         n = cb.n
         if self.assigner.is_event_time():
@@ -281,6 +361,7 @@ class NativeWindowOp(_ColumnInput, Operator):
             self._to_fallback()
             return self.fallback.process(recs)
         self._cb_templates(cb, kid)
+        self._ensure_capacity()
         event = self.assigner.is_event_time()
         if event:
             tsa = cb.ts if cb.ts is not None else np.full(cb.n, LONG_MIN, dtype=np.int64)
@@ -386,6 +467,8 @@ class NativeWindowOp(_ColumnInput, Operator):
         return out
 
     def process(self, items):
+        if self.device_exchange:
+            return self._process_exchange(items)
         if self.fallback is not None:
             return self.fallback.process(expand_columns(items))
         out = []

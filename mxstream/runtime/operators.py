@@ -46,12 +46,16 @@ class OpContext:
     """What the executor hands every operator at open()."""
 
     def __init__(self, name: str, parallelism: int, max_parallelism: int, clock: Callable[[], int],
-                 time_characteristic: str):
+                 time_characteristic: str, comm=None, ctrl=None):
         self.name = name
         self.parallelism = parallelism
         self.max_parallelism = max_parallelism
         self.clock = clock
         self.time_characteristic = time_characteristic
+        # Multi-rank jobs: `comm` carries device tensors (RCCL for GPU operators, gloo/loopback
+        # otherwise), `ctrl` host objects; both None on one rank.
+        self.comm = comm
+        self.ctrl = ctrl
 
 
 class Operator:

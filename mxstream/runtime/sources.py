@@ -339,6 +339,10 @@ class SocketTextSource(Source):
         self.max_lines = max_lines
         self.reader = None
 
+    # Set by the executor on multi-rank jobs (host-object collectives): a columnar socket source
+    # then spreads rank 0's text batches over every rank (K18, Main.java:17 -> 18 rebalance).
+    comm = None
+
     def open(self, rank, world, clock):
         super().open(rank, world, clock)
         if rank != 0:
@@ -348,7 +352,38 @@ class SocketTextSource(Source):
         self.reader = load().SocketSource(self.host, self.port, self.delim, self.max_retry)
         self.reader.start()
 
+    def _poll_spread(self):
+        """Multi-rank columnar: rank 0 reads, cuts the batch into newline-aligned chunks of
+        about equal size, one per rank, and every rank takes its chunk (a collective on every
+        pass, so all ranks also learn end-of-stream on the same pass)."""
+        from .columnar import TextBatch
+
+        world, rank = self.comm.world, self.comm.rank
+        msg = None
+        if rank == 0:
+            data, n, eof, err = self.reader.poll(self.max_lines, self.poll_timeout_ms)
+            chunks = [b""] * world
+            if n:
+                data = bytes(data)
+                cuts = [0]
+                for r in range(1, world):
+                    c = max(cuts[-1], len(data) * r // world)
+                    j = data.find(b"\n", c - 1) if c > 0 else -1
+                    cuts.append(len(data) if j < 0 else j + 1)
+                cuts.append(len(data))
+                chunks = [data[cuts[r]:cuts[r + 1]] for r in range(world)]
+            msg = (chunks, bool(eof), err)
+        chunks, eof, err = self.comm.broadcast_object(msg, src=0)
+        if err:
+            raise ConnectionError(err)
+        mine = chunks[rank]
+        if not mine:
+            return [], eof
+        return [TextBatch(mine, mine.count(b"\n") + (0 if mine.endswith(b"\n") else 1))], eof
+
     def poll(self, now):
+        if self.columnar and self.comm is not None and self.comm.world > 1:
+            return self._poll_spread()
         if self.reader is None:
             return [], True
         data, n, eof, err = self.reader.poll(self.max_lines, self.poll_timeout_ms)
