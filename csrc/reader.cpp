@@ -1,225 +1,35 @@
-// mxstream — text file reader into pinned host slots (SURVEY.md F-src / K18: host reader ->
-// pinned ring -> async H2D -> device parse).
-//
-// A background thread cuts the byte range [lo, hi) of a file into newline-aligned chunks of at
-// most `chunk` bytes and reads each one with `threads` parallel pread()s straight into one of the
-// caller's slots (page-locked buffers, so the H2D copy is one DMA). It also counts the chunk's
-// lines, so the consumer never scans the text on the host. Slots cycle: the consumer takes a
-// filled slot with next(), uploads it, and release()s it once its copy has completed; the
-// reader stays up to (slots - 1) chunks ahead (bounded memory, back-pressure on a slow
-// consumer).
-#include <fcntl.h>
+// mxstream — Python binding of the pinned-slot text file reader (csrc/text_ring.h).
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
-#include <sys/stat.h>
-#include <unistd.h>
-
-#include <algorithm>
-#include <atomic>
-#include <cerrno>
-#include <chrono>
-#include <condition_variable>
-#include <cstring>
-#include <deque>
-#include <mutex>
-#include <stdexcept>
-#include <string>
-#include <thread>
-#include <vector>
 
 #include "mxs_runtime.h"
+#include "text_ring.h"
 
 namespace py = pybind11;
 
-namespace mxs {
-namespace {
-
-struct Ready {
-  int slot;
-  int64_t nbytes;
-  int64_t nlines;
-  int64_t end_off;  // file offset just past the chunk (relative to lo)
-};
-
-class TextFileRing {
- public:
-  TextFileRing(const std::string& path, int64_t lo, int64_t hi,
-               std::vector<std::pair<intptr_t, int64_t>> slots, int64_t chunk, int threads)
-      : lo_(lo), hi_(hi), chunk_(chunk), threads_(std::max(1, std::min(threads, 64))) {
-    fd_ = ::open(path.c_str(), O_RDONLY);
-    if (fd_ < 0) throw std::runtime_error("cannot open " + path + ": " + std::strerror(errno));
-    if (slots.size() < 2) throw std::invalid_argument("TextFileRing needs at least 2 slots");
-    if (lo < 0 || hi < lo) throw std::invalid_argument("bad byte range");
-    for (auto& s : slots) {
-      if (s.second < chunk) throw std::invalid_argument("slot smaller than the chunk size");
-      slots_.push_back({reinterpret_cast<char*>(s.first), s.second});
-      free_.push_back((int)slots_.size() - 1);
-    }
-  }
-  ~TextFileRing() { close(); }
-
-  void start() {
-    if (!th_.joinable()) th_ = std::thread([this] { run(); });
-  }
-
-  // (slot, nbytes, nlines, end_offset, eof): slot -1 when nothing is ready within timeout_ms;
-  // eof when every chunk has been handed out.
-  py::tuple next(int timeout_ms) {
-    Ready r{-1, 0, 0, 0};
-    bool eof = false;
-    std::string err;
-    {
-      py::gil_scoped_release nogil;
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms),
-                   [&] { return !ready_.empty() || done_; });
-      if (!ready_.empty()) {
-        r = ready_.front();
-        ready_.pop_front();
-      }
-      eof = done_ && ready_.empty() && r.slot < 0;
-      err = err_;
-    }
-    if (!err.empty()) throw std::runtime_error(err);
-    return py::make_tuple(r.slot, r.nbytes, r.nlines, r.end_off, eof);
-  }
-
-  void release(int slot) {
-    std::lock_guard<std::mutex> g(mu_);
-    if (slot < 0 || slot >= (int)slots_.size()) throw std::invalid_argument("bad slot");
-    free_.push_back(slot);
-    cv_.notify_all();
-  }
-
-  void close() {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
-      cv_.notify_all();
-    }
-    if (th_.joinable()) th_.join();
-    if (fd_ >= 0) {
-      ::close(fd_);
-      fd_ = -1;
-    }
-  }
-
- private:
-  struct Slot {
-    char* p;
-    int64_t cap;
-  };
-
-  bool read_range(char* dst, int64_t off, int64_t len) {
-    // `threads_` contiguous pieces read in parallel (page cache -> pinned memory copies).
-    const int T = (int)std::min<int64_t>(threads_, std::max<int64_t>(1, len >> 20));
-    std::atomic<bool> ok{true};
-    auto piece = [&](int t) {
-      const int64_t a = len * t / T, b = len * (t + 1) / T;
-      int64_t pos = a;
-      while (pos < b) {
-        const ssize_t r = ::pread(fd_, dst + pos, (size_t)(b - pos), (off_t)(off + pos));
-        if (r <= 0) {
-          if (r < 0 && errno == EINTR) continue;
-          ok = false;
-          return;
-        }
-        pos += r;
-      }
-    };
-    if (T == 1) {
-      piece(0);
-    } else {
-      std::vector<std::thread> th;
-      for (int t = 0; t < T; ++t) th.emplace_back(piece, t);
-      for (auto& x : th) x.join();
-    }
-    return ok;
-  }
-
-  int64_t count_lines(const char* p, int64_t n) {
-    const int T = (int)std::min<int64_t>(threads_, std::max<int64_t>(1, n >> 22));
-    std::vector<int64_t> c(T, 0);
-    auto piece = [&](int t) {
-      const int64_t a = n * t / T, b = n * (t + 1) / T;
-      c[t] = std::count(p + a, p + b, '\n');
-    };
-    if (T == 1) {
-      piece(0);
-    } else {
-      std::vector<std::thread> th;
-      for (int t = 0; t < T; ++t) th.emplace_back(piece, t);
-      for (auto& x : th) x.join();
-    }
-    int64_t k = 0;
-    for (int64_t x : c) k += x;
-    return k + (n > 0 && p[n - 1] != '\n' ? 1 : 0);
-  }
-
-  void run() {
-    int64_t off = lo_;
-    std::string err;
-    while (off < hi_) {
-      int slot;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || !free_.empty(); });
-        if (stop_) return;
-        slot = free_.front();
-        free_.pop_front();
-      }
-      char* dst = slots_[slot].p;
-      const int64_t want = std::min(chunk_, hi_ - off);
-      if (!read_range(dst, off, want)) {
-        err = "read failed at offset " + std::to_string(off);
-        break;
-      }
-      int64_t used = want;
-      if (off + want < hi_) {
-        const char* nl = static_cast<const char*>(memrchr(dst, '\n', (size_t)want));
-        if (!nl) {
-          err = "a line is longer than the ingest chunk (" + std::to_string(chunk_) + " bytes)";
-          break;
-        }
-        used = nl - dst + 1;
-      }
-      const int64_t nl = count_lines(dst, used);
-      off += used;
-      std::lock_guard<std::mutex> g(mu_);
-      ready_.push_back({slot, used, nl, off - lo_});
-      cv_.notify_all();
-    }
-    std::lock_guard<std::mutex> g(mu_);
-    err_ = err;
-    done_ = true;
-    cv_.notify_all();
-  }
-
-  int fd_ = -1;
-  int64_t lo_, hi_, chunk_;
-  int threads_;
-  std::vector<Slot> slots_;
-  std::deque<int> free_;
-  std::deque<Ready> ready_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  bool done_ = false, stop_ = false;
-  std::string err_;
-  std::thread th_;
-};
-
-}  // namespace
-}  // namespace mxs
-
 void bind_reader(py::module_& m) {
-  using mxs::TextFileRing;
-  py::class_<TextFileRing>(m, "TextFileRing")
+  using mxs::Ready;
+  using mxs::TextRingCore;
+  py::class_<TextRingCore>(m, "TextFileRing")
       .def(py::init<const std::string&, int64_t, int64_t, std::vector<std::pair<intptr_t, int64_t>>,
                     int64_t, int>(),
            py::arg("path"), py::arg("lo"), py::arg("hi"), py::arg("slots"), py::arg("chunk"),
            py::arg("threads") = 8)
-      .def("start", &TextFileRing::start)
-      .def("next", &TextFileRing::next, py::arg("timeout_ms") = 1000)
-      .def("release", &TextFileRing::release)
-      .def("close", &TextFileRing::close);
+      .def("start", &TextRingCore::start)
+      // (slot, nbytes, nlines, end_offset, eof): slot -1 when nothing is ready within timeout_ms;
+      // eof when every chunk has been handed out.
+      .def("next", [](TextRingCore& r, int timeout_ms) {
+        Ready x{-1, 0, 0, 0};
+        bool eof = false;
+        {
+          py::gil_scoped_release nogil;
+          if (!r.next(timeout_ms, &x, &eof)) x.slot = -1;
+        }
+        return py::make_tuple(x.slot, x.nbytes, x.nlines, x.end_off, eof);
+      }, py::arg("timeout_ms") = 1000)
+      .def("release", &TextRingCore::release)
+      .def("close", [](TextRingCore& r) {
+        py::gil_scoped_release nogil;
+        r.close();
+      });
 }

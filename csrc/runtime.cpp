@@ -39,48 +39,15 @@
 #include <vector>
 
 #include "mxs_common.h"
+#include "mxs_log.h"
 #include "mxs_runtime.h"
+#include "kg_file.h"
+#include "socket_reader.h"
 
 namespace py = pybind11;
 
 namespace mxs {
 namespace {
-
-// ------------------------------------------------------------------------------------------
-// Minimal leveled logger for the native runtime (threads without the GIL): level from
-// MXS_LOG_LEVEL (DEBUG/INFO/WARN/ERROR, default WARN), log4j-like layout on stderr.
-// ------------------------------------------------------------------------------------------
-enum LogLevel { kDebug = 0, kInfo = 1, kWarn = 2, kError = 3 };
-
-int log_threshold() {
-  static const int lvl = [] {
-    const char* e = std::getenv("MXS_LOG_LEVEL");
-    if (!e) return (int)kWarn;
-    const std::string v(e);
-    if (v == "DEBUG" || v == "debug" || v == "TRACE") return (int)kDebug;
-    if (v == "INFO" || v == "info") return (int)kInfo;
-    if (v == "ERROR" || v == "error") return (int)kError;
-    return (int)kWarn;
-  }();
-  return lvl;
-}
-
-void mxs_log(LogLevel level, const std::string& logger, const std::string& msg) {
-  if ((int)level < log_threshold()) return;
-  static std::mutex mu;
-  static const char* names[] = {"DEBUG", "INFO", "WARN", "ERROR"};
-  const auto now = std::chrono::system_clock::now();
-  const std::time_t tt = std::chrono::system_clock::to_time_t(now);
-  const int ms = (int)(std::chrono::duration_cast<std::chrono::milliseconds>(
-                           now.time_since_epoch()).count() % 1000);
-  std::tm tm{};
-  localtime_r(&tt, &tm);
-  char ts[32];
-  std::strftime(ts, sizeof(ts), "%Y-%m-%d %H:%M:%S", &tm);
-  std::lock_guard<std::mutex> g(mu);
-  std::fprintf(stderr, "%s,%03d %-5s mxstream.native.%-25s - %s\n", ts, ms, names[level],
-               logger.c_str(), msg.c_str());
-}
 
 // ------------------------------------------------------------------------------------------
 // Java String.hashCode over the UTF-16 encoding of UTF-8 input (invalid bytes -> U+FFFD).
@@ -467,140 +434,6 @@ py::tuple parse_lines(py::bytes data, std::vector<std::pair<int, int>> spec, std
 }
 
 // ------------------------------------------------------------------------------------------
-// Socket source (SocketTextStreamFunction semantics, maxRetry = 0 by default)
-// ------------------------------------------------------------------------------------------
-class SocketSource {
- public:
-  SocketSource(std::string host, int port, std::string delimiter, int max_retry, int64_t retry_ms)
-      : host_(std::move(host)), port_(port), delim_(std::move(delimiter)), max_retry_(max_retry),
-        retry_ms_(retry_ms) {
-    if (delim_.empty()) throw std::invalid_argument("empty delimiter");
-  }
-  ~SocketSource() { close(); }
-
-  void start() {
-    if (th_.joinable()) return;
-    th_ = std::thread([this] { run(); });
-  }
-
-  // Returns (joined_lines_bytes, nlines, eof, error).
-  py::tuple poll(size_t max_lines, int timeout_ms) {
-    std::string joined;
-    size_t n = 0;
-    bool eof;
-    std::string err;
-    {
-      py::gil_scoped_release nogil;
-      std::unique_lock<std::mutex> lk(mu_);
-      cv_.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return !q_.empty() || eof_; });
-      while (!q_.empty() && n < max_lines) {
-        joined += q_.front();
-        joined.push_back('\n');
-        q_.pop_front();
-        ++n;
-      }
-      eof = eof_ && q_.empty();
-      err = err_;
-    }
-    return py::make_tuple(py::bytes(joined), (int64_t)n, eof, err);
-  }
-
-  void close() {
-    stop_ = true;
-    const int fd = fd_.exchange(-1);
-    if (fd >= 0) {
-      ::shutdown(fd, SHUT_RDWR);
-      ::close(fd);
-    }
-    if (th_.joinable()) th_.join();
-  }
-
- private:
-  void push(std::string line) {
-    std::lock_guard<std::mutex> g(mu_);
-    q_.push_back(std::move(line));
-    cv_.notify_one();
-  }
-  void finish(const std::string& err) {
-    std::lock_guard<std::mutex> g(mu_);
-    eof_ = true;
-    err_ = err;
-    cv_.notify_all();
-  }
-  int connect_once() {
-    addrinfo hints{}, *res = nullptr;
-    hints.ai_family = AF_UNSPEC;
-    hints.ai_socktype = SOCK_STREAM;
-    if (getaddrinfo(host_.c_str(), std::to_string(port_).c_str(), &hints, &res) != 0) return -1;
-    int fd = -1;
-    for (addrinfo* p = res; p; p = p->ai_next) {
-      fd = ::socket(p->ai_family, p->ai_socktype, p->ai_protocol);
-      if (fd < 0) continue;
-      if (::connect(fd, p->ai_addr, p->ai_addrlen) == 0) break;
-      ::close(fd);
-      fd = -1;
-    }
-    freeaddrinfo(res);
-    return fd;
-  }
-  void run() {
-    int attempt = 0;
-    std::string buffer;
-    while (!stop_) {
-      const int fd = connect_once();
-      if (fd < 0) {
-        if (max_retry_ >= 0 && attempt >= max_retry_) {
-          mxs_log(kError, "socket", "could not connect to " + host_ + ":" + std::to_string(port_));
-          finish("ConnectException: could not connect to " + host_ + ":" + std::to_string(port_));
-          return;
-        }
-        ++attempt;
-        mxs_log(kWarn, "socket", "connect to " + host_ + ":" + std::to_string(port_) +
-                                     " failed, retry " + std::to_string(attempt));
-        std::this_thread::sleep_for(std::chrono::milliseconds(retry_ms_));
-        continue;
-      }
-      fd_ = fd;
-      mxs_log(kInfo, "socket", "connected to " + host_ + ":" + std::to_string(port_));
-      char chunk[8192];
-      while (!stop_) {
-        const ssize_t r = ::recv(fd, chunk, sizeof(chunk), 0);
-        if (r <= 0) break;
-        buffer.append(chunk, (size_t)r);
-        size_t pos;
-        while ((pos = buffer.find(delim_)) != std::string::npos) {
-          std::string line = buffer.substr(0, pos);
-          if (delim_ == "\n" && !line.empty() && line.back() == '\r') line.pop_back();
-          push(std::move(line));
-          buffer.erase(0, pos + delim_.size());
-        }
-      }
-      const int cur = fd_.exchange(-1);
-      if (cur >= 0) ::close(cur);
-      ++attempt;
-      if (stop_ || max_retry_ == 0 || (max_retry_ > 0 && attempt > max_retry_)) break;
-      std::this_thread::sleep_for(std::chrono::milliseconds(retry_ms_));
-    }
-    if (!buffer.empty()) push(buffer);
-    finish("");
-  }
-
-  std::string host_;
-  int port_;
-  std::string delim_;
-  int max_retry_;
-  int64_t retry_ms_;
-  std::thread th_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::deque<std::string> q_;
-  bool eof_ = false;
-  std::string err_;
-  std::atomic<bool> stop_{false};
-  std::atomic<int> fd_{-1};
-};
-
-// ------------------------------------------------------------------------------------------
 // Key-group indexed state files.
 // Layout: "MXSKG001" | u64 header_len | header (UTF-8 JSON from Python) | u32 kg_lo | u32 kg_hi |
 //         u64 offsets[kg_hi - kg_lo + 2] (row offsets) | columns (each nrows * itemsize, kg-sorted)
@@ -621,39 +454,7 @@ void write_kg_file(const std::string& path, const std::string& header, uint32_t 
     cols.emplace_back((const char*)keep.back().data(), (size_t)keep.back().itemsize());
   }
   py::gil_scoped_release nogil;
-  const uint32_t ngroups = kg_hi - kg_lo + 1;
-  std::vector<uint64_t> off(ngroups + 1, 0);
-  for (size_t i = 0; i < n; ++i) {
-    const int32_t g = kgp[i];
-    if (g < (int32_t)kg_lo || g > (int32_t)kg_hi) throw std::invalid_argument("row key group outside file range");
-    off[g - kg_lo + 1]++;
-  }
-  for (uint32_t g = 0; g < ngroups; ++g) off[g + 1] += off[g];
-  std::vector<uint64_t> perm(n);
-  {
-    std::vector<uint64_t> cur(off.begin(), off.end() - 1);
-    for (size_t i = 0; i < n; ++i) perm[cur[kgp[i] - kg_lo]++] = i;  // stable counting sort
-  }
-  const std::string tmp = path + ".inprogress";
-  std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
-  if (!f) throw std::runtime_error("cannot open " + tmp);
-  f.write("MXSKG001", 8);
-  const uint64_t hl = header.size();
-  f.write((const char*)&hl, 8);
-  f.write(header.data(), (std::streamsize)hl);
-  f.write((const char*)&kg_lo, 4);
-  f.write((const char*)&kg_hi, 4);
-  f.write((const char*)off.data(), (std::streamsize)(off.size() * 8));
-  std::vector<char> tmpbuf;
-  for (const auto& [src, isz] : cols) {
-    tmpbuf.resize(n * isz);
-    for (size_t i = 0; i < n; ++i) std::memcpy(&tmpbuf[i * isz], src + perm[i] * isz, isz);
-    f.write(tmpbuf.data(), (std::streamsize)tmpbuf.size());
-  }
-  f.flush();
-  if (!f) throw std::runtime_error("write failed: " + tmp);
-  f.close();
-  if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("rename failed: " + path);
+  write_kg_columns(path, header, kg_lo, kg_hi, kgp, n, cols);
 }
 
 // Returns (header, kg_lo, kg_hi, offsets(np.uint64), raw column bytes for rows in [lo, hi]).
@@ -727,12 +528,25 @@ void bind_runtime(py::module_& m) {
   m.def("parse_lines", &parse_lines, py::arg("data"), py::arg("spec"), py::arg("sep"),
         py::arg("dict"), py::arg("offset_s") = 0, py::arg("threads") = 1);
 
-  py::class_<SocketSource>(m, "SocketSource")
+  py::class_<SocketReaderCore>(m, "SocketSource")
       .def(py::init<std::string, int, std::string, int, int64_t>(), py::arg("host"), py::arg("port"),
            py::arg("delimiter") = "\n", py::arg("max_retry") = 0, py::arg("retry_ms") = 500)
-      .def("start", &SocketSource::start)
-      .def("poll", &SocketSource::poll, py::arg("max_lines") = 1 << 20, py::arg("timeout_ms") = 100)
-      .def("close", &SocketSource::close);
+      .def("start", &SocketReaderCore::start)
+      // Returns (joined_lines_bytes, nlines, eof, error).
+      .def("poll", [](SocketReaderCore& s, size_t max_lines, int timeout_ms) {
+        std::string joined, err;
+        size_t n = 0;
+        bool eof = false;
+        {
+          py::gil_scoped_release nogil;
+          s.poll(max_lines, timeout_ms, &joined, &n, &eof, &err);
+        }
+        return py::make_tuple(py::bytes(joined), (int64_t)n, eof, err);
+      }, py::arg("max_lines") = 1 << 20, py::arg("timeout_ms") = 100)
+      .def("close", [](SocketReaderCore& s) {
+        py::gil_scoped_release nogil;
+        s.close();
+      });
 
   m.def("write_kg_file", &write_kg_file);
   m.def("read_kg_file", &read_kg_file);

@@ -1,0 +1,210 @@
+// mxstream — text file reader into pinned host slots (SURVEY.md F-src / K18: host reader ->
+// pinned ring -> async H2D -> device parse). Core without Python (csrc/reader.cpp binds it; the
+// ThreadSanitizer harness csrc/tests/tsan_main.cpp drives it from several threads).
+//
+// A background thread cuts the byte range [lo, hi) of a file into newline-aligned chunks of at
+// most `chunk` bytes and reads each one with `threads` parallel pread()s straight into one of the
+// caller's slots (page-locked buffers, so the H2D copy is one DMA). It also counts the chunk's
+// lines, so the consumer never scans the text on the host. Slots cycle: the consumer takes a
+// filled slot with next(), uploads it, and release()s it once its copy has completed; the
+// reader stays up to (slots - 1) chunks ahead (bounded memory, back-pressure on a slow
+// consumer).
+#pragma once
+#include <fcntl.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <utility>
+#include <vector>
+
+namespace mxs {
+
+struct Ready {
+  int slot;
+  int64_t nbytes;
+  int64_t nlines;
+  int64_t end_off;  // file offset just past the chunk (relative to lo)
+};
+
+class TextRingCore {
+ public:
+  TextRingCore(const std::string& path, int64_t lo, int64_t hi,
+               std::vector<std::pair<intptr_t, int64_t>> slots, int64_t chunk, int threads)
+      : lo_(lo), hi_(hi), chunk_(chunk), threads_(std::max(1, std::min(threads, 64))) {
+    fd_ = ::open(path.c_str(), O_RDONLY);
+    if (fd_ < 0) throw std::runtime_error("cannot open " + path + ": " + std::strerror(errno));
+    if (slots.size() < 2) throw std::invalid_argument("TextFileRing needs at least 2 slots");
+    if (lo < 0 || hi < lo) throw std::invalid_argument("bad byte range");
+    for (auto& s : slots) {
+      if (s.second < chunk) throw std::invalid_argument("slot smaller than the chunk size");
+      slots_.push_back({reinterpret_cast<char*>(s.first), s.second});
+      free_.push_back((int)slots_.size() - 1);
+    }
+  }
+  ~TextRingCore() { close(); }
+
+  void start() {
+    if (!th_.joinable()) th_ = std::thread([this] { run(); });
+  }
+
+  // Waits up to timeout_ms for a filled slot. Returns false when none is ready (then *eof tells
+  // whether every chunk has been handed out); throws the reader's error.
+  bool next(int timeout_ms, Ready* r, bool* eof) {
+    std::string err;
+    bool got = false;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      // system_clock deadline: pthread_cond_timedwait, which ThreadSanitizer intercepts
+    // (steady_clock waits use pthread_cond_clockwait, invisible to GCC 11's TSan).
+    cv_.wait_until(lk, std::chrono::system_clock::now() + std::chrono::milliseconds(timeout_ms),
+                   [&] { return !ready_.empty() || done_; });
+      if (!ready_.empty()) {
+        *r = ready_.front();
+        ready_.pop_front();
+        got = true;
+      }
+      *eof = done_ && ready_.empty() && !got;
+      err = err_;
+    }
+    if (!err.empty()) throw std::runtime_error(err);
+    return got;
+  }
+
+  void release(int slot) {
+    std::lock_guard<std::mutex> g(mu_);
+    if (slot < 0 || slot >= (int)slots_.size()) throw std::invalid_argument("bad slot");
+    free_.push_back(slot);
+    cv_.notify_all();
+  }
+
+  void close() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+      cv_.notify_all();
+    }
+    if (th_.joinable()) th_.join();
+    if (fd_ >= 0) {
+      ::close(fd_);
+      fd_ = -1;
+    }
+  }
+
+ private:
+  struct Slot {
+    char* p;
+    int64_t cap;
+  };
+
+  bool read_range(char* dst, int64_t off, int64_t len) {
+    // `threads_` contiguous pieces read in parallel (page cache -> pinned memory copies).
+    const int T = (int)std::min<int64_t>(threads_, std::max<int64_t>(1, len >> 20));
+    std::atomic<bool> ok{true};
+    auto piece = [&](int t) {
+      const int64_t a = len * t / T, b = len * (t + 1) / T;
+      int64_t pos = a;
+      while (pos < b) {
+        const ssize_t r = ::pread(fd_, dst + pos, (size_t)(b - pos), (off_t)(off + pos));
+        if (r <= 0) {
+          if (r < 0 && errno == EINTR) continue;
+          ok = false;
+          return;
+        }
+        pos += r;
+      }
+    };
+    if (T == 1) {
+      piece(0);
+    } else {
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; ++t) th.emplace_back(piece, t);
+      for (auto& x : th) x.join();
+    }
+    return ok;
+  }
+
+  int64_t count_lines(const char* p, int64_t n) {
+    const int T = (int)std::min<int64_t>(threads_, std::max<int64_t>(1, n >> 22));
+    std::vector<int64_t> c(T, 0);
+    auto piece = [&](int t) {
+      const int64_t a = n * t / T, b = n * (t + 1) / T;
+      c[t] = std::count(p + a, p + b, '\n');
+    };
+    if (T == 1) {
+      piece(0);
+    } else {
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; ++t) th.emplace_back(piece, t);
+      for (auto& x : th) x.join();
+    }
+    int64_t k = 0;
+    for (int64_t x : c) k += x;
+    return k + (n > 0 && p[n - 1] != '\n' ? 1 : 0);
+  }
+
+  void run() {
+    int64_t off = lo_;
+    std::string err;
+    while (off < hi_) {
+      int slot;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !free_.empty(); });
+        if (stop_) return;
+        slot = free_.front();
+        free_.pop_front();
+      }
+      char* dst = slots_[slot].p;
+      const int64_t want = std::min(chunk_, hi_ - off);
+      if (!read_range(dst, off, want)) {
+        err = "read failed at offset " + std::to_string(off);
+        break;
+      }
+      int64_t used = want;
+      if (off + want < hi_) {
+        const char* nl = static_cast<const char*>(memrchr(dst, '\n', (size_t)want));
+        if (!nl) {
+          err = "a line is longer than the ingest chunk (" + std::to_string(chunk_) + " bytes)";
+          break;
+        }
+        used = nl - dst + 1;
+      }
+      const int64_t nl = count_lines(dst, used);
+      off += used;
+      std::lock_guard<std::mutex> g(mu_);
+      ready_.push_back({slot, used, nl, off - lo_});
+      cv_.notify_all();
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    err_ = err;
+    done_ = true;
+    cv_.notify_all();
+  }
+
+  int fd_ = -1;
+  int64_t lo_, hi_, chunk_;
+  int threads_;
+  std::vector<Slot> slots_;
+  std::deque<int> free_;
+  std::deque<Ready> ready_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool done_ = false, stop_ = false;
+  std::string err_;
+  std::thread th_;
+};
+
+}  // namespace mxs

@@ -139,6 +139,30 @@ def build_sanitize(verbose: bool = False) -> Path:
     return exe
 
 
+TSAN_SOURCES = ["tests/tsan_main.cpp"]
+TSAN_FLAGS = ["-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=thread", "-pthread"]
+
+
+def build_tsan(verbose: bool = False) -> Path:
+    """ThreadSanitizer harness over the threaded host code: the pinned-slot
+    file reader, the socket source, the session store's spill-worker hand-off and concurrent
+    key-group checkpoint writers (csrc/tests/tsan_main.cpp). Returns the executable's path."""
+    out_dir = ROOT / "build" / "tsan"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    exe = out_dir / "mxs_tsan"
+    srcs = [CSRC / s for s in TSAN_SOURCES]
+    cmd = ["g++", "-std=c++17", *TSAN_FLAGS, f"-I{CSRC}", "-I/opt/rocm/include",
+           "-D__HIP_PLATFORM_AMD__", *[str(s) for s in srcs], "-o", str(exe)]
+    newest = max(s.stat().st_mtime for s in srcs + sorted(CSRC.glob("*.h")))
+    if not exe.exists() or exe.stat().st_mtime < newest:
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"tsan build failed: {' '.join(cmd)}\n{res.stderr}")
+        if verbose:
+            print(f"[mxstream.build] built {exe}")
+    return exe
+
+
 CAPI_SOURCES = ["kernels_hip.hip", "check_hip.hip", "sort_hip.hip", "rolling_hist_hip.hip",
                 "kernels_cpu.cpp", "pipeline.cpp"]
 
@@ -175,6 +199,8 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--sanitize", action="store_true",
                     help="build the ASan/UBSan host harness (build/sanitize/mxs_sanitize)")
+    ap.add_argument("--tsan", action="store_true",
+                    help="build the ThreadSanitizer host harness (build/tsan/mxs_tsan)")
     ap.add_argument("--capi", action="store_true",
                     help="build the C ABI library build/lib/libmxstream.so (csrc/mxs_c.h)")
     a = ap.parse_args(argv)
@@ -183,6 +209,9 @@ def main(argv: list[str] | None = None) -> int:
         return 0
     if a.sanitize:
         print(build_sanitize(verbose=True))
+        return 0
+    if a.tsan:
+        print(build_tsan(verbose=True))
         return 0
     p = build(force=a.force, jobs=a.jobs, verbose=True)
     print(p)

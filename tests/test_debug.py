@@ -86,6 +86,22 @@ def test_host_sanitizer_harness():
     assert "sanitize_main ok" in res.stdout
 
 
+def test_thread_sanitizer_harness():
+    """ThreadSanitizer over the threaded host code: pinned-slot file reader, socket source
+    (incl. close() from another thread while recv() blocks), the session store's spill-worker
+    hand-off and concurrent key-group checkpoint writers (csrc/tests/tsan_main.cpp)."""
+    import os
+
+    from mxstream.build import build_tsan
+
+    exe = build_tsan()
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    res = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300, env=env)
+    assert "ThreadSanitizer" not in res.stderr, res.stderr[-4000:]
+    assert res.returncode == 0, res.stderr[-3000:]
+    assert "tsan_main ok" in res.stdout
+
+
 @pytest.mark.gpu
 def test_gpu_checker_matches_cpu(gpu_device):
     op = _populated_op(gpu_device)
