@@ -1608,6 +1608,7 @@ __global__ void copy_u32_kernel(const uint32_t* __restrict__ src, uint32_t* __re
 
 constexpr int kFireThreads = 1024;
 constexpr int kFireU = 4;  // slots per thread per round (ILP)
+constexpr int kFireP = 8;  // panes whose counts are loaded together
 
 __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
     const uint64_t* __restrict__ keys_g, const uint64_t* __restrict__ acc_g,
@@ -1645,14 +1646,25 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
         const int64_t s = p.list ? (int64_t)p.list[v] : v;
         bool dirty = !p.only_dirty;
         bool have = false;
-        for (int j = 0; j < p.npanes; ++j) {
-          const size_t gi = (size_t)((p.p0 + j) & (p.ring - 1)) * nslots + s;
-          const uint32_t c = cnt_g[gi];
-          if (c) {
+        // Panes in groups of kFireP: the group's count loads are all in flight before the first
+        // is used (a window of 60 panes -- 5 min / 5 s -- was 60 serial memory round trips per
+        // slot, and a small table has too few slots to hide them).
+        for (int j0 = 0; j0 < p.npanes; j0 += kFireP) {
+          uint32_t cg[kFireP];
+#pragma unroll
+          for (int q = 0; q < kFireP; ++q) {
+            const int j = j0 + q < p.npanes ? j0 + q : p.npanes - 1;
+            const uint32_t c = cnt_g[(size_t)((p.p0 + j) & (p.ring - 1)) * nslots + s];
+            cg[q] = j0 + q < p.npanes ? c : 0u;
+          }
+#pragma unroll
+          for (int q = 0; q < kFireP; ++q) {
+            if (!cg[q]) continue;
+            const size_t gi = (size_t)((p.p0 + j0 + q) & (p.ring - 1)) * nslots + s;
             const uint64_t a = acc_g[gi];
             acc[u] = have ? agg_combine(p.agg, acc[u], a) : a;
             have = true;
-            cnt[u] += c;
+            cnt[u] += cg[q];
             if (p.only_dirty && dirty_g[gi]) dirty = true;
           }
         }

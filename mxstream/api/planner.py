@@ -224,11 +224,12 @@ def _lower_text(env, sinks) -> None:
             fnode.meta = dict(fnode.meta, fused=True)
         src_factory = parent.factory
 
-        def columnar_source(f=src_factory, ring=ingest_dev is not None):
+        def columnar_source(f=src_factory, ring=ingest_dev is not None, dev=ingest_dev):
             s = f()
             s.columnar = True
             if ring and hasattr(type(s), "ring"):
                 s.ring = True  # file -> pinned ring slots (C++ reader) -> device ingest
+                s.ring_device = dev
             return s
 
         parent.factory = columnar_source

@@ -281,7 +281,8 @@ class TextIngest:
         return dev, slot[0]
 
     # ---- parse ----------------------------------------------------------------------------------
-    def parse(self, data, nlines: int | None = None, on_upload=None, agree=None) -> IngestResult:
+    def parse(self, data, nlines: int | None = None, on_upload=None, agree=None,
+              ready=None) -> IngestResult:
         """on_upload(event): called with a device event recorded after the H2D copy of a host
         tensor input (its pinned slot may be reused once the event completed).
 
@@ -303,6 +304,11 @@ class TextIngest:
                      for k in self.kinds]
             return IngestResult(0, empty, None if self.ts_field < 0 else empty[self.ts_field],
                                 None, None, 0)
+        if ready is not None and self.cuda:
+            # Device text copied by the source on its copy stream: order after that copy, and
+            # let the allocator know this stream uses the buffer.
+            torch.cuda.current_stream(self.device).wait_event(ready)
+            data.record_stream(torch.cuda.current_stream(self.device))
         buf, keep_alive = self._upload(data)
         if on_upload is not None:
             ev = None

@@ -40,11 +40,14 @@ class TextBatch:
     sub0: int = 0        # subtask of the first line (round-robin from the source edge)
     parallelism: int = 1
     token: object = None
+    ready: object = None  # device data: event after which the H2D copy is complete
 
     def host_bytes(self) -> bytes:
         if isinstance(self.data, (bytes, bytearray)):
             return bytes(self.data)
-        b = self.data.numpy().tobytes()
+        if self.ready is not None:
+            self.ready.synchronize()
+        b = self.data.cpu().numpy().tobytes()
         if self.token is not None:
             self.token.consumed()
         return b
@@ -253,8 +256,8 @@ class TextParseOp(Operator):
             self.strings = self.m.StringDict()
 
     def _parse_device(self, tb: TextBatch) -> DeviceColumnBatch:
-        res = self.ingest.parse(tb.data, tb.n, on_upload=None if tb.token is None
-                                else tb.token.uploaded, agree=self.agree)
+        res = self.ingest.parse(tb.data, tb.n, on_upload=None if (tb.token is None or tb.ready)
+                                else tb.token.uploaded, agree=self.agree, ready=tb.ready)
         nf = len(self.spec.fields)
         return DeviceColumnBatch(res.n, res.cols[:nf], tuple(k for _, k in self.spec.fields),
                                  self.strings, res.ts, sub0=tb.sub0,

@@ -590,7 +590,7 @@ class Executor:
                 out.append(Rec(it.value, it.ts, nxt % p))
                 nxt += 1
             elif isinstance(it, TextBatch):
-                out.append(TextBatch(it.data, it.n, nxt % p, p, it.token))
+                out.append(TextBatch(it.data, it.n, nxt % p, p, it.token, it.ready))
                 nxt += it.n
             else:
                 out.append(it)

@@ -252,6 +252,11 @@ class NativeWindowOp(_ColumnInput, Operator):
         a = self.assigner
         event = a.is_event_time()
         dev = torch.device(self.device)
+        if dense:
+            # Dense dictionary-id state sized to the dictionary (x2 headroom, regrown as it
+            # grows): a firing sweeps every slot of its panes, so a 2^16-slot table for a
+            # thousand channels would cost 64x the sweep (5 min / 5 s windows: 60 panes each).
+            self.max_keys = max(2048, 1 << max(1, 2 * max(1, len(self.dict))).bit_length())
         cap_log2 = 12 if self.max_keys > 100_000 else 9
         comm = getattr(self, "comm", None)
         multi = comm is not None and comm.world > 1
@@ -295,13 +300,13 @@ class NativeWindowOp(_ColumnInput, Operator):
             vk = cb.kinds[self.val_pos]
             if vk == FK_STR or (self.ok_arities and len(cb.kinds) not in self.ok_arities):
                 raise TypeError("value column not numeric")
+            kid = self._device_keys(cb)  # adopts the dictionary before the state is sized
             if self.op is None:
                 dense = cb.kinds[self.key_pos] == FK_STR
                 if not self._build(1.0 if vk == FK_DOUBLE else 1, dense=dense):
                     raise TypeError("unsupported value")
             elif (vk == FK_DOUBLE) != self.is_float:
                 raise TypeError("mixed value types")
-            kid = self._device_keys(cb)
         except TypeError:
             if self.templates or getattr(self, "_lazy_tpl", None):
                 raise

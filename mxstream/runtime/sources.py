@@ -175,11 +175,32 @@ def _aligned_range(path: str, rank: int, world: int) -> tuple[int, int]:
     return next_line(lo) if rank else 0, next_line(hi) if rank + 1 < world else size
 
 
+_PINNED_SLOTS: dict = {}  # (bytes, pinned) -> free page-locked slot tensors, reused across jobs
+
+
+def _take_slots(nbytes: int, count: int, pin: bool) -> list:
+    import torch
+
+    free = _PINNED_SLOTS.setdefault((nbytes, pin), [])
+    out = [free.pop() for _ in range(min(count, len(free)))]
+    while len(out) < count:
+        out.append(torch.empty(nbytes, dtype=torch.uint8, pin_memory=pin))
+    return out
+
+
+def _give_slots(slots: list, pin: bool) -> None:
+    if slots:
+        _PINNED_SLOTS.setdefault((slots[0].numel(), pin), []).extend(slots)
+
+
 class TextFileSource(Source):
     name = "Text File Source"
     # Set by the planner with the device ingest: batches are read by the C++ reader
-    # (csrc/reader.cpp) into pinned ring slots and handed over without a host copy.
+    # (csrc/reader.cpp) into pinned ring slots and handed over without a host copy;
+    # ring_device: the GPU of the ingest -- the next ready slot's H2D copy is started on a copy
+    # stream while the current batch is processed (copy engine || compute).
     ring = False
+    ring_device = None
 
     def __init__(self, path: str, batch_size: int = 65536):
         self.path = path
@@ -194,13 +215,21 @@ class TextFileSource(Source):
         from ..ops.native import load
 
         chunk = max(1 << 20, self.batch * 48)
-        pin = torch.cuda.is_available()
-        self._slots = [torch.empty(chunk, dtype=torch.uint8, pin_memory=pin) for _ in range(4)]
+        self._pin = torch.cuda.is_available()
+        self._slots = _take_slots(chunk, 4, self._pin)
         self._ring = load().TextFileRing(self.path, self.lo + start, self.hi,
                                          [(t.data_ptr(), t.numel()) for t in self._slots], chunk,
                                          min(16, max(1, __import__("os").cpu_count() or 1)))
         self._ring.start()
         self._held: list = []
+        self._pre = None  # prefetched (TextBatch, end offset)
+        self._cstream = None
+        if self.ring_device is not None and str(self.ring_device).startswith("cuda") \
+                and torch.cuda.is_available():
+            self._dev = torch.device(self.ring_device)
+            if self._dev.index is None:
+                self._dev = torch.device("cuda", torch.cuda.current_device())
+            self._cstream = torch.cuda.Stream(self._dev)
         self.bpos = start
         self._ring_done = self.lo + start >= self.hi
 
@@ -248,12 +277,38 @@ class TextFileSource(Source):
         if self._ring is not None:
             for t in self._held:
                 t.ready(wait=True)
+            if self._pre is not None:
+                self._pre[0].token.ready(wait=True)
             self._ring.close()
             self._ring = None
+            _give_slots(self._slots, self._pin)
+            self._slots = []
 
-    def _poll_ring(self):
+    def _take(self, timeout_ms: int):
+        """The next filled slot as a TextBatch (+ its end offset), or None."""
         from .columnar import TextBatch
 
+        slot, nbytes, nlines, end, eof = self._ring.next(timeout_ms)
+        if slot < 0:
+            if eof:
+                self._ring_eof = True
+            return None
+        tok = SlotToken(slot)
+        tb = TextBatch(self._slots[slot][:nbytes], int(nlines), token=tok)
+        if self._cstream is not None:
+            # H2D on the copy stream now: the consumer waits for `ready` (an event) instead of
+            # copying; the pinned slot is released once that copy has completed.
+            import torch
+
+            with torch.cuda.stream(self._cstream):
+                dev = tb.data.to(self._dev, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self._cstream)
+            tok.uploaded(ev)
+            tb.data, tb.ready = dev, ev
+        return tb, end
+
+    def _poll_ring(self):
         # Slots whose upload completed go back to the reader.
         keep = []
         for t in self._held:
@@ -262,17 +317,25 @@ class TextFileSource(Source):
             else:
                 keep.append(t)
         self._held = keep
-        if self._ring_done:
+        if self._pre is not None:
+            got, self._pre = self._pre, None
+        elif self._ring_done:
             return [], True
-        slot, nbytes, nlines, end, eof = self._ring.next(1000)
-        if slot < 0:
-            self._ring_done = bool(eof)
-            return [], self._ring_done
-        tok = SlotToken(slot)
-        self._held.append(tok)
+        else:
+            self._ring_eof = False
+            got = self._take(1000)
+            if got is None:
+                self._ring_done = self._ring_eof
+                return [], self._ring_done
+        tb, end = got
+        self._held.append(tb.token)
         self.bpos = end
         self._ring_done = self.lo + end >= self.hi
-        return [TextBatch(self._slots[slot][:nbytes], int(nlines), token=tok)], self._ring_done
+        if self._cstream is not None and not self._ring_done \
+                and len(self._held) < len(self._slots) - 1:
+            self._ring_eof = False
+            self._pre = self._take(0)  # prefetch: its H2D overlaps this batch's processing
+        return [tb], self._ring_done and self._pre is None
 
     def poll(self, now):
         if self.columnar and self._ring is not None:
