@@ -398,7 +398,7 @@ PYBIND11_MODULE(_mxs_native, m) {
                                intptr_t dirty_g, py::dict plan,
                                std::vector<std::tuple<int64_t, int32_t, double, double>> wins,
                                intptr_t ok, intptr_t ov, intptr_t oraw, intptr_t oc, intptr_t on,
-                               intptr_t bounds, intptr_t stream) {
+                               intptr_t bounds, intptr_t stream, py::object stage) {
     const FirePlan base = make_fire(plan);
     std::vector<FireWin> w(wins.size());
     for (size_t i = 0; i < wins.size(); ++i) {
@@ -410,8 +410,13 @@ PYBIND11_MODULE(_mxs_native, m) {
         throw std::invalid_argument("window_fire_many: window panes exceed the ring");
     }
     if (cuda) {
+      // stage = (keys, vals, raw, cnt, win_n, region): the per-window staging regions
+      const auto t = stage.cast<std::tuple<intptr_t, intptr_t, intptr_t, intptr_t, intptr_t, int64_t>>();
+      FireStage st{P<uint64_t>(std::get<0>(t)), P<double>(std::get<1>(t)), P<uint64_t>(std::get<2>(t)),
+                   P<uint32_t>(std::get<3>(t)), P<uint32_t>(std::get<4>(t)),
+                   (uint32_t)std::get<5>(t)};
       gpu::window_fire_many(P<uint64_t>(keys_g), P<uint64_t>(acc_g), P<uint32_t>(cnt_g),
-                            P<uint8_t>(dirty_g), base, w.data(), (int)w.size(), P<uint64_t>(ok),
+                            P<uint8_t>(dirty_g), base, w.data(), (int)w.size(), st, P<uint64_t>(ok),
                             P<double>(ov), P<uint64_t>(oraw), P<uint32_t>(oc), P<uint32_t>(on),
                             P<uint32_t>(bounds), stream);
       return;
@@ -908,4 +913,5 @@ PYBIND11_MODULE(_mxs_native, m) {
   bind_trace(m);
   bind_check(m);
   bind_reader(m);
+  bind_format(m);
 }

@@ -1,0 +1,75 @@
+// mxstream — Python binding of the bulk Java formatter (csrc/javafmt.h): the print sink's
+// columnar path (runtime/operators.py PrintSinkOp.process_columns).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "javafmt.h"
+#include "mxs_runtime.h"
+
+namespace py = pybind11;
+
+void bind_format(py::module_& m) {
+  // rows i < n of the columns (kind, address): kind 0 = int64 ids into `names` (str), 1 = f64
+  // (Double.toString), 2 = int64 (Long.toString). as_tuple: "(f0,f1,...)", else the single
+  // column's text. prefixes[sub[i]] is prepended when `sub` (int32 address) is non-zero.
+  m.def("java_format_rows", [](std::vector<std::tuple<int, intptr_t>> cols, int64_t n,
+                               py::object names, intptr_t sub, std::vector<std::string> prefixes,
+                               bool as_tuple) {
+    if (cols.empty() || n < 0) throw std::invalid_argument("java_format_rows: no columns");
+    if (!as_tuple && cols.size() != 1) throw std::invalid_argument("java_format_rows: arity");
+    std::vector<std::string> nm;
+    for (auto& c : cols)
+      if (std::get<0>(c) == 0) {
+        if (names.is_none()) throw std::invalid_argument("java_format_rows: string ids need names");
+        if (nm.empty()) nm = names.cast<std::vector<std::string>>();
+        break;
+      }
+    std::vector<std::string> out((size_t)n);
+    {
+      py::gil_scoped_release nogil;
+      const int32_t* sb = reinterpret_cast<const int32_t*>(sub);
+      std::string s;
+      for (int64_t i = 0; i < n; ++i) {
+        s.clear();
+        if (sb) {
+          const int32_t k = sb[i];
+          if (k < 0 || (size_t)k >= prefixes.size())
+            throw std::out_of_range("java_format_rows: subtask without prefix");
+          s += prefixes[(size_t)k];
+        }
+        if (as_tuple) s.push_back('(');
+        for (size_t j = 0; j < cols.size(); ++j) {
+          if (j) s.push_back(',');
+          const int kind = std::get<0>(cols[j]);
+          const intptr_t a = std::get<1>(cols[j]);
+          if (kind == 0) {
+            const int64_t id = reinterpret_cast<const int64_t*>(a)[i];
+            if (id < 0 || (size_t)id >= nm.size())
+              throw std::out_of_range("java_format_rows: string id outside the dictionary");
+            s += nm[(size_t)id];
+          } else if (kind == 1) {
+            mxs::java_double_append(reinterpret_cast<const double*>(a)[i], s);
+          } else if (kind == 2) {
+            mxs::java_long_append(reinterpret_cast<const int64_t*>(a)[i], s);
+          } else {
+            throw std::invalid_argument("java_format_rows: unknown column kind");
+          }
+        }
+        if (as_tuple) s.push_back(')');
+        out[(size_t)i] = s;
+      }
+    }
+    return out;
+  }, py::arg("cols"), py::arg("n"), py::arg("names"), py::arg("sub"), py::arg("prefixes"),
+     py::arg("as_tuple") = true);
+  m.def("java_double_str", [](double x) {
+    std::string s;
+    mxs::java_double_append(x, s);
+    return s;
+  });
+}

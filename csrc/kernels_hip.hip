@@ -1602,41 +1602,41 @@ struct RegVars {
   }
 };
 
-__global__ void copy_u32_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst) {
-  if (threadIdx.x == 0) *dst = *src;
-}
-
 constexpr int kFireThreads = 1024;
 constexpr int kFireU = 4;  // slots per thread per round (ILP)
 constexpr int kFireP = 8;  // panes whose counts are loaded together
+constexpr int kFireMultiThreads = 256;
 
-__global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
+// One window's sweep, shared by the single-window kernel (T = 1024, the whole grid on one window)
+// and the batched kernel (T = 256, blockIdx.y = window): the window fields (p0, npanes, wstart,
+// wend) come as arguments so the plan itself stays in the kernel-argument segment.
+template <int T, int U>
+__device__ __forceinline__ void fire_window_body(
     const uint64_t* __restrict__ keys_g, const uint64_t* __restrict__ acc_g,
-    const uint32_t* __restrict__ cnt_g, const uint8_t* __restrict__ dirty_g, FirePlan p,
-    uint64_t* __restrict__ out_keys, double* __restrict__ out_vals, uint64_t* __restrict__ out_raw,
-    uint32_t* __restrict__ out_cnt, uint32_t* __restrict__ out_n) {
-  // LDS: [kExprVars + depth][kFireThreads] f64 VM columns | 16 wave counts | block base
-  extern __shared__ __attribute__((aligned(16))) double fsm[];
-  LdsCol vars{fsm + threadIdx.x, kFireThreads};
-  LdsCol stack{fsm + kExprVars * kFireThreads + threadIdx.x, kFireThreads};
+    const uint32_t* __restrict__ cnt_g, const uint8_t* __restrict__ dirty_g, const FirePlan& p,
+    int64_t p0, int npanes, double wstart, double wend, uint64_t* __restrict__ out_keys,
+    double* __restrict__ out_vals, uint64_t* __restrict__ out_raw, uint32_t* __restrict__ out_cnt,
+    uint32_t* __restrict__ out_n, uint32_t out_cap, double* fsm, int64_t bx, int64_t gx) {
+  // LDS: [kExprVars + depth][T] f64 VM columns | T/64 wave counts | block base
+  LdsCol vars{fsm + threadIdx.x, T};
+  LdsCol stack{fsm + kExprVars * T + threadIdx.x, T};
   const int depth = p.map.depth > p.filt.depth ? p.map.depth : p.filt.depth;
-  uint32_t* wcnt = (uint32_t*)(fsm + (size_t)(kExprVars + depth) * kFireThreads);
-  const int wid = threadIdx.x >> 6, nw = kFireThreads >> 6;
+  uint32_t* wcnt = (uint32_t*)(fsm + (size_t)(kExprVars + depth) * T);
+  const int wid = threadIdx.x >> 6, nw = T >> 6;
   const int64_t nslots = p.nslots;
-  const int64_t per_round = (int64_t)kFireThreads * kFireU;
+  const int64_t per_round = (int64_t)T * U;
   const bool chain_only = (!p.map.ncode || p.map.chain) && (!p.filt.ncode || p.filt.chain);
   // Slot-list mode (re-firings): visit only the listed slots.
   const int64_t nvisit = p.list ? (int64_t)*p.list_n : nslots;
   // Rounds are block-uniform, so every lane reaches the barriers and the ballots.
-  for (int64_t base = (int64_t)blockIdx.x * per_round; base < nvisit;
-       base += (int64_t)gridDim.x * per_round) {
-    bool emit[kFireU];
-    uint64_t acc[kFireU], key[kFireU];
-    uint32_t cnt[kFireU];
-    double val[kFireU];
+  for (int64_t base = bx * per_round; base < nvisit; base += gx * per_round) {
+    bool emit[U];
+    uint64_t acc[U], key[U];
+    uint32_t cnt[U];
+    double val[U];
 #pragma unroll
-    for (int u = 0; u < kFireU; ++u) {
-      const int64_t v = base + (int64_t)u * kFireThreads + threadIdx.x;
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = base + (int64_t)u * T + threadIdx.x;
       emit[u] = false;
       acc[u] = 0;
       key[u] = 0;
@@ -1649,18 +1649,18 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
         // Panes in groups of kFireP: the group's count loads are all in flight before the first
         // is used (a window of 60 panes -- 5 min / 5 s -- was 60 serial memory round trips per
         // slot, and a small table has too few slots to hide them).
-        for (int j0 = 0; j0 < p.npanes; j0 += kFireP) {
+        for (int j0 = 0; j0 < npanes; j0 += kFireP) {
           uint32_t cg[kFireP];
 #pragma unroll
           for (int q = 0; q < kFireP; ++q) {
-            const int j = j0 + q < p.npanes ? j0 + q : p.npanes - 1;
-            const uint32_t c = cnt_g[(size_t)((p.p0 + j) & (p.ring - 1)) * nslots + s];
-            cg[q] = j0 + q < p.npanes ? c : 0u;
+            const int j = j0 + q < npanes ? j0 + q : npanes - 1;
+            const uint32_t c = cnt_g[(size_t)((p0 + j) & (p.ring - 1)) * nslots + s];
+            cg[q] = j0 + q < npanes ? c : 0u;
           }
 #pragma unroll
           for (int q = 0; q < kFireP; ++q) {
             if (!cg[q]) continue;
-            const size_t gi = (size_t)((p.p0 + j0 + q) & (p.ring - 1)) * nslots + s;
+            const size_t gi = (size_t)((p0 + j0 + q) & (p.ring - 1)) * nslots + s;
             const uint64_t a = acc_g[gi];
             acc[u] = have ? agg_combine(p.agg, acc[u], a) : a;
             have = true;
@@ -1675,7 +1675,7 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
           emit[u] = true;
           if ((p.map.ncode || p.filt.ncode) && !(p.ablate & 1u) && chain_only) {
             // Register-only epilogue (plan-uniform branch): no LDS stack / variable columns.
-            const RegVars rv{v0, (double)cnt[u], p.wstart, p.wend, (double)key[u],
+            const RegVars rv{v0, (double)cnt[u], wstart, wend, (double)key[u],
                              (double)(int64_t)acc[u], 0.0};
             if (p.map.ncode) val[u] = expr_eval_chain(p.map, rv);
             if (p.filt.ncode) {
@@ -1686,8 +1686,8 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
           } else if ((p.map.ncode || p.filt.ncode) && !(p.ablate & 1u)) {
             vars.set(0, v0);
             vars.set(1, (double)cnt[u]);
-            vars.set(2, p.wstart);
-            vars.set(3, p.wend);
+            vars.set(2, wstart);
+            vars.set(3, wend);
             vars.set(4, (double)key[u]);
             vars.set(5, (double)(int64_t)acc[u]);
             if (p.map.ncode) val[u] = expr_eval_t(p.map, stack, vars);
@@ -1698,11 +1698,11 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
       }
     }
     // Block-level compaction: wave ballots -> LDS prefix over waves -> ONE global atomic per
-    // round of 4096 slots (a per-wave atomic on one counter serialises ~65K times at 4M slots).
+    // round (a per-wave atomic on one counter serialises ~65K times at 4M slots).
     uint32_t mine = 0;
-    unsigned long long masks[kFireU];
+    unsigned long long masks[U];
 #pragma unroll
-    for (int u = 0; u < kFireU; ++u) {
+    for (int u = 0; u < U; ++u) {
       masks[u] = __ballot(emit[u]);
       mine += (uint32_t)__popcll(masks[u]);
     }
@@ -1722,10 +1722,10 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
     uint32_t pos = wcnt[nw] + wcnt[wid];
     const unsigned long long lt = (1ull << lane_id()) - 1ull;
 #pragma unroll
-    for (int u = 0; u < kFireU; ++u) {
+    for (int u = 0; u < U; ++u) {
       if (emit[u]) {
         const uint32_t q = pos + (uint32_t)__popcll(masks[u] & lt);
-        if (q < p.out_cap) {
+        if (q < out_cap) {
           out_keys[q] = key[u];
           out_vals[q] = val[u];
           out_raw[q] = acc[u];
@@ -1734,6 +1734,80 @@ __global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
       }
       pos += (uint32_t)__popcll(masks[u]);
     }
+  }
+}
+
+__global__ __launch_bounds__(kFireThreads) void window_fire_kernel(
+    const uint64_t* __restrict__ keys_g, const uint64_t* __restrict__ acc_g,
+    const uint32_t* __restrict__ cnt_g, const uint8_t* __restrict__ dirty_g, FirePlan p,
+    uint64_t* __restrict__ out_keys, double* __restrict__ out_vals, uint64_t* __restrict__ out_raw,
+    uint32_t* __restrict__ out_cnt, uint32_t* __restrict__ out_n) {
+  extern __shared__ __attribute__((aligned(16))) double fsm[];
+  fire_window_body<kFireThreads, kFireU>(keys_g, acc_g, cnt_g, dirty_g, p, p.p0, p.npanes,
+                                         p.wstart, p.wend, out_keys, out_vals, out_raw, out_cnt,
+                                         out_n, p.out_cap, fsm, blockIdx.x, gridDim.x);
+}
+
+// Batched firing: blockIdx.y = window of the pack. Window w appends to its own region
+// [w * region, (w + 1) * region) of the staging columns at its own counter win_n[w] (a window
+// emits at most one row per slot, so region = nslots never overflows); fire_pack_kernel then
+// lays the regions out back to back in window order. A 5 min / 5 s window over a 2K-key table
+// is 8 workgroups of 256 slots; 32 windows fill the chip where one window's sweep had ONE
+// 1024-thread workgroup and 52 us of serial pane loads.
+constexpr int kFireMultiMax = 32;  // windows per launch (kernel-argument segment)
+struct FireWinPack {
+  FireWin w[kFireMultiMax];
+  int n;
+};
+
+template <int U>
+__global__ __launch_bounds__(kFireMultiThreads) void window_fire_multi_kernel(
+    const uint64_t* __restrict__ keys_g, const uint64_t* __restrict__ acc_g,
+    const uint32_t* __restrict__ cnt_g, const uint8_t* __restrict__ dirty_g, FirePlan p,
+    FireWinPack pack, int w0, FireStage st) {
+  extern __shared__ __attribute__((aligned(16))) double fsm[];
+  const int y = blockIdx.y;
+  const FireWin& w = pack.w[y];
+  const size_t o = (size_t)(w0 + y) * st.region;
+  fire_window_body<kFireMultiThreads, U>(keys_g, acc_g, cnt_g, dirty_g, p, w.p0, w.npanes,
+                                         w.wstart, w.wend, st.keys + o, st.vals + o, st.raw + o,
+                                         st.cnt + o, st.win_n + w0 + y, st.region, fsm, blockIdx.x,
+                                         gridDim.x);
+}
+
+// Regions -> contiguous rows in window order; bounds[w] = rows of windows 0..w, *out_n = total.
+__global__ __launch_bounds__(256) void fire_pack_kernel(FireStage st, int k,
+                                                        uint64_t* __restrict__ out_keys,
+                                                        double* __restrict__ out_vals,
+                                                        uint64_t* __restrict__ out_raw,
+                                                        uint32_t* __restrict__ out_cnt,
+                                                        uint32_t* __restrict__ bounds,
+                                                        uint32_t* __restrict__ out_n) {
+  const int w = blockIdx.y;
+  __shared__ uint32_t s_off;
+  if (threadIdx.x < 64) {  // wave 0: prefix of the earlier windows' row counts
+    uint32_t c = 0;
+    for (int j = threadIdx.x; j < w; j += 64) {
+      const uint32_t x = st.win_n[j];
+      c += x < st.region ? x : st.region;
+    }
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
+    if (threadIdx.x == 0) s_off = c;
+  }
+  __syncthreads();
+  const uint32_t off = s_off;
+  uint32_t n = st.win_n[w];
+  n = n < st.region ? n : st.region;
+  const size_t src = (size_t)w * st.region;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    out_keys[off + i] = st.keys[src + i];
+    out_vals[off + i] = st.vals[src + i];
+    out_raw[off + i] = st.raw[src + i];
+    out_cnt[off + i] = st.cnt[src + i];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    bounds[w] = off + n;
+    if (w == k - 1) *out_n = off + n;
   }
 }
 
@@ -3514,21 +3588,33 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
 
 void window_fire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
                       const uint8_t* dirty_g, const FirePlan& base, const FireWin* wins, int k,
-                      uint64_t* out_keys, double* out_vals, uint64_t* out_raw, uint32_t* out_cnt,
-                      uint32_t* out_n, uint32_t* bounds, intptr_t stream) {
-  for (int i = 0; i < k; ++i) {
-    FirePlan p = base;
-    p.p0 = wins[i].p0;
-    p.npanes = wins[i].npanes;
-    p.wstart = wins[i].wstart;
-    p.wend = wins[i].wend;
-    window_fire(keys_g, acc_g, cnt_g, dirty_g, p, out_keys, out_vals, out_raw, out_cnt, out_n,
-                stream);
-    // rows of windows 0..i = the cursor after window i (stream order)
-    hipLaunchKernelGGL(copy_u32_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, out_n,
-                       bounds + i);
+                      const FireStage& st, uint64_t* out_keys, double* out_vals, uint64_t* out_raw,
+                      uint32_t* out_cnt, uint32_t* out_n, uint32_t* bounds, intptr_t stream) {
+  if (k <= 0 || base.nslots <= 0) return;
+  if (st.region < (uint32_t)base.nslots)
+    throw std::invalid_argument("window_fire_many: staging region smaller than the table");
+  const int depth = base.map.depth > base.filt.depth ? base.map.depth : base.filt.depth;
+  const size_t lds = (size_t)(kExprVars + depth) * kFireMultiThreads * sizeof(double) + 8 * 4;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_CHECK(hipMemsetAsync(st.win_n, 0, sizeof(uint32_t) * k, s));
+  const int64_t nvisit = base.nslots;
+  const bool big = nvisit >= 65536;
+  const int gx = grid_for(nvisit, kFireMultiThreads * (big ? 4 : 1), big ? 256 : 1024);
+  for (int w0 = 0; w0 < k; w0 += kFireMultiMax) {
+    FireWinPack pack{};
+    pack.n = k - w0 < kFireMultiMax ? k - w0 : kFireMultiMax;
+    for (int i = 0; i < pack.n; ++i) pack.w[i] = wins[w0 + i];
+    if (big)
+      hipLaunchKernelGGL(window_fire_multi_kernel<4>, dim3(gx, pack.n), dim3(kFireMultiThreads),
+                         lds, s, keys_g, acc_g, cnt_g, dirty_g, base, pack, w0, st);
+    else
+      hipLaunchKernelGGL(window_fire_multi_kernel<1>, dim3(gx, pack.n), dim3(kFireMultiThreads),
+                         lds, s, keys_g, acc_g, cnt_g, dirty_g, base, pack, w0, st);
     HIP_CHECK(hipGetLastError());
   }
+  hipLaunchKernelGGL(fire_pack_kernel, dim3(grid_for(nvisit, 256 * 4, 64), k), dim3(256), 0, s,
+                     st, k, out_keys, out_vals, out_raw, out_cnt, bounds, out_n);
+  HIP_CHECK(hipGetLastError());
 }
 
 void direct_agg_probe(const uint64_t* keys, const int64_t* ts, const uint64_t* vals, int64_t n,

@@ -74,6 +74,17 @@ struct FireWin {
   double wstart, wend;
 };
 
+// Staging of a batched firing on the GPU: window w of the batch writes its rows to
+// [w * region, (w + 1) * region) of these columns at counter win_n[w] (region >= nslots).
+struct FireStage {
+  uint64_t* keys;
+  double* vals;
+  uint64_t* raw;
+  uint32_t* cnt;
+  uint32_t* win_n;
+  uint32_t region;
+};
+
 // Local-global window aggregation (G > 1): where the rows of a locally fired window go.
 struct ScatPlan {
   int32_t max_parallelism;  // Flink maxParallelism (key groups)
@@ -166,8 +177,9 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
 // cursor out_n; bounds[i] = rows of windows 0..i (device).
 void window_fire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
                       const uint8_t* dirty_g, const FirePlan& base, const FireWin* wins, int k,
-                      uint64_t* out_keys, double* out_vals, uint64_t* out_raw, uint32_t* out_cnt,
-                      uint32_t* out_n, uint32_t* bounds, intptr_t stream);
+                      const FireStage& stage, uint64_t* out_keys, double* out_vals,
+                      uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n, uint32_t* bounds,
+                      intptr_t stream);
 void rolling(const Rec* recs, const uint32_t* counts, const RollPlan& plan, uint64_t* keys_g,
              uint64_t* acc_g, uint32_t* cnt_g, uint32_t* occupancy, uint32_t* flags,
              uint64_t* out_vals, intptr_t stream);

@@ -9,3 +9,4 @@ void bind_vector(pybind11::module_& m);
 void bind_trace(pybind11::module_& m);
 void bind_check(pybind11::module_& m);
 void bind_reader(pybind11::module_& m);
+void bind_format(pybind11::module_& m);

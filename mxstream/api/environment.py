@@ -109,6 +109,19 @@ class RestartStrategies:
     fixedDelayRestart = fixed_delay_restart
 
 
+class _StdoutWriter:
+    """print() sink target: one line per call, or a whole column batch in one write."""
+
+    def __call__(self, s: str) -> None:
+        print(s, flush=True)
+
+    @staticmethod
+    def many(lines: list) -> None:
+        if lines:
+            sys.stdout.write("\n".join(lines) + "\n")
+            sys.stdout.flush()
+
+
 class StreamExecutionEnvironment:
     DEFAULT_PARALLELISM = 4
 
@@ -122,7 +135,7 @@ class StreamExecutionEnvironment:
         self.restart_strategy = RestartStrategies.no_restart()
         self.clock = clock or SystemClock()
         self._sinks: list[Transformation] = []
-        self._writer = lambda s: print(s, flush=True)
+        self._writer = _StdoutWriter()
         self.rank = int(os.environ.get("RANK", "0"))
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.state_backend = None

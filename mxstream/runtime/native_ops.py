@@ -18,7 +18,7 @@ import torch
 from ..api.tuples import Tuple
 from ..ops import expr as E
 from ..ops import kernels as K
-from ..ops.text import FK_DOUBLE, FK_STR
+from ..ops.text import FK_DOUBLE, FK_LONG, FK_STR
 from ..utils.hashing import java_hash
 from .columnar import ColumnBatch, DeviceColumnBatch, concat_device, expand_columns
 from .operators import LONG_MAX, LONG_MIN, Operator, Rec, WM, WindowOp
@@ -441,7 +441,69 @@ class NativeWindowOp(_ColumnInput, Operator):
             self.num_late_records_dropped += self.op.metrics.num_late_records_dropped - late_before
         return self._emit(fired)
 
+    def _columnar_kinds(self):
+        """Column kinds of the fused output tuple when every field is the key, the window
+        result or the mapped value (no keep-first template fields); None otherwise."""
+        if self.fused_layout is None or self.fused_scalar or self.str_keys is None:
+            return None
+        kinds = []
+        for j in self.fused_layout:
+            if j < 0 or (j == self.val_pos and self.kind == "avg"):
+                kinds.append(FK_DOUBLE)
+            elif j == self.val_pos:
+                kinds.append(FK_DOUBLE if self.is_float and self.kind != "count" else FK_LONG)
+            elif j == self.key_pos:
+                kinds.append(FK_STR if self.str_keys else FK_LONG)
+            else:
+                return None
+        return tuple(kinds)
+
+    def _subtasks(self, keys: np.ndarray) -> np.ndarray:
+        """Output subtask of every key id (Java hash + murmur, cached per key)."""
+        P, MP = self.ctx.parallelism, self.ctx.max_parallelism
+        u, inv = np.unique(keys, return_inverse=True)
+        su = np.empty(u.size, dtype=np.int32)
+        for i, k in enumerate(u.tolist()):
+            sub = self._subs.get(k)
+            if sub is None:
+                from ..utils.hashing import flink_murmur
+
+                key_obj = self.dict.get(k) if self.str_keys else k
+                sub = self._subs[k] = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
+            su[i] = sub
+        return su[inv.reshape(-1)]
+
+    def _emit_columns(self, fired, kinds) -> list:
+        """The fired rows of all windows as ONE ColumnBatch (window order, then row order --
+        the order of the per-record path): a columnar sink (print) formats them in bulk,
+        any other operator receives the same Recs through ColumnBatch.to_recs."""
+        fired = [fr for fr in fired if fr.keys.size]
+        if not fired:
+            return []
+        keys = np.concatenate([fr.keys for fr in fired])
+        keys = keys.view(np.int64) if keys.dtype == np.uint64 else keys.astype(np.int64)
+        cols = []
+        for j, k in zip(self.fused_layout, kinds):
+            if j < 0 or (j == self.val_pos and self.kind == "avg"):
+                cols.append(np.concatenate([fr.values for fr in fired]).astype(np.float64, copy=False))
+            elif j == self.val_pos:
+                if self.kind == "count":
+                    cols.append(np.concatenate([fr.counts for fr in fired]).astype(np.int64))
+                else:
+                    raw = np.concatenate([fr.raw for fr in fired])
+                    raw = raw.view(np.int64) if raw.dtype == np.uint64 else raw.astype(np.int64)
+                    cols.append(raw.view(np.float64) if k == FK_DOUBLE else raw)
+            else:
+                cols.append(keys)
+        ts = np.repeat(np.array([fr.window_end - 1 for fr in fired], dtype=np.int64),
+                       [fr.keys.size for fr in fired])
+        return [ColumnBatch(int(keys.size), cols, kinds, self.dict if self.str_keys else None,
+                            ts, self._subtasks(keys))]
+
     def _emit(self, fired) -> list:
+        kinds = self._columnar_kinds() if fired else None
+        if kinds is not None:
+            return self._emit_columns(fired, kinds)
         out = []
         P, MP = self.ctx.parallelism, self.ctx.max_parallelism
         for fr in fired:

@@ -16,11 +16,12 @@ Flink 1.8 behaviour reproduced (class names are Flink's):
 from __future__ import annotations
 
 import copy
-
 import heapq
 import itertools
 from dataclasses import dataclass
 from typing import Any, Callable
+
+import numpy as np
 
 from ..api import functions as F
 from ..api.state import (AggregatingStateDescriptor, HeapKeyedStateBackend, ListStateDescriptor,
@@ -836,6 +837,73 @@ class PrintSinkOp(Operator):
         self.ident = sink_identifier
         self.to_stderr = to_stderr
         self.parallelism = parallelism
+
+    accepts_columns = True
+
+    def process(self, items: list) -> list:
+        from .columnar import ColumnBatch
+
+        if not any(isinstance(it, ColumnBatch) for it in items):
+            return super().process(items)
+        out = []
+        for it in items:
+            if isinstance(it, ColumnBatch):
+                self._print_columns(it)
+            else:
+                out.extend(super().process([it]))
+        return out
+
+    def _prefixes(self, nsub: int) -> list[str]:
+        p = self.parallelism or self.ctx.parallelism
+        if self.ident:
+            return [self.ident + (f":{k + 1}> " if p > 1 else "> ") for k in range(nsub)]
+        return [f"{k + 1}> " if p > 1 else "" for k in range(nsub)]
+
+    def _print_columns(self, cb) -> None:
+        """A column batch in one native call (csrc/javafmt.h: Tuple/Double/Long toString), the
+        lines handed to the writer at once when it takes many (the default stdout writer)."""
+        from ..ops.native import load
+        from ..ops.text import FK_DOUBLE, FK_INT, FK_LONG, FK_STR
+
+        cb = cb.host() if hasattr(cb, "host") else cb
+        if cb.n == 0:
+            return
+        cols, keep, names = [], [], None
+        for c, k in zip(cb.cols, cb.kinds):
+            c = np.asarray(c)[:cb.n]
+            if k == FK_STR:
+                u, inv = np.unique(c, return_inverse=True)
+                if names is not None:  # several string columns: one name list for all
+                    off = len(names)
+                    names.extend(cb.strings.get(int(x)) for x in u.tolist())
+                else:
+                    off, names = 0, [cb.strings.get(int(x)) for x in u.tolist()]
+                a = np.ascontiguousarray(inv.reshape(-1).astype(np.int64) + off)
+                cols.append((0, a.ctypes.data))
+            elif k == FK_DOUBLE:
+                a = np.ascontiguousarray(c, dtype=np.float64)
+                cols.append((1, a.ctypes.data))
+            elif k in (FK_LONG, FK_INT):
+                a = np.ascontiguousarray(c, dtype=np.int64)
+                cols.append((2, a.ctypes.data))
+            else:  # a kind without a bulk format: the per-record path
+                for r in cb.to_recs():
+                    self.on_record(r)
+                return
+            keep.append(a)
+        sub = cb.sub
+        if sub is not None:
+            sub = np.ascontiguousarray(sub[:cb.n], dtype=np.int32)
+            keep.append(sub)
+        nsub = int(sub.max()) + 1 if sub is not None else 1
+        lines = load().java_format_rows(cols, cb.n, names, 0 if sub is None else sub.ctypes.data,
+                                        self._prefixes(nsub), True)
+        many = getattr(self.writer, "many", None)
+        if many is not None:
+            many(lines)
+        else:
+            for ln in lines:
+                self.writer(ln)
 
     def on_record(self, r):
         from ..utils.javafmt import java_str

@@ -102,10 +102,11 @@ class VectorWindowOperator(KeyedWindowOperator):
         V.vec_window_agg(recs, counts, plan, vec, self.keys_g, self.vacc_g, self.cnt_g,
                          self.dirty_g, self.occ, self.flags)
 
-    def _zero_pane(self, so: int) -> None:
-        self.vacc_g[so * self.dim:(so + self.nslots) * self.dim].zero_()
-        self.cnt_g[so:so + self.nslots].zero_()
-        self.dirty_g[so:so + self.nslots].zero_()
+    def _zero_pane(self, so: int, k: int = 1) -> None:
+        e = so + k * self.nslots
+        self.vacc_g[so * self.dim:e * self.dim].zero_()
+        self.cnt_g[so:e].zero_()
+        self.dirty_g[so:e].zero_()
 
     def _grow_ring(self, need: int) -> None:
         new_ring = _next_pow2(need)

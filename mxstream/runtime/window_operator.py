@@ -1074,11 +1074,12 @@ class KeyedWindowOperator:
                                self.occ.data_ptr(), self.flags.data_ptr(),
                                torch.cuda.current_stream(self.device).cuda_stream if cuda else 0)
 
-    def _zero_pane(self, so: int) -> None:
-        """Reset the pane slab starting at slot index `so` (pane-major state)."""
-        self.acc_g[so:so + self.nslots].zero_()
-        self.cnt_g[so:so + self.nslots].zero_()
-        self.dirty_g[so:so + self.nslots].zero_()
+    def _zero_pane(self, so: int, k: int = 1) -> None:
+        """Reset k consecutive pane slabs starting at slot index `so` (pane-major state)."""
+        e = so + k * self.nslots
+        self.acc_g[so:e].zero_()
+        self.cnt_g[so:e].zero_()
+        self.dirty_g[so:e].zero_()
 
     def _stage(self, name: str):
         import contextlib
@@ -1306,16 +1307,18 @@ class KeyedWindowOperator:
             if p1 >= p0:
                 wins.append((s, (p0, p1 - p0 + 1, float(s), float(s + self.size))))
         stream = torch.cuda.current_stream(self.device).cuda_stream if cuda else 0
+        stage = self._fire_stage() if cuda else None
         g = self._fire_group
         for i in range(0, len(wins), g):
             chunk = wins[i:i + g]
-            self.out_n.zero_()
+            if not cuda:
+                self.out_n.zero_()
             self._m.window_fire_many(cuda, self.keys_g.data_ptr(), self.acc_g.data_ptr(),
                                      self.cnt_g.data_ptr(), self.dirty_g.data_ptr(), plan,
                                      [w for _, w in chunk], self.out_keys.data_ptr(),
                                      self.out_vals.data_ptr(), self.out_raw.data_ptr(),
                                      self.out_cnt.data_ptr(), self.out_n.data_ptr(),
-                                     self.fire_bounds.data_ptr(), stream)
+                                     self.fire_bounds.data_ptr(), stream, stage)
             bounds = self._fired_bounds(len(chunk))
             self.metrics.num_fires += len(chunk)
             n = min(bounds[-1], self.out_keys.numel())
@@ -1333,6 +1336,22 @@ class KeyedWindowOperator:
                                           host[2][lo:hi], host[3][lo:hi], refire=only_dirty))
                 lo = hi
         return out
+
+    def _fire_stage(self) -> tuple:
+        """Per-window staging regions of the GPU batched firing (window_fire_many: window w of
+        a group writes rows [w * nslots, (w + 1) * nslots) at its own counter, a pack kernel
+        then lays the group out in window order into out_*). Allocated on first use; sized like
+        out_* (nslots x fire group)."""
+        st = getattr(self, "_stage_cols", None)
+        if st is None or st[0].numel() != self.out_keys.numel():
+            n, dev = self.out_keys.numel(), self.out_keys.device
+            st = (torch.empty(n, dtype=torch.int64, device=dev),
+                  torch.empty(n, dtype=torch.float64, device=dev),
+                  torch.empty(n, dtype=torch.int64, device=dev),
+                  torch.empty(n, dtype=torch.int32, device=dev),
+                  torch.empty(self._fire_group, dtype=torch.int32, device=dev))
+            self._stage_cols = st
+        return tuple(t.data_ptr() for t in st) + (self.nslots,)
 
     def _fire_ready(self, wm: int) -> list[FireResult]:
         out: list[FireResult] = []
@@ -1398,9 +1417,11 @@ class KeyedWindowOperator:
         stop = min(keep_from, self.max_seen_pane + 1)
         if stop - p > self.ring:
             p = stop - self.ring
-        while p < stop:
-            self._zero_pane((p & (self.ring - 1)) * self.nslots)
-            p += 1
+        while p < stop:  # at most two runs of consecutive ring positions (wrap-around)
+            r = p & (self.ring - 1)
+            k = min(stop - p, self.ring - r)
+            self._zero_pane(r * self.nslots, k)
+            p += k
         if keep_from > self.min_live_pane:
             self.min_live_pane = keep_from
             if self.min_live_pane > self.max_seen_pane:
