@@ -73,6 +73,7 @@ PartPlan make_part(py::dict d) {
   p.hash_mode = d["hash_mode"].cast<int32_t>();
   p.bucket_cap = d["bucket_cap"].cast<uint32_t>();
   p.ablate = d.contains("ablate") ? d["ablate"].cast<uint32_t>() : 0u;
+  p.key32 = d.contains("key32") ? d["key32"].cast<int32_t>() : 0;
   p.late_ts = d["late_ts"].cast<int64_t>();
   p.tbase = d["tbase"].cast<int64_t>();
   p.pane = d["pane"].cast<int64_t>();
@@ -163,6 +164,7 @@ FirePlan make_fire(py::dict d) {
   p.wend = d["wend"].cast<double>();
   p.out_cap = d["out_cap"].cast<uint32_t>();
   p.ablate = d.contains("ablate") ? d["ablate"].cast<uint32_t>() : 0u;
+  p.key32 = d.contains("key32") ? d["key32"].cast<int32_t>() : 0;
   if (d.contains("list") && d["list"].cast<intptr_t>()) {
     p.list = reinterpret_cast<const uint32_t*>(d["list"].cast<intptr_t>());
     p.list_n = reinterpret_cast<const uint32_t*>(d["list_n"].cast<intptr_t>());
@@ -409,8 +411,10 @@ PYBIND11_MODULE(_mxs_native, m) {
       if (w[i].npanes <= 0 || w[i].npanes > base.ring)
         throw std::invalid_argument("window_fire_many: window panes exceed the ring");
     }
+    if (!ov || !ok) throw std::invalid_argument("window_fire_many: key and value columns");
     if (cuda) {
       // stage = (keys, vals, raw, cnt, win_n, region): the per-window staging regions
+      // (raw / cnt 0 in compact mode)
       const auto t = stage.cast<std::tuple<intptr_t, intptr_t, intptr_t, intptr_t, intptr_t, int64_t>>();
       FireStage st{P<uint64_t>(std::get<0>(t)), P<double>(std::get<1>(t)), P<uint64_t>(std::get<2>(t)),
                    P<uint32_t>(std::get<3>(t)), P<uint32_t>(std::get<4>(t)),

@@ -291,10 +291,13 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
     const bool emit = p.filt.ncode ? (expr_eval(p.filt, vars) != 0.0) : true;
     if (!emit) continue;
     if (n < p.out_cap) {
-      out_keys[n] = key;
+      if (p.key32)
+        reinterpret_cast<uint32_t*>(out_keys)[n] = (uint32_t)key;
+      else
+        out_keys[n] = key;
       out_vals[n] = vars[6];
-      out_raw[n] = acc;
-      out_cnt[n] = cnt;
+      if (out_raw) out_raw[n] = acc;
+      if (out_cnt) out_cnt[n] = cnt;
     }
     ++n;
   }

@@ -1726,10 +1726,13 @@ __device__ __forceinline__ void fire_window_body(
       if (emit[u]) {
         const uint32_t q = pos + (uint32_t)__popcll(masks[u] & lt);
         if (q < out_cap) {
-          out_keys[q] = key[u];
+          if (p.key32)
+            reinterpret_cast<uint32_t*>(out_keys)[q] = (uint32_t)key[u];
+          else
+            out_keys[q] = key[u];
           out_vals[q] = val[u];
-          out_raw[q] = acc[u];
-          out_cnt[q] = cnt[u];
+          if (out_raw) out_raw[q] = acc[u];
+          if (out_cnt) out_cnt[q] = cnt[u];
         }
       }
       pos += (uint32_t)__popcll(masks[u]);
@@ -1769,14 +1772,14 @@ __global__ __launch_bounds__(kFireMultiThreads) void window_fire_multi_kernel(
   const int y = blockIdx.y;
   const FireWin& w = pack.w[y];
   const size_t o = (size_t)(w0 + y) * st.region;
-  fire_window_body<kFireMultiThreads, U>(keys_g, acc_g, cnt_g, dirty_g, p, w.p0, w.npanes,
-                                         w.wstart, w.wend, st.keys + o, st.vals + o, st.raw + o,
-                                         st.cnt + o, st.win_n + w0 + y, st.region, fsm, blockIdx.x,
-                                         gridDim.x);
+  fire_window_body<kFireMultiThreads, U>(
+      keys_g, acc_g, cnt_g, dirty_g, p, w.p0, w.npanes, w.wstart, w.wend, st.keys + o,
+      st.vals + o, st.raw ? st.raw + o : nullptr, st.cnt ? st.cnt + o : nullptr,
+      st.win_n + w0 + y, st.region, fsm, blockIdx.x, gridDim.x);
 }
 
 // Regions -> contiguous rows in window order; bounds[w] = rows of windows 0..w, *out_n = total.
-__global__ __launch_bounds__(256) void fire_pack_kernel(FireStage st, int k,
+__global__ __launch_bounds__(256) void fire_pack_kernel(FireStage st, int k, int key32,
                                                         uint64_t* __restrict__ out_keys,
                                                         double* __restrict__ out_vals,
                                                         uint64_t* __restrict__ out_raw,
@@ -1800,10 +1803,14 @@ __global__ __launch_bounds__(256) void fire_pack_kernel(FireStage st, int k,
   n = n < st.region ? n : st.region;
   const size_t src = (size_t)w * st.region;
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    out_keys[off + i] = st.keys[src + i];
+    if (key32)
+      reinterpret_cast<uint32_t*>(out_keys)[off + i] =
+          reinterpret_cast<const uint32_t*>(st.keys)[src + i];
+    else
+      out_keys[off + i] = st.keys[src + i];
     out_vals[off + i] = st.vals[src + i];
-    out_raw[off + i] = st.raw[src + i];
-    out_cnt[off + i] = st.cnt[src + i];
+    if (out_raw) out_raw[off + i] = st.raw[src + i];
+    if (out_cnt) out_cnt[off + i] = st.cnt[src + i];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     bounds[w] = off + n;
@@ -3613,7 +3620,7 @@ void window_fire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uint3
     HIP_CHECK(hipGetLastError());
   }
   hipLaunchKernelGGL(fire_pack_kernel, dim3(grid_for(nvisit, 256 * 4, 64), k), dim3(256), 0, s,
-                     st, k, out_keys, out_vals, out_raw, out_cnt, bounds, out_n);
+                     st, k, base.key32, out_keys, out_vals, out_raw, out_cnt, bounds, out_n);
   HIP_CHECK(hipGetLastError());
 }
 

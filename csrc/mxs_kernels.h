@@ -65,6 +65,10 @@ struct FirePlan {
   ExprProg filt;        // predicate on the mapped value (empty = true)
   const uint32_t* list;    // optional: visit only these slots (touched-slot list) ...
   const uint32_t* list_n;  // ... of this length (device counter)
+  // Compact rows (key id + mapped value: 12 bytes instead of 28) for sinks that read nothing
+  // else: keys written as uint32 (dense ids) into the key column's first 4*n bytes; a null
+  // out_raw / out_cnt column is not written.
+  int32_t key32;
 };
 
 // One window of a batched firing (window_fire_many): the per-window fields of FirePlan.

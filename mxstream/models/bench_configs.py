@@ -154,7 +154,7 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
                              device=dev, max_keys=keys, batch_capacity=batch, ooo_bound=5_000,
                              map_prog=E.compile_expr(mbps),
                              filter_prog=E.compile_expr(E.var(E.VAR_MAPPED) < thr),
-                             dense_keys=dense_keys, pipeline=pipeline)
+                             dense_keys=dense_keys, pipeline=pipeline, emit="key_value")
     kt = torch.empty(batch, dtype=torch.int64, device=dev)
     tt = torch.empty_like(kt)
     vt = torch.empty_like(kt)

@@ -232,9 +232,10 @@ def window_agg(recs, counts, plan: AggPlan, keys_g, acc_g, cnt_g, dirty_g, occ, 
 def window_fire(keys_g, acc_g, cnt_g, dirty_g, *, agg: int, npanes: int, ring: int, p0: int,
                 wstart: int, wend: int, only_dirty: bool, map_prog: _expr.Program,
                 filt_prog: _expr.Program, out_keys, out_vals, out_raw, out_cnt, out_n,
-                ablate: int = 0, slot_list=None, slot_list_n=None) -> None:
+                ablate: int = 0, slot_list=None, slot_list_n=None, key32: bool = False) -> None:
     """slot_list/slot_list_n (int32 device tensors): visit only the listed slots (re-firings of
-    late-but-allowed data) instead of sweeping the table."""
+    late-but-allowed data) instead of sweeping the table. Compact rows: out_raw / out_cnt None
+    (not written) and key32 (keys < 2^32 written as uint32 into out_keys' first 4*n bytes)."""
     dev = keys_g.device
     nslots = keys_g.numel()
     cap = out_keys.numel()
@@ -242,21 +243,25 @@ def window_fire(keys_g, acc_g, cnt_g, dirty_g, *, agg: int, npanes: int, ring: i
     _check(cnt_g, torch.int32, ring * nslots, "cnt_g", dev)
     _check(dirty_g, torch.uint8, ring * nslots, "dirty_g", dev)
     _check(out_vals, torch.float64, cap, "out_vals", dev)
-    _check(out_raw, torch.int64, cap, "out_raw", dev)
-    _check(out_cnt, torch.int32, cap, "out_cnt", dev)
+    if out_raw is not None:
+        _check(out_raw, torch.int64, cap, "out_raw", dev)
+    if out_cnt is not None:
+        _check(out_cnt, torch.int32, cap, "out_cnt", dev)
     _check(out_n, torch.int32, 1, "out_n", dev)
     if npanes > ring:
         raise ValueError("window spans more panes than the ring")
     plan = dict(agg=agg, npanes=npanes, ring=ring, only_dirty=int(only_dirty), nslots=nslots,
                 p0=p0, wstart=float(wstart), wend=float(wend), out_cap=cap,
-                map=tuple(map_prog.as_args()), filt=tuple(filt_prog.as_args()), ablate=ablate)
+                map=tuple(map_prog.as_args()), filt=tuple(filt_prog.as_args()), ablate=ablate,
+                key32=int(key32))
     if slot_list is not None:
         _check(slot_list, torch.int32, 0, "slot_list", dev)
         _check(slot_list_n, torch.int32, 1, "slot_list_n", dev)
         plan.update(list=_p(slot_list), list_n=_p(slot_list_n))
     m = load()
     args = (_p(keys_g), _p(acc_g), _p(cnt_g), _p(dirty_g), plan, _p(out_keys), _p(out_vals),
-            _p(out_raw), _p(out_cnt), _p(out_n))
+            0 if out_raw is None else _p(out_raw), 0 if out_cnt is None else _p(out_cnt),
+            _p(out_n))
     if _is_gpu(keys_g):
         m.gpu_window_fire(*args, _stream(keys_g))
     else:

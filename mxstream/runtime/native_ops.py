@@ -272,8 +272,17 @@ class NativeWindowOp(_ColumnInput, Operator):
             time_mode="event" if event else "processing", external_watermark=True,
             side_output_late=self.late_tag is not None, clock=self.ctx.clock,
             dense_keys=dense, map_prog=self.map_prog or E.EMPTY,
-            filter_prog=self.filter_prog or E.EMPTY)
+            filter_prog=self.filter_prog or E.EMPTY,
+            emit="key_value" if self._key_value_only() else "full")
         return True
+
+    def _key_value_only(self) -> bool:
+        """The output tuple reads only the key and the mapped value (no raw result, count or
+        keep-first template field): fired rows can be 12-byte (key id, value) rows."""
+        if self.fused_scalar:
+            return True
+        return self.fused_layout is not None and all(
+            j < 0 or (j == self.key_pos and j != self.val_pos) for j in self.fused_layout)
 
     def _to_fallback(self):
         self.fallback = self.fallback_factory()
@@ -508,8 +517,10 @@ class NativeWindowOp(_ColumnInput, Operator):
         P, MP = self.ctx.parallelism, self.ctx.max_parallelism
         for fr in fired:
             ts = fr.window_end - 1
-            for k, val, raw, cnt in zip(fr.keys.tolist(), fr.values.tolist(), fr.raw.tolist(),
-                                        fr.counts.tolist()):
+            n = len(fr.keys)
+            raws = fr.raw.tolist() if fr.raw is not None else [0] * n
+            cnts = fr.counts.tolist() if fr.counts is not None else [0] * n
+            for k, val, raw, cnt in zip(fr.keys.tolist(), fr.values.tolist(), raws, cnts):
                 key_obj = self.dict.get(k) if self.str_keys else k
                 if self.kind in ("sum", "min", "max"):
                     res = float(np.int64(raw).view(np.float64)) if self.is_float else int(raw)

@@ -186,10 +186,11 @@ def combine_partials(agg: int, acc: torch.Tensor, inv: torch.Tensor, n: int) -> 
 class FireResult:
     window_start: int
     window_end: int
-    keys: np.ndarray        # uint64 key ids (dictionary ids for string keys)
+    keys: np.ndarray        # uint64 key ids (dictionary ids for string keys; uint32 ids for
+                            # emit="key_value")
     values: np.ndarray      # float64 (result after the fused map epilogue)
-    raw: np.ndarray         # int64 raw accumulator (exact integer sums / f64 bit pattern)
-    counts: np.ndarray      # int32 element counts
+    raw: np.ndarray | None  # int64 raw accumulator (exact integer sums / f64 bit pattern)
+    counts: np.ndarray | None  # int32 element counts (raw / counts: None for emit="key_value")
     refire: bool = False
 
 
@@ -265,14 +266,21 @@ class KeyedWindowOperator:
                  pipeline: bool | str | None = None, exchange: str = "auto",
                  idle_timeout_steps: int | None = None, deterministic: bool = False,
                  spill: bool = False, spill_load: float = 0.8, spill_check_steps: int = 8,
-                 spill_keep_panes: int | None = None):
+                 spill_keep_panes: int | None = None, emit: str = "full"):
         """deterministic: f64 sums/averages accumulate each step's per-slot sum in 128-bit fixed
         point (order-independent integer adds, one rounding per slot and step), so results are
         bit-identical between runs, between the GPU and the C++ twin, and independent of the
         number of virtual ranks' exchange order; values must satisfy |x| < 2^63 and are
         truncated to multiples of 2^-64. The sender-side combiner is off in
-        this mode (raw records are exchanged). Integer aggregates are always exact."""
+        this mode (raw records are exchanged). Integer aggregates are always exact.
+
+        emit: "full" fired rows carry (key, mapped value, raw accumulator, count); "key_value"
+        only (key id, mapped value) -- 12 bytes a row instead of 28 from the fire kernel to the
+        host (dense keys; FireResult.raw / counts are None) for sinks that read nothing else."""
         self.device = K.resolve_device(device)
+        if emit not in ("full", "key_value"):
+            raise ValueError("emit must be 'full' or 'key_value'")
+        self.emit = emit
         self.deterministic = bool(deterministic) and agg in (K.AGG_SUM_F64, K.AGG_AVG_F64)
         # spill: host-DRAM tier for hashed keys (runtime/window_spill.py). Every
         # `spill_check_steps` steps, a sub-table above `spill_load` of its slots triggers
@@ -1126,23 +1134,38 @@ class KeyedWindowOperator:
         if self.host_tier is not None and self.host_tier.overlaps(p0, p1):
             return self._fire_window_tiered(s, p0, p1, only_dirty)
         self.out_n.zero_()
+        kv = self._key_value_rows()
         K.window_fire(self.keys_g, self.acc_g, self.cnt_g, self.dirty_g, agg=self.agg,
                       npanes=p1 - p0 + 1, ring=self.ring, p0=p0, wstart=s,
                       wend=s + self.size, only_dirty=only_dirty, map_prog=self.map_prog,
                       filt_prog=self.filter_prog, out_keys=self.out_keys, out_vals=self.out_vals,
-                      out_raw=self.out_raw, out_cnt=self.out_cnt, out_n=self.out_n,
-                      slot_list=self.dlist if only_dirty else None,
-                      slot_list_n=self.dlist_n if only_dirty else None)
+                      out_raw=None if kv else self.out_raw, out_cnt=None if kv else self.out_cnt,
+                      out_n=self.out_n, slot_list=self.dlist if only_dirty else None,
+                      slot_list_n=self.dlist_n if only_dirty else None, key32=kv)
         n = self._fired_count()
         self.metrics.num_fires += 1
         if n == 0:
             return None
         n = min(n, self.out_keys.numel())
         self.metrics.num_records_out += n
+        host = self._rows_to_host(n, kv)
+        return FireResult(s, s + self.size, host[0], host[1], host[2], host[3],
+                          refire=only_dirty)
+
+    def _key_value_rows(self) -> bool:
+        """Compact fired rows (emit="key_value"): dense key ids fit 32 bits."""
+        return self.emit == "key_value" and bool(self.dense_bits)
+
+    def _rows_to_host(self, n: int, kv: bool) -> list:
+        """First n fired rows as host arrays: keys (uint64, or uint32 ids for compact rows),
+        values, raw, counts (None, None for compact rows)."""
+        if kv:
+            keys, vals = to_host_arrays([self.out_keys.view(torch.int32), self.out_vals], n,
+                                        self._pool)
+            return [keys.view(np.uint32), vals, None, None]
         host = to_host_arrays([self.out_keys, self.out_vals, self.out_raw, self.out_cnt], n,
                               self._pool)
-        return FireResult(s, s + self.size, host[0].view(np.uint64), host[1], host[2], host[3],
-                          refire=only_dirty)
+        return [host[0].view(np.uint64), host[1], host[2], host[3]]
 
     def _fire_window_tiered(self, s: int, p0: int, p1: int, only_dirty: bool) -> FireResult | None:
         """Window [s, s + size) with part of its state in the host tier: the device fires
@@ -1295,9 +1318,11 @@ class KeyedWindowOperator:
         host round trips per window."""
         out: list[FireResult] = []
         cuda = self.device.type == "cuda"
+        kv = self._key_value_rows()
         plan = dict(agg=self.agg, npanes=1, ring=self.ring, only_dirty=int(only_dirty),
                     nslots=self.nslots, p0=0, wstart=0.0, wend=0.0, out_cap=self.out_keys.numel(),
-                    map=tuple(self.map_prog.as_args()), filt=tuple(self.filter_prog.as_args()))
+                    map=tuple(self.map_prog.as_args()), filt=tuple(self.filter_prog.as_args()),
+                    key32=int(kv))
         if only_dirty and self.dlist is not None:
             plan.update(list=self.dlist.data_ptr(), list_n=self.dlist_n.data_ptr())
         wins = []
@@ -1307,7 +1332,7 @@ class KeyedWindowOperator:
             if p1 >= p0:
                 wins.append((s, (p0, p1 - p0 + 1, float(s), float(s + self.size))))
         stream = torch.cuda.current_stream(self.device).cuda_stream if cuda else 0
-        stage = self._fire_stage() if cuda else None
+        stage = self._fire_stage(kv) if cuda else None
         g = self._fire_group
         for i in range(0, len(wins), g):
             chunk = wins[i:i + g]
@@ -1316,8 +1341,9 @@ class KeyedWindowOperator:
             self._m.window_fire_many(cuda, self.keys_g.data_ptr(), self.acc_g.data_ptr(),
                                      self.cnt_g.data_ptr(), self.dirty_g.data_ptr(), plan,
                                      [w for _, w in chunk], self.out_keys.data_ptr(),
-                                     self.out_vals.data_ptr(), self.out_raw.data_ptr(),
-                                     self.out_cnt.data_ptr(), self.out_n.data_ptr(),
+                                     self.out_vals.data_ptr(),
+                                     0 if kv else self.out_raw.data_ptr(),
+                                     0 if kv else self.out_cnt.data_ptr(), self.out_n.data_ptr(),
                                      self.fire_bounds.data_ptr(), stream, stage)
             bounds = self._fired_bounds(len(chunk))
             self.metrics.num_fires += len(chunk)
@@ -1325,19 +1351,18 @@ class KeyedWindowOperator:
             if n == 0:
                 continue
             self.metrics.num_records_out += n
-            host = to_host_arrays([self.out_keys, self.out_vals, self.out_raw, self.out_cnt], n,
-                                  self._pool)
-            keys = host[0].view(np.uint64)
+            host = self._rows_to_host(n, kv)
             lo = 0
             for (s, _), hi in zip(chunk, bounds):
                 hi = min(hi, n)
                 if hi > lo:
-                    out.append(FireResult(s, s + self.size, keys[lo:hi], host[1][lo:hi],
-                                          host[2][lo:hi], host[3][lo:hi], refire=only_dirty))
+                    out.append(FireResult(s, s + self.size, host[0][lo:hi], host[1][lo:hi],
+                                          None if kv else host[2][lo:hi],
+                                          None if kv else host[3][lo:hi], refire=only_dirty))
                 lo = hi
         return out
 
-    def _fire_stage(self) -> tuple:
+    def _fire_stage(self, kv: bool = False) -> tuple:
         """Per-window staging regions of the GPU batched firing (window_fire_many: window w of
         a group writes rows [w * nslots, (w + 1) * nslots) at its own counter, a pack kernel
         then lays the group out in window order into out_*). Allocated on first use; sized like
@@ -1351,7 +1376,10 @@ class KeyedWindowOperator:
                   torch.empty(n, dtype=torch.int32, device=dev),
                   torch.empty(self._fire_group, dtype=torch.int32, device=dev))
             self._stage_cols = st
-        return tuple(t.data_ptr() for t in st) + (self.nslots,)
+        ptrs = [t.data_ptr() for t in st]
+        if kv:  # compact rows: no raw / count columns
+            ptrs[2] = ptrs[3] = 0
+        return tuple(ptrs) + (self.nslots,)
 
     def _fire_ready(self, wm: int) -> list[FireResult]:
         out: list[FireResult] = []

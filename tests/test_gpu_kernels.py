@@ -443,3 +443,34 @@ def test_segment_median_select_gpu_matches_cpu(gpu_device):
     c = K.segment_median(heads, ordb, sorted_values=False)
     ref = [np.median(vals[a:a + n]) for a, n in zip(heads.tolist(), lens)]
     assert torch.equal(g, c) and np.allclose(c.numpy(), ref, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("emit", ["full", "key_value"])
+def test_batched_fire_gpu_equals_cpu(gpu_device, emit):
+    """Watermark jumps over many slides fire a group of windows in one window_fire_many call
+    (blockIdx.y = window, staging regions, pack kernel): the rows per window -- full 28-byte or
+    compact 12-byte (uint32 key id + value) -- equal the C++ twin's, window by window."""
+    from mxstream.ops import expr as E
+
+    prog = E.compile_expr(E.var(E.VAR_RESULT) * 0.25)
+
+    def run(dev):
+        op = KeyedWindowOperator(size=60_000, slide=1_000, lateness=0, agg=K.AGG_SUM_I64,
+                                 device=dev, max_keys=4096, batch_capacity=100_000,
+                                 ooo_bound=100, dense_keys=True, map_prog=prog, emit=emit)
+        rows = []
+        for step in range(6):
+            k = torch.empty(100_000, dtype=torch.int64, device=dev)
+            t = torch.empty_like(k)
+            v = torch.empty_like(k)
+            # 30 s of event time per step: every step fires ~30 windows at once
+            K.gen_events(k, t, v, seed=23, stream_id=0, idx0=step * 100_000, nkeys=3000,
+                         ts_base=step * 30_000, ts_span=30_000, disorder=50, val_lo=0,
+                         val_span=1000)
+            rows += op.process(k, t, v)
+        rows += op.finish()
+        return [(r.window_start, sorted(zip(r.keys.tolist(), r.values.tolist()))) for r in rows]
+
+    g, c = run(gpu_device), run("cpu")
+    assert len(c) > 100
+    assert g == c

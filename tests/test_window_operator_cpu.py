@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 import torch
 
+from mxstream.ops import expr as E
 from mxstream.ops import kernels as K
 from mxstream.oracle.flink import BoundedOutOfOrderness, WindowOracle
 from mxstream.runtime.window_operator import KeyedWindowOperator
@@ -524,3 +525,36 @@ def test_async_snapshot_with_spill_is_isolated_from_later_evictions():
         return df
 
     assert canon(frozen) == canon(sync)
+
+
+@pytest.mark.parametrize("size,slide,lateness", [(2000, 2000, 0), (6000, 1000, 3000)])
+def test_key_value_rows_equal_full_rows(size, slide, lateness):
+    """emit="key_value" (12-byte fired rows: uint32 key id + mapped value) fires the same
+    (window, key, value) rows as the full 28-byte rows, single and batched firings alike."""
+    prog = E.compile_expr(E.var(E.VAR_RESULT) * 0.5)
+
+    def run(emit):
+        op = KeyedWindowOperator(size=size, slide=slide, lateness=lateness, agg=K.AGG_SUM_I64,
+                                 device="cpu", max_keys=3000, batch_capacity=5000, ooo_bound=300,
+                                 dense_keys=True, cap_log2=8, map_prog=prog, emit=emit)
+        out = []
+        for step in range(9):
+            k = torch.empty(5000, dtype=torch.int64)
+            t = torch.empty_like(k)
+            v = torch.empty_like(k)
+            K.gen_events(k, t, v, seed=17, stream_id=0, idx0=step * 5000, nkeys=3000,
+                         ts_base=step * 1000 + (4000 if step == 5 else 0), ts_span=1000,
+                         disorder=400, val_lo=0, val_span=1000)
+            if step > 3:
+                t[:200] -= 1500
+            out += op.process(k, t, v)
+        out += op.finish()
+        if emit == "key_value":
+            assert all(r.raw is None and r.counts is None and r.keys.dtype == np.uint32
+                       for r in out)
+        return sorted((r.window_start, r.refire, int(a), float(b))
+                      for r in out for a, b in zip(r.keys, r.values))
+
+    full = run("full")
+    assert len(full) > 1000
+    assert run("key_value") == full
