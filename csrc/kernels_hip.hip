@@ -1804,8 +1804,8 @@ __global__ __launch_bounds__(256) void fire_pack_kernel(FireStage st, int k, int
   const size_t src = (size_t)w * st.region;
   for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
     if (key32)
-      reinterpret_cast<uint32_t*>(out_keys)[off + i] =
-          reinterpret_cast<const uint32_t*>(st.keys)[src + i];
+      reinterpret_cast<uint32_t*>(out_keys)[off + i] =  // region w's compact keys start at
+          reinterpret_cast<const uint32_t*>(st.keys + src)[i];  // its first 64-bit word
     else
       out_keys[off + i] = st.keys[src + i];
     out_vals[off + i] = st.vals[src + i];
