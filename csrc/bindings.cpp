@@ -513,6 +513,18 @@ PYBIND11_MODULE(_mxs_native, m) {
                         P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_out), P<Rec>(host_recs),
                         P<uint32_t>(n_host), host_cap, P<uint32_t>(n_ins), tbits, stream);
   });
+  m.def("gpu_session_lookup_sort", [](intptr_t recs, intptr_t counts, int nsrc, int nsub,
+                                      uint32_t bcap, int cap_log2, intptr_t keys_g,
+                                      intptr_t spill_set, uint32_t spill_mask, int spill_any,
+                                      intptr_t sk, intptr_t vals, intptr_t n_out,
+                                      intptr_t host_recs, intptr_t n_host, uint32_t host_cap,
+                                      intptr_t n_ins, int tbits, intptr_t stream) {
+    return gpu::session_lookup_sort(P<Rec>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2,
+                                    P<uint64_t>(keys_g), P<uint64_t>(spill_set), spill_mask,
+                                    spill_any, P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_out),
+                                    P<Rec>(host_recs), P<uint32_t>(n_host), host_cap,
+                                    P<uint32_t>(n_ins), tbits, stream);
+  });
   m.def("gpu_session_heads", [](intptr_t sk, intptr_t n_in, int64_t n_cap, intptr_t heads,
                                 intptr_t n_heads, intptr_t stream) {
     gpu::session_heads(P<int64_t>(sk), P<uint32_t>(n_in), n_cap, P<uint32_t>(heads),

@@ -2498,6 +2498,171 @@ __global__ __launch_bounds__(kSessLookupBlock) void session_lookup_lds_kernel(
   if (threadIdx.x == 0 && n_inserted && lins) atomicAdd(n_inserted, lins);
 }
 
+// Fused lookup + LDS-staged segmented sort (the session fold's replacement for a device-wide
+// radix sort). Records arrive bucketed by sub-table, so the global (slot, ts) order is just every
+// sub-table's records in (local slot, ts) order: one workgroup per sub-table
+//   1. looks its records up in the LDS-staged slot table (insert / divert exactly as
+//      session_lookup_lds) and keeps (local slot << 32 | t) per record in LDS, in arrival order;
+//   2. writes the table back, then counts records per local slot (u16 LDS histogram in the
+//      table's space), scans the counts and scatters record indices into slot segments;
+//   3. ranks every record inside its slot segment by (t, arrival index) -- segments are short
+//      (a few records per key and step), a hot key's long segment costs O(len^2) LDS reads in
+//      its own workgroup only -- and writes (slot << tbits | t, value) at
+//      block base + segment start + rank.
+// The output equals a stable sort of session_lookup's keys with the holes removed, so
+// session_merge runs on it unchanged. LDS: max(cap*8, cap*2 + m*2) + m*8 bytes for m records.
+constexpr int kSessSortBlock = 1024;
+
+__global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
+    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
+    uint32_t bucket_cap, int cap_log2, uint64_t* __restrict__ keys_g,
+    uint64_t* __restrict__ spill_set, uint32_t spill_mask, int32_t spill_any,
+    int64_t* __restrict__ sort_out, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
+    Rec* __restrict__ host_recs, uint32_t* __restrict__ n_host, uint32_t host_cap,
+    uint32_t* __restrict__ n_inserted, int tbits, uint32_t m_cap) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t slds[];
+  __shared__ uint32_t s_base, s_lins, s_kept, s_m;
+  __shared__ uint32_t s_src_off[65];
+  const int sub = blockIdx.x;
+  const uint32_t cap = 1u << cap_log2, mask = cap - 1;
+  const uint32_t regA = (cap * 8 > cap * 2 + m_cap * 2 ? cap * 8 : cap * 2 + m_cap * 2);
+  uint64_t* lkeys = slds;                                              // phase 1: slot table
+  uint16_t* cur = reinterpret_cast<uint16_t*>(slds);                   // phase 2: per-slot cursors
+  // (u16 cursors, two per 32-bit word: the atomics add 1 << 16 * (slot & 1) to the word; a
+  // block holds < 65536 records, so a half never carries into the other)
+  uint32_t* cur32 = reinterpret_cast<uint32_t*>(slds);
+  uint16_t* idxl = cur + cap;                                          // phase 2: slot segments
+  uint64_t* rk = slds + regA / 8;                                      // (slot << 32 | t) per record
+  uint64_t* gkeys = keys_g + ((size_t)sub << cap_log2);
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) lkeys[i] = gkeys[i];
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int src = 0; src < nsrc; ++src) {
+      s_src_off[src] = tot;
+      const uint32_t c = counts[src * nsub + sub];
+      tot += c < bucket_cap ? c : bucket_cap;
+    }
+    s_src_off[nsrc] = tot;
+    s_m = tot;
+    s_lins = 0;
+    s_kept = 0;
+  }
+  __syncthreads();
+  const uint32_t m = s_m;  // the launcher sized m_cap >= nsrc * bucket_cap >= m
+  // Phase 1: lookup / insert / divert; rk[i] = (local slot << 32 | t) or ~0 (not folded here).
+  uint32_t kept = 0;
+  for (int src = 0; src < nsrc; ++src) {
+    const int b = src * nsub + sub;
+    const uint32_t c = s_src_off[src + 1] - s_src_off[src];
+    const Rec* seg = recs + (size_t)b * bucket_cap;
+    for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
+      const Rec r = seg[e];
+      uint64_t v = ~0ull;
+      if (r.t != 0xFFFFFFFFu) {
+        uint32_t sl = sess_find<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask);
+        bool to_host = sl == kNoSlot && spill_any && set_contains(spill_set, spill_mask, r.key);
+        if (!to_host && sl == kNoSlot) {
+          sl = sess_probe_insert<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask, &s_lins);
+          if (sl == kNoSlot) {  // sub-table full: the key lives in host DRAM from now on
+            to_host = true;
+            set_insert(spill_set, spill_mask, r.key);
+          }
+        }
+        if (to_host) {
+          const uint32_t q = atomicAdd(n_host, 1u);
+          if (q < host_cap) host_recs[q] = r;
+        } else {
+          v = ((uint64_t)sl << 32) | r.t;
+          ++kept;
+        }
+      }
+      rk[s_src_off[src] + e] = v;
+    }
+  }
+  if (kept) atomicAdd(&s_kept, kept);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) gkeys[i] = lkeys[i];
+  if (threadIdx.x == 0) {
+    if (n_inserted && s_lins) atomicAdd(n_inserted, s_lins);
+    s_base = s_kept ? atomicAdd(n_out, s_kept) : 0u;
+  }
+  __syncthreads();
+  // Phase 2: per-slot counts -> exclusive offsets -> segments of record indices.
+  for (uint32_t i = threadIdx.x; i < cap / 2; i += blockDim.x) cur32[i] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+    const uint64_t v = rk[i];
+    if (v != ~0ull) {
+      const uint32_t sl = (uint32_t)(v >> 32);
+      atomicAdd(&cur32[sl >> 1], 1u << ((sl & 1u) * 16));
+    }
+  }
+  __syncthreads();
+  // Block-wide exclusive scan of cap (<= 4096) u16 counts: each thread sums a run of cap/T,
+  // wave prefix with shuffles, wave totals through LDS.
+  {
+    __shared__ uint32_t s_wave[kSessSortBlock / 64];
+    const uint32_t per = (cap + kSessSortBlock - 1) / kSessSortBlock;
+    const uint32_t lo = threadIdx.x * per, hi = lo + per < cap ? lo + per : cap;
+    uint32_t run = 0;
+    for (uint32_t i = lo; i < hi; ++i) run += cur[i];
+    uint32_t incl = run;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d);
+      if (lane_id() >= d) incl += y;
+    }
+    const int w = threadIdx.x >> 6;
+    if (lane_id() == 63) s_wave[w] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int i = 0; i < kSessSortBlock / 64; ++i) {
+        const uint32_t c = s_wave[i];
+        s_wave[i] = t;
+        t += c;
+      }
+    }
+    __syncthreads();
+    uint32_t o = s_wave[w] + incl - run;
+    for (uint32_t i = lo; i < hi; ++i) {
+      const uint32_t c = cur[i];
+      cur[i] = (uint16_t)o;
+      o += c;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+    const uint64_t v = rk[i];
+    if (v != ~0ull) {
+      const uint32_t sl = (uint32_t)(v >> 32), sh = (sl & 1u) * 16;
+      const uint32_t pos = (atomicAdd(&cur32[sl >> 1], 1u << sh) >> sh) & 0xFFFFu;
+      idxl[pos] = (uint16_t)i;
+    }
+  }
+  __syncthreads();
+  // Phase 3: rank inside the slot segment [end(slot - 1), end(slot)) by (t, arrival index).
+  const uint64_t sub_slot0 = (uint64_t)sub << cap_log2;
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+    const uint64_t v = rk[i];
+    if (v == ~0ull) continue;
+    const uint32_t sl = (uint32_t)(v >> 32), t = (uint32_t)v;
+    const uint32_t end = cur[sl], start = sl ? cur[sl - 1] : 0u;
+    uint32_t rank = 0;
+    for (uint32_t q = start; q < end; ++q) {
+      const uint32_t j = idxl[q];
+      const uint32_t tj = (uint32_t)rk[j];
+      rank += (tj < t || (tj == t && j < i)) ? 1u : 0u;
+    }
+    // arrival index i -> (source bucket, position) for the value
+    int src = 0;
+    while (src + 1 < nsrc && i >= s_src_off[src + 1]) ++src;
+    const Rec& r = recs[(size_t)(src * nsub + sub) * bucket_cap + (i - s_src_off[src])];
+    const uint32_t out = s_base + start + rank;
+    sort_out[out] = (int64_t)(((sub_slot0 | sl) << tbits) | t);
+    vals_out[out] = r.val;
+  }
+}
+
 __global__ __launch_bounds__(256) void session_heads_kernel(const int64_t* __restrict__ sk,
                                                             const uint32_t* __restrict__ n_in,
                                                             uint32_t* __restrict__ heads,
@@ -3867,6 +4032,38 @@ void session_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
                        host_cap, n_inserted, tbits);
   }
   HIP_CHECK(hipGetLastError());
+}
+
+size_t session_lookup_sort_lds(int cap_log2, uint32_t m_cap) {
+  const size_t cap = (size_t)1 << cap_log2;
+  const size_t a = cap * 8 > cap * 2 + (size_t)m_cap * 2 ? cap * 8 : cap * 2 + (size_t)m_cap * 2;
+  return a + (size_t)m_cap * 8;
+}
+
+bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
+                         uint32_t bcap, int cap_log2, uint64_t* keys_g, uint64_t* spill_set,
+                         uint32_t spill_mask, int spill_any, int64_t* sort_out, uint64_t* vals_out,
+                         uint32_t* n_out, Rec* host_recs, uint32_t* n_host, uint32_t host_cap,
+                         uint32_t* n_inserted, int tbits, intptr_t stream) {
+  if (nsrc * nsub <= 0) return true;
+  if (tbits < 1 || tbits > 32) throw std::invalid_argument("session_lookup_sort: tbits out of range");
+  const uint64_t m64 = (uint64_t)nsrc * bcap;
+  if (nsrc > 64 || cap_log2 > kSessLookupLdsMaxLog2 || m64 > 65535) return false;
+  const uint32_t m_cap = ((uint32_t)m64 + 7) & ~7u;
+  const size_t lds = session_lookup_sort_lds(cap_log2, m_cap);
+  if (lds > 156 * 1024) return false;  // static LDS (offsets, counters) takes the rest
+  static bool attr = false;
+  if (!attr) {
+    HIP_CHECK(hipFuncSetAttribute((const void*)session_lookup_sort_kernel,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr = true;
+  }
+  hipLaunchKernelGGL(session_lookup_sort_kernel, dim3(nsub), dim3(kSessSortBlock), lds,
+                     (hipStream_t)stream, recs, counts, nsrc, nsub, bcap, cap_log2, keys_g,
+                     spill_set, spill_mask, spill_any, sort_out, vals_out, n_out, host_recs,
+                     n_host, host_cap, n_inserted, tbits, m_cap);
+  HIP_CHECK(hipGetLastError());
+  return true;
 }
 
 void session_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,

@@ -243,6 +243,14 @@ void session_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
                     int spill_any, int64_t* sk, uint64_t* vals, uint32_t* n_out, Rec* host_recs,
                     uint32_t* n_host, uint32_t host_cap, uint32_t* n_inserted, int tbits,
                     intptr_t stream);
+// Fused lookup + per-sub-table LDS segmented sort: writes the kept records in (slot, ts) order
+// (the stable sort of session_lookup's keys without holes). Returns false (nothing launched)
+// when a sub-table's records cannot be staged in LDS (then: session_lookup + a device sort).
+bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
+                         uint32_t bcap, int cap_log2, uint64_t* keys_g, uint64_t* spill_set,
+                         uint32_t spill_mask, int spill_any, int64_t* sort_out, uint64_t* vals_out,
+                         uint32_t* n_out, Rec* host_recs, uint32_t* n_host, uint32_t host_cap,
+                         uint32_t* n_inserted, int tbits, intptr_t stream);
 void session_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
                    uint32_t* n_heads, intptr_t stream);
 void session_merge(const int64_t* sk, const uint64_t* vals, const uint32_t* n_in,

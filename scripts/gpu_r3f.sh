@@ -7,6 +7,8 @@ export TMPDIR=/tmp
 export PYTHONPATH=$GRAFT_REPO_ROOT
 timeout -k 10 300 python -u -m mxstream.models.bench_configs --config 5 > gpurun_out/r3f_cfg5.json 2> gpurun_out/r3f_cfg5.err || { tail -30 gpurun_out/r3f_cfg5.err; exit 1; }
 cat gpurun_out/r3f_cfg5.json
+MXS_SESSION_SORT=radix timeout -k 10 300 python -u -m mxstream.models.bench_configs --config 5 > gpurun_out/r3f_cfg5_radix.json 2> gpurun_out/r3f_cfg5.err || { tail -30 gpurun_out/r3f_cfg5.err; exit 1; }
+cat gpurun_out/r3f_cfg5_radix.json
 timeout -k 10 300 python -u -m mxstream.models.bench_configs --config 5 --revisit 0.01 > gpurun_out/r3f_cfg5r.json 2> gpurun_out/r3f_cfg5r.err || { tail -30 gpurun_out/r3f_cfg5r.err; exit 1; }
 cat gpurun_out/r3f_cfg5r.json
 timeout -k 10 300 python -u -m mxstream.models.bench_configs --config 4 > gpurun_out/r3f_cfg4.json 2> gpurun_out/r3f_cfg4.err || { tail -30 gpurun_out/r3f_cfg4.err; exit 1; }
