@@ -4054,8 +4054,9 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
   if (lds > 156 * 1024) return false;  // static LDS (offsets, counters) takes the rest
   static bool attr = false;
   if (!attr) {
+    // dynamic + the kernel's static LDS (segment offsets, scan scratch) must stay <= 160 KiB
     HIP_CHECK(hipFuncSetAttribute((const void*)session_lookup_sort_kernel,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024));
     attr = true;
   }
   hipLaunchKernelGGL(session_lookup_sort_kernel, dim3(nsub), dim3(kSessSortBlock), lds,
