@@ -410,7 +410,8 @@ class KeyedSessionOperator:
             # stays on the device (the merge reads it); the host learns it with the counters.
             m.gpu_session_merge(self.sort_out.data_ptr(), self.vals_out.data_ptr(),
                                 c[0:1].data_ptr(), self.heads.data_ptr(), c[1:2].data_ptr(),
-                                nsrc * bucket_cap, tbits, self.gap, self.lateness, wm, tbase,
+                                nsrc * self.nsub * bucket_cap, tbits, self.gap, self.lateness,
+                                wm, tbase,
                                 self.agg, self.cap_log2, self.nslots, self.sess.data_ptr(),
                                 self.slot_due.data_ptr(), self.slot_last.data_ptr(),
                                 self.late_cnt.data_ptr(), self.ovf_slots.data_ptr(),
