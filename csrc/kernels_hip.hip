@@ -1657,15 +1657,22 @@ __device__ __forceinline__ void fire_window_body(
             const uint32_t c = cnt_g[(size_t)((p0 + j) & (p.ring - 1)) * nslots + s];
             cg[q] = j0 + q < npanes ? c : 0u;
           }
+          // The group's accumulator loads are issued together as well (predicated on a
+          // non-zero count), then combined: one memory round trip per group, not per pane.
+          uint64_t ag[kFireP];
+#pragma unroll
+          for (int q = 0; q < kFireP; ++q) {
+            const size_t gi = (size_t)((p0 + j0 + q) & (p.ring - 1)) * nslots + s;
+            ag[q] = cg[q] ? acc_g[gi] : 0ull;
+          }
 #pragma unroll
           for (int q = 0; q < kFireP; ++q) {
             if (!cg[q]) continue;
-            const size_t gi = (size_t)((p0 + j0 + q) & (p.ring - 1)) * nslots + s;
-            const uint64_t a = acc_g[gi];
-            acc[u] = have ? agg_combine(p.agg, acc[u], a) : a;
+            acc[u] = have ? agg_combine(p.agg, acc[u], ag[q]) : ag[q];
             have = true;
             cnt[u] += cg[q];
-            if (p.only_dirty && dirty_g[gi]) dirty = true;
+            if (p.only_dirty && dirty_g[(size_t)((p0 + j0 + q) & (p.ring - 1)) * nslots + s])
+              dirty = true;
           }
         }
         if (cnt[u] && dirty) {
