@@ -729,6 +729,12 @@ PYBIND11_MODULE(_mxs_native, m) {
     gpu::session_slot_insert(P<uint64_t>(keys), n, nsub_log2, cap_log2, P<uint64_t>(keys_g),
                              P<int64_t>(slots), P<uint32_t>(ins), stream);
   });
+  m.def("gpu_session_promote", [](intptr_t slots, intptr_t rec, intptr_t last, int64_t n,
+                                  intptr_t sess, intptr_t due, intptr_t slast, intptr_t n_bad,
+                                  intptr_t stream) {
+    gpu::session_promote(P<int64_t>(slots), P<int64_t>(rec), P<int64_t>(last), n, P<int64_t>(sess),
+                         P<int64_t>(due), P<int64_t>(slast), P<uint32_t>(n_bad), stream);
+  });
   m.def("gpu_set_rehash", [](intptr_t old, int64_t n_old, intptr_t neu, uint32_t new_mask,
                              intptr_t stream) {
     gpu::set_rehash(P<uint64_t>(old), n_old, P<uint64_t>(neu), new_mask, stream);

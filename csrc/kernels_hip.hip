@@ -3264,6 +3264,27 @@ __global__ __launch_bounds__(256) void session_slot_insert_kernel(
   }
 }
 
+// Promoted keys' slot records (host store -> HBM): rec rows [key][kSess][4] go to the slots the
+// insert found; a key without a slot (sub-table full) is counted in n_bad and stays on the host.
+__global__ __launch_bounds__(256) void session_promote_kernel(
+    const int64_t* __restrict__ slots, const int64_t* __restrict__ rec,
+    const int64_t* __restrict__ last, int64_t n, int64_t* __restrict__ sess,
+    int64_t* __restrict__ slot_due, int64_t* __restrict__ slot_last, uint32_t* __restrict__ n_bad) {
+  constexpr int W = kSess * 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = slots[i];
+    if (s < 0) {
+      atomicAdd(n_bad, 1u);
+      continue;
+    }
+#pragma unroll
+    for (int j = 0; j < W; ++j) sess[s * W + j] = rec[i * W + j];
+    slot_due[s] = INT64_MIN;  // the next fire sweep recomputes the due time
+    slot_last[s] = last[i];
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Median of `process` windows (ComputeCpuMiddle.java:36-47): elements are radix-
 // sorted by (key, order-preserving value bits); one thread per key segment reads the middle
@@ -4170,6 +4191,15 @@ void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
   if (n <= 0) return;
   hipLaunchKernelGGL(table_insert_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, keys, n, nsub_log2, cap_log2, keys_g, slots);
+  HIP_CHECK(hipGetLastError());
+}
+
+void session_promote(const int64_t* slots, const int64_t* rec, const int64_t* last, int64_t n,
+                     int64_t* sess, int64_t* slot_due, int64_t* slot_last, uint32_t* n_bad,
+                     intptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(session_promote_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, slots, rec, last, n, sess, slot_due, slot_last, n_bad);
   HIP_CHECK(hipGetLastError());
 }
 

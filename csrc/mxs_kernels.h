@@ -293,6 +293,9 @@ void segment_median_select(const int64_t* heads, int64_t nseg, int64_t total,
                            const uint64_t* ord, double* out, intptr_t stream);
 void set_erase(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, intptr_t stream);
 // Insert keys into the session slot table (tombstone reuse); slot -1 when a sub-table is full.
+void session_promote(const int64_t* slots, const int64_t* rec, const int64_t* last, int64_t n,
+                     int64_t* sess, int64_t* slot_due, int64_t* slot_last, uint32_t* n_bad,
+                     intptr_t stream);
 void session_slot_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2,
                          uint64_t* keys_g, int64_t* slots, uint32_t* inserted, intptr_t stream);
 // Re-insert the live keys of a spill set into a fresh (empty-filled) set of new_mask + 1 entries.

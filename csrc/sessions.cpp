@@ -27,6 +27,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
+#include <climits>
+
 #include "session_store.h"
 
 namespace py = pybind11;
@@ -88,6 +91,41 @@ class SessionStore : public sess::SessionCore {
     d["moved"] = to_np(moved);
     return d;
   }
+  // extract() laid out for the HBM slot records in one pass (the promote path's assembly):
+  // "key" = the distinct keys that got sessions back (ascending), "rec" = [key][max_sess][4]
+  // int64 slot records {start, end, acc, cnt | flags << 32} (unused positions zero), "last" =
+  // each key's last activity (max end - gap), "moved" = as extract().
+  py::dict extract_packed_np(const I64Array& keys, int64_t wm, int64_t max_sess, int64_t gap) {
+    std::vector<int64_t> moved, ukey, rec, last;
+    {
+      py::gil_scoped_release nogil;
+      const sess::Columns c = extract(keys.data(), keys.size(), wm, max_sess, &moved);
+      const size_t n = c.key.size();
+      int64_t pos = 0;
+      for (size_t i = 0; i < n; ++i) {
+        if (i == 0 || c.key[i] != c.key[i - 1]) {
+          ukey.push_back(c.key[i]);
+          rec.resize(rec.size() + (size_t)max_sess * 4, 0);
+          last.push_back(INT64_MIN);
+          pos = 0;
+        }
+        if (pos >= max_sess) throw std::logic_error("extract_packed: more sessions than a slot");
+        int64_t* r = rec.data() + ((ukey.size() - 1) * (size_t)max_sess + (size_t)pos) * 4;
+        r[0] = c.start[i];
+        r[1] = c.end[i];
+        r[2] = c.acc[i];
+        r[3] = (int64_t)(((uint64_t)c.cnt[i] & 0xFFFFFFFFull) | ((uint64_t)c.flags[i] << 32));
+        last.back() = std::max(last.back(), c.end[i] - gap);
+        ++pos;
+      }
+    }
+    py::dict d;
+    d["key"] = to_np(ukey);
+    d["rec"] = to_np(rec);
+    d["last"] = to_np(last);
+    d["moved"] = to_np(moved);
+    return d;
+  }
   // Fire / clean up everything the watermark allows. Returns columns of emitted rows plus the
   // keys that left the store ("released").
   py::dict fire_np(int64_t wm, std::vector<int32_t> map_code, std::vector<double> map_consts,
@@ -130,6 +168,7 @@ void bind_sessions(py::module_& m) {
            py::arg("cold") = false, py::call_guard<py::gil_scoped_release>())
       .def("merge_runs", &SessionStore::merge_runs_np)
       .def("extract", &SessionStore::extract_np)
+      .def("extract_packed", &SessionStore::extract_packed_np)
       .def("fire", &SessionStore::fire_np)
       .def("spill_set", &SessionStore::spill_set_np)
       .def("contains", &SessionStore::contains)

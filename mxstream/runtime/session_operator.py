@@ -475,46 +475,45 @@ class KeyedSessionOperator:
         with self._phase("promote"):
             dk, dt, dv = (x.clone(memory_format=torch.contiguous_format)
                           for x in self._diverted(n_host, tbase))
-            ex = self.store.extract(torch.unique(dk).cpu().numpy(), wm, K_SESS)
-            moved = ex["moved"]
-            keys = ex["key"]
             dev = self.device
-            if len(keys):
-                uniq, first, counts = np.unique(keys, return_index=True, return_counts=True)
-                ukeys = torch.from_numpy(uniq).to(dev)
-                slots_t = torch.empty_like(ukeys)
-                self.ctr[3:4].zero_()
-                self.native.gpu_session_slot_insert(ukeys.data_ptr(), ukeys.numel(),
-                                                    self.nsub_log2, self.cap_log2,
-                                                    self.keys_g.data_ptr(), slots_t.data_ptr(),
-                                                    self.ctr[3:4].data_ptr(), self._st())
-                slots = slots_t.cpu().numpy()
-                bad = slots < 0
-                if bad.any():  # sub-table full: those keys' sessions go back to the store
-                    rb = np.repeat(bad, counts)
-                    self.store.insert(*(np.ascontiguousarray(ex[f][rb], dtype=np.int64) for f in
-                                        ("key", "start", "end", "acc", "cnt", "flags")), False)
-                    moved = np.setdiff1d(moved, uniq[bad])
-                ok = ~bad
-                if ok.any():
-                    ro = np.repeat(ok, counts)
-                    pos = (np.arange(len(keys)) - np.repeat(first, counts))[ro]
-                    srow = np.repeat(np.arange(len(uniq)), counts)[ro]
-                    nk = int(ok.sum())
-                    remap = np.cumsum(ok) - 1  # index among the inserted keys
-                    rec = np.zeros((nk, K_SESS, 4), dtype=np.int64)
-                    ri = remap[srow]
-                    rec[ri, pos, 0] = ex["start"][ro]
-                    rec[ri, pos, 1] = ex["end"][ro]
-                    rec[ri, pos, 2] = ex["acc"][ro]
-                    rec[ri, pos, 3] = (ex["cnt"][ro] & 0xFFFFFFFF) | (ex["flags"][ro] << 32)
-                    last = np.full(len(uniq), I64_MIN, dtype=np.int64)
-                    np.maximum.at(last, srow, ex["end"][ro] - self.gap)
-                    sl = torch.from_numpy(slots[ok]).to(dev)
-                    self.sess.view(self.nslots, K_SESS * 4)[sl] = \
-                        torch.from_numpy(rec.reshape(nk, K_SESS * 4)).to(dev)
-                    self.slot_due[sl] = I64_MIN  # the next fire sweep recomputes due times
-                    self.slot_last[sl] = torch.from_numpy(last[ok]).to(dev)
+            with self._phase("promote.extract"):
+                # One C++ pass: the keys' sessions leave the store already laid out as HBM slot
+                # records ([key][kSess][start, end, acc, cnt | flags << 32]) + last activity.
+                ex = self.store.extract_packed(torch.unique(dk).cpu().numpy(), wm, K_SESS,
+                                               self.gap)
+            moved = ex["moved"]
+            nk = len(ex["key"])
+            if nk:
+                with self._phase("promote.scatter"):
+                    ukeys = torch.from_numpy(ex["key"]).to(dev, non_blocking=True)
+                    rec = torch.from_numpy(ex["rec"]).to(dev, non_blocking=True)
+                    last = torch.from_numpy(ex["last"]).to(dev, non_blocking=True)
+                    slots_t = torch.empty_like(ukeys)
+                    self.ctr[3:5].zero_()
+                    self.native.gpu_session_slot_insert(ukeys.data_ptr(), nk, self.nsub_log2,
+                                                        self.cap_log2, self.keys_g.data_ptr(),
+                                                        slots_t.data_ptr(),
+                                                        self.ctr[3:4].data_ptr(), self._st())
+                    self.native.gpu_session_promote(slots_t.data_ptr(), rec.data_ptr(),
+                                                    last.data_ptr(), nk, self.sess.data_ptr(),
+                                                    self.slot_due.data_ptr(),
+                                                    self.slot_last.data_ptr(),
+                                                    self.ctr[4:5].data_ptr(), self._st())
+                    n_bad = int(self.ctr[4].item())
+                if n_bad:  # sub-table full (rare): those keys' sessions go back to the store
+                    slots = slots_t.cpu().numpy()
+                    bad = slots < 0
+                    r = ex["rec"].reshape(nk, K_SESS, 4)[bad]
+                    kk = np.repeat(ex["key"][bad], K_SESS)
+                    rr = r.reshape(-1, 4)
+                    live = (rr[:, 3] & 0xFFFFFFFF) != 0
+                    self.store.insert(np.ascontiguousarray(kk[live]),
+                                      np.ascontiguousarray(rr[live, 0]),
+                                      np.ascontiguousarray(rr[live, 1]),
+                                      np.ascontiguousarray(rr[live, 2]),
+                                      np.ascontiguousarray(rr[live, 3] & 0xFFFFFFFF),
+                                      np.ascontiguousarray(rr[live, 3] >> 32), False)
+                    moved = np.setdiff1d(moved, ex["key"][bad])
             if len(moved):
                 mt = torch.from_numpy(np.ascontiguousarray(moved, dtype=np.int64)).to(dev)
                 self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
