@@ -936,4 +936,5 @@ PYBIND11_MODULE(_mxs_native, m) {
   bind_check(m);
   bind_reader(m);
   bind_format(m);
+  bind_listwin(m);
 }

@@ -10,3 +10,4 @@ void bind_trace(pybind11::module_& m);
 void bind_check(pybind11::module_& m);
 void bind_reader(pybind11::module_& m);
 void bind_format(pybind11::module_& m);
+void bind_listwin(pybind11::module_& m);

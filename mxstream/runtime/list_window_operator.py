@@ -1,14 +1,24 @@
 """Keyed windows that need every element (``process`` windows: ComputeCpuMiddle.java:34-48).
 
 Flink keeps a ListState per (key, window) and hands the full Iterable to the ProcessWindowFunction.
-Here the elements of each pane (pane = gcd(size, slide)) stay on the device as columns
-(key id, value bits); when a window fires its panes are concatenated, radix-sorted by
-(key, order-preserving value bits) -- two stable passes, value first -- and reduced per key
-segment by a kernel (median: csrc/kernels_hip.hip ``segment_median``). Late data
-within the allowed lateness re-fires the touched windows, like the pane operator.
+Here the elements live in a **device pane arena** (csrc/mxs_listwin.h): pane = gcd(size, slide),
+a power-of-two ring of pane slots, each an append buffer of (key, f64 bits) on the device.
 
-Runs on one device (the DataStream API's logical subtasks map onto it); the all-to-all path of the
-pane operator is not needed for the reference's process-window job.
+* ``process``: one readback of the batch's timestamp/key range (ring sizing), one of its
+  per-pane counts (``lw_pane_count``: buffer growth), then ``lw_pane_scatter`` appends every
+  element to its pane with one global cursor atomic per touched pane per workgroup. Elements
+  older than the allowed lateness are dropped (counted).
+* a firing counts the window's elements per dense key id (``lw_key_count``), scans the counts in
+  key order (``lw_scan``: offsets + the non-empty keys), scatters the values into their key
+  segments as order bits (``lw_key_scatter``) and selects each segment's median
+  (``segment_median_select``: LDS bitonic sort / radix select per segment). No comparison sort
+  of the window, no per-pane host loop. Key ranges wider than 16 Mi ids (arbitrary integer keys)
+  are mapped to dense ids first.
+* late-but-allowed data re-fires the already fired windows of its panes for the keys it touched
+  (EventTimeTrigger.onElement per key).
+* ``snapshot_state`` / ``restore_state``: the live panes' elements as rows (pane, key, value).
+
+CPU (device="cpu") runs the same arena through the C++ twins (csrc/listwin_cpu.cpp).
 """
 from __future__ import annotations
 
@@ -18,9 +28,15 @@ import numpy as np
 import torch
 
 from ..ops import kernels as K
+from ..ops.native import load
 from .window_operator import OperatorMetrics, java_window_start
 
 I64_MIN, I64_MAX = K.I64_MIN, K.I64_MAX
+_MAX_DENSE = 1 << 24  # key range of the direct counting sort
+
+
+def _next_pow2(x: int) -> int:
+    return 1 << max(0, int(x - 1).bit_length())
 
 
 class KeyedListWindowOperator:
@@ -31,52 +47,163 @@ class KeyedListWindowOperator:
             raise ValueError("supported list-window functions: median")
         self.size, self.slide, self.offset, self.lateness = int(size), int(slide), int(offset), int(lateness)
         self.pane = math.gcd(self.size, self.slide)
+        self.ppw = self.size // self.pane
         self.device = K.resolve_device(device)
+        self.cuda = self.device.type == "cuda"
         self.time_mode = time_mode
         self.wm = I64_MIN
-        self.panes: dict[int, list[tuple[torch.Tensor, torch.Tensor]]] = {}
         self.next_fire_start: int | None = None
         self.metrics = OperatorMetrics()
         self.late_side: list = []
+        self._m = load()
+        # Pane arena: ring slot -> absolute pane id (or None), buffers, fill, key range.
+        self.ring = _next_pow2(self.ppw + -(-self.lateness // self.pane) + 2)
+        self._alloc_ring(self.ring)
 
+    # ---- arena -----------------------------------------------------------------------------
+    def _alloc_ring(self, ring: int) -> None:
+        self.ring = ring
+        self.slot_pane: list[int | None] = [None] * ring
+        self.kbuf: list[torch.Tensor | None] = [None] * ring
+        self.vbuf: list[torch.Tensor | None] = [None] * ring
+        self.fill = [0] * ring
+        self.krange: list[tuple[int, int] | None] = [None] * ring
+        self._tab = torch.zeros(2 * ring, dtype=torch.int64, device=self.device)
+        self._tab_dirty = True
+
+    @property
+    def panes(self) -> dict:
+        """Live pane ids -> element count (inspection / tests)."""
+        return {p: self.fill[r] for r, p in enumerate(self.slot_pane) if p is not None}
+
+    def _slot_of(self, p: int) -> int:
+        return p & (self.ring - 1)
+
+    def _live_range(self):
+        live = [p for p in self.slot_pane if p is not None]
+        return (min(live), max(live)) if live else None
+
+    def _regrow_ring(self, need_lo: int, need_hi: int) -> None:
+        """Re-lay the ring so panes need_lo..need_hi fit without aliasing (keeps buffers)."""
+        old = [(p, self.kbuf[r], self.vbuf[r], self.fill[r], self.krange[r])
+               for r, p in enumerate(self.slot_pane) if p is not None]
+        self._alloc_ring(_next_pow2(need_hi - need_lo + 1))
+        for p, kb, vb, f, kr in old:
+            r = self._slot_of(p)
+            self.slot_pane[r], self.kbuf[r], self.vbuf[r], self.fill[r], self.krange[r] = p, kb, vb, f, kr
+
+    def _ensure_capacity(self, r: int, extra: int) -> None:
+        need = self.fill[r] + extra
+        kb = self.kbuf[r]
+        if kb is not None and kb.numel() >= need:
+            return
+        cap = _next_pow2(max(need, 1 << 12))
+        nk = torch.empty(cap, dtype=torch.int64, device=self.device)
+        nv = torch.empty(cap, dtype=torch.int64, device=self.device)
+        f = self.fill[r]
+        if kb is not None and f:
+            nk[:f].copy_(kb[:f])
+            nv[:f].copy_(self.vbuf[r][:f])
+        self.kbuf[r], self.vbuf[r] = nk, nv
+        self._tab_dirty = True
+
+    def _sync_tab(self) -> None:
+        if not self._tab_dirty:
+            return
+        addr = [0] * (2 * self.ring)
+        for r in range(self.ring):
+            if self.kbuf[r] is not None:
+                addr[r] = self.kbuf[r].data_ptr()
+                addr[self.ring + r] = self.vbuf[r].data_ptr()
+        self._tab.copy_(torch.tensor(addr, dtype=torch.int64))
+        self._tab_dirty = False
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream if self.cuda else 0
+
+    # ---- window arithmetic ----------------------------------------------------------------
     def _pane_of(self, t):
         return (t - self.offset) // self.pane
 
     def _late_ts(self) -> int:
         if self.wm == I64_MIN or self.time_mode != "event":
             return I64_MIN
-        s = self._align_up(self.wm - self.size - self.lateness + 2)
-        return s
+        return self._align_up(self.wm - self.size - self.lateness + 2)
 
     def _align_up(self, t: int) -> int:
         ls = java_window_start(t, self.offset, self.slide)
         return ls if ls >= t else ls + self.slide
 
+    def _first_start_containing(self, t: int) -> int:
+        ls = java_window_start(t, self.offset, self.slide)
+        return ls - ((ls - (t - self.size + 1)) // self.slide) * self.slide
+
+    # ---- ingest ---------------------------------------------------------------------------
     def process(self, keys: torch.Tensor, ts: torch.Tensor, vals_f64: torch.Tensor) -> list:
         """keys int64 (or int32 dictionary ids), ts int64, vals: f64 bit patterns (int64).
-        Returns fired rows."""
+        Returns fired rows (window_start, window_end, keys, medians) of late re-firings."""
+        n = keys.numel()
+        if n == 0:
+            return []
+        keys = keys.to(torch.int64).contiguous()
+        ts = ts.contiguous()
+        vals_f64 = vals_f64.contiguous()
+        late_ts = self._late_ts()
+        # Readback 1: timestamp and key range of the batch (ring sizing, dense key range).
+        tmin, tmax, kmin, kmax = torch.stack([ts.min(), ts.max(), keys.min(), keys.max()]).tolist()
+        lo_t = max(tmin, late_ts) if late_ts > I64_MIN else tmin
+        if lo_t > tmax:  # everything late
+            self.metrics.num_late_records_dropped += n
+            return []
+        plo, phi = self._pane_of(lo_t), self._pane_of(tmax)
+        live = self._live_range()
+        need_lo, need_hi = (plo, phi) if live is None else (min(plo, live[0]), max(phi, live[1]))
+        if need_hi - need_lo + 1 > self.ring:
+            self._regrow_ring(need_lo, need_hi)
+        R, st = self.ring, self._stream()
+        counts = torch.zeros(R + 1, dtype=torch.int64, device=self.device)
+        self._m.lw_pane_count(self.cuda, ts.data_ptr(), n, self.offset, self.pane, R, late_ts,
+                              counts.data_ptr(), st)
+        # Readback 2: elements per ring slot (buffer growth) + late count.
+        hc = counts.tolist()
+        self.metrics.num_late_records_dropped += hc[R]
+        self.metrics.num_records_in += n - hc[R]
+        touched_panes = []
+        for r in range(R):
+            if not hc[r]:
+                continue
+            p = plo + ((r - plo) & (R - 1))  # the batch's pane in ring slot r
+            if self.slot_pane[r] is not None and self.slot_pane[r] != p:
+                raise RuntimeError("list window: pane ring aliasing")  # sizing above prevents it
+            self.slot_pane[r] = p
+            self._ensure_capacity(r, hc[r])
+            kr = self.krange[r]
+            self.krange[r] = (kmin, kmax) if kr is None else (min(kr[0], kmin), max(kr[1], kmax))
+            touched_panes.append(p)
+        self._sync_tab()
+        cursor = torch.tensor(self.fill, dtype=torch.int64).to(self.device, non_blocking=True)
+        self._m.lw_pane_scatter(self.cuda, keys.data_ptr(), ts.data_ptr(), vals_f64.data_ptr(), n,
+                                self.offset, self.pane, R, late_ts, self._tab.data_ptr(),
+                                cursor.data_ptr(), st)
+        for r in range(R):
+            self.fill[r] += hc[r]
+        if not touched_panes:
+            return []
+        first = self._first_start_containing(self.offset + min(touched_panes) * self.pane)
+        if self.wm > I64_MIN:
+            first = max(first, self._align_up(self.wm - self.size + 2))
+        self.next_fire_start = first if self.next_fire_start is None else min(self.next_fire_start, first)
         out = []
-        keys = keys.to(torch.int64)
-        if keys.numel():
-            late_ts = self._late_ts()
-            keep = ts >= late_ts
-            self.metrics.num_late_records_dropped += int((~keep).sum().item())
-            keys, ts, vals_f64 = keys[keep], ts[keep], vals_f64[keep]
-        if keys.numel():
-            panes = torch.div(ts - self.offset, self.pane, rounding_mode="floor")
-            pu = torch.unique(panes).tolist()
-            for p in pu:
-                sel = panes == p
-                self.panes.setdefault(int(p), []).append((keys[sel], vals_f64[sel]))
-            first = self._first_start_containing(self.offset + min(pu) * self.pane)
-            if self.wm > I64_MIN:
-                first = max(first, self._align_up(self.wm - self.size + 2))
-            self.next_fire_start = first if self.next_fire_start is None else min(self.next_fire_start, first)
-            # Late-but-allowed data: re-fire, for the keys that received it, the windows that
-            # already fired and contain those panes (EventTimeTrigger.onElement per key).
-            if self.wm > I64_MIN:
-                for p in pu:
-                    touched = torch.unique(keys[panes == p])
+        # Late-but-allowed data: re-fire, for the keys that received it, the windows that
+        # already fired and contain those panes (EventTimeTrigger.onElement per key).
+        if self.wm > I64_MIN:
+            fired_panes = [p for p in touched_panes
+                           if self._first_start_containing(self.offset + p * self.pane)
+                           + self.size - 1 <= self.wm]
+            if fired_panes:
+                pcol = torch.div(ts - self.offset, self.pane, rounding_mode="floor")
+                for p in sorted(fired_panes):
+                    touched = torch.unique(keys[pcol == p])
                     s = self._first_start_containing(self.offset + p * self.pane)
                     while s <= self.offset + p * self.pane:
                         if s + self.size - 1 <= self.wm < s + self.size - 1 + self.lateness:
@@ -84,10 +211,7 @@ class KeyedListWindowOperator:
                         s += self.slide
         return out
 
-    def _first_start_containing(self, t: int) -> int:
-        ls = java_window_start(t, self.offset, self.slide)
-        return ls - ((ls - (t - self.size + 1)) // self.slide) * self.slide
-
+    # ---- firing -----------------------------------------------------------------------------
     def advance_watermark(self, wm: int) -> list:
         if wm <= self.wm:
             return []
@@ -95,8 +219,9 @@ class KeyedListWindowOperator:
         out = []
         if self.next_fire_start is not None:
             s = self.next_fire_start
+            live = self._live_range()
+            last_pane = live[1] if live else None
             # Windows after the last pane hold no data: never iterate past it (wm may be MAX).
-            last_pane = max(self.panes) if self.panes else None
             while s + self.size - 1 <= wm and last_pane is not None \
                     and self._pane_of(s) <= last_pane:
                 out += self._fire_window(s)
@@ -109,39 +234,151 @@ class KeyedListWindowOperator:
 
     def _purge(self) -> None:
         if self.wm == I64_MAX:
-            self.panes.clear()
-            return
-        keep_from = self._pane_of(self._align_up(self.wm - self.size - self.lateness + 2))
-        for p in [p for p in self.panes if p < keep_from]:
-            del self.panes[p]
+            keep_from = None
+        else:
+            keep_from = self._pane_of(self._align_up(self.wm - self.size - self.lateness + 2))
+        for r, p in enumerate(self.slot_pane):
+            if p is not None and (keep_from is None or p < keep_from):
+                self.slot_pane[r] = None
+                self.fill[r] = 0
+                self.krange[r] = None
+
+    def _window_panes(self, s: int) -> list[int]:
+        p0 = self._pane_of(s)
+        out = []
+        for p in range(p0, p0 + self.ppw):
+            r = self._slot_of(p)
+            if self.slot_pane[r] == p and self.fill[r]:
+                out.append(r)
+        return out
 
     def _fire_window(self, s: int, only_keys: torch.Tensor | None = None) -> list:
-        p0 = self._pane_of(s)
-        parts = [c for p in range(p0, p0 + self.size // self.pane) for c in self.panes.get(p, [])]
-        if not parts:
+        slots = self._window_panes(s)
+        if not slots:
             return []
-        keys = torch.cat([k for k, _ in parts])
-        vals = torch.cat([v for _, v in parts])
-        if only_keys is not None:
-            sel = torch.isin(keys, only_keys)
-            keys, vals = keys[sel], vals[sel]
-            if not keys.numel():
-                return []
-        ordv = K.f64_order_bits(vals.contiguous())
-        # One radix sort by key over the used key bits (dictionary ids / small ints sort as they
-        # are; anything else through dense ids), the values ride along unsorted; the median of
-        # each key segment is then selected per segment (LDS bitonic sort / radix select) -- no
-        # 64-bit sort of every value of the window.
-        kmin, kmax = (int(x) for x in torch.aminmax(keys))
-        if kmin >= 0 and kmax < (1 << 40):
-            uniq, ids = None, keys.contiguous()
-            kbits = max(1, kmax.bit_length())
+        self.metrics.num_fires += 1
+        total = sum(self.fill[r] for r in slots)
+        kmin = min(self.krange[r][0] for r in slots)
+        kmax = max(self.krange[r][1] for r in slots)
+        if kmin >= 0 and kmax - kmin < _MAX_DENSE and len(slots) <= 64:
+            keys_out, med = self._median_dense(slots, kmin, kmax - kmin + 1, total)
         else:
-            uniq, ids = torch.unique(keys, return_inverse=True)
-            kbits = max(1, int(uniq.numel() - 1).bit_length())
-        ids, ordv = K.sort_pairs(ids.contiguous(), ordv, bits=kbits)
-        heads = torch.nonzero(torch.cat([torch.ones(1, dtype=torch.bool, device=ids.device),
-                                         ids[1:] != ids[:-1]])).flatten()
-        med = K.segment_median(heads.contiguous(), ordv, sorted_values=False)
-        out_keys = ids[heads] if uniq is None else uniq[ids[heads]]
-        return [(s, s + self.size, out_keys.cpu().numpy(), med.cpu().numpy())]
+            keys_out, med = self._median_mapped(slots)
+        if only_keys is not None:
+            sel = torch.isin(keys_out, only_keys.to(keys_out.device))
+            keys_out, med = keys_out[sel], med[sel]
+        if not keys_out.numel():
+            return []
+        self.metrics.num_records_out += int(keys_out.numel())
+        return [(s, s + self.size, keys_out.cpu().numpy(), med.cpu().numpy())]
+
+    def _median_dense(self, slots, kmin: int, nk: int, total: int):
+        m, st, dev = self._m, self._stream(), self.device
+        panes = [(self.kbuf[r].data_ptr(), self.vbuf[r].data_ptr(), self.fill[r]) for r in slots]
+        counts = torch.zeros(nk, dtype=torch.int32, device=dev)
+        m.lw_key_count(self.cuda, panes, kmin, nk, counts.data_ptr(), st)
+        offs = torch.empty(nk + 1, dtype=torch.int64, device=dev)
+        heads = torch.empty(nk, dtype=torch.int64, device=dev)
+        hkeys = torch.empty(nk, dtype=torch.int64, device=dev)
+        nh = torch.zeros(1, dtype=torch.int64, device=dev)
+        scratch = torch.empty(max(16, m.lw_scan_scratch_bytes(nk)), dtype=torch.uint8, device=dev)
+        m.lw_scan(self.cuda, counts.data_ptr(), nk, kmin, scratch.data_ptr(), offs.data_ptr(),
+                  heads.data_ptr(), hkeys.data_ptr(), nh.data_ptr(), st)
+        cursor = offs[:nk].clone()
+        ordv = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+        m.lw_key_scatter(self.cuda, panes, kmin, cursor.data_ptr(), ordv.data_ptr(), st)
+        k = int(nh.item())
+        med = torch.empty(k, dtype=torch.float64, device=dev)
+        if k:
+            args = (heads.data_ptr(), k, total, ordv.data_ptr(), med.data_ptr())
+            if self.cuda:
+                m.gpu_segment_median_select(*args, st)
+            else:
+                m.cpu_segment_median_select(*args)
+        return hkeys[:k], med
+
+    def _median_mapped(self, slots):
+        """Keys outside a dense id range: dense ids by torch.unique, then the same firing."""
+        keys = torch.cat([self.kbuf[r][:self.fill[r]] for r in slots])
+        vals = torch.cat([self.vbuf[r][:self.fill[r]] for r in slots])
+        uniq, ids = torch.unique(keys, return_inverse=True)
+        ids = ids.to(torch.int64).contiguous()
+        vals = vals.contiguous()
+        m, st, dev = self._m, self._stream(), self.device
+        n, nk = ids.numel(), uniq.numel()
+        panes = [(ids.data_ptr(), vals.data_ptr(), n)]
+        counts = torch.zeros(nk, dtype=torch.int32, device=dev)
+        m.lw_key_count(self.cuda, panes, 0, nk, counts.data_ptr(), st)
+        offs = torch.empty(nk + 1, dtype=torch.int64, device=dev)
+        heads = torch.empty(nk, dtype=torch.int64, device=dev)
+        hkeys = torch.empty(nk, dtype=torch.int64, device=dev)
+        nh = torch.zeros(1, dtype=torch.int64, device=dev)
+        scratch = torch.empty(max(16, m.lw_scan_scratch_bytes(nk)), dtype=torch.uint8, device=dev)
+        m.lw_scan(self.cuda, counts.data_ptr(), nk, 0, scratch.data_ptr(), offs.data_ptr(),
+                  heads.data_ptr(), hkeys.data_ptr(), nh.data_ptr(), st)
+        cursor = offs[:nk].clone()
+        ordv = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        m.lw_key_scatter(self.cuda, panes, 0, cursor.data_ptr(), ordv.data_ptr(), st)
+        med = torch.empty(nk, dtype=torch.float64, device=dev)
+        args = (heads.data_ptr(), nk, n, ordv.data_ptr(), med.data_ptr())
+        if self.cuda:
+            m.gpu_segment_median_select(*args, st)
+        else:
+            m.cpu_segment_median_select(*args)
+        return uniq, med
+
+    # ---- checkpoints ------------------------------------------------------------------------
+    def snapshot_state(self):
+        """Live panes' elements as rows (pane, key, f64 bits) + the firing bookkeeping."""
+        from .checkpoint import OperatorSnapshot
+
+        pk, kk, vv = [], [], []
+        for r, p in enumerate(self.slot_pane):
+            if p is None or not self.fill[r]:
+                continue
+            f = self.fill[r]
+            kk.append(self.kbuf[r][:f].cpu().numpy())
+            vv.append(self.vbuf[r][:f].cpu().numpy())
+            pk.append(np.full(f, p, dtype=np.int64))
+        cat = lambda xs: np.concatenate(xs) if xs else np.zeros(0, np.int64)  # noqa: E731
+        keys = cat(kk)
+        kg = (K.keygroups(torch.from_numpy(keys), max_parallelism=128).numpy()
+              if keys.size else np.zeros(0, np.int32))
+        cols = {"key": keys, "pane": cat(pk), "val": cat(vv)}
+        meta = {"kind": "list_window", "size": self.size, "slide": self.slide,
+                "offset": self.offset, "lateness": self.lateness, "wm": self.wm,
+                "next_fire_start": self.next_fire_start,
+                "metrics": {"num_records_in": self.metrics.num_records_in,
+                            "num_late_records_dropped": self.metrics.num_late_records_dropped,
+                            "num_records_out": self.metrics.num_records_out,
+                            "num_fires": self.metrics.num_fires}}
+        return OperatorSnapshot(kg, cols, meta)
+
+    def restore_state(self, rows: dict, meta: dict) -> None:
+        if meta.get("kind") != "list_window" or (meta["size"], meta["slide"], meta["offset"]) != \
+                (self.size, self.slide, self.offset):
+            raise ValueError("checkpoint of a different list window")
+        self._alloc_ring(self.ring)
+        self.wm = meta["wm"]
+        self.next_fire_start = meta["next_fire_start"]
+        for k, v in meta.get("metrics", {}).items():
+            setattr(self.metrics, k, v)
+        panes = np.asarray(rows.get("pane", np.zeros(0, np.int64)), dtype=np.int64)
+        if not panes.size:
+            return
+        keys = np.asarray(rows["key"], dtype=np.int64)
+        vals = np.asarray(rows["val"], dtype=np.int64)
+        up = np.unique(panes)
+        if up.max() - up.min() + 1 > self.ring:
+            self._alloc_ring(_next_pow2(int(up.max() - up.min() + 1)))
+        for p in up.tolist():
+            sel = panes == p
+            r = self._slot_of(p)
+            f = int(sel.sum())
+            self.slot_pane[r] = p
+            self._ensure_capacity(r, f)
+            self.kbuf[r][:f].copy_(torch.from_numpy(keys[sel]))
+            self.vbuf[r][:f].copy_(torch.from_numpy(vals[sel]))
+            self.fill[r] = f
+            self.krange[r] = (int(keys[sel].min()), int(keys[sel].max()))
+        self._tab_dirty = True

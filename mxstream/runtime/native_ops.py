@@ -935,8 +935,9 @@ class NativeSessionOp(NativeWindowOp):
 
 class NativeMedianOp(NativeWindowOp):
     """``process(<median>)`` windows (ComputeCpuMiddle.java:34-48) on the device list-window
-    operator: elements stay on the device per pane, the fire sorts (key, value) with two radix
-    passes and a kernel takes the per-key median."""
+    operator (runtime/list_window_operator.py): elements stay in a device pane arena, a firing
+    counting-sorts the window by key id and a kernel selects each key's median.
+    Checkpoints carry the live panes' elements (NativeWindowOp.snapshot -> snapshot_state)."""
 
     _key32_ok = False
 
@@ -965,10 +966,6 @@ class NativeMedianOp(NativeWindowOp):
                 sub = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
                 out.append(Rec(value, e - 1, sub))
         return out
-
-    def snapshot(self) -> dict:
-        raise NotImplementedError("checkpointing of native process windows is not supported; "
-                                  "run with native='off' for checkpointed process windows")
 
 
 class NativeVectorWindowOp(NativeWindowOp):
