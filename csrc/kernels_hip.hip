@@ -3314,11 +3314,11 @@ __global__ __launch_bounds__(256) void segment_median_kernel(const int64_t* __re
   }
 }
 
-// Median of every segment of *unsorted* order-preserving f64 bits (segments = runs of equal key
-// after a radix sort by key only; the values ride along unsorted). One wave per segment: a
-// segment of up to kMedLds values is bitonic-sorted in the wave's LDS slice; a longer one is
-// resolved by two radix selects (8 byte passes each over the segment, 256-bin LDS histograms).
-// Replaces the second, 64-bit radix sort over every value of the window (8 of the 11 passes).
+// Median of every segment of *unsorted* order-preserving f64 bits (segments = a key's values
+// after the list window's counting sort by key, csrc/listwin_hip.hip). One wave per segment: a
+// segment of up to kMedLds values is staged in the wave's LDS slice and radix-selected there (8
+// byte passes, 256-bin LDS histogram; the lower middle element from one more pass); a longer
+// one is resolved by two radix selects over global memory.
 constexpr int kMedLds = 2048;
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -3377,6 +3377,7 @@ __global__ __launch_bounds__(256) void segment_median_select_kernel(
     const int64_t* __restrict__ heads, int64_t nseg, int64_t total, const uint64_t* __restrict__ ord,
     double* __restrict__ out) {
   __shared__ uint64_t buf[4][kMedLds];
+  __shared__ uint32_t hbuf[4][256];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint64_t* b = buf[w];
   for (int64_t s = (int64_t)blockIdx.x * 4 + w; s < nseg; s += (int64_t)gridDim.x * 4) {
@@ -3388,28 +3389,37 @@ __global__ __launch_bounds__(256) void segment_median_select_kernel(
       continue;
     }
     if (n <= kMedLds) {
-      int P = 64;
-      while (P < n) P <<= 1;
-      for (int i = lane; i < P; i += 64) b[i] = i < n ? ord[a + i] : ~0ull;
+      // Segment staged in LDS once, then a radix select of the upper middle element (8 byte
+      // passes over LDS, 256-bin histogram) -- a full bitonic sort of the segment did ~10x more
+      // LDS traffic -- and the lower middle one from one more pass: the largest element below
+      // it, unless enough elements tie with it.
+      for (int i = lane; i < n; i += 64) b[i] = ord[a + i];
       wave_lds_sync();
-      for (int k = 2; k <= P; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          for (int i = lane; i < P; i += 64) {
-            const int ixj = i ^ j;
-            if (ixj > i) {
-              const uint64_t x = b[i], y = b[ixj];
-              const bool up = (i & k) == 0;
-              if ((x > y) == up) {
-                b[i] = y;
-                b[ixj] = x;
-              }
-            }
+      hi_bits = wave_radix_select(b, n, n / 2, hbuf[w], lane);
+      if (n & 1) {
+        lo_bits = hi_bits;
+      } else {
+        uint32_t less = 0;
+        uint64_t below = 0;
+        bool any = false;
+        for (int i = lane; i < n; i += 64) {
+          const uint64_t x = b[i];
+          if (x < hi_bits) {
+            ++less;
+            if (!any || x > below) below = x;
+            any = true;
           }
-          wave_lds_sync();
         }
+        for (int o = 32; o >= 1; o >>= 1) {
+          less += __shfl_xor(less, o);
+          const uint64_t ob = __shfl_xor(below, o);
+          const bool oa = __shfl_xor((int)any, o) != 0;
+          if (oa && (!any || ob > below)) below = ob;
+          any = any || oa;
+        }
+        // sorted[n/2 - 1] is hi itself when fewer than n/2 elements are below it
+        lo_bits = less < (uint32_t)(n / 2) ? hi_bits : below;
       }
-      hi_bits = b[n / 2];
-      lo_bits = b[(n - 1) / 2];
       wave_lds_sync();
     } else {
       uint32_t* hist = reinterpret_cast<uint32_t*>(b);

@@ -36,6 +36,27 @@ LwPanes make_panes(const std::vector<std::tuple<intptr_t, intptr_t, int64_t>>& v
   return w;
 }
 
+LwRankPanes make_rank_panes(
+    const std::vector<std::tuple<intptr_t, intptr_t, intptr_t, intptr_t, int64_t, int64_t, int64_t>>& v) {
+  if (v.empty() || v.size() > (size_t)kLwMaxRankPanes)
+    throw std::invalid_argument("list window: 1..32 panes per ranked firing");
+  LwRankPanes w{};
+  w.n = (int32_t)v.size();
+  for (size_t i = 0; i < v.size(); ++i) {
+    auto& p = w.p[i];
+    p.keys = LP<const int64_t>(std::get<0>(v[i]));
+    p.vals = LP<const uint64_t>(std::get<1>(v[i]));
+    p.ranks = LP<const uint32_t>(std::get<2>(v[i]));
+    p.counts = LP<const uint32_t>(std::get<3>(v[i]));
+    p.kbase = std::get<4>(v[i]);
+    p.ksize = std::get<5>(v[i]);
+    p.len = std::get<6>(v[i]);
+    if (!p.counts || !p.ranks || p.ksize <= 0 || p.len < 0)
+      throw std::invalid_argument("list window: ranked pane without counts / ranks");
+  }
+  return w;
+}
+
 void check_ring(int ring) {
   if (ring < 1 || ring > kLwMaxRing || (ring & (ring - 1)))
     throw std::invalid_argument("list window: ring must be a power of two <= 4096");
@@ -85,6 +106,26 @@ void bind_listwin(py::module_& m) {
     else
       cpu::lw_scan(LP<uint32_t>(counts), nkeys, kmin, LP<int64_t>(offs), LP<int64_t>(heads),
                    LP<int64_t>(head_keys), LP<int64_t>(nheads));
+  });
+  using RankPaneArg = std::tuple<intptr_t, intptr_t, intptr_t, intptr_t, int64_t, int64_t, int64_t>;
+  m.def("lw_rank_prefix", [](bool cuda, std::vector<RankPaneArg> panes, int64_t kmin,
+                             int64_t nkeys, intptr_t total, intptr_t pre, intptr_t stream) {
+    const LwRankPanes w = make_rank_panes(panes);
+    if (cuda)
+      gpu::lw_rank_prefix(w, kmin, nkeys, LP<uint32_t>(total), LP<uint32_t>(pre), stream);
+    else
+      cpu::lw_rank_prefix(w, kmin, nkeys, LP<uint32_t>(total), LP<uint32_t>(pre));
+  });
+  m.def("lw_rank_scatter", [](bool cuda, std::vector<RankPaneArg> panes, int64_t kmin,
+                              int64_t nkeys, intptr_t offs, intptr_t pre, intptr_t out_ord,
+                              intptr_t stream) {
+    const LwRankPanes w = make_rank_panes(panes);
+    if (cuda)
+      gpu::lw_rank_scatter(w, kmin, nkeys, LP<int64_t>(offs), LP<uint32_t>(pre),
+                           LP<uint64_t>(out_ord), stream);
+    else
+      cpu::lw_rank_scatter(w, kmin, nkeys, LP<int64_t>(offs), LP<uint32_t>(pre),
+                           LP<uint64_t>(out_ord));
   });
   m.def("lw_key_scatter", [](bool cuda,
                              std::vector<std::tuple<intptr_t, intptr_t, int64_t>> panes,

@@ -90,8 +90,13 @@ __global__ __launch_bounds__(kLwBlock) void lw_pane_scatter_kernel(
       if (i < n && slot[u] < ring) {
         const int r = slot[u];
         const unsigned long long pos = base[r] + atomicAdd(&cnt[r], 1u);
-        reinterpret_cast<int64_t*>(tab[r])[pos] = keys[i];
+        const int64_t key = keys[i];
+        reinterpret_cast<int64_t*>(tab[r])[pos] = key;
         reinterpret_cast<uint64_t*>(tab[ring + r])[pos] = vals[i];
+        uint32_t* kc = reinterpret_cast<uint32_t*>(tab[3 * ring + r]);
+        if (kc)  // rank of the element among its key's elements of this pane
+          reinterpret_cast<uint32_t*>(tab[2 * ring + r])[pos] =
+              atomicAdd(&kc[key - tab[4 * ring + r]], 1u);
       }
     }
     __syncthreads();
@@ -115,6 +120,40 @@ __global__ __launch_bounds__(kLwBlock) void lw_key_scatter_kernel(LwPanes w, int
     const unsigned long long pos =
         atomicAdd((unsigned long long*)&cursor[p.keys[i] - kmin], 1ull);
     out[pos] = f64_order_bits(p.vals[i]);
+  }
+}
+
+// Per key of the window: the panes' counts -> each pane's prefix and the total.
+__global__ __launch_bounds__(kLwBlock) void lw_rank_prefix_kernel(LwRankPanes w, int64_t kmin,
+                                                                  int64_t nkeys,
+                                                                  uint32_t* __restrict__ total,
+                                                                  uint32_t* __restrict__ pre) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nkeys;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t key = kmin + k;
+    uint32_t run = 0;
+    for (int j = 0; j < w.n; ++j) {
+      const LwRankPane& p = w.p[j];
+      const int64_t o = key - p.kbase;
+      pre[(int64_t)j * nkeys + k] = run;
+      run += (o >= 0 && o < p.ksize) ? p.counts[o] : 0u;
+    }
+    total[k] = run;
+  }
+}
+
+// Placement without atomics: segment start + earlier panes' count of the key + rank.
+__global__ __launch_bounds__(kLwBlock) void lw_rank_scatter_kernel(LwRankPanes w, int64_t kmin,
+                                                                   int64_t nkeys,
+                                                                   const int64_t* __restrict__ offs,
+                                                                   const uint32_t* __restrict__ pre,
+                                                                   uint64_t* __restrict__ out) {
+  const LwRankPane& p = w.p[blockIdx.y];
+  const uint32_t* pj = pre + (int64_t)blockIdx.y * nkeys;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.len;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = p.keys[i] - kmin;
+    out[offs[k] + pj[k] + p.ranks[i]] = f64_order_bits(p.vals[i]);
   }
 }
 
@@ -320,6 +359,26 @@ void lw_key_scatter(const LwPanes& w, int64_t kmin, int64_t* cursor, uint64_t* o
   if (mx <= 0) return;
   hipLaunchKernelGGL(lw_key_scatter_kernel, dim3(grid_of(mx, kLwBlock * 8, 4096), w.n),
                      dim3(kLwBlock), 0, (hipStream_t)stream, w, kmin, cursor, out_ord);
+  LW_CHECK(hipGetLastError());
+}
+
+void lw_rank_prefix(const LwRankPanes& w, int64_t kmin, int64_t nkeys, uint32_t* total,
+                    uint32_t* pre, intptr_t stream) {
+  if (w.n <= 0 || w.n > kLwMaxRankPanes) throw std::invalid_argument("lw_rank_prefix: 1..32 panes");
+  if (nkeys <= 0) return;
+  hipLaunchKernelGGL(lw_rank_prefix_kernel, dim3(grid_of(nkeys, kLwBlock, 4096)), dim3(kLwBlock),
+                     0, (hipStream_t)stream, w, kmin, nkeys, total, pre);
+  LW_CHECK(hipGetLastError());
+}
+
+void lw_rank_scatter(const LwRankPanes& w, int64_t kmin, int64_t nkeys, const int64_t* offs,
+                     const uint32_t* pre, uint64_t* out_ord, intptr_t stream) {
+  if (w.n <= 0 || w.n > kLwMaxRankPanes) throw std::invalid_argument("lw_rank_scatter: 1..32 panes");
+  int64_t mx = 0;
+  for (int i = 0; i < w.n; ++i) mx = w.p[i].len > mx ? w.p[i].len : mx;
+  if (mx <= 0) return;
+  hipLaunchKernelGGL(lw_rank_scatter_kernel, dim3(grid_of(mx, kLwBlock * 8, 4096), w.n),
+                     dim3(kLwBlock), 0, (hipStream_t)stream, w, kmin, nkeys, offs, pre, out_ord);
   LW_CHECK(hipGetLastError());
 }
 

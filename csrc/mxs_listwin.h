@@ -34,9 +34,27 @@ struct LwPanes {
   int32_t n;
 };
 
-// Arena targets of a batch scatter: a table (device memory for the GPU launch) of 2 * ring
-// addresses -- [r] the key buffer of ring slot r, [ring + r] its value buffer -- and a fill
-// cursor per slot.
+// Arena targets of a batch scatter: a table (device memory for the GPU launch) of 5 * ring
+// words -- [r] the key buffer of ring slot r, [ring + r] its value buffer, [2 ring + r] its
+// per-element rank buffer (u32), [3 ring + r] its per-key element counts (u32, over the slot's
+// key range), [4 ring + r] the first key of that range -- and a fill cursor per slot. The
+// append records each element's rank among its key's elements in the pane (the atomic count),
+// so a firing places every element without atomics: segment start + earlier panes' counts of
+// the key + rank. A slot with a null count array (key range too wide) records no ranks.
+
+// One pane of a ranked firing.
+struct LwRankPane {
+  const int64_t* keys;
+  const uint64_t* vals;
+  const uint32_t* ranks;
+  const uint32_t* counts;  // per key of [kbase, kbase + ksize)
+  int64_t kbase, ksize, len;
+};
+constexpr int kLwMaxRankPanes = 32;
+struct LwRankPanes {
+  LwRankPane p[kLwMaxRankPanes];
+  int32_t n;
+};
 
 namespace gpu {
 void lw_pane_count(const int64_t* ts, int64_t n, int64_t offset, int64_t pane, int ring,
@@ -51,6 +69,12 @@ void lw_scan(const uint32_t* counts, int64_t nkeys, int64_t kmin, void* scratch,
              int64_t* heads, int64_t* head_keys, int64_t* nheads, intptr_t stream);
 void lw_key_scatter(const LwPanes& w, int64_t kmin, int64_t* cursor, uint64_t* out_ord,
                     intptr_t stream);
+// Ranked firing: total per-key counts of the window and each pane's prefix (pre[j * nkeys + k]),
+// then the placement scatter.
+void lw_rank_prefix(const LwRankPanes& w, int64_t kmin, int64_t nkeys, uint32_t* total,
+                    uint32_t* pre, intptr_t stream);
+void lw_rank_scatter(const LwRankPanes& w, int64_t kmin, int64_t nkeys, const int64_t* offs,
+                     const uint32_t* pre, uint64_t* out_ord, intptr_t stream);
 }  // namespace gpu
 
 namespace cpu {
@@ -63,6 +87,10 @@ void lw_key_count(const LwPanes& w, int64_t kmin, int64_t nkeys, uint32_t* count
 void lw_scan(const uint32_t* counts, int64_t nkeys, int64_t kmin, int64_t* offs, int64_t* heads,
              int64_t* head_keys, int64_t* nheads);
 void lw_key_scatter(const LwPanes& w, int64_t kmin, int64_t* cursor, uint64_t* out_ord);
+void lw_rank_prefix(const LwRankPanes& w, int64_t kmin, int64_t nkeys, uint32_t* total,
+                    uint32_t* pre);
+void lw_rank_scatter(const LwRankPanes& w, int64_t kmin, int64_t nkeys, const int64_t* offs,
+                     const uint32_t* pre, uint64_t* out_ord);
 }  // namespace cpu
 
 // Java floorDiv for the pane of a timestamp.

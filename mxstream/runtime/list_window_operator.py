@@ -8,12 +8,15 @@ a power-of-two ring of pane slots, each an append buffer of (key, f64 bits) on t
   per-pane counts (``lw_pane_count``: buffer growth), then ``lw_pane_scatter`` appends every
   element to its pane with one global cursor atomic per touched pane per workgroup. Elements
   older than the allowed lateness are dropped (counted).
-* a firing counts the window's elements per dense key id (``lw_key_count``), scans the counts in
-  key order (``lw_scan``: offsets + the non-empty keys), scatters the values into their key
-  segments as order bits (``lw_key_scatter``) and selects each segment's median
-  (``segment_median_select``: LDS bitonic sort / radix select per segment). No comparison sort
-  of the window, no per-pane host loop. Key ranges wider than 16 Mi ids (arbitrary integer keys)
-  are mapped to dense ids first.
+* the append also records each element's rank among its key's elements of the pane (per-pane
+  per-key counts, dense key ranges up to 16 Mi ids), so a firing needs no atomics: per-key
+  totals and per-pane prefixes from the panes' counts (``lw_rank_prefix``), the order-preserving
+  scan of the totals (``lw_scan``: offsets + the non-empty keys in key order), every element
+  placed at segment start + prefix + rank (``lw_rank_scatter``, as order bits), and each
+  segment's median selected in LDS (``segment_median_select``). Panes without ranks (wide key
+  ranges, restored panes) fire through a counting sort with atomics (``lw_key_count`` /
+  ``lw_key_scatter``); key ranges over 16 Mi ids are mapped to dense ids first. No comparison
+  sort of the window, no per-pane host loop.
 * late-but-allowed data re-fires the already fired windows of its panes for the keys it touched
   (EventTimeTrigger.onElement per key).
 * ``snapshot_state`` / ``restore_state``: the live panes' elements as rows (pane, key, value).
@@ -68,7 +71,14 @@ class KeyedListWindowOperator:
         self.vbuf: list[torch.Tensor | None] = [None] * ring
         self.fill = [0] * ring
         self.krange: list[tuple[int, int] | None] = [None] * ring
-        self._tab = torch.zeros(2 * ring, dtype=torch.int64, device=self.device)
+        # Ranked slots: per-element rank among the key's elements of the pane (rbuf) and the
+        # per-key counts over [kbase, kbase + numel) (kcnt): the firing places elements without
+        # atomics. A slot whose key range grows past _MAX_DENSE (or was restored) is unranked.
+        self.rbuf: list[torch.Tensor | None] = [None] * ring
+        self.kcnt: list[torch.Tensor | None] = [None] * ring
+        self.kbase = [0] * ring
+        self.ranked = [True] * ring
+        self._tab = torch.zeros(5 * ring, dtype=torch.int64, device=self.device)
         self._tab_dirty = True
 
     @property
@@ -83,14 +93,42 @@ class KeyedListWindowOperator:
         live = [p for p in self.slot_pane if p is not None]
         return (min(live), max(live)) if live else None
 
+    _SLOT_FIELDS = ("slot_pane", "kbuf", "vbuf", "fill", "krange", "rbuf", "kcnt", "kbase",
+                    "ranked")
+
     def _regrow_ring(self, need_lo: int, need_hi: int) -> None:
         """Re-lay the ring so panes need_lo..need_hi fit without aliasing (keeps buffers)."""
-        old = [(p, self.kbuf[r], self.vbuf[r], self.fill[r], self.krange[r])
+        old = [[getattr(self, f)[r] for f in self._SLOT_FIELDS]
                for r, p in enumerate(self.slot_pane) if p is not None]
         self._alloc_ring(_next_pow2(need_hi - need_lo + 1))
-        for p, kb, vb, f, kr in old:
-            r = self._slot_of(p)
-            self.slot_pane[r], self.kbuf[r], self.vbuf[r], self.fill[r], self.krange[r] = p, kb, vb, f, kr
+        for vals in old:
+            r = self._slot_of(vals[0])
+            for f, v in zip(self._SLOT_FIELDS, vals):
+                getattr(self, f)[r] = v
+
+    def _ensure_key_range(self, r: int, kmin: int, kmax: int) -> None:
+        """The slot's per-key counts cover [kmin, kmax] (grown by copy), or the slot stops
+        recording ranks when its key range would exceed _MAX_DENSE ids."""
+        if not self.ranked[r]:
+            return
+        kc = self.kcnt[r]
+        lo, hi = (kmin, kmax) if kc is None else (min(kmin, self.kbase[r]),
+                                                 max(kmax, self.kbase[r] + kc.numel() - 1))
+        if hi - lo + 1 > _MAX_DENSE:
+            self.ranked[r] = False
+            self.kcnt[r] = None
+            self._tab_dirty = True
+            return
+        if kc is not None and lo == self.kbase[r] and hi - lo + 1 <= kc.numel():
+            return
+        size = _next_pow2(hi - lo + 1) if kc is None else max(_next_pow2(hi - lo + 1), kc.numel())
+        size = min(size, _MAX_DENSE) if hi - lo + 1 <= _MAX_DENSE else hi - lo + 1
+        nc = torch.zeros(size, dtype=torch.int32, device=self.device)
+        if kc is not None:
+            o = self.kbase[r] - lo
+            nc[o:o + kc.numel()].copy_(kc)
+        self.kcnt[r], self.kbase[r] = nc, lo
+        self._tab_dirty = True
 
     def _ensure_capacity(self, r: int, extra: int) -> None:
         need = self.fill[r] + extra
@@ -100,21 +138,28 @@ class KeyedListWindowOperator:
         cap = _next_pow2(max(need, 1 << 12))
         nk = torch.empty(cap, dtype=torch.int64, device=self.device)
         nv = torch.empty(cap, dtype=torch.int64, device=self.device)
+        nr = torch.empty(cap, dtype=torch.int32, device=self.device)
         f = self.fill[r]
         if kb is not None and f:
             nk[:f].copy_(kb[:f])
             nv[:f].copy_(self.vbuf[r][:f])
-        self.kbuf[r], self.vbuf[r] = nk, nv
+            nr[:f].copy_(self.rbuf[r][:f])
+        self.kbuf[r], self.vbuf[r], self.rbuf[r] = nk, nv, nr
         self._tab_dirty = True
 
     def _sync_tab(self) -> None:
         if not self._tab_dirty:
             return
-        addr = [0] * (2 * self.ring)
-        for r in range(self.ring):
+        R = self.ring
+        addr = [0] * (5 * R)
+        for r in range(R):
             if self.kbuf[r] is not None:
                 addr[r] = self.kbuf[r].data_ptr()
-                addr[self.ring + r] = self.vbuf[r].data_ptr()
+                addr[R + r] = self.vbuf[r].data_ptr()
+                addr[2 * R + r] = self.rbuf[r].data_ptr()
+            if self.ranked[r] and self.kcnt[r] is not None:
+                addr[3 * R + r] = self.kcnt[r].data_ptr()
+                addr[4 * R + r] = self.kbase[r]
         self._tab.copy_(torch.tensor(addr, dtype=torch.int64))
         self._tab_dirty = False
 
@@ -179,6 +224,7 @@ class KeyedListWindowOperator:
             self._ensure_capacity(r, hc[r])
             kr = self.krange[r]
             self.krange[r] = (kmin, kmax) if kr is None else (min(kr[0], kmin), max(kr[1], kmax))
+            self._ensure_key_range(r, kmin, kmax)
             touched_panes.append(p)
         self._sync_tab()
         cursor = torch.tensor(self.fill, dtype=torch.int64).to(self.device, non_blocking=True)
@@ -242,6 +288,9 @@ class KeyedListWindowOperator:
                 self.slot_pane[r] = None
                 self.fill[r] = 0
                 self.krange[r] = None
+                self.kcnt[r] = None  # a new pane in this slot starts its counts afresh
+                self.ranked[r] = True
+                self._tab_dirty = True
 
     def _window_panes(self, s: int) -> list[int]:
         p0 = self._pane_of(s)
@@ -260,7 +309,15 @@ class KeyedListWindowOperator:
         total = sum(self.fill[r] for r in slots)
         kmin = min(self.krange[r][0] for r in slots)
         kmax = max(self.krange[r][1] for r in slots)
-        if kmin >= 0 and kmax - kmin < _MAX_DENSE and len(slots) <= 64:
+        ranked = len(slots) <= 32 and all(self.ranked[r] and self.kcnt[r] is not None
+                                          for r in slots)
+        if ranked:
+            rlo = min(self.kbase[r] for r in slots)
+            rhi = max(self.kbase[r] + self.kcnt[r].numel() for r in slots)
+            ranked = rhi - rlo <= _MAX_DENSE
+        if ranked:
+            keys_out, med = self._median_ranked(slots, rlo, rhi - rlo, total)
+        elif kmin >= 0 and kmax - kmin < _MAX_DENSE and len(slots) <= 64:
             keys_out, med = self._median_dense(slots, kmin, kmax - kmin + 1, total)
         else:
             keys_out, med = self._median_mapped(slots)
@@ -271,6 +328,37 @@ class KeyedListWindowOperator:
             return []
         self.metrics.num_records_out += int(keys_out.numel())
         return [(s, s + self.size, keys_out.cpu().numpy(), med.cpu().numpy())]
+
+    def _median_ranked(self, slots, kmin: int, nk: int, total: int):
+        """Ranked firing: per-key totals and per-pane prefixes from the panes' counts, the
+        order-preserving scan, then every element placed at segment start + prefix + rank (no
+        atomics), then the per-segment median."""
+        m, st, dev = self._m, self._stream(), self.device
+        panes = [(self.kbuf[r].data_ptr(), self.vbuf[r].data_ptr(), self.rbuf[r].data_ptr(),
+                  self.kcnt[r].data_ptr(), self.kbase[r], self.kcnt[r].numel(), self.fill[r])
+                 for r in slots]
+        tot = torch.empty(nk, dtype=torch.int32, device=dev)
+        pre = torch.empty(len(slots) * nk, dtype=torch.int32, device=dev)
+        m.lw_rank_prefix(self.cuda, panes, kmin, nk, tot.data_ptr(), pre.data_ptr(), st)
+        offs = torch.empty(nk + 1, dtype=torch.int64, device=dev)
+        heads = torch.empty(nk, dtype=torch.int64, device=dev)
+        hkeys = torch.empty(nk, dtype=torch.int64, device=dev)
+        nh = torch.zeros(1, dtype=torch.int64, device=dev)
+        scratch = torch.empty(max(16, m.lw_scan_scratch_bytes(nk)), dtype=torch.uint8, device=dev)
+        m.lw_scan(self.cuda, tot.data_ptr(), nk, kmin, scratch.data_ptr(), offs.data_ptr(),
+                  heads.data_ptr(), hkeys.data_ptr(), nh.data_ptr(), st)
+        ordv = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+        m.lw_rank_scatter(self.cuda, panes, kmin, nk, offs.data_ptr(), pre.data_ptr(),
+                          ordv.data_ptr(), st)
+        k = int(nh.item())
+        med = torch.empty(k, dtype=torch.float64, device=dev)
+        if k:
+            args = (heads.data_ptr(), k, total, ordv.data_ptr(), med.data_ptr())
+            if self.cuda:
+                m.gpu_segment_median_select(*args, st)
+            else:
+                m.cpu_segment_median_select(*args)
+        return hkeys[:k], med
 
     def _median_dense(self, slots, kmin: int, nk: int, total: int):
         m, st, dev = self._m, self._stream(), self.device
@@ -381,4 +469,5 @@ class KeyedListWindowOperator:
             self.vbuf[r][:f].copy_(torch.from_numpy(vals[sel]))
             self.fill[r] = f
             self.krange[r] = (int(keys[sel].min()), int(keys[sel].max()))
+            self.ranked[r] = False  # no element ranks in the checkpoint: counting-sort firing
         self._tab_dirty = True

@@ -180,3 +180,16 @@ def test_gpu_arena_median_equals_cpu_and_torch(gpu_device, size, slide, lateness
             n = ref.numel()
             want = float(ref[n // 2]) if n % 2 else float((ref[n // 2 - 1] + ref[n // 2]) / 2)
             assert med == want
+
+
+def test_wide_key_range_takes_the_mapped_firing():
+    """Keys spread over 2^40 ids record no ranks (the per-key counts would not fit) and fire
+    through dense ids from torch.unique: same medians as the oracle."""
+    k, t, v = _events(3000, 29, 20_000, seed=9)
+    big = (k * (1 << 35) + 7).astype(np.int64)
+    op, rows = _run_op("cpu", big, t, v, size=4000, slide=4000, lateness=0, steps=5)
+    got = {(s, key): m for s, e, key, m in rows}
+    ref = {(s, key * (1 << 35) + 7): m for (s, key), m in _oracle(k, t, v, 4000, 4000).items()}
+    assert got == ref
+    assert not any(op.ranked[r] for r, p in enumerate(op.slot_pane) if p is not None) or \
+        all(p is None for p in op.slot_pane)
