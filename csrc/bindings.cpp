@@ -937,4 +937,5 @@ PYBIND11_MODULE(_mxs_native, m) {
   bind_reader(m);
   bind_format(m);
   bind_listwin(m);
+  bind_window_tier(m);
 }

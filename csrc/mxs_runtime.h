@@ -11,3 +11,4 @@ void bind_check(pybind11::module_& m);
 void bind_reader(pybind11::module_& m);
 void bind_format(pybind11::module_& m);
 void bind_listwin(pybind11::module_& m);
+void bind_window_tier(pybind11::module_& m);

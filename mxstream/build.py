@@ -28,7 +28,7 @@ HIP_SOURCES = ["kernels_hip.hip", "sort_hip.hip", "parse_hip.hip", "vector_hip.h
                "check_hip.hip", "rolling_hist_hip.hip", "ingest_hip.hip", "listwin_hip.hip"]
 CXX_SOURCES = ["kernels_cpu.cpp", "ingest_cpu.cpp", "runtime.cpp", "sessions.cpp", "vector_cpu.cpp",
                "vector_bindings.cpp", "trace.cpp", "check_cpu.cpp", "reader.cpp", "format.cpp", "listwin_cpu.cpp",
-               "listwin_bindings.cpp",
+               "listwin_bindings.cpp", "window_tier_bindings.cpp",
                "bindings.cpp"]
 # roctx ranges (csrc/trace.cpp) come from the ROCm profiler SDK's marker library.
 LINK_LIBS = ["-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]

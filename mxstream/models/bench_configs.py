@@ -198,6 +198,59 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
             "events_per_step": batch, "state_bytes": op.state_bytes(), "device": str(dev)}
 
 
+def config4_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 1_000_000,
+                  drift: int = 100_000, table_keys: int = 2_000_000, device: str = "cuda") -> dict:
+    """Config 4's sliding 1 min / 10 s window + 30 s lateness over a key space that outgrows the
+    HBM table: each step draws its events from `active` consecutive key ids whose range moves by
+    `drift` per step, so the keys live during a window's lifetime (90 s = 45 steps) number
+    active + 45 * drift = 5.5M against a table sized for `table_keys` = 2M (>= 2x over). Hashed
+    keyed state with the host-DRAM tier: every 4 steps, sub-tables above 80 % load evict the keys
+    whose newest data is more than one pane old (window_compact -> C++ tier); firings combine the
+    tier's share of the window on the host. Reports events/s and the tier's size."""
+    dev = torch.device(device)
+    span = 2_000
+    mbps = E.var(E.VAR_RESULT) * 8.0 / 60 / 1024 / 1024
+    op = KeyedWindowOperator(size=60_000, slide=10_000, lateness=30_000, agg=K.AGG_SUM_I64,
+                             device=dev, max_keys=table_keys, batch_capacity=batch,
+                             ooo_bound=5_000, map_prog=E.compile_expr(mbps),
+                             filter_prog=E.compile_expr(E.var(E.VAR_MAPPED) < 1e-4),
+                             dense_keys=False, spill=True, spill_keep_panes=1,
+                             spill_check_steps=4)
+    kt = torch.empty(batch, dtype=torch.int64, device=dev)
+    tt = torch.empty_like(kt)
+    vt = torch.empty_like(kt)
+    step_i = [0]
+
+    def step():
+        i = step_i[0]
+        K.gen_events(kt, tt, vt, seed=41, stream_id=0, idx0=i * batch, nkeys=active,
+                     ts_base=i * span, ts_span=span, disorder=2_000, val_lo=0, val_span=20_000)
+        kt.add_(i * drift)
+        fired = op.process(kt, tt, vt)
+        step_i[0] += 1
+        return sum(len(r.keys) for r in fired)
+
+    for _ in range(warmup):
+        step()
+    _sync(dev)
+    t0 = time.perf_counter()
+    alerts = 0
+    for _ in range(steps):
+        alerts += step()
+    alerts += sum(len(r.keys) for r in op.flush())
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    ex = op.metrics.extra
+    return {"config": "4-spill", "metric": "events/sec (sliding 1min/10s + lateness, key space "
+            "outgrowing HBM, host-DRAM tier)", "value": batch * steps / dt, "unit": "events/s",
+            "ms_per_step": dt / steps * 1e3, "alerts": alerts, "events_per_step": batch,
+            "table_keys": table_keys, "live_keys_per_window": active + 45 * drift,
+            "spilled_keys": ex.get("spilled_keys", 0), "spilled_rows": ex.get("spilled_rows", 0),
+            "dropped_keys": ex.get("dropped_keys", 0), "host_tier_rows": op.host_tier.nrows,
+            "host_tier_bytes": op.host_tier.nbytes, "hbm_state_bytes": op.state_bytes(),
+            "device": str(dev)}
+
+
 def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_000,
             drift: int = 400_000, table_keys: int = 4_000_000, device: str = "cuda",
             revisit: float = 0.0, promote: bool = True) -> dict:
@@ -488,6 +541,8 @@ def main(argv=None) -> int:
     ap.add_argument("--zipf", type=float, default=0.0, help="config 6: power-law key skew")
     ap.add_argument("--host-fold", action="store_true",
                     help="config 5: fold records of spilled keys in host DRAM (no promotion to HBM)")
+    ap.add_argument("--spill", action="store_true",
+                    help="config 4: key space outgrowing the HBM table (host-DRAM tier)")
     ap.add_argument("--revisit", type=float, default=0.0,
                     help="config 5: fraction of events for spilled (long idle) keys")
     ap.add_argument("--steps", type=int, default=20)
@@ -511,6 +566,8 @@ def main(argv=None) -> int:
     elif a.config == 2:
         r = config2(a.steps, a.warmup, a.batch or (1 << 24), device=a.device,
                     dense_keys=not a.hashed_keys, sort_free=not a.sort_path)
+    elif a.config == 4 and a.spill:
+        r = config4_spill(a.steps, a.warmup, a.batch or (1 << 22), device=a.device)
     elif a.config == 4:
         r = config4(a.steps, a.warmup, a.batch or (1 << 24), device=a.device,
                     dense_keys=not a.hashed_keys)

@@ -1043,9 +1043,11 @@ class KeyedWindowOperator:
             raise RuntimeError("window_compact: eviction rows overflowed (internal error)")
         n = ctr[3]
         if n and self.host_tier is not None:
-            self.host_tier.absorb(o["key"][:n].cpu().numpy().view(np.uint64),
-                                  o["pane"][:n].cpu().numpy(), o["acc"][:n].cpu().numpy(),
-                                  o["cnt"][:n].cpu().numpy(), o["dirty"][:n].cpu().numpy())
+            # One copy of the five columns into a pinned slab (one sync), appended to the C++
+            # tier as a chunk.
+            h = to_host_arrays([o["key"], o["pane"], o["acc"], o["cnt"], o["dirty"]], n,
+                               self._pool)
+            self.host_tier.absorb(h[0].view(np.uint64), h[1], h[2], h[3], h[4])
         # (Touched-slot lists and dirty bytes are empty here: every step's re-firings cleared
         # them before this step boundary, so no slot id survives the rehash.)
         ex = self.metrics.extra
@@ -1186,8 +1188,9 @@ class KeyedWindowOperator:
         if only_dirty and n == 0:
             return None
         keys, vals, raw, cnt = merge_fire(self.agg, dk.view(np.uint64), dr, dc,
-                                          self.host_tier.part(p0, p1), only_dirty,
-                                          self.map_prog, self.filter_prog, s, s + self.size)
+                                          self.host_tier, only_dirty,
+                                          self.map_prog, self.filter_prog, s, s + self.size,
+                                          panes=(p0, p1))
         if not keys.size:
             return None
         self.metrics.num_records_out += int(keys.size)

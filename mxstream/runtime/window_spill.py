@@ -10,8 +10,10 @@ device fires without its epilogue, this tier's part of the same window is combin
 (every aggregate is associative), and the map/filter epilogue is evaluated on the host with the
 fire kernel's expression-VM semantics (``expr.eval_numpy``).
 
-The tier is columnar rows (key, pane, acc, cnt, dirty) in numpy arrays, merged per (key, pane)
-lazily; it is purged with the device's panes.
+The tier itself is C++ (csrc/window_tier.h): evicted rows (key, pane, acc, cnt, dirty) are
+appended as chunks (no re-concatenation per eviction), a firing hash-combines the chunks that
+overlap its panes, a purge drops whole chunks below the live range; rows are merged per
+(key, pane) only for a snapshot.
 """
 from __future__ import annotations
 
@@ -61,55 +63,37 @@ def result_values(agg: int, raw: np.ndarray, cnt: np.ndarray) -> np.ndarray:
 
 
 class HostWindowTier:
-    def __init__(self, agg: int):
-        self.agg = agg
-        self._cols = self._empty()
-        self._merged = 0          # rows [0, _merged) are unique per (key, pane)
-        self.rows_in = 0
+    """Thin wrapper of the C++ tier (csrc/window_tier.h): append-only chunks of evicted rows,
+    hash-combined per key for a firing, whole chunks dropped by a purge."""
 
-    @staticmethod
-    def _empty():
-        return {"key": np.zeros(0, np.uint64), "pane": np.zeros(0, np.int64),
-                "acc": np.zeros(0, np.int64), "cnt": np.zeros(0, np.int64),
-                "dirty": np.zeros(0, np.uint8)}
+    def __init__(self, agg: int, _core=None):
+        from ..ops.native import load
+
+        self.agg = agg
+        self._t = _core if _core is not None else load().WindowTier(agg)
 
     @property
     def nrows(self) -> int:
-        return int(self._cols["key"].size)
+        return int(self._t.nrows)
 
     @property
     def nbytes(self) -> int:
-        return sum(v.nbytes for v in self._cols.values())
+        return int(self._t.nbytes)
+
+    @property
+    def rows_in(self) -> int:
+        return int(self._t.rows_in)
 
     def absorb(self, key, pane, acc, cnt, dirty) -> None:
-        c = self._cols
-        self._cols = {"key": np.concatenate([c["key"], key.astype(np.uint64)]),
-                      "pane": np.concatenate([c["pane"], pane.astype(np.int64)]),
-                      "acc": np.concatenate([c["acc"], acc.astype(np.int64)]),
-                      "cnt": np.concatenate([c["cnt"], cnt.astype(np.int64)]),
-                      "dirty": np.concatenate([c["dirty"], dirty.astype(np.uint8)])}
-        self.rows_in += int(key.size)
-        if self.nrows > 2 * max(self._merged, 1 << 16):
-            self._merge()
-
-    def _merge(self) -> None:
-        """Fold rows of the same (key, pane) (a key evicted, re-inserted and evicted again)."""
-        c = self._cols
-        if not c["key"].size:
-            self._merged = 0
-            return
-        order = np.lexsort((c["key"], c["pane"]))
-        k, p = c["key"][order], c["pane"][order]
-        starts = np.flatnonzero(np.r_[True, (k[1:] != k[:-1]) | (p[1:] != p[:-1])])
-        self._cols = {"key": k[starts], "pane": p[starts],
-                      "acc": _reduce(self.agg, c["acc"][order], starts),
-                      "cnt": np.add.reduceat(c["cnt"][order], starts),
-                      "dirty": np.maximum.reduceat(c["dirty"][order], starts)}
-        self._merged = self.nrows
+        self._t.absorb(np.ascontiguousarray(key).view(np.uint64) if key.dtype == np.int64
+                       else np.ascontiguousarray(key, dtype=np.uint64),
+                       np.ascontiguousarray(pane, dtype=np.int64),
+                       np.ascontiguousarray(acc, dtype=np.int64),
+                       np.ascontiguousarray(cnt, dtype=np.int64),
+                       np.ascontiguousarray(dirty, dtype=np.uint8))
 
     def pane_range(self) -> tuple[int, int] | None:
-        p = self._cols["pane"]
-        return (int(p.min()), int(p.max())) if p.size else None
+        return self._t.pane_range()
 
     def overlaps(self, p0: int, p1: int) -> bool:
         r = self.pane_range()
@@ -117,44 +101,42 @@ class HostWindowTier:
 
     def part(self, p0: int, p1: int):
         """This tier's share of the window over panes [p0, p1]: (keys, acc, cnt) per key."""
-        c = self._cols
-        sel = (c["pane"] >= p0) & (c["pane"] <= p1)
-        return combine_rows(self.agg, c["key"][sel], c["acc"][sel], c["cnt"][sel])
+        return self._t.part(int(p0), int(p1))
 
     def purge(self, keep_from: int) -> None:
-        c = self._cols
-        if c["pane"].size and int(c["pane"].min()) < keep_from:
-            sel = c["pane"] >= keep_from
-            self._cols = {k: v[sel] for k, v in c.items()}
-            self._merged = min(self._merged, self.nrows)
+        self._t.purge(int(keep_from))
 
     def rows(self) -> dict:
-        self._merge()
-        return {k: v.copy() for k, v in self._cols.items()}
+        return self._t.rows()
 
     def clear(self) -> None:
-        self._cols = self._empty()
-        self._merged = 0
+        self._t.clear()
 
     def copy(self) -> "HostWindowTier":
         """An independent copy (the frozen tier of an asynchronous snapshot)."""
-        t = HostWindowTier(self.agg)
-        t._cols = {k: v.copy() for k, v in self._cols.items()}
-        t._merged, t.rows_in = self._merged, self.rows_in
-        return t
+        return HostWindowTier(self.agg, _core=self._t.copy())
 
 
-def merge_fire(agg: int, dev_keys, dev_raw, dev_cnt, host_part, only_dirty: bool,
-               map_prog: E.Program, filter_prog: E.Program, wstart: int, wend: int):
+def merge_fire(agg: int, dev_keys, dev_raw, dev_cnt, host, only_dirty: bool,
+               map_prog: E.Program, filter_prog: E.Program, wstart: int, wend: int,
+               panes: tuple[int, int] | None = None):
     """Device rows (no epilogue) + the host tier's part of the same window -> the epilogue's
-    (keys, values, raw, counts). A re-firing covers only the device's dirty keys."""
-    hk, hacc, hcnt = host_part
-    if only_dirty and hk.size:
-        sel = np.isin(hk, dev_keys)
-        hk, hacc, hcnt = hk[sel], hacc[sel], hcnt[sel]
-    keys, raw, cnt = combine_rows(agg, np.concatenate([dev_keys.astype(np.uint64), hk]),
-                                  np.concatenate([dev_raw.astype(np.int64), hacc]),
-                                  np.concatenate([dev_cnt.astype(np.int64), hcnt]))
+    (keys, values, raw, counts). A re-firing covers only the device's dirty keys.
+    host: a HostWindowTier (combined in C++ with the device rows over `panes`) or an already
+    combined (keys, acc, cnt) part."""
+    if isinstance(host, HostWindowTier):
+        keys, raw, cnt = host._t.merge_fire(
+            int(panes[0]), int(panes[1]), np.ascontiguousarray(dev_keys, dtype=np.uint64),
+            np.ascontiguousarray(dev_raw, dtype=np.int64),
+            np.ascontiguousarray(dev_cnt, dtype=np.int64), bool(only_dirty))
+    else:
+        hk, hacc, hcnt = host
+        if only_dirty and hk.size:
+            sel = np.isin(hk, dev_keys)
+            hk, hacc, hcnt = hk[sel], hacc[sel], hcnt[sel]
+        keys, raw, cnt = combine_rows(agg, np.concatenate([dev_keys.astype(np.uint64), hk]),
+                                      np.concatenate([dev_raw.astype(np.int64), hacc]),
+                                      np.concatenate([dev_cnt.astype(np.int64), hcnt]))
     res = result_values(agg, raw, cnt)
     vars_ = [res, cnt.astype(np.float64), float(wstart), float(wend), keys.astype(np.float64),
              raw.astype(np.float64), res, 0.0]

@@ -558,3 +558,43 @@ def test_key_value_rows_equal_full_rows(size, slide, lateness):
     full = run("full")
     assert len(full) > 1000
     assert run("key_value") == full
+
+
+def test_cxx_window_tier_equals_numpy_combine():
+    """csrc/window_tier.h: chunked absorb, per-key part() and the tiered merge_fire equal the
+    numpy combine of the same rows; purge drops exactly the rows below the cutoff."""
+    from mxstream.runtime.window_spill import HostWindowTier, combine_rows, merge_fire
+
+    rng = np.random.default_rng(4)
+    t = HostWindowTier(K.AGG_SUM_I64)
+    cols = {k: [] for k in ("key", "pane", "acc", "cnt", "dirty")}
+    for _ in range(5):  # evictions -> chunks (a key may be evicted twice)
+        n = 4000
+        c = {"key": rng.integers(0, 3000, n).astype(np.uint64),
+             "pane": rng.integers(10, 20, n).astype(np.int64),
+             "acc": rng.integers(-1000, 1000, n).astype(np.int64),
+             "cnt": rng.integers(1, 5, n).astype(np.int64),
+             "dirty": rng.integers(0, 2, n).astype(np.uint8)}
+        t.absorb(c["key"], c["pane"], c["acc"], c["cnt"], c["dirty"])
+        for k in cols:
+            cols[k].append(c[k])
+    cols = {k: np.concatenate(v) for k, v in cols.items()}
+    assert t.nrows == cols["key"].size and t.pane_range() == (10, 19)
+    sel = (cols["pane"] >= 12) & (cols["pane"] <= 15)
+    k, a, c = t.part(12, 15)
+    ek, ea, ec = combine_rows(K.AGG_SUM_I64, cols["key"][sel], cols["acc"][sel], cols["cnt"][sel])
+    assert np.array_equal(k, ek) and np.array_equal(a, ea) and np.array_equal(c, ec)
+    dk = np.arange(0, 3500, 7, dtype=np.uint64)
+    dr = rng.integers(0, 100, dk.size).astype(np.int64)
+    dc = np.ones(dk.size, np.int64)
+    for only in (False, True):
+        got = merge_fire(K.AGG_SUM_I64, dk, dr, dc, t, only, E.EMPTY, E.EMPTY, 0, 1,
+                         panes=(12, 15))
+        ref = merge_fire(K.AGG_SUM_I64, dk, dr, dc, (k, a, c), only, E.EMPTY, E.EMPTY, 0, 1)
+        o1, o2 = np.argsort(got[0]), np.argsort(ref[0])
+        for x, y in zip(got, ref):
+            assert np.array_equal(np.asarray(x)[o1], np.asarray(y)[o2])
+    t.purge(15)
+    assert t.nrows == int((cols["pane"] >= 15).sum()) and t.pane_range() == (15, 19)
+    r = t.rows()
+    assert int(r["cnt"].sum()) == int(cols["cnt"][cols["pane"] >= 15].sum())
