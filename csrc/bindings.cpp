@@ -518,43 +518,13 @@ PYBIND11_MODULE(_mxs_native, m) {
                                       intptr_t spill_set, uint32_t spill_mask, int spill_any,
                                       intptr_t sk, intptr_t vals, intptr_t n_out,
                                       intptr_t host_recs, intptr_t n_host, uint32_t host_cap,
-                                      intptr_t n_ins, int tbits, intptr_t stream, py::object merge) {
-    // merge: None, or (gap, lateness, wm, tbase, agg, nslots, sess, slot_due, slot_last,
-    // late_cnt, ovf_slots, n_ovf, ovf_rows, n_ovf_runs, ovf_cap, long_heads, n_long)
-    gpu::SessMergeArgs ma{};
-    const gpu::SessMergeArgs* mp = nullptr;
-    if (!merge.is_none()) {
-      py::tuple t = merge.cast<py::tuple>();
-      if (t.size() != 17) throw std::invalid_argument("session merge args: 17 fields");
-      ma.gap = t[0].cast<int64_t>();
-      ma.lateness = t[1].cast<int64_t>();
-      ma.wm = t[2].cast<int64_t>();
-      ma.tbase = t[3].cast<int64_t>();
-      ma.agg = t[4].cast<int32_t>();
-      ma.nslots = t[5].cast<int64_t>();
-      ma.sess = P<int64_t>(t[6].cast<intptr_t>());
-      ma.slot_due = P<int64_t>(t[7].cast<intptr_t>());
-      ma.slot_last = P<int64_t>(t[8].cast<intptr_t>());
-      ma.late_cnt = P<uint64_t>(t[9].cast<intptr_t>());
-      ma.ovf_slots = P<int64_t>(t[10].cast<intptr_t>());
-      ma.n_ovf = P<uint32_t>(t[11].cast<intptr_t>());
-      ma.ovf_rows = P<int64_t>(t[12].cast<intptr_t>());
-      ma.n_ovf_runs = P<uint32_t>(t[13].cast<intptr_t>());
-      ma.ovf_cap = t[14].cast<uint32_t>();
-      ma.long_heads = P<uint32_t>(t[15].cast<intptr_t>());
-      ma.n_long = P<uint32_t>(t[16].cast<intptr_t>());
-      mp = &ma;
-    }
+                                      intptr_t n_ins, int tbits, intptr_t stream) {
     return gpu::session_lookup_sort(P<Rec>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2,
                                     P<uint64_t>(keys_g), P<uint64_t>(spill_set), spill_mask,
                                     spill_any, P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_out),
                                     P<Rec>(host_recs), P<uint32_t>(n_host), host_cap,
-                                    P<uint32_t>(n_ins), tbits, stream, mp);
-  }, py::arg("recs"), py::arg("counts"), py::arg("nsrc"), py::arg("nsub"), py::arg("bcap"),
-     py::arg("cap_log2"), py::arg("keys_g"), py::arg("spill_set"), py::arg("spill_mask"),
-     py::arg("spill_any"), py::arg("sk"), py::arg("vals"), py::arg("n_out"),
-     py::arg("host_recs"), py::arg("n_host"), py::arg("host_cap"), py::arg("n_ins"),
-     py::arg("tbits"), py::arg("stream"), py::arg("merge") = py::none());
+                                    P<uint32_t>(n_ins), tbits, stream);
+  });
   m.def("gpu_session_heads", [](intptr_t sk, intptr_t n_in, int64_t n_cap, intptr_t heads,
                                 intptr_t n_heads, intptr_t stream) {
     gpu::session_heads(P<int64_t>(sk), P<uint32_t>(n_in), n_cap, P<uint32_t>(heads),

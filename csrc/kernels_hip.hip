@@ -2505,6 +2505,171 @@ __global__ __launch_bounds__(kSessLookupBlock) void session_lookup_lds_kernel(
   if (threadIdx.x == 0 && n_inserted && lins) atomicAdd(n_inserted, lins);
 }
 
+// Fused lookup + LDS-staged segmented sort (the session fold's replacement for a device-wide
+// radix sort). Records arrive bucketed by sub-table, so the global (slot, ts) order is just every
+// sub-table's records in (local slot, ts) order: one workgroup per sub-table
+//   1. looks its records up in the LDS-staged slot table (insert / divert exactly as
+//      session_lookup_lds) and keeps (local slot << 32 | t) per record in LDS, in arrival order;
+//   2. writes the table back, then counts records per local slot (u16 LDS histogram in the
+//      table's space), scans the counts and scatters record indices into slot segments;
+//   3. ranks every record inside its slot segment by (t, arrival index) -- segments are short
+//      (a few records per key and step), a hot key's long segment costs O(len^2) LDS reads in
+//      its own workgroup only -- and writes (slot << tbits | t, value) at
+//      block base + segment start + rank.
+// The output equals a stable sort of session_lookup's keys with the holes removed, so
+// session_merge runs on it unchanged. LDS: max(cap*8, cap*2 + m*2) + m*8 bytes for m records.
+constexpr int kSessSortBlock = 1024;
+
+__global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
+    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
+    uint32_t bucket_cap, int cap_log2, uint64_t* __restrict__ keys_g,
+    uint64_t* __restrict__ spill_set, uint32_t spill_mask, int32_t spill_any,
+    int64_t* __restrict__ sort_out, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
+    Rec* __restrict__ host_recs, uint32_t* __restrict__ n_host, uint32_t host_cap,
+    uint32_t* __restrict__ n_inserted, int tbits, uint32_t m_cap) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t slds[];
+  __shared__ uint32_t s_base, s_lins, s_kept, s_m;
+  __shared__ uint32_t s_src_off[65];
+  const int sub = blockIdx.x;
+  const uint32_t cap = 1u << cap_log2, mask = cap - 1;
+  const uint32_t regA = (cap * 8 > cap * 2 + m_cap * 2 ? cap * 8 : cap * 2 + m_cap * 2);
+  uint64_t* lkeys = slds;                                              // phase 1: slot table
+  uint16_t* cur = reinterpret_cast<uint16_t*>(slds);                   // phase 2: per-slot cursors
+  // (u16 cursors, two per 32-bit word: the atomics add 1 << 16 * (slot & 1) to the word; a
+  // block holds < 65536 records, so a half never carries into the other)
+  uint32_t* cur32 = reinterpret_cast<uint32_t*>(slds);
+  uint16_t* idxl = cur + cap;                                          // phase 2: slot segments
+  uint64_t* rk = slds + regA / 8;                                      // (slot << 32 | t) per record
+  uint64_t* gkeys = keys_g + ((size_t)sub << cap_log2);
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) lkeys[i] = gkeys[i];
+  if (threadIdx.x == 0) {
+    uint32_t tot = 0;
+    for (int src = 0; src < nsrc; ++src) {
+      s_src_off[src] = tot;
+      const uint32_t c = counts[src * nsub + sub];
+      tot += c < bucket_cap ? c : bucket_cap;
+    }
+    s_src_off[nsrc] = tot;
+    s_m = tot;
+    s_lins = 0;
+    s_kept = 0;
+  }
+  __syncthreads();
+  const uint32_t m = s_m;  // the launcher sized m_cap >= nsrc * bucket_cap >= m
+  // Phase 1: lookup / insert / divert; rk[i] = (local slot << 32 | t) or ~0 (not folded here).
+  uint32_t kept = 0;
+  for (int src = 0; src < nsrc; ++src) {
+    const int b = src * nsub + sub;
+    const uint32_t c = s_src_off[src + 1] - s_src_off[src];
+    const Rec* seg = recs + (size_t)b * bucket_cap;
+    for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
+      const Rec r = seg[e];
+      uint64_t v = ~0ull;
+      if (r.t != 0xFFFFFFFFu) {
+        uint32_t sl = sess_find<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask);
+        bool to_host = sl == kNoSlot && spill_any && set_contains(spill_set, spill_mask, r.key);
+        if (!to_host && sl == kNoSlot) {
+          sl = sess_probe_insert<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask, &s_lins);
+          if (sl == kNoSlot) {  // sub-table full: the key lives in host DRAM from now on
+            to_host = true;
+            set_insert(spill_set, spill_mask, r.key);
+          }
+        }
+        if (to_host) {
+          const uint32_t q = atomicAdd(n_host, 1u);
+          if (q < host_cap) host_recs[q] = r;
+        } else {
+          v = ((uint64_t)sl << 32) | r.t;
+          ++kept;
+        }
+      }
+      rk[s_src_off[src] + e] = v;
+    }
+  }
+  if (kept) atomicAdd(&s_kept, kept);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) gkeys[i] = lkeys[i];
+  if (threadIdx.x == 0) {
+    if (n_inserted && s_lins) atomicAdd(n_inserted, s_lins);
+    s_base = s_kept ? atomicAdd(n_out, s_kept) : 0u;
+  }
+  __syncthreads();
+  // Phase 2: per-slot counts -> exclusive offsets -> segments of record indices.
+  for (uint32_t i = threadIdx.x; i < cap / 2; i += blockDim.x) cur32[i] = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+    const uint64_t v = rk[i];
+    if (v != ~0ull) {
+      const uint32_t sl = (uint32_t)(v >> 32);
+      atomicAdd(&cur32[sl >> 1], 1u << ((sl & 1u) * 16));
+    }
+  }
+  __syncthreads();
+  // Block-wide exclusive scan of cap (<= 4096) u16 counts: each thread sums a run of cap/T,
+  // wave prefix with shuffles, wave totals through LDS.
+  {
+    __shared__ uint32_t s_wave[kSessSortBlock / 64];
+    const uint32_t per = (cap + kSessSortBlock - 1) / kSessSortBlock;
+    const uint32_t lo = threadIdx.x * per, hi = lo + per < cap ? lo + per : cap;
+    uint32_t run = 0;
+    for (uint32_t i = lo; i < hi; ++i) run += cur[i];
+    uint32_t incl = run;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d);
+      if (lane_id() >= d) incl += y;
+    }
+    const int w = threadIdx.x >> 6;
+    if (lane_id() == 63) s_wave[w] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t t = 0;
+      for (int i = 0; i < kSessSortBlock / 64; ++i) {
+        const uint32_t c = s_wave[i];
+        s_wave[i] = t;
+        t += c;
+      }
+    }
+    __syncthreads();
+    uint32_t o = s_wave[w] + incl - run;
+    for (uint32_t i = lo; i < hi; ++i) {
+      const uint32_t c = cur[i];
+      cur[i] = (uint16_t)o;
+      o += c;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+    const uint64_t v = rk[i];
+    if (v != ~0ull) {
+      const uint32_t sl = (uint32_t)(v >> 32), sh = (sl & 1u) * 16;
+      const uint32_t pos = (atomicAdd(&cur32[sl >> 1], 1u << sh) >> sh) & 0xFFFFu;
+      idxl[pos] = (uint16_t)i;
+    }
+  }
+  __syncthreads();
+  // Phase 3: rank inside the slot segment [end(slot - 1), end(slot)) by (t, arrival index).
+  const uint64_t sub_slot0 = (uint64_t)sub << cap_log2;
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+    const uint64_t v = rk[i];
+    if (v == ~0ull) continue;
+    const uint32_t sl = (uint32_t)(v >> 32), t = (uint32_t)v;
+    const uint32_t end = cur[sl], start = sl ? cur[sl - 1] : 0u;
+    uint32_t rank = 0;
+    for (uint32_t q = start; q < end; ++q) {
+      const uint32_t j = idxl[q];
+      const uint32_t tj = (uint32_t)rk[j];
+      rank += (tj < t || (tj == t && j < i)) ? 1u : 0u;
+    }
+    // arrival index i -> (source bucket, position) for the value
+    int src = 0;
+    while (src + 1 < nsrc && i >= s_src_off[src + 1]) ++src;
+    const Rec& r = recs[(size_t)(src * nsub + sub) * bucket_cap + (i - s_src_off[src])];
+    const uint32_t out = s_base + start + rank;
+    sort_out[out] = (int64_t)(((sub_slot0 | sl) << tbits) | t);
+    vals_out[out] = r.val;
+  }
+}
+
 __global__ __launch_bounds__(256) void session_heads_kernel(const int64_t* __restrict__ sk,
                                                             const uint32_t* __restrict__ n_in,
                                                             uint32_t* __restrict__ heads,
@@ -2692,42 +2857,6 @@ constexpr uint32_t kSessLongSeg = 96;  // segments longer than this go to the wa
 // records serially, splitting runs at ts gaps > gap. Typical session workloads have a few records
 // per key and step, where a wave per key would idle most lanes. Long segments are queued for
 // session_merge_long_kernel.
-// One key's records [i, j) (ts order) folded into its slot's sessions by one thread: runs
-// closer than the gap become candidates, merged into the resident sessions (sess_commit).
-__device__ __forceinline__ void sess_merge_segment(const int64_t* __restrict__ sk,
-                                                   const uint64_t* __restrict__ vals, uint32_t i,
-                                                   uint32_t j, int64_t slot, const SessArgs& a,
-                                                   const SessOut& o) {
-  const int64_t tmask = ((int64_t)1 << a.tbits) - 1;
-  SessState st;
-  sess_load(st, o.sess + slot * kSess);
-  uint64_t late = 0;
-  bool overflow = false;
-  bool pv = false;
-  int64_t ps = 0, pe = 0;
-  uint64_t pa = 0;
-  uint32_t pc = 0;
-  int64_t ts = 0;
-  for (uint32_t r = i; r < j; ++r) {
-    ts = a.tbase + (sk[r] & tmask);
-    const uint64_t v = agg_lift(a.agg, vals[r]);
-    if (pv && ts <= pe) {
-      pe = ts + a.gap;
-      pa = agg_combine(a.agg, pa, v);
-      pc += 1;
-    } else {
-      if (pv) sess_commit(st, overflow, late, slot, ps, pe, pa, pc, a, o);
-      ps = ts;
-      pe = ts + a.gap;
-      pa = v;
-      pc = 1;
-      pv = true;
-    }
-  }
-  sess_commit(st, overflow, late, slot, ps, pe, pa, pc, a, o);
-  sess_finish(st, slot, ts, late, overflow, a, o);
-}
-
 __global__ __launch_bounds__(256) void session_merge_small_kernel(
     const int64_t* __restrict__ sk,
     const uint64_t* __restrict__ vals, const uint32_t* __restrict__ n_in, SessArgs a, SessOut o,
@@ -2749,7 +2878,33 @@ __global__ __launch_bounds__(256) void session_merge_small_kernel(
       long_heads[atomicAdd(n_long, 1u)] = i;
       continue;
     }
-    sess_merge_segment(sk, vals, i, j, slot, a, o);
+    SessState st;
+    sess_load(st, o.sess + slot * kSess);
+    uint64_t late = 0;
+    bool overflow = false;
+    bool pv = false;
+    int64_t ps = 0, pe = 0;
+    uint64_t pa = 0;
+    uint32_t pc = 0;
+    int64_t ts = 0;
+    for (uint32_t r = i; r < j; ++r) {
+      ts = a.tbase + (sk[r] & tmask);
+      const uint64_t v = agg_lift(a.agg, vals[r]);
+      if (pv && ts <= pe) {
+        pe = ts + a.gap;
+        pa = agg_combine(a.agg, pa, v);
+        pc += 1;
+      } else {
+        if (pv) sess_commit(st, overflow, late, slot, ps, pe, pa, pc, a, o);
+        ps = ts;
+        pe = ts + a.gap;
+        pa = v;
+        pc = 1;
+        pv = true;
+      }
+    }
+    sess_commit(st, overflow, late, slot, ps, pe, pa, pc, a, o);
+    sess_finish(st, slot, ts, late, overflow, a, o);
   }
 }
 
@@ -2842,191 +2997,6 @@ __global__ __launch_bounds__(256) void session_merge_long_kernel(
     }
   }
 }
-
-// Fused lookup + LDS-staged segmented sort (the session fold's replacement for a device-wide
-// radix sort). Records arrive bucketed by sub-table, so the global (slot, ts) order is just every
-// sub-table's records in (local slot, ts) order: one workgroup per sub-table
-//   1. looks its records up in the LDS-staged slot table (insert / divert exactly as
-//      session_lookup_lds) and keeps (local slot << 32 | t) per record in LDS, in arrival order;
-//   2. writes the table back, then counts records per local slot (u16 LDS histogram in the
-//      table's space), scans the counts and scatters record indices into slot segments;
-//   3. ranks every record inside its slot segment by (t, arrival index) -- segments are short
-//      (a few records per key and step), a hot key's long segment costs O(len^2) LDS reads in
-//      its own workgroup only -- and writes (slot << tbits | t, value) at
-//      block base + segment start + rank.
-// The output equals a stable sort of session_lookup's keys with the holes removed (so
-// session_merge could run on it unchanged); with do_merge the same workgroup then folds every
-// slot's segment into its sessions (phase 4), so no separate pass over all records looks for
-// segment heads. LDS: max(cap*8, cap*2 + m*2) + m*8 bytes for m records.
-constexpr int kSessSortBlock = 1024;
-
-__global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
-    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
-    uint32_t bucket_cap, int cap_log2, uint64_t* __restrict__ keys_g,
-    uint64_t* __restrict__ spill_set, uint32_t spill_mask, int32_t spill_any,
-    int64_t* __restrict__ sort_out, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
-    Rec* __restrict__ host_recs, uint32_t* __restrict__ n_host, uint32_t host_cap,
-    uint32_t* __restrict__ n_inserted, int tbits, uint32_t m_cap, int32_t do_merge, SessArgs sa,
-    SessOut so, uint32_t* __restrict__ long_heads, uint32_t* __restrict__ n_long) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t slds[];
-  __shared__ uint32_t s_base, s_lins, s_kept, s_m;
-  __shared__ uint32_t s_src_off[65];
-  const int sub = blockIdx.x;
-  const uint32_t cap = 1u << cap_log2, mask = cap - 1;
-  const uint32_t regA = (cap * 8 > cap * 2 + m_cap * 2 ? cap * 8 : cap * 2 + m_cap * 2);
-  uint64_t* lkeys = slds;                                              // phase 1: slot table
-  uint16_t* cur = reinterpret_cast<uint16_t*>(slds);                   // phase 2: per-slot cursors
-  // (u16 cursors, two per 32-bit word: the atomics add 1 << 16 * (slot & 1) to the word; a
-  // block holds < 65536 records, so a half never carries into the other)
-  uint32_t* cur32 = reinterpret_cast<uint32_t*>(slds);
-  uint16_t* idxl = cur + cap;                                          // phase 2: slot segments
-  uint64_t* rk = slds + regA / 8;                                      // (slot << 32 | t) per record
-  uint64_t* gkeys = keys_g + ((size_t)sub << cap_log2);
-  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) lkeys[i] = gkeys[i];
-  if (threadIdx.x == 0) {
-    uint32_t tot = 0;
-    for (int src = 0; src < nsrc; ++src) {
-      s_src_off[src] = tot;
-      const uint32_t c = counts[src * nsub + sub];
-      tot += c < bucket_cap ? c : bucket_cap;
-    }
-    s_src_off[nsrc] = tot;
-    s_m = tot;
-    s_lins = 0;
-    s_kept = 0;
-  }
-  __syncthreads();
-  const uint32_t m = s_m;  // the launcher sized m_cap >= nsrc * bucket_cap >= m
-  // Phase 1: lookup / insert / divert; rk[i] = (local slot << 32 | t) or ~0 (not folded here).
-  uint32_t kept = 0;
-  for (int src = 0; src < nsrc; ++src) {
-    const int b = src * nsub + sub;
-    const uint32_t c = s_src_off[src + 1] - s_src_off[src];
-    const Rec* seg = recs + (size_t)b * bucket_cap;
-    for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
-      const Rec r = seg[e];
-      uint64_t v = ~0ull;
-      if (r.t != 0xFFFFFFFFu) {
-        uint32_t sl = sess_find<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask);
-        bool to_host = sl == kNoSlot && spill_any && set_contains(spill_set, spill_mask, r.key);
-        if (!to_host && sl == kNoSlot) {
-          sl = sess_probe_insert<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask, &s_lins);
-          if (sl == kNoSlot) {  // sub-table full: the key lives in host DRAM from now on
-            to_host = true;
-            set_insert(spill_set, spill_mask, r.key);
-          }
-        }
-        if (to_host) {
-          const uint32_t q = atomicAdd(n_host, 1u);
-          if (q < host_cap) host_recs[q] = r;
-        } else {
-          v = ((uint64_t)sl << 32) | r.t;
-          ++kept;
-        }
-      }
-      rk[s_src_off[src] + e] = v;
-    }
-  }
-  if (kept) atomicAdd(&s_kept, kept);
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) gkeys[i] = lkeys[i];
-  if (threadIdx.x == 0) {
-    if (n_inserted && s_lins) atomicAdd(n_inserted, s_lins);
-    s_base = s_kept ? atomicAdd(n_out, s_kept) : 0u;
-  }
-  __syncthreads();
-  // Phase 2: per-slot counts -> exclusive offsets -> segments of record indices.
-  for (uint32_t i = threadIdx.x; i < cap / 2; i += blockDim.x) cur32[i] = 0;
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-    const uint64_t v = rk[i];
-    if (v != ~0ull) {
-      const uint32_t sl = (uint32_t)(v >> 32);
-      atomicAdd(&cur32[sl >> 1], 1u << ((sl & 1u) * 16));
-    }
-  }
-  __syncthreads();
-  // Block-wide exclusive scan of cap (<= 4096) u16 counts: each thread sums a run of cap/T,
-  // wave prefix with shuffles, wave totals through LDS.
-  {
-    __shared__ uint32_t s_wave[kSessSortBlock / 64];
-    const uint32_t per = (cap + kSessSortBlock - 1) / kSessSortBlock;
-    const uint32_t lo = threadIdx.x * per, hi = lo + per < cap ? lo + per : cap;
-    uint32_t run = 0;
-    for (uint32_t i = lo; i < hi; ++i) run += cur[i];
-    uint32_t incl = run;
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(incl, d);
-      if (lane_id() >= d) incl += y;
-    }
-    const int w = threadIdx.x >> 6;
-    if (lane_id() == 63) s_wave[w] = incl;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      uint32_t t = 0;
-      for (int i = 0; i < kSessSortBlock / 64; ++i) {
-        const uint32_t c = s_wave[i];
-        s_wave[i] = t;
-        t += c;
-      }
-    }
-    __syncthreads();
-    uint32_t o = s_wave[w] + incl - run;
-    for (uint32_t i = lo; i < hi; ++i) {
-      const uint32_t c = cur[i];
-      cur[i] = (uint16_t)o;
-      o += c;
-    }
-  }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-    const uint64_t v = rk[i];
-    if (v != ~0ull) {
-      const uint32_t sl = (uint32_t)(v >> 32), sh = (sl & 1u) * 16;
-      const uint32_t pos = (atomicAdd(&cur32[sl >> 1], 1u << sh) >> sh) & 0xFFFFu;
-      idxl[pos] = (uint16_t)i;
-    }
-  }
-  __syncthreads();
-  // Phase 3: rank inside the slot segment [end(slot - 1), end(slot)) by (t, arrival index).
-  const uint64_t sub_slot0 = (uint64_t)sub << cap_log2;
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-    const uint64_t v = rk[i];
-    if (v == ~0ull) continue;
-    const uint32_t sl = (uint32_t)(v >> 32), t = (uint32_t)v;
-    const uint32_t end = cur[sl], start = sl ? cur[sl - 1] : 0u;
-    uint32_t rank = 0;
-    for (uint32_t q = start; q < end; ++q) {
-      const uint32_t j = idxl[q];
-      const uint32_t tj = (uint32_t)rk[j];
-      rank += (tj < t || (tj == t && j < i)) ? 1u : 0u;
-    }
-    // arrival index i -> (source bucket, position) for the value
-    int src = 0;
-    while (src + 1 < nsrc && i >= s_src_off[src + 1]) ++src;
-    const Rec& r = recs[(size_t)(src * nsub + sub) * bucket_cap + (i - s_src_off[src])];
-    const uint32_t out = s_base + start + rank;
-    sort_out[out] = (int64_t)(((sub_slot0 | sl) << tbits) | t);
-    vals_out[out] = r.val;
-  }
-  if (!do_merge) return;
-  // Phase 4 (fused merge): one thread per slot of this sub-table folds its now ordered records
-  // (this block's own writes, visible after the fence + barrier) into the slot's sessions;
-  // segments longer than kSessLongSeg go to the wave kernel (session_merge_long) afterwards.
-  __threadfence();
-  __syncthreads();
-  for (uint32_t sl = threadIdx.x; sl < cap; sl += blockDim.x) {
-    const uint32_t end = cur[sl], start = sl ? cur[sl - 1] : 0u;
-    if (end == start) continue;
-    const uint32_t i = s_base + start, j = s_base + end;
-    if (j - i > kSessLongSeg) {
-      long_heads[atomicAdd(n_long, 1u)] = i;
-      continue;
-    }
-    sess_merge_segment(sort_out, vals_out, i, j, (int64_t)(sub_slot0 | sl), sa, so);
-  }
-}
-
 
 // Fire due sessions: one lane per slot whose due time has passed.
 __global__ __launch_bounds__(256) void session_fire_kernel(
@@ -4112,8 +4082,7 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
                          uint32_t bcap, int cap_log2, uint64_t* keys_g, uint64_t* spill_set,
                          uint32_t spill_mask, int spill_any, int64_t* sort_out, uint64_t* vals_out,
                          uint32_t* n_out, Rec* host_recs, uint32_t* n_host, uint32_t host_cap,
-                         uint32_t* n_inserted, int tbits, intptr_t stream,
-                         const SessMergeArgs* merge) {
+                         uint32_t* n_inserted, int tbits, intptr_t stream) {
   if (nsrc * nsub <= 0) return true;
   if (tbits < 1 || tbits > 32) throw std::invalid_argument("session_lookup_sort: tbits out of range");
   const uint64_t m64 = (uint64_t)nsrc * bcap;
@@ -4128,28 +4097,11 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024));
     attr = true;
   }
-  SessArgs sa{};
-  SessOut so{};
-  int32_t do_merge = 0;
-  if (merge) {
-    sa = make_sess_args(merge->gap, merge->lateness, merge->wm, merge->tbase, merge->agg,
-                        cap_log2, merge->nslots, tbits);
-    so = SessOut{reinterpret_cast<SessRec*>(merge->sess), merge->slot_due, merge->slot_last,
-                 merge->late_cnt, merge->ovf_slots, merge->n_ovf, merge->ovf_rows,
-                 merge->n_ovf_runs, merge->ovf_cap};
-    do_merge = 1;
-  }
   hipLaunchKernelGGL(session_lookup_sort_kernel, dim3(nsub), dim3(kSessSortBlock), lds,
                      (hipStream_t)stream, recs, counts, nsrc, nsub, bcap, cap_log2, keys_g,
                      spill_set, spill_mask, spill_any, sort_out, vals_out, n_out, host_recs,
-                     n_host, host_cap, n_inserted, tbits, m_cap, do_merge, sa, so,
-                     merge ? merge->long_heads : nullptr, merge ? merge->n_long : nullptr);
+                     n_host, host_cap, n_inserted, tbits, m_cap);
   HIP_CHECK(hipGetLastError());
-  if (merge) {  // hot keys' long segments: a wave each (count stays on the device)
-    hipLaunchKernelGGL(session_merge_long_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream,
-                       sort_out, vals_out, n_out, merge->long_heads, merge->n_long, sa, so);
-    HIP_CHECK(hipGetLastError());
-  }
   return true;
 }
 

@@ -246,30 +246,11 @@ void session_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
 // Fused lookup + per-sub-table LDS segmented sort: writes the kept records in (slot, ts) order
 // (the stable sort of session_lookup's keys without holes). Returns false (nothing launched)
 // when a sub-table's records cannot be staged in LDS (then: session_lookup + a device sort).
-// merge (optional): the same kernel then folds every slot's ordered segment into its sessions
-// (session_merge semantics; long segments go to the wave kernel, launched after it).
-struct SessMergeArgs {
-  int64_t gap, lateness, wm, tbase;
-  int32_t agg;
-  int64_t nslots;
-  int64_t* sess;
-  int64_t* slot_due;
-  int64_t* slot_last;
-  uint64_t* late_cnt;
-  int64_t* ovf_slots;
-  uint32_t* n_ovf;
-  int64_t* ovf_rows;
-  uint32_t* n_ovf_runs;
-  uint32_t ovf_cap;
-  uint32_t* long_heads;
-  uint32_t* n_long;
-};
 bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
                          uint32_t bcap, int cap_log2, uint64_t* keys_g, uint64_t* spill_set,
                          uint32_t spill_mask, int spill_any, int64_t* sort_out, uint64_t* vals_out,
                          uint32_t* n_out, Rec* host_recs, uint32_t* n_host, uint32_t host_cap,
-                         uint32_t* n_inserted, int tbits, intptr_t stream,
-                         const SessMergeArgs* merge = nullptr);
+                         uint32_t* n_inserted, int tbits, intptr_t stream);
 void session_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
                    uint32_t* n_heads, intptr_t stream);
 void session_merge(const int64_t* sk, const uint64_t* vals, const uint32_t* n_in,

@@ -398,21 +398,25 @@ class KeyedSessionOperator:
         sbits = self.nslots.bit_length()  # one spare bit: valid keys stay below the sentinel
         c[:7].zero_()
         self.late_cnt.zero_()
-        merge = (self.gap, self.lateness, wm, tbase, self.agg, self.nslots,
-                 self.sess.data_ptr(), self.slot_due.data_ptr(), self.slot_last.data_ptr(),
-                 self.late_cnt.data_ptr(), self.ovf_slots.data_ptr(), c[4:5].data_ptr(),
-                 self.ovf_rows.data_ptr(), c[5:6].data_ptr(), self.ovf_cap,
-                 self.heads.data_ptr(), c[1:2].data_ptr())
         if _SESSION_SORT == "lds" and nsrc * self.nsub * bucket_cap <= self.sort_out.numel() and \
                 m.gpu_session_lookup_sort(
                     recs.data_ptr(), counts.data_ptr(), nsrc, self.nsub, bucket_cap,
                     self.cap_log2, self.keys_g.data_ptr(), self.spill_set.data_ptr(),
                     self.spill_set.numel() - 1, int(self.spill_any), self.sort_out.data_ptr(),
                     self.vals_out.data_ptr(), c[0:1].data_ptr(), self.host_recs.data_ptr(),
-                    c[2:3].data_ptr(), self.host_cap, 0, tbits, st, merge):
-            # One kernel per sub-table: lookup, LDS segmented sort by (slot, ts) and the session
-            # merge of every slot's segment (hot keys' long segments: the wave kernel after it).
-            # No device-wide radix sort, no pass over all records looking for segment heads.
+                    c[2:3].data_ptr(), self.host_cap, 0, tbits, st):
+            # Lookup + per-sub-table LDS segmented sort in one kernel: (slot, ts)-ordered records
+            # without holes, straight into the merge (no device-wide radix sort). The record count
+            # stays on the device (the merge reads it); the host learns it with the counters.
+            m.gpu_session_merge(self.sort_out.data_ptr(), self.vals_out.data_ptr(),
+                                c[0:1].data_ptr(), self.heads.data_ptr(), c[1:2].data_ptr(),
+                                nsrc * self.nsub * bucket_cap, tbits, self.gap, self.lateness,
+                                wm, tbase,
+                                self.agg, self.cap_log2, self.nslots, self.sess.data_ptr(),
+                                self.slot_due.data_ptr(), self.slot_last.data_ptr(),
+                                self.late_cnt.data_ptr(), self.ovf_slots.data_ptr(),
+                                c[4:5].data_ptr(), self.ovf_rows.data_ptr(), c[5:6].data_ptr(),
+                                self.ovf_cap, st)
             with self._phase("fold_gpu.sync"):
                 h = c[:6].cpu().tolist()
             if h[2] > self.host_cap:
