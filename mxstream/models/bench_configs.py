@@ -268,6 +268,8 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
     exp_sum = per_key_step * (active / drift) * 5_000
     op = KeyedSessionOperator(gap=gap, lateness=30_000, agg=K.AGG_SUM_I64, device=dev,
                               max_keys=table_keys, batch_capacity=batch, ooo_bound=1_000,
+                              sub_table_log2=int(__import__("os").environ.get("MXS_SESS_SUB_LOG2", 0))
+                              or None,
                               idle_spill_ms=gap + 2 * span, spill_rows=1 << 22,
                               filter_prog=E.compile_expr(E.var(E.VAR_RESULT) > 1.5 * exp_sum))
     op.promote_spilled = promote

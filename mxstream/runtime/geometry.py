@@ -36,3 +36,12 @@ def state_geometry(max_keys: int, world: int, cap_log2: int | None = None) -> tu
     while cl < MAX_CAP_LOG2 and mean + 4 * math.sqrt(mean) + 8 > (1 << cl) * 0.85:
         cl += 1
     return nsub, cl
+
+
+def fixed_geometry(max_keys: int, world: int, cap_log2: int) -> tuple[int, int]:
+    """(nsub, cap_log2) for a fixed sub-table size: as many sub-tables as that size needs at
+    <= 0.7 load (at least MIN_SUBTABLES_NODE over the node)."""
+    per_rank = int(max_keys / world * (1.3 if world > 1 else 1.0)) + 64
+    cl = max(MIN_CAP_LOG2, min(MAX_CAP_LOG2, int(cap_log2)))
+    nsub = _next_pow2(max(1, math.ceil(per_rank / ((1 << cl) * 0.7))))
+    return max(nsub, _next_pow2(max(1, MIN_SUBTABLES_NODE // world))), cl

@@ -111,7 +111,8 @@ class KeyedSessionOperator:
                  ooo_bound: int = 0, max_load: float = 0.7, idle_spill_ms: int | None = None,
                  spill_rows: int = 1 << 20, emit_capacity: int | None = None,
                  external_watermark: bool = False, host_budget_bytes: int | None = None,
-                 idle_timeout_steps: int | None = None, spill_set_log2: int = 16):
+                 idle_timeout_steps: int | None = None, spill_set_log2: int = 16,
+                 sub_table_log2: int | None = None):
         if gap <= 0:
             raise ValueError("session gap must be positive")
         self.device = K.resolve_device(device)
@@ -138,9 +139,13 @@ class KeyedSessionOperator:
         self.wm = I64_MIN
         self.gpu = self.device.type == "cuda"
 
-        from .geometry import state_geometry
+        from .geometry import fixed_geometry, state_geometry
 
-        self.nsub, self.cap_log2 = state_geometry(max_keys, self.world, cap_log2)
+        # sub_table_log2: a fixed sub-table size (smaller tables -> more, smaller fold
+        # workgroups with less LDS each); default: the shared geometry.
+        self.nsub, self.cap_log2 = (fixed_geometry(max_keys, self.world, sub_table_log2)
+                                    if sub_table_log2 else
+                                    state_geometry(max_keys, self.world, cap_log2))
         self.nsub_log2 = self.nsub.bit_length() - 1
         self.nslots = self.nsub << self.cap_log2
         dev = self.device

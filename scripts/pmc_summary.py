@@ -7,7 +7,7 @@ from collections import defaultdict
 
 vals = defaultdict(lambda: defaultdict(list))
 for path in sys.argv[1:]:
-    for f in glob.glob(path):
+    for f in glob.glob(path, recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 k = row["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
