@@ -529,9 +529,11 @@ void bind_runtime(py::module_& m) {
         py::arg("dict"), py::arg("offset_s") = 0, py::arg("threads") = 1);
 
   py::class_<SocketReaderCore>(m, "SocketSource")
-      .def(py::init<std::string, int, std::string, int, int64_t>(), py::arg("host"), py::arg("port"),
-           py::arg("delimiter") = "\n", py::arg("max_retry") = 0, py::arg("retry_ms") = 500)
+      .def(py::init<std::string, int, std::string, int, int64_t, size_t>(), py::arg("host"),
+           py::arg("port"), py::arg("delimiter") = "\n", py::arg("max_retry") = 0,
+           py::arg("retry_ms") = 500, py::arg("max_queue") = 1 << 22)
       .def("start", &SocketReaderCore::start)
+      .def("blocked", &SocketReaderCore::blocked)
       // Returns (joined_lines_bytes, nlines, eof, error).
       .def("poll", [](SocketReaderCore& s, size_t max_lines, int timeout_ms) {
         std::string joined, err;

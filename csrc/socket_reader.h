@@ -2,6 +2,11 @@
 // delimiter, trailing '\r' stripped, remainder flushed at EOF, maxRetry = 0 by default). A
 // background thread reads the connection; the consumer polls batches of lines. No Python here
 // (csrc/runtime.cpp binds it; csrc/tests/tsan_main.cpp runs it under ThreadSanitizer).
+//
+// Back-pressure: the queue between the reader and the consumer holds at most `max_queue` lines.
+// A full queue blocks the reader thread, which stops draining the socket, so the kernel's
+// receive buffer fills and TCP flow control slows the sender -- a slow job throttles its source
+// instead of growing host memory without bound (Flink's credit-based network stack, F-net).
 #pragma once
 #include <arpa/inet.h>
 #include <netdb.h>
@@ -24,11 +29,15 @@ namespace mxs {
 
 class SocketReaderCore {
  public:
-  SocketReaderCore(std::string host, int port, std::string delimiter, int max_retry, int64_t retry_ms)
+  SocketReaderCore(std::string host, int port, std::string delimiter, int max_retry, int64_t retry_ms,
+                   size_t max_queue = 1 << 22)
       : host_(std::move(host)), port_(port), delim_(std::move(delimiter)), max_retry_(max_retry),
-        retry_ms_(retry_ms) {
+        retry_ms_(retry_ms), max_queue_(max_queue ? max_queue : 1) {
     if (delim_.empty()) throw std::invalid_argument("empty delimiter");
   }
+
+  // Times the reader waited for queue space (back-pressure events) -- for metrics and tests.
+  int64_t blocked() const { return blocked_.load(); }
   ~SocketReaderCore() { close(); }
 
   void start() {
@@ -54,23 +63,29 @@ class SocketReaderCore {
     }
     *eof = eof_ && q_.empty();
     *err = err_;
+    if (*n) space_.notify_all();
   }
 
   // Stops the reader: shutdown() wakes a recv() blocked on the connection; the reader thread
   // itself closes the descriptor (closing it here would race with that recv and could hit a
   // reused descriptor number). fd_ changes only under mu_.
   void close() {
-    stop_ = true;
     {
       std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
       if (fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);
+      space_.notify_all();  // a reader blocked on a full queue
     }
     if (th_.joinable()) th_.join();
   }
 
  private:
   void push(std::string line) {
-    std::lock_guard<std::mutex> g(mu_);
+    std::unique_lock<std::mutex> lk(mu_);
+    if (q_.size() >= max_queue_) {
+      blocked_.fetch_add(1);
+      space_.wait(lk, [&] { return q_.size() < max_queue_ || stop_; });
+    }
     q_.push_back(std::move(line));
     cv_.notify_one();
   }
@@ -151,8 +166,11 @@ class SocketReaderCore {
   int64_t retry_ms_;
   std::thread th_;
   std::mutex mu_;
-  std::condition_variable cv_;
+  size_t max_queue_;
+  std::condition_variable cv_;     // consumer: lines available / end of stream
+  std::condition_variable space_;  // reader: room in the queue (back-pressure)
   std::deque<std::string> q_;
+  std::atomic<int64_t> blocked_{0};
   bool eof_ = false;
   std::string err_;
   std::atomic<bool> stop_{false};

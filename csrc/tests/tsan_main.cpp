@@ -155,6 +155,39 @@ static int test_socket() {
   closer.join();
   stop = true;
   silent.join();
+
+  // Back-pressure: a 64-line queue, a slow consumer -- the reader blocks, nothing is lost, and a
+  // close() while the reader waits for space returns.
+  int port3 = 0;
+  const int ls3 = listen_any(&port3);
+  const int n3 = 20000;
+  std::thread fast([&] {
+    const int c = accept(ls3, nullptr, nullptr);
+    std::string payload;
+    for (int i = 0; i < n3; ++i) payload += std::to_string(i) + "\n";
+    for (size_t i = 0; i < payload.size(); i += 4096) {
+      const size_t m = std::min<size_t>(4096, payload.size() - i);
+      if (send(c, payload.data() + i, m, 0) < 0) break;
+    }
+    ::close(c);
+    ::close(ls3);
+  });
+  SocketReaderCore src3("127.0.0.1", port3, "\n", 0, 100, 64);
+  src3.start();
+  int got3 = 0;
+  for (;;) {
+    std::string joined, err;
+    size_t k3 = 0;
+    bool eof3 = false;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+    src3.poll(50, 50, &joined, &k3, &eof3, &err);
+    got3 += (int)k3;
+    if (eof3) break;
+  }
+  fast.join();
+  src3.close();
+  if (got3 != n3) return fail("socket back-pressure: " + std::to_string(got3) + " lines");
+  if (src3.blocked() == 0) return fail("socket back-pressure: the reader never waited");
   return 0;
 }
 

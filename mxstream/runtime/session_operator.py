@@ -610,37 +610,55 @@ class KeyedSessionOperator:
         with self._phase("spill.evict_kernel"):
             nr_all, ne = self.ctr[7:9].cpu().tolist()
         nr = min(nr_all, R)
-        h = None
-        if nr:
-            t0 = time.perf_counter()
-            # Six contiguous DMA copies into pinned host memory; the host store reads the pinned
-            # rows in place (the buffer is reused only after the insert has been joined).
-            for j in range(6):
-                self._pin_rows[j, :nr].copy_(rows[j, :nr], non_blocking=True)
-            torch.cuda.current_stream(self.device).synchronize()
+        cold = slots is None  # idle keys: fired-and-unmodified sessions go to a cold chunk
+        if not nr:
+            self._apply_spill((0, ne))
+            return
+        t0 = time.perf_counter()
+        # Six contiguous DMA copies into pinned host memory; the host store reads the pinned
+        # rows in place (the buffer is reused only after the insert has been joined).
+        for j in range(6):
+            self._pin_rows[j, :nr].copy_(rows[j, :nr], non_blocking=True)
+
+        def host_rows():
             pin = self._pin_rows.numpy()
             h = [pin[j, :nr] for j in range(6)]
             if nr_all > R:  # staging overflowed: rows of skipped slots stay zero (cnt == 0)
                 ok = h[4] > 0
                 h = [np.ascontiguousarray(x[ok]) for x in h]
-            self.phase_s["spill.d2h"] += time.perf_counter() - t0
-        nk = int(np.count_nonzero(h[0][1:] != h[0][:-1])) + 1 if h is not None and len(h[0]) else 0
-        self._apply_spill((nk, ne))
-        if h is None or not len(h[0]):
-            return
-        cold = slots is None  # idle keys: fired-and-unmodified sessions go to a cold chunk
+            return h
+
         if not cold:
-            self.store.insert(h[0], h[1], h[2], h[3], h[4], h[5], False)
+            torch.cuda.current_stream(self.device).synchronize()
+            self.phase_s["spill.d2h"] += time.perf_counter() - t0
+            h = host_rows()
+            nk = int(np.count_nonzero(h[0][1:] != h[0][:-1])) + 1 if len(h[0]) else 0
+            self._apply_spill((nk, ne))
+            if len(h[0]):
+                self.store.insert(h[0], h[1], h[2], h[3], h[4], h[5], False)
             return
-        # The host-store insert (C++, GIL released) overlaps the next step's GPU work; joined
-        # before the store is used again.
+        # Idle eviction: the copy completes on the stream while the step goes on; a worker
+        # thread waits for it (event) and inserts into the host store (C++, GIL released),
+        # overlapping the next step's GPU work; joined before the store is used again. The
+        # spill-set occupancy takes the row count now (an upper bound of the keys).
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.set_used += nr
+        self.metrics.freed_slots += ne
         self._spill_err = None
 
         def work():
             try:
                 t0 = time.perf_counter()
-                self.store.insert(h[0], h[1], h[2], h[3], h[4], h[5], True)
-                self.phase_s["spill.host_insert"] += time.perf_counter() - t0
+                ev.synchronize()
+                h = host_rows()
+                t1 = time.perf_counter()
+                self.phase_s["spill.d2h_wait"] += t1 - t0
+                self.metrics.spilled_keys += (int(np.count_nonzero(h[0][1:] != h[0][:-1])) + 1
+                                              if len(h[0]) else 0)
+                if len(h[0]):
+                    self.store.insert(h[0], h[1], h[2], h[3], h[4], h[5], True)
+                self.phase_s["spill.host_insert"] += time.perf_counter() - t1
             except BaseException as e:  # re-raised by _join_spill
                 self._spill_err = e
 

@@ -405,6 +405,7 @@ class SocketTextSource(Source):
     # Set by the executor on multi-rank jobs (host-object collectives): a columnar socket source
     # then spreads rank 0's text batches over every rank (K18, Main.java:17 -> 18 rebalance).
     comm = None
+    max_queue_lines = 1 << 22  # lines buffered between the socket and the job
 
     def open(self, rank, world, clock):
         super().open(rank, world, clock)
@@ -412,7 +413,9 @@ class SocketTextSource(Source):
             return
         from ..ops.native import load
 
-        self.reader = load().SocketSource(self.host, self.port, self.delim, self.max_retry)
+        # Bounded reader queue: a slow job back-pressures the sender through TCP flow control.
+        self.reader = load().SocketSource(self.host, self.port, self.delim, self.max_retry,
+                                          max_queue=self.max_queue_lines)
         self.reader.start()
 
     def _poll_spread(self):

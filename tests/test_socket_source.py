@@ -90,3 +90,40 @@ def test_socket_batches_spread_over_ranks(world):
     got = [l for out in res for l in out]
     assert Counter(got) == Counter(ref)
     assert sum(seen.values()) == len(lines) and all(seen[r] > 0 for r in range(world))
+
+
+def test_socket_reader_back_pressure():
+    """The reader queue is bounded: with a slow consumer the reader thread waits for space
+    (TCP flow control then slows the sender) and no line is lost."""
+    import time
+
+    from mxstream.ops.native import load
+
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    port = srv.getsockname()[1]
+    n = 50_000
+
+    def serve():
+        c, _ = srv.accept()
+        c.sendall(b"".join(b"%d\n" % i for i in range(n)))
+        c.close()
+        srv.close()
+
+    th = threading.Thread(target=serve)
+    th.start()
+    r = load().SocketSource("127.0.0.1", port, "\n", 0, max_queue=256)
+    r.start()
+    got = []
+    while True:
+        data, k, eof, err = r.poll(100, 100)
+        assert not err
+        got += data.decode().split("\n")[:k]
+        if eof:
+            break
+        time.sleep(0.0005)
+    th.join()
+    r.close()
+    assert got == [str(i) for i in range(n)]
+    assert r.blocked() > 0
