@@ -307,7 +307,8 @@ __global__ __launch_bounds__(1024) void partition_kernel(
   }
   __syncthreads();
 
-  bool wide = false;  // a value does not fit a 16-byte record
+  bool wide = false;   // a value does not fit a 16-byte record
+  bool nwide = false;  // a record does not fit the 8-byte format
   // Pass B: scatter records into their bucket runs.
   const uint32_t bcap = plan.bucket_cap;
   for (int64_t i0 = start + threadIdx.x; i0 < end; i0 += bstep) {
@@ -329,7 +330,13 @@ __global__ __launch_bounds__(1024) void partition_kernel(
       const PartEval e = part_eval(k[u], t[u], jhash_tab, plan, kg_dest);
       if (e.kind) continue;
       const uint32_t pos = atomicAdd(&lhist[e.bucket], 1u);
-      if (pos < bcap && !(plan.ablate & 1u) && plan.rec_words == 2) {
+      if (pos < bcap && !(plan.ablate & 1u) && plan.rec_words == 1) {
+        // 8-byte record (one destination, more buckets than the staged kernel takes): 32-bit key
+        // id, 28-bit value, 4-bit pane; a record that does not fit flags bit 16 (widen, redo).
+        if (!narrow_fits(k[u], (int64_t)v[u], e.t)) nwide = true;
+        ((uint2*)out)[(size_t)e.bucket * bcap + pos] =
+            make_uint2((uint32_t)k[u], ((uint32_t)v[u] << 4) | (e.t & 15u));
+      } else if (pos < bcap && !(plan.ablate & 1u) && plan.rec_words == 2) {
         // 16-byte record: one vector store (int32 value; wider values flag bit 2).
         if ((int64_t)(int32_t)v[u] != (int64_t)v[u]) wide = true;
         ((uint4*)out)[(size_t)e.bucket * bcap + pos] =
@@ -360,7 +367,8 @@ __global__ __launch_bounds__(1024) void partition_kernel(
   if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
   const int64_t flags = block_reduce_i64(overflow ? 1 : 0, lred, 0) |
                         block_reduce_i64(bad & 2, lred, 0) | block_reduce_i64(bad & 8, lred, 0) |
-                        block_reduce_i64(wide ? 4 : 0, lred, 0);
+                        block_reduce_i64(wide ? 4 : 0, lred, 0) |
+                        block_reduce_i64(nwide ? 16 : 0, lred, 0);
   if (threadIdx.x == 0) {
     atomicMax((long long*)&stats[kStatMaxTs], (long long)tmax);
     if (nacc) {
@@ -3572,10 +3580,18 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                intptr_t stream) {
   const int nb = plan.nranks << plan.nsub_log2;
   if (plan.rec_words == 1) {
-    // Narrow 8-byte records: only the single-destination compact kernel writes them.
-    if (plan.nranks != 1 || nb > kCMaxNb || (uint64_t)nb * plan.bucket_cap >= (1ull << 32))
-      throw std::invalid_argument("partition: 8-byte records need one destination, <= 512 buckets");
+    // Narrow 8-byte records: one destination only. Up to 512 buckets the LDS-staged compact
+    // kernel; more (e.g. 4096 dense sub-tables of a 10M-key window) the plain scatter.
+    if (plan.nranks != 1 || (uint64_t)nb * plan.bucket_cap >= (1ull << 32))
+      throw std::invalid_argument("partition: 8-byte records need one destination");
     if (n <= 0) return;
+    if (nb > kCMaxNb) {
+      if (plan.key32)
+        throw std::invalid_argument("partition: int32 keys need <= 512 buckets");
+      partition_variant(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats,
+                        late_idx, late_cap, stream, 1);
+      return;
+    }
     dispatch_compact<true, 8>(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats,
                               late_idx, late_cap, stream);
     return;

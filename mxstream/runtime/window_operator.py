@@ -475,8 +475,7 @@ class KeyedWindowOperator:
         # record that does not fit widens the format for good (step redone).
         if narrow is None:
             narrow = compact and self.device.type == "cuda"
-        narrow = bool(narrow and compact and not self._exchanging and self.nbuckets <= 512
-                      and type(self)._narrow_ok)
+        narrow = bool(narrow and compact and not self._exchanging and type(self)._narrow_ok)
         # Record words: 1 = 8-byte RecN, 2 = 16-byte RecC (int32 values), 3 = 24-byte Rec.
         self.rec_w = 1 if narrow else 2 if compact else 3
         self.timer = None  # utils.metrics.StageTimer: per-stage step_ms histograms when attached
