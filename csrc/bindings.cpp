@@ -301,6 +301,8 @@ PYBIND11_MODULE(_mxs_native, m) {
   py::class_<AggPlan>(m, "AggPlanObj")
       .def(py::init(&make_agg))
       .def_readwrite("split", &AggPlan::split)
+      .def_property("skip", [](const AggPlan& a) { return (intptr_t)a.skip; },
+                    [](AggPlan& a, intptr_t v) { a.skip = reinterpret_cast<const int64_t*>(v); })
       .def_readwrite("bucket_cap", &AggPlan::bucket_cap)
       .def_readwrite("np_step", &AggPlan::np_step)
       .def_readwrite("pg", &AggPlan::pg)

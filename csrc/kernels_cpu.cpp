@@ -167,6 +167,7 @@ static inline uint32_t probe_insert(uint64_t* keys, uint64_t key, uint32_t mask,
 void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& p, uint64_t* keys_g,
                 uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g, uint32_t* occupancy,
                 uint32_t* flags) {
+  if (p.skip && *p.skip) return;  // incomplete exchange (AggPlan.skip)
   const uint32_t cap = 1u << p.cap_log2, mask = cap - 1;
   const size_t nslots = (size_t)p.nsub << p.cap_log2;
   // Deterministic f64 sums: per-step slot sums in 128-bit fixed point, folded once per slot

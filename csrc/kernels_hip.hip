@@ -1150,6 +1150,7 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // Split sub-tables (AggPlan.split, hot keys): workgroup `slice` of `split` takes an equal
   // share of the sub-table's records; the shares merge into the state with atomic adds.
+  if (p.skip && *p.skip) return;  // incomplete exchange: redone by the host (AggPlan.skip)
   const int split = p.split;  // launcher guarantees 1 unless the layout/aggregate allows it
   const int sub = split > 1 ? (int)blockIdx.x / split : (int)blockIdx.x;
   const int slice = split > 1 ? (int)blockIdx.x % split : 0;

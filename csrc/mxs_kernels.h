@@ -48,6 +48,12 @@ struct AggPlan {
   // so a re-firing ships only the deltas to the window's owner. Needs the touched-slot list.
   uint64_t* dacc;
   uint32_t* dcnt;
+  // Optional device word (the all-reduced combiner check of a records exchange): non-zero means
+  // some rank's combined bucket overflowed, so this step's records are incomplete -- the
+  // aggregation leaves the state untouched and the host redoes the step's exchange once it reads
+  // the check (window_operator.py _verify_combine), instead of waiting for it before the
+  // all-to-all.
+  const int64_t* skip;
 };
 
 // Plan of one window firing.

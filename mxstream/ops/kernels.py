@@ -182,6 +182,7 @@ class AggPlan:
     det: int = 0         # 1: deterministic f64 sums (128-bit fixed-point per-step slot sums)
     dacc: int = 0        # local-global delta ring of late data (data pointers, 0 = off) ...
     dcnt: int = 0        # ... and its counts
+    skip: int = 0        # device int64: non-zero -> leave the state untouched (incomplete exchange)
 
     def as_dict(self) -> dict:
         return dict(self.__dict__)

@@ -230,6 +230,8 @@ class _Back:
     ccap: int = 0
     hard: int = 0
     chk_ev: object = None
+    chk_dev: object = None  # all-reduced combiner check on the device (AggPlan.skip)
+    aplan: object = None    # the step's aggregation plan (redo after a combiner overflow)
     maxb: int = 0  # largest bucket fill of the step's partition (0: not reported)
 
 
@@ -464,6 +466,7 @@ class KeyedWindowOperator:
         self.comb_send = self.comb_recv = None
         self.comb_counts = torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
         self._ccap_hint = 1 << self.cap_log2
+        self._unverified: _Back | None = None  # combined exchange whose check is unread
         # 16-byte records (int32 values) for integer aggregates on the GPU staged path; a value
         # outside int32 switches the operator to 24-byte records for good (step redone).
         int_agg = agg in (K.AGG_SUM_I64, K.AGG_MIN_I64, K.AGG_MAX_I64, K.AGG_COUNT, K.AGG_AVG_I64)
@@ -628,7 +631,7 @@ class KeyedWindowOperator:
         chk = torch.stack([-(self.flags[1].to(torch.int64) & 2),
                            -self.comb_counts.max().to(torch.int64)])
         self.comm.allreduce_min_(chk)
-        b.ccap, b.hard = ccap, hard
+        b.ccap, b.hard, b.chk_dev = ccap, hard, chk
         if self.device.type == "cuda":
             self._hchk.copy_(chk, non_blocking=True)
             b.chk_ev = self._event()
@@ -637,18 +640,11 @@ class KeyedWindowOperator:
             b.chk_ev = None
 
     def _combine_finish(self, b: "_Back"):
-        while True:
-            if b.chk_ev is not None:
-                _host_wait(b.chk_ev, self.device, self.pipeline)
-            ovf, fill = (-int(x) for x in self._hchk.tolist())
-            if not ovf:
-                break
-            if b.ccap >= b.hard:
-                raise RuntimeError("window_combine: a send bucket exceeds its sub-table capacity")
-            self._ccap_hint = b.ccap * 2
-            self.metrics.extra["combine_regrows"] = self.metrics.extra.get("combine_regrows", 0) + 1
-            self._combine_begin(b)
-        self._ccap_hint = max(64, int(fill * 1.25) + 8)
+        """The all-to-all of the combined buckets, without waiting for the overflow check: the
+        step's aggregation skips itself on the device when the all-reduced check reports an
+        overflow (AggPlan.skip), and _verify_combine reads the check later -- at the step's first
+        host sync that needs the state (a firing) or at the next entry point -- and redoes the
+        exchange with larger buckets then (the send buffers are still intact)."""
         ccap, nb = b.ccap, self.nbuckets
         send = self.comb_send[: nb * ccap * K.REC_WORDS]
         recv = self.comb_recv[: nb * ccap * K.REC_WORDS]
@@ -656,6 +652,35 @@ class KeyedWindowOperator:
         self.comm.all_to_all(self.recv_counts, self.comb_counts)
         self.metrics.extra["a2a_bytes"] = self.metrics.extra.get("a2a_bytes", 0) + send.numel() * 8
         return recv, self.recv_counts, ccap
+
+    def _verify_combine(self) -> None:
+        """Read the overflow check of the last combined exchange (see _combine_finish); on
+        overflow (every rank sees the same all-reduced check) recombine the step's send buckets
+        with twice the capacity, exchange again and aggregate. Called before anything reads or
+        replaces the state."""
+        b, self._unverified = self._unverified, None
+        if b is None:
+            return
+        with self._s1():
+            redo = False
+            while True:
+                if b.chk_ev is not None:
+                    _host_wait(b.chk_ev, self.device, self.pipeline)
+                ovf, fill = (-int(x) for x in self._hchk.tolist())
+                if not ovf:
+                    break
+                if b.ccap >= b.hard:
+                    raise RuntimeError("window_combine: a send bucket exceeds its sub-table capacity")
+                self._ccap_hint = b.ccap * 2
+                self.metrics.extra["combine_regrows"] = self.metrics.extra.get("combine_regrows", 0) + 1
+                self._use_par(b.par)
+                self._combine_begin(b)
+                redo = True
+            self._ccap_hint = max(64, int(fill * 1.25) + 8)
+            if redo:
+                recs, counts, bcap = self._combine_finish(b)
+                b.aplan.bucket_cap, b.aplan.skip = bcap, 0
+                self._aggregate(recs, counts, b.aplan)
 
     def _grow_ring(self, need: int) -> None:
         """Re-lay the pane ring so `need` consecutive panes fit (rare; keeps absolute pane ids)."""
@@ -739,6 +764,7 @@ class KeyedWindowOperator:
         aggregation, firing, purge) on the state stream (S1), so the two overlap; it returns the
         windows fired by the previous batch (``flush()`` / ``finish()`` drain the last one). One
         host sync per step, on this batch's reduced vector, while S1 still works."""
+        self._verify_combine()
         out, self._carry = self._carry, []
         if not self.pipeline:
             b = self._settle(self._front(keys, ts, vals))
@@ -757,13 +783,16 @@ class KeyedWindowOperator:
     def flush(self) -> list[FireResult]:
         """Complete the pending state half of the last batch (pipelined mode); returns what it
         fired. Every entry point that reads or replaces state calls it first."""
+        self._verify_combine()
         out, self._carry = self._carry, []
         prev, self._pending = self._pending, None
         if prev is None:
             return out
         with self._s1():
             self._back_begin(prev)
-        return out + self._back_finish(prev)
+        out += self._back_finish(prev)
+        self._verify_combine()  # callers read or replace the state next
+        return out
 
     # ---- step phases ------------------------------------------------------------------------
     def _front(self, keys, ts, vals) -> "_Front":
@@ -971,8 +1000,12 @@ class KeyedWindowOperator:
                     aplan.slot_mark = self.slot_mark.data_ptr()
                 if self.dacc_g is not None:
                     aplan.dacc, aplan.dcnt = self.dacc_g.data_ptr(), self.dcnt_g.data_ptr()
+                if combined:
+                    aplan.skip = b.chk_dev.data_ptr()
                 with self._stage("window_agg"):
                     self._aggregate(recs, counts, aplan)
+                if combined:
+                    b.aplan, self._unverified = aplan, b
                 if cuda and not self._exchanging:
                     self._ev_consumed[b.par] = self._event()
                 if self._debug:
@@ -1075,7 +1108,7 @@ class KeyedWindowOperator:
         ap = self._aplan
         ap.np_step, ap.pane_base, ap.p_lo, ap.fired_hi = (aplan.np_step, aplan.pane_base,
                                                           aplan.p_lo, aplan.fired_hi)
-        ap.split = aplan.split
+        ap.split, ap.skip = aplan.split, aplan.skip
         cuda = self.device.type == "cuda"
         self._m.window_agg_obj(cuda, recs.data_ptr(), counts.data_ptr(), ap,
                                self.keys_g.data_ptr(), self.acc_g.data_ptr(),
@@ -1303,6 +1336,8 @@ class KeyedWindowOperator:
 
     def _fire_list(self, starts: list[int], only_dirty: bool) -> list[FireResult]:
         """Fire the windows starting at `starts` (in order)."""
+        if starts:
+            self._verify_combine()
         if len(starts) > 1 and self._batched_fire_ok():
             return self._fire_many(starts, only_dirty)
         out = []
@@ -1412,6 +1447,7 @@ class KeyedWindowOperator:
         return ls if ls >= t else ls + self.slide
 
     def _refire(self, pmin: int, pmax: int, old_wm: int) -> list[FireResult]:
+        self._verify_combine()
         out: list[FireResult] = []
         s = self.first_start_containing(self.pane_start(pmin))
         end_s = min(self.next_fire_start - self.slide, self.last_start(self.pane_start(pmax)))
@@ -1447,6 +1483,8 @@ class KeyedWindowOperator:
         stop = min(keep_from, self.max_seen_pane + 1)
         if stop - p > self.ring:
             p = stop - self.ring
+        if p < stop:
+            self._verify_combine()  # a redo must not land in a zeroed pane
         while p < stop:  # at most two runs of consecutive ring positions (wrap-around)
             r = p & (self.ring - 1)
             k = min(stop - p, self.ring - r)

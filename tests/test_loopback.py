@@ -528,3 +528,43 @@ def test_deterministic_f64_sums_invariant_to_world(dev, world):
         run_loopback(2, lambda comm: KeyedWindowOperator(
             size=3000, agg=K.AGG_SUM_F64, device=dev, comm=comm, max_keys=nkeys,
             parallelism=2, deterministic=True, exchange="partials"), device=torch.device(dev))
+
+
+@pytest.mark.parametrize("dev", _devices())
+@pytest.mark.parametrize("pipeline", [False, "stream"])
+@pytest.mark.parametrize("lateness", [0, 1500])
+def test_combiner_overflow_redone_after_the_exchange(dev, pipeline, lateness):
+    """The records exchange does not wait for the combiner's overflow check before the
+    all-to-all: an overflowing step's aggregation skips itself on the device and the step is
+    redone (larger combined buckets) when the check is read -- before any firing, re-firing or
+    purge reads the state. Forced here by tiny combined buckets every step."""
+    _skip_no_gpu(dev)
+    per, nkeys, cap_log2 = (40_000, 20_000, 8) if dev == "cpu" else _sizes(dev)
+    world = 4
+    late = lateness * 9 // 10 + 700 if lateness else 0
+
+    def make(comm, bc, pipe):
+        return KeyedWindowOperator(size=4000, slide=1000, lateness=lateness, agg=K.AGG_SUM_I64,
+                                   device=dev, comm=comm, max_keys=nkeys, batch_capacity=bc,
+                                   ooo_bound=500, cap_log2=cap_log2, pipeline=pipe,
+                                   exchange="records")
+
+    def rank_fn(comm):
+        op = make(comm, per, pipeline)
+        out = []
+        for step in range(STEPS):
+            op._ccap_hint = 64  # force an overflow of the combined buckets
+            out += op.process(*_batch(dev, comm.rank, step, per, nkeys, late=late))
+        out += op.finish()
+        return _collect_seq(out), op.metrics.extra.get("combine_regrows", 0)
+
+    res = run_loopback(world, rank_fn, device=torch.device(dev))
+    assert all(r[1] >= STEPS // 2 for r in res)
+    merged = {}
+    for d, _ in res:
+        merged.update(d)
+    ref_op = make(None, per * world, False)
+    out = []
+    for step in range(STEPS):
+        out += ref_op.process(*_concat(dev, world, step, per, nkeys, late=late))
+    assert merged == _collect_seq(out + ref_op.finish())
