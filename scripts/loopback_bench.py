@@ -44,7 +44,10 @@ def main() -> int:
     def rank_fn(comm):
         b = TumblingWindowBench(TumblingBenchConfig(keys=a.keys, batch=a.batch,
                                                     pipeline=False if a.no_pipeline else "stream",
-                                                    exchange=a.exchange), comm, dev)
+                                                    exchange=a.exchange,
+                                                    # the records exchange needs hashed keys
+                                                    dense_keys=a.exchange != "records"),
+                               comm, dev)
         for _ in range(a.warmup):
             b.step()
         torch.cuda.synchronize()
