@@ -440,6 +440,29 @@ PYBIND11_MODULE(_mxs_native, m) {
       P<uint32_t>(bounds)[i] = *P<uint32_t>(on);
     }
   });
+  // Fused GPU re-firing of several windows over the touched-slot list (plan: list / list_n);
+  // stage as in window_fire_many with region = the stage split k ways; ovf: flags word (bit 16 =
+  // a window outgrew its region). Returns False when the windows cannot be fused.
+  m.def("gpu_window_refire_many", [](intptr_t keys_g, intptr_t acc_g, intptr_t cnt_g,
+                                     intptr_t dirty_g, py::dict plan,
+                                     std::vector<std::tuple<int64_t, int32_t, double, double>> wins,
+                                     intptr_t ok, intptr_t ov, intptr_t oraw, intptr_t oc,
+                                     intptr_t on, intptr_t bounds, intptr_t ovf, intptr_t stream,
+                                     py::object stage) {
+    const FirePlan base = make_fire(plan);
+    std::vector<FireWin> w(wins.size());
+    for (size_t i = 0; i < wins.size(); ++i)
+      w[i] = FireWin{std::get<0>(wins[i]), std::get<1>(wins[i]), std::get<2>(wins[i]),
+                     std::get<3>(wins[i])};
+    const auto t = stage.cast<std::tuple<intptr_t, intptr_t, intptr_t, intptr_t, intptr_t, int64_t>>();
+    FireStage st{P<uint64_t>(std::get<0>(t)), P<double>(std::get<1>(t)), P<uint64_t>(std::get<2>(t)),
+                 P<uint32_t>(std::get<3>(t)), P<uint32_t>(std::get<4>(t)), (uint32_t)std::get<5>(t)};
+    return gpu::window_refire_many(P<uint64_t>(keys_g), P<uint64_t>(acc_g), P<uint32_t>(cnt_g),
+                                   P<uint8_t>(dirty_g), base, w.data(), (int)w.size(), st,
+                                   P<uint64_t>(ok), P<double>(ov), P<uint64_t>(oraw),
+                                   P<uint32_t>(oc), P<uint32_t>(on), P<uint32_t>(bounds),
+                                   P<uint32_t>(ovf), stream);
+  });
   m.def("gpu_rolling", [](intptr_t recs, intptr_t counts, py::dict plan, intptr_t keys_g,
                           intptr_t acc_g, intptr_t cnt_g, intptr_t occ, intptr_t flags,
                           intptr_t out_vals, intptr_t stream) {
@@ -520,13 +543,18 @@ PYBIND11_MODULE(_mxs_native, m) {
                                       intptr_t spill_set, uint32_t spill_mask, int spill_any,
                                       intptr_t sk, intptr_t vals, intptr_t n_out,
                                       intptr_t host_recs, intptr_t n_host, uint32_t host_cap,
-                                      intptr_t n_ins, int tbits, intptr_t stream) {
+                                      intptr_t n_ins, int tbits, intptr_t stream, intptr_t skip,
+                                      uint32_t skip_mask) {
     return gpu::session_lookup_sort(P<Rec>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2,
                                     P<uint64_t>(keys_g), P<uint64_t>(spill_set), spill_mask,
                                     spill_any, P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_out),
                                     P<Rec>(host_recs), P<uint32_t>(n_host), host_cap,
-                                    P<uint32_t>(n_ins), tbits, stream);
-  });
+                                    P<uint32_t>(n_ins), tbits, stream, P<int64_t>(skip), skip_mask);
+  }, py::arg("recs"), py::arg("counts"), py::arg("nsrc"), py::arg("nsub"), py::arg("bcap"),
+     py::arg("cap_log2"), py::arg("keys_g"), py::arg("spill_set"), py::arg("spill_mask"),
+     py::arg("spill_any"), py::arg("sk"), py::arg("vals"), py::arg("n_out"), py::arg("host_recs"),
+     py::arg("n_host"), py::arg("host_cap"), py::arg("n_ins"), py::arg("tbits"), py::arg("stream"),
+     py::arg("skip") = 0, py::arg("skip_mask") = 0);
   m.def("gpu_session_heads", [](intptr_t sk, intptr_t n_in, int64_t n_cap, intptr_t heads,
                                 intptr_t n_heads, intptr_t stream) {
     gpu::session_heads(P<int64_t>(sk), P<uint32_t>(n_in), n_cap, P<uint32_t>(heads),
@@ -615,6 +643,20 @@ PYBIND11_MODULE(_mxs_native, m) {
     for (size_t i = 0; i < copies.size(); ++i)
       c[i] = D2HCopy{(const void*)std::get<0>(copies[i]), std::get<1>(copies[i]), std::get<2>(copies[i])};
     return gpu::d2h_kernel((void*)dst, c, (int)copies.size(), stream);
+  });
+  // Copy kernel whose row count is read on the device (no host sync before the copy):
+  // copies = [(src, max_bytes, dst_offset, element_size)] (element_size 0: copy max_bytes as is);
+  // n_dev = uint32 row counter. Returns the hipError_t code (0 = ok).
+  m.def("gpu_d2h_counted", [](intptr_t dst,
+                              const std::vector<std::tuple<intptr_t, int64_t, int64_t, int64_t>>& copies,
+                              intptr_t n_dev, intptr_t stream) {
+    if (copies.empty() || copies.size() > (size_t)kD2HMax)
+      throw std::invalid_argument("gpu_d2h_counted: 1..8 columns");
+    D2HCopy c[kD2HMax];
+    for (size_t i = 0; i < copies.size(); ++i)
+      c[i] = D2HCopy{(const void*)std::get<0>(copies[i]), std::get<1>(copies[i]),
+                     std::get<2>(copies[i]), std::get<3>(copies[i])};
+    return gpu::d2h_kernel((void*)dst, c, (int)copies.size(), stream, P<uint32_t>(n_dev));
   });
   // Keyed-window compaction / eviction (host-DRAM spill tier). out = (key, pane, acc, cnt, dirty,
   // n, cap, counters) pointers.

@@ -110,13 +110,21 @@ __global__ __launch_bounds__(256) void gen_events_kernel(
 // the DMA path (hipMemcpyAsync D2H) stalled the host for 7-9 ms at one firing in some runs
 // (profiles/r2_fire_d2h.md); a kernel copy has no lazily initialised engine behind it.
 // ------------------------------------------------------------------------------------------
+// With b.n_dev the row count stays on the device: copies with esz > 0 move only the rows the
+// producer counted (the fire needs no host round trip for its count before the copy).
 __global__ __launch_bounds__(256) void d2h_copy_kernel(unsigned char* __restrict__ dst, D2HBatch b) {
   typedef unsigned int v4u __attribute__((ext_vector_type(4)));
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t rows = b.n_dev ? (int64_t)*b.n_dev : -1;
   for (int k = 0; k < b.n; ++k) {
     const v4u* __restrict__ s = reinterpret_cast<const v4u*>(b.c[k].src);
     v4u* __restrict__ d = reinterpret_cast<v4u*>(dst + b.c[k].dst_off);
-    const int64_t n16 = b.c[k].bytes >> 4;
+    int64_t bytes = b.c[k].bytes;
+    if (rows >= 0 && b.c[k].esz > 0) {
+      const int64_t want = (rows * b.c[k].esz + 15) & ~(int64_t)15;
+      bytes = want < bytes ? want : bytes;
+    }
+    const int64_t n16 = bytes >> 4;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
       d[i] = __builtin_nontemporal_load(&s[i]);
   }
@@ -1794,14 +1802,132 @@ __global__ __launch_bounds__(kFireMultiThreads) void window_fire_multi_kernel(
       st.win_n + w0 + y, st.region, fsm, blockIdx.x, gridDim.x);
 }
 
+
+// Fused re-firing of several windows over ONE touched-slot list (allowed lateness): late data of
+// a step lands in a few panes, and every already-fired window containing them re-fires. One
+// thread per listed slot loads the union of the windows' panes once (<= kRefireP panes: count,
+// then accumulator and dirty byte where the count is non-zero, all in flight together) and
+// evaluates every window from registers -- the per-window sweep read each slot's panes once per
+// window (3 re-fired windows of 6 panes: 18 random (count, acc, dirty) triples per slot, here 8).
+// Window w appends to staging region w at counter win_n[w] (block-level compaction per window);
+// fire_pack_kernel lays the regions out in window order.
+constexpr int kRefireP = 16;
+constexpr int kRefireThreads = 256;
+
+__global__ __launch_bounds__(kRefireThreads) void window_refire_multi_kernel(
+    const uint64_t* __restrict__ keys_g, const uint64_t* __restrict__ acc_g,
+    const uint32_t* __restrict__ cnt_g, const uint8_t* __restrict__ dirty_g, FirePlan p,
+    FireWinPack pack, int64_t u0, int nu, FireStage st) {
+  extern __shared__ __attribute__((aligned(16))) double fsm[];
+  constexpr int T = kRefireThreads;
+  LdsCol vars{fsm + threadIdx.x, T};
+  LdsCol stack{fsm + kExprVars * T + threadIdx.x, T};
+  const int depth = p.map.depth > p.filt.depth ? p.map.depth : p.filt.depth;
+  uint32_t* wcnt = (uint32_t*)(fsm + (size_t)(kExprVars + depth) * T);
+  const int wid = threadIdx.x >> 6, nw = T >> 6;
+  const int64_t nslots = p.nslots;
+  const bool chain_only = (!p.map.ncode || p.map.chain) && (!p.filt.ncode || p.filt.chain);
+  const int64_t nvisit = (int64_t)*p.list_n;
+  for (int64_t base = (int64_t)blockIdx.x * T; base < nvisit; base += (int64_t)gridDim.x * T) {
+    const int64_t v = base + threadIdx.x;
+    const bool live = v < nvisit;
+    const int64_t s = live ? (int64_t)p.list[v] : 0;
+    uint32_t cg[kRefireP];
+    uint64_t ag[kRefireP];
+    uint32_t dmask = 0;
+#pragma unroll
+    for (int q = 0; q < kRefireP; ++q)
+      cg[q] = (live && q < nu) ? cnt_g[(size_t)((u0 + q) & (p.ring - 1)) * nslots + s] : 0u;
+#pragma unroll
+    for (int q = 0; q < kRefireP; ++q) {
+      const size_t gi = (size_t)((u0 + q) & (p.ring - 1)) * nslots + s;
+      ag[q] = cg[q] ? acc_g[gi] : 0ull;
+      if (cg[q] && dirty_g[gi]) dmask |= 1u << q;
+    }
+    const uint64_t key = live ? keys_g[s] : 0ull;
+    for (int w = 0; w < pack.n; ++w) {  // block-uniform: every lane reaches the barriers
+      const FireWin& fw = pack.w[w];
+      const int off = (int)(fw.p0 - u0);
+      uint64_t acc = 0;
+      uint32_t cnt = 0;
+      bool have = false, dirty = false;
+#pragma unroll
+      for (int q = 0; q < kRefireP; ++q) {
+        if (q < off || q >= off + fw.npanes || !cg[q]) continue;
+        acc = have ? agg_combine(p.agg, acc, ag[q]) : ag[q];
+        have = true;
+        cnt += cg[q];
+        dirty = dirty || (dmask >> q & 1u);
+      }
+      bool emit = false;
+      double val = 0.0;
+      if (cnt && dirty) {
+        const double v0 = agg_result_f64(p.agg, acc, cnt);
+        val = v0;
+        emit = true;
+        if ((p.map.ncode || p.filt.ncode) && chain_only) {
+          const RegVars rv{v0, (double)cnt, fw.wstart, fw.wend, (double)key, (double)(int64_t)acc,
+                           0.0};
+          if (p.map.ncode) val = expr_eval_chain(p.map, rv);
+          if (p.filt.ncode) {
+            RegVars rf = rv;
+            rf.v6 = val;
+            emit = expr_eval_chain(p.filt, rf) != 0.0;
+          }
+        } else if (p.map.ncode || p.filt.ncode) {
+          vars.set(0, v0);
+          vars.set(1, (double)cnt);
+          vars.set(2, fw.wstart);
+          vars.set(3, fw.wend);
+          vars.set(4, (double)key);
+          vars.set(5, (double)(int64_t)acc);
+          if (p.map.ncode) val = expr_eval_t(p.map, stack, vars);
+          vars.set(6, val);
+          if (p.filt.ncode) emit = expr_eval_t(p.filt, stack, vars) != 0.0;
+        }
+      }
+      const unsigned long long m = __ballot(emit);
+      __syncthreads();
+      if (lane_id() == 0) wcnt[wid] = (uint32_t)__popcll(m);
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int i = 0; i < nw; ++i) {
+          const uint32_t c = wcnt[i];
+          wcnt[i] = tot;
+          tot += c;
+        }
+        wcnt[nw] = tot ? atomicAdd(&st.win_n[w], tot) : 0u;
+      }
+      __syncthreads();
+      if (emit) {
+        const uint32_t q = wcnt[nw] + wcnt[wid] + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+        if (q < st.region) {
+          const size_t o = (size_t)w * st.region;
+          if (p.key32)
+            reinterpret_cast<uint32_t*>(st.keys + o)[q] = (uint32_t)key;
+          else
+            st.keys[o + q] = key;
+          st.vals[o + q] = val;
+          if (st.raw) st.raw[o + q] = acc;
+          if (st.cnt) st.cnt[o + q] = cnt;
+        }
+      }
+    }
+  }
+}
+
 // Regions -> contiguous rows in window order; bounds[w] = rows of windows 0..w, *out_n = total.
+// A window with more rows than its region sets bit 16 of *ovf (when given): its rows past the
+// region were not staged (the fused re-firing's regions are the stage split k ways).
 __global__ __launch_bounds__(256) void fire_pack_kernel(FireStage st, int k, int key32,
                                                         uint64_t* __restrict__ out_keys,
                                                         double* __restrict__ out_vals,
                                                         uint64_t* __restrict__ out_raw,
                                                         uint32_t* __restrict__ out_cnt,
                                                         uint32_t* __restrict__ bounds,
-                                                        uint32_t* __restrict__ out_n) {
+                                                        uint32_t* __restrict__ out_n,
+                                                        uint32_t* __restrict__ ovf) {
   const int w = blockIdx.y;
   __shared__ uint32_t s_off;
   if (threadIdx.x < 64) {  // wave 0: prefix of the earlier windows' row counts
@@ -1831,6 +1957,7 @@ __global__ __launch_bounds__(256) void fire_pack_kernel(FireStage st, int k, int
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     bounds[w] = off + n;
     if (w == k - 1) *out_n = off + n;
+    if (ovf && st.win_n[w] > st.region) atomicOr(ovf, 16u);
   }
 }
 
@@ -2535,8 +2662,18 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
     uint64_t* __restrict__ spill_set, uint32_t spill_mask, int32_t spill_any,
     int64_t* __restrict__ sort_out, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
     Rec* __restrict__ host_recs, uint32_t* __restrict__ n_host, uint32_t host_cap,
-    uint32_t* __restrict__ n_inserted, int tbits, uint32_t m_cap) {
+    uint32_t* __restrict__ n_inserted, int tbits, uint32_t m_cap, const int64_t* __restrict__ skip,
+    uint32_t skip_mask) {
   extern __shared__ __attribute__((aligned(16))) uint64_t slds[];
+  // Launched before the host has read the step's partition flags: any flagged word of the
+  // reduced vector (bucket overflow, unrepresentable span, reserved key) means the step is
+  // redone -- nothing is looked up, inserted or counted (the merge then sees 0 records).
+  if (skip) {
+    int64_t any = 0;
+    for (int w = 0; w < 32; ++w)
+      if (skip_mask >> w & 1u) any |= skip[w];
+    if (any) return;
+  }
   __shared__ uint32_t s_base, s_lins, s_kept, s_m;
   __shared__ uint32_t s_src_off[65];
   const int sub = blockIdx.x;
@@ -3460,7 +3597,8 @@ int d2h_async(void* dst, const void* src, size_t bytes, intptr_t stream) {
   return (int)hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream);
 }
 
-int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream) {
+int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream,
+               const uint32_t* n_dev) {
   // Device-side address of the pinned host slab (mapped host memory).
   void* dd = nullptr;
   hipError_t e = hipHostGetDevicePointer(&dd, dst_host, 0);
@@ -3468,6 +3606,7 @@ int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream) {
   D2HBatch b{};
   if (n < 1 || n > kD2HMax) return (int)hipErrorInvalidValue;
   b.n = n;
+  b.n_dev = n_dev;
   int64_t total = 0;
   for (int i = 0; i < n; ++i) {
     b.c[i] = copies[i];
@@ -3840,8 +3979,41 @@ void window_fire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uint3
     HIP_CHECK(hipGetLastError());
   }
   hipLaunchKernelGGL(fire_pack_kernel, dim3(grid_for(nvisit, 256 * 4, 64), k), dim3(256), 0, s,
-                     st, k, base.key32, out_keys, out_vals, out_raw, out_cnt, bounds, out_n);
+                     st, k, base.key32, out_keys, out_vals, out_raw, out_cnt, bounds, out_n,
+                     nullptr);
   HIP_CHECK(hipGetLastError());
+}
+
+bool window_refire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
+                        const uint8_t* dirty_g, const FirePlan& base, const FireWin* wins, int k,
+                        const FireStage& st, uint64_t* out_keys, double* out_vals,
+                        uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n, uint32_t* bounds,
+                        uint32_t* ovf, intptr_t stream) {
+  if (k <= 0 || k > kFireMultiMax || !base.list || !base.list_n || base.nslots <= 0) return false;
+  int64_t u0 = wins[0].p0, u1 = wins[0].p0 + wins[0].npanes;
+  for (int i = 1; i < k; ++i) {
+    u0 = wins[i].p0 < u0 ? wins[i].p0 : u0;
+    u1 = wins[i].p0 + wins[i].npanes > u1 ? wins[i].p0 + wins[i].npanes : u1;
+  }
+  if (u1 - u0 > kRefireP || u1 - u0 > base.ring) return false;
+  const int depth = base.map.depth > base.filt.depth ? base.map.depth : base.filt.depth;
+  const size_t lds = (size_t)(kExprVars + depth) * kRefireThreads * sizeof(double) + 8 * 4;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_CHECK(hipMemsetAsync(st.win_n, 0, sizeof(uint32_t) * k, s));
+  FireWinPack pack{};
+  pack.n = k;
+  for (int i = 0; i < k; ++i) pack.w[i] = wins[i];
+  // The list length stays on the device: a grid for the list's capacity (nslots), rounds of
+  // 256 slots per workgroup; workgroups past the list end exit at once.
+  hipLaunchKernelGGL(window_refire_multi_kernel, dim3(grid_for(base.nslots, kRefireThreads * 4, 2048)),
+                     dim3(kRefireThreads), lds, s, keys_g, acc_g, cnt_g, dirty_g, base, pack, u0,
+                     (int)(u1 - u0), st);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(fire_pack_kernel, dim3(grid_for(base.nslots / k, 256 * 4, 64), k), dim3(256),
+                     0, s, st, k, base.key32, out_keys, out_vals, out_raw, out_cnt, bounds, out_n,
+                     ovf);
+  HIP_CHECK(hipGetLastError());
+  return true;
 }
 
 void direct_agg_probe(const uint64_t* keys, const int64_t* ts, const uint64_t* vals, int64_t n,
@@ -4099,7 +4271,8 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
                          uint32_t bcap, int cap_log2, uint64_t* keys_g, uint64_t* spill_set,
                          uint32_t spill_mask, int spill_any, int64_t* sort_out, uint64_t* vals_out,
                          uint32_t* n_out, Rec* host_recs, uint32_t* n_host, uint32_t host_cap,
-                         uint32_t* n_inserted, int tbits, intptr_t stream) {
+                         uint32_t* n_inserted, int tbits, intptr_t stream, const int64_t* skip,
+                         uint32_t skip_mask) {
   if (nsrc * nsub <= 0) return true;
   if (tbits < 1 || tbits > 32) throw std::invalid_argument("session_lookup_sort: tbits out of range");
   const uint64_t m64 = (uint64_t)nsrc * bcap;
@@ -4117,7 +4290,7 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
   hipLaunchKernelGGL(session_lookup_sort_kernel, dim3(nsub), dim3(kSessSortBlock), lds,
                      (hipStream_t)stream, recs, counts, nsrc, nsub, bcap, cap_log2, keys_g,
                      spill_set, spill_mask, spill_any, sort_out, vals_out, n_out, host_recs,
-                     n_host, host_cap, n_inserted, tbits, m_cap);
+                     n_host, host_cap, n_inserted, tbits, m_cap, skip, skip_mask);
   HIP_CHECK(hipGetLastError());
   return true;
 }

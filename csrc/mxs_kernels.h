@@ -131,12 +131,14 @@ struct CompactOut {
 constexpr int kD2HMax = 8;
 struct D2HCopy {
   const void* src;
-  int64_t bytes;
+  int64_t bytes;    // bytes to copy (16-byte multiple); with a device row count: the maximum
   int64_t dst_off;
+  int64_t esz = 0;  // > 0: bytes = min(bytes, round16(*n_dev * esz)) -- rows counted on the device
 };
 struct D2HBatch {
   D2HCopy c[kD2HMax];
   int n;
+  const uint32_t* n_dev;  // device row count (fired rows), read by the copy kernel; may be null
 };
 
 constexpr int64_t kRollHistMaxSlots = 16384;  // LDS running-count table of the emit pass
@@ -158,7 +160,8 @@ int set_spin_schedule();
 int d2h_async(void* dst, const void* src, size_t bytes, intptr_t stream);
 // Up to kD2HMax device buffers -> one pinned (mapped) host slab by a copy kernel on `stream`;
 // every size, source address and slab offset a multiple of 16 bytes. Returns hipError_t.
-int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream);
+int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream,
+               const uint32_t* n_dev = nullptr);
 // Experiment: pane accumulation by global atomics from the source columns (see kernels_hip).
 void direct_agg_probe(const uint64_t* keys, const int64_t* ts, const uint64_t* vals, int64_t n,
                       int64_t tbase, int64_t pane, int ring, int64_t nslots, uint32_t mul,
@@ -185,6 +188,15 @@ void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* 
                  intptr_t stream);
 // Several windows in one call: each window's rows follow the previous ones at the shared
 // cursor out_n; bounds[i] = rows of windows 0..i (device).
+// Fused re-firing of k windows over the touched-slot list (plan.list / list_n): one pass loads
+// the union of the windows' panes (<= 16) per listed slot. Staging region per window =
+// st.region (the caller splits the stage k ways); a window that outgrows it sets bit 16 of *ovf
+// (re-run unfused). Returns false (nothing launched) when the union is too wide or k > 32.
+bool window_refire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
+                        const uint8_t* dirty_g, const FirePlan& base, const FireWin* wins, int k,
+                        const FireStage& st, uint64_t* out_keys, double* out_vals,
+                        uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n, uint32_t* bounds,
+                        uint32_t* ovf, intptr_t stream);
 void window_fire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
                       const uint8_t* dirty_g, const FirePlan& base, const FireWin* wins, int k,
                       const FireStage& stage, uint64_t* out_keys, double* out_vals,
@@ -256,7 +268,8 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
                          uint32_t bcap, int cap_log2, uint64_t* keys_g, uint64_t* spill_set,
                          uint32_t spill_mask, int spill_any, int64_t* sort_out, uint64_t* vals_out,
                          uint32_t* n_out, Rec* host_recs, uint32_t* n_host, uint32_t host_cap,
-                         uint32_t* n_inserted, int tbits, intptr_t stream);
+                         uint32_t* n_inserted, int tbits, intptr_t stream,
+                         const int64_t* skip = nullptr, uint32_t skip_mask = 0);
 void session_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
                    uint32_t* n_heads, intptr_t stream);
 void session_merge(const int64_t* sk, const uint64_t* vals, const uint32_t* n_in,

@@ -162,6 +162,16 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
     step_i = [0]
     lat = []
 
+    t_ing = {}
+
+    def account(fired):
+        # latency: ingest of the batch that triggered the firing (FireResult.seq) -> rows here
+        now = time.perf_counter()
+        for seq in {r.seq for r in fired}:
+            if seq in t_ing:
+                lat.append((now - t_ing[seq]) * 1e3)
+        return sum(len(r.keys) for r in fired)
+
     def step():
         t_in = time.perf_counter()
         i = step_i[0]
@@ -169,11 +179,10 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
                      ts_base=i * span, ts_span=span, disorder=5_000, val_lo=0, val_span=20_000)
         if i > 20:
             tt[:late_n] -= 40_000  # late but (mostly) within the allowed lateness
+        t_ing[op.metrics.steps + 1] = t_in
         fired = op.process(kt, tt, vt)
         step_i[0] += 1
-        if fired:
-            lat.append((time.perf_counter() - t_in) * 1e3)
-        return sum(len(r.keys) for r in fired)
+        return account(fired)
 
     # Steady state: the first windows (started before the stream) hold a partial minute of
     # data and nearly every key of them is below the alert threshold -- an artefact of the
@@ -188,7 +197,7 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
     alerts = 0
     for _ in range(steps):
         alerts += step()
-    alerts += sum(len(r.keys) for r in op.flush())  # pipelined: the last state half
+    alerts += account(op.flush())  # pipelined: the last state half
     _sync(dev)
     dt = time.perf_counter() - t0
     return {"config": 4, "warmup": warmup, "keyed_state": "dense" if dense_keys else "hashed", "metric": "events/sec (sliding 1min/10s + lateness, 10M keys)",

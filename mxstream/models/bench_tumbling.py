@@ -76,17 +76,29 @@ class TumblingWindowBench:
         self.alerts = 0
         self.latencies_ms: list[tuple[float, int]] = []  # (latency, alerts) per firing step
         self.t0_event = 1_566_957_600_000  # 2019-08-28T10:00:00+08:00 (chapter3/README.md:286)
-        self._ingest: list[float] = []  # ingest wall time of steps whose state half is pending
+        self._ingest: dict[int, float] = {}  # batch seq (FireResult.seq) -> ingest wall time
 
-    def _account(self, fired, t_ingest: float) -> int:
-        n = sum(len(r.keys) for r in fired)
-        if fired:
-            self.latencies_ms.append(((time.perf_counter() - t_ingest) * 1e3, n))
+    def _account(self, fired) -> int:
+        """Alerts of the returned firings; each firing's latency runs from the ingest of the
+        batch that triggered it (FireResult.seq) to now -- pipelined results come back one or
+        more calls later, and that delay is part of the latency."""
+        now = time.perf_counter()
+        per_seq: dict[int, int] = {}
+        for r in fired:
+            per_seq[r.seq] = per_seq.get(r.seq, 0) + len(r.keys)
+        for seq, n in per_seq.items():
+            t = self._ingest.get(seq)
+            if t is not None:
+                self.latencies_ms.append(((now - t) * 1e3, n))
+        n = sum(per_seq.values())
         self.alerts += n
+        seq_now = self.op.metrics.steps
+        for k in [k for k in self._ingest if k < seq_now - 64]:
+            del self._ingest[k]
         return n
 
     def step(self) -> int:
-        """One micro-batch. Pipelined, the windows a step fires come back from the NEXT call;
+        """One micro-batch. Pipelined, the windows a step fires come back from a LATER call;
         their alert latency is measured from the ingest time of the step that fired them."""
         cfg = self.cfg
         t_ingest = time.perf_counter()
@@ -95,20 +107,14 @@ class TumblingWindowBench:
                      ts_base=self.t0_event + self.step_idx * cfg.step_span_ms,
                      ts_span=cfg.step_span_ms, disorder=cfg.disorder_ms, val_lo=0,
                      val_span=cfg.val_max, zipf=cfg.zipf)
-        self._ingest.append(t_ingest)
+        self._ingest[self.op.metrics.steps + 1] = t_ingest
         fired = self.op.process(self.keys, self.ts, self.vals)
-        src = self._ingest.pop(0) if self.op.pipeline and len(self._ingest) > 1 else t_ingest
-        if not self.op.pipeline:
-            self._ingest.clear()
         self.step_idx += 1
-        return self._account(fired, src)
+        return self._account(fired)
 
     def drain(self) -> int:
-        """Run the pending state half (pipelined mode) so every ingested step is fully applied."""
-        if not self._ingest:
-            return 0
-        t = self._ingest.pop(0)
-        return self._account(self.op.flush(), t)
+        """Run the pending state half (pipelined mode) and collect every queued firing."""
+        return self._account(self.op.flush())
 
     def p50_latency_ms(self) -> float | None:
         return self.latency_quantile_ms(0.5)

@@ -167,7 +167,7 @@ class KeyedSessionOperator:
             self._pin_rows = torch.empty((6, self.spill_rows), dtype=torch.int64).pin_memory()
             self._spill_thread = None
             # A fire can close every resident session of every slot (end of input: all kSess).
-            self.ocap = int(emit_capacity or max(self.nslots * K_SESS, 1 << 16))
+            self.ocap = (int(emit_capacity or max(self.nslots * K_SESS, 1 << 16)) + 3) & ~3
             self.out_key = torch.empty(self.ocap, dtype=torch.int64, device=dev)
             self.out_start = torch.empty(self.ocap, dtype=torch.int64, device=dev)
             self.out_end = torch.empty(self.ocap, dtype=torch.int64, device=dev)
@@ -183,6 +183,21 @@ class KeyedSessionOperator:
                                         device=dev)
             self.set_used = 0  # occupied spill-set entries (keys + tombstones)
             self._live_estimate = 0
+            # Occupancy bookkeeping from the kernels' own counters (no table scan per step):
+            # live keys = inserted - evicted (exact); occupied = live + tombstones, where the
+            # tombstone count is an upper bound (an insert may reuse one) -- a rehash decision
+            # re-counts exactly first. _occ_exact: the next check scans the table.
+            self._tombs_bound = 0
+            self._occ_exact = True
+            # Fired rows: the device-counted copy into a pinned slab (one wait per firing);
+            # more rows than the slab column holds take the synchronous copy.
+            from .window_operator import PinnedSlabPool
+
+            self._pool = PinnedSlabPool()
+            self._fire_rows_async = min(self.ocap, 1 << 20)
+            self._hctr = torch.zeros(16, dtype=torch.int32, pin_memory=True)
+            self._hlate = torch.zeros(1, dtype=torch.int64, pin_memory=True)
+            self._hred = torch.zeros(K.RED_WORDS, dtype=torch.int64, pin_memory=True)
             self.spill_any = False
 
     # ---- buffers ----------------------------------------------------------------------------
@@ -260,6 +275,11 @@ class KeyedSessionOperator:
         tbase = int(t.item())
         if tbase == I64_MAX:
             tbase = 0
+        # GPU, LDS fold: the fold is enqueued right behind the partition and skips itself on the
+        # device when the step's reduced flags ask for a redo -- the partition's flags, the
+        # fold's counters and its late count come back in ONE host wait (tbits fixed at 32).
+        spec = (self.gpu and _SESSION_SORT == "lds"
+                and self.nslots.bit_length() + 32 <= 62)
         while True:
             K.step_begin(self.cursor, self.stats)
             plan = K.PartitionPlan(max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2,
@@ -275,7 +295,16 @@ class KeyedSessionOperator:
             if self.world > 1:
                 self.comm.all_to_all(self.recv, self.send)
                 self.comm.all_to_all(self.recv_counts, self.cursor)
-            host = self.red.cpu().tolist()
+            folded = None
+            if spec:
+                with self._phase("fold_gpu"):
+                    self._fold_prepare()
+                    if self._fold_launch(self.recv, self.recv_counts, self.world, tbase, old_wm,
+                                         32, self.bucket_cap, skip=self.red):
+                        folded = self._fold_counters(with_red=True)
+                        host = self._hred.tolist()
+            if folded is None:
+                host = self.red.cpu().tolist()
             if host[4]:
                 raise RuntimeError("session batch spans more than 2^32 ms")
             if host[7]:
@@ -289,7 +318,10 @@ class KeyedSessionOperator:
             wm_global = old_wm  # every partition idle: the watermark holds
         self.metrics.num_records_in += n
         self.metrics.steps += 1
-        if self.gpu:
+        if folded is not None:
+            with self._phase("fold_gpu"):
+                self._fold_finish(folded, folded[0], tbase, old_wm, 32)
+        elif self.gpu:
             with self._phase("fold_gpu"):
                 self._fold_gpu(tbase, old_wm, max(0, -host[0]))
         else:
@@ -377,14 +409,24 @@ class KeyedSessionOperator:
     def _fold_gpu(self, tbase: int, wm: int, tspan: int) -> None:
         """tspan: the step's largest ts - tbase over all ranks (sizes the sort key's time bits)."""
         tbits = min(32, max(1, int(tspan).bit_length()))  # (no records: tspan is meaningless)
+        self._fold_prepare()
+        h, total = self._fold_recs(self.recv, self.recv_counts, self.world, tbase, wm, tbits,
+                                   self.bucket_cap)
+        self._fold_finish(h, total, tbase, wm, tbits)
+
+    def _fold_prepare(self) -> None:
         if self._live_estimate > 0.9 * self.nslots:
             self._join_spill()
             # Sub-tables may fill up: room in the spill set for every key the lookup may divert.
             self._ensure_spill_capacity(self.batch_capacity)
-        h, total = self._fold_recs(self.recv, self.recv_counts, self.world, tbase, wm, tbits,
-                                   self.bucket_cap)
+
+    def _fold_finish(self, h: list[int], total: int, tbase: int, wm: int, tbits: int) -> None:
+        """Host side of a fold whose counters are read: overflow runs, promotion or host fold
+        of records diverted to spilled keys."""
+        if h[2] > self.host_cap:
+            raise RuntimeError("host diversion buffer overflow")
         self._join_spill()  # the host store must hold last step's spilled rows
-        late = int(self.late_cnt.item()) if total else 0
+        late = h[6] if total else 0
         n_host = h[2]
         # Overflow runs first: the refold below reuses the overflow buffers.
         late += self._overflow_runs(h, wm)
@@ -401,29 +443,8 @@ class KeyedSessionOperator:
         Returns the host counters c[:6] and the number of looked-up records."""
         m, st, c = self.native, self._st(), self.ctr
         sbits = self.nslots.bit_length()  # one spare bit: valid keys stay below the sentinel
-        c[:7].zero_()
-        self.late_cnt.zero_()
-        if _SESSION_SORT == "lds" and nsrc * self.nsub * bucket_cap <= self.sort_out.numel() and \
-                m.gpu_session_lookup_sort(
-                    recs.data_ptr(), counts.data_ptr(), nsrc, self.nsub, bucket_cap,
-                    self.cap_log2, self.keys_g.data_ptr(), self.spill_set.data_ptr(),
-                    self.spill_set.numel() - 1, int(self.spill_any), self.sort_out.data_ptr(),
-                    self.vals_out.data_ptr(), c[0:1].data_ptr(), self.host_recs.data_ptr(),
-                    c[2:3].data_ptr(), self.host_cap, 0, tbits, st):
-            # Lookup + per-sub-table LDS segmented sort in one kernel: (slot, ts)-ordered records
-            # without holes, straight into the merge (no device-wide radix sort). The record count
-            # stays on the device (the merge reads it); the host learns it with the counters.
-            m.gpu_session_merge(self.sort_out.data_ptr(), self.vals_out.data_ptr(),
-                                c[0:1].data_ptr(), self.heads.data_ptr(), c[1:2].data_ptr(),
-                                nsrc * self.nsub * bucket_cap, tbits, self.gap, self.lateness,
-                                wm, tbase,
-                                self.agg, self.cap_log2, self.nslots, self.sess.data_ptr(),
-                                self.slot_due.data_ptr(), self.slot_last.data_ptr(),
-                                self.late_cnt.data_ptr(), self.ovf_slots.data_ptr(),
-                                c[4:5].data_ptr(), self.ovf_rows.data_ptr(), c[5:6].data_ptr(),
-                                self.ovf_cap, st)
-            with self._phase("fold_gpu.sync"):
-                h = c[:6].cpu().tolist()
+        if self._fold_launch(recs, counts, nsrc, tbase, wm, tbits, bucket_cap):
+            h = self._fold_counters()
             if h[2] > self.host_cap:
                 raise RuntimeError("host diversion buffer overflow")
             return h, h[0]
@@ -432,7 +453,7 @@ class KeyedSessionOperator:
                              self.spill_set.data_ptr(), self.spill_set.numel() - 1,
                              int(self.spill_any), self.sort_key.data_ptr(), self.vals_buf.data_ptr(),
                              c[0:1].data_ptr(), self.host_recs.data_ptr(), c[2:3].data_ptr(),
-                             self.host_cap, 0, tbits, st)
+                             self.host_cap, c[3:4].data_ptr(), tbits, st)
         total = int(c[0].item())
         if total:
             # Key-value radix sort over the used bits only (slot | ts - tbase); values ride along.
@@ -451,11 +472,59 @@ class KeyedSessionOperator:
                                 self.slot_last.data_ptr(), self.late_cnt.data_ptr(),
                                 self.ovf_slots.data_ptr(), c[4:5].data_ptr(),
                                 self.ovf_rows.data_ptr(), c[5:6].data_ptr(), self.ovf_cap, st)
-        with self._phase("fold_gpu.sync"):
-            h = c[:6].cpu().tolist()
+        h = self._fold_counters()
         if h[2] > self.host_cap:
             raise RuntimeError("host diversion buffer overflow")
         return h, total
+
+    # Reduced-vector words whose non-zero value makes a speculatively launched fold skip itself:
+    # [3] bucket overflow (redo), [4] span > 2^32 ms, [7] reserved key id.
+    _SKIP_MASK = (1 << 3) | (1 << 4) | (1 << 7)
+
+    def _fold_launch(self, recs, counts, nsrc: int, tbase: int, wm: int, tbits: int,
+                     bucket_cap: int, skip: torch.Tensor | None = None) -> bool:
+        """Lookup + per-sub-table LDS segmented sort in one kernel -- (slot, ts)-ordered records
+        without holes, straight into the merge (no device-wide radix sort). The record count
+        stays on the device (the merge reads it); the host learns it with the counters. False:
+        the LDS path does not apply (nothing launched)."""
+        m, st, c = self.native, self._st(), self.ctr
+        c[:7].zero_()
+        self.late_cnt.zero_()
+        if _SESSION_SORT != "lds" or nsrc * self.nsub * bucket_cap > self.sort_out.numel():
+            return False
+        if not m.gpu_session_lookup_sort(
+                recs.data_ptr(), counts.data_ptr(), nsrc, self.nsub, bucket_cap,
+                self.cap_log2, self.keys_g.data_ptr(), self.spill_set.data_ptr(),
+                self.spill_set.numel() - 1, int(self.spill_any), self.sort_out.data_ptr(),
+                self.vals_out.data_ptr(), c[0:1].data_ptr(), self.host_recs.data_ptr(),
+                c[2:3].data_ptr(), self.host_cap, c[3:4].data_ptr(), tbits, st,
+                skip.data_ptr() if skip is not None else 0,
+                self._SKIP_MASK if skip is not None else 0):
+            return False
+        m.gpu_session_merge(self.sort_out.data_ptr(), self.vals_out.data_ptr(),
+                            c[0:1].data_ptr(), self.heads.data_ptr(), c[1:2].data_ptr(),
+                            nsrc * self.nsub * bucket_cap, tbits, self.gap, self.lateness,
+                            wm, tbase,
+                            self.agg, self.cap_log2, self.nslots, self.sess.data_ptr(),
+                            self.slot_due.data_ptr(), self.slot_last.data_ptr(),
+                            self.late_cnt.data_ptr(), self.ovf_slots.data_ptr(),
+                            c[4:5].data_ptr(), self.ovf_rows.data_ptr(), c[5:6].data_ptr(),
+                            self.ovf_cap, st)
+        return True
+
+    def _fold_counters(self, with_red: bool = False) -> list[int]:
+        """The fold's counters and late count in one wait (two small copies into pinned memory,
+        one stream sync); inserted keys go into the occupancy bookkeeping. Returns c[:6] with
+        the late-dropped count of the fold appended (h[6])."""
+        with self._phase("fold_gpu.sync"):
+            if with_red:
+                self._hred.copy_(self.red, non_blocking=True)
+            self._hctr.copy_(self.ctr, non_blocking=True)
+            self._hlate.copy_(self.late_cnt, non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            h = self._hctr[:6].tolist() + [int(self._hlate[0])]
+        self._live_estimate += h[3]
+        return h
 
     def _diverted(self, n_host: int, tbase: int):
         r = self.host_recs[: n_host * K.REC_WORDS].view(-1, K.REC_WORDS)
@@ -504,7 +573,8 @@ class KeyedSessionOperator:
                                                     self.slot_due.data_ptr(),
                                                     self.slot_last.data_ptr(),
                                                     self.ctr[4:5].data_ptr(), self._st())
-                    n_bad = int(self.ctr[4].item())
+                    ins, n_bad = self.ctr[3:5].tolist()
+                    self._live_estimate += ins
                 if n_bad:  # sub-table full (rare): those keys' sessions go back to the store
                     slots = slots_t.cpu().numpy()
                     bad = slots < 0
@@ -546,7 +616,7 @@ class KeyedSessionOperator:
                 cap *= 2  # a bucket overflowed (skewed keys): larger buckets, partition again
             h, total = self._fold_recs(self._rf_send, self._rf_cursor, 1, tbase, wm, tbits, cap)
             self.metrics.records_promoted += n_host - h[2]
-            late = int(self.late_cnt.item()) if total else 0
+            late = h[6] if total else 0
             late += self._overflow_runs(h, wm)
             return h[2], late
 
@@ -577,9 +647,20 @@ class KeyedSessionOperator:
                            self.out_start.data_ptr(), self.out_end.data_ptr(),
                            self.out_val.data_ptr(), self.out_raw.data_ptr(),
                            self.out_cnt.data_ptr(), c[6:7].data_ptr(), self.ocap, st)
-        k = int(c[6].item())
+        from .window_operator import CountedHostRows
+
+        ka = self._fire_rows_async
+        cols = [t[:ka] for t in (self.out_key, self.out_start, self.out_end, self.out_val,
+                                 self.out_raw, self.out_cnt)]
+        rows = CountedHostRows(self._pool, cols, c[6:7], [c])
+        rows.wait()
+        k = int(rows.fixed(0)[6])
         if k > self.ocap:
             raise RuntimeError(f"session emit buffer overflow ({k} > {self.ocap})")
+        if k <= ka:
+            h = rows.columns(k)
+            return SessionRows(h[0].view(np.uint64), h[1], h[2], h[3], h[4],
+                               h[5].astype(np.int64))
         return SessionRows(self.out_key[:k].cpu().numpy().view(np.uint64),
                            self.out_start[:k].cpu().numpy(), self.out_end[:k].cpu().numpy(),
                            self.out_val[:k].cpu().numpy(), self.out_raw[:k].cpu().numpy(),
@@ -609,6 +690,8 @@ class KeyedSessionOperator:
         self.spill_any = True
         with self._phase("spill.evict_kernel"):
             nr_all, ne = self.ctr[7:9].cpu().tolist()
+        self._live_estimate -= ne
+        self._tombs_bound += ne
         nr = min(nr_all, R)
         cold = slots is None  # idle keys: fired-and-unmodified sessions go to a cold chunk
         if not nr:
@@ -726,14 +809,28 @@ class KeyedSessionOperator:
                              self.ctr[9:10].data_ptr(), st)
         self.metrics.rehashes += 1
 
-    def _maybe_spill(self, wm: int) -> None:
+    def _count_occupancy(self) -> tuple[int, int]:
+        """Exact (live, occupied) slot counts: a table scan and a host sync."""
         k = self.keys_g
         with self._phase("spill.occupancy"):
             live, occupied = torch.stack([((k != EMPTY_KEY) & (k != TOMB_KEY)).sum(),
                                           (k != EMPTY_KEY).sum()]).tolist()
-        self._live_estimate = int(live)
+        self._live_estimate, self._tombs_bound = int(live), int(occupied - live)
+        self._occ_exact = False
+        return int(live), int(occupied)
+
+    def _maybe_spill(self, wm: int) -> None:
+        # Live keys come from the kernels' insert / evict counters; the table is scanned only
+        # after a restore and when the tombstone bound suggests a rehash.
+        if self._occ_exact:
+            live, occupied = self._count_occupancy()
+        else:
+            live, occupied = self._live_estimate, self._live_estimate + self._tombs_bound
+            if occupied > 0.85 * self.nslots and live < 0.6 * self.nslots:
+                live, occupied = self._count_occupancy()
         if occupied > 0.85 * self.nslots and live < 0.6 * self.nslots:
             self._rehash()
+            self._tombs_bound = 0
         if live > self.max_load * self.nslots and wm > I64_MIN:
             # LRU by last event time: keys idle for idle_spill_ms move to host DRAM (keys with no
             # live session are simply freed).
@@ -799,6 +896,8 @@ class KeyedSessionOperator:
         for k, v in meta.get("metrics", {}).items():
             setattr(self.metrics, k, v)
         self.store = self.native.SessionStore(self.gap, self.lateness, self.agg)
+        if self.gpu:
+            self._occ_exact = True  # slots written below: the next check scans the table
         cols = [np.ascontiguousarray(rows[k], dtype=np.int64)
                 for k in ("key", "start", "end", "acc", "cnt", "flags")]
         if not self.gpu:

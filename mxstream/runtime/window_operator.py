@@ -128,6 +128,66 @@ def to_host_arrays(cols: list[torch.Tensor], n: int, pool: PinnedSlabPool | None
 _D2H = _os.environ.get("MXS_D2H", "kernel")  # "dma": hipMemcpyAsync (A/B)
 
 
+class CountedHostRows:
+    """Columns whose row count is still on the device, copied to one pinned slab WITHOUT a host
+    round trip: the copy kernel reads the uint32 count (`n_dev`) itself and moves only that many
+    rows (gpu_d2h_counted); small `fixed` device tensors (flags, per-window bounds) ride along
+    whole. The host reads the slab once `ready()` -- nothing blocks at launch, so a firing no
+    longer drains the stream twice (once for its count, once for its rows).
+
+    Layout: fixed tensors first (16-byte granules), then each column at its capacity."""
+
+    def __init__(self, pool: PinnedSlabPool, cols: list[torch.Tensor], n_dev: torch.Tensor,
+                 fixed: list[torch.Tensor] = ()):
+        from ..ops.native import load
+
+        self.cols_meta, self.fixed_meta, copies, off = [], [], [], 0
+        for t in fixed:
+            nb = t.numel() * t.element_size()
+            if nb % 16 or not t.is_contiguous() or t.data_ptr() % 16:
+                raise ValueError("CountedHostRows: fixed tensors must be 16-byte granules")
+            copies.append((t.data_ptr(), nb, off, 0))
+            self.fixed_meta.append((off, nb, t.dtype))
+            off += (nb + 255) & ~255
+        self.cap = min(c.numel() for c in cols)
+        for c in cols:
+            nb = self.cap * c.element_size()
+            if not c.is_contiguous() or c.data_ptr() % 16 or nb % 16:
+                raise ValueError("CountedHostRows: columns must be contiguous, 16-byte aligned "
+                                 "and a 16-byte multiple long")
+            copies.append((c.data_ptr(), nb, off, c.element_size()))
+            self.cols_meta.append((off, c.dtype))
+            off += (nb + 255) & ~255
+        self.t, self.arr = pool.take(off)
+        dev = cols[0].device
+        e = load().gpu_d2h_counted(self.t.data_ptr(), copies, n_dev.data_ptr(),
+                                   torch.cuda.current_stream(dev).cuda_stream)
+        if e != 0:
+            raise RuntimeError(f"gpu_d2h_counted failed (hipError {e})")
+        self.ev = torch.cuda.Event()
+        self.ev.record(torch.cuda.current_stream(dev))
+
+    def ready(self) -> bool:
+        return self.ev.query()
+
+    def wait(self) -> None:
+        while not self.ev.query():
+            pass
+
+    def fixed(self, i: int) -> np.ndarray:
+        off, nb, dt = self.fixed_meta[i]
+        return self.arr[off:off + nb].view(_NP_DTYPE[dt])
+
+    def columns(self, n: int) -> list[np.ndarray]:
+        """The first n rows of every column (views of the slab); n is capped at the capacity."""
+        n = min(n, self.cap)
+        out = []
+        for off, dt in self.cols_meta:
+            es = torch.empty((), dtype=dt).element_size()
+            out.append(self.arr[off:off + n * es].view(_NP_DTYPE[dt]))
+        return out
+
+
 _NP_DTYPE = {torch.int64: np.int64, torch.int32: np.int32, torch.float64: np.float64,
              torch.float32: np.float32, torch.uint8: np.uint8, torch.int16: np.int16,
              torch.bfloat16: np.uint16, torch.float16: np.float16}
@@ -192,6 +252,20 @@ class FireResult:
     raw: np.ndarray | None  # int64 raw accumulator (exact integer sums / f64 bit pattern)
     counts: np.ndarray | None  # int32 element counts (raw / counts: None for emit="key_value")
     refire: bool = False
+    seq: int = 0            # the operator's batch count when the firing was triggered (1-based
+                            # process() call; latency accounting of deferred results)
+
+
+@dataclass
+class _PendingFire:
+    """A firing whose rows are on their way to the host (CountedHostRows): stands in the output
+    list at its place until resolved (KeyedWindowOperator._resolve)."""
+    rows: "CountedHostRows"
+    wins: list              # window starts of the group, in firing order
+    kv: bool                # compact (key id, value) rows
+    only_dirty: bool
+    bounds: bool            # per-window cumulative counts in fixed(1); else the count is flags[2]
+    seq: int = 0
 
 
 @dataclass
@@ -233,6 +307,7 @@ class _Back:
     chk_dev: object = None  # all-reduced combiner check on the device (AggPlan.skip)
     aplan: object = None    # the step's aggregation plan (redo after a combiner overflow)
     maxb: int = 0  # largest bucket fill of the step's partition (0: not reported)
+    seq: int = 0   # metrics.steps after this batch (FireResult.seq of what it fires)
 
 
 @dataclass
@@ -440,7 +515,9 @@ class KeyedWindowOperator:
         self.out_vals = torch.empty(orows, dtype=torch.float64, device=dev)
         self.out_raw = torch.empty(orows, dtype=torch.int64, device=dev)
         self.out_cnt = torch.empty(orows, dtype=torch.int32, device=dev)
-        self.fire_bounds = torch.zeros(self._fire_group, dtype=torch.int32, device=dev)
+        # (>= 32 entries: a fused re-firing reports up to 32 windows' bounds)
+        self.fire_bounds = torch.zeros((max(self._fire_group, 32) + 3) & ~3, dtype=torch.int32,
+                                       device=dev)
         self._hbounds = torch.zeros(self._fire_group, dtype=torch.int32,
                                     pin_memory=dev.type == "cuda")
         # flags: [0] table full (bit0) / [1] combiner overflow / [2] fired-row cursor (out_n), so
@@ -449,6 +526,9 @@ class KeyedWindowOperator:
         # Pinned slabs for fired rows, allocated here: a first-fire pinned allocation of the
         # whole-table slab costs milliseconds of host time inside a step.
         self._pool = None
+        # Firings copy their rows with a device-counted kernel and resolve later (no host sync
+        # per firing); MXS_ASYNC_FIRE=0 restores the synchronous count -> copy path (A/B).
+        self._async_fire = dev.type == "cuda" and _os.environ.get("MXS_ASYNC_FIRE", "1") != "0"
         if dev.type == "cuda":
             self._pool = PinnedSlabPool()
             self._pool.take(orows * 28 + 4 * 256)
@@ -769,7 +849,7 @@ class KeyedWindowOperator:
         if not self.pipeline:
             b = self._settle(self._front(keys, ts, vals))
             self._back_begin(b)
-            return out + self._back_finish(b)
+            return self._resolve(out + self._back_finish(b))
         prev, self._pending = self._pending, None
         if prev is not None:
             with self._s1():
@@ -778,7 +858,9 @@ class KeyedWindowOperator:
         if prev is not None:
             out += self._back_finish(prev)
         self._pending = self._settle(f)     # the step's one host sync (S1 keeps working)
-        return out
+        # Firings whose rows have reached the host are returned now; the others stay queued
+        # (in order) for the next call -- the host never waits on a fire's copy here.
+        return self._resolve(out, block=False)
 
     def flush(self) -> list[FireResult]:
         """Complete the pending state half of the last batch (pipelined mode); returns what it
@@ -787,12 +869,12 @@ class KeyedWindowOperator:
         out, self._carry = self._carry, []
         prev, self._pending = self._pending, None
         if prev is None:
-            return out
+            return self._resolve(out)
         with self._s1():
             self._back_begin(prev)
         out += self._back_finish(prev)
         self._verify_combine()  # callers read or replace the state next
-        return out
+        return self._resolve(out)
 
     # ---- step phases ------------------------------------------------------------------------
     def _front(self, keys, ts, vals) -> "_Front":
@@ -927,7 +1009,7 @@ class KeyedWindowOperator:
             nl = min(int(st[K.STAT_LATE]), self.late_idx.numel())
             self.late_side.append(self.late_idx[:nl].cpu().numpy().copy())
         b = _Back(par=f.par, n=f.n, old_wm=f.old_wm, rw=f.rw, pane_base=f.pane_base,
-                  maxb=int(st[K.STAT_MAXBUCKET]))
+                  maxb=int(st[K.STAT_MAXBUCKET]), seq=self.metrics.steps + 1)
         if qmin <= qmax:
             gmin, gmax = f.pane_base + qmin, f.pane_base + qmax
             lo = gmin if self.min_live_pane is None else min(self.min_live_pane, gmin)
@@ -1024,6 +1106,8 @@ class KeyedWindowOperator:
                 self._maybe_spill()
         if self.timer is not None:
             self.timer.flush()
+        for r in out:
+            r.seq = b.seq
         return out
 
     # ---- host-DRAM spill tier (runtime/window_spill.py) -----------------------------------
@@ -1137,9 +1221,11 @@ class KeyedWindowOperator:
         self.wm = wm
         self.metrics.current_watermark = wm
         with self._s1():
-            out.extend(self._fire_ready(wm))
+            fired = self._fire_ready(wm)
             self._purge(wm)
-        return out
+        for r in fired:
+            r.seq = self.metrics.steps
+        return out + self._resolve(fired)
 
     def finish(self) -> list[FireResult]:
         """End of input: event time emits Long.MAX_VALUE (fires everything); processing time does
@@ -1176,8 +1262,11 @@ class KeyedWindowOperator:
                       out_raw=None if kv else self.out_raw, out_cnt=None if kv else self.out_cnt,
                       out_n=self.out_n, slot_list=self.dlist if only_dirty else None,
                       slot_list_n=self.dlist_n if only_dirty else None, key32=kv)
-        n = self._fired_count()
         self.metrics.num_fires += 1
+        pend = self._fire_async([s], kv, only_dirty, bounds=False)
+        if pend is not None:
+            return pend
+        n = self._fired_count()
         if n == 0:
             return None
         n = min(n, self.out_keys.numel())
@@ -1185,6 +1274,68 @@ class KeyedWindowOperator:
         host = self._rows_to_host(n, kv)
         return FireResult(s, s + self.size, host[0], host[1], host[2], host[3],
                           refire=only_dirty)
+
+    def _fire_cols(self, kv: bool) -> list[torch.Tensor]:
+        if kv:
+            return [self.out_keys.view(torch.int32), self.out_vals]
+        return [self.out_keys, self.out_vals, self.out_raw, self.out_cnt]
+
+    def _fire_async(self, wins: list[int], kv: bool, only_dirty: bool,
+                    bounds: bool) -> "_PendingFire | None":
+        """The enqueued firing's rows -> pinned slab by the device-counted copy kernel, with the
+        flags (and the group's bounds) alongside; no host sync. None: not available here (CPU,
+        MXS_ASYNC_FIRE=0) -- the caller syncs as before."""
+        if not self._async_fire:
+            return None
+        k = len(wins)
+        n_dev = self.fire_bounds[k - 1:k] if bounds else self.out_n
+        fixed = [self.flags, self.fire_bounds] if bounds else [self.flags]
+        try:
+            rows = CountedHostRows(self._pool, self._fire_cols(kv), n_dev, fixed)
+        except ValueError:
+            return None
+        return _PendingFire(rows, list(wins), kv, only_dirty, bounds)
+
+    def _finish_pending(self, p: _PendingFire) -> list[FireResult]:
+        """Rows of a resolved firing (its copy has completed) as FireResults, one per window."""
+        hf = p.rows.fixed(0).tolist()
+        n_single = self._check_fire_flags(hf)
+        b = p.rows.fixed(1)[:len(p.wins)].tolist() if p.bounds else [n_single]
+        n = min(b[-1], p.rows.cap)
+        if n <= 0:
+            return []
+        self.metrics.num_records_out += n
+        cols = p.rows.columns(n)
+        keys = cols[0].view(np.uint32) if p.kv else cols[0].view(np.uint64)
+        vals = cols[1]
+        raw = None if p.kv else cols[2]
+        cnt = None if p.kv else cols[3]
+        out, lo = [], 0
+        for s, hi in zip(p.wins, b):
+            hi = min(hi, n)
+            if hi > lo:
+                out.append(FireResult(s, s + self.size, keys[lo:hi], vals[lo:hi],
+                                      None if raw is None else raw[lo:hi],
+                                      None if cnt is None else cnt[lo:hi],
+                                      refire=p.only_dirty, seq=p.seq))
+            lo = hi
+        return out
+
+    def _resolve(self, items: list, block: bool = True) -> list[FireResult]:
+        """Replace pending firings by their rows, in order. block=False: stop at the first
+        firing whose copy is still running and keep it and everything after it (in order) for
+        the next call (self._carry)."""
+        out = []
+        for i, it in enumerate(items):
+            if isinstance(it, _PendingFire):
+                if not block and not it.rows.ready():
+                    self._carry = items[i:] + self._carry
+                    return out
+                it.rows.wait()
+                out.extend(self._finish_pending(it))
+            else:
+                out.append(it)
+        return out
 
     def _key_value_rows(self) -> bool:
         """Compact fired rows (emit="key_value"): dense key ids fit 32 bits."""
@@ -1347,7 +1498,7 @@ class KeyedWindowOperator:
                 out.append(r)
         return out
 
-    def _fire_many(self, starts: list[int], only_dirty: bool) -> list[FireResult]:
+    def _fire_many(self, starts: list[int], only_dirty: bool) -> list:
         """Batched firing: a group of due windows is evaluated by one native call (one fire
         launch per window, rows appended at a shared cursor, the cursor recorded after each
         window), then ONE host sync and ONE copy to the pinned slab for the whole group -- a
@@ -1370,6 +1521,11 @@ class KeyedWindowOperator:
                 wins.append((s, (p0, p1 - p0 + 1, float(s), float(s + self.size))))
         stream = torch.cuda.current_stream(self.device).cuda_stream if cuda else 0
         stage = self._fire_stage(kv) if cuda else None
+        if cuda and only_dirty and self.dlist is not None and 1 < len(wins) <= 32 \
+                and _os.environ.get("MXS_FUSED_REFIRE", "1") != "0":
+            res = self._refire_fused(wins, kv, plan, stage, stream)
+            if res is not None:
+                return res
         g = self._fire_group
         for i in range(0, len(wins), g):
             chunk = wins[i:i + g]
@@ -1382,8 +1538,13 @@ class KeyedWindowOperator:
                                      0 if kv else self.out_raw.data_ptr(),
                                      0 if kv else self.out_cnt.data_ptr(), self.out_n.data_ptr(),
                                      self.fire_bounds.data_ptr(), stream, stage)
-            bounds = self._fired_bounds(len(chunk))
             self.metrics.num_fires += len(chunk)
+            pend = self._fire_async([s for s, _ in chunk], kv, only_dirty, bounds=True) \
+                if cuda else None
+            if pend is not None:
+                out.append(pend)
+                continue
+            bounds = self._fired_bounds(len(chunk))
             n = min(bounds[-1], self.out_keys.numel())
             if n == 0:
                 continue
@@ -1399,6 +1560,36 @@ class KeyedWindowOperator:
                 lo = hi
         return out
 
+    def _refire_fused(self, wins: list, kv: bool, plan: dict, stage: tuple,
+                      stream: int) -> list | None:
+        """Every re-fired window of the step in ONE pass over the touched-slot list
+        (gpu_window_refire_many: each listed slot's union of panes is loaded once), packed in
+        window order and copied with the device-counted kernel; one wait. The stage is split k
+        ways; a window that outgrows its share (more touched slots than nslots * group / k)
+        flags it and the group re-runs per window. None: not fusable here."""
+        k = len(wins)
+        region = (self.out_keys.numel() // k) & ~3
+        if region < 4:
+            return None
+        self.flags[3:4].zero_()
+        ok = self._m.gpu_window_refire_many(
+            self.keys_g.data_ptr(), self.acc_g.data_ptr(), self.cnt_g.data_ptr(),
+            self.dirty_g.data_ptr(), plan, [w for _, w in wins], self.out_keys.data_ptr(),
+            self.out_vals.data_ptr(), 0 if kv else self.out_raw.data_ptr(),
+            0 if kv else self.out_cnt.data_ptr(), self.out_n.data_ptr(),
+            self.fire_bounds.data_ptr(), self.flags[3:4].data_ptr(), stream,
+            stage[:5] + (region,))
+        if not ok:
+            return None
+        rows = CountedHostRows(self._pool, self._fire_cols(kv), self.fire_bounds[k - 1:k],
+                               [self.flags, self.fire_bounds])
+        rows.wait()
+        if int(rows.fixed(0)[3]) & 16:
+            self.metrics.extra["refire_unfused"] = self.metrics.extra.get("refire_unfused", 0) + 1
+            return None
+        self.metrics.num_fires += k
+        return self._finish_pending(_PendingFire(rows, [s for s, _ in wins], kv, True, True))
+
     def _fire_stage(self, kv: bool = False) -> tuple:
         """Per-window staging regions of the GPU batched firing (window_fire_many: window w of
         a group writes rows [w * nslots, (w + 1) * nslots) at its own counter, a pack kernel
@@ -1411,7 +1602,7 @@ class KeyedWindowOperator:
                   torch.empty(n, dtype=torch.float64, device=dev),
                   torch.empty(n, dtype=torch.int64, device=dev),
                   torch.empty(n, dtype=torch.int32, device=dev),
-                  torch.empty(self._fire_group, dtype=torch.int32, device=dev))
+                  torch.empty(max(self._fire_group, 32), dtype=torch.int32, device=dev))
             self._stage_cols = st
         ptrs = [t.data_ptr() for t in st]
         if kv:  # compact rows: no raw / count columns

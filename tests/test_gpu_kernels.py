@@ -474,3 +474,98 @@ def test_batched_fire_gpu_equals_cpu(gpu_device, emit):
     g, c = run(gpu_device), run("cpu")
     assert len(c) > 100
     assert g == c
+
+
+def test_counted_d2h_copies_device_count(gpu_device):
+    """gpu_d2h_counted: the copy kernel reads the row count on the device and moves only those
+    rows (rounded to 16 bytes) of each column; fixed tensors travel whole."""
+    from mxstream.runtime.window_operator import CountedHostRows, PinnedSlabPool
+
+    cap = 4096
+    a = torch.arange(cap, dtype=torch.int64, device=gpu_device) * 3
+    b = torch.arange(cap, dtype=torch.int32, device=gpu_device) - 7
+    flags = torch.tensor([5, 0, 1234, 0], dtype=torch.int32, device=gpu_device)
+    n = torch.tensor([1234, 0, 0, 0], dtype=torch.int32, device=gpu_device)
+    pool = PinnedSlabPool()
+    t, arr = pool.take(1 << 16)
+    arr[:] = 0xAB  # sentinel: rows past the count must stay untouched
+    del t, arr
+    rows = CountedHostRows(pool, [a, b], n[:1], [flags])
+    rows.wait()
+    assert rows.fixed(0).tolist() == [5, 0, 1234, 0]
+    ca, cb = rows.columns(1234)
+    assert np.array_equal(ca, a[:1234].cpu().numpy())
+    assert np.array_equal(cb, b[:1234].cpu().numpy())
+    # 1234 int64 rows = 9872 bytes (a 16-byte multiple): the next row was not copied
+    off_a = rows.cols_meta[0][0]
+    assert (rows.arr[off_a + 9872:off_a + 9880] == 0xAB).all()
+
+
+@pytest.mark.parametrize("emit", ["full", "key_value"])
+@pytest.mark.parametrize("pipeline", [False, "stream", True])
+def test_async_fire_equals_sync_fire(gpu_device, emit, pipeline, monkeypatch):
+    """Firings resolved later (device-counted copy, no host sync per firing; pipelined calls
+    return only what has reached the host and queue the rest in order) emit exactly the
+    synchronous path's firings and re-firings, in the same order, with batch tags that never
+    precede the batch that triggered them."""
+
+    def run(async_fire):
+        monkeypatch.setenv("MXS_ASYNC_FIRE", "1" if async_fire else "0")
+        op = KeyedWindowOperator(size=6000, slide=1000, lateness=3000, agg=K.AGG_SUM_I64,
+                                 device=gpu_device, max_keys=100_000, batch_capacity=200_000,
+                                 ooo_bound=500, dense_keys=True, emit=emit, pipeline=pipeline)
+        assert op._async_fire == async_fire
+        rows, tags = [], []
+        for step in range(16):
+            k = torch.empty(200_000, dtype=torch.int64, device=gpu_device)
+            t = torch.empty_like(k)
+            v = torch.empty_like(k)
+            K.gen_events(k, t, v, seed=31, stream_id=0, idx0=step * 200_000, nkeys=80_000,
+                         ts_base=step * 1000, ts_span=1000, disorder=500, val_lo=0,
+                         val_span=1000)
+            if step > 6:
+                t[:10_000] -= 2500
+            out = op.process(k, t, v)
+            tags += [(step + 1, r.seq) for r in out]
+            rows += out
+        rows += op.finish()
+        assert all(seq <= call for call, seq in tags)
+        return [(r.window_start, r.refire, sorted(zip(r.keys.tolist(), r.values.tolist())))
+                for r in rows]
+
+    a, s = run(True), run(False)
+    assert sum(1 for r in s if r[1]) > 5  # re-firings happened
+    assert a == s
+
+
+@pytest.mark.parametrize("emit", ["full", "key_value"])
+def test_fused_refire_equals_per_window(gpu_device, emit, monkeypatch):
+    """All windows a step re-fires in one pass over the touched-slot list (union of their panes
+    loaded once per slot, map/filter epilogue per window) == one sweep per window."""
+    prog = E.compile_expr(E.var(E.VAR_RESULT) * 0.5)
+    filt = E.compile_expr(E.var(E.VAR_MAPPED) > 40.0)
+
+    def run(fused):
+        monkeypatch.setenv("MXS_FUSED_REFIRE", "1" if fused else "0")
+        op = KeyedWindowOperator(size=6000, slide=1000, lateness=4000, agg=K.AGG_SUM_I64,
+                                 device=gpu_device, max_keys=50_000, batch_capacity=100_000,
+                                 ooo_bound=300, dense_keys=True, emit=emit, map_prog=prog,
+                                 filter_prog=filt)
+        rows = []
+        for step in range(14):
+            k = torch.empty(100_000, dtype=torch.int64, device=gpu_device)
+            t = torch.empty_like(k)
+            v = torch.empty_like(k)
+            K.gen_events(k, t, v, seed=41, stream_id=0, idx0=step * 100_000, nkeys=40_000,
+                         ts_base=step * 1000, ts_span=1000, disorder=300, val_lo=0, val_span=100)
+            if step > 7:
+                t[:8_000] -= 3500  # re-fires 3-4 already fired windows per step
+            rows += op.process(k, t, v)
+        rows += op.finish()
+        return [(r.window_start, r.refire, sorted(zip(r.keys.tolist(), r.values.tolist())))
+                for r in rows], op
+
+    (f, fop), (u, _) = run(True), run(False)
+    assert sum(1 for r in u if r[1]) > 10
+    assert f == u
+    assert fop.metrics.extra.get("refire_unfused", 0) == 0
