@@ -82,6 +82,11 @@ PartPlan make_part(py::dict d) {
   p.dense_bits = d.contains("dense_bits") ? d["dense_bits"].cast<int32_t>() : 0;
   p.dense_mul = d.contains("dense_mul") ? d["dense_mul"].cast<uint32_t>() : 0u;
   p.key32 = d.contains("key32") ? d["key32"].cast<int32_t>() : 0;
+  p.scratch = reinterpret_cast<uint64_t*>(d.contains("scratch") ? d["scratch"].cast<intptr_t>() : 0);
+  p.scratch_cursor = reinterpret_cast<uint32_t*>(
+      d.contains("scratch_cursor") ? d["scratch_cursor"].cast<intptr_t>() : 0);
+  if ((p.scratch != nullptr) != (p.scratch_cursor != nullptr))
+    throw std::invalid_argument("two-level partition: scratch and scratch_cursor together");
   if (p.dense_bits < 0 || p.dense_bits > 32 || (p.dense_bits && (p.nranks != 1 ||
       p.nsub_log2 > p.dense_bits || !(p.dense_mul & 1u))))
     throw std::invalid_argument("dense keys: one destination, nsub <= 2^bits, odd multiplier");
@@ -148,6 +153,9 @@ AggPlan make_agg(py::dict d) {
     if (!p.dcnt || !p.dlist) throw std::invalid_argument("delta ring needs dcnt and the slot list");
   }
   if (p.split < 1 || p.split > 1024) throw std::invalid_argument("agg split out of range");
+  p.pmask = d.contains("pmask") ? d["pmask"].cast<uint32_t>() : 0u;
+  if (p.pmask && !(p.pmask >> 31) && __builtin_popcount(p.pmask) != p.np_step)
+    throw std::invalid_argument("sparse panes: np_step must equal popcount(pmask)");
   return p;
 }
 
@@ -297,7 +305,11 @@ PYBIND11_MODULE(_mxs_native, m) {
       .def_readwrite("tbase", &PartPlan::tbase)
       .def_readwrite("rec_words", &PartPlan::rec_words)
       .def_readwrite("bucket_cap", &PartPlan::bucket_cap)
-      .def_readwrite("drop_late", &PartPlan::drop_late);
+      .def_readwrite("drop_late", &PartPlan::drop_late)
+      .def_property("scratch", [](const PartPlan& a) { return (intptr_t)a.scratch; },
+                    [](PartPlan& a, intptr_t v) { a.scratch = reinterpret_cast<uint64_t*>(v); })
+      .def_property("scratch_cursor", [](const PartPlan& a) { return (intptr_t)a.scratch_cursor; },
+                    [](PartPlan& a, intptr_t v) { a.scratch_cursor = reinterpret_cast<uint32_t*>(v); });
   py::class_<AggPlan>(m, "AggPlanObj")
       .def(py::init(&make_agg))
       .def_readwrite("split", &AggPlan::split)
@@ -312,7 +324,8 @@ PYBIND11_MODULE(_mxs_native, m) {
       .def_readwrite("rec_words", &AggPlan::rec_words)
       .def_readwrite("ring", &AggPlan::ring)
       .def_readwrite("nsrc", &AggPlan::nsrc)
-      .def_readwrite("combined", &AggPlan::combined);
+      .def_readwrite("combined", &AggPlan::combined)
+      .def_readwrite("pmask", &AggPlan::pmask);
   m.def("window_front", [](bool gpu, intptr_t keys, intptr_t ts, intptr_t vals, intptr_t jhash,
                            int64_t n, const PartPlan& p, intptr_t kg_dest, intptr_t cursor,
                            intptr_t out, intptr_t stats, intptr_t late_idx, uint32_t late_cap,

@@ -64,6 +64,7 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
   int64_t tmax = stats[kStatMaxTs], qmin = stats[kStatMinPane], qmax = stats[kStatMaxPane];
   int64_t nlate = 0, nacc = 0;
   int64_t ovf = 0;
+  uint32_t pmask = 0;  // kStatPaneMask, as the GPU partitions report it
   for (int64_t i = 0; i < n; ++i) {
     const uint64_t key = keys[i];
     const int64_t t = ts[i];
@@ -89,6 +90,7 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
       }
       qmin = std::min(qmin, q);
       qmax = std::max(qmax, q);
+      pmask |= 1u << (rt < 31u ? rt : 31u);
     }
     ++nacc;
     const int32_t jh = p.nranks == 1 ? 0 : p.hash_mode ? jhash_tab[key] : java_long_hash((int64_t)key);
@@ -122,6 +124,7 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
   stats[kStatLate] += nlate;
   stats[kStatAccepted] += nacc;
   stats[kStatOverflow] |= ovf;
+  stats[kStatPaneMask] |= pmask;
 }
 
 void step_begin(uint32_t* cursor, int nb, int64_t* stats) {

@@ -180,7 +180,7 @@ __device__ __forceinline__ int64_t block_reduce_i64(int64_t v, int64_t* red, int
   // op: 0 = max, 1 = min, 2 = sum. `red` = kMaxWaves int64 of LDS.
   for (int o = 32; o > 0; o >>= 1) {
     const int64_t w = __shfl_xor(v, o);
-    v = op == 0 ? (v > w ? v : w) : op == 1 ? (v < w ? v : w) : v + w;
+    v = op == 0 ? (v > w ? v : w) : op == 1 ? (v < w ? v : w) : op == 3 ? (v | w) : v + w;
   }
   const int wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   __syncthreads();
@@ -189,10 +189,13 @@ __device__ __forceinline__ int64_t block_reduce_i64(int64_t v, int64_t* red, int
   v = red[0];
   for (int i = 1; i < nw; ++i) {
     const int64_t w = red[i];
-    v = op == 0 ? (v > w ? v : w) : op == 1 ? (v < w ? v : w) : v + w;
+    v = op == 0 ? (v > w ? v : w) : op == 1 ? (v < w ? v : w) : op == 3 ? (v | w) : v + w;
   }
   return v;
 }
+
+// Relative pane -> kStatPaneMask bit (bit 31: pane >= 31, mask unusable).
+__device__ __forceinline__ uint32_t pane_bit(uint32_t q) { return 1u << (q < 31u ? q : 31u); }
 
 // ILP factor: each thread issues kPartU independent loads before it consumes any, so 16 waves
 // per CU keep ~16 x 64 x kPartU loads in flight (the loop was latency-bound at one chain).
@@ -262,6 +265,7 @@ __global__ __launch_bounds__(1024) void partition_kernel(
   const int64_t end = start + chunk < n ? start + chunk : n;
   const int64_t bstep = (int64_t)blockDim.x * kPlainU;
   int64_t tmax = INT64_MIN, qmin = INT64_MAX, qmax = INT64_MIN, nlate = 0, nacc = 0;
+  uint32_t pmask = 0;
   int bad = 0;  // stats overflow bits: 2 unrepresentable pane, 8 reserved key
 
   // Pass A: histogram + stats.
@@ -297,6 +301,7 @@ __global__ __launch_bounds__(1024) void partition_kernel(
       ++nacc;
       qmin = (int64_t)e.t < qmin ? (int64_t)e.t : qmin;
       qmax = (int64_t)e.t > qmax ? (int64_t)e.t : qmax;
+      pmask |= pane_bit(e.t);
       atomicAdd(&lhist[e.bucket], 1u);
     }
   }
@@ -372,6 +377,7 @@ __global__ __launch_bounds__(1024) void partition_kernel(
   qmin = block_reduce_i64(qmin, lred, 1);
   qmax = block_reduce_i64(qmax, lred, 0);
   nacc = block_reduce_i64(nacc, lred, 2);
+  pmask = (uint32_t)block_reduce_i64(pmask, lred, 3);
   if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
   const int64_t flags = block_reduce_i64(overflow ? 1 : 0, lred, 0) |
                         block_reduce_i64(bad & 2, lred, 0) | block_reduce_i64(bad & 8, lred, 0) |
@@ -383,6 +389,7 @@ __global__ __launch_bounds__(1024) void partition_kernel(
       atomicMin((long long*)&stats[kStatMinPane], (long long)qmin);
       atomicMax((long long*)&stats[kStatMaxPane], (long long)qmax);
       atomicAdd((unsigned long long*)&stats[kStatAccepted], (unsigned long long)nacc);
+      if (pmask) atomicOr((unsigned long long*)&stats[kStatPaneMask], (unsigned long long)pmask);
     }
     if (!late_idx && nlate) atomicAdd((unsigned long long*)&stats[kStatLate], (unsigned long long)nlate);
     if (flags) atomicOr((unsigned long long*)&stats[kStatOverflow], (unsigned long long)flags);
@@ -464,6 +471,7 @@ __global__ __launch_bounds__(1024) void partition_staged_kernel(
   const int64_t start = (int64_t)blockIdx.x * chunk;
   const int64_t end = start + chunk < n ? start + chunk : n;
   int64_t tmax = INT64_MIN, qmin = INT64_MAX, qmax = INT64_MIN, nlate = 0, nacc = 0;
+  uint32_t pmask = 0;
   int bad = 0;  // stats overflow bits: 2 unrepresentable pane, 8 reserved key
 
   // Pass A: histogram (into run_base) + stats.
@@ -498,6 +506,7 @@ __global__ __launch_bounds__(1024) void partition_staged_kernel(
       }
       ++nacc;
       qmin = (int64_t)e.t < qmin ? (int64_t)e.t : qmin;
+      pmask |= pane_bit(e.t);
       qmax = (int64_t)e.t > qmax ? (int64_t)e.t : qmax;
       atomicAdd(&run_base[e.bucket], 1u);
     }
@@ -635,6 +644,7 @@ __global__ __launch_bounds__(1024) void partition_staged_kernel(
   qmin = block_reduce_i64(qmin, lred, 1);
   qmax = block_reduce_i64(qmax, lred, 0);
   nacc = block_reduce_i64(nacc, lred, 2);
+  pmask = (uint32_t)block_reduce_i64(pmask, lred, 3);
   if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
   const int64_t flags = (any_ovf ? 1 : 0) | block_reduce_i64(bad & 2, lred, 0) |
                         block_reduce_i64(bad & 8, lred, 0);
@@ -644,6 +654,7 @@ __global__ __launch_bounds__(1024) void partition_staged_kernel(
       atomicMin((long long*)&stats[kStatMinPane], (long long)qmin);
       atomicMax((long long*)&stats[kStatMaxPane], (long long)qmax);
       atomicAdd((unsigned long long*)&stats[kStatAccepted], (unsigned long long)nacc);
+      if (pmask) atomicOr((unsigned long long*)&stats[kStatPaneMask], (unsigned long long)pmask);
     }
     if (!late_idx && nlate) atomicAdd((unsigned long long*)&stats[kStatLate], (unsigned long long)nlate);
     if (flags) atomicOr((unsigned long long*)&stats[kStatOverflow], (unsigned long long)flags);
@@ -800,6 +811,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
 
   int64_t tmax = INT64_MIN, nlate = 0, nacc = 0;
   uint32_t qmin32 = 0xFFFFFFFFu, qmax32 = 0;  // relative panes are u32: 32-bit min/max per event
+  uint32_t pmask = 0;  // kStatPaneMask
   int64_t flags = 0;
   const bool pane32 = plan.window_mode && plan.pane > 0 && plan.pane < ((int64_t)1 << 31);
   const uint32_t pane_u = (uint32_t)plan.pane;
@@ -880,6 +892,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
         const uint32_t qp = q * pane_u;
         q = qp > du ? q - 1u : (du - qp >= pane_u ? q + 1u : q);
         qmin32 = q < qmin32 ? q : qmin32;
+        pmask |= pane_bit(q);
         qmax32 = q > qmax32 ? q : qmax32;
         flags |= (int64_t)(int32_t)v != (int64_t)v ? 4 : 0;  // needs 24-byte records
         uint32_t b;
@@ -924,6 +937,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
         } else {
           if ((int64_t)(int32_t)v != (int64_t)v) flags |= 4;  // needs 24-byte records
           qmin32 = e.t < qmin32 ? e.t : qmin32;
+          pmask |= pane_bit(e.t);
           qmax32 = e.t > qmax32 ? e.t : qmax32;
           keep[u] = true;
           bk[u] = e.bucket;
@@ -984,6 +998,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
   tmax = block_reduce_i64(tmax, lred, 0);
   qmin = block_reduce_i64(qmin, lred, 1);
   qmax = block_reduce_i64(qmax, lred, 0);
+  pmask = (uint32_t)block_reduce_i64(pmask, lred, 3);
   if (!late_idx) nlate = block_reduce_i64(nlate, lred, 2);
   flags = (any_ovf ? 1 : 0) | block_reduce_i64(flags & 2, lred, 0) |
           block_reduce_i64(flags & 4, lred, 0) | block_reduce_i64(flags & 8, lred, 0) |
@@ -994,6 +1009,7 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
       atomicMin((long long*)&stats[kStatMinPane], (long long)qmin);
       atomicMax((long long*)&stats[kStatMaxPane], (long long)qmax);
       atomicAdd((unsigned long long*)&stats[kStatAccepted], (unsigned long long)nacc);
+      if (pmask) atomicOr((unsigned long long*)&stats[kStatPaneMask], (unsigned long long)pmask);
     }
     if (!late_idx && nlate) atomicAdd((unsigned long long*)&stats[kStatLate], (unsigned long long)nlate);
     if (flags) atomicOr((unsigned long long*)&stats[kStatOverflow], (unsigned long long)flags);
@@ -1196,6 +1212,14 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
     for (uint32_t i = threadIdx.x; i < (cap >> 5); i += blockDim.x) sbit[i] = 0;
   }
 
+  // Sparse pane rows (AggPlan.pmask): LDS row j of the step holds relative pane srel[j].
+  __shared__ int32_t srel[32];
+  const bool sparse = p.pmask != 0u && !(p.pmask >> 31);
+  if (sparse && threadIdx.x == 0) {
+    int j = 0;
+    for (int b = 0; b < 31; ++b)
+      if (p.pmask >> b & 1u) srel[j++] = b;
+  }
   int inserted = 0;
   bool ovf = false, fxbad = false;
   for (int pg0 = 0; pg0 < p.np_step; pg0 += p.pg) {
@@ -1237,7 +1261,8 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
           if (e >= c) break;
           const Rec& r = rr[u];
           if (r.t == 0xFFFFFFFFu) continue;  // hole record (staged partition padding)
-          const int64_t q = (int64_t)r.t - q0;
+          const int64_t q = sparse ? (r.t < 31u ? (int64_t)__popc(p.pmask & ((1u << r.t) - 1u)) - pg0 : -1)
+                                   : (int64_t)r.t - q0;
           if (q < 0 || q >= npg) continue;
           uint32_t s;
           if constexpr (DENSE) {
@@ -1294,7 +1319,8 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
         oa[w] = 0;
         gi[w] = 0;
         if (dc[w]) {
-          const int64_t pane = p.pane_base + q0 + (i >> p.cap_log2);
+          const int64_t pane = p.pane_base + (sparse ? (int64_t)srel[pg0 + (i >> p.cap_log2)]
+                                                     : q0 + (int64_t)(i >> p.cap_log2));
           gi[w] = (size_t)(pane & (p.ring - 1)) * nslots + sbase + (i & mask);
           if (!shared_sub) {
             oc[w] = cnt_g[gi[w]];
@@ -1318,7 +1344,8 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
           if (AGG != AGG_COUNT) acc_g[gi[w]] = oc[w] ? agg_combine(AGG, oa[w], d) : d;
           cnt_g[gi[w]] = oc[w] + dc[w];
         }
-        if (p.pane_base + q0 + (int64_t)(i >> p.cap_log2) <= p.fired_hi) {
+        if (p.pane_base + (sparse ? (int64_t)srel[pg0 + (i >> p.cap_log2)]
+                                  : q0 + (int64_t)(i >> p.cap_log2)) <= p.fired_hi) {
           dirty_g[gi[w]] = 1;
           late[w] = true;
           if (p.dacc) {  // local-global delta ring (this workgroup owns the slot: plain RMW)
@@ -2507,7 +2534,9 @@ __device__ __forceinline__ uint32_t sess_probe_insert(uint64_t* keys, uint64_t k
     const uint64_t prev = atomicCAS((unsigned long long*)&keys[target], (unsigned long long)expect,
                                     (unsigned long long)key);
     if (prev == expect) {
-      if (!use_tomb && inserted) atomicAdd(inserted, 1u);
+      // every new key counts (into an empty slot or a reused tombstone): the host derives the
+      // live-key count from inserts - evictions (session_operator occupancy bookkeeping)
+      if (inserted) atomicAdd(inserted, 1u);
       return target;
     }
     if (prev == key) return target;
@@ -3680,6 +3709,82 @@ void launch_compact(const uint64_t* keys, const int64_t* ts, const uint64_t* val
 static const bool kPairEnv = getenv_int("MXS_PAIR", 1) != 0;  // A/B knobs (profiles)
 static const bool kFastEnv = getenv_int("MXS_PART_FAST", 1) != 0;
 
+
+// ------------------------------------------------------------------------------------------
+// Two-level partition, level 2 (8-byte records, one destination, > 512 buckets): one workgroup
+// per coarse bucket splits its records into the 2^L fine buckets it owns (fine = the low L bits
+// of the sub-table). The plain scatter wrote every record into one of 4096 open runs per
+// workgroup -- partially written lines evicted long before they filled; here a workgroup has
+// 2^L open runs, each wave writes its records as <= 2^L contiguous pieces (wave ballot per
+// distinct fine bucket, one LDS atomic per piece), and no global atomic is needed: the fine
+// buckets' cursors are this workgroup's LDS counters. Holes of the coarse staging are dropped.
+// ------------------------------------------------------------------------------------------
+constexpr int kSplitThreads = 1024;
+
+__global__ __launch_bounds__(kSplitThreads) void partition_split_kernel(
+    const uint2* __restrict__ coarse, const uint32_t* __restrict__ coarse_n, uint32_t ccap,
+    PartPlan plan, int L, uint32_t* __restrict__ cursor, uint2* __restrict__ out,
+    int64_t* __restrict__ stats) {
+  __shared__ uint32_t scnt[32];
+  __shared__ uint32_t sovf;
+  const uint32_t c = blockIdx.x;
+  const uint32_t nf = 1u << L, fmask = nf - 1u;
+  if (threadIdx.x < nf) scnt[threadIdx.x] = 0;
+  if (threadIdx.x == 0) sovf = 0;
+  __syncthreads();
+  uint32_t n = coarse_n[c];
+  n = n < ccap ? n : ccap;
+  const uint2* src = coarse + (size_t)c * ccap;
+  const uint32_t bcap = plan.bucket_cap;
+  const unsigned long long lt = (1ull << lane_id()) - 1ull;
+  bool ovf = false;
+  for (uint32_t base = 0; base < n; base += kSplitThreads * 4) {
+    uint2 r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t e = base + u * kSplitThreads + threadIdx.x;
+      if (e < n) {
+        const unsigned long long w =
+            __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(src) + e);
+        r[u] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+      } else {
+        r[u] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const bool live = (r[u].y & 15u) != kNarrowHoleT;
+      const uint32_t f = live ? sub_of((uint64_t)r[u].x, plan) & fmask : 0xFFFFFFFFu;
+      // One piece per distinct fine bucket in the wave: its lanes write contiguously.
+      unsigned long long todo = __ballot(live);
+      while (todo) {
+        const int leader = __ffsll((long long)todo) - 1;
+        const uint32_t fl = __shfl(f, leader);
+        const unsigned long long m = __ballot(live && f == fl);
+        uint32_t b = 0;
+        if (lane_id() == leader) b = atomicAdd(&scnt[fl], (uint32_t)__popcll(m));
+        b = __shfl(b, leader);
+        if (live && f == fl) {
+          const uint32_t pos = b + (uint32_t)__popcll(m & lt);
+          if (pos < bcap)
+            out[(size_t)((c << L) | fl) * bcap + pos] = r[u];
+          else
+            ovf = true;
+        }
+        todo &= ~m;
+      }
+    }
+  }
+  if (ovf) sovf = 1;
+  __syncthreads();
+  if (threadIdx.x < nf) {
+    const uint32_t k = scnt[threadIdx.x];
+    cursor[(c << L) | threadIdx.x] = k;
+  }
+  if (threadIdx.x == 0 && sovf)
+    atomicOr((unsigned long long*)&stats[kStatOverflow], 1ull);  // bucket overflow: redo
+}
+
 template <bool ONE, int RB>
 void dispatch_compact(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                       const int32_t* jhash_tab, int64_t n, const PartPlan& plan,
@@ -3725,6 +3830,23 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
     if (plan.nranks != 1 || (uint64_t)nb * plan.bucket_cap >= (1ull << 32))
       throw std::invalid_argument("partition: 8-byte records need one destination");
     if (n <= 0) return;
+    if (nb > kCMaxNb && plan.scratch && plan.scratch_cursor && nb <= kCMaxNb * 32) {
+      // Two-level: compact staged partition into 512 coarse buckets, then the split kernel.
+      int L = 0;
+      while ((nb >> L) > kCMaxNb) ++L;
+      PartPlan pc = plan;
+      pc.nsub_log2 = plan.nsub_log2 - L;
+      pc.bucket_cap = plan.bucket_cap << L;
+      hipStream_t st = (hipStream_t)stream;
+      HIP_CHECK(hipMemsetAsync(plan.scratch_cursor, 0, sizeof(uint32_t) * (nb >> L), st));
+      dispatch_compact<true, 8>(keys, ts, vals, jhash_tab, n, pc, kg_dest, plan.scratch_cursor,
+                                (Rec*)plan.scratch, stats, late_idx, late_cap, stream);
+      hipLaunchKernelGGL(partition_split_kernel, dim3(nb >> L), dim3(kSplitThreads), 0, st,
+                         (const uint2*)plan.scratch, plan.scratch_cursor, pc.bucket_cap, plan, L,
+                         cursor, (uint2*)out, stats);
+      HIP_CHECK(hipGetLastError());
+      return;
+    }
     if (nb > kCMaxNb) {
       if (plan.key32)
         throw std::invalid_argument("partition: int32 keys need <= 512 buckets");
@@ -3843,6 +3965,7 @@ template <int AGG, int RW, bool PK, bool DENSE, bool DET = false>
 static void launch_agg_v(const Rec* recs, const uint32_t* counts, const AggPlan& p,
                          uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
                          uint32_t* occ, uint32_t* flags, size_t lds, hipStream_t s) {
+  if (lds + 32 * 4 > 160 * 1024) throw std::runtime_error("window_agg: LDS image exceeds 160 KiB");
   static bool attr = false;
   if (!attr) {  // allow the full 160 KiB LDS
     HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, RW, PK, DENSE, DET>,
@@ -3915,9 +4038,9 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& plan, ui
                 uint32_t* flags, intptr_t stream) {
   if (plan.np_step <= 0 || plan.nsub <= 0) return;
   const size_t cap = (size_t)1 << plan.cap_log2;
+  // (conservative LDS size; launch_agg_d sizes each variant exactly and checks the limit)
   const size_t lds = cap * 8 + (size_t)plan.pg * cap * (plan.det ? 20 : 12) + 16 +
                      (plan.dlist ? 16 + cap / 8 + cap * 4 : 0);  // touched-slot bitmap + buffer
-  if (lds > 160 * 1024) throw std::runtime_error("window_agg: LDS image exceeds 160 KiB");
   if (plan.rec_words < 3 && plan.combined)
     throw std::invalid_argument("window_agg: combined records are 24-byte records");
   hipStream_t s = (hipStream_t)stream;

@@ -498,6 +498,11 @@ struct PartPlan {
   int32_t dense_bits;        // > 0: dense key ids < 2^dense_bits, directly addressed (dense_slot)
   uint32_t dense_mul;        // odd multiplier of the dense slot bijection
   int32_t key32;             // 1: the key column is int32 (dictionary ids), sign-extended on load
+  // GPU, 8-byte records, one destination, more than 512 buckets: a two-level partition -- the
+  // LDS-staged compact kernel into nb / 2^L coarse buckets (this scratch, bucket_cap << L each),
+  // then a split kernel per coarse bucket into its 2^L fine buckets. 0: the plain scatter.
+  uint64_t* scratch;
+  uint32_t* scratch_cursor;  // [512] coarse fills
 };
 
 // Sub-table of a key: a 32-bit multiplicative hash of both key halves (3 32-bit multiplies).
@@ -580,7 +585,9 @@ MXS_HD bool rel_pane(int64_t ts, const PartPlan& p, uint32_t* t_out, int64_t* pa
 //       bit1 an element's pane is not representable
 // Panes in [1]/[2] are relative to the step's pane base.
 constexpr int kStatMaxTs = 0, kStatMinPane = 1, kStatMaxPane = 2, kStatLate = 3, kStatOverflow = 4,
-              kStatAccepted = 5, kStatMaxBucket = 6, kStatCount = 8;
+              kStatAccepted = 5, kStatMaxBucket = 6, kStatPaneMask = 7, kStatCount = 8;
+// kStatPaneMask (GPU partitions): bit j = some accepted record has relative pane j (j < 31);
+// bit 31 = a record has relative pane >= 31 (the mask is then not used). 0 = not computed.
 
 
 // ------------------------------------------------------------------------------------------

@@ -54,6 +54,11 @@ struct AggPlan {
   // the check (window_operator.py _verify_combine), instead of waiting for it before the
   // all-to-all.
   const int64_t* skip;
+  // Sparse pane groups: non-zero (bit 31 clear) = the relative panes with records this step
+  // (the partition's kStatPaneMask); np_step then counts the set bits and the LDS rows of a pass
+  // map to those panes only -- the empty panes between a late pane and the current ones cost no
+  // record pass. 0: the dense range [p_lo, p_lo + np_step).
+  uint32_t pmask;
 };
 
 // Plan of one window firing.

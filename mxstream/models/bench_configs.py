@@ -155,9 +155,10 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
                              map_prog=E.compile_expr(mbps),
                              filter_prog=E.compile_expr(E.var(E.VAR_MAPPED) < thr),
                              dense_keys=dense_keys, pipeline=pipeline, emit="key_value")
-    kt = torch.empty(batch, dtype=torch.int64, device=dev)
-    tt = torch.empty_like(kt)
-    vt = torch.empty_like(kt)
+    # dense keyed state: the keys are dictionary ids (int32, as the columnar ingest emits them)
+    kt = torch.empty(batch, dtype=torch.int32 if dense_keys else torch.int64, device=dev)
+    tt = torch.empty(batch, dtype=torch.int64, device=dev)
+    vt = torch.empty_like(tt)
     late_n = batch // 20
     step_i = [0]
     lat = []

@@ -183,6 +183,7 @@ class AggPlan:
     dacc: int = 0        # local-global delta ring of late data (data pointers, 0 = off) ...
     dcnt: int = 0        # ... and its counts
     skip: int = 0        # device int64: non-zero -> leave the state untouched (incomplete exchange)
+    pmask: int = 0       # GPU: relative panes with records (sparse pane rows; np_step = popcount)
 
     def as_dict(self) -> dict:
         return dict(self.__dict__)

@@ -307,6 +307,8 @@ class _Back:
     chk_dev: object = None  # all-reduced combiner check on the device (AggPlan.skip)
     aplan: object = None    # the step's aggregation plan (redo after a combiner overflow)
     maxb: int = 0  # largest bucket fill of the step's partition (0: not reported)
+    pmask: int = 0  # relative panes with records (GPU partition, one rank's own records)
+    np_act: int = 0  # panes the aggregation visits (popcount(pmask), else np_step)
     seq: int = 0   # metrics.steps after this batch (FireResult.seq of what it fires)
 
 
@@ -658,7 +660,20 @@ class KeyedWindowOperator:
                      if self._exchanging and not self.combine else None)
         self._recv_counts = (torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
                              if self._exchanging else None)
+        # Two-level GPU partition (8-byte records, one destination, > 512 buckets): the coarse
+        # staging buffer and its 512 cursors (csrc partition_split_kernel).
+        self._scratch = self._scratch_cursor = None
+        if self._two_level_ok():
+            self._scratch = torch.empty(self.nbuckets * self.bucket_cap, dtype=torch.int64,
+                                        device=dev)
+            self._scratch_cursor = torch.zeros(512, dtype=torch.int32, device=dev)
+        self._pplan_key = None  # bucket capacity / scratch changed: rebuild the plan object
         self._use_par(0)
+
+    def _two_level_ok(self) -> bool:
+        return (self.device.type == "cuda" and self._part_ranks == 1
+                and 512 < self.nbuckets <= 512 * 32
+                and _os.environ.get("MXS_TWO_LEVEL", "1") != "0")
 
     def _use_par(self, p: int) -> None:
         """Point send/cursor (and, at G = 1, recv/recv_counts) at buffer set `p`."""
@@ -920,11 +935,12 @@ class KeyedWindowOperator:
         # int32 key ids (the columnar sources' dictionary ids): read as they are by the compact
         # GPU partition (4 bytes less per event in both passes); widened for the other paths.
         key32 = f.keys.dtype == torch.int32
-        if key32 and cuda and not (self.rec_w in (1, 2) and self.nbuckets <= 512
+        two_level = self.rec_w == 1 and self._scratch is not None
+        if key32 and cuda and not ((self.rec_w in (1, 2) and self.nbuckets <= 512 or two_level)
                                    and self.nbuckets * self.bucket_cap < (1 << 32)):
             f.keys = f.keys.to(torch.int64)
             key32 = False
-        key = (self.bucket_cap, self.rec_w, int(event_mode), key32)
+        key = (self.bucket_cap, self.rec_w, int(event_mode), key32, two_level)
         if self._pplan_key != key:
             self._pplan = self._m.PartPlanObj(K.PartitionPlan(
                 max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2,
@@ -932,6 +948,9 @@ class KeyedWindowOperator:
                 hash_mode=self.hash_mode, bucket_cap=self.bucket_cap, pane=self.pane,
                 rec_words=self.rec_w, dense_bits=self.dense_bits,
                 dense_mul=self.dense_mul, key32=int(key32)).as_dict())
+            if two_level:
+                self._pplan.scratch = self._scratch.data_ptr()
+                self._pplan.scratch_cursor = self._scratch_cursor.data_ptr()
             self._pplan_key = key
         pp = self._pplan
         pp.late_ts = self._late_ts(f.old_wm)
@@ -1032,7 +1051,18 @@ class KeyedWindowOperator:
                                                  if self.dlist is not None else 0)
             b.has_data = True
             b.qmin, b.np_step = qmin, gmax - gmin + 1
-            b.pg = max(1, min(b.np_step, lds_budget // (cap * (20 if self.deterministic else 12))))
+            # Sparse pane rows: the aggregation visits only the panes that received records (a
+            # late pane and the current ones, not the empty panes between them). Own records
+            # only: the exchanged / combined paths keep the dense range.
+            pm = int(st[7]) & 0xFFFFFFFF
+            b.pmask = pm if (pm and not pm >> 31 and self.device.type == "cuda"
+                             and not self._exchanging and not self.combine
+                             and _os.environ.get("MXS_SPARSE_PANES", "1") != "0") else 0
+            b.np_act = bin(b.pmask).count("1") if b.pmask else b.np_step
+            if self.dense_bits:
+                lds_budget += cap * 8  # no LDS key table for dense ids
+            per_pane = 20 if self.deterministic else (8 if self._agg_pack_ok(b.rw) else 12)
+            b.pg = max(1, min(b.np_act, lds_budget // (cap * per_pane)))
             b.gmin, b.gmax = gmin, gmax
         self.metrics.steps += 1
         if not self.external_watermark:
@@ -1067,11 +1097,14 @@ class KeyedWindowOperator:
                         self._exchange(b.rw)
                 if cuda and self._exchanging:
                     self._ev_consumed[b.par] = self._event()
+                sparse = bool(b.pmask) and not combined
                 aplan = K.AggPlan(cap_log2=self.cap_log2, nsub=self.nsub, ring=self.ring,
                                   agg=self.agg, nsrc=self._part_ranks, bucket_cap=bcap,
-                                  np_step=b.np_step, pg=b.pg, pane_base=b.pane_base,
+                                  np_step=b.np_act if sparse else b.np_step, pg=b.pg,
+                                  pane_base=b.pane_base,
                                   p_lo=b.qmin, fired_hi=b.fired_hi, combined=combined,
-                                  rec_words=3 if combined else b.rw)
+                                  rec_words=3 if combined else b.rw,
+                                  pmask=b.pmask if sparse else 0)
                 aplan.dense_bits, aplan.dense_mul = self.dense_bits, self.dense_mul
                 aplan.det = int(self.deterministic)
                 # Hot keys: a sub-table holding more than AGG_SLICE records is shared by several
@@ -1192,13 +1225,21 @@ class KeyedWindowOperator:
         ap = self._aplan
         ap.np_step, ap.pane_base, ap.p_lo, ap.fired_hi = (aplan.np_step, aplan.pane_base,
                                                           aplan.p_lo, aplan.fired_hi)
-        ap.split, ap.skip = aplan.split, aplan.skip
+        ap.split, ap.skip, ap.pmask = aplan.split, aplan.skip, aplan.pmask
         cuda = self.device.type == "cuda"
         self._m.window_agg_obj(cuda, recs.data_ptr(), counts.data_ptr(), ap,
                                self.keys_g.data_ptr(), self.acc_g.data_ptr(),
                                self.cnt_g.data_ptr(), self.dirty_g.data_ptr(),
                                self.occ.data_ptr(), self.flags.data_ptr(),
                                torch.cuda.current_stream(self.device).cuda_stream if cuda else 0)
+
+    def _agg_pack_ok(self, rw: int) -> bool:
+        """Mirror of the launcher's packed (sum, count) LDS accumulator condition (8 bytes per
+        slot and pane instead of 12): integer sums of 8/16-byte own records, < 65536 records
+        per sub-table."""
+        return (self.agg in (K.AGG_SUM_I64, K.AGG_AVG_I64) and rw <= 2 and not self.combine
+                and self._part_ranks * self.bucket_cap < 65536
+                and _os.environ.get("MXS_AGG_PACK", "1") != "0")
 
     def _zero_pane(self, so: int, k: int = 1) -> None:
         """Reset k consecutive pane slabs starting at slot index `so` (pane-major state)."""

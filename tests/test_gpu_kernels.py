@@ -569,3 +569,70 @@ def test_fused_refire_equals_per_window(gpu_device, emit, monkeypatch):
     assert sum(1 for r in u if r[1]) > 10
     assert f == u
     assert fop.metrics.extra.get("refire_unfused", 0) == 0
+
+
+@pytest.mark.parametrize("narrow", [True, False])
+def test_sparse_pane_rows_equal_dense(gpu_device, narrow, monkeypatch):
+    """A step whose records fall into a late pane and the current panes (empty panes between
+    them) aggregates only the panes that have records (partition pane mask -> sparse LDS rows):
+    every firing and re-firing equals the dense pane range's, and both equal the C++ twin."""
+
+    def run(dev, sparse):
+        monkeypatch.setenv("MXS_SPARSE_PANES", "1" if sparse else "0")
+        op = KeyedWindowOperator(size=8000, slide=1000, lateness=6000, agg=K.AGG_SUM_I64,
+                                 device=dev, max_keys=60_000, batch_capacity=150_000,
+                                 ooo_bound=200, dense_keys=True,
+                                 narrow=narrow if dev != "cpu" else False)
+        rows = []
+        for step in range(16):
+            k = torch.empty(150_000, dtype=torch.int64, device=dev)
+            t = torch.empty_like(k)
+            v = torch.empty_like(k)
+            K.gen_events(k, t, v, seed=43, stream_id=0, idx0=step * 150_000, nkeys=50_000,
+                         ts_base=step * 1000, ts_span=1000, disorder=200, val_lo=0,
+                         val_span=500)
+            if step > 8:
+                t[:9_000] -= 5200   # 5 panes back
+                t[9_000:12_000] -= 3100  # and 3 panes back
+            rows += op.process(k, t, v)
+        rows += op.finish()
+        return sorted((r.window_start, r.refire, int(a), int(b), int(c))
+                      for r in rows for a, b, c in zip(r.keys, r.raw, r.counts))
+
+    s, d, c = run(gpu_device, True), run(gpu_device, False), run("cpu", False)
+    assert sum(1 for x in c if x[1]) > 1000
+    assert s == d == c
+
+
+@pytest.mark.parametrize("key_dtype", [torch.int32, torch.int64])
+def test_two_level_partition_equals_plain(gpu_device, key_dtype, monkeypatch):
+    """More than 512 sub-tables with 8-byte records: the two-level partition (LDS-staged compact
+    kernel into 512 coarse buckets + per-coarse-bucket split into the fine buckets) fires
+    exactly the plain scatter's rows, re-firings included; int32 key ids go through the
+    compact kernel natively."""
+
+    def run(two_level):
+        monkeypatch.setenv("MXS_TWO_LEVEL", "1" if two_level else "0")
+        op = KeyedWindowOperator(size=4000, slide=1000, lateness=2000, agg=K.AGG_SUM_I64,
+                                 device=gpu_device, max_keys=3_000_000, batch_capacity=1 << 20,
+                                 ooo_bound=300, dense_keys=True, narrow=True)
+        assert op.nbuckets > 512 and (op._scratch is not None) == two_level
+        rows = []
+        for step in range(9):
+            k = torch.empty(1 << 20, dtype=key_dtype, device=gpu_device)
+            t = torch.empty(1 << 20, dtype=torch.int64, device=gpu_device)
+            v = torch.empty_like(t)
+            K.gen_events(k, t, v, seed=47, stream_id=0, idx0=step << 20, nkeys=2_000_000,
+                         ts_base=step * 1000, ts_span=1000, disorder=300, val_lo=0,
+                         val_span=2000)
+            if step > 4:
+                t[:30_000] -= 2500
+            rows += op.process(k, t, v)
+        rows += op.finish()
+        return sorted((r.window_start, r.refire, int(a), int(b), int(c))
+                      for r in rows for a, b, c in zip(r.keys, r.raw, r.counts)), op
+
+    (a, aop), (b, _) = run(True), run(False)
+    assert len(a) > 100_000 and sum(1 for x in a if x[1]) > 1000
+    assert a == b
+    assert aop.metrics.bucket_regrows == 0
