@@ -662,15 +662,17 @@ PYBIND11_MODULE(_mxs_native, m) {
   // n_dev = uint32 row counter. Returns the hipError_t code (0 = ok).
   m.def("gpu_d2h_counted", [](intptr_t dst,
                               const std::vector<std::tuple<intptr_t, int64_t, int64_t, int64_t>>& copies,
-                              intptr_t n_dev, intptr_t stream) {
+                              intptr_t n_dev, intptr_t stream, int max_blocks) {
     if (copies.empty() || copies.size() > (size_t)kD2HMax)
       throw std::invalid_argument("gpu_d2h_counted: 1..8 columns");
     D2HCopy c[kD2HMax];
     for (size_t i = 0; i < copies.size(); ++i)
       c[i] = D2HCopy{(const void*)std::get<0>(copies[i]), std::get<1>(copies[i]),
                      std::get<2>(copies[i]), std::get<3>(copies[i])};
-    return gpu::d2h_kernel((void*)dst, c, (int)copies.size(), stream, P<uint32_t>(n_dev));
-  });
+    return gpu::d2h_kernel((void*)dst, c, (int)copies.size(), stream, P<uint32_t>(n_dev),
+                           max_blocks);
+  }, py::arg("dst"), py::arg("copies"), py::arg("n_dev"), py::arg("stream"),
+     py::arg("max_blocks") = 1024);
   // Keyed-window compaction / eviction (host-DRAM spill tier). out = (key, pane, acc, cnt, dirty,
   // n, cap, counters) pointers.
   auto compact_out = [](const std::vector<intptr_t>& o, uint32_t cap) {

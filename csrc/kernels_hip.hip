@@ -3627,7 +3627,7 @@ int d2h_async(void* dst, const void* src, size_t bytes, intptr_t stream) {
 }
 
 int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream,
-               const uint32_t* n_dev) {
+               const uint32_t* n_dev, int max_blocks) {
   // Device-side address of the pinned host slab (mapped host memory).
   void* dd = nullptr;
   hipError_t e = hipHostGetDevicePointer(&dd, dst_host, 0);
@@ -3643,7 +3643,9 @@ int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream,
       return (int)hipErrorInvalidValue;  // 16-byte granules only (the caller pads)
     total += copies[i].bytes;
   }
-  const int grid = grid_for(total / 16, 256 * 4, 1024);
+  // max_blocks: a copy overlapping compute on a side stream is PCIe-bound; a small grid leaves
+  // the CUs to the compute stream.
+  const int grid = grid_for(total / 16, 256 * 4, max_blocks < 1 ? 1 : max_blocks > 1024 ? 1024 : max_blocks);
   hipLaunchKernelGGL(d2h_copy_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
                      (unsigned char*)dd, b);
   return (int)hipGetLastError();
@@ -3721,9 +3723,48 @@ static const bool kFastEnv = getenv_int("MXS_PART_FAST", 1) != 0;
 // ------------------------------------------------------------------------------------------
 constexpr int kSplitThreads = 1024;
 
+// RB = 8: narrow RecN (hole: pane nibble 15); RB = 24: Rec (hole: t == kHoleT).
+template <int RB>
+struct SplitRec;
+template <>
+struct SplitRec<8> {
+  uint2 r;
+  __device__ __forceinline__ void load(const void* base, size_t i) {
+    const unsigned long long w =
+        __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(base) + i);
+    r = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+  }
+  __device__ __forceinline__ void hole() { r = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu); }
+  __device__ __forceinline__ bool live() const { return (r.y & 15u) != kNarrowHoleT; }
+  __device__ __forceinline__ uint64_t key() const { return (uint64_t)r.x; }
+  __device__ __forceinline__ void store(void* base, size_t i) const {
+    reinterpret_cast<uint2*>(base)[i] = r;
+  }
+};
+template <>
+struct SplitRec<24> {
+  uint64_t w0, w1, w2;  // key | val | aux << 32 | t
+  __device__ __forceinline__ void load(const void* base, size_t i) {
+    const unsigned long long* q = reinterpret_cast<const unsigned long long*>(base) + 3 * i;
+    w0 = __builtin_nontemporal_load(q);
+    w1 = __builtin_nontemporal_load(q + 1);
+    w2 = __builtin_nontemporal_load(q + 2);
+  }
+  __device__ __forceinline__ void hole() { w0 = w1 = w2 = ~0ull; }
+  __device__ __forceinline__ bool live() const { return (uint32_t)w2 != kHoleT; }
+  __device__ __forceinline__ uint64_t key() const { return w0; }
+  __device__ __forceinline__ void store(void* base, size_t i) const {
+    uint64_t* d = reinterpret_cast<uint64_t*>(base) + 3 * i;
+    d[0] = w0;
+    d[1] = w1;
+    d[2] = w2;
+  }
+};
+
+template <int RB>
 __global__ __launch_bounds__(kSplitThreads) void partition_split_kernel(
-    const uint2* __restrict__ coarse, const uint32_t* __restrict__ coarse_n, uint32_t ccap,
-    PartPlan plan, int L, uint32_t* __restrict__ cursor, uint2* __restrict__ out,
+    const void* __restrict__ coarse, const uint32_t* __restrict__ coarse_n, uint32_t ccap,
+    PartPlan plan, int L, uint32_t* __restrict__ cursor, void* __restrict__ out,
     int64_t* __restrict__ stats) {
   __shared__ uint32_t scnt[32];
   __shared__ uint32_t sovf;
@@ -3734,27 +3775,24 @@ __global__ __launch_bounds__(kSplitThreads) void partition_split_kernel(
   __syncthreads();
   uint32_t n = coarse_n[c];
   n = n < ccap ? n : ccap;
-  const uint2* src = coarse + (size_t)c * ccap;
+  const size_t src0 = (size_t)c * ccap;
   const uint32_t bcap = plan.bucket_cap;
   const unsigned long long lt = (1ull << lane_id()) - 1ull;
   bool ovf = false;
   for (uint32_t base = 0; base < n; base += kSplitThreads * 4) {
-    uint2 r[4];
+    SplitRec<RB> r[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const uint32_t e = base + u * kSplitThreads + threadIdx.x;
-      if (e < n) {
-        const unsigned long long w =
-            __builtin_nontemporal_load(reinterpret_cast<const unsigned long long*>(src) + e);
-        r[u] = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
-      } else {
-        r[u] = make_uint2(0xFFFFFFFFu, 0xFFFFFFFFu);
-      }
+      if (e < n)
+        r[u].load(coarse, src0 + e);
+      else
+        r[u].hole();
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const bool live = (r[u].y & 15u) != kNarrowHoleT;
-      const uint32_t f = live ? sub_of((uint64_t)r[u].x, plan) & fmask : 0xFFFFFFFFu;
+      const bool live = r[u].live();
+      const uint32_t f = live ? sub_of(r[u].key(), plan) & fmask : 0xFFFFFFFFu;
       // One piece per distinct fine bucket in the wave: its lanes write contiguously.
       unsigned long long todo = __ballot(live);
       while (todo) {
@@ -3767,7 +3805,7 @@ __global__ __launch_bounds__(kSplitThreads) void partition_split_kernel(
         if (live && f == fl) {
           const uint32_t pos = b + (uint32_t)__popcll(m & lt);
           if (pos < bcap)
-            out[(size_t)((c << L) | fl) * bcap + pos] = r[u];
+            r[u].store(out, (size_t)((c << L) | fl) * bcap + pos);
           else
             ovf = true;
         }
@@ -3777,10 +3815,7 @@ __global__ __launch_bounds__(kSplitThreads) void partition_split_kernel(
   }
   if (ovf) sovf = 1;
   __syncthreads();
-  if (threadIdx.x < nf) {
-    const uint32_t k = scnt[threadIdx.x];
-    cursor[(c << L) | threadIdx.x] = k;
-  }
+  if (threadIdx.x < nf) cursor[(c << L) | threadIdx.x] = scnt[threadIdx.x];
   if (threadIdx.x == 0 && sovf)
     atomicOr((unsigned long long*)&stats[kStatOverflow], 1ull);  // bucket overflow: redo
 }
@@ -3841,9 +3876,9 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
       HIP_CHECK(hipMemsetAsync(plan.scratch_cursor, 0, sizeof(uint32_t) * (nb >> L), st));
       dispatch_compact<true, 8>(keys, ts, vals, jhash_tab, n, pc, kg_dest, plan.scratch_cursor,
                                 (Rec*)plan.scratch, stats, late_idx, late_cap, stream);
-      hipLaunchKernelGGL(partition_split_kernel, dim3(nb >> L), dim3(kSplitThreads), 0, st,
-                         (const uint2*)plan.scratch, plan.scratch_cursor, pc.bucket_cap, plan, L,
-                         cursor, (uint2*)out, stats);
+      hipLaunchKernelGGL(partition_split_kernel<8>, dim3(nb >> L), dim3(kSplitThreads), 0, st,
+                         (const void*)plan.scratch, plan.scratch_cursor, pc.bucket_cap, plan, L,
+                         cursor, (void*)out, stats);
       HIP_CHECK(hipGetLastError());
       return;
     }
@@ -3870,6 +3905,27 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
   }
   if (plan.key32)
     throw std::invalid_argument("partition: int32 keys need compact records (<= 512 buckets)");
+  if (plan.rec_words == 3 && nb > kStageMaxNb && plan.scratch && plan.scratch_cursor &&
+      nb <= kStageMaxNb * 32 && (uint64_t)nb * plan.bucket_cap < (1ull << 32)) {
+    // Two-level 24-byte partition (session / generic records): the write-combined staged
+    // kernel into 512 coarse buckets, then the split kernel into the fine buckets.
+    if (n <= 0) return;
+    int L = 0;
+    while ((nb >> L) > kStageMaxNb) ++L;
+    PartPlan pc = plan;
+    pc.nsub_log2 = plan.nsub_log2 - L;
+    pc.bucket_cap = plan.bucket_cap << L;
+    if (pc.nsub_log2 < 0) throw std::invalid_argument("two-level partition: too few sub-tables");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_CHECK(hipMemsetAsync(plan.scratch_cursor, 0, sizeof(uint32_t) * (nb >> L), st));
+    partition_variant(keys, ts, vals, jhash_tab, n, pc, kg_dest, plan.scratch_cursor,
+                      (Rec*)plan.scratch, stats, late_idx, late_cap, stream, 5);
+    hipLaunchKernelGGL(partition_split_kernel<24>, dim3(nb >> L), dim3(kSplitThreads), 0, st,
+                       (const void*)plan.scratch, plan.scratch_cursor, pc.bucket_cap, plan, L,
+                       cursor, (void*)out, stats);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   // Write-combined staged scatter when the LDS carry buffers fit (<= 512 buckets); otherwise
   // the plain scatter. Both stream their inputs with non-temporal loads (kbench A/B).
   partition_variant(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats, late_idx,
@@ -3965,11 +4021,13 @@ template <int AGG, int RW, bool PK, bool DENSE, bool DET = false>
 static void launch_agg_v(const Rec* recs, const uint32_t* counts, const AggPlan& p,
                          uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
                          uint32_t* occ, uint32_t* flags, size_t lds, hipStream_t s) {
-  if (lds + 32 * 4 > 160 * 1024) throw std::runtime_error("window_agg: LDS image exceeds 160 KiB");
+  // dynamic LDS + the kernel's static sparse-pane table (srel, 128 B) stay <= 160 KiB
+  constexpr size_t kAggDynMax = 160 * 1024 - 512;
+  if (lds > kAggDynMax) throw std::runtime_error("window_agg: LDS image exceeds 160 KiB");
   static bool attr = false;
-  if (!attr) {  // allow the full 160 KiB LDS
+  if (!attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, RW, PK, DENSE, DET>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggDynMax));
     attr = true;
   }
   // Split only what the kernel's atomic merge supports: dense ids (no LDS key table to share),

@@ -166,7 +166,7 @@ int d2h_async(void* dst, const void* src, size_t bytes, intptr_t stream);
 // Up to kD2HMax device buffers -> one pinned (mapped) host slab by a copy kernel on `stream`;
 // every size, source address and slab offset a multiple of 16 bytes. Returns hipError_t.
 int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream,
-               const uint32_t* n_dev = nullptr);
+               const uint32_t* n_dev = nullptr, int max_blocks = 1024);
 // Experiment: pane accumulation by global atomics from the source columns (see kernels_hip).
 void direct_agg_probe(const uint64_t* keys, const int64_t* ts, const uint64_t* vals, int64_t n,
                       int64_t tbase, int64_t pane, int ring, int64_t nslots, uint32_t mul,

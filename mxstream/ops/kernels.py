@@ -117,6 +117,8 @@ class PartitionPlan:
     dense_bits: int = 0      # > 0: dense key ids < 2^dense_bits, directly addressed
     dense_mul: int = 0       # odd multiplier of the dense slot bijection
     key32: int = 0           # 1: int32 key column (compact-record GPU partition only)
+    scratch: int = 0         # GPU two-level partition (> 512 buckets): coarse staging buffer
+    scratch_cursor: int = 0  # ... and its 512 coarse cursors (data pointers; 0 = plain scatter)
 
     @property
     def nbuckets(self) -> int:

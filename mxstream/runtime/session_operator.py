@@ -215,6 +215,15 @@ class KeyedSessionOperator:
         self.cursor = torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
         self.recv_counts = (torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
                             if self.world > 1 else self.cursor)
+        # Two-level GPU partition (> 512 buckets): write-combined staged kernel into 512 coarse
+        # buckets, then the split kernel (csrc partition_split_kernel<24>). Opt-in: for config 5's
+        # 24-byte records it measured 407 + 205 us against 464 us for the plain scatter
+        # (profiles/r3_cfg5_two_level.md).
+        self._scratch = self._scratch_cursor = None
+        if self.gpu and 512 < self.nbuckets <= 512 * 32 and \
+                __import__("os").environ.get("MXS_TWO_LEVEL24", "0") == "1":
+            self._scratch = torch.empty(words, dtype=torch.int64, device=dev)
+            self._scratch_cursor = torch.zeros(512, dtype=torch.int32, device=dev)
         if self.gpu:
             total = self.nbuckets * self.bucket_cap
             self.sort_key = torch.empty(total, dtype=torch.int64, device=dev)
@@ -285,6 +294,9 @@ class KeyedSessionOperator:
             plan = K.PartitionPlan(max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2,
                                    nranks=self.world, window_mode=1, drop_late=0, hash_mode=0,
                                    bucket_cap=self.bucket_cap, late_ts=I64_MIN, tbase=tbase, pane=1)
+            if self._scratch is not None:
+                plan.scratch = self._scratch.data_ptr()
+                plan.scratch_cursor = self._scratch_cursor.data_ptr()
             if n:
                 K.partition(keys, ts, vals, plan, self.kg_dest, self.cursor, self.send, self.stats)
             K.step_finish(self.stats, self.local_maxts, self.red, bound=self.ooo_bound,

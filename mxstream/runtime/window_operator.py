@@ -138,7 +138,10 @@ class CountedHostRows:
     Layout: fixed tensors first (16-byte granules), then each column at its capacity."""
 
     def __init__(self, pool: PinnedSlabPool, cols: list[torch.Tensor], n_dev: torch.Tensor,
-                 fixed: list[torch.Tensor] = ()):
+                 fixed: list[torch.Tensor] = (), copy_stream=None):
+        """copy_stream: run the copy there, after the producer's work on the current stream
+        (it overlaps the compute that follows; ``done`` is the event the producer must wait for
+        before it overwrites the columns)."""
         from ..ops.native import load
 
         self.cols_meta, self.fixed_meta, copies, off = [], [], [], 0
@@ -160,12 +163,20 @@ class CountedHostRows:
             off += (nb + 255) & ~255
         self.t, self.arr = pool.take(off)
         dev = cols[0].device
-        e = load().gpu_d2h_counted(self.t.data_ptr(), copies, n_dev.data_ptr(),
-                                   torch.cuda.current_stream(dev).cuda_stream)
+        cur = torch.cuda.current_stream(dev)
+        st = cur
+        if copy_stream is not None:
+            ready = torch.cuda.Event()
+            ready.record(cur)
+            copy_stream.wait_event(ready)
+            st = copy_stream
+        e = load().gpu_d2h_counted(self.t.data_ptr(), copies, n_dev.data_ptr(), st.cuda_stream,
+                                   64 if copy_stream is not None else 1024)
         if e != 0:
             raise RuntimeError(f"gpu_d2h_counted failed (hipError {e})")
         self.ev = torch.cuda.Event()
-        self.ev.record(torch.cuda.current_stream(dev))
+        self.ev.record(st)
+        self.done = self.ev
 
     def ready(self) -> bool:
         return self.ev.query()
@@ -531,6 +542,13 @@ class KeyedWindowOperator:
         # Firings copy their rows with a device-counted kernel and resolve later (no host sync
         # per firing); MXS_ASYNC_FIRE=0 restores the synchronous count -> copy path (A/B).
         self._async_fire = dev.type == "cuda" and _os.environ.get("MXS_ASYNC_FIRE", "1") != "0"
+        # Fired-row copies run on a side stream, overlapping the next step's kernels; a firing
+        # that reuses an output buffer first waits for the copy still reading it (_claim).
+        self._copy_stream = (torch.cuda.Stream(dev) if self._async_fire
+                             and _os.environ.get("MXS_COPY_STREAM", "1") != "0" else None)
+        self._out_busy = None    # copy of out_* in flight (event)
+        self._rout_busy = None   # copy of the re-firing rows in flight (event)
+        self._rout = None        # re-firing output columns (keys, vals[, raw, cnt])
         if dev.type == "cuda":
             self._pool = PinnedSlabPool()
             self._pool.take(orows * 28 + 4 * 256)
@@ -1283,9 +1301,19 @@ class KeyedWindowOperator:
         p1 = p0 + self.panes_per_window - 1
         return not (p1 < self.min_live_pane or p0 > self.max_seen_pane)
 
+    def _claim(self, which: str = "_out_busy") -> None:
+        """Before a firing overwrites an output buffer: the current stream waits for the
+        side-stream copy still reading it."""
+        ev = getattr(self, which)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+            setattr(self, which, None)
+
     def _fire_window(self, s: int, only_dirty: bool) -> FireResult | None:
         # Only panes inside the live span exist in the ring; older/newer panes of the window
         # never held data and their ring slots belong to other panes (aliasing).
+        if self.device.type == "cuda":
+            self._claim()
         p0 = max(self.pane_of(s), self.min_live_pane)
         p1 = min(self.pane_of(s) + self.panes_per_window - 1, self.max_seen_pane)
         if p1 < p0:
@@ -1332,9 +1360,11 @@ class KeyedWindowOperator:
         n_dev = self.fire_bounds[k - 1:k] if bounds else self.out_n
         fixed = [self.flags, self.fire_bounds] if bounds else [self.flags]
         try:
-            rows = CountedHostRows(self._pool, self._fire_cols(kv), n_dev, fixed)
+            rows = CountedHostRows(self._pool, self._fire_cols(kv), n_dev, fixed,
+                                   copy_stream=self._copy_stream)
         except ValueError:
             return None
+        self._out_busy = rows.done
         return _PendingFire(rows, list(wins), kv, only_dirty, bounds)
 
     def _finish_pending(self, p: _PendingFire) -> list[FireResult]:
@@ -1561,12 +1591,14 @@ class KeyedWindowOperator:
             if p1 >= p0:
                 wins.append((s, (p0, p1 - p0 + 1, float(s), float(s + self.size))))
         stream = torch.cuda.current_stream(self.device).cuda_stream if cuda else 0
-        stage = self._fire_stage(kv) if cuda else None
         if cuda and only_dirty and self.dlist is not None and 1 < len(wins) <= 32 \
                 and _os.environ.get("MXS_FUSED_REFIRE", "1") != "0":
-            res = self._refire_fused(wins, kv, plan, stage, stream)
+            res = self._refire_fused(wins, kv, plan, stream)
             if res is not None:
                 return res
+        if cuda:
+            self._claim()
+        stage = self._fire_stage(kv) if cuda else None
         g = self._fire_group
         for i in range(0, len(wins), g):
             chunk = wins[i:i + g]
@@ -1601,35 +1633,52 @@ class KeyedWindowOperator:
                 lo = hi
         return out
 
-    def _refire_fused(self, wins: list, kv: bool, plan: dict, stage: tuple,
-                      stream: int) -> list | None:
+    def _refire_fused(self, wins: list, kv: bool, plan: dict, stream: int) -> list | None:
         """Every re-fired window of the step in ONE pass over the touched-slot list
         (gpu_window_refire_many: each listed slot's union of panes is loaded once), packed in
-        window order and copied with the device-counted kernel; one wait. The stage is split k
-        ways; a window that outgrows its share (more touched slots than nslots * group / k)
-        flags it and the group re-runs per window. None: not fusable here."""
+        window order into the re-firing's own output columns and copied on the side stream;
+        resolved later (no wait here). The touched-slot count is read first (one small wait on
+        the aggregation): each window's staging region is sized to it, so no window can
+        outgrow its region. None: not fusable here."""
         k = len(wins)
-        region = (self.out_keys.numel() // k) & ~3
-        if region < 4:
-            return None
+        n_list = int(self.dlist_n[0])  # host wait: the step's aggregation has run
+        if n_list == 0:
+            self.metrics.num_fires += k
+            return []
+        region = (n_list + 3) & ~3
+        rows_cap = k * region
+        self._claim("_rout_busy")  # the previous re-firing's copy reads the staging / columns
+        r = self._rout
+        if r is None or r[0].numel() < rows_cap or (r[2] is None) != kv:
+            cap = max(rows_cap, 1 << 16)
+            dev = self.device
+            r = self._rout = (torch.empty(cap, dtype=torch.int64, device=dev),
+                              torch.empty(cap, dtype=torch.float64, device=dev),
+                              None if kv else torch.empty(cap, dtype=torch.int64, device=dev),
+                              None if kv else torch.empty(cap, dtype=torch.int32, device=dev),
+                              torch.empty(cap, dtype=torch.int64, device=dev),
+                              torch.empty(cap, dtype=torch.float64, device=dev),
+                              None if kv else torch.empty(cap, dtype=torch.int64, device=dev),
+                              None if kv else torch.empty(cap, dtype=torch.int32, device=dev),
+                              torch.zeros(32, dtype=torch.int32, device=dev),
+                              torch.zeros(36, dtype=torch.int32, device=dev))
+        st_keys, st_vals, st_raw, st_cnt, o_keys, o_vals, o_raw, o_cnt, win_n, bnd = r
+        stage = (st_keys.data_ptr(), st_vals.data_ptr(), 0 if kv else st_raw.data_ptr(),
+                 0 if kv else st_cnt.data_ptr(), win_n.data_ptr(), region)
         self.flags[3:4].zero_()
         ok = self._m.gpu_window_refire_many(
             self.keys_g.data_ptr(), self.acc_g.data_ptr(), self.cnt_g.data_ptr(),
-            self.dirty_g.data_ptr(), plan, [w for _, w in wins], self.out_keys.data_ptr(),
-            self.out_vals.data_ptr(), 0 if kv else self.out_raw.data_ptr(),
-            0 if kv else self.out_cnt.data_ptr(), self.out_n.data_ptr(),
-            self.fire_bounds.data_ptr(), self.flags[3:4].data_ptr(), stream,
-            stage[:5] + (region,))
+            self.dirty_g.data_ptr(), plan, [w for _, w in wins], o_keys.data_ptr(),
+            o_vals.data_ptr(), 0 if kv else o_raw.data_ptr(), 0 if kv else o_cnt.data_ptr(),
+            bnd[32:33].data_ptr(), bnd.data_ptr(), self.flags[3:4].data_ptr(), stream, stage)
         if not ok:
             return None
-        rows = CountedHostRows(self._pool, self._fire_cols(kv), self.fire_bounds[k - 1:k],
-                               [self.flags, self.fire_bounds])
-        rows.wait()
-        if int(rows.fixed(0)[3]) & 16:
-            self.metrics.extra["refire_unfused"] = self.metrics.extra.get("refire_unfused", 0) + 1
-            return None
+        cols = [o_keys.view(torch.int32), o_vals] if kv else [o_keys, o_vals, o_raw, o_cnt]
+        rows = CountedHostRows(self._pool, [c[:rows_cap] for c in cols], bnd[k - 1:k],
+                               [self.flags, bnd], copy_stream=self._copy_stream)
+        self._rout_busy = rows.done
         self.metrics.num_fires += k
-        return self._finish_pending(_PendingFire(rows, [s for s, _ in wins], kv, True, True))
+        return [_PendingFire(rows, [s for s, _ in wins], kv, True, True)]
 
     def _fire_stage(self, kv: bool = False) -> tuple:
         """Per-window staging regions of the GPU batched firing (window_fire_many: window w of
