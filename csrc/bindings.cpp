@@ -461,7 +461,7 @@ PYBIND11_MODULE(_mxs_native, m) {
                                      std::vector<std::tuple<int64_t, int32_t, double, double>> wins,
                                      intptr_t ok, intptr_t ov, intptr_t oraw, intptr_t oc,
                                      intptr_t on, intptr_t bounds, intptr_t ovf, intptr_t stream,
-                                     py::object stage) {
+                                     py::object stage, int64_t dlo, uint32_t dmask) {
     const FirePlan base = make_fire(plan);
     std::vector<FireWin> w(wins.size());
     for (size_t i = 0; i < wins.size(); ++i)
@@ -474,8 +474,11 @@ PYBIND11_MODULE(_mxs_native, m) {
                                    P<uint8_t>(dirty_g), base, w.data(), (int)w.size(), st,
                                    P<uint64_t>(ok), P<double>(ov), P<uint64_t>(oraw),
                                    P<uint32_t>(oc), P<uint32_t>(on), P<uint32_t>(bounds),
-                                   P<uint32_t>(ovf), stream);
-  });
+                                   P<uint32_t>(ovf), stream, dlo, dmask);
+  }, py::arg("keys_g"), py::arg("acc_g"), py::arg("cnt_g"), py::arg("dirty_g"), py::arg("plan"),
+     py::arg("wins"), py::arg("ok"), py::arg("ov"), py::arg("oraw"), py::arg("oc"), py::arg("on"),
+     py::arg("bounds"), py::arg("ovf"), py::arg("stream"), py::arg("stage"), py::arg("dlo") = 0,
+     py::arg("dmask") = 0);
   m.def("gpu_rolling", [](intptr_t recs, intptr_t counts, py::dict plan, intptr_t keys_g,
                           intptr_t acc_g, intptr_t cnt_g, intptr_t occ, intptr_t flags,
                           intptr_t out_vals, intptr_t stream) {

@@ -1844,7 +1844,7 @@ constexpr int kRefireThreads = 256;
 __global__ __launch_bounds__(kRefireThreads) void window_refire_multi_kernel(
     const uint64_t* __restrict__ keys_g, const uint64_t* __restrict__ acc_g,
     const uint32_t* __restrict__ cnt_g, const uint8_t* __restrict__ dirty_g, FirePlan p,
-    FireWinPack pack, int64_t u0, int nu, FireStage st) {
+    FireWinPack pack, int64_t u0, int nu, uint32_t dmask, FireStage st) {
   extern __shared__ __attribute__((aligned(16))) double fsm[];
   constexpr int T = kRefireThreads;
   LdsCol vars{fsm + threadIdx.x, T};
@@ -1861,7 +1861,7 @@ __global__ __launch_bounds__(kRefireThreads) void window_refire_multi_kernel(
     const int64_t s = live ? (int64_t)p.list[v] : 0;
     uint32_t cg[kRefireP];
     uint64_t ag[kRefireP];
-    uint32_t dmask = 0;
+    uint32_t dirt = 0;
 #pragma unroll
     for (int q = 0; q < kRefireP; ++q)
       cg[q] = (live && q < nu) ? cnt_g[(size_t)((u0 + q) & (p.ring - 1)) * nslots + s] : 0u;
@@ -1869,7 +1869,9 @@ __global__ __launch_bounds__(kRefireThreads) void window_refire_multi_kernel(
     for (int q = 0; q < kRefireP; ++q) {
       const size_t gi = (size_t)((u0 + q) & (p.ring - 1)) * nslots + s;
       ag[q] = cg[q] ? acc_g[gi] : 0ull;
-      if (cg[q] && dirty_g[gi]) dmask |= 1u << q;
+      // dirty bytes only in the panes that received late data this step (dmask: every other
+      // pane's dirty bytes are clear -- dirty_clear ran after the previous re-firing)
+      if (cg[q] && (dmask >> q & 1u) && dirty_g[gi]) dirt |= 1u << q;
     }
     const uint64_t key = live ? keys_g[s] : 0ull;
     for (int w = 0; w < pack.n; ++w) {  // block-uniform: every lane reaches the barriers
@@ -1884,7 +1886,7 @@ __global__ __launch_bounds__(kRefireThreads) void window_refire_multi_kernel(
         acc = have ? agg_combine(p.agg, acc, ag[q]) : ag[q];
         have = true;
         cnt += cg[q];
-        dirty = dirty || (dmask >> q & 1u);
+        dirty = dirty || (dirt >> q & 1u);
       }
       bool emit = false;
       double val = 0.0;
@@ -4169,7 +4171,7 @@ bool window_refire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uin
                         const uint8_t* dirty_g, const FirePlan& base, const FireWin* wins, int k,
                         const FireStage& st, uint64_t* out_keys, double* out_vals,
                         uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n, uint32_t* bounds,
-                        uint32_t* ovf, intptr_t stream) {
+                        uint32_t* ovf, intptr_t stream, int64_t dlo, uint32_t dmask_abs) {
   if (k <= 0 || k > kFireMultiMax || !base.list || !base.list_n || base.nslots <= 0) return false;
   int64_t u0 = wins[0].p0, u1 = wins[0].p0 + wins[0].npanes;
   for (int i = 1; i < k; ++i) {
@@ -4177,6 +4179,12 @@ bool window_refire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uin
     u1 = wins[i].p0 + wins[i].npanes > u1 ? wins[i].p0 + wins[i].npanes : u1;
   }
   if (u1 - u0 > kRefireP || u1 - u0 > base.ring) return false;
+  // Panes that may hold dirty bytes (late data of this step), union-relative; 0 = unknown: all.
+  uint32_t dmask = 0;
+  for (int64_t q = 0; q < u1 - u0; ++q) {
+    const int64_t b = u0 + q - dlo;
+    if (!dmask_abs || (b >= 0 && b < 31 && (dmask_abs >> b & 1u))) dmask |= 1u << q;
+  }
   const int depth = base.map.depth > base.filt.depth ? base.map.depth : base.filt.depth;
   const size_t lds = (size_t)(kExprVars + depth) * kRefireThreads * sizeof(double) + 8 * 4;
   hipStream_t s = (hipStream_t)stream;
@@ -4188,7 +4196,7 @@ bool window_refire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uin
   // 256 slots per workgroup; workgroups past the list end exit at once.
   hipLaunchKernelGGL(window_refire_multi_kernel, dim3(grid_for(base.nslots, kRefireThreads * 4, 2048)),
                      dim3(kRefireThreads), lds, s, keys_g, acc_g, cnt_g, dirty_g, base, pack, u0,
-                     (int)(u1 - u0), st);
+                     (int)(u1 - u0), dmask, st);
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(fire_pack_kernel, dim3(grid_for(base.nslots / k, 256 * 4, 64), k), dim3(256),
                      0, s, st, k, base.key32, out_keys, out_vals, out_raw, out_cnt, bounds, out_n,

@@ -201,7 +201,7 @@ bool window_refire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uin
                         const uint8_t* dirty_g, const FirePlan& base, const FireWin* wins, int k,
                         const FireStage& st, uint64_t* out_keys, double* out_vals,
                         uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n, uint32_t* bounds,
-                        uint32_t* ovf, intptr_t stream);
+                        uint32_t* ovf, intptr_t stream, int64_t dlo = 0, uint32_t dmask_abs = 0);
 void window_fire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
                       const uint8_t* dirty_g, const FirePlan& base, const FireWin* wins, int k,
                       const FireStage& stage, uint64_t* out_keys, double* out_vals,

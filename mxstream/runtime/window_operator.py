@@ -1148,7 +1148,12 @@ class KeyedWindowOperator:
                                     cap_log2=self.cap_log2, where=f"after step {self.metrics.steps}")
                 # Late-but-allowed data: re-fire already-passed windows that are not cleaned yet.
                 if b.gmin <= b.fired_hi:
+                    # panes that can hold dirty bytes: this step's panes up to fired_hi
+                    fr = b.fired_hi - b.pane_base
+                    self._dirty_panes = ((b.pane_base, b.pmask & ((1 << (fr + 1)) - 1))
+                                         if b.pmask and 0 <= fr < 31 else (0, 0))
                     out.extend(self._refire(b.gmin, min(b.gmax, b.fired_hi), b.old_wm))
+                    self._dirty_panes = (0, 0)
             if b.new_wm is not None:
                 with self._stage("fire"):
                     out.extend(self._fire_ready(b.new_wm))
@@ -1602,7 +1607,9 @@ class KeyedWindowOperator:
         g = self._fire_group
         for i in range(0, len(wins), g):
             chunk = wins[i:i + g]
-            if not cuda:
+            if cuda:
+                self._claim()  # the previous chunk's copy may still read out_*
+            else:
                 self.out_n.zero_()
             self._m.window_fire_many(cuda, self.keys_g.data_ptr(), self.acc_g.data_ptr(),
                                      self.cnt_g.data_ptr(), self.dirty_g.data_ptr(), plan,
@@ -1670,7 +1677,8 @@ class KeyedWindowOperator:
             self.keys_g.data_ptr(), self.acc_g.data_ptr(), self.cnt_g.data_ptr(),
             self.dirty_g.data_ptr(), plan, [w for _, w in wins], o_keys.data_ptr(),
             o_vals.data_ptr(), 0 if kv else o_raw.data_ptr(), 0 if kv else o_cnt.data_ptr(),
-            bnd[32:33].data_ptr(), bnd.data_ptr(), self.flags[3:4].data_ptr(), stream, stage)
+            bnd[32:33].data_ptr(), bnd.data_ptr(), self.flags[3:4].data_ptr(), stream, stage,
+            *getattr(self, "_dirty_panes", (0, 0)))
         if not ok:
             return None
         cols = [o_keys.view(torch.int32), o_vals] if kv else [o_keys, o_vals, o_raw, o_cnt]
