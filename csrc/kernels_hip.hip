@@ -2342,32 +2342,52 @@ __global__ __launch_bounds__(256) void rolling_lookup_direct_kernel(
   }
 }
 
-__global__ __launch_bounds__(256) void rolling_heads_kernel(const int64_t* __restrict__ sk,
-                                                            const uint32_t* __restrict__ n_in,
-                                                            uint32_t* __restrict__ heads,
-                                                            uint32_t* __restrict__ n_heads,
-                                                            int shift) {
+// Segment starts of a (slot << shift)-sorted key array (first record of every slot), compacted.
+// A workgroup owns a chunk of kHeadsChunk records: it counts the chunk's heads, reserves their
+// run with ONE device-scope atomic (a same-address atomic per wave serialises across the 8 XCDs:
+// it made this kernel 3 ms at 16M records), then writes them through an LDS cursor. The list is
+// unordered across chunks; its consumers treat segments independently.
+constexpr uint32_t kHeadsChunk = 16384;
+
+__device__ __forceinline__ bool seg_head_at(const int64_t* __restrict__ sk, uint32_t i, uint32_t n,
+                                            int shift) {
+  if (i >= n) return false;
+  const int64_t k = sk[i];
+  return k != INT64_MAX && (i == 0 || (sk[i - 1] >> shift) != (k >> shift));
+}
+
+__global__ __launch_bounds__(256) void seg_heads_kernel(const int64_t* __restrict__ sk,
+                                                        const uint32_t* __restrict__ n_in,
+                                                        uint32_t* __restrict__ heads,
+                                                        uint32_t* __restrict__ n_heads, int shift) {
+  __shared__ uint32_t s_w[4], s_base, s_cur;
   const uint32_t n = *n_in;
-  // Four elements per thread per round, loads issued together (the kernel is load-latency bound).
-  constexpr int U = 4;
-  for (uint32_t base = blockIdx.x * blockDim.x * U; base < n; base += gridDim.x * blockDim.x * U) {
-    int64_t k[U], p[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t i = base + u * blockDim.x + threadIdx.x;
-      k[u] = i < n ? sk[i] : INT64_MAX;
-      p[u] = (i < n && i > 0) ? sk[i - 1] : 0;
+  const uint32_t lane = lane_id(), w = threadIdx.x >> 6;
+  for (uint32_t c0 = blockIdx.x * kHeadsChunk; c0 < n; c0 += gridDim.x * kHeadsChunk) {
+    const uint32_t c1 = c0 + kHeadsChunk < n ? c0 + kHeadsChunk : n;
+    uint32_t cnt = 0;
+    for (uint32_t i = c0 + threadIdx.x; i < c1; i += 256) cnt += seg_head_at(sk, i, n, shift);
+    for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d);
+    if (lane == 0) s_w[w] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t tot = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+      s_base = tot ? atomicAdd(n_heads, tot) : 0u;
+      s_cur = 0;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const uint32_t i = base + u * blockDim.x + threadIdx.x;
-      const bool h = i < n && k[u] != INT64_MAX && (i == 0 || (p[u] >> shift) != (k[u] >> shift));
+    __syncthreads();
+    for (uint32_t i0 = c0; i0 < c1; i0 += 256) {  // block-uniform trip count
+      const uint32_t i = i0 + threadIdx.x;
+      const bool h = i < c1 && seg_head_at(sk, i, n, shift);
       const unsigned long long m = __ballot(h);
-      uint32_t wb = 0;
-      if (lane_id() == 0 && m) wb = atomicAdd(n_heads, (uint32_t)__popcll(m));
-      wb = __shfl(wb, 0);
-      if (h) heads[wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = i;
+      if (m) {
+        uint32_t wb = 0;
+        if (lane == 0) wb = s_base + atomicAdd(&s_cur, (uint32_t)__popcll(m));
+        wb = __shfl(wb, 0);
+        if (h) heads[wb + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = i;
+      }
     }
+    __syncthreads();  // s_w / s_base / s_cur are reused by the next chunk
   }
 }
 
@@ -2694,7 +2714,7 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
     int64_t* __restrict__ sort_out, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
     Rec* __restrict__ host_recs, uint32_t* __restrict__ n_host, uint32_t host_cap,
     uint32_t* __restrict__ n_inserted, int tbits, uint32_t m_cap, const int64_t* __restrict__ skip,
-    uint32_t skip_mask) {
+    uint32_t skip_mask, uint64_t* __restrict__ heads_out, uint32_t* __restrict__ n_heads) {
   extern __shared__ __attribute__((aligned(16))) uint64_t slds[];
   // Launched before the host has read the step's partition flags: any flagged word of the
   // reduced vector (bucket overflow, unrepresentable span, reserved key) means the step is
@@ -2705,7 +2725,7 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
       if (skip_mask >> w & 1u) any |= skip[w];
     if (any) return;
   }
-  __shared__ uint32_t s_base, s_lins, s_kept, s_m;
+  __shared__ uint32_t s_base, s_lins, s_kept, s_m, s_hbase, s_hcnt;
   __shared__ uint32_t s_src_off[65];
   const int sub = blockIdx.x;
   const uint32_t cap = 1u << cap_log2, mask = cap - 1;
@@ -2785,26 +2805,37 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
   // Block-wide exclusive scan of cap (<= 4096) u16 counts: each thread sums a run of cap/T,
   // wave prefix with shuffles, wave totals through LDS.
   {
-    __shared__ uint32_t s_wave[kSessSortBlock / 64];
+    __shared__ uint32_t s_wave[kSessSortBlock / 64], s_nz[kSessSortBlock / 64];
     const uint32_t per = (cap + kSessSortBlock - 1) / kSessSortBlock;
     const uint32_t lo = threadIdx.x * per, hi = lo + per < cap ? lo + per : cap;
-    uint32_t run = 0;
-    for (uint32_t i = lo; i < hi; ++i) run += cur[i];
+    uint32_t run = 0, nz = 0;
+    for (uint32_t i = lo; i < hi; ++i) {
+      const uint32_t c = cur[i];
+      run += c;
+      nz += c != 0u;
+    }
     uint32_t incl = run;
     for (int d = 1; d < 64; d <<= 1) {
       const uint32_t y = __shfl_up(incl, d);
       if (lane_id() >= d) incl += y;
     }
+    for (int d = 32; d >= 1; d >>= 1) nz += __shfl_xor(nz, d);
     const int w = threadIdx.x >> 6;
     if (lane_id() == 63) s_wave[w] = incl;
+    if (lane_id() == 0) s_nz[w] = nz;
     __syncthreads();
     if (threadIdx.x == 0) {
-      uint32_t t = 0;
+      uint32_t t = 0, segs = 0;
       for (int i = 0; i < kSessSortBlock / 64; ++i) {
         const uint32_t c = s_wave[i];
         s_wave[i] = t;
         t += c;
+        segs += s_nz[i];
       }
+      // One device-scope atomic per workgroup reserves its segment-list run (a same-address
+      // atomic per wave serialises across the XCDs: 3x the kernel time at 16M records).
+      s_hbase = (heads_out && segs) ? atomicAdd(n_heads, segs) : 0u;
+      s_hcnt = 0;
     }
     __syncthreads();
     uint32_t o = s_wave[w] + incl - run;
@@ -2825,45 +2856,42 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
   }
   __syncthreads();
   // Phase 3: rank inside the slot segment [end(slot - 1), end(slot)) by (t, arrival index).
+  // The record ranked first in its segment also lists the segment (output position | length <<
+  // 32) for session_merge_heads: the merge then runs one lane per key instead of one per record.
   const uint64_t sub_slot0 = (uint64_t)sub << cap_log2;
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-    const uint64_t v = rk[i];
-    if (v == ~0ull) continue;
-    const uint32_t sl = (uint32_t)(v >> 32), t = (uint32_t)v;
-    const uint32_t end = cur[sl], start = sl ? cur[sl - 1] : 0u;
-    uint32_t rank = 0;
-    for (uint32_t q = start; q < end; ++q) {
-      const uint32_t j = idxl[q];
-      const uint32_t tj = (uint32_t)rk[j];
-      rank += (tj < t || (tj == t && j < i)) ? 1u : 0u;
+  for (uint32_t i0 = 0; i0 < m; i0 += blockDim.x) {  // block-uniform trip count (ballot below)
+    const uint32_t i = i0 + threadIdx.x;
+    const uint64_t v = i < m ? rk[i] : ~0ull;
+    bool head = false;
+    uint64_t hv = 0;
+    if (v != ~0ull) {
+      const uint32_t sl = (uint32_t)(v >> 32), t = (uint32_t)v;
+      const uint32_t end = cur[sl], start = sl ? cur[sl - 1] : 0u;
+      uint32_t rank = 0;
+      for (uint32_t q = start; q < end; ++q) {
+        const uint32_t j = idxl[q];
+        const uint32_t tj = (uint32_t)rk[j];
+        rank += (tj < t || (tj == t && j < i)) ? 1u : 0u;
+      }
+      // arrival index i -> (source bucket, position) for the value
+      int src = 0;
+      while (src + 1 < nsrc && i >= s_src_off[src + 1]) ++src;
+      const Rec& r = recs[(size_t)(src * nsub + sub) * bucket_cap + (i - s_src_off[src])];
+      const uint32_t out = s_base + start + rank;
+      sort_out[out] = (int64_t)(((sub_slot0 | sl) << tbits) | t);
+      vals_out[out] = r.val;
+      head = rank == 0;
+      hv = (uint64_t)(s_base + start) | ((uint64_t)(end - start) << 32);
     }
-    // arrival index i -> (source bucket, position) for the value
-    int src = 0;
-    while (src + 1 < nsrc && i >= s_src_off[src + 1]) ++src;
-    const Rec& r = recs[(size_t)(src * nsub + sub) * bucket_cap + (i - s_src_off[src])];
-    const uint32_t out = s_base + start + rank;
-    sort_out[out] = (int64_t)(((sub_slot0 | sl) << tbits) | t);
-    vals_out[out] = r.val;
-  }
-}
-
-__global__ __launch_bounds__(256) void session_heads_kernel(const int64_t* __restrict__ sk,
-                                                            const uint32_t* __restrict__ n_in,
-                                                            uint32_t* __restrict__ heads,
-                                                            uint32_t* __restrict__ n_heads) {
-  const uint32_t n = *n_in;
-  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
-    const uint32_t i = base + threadIdx.x;
-    bool h = false;
-    if (i < n) {
-      const int64_t k = sk[i];
-      h = k != INT64_MAX && (i == 0 || (sk[i - 1] >> 32) != (k >> 32));
+    if (heads_out) {
+      const unsigned long long hm = __ballot(head);
+      if (hm) {
+        uint32_t wb = 0;
+        if (lane_id() == 0) wb = s_hbase + atomicAdd(&s_hcnt, (uint32_t)__popcll(hm));
+        wb = __shfl(wb, 0);
+        if (head) heads_out[wb + (uint32_t)__popcll(hm & ((1ull << lane_id()) - 1ull))] = hv;
+      }
     }
-    const unsigned long long m = __ballot(h);
-    uint32_t wb = 0;
-    if (lane_id() == 0 && m) wb = atomicAdd(n_heads, (uint32_t)__popcll(m));
-    wb = __shfl(wb, 0);
-    if (h) heads[wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = i;
   }
 }
 
@@ -3030,6 +3058,42 @@ __device__ __forceinline__ void sess_finish(const SessState& st, int64_t slot, i
 
 constexpr uint32_t kSessLongSeg = 96;  // segments longer than this go to the wave kernel
 
+// One key's records [i, j) (ts order): runs split at gaps > gap, each run merged into the key's
+// sessions, state written back once.
+__device__ __forceinline__ void sess_merge_segment(const int64_t* __restrict__ sk,
+                                                   const uint64_t* __restrict__ vals, uint32_t i,
+                                                   uint32_t j, int64_t slot, const SessArgs& a,
+                                                   const SessOut& o) {
+  const int64_t tmask = ((int64_t)1 << a.tbits) - 1;
+  SessState st;
+  sess_load(st, o.sess + slot * kSess);
+  uint64_t late = 0;
+  bool overflow = false;
+  bool pv = false;
+  int64_t ps = 0, pe = 0;
+  uint64_t pa = 0;
+  uint32_t pc = 0;
+  int64_t ts = 0;
+  for (uint32_t r = i; r < j; ++r) {
+    ts = a.tbase + (sk[r] & tmask);
+    const uint64_t v = agg_lift(a.agg, vals[r]);
+    if (pv && ts <= pe) {
+      pe = ts + a.gap;
+      pa = agg_combine(a.agg, pa, v);
+      pc += 1;
+    } else {
+      if (pv) sess_commit(st, overflow, late, slot, ps, pe, pa, pc, a, o);
+      ps = ts;
+      pe = ts + a.gap;
+      pa = v;
+      pc = 1;
+      pv = true;
+    }
+  }
+  sess_commit(st, overflow, late, slot, ps, pe, pa, pc, a, o);
+  sess_finish(st, slot, ts, late, overflow, a, o);
+}
+
 // Thread per key segment (sorted by slot, then ts): the thread at a segment head walks its
 // records serially, splitting runs at ts gaps > gap. Typical session workloads have a few records
 // per key and step, where a wave per key would idle most lanes. Long segments are queued for
@@ -3039,7 +3103,6 @@ __global__ __launch_bounds__(256) void session_merge_small_kernel(
     const uint64_t* __restrict__ vals, const uint32_t* __restrict__ n_in, SessArgs a, SessOut o,
     uint32_t* __restrict__ long_heads, uint32_t* __restrict__ n_long) {
   const uint32_t n = *n_in;
-  const int64_t tmask = ((int64_t)1 << a.tbits) - 1;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int64_t k = sk[i];
     if (k == INT64_MAX) continue;
@@ -3055,33 +3118,25 @@ __global__ __launch_bounds__(256) void session_merge_small_kernel(
       long_heads[atomicAdd(n_long, 1u)] = i;
       continue;
     }
-    SessState st;
-    sess_load(st, o.sess + slot * kSess);
-    uint64_t late = 0;
-    bool overflow = false;
-    bool pv = false;
-    int64_t ps = 0, pe = 0;
-    uint64_t pa = 0;
-    uint32_t pc = 0;
-    int64_t ts = 0;
-    for (uint32_t r = i; r < j; ++r) {
-      ts = a.tbase + (sk[r] & tmask);
-      const uint64_t v = agg_lift(a.agg, vals[r]);
-      if (pv && ts <= pe) {
-        pe = ts + a.gap;
-        pa = agg_combine(a.agg, pa, v);
-        pc += 1;
-      } else {
-        if (pv) sess_commit(st, overflow, late, slot, ps, pe, pa, pc, a, o);
-        ps = ts;
-        pe = ts + a.gap;
-        pa = v;
-        pc = 1;
-        pv = true;
-      }
+    sess_merge_segment(sk, vals, i, j, slot, a, o);
+  }
+}
+
+// Dense variant over the segment list written by session_lookup_sort (position | length << 32):
+// every lane owns a key, none scans for segment heads.
+__global__ __launch_bounds__(256) void session_merge_heads_kernel(
+    const int64_t* __restrict__ sk, const uint64_t* __restrict__ vals,
+    const uint64_t* __restrict__ heads, const uint32_t* __restrict__ n_heads, SessArgs a,
+    SessOut o, uint32_t* __restrict__ long_heads, uint32_t* __restrict__ n_long) {
+  const uint32_t nh = *n_heads;
+  for (uint32_t h = blockIdx.x * blockDim.x + threadIdx.x; h < nh; h += gridDim.x * blockDim.x) {
+    const uint64_t hv = heads[h];
+    const uint32_t i = (uint32_t)hv, len = (uint32_t)(hv >> 32);
+    if (len > kSessLongSeg) {
+      long_heads[atomicAdd(n_long, 1u)] = i;
+      continue;
     }
-    sess_commit(st, overflow, late, slot, ps, pe, pa, pc, a, o);
-    sess_finish(st, slot, ts, late, overflow, a, o);
+    sess_merge_segment(sk, vals, i, i + len, sk[i] >> a.tbits, a, o);
   }
 }
 
@@ -4374,7 +4429,7 @@ void rolling_lookup_direct(const uint64_t* keys, const uint64_t* vals, uint32_t 
 
 void rolling_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
                    uint32_t* n_heads, int shift, intptr_t stream) {
-  hipLaunchKernelGGL(rolling_heads_kernel, dim3(grid_for((n_cap + 3) / 4, 256, 8192)), dim3(256), 0,
+  hipLaunchKernelGGL(seg_heads_kernel, dim3(grid_for((n_cap + 63) / 64, 256, 4096)), dim3(256), 0,
                      (hipStream_t)stream, sk, n_in, heads, n_heads, shift);
   HIP_CHECK(hipGetLastError());
 }
@@ -4461,7 +4516,7 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
                          uint32_t spill_mask, int spill_any, int64_t* sort_out, uint64_t* vals_out,
                          uint32_t* n_out, Rec* host_recs, uint32_t* n_host, uint32_t host_cap,
                          uint32_t* n_inserted, int tbits, intptr_t stream, const int64_t* skip,
-                         uint32_t skip_mask) {
+                         uint32_t skip_mask, uint64_t* heads_out, uint32_t* n_heads) {
   if (nsrc * nsub <= 0) return true;
   if (tbits < 1 || tbits > 32) throw std::invalid_argument("session_lookup_sort: tbits out of range");
   const uint64_t m64 = (uint64_t)nsrc * bcap;
@@ -4479,15 +4534,16 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
   hipLaunchKernelGGL(session_lookup_sort_kernel, dim3(nsub), dim3(kSessSortBlock), lds,
                      (hipStream_t)stream, recs, counts, nsrc, nsub, bcap, cap_log2, keys_g,
                      spill_set, spill_mask, spill_any, sort_out, vals_out, n_out, host_recs,
-                     n_host, host_cap, n_inserted, tbits, m_cap, skip, skip_mask);
+                     n_host, host_cap, n_inserted, tbits, m_cap, skip, skip_mask, heads_out,
+                     n_heads);
   HIP_CHECK(hipGetLastError());
   return true;
 }
 
 void session_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
                    uint32_t* n_heads, intptr_t stream) {
-  hipLaunchKernelGGL(session_heads_kernel, dim3(grid_for(n_cap, 256, 8192)), dim3(256), 0,
-                     (hipStream_t)stream, sk, n_in, heads, n_heads);
+  hipLaunchKernelGGL(seg_heads_kernel, dim3(grid_for((n_cap + 63) / 64, 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, sk, n_in, heads, n_heads, 32);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -4504,6 +4560,24 @@ void session_merge(const int64_t* sk, const uint64_t* vals, const uint32_t* n_in
                      (hipStream_t)stream, sk, vals, n_in, a, o, long_heads, n_long);
   HIP_CHECK(hipGetLastError());
   // Long segments (hot keys): a wave each; the count stays on the device (grid-stride waves).
+  hipLaunchKernelGGL(session_merge_long_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, sk,
+                     vals, n_in, long_heads, n_long, a, o);
+  HIP_CHECK(hipGetLastError());
+}
+
+void session_merge_heads(const int64_t* sk, const uint64_t* vals, const uint32_t* n_in,
+                         const uint64_t* heads, const uint32_t* n_heads, int64_t head_cap,
+                         uint32_t* long_heads, uint32_t* n_long, int tbits, int64_t gap,
+                         int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
+                         int64_t nslots, int64_t* sess, int64_t* slot_due, int64_t* slot_last,
+                         uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf, int64_t* ovf_rows,
+                         uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream) {
+  const SessArgs a = make_sess_args(gap, lateness, wm, tbase, agg, cap_log2, nslots, tbits);
+  const SessOut o{reinterpret_cast<SessRec*>(sess), slot_due, slot_last, late_cnt,
+                  ovf_slots, n_ovf, ovf_rows, n_ovf_runs, ovf_cap};
+  hipLaunchKernelGGL(session_merge_heads_kernel, dim3(grid_for(head_cap, 256, 16384)), dim3(256),
+                     0, (hipStream_t)stream, sk, vals, heads, n_heads, a, o, long_heads, n_long);
+  HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(session_merge_long_kernel, dim3(512), dim3(256), 0, (hipStream_t)stream, sk,
                      vals, n_in, long_heads, n_long, a, o);
   HIP_CHECK(hipGetLastError());

@@ -135,7 +135,7 @@ def config2(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000,
     dt = time.perf_counter() - t0
     return {"config": 2, "keyed_state": "dense" if dense_keys else "hashed",
             "path": "sort-free" if sort_free else "radix-sort",
-            "metric": "events/sec (keyed ValueState counter, 10k keys)",
+            "metric": f"events/sec (keyed ValueState counter, {keys // 1000}k keys)",
             "value": batch * steps / dt, "unit": "events/s", "ms_per_step": dt / steps * 1e3,
             "alerts": alerts, "keys": keys, "events_per_step": batch, "device": str(dev)}
 
@@ -568,6 +568,7 @@ def main(argv=None) -> int:
                     help="configs 2/4: hashed keyed state instead of dictionary-id slots")
     ap.add_argument("--sort-path", action="store_true",
                     help="config 2: the radix-sort rolling path instead of the sort-free one")
+    ap.add_argument("--keys", type=int, default=None, help="config 2: key space (default 10k)")
     ap.add_argument("--threads", type=int, default=4,
                     help="config 1 CPU path: parse threads (the reference job runs at P = 4)")
     a = ap.parse_args(argv)
@@ -577,7 +578,8 @@ def main(argv=None) -> int:
                     threads=a.threads)
     elif a.config == 2:
         r = config2(a.steps, a.warmup, a.batch or (1 << 24), device=a.device,
-                    dense_keys=not a.hashed_keys, sort_free=not a.sort_path)
+                    keys=a.keys or 10_000, dense_keys=not a.hashed_keys,
+                    sort_free=not a.sort_path)
     elif a.config == 4 and a.spill:
         r = config4_spill(a.steps, a.warmup, a.batch or (1 << 22), device=a.device)
     elif a.config == 4:

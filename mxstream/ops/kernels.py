@@ -461,7 +461,7 @@ def table_insert(keys: torch.Tensor, keys_g: torch.Tensor, *, nsub_log2: int,
 
 def sort_pairs(keys: torch.Tensor, vals: torch.Tensor, *, bits: int = 64):
     """Stable ascending sort of (uint64 key bits, int64 value) pairs over the low `bits` key bits.
-    GPU: rocPRIM onesweep radix sort (csrc/sort_hip.hip); CPU: torch stable sort."""
+    GPU: the hand-written LSD radix sort (csrc/sort_hip.hip); CPU: torch stable sort."""
     n = keys.numel()
     dev = keys.device
     _check(keys, torch.int64, n, "keys", dev)

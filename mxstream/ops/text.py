@@ -70,8 +70,18 @@ def parse_text_gpu(data, spec: list[tuple[int, int]], sep: str = " ", offset_s: 
             1, dtype=torch.uint8, device=dev)
         host = None
     # Line starts (0 and every byte after a newline, below n_bytes: a trailing newline starts no
-    # line) by the order-preserving ballot/scan/write kernels; one host sync for the count.
-    starts_buf = torch.empty(max(n_bytes, 1), dtype=torch.int64, device=dev)
+    # line) by the order-preserving ballot/scan/write kernels; one host sync for the count. The
+    # index array is sized by the line count when the host holds the text (a device-only batch
+    # falls back to the byte count, the only bound known without reading it).
+    from .ingest import count_lines
+
+    if host is not None and host.device.type == "cpu":
+        bound = count_lines(host) + 1
+    elif host is None:
+        bound = count_lines(data) + 1
+    else:
+        bound = n_bytes
+    starts_buf = torch.empty(max(min(bound + 64, n_bytes), 1), dtype=torch.int64, device=dev)
     total = torch.zeros(1, dtype=torch.int64, device=dev)
     scratch = torch.empty(max(1, m.gpu_filter_compact_scratch_bytes(n_bytes)), dtype=torch.uint8,
                           device=dev)

@@ -232,6 +232,8 @@ class KeyedSessionOperator:
             self.vals_out = torch.empty(total, dtype=torch.int64, device=dev)
             self._sort_tmp = None
             self.heads = torch.empty(total, dtype=torch.int32, device=dev)
+            # key segments of the fused lookup-sort (output position | length << 32)
+            self.seg_heads = torch.empty(total, dtype=torch.int64, device=dev)
             self.host_cap = total
             self.host_recs = torch.empty(total * K.REC_WORDS, dtype=torch.int64, device=dev)
             # The merge folds runs into the state as it goes (no redo), so the overflow-run buffer
@@ -501,8 +503,10 @@ class KeyedSessionOperator:
         the LDS path does not apply (nothing launched)."""
         m, st, c = self.native, self._st(), self.ctr
         c[:7].zero_()
+        c[10:11].zero_()
         self.late_cnt.zero_()
-        if _SESSION_SORT != "lds" or nsrc * self.nsub * bucket_cap > self.sort_out.numel():
+        n_cap = nsrc * self.nsub * bucket_cap
+        if _SESSION_SORT != "lds" or n_cap > self.sort_out.numel():
             return False
         if not m.gpu_session_lookup_sort(
                 recs.data_ptr(), counts.data_ptr(), nsrc, self.nsub, bucket_cap,
@@ -511,17 +515,19 @@ class KeyedSessionOperator:
                 self.vals_out.data_ptr(), c[0:1].data_ptr(), self.host_recs.data_ptr(),
                 c[2:3].data_ptr(), self.host_cap, c[3:4].data_ptr(), tbits, st,
                 skip.data_ptr() if skip is not None else 0,
-                self._SKIP_MASK if skip is not None else 0):
+                self._SKIP_MASK if skip is not None else 0,
+                self.seg_heads.data_ptr(), c[10:11].data_ptr()):
             return False
-        m.gpu_session_merge(self.sort_out.data_ptr(), self.vals_out.data_ptr(),
-                            c[0:1].data_ptr(), self.heads.data_ptr(), c[1:2].data_ptr(),
-                            nsrc * self.nsub * bucket_cap, tbits, self.gap, self.lateness,
-                            wm, tbase,
-                            self.agg, self.cap_log2, self.nslots, self.sess.data_ptr(),
-                            self.slot_due.data_ptr(), self.slot_last.data_ptr(),
-                            self.late_cnt.data_ptr(), self.ovf_slots.data_ptr(),
-                            c[4:5].data_ptr(), self.ovf_rows.data_ptr(), c[5:6].data_ptr(),
-                            self.ovf_cap, st)
+        # One lane per key segment listed by the lookup-sort (c[10] segments on the device).
+        m.gpu_session_merge_heads(self.sort_out.data_ptr(), self.vals_out.data_ptr(),
+                                  c[0:1].data_ptr(), self.seg_heads.data_ptr(),
+                                  c[10:11].data_ptr(), min(n_cap, self.nslots),
+                                  self.heads.data_ptr(), c[1:2].data_ptr(), tbits, self.gap,
+                                  self.lateness, wm, tbase, self.agg, self.cap_log2, self.nslots,
+                                  self.sess.data_ptr(), self.slot_due.data_ptr(),
+                                  self.slot_last.data_ptr(), self.late_cnt.data_ptr(),
+                                  self.ovf_slots.data_ptr(), c[4:5].data_ptr(),
+                                  self.ovf_rows.data_ptr(), c[5:6].data_ptr(), self.ovf_cap, st)
         return True
 
     def _fold_counters(self, with_red: bool = False) -> list[int]:
