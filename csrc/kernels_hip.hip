@@ -2706,6 +2706,7 @@ __global__ __launch_bounds__(kSessLookupBlock) void session_lookup_lds_kernel(
 // The output equals a stable sort of session_lookup's keys with the holes removed, so
 // session_merge runs on it unchanged. LDS: max(cap*8, cap*2 + m*2) + m*8 bytes for m records.
 constexpr int kSessSortBlock = 1024;
+constexpr int kLsRegs = 16;  // record values kept in registers per thread (m <= 16K: all of them)
 
 __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
     const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
@@ -2754,35 +2755,46 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
   __syncthreads();
   const uint32_t m = s_m;  // the launcher sized m_cap >= nsrc * bucket_cap >= m
   // Phase 1: lookup / insert / divert; rk[i] = (local slot << 32 | t) or ~0 (not folded here).
+  // Records are visited by arrival index i = k * blockDim + tid, the same thread-to-record map as
+  // phase 3, so each thread keeps the values of its first kLsRegs records in registers and phase
+  // 3 writes them without re-reading the bucket (an uncoalesced gather).
   uint32_t kept = 0;
-  for (int src = 0; src < nsrc; ++src) {
-    const int b = src * nsub + sub;
-    const uint32_t c = s_src_off[src + 1] - s_src_off[src];
-    const Rec* seg = recs + (size_t)b * bucket_cap;
-    for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
-      const Rec r = seg[e];
-      uint64_t v = ~0ull;
-      if (r.t != 0xFFFFFFFFu) {
-        uint32_t sl = sess_find<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask);
-        bool to_host = sl == kNoSlot && spill_any && set_contains(spill_set, spill_mask, r.key);
-        if (!to_host && sl == kNoSlot) {
-          sl = sess_probe_insert<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask, &s_lins);
-          if (sl == kNoSlot) {  // sub-table full: the key lives in host DRAM from now on
-            to_host = true;
-            set_insert(spill_set, spill_mask, r.key);
-          }
-        }
-        if (to_host) {
-          const uint32_t q = atomicAdd(n_host, 1u);
-          if (q < host_cap) host_recs[q] = r;
-        } else {
-          v = ((uint64_t)sl << 32) | r.t;
-          ++kept;
+  auto rec_at = [&](uint32_t i) -> const Rec& {
+    int src = 0;
+    while (src + 1 < nsrc && i >= s_src_off[src + 1]) ++src;
+    return recs[(size_t)(src * nsub + sub) * bucket_cap + (i - s_src_off[src])];
+  };
+  auto lookup = [&](uint32_t i) -> uint64_t {
+    const Rec r = rec_at(i);
+    uint64_t v = ~0ull;
+    if (r.t != 0xFFFFFFFFu) {
+      uint32_t sl = sess_find<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask);
+      bool to_host = sl == kNoSlot && spill_any && set_contains(spill_set, spill_mask, r.key);
+      if (!to_host && sl == kNoSlot) {
+        sl = sess_probe_insert<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask, &s_lins);
+        if (sl == kNoSlot) {  // sub-table full: the key lives in host DRAM from now on
+          to_host = true;
+          set_insert(spill_set, spill_mask, r.key);
         }
       }
-      rk[s_src_off[src] + e] = v;
+      if (to_host) {
+        const uint32_t q = atomicAdd(n_host, 1u);
+        if (q < host_cap) host_recs[q] = r;
+      } else {
+        v = ((uint64_t)sl << 32) | r.t;
+        ++kept;
+      }
     }
+    rk[i] = v;
+    return r.val;
+  };
+  uint64_t vreg[kLsRegs];
+#pragma unroll
+  for (int k = 0; k < kLsRegs; ++k) {
+    const uint32_t i = k * kSessSortBlock + threadIdx.x;
+    vreg[k] = i < m ? lookup(i) : 0ull;
   }
+  for (uint32_t i = kLsRegs * kSessSortBlock + threadIdx.x; i < m; i += kSessSortBlock) lookup(i);
   if (kept) atomicAdd(&s_kept, kept);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) gkeys[i] = lkeys[i];
@@ -2859,30 +2871,32 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
   // The record ranked first in its segment also lists the segment (output position | length <<
   // 32) for session_merge_heads: the merge then runs one lane per key instead of one per record.
   const uint64_t sub_slot0 = (uint64_t)sub << cap_log2;
-  for (uint32_t i0 = 0; i0 < m; i0 += blockDim.x) {  // block-uniform trip count (ballot below)
+  auto place = [&](uint32_t i, uint64_t v, uint64_t val, bool& head, uint64_t& hv) {
+    const uint32_t sl = (uint32_t)(v >> 32), t = (uint32_t)v;
+    const uint32_t end = cur[sl], start = sl ? cur[sl - 1] : 0u;
+    uint32_t rank = 0;
+    for (uint32_t q = start; q < end; ++q) {
+      const uint32_t j = idxl[q];
+      const uint32_t tj = (uint32_t)rk[j];
+      rank += (tj < t || (tj == t && j < i)) ? 1u : 0u;
+    }
+    const uint32_t out = s_base + start + rank;
+    sort_out[out] = (int64_t)(((sub_slot0 | sl) << tbits) | t);
+    vals_out[out] = val;
+    head = rank == 0;
+    hv = (uint64_t)(s_base + start) | ((uint64_t)(end - start) << 32);
+  };
+#pragma unroll
+  for (int k = 0; k < kLsRegs + 1; ++k) {
+   // k < kLsRegs: the record's value is in vreg[k]; k == kLsRegs: every remaining record (values
+   // re-read from the bucket)
+   for (uint32_t i0 = k * kSessSortBlock; i0 < (k < kLsRegs ? (k + 1) * kSessSortBlock : m) &&
+                                          i0 < m; i0 += kSessSortBlock) {  // block-uniform
     const uint32_t i = i0 + threadIdx.x;
     const uint64_t v = i < m ? rk[i] : ~0ull;
     bool head = false;
     uint64_t hv = 0;
-    if (v != ~0ull) {
-      const uint32_t sl = (uint32_t)(v >> 32), t = (uint32_t)v;
-      const uint32_t end = cur[sl], start = sl ? cur[sl - 1] : 0u;
-      uint32_t rank = 0;
-      for (uint32_t q = start; q < end; ++q) {
-        const uint32_t j = idxl[q];
-        const uint32_t tj = (uint32_t)rk[j];
-        rank += (tj < t || (tj == t && j < i)) ? 1u : 0u;
-      }
-      // arrival index i -> (source bucket, position) for the value
-      int src = 0;
-      while (src + 1 < nsrc && i >= s_src_off[src + 1]) ++src;
-      const Rec& r = recs[(size_t)(src * nsub + sub) * bucket_cap + (i - s_src_off[src])];
-      const uint32_t out = s_base + start + rank;
-      sort_out[out] = (int64_t)(((sub_slot0 | sl) << tbits) | t);
-      vals_out[out] = r.val;
-      head = rank == 0;
-      hv = (uint64_t)(s_base + start) | ((uint64_t)(end - start) << 32);
-    }
+    if (v != ~0ull) place(i, v, k < kLsRegs ? vreg[k] : rec_at(i).val, head, hv);
     if (heads_out) {
       const unsigned long long hm = __ballot(head);
       if (hm) {
@@ -2892,6 +2906,7 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
         if (head) heads_out[wb + (uint32_t)__popcll(hm & ((1ull << lane_id()) - 1ull))] = hv;
       }
     }
+   }
   }
 }
 

@@ -47,13 +47,40 @@ struct ColdChunk {
   }
   void ensure_index() {
     if (by_key.size() == key.size()) return;
+    const size_t n = key.size();
+    const uint64_t span = n ? kmax - kmin : 0;
+    if (n && span < ((uint64_t)1 << 32)) {
+      // Keys within 2^32 of each other (dictionary ids, drifting id ranges): stable LSD radix
+      // sort of the row ids by (key - kmin), 11-bit digits over the span's bits -- O(n) per
+      // pass instead of an O(n log n) comparison sort (the chunks hold 10^5-10^6 rows).
+      int bits = 0;
+      while (bits < 64 && (span >> bits)) ++bits;
+      std::vector<uint32_t> a(n), b(n);
+      std::vector<uint32_t> off((size_t)1 << 11);
+      for (size_t i = 0; i < n; ++i) a[i] = (uint32_t)i;
+      for (int sh = 0; sh < bits || sh == 0; sh += 11) {
+        std::fill(off.begin(), off.end(), 0u);
+        for (size_t i = 0; i < n; ++i) ++off[((key[a[i]] - kmin) >> sh) & 2047u];
+        uint32_t t = 0;
+        for (auto& c : off) {
+          const uint32_t x = c;
+          c = t;
+          t += x;
+        }
+        for (size_t i = 0; i < n; ++i) b[off[((key[a[i]] - kmin) >> sh) & 2047u]++] = a[i];
+        a.swap(b);
+        if (bits == 0) break;
+      }
+      by_key.swap(a);
+      return;
+    }
     // (key, row) pairs sorted contiguously: an index sort with key[] lookups in the comparator
     // was 5x slower (random reads).
-    std::vector<std::pair<uint64_t, uint32_t>> kr(key.size());
-    for (size_t i = 0; i < kr.size(); ++i) kr[i] = {key[i], (uint32_t)i};
+    std::vector<std::pair<uint64_t, uint32_t>> kr(n);
+    for (size_t i = 0; i < n; ++i) kr[i] = {key[i], (uint32_t)i};
     std::sort(kr.begin(), kr.end());
-    by_key.resize(kr.size());
-    for (size_t i = 0; i < kr.size(); ++i) by_key[i] = kr[i].second;
+    by_key.resize(n);
+    for (size_t i = 0; i < n; ++i) by_key[i] = kr[i].second;
   }
 };
 
@@ -332,8 +359,12 @@ class SessionCore {
     // Cold chunks: dropped as a whole once every row is past cleanup.
     for (auto it = cold_.begin(); it != cold_.end();) {
       if (it->max_due <= wm) {
+        // (a key whose cold row expires leaves unless it also has hot sessions; with no hot keys
+        // -- the common case, hot state is overflow only -- no per-row map probe)
+        released.reserve(released.size() + it->key.size());
+        const bool no_hot = m_.empty();
         for (size_t r = 0; r < it->key.size(); ++r)
-          if (it->cnt[r] && m_.find(it->key[r]) == m_.end())
+          if (it->cnt[r] && (no_hot || m_.find(it->key[r]) == m_.end()))
             released.push_back((int64_t)it->key[r]);
         cold_rows_ -= it->live;
         if (spare_.size() < 4) {  // keep the columns' memory for the next eviction's chunk

@@ -360,13 +360,20 @@ class KeyedSessionOperator:
         if wm == I64_MIN:
             return SessionRows.concat([])
         parts = []
+        pending = None
         if self.gpu:
+            # The GPU firing is launched first; the host store fires while it runs and its rows
+            # come back.
             with self._phase("fire_gpu"):
-                parts.append(self._fire_gpu(wm))
+                pending = self._fire_gpu_launch(wm)
         with self._phase("fire_host"):
             if self.gpu:
                 self._join_spill()
-            parts.append(self._fire_host(wm))
+            host_rows = self._fire_host(wm)
+        if pending is not None:
+            with self._phase("fire_gpu"):
+                parts.append(self._fire_gpu_collect(pending))
+        parts.append(host_rows)
         out = SessionRows.concat(parts)
         self.metrics.num_records_out += len(out)
         if self.gpu:
@@ -439,7 +446,10 @@ class KeyedSessionOperator:
         of records diverted to spilled keys."""
         if h[2] > self.host_cap:
             raise RuntimeError("host diversion buffer overflow")
-        self._join_spill()  # the host store must hold last step's spilled rows
+        if h[2] or h[4]:
+            # Diverted records / overflow runs go to the host store, which must hold last step's
+            # spilled rows; otherwise the spill worker keeps running until the host fire needs it.
+            self._join_spill()
         late = h[6] if total else 0
         n_host = h[2]
         # Overflow runs first: the refold below reuses the overflow buffers.
@@ -656,6 +666,9 @@ class KeyedSessionOperator:
                                          rows[4].copy(), wm))
 
     def _fire_gpu(self, wm: int) -> SessionRows:
+        return self._fire_gpu_collect(self._fire_gpu_launch(wm))
+
+    def _fire_gpu_launch(self, wm: int):
         m, st, c = self.native, self._st(), self.ctr
         mc, mk = self.map_prog.as_args()
         fc, fk = self.filter_prog.as_args()
@@ -670,7 +683,10 @@ class KeyedSessionOperator:
         ka = self._fire_rows_async
         cols = [t[:ka] for t in (self.out_key, self.out_start, self.out_end, self.out_val,
                                  self.out_raw, self.out_cnt)]
-        rows = CountedHostRows(self._pool, cols, c[6:7], [c])
+        return CountedHostRows(self._pool, cols, c[6:7], [c])
+
+    def _fire_gpu_collect(self, rows) -> SessionRows:
+        ka = self._fire_rows_async
         rows.wait()
         k = int(rows.fixed(0)[6])
         if k > self.ocap:

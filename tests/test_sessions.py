@@ -175,6 +175,42 @@ def test_store_cold_tier_promotion_equals_hot():
     assert cold.num_keys() == 0 and hot.num_keys() == 0
 
 
+@pytest.mark.parametrize("spread", ["dense", "sparse"])
+def test_store_cold_index_lookup_equals_hot(spread):
+    """Few revisited keys in a large cold chunk take the chunk's sorted row index (radix-sorted
+    for keys within 2^32 of each other, a comparison sort otherwise): same results as a store
+    that holds the same sessions hot."""
+    from mxstream.ops.native import load
+
+    m = load()
+    rng = np.random.default_rng(11)
+    nk = 20_000
+    if spread == "dense":
+        k = np.arange(5_000_000, 5_000_000 + nk, dtype=np.int64)
+    else:
+        k = np.unique(rng.integers(-(1 << 62), 1 << 62, nk)).astype(np.int64)
+    rng.shuffle(k)  # eviction order is slot order, not key order
+    s = (np.abs(k) % 4000).astype(np.int64)
+    e = s + 100
+    ones = np.ones_like(k)
+    hot = m.SessionStore(100, 1000, K.AGG_SUM_I64)
+    cold = m.SessionStore(100, 1000, K.AGG_SUM_I64)
+    hot.insert(k, s, e, k % 97, ones, ones, False)
+    cold.insert(k, s, e, k % 97, ones, ones, True)
+    pick = rng.choice(k, 300, replace=False)
+    ts = (np.abs(pick) % 4000) + 50  # inside the stored session: merges into it
+    outs = []
+    for st_ in (hot, cold):
+        st_.fire(3000, [], [], [], [])
+        late = st_.process(pick.astype(np.int64), ts.astype(np.int64), np.full(300, 5, np.int64),
+                           3000)
+        d = st_.fire((1 << 63) - 1, [], [], [], [])
+        outs.append((late, sorted(zip(d["keys"].tolist(), d["start"].tolist(),
+                                      d["raw"].tolist(), d["counts"].tolist()))))
+    assert outs[0] == outs[1]
+    assert cold.num_keys() == 0
+
+
 # ----------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
 @settings(max_examples=15, deadline=None, suppress_health_check=[HealthCheck.too_slow])
