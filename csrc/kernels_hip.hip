@@ -1450,15 +1450,25 @@ __global__ __launch_bounds__(1024) void window_compact_kernel(
     snew[i] = kEmptyKey;
     sfrom[i] = kNoSlot;
   }
-  if (threadIdx.x < 4) sc[threadIdx.x] = 0;
+  if (threadIdx.x < 6) sc[threadIdx.x] = 0;
+  __syncthreads();
+  // Evicted keys' rows: counted and placed inside the block first (LDS cursor sc[4], the slot's
+  // run start + 1 kept in scnt[s], which the permutation below overwrites), then ONE device-scope
+  // atomic reserves the block's run in the output (a same-address atomic per row serialises
+  // across the XCDs).
+  for (uint32_t s = threadIdx.x; s < cap; s += blockDim.x) scnt[s] = 0;
   __syncthreads();
   for (uint32_t s = threadIdx.x; s < cap; s += blockDim.x) {
     const uint64_t k = sold[s];
     if (k == kEmptyKey || k == kTombKey) continue;
     int64_t newest = INT64_MIN;
+    uint32_t nrows = 0;
     for (int j = 0; j < np; ++j) {
       const int64_t p = p_lo + j;
-      if (cnt_g[(size_t)(p & (ring - 1)) * nslots + sbase + s]) newest = p;
+      if (cnt_g[(size_t)(p & (ring - 1)) * nslots + sbase + s]) {
+        newest = p;
+        ++nrows;
+      }
     }
     if (newest == INT64_MIN) {
       atomicAdd(&sc[0], 1u);
@@ -1466,22 +1476,7 @@ __global__ __launch_bounds__(1024) void window_compact_kernel(
     }
     if (newest <= cutoff) {
       atomicAdd(&sc[1], 1u);
-      for (int j = 0; j < np; ++j) {
-        const int64_t p = p_lo + j;
-        const size_t gi = (size_t)(p & (ring - 1)) * nslots + sbase + s;
-        const uint32_t c = cnt_g[gi];
-        if (!c) continue;
-        const uint32_t q = atomicAdd(out.n, 1u);
-        if (q < out.cap) {
-          out.key[q] = k;
-          out.pane[q] = p;
-          out.acc[q] = acc_g[gi];
-          out.cnt[q] = c;
-          out.dirty[q] = dirty_g[gi];
-        } else {
-          atomicOr(&sc[2], 1u);
-        }
-      }
+      scnt[s] = atomicAdd(&sc[4], nrows) + 1u;
       continue;
     }
     int ins = 0;
@@ -1492,6 +1487,31 @@ __global__ __launch_bounds__(1024) void window_compact_kernel(
     }
     sfrom[t] = s;
     atomicAdd(&sc[3], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) sc[5] = sc[4] ? atomicAdd(out.n, sc[4]) : 0u;
+  __syncthreads();
+  for (uint32_t s = threadIdx.x; s < cap; s += blockDim.x) {
+    const uint32_t o1 = scnt[s];
+    if (!o1) continue;
+    const uint64_t k = sold[s];
+    uint32_t q = sc[5] + o1 - 1;
+    for (int j = 0; j < np; ++j) {
+      const int64_t p = p_lo + j;
+      const size_t gi = (size_t)(p & (ring - 1)) * nslots + sbase + s;
+      const uint32_t c = cnt_g[gi];
+      if (!c) continue;
+      if (q < out.cap) {
+        out.key[q] = k;
+        out.pane[q] = p;
+        out.acc[q] = acc_g[gi];
+        out.cnt[q] = c;
+        out.dirty[q] = dirty_g[gi];
+      } else {
+        atomicOr(&sc[2], 1u);
+      }
+      ++q;
+    }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) keys_g[sbase + i] = snew[i];
@@ -4292,7 +4312,7 @@ void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t*
   if (cap_log2 > 12 || np > ring || np < 0)
     throw std::invalid_argument("window_compact: sub-table > 4096 slots or bad pane range");
   const size_t cap = (size_t)1 << cap_log2;
-  const size_t lds = cap * (8 * 3 + 4 * 2 + 1) + 16;
+  const size_t lds = cap * (8 * 3 + 4 * 2 + 1) + 32;
   static bool attr = false;
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)window_compact_kernel,
