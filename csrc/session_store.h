@@ -212,9 +212,37 @@ class SessionCore {
   // than an HBM slot holds stay here.
   Columns extract(const int64_t* keys, int64_t n, int64_t wm, int64_t max_sess,
                   std::vector<int64_t>* moved) {
-    std::vector<uint64_t> want((const uint64_t*)keys, (const uint64_t*)keys + n);
-    std::sort(want.begin(), want.end());
-    want.erase(std::unique(want.begin(), want.end()), want.end());
+    // Dense key spans (dictionary ids, drifting id ranges -- every keyed state here is fed by
+    // those): the wanted set is a bitmap over [wmin, wmax] and cold rows are grouped by a
+    // counting sort on the key offset, O(n + span) instead of sorts and hash probes.
+    uint64_t wmin = ~0ull, wmax = 0;
+    for (int64_t i = 0; i < n; ++i) {
+      const uint64_t k = (uint64_t)keys[i];
+      wmin = k < wmin ? k : wmin;
+      wmax = k > wmax ? k : wmax;
+    }
+    const uint64_t wspan = n ? wmax - wmin + 1 : 0;
+    const bool dense = n && wspan <= (uint64_t)16 * n + 65536 && wspan <= ((uint64_t)1 << 27);
+    std::vector<uint64_t> want;
+    std::vector<uint64_t> wbits;  // dense: bit (key - wmin) set for wanted keys
+    if (dense) {
+      wbits.assign((wspan + 63) / 64, 0);
+      for (int64_t i = 0; i < n; ++i) {
+        const uint64_t o = (uint64_t)keys[i] - wmin;
+        wbits[o >> 6] |= 1ull << (o & 63);
+      }
+      for (size_t w = 0; w < wbits.size(); ++w)
+        for (uint64_t b = wbits[w]; b; b &= b - 1)
+          want.push_back(wmin + (w << 6) + (uint64_t)__builtin_ctzll(b));
+    } else {
+      want.assign((const uint64_t*)keys, (const uint64_t*)keys + n);
+      std::sort(want.begin(), want.end());
+      want.erase(std::unique(want.begin(), want.end()), want.end());
+    }
+    auto wanted_dense = [&](uint64_t k) {
+      const uint64_t o = k - wmin;
+      return k >= wmin && o < wspan && ((wbits[o >> 6] >> (o & 63)) & 1ull);
+    };
     // Cold rows of the wanted keys come straight out of their chunks (no detour through the hot
     // map); rows already past cleanup at `wm` are dropped, as a promote would.
     std::vector<std::pair<uint64_t, Session>> cold;
@@ -235,6 +263,11 @@ class SessionCore {
           cold_rows_ -= 1;
         };
         const size_t nw = (size_t)(hi - lo), nc = ch.key.size();
+        if (dense && (ch.by_key.size() != nc || nw * 20 >= nc)) {
+          for (uint32_t r = 0; r < (uint32_t)nc; ++r)
+            if (ch.cnt[r] && wanted_dense(ch.key[r])) take(r);
+          continue;
+        }
         if (ch.by_key.size() != nc && nw * 20 >= nc) {
           // Many wanted keys and no row index yet: one pass over the chunk probing a hash set
           // of the wanted keys (sorting the chunk's 10^5-10^6 rows for an index costs more).
@@ -265,9 +298,20 @@ class SessionCore {
           for (; p != ch.by_key.end() && ch.key[*p] == *it; ++p) take(*p);
         }
       }
-      std::stable_sort(cold.begin(), cold.end(),
-                       [](const auto& a, const auto& b) { return a.first < b.first; });
+      if (dense && cold.size() > 1) {
+        // stable counting sort by key offset (same order as the stable comparison sort)
+        std::vector<uint32_t> cnt(wspan + 1, 0);
+        for (const auto& c : cold) ++cnt[c.first - wmin + 1];
+        for (size_t i = 1; i < cnt.size(); ++i) cnt[i] += cnt[i - 1];
+        std::vector<std::pair<uint64_t, Session>> sorted(cold.size());
+        for (const auto& c : cold) sorted[cnt[c.first - wmin]++] = c;
+        cold.swap(sorted);
+      } else {
+        std::stable_sort(cold.begin(), cold.end(),
+                         [](const auto& a, const auto& b) { return a.first < b.first; });
+      }
     }
+    const bool no_hot = m_.empty();
     Columns out;
     size_t c = 0;
     for (uint64_t key : want) {
@@ -276,7 +320,7 @@ class SessionCore {
       const size_t cb = c;
       while (c < cold.size() && cold[c].first == key) ++c;
       (void)c0;
-      auto it = m_.find(key);
+      auto it = no_hot ? m_.end() : m_.find(key);
       const int64_t nhot = it == m_.end() ? 0 : (int64_t)it->second.size();
       if (nhot + (int64_t)(c - cb) > max_sess) {  // stays on the host: cold rows turn hot
         auto& vec = m_[key];

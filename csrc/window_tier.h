@@ -10,6 +10,7 @@
 #include <cstring>
 #include <deque>
 #include <stdexcept>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -117,48 +118,209 @@ class WindowTierCore {
   }
 
   // A tiered firing: the device's rows of the window (dev_*: one per key, no epilogue) combined
-  // with this tier's rows of panes [p0, p1] per key, in one hash aggregation. only_dev: a
-  // re-firing -- tier rows count only for keys the device fired. Output order: hash order.
+  // with this tier's rows of panes [p0, p1] per key. only_dev: a re-firing -- tier rows count
+  // only for keys the device fired. Output order: partition order (unspecified).
+  //
+  // Radix-partitioned parallel hash aggregation (the single-table version spent ~300 ms per
+  // firing on cache misses at 10M rows): threads count their share of every source per
+  // partition (top bits of mix64(key)), scatter the rows into partition-contiguous buffers, then
+  // aggregate partitions independently in cache-sized tables. Device rows of a partition are
+  // folded before its tier rows, so only_dev sees every device key first.
   void merge_fire(int64_t p0, int64_t p1, const uint64_t* dk, const int64_t* da,
                   const int64_t* dc, size_t nd, bool only_dev, std::vector<uint64_t>* keys,
                   std::vector<int64_t>* acc, std::vector<int64_t>* cnt) const {
     keys->clear();
     acc->clear();
     cnt->clear();
+    struct Src {
+      const uint64_t* k;
+      const int64_t *a, *c, *pane;
+      size_t n;
+      bool dev;
+    };
+    std::vector<Src> src;
+    if (nd) src.push_back({dk, da, dc, nullptr, nd, true});
     size_t cand = nd;
     for (auto& c : chunks_)
-      if (c.pmax >= p0 && c.pmin <= p1) cand += c.size();
-    size_t cap = 16;
-    while (cap < 2 * cand) cap <<= 1;
-    std::vector<uint64_t> hk(cap, kEmptyKey);
-    std::vector<int64_t> ha(cap), hc(cap, 0);
-    const size_t mask = cap - 1;
-    auto put = [&](uint64_t k, int64_t a, int64_t c, bool insert) {
-      size_t h = (size_t)(mix64(k) >> 32) & mask;
-      while (hk[h] != kEmptyKey && hk[h] != k) h = (h + 1) & mask;
-      if (hk[h] == kEmptyKey) {
-        if (!insert) return;
-        hk[h] = k;
-        ha[h] = a;
-        hc[h] = c;
-      } else {
-        ha[h] = (int64_t)agg_combine(agg_, (uint64_t)ha[h], (uint64_t)a);
-        hc[h] += c;
+      if (c.pmax >= p0 && c.pmin <= p1 && c.size()) {
+        src.push_back({c.key.data(), c.acc.data(), c.cnt.data(), c.pane.data(), c.size(), false});
+        cand += c.size();
+      }
+    if (!cand) return;
+    const int pbits = cand > (1u << 20) ? 8 : 4;
+    const size_t P = (size_t)1 << pbits;
+    unsigned hw = std::thread::hardware_concurrency();
+    const size_t T = cand < (1u << 16) ? 1 : std::max(1u, std::min(hw ? hw : 1u, 16u));
+    auto part_of = [&](uint64_t k) { return (size_t)(mix64(k) >> (64 - pbits)); };
+    auto keep = [&](const Src& s, size_t i) {
+      return s.dev || (s.pane[i] >= p0 && s.pane[i] <= p1 && s.c[i]);
+    };
+    auto piece = [&](const Src& s, size_t t, size_t* lo, size_t* hi) {
+      *lo = s.n * t / T;
+      *hi = s.n * (t + 1) / T;
+    };
+    auto run = [&](auto&& fn) {
+      if (T == 1) {
+        fn((size_t)0);
+        return;
+      }
+      std::vector<std::thread> th;
+      for (size_t t = 0; t < T; ++t) th.emplace_back(fn, t);
+      for (auto& x : th) x.join();
+    };
+    // 1. counts per (thread, partition)
+    std::vector<size_t> cnts(T * P, 0);
+    run([&](size_t t) {
+      size_t* ct = cnts.data() + t * P;
+      for (auto& s : src) {
+        size_t lo, hi;
+        piece(s, t, &lo, &hi);
+        for (size_t i = lo; i < hi; ++i)
+          if (keep(s, i)) ++ct[part_of(s.k[i])];
+      }
+    });
+    // partition-major offsets: partition p holds thread 0's rows, then thread 1's, ...
+    std::vector<size_t> off(T * P), pstart(P + 1, 0);
+    size_t tot = 0;
+    for (size_t p = 0; p < P; ++p) {
+      pstart[p] = tot;
+      for (size_t t = 0; t < T; ++t) {
+        off[t * P + p] = tot;
+        tot += cnts[t * P + p];
+      }
+    }
+    pstart[P] = tot;
+    struct Row {
+      uint64_t k;
+      int64_t a, c;
+      uint64_t dev;
+    };
+    std::vector<Row> rows(tot);
+    // 2. scatter
+    run([&](size_t t) {
+      size_t* o = off.data() + t * P;
+      for (auto& s : src) {
+        size_t lo, hi;
+        piece(s, t, &lo, &hi);
+        for (size_t i = lo; i < hi; ++i)
+          if (keep(s, i)) rows[o[part_of(s.k[i])]++] = Row{s.k[i], s.a[i], s.c[i], s.dev};
+      }
+    });
+    // 3. aggregate partitions (thread t takes partitions t, t + T, ...)
+    std::vector<std::vector<Row>> outp(P);
+    run([&](size_t t) {
+      std::vector<uint64_t> hk;
+      std::vector<int64_t> ha, hc;
+      for (size_t p = t; p < P; p += T) {
+        const size_t b = pstart[p], e = pstart[p + 1];
+        if (b == e) continue;
+        size_t cap = 16;
+        while (cap < 2 * (e - b)) cap <<= 1;
+        hk.assign(cap, kEmptyKey);
+        ha.assign(cap, 0);
+        hc.assign(cap, 0);
+        const size_t mask = cap - 1;
+        for (int pass = 0; pass < 2; ++pass) {  // device rows first, then tier rows
+          for (size_t i = b; i < e; ++i) {
+            const Row& r = rows[i];
+            if ((r.dev != 0) != (pass == 0)) continue;
+            // (mix64's low bits: the partition took the top ones)
+            size_t h = (size_t)mix64(r.k) & mask;
+            while (hk[h] != kEmptyKey && hk[h] != r.k) h = (h + 1) & mask;
+            if (hk[h] == kEmptyKey) {
+              if (!r.dev && only_dev) continue;
+              hk[h] = r.k;
+              ha[h] = r.a;
+              hc[h] = r.c;
+            } else {
+              ha[h] = (int64_t)agg_combine(agg_, (uint64_t)ha[h], (uint64_t)r.a);
+              hc[h] += r.c;
+            }
+          }
+        }
+        auto& out = outp[p];
+        for (size_t h = 0; h < cap; ++h)
+          if (hk[h] != kEmptyKey) out.push_back(Row{hk[h], ha[h], hc[h], 0});
+      }
+    });
+    size_t nout = 0;
+    for (auto& o : outp) nout += o.size();
+    keys->reserve(nout);
+    acc->reserve(nout);
+    cnt->reserve(nout);
+    for (auto& o : outp)
+      for (auto& r : o) {
+        keys->push_back(r.k);
+        acc->push_back(r.a);
+        cnt->push_back(r.c);
+      }
+  }
+
+  // A traced program from its (op, arg) code list and constants (csrc/mxs_common.h ExprProg).
+  static ExprProg prog(const int32_t* code, size_t ncode, const double* consts, size_t nconst) {
+    ExprProg p;
+    std::memset(&p, 0, sizeof(p));
+    if (ncode > (size_t)2 * kExprMaxCode || nconst > (size_t)kExprMaxConst)
+      throw std::invalid_argument("expr program too large");
+    for (size_t i = 0; i < ncode; ++i) p.code[i] = code[i];
+    for (size_t i = 0; i < nconst; ++i) p.consts[i] = consts[i];
+    p.ncode = (int32_t)(ncode / 2);
+    return p;
+  }
+
+  // The window epilogue over merged rows (the host twin of window_fire's fused map/filter):
+  // result, traced map, traced filter; kept rows in input order. Threaded over row ranges.
+  void epilogue(const std::vector<uint64_t>& keys, const std::vector<int64_t>& acc,
+                const std::vector<int64_t>& cnt, const ExprProg& mp, const ExprProg& fp,
+                int64_t wstart, int64_t wend, std::vector<uint64_t>* ok,
+                std::vector<double>* oval, std::vector<int64_t>* oraw,
+                std::vector<int32_t>* ocnt) const {
+    const size_t n = keys.size();
+    unsigned hw = std::thread::hardware_concurrency();
+    const size_t T = n < (1u << 15) ? 1 : std::max(1u, std::min(hw ? hw : 1u, 16u));
+    struct Part {
+      std::vector<uint64_t> k;
+      std::vector<double> v;
+      std::vector<int64_t> r;
+      std::vector<int32_t> c;
+    };
+    std::vector<Part> parts(T);
+    auto work = [&](size_t t) {
+      const size_t lo = n * t / T, hi = n * (t + 1) / T;
+      Part& pt = parts[t];
+      for (size_t i = lo; i < hi; ++i) {
+        double vars[kExprVars] = {0};
+        vars[0] = agg_result_f64(agg_, (uint64_t)acc[i], (uint32_t)cnt[i]);
+        vars[1] = (double)cnt[i];
+        vars[2] = (double)wstart;
+        vars[3] = (double)wend;
+        vars[4] = (double)keys[i];
+        vars[5] = (double)acc[i];
+        vars[6] = mp.ncode ? expr_eval(mp, vars) : vars[0];
+        if (fp.ncode && expr_eval(fp, vars) == 0.0) continue;
+        pt.k.push_back(keys[i]);
+        pt.v.push_back(vars[6]);
+        pt.r.push_back(acc[i]);
+        pt.c.push_back((int32_t)cnt[i]);
       }
     };
-    for (size_t i = 0; i < nd; ++i) put(dk[i], da[i], dc[i], true);
-    for (auto& c : chunks_) {
-      if (c.pmax < p0 || c.pmin > p1) continue;
-      for (size_t i = 0; i < c.size(); ++i)
-        if (c.pane[i] >= p0 && c.pane[i] <= p1 && c.cnt[i])
-          put(c.key[i], c.acc[i], c.cnt[i], !only_dev);
+    if (T == 1) {
+      work(0);
+    } else {
+      std::vector<std::thread> th;
+      for (size_t t = 0; t < T; ++t) th.emplace_back(work, t);
+      for (auto& x : th) x.join();
     }
-    for (size_t h = 0; h < cap; ++h)
-      if (hk[h] != kEmptyKey) {
-        keys->push_back(hk[h]);
-        acc->push_back(ha[h]);
-        cnt->push_back(hc[h]);
-      }
+    ok->clear();
+    oval->clear();
+    oraw->clear();
+    ocnt->clear();
+    for (auto& pt : parts) {
+      ok->insert(ok->end(), pt.k.begin(), pt.k.end());
+      oval->insert(oval->end(), pt.v.begin(), pt.v.end());
+      oraw->insert(oraw->end(), pt.r.begin(), pt.r.end());
+      ocnt->insert(ocnt->end(), pt.c.begin(), pt.c.end());
+    }
   }
 
   // Drop rows of panes < keep_from: whole chunks below it, filtered straddling chunks.

@@ -2,6 +2,7 @@
 // runtime/window_spill.py HostWindowTier.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include "mxs_runtime.h"
 #include "window_tier.h"
@@ -64,6 +65,28 @@ void bind_window_tier(py::module_& m) {
         }
         return py::make_tuple(np_of(k), np_of(a), np_of(c));
       })
+      .def("merge_fire_epilogue",
+           [](const WindowTierCore& t, int64_t p0, int64_t p1, Arr<uint64_t> dk, Arr<int64_t> da,
+              Arr<int64_t> dc, bool only_dev, std::vector<int32_t> mc, std::vector<double> mk,
+              std::vector<int32_t> fc, std::vector<double> fk, int64_t wstart, int64_t wend) {
+             const size_t n = (size_t)dk.size();
+             if ((size_t)da.size() != n || (size_t)dc.size() != n)
+               throw std::invalid_argument("WindowTier.merge_fire_epilogue: column lengths differ");
+             const mxs::ExprProg mp = WindowTierCore::prog(mc.data(), mc.size(), mk.data(),
+                                                                   mk.size());
+             const mxs::ExprProg fp = WindowTierCore::prog(fc.data(), fc.size(), fk.data(),
+                                                                   fk.size());
+             std::vector<uint64_t> k, ok;
+             std::vector<int64_t> a, c, oraw;
+             std::vector<double> ov;
+             std::vector<int32_t> oc;
+             {
+               py::gil_scoped_release nogil;
+               t.merge_fire(p0, p1, dk.data(), da.data(), dc.data(), n, only_dev, &k, &a, &c);
+               t.epilogue(k, a, c, mp, fp, wstart, wend, &ok, &ov, &oraw, &oc);
+             }
+             return py::make_tuple(np_of(ok), np_of(ov), np_of(oraw), np_of(oc));
+           })
       .def("purge", [](WindowTierCore& t, int64_t keep_from) {
         py::gil_scoped_release nogil;
         t.purge(keep_from);

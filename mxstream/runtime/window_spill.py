@@ -125,18 +125,23 @@ def merge_fire(agg: int, dev_keys, dev_raw, dev_cnt, host, only_dirty: bool,
     host: a HostWindowTier (combined in C++ with the device rows over `panes`) or an already
     combined (keys, acc, cnt) part."""
     if isinstance(host, HostWindowTier):
-        keys, raw, cnt = host._t.merge_fire(
+        # Merge + result + map + filter in C++ (threaded), the numpy epilogue below stays the
+        # path for an already combined part.
+        mc, mk = map_prog.as_args()
+        fc, fk = filter_prog.as_args()
+        keys, mapped, raw, cnt = host._t.merge_fire_epilogue(
             int(panes[0]), int(panes[1]), np.ascontiguousarray(dev_keys, dtype=np.uint64),
             np.ascontiguousarray(dev_raw, dtype=np.int64),
-            np.ascontiguousarray(dev_cnt, dtype=np.int64), bool(only_dirty))
-    else:
-        hk, hacc, hcnt = host
-        if only_dirty and hk.size:
-            sel = np.isin(hk, dev_keys)
-            hk, hacc, hcnt = hk[sel], hacc[sel], hcnt[sel]
-        keys, raw, cnt = combine_rows(agg, np.concatenate([dev_keys.astype(np.uint64), hk]),
-                                      np.concatenate([dev_raw.astype(np.int64), hacc]),
-                                      np.concatenate([dev_cnt.astype(np.int64), hcnt]))
+            np.ascontiguousarray(dev_cnt, dtype=np.int64), bool(only_dirty), mc, mk, fc, fk,
+            int(wstart), int(wend))
+        return keys, mapped, raw, cnt
+    hk, hacc, hcnt = host
+    if only_dirty and hk.size:
+        sel = np.isin(hk, dev_keys)
+        hk, hacc, hcnt = hk[sel], hacc[sel], hcnt[sel]
+    keys, raw, cnt = combine_rows(agg, np.concatenate([dev_keys.astype(np.uint64), hk]),
+                                  np.concatenate([dev_raw.astype(np.int64), hacc]),
+                                  np.concatenate([dev_cnt.astype(np.int64), hcnt]))
     res = result_values(agg, raw, cnt)
     vars_ = [res, cnt.astype(np.float64), float(wstart), float(wend), keys.astype(np.float64),
              raw.astype(np.float64), res, 0.0]

@@ -306,6 +306,37 @@ def engine_with(events, gap, bound, lateness, *, promote, device, batch, **kw):
     return out, op
 
 
+def test_store_extract_dense_span_equals_sparse():
+    """extract() over a dense key span (bitmap + counting-sort path) returns exactly what the
+    sparse path (sort + hash probe / row index) returns for the same sessions under an
+    order-preserving key map: rows grouped by key in ascending order, arrival order within a
+    key, rows past cleanup dropped."""
+    from mxstream.ops.native import load
+
+    m = load()
+    rng = np.random.default_rng(21)
+    base = rng.permutation(np.arange(1000, 41000, dtype=np.int64))
+    k = np.concatenate([base, base[:5000]])  # 5000 keys with two cold rows
+    st_ = (k % 5000).astype(np.int64) + np.where(np.arange(len(k)) >= len(base), 2000, 0)
+    en = st_ + 100
+    acc = np.arange(len(k), dtype=np.int64)
+    ones = np.ones_like(k)
+    sparse_of = lambda x: x * 1_000_003 + 7  # noqa: E731  (monotone: same key order)
+    dense_st = m.SessionStore(100, 1000, K.AGG_SUM_I64)
+    sparse_st = m.SessionStore(100, 1000, K.AGG_SUM_I64)
+    dense_st.insert(k, st_, en, acc, ones, ones, True)
+    sparse_st.insert(sparse_of(k), st_, en, acc, ones, ones, True)
+    for rnd in range(3):
+        want = rng.choice(np.arange(900, 41100, dtype=np.int64), 3000 + 9000 * rnd)
+        a = dense_st.extract(want, 4500, 4)
+        b = sparse_st.extract(sparse_of(want), 4500, 4)
+        assert np.array_equal(sparse_of(a["key"]), b["key"])
+        for c in ("start", "end", "acc", "cnt", "flags"):
+            assert np.array_equal(a[c], b[c]), c
+        assert np.array_equal(np.sort(sparse_of(a["moved"])), np.sort(b["moved"]))
+    assert dense_st.num_keys() == sparse_st.num_keys()
+
+
 def test_store_extract_hands_back_sessions():
     # Promotion back to HBM (GPU operator) takes keys out of the host store: cold rows and hot
     # sessions of keys with <= max_sess sessions; rows past cleanup are dropped; keys with more

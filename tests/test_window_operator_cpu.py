@@ -560,17 +560,19 @@ def test_key_value_rows_equal_full_rows(size, slide, lateness):
     assert run("key_value") == full
 
 
-def test_cxx_window_tier_equals_numpy_combine():
+@pytest.mark.parametrize("n", [4000, 250_000])
+def test_cxx_window_tier_equals_numpy_combine(n):
     """csrc/window_tier.h: chunked absorb, per-key part() and the tiered merge_fire equal the
-    numpy combine of the same rows; purge drops exactly the rows below the cutoff."""
+    numpy combine of the same rows; purge drops exactly the rows below the cutoff. n = 250K rows
+    per eviction takes merge_fire's threaded radix-partitioned aggregation (256 partitions)."""
     from mxstream.runtime.window_spill import HostWindowTier, combine_rows, merge_fire
 
     rng = np.random.default_rng(4)
     t = HostWindowTier(K.AGG_SUM_I64)
     cols = {k: [] for k in ("key", "pane", "acc", "cnt", "dirty")}
+    nkeys = n * 3 // 4
     for _ in range(5):  # evictions -> chunks (a key may be evicted twice)
-        n = 4000
-        c = {"key": rng.integers(0, 3000, n).astype(np.uint64),
+        c = {"key": rng.integers(0, nkeys, n).astype(np.uint64),
              "pane": rng.integers(10, 20, n).astype(np.int64),
              "acc": rng.integers(-1000, 1000, n).astype(np.int64),
              "cnt": rng.integers(1, 5, n).astype(np.int64),
@@ -584,7 +586,7 @@ def test_cxx_window_tier_equals_numpy_combine():
     k, a, c = t.part(12, 15)
     ek, ea, ec = combine_rows(K.AGG_SUM_I64, cols["key"][sel], cols["acc"][sel], cols["cnt"][sel])
     assert np.array_equal(k, ek) and np.array_equal(a, ea) and np.array_equal(c, ec)
-    dk = np.arange(0, 3500, 7, dtype=np.uint64)
+    dk = np.arange(0, nkeys + nkeys // 6, 7, dtype=np.uint64)
     dr = rng.integers(0, 100, dk.size).astype(np.int64)
     dc = np.ones(dk.size, np.int64)
     for only in (False, True):
