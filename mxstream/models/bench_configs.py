@@ -140,6 +140,57 @@ def config2(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000,
             "alerts": alerts, "keys": keys, "events_per_step": batch, "device": str(dev)}
 
 
+def config2_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 500_000,
+                  drift: int = 50_000, table_keys: int = 1_000_000, revisit: float = 0.01,
+                  device: str = "cuda") -> dict:
+    """Keyed ValueState counter (config 2's operator, hashed keys) over a key space that outgrows
+    the HBM table: each step's events come from `active` consecutive ids whose window moves by
+    `drift` per step, and `revisit` of the events go to keys that went idle ~10 steps ago (their
+    counts live in host DRAM by then and come back before the step folds them). Reports events/s,
+    spilled / promoted keys and the host tier's size."""
+    dev = torch.device(device)
+    op = KeyedRollingOperator(agg=K.AGG_COUNT, device=dev, max_keys=table_keys,
+                              batch_capacity=batch,
+                              filter_prog=E.compile_expr(E.var(E.VAR_COUNT) % 1000 == 0),
+                              emit_capacity=1 << 20, spill=True)
+    kt = torch.empty(batch, dtype=torch.int64, device=dev)
+    tt = torch.empty_like(kt)
+    vt = torch.empty_like(kt)
+    step_i = [0]
+    stride = max(2, round(1.0 / revisit)) if revisit > 0 else 0
+
+    def step():
+        i = step_i[0]
+        K.gen_events(kt, tt, vt, seed=2, stream_id=0, idx0=i * batch, nkeys=active, ts_base=0,
+                     ts_span=1000, disorder=0, val_lo=0, val_span=100)
+        kt.add_(i * drift)
+        if stride and i >= 12:
+            old = kt[::stride]
+            old.sub_(i * drift).remainder_(drift).add_((i - 10) * drift)
+        rows = op.process(kt, vt)
+        step_i[0] += 1
+        return len(rows.keys)
+
+    for _ in range(warmup):
+        step()
+    _sync(dev)
+    st0 = dict(op.spill_stats)
+    t0 = time.perf_counter()
+    alerts = 0
+    for _ in range(steps):
+        alerts += step()
+    _sync(dev)
+    dt = time.perf_counter() - t0
+    return {"config": "2-spill", "metric": "events/sec (keyed ValueState counter, key space "
+            "outgrowing HBM, host-DRAM tier)", "value": batch * steps / dt, "unit": "events/s",
+            "ms_per_step": dt / steps * 1e3, "alerts": alerts, "events_per_step": batch,
+            "table_keys": table_keys, "active_keys": active, "drift_per_step": drift,
+            "revisit": revisit,
+            **{k: op.spill_stats[k] - st0[k] for k in op.spill_stats},
+            "host_keys": len(op.store), "host_bytes": op.host_bytes(),
+            "resident_keys": op.live_keys, "device": str(dev)}
+
+
 def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_000,
             device: str = "cuda", dense_keys: bool = True, pipeline="stream") -> dict:
     """Sliding 1 min / 10 s event-time window sum + 30 s allowed lateness, 10M keys; 5 % of
@@ -554,7 +605,7 @@ def main(argv=None) -> int:
     ap.add_argument("--host-fold", action="store_true",
                     help="config 5: fold records of spilled keys in host DRAM (no promotion to HBM)")
     ap.add_argument("--spill", action="store_true",
-                    help="config 4: key space outgrowing the HBM table (host-DRAM tier)")
+                    help="configs 2/4: key space outgrowing the HBM table (host-DRAM tier)")
     ap.add_argument("--revisit", type=float, default=0.0,
                     help="config 5: fraction of events for spilled (long idle) keys")
     ap.add_argument("--steps", type=int, default=20)
@@ -576,6 +627,9 @@ def main(argv=None) -> int:
         r = config1(a.steps, a.warmup, a.batch or (1 << 20),
                     device="cpu" if a.device == "cuda" and not a.gpu_parse else a.device,
                     threads=a.threads)
+    elif a.config == 2 and a.spill:
+        r = config2_spill(a.steps, a.warmup, a.batch or (1 << 22), device=a.device,
+                          revisit=a.revisit or 0.01)
     elif a.config == 2:
         r = config2(a.steps, a.warmup, a.batch or (1 << 24), device=a.device,
                     keys=a.keys or 10_000, dense_keys=not a.hashed_keys,

@@ -40,7 +40,8 @@ class KeyedRollingOperator:
                  max_keys: int = 1 << 16, parallelism: int | None = None,
                  max_parallelism: int = 128, batch_capacity: int = 1 << 20,
                  cap_log2: int | None = None, filter_prog: E.Program = E.EMPTY, emit_capacity: int | None = None,
-                 count_window: int = 0, dense_keys: bool = False):
+                 count_window: int = 0, dense_keys: bool = False, spill: bool = False,
+                 spill_load: float = 0.75, spill_target: float = 0.5):
         """count_window = n > 0: tumbling count windows instead of a rolling aggregate
         (``keyBy(..).countWindow(n)`` with an incremental reduce/aggregate: GlobalWindows +
         PurgingTrigger(CountTrigger(n)), chapter2/README.md:78) -- a row is emitted when a key's
@@ -48,7 +49,15 @@ class KeyedRollingOperator:
         count is n), and the state keeps each key's open window.
 
         dense_keys: keys are dictionary ids in [0, max_keys) (columnar ingest, device-generated
-        ids): the slot IS the key id -- no hash probe. Single-rank GPU sort-free COUNT only."""
+        ids): the slot IS the key id -- no hash probe. Single-rank GPU sort-free COUNT only.
+
+        spill: keyed state beyond the HBM table lives in host DRAM (RollingSpillStore). Every
+        slot records the step that last touched it; when the table's load passes `spill_load`
+        after a step, the least recently touched keys move to the host store until the load is
+        `spill_target` (the table is rebuilt without them). A batch whose keys include spilled
+        ones first promotes them back (their (acc, count) re-inserted into HBM), so every record
+        is still folded by the GPU pass in arrival order. The headroom (1 - spill_load) must hold
+        one micro-batch's new keys."""
         self.device = K.resolve_device(device)
         self.comm = comm or LocalComm()
         self.world, self.rank = self.comm.world, self.comm.rank
@@ -83,6 +92,18 @@ class KeyedRollingOperator:
         self.acc_g = torch.zeros(self.nslots, dtype=torch.int64, device=dev)
         self.cnt_g = torch.zeros(self.nslots, dtype=torch.int32, device=dev)
         self.flags = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.spill = bool(spill)
+        if self.spill:
+            if self.dense:
+                raise ValueError("spill: hashed keyed state only (dense ids address the table)")
+            if not 0.0 < spill_target < spill_load < 1.0:
+                raise ValueError("spill: need 0 < spill_target < spill_load < 1")
+            self.spill_load, self.spill_target = float(spill_load), float(spill_target)
+            # last touching step per slot (+1 sink entry for hole records)
+            self.last_g = torch.zeros(self.nslots + 1, dtype=torch.int64, device=dev)
+            self.store = RollingSpillStore(dev)
+            self.live_keys = 0
+            self.spill_stats = {"evictions": 0, "spilled_keys": 0, "promoted_keys": 0}
         kgd = [(kg * self.parallelism // max_parallelism) * self.world // self.parallelism
                for kg in range(max_parallelism)]
         self.kg_dest = torch.tensor(kgd, dtype=torch.int32, device=dev)
@@ -97,7 +118,7 @@ class KeyedRollingOperator:
         self.direct_single_rank = True  # world 1 on the GPU: no partition pass (_process_direct)
         # Sort-free COUNT path (rolling_hist) when the table fits its LDS counter; False forces
         # the sort path (A/B, tests).
-        self.sort_free = True
+        self.sort_free = not self.spill  # the spill tier tracks slots through the sort path
         self._hist_tmp = None
         if self.dense:
             code, consts = filter_prog.as_args()
@@ -174,6 +195,8 @@ class KeyedRollingOperator:
                                     self.cap_log2, self.keys_g.data_ptr(),
                                     self.sort_key.data_ptr(), self.vals_buf.data_ptr(),
                                     self.n_buf.data_ptr(), self.flags.data_ptr(), shift, st)
+        if self.spill:
+            self._touch_sorted(self.sort_key[:n], shift)
         nbits = shift + self.nslots.bit_length()
         need = m.gpu_sort_pairs_temp_bytes(n, shift, nbits)
         if self._sort_tmp is None or self._sort_tmp.numel() < need:
@@ -195,6 +218,17 @@ class KeyedRollingOperator:
 
     def process(self, keys: torch.Tensor, vals: torch.Tensor, to_host: bool = True):
         """Update state with one micro-batch; returns the emitted rows (host) or the device count."""
+        if not self.spill:
+            return self._process(keys, vals, to_host)
+        self._promote(keys)
+        out = self._process(keys, vals, to_host)
+        if self.device.type != "cuda":
+            touched = torch.isin(self.keys_g, keys)
+            self.last_g[:self.nslots][touched] = self.steps
+        self._maybe_evict()
+        return out
+
+    def _process(self, keys: torch.Tensor, vals: torch.Tensor, to_host: bool):
         n = keys.numel()
         if n > self.batch_capacity:
             self._alloc(n, self.slack)
@@ -242,6 +276,8 @@ class KeyedRollingOperator:
                                  self.sort_key.data_ptr(), self.vals_buf.data_ptr(),
                                  self.n_buf.data_ptr(), self.flags.data_ptr(), abits, shift, st)
             total = int(self.n_buf[0].item())
+            if total and self.spill:
+                self._touch_sorted(self.sort_key[:total], shift)
             if total:
                 # Key-value radix sort over the used bits (slot | src | arrival): the values ride
                 # along, so the scan reads them in order (no permutation gather).
@@ -275,6 +311,73 @@ class KeyedRollingOperator:
                                self.count_window)
         return self._emit(to_host)
 
+    # ---- host-DRAM spill tier ------------------------------------------------------------------
+    def _touch_sorted(self, sk: torch.Tensor, shift: int) -> None:
+        """last_g[slot] = step for every slot of the step's sort keys (slot << shift | ...;
+        INT64_MAX holes land on the sink entry). Stream-ordered, no host sync."""
+        slot = torch.where(sk == I64_MAX, torch.full_like(sk, self.nslots), sk >> shift)
+        self.last_g.index_fill_(0, slot, self.steps)
+
+    def _promote(self, keys: torch.Tensor) -> None:
+        """Spilled keys of this batch go back to HBM with their (acc, count) before the pass."""
+        if not len(self.store) or not keys.numel():
+            return
+        hit = torch.isin(keys, self.store.keys_on(self.device))
+        if not bool(hit.any()):
+            return
+        uk = torch.unique(keys[hit])
+        acc, cnt = self.store.take(uk.cpu().numpy())
+        self._make_room(uk.numel(), protect=keys)
+        slots = K.table_insert(uk, self.keys_g, nsub_log2=self.nsub_log2, cap_log2=self.cap_log2)
+        if bool((slots < 0).any()):
+            raise RuntimeError("keyed state table full while promoting spilled keys "
+                               "(lower spill_load or raise max_keys)")
+        self.acc_g[slots] = torch.from_numpy(acc).to(self.device)
+        self.cnt_g[slots] = torch.from_numpy(cnt.astype(np.int32)).to(self.device)
+        self.last_g[slots] = self.steps
+        self.live_keys += uk.numel()
+        self.spill_stats["promoted_keys"] += uk.numel()
+
+    def _maybe_evict(self) -> None:
+        self.live_keys = int((self.keys_g != -1).sum())
+        self._make_room(0)
+
+    def _make_room(self, extra: int, protect: torch.Tensor | None = None) -> None:
+        """Evict the least recently touched keys when live + extra passes spill_load. Keys in
+        `protect` (the batch about to be folded) stay resident."""
+        if self.live_keys + extra <= self.spill_load * self.nslots:
+            return
+        need = self.live_keys + extra - int(self.spill_target * self.nslots)
+        valid = self.keys_g != -1
+        lg = torch.where(valid, self.last_g[:self.nslots], torch.full_like(self.last_g[:1], I64_MAX))
+        if protect is not None:
+            lg = torch.where(torch.isin(self.keys_g, protect), torch.full_like(lg, I64_MAX), lg)
+        need = max(1, min(need, self.live_keys))
+        thr = torch.kthvalue(lg, need).values
+        ev = valid & (lg <= thr) & (lg != I64_MAX)
+        idx = torch.nonzero(ev).flatten()
+        self.store.add(self.keys_g[idx].cpu().numpy(), self.acc_g[idx].cpu().numpy(),
+                       self.cnt_g[idx].cpu().numpy().astype(np.int64))
+        keep = torch.nonzero(valid & ~ev).flatten()
+        kk, ka = self.keys_g[keep].clone(), self.acc_g[keep].clone()
+        kc, kl = self.cnt_g[keep].clone(), self.last_g[keep].clone()
+        self.keys_g.fill_(-1)
+        self.acc_g.zero_()
+        self.cnt_g.zero_()
+        self.last_g.zero_()
+        if kk.numel():
+            slots = K.table_insert(kk, self.keys_g, nsub_log2=self.nsub_log2,
+                                   cap_log2=self.cap_log2)
+            self.acc_g[slots] = ka
+            self.cnt_g[slots] = kc
+            self.last_g[slots] = kl
+        self.live_keys = kk.numel()
+        self.spill_stats["evictions"] += 1
+        self.spill_stats["spilled_keys"] += idx.numel()
+
+    def host_bytes(self) -> int:
+        return self.store.nbytes() if self.spill else 0
+
     def check(self) -> int:
         """Host check of the sticky flags (table full, reserved key); returns the last step's
         emitted row count. to_host=False callers (benchmarks) call it at the end."""
@@ -307,7 +410,7 @@ class KeyedRollingOperator:
         keys = self.keys_g.cpu().numpy()
         idx = np.nonzero(keys == np.int64(key))[0]
         if not len(idx):
-            return None
+            return self.store.get(int(key)) if self.spill else None
         i = int(idx[0])
         return int(self.acc_g[i].item()), int(self.cnt_g[i].item())
 
@@ -323,9 +426,15 @@ class KeyedRollingOperator:
 
         live = torch.nonzero(self.keys_g != -1).flatten()
         keys = self.keys_g[live].contiguous()
-        kg = K.keygroups(keys, max_parallelism=self.max_parallelism).cpu().numpy()
         cols = {"key": keys.cpu().numpy(), "acc": self.acc_g[live].cpu().numpy(),
                 "cnt": self.cnt_g[live].cpu().numpy()}
+        if self.spill and len(self.store):
+            hk, ha, hc = self.store.rows()
+            cols = {"key": np.concatenate([cols["key"], hk]),
+                    "acc": np.concatenate([cols["acc"], ha]),
+                    "cnt": np.concatenate([cols["cnt"], hc.astype(cols["cnt"].dtype)])}
+            keys = torch.from_numpy(cols["key"]).to(self.device)
+        kg = K.keygroups(keys, max_parallelism=self.max_parallelism).cpu().numpy()
         meta = {"kind": "rolling", "agg": self.agg, "records_in": self.records_in,
                 "steps": self.steps, "count_window": self.count_window}
         return OperatorSnapshot(kg, cols, meta)
@@ -338,6 +447,15 @@ class KeyedRollingOperator:
         self.acc_g.zero_()
         self.cnt_g.zero_()
         if not len(rows["key"]):
+            return
+        if self.spill:
+            # every key restarts in host DRAM and is promoted when its next record arrives
+            self.store.clear()
+            self.last_g.zero_()
+            self.store.add(np.ascontiguousarray(rows["key"], dtype=np.int64),
+                           np.ascontiguousarray(rows["acc"], dtype=np.int64),
+                           np.ascontiguousarray(rows["cnt"], dtype=np.int64))
+            self.live_keys = 0
             return
         dev = self.device
         keys = torch.from_numpy(np.ascontiguousarray(rows["key"])).to(dev)
@@ -353,3 +471,73 @@ class KeyedRollingOperator:
             raise RuntimeError("restore: keyed state does not fit the table (raise max_keys)")
         self.acc_g[slots] = torch.from_numpy(np.ascontiguousarray(rows["acc"])).to(dev)
         self.cnt_g[slots] = torch.from_numpy(np.ascontiguousarray(rows["cnt"])).to(dev)
+
+
+class RollingSpillStore:
+    """Host-DRAM tier of rolling keyed state: (key, acc, count) rows as sorted numpy columns.
+    Evictions append (merged into the sorted columns lazily, when a lookup needs them);
+    promotions take keys out. `keys_on(device)` is the sorted key column on the device for the
+    batch membership test (cached until the store changes)."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self._k = np.zeros(0, np.int64)
+        self._a = np.zeros(0, np.int64)
+        self._c = np.zeros(0, np.int64)
+        self._pending: list[tuple[np.ndarray, np.ndarray, np.ndarray]] = []
+        self._dev = None
+
+    def __len__(self) -> int:
+        return self._k.size + sum(p[0].size for p in self._pending)
+
+    def nbytes(self) -> int:
+        return 24 * len(self)
+
+    def clear(self) -> None:
+        self.__init__(self.device)
+
+    def add(self, k: np.ndarray, a: np.ndarray, c: np.ndarray) -> None:
+        if k.size:
+            self._pending.append((np.asarray(k, np.int64), np.asarray(a, np.int64),
+                                  np.asarray(c, np.int64)))
+            self._dev = None
+
+    def _merge(self) -> None:
+        if not self._pending:
+            return
+        k = np.concatenate([self._k] + [p[0] for p in self._pending])
+        a = np.concatenate([self._a] + [p[1] for p in self._pending])
+        c = np.concatenate([self._c] + [p[2] for p in self._pending])
+        o = np.argsort(k, kind="stable")
+        self._k, self._a, self._c = k[o], a[o], c[o]
+        self._pending = []
+
+    def keys_on(self, device) -> torch.Tensor:
+        self._merge()
+        if self._dev is None:
+            self._dev = torch.from_numpy(self._k).to(device)
+        return self._dev
+
+    def take(self, keys: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+        """(acc, count) of `keys` (all present), removed from the store."""
+        self._merge()
+        i = np.searchsorted(self._k, keys)
+        if keys.size and (i.max() >= self._k.size or not np.array_equal(self._k[i], keys)):
+            raise KeyError("rolling spill store: promoted key not present")
+        a, c = self._a[i], self._c[i]
+        keep = np.ones(self._k.size, bool)
+        keep[i] = False
+        self._k, self._a, self._c = self._k[keep], self._a[keep], self._c[keep]
+        self._dev = None
+        return a, c
+
+    def get(self, key: int):
+        self._merge()
+        i = int(np.searchsorted(self._k, key))
+        if i < self._k.size and self._k[i] == key:
+            return int(self._a[i]), int(self._c[i])
+        return None
+
+    def rows(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        self._merge()
+        return self._k.copy(), self._a.copy(), self._c.copy()

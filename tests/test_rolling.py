@@ -218,3 +218,63 @@ def test_count_window_gpu_equals_cpu(gpu_device, agg, n, direct):
         res[d.type] = got
     assert res["cuda"] == res["cpu"]
     assert sum(len(v) for v in res["cpu"].values()) > 0
+
+
+def _drifting_batches(dev, nbatches, per, window, drift, seed):
+    """Keys from a moving id window, plus a few revisits of long-gone keys (spilled state that
+    must come back with its value)."""
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for b in range(nbatches):
+        k = torch.randint(0, window, (per,), generator=g, dtype=torch.int64) + b * drift
+        if b >= 6:
+            k[::17] = torch.randint(0, drift, (k[::17].numel(),), generator=g) + (b - 6) * drift
+        v = torch.randint(-500, 500, (per,), generator=g, dtype=torch.int64)
+        out.append((k.to(dev), v.to(dev)))
+    return out
+
+
+def _spill_run(dev, batches, agg, spill, max_keys):
+    op = KeyedRollingOperator(agg=agg, device=dev, max_keys=max_keys, batch_capacity=4096,
+                              spill=spill)
+    rows = [op.process(k, v) for k, v in batches]
+    got = {}
+    for r in rows:
+        for k, val in _per_key(r).items():
+            got.setdefault(k, []).extend(val)
+    return got, op
+
+
+@pytest.mark.parametrize("agg", [K.AGG_SUM_I64, K.AGG_MAX_I64, K.AGG_COUNT])
+def test_rolling_spill_tier_matches_unbounded_cpu(agg):
+    """Keyed rolling state over a key space ~4x the table: LRU keys move to host DRAM and come
+    back with their values when they reappear; emissions equal an unbounded table's and the
+    oracle's."""
+    dev = torch.device("cpu")
+    batches = _drifting_batches(dev, 14, 600, 120, 80, 3)
+    got, op = _spill_run(dev, batches, agg, True, 256)
+    ref, _ = _spill_run(dev, batches, agg, False, 1 << 13)
+    assert got == ref == _oracle(batches, agg)
+    assert op.spill_stats["spilled_keys"] > 0 and op.spill_stats["promoted_keys"] > 0
+    assert len(op.store) > 0 and op.host_bytes() > 0
+    # checkpoint with spilled keys restores into an operator of the same (small) table
+    snap = op.snapshot_state()
+    fresh = KeyedRollingOperator(agg=agg, device=dev, max_keys=256, batch_capacity=4096,
+                                 spill=True)
+    fresh.restore_state(dict(snap.columns), snap.meta)
+    more = _drifting_batches(dev, 3, 600, 120, 80, 9)
+    a = [fresh.process(k, v) for k, v in more]
+    b = [op.process(k, v) for k, v in more]
+    for x, y in zip(a, b):
+        assert _per_key(x) == _per_key(y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", [K.AGG_SUM_I64, K.AGG_COUNT])
+def test_rolling_spill_tier_gpu_matches_unbounded(gpu_device, agg):
+    batches = _drifting_batches(gpu_device, 14, 600, 120, 80, 4)
+    got, op = _spill_run(gpu_device, batches, agg, True, 256)
+    ref, _ = _spill_run(gpu_device, batches, agg, False, 1 << 13)
+    cpu = [(k.cpu(), v.cpu()) for k, v in batches]
+    assert got == ref == _oracle(cpu, agg)
+    assert op.spill_stats["spilled_keys"] > 0 and op.spill_stats["promoted_keys"] > 0
