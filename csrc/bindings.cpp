@@ -818,6 +818,15 @@ PYBIND11_MODULE(_mxs_native, m) {
                              intptr_t stream) {
     gpu::set_rehash(P<uint64_t>(old), n_old, P<uint64_t>(neu), new_mask, stream);
   });
+  m.def("gpu_set_insert", [](intptr_t set, uint32_t mask, intptr_t keys, int64_t n,
+                             intptr_t stream) {
+    gpu::set_insert_keys(P<uint64_t>(set), mask, P<int64_t>(keys), n, stream);
+  });
+  m.def("gpu_set_probe", [](intptr_t set, uint32_t mask, intptr_t keys, int64_t n, intptr_t hit,
+                            intptr_t n_hit, intptr_t stream) {
+    gpu::set_probe(P<uint64_t>(set), mask, P<int64_t>(keys), n, P<uint8_t>(hit),
+                   P<uint32_t>(n_hit), stream);
+  });
   m.def("gpu_set_erase", [](intptr_t set, uint32_t mask, intptr_t keys, int64_t n,
                             intptr_t stream) {
     gpu::set_erase(P<uint64_t>(set), mask, P<int64_t>(keys), n, stream);

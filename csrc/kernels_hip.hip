@@ -3450,6 +3450,39 @@ __global__ __launch_bounds__(256) void set_erase_kernel(uint64_t* __restrict__ s
 // set (not empty, not a tombstone) is re-inserted into the fresh, larger set. The old set holds
 // exactly the host store's keys (inserted by the lookup/evict kernels, erased on release), so
 // the result equals a rebuild from the store, including keys whose host insert is still queued.
+// Batch insert into / membership probe of a device key set (open addressing on mix64 >> 32,
+// linear probing, kEmptyKey empty, kTombKey erased) -- the rolling spill tier's set of keys that
+// live in host DRAM. The probe writes one byte per key and counts hits with one device-scope
+// atomic per workgroup.
+__global__ __launch_bounds__(256) void set_insert_kernel(uint64_t* __restrict__ set, uint32_t mask,
+                                                         const int64_t* __restrict__ keys,
+                                                         int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    set_insert(set, mask, (uint64_t)keys[i]);
+}
+
+__global__ __launch_bounds__(256) void set_probe_kernel(const uint64_t* __restrict__ set,
+                                                        uint32_t mask,
+                                                        const int64_t* __restrict__ keys, int64_t n,
+                                                        uint8_t* __restrict__ hit,
+                                                        uint32_t* __restrict__ n_hit) {
+  __shared__ uint32_t s_hits;
+  if (threadIdx.x == 0) s_hits = 0;
+  __syncthreads();
+  uint32_t h = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const bool in = set_contains(set, mask, (uint64_t)keys[i]);
+    hit[i] = in ? 1 : 0;
+    h += in;
+  }
+  for (int d = 32; d >= 1; d >>= 1) h += __shfl_xor(h, d);
+  if (lane_id() == 0 && h) atomicAdd(&s_hits, h);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_hits) atomicAdd(n_hit, s_hits);
+}
+
 __global__ __launch_bounds__(256) void set_rehash_kernel(const uint64_t* __restrict__ old,
                                                          int64_t n_old, uint64_t* __restrict__ neu,
                                                          uint32_t new_mask) {
@@ -4666,6 +4699,22 @@ void set_rehash(const uint64_t* old, int64_t n_old, uint64_t* neu, uint32_t new_
   if (n_old <= 0) return;
   hipLaunchKernelGGL(set_rehash_kernel, dim3(grid_for(n_old, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, old, n_old, neu, new_mask);
+  HIP_CHECK(hipGetLastError());
+}
+
+void set_insert_keys(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n,
+                     intptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(set_insert_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, set, mask, keys, n);
+  HIP_CHECK(hipGetLastError());
+}
+
+void set_probe(const uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, uint8_t* hit,
+               uint32_t* n_hit, intptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(set_probe_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0,
+                     (hipStream_t)stream, set, mask, keys, n, hit, n_hit);
   HIP_CHECK(hipGetLastError());
 }
 

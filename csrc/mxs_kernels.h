@@ -325,6 +325,10 @@ void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uin
 void segment_median_select(const int64_t* heads, int64_t nseg, int64_t total,
                            const uint64_t* ord, double* out, intptr_t stream);
 void set_erase(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, intptr_t stream);
+void set_insert_keys(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n,
+                     intptr_t stream);
+void set_probe(const uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, uint8_t* hit,
+               uint32_t* n_hit, intptr_t stream);
 // Insert keys into the session slot table (tombstone reuse); slot -1 when a sub-table is full.
 void session_promote(const int64_t* slots, const int64_t* rec, const int64_t* last, int64_t n,
                      int64_t* sess, int64_t* slot_due, int64_t* slot_last, uint32_t* n_bad,

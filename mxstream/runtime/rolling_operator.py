@@ -103,6 +103,12 @@ class KeyedRollingOperator:
             self.last_g = torch.zeros(self.nslots + 1, dtype=torch.int64, device=dev)
             self.store = RollingSpillStore(dev)
             self.live_keys = 0
+            # GPU: keys in host DRAM as a device hash set (membership probe per batch); the CPU
+            # twin tests membership against the store's sorted keys
+            self._set = None
+            self._set_used = 0
+            self._hit = None
+            self._nhit = torch.zeros(1, dtype=torch.int32, device=dev)
             self.spill_stats = {"evictions": 0, "spilled_keys": 0, "promoted_keys": 0}
         kgd = [(kg * self.parallelism // max_parallelism) * self.world // self.parallelism
                for kg in range(max_parallelism)]
@@ -322,10 +328,25 @@ class KeyedRollingOperator:
         """Spilled keys of this batch go back to HBM with their (acc, count) before the pass."""
         if not len(self.store) or not keys.numel():
             return
-        hit = torch.isin(keys, self.store.keys_on(self.device))
-        if not bool(hit.any()):
-            return
+        if self.device.type == "cuda":
+            n = keys.numel()
+            if self._hit is None or self._hit.numel() < n:
+                self._hit = torch.empty(max(n, 1024), dtype=torch.uint8, device=self.device)
+            self._nhit.zero_()
+            st = torch.cuda.current_stream(self.device).cuda_stream
+            load().gpu_set_probe(self._set.data_ptr(), self._set.numel() - 1, keys.data_ptr(), n,
+                                 self._hit.data_ptr(), self._nhit.data_ptr(), st)
+            if not int(self._nhit.item()):
+                return
+            hit = self._hit[:n].bool()
+        else:
+            hit = torch.isin(keys, self.store.keys_on(self.device))
+            if not bool(hit.any()):
+                return
         uk = torch.unique(keys[hit])
+        if self.device.type == "cuda":
+            load().gpu_set_erase(self._set.data_ptr(), self._set.numel() - 1, uk.data_ptr(),
+                                 uk.numel(), torch.cuda.current_stream(self.device).cuda_stream)
         acc, cnt = self.store.take(uk.cpu().numpy())
         self._make_room(uk.numel(), protect=keys)
         slots = K.table_insert(uk, self.keys_g, nsub_log2=self.nsub_log2, cap_log2=self.cap_log2)
@@ -356,8 +377,10 @@ class KeyedRollingOperator:
         thr = torch.kthvalue(lg, need).values
         ev = valid & (lg <= thr) & (lg != I64_MAX)
         idx = torch.nonzero(ev).flatten()
-        self.store.add(self.keys_g[idx].cpu().numpy(), self.acc_g[idx].cpu().numpy(),
+        ek = self.keys_g[idx]
+        self.store.add(ek.cpu().numpy(), self.acc_g[idx].cpu().numpy(),
                        self.cnt_g[idx].cpu().numpy().astype(np.int64))
+        self._set_add(ek)
         keep = torch.nonzero(valid & ~ev).flatten()
         kk, ka = self.keys_g[keep].clone(), self.acc_g[keep].clone()
         kc, kl = self.cnt_g[keep].clone(), self.last_g[keep].clone()
@@ -374,6 +397,24 @@ class KeyedRollingOperator:
         self.live_keys = kk.numel()
         self.spill_stats["evictions"] += 1
         self.spill_stats["spilled_keys"] += idx.numel()
+
+    def _set_add(self, keys: torch.Tensor) -> None:
+        """GPU: add evicted keys to the device set (rebuilt from the store at twice its size,
+        dropping tombstones, when live + erased entries would pass half the capacity)."""
+        if self.device.type != "cuda" or not keys.numel():
+            return
+        m = load()
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        self._set_used += keys.numel()
+        if self._set is None or 2 * self._set_used > self._set.numel():
+            cap = 1 << max(16, int(4 * len(self.store)).bit_length())
+            self._set = torch.full((cap,), -1, dtype=torch.int64, device=self.device)
+            allk = self.store.keys_on(self.device)
+            m.gpu_set_insert(self._set.data_ptr(), cap - 1, allk.data_ptr(), allk.numel(), st)
+            self._set_used = allk.numel()
+            return
+        m.gpu_set_insert(self._set.data_ptr(), self._set.numel() - 1, keys.data_ptr(),
+                         keys.numel(), st)
 
     def host_bytes(self) -> int:
         return self.store.nbytes() if self.spill else 0
@@ -456,6 +497,8 @@ class KeyedRollingOperator:
                            np.ascontiguousarray(rows["acc"], dtype=np.int64),
                            np.ascontiguousarray(rows["cnt"], dtype=np.int64))
             self.live_keys = 0
+            self._set = None
+            self._set_add(self.store.keys_on(self.device))
             return
         dev = self.device
         keys = torch.from_numpy(np.ascontiguousarray(rows["key"])).to(dev)
@@ -476,22 +519,25 @@ class KeyedRollingOperator:
 class RollingSpillStore:
     """Host-DRAM tier of rolling keyed state: (key, acc, count) rows as sorted numpy columns.
     Evictions append (merged into the sorted columns lazily, when a lookup needs them);
-    promotions take keys out. `keys_on(device)` is the sorted key column on the device for the
-    batch membership test (cached until the store changes)."""
+    promotions mark rows dead (compacted once half the rows are dead), so a step's promotion
+    costs O(promoted keys), not O(store). `keys_on(device)` is the sorted live-key column on the
+    device (the CPU twin's membership test), cached until the store changes."""
 
     def __init__(self, device):
         self.device = torch.device(device)
         self._k = np.zeros(0, np.int64)
         self._a = np.zeros(0, np.int64)
         self._c = np.zeros(0, np.int64)
+        self._alive = np.zeros(0, bool)
+        self._dead = 0
         self._pending: list[tuple[np.ndarray, np.ndarray, np.ndarray]] = []
         self._dev = None
 
     def __len__(self) -> int:
-        return self._k.size + sum(p[0].size for p in self._pending)
+        return self._k.size - self._dead + sum(p[0].size for p in self._pending)
 
     def nbytes(self) -> int:
-        return 24 * len(self)
+        return 25 * (self._k.size + sum(p[0].size for p in self._pending))
 
     def clear(self) -> None:
         self.__init__(self.device)
@@ -503,41 +549,46 @@ class RollingSpillStore:
             self._dev = None
 
     def _merge(self) -> None:
-        if not self._pending:
+        if not self._pending and 2 * self._dead <= self._k.size:
             return
-        k = np.concatenate([self._k] + [p[0] for p in self._pending])
-        a = np.concatenate([self._a] + [p[1] for p in self._pending])
-        c = np.concatenate([self._c] + [p[2] for p in self._pending])
+        live = self._alive
+        k = np.concatenate([self._k[live]] + [p[0] for p in self._pending])
+        a = np.concatenate([self._a[live]] + [p[1] for p in self._pending])
+        c = np.concatenate([self._c[live]] + [p[2] for p in self._pending])
         o = np.argsort(k, kind="stable")
         self._k, self._a, self._c = k[o], a[o], c[o]
+        self._alive = np.ones(self._k.size, bool)
+        self._dead = 0
         self._pending = []
 
     def keys_on(self, device) -> torch.Tensor:
         self._merge()
         if self._dev is None:
-            self._dev = torch.from_numpy(self._k).to(device)
+            k = self._k if not self._dead else self._k[self._alive]
+            self._dev = torch.from_numpy(np.ascontiguousarray(k)).to(device)
         return self._dev
 
     def take(self, keys: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
-        """(acc, count) of `keys` (all present), removed from the store."""
+        """(acc, count) of `keys` (all present and alive), which leave the store."""
         self._merge()
         i = np.searchsorted(self._k, keys)
-        if keys.size and (i.max() >= self._k.size or not np.array_equal(self._k[i], keys)):
+        if keys.size and (i.max() >= self._k.size or not np.array_equal(self._k[i], keys)
+                          or not self._alive[i].all()):
             raise KeyError("rolling spill store: promoted key not present")
         a, c = self._a[i], self._c[i]
-        keep = np.ones(self._k.size, bool)
-        keep[i] = False
-        self._k, self._a, self._c = self._k[keep], self._a[keep], self._c[keep]
+        self._alive[i] = False
+        self._dead += keys.size
         self._dev = None
         return a, c
 
     def get(self, key: int):
         self._merge()
         i = int(np.searchsorted(self._k, key))
-        if i < self._k.size and self._k[i] == key:
+        if i < self._k.size and self._k[i] == key and self._alive[i]:
             return int(self._a[i]), int(self._c[i])
         return None
 
     def rows(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
         self._merge()
-        return self._k.copy(), self._a.copy(), self._c.copy()
+        live = self._alive
+        return self._k[live].copy(), self._a[live].copy(), self._c[live].copy()
