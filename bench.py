@@ -160,8 +160,14 @@ def main() -> int:
     # untimed steps until `--latency-firings` firings were observed.
     timed_firings = len(bench.latencies_ms)
     lat_steps = 0
-    while a.latency_firings > 0 and len(bench.latencies_ms) < a.latency_firings \
-            and lat_steps < 40 * a.latency_firings:
+    # Every rank runs the same number of extra steps (they are collective): the stop decision
+    # takes the smallest firing count over the ranks.
+    have = torch.zeros(1, dtype=torch.int64, device=device)
+    while a.latency_firings > 0 and lat_steps < 40 * a.latency_firings:
+        have.fill_(len(bench.latencies_ms))
+        comm.allreduce_min_(have)
+        if int(have.item()) >= a.latency_firings:
+            break
         bench.step()
         lat_steps += 1
     bench.drain()

@@ -722,6 +722,12 @@ class KeyedSessionOperator:
                             rows[3].data_ptr(), rows[4].data_ptr(), rows[5].data_ptr(),
                             c[7:8].data_ptr(), R, c[8:9].data_ptr(), st)
         self.spill_any = True
+        if slots is None and self.gpu:
+            # Idle eviction without a host round trip: the rows' count stays on the device, a
+            # counted copy on a side stream moves just those rows to pinned memory, and the
+            # worker applies the counts when it is joined.
+            self._evict_async(rows, R)
+            return
         with self._phase("spill.evict_kernel"):
             nr_all, ne = self.ctr[7:9].cpu().tolist()
         self._live_estimate -= ne
@@ -782,6 +788,41 @@ class KeyedSessionOperator:
         self._spill_thread = threading.Thread(target=work, name="mxs-spill", daemon=True)
         self._spill_thread.start()
 
+    def _evict_async(self, rows: torch.Tensor, R: int) -> None:
+        from .window_operator import CountedHostRows, PinnedSlabPool
+
+        if getattr(self, "_spill_pool", None) is None:
+            self._spill_pool = PinnedSlabPool(max_slabs=2)
+            self._spill_stream = torch.cuda.Stream(self.device)
+        hr = CountedHostRows(self._spill_pool, [rows[j] for j in range(6)], self.ctr[7:8],
+                             [self.ctr], copy_stream=self._spill_stream)
+        self._spill_err = None
+        self._spill_res = None
+
+        def work():
+            try:
+                t0 = time.perf_counter()
+                hr.ev.synchronize()
+                f = hr.fixed(0)
+                nr_all, ne = int(f[7]), int(f[8])
+                nr = min(nr_all, R)
+                h = hr.columns(nr)
+                if nr_all > R:  # staging overflowed: rows of skipped slots stay zero (cnt == 0)
+                    ok = h[4] > 0
+                    h = [np.ascontiguousarray(x[ok]) for x in h]
+                t1 = time.perf_counter()
+                self.phase_s["spill.d2h_wait"] += t1 - t0
+                nk = int(np.count_nonzero(h[0][1:] != h[0][:-1])) + 1 if len(h[0]) else 0
+                if len(h[0]):
+                    self.store.insert(h[0], h[1], h[2], h[3], h[4], h[5], True)
+                self.phase_s["spill.host_insert"] += time.perf_counter() - t1
+                self._spill_res = (nr, ne, nk)
+            except BaseException as e:  # re-raised by _join_spill
+                self._spill_err = e
+
+        self._spill_thread = threading.Thread(target=work, name="mxs-spill", daemon=True)
+        self._spill_thread.start()
+
     def _apply_spill(self, res: tuple[int, int]) -> None:
         nk, ne = res
         self.set_used += nk
@@ -797,6 +838,15 @@ class KeyedSessionOperator:
         self._spill_thread = None
         if self._spill_err is not None:
             raise self._spill_err
+        res = getattr(self, "_spill_res", None)
+        if res is not None:  # counts of an asynchronous idle eviction
+            self._spill_res = None
+            nr, ne, nk = res
+            self._live_estimate -= ne
+            self._tombs_bound += ne
+            self.set_used += nr
+            self.metrics.freed_slots += ne
+            self.metrics.spilled_keys += nk
 
     def _ensure_spill_capacity(self, extra: int) -> None:
         """Keep the device spill set (live keys + tombstones) at most half full after `extra`
