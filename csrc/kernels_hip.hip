@@ -2585,6 +2585,38 @@ __device__ __forceinline__ uint32_t sess_probe_insert(uint64_t* keys, uint64_t k
   }
 }
 
+// sess_probe_insert reporting whether THIS call claimed the slot for the key.
+template <int kScope = __HIP_MEMORY_SCOPE_AGENT>
+__device__ __forceinline__ uint32_t sess_probe_claim(uint64_t* keys, uint64_t key, uint32_t mask,
+                                                     bool* claimed) {
+  const uint32_t s0 = slot_hash(key) & mask;
+  for (;;) {
+    uint32_t s = s0, tomb = kNoSlot, target = kNoSlot;
+    for (uint32_t i = 0; i <= mask; ++i) {
+      const uint64_t k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, kScope);
+      if (k == key) return s;
+      if (k == kTombKey) {
+        if (tomb == kNoSlot) tomb = s;
+      } else if (k == kEmptyKey) {
+        target = s;
+        break;
+      }
+      s = (s + 1) & mask;
+    }
+    const bool use_tomb = tomb != kNoSlot;
+    if (use_tomb) target = tomb;
+    if (target == kNoSlot) return kNoSlot;
+    const uint64_t expect = use_tomb ? kTombKey : kEmptyKey;
+    const uint64_t prev = atomicCAS((unsigned long long*)&keys[target], (unsigned long long)expect,
+                                    (unsigned long long)key);
+    if (prev == expect) {
+      *claimed = true;
+      return target;
+    }
+    if (prev == key) return target;
+  }
+}
+
 // Read-only probe: the key's slot, or kNoSlot (first empty slot reached / table scanned).
 template <int kScope = __HIP_MEMORY_SCOPE_AGENT>
 __device__ __forceinline__ uint32_t sess_find(const uint64_t* keys, uint64_t key, uint32_t mask) {
@@ -2759,7 +2791,10 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
   uint16_t* idxl = cur + cap;                                          // phase 2: slot segments
   uint64_t* rk = slds + regA / 8;                                      // (slot << 32 | t) per record
   uint64_t* gkeys = keys_g + ((size_t)sub << cap_log2);
+  // per slot, 2 bits: key claimed this step (1 resident, 2 spilled); 1 KB of static LDS
+  __shared__ uint32_t sflag[(1u << kSessLookupLdsMaxLog2) / 16];
   for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) lkeys[i] = gkeys[i];
+  for (uint32_t i = threadIdx.x; i < (cap + 15) / 16; i += blockDim.x) sflag[i] = 0;
   if (threadIdx.x == 0) {
     uint32_t tot = 0;
     for (int src = 0; src < nsrc; ++src) {
@@ -2784,26 +2819,28 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
     while (src + 1 < nsrc && i >= s_src_off[src + 1]) ++src;
     return recs[(size_t)(src * nsub + sub) * bucket_cap + (i - s_src_off[src])];
   };
+  // 1a: insert-or-find every record's key in the LDS table. Only the thread that claims a slot
+  //     for a key new to the table probes the device spill set (once per key instead of once per
+  //     record of every key still missing: those global probes made the kernel latency-bound)
+  //     and flags the slot: 1 resident, 2 spilled (records go to the host tier), 3 table full.
   auto lookup = [&](uint32_t i) -> uint64_t {
     const Rec r = rec_at(i);
     uint64_t v = ~0ull;
     if (r.t != 0xFFFFFFFFu) {
       uint32_t sl = sess_find<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask);
-      bool to_host = sl == kNoSlot && spill_any && set_contains(spill_set, spill_mask, r.key);
-      if (!to_host && sl == kNoSlot) {
-        sl = sess_probe_insert<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask, &s_lins);
+      if (sl == kNoSlot) {
+        bool claimed = false;
+        sl = sess_probe_claim<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask, &claimed);
         if (sl == kNoSlot) {  // sub-table full: the key lives in host DRAM from now on
-          to_host = true;
           set_insert(spill_set, spill_mask, r.key);
+          const uint32_t q = atomicAdd(n_host, 1u);
+          if (q < host_cap) host_recs[q] = r;
+        } else if (claimed) {
+          const uint32_t f = (spill_any && set_contains(spill_set, spill_mask, r.key)) ? 2u : 1u;
+          atomicOr(&sflag[sl >> 4], f << ((sl & 15u) * 2));
         }
       }
-      if (to_host) {
-        const uint32_t q = atomicAdd(n_host, 1u);
-        if (q < host_cap) host_recs[q] = r;
-      } else {
-        v = ((uint64_t)sl << 32) | r.t;
-        ++kept;
-      }
+      if (sl != kNoSlot) v = ((uint64_t)sl << 32) | r.t;
     }
     rk[i] = v;
     return r.val;
@@ -2815,9 +2852,32 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
     vreg[k] = i < m ? lookup(i) : 0ull;
   }
   for (uint32_t i = kLsRegs * kSessSortBlock + threadIdx.x; i < m; i += kSessSortBlock) lookup(i);
+  __syncthreads();
+  // 1b: records of keys found in the spill set go to the host tier; the rest are kept.
+  for (uint32_t i = threadIdx.x; i < m; i += kSessSortBlock) {
+    const uint64_t v = rk[i];
+    if (v == ~0ull) continue;
+    const uint32_t sl = (uint32_t)(v >> 32);
+    if (((sflag[sl >> 4] >> ((sl & 15u) * 2)) & 3u) == 2u) {
+      const uint32_t q = atomicAdd(n_host, 1u);
+      if (q < host_cap) host_recs[q] = rec_at(i);
+      rk[i] = ~0ull;
+    } else {
+      ++kept;
+    }
+  }
   if (kept) atomicAdd(&s_kept, kept);
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) gkeys[i] = lkeys[i];
+  // Spilled keys leave the table again (tombstones, reusable); new resident keys are counted.
+  uint32_t ins = 0;
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
+    const uint32_t f = (sflag[i >> 4] >> ((i & 15u) * 2)) & 3u;
+    if (f == 2) lkeys[i] = kTombKey;
+    ins += f == 1;
+    gkeys[i] = f == 2 ? kTombKey : lkeys[i];
+  }
+  if (ins) atomicAdd(&s_lins, ins);
+  __syncthreads();
   if (threadIdx.x == 0) {
     if (n_inserted && s_lins) atomicAdd(n_inserted, s_lins);
     s_base = s_kept ? atomicAdd(n_out, s_kept) : 0u;
@@ -3500,20 +3560,32 @@ __global__ __launch_bounds__(256) void session_rehash_kernel(
     const int64_t* __restrict__ due_o, const int64_t* __restrict__ last_o,
     uint64_t* __restrict__ keys_n, SessRec* __restrict__ sess_n, int64_t* __restrict__ due_n,
     int64_t* __restrict__ last_n, uint32_t* __restrict__ inserted) {
+  // Inserted keys are counted per workgroup (a device-scope atomic per key on one counter
+  // serialised across the XCDs: 7.4 ms for 5.5M keys).
+  __shared__ uint32_t s_ins;
+  if (threadIdx.x == 0) s_ins = 0;
+  __syncthreads();
   const uint32_t mask = (1u << a.cap_log2) - 1;
+  uint32_t ins = 0;
   for (int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; slot < a.nslots;
        slot += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t key = keys_o[slot];
     if (key == kEmptyKey || key == kTombKey) continue;
     const int64_t sub = slot >> a.cap_log2;
     uint64_t* keys = keys_n + (sub << a.cap_log2);
-    const uint32_t s = sess_probe_insert(keys, key, mask, inserted);
+    bool claimed = false;
+    const uint32_t s = sess_probe_claim(keys, key, mask, &claimed);
+    ins += claimed;
     const int64_t ns = (sub << a.cap_log2) | s;  // never kNoSlot: the old table held the key
 #pragma unroll
     for (int j = 0; j < kSess; ++j) sess_n[ns * kSess + j] = sess_o[slot * kSess + j];
     due_n[ns] = due_o[slot];
     last_n[ns] = last_o[slot];
   }
+  for (int d = 32; d >= 1; d >>= 1) ins += __shfl_xor(ins, d);
+  if (lane_id() == 0 && ins) atomicAdd(&s_ins, ins);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_ins && inserted) atomicAdd(inserted, s_ins);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -4591,10 +4663,10 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
   if (nsrc > 64 || cap_log2 > kSessLookupLdsMaxLog2 || m64 > 65535) return false;
   const uint32_t m_cap = ((uint32_t)m64 + 7) & ~7u;
   const size_t lds = session_lookup_sort_lds(cap_log2, m_cap);
-  if (lds > 156 * 1024) return false;  // static LDS (offsets, counters) takes the rest
+  if (lds > 156 * 1024) return false;  // static LDS (slot flags, offsets, counters) takes the rest
   static bool attr = false;
   if (!attr) {
-    // dynamic + the kernel's static LDS (segment offsets, scan scratch) must stay <= 160 KiB
+    // dynamic + the kernel's static LDS (slot flags, segment offsets, scan scratch) <= 160 KiB
     HIP_CHECK(hipFuncSetAttribute((const void*)session_lookup_sort_kernel,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024));
     attr = true;

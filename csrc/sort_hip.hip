@@ -140,7 +140,6 @@ __global__ __launch_bounds__(kSortBlock) void radix_scatter_kernel(
     uint64_t* __restrict__ kout, uint64_t* __restrict__ vout, uint32_t n, int shift, int nb,
     const uint32_t* __restrict__ hist, uint32_t ntiles, const uint32_t* __restrict__ totals) {
   __shared__ uint64_t buf[kTile];                 // keys, then values, in tile-sorted order
-  __shared__ uint8_t sdig[kTile];                 // digit of every sorted position
   __shared__ uint32_t wcnt[kSortWaves][kBins];    // per-wave running digit counts -> offsets
   __shared__ uint32_t gbase[kBins];               // global position of tile-local position 0
   __shared__ uint32_t tstart[kBins];              // tile-local start of every digit
@@ -204,13 +203,25 @@ __global__ __launch_bounds__(kSortBlock) void radix_scatter_kernel(
     if (i < n) {
       const uint32_t p = tstart[dg[j]] + wcnt[w][dg[j]] + pos[j];
       buf[p] = k[j];
-      sdig[p] = dg[j];
       pos[j] = (uint16_t)p;
     }
   }
   __syncthreads();
+  // Sorted positions q = t + 256 * r leave in order; each thread keeps its positions' global
+  // destinations for the value pass (registers instead of a per-position digit array in LDS:
+  // 4 KB less LDS, one more workgroup per CU).
   const uint32_t m = n - tile0 < (uint32_t)kTile ? n - tile0 : (uint32_t)kTile;
-  for (uint32_t q = t; q < m; q += kSortBlock) kout[gbase[sdig[q]] + q] = buf[q];
+  uint32_t dst[kItems];
+#pragma unroll
+  for (int r = 0; r < kItems; ++r) {
+    const uint32_t q = t + r * kSortBlock;
+    dst[r] = 0;
+    if (q < m) {
+      const uint64_t key = buf[q];
+      dst[r] = gbase[(uint32_t)(key >> shift) & mask] + q;
+      kout[dst[r]] = key;
+    }
+  }
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < kItems; ++j) {
@@ -218,7 +229,11 @@ __global__ __launch_bounds__(kSortBlock) void radix_scatter_kernel(
     if (i < n) buf[pos[j]] = vin[i];
   }
   __syncthreads();
-  for (uint32_t q = t; q < m; q += kSortBlock) vout[gbase[sdig[q]] + q] = buf[q];
+#pragma unroll
+  for (int r = 0; r < kItems; ++r) {
+    const uint32_t q = t + r * kSortBlock;
+    if (q < m) vout[dst[r]] = buf[q];
+  }
 }
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }

@@ -906,13 +906,20 @@ class KeyedSessionOperator:
     def _maybe_spill(self, wm: int) -> None:
         # Live keys come from the kernels' insert / evict counters; the table is scanned only
         # after a restore and when the tombstone bound suggests a rehash.
+        # Rehash (drop tombstones) once live + tombstones pass 0.8 of the slots with at least 8 %
+        # tombstones: evicted keys leave tombstones that new keys only partly reuse, and the
+        # LDS probes of the fold (a missing key scans to the first empty slot) grow with the
+        # occupied fraction, not with the live one.
+        def due(live, occupied):
+            return occupied > 0.8 * self.nslots and occupied - live > 0.08 * self.nslots
+
         if self._occ_exact:
             live, occupied = self._count_occupancy()
         else:
             live, occupied = self._live_estimate, self._live_estimate + self._tombs_bound
-            if occupied > 0.85 * self.nslots and live < 0.6 * self.nslots:
+            if due(live, occupied):
                 live, occupied = self._count_occupancy()
-        if occupied > 0.85 * self.nslots and live < 0.6 * self.nslots:
+        if due(live, occupied):
             self._rehash()
             self._tombs_bound = 0
         if live > self.max_load * self.nslots and wm > I64_MIN:
