@@ -186,9 +186,11 @@ class KeyedSessionOperator:
             # Occupancy bookkeeping from the kernels' own counters (no table scan per step):
             # live keys = inserted - evicted (exact); occupied = live + tombstones, where the
             # tombstone count is an upper bound (an insert may reuse one) -- a rehash decision
-            # re-counts exactly first. _occ_exact: the next check scans the table.
+            # takes exact counts (launched without a host wait, read a step later). _occ_exact:
+            # the next check scans the table.
             self._tombs_bound = 0
             self._occ_exact = True
+            self._occ_pending = None  # event of an in-flight occupancy count (_occ_launch)
             # Fired rows: the device-counted copy into a pinned slab (one wait per firing);
             # more rows than the slab column holds take the synchronous copy.
             from .window_operator import PinnedSlabPool
@@ -883,6 +885,7 @@ class KeyedSessionOperator:
         self.phase_s["spill.set_rebuild"] += time.perf_counter() - t0
 
     def _rehash(self) -> None:
+        self._occ_pending = None  # counts of the old table
         m, st = self.native, self._st()
         old = (self.keys_g, self.sess, self.slot_due, self.slot_last)
         self._alloc_state()
@@ -903,6 +906,25 @@ class KeyedSessionOperator:
         self._occ_exact = False
         return int(live), int(occupied)
 
+    def _occ_launch(self) -> None:
+        k = self.keys_g
+        if getattr(self, "_occ_pin", None) is None:
+            self._occ_pin = torch.zeros(2, dtype=torch.int64, pin_memory=True)
+        c = torch.stack([((k != EMPTY_KEY) & (k != TOMB_KEY)).sum(), (k != EMPTY_KEY).sum()])
+        self._occ_pin.copy_(c, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._occ_pending = ev
+
+    def _occ_poll(self):
+        """(live, occupied) of a count launched earlier, once it has landed (else None)."""
+        ev = self._occ_pending
+        if ev is None or not ev.query():
+            return None
+        self._occ_pending = None
+        live, occupied = self._occ_pin.tolist()
+        return int(live), int(occupied)
+
     def _maybe_spill(self, wm: int) -> None:
         # Live keys come from the kernels' insert / evict counters; the table is scanned only
         # after a restore and when the tombstone bound suggests a rehash.
@@ -915,13 +937,20 @@ class KeyedSessionOperator:
 
         if self._occ_exact:
             live, occupied = self._count_occupancy()
-        else:
-            live, occupied = self._live_estimate, self._live_estimate + self._tombs_bound
             if due(live, occupied):
-                live, occupied = self._count_occupancy()
-        if due(live, occupied):
-            self._rehash()
-            self._tombs_bound = 0
+                self._rehash()
+                self._tombs_bound = 0
+        else:
+            # The tombstone bound only grows (new keys reuse tombstones unseen), so the exact
+            # counts are taken without a host wait: launched when the bound suggests a rehash and
+            # read at a later step once they have landed (a one-step-late rehash decision).
+            live = self._live_estimate
+            stale = self._occ_poll()
+            if stale is not None and due(*stale):
+                self._rehash()
+                self._tombs_bound = 0
+            elif due(live, live + self._tombs_bound) and self._occ_pending is None:
+                self._occ_launch()
         if live > self.max_load * self.nslots and wm > I64_MIN:
             # LRU by last event time: keys idle for idle_spill_ms move to host DRAM (keys with no
             # live session are simply freed).
