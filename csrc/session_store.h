@@ -347,7 +347,8 @@ class SessionCore {
     std::vector<int64_t> okey, ostart, oend, oraw, ocnt, oref, released;
     std::vector<double> oval;
   };
-  void fire(int64_t wm, const ExprProg& mp, const ExprProg& fp, FireOut& o) {
+  void fire(int64_t wm, const ExprProg& mp, const ExprProg& fp, FireOut& o,
+            bool expire_cold = true) {
     auto& okey = o.okey;
     auto& ostart = o.ostart;
     auto& oend = o.oend;
@@ -400,7 +401,13 @@ class SessionCore {
     for (uint64_t key : pending_released_)
       if (m_.find(key) == m_.end()) released.push_back((int64_t)key);
     pending_released_.clear();
-    // Cold chunks: dropped as a whole once every row is past cleanup.
+    if (expire_cold) this->expire_cold(wm, released);
+  }
+
+  // Cold chunks: dropped as a whole once every row is past cleanup at `wm`; their keys without
+  // hot sessions leave the store (appended to `released`). Emits no rows, so the GPU operator
+  // runs it on its spill worker, off the step's critical path.
+  void expire_cold(int64_t wm, std::vector<int64_t>& released) {
     for (auto it = cold_.begin(); it != cold_.end();) {
       if (it->max_due <= wm) {
         // (a key whose cold row expires leaves unless it also has hot sessions; with no hot keys

@@ -129,10 +129,10 @@ class SessionStore : public sess::SessionCore {
   // Fire / clean up everything the watermark allows. Returns columns of emitted rows plus the
   // keys that left the store ("released").
   py::dict fire_np(int64_t wm, std::vector<int32_t> map_code, std::vector<double> map_consts,
-                   std::vector<int32_t> f_code, std::vector<double> f_consts) {
+                   std::vector<int32_t> f_code, std::vector<double> f_consts, bool expire) {
     FireOut o;
     fire(wm, prog(map_code.data(), map_code.size(), map_consts.data(), map_consts.size()),
-         prog(f_code.data(), f_code.size(), f_consts.data(), f_consts.size()), o);
+         prog(f_code.data(), f_code.size(), f_consts.data(), f_consts.size()), o, expire);
     py::dict d;
     d["keys"] = to_np(o.okey);
     d["start"] = to_np(o.ostart);
@@ -143,6 +143,15 @@ class SessionStore : public sess::SessionCore {
     d["refire"] = to_np(o.oref);
     d["released"] = to_np(o.released);
     return d;
+  }
+  // Cold-chunk expiry alone (GIL released: the GPU operator's spill worker runs it).
+  py::array_t<int64_t> expire_cold_np(int64_t wm) {
+    std::vector<int64_t> rel;
+    {
+      py::gil_scoped_release nogil;
+      expire_cold(wm, rel);
+    }
+    return to_np(rel);
   }
   py::array_t<int64_t> spill_set_np(int cap_log2) const {
     py::array_t<int64_t> out((py::ssize_t)1 << cap_log2);
@@ -169,7 +178,10 @@ void bind_sessions(py::module_& m) {
       .def("merge_runs", &SessionStore::merge_runs_np)
       .def("extract", &SessionStore::extract_np)
       .def("extract_packed", &SessionStore::extract_packed_np)
-      .def("fire", &SessionStore::fire_np)
+      .def("fire", &SessionStore::fire_np, py::arg("wm"), py::arg("map_code"),
+           py::arg("map_consts"), py::arg("f_code"), py::arg("f_consts"),
+           py::arg("expire_cold") = true)
+      .def("expire_cold", &SessionStore::expire_cold_np)
       .def("spill_set", &SessionStore::spill_set_np)
       .def("contains", &SessionStore::contains)
       .def("num_keys", &SessionStore::num_keys)

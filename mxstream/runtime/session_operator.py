@@ -415,7 +415,12 @@ class KeyedSessionOperator:
     def _fire_host(self, wm: int) -> SessionRows:
         mc, mk = self.map_prog.as_args()
         fc, fk = self.filter_prog.as_args()
-        d = self.store.fire(wm, mc, mk, fc, fk)
+        # GPU: cold-chunk expiry (no rows, only released keys) runs on the spill worker after
+        # its insert, except at end of input.
+        defer = self.gpu and wm != I64_MAX
+        d = self.store.fire(wm, mc, mk, fc, fk, not defer)
+        if defer:
+            self._expire_wm = wm
         rel = d["released"]
         if self.gpu and len(rel) and self.spill_any:
             # Keys that left the host store leave the device spill set (tombstoned).
@@ -728,7 +733,7 @@ class KeyedSessionOperator:
             # Idle eviction without a host round trip: the rows' count stays on the device, a
             # counted copy on a side stream moves just those rows to pinned memory, and the
             # worker applies the counts when it is joined.
-            self._evict_async(rows, R)
+            self._evict_async(rows, R, getattr(self, "_expire_wm", None))
             return
         with self._phase("spill.evict_kernel"):
             nr_all, ne = self.ctr[7:9].cpu().tolist()
@@ -790,7 +795,7 @@ class KeyedSessionOperator:
         self._spill_thread = threading.Thread(target=work, name="mxs-spill", daemon=True)
         self._spill_thread.start()
 
-    def _evict_async(self, rows: torch.Tensor, R: int) -> None:
+    def _evict_async(self, rows: torch.Tensor, R: int, expire_wm: int | None = None) -> None:
         from .window_operator import CountedHostRows, PinnedSlabPool
 
         if getattr(self, "_spill_pool", None) is None:
@@ -817,8 +822,10 @@ class KeyedSessionOperator:
                 nk = int(np.count_nonzero(h[0][1:] != h[0][:-1])) + 1 if len(h[0]) else 0
                 if len(h[0]):
                     self.store.insert(h[0], h[1], h[2], h[3], h[4], h[5], True)
+                # keys of expired cold chunks leave the device spill set at the join
+                rel = self.store.expire_cold(expire_wm) if expire_wm is not None else None
                 self.phase_s["spill.host_insert"] += time.perf_counter() - t1
-                self._spill_res = (nr, ne, nk)
+                self._spill_res = (nr, ne, nk, rel)
             except BaseException as e:  # re-raised by _join_spill
                 self._spill_err = e
 
@@ -843,7 +850,11 @@ class KeyedSessionOperator:
         res = getattr(self, "_spill_res", None)
         if res is not None:  # counts of an asynchronous idle eviction
             self._spill_res = None
-            nr, ne, nk = res
+            nr, ne, nk, rel = res
+            if rel is not None and len(rel) and self.spill_any:
+                kt = torch.from_numpy(rel).to(self.device)
+                self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
+                                          kt.data_ptr(), kt.numel(), self._st())
             self._live_estimate -= ne
             self._tombs_bound += ne
             self.set_used += nr
