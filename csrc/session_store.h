@@ -156,6 +156,7 @@ class SessionCore {
   // fired-and-unmodified sessions of keys without hot state go to one new cold chunk.
   void insert(const int64_t* K, const int64_t* S, const int64_t* E, const int64_t* A,
               const int64_t* C, const int64_t* F, int64_t n, bool cold) {
+    refresh_hot_filter();
     ColdChunk ch;
     if (cold && !spare_.empty()) {
       // A dropped chunk's columns: capacity whose pages are already mapped. Fresh columns of a
@@ -176,7 +177,7 @@ class SessionCore {
     int64_t nc = 0, emax = INT64_MIN;
     for (int64_t i = 0; i < n; ++i) {
       const uint64_t key = (uint64_t)K[i];
-      if (cold && F[i] == 1 && (no_hot || m_.find(key) == m_.end())) {
+      if (cold && F[i] == 1 && (no_hot || !is_hot(key))) {
         ch.key[nc] = key;
         ch.start[nc] = S[i];
         ch.end[nc] = E[i];
@@ -187,6 +188,7 @@ class SessionCore {
         continue;
       }
       m_[key].push_back(Session{S[i], E[i], (uint64_t)A[i], (uint32_t)C[i], (uint32_t)F[i]});
+      mark_hot(key);
       schedule(key);
     }
     if (cold) {
@@ -324,6 +326,7 @@ class SessionCore {
       const int64_t nhot = it == m_.end() ? 0 : (int64_t)it->second.size();
       if (nhot + (int64_t)(c - cb) > max_sess) {  // stays on the host: cold rows turn hot
         auto& vec = m_[key];
+        mark_hot(key);
         for (size_t q = cb; q < c; ++q) vec.push_back(cold[q].second);
         schedule(key);
         continue;
@@ -415,7 +418,7 @@ class SessionCore {
         released.reserve(released.size() + it->key.size());
         const bool no_hot = m_.empty();
         for (size_t r = 0; r < it->key.size(); ++r)
-          if (it->cnt[r] && (no_hot || m_.find(it->key[r]) == m_.end()))
+          if (it->cnt[r] && (no_hot || !is_hot(it->key[r])))
             released.push_back((int64_t)it->key[r]);
         cold_rows_ -= it->live;
         if (spare_.size() < 4) {  // keep the columns' memory for the next eviction's chunk
@@ -533,6 +536,7 @@ class SessionCore {
       if (!ch.cnt[r]) return;
       if (cleanup_time(ch.end[r] - 1) > wm) {
         m_[ch.key[r]].push_back(Session{ch.start[r], ch.end[r], ch.acc[r], ch.cnt[r], 1u});
+        mark_hot(ch.key[r]);
         schedule(ch.key[r]);
       } else {
         pending_released_.push_back(ch.key[r]);  // reported by fire() unless it turns hot
@@ -596,7 +600,10 @@ class SessionCore {
     // A fired session that grows (or a new session already past its end within lateness)
     // fires again at the next fire() with the watermark (EventTimeTrigger.onElement).
     if (merged.flags & 1u) merged.flags |= 2u;
-    if (found == m_.end()) found = m_.emplace(key, Hot()).first;
+    if (found == m_.end()) {
+      found = m_.emplace(key, Hot()).first;
+      mark_hot(key);
+    }
     found->second.push_back(merged);
     schedule(key);
     return 0;
@@ -624,6 +631,30 @@ class SessionCore {
     int64_t due = INT64_MAX;
   };
   std::unordered_map<uint64_t, Hot> m_;
+  // "May be hot" filter over the hot map's keys (one bit per mix64 bucket, set on every hot
+  // insert, never cleared; rebuilt when mostly stale): eviction inserts and cold-chunk expiry
+  // ask it before probing m_, so the common cold key costs one bit test instead of a hash-map
+  // miss.
+  static constexpr int kHotBits = 24;
+  std::vector<uint64_t> hot_filter_ = std::vector<uint64_t>((size_t)1 << (kHotBits - 6), 0);
+  size_t hot_marks_ = 0;
+  void mark_hot(uint64_t key) {
+    const uint64_t b = mix64(key) >> (64 - kHotBits);
+    hot_filter_[b >> 6] |= 1ull << (b & 63);
+    ++hot_marks_;
+  }
+  bool is_hot(uint64_t key) const {
+    if (m_.empty()) return false;
+    const uint64_t b = mix64(key) >> (64 - kHotBits);
+    if (!((hot_filter_[b >> 6] >> (b & 63)) & 1ull)) return false;
+    return m_.find(key) != m_.end();
+  }
+  void refresh_hot_filter() {
+    if (hot_marks_ < ((size_t)1 << 20) || hot_marks_ < 4 * m_.size()) return;
+    std::fill(hot_filter_.begin(), hot_filter_.end(), 0ull);
+    hot_marks_ = 0;
+    for (const auto& kv : m_) mark_hot(kv.first);
+  }
   std::priority_queue<std::pair<int64_t, uint64_t>, std::vector<std::pair<int64_t, uint64_t>>,
                       std::greater<>>
       heap_;

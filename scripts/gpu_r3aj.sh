@@ -8,6 +8,7 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -1 gpurun_out/r3aj_tests.log
 timeout -k 10 300 python -m mxstream.models.bench_configs --config 5 --steps 20 --warmup 10 > gpurun_out/r3aj_cfg5.log 2>&1 || { tail -20 gpurun_out/r3aj_cfg5.log; exit 1; }
 tail -1 gpurun_out/r3aj_cfg5.log
+timeout -k 10 300 python -m mxstream.models.bench_configs --config 5 --steps 20 --warmup 10 > gpurun_out/r3aj_cfg5b.log 2>&1 && tail -1 gpurun_out/r3aj_cfg5b.log
 timeout -k 10 300 python -m mxstream.models.bench_configs --config 5 --revisit 0.01 --steps 20 --warmup 14 > gpurun_out/r3aj_cfg5r.log 2>&1 || { tail -20 gpurun_out/r3aj_cfg5r.log; exit 1; }
 tail -1 gpurun_out/r3aj_cfg5r.log
 cd /tmp && export TMPDIR=/tmp
