@@ -19,6 +19,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <string>
 #include <thread>
@@ -28,6 +29,7 @@
 #include "session_store.h"
 #include "socket_reader.h"
 #include "text_ring.h"
+#include "window_tier.h"
 
 using namespace mxs;
 
@@ -248,7 +250,42 @@ static int test_kg_writers() {
   return 0;
 }
 
+// The host window tier's threaded firing: radix-partitioned merge (threads scatter rows into
+// partition buffers, then aggregate partitions) and the threaded epilogue, checked against the
+// single-threaded sums.
+static int test_window_tier_threads() {
+  mxs::WindowTierCore t(mxs::AGG_SUM_I64);
+  const size_t n = 300000;
+  std::vector<uint64_t> key(n);
+  std::vector<int64_t> pane(n), acc(n), cnt(n, 1);
+  std::vector<uint8_t> dirty(n, 0);
+  int64_t expect = 0;
+  for (size_t i = 0; i < n; ++i) {
+    key[i] = (i * 2654435761u) % 90000;
+    pane[i] = (int64_t)(i % 6);
+    acc[i] = (int64_t)(i % 97);
+    if (pane[i] >= 1 && pane[i] <= 4) expect += acc[i];
+  }
+  t.absorb(key.data(), pane.data(), acc.data(), cnt.data(), dirty.data(), n / 2);
+  t.absorb(key.data() + n / 2, pane.data() + n / 2, acc.data() + n / 2, cnt.data() + n / 2,
+           dirty.data() + n / 2, n - n / 2);
+  std::vector<uint64_t> dk(1000), k, ok;
+  std::vector<int64_t> da(1000, 1), dc(1000, 1), a, c, oraw;
+  std::vector<double> ov;
+  std::vector<int32_t> oc;
+  for (size_t i = 0; i < dk.size(); ++i) dk[i] = 100000 + i;  // keys only the device holds
+  t.merge_fire(1, 4, dk.data(), da.data(), dc.data(), dk.size(), false, &k, &a, &c);
+  mxs::ExprProg none;
+  std::memset(&none, 0, sizeof(none));
+  t.epilogue(k, a, c, none, none, 0, 1, &ok, &ov, &oraw, &oc);
+  int64_t got = 0;
+  for (int64_t x : oraw) got += x;
+  if (got != expect + (int64_t)dk.size()) return fail("window tier: threaded merge sum");
+  return 0;
+}
+
 int main() {
+  if (int rc = test_window_tier_threads()) return rc;
   if (int rc = test_text_ring()) return rc;
   if (int rc = test_socket()) return rc;
   if (int rc = test_session_spill_worker()) return rc;
