@@ -25,7 +25,17 @@ class WindowTierCore {
     std::vector<uint64_t> key;
     std::vector<int64_t> pane, acc, cnt;
     std::vector<uint8_t> dirty;
+    // Lazy purge: rows of panes < live_from are dead (skipped by every reader) until they are
+    // half the chunk, then the chunk is filtered. pane_rows[p - pmin] = rows of pane p.
+    int64_t live_from = INT64_MIN;
+    size_t dead = 0;
+    std::vector<size_t> pane_rows;
     size_t size() const { return key.size(); }
+    bool live(size_t i) const { return pane[i] >= live_from; }
+    void count_panes() {
+      pane_rows.assign(size() ? (size_t)(pmax - pmin + 1) : 0, 0);
+      for (int64_t p : pane) ++pane_rows[(size_t)(p - pmin)];
+    }
   };
   struct Rows {
     std::vector<uint64_t> key;
@@ -46,7 +56,13 @@ class WindowTierCore {
     *lo = INT64_MAX;
     *hi = INT64_MIN;
     for (auto& c : chunks_) {
-      *lo = std::min(*lo, c.pmin);
+      int64_t first = c.pmin;  // lowest live pane (dead rows of a lazy purge excluded)
+      if (c.live_from > first) {
+        first = c.live_from;
+        if (!c.pane_rows.empty())
+          while (first < c.pmax && !c.pane_rows[(size_t)(first - c.pmin)]) ++first;
+      }
+      *lo = std::min(*lo, first);
       *hi = std::max(*hi, c.pmax);
     }
     return true;
@@ -65,6 +81,7 @@ class WindowTierCore {
       c.pmin = std::min(c.pmin, pane[i]);
       c.pmax = std::max(c.pmax, pane[i]);
     }
+    if ((uint64_t)(c.pmax - c.pmin) < ((uint64_t)1 << 20)) c.count_panes();
     rows_ += n;
     rows_in_ += (int64_t)n;
     chunks_.push_back(std::move(c));
@@ -89,7 +106,7 @@ class WindowTierCore {
     for (auto& c : chunks_) {
       if (c.pmax < p0 || c.pmin > p1) continue;
       for (size_t i = 0; i < c.size(); ++i) {
-        if (c.pane[i] < p0 || c.pane[i] > p1 || !c.cnt[i]) continue;
+        if (c.pane[i] < p0 || c.pane[i] > p1 || !c.cnt[i] || !c.live(i)) continue;
         const uint64_t k = c.key[i];
         size_t h = (size_t)(mix64(k) >> 32) & mask;
         while (hk[h] != kEmptyKey && hk[h] != k) h = (h + 1) & mask;
@@ -137,13 +154,15 @@ class WindowTierCore {
       const int64_t *a, *c, *pane;
       size_t n;
       bool dev;
+      int64_t live_from;
     };
     std::vector<Src> src;
-    if (nd) src.push_back({dk, da, dc, nullptr, nd, true});
+    if (nd) src.push_back({dk, da, dc, nullptr, nd, true, INT64_MIN});
     size_t cand = nd;
     for (auto& c : chunks_)
       if (c.pmax >= p0 && c.pmin <= p1 && c.size()) {
-        src.push_back({c.key.data(), c.acc.data(), c.cnt.data(), c.pane.data(), c.size(), false});
+        src.push_back({c.key.data(), c.acc.data(), c.cnt.data(), c.pane.data(), c.size(), false,
+                       c.live_from});
         cand += c.size();
       }
     if (!cand) return;
@@ -153,7 +172,7 @@ class WindowTierCore {
     const size_t T = cand < (1u << 16) ? 1 : std::max(1u, std::min(hw ? hw : 1u, 16u));
     auto part_of = [&](uint64_t k) { return (size_t)(mix64(k) >> (64 - pbits)); };
     auto keep = [&](const Src& s, size_t i) {
-      return s.dev || (s.pane[i] >= p0 && s.pane[i] <= p1 && s.c[i]);
+      return s.dev || (s.pane[i] >= p0 && s.pane[i] <= p1 && s.c[i] && s.pane[i] >= s.live_from);
     };
     auto piece = [&](const Src& s, size_t t, size_t* lo, size_t* hi) {
       *lo = s.n * t / T;
@@ -328,8 +347,20 @@ class WindowTierCore {
     std::deque<Chunk> kept;
     for (auto& c : chunks_) {
       if (c.pmax < keep_from) {
-        rows_ -= c.size();
+        rows_ -= c.size() - c.dead;
         continue;
+      }
+      if (c.pmin < keep_from && !c.pane_rows.empty() && keep_from <= c.pmax) {
+        // rows below keep_from from the pane histogram; mark them dead unless they are half
+        size_t below = 0;
+        for (int64_t p = c.pmin; p < keep_from; ++p) below += c.pane_rows[(size_t)(p - c.pmin)];
+        if (2 * below < c.size()) {
+          rows_ -= below - c.dead;
+          c.dead = below;
+          c.live_from = std::max(c.live_from, keep_from);
+          kept.push_back(std::move(c));
+          continue;
+        }
       }
       if (c.pmin < keep_from) {
         Chunk f;
@@ -343,8 +374,11 @@ class WindowTierCore {
           f.pmin = std::min(f.pmin, c.pane[i]);
           f.pmax = std::max(f.pmax, c.pane[i]);
         }
-        rows_ -= c.size() - f.size();
-        if (f.size()) kept.push_back(std::move(f));
+        rows_ -= c.size() - c.dead - f.size();
+        if (f.size()) {
+          if ((uint64_t)(f.pmax - f.pmin) < ((uint64_t)1 << 20)) f.count_panes();
+          kept.push_back(std::move(f));
+        }
         continue;
       }
       kept.push_back(std::move(c));
@@ -366,7 +400,7 @@ class WindowTierCore {
     idx.reserve(rows_);
     for (size_t ci = 0; ci < chunks_.size(); ++ci)
       for (size_t i = 0; i < chunks_[ci].size(); ++i)
-        idx.push_back({chunks_[ci].pane[i], chunks_[ci].key[i], ci, i});
+        if (chunks_[ci].live(i)) idx.push_back({chunks_[ci].pane[i], chunks_[ci].key[i], ci, i});
     std::sort(idx.begin(), idx.end(), [](const R& a, const R& b) {
       return a.pane != b.pane ? a.pane < b.pane : a.key < b.key;
     });
@@ -395,6 +429,7 @@ class WindowTierCore {
     out.dirty = m.dirty;
     chunks_.clear();
     rows_ = m.size();
+    if (rows_ && (uint64_t)(m.pmax - m.pmin) < ((uint64_t)1 << 20)) m.count_panes();
     if (rows_) chunks_.push_back(std::move(m));
     return out;
   }

@@ -596,6 +596,20 @@ def test_cxx_window_tier_equals_numpy_combine(n):
         o1, o2 = np.argsort(got[0]), np.argsort(ref[0])
         for x, y in zip(got, ref):
             assert np.array_equal(np.asarray(x)[o1], np.asarray(y)[o2])
+    # purge(12): a fifth of every chunk is below -- marked dead, not copied (lazy purge); every
+    # reader skips the dead rows
+    before = merge_fire(K.AGG_SUM_I64, dk, dr, dc, t, False, E.EMPTY, E.EMPTY, 0, 1,
+                        panes=(12, 15))
+    t.purge(12)
+    assert t.nrows == int((cols["pane"] >= 12).sum()) and t.pane_range() == (12, 19)
+    r = t.copy().rows()  # (rows() merges the tier into one chunk: read a copy)
+    assert int(r["cnt"].sum()) == int(cols["cnt"][cols["pane"] >= 12].sum())
+    assert int(r["pane"].min()) == 12
+    after = merge_fire(K.AGG_SUM_I64, dk, dr, dc, t, False, E.EMPTY, E.EMPTY, 0, 1,
+                       panes=(12, 15))
+    o1, o2 = np.argsort(before[0]), np.argsort(after[0])
+    for x, y in zip(before, after):
+        assert np.array_equal(np.asarray(x)[o1], np.asarray(y)[o2])
     t.purge(15)
     assert t.nrows == int((cols["pane"] >= 15).sum()) and t.pane_range() == (15, 19)
     r = t.rows()
