@@ -768,16 +768,22 @@ PYBIND11_MODULE(_mxs_native, m) {
     cpu::window_combine(P<Rec>(recs), P<uint32_t>(counts), nbuckets, make_agg(plan), P<Rec>(out),
                         ccap, P<uint32_t>(out_counts), P<uint32_t>(flags));
   });
+  // nlines: the number of lines, or (nlines_dev != 0) the bound the outputs are sized for, the
+  // count itself read by the kernel from nlines_dev (line_starts' device total, no host sync).
   m.def("gpu_parse_text", [](intptr_t text, int64_t text_len, intptr_t starts, int64_t nlines,
                              std::vector<int32_t> fields, std::vector<int32_t> kinds,
                              std::string sep, int64_t offset_s, intptr_t cols, intptr_t jhash,
-                             intptr_t status, intptr_t stream) {
+                             intptr_t status, intptr_t stream, intptr_t nlines_dev,
+                             intptr_t nflag) {
     if (fields.size() != kinds.size() || sep.size() != 1)
       throw std::invalid_argument("parse_text: spec / separator");
     gpu::parse_text(reinterpret_cast<const char*>(text), text_len, P<int64_t>(starts), nlines,
                     fields.data(), kinds.data(), (int)fields.size(), sep[0], offset_s,
-                    P<int64_t>(cols), P<int32_t>(jhash), P<uint8_t>(status), stream);
-  });
+                    P<int64_t>(cols), P<int32_t>(jhash), P<uint8_t>(status), stream,
+                    P<int64_t>(nlines_dev), P<uint32_t>(nflag));
+  }, py::arg("text"), py::arg("text_len"), py::arg("starts"), py::arg("nlines"), py::arg("fields"),
+     py::arg("kinds"), py::arg("sep"), py::arg("offset_s"), py::arg("cols"), py::arg("jhash"),
+     py::arg("status"), py::arg("stream"), py::arg("nlines_dev") = 0, py::arg("nflag") = 0);
   m.def("gpu_f64_order_bits", [](intptr_t v, int64_t n, intptr_t o, intptr_t stream) {
     gpu::f64_order_bits(P<uint64_t>(v), n, P<uint64_t>(o), stream);
   });
@@ -925,11 +931,13 @@ PYBIND11_MODULE(_mxs_native, m) {
     py::gil_scoped_release nogil;
     cpu::line_starts(P<uint8_t>(buf), n, P<int64_t>(idx), P<int64_t>(total));
   });
+  // cap: entries of idx (starts past it are counted, not written; total is always exact)
   m.def("gpu_line_starts", [](intptr_t buf, int64_t n, intptr_t scratch, intptr_t idx,
-                              intptr_t total, intptr_t stream) {
+                              intptr_t total, intptr_t stream, int64_t cap) {
     gpu::line_starts(P<uint8_t>(buf), n, P<void>(scratch), P<int64_t>(idx), P<int64_t>(total),
-                     stream);
-  });
+                     stream, cap < 0 ? INT64_MAX : cap);
+  }, py::arg("buf"), py::arg("n"), py::arg("scratch"), py::arg("idx"), py::arg("total"),
+     py::arg("stream"), py::arg("cap") = -1);
   m.def("gpu_expr_filter_compact", [](intptr_t x, int64_t n, std::vector<int32_t> code,
                                       std::vector<double> consts, intptr_t scratch, intptr_t idx,
                                       intptr_t total, intptr_t stream) {

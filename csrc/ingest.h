@@ -139,10 +139,14 @@ MXS_HD bool fast_parse_double(const char* s, int64_t len, double* out) {
   return true;
 }
 
+MXS_HD const char* text_at(const char* t, int64_t i) { return t + i; }
+
 // One line [a, b) of `text` (no '\n', trailing '\r' already dropped). Returns 1 when the host
 // must decide the line. Numeric columns are written at row li; string fields are described at
-// positions li * nstr + s (the dictionary probe follows in the caller).
-MXS_HD uint8_t ingest_line(const char* text, int64_t a, int64_t b, int64_t li, int64_t n,
+// positions li * nstr + s (the dictionary probe follows in the caller). `text` is the batch in
+// global memory, or its LDS tile (csrc/line_tile.h LdsText: same absolute positions).
+template <class Text>
+MXS_HD uint8_t ingest_line(Text text, int64_t a, int64_t b, int64_t li, int64_t n,
                            const IngestSpec& sp, const IngestOut& o, int64_t* ts_val) {
   // Field boundaries of the requested split indices (Java String.split: trailing empty fields
   // are dropped, "" splits to [""]).
@@ -179,7 +183,7 @@ MXS_HD uint8_t ingest_line(const char* text, int64_t a, int64_t b, int64_t li, i
         st = 1;  // ArrayIndexOutOfBounds: the host reports it
         continue;
       }
-      const char* q = text + fs[f];
+      const char* q = text_at(text, fs[f]);
       const int64_t len = fe[f] - fs[f];
       o.spos[p] = fs[f];
       o.slen[p] = (int32_t)len;
@@ -191,7 +195,7 @@ MXS_HD uint8_t ingest_line(const char* text, int64_t a, int64_t b, int64_t li, i
       st = 1;
       continue;
     }
-    const char* q = text + fs[f];
+    const char* q = text_at(text, fs[f]);
     const int64_t len = fe[f] - fs[f];
     int64_t* out = o.cols + (int64_t)f * n + li;
     int64_t v = 0;

@@ -17,6 +17,7 @@
 #include <string>
 
 #include "ingest.h"
+#include "line_tile.h"
 #include "mxs_kernels.h"
 
 namespace mxs {
@@ -44,55 +45,78 @@ __device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void ingest_parse_kernel(
-    const char* __restrict__ text, int64_t text_len, const int64_t* __restrict__ starts,
-    int64_t n, IngestSpec sp, IngestOut o, DictState d) {
-  int64_t local_max = INT64_MIN;
-  uint32_t local_flag = 0;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < n; li += stride) {
-    const int64_t a = starts[li];
-    int64_t b = li + 1 < n ? starts[li + 1] - 1 : text_len;  // exclusive end (drop '\n')
-    if (b > text_len) b = text_len;
-    if (b > a && text[b - 1] == '\n') --b;  // the last line of a batch ending in '\n'
-    if (b > a && text[b - 1] == '\r') --b;  // SocketTextStreamFunction strips a trailing '\r'
-    int64_t ts = INT64_MIN;
-    const uint8_t st = ingest_line(text, a, b, li, n, sp, o, &ts);
-    o.status[li] = st;
-    local_flag += st;
-    if (!st && ts > local_max) local_max = ts;
-    // Dictionary probe of every string field of the line.
-    for (int s = 0; s < sp.nstr; ++s) {
-      const int64_t p = li * sp.nstr + s;
-      int32_t slot = -1;
-      if (o.slen[p] >= 0) {
-        const uint64_t h = o.shash[p];
-        uint32_t q = dict_home(h, d.mask);
-        for (uint32_t i = 0; i <= d.mask; ++i) {
-          const uint64_t k = __hip_atomic_load(&d.tab_h[q], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-          if (k == h) {
+// One workgroup per tile of 256 lines: the tile's bytes are staged into LDS (line_tile.h), every
+// thread splits and parses its line there, then probes the dictionary for its string fields.
+template <class Text>
+__device__ __forceinline__ void ingest_one_line(Text text, const char* __restrict__ gtext,
+                                                int64_t text_len,
+                                                const int64_t* __restrict__ starts, int64_t n,
+                                                int64_t li, const IngestSpec& sp,
+                                                const IngestOut& o, const DictState& d,
+                                                int64_t* local_max, uint32_t* local_flag) {
+  const int64_t a = starts[li];
+  int64_t b = li + 1 < n ? starts[li + 1] - 1 : text_len;  // exclusive end (drop '\n')
+  if (b > text_len) b = text_len;
+  if (b > a && text[b - 1] == '\n') --b;  // the last line of a batch ending in '\n'
+  if (b > a && text[b - 1] == '\r') --b;  // SocketTextStreamFunction strips a trailing '\r'
+  int64_t ts = INT64_MIN;
+  const uint8_t st = ingest_line(text, a, b, li, n, sp, o, &ts);
+  o.status[li] = st;
+  *local_flag += st;
+  if (!st && ts > *local_max) *local_max = ts;
+  (void)gtext;
+  // Dictionary probe of every string field of the line.
+  for (int s = 0; s < sp.nstr; ++s) {
+    const int64_t p = li * sp.nstr + s;
+    int32_t slot = -1;
+    if (o.slen[p] >= 0) {
+      const uint64_t h = o.shash[p];
+      uint32_t q = dict_home(h, d.mask);
+      for (uint32_t i = 0; i <= d.mask; ++i) {
+        const uint64_t k = __hip_atomic_load(&d.tab_h[q], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        if (k == h) {
+          slot = (int32_t)q;
+          break;
+        }
+        if (k == 0) {
+          const uint64_t prev = atomicCAS((unsigned long long*)&d.tab_h[q], 0ull,
+                                          (unsigned long long)h);
+          if (prev == 0 || prev == h) {
             slot = (int32_t)q;
             break;
           }
-          if (k == 0) {
-            const uint64_t prev = atomicCAS((unsigned long long*)&d.tab_h[q], 0ull,
-                                            (unsigned long long)h);
-            if (prev == 0 || prev == h) {
-              slot = (int32_t)q;
-              break;
-            }
-          }
-          q = (q + 1) & d.mask;
         }
-        if (slot < 0) {
-          atomicOr((unsigned long long*)&d.ctr[2], (unsigned long long)kDictErrFull);
-        } else if (d.tab_id[slot] < 0 && d.tab_first[slot] > p) {
-          atomicMin((unsigned long long*)&d.tab_first[slot], (unsigned long long)p);
-        }
+        q = (q + 1) & d.mask;
       }
-      o.sslot[p] = slot;
+      if (slot < 0) {
+        atomicOr((unsigned long long*)&d.ctr[2], (unsigned long long)kDictErrFull);
+      } else if (d.tab_id[slot] < 0 && d.tab_first[slot] > p) {
+        atomicMin((unsigned long long*)&d.tab_first[slot], (unsigned long long)p);
+      }
     }
+    o.sslot[p] = slot;
+  }
+}
+
+__global__ __launch_bounds__(256) void ingest_parse_kernel(
+    const char* __restrict__ text, int64_t text_len, const int64_t* __restrict__ starts,
+    int64_t n, IngestSpec sp, IngestOut o, DictState d) {
+  __shared__ __attribute__((aligned(16))) char tile[kTileLdsBytes];
+  int64_t local_max = INT64_MIN;
+  uint32_t local_flag = 0;
+  const int64_t l0 = (int64_t)blockIdx.x * kTileLines;
+  const int64_t l1 = l0 + kTileLines < n ? l0 + kTileLines : n;
+  const int64_t lo = starts[l0];
+  int64_t hi = l1 < n ? starts[l1] : text_len;
+  if (hi > text_len) hi = text_len;
+  const LdsText lt = stage_line_tile(text, lo, hi, tile, kTileLdsBytes);
+  const int64_t li = l0 + threadIdx.x;
+  if (li < l1) {
+    if (lt.p != nullptr)
+      ingest_one_line(lt, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag);
+    else
+      ingest_one_line(text, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag);
   }
   // One atomic per wave for the flag count and the max timestamp.
   local_max = wave_max_i64(local_max);
@@ -345,7 +369,9 @@ void ingest_parse(const char* text, int64_t text_len, const int64_t* starts, int
                   const IngestSpec& sp, const IngestOut& o, const DictState& d, intptr_t stream) {
   if (n <= 0) return;
   if (sp.nfields < 1 || sp.nfields > kIngestMaxFields) throw std::invalid_argument("ingest: fields");
-  hipLaunchKernelGGL(ingest_parse_kernel, dim3(ing_grid(n, 256, 8192)), dim3(256), 0,
+  const int64_t tiles = (n + kTileLines - 1) / kTileLines;
+  if (tiles > INT32_MAX) throw std::invalid_argument("ingest: batch too large");
+  hipLaunchKernelGGL(ingest_parse_kernel, dim3((uint32_t)tiles), dim3(kTileLines), 0,
                      (hipStream_t)stream, text, text_len, starts, n, sp, o, d);
   ING_CHECK(hipGetLastError());
 }

@@ -2214,7 +2214,9 @@ __global__ __launch_bounds__(1024) void filter_scan_kernel(const uint32_t* __res
 
 __global__ __launch_bounds__(256) void filter_write_kernel(const uint64_t* __restrict__ masks,
                                                            const int64_t* __restrict__ offs,
-                                                           int64_t n, int64_t* __restrict__ idx) {
+                                                           int64_t n, int64_t* __restrict__ idx,
+                                                           int64_t cap) {
+  // cap: idx holds this many entries (line starts sized by a bound; the count is exact anyway)
   __shared__ uint32_t wpre[kFcWords];
   const uint64_t* tm = masks + (size_t)blockIdx.x * kFcWords;
   if (threadIdx.x == 0) {
@@ -2233,7 +2235,8 @@ __global__ __launch_bounds__(256) void filter_write_kernel(const uint64_t* __res
     const int w = j * 4 + wave;
     const uint64_t m = tm[w];
     const int64_t i = tile + j * 256 + threadIdx.x;
-    if (((m >> lane) & 1ull) && i < n) idx[off + wpre[w] + __popcll(m & below)] = i;
+    const int64_t q = off + wpre[w] + __popcll(m & below);
+    if (((m >> lane) & 1ull) && i < n && q < cap) idx[q] = i;
   }
 }
 
@@ -4474,7 +4477,7 @@ void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep
 }
 
 void line_starts(const uint8_t* buf, int64_t n, void* scratch, int64_t* idx, int64_t* total,
-                 intptr_t stream) {
+                 intptr_t stream, int64_t cap) {
   if (n <= 0) {
     HIP_CHECK(hipMemsetAsync(total, 0, 8, (hipStream_t)stream));
     return;
@@ -4490,7 +4493,7 @@ void line_starts(const uint8_t* buf, int64_t n, void* scratch, int64_t* idx, int
                      offs, total);
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(filter_write_kernel, dim3((uint32_t)nt), dim3(256), 0, (hipStream_t)stream,
-                     masks, offs, n, idx);
+                     masks, offs, n, idx, cap);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -4500,7 +4503,7 @@ void compact_from_masks(const uint64_t* masks, const uint32_t* counts, int64_t n
                      offs, total);
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(filter_write_kernel, dim3((uint32_t)nt), dim3(256), 0, (hipStream_t)stream,
-                     masks, offs, n, idx);
+                     masks, offs, n, idx, INT64_MAX);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -4527,7 +4530,7 @@ void expr_filter_compact(const double* x, int64_t n, const ExprProg& prog, void*
                      offs, total);
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(filter_write_kernel, dim3((uint32_t)nt), dim3(256), 0, (hipStream_t)stream,
-                     masks, offs, n, idx);
+                     masks, offs, n, idx, INT64_MAX);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -215,7 +215,7 @@ void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep
 int64_t filter_compact_scratch_bytes(int64_t n);
 // Line-start offsets of a text batch, in order (scratch: filter_compact_scratch_bytes(n)).
 void line_starts(const uint8_t* buf, int64_t n, void* scratch, int64_t* idx, int64_t* total,
-                 intptr_t stream);
+                 intptr_t stream, int64_t cap = INT64_MAX);
 void expr_filter_compact(const double* x, int64_t n, const ExprProg& prog, void* scratch,
                          int64_t* idx, int64_t* total, intptr_t stream);
 // Scan + write half of the compaction over tile masks/counts made by any mask kernel.
@@ -317,7 +317,7 @@ void window_combine(const Rec* recs, const uint32_t* counts, int nbuckets, const
 void parse_text(const char* text, int64_t text_len, const int64_t* starts, int64_t nlines,
                 const int32_t* fields, const int32_t* kinds, int nfields, char sep,
                 int64_t offset_s, int64_t* cols, int32_t* jhash, uint8_t* status,
-                intptr_t stream);
+                intptr_t stream, const int64_t* nlines_dev = nullptr, uint32_t* nflag = nullptr);
 void f64_order_bits(const uint64_t* v, int64_t n, uint64_t* o, intptr_t stream);
 void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uint64_t* ord,
                     double* out, intptr_t stream);

@@ -245,7 +245,8 @@ inline int num_passes(int begin_bit, int end_bit) {
 }  // namespace
 
 size_t sort_pairs_temp_bytes(int64_t n, int begin_bit, int end_bit) {
-  if (n < 0 || n >= ((int64_t)1 << 32)) throw std::invalid_argument("sort_pairs: n out of range");
+  // The kernels index in uint32 (tile base + in-tile offset): the last tile must end below 2^32.
+  if (n < 0 || n > ((int64_t)1 << 32) - kTile) throw std::invalid_argument("sort_pairs: n out of range");
   if (begin_bit < 0 || end_bit > 64 || begin_bit >= end_bit)
     throw std::invalid_argument("sort_pairs: bad bit range");
   const size_t ntiles = (size_t)((n + kTile - 1) / kTile);

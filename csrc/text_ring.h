@@ -44,8 +44,7 @@ class TextRingCore {
   TextRingCore(const std::string& path, int64_t lo, int64_t hi,
                std::vector<std::pair<intptr_t, int64_t>> slots, int64_t chunk, int threads)
       : lo_(lo), hi_(hi), chunk_(chunk), threads_(std::max(1, std::min(threads, 64))) {
-    fd_ = ::open(path.c_str(), O_RDONLY);
-    if (fd_ < 0) throw std::runtime_error("cannot open " + path + ": " + std::strerror(errno));
+    // Validate before opening: a throwing constructor never runs the destructor (no fd leak).
     if (slots.size() < 2) throw std::invalid_argument("TextFileRing needs at least 2 slots");
     if (lo < 0 || hi < lo) throw std::invalid_argument("bad byte range");
     for (auto& s : slots) {
@@ -53,6 +52,8 @@ class TextRingCore {
       slots_.push_back({reinterpret_cast<char*>(s.first), s.second});
       free_.push_back((int)slots_.size() - 1);
     }
+    fd_ = ::open(path.c_str(), O_RDONLY);
+    if (fd_ < 0) throw std::runtime_error("cannot open " + path + ": " + std::strerror(errno));
   }
   ~TextRingCore() { close(); }
 

@@ -342,30 +342,33 @@ class WindowTierCore {
     }
   }
 
-  // Drop rows of panes < keep_from: whole chunks below it, filtered straddling chunks.
+  // Drop rows of panes < keep_from: whole chunks below it, filtered straddling chunks. A chunk
+  // whose rows below live_from are already dead purges from max(keep_from, live_from), so a
+  // keep_from lower than an earlier purge's never revives dead rows or rewinds the counts.
   void purge(int64_t keep_from) {
     std::deque<Chunk> kept;
     for (auto& c : chunks_) {
-      if (c.pmax < keep_from) {
+      const int64_t kf = std::max(keep_from, c.live_from);
+      if (c.pmax < kf) {
         rows_ -= c.size() - c.dead;
         continue;
       }
-      if (c.pmin < keep_from && !c.pane_rows.empty() && keep_from <= c.pmax) {
-        // rows below keep_from from the pane histogram; mark them dead unless they are half
+      if (c.pmin < kf && !c.pane_rows.empty() && kf <= c.pmax) {
+        // rows below kf from the pane histogram; mark them dead unless they are half
         size_t below = 0;
-        for (int64_t p = c.pmin; p < keep_from; ++p) below += c.pane_rows[(size_t)(p - c.pmin)];
+        for (int64_t p = c.pmin; p < kf; ++p) below += c.pane_rows[(size_t)(p - c.pmin)];
         if (2 * below < c.size()) {
-          rows_ -= below - c.dead;
+          rows_ -= below - c.dead;  // below >= c.dead: kf >= live_from
           c.dead = below;
-          c.live_from = std::max(c.live_from, keep_from);
+          c.live_from = kf;
           kept.push_back(std::move(c));
           continue;
         }
       }
-      if (c.pmin < keep_from) {
+      if (c.pmin < kf) {
         Chunk f;
         for (size_t i = 0; i < c.size(); ++i) {
-          if (c.pane[i] < keep_from) continue;
+          if (c.pane[i] < kf) continue;
           f.key.push_back(c.key[i]);
           f.pane.push_back(c.pane[i]);
           f.acc.push_back(c.acc[i]);

@@ -121,6 +121,19 @@ class _StdoutWriter:
             sys.stdout.write("\n".join(lines) + "\n")
             sys.stdout.flush()
 
+    @staticmethod
+    def raw(data: bytes) -> None:
+        """A column batch already formatted as newline-terminated lines (native formatter)."""
+        if data:
+            buf = getattr(sys.stdout, "buffer", None)
+            if buf is None:  # a text-only stream (captured stdout)
+                sys.stdout.write(data.decode())
+                sys.stdout.flush()
+                return
+            sys.stdout.flush()
+            buf.write(data)
+            buf.flush()
+
 
 class StreamExecutionEnvironment:
     DEFAULT_PARALLELISM = 4

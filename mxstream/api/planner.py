@@ -234,7 +234,8 @@ def _lower_text(env, sinks) -> None:
 
         parent.factory = columnar_source
         t.meta = dict(meta, columnar=True, text_spec=spec,
-                      device_ingest=shared if ingest_dev is not None else None)
+                      device_ingest=shared if ingest_dev is not None else None,
+                      event_ts=ts_spec is not None)
 
 
 def plan(env, sinks):
@@ -536,6 +537,7 @@ def _install_native(env, t, ws, spec, key_pos, val_pos, kind, result, ok_arities
                  assigner=assigner, lateness=late, late_tag=tag, device=device,
                  fallback_factory=fallback, result_builder=builder, ok_arities=ok_arities)
         op.device_input = device_input
+        op.scalar_result = result == "value"
         return op
 
     t.factory = factory
@@ -550,10 +552,18 @@ def _install_native_rolling(env, t, meta):
     fallback = t.factory
     device = env.config.device
     key_fn, key_pos, pos, kind = meta["key_fn"], meta["key_pos"], meta["pos"], meta["agg"]
+    device_input, event_ts = None, True
+    for p in t.parents:
+        pm = getattr(p, "meta", None) or {}
+        if pm.get("device_ingest") is not None and pm.get("text_spec") is not None:
+            device_input = (tuple(k for _, k in pm["text_spec"].fields), pm["device_ingest"])
+            event_ts = bool(pm.get("event_ts"))
 
     def factory():
-        return NativeRollingOp(key_fn=key_fn, key_pos=key_pos, val_pos=pos, kind=kind,
-                               device=device, fallback_factory=fallback)
+        op = NativeRollingOp(key_fn=key_fn, key_pos=key_pos, val_pos=pos, kind=kind,
+                             device=device, fallback_factory=fallback)
+        op.device_input, op.event_ts = device_input, event_ts
+        return op
 
     t.factory = factory
     t.meta = dict(t.meta, native=True)

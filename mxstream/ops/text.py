@@ -46,20 +46,29 @@ def pinned_text_batch(data: bytes) -> torch.Tensor:
 
 
 def parse_text_gpu(data, spec: list[tuple[int, int]], sep: str = " ", offset_s: int = 0,
-                   device="cuda") -> list:
+                   device="cuda", *, ready=None, min_line_bytes: int = 8) -> list:
     """Returns one entry per spec field: a float64/int64 device tensor, or for FK_STR a
     (key int64, java_hash int32) pair of device tensors.
 
-    ``data`` is ``bytes`` or a 1-D uint8 tensor (a pinned host batch from ``pinned_text_batch``
-    or a batch already on the device); a pinned batch is uploaded asynchronously."""
+    ``data`` is ``bytes`` or a 1-D uint8 tensor (a pinned host batch from ``pinned_text_batch``,
+    uploaded asynchronously, or a batch already on the device -- ``ready``: an event after which
+    its copy, e.g. on a side stream, is complete).
+
+    No host pass over the text: the line-start index is sized for ``n_bytes / min_line_bytes``
+    lines (line_starts writes at most that many, counts them all), the parse kernel reads the
+    device line count, and ONE readback returns (lines, flagged lines). A batch with more lines
+    than the bound -- shorter lines than assumed -- is redone with the exact size."""
     if not spec or len(spec) > 8:
         raise ValueError("1..8 fields")
     dev = torch.device(device)
     m = load()
+    st = torch.cuda.current_stream(dev).cuda_stream
     if isinstance(data, torch.Tensor):
         if data.dtype != torch.uint8 or data.dim() != 1:
             raise ValueError("text batch tensor must be 1-D uint8")
         n_bytes = data.numel()
+        if ready is not None:
+            torch.cuda.current_stream(dev).wait_event(ready)
         buf = (data.to(dev, non_blocking=data.is_pinned()) if n_bytes
                else torch.zeros(1, dtype=torch.uint8, device=dev))
         host = data
@@ -69,41 +78,41 @@ def parse_text_gpu(data, spec: list[tuple[int, int]], sep: str = " ", offset_s: 
         buf = torch.from_numpy(raw.copy()).to(dev) if n_bytes else torch.zeros(
             1, dtype=torch.uint8, device=dev)
         host = None
-    # Line starts (0 and every byte after a newline, below n_bytes: a trailing newline starts no
-    # line) by the order-preserving ballot/scan/write kernels; one host sync for the count. The
-    # index array is sized by the line count when the host holds the text (a device-only batch
-    # falls back to the byte count, the only bound known without reading it).
-    from .ingest import count_lines
-
-    if host is not None and host.device.type == "cpu":
-        bound = count_lines(host) + 1
-    elif host is None:
-        bound = count_lines(data) + 1
-    else:
-        bound = n_bytes
-    starts_buf = torch.empty(max(min(bound + 64, n_bytes), 1), dtype=torch.int64, device=dev)
-    total = torch.zeros(1, dtype=torch.int64, device=dev)
+    nf = len(spec)
+    if n_bytes == 0:
+        return [torch.empty(0, dtype=torch.float64 if k == FK_DOUBLE else torch.int64, device=dev)
+                if k != FK_STR else (torch.empty(0, dtype=torch.int64, device=dev),
+                                     torch.empty(0, dtype=torch.int32, device=dev))
+                for _, k in spec]
     scratch = torch.empty(max(1, m.gpu_filter_compact_scratch_bytes(n_bytes)), dtype=torch.uint8,
                           device=dev)
-    m.gpu_line_starts(buf.data_ptr(), n_bytes, scratch.data_ptr(), starts_buf.data_ptr(),
-                      total.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
-    n = int(total.item()) if n_bytes else 0
-    starts = starts_buf[:n]
-    nf = len(spec)
-    cols = torch.empty(nf * max(n, 1), dtype=torch.int64, device=dev)
-    jh = torch.zeros(nf * max(n, 1), dtype=torch.int32, device=dev)
-    status = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
-    if n:
-        m.gpu_parse_text(buf.data_ptr(), n_bytes, starts.contiguous().data_ptr(), n,
+    ctl = torch.zeros(2, dtype=torch.int64, device=dev)  # [0] lines  [1] flagged lines (u32)
+    bound = min(n_bytes, n_bytes // max(1, int(min_line_bytes)) + 256)
+    while True:
+        starts_buf = torch.empty(max(bound, 1), dtype=torch.int64, device=dev)
+        cols = torch.empty(nf * bound, dtype=torch.int64, device=dev)
+        jh = torch.zeros(nf * bound, dtype=torch.int32, device=dev)
+        status = torch.empty(bound, dtype=torch.uint8, device=dev)
+        ctl.zero_()
+        m.gpu_line_starts(buf.data_ptr(), n_bytes, scratch.data_ptr(), starts_buf.data_ptr(),
+                          ctl[0:1].data_ptr(), st, bound)
+        m.gpu_parse_text(buf.data_ptr(), n_bytes, starts_buf.data_ptr(), bound,
                          [f for f, _ in spec], [k for _, k in spec], sep, int(offset_s),
-                         cols.data_ptr(), jh.data_ptr(), status.data_ptr(),
-                         torch.cuda.current_stream(dev).cuda_stream)
+                         cols.data_ptr(), jh.data_ptr(), status.data_ptr(), st,
+                         nlines_dev=ctl[0:1].data_ptr(), nflag=ctl[1:2].data_ptr())
+        n, nflag = ctl.tolist()  # the batch's one host synchronisation
+        nflag &= 0xFFFFFFFF
+        if n <= bound:
+            break
+        bound = n  # lines shorter than min_line_bytes: exact size, once
+    starts = starts_buf[:n]
+    if nflag:
         bad = torch.nonzero(status[:n]).flatten()
-        if bad.numel():
-            if host is not None:
-                data = host.cpu().numpy().tobytes()
-            _host_patch(m, data, starts.cpu().numpy(), bad.cpu().numpy(), spec, sep, offset_s,
-                        cols, jh, n)
+        if host is not None:
+            data = host.cpu().numpy().tobytes()
+        # the kernel laid columns out with the device count n as the column stride
+        _host_patch(m, data, starts.cpu().numpy(), bad.cpu().numpy(), spec, sep, offset_s,
+                    cols, jh, n)
     out = []
     for f, (_, kind) in enumerate(spec):
         c = cols[f * n:(f + 1) * n]

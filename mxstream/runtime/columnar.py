@@ -62,6 +62,7 @@ class ColumnBatch:
     strings: object                      # StringDict of FK_STR columns
     ts: np.ndarray | None = None         # event timestamps (None: no timestamp)
     sub: np.ndarray | None = None        # subtask per row
+    scalar: bool = False                 # one column of bare values (not Tuple1 rows)
     _cache: dict = field(default_factory=dict)
 
     def field_value(self, j: int, i: int):
@@ -73,7 +74,9 @@ class ColumnBatch:
             return float(v)
         return int(v)
 
-    def value(self, i: int) -> Tuple:
+    def value(self, i: int):
+        if self.scalar:
+            return self.field_value(0, i)
         return Tuple([self.field_value(j, i) for j in range(len(self.cols))])
 
     def to_recs(self) -> list[Rec]:
@@ -90,13 +93,15 @@ class ColumnBatch:
                 cols.append(c.tolist())
         ts = self.ts.tolist() if self.ts is not None else [LONG_MIN] * self.n
         sub = self.sub.tolist() if self.sub is not None else [0] * self.n
+        if self.scalar:
+            return [Rec(v, t, s) for v, t, s in zip(cols[0], ts, sub)]
         return [Rec(Tuple(row), t, s) for row, t, s in zip(zip(*cols), ts, sub)]
 
     def take(self, mask: np.ndarray) -> "ColumnBatch":
         idx = np.nonzero(mask)[0]
         return ColumnBatch(int(idx.size), [c[idx] for c in self.cols], self.kinds, self.strings,
                            None if self.ts is None else self.ts[idx],
-                           None if self.sub is None else self.sub[idx])
+                           None if self.sub is None else self.sub[idx], self.scalar)
 
 
 class DeviceColumnBatch(ColumnBatch):
@@ -106,9 +111,13 @@ class DeviceColumnBatch(ColumnBatch):
     (host operators, print sinks, late side outputs) materialises ``host()`` once."""
 
     def __init__(self, n: int, cols: list, kinds: tuple, strings, ts, *, sub0: int = 0,
-                 parallelism: int = 1, line_idx=None, max_ts: int | None = None):
+                 parallelism: int = 1, line_idx=None, max_ts: int | None = None,
+                 sub_dev=None, scalar: bool = False):
+        """sub_dev: the subtask of every row as a device int32 column (a keyed operator's
+        output: the key's subtask); otherwise rows are round-robin from sub0 (source edge)."""
         self.n, self.cols, self.kinds, self.strings, self.ts = n, cols, kinds, strings, ts
         self.sub0, self.parallelism, self.line_idx, self.max_ts = sub0, parallelism, line_idx, max_ts
+        self.sub_dev, self.scalar = sub_dev, scalar
         self._cache = {}
         self._host = None
 
@@ -117,16 +126,32 @@ class DeviceColumnBatch(ColumnBatch):
         return self.host().sub
 
     def host(self) -> ColumnBatch:
+        parts = getattr(self, "_parts", None)
+        if self._host is None and parts:
+            self._host = _concat_host([b.host() for b in parts])
         if self._host is None:
+            import torch
+
+            # one D2H for all columns (a keyed operator's emit: several narrow columns)
+            dev = [c[:self.n] for c in self.cols]
+            if self.sub_dev is not None:
+                dev.append(self.sub_dev[:self.n].to(torch.int64))
+            elif self.line_idx is not None:
+                dev.append(self.line_idx[:self.n].to(torch.int64))
+            if self.ts is not None:
+                dev.append(self.ts[:self.n])
+            host = _to_host(dev)
             cols = []
-            for c, k in zip(self.cols, self.kinds):
-                a = c[:self.n].cpu().numpy()
+            for a, k in zip(host, self.kinds):
                 cols.append(a.astype(np.int64) if k == FK_STR else a)
-            line = (self.line_idx[:self.n].cpu().numpy() if self.line_idx is not None
-                    else np.arange(self.n, dtype=np.int64))
-            sub = ((self.sub0 + line) % max(1, self.parallelism)).astype(np.int32)
-            ts = None if self.ts is None else self.ts[:self.n].cpu().numpy()
-            self._host = ColumnBatch(self.n, cols, self.kinds, self.strings, ts, sub)
+            rest = host[len(self.cols):]
+            if self.sub_dev is not None:
+                sub = rest.pop(0).astype(np.int32)
+            else:
+                line = rest.pop(0) if self.line_idx is not None else np.arange(self.n, dtype=np.int64)
+                sub = ((self.sub0 + line) % max(1, self.parallelism)).astype(np.int32)
+            ts = rest.pop(0) if self.ts is not None else None
+            self._host = ColumnBatch(self.n, cols, self.kinds, self.strings, ts, sub, self.scalar)
         return self._host
 
     def field_value(self, j: int, i: int):
@@ -142,6 +167,33 @@ class DeviceColumnBatch(ColumnBatch):
         return self.host().take(mask)
 
 
+def _to_host(cols: list) -> list:
+    """Device columns -> numpy arrays with one D2H copy: the columns are packed as bytes into
+    one device buffer (a cat of byte views), copied once, and cut back into typed arrays."""
+    import torch
+
+    if not cols:
+        return []
+    if cols[0].device.type != "cuda" or len(cols) == 1:
+        return [c.cpu().numpy() for c in cols]
+    parts, meta = [], []
+    for c in cols:
+        c = c.contiguous()
+        b = c.view(torch.uint8) if c.numel() else torch.empty(0, dtype=torch.uint8, device=c.device)
+        pad = (-b.numel()) % 8
+        parts.append(b)
+        if pad:
+            parts.append(torch.zeros(pad, dtype=torch.uint8, device=c.device))
+        meta.append((c.dtype, c.numel(), b.numel() + pad))
+    buf = torch.cat(parts).cpu().numpy()
+    out, off = [], 0
+    for dt, n, nb in meta:
+        npdt = torch.empty(0, dtype=dt).numpy().dtype
+        out.append(buf[off:off + n * npdt.itemsize].view(npdt).copy() if n else np.zeros(0, npdt))
+        off += nb
+    return out
+
+
 def concat_device(batches: list) -> DeviceColumnBatch:
     """Concatenate device batches of one layout and one dictionary."""
     if len(batches) == 1:
@@ -154,7 +206,7 @@ def concat_device(batches: list) -> DeviceColumnBatch:
     cols = [torch.cat([b.cols[j][:b.n] for b in batches]) for j in range(len(b0.cols))]
     ts = None if b0.ts is None else torch.cat([b.ts[:b.n] for b in batches])
     out = DeviceColumnBatch(sum(b.n for b in batches), cols, b0.kinds, b0.strings, ts)
-    out._host = _concat_host([b.host() for b in batches])  # sub / late rows, if ever needed
+    out._parts = list(batches)  # host() concatenates the parts' host views (sub / late rows)
     return out
 
 
@@ -164,7 +216,7 @@ def _concat_host(batches: list) -> ColumnBatch:
     return ColumnBatch(sum(b.n for b in batches),
                        [np.concatenate([b.cols[j] for b in batches]) for j in range(len(b0.cols))],
                        b0.kinds, b0.strings, cat([b.ts for b in batches]),
-                       cat([b.sub for b in batches]))
+                       cat([b.sub for b in batches]), b0.scalar)
 
 
 def expand_columns(items: list) -> list:

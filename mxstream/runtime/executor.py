@@ -130,6 +130,7 @@ class Executor:
         self._wm_in: dict = {}  # keyed node -> latest watermark received from every rank
         self._failure: Exception | None = None  # multi-rank: first operator failure of this rank
         self.dev_comm = None  # device collectives of the native operators (G > 1)
+        self._step_now = None  # G > 1: the step's agreed processing time (_step_begin)
         if comm is not None and comm.world > 1:
             # Injected communicator (LoopbackComm: G virtual ranks in one process, tests).
             self.comm = self.dev_comm = comm
@@ -191,7 +192,7 @@ class Executor:
                 self.ops[n.id] = op
             else:
                 op = n.factory()
-                op.open(OpContext(n.name, p, env.max_parallelism, self.clock, tc,
+                op.open(OpContext(n.name, p, env.max_parallelism, self._op_clock, tc,
                                   comm=self.dev_comm, ctrl=self.comm))
                 self.ops[n.id] = op
 
@@ -348,11 +349,31 @@ class Executor:
                 return [WM(wm)]
         return []
 
-    def _all_done(self, finished: dict) -> bool:
-        done = all(finished.values())
+    def _op_clock(self) -> int:
+        """Processing time as operators see it: one rank reads its clock; several ranks read the
+        step's agreed time (_step_begin), so every rank stamps and fires the same windows."""
+        if self.comm is None or self._step_now is None:
+            return self.clock()
+        return self._step_now
+
+    def _step_begin(self, finished: dict, sources: list, manual: bool) -> tuple[bool, int]:
+        """(every source finished on every rank, the step's processing time). Multi-rank: one
+        gather of (done, clock) -- the step's time is the MAX over the ranks' clocks (a manual
+        clock advances to it), the agreement processing-time windows fire on."""
+        if manual:
+            nxt = [self.ops[n.id].next_event_time() for n in sources if not finished[n.id]]
+            nxt = [t for t in nxt if t is not None]
+            if nxt:
+                self.clock.advance_to(min(nxt))
+        done, now = all(finished.values()), self.clock()
         if self.comm is None:
-            return done
-        return all(self.comm.all_gather_object(done))
+            return done, now
+        got = self.comm.all_gather_object((done, now))
+        now = max(t for _, t in got)
+        if manual:
+            self.clock.advance_to(now)
+        self._step_now = now
+        return all(d for d, _ in got), now
 
     # ---- checkpoints ---------------------------------------------------------------------
     def _storage(self):
@@ -505,13 +526,10 @@ class Executor:
         if getattr(cfg_x, "step_timeout_ms", 0) and cfg_x.step_timeout_ms > 0:
             wd = Watchdog(cfg_x.step_timeout_ms, name=self.job_name).start()
         try:
-            while not self._all_done(finished):
-                if manual:
-                    nxt = [self.ops[n.id].next_event_time() for n in sources if not finished[n.id]]
-                    nxt = [t for t in nxt if t is not None]
-                    if nxt:
-                        self.clock.advance_to(min(nxt))
-                now = self.clock()
+            while True:
+                done, now = self._step_begin(finished, sources, manual)
+                if done:
+                    break
                 inbox: dict = {}
                 for n in sources:
                     if finished[n.id]:

@@ -170,22 +170,31 @@ class NativeWindowOp(_ColumnInput, Operator):
         self.device_exchange = self.collective = False
         comm = getattr(ctx, "comm", None)
         if (comm is not None and comm.world > 1 and self.device_input is not None
-                and type(self) is NativeWindowOp and self.assigner.is_event_time()):
+                and self._exchange_ok):
             # Multi-rank with device-ingest input: the operator exchanges keys itself (local-
-            # global partials over RCCL, key groups from the shared dictionary's Java hashes)
-            # and runs one collective step per pass -- built now, identically on every rank.
+            # global partials or records over RCCL, key groups from the shared dictionary's Java
+            # hashes) and runs one collective step per pass -- built now, identically on every
+            # rank. Processing-time windows stamp and fire on the step's agreed clock (the
+            # executor's MAX over the ranks' clocks), so every rank fires the same windows.
             kinds, shared = self.device_input
             vk = kinds[self.val_pos]
             if vk == FK_STR or (self.ok_arities and len(kinds) not in self.ok_arities):
                 return
-            self.dict = shared["dict"]
-            self.str_keys = kinds[self.key_pos] == FK_STR
             if kinds[self.key_pos] == FK_DOUBLE:
                 return
+            self.dict = shared["dict"]
+            self.str_keys = kinds[self.key_pos] == FK_STR
             self.comm = comm
             self.device_exchange = self.collective = True
             self._lazy_tpl, self._lazy_arity = {}, len(kinds)
-            self._build(1.0 if vk == FK_DOUBLE else 1, dense=self.str_keys)
+            if not self._build(1.0 if vk == FK_DOUBLE else 1, dense=self.str_keys):
+                self.device_exchange = self.collective = False
+                self.op, self.comm = None, None
+                self.dict, self.str_keys = load().StringDict(), None
+                self._lazy_tpl = None
+
+    _exchange_ok = True  # subclasses that cannot exchange their keys at G > 1 opt out
+    scalar_result = False  # planner: the window emits the bare aggregate (a Double), no tuple
 
     def _jhash(self):
         """Java hashes of the dictionary ids (key groups of string keys at G > 1)."""
@@ -207,34 +216,49 @@ class NativeWindowOp(_ColumnInput, Operator):
         self._build(1.0 if self.is_float else 1, dense=True)
         self.op.restore_state(es.columns, es.meta)
 
-    def _process_exchange(self, items) -> list:
-        """G > 1 device exchange: one engine step per pass (an empty batch if this rank got no
-        rows), then the merged watermark (identical on every rank) advances every rank."""
-        data = [it for it in items if not isinstance(it, WM)]
-        wms = [it.ts for it in items if isinstance(it, WM)]
-        dev = self.op.device
+    def _local_columns(self, data: list):
+        """This rank's (key id, timestamp, value bits) device columns of a pass (empty columns
+        when it got no rows). Processing time: every row carries the step's agreed time."""
+        dev = self.op.device if self.op is not None else torch.device(self.device)
         if any(not isinstance(b, DeviceColumnBatch) for b in data):
             raise TypeError("multi-rank native window: device-ingest batches expected")
-        self._ensure_capacity()
-        self.op.jhash = self._jhash()
+        event = self.assigner.is_event_time()
         if data:
             cb = concat_device(data)
             n = cb.n
             kid = cb.cols[self.key_pos][:n]
-            ts = cb.ts[:n] if cb.ts is not None else torch.full((n,), LONG_MIN, dtype=torch.int64,
-                                                                 device=dev)
+            if event:
+                ts = cb.ts[:n] if cb.ts is not None else torch.full((n,), LONG_MIN,
+                                                                     dtype=torch.int64, device=dev)
+            else:
+                ts = torch.full((n,), self.ctx.clock(), dtype=torch.int64, device=dev)
             vals = cb.cols[self.val_pos][:n]
             vals = vals.view(torch.int64) if vals.dtype == torch.float64 else vals.to(torch.int64)
         else:
             kid = torch.empty(0, dtype=torch.int32 if self.str_keys else torch.int64, device=dev)
             ts = torch.empty(0, dtype=torch.int64, device=dev)
             vals = torch.empty(0, dtype=torch.int64, device=dev)
+        return kid.contiguous(), ts.contiguous(), vals.contiguous()
+
+    def _process_exchange(self, items) -> list:
+        """G > 1 device exchange: one engine step per pass (an empty batch if this rank got no
+        rows), then the merged watermark (identical on every rank) advances every rank (event
+        time; processing-time windows fire in on_processing_time on the agreed clock)."""
+        data = [it for it in items if not isinstance(it, WM)]
+        wms = [it.ts for it in items if isinstance(it, WM)]
+        self._ensure_capacity()
+        self.op.jhash = self._jhash()
+        kid, ts, vals = self._local_columns(data)
+        if kid.dtype == torch.int32 and not self._key32_ok:
+            kid = kid.to(torch.int64)
         late_before = self.op.metrics.num_late_records_dropped
-        out = self._emit(self.op.process(kid.contiguous(), ts.contiguous(), vals.contiguous()))
+        out = self._emit(self.op.process(kid, ts, vals))
         self.num_late_records_dropped += self.op.metrics.num_late_records_dropped - late_before
+        event = self.assigner.is_event_time()
         for w in wms:
             self.wm = w
-            out.extend(self._emit(self.op.advance_watermark(w)))
+            if event:
+                out.extend(self._emit(self.op.advance_watermark(w)))
             out.append(WM(w))
         return out
 
@@ -450,13 +474,23 @@ class NativeWindowOp(_ColumnInput, Operator):
             self.num_late_records_dropped += self.op.metrics.num_late_records_dropped - late_before
         return self._emit(fired)
 
+    def _out_layout(self):
+        """(layout, scalar) of the output rows: field indices of the output tuple (-1 = the
+        mapped value), or one column for a bare result / a map to a scalar."""
+        if self.fused_scalar:
+            return (-1,), True
+        if self.fused_layout is None and self.scalar_result:
+            return (self.val_pos,), True
+        return self.fused_layout, False
+
     def _columnar_kinds(self):
-        """Column kinds of the fused output tuple when every field is the key, the window
-        result or the mapped value (no keep-first template fields); None otherwise."""
-        if self.fused_layout is None or self.fused_scalar or self.str_keys is None:
+        """Column kinds of the output rows when every field is the key, the window result or
+        the mapped value (no keep-first template fields); None otherwise."""
+        layout, _ = self._out_layout()
+        if layout is None or self.str_keys is None:
             return None
         kinds = []
-        for j in self.fused_layout:
+        for j in layout:
             if j < 0 or (j == self.val_pos and self.kind == "avg"):
                 kinds.append(FK_DOUBLE)
             elif j == self.val_pos:
@@ -492,7 +526,8 @@ class NativeWindowOp(_ColumnInput, Operator):
         keys = np.concatenate([fr.keys for fr in fired])
         keys = keys.view(np.int64) if keys.dtype == np.uint64 else keys.astype(np.int64)
         cols = []
-        for j, k in zip(self.fused_layout, kinds):
+        layout, scalar = self._out_layout()
+        for j, k in zip(layout, kinds):
             if j < 0 or (j == self.val_pos and self.kind == "avg"):
                 cols.append(np.concatenate([fr.values for fr in fired]).astype(np.float64, copy=False))
             elif j == self.val_pos:
@@ -507,7 +542,7 @@ class NativeWindowOp(_ColumnInput, Operator):
         ts = np.repeat(np.array([fr.window_end - 1 for fr in fired], dtype=np.int64),
                        [fr.keys.size for fr in fired])
         return [ColumnBatch(int(keys.size), cols, kinds, self.dict if self.str_keys else None,
-                            ts, self._subtasks(keys))]
+                            ts, self._subtasks(keys), scalar)]
 
     def _emit(self, fired) -> list:
         kinds = self._columnar_kinds() if fired else None
@@ -568,6 +603,11 @@ class NativeWindowOp(_ColumnInput, Operator):
     def on_processing_time(self, now):
         if self.fallback is not None:
             return self.fallback.on_processing_time(now)
+        if self.device_exchange:
+            # collective on every rank and pass: `now` is the step's agreed time
+            if self.assigner.is_event_time():
+                return []
+            return self._emit(self.op.advance_watermark(now))
         out = self._flush()
         if self.op is not None and not self.assigner.is_event_time():
             out.extend(self._emit(self.op.advance_watermark(now)))
@@ -621,6 +661,130 @@ class NativeWindowOp(_ColumnInput, Operator):
 _ = LONG_MAX
 
 
+class DeviceTemplates:
+    """Keep-first template fields of a rolling aggregate's keys on the device (Flink's
+    ``max(p)`` keeps the first record's other fields, ComputeCpuMax.java:26): one column per
+    output field indexed by dictionary id, plus a `have` mask and each key's output subtask.
+
+    A batch's first occurrence of every key without a template wins (scatter-amin of the row
+    index, then masked selects over the table -- no host sync). At G > 1 the table is
+    replicated: the winner of a key is the smallest (rank, row) over the ranks (one MIN
+    all-reduce of the table's codes), and every field is merged by a SUM all-reduce of the
+    winner's value (zeros elsewhere, so the sum is exact) -- the ranks' dictionary ids agree,
+    so a key's template is the same row on every rank and the owner of the key finds it."""
+
+    def __init__(self, kinds, key_pos: int, val_pos: int, device, comm):
+        self.kinds = tuple(kinds)
+        self.key_pos, self.val_pos = key_pos, val_pos
+        self.device = device
+        self.comm = comm if comm is not None and comm.world > 1 else None
+        self.cap = 0
+        self.have = None
+        self.tpl: dict = {}
+        self.sub = None
+        self._sub_n = 0
+
+    @staticmethod
+    def _dtype(kind):
+        return {FK_STR: torch.int32, FK_DOUBLE: torch.float64}.get(kind, torch.int64)
+
+    def _grow(self, need: int) -> None:
+        if need <= self.cap:
+            return
+        cap = max(1024, 1 << max(0, need - 1).bit_length())
+        dev = self.device
+
+        def grown(t, dt):
+            g = torch.zeros(cap, dtype=dt, device=dev)
+            if t is not None:
+                g[:t.numel()] = t
+            return g
+        self.have = grown(self.have, torch.bool)
+        for j, k in enumerate(self.kinds):
+            if j not in (self.key_pos, self.val_pos):
+                self.tpl[j] = grown(self.tpl.get(j), self._dtype(k))
+        self.sub = grown(self.sub, torch.int32)
+        self.cap = cap
+
+    def _subtasks(self, nkeys: int, jhash, ctx) -> None:
+        """Output subtask (Java hash -> murmur -> key group -> subtask) of new dictionary ids."""
+        if nkeys <= self._sub_n:
+            return
+        ids = torch.arange(self._sub_n, nkeys, dtype=torch.int64, device=self.device)
+        kg = K.keygroups(ids, max_parallelism=ctx.max_parallelism, hash_mode=1, jhash=jhash)
+        P, MP = ctx.parallelism, ctx.max_parallelism
+        self.sub[self._sub_n:nkeys] = ((kg.to(torch.int64) * P) // MP).to(torch.int32)
+        self._sub_n = nkeys
+
+    def update(self, cb, nkeys: int, jhash, ctx) -> None:
+        """Take the templates of keys first seen in batch `cb` (None: no rows on this rank)."""
+        self._grow(max(nkeys, 1))
+        if jhash is not None:
+            self._subtasks(nkeys, jhash, ctx)
+        cap, dev = self.cap, self.device
+        n = cb.n if cb is not None else 0
+        first = torch.full((cap,), 1 << 62, dtype=torch.int64, device=dev)
+        if n:
+            kid = cb.cols[self.key_pos][:n].to(torch.int64)
+            first.scatter_reduce_(0, kid, torch.arange(n, dtype=torch.int64, device=dev),
+                                  reduce="amin")
+        new = (first < (1 << 62)) & ~self.have
+        if self.comm is None:
+            if not n:
+                return
+            idx = torch.where(new, first, torch.zeros_like(first))
+            for j, t in self.tpl.items():
+                col = cb.cols[j][:n].to(t.dtype)
+                self.tpl[j] = torch.where(new, col[idx], t)
+            self.have |= new
+            return
+        # G > 1: the smallest (rank, row) over the ranks wins each new key
+        code = torch.where(new, (self.comm.rank << 40) + first,
+                           torch.full_like(first, K.I64_MAX))
+        self.comm.allreduce_min_(code)
+        won = code != K.I64_MAX
+        if not bool(won.any()):  # (all ranks agree: the reduced codes are identical)
+            return
+        mine = won & ((code >> 40) == self.comm.rank)
+        idx = torch.where(mine, code & ((1 << 40) - 1), torch.zeros_like(code))
+        for j, t in self.tpl.items():
+            if n:
+                col = cb.cols[j][:n].to(t.dtype)
+                part = torch.where(mine, col[idx.clamp(max=n - 1)], torch.zeros_like(t))
+            else:
+                part = torch.zeros_like(t)
+            self.comm.allreduce_sum_(part)
+            self.tpl[j] = torch.where(won, part, t)
+        self.have |= won
+
+    def rows(self, key: torch.Tensor, val: torch.Tensor) -> list:
+        """Output columns of emitted rows (key id, value, templates gathered by key id)."""
+        cols = []
+        for j in range(len(self.kinds)):
+            if j == self.key_pos:
+                cols.append(key.to(torch.int32))
+            elif j == self.val_pos:
+                cols.append(val)
+            else:
+                cols.append(self.tpl[j][key])
+        return cols
+
+    def snapshot(self) -> dict:
+        return {"kinds": list(self.kinds), "cap": self.cap,
+                "have": None if self.have is None else self.have.cpu().numpy(),
+                "tpl": {j: t.cpu().numpy() for j, t in self.tpl.items()}}
+
+    def restore(self, snap: dict) -> None:
+        if not snap["cap"]:
+            return
+        self._grow(int(snap["cap"]))
+        n = len(snap["have"])
+        self.have[:n] = torch.from_numpy(snap["have"]).to(self.device)
+        for j, a in snap["tpl"].items():
+            self.tpl[int(j)][:len(a)] = torch.from_numpy(a).to(self.device)
+        self._sub_n = 0  # recomputed from the dictionary's Java hashes
+
+
 class NativeRollingOp(_ColumnInput, Operator):
     """``keyBy(k).sum/min/max(p)`` (StreamGroupedReduce + ComparableAggregator,
     ComputeCpuMax.java:26) on the native ``KeyedRollingOperator``: per micro-batch the records
@@ -645,16 +809,39 @@ class NativeRollingOp(_ColumnInput, Operator):
         self.is_float = None
         self.str_keys = None
 
+    device_input = None  # planner: (column kinds, shared ingest state) of a device-ingest input
+    event_ts = True      # planner: the device-ingest rows carry event timestamps
+
     def open(self, ctx):
         super().open(ctx)
         from ..ops.native import load
 
         self.dict = load().StringDict()
+        self.device_exchange = self.collective = False
+        self.dtpl = None  # device keep-first templates (DeviceTemplates), device batches only
+        comm = getattr(ctx, "comm", None)
+        if comm is not None and comm.world > 1 and self.device_input is not None:
+            # Multi-rank with device-ingest input and dictionary keys: the rolling operator
+            # partitions by key group and exchanges the records itself (RCCL all-to-all), the
+            # keep-first templates are a replicated device table merged by two all-reduces, and
+            # the per-record emit stays a device column batch -- nothing is pickled. (Rows with
+            # event timestamps keep the executor's exchange: the owner could not stamp them.)
+            kinds, shared = self.device_input
+            if (kinds[self.key_pos] != FK_STR or kinds[self.val_pos] == FK_STR
+                    or len(kinds) <= max(self.key_pos, self.val_pos) or self.event_ts):
+                return
+            self.dict = shared["dict"]
+            self.str_keys = True
+            self.comm = comm
+            if not self._build(1.0 if kinds[self.val_pos] == FK_DOUBLE else 1):
+                return
+            self.device_exchange = self.collective = True
+            self.dtpl = DeviceTemplates(kinds, self.key_pos, self.val_pos, self.op.device, comm)
 
     def _to_fallback(self):
         self.fallback = self.fallback_factory()
         self.fallback.open(self.ctx)
-        if self.templates:
+        if self.templates or self.dtpl is not None:
             raise RuntimeError("native rolling state cannot be handed to the host operator")
 
     def _build(self, v) -> bool:
@@ -666,10 +853,54 @@ class NativeRollingOp(_ColumnInput, Operator):
         agg = {("sum", False): K.AGG_SUM_I64, ("sum", True): K.AGG_SUM_F64,
                ("max", False): K.AGG_MAX_I64, ("max", True): K.AGG_MAX_F64,
                ("min", False): K.AGG_MIN_I64, ("min", True): K.AGG_MIN_F64}[(self.kind, self.is_float)]
+        comm = getattr(self, "comm", None)
+        multi = comm is not None and comm.world > 1
         self.op = KeyedRollingOperator(agg=agg, device=torch.device(self.device),
-                                       max_keys=self.max_keys, parallelism=1,
+                                       max_keys=self.max_keys, comm=comm if multi else None,
+                                       parallelism=self.ctx.parallelism if multi else 1,
+                                       max_parallelism=self.ctx.max_parallelism if multi else 128,
                                        batch_capacity=1024)
         return True
+
+    def _run_device(self, batches: list) -> list:
+        """Device-ingest batches with dictionary keys (G = 1, or every pass at G > 1): keys and
+        values go to the engine in place, the post-update value of every record comes back as
+        device rows, and the output is ONE device column batch -- key ids, keep-first template
+        fields gathered by key id, the value column, the key's subtask -- in arrival order
+        ((source rank, row) at G > 1). The print sink formats it natively."""
+        dev = self.op.device if self.op is not None else torch.device(self.device)
+        cb = concat_device(batches) if batches else None
+        n = cb.n if cb is not None else 0
+        if cb is not None:
+            kid = cb.cols[self.key_pos][:n].to(torch.int64)
+            v = cb.cols[self.val_pos][:n]
+            vals = v.view(torch.int64) if v.dtype == torch.float64 else v.to(torch.int64)
+        else:
+            kid = torch.empty(0, dtype=torch.int64, device=dev)
+            vals = torch.empty(0, dtype=torch.int64, device=dev)
+        self.dtpl.update(cb, len(self.dict), self._jhash_dev(), self.ctx)
+        self.op.process(kid.contiguous(), vals.contiguous(), to_host=False)
+        k = min(self.op.check(), self.op.out_key.numel())
+        if k == 0:
+            return []
+        tag = self.op.out_tag[:k]
+        order = torch.argsort(tag)  # (source rank, row): arrival order
+        key = self.op.out_key[:k][order]
+        val = self.op.out_val[:k][order]
+        ts = None
+        if cb is not None and cb.ts is not None and self.comm_world() == 1:
+            ts = cb.ts[:n][(tag[order] & 0xFFFFFFFF)]
+        cols = self.dtpl.rows(key, val.view(torch.float64) if self.is_float else val)
+        return [DeviceColumnBatch(k, cols, self.dtpl.kinds, self.dict, ts,
+                                  sub_dev=self.dtpl.sub[key])]
+
+    def comm_world(self) -> int:
+        c = getattr(self, "comm", None)
+        return c.world if c is not None else 1
+
+    def _jhash_dev(self):
+        jh = getattr(self.dict, "id_jh", None)
+        return jh
 
     def _key_id(self, k) -> int:
         if isinstance(k, str):
@@ -684,9 +915,38 @@ class NativeRollingOp(_ColumnInput, Operator):
             return k
         raise TypeError("unsupported key type for the native path")
 
+    def _device_ok(self, batches: list) -> bool:
+        """Device batches of dictionary keys and a numeric value (the device emit path)."""
+        if not batches or not all(isinstance(b, DeviceColumnBatch) for b in batches):
+            return False
+        kinds = batches[0].kinds
+        if len(kinds) <= max(self.key_pos, self.val_pos) or kinds[self.key_pos] != FK_STR \
+                or kinds[self.val_pos] == FK_STR or self.templates:
+            return False
+        if self.str_keys is False:
+            return False
+        return True
+
     def _run_columns(self, batches: list) -> list:
         """ColumnBatch input: key/value columns straight to the engine; the output (one row per
         input record, Flink's rolling emit) is built per row only for the host sink."""
+        if self._device_ok(batches):
+            b0 = batches[0]
+            if b0.strings is not self.dict:
+                if len(self.dict) and self.dtpl is None:
+                    batches = [b.host() for b in batches]
+                    return self._run_columns(batches)
+                self.dict = b0.strings
+            self.str_keys = True
+            vk = b0.kinds[self.val_pos]
+            if self.op is None and not self._build(1.0 if vk == FK_DOUBLE else 1):
+                raise TypeError("unsupported value")
+            if (vk == FK_DOUBLE) != self.is_float:
+                raise TypeError("mixed value types")
+            if self.dtpl is None:
+                self.dtpl = DeviceTemplates(b0.kinds, self.key_pos, self.val_pos, self.op.device,
+                                            None)
+            return self._run_device(batches)
         # One output row per input record goes to a host sink anyway: device batches come over.
         batches = [b.host() if isinstance(b, DeviceColumnBatch) else b for b in batches]
         try:
@@ -789,6 +1049,12 @@ class NativeRollingOp(_ColumnInput, Operator):
     def process(self, items):
         if self.fallback is not None:
             return self.fallback.process(expand_columns(items))
+        if self.device_exchange:
+            # one collective engine step per pass (empty if this rank got no rows)
+            data = [it for it in items if not isinstance(it, WM)]
+            if any(not isinstance(b, DeviceColumnBatch) for b in data):
+                raise TypeError("multi-rank native rolling: device-ingest batches expected")
+            return self._run_device(data) + [it for it in items if isinstance(it, WM)]
         out, pending = [], []
         for it in items:
             if isinstance(it, WM):
@@ -808,6 +1074,8 @@ class NativeRollingOp(_ColumnInput, Operator):
         if self.op is not None:
             es = self.op.snapshot_state()
             snap["engine"] = {"columns": es.columns, "meta": es.meta}
+        if self.dtpl is not None:
+            snap["device_templates"] = self.dtpl.snapshot()
         return snap
 
     def restore(self, snap: dict) -> None:
@@ -820,9 +1088,16 @@ class NativeRollingOp(_ColumnInput, Operator):
         self.str_keys = snap["str_keys"]
         for st in snap["strings"]:
             self.dict.intern(st)
-        if "engine" in snap:
+        if "engine" in snap and self.op is None:
             self._build(1.0 if snap["is_float"] else 1)
+        if "engine" in snap:
             self.op.restore_state(snap["engine"]["columns"], snap["engine"]["meta"])
+        dt = snap.get("device_templates")
+        if dt is not None:
+            if self.dtpl is None:
+                self.dtpl = DeviceTemplates(tuple(dt["kinds"]), self.key_pos, self.val_pos,
+                                            self.op.device, None)
+            self.dtpl.restore(dt)
 
 
 class NativeCountWindowOp(NativeRollingOp):
@@ -906,13 +1181,39 @@ class NativeSessionOp(NativeWindowOp):
                ("count", False): K.AGG_COUNT, ("count", True): K.AGG_COUNT,
                ("avg", False): K.AGG_AVG_I64, ("avg", True): K.AGG_AVG_F64}[(self.kind, is_float)]
         self.is_float = is_float
+        comm = getattr(self, "comm", None)
+        multi = comm is not None and comm.world > 1
+        # G > 1: the session operator partitions by key group and exchanges its records itself
+        # (RCCL all-to-all inside process()); firing is local to each key's owner.
         self.op = KeyedSessionOperator(gap=self.assigner.gap, lateness=self.lateness, agg=agg,
                                        device=torch.device(self.device), max_keys=self.max_keys,
-                                       parallelism=1, batch_capacity=max(1024, self.ctx.parallelism),
+                                       comm=comm if multi else None,
+                                       parallelism=self.ctx.parallelism if multi else 1,
+                                       max_parallelism=self.ctx.max_parallelism if multi else 128,
+                                       batch_capacity=max(1024, self.ctx.parallelism),
                                        external_watermark=True)
         return True
 
+    def _result_column(self, raw: np.ndarray, values: np.ndarray, counts: np.ndarray):
+        """(column, kind) of the window result of fired rows."""
+        if self.kind in ("sum", "min", "max"):
+            r = raw.view(np.int64) if raw.dtype == np.uint64 else raw.astype(np.int64)
+            return (r.view(np.float64), FK_DOUBLE) if self.is_float else (r, FK_LONG)
+        if self.kind == "count":
+            return counts.astype(np.int64), FK_LONG
+        return values.astype(np.float64, copy=False), FK_DOUBLE
+
     def _emit(self, rows) -> list:
+        if not len(rows):
+            return []
+        if self.scalar_result:
+            col, k = self._result_column(np.asarray(rows.raw), np.asarray(rows.values),
+                                         np.asarray(rows.counts))
+            keys = np.asarray(rows.keys)
+            keys = keys.view(np.int64) if keys.dtype == np.uint64 else keys.astype(np.int64)
+            return [ColumnBatch(int(keys.size), [col], (k,), None,
+                                np.asarray(rows.end, dtype=np.int64) - 1, self._subtasks(keys),
+                                True)]
         out = []
         P, MP = self.ctx.parallelism, self.ctx.max_parallelism
         from ..utils.hashing import flink_murmur
@@ -952,9 +1253,51 @@ class NativeMedianOp(NativeWindowOp):
             size=a.size, slide=a.slide, offset=a.offset,
             lateness=self.lateness if a.is_event_time() else 0, device=torch.device(self.device),
             time_mode="event" if a.is_event_time() else "processing")
+        comm = getattr(self, "comm", None)
+        if comm is not None and comm.world > 1:
+            # G > 1: the pane arena holds this rank's key groups; records reach their owner by
+            # one row all-to-all per pass (parallel/exchange.py), firing is local
+            P, MP = self.ctx.parallelism, self.ctx.max_parallelism
+            kgd = [((kg * P // MP) * comm.world) // P for kg in range(MP)]
+            self._kg_dest = torch.tensor(kgd, dtype=torch.int64, device=torch.device(self.device))
         return True
 
+    def _process_exchange(self, items) -> list:
+        """G > 1: this rank's (key id, ts, value) rows to the owners of their key groups, the
+        owner's pane arena folds them; the merged watermark fires each rank's own keys."""
+        from ..parallel.exchange import exchange_rows
+
+        data = [it for it in items if not isinstance(it, WM)]
+        wms = [it.ts for it in items if isinstance(it, WM)]
+        kid, ts, vals = self._local_columns(data)
+        kid = kid.to(torch.int64)
+        kg = K.keygroups(kid, max_parallelism=self.ctx.max_parallelism,
+                         hash_mode=1 if self.str_keys else 0,
+                         jhash=self._jhash() if self.str_keys else None)
+        kid, ts, vals = exchange_rows(self.comm, self._kg_dest[kg.to(torch.int64)],
+                                      [kid, ts, vals])
+        late_before = self.op.metrics.num_late_records_dropped
+        out = self._emit(self.op.process(kid, ts, vals)) if kid.numel() else []
+        self.num_late_records_dropped += self.op.metrics.num_late_records_dropped - late_before
+        event = self.assigner.is_event_time()
+        for w in wms:
+            self.wm = w
+            if event:
+                out.extend(self._emit(self.op.advance_watermark(w)))
+            out.append(WM(w))
+        return out
+
     def _emit(self, fired) -> list:
+        fired = [f for f in fired if len(f[2])]
+        if not fired:
+            return []
+        if self.scalar_result:
+            keys = np.concatenate([np.asarray(f[2]) for f in fired]).astype(np.int64)
+            med = np.concatenate([np.asarray(f[3]) for f in fired]).astype(np.float64)
+            ts = np.repeat(np.array([f[1] - 1 for f in fired], dtype=np.int64),
+                           [len(f[2]) for f in fired])
+            return [ColumnBatch(int(keys.size), [med], (FK_DOUBLE,), None, ts,
+                                self._subtasks(keys), True)]
         out = []
         P, MP = self.ctx.parallelism, self.ctx.max_parallelism
         from ..utils.hashing import flink_murmur
@@ -976,6 +1319,7 @@ class NativeVectorWindowOp(NativeWindowOp):
     input length. Windows and watermarks behave exactly as in NativeWindowOp."""
 
     name = "VectorWindow(native)"
+    _exchange_ok = False  # vector rows come from host records (no device ingest of vectors)
 
     def _build(self, sample_val, dense: bool = False) -> bool:
         if not isinstance(sample_val, (list, tuple)) or not sample_val \

@@ -896,8 +896,18 @@ class PrintSinkOp(Operator):
             sub = np.ascontiguousarray(sub[:cb.n], dtype=np.int32)
             keep.append(sub)
         nsub = int(sub.max()) + 1 if sub is not None else 1
+        as_tuple = not getattr(cb, "scalar", False)
+        raw = getattr(self.writer, "raw", None)
+        if raw is not None:
+            # one bytes object formatted by native threads (no Python string per row)
+            import os
+
+            raw(load().java_format_bytes(cols, cb.n, names, 0 if sub is None else sub.ctypes.data,
+                                         self._prefixes(nsub), as_tuple,
+                                         min(16, os.cpu_count() or 1)))
+            return
         lines = load().java_format_rows(cols, cb.n, names, 0 if sub is None else sub.ctypes.data,
-                                        self._prefixes(nsub), True)
+                                        self._prefixes(nsub), as_tuple)
         many = getattr(self.writer, "many", None)
         if many is not None:
             many(lines)

@@ -923,6 +923,8 @@ class KeyedSessionOperator:
             self._occ_pin = torch.zeros(2, dtype=torch.int64, pin_memory=True)
         c = torch.stack([((k != EMPTY_KEY) & (k != TOMB_KEY)).sum(), (k != EMPTY_KEY).sum()])
         self._occ_pin.copy_(c, non_blocking=True)
+        # estimates at the launch: the landed exact counts are corrected by what changed since
+        self._occ_base = (self._live_estimate, self._tombs_bound)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
         self._occ_pending = ev
@@ -960,6 +962,14 @@ class KeyedSessionOperator:
             if stale is not None and due(*stale):
                 self._rehash()
                 self._tombs_bound = 0
+            elif stale is not None:
+                # Not due: tighten the estimates from the exact counts (plus the inserts and
+                # evictions counted since the launch), so the bound stops re-launching the scan
+                # every step until a rehash.
+                live0, tombs0 = self._occ_base
+                self._live_estimate = stale[0] + (self._live_estimate - live0)
+                self._tombs_bound = (stale[1] - stale[0]) + (self._tombs_bound - tombs0)
+                live = self._live_estimate
             elif due(live, live + self._tombs_bound) and self._occ_pending is None:
                 self._occ_launch()
         if live > self.max_load * self.nslots and wm > I64_MIN:

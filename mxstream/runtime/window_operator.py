@@ -1168,6 +1168,7 @@ class KeyedWindowOperator:
 
     # ---- host-DRAM spill tier (runtime/window_spill.py) -----------------------------------
     def _maybe_spill(self) -> None:
+        self._verify_combine()  # the occupancy must include a redone combined step's inserts
         cap = 1 << self.cap_log2
         if int(self.occ.max()) <= self.spill_load * cap or self.max_seen_pane is None:
             return
@@ -1177,6 +1178,7 @@ class KeyedWindowOperator:
     def compact_state(self, cutoff_pane: int | None = None) -> dict:
         """Table maintenance at a step boundary: drop keys without live data and (with the spill
         tier) move keys whose newest data pane is <= cutoff_pane to host DRAM. Returns counts."""
+        self._verify_combine()  # a combined step skipped on the device is redone before this
         if self.dense_bits:
             return {"dropped": 0, "evicted": 0, "rows": 0}
         if cutoff_pane is not None and self.host_tier is None:

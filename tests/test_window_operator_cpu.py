@@ -614,3 +614,29 @@ def test_cxx_window_tier_equals_numpy_combine(n):
     assert t.nrows == int((cols["pane"] >= 15).sum()) and t.pane_range() == (15, 19)
     r = t.rows()
     assert int(r["cnt"].sum()) == int(cols["cnt"][cols["pane"] >= 15].sum())
+
+
+def test_cxx_window_tier_purge_never_rewinds():
+    """A purge with a cutoff below an earlier purge's (15, then 12) leaves the tier as the first
+    purge left it: dead rows stay dead, counts do not wrap (csrc/window_tier.h purge)."""
+    from mxstream.runtime.window_spill import HostWindowTier
+
+    rng = np.random.default_rng(9)
+    t = HostWindowTier(K.AGG_SUM_I64)
+    n = 5000
+    pane = rng.integers(10, 20, n).astype(np.int64)
+    cnt = rng.integers(1, 5, n).astype(np.int64)
+    t.absorb(rng.integers(0, 3000, n).astype(np.uint64), pane,
+             rng.integers(-9, 9, n).astype(np.int64), cnt, np.zeros(n, np.uint8))
+    t.purge(13)  # lazy: below 13 is less than half -> rows marked dead
+    keep = int((pane >= 13).sum())
+    assert t.nrows == keep
+    t.purge(12)
+    assert t.nrows == keep and t.pane_range() == (13, 19)
+    r = t.copy().rows()
+    assert int(r["pane"].min()) == 13 and int(r["cnt"].sum()) == int(cnt[pane >= 13].sum())
+    t.purge(17)  # filter branch (more than half below)
+    t.purge(15)
+    assert t.nrows == int((pane >= 17).sum())
+    r = t.rows()
+    assert int(r["pane"].min()) == 17 and int(r["cnt"].sum()) == int(cnt[pane >= 17].sum())
