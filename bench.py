@@ -56,6 +56,13 @@ def main() -> int:
                          "for the p50/p99 alert latency (0: timed firings only)")
     ap.add_argument("--no-hashed-figure", action="store_true",
                     help="skip the untimed-in-headline hashed-key run reported next to it")
+    ap.add_argument("--exchange", choices=["auto", "partials", "records"], default="auto",
+                    help="G > 1 keyBy strategy of the headline: partials = local-global "
+                         "aggregation (partial accumulators cross one all-to-all per fired "
+                         "window), records = every step's (key, pane)-combined records cross the "
+                         "all-to-all to the key's owner (hashed state); auto = partials")
+    ap.add_argument("--no-records-figure", action="store_true",
+                    help="G > 1: skip the per-event-exchange (records) run reported next to it")
     a = ap.parse_args()
 
     if os.environ.get("MXS_SPIN") == "1" and a.device == "cuda":
@@ -76,9 +83,13 @@ def main() -> int:
     else:
         device = torch.device("cpu")
 
+    # records exchange: every event reaches its key's owner, whose table holds a key share
+    # (hashed state: dense dictionary-id slots need one destination per event)
+    records = a.exchange == "records" and comm.world > 1
     cfg = TumblingBenchConfig(keys=a.keys, batch=a.batch, cap_log2=a.cap_log2,
-                              dense_keys=not a.hashed_keys, key32=a.int32_keys, zipf=a.zipf,
-                              pipeline=False if a.no_pipeline else None)
+                              dense_keys=not a.hashed_keys and not records, key32=a.int32_keys,
+                              zipf=a.zipf, pipeline=False if a.no_pipeline else None,
+                              exchange=a.exchange)
     bench = TumblingWindowBench(cfg, comm, device)
     if a.trace:
         from mxstream.utils import trace
@@ -179,30 +190,42 @@ def main() -> int:
     comm.allreduce_max_(lt)
     # The same step on hashed keyed state (arbitrary int64 keys: open-addressing sub-tables
     # instead of the dense dictionary-id bijection), timed the same way, reported next to it.
-    hashed = None
-    if not a.no_hashed_figure and not a.hashed_keys:
-        hcfg = TumblingBenchConfig(keys=a.keys, batch=a.batch, cap_log2=a.cap_log2,
-                                   dense_keys=False, zipf=a.zipf,
-                                   pipeline=False if a.no_pipeline else None)
-        del bench
-        hb = TumblingWindowBench(hcfg, comm, device)
+    def side_run(xcfg) -> tuple[float, float]:
+        """The same timed loop on another configuration: (node events/s, ms per step)."""
+        xb = TumblingWindowBench(xcfg, comm, device)
         for _ in range(a.warmup):
-            hb.step()
+            xb.step()
         sync()
         comm.barrier()
         sync()
         th = time.perf_counter()
         for _ in range(a.steps):
-            hb.step()
-        hb.drain()
+            xb.step()
+        xb.drain()
         sync()
         comm.barrier()
         sync()
         tt = torch.tensor([time.perf_counter() - th], dtype=torch.float64, device=device)
         comm.allreduce_max_(tt)
-        hashed = {"hashed_events_per_s": a.batch * a.steps * comm.world / float(tt.item()),
-                  "hashed_ms_per_step": float(tt.item()) / a.steps * 1e3}
-        bench = hb
+        return a.batch * a.steps * comm.world / float(tt.item()), float(tt.item()) / a.steps * 1e3
+
+    hashed = None
+    if not a.no_hashed_figure and not a.hashed_keys and not records:
+        del bench
+        ev_s, ms = side_run(TumblingBenchConfig(keys=a.keys, batch=a.batch, cap_log2=a.cap_log2,
+                                                dense_keys=False, zipf=a.zipf,
+                                                pipeline=False if a.no_pipeline else None,
+                                                exchange=a.exchange))
+        hashed = {"hashed_events_per_s": ev_s, "hashed_ms_per_step": ms}
+    # G > 1 and a partials headline: the per-event keyBy shuffle (BASELINE config 3's
+    # "all-to-all") measured the same way, reported next to it (not the headline value).
+    recfig = None
+    if comm.world > 1 and not records and not a.no_records_figure:
+        ev_s, ms = side_run(TumblingBenchConfig(keys=a.keys, batch=a.batch, cap_log2=a.cap_log2,
+                                                dense_keys=False, zipf=a.zipf,
+                                                pipeline=False if a.no_pipeline else None,
+                                                exchange="records"))
+        recfig = {"records_events_per_s": ev_s, "records_ms_per_step": ms}
 
     n = comm.world
     events = a.batch * a.steps * n
@@ -230,8 +253,10 @@ def main() -> int:
             "firings_for_latency": int(lt[2].item()),
             "alerts": int(al.item()),
             "late_dropped": op_metrics.num_late_records_dropped,
-            # untimed extra run, NOT the headline: the same job on hashed keyed state
+            # untimed extra runs, NOT the headline: the same job on hashed keyed state, and
+            # (G > 1) with the per-event records exchange instead of local-global partials
             **(hashed or {}),
+            **(recfig or {}),
             "config": {
                 "model": "chapter3 1-min tumbling event-time window sum (BandwidthMonitorWithEventTime shape), 1M keys",
                 "global_batch": a.batch * n,
@@ -254,7 +279,7 @@ def main() -> int:
         print(json.dumps(out), flush=True)
     if wd is not None:
         wd.stop()
-    if a.trace:
+    if a.trace and "bench" in locals():
         from mxstream.utils import trace
 
         if bench.op.timer is not None:

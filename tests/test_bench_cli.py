@@ -33,3 +33,19 @@ def test_bench_two_ranks_gloo():
     assert d["config"]["global_batch"] == 2 * 32768
     assert d["alerts"] > 0 and d["value"] > 0
     assert abs(d["value"] - 2 * 32768 * 14 / (d["ms_per_step"] * 14 / 1e3)) / d["value"] < 1e-6
+    # the per-event keyBy shuffle is measured next to the local-global headline
+    assert d["records_events_per_s"] > 0 and d["records_ms_per_step"] > 0
+
+
+def test_bench_two_ranks_records_exchange():
+    """--exchange records: the headline itself is the per-event all-to-all (hashed state)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+           "--device", "cpu", "--batch", "32768", "--keys", "5000", "--steps", "14",
+           "--warmup", "1", "--exchange", "records"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["config"]["exchange"] == "records" and d["config"]["keyed_state"] == "hashed"
+    assert d["alerts"] > 0 and "records_events_per_s" not in d
