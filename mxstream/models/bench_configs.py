@@ -217,7 +217,8 @@ def config2_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 5
 
 
 def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_000,
-            device: str = "cuda", dense_keys: bool = True, pipeline="stream") -> dict:
+            device: str = "cuda", dense_keys: bool = True, pipeline="stream",
+            latency_fire: int = 0) -> dict:
     """Sliding 1 min / 10 s event-time window sum + 30 s allowed lateness, 10M keys; 5 % of
     events arrive up to 40 s late (within lateness -> re-firings)."""
     dev = torch.device(device)
@@ -230,7 +231,8 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
                              device=dev, max_keys=keys, batch_capacity=batch, ooo_bound=5_000,
                              map_prog=E.compile_expr(mbps),
                              filter_prog=E.compile_expr(E.var(E.VAR_MAPPED) < thr),
-                             dense_keys=dense_keys, pipeline=pipeline, emit="key_value")
+                             dense_keys=dense_keys, pipeline=pipeline, emit="key_value",
+                             latency_fire=latency_fire)
     # dense keyed state: the keys are dictionary ids (int32, as the columnar ingest emits them)
     kt = torch.empty(batch, dtype=torch.int32 if dense_keys else torch.int64, device=dev)
     tt = torch.empty(batch, dtype=torch.int64, device=dev)
@@ -279,7 +281,11 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
     dt = time.perf_counter() - t0
     return {"config": 4, "warmup": warmup, "keyed_state": "dense" if dense_keys else "hashed", "metric": "events/sec (sliding 1min/10s + lateness, 10M keys)",
             "value": batch * steps / dt, "unit": "events/s", "ms_per_step": dt / steps * 1e3,
-            "p50_alert_latency_ms": statistics.median(lat) if lat else None, "alerts": alerts,
+            "p50_alert_latency_ms": statistics.median(lat) if lat else None,
+            "p99_alert_latency_ms": (sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))]
+                                     if lat else None),
+            "firings_measured": len(lat), "latency_fire": latency_fire,
+            "latency_fire_steps": op.metrics.extra.get("latency_fires", 0), "alerts": alerts,
             "late_dropped": op.metrics.num_late_records_dropped, "keys": keys,
             "events_per_step": batch, "state_bytes": op.state_bytes(), "device": str(dev)}
 
@@ -396,7 +402,11 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
     mt = op.metrics
     return {"config": 5, "metric": "events/sec (session-window alert + host-DRAM spill)",
             "value": batch * steps / dt, "unit": "events/s", "ms_per_step": dt / steps * 1e3,
-            "p50_alert_latency_ms": statistics.median(lat) if lat else None, "alerts": alerts,
+            "p50_alert_latency_ms": statistics.median(lat) if lat else None,
+            "p99_alert_latency_ms": (sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))]
+                                     if lat else None),
+            "firings_measured": len(lat), "latency_fire": latency_fire,
+            "latency_fire_steps": op.metrics.extra.get("latency_fires", 0), "alerts": alerts,
             "late_dropped": mt.num_late_records_dropped - m0["num_late_records_dropped"],
             "spilled_keys": mt.spilled_keys - m0["spilled_keys"],
             "records_to_host": mt.records_to_host - m0["records_to_host"],
@@ -464,7 +474,11 @@ def config6(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 1_000_000
     return {"config": 6, "metric": "events/sec (vector-metric tumbling window avg, MFMA reduce)",
             "value": batch * steps / dt, "unit": "events/s", "ms_per_step": dt / steps * 1e3,
             "metric_values_per_sec": batch * steps * dim / dt,
-            "p50_alert_latency_ms": statistics.median(lat) if lat else None, "alerts": alerts,
+            "p50_alert_latency_ms": statistics.median(lat) if lat else None,
+            "p99_alert_latency_ms": (sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))]
+                                     if lat else None),
+            "firings_measured": len(lat), "latency_fire": latency_fire,
+            "latency_fire_steps": op.metrics.extra.get("latency_fires", 0), "alerts": alerts,
             "keys": keys, "dim": dim, "events_per_step": batch, "mode": "mfma" if mfma else "valu",
             "key_distribution": f"zipf({zipf:g})" if zipf > 0 else "uniform",
             "state_bytes": op.state_bytes(), "device": str(dev)}
@@ -645,6 +659,9 @@ def main(argv=None) -> int:
     ap.add_argument("--sort-path", action="store_true",
                     help="config 2: the radix-sort rolling path instead of the sort-free one")
     ap.add_argument("--keys", type=int, default=None, help="config 2: key space (default 10k)")
+    ap.add_argument("--latency-fire", type=int, default=0,
+                    help="config 4: fire right away when at most this many windows are due "
+                         "(latency-bounded mode; 0 = pipelined firing)")
     ap.add_argument("--threads", type=int, default=4,
                     help="config 1 CPU path: parse threads (the reference job runs at P = 4)")
     a = ap.parse_args(argv)
@@ -663,7 +680,7 @@ def main(argv=None) -> int:
         r = config4_spill(a.steps, a.warmup, a.batch or (1 << 22), device=a.device)
     elif a.config == 4:
         r = config4(a.steps, a.warmup, a.batch or (1 << 24), device=a.device,
-                    dense_keys=not a.hashed_keys)
+                    dense_keys=not a.hashed_keys, latency_fire=a.latency_fire)
     elif a.config == 7:
         r = config7(lines=a.lines or 16_000_000, device=a.device,
                     batch_lines=a.batch or (1 << 20), profile=a.profile)

@@ -356,7 +356,8 @@ class KeyedWindowOperator:
                  pipeline: bool | str | None = None, exchange: str = "auto",
                  idle_timeout_steps: int | None = None, deterministic: bool = False,
                  spill: bool = False, spill_load: float = 0.8, spill_check_steps: int = 8,
-                 spill_keep_panes: int | None = None, emit: str = "full"):
+                 spill_keep_panes: int | None = None, emit: str = "full",
+                 latency_fire: int = 0):
         """deterministic: f64 sums/averages accumulate each step's per-slot sum in 128-bit fixed
         point (order-independent integer adds, one rounding per slot and step), so results are
         bit-identical between runs, between the GPU and the C++ twin, and independent of the
@@ -366,11 +367,19 @@ class KeyedWindowOperator:
 
         emit: "full" fired rows carry (key, mapped value, raw accumulator, count); "key_value"
         only (key id, mapped value) -- 12 bytes a row instead of 28 from the fire kernel to the
-        host (dense keys; FireResult.raw / counts are None) for sinks that read nothing else."""
+        host (dense keys; FireResult.raw / counts are None) for sinks that read nothing else.
+
+        latency_fire = N > 0 (pipelined mode): a step whose watermark makes at most N windows due
+        (first firings and late-data re-firings) runs its state half right away instead of one
+        call later, and its firings are resolved before the call returns -- the alert leaves in
+        the call of the batch that triggered it (one step of latency, not two or three), at the
+        cost of that step's overlap with the next partition. Steps firing more windows (a
+        watermark jump) keep the pipelined, batched path."""
         self.device = K.resolve_device(device)
         if emit not in ("full", "key_value"):
             raise ValueError("emit must be 'full' or 'key_value'")
         self.emit = emit
+        self.latency_fire = max(0, int(latency_fire))
         self.deterministic = bool(deterministic) and agg in (K.AGG_SUM_F64, K.AGG_AVG_F64)
         # spill: host-DRAM tier for hashed keys (runtime/window_spill.py). Every
         # `spill_check_steps` steps, a sub-table above `spill_load` of its slots triggers
@@ -890,10 +899,34 @@ class KeyedWindowOperator:
         f = self._front(keys, ts, vals)     # partition of this batch (S0)
         if prev is not None:
             out += self._back_finish(prev)
-        self._pending = self._settle(f)     # the step's one host sync (S1 keeps working)
+        b = self._settle(f)                 # the step's one host sync (S1 keeps working)
+        if self.latency_fire and 0 < self._due_windows(b) <= self.latency_fire:
+            # Latency-bounded firing: this batch's firings leave in this call.
+            with self._s1():
+                self._back_begin(b)
+            out += self._back_finish(b)
+            self.metrics.extra["latency_fires"] = self.metrics.extra.get("latency_fires", 0) + 1
+            return self._resolve(out, block=True)
+        self._pending = b
         # Firings whose rows have reached the host are returned now; the others stay queued
         # (in order) for the next call -- the host never waits on a fire's copy here.
         return self._resolve(out, block=False)
+
+    def _due_windows(self, b: "_Back") -> int:
+        """Windows the state half of settled step `b` will fire or re-fire (host bookkeeping,
+        an upper bound: windows without live panes are counted too)."""
+        n = 0
+        if b.has_data and b.gmin <= b.fired_hi:  # late-but-allowed data: re-firings
+            s0 = self.first_start_containing(self.pane_start(b.gmin))
+            s1 = min(self.next_fire_start - self.slide,
+                     self.last_start(self.pane_start(min(b.gmax, b.fired_hi))))
+            if s1 >= s0:
+                n += (s1 - s0) // self.slide + 1
+        if b.new_wm is not None and self.next_fire_start is not None:
+            last = b.new_wm - self.size + 1  # windows with start <= last are due
+            if last >= self.next_fire_start:
+                n += (last - self.next_fire_start) // self.slide + 1
+        return n
 
     def flush(self) -> list[FireResult]:
         """Complete the pending state half of the last batch (pipelined mode); returns what it
