@@ -5,6 +5,7 @@
   python -m mxstream.models.bench_configs --config 4   # sliding 1 min / 10 s + lateness, 10M keys
   python -m mxstream.models.bench_configs --config 5   # session alert + host-DRAM spill
   python -m mxstream.models.bench_configs --config 6   # vector-metric window avg (MFMA reduce)
+  python -m mxstream.models.bench_configs --config 9   # ComputeCpuMax through env.execute (file)
 
 Each prints one JSON line: events/s and the step time (and p50 alert latency where alerts fire).
 Config 1 runs the reference's exact text path: Java-semantics split + Double.parseDouble in the
@@ -572,6 +573,103 @@ def bandwidth_text(lines: int, channels: int = 1_000, seed: int = 7) -> np.ndarr
     return out.reshape(-1)
 
 
+def cpu_metric_text(lines: int, hosts: int = 10_000, seed: int = 11) -> np.ndarray:
+    """Synthetic chapter1/2 input ``ts ip cpuN usage`` (Main.java:21-24, ComputeCpuMax.java:20-23)
+    as fixed-width lines built with numpy: epoch seconds, an IPv4-like host name out of `hosts`,
+    cpu0..cpu63, usage with one decimal (``dd.d``)."""
+    rng = np.random.default_rng(seed)
+    hn = np.frombuffer("".join(f"10.{i // 65536 % 256:03d}.{i // 256 % 256:03d}.{i % 256:03d}"
+                               for i in range(hosts)).encode(), np.uint8).reshape(hosts, 14)
+    cn = np.frombuffer("".join(f"cpu{c:02d}" for c in range(64)).encode(), np.uint8).reshape(64, 5)
+    h = rng.integers(0, hosts, lines)
+    c = rng.integers(0, 64, lines)
+    u = rng.integers(0, 1000, lines)  # usage * 10
+    w = 10 + 1 + 14 + 1 + 5 + 1 + 4 + 1
+    out = np.empty((lines, w), np.uint8)
+    t = 1_563_452_000 + np.arange(lines, dtype=np.int64) // max(1, lines // 3600)
+    for k in range(9, -1, -1):
+        out[:, k] = 48 + (t % 10)
+        t //= 10
+    out[:, 10] = 32
+    out[:, 11:25] = hn[h]
+    out[:, 25] = 32
+    out[:, 26:31] = cn[c]
+    out[:, 31] = 32
+    out[:, 32] = 48 + u // 100
+    out[:, 33] = 48 + (u // 10) % 10
+    out[:, 34] = 46
+    out[:, 35] = 48 + u % 10
+    out[:, w - 1] = 10
+    return out.reshape(-1)
+
+
+class _ByteCounter:
+    """print() target of the API benches: takes the native formatter's bytes (every output row
+    is formatted -- Tuple/Double.toString, subtask prefix -- and counted, not written)."""
+
+    def __init__(self):
+        self.lines = 0
+        self.bytes = 0
+
+    def __call__(self, s: str) -> None:
+        self.lines += 1
+        self.bytes += len(s) + 1
+
+    def raw(self, data: bytes) -> None:
+        self.lines += data.count(b"\n")
+        self.bytes += len(data)
+
+
+def config9(lines: int = 16_000_000, hosts: int = 10_000, device: str = "cuda",
+            batch_lines: int = 1 << 20, text_ingest: str = "auto") -> dict:
+    """The reference's ComputeCpuMax job (ComputeCpuMax.java:15-27: keyBy(0).max(2), one output
+    record per input record) through the DataStream API over a text file: readTextFile ->
+    map(parse) -> keyBy(host) -> max(usage) -> print. On a GPU: device ingest (dictionary ids),
+    the rolling max on the device, the per-record emit as ONE device column batch per micro-batch
+    (keep-first template fields gathered by key id), formatted by the native threaded formatter.
+    Lines per second end to end (wall clock of env.execute, every output line formatted)."""
+    import os
+    import tempfile
+
+    from ..api.environment import StreamExecutionEnvironment
+    from . import chapters as C
+
+    text = cpu_metric_text(lines, hosts)
+    fd, path = tempfile.mkstemp(suffix=".txt")
+    with os.fdopen(fd, "wb") as f:
+        f.write(text.tobytes())
+    line_w = text.size // max(lines, 1)
+    fd, head = tempfile.mkstemp(suffix=".txt")
+    with os.fdopen(fd, "wb") as f:
+        f.write(text[:50_000 * line_w].tobytes())
+    del text
+
+    def run(file, batch):
+        sink = _ByteCounter()
+        env = StreamExecutionEnvironment(4).set_output(sink)
+        env.config.native = "auto"
+        env.config.device = device
+        env.config.batch_size = batch
+        env.config.text_ingest = text_ingest
+        C.build_compute_cpu_max(env, env.read_text_file(file))
+        t = time.perf_counter()
+        env.execute("ComputeCpuMax")
+        return time.perf_counter() - t, sink
+
+    try:
+        run(head, batch_lines)  # warm-up job (module loads, code objects, pinned slots)
+        dt, sink = run(path, batch_lines)
+    finally:
+        os.unlink(path)
+        os.unlink(head)
+    return {"config": 9, "metric": "lines/sec through the DataStream API (file replay)",
+            "value": lines / dt, "unit": "lines/s", "seconds": dt, "output_lines": sink.lines,
+            "output_bytes": sink.bytes, "lines": lines, "bytes_per_line": line_w, "hosts": hosts,
+            "batch_lines": batch_lines, "job": "ComputeCpuMax (keyBy(0).max(2), rolling emit)",
+            "ingest": ("device" if text_ingest == "device" or str(device).startswith("cuda")
+                       else "host"), "device": device}
+
+
 def config7(lines: int = 16_000_000, channels: int = 1_000, device: str = "cuda",
             batch_lines: int = 1 << 20, profile: bool = False) -> dict:
     """The reference's BandwidthMonitorWithEventTime job (BandwidthMonitorWithEventTime.java:25-57)
@@ -637,7 +735,7 @@ def config7(lines: int = 16_000_000, channels: int = 1_000, device: str = "cuda"
 
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 4, 5, 6, 7, 8])
+    ap.add_argument("--config", type=int, required=True, choices=[1, 2, 4, 5, 6, 7, 8, 9])
     ap.add_argument("--dim", type=int, default=32, help="config 6: metric vector width")
     ap.add_argument("--valu", action="store_true", help="config 6: VALU instead of MFMA reduce")
     ap.add_argument("--zipf", type=float, default=0.0, help="config 6: power-law key skew")
@@ -684,6 +782,9 @@ def main(argv=None) -> int:
     elif a.config == 7:
         r = config7(lines=a.lines or 16_000_000, device=a.device,
                     batch_lines=a.batch or (1 << 20), profile=a.profile)
+    elif a.config == 9:
+        r = config9(lines=a.lines or 16_000_000, device=a.device,
+                    batch_lines=a.batch or (1 << 20))
     elif a.config == 8:
         r = config8(a.steps, a.warmup, a.batch or (1 << 22), device=a.device)
     elif a.config == 6:
