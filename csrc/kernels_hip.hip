@@ -81,6 +81,24 @@ __device__ __forceinline__ uint64_t f64_unord(int64_t o) {
 // Synthetic source: SoA (key, ts, val) batch from a counter-based RNG (device-side so the
 // benchmark measures the engine, not PCIe).
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void gen_one(uint64_t seed, uint64_t stream_id, uint64_t idx,
+                                        int64_t i, uint64_t nkeys, int64_t ts_base,
+                                        double span_per_event, uint64_t disorder_p1,
+                                        int64_t val_lo, uint64_t val_span, int32_t mode,
+                                        double zipf_s, uint64_t& key, int64_t& t, uint64_t& v) {
+  const uint64_t r = rng64(seed, stream_id, idx);
+  const uint64_t r2 = mix64(r);
+  const uint64_t r3 = mix64(r2);
+  key = zipf_s > 0.0 ? zipf_key(r, nkeys, zipf_s) : __umul64hi(r, nkeys);  // multiply-shift
+  t = ts_base + (int64_t)((double)i * span_per_event);
+  if (disorder_p1 > 1) t -= (int64_t)__umul64hi(r2, disorder_p1);
+  const int64_t x = val_lo + (val_span ? (int64_t)__umul64hi(r3, val_span) : 0);
+  v = (mode & 1) ? f64_bits((double)x) : (uint64_t)x;
+}
+
+// Two consecutive events per lane: every column is written with 16-byte stores (8-byte int32
+// key pairs), so a wave moves whole 1 KiB lines per store instruction. Event i is a pure function
+// of (seed, stream, idx0 + i), independent of the launch shape.
 __global__ __launch_bounds__(256) void gen_events_kernel(
     uint64_t* __restrict__ keys, int64_t* __restrict__ ts, uint64_t* __restrict__ vals,
     int64_t n, uint64_t seed, uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
@@ -89,19 +107,47 @@ __global__ __launch_bounds__(256) void gen_events_kernel(
   // mode bit 0: values as f64 bits; bit 1: int32 key ids (the columnar sources' dictionary ids)
   // zipf_s > 0: skewed keys (key_of_draw: power law, rank 0 hottest); 0: uniform.
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint64_t r = rng64(seed, stream_id, idx0 + (uint64_t)i);
-    const uint64_t r2 = mix64(r);
-    const uint64_t r3 = mix64(r2);
-    const uint64_t key = zipf_s > 0.0 ? zipf_key(r, nkeys, zipf_s)
-                                      : __umul64hi(r, nkeys);  // multiply-shift: uniform
-    if (mode & 2) reinterpret_cast<int32_t*>(keys)[i] = (int32_t)key;
-    else keys[i] = key;
-    int64_t t = ts_base + (int64_t)((double)i * span_per_event);
-    if (disorder_p1 > 1) t -= (int64_t)__umul64hi(r2, disorder_p1);
+  const int64_t npairs = n >> 1;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npairs; p += stride) {
+    const int64_t i = 2 * p;
+    uint64_t k0, k1, v0, v1;
+    int64_t t0, t1;
+    gen_one(seed, stream_id, idx0 + (uint64_t)i, i, nkeys, ts_base, span_per_event, disorder_p1,
+            val_lo, val_span, mode, zipf_s, k0, t0, v0);
+    gen_one(seed, stream_id, idx0 + (uint64_t)i + 1, i + 1, nkeys, ts_base, span_per_event,
+            disorder_p1, val_lo, val_span, mode, zipf_s, k1, t1, v1);
+    if (mode & 4) {  // a column not 16-byte aligned (a sliced tensor): scalar stores
+      if (mode & 2) {
+        reinterpret_cast<int32_t*>(keys)[i] = (int32_t)k0;
+        reinterpret_cast<int32_t*>(keys)[i + 1] = (int32_t)k1;
+      } else {
+        keys[i] = k0;
+        keys[i + 1] = k1;
+      }
+      ts[i] = t0;
+      ts[i + 1] = t1;
+      vals[i] = v0;
+      vals[i + 1] = v1;
+      continue;
+    }
+    if (mode & 2) {
+      reinterpret_cast<uint2*>(keys)[p] = make_uint2((uint32_t)k0, (uint32_t)k1);
+    } else {
+      reinterpret_cast<ulonglong2*>(keys)[p] = make_ulonglong2(k0, k1);
+    }
+    reinterpret_cast<longlong2*>(ts)[p] = make_longlong2(t0, t1);
+    reinterpret_cast<ulonglong2*>(vals)[p] = make_ulonglong2(v0, v1);
+  }
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {  // odd tail
+    const int64_t i = n - 1;
+    uint64_t k, v;
+    int64_t t;
+    gen_one(seed, stream_id, idx0 + (uint64_t)i, i, nkeys, ts_base, span_per_event, disorder_p1,
+            val_lo, val_span, mode, zipf_s, k, t, v);
+    if (mode & 2) reinterpret_cast<int32_t*>(keys)[i] = (int32_t)k;
+    else keys[i] = k;
     ts[i] = t;
-    const int64_t v = val_lo + (val_span ? (int64_t)__umul64hi(r3, val_span) : 0);
-    vals[i] = (mode & 1) ? f64_bits((double)v) : (uint64_t)v;
+    vals[i] = v;
   }
 }
 
@@ -3862,10 +3908,13 @@ void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
                 int32_t val_f64, double zipf_s, intptr_t stream) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(gen_events_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+  // mode bit 2: scalar stores (a column that is not 16-byte aligned; int32 keys need 8 bytes)
+  const uintptr_t kmis = (uintptr_t)keys & ((val_f64 & 2) ? 7 : 15);
+  const int32_t mode = val_f64 | ((kmis | (((uintptr_t)ts | (uintptr_t)vals) & 15)) ? 4 : 0);
+  hipLaunchKernelGGL(gen_events_kernel, dim3(grid_for((n + 1) / 2, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, keys, ts, vals, n, seed, stream_id, idx0, nkeys, ts_base,
                      (double)ts_span / (double)n, (uint64_t)(disorder + 1), val_lo,
-                     (uint64_t)val_span, val_f64, zipf_s);
+                     (uint64_t)val_span, mode, zipf_s);
   HIP_CHECK(hipGetLastError());
 }
 
