@@ -502,8 +502,22 @@ class NativeWindowOp(_ColumnInput, Operator):
         return tuple(kinds)
 
     def _subtasks(self, keys: np.ndarray) -> np.ndarray:
-        """Output subtask of every key id (Java hash + murmur, cached per key)."""
+        """Output subtask of every key id (Java hash + murmur, cached per key). Dictionary keys
+        of a device dictionary: one vectorised pass over the ids' Java hashes."""
         P, MP = self.ctx.parallelism, self.ctx.max_parallelism
+        jh = getattr(self.dict, "jhash_table", None) if self.str_keys else None
+        if jh is not None and keys.size:
+            from ..utils.hashing import key_groups_of_java_hashes
+
+            tab = getattr(self, "_sub_tab", None)
+            need = int(keys.max()) + 1
+            if tab is None or tab.size < need:
+                hashes = jh()
+                if hashes.size >= need:
+                    tab = self._sub_tab = (key_groups_of_java_hashes(hashes, MP).astype(np.int64)
+                                           * P // MP).astype(np.int32)
+            if tab is not None and tab.size >= need:
+                return tab[keys]
         u, inv = np.unique(keys, return_inverse=True)
         su = np.empty(u.size, dtype=np.int32)
         for i, k in enumerate(u.tolist()):

@@ -91,6 +91,32 @@ def flink_murmur(code: int) -> int:
     return 0
 
 
+def key_groups_of_java_hashes(hashes, max_parallelism: int = 128):
+    """flink_murmur(h) % max_parallelism of an int32 array of Java hashes (numpy, vectorised;
+    the per-key Python path of flink_murmur for whole dictionaries)."""
+    import numpy as np
+
+    h = np.asarray(hashes).astype(np.int64) & M32
+
+    def rotl(x, r):
+        return ((x << r) | (x >> (32 - r))) & M32
+
+    h = (h * 0xCC9E2D51) & M32
+    h = rotl(h, 15)
+    h = (h * 0x1B873593) & M32
+    h = rotl(h, 13)
+    h = (h * 5 + 0xE6546B64) & M32
+    h ^= 4
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & M32
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & M32
+    h ^= h >> 16
+    c = np.where(h >= 1 << 31, h - (1 << 32), h)  # as int32
+    c = np.where(c == -(1 << 31), 0, np.abs(c))
+    return (c % max_parallelism).astype(np.int32)
+
+
 def default_max_parallelism(p: int) -> int:
     x = p + p // 2
     pow2 = 1 << (max(x, 1) - 1).bit_length()
