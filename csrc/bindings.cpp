@@ -718,6 +718,22 @@ PYBIND11_MODULE(_mxs_native, m) {
                         P<uint8_t>(dirty_g), nsub, cap_log2, ring, p_lo, np, cutoff,
                         compact_out(o, cap), P<uint32_t>(occ));
   });
+  // Tiered firing: rows -> per-key combine table (mxs_kernels.h tier_merge).
+  m.def("tier_merge", [](bool gpu, intptr_t keys, intptr_t acc, intptr_t cnt, int64_t n,
+                         intptr_t n_dev, int mode, int agg, intptr_t tkeys, intptr_t tacc,
+                         intptr_t tcnt, intptr_t tdirty, uint32_t mask, intptr_t flags,
+                         intptr_t stream) {
+    if (gpu) {
+      gpu::tier_merge(P<uint64_t>(keys), P<uint64_t>(acc), P<uint32_t>(cnt), n,
+                      P<uint32_t>(n_dev), mode, agg, P<uint64_t>(tkeys), P<uint64_t>(tacc),
+                      P<uint32_t>(tcnt), P<uint8_t>(tdirty), mask, P<uint32_t>(flags), stream);
+    } else {
+      py::gil_scoped_release nogil;
+      cpu::tier_merge(P<uint64_t>(keys), P<uint64_t>(acc), P<uint32_t>(cnt), n,
+                      P<uint32_t>(n_dev), mode, agg, P<uint64_t>(tkeys), P<uint64_t>(tacc),
+                      P<uint32_t>(tcnt), P<uint8_t>(tdirty), mask, P<uint32_t>(flags));
+    }
+  });
   m.def("gpu_direct_agg_probe", [](intptr_t keys, intptr_t ts, intptr_t vals, int64_t n,
                                    int64_t tbase, int64_t pane, int ring, int64_t nslots,
                                    uint32_t mul, int bits, int64_t pane_base, intptr_t acc,

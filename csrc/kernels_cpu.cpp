@@ -660,5 +660,39 @@ void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t*
   }
 }
 
+void tier_merge(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt, int64_t n,
+                const uint32_t* n_dev, int mode, int agg, uint64_t* tkeys, uint64_t* tacc,
+                uint32_t* tcnt, uint8_t* tdirty, uint32_t mask, uint32_t* flags) {
+  if (n_dev) n = std::min<int64_t>(n, (int64_t)*n_dev);
+  const bool find_only = (mode & 2) != 0, mark = (mode & 1) != 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t k = keys[i];
+    if (k >= kTombKey || cnt[i] == 0) continue;
+    uint32_t s = (uint32_t)(mix64(k) >> 20) & mask;
+    uint32_t found = kNoSlot;
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
+      if (tkeys[s] == k) {
+        found = s;
+        break;
+      }
+      if (tkeys[s] == kEmptyKey) {
+        if (!find_only) {
+          tkeys[s] = k;
+          found = s;
+        }
+        break;
+      }
+      s = (s + 1) & mask;
+    }
+    if (found == kNoSlot) {
+      if (!find_only) flags[0] |= 1u;
+      continue;
+    }
+    tacc[found] = agg_combine(agg, tacc[found], acc[i]);
+    tcnt[found] += cnt[i];
+    if (mark) tdirty[found] = 1;
+  }
+}
+
 }  // namespace cpu
 }  // namespace mxs

@@ -4361,6 +4361,86 @@ void window_agg(const Rec* recs, const uint32_t* counts, const AggPlan& plan, ui
   HIP_CHECK(hipGetLastError());
 }
 
+// Tiered firing: combine rows per key into a global open-addressing table with atomics (see
+// mxs_kernels.h tier_merge). One row per lane; the probe is linear from the key's hash.
+__device__ __forceinline__ void tier_atomic_combine(int agg, uint64_t* p, uint64_t v) {
+  switch (agg) {
+    case AGG_SUM_I64:
+    case AGG_AVG_I64:
+    case AGG_COUNT:
+      atomicAdd((unsigned long long*)p, (unsigned long long)v);
+      return;
+    case AGG_SUM_F64:
+    case AGG_AVG_F64:
+      atomicAdd((double*)p, as_f64(v));
+      return;
+    case AGG_MIN_I64:
+      atomicMin((long long*)p, (long long)v);
+      return;
+    case AGG_MAX_I64:
+      atomicMax((long long*)p, (long long)v);
+      return;
+    default: {  // f64 min / max: compare-and-swap on the bit pattern
+      uint64_t old = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (true) {
+        const uint64_t nv = agg_combine(agg, old, v);
+        if (nv == old) return;
+        const uint64_t prev = atomicCAS((unsigned long long*)p, (unsigned long long)old,
+                                        (unsigned long long)nv);
+        if (prev == old) return;
+        old = prev;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void tier_merge_kernel(
+    const uint64_t* __restrict__ keys, const uint64_t* __restrict__ acc,
+    const uint32_t* __restrict__ cnt, int64_t n, const uint32_t* __restrict__ n_dev, int mode,
+    int agg, uint64_t* __restrict__ tkeys, uint64_t* __restrict__ tacc,
+    uint32_t* __restrict__ tcnt, uint8_t* __restrict__ tdirty, uint32_t mask,
+    uint32_t* __restrict__ flags) {
+  if (n_dev) {
+    const int64_t d = (int64_t)*n_dev;
+    n = d < n ? d : n;
+  }
+  const bool find_only = (mode & 2) != 0, mark = (mode & 1) != 0;
+  bool full = false;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t k = keys[i];
+    const uint32_t c = cnt[i];
+    if (k >= kTombKey || c == 0) continue;
+    uint32_t s = (uint32_t)(mix64(k) >> 20) & mask;
+    uint32_t found = kNoSlot;
+    for (uint32_t probe = 0; probe <= mask; ++probe) {
+      const uint64_t cur = __hip_atomic_load(&tkeys[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == k) {
+        found = s;
+        break;
+      }
+      if (cur == kEmptyKey) {
+        if (find_only) break;
+        const uint64_t prev = atomicCAS((unsigned long long*)&tkeys[s],
+                                        (unsigned long long)kEmptyKey, (unsigned long long)k);
+        if (prev == kEmptyKey || prev == k) {
+          found = s;
+          break;
+        }
+      }
+      s = (s + 1) & mask;
+    }
+    if (found == kNoSlot) {
+      full = full || !find_only;
+      continue;
+    }
+    tier_atomic_combine(agg, &tacc[found], acc[i]);
+    atomicAdd(&tcnt[found], c);
+    if (mark) tdirty[found] = 1;
+  }
+  if (full) atomicOr(&flags[0], 1u);
+}
+
 void window_fire(const uint64_t* keys_g, const uint64_t* acc_g, const uint32_t* cnt_g,
                  const uint8_t* dirty_g, const FirePlan& plan, uint64_t* out_keys,
                  double* out_vals, uint64_t* out_raw, uint32_t* out_cnt, uint32_t* out_n,
@@ -4940,6 +5020,16 @@ void segment_median(const int64_t* heads, int64_t nseg, int64_t total, const uin
   if (nseg <= 0) return;
   hipLaunchKernelGGL(segment_median_kernel, dim3(grid_for(nseg, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, heads, nseg, total, ord, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void tier_merge(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt, int64_t n,
+                const uint32_t* n_dev, int mode, int agg, uint64_t* tkeys, uint64_t* tacc,
+                uint32_t* tcnt, uint8_t* tdirty, uint32_t mask, uint32_t* flags, intptr_t stream) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(tier_merge_kernel, dim3(grid_for(n, 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, keys, acc, cnt, n, n_dev, mode, agg, tkeys, tacc, tcnt,
+                     tdirty, mask, flags);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -276,6 +276,22 @@ MXS_HD uint64_t agg_combine(int32_t k, uint64_t a, uint64_t b) {
   return a;
 }
 
+// Identity of agg_combine (the initial accumulator of a table combined with atomics).
+MXS_HD uint64_t agg_identity(int32_t k) {
+  switch (k) {
+    case AGG_MIN_I64:
+      return (uint64_t)INT64_MAX;
+    case AGG_MAX_I64:
+      return (uint64_t)INT64_MIN;
+    case AGG_MIN_F64:
+      return 0x7FF0000000000000ull;  // +inf
+    case AGG_MAX_F64:
+      return 0xFFF0000000000000ull;  // -inf
+    default:
+      return 0;
+  }
+}
+
 // The accumulator value a single element contributes.
 MXS_HD uint64_t agg_lift(int32_t k, uint64_t v) { return k == AGG_COUNT ? 1ull : v; }
 

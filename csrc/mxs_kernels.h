@@ -363,6 +363,15 @@ void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t*
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
                  int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np,
                  intptr_t stream, uint64_t* dacc = nullptr, uint32_t* dcnt = nullptr);
+// Tiered firing (host-DRAM window tier): rows (key, raw accumulator, count) -- a window's device
+// rows and the tier's rows of its panes -- combined per key into a global open-addressing table
+// (tkeys = kEmptyKey, tacc = agg_identity, tcnt = 0 initially; mask + 1 slots). n_dev (optional):
+// the device row count, read on the device (rows = min(n, *n_dev)). mode bit0: mark the row's
+// key dirty (a re-firing's device rows); bit1: find only (rows of keys not in the table are
+// skipped: a re-firing's tier rows). A full table sets flags[0] bit0.
+void tier_merge(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt, int64_t n,
+                const uint32_t* n_dev, int mode, int agg, uint64_t* tkeys, uint64_t* tacc,
+                uint32_t* tcnt, uint8_t* tdirty, uint32_t mask, uint32_t* flags, intptr_t stream);
 }  // namespace gpu
 
 // ---- CPU twins (kernels_cpu.cpp) ------------------------------------------------------------
@@ -436,6 +445,9 @@ void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t*
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
                  int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np,
                  uint64_t* dacc = nullptr, uint32_t* dcnt = nullptr);
+void tier_merge(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt, int64_t n,
+                const uint32_t* n_dev, int mode, int agg, uint64_t* tkeys, uint64_t* tacc,
+                uint32_t* tcnt, uint8_t* tdirty, uint32_t mask, uint32_t* flags);
 }  // namespace cpu
 
 }  // namespace mxs

@@ -134,6 +134,58 @@ class WindowTierCore {
     }
   }
 
+  // Live rows of panes [p0, p1], uncombined (the device-merged tiered firing combines them on
+  // the GPU): written to k / a / c when they fit `cap` rows; returns the row count either way.
+  // Threaded: chunks are counted in parallel, then copied to their prefix offsets.
+  size_t export_rows(int64_t p0, int64_t p1, uint64_t* k, uint64_t* a, uint32_t* c,
+                     size_t cap) const {
+    std::vector<const Chunk*> src;
+    for (auto& ch : chunks_)
+      if (ch.pmax >= p0 && ch.pmin <= p1 && ch.size()) src.push_back(&ch);
+    if (src.empty()) return 0;
+    auto keep = [&](const Chunk& ch, size_t i) {
+      return ch.pane[i] >= p0 && ch.pane[i] <= p1 && ch.cnt[i] && ch.live(i);
+    };
+    unsigned hw = std::thread::hardware_concurrency();
+    const size_t T = std::max<size_t>(1, std::min<size_t>(src.size(), std::min(hw ? hw : 1u, 16u)));
+    auto run = [&](auto&& fn) {
+      if (T == 1) {
+        fn((size_t)0);
+        return;
+      }
+      std::vector<std::thread> th;
+      for (size_t t = 0; t < T; ++t) th.emplace_back(fn, t);
+      for (auto& x : th) x.join();
+    };
+    std::vector<size_t> cnt(src.size(), 0);
+    run([&](size_t t) {
+      for (size_t j = t; j < src.size(); j += T) {
+        const Chunk& ch = *src[j];
+        size_t m = 0;
+        for (size_t i = 0; i < ch.size(); ++i) m += keep(ch, i) ? 1 : 0;
+        cnt[j] = m;
+      }
+    });
+    std::vector<size_t> off(src.size() + 1, 0);
+    for (size_t j = 0; j < src.size(); ++j) off[j + 1] = off[j] + cnt[j];
+    const size_t total = off.back();
+    if (total > cap) return total;
+    run([&](size_t t) {
+      for (size_t j = t; j < src.size(); j += T) {
+        const Chunk& ch = *src[j];
+        size_t o = off[j];
+        for (size_t i = 0; i < ch.size(); ++i) {
+          if (!keep(ch, i)) continue;
+          k[o] = ch.key[i];
+          a[o] = (uint64_t)ch.acc[i];
+          c[o] = (uint32_t)ch.cnt[i];
+          ++o;
+        }
+      }
+    });
+    return total;
+  }
+
   // A tiered firing: the device's rows of the window (dev_*: one per key, no epilogue) combined
   // with this tier's rows of panes [p0, p1] per key. only_dev: a re-firing -- tier rows count
   // only for keys the device fired. Output order: partition order (unspecified).

@@ -43,6 +43,14 @@ void bind_window_tier(py::module_& m) {
         py::gil_scoped_release nogil;
         t.absorb(key.data(), pane.data(), acc.data(), cnt.data(), dirty.data(), n);
       })
+      // Live rows of panes [p0, p1] into caller buffers (addresses; pinned host memory of the
+      // device-merged firing): returns the row count, rows written only when it is <= cap.
+      .def("export_rows", [](const WindowTierCore& t, int64_t p0, int64_t p1, intptr_t k,
+                             intptr_t a, intptr_t c, size_t cap) {
+        py::gil_scoped_release nogil;
+        return t.export_rows(p0, p1, reinterpret_cast<uint64_t*>(k), reinterpret_cast<uint64_t*>(a),
+                             reinterpret_cast<uint32_t*>(c), cap);
+      })
       .def("part", [](const WindowTierCore& t, int64_t p0, int64_t p1) {
         std::vector<uint64_t> k;
         std::vector<int64_t> a, c;

@@ -298,8 +298,10 @@ def config4_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 1
     `drift` per step, so the keys live during a window's lifetime (90 s = 45 steps) number
     active + 45 * drift = 5.5M against a table sized for `table_keys` = 2M (>= 2x over). Hashed
     keyed state with the host-DRAM tier: every 4 steps, sub-tables above 80 % load evict the keys
-    whose newest data is more than one pane old (window_compact -> C++ tier); firings combine the
-    tier's share of the window on the host. Reports events/s and the tier's size."""
+    whose newest data is more than one pane old (window_compact -> pinned slab on the copy stream,
+    absorbed by the C++ tier at the next boundary); firings export the tier's rows of the window
+    and combine them with the device's rows ON THE DEVICE (tier_merge + fused epilogue).
+    Reports events/s and the tier's size."""
     dev = torch.device(device)
     span = 2_000
     mbps = E.var(E.VAR_RESULT) * 8.0 / 60 / 1024 / 1024
@@ -339,7 +341,9 @@ def config4_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 1
             "ms_per_step": dt / steps * 1e3, "alerts": alerts, "events_per_step": batch,
             "table_keys": table_keys, "live_keys_per_window": active + 45 * drift,
             "spilled_keys": ex.get("spilled_keys", 0), "spilled_rows": ex.get("spilled_rows", 0),
-            "dropped_keys": ex.get("dropped_keys", 0), "host_tier_rows": op.host_tier.nrows,
+            "dropped_keys": ex.get("dropped_keys", 0), "async_evictions": ex.get("async_evictions", 0),
+            "tier_merge": __import__("os").environ.get("MXS_TIER_MERGE", "device"),
+            "host_tier_rows": op.host_tier.nrows,
             "host_tier_bytes": op.host_tier.nbytes, "hbm_state_bytes": op.state_bytes(),
             "device": str(dev)}
 

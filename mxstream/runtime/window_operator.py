@@ -126,6 +126,22 @@ def to_host_arrays(cols: list[torch.Tensor], n: int, pool: PinnedSlabPool | None
 
 
 _D2H = _os.environ.get("MXS_D2H", "kernel")  # "dma": hipMemcpyAsync (A/B)
+# Tiered firings (host-DRAM window tier): "device" (default) combines the tier's rows with the
+# device's on the GPU; "host": the C++ host merge (A/B, the round-3 path).
+_TIER_MERGE = _os.environ.get("MXS_TIER_MERGE", "device")
+
+
+def _agg_identity(agg: int) -> int:
+    """agg_identity (csrc/mxs_common.h) as an int64 bit pattern."""
+    if agg == K.AGG_MIN_I64:
+        return I64_MAX
+    if agg == K.AGG_MAX_I64:
+        return I64_MIN
+    if agg == K.AGG_MIN_F64:
+        return 0x7FF0000000000000
+    if agg == K.AGG_MAX_F64:
+        return 0xFFF0000000000000 - (1 << 64)
+    return 0
 
 
 class CountedHostRows:
@@ -357,7 +373,7 @@ class KeyedWindowOperator:
                  idle_timeout_steps: int | None = None, deterministic: bool = False,
                  spill: bool = False, spill_load: float = 0.8, spill_check_steps: int = 8,
                  spill_keep_panes: int | None = None, emit: str = "full",
-                 latency_fire: int = 0):
+                 latency_fire: int = 0, window_keys: int | None = None):
         """deterministic: f64 sums/averages accumulate each step's per-slot sum in 128-bit fixed
         point (order-independent integer adds, one rounding per slot and step), so results are
         bit-identical between runs, between the GPU and the C++ twin, and independent of the
@@ -528,11 +544,18 @@ class KeyedWindowOperator:
         self._hflags = torch.zeros(4, dtype=torch.int32, pin_memory=pin)
         self.stats, self.red = self._stats[0], self._red[0]
         self.local_maxts = torch.full((1,), I64_MIN, dtype=torch.int64, device=dev)
+        if self.local_global:
+            # window_keys: keys one window can hold over all ranks -- with the spill tier a window
+            # holds keys evicted from the table, so the owners' merge tables are sized for more
+            self._init_owner_tables(int(window_keys or (4 * max_keys if spill else max_keys)),
+                                    cap_log2)
         # Batched firing: up to `_fire_group` due windows per native call and host sync (one
         # window's rows never exceed nslots, so the output holds the group's rows).
         self._fire_group = (max(1, min(64, (1 << 21) // self.nslots))
                             if type(self)._fire_window is KeyedWindowOperator._fire_window else 1)
         orows = self.nslots * self._fire_group
+        if self.local_global:  # the owner's merge table fires into the same columns
+            orows = max(orows, self.nslots_o)
         self.out_keys = torch.empty(orows, dtype=torch.int64, device=dev)
         self.out_vals = torch.empty(orows, dtype=torch.float64, device=dev)
         self.out_raw = torch.empty(orows, dtype=torch.int64, device=dev)
@@ -570,8 +593,6 @@ class KeyedWindowOperator:
             self.dlist = torch.empty(self.nslots, dtype=torch.int32, device=dev)
             self.dlist_n = torch.zeros(1, dtype=torch.int32, device=dev)
             self.slot_mark = torch.zeros(self.nslots, dtype=torch.int32, device=dev)
-        if self.local_global:
-            self._init_owner_tables(max_keys, cap_log2)
         self.comb_send = self.comb_recv = None
         self.comb_counts = torch.zeros(self.nbuckets, dtype=torch.int32, device=dev)
         self._ccap_hint = 1 << self.cap_log2
@@ -601,14 +622,21 @@ class KeyedWindowOperator:
         self._debug = debug_enabled()  # MXS_DEBUG: table invariant check after every step
         self.host_tier = None
         if spill:
-            if self.dense_bits or self.local_global or not type(self)._spill_ok:
-                raise ValueError("spill needs hashed keys, records exchange and a plain reduce")
+            if self.dense_bits or not type(self)._spill_ok:
+                raise ValueError("spill needs hashed keys and a plain reduce")
             from .window_spill import HostWindowTier
 
             self.host_tier = HostWindowTier(agg)
         self.spill_load, self.spill_check_steps = float(spill_load), max(1, int(spill_check_steps))
         self.spill_keep_panes = spill_keep_panes
         self._spill_out = None
+        self._evict_pending = None   # asynchronous eviction rows on their way to host DRAM
+        self._evict_busy = None      # event: the eviction copy stopped reading the device rows
+        self._evict_pool = None
+        self._tier_pool = None       # pinned slabs of the tier's rows for device-merged firings
+        self._tier_h2d: list = []    # (event, slab) of tier rows still being copied H2D
+        self._tier_tab = None        # the device-merged firing's combine table + outputs
+        self._tout_busy = None
 
         # ---- watermark / firing bookkeeping (host, identical on every rank) ----
         self.wm = I64_MIN
@@ -1206,16 +1234,22 @@ class KeyedWindowOperator:
         if int(self.occ.max()) <= self.spill_load * cap or self.max_seen_pane is None:
             return
         keep = self.spill_keep_panes or self.panes_per_window
-        self.compact_state(self.max_seen_pane - keep)
+        self.compact_state(self.max_seen_pane - keep, wait=False)
 
-    def compact_state(self, cutoff_pane: int | None = None) -> dict:
+    def compact_state(self, cutoff_pane: int | None = None, wait: bool = True) -> dict:
         """Table maintenance at a step boundary: drop keys without live data and (with the spill
-        tier) move keys whose newest data pane is <= cutoff_pane to host DRAM. Returns counts."""
+        tier) move keys whose newest data pane is <= cutoff_pane to host DRAM. Returns counts.
+
+        wait=False (the spill check inside a step, GPU): the evicted rows go to a pinned slab by
+        the counted copy kernel on the copy stream, with no host sync; the tier absorbs them at
+        the next point that reads it (_land_evictions: a firing over tier panes, a purge, a
+        snapshot, the next eviction) and the counts are returned as None."""
         self._verify_combine()  # a combined step skipped on the device is redone before this
         if self.dense_bits:
             return {"dropped": 0, "evicted": 0, "rows": 0}
         if cutoff_pane is not None and self.host_tier is None:
             raise ValueError("evicting keys needs the spill tier (spill=True)")
+        self._land_evictions()
         self._drain()
         dev = self.device
         cuda = dev.type == "cuda"
@@ -1224,7 +1258,15 @@ class KeyedWindowOperator:
         else:
             p_lo, np_ = self.min_live_pane, min(self.ring, self.max_seen_pane - self.min_live_pane + 1)
         cutoff = I64_MIN if cutoff_pane is None else int(cutoff_pane)
-        rows_cap = max(1, int(self.occ.sum()) * max(np_, 1)) if cutoff != I64_MIN else 1
+        asynchronous = cuda and not wait and self._copy_stream is not None and \
+            self.host_tier is not None
+        if cutoff == I64_MIN:
+            rows_cap = 1
+        elif asynchronous:
+            # bound without a host read of the occupancy: every slot's live panes (x 16 rows)
+            rows_cap = (self.nslots * max(np_, 1) + 15) & ~15
+        else:
+            rows_cap = max(1, int(self.occ.sum()) * max(np_, 1))
         o = self._spill_out
         if o is None or o["key"].numel() < rows_cap:
             o = self._spill_out = {
@@ -1234,6 +1276,9 @@ class KeyedWindowOperator:
                 "cnt": torch.empty(rows_cap, dtype=torch.int32, device=dev),
                 "dirty": torch.empty(rows_cap, dtype=torch.uint8, device=dev),
                 "ctr": torch.zeros(4, dtype=torch.int32, device=dev)}
+        if asynchronous and self._evict_busy is not None:
+            torch.cuda.current_stream(dev).wait_event(self._evict_busy)  # last copy read o[...]
+            self._evict_busy = None
         o["ctr"].zero_()
         ptrs = [o["key"].data_ptr(), o["pane"].data_ptr(), o["acc"].data_ptr(),
                 o["cnt"].data_ptr(), o["dirty"].data_ptr(), o["ctr"][3:4].data_ptr(),
@@ -1245,23 +1290,49 @@ class KeyedWindowOperator:
             self._m.gpu_window_compact(*args, torch.cuda.current_stream(dev).cuda_stream)
         else:
             self._m.cpu_window_compact(*args)
-        ctr = o["ctr"].tolist()
+        if asynchronous:
+            if self._evict_pool is None:
+                self._evict_pool = PinnedSlabPool(max_slabs=2)
+            n_cap = o["key"].numel()
+            cols = [o["key"][:n_cap], o["pane"][:n_cap], o["acc"][:n_cap], o["cnt"][:n_cap],
+                    o["dirty"][:n_cap]]
+            rows = CountedHostRows(self._evict_pool, cols, o["ctr"][3:4], [o["ctr"]],
+                                   copy_stream=self._copy_stream)
+            self._evict_pending = rows
+            self._evict_busy = rows.done
+            self.metrics.extra["async_evictions"] = self.metrics.extra.get("async_evictions", 0) + 1
+            return {"dropped": None, "evicted": None, "rows": None}
+        return self._absorb_evicted(o["ctr"].tolist(), None, o)
+
+    def _absorb_evicted(self, ctr, rows, o) -> dict:
+        """Append evicted rows to the tier: from a landed asynchronous copy (`rows`) or, after a
+        synchronous compaction, by one pinned copy of the device columns (`o`)."""
         if ctr[2]:
             raise RuntimeError("window_compact: eviction rows overflowed (internal error)")
-        n = ctr[3]
+        n = int(ctr[3])
         if n and self.host_tier is not None:
-            # One copy of the five columns into a pinned slab (one sync), appended to the C++
-            # tier as a chunk.
-            h = to_host_arrays([o["key"], o["pane"], o["acc"], o["cnt"], o["dirty"]], n,
-                               self._pool)
+            if rows is not None:
+                h = rows.columns(n)
+            else:
+                h = to_host_arrays([o["key"], o["pane"], o["acc"], o["cnt"], o["dirty"]], n,
+                                   self._pool)
             self.host_tier.absorb(h[0].view(np.uint64), h[1], h[2], h[3], h[4])
         # (Touched-slot lists and dirty bytes are empty here: every step's re-firings cleared
         # them before this step boundary, so no slot id survives the rehash.)
         ex = self.metrics.extra
-        ex["dropped_keys"] = ex.get("dropped_keys", 0) + ctr[0]
-        ex["spilled_keys"] = ex.get("spilled_keys", 0) + ctr[1]
+        ex["dropped_keys"] = ex.get("dropped_keys", 0) + int(ctr[0])
+        ex["spilled_keys"] = ex.get("spilled_keys", 0) + int(ctr[1])
         ex["spilled_rows"] = ex.get("spilled_rows", 0) + n
-        return {"dropped": ctr[0], "evicted": ctr[1], "rows": n}
+        return {"dropped": int(ctr[0]), "evicted": int(ctr[1]), "rows": n}
+
+    def _land_evictions(self) -> None:
+        """Absorb an asynchronous eviction's rows into the tier (its copy has long completed when
+        this runs: the next spill check, firing over tier panes or purge)."""
+        rows, self._evict_pending = self._evict_pending, None
+        if rows is None:
+            return
+        rows.wait()
+        self._absorb_evicted(rows.fixed(0).tolist(), rows, None)
 
     # ---- hooks (overridden by the vector-metric operator) ---------------------------------
     def _exchange(self, rw: int) -> None:
@@ -1360,8 +1431,10 @@ class KeyedWindowOperator:
             return None
         if self.local_global:
             return self._fire_window_partials(s, p0, p1, only_dirty)
-        if self.host_tier is not None and self.host_tier.overlaps(p0, p1):
-            return self._fire_window_tiered(s, p0, p1, only_dirty)
+        if self.host_tier is not None:
+            self._land_evictions()
+            if self.host_tier.overlaps(p0, p1):
+                return self._fire_window_tiered(s, p0, p1, only_dirty)
         self.out_n.zero_()
         kv = self._key_value_rows()
         K.window_fire(self.keys_g, self.acc_g, self.cnt_g, self.dirty_g, agg=self.agg,
@@ -1463,11 +1536,25 @@ class KeyedWindowOperator:
                               self._pool)
         return [host[0].view(np.uint64), host[1], host[2], host[3]]
 
-    def _fire_window_tiered(self, s: int, p0: int, p1: int, only_dirty: bool) -> FireResult | None:
-        """Window [s, s + size) with part of its state in the host tier: the device fires
-        without its epilogue, the tier's share is combined per key, the epilogue runs here."""
+    def _fire_window_tiered(self, s: int, p0: int, p1: int, only_dirty: bool):
+        """Window [s, s + size) with part of its state in the host tier, merged on the device:
+        1. the device fires its rows of the window without the epilogue (key, raw accumulator,
+           count; the count stays on the device);
+        2. the tier's live rows of panes [p0, p1] are exported uncombined into a pinned slab
+           (threaded C++) and copied H2D;
+        3. tier_merge combines both per key into a transient table with atomics (a re-firing
+           marks the device's dirty keys and folds tier rows of those keys only);
+        4. window_fire over the table (one pane) with the fused map/filter epilogue: only the
+           emitted rows leave the device, by the asynchronous counted copy of every firing.
+        No host merge, no copy of the device's rows to the host."""
         from .window_spill import merge_fire
 
+        dev = self.device
+        cuda = dev.type == "cuda"
+        m = self._m
+        st = torch.cuda.current_stream(dev).cuda_stream if cuda else 0
+        if cuda:
+            self._claim()
         self.out_n.zero_()
         K.window_fire(self.keys_g, self.acc_g, self.cnt_g, self.dirty_g, agg=self.agg,
                       npanes=p1 - p0 + 1, ring=self.ring, p0=p0, wstart=s, wend=s + self.size,
@@ -1476,19 +1563,112 @@ class KeyedWindowOperator:
                       out_cnt=self.out_cnt, out_n=self.out_n,
                       slot_list=self.dlist if only_dirty else None,
                       slot_list_n=self.dlist_n if only_dirty else None)
-        n = min(self._fired_count(), self.out_keys.numel())
         self.metrics.num_fires += 1
-        dk, dr, dc = (t[:n].cpu().numpy() for t in (self.out_keys, self.out_raw, self.out_cnt))
-        if only_dirty and n == 0:
+        if _TIER_MERGE == "host":  # A/B: the host merge (C++ radix-partitioned hash combine)
+            n = min(self._fired_count(), self.out_keys.numel())
+            dk, dr, dc = (t[:n].cpu().numpy() for t in (self.out_keys, self.out_raw, self.out_cnt))
+            if only_dirty and n == 0:
+                return None
+            keys, vals, raw, cnt = merge_fire(self.agg, dk.view(np.uint64), dr, dc,
+                                              self.host_tier, only_dirty, self.map_prog,
+                                              self.filter_prog, s, s + self.size, panes=(p0, p1))
+            if not keys.size:
+                return None
+            self.metrics.num_records_out += int(keys.size)
+            return FireResult(s, s + self.size, keys, vals, raw, cnt, refire=only_dirty)
+        # 2. the tier's rows of the window's panes (H2D on this stream)
+        ex = self._tier_rows(p0, p1)
+        # 3. per-key combine table of the device's rows (count on the device) + the tier's
+        tkeys, tacc, tcnt, tdirty, ok_, ov_, or_, oc_ = self._tier_combine(
+            ex, self.out_n, 1 if only_dirty else 0, 2 if only_dirty else 0)
+        # 4. the fused epilogue over the combined table
+        self.out_n.zero_()
+        K.window_fire(tkeys, tacc, tcnt, tdirty, agg=self.agg, npanes=1, ring=1, p0=0,
+                      wstart=s, wend=s + self.size, only_dirty=only_dirty,
+                      map_prog=self.map_prog, filt_prog=self.filter_prog, out_keys=ok_,
+                      out_vals=ov_, out_raw=or_, out_cnt=oc_, out_n=self.out_n)
+        if cuda and self._async_fire:
+            rows = CountedHostRows(self._pool, [ok_, ov_, or_, oc_], self.out_n, [self.flags],
+                                   copy_stream=self._copy_stream)
+            self._tout_busy = rows.done
+            return _PendingFire(rows, [s], False, only_dirty, False)
+        n = self._fired_count()
+        if n == 0:
             return None
-        keys, vals, raw, cnt = merge_fire(self.agg, dk.view(np.uint64), dr, dc,
-                                          self.host_tier, only_dirty,
-                                          self.map_prog, self.filter_prog, s, s + self.size,
-                                          panes=(p0, p1))
-        if not keys.size:
-            return None
-        self.metrics.num_records_out += int(keys.size)
-        return FireResult(s, s + self.size, keys, vals, raw, cnt, refire=only_dirty)
+        n = min(n, ok_.numel())
+        self.metrics.num_records_out += n
+        host = to_host_arrays([ok_, ov_, or_, oc_], n, self._pool)
+        return FireResult(s, s + self.size, host[0].view(np.uint64), host[1], host[2], host[3],
+                          refire=only_dirty)
+
+    def _tier_rows(self, p0: int, p1: int):
+        """The tier's live rows of panes [p0, p1] on the device (window_spill.HostWindowTier
+        .export; the pinned slab is held until its H2D copy has completed)."""
+        dev = self.device
+        cuda = dev.type == "cuda"
+        for ev, _arr in self._tier_h2d:
+            ev.synchronize()  # (long done: a previous firing's copy) -- the slab may be reused
+        self._tier_h2d = []
+        if self._tier_pool is None and cuda:
+            self._tier_pool = PinnedSlabPool(max_slabs=2)
+        ex = self.host_tier.export(p0, p1, dev, self._tier_pool)
+        if cuda and ex is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            self._tier_h2d.append((ev, ex[4]))
+        return ex
+
+    def _tier_combine(self, ex, n_dev, dev_mode: int, tier_mode: int):
+        """tier_merge of the device rows in out_keys / out_raw / out_cnt (count n_dev on the
+        device) and the tier rows `ex` into the transient combine table; returns the table and
+        its output columns (keys, vals, raw, cnt), >= 2x the rows it can receive."""
+        dev = self.device
+        cuda = dev.type == "cuda"
+        n_t = 0 if ex is None else ex[3]
+        need = _next_pow2(max(1024, 2 * (self.out_keys.numel() + n_t)))
+        tt = self._tier_tab
+        if tt is None or tt[0].numel() < need:
+            if cuda and self._tout_busy is not None:
+                self._claim("_tout_busy")
+            tt = self._tier_tab = (torch.empty(need, dtype=torch.int64, device=dev),
+                                   torch.empty(need, dtype=torch.int64, device=dev),
+                                   torch.empty(need, dtype=torch.int32, device=dev),
+                                   torch.empty(need, dtype=torch.uint8, device=dev),
+                                   torch.empty(need // 2, dtype=torch.int64, device=dev),
+                                   torch.empty(need // 2, dtype=torch.float64, device=dev),
+                                   torch.empty(need // 2, dtype=torch.int64, device=dev),
+                                   torch.empty(need // 2, dtype=torch.int32, device=dev))
+        tkeys, tacc, tcnt, tdirty = tt[:4]
+        if cuda:
+            self._claim("_tout_busy")  # the previous tiered firing's copy reads the outputs
+        size = tkeys.numel()
+        tkeys.fill_(-1)
+        tacc.fill_(_agg_identity(self.agg))
+        tcnt.zero_()
+        tdirty.zero_()
+        st = torch.cuda.current_stream(dev).cuda_stream if cuda else 0
+        m = self._m
+        m.tier_merge(cuda, self.out_keys.data_ptr(), self.out_raw.data_ptr(),
+                     self.out_cnt.data_ptr(), self.out_keys.numel(), n_dev.data_ptr(), dev_mode,
+                     self.agg, tkeys.data_ptr(), tacc.data_ptr(), tcnt.data_ptr(),
+                     tdirty.data_ptr(), size - 1, self.flags.data_ptr(), st)
+        if ex is not None:
+            m.tier_merge(cuda, ex[0].data_ptr(), ex[1].data_ptr(), ex[2].data_ptr(), n_t, 0,
+                         tier_mode, self.agg, tkeys.data_ptr(), tacc.data_ptr(),
+                         tcnt.data_ptr(), tdirty.data_ptr(), size - 1, self.flags.data_ptr(), st)
+        return tt
+
+    def _merge_tier_partials(self, p0: int, p1: int):
+        """Local-global with the spill tier: this rank's local partial rows of a window (count
+        part_n) plus its tier rows of the window's panes, combined per key on the device and
+        re-emitted as partial rows (no epilogue) -- the columns scatter_partials reads."""
+        ex = self._tier_rows(p0, p1)
+        tkeys, tacc, tcnt, tdirty, ok_, ov_, or_, oc_ = self._tier_combine(ex, self.part_n, 0, 0)
+        self.part_n.zero_()
+        K.window_fire(tkeys, tacc, tcnt, tdirty, agg=self.agg, npanes=1, ring=1, p0=0, wstart=0,
+                      wend=self.size, only_dirty=False, map_prog=E.EMPTY, filt_prog=E.EMPTY,
+                      out_keys=ok_, out_vals=ov_, out_raw=or_, out_cnt=oc_, out_n=self.part_n)
+        return ok_, or_, oc_
 
     def _fire_window_partials(self, s: int, p0: int, p1: int, only_dirty: bool = False,
                               emit: bool = True) -> FireResult | None:
@@ -1515,9 +1695,15 @@ class KeyedWindowOperator:
                       out_cnt=self.out_cnt, out_n=self.part_n,
                       slot_list=self.dlist if only_dirty else None,
                       slot_list_n=self.dlist_n if only_dirty else None)
+        pk, pa, pc = self.out_keys, self.out_raw, self.out_cnt
+        if not delta and self.host_tier is not None:
+            self._land_evictions()
+            if self.host_tier.overlaps(p0, p1):
+                # spilled keys: this rank's tier rows of the window join its local partials
+                pk, pa, pc = self._merge_tier_partials(p0, p1)
         self.fcursor.zero_()
-        K.scatter_partials(self.out_keys, self.out_raw, self.out_cnt, self.part_n,
-                           n_cap=self.out_keys.numel(), max_parallelism=self.max_parallelism,
+        K.scatter_partials(pk, pa, pc, self.part_n,
+                           n_cap=pk.numel(), max_parallelism=self.max_parallelism,
                            nranks=self.world, nsub_log2=self.nsub_o_log2,
                            hash_mode=self.hash_mode, jhash=self.jhash, kg_dest=self.kg_dest,
                            bucket_cap=self.fbcap, cursor=self.fcursor, out=self.fsend,
@@ -1802,6 +1988,7 @@ class KeyedWindowOperator:
             s = self._align_up(wm - self.size - self.lateness + 2)
             keep_from = self.pane_of(s)
         if self.host_tier is not None:
+            self._land_evictions()
             self.host_tier.purge(keep_from)
         p = self.min_live_pane
         stop = min(keep_from, self.max_seen_pane + 1)
@@ -1827,7 +2014,10 @@ class KeyedWindowOperator:
 
     def host_state_bytes(self) -> int:
         """Bytes of keyed state in the host-DRAM tier (0 without spill)."""
-        return 0 if self.host_tier is None else self.host_tier.nbytes
+        if self.host_tier is None:
+            return 0
+        self._land_evictions()
+        return self.host_tier.nbytes
 
     def num_keys(self) -> int:
         self._sync_state()
@@ -1841,6 +2031,7 @@ class KeyedWindowOperator:
         if self._pending is not None:
             self._carry.extend(self.flush())
         self._drain()
+        self._land_evictions()  # evicted rows still in flight belong to the tier's state
 
     # ---- checkpoint / restore (runtime/checkpoint.py) --------------------------------------
     def owned_key_groups(self) -> tuple[int, int]:
@@ -1921,6 +2112,7 @@ class KeyedWindowOperator:
         """Rebuild the tables from checkpoint rows (this rank's key groups only)."""
         self._check_ckpt_meta(meta)
         if self.host_tier is not None:
+            self._evict_pending = None  # rows of the replaced state
             self.host_tier.clear()
         self._pending, self._carry = None, []
         self._drain()

@@ -11,9 +11,11 @@ device fires without its epilogue, this tier's part of the same window is combin
 fire kernel's expression-VM semantics (``expr.eval_numpy``).
 
 The tier itself is C++ (csrc/window_tier.h): evicted rows (key, pane, acc, cnt, dirty) are
-appended as chunks (no re-concatenation per eviction), a firing hash-combines the chunks that
-overlap its panes, a purge drops whole chunks below the live range; rows are merged per
-(key, pane) only for a snapshot.
+appended as chunks (no re-concatenation per eviction), a purge drops whole chunks below the live
+range; rows are merged per (key, pane) only for a snapshot. A firing exports the live rows of its
+panes (threaded, uncombined) into a pinned slab; on a GPU they are combined with the device's rows
+ON THE DEVICE (KeyedWindowOperator._fire_window_tiered: tier_merge + the fused fire epilogue), the
+host-side merge_fire below is the CPU-free fallback and the test oracle.
 """
 from __future__ import annotations
 
@@ -98,6 +100,37 @@ class HostWindowTier:
     def overlaps(self, p0: int, p1: int) -> bool:
         r = self.pane_range()
         return r is not None and r[0] <= p1 and r[1] >= p0
+
+    def export(self, p0: int, p1: int, device, pool=None):
+        """Live rows of panes [p0, p1], uncombined, as (keys int64, acc int64, cnt int32, n) on
+        `device` (the device-merged tiered firing). GPU: the threaded C++ export writes a pinned
+        slab, the columns go H2D on the current stream (asynchronous); the slab's numpy array is
+        returned as a fifth element -- hold it until the copy has completed. None: no rows."""
+        import torch
+
+        bound = self.nrows
+        if bound == 0:
+            return None
+        if torch.device(device).type == "cuda":
+            a8 = (bound * 8 + 255) & ~255
+            t, arr = pool.take(2 * a8 + bound * 4 + 256)
+            base = t.data_ptr()
+            n = int(self._t.export_rows(int(p0), int(p1), base, base + a8, base + 2 * a8, bound))
+            if n == 0:
+                return None
+            k = t[:n * 8].view(torch.int64).to(device, non_blocking=True)
+            a = t[a8:a8 + n * 8].view(torch.int64).to(device, non_blocking=True)
+            c = t[2 * a8:2 * a8 + n * 4].view(torch.int32).to(device, non_blocking=True)
+            return k, a, c, n, arr
+        k = np.empty(bound, np.int64)
+        a = np.empty(bound, np.int64)
+        c = np.empty(bound, np.int32)
+        n = int(self._t.export_rows(int(p0), int(p1), k.ctypes.data, a.ctypes.data, c.ctypes.data,
+                                    bound))
+        if n == 0:
+            return None
+        return (torch.from_numpy(k[:n]), torch.from_numpy(a[:n]), torch.from_numpy(c[:n]), n,
+                None)
 
     def part(self, p0: int, p1: int):
         """This tier's share of the window over panes [p0, p1]: (keys, acc, cnt) per key."""

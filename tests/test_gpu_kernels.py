@@ -427,6 +427,36 @@ def test_spill_tier_gpu_matches_unbounded_cpu(gpu_device):
     got, op = _run_windows(batches, device=gpu_device, max_keys=3000, spill=True,
                            spill_check_steps=1, spill_load=0.5, cap_log2=7, spill_keep_panes=1)
     assert op.metrics.extra.get("spilled_keys", 0) > 0
+    # evictions went to host DRAM asynchronously; firings merged the tier on the device
+    assert op.metrics.extra.get("async_evictions", 0) > 0
+    assert got == ref
+
+
+@pytest.mark.parametrize("exchange", ["partials", "records"])
+def test_spill_tier_gpu_loopback_g4_matches_unbounded_cpu(gpu_device, exchange):
+    """The host-DRAM tier at G = 4 (virtual ranks on one MI355X): asynchronous eviction, tier
+    rows merged on the device into each rank's local partials (local-global) or into the
+    owner's tiered firing (records exchange) == one unbounded C++-twin table."""
+    import sys
+
+    from mxstream.parallel.comm import run_loopback
+
+    sys.path.insert(0, __import__("os").path.dirname(__file__))
+    from test_window_operator_cpu import _drift_batches, _run_windows
+
+    batches = _drift_batches(20, 6000, seed=5)
+    ref, _ = _run_windows(batches, max_keys=80_000)
+
+    def rank(comm):
+        mine = [(k[comm.rank::4].contiguous(), t[comm.rank::4].contiguous(),
+                 v[comm.rank::4].contiguous()) for k, t, v in batches]
+        return _run_windows(mine, device=gpu_device, max_keys=3000, spill=True,
+                            spill_check_steps=1, spill_load=0.5, cap_log2=7, spill_keep_panes=1,
+                            comm=comm, parallelism=4, exchange=exchange, window_keys=80_000)
+
+    res = run_loopback(4, rank, device=gpu_device)
+    got = sorted(r for rows, _ in res for r in rows)
+    assert sum(op.metrics.extra.get("spilled_keys", 0) for _, op in res) > 0
     assert got == ref
 
 

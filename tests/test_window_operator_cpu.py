@@ -670,3 +670,27 @@ def test_latency_fire_equals_pipelined():
     got, n_fast, imm = run(64)
     assert got == ref and len(ref) > 1000
     assert n_fast > 10 and imm > 10  # firings returned by the call of their own batch
+
+
+@pytest.mark.parametrize("world,exchange", [(2, "partials"), (4, "partials"), (2, "records")])
+def test_spill_tier_multirank_matches_unbounded_table(world, exchange):
+    """The host-DRAM tier at G > 1 (LoopbackComm ranks): local-global partials (each rank's tier
+    rows join its local partials on the device before the owners merge) and the records
+    exchange both equal one rank with a table that holds every key."""
+    from mxstream.parallel.comm import run_loopback
+
+    batches = _drift_batches(20, 6000, seed=5)
+    ref, _ = _run_windows(batches, max_keys=80_000)
+
+    def rank(comm):
+        mine = [(k[comm.rank::world].contiguous(), t[comm.rank::world].contiguous(),
+                 v[comm.rank::world].contiguous())
+                for k, t, v in batches]
+        return _run_windows(mine, max_keys=3000, spill=True, spill_check_steps=1,
+                            spill_load=0.5, cap_log2=7, spill_keep_panes=1, comm=comm,
+                            parallelism=world, exchange=exchange, window_keys=80_000)
+
+    res = run_loopback(world, rank)
+    got = sorted(r for rows, _ in res for r in rows)
+    assert sum(op.metrics.extra.get("spilled_keys", 0) for _, op in res) > 0
+    assert got == ref
