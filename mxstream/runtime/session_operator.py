@@ -282,12 +282,15 @@ class KeyedSessionOperator:
         self._empty_steps = self._empty_steps + 1 if n == 0 else 0
         idle = self._idle_marked or (self.idle_timeout_steps is not None
                                      and self._empty_steps >= self.idle_timeout_steps)
-        t = ts.min().reshape(1) if n else torch.full((1,), I64_MAX, dtype=torch.int64,
-                                                    device=ts.device)
-        self.comm.allreduce_min_(t)
-        tbase = int(t.item())
-        if tbase == I64_MAX:
-            tbase = 0
+        # Time base of the step's relative record times: after the first watermark a provisional
+        # base 2^30 ms (12 days) below it -- identical on every rank, no MIN all-reduce and no
+        # host sync -- and a step with an older record is redone with the exact minimum (the
+        # partition flags it like an unrepresentable span).
+        exact = self.wm == I64_MIN
+        if exact:
+            tbase = self._exact_tbase(ts, n)
+        else:
+            tbase = self.wm - (1 << 30)
         # GPU, LDS fold: the fold is enqueued right behind the partition and skips itself on the
         # device when the step's reduced flags ask for a redo -- the partition's flags, the
         # fold's counters and its late count come back in ONE host wait (tbits fixed at 32).
@@ -322,6 +325,11 @@ class KeyedSessionOperator:
             if folded is None:
                 host = self.red.cpu().tolist()
             if host[4]:
+                if not exact:  # a record older than the provisional base: exact base, redo
+                    exact = True
+                    tbase = self._exact_tbase(ts, n)
+                    self.metrics.extra["tbase_redos"] = self.metrics.extra.get("tbase_redos", 0) + 1
+                    continue
                 raise RuntimeError("session batch spans more than 2^32 ms")
             if host[7]:
                 raise ValueError("key ids -1 and -2 are reserved (the state tables' markers)")
@@ -346,6 +354,14 @@ class KeyedSessionOperator:
         # (EventTimeTrigger.onElement: maxTimestamp <= currentWatermark -> FIRE).
         wm = old_wm if self.external_watermark else max(old_wm, wm_global)
         return self._fire_at(wm)
+
+    def _exact_tbase(self, ts: torch.Tensor, n: int) -> int:
+        """The step's minimum timestamp over all ranks (one MIN all-reduce + host read)."""
+        t = ts.min().reshape(1) if n else torch.full((1,), I64_MAX, dtype=torch.int64,
+                                                    device=ts.device)
+        self.comm.allreduce_min_(t)
+        tbase = int(t.item())
+        return 0 if tbase == I64_MAX else tbase
 
     def mark_idle(self, idle: bool = True) -> None:
         self._idle_marked = bool(idle)
