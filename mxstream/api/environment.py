@@ -31,6 +31,10 @@ class ExecutionConfig:
     # device string dictionary (ops/ingest.py; the C++ twins when device is "cpu"), "host" with
     # the multi-threaded host parser, "auto" = device on a GPU. MXS_TEXT_INGEST overrides.
     text_ingest: str = field(default_factory=lambda: os.environ.get("MXS_TEXT_INGEST", "auto"))
+    # Device ingest, one rank: read each batch's parse result one pass later (the host's work on
+    # batch i overlaps the GPU's parse of batch i + 1). Applied only where a pass's delay cannot
+    # be observed (planner._defer_safe); MXS_INGEST_DEFER=0 turns it off.
+    ingest_defer: bool = field(default_factory=lambda: os.environ.get("MXS_INGEST_DEFER", "1") != "0")
     global_job_parameters: dict = field(default_factory=dict)
     # "<operator name>:<records>[:<attempts>]" (tests / chaos runs); default from MXS_FAULT.
     fault_injection: str | None = field(default_factory=lambda: os.environ.get("MXS_FAULT"))

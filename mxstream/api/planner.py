@@ -169,6 +169,26 @@ def _dead_fields_ok(t: Transformation, children, key_pos: int, val_pos: int, ari
     return not (probe.used & keep)
 
 
+def _defer_safe(env, nodes) -> bool:
+    """A pass's delay of the device ingest's output changes nothing the job can observe: no
+    checkpoints (a deferred batch would sit between two passes), and every operator is a
+    map / filter / timestamp assigner / rolling aggregate / event-time window / sink -- none
+    reads the processing-time clock."""
+    if env.checkpoint_config.is_checkpointing_enabled():
+        return False
+    for n in nodes:
+        if n.kind in ("source", "sink", "union", "side"):
+            continue
+        meta = getattr(n, "meta", None) or {}
+        kind = meta.get("kind")
+        if kind in ("map", "filter", "timestamps", "rolling"):
+            continue
+        if kind == "window" and meta["stream"].assigner.is_event_time():
+            continue
+        return False
+    return True
+
+
 def _lower_text(env, sinks) -> None:
     """Columnar text ingest: source(text) -> [timestamps] -> map(parse) -> [filter] becomes one
     TextParseOp fed by raw line batches, when the map (and extractor / filter) trace
@@ -177,6 +197,7 @@ def _lower_text(env, sinks) -> None:
     from . import textplan as T
 
     nodes, children = _consumers(sinks)
+    defer = _defer_safe(env, nodes) and getattr(env.config, "ingest_defer", True)
     for t in nodes:
         meta = getattr(t, "meta", None) or {}
         if meta.get("kind") != "map" or meta.get("columnar") or len(t.parents) != 1:
@@ -216,8 +237,9 @@ def _lower_text(env, sinks) -> None:
         # (names of fired keys, Java hashes of key groups at G > 1).
         shared: dict = {}
         t.factory = (lambda spec=spec, ts_spec=ts_spec, bound=bound, filt=filt, d=ingest_dev,
-                     sh=shared: TextParseOp(spec, ts_spec=ts_spec, bound=bound, filter_prog=filt,
-                                            device=d, shared=sh))
+                     sh=shared, df=defer: TextParseOp(spec, ts_spec=ts_spec, bound=bound,
+                                                      filter_prog=filt, device=d, shared=sh,
+                                                      defer=df))
         t.parents = [parent]
         if fnode is not None:
             fnode.factory = PassThroughOp

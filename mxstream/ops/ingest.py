@@ -206,6 +206,18 @@ class IngestResult:
         self.n_lines = n_lines
 
 
+class _PendingParse:
+    """A batch whose parse is enqueued (TextIngest.begin) and whose control words are on their
+    way to pinned memory; TextIngest.finish completes it."""
+
+    __slots__ = ("data", "keep_alive", "buf", "starts", "status", "cols", "ids", "n", "fidx",
+                 "fscr", "ocols", "oids", "hb", "ev")
+
+    def __init__(self, **kw):
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+
 class TextIngest:
     """Parser of one text layout (separator + fields) onto `device`; see the module docstring.
 
@@ -290,6 +302,15 @@ class TextIngest:
         needs the same id for the same string everywhere): the batch's new strings go to `agree`
         (a collective: every rank's new strings, in rank order, deduplicated), every rank appends
         the agreed list to its dictionary, and the batch is resolved against it."""
+        p = self.begin(data, nlines, on_upload, agree, ready)
+        return p if isinstance(p, IngestResult) else self.finish(p)
+
+    def begin(self, data, nlines: int | None = None, on_upload=None, agree=None, ready=None):
+        """Enqueue a batch's whole parse -- upload, line starts, parse + dictionary probes, id
+        assignment, filter compaction, gather -- and the copy of its control words to pinned
+        memory, with NO host wait: finish() reads them (one batch later in the deferred ingest of
+        TextParseOp, so the host's work on batch i overlaps the GPU's parse of batch i + 1).
+        Returns a pending handle (or the IngestResult of an empty batch)."""
         m = self._m
         n = count_lines(data) if nlines is None else int(nlines)
         nbytes = len(data) if not isinstance(data, torch.Tensor) else data.numel()
@@ -318,10 +339,13 @@ class TextIngest:
             on_upload(ev)
         dev, st = self.device, self._stream()
         nf, S = self.nf, self.nstr
+        # Two sets of per-batch workspace (a deferred batch's status / line starts are read by
+        # its host patch after the next batch was enqueued).
+        par = self._par = getattr(self, "_par", 0) ^ 1
         ctl = self._buf("ctl", 8, torch.int64)[:8]
         ctl.zero_()
         ctl[1] = I64_MIN
-        starts = self._buf("starts", n + 64, torch.int64)
+        starts = self._buf(f"starts{par}", n + 64, torch.int64)
         if self.cuda:
             scratch = self._buf("scratch", max(m.gpu_filter_compact_scratch_bytes(max(nbytes, n * max(S, 1))), 1),
                                 torch.uint8)
@@ -330,12 +354,18 @@ class TextIngest:
         else:
             scratch = self._buf("scratch", 1, torch.uint8)
             m.cpu_line_starts(buf.data_ptr(), nbytes, starts.data_ptr(), ctl[3:4].data_ptr())
-        self.dict.reserve(n * S, nbytes)
+        # A batch still in flight may add up to its own bound of new strings / bytes (the host's
+        # id count learns them at its finish()).
+        infl = getattr(self, "_inflight", None)
+        if infl is None:
+            infl = self._inflight = {}
+        self.dict.reserve(n * S + sum(a for a, _ in infl.values()),
+                          nbytes + sum(b for _, b in infl.values()))
         # Output columns are fresh per batch (consumers may hold a batch across ticks); the
         # per-string work arrays are workspace.
         cols = torch.empty(nf * n, dtype=torch.int64, device=dev)
         ids = torch.empty(max(S, 1) * n, dtype=torch.int32, device=dev)
-        status = self._buf("status", n, torch.uint8)
+        status = self._buf(f"status{par}", n, torch.uint8)
         np_ = max(n * S, 1)
         out = {"cols": cols.data_ptr(), "ids": ids.data_ptr(), "status": status.data_ptr(),
                "spos": self._buf("spos", np_, torch.int64).data_ptr(),
@@ -353,16 +383,55 @@ class TextIngest:
                               newpos.data_ptr(), st)
         elif agree is not None:
             self._agree_ids(agree, data, keep_alive, buf, nbytes, starts, n, out, scratch)
-        fidx = None
+        fidx = fscr = ocols = oids = None
         if self.filter_prog is not None:
-            fidx = self._buf("fidx", n, torch.int64)
+            # fresh per batch: the kept rows' line indices leave with the batch (line_idx)
+            fidx = torch.empty(n, dtype=torch.int64, device=dev)
             fscr = (self._buf("fscratch", m.gpu_filter_compact_scratch_bytes(n), torch.uint8)
                     if self.cuda else scratch)
             m.ingest_filter_compact(self.cuda, cols.data_ptr(), n, nf, self.dbl_mask,
                                     self.filter_prog.code, self.filter_prog.consts,
                                     fscr.data_ptr(), fidx.data_ptr(), ctl[2:3].data_ptr(), st)
-        # ---- the batch's one host synchronisation: 8 control words + 4 dictionary counters ----
-        h = self._readback(ctl, self.dict.ctr)
+            # the kept rows, gathered with the device count (sized for every line)
+            ocols = torch.empty(nf * n, dtype=torch.int64, device=dev)
+            oids = torch.empty(max(S, 1) * n, dtype=torch.int32, device=dev)
+            m.ingest_gather(self.cuda, cols.data_ptr(), n, nf, ids.data_ptr(), S,
+                            fidx.data_ptr(), ctl[2:3].data_ptr(), ocols.data_ptr(),
+                            oids.data_ptr(), n, st)
+        # ---- the batch's control words + dictionary counters -> pinned memory (no wait) ----
+        hb = self._hbuf_for(par)
+        ev = None
+        if self.cuda:
+            hb[:8].copy_(ctl, non_blocking=True)
+            hb[8:12].copy_(self.dict.ctr, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+        else:
+            hb[:8].copy_(ctl)
+            hb[8:12].copy_(self.dict.ctr)
+        p = _PendingParse(data=data, keep_alive=keep_alive, buf=buf, starts=starts,
+                          status=status, cols=cols, ids=ids, n=n, fidx=fidx, fscr=fscr,
+                          ocols=ocols, oids=oids, hb=hb, ev=ev)
+        infl[id(p)] = (n * S, nbytes)  # new strings / bytes it may add, until its finish()
+        return p
+
+    def _hbuf_for(self, par: int) -> torch.Tensor:
+        hb = getattr(self, "_hbufs", None)
+        if hb is None:
+            pin = self.cuda
+            hb = self._hbufs = [torch.zeros(12, dtype=torch.int64, pin_memory=pin)
+                                for _ in range(2)]
+        return hb[par]
+
+    def finish(self, p: "_PendingParse") -> IngestResult:
+        """The batch's one host synchronisation (usually long complete when deferred): counters,
+        dictionary errors, host patch of flagged lines, then the (kept) columns."""
+        m, nf, S, n = self._m, self.nf, self.nstr, p.n
+        if p.ev is not None:
+            while not p.ev.query():  # poll: a blocking wait wakes tens of microseconds late
+                pass
+        h = p.hb.tolist()
+        self._inflight.pop(id(p), None)
         nflag, max_ts, ftotal, ltotal = h[0] & 0xFFFFFFFF, h[1], h[2], h[3]
         if ltotal != n:
             raise RuntimeError(f"ingest: {ltotal} line starts on the device, {n} counted")
@@ -370,24 +439,23 @@ class TextIngest:
         max_ts = None if max_ts == I64_MIN else max_ts
         if nflag:
             self.stats["flagged_lines"] += nflag
-            max_ts = self._host_patch(data, keep_alive, buf, starts, status, cols, n, max_ts)
+            max_ts = self._host_patch(p.data, p.keep_alive, p.buf, p.starts, p.status, p.cols, n,
+                                      max_ts)
             if self.filter_prog is not None:
-                m.ingest_filter_compact(self.cuda, cols.data_ptr(), n, nf, self.dbl_mask,
+                st = self._stream()
+                ctl = self._buf("ctl", 8, torch.int64)[:8]
+                m.ingest_filter_compact(self.cuda, p.cols.data_ptr(), n, nf, self.dbl_mask,
                                         self.filter_prog.code, self.filter_prog.consts,
-                                        fscr.data_ptr(), fidx.data_ptr(), ctl[2:3].data_ptr(), st)
-                ftotal = self._readback(ctl, self.dict.ctr)[2]
-        del keep_alive
+                                        p.fscr.data_ptr(), p.fidx.data_ptr(),
+                                        ctl[2:3].data_ptr(), st)
+                m.ingest_gather(self.cuda, p.cols.data_ptr(), n, nf, p.ids.data_ptr(), S,
+                                p.fidx.data_ptr(), ctl[2:3].data_ptr(), p.ocols.data_ptr(),
+                                p.oids.data_ptr(), n, st)
+                ftotal = int(ctl[2].item())
         if self.filter_prog is not None:
             k = int(ftotal)
-            ocols = torch.empty(nf * max(k, 1), dtype=torch.int64, device=dev)
-            oids = torch.empty(max(S, 1) * max(k, 1), dtype=torch.int32, device=dev)
-            if k:
-                m.ingest_gather(self.cuda, cols.data_ptr(), n, nf, ids.data_ptr(), S,
-                                fidx.data_ptr(), ctl[2:3].data_ptr(), ocols.data_ptr(),
-                                oids.data_ptr(), max(k, 1), st)
-            line_idx = fidx[:k].clone()
-            return self._result(ocols, oids, max(k, 1), k, max_ts, line_idx, n)
-        return self._result(cols, ids, n, n, max_ts, None, n)
+            return self._result(p.ocols, p.oids, n, k, max_ts, p.fidx[:k], n)
+        return self._result(p.cols, p.ids, n, n, max_ts, None, n)
 
     def _agree_ids(self, agree, data, keep_alive, buf, nbytes, starts, n, out, scratch) -> None:
         """Several ranks: this batch's new strings -> agree() -> the agreed list appended on every

@@ -251,7 +251,8 @@ class TextParseOp(Operator):
     name = "Map"
 
     def __init__(self, spec, *, ts_spec=None, bound: int = 0, filter_prog=None,
-                 threads: int | None = None, device: str | None = None, shared=None):
+                 threads: int | None = None, device: str | None = None, shared=None,
+                 defer: bool = False):
         self.spec = spec
         self.ts_spec = ts_spec
         self.bound = int(bound)
@@ -262,6 +263,12 @@ class TextParseOp(Operator):
         self.device = device
         self.shared = shared if shared is not None else {}
         self.agree = None
+        # defer (device ingest, one rank): batch i's parse is enqueued and its result is read
+        # one pass later, after batch i + 1's parse was enqueued -- the host's work downstream of
+        # batch i overlaps the GPU's parse of batch i + 1. The planner enables it only where a
+        # pass's delay changes nothing (no processing-time windows, no checkpoints).
+        self.defer = bool(defer)
+        self._pending = None
         self.cur_max = LONG_MIN + self.bound  # BoundedOutOfOrdernessTimestampExtractor state
         self.cur_wm = LONG_MIN
 
@@ -307,9 +314,10 @@ class TextParseOp(Operator):
         else:
             self.strings = self.m.StringDict()
 
-    def _parse_device(self, tb: TextBatch) -> DeviceColumnBatch:
-        res = self.ingest.parse(tb.data, tb.n, on_upload=None if (tb.token is None or tb.ready)
-                                else tb.token.uploaded, agree=self.agree, ready=tb.ready)
+    def _parse_device(self, tb: TextBatch, res=None) -> DeviceColumnBatch:
+        if res is None:
+            res = self.ingest.parse(tb.data, tb.n, on_upload=None if (tb.token is None or tb.ready)
+                                    else tb.token.uploaded, agree=self.agree, ready=tb.ready)
         nf = len(self.spec.fields)
         return DeviceColumnBatch(res.n, res.cols[:nf], tuple(k for _, k in self.spec.fields),
                                  self.strings, res.ts, sub0=tb.sub0,
@@ -369,7 +377,38 @@ class TextParseOp(Operator):
         return TextBatch(b"".join(parts), sum(b.n for b in batches), batches[0].sub0,
                          batches[0].parallelism)
 
+    def _complete(self) -> list:
+        """The deferred batch's columns and watermark (TextIngest.finish)."""
+        p, self._pending = self._pending, None
+        if p is None:
+            return []
+        pend, tb = p
+        res = pend if not hasattr(pend, "hb") else self.ingest.finish(pend)
+        dcb = self._parse_device(tb, res)
+        wm = self._advance(dcb.max_ts)
+        return ([dcb] if dcb.n else []) + wm
+
+    def finish(self):
+        return self._complete()
+
     def process(self, items):
+        if self.defer and self.ingest is not None and self.agree is None:
+            out = []
+            for it in items:
+                if isinstance(it, WM):
+                    if it.ts == LONG_MAX:
+                        out.extend(self._complete())  # every batch before end of input
+                    if self.ts_spec is None or it.ts == LONG_MAX:
+                        out.append(it)
+                    continue
+                if not isinstance(it, TextBatch):
+                    raise TypeError(f"TextParseOp got {type(it).__name__}")
+                pend = self.ingest.begin(it.data, it.n,
+                                         on_upload=None if (it.token is None or it.ready)
+                                         else it.token.uploaded, ready=it.ready)
+                out.extend(self._complete())
+                self._pending = (pend, it)
+            return out
         if self.agree is not None:
             # Multi-rank device ingest: exactly one parse (and dictionary agreement) per pass.
             tbs = [it for it in items if isinstance(it, TextBatch)]
@@ -407,6 +446,8 @@ class TextParseOp(Operator):
         return out
 
     def snapshot(self) -> dict:
+        if self._pending is not None:
+            raise RuntimeError("snapshot with a deferred ingest batch in flight")
         return {"cur_max": self.cur_max, "cur_wm": self.cur_wm, "strings": list(self.strings.strings())}
 
     def restore(self, snap: dict) -> None:

@@ -92,3 +92,32 @@ def test_columnar_parse_error_fails_job(tmp_path):
     lines[3210] = "1563452056 10.8.22.1"
     with pytest.raises(JobExecutionException, match="ArrayIndexOutOfBounds"):
         _run_file(tmp_path, C.build_cpu_alert, lines, "auto")
+
+
+def test_deferred_device_ingest_equals_synchronous():
+    """Deferred device ingest (each batch's parse result read one pass later, TextParseOp
+    defer) prints exactly what the synchronous ingest prints, in the same order -- event-time
+    sliding windows (BandwidthMonitorWithEventTime) and the rolling max (ComputeCpuMax)."""
+    from mxstream.api.environment import StreamExecutionEnvironment
+    from mxstream.models import chapters as C
+
+    bw = [f"2019-08-28T10:{(i // 60) % 60:02d}:{i % 60:02d} www.ch{(i * 7) % 13}.com "
+          f"{40 + i % 11 if i % 5 == 0 else 9_000_000 + i}" for i in range(3000)]
+    cpu = [f"{1563452000 + i} 10.8.{i % 37}.1 cpu{i % 4} {(i * 37 % 400) / 4.0}"
+           for i in range(3000)]
+
+    def run(build, lines, defer):
+        out = []
+        env = StreamExecutionEnvironment(4).set_output(out.append)
+        env.config.native = "auto"
+        env.config.device = "cpu"
+        env.config.text_ingest = "device"
+        env.config.ingest_defer = defer
+        build(env, env.from_collection(lines, batch_size=256))
+        env.execute("defer")
+        return out
+
+    for build, lines in ((C.build_bandwidth_event_time, bw), (C.build_compute_cpu_max, cpu)):
+        ref = run(build, lines, False)
+        assert len(ref) > 10
+        assert run(build, lines, True) == ref
