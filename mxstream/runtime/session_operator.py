@@ -680,10 +680,13 @@ class KeyedSessionOperator:
             raise RuntimeError("session overflow-run buffer too small")
         slots = self.ovf_slots[:n_ovf]
         okeys = self.keys_g[slots].cpu().numpy()
-        slot_key = dict(zip(slots.cpu().tolist(), okeys.tolist()))
+        sl = slots.cpu().numpy()
         self._evict(slots=slots)
         rows = self.ovf_rows.view(5, self.ovf_cap)[:, :n_runs].cpu().numpy()
-        rk = np.array([slot_key[s] for s in rows[0].tolist()], dtype=np.int64)
+        # key of every run's slot (vectorised: sorted slots + searchsorted)
+        o = np.argsort(sl, kind="stable")
+        pos = np.searchsorted(sl[o], rows[0])
+        rk = okeys[o][np.minimum(pos, max(o.size - 1, 0))].astype(np.int64)
         self.metrics.overflow_keys += n_ovf
         return int(self.store.merge_runs(rk, rows[1].copy(), rows[2].copy(), rows[3].copy(),
                                          rows[4].copy(), wm))
