@@ -560,18 +560,19 @@ PYBIND11_MODULE(_mxs_native, m) {
                                       intptr_t sk, intptr_t vals, intptr_t n_out,
                                       intptr_t host_recs, intptr_t n_host, uint32_t host_cap,
                                       intptr_t n_ins, int tbits, intptr_t stream, intptr_t skip,
-                                      uint32_t skip_mask, intptr_t heads, intptr_t n_heads) {
+                                      uint32_t skip_mask, intptr_t heads, intptr_t n_heads,
+                                      int pair) {
     return gpu::session_lookup_sort(P<Rec>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2,
                                     P<uint64_t>(keys_g), P<uint64_t>(spill_set), spill_mask,
                                     spill_any, P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_out),
                                     P<Rec>(host_recs), P<uint32_t>(n_host), host_cap,
                                     P<uint32_t>(n_ins), tbits, stream, P<int64_t>(skip), skip_mask,
-                                    P<uint64_t>(heads), P<uint32_t>(n_heads));
+                                    P<uint64_t>(heads), P<uint32_t>(n_heads), pair);
   }, py::arg("recs"), py::arg("counts"), py::arg("nsrc"), py::arg("nsub"), py::arg("bcap"),
      py::arg("cap_log2"), py::arg("keys_g"), py::arg("spill_set"), py::arg("spill_mask"),
      py::arg("spill_any"), py::arg("sk"), py::arg("vals"), py::arg("n_out"), py::arg("host_recs"),
      py::arg("n_host"), py::arg("host_cap"), py::arg("n_ins"), py::arg("tbits"), py::arg("stream"),
-     py::arg("skip") = 0, py::arg("skip_mask") = 0, py::arg("heads") = 0, py::arg("n_heads") = 0);
+     py::arg("skip") = 0, py::arg("skip_mask") = 0, py::arg("heads") = 0, py::arg("n_heads") = 0, py::arg("pair") = 0);
   m.def("gpu_session_heads", [](intptr_t sk, intptr_t n_in, int64_t n_cap, intptr_t heads,
                                 intptr_t n_heads, intptr_t stream) {
     gpu::session_heads(P<int64_t>(sk), P<uint32_t>(n_in), n_cap, P<uint32_t>(heads),
@@ -598,15 +599,21 @@ PYBIND11_MODULE(_mxs_native, m) {
                                       int64_t nslots, intptr_t sess, intptr_t slot_due,
                                       intptr_t slot_last, intptr_t late_cnt, intptr_t ovf_slots,
                                       intptr_t n_ovf, intptr_t ovf_rows, intptr_t n_ovf_runs,
-                                      uint32_t ovf_cap, intptr_t stream) {
+                                      uint32_t ovf_cap, intptr_t stream, int pair) {
     gpu::session_merge_heads(P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_in),
                              P<uint64_t>(heads), P<uint32_t>(n_heads), head_cap,
                              P<uint32_t>(long_heads), P<uint32_t>(n_long), tbits, gap, lateness,
                              wm, tbase, agg, cap_log2, nslots, P<int64_t>(sess),
                              P<int64_t>(slot_due), P<int64_t>(slot_last), P<uint64_t>(late_cnt),
                              P<int64_t>(ovf_slots), P<uint32_t>(n_ovf), P<int64_t>(ovf_rows),
-                             P<uint32_t>(n_ovf_runs), ovf_cap, stream);
-  });
+                             P<uint32_t>(n_ovf_runs), ovf_cap, stream, pair);
+  }, py::arg("sk"), py::arg("vals"), py::arg("n_in"), py::arg("heads"), py::arg("n_heads"),
+     py::arg("head_cap"), py::arg("long_heads"), py::arg("n_long"), py::arg("tbits"),
+     py::arg("gap"), py::arg("lateness"), py::arg("wm"), py::arg("tbase"), py::arg("agg"),
+     py::arg("cap_log2"), py::arg("nslots"), py::arg("sess"), py::arg("slot_due"),
+     py::arg("slot_last"), py::arg("late_cnt"), py::arg("ovf_slots"), py::arg("n_ovf"),
+     py::arg("ovf_rows"), py::arg("n_ovf_runs"), py::arg("ovf_cap"), py::arg("stream"),
+     py::arg("pair") = 0);
   m.def("gpu_session_fire", [](int64_t gap, int64_t lateness, int64_t wm, int agg, int cap_log2,
                                int64_t nslots, intptr_t keys_g, intptr_t sess, intptr_t slot_due,
                                std::vector<int32_t> mc, std::vector<double> mk,

@@ -2571,6 +2571,7 @@ struct SessArgs {
   int32_t agg, cap_log2;
   int64_t nslots;
   int32_t tbits;  // sort key = slot << tbits | (ts - tbase)
+  int32_t st;     // element stride of sk / vals: 1 (two arrays) or 2 (interleaved (key, value))
 };
 
 __device__ __forceinline__ bool set_contains(const uint64_t* set, uint32_t mask, uint64_t key) {
@@ -2816,7 +2817,8 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
     int64_t* __restrict__ sort_out, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
     Rec* __restrict__ host_recs, uint32_t* __restrict__ n_host, uint32_t host_cap,
     uint32_t* __restrict__ n_inserted, int tbits, uint32_t m_cap, const int64_t* __restrict__ skip,
-    uint32_t skip_mask, uint64_t* __restrict__ heads_out, uint32_t* __restrict__ n_heads) {
+    uint32_t skip_mask, uint64_t* __restrict__ heads_out, uint32_t* __restrict__ n_heads,
+    int pair) {
   extern __shared__ __attribute__((aligned(16))) uint64_t slds[];
   // Launched before the host has read the step's partition flags: any flagged word of the
   // reduced vector (bucket overflow, unrepresentable span, reserved key) means the step is
@@ -3010,8 +3012,15 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
       rank += (tj < t || (tj == t && j < i)) ? 1u : 0u;
     }
     const uint32_t out = s_base + start + rank;
-    sort_out[out] = (int64_t)(((sub_slot0 | sl) << tbits) | t);
-    vals_out[out] = val;
+    const int64_t key = (int64_t)(((sub_slot0 | sl) << tbits) | t);
+    if (pair) {
+      // one 16-byte store of the (key, value) pair: half the partial-line write requests of
+      // two scattered 8-byte stores, and the merge reads the pair with one 16-byte load
+      reinterpret_cast<longlong2*>(sort_out)[out] = make_longlong2(key, (long long)val);
+    } else {
+      sort_out[out] = key;
+      vals_out[out] = val;
+    }
     head = rank == 0;
     hv = (uint64_t)(s_base + start) | ((uint64_t)(end - start) << 32);
   };
@@ -3219,8 +3228,8 @@ __device__ __forceinline__ void sess_merge_segment(const int64_t* __restrict__ s
   uint32_t pc = 0;
   int64_t ts = 0;
   for (uint32_t r = i; r < j; ++r) {
-    ts = a.tbase + (sk[r] & tmask);
-    const uint64_t v = agg_lift(a.agg, vals[r]);
+    ts = a.tbase + (sk[(size_t)r * a.st] & tmask);
+    const uint64_t v = agg_lift(a.agg, vals[(size_t)r * a.st]);
     if (pv && ts <= pe) {
       pe = ts + a.gap;
       pa = agg_combine(a.agg, pa, v);
@@ -3280,7 +3289,7 @@ __global__ __launch_bounds__(256) void session_merge_heads_kernel(
       long_heads[atomicAdd(n_long, 1u)] = i;
       continue;
     }
-    sess_merge_segment(sk, vals, i, i + len, sk[i] >> a.tbits, a, o);
+    sess_merge_segment(sk, vals, i, i + len, sk[(size_t)i * a.st] >> a.tbits, a, o);
   }
 }
 
@@ -3297,7 +3306,7 @@ __global__ __launch_bounds__(256) void session_merge_long_kernel(
   const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
   for (uint32_t h = wave; h < nh; h += nwaves) {
     const uint32_t start = heads[h];
-    const int64_t slot = sk[start] >> a.tbits;
+    const int64_t slot = sk[(size_t)start * a.st] >> a.tbits;
     const int64_t tmask = ((int64_t)1 << a.tbits) - 1;
     SessState st;
     sess_load(st, o.sess + slot * kSess);
@@ -3312,11 +3321,12 @@ __global__ __launch_bounds__(256) void session_merge_long_kernel(
     uint32_t pc = 0;
     for (uint32_t b0 = start;; b0 += 64) {
       const uint32_t i = b0 + lane;
-      const bool in = i < n && sk[i] != INT64_MAX && (sk[i] >> a.tbits) == slot;
+      const int64_t ki = i < n ? sk[(size_t)i * a.st] : INT64_MAX;
+      const bool in = ki != INT64_MAX && (ki >> a.tbits) == slot;
       const unsigned long long inm = __ballot(in);
       if (!inm) break;
-      const int64_t ts = in ? a.tbase + (sk[i] & tmask) : 0;
-      const uint64_t v = in ? agg_lift(a.agg, vals[i]) : 0;
+      const int64_t ts = in ? a.tbase + (ki & tmask) : 0;
+      const uint64_t v = in ? agg_lift(a.agg, vals[(size_t)i * a.st]) : 0;
       const int64_t prev_ts = __shfl_up(ts, 1);
       const bool head = in && (lane == 0 || ts > prev_ts + a.gap);
       // Segmented inclusive scan of (acc, cnt) over runs.
@@ -4741,8 +4751,9 @@ void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_
 
 
 static SessArgs make_sess_args(int64_t gap, int64_t lateness, int64_t wm, int64_t tbase, int agg,
-                               int cap_log2, int64_t nslots, int tbits = 32) {
+                               int cap_log2, int64_t nslots, int tbits = 32, int st = 1) {
   SessArgs a;
+  a.st = st;
   a.tbits = tbits;
   a.gap = gap;
   a.lateness = lateness;
@@ -4788,8 +4799,10 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
                          uint32_t spill_mask, int spill_any, int64_t* sort_out, uint64_t* vals_out,
                          uint32_t* n_out, Rec* host_recs, uint32_t* n_host, uint32_t host_cap,
                          uint32_t* n_inserted, int tbits, intptr_t stream, const int64_t* skip,
-                         uint32_t skip_mask, uint64_t* heads_out, uint32_t* n_heads) {
+                         uint32_t skip_mask, uint64_t* heads_out, uint32_t* n_heads, int pair) {
   if (nsrc * nsub <= 0) return true;
+  if (pair && ((uintptr_t)sort_out & 15))
+    throw std::invalid_argument("session_lookup_sort: pair output must be 16-byte aligned");
   if (tbits < 1 || tbits > 32) throw std::invalid_argument("session_lookup_sort: tbits out of range");
   const uint64_t m64 = (uint64_t)nsrc * bcap;
   if (nsrc > 64 || cap_log2 > kSessLookupLdsMaxLog2 || m64 > 65535) return false;
@@ -4807,7 +4820,7 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
                      (hipStream_t)stream, recs, counts, nsrc, nsub, bcap, cap_log2, keys_g,
                      spill_set, spill_mask, spill_any, sort_out, vals_out, n_out, host_recs,
                      n_host, host_cap, n_inserted, tbits, m_cap, skip, skip_mask, heads_out,
-                     n_heads);
+                     n_heads, pair);
   HIP_CHECK(hipGetLastError());
   return true;
 }
@@ -4843,8 +4856,11 @@ void session_merge_heads(const int64_t* sk, const uint64_t* vals, const uint32_t
                          int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
                          int64_t nslots, int64_t* sess, int64_t* slot_due, int64_t* slot_last,
                          uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf, int64_t* ovf_rows,
-                         uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream) {
-  const SessArgs a = make_sess_args(gap, lateness, wm, tbase, agg, cap_log2, nslots, tbits);
+                         uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream, int pair) {
+  // pair: session_lookup_sort wrote interleaved (sort key, value) pairs at sk (vals unused)
+  const SessArgs a = make_sess_args(gap, lateness, wm, tbase, agg, cap_log2, nslots, tbits,
+                                    pair ? 2 : 1);
+  if (pair) vals = reinterpret_cast<const uint64_t*>(sk) + 1;
   const SessOut o{reinterpret_cast<SessRec*>(sess), slot_due, slot_last, late_cnt,
                   ovf_slots, n_ovf, ovf_rows, n_ovf_runs, ovf_cap};
   hipLaunchKernelGGL(session_merge_heads_kernel, dim3(grid_for(head_cap, 256, 16384)), dim3(256),

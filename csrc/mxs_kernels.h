@@ -275,7 +275,8 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
                          uint32_t* n_out, Rec* host_recs, uint32_t* n_host, uint32_t host_cap,
                          uint32_t* n_inserted, int tbits, intptr_t stream,
                          const int64_t* skip = nullptr, uint32_t skip_mask = 0,
-                         uint64_t* heads_out = nullptr, uint32_t* n_heads = nullptr);
+                         uint64_t* heads_out = nullptr, uint32_t* n_heads = nullptr,
+                         int pair = 0);
 void session_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
                    uint32_t* n_heads, intptr_t stream);
 void session_merge(const int64_t* sk, const uint64_t* vals, const uint32_t* n_in,
@@ -291,7 +292,7 @@ void session_merge_heads(const int64_t* sk, const uint64_t* vals, const uint32_t
                          int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
                          int64_t nslots, int64_t* sess, int64_t* slot_due, int64_t* slot_last,
                          uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf, int64_t* ovf_rows,
-                         uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream);
+                         uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream, int pair = 0);
 void session_fire(int64_t gap, int64_t lateness, int64_t wm, int agg, int cap_log2,
                   int64_t nslots, const uint64_t* keys_g, int64_t* sess, int64_t* slot_due,
                   const ExprProg& map, const ExprProg& filt, uint64_t* out_key, int64_t* out_start,

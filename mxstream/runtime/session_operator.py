@@ -55,6 +55,9 @@ TOMB_KEY = -2             # ~1ull
 # "radix" = lookup + device-wide radix sort (A/B and the fallback when a sub-table's records
 # cannot be staged in LDS).
 _SESSION_SORT = __import__("os").environ.get("MXS_SESSION_SORT", "lds")
+# The fused lookup-sort writes interleaved (key, value) pairs (one 16-byte store per record)
+# instead of two scattered 8-byte stores; "0" keeps the two arrays.
+_SESSION_PAIR = int(__import__("os").environ.get("MXS_SESSION_PAIR", "1"))
 
 
 def _next_pow2(x: int) -> int:
@@ -230,8 +233,10 @@ class KeyedSessionOperator:
             total = self.nbuckets * self.bucket_cap
             self.sort_key = torch.empty(total, dtype=torch.int64, device=dev)
             self.vals_buf = torch.empty(total, dtype=torch.int64, device=dev)
-            self.sort_out = torch.empty(total, dtype=torch.int64, device=dev)
-            self.vals_out = torch.empty(total, dtype=torch.int64, device=dev)
+            # One buffer: (sort_out | vals_out) for the radix path, or the interleaved
+            # (key, value) pairs the fused lookup-sort writes with 16-byte stores.
+            self._sv_out = torch.empty(2 * total, dtype=torch.int64, device=dev)
+            self.sort_out, self.vals_out = self._sv_out[:total], self._sv_out[total:]
             self._sort_tmp = None
             self.heads = torch.empty(total, dtype=torch.int32, device=dev)
             # key segments of the fused lookup-sort (output position | length << 32)
@@ -549,7 +554,7 @@ class KeyedSessionOperator:
                 c[2:3].data_ptr(), self.host_cap, c[3:4].data_ptr(), tbits, st,
                 skip.data_ptr() if skip is not None else 0,
                 self._SKIP_MASK if skip is not None else 0,
-                self.seg_heads.data_ptr(), c[10:11].data_ptr()):
+                self.seg_heads.data_ptr(), c[10:11].data_ptr(), _SESSION_PAIR):
             return False
         # One lane per key segment listed by the lookup-sort (c[10] segments on the device).
         m.gpu_session_merge_heads(self.sort_out.data_ptr(), self.vals_out.data_ptr(),
@@ -560,7 +565,8 @@ class KeyedSessionOperator:
                                   self.sess.data_ptr(), self.slot_due.data_ptr(),
                                   self.slot_last.data_ptr(), self.late_cnt.data_ptr(),
                                   self.ovf_slots.data_ptr(), c[4:5].data_ptr(),
-                                  self.ovf_rows.data_ptr(), c[5:6].data_ptr(), self.ovf_cap, st)
+                                  self.ovf_rows.data_ptr(), c[5:6].data_ptr(), self.ovf_cap, st,
+                                  _SESSION_PAIR)
         return True
 
     def _fold_counters(self, with_red: bool = False) -> list[int]:
