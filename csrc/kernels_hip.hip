@@ -3162,6 +3162,10 @@ __device__ __forceinline__ void sess_store(const SessState& st, SessRec* r) {
 }
 
 // Per-key fold state shared by the thread-per-segment and wave-per-segment merge kernels.
+// Per-slot (due, last) words are interleaved: slot_due points at word 0 of a 16-byte pair per
+// slot, slot_last at word 1 (session_operator.py allocates one (nslots, 2) tensor).
+constexpr int64_t kSlotMeta = 2;
+
 struct SessOut {
   SessRec* sess;
   int64_t* slot_due;
@@ -3200,8 +3204,10 @@ __device__ __forceinline__ void sess_finish(const SessState& st, int64_t slot, i
                                             uint64_t late, bool overflow, const SessArgs& a,
                                             const SessOut& o) {
   sess_store(st, o.sess + slot * kSess);
-  o.slot_due[slot] = sess_due(st, a.lateness);
-  if (last_ts > o.slot_last[slot]) o.slot_last[slot] = last_ts;
+  // (due, last) of the slot share one 16-byte word: one read and one store per merged key
+  longlong2* meta = reinterpret_cast<longlong2*>(o.slot_due) + slot;
+  const long long prev_last = meta->y;
+  *meta = make_longlong2(sess_due(st, a.lateness), last_ts > prev_last ? last_ts : prev_last);
   if (late) atomicAdd((unsigned long long*)o.late_cnt, (unsigned long long)late);
   if (overflow) {
     const uint32_t q = atomicAdd(o.n_ovf, 1u);
@@ -3396,7 +3402,7 @@ __global__ __launch_bounds__(256) void session_fire_kernel(
   for (int64_t base = (int64_t)blockIdx.x * blockDim.x; base < a.nslots;
        base += (int64_t)gridDim.x * blockDim.x) {
     const int64_t slot = base + threadIdx.x;
-    const bool due = slot < a.nslots && slot_due[slot] <= a.wm;
+    const bool due = slot < a.nslots && slot_due[slot * kSlotMeta] <= a.wm;
     if (!__ballot(due)) continue;
     SessState st;
     sess_clear(st);
@@ -3450,7 +3456,7 @@ __global__ __launch_bounds__(256) void session_fire_kernel(
       for (int j = 0; j < kSess; ++j)
         if (st.cnt[j] && (st.end[j] - 1) + a.lateness <= a.wm) st.cnt[j] = 0;
       sess_store(st, sess + slot * kSess);
-      slot_due[slot] = sess_due(st, a.lateness);
+      slot_due[slot * kSlotMeta] = sess_due(st, a.lateness);
     }
   }
 }
@@ -3477,7 +3483,7 @@ __global__ __launch_bounds__(kEvictBlock) void session_evict_kernel(
     if (i < total) {
       slot = slots ? slots[i] : i;
       key = keys_g[slot];
-      take = key != kEmptyKey && key != kTombKey && (slots || slot_last[slot] < idle_before);
+      take = key != kEmptyKey && key != kTombKey && (slots || slot_last[slot * kSlotMeta] < idle_before);
     }
     SessState st;
     sess_clear(st);
@@ -3533,8 +3539,8 @@ __global__ __launch_bounds__(kEvictBlock) void session_evict_kernel(
       done = true;
     }  // else: staging full, the key stays resident this round
     if (done) {
-      slot_due[slot] = INT64_MAX;
-      slot_last[slot] = INT64_MIN;
+      slot_due[slot * kSlotMeta] = INT64_MAX;
+      slot_last[slot * kSlotMeta] = INT64_MIN;
       keys_g[slot] = kTombKey;
     }
     const unsigned long long dm = __ballot(done);
@@ -3638,8 +3644,8 @@ __global__ __launch_bounds__(256) void session_rehash_kernel(
     const int64_t ns = (sub << a.cap_log2) | s;  // never kNoSlot: the old table held the key
 #pragma unroll
     for (int j = 0; j < kSess; ++j) sess_n[ns * kSess + j] = sess_o[slot * kSess + j];
-    due_n[ns] = due_o[slot];
-    last_n[ns] = last_o[slot];
+    due_n[ns * kSlotMeta] = due_o[slot * kSlotMeta];
+    last_n[ns * kSlotMeta] = last_o[slot * kSlotMeta];
   }
   for (int d = 32; d >= 1; d >>= 1) ins += __shfl_xor(ins, d);
   if (lane_id() == 0 && ins) atomicAdd(&s_ins, ins);
@@ -3711,8 +3717,8 @@ __global__ __launch_bounds__(256) void session_promote_kernel(
     }
 #pragma unroll
     for (int j = 0; j < W; ++j) sess[s * W + j] = rec[i * W + j];
-    slot_due[s] = INT64_MIN;  // the next fire sweep recomputes the due time
-    slot_last[s] = last[i];
+    slot_due[s * kSlotMeta] = INT64_MIN;  // the next fire sweep recomputes the due time
+    slot_last[s * kSlotMeta] = last[i];
   }
 }
 

@@ -254,8 +254,12 @@ class KeyedSessionOperator:
         self.keys_g = torch.full((n,), EMPTY_KEY, dtype=torch.int64, device=dev)
         # [slot][kSess] x {start, end, acc, cnt | flags << 32}: one 128-byte record per slot.
         self.sess = torch.zeros(n * K_SESS * 4, dtype=torch.int64, device=dev)
-        self.slot_due = torch.full((n,), I64_MAX, dtype=torch.int64, device=dev)
-        self.slot_last = torch.full((n,), I64_MIN, dtype=torch.int64, device=dev)
+        # (due, last) per slot in one 16-byte pair (the merge reads and writes both at once);
+        # slot_due / slot_last are strided views of it (kSlotMeta in csrc/kernels_hip.hip)
+        self._slot_meta = torch.empty((n, 2), dtype=torch.int64, device=dev)
+        self.slot_due, self.slot_last = self._slot_meta[:, 0], self._slot_meta[:, 1]
+        self.slot_due.fill_(I64_MAX)
+        self.slot_last.fill_(I64_MIN)
 
     def state_bytes(self) -> int:
         if self.gpu:
