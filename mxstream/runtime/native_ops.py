@@ -1333,7 +1333,109 @@ class NativeVectorWindowOp(NativeWindowOp):
     input length. Windows and watermarks behave exactly as in NativeWindowOp."""
 
     name = "VectorWindow(native)"
-    _exchange_ok = False  # vector rows come from host records (no device ingest of vectors)
+    _exchange_ok = False  # no device ingest of vectors: the host-record exchange below instead
+
+    def open(self, ctx):
+        super().open(ctx)
+        comm = getattr(ctx, "comm", None)
+        if comm is not None and comm.world > 1 and self.scalar_result and self.late_tag is None:
+            # G > 1: the operator takes this rank's records as they are and moves (key id, ts,
+            # row) records plus their vectors to the key's owner inside VectorWindowOperator's
+            # all-to-all (RCCL). Only the pass's NEW key strings travel as objects, so every
+            # rank interns them in the same order and the ids agree (the key groups come from
+            # the ids' Java hashes). The result is the aggregate alone (no keep-first
+            # template), so the owner needs nothing else from the record's source rank.
+            self.comm = comm
+            self.device_exchange = self.collective = True
+            self._vknown: set = set()  # key strings interned (identically on every rank)
+
+    def _process_exchange(self, items) -> list:
+        """One collective step per pass: agree on new keys and the vector length, then the
+        engine step (records and vectors exchanged inside), then the merged watermark."""
+        recs = [r for r in expand_columns([it for it in items if not isinstance(it, WM)])
+                if isinstance(r, Rec)]
+        wms = [it.ts for it in items if isinstance(it, WM)]
+        err, new, seen_new, vlen, kind = None, [], set(), None, None
+        try:
+            for r in recs:
+                v = r.value
+                if not isinstance(v, tuple) or (self.ok_arities and len(v) not in self.ok_arities):
+                    raise TypeError("vector window input must be a tuple")
+                k, x = v[self.key_pos], v[self.val_pos]
+                if not isinstance(x, (list, tuple)):
+                    raise TypeError("metric vector field must be a list")
+                vlen = len(x) if vlen is None else vlen
+                if isinstance(k, str):
+                    kind = kind or "str"
+                    if k not in seen_new and k not in self._vknown:
+                        seen_new.add(k)
+                        new.append(k)
+                elif isinstance(k, int) and not isinstance(k, bool) and 0 <= k < (1 << 63) - 1:
+                    kind = kind or "int"
+                else:
+                    raise TypeError("unsupported key type for the native path")
+        except TypeError as e:
+            err = str(e)
+        got = self.comm.all_gather_object((new, vlen, kind, err))
+        errs = [e for *_, e in got if e]
+        if errs:
+            raise TypeError(f"native vector window at G > 1: {errs[0]}")
+        kinds = {k for _, _, k, _ in got if k} | ({"str" if self.str_keys else "int"}
+                                                 if self.str_keys is not None else set())
+        if len(kinds) > 1:
+            raise TypeError("mixed key types")
+        if kinds:
+            self.str_keys = kinds.pop() == "str"
+        lens = {n for _, n, _, _ in got if n is not None}
+        if self.op is not None:
+            lens.add(self.vlen)
+        if len(lens) > 1:
+            raise TypeError("metric vectors must all have the first vector's length")
+        grew = False
+        for strs, *_ in got:  # rank order: identical interning on every rank
+            for st in strs:
+                if st not in self._vknown:
+                    self._vknown.add(st)
+                    self.dict.intern(st)
+                    grew = True
+        if grew or getattr(self, "_vjh_t", None) is None:
+            self._vjh_t = torch.from_numpy(self.dict.jhash_table())
+        if self.op is None and lens:
+            if not self._build([0.0] * lens.pop()):
+                raise TypeError("metric vectors wider than the kernel")
+        out = []
+        if self.op is not None:
+            if self.str_keys:
+                self.op.jhash = self._vjh_t.to(self.op.device)
+            n, dim = len(recs), self.op.dim
+            kid = np.empty(n, dtype=np.int64)
+            tsa = np.empty(n, dtype=np.int64)
+            vv = np.zeros((n, dim), dtype=np.float32)
+            event = self.assigner.is_event_time()
+            now = self.ctx.clock()
+            for i, r in enumerate(recs):
+                v = r.value
+                k = v[self.key_pos]
+                kid[i] = self.dict.intern(k) if self.str_keys else k  # agreed id
+                tsa[i] = r.ts if event else now
+                vv[i, :self.vlen] = v[self.val_pos]
+            dev = self.op.device
+            late_before = self.op.metrics.num_late_records_dropped
+            out = self._emit(self.op.process(torch.from_numpy(kid).to(dev),
+                                             torch.from_numpy(tsa).to(dev),
+                                             torch.from_numpy(vv).to(dev)))
+            self.num_late_records_dropped += self.op.metrics.num_late_records_dropped - late_before
+        for w in wms:
+            self.wm = w
+            if self.op is not None and self.assigner.is_event_time():
+                out.extend(self._emit(self.op.advance_watermark(w)))
+            out.append(WM(w))
+        return out
+
+    def on_processing_time(self, now):
+        if self.device_exchange and self.op is None:
+            return []  # collective: no rank has built the operator yet (agreed in the pass)
+        return super().on_processing_time(now)
 
     def _build(self, sample_val, dense: bool = False) -> bool:
         if not isinstance(sample_val, (list, tuple)) or not sample_val \
@@ -1349,10 +1451,17 @@ class NativeVectorWindowOp(NativeWindowOp):
             return False
         a = self.assigner
         event = a.is_event_time()
+        comm = getattr(self, "comm", None)
+        multi = comm is not None and comm.world > 1
         self.op = VectorWindowOperator(
             dim=dim, avg=self.kind == "vavg", size=a.size, slide=a.slide, offset=a.offset,
             lateness=self.lateness if event else 0, device=torch.device(self.device),
-            max_keys=self.max_keys, parallelism=1, batch_capacity=max(1024, self.ctx.parallelism),
+            max_keys=self.max_keys, parallelism=self.ctx.parallelism if multi else 1,
+            comm=comm if multi else None,
+            max_parallelism=self.ctx.max_parallelism if multi else 128,
+            hash_mode=1 if (multi and self.str_keys) else 0,
+            jhash_table=self._vjh_t if (multi and self.str_keys) else None,
+            batch_capacity=max(1024, self.ctx.parallelism),
             cap_log2=9, time_mode="event" if event else "processing", external_watermark=True,
             side_output_late=self.late_tag is not None, clock=self.ctx.clock)
         return True
@@ -1410,7 +1519,9 @@ class NativeVectorWindowOp(NativeWindowOp):
             for k, vec in zip(fr.keys.tolist(), fr.values):
                 key_obj = self.dict.get(k) if self.str_keys else k
                 res = [float(x) for x in vec[:self.vlen]]
-                value = self.result_builder(self._template(k), res, key_obj)
+                # a bare aggregate result reads no template (none exists off the source rank)
+                tpl = None if self.scalar_result else self._template(k)
+                value = self.result_builder(tpl, res, key_obj)
                 sub = (flink_murmur(java_hash(key_obj)) % MP) * P // MP
                 out.append(Rec(value, ts, sub))
         return out
@@ -1431,5 +1542,8 @@ class NativeVectorWindowOp(NativeWindowOp):
         self.templates = dict(snap["templates"])
         for st in snap["strings"]:
             self.dict.intern(st)
+        if self.device_exchange:
+            self._vknown.update(snap["strings"])
+            self._vjh_t = torch.from_numpy(self.dict.jhash_table())
         self._build([0.0] * eng["vlen"])
         self.op.restore_state(eng["columns"], eng["meta"])

@@ -87,3 +87,73 @@ def test_vector_api_gpu_equals_host(gpu_device):
     a = _run(events, 3000, 1000, 500, "off", VectorAvgAggregate)
     b = _run(events, 3000, 1000, 500, "auto", VectorAvgAggregate, device="cuda")
     _same(a, b)
+
+
+def _run_ranks(events, world, device="cpu"):
+    """The vector job on `world` loopback ranks: keyed records and their vectors move inside
+    the operator's all-to-all; the executor's pickled exchange carries no record."""
+    from mxstream.parallel.comm import run_loopback
+    from mxstream.runtime import executor as X
+
+    seen = {"recs": 0, "device": []}
+    orig = X.Executor._exchange
+
+    def spy(self, n, items):
+        out = orig(self, n, items)
+        if n.key_fn_in is not None:
+            dx = getattr(self.ops.get(n.id), "device_exchange", False)
+            # records that stay on their rank for the operator's own exchange are not pickled
+            if not dx:
+                seen["recs"] += sum(1 for it in out if isinstance(it, X.Rec))
+            seen["device"].append(dx)
+        return out
+
+    def body(comm):
+        out = []
+        env = StreamExecutionEnvironment(4, clock=ManualClock(0)).set_output(out.append)
+        env.config.native = "auto"
+        env.config.device = device
+        env._comm = comm
+        env.set_stream_time_characteristic(TimeCharacteristic.EventTime)
+        (env.from_collection(events, batch_size=16)
+            .assign_timestamps_and_watermarks(
+                BoundedOutOfOrdernessTimestampExtractor(Time.milliseconds(500),
+                                                        extractor=lambda e: e[2]))
+            .map(lambda e: Tuple2(e[0], list(e[1])))
+            .key_by(0)
+            .time_window(Time.milliseconds(3000), Time.milliseconds(1000))
+            .aggregate(VectorAvgAggregate(1))
+            .print())
+        env.execute("vector-ranks")
+        return out
+
+    X.Executor._exchange = spy
+    try:
+        kw = {"device": __import__("torch").device("cuda", 0)} if device == "cuda" else {}
+        res = run_loopback(world, body, **kw)
+    finally:
+        X.Executor._exchange = orig
+    return [l for out in res for l in out], seen
+
+
+def _vec_events(n=320):
+    return [("h%d" % (i % 7), [i % 13, (i * 7) % 100, 3], 100 * i) for i in range(n)]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_vector_window_device_exchange_ranks(world):
+    events = _vec_events()
+    ref = _run(events, 3000, 1000, 500, "auto", VectorAvgAggregate)
+    got, seen = _run_ranks(events, world)
+    assert seen["recs"] == 0 and seen["device"] and all(seen["device"])
+    _same(ref, got)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_gpu_vector_window_device_exchange_ranks(world, gpu_device):
+    events = _vec_events()
+    ref = _run(events, 3000, 1000, 500, "off", VectorAvgAggregate)
+    got, seen = _run_ranks(events, world, device="cuda")
+    assert seen["recs"] == 0 and all(seen["device"])
+    _same(ref, got)
