@@ -5,10 +5,12 @@
 #define MXS_SESSION_STORE_H_
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <deque>
 #include <queue>
 #include <stdexcept>
+#include <thread>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -224,7 +226,9 @@ class SessionCore {
       wmax = k > wmax ? k : wmax;
     }
     const uint64_t wspan = n ? wmax - wmin + 1 : 0;
-    const bool dense = n && wspan <= (uint64_t)16 * n + 65536 && wspan <= ((uint64_t)1 << 27);
+    // The bitmap (<= 16 MB) pays even for few keys in a wide span: membership tests in a
+    // chunk scan stay sequential and cache-resident (a hash-set probe per cold row cost 20 ns).
+    const bool dense = n && wspan <= ((uint64_t)1 << 27);
     std::vector<uint64_t> want;
     std::vector<uint64_t> wbits;  // dense: bit (key - wmin) set for wanted keys
     if (dense) {
@@ -251,7 +255,78 @@ class SessionCore {
     std::vector<uint64_t> wset;  // hash set of `want`, built on first use
     size_t wmask = 0;
     if (cold_rows_ && !want.empty()) {
-      for (auto& ch : cold_) {
+      // Dense keys: the chunks that need a full scan (no row index, or many wanted keys --
+      // every chunk of scattered evictions spans the whole id range) are scanned in parallel,
+      // one chunk per task; their rows lead `cold` (a key's rows keep their order: they sit in
+      // one chunk, and the key sort below is stable).
+      std::vector<char> pdone;
+      if (dense) {
+        std::vector<size_t> scan;
+        size_t rows = 0;
+        for (size_t ci = 0; ci < cold_.size(); ++ci) {
+          const ColdChunk& ch = cold_[ci];
+          if (!ch.live || want.back() < ch.kmin || want.front() > ch.kmax) continue;
+          auto lo = std::lower_bound(want.begin(), want.end(), ch.kmin);
+          auto hi = std::upper_bound(lo, want.end(), ch.kmax);
+          const size_t nw = (size_t)(hi - lo), nc = ch.key.size();
+          if (lo != hi && (ch.by_key.size() != nc || nw * 20 >= nc)) {
+            scan.push_back(ci);
+            rows += nc;
+          }
+        }
+        unsigned hw = std::thread::hardware_concurrency();
+        const size_t nth = std::min<size_t>({scan.size(), hw ? hw : 1, 16, rows / 65536 + 1});
+        if (nth > 1) {
+          // Two passes, each one chunk per task: count the kept rows, then write them at their
+          // offsets in `cold` (growing per-task vectors cost more in page faults and unmaps
+          // than the scan itself).
+          pdone.assign(cold_.size(), 0);
+          std::vector<size_t> keep(scan.size() + 1, 0), gone(scan.size(), 0);
+          auto pfor = [&](auto&& body) {
+            std::atomic<size_t> next{0};
+            auto work = [&] {
+              for (size_t j; (j = next.fetch_add(1)) < scan.size();) body(j);
+            };
+            std::vector<std::thread> th;
+            for (size_t t = 1; t < nth; ++t) th.emplace_back(work);
+            work();
+            for (auto& t : th) t.join();
+          };
+          pfor([&](size_t j) {
+            const ColdChunk& ch = cold_[scan[j]];
+            const uint32_t nc = (uint32_t)ch.key.size();
+            size_t k = 0, g = 0;
+            for (uint32_t r = 0; r < nc; ++r) {
+              if (!ch.cnt[r] || !wanted_dense(ch.key[r])) continue;
+              ++g;
+              k += cleanup_time(ch.end[r] - 1) > wm;
+            }
+            keep[j + 1] = k;
+            gone[j] = g;
+          });
+          for (size_t j = 0; j < scan.size(); ++j) keep[j + 1] += keep[j];
+          cold.resize(keep[scan.size()]);
+          pfor([&](size_t j) {
+            ColdChunk& ch = cold_[scan[j]];
+            const uint32_t nc = (uint32_t)ch.key.size();
+            auto* o = cold.data() + keep[j];
+            for (uint32_t r = 0; r < nc; ++r) {
+              if (!ch.cnt[r] || !wanted_dense(ch.key[r])) continue;
+              if (cleanup_time(ch.end[r] - 1) > wm)
+                *o++ = {ch.key[r], Session{ch.start[r], ch.end[r], ch.acc[r], ch.cnt[r], 1u}};
+              ch.cnt[r] = 0;
+            }
+            ch.live -= gone[j];
+          });
+          for (size_t j = 0; j < scan.size(); ++j) {
+            pdone[scan[j]] = 1;
+            cold_rows_ -= gone[j];
+          }
+        }
+      }
+      for (size_t ci = 0; ci < cold_.size(); ++ci) {
+        auto& ch = cold_[ci];
+        if (!pdone.empty() && pdone[ci]) continue;  // scanned above
         if (!ch.live || want.back() < ch.kmin || want.front() > ch.kmax) continue;
         auto lo = std::lower_bound(want.begin(), want.end(), ch.kmin);
         auto hi = std::upper_bound(lo, want.end(), ch.kmax);
@@ -300,7 +375,7 @@ class SessionCore {
           for (; p != ch.by_key.end() && ch.key[*p] == *it; ++p) take(*p);
         }
       }
-      if (dense && cold.size() > 1) {
+      if (dense && cold.size() > 1 && wspan <= (uint64_t)4 * cold.size() + 65536) {
         // stable counting sort by key offset (same order as the stable comparison sort)
         std::vector<uint32_t> cnt(wspan + 1, 0);
         for (const auto& c : cold) ++cnt[c.first - wmin + 1];
@@ -308,13 +383,40 @@ class SessionCore {
         std::vector<std::pair<uint64_t, Session>> sorted(cold.size());
         for (const auto& c : cold) sorted[cnt[c.first - wmin]++] = c;
         cold.swap(sorted);
-      } else {
+      } else if (cold.size() > 1 && cold.size() < ((size_t)1 << 24) && wspan != 0 &&
+                 64 - __builtin_clzll(wspan | 1) + 24 <= 64) {
+        // Few rows in a wide key span: LSD radix sort of (key offset << 24 | row) words, 11-bit
+        // digits (a stable_sort of the 40-byte rows moved ~100 MB for 10^5 rows). The row
+        // index in the low bits keeps equal keys in their original order.
+        const int kb = 64 - __builtin_clzll(wspan | 1) + 24;
+        std::vector<uint64_t> a(cold.size()), b(cold.size());
+        for (size_t i = 0; i < cold.size(); ++i) a[i] = ((cold[i].first - wmin) << 24) | i;
+        std::vector<uint32_t> off(2048);
+        for (int sh = 24; sh < kb; sh += 11) {  // the row bits are already in order
+          std::fill(off.begin(), off.end(), 0u);
+          for (uint64_t x : a) ++off[(x >> sh) & 2047u];
+          uint32_t t = 0;
+          for (auto& c : off) {
+            const uint32_t y = c;
+            c = t;
+            t += y;
+          }
+          for (uint64_t x : a) b[off[(x >> sh) & 2047u]++] = x;
+          a.swap(b);
+        }
+        std::vector<std::pair<uint64_t, Session>> sorted(cold.size());
+        for (size_t i = 0; i < a.size(); ++i) sorted[i] = cold[a[i] & 0xFFFFFFu];
+        cold.swap(sorted);
+      } else if (cold.size() > 1) {
         std::stable_sort(cold.begin(), cold.end(),
                          [](const auto& a, const auto& b) { return a.first < b.first; });
       }
     }
     const bool no_hot = m_.empty();
     Columns out;
+    for (auto* v : {&out.key, &out.start, &out.end, &out.acc, &out.cnt, &out.flags})
+      v->reserve(cold.size() + (no_hot ? 0 : want.size()));
+    moved->reserve(moved->size() + want.size());
     size_t c = 0;
     for (uint64_t key : want) {
       const size_t c0 = c;

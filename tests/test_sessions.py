@@ -211,6 +211,41 @@ def test_store_cold_index_lookup_equals_hot(spread):
     assert cold.num_keys() == 0
 
 
+def test_store_extract_parallel_chunk_scan():
+    """extract_packed over several large cold chunks of scattered dense keys (the promote path
+    of config 5 with revisits): the chunks are scanned in parallel; the packed slot records
+    equal the inserted sessions of the wanted keys, in key order, and the rows leave the store."""
+    from mxstream.ops.native import load
+
+    m = load()
+    rng = np.random.default_rng(5)
+    st_ = m.SessionStore(100, 1000, K.AGG_SUM_I64)
+    nk, nchunks = 600_000, 4
+    keys = rng.permutation(nk).astype(np.int64)
+    s = (keys % 4000).astype(np.int64) + 10_000
+    e = s + 100
+    acc = keys * 3
+    ones = np.ones_like(keys)
+    for c in np.array_split(np.arange(nk), nchunks):  # one cold chunk per eviction batch
+        st_.insert(keys[c], s[c], e[c], acc[c], ones[c], ones[c], True)
+    assert st_.num_cold_rows() == nk
+    want = rng.choice(nk, 20_000, replace=False).astype(np.int64)
+    ex = st_.extract_packed(want, 0, 4, 100)
+    uk = np.sort(want)
+    assert np.array_equal(ex["key"], uk)
+    assert np.array_equal(np.sort(ex["moved"]), uk)
+    rec = ex["rec"].reshape(uk.size, 4, 4)
+    assert np.array_equal(rec[:, 0, 0], (uk % 4000) + 10_000)
+    assert np.array_equal(rec[:, 0, 1], (uk % 4000) + 10_100)
+    assert np.array_equal(rec[:, 0, 2], uk * 3)
+    assert np.array_equal(rec[:, 0, 3], np.full(uk.size, 1 | (1 << 32)))
+    assert not rec[:, 1:].any()
+    assert np.array_equal(ex["last"], (uk % 4000) + 10_000)
+    assert st_.num_cold_rows() == nk - uk.size
+    again = st_.extract_packed(want, 0, 4, 100)  # already gone
+    assert again["key"].size == 0
+
+
 # ----------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
 @settings(max_examples=15, deadline=None, suppress_health_check=[HealthCheck.too_slow])
