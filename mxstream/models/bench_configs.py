@@ -410,8 +410,8 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
             "p50_alert_latency_ms": statistics.median(lat) if lat else None,
             "p99_alert_latency_ms": (sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))]
                                      if lat else None),
-            "firings_measured": len(lat), "latency_fire": latency_fire,
-            "latency_fire_steps": op.metrics.extra.get("latency_fires", 0), "alerts": alerts,
+            "firings_measured": len(lat), "alerts": alerts,
+            "tbase_redos": op.metrics.extra.get("tbase_redos", 0),
             "late_dropped": mt.num_late_records_dropped - m0["num_late_records_dropped"],
             "spilled_keys": mt.spilled_keys - m0["spilled_keys"],
             "records_to_host": mt.records_to_host - m0["records_to_host"],
@@ -482,8 +482,8 @@ def config6(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 1_000_000
             "p50_alert_latency_ms": statistics.median(lat) if lat else None,
             "p99_alert_latency_ms": (sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))]
                                      if lat else None),
-            "firings_measured": len(lat), "latency_fire": latency_fire,
-            "latency_fire_steps": op.metrics.extra.get("latency_fires", 0), "alerts": alerts,
+            "firings_measured": len(lat),
+            "alerts": alerts,
             "keys": keys, "dim": dim, "events_per_step": batch, "mode": "mfma" if mfma else "valu",
             "key_distribution": f"zipf({zipf:g})" if zipf > 0 else "uniform",
             "state_bytes": op.state_bytes(), "device": str(dev)}
