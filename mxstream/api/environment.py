@@ -126,8 +126,9 @@ class _StdoutWriter:
             sys.stdout.flush()
 
     @staticmethod
-    def raw(data: bytes) -> None:
-        """A column batch already formatted as newline-terminated lines (native formatter)."""
+    def raw(data: bytes, nlines: int | None = None) -> None:
+        """A column batch already formatted as `nlines` newline-terminated lines (native
+        formatter)."""
         if data:
             buf = getattr(sys.stdout, "buffer", None)
             if buf is None:  # a text-only stream (captured stdout)

@@ -619,8 +619,8 @@ class _ByteCounter:
         self.lines += 1
         self.bytes += len(s) + 1
 
-    def raw(self, data: bytes) -> None:
-        self.lines += data.count(b"\n")
+    def raw(self, data: bytes, nlines: int | None = None) -> None:
+        self.lines += data.count(b"\n") if nlines is None else nlines
         self.bytes += len(data)
 
 

@@ -859,6 +859,17 @@ class PrintSinkOp(Operator):
             return [self.ident + (f":{k + 1}> " if p > 1 else "> ") for k in range(nsub)]
         return [f"{k + 1}> " if p > 1 else "" for k in range(nsub)]
 
+    def _dict_names(self, d) -> list:
+        """The names of dictionary `d` by id (mirror kept across batches, extended in place)."""
+        cache = getattr(self, "_names_of", None)
+        if cache is None or cache[0] is not d:
+            cache = self._names_of = (d, [])
+        names = cache[1]
+        n = len(d)
+        if len(names) < n:
+            names.extend(d.get(i) for i in range(len(names), n))
+        return names
+
     def _print_columns(self, cb) -> None:
         """A column batch in one native call (csrc/javafmt.h: Tuple/Double/Long toString), the
         lines handed to the writer at once when it takes many (the default stdout writer)."""
@@ -869,9 +880,20 @@ class PrintSinkOp(Operator):
         if cb.n == 0:
             return
         cols, keep, names = [], [], None
+        # Dictionary ids index the dictionary's whole name list when it is not much larger than
+        # the batch (a cached mirror, extended as the dictionary grows): no per-batch unique
+        # (two sorts of the id columns) before formatting.
+        whole = None
+        if FK_STR in cb.kinds and cb.strings is not None and hasattr(cb.strings, "strings") \
+                and len(cb.strings) <= 4 * cb.n + 4096:
+            whole = self._dict_names(cb.strings)
         for c, k in zip(cb.cols, cb.kinds):
             c = np.asarray(c)[:cb.n]
-            if k == FK_STR:
+            if k == FK_STR and whole is not None:
+                names = whole
+                a = np.ascontiguousarray(c, dtype=np.int64)
+                cols.append((0, a.ctypes.data))
+            elif k == FK_STR:
                 u, inv = np.unique(c, return_inverse=True)
                 if names is not None:  # several string columns: one name list for all
                     off = len(names)
@@ -904,7 +926,7 @@ class PrintSinkOp(Operator):
 
             raw(load().java_format_bytes(cols, cb.n, names, 0 if sub is None else sub.ctypes.data,
                                          self._prefixes(nsub), as_tuple,
-                                         min(16, os.cpu_count() or 1)))
+                                         min(16, os.cpu_count() or 1)), cb.n)
             return
         lines = load().java_format_rows(cols, cb.n, names, 0 if sub is None else sub.ctypes.data,
                                         self._prefixes(nsub), as_tuple)
