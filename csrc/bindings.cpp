@@ -725,6 +725,57 @@ PYBIND11_MODULE(_mxs_native, m) {
                         P<uint8_t>(dirty_g), nsub, cap_log2, ring, p_lo, np, cutoff,
                         compact_out(o, cap), P<uint32_t>(occ));
   });
+  // print() rows formatted where the columns live (csrc/row_format.h). `d`: cols [(kind,
+  // width, ptr)], arena / id_off / id_len / n_ids of the dictionary, sub / sub0 / par, prefix
+  // bytes + offsets (npfx), as_tuple. Stage "len": lengths + flag; "write": bytes at `end`.
+  auto fmt_args = [](const py::dict& d) {
+    FmtArgs a{};
+    const auto cols = d["cols"].cast<std::vector<std::tuple<int, int, intptr_t>>>();
+    if (cols.empty() || cols.size() > (size_t)kFmtMaxCols)
+      throw std::invalid_argument("format_rows: 1..8 columns");
+    a.ncols = (int32_t)cols.size();
+    for (size_t j = 0; j < cols.size(); ++j) {
+      const int kind = std::get<0>(cols[j]), width = std::get<1>(cols[j]);
+      if (kind < 0 || kind > 2 || (width != 4 && width != 8) || (kind == 1 && width != 8))
+        throw std::invalid_argument("format_rows: column kind / width");
+      a.col[j] = FmtCol{kind, width, reinterpret_cast<const void*>(std::get<2>(cols[j]))};
+      if (kind == 0 && d["n_ids"].cast<int64_t>() > 0 && !d["arena"].cast<intptr_t>())
+        throw std::invalid_argument("format_rows: string column without a dictionary");
+    }
+    a.as_tuple = d["as_tuple"].cast<bool>() ? 1 : 0;
+    if (!a.as_tuple && a.ncols != 1) throw std::invalid_argument("format_rows: arity");
+    a.arena = P<uint8_t>(d["arena"].cast<intptr_t>());
+    a.id_off = P<int64_t>(d["id_off"].cast<intptr_t>());
+    a.id_len = P<int32_t>(d["id_len"].cast<intptr_t>());
+    a.n_ids = d["n_ids"].cast<int64_t>();
+    a.sub = P<int32_t>(d["sub"].cast<intptr_t>());
+    a.sub0 = d["sub0"].cast<int64_t>();
+    a.par = d["par"].cast<int32_t>();
+    a.npfx = d["npfx"].cast<int32_t>();
+    a.pfx = P<char>(d["pfx"].cast<intptr_t>());
+    a.pfx_off = P<int32_t>(d["pfx_off"].cast<intptr_t>());
+    return a;
+  };
+  m.def("format_rows_len", [fmt_args](bool gpu, const py::dict& d, int64_t n, intptr_t len,
+                                      intptr_t bad, intptr_t stream) {
+    const FmtArgs a = fmt_args(d);
+    if (gpu) {
+      gpu::format_rows_len(a, n, P<int64_t>(len), P<uint32_t>(bad), stream);
+    } else {
+      py::gil_scoped_release nogil;
+      cpu::format_rows_len(a, n, P<int64_t>(len), P<uint32_t>(bad));
+    }
+  });
+  m.def("format_rows_write", [fmt_args](bool gpu, const py::dict& d, int64_t n, intptr_t end,
+                                        intptr_t out, intptr_t stream) {
+    const FmtArgs a = fmt_args(d);
+    if (gpu) {
+      gpu::format_rows_write(a, n, P<int64_t>(end), P<char>(out), stream);
+    } else {
+      py::gil_scoped_release nogil;
+      cpu::format_rows_write(a, n, P<int64_t>(end), P<char>(out));
+    }
+  });
   // Tiered firing: rows -> per-key combine table (mxs_kernels.h tier_merge).
   m.def("tier_merge", [](bool gpu, intptr_t keys, intptr_t acc, intptr_t cnt, int64_t n,
                          intptr_t n_dev, int mode, int agg, intptr_t tkeys, intptr_t tacc,

@@ -413,6 +413,31 @@ static void parallel_for(int64_t n, int64_t min_per_thread, F&& body) {
   for (auto& x : th) x.join();
 }
 
+void format_rows_len(const FmtArgs& a, int64_t n, int64_t* len, uint32_t* bad) {
+  if (a.ncols < 1 || a.ncols > kFmtMaxCols) throw std::invalid_argument("format: column count");
+  std::atomic<uint32_t> flag{0};
+  parallel_for(n, 1 << 16, [&](int64_t lo, int64_t hi) {
+    bool all = true;
+    for (int64_t i = lo; i < hi; ++i) {
+      bool ok = true;
+      len[i] = fmt_row(a, i, nullptr, ok);
+      all = all && ok;
+    }
+    if (!all) flag.fetch_or(1u);
+  });
+  if (flag.load()) *bad |= 1u;
+}
+
+void format_rows_write(const FmtArgs& a, int64_t n, const int64_t* end, char* out) {
+  if (a.ncols < 1 || a.ncols > kFmtMaxCols) throw std::invalid_argument("format: column count");
+  parallel_for(n, 1 << 16, [&](int64_t lo, int64_t hi) {
+    for (int64_t i = lo; i < hi; ++i) {
+      bool ok = true;
+      fmt_row(a, i, out + (i ? end[i - 1] : 0), ok);
+    }
+  });
+}
+
 void expr_filter(const double* x, int64_t n, const ExprProg& prog, uint8_t* keep) {
   parallel_for(n, 1 << 16, [&](int64_t a, int64_t b) {
     for (int64_t i = a; i < b; ++i) {

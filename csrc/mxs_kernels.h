@@ -9,6 +9,7 @@
 #include <stdint.h>
 
 #include "mxs_common.h"
+#include "row_format.h"
 
 namespace mxs {
 
@@ -159,6 +160,11 @@ struct IngestOut;
 struct DictState;
 
 namespace gpu {
+// print() rows in Java text (csrc/row_format.h): lengths (+ a flag for rows the device cannot
+// format), then, after an inclusive scan of the lengths into `end`, the bytes.
+void format_rows_len(const FmtArgs& a, int64_t n, int64_t* len, uint32_t* bad, intptr_t stream);
+void format_rows_write(const FmtArgs& a, int64_t n, const int64_t* end, char* out,
+                       intptr_t stream);
 int device_count();
 int set_spin_schedule();
 // Async device->host copy on `stream` (hipMemcpyAsync); returns the hipError_t code.
@@ -377,6 +383,8 @@ void tier_merge(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt, 
 
 // ---- CPU twins (kernels_cpu.cpp) ------------------------------------------------------------
 namespace cpu {
+void format_rows_len(const FmtArgs& a, int64_t n, int64_t* len, uint32_t* bad);
+void format_rows_write(const FmtArgs& a, int64_t n, const int64_t* end, char* out);
 void set_threads(int n);  // worker threads of the parallel CPU twins (expr_filter, ...)
 int get_threads();
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,

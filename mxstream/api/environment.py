@@ -132,7 +132,7 @@ class _StdoutWriter:
         if data:
             buf = getattr(sys.stdout, "buffer", None)
             if buf is None:  # a text-only stream (captured stdout)
-                sys.stdout.write(data.decode())
+                sys.stdout.write(bytes(data).decode())
                 sys.stdout.flush()
                 return
             sys.stdout.flush()

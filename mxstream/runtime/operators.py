@@ -826,6 +826,11 @@ class SinkOp(Operator):
             self.fn.close()
 
 
+# Device column batches are printed by the device row formatter (ops/rowfmt.py);
+# MXS_DEVICE_FORMAT=0 formats them on the host (A/B).
+_DEVICE_FORMAT = __import__("os").environ.get("MXS_DEVICE_FORMAT", "1") != "0"
+
+
 class PrintSinkOp(Operator):
     """PrintSinkFunction: '{subtask+1}> ' + toString when parallelism > 1."""
 
@@ -876,6 +881,28 @@ class PrintSinkOp(Operator):
         from ..ops.native import load
         from ..ops.text import FK_DOUBLE, FK_INT, FK_LONG, FK_STR
 
+        if hasattr(cb, "host") and cb.n and _DEVICE_FORMAT:
+            # device batch: formatted where its columns live, one copy of the finished bytes
+            if getattr(self, "_rowfmt", None) is None:
+                from ..ops.rowfmt import RowFormatter
+
+                self._rowfmt = RowFormatter()
+            p = self.parallelism or self.ctx.parallelism
+            mv = self._rowfmt.format(cb, self._prefixes(max(1, p)),
+                                     not getattr(cb, "scalar", False))
+            if mv is not None:
+                raw = getattr(self.writer, "raw", None)
+                if raw is not None:
+                    raw(mv, cb.n)
+                    return
+                lines = bytes(mv).decode().split("\n")[:-1]
+                many = getattr(self.writer, "many", None)
+                if many is not None:
+                    many(lines)
+                else:
+                    for ln in lines:
+                        self.writer(ln)
+                return
         cb = cb.host() if hasattr(cb, "host") else cb
         if cb.n == 0:
             return
