@@ -2,10 +2,13 @@
 python scripts/cprofile_config.py <out.txt> <bench_configs args...>"""
 import cProfile
 import io
+import os
 import pstats
 import sys
 
-from mxstream.models import bench_configs
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from mxstream.models import bench_configs  # noqa: E402
 
 out = sys.argv[1]
 prof = cProfile.Profile()
