@@ -35,6 +35,11 @@ class ExecutionConfig:
     # batch i overlaps the GPU's parse of batch i + 1). Applied only where a pass's delay cannot
     # be observed (planner._defer_safe); MXS_INGEST_DEFER=0 turns it off.
     ingest_defer: bool = field(default_factory=lambda: os.environ.get("MXS_INGEST_DEFER", "1") != "0")
+    # Native keyed windows over dictionary ids: dense id-addressed HBM state up to this many
+    # ids; a dictionary that outgrows it moves the state to hashed keys with the host-DRAM tier
+    # (cold keys leave HBM). MXS_WINDOW_DENSE_MAX_KEYS.
+    window_dense_max_keys: int = field(default_factory=lambda: int(
+        os.environ.get("MXS_WINDOW_DENSE_MAX_KEYS", str(1 << 27))))
     global_job_parameters: dict = field(default_factory=dict)
     # "<operator name>:<records>[:<attempts>]" (tests / chaos runs); default from MXS_FAULT.
     fault_injection: str | None = field(default_factory=lambda: os.environ.get("MXS_FAULT"))

@@ -560,6 +560,7 @@ def _install_native(env, t, ws, spec, key_pos, val_pos, kind, result, ok_arities
                  fallback_factory=fallback, result_builder=builder, ok_arities=ok_arities)
         op.device_input = device_input
         op.scalar_result = result == "value"
+        op.dense_budget = int(env.config.window_dense_max_keys)
         return op
 
     t.factory = factory

@@ -202,18 +202,30 @@ class NativeWindowOp(_ColumnInput, Operator):
         return jh if jh is not None else torch.zeros(1, dtype=torch.int32,
                                                      device=torch.device(self.device))
 
+    dense_budget = 1 << 27  # planner: ExecutionConfig.window_dense_max_keys
+    _spill_state = False    # hashed keys + host-DRAM tier (a dictionary beyond dense_budget)
+
     def _ensure_capacity(self) -> None:
         """Dense state covers dictionary ids < max_keys: a growing dictionary regrows the state
-        (snapshot -> larger operator -> restore). At G > 1 every rank sees the same dictionary
-        size, so every rank regrows in the same pass (the restore is collective)."""
+        (snapshot -> larger operator -> restore). Beyond `dense_budget` ids the state moves to
+        hashed keys of that HBM size with the host-DRAM tier: keys whose data is older than a
+        window leave HBM (runtime/window_spill.py) instead of every id holding a slot. At G > 1
+        every rank sees the same dictionary size, so every rank switches in the same pass (the
+        restore is collective)."""
         if not (self.str_keys and self.op is not None and getattr(self.op, "dense_bits", 0)):
             return
         need = len(self.dict)
         if need <= (1 << self.op.dense_bits):
             return
         es = self.op.snapshot_state()
-        self.max_keys = 1 << max(need - 1, 1).bit_length()
-        self._build(1.0 if self.is_float else 1, dense=True)
+        budget = max(1024, int(self.dense_budget))
+        if need > budget:
+            self.max_keys = 1 << max(budget - 1, 1).bit_length()
+            self._spill_state = True
+            self._build(1.0 if self.is_float else 1, dense=False)
+        else:
+            self.max_keys = 1 << max(need - 1, 1).bit_length()
+            self._build(1.0 if self.is_float else 1, dense=True)
         self.op.restore_state(es.columns, es.meta)
 
     def _local_columns(self, data: list):
@@ -281,7 +293,7 @@ class NativeWindowOp(_ColumnInput, Operator):
             # grows): a firing sweeps every slot of its panes, so a 2^16-slot table for a
             # thousand channels would cost 64x the sweep (5 min / 5 s windows: 60 panes each).
             self.max_keys = max(2048, 1 << max(1, 2 * max(1, len(self.dict))).bit_length())
-        cap_log2 = 12 if self.max_keys > 100_000 else 9
+        cap_log2 = 12 if self.max_keys > 100_000 else (6 if self._spill_state else 9)
         comm = getattr(self, "comm", None)
         multi = comm is not None and comm.world > 1
         self.op = KeyedWindowOperator(
@@ -289,9 +301,9 @@ class NativeWindowOp(_ColumnInput, Operator):
             agg=agg, device=dev, max_keys=self.max_keys,
             parallelism=self.ctx.parallelism if multi else 1, comm=comm if multi else None,
             max_parallelism=self.ctx.max_parallelism if multi else 128,
-            hash_mode=1 if (multi and dense) else 0,
-            jhash_table=self._jhash() if (multi and dense) else None,
-            exchange="partials" if multi else "auto",
+            hash_mode=1 if (multi and self.str_keys) else 0,
+            jhash_table=self._jhash() if (multi and self.str_keys) else None,
+            exchange="partials" if multi else "auto", spill=self._spill_state,
             batch_capacity=max(1024, self.ctx.parallelism), cap_log2=cap_log2,
             time_mode="event" if event else "processing", external_watermark=True,
             side_output_late=self.late_tag is not None, clock=self.ctx.clock,

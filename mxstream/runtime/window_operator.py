@@ -1231,10 +1231,18 @@ class KeyedWindowOperator:
     def _maybe_spill(self) -> None:
         self._verify_combine()  # the occupancy must include a redone combined step's inserts
         cap = 1 << self.cap_log2
-        if int(self.occ.max()) <= self.spill_load * cap or self.max_seen_pane is None:
+        occ = int(self.occ.max())
+        # Compact above `spill_load`, or earlier when the fullest sub-table's growth since the
+        # last check (twice over: checks are spill_check_steps apart) would fill it first --
+        # small sub-tables (a few dozen slots) have little headroom above the load threshold.
+        prev, self._occ_prev = getattr(self, "_occ_prev", None), occ
+        growth = max(0, occ - prev) if prev is not None else 0
+        if self.max_seen_pane is None or (occ <= self.spill_load * cap
+                                          and occ + 2 * growth <= 0.95 * cap):
             return
         keep = self.spill_keep_panes or self.panes_per_window
         self.compact_state(self.max_seen_pane - keep, wait=False)
+        self._occ_prev = None  # the compacted occupancy is not read back (asynchronous)
 
     def compact_state(self, cutoff_pane: int | None = None, wait: bool = True) -> dict:
         """Table maintenance at a step boundary: drop keys without live data and (with the spill
@@ -1736,6 +1744,7 @@ class KeyedWindowOperator:
         if only_dirty:
             self.dirty_m[so:so + self.nslots_o].zero_()
         n = self._fired_count()
+        self._maybe_compact_merge()
         self.metrics.num_fires += 1
         if n == 0:
             return None
@@ -1745,6 +1754,39 @@ class KeyedWindowOperator:
                               self._pool)
         return FireResult(s, s + self.size, host[0].view(np.uint64), host[1], host[2], host[3],
                           refire=only_dirty)
+
+    def _maybe_compact_merge(self) -> None:
+        """The owner's merge table keeps a key while any merge slice (a fired window inside its
+        allowed lateness) holds a value for it. Keys whose slices were all recycled are dead;
+        with a drifting key space they would fill the table, so every 16 partial fires the
+        fullest sub-table is checked (the fire has just synchronised) and, above 0.6 load, the
+        live keys are rehashed into a cleared table with their slices."""
+        self._mfires = getattr(self, "_mfires", 0) + 1
+        if self._mfires % 16 or int(self.occ_m.max()) <= 0.6 * (1 << self.cap_log2_o):
+            return
+        R, N = self.ring_m, self.nslots_o
+        cnt = self.cnt_m.view(R, N)
+        live = torch.nonzero(((cnt != 0).any(0)) & (self.keys_m >= 0)).flatten()
+        keys = self.keys_m[live]
+        acc = self.acc_m.view(R, N)[:, live]
+        cnt_l = cnt[:, live]
+        dirty = self.dirty_m.view(R, N)[:, live]
+        self.keys_m.fill_(-1)
+        self.acc_m.zero_()
+        self.cnt_m.zero_()
+        self.dirty_m.zero_()
+        self.occ_m.zero_()
+        if live.numel():
+            slots = K.table_insert(keys.contiguous(), self.keys_m, nsub_log2=self.nsub_o_log2,
+                                   cap_log2=self.cap_log2_o)
+            if bool((slots < 0).any()):
+                raise RuntimeError("merge table compaction: live keys do not fit")
+            self.acc_m.view(R, N)[:, slots] = acc
+            self.cnt_m.view(R, N)[:, slots] = cnt_l
+            self.dirty_m.view(R, N)[:, slots] = dirty
+            self.occ_m.copy_(torch.bincount(slots >> self.cap_log2_o, minlength=self.nsub_o)
+                             .to(torch.int32))
+        self.metrics.extra["merge_compactions"] = self.metrics.extra.get("merge_compactions", 0) + 1
 
     def _fired_count(self) -> int:
         """Rows the last fire produced; raises if any aggregation found its table full (a key

@@ -228,3 +228,68 @@ def test_reference_job_gloo_processes(name):
     assert Counter(got) == Counter(ref)
     for _, _, seen, _ in res:
         assert seen["recs"] == 0 and seen["device"] and all(seen["device"])
+
+
+def _drift_lines(n=60000, channels=30000):
+    """Timed flow lines over a channel dictionary far larger than the dense budget below; each
+    channel is active for half a second, then idles (its windows stay live for the allowed
+    lateness, so idle keys are moved to the host tier, not dropped)."""
+    out = []
+    for i in range(n):
+        c = (i // 2) % channels
+        t = i // 4
+        out.append(f"2019-08-28T{10 + t // 3600:02d}:{(t // 60) % 60:02d}:{t % 60:02d} "
+                   f"www.ch{c}.com {100 + i % 97}")
+    return out
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_dictionary_beyond_dense_budget_moves_to_hashed_tier(world, monkeypatch):
+    """A channel dictionary that outgrows the dense id budget switches the window state to hashed
+    keys with the host-DRAM tier: idle keys leave HBM, the output equals the all-dense run, at
+    G = 1 and G = 2."""
+    from mxstream.api.time import TimeCharacteristic
+    from mxstream.parallel.comm import run_loopback
+    from mxstream.runtime import native_ops as N
+
+    lines = _drift_lines()
+
+    def run(budget, comm=None):
+        out = []
+        env = StreamExecutionEnvironment(4, clock=ManualClock(0)).set_output(out.append)
+        env.config.native = "auto"
+        env.config.text_ingest = "device"
+        env.config.window_dense_max_keys = budget
+        env._comm = comm
+        env.set_stream_time_characteristic(TimeCharacteristic.EventTime)
+        (env.from_collection(lines, batch_size=500)
+            .assign_timestamps_and_watermarks(C.EventTimeExtractor())
+            .map(C.ParseTimedFlow())
+            .key_by(1)
+            .time_window(Time.minutes(1))
+            .allowed_lateness(Time.minutes(10))
+            .reduce(lambda a, b: Tuple3(a.f0, a.f1, a.f2 + b.f2))
+            .map(lambda t: Tuple2(t.f1, t.f2))
+            .print())
+        env.execute("drift")
+        return out
+
+    ref = run(1 << 27)
+    assert len(ref) > 1000
+    switched = []
+    orig = N.NativeWindowOp._ensure_capacity
+
+    def spy(self):
+        orig(self)
+        if self._spill_state:
+            switched.append(self)
+
+    monkeypatch.setattr(N.NativeWindowOp, "_ensure_capacity", spy)
+    if world == 1:
+        got = run(4096)
+    else:
+        got = [l for out in run_loopback(world, lambda comm: run(4096, comm)) for l in out]
+    ops = set(switched)
+    assert ops and all(o.op.host_tier is not None and not o.op.dense_bits for o in ops)
+    assert sum(o.op.metrics.extra.get("spilled_keys", 0) for o in ops) > 0  # keys left HBM
+    assert Counter(got) == Counter(ref)

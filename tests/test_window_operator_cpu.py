@@ -694,3 +694,26 @@ def test_spill_tier_multirank_matches_unbounded_table(world, exchange):
     got = sorted(r for rows, _ in res for r in rows)
     assert sum(op.metrics.extra.get("spilled_keys", 0) for _, op in res) > 0
     assert got == ref
+
+
+def test_partials_merge_table_drops_dead_keys():
+    """Local-global owners keep a key in the merge table while a fired window inside its allowed
+    lateness holds a value for it. With drifting keys the dead ones are compacted away (the
+    table is sized for ~one window's keys here, far below the keys of the whole run) and the
+    output still equals one rank with an unbounded table."""
+    from mxstream.parallel.comm import run_loopback
+
+    batches = _drift_batches(40, 6000, seed=8)  # ~60K distinct keys over the run
+    ref, _ = _run_windows(batches, max_keys=120_000)
+    world = 2
+
+    def rank(comm):
+        mine = [(k[comm.rank::world].contiguous(), t[comm.rank::world].contiguous(),
+                 v[comm.rank::world].contiguous()) for k, t, v in batches]
+        return _run_windows(mine, max_keys=120_000, comm=comm, parallelism=world,
+                            exchange="partials", window_keys=16_000, cap_log2=7)
+
+    res = run_loopback(world, rank)
+    got = sorted(r for rows, _ in res for r in rows)
+    assert sum(op.metrics.extra.get("merge_compactions", 0) for _, op in res) > 0
+    assert got == ref
