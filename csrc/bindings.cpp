@@ -94,8 +94,8 @@ PartPlan make_part(py::dict d) {
   if (p.rec_words < 1 || p.rec_words > 3) throw std::invalid_argument("rec_words must be 1, 2 or 3");
   if (p.rec_words < 3 && !p.window_mode)
     throw std::invalid_argument("compact records are for the window path");
-  if (p.rec_words == 1 && p.nranks != 1)
-    throw std::invalid_argument("8-byte records need a single destination");
+  if (p.rec_words == 1 && p.nranks != 1 && (p.nranks << p.nsub_log2) > 512)
+    throw std::invalid_argument("8-byte records to several ranks need <= 512 buckets");
   if (p.max_parallelism <= 0 || p.nranks <= 0 || p.nsub_log2 < 0 || p.nsub_log2 > 20)
     throw std::invalid_argument("bad partition plan");
   return p;

@@ -4125,10 +4125,20 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                intptr_t stream) {
   const int nb = plan.nranks << plan.nsub_log2;
   if (plan.rec_words == 1) {
-    // Narrow 8-byte records: one destination only. Up to 512 buckets the LDS-staged compact
-    // kernel; more (e.g. 4096 dense sub-tables of a 10M-key window) the plain scatter.
-    if (plan.nranks != 1 || (uint64_t)nb * plan.bucket_cap >= (1ull << 32))
-      throw std::invalid_argument("partition: 8-byte records need one destination");
+    // Narrow 8-byte records. Up to 512 buckets the LDS-staged compact kernel; more (e.g. 4096
+    // dense sub-tables of a 10M-key window) the plain scatter (one destination). Several
+    // destinations (the records exchange): the compact kernel's general bucket path, which
+    // halves the all-to-all bytes of 16-byte records.
+    if ((uint64_t)nb * plan.bucket_cap >= (1ull << 32))
+      throw std::invalid_argument("partition: 8-byte record buffer above 2^32 records");
+    if (plan.nranks != 1) {
+      if (nb > kCMaxNb)
+        throw std::invalid_argument("partition: 8-byte records to several ranks need <= 512 buckets");
+      if (n <= 0) return;
+      dispatch_compact<false, 8>(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats,
+                                 late_idx, late_cap, stream);
+      return;
+    }
     if (n <= 0) return;
     if (nb > kCMaxNb && plan.scratch && plan.scratch_cursor && nb <= kCMaxNb * 32) {
       // Two-level: compact staged partition into 512 coarse buckets, then the split kernel.
@@ -4994,9 +5004,14 @@ static void launch_combine(const Rec* recs, const uint32_t* counts, int nbuckets
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIP_CHECK(hipFuncSetAttribute((const void*)window_combine_kernel<AGG, 2>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_CHECK(hipFuncSetAttribute((const void*)window_combine_kernel<AGG, 1>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
-  if (p.rec_words == 2)
+  if (p.rec_words == 1)
+    hipLaunchKernelGGL((window_combine_kernel<AGG, 1>), dim3(nbuckets), dim3(1024), lds, s,
+                       (const void*)recs, counts, p, out, ccap, out_counts, flags);
+  else if (p.rec_words == 2)
     hipLaunchKernelGGL((window_combine_kernel<AGG, 2>), dim3(nbuckets), dim3(1024), lds, s,
                        (const void*)recs, counts, p, out, ccap, out_counts, flags);
   else

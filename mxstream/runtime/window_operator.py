@@ -608,7 +608,13 @@ class KeyedWindowOperator:
         # record that does not fit widens the format for good (step redone).
         if narrow is None:
             narrow = compact and self.device.type == "cuda"
-        narrow = bool(narrow and compact and not self._exchanging and type(self)._narrow_ok)
+        # The records exchange takes 8-byte records too when its buckets fit the compact
+        # partition (<= 512 per rank): half the all-to-all and combiner read bytes of 16-byte
+        # records. MXS_NARROW_EXCHANGE=0 keeps 16-byte records there (A/B).
+        narrow_x = _os.environ.get("MXS_NARROW_EXCHANGE", "1") != "0"
+        narrow = bool(narrow and compact and type(self)._narrow_ok
+                      and (not self._exchanging
+                           or (narrow_x and (self._part_ranks << self.nsub_log2) <= 512)))
         # Record words: 1 = 8-byte RecN, 2 = 16-byte RecC (int32 values), 3 = 24-byte Rec.
         self.rec_w = 1 if narrow else 2 if compact else 3
         self.timer = None  # utils.metrics.StageTimer: per-stage step_ms histograms when attached

@@ -717,3 +717,25 @@ def test_partials_merge_table_drops_dead_keys():
     got = sorted(r for rows, _ in res for r in rows)
     assert sum(op.metrics.extra.get("merge_compactions", 0) for _, op in res) > 0
     assert got == ref
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("combine", [True, False])
+def test_narrow_records_exchange_equals_one_rank(world, combine):
+    """8-byte records across the records exchange (key id < 2^32, int28 value, pane offset < 15;
+    anything else widens the step's records): sender-side combiner or raw records, the output
+    equals one rank."""
+    from mxstream.parallel.comm import run_loopback
+
+    batches = _drift_batches(12, 6000, seed=3)
+    ref, _ = _run_windows(batches, max_keys=80_000)
+
+    def rank(comm):
+        mine = [(k[comm.rank::world].contiguous(), t[comm.rank::world].contiguous(),
+                 v[comm.rank::world].contiguous()) for k, t, v in batches]
+        return _run_windows(mine, max_keys=80_000, comm=comm, parallelism=world,
+                            exchange="records", compact=True, narrow=True, combine=combine)
+
+    res = run_loopback(world, rank)
+    assert all(op.rec_w == 1 for _, op in res)
+    assert sorted(r for rows, _ in res for r in rows) == ref
