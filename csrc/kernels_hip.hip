@@ -1593,19 +1593,23 @@ __global__ __launch_bounds__(1024) void window_compact_kernel(
 // moves ~#distinct (key, pane) records instead of every event (sum/min/max/count/avg are all
 // associative, so the receiver's window_agg result is unchanged).
 // ------------------------------------------------------------------------------------------
-template <int AGG, int RW>
+// PK: packed (sum, count) words for integer sums of int32 values (see kPkOne): one LDS atomic
+// per record instead of two, and no count array (the launcher checks bucket_cap < 2^16).
+template <int AGG, int RW, bool PK = false>
 __global__ __launch_bounds__(1024) void window_combine_kernel(
     const void* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
     Rec* __restrict__ out, uint32_t ccap, uint32_t* __restrict__ out_counts,
     uint32_t* __restrict__ flags) {
+  static_assert(!PK || ((AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) && RW <= 2),
+                "packed combiner: integer sum/avg of 8/16-byte records only");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int b = blockIdx.x;
   const uint32_t cap = 1u << p.cap_log2;
   const uint32_t mask = cap - 1;
   uint64_t* skeys = (uint64_t*)smem;
   uint64_t* sacc = skeys + cap;
-  uint32_t* scnt = (uint32_t*)(sacc + (size_t)p.pg * cap);
-  uint32_t* sflag = scnt + (size_t)p.pg * cap;  // [0] records written, [1] overflow
+  uint32_t* scnt = (uint32_t*)(sacc + (size_t)p.pg * cap);      // unused when PK
+  uint32_t* sflag = scnt + (PK ? 0 : (size_t)p.pg * cap);  // [0] records written, [1] overflow
   for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) skeys[i] = kEmptyKey;
   if (threadIdx.x < 2) sflag[threadIdx.x] = 0;
   uint32_t c = counts[b];
@@ -1617,8 +1621,8 @@ __global__ __launch_bounds__(1024) void window_combine_kernel(
   for (int pg0 = 0; pg0 < p.np_step; pg0 += p.pg) {
     const int npg = (p.np_step - pg0) < p.pg ? (p.np_step - pg0) : p.pg;
     for (uint32_t i = threadIdx.x; i < (uint32_t)npg * cap; i += blockDim.x) {
-      sacc[i] = (uint64_t)lds_identity<AGG>();
-      scnt[i] = 0;
+      sacc[i] = PK ? 0ull : (uint64_t)lds_identity<AGG>();
+      if (!PK) scnt[i] = 0;
     }
     __syncthreads();
     const int64_t q0 = p.p_lo + pg0;
@@ -1645,8 +1649,12 @@ __global__ __launch_bounds__(1024) void window_combine_kernel(
           continue;
         }
         const uint32_t li = (uint32_t)q * cap + s;
-        lds_accumulate<AGG>(&sacc[li], r.val);
-        atomicAdd(&scnt[li], 1u);
+        if (PK) {
+          atomicAdd((unsigned long long*)&sacc[li], (unsigned long long)(r.val + kPkOne));
+        } else {
+          lds_accumulate<AGG>(&sacc[li], r.val);
+          atomicAdd(&scnt[li], 1u);
+        }
       }
     }
     __syncthreads();
@@ -1654,7 +1662,7 @@ __global__ __launch_bounds__(1024) void window_combine_kernel(
     // wave).
     for (uint32_t i0 = 0; i0 < (uint32_t)npg * cap; i0 += blockDim.x) {
       const uint32_t i = i0 + threadIdx.x;
-      const bool have = i < (uint32_t)npg * cap && scnt[i] != 0;
+      const bool have = i < (uint32_t)npg * cap && (PK ? sacc[i] != 0ull : scnt[i] != 0);
       const unsigned long long m = __ballot(have);
       uint32_t wb = 0;
       if (lane_id() == 0 && m) wb = atomicAdd(&sflag[0], (uint32_t)__popcll(m));
@@ -1664,9 +1672,9 @@ __global__ __launch_bounds__(1024) void window_combine_kernel(
         if (pos < ccap) {
           Rec o;
           o.key = skeys[i & mask];
-          o.val = lds_export<AGG>(sacc[i]);
+          o.val = PK ? (uint64_t)pk_sum(sacc[i]) : lds_export<AGG>(sacc[i]);
           o.t = (uint32_t)(q0 + (int64_t)(i >> p.cap_log2));
-          o.aux = scnt[i];
+          o.aux = PK ? pk_cnt(sacc[i]) : scnt[i];
           dst[pos] = o;
         } else {
           ovf = true;
@@ -4998,6 +5006,30 @@ template <int AGG>
 static void launch_combine(const Rec* recs, const uint32_t* counts, int nbuckets,
                            const AggPlan& p, Rec* out, uint32_t ccap, uint32_t* out_counts,
                            uint32_t* flags, size_t lds, hipStream_t s) {
+  if constexpr (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) {
+    // packed accumulators: int32 values (8/16-byte records), < 2^16 records per bucket
+    AggPlan q = p;
+    q.combined = 0;
+    if (p.rec_words <= 2 && agg_pack_ok(q)) {
+      static bool attr_pk = false;
+      if (!attr_pk) {
+        HIP_CHECK(hipFuncSetAttribute((const void*)window_combine_kernel<AGG, 1, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        HIP_CHECK(hipFuncSetAttribute((const void*)window_combine_kernel<AGG, 2, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr_pk = true;
+      }
+      const size_t cap = (size_t)1 << p.cap_log2;
+      const size_t lds_pk = cap * 8 + (size_t)p.pg * cap * 8 + 16;
+      if (p.rec_words == 1)
+        hipLaunchKernelGGL((window_combine_kernel<AGG, 1, true>), dim3(nbuckets), dim3(1024),
+                           lds_pk, s, (const void*)recs, counts, p, out, ccap, out_counts, flags);
+      else
+        hipLaunchKernelGGL((window_combine_kernel<AGG, 2, true>), dim3(nbuckets), dim3(1024),
+                           lds_pk, s, (const void*)recs, counts, p, out, ccap, out_counts, flags);
+      return;
+    }
+  }
   static bool attr = false;
   if (!attr) {
     HIP_CHECK(hipFuncSetAttribute((const void*)window_combine_kernel<AGG, 3>,
