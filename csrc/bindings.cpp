@@ -675,6 +675,11 @@ PYBIND11_MODULE(_mxs_native, m) {
       if (e != 0) throw std::runtime_error("hipMemcpyAsync D2H failed: " + std::to_string(e));
     }
   });
+  m.def("gpu_h2d_kernel", [](intptr_t dst, intptr_t src, int64_t bytes, intptr_t stream,
+                             int max_blocks) {
+    return gpu::h2d_kernel((void*)dst, (const void*)src, bytes, stream, max_blocks);
+  }, py::arg("dst"), py::arg("src"), py::arg("bytes"), py::arg("stream"),
+     py::arg("max_blocks") = 1024);
   // Kernel variant of gpu_d2h_many (16-byte granules); returns the hipError_t code (0 = ok).
   m.def("gpu_d2h_kernel", [](intptr_t dst, const std::vector<std::tuple<intptr_t, int64_t, int64_t>>& copies,
                              intptr_t stream) {

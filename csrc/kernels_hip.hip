@@ -3921,6 +3921,28 @@ int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream,
   return (int)hipGetLastError();
 }
 
+int h2d_kernel(void* dst_dev, const void* src_host, int64_t bytes, intptr_t stream,
+               int max_blocks) {
+  // The copy kernel reading a mapped pinned host buffer over PCIe (every CU's loads in flight
+  // at once) instead of the SDMA engine: the text batches of the file/socket sources.
+  void* sd = nullptr;
+  hipError_t e = hipHostGetDevicePointer(&sd, const_cast<void*>(src_host), 0);
+  if (e != hipSuccess || !sd) return (int)(e != hipSuccess ? e : hipErrorInvalidValue);
+  if (bytes <= 0) return 0;
+  if ((bytes & 15) || ((uintptr_t)sd & 15) || ((uintptr_t)dst_dev & 15))
+    return (int)hipErrorInvalidValue;  // 16-byte granules only (the caller pads)
+  D2HBatch b{};
+  b.n = 1;
+  b.c[0].src = sd;
+  b.c[0].dst_off = 0;
+  b.c[0].bytes = bytes;
+  b.c[0].esz = 0;
+  const int grid = grid_for(bytes / 16, 256 * 4, max_blocks < 1 ? 1 : max_blocks > 2048 ? 2048 : max_blocks);
+  hipLaunchKernelGGL(d2h_copy_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                     (unsigned char*)dst_dev, b);
+  return (int)hipGetLastError();
+}
+
 int device_count() {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

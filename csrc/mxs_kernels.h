@@ -165,6 +165,10 @@ namespace gpu {
 void format_rows_len(const FmtArgs& a, int64_t n, int64_t* len, uint32_t* bad, intptr_t stream);
 void format_rows_write(const FmtArgs& a, int64_t n, const int64_t* end, char* out,
                        intptr_t stream);
+// Host-to-device copy by the copy kernel reading a pinned (mapped) host buffer; 16-byte
+// granules. Returns the hipError_t code (0 = ok).
+int h2d_kernel(void* dst_dev, const void* src_host, int64_t bytes, intptr_t stream,
+               int max_blocks = 1024);
 int device_count();
 int set_spin_schedule();
 // Async device->host copy on `stream` (hipMemcpyAsync); returns the hipError_t code.

@@ -177,6 +177,18 @@ def _aligned_range(path: str, rank: int, world: int) -> tuple[int, int]:
 
 _PINNED_SLOTS: dict = {}  # (bytes, pinned) -> free page-locked slot tensors, reused across jobs
 
+# Text batch upload: "1" = the copy kernel reading the pinned slot (csrc gpu::h2d_kernel, at
+# most MXS_H2D_BLOCKS workgroups so the parse of the previous batch keeps the other CUs),
+# "0" = the SDMA engine (hipMemcpyAsync).
+_H2D_KERNEL = __import__("os").environ.get("MXS_H2D_KERNEL", "0") == "1"
+_H2D_BLOCKS = int(__import__("os").environ.get("MXS_H2D_BLOCKS", "512"))
+
+
+def _native():
+    from ..ops.native import load
+
+    return load()
+
 
 def _take_slots(nbytes: int, count: int, pin: bool) -> list:
     import torch
@@ -301,7 +313,18 @@ class TextFileSource(Source):
             import torch
 
             with torch.cuda.stream(self._cstream):
-                dev = tb.data.to(self._dev, non_blocking=True)
+                r16 = (int(nbytes) + 15) & ~15
+                if _H2D_KERNEL and r16 <= self._slots[slot].numel():
+                    # the copy kernel reads the pinned slot over PCIe (16-byte granules: the
+                    # slot's bytes past nbytes ride along and are never parsed)
+                    buf = torch.empty(max(r16, 16), dtype=torch.uint8, device=self._dev)
+                    rc = _native().gpu_h2d_kernel(buf.data_ptr(), self._slots[slot].data_ptr(),
+                                                  r16, self._cstream.cuda_stream, _H2D_BLOCKS)
+                    if rc:
+                        raise RuntimeError(f"text upload: hip error {rc}")
+                    dev = buf[:nbytes]
+                else:
+                    dev = tb.data.to(self._dev, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self._cstream)
             tok.uploaded(ev)

@@ -475,6 +475,24 @@ def test_segment_median_select_gpu_matches_cpu(gpu_device):
     assert torch.equal(g, c) and np.allclose(c.numpy(), ref, rtol=0, atol=0)
 
 
+def test_h2d_kernel_copies_pinned_bytes(gpu_device):
+    """gpu_h2d_kernel: the copy kernel reads a pinned host buffer over PCIe (16-byte granules);
+    misaligned sizes are refused, not truncated."""
+    from mxstream.ops.native import load
+
+    m = load()
+    st = torch.cuda.current_stream(gpu_device).cuda_stream
+    for nb in (16, 4096, (3 << 20) + 48):
+        src = torch.randint(0, 256, (nb,), dtype=torch.uint8).pin_memory()
+        dst = torch.zeros(nb, dtype=torch.uint8, device=gpu_device)
+        assert m.gpu_h2d_kernel(dst.data_ptr(), src.data_ptr(), nb, st, 64) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(dst.cpu(), src)
+    src = torch.zeros(64, dtype=torch.uint8).pin_memory()
+    dst = torch.zeros(64, dtype=torch.uint8, device=gpu_device)
+    assert m.gpu_h2d_kernel(dst.data_ptr(), src.data_ptr(), 40, st, 64) != 0
+
+
 @pytest.mark.parametrize("emit", ["full", "key_value"])
 def test_batched_fire_gpu_equals_cpu(gpu_device, emit):
     """Watermark jumps over many slides fire a group of windows in one window_fire_many call
