@@ -275,7 +275,8 @@ class SessionCore {
           }
         }
         unsigned hw = std::thread::hardware_concurrency();
-        const size_t nth = std::min<size_t>({scan.size(), hw ? hw : 1, 16, rows / 65536 + 1});
+        const size_t nth = std::min<size_t>({scan.size(), hw ? hw : 1, (size_t)max_threads_,
+                                             rows / 65536 + 1});
         if (nth > 1) {
           // Two passes, each one chunk per task: count the kept rows, then write them at their
           // offsets in `cold` (growing per-task vectors cost more in page faults and unmaps
@@ -551,6 +552,11 @@ class SessionCore {
     const size_t cap = (size_t)1 << cap_log2;
     if (num_keys() * 2 > cap) throw std::invalid_argument("spill set too small");
     std::fill(d, d + cap, (int64_t)kEmptyKey);
+    spill_set_add(cap_log2, d);
+  }
+  // This store's keys added to a spill set `d` that may already hold other keys (shards).
+  void spill_set_add(int cap_log2, int64_t* d) const {
+    const size_t cap = (size_t)1 << cap_log2;
     const uint32_t mask = (uint32_t)(cap - 1);
     auto put = [&](uint64_t key) {
       uint32_t s = (uint32_t)(mix64(key) >> 32) & mask;
@@ -726,6 +732,9 @@ class SessionCore {
   }
 
   int64_t gap_, late_;
+ public:
+  int max_threads_ = 16;  // extract's chunk-scan threads (1 inside a sharded store)
+ private:
   int agg_;
   // A key's live sessions plus the due time of its one valid heap entry (schedule() pushes only
   // when the due time changes; fire() skips popped entries whose time is not the key's due).

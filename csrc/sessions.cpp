@@ -30,7 +30,7 @@
 #include <algorithm>
 #include <climits>
 
-#include "session_store.h"
+#include "session_shards.h"
 
 namespace py = pybind11;
 
@@ -61,20 +61,23 @@ void same_len(int64_t n, std::initializer_list<int64_t> sizes) {
 }
 
 // NumPy adapter of the store core (csrc/session_store.h).
-class SessionStore : public sess::SessionCore {
+class SessionStore {
  public:
-  using SessionCore::SessionCore;
+  // shards > 1: key shards worked in parallel by a persistent pool (csrc/session_shards.h)
+  SessionStore(int64_t gap, int64_t lateness, int agg, int shards = 1)
+      : c_(gap, lateness, agg, shards) {}
+  int shards() const { return c_.shards(); }
 
   // Fold a batch (keys, ts, vals) with the current watermark `wm`; returns late-dropped count.
   int64_t process_np(const I64Array& keys, const I64Array& ts, const I64Array& vals, int64_t wm) {
     same_len(keys.size(), {ts.size(), vals.size()});
-    return process(keys.data(), ts.data(), vals.data(), keys.size(), wm);
+    return c_.process(keys.data(), ts.data(), vals.data(), keys.size(), wm);
   }
   // Merge pre-built runs (GPU overflow path): each is a candidate session.
   int64_t merge_runs_np(const I64Array& keys, const I64Array& starts, const I64Array& ends,
                         const I64Array& accs, const I64Array& cnts, int64_t wm) {
     same_len(keys.size(), {starts.size(), ends.size(), accs.size(), cnts.size()});
-    return merge_runs(keys.data(), starts.data(), ends.data(), accs.data(), cnts.data(),
+    return c_.merge_runs(keys.data(), starts.data(), ends.data(), accs.data(), cnts.data(),
                       keys.size(), wm);
   }
   // Arguments by const reference: the call runs without the GIL, so no Python object may be
@@ -82,12 +85,12 @@ class SessionStore : public sess::SessionCore {
   void insert_np(const I64Array& keys, const I64Array& starts, const I64Array& ends,
                  const I64Array& accs, const I64Array& cnts, const I64Array& flags, bool cold) {
     same_len(keys.size(), {starts.size(), ends.size(), accs.size(), cnts.size(), flags.size()});
-    insert(keys.data(), starts.data(), ends.data(), accs.data(), cnts.data(), flags.data(),
+    c_.insert(keys.data(), starts.data(), ends.data(), accs.data(), cnts.data(), flags.data(),
            keys.size(), cold);
   }
   py::dict extract_np(const I64Array& keys, int64_t wm, int64_t max_sess) {
     std::vector<int64_t> moved;
-    py::dict d = columns_dict(extract(keys.data(), keys.size(), wm, max_sess, &moved));
+    py::dict d = columns_dict(c_.extract(keys.data(), keys.size(), wm, max_sess, &moved));
     d["moved"] = to_np(moved);
     return d;
   }
@@ -99,7 +102,7 @@ class SessionStore : public sess::SessionCore {
     std::vector<int64_t> moved, ukey, rec, last;
     {
       py::gil_scoped_release nogil;
-      const sess::Columns c = extract(keys.data(), keys.size(), wm, max_sess, &moved);
+      const sess::Columns c = c_.extract(keys.data(), keys.size(), wm, max_sess, &moved);
       const size_t n = c.key.size();
       int64_t pos = 0;
       for (size_t i = 0; i < n; ++i) {
@@ -130,9 +133,9 @@ class SessionStore : public sess::SessionCore {
   // keys that left the store ("released").
   py::dict fire_np(int64_t wm, std::vector<int32_t> map_code, std::vector<double> map_consts,
                    std::vector<int32_t> f_code, std::vector<double> f_consts, bool expire) {
-    FireOut o;
-    fire(wm, prog(map_code.data(), map_code.size(), map_consts.data(), map_consts.size()),
-         prog(f_code.data(), f_code.size(), f_consts.data(), f_consts.size()), o, expire);
+    sess::SessionCore::FireOut o;
+    c_.fire(wm, sess::SessionCore::prog(map_code.data(), map_code.size(), map_consts.data(), map_consts.size()),
+         sess::SessionCore::prog(f_code.data(), f_code.size(), f_consts.data(), f_consts.size()), o, expire);
     py::dict d;
     d["keys"] = to_np(o.okey);
     d["start"] = to_np(o.ostart);
@@ -149,17 +152,25 @@ class SessionStore : public sess::SessionCore {
     std::vector<int64_t> rel;
     {
       py::gil_scoped_release nogil;
-      expire_cold(wm, rel);
+      c_.expire_cold(wm, rel);
     }
     return to_np(rel);
   }
   py::array_t<int64_t> spill_set_np(int cap_log2) const {
     py::array_t<int64_t> out((py::ssize_t)1 << cap_log2);
-    spill_set(cap_log2, out.mutable_data());
+    c_.spill_set(cap_log2, out.mutable_data());
     return out;
   }
-  py::array_t<int64_t> key_list_np() const { return to_np(key_list()); }
-  py::dict snapshot_np() const { return columns_dict(snapshot()); }
+  py::array_t<int64_t> key_list_np() const { return to_np(c_.key_list()); }
+  py::dict snapshot_np() const { return columns_dict(c_.snapshot()); }
+  bool contains(uint64_t key) const { return c_.contains(key); }
+  size_t num_keys() const { return c_.num_keys(); }
+  size_t num_sessions() const { return c_.num_sessions(); }
+  size_t num_cold_rows() const { return c_.num_cold_rows(); }
+  size_t bytes() const { return c_.bytes(); }
+
+ private:
+  sess::ShardedCore c_;
 };
 
 }  // namespace
@@ -168,7 +179,9 @@ class SessionStore : public sess::SessionCore {
 void bind_sessions(py::module_& m) {
   using mxs::SessionStore;
   py::class_<SessionStore>(m, "SessionStore")
-      .def(py::init<int64_t, int64_t, int>(), py::arg("gap"), py::arg("lateness"), py::arg("agg"))
+      .def(py::init<int64_t, int64_t, int, int>(), py::arg("gap"), py::arg("lateness"),
+           py::arg("agg"), py::arg("shards") = 1)
+      .def_property_readonly("shards", &SessionStore::shards)
       .def("process", &SessionStore::process_np)
       // GIL released: the operator inserts spilled rows from a worker thread while the main
       // thread keeps launching the next step's kernels (the store is not touched concurrently).

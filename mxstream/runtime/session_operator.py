@@ -58,6 +58,10 @@ _SESSION_SORT = __import__("os").environ.get("MXS_SESSION_SORT", "lds")
 # The fused lookup-sort writes interleaved (key, value) pairs (one 16-byte store per record)
 # instead of two scattered 8-byte stores; "0" keeps the two arrays.
 _SESSION_PAIR = int(__import__("os").environ.get("MXS_SESSION_PAIR", "1"))
+# Key shards of the host session store, worked in parallel by a persistent pool
+# (csrc/session_shards.h); MXS_SESSION_SHARDS=1: one store.
+_STORE_SHARDS = int(__import__("os").environ.get(
+    "MXS_SESSION_SHARDS", str(min(16, max(1, __import__("os").cpu_count() or 1)))))
 
 
 def _next_pow2(x: int) -> int:
@@ -138,7 +142,7 @@ class KeyedSessionOperator:
         self.late_side: list = []  # late records are dropped (no side output on this path)
         self.phase_s: dict[str, float] = defaultdict(float)  # host wall time per phase
         self.native = load()
-        self.store = self.native.SessionStore(self.gap, self.lateness, agg)
+        self.store = self.native.SessionStore(self.gap, self.lateness, agg, _STORE_SHARDS)
         self.wm = I64_MIN
         self.gpu = self.device.type == "cuda"
 
@@ -1065,7 +1069,7 @@ class KeyedSessionOperator:
         self.wm = meta["wm"]
         for k, v in meta.get("metrics", {}).items():
             setattr(self.metrics, k, v)
-        self.store = self.native.SessionStore(self.gap, self.lateness, self.agg)
+        self.store = self.native.SessionStore(self.gap, self.lateness, self.agg, _STORE_SHARDS)
         if self.gpu:
             self._occ_exact = True  # slots written below: the next check scans the table
         cols = [np.ascontiguousarray(rows[k], dtype=np.int64)

@@ -472,6 +472,10 @@ class KeyedWindowOperator:
             if bits > 32:
                 raise ValueError("dense_keys: ids must fit 32 bits")
             cl = min(12, bits) if cap_log2 is None else min(int(cap_log2), bits)
+            # Small dense key spaces (a thousand channels) still get ~256 sub-tables: one
+            # aggregation workgroup each, instead of 4 workgroups over the whole batch (>= 32
+            # slots: the touched-slot bitmap of late data needs a word per 32).
+            cl = min(cl, max(5, bits - 8))
             self.nsub, self.cap_log2 = 1 << (bits - cl), cl
             self.dense_bits = bits
             self.dense_mul = (0x9E3779B1 & ((1 << bits) - 1)) | 1

@@ -246,6 +246,47 @@ def test_store_extract_parallel_chunk_scan():
     assert again["key"].size == 0
 
 
+@pytest.mark.parametrize("shards", [2, 8])
+def test_sharded_store_equals_one_store(shards):
+    """Key shards worked by the pool (csrc/session_shards.h) give the single store's results:
+    element folds, evicted-row inserts (hot and cold), extracts, firings and snapshots."""
+    from collections import Counter as Ctr
+
+    from mxstream.ops.native import load
+
+    m = load()
+    rng = np.random.default_rng(17)
+    a = m.SessionStore(100, 500, K.AGG_SUM_I64)
+    b = m.SessionStore(100, 500, K.AGG_SUM_I64, shards)
+    assert b.shards == shards
+    res = {0: [], 1: []}
+    for step in range(12):
+        n = 3000
+        k = rng.integers(0, 5000, n).astype(np.int64)
+        t = (step * 400 + rng.integers(0, 600, n)).astype(np.int64)
+        v = rng.integers(0, 50, n).astype(np.int64)
+        ek = np.unique(rng.integers(5000, 9000, 400)).astype(np.int64)
+        es = (step * 400 + (ek % 300)).astype(np.int64)
+        ones = np.ones_like(ek)
+        for j, st_ in enumerate((a, b)):
+            r = res[j]
+            r.append(st_.process(k, t, v, step * 400 - 200))
+            st_.insert(ek, es, es + 100, ek % 7, ones, ones, step % 2 == 0)
+            ex = st_.extract(np.unique(k[:50]), step * 400 - 200, 4)
+            r.append((ex["key"].tolist(), ex["start"].tolist(), ex["acc"].tolist(),
+                      sorted(ex["moved"].tolist())))
+            d = st_.fire(step * 400, [], [], [], [])
+            r.append((Ctr(zip(d["keys"].tolist(), d["start"].tolist(), d["raw"].tolist())),
+                      sorted(d["released"].tolist())))
+            r.append((st_.num_keys(), st_.num_sessions(), st_.num_cold_rows(),
+                      sorted(st_.key_list().tolist())))
+            sn = st_.snapshot()
+            r.append(sorted(zip(sn["key"].tolist(), sn["start"].tolist(), sn["acc"].tolist())))
+    assert res[0] == res[1]
+    d = b.fire((1 << 63) - 1, [], [], [], [])
+    assert b.num_keys() == 0 and len(d["keys"]) > 0
+
+
 # ----------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
 @settings(max_examples=15, deadline=None, suppress_health_check=[HealthCheck.too_slow])
