@@ -59,9 +59,9 @@ _SESSION_SORT = __import__("os").environ.get("MXS_SESSION_SORT", "lds")
 # instead of two scattered 8-byte stores; "0" keeps the two arrays.
 _SESSION_PAIR = int(__import__("os").environ.get("MXS_SESSION_PAIR", "1"))
 # Key shards of the host session store, worked in parallel by a persistent pool
-# (csrc/session_shards.h); MXS_SESSION_SHARDS=1: one store.
-_STORE_SHARDS = int(__import__("os").environ.get(
-    "MXS_SESSION_SHARDS", str(min(16, max(1, __import__("os").cpu_count() or 1)))))
+# (csrc/session_shards.h). Off by default: on the MI355X box 16 shards made config 5's host
+# insert and firing 3-6x slower than one store (profiles/r4_cfg5_shards.md).
+_STORE_SHARDS = int(__import__("os").environ.get("MXS_SESSION_SHARDS", "1"))
 
 
 def _next_pow2(x: int) -> int:
