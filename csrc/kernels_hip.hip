@@ -1126,6 +1126,41 @@ __device__ __forceinline__ uint32_t lds_probe_insert(uint64_t* skeys, uint64_t k
   return kNoSlot;
 }
 
+// lds_probe_insert with four slots per step: the four relaxed 64-bit loads of s..s+3 are
+// independent, so a probe costs one LDS round trip per four slots instead of one per slot --
+// and a wave's lanes, which wait for the longest probe among them, do ~4x fewer dependent
+// rounds (hashed window_agg: 160 us per 16.7M events with the one-slot loop). Same slot order
+// and CAS protocol as the one-slot loop: a slot read as empty but taken meanwhile fails its CAS
+// and the scan goes on, so the table layout is unchanged.
+__device__ __forceinline__ uint32_t lds_probe_insert4(uint64_t* skeys, uint64_t key,
+                                                      uint32_t mask, int* inserted) {
+  uint32_t s = slot_hash(key) & mask;
+  for (uint32_t i = 0; i <= mask; i += 4) {
+    uint64_t k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      k[u] = __hip_atomic_load(&skeys[(s + u) & mask], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i + u > mask) return kNoSlot;  // every slot seen
+      const uint32_t j = (s + u) & mask;
+      if (k[u] == key) return j;
+      if (k[u] == kEmptyKey) {
+        const uint64_t prev = atomicCAS((unsigned long long*)&skeys[j],
+                                        (unsigned long long)kEmptyKey, (unsigned long long)key);
+        if (prev == kEmptyKey) {
+          *inserted = 1;
+          return j;
+        }
+        if (prev == key) return j;
+      }
+    }
+    s = (s + 4) & mask;
+  }
+  return kNoSlot;
+}
+
 template <int AGG>
 __device__ __forceinline__ int64_t lds_identity() {
   if (AGG == AGG_MIN_I64 || AGG == AGG_MIN_F64) return INT64_MAX;
@@ -1318,7 +1353,7 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
             }
             s = dense_slot(r.key, p.dense_mul, p.dense_bits) & mask;
           } else {
-            s = lds_probe_insert(skeys, r.key, mask, &inserted);
+            s = lds_probe_insert4(skeys, r.key, mask, &inserted);
             if (s == kNoSlot) {
               ovf = true;
               continue;
@@ -1643,7 +1678,7 @@ __global__ __launch_bounds__(1024) void window_combine_kernel(
         if (r.t == 0xFFFFFFFFu) continue;  // hole record (staged partition padding)
         const int64_t q = (int64_t)r.t - q0;
         if (q < 0 || q >= npg) continue;
-        const uint32_t s = lds_probe_insert(skeys, r.key, mask, &inserted);
+        const uint32_t s = lds_probe_insert4(skeys, r.key, mask, &inserted);
         if (s == kNoSlot) {
           ovf = true;
           continue;
