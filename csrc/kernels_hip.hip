@@ -2713,12 +2713,20 @@ __device__ __forceinline__ uint32_t sess_probe_claim(uint64_t* keys, uint64_t ke
 // Read-only probe: the key's slot, or kNoSlot (first empty slot reached / table scanned).
 template <int kScope = __HIP_MEMORY_SCOPE_AGENT>
 __device__ __forceinline__ uint32_t sess_find(const uint64_t* keys, uint64_t key, uint32_t mask) {
+  // Four independent loads per round (tombstones make the session tables' chains long; a
+  // wave waits for its longest chain, so rounds -- not slots -- set the cost).
   uint32_t s = slot_hash(key) & mask;
-  for (uint32_t i = 0; i <= mask; ++i) {
-    const uint64_t k = __hip_atomic_load(&keys[s], __ATOMIC_RELAXED, kScope);
-    if (k == key) return s;
-    if (k == kEmptyKey) return kNoSlot;
-    s = (s + 1) & mask;
+  for (uint32_t i = 0; i <= mask; i += 4) {
+    uint64_t k[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) k[u] = __hip_atomic_load(&keys[(s + u) & mask], __ATOMIC_RELAXED, kScope);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i + u > mask) return kNoSlot;
+      if (k[u] == key) return (s + u) & mask;
+      if (k[u] == kEmptyKey) return kNoSlot;
+    }
+    s = (s + 4) & mask;
   }
   return kNoSlot;
 }
