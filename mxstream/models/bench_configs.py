@@ -177,7 +177,9 @@ def config2_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 5
     dev = torch.device(device)
     op = KeyedRollingOperator(agg=K.AGG_COUNT, device=dev, max_keys=table_keys,
                               batch_capacity=batch,
-                              filter_prog=E.compile_expr(E.var(E.VAR_COUNT) % 1000 == 0),
+                              # a key lives ~10 steps x ~8 events: every 64th count alerts,
+                              # so the emit path runs inside the timed steps
+                              filter_prog=E.compile_expr(E.var(E.VAR_COUNT) % 64 == 0),
                               emit_capacity=1 << 20, spill=True)
     kt = torch.empty(batch, dtype=torch.int64, device=dev)
     tt = torch.empty_like(kt)
