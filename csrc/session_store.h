@@ -471,8 +471,9 @@ class SessionCore {
       if (it == m_.end() || it->second.due != due) continue;  // stale entry
       it->second.due = INT64_MAX;  // this entry is consumed
       auto& vec = it->second;
-      std::vector<Session> keep;
-      for (auto& s : vec) {
+      size_t w = 0;  // sessions kept (not cleaned yet), compacted in place: no allocation per key
+      for (size_t r = 0; r < vec.size(); ++r) {
+        Session& s = vec[r];
         const int64_t maxts = s.end - 1;
         if (maxts <= wm && (!(s.flags & 1u) || (s.flags & 2u))) {
           double vars[kExprVars] = {0};
@@ -494,13 +495,13 @@ class SessionCore {
           }
           s.flags = 1u;
         }
-        if (cleanup_time(maxts) > wm) keep.push_back(s);  // not cleaned yet
+        if (cleanup_time(maxts) > wm) vec[w++] = s;  // not cleaned yet
       }
-      if (keep.empty()) {
+      if (w == 0) {
         m_.erase(it);
         released.push_back((int64_t)key);
       } else {
-        vec.swap(keep);
+        vec.resize(w);
         schedule(key);
       }
     }
@@ -738,8 +739,53 @@ class SessionCore {
   int agg_;
   // A key's live sessions plus the due time of its one valid heap entry (schedule() pushes only
   // when the due time changes; fire() skips popped entries whose time is not the key's due).
-  struct Hot : std::vector<Session> {
+  // A hot key's sessions: up to two inline (nearly every key holds one or two), more on the
+  // heap -- an eviction that sends 10^5 keys to the hot map no longer allocates a session
+  // buffer per key on top of the map node.
+  struct Hot {
     int64_t due = INT64_MAX;
+    uint32_t n = 0, cap = 2;
+    Session inl[2];
+    Session* ext = nullptr;
+
+    Hot() = default;
+    Hot(const Hot& o) : due(o.due) { for (const Session& x : o) push_back(x); }
+    Hot& operator=(const Hot& o) {
+      if (this != &o) {
+        n = 0;
+        due = o.due;
+        for (const Session& x : o) push_back(x);
+      }
+      return *this;
+    }
+    Hot(Hot&& o) noexcept : due(o.due), n(o.n), cap(o.cap), ext(o.ext) {
+      if (!ext) for (uint32_t i = 0; i < n; ++i) inl[i] = o.inl[i];
+      o.ext = nullptr;
+      o.n = 0;
+      o.cap = 2;
+    }
+    ~Hot() { delete[] ext; }
+    Session* data() { return ext ? ext : inl; }
+    const Session* data() const { return ext ? ext : inl; }
+    size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+    size_t capacity() const { return cap; }
+    Session& operator[](size_t i) { return data()[i]; }
+    Session* begin() { return data(); }
+    Session* end() { return data() + n; }
+    const Session* begin() const { return data(); }
+    const Session* end() const { return data() + n; }
+    void resize(size_t w) { n = (uint32_t)(w < n ? w : n); }  // shrink only
+    void push_back(const Session& x) {
+      if (n == cap) {
+        Session* nb = new Session[(size_t)cap * 2];
+        for (uint32_t i = 0; i < n; ++i) nb[i] = data()[i];
+        delete[] ext;
+        ext = nb;
+        cap *= 2;
+      }
+      data()[n++] = x;
+    }
   };
   std::unordered_map<uint64_t, Hot> m_;
   // "May be hot" filter over the hot map's keys (one bit per mix64 bucket, set on every hot
