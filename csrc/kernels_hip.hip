@@ -736,6 +736,12 @@ constexpr size_t kCompactLds = compact_lds(kCU);
 static_assert(kCompactLds <= 80 * 1024, "compact partition must fit two workgroups per CU");
 constexpr int kCUProd = 4;               // production round: 4096 records, one group per CU
 static_assert(compact_lds(kCUProd) <= 160 * 1024, "compact partition LDS exceeds 160 KiB");
+// LDS image of a round of 1024 * cu records of rb bytes (8-byte RecN rounds fit 8192 records).
+constexpr size_t compact_lds_rb(int cu, int rb) {
+  return (size_t)1024 * cu * rb + (size_t)kCMaxNb * 6 * 4 + 20 * 4 + 16 * 8 +
+         (size_t)1024 * cu * 2 + (size_t)kKgLdsMax * 4;
+}
+static_assert(compact_lds_rb(8, 8) <= 160 * 1024, "8K-record RecN rounds exceed 160 KiB");
 
 // RB = 16: RecC records; RB = 8: RecN records (one destination, see RecN).
 template <int V, int CU = kCU, bool ONE = false, int RB = 16, bool K32 = false, bool PAIR = false>
@@ -4031,6 +4037,26 @@ void launch_compact(const uint64_t* keys, const int64_t* ts, const uint64_t* val
                     const int32_t* jhash_tab, int64_t n, int64_t chunk, int blocks,
                     const PartPlan& plan, const int32_t* kg_dest, uint32_t* cursor, Rec* out,
                     int64_t* stats, uint32_t* late_idx, uint32_t late_cap, intptr_t stream) {
+  if constexpr (RB == 8) {
+    // MXS_PART_CU8=1: 8192-record rounds (half the rounds, barriers and per-round scans of a
+    // workgroup's 64K events; A/B knob)
+    static const bool cu8 = getenv_int("MXS_PART_CU8", 0) != 0;
+    if (cu8) {
+      auto k8 = partition_compact_kernel<1, 8, ONE, RB, K32, PAIR>;
+      static bool attr8 = false;
+      if (!attr8) {
+        HIP_CHECK(hipFuncSetAttribute((const void*)k8, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)compact_lds_rb(8, 8)));
+        attr8 = true;
+      }
+      const size_t lds8 = compact_lds_rb(8, 8) - (ONE ? (size_t)kKgLdsMax * 4 : 0);
+      hipLaunchKernelGGL(k8, dim3(blocks), dim3(1024), lds8, (hipStream_t)stream, keys, ts, vals,
+                         jhash_tab, n, chunk, plan, kg_dest, cursor, reinterpret_cast<RecC*>(out),
+                         stats, late_idx, late_cap);
+      HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
   auto kfn = partition_compact_kernel<1, kCUProd, ONE, RB, K32, PAIR>;
   static bool attr = false;
   if (!attr) {

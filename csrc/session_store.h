@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <queue>
@@ -27,11 +28,68 @@ struct Session {
   uint32_t flags;      // bit0: fired, bit1: modified since firing
 };
 
+// A growable column of trivially copyable values whose resize does not initialise: an eviction
+// of 10^5-10^6 rows into a cold chunk writes every element itself (std::vector's zero fill was a
+// whole extra pass over the chunk's ~40 bytes a row).
+template <class T>
+struct PodVec {
+  T* p = nullptr;
+  size_t n = 0, cap = 0;
+  PodVec() = default;
+  PodVec(const PodVec& o) { assign(o); }
+  PodVec& operator=(const PodVec& o) {
+    if (this != &o) assign(o);
+    return *this;
+  }
+  PodVec(PodVec&& o) noexcept : p(o.p), n(o.n), cap(o.cap) {
+    o.p = nullptr;
+    o.n = o.cap = 0;
+  }
+  PodVec& operator=(PodVec&& o) noexcept {
+    if (this != &o) {
+      std::free(p);
+      p = o.p;
+      n = o.n;
+      cap = o.cap;
+      o.p = nullptr;
+      o.n = o.cap = 0;
+    }
+    return *this;
+  }
+  ~PodVec() { std::free(p); }
+  void assign(const PodVec& o) {
+    resize(o.n);
+    if (o.n) std::memcpy(p, o.p, o.n * sizeof(T));
+  }
+  void reserve(size_t m) {
+    if (m <= cap) return;
+    T* q = static_cast<T*>(std::realloc(p, m * sizeof(T)));
+    if (!q) throw std::bad_alloc();
+    p = q;
+    cap = m;
+  }
+  void resize(size_t m) {  // new elements are NOT initialised
+    reserve(m);
+    n = m;
+  }
+  void clear() { n = 0; }
+  size_t size() const { return n; }
+  bool empty() const { return n == 0; }
+  size_t capacity() const { return cap; }
+  T* data() { return p; }
+  T& operator[](size_t i) { return p[i]; }
+  const T& operator[](size_t i) const { return p[i]; }
+  T* begin() { return p; }
+  T* end() { return p + n; }
+  const T* begin() const { return p; }
+  const T* end() const { return p + n; }
+};
+
 struct ColdChunk {
-  std::vector<uint64_t> key;
-  std::vector<int64_t> start, end;
-  std::vector<uint64_t> acc;
-  std::vector<uint32_t> cnt;  // 0 = row gone (promoted or discarded)
+  PodVec<uint64_t> key;
+  PodVec<int64_t> start, end;
+  PodVec<uint64_t> acc;
+  PodVec<uint32_t> cnt;  // 0 = row gone (promoted or discarded)
   int64_t max_due = INT64_MIN;
   size_t live = 0;
   // Rows by key: promote() looks keys up by binary search or a merge join instead of probing a
@@ -167,39 +225,107 @@ class SessionCore {
       spare_.pop_back();
     }
     const bool no_hot = m_.empty();
+    // Row i goes to the cold chunk iff it fired unmodified (F == 1) and its key is not hot --
+    // hot already at the call, or made hot by an EARLIER row of this call (the serial rule).
+    // Rows that turn keys hot are few: they are found first (one pass over F), so the cold rows
+    // can be classified, counted and written by several threads (two passes at prefix offsets).
+    // (key, first row) of the rows that turn keys hot, sorted by key, behind a bit filter: a
+    // cold-eligible row pays one bit test unless its key also has such a row.
+    std::vector<std::pair<uint64_t, int64_t>> first_hot;
+    std::vector<uint64_t> fh_bits;
+    uint64_t fh_mask = 0;
     if (cold) {
-      // Columns written by index (no per-row push_back bookkeeping), shrunk at the end; the
-      // cleanup bound is the largest end (cleanup_time is monotone in it).
-      ch.key.resize(n);
-      ch.start.resize(n);
-      ch.end.resize(n);
-      ch.acc.resize(n);
-      ch.cnt.resize(n);
-    }
-    int64_t nc = 0, emax = INT64_MIN;
-    for (int64_t i = 0; i < n; ++i) {
-      const uint64_t key = (uint64_t)K[i];
-      if (cold && F[i] == 1 && (no_hot || !is_hot(key))) {
-        ch.key[nc] = key;
-        ch.start[nc] = S[i];
-        ch.end[nc] = E[i];
-        ch.acc[nc] = (uint64_t)A[i];
-        ch.cnt[nc] = (uint32_t)C[i];
-        emax = E[i] > emax ? E[i] : emax;
-        ++nc;
-        continue;
+      for (int64_t i = 0; i < n; ++i)
+        if (F[i] != 1) first_hot.push_back({(uint64_t)K[i], i});
+      if (!first_hot.empty()) {
+        std::sort(first_hot.begin(), first_hot.end());  // (key, row): the first row leads
+        size_t nb = 64;
+        while (nb < first_hot.size() * 16) nb <<= 1;
+        fh_bits.assign(nb / 64, 0);
+        fh_mask = nb - 1;
+        for (auto& kv : first_hot) {
+          const uint64_t b = mix64(kv.first) & fh_mask;
+          fh_bits[b >> 6] |= 1ull << (b & 63);
+        }
       }
-      m_[key].push_back(Session{S[i], E[i], (uint64_t)A[i], (uint32_t)C[i], (uint32_t)F[i]});
-      mark_hot(key);
-      schedule(key);
     }
+    auto goes_cold = [&](int64_t i) -> bool {
+      if (!cold || F[i] != 1) return false;
+      const uint64_t key = (uint64_t)K[i];
+      if (!no_hot && is_hot(key)) return false;
+      if (!first_hot.empty()) {
+        const uint64_t b = mix64(key) & fh_mask;
+        if ((fh_bits[b >> 6] >> (b & 63)) & 1ull) {
+          auto f = std::lower_bound(first_hot.begin(), first_hot.end(),
+                                    std::make_pair(key, (int64_t)INT64_MIN));
+          if (f != first_hot.end() && f->first == key && f->second < i) return false;
+        }
+      }
+      return true;
+    };
+    int64_t nc = 0, emax = INT64_MIN;
+    std::vector<uint8_t> isc;
     if (cold) {
+      unsigned hw = std::thread::hardware_concurrency();
+      const int T = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)(hw ? hw : 1),
+                                                                 (int64_t)max_threads_,
+                                                                 n / 65536}));
+      std::vector<int64_t> cnt_b(T + 1, 0), emax_b(T, INT64_MIN);
+      isc.resize((size_t)n);  // the classification, made once (pass 2 and the hot rows read it)
+      auto par = [&](auto&& body) {
+        if (T == 1) {
+          body(0);
+          return;
+        }
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; ++t) th.emplace_back(body, t);
+        body(0);
+        for (auto& x : th) x.join();
+      };
+      par([&](int t) {
+        const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+        int64_t c = 0, em = INT64_MIN;
+        for (int64_t i = lo; i < hi; ++i) {
+          isc[i] = goes_cold(i) ? 1 : 0;
+          if (isc[i]) {
+            ++c;
+            em = E[i] > em ? E[i] : em;
+          }
+        }
+        cnt_b[t + 1] = c;
+        emax_b[t] = em;
+      });
+      for (int t = 0; t < T; ++t) {
+        cnt_b[t + 1] += cnt_b[t];
+        emax = std::max(emax, emax_b[t]);
+      }
+      nc = cnt_b[T];
       ch.key.resize(nc);
       ch.start.resize(nc);
       ch.end.resize(nc);
       ch.acc.resize(nc);
       ch.cnt.resize(nc);
+      par([&](int t) {
+        const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+        int64_t o = cnt_b[t];
+        for (int64_t i = lo; i < hi; ++i) {
+          if (!isc[i]) continue;
+          ch.key[o] = (uint64_t)K[i];
+          ch.start[o] = S[i];
+          ch.end[o] = E[i];
+          ch.acc[o] = (uint64_t)A[i];
+          ch.cnt[o] = (uint32_t)C[i];
+          ++o;
+        }
+      });
       if (nc) ch.max_due = std::max(ch.max_due, cleanup_time(emax - 1));
+    }
+    for (int64_t i = 0; i < n; ++i) {
+      if (cold && isc[i]) continue;
+      const uint64_t key = (uint64_t)K[i];
+      m_[key].push_back(Session{S[i], E[i], (uint64_t)A[i], (uint32_t)C[i], (uint32_t)F[i]});
+      mark_hot(key);
+      schedule(key);
     }
     if (!ch.key.empty()) {
       ch.live = ch.key.size();

@@ -287,6 +287,26 @@ def test_sharded_store_equals_one_store(shards):
     assert b.num_keys() == 0 and len(d["keys"]) > 0
 
 
+def test_store_insert_hot_cold_split_follows_row_order():
+    """An evicted row goes to a cold chunk iff it fired unmodified and no earlier row of the call
+    (or the store) made its key hot -- also when the rows are classified by several threads."""
+    from mxstream.ops.native import load
+
+    m = load()
+    n = 300_000
+    k = np.repeat(np.arange(n // 2, dtype=np.int64), 2)      # two rows per key, adjacent
+    f = np.ones(n, dtype=np.int64)
+    f[1::4] = 0   # keys 0, 2, 4, ...: [fired, unfired] -> first row cold, second hot
+    f[2::4] = 0   # keys 1, 3, 5, ...: [unfired, fired] -> both hot
+    st_ = m.SessionStore(100, 1000, K.AGG_SUM_I64)
+    s = (k * 10).astype(np.int64)
+    ones = np.ones_like(k)
+    st_.insert(k, s, s + 50, k, ones, f, True)
+    assert st_.num_cold_rows() == n // 4
+    assert st_.num_sessions() == n
+    assert st_.num_keys() == n // 2 + n // 4  # hot keys + cold rows (one per cold key here)
+
+
 # ----------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
 @settings(max_examples=15, deadline=None, suppress_health_check=[HealthCheck.too_slow])
