@@ -268,7 +268,7 @@ class SessionCore {
     if (cold) {
       unsigned hw = std::thread::hardware_concurrency();
       const int T = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)(hw ? hw : 1),
-                                                                 (int64_t)max_threads_,
+                                                                 (int64_t)insert_threads_,
                                                                  n / 65536}));
       std::vector<int64_t> cnt_b(T + 1, 0), emax_b(T, INT64_MIN);
       isc.resize((size_t)n);  // the classification, made once (pass 2 and the hot rows read it)
@@ -861,6 +861,10 @@ class SessionCore {
   int64_t gap_, late_;
  public:
   int max_threads_ = 16;  // extract's chunk-scan threads (1 inside a sharded store)
+  // Threads of the cold insert's two passes. 1: on the MI355X box the threaded passes made
+  // config 5's insert slower (3.6 -> 4.8 ms/step), thread starts and the runtime's threads
+  // competing for the box's CPU share (profiles/r4_cfg5_shards.md).
+  int insert_threads_ = 1;
  private:
   int agg_;
   // A key's live sessions plus the due time of its one valid heap entry (schedule() pushes only

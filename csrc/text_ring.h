@@ -110,10 +110,13 @@ class TextRingCore {
     int64_t cap;
   };
 
-  bool read_range(char* dst, int64_t off, int64_t len) {
-    // `threads_` contiguous pieces read in parallel (page cache -> pinned memory copies).
+  bool read_range(char* dst, int64_t off, int64_t len, int64_t* newlines) {
+    // `threads_` contiguous pieces read in parallel (page cache -> pinned memory copies); each
+    // piece's newlines are counted right after its read, while the bytes are still in cache
+    // (a separate counting pass re-read the whole chunk from memory).
     const int T = (int)std::min<int64_t>(threads_, std::max<int64_t>(1, len >> 20));
     std::atomic<bool> ok{true};
+    std::vector<int64_t> cnt((size_t)T, 0);
     auto piece = [&](int t) {
       const int64_t a = len * t / T, b = len * (t + 1) / T;
       int64_t pos = a;
@@ -126,23 +129,7 @@ class TextRingCore {
         }
         pos += r;
       }
-    };
-    if (T == 1) {
-      piece(0);
-    } else {
-      std::vector<std::thread> th;
-      for (int t = 0; t < T; ++t) th.emplace_back(piece, t);
-      for (auto& x : th) x.join();
-    }
-    return ok;
-  }
-
-  int64_t count_lines(const char* p, int64_t n) {
-    const int T = (int)std::min<int64_t>(threads_, std::max<int64_t>(1, n >> 22));
-    std::vector<int64_t> c(T, 0);
-    auto piece = [&](int t) {
-      const int64_t a = n * t / T, b = n * (t + 1) / T;
-      c[t] = std::count(p + a, p + b, '\n');
+      cnt[(size_t)t] = std::count(dst + a, dst + b, '\n');
     };
     if (T == 1) {
       piece(0);
@@ -152,8 +139,9 @@ class TextRingCore {
       for (auto& x : th) x.join();
     }
     int64_t k = 0;
-    for (int64_t x : c) k += x;
-    return k + (n > 0 && p[n - 1] != '\n' ? 1 : 0);
+    for (int64_t x : cnt) k += x;
+    *newlines = k;
+    return ok;
   }
 
   void run() {
@@ -170,7 +158,8 @@ class TextRingCore {
       }
       char* dst = slots_[slot].p;
       const int64_t want = std::min(chunk_, hi_ - off);
-      if (!read_range(dst, off, want)) {
+      int64_t nl_read = 0;
+      if (!read_range(dst, off, want, &nl_read)) {
         err = "read failed at offset " + std::to_string(off);
         break;
       }
@@ -183,7 +172,8 @@ class TextRingCore {
         }
         used = nl - dst + 1;
       }
-      const int64_t nl = count_lines(dst, used);
+      // (the bytes past `used` hold no newline: used ends at the chunk's last one)
+      const int64_t nl = nl_read + (used > 0 && dst[used - 1] != '\n' ? 1 : 0);
       off += used;
       std::lock_guard<std::mutex> g(mu_);
       ready_.push_back({slot, used, nl, off - lo_});
