@@ -19,87 +19,10 @@
 #include <vector>
 
 #include "session_store.h"
+#include "thread_pool.h"
 
 namespace mxs {
 namespace sess {
-
-// Fixed workers; run(n, f) calls f(0..n-1) across them and the calling thread, returns when all
-// tasks are done. One run at a time (the store's callers are serialised by the operator).
-class ShardPool {
- public:
-  explicit ShardPool(int workers) {
-    for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
-  }
-  ~ShardPool() {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
-      ++gen_;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  void run(int n, const std::function<void(int)>& f) {
-    if (n <= 0) return;
-    if (th_.empty() || n == 1) {
-      for (int i = 0; i < n; ++i) f(i);
-      return;
-    }
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      job_ = &f;
-      ntask_ = n;
-      next_.store(0);
-      left_ = n;
-      err_ = nullptr;
-      ++gen_;
-    }
-    cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [this] { return left_ == 0; });
-    job_ = nullptr;
-    if (err_) std::rethrow_exception(err_);
-  }
-
- private:
-  void work() {
-    for (;;) {
-      const int i = next_.fetch_add(1);
-      if (i >= ntask_) return;
-      try {
-        (*job_)(i);
-      } catch (...) {
-        std::lock_guard<std::mutex> g(mu_);
-        if (!err_) err_ = std::current_exception();
-      }
-      std::lock_guard<std::mutex> g(mu_);
-      if (--left_ == 0) done_cv_.notify_all();
-    }
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-        if (stop_) return;
-        if (!job_) continue;
-      }
-      work();
-    }
-  }
-  std::vector<std::thread> th_;
-  std::mutex mu_;
-  std::condition_variable cv_, done_cv_;
-  const std::function<void(int)>* job_ = nullptr;
-  std::atomic<int> next_{0};
-  int ntask_ = 0, left_ = 0;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-  std::exception_ptr err_;
-};
 
 class ShardedCore {
  public:
@@ -114,7 +37,7 @@ class ShardedCore {
     if ((1 << b) > 1) {
       const unsigned hw = std::thread::hardware_concurrency();
       const int workers = std::min<int>((1 << b), std::min<int>(hw ? (int)hw : 1, 16)) - 1;
-      pool_.reset(new ShardPool(std::max(0, workers)));
+      pool_.reset(new WorkerPool(std::max(0, workers)));
     }
   }
   int shards() const { return (int)sh_.size(); }
@@ -313,7 +236,7 @@ class ShardedCore {
  private:
   int bits_ = 0;
   std::vector<std::unique_ptr<SessionCore>> sh_;
-  std::unique_ptr<ShardPool> pool_;
+  std::unique_ptr<WorkerPool> pool_;
 };
 
 }  // namespace sess

@@ -23,12 +23,15 @@
 #include <cstdint>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
 #include <utility>
 #include <vector>
+
+#include "thread_pool.h"
 
 namespace mxs {
 
@@ -54,6 +57,8 @@ class TextRingCore {
     }
     fd_ = ::open(path.c_str(), O_RDONLY);
     if (fd_ < 0) throw std::runtime_error("cannot open " + path + ": " + std::strerror(errno));
+    // persistent readers: starting `threads` threads per chunk cost ~1 ms per 48 MB chunk
+    if (threads_ > 1) pool_.reset(new WorkerPool(threads_ - 1));
   }
   ~TextRingCore() { close(); }
 
@@ -131,12 +136,10 @@ class TextRingCore {
       }
       cnt[(size_t)t] = std::count(dst + a, dst + b, '\n');
     };
-    if (T == 1) {
-      piece(0);
+    if (T == 1 || !pool_) {
+      for (int t = 0; t < T; ++t) piece(t);
     } else {
-      std::vector<std::thread> th;
-      for (int t = 0; t < T; ++t) th.emplace_back(piece, t);
-      for (auto& x : th) x.join();
+      pool_->run(T, piece);
     }
     int64_t k = 0;
     for (int64_t x : cnt) k += x;
@@ -188,6 +191,7 @@ class TextRingCore {
   int fd_ = -1;
   int64_t lo_, hi_, chunk_;
   int threads_;
+  std::unique_ptr<WorkerPool> pool_;
   std::vector<Slot> slots_;
   std::deque<int> free_;
   std::deque<Ready> ready_;
