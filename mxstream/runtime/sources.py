@@ -182,6 +182,8 @@ _PINNED_SLOTS: dict = {}  # (bytes, pinned) -> free page-locked slot tensors, re
 # "0" = the SDMA engine (hipMemcpyAsync).
 _H2D_KERNEL = __import__("os").environ.get("MXS_H2D_KERNEL", "0") == "1"
 _H2D_BLOCKS = int(__import__("os").environ.get("MXS_H2D_BLOCKS", "512"))
+# Pinned slots of the file reader's ring (>= 3): the reader stays up to slots - 1 chunks ahead.
+_RING_SLOTS = max(3, int(__import__("os").environ.get("MXS_RING_SLOTS", "4")))
 
 
 def _native():
@@ -228,7 +230,7 @@ class TextFileSource(Source):
 
         chunk = max(1 << 20, self.batch * 48)
         self._pin = torch.cuda.is_available()
-        self._slots = _take_slots(chunk, 4, self._pin)
+        self._slots = _take_slots(chunk, _RING_SLOTS, self._pin)
         self._ring = load().TextFileRing(self.path, self.lo + start, self.hi,
                                          [(t.data_ptr(), t.numel()) for t in self._slots], chunk,
                                          min(16, max(1, __import__("os").cpu_count() or 1)))

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--mb", type=int, default=768)
     ap.add_argument("--chunk-mb", type=int, default=48)
     ap.add_argument("--threads", type=int, nargs="+", default=[4, 8, 16])
+    ap.add_argument("--pageable", action="store_true", help="read into pageable slots")
     a = ap.parse_args()
     line = b"2019-08-28T10:00:00 www.channel0001.com 12345678\n"
     n = (a.mb << 20) // len(line)
@@ -31,7 +32,7 @@ def main():
         f.write(line * n)
     size = os.path.getsize(path)
     chunk = a.chunk_mb << 20
-    pin = torch.cuda.is_available()
+    pin = torch.cuda.is_available() and not a.pageable
     slots = [torch.empty(chunk, dtype=torch.uint8, pin_memory=pin) for _ in range(4)]
     try:
         for th in a.threads:
@@ -52,7 +53,7 @@ def main():
                     ring.release(slot)
                 dt = time.perf_counter() - t0
                 ring.close()
-            print(json.dumps({"threads": th, "bytes": got, "lines": lines, "seconds": dt,
+            print(json.dumps({"threads": th, "pinned": pin, "bytes": got, "lines": lines, "seconds": dt,
                               "gb_per_s": got / dt / 1e9, "lines_per_s": lines / dt}), flush=True)
     finally:
         os.unlink(path)
