@@ -667,6 +667,13 @@ PYBIND11_MODULE(_mxs_native, m) {
   });
   // Fired rows -> one pinned host slab: one hipMemcpyAsync per column on `stream`, no sync
   // (window_operator.to_host_arrays syncs once). copies = [(src, nbytes, dst_offset)].
+  m.def("gpu_h2d_async", [](intptr_t dst, intptr_t src, int64_t bytes, intptr_t stream) {
+    return gpu::h2d_async((void*)dst, (const void*)src, (size_t)bytes, stream);
+  });
+  m.def("gpu_host_register", [](intptr_t p, int64_t bytes) {
+    return gpu::host_register((void*)p, (size_t)bytes);
+  });
+  m.def("gpu_host_unregister", [](intptr_t p) { return gpu::host_unregister((void*)p); });
   m.def("gpu_d2h_many", [](intptr_t dst, const std::vector<std::tuple<intptr_t, int64_t, int64_t>>& copies,
                            intptr_t stream) {
     for (const auto& c : copies) {

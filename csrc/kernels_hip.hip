@@ -3941,6 +3941,16 @@ namespace gpu {
 // synchronisation; set before the device's context exists (bench.py MXS_SPIN=1).
 int set_spin_schedule() { return (int)hipSetDeviceFlags(hipDeviceScheduleSpin); }
 
+int h2d_async(void* dst, const void* src, size_t bytes, intptr_t stream) {
+  return (int)hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream);
+}
+
+int host_register(void* p, size_t bytes) {
+  return (int)hipHostRegister(p, bytes, hipHostRegisterDefault);
+}
+
+int host_unregister(void* p) { return (int)hipHostUnregister(p); }
+
 int d2h_async(void* dst, const void* src, size_t bytes, intptr_t stream) {
   return (int)hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream);
 }

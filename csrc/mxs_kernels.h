@@ -173,6 +173,12 @@ int device_count();
 int set_spin_schedule();
 // Async device->host copy on `stream` (hipMemcpyAsync); returns the hipError_t code.
 int d2h_async(void* dst, const void* src, size_t bytes, intptr_t stream);
+// Async host -> device copy (hipMemcpyAsync); page-lock / release an existing host buffer
+// (hipHostRegister keeps its ordinary cacheable mapping: host writes into it run at memcpy
+// speed, unlike some pinned allocations). All return the hipError_t code.
+int h2d_async(void* dst, const void* src, size_t bytes, intptr_t stream);
+int host_register(void* p, size_t bytes);
+int host_unregister(void* p);
 // Up to kD2HMax device buffers -> one pinned (mapped) host slab by a copy kernel on `stream`;
 // every size, source address and slab offset a multiple of 16 bytes. Returns hipError_t.
 int d2h_kernel(void* dst_host, const D2HCopy* copies, int n, intptr_t stream,

@@ -183,7 +183,9 @@ _PINNED_SLOTS: dict = {}  # (bytes, pinned) -> free page-locked slot tensors, re
 _H2D_KERNEL = __import__("os").environ.get("MXS_H2D_KERNEL", "0") == "1"
 _H2D_BLOCKS = int(__import__("os").environ.get("MXS_H2D_BLOCKS", "512"))
 # Pinned slots of the file reader's ring (>= 3): the reader stays up to slots - 1 chunks ahead.
-_RING_SLOTS = max(3, int(__import__("os").environ.get("MXS_RING_SLOTS", "4")))
+_RING_SLOTS = max(3, int(__import__("os").environ.get("MXS_RING_SLOTS", "8")))
+# Slots are page-locked pageable buffers (hipHostRegister) instead of pinned allocations.
+_SLOT_REGISTER = __import__("os").environ.get("MXS_SLOT_REGISTER", "0") == "1"
 
 
 def _native():
@@ -192,19 +194,43 @@ def _native():
     return load()
 
 
+_REGISTERED: list = []  # page-locked pageable buffers (kept for the process' lifetime)
+
+
+def _registered_slot(nbytes: int):
+    """A page-aligned ordinary host buffer, page-locked with hipHostRegister: DMA-able like a
+    pinned allocation, but with the cacheable mapping of pageable memory -- the reader's copies
+    from the page cache into it ran at 32 GB/s on the box against 23 GB/s into torch's pinned
+    allocations (profiles/r4_reader_box.md)."""
+    import torch
+
+    raw = torch.empty(nbytes + 4096, dtype=torch.uint8)
+    off = (-raw.data_ptr()) % 4096
+    t = raw[off:off + nbytes]
+    rc = _native().gpu_host_register(t.data_ptr(), nbytes)
+    if rc:
+        raise RuntimeError(f"hipHostRegister failed ({rc})")
+    _REGISTERED.append(raw)
+    t._mxs_registered = True
+    return t
+
+
 def _take_slots(nbytes: int, count: int, pin: bool) -> list:
     import torch
 
-    free = _PINNED_SLOTS.setdefault((nbytes, pin), [])
+    reg = pin and _SLOT_REGISTER
+    free = _PINNED_SLOTS.setdefault((nbytes, pin, reg), [])
     out = [free.pop() for _ in range(min(count, len(free)))]
     while len(out) < count:
-        out.append(torch.empty(nbytes, dtype=torch.uint8, pin_memory=pin))
+        out.append(_registered_slot(nbytes) if reg else
+                   torch.empty(nbytes, dtype=torch.uint8, pin_memory=pin))
     return out
 
 
 def _give_slots(slots: list, pin: bool) -> None:
     if slots:
-        _PINNED_SLOTS.setdefault((slots[0].numel(), pin), []).extend(slots)
+        reg = bool(getattr(slots[0], "_mxs_registered", False))
+        _PINNED_SLOTS.setdefault((slots[0].numel(), pin, reg), []).extend(slots)
 
 
 class TextFileSource(Source):
@@ -325,6 +351,15 @@ class TextFileSource(Source):
                     if rc:
                         raise RuntimeError(f"text upload: hip error {rc}")
                     dev = buf[:nbytes]
+                elif getattr(self._slots[slot], "_mxs_registered", False):
+                    # registered (page-locked) pageable slot: an async DMA copy; torch would
+                    # take it for pageable memory and copy synchronously
+                    dev = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self._dev)
+                    rc = _native().gpu_h2d_async(dev.data_ptr(), self._slots[slot].data_ptr(),
+                                                 int(nbytes), self._cstream.cuda_stream)
+                    if rc:
+                        raise RuntimeError(f"text upload: hip error {rc}")
+                    dev = dev[:nbytes]
                 else:
                     dev = tb.data.to(self._dev, non_blocking=True)
                 ev = torch.cuda.Event()

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--chunk-mb", type=int, default=48)
     ap.add_argument("--threads", type=int, nargs="+", default=[4, 8, 16])
     ap.add_argument("--pageable", action="store_true", help="read into pageable slots")
+    ap.add_argument("--registered", action="store_true",
+                    help="read into page-locked pageable slots (hipHostRegister)")
     a = ap.parse_args()
     line = b"2019-08-28T10:00:00 www.channel0001.com 12345678\n"
     n = (a.mb << 20) // len(line)
@@ -33,7 +35,13 @@ def main():
     size = os.path.getsize(path)
     chunk = a.chunk_mb << 20
     pin = torch.cuda.is_available() and not a.pageable
-    slots = [torch.empty(chunk, dtype=torch.uint8, pin_memory=pin) for _ in range(4)]
+    if a.registered:
+        from mxstream.runtime.sources import _registered_slot
+
+        slots = [_registered_slot(chunk) for _ in range(4)]
+        pin = "registered"
+    else:
+        slots = [torch.empty(chunk, dtype=torch.uint8, pin_memory=pin) for _ in range(4)]
     try:
         for th in a.threads:
             for rep in range(2):  # the first pass also warms the page cache
