@@ -47,18 +47,29 @@ __device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
 
 // One workgroup per tile of 256 lines: the tile's bytes are staged into LDS (line_tile.h), every
 // thread splits and parses its line there, then probes the dictionary for its string fields.
+// Line li's bytes [a, b): exclusive end without the '\n' (and a trailing '\r').
+template <class Text>
+__device__ __forceinline__ void line_bounds(Text text, int64_t text_len,
+                                            const int64_t* __restrict__ starts, int64_t n,
+                                            int64_t li, int64_t* pa, int64_t* pb) {
+  const int64_t a = starts[li];
+  int64_t b = li + 1 < n ? starts[li + 1] - 1 : text_len;  // exclusive end (drop '\n')
+  if (b > text_len) b = text_len;
+  if (b > a && text[b - 1] == '\n') --b;  // the last line of a batch ending in '\n'
+  if (b > a && text[b - 1] == '\r') --b;  // SocketTextStreamFunction strips a trailing '\r'
+  *pa = a;
+  *pb = b;
+}
+
 template <class Text>
 __device__ __forceinline__ void ingest_one_line(Text text, const char* __restrict__ gtext,
                                                 int64_t text_len,
                                                 const int64_t* __restrict__ starts, int64_t n,
                                                 int64_t li, const IngestSpec& sp,
                                                 const IngestOut& o, const DictState& d,
-                                                int64_t* local_max, uint32_t* local_flag) {
-  const int64_t a = starts[li];
-  int64_t b = li + 1 < n ? starts[li + 1] - 1 : text_len;  // exclusive end (drop '\n')
-  if (b > text_len) b = text_len;
-  if (b > a && text[b - 1] == '\n') --b;  // the last line of a batch ending in '\n'
-  if (b > a && text[b - 1] == '\r') --b;  // SocketTextStreamFunction strips a trailing '\r'
+                                                int64_t* local_max, uint32_t* local_flag,
+                                                int64_t a = -1, int64_t b = -1) {
+  if (a < 0) line_bounds(text, text_len, starts, n, li, &a, &b);
   int64_t ts = INT64_MIN;
   const uint8_t st = ingest_line(text, a, b, li, n, sp, o, &ts);
   o.status[li] = st;
@@ -99,10 +110,33 @@ __device__ __forceinline__ void ingest_one_line(Text text, const char* __restric
   }
 }
 
+// Per-thread line slots of 17 dwords (an odd stride): the byte-wise split / hash / parse reads
+// of a wave's 64 lines then spread over the LDS banks. Read in place from the contiguous tile,
+// lines ~48 bytes (12 dwords) apart put 8 lanes on every bank (PMC: bank-conflict cycles 4.3x
+// the active LDS cycles, profiles/r4_cfg7_pmc.md). A line is moved into its slot with dword
+// reads and byte-aligning shifts; longer lines stay in the tile.
+constexpr int kPadWords = 17;
+constexpr int kPadBytes = kPadWords * 4;
+
+__device__ __forceinline__ void copy_line_to_slot(const char* src, int64_t len, uint32_t* dst) {
+  const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
+  const uint32_t* sw = reinterpret_cast<const uint32_t*>(sa & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(sa & 3) * 8;
+  const int nw = (int)((len + 3) >> 2);
+  uint32_t w0 = sw[0];
+  for (int k = 0; k < nw; ++k) {
+    const uint32_t w1 = sw[k + 1];
+    dst[k] = sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
+    w0 = w1;
+  }
+}
+
 __global__ __launch_bounds__(256) void ingest_parse_kernel(
     const char* __restrict__ text, int64_t text_len, const int64_t* __restrict__ starts,
     int64_t n, IngestSpec sp, IngestOut o, DictState d) {
-  __shared__ __attribute__((aligned(16))) char tile[kTileLdsBytes];
+  // (+16: the slot copy reads the dword after a line that ends the staged range)
+  __shared__ __attribute__((aligned(16))) char tile[kTileLdsBytes + 16];
+  __shared__ uint32_t slots[kTileLines * kPadWords];
   int64_t local_max = INT64_MIN;
   uint32_t local_flag = 0;
   const int64_t l0 = (int64_t)blockIdx.x * kTileLines;
@@ -113,10 +147,22 @@ __global__ __launch_bounds__(256) void ingest_parse_kernel(
   const LdsText lt = stage_line_tile(text, lo, hi, tile, kTileLdsBytes);
   const int64_t li = l0 + threadIdx.x;
   if (li < l1) {
-    if (lt.p != nullptr)
-      ingest_one_line(lt, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag);
-    else
+    if (lt.p != nullptr) {
+      int64_t a, b;
+      line_bounds(lt, text_len, starts, n, li, &a, &b);
+      if (b - a <= kPadBytes - 4) {
+        uint32_t* slot = slots + threadIdx.x * kPadWords;
+        copy_line_to_slot(lt.p + (a - lt.base), b - a, slot);
+        const LdsText pv{reinterpret_cast<const char*>(slot), a};
+        ingest_one_line(pv, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag,
+                        a, b);
+      } else {
+        ingest_one_line(lt, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag,
+                        a, b);
+      }
+    } else {
       ingest_one_line(text, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag);
+    }
   }
   // One atomic per wave for the flag count and the max timestamp.
   local_max = wave_max_i64(local_max);
