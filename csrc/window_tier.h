@@ -30,11 +30,33 @@ class WindowTierCore {
     int64_t live_from = INT64_MIN;
     size_t dead = 0;
     std::vector<size_t> pane_rows;
+    // Pane-sorted chunk (every absorbed eviction): rows grouped by pane ascending, pane p's rows
+    // at [pane_off[p - pmin], pane_off[p - pmin + 1]), no zero-count rows. A firing's export is
+    // then one contiguous segment per chunk (no per-row filter) and a purge only moves
+    // live_from: the dead rows are a prefix.
+    bool sorted = false;
+    std::vector<size_t> pane_off;
     size_t size() const { return key.size(); }
     bool live(size_t i) const { return pane[i] >= live_from; }
     void count_panes() {
       pane_rows.assign(size() ? (size_t)(pmax - pmin + 1) : 0, 0);
       for (int64_t p : pane) ++pane_rows[(size_t)(p - pmin)];
+      pane_off.clear();
+      if (sorted) {
+        pane_off.assign(pane_rows.size() + 1, 0);
+        for (size_t j = 0; j < pane_rows.size(); ++j) pane_off[j + 1] = pane_off[j] + pane_rows[j];
+      }
+    }
+    // Rows [lo, hi) of the live rows of panes [p0, p1] (sorted chunks only).
+    void segment(int64_t p0, int64_t p1, size_t* lo, size_t* hi) const {
+      const int64_t a = std::max(std::max(p0, pmin), live_from);
+      const int64_t b = std::min(p1, pmax);
+      if (a > b) {
+        *lo = *hi = 0;
+        return;
+      }
+      *lo = pane_off[(size_t)(a - pmin)];
+      *hi = pane_off[(size_t)(b - pmin) + 1];
     }
   };
   struct Rows {
@@ -72,19 +94,22 @@ class WindowTierCore {
               const uint8_t* dirty, size_t n) {
     if (!n) return;
     Chunk c;
-    c.key.assign(key, key + n);
-    c.pane.assign(pane, pane + n);
-    c.acc.assign(acc, acc + n);
-    c.cnt.assign(cnt, cnt + n);
-    c.dirty.assign(dirty, dirty + n);
     for (size_t i = 0; i < n; ++i) {
       c.pmin = std::min(c.pmin, pane[i]);
       c.pmax = std::max(c.pmax, pane[i]);
     }
-    if ((uint64_t)(c.pmax - c.pmin) < ((uint64_t)1 << 20)) c.count_panes();
-    rows_ += n;
+    if ((uint64_t)(c.pmax - c.pmin) < ((uint64_t)1 << 20)) {
+      absorb_sorted(c, key, pane, acc, cnt, dirty, n);
+    } else {
+      c.key.assign(key, key + n);
+      c.pane.assign(pane, pane + n);
+      c.acc.assign(acc, acc + n);
+      c.cnt.assign(cnt, cnt + n);
+      c.dirty.assign(dirty, dirty + n);
+    }
+    rows_ += c.size();
     rows_in_ += (int64_t)n;
-    chunks_.push_back(std::move(c));
+    if (c.size()) chunks_.push_back(std::move(c));
   }
 
   // The tier's share of the window over panes [p0, p1]: one (key, acc, cnt) per key, keys
@@ -136,53 +161,78 @@ class WindowTierCore {
 
   // Live rows of panes [p0, p1], uncombined (the device-merged tiered firing combines them on
   // the GPU): written to k / a / c when they fit `cap` rows; returns the row count either way.
-  // Threaded: chunks are counted in parallel, then copied to their prefix offsets.
+  // Pane-sorted chunks contribute one contiguous segment each (copied by threads in equal row
+  // shares); other chunks are filtered row by row (counted in parallel, then copied to their
+  // prefix offsets). Row order is unspecified.
   size_t export_rows(int64_t p0, int64_t p1, uint64_t* k, uint64_t* a, uint32_t* c,
                      size_t cap) const {
+    struct Seg {
+      const Chunk* ch;
+      size_t lo, hi, out;
+    };
+    std::vector<Seg> segs;
     std::vector<const Chunk*> src;
-    for (auto& ch : chunks_)
-      if (ch.pmax >= p0 && ch.pmin <= p1 && ch.size()) src.push_back(&ch);
-    if (src.empty()) return 0;
+    size_t nseg = 0;
+    for (auto& ch : chunks_) {
+      if (ch.pmax < p0 || ch.pmin > p1 || !ch.size()) continue;
+      if (ch.sorted) {
+        size_t lo, hi;
+        ch.segment(p0, p1, &lo, &hi);
+        if (hi > lo) {
+          segs.push_back({&ch, lo, hi, nseg});
+          nseg += hi - lo;
+        }
+      } else {
+        src.push_back(&ch);
+      }
+    }
     auto keep = [&](const Chunk& ch, size_t i) {
       return ch.pane[i] >= p0 && ch.pane[i] <= p1 && ch.cnt[i] && ch.live(i);
     };
-    unsigned hw = std::thread::hardware_concurrency();
-    const size_t T = std::max<size_t>(1, std::min<size_t>(src.size(), std::min(hw ? hw : 1u, 16u)));
-    auto run = [&](auto&& fn) {
-      if (T == 1) {
-        fn((size_t)0);
-        return;
-      }
-      std::vector<std::thread> th;
-      for (size_t t = 0; t < T; ++t) th.emplace_back(fn, t);
-      for (auto& x : th) x.join();
-    };
     std::vector<size_t> cnt(src.size(), 0);
-    run([&](size_t t) {
-      for (size_t j = t; j < src.size(); j += T) {
-        const Chunk& ch = *src[j];
-        size_t m = 0;
-        for (size_t i = 0; i < ch.size(); ++i) m += keep(ch, i) ? 1 : 0;
-        cnt[j] = m;
-      }
-    });
-    std::vector<size_t> off(src.size() + 1, 0);
+    const size_t Tu = std::max<size_t>(1, std::min<size_t>(src.size(), host_threads(1u << 30)));
+    if (!src.empty())
+      run_threads(Tu, [&](size_t t) {
+        for (size_t j = t; j < src.size(); j += Tu) {
+          const Chunk& ch = *src[j];
+          size_t m = 0;
+          for (size_t i = 0; i < ch.size(); ++i) m += keep(ch, i) ? 1 : 0;
+          cnt[j] = m;
+        }
+      });
+    std::vector<size_t> off(src.size() + 1, nseg);
     for (size_t j = 0; j < src.size(); ++j) off[j + 1] = off[j] + cnt[j];
     const size_t total = off.back();
-    if (total > cap) return total;
-    run([&](size_t t) {
-      for (size_t j = t; j < src.size(); j += T) {
-        const Chunk& ch = *src[j];
-        size_t o = off[j];
-        for (size_t i = 0; i < ch.size(); ++i) {
-          if (!keep(ch, i)) continue;
-          k[o] = ch.key[i];
-          a[o] = (uint64_t)ch.acc[i];
-          c[o] = (uint32_t)ch.cnt[i];
-          ++o;
+    if (total > cap || total == 0) return total;
+    // sorted segments: thread t copies output rows [nseg * t / T, nseg * (t + 1) / T)
+    const size_t T = host_threads(nseg);
+    if (nseg)
+      run_threads(T, [&](size_t t) {
+        const size_t r0 = nseg * t / T, r1 = nseg * (t + 1) / T;
+        for (const Seg& s : segs) {
+          const size_t o0 = std::max(r0, s.out), o1 = std::min(r1, s.out + (s.hi - s.lo));
+          if (o0 >= o1) continue;
+          const size_t i0 = s.lo + (o0 - s.out), m = o1 - o0;
+          std::memcpy(k + o0, s.ch->key.data() + i0, m * 8);
+          std::memcpy(a + o0, s.ch->acc.data() + i0, m * 8);
+          const int64_t* cs = s.ch->cnt.data() + i0;
+          for (size_t q = 0; q < m; ++q) c[o0 + q] = (uint32_t)cs[q];
         }
-      }
-    });
+      });
+    if (!src.empty())
+      run_threads(Tu, [&](size_t t) {
+        for (size_t j = t; j < src.size(); j += Tu) {
+          const Chunk& ch = *src[j];
+          size_t o = off[j];
+          for (size_t i = 0; i < ch.size(); ++i) {
+            if (!keep(ch, i)) continue;
+            k[o] = ch.key[i];
+            a[o] = (uint64_t)ch.acc[i];
+            c[o] = (uint32_t)ch.cnt[i];
+            ++o;
+          }
+        }
+      });
     return total;
   }
 
@@ -405,6 +455,14 @@ class WindowTierCore {
         rows_ -= c.size() - c.dead;
         continue;
       }
+      if (c.sorted && c.pmin < kf) {  // dead rows are the prefix below kf's segment
+        const size_t below = c.pane_off[(size_t)(kf - c.pmin)];
+        rows_ -= below - c.dead;
+        c.dead = below;
+        c.live_from = kf;
+        kept.push_back(std::move(c));
+        continue;
+      }
       if (c.pmin < kf && !c.pane_rows.empty() && kf <= c.pmax) {
         // rows below kf from the pane histogram; mark them dead unless they are half
         size_t below = 0;
@@ -484,7 +542,10 @@ class WindowTierCore {
     out.dirty = m.dirty;
     chunks_.clear();
     rows_ = m.size();
-    if (rows_ && (uint64_t)(m.pmax - m.pmin) < ((uint64_t)1 << 20)) m.count_panes();
+    if (rows_ && (uint64_t)(m.pmax - m.pmin) < ((uint64_t)1 << 20)) {
+      m.sorted = true;  // ordered by (pane, key)
+      m.count_panes();
+    }
     if (rows_) chunks_.push_back(std::move(m));
     return out;
   }
@@ -495,7 +556,73 @@ class WindowTierCore {
   }
 
  private:
+  // fn(t) for t in [0, T) on T host threads (the caller runs t = 0).
+  template <class F>
+  static void run_threads(size_t T, F&& fn) {
+    if (T <= 1) {
+      fn((size_t)0);
+      return;
+    }
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < T; ++t) th.emplace_back(fn, t);
+    fn((size_t)0);
+    for (auto& x : th) x.join();
+  }
+  static size_t host_threads(size_t rows, size_t per = (size_t)1 << 18) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    return std::max<size_t>(1, std::min<size_t>({(size_t)(hw ? hw : 1), (size_t)16,
+                                                 rows / per + 1}));
+  }
+  // Counting sort of an eviction's rows by pane into `c` (zero-count rows dropped): threads
+  // histogram their row range per pane, then scatter at (pane, thread) prefix offsets, so the
+  // order inside a pane stays the input order.
+  void absorb_sorted(Chunk& c, const uint64_t* key, const int64_t* pane, const int64_t* acc,
+                     const int64_t* cnt, const uint8_t* dirty, size_t n) {
+    const size_t P = (size_t)(c.pmax - c.pmin + 1);
+    const size_t T = host_threads(n);
+    std::vector<size_t> h(T * P, 0);
+    const int64_t pmin = c.pmin;
+    run_threads(T, [&](size_t t) {
+      size_t* ht = h.data() + t * P;
+      for (size_t i = n * t / T, e = n * (t + 1) / T; i < e; ++i)
+        if (cnt[i]) ++ht[(size_t)(pane[i] - pmin)];
+    });
+    std::vector<size_t> off(T * P);
+    c.pane_rows.assign(P, 0);
+    c.pane_off.assign(P + 1, 0);
+    size_t tot = 0;
+    for (size_t p = 0; p < P; ++p) {
+      c.pane_off[p] = tot;
+      for (size_t t = 0; t < T; ++t) {
+        off[t * P + p] = tot;
+        tot += h[t * P + p];
+      }
+      c.pane_rows[p] = tot - c.pane_off[p];
+    }
+    c.pane_off[P] = tot;
+    c.key.resize(tot);
+    c.pane.resize(tot);
+    c.acc.resize(tot);
+    c.cnt.resize(tot);
+    c.dirty.resize(tot);
+    run_threads(T, [&](size_t t) {
+      size_t* o = off.data() + t * P;
+      for (size_t i = n * t / T, e = n * (t + 1) / T; i < e; ++i) {
+        if (!cnt[i]) continue;
+        const size_t q = o[(size_t)(pane[i] - pmin)]++;
+        c.key[q] = key[i];
+        c.pane[q] = pane[i];
+        c.acc[q] = acc[i];
+        c.cnt[q] = cnt[i];
+        c.dirty[q] = dirty[i];
+      }
+    });
+    c.sorted = true;
+    // (pmin / pmax may bound panes whose rows were all zero-count: harmless)
+  }
+
   int agg_;
+
   std::deque<Chunk> chunks_;
   size_t rows_ = 0;
   int64_t rows_in_ = 0;

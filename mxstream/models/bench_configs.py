@@ -345,6 +345,9 @@ def config4_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 1
             "spilled_keys": ex.get("spilled_keys", 0), "spilled_rows": ex.get("spilled_rows", 0),
             "dropped_keys": ex.get("dropped_keys", 0), "async_evictions": ex.get("async_evictions", 0),
             "tier_merge": __import__("os").environ.get("MXS_TIER_MERGE", "device"),
+            "pinned_slab_allocs": {k: getattr(getattr(op, a, None), "allocs", 0) for k, a in
+                                   (("fire", "_pool"), ("tier", "_tier_pool"),
+                                    ("evict", "_evict_pool"))},
             "host_tier_rows": op.host_tier.nrows,
             "host_tier_bytes": op.host_tier.nbytes, "hbm_state_bytes": op.state_bytes(),
             "device": str(dev)}

@@ -642,6 +642,55 @@ def test_cxx_window_tier_purge_never_rewinds():
     assert int(r["pane"].min()) == 17 and int(r["cnt"].sum()) == int(cnt[pane >= 17].sum())
 
 
+def test_cxx_window_tier_export_segments():
+    """export_rows (the device-merged tiered firing's upload): pane-sorted chunks give one
+    contiguous segment each, a chunk spanning >= 2^20 panes is filtered row by row; the exported
+    (key, acc, cnt) multiset equals the live rows of the panes, before and after purges, and
+    zero-count rows never leave the tier."""
+    from mxstream.runtime.window_spill import HostWindowTier
+
+    rng = np.random.default_rng(11)
+    t = HostWindowTier(K.AGG_SUM_I64)
+    cols = {k: [] for k in ("key", "pane", "acc", "cnt")}
+    for j in range(6):
+        n = 300_000 if j % 2 else 7000
+        pane = rng.integers(10, 22, n).astype(np.int64)
+        if j == 5:
+            pane[0] = 10 + (1 << 21)  # one far pane: this chunk stays unsorted
+        c = {"key": rng.integers(0, 1 << 40, n).astype(np.uint64), "pane": pane,
+             "acc": rng.integers(-1000, 1000, n).astype(np.int64),
+             "cnt": rng.integers(0, 4, n).astype(np.int64)}
+        t.absorb(c["key"], c["pane"], c["acc"], c["cnt"], np.zeros(n, np.uint8))
+        for k in cols:
+            cols[k].append(c[k])
+    cols = {k: np.concatenate(v) for k, v in cols.items()}
+
+    def check(p0, p1, live_from):
+        got = t.export(p0, p1, "cpu")
+        sel = ((cols["pane"] >= max(p0, live_from)) & (cols["pane"] <= p1) & (cols["cnt"] > 0))
+        if got is None:
+            assert not sel.any()
+            return
+        k, a, c, n, _ = got
+        assert n == int(sel.sum())
+        want = np.stack([cols["key"][sel].view(np.int64), cols["acc"][sel], cols["cnt"][sel]], 1)
+        have = np.stack([k.numpy(), a.numpy(), c.numpy().astype(np.int64)], 1)
+        want = want[np.lexsort(want.T[::-1])]
+        have = have[np.lexsort(have.T[::-1])]
+        assert np.array_equal(want, have)
+
+    check(12, 17, 0)
+    check(0, 1 << 30, 0)
+    t.purge(14)
+    check(12, 17, 14)
+    check(20, 21, 14)
+    t.purge(21)
+    check(0, 1 << 30, 21)
+    # (the unsorted chunk -- the last 300K rows -- keeps its zero-count rows)
+    unsorted = np.arange(cols["pane"].size) >= cols["pane"].size - 300_000
+    assert t.nrows == int(((cols["pane"] >= 21) & ((cols["cnt"] > 0) | unsorted)).sum())
+
+
 def test_latency_fire_equals_pipelined():
     """latency_fire (fire in the call of the triggering batch when few windows are due) emits
     exactly the pipelined operator's rows -- sliding windows, allowed lateness, late data."""
