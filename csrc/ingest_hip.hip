@@ -47,29 +47,18 @@ __device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
 
 // One workgroup per tile of 256 lines: the tile's bytes are staged into LDS (line_tile.h), every
 // thread splits and parses its line there, then probes the dictionary for its string fields.
-// Line li's bytes [a, b): exclusive end without the '\n' (and a trailing '\r').
-template <class Text>
-__device__ __forceinline__ void line_bounds(Text text, int64_t text_len,
-                                            const int64_t* __restrict__ starts, int64_t n,
-                                            int64_t li, int64_t* pa, int64_t* pb) {
-  const int64_t a = starts[li];
-  int64_t b = li + 1 < n ? starts[li + 1] - 1 : text_len;  // exclusive end (drop '\n')
-  if (b > text_len) b = text_len;
-  if (b > a && text[b - 1] == '\n') --b;  // the last line of a batch ending in '\n'
-  if (b > a && text[b - 1] == '\r') --b;  // SocketTextStreamFunction strips a trailing '\r'
-  *pa = a;
-  *pb = b;
-}
-
 template <class Text>
 __device__ __forceinline__ void ingest_one_line(Text text, const char* __restrict__ gtext,
                                                 int64_t text_len,
                                                 const int64_t* __restrict__ starts, int64_t n,
                                                 int64_t li, const IngestSpec& sp,
                                                 const IngestOut& o, const DictState& d,
-                                                int64_t* local_max, uint32_t* local_flag,
-                                                int64_t a = -1, int64_t b = -1) {
-  if (a < 0) line_bounds(text, text_len, starts, n, li, &a, &b);
+                                                int64_t* local_max, uint32_t* local_flag) {
+  const int64_t a = starts[li];
+  int64_t b = li + 1 < n ? starts[li + 1] - 1 : text_len;  // exclusive end (drop '\n')
+  if (b > text_len) b = text_len;
+  if (b > a && text[b - 1] == '\n') --b;  // the last line of a batch ending in '\n'
+  if (b > a && text[b - 1] == '\r') --b;  // SocketTextStreamFunction strips a trailing '\r'
   int64_t ts = INT64_MIN;
   const uint8_t st = ingest_line(text, a, b, li, n, sp, o, &ts);
   o.status[li] = st;
@@ -110,40 +99,10 @@ __device__ __forceinline__ void ingest_one_line(Text text, const char* __restric
   }
 }
 
-// Per-thread line slots of 17 dwords (an odd stride): the byte-wise split / hash / parse reads
-// of a wave's 64 lines then spread over the LDS banks. Read in place from the contiguous tile,
-// lines ~48 bytes (12 dwords) apart put 8 lanes on every bank (PMC: bank-conflict cycles 4.3x
-// the active LDS cycles, profiles/r4_cfg7_pmc.md). Each thread pulls its line into registers with
-// byte-aligning dword reads, the workgroup syncs, and the slots are written OVER the tile: a
-// separate slot array (17 KB) halved the workgroups per CU (24 -> 41 KB of LDS) and the kernel
-// got slower (192 vs 181 us per call, profiles/r4o_cfg7_kernels.md) although bank conflicts fell
-// 8.7x. Lines longer than a slot are parsed from global memory (the tile is overwritten).
-constexpr int kPadWords = 17;
-constexpr int kSlotWords = kPadWords - 1;  // a line of <= 64 bytes fits its slot
-static_assert(kTileLines * kPadWords * 4 <= kTileLdsBytes, "line slots must fit the tile");
-
-__device__ __forceinline__ void load_line_words(const char* src, int64_t len,
-                                                uint32_t (&w)[kSlotWords]) {
-  const uintptr_t sa = reinterpret_cast<uintptr_t>(src);
-  const uint32_t* sw = reinterpret_cast<const uint32_t*>(sa & ~(uintptr_t)3);
-  const uint32_t sh = (uint32_t)(sa & 3) * 8;
-  const int nw = (int)((len + 3) >> 2);
-  uint32_t w0 = sw[0];
-#pragma unroll
-  for (int k = 0; k < kSlotWords; ++k) {
-    if (k < nw) {
-      const uint32_t w1 = sw[k + 1];
-      w[k] = sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0;
-      w0 = w1;
-    }
-  }
-}
-
 __global__ __launch_bounds__(256) void ingest_parse_kernel(
     const char* __restrict__ text, int64_t text_len, const int64_t* __restrict__ starts,
     int64_t n, IngestSpec sp, IngestOut o, DictState d) {
-  // (+16: the slot load reads the dword after a line that ends the staged range)
-  __shared__ __attribute__((aligned(16))) char tile[kTileLdsBytes + 16];
+  __shared__ __attribute__((aligned(16))) char tile[kTileLdsBytes];
   int64_t local_max = INT64_MIN;
   uint32_t local_flag = 0;
   const int64_t l0 = (int64_t)blockIdx.x * kTileLines;
@@ -153,30 +112,11 @@ __global__ __launch_bounds__(256) void ingest_parse_kernel(
   if (hi > text_len) hi = text_len;
   const LdsText lt = stage_line_tile(text, lo, hi, tile, kTileLdsBytes);
   const int64_t li = l0 + threadIdx.x;
-  if (lt.p != nullptr) {  // (uniform over the workgroup)
-    int64_t a = 0, b = 0;
-    bool slot_ok = false;
-    uint32_t w[kSlotWords];
-    if (li < l1) {
-      line_bounds(lt, text_len, starts, n, li, &a, &b);
-      slot_ok = b - a <= (int64_t)kSlotWords * 4;
-      if (slot_ok) load_line_words(lt.p + (a - lt.base), b - a, w);
-    }
-    __syncthreads();  // every line is in registers: the slots may overwrite the tile
-    uint32_t* slot = reinterpret_cast<uint32_t*>(tile) + threadIdx.x * kPadWords;
-    if (slot_ok) {
-      const int nw = (int)((b - a + 3) >> 2);
-#pragma unroll
-      for (int k = 0; k < kSlotWords; ++k)
-        if (k < nw) slot[k] = w[k];
-      const LdsText pv{reinterpret_cast<const char*>(slot), a};
-      ingest_one_line(pv, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag, a, b);
-    } else if (li < l1) {
-      ingest_one_line(text, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag, a,
-                      b);
-    }
-  } else if (li < l1) {
-    ingest_one_line(text, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag);
+  if (li < l1) {
+    if (lt.p != nullptr)
+      ingest_one_line(lt, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag);
+    else
+      ingest_one_line(text, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag);
   }
   // One atomic per wave for the flag count and the max timestamp.
   local_max = wave_max_i64(local_max);

@@ -9,6 +9,7 @@
 #include <cstdint>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <stdexcept>
 #include <thread>
 #include <utility>
@@ -18,13 +19,35 @@
 
 namespace mxs {
 
+// Allocator whose resize() leaves new elements uninitialised: the tier's columns are always
+// written in full right after they grow (an eviction's counting sort scatters every row), and
+// std::vector's zero fill was a whole extra single-threaded pass over ~33 bytes a row.
+template <class T>
+struct NoInitAlloc {
+  using value_type = T;
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) {}
+  T* allocate(size_t n) { return std::allocator<T>().allocate(n); }
+  void deallocate(T* p, size_t n) { std::allocator<T>().deallocate(p, n); }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    if constexpr (sizeof...(A) == 0) ::new ((void*)p) U;
+    else ::new ((void*)p) U(std::forward<A>(a)...);
+  }
+  bool operator==(const NoInitAlloc&) const { return true; }
+  bool operator!=(const NoInitAlloc&) const { return false; }
+};
+template <class T>
+using RowVec = std::vector<T, NoInitAlloc<T>>;
+
 class WindowTierCore {
  public:
   struct Chunk {
     int64_t pmin = INT64_MAX, pmax = INT64_MIN;
-    std::vector<uint64_t> key;
-    std::vector<int64_t> pane, acc, cnt;
-    std::vector<uint8_t> dirty;
+    RowVec<uint64_t> key;
+    RowVec<int64_t> pane, acc, cnt;
+    RowVec<uint8_t> dirty;
     // Lazy purge: rows of panes < live_from are dead (skipped by every reader) until they are
     // half the chunk, then the chunk is filtered. pane_rows[p - pmin] = rows of pane p.
     int64_t live_from = INT64_MIN;
@@ -66,6 +89,9 @@ class WindowTierCore {
   };
 
   explicit WindowTierCore(int agg) : agg_(agg) {}
+  // A copy (the frozen tier of an asynchronous snapshot) leaves the spare columns behind.
+  WindowTierCore(const WindowTierCore& o)
+      : agg_(o.agg_), chunks_(o.chunks_), rows_(o.rows_), rows_in_(o.rows_in_) {}
 
   int agg() const { return agg_; }
   size_t nrows() const { return rows_; }
@@ -99,6 +125,17 @@ class WindowTierCore {
       c.pmax = std::max(c.pmax, pane[i]);
     }
     if ((uint64_t)(c.pmax - c.pmin) < ((uint64_t)1 << 20)) {
+      if (!spare_.empty()) {
+        // A purged chunk's columns: capacity whose pages are already mapped (fresh columns of a
+        // 5M-row eviction page-fault ~190 MB in).
+        Chunk& sp = spare_.back();
+        c.key.swap(sp.key);
+        c.pane.swap(sp.pane);
+        c.acc.swap(sp.acc);
+        c.cnt.swap(sp.cnt);
+        c.dirty.swap(sp.dirty);
+        spare_.pop_back();
+      }
       absorb_sorted(c, key, pane, acc, cnt, dirty, n);
     } else {
       c.key.assign(key, key + n);
@@ -453,6 +490,7 @@ class WindowTierCore {
       const int64_t kf = std::max(keep_from, c.live_from);
       if (c.pmax < kf) {
         rows_ -= c.size() - c.dead;
+        if (c.sorted && spare_.size() < 2) spare_.push_back(std::move(c));
         continue;
       }
       if (c.sorted && c.pmin < kf) {  // dead rows are the prefix below kf's segment
@@ -535,11 +573,11 @@ class WindowTierCore {
       m.pmin = std::min(m.pmin, c.pane[i]);
       m.pmax = std::max(m.pmax, c.pane[i]);
     }
-    out.key = m.key;
-    out.pane = m.pane;
-    out.acc = m.acc;
-    out.cnt = m.cnt;
-    out.dirty = m.dirty;
+    out.key.assign(m.key.begin(), m.key.end());
+    out.pane.assign(m.pane.begin(), m.pane.end());
+    out.acc.assign(m.acc.begin(), m.acc.end());
+    out.cnt.assign(m.cnt.begin(), m.cnt.end());
+    out.dirty.assign(m.dirty.begin(), m.dirty.end());
     chunks_.clear();
     rows_ = m.size();
     if (rows_ && (uint64_t)(m.pmax - m.pmin) < ((uint64_t)1 << 20)) {
@@ -552,6 +590,7 @@ class WindowTierCore {
 
   void clear() {
     chunks_.clear();
+    spare_.clear();
     rows_ = 0;
   }
 
@@ -624,6 +663,7 @@ class WindowTierCore {
   int agg_;
 
   std::deque<Chunk> chunks_;
+  std::vector<Chunk> spare_;  // purged pane-sorted chunks whose columns absorb() reuses
   size_t rows_ = 0;
   int64_t rows_in_ = 0;
 };

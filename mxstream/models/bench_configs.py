@@ -293,6 +293,30 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
             "events_per_step": batch, "state_bytes": op.state_bytes(), "device": str(dev)}
 
 
+@__import__("contextlib").contextmanager
+def _timed_profile():
+    """MXS_BENCH_PROFILE=<file>: cProfile of the timed region only (host hot spots without the
+    warmup's one-time allocations), top entries by own time written to <file>."""
+    out = __import__("os").environ.get("MXS_BENCH_PROFILE")
+    if not out:
+        yield
+        return
+    import cProfile
+    import io
+    import pstats
+
+    prof = cProfile.Profile()
+    prof.enable()
+    try:
+        yield
+    finally:
+        prof.disable()
+        s = io.StringIO()
+        pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(30)
+        with open(out, "w") as f:
+            f.write(s.getvalue())
+
+
 def config4_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 1_000_000,
                   drift: int = 100_000, table_keys: int = 2_000_000, device: str = "cuda") -> dict:
     """Config 4's sliding 1 min / 10 s window + 30 s lateness over a key space that outgrows the
@@ -330,13 +354,14 @@ def config4_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 1
     for _ in range(warmup):
         step()
     _sync(dev)
-    t0 = time.perf_counter()
-    alerts = 0
-    for _ in range(steps):
-        alerts += step()
-    alerts += sum(len(r.keys) for r in op.flush())
-    _sync(dev)
-    dt = time.perf_counter() - t0
+    with _timed_profile():
+        t0 = time.perf_counter()
+        alerts = 0
+        for _ in range(steps):
+            alerts += step()
+        alerts += sum(len(r.keys) for r in op.flush())
+        _sync(dev)
+        dt = time.perf_counter() - t0
     ex = op.metrics.extra
     return {"config": "4-spill", "metric": "events/sec (sliding 1min/10s + lateness, key space "
             "outgrowing HBM, host-DRAM tier)", "value": batch * steps / dt, "unit": "events/s",
