@@ -728,6 +728,16 @@ PYBIND11_MODULE(_mxs_native, m) {
                         P<uint8_t>(dirty_g), nsub, cap_log2, ring, p_lo, np, cutoff,
                         compact_out(o, cap), P<uint32_t>(occ), stream);
   });
+  m.def("gpu_window_rows_pane_sort", [](intptr_t key, intptr_t pane, intptr_t acc, intptr_t cnt,
+                                         intptr_t dirty, intptr_t n_dev, uint32_t cap,
+                                         int64_t p_lo, int np, intptr_t okey, intptr_t oacc,
+                                         intptr_t ocnt, intptr_t odirty, intptr_t counts,
+                                         intptr_t stream) {
+    gpu::window_rows_pane_sort(P<uint64_t>(key), P<int64_t>(pane), P<uint64_t>(acc),
+                               P<uint32_t>(cnt), P<uint8_t>(dirty), P<uint32_t>(n_dev), cap, p_lo,
+                               np, P<uint64_t>(okey), P<uint64_t>(oacc), P<uint32_t>(ocnt),
+                               P<uint8_t>(odirty), P<uint32_t>(counts), stream);
+  });
   m.def("cpu_window_compact", [compact_out](intptr_t keys_g, intptr_t acc_g, intptr_t cnt_g,
                                             intptr_t dirty_g, int nsub, int cap_log2, int ring,
                                             int64_t p_lo, int np, int64_t cutoff,

@@ -1628,6 +1628,72 @@ __global__ __launch_bounds__(1024) void window_compact_kernel(
 }
 
 // ------------------------------------------------------------------------------------------
+// Evicted window rows grouped by pane on the device (host-DRAM tier, csrc/window_tier.h): the
+// tier keeps every chunk pane-sorted, and a host counting sort of a 5M-row eviction cost 42 ms
+// per eviction on the box (55 % of config 4-spill's timed host time, profiles/r4q_*). Two
+// passes over the compaction's n rows (count read on the device): per-pane counts (LDS
+// histogram, one global atomic per pane and workgroup), then each workgroup reserves its
+// per-pane runs and scatters its rows through an LDS cursor. The pane column is not written:
+// the counts carry it. Row order inside a pane is unspecified (the tier's merges are
+// order-free).
+// ------------------------------------------------------------------------------------------
+constexpr int kPaneSortMax = 64;
+
+__global__ __launch_bounds__(256) void pane_sort_hist_kernel(const int64_t* __restrict__ pane,
+                                                             const uint32_t* __restrict__ n_dev,
+                                                             uint32_t cap, int64_t p_lo, int np,
+                                                             uint32_t* __restrict__ gcount) {
+  __shared__ uint32_t h[kPaneSortMax];
+  if (threadIdx.x < kPaneSortMax) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t n = *n_dev < cap ? *n_dev : cap;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int64_t j = pane[i] - p_lo;
+    if (j >= 0 && j < np) atomicAdd(&h[j], 1u);
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < np && h[threadIdx.x]) atomicAdd(&gcount[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(256) void pane_sort_scatter_kernel(
+    const uint64_t* __restrict__ key, const int64_t* __restrict__ pane,
+    const uint64_t* __restrict__ acc, const uint32_t* __restrict__ cnt,
+    const uint8_t* __restrict__ dirty, const uint32_t* __restrict__ n_dev, uint32_t cap,
+    int64_t p_lo, int np, const uint32_t* __restrict__ gcount, uint32_t* __restrict__ gcur,
+    uint64_t* __restrict__ okey, uint64_t* __restrict__ oacc, uint32_t* __restrict__ ocnt,
+    uint8_t* __restrict__ odirty) {
+  __shared__ uint32_t h[kPaneSortMax], base[kPaneSortMax];
+  if (threadIdx.x < kPaneSortMax) h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t n = *n_dev < cap ? *n_dev : cap;
+  const uint32_t step = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+    const int64_t j = pane[i] - p_lo;
+    if (j >= 0 && j < np) atomicAdd(&h[j], 1u);
+  }
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+    for (int j = 0; j < np; ++j) {
+      base[j] = s;
+      s += gcount[j];
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < np && h[threadIdx.x])
+    base[threadIdx.x] += atomicAdd(&gcur[threadIdx.x], h[threadIdx.x]);
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += step) {
+    const int64_t j = pane[i] - p_lo;
+    if (j < 0 || j >= np) continue;
+    const uint32_t q = atomicAdd(&base[j], 1u);
+    okey[q] = key[i];
+    oacc[q] = acc[i];
+    ocnt[q] = cnt[i];
+    odirty[q] = dirty[i];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // Sender-side combiner (G > 1): one workgroup per send bucket (dest rank, sub-table) folds its raw
 // records into a fresh LDS table of that sub-table's geometry and writes one pre-aggregated
 // record per (key, pane): val = exported accumulator, aux = element count. The all-to-all then
@@ -4695,6 +4761,26 @@ void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t*
   hipLaunchKernelGGL(window_compact_kernel, dim3(nsub), dim3(1024), lds, (hipStream_t)stream,
                      keys_g, acc_g, cnt_g, dirty_g, cap_log2, ring, nslots, p_lo, np, cutoff, out,
                      occupancy);
+  HIP_CHECK(hipGetLastError());
+}
+
+void window_rows_pane_sort(const uint64_t* key, const int64_t* pane, const uint64_t* acc,
+                           const uint32_t* cnt, const uint8_t* dirty, const uint32_t* n_dev,
+                           uint32_t cap, int64_t p_lo, int np, uint64_t* okey, uint64_t* oacc,
+                           uint32_t* ocnt, uint8_t* odirty, uint32_t* counts, intptr_t stream) {
+  if (np <= 0 || np > kPaneSortMax)
+    throw std::invalid_argument("window_rows_pane_sort: 1..64 panes");
+  hipStream_t s = (hipStream_t)stream;
+  // counts[0, 64): rows per pane (read by the host with the rows), [64, 128): scatter cursors
+  HIP_CHECK(hipMemsetAsync(counts, 0, 2 * kPaneSortMax * sizeof(uint32_t), s));
+  if (cap == 0) return;
+  const uint32_t want = (cap + 256 * 8 - 1) / (256 * 8);
+  const uint32_t blocks = want < 2048 ? (want ? want : 1) : 2048;
+  hipLaunchKernelGGL(pane_sort_hist_kernel, dim3(blocks), dim3(256), 0, s, pane, n_dev, cap, p_lo,
+                     np, counts);
+  hipLaunchKernelGGL(pane_sort_scatter_kernel, dim3(blocks), dim3(256), 0, s, key, pane, acc, cnt,
+                     dirty, n_dev, cap, p_lo, np, counts, counts + kPaneSortMax, okey, oacc, ocnt,
+                     odirty);
   HIP_CHECK(hipGetLastError());
 }
 

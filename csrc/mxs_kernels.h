@@ -376,6 +376,13 @@ void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t*
 void window_compact(uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
                     int nsub, int cap_log2, int ring, int64_t p_lo, int np, int64_t cutoff,
                     const CompactOut& out, uint32_t* occupancy, intptr_t stream);
+// The compaction's first min(*n_dev, cap) evicted rows grouped by pane (panes [p_lo, p_lo + np),
+// np <= 64) into okey / oacc / ocnt / odirty; counts[j] = rows of pane p_lo + j (counts holds
+// 128 words: [64, 128) are the scatter cursors).
+void window_rows_pane_sort(const uint64_t* key, const int64_t* pane, const uint64_t* acc,
+                           const uint32_t* cnt, const uint8_t* dirty, const uint32_t* n_dev,
+                           uint32_t cap, int64_t p_lo, int np, uint64_t* okey, uint64_t* oacc,
+                           uint32_t* ocnt, uint8_t* odirty, uint32_t* counts, intptr_t stream);
 // (dacc/dcnt: the delta ring of local-global aggregation, zeroed for the same slots and panes.)
 void dirty_clear(const uint32_t* list, const uint32_t* list_n, uint32_t list_cap, int ring,
                  int64_t nslots, uint8_t* dirty_g, uint32_t* slot_mark, int64_t p_lo, int np,

@@ -149,6 +149,67 @@ class WindowTierCore {
     if (c.size()) chunks_.push_back(std::move(c));
   }
 
+  // An eviction already grouped by pane on the device (window_rows_pane_sort): rows of pane
+  // p0 + j are the next counts[j] rows. Threads copy equal row shares; no per-row sort here.
+  void absorb_presorted(const uint64_t* key, const uint64_t* acc, const uint32_t* cnt,
+                        const uint8_t* dirty, int64_t p0, const uint32_t* counts, int np) {
+    size_t n = 0;
+    int j0 = -1, j1 = -1;
+    for (int j = 0; j < np; ++j)
+      if (counts[j]) {
+        n += counts[j];
+        if (j0 < 0) j0 = j;
+        j1 = j;
+      }
+    if (!n) return;
+    Chunk c;
+    if (!spare_.empty()) {
+      Chunk& sp = spare_.back();
+      c.key.swap(sp.key);
+      c.pane.swap(sp.pane);
+      c.acc.swap(sp.acc);
+      c.cnt.swap(sp.cnt);
+      c.dirty.swap(sp.dirty);
+      spare_.pop_back();
+    }
+    c.pmin = p0 + j0;
+    c.pmax = p0 + j1;
+    const size_t P = (size_t)(j1 - j0 + 1);
+    c.pane_rows.assign(P, 0);
+    c.pane_off.assign(P + 1, 0);
+    for (size_t p = 0; p < P; ++p) {
+      c.pane_rows[p] = counts[j0 + p];
+      c.pane_off[p + 1] = c.pane_off[p] + c.pane_rows[p];
+    }
+    c.key.resize(n);
+    c.pane.resize(n);
+    c.acc.resize(n);
+    c.cnt.resize(n);
+    c.dirty.resize(n);
+    const size_t T = host_threads(n);
+    run_threads(T, [&](size_t t) {
+      const size_t lo = n * t / T, hi = n * (t + 1) / T;
+      if (lo >= hi) return;
+      std::memcpy(c.key.data() + lo, key + lo, (hi - lo) * 8);
+      std::memcpy(c.acc.data() + lo, acc + lo, (hi - lo) * 8);
+      std::memcpy(c.dirty.data() + lo, dirty + lo, hi - lo);
+      for (size_t i = lo; i < hi; ++i) c.cnt[i] = cnt[i];
+      // pane column from the segments
+      size_t p = (size_t)(std::upper_bound(c.pane_off.begin(), c.pane_off.end(), lo) -
+                          c.pane_off.begin()) - 1;
+      for (size_t i = lo; i < hi;) {
+        const size_t e = std::min(hi, c.pane_off[p + 1]);
+        std::fill(c.pane.data() + i, c.pane.data() + e, c.pmin + (int64_t)p);
+        i = e;
+        ++p;
+      }
+    });
+    c.sorted = true;
+    rows_ += n;
+    rows_in_ += (int64_t)n;
+    chunks_.push_back(std::move(c));
+  }
+
   // The tier's share of the window over panes [p0, p1]: one (key, acc, cnt) per key, keys
   // ascending. Hash aggregation over the overlapping chunks only.
   void part(int64_t p0, int64_t p1, std::vector<uint64_t>* keys, std::vector<int64_t>* acc,

@@ -43,6 +43,18 @@ void bind_window_tier(py::module_& m) {
         py::gil_scoped_release nogil;
         t.absorb(key.data(), pane.data(), acc.data(), cnt.data(), dirty.data(), n);
       })
+      .def("absorb_presorted", [](WindowTierCore& t, Arr<uint64_t> key, Arr<uint64_t> acc,
+                                  Arr<uint32_t> cnt, Arr<uint8_t> dirty, int64_t p0,
+                                  Arr<uint32_t> counts) {
+        uint64_t n = 0;
+        for (py::ssize_t j = 0; j < counts.size(); ++j) n += counts.data()[j];
+        if ((uint64_t)key.size() < n || (uint64_t)acc.size() < n || (uint64_t)cnt.size() < n ||
+            (uint64_t)dirty.size() < n)
+          throw std::invalid_argument("WindowTier.absorb_presorted: columns shorter than counts");
+        py::gil_scoped_release nogil;
+        t.absorb_presorted(key.data(), acc.data(), cnt.data(), dirty.data(), p0, counts.data(),
+                           (int)counts.size());
+      })
       // Live rows of panes [p0, p1] into caller buffers (addresses; pinned host memory of the
       // device-merged firing): returns the row count, rows written only when it is <= cap.
       .def("export_rows", [](const WindowTierCore& t, int64_t p0, int64_t p1, intptr_t k,

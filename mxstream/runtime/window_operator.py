@@ -129,6 +129,9 @@ _D2H = _os.environ.get("MXS_D2H", "kernel")  # "dma": hipMemcpyAsync (A/B)
 # Tiered firings (host-DRAM window tier): "device" (default) combines the tier's rows with the
 # device's on the GPU; "host": the C++ host merge (A/B, the round-3 path).
 _TIER_MERGE = _os.environ.get("MXS_TIER_MERGE", "device")
+# Evicted rows grouped by pane on the GPU before their D2H (window_rows_pane_sort); "0": the
+# tier's host counting sort (A/B).
+_EVICT_PANE_SORT = _os.environ.get("MXS_EVICT_PANE_SORT", "1") != "0"
 
 
 def _agg_identity(agg: int) -> int:
@@ -1312,10 +1315,33 @@ class KeyedWindowOperator:
             if self._evict_pool is None:
                 self._evict_pool = PinnedSlabPool(max_slabs=2)
             n_cap = o["key"].numel()
-            cols = [o["key"][:n_cap], o["pane"][:n_cap], o["acc"][:n_cap], o["cnt"][:n_cap],
-                    o["dirty"][:n_cap]]
-            rows = CountedHostRows(self._evict_pool, cols, o["ctr"][3:4], [o["ctr"]],
+            presorted = None
+            if _EVICT_PANE_SORT and 0 < np_ <= 64:
+                # Rows grouped by pane on the device: the tier takes them with memcpy instead
+                # of a host counting sort (csrc/window_tier.h absorb_presorted).
+                if "skey" not in o or o["skey"].numel() < n_cap:
+                    o["skey"] = torch.empty(n_cap, dtype=torch.int64, device=dev)
+                    o["sacc"] = torch.empty(n_cap, dtype=torch.int64, device=dev)
+                    o["scnt"] = torch.empty(n_cap, dtype=torch.int32, device=dev)
+                    o["sdirty"] = torch.empty(n_cap, dtype=torch.uint8, device=dev)
+                    o["pcount"] = torch.zeros(128, dtype=torch.int32, device=dev)
+                self._m.gpu_window_rows_pane_sort(
+                    o["key"].data_ptr(), o["pane"].data_ptr(), o["acc"].data_ptr(),
+                    o["cnt"].data_ptr(), o["dirty"].data_ptr(), o["ctr"][3:4].data_ptr(), n_cap,
+                    p_lo, np_, o["skey"].data_ptr(), o["sacc"].data_ptr(), o["scnt"].data_ptr(),
+                    o["sdirty"].data_ptr(), o["pcount"].data_ptr(),
+                    torch.cuda.current_stream(dev).cuda_stream)
+                cols = [o["skey"][:n_cap], o["sacc"][:n_cap], o["scnt"][:n_cap],
+                        o["sdirty"][:n_cap]]
+                fixed = [o["ctr"], o["pcount"]]
+                presorted = (p_lo, np_)
+            else:
+                cols = [o["key"][:n_cap], o["pane"][:n_cap], o["acc"][:n_cap], o["cnt"][:n_cap],
+                        o["dirty"][:n_cap]]
+                fixed = [o["ctr"]]
+            rows = CountedHostRows(self._evict_pool, cols, o["ctr"][3:4], fixed,
                                    copy_stream=self._copy_stream)
+            rows.presorted = presorted
             self._evict_pending = rows
             self._evict_busy = rows.done
             self.metrics.extra["async_evictions"] = self.metrics.extra.get("async_evictions", 0) + 1
@@ -1329,12 +1355,22 @@ class KeyedWindowOperator:
             raise RuntimeError("window_compact: eviction rows overflowed (internal error)")
         n = int(ctr[3])
         if n and self.host_tier is not None:
-            if rows is not None:
+            if rows is not None and getattr(rows, "presorted", None):
+                p_lo, np_ = rows.presorted
+                counts = rows.fixed(1)[:np_]
+                if int(counts.sum()) != n:
+                    raise RuntimeError("window_rows_pane_sort: pane counts do not add up "
+                                       "(internal error)")
+                h = rows.columns(n)
+                self.host_tier.absorb_presorted(h[0], h[1], h[2], h[3], p_lo, counts)
+                h = None
+            elif rows is not None:
                 h = rows.columns(n)
             else:
                 h = to_host_arrays([o["key"], o["pane"], o["acc"], o["cnt"], o["dirty"]], n,
                                    self._pool)
-            self.host_tier.absorb(h[0].view(np.uint64), h[1], h[2], h[3], h[4])
+            if h is not None:
+                self.host_tier.absorb(h[0].view(np.uint64), h[1], h[2], h[3], h[4])
         # (Touched-slot lists and dirty bytes are empty here: every step's re-firings cleared
         # them before this step boundary, so no slot id survives the rehash.)
         ex = self.metrics.extra

@@ -94,6 +94,15 @@ class HostWindowTier:
                        np.ascontiguousarray(cnt, dtype=np.int64),
                        np.ascontiguousarray(dirty, dtype=np.uint8))
 
+    def absorb_presorted(self, key, acc, cnt, dirty, p0: int, counts) -> None:
+        """Rows grouped by pane on the device (window_rows_pane_sort): pane p0 + j holds the
+        next counts[j] rows."""
+        self._t.absorb_presorted(np.ascontiguousarray(key).view(np.uint64),
+                                 np.ascontiguousarray(acc).view(np.uint64),
+                                 np.ascontiguousarray(cnt).view(np.uint32),
+                                 np.ascontiguousarray(dirty, dtype=np.uint8), int(p0),
+                                 np.ascontiguousarray(counts).view(np.uint32))
+
     def pane_range(self) -> tuple[int, int] | None:
         return self._t.pane_range()
 

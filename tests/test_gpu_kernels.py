@@ -414,10 +414,16 @@ def test_deterministic_f64_sums_gpu_bit_exact(gpu_device, dense):
     assert g1 == c and g2 == c and len(c) > 1000
 
 
-def test_spill_tier_gpu_matches_unbounded_cpu(gpu_device):
+@pytest.mark.parametrize("pane_sort", [True, False])
+def test_spill_tier_gpu_matches_unbounded_cpu(gpu_device, pane_sort, monkeypatch):
     """window_compact on the GPU (LDS rehash of every sub-table, eviction rows to the host
-    tier) + tiered firings == an unbounded C++-twin table."""
+    tier, grouped by pane on the device or by the tier's host sort) + tiered firings == an
+    unbounded C++-twin table."""
     import sys
+
+    from mxstream.runtime import window_operator as W
+
+    monkeypatch.setattr(W, "_EVICT_PANE_SORT", pane_sort)
 
     sys.path.insert(0, __import__("os").path.dirname(__file__))
     from test_window_operator_cpu import _drift_batches, _run_windows
@@ -684,3 +690,40 @@ def test_two_level_partition_equals_plain(gpu_device, key_dtype, monkeypatch):
     assert len(a) > 100_000 and sum(1 for x in a if x[1]) > 1000
     assert a == b
     assert aop.metrics.bucket_regrows == 0
+
+
+def test_window_rows_pane_sort(gpu_device):
+    """window_rows_pane_sort: the first min(n, cap) rows grouped by pane (counts per pane), each
+    pane's (key, acc, cnt, dirty) multiset unchanged; rows past n are ignored."""
+    from mxstream.ops.native import load
+
+    m = load()
+    g = torch.Generator().manual_seed(7)
+    cap, n, p_lo, np_ = 300_000, 271_113, 40, 11
+    key = torch.randint(0, 1 << 40, (cap,), generator=g)
+    pane = torch.randint(p_lo, p_lo + np_, (cap,), generator=g)
+    pane[n:] = p_lo + 99  # beyond the count: must not be read as rows
+    acc = torch.randint(-1000, 1000, (cap,), generator=g)
+    cnt = torch.randint(1, 9, (cap,), generator=g, dtype=torch.int32)
+    dirty = torch.randint(0, 2, (cap,), generator=g, dtype=torch.uint8)
+    d = [t.to(gpu_device) for t in (key, pane, acc, cnt, dirty)]
+    n_dev = torch.tensor([n], dtype=torch.int32, device=gpu_device)
+    ok, oa = torch.empty_like(d[0]), torch.empty_like(d[2])
+    oc, od = torch.empty_like(d[3]), torch.empty_like(d[4])
+    counts = torch.empty(128, dtype=torch.int32, device=gpu_device)
+    m.gpu_window_rows_pane_sort(d[0].data_ptr(), d[1].data_ptr(), d[2].data_ptr(),
+                                d[3].data_ptr(), d[4].data_ptr(), n_dev.data_ptr(), cap, p_lo,
+                                np_, ok.data_ptr(), oa.data_ptr(), oc.data_ptr(), od.data_ptr(),
+                                counts.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    c = counts[:np_].cpu().numpy()
+    want_c = np.bincount(pane[:n].numpy() - p_lo, minlength=np_)
+    assert np.array_equal(c, want_c)
+    off = np.concatenate([[0], np.cumsum(c)])
+    got = np.stack([ok.cpu().numpy()[:n], oa.cpu().numpy()[:n], oc.cpu().numpy()[:n],
+                    od.cpu().numpy()[:n]], 1)
+    src = np.stack([key.numpy()[:n], acc.numpy()[:n], cnt.numpy()[:n], dirty.numpy()[:n]], 1)
+    for j in range(np_):
+        a = got[off[j]:off[j + 1]]
+        b = src[pane[:n].numpy() == p_lo + j]
+        assert np.array_equal(a[np.lexsort(a.T[::-1])], b[np.lexsort(b.T[::-1])])

@@ -691,6 +691,42 @@ def test_cxx_window_tier_export_segments():
     assert t.nrows == int(((cols["pane"] >= 21) & ((cols["cnt"] > 0) | unsorted)).sum())
 
 
+def test_cxx_window_tier_presorted_absorb_equals_sort():
+    """absorb_presorted (rows grouped by pane on the device) builds the same tier as absorb's
+    host counting sort of the same rows: same rows(), same exports, same purges."""
+    from mxstream.runtime.window_spill import HostWindowTier
+
+    rng = np.random.default_rng(12)
+    a, b = HostWindowTier(K.AGG_SUM_I64), HostWindowTier(K.AGG_SUM_I64)
+    for j in range(4):
+        n = 200_000 if j % 2 else 3000
+        p_lo, np_ = 20 + 2 * j, 9
+        pane = rng.integers(p_lo + 1, p_lo + np_ - 1, n).astype(np.int64)
+        key = rng.integers(0, 1 << 40, n).astype(np.uint64)
+        acc = rng.integers(-1000, 1000, n).astype(np.int64)
+        cnt = rng.integers(1, 6, n).astype(np.int32)
+        dirty = rng.integers(0, 2, n).astype(np.uint8)
+        a.absorb(key, pane, acc, cnt.astype(np.int64), dirty)
+        o = np.argsort(pane, kind="stable")  # what the device hands over: grouped by pane
+        counts = np.bincount(pane - p_lo, minlength=np_).astype(np.uint32)
+        b.absorb_presorted(key[o], acc[o], cnt[o], dirty[o], p_lo, counts)
+        assert a.nrows == b.nrows and a.pane_range() == b.pane_range()
+        if j == 2:
+            a.purge(24)
+            b.purge(24)
+
+    def canon(t, p0, p1):
+        k, x, c, n, _ = t.export(p0, p1, "cpu")
+        m = np.stack([k.numpy(), x.numpy(), c.numpy().astype(np.int64)], 1)
+        return m[np.lexsort(m.T[::-1])]
+
+    for p0, p1 in ((20, 40), (25, 27), (30, 31)):
+        assert np.array_equal(canon(a, p0, p1), canon(b, p0, p1))
+    ra, rb = a.rows(), b.rows()
+    for k in ("key", "pane", "acc", "cnt", "dirty"):
+        assert np.array_equal(ra[k], rb[k])
+
+
 def test_latency_fire_equals_pipelined():
     """latency_fire (fire in the call of the triggering batch when few windows are due) emits
     exactly the pipelined operator's rows -- sliding windows, allowed lateness, late data."""
