@@ -312,7 +312,9 @@ def _timed_profile():
     finally:
         prof.disable()
         s = io.StringIO()
-        pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(30)
+        st = pstats.Stats(prof, stream=s)
+        st.sort_stats("tottime").print_stats(30)
+        st.print_callers("empty|absorb|export")
         with open(out, "w") as f:
             f.write(s.getvalue())
 

@@ -73,20 +73,41 @@ class HostWindowTier:
 
         self.agg = agg
         self._t = _core if _core is not None else load().WindowTier(agg)
+        # An eviction absorbed on a background thread (absorb_presorted(background=True)): every
+        # reader joins it first; a purge meanwhile is deferred to the join (purges only free
+        # memory -- a firing's export never reads panes below the purge cutoff).
+        self._bg = None
+        self._bg_err = None
+        self._purge_pending = None
+
+    def _join(self) -> None:
+        t, self._bg = self._bg, None
+        if t is not None:
+            t.join()
+            if self._bg_err is not None:
+                e, self._bg_err = self._bg_err, None
+                raise e
+        if self._purge_pending is not None:
+            k, self._purge_pending = self._purge_pending, None
+            self._t.purge(int(k))
 
     @property
     def nrows(self) -> int:
+        self._join()
         return int(self._t.nrows)
 
     @property
     def nbytes(self) -> int:
+        self._join()
         return int(self._t.nbytes)
 
     @property
     def rows_in(self) -> int:
+        self._join()
         return int(self._t.rows_in)
 
     def absorb(self, key, pane, acc, cnt, dirty) -> None:
+        self._join()
         self._t.absorb(np.ascontiguousarray(key).view(np.uint64) if key.dtype == np.int64
                        else np.ascontiguousarray(key, dtype=np.uint64),
                        np.ascontiguousarray(pane, dtype=np.int64),
@@ -94,16 +115,33 @@ class HostWindowTier:
                        np.ascontiguousarray(cnt, dtype=np.int64),
                        np.ascontiguousarray(dirty, dtype=np.uint8))
 
-    def absorb_presorted(self, key, acc, cnt, dirty, p0: int, counts) -> None:
+    def absorb_presorted(self, key, acc, cnt, dirty, p0: int, counts,
+                         background: bool = False) -> None:
         """Rows grouped by pane on the device (window_rows_pane_sort): pane p0 + j holds the
-        next counts[j] rows."""
-        self._t.absorb_presorted(np.ascontiguousarray(key).view(np.uint64),
-                                 np.ascontiguousarray(acc).view(np.uint64),
-                                 np.ascontiguousarray(cnt).view(np.uint32),
-                                 np.ascontiguousarray(dirty, dtype=np.uint8), int(p0),
-                                 np.ascontiguousarray(counts).view(np.uint32))
+        next counts[j] rows. background=True: the copy into the tier (threaded C++, GIL
+        released) runs on a thread while the caller goes on; the arrays must stay valid until
+        the next reader joins it (the pinned slab they view is held by these references)."""
+        self._join()
+        args = (np.ascontiguousarray(key).view(np.uint64), np.ascontiguousarray(acc).view(np.uint64),
+                np.ascontiguousarray(cnt).view(np.uint32),
+                np.ascontiguousarray(dirty, dtype=np.uint8), int(p0),
+                np.ascontiguousarray(counts).view(np.uint32))
+        if not background:
+            self._t.absorb_presorted(*args)
+            return
+        import threading
+
+        def work():
+            try:
+                self._t.absorb_presorted(*args)
+            except BaseException as e:  # re-raised by _join
+                self._bg_err = e
+
+        self._bg = threading.Thread(target=work, name="mxs-tier-absorb", daemon=True)
+        self._bg.start()
 
     def pane_range(self) -> tuple[int, int] | None:
+        self._join()
         return self._t.pane_range()
 
     def overlaps(self, p0: int, p1: int) -> bool:
@@ -117,6 +155,7 @@ class HostWindowTier:
         returned as a fifth element -- hold it until the copy has completed. None: no rows."""
         import torch
 
+        self._join()
         bound = self.nrows
         if bound == 0:
             return None
@@ -143,19 +182,28 @@ class HostWindowTier:
 
     def part(self, p0: int, p1: int):
         """This tier's share of the window over panes [p0, p1]: (keys, acc, cnt) per key."""
+        self._join()
         return self._t.part(int(p0), int(p1))
 
     def purge(self, keep_from: int) -> None:
+        if self._bg is not None:
+            self._purge_pending = (keep_from if self._purge_pending is None
+                                   else max(keep_from, self._purge_pending))
+            return
+        self._join()
         self._t.purge(int(keep_from))
 
     def rows(self) -> dict:
+        self._join()
         return self._t.rows()
 
     def clear(self) -> None:
+        self._join()
         self._t.clear()
 
     def copy(self) -> "HostWindowTier":
         """An independent copy (the frozen tier of an asynchronous snapshot)."""
+        self._join()
         return HostWindowTier(self.agg, _core=self._t.copy())
 
 
@@ -171,6 +219,7 @@ def merge_fire(agg: int, dev_keys, dev_raw, dev_cnt, host, only_dirty: bool,
         # path for an already combined part.
         mc, mk = map_prog.as_args()
         fc, fk = filter_prog.as_args()
+        host._join()
         keys, mapped, raw, cnt = host._t.merge_fire_epilogue(
             int(panes[0]), int(panes[1]), np.ascontiguousarray(dev_keys, dtype=np.uint64),
             np.ascontiguousarray(dev_raw, dtype=np.int64),

@@ -698,6 +698,7 @@ def test_cxx_window_tier_presorted_absorb_equals_sort():
 
     rng = np.random.default_rng(12)
     a, b = HostWindowTier(K.AGG_SUM_I64), HostWindowTier(K.AGG_SUM_I64)
+    c3 = HostWindowTier(K.AGG_SUM_I64)  # background absorbs, purges deferred to the join
     for j in range(4):
         n = 200_000 if j % 2 else 3000
         p_lo, np_ = 20 + 2 * j, 9
@@ -710,10 +711,14 @@ def test_cxx_window_tier_presorted_absorb_equals_sort():
         o = np.argsort(pane, kind="stable")  # what the device hands over: grouped by pane
         counts = np.bincount(pane - p_lo, minlength=np_).astype(np.uint32)
         b.absorb_presorted(key[o], acc[o], cnt[o], dirty[o], p_lo, counts)
-        assert a.nrows == b.nrows and a.pane_range() == b.pane_range()
+        c3.absorb_presorted(key[o], acc[o], cnt[o], dirty[o], p_lo, counts, background=True)
         if j == 2:
             a.purge(24)
             b.purge(24)
+            c3.purge(23)
+            c3.purge(24)  # both deferred while the absorb runs; the larger cutoff applies
+        assert a.nrows == b.nrows == c3.nrows and a.pane_range() == b.pane_range()
+        assert c3.pane_range() == a.pane_range()
 
     def canon(t, p0, p1):
         k, x, c, n, _ = t.export(p0, p1, "cpu")
@@ -722,6 +727,7 @@ def test_cxx_window_tier_presorted_absorb_equals_sort():
 
     for p0, p1 in ((20, 40), (25, 27), (30, 31)):
         assert np.array_equal(canon(a, p0, p1), canon(b, p0, p1))
+        assert np.array_equal(canon(a, p0, p1), canon(c3, p0, p1))
     ra, rb = a.rows(), b.rows()
     for k in ("key", "pane", "acc", "cnt", "dirty"):
         assert np.array_equal(ra[k], rb[k])
