@@ -132,8 +132,10 @@ _TIER_MERGE = _os.environ.get("MXS_TIER_MERGE", "device")
 # Evicted rows grouped by pane on the GPU before their D2H (window_rows_pane_sort); "0": the
 # tier's host counting sort (A/B).
 _EVICT_PANE_SORT = _os.environ.get("MXS_EVICT_PANE_SORT", "1") != "0"
-# The presorted eviction's copy into the tier on a background thread ("0": inline, A/B).
-_TIER_BG_ABSORB = _os.environ.get("MXS_TIER_BG_ABSORB", "1") != "0"
+# The presorted eviction's copy into the tier on a background thread ("1"; off by default: a
+# re-firing over tier panes joins it within the step, config 4-spill 1.44 vs 1.60 G events/s,
+# profiles/r4s_cfg4spill_bg_absorb.json).
+_TIER_BG_ABSORB = _os.environ.get("MXS_TIER_BG_ABSORB", "0") == "1"
 
 
 def _agg_identity(agg: int) -> int:
@@ -1364,7 +1366,6 @@ class KeyedWindowOperator:
                     raise RuntimeError("window_rows_pane_sort: pane counts do not add up "
                                        "(internal error)")
                 h = rows.columns(n)
-                # (on a thread: the next firing over tier panes, snapshot or eviction joins it)
                 self.host_tier.absorb_presorted(h[0], h[1], h[2], h[3], p_lo, counts,
                                                 background=_TIER_BG_ABSORB)
                 h = None
