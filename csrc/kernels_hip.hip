@@ -1167,6 +1167,34 @@ __device__ __forceinline__ uint32_t lds_probe_insert4(uint64_t* skeys, uint64_t 
   return kNoSlot;
 }
 
+// 32-bit key ids (8-byte RecN records) in a table private to one kernel (the sender-side
+// combiner): slots in aligned groups of four, one 16-byte LDS read per group, groups probed
+// linearly. Half the LDS bytes per key and one read instruction per four slots (PMC of the G = 8
+// records path: combiner bank-conflict cycles 1.65x its active LDS cycles with 64-bit keys).
+constexpr uint32_t kEmpty32 = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t lds_probe_insert_g4(uint32_t* sk, uint32_t key, uint32_t mask,
+                                                        int* inserted) {
+  uint32_t g = slot_hash((uint64_t)key) & mask & ~3u;
+  for (uint32_t i = 0; i <= mask; i += 4) {
+    const uint4 v = *reinterpret_cast<const uint4*>(&sk[g]);
+    const uint32_t k[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (k[u] == key) return g + u;
+      if (k[u] == kEmpty32) {
+        const uint32_t prev = atomicCAS(&sk[g + u], kEmpty32, key);
+        if (prev == kEmpty32) {
+          *inserted = 1;
+          return g + u;
+        }
+        if (prev == key) return g + u;
+      }
+    }
+    g = (g + 4) & mask;
+  }
+  return kNoSlot;
+}
+
 template <int AGG>
 __device__ __forceinline__ int64_t lds_identity() {
   if (AGG == AGG_MIN_I64 || AGG == AGG_MIN_F64) return INT64_MAX;
@@ -1710,14 +1738,20 @@ __global__ __launch_bounds__(1024) void window_combine_kernel(
   static_assert(!PK || ((AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) && RW <= 2),
                 "packed combiner: integer sum/avg of 8/16-byte records only");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // KN: 8-byte RecN records carry 32-bit key ids -- 32-bit LDS keys, four-slot groups.
+  constexpr bool KN = RW == 1 && PK;
   const int b = blockIdx.x;
   const uint32_t cap = 1u << p.cap_log2;
   const uint32_t mask = cap - 1;
   uint64_t* skeys = (uint64_t*)smem;
-  uint64_t* sacc = skeys + cap;
+  uint32_t* skeys32 = (uint32_t*)smem;
+  uint64_t* sacc = KN ? (uint64_t*)(skeys32 + cap) : skeys + cap;
   uint32_t* scnt = (uint32_t*)(sacc + (size_t)p.pg * cap);      // unused when PK
   uint32_t* sflag = scnt + (PK ? 0 : (size_t)p.pg * cap);  // [0] records written, [1] overflow
-  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) skeys[i] = kEmptyKey;
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
+    if constexpr (KN) skeys32[i] = kEmpty32;
+    else skeys[i] = kEmptyKey;
+  }
   if (threadIdx.x < 2) sflag[threadIdx.x] = 0;
   uint32_t c = counts[b];
   c = c < p.bucket_cap ? c : p.bucket_cap;
@@ -1750,7 +1784,15 @@ __global__ __launch_bounds__(1024) void window_combine_kernel(
         if (r.t == 0xFFFFFFFFu) continue;  // hole record (staged partition padding)
         const int64_t q = (int64_t)r.t - q0;
         if (q < 0 || q >= npg) continue;
-        const uint32_t s = lds_probe_insert4(skeys, r.key, mask, &inserted);
+        uint32_t s;
+        if constexpr (KN) {
+          // (an id equal to the empty marker cannot be combined: the step goes out raw)
+          s = (uint32_t)r.key != kEmpty32 ? lds_probe_insert_g4(skeys32, (uint32_t)r.key, mask,
+                                                                &inserted)
+                                          : kNoSlot;
+        } else {
+          s = lds_probe_insert4(skeys, r.key, mask, &inserted);
+        }
         if (s == kNoSlot) {
           ovf = true;
           continue;
@@ -1778,7 +1820,7 @@ __global__ __launch_bounds__(1024) void window_combine_kernel(
         const uint32_t pos = wb + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
         if (pos < ccap) {
           Rec o;
-          o.key = skeys[i & mask];
+          o.key = KN ? (uint64_t)skeys32[i & mask] : skeys[i & mask];
           o.val = PK ? (uint64_t)pk_sum(sacc[i]) : lds_export<AGG>(sacc[i]);
           o.t = (uint32_t)(q0 + (int64_t)(i >> p.cap_log2));
           o.aux = PK ? pk_cnt(sacc[i]) : scnt[i];
@@ -5207,7 +5249,7 @@ static void launch_combine(const Rec* recs, const uint32_t* counts, int nbuckets
         attr_pk = true;
       }
       const size_t cap = (size_t)1 << p.cap_log2;
-      const size_t lds_pk = cap * 8 + (size_t)p.pg * cap * 8 + 16;
+      const size_t lds_pk = cap * (p.rec_words == 1 ? 4 : 8) + (size_t)p.pg * cap * 8 + 16;
       if (p.rec_words == 1)
         hipLaunchKernelGGL((window_combine_kernel<AGG, 1, true>), dim3(nbuckets), dim3(1024),
                            lds_pk, s, (const void*)recs, counts, p, out, ccap, out_counts, flags);
