@@ -747,7 +747,9 @@ class KeyedSessionOperator:
         runs on a worker thread while the next step's kernels run."""
         self._join_spill()
         m, st, c = self.native, self._st(), self.ctr
-        self._ensure_spill_capacity(slots.numel() if slots is not None else self._live_estimate)
+        with self._phase("spill.capacity"):
+            self._ensure_spill_capacity(slots.numel() if slots is not None
+                                        else self._live_estimate)
         R = self.spill_rows
         rows = self.st_rows.view(6, R)
         rows[4].zero_()
@@ -766,7 +768,8 @@ class KeyedSessionOperator:
             # Idle eviction without a host round trip: the rows' count stays on the device, a
             # counted copy on a side stream moves just those rows to pinned memory, and the
             # worker applies the counts when it is joined.
-            self._evict_async(rows, R, getattr(self, "_expire_wm", None))
+            with self._phase("spill.async_launch"):
+                self._evict_async(rows, R, getattr(self, "_expire_wm", None))
             return
         with self._phase("spill.evict_kernel"):
             nr_all, ne = self.ctr[7:9].cpu().tolist()
@@ -981,6 +984,8 @@ class KeyedSessionOperator:
         def due(live, occupied):
             return occupied > 0.8 * self.nslots and occupied - live > 0.08 * self.nslots
 
+        t_occ = time.perf_counter()
+
         if self._occ_exact:
             live, occupied = self._count_occupancy()
             if due(live, occupied):
@@ -1005,6 +1010,7 @@ class KeyedSessionOperator:
                 live = self._live_estimate
             elif due(live, live + self._tombs_bound) and self._occ_pending is None:
                 self._occ_launch()
+        self.phase_s["spill.occupancy_logic"] += time.perf_counter() - t_occ
         if live > self.max_load * self.nslots and wm > I64_MIN:
             # LRU by last event time: keys idle for idle_spill_ms move to host DRAM (keys with no
             # live session are simply freed).
