@@ -837,8 +837,10 @@ class KeyedSessionOperator:
         if getattr(self, "_spill_pool", None) is None:
             self._spill_pool = PinnedSlabPool(max_slabs=2)
             self._spill_stream = torch.cuda.Stream(self.device)
-        hr = CountedHostRows(self._spill_pool, [rows[j] for j in range(6)], self.ctr[7:8],
-                             [self.ctr], copy_stream=self._spill_stream)
+        with self._phase("spill.async_launch.copy"):
+            hr = CountedHostRows(self._spill_pool, [rows[j] for j in range(6)], self.ctr[7:8],
+                                 [self.ctr], copy_stream=self._spill_stream)
+        self.metrics.extra["spill_slab_allocs"] = self._spill_pool.allocs
         self._spill_err = None
         self._spill_res = None
 
