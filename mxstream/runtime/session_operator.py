@@ -62,6 +62,25 @@ _SESSION_PAIR = int(__import__("os").environ.get("MXS_SESSION_PAIR", "1"))
 # (csrc/session_shards.h). Off by default: on the MI355X box 16 shards made config 5's host
 # insert and firing 3-6x slower than one store (profiles/r4_cfg5_shards.md).
 _STORE_SHARDS = int(__import__("os").environ.get("MXS_SESSION_SHARDS", "1"))
+# The idle eviction's counted D2H on a side stream ("1", default) or behind the eviction on the
+# compute stream ("0", A/B: the side-stream launch cost the host 1.2 ms per step at config 5
+# while the GPU was busy, against 26 us on an idle GPU -- scripts/d2h_launch_bench.py).
+_SPILL_SIDE_STREAM = __import__("os").environ.get("MXS_SPILL_SIDE_STREAM", "1") != "0"
+
+
+class _OneSlab:
+    """The session eviction's pinned slab (PinnedSlabPool interface): handed out again for every
+    eviction once the previous one's worker has been joined."""
+
+    def __init__(self, t, arr, allocs: int):
+        self.slab, self.allocs = (t, arr), allocs
+
+    def take(self, nbytes: int):
+        if nbytes > self.slab[0].numel():
+            t = torch.empty(_next_pow2(nbytes), dtype=torch.uint8, pin_memory=True)
+            self.slab = (t, t.numpy())
+            self.allocs += 1
+        return self.slab
 
 
 def _next_pow2(x: int) -> int:
@@ -839,8 +858,15 @@ class KeyedSessionOperator:
             self._spill_stream = torch.cuda.Stream(self.device)
         with self._phase("spill.async_launch.copy"):
             hr = CountedHostRows(self._spill_pool, [rows[j] for j in range(6)], self.ctr[7:8],
-                                 [self.ctr], copy_stream=self._spill_stream)
+                                 [self.ctr],
+                                 copy_stream=self._spill_stream if _SPILL_SIDE_STREAM else None)
         self.metrics.extra["spill_slab_allocs"] = self._spill_pool.allocs
+        self.phase_s["spill.async_launch.copy.take"] += hr.t_take
+        self.phase_s["spill.async_launch.copy.launch"] += hr.t_launch
+        if not isinstance(self._spill_pool, _OneSlab):
+            # One eviction copy is in flight at a time (each is joined before the next is
+            # launched): its slab is reused as is, without the pool's free-slab search.
+            self._spill_pool = _OneSlab(hr.t, hr.arr, self._spill_pool.allocs)
         self._spill_err = None
         self._spill_res = None
 

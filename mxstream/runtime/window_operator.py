@@ -184,7 +184,9 @@ class CountedHostRows:
             copies.append((c.data_ptr(), nb, off, c.element_size()))
             self.cols_meta.append((off, c.dtype))
             off += (nb + 255) & ~255
+        t0 = __import__("time").perf_counter()
         self.t, self.arr = pool.take(off)
+        t1 = __import__("time").perf_counter()
         dev = cols[0].device
         cur = torch.cuda.current_stream(dev)
         st = cur
@@ -200,6 +202,8 @@ class CountedHostRows:
         self.ev = torch.cuda.Event()
         self.ev.record(st)
         self.done = self.ev
+        # host seconds: slab take, the rest of the launch (phase timers of the callers)
+        self.t_take, self.t_launch = t1 - t0, __import__("time").perf_counter() - t1
 
     def ready(self) -> bool:
         return self.ev.query()
