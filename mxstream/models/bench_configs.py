@@ -293,6 +293,18 @@ def config4(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 10_000_00
             "events_per_step": batch, "state_bytes": op.state_bytes(), "device": str(dev)}
 
 
+def _gc_settle() -> None:
+    """MXS_GC_FREEZE=1: after the warmup, collect once and move every surviving object to the
+    permanent generation (gc.freeze), so the cyclic collector's full passes no longer walk the
+    job's long-lived state during the timed steps (A/B knob)."""
+    import gc
+    import os
+
+    if os.environ.get("MXS_GC_FREEZE", "0") == "1":
+        gc.collect()
+        gc.freeze()
+
+
 @__import__("contextlib").contextmanager
 def _timed_profile():
     """MXS_BENCH_PROFILE=<file>: cProfile of the timed region only (host hot spots without the
@@ -427,6 +439,7 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
     for _ in range(warmup):
         step()
     _sync(dev)
+    _gc_settle()
     lat.clear()
     op.phase_s.clear()
     m0 = dict(op.metrics.__dict__)
