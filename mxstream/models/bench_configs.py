@@ -303,6 +303,10 @@ def _gc_settle() -> None:
     if os.environ.get("MXS_GC_FREEZE", "0") == "1":
         gc.collect()
         gc.freeze()
+    # MXS_SWITCH_INTERVAL=<seconds>: the interpreter's thread switch interval (A/B of GIL
+    # hand-offs between the step and the spill worker; Python's default is 0.005).
+    if os.environ.get("MXS_SWITCH_INTERVAL"):
+        __import__("sys").setswitchinterval(float(os.environ["MXS_SWITCH_INTERVAL"]))
 
 
 @__import__("contextlib").contextmanager
