@@ -7,6 +7,7 @@
 #include <condition_variable>
 #include <exception>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -35,60 +36,68 @@ class WorkerPool {
       for (int i = 0; i < n; ++i) f(i);
       return;
     }
+    // Each run gets its own task counter: a worker still inside work() from an earlier run
+    // holds that run's Job, whose counter is exhausted, so it can never take (or double-count)
+    // a task index of this one.
+    auto job = std::make_shared<Job>();
+    job->f = &f;
+    job->n = n;
+    job->left = n;
     {
       std::lock_guard<std::mutex> g(mu_);
-      job_ = &f;
-      ntask_ = n;
-      next_.store(0);
-      left_ = n;
-      err_ = nullptr;
+      cur_ = job;
       ++gen_;
     }
     cv_.notify_all();
-    work();
+    work(*job);
     std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [this] { return left_ == 0; });
-    job_ = nullptr;
-    if (err_) std::rethrow_exception(err_);
+    done_cv_.wait(lk, [&] { return job->left == 0; });
+    cur_.reset();
+    if (job->err) std::rethrow_exception(job->err);
   }
 
  private:
-  void work() {
+  struct Job {
+    const std::function<void(int)>* f = nullptr;
+    int n = 0;
+    std::atomic<int> next{0};
+    int left = 0;  // guarded by mu_
+    std::exception_ptr err;
+  };
+  void work(Job& j) {
     for (;;) {
-      const int i = next_.fetch_add(1);
-      if (i >= ntask_) return;
+      const int i = j.next.fetch_add(1);
+      if (i >= j.n) return;
       try {
-        (*job_)(i);
+        (*j.f)(i);
       } catch (...) {
         std::lock_guard<std::mutex> g(mu_);
-        if (!err_) err_ = std::current_exception();
+        if (!j.err) j.err = std::current_exception();
       }
       std::lock_guard<std::mutex> g(mu_);
-      if (--left_ == 0) done_cv_.notify_all();
+      if (--j.left == 0) done_cv_.notify_all();
     }
   }
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      std::shared_ptr<Job> j;
       {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_ != seen; });
         seen = gen_;
         if (stop_) return;
-        if (!job_) continue;
+        j = cur_;
       }
-      work();
+      if (j) work(*j);
     }
   }
   std::vector<std::thread> th_;
   std::mutex mu_;
   std::condition_variable cv_, done_cv_;
-  const std::function<void(int)>* job_ = nullptr;
-  std::atomic<int> next_{0};
-  int ntask_ = 0, left_ = 0;
+  std::shared_ptr<Job> cur_;
   uint64_t gen_ = 0;
   bool stop_ = false;
-  std::exception_ptr err_;
 };
 
 

@@ -645,6 +645,11 @@ class KeyedWindowOperator:
         if spill:
             if self.dense_bits or not type(self)._spill_ok:
                 raise ValueError("spill needs hashed keys and a plain reduce")
+            if self.deterministic:
+                # A tiered firing folds device and tier rows of a key with f64 atomics
+                # (tier_merge), whose order varies between runs: the bit-identical promise of
+                # deterministic=True cannot hold once a window has rows in the host tier.
+                raise ValueError("deterministic=True does not combine with spill=True")
             from .window_spill import HostWindowTier
 
             self.host_tier = HostWindowTier(agg)
@@ -1821,7 +1826,8 @@ class KeyedWindowOperator:
             return
         R, N = self.ring_m, self.nslots_o
         cnt = self.cnt_m.view(R, N)
-        live = torch.nonzero(((cnt != 0).any(0)) & (self.keys_m >= 0)).flatten()
+        live = torch.nonzero(((cnt != 0).any(0)) & (self.keys_m != -1)
+                             & (self.keys_m != -2)).flatten()
         keys = self.keys_m[live]
         acc = self.acc_m.view(R, N)[:, live]
         cnt_l = cnt[:, live]

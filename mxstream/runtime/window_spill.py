@@ -167,6 +167,8 @@ class HostWindowTier:
             t, arr = pool.take(2 * a8 + bound * 4 + 256)
             base = t.data_ptr()
             n = int(self._t.export_rows(int(p0), int(p1), base, base + a8, base + 2 * a8, bound))
+            if n > bound:  # export_rows writes nothing past `bound` and returns the total
+                raise RuntimeError(f"tier export: {n} live rows exceed the {bound}-row slab")
             if n == 0:
                 return None
             k = t[:n * 8].view(torch.int64).to(device, non_blocking=True)
@@ -178,6 +180,8 @@ class HostWindowTier:
         c = np.empty(bound, np.int32)
         n = int(self._t.export_rows(int(p0), int(p1), k.ctypes.data, a.ctypes.data, c.ctypes.data,
                                     bound))
+        if n > bound:
+            raise RuntimeError(f"tier export: {n} live rows exceed the {bound}-row bound")
         if n == 0:
             return None
         return (torch.from_numpy(k[:n]), torch.from_numpy(a[:n]), torch.from_numpy(c[:n]), n,

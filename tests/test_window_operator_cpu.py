@@ -787,14 +787,19 @@ def test_spill_tier_multirank_matches_unbounded_table(world, exchange):
     assert got == ref
 
 
-def test_partials_merge_table_drops_dead_keys():
+@pytest.mark.parametrize("high_bit", [False, True])
+def test_partials_merge_table_drops_dead_keys(high_bit):
     """Local-global owners keep a key in the merge table while a fired window inside its allowed
     lateness holds a value for it. With drifting keys the dead ones are compacted away (the
     table is sized for ~one window's keys here, far below the keys of the whole run) and the
-    output still equals one rank with an unbounded table."""
+    output still equals one rank with an unbounded table. high_bit: every key has its top bit
+    set (negative int64); only -1 / -2 are reserved slot markers, so compaction must keep them
+    and late re-firings must still see their merge slices."""
     from mxstream.parallel.comm import run_loopback
 
     batches = _drift_batches(40, 6000, seed=8)  # ~60K distinct keys over the run
+    if high_bit:
+        batches = [(k + np.iinfo(np.int64).min, t, v) for k, t, v in batches]
     ref, _ = _run_windows(batches, max_keys=120_000)
     world = 2
 
