@@ -15,6 +15,7 @@ the timed region: source -> partition -> RCCL all-to-all -> window aggregation -
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import sys
@@ -64,6 +65,7 @@ def main() -> int:
     ap.add_argument("--no-records-figure", action="store_true",
                     help="G > 1: skip the per-event-exchange (records) run reported next to it")
     a = ap.parse_args()
+    faulthandler.enable()  # an abort or fault prints every thread's Python stack to stderr
 
     if os.environ.get("MXS_SPIN") == "1" and a.device == "cuda":
         # Spin-wait host syncs (hipDeviceScheduleSpin) before torch creates the HIP context.
@@ -286,6 +288,9 @@ def main() -> int:
             bench.op.timer.flush()
         path = a.trace if comm.world == 1 else f"{a.trace}.rank{comm.rank}"
         trace.dump(path, comm.rank)
+    from mxstream.parallel.comm import shutdown_distributed
+
+    shutdown_distributed(comm)
     return 0
 
 

@@ -41,6 +41,8 @@ class ShardedCore {
     }
   }
   int shards() const { return (int)sh_.size(); }
+  // The one core of an unsharded store (the asynchronous spill worker's phased insert), else null.
+  SessionCore* single() { return sh_.size() == 1 ? sh_[0].get() : nullptr; }
   int shard_of(uint64_t key) const {
     return bits_ ? (int)((mix64(key ^ 0x5bd1e9955bd1e995ull) * 0x9e3779b97f4a7c15ull) >> (64 - bits_))
                  : 0;
@@ -190,6 +192,7 @@ class ShardedCore {
     for (auto& s : sh_) s->spill_set_add(cap_log2, d);
   }
   bool contains(uint64_t key) const { return sh_[shard_of(key)]->contains(key); }
+  bool hot(uint64_t key) const { return sh_[shard_of(key)]->hot(key); }
   size_t num_keys() const {
     size_t t = 0;
     for (auto& s : sh_) t += s->num_keys();

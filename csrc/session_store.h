@@ -214,21 +214,36 @@ class SessionCore {
 
   // Insert sessions evicted from HBM. Arrays: key, start, end, acc, cnt, flags. With `cold`,
   // fired-and-unmodified sessions of keys without hot state go to one new cold chunk.
+  // Three phases, so the asynchronous spill worker (csrc/sessions.cpp) can hold the store's lock
+  // only where the store is touched: insert_hot (classify every row, hot rows into the map),
+  // build_cold (the cold rows copied into a chunk: no store state), publish_cold (the chunk
+  // joins the store).
+  struct ColdPlan {
+    ColdChunk ch;
+    std::vector<uint8_t> isc;  // per row: 1 = goes to the cold chunk
+    int64_t nc = 0, emax = INT64_MIN;
+  };
   void insert(const int64_t* K, const int64_t* S, const int64_t* E, const int64_t* A,
               const int64_t* C, const int64_t* F, int64_t n, bool cold) {
+    ColdPlan p;
+    insert_hot(K, S, E, A, C, F, n, cold, p);
+    if (cold) {
+      build_cold(K, S, E, A, C, n, p);
+      publish_cold(p);
+    }
+  }
+  void insert_hot(const int64_t* K, const int64_t* S, const int64_t* E, const int64_t* A,
+                  const int64_t* C, const int64_t* F, int64_t n, bool cold, ColdPlan& p) {
     refresh_hot_filter();
-    ColdChunk ch;
     if (cold && !spare_.empty()) {
       // A dropped chunk's columns: capacity whose pages are already mapped. Fresh columns of a
       // 400K-row eviction cost ~3500 page faults, most of the insert's time.
-      ch = std::move(spare_.back());
+      p.ch = std::move(spare_.back());
       spare_.pop_back();
     }
     const bool no_hot = m_.empty();
     // Row i goes to the cold chunk iff it fired unmodified (F == 1) and its key is not hot --
     // hot already at the call, or made hot by an EARLIER row of this call (the serial rule).
-    // Rows that turn keys hot are few: they are found first (one pass over F), so the cold rows
-    // can be classified, counted and written by several threads (two passes at prefix offsets).
     // (key, first row) of the rows that turn keys hot, sorted by key, behind a bit filter: a
     // cold-eligible row pays one bit test unless its key also has such a row.
     std::vector<std::pair<uint64_t, int64_t>> first_hot;
@@ -263,76 +278,69 @@ class SessionCore {
       }
       return true;
     };
-    int64_t nc = 0, emax = INT64_MIN;
-    std::vector<uint8_t> isc;
     if (cold) {
-      unsigned hw = std::thread::hardware_concurrency();
-      const int T = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)(hw ? hw : 1),
-                                                                 (int64_t)insert_threads_,
-                                                                 n / 65536}));
-      std::vector<int64_t> cnt_b(T + 1, 0), emax_b(T, INT64_MIN);
-      isc.resize((size_t)n);  // the classification, made once (pass 2 and the hot rows read it)
-      auto par = [&](auto&& body) {
-        if (T == 1) {
-          body(0);
-          return;
+      p.isc.resize((size_t)n);
+      int64_t c = 0, em = INT64_MIN;
+      for (int64_t i = 0; i < n; ++i) {
+        const uint8_t x = goes_cold(i) ? 1 : 0;
+        p.isc[i] = x;
+        if (x) {
+          ++c;
+          em = E[i] > em ? E[i] : em;
         }
-        std::vector<std::thread> th;
-        for (int t = 1; t < T; ++t) th.emplace_back(body, t);
-        body(0);
-        for (auto& x : th) x.join();
-      };
-      par([&](int t) {
-        const int64_t lo = n * t / T, hi = n * (t + 1) / T;
-        int64_t c = 0, em = INT64_MIN;
-        for (int64_t i = lo; i < hi; ++i) {
-          isc[i] = goes_cold(i) ? 1 : 0;
-          if (isc[i]) {
-            ++c;
-            em = E[i] > em ? E[i] : em;
-          }
-        }
-        cnt_b[t + 1] = c;
-        emax_b[t] = em;
-      });
-      for (int t = 0; t < T; ++t) {
-        cnt_b[t + 1] += cnt_b[t];
-        emax = std::max(emax, emax_b[t]);
       }
-      nc = cnt_b[T];
-      ch.key.resize(nc);
-      ch.start.resize(nc);
-      ch.end.resize(nc);
-      ch.acc.resize(nc);
-      ch.cnt.resize(nc);
-      par([&](int t) {
-        const int64_t lo = n * t / T, hi = n * (t + 1) / T;
-        int64_t o = cnt_b[t];
-        for (int64_t i = lo; i < hi; ++i) {
-          if (!isc[i]) continue;
-          ch.key[o] = (uint64_t)K[i];
-          ch.start[o] = S[i];
-          ch.end[o] = E[i];
-          ch.acc[o] = (uint64_t)A[i];
-          ch.cnt[o] = (uint32_t)C[i];
-          ++o;
-        }
-      });
-      if (nc) ch.max_due = std::max(ch.max_due, cleanup_time(emax - 1));
+      p.nc = c;
+      p.emax = em;
+      if (c == n) return;  // every row cold: nothing for the hot map
     }
     for (int64_t i = 0; i < n; ++i) {
-      if (cold && isc[i]) continue;
+      if (cold && p.isc[i]) continue;
       const uint64_t key = (uint64_t)K[i];
       m_[key].push_back(Session{S[i], E[i], (uint64_t)A[i], (uint32_t)C[i], (uint32_t)F[i]});
       mark_hot(key);
       schedule(key);
     }
-    if (!ch.key.empty()) {
-      ch.live = ch.key.size();
-      ch.seal();
-      cold_rows_ += ch.live;
-      cold_.push_back(std::move(ch));
+  }
+  // The classified cold rows into p.ch (touches no store state: runs outside the store lock).
+  static void build_cold(const int64_t* K, const int64_t* S, const int64_t* E, const int64_t* A,
+                         const int64_t* C, int64_t n, ColdPlan& p) {
+    ColdChunk& ch = p.ch;
+    const int64_t nc = p.nc;
+    ch.key.resize(nc);
+    ch.start.resize(nc);
+    ch.end.resize(nc);
+    ch.acc.resize(nc);
+    ch.cnt.resize(nc);
+    if (nc == n) {  // the common eviction: every row cold, straight column copies
+      std::memcpy(ch.key.data(), K, (size_t)n * 8);
+      std::memcpy(ch.start.data(), S, (size_t)n * 8);
+      std::memcpy(ch.end.data(), E, (size_t)n * 8);
+      std::memcpy(ch.acc.data(), A, (size_t)n * 8);
+      for (int64_t i = 0; i < n; ++i) ch.cnt[i] = (uint32_t)C[i];
+    } else {
+      int64_t o = 0;
+      for (int64_t i = 0; i < n; ++i) {
+        if (!p.isc[i]) continue;
+        ch.key[o] = (uint64_t)K[i];
+        ch.start[o] = S[i];
+        ch.end[o] = E[i];
+        ch.acc[o] = (uint64_t)A[i];
+        ch.cnt[o] = (uint32_t)C[i];
+        ++o;
+      }
     }
+    if (nc) ch.seal();
+  }
+  void publish_cold(ColdPlan& p) {
+    ColdChunk& ch = p.ch;
+    if (ch.key.empty()) {
+      if (ch.key.capacity() && spare_.size() < 4) spare_.push_back(std::move(ch));
+      return;
+    }
+    ch.max_due = std::max(ch.max_due, cleanup_time(p.emax - 1));
+    ch.live = ch.key.size();
+    cold_rows_ += ch.live;
+    cold_.push_back(std::move(ch));
   }
 
   // Hand keys back to the HBM tier: every listed key with at most `max_sess` live sessions
@@ -706,6 +714,8 @@ class SessionCore {
         if (ch.cnt[r] && ch.key[r] == key) return true;
     return false;
   }
+  // The key has sessions in the hot map.
+  bool hot(uint64_t key) const { return is_hot(key); }
   // Keys (cold rows are one session per key in practice: an upper bound otherwise).
   size_t num_keys() const { return m_.size() + cold_rows_; }
   size_t num_sessions() const {
@@ -861,10 +871,6 @@ class SessionCore {
   int64_t gap_, late_;
  public:
   int max_threads_ = 16;  // extract's chunk-scan threads (1 inside a sharded store)
-  // Threads of the cold insert's two passes. 1: on the MI355X box the threaded passes made
-  // config 5's insert slower (3.6 -> 4.8 ms/step), thread starts and the runtime's threads
-  // competing for the box's CPU share (profiles/r4_cfg5_shards.md).
-  int insert_threads_ = 1;
  private:
   int agg_;
   // A key's live sessions plus the due time of its one valid heap entry (schedule() pushes only

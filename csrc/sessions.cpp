@@ -27,8 +27,15 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <hip/hip_runtime_api.h>
+
 #include <algorithm>
+#include <chrono>
 #include <climits>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
 
 #include "session_shards.h"
 
@@ -60,23 +67,64 @@ void same_len(int64_t n, std::initializer_list<int64_t> sizes) {
     if (s != n) throw std::invalid_argument("length mismatch");
 }
 
+// The GPU operator's idle-key eviction, off the interpreter (the per-eviction
+// Python thread): a persistent C++ worker owned by the store. spill_submit() records a HIP event
+// behind the counted D2H of the evicted rows and queues the job; the worker waits for the event
+// (blocking sync, no spin), classifies the rows and inserts the hot ones under the store lock,
+// copies the cold rows into a chunk WITHOUT the lock, publishes the chunk and expires dead cold
+// chunks under the lock again. The main thread never waits for the cold copy: fire() waits only
+// for the hot phase of every submitted job (rows that may still fire must be in the map), and
+// the calls that read cold rows (extract, snapshot, key counts, ...) join the worker first.
+// Results (rows, evicted slots, keys, released keys) are collected by spill_poll / spill_join.
+struct SpillJob {
+  uint64_t id = 0;
+  hipEvent_t ev = nullptr;  // null: the rows are already in host memory (CPU tests)
+  const uint8_t* slab = nullptr;
+  int64_t ctr_off = 0;      // int32 counters: [7] rows written (may exceed R), [8] slots evicted
+  int64_t col_off[6] = {0, 0, 0, 0, 0, 0};  // int64 key, start, end, acc, cnt, flags (R rows)
+  int64_t R = 0;
+  bool expire = false;
+  int64_t expire_wm = INT64_MIN;
+};
+
+struct SpillDone {
+  uint64_t id = 0;
+  int64_t nr = 0, ne = 0, nk = 0;
+  std::vector<int64_t> released;
+  double t_wait = 0, t_hot = 0, t_build = 0, t_publish = 0;  // seconds per phase
+  std::exception_ptr err;
+};
+
 // NumPy adapter of the store core (csrc/session_store.h).
 class SessionStore {
  public:
   // shards > 1: key shards worked in parallel by a persistent pool (csrc/session_shards.h)
   SessionStore(int64_t gap, int64_t lateness, int agg, int shards = 1)
       : c_(gap, lateness, agg, shards) {}
+  ~SessionStore() {
+    if (th_.joinable()) {
+      {
+        std::lock_guard<std::mutex> g(qmu_);
+        stop_ = true;
+      }
+      qcv_.notify_all();
+      th_.join();
+    }
+    for (hipEvent_t e : free_ev_) (void)hipEventDestroy(e);
+  }
   int shards() const { return c_.shards(); }
 
   // Fold a batch (keys, ts, vals) with the current watermark `wm`; returns late-dropped count.
   int64_t process_np(const I64Array& keys, const I64Array& ts, const I64Array& vals, int64_t wm) {
     same_len(keys.size(), {ts.size(), vals.size()});
+    auto g = joined();
     return c_.process(keys.data(), ts.data(), vals.data(), keys.size(), wm);
   }
   // Merge pre-built runs (GPU overflow path): each is a candidate session.
   int64_t merge_runs_np(const I64Array& keys, const I64Array& starts, const I64Array& ends,
                         const I64Array& accs, const I64Array& cnts, int64_t wm) {
     same_len(keys.size(), {starts.size(), ends.size(), accs.size(), cnts.size()});
+    auto g = joined();
     return c_.merge_runs(keys.data(), starts.data(), ends.data(), accs.data(), cnts.data(),
                       keys.size(), wm);
   }
@@ -85,11 +133,13 @@ class SessionStore {
   void insert_np(const I64Array& keys, const I64Array& starts, const I64Array& ends,
                  const I64Array& accs, const I64Array& cnts, const I64Array& flags, bool cold) {
     same_len(keys.size(), {starts.size(), ends.size(), accs.size(), cnts.size(), flags.size()});
+    auto g = joined_nogil();
     c_.insert(keys.data(), starts.data(), ends.data(), accs.data(), cnts.data(), flags.data(),
            keys.size(), cold);
   }
   py::dict extract_np(const I64Array& keys, int64_t wm, int64_t max_sess) {
     std::vector<int64_t> moved;
+    auto g = joined();
     py::dict d = columns_dict(c_.extract(keys.data(), keys.size(), wm, max_sess, &moved));
     d["moved"] = to_np(moved);
     return d;
@@ -102,6 +152,8 @@ class SessionStore {
     std::vector<int64_t> moved, ukey, rec, last;
     {
       py::gil_scoped_release nogil;
+      join_all();
+      std::lock_guard<std::mutex> g(mu_);
       const sess::Columns c = c_.extract(keys.data(), keys.size(), wm, max_sess, &moved);
       const size_t n = c.key.size();
       int64_t pos = 0;
@@ -130,12 +182,18 @@ class SessionStore {
     return d;
   }
   // Fire / clean up everything the watermark allows. Returns columns of emitted rows plus the
-  // keys that left the store ("released").
+  // keys that left the store ("released"). Waits only for the hot phase of queued evictions.
   py::dict fire_np(int64_t wm, std::vector<int32_t> map_code, std::vector<double> map_consts,
                    std::vector<int32_t> f_code, std::vector<double> f_consts, bool expire) {
     sess::SessionCore::FireOut o;
-    c_.fire(wm, sess::SessionCore::prog(map_code.data(), map_code.size(), map_consts.data(), map_consts.size()),
-         sess::SessionCore::prog(f_code.data(), f_code.size(), f_consts.data(), f_consts.size()), o, expire);
+    {
+      py::gil_scoped_release nogil;
+      if (expire) join_all();
+      else wait_hot();
+      std::lock_guard<std::mutex> g(mu_);
+      c_.fire(wm, sess::SessionCore::prog(map_code.data(), map_code.size(), map_consts.data(), map_consts.size()),
+           sess::SessionCore::prog(f_code.data(), f_code.size(), f_consts.data(), f_consts.size()), o, expire);
+    }
     py::dict d;
     d["keys"] = to_np(o.okey);
     d["start"] = to_np(o.ostart);
@@ -147,30 +205,256 @@ class SessionStore {
     d["released"] = to_np(o.released);
     return d;
   }
-  // Cold-chunk expiry alone (GIL released: the GPU operator's spill worker runs it).
+  // Cold-chunk expiry alone (GIL released).
   py::array_t<int64_t> expire_cold_np(int64_t wm) {
     std::vector<int64_t> rel;
     {
-      py::gil_scoped_release nogil;
+      auto g = joined_nogil();
       c_.expire_cold(wm, rel);
     }
     return to_np(rel);
   }
-  py::array_t<int64_t> spill_set_np(int cap_log2) const {
+  py::array_t<int64_t> spill_set_np(int cap_log2) {
     py::array_t<int64_t> out((py::ssize_t)1 << cap_log2);
+    auto g = joined();
     c_.spill_set(cap_log2, out.mutable_data());
     return out;
   }
-  py::array_t<int64_t> key_list_np() const { return to_np(c_.key_list()); }
-  py::dict snapshot_np() const { return columns_dict(c_.snapshot()); }
-  bool contains(uint64_t key) const { return c_.contains(key); }
-  size_t num_keys() const { return c_.num_keys(); }
-  size_t num_sessions() const { return c_.num_sessions(); }
-  size_t num_cold_rows() const { return c_.num_cold_rows(); }
-  size_t bytes() const { return c_.bytes(); }
+  py::array_t<int64_t> key_list_np() {
+    auto g = joined();
+    return to_np(c_.key_list());
+  }
+  py::dict snapshot_np() {
+    auto g = joined();
+    return columns_dict(c_.snapshot());
+  }
+  bool contains(uint64_t key) {
+    auto g = joined();
+    return c_.contains(key);
+  }
+  size_t num_keys() {
+    auto g = joined();
+    return c_.num_keys();
+  }
+  size_t num_sessions() {
+    auto g = joined();
+    return c_.num_sessions();
+  }
+  size_t num_cold_rows() {
+    auto g = joined();
+    return c_.num_cold_rows();
+  }
+  size_t bytes() {
+    auto g = joined();
+    return c_.bytes();
+  }
+
+  // ---- asynchronous eviction (GPU operator) ---------------------------------------------------
+  // stream >= 0: a HIP stream handle whose queued work (the counted D2H into `slab`) must finish
+  // before the rows are read; < 0: the rows are already there. Returns the job id (1, 2, ...).
+  uint64_t spill_submit(int64_t stream, uintptr_t slab, int64_t ctr_off, std::vector<int64_t> col_off,
+                        int64_t R, py::object expire_wm) {
+    if (col_off.size() != 6) throw std::invalid_argument("spill_submit: 6 column offsets");
+    SpillJob j;
+    j.slab = reinterpret_cast<const uint8_t*>(slab);
+    j.ctr_off = ctr_off;
+    for (int k = 0; k < 6; ++k) j.col_off[k] = col_off[k];
+    j.R = R;
+    j.expire = !expire_wm.is_none();
+    if (j.expire) j.expire_wm = expire_wm.cast<int64_t>();
+    py::gil_scoped_release nogil;
+    if (stream >= 0) {
+      {
+        std::lock_guard<std::mutex> g(qmu_);
+        if (!free_ev_.empty()) {
+          j.ev = free_ev_.back();
+          free_ev_.pop_back();
+        }
+      }
+      if (!j.ev && hipEventCreateWithFlags(&j.ev, hipEventDisableTiming | hipEventBlockingSync) !=
+                       hipSuccess)
+        throw std::runtime_error("spill_submit: hipEventCreate failed");
+      if (hipEventRecord(j.ev, reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
+        throw std::runtime_error("spill_submit: hipEventRecord failed");
+    }
+    std::lock_guard<std::mutex> g(qmu_);
+    if (!th_.joinable()) th_ = std::thread([this] { worker(); });
+    j.id = ++submitted_;
+    q_.push_back(j);
+    qcv_.notify_all();
+    return j.id;
+  }
+  uint64_t spill_submitted() const { return submitted_; }
+  uint64_t spill_completed() {
+    std::lock_guard<std::mutex> g(qmu_);
+    return completed_;
+  }
+  // Completed jobs' results (non-blocking); the first failed job's error is raised.
+  py::list spill_poll() { return take_results(); }
+  // Every submitted job completed (GIL released while waiting), then as spill_poll.
+  py::list spill_join() {
+    {
+      py::gil_scoped_release nogil;
+      join_all();
+    }
+    return take_results();
+  }
 
  private:
+  struct Guard {
+    std::unique_lock<std::mutex> lk;
+  };
+  // Join the worker, then hold the store lock for the caller's scope (the GIL is held: for calls
+  // that build Python objects under it; the wait itself releases it).
+  Guard joined() {
+    {
+      py::gil_scoped_release nogil;
+      join_all();
+    }
+    return Guard{std::unique_lock<std::mutex>(mu_)};
+  }
+  Guard joined_nogil() {
+    join_all();
+    return Guard{std::unique_lock<std::mutex>(mu_)};
+  }
+  void join_all() {
+    std::unique_lock<std::mutex> lk(qmu_);
+    dcv_.wait(lk, [&] { return completed_ == submitted_; });
+  }
+  void wait_hot() {
+    std::unique_lock<std::mutex> lk(qmu_);
+    dcv_.wait(lk, [&] { return hot_done_ == submitted_; });
+  }
+  py::list take_results() {
+    std::deque<SpillDone> done;
+    {
+      std::lock_guard<std::mutex> g(qmu_);
+      done.swap(done_);
+    }
+    if (!done.empty()) {
+      // A released key that has hot sessions again (a host fold after the expiry) must stay in
+      // the device spill set: dropped from the list here, under the store lock.
+      py::gil_scoped_release nogil;
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto& d : done) {
+        size_t w = 0;
+        for (int64_t k : d.released)
+          if (!c_.hot((uint64_t)k)) d.released[w++] = k;
+        d.released.resize(w);
+      }
+    }
+    py::list out;
+    std::exception_ptr err;
+    for (auto& d : done) {
+      if (d.err && !err) err = d.err;
+      py::dict r;
+      r["id"] = d.id;
+      r["nr"] = d.nr;
+      r["ne"] = d.ne;
+      r["nk"] = d.nk;
+      r["released"] = to_np(d.released);
+      r["t_wait"] = d.t_wait;
+      r["t_hot"] = d.t_hot;
+      r["t_build"] = d.t_build;
+      r["t_publish"] = d.t_publish;
+      out.append(r);
+    }
+    if (err) std::rethrow_exception(err);
+    return out;
+  }
+  void worker() {
+    using clk = std::chrono::steady_clock;
+    auto sec = [](clk::time_point a, clk::time_point b) {
+      return std::chrono::duration<double>(b - a).count();
+    };
+    for (;;) {
+      SpillJob j;
+      {
+        std::unique_lock<std::mutex> lk(qmu_);
+        qcv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;  // stop_
+        j = q_.front();
+        q_.pop_front();
+      }
+      SpillDone d;
+      d.id = j.id;
+      bool hot_marked = false;
+      try {
+        const auto t0 = clk::now();
+        if (j.ev && hipEventSynchronize(j.ev) != hipSuccess)
+          throw std::runtime_error("spill worker: hipEventSynchronize failed");
+        const auto t1 = clk::now();
+        const int32_t* ctr = reinterpret_cast<const int32_t*>(j.slab + j.ctr_off);
+        const int64_t nr_all = ctr[7];
+        d.ne = ctr[8];
+        int64_t nr = std::min<int64_t>(nr_all, j.R);
+        const int64_t* col[6];
+        for (int k = 0; k < 6; ++k) col[k] = reinterpret_cast<const int64_t*>(j.slab + j.col_off[k]);
+        std::vector<int64_t> tmp[6];
+        if (nr_all > j.R) {  // staging overflowed: rows of skipped slots stay zero (cnt == 0)
+          for (int64_t i = 0; i < nr; ++i)
+            if (col[4][i] > 0)
+              for (int k = 0; k < 6; ++k) tmp[k].push_back(col[k][i]);
+          for (int k = 0; k < 6; ++k) col[k] = tmp[k].data();
+          nr = (int64_t)tmp[0].size();
+        }
+        d.nr = nr;
+        int64_t nk = nr ? 1 : 0;
+        for (int64_t i = 1; i < nr; ++i) nk += col[0][i] != col[0][i - 1];
+        d.nk = nk;
+        sess::SessionCore::ColdPlan plan;
+        sess::SessionCore* one = c_.single();
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          if (nr) {
+            if (one) one->insert_hot(col[0], col[1], col[2], col[3], col[4], col[5], nr, true, plan);
+            else c_.insert(col[0], col[1], col[2], col[3], col[4], col[5], nr, true);
+          }
+        }
+        {
+          std::lock_guard<std::mutex> g(qmu_);
+          hot_done_ = j.id;
+          hot_marked = true;
+        }
+        dcv_.notify_all();
+        const auto t2 = clk::now();
+        if (one && nr) sess::SessionCore::build_cold(col[0], col[1], col[2], col[3], col[4], nr, plan);
+        const auto t3 = clk::now();
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          if (one && nr) one->publish_cold(plan);
+          if (j.expire) c_.expire_cold(j.expire_wm, d.released);
+        }
+        const auto t4 = clk::now();
+        d.t_wait = sec(t0, t1);
+        d.t_hot = sec(t1, t2);
+        d.t_build = sec(t2, t3);
+        d.t_publish = sec(t3, t4);
+      } catch (...) {
+        d.err = std::current_exception();
+      }
+      {
+        std::lock_guard<std::mutex> g(qmu_);
+        if (j.ev) free_ev_.push_back(j.ev);
+        if (!hot_marked) hot_done_ = j.id;
+        completed_ = j.id;
+        done_.push_back(std::move(d));
+      }
+      dcv_.notify_all();
+    }
+  }
+
   sess::ShardedCore c_;
+  std::mutex mu_;  // the store core: the main thread's calls vs the worker's locked phases
+  // worker queue state (qmu_)
+  std::thread th_;
+  std::mutex qmu_;
+  std::condition_variable qcv_, dcv_;
+  std::deque<SpillJob> q_;
+  std::deque<SpillDone> done_;
+  std::vector<hipEvent_t> free_ev_;
+  uint64_t submitted_ = 0, hot_done_ = 0, completed_ = 0;
+  bool stop_ = false;
 };
 
 }  // namespace
@@ -183,8 +467,7 @@ void bind_sessions(py::module_& m) {
            py::arg("agg"), py::arg("shards") = 1)
       .def_property_readonly("shards", &SessionStore::shards)
       .def("process", &SessionStore::process_np)
-      // GIL released: the operator inserts spilled rows from a worker thread while the main
-      // thread keeps launching the next step's kernels (the store is not touched concurrently).
+      // GIL released: the rows are read in place (no Python object is touched).
       .def("insert", &SessionStore::insert_np, py::arg("keys"), py::arg("starts"),
            py::arg("ends"), py::arg("accs"), py::arg("cnts"), py::arg("flags"),
            py::arg("cold") = false, py::call_guard<py::gil_scoped_release>())
@@ -202,5 +485,11 @@ void bind_sessions(py::module_& m) {
       .def("num_cold_rows", &SessionStore::num_cold_rows)
       .def("bytes", &SessionStore::bytes)
       .def("key_list", &SessionStore::key_list_np)
-      .def("snapshot", &SessionStore::snapshot_np);
+      .def("snapshot", &SessionStore::snapshot_np)
+      .def("spill_submit", &SessionStore::spill_submit, py::arg("stream"), py::arg("slab"),
+           py::arg("ctr_off"), py::arg("col_off"), py::arg("rows"), py::arg("expire_wm") = py::none())
+      .def("spill_submitted", &SessionStore::spill_submitted)
+      .def("spill_completed", &SessionStore::spill_completed)
+      .def("spill_poll", &SessionStore::spill_poll)
+      .def("spill_join", &SessionStore::spill_join);
 }

@@ -39,6 +39,10 @@ class Comm:
     def barrier(self) -> None:
         pass
 
+    def broadcast_(self, t: torch.Tensor, src: int = 0) -> None:
+        """In place: every rank's `t` (same shape and dtype everywhere) becomes rank src's."""
+        return None
+
     def broadcast_object(self, obj, src: int = 0):
         return obj
 
@@ -197,6 +201,16 @@ class LoopbackComm(Comm):
         if self.world > 1:
             self.group_obj.wait()
 
+    def broadcast_(self, t, src: int = 0):
+        if self.world == 1:
+            return
+        self._deposit(t)
+        if self.rank != src:
+            peer = self._read(src, t)
+            t.copy_(peer)
+        self._mark_read(src, t)
+        self._finish(t)
+
     def broadcast_object(self, obj, src: int = 0):
         if self.world == 1:
             return obj
@@ -216,6 +230,23 @@ class LoopbackComm(Comm):
         v = list(g._slots)
         g.wait()
         return v
+
+
+I64_MIN, I64_MAX = -(1 << 63), (1 << 63) - 1
+
+
+def control_reduce(comm: Comm, mins: list[int] = (), maxs: list[int] = ()) -> tuple[list, list]:
+    """The host control plane's one collective: a packed int64 MIN all-reduce of small integers
+    (flags, clocks, watermarks). MAX words travel negated (I64_MIN clamps to I64_MIN + 1, so its
+    negation fits). One CPU tensor over the control group (gloo) or the loopback ranks -- no
+    pickling, a fixed 8 bytes per word."""
+    mins, maxs = [int(x) for x in mins], [int(x) for x in maxs]
+    if comm is None or comm.world == 1:
+        return mins, maxs
+    t = torch.tensor(mins + [-max(x, I64_MIN + 1) for x in maxs], dtype=torch.int64)
+    comm.allreduce_min_(t)
+    v = t.tolist()
+    return v[:len(mins)], [-x for x in v[len(mins):]]
 
 
 def run_loopback(world: int, fn, *args, device: torch.device | None = None,
@@ -308,6 +339,10 @@ class TorchComm(Comm):
             else:
                 dist.barrier(group=self.group)
 
+    def broadcast_(self, t, src: int = 0):
+        if self.world > 1:
+            dist.broadcast(t, src=src, group=self.group)
+
     def broadcast_object(self, obj, src: int = 0):
         lst = [obj]
         dist.broadcast_object_list(lst, src=src, group=self.group)
@@ -343,3 +378,16 @@ def init_distributed(device: str = "auto", timeout_s: int = 600) -> Comm:
             kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(**kw)
     return TorchComm()
+
+
+def shutdown_distributed(comm: Comm | None = None) -> None:
+    """Orderly end of a multi-process run: a barrier on every rank, then the process groups are
+    destroyed. Without it the first rank to exit closes its gloo sockets while a slower peer may
+    still be completing the last collective; gloo's transport thread then sees the reset
+    connection and aborts that peer (SIGABRT: the round-4 2-rank records bench under load)."""
+    if not dist.is_initialized():
+        return
+    if comm is not None and comm.world > 1:
+        comm.barrier()
+    dist.barrier()
+    dist.destroy_process_group()

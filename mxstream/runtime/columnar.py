@@ -302,6 +302,13 @@ class TextParseOp(Operator):
                 self.collective = True
 
                 def agree(local, ctrl=ctrl):
+                    # Steady state (no rank met a new string): one packed int64 all-reduce and
+                    # no pickling; the strings themselves move only on passes that have some.
+                    from ..parallel.comm import control_reduce
+
+                    _, (nmax,) = control_reduce(ctrl, maxs=[len(local)])
+                    if nmax == 0:
+                        return []
                     seen, out = set(), []
                     for lst in ctrl.all_gather_object(local):
                         for b in lst:

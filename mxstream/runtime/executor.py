@@ -272,19 +272,29 @@ class Executor:
     def _control(self, want_ckpt: bool) -> bool:
         """End-of-step agreement between ranks: a failure anywhere fails every rank (the
         restart strategy then restarts all of them from the same checkpoint), and a checkpoint
-        is taken when any rank's interval elapsed (ranks' clocks need not agree)."""
+        is taken when any rank's interval elapsed (ranks' clocks need not agree). Multi-rank:
+        one packed int64 all-reduce (control_reduce); the failure text moves only when a rank
+        failed."""
         if self.comm is None:
             return want_ckpt
-        got = self.comm.all_gather_object(
-            (bool(want_ckpt), None if self._failure is None else
-             f"{type(self._failure).__name__}: {self._failure}"))
-        failed = [(r, f) for r, (_, f) in enumerate(got) if f is not None]
+        from ..parallel.comm import control_reduce
+
+        _, (want, failed) = control_reduce(self.comm, maxs=[int(want_ckpt),
+                                                            int(self._failure is not None)])
         if failed:
-            if self._failure is not None:
-                raise self._failure
-            raise JobExecutionException(f"Job '{self.job_name}' failed on rank(s) "
-                                        f"{[r for r, _ in failed]}: {failed[0][1]}")
-        return any(w for w, _ in got)
+            self._raise_agreed_failure()
+        return bool(want)
+
+    def _raise_agreed_failure(self) -> None:
+        """Some rank failed (agreed by the control all-reduce): gather the failure texts (the
+        only object collective of the control plane) and fail every rank."""
+        got = self.comm.all_gather_object(None if self._failure is None else
+                                          f"{type(self._failure).__name__}: {self._failure}")
+        failed = [(r, f) for r, f in enumerate(got) if f is not None]
+        if self._failure is not None:
+            raise self._failure
+        raise JobExecutionException(f"Job '{self.job_name}' failed on rank(s) "
+                                    f"{[r for r, _ in failed]}: {failed[0][1] if failed else '?'}")
 
     # ---- multi-rank exchange ---------------------------------------------------------------
     def _exchange(self, n: Transformation, items: list) -> list:
@@ -332,21 +342,34 @@ class Executor:
 
     def _merge_watermarks(self, n: Transformation, last_wm, got_wms=None) -> list:
         """Watermarks across a keyed edge: the minimum over the ranks of the latest watermark
-        each one has sent (Flink's StatusWatermarkValve over the input channels). Collective when
-        `got_wms` is not given."""
+        each one has sent (Flink's StatusWatermarkValve over the input channels). Without
+        `got_wms` (device-exchange edges) this is collective: each rank keeps the max of what it
+        sent and one MIN all-reduce of (sent anything?, that max) gives the valve's minimum."""
         world = self.comm.world
         if got_wms is None:
-            got_wms = self.comm.all_gather_object(last_wm)
-        seen = self._wm_in.setdefault(n.id, [None] * world)
-        for r, w in enumerate(got_wms):
-            if w is not None:
-                seen[r] = w if seen[r] is None else max(seen[r], w)
-        if all(w is not None for w in seen):
+            from ..parallel.comm import I64_MIN, control_reduce
+
+            mine = self._wm_in.get((n.id, "self"))
+            if last_wm is not None:
+                mine = last_wm if mine is None else max(mine, last_wm)
+                self._wm_in[(n.id, "self")] = mine
+            (has, low), _ = control_reduce(self.comm, mins=[int(mine is not None),
+                                                            I64_MIN if mine is None else mine])
+            if not has:
+                return []
+            wm = low
+        else:
+            seen = self._wm_in.setdefault(n.id, [None] * world)
+            for r, w in enumerate(got_wms):
+                if w is not None:
+                    seen[r] = w if seen[r] is None else max(seen[r], w)
+            if not all(w is not None for w in seen):
+                return []
             wm = min(seen)
-            prev = self._wm_in.get((n.id, "emitted"))
-            if prev is None or wm > prev:
-                self._wm_in[(n.id, "emitted")] = wm
-                return [WM(wm)]
+        prev = self._wm_in.get((n.id, "emitted"))
+        if prev is None or wm > prev:
+            self._wm_in[(n.id, "emitted")] = wm
+            return [WM(wm)]
         return []
 
     def _op_clock(self) -> int:
@@ -356,24 +379,40 @@ class Executor:
             return self.clock()
         return self._step_now
 
-    def _step_begin(self, finished: dict, sources: list, manual: bool) -> tuple[bool, int]:
-        """(every source finished on every rank, the step's processing time). Multi-rank: one
-        gather of (done, clock) -- the step's time is the MAX over the ranks' clocks (a manual
-        clock advances to it), the agreement processing-time windows fire on."""
+    def _step_begin(self, finished: dict, sources: list, manual: bool,
+                    want_ckpt: bool = False) -> tuple[bool, int]:
+        """(every source finished on every rank, the step's processing time). Multi-rank: ONE
+        packed int64 all-reduce per pass (parallel/comm.control_reduce) carries done (MIN),
+        the clock (MAX: the step's time, which a manual clock advances to), and the previous
+        pass's control words -- checkpoint request and failure flag (MAX). A failure fails
+        every rank here; a requested checkpoint is taken here, at the cut between the previous
+        pass and this one, before the clock moves."""
+        nxt_t = None
         if manual:
             nxt = [self.ops[n.id].next_event_time() for n in sources if not finished[n.id]]
             nxt = [t for t in nxt if t is not None]
             if nxt:
-                self.clock.advance_to(min(nxt))
-        done, now = all(finished.values()), self.clock()
+                nxt_t = min(nxt)
+        done = all(finished.values())
         if self.comm is None:
-            return done, now
-        got = self.comm.all_gather_object((done, now))
-        now = max(t for _, t in got)
+            if nxt_t is not None:
+                self.clock.advance_to(nxt_t)
+            return done, self.clock()
+        from ..parallel.comm import control_reduce
+
+        now = self.clock() if nxt_t is None else max(self.clock(), nxt_t)
+        (all_done,), (now, want, failed) = control_reduce(
+            self.comm, mins=[int(done)],
+            maxs=[now, int(want_ckpt), int(self._failure is not None)])
+        if failed:
+            self._raise_agreed_failure()
+        if want:
+            self._checkpoint(finished)
+            self._last_ckpt = self.clock()
         if manual:
             self.clock.advance_to(now)
         self._step_now = now
-        return all(d for d, _ in got), now
+        return bool(all_done), now
 
     # ---- checkpoints ---------------------------------------------------------------------
     def _storage(self):
@@ -515,7 +554,7 @@ class Executor:
             done = self._storage().completed_checkpoints()
             if done:
                 self._next_ckpt = int(done[-1].name[4:]) + 1
-        last_ckpt = self.clock()
+        self._last_ckpt = self.clock()
         reporter = self._reporter()
         cfg_x = self.env.config
         trace_path = getattr(cfg_x, "trace_path", None)
@@ -526,8 +565,9 @@ class Executor:
         if getattr(cfg_x, "step_timeout_ms", 0) and cfg_x.step_timeout_ms > 0:
             wd = Watchdog(cfg_x.step_timeout_ms, name=self.job_name).start()
         try:
+            want = False
             while True:
-                done, now = self._step_begin(finished, sources, manual)
+                done, now = self._step_begin(finished, sources, manual, want)
                 if done:
                     break
                 inbox: dict = {}
@@ -544,10 +584,13 @@ class Executor:
                 self._push(inbox, now)
                 if wd is not None:
                     wd.beat()
-                want = cfg.is_checkpointing_enabled() and self.clock() - last_ckpt >= cfg.interval_ms
-                if self._control(want):
+                want = (cfg.is_checkpointing_enabled()
+                        and self.clock() - self._last_ckpt >= cfg.interval_ms)
+                if self.comm is None and want:
                     self._checkpoint(finished)
-                    last_ckpt = self.clock()
+                    self._last_ckpt = self.clock()
+                    want = False
+                # (multi-rank: the request and any failure are agreed at the next _step_begin)
                 if reporter is not None:
                     reporter.maybe_report(job=self.job_name)
             # End of input: MAX watermark (event time), then operators' finish hooks.

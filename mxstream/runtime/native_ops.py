@@ -1388,7 +1388,23 @@ class NativeVectorWindowOp(NativeWindowOp):
                     raise TypeError("unsupported key type for the native path")
         except TypeError as e:
             err = str(e)
-        got = self.comm.all_gather_object((new, vlen, kind, err))
+        # Steady state (no new key string, no error, the known vector length and key kind on
+        # every rank): one packed int64 all-reduce; the object gather runs only otherwise.
+        from ..parallel.comm import control_reduce
+
+        kc = {"str": 1, "int": 2}.get(kind, 0)
+        vl = -1 if vlen is None else vlen
+        (vmin, kmin), (nnew, bad, vmax, kmax) = control_reduce(
+            self.comm, mins=[vl if vl >= 0 else (1 << 62), kc or 3],
+            maxs=[len(new), int(err is not None), vl, kc])
+        known_k = None if self.str_keys is None else (1 if self.str_keys else 2)
+        quiet = (nnew == 0 and not bad and getattr(self, "_vjh_t", None) is not None
+                 and (vmax < 0 or (self.op is not None and vmin == vmax == self.vlen))
+                 and (kmax == 0 or (kmin == kmax == known_k)))
+        if quiet:
+            got = [([], None, None, None)]
+        else:
+            got = self.comm.all_gather_object((new, vlen, kind, err))
         errs = [e for *_, e in got if e]
         if errs:
             raise TypeError(f"native vector window at G > 1: {errs[0]}")

@@ -32,7 +32,6 @@ from __future__ import annotations
 
 import contextlib
 import math
-import threading
 import time
 from collections import defaultdict
 from dataclasses import dataclass, field
@@ -66,21 +65,6 @@ _STORE_SHARDS = int(__import__("os").environ.get("MXS_SESSION_SHARDS", "1"))
 # compute stream ("0", A/B: the side-stream launch cost the host 1.2 ms per step at config 5
 # while the GPU was busy, against 26 us on an idle GPU -- scripts/d2h_launch_bench.py).
 _SPILL_SIDE_STREAM = __import__("os").environ.get("MXS_SPILL_SIDE_STREAM", "1") != "0"
-
-
-class _OneSlab:
-    """The session eviction's pinned slab (PinnedSlabPool interface): handed out again for every
-    eviction once the previous one's worker has been joined."""
-
-    def __init__(self, t, arr, allocs: int):
-        self.slab, self.allocs = (t, arr), allocs
-
-    def take(self, nbytes: int):
-        if nbytes > self.slab[0].numel():
-            t = torch.empty(_next_pow2(nbytes), dtype=torch.uint8, pin_memory=True)
-            self.slab = (t, t.numpy())
-            self.allocs += 1
-        return self.slab
 
 
 def _next_pow2(x: int) -> int:
@@ -191,7 +175,6 @@ class KeyedSessionOperator:
             self.spill_rows = int(spill_rows)
             self.st_rows = torch.empty(6 * self.spill_rows, dtype=torch.int64, device=dev)
             self._pin_rows = torch.empty((6, self.spill_rows), dtype=torch.int64).pin_memory()
-            self._spill_thread = None
             # A fire can close every resident session of every slot (end of input: all kSess).
             self.ocap = (int(emit_capacity or max(self.nslots * K_SESS, 1 << 16)) + 3) & ~3
             self.out_key = torch.empty(self.ocap, dtype=torch.int64, device=dev)
@@ -417,8 +400,7 @@ class KeyedSessionOperator:
             with self._phase("fire_gpu"):
                 pending = self._fire_gpu_launch(wm)
         with self._phase("fire_host"):
-            if self.gpu:
-                self._join_spill()
+            # (the store's fire waits for the hot phase of queued eviction jobs itself)
             host_rows = self._fire_host(wm)
         if pending is not None:
             with self._phase("fire_gpu"):
@@ -763,8 +745,22 @@ class KeyedSessionOperator:
     def _evict(self, *, slots: torch.Tensor | None = None, idle_before: int = I64_MIN) -> None:
         """Pack slots (listed, or idle since before `idle_before`) into staging rows and
         tombstone them; the rows go to the host store. For idle evictions the host-store insert
-        runs on a worker thread while the next step's kernels run."""
-        self._join_spill()
+        runs on the store's C++ worker while the next step's kernels run."""
+        if slots is not None or not self.gpu:
+            self._join_spill()
+        else:
+            # The previous job's results (its released keys leave the device spill set) are
+            # applied before this eviction adds keys to the set: stream order of erase and add.
+            self._poll_spill()
+            if self.store.spill_completed() < self.store.spill_submitted():
+                with self._phase("spill.wait_prev"):
+                    self._join_spill()
+        prev = getattr(self, "_spill_copy_done", None)
+        if prev is not None:
+            # The staging rows and counters are rewritten below: after the previous eviction's
+            # counted copy has read them (a stream wait, no host block).
+            torch.cuda.current_stream(self.device).wait_event(prev)
+            self._spill_copy_done = None
         m, st, c = self.native, self._st(), self.ctr
         with self._phase("spill.capacity"):
             self._ensure_spill_capacity(slots.numel() if slots is not None
@@ -795,7 +791,6 @@ class KeyedSessionOperator:
         self._live_estimate -= ne
         self._tombs_bound += ne
         nr = min(nr_all, R)
-        cold = slots is None  # idle keys: fired-and-unmodified sessions go to a cold chunk
         if not nr:
             self._apply_spill((0, ne))
             return
@@ -813,88 +808,48 @@ class KeyedSessionOperator:
                 h = [np.ascontiguousarray(x[ok]) for x in h]
             return h
 
-        if not cold:
-            torch.cuda.current_stream(self.device).synchronize()
-            self.phase_s["spill.d2h"] += time.perf_counter() - t0
-            h = host_rows()
-            nk = int(np.count_nonzero(h[0][1:] != h[0][:-1])) + 1 if len(h[0]) else 0
-            self._apply_spill((nk, ne))
-            if len(h[0]):
-                self.store.insert(h[0], h[1], h[2], h[3], h[4], h[5], False)
-            return
-        # Idle eviction: the copy completes on the stream while the step goes on; a worker
-        # thread waits for it (event) and inserts into the host store (C++, GIL released),
-        # overlapping the next step's GPU work; joined before the store is used again. The
-        # spill-set occupancy takes the row count now (an upper bound of the keys).
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        self.set_used += nr
-        self.metrics.freed_slots += ne
-        self._spill_err = None
-
-        def work():
-            try:
-                t0 = time.perf_counter()
-                ev.synchronize()
-                h = host_rows()
-                t1 = time.perf_counter()
-                self.phase_s["spill.d2h_wait"] += t1 - t0
-                self.metrics.spilled_keys += (int(np.count_nonzero(h[0][1:] != h[0][:-1])) + 1
-                                              if len(h[0]) else 0)
-                if len(h[0]):
-                    self.store.insert(h[0], h[1], h[2], h[3], h[4], h[5], True)
-                self.phase_s["spill.host_insert"] += time.perf_counter() - t1
-            except BaseException as e:  # re-raised by _join_spill
-                self._spill_err = e
-
-        self._spill_thread = threading.Thread(target=work, name="mxs-spill", daemon=True)
-        self._spill_thread.start()
+        torch.cuda.current_stream(self.device).synchronize()
+        self.phase_s["spill.d2h"] += time.perf_counter() - t0
+        h = host_rows()
+        nk = int(np.count_nonzero(h[0][1:] != h[0][:-1])) + 1 if len(h[0]) else 0
+        self._apply_spill((nk, ne))
+        if len(h[0]):
+            self.store.insert(h[0], h[1], h[2], h[3], h[4], h[5], False)
 
     def _evict_async(self, rows: torch.Tensor, R: int, expire_wm: int | None = None) -> None:
-        from .window_operator import CountedHostRows, PinnedSlabPool
+        """The evicted rows' counted D2H into one of two pinned slabs on the copy stream, then
+        a job for the store's persistent C++ worker (csrc/sessions.cpp SessionStore.spill_submit):
+        it waits for the copy's HIP event, inserts the rows and expires dead cold chunks with no
+        GIL and no Python thread. Its results are applied when polled (_apply_spill_results)."""
+        from .window_operator import CountedHostRows
 
-        if getattr(self, "_spill_pool", None) is None:
-            self._spill_pool = PinnedSlabPool(max_slabs=2)
+        if getattr(self, "_spill_slabs", None) is None:
+            self._spill_slabs = [[None, None, 0], [None, None, 0]]  # tensor, array, job id
+            self._spill_turn = 0
             self._spill_stream = torch.cuda.Stream(self.device)
+            self._spill_allocs = 0
+        slab = self._spill_slabs[self._spill_turn]
+        self._spill_turn ^= 1
+        if slab[2] > self.store.spill_completed():
+            self._join_spill()  # that slab's rows are still being read by the worker
+
+        class _Slab:  # PinnedSlabPool interface over this one slab (grows when too small)
+            def take(_, nbytes):
+                if slab[0] is None or slab[0].numel() < nbytes:
+                    t = torch.empty(_next_pow2(nbytes), dtype=torch.uint8, pin_memory=True)
+                    slab[0], slab[1] = t, t.numpy()
+                    self._spill_allocs += 1
+                return slab[0], slab[1]
+
         with self._phase("spill.async_launch.copy"):
-            hr = CountedHostRows(self._spill_pool, [rows[j] for j in range(6)], self.ctr[7:8],
-                                 [self.ctr],
+            hr = CountedHostRows(_Slab(), [rows[j] for j in range(6)], self.ctr[7:8], [self.ctr],
                                  copy_stream=self._spill_stream if _SPILL_SIDE_STREAM else None)
-        self.metrics.extra["spill_slab_allocs"] = self._spill_pool.allocs
-        self.phase_s["spill.async_launch.copy.take"] += hr.t_take
-        self.phase_s["spill.async_launch.copy.launch"] += hr.t_launch
-        if not isinstance(self._spill_pool, _OneSlab):
-            # One eviction copy is in flight at a time (each is joined before the next is
-            # launched): its slab is reused as is, without the pool's free-slab search.
-            self._spill_pool = _OneSlab(hr.t, hr.arr, self._spill_pool.allocs)
-        self._spill_err = None
-        self._spill_res = None
-
-        def work():
-            try:
-                t0 = time.perf_counter()
-                hr.ev.synchronize()
-                f = hr.fixed(0)
-                nr_all, ne = int(f[7]), int(f[8])
-                nr = min(nr_all, R)
-                h = hr.columns(nr)
-                if nr_all > R:  # staging overflowed: rows of skipped slots stay zero (cnt == 0)
-                    ok = h[4] > 0
-                    h = [np.ascontiguousarray(x[ok]) for x in h]
-                t1 = time.perf_counter()
-                self.phase_s["spill.d2h_wait"] += t1 - t0
-                nk = int(np.count_nonzero(h[0][1:] != h[0][:-1])) + 1 if len(h[0]) else 0
-                if len(h[0]):
-                    self.store.insert(h[0], h[1], h[2], h[3], h[4], h[5], True)
-                # keys of expired cold chunks leave the device spill set at the join
-                rel = self.store.expire_cold(expire_wm) if expire_wm is not None else None
-                self.phase_s["spill.host_insert"] += time.perf_counter() - t1
-                self._spill_res = (nr, ne, nk, rel)
-            except BaseException as e:  # re-raised by _join_spill
-                self._spill_err = e
-
-        self._spill_thread = threading.Thread(target=work, name="mxs-spill", daemon=True)
-        self._spill_thread.start()
+        self.metrics.extra["spill_slab_allocs"] = self._spill_allocs
+        self._spill_copy_done = hr.done
+        st = self._spill_stream if _SPILL_SIDE_STREAM else torch.cuda.current_stream(self.device)
+        slab[2] = self.store.spill_submit(st.cuda_stream, hr.t.data_ptr(), hr.fixed_meta[0][0],
+                                          [off for off, _ in hr.cols_meta], R, expire_wm)
+        self.metrics.extra["spill_jobs"] = self.metrics.extra.get("spill_jobs", 0) + 1
 
     def _apply_spill(self, res: tuple[int, int]) -> None:
         nk, ne = res
@@ -903,27 +858,33 @@ class KeyedSessionOperator:
         self.metrics.freed_slots += ne
 
     def _join_spill(self) -> None:
-        t = getattr(self, "_spill_thread", None)
-        if t is None:
+        """Wait for every queued eviction job of the store's worker and apply the results."""
+        if not self.gpu or self.store.spill_submitted() == 0:
             return
         with self._phase("spill.join"):
-            t.join()
-        self._spill_thread = None
-        if self._spill_err is not None:
-            raise self._spill_err
-        res = getattr(self, "_spill_res", None)
-        if res is not None:  # counts of an asynchronous idle eviction
-            self._spill_res = None
-            nr, ne, nk, rel = res
-            if rel is not None and len(rel) and self.spill_any:
+            res = self.store.spill_join()
+        self._apply_spill_results(res)
+
+    def _poll_spill(self) -> None:
+        """Apply the results of eviction jobs the worker has finished (no wait)."""
+        if self.gpu and self.store.spill_submitted():
+            self._apply_spill_results(self.store.spill_poll())
+
+    def _apply_spill_results(self, res: list) -> None:
+        for r in res:
+            rel = r["released"]
+            if len(rel) and self.spill_any:
+                # keys of expired cold chunks leave the device spill set
                 kt = torch.from_numpy(rel).to(self.device)
                 self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
                                           kt.data_ptr(), kt.numel(), self._st())
-            self._live_estimate -= ne
-            self._tombs_bound += ne
-            self.set_used += nr
-            self.metrics.freed_slots += ne
-            self.metrics.spilled_keys += nk
+            self._live_estimate -= r["ne"]
+            self._tombs_bound += r["ne"]
+            self.set_used += r["nr"]
+            self.metrics.freed_slots += r["ne"]
+            self.metrics.spilled_keys += r["nk"]
+            for k in ("wait", "hot", "build", "publish"):  # the worker's own phase times
+                self.phase_s[f"spill.worker.{k}"] += r[f"t_{k}"]
 
     def _ensure_spill_capacity(self, extra: int) -> None:
         """Keep the device spill set (live keys + tombstones) at most half full after `extra`
@@ -1012,6 +973,7 @@ class KeyedSessionOperator:
         def due(live, occupied):
             return occupied > 0.8 * self.nslots and occupied - live > 0.08 * self.nslots
 
+        self._poll_spill()
         t_occ = time.perf_counter()
 
         if self._occ_exact:
@@ -1044,7 +1006,8 @@ class KeyedSessionOperator:
             # live session are simply freed).
             self._evict(idle_before=wm - self.idle_spill_ms)
         # Store empty again: clear the device set (drops its tombstones) and skip set probes.
-        if self.spill_any and self._spill_thread is None and self.store.num_keys() == 0:
+        if (self.spill_any and self.store.spill_completed() == self.store.spill_submitted()
+                and self.store.num_keys() == 0):
             self.spill_set.fill_(EMPTY_KEY)
             self.set_used = 0
             self.spill_any = False

@@ -484,11 +484,17 @@ class SocketTextSource(Source):
         pass, so all ranks also learn end-of-stream on the same pass)."""
         from .columnar import TextBatch
 
+        import torch
+
         world, rank = self.comm.world, self.comm.rank
-        msg = None
+        # Header (int64): eof, error flag, then each rank's chunk length; then the chunks as one
+        # uint8 tensor. Two tensor broadcasts, no pickling (the error text alone is an object).
+        head = torch.zeros(2 + world, dtype=torch.int64)
+        payload = b""
+        err = None
         if rank == 0:
             data, n, eof, err = self.reader.poll(self.max_lines, self.poll_timeout_ms)
-            chunks = [b""] * world
+            cuts = [0] * (world + 1)
             if n:
                 data = bytes(data)
                 cuts = [0]
@@ -497,11 +503,22 @@ class SocketTextSource(Source):
                     j = data.find(b"\n", c - 1) if c > 0 else -1
                     cuts.append(len(data) if j < 0 else j + 1)
                 cuts.append(len(data))
-                chunks = [data[cuts[r]:cuts[r + 1]] for r in range(world)]
-            msg = (chunks, bool(eof), err)
-        chunks, eof, err = self.comm.broadcast_object(msg, src=0)
-        if err:
-            raise ConnectionError(err)
+                payload = data
+            head[0], head[1] = int(bool(eof)), int(bool(err))
+            head[2:] = torch.tensor([cuts[r + 1] - cuts[r] for r in range(world)])
+        self.comm.broadcast_(head, src=0)
+        eof, has_err = bool(head[0]), bool(head[1])
+        if has_err:
+            raise ConnectionError(self.comm.broadcast_object(err, src=0))
+        lens = head[2:].tolist()
+        total = sum(lens)
+        chunks = [b""] * world
+        if total:
+            buf = (torch.frombuffer(bytearray(payload), dtype=torch.uint8) if rank == 0
+                   else torch.empty(total, dtype=torch.uint8))
+            self.comm.broadcast_(buf, src=0)
+            off = sum(lens[:rank])
+            chunks[rank] = buf[off:off + lens[rank]].numpy().tobytes()
         mine = chunks[rank]
         if not mine:
             return [], eof

@@ -17,6 +17,12 @@ def _port():
     return p
 
 
+def _ranks_stderr(r):
+    """Both ranks' stderr as torchrun relayed it (faulthandler stacks of an aborting rank
+    included) -- not just the launcher's summary at the end."""
+    return f"rc={r.returncode}\n--- stderr ---\n{r.stderr[-20000:]}\n--- stdout ---\n{r.stdout[-4000:]}"
+
+
 def test_bench_two_ranks_gloo():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
@@ -24,7 +30,7 @@ def test_bench_two_ranks_gloo():
            "--warmup", "1"]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _ranks_stderr(r)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 prints one JSON line
     d = json.loads(lines[0])
@@ -45,7 +51,7 @@ def test_bench_two_ranks_records_exchange():
            "--warmup", "1", "--exchange", "records"]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
-    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.returncode == 0, _ranks_stderr(r)
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
     assert d["config"]["exchange"] == "records" and d["config"]["keyed_state"] == "hashed"
     assert d["alerts"] > 0 and "records_events_per_s" not in d

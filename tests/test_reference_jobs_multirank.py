@@ -167,6 +167,73 @@ def test_gpu_reference_job_loopback_ranks(name, world, gpu_device, monkeypatch):
     _check(name, ref, got, seen)
 
 
+def _object_spy(comm_cls, executor_cls):
+    """Counts pickled (object) collectives per executor pass: returns the per-pass list of one
+    rank (a pass = one Executor._push)."""
+    import threading
+
+    passes = {}
+    orig_push = executor_cls._push
+
+    def push(self, inbox, now):
+        passes.setdefault(threading.get_ident(), []).append(0)
+        return orig_push(self, inbox, now)
+
+    def wrap(name):
+        orig = getattr(comm_cls, name)
+
+        def f(self, *a, **k):
+            lst = passes.get(threading.get_ident())
+            if lst:
+                lst[-1] += 1
+            return orig(self, *a, **k)
+
+        return orig, f
+
+    saved = {}
+    for nm in ("all_gather_object", "broadcast_object"):
+        saved[nm], f = wrap(nm)
+        setattr(comm_cls, nm, f)
+    executor_cls._push = push
+
+    def undo():
+        executor_cls._push = orig_push
+        for nm, o in saved.items():
+            setattr(comm_cls, nm, o)
+
+    return passes, undo
+
+
+def _steady_state_quiet(per_pass):
+    """Object collectives only while the ranks still meet new dictionary strings (the first
+    passes): the second half of the job's passes has none."""
+    assert len(per_pass) >= 2, per_pass
+    tail = per_pass[len(per_pass) // 2:]
+    assert sum(tail) == 0, per_pass
+
+
+@pytest.mark.parametrize("name", list(JOBS))
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_control_plane_has_no_object_collectives(name, world):
+    """The executor's control plane at G > 1 (done flag, clock, checkpoint request, failure flag,
+    watermark valve of device-exchange edges) is a packed int64 all-reduce: after the dictionary
+    has settled, a pass makes no pickled all_gather_object / broadcast_object (VERDICT r4 #4)."""
+    from mxstream.parallel.comm import LoopbackComm, run_loopback
+    from mxstream.runtime import executor as X
+
+    passes, undo = _object_spy(LoopbackComm, X.Executor)
+    try:
+        res = run_loopback(world, lambda comm: _run(name, comm))
+    finally:
+        undo()
+    ref, _, _ = _run(name)
+    got = [l for out, _, _ in res for l in out]
+    _check(name, ref, got, {"recs": 0, "device": [True]})
+    assert len(passes) == world
+    for per_pass in passes.values():
+        _steady_state_quiet(per_pass)
+
+
 def _gloo_worker(rank, world, port, name, q):
     import os
 
@@ -186,7 +253,11 @@ def _gloo_worker(rank, world, port, name, q):
             return out
 
         X.Executor._exchange = spy
+        from mxstream.parallel.comm import TorchComm
+
+        passes, _ = _object_spy(TorchComm, X.Executor)
         out, _, _ = _run(name)
+        seen["passes"] = next(iter(passes.values()), [])
         q.put((rank, out, seen, None))
     except Exception:  # noqa: BLE001
         import traceback
@@ -228,6 +299,7 @@ def test_reference_job_gloo_processes(name):
     assert Counter(got) == Counter(ref)
     for _, _, seen, _ in res:
         assert seen["recs"] == 0 and seen["device"] and all(seen["device"])
+        _steady_state_quiet(seen["passes"])
 
 
 def _drift_lines(n=60000, channels=30000):

@@ -307,6 +307,111 @@ def test_store_insert_hot_cold_split_follows_row_order():
     assert st_.num_keys() == n // 2 + n // 4  # hot keys + cold rows (one per cold key here)
 
 
+def _slab(cols, R, overflow=0):
+    """A pinned-slab image as the GPU eviction's counted copy lays it out: int32 counters
+    ([7] rows written, [8] slots evicted) in the first 256 bytes, then six int64 columns of R
+    rows each (256-byte aligned)."""
+    n = len(cols[0])
+    a8 = (R * 8 + 255) & ~255
+    buf = np.zeros(256 + 6 * a8, dtype=np.uint8)
+    ctr = buf[:64].view(np.int32)
+    ctr[7], ctr[8] = n + overflow, n // 2 + 1
+    offs = []
+    for j, c in enumerate(cols):
+        off = 256 + j * a8
+        buf[off:off + n * 8].view(np.int64)[:] = c
+        offs.append(off)
+    return buf, offs
+
+
+@pytest.mark.parametrize("shards", [1, 4])
+def test_store_async_spill_worker_equals_insert(shards):
+    """The asynchronous eviction (SessionStore.spill_submit: the persistent C++ worker reads the
+    slab, inserts hot rows under the lock, builds the cold chunk outside it, expires) leaves the
+    store exactly as the synchronous cold insert + expire_cold: same firings (fire waits only
+    for the hot phase), same released keys, same snapshot; a staging overflow keeps only rows
+    with cnt > 0."""
+    from collections import Counter as Ctr
+
+    from mxstream.ops.native import load
+
+    m = load()
+    rng = np.random.default_rng(3)
+    a = m.SessionStore(100, 500, K.AGG_SUM_I64, shards)
+    b = m.SessionStore(100, 500, K.AGG_SUM_I64, shards)
+    keep = []
+    got_a, got_b, stats = [], [], {"nr": 0, "ne": 0, "nk": 0}
+    for step in range(10):
+        n = 2000
+        ek = np.sort(rng.integers(step * 1000, step * 1000 + 3000, n)).astype(np.int64)
+        es = (step * 400 + (ek % 300)).astype(np.int64)
+        acc = (ek % 7).astype(np.int64)
+        cnt = np.ones_like(ek)
+        flags = np.where(rng.random(n) < 0.9, 1, 0).astype(np.int64)  # 10 % hot rows
+        overflow = 5 if step == 4 else 0
+        if overflow:
+            cnt[::3] = 0  # skipped slots of an overflowed staging buffer
+        cols = [ek, es, es + 100, acc, cnt, flags]
+        wm = step * 400 - 100
+        ok = cnt > 0
+        a.insert(*[np.ascontiguousarray(c[ok]) for c in cols], True)
+        rel_a = a.expire_cold(wm)
+        R = n if overflow else n + 64
+        buf, offs = _slab(cols, R, overflow)
+        keep.append(buf)
+        jid = b.spill_submit(-1, buf.ctypes.data, 0, offs, R, wm)
+        assert jid == step + 1
+        da = a.fire(step * 400, [], [], [], [], False)
+        db = b.fire(step * 400, [], [], [], [], False)
+        got_a.append(Ctr(zip(da["keys"].tolist(), da["start"].tolist(), da["raw"].tolist())))
+        got_b.append(Ctr(zip(db["keys"].tolist(), db["start"].tolist(), db["raw"].tolist())))
+        res = b.spill_join()
+        assert [r["id"] for r in res] == [jid]
+        r = res[0]
+        assert r["nr"] == int(ok.sum()) and r["ne"] == n // 2 + 1
+        assert r["nk"] == len(np.unique(ek[ok]))
+        # The worker's expiry may run before or after this fire (the fire waits for the hot
+        # phase only): a key whose hot sessions the fire cleaned can be reported by both; the
+        # keys that left the store are the same.
+        assert (set(r["released"].tolist()) | set(db["released"].tolist())
+                == set(rel_a.tolist()) | set(da["released"].tolist()))
+        assert b.spill_completed() == b.spill_submitted() == jid
+    assert got_a == got_b and sum(len(x) for x in got_a) > 0
+    sa, sb = a.snapshot(), b.snapshot()
+    key = lambda d: sorted(zip(d["key"].tolist(), d["start"].tolist(), d["acc"].tolist(),  # noqa: E731
+                               d["cnt"].tolist(), d["flags"].tolist()))
+    assert key(sa) == key(sb) and a.num_cold_rows() == b.num_cold_rows() > 0
+
+
+def test_store_async_spill_poll_and_implicit_join():
+    """Results arrive through spill_poll without a wait once the worker is done; every call that
+    reads cold rows (here num_keys, extract) joins the worker first."""
+    import time as _t
+
+    from mxstream.ops.native import load
+
+    m = load()
+    st_ = m.SessionStore(100, 10_000, K.AGG_SUM_I64)
+    bufs = []
+    total = 0
+    for step in range(4):
+        k = np.arange(step * 50_000, (step + 1) * 50_000, dtype=np.int64)
+        one = np.ones_like(k)
+        buf, offs = _slab([k, k, k + 100, k % 5, one, one], len(k))
+        bufs.append(buf)
+        st_.spill_submit(-1, buf.ctypes.data, 0, offs, len(k))
+        total += len(k)
+    assert st_.num_keys() == total  # joined
+    ex = st_.extract(np.array([7, 50_001], dtype=np.int64), 0, 4)
+    assert sorted(ex["key"].tolist()) == [7, 50_001]
+    t0 = _t.time()
+    res = []
+    while len(res) < 4 and _t.time() - t0 < 30:
+        res += st_.spill_poll()
+    assert [r["id"] for r in res] == [1, 2, 3, 4]
+    assert sum(r["nr"] for r in res) == total
+
+
 # ----------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
 @settings(max_examples=15, deadline=None, suppress_health_check=[HealthCheck.too_slow])
