@@ -19,6 +19,7 @@ mkdir -p gpurun_out
 TAG=${1:?tag}
 shift
 expand() {
+  if [[ $1 == *"|"* ]]; then echo "$1"; return; fi
   case "$1" in
     tests) echo "tests|900|python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" ;;
     bench) echo "bench|300|python bench.py --steps 24 --warmup 6" ;;
