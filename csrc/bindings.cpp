@@ -5,6 +5,7 @@
 // kernel never sees an operand whose shape disagrees with its grid.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+#include <hip/hip_runtime_api.h>
 
 #include <cstring>
 #include <stdexcept>
@@ -669,6 +670,17 @@ PYBIND11_MODULE(_mxs_native, m) {
   // (window_operator.to_host_arrays syncs once). copies = [(src, nbytes, dst_offset)].
   m.def("gpu_h2d_async", [](intptr_t dst, intptr_t src, int64_t bytes, intptr_t stream) {
     return gpu::h2d_async((void*)dst, (const void*)src, (size_t)bytes, stream);
+  });
+  // Wait for a HIP event by polling hipEventQuery with the GIL released: the host resumes
+  // within a microsecond of the event (a blocking hipEventSynchronize sleeps in the driver and
+  // wakes tens of microseconds late), and other Python threads (loopback ranks, workers) keep
+  // the interpreter meanwhile -- the Python `while not ev.query()` loop held it. Returns the
+  // hipError_t of the final query (0 = complete).
+  m.def("gpu_event_spin", [](intptr_t ev) {
+    py::gil_scoped_release nogil;
+    hipError_t e;
+    while ((e = hipEventQuery((hipEvent_t)ev)) == hipErrorNotReady) __builtin_ia32_pause();
+    return (int)e;
   });
   m.def("gpu_host_register", [](intptr_t p, int64_t bytes) {
     return gpu::host_register((void*)p, (size_t)bytes);

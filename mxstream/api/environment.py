@@ -341,7 +341,12 @@ class StreamExecutionEnvironment:
         from .planner import plan
 
         sinks = plan(self, list(self._sinks))
-        result = Executor(self, sinks, job_name, restore_from=path).run()
+        comm = getattr(self, "_comm", None)  # injected (LoopbackComm: virtual ranks in tests)
+        if comm is not None:
+            self.rank, self.world = comm.rank, comm.world
+        # The checkpoint may come from another world size: the executor re-splits keyed state
+        # by key group and source positions by partition (checkpoint.read_host_checkpoint).
+        result = Executor(self, sinks, job_name, restore_from=path, comm=comm).run()
         self._sinks = []
         return result
 

@@ -29,6 +29,13 @@ I64_MAX = (1 << 63) - 1
 FK_ISO_SEC = 7
 
 
+
+def _spin(ev) -> None:
+    """hipEventQuery polled in C++ with the GIL released (runtime/window_operator._event_spin)."""
+    from ..runtime.window_operator import _event_spin
+
+    _event_spin(ev)
+
 def _pow2(x: int) -> int:
     return 1 << max(1, int(x - 1).bit_length())
 
@@ -428,8 +435,7 @@ class TextIngest:
         dictionary errors, host patch of flagged lines, then the (kept) columns."""
         m, nf, S, n = self._m, self.nf, self.nstr, p.n
         if p.ev is not None:
-            while not p.ev.query():  # poll: a blocking wait wakes tens of microseconds late
-                pass
+            _spin(p.ev)  # poll: a blocking wait wakes tens of microseconds late
         h = p.hb.tolist()
         self._inflight.pop(id(p), None)
         nflag, max_ts, ftotal, ltotal = h[0] & 0xFFFFFFFF, h[1], h[2], h[3]
@@ -516,8 +522,7 @@ class TextIngest:
         self._hbuf[8:12].copy_(dctr, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.device))
-        while not ev.query():  # poll: a blocking wait wakes tens of microseconds late
-            pass
+        _spin(ev)  # poll: a blocking wait wakes tens of microseconds late
         return self._hbuf.tolist()
 
     def _host_patch(self, data, keep_alive, buf, starts, status, cols, n, max_ts):

@@ -424,21 +424,21 @@ def owned_key_groups(rank: int, world: int, parallelism: int, max_parallelism: i
 
 
 # ---- host executor checkpoints (DataStream API jobs) ------------------------------------------
-# Host operators hold arbitrary Python values (user tuples, accumulators, timers), so their state
-# files are pickles written and read only by this engine (never files from elsewhere); keyed
-# state inside them is already partitioned by key group (HeapKeyedStateBackend.snapshot).
+# Host operators hold Python values (user tuples, accumulators, timers); their state files use the
+# typed, code-free encoding of runtime/statecodec.py (JSON + an allow_pickle=False npz), never
+# pickle: restoring a checkpoint directory runs no code from it. Keyed state inside them is
+# partitioned by key group (HeapKeyedStateBackend.snapshot), which lets a restore at another
+# world size re-split it (rescale_host_state).
 def write_host_states(d: Path, states: dict[str, dict], rank: int = 0) -> dict[str, str]:
-    """One state file per operator of this rank (``op<i>-<rank>.state``); returns uid -> file."""
-    import pickle
+    """One state file per operator of this rank (``op<i>-<rank>.state.json`` [+ ``.npz``]);
+    returns uid -> file."""
+    from .statecodec import write_state
 
     d.mkdir(parents=True, exist_ok=True)
     files = {}
     for i, (node_id, st) in enumerate(states.items()):
-        name = f"op{i:03d}-{rank}.state"  # uid -> file map lives in _metadata
-        tmp = d / (name + ".inprogress")
-        with open(tmp, "wb") as f:
-            pickle.dump(st, f, protocol=pickle.HIGHEST_PROTOCOL)
-        os.replace(tmp, d / name)
+        name = f"op{i:03d}-{rank}.state.json"  # uid -> file map lives in _metadata
+        write_state(d / name, st)
         files[node_id] = name
     return files
 
@@ -451,6 +451,7 @@ def write_host_checkpoint(d: Path, *, job_id: str, checkpoint_id: int, states: d
     files = write_host_states(d, states) if ranks is None else ranks[0]["host_operators"]
     meta = {"format": FORMAT, "type": kind, "job_id": job_id, "checkpoint_id": checkpoint_id,
             "timestamp_ms": int(time.time() * 1000), "host_operators": files,
+            "state_encoding": "mxs-typed-v1",
             "extra": extra if ranks is None else ranks[0]["extra"]}
     if ranks is not None:
         meta["world"] = len(ranks)
@@ -458,26 +459,102 @@ def write_host_checkpoint(d: Path, *, job_id: str, checkpoint_id: int, states: d
     _atomic_write_json(d / META, meta)
 
 
-def read_host_checkpoint(path: str | os.PathLike, rank: int = 0,
-                         world: int = 1) -> tuple[dict, dict[str, dict]]:
-    """Metadata (with this rank's ``extra``) and this rank's operator states. A multi-rank host
-    checkpoint restores at the world size that wrote it (host operator state is per subtask
-    set, not re-split by key group)."""
-    import pickle
+def read_host_checkpoint(path: str | os.PathLike, rank: int = 0, world: int = 1,
+                         parallelism: int | None = None,
+                         max_parallelism: int = 128) -> tuple[dict, dict[str, dict]]:
+    """Metadata (with this rank's ``extra``) and this rank's operator states. At the world size
+    that wrote the checkpoint every rank reads its own files; at another world size every rank
+    reads all of them and keeps the key groups it now owns (rescale_host_state)."""
+    from .statecodec import read_state
 
     d = Path(path)
     meta = read_metadata(d)
-    files = meta["host_operators"]
-    if "ranks" in meta or world > 1:
-        w = int(meta.get("world", 1))
-        if w != world:
-            raise ValueError(f"checkpoint {d} was written by {w} rank(s); restoring it needs the "
-                             f"same world size (got {world})")
-        if "ranks" in meta:
-            files = meta["ranks"][rank]["host_operators"]
-            meta = dict(meta, extra=meta["ranks"][rank]["extra"])
-    states = {}
-    for node_id, name in files.items():
-        with open(d / name, "rb") as f:
-            states[node_id] = pickle.load(f)  # written by write_host_states above
-    return meta, states
+    if meta.get("state_encoding") != "mxs-typed-v1":
+        raise ValueError(f"checkpoint {d}: unsupported host state encoding "
+                         f"{meta.get('state_encoding')!r} (only mxs-typed-v1 is read)")
+    w = int(meta.get("world", 1))
+    per_rank = ([r["host_operators"] for r in meta["ranks"]] if "ranks" in meta
+                else [meta["host_operators"]])
+    extras = [r["extra"] for r in meta["ranks"]] if "ranks" in meta else [meta["extra"]]
+    if w == world:
+        states = {nid: read_state(d / name) for nid, name in per_rank[rank].items()}
+        return dict(meta, extra=extras[rank]), states
+    old = [{nid: read_state(d / name) for nid, name in files.items()} for files in per_rank]
+    lo, hi = owned_key_groups(rank, world, parallelism or world, max_parallelism)
+    states = {nid: rescale_host_state([o[nid] for o in old], rank, world, (lo, hi),
+                                      max_parallelism)
+              for nid in per_rank[0]}
+    return dict(meta, extra=rescale_extra(extras, rank, world)), states
+
+
+_KEYED_PARTS = ("keyed", "timers", "wm", "merging", "trigger_state")
+
+
+def rescale_host_state(snaps: list[dict], rank: int, world: int, kg_range: tuple[int, int],
+                       max_parallelism: int) -> dict:
+    """One operator's state at a new rank from every old rank's snapshot.
+
+    * keyed operators (``keyed`` / ``timers`` / ``wm`` / ``merging`` / ``trigger_state``): the
+      key groups in ``kg_range`` from every old rank, timers and merging/trigger entries of
+      those keys, the minimum watermark;
+    * sources (``{"rescale": ...}``): the source merges its old positions itself
+      (Source.restore_rescaled);
+    * stateless operators ({}): nothing;
+    * anything else (a parallelism-1 operator's state lives on rank 0): rank 0's snapshot at
+      the new rank 0 only."""
+    from ..utils.hashing import key_group
+
+    if not any(snaps):
+        return {}
+    if all(not s or set(s) <= set(_KEYED_PARTS) for s in snaps):
+        lo, hi = kg_range
+        out: dict = {"keyed": {}}
+
+        def mine(key) -> bool:
+            return lo <= key_group(key, max_parallelism) <= hi
+
+        for s in snaps:
+            for kg, tables in s.get("keyed", {}).items():
+                if lo <= int(kg) <= hi:
+                    dst = out["keyed"].setdefault(int(kg), {})
+                    for name, entries in tables.items():
+                        dst.setdefault(name, {}).update(entries)
+        if any("timers" in s for s in snaps):
+            out["timers"] = {kind: sorted(t for s in snaps for t in s.get("timers", {}).get(kind, [])
+                                          if mine(t[1]))
+                             for kind in ("event", "proc")}
+        wms = [s["wm"] for s in snaps if "wm" in s]
+        if wms:
+            out["wm"] = min(wms)
+        for part in ("merging", "trigger_state"):
+            if any(part in s for s in snaps):
+                out[part] = {}
+                for s in snaps:
+                    for k, v in s.get(part, {}).items():
+                        kk = k[0] if part == "trigger_state" and isinstance(k, tuple) else k
+                        if mine(kk):
+                            out[part][k] = v
+        return out
+    if all("rescale" in s for s in snaps if s):
+        return {"rescaled": [s["rescale"] for s in snaps], "rank": rank, "world": world}
+    if rank == 0:
+        if any(snaps[1:]):
+            raise ValueError("host checkpoint: an operator with state on several ranks that is "
+                             "not keyed cannot be restored at another world size")
+        return snaps[0]
+    return {}
+
+
+def rescale_extra(extras: list[dict], rank: int, world: int) -> dict:
+    """Executor bookkeeping at a new world size: the clock is the maximum (the ranks agree on a
+    step clock), round-robin counters restart, a source is finished only if it was everywhere."""
+    ex = dict(extras[0])
+    clocks = [e.get("clock") for e in extras if e.get("clock") is not None]
+    ex["clock"] = max(clocks) if clocks else None
+    ex["rr"] = []
+    fin = {}
+    for e in extras:
+        for k, v in e.get("finished", {}).items():
+            fin[k] = fin.get(k, True) and bool(v)
+    ex["finished"] = fin
+    return ex

@@ -480,7 +480,8 @@ class Executor:
         from .checkpoint import read_host_checkpoint
 
         rank, world = (self.comm.rank, self.comm.world) if self.comm is not None else (0, 1)
-        meta, states = read_host_checkpoint(path, rank, world)
+        meta, states = read_host_checkpoint(path, rank, world, self.env.parallelism,
+                                            self.env.max_parallelism)
         names = meta["extra"]["nodes"]
         for nd in self.nodes:
             key = self._uid(nd)

@@ -44,11 +44,29 @@ class Source:
     # restore (Flink's source offsets). Non-replayable ones (socket) return {}.
     def snapshot(self) -> dict:
         pos = getattr(self, "pos", None)
-        return {} if pos is None else {"pos": pos}
+        return {} if pos is None else {"pos": pos, "rescale": self._rescale_info()}
 
     def restore(self, snap: dict) -> None:
-        if "pos" in snap:
+        if "rescaled" in snap:
+            self.restore_rescaled(snap["rescaled"])
+        elif "pos" in snap:
             self.pos = snap["pos"]
+
+    def _rescale_info(self) -> dict:
+        return {"rank": self.rank, "world": self.world, "pos": getattr(self, "pos", None)}
+
+    def restore_rescaled(self, old: list[dict]) -> None:
+        """Resume from a checkpoint written at another world size: `old` = every old rank's
+        _rescale_info(). Sources whose partitions can be re-split override this."""
+        raise ValueError(f"{self.name}: no restore at a different world size")
+
+    @staticmethod
+    def _consumed(old: list[dict]):
+        """Global index i of a rank-strided source (index i on rank i % G at position i // G)
+        was emitted before the checkpoint iff i // G < pos of that old rank."""
+        g = len(old)
+        pos = [o["pos"] for o in sorted(old, key=lambda o: o["rank"])]
+        return lambda i: i // g < pos[i % g]
 
 
 class CollectionSource(Source):
@@ -63,11 +81,21 @@ class CollectionSource(Source):
 
     def open(self, rank, world, clock):
         super().open(rank, world, clock)
-        # Distributed runs: each rank is one source partition.
+        # Distributed runs: each rank is one source partition (global index i on rank i % G).
+        self._all = (self.values, self.timestamps)
         idx = list(range(len(self.values)))[rank::world]
         self.values = [self.values[i] for i in idx]
         if self.timestamps is not None:
             self.timestamps = [self.timestamps[i] for i in idx]
+
+    def restore_rescaled(self, old):
+        done = self._consumed(old)
+        values, ts = self._all
+        idx = [i for i in range(self.rank, len(values), self.world) if not done(i)]
+        self.values = [values[i] for i in idx]
+        if ts is not None:
+            self.timestamps = [ts[i] for i in idx]
+        self.pos = 0
 
     def poll(self, now):
         if self.pos >= len(self.values):
@@ -101,6 +129,10 @@ class TimedCollectionSource(Source):
         if rank != 0:
             self.timed = []
             self.end_time = 0
+
+    def restore_rescaled(self, old):
+        # every item lives on rank 0 (a non-parallel source): its position carries over
+        self.pos = next(o["pos"] for o in old if o["rank"] == 0) if self.rank == 0 else 0
 
     def next_event_time(self):
         if self.pos < len(self.timed):
@@ -303,6 +335,19 @@ class TextFileSource(Source):
     def snapshot(self) -> dict:
         return {"bpos": self.bpos} if self.columnar else super().snapshot()
 
+    def restore_rescaled(self, old):
+        if self.columnar or self.lines is None:
+            raise ValueError("text file source: the columnar reader's byte ranges cannot be "
+                             "re-split at another world size")
+        done = self._consumed(old)
+        with open(self.path, "r", encoding="utf-8") as f:
+            lines = f.read().split("\n")
+        if lines and lines[-1] == "":
+            lines.pop()
+        lines = [l[:-1] if l.endswith("\r") else l for l in lines]
+        self.lines = [lines[i] for i in range(self.rank, len(lines), self.world) if not done(i)]
+        self.pos = 0
+
     def restore(self, snap: dict) -> None:
         if self.columnar and "bpos" in snap:
             if self._ring is not None:
@@ -439,15 +484,28 @@ class SequenceSource(Source):
         self.step = world
 
     def snapshot(self) -> dict:
-        return {"cur": self.cur}
+        return {"cur": self.cur, "rescale": {"rank": self.rank, "world": self.world,
+                                             "cur": self.cur}}
 
     def restore(self, snap: dict) -> None:
-        self.cur = snap.get("cur", self.cur)
+        if "rescaled" in snap:
+            self.restore_rescaled(snap["rescaled"])
+        else:
+            self.cur = snap.get("cur", self.cur)
+
+    def restore_rescaled(self, old):
+        # old rank r emitted start + r, start + r + G, ... below its cursor
+        g = len(old)
+        cur = [o["cur"] for o in sorted(old, key=lambda o: o["rank"])]
+        self._skip = lambda x: x < cur[(x - self.start) % g]
+        self.cur = self.start + self.rank
 
     def poll(self, now):
         out = []
+        skip = getattr(self, "_skip", None)
         while self.cur <= self.end and len(out) < self.batch:
-            out.append(Rec(self.cur))
+            if skip is None or not skip(self.cur):
+                out.append(Rec(self.cur))
             self.cur += self.step
         return out, self.cur > self.end
 

@@ -209,8 +209,7 @@ class CountedHostRows:
         return self.ev.query()
 
     def wait(self) -> None:
-        while not self.ev.query():
-            pass
+        _event_spin(self.ev)
 
     def fixed(self, i: int) -> np.ndarray:
         off, nb, dt = self.fixed_meta[i]
@@ -240,10 +239,18 @@ _NP_DTYPE = {torch.int64: np.int64, torch.int32: np.int32, torch.float64: np.flo
 _SYNC = __import__("os").environ.get("MXS_SYNC", "query")
 
 
+def _event_spin(ev) -> None:
+    """Poll the event in C++ with the GIL released (csrc/bindings.cpp gpu_event_spin)."""
+    from ..ops.native import load
+
+    e = load().gpu_event_spin(ev.cuda_event)
+    if e != 0:
+        raise RuntimeError(f"hipEventQuery failed (hipError {e})")
+
+
 def _host_wait(ev, device, pipelined: bool) -> None:
     if _SYNC == "query":
-        while not ev.query():
-            pass
+        _event_spin(ev)
     elif _SYNC == "event" or pipelined:
         ev.synchronize()
     else:
