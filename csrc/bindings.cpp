@@ -549,12 +549,18 @@ PYBIND11_MODULE(_mxs_native, m) {
                                  int cap_log2, intptr_t keys_g, intptr_t spill_set,
                                  uint32_t spill_mask, int spill_any, intptr_t sk, intptr_t vals,
                                  intptr_t n_out, intptr_t host_recs, intptr_t n_host,
-                                 uint32_t host_cap, intptr_t n_ins, int tbits, intptr_t stream) {
-    gpu::session_lookup(P<Rec>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2,
+                                 uint32_t host_cap, intptr_t n_ins, int tbits, intptr_t stream,
+                                 int rec_words) {
+    gpu::session_lookup(P<void>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2,
                         P<uint64_t>(keys_g), P<uint64_t>(spill_set), spill_mask, spill_any,
                         P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_out), P<Rec>(host_recs),
-                        P<uint32_t>(n_host), host_cap, P<uint32_t>(n_ins), tbits, stream);
-  });
+                        P<uint32_t>(n_host), host_cap, P<uint32_t>(n_ins), tbits, stream,
+                        rec_words);
+  }, py::arg("recs"), py::arg("counts"), py::arg("nsrc"), py::arg("nsub"), py::arg("bcap"),
+     py::arg("cap_log2"), py::arg("keys_g"), py::arg("spill_set"), py::arg("spill_mask"),
+     py::arg("spill_any"), py::arg("sk"), py::arg("vals"), py::arg("n_out"), py::arg("host_recs"),
+     py::arg("n_host"), py::arg("host_cap"), py::arg("n_ins"), py::arg("tbits"), py::arg("stream"),
+     py::arg("rec_words") = 3);
   m.def("gpu_session_lookup_sort", [](intptr_t recs, intptr_t counts, int nsrc, int nsub,
                                       uint32_t bcap, int cap_log2, intptr_t keys_g,
                                       intptr_t spill_set, uint32_t spill_mask, int spill_any,
@@ -562,18 +568,19 @@ PYBIND11_MODULE(_mxs_native, m) {
                                       intptr_t host_recs, intptr_t n_host, uint32_t host_cap,
                                       intptr_t n_ins, int tbits, intptr_t stream, intptr_t skip,
                                       uint32_t skip_mask, intptr_t heads, intptr_t n_heads,
-                                      int pair) {
-    return gpu::session_lookup_sort(P<Rec>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2,
+                                      int pair, int rec_words) {
+    return gpu::session_lookup_sort(P<void>(recs), P<uint32_t>(counts), nsrc, nsub, bcap, cap_log2,
                                     P<uint64_t>(keys_g), P<uint64_t>(spill_set), spill_mask,
                                     spill_any, P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_out),
                                     P<Rec>(host_recs), P<uint32_t>(n_host), host_cap,
                                     P<uint32_t>(n_ins), tbits, stream, P<int64_t>(skip), skip_mask,
-                                    P<uint64_t>(heads), P<uint32_t>(n_heads), pair);
+                                    P<uint64_t>(heads), P<uint32_t>(n_heads), pair, rec_words);
   }, py::arg("recs"), py::arg("counts"), py::arg("nsrc"), py::arg("nsub"), py::arg("bcap"),
      py::arg("cap_log2"), py::arg("keys_g"), py::arg("spill_set"), py::arg("spill_mask"),
      py::arg("spill_any"), py::arg("sk"), py::arg("vals"), py::arg("n_out"), py::arg("host_recs"),
      py::arg("n_host"), py::arg("host_cap"), py::arg("n_ins"), py::arg("tbits"), py::arg("stream"),
-     py::arg("skip") = 0, py::arg("skip_mask") = 0, py::arg("heads") = 0, py::arg("n_heads") = 0, py::arg("pair") = 0);
+     py::arg("skip") = 0, py::arg("skip_mask") = 0, py::arg("heads") = 0, py::arg("n_heads") = 0, py::arg("pair") = 0,
+     py::arg("rec_words") = 3);
   m.def("gpu_session_heads", [](intptr_t sk, intptr_t n_in, int64_t n_cap, intptr_t heads,
                                 intptr_t n_heads, intptr_t stream) {
     gpu::session_heads(P<int64_t>(sk), P<uint32_t>(n_in), n_cap, P<uint32_t>(heads),

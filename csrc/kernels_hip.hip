@@ -2484,14 +2484,14 @@ __global__ __launch_bounds__(256) void rolling_lookup_kernel(
   const uint32_t lo = blockIdx.x * kLookupChunk;
   if (lo >= c) return;  // whole workgroup exits together
   const uint32_t hi = lo + kLookupChunk < c ? lo + kLookupChunk : c;
-  const Rec* seg = recs + (size_t)b * bucket_cap;
+  const size_t seg = (size_t)b * bucket_cap;
   __shared__ uint32_t base;
   if (threadIdx.x == 0) base = atomicAdd(n_out, hi - lo);
   __syncthreads();
   uint64_t* keys = keys_g + ((size_t)sub << cap_log2);
   const uint32_t mask = (1u << cap_log2) - 1;
   for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
-    const Rec r = seg[e];
+    const Rec r = recs[seg + e];
     int64_t sk = INT64_MAX;  // holes and overflow sort last and are ignored
     if (r.t != 0xFFFFFFFFu) {
       const uint32_t s = global_probe_insert(keys, r.key, mask);
@@ -2845,8 +2845,10 @@ __device__ __forceinline__ uint32_t sess_find(const uint64_t* keys, uint64_t key
   return kNoSlot;
 }
 
+// RW: record width of the bucketed input (3 = 24-byte Rec, 2 = 16-byte RecC, load_rec).
+template <int RW>
 __global__ __launch_bounds__(256) void session_lookup_kernel(
-    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
+    const void* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
     uint32_t bucket_cap, int cap_log2, uint64_t* __restrict__ keys_g,
     uint64_t* __restrict__ spill_set, uint32_t spill_mask, int32_t spill_any,
     int64_t* __restrict__ sort_key, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
@@ -2859,14 +2861,14 @@ __global__ __launch_bounds__(256) void session_lookup_kernel(
   const uint32_t lo = blockIdx.x * kLookupChunk;
   if (lo >= c) return;
   const uint32_t hi = lo + kLookupChunk < c ? lo + kLookupChunk : c;
-  const Rec* seg = recs + (size_t)b * bucket_cap;
+  const size_t seg = (size_t)b * bucket_cap;
   __shared__ uint32_t base;
   if (threadIdx.x == 0) base = atomicAdd(n_out, hi - lo);
   __syncthreads();
   uint64_t* keys = keys_g + ((size_t)sub << cap_log2);
   const uint32_t mask = (1u << cap_log2) - 1;
   for (uint32_t e = lo + threadIdx.x; e < hi; e += blockDim.x) {
-    const Rec r = seg[e];
+    const Rec r = load_rec<RW>(recs, seg + e);
     int64_t sk = INT64_MAX;
     if (r.t != 0xFFFFFFFFu) {
       // Resident keys are found in the slot table (a key is never resident and spilled at once),
@@ -2899,8 +2901,9 @@ __global__ __launch_bounds__(256) void session_lookup_kernel(
 constexpr int kSessLookupBlock = 512;
 constexpr int kSessLookupLdsMaxLog2 = 12;  // 32 KB of keys
 
+template <int RW>
 __global__ __launch_bounds__(kSessLookupBlock) void session_lookup_lds_kernel(
-    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
+    const void* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
     uint32_t bucket_cap, int cap_log2, uint64_t* __restrict__ keys_g,
     uint64_t* __restrict__ spill_set, uint32_t spill_mask, int32_t spill_any,
     int64_t* __restrict__ sort_key, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
@@ -2927,9 +2930,9 @@ __global__ __launch_bounds__(kSessLookupBlock) void session_lookup_lds_kernel(
     const int b = src * nsub + sub;
     uint32_t c = counts[b];
     c = c < bucket_cap ? c : bucket_cap;
-    const Rec* seg = recs + (size_t)b * bucket_cap;
+    const size_t seg = (size_t)b * bucket_cap;
     for (uint32_t e = threadIdx.x; e < c; e += blockDim.x) {
-      const Rec r = seg[e];
+      const Rec r = load_rec<RW>(recs, seg + e);
       int64_t sk = INT64_MAX;
       if (r.t != 0xFFFFFFFFu) {
         uint32_t s = sess_find<__HIP_MEMORY_SCOPE_WORKGROUP>(lkeys, r.key, mask);
@@ -2975,8 +2978,9 @@ __global__ __launch_bounds__(kSessLookupBlock) void session_lookup_lds_kernel(
 constexpr int kSessSortBlock = 1024;
 constexpr int kLsRegs = 16;  // record values kept in registers per thread (m <= 16K: all of them)
 
+template <int RW>
 __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
-    const Rec* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
+    const void* __restrict__ recs, const uint32_t* __restrict__ counts, int nsrc, int nsub,
     uint32_t bucket_cap, int cap_log2, uint64_t* __restrict__ keys_g,
     uint64_t* __restrict__ spill_set, uint32_t spill_mask, int32_t spill_any,
     int64_t* __restrict__ sort_out, uint64_t* __restrict__ vals_out, uint32_t* __restrict__ n_out,
@@ -3030,10 +3034,10 @@ __global__ __launch_bounds__(kSessSortBlock) void session_lookup_sort_kernel(
   // phase 3, so each thread keeps the values of its first kLsRegs records in registers and phase
   // 3 writes them without re-reading the bucket (an uncoalesced gather).
   uint32_t kept = 0;
-  auto rec_at = [&](uint32_t i) -> const Rec& {
+  auto rec_at = [&](uint32_t i) -> Rec {
     int src = 0;
     while (src + 1 < nsrc && i >= s_src_off[src + 1]) ++src;
-    return recs[(size_t)(src * nsub + sub) * bucket_cap + (i - s_src_off[src])];
+    return load_rec<RW>(recs, (size_t)(src * nsub + sub) * bucket_cap + (i - s_src_off[src]));
   };
   // 1a: insert-or-find every record's key in the LDS table. Only the thread that claims a slot
   //     for a key new to the table probes the device spill set (once per key instead of once per
@@ -4243,6 +4247,21 @@ struct SplitRec<24> {
   }
 };
 
+template <>
+struct SplitRec<16> {  // RecC: key lo | key hi | int32 value | t (hole: t == kHoleT)
+  uint4 r;
+  __device__ __forceinline__ void load(const void* base, size_t i) {
+    const u32x4_t w = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(base) + i);
+    r = make_uint4(w.x, w.y, w.z, w.w);
+  }
+  __device__ __forceinline__ void hole() { r = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, kHoleT); }
+  __device__ __forceinline__ bool live() const { return r.w != kHoleT; }
+  __device__ __forceinline__ uint64_t key() const { return (uint64_t)r.x | ((uint64_t)r.y << 32); }
+  __device__ __forceinline__ void store(void* base, size_t i) const {
+    reinterpret_cast<uint4*>(base)[i] = r;
+  }
+};
+
 template <int RB>
 __global__ __launch_bounds__(kSplitThreads) void partition_split_kernel(
     const void* __restrict__ coarse, const uint32_t* __restrict__ coarse_n, uint32_t ccap,
@@ -4383,6 +4402,32 @@ void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
     }
     dispatch_compact<true, 8>(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats,
                               late_idx, late_cap, stream);
+    return;
+  }
+  if (plan.rec_words == 2 && nb > kCMaxNb && plan.scratch && plan.scratch_cursor &&
+      nb <= kCMaxNb * 32 && (uint64_t)nb * plan.bucket_cap < (1ull << 32)) {
+    // Two-level 16-byte partition (session records, more than 512 buckets): the compact staged
+    // kernel into 512 coarse buckets (one LDS counting sort per 4096-record round, contiguous
+    // run writes), then one workgroup per coarse bucket splits it into its 2^L fine buckets.
+    if (n <= 0) return;
+    int L = 0;
+    while ((nb >> L) > kCMaxNb) ++L;
+    PartPlan pc = plan;
+    pc.nsub_log2 = plan.nsub_log2 - L;
+    pc.bucket_cap = plan.bucket_cap << L;
+    if (pc.nsub_log2 < 0) throw std::invalid_argument("two-level partition: too few sub-tables");
+    hipStream_t st = (hipStream_t)stream;
+    HIP_CHECK(hipMemsetAsync(plan.scratch_cursor, 0, sizeof(uint32_t) * (nb >> L), st));
+    if (plan.nranks == 1)
+      dispatch_compact<true, 16>(keys, ts, vals, jhash_tab, n, pc, kg_dest, plan.scratch_cursor,
+                                 (Rec*)plan.scratch, stats, late_idx, late_cap, stream);
+    else
+      dispatch_compact<false, 16>(keys, ts, vals, jhash_tab, n, pc, kg_dest, plan.scratch_cursor,
+                                  (Rec*)plan.scratch, stats, late_idx, late_cap, stream);
+    hipLaunchKernelGGL(partition_split_kernel<16>, dim3(nb >> L), dim3(kSplitThreads), 0, st,
+                       (const void*)plan.scratch, plan.scratch_cursor, pc.bucket_cap, plan, L,
+                       cursor, (void*)out, stats);
+    HIP_CHECK(hipGetLastError());
     return;
   }
   if (plan.rec_words == 2 && nb <= kCMaxNb && (uint64_t)nb * plan.bucket_cap < (1ull << 32)) {
@@ -5018,22 +5063,26 @@ static SessArgs make_sess_args(int64_t gap, int64_t lateness, int64_t wm, int64_
   return a;
 }
 
-void session_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bcap,
+void session_lookup(const void* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bcap,
                     int cap_log2, uint64_t* keys_g, uint64_t* spill_set, uint32_t spill_mask,
                     int spill_any, int64_t* sk, uint64_t* vals, uint32_t* n_out, Rec* host_recs,
                     uint32_t* n_host, uint32_t host_cap, uint32_t* n_inserted, int tbits,
-                    intptr_t stream) {
+                    intptr_t stream, int rec_words) {
   if (nsrc * nsub <= 0) return;
   if (tbits < 1 || tbits > 32) throw std::invalid_argument("session_lookup: tbits out of range");
+  if (rec_words != 2 && rec_words != 3)
+    throw std::invalid_argument("session_lookup: 16- or 24-byte records");
   if (cap_log2 <= kSessLookupLdsMaxLog2) {
     const size_t lds = (size_t)sizeof(uint64_t) << cap_log2;
-    hipLaunchKernelGGL(session_lookup_lds_kernel, dim3(nsub), dim3(kSessLookupBlock), lds,
+    hipLaunchKernelGGL(rec_words == 2 ? session_lookup_lds_kernel<2> : session_lookup_lds_kernel<3>,
+                       dim3(nsub), dim3(kSessLookupBlock), lds,
                        (hipStream_t)stream, recs, counts, nsrc, nsub, bcap, cap_log2, keys_g,
                        spill_set, spill_mask, spill_any, sk, vals, n_out, host_recs, n_host,
                        host_cap, n_inserted, tbits);
   } else {
     const uint32_t chunks = (bcap + kLookupChunk - 1) / kLookupChunk;
-    hipLaunchKernelGGL(session_lookup_kernel, dim3(chunks, nsrc * nsub), dim3(256), 0,
+    hipLaunchKernelGGL(rec_words == 2 ? session_lookup_kernel<2> : session_lookup_kernel<3>,
+                       dim3(chunks, nsrc * nsub), dim3(256), 0,
                        (hipStream_t)stream, recs, counts, nsrc, nsub, bcap, cap_log2, keys_g,
                        spill_set, spill_mask, spill_any, sk, vals, n_out, host_recs, n_host,
                        host_cap, n_inserted, tbits);
@@ -5047,12 +5096,15 @@ size_t session_lookup_sort_lds(int cap_log2, uint32_t m_cap) {
   return a + (size_t)m_cap * 8;
 }
 
-bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
+bool session_lookup_sort(const void* recs, const uint32_t* counts, int nsrc, int nsub,
                          uint32_t bcap, int cap_log2, uint64_t* keys_g, uint64_t* spill_set,
                          uint32_t spill_mask, int spill_any, int64_t* sort_out, uint64_t* vals_out,
                          uint32_t* n_out, Rec* host_recs, uint32_t* n_host, uint32_t host_cap,
                          uint32_t* n_inserted, int tbits, intptr_t stream, const int64_t* skip,
-                         uint32_t skip_mask, uint64_t* heads_out, uint32_t* n_heads, int pair) {
+                         uint32_t skip_mask, uint64_t* heads_out, uint32_t* n_heads, int pair,
+                         int rec_words) {
+  if (rec_words != 2 && rec_words != 3)
+    throw std::invalid_argument("session_lookup_sort: 16- or 24-byte records");
   if (nsrc * nsub <= 0) return true;
   if (pair && ((uintptr_t)sort_out & 15))
     throw std::invalid_argument("session_lookup_sort: pair output must be 16-byte aligned");
@@ -5062,14 +5114,15 @@ bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int 
   const uint32_t m_cap = ((uint32_t)m64 + 7) & ~7u;
   const size_t lds = session_lookup_sort_lds(cap_log2, m_cap);
   if (lds > 156 * 1024) return false;  // static LDS (slot flags, offsets, counters) takes the rest
-  static bool attr = false;
-  if (!attr) {
+  auto kfn = rec_words == 2 ? session_lookup_sort_kernel<2> : session_lookup_sort_kernel<3>;
+  static bool attr[2] = {false, false};
+  if (!attr[rec_words - 2]) {
     // dynamic + the kernel's static LDS (slot flags, segment offsets, scan scratch) <= 160 KiB
-    HIP_CHECK(hipFuncSetAttribute((const void*)session_lookup_sort_kernel,
+    HIP_CHECK(hipFuncSetAttribute((const void*)kfn,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024));
-    attr = true;
+    attr[rec_words - 2] = true;
   }
-  hipLaunchKernelGGL(session_lookup_sort_kernel, dim3(nsub), dim3(kSessSortBlock), lds,
+  hipLaunchKernelGGL(kfn, dim3(nsub), dim3(kSessSortBlock), lds,
                      (hipStream_t)stream, recs, counts, nsrc, nsub, bcap, cap_log2, keys_g,
                      spill_set, spill_mask, spill_any, sort_out, vals_out, n_out, host_recs,
                      n_host, host_cap, n_inserted, tbits, m_cap, skip, skip_mask, heads_out,

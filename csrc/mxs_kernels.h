@@ -277,22 +277,24 @@ void rolling_hist(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
                   uint32_t* cnt_g, void* scratch, size_t scratch_bytes, const ExprProg& filt,
                   uint64_t* out_key, uint64_t* out_val, int64_t* out_tag, uint32_t* out_n,
                   uint32_t out_cap, uint32_t* flags, int dense, intptr_t stream);
-void session_lookup(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bcap,
+// rec_words: the bucketed records' width (3 = 24-byte Rec, 2 = 16-byte RecC); the diverted
+// host records are always written as 24-byte Rec.
+void session_lookup(const void* recs, const uint32_t* counts, int nsrc, int nsub, uint32_t bcap,
                     int cap_log2, uint64_t* keys_g, uint64_t* spill_set, uint32_t spill_mask,
                     int spill_any, int64_t* sk, uint64_t* vals, uint32_t* n_out, Rec* host_recs,
                     uint32_t* n_host, uint32_t host_cap, uint32_t* n_inserted, int tbits,
-                    intptr_t stream);
+                    intptr_t stream, int rec_words = 3);
 // Fused lookup + per-sub-table LDS segmented sort: writes the kept records in (slot, ts) order
 // (the stable sort of session_lookup's keys without holes). Returns false (nothing launched)
 // when a sub-table's records cannot be staged in LDS (then: session_lookup + a device sort).
-bool session_lookup_sort(const Rec* recs, const uint32_t* counts, int nsrc, int nsub,
+bool session_lookup_sort(const void* recs, const uint32_t* counts, int nsrc, int nsub,
                          uint32_t bcap, int cap_log2, uint64_t* keys_g, uint64_t* spill_set,
                          uint32_t spill_mask, int spill_any, int64_t* sort_out, uint64_t* vals_out,
                          uint32_t* n_out, Rec* host_recs, uint32_t* n_host, uint32_t host_cap,
                          uint32_t* n_inserted, int tbits, intptr_t stream,
                          const int64_t* skip = nullptr, uint32_t skip_mask = 0,
                          uint64_t* heads_out = nullptr, uint32_t* n_heads = nullptr,
-                         int pair = 0);
+                         int pair = 0, int rec_words = 3);
 void session_heads(const int64_t* sk, const uint32_t* n_in, int64_t n_cap, uint32_t* heads,
                    uint32_t* n_heads, intptr_t stream);
 void session_merge(const int64_t* sk, const uint64_t* vals, const uint32_t* n_in,

@@ -65,6 +65,10 @@ _STORE_SHARDS = int(__import__("os").environ.get("MXS_SESSION_SHARDS", "1"))
 # compute stream ("0", A/B: the side-stream launch cost the host 1.2 ms per step at config 5
 # while the GPU was busy, against 26 us on an idle GPU -- scripts/d2h_launch_bench.py).
 _SPILL_SIDE_STREAM = __import__("os").environ.get("MXS_SPILL_SIDE_STREAM", "1") != "0"
+# GPU keyBy records: 16-byte (key, int32 value, ts - tbase) through the two-level compact
+# partition ("1", default; a value outside int32 widens the step to 24-byte records and redoes
+# it) or the 24-byte plain scatter ("0", A/B).
+_REC16 = __import__("os").environ.get("MXS_SESSION_REC16", "1") != "0"
 
 
 def _next_pow2(x: int) -> int:
@@ -169,6 +173,8 @@ class KeyedSessionOperator:
         self.promote_spilled = True
         self.local_maxts = torch.full((1,), I64_MIN, dtype=torch.int64, device=dev)
         self.red = torch.zeros(K.RED_WORDS, dtype=torch.int64, device=dev)
+        # keyBy record width of the GPU step (2: 16-byte records, 3: 24-byte; CPU: 3)
+        self.rec_w = 2 if self.gpu and _REC16 else 3
         self._alloc(batch_capacity)
         if self.gpu:
             self._alloc_state()
@@ -231,10 +237,12 @@ class KeyedSessionOperator:
         # 24-byte records it measured 407 + 205 us against 464 us for the plain scatter
         # (profiles/r3_cfg5_two_level.md).
         self._scratch = self._scratch_cursor = None
-        if self.gpu and 512 < self.nbuckets <= 512 * 32 and \
-                __import__("os").environ.get("MXS_TWO_LEVEL24", "0") == "1":
+        if self.gpu and 512 < self.nbuckets <= 512 * 32 and (
+                _REC16 or __import__("os").environ.get("MXS_TWO_LEVEL24", "0") == "1"):
+            # (sized for 24-byte records: a widened step may take the 24-byte two-level path)
             self._scratch = torch.empty(words, dtype=torch.int64, device=dev)
             self._scratch_cursor = torch.zeros(512, dtype=torch.int32, device=dev)
+        self._two_level24 = __import__("os").environ.get("MXS_TWO_LEVEL24", "0") == "1"
         if self.gpu:
             total = self.nbuckets * self.bucket_cap
             self.sort_key = torch.empty(total, dtype=torch.int64, device=dev)
@@ -315,8 +323,9 @@ class KeyedSessionOperator:
             K.step_begin(self.cursor, self.stats)
             plan = K.PartitionPlan(max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2,
                                    nranks=self.world, window_mode=1, drop_late=0, hash_mode=0,
-                                   bucket_cap=self.bucket_cap, late_ts=I64_MIN, tbase=tbase, pane=1)
-            if self._scratch is not None:
+                                   bucket_cap=self.bucket_cap, late_ts=I64_MIN, tbase=tbase, pane=1,
+                                   rec_words=self.rec_w)
+            if self._scratch is not None and (self.rec_w == 2 or self._two_level24):
                 plan.scratch = self._scratch.data_ptr()
                 plan.scratch_cursor = self._scratch_cursor.data_ptr()
             if n:
@@ -334,7 +343,7 @@ class KeyedSessionOperator:
                 with self._phase("fold_gpu"):
                     self._fold_prepare()
                     if self._fold_launch(self.recv, self.recv_counts, self.world, tbase, old_wm,
-                                         32, self.bucket_cap, skip=self.red):
+                                         32, self.bucket_cap, skip=self.red, rw=self.rec_w):
                         folded = self._fold_counters(with_red=True)
                         host = self._hred.tolist()
             if folded is None:
@@ -348,6 +357,12 @@ class KeyedSessionOperator:
                 raise RuntimeError("session batch spans more than 2^32 ms")
             if host[7]:
                 raise ValueError("key ids -1 and -2 are reserved (the state tables' markers)")
+            if host[5] and self.rec_w < 3:
+                # a value outside int32: 24-byte records from now on, redo the step
+                self.rec_w = 3
+                self.metrics.extra["record_widenings"] = \
+                    self.metrics.extra.get("record_widenings", 0) + 1
+                continue
             if host[3]:
                 self._alloc(self.batch_capacity, self.slack * 2)
                 continue
@@ -469,7 +484,7 @@ class KeyedSessionOperator:
         tbits = min(32, max(1, int(tspan).bit_length()))  # (no records: tspan is meaningless)
         self._fold_prepare()
         h, total = self._fold_recs(self.recv, self.recv_counts, self.world, tbase, wm, tbits,
-                                   self.bucket_cap)
+                                   self.bucket_cap, rw=self.rec_w)
         self._fold_finish(h, total, tbase, wm, tbits)
 
     def _fold_prepare(self) -> None:
@@ -499,12 +514,13 @@ class KeyedSessionOperator:
         self.metrics.num_late_records_dropped += late
 
     def _fold_recs(self, recs, counts, nsrc: int, tbase: int, wm: int, tbits: int,
-                   bucket_cap: int):
-        """Lookup -> (slot | ts) radix sort -> ordered session merge of bucketed records.
-        Returns the host counters c[:6] and the number of looked-up records."""
+                   bucket_cap: int, rw: int = 3):
+        """Lookup -> (slot | ts) radix sort -> ordered session merge of bucketed records
+        (`rw`: their width, 2 = 16-byte, 3 = 24-byte). Returns the host counters c[:6] and the
+        number of looked-up records."""
         m, st, c = self.native, self._st(), self.ctr
         sbits = self.nslots.bit_length()  # one spare bit: valid keys stay below the sentinel
-        if self._fold_launch(recs, counts, nsrc, tbase, wm, tbits, bucket_cap):
+        if self._fold_launch(recs, counts, nsrc, tbase, wm, tbits, bucket_cap, rw=rw):
             h = self._fold_counters()
             if h[2] > self.host_cap:
                 raise RuntimeError("host diversion buffer overflow")
@@ -514,7 +530,7 @@ class KeyedSessionOperator:
                              self.spill_set.data_ptr(), self.spill_set.numel() - 1,
                              int(self.spill_any), self.sort_key.data_ptr(), self.vals_buf.data_ptr(),
                              c[0:1].data_ptr(), self.host_recs.data_ptr(), c[2:3].data_ptr(),
-                             self.host_cap, c[3:4].data_ptr(), tbits, st)
+                             self.host_cap, c[3:4].data_ptr(), tbits, st, rec_words=rw)
         total = int(c[0].item())
         if total:
             # Key-value radix sort over the used bits only (slot | ts - tbase); values ride along.
@@ -539,11 +555,12 @@ class KeyedSessionOperator:
         return h, total
 
     # Reduced-vector words whose non-zero value makes a speculatively launched fold skip itself:
-    # [3] bucket overflow (redo), [4] span > 2^32 ms, [7] reserved key id.
+    # [3] bucket overflow (redo), [4] span > 2^32 ms, [7] reserved key id (and, with 16-byte
+    # records, [5]: a value that needs 24-byte records).
     _SKIP_MASK = (1 << 3) | (1 << 4) | (1 << 7)
 
     def _fold_launch(self, recs, counts, nsrc: int, tbase: int, wm: int, tbits: int,
-                     bucket_cap: int, skip: torch.Tensor | None = None) -> bool:
+                     bucket_cap: int, skip: torch.Tensor | None = None, rw: int = 3) -> bool:
         """Lookup + per-sub-table LDS segmented sort in one kernel -- (slot, ts)-ordered records
         without holes, straight into the merge (no device-wide radix sort). The record count
         stays on the device (the merge reads it); the host learns it with the counters. False:
@@ -562,8 +579,8 @@ class KeyedSessionOperator:
                 self.vals_out.data_ptr(), c[0:1].data_ptr(), self.host_recs.data_ptr(),
                 c[2:3].data_ptr(), self.host_cap, c[3:4].data_ptr(), tbits, st,
                 skip.data_ptr() if skip is not None else 0,
-                self._SKIP_MASK if skip is not None else 0,
-                self.seg_heads.data_ptr(), c[10:11].data_ptr(), _SESSION_PAIR):
+                (self._SKIP_MASK | (1 << 5 if rw < 3 else 0)) if skip is not None else 0,
+                self.seg_heads.data_ptr(), c[10:11].data_ptr(), _SESSION_PAIR, rec_words=rw):
             return False
         # One lane per key segment listed by the lookup-sort (c[10] segments on the device).
         m.gpu_session_merge_heads(self.sort_out.data_ptr(), self.vals_out.data_ptr(),
