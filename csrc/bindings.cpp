@@ -689,6 +689,50 @@ PYBIND11_MODULE(_mxs_native, m) {
     while ((e = hipEventQuery((hipEvent_t)ev)) == hipErrorNotReady) __builtin_ia32_pause();
     return (int)e;
   });
+  // Packed-row exchange (parallel/exchange.py): cols = [(src ptr, dst ptr, words per row)].
+  auto xcols = [](const std::vector<std::tuple<intptr_t, intptr_t, int>>& cols) {
+    if (cols.empty() || cols.size() > 8) throw std::invalid_argument("exchange_rows: 1..8 columns");
+    XRowCols c{};
+    c.ncol = (int)cols.size();
+    c.rw = 0;
+    for (int k = 0; k < c.ncol; ++k) {
+      c.src[k] = P<const uint32_t>(std::get<0>(cols[k]));
+      c.dst[k] = P<uint32_t>(std::get<1>(cols[k]));
+      c.words[k] = std::get<2>(cols[k]);
+      c.rw += c.words[k];
+    }
+    return c;
+  };
+  m.def("xrows_blocks", &gpu::xrows_blocks);
+  m.def("gpu_xrows_count", [](intptr_t dest, int64_t n, int world, intptr_t blk, intptr_t counts,
+                              intptr_t bad, intptr_t stream) {
+    gpu::xrows_count(P<int64_t>(dest), n, world, P<uint32_t>(blk), P<uint32_t>(counts),
+                     P<uint32_t>(bad), stream);
+  });
+  m.def("gpu_xrows_scatter", [xcols](intptr_t dest, int64_t n, int world, intptr_t blk,
+                                     uint32_t cap, const std::vector<std::tuple<intptr_t, intptr_t, int>>& cols,
+                                     intptr_t send, intptr_t ovf, intptr_t stream) {
+    gpu::xrows_scatter(P<int64_t>(dest), n, world, P<uint32_t>(blk), cap, xcols(cols),
+                       P<uint32_t>(send), P<uint32_t>(ovf), stream);
+  });
+  m.def("gpu_xrows_unpack", [xcols](intptr_t recv, intptr_t rc, int world, uint32_t cap,
+                                    const std::vector<std::tuple<intptr_t, intptr_t, int>>& cols,
+                                    intptr_t stream) {
+    gpu::xrows_unpack(P<uint32_t>(recv), P<uint32_t>(rc), world, cap, xcols(cols), stream);
+  });
+  m.def("cpu_xrows_count", [](intptr_t dest, int64_t n, int world, intptr_t counts, intptr_t bad) {
+    cpu::xrows_count(P<int64_t>(dest), n, world, P<uint32_t>(counts), P<uint32_t>(bad));
+  });
+  m.def("cpu_xrows_scatter", [xcols](intptr_t dest, int64_t n, int world, uint32_t cap,
+                                     const std::vector<std::tuple<intptr_t, intptr_t, int>>& cols,
+                                     intptr_t send, intptr_t ovf) {
+    cpu::xrows_scatter(P<int64_t>(dest), n, world, cap, xcols(cols), P<uint32_t>(send),
+                       P<uint32_t>(ovf));
+  });
+  m.def("cpu_xrows_unpack", [xcols](intptr_t recv, intptr_t rc, int world, uint32_t cap,
+                                    const std::vector<std::tuple<intptr_t, intptr_t, int>>& cols) {
+    cpu::xrows_unpack(P<uint32_t>(recv), P<uint32_t>(rc), world, cap, xcols(cols));
+  });
   m.def("gpu_host_register", [](intptr_t p, int64_t bytes) {
     return gpu::host_register((void*)p, (size_t)bytes);
   });

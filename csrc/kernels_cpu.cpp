@@ -719,5 +719,50 @@ void tier_merge(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt, 
   }
 }
 
+// ---- packed-row exchange (twin of csrc/exchange_hip.hip) ------------------------------------
+void xrows_count(const int64_t* dest, int64_t n, int world, uint32_t* counts, uint32_t* bad) {
+  for (int d = 0; d < world; ++d) counts[d] = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (dest[i] >= 0 && dest[i] < world) ++counts[dest[i]];
+    else *bad |= 1u;
+  }
+}
+
+void xrows_scatter(const int64_t* dest, int64_t n, int world, uint32_t cap, const XRowCols& c,
+                   uint32_t* send, uint32_t* ovf) {
+  std::vector<uint32_t> pos((size_t)world, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t d = dest[i];
+    if (d < 0 || d >= world) continue;
+    const uint32_t p = pos[d]++;
+    if (p >= cap) {
+      *ovf |= 1u;
+      continue;
+    }
+    uint32_t* row = send + ((size_t)d * cap + p) * (size_t)c.rw;
+    int o = 0;
+    for (int k = 0; k < c.ncol; ++k) {
+      std::memcpy(row + o, c.src[k] + (size_t)i * c.words[k], sizeof(uint32_t) * c.words[k]);
+      o += c.words[k];
+    }
+  }
+}
+
+void xrows_unpack(const uint32_t* recv, const uint32_t* rc, int world, uint32_t cap,
+                  const XRowCols& c) {
+  size_t orow = 0;
+  for (int s = 0; s < world; ++s) {
+    const uint32_t m = rc[s] < cap ? rc[s] : cap;
+    for (uint32_t idx = 0; idx < m; ++idx, ++orow) {
+      const uint32_t* row = recv + ((size_t)s * cap + idx) * (size_t)c.rw;
+      int o = 0;
+      for (int k = 0; k < c.ncol; ++k) {
+        std::memcpy(c.dst[k] + orow * c.words[k], row + o, sizeof(uint32_t) * c.words[k]);
+        o += c.words[k];
+      }
+    }
+  }
+}
+
 }  // namespace cpu
 }  // namespace mxs

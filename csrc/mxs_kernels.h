@@ -159,7 +159,28 @@ struct IngestSpec;
 struct IngestOut;
 struct DictState;
 
+// Columns of a packed-row exchange (parallel/exchange.py): up to 8 columns whose rows are
+// whole 32-bit words; src = the sender's columns, dst = the receiver's compacted outputs.
+struct XRowCols {
+  const uint32_t* src[8];
+  uint32_t* dst[8];
+  int words[8];
+  int ncol;
+  int rw;  // words of one packed row (sum of words[])
+};
+
 namespace gpu {
+// Packed-row exchange (csrc/exchange_hip.hip): per-workgroup destination counts + their scan
+// (blk_cnt: xrows_blocks(n) x world words, scanned in place; counts: world totals), the stable
+// scatter into [world][cap] packed rows, and the receive-side compaction.
+int64_t xrows_blocks(int64_t n);
+void xrows_count(const int64_t* dest, int64_t n, int world, uint32_t* blk_cnt, uint32_t* counts,
+                 uint32_t* bad, intptr_t stream);
+void xrows_scatter(const int64_t* dest, int64_t n, int world, const uint32_t* blk_off,
+                   uint32_t cap, const XRowCols& c, uint32_t* send, uint32_t* ovf,
+                   intptr_t stream);
+void xrows_unpack(const uint32_t* recv, const uint32_t* rc, int world, uint32_t cap,
+                  const XRowCols& c, intptr_t stream);
 // print() rows in Java text (csrc/row_format.h): lengths (+ a flag for rows the device cannot
 // format), then, after an inclusive scan of the lengths into `end`, the bytes.
 void format_rows_len(const FmtArgs& a, int64_t n, int64_t* len, uint32_t* bad, intptr_t stream);
@@ -402,6 +423,12 @@ void tier_merge(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt, 
 
 // ---- CPU twins (kernels_cpu.cpp) ------------------------------------------------------------
 namespace cpu {
+// C++ twins of the packed-row exchange (same layouts; counts then stable scatter, unpack).
+void xrows_count(const int64_t* dest, int64_t n, int world, uint32_t* counts, uint32_t* bad);
+void xrows_scatter(const int64_t* dest, int64_t n, int world, uint32_t cap, const XRowCols& c,
+                   uint32_t* send, uint32_t* ovf);
+void xrows_unpack(const uint32_t* recv, const uint32_t* rc, int world, uint32_t cap,
+                  const XRowCols& c);
 void format_rows_len(const FmtArgs& a, int64_t n, int64_t* len, uint32_t* bad);
 void format_rows_write(const FmtArgs& a, int64_t n, const int64_t* end, char* out);
 void set_threads(int n);  // worker threads of the parallel CPU twins (expr_filter, ...)

@@ -26,7 +26,7 @@ ARCH = os.environ.get("MXS_OFFLOAD_ARCH", "gfx950")
 
 HIP_SOURCES = ["kernels_hip.hip", "sort_hip.hip", "parse_hip.hip", "vector_hip.hip",
                "check_hip.hip", "rolling_hist_hip.hip", "ingest_hip.hip", "listwin_hip.hip",
-               "format_hip.hip"]
+               "format_hip.hip", "exchange_hip.hip"]
 CXX_SOURCES = ["kernels_cpu.cpp", "ingest_cpu.cpp", "runtime.cpp", "sessions.cpp", "vector_cpu.cpp",
                "vector_bindings.cpp", "trace.cpp", "check_cpu.cpp", "reader.cpp", "format.cpp", "listwin_cpu.cpp",
                "listwin_bindings.cpp", "window_tier_bindings.cpp",

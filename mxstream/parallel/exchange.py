@@ -6,57 +6,84 @@ window/rolling/session partition kernels: the median pane arena's (key id, ts, f
 rolling operator's template rows). ``gather_rows(comm, cols)`` gives every rank every rank's
 rows (a replicated table's new entries).
 
-Shape of the exchange: ONE equal-split all-to-all per column of fixed-capacity
-per-destination slices -- the capacity is the largest slice over all ranks, one MAX all-reduce
-of an int64, so no count round trip precedes the payload -- plus an all-to-all of the
-per-destination counts. Received rows come back compacted in (source rank, source row) order,
-which keeps every key's rows in arrival order when each source sends its rows in order.
-On RCCL the slices move over xGMI peer links; LoopbackComm and gloo move the same layout.
+Shape of the exchange: the columns travel as ONE packed row (their 32-bit
+words back to back) in ONE equal-split all-to-all of fixed-capacity per-destination slices,
+built by the hand-written stable scatter of csrc/exchange_hip.hip (C++ twin on the CPU): no
+library sort, no per-column collective. The slice capacity is the largest per-destination count
+over all ranks (one MAX all-reduce), read on the host together with the received counts (one
+all-to-all of int32 counts) in the exchange's ONE host read, which sizes the outputs. Received
+rows come back compacted in (source rank, source row) order, which keeps every key's rows in
+arrival order when each source sends its rows in order. On RCCL the slices move over xGMI peer
+links; LoopbackComm and gloo move the same layout.
 """
 from __future__ import annotations
 
 import torch
 
 
-def _cap(comm, counts: torch.Tensor) -> int:
-    m = counts.max().reshape(1).to(torch.int64) if counts.numel() else \
-        torch.zeros(1, dtype=torch.int64, device=counts.device)
-    comm.allreduce_max_(m)
-    return int(m.item())
+def _words(c: torch.Tensor) -> int:
+    per = c.element_size()
+    for d in c.shape[1:]:
+        per *= d
+    if per % 4:
+        raise ValueError("exchange_rows: a row of every column must be whole 32-bit words")
+    return per // 4
 
 
 def exchange_rows(comm, dest: torch.Tensor, cols: list[torch.Tensor]) -> list[torch.Tensor]:
     """Rows to their destination ranks; returns the received columns (same dtypes and trailing
     shapes). Collective: every rank calls it, with or without rows."""
+    from ..ops.native import load
+
     world = comm.world
     dev = dest.device
     n = dest.numel()
     if world == 1:
         return [c[:n] for c in cols]
-    dest = dest.to(torch.int64)
-    counts = torch.bincount(dest, minlength=world)[:world] if n else \
-        torch.zeros(world, dtype=torch.int64, device=dev)
-    cap = _cap(comm, counts)
+    m = load()
+    gpu = dev.type == "cuda"
+    st = torch.cuda.current_stream(dev).cuda_stream if gpu else 0
+    dest = dest.to(torch.int64).contiguous()
+    cols = [c[:n].contiguous() for c in cols]
+    words = [_words(c) for c in cols]
+    rw = sum(words)
+    counts = torch.empty(world, dtype=torch.int32, device=dev)
+    flags = torch.zeros(1, dtype=torch.int32, device=dev)  # a destination outside [0, world)
+    if gpu:
+        blk = torch.empty(max(1, m.xrows_blocks(n) * world), dtype=torch.int32, device=dev)
+        m.gpu_xrows_count(dest.data_ptr(), n, world, blk.data_ptr(), counts.data_ptr(),
+                          flags.data_ptr(), st)
+    else:
+        m.cpu_xrows_count(dest.data_ptr(), n, world, counts.data_ptr(), flags.data_ptr())
+    mx = counts.max().to(torch.int64).reshape(1)
+    comm.allreduce_max_(mx)
     rc = torch.empty_like(counts)
     comm.all_to_all(rc, counts)
+    h = torch.cat([mx, flags.to(torch.int64), rc.to(torch.int64)]).cpu().tolist()  # one read
+    if h[1]:
+        raise ValueError("exchange_rows: a destination rank outside [0, world)")
+    cap = int(h[0])
     if cap == 0:
         return [c[:0] for c in cols]
-    # Stable order by destination: slot of row i = dest * cap + (rank among its destination).
-    order = torch.sort(dest, stable=True).indices if n else dest
-    starts = torch.cumsum(counts, 0) - counts
-    ds = dest[order]
-    pos = ds * cap + (torch.arange(n, device=dev, dtype=torch.int64) - starts[ds])
-    # Valid received rows: source slice s holds rc[s] rows at the front.
-    valid = (torch.arange(cap, device=dev).unsqueeze(0) < rc.unsqueeze(1)).reshape(-1)
-    out = []
-    for c in cols:
-        c = c[:n]
-        send = torch.zeros((world * cap,) + tuple(c.shape[1:]), dtype=c.dtype, device=dev)
-        send[pos] = c[order]
-        recv = torch.empty_like(send)
-        comm.all_to_all(_flat(recv), _flat(send))
-        out.append(recv[valid])
-    return out
+    total = sum(min(x, cap) for x in h[2:])
+    send = torch.empty(world * cap * rw, dtype=torch.int32, device=dev)
+    ovf = torch.zeros(1, dtype=torch.int32, device=dev)
+    spec_send = [(c.data_ptr(), 0, w) for c, w in zip(cols, words)]
+    if gpu:
+        m.gpu_xrows_scatter(dest.data_ptr(), n, world, blk.data_ptr(), cap, spec_send,
+                            send.data_ptr(), ovf.data_ptr(), st)
+    else:
+        m.cpu_xrows_scatter(dest.data_ptr(), n, world, cap, spec_send, send.data_ptr(),
+                            ovf.data_ptr())
+    recv = torch.empty_like(send)
+    comm.all_to_all(recv, send)
+    outs = [torch.empty((total,) + tuple(c.shape[1:]), dtype=c.dtype, device=dev) for c in cols]
+    spec_recv = [(0, o.data_ptr(), w) for o, w in zip(outs, words)]
+    if gpu:
+        m.gpu_xrows_unpack(recv.data_ptr(), rc.data_ptr(), world, cap, spec_recv, st)
+    else:
+        m.cpu_xrows_unpack(recv.data_ptr(), rc.data_ptr(), world, cap, spec_recv)
+    return outs
 
 
 def gather_rows(comm, cols: list[torch.Tensor]) -> list[torch.Tensor]:
