@@ -733,6 +733,10 @@ PYBIND11_MODULE(_mxs_native, m) {
                                     const std::vector<std::tuple<intptr_t, intptr_t, int>>& cols) {
     cpu::xrows_unpack(P<uint32_t>(recv), P<uint32_t>(rc), world, cap, xcols(cols));
   });
+  m.def("gpu_host_register_flags", [](intptr_t p, int64_t bytes, unsigned flags) {
+    py::gil_scoped_release nogil;
+    return (int)hipHostRegister((void*)p, (size_t)bytes, flags);
+  });
   m.def("gpu_host_register", [](intptr_t p, int64_t bytes) {
     return gpu::host_register((void*)p, (size_t)bytes);
   });

@@ -19,5 +19,6 @@ s = io.StringIO()
 st = pstats.Stats(prof, stream=s)
 st.sort_stats("tottime").print_stats(40)
 st.sort_stats("cumulative").print_stats(40)
+st.print_callers("torch.empty|absorb|export|query")
 with open(out, "w") as f:
     f.write(s.getvalue())
