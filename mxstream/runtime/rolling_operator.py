@@ -422,7 +422,10 @@ class KeyedRollingOperator:
     def check(self) -> int:
         """Host check of the sticky flags (table full, reserved key); returns the last step's
         emitted row count. to_host=False callers (benchmarks) call it at the end."""
-        hf = self.flags.tolist()
+        return self._check_flags(self.flags.tolist())
+
+    @staticmethod
+    def _check_flags(hf) -> int:
         if hf[0] & 1:
             raise RuntimeError("keyed state table full: a key found no free slot (raise max_keys)")
         if hf[0] & 4:
@@ -434,6 +437,22 @@ class KeyedRollingOperator:
     def _emit(self, to_host: bool):
         if not to_host:
             return self.out_n
+        if self.device.type == "cuda" and self.out_key.numel() % 2 == 0:
+            # One device-counted copy of the emitted rows and the sticky flags into a pinned slab
+            # (the copy kernel reads the row count itself) and ONE wait -- instead of a flag read
+            # plus three pageable D2H copies, each its own sync. The rows are copied out of the
+            # slab (callers may keep them), so the slab is free again at once.
+            from .window_operator import CountedHostRows, PinnedSlabPool
+
+            if getattr(self, "_emit_pool", None) is None:
+                self._emit_pool = PinnedSlabPool(max_slabs=4)
+            hr = CountedHostRows(self._emit_pool, [self.out_key, self.out_val, self.out_tag],
+                                 self.out_n, [self.flags])
+            hr.wait()
+            self._check_flags(hr.fixed(0).tolist())
+            k = min(int(hr.fixed(0)[2]), self.out_key.numel())
+            cols = hr.columns(k)
+            return RollingRows(cols[0].copy().view(np.uint64), cols[1].copy(), cols[2].copy())
         k = min(self.check(), self.out_key.numel())
         return RollingRows(self.out_key[:k].cpu().numpy().copy().view(np.uint64),
                            self.out_val[:k].cpu().numpy().copy(),
