@@ -1197,4 +1197,5 @@ PYBIND11_MODULE(_mxs_native, m) {
   bind_format(m);
   bind_listwin(m);
   bind_window_tier(m);
+  bind_window_control(m);
 }

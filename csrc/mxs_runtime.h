@@ -12,3 +12,4 @@ void bind_reader(pybind11::module_& m);
 void bind_format(pybind11::module_& m);
 void bind_listwin(pybind11::module_& m);
 void bind_window_tier(pybind11::module_& m);
+void bind_window_control(pybind11::module_& m);

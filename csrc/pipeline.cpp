@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "mxs_c.h"
+#include "window_control.h"
 #include "mxs_check.h"
 #include "mxs_kernels.h"
 #include "session_store.h"
@@ -125,7 +126,8 @@ void state_geometry(int64_t max_keys, int* nsub_out, int* cap_log2_out) {
 
 class WindowPipeline {
  public:
-  explicit WindowPipeline(const mxs_window_config& c) : cfg_(c) {
+  explicit WindowPipeline(const mxs_window_config& c)
+      : cfg_(c), ctl_(c.size_ms, c.slide_ms, c.offset_ms, c.lateness_ms) {
     if (c.size_ms <= 0 || c.slide_ms <= 0) throw std::invalid_argument("window size and slide must be positive");
     if (c.agg < AGG_SUM_I64 || c.agg > AGG_AVG_I64) throw std::invalid_argument("unknown aggregate");
     if (c.lateness_ms < 0 || c.ooo_bound_ms < 0) throw std::invalid_argument("negative lateness / bound");
@@ -134,20 +136,15 @@ class WindowPipeline {
       hip_ok(hipSetDevice(c.device_index), "hipSetDevice");
       hip_ok(hipStreamCreateWithFlags(&mem_.stream, hipStreamNonBlocking), "hipStreamCreate");
     }
-    size_ = c.size_ms;
-    slide_ = c.slide_ms;
-    offset_ = c.offset_ms;
-    lateness_ = c.lateness_ms;
     ooo_ = c.ooo_bound_ms;
     max_par_ = c.max_parallelism > 0 ? c.max_parallelism : 128;
-    pane_ = std::gcd(size_, slide_);
-    ppw_ = size_ / pane_;
+    const int64_t pane = ctl_.pane(), slide = c.slide_ms, lateness = c.lateness_ms;
     state_geometry(std::max<int64_t>(c.max_keys, 1), &nsub_, &cap_log2_);
     nsub_log2_ = 0;
     while ((1 << nsub_log2_) < nsub_) ++nsub_log2_;
     nslots_ = (int64_t)nsub_ << cap_log2_;
-    ring_ = std::max<int64_t>(4, next_pow2(ppw_ + 2 + (lateness_ + pane_ - 1) / pane_ +
-                                           (std::max(ooo_, slide_) + pane_ - 1) / pane_));
+    ring_ = std::max<int64_t>(4, next_pow2(ctl_.panes_per_window() + 2 + (lateness + pane - 1) / pane +
+                                           (std::max(ooo_, slide) + pane - 1) / pane));
     const bool int_agg = c.agg == AGG_SUM_I64 || c.agg == AGG_MIN_I64 || c.agg == AGG_MAX_I64 ||
                          c.agg == AGG_COUNT || c.agg == AGG_AVG_I64;
     compact_ = mem_.gpu && int_agg;
@@ -209,10 +206,10 @@ class WindowPipeline {
       pp.drop_late = 1;
       pp.hash_mode = 0;
       pp.bucket_cap = (uint32_t)bucket_cap_;
-      pp.late_ts = late_ts(old_wm);
-      pp.tbase = pane_start(pane_base);
-      pp.pane = pane_;
-      pp.inv_pane = 1.0 / (double)pane_;
+      pp.late_ts = ctl_.late_ts(old_wm);
+      pp.tbase = ctl_.pane_start(pane_base);
+      pp.pane = ctl_.pane();
+      pp.inv_pane = 1.0 / (double)ctl_.pane();
       pp.rec_words = compact_ ? 2 : 3;
       if (n) {
         if (mem_.gpu)
@@ -243,17 +240,10 @@ class WindowPipeline {
     late_dropped_ += host[8 + kStatLate];
     if (qmin <= qmax) {
       const int64_t gmin = pane_base + qmin, gmax = pane_base + qmax;
-      const int64_t lo = has_live_ ? std::min(min_live_, gmin) : gmin;
-      const int64_t hi = has_live_ ? std::max(max_seen_, gmax) : gmax;
-      if (hi - lo + 1 > ring_) grow_ring(hi - lo + 1);
-      min_live_ = lo;
-      max_seen_ = hi;
-      has_live_ = true;
-      int64_t cand = first_start_containing(pane_start(gmin));
-      if (old_wm > kMin) cand = std::max(cand, align_up((i128)old_wm - size_ + 2));
-      nfs_ = has_nfs_ ? std::min(nfs_, cand) : cand;
-      has_nfs_ = true;
-      const int64_t fhi = fired_hi();
+      const int64_t span = ctl_.live_span_with(gmin, gmax);
+      if (span > ring_) grow_ring(span);
+      ctl_.observe(gmin, gmax, old_wm);
+      const int64_t fhi = ctl_.fired_hi();
       const int64_t cap = (int64_t)1 << cap_log2_;
       const int64_t np = gmax - gmin + 1;
       const int64_t pg = std::max<int64_t>(1, std::min<int64_t>(np, (150 * 1024 - cap * 8) / (cap * 12)));
@@ -328,8 +318,8 @@ class WindowPipeline {
     uint32_t* ocnt = cnt_g_;
     uint8_t* odirty = dirty_g_;
     alloc_state(nr);
-    if (has_live_)
-      for (int64_t p = min_live_; p <= max_seen_; ++p) {
+    if (ctl_.has_live())
+      for (int64_t p = ctl_.min_live(); p <= ctl_.max_seen(); ++p) {
         const int64_t so = (p & (old - 1)) * nslots_, sn = (p & (nr - 1)) * nslots_;
         mem_.dev_copy(acc_g_ + sn, oacc + so, nslots_ * 8);
         mem_.dev_copy(cnt_g_ + sn, ocnt + so, nslots_ * 4);
@@ -342,28 +332,10 @@ class WindowPipeline {
     ring_ = nr;
   }
 
-  // ---- window arithmetic (Flink 1.8 TimeWindow / SlidingEventTimeWindows) ----
-  int64_t pane_of(i128 t) const { return clamp64(fdiv128(t - offset_, pane_)); }
-  int64_t pane_start(i128 p) const { return clamp64((i128)offset_ + p * pane_); }
-  i128 last_start(i128 t) const { return t - java_rem(t - offset_ + slide_, slide_); }
-  int64_t first_start_containing(i128 t) const {
-    const i128 ls = last_start(t);
-    return clamp64(ls - fdiv128(ls - (t - size_ + 1), slide_) * slide_);
-  }
-  int64_t align_up(i128 t) const {
-    const i128 ls = last_start(t);
-    return clamp64(ls >= t ? ls : ls + slide_);
-  }
-  int64_t fired_hi() const {
-    if (!has_nfs_) return kMin;
-    return pane_of((i128)nfs_ - slide_ + size_ - 1);
-  }
-  int64_t late_ts(int64_t wm) const {
-    if (wm == kMin) return kMin;
-    return align_up((i128)wm - size_ - lateness_ + 2);
-  }
+  // The step's base pane: from the watermark once there is one (every non-late element has
+  // ts >= wm - size - lateness + 1), else the batch's minimum timestamp.
   int64_t pane_base_of(int64_t n) {
-    if (wm_ > kMin) return pane_of((i128)wm_ - size_ - lateness_ + 1);
+    if (wm_ > kMin) return ctl_.pane_base_from_wm(wm_);
     int64_t m = kMax;
     if (n) {
       if (mem_.gpu) {
@@ -374,19 +346,14 @@ class WindowPipeline {
         for (int64_t i = 0; i < n; ++i) m = std::min(m, in_ts_[i]);
       }
     }
-    int64_t base = m != kMax ? pane_of(m) : 0;
-    if (has_live_) base = std::min(base, min_live_);
+    int64_t base = m != kMax ? ctl_.pane_of(m) : 0;
+    if (ctl_.has_live()) base = std::min(base, ctl_.min_live());
     return base;
-  }
-  bool overlaps_live(int64_t s) const {
-    if (!has_live_) return false;
-    const int64_t p0 = pane_of(s), p1 = p0 + ppw_ - 1;
-    return !(p1 < min_live_ || p0 > max_seen_);
   }
 
   void fire_window(int64_t s, bool only_dirty) {
-    const int64_t p0 = std::max(pane_of(s), min_live_);
-    const int64_t p1 = std::min(pane_of(s) + ppw_ - 1, max_seen_);
+    const auto pr = ctl_.window_panes(s);
+    const int64_t p0 = pr.first, p1 = pr.second;
     if (p1 < p0) return;
     const uint32_t zero = 0;
     mem_.to_dev(out_n_, &zero, 4);
@@ -399,7 +366,7 @@ class WindowPipeline {
     fp.nslots = nslots_;
     fp.p0 = p0;
     fp.wstart = (double)s;
-    fp.wend = (double)s + (double)size_;
+    fp.wend = (double)s + (double)ctl_.size();
     fp.out_cap = (uint32_t)nslots_;
     if (mem_.gpu)
       gpu::window_fire(keys_g_, acc_g_, cnt_g_, dirty_g_, fp, out_keys_, out_vals_, out_raw_,
@@ -419,59 +386,35 @@ class WindowPipeline {
     mem_.to_host(raw.data(), out_raw_, n * 8);
     mem_.to_host(c.data(), out_cnt_, n * 4);
     for (uint32_t i = 0; i < n; ++i)
-      results.push_back({s, clamp64((i128)s + size_), k[i], v[i], (int64_t)raw[i], c[i],
+      results.push_back({s, clamp64((i128)s + ctl_.size()), k[i], v[i], (int64_t)raw[i], c[i],
                          only_dirty ? 1 : 0});
   }
 
   void fire_ready(int64_t wm) {
-    if (!has_nfs_ || !has_live_) return;
-    int64_t s = nfs_;
-    const int64_t first_live = first_start_containing(pane_start(min_live_));
-    if (s < first_live) s = first_live;
-    const int64_t last_data_start = clamp64(last_start((i128)pane_start((i128)max_seen_ + 1) - 1));
-    while ((i128)s + size_ - 1 <= wm) {
-      if (s > last_data_start) {
-        s = std::max(s, align_up((i128)wm - size_ + 2));
-        break;
-      }
-      if (overlaps_live(s)) fire_window(s, false);
-      s += slide_;
-    }
-    nfs_ = s;
+    for (int64_t s : ctl_.take_due(wm)) fire_window(s, false);
   }
 
   void refire(int64_t pmin, int64_t pmax, int64_t old_wm) {
-    int64_t s = first_start_containing(pane_start(pmin));
-    const int64_t end_s = std::min<int64_t>(nfs_ - slide_, clamp64(last_start(pane_start(pmax))));
-    for (; s <= end_s; s += slide_)
-      if ((i128)s + size_ - 1 + lateness_ > old_wm) fire_window(s, true);
+    for (int64_t s : ctl_.refire_windows(pmin, pmax, old_wm)) fire_window(s, true);
     for (int64_t p = pmin; p <= pmax; ++p)
       mem_.fill(dirty_g_ + (p & (ring_ - 1)) * nslots_, 0, nslots_);
   }
 
   void purge(int64_t wm) {
-    if (!has_live_) return;
-    int64_t keep_from;
-    if (wm == kMax) keep_from = max_seen_ + 1;
-    else keep_from = pane_of(align_up((i128)wm - size_ - lateness_ + 2));
-    int64_t p = min_live_;
-    const int64_t stop = std::min(keep_from, max_seen_ + 1);
-    if (stop - p > ring_) p = stop - ring_;
-    for (; p < stop; ++p) {
+    const auto r = ctl_.purge_range(wm, ring_);
+    for (int64_t p = r.from; p < r.stop; ++p) {
       const int64_t so = (p & (ring_ - 1)) * nslots_;
       mem_.fill(acc_g_ + so, 0, nslots_ * 8);
       mem_.fill(cnt_g_ + so, 0, nslots_ * 4);
       mem_.fill(dirty_g_ + so, 0, nslots_);
     }
-    if (keep_from > min_live_) {
-      min_live_ = keep_from;
-      if (min_live_ > max_seen_) has_live_ = false;
-    }
+    ctl_.commit_purge(r.keep_from);
   }
 
   mxs_window_config cfg_;
+  WindowControl ctl_;  // window arithmetic + firing bookkeeping (shared with the Python operator)
   Mem mem_;
-  int64_t size_, slide_, offset_, lateness_, ooo_, pane_, ppw_, ring_, nslots_;
+  int64_t ooo_, ring_, nslots_;
   int max_par_, nsub_, cap_log2_, nsub_log2_;
   bool compact_ = false;
   int64_t batch_capacity_ = 0, bucket_cap_ = 0, in_cap_ = 0;
@@ -486,9 +429,7 @@ class WindowPipeline {
   int32_t* kg_dest_ = nullptr;
   double* out_vals_ = nullptr;
   Rec* send_ = nullptr;
-  // firing bookkeeping (identical to KeyedWindowOperator)
-  int64_t wm_ = kMin, nfs_ = 0, min_live_ = 0, max_seen_ = 0;
-  bool has_nfs_ = false, has_live_ = false;
+  int64_t wm_ = kMin;
   int64_t records_in_ = 0, late_dropped_ = 0, steps_ = 0;
 };
 

@@ -29,7 +29,7 @@ HIP_SOURCES = ["kernels_hip.hip", "sort_hip.hip", "parse_hip.hip", "vector_hip.h
                "format_hip.hip", "exchange_hip.hip"]
 CXX_SOURCES = ["kernels_cpu.cpp", "ingest_cpu.cpp", "runtime.cpp", "sessions.cpp", "vector_cpu.cpp",
                "vector_bindings.cpp", "trace.cpp", "check_cpu.cpp", "reader.cpp", "format.cpp", "listwin_cpu.cpp",
-               "listwin_bindings.cpp", "window_tier_bindings.cpp",
+               "listwin_bindings.cpp", "window_tier_bindings.cpp", "window_control_bindings.cpp",
                "bindings.cpp"]
 # roctx ranges (csrc/trace.cpp) come from the ROCm profiler SDK's marker library.
 LINK_LIBS = ["-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]

@@ -32,7 +32,7 @@ import torch
 
 from ..ops import kernels as K
 from ..ops.native import load
-from .window_operator import OperatorMetrics, java_window_start
+from .window_operator import OperatorMetrics
 
 I64_MIN, I64_MAX = K.I64_MIN, K.I64_MAX
 _MAX_DENSE = 1 << 24  # key range of the direct counting sort
@@ -59,6 +59,7 @@ class KeyedListWindowOperator:
         self.metrics = OperatorMetrics()
         self.late_side: list = []
         self._m = load()
+        self._ctl = self._m.WindowControl(self.size, self.slide, self.offset, self.lateness)
         # Pane arena: ring slot -> absolute pane id (or None), buffers, fill, key range.
         self.ring = _next_pow2(self.ppw + -(-self.lateness // self.pane) + 2)
         self._alloc_ring(self.ring)
@@ -167,21 +168,18 @@ class KeyedListWindowOperator:
         return torch.cuda.current_stream(self.device).cuda_stream if self.cuda else 0
 
     # ---- window arithmetic ----------------------------------------------------------------
+    # Flink window arithmetic: the shared C++ implementation (csrc/window_control.h).
     def _pane_of(self, t):
-        return (t - self.offset) // self.pane
+        return self._ctl.pane_of(t)
 
     def _late_ts(self) -> int:
-        if self.wm == I64_MIN or self.time_mode != "event":
-            return I64_MIN
-        return self._align_up(self.wm - self.size - self.lateness + 2)
+        return self._ctl.late_ts(self.wm, self.time_mode == "event")
 
     def _align_up(self, t: int) -> int:
-        ls = java_window_start(t, self.offset, self.slide)
-        return ls if ls >= t else ls + self.slide
+        return self._ctl.align_up(t)
 
     def _first_start_containing(self, t: int) -> int:
-        ls = java_window_start(t, self.offset, self.slide)
-        return ls - ((ls - (t - self.size + 1)) // self.slide) * self.slide
+        return self._ctl.first_start_containing(t)
 
     # ---- ingest ---------------------------------------------------------------------------
     def process(self, keys: torch.Tensor, ts: torch.Tensor, vals_f64: torch.Tensor) -> list:

@@ -261,17 +261,6 @@ def _next_pow2(x: int) -> int:
     return 1 << max(0, int(x - 1).bit_length())
 
 
-def java_rem(a: int, b: int) -> int:
-    """Java's `%` on long (truncated remainder, sign of the dividend)."""
-    r = abs(a) % abs(b)
-    return -r if a < 0 else r
-
-
-def java_window_start(ts: int, offset: int, size: int) -> int:
-    """TimeWindow.getWindowStartWithOffset with Java's truncated remainder."""
-    return ts - java_rem(ts - offset + size, size)
-
-
 def combine_partials(agg: int, acc: torch.Tensor, inv: torch.Tensor, n: int) -> torch.Tensor:
     """Fold rows of exported accumulators (int64 bit patterns) into n groups (`inv`: group of
     each row) with the aggregate's combine: sum / min / max over int64 or float64 values."""
@@ -426,8 +415,13 @@ class KeyedWindowOperator:
         if size <= 0 or slide <= 0:
             raise ValueError("window size and slide must be positive")
         self.size, self.slide, self.offset, self.lateness = int(size), int(slide), int(offset), int(lateness)
-        self.pane = math.gcd(self.size, self.slide)
-        self.panes_per_window = self.size // self.pane
+        # Window arithmetic and the firing / re-firing / purge bookkeeping: the C++ state machine
+        # the C ABI pipeline runs too (csrc/window_control.h).
+        from ..ops.native import load as _load_native
+
+        self._ctl = _load_native().WindowControl(self.size, self.slide, self.offset, self.lateness)
+        self.pane = self._ctl.pane
+        self.panes_per_window = self._ctl.panes_per_window
         self.agg = agg
         self.time_mode = time_mode
         if time_mode not in ("event", "processing"):
@@ -673,9 +667,7 @@ class KeyedWindowOperator:
 
         # ---- watermark / firing bookkeeping (host, identical on every rank) ----
         self.wm = I64_MIN
-        self.next_fire_start: int | None = None   # smallest window start not yet passed
-        self.min_live_pane: int | None = None      # oldest unpurged pane
-        self.max_seen_pane: int | None = None
+        # next_fire_start / min_live_pane / max_seen_pane: properties over self._ctl (unset)
         self.late_side: list[np.ndarray] = []
 
     _local_global_ok = True  # subclasses whose fire is not a plain reduce opt out
@@ -892,32 +884,61 @@ class KeyedWindowOperator:
         self.acc_g, self.cnt_g, self.dirty_g, self.ring = acc, cnt, dirty, new_ring
         self.metrics.ring_regrows += 1
 
-    # ---- window arithmetic -------------------------------------------------------------
+    # ---- window arithmetic + bookkeeping (csrc/window_control.h) ---------------------------
     def pane_of(self, t: int) -> int:
-        return (t - self.offset) // self.pane
+        return self._ctl.pane_of(t)
 
     def pane_start(self, p: int) -> int:
-        return self.offset + p * self.pane
+        return self._ctl.pane_start(p)
 
     def last_start(self, t: int) -> int:
-        return java_window_start(t, self.offset, self.slide)
+        return self._ctl.last_start(t)
 
     def first_start_containing(self, t: int) -> int:
-        ls = self.last_start(t)
-        return ls - ((ls - (t - self.size + 1)) // self.slide) * self.slide
+        return self._ctl.first_start_containing(t)
 
     def _fired_hi(self) -> int:
-        if self.next_fire_start is None:
-            return I64_MIN
-        last_passed_end = self.next_fire_start - self.slide + self.size
-        return self.pane_of(last_passed_end - 1)
+        return self._ctl.fired_hi()
+
+    @property
+    def next_fire_start(self) -> int | None:
+        """Smallest window start not yet evaluated (None: no data yet)."""
+        return self._ctl.nfs() if self._ctl.has_nfs() else None
+
+    @next_fire_start.setter
+    def next_fire_start(self, v: int | None) -> None:
+        self._ctl.set_nfs(v is not None, 0 if v is None else int(v))
+
+    @property
+    def min_live_pane(self) -> int | None:
+        return self._ctl.min_live() if self._ctl.has_live() else None
+
+    @min_live_pane.setter
+    def min_live_pane(self, v: int | None) -> None:
+        c = self._ctl
+        if v is None:
+            c.set_live(False, 0, 0)
+        else:
+            c.set_live(True, int(v), c.max_seen() if c.has_live() else int(v))
+
+    @property
+    def max_seen_pane(self) -> int | None:
+        return self._ctl.max_seen() if self._ctl.has_live() else None
+
+    @max_seen_pane.setter
+    def max_seen_pane(self, v: int | None) -> None:
+        c = self._ctl
+        if v is None:
+            c.set_live(False, 0, 0)
+        else:
+            c.set_live(True, c.min_live() if c.has_live() else int(v), int(v))
 
     # ---- main entry points ---------------------------------------------------------------
     def _pane_base(self, ts: torch.Tensor) -> int:
         """Base pane of the step, identical on every rank (records carry pane - base)."""
         if self.wm > I64_MIN:
             # Every non-late element has ts >= wm - size - lateness + 1.
-            return self.pane_of(self.wm - self.size - self.lateness + 1)
+            return self._ctl.pane_base_from_wm(self.wm)
         # No watermark yet: the global minimum timestamp (one MIN all-reduce, first steps only).
         t = ts.min().reshape(1) if ts.numel() else torch.full((1,), I64_MAX, dtype=torch.int64,
                                                                 device=ts.device)
@@ -930,9 +951,7 @@ class KeyedWindowOperator:
 
     def _late_ts(self, wm: int) -> int:
         """Smallest window start whose cleanup time (maxTs + lateness) is after `wm`."""
-        if wm == I64_MIN or self.time_mode != "event":
-            return I64_MIN
-        return self._align_up(wm - self.size - self.lateness + 2)
+        return self._ctl.late_ts(wm, self.time_mode == "event")
 
     def current_processing_time(self) -> int:
         import time
@@ -976,18 +995,9 @@ class KeyedWindowOperator:
     def _due_windows(self, b: "_Back") -> int:
         """Windows the state half of settled step `b` will fire or re-fire (host bookkeeping,
         an upper bound: windows without live panes are counted too)."""
-        n = 0
-        if b.has_data and b.gmin <= b.fired_hi:  # late-but-allowed data: re-firings
-            s0 = self.first_start_containing(self.pane_start(b.gmin))
-            s1 = min(self.next_fire_start - self.slide,
-                     self.last_start(self.pane_start(min(b.gmax, b.fired_hi))))
-            if s1 >= s0:
-                n += (s1 - s0) // self.slide + 1
-        if b.new_wm is not None and self.next_fire_start is not None:
-            last = b.new_wm - self.size + 1  # windows with start <= last are due
-            if last >= self.next_fire_start:
-                n += (last - self.next_fire_start) // self.slide + 1
-        return n
+        return self._ctl.due_count(bool(b.has_data), b.gmin if b.has_data else 0,
+                                   b.gmax if b.has_data else 0, b.fired_hi,
+                                   b.new_wm is not None, b.new_wm or 0)
 
     def flush(self) -> list[FireResult]:
         """Complete the pending state half of the last batch (pipelined mode); returns what it
@@ -1143,21 +1153,14 @@ class KeyedWindowOperator:
                   maxb=int(st[K.STAT_MAXBUCKET]), seq=self.metrics.steps + 1)
         if qmin <= qmax:
             gmin, gmax = f.pane_base + qmin, f.pane_base + qmax
-            lo = gmin if self.min_live_pane is None else min(self.min_live_pane, gmin)
-            hi = gmax if self.max_seen_pane is None else max(self.max_seen_pane, gmax)
-            if hi - lo + 1 > self.ring:
+            span = self._ctl.live_span_with(gmin, gmax)
+            if span > self.ring:
                 self._drain()
-                self._grow_ring(hi - lo + 1)
-            self.min_live_pane, self.max_seen_pane = lo, hi
-            # Invariant: every window starting before next_fire_start is due (maxTs <= wm) and
-            # has been evaluated. New data can belong to not-yet-due windows before the current
-            # cursor (older but not late): lower the cursor to the first such window. Windows
-            # that are already due and receive data (allowed lateness) go through _refire.
-            cand = self.first_start_containing(self.pane_start(gmin))
-            if f.old_wm > I64_MIN:
-                cand = max(cand, self._align_up(f.old_wm - self.size + 2))
-            self.next_fire_start = cand if self.next_fire_start is None else min(self.next_fire_start, cand)
-            b.fired_hi = self._fired_hi()
+                self._grow_ring(span)
+            # live range += [gmin, gmax]; the fire cursor moves back to the first not-yet-due
+            # window holding new data (due windows receiving data re-fire: _refire)
+            self._ctl.observe(gmin, gmax, f.old_wm)
+            b.fired_hi = self._ctl.fired_hi()
             cap = 1 << self.cap_log2
             lds_budget = 150 * 1024 - cap * 8 - (cap * 4 + cap // 8 + 16
                                                  if self.dlist is not None else 0)
@@ -1481,11 +1484,7 @@ class KeyedWindowOperator:
 
     # ---- firing ---------------------------------------------------------------------------
     def _window_overlaps_live(self, s: int) -> bool:
-        if self.min_live_pane is None:
-            return False
-        p0 = self.pane_of(s)
-        p1 = p0 + self.panes_per_window - 1
-        return not (p1 < self.min_live_pane or p0 > self.max_seen_pane)
+        return self._ctl.overlaps_live(s)
 
     def _claim(self, which: str = "_out_busy") -> None:
         """Before a firing overwrites an output buffer: the current stream waits for the
@@ -1500,8 +1499,7 @@ class KeyedWindowOperator:
         # never held data and their ring slots belong to other panes (aliasing).
         if self.device.type == "cuda":
             self._claim()
-        p0 = max(self.pane_of(s), self.min_live_pane)
-        p1 = min(self.pane_of(s) + self.panes_per_window - 1, self.max_seen_pane)
+        p0, p1 = self._ctl.window_panes(s)
         if p1 < p0:
             return None
         if self.local_global:
@@ -1922,8 +1920,7 @@ class KeyedWindowOperator:
             plan.update(list=self.dlist.data_ptr(), list_n=self.dlist_n.data_ptr())
         wins = []
         for s in starts:
-            p0 = max(self.pane_of(s), self.min_live_pane)
-            p1 = min(self.pane_of(s) + self.panes_per_window - 1, self.max_seen_pane)
+            p0, p1 = self._ctl.window_panes(s)
             if p1 >= p0:
                 wins.append((s, (p0, p1 - p0 + 1, float(s), float(s + self.size))))
         stream = torch.cuda.current_stream(self.device).cuda_stream if cuda else 0
@@ -2039,44 +2036,17 @@ class KeyedWindowOperator:
         return tuple(ptrs) + (self.nslots,)
 
     def _fire_ready(self, wm: int) -> list[FireResult]:
-        out: list[FireResult] = []
-        if self.next_fire_start is None or self.max_seen_pane is None:
-            return out
-        s = self.next_fire_start
-        # Skip windows that cannot hold data (before the oldest live pane).
-        first_live = self.first_start_containing(self.pane_start(self.min_live_pane))
-        if s < first_live:
-            s = first_live
-        last_data_start = self.last_start(self.pane_start(self.max_seen_pane + 1) - 1)
-        due = []
-        while s + self.size - 1 <= wm:
-            if s > last_data_start:
-                # No window beyond the newest pane holds data: jump to the first window that can.
-                s = max(s, self._align_up(wm - self.size + 2))
-                break
-            if self._window_overlaps_live(s):
-                due.append(s)
-            s += self.slide
-        out.extend(self._fire_list(due, only_dirty=False))
-        self.next_fire_start = s
-        return out
+        """Fire every window the watermark makes due (the cursor moves past them)."""
+        return self._fire_list(self._ctl.take_due(wm), only_dirty=False)
 
     def _align_up(self, t: int) -> int:
         """Smallest window start >= t."""
-        ls = self.last_start(t)
-        return ls if ls >= t else ls + self.slide
+        return self._ctl.align_up(t)
 
     def _refire(self, pmin: int, pmax: int, old_wm: int) -> list[FireResult]:
         self._verify_combine()
         out: list[FireResult] = []
-        s = self.first_start_containing(self.pane_start(pmin))
-        end_s = min(self.next_fire_start - self.slide, self.last_start(self.pane_start(pmax)))
-        due = []
-        while s <= end_s:
-            if s + self.size - 1 + self.lateness > old_wm:
-                due.append(s)
-            s += self.slide
-        out.extend(self._fire_list(due, only_dirty=True))
+        out.extend(self._fire_list(self._ctl.refire_windows(pmin, pmax, old_wm), only_dirty=True))
         if self.dlist is not None:
             K.dirty_clear(self.dlist, self.dlist_n, ring=self.ring, nslots=self.nslots,
                           dirty_g=self.dirty_g, slot_mark=self.slot_mark, p_lo=pmin,
@@ -2091,19 +2061,12 @@ class KeyedWindowOperator:
     def _purge(self, wm: int) -> None:
         if self.min_live_pane is None:
             return
-        if wm == I64_MAX:
-            keep_from = self.max_seen_pane + 1
-        else:
-            # Earliest window that is not cleaned: s + size - 1 + lateness > wm.
-            s = self._align_up(wm - self.size - self.lateness + 2)
-            keep_from = self.pane_of(s)
+        # keep_from: first pane of the earliest window not cleaned (s + size - 1 + lateness > wm);
+        # panes [p, stop) are zeroed (at most one ring of them)
+        keep_from, p, stop = self._ctl.purge_range(wm, self.ring)
         if self.host_tier is not None:
             self._land_evictions()
             self.host_tier.purge(keep_from)
-        p = self.min_live_pane
-        stop = min(keep_from, self.max_seen_pane + 1)
-        if stop - p > self.ring:
-            p = stop - self.ring
         if p < stop:
             self._verify_combine()  # a redo must not land in a zeroed pane
         while p < stop:  # at most two runs of consecutive ring positions (wrap-around)
@@ -2111,11 +2074,7 @@ class KeyedWindowOperator:
             k = min(stop - p, self.ring - r)
             self._zero_pane(r * self.nslots, k)
             p += k
-        if keep_from > self.min_live_pane:
-            self.min_live_pane = keep_from
-            if self.min_live_pane > self.max_seen_pane:
-                self.min_live_pane = None
-                self.max_seen_pane = None
+        self._ctl.commit_purge(keep_from)
 
     # ---- introspection ---------------------------------------------------------------------
     def state_bytes(self) -> int:
