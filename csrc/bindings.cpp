@@ -983,6 +983,14 @@ PYBIND11_MODULE(_mxs_native, m) {
     gpu::session_promote(P<int64_t>(slots), P<int64_t>(rec), P<int64_t>(last), n, P<int64_t>(sess),
                          P<int64_t>(due), P<int64_t>(slast), P<uint32_t>(n_bad), stream);
   });
+  m.def("gpu_session_promote_rows", [](intptr_t rows, int64_t n, int nsub_log2, int cap_log2,
+                                       intptr_t keys_g, intptr_t slots, intptr_t sess, intptr_t due,
+                                       intptr_t slast, intptr_t ins, intptr_t n_bad,
+                                       intptr_t stream) {
+    gpu::session_promote_rows(P<int64_t>(rows), n, nsub_log2, cap_log2, P<uint64_t>(keys_g),
+                              P<int64_t>(slots), P<int64_t>(sess), P<int64_t>(due),
+                              P<int64_t>(slast), P<uint32_t>(ins), P<uint32_t>(n_bad), stream);
+  });
   m.def("gpu_set_rehash", [](intptr_t old, int64_t n_old, intptr_t neu, uint32_t new_mask,
                              intptr_t stream) {
     gpu::set_rehash(P<uint64_t>(old), n_old, P<uint64_t>(neu), new_mask, stream);

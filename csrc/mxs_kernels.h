@@ -370,6 +370,10 @@ void set_insert_keys(uint64_t* set, uint32_t mask, const int64_t* keys, int64_t 
 void set_probe(const uint64_t* set, uint32_t mask, const int64_t* keys, int64_t n, uint8_t* hit,
                uint32_t* n_hit, intptr_t stream);
 // Insert keys into the session slot table (tombstone reuse); slot -1 when a sub-table is full.
+void session_promote_rows(const int64_t* rows, int64_t n, int nsub_log2, int cap_log2,
+                          uint64_t* keys_g, int64_t* slots, int64_t* sess, int64_t* slot_due,
+                          int64_t* slot_last, uint32_t* inserted, uint32_t* n_bad,
+                          intptr_t stream);
 void session_promote(const int64_t* slots, const int64_t* rec, const int64_t* last, int64_t n,
                      int64_t* sess, int64_t* slot_due, int64_t* slot_last, uint32_t* n_bad,
                      intptr_t stream);

@@ -162,6 +162,13 @@ class ShardedCore {
     for (auto& m : mv) moved->insert(moved->end(), m.begin(), m.end());
     return out;
   }
+  // The promote path's dense extract (SessionCore::extract_dense_into); a sharded store
+  // returns -1 (the caller takes the general extract).
+  int64_t extract_dense_into(const int64_t* keys, int64_t n, int64_t wm, int64_t gap,
+                             int64_t* rows, int64_t cap) {
+    if (shards() != 1) return -1;
+    return sh_[0]->extract_dense_into(keys, n, wm, gap, rows, cap);
+  }
   void fire(int64_t wm, const ExprProg& mp, const ExprProg& fp, SessionCore::FireOut& o,
             bool expire_cold = true) {
     if (shards() == 1) return sh_[0]->fire(wm, mp, fp, o, expire_cold);

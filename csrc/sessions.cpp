@@ -181,6 +181,19 @@ class SessionStore {
     d["moved"] = to_np(moved);
     return d;
   }
+  // The promote path's fast extract (sessions of the wanted keys leave the store): when every
+  // wanted key is cold with at most one live session, writes one row of 6 int64 {key, start,
+  // end, acc, cnt | flags << 32, end - gap} per kept key into `out` (caller memory, cap rows, in
+  // no particular order) and returns the row count; -1 (nothing changed) when not applicable --
+  // the caller falls back to extract_packed. `keys` must be distinct.
+  int64_t extract_dense_into_np(const I64Array& keys, int64_t wm, int64_t gap, intptr_t out,
+                                int64_t cap) {
+    py::gil_scoped_release nogil;
+    join_all();
+    std::lock_guard<std::mutex> g(mu_);
+    return c_.extract_dense_into(keys.data(), keys.size(), wm, gap,
+                                 reinterpret_cast<int64_t*>(out), cap);
+  }
   // Fire / clean up everything the watermark allows. Returns columns of emitted rows plus the
   // keys that left the store ("released"). Waits only for the hot phase of queued evictions.
   py::dict fire_np(int64_t wm, std::vector<int32_t> map_code, std::vector<double> map_consts,
@@ -474,6 +487,7 @@ void bind_sessions(py::module_& m) {
       .def("merge_runs", &SessionStore::merge_runs_np)
       .def("extract", &SessionStore::extract_np)
       .def("extract_packed", &SessionStore::extract_packed_np)
+      .def("extract_dense_into", &SessionStore::extract_dense_into_np)
       .def("fire", &SessionStore::fire_np, py::arg("wm"), py::arg("map_code"),
            py::arg("map_consts"), py::arg("f_code"), py::arg("f_consts"),
            py::arg("expire_cold") = true)

@@ -6,10 +6,12 @@
 // most the chunks that straddle it. No Python in here (csrc/window_tier_bindings.cpp binds it).
 #pragma once
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <deque>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <thread>
 #include <utility>
@@ -92,6 +94,9 @@ class WindowTierCore {
   // A copy (the frozen tier of an asynchronous snapshot) leaves the spare columns behind.
   WindowTierCore(const WindowTierCore& o)
       : agg_(o.agg_), chunks_(o.chunks_), rows_(o.rows_), rows_in_(o.rows_in_) {}
+  ~WindowTierCore() {
+    if (pf_.joinable()) pf_.join();
+  }
 
   int agg() const { return agg_; }
   size_t nrows() const { return rows_; }
@@ -125,18 +130,11 @@ class WindowTierCore {
       c.pmax = std::max(c.pmax, pane[i]);
     }
     if ((uint64_t)(c.pmax - c.pmin) < ((uint64_t)1 << 20)) {
-      if (!spare_.empty()) {
-        // A purged chunk's columns: capacity whose pages are already mapped (fresh columns of a
-        // 5M-row eviction page-fault ~190 MB in).
-        Chunk& sp = spare_.back();
-        c.key.swap(sp.key);
-        c.pane.swap(sp.pane);
-        c.acc.swap(sp.acc);
-        c.cnt.swap(sp.cnt);
-        c.dirty.swap(sp.dirty);
-        spare_.pop_back();
-      }
+      // A purged or pre-faulted chunk's columns: capacity whose pages are already mapped
+      // (fresh columns of a 5M-row eviction page-fault ~190 MB in).
+      take_spare(c, n);
       absorb_sorted(c, key, pane, acc, cnt, dirty, n);
+      prefault_async(n);
     } else {
       c.key.assign(key, key + n);
       c.pane.assign(pane, pane + n);
@@ -163,15 +161,7 @@ class WindowTierCore {
       }
     if (!n) return;
     Chunk c;
-    if (!spare_.empty()) {
-      Chunk& sp = spare_.back();
-      c.key.swap(sp.key);
-      c.pane.swap(sp.pane);
-      c.acc.swap(sp.acc);
-      c.cnt.swap(sp.cnt);
-      c.dirty.swap(sp.dirty);
-      spare_.pop_back();
-    }
+    take_spare(c, n);
     c.pmin = p0 + j0;
     c.pmax = p0 + j1;
     const size_t P = (size_t)(j1 - j0 + 1);
@@ -208,6 +198,7 @@ class WindowTierCore {
     rows_ += n;
     rows_in_ += (int64_t)n;
     chunks_.push_back(std::move(c));
+    prefault_async(n);
   }
 
   // The tier's share of the window over panes [p0, p1]: one (key, acc, cnt) per key, keys
@@ -551,7 +542,7 @@ class WindowTierCore {
       const int64_t kf = std::max(keep_from, c.live_from);
       if (c.pmax < kf) {
         rows_ -= c.size() - c.dead;
-        if (c.sorted && spare_.size() < 2) spare_.push_back(std::move(c));
+        if (c.sorted) give_spare(std::move(c));
         continue;
       }
       if (c.sorted && c.pmin < kf) {  // dead rows are the prefix below kf's segment
@@ -650,9 +641,18 @@ class WindowTierCore {
   }
 
   void clear() {
+    if (pf_.joinable()) pf_.join();
     chunks_.clear();
     spare_.clear();
     rows_ = 0;
+  }
+  // Spare chunks held for the next absorb (tests / metrics).
+  size_t spare_chunks() {
+    std::lock_guard<std::mutex> g(sp_mu_);
+    return spare_.size();
+  }
+  void join_prefault() {
+    if (pf_.joinable()) pf_.join();
   }
 
  private:
@@ -721,10 +721,76 @@ class WindowTierCore {
     // (pmin / pmax may bound panes whose rows were all zero-count: harmless)
   }
 
+  // Spare columns for the next absorb: the spare with the most capacity (an eviction of n rows
+  // into fresh columns pays its page faults -- ~10 GB/s of first touch -- on the caller).
+  void take_spare(Chunk& c, size_t n) {
+    std::lock_guard<std::mutex> g(sp_mu_);
+    if (spare_.empty()) return;
+    size_t best = 0;
+    for (size_t i = 1; i < spare_.size(); ++i)
+      if (spare_[i].key.capacity() > spare_[best].key.capacity()) best = i;
+    (void)n;
+    Chunk& sp = spare_[best];
+    c.key.swap(sp.key);
+    c.pane.swap(sp.pane);
+    c.acc.swap(sp.acc);
+    c.cnt.swap(sp.cnt);
+    c.dirty.swap(sp.dirty);
+    spare_.erase(spare_.begin() + (std::ptrdiff_t)best);
+  }
+  void give_spare(Chunk&& c) {
+    std::lock_guard<std::mutex> g(sp_mu_);
+    if (spare_.size() >= kMaxSpare) return;  // freed
+    c.key.clear();
+    c.pane.clear();
+    c.acc.clear();
+    c.cnt.clear();
+    c.dirty.clear();
+    spare_.push_back(std::move(c));
+  }
+  // After an absorb of n rows: unless a spare already holds 1.25 n rows, a background thread
+  // maps and touches the columns of the next one (the next eviction is of similar size), so the
+  // page faults run beside the stream's next steps instead of inside the next absorb.
+  void prefault_async(size_t n) {
+    const size_t want = n + n / 4;
+    {
+      std::lock_guard<std::mutex> g(sp_mu_);
+      for (auto& sp : spare_)
+        if (sp.key.capacity() >= want) return;
+      if (spare_.size() >= kMaxSpare) return;
+    }
+    if (pf_.joinable()) {
+      if (!pf_done_.load(std::memory_order_acquire)) return;  // one at a time
+      pf_.join();
+    }
+    pf_done_.store(false, std::memory_order_relaxed);
+    pf_ = std::thread([this, want] {
+      Chunk c;
+      touch(c.key, want);
+      touch(c.pane, want);
+      touch(c.acc, want);
+      touch(c.cnt, want);
+      touch(c.dirty, want);
+      give_spare(std::move(c));
+      pf_done_.store(true, std::memory_order_release);
+    });
+  }
+  template <class V>
+  static void touch(V& v, size_t n) {
+    v.resize(n);
+    auto* b = reinterpret_cast<volatile unsigned char*>(v.data());
+    const size_t bytes = n * sizeof(typename V::value_type);
+    for (size_t o = 0; o < bytes; o += 4096) b[o] = 0;
+  }
+  static constexpr size_t kMaxSpare = 3;
+
   int agg_;
 
   std::deque<Chunk> chunks_;
-  std::vector<Chunk> spare_;  // purged pane-sorted chunks whose columns absorb() reuses
+  std::mutex sp_mu_;
+  std::thread pf_;
+  std::atomic<bool> pf_done_{true};
+  std::vector<Chunk> spare_;  // purged / pre-faulted chunks whose columns absorb() reuses
   size_t rows_ = 0;
   int64_t rows_in_ = 0;
 };

@@ -69,6 +69,9 @@ _SPILL_SIDE_STREAM = __import__("os").environ.get("MXS_SPILL_SIDE_STREAM", "1") 
 # partition ("1", default; a value outside int32 widens the step to 24-byte records and redoes
 # it) or the 24-byte plain scatter ("0", A/B).
 _REC16 = __import__("os").environ.get("MXS_SESSION_REC16", "1") != "0"
+# Promotion of revisited spilled keys through the dense-row fast path (SessionStore.
+# extract_dense_into + session_promote_rows); "0": always the general extract_packed (A/B).
+_PROMOTE_DENSE = __import__("os").environ.get("MXS_PROMOTE_DENSE", "1") != "0"
 
 
 def _next_pow2(x: int) -> int:
@@ -109,6 +112,8 @@ class SessionMetrics:
     rehashes: int = 0
     promoted_keys: int = 0      # spilled keys handed back to HBM (records arrived for them)
     records_promoted: int = 0   # records of those keys folded on the GPU instead of the host
+    promote_dense: int = 0      # promotions that took the dense-row fast path
+    promote_fallbacks: int = 0  # promotions the fast path declined (extract_packed instead)
     current_watermark: int = I64_MIN
     steps: int = 0
     extra: dict = field(default_factory=dict)
@@ -634,13 +639,20 @@ class KeyedSessionOperator:
                           for x in self._diverted(n_host, tbase))
             dev = self.device
             with self._phase("promote.extract"):
-                # One C++ pass: the keys' sessions leave the store already laid out as HBM slot
-                # records ([key][kSess][start, end, acc, cnt | flags << 32]) + last activity.
-                ex = self.store.extract_packed(torch.unique(dk).cpu().numpy(), wm, K_SESS,
-                                               self.gap)
-            moved = ex["moved"]
-            nk = len(ex["key"])
-            if nk:
+                uk = torch.unique(dk)
+                ukh = uk.cpu().numpy()
+                nd = self._promote_dense(uk, ukh, wm)
+                if nd is None:
+                    # One C++ pass: the keys' sessions leave the store already laid out as HBM
+                    # slot records ([key][kSess][start, end, acc, cnt | flags << 32]) + last
+                    # activity.
+                    ex = self.store.extract_packed(ukh, wm, K_SESS, self.gap)
+            if nd is not None:
+                moved = ukh
+            else:
+                moved = ex["moved"]
+                nk = len(ex["key"])
+            if nd is None and nk:
                 with self._phase("promote.scatter"):
                     ukeys = torch.from_numpy(ex["key"]).to(dev, non_blocking=True)
                     rec = torch.from_numpy(ex["rec"]).to(dev, non_blocking=True)
@@ -672,7 +684,9 @@ class KeyedSessionOperator:
                                       np.ascontiguousarray(rr[live, 3] & 0xFFFFFFFF),
                                       np.ascontiguousarray(rr[live, 3] >> 32), False)
                     moved = np.setdiff1d(moved, ex["key"][bad])
-            if len(moved):
+            if nd is not None:
+                pass  # the spill set already lost the keys (_promote_dense)
+            elif len(moved):
                 mt = torch.from_numpy(np.ascontiguousarray(moved, dtype=np.int64)).to(dev)
                 self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
                                           mt.data_ptr(), mt.numel(), self._st())
@@ -702,6 +716,64 @@ class KeyedSessionOperator:
             late = h[6] if total else 0
             late += self._overflow_runs(h, wm)
             return h[2], late
+
+    def _promote_dense(self, uk, ukh, wm: int):
+        """The revisit fast path (config 5 with revisits): when every revisited key is cold in the
+        store with at most one session, the store writes one dense row per kept session
+        {key, start, end, acc, cnt | flags << 32, last activity} straight into a reused pinned
+        buffer (SessionStore.extract_dense_into: one parallel scan, no per-key containers); ONE
+        copy takes the rows to HBM and ONE kernel (session_promote_rows) inserts each key's slot
+        and writes its record. The keys leave the device spill set from the device copy of the
+        unique keys (no second upload). Returns None when the store says the fast path does not
+        apply (nothing changed: the caller takes extract_packed)."""
+        n = len(ukh)
+        if n == 0 or not _PROMOTE_DENSE or self.store.shards() != 1:
+            return None
+        if getattr(self, "_pd_host", None) is None or self._pd_host.shape[0] < n:
+            cap = max(1024, 1 << (n - 1).bit_length())
+            self._pd_host = torch.empty((cap, 6), dtype=torch.int64, pin_memory=True)
+            self._pd_dev = torch.empty((cap, 6), dtype=torch.int64, device=self.device)
+            self._pd_slots = torch.empty(cap, dtype=torch.int64, device=self.device)
+        if getattr(self, "_pd_copied", None) is not None:
+            self._pd_copied.synchronize()  # the previous upload has left the pinned rows
+        hrows = self._pd_host
+        nk = self.store.extract_dense_into(ukh, wm, self.gap, hrows.data_ptr(), hrows.shape[0])
+        if nk < 0:
+            self.metrics.promote_fallbacks += 1
+            return None
+        st = self._st()
+        self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
+                                  uk.data_ptr(), uk.numel(), st)
+        if nk == 0:
+            return 0
+        with self._phase("promote.scatter"):
+            self._pd_dev[:nk].copy_(hrows[:nk], non_blocking=True)
+            if getattr(self, "_pd_copied", None) is None:
+                self._pd_copied = torch.cuda.Event()
+            self._pd_copied.record(torch.cuda.current_stream(self.device))
+            self.ctr[3:5].zero_()
+            self.native.gpu_session_promote_rows(self._pd_dev.data_ptr(), nk, self.nsub_log2,
+                                                 self.cap_log2, self.keys_g.data_ptr(),
+                                                 self._pd_slots.data_ptr(), self.sess.data_ptr(),
+                                                 self.slot_due.data_ptr(),
+                                                 self.slot_last.data_ptr(),
+                                                 self.ctr[3:4].data_ptr(),
+                                                 self.ctr[4:5].data_ptr(), st)
+            ins, n_bad = self.ctr[3:5].tolist()
+            self._live_estimate += ins
+        if n_bad:  # sub-table full (rare): those keys' sessions go back to the store
+            bad = (self._pd_slots[:nk] < 0).cpu().numpy()
+            r = hrows[:nk].numpy()[bad]
+            self.store.insert(np.ascontiguousarray(r[:, 0]), np.ascontiguousarray(r[:, 1]),
+                              np.ascontiguousarray(r[:, 2]), np.ascontiguousarray(r[:, 3]),
+                              np.ascontiguousarray(r[:, 4] & 0xFFFFFFFF),
+                              np.ascontiguousarray(r[:, 4] >> 32), False)
+            bk = torch.from_numpy(np.ascontiguousarray(r[:, 0])).to(self.device)
+            self.native.gpu_set_insert(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
+                                       bk.data_ptr(), bk.numel(), st)
+            self.set_used += int(bk.numel())
+        self.metrics.promote_dense += 1
+        return nk
 
     def _overflow_runs(self, h, wm: int) -> int:
         """Keys whose merge produced more than kSess sessions move to the host tier."""
@@ -766,12 +838,13 @@ class KeyedSessionOperator:
         if slots is not None or not self.gpu:
             self._join_spill()
         else:
-            # The previous job's results (its released keys leave the device spill set) are
-            # applied before this eviction adds keys to the set: stream order of erase and add.
+            # Finished jobs' results (their released keys leave the device spill set) are applied
+            # before this eviction adds keys to the set. A job still running cannot release a
+            # key this eviction adds: a released key was in the store when that job expired it,
+            # an evicted key is resident in HBM, and a key only moves from the store back to HBM
+            # through a store call that joins every queued job first (extract for a promote,
+            # process for a host fold) -- whose results the poll below then applies.
             self._poll_spill()
-            if self.store.spill_completed() < self.store.spill_submitted():
-                with self._phase("spill.wait_prev"):
-                    self._join_spill()
         prev = getattr(self, "_spill_copy_done", None)
         if prev is not None:
             # The staging rows and counters are rewritten below: after the previous eviction's
@@ -861,6 +934,8 @@ class KeyedSessionOperator:
         with self._phase("spill.async_launch.copy"):
             hr = CountedHostRows(_Slab(), [rows[j] for j in range(6)], self.ctr[7:8], [self.ctr],
                                  copy_stream=self._spill_stream if _SPILL_SIDE_STREAM else None)
+        self.phase_s["spill.async_launch.take"] += hr.t_take
+        self.phase_s["spill.async_launch.kernel"] += hr.t_launch
         self.metrics.extra["spill_slab_allocs"] = self._spill_allocs
         self._spill_copy_done = hr.done
         st = self._spill_stream if _SPILL_SIDE_STREAM else torch.cuda.current_stream(self.device)

@@ -60,7 +60,52 @@ class PinnedSlabPool:
 
         return sys.getrefcount(self.slabs[i][1]) <= 2
 
+    def reserve_async(self, nbytes: int) -> None:
+        """Allocate a slab of `nbytes` (rounded up) on a background thread, for a later take():
+        a growing caller (the host tier's firing export) asks ahead of need, so the page-locking
+        of a large slab (~25 ms at 512 MB on the box; torch releases the GIL inside it) runs
+        beside the step instead of inside it."""
+        if not self.pin or getattr(self, "_reserving", None) is not None:
+            return
+        size = _next_pow2(max(nbytes, 1 << 16))
+        if any(s[0].numel() >= size for s in self.slabs):
+            return
+        import threading
+
+        box = {}
+
+        def work():
+            try:
+                box["t"] = torch.empty(size, dtype=torch.uint8, pin_memory=True)
+            except BaseException as e:  # surfaced by the next take()
+                box["err"] = e
+
+        th = threading.Thread(target=work, name="mxs-pin-reserve", daemon=True)
+        th.start()
+        self._reserving = (th, box)
+
+    def _land_reserve(self, block: bool) -> None:
+        r = getattr(self, "_reserving", None)
+        if r is None or (not block and r[0].is_alive()):
+            return
+        r[0].join()
+        self._reserving = None
+        if "err" in r[1]:
+            raise r[1]["err"]
+        t = r[1]["t"]
+        if len(self.slabs) >= self.max_slabs:
+            free = [i for i in range(len(self.slabs)) if self._free(i)]
+            if not free:
+                return  # every slab is in use: the reserve is dropped
+            self.slabs.pop(min(free, key=lambda i: self.slabs[i][0].numel()))
+        self.allocs += 1
+        self.slabs.append((t, t.numpy()))
+
     def take(self, nbytes: int) -> tuple[torch.Tensor, np.ndarray]:
+        if getattr(self, "_reserving", None) is not None:
+            # a reserve in flight that this take needs is waited for (not allocated twice)
+            self._land_reserve(block=not any(s[0].numel() >= nbytes and self._free(i)
+                                             for i, s in enumerate(self.slabs)))
         for i in range(len(self.slabs)):
             if self.slabs[i][0].numel() >= nbytes and self._free(i):
                 return self.slabs[i]

@@ -164,7 +164,10 @@ class HostWindowTier:
             # pinned slab is a fresh page-locked allocation (~12 ms at 256 MB on the box).
             bound = bound * 3 // 2
             a8 = (bound * 8 + 255) & ~255
-            t, arr = pool.take(2 * a8 + bound * 4 + 256)
+            need = 2 * a8 + bound * 4 + 256
+            t, arr = pool.take(need)
+            if t.numel() < 2 * need and hasattr(pool, "reserve_async"):
+                pool.reserve_async(2 * need)  # the tier grows: the next slab, off the step
             base = t.data_ptr()
             n = int(self._t.export_rows(int(p0), int(p1), base, base + a8, base + 2 * a8, bound))
             if n > bound:  # export_rows writes nothing past `bound` and returns the total

@@ -246,6 +246,64 @@ def test_store_extract_parallel_chunk_scan():
     assert again["key"].size == 0
 
 
+def _dense_store(m, nk, nchunks, seed):
+    rng = np.random.default_rng(seed)
+    st_ = m.SessionStore(100, 1000, K.AGG_SUM_I64)
+    keys = rng.permutation(nk).astype(np.int64)
+    s = (keys % 4000).astype(np.int64) + 10_000
+    ones = np.ones_like(keys)
+    for c in np.array_split(np.arange(nk), nchunks):
+        st_.insert(keys[c], s[c], s[c] + 100, keys[c] * 3, ones[c], ones[c], True)
+    return st_, rng
+
+
+def test_store_extract_dense_into_equals_extract_packed():
+    """The revisit fast path (SessionStore.extract_dense_into, one parallel block scan writing
+    dense rows into caller memory) hands back exactly extract_packed's sessions: same keys, same
+    slot record 0, same last activity; rows past cleanup at wm are dropped, every wanted key
+    leaves the store, and a second extract finds nothing."""
+    from mxstream.ops.native import load
+
+    m = load()
+    a, rng = _dense_store(m, 300_000, 3, 11)
+    b, _ = _dense_store(m, 300_000, 3, 11)
+    want = rng.choice(300_000, 40_000, replace=False).astype(np.int64)
+    wm = 10_000 + 2000 + 100 + 1000  # keys with start < 12_000 - 1 are past cleanup
+    out = np.zeros((want.size, 6), np.int64)
+    nk = a.extract_dense_into(want, wm, 100, out.ctypes.data, want.size)
+    ex = b.extract_packed(want, wm, 4, 100)
+    assert nk == ex["key"].size > 0
+    order = np.argsort(out[:nk, 0])
+    got = out[:nk][order]
+    rec = ex["rec"].reshape(-1, 4, 4)
+    assert np.array_equal(got[:, 0], ex["key"])
+    assert np.array_equal(got[:, 1:5], rec[:, 0, :])
+    assert np.array_equal(got[:, 5], ex["last"])
+    assert a.num_cold_rows() == b.num_cold_rows() == 300_000 - want.size
+    assert a.extract_dense_into(want, wm, 100, out.ctypes.data, want.size) in (0, -1)
+
+
+def test_store_extract_dense_into_declines_without_change():
+    """-1 and an unchanged store when the fast path does not apply: a key with two cold rows, or
+    hot sessions in the store."""
+    from mxstream.ops.native import load
+
+    m = load()
+    st_, _ = _dense_store(m, 10_000, 2, 3)
+    k = np.array([7], np.int64)
+    st_.insert(k, np.array([50_000], np.int64), np.array([50_100], np.int64), k, np.ones(1, np.int64),
+               np.ones(1, np.int64), True)  # key 7's second cold row
+    out = np.zeros((100, 6), np.int64)
+    want = np.arange(0, 100, dtype=np.int64)
+    rows = st_.num_cold_rows()
+    assert st_.extract_dense_into(want, 0, 100, out.ctypes.data, 100) == -1
+    assert st_.num_cold_rows() == rows
+    hot, _ = _dense_store(m, 10_000, 2, 3)
+    hot.process(np.array([20_000], np.int64), np.array([5], np.int64), np.array([1], np.int64), 0)
+    assert hot.extract_dense_into(want, 0, 100, out.ctypes.data, 100) == -1
+    assert hot.num_cold_rows() == 10_000
+
+
 @pytest.mark.parametrize("shards", [2, 8])
 def test_sharded_store_equals_one_store(shards):
     """Key shards worked by the pool (csrc/session_shards.h) give the single store's results:
@@ -463,8 +521,8 @@ def test_gpu_sessions_spill_set_grows_on_device():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("promote", [True, False])
-def test_gpu_spilled_keys_return_to_hbm(promote):
+@pytest.mark.parametrize("promote,dense", [(True, True), (True, False), (False, False)])
+def test_gpu_spilled_keys_return_to_hbm(promote, dense, monkeypatch):
     # Keys go idle (spilled to host DRAM with fired sessions inside the lateness), then receive
     # records again: with promotion their sessions come back to HBM slots and the records are
     # folded on the GPU; without it the host store folds them. Both equal the CPU store.
@@ -477,12 +535,18 @@ def test_gpu_spilled_keys_return_to_hbm(promote):
                 events.append((k + 300 * (rnd % 2), int(t), int(rng.integers(0, 9))))
     events.sort(key=lambda e: e[1])
     kw = dict(max_load=0.05, idle_spill_ms=3_000, cap_log2=7)
+    import mxstream.runtime.session_operator as so
+
+    monkeypatch.setattr(so, "_PROMOTE_DENSE", dense)
     b, op = engine_with(events, 5_000, 2_000, 30_000, promote=promote, device="cuda", batch=600, **kw)
     a2, _ = engine(events, 5_000, 2_000, 30_000, device="cpu", batch=600)
     assert a2 == b
     assert op.metrics.spilled_keys > 0
     if promote:
         assert op.metrics.promoted_keys > 0 and op.metrics.records_promoted > 0
+        print("promote dense/fallback:", op.metrics.promote_dense, op.metrics.promote_fallbacks)
+        if not dense:
+            assert op.metrics.promote_dense == 0
     else:
         assert op.metrics.records_to_host > 0
 
