@@ -3891,12 +3891,15 @@ __global__ __launch_bounds__(256) void session_promote_kernel(
   }
 }
 
-// Promoted keys from dense host rows (SessionStore.extract_dense_into): one row of 6 int64
-// {key, start, end, acc, cnt | flags << 32, last activity} per key with a single session. The
-// key gets a slot (insert-or-find in its sub-table), the session goes to slot record 0, the other
-// records are zeroed. slots[i] = -1 (counted in n_bad) when the sub-table is full.
+// Promoted keys from host promote rows (SessionStore.extract_rows_into): one row of 8 int64
+// {key, start, end, acc, cnt | flags << 32, last activity, position, sessions of the key} per
+// session, a key's rows adjacent with position 0 first. Phase 0 (position-0 rows, one per key:
+// no two threads insert the same key) finds or inserts the key's slot, writes record 0 and
+// zeroes the records the key does not fill; phase 1 writes the other positions into the slot
+// their position-0 row found. slots[i] = -1 (phase 0: counted in n_bad) when the sub-table is
+// full.
 __global__ __launch_bounds__(256) void session_promote_rows_kernel(
-    const int64_t* __restrict__ rows, int64_t n, int nsub_log2, int cap_log2,
+    const int64_t* __restrict__ rows, int64_t n, int nsub_log2, int cap_log2, int phase,
     uint64_t* __restrict__ keys_g, int64_t* __restrict__ slots, int64_t* __restrict__ sess,
     int64_t* __restrict__ slot_due, int64_t* __restrict__ slot_last,
     uint32_t* __restrict__ inserted, uint32_t* __restrict__ n_bad) {
@@ -3904,26 +3907,34 @@ __global__ __launch_bounds__(256) void session_promote_rows_kernel(
   const uint32_t mask = (1u << cap_log2) - 1;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t* r = rows + i * 6;
-    const uint64_t key = (uint64_t)r[0];
-    const uint64_t sub = sub_table_of(key, nsub_log2);
-    const uint32_t s32 = sess_probe_insert(keys_g + (sub << cap_log2), key, mask, inserted);
-    if (s32 == kNoSlot) {
-      slots[i] = -1;
-      atomicAdd(n_bad, 1u);
-      continue;
+    const int64_t* r = rows + i * 8;
+    const int64_t pos = r[6], nsess = r[7];
+    if ((phase == 0) != (pos == 0)) continue;
+    int64_t s;
+    if (phase == 0) {
+      const uint64_t key = (uint64_t)r[0];
+      const uint64_t sub = sub_table_of(key, nsub_log2);
+      const uint32_t s32 = sess_probe_insert(keys_g + (sub << cap_log2), key, mask, inserted);
+      if (s32 == kNoSlot) {
+        slots[i] = -1;
+        atomicAdd(n_bad, 1u);
+        continue;
+      }
+      s = (int64_t)((sub << cap_log2) | s32);
+      slots[i] = s;
+      for (int j = (int)nsess * 4; j < W; ++j) sess[s * W + j] = 0;
+      slot_due[s * kSlotMeta] = INT64_MIN;  // the next fire sweep recomputes the due time
+      slot_last[s * kSlotMeta] = r[5];
+    } else {
+      s = slots[i - pos];
+      slots[i] = s;
+      if (s < 0) continue;
     }
-    const int64_t s = (int64_t)((sub << cap_log2) | s32);
-    slots[i] = s;
-    int64_t* o = sess + s * W;
+    int64_t* o = sess + s * W + pos * 4;
     o[0] = r[1];
     o[1] = r[2];
     o[2] = r[3];
     o[3] = r[4];
-#pragma unroll
-    for (int j = 4; j < W; ++j) o[j] = 0;
-    slot_due[s * kSlotMeta] = INT64_MIN;  // the next fire sweep recomputes the due time
-    slot_last[s * kSlotMeta] = r[5];
   }
 }
 
@@ -5317,9 +5328,10 @@ void session_promote_rows(const int64_t* rows, int64_t n, int nsub_log2, int cap
                           int64_t* slot_last, uint32_t* inserted, uint32_t* n_bad,
                           intptr_t stream) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(session_promote_rows_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0,
-                     (hipStream_t)stream, rows, n, nsub_log2, cap_log2, keys_g, slots, sess,
-                     slot_due, slot_last, inserted, n_bad);
+  for (int phase = 0; phase < 2; ++phase)
+    hipLaunchKernelGGL(session_promote_rows_kernel, dim3(grid_for(n, 256, 4096)), dim3(256), 0,
+                       (hipStream_t)stream, rows, n, nsub_log2, cap_log2, phase, keys_g, slots,
+                       sess, slot_due, slot_last, inserted, n_bad);
   HIP_CHECK(hipGetLastError());
 }
 

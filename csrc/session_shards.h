@@ -162,12 +162,30 @@ class ShardedCore {
     for (auto& m : mv) moved->insert(moved->end(), m.begin(), m.end());
     return out;
   }
-  // The promote path's dense extract (SessionCore::extract_dense_into); a sharded store
-  // returns -1 (the caller takes the general extract).
-  int64_t extract_dense_into(const int64_t* keys, int64_t n, int64_t wm, int64_t gap,
-                             int64_t* rows, int64_t cap) {
-    if (shards() != 1) return -1;
-    return sh_[0]->extract_dense_into(keys, n, wm, gap, rows, cap);
+  SessionCore::IndexStats index_stats() const {
+    SessionCore::IndexStats t;
+    for (auto& c : sh_) {
+      const auto x = c->index_stats();
+      t.indexed += x.indexed;
+      t.multi += x.multi;
+      t.hot += x.hot;
+      t.scans += x.scans;
+      t.off += x.off;
+      t.span += x.span;
+    }
+    return t;
+  }
+  // The promote path's extract as promote rows (SessionCore::extract_rows_into).
+  std::pair<int64_t, int64_t> extract_rows_into(const int64_t* keys, int64_t n, int64_t wm,
+                                                int64_t max_sess, int64_t gap, int64_t* rows,
+                                                int64_t cap, int64_t* moved_out,
+                                                int64_t moved_cap) {
+    if (shards() == 1)
+      return sh_[0]->extract_rows_into(keys, n, wm, max_sess, gap, rows, cap, moved_out,
+                                       moved_cap);
+    std::vector<int64_t> moved;
+    const Columns c = extract(keys, n, wm, max_sess, &moved);
+    return SessionCore::promote_rows(c, moved, gap, rows, cap, moved_out, moved_cap);
   }
   void fire(int64_t wm, const ExprProg& mp, const ExprProg& fp, SessionCore::FireOut& o,
             bool expire_cold = true) {

@@ -10,6 +10,7 @@
 #include <cstring>
 #include <deque>
 #include <queue>
+#include <sys/mman.h>
 #include <stdexcept>
 #include <thread>
 #include <unordered_map>
@@ -93,6 +94,7 @@ struct ColdChunk {
   PodVec<uint32_t> cnt;  // 0 = row gone (promoted or discarded)
   int64_t max_due = INT64_MIN;
   size_t live = 0;
+  uint32_t seq = 0;  // identity in the dense cold-row index (SessionCore::loc_), 0 = none
   // Rows by key: promote() looks keys up by binary search or a merge join instead of probing a
   // hash set with every cold row of the store.
   std::vector<uint32_t> by_key;
@@ -223,6 +225,7 @@ class SessionCore {
     ColdChunk ch;
     std::vector<uint8_t> isc;  // per row: 1 = goes to the cold chunk
     int64_t nc = 0, emax = INT64_MIN;
+    bool indexed = false;  // index_cold() ran (the spill worker runs it outside the lock)
   };
   void insert(const int64_t* K, const int64_t* S, const int64_t* E, const int64_t* A,
               const int64_t* C, const int64_t* F, int64_t n, bool cold) {
@@ -230,6 +233,7 @@ class SessionCore {
     insert_hot(K, S, E, A, C, F, n, cold, p);
     if (cold) {
       build_cold(K, S, E, A, C, n, p);
+      index_cold(p);
       publish_cold(p);
     }
   }
@@ -338,11 +342,87 @@ class SessionCore {
       if (ch.key.capacity() && spare_.size() < 4) spare_.push_back(std::move(ch));
       return;
     }
+    if (!p.indexed) index_cold(p);
     ch.max_due = std::max(ch.max_due, cleanup_time(p.emax - 1));
     ch.live = ch.key.size();
     cold_rows_ += ch.live;
+    if (ch.seq) set_seq_pos(ch.seq, (int32_t)cold_.size());
     cold_.push_back(std::move(ch));
   }
+
+  // Dense cold-row index: loc_[key - loc_base_] = (chunk seq << 32 | row) of the first cold
+  // row of the key's run in its chunk (an evicted slot's sessions are adjacent rows), so an
+  // extract finds the rows of its wanted keys with one lookup per key instead of a scan of
+  // every cold row of the store (config 5 with revisits: ~10^5 wanted keys against ~10^7 cold
+  // rows per step). An entry is trusted only after checking that its chunk is still in the
+  // store and that its row still holds the key with cnt > 0 (taken rows, expired chunks and
+  // reused chunk memory leave stale entries behind). A key with live rows in two chunks (or two
+  // runs of one chunk) is marked kMultiLoc and sends the extract that wants it to the scan.
+  // The index is one reserved virtual range of kMaxLocSpan entries (no copies as it grows:
+  // untouched pages cost nothing); keys outside it (hashed keys) switch it off for good.
+  // Runs outside the store lock in the spill worker (every other index user joins the worker
+  // first): the chunk is not published yet, so its own rows are checked against `p.ch`.
+  void index_cold(ColdPlan& p) {
+    p.indexed = true;
+    ColdChunk& ch = p.ch;
+    ch.seq = 0;
+    if (ch.key.empty() || loc_off_) return;
+    if (!loc_) {
+      void* m = ::mmap(nullptr, kMaxLocSpan * sizeof(uint64_t), PROT_READ | PROT_WRITE,
+                       MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+      if (m == MAP_FAILED) {
+        loc_off_ = true;
+        return;
+      }
+      (void)::madvise(m, kMaxLocSpan * sizeof(uint64_t), MADV_HUGEPAGE);
+      loc_ = static_cast<uint64_t*>(m);
+      // room below the first keys for ids a little older than them
+      loc_base_ = ch.kmin > kMaxLocSpan / 8 ? ch.kmin - kMaxLocSpan / 8 : 0;
+    }
+    if (ch.kmin < loc_base_ || ch.kmax - loc_base_ >= kMaxLocSpan) {
+      drop_index();
+      return;
+    }
+    ch.seq = next_seq_++;
+    // Row blocks on the pool; an entry changes by compare-and-swap, so two runs of one key (in
+    // this chunk or an older one) always end as kMultiLoc whatever the interleaving.
+    const uint32_t cur = ch.seq;
+    const size_t n = ch.key.size();
+    auto block = [&](size_t lo, size_t hi) {
+      for (size_t r = lo; r < hi; ++r) {
+        const uint64_t k = ch.key[r];
+        if (r && ch.key[r - 1] == k) continue;  // a run's later rows: reached from its first
+        uint64_t* e = loc_ + (k - loc_base_);
+        const uint64_t mine = ((uint64_t)cur << 32) | (uint64_t)r;
+        uint64_t old = __atomic_load_n(e, __ATOMIC_RELAXED);
+        for (;;) {
+          if (old == kMultiLoc) break;
+          uint64_t want = mine;
+          if (old != kNoLoc) {
+            const uint32_t es = (uint32_t)(old >> 32), er = (uint32_t)old;
+            const bool live = es == cur ? (er < n && ch.key[er] == k && ch.cnt[er])
+                                        : live_loc(old, k);
+            if (live) want = kMultiLoc;
+          }
+          if (__atomic_compare_exchange_n(e, &old, want, false, __ATOMIC_RELAXED,
+                                          __ATOMIC_RELAXED))
+            break;
+        }
+      }
+    };
+    constexpr size_t kBlk = 65536;
+    const size_t nb = (n + kBlk - 1) / kBlk;
+    if (nb > 1) {
+      if (!pool_) {
+        unsigned hw = std::thread::hardware_concurrency();
+        pool_.reset(new WorkerPool(std::max(0, std::min<int>(hw ? (int)hw : 1, max_threads_) - 1)));
+      }
+      pool_->run((int)nb, [&](int b) { block((size_t)b * kBlk, std::min(n, (size_t)(b + 1) * kBlk)); });
+    } else {
+      block(0, n);
+    }
+  }
+  ~SessionCore() { drop_index(); }
 
   // Hand keys back to the HBM tier: every listed key with at most `max_sess` live sessions
   // leaves the store (hot sessions and cold rows; rows past cleanup at `wm` are dropped).
@@ -384,27 +464,14 @@ class SessionCore {
       const uint64_t o = k - wmin;
       return k >= wmin && o < wspan && ((wbits[o >> 6] >> (o & 63)) & 1ull);
     };
-    if (dense && m_.empty() && cold_rows_ && max_sess >= 1) {
-      std::vector<int64_t> rows(want.size() * kDenseRow);
-      const int64_t nk = dense_cold_take(want, wmin, wspan, wbits, wm, gap_, rows.data(),
-                                         (int64_t)want.size());
-      if (nk >= 0) {
-        Columns out;
-        for (int64_t i = 0; i < nk; ++i) {
-          const int64_t* r = rows.data() + i * kDenseRow;
-          out.add((uint64_t)r[0], r[1], r[2], (uint64_t)r[3], (uint32_t)(r[4] & 0xFFFFFFFF),
-                  (uint32_t)((uint64_t)r[4] >> 32));
-        }
-        moved->insert(moved->end(), want.begin(), want.end());
-        return out;
-      }
-    }
     // Cold rows of the wanted keys come straight out of their chunks (no detour through the hot
     // map); rows already past cleanup at `wm` are dropped, as a promote would.
     std::vector<std::pair<uint64_t, Session>> cold;
     std::vector<uint64_t> wset;  // hash set of `want`, built on first use
     size_t wmask = 0;
-    if (cold_rows_ && !want.empty()) {
+    const bool indexed = cold_rows_ && !want.empty() && take_indexed(want, wm, cold);
+    if (cold_rows_ && !want.empty() && !indexed) ++ixs_.scans;
+    if (cold_rows_ && !want.empty() && !indexed) {
       // Dense keys: the chunks that need a full scan (no row index, or many wanted keys --
       // every chunk of scattered evictions spans the whole id range) are scanned in parallel,
       // one chunk per task; their rows lead `cold` (a key's rows keep their order: they sit in
@@ -562,6 +629,7 @@ class SessionCore {
         std::stable_sort(cold.begin(), cold.end(),
                          [](const auto& a, const auto& b) { return a.first < b.first; });
       }
+      forget_keys(want);  // every cold row of the wanted keys is gone (moved or turned hot)
     }
     const bool no_hot = m_.empty();
     Columns out;
@@ -597,165 +665,96 @@ class SessionCore {
     return out;
   }
 
-  // extract() fast path for the common revisit shape (config 5 with revisits): dense wanted
-  // keys (a bitmap over [wmin, wmin + wspan)), no hot sessions, at most one cold row per key.
-  // The overlapping chunks are scanned in row blocks on the persistent pool (a single large
-  // chunk no longer means one thread) in two passes: count the matches per key rank (the key's
-  // position in `want`, from per-word popcount prefixes of the bitmap), then -- when no key has
-  // two rows -- write each kept row straight to its rank and clear it in its chunk. The kept
-  // rows come out in ascending key order without a sort, as AoS rows of kDenseRow int64 words
-  // {key, start, end, acc, cnt | flags << 32, last activity (end - gap)} at `rows` (capacity
-  // `cap` rows). Every wanted key leaves the store (moved). Scratch buffers persist between
-  // calls (fresh pages cost more than the scan: ~1 GB/s first touch in a VM).
-  // Returns the number of kept rows, or -1 (nothing changed) when the fast path does not apply.
-  static constexpr int kDenseRow = 6;
-  int64_t dense_cold_take(const std::vector<uint64_t>& want, uint64_t wmin, uint64_t wspan,
-                          const std::vector<uint64_t>& wbits, int64_t wm, int64_t gap,
-                          int64_t* rows, int64_t cap, bool ascending = true) {
-    if (!m_.empty() || !cold_rows_ || want.empty()) return -1;
-    const size_t nw = want.size();
-    dx_prefix_.resize(wbits.size() + 1);
-    dx_prefix_[0] = 0;
-    for (size_t w = 0; w < wbits.size(); ++w)
-      dx_prefix_[w + 1] = dx_prefix_[w] + (uint32_t)__builtin_popcountll(wbits[w]);
-    const uint32_t* prefix = dx_prefix_.data();
-    auto rank_of = [&](uint64_t k, uint32_t* rk) -> bool {
-      const uint64_t o = k - wmin;
-      if (k < wmin || o >= wspan) return false;
-      const uint64_t w = wbits[o >> 6], bit = 1ull << (o & 63);
-      if (!(w & bit)) return false;
-      *rk = prefix[o >> 6] + (uint32_t)__builtin_popcountll(w & (bit - 1));
-      return true;
-    };
-    struct Task {
-      size_t ci, lo, hi;
-    };
-    std::vector<Task> tasks;
-    const size_t kBlock = 65536;
-    for (size_t ci = 0; ci < cold_.size(); ++ci) {
-      const ColdChunk& ch = cold_[ci];
-      if (!ch.live || want.back() < ch.kmin || want.front() > ch.kmax) continue;
-      for (size_t lo = 0; lo < ch.key.size(); lo += kBlock)
-        tasks.push_back({ci, lo, std::min(ch.key.size(), lo + kBlock)});
-    }
-    if (!pool_) {
-      unsigned hw = std::thread::hardware_concurrency();
-      const int w = std::max(0, std::min<int>(hw ? (int)hw : 1, max_threads_) - 1);
-      pool_.reset(new WorkerPool(w));
-    }
-    // One scan (no store change): every matching row is counted at its key rank and staged
-    // there (the cleanup test decides "kept"); the task keeps the row ids it matched. A second
-    // match of a rank means a key with several cold rows: nothing has changed yet, so the
-    // general path takes over.
-    dx_hits_.assign(nw, 0);
-    dx_kept_.assign(nw, 0);
-    uint8_t* hits = dx_hits_.data();
-    uint8_t* kept = dx_kept_.data();
-    if (ascending) dx_rows_.resize(nw * kDenseRow);
-    int64_t* staged = dx_rows_.data();
-    if (dx_match_.size() < tasks.size()) dx_match_.resize(tasks.size());
-    if (dx_local_.size() < tasks.size()) dx_local_.resize(tasks.size());
-    std::atomic<bool> multi{false};
-    pool_->run((int)tasks.size(), [&](int t) {
-      const Task& tk = tasks[(size_t)t];
-      const ColdChunk& ch = cold_[tk.ci];
-      std::vector<uint32_t>& match = dx_match_[(size_t)t];
-      std::vector<int64_t>& local = dx_local_[(size_t)t];
-      match.clear();
-      local.clear();
-      uint32_t rk;
-      for (size_t r = tk.lo; r < tk.hi; ++r) {
-        if (!ch.cnt[r] || !rank_of(ch.key[r], &rk)) continue;
-        if (__atomic_fetch_add(&hits[rk], (uint8_t)1, __ATOMIC_RELAXED) != 0) {
-          multi.store(true, std::memory_order_relaxed);
-          return;
-        }
-        match.push_back((uint32_t)r);
-        if (cleanup_time(ch.end[r] - 1) > wm) {
-          // ascending: staged at the key's rank (scattered); else appended in scan order
-          int64_t* o;
-          if (ascending) {
-            o = staged + (size_t)rk * kDenseRow;
-          } else {
-            local.resize(local.size() + kDenseRow);
-            o = local.data() + local.size() - kDenseRow;
-          }
-          o[0] = (int64_t)ch.key[r];
-          o[1] = ch.start[r];
-          o[2] = ch.end[r];
-          o[3] = (int64_t)ch.acc[r];
-          o[4] = (int64_t)(((uint64_t)ch.cnt[r] & 0xFFFFFFFFull) | (1ull << 32));  // fired, cold
-          o[5] = ch.end[r] - gap;
-          kept[rk] = 1;
-        }
-      }
-    });
-    if (multi.load()) return -1;
-    // the matched rows leave their chunks
-    std::vector<size_t> gone(tasks.size(), 0);
-    for (size_t t = 0; t < tasks.size(); ++t) {
-      ColdChunk& ch = cold_[tasks[t].ci];
-      for (uint32_t r : dx_match_[t]) ch.cnt[r] = 0;
-      gone[t] = dx_match_[t].size();
-    }
-    for (size_t t = 0; t < tasks.size(); ++t) {
-      cold_[tasks[t].ci].live -= gone[t];
-      cold_rows_ -= gone[t];
-    }
-    int64_t nk = 0;
-    if (!ascending) {
-      for (size_t t = 0; t < tasks.size(); ++t) {
-        const std::vector<int64_t>& local = dx_local_[t];
-        const int64_t m = (int64_t)local.size() / kDenseRow;
-        if (nk + m > cap) throw std::length_error("dense_cold_take: output capacity");
-        if (m) std::memcpy(rows + nk * kDenseRow, local.data(), sizeof(int64_t) * local.size());
-        nk += m;
-      }
-      return nk;
-    }
-    for (size_t i = 0; i < nw; ++i) {
-      if (!kept[i]) continue;
-      if (nk >= cap) throw std::length_error("dense_cold_take: output capacity");
-      std::memcpy(rows + nk * kDenseRow, staged + i * kDenseRow, sizeof(int64_t) * kDenseRow);
-      ++nk;
-    }
-    return nk;
+  // Counters of the dense cold-row index: extracts served by it, sent to the scan by a
+  // multi-row key, declined by hot keys (direct promote rows), full scans, index switched off.
+  struct IndexStats {
+    int64_t indexed = 0, multi = 0, hot = 0, scans = 0, off = 0, span = 0;
+  };
+  IndexStats index_stats() const {
+    IndexStats t = ixs_;
+    t.off = loc_off_ ? 1 : 0;
+    t.span = loc_ ? (int64_t)kMaxLocSpan : 0;
+    return t;
   }
-  // The wanted-key bitmap of extract(): {want (ascending, unique), wmin, wspan, bits}; false when
-  // the span is too wide for a bitmap.
-  static bool want_bitmap(const int64_t* keys, int64_t n, std::vector<uint64_t>* want,
-                          uint64_t* wmin_out, uint64_t* wspan_out, std::vector<uint64_t>* wbits) {
-    uint64_t wmin = ~0ull, wmax = 0;
-    for (int64_t i = 0; i < n; ++i) {
-      const uint64_t k = (uint64_t)keys[i];
-      wmin = k < wmin ? k : wmin;
-      wmax = k > wmax ? k : wmax;
+
+  // The promote path's extract laid out for the HBM slot records in caller memory (pinned,
+  // reused): one row of kPromoteRow int64 per returned session {key, start, end, acc,
+  // cnt | flags << 32, last activity of the key (max end - gap), position of the session in its
+  // key, sessions of the key}; rows of a key are adjacent, position 0 first. `moved` receives
+  // the keys that left the store. Returns {rows, moved}.
+  static constexpr int kPromoteRow = 8;
+  std::pair<int64_t, int64_t> extract_rows_into(const int64_t* keys, int64_t n, int64_t wm,
+                                                int64_t max_sess, int64_t gap, int64_t* rows,
+                                                int64_t cap, int64_t* moved_out,
+                                                int64_t moved_cap) {
+    // No hot sessions among the wanted keys and one cold row per key (the revisit shape): the
+    // rows go from the chunks straight into `rows`, no intermediate columns.
+    if (max_sess >= 1 && index_usable() && n > 0) {
+      std::vector<uint64_t>& want = ix_want_;
+      want.assign((const uint64_t*)keys, (const uint64_t*)keys + n);
+      bool sorted = true;
+      for (int64_t i = 1; i < n && sorted; ++i) sorted = want[i - 1] < want[i];
+      if (!sorted) {
+        std::sort(want.begin(), want.end());
+        want.erase(std::unique(want.begin(), want.end()), want.end());
+      }
+      if ((int64_t)want.size() > moved_cap)
+        throw std::length_error("extract_rows_into: moved capacity");
+      int64_t nk = 0;
+      const bool ok = take_indexed_with(
+          want, wm, true, (size_t)max_sess,
+          [&](size_t total) {
+            if ((int64_t)total > cap) throw std::length_error("extract_rows_into: row capacity");
+            nk = (int64_t)total;
+          },
+          [&](size_t o, const ColdChunk& ch, uint32_t r, uint32_t j, uint32_t nkey,
+              int64_t last_end) {
+            int64_t* w = rows + o * kPromoteRow;
+            w[0] = (int64_t)ch.key[r];
+            w[1] = ch.start[r];
+            w[2] = ch.end[r];
+            w[3] = (int64_t)ch.acc[r];
+            w[4] = (int64_t)(((uint64_t)ch.cnt[r] & 0xFFFFFFFFull) | (1ull << 32));  // fired
+            w[5] = last_end - gap;
+            w[6] = j;
+            w[7] = nkey;
+          });
+      if (ok) {
+        std::memcpy(moved_out, want.data(), want.size() * sizeof(int64_t));
+        return {nk, (int64_t)want.size()};
+      }
     }
-    const uint64_t wspan = n ? wmax - wmin + 1 : 0;
-    if (!n || wspan > ((uint64_t)1 << 27)) return false;
-    wbits->assign((wspan + 63) / 64, 0);
-    for (int64_t i = 0; i < n; ++i) {
-      const uint64_t o = (uint64_t)keys[i] - wmin;
-      (*wbits)[o >> 6] |= 1ull << (o & 63);
-    }
-    want->clear();
-    for (size_t w = 0; w < wbits->size(); ++w)
-      for (uint64_t b = (*wbits)[w]; b; b &= b - 1)
-        want->push_back(wmin + (w << 6) + (uint64_t)__builtin_ctzll(b));
-    *wmin_out = wmin;
-    *wspan_out = wspan;
-    return true;
+    std::vector<int64_t> moved;
+    const Columns c = extract(keys, n, wm, max_sess, &moved);
+    return promote_rows(c, moved, gap, rows, cap, moved_out, moved_cap);
   }
-  // Fast revisit extract into caller memory (pinned, reused): kept sessions as dense rows in
-  // scan order (no key order: the promote path inserts slots per row), every wanted key leaves
-  // the store. -1: not applicable (use extract).
-  int64_t extract_dense_into(const int64_t* keys, int64_t n, int64_t wm, int64_t gap,
-                             int64_t* rows, int64_t cap) {
-    std::vector<uint64_t> want, wbits;
-    uint64_t wmin = 0, wspan = 0;
-    if (!m_.empty() || !cold_rows_ || !want_bitmap(keys, n, &want, &wmin, &wspan, &wbits))
-      return -1;
-    return dense_cold_take(want, wmin, wspan, wbits, wm, gap, rows, cap, false);
+  // extract()'s output (keys grouped, ascending) as promote rows + the moved keys.
+  static std::pair<int64_t, int64_t> promote_rows(const Columns& c,
+                                                  const std::vector<int64_t>& moved, int64_t gap,
+                                                  int64_t* rows, int64_t cap, int64_t* moved_out,
+                                                  int64_t moved_cap) {
+    const size_t m = c.key.size();
+    if ((int64_t)m > cap) throw std::length_error("extract_rows_into: row capacity");
+    if ((int64_t)moved.size() > moved_cap) throw std::length_error("extract_rows_into: moved capacity");
+    for (size_t i = 0; i < m;) {
+      size_t j = i;
+      int64_t last = INT64_MIN;
+      while (j < m && c.key[j] == c.key[i]) last = std::max(last, c.end[j++] - gap);
+      for (size_t q = i; q < j; ++q) {
+        int64_t* r = rows + q * kPromoteRow;
+        r[0] = c.key[q];
+        r[1] = c.start[q];
+        r[2] = c.end[q];
+        r[3] = c.acc[q];
+        r[4] = (int64_t)(((uint64_t)c.cnt[q] & 0xFFFFFFFFull) | ((uint64_t)c.flags[q] << 32));
+        r[5] = last;
+        r[6] = (int64_t)(q - i);
+        r[7] = (int64_t)(j - i);
+      }
+      i = j;
+    }
+    if (!moved.empty()) std::memcpy(moved_out, moved.data(), moved.size() * sizeof(int64_t));
+    return {(int64_t)m, (int64_t)moved.size()};
   }
 
   // Fire / clean up everything the watermark allows. Returns columns of emitted rows plus the
@@ -826,6 +825,7 @@ class SessionCore {
   // hot sessions leave the store (appended to `released`). Emits no rows, so the GPU operator
   // runs it on its spill worker, off the step's critical path.
   void expire_cold(int64_t wm, std::vector<int64_t>& released) {
+    bool erased = false;
     for (auto it = cold_.begin(); it != cold_.end();) {
       if (it->max_due <= wm) {
         // (a key whose cold row expires leaves unless it also has hot sessions; with no hot keys
@@ -848,13 +848,16 @@ class SessionCore {
           sp.live = 0;
           sp.kmin = ~0ull;
           sp.kmax = 0;
+          sp.seq = 0;
           spare_.push_back(std::move(sp));
         }
         it = cold_.erase(it);
+        erased = true;
       } else {
         ++it;
       }
     }
+    if (erased) reindex_chunks();
   }
 
   // Device spill set (open addressing on mix64(key) >> 32, linear probing, empty = ~0) holding
@@ -948,12 +951,185 @@ class SessionCore {
     return c < maxts ? INT64_MAX : c;  // overflow: never cleaned before end of input
   }
 
+  // ---- dense cold-row index (index_cold) ----------------------------------------------------
+  // (seq >= 1: a real entry is never 0, so fresh zero pages read as kNoLoc)
+  static constexpr uint64_t kNoLoc = 0, kMultiLoc = ~0ull;
+  static constexpr uint64_t kNoHit = ~0ull;  // take_indexed: (chunk position << 32 | row) or this
+  static constexpr uint64_t kMaxLocSpan = (uint64_t)1 << 28;  // 2 GB of virtual index
+  int32_t seq_pos(uint32_t seq) const {
+    const uint64_t i = (uint64_t)seq - seq_lo_;
+    return seq >= seq_lo_ && i < seq_pos_.size() ? seq_pos_[(size_t)i] : -1;
+  }
+  void set_seq_pos(uint32_t seq, int32_t pos) {
+    if (seq_pos_.empty()) seq_lo_ = seq;
+    const size_t i = (size_t)(seq - seq_lo_);
+    if (i >= seq_pos_.size()) seq_pos_.resize(i + 1, -1);
+    seq_pos_[i] = pos;
+  }
+  // Chunk positions after an erase from cold_ (tens of chunks).
+  void reindex_chunks() {
+    uint32_t lo = next_seq_;
+    for (auto& ch : cold_)
+      if (ch.seq) lo = std::min(lo, ch.seq);
+    seq_pos_.assign(next_seq_ > lo ? (size_t)(next_seq_ - lo) : 0, -1);
+    seq_lo_ = lo;
+    for (size_t i = 0; i < cold_.size(); ++i)
+      if (cold_[i].seq) seq_pos_[(size_t)(cold_[i].seq - lo)] = (int32_t)i;
+  }
+  // The entry still names a live cold row of `key`.
+  bool live_loc(uint64_t e, uint64_t key) const {
+    const int32_t pos = seq_pos((uint32_t)(e >> 32));
+    if (pos < 0) return false;
+    const ColdChunk& ch = cold_[(size_t)pos];
+    const uint32_t r = (uint32_t)e;
+    return r < ch.key.size() && ch.key[r] == key && ch.cnt[r];
+  }
+  bool index_usable() const { return !loc_off_ && loc_ != nullptr; }
+  void drop_index() {
+    if (loc_) ::munmap(loc_, kMaxLocSpan * sizeof(uint64_t));
+    loc_ = nullptr;
+    loc_off_ = true;
+  }
+  // The wanted keys (ascending, unique) lost every cold row: their entries are cleared (a
+  // multi-row key goes back to the indexed path).
+  void forget_keys(const std::vector<uint64_t>& want) {
+    if (!index_usable()) return;
+    for (uint64_t k : want) {
+      const uint64_t o = k - loc_base_;
+      if (k >= loc_base_ && o < kMaxLocSpan) loc_[o] = kNoLoc;
+    }
+  }
+  // Cold rows of the wanted keys (ascending, unique) through the index, in key order: `cold`
+  // gets the kept ones (rows past cleanup at wm are dropped), every found row leaves its chunk.
+  // False (nothing changed) when the index is off or a wanted key has rows in two places (the
+  // scan path takes over).
+  bool take_indexed(const std::vector<uint64_t>& want, int64_t wm,
+                    std::vector<std::pair<uint64_t, Session>>& cold) {
+    return take_indexed_with(
+        want, wm, false, SIZE_MAX, [&](size_t total) { cold.resize(total); },
+        [&](size_t o, const ColdChunk& ch, uint32_t r, uint32_t, uint32_t, int64_t) {
+          cold[o] = {ch.key[r], Session{ch.start[r], ch.end[r], ch.acc[r], ch.cnt[r], 1u}};
+        });
+  }
+  // Two passes over blocks of wanted keys on the pool: resolve every key to its live run of
+  // cold rows and count the kept rows (nothing changes; a multi-place key, a key with more
+  // than max_kept kept rows, or -- with no_hot -- a key with hot sessions aborts), then
+  // size(total kept) and emit(offset, chunk, row, position in the key, kept rows of the key,
+  // max end of the key's kept rows) each kept row in key order while the found rows leave their
+  // chunks.
+  template <class Size, class Emit>
+  bool take_indexed_with(const std::vector<uint64_t>& want, int64_t wm, bool no_hot,
+                         size_t max_kept, Size&& size, Emit&& emit) {
+    if (!index_usable()) return false;
+    const size_t nw = want.size();
+    constexpr size_t kBlk = 8192;
+    const size_t nb = (nw + kBlk - 1) / kBlk;
+    ix_hit_.resize(nw);
+    ix_run_.resize(nw);
+    ix_kept_.assign(nb + 1, 0);
+    std::atomic<int> abort{0};  // 1 multi, 2 hot, 3 too many sessions
+    if (!pool_) {
+      unsigned hw = std::thread::hardware_concurrency();
+      pool_.reset(new WorkerPool(std::max(0, std::min<int>(hw ? (int)hw : 1, max_threads_) - 1)));
+    }
+    const uint64_t base = loc_base_;
+    const bool check_hot = no_hot && !m_.empty();
+    auto blocks = [&](auto&& body) {
+      if (nb <= 1) {
+        for (size_t b = 0; b < nb; ++b) body(b);
+      } else {
+        pool_->run((int)nb, [&](int b) { body((size_t)b); });
+      }
+    };
+    blocks([&](size_t b) {
+      size_t kept = 0;
+      for (size_t i = b * kBlk, e = std::min(nw, i + kBlk); i < e; ++i) {
+        const uint64_t k = want[i];
+        uint64_t hit = kNoHit;
+        uint32_t run = 0;
+        const uint64_t o = k - base;
+        if (check_hot && is_hot(k)) {
+          abort.store(2, std::memory_order_relaxed);
+          return;
+        }
+        if (k >= base && o < kMaxLocSpan) {
+          const uint64_t en = loc_[o];
+          if (en == kMultiLoc) {
+            abort.store(1, std::memory_order_relaxed);
+            return;
+          }
+          if (en != kNoLoc) {
+            const int32_t pos = seq_pos((uint32_t)(en >> 32));
+            const uint32_t r = (uint32_t)en;
+            if (pos >= 0) {
+              const ColdChunk& ch = cold_[(size_t)pos];
+              if (r < ch.key.size() && ch.key[r] == k && ch.cnt[r]) {
+                hit = ((uint64_t)(uint32_t)pos << 32) | r;
+                size_t kk = 0;
+                for (uint32_t q = r; q < ch.key.size() && ch.key[q] == k; ++q, ++run)
+                  kk += ch.cnt[q] && cleanup_time(ch.end[q] - 1) > wm;
+                if (kk > max_kept) {
+                  abort.store(3, std::memory_order_relaxed);
+                  return;
+                }
+                kept += kk;
+              }
+            }
+          }
+        }
+        ix_hit_[i] = hit;
+        ix_run_[i] = run;
+      }
+      ix_kept_[b + 1] = kept;
+    });
+    if (const int a = abort.load()) {
+      ++(a == 2 ? ixs_.hot : ixs_.multi);
+      return false;
+    }
+    ++ixs_.indexed;
+    for (size_t b = 0; b < nb; ++b) ix_kept_[b + 1] += ix_kept_[b];
+    size(ix_kept_[nb]);
+    std::atomic<size_t> gone{0};
+    // (a chunk's live count is shared between blocks: atomic)
+    blocks([&](size_t b) {
+      size_t o = ix_kept_[b], g = 0;
+      for (size_t i = b * kBlk, e = std::min(nw, i + kBlk); i < e; ++i) {
+        const uint64_t h = ix_hit_[i];
+        if (h == kNoHit) continue;
+        ColdChunk& ch = cold_[(size_t)(h >> 32)];
+        const uint32_t r0 = (uint32_t)h, r1 = r0 + ix_run_[i];
+        uint32_t nk = 0;
+        int64_t last = INT64_MIN;
+        for (uint32_t r = r0; r < r1; ++r)
+          if (ch.cnt[r] && cleanup_time(ch.end[r] - 1) > wm) {
+            ++nk;
+            last = std::max(last, ch.end[r]);
+          }
+        uint32_t j = 0;
+        size_t taken = 0;
+        for (uint32_t r = r0; r < r1; ++r) {
+          if (!ch.cnt[r]) continue;
+          if (cleanup_time(ch.end[r] - 1) > wm) emit(o++, ch, r, j++, nk, last);
+          ch.cnt[r] = 0;
+          ++taken;
+        }
+        __atomic_fetch_sub(&ch.live, taken, __ATOMIC_RELAXED);
+        loc_[want[i] - base] = kNoLoc;
+        g += taken;
+      }
+      gone.fetch_add(g, std::memory_order_relaxed);
+    });
+    cold_rows_ -= gone.load();
+    return true;
+  }
+
   // Move cold rows of `keys` into the hot map (rows past cleanup at `wm` are discarded).
   void promote(const int64_t* keys, int64_t n, int64_t wm) {
     if (cold_rows_ == 0 || n == 0) return;
     std::vector<uint64_t> want((const uint64_t*)keys, (const uint64_t*)keys + n);
     std::sort(want.begin(), want.end());
     want.erase(std::unique(want.begin(), want.end()), want.end());
+    forget_keys(want);  // every cold row of these keys leaves below
     auto take = [&](ColdChunk& ch, uint32_t r) {
       if (!ch.cnt[r]) return;
       if (cleanup_time(ch.end[r] - 1) > wm) {
@@ -1048,13 +1224,7 @@ class SessionCore {
   int64_t gap_, late_;
  public:
   int max_threads_ = 16;  // extract's chunk-scan threads (1 inside a sharded store)
-  std::unique_ptr<WorkerPool> pool_;  // extract's row-block scans (created on first use)
-  // dense_cold_take scratch, kept between calls
-  std::vector<uint32_t> dx_prefix_;
-  std::vector<uint8_t> dx_hits_, dx_kept_;
-  std::vector<int64_t> dx_rows_;
-  std::vector<std::vector<uint32_t>> dx_match_;
-  std::vector<std::vector<int64_t>> dx_local_;
+  std::unique_ptr<WorkerPool> pool_;  // indexed extract's key blocks (created on first use)
  private:
   int agg_;
   // A key's live sessions plus the due time of its one valid heap entry (schedule() pushes only
@@ -1138,6 +1308,15 @@ class SessionCore {
   std::deque<ColdChunk> cold_;
   std::vector<ColdChunk> spare_;  // emptied chunks whose column capacity is reused
   size_t cold_rows_ = 0;
+  uint64_t* loc_ = nullptr;  // dense cold-row index (index_cold): kMaxLocSpan reserved entries
+  uint64_t loc_base_ = 0;
+  bool loc_off_ = false;
+  uint32_t next_seq_ = 1, seq_lo_ = 1;
+  std::vector<int32_t> seq_pos_;  // chunk seq - seq_lo_ -> position in cold_ (-1: gone)
+  std::vector<uint64_t> ix_hit_, ix_want_;  // take_indexed scratch (kept between calls)
+  std::vector<uint32_t> ix_run_;
+  IndexStats ixs_;
+  std::vector<size_t> ix_kept_;
   std::vector<uint64_t> pending_released_;
 };
 

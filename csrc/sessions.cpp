@@ -91,7 +91,7 @@ struct SpillDone {
   uint64_t id = 0;
   int64_t nr = 0, ne = 0, nk = 0;
   std::vector<int64_t> released;
-  double t_wait = 0, t_hot = 0, t_build = 0, t_publish = 0;  // seconds per phase
+  double t_wait = 0, t_hot = 0, t_build = 0, t_index = 0, t_publish = 0;  // seconds per phase
   std::exception_ptr err;
 };
 
@@ -181,18 +181,41 @@ class SessionStore {
     d["moved"] = to_np(moved);
     return d;
   }
-  // The promote path's fast extract (sessions of the wanted keys leave the store): when every
-  // wanted key is cold with at most one live session, writes one row of 6 int64 {key, start,
-  // end, acc, cnt | flags << 32, end - gap} per kept key into `out` (caller memory, cap rows, in
-  // no particular order) and returns the row count; -1 (nothing changed) when not applicable --
-  // the caller falls back to extract_packed. `keys` must be distinct.
-  int64_t extract_dense_into_np(const I64Array& keys, int64_t wm, int64_t gap, intptr_t out,
-                                int64_t cap) {
+  // The promote path's extract straight into caller memory (pinned, reused): promote rows of
+  // 8 int64 (csrc/session_store.h extract_rows_into) at `rows` (cap rows) and the keys that left
+  // the store at `moved` (moved_cap). Returns (rows, moved).
+  std::pair<int64_t, int64_t> extract_rows_into_np(const I64Array& keys, int64_t wm,
+                                                   int64_t max_sess, int64_t gap, intptr_t rows,
+                                                   int64_t cap, intptr_t moved,
+                                                   int64_t moved_cap) {
     py::gil_scoped_release nogil;
     join_all();
     std::lock_guard<std::mutex> g(mu_);
-    return c_.extract_dense_into(keys.data(), keys.size(), wm, gap,
-                                 reinterpret_cast<int64_t*>(out), cap);
+    const auto r = c_.extract_rows_into(keys.data(), keys.size(), wm, max_sess, gap,
+                                        reinterpret_cast<int64_t*>(rows), cap,
+                                        reinterpret_cast<int64_t*>(moved), moved_cap);
+    // the promote kernel writes record `position` of a slot: never past the slot's kSess
+    const int64_t* w = reinterpret_cast<const int64_t*>(rows);
+    for (int64_t i = 0; i < r.first; ++i)
+      if (w[i * 8 + 7] > max_sess || w[i * 8 + 6] >= w[i * 8 + 7])
+        throw std::logic_error("extract_rows_into: session position out of range");
+    return r;
+  }
+  // The dense cold-row index's counters (csrc/session_store.h IndexStats) summed over shards.
+  py::dict index_stats() {
+    sess::SessionCore::IndexStats t;
+    {
+      auto g = joined_nogil();
+      t = c_.index_stats();
+    }
+    py::dict d;
+    d["indexed_takes"] = t.indexed;
+    d["multi_aborts"] = t.multi;
+    d["hot_aborts"] = t.hot;
+    d["scans"] = t.scans;
+    d["off"] = t.off;
+    d["span"] = t.span;
+    return d;
   }
   // Fire / clean up everything the watermark allows. Returns columns of emitted rows plus the
   // keys that left the store ("released"). Waits only for the hot phase of queued evictions.
@@ -369,6 +392,7 @@ class SessionStore {
       r["t_wait"] = d.t_wait;
       r["t_hot"] = d.t_hot;
       r["t_build"] = d.t_build;
+      r["t_index"] = d.t_index;
       r["t_publish"] = d.t_publish;
       out.append(r);
     }
@@ -432,6 +456,10 @@ class SessionStore {
         dcv_.notify_all();
         const auto t2 = clk::now();
         if (one && nr) sess::SessionCore::build_cold(col[0], col[1], col[2], col[3], col[4], nr, plan);
+        const auto t2b = clk::now();
+        // The cold-row index entries of the new chunk, still outside the lock: every other user
+        // of the index (extract, promote, expiry) joins this worker first.
+        if (one && nr) one->index_cold(plan);
         const auto t3 = clk::now();
         {
           std::lock_guard<std::mutex> g(mu_);
@@ -441,7 +469,8 @@ class SessionStore {
         const auto t4 = clk::now();
         d.t_wait = sec(t0, t1);
         d.t_hot = sec(t1, t2);
-        d.t_build = sec(t2, t3);
+        d.t_build = sec(t2, t2b);
+        d.t_index = sec(t2b, t3);
         d.t_publish = sec(t3, t4);
       } catch (...) {
         d.err = std::current_exception();
@@ -487,7 +516,8 @@ void bind_sessions(py::module_& m) {
       .def("merge_runs", &SessionStore::merge_runs_np)
       .def("extract", &SessionStore::extract_np)
       .def("extract_packed", &SessionStore::extract_packed_np)
-      .def("extract_dense_into", &SessionStore::extract_dense_into_np)
+      .def("extract_rows_into", &SessionStore::extract_rows_into_np)
+      .def("index_stats", &SessionStore::index_stats)
       .def("fire", &SessionStore::fire_np, py::arg("wm"), py::arg("map_code"),
            py::arg("map_consts"), py::arg("f_code"), py::arg("f_consts"),
            py::arg("expire_cold") = true)

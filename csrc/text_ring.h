@@ -12,6 +12,7 @@
 #pragma once
 #include <fcntl.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -39,8 +40,18 @@ struct Ready {
   int slot;
   int64_t nbytes;
   int64_t nlines;
-  int64_t end_off;  // file offset just past the chunk (relative to lo)
+  int64_t end_off;   // file offset just past the chunk (relative to lo)
+  intptr_t ptr = 0;  // mapped mode: the chunk's first byte inside the file mapping
 };
+
+// Mapped mode (TextRingCore(MappedTag, ...)): no slot buffers and no copy on the host. The file
+// is mmapped once; a chunk is "read" by counting its newlines with the parallel readers straight
+// from the mapping -- which also faults its pages into the process page table -- and is handed
+// out as a pointer into the mapping. The caller page-locks the mapping (hipHostRegister,
+// read-only) and the copy engine reads the page cache directly: one DMA, no CPU memcpy (the
+// pread path copies every byte once on the host). Slots are virtual: they only bound how far
+// the reader runs ahead of the consumer.
+struct MappedTag {};
 
 class TextRingCore {
  public:
@@ -60,7 +71,47 @@ class TextRingCore {
     // persistent readers: starting `threads` threads per chunk cost ~1 ms per 48 MB chunk
     if (threads_ > 1) pool_.reset(new WorkerPool(threads_ - 1));
   }
-  ~TextRingCore() { close(); }
+  // count_lines = false: no pass over the bytes on the host (nlines = -1: the consumer counts
+  // on the device); only the last page of each chunk is read (its cut at the last newline).
+  TextRingCore(MappedTag, const std::string& path, int64_t lo, int64_t hi, int nslots,
+               int64_t chunk, int threads, bool count_lines = true)
+      : lo_(lo), hi_(hi), chunk_(chunk), threads_(std::max(1, std::min(threads, 64))),
+        count_(count_lines) {
+    if (nslots < 2) throw std::invalid_argument("TextFileRing needs at least 2 slots");
+    if (lo < 0 || hi < lo) throw std::invalid_argument("bad byte range");
+    if (chunk <= 0) throw std::invalid_argument("bad chunk size");
+    for (int i = 0; i < nslots; ++i) {
+      slots_.push_back({nullptr, chunk});
+      free_.push_back(i);
+    }
+    fd_ = ::open(path.c_str(), O_RDONLY);
+    if (fd_ < 0) throw std::runtime_error("cannot open " + path + ": " + std::strerror(errno));
+    struct stat stt;
+    if (::fstat(fd_, &stt) != 0 || stt.st_size < hi) {
+      ::close(fd_);
+      fd_ = -1;
+      throw std::invalid_argument("byte range past the end of " + path);
+    }
+    map_len_ = (size_t)stt.st_size;
+    if (map_len_) {
+      void* m = ::mmap(nullptr, map_len_, PROT_READ, MAP_SHARED, fd_, 0);
+      if (m == MAP_FAILED) {
+        ::close(fd_);
+        fd_ = -1;
+        throw std::runtime_error("cannot map " + path + ": " + std::strerror(errno));
+      }
+      map_ = static_cast<char*>(m);
+      (void)::madvise(map_, map_len_, MADV_SEQUENTIAL);
+    }
+    if (threads_ > 1) pool_.reset(new WorkerPool(threads_ - 1));
+  }
+  ~TextRingCore() {
+    close();
+    if (map_) ::munmap(map_, map_len_);
+  }
+  // Mapped mode: the whole file's mapping (base, bytes); (0, 0) otherwise.
+  intptr_t map_base() const { return reinterpret_cast<intptr_t>(map_); }
+  int64_t map_bytes() const { return (int64_t)map_len_; }
 
   void start() {
     if (!th_.joinable()) th_ = std::thread([this] { run(); });
@@ -115,6 +166,26 @@ class TextRingCore {
     int64_t cap;
   };
 
+  // Mapped mode: the newlines of [off, off + len) counted from the mapping by the parallel
+  // readers (the first touch of each page happens here, off the consumer's thread).
+  void count_mapped(int64_t off, int64_t len, int64_t* newlines) {
+    const int T = (int)std::min<int64_t>(threads_, std::max<int64_t>(1, len >> 20));
+    std::vector<int64_t> cnt((size_t)T, 0);
+    const char* src = map_ + off;
+    auto piece = [&](int t) {
+      const int64_t a = len * t / T, b = len * (t + 1) / T;
+      cnt[(size_t)t] = std::count(src + a, src + b, '\n');
+    };
+    if (T == 1 || !pool_) {
+      for (int t = 0; t < T; ++t) piece(t);
+    } else {
+      pool_->run(T, piece);
+    }
+    int64_t k = 0;
+    for (int64_t x : cnt) k += x;
+    *newlines = k;
+  }
+
   bool read_range(char* dst, int64_t off, int64_t len, int64_t* newlines) {
     // `threads_` contiguous pieces read in parallel (page cache -> pinned memory copies); each
     // piece's newlines are counted right after its read, while the bytes are still in cache
@@ -159,12 +230,19 @@ class TextRingCore {
         slot = free_.front();
         free_.pop_front();
       }
-      char* dst = slots_[slot].p;
       const int64_t want = std::min(chunk_, hi_ - off);
       int64_t nl_read = 0;
-      if (!read_range(dst, off, want, &nl_read)) {
-        err = "read failed at offset " + std::to_string(off);
-        break;
+      const char* dst;
+      if (map_) {
+        dst = map_ + off;
+        if (count_) count_mapped(off, want, &nl_read);
+      } else {
+        char* buf = slots_[slot].p;
+        dst = buf;
+        if (!read_range(buf, off, want, &nl_read)) {
+          err = "read failed at offset " + std::to_string(off);
+          break;
+        }
       }
       int64_t used = want;
       if (off + want < hi_) {
@@ -176,10 +254,12 @@ class TextRingCore {
         used = nl - dst + 1;
       }
       // (the bytes past `used` hold no newline: used ends at the chunk's last one)
-      const int64_t nl = nl_read + (used > 0 && dst[used - 1] != '\n' ? 1 : 0);
+      const int64_t nl = (map_ && !count_) ? -1
+                         : nl_read + (used > 0 && dst[used - 1] != '\n' ? 1 : 0);
+      const intptr_t ptr = map_ ? reinterpret_cast<intptr_t>(dst) : 0;
       off += used;
       std::lock_guard<std::mutex> g(mu_);
-      ready_.push_back({slot, used, nl, off - lo_});
+      ready_.push_back({slot, used, nl, off - lo_, ptr});
       cv_.notify_all();
     }
     std::lock_guard<std::mutex> g(mu_);
@@ -189,8 +269,11 @@ class TextRingCore {
   }
 
   int fd_ = -1;
+  char* map_ = nullptr;
+  size_t map_len_ = 0;
   int64_t lo_, hi_, chunk_;
   int threads_;
+  bool count_ = true;
   std::unique_ptr<WorkerPool> pool_;
   std::vector<Slot> slots_;
   std::deque<int> free_;

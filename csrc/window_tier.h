@@ -752,6 +752,7 @@ class WindowTierCore {
   // maps and touches the columns of the next one (the next eviction is of similar size), so the
   // page faults run beside the stream's next steps instead of inside the next absorb.
   void prefault_async(size_t n) {
+    if (!prefault_) return;
     const size_t want = n + n / 4;
     {
       std::lock_guard<std::mutex> g(sp_mu_);
@@ -783,6 +784,11 @@ class WindowTierCore {
     for (size_t o = 0; o < bytes; o += 4096) b[o] = 0;
   }
   static constexpr size_t kMaxSpare = 3;
+
+ public:
+  bool prefault_ = true;  // A/B knob (MXS_TIER_PREFAULT=0 on the Python side)
+
+ private:
 
   int agg_;
 

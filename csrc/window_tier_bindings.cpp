@@ -26,6 +26,8 @@ void bind_window_tier(py::module_& m) {
   py::class_<WindowTierCore>(m, "WindowTier")
       .def(py::init<int>(), py::arg("agg"))
       .def("copy", [](const WindowTierCore& t) { return WindowTierCore(t); })
+      .def_readwrite("prefault", &WindowTierCore::prefault_)
+      .def_property_readonly("spare_chunks", &WindowTierCore::spare_chunks)
       .def_property_readonly("nrows", &WindowTierCore::nrows)
       .def_property_readonly("nbytes", &WindowTierCore::nbytes)
       .def_property_readonly("rows_in", &WindowTierCore::rows_in)

@@ -472,7 +472,8 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
             "active_keys": active, "table_keys": table_keys, "device": str(dev),
             "host_phase_ms_per_step": {k: round(v * 1e3 / steps, 2)
                                        for k, v in sorted(op.phase_s.items())},
-            "spill_slab_allocs": op.metrics.extra.get("spill_slab_allocs", 0)}
+            "spill_slab_allocs": op.metrics.extra.get("spill_slab_allocs", 0),
+            "store_index": op.store.index_stats() if hasattr(op.store, "index_stats") else None}
 
 
 def config6(steps: int, warmup: int, batch: int = 1 << 24, keys: int = 1_000_000,

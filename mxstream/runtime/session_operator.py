@@ -69,9 +69,9 @@ _SPILL_SIDE_STREAM = __import__("os").environ.get("MXS_SPILL_SIDE_STREAM", "1") 
 # partition ("1", default; a value outside int32 widens the step to 24-byte records and redoes
 # it) or the 24-byte plain scatter ("0", A/B).
 _REC16 = __import__("os").environ.get("MXS_SESSION_REC16", "1") != "0"
-# Promotion of revisited spilled keys through the dense-row fast path (SessionStore.
-# extract_dense_into + session_promote_rows); "0": always the general extract_packed (A/B).
-_PROMOTE_DENSE = __import__("os").environ.get("MXS_PROMOTE_DENSE", "1") != "0"
+# Promotion of revisited spilled keys through promote rows (SessionStore.extract_rows_into +
+# session_promote_rows); "0": the previous extract_packed path (A/B).
+_PROMOTE_ROWS = __import__("os").environ.get("MXS_PROMOTE_ROWS", "1") != "0"
 
 
 def _next_pow2(x: int) -> int:
@@ -112,8 +112,6 @@ class SessionMetrics:
     rehashes: int = 0
     promoted_keys: int = 0      # spilled keys handed back to HBM (records arrived for them)
     records_promoted: int = 0   # records of those keys folded on the GPU instead of the host
-    promote_dense: int = 0      # promotions that took the dense-row fast path
-    promote_fallbacks: int = 0  # promotions the fast path declined (extract_packed instead)
     current_watermark: int = I64_MIN
     steps: int = 0
     extra: dict = field(default_factory=dict)
@@ -638,59 +636,13 @@ class KeyedSessionOperator:
             dk, dt, dv = (x.clone(memory_format=torch.contiguous_format)
                           for x in self._diverted(n_host, tbase))
             dev = self.device
-            with self._phase("promote.extract"):
-                uk = torch.unique(dk)
-                ukh = uk.cpu().numpy()
-                nd = self._promote_dense(uk, ukh, wm)
-                if nd is None:
-                    # One C++ pass: the keys' sessions leave the store already laid out as HBM
-                    # slot records ([key][kSess][start, end, acc, cnt | flags << 32]) + last
-                    # activity.
-                    ex = self.store.extract_packed(ukh, wm, K_SESS, self.gap)
-            if nd is not None:
-                moved = ukh
+            uk = torch.unique(dk)
+            ukh = uk.cpu().numpy()
+            if _PROMOTE_ROWS:
+                n_moved = self._promote_rows(uk, ukh, wm)
             else:
-                moved = ex["moved"]
-                nk = len(ex["key"])
-            if nd is None and nk:
-                with self._phase("promote.scatter"):
-                    ukeys = torch.from_numpy(ex["key"]).to(dev, non_blocking=True)
-                    rec = torch.from_numpy(ex["rec"]).to(dev, non_blocking=True)
-                    last = torch.from_numpy(ex["last"]).to(dev, non_blocking=True)
-                    slots_t = torch.empty_like(ukeys)
-                    self.ctr[3:5].zero_()
-                    self.native.gpu_session_slot_insert(ukeys.data_ptr(), nk, self.nsub_log2,
-                                                        self.cap_log2, self.keys_g.data_ptr(),
-                                                        slots_t.data_ptr(),
-                                                        self.ctr[3:4].data_ptr(), self._st())
-                    self.native.gpu_session_promote(slots_t.data_ptr(), rec.data_ptr(),
-                                                    last.data_ptr(), nk, self.sess.data_ptr(),
-                                                    self.slot_due.data_ptr(),
-                                                    self.slot_last.data_ptr(),
-                                                    self.ctr[4:5].data_ptr(), self._st())
-                    ins, n_bad = self.ctr[3:5].tolist()
-                    self._live_estimate += ins
-                if n_bad:  # sub-table full (rare): those keys' sessions go back to the store
-                    slots = slots_t.cpu().numpy()
-                    bad = slots < 0
-                    r = ex["rec"].reshape(nk, K_SESS, 4)[bad]
-                    kk = np.repeat(ex["key"][bad], K_SESS)
-                    rr = r.reshape(-1, 4)
-                    live = (rr[:, 3] & 0xFFFFFFFF) != 0
-                    self.store.insert(np.ascontiguousarray(kk[live]),
-                                      np.ascontiguousarray(rr[live, 0]),
-                                      np.ascontiguousarray(rr[live, 1]),
-                                      np.ascontiguousarray(rr[live, 2]),
-                                      np.ascontiguousarray(rr[live, 3] & 0xFFFFFFFF),
-                                      np.ascontiguousarray(rr[live, 3] >> 32), False)
-                    moved = np.setdiff1d(moved, ex["key"][bad])
-            if nd is not None:
-                pass  # the spill set already lost the keys (_promote_dense)
-            elif len(moved):
-                mt = torch.from_numpy(np.ascontiguousarray(moved, dtype=np.int64)).to(dev)
-                self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
-                                          mt.data_ptr(), mt.numel(), self._st())
-            self.metrics.promoted_keys += len(moved)
+                n_moved = self._promote_packed(ukh, wm)
+            self.metrics.promoted_keys += n_moved
             # Re-partition the diverted records (local sub-tables only) and fold them.
             # Private bucket buffers sized for these records (the exchange buffers must keep the
             # same size on every rank, so they are never regrown locally).
@@ -717,40 +669,49 @@ class KeyedSessionOperator:
             late += self._overflow_runs(h, wm)
             return h[2], late
 
-    def _promote_dense(self, uk, ukh, wm: int):
-        """The revisit fast path (config 5 with revisits): when every revisited key is cold in the
-        store with at most one session, the store writes one dense row per kept session
-        {key, start, end, acc, cnt | flags << 32, last activity} straight into a reused pinned
-        buffer (SessionStore.extract_dense_into: one parallel scan, no per-key containers); ONE
-        copy takes the rows to HBM and ONE kernel (session_promote_rows) inserts each key's slot
-        and writes its record. The keys leave the device spill set from the device copy of the
-        unique keys (no second upload). Returns None when the store says the fast path does not
-        apply (nothing changed: the caller takes extract_packed)."""
+    def _promote_rows(self, uk, ukh, wm: int) -> int:
+        """The promote path's host side in one C++ call and one copy: the store writes the
+        revisited keys' sessions as promote rows {key, start, end, acc, cnt | flags << 32, last
+        activity, position, sessions of the key} straight into a reused pinned buffer
+        (SessionStore.extract_rows_into: with the dense cold-row index, one lookup per key
+        instead of a scan of every cold row; the general extract otherwise), plus the keys that
+        left the store. ONE copy takes the rows to HBM and session_promote_rows (two launches:
+        slot insert + record 0, then further positions) writes the slots. The keys leave the
+        device spill set from the device copy of the unique keys when all of them moved (no
+        upload). Returns the number of keys that left the store."""
         n = len(ukh)
-        if n == 0 or not _PROMOTE_DENSE or self.store.shards() != 1:
-            return None
-        if getattr(self, "_pd_host", None) is None or self._pd_host.shape[0] < n:
-            cap = max(1024, 1 << (n - 1).bit_length())
-            self._pd_host = torch.empty((cap, 6), dtype=torch.int64, pin_memory=True)
-            self._pd_dev = torch.empty((cap, 6), dtype=torch.int64, device=self.device)
+        if n == 0:
+            return 0
+        rows_cap = n * K_SESS
+        if getattr(self, "_pd_host", None) is None or self._pd_host.shape[0] < rows_cap:
+            cap = max(1024, 1 << (rows_cap - 1).bit_length())
+            self._pd_host = torch.empty((cap, 8), dtype=torch.int64, pin_memory=True)
+            self._pd_moved = torch.empty(cap, dtype=torch.int64, pin_memory=True)
+            self._pd_dev = torch.empty((cap, 8), dtype=torch.int64, device=self.device)
             self._pd_slots = torch.empty(cap, dtype=torch.int64, device=self.device)
         if getattr(self, "_pd_copied", None) is not None:
-            self._pd_copied.synchronize()  # the previous upload has left the pinned rows
-        hrows = self._pd_host
-        nk = self.store.extract_dense_into(ukh, wm, self.gap, hrows.data_ptr(), hrows.shape[0])
-        if nk < 0:
-            self.metrics.promote_fallbacks += 1
-            return None
+            self._pd_copied.synchronize()  # the previous upload has left the pinned buffers
+        hrows, hmoved = self._pd_host, self._pd_moved
+        with self._phase("promote.extract"):
+            nk, nm = self.store.extract_rows_into(ukh, wm, K_SESS, self.gap, hrows.data_ptr(),
+                                                  hrows.shape[0], hmoved.data_ptr(),
+                                                  hmoved.numel())
         st = self._st()
-        self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
-                                  uk.data_ptr(), uk.numel(), st)
-        if nk == 0:
-            return 0
         with self._phase("promote.scatter"):
-            self._pd_dev[:nk].copy_(hrows[:nk], non_blocking=True)
+            if nm == n:
+                mt = uk  # every wanted key left the store
+            else:
+                mt = hmoved[:nm].to(self.device, non_blocking=True)
+            if nm:
+                self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
+                                          mt.data_ptr(), nm, st)
+            if nk:
+                self._pd_dev[:nk].copy_(hrows[:nk], non_blocking=True)
             if getattr(self, "_pd_copied", None) is None:
                 self._pd_copied = torch.cuda.Event()
             self._pd_copied.record(torch.cuda.current_stream(self.device))
+            if nk == 0:
+                return nm
             self.ctr[3:5].zero_()
             self.native.gpu_session_promote_rows(self._pd_dev.data_ptr(), nk, self.nsub_log2,
                                                  self.cap_log2, self.keys_g.data_ptr(),
@@ -768,12 +729,57 @@ class KeyedSessionOperator:
                               np.ascontiguousarray(r[:, 2]), np.ascontiguousarray(r[:, 3]),
                               np.ascontiguousarray(r[:, 4] & 0xFFFFFFFF),
                               np.ascontiguousarray(r[:, 4] >> 32), False)
-            bk = torch.from_numpy(np.ascontiguousarray(r[:, 0])).to(self.device)
+            bk = torch.from_numpy(np.unique(r[:, 0])).to(self.device)
             self.native.gpu_set_insert(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
                                        bk.data_ptr(), bk.numel(), st)
             self.set_used += int(bk.numel())
-        self.metrics.promote_dense += 1
-        return nk
+            nm -= int(bk.numel())
+        return nm
+
+    def _promote_packed(self, ukh, wm: int) -> int:
+        """The previous promote path (MXS_PROMOTE_ROWS=0, A/B): extract_packed's slot records
+        ([key][kSess][4]) + last activity, three uploads, slot insert + promote kernels, the
+        moved keys uploaded for the spill-set erase. Returns the number of keys that left."""
+        dev = self.device
+        with self._phase("promote.extract"):
+            ex = self.store.extract_packed(ukh, wm, K_SESS, self.gap)
+        moved = ex["moved"]
+        nk = len(ex["key"])
+        if nk:
+            with self._phase("promote.scatter"):
+                ukeys = torch.from_numpy(ex["key"]).to(dev, non_blocking=True)
+                rec = torch.from_numpy(ex["rec"]).to(dev, non_blocking=True)
+                last = torch.from_numpy(ex["last"]).to(dev, non_blocking=True)
+                slots_t = torch.empty_like(ukeys)
+                self.ctr[3:5].zero_()
+                self.native.gpu_session_slot_insert(ukeys.data_ptr(), nk, self.nsub_log2,
+                                                    self.cap_log2, self.keys_g.data_ptr(),
+                                                    slots_t.data_ptr(),
+                                                    self.ctr[3:4].data_ptr(), self._st())
+                self.native.gpu_session_promote(slots_t.data_ptr(), rec.data_ptr(),
+                                                last.data_ptr(), nk, self.sess.data_ptr(),
+                                                self.slot_due.data_ptr(),
+                                                self.slot_last.data_ptr(),
+                                                self.ctr[4:5].data_ptr(), self._st())
+                ins, n_bad = self.ctr[3:5].tolist()
+                self._live_estimate += ins
+            if n_bad:  # sub-table full (rare): those keys' sessions go back to the store
+                bad = slots_t.cpu().numpy() < 0
+                rr = ex["rec"].reshape(nk, K_SESS, 4)[bad].reshape(-1, 4)
+                kk = np.repeat(ex["key"][bad], K_SESS)
+                live = (rr[:, 3] & 0xFFFFFFFF) != 0
+                self.store.insert(np.ascontiguousarray(kk[live]),
+                                  np.ascontiguousarray(rr[live, 0]),
+                                  np.ascontiguousarray(rr[live, 1]),
+                                  np.ascontiguousarray(rr[live, 2]),
+                                  np.ascontiguousarray(rr[live, 3] & 0xFFFFFFFF),
+                                  np.ascontiguousarray(rr[live, 3] >> 32), False)
+                moved = np.setdiff1d(moved, ex["key"][bad])
+        if len(moved):
+            mt = torch.from_numpy(np.ascontiguousarray(moved, dtype=np.int64)).to(dev)
+            self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
+                                      mt.data_ptr(), mt.numel(), self._st())
+        return len(moved)
 
     def _overflow_runs(self, h, wm: int) -> int:
         """Keys whose merge produced more than kSess sessions move to the host tier."""
@@ -975,7 +981,7 @@ class KeyedSessionOperator:
             self.set_used += r["nr"]
             self.metrics.freed_slots += r["ne"]
             self.metrics.spilled_keys += r["nk"]
-            for k in ("wait", "hot", "build", "publish"):  # the worker's own phase times
+            for k in ("wait", "hot", "build", "index", "publish"):  # the worker's own phase times
                 self.phase_s[f"spill.worker.{k}"] += r[f"t_{k}"]
 
     def _ensure_spill_capacity(self, extra: int) -> None:

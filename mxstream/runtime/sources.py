@@ -218,6 +218,11 @@ _H2D_BLOCKS = int(__import__("os").environ.get("MXS_H2D_BLOCKS", "512"))
 _RING_SLOTS = max(3, int(__import__("os").environ.get("MXS_RING_SLOTS", "8")))
 # Slots are page-locked pageable buffers (hipHostRegister) instead of pinned allocations.
 _SLOT_REGISTER = __import__("os").environ.get("MXS_SLOT_REGISTER", "0") == "1"
+# Device ingest reads the file through its mapping (csrc/text_ring.h mapped mode): the mapping is
+# page-locked read-only once and every chunk goes page cache -> HBM in one DMA, no host memcpy.
+# "0": the pread reader into pinned slots.
+_TEXT_MMAP = __import__("os").environ.get("MXS_TEXT_MMAP", "1") != "0"
+_HIP_REGISTER_READONLY = 0x08
 
 
 def _native():
@@ -288,13 +293,7 @@ class TextFileSource(Source):
 
         chunk = max(1 << 20, self.batch * 48)
         self._pin = torch.cuda.is_available()
-        self._slots = _take_slots(chunk, _RING_SLOTS, self._pin)
-        self._ring = load().TextFileRing(self.path, self.lo + start, self.hi,
-                                         [(t.data_ptr(), t.numel()) for t in self._slots], chunk,
-                                         min(16, max(1, __import__("os").cpu_count() or 1)))
-        self._ring.start()
-        self._held: list = []
-        self._pre = None  # prefetched (TextBatch, end offset)
+        threads = min(16, max(1, __import__("os").cpu_count() or 1))
         self._cstream = None
         if self.ring_device is not None and str(self.ring_device).startswith("cuda") \
                 and torch.cuda.is_available():
@@ -302,6 +301,24 @@ class TextFileSource(Source):
             if self._dev.index is None:
                 self._dev = torch.device("cuda", torch.cuda.current_device())
             self._cstream = torch.cuda.Stream(self._dev)
+        self._mapped = False
+        self._slots = []
+        self._nslots = _RING_SLOTS
+        if _TEXT_MMAP and self._cstream is not None:
+            ring = load().TextFileRing.mapped(self.path, self.lo + start, self.hi, _RING_SLOTS,
+                                              chunk, threads)
+            if ring.register_mapping(_HIP_REGISTER_READONLY) == 0:
+                self._ring, self._mapped = ring, True
+            else:  # no page-locked mapping on this system: the pread reader
+                ring.close()
+        if not self._mapped:
+            self._slots = _take_slots(chunk, _RING_SLOTS, self._pin)
+            self._ring = load().TextFileRing(self.path, self.lo + start, self.hi,
+                                             [(t.data_ptr(), t.numel()) for t in self._slots],
+                                             chunk, threads)
+        self._ring.start()
+        self._held: list = []
+        self._pre = None  # prefetched (TextBatch, end offset)
         self.bpos = start
         self._ring_done = self.lo + start >= self.hi
 
@@ -373,12 +390,26 @@ class TextFileSource(Source):
         """The next filled slot as a TextBatch (+ its end offset), or None."""
         from .columnar import TextBatch
 
-        slot, nbytes, nlines, end, eof = self._ring.next(timeout_ms)
+        slot, nbytes, nlines, end, eof, ptr = self._ring.next(timeout_ms)
         if slot < 0:
             if eof:
                 self._ring_eof = True
             return None
         tok = SlotToken(slot)
+        if self._mapped:
+            # the chunk's bytes in the page-locked file mapping: one DMA on the copy stream
+            import torch
+
+            with torch.cuda.stream(self._cstream):
+                dev = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self._dev)
+                rc = _native().gpu_h2d_async(dev.data_ptr(), int(ptr), int(nbytes),
+                                             self._cstream.cuda_stream)
+                if rc:
+                    raise RuntimeError(f"text upload: hip error {rc}")
+                ev = torch.cuda.Event()
+                ev.record(self._cstream)
+            tok.uploaded(ev)
+            return TextBatch(dev[:nbytes], int(nlines), token=tok, ready=ev), end
         tb = TextBatch(self._slots[slot][:nbytes], int(nlines), token=tok)
         if self._cstream is not None:
             # H2D on the copy stream now: the consumer waits for `ready` (an event) instead of
@@ -417,7 +448,7 @@ class TextFileSource(Source):
         # Slots whose upload completed go back to the reader.
         keep = []
         for t in self._held:
-            if t.ready(wait=len(self._held) >= len(self._slots) - 1 and t is self._held[0]):
+            if t.ready(wait=len(self._held) >= self._nslots - 1 and t is self._held[0]):
                 self._ring.release(t.slot)
             else:
                 keep.append(t)
@@ -437,7 +468,7 @@ class TextFileSource(Source):
         self.bpos = end
         self._ring_done = self.lo + end >= self.hi
         if self._cstream is not None and not self._ring_done \
-                and len(self._held) < len(self._slots) - 1:
+                and len(self._held) < self._nslots - 1:
             self._ring_eof = False
             self._pre = self._take(0)  # prefetch: its H2D overlaps this batch's processing
         return [tb], self._ring_done and self._pre is None

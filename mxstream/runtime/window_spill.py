@@ -73,6 +73,9 @@ class HostWindowTier:
 
         self.agg = agg
         self._t = _core if _core is not None else load().WindowTier(agg)
+        # columns of the next eviction's chunk mapped on a background thread after every absorb
+        # (csrc/window_tier.h prefault_async); "0": A/B
+        self._t.prefault = __import__("os").environ.get("MXS_TIER_PREFAULT", "1") != "0"
         # An eviction absorbed on a background thread (absorb_presorted(background=True)): every
         # reader joins it first; a purge meanwhile is deferred to the join (purges only free
         # memory -- a firing's export never reads panes below the purge cutoff).

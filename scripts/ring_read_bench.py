@@ -51,7 +51,7 @@ def main():
                 ring.start()
                 got = lines = 0
                 while True:
-                    slot, nbytes, nl, end, eof = ring.next(1000)
+                    slot, nbytes, nl, end, eof, _ = ring.next(1000)
                     if slot < 0:
                         if eof:
                             break

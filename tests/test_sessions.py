@@ -257,51 +257,86 @@ def _dense_store(m, nk, nchunks, seed):
     return st_, rng
 
 
-def test_store_extract_dense_into_equals_extract_packed():
-    """The revisit fast path (SessionStore.extract_dense_into, one parallel block scan writing
-    dense rows into caller memory) hands back exactly extract_packed's sessions: same keys, same
-    slot record 0, same last activity; rows past cleanup at wm are dropped, every wanted key
-    leaves the store, and a second extract finds nothing."""
+def _rows_by_key(rows, nk):
+    out, lasts = {}, {}
+    for r in rows[:nk]:
+        key, s, e, a, cf, last, pos, ns = (int(x) for x in r)
+        assert 0 <= pos < ns <= 4
+        out.setdefault(key, [None] * ns)[pos] = (s, e, a, cf)
+        lasts[key] = last
+    return {k: v + [("last", lasts[k])] for k, v in out.items()}
+
+
+def _packed_by_key(ex):
+    out = {}
+    rec = ex["rec"].reshape(-1, 4, 4)
+    for i, key in enumerate(ex["key"].tolist()):
+        ss = [tuple(int(x) for x in rec[i, j]) for j in range(4) if rec[i, j, 3] & 0xFFFFFFFF]
+        out[key] = ss + [("last", int(ex["last"][i]))]
+    return out
+
+
+def _extract_both(a, b, want, wm):
+    rows = np.zeros((want.size * 4, 8), np.int64)
+    moved = np.zeros(want.size, np.int64)
+    nk, nm = a.extract_rows_into(want, wm, 4, 100, rows.ctypes.data, rows.shape[0],
+                                 moved.ctypes.data, moved.size)
+    ex = b.extract_packed(want, wm, 4, 100)
+    assert _rows_by_key(rows, nk) == _packed_by_key(ex)
+    assert np.array_equal(np.sort(moved[:nm]), np.sort(ex["moved"]))
+    return nk, nm
+
+
+def test_store_extract_rows_into_equals_extract_packed():
+    """The promote path's extract into caller memory (SessionStore.extract_rows_into: the dense
+    cold-row index, one lookup per wanted key) hands back exactly extract_packed's sessions:
+    same keys, same slot records, same last activity, same moved keys; rows past cleanup at wm
+    are dropped and the rows leave the store (a second extract finds nothing)."""
     from mxstream.ops.native import load
 
     m = load()
     a, rng = _dense_store(m, 300_000, 3, 11)
     b, _ = _dense_store(m, 300_000, 3, 11)
-    want = rng.choice(300_000, 40_000, replace=False).astype(np.int64)
+    want = np.sort(rng.choice(300_000, 40_000, replace=False)).astype(np.int64)
     wm = 10_000 + 2000 + 100 + 1000  # keys with start < 12_000 - 1 are past cleanup
-    out = np.zeros((want.size, 6), np.int64)
-    nk = a.extract_dense_into(want, wm, 100, out.ctypes.data, want.size)
-    ex = b.extract_packed(want, wm, 4, 100)
-    assert nk == ex["key"].size > 0
-    order = np.argsort(out[:nk, 0])
-    got = out[:nk][order]
-    rec = ex["rec"].reshape(-1, 4, 4)
-    assert np.array_equal(got[:, 0], ex["key"])
-    assert np.array_equal(got[:, 1:5], rec[:, 0, :])
-    assert np.array_equal(got[:, 5], ex["last"])
+    nk, nm = _extract_both(a, b, want, wm)
+    assert 0 < nk < want.size and nm == want.size
+    # independent of the store: the sessions inserted by _dense_store, cleanup = end - 1 + 1000
+    start = want % 4000 + 10_000
+    assert nk == int(np.count_nonzero(start + 100 - 1 + 1000 > wm))
     assert a.num_cold_rows() == b.num_cold_rows() == 300_000 - want.size
-    assert a.extract_dense_into(want, wm, 100, out.ctypes.data, want.size) in (0, -1)
+    nk2, _ = _extract_both(a, b, want, wm)
+    assert nk2 == 0
 
 
-def test_store_extract_dense_into_declines_without_change():
-    """-1 and an unchanged store when the fast path does not apply: a key with two cold rows, or
-    hot sessions in the store."""
+def test_store_extract_rows_into_multi_and_hot_keys():
+    """Keys with two cold rows (the index marks them and the scan takes over), keys with hot
+    sessions, unsorted wanted keys and keys the store never held: still extract_packed's
+    result, with several sessions of a key at positions 0, 1, ... and keys above max_sess
+    staying in the store."""
     from mxstream.ops.native import load
 
     m = load()
-    st_, _ = _dense_store(m, 10_000, 2, 3)
-    k = np.array([7], np.int64)
-    st_.insert(k, np.array([50_000], np.int64), np.array([50_100], np.int64), k, np.ones(1, np.int64),
-               np.ones(1, np.int64), True)  # key 7's second cold row
-    out = np.zeros((100, 6), np.int64)
-    want = np.arange(0, 100, dtype=np.int64)
-    rows = st_.num_cold_rows()
-    assert st_.extract_dense_into(want, 0, 100, out.ctypes.data, 100) == -1
-    assert st_.num_cold_rows() == rows
-    hot, _ = _dense_store(m, 10_000, 2, 3)
-    hot.process(np.array([20_000], np.int64), np.array([5], np.int64), np.array([1], np.int64), 0)
-    assert hot.extract_dense_into(want, 0, 100, out.ctypes.data, 100) == -1
-    assert hot.num_cold_rows() == 10_000
+    stores = []
+    for _ in range(2):
+        st_, _ = _dense_store(m, 50_000, 2, 3)
+        k = np.array([7, 8], np.int64)
+        one = np.ones(2, np.int64)
+        st_.insert(k, np.array([50_000, 60_000], np.int64), np.array([50_100, 60_100], np.int64),
+                   k, one, one, True)  # keys 7 and 8: a second cold row
+        st_.process(np.array([20, 20, 21], np.int64), np.array([90_000, 95_000, 5], np.int64),
+                    np.array([1, 2, 3], np.int64), 0)  # hot sessions of keys 20 and 21
+        for t in range(5):  # key 30: five sessions, more than a slot holds
+            st_.process(np.array([30], np.int64), np.array([200_000 + t * 1000], np.int64),
+                        np.array([1], np.int64), 0)
+        stores.append(st_)
+    want = np.array([21, 8, 7, 20, 30, 999_999, 3, 4, 5], np.int64)
+    nk, nm = _extract_both(stores[0], stores[1], want, 0)
+    assert nm == want.size - 1  # key 30 stays
+    assert stores[0].num_keys() == stores[1].num_keys()
+    # the multi keys' entries are cleared: the next extract takes the indexed path again
+    w2 = np.arange(100, 200, dtype=np.int64)
+    _extract_both(stores[0], stores[1], w2, 0)
 
 
 @pytest.mark.parametrize("shards", [2, 8])
@@ -521,8 +556,8 @@ def test_gpu_sessions_spill_set_grows_on_device():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("promote,dense", [(True, True), (True, False), (False, False)])
-def test_gpu_spilled_keys_return_to_hbm(promote, dense, monkeypatch):
+@pytest.mark.parametrize("promote,rows", [(True, True), (True, False), (False, False)])
+def test_gpu_spilled_keys_return_to_hbm(promote, rows, monkeypatch):
     # Keys go idle (spilled to host DRAM with fired sessions inside the lateness), then receive
     # records again: with promotion their sessions come back to HBM slots and the records are
     # folded on the GPU; without it the host store folds them. Both equal the CPU store.
@@ -537,16 +572,13 @@ def test_gpu_spilled_keys_return_to_hbm(promote, dense, monkeypatch):
     kw = dict(max_load=0.05, idle_spill_ms=3_000, cap_log2=7)
     import mxstream.runtime.session_operator as so
 
-    monkeypatch.setattr(so, "_PROMOTE_DENSE", dense)
+    monkeypatch.setattr(so, "_PROMOTE_ROWS", rows)
     b, op = engine_with(events, 5_000, 2_000, 30_000, promote=promote, device="cuda", batch=600, **kw)
     a2, _ = engine(events, 5_000, 2_000, 30_000, device="cpu", batch=600)
     assert a2 == b
     assert op.metrics.spilled_keys > 0
     if promote:
         assert op.metrics.promoted_keys > 0 and op.metrics.records_promoted > 0
-        print("promote dense/fallback:", op.metrics.promote_dense, op.metrics.promote_fallbacks)
-        if not dense:
-            assert op.metrics.promote_dense == 0
     else:
         assert op.metrics.records_to_host > 0
 
