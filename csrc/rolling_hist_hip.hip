@@ -358,10 +358,20 @@ __global__ __launch_bounds__(256) void rolling_hist_prefix_kernel(uint32_t* __re
   }
 }
 
+// Select path of the emit pass (a filtered counter whose filter passes few counts, e.g.
+// `count % 1000 == 0`, config 2): instead of ranking every record of the chunk, find the few
+// records whose post-update count passes. Limits of the chunk-local lists (over them, or for a
+// slot with more than kSelMaxRun records in the chunk, the chunk takes the ranking path).
+constexpr uint32_t kSelSlots = 1024;   // distinct slots with a passing count in the chunk
+constexpr uint32_t kSelRecs = 8192;    // records of those slots in the chunk
+constexpr uint32_t kSelMaxRun = 512;   // records of one such slot in the chunk
+constexpr uint32_t kSelNone = 0xFFFFFFFFu;
+
 __global__ __launch_bounds__(kTile) void rolling_hist_emit_kernel(
     const uint16_t* __restrict__ slot16, uint32_t n, uint32_t chunk,
     const uint32_t* __restrict__ part, uint32_t nslots, const uint64_t* __restrict__ keys_g,
-    ExprProg filt, int need_key, int dense, uint64_t* __restrict__ out_key,
+    const uint32_t* __restrict__ cnt_g, ExprProg filt, int need_key, int dense,
+    uint64_t* __restrict__ out_key,
     uint64_t* __restrict__ out_val, int64_t* __restrict__ out_tag, uint32_t* __restrict__ out_n,
     uint32_t out_cap, uint32_t ablate) {
   // LDS (<= 160 KB at 16K slots): run[nslots] u32 | owner[nslots] u16 | lane masks
@@ -379,12 +389,118 @@ __global__ __launch_bounds__(kTile) void rolling_hist_emit_kernel(
   const uint32_t lo = blockIdx.x * chunk;
   const uint32_t hi = n - lo < chunk ? n : lo + chunk;
   const uint32_t* pre = part + (size_t)blockIdx.x * nslots;
+  const uint64_t below = (1ull << lane) - 1ull;
+  const ChainRegs chain = decode_chain(filt);
+  // The filter on a post-update count of a slot (the rolling epilogue's variables).
+  auto passes = [&](uint32_t pcount, uint32_t slot) -> bool {
+    if (ablate & 64u) return pcount % 100000u == 0;  // timing reference only
+    if (chain.intmode && !(ablate & 128u)) return eval_chain_int(chain, pcount);
+    const double key = !need_key ? 0.0 : dense ? (double)slot : (double)keys_g[slot];
+    const RollVars rv{(double)pcount, (double)pcount, key, (double)pcount};
+    return eval_chain_regs(chain, filt, rv) != 0.0;
+  };
+  if (filt.ncode && !(ablate & (16u | 256u))) {
+    // ---- select path --------------------------------------------------------------------
+    // 1. per slot: its records in this chunk take counts pre+1 .. pre+h (h from the next
+    //    chunk's prefix); a slot with a passing count among them joins the distinct list.
+    // 2. every record of a listed slot drops its chunk-local index into the slot's bucket.
+    // 3. a bucket entry's rank = entries of its bucket with a smaller index (buckets are
+    //    short): count = pre + rank + 1, emitted when it passes. Rows are unordered (tagged).
+    // LDS: aidx[nslots] (over run[]), the lists (over the lane masks).
+    uint32_t* aidx = lds;
+    uint32_t* L = (uint32_t*)m64;
+    uint32_t* dslot = L;
+    uint32_t* dlo = L + kSelSlots;
+    uint32_t* dh = L + 2 * kSelSlots;
+    uint32_t* doff = L + 3 * kSelSlots;
+    uint32_t* dfill = L + 4 * kSelSlots;
+    uint16_t* bucket = (uint16_t*)(L + 5 * kSelSlots);
+    uint16_t* bslot = bucket + kSelRecs;
+    uint32_t* sc = L + 5 * kSelSlots + kSelRecs;  // [0] distinct, [1] records, [2] over
+    // the chunk's end counts: the next chunk's prefixes, or the slots' totals for the last
+    const uint32_t* nxt = blockIdx.x + 1 < gridDim.x ? pre + nslots : cnt_g;
+    for (uint32_t s = tid; s < nslots; s += kTile) aidx[s] = kSelNone;
+    if (tid < 4) sc[tid] = 0;
+    __syncthreads();
+    for (uint32_t s = tid; s < nslots; s += kTile) {
+      const uint32_t p0 = pre[s];
+      const uint32_t p1 = nxt[s];
+      const uint32_t h = p1 - p0;
+      if (!h) continue;
+      if (h > kSelMaxRun) {  // a hot slot: its bucket would be too long to rank by counting
+        sc[2] = 1u;
+        continue;
+      }
+      bool any = false;
+      for (uint32_t c = p0 + 1; c <= p1 && !any; ++c) any = passes(c, s);
+      if (!any) continue;
+      const uint32_t d = atomicAdd(&sc[0], 1u);
+      const uint32_t at = atomicAdd(&sc[1], h);
+      if (d >= kSelSlots || at + h > kSelRecs) {
+        sc[2] = 1u;
+        continue;
+      }
+      aidx[s] = d;
+      dslot[d] = s;
+      dlo[d] = p0;
+      dh[d] = h;
+      doff[d] = at;
+      dfill[d] = 0;
+    }
+    __syncthreads();
+    const bool sel = sc[2] == 0u;
+    if (sel) {
+      const uint32_t nd = sc[0];
+      if (nd) {
+        for (uint32_t i = lo + tid; i < hi; i += kTile) {
+          const uint32_t slot = slot16[i];
+          if (slot == kNoSlot16) continue;
+          const uint32_t d = aidx[slot];
+          if (d == kSelNone) continue;
+          const uint32_t q = doff[d] + atomicAdd(&dfill[d], 1u);
+          bucket[q] = (uint16_t)(i - lo);
+          bslot[q] = (uint16_t)d;
+        }
+        __syncthreads();
+        const uint32_t nrec = sc[1];
+        for (uint32_t base = 0; base < nrec; base += kTile) {  // block-uniform trip count
+          const uint32_t e = base + tid;
+          bool emit = false;
+          uint32_t slot = 0, pcount = 0, li = 0;
+          if (e < nrec) {
+            const uint32_t d = bslot[e];
+            li = bucket[e];
+            const uint32_t b0 = doff[d], b1 = b0 + dh[d];
+            uint32_t rank = 0;
+            for (uint32_t j = b0; j < b1; ++j) rank += bucket[j] < li;
+            slot = dslot[d];
+            pcount = dlo[d] + rank + 1;
+            emit = passes(pcount, slot);
+          }
+          const unsigned long long m = __ballot(emit);
+          if (m) {  // wave-uniform
+            uint32_t wb = 0;
+            if (lane == 0) wb = atomicAdd(out_n, (uint32_t)__popcll(m));
+            wb = __shfl(wb, 0);
+            if (emit) {
+              const uint32_t q = wb + (uint32_t)__popcll(m & below);
+              if (q < out_cap) {
+                out_key[q] = dense ? slot : keys_g[slot];
+                out_val[q] = pcount;
+                out_tag[q] = (int64_t)(lo + li);
+              }
+            }
+          }
+        }
+      }
+      return;  // block-uniform
+    }
+    __syncthreads();  // the ranking path below reuses the LDS
+  }
   for (uint32_t s = tid; s < nslots; s += kTile) run[s] = pre[s];
   for (uint32_t e = tid; e < 2 * kTile * kTileWaves; e += kTile) m64[e] = 0;
   if (!filt.ncode && blockIdx.x == 0 && tid == 0) atomicAdd(out_n, n);  // rows = records
   __syncthreads();
-  const uint64_t below = (1ull << lane) - 1ull;
-  const ChainRegs chain = decode_chain(filt);
   uint32_t pend_slot = kNoSlot, pend_cnt = 0;  // running-count update of the previous tile
   bool was_owner = false;                        // this thread's masks of the previous tile
   uint32_t buf = 0;
@@ -434,17 +550,7 @@ __global__ __launch_bounds__(kTile) void rolling_hist_emit_kernel(
         pend_cnt = pcount;
       }
       emit = !(ablate & 16u);
-      if (filt.ncode && !(ablate & 16u)) {
-        if (ablate & 64u) {
-          emit = pcount % 100000u == 0;  // timing reference only
-        } else if (chain.intmode && !(ablate & 128u)) {
-          emit = eval_chain_int(chain, pcount);
-        } else {
-          const double key = !need_key ? 0.0 : dense ? (double)slot : (double)keys_g[slot];
-          const RollVars rv{(double)pcount, (double)pcount, key, (double)pcount};
-          emit = eval_chain_regs(chain, filt, rv) != 0.0;
-        }
-      }
+      if (filt.ncode && !(ablate & 16u)) emit = passes(pcount, slot);
     }
     buf ^= 1;
     if (!filt.ncode) {  // every record emits: its row index is its arrival index (no atomics)
@@ -526,10 +632,11 @@ void rolling_hist(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
   for (int i = 0; i < filt.ncode; ++i)
     if (filt.code[2 * i] == OP_VAR && filt.code[2 * i + 1] == 4) need_key = 1;
   hipStream_t s = (hipStream_t)stream;
-  // MXS_RH_ABLATE (timing experiments only; results are wrong when set): 1 no probe past the
-  // home window, 2 no histogram atomics, 4 owner = slot % 512, 8 no lane-mask ORs, 16 no filter
-  // evaluation and no rows, 32 no lane-mask reads, 64 filter hard-coded as count % 100000 == 0,
-  // 128 no integer-mode chain (f64 evaluation of the decoded chain).
+  // MXS_RH_ABLATE (timing experiments only; results are wrong when set, except 128 and 256): 1
+  // no probe past the home window, 2 no histogram atomics, 4 owner = slot % 512, 8 no lane-mask
+  // ORs, 16 no filter evaluation and no rows, 32 no lane-mask reads, 64 filter hard-coded as
+  // count % 100000 == 0, 128 no integer-mode chain (f64 evaluation of the decoded chain), 256 no
+  // select path (every filtered chunk ranks all its records).
   static const uint32_t ablate = [] {
     const char* e = std::getenv("MXS_RH_ABLATE");
     return e ? (uint32_t)std::strtoul(e, nullptr, 0) : 0u;
@@ -552,7 +659,7 @@ void rolling_hist(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, 
                      keys_g, dense);
   const size_t lds = (size_t)ns * 6 + (size_t)2 * kTile * kTileWaves * 8;  // 160 KB at 16K
   hipLaunchKernelGGL(rolling_hist_emit_kernel, dim3(g.nb), dim3(kTile), lds, s, slot16,
-                     (uint32_t)n, g.chunk, part, ns, keys_g, filt, need_key, dense, out_key,
+                     (uint32_t)n, g.chunk, part, ns, keys_g, cnt_g, filt, need_key, dense, out_key,
                      out_val, out_tag, out_n, out_cap, ablate);
   HIP_CHECK(hipGetLastError());
 }

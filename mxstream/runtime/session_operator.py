@@ -195,6 +195,15 @@ class KeyedSessionOperator:
             # counters: [0] n_out [1] n_heads [2] n_host [3] n_inserted(step) [4] n_ovf
             #           [5] n_ovf_runs [6] fire n_out [7] evict rows [8] evicted [9] rehash ins
             self.ctr = torch.zeros(16, dtype=torch.int32, device=dev)
+            # The two pinned slabs of the asynchronous eviction copy, at their final size now
+            # (page-locking ~100 MB costs ~15 ms: never inside a step).
+            nb = ((self.ctr.numel() * 4 + 255) & ~255) + 6 * ((self.spill_rows * 8 + 255) & ~255)
+            self._spill_slabs = []
+            for _ in range(2):
+                t = torch.empty(_next_pow2(nb), dtype=torch.uint8, pin_memory=True)
+                self._spill_slabs.append([t, t.numpy(), 0])  # tensor, array, job id
+            self._spill_turn = 0
+            self._spill_allocs = 0
             self.late_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
             self.spill_log2 = int(spill_set_log2)  # grows on the GPU (_rehash_spill_set)
             self.spill_set = torch.full((1 << self.spill_log2,), EMPTY_KEY, dtype=torch.int64,
@@ -919,11 +928,8 @@ class KeyedSessionOperator:
         GIL and no Python thread. Its results are applied when polled (_apply_spill_results)."""
         from .window_operator import CountedHostRows
 
-        if getattr(self, "_spill_slabs", None) is None:
-            self._spill_slabs = [[None, None, 0], [None, None, 0]]  # tensor, array, job id
-            self._spill_turn = 0
+        if getattr(self, "_spill_stream", None) is None:
             self._spill_stream = torch.cuda.Stream(self.device)
-            self._spill_allocs = 0
         slab = self._spill_slabs[self._spill_turn]
         self._spill_turn ^= 1
         if slab[2] > self.store.spill_completed():

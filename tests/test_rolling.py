@@ -94,15 +94,18 @@ def test_rolling_gpu_equals_cpu(gpu_device, agg, nkeys, direct):
 @pytest.mark.parametrize("n,nkeys,zipf", [(1, 10, 0.0), (777, 50, 0.0), (70_001, 10_000, 0.0),
                                           (3_000_000, 10_000, 0.0), (1 << 20, 5_000, 1.2),
                                           (1 << 18, 11_000, 0.0)])
-@pytest.mark.parametrize("filt", ["none", "count", "key", "stack", "ge"])
+@pytest.mark.parametrize("filt", ["none", "count", "key", "stack", "ge", "k1000"])
 def test_rolling_sort_free_count(gpu_device, n, nkeys, zipf, filt):
     """Sort-free COUNT (csrc/rolling_hist_hip.hip: chunk histograms, cross-chunk prefix, tile
-    ranking by lane masks) == the sort path on the GPU == the C++ twin, per record, over several
-    batches (state carried), chunk counts > 16 (two-level prefix) and a Zipf hot key."""
+    ranking by lane masks or, for rarely passing filters, the select path) == the sort path on
+    the GPU == the C++ twin, per record, over several batches (state carried), chunk counts > 16
+    (two-level prefix) and a Zipf hot key (its chunks fall back to ranking)."""
     fp = {"none": E.EMPTY, "count": E.compile_expr(E.var(E.VAR_COUNT) % 7 == 0),
           "key": E.compile_expr(E.var(E.VAR_KEY) % 3 == 1),
           # integer-mode chain (remainder, then an integer compare)
           "ge": E.compile_expr(E.var(E.VAR_COUNT) % 1000 >= 997),
+          # config 2's alert: few passing counts per chunk (the emit pass's select path)
+          "k1000": E.compile_expr(E.var(E.VAR_COUNT) % 1000 == 0),
           # not a chain program: the operator falls back to the sort path
           "stack": E.compile_expr((E.var(E.VAR_KEY) % 3 == 1) & (E.var(E.VAR_COUNT) > 2))}[filt]
     res = {}
