@@ -1,7 +1,11 @@
 // mxstream — Python binding of the pinned-slot text file reader (csrc/text_ring.h).
 #include <hip/hip_runtime_api.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/functional.h>
 #include <pybind11/stl.h>
+
+#include <mutex>
+#include <vector>
 
 #include "mxs_runtime.h"
 #include "text_ring.h"
@@ -16,7 +20,10 @@ namespace {
 class TextFileRing : public mxs::TextRingCore {
  public:
   using mxs::TextRingCore::TextRingCore;
-  ~TextFileRing() { unregister(); }
+  ~TextFileRing() {
+    close();  // the reader thread (which page-locks segments) has stopped
+    unregister();
+  }
   // 0 on success (or nothing to register), else the hipError_t.
   int register_mapping(unsigned flags) {
     if (registered_ || !map_bytes()) return 0;
@@ -25,14 +32,30 @@ class TextFileRing : public mxs::TextRingCore {
     registered_ = e == hipSuccess;
     return (int)e;
   }
+  // The mapping page-locked segment by segment by the reader thread (TextRingCore::on_segments).
+  void register_segments(int64_t seg, unsigned flags) {
+    on_segments(seg, [this, flags](intptr_t p, int64_t len) {
+      const hipError_t e = hipHostRegister(reinterpret_cast<void*>(p), (size_t)len, flags);
+      if (e == hipSuccess) {
+        std::lock_guard<std::mutex> g(seg_mu_);
+        segs_.push_back(p);
+      }
+      return (int)e;
+    });
+  }
   void unregister() {
     if (registered_) (void)hipHostUnregister(reinterpret_cast<void*>(map_base()));
     registered_ = false;
+    std::lock_guard<std::mutex> g(seg_mu_);
+    for (intptr_t p : segs_) (void)hipHostUnregister(reinterpret_cast<void*>(p));
+    segs_.clear();
   }
   bool registered() const { return registered_; }
 
  private:
   bool registered_ = false;
+  std::mutex seg_mu_;
+  std::vector<intptr_t> segs_;
 };
 
 }  // namespace
@@ -68,6 +91,9 @@ void bind_reader(py::module_& m) {
       .def_property_readonly("map_base", &TextFileRing::map_base)
       .def_property_readonly("map_bytes", &TextFileRing::map_bytes)
       .def("register_mapping", &TextFileRing::register_mapping, py::arg("flags") = 8u)
+      .def("register_segments", &TextFileRing::register_segments, py::arg("seg"),
+           py::arg("flags") = 8u)
+      .def_property_readonly("segment_bytes", &TextFileRing::segment_bytes)
       .def_property_readonly("registered", &TextFileRing::registered)
       .def("close", [](TextFileRing& r) {
         py::gil_scoped_release nogil;

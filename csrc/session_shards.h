@@ -32,7 +32,8 @@ class ShardedCore {
     bits_ = b;
     for (int i = 0; i < (1 << b); ++i) {
       sh_.emplace_back(new SessionCore(gap, lateness, agg));
-      sh_.back()->max_threads_ = 1;
+      // shards run in parallel on the pool below: each one alone stays single-threaded
+      if ((1 << b) > 1) sh_.back()->max_threads_ = 1;
     }
     if ((1 << b) > 1) {
       const unsigned hw = std::thread::hardware_concurrency();

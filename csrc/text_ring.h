@@ -24,6 +24,7 @@
 #include <cstdint>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -112,6 +113,18 @@ class TextRingCore {
   // Mapped mode: the whole file's mapping (base, bytes); (0, 0) otherwise.
   intptr_t map_base() const { return reinterpret_cast<intptr_t>(map_); }
   int64_t map_bytes() const { return (int64_t)map_len_; }
+  // Mapped mode: the reader thread hands every `seg` bytes of the mapping (page-aligned file
+  // offsets k * seg) to fn(address, bytes) -- the binding page-locks them -- before it hands out
+  // a chunk that touches them, so the page-locking runs segment by segment beside the stream
+  // instead of once for the whole file before the first chunk. fn returns 0 or an error code.
+  // Set before start().
+  void on_segments(int64_t seg, std::function<int(intptr_t, int64_t)> fn) {
+    if (seg <= 0 || seg % 4096) throw std::invalid_argument("segment size must be whole pages");
+    seg_ = seg;
+    seg_fn_ = std::move(fn);
+    seg_done_ = lo_ / seg * seg;
+  }
+  int64_t segment_bytes() const { return seg_; }
 
   void start() {
     if (!th_.joinable()) th_ = std::thread([this] { run(); });
@@ -233,6 +246,20 @@ class TextRingCore {
       const int64_t want = std::min(chunk_, hi_ - off);
       int64_t nl_read = 0;
       const char* dst;
+      if (map_ && seg_fn_) {
+        bool seg_ok = true;
+        while (seg_done_ < off + want && seg_done_ < (int64_t)map_len_) {
+          const int64_t len = std::min<int64_t>(seg_, (int64_t)map_len_ - seg_done_);
+          const int rc = seg_fn_(reinterpret_cast<intptr_t>(map_ + seg_done_), len);
+          if (rc) {
+            err = "page-locking the file mapping failed (error " + std::to_string(rc) + ")";
+            seg_ok = false;
+            break;
+          }
+          seg_done_ += seg_;
+        }
+        if (!seg_ok) break;
+      }
       if (map_) {
         dst = map_ + off;
         if (count_) count_mapped(off, want, &nl_read);
@@ -274,6 +301,8 @@ class TextRingCore {
   int64_t lo_, hi_, chunk_;
   int threads_;
   bool count_ = true;
+  int64_t seg_ = 0, seg_done_ = 0;
+  std::function<int(intptr_t, int64_t)> seg_fn_;
   std::unique_ptr<WorkerPool> pool_;
   std::vector<Slot> slots_;
   std::deque<int> free_;

@@ -223,12 +223,41 @@ _SLOT_REGISTER = __import__("os").environ.get("MXS_SLOT_REGISTER", "0") == "1"
 # "0": the pread reader into pinned slots.
 _TEXT_MMAP = __import__("os").environ.get("MXS_TEXT_MMAP", "1") != "0"
 _HIP_REGISTER_READONLY = 0x08
+_TEXT_SEG = 64 << 20  # page-locked segment of the mapped reader (bytes; raised to the chunk size)
 
 
 def _native():
     from ..ops.native import load
 
     return load()
+
+
+_LOCKABLE: list = []
+
+
+def _mapping_lockable() -> bool:
+    """Once per process: can a read-only file mapping be page-locked (hipHostRegister ReadOnly)?
+    Otherwise the device ingest keeps the pread reader."""
+    if not _LOCKABLE:
+        import mmap
+        import tempfile
+
+        ok = False
+        with tempfile.TemporaryFile() as f:
+            f.write(b"\n" * 4096)
+            f.flush()
+            mm = mmap.mmap(f.fileno(), 4096, prot=mmap.PROT_READ, flags=mmap.MAP_SHARED)
+            try:
+                import numpy as np
+
+                p = np.frombuffer(mm, dtype=np.uint8).ctypes.data  # (the view is released here)
+                if _native().gpu_host_register_flags(p, 4096, _HIP_REGISTER_READONLY) == 0:
+                    _native().gpu_host_unregister(p)
+                    ok = True
+            finally:
+                mm.close()
+        _LOCKABLE.append(ok)
+    return _LOCKABLE[0]
 
 
 _REGISTERED: list = []  # page-locked pageable buffers (kept for the process' lifetime)
@@ -304,13 +333,14 @@ class TextFileSource(Source):
         self._mapped = False
         self._slots = []
         self._nslots = _RING_SLOTS
-        if _TEXT_MMAP and self._cstream is not None:
+        if _TEXT_MMAP and self._cstream is not None and _mapping_lockable():
             ring = load().TextFileRing.mapped(self.path, self.lo + start, self.hi, _RING_SLOTS,
                                               chunk, threads)
-            if ring.register_mapping(_HIP_REGISTER_READONLY) == 0:
-                self._ring, self._mapped = ring, True
-            else:  # no page-locked mapping on this system: the pread reader
-                ring.close()
+            # page-locked by the reader thread a segment at a time (whole pages, >= a chunk:
+            # a chunk's copy splits at most once, at a segment boundary)
+            self._seg = max(_TEXT_SEG, (chunk + 4095) & ~4095)
+            ring.register_segments(self._seg, _HIP_REGISTER_READONLY)
+            self._ring, self._mapped = ring, True
         if not self._mapped:
             self._slots = _take_slots(chunk, _RING_SLOTS, self._pin)
             self._ring = load().TextFileRing(self.path, self.lo + start, self.hi,
@@ -402,10 +432,14 @@ class TextFileSource(Source):
 
             with torch.cuda.stream(self._cstream):
                 dev = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self._dev)
-                rc = _native().gpu_h2d_async(dev.data_ptr(), int(ptr), int(nbytes),
-                                             self._cstream.cuda_stream)
-                if rc:
-                    raise RuntimeError(f"text upload: hip error {rc}")
+                off = int(ptr) - self._ring.map_base
+                cut = min(int(nbytes), (off // self._seg + 1) * self._seg - off)
+                for a, b in ((0, cut), (cut, int(nbytes))):  # one copy per page-locked segment
+                    if b > a:
+                        rc = _native().gpu_h2d_async(dev.data_ptr() + a, int(ptr) + a, b - a,
+                                                     self._cstream.cuda_stream)
+                        if rc:
+                            raise RuntimeError(f"text upload: hip error {rc}")
                 ev = torch.cuda.Event()
                 ev.record(self._cstream)
             tok.uploaded(ev)

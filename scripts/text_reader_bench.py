@@ -4,6 +4,7 @@ chunk through csrc/text_ring.h, without parsing -- the config 7 reader ceiling p
   pread           parallel pread into pinned slots, one DMA per chunk (the default until r5)
   mapped          file mapping page-locked read-only once; the reader threads count each
                   chunk's newlines from the mapping (first touch of its pages), one DMA per chunk
+  mapped_seg      as mapped, the mapping page-locked segment by segment by the reader thread
   mapped_nocount  as mapped, without the host pass over the bytes (lines counted on the device)
 
 Every mode opens a fresh ring (a fresh mapping: no page-table entries yet).
@@ -36,7 +37,11 @@ def run(m, mode, path, size, chunk, threads, dev_bufs, stream):
                                      mode != "mapped_nocount")
     t_open = time.perf_counter() - t0
     t_reg = 0.0
-    if mode != "pread":
+    seg = 0
+    if mode == "mapped_seg":
+        seg = max(64 << 20, chunk)
+        ring.register_segments(seg, 8)
+    elif mode != "pread":
         r0 = time.perf_counter()
         rc = ring.register_mapping(8)
         t_reg = time.perf_counter() - r0
@@ -57,9 +62,16 @@ def run(m, mode, path, size, chunk, threads, dev_bufs, stream):
                 break
             continue
         src = ptr if ptr else slots[slot].data_ptr()
-        rc = m.gpu_h2d_async(dev_bufs[slot].data_ptr(), src, nb, stream.cuda_stream)
-        if rc:
-            raise RuntimeError(f"h2d failed: {rc}")
+        cut = nb
+        if seg:
+            off = ptr - ring.map_base
+            cut = min(nb, (off // seg + 1) * seg - off)
+        for a, b in ((0, cut), (cut, nb)):
+            if b > a:
+                rc = m.gpu_h2d_async(dev_bufs[slot].data_ptr() + a, src + a, b - a,
+                                     stream.cuda_stream)
+                if rc:
+                    raise RuntimeError(f"h2d failed: {rc}")
         ev = torch.cuda.Event()
         ev.record(stream)
         inflight.append((slot, ev))
@@ -90,7 +102,7 @@ def main():
     ap.add_argument("--chunk-mb", type=int, default=48)
     ap.add_argument("--slots", type=int, default=8)
     ap.add_argument("--threads", type=int, default=16)
-    ap.add_argument("--modes", default="pread,mapped,mapped_nocount,pread,mapped")
+    ap.add_argument("--modes", default="pread,mapped,mapped_seg,pread,mapped,mapped_seg")
     a = ap.parse_args()
     m = load()
     line = b"2019-08-28T10:00:00 www.channel0001.com 12345678\n"

@@ -99,18 +99,21 @@ def test_mapped_ring_line_longer_than_chunk(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mapped", ["1", "0"])
+@pytest.mark.parametrize("mapped", ["1", "seg", "0"])
 def test_gpu_text_source_device_batches_equal_file(tmp_path, monkeypatch, mapped):
     """TextFileSource's device ingest (ring + copy stream) hands over device batches whose bytes
-    are the file's, through the page-locked mapping (MXS_TEXT_MMAP=1) or pinned slots (0)."""
+    are the file's, through the page-locked mapping (MXS_TEXT_MMAP=1; "seg": 1 MB segments, so
+    chunks are copied in two pieces across segment boundaries) or pinned slots (0)."""
     import mxstream.runtime.sources as S
 
-    monkeypatch.setattr(S, "_TEXT_MMAP", mapped == "1")
+    monkeypatch.setattr(S, "_TEXT_MMAP", mapped != "0")
+    if mapped == "seg":
+        monkeypatch.setattr(S, "_TEXT_SEG", 1 << 20)
     path, data = _file(tmp_path, 200_000)
     src = S.TextFileSource(path, batch_size=1 << 14)
     src.columnar, src.ring, src.ring_device = True, True, "cuda"
     src.open(0, 1, None)
-    assert src._mapped == (mapped == "1")
+    assert src._mapped == (mapped != "0")
     got, lines = [], 0
     done = False
     while not done:
