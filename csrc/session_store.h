@@ -384,42 +384,42 @@ class SessionCore {
       return;
     }
     ch.seq = next_seq_++;
-    // Row blocks on the pool; an entry changes by compare-and-swap, so two runs of one key (in
-    // this chunk or an older one) always end as kMultiLoc whatever the interleaving.
+    // Tasks own disjoint key ranges of the chunk's span (every task reads the key column, a
+    // sequential 8 bytes a row, and writes only its own keys' entries): plain stores, so the
+    // random index writes overlap -- atomic read-modify-writes would serialize each miss.
     const uint32_t cur = ch.seq;
     const size_t n = ch.key.size();
-    auto block = [&](size_t lo, size_t hi) {
-      for (size_t r = lo; r < hi; ++r) {
+    const uint64_t klo = ch.kmin, kspan = ch.kmax - ch.kmin + 1;
+    auto task = [&](uint64_t a, uint64_t b) {  // keys [klo + a, klo + b)
+      for (size_t r = 0; r < n; ++r) {
         const uint64_t k = ch.key[r];
+        if (k - klo < a || k - klo >= b) continue;
         if (r && ch.key[r - 1] == k) continue;  // a run's later rows: reached from its first
-        uint64_t* e = loc_ + (k - loc_base_);
-        const uint64_t mine = ((uint64_t)cur << 32) | (uint64_t)r;
-        uint64_t old = __atomic_load_n(e, __ATOMIC_RELAXED);
-        for (;;) {
-          if (old == kMultiLoc) break;
-          uint64_t want = mine;
-          if (old != kNoLoc) {
-            const uint32_t es = (uint32_t)(old >> 32), er = (uint32_t)old;
-            const bool live = es == cur ? (er < n && ch.key[er] == k && ch.cnt[er])
-                                        : live_loc(old, k);
-            if (live) want = kMultiLoc;
+        uint64_t& e = loc_[k - loc_base_];
+        if (e == kMultiLoc) continue;
+        if (e != kNoLoc) {
+          const uint32_t es = (uint32_t)(e >> 32), er = (uint32_t)e;
+          const bool live = es == cur ? (er < n && ch.key[er] == k && ch.cnt[er]) : live_loc(e, k);
+          if (live) {
+            e = kMultiLoc;
+            continue;
           }
-          if (__atomic_compare_exchange_n(e, &old, want, false, __ATOMIC_RELAXED,
-                                          __ATOMIC_RELAXED))
-            break;
         }
+        e = ((uint64_t)cur << 32) | (uint64_t)r;
       }
     };
-    constexpr size_t kBlk = 65536;
-    const size_t nb = (n + kBlk - 1) / kBlk;
-    if (nb > 1) {
+    int T = 1;
+    if (n >= 65536) {
       if (!pool_) {
         unsigned hw = std::thread::hardware_concurrency();
         pool_.reset(new WorkerPool(std::max(0, std::min<int>(hw ? (int)hw : 1, max_threads_) - 1)));
       }
-      pool_->run((int)nb, [&](int b) { block((size_t)b * kBlk, std::min(n, (size_t)(b + 1) * kBlk)); });
+      T = std::max(1, std::min<int>(pool_->workers() + 1, (int)(n / 32768)));
+    }
+    if (T == 1) {
+      task(0, kspan);
     } else {
-      block(0, n);
+      pool_->run(T, [&](int t) { task(kspan * (uint64_t)t / T, kspan * (uint64_t)(t + 1) / T); });
     }
   }
   ~SessionCore() { drop_index(); }
@@ -1089,14 +1089,17 @@ class SessionCore {
     ++ixs_.indexed;
     for (size_t b = 0; b < nb; ++b) ix_kept_[b + 1] += ix_kept_[b];
     size(ix_kept_[nb]);
-    std::atomic<size_t> gone{0};
-    // (a chunk's live count is shared between blocks: atomic)
+    // per block and chunk: rows taken (a shared atomic per chunk ping-pongs between cores)
+    const size_t nch = cold_.size();
+    ix_gone_.assign(nb * nch, 0);
     blocks([&](size_t b) {
-      size_t o = ix_kept_[b], g = 0;
+      size_t o = ix_kept_[b];
+      uint32_t* gb = ix_gone_.data() + b * nch;
       for (size_t i = b * kBlk, e = std::min(nw, i + kBlk); i < e; ++i) {
         const uint64_t h = ix_hit_[i];
         if (h == kNoHit) continue;
-        ColdChunk& ch = cold_[(size_t)(h >> 32)];
+        const size_t pos = (size_t)(h >> 32);
+        ColdChunk& ch = cold_[pos];
         const uint32_t r0 = (uint32_t)h, r1 = r0 + ix_run_[i];
         uint32_t nk = 0;
         int64_t last = INT64_MIN;
@@ -1113,13 +1116,16 @@ class SessionCore {
           ch.cnt[r] = 0;
           ++taken;
         }
-        __atomic_fetch_sub(&ch.live, taken, __ATOMIC_RELAXED);
+        gb[pos] += (uint32_t)taken;
         loc_[want[i] - base] = kNoLoc;
-        g += taken;
       }
-      gone.fetch_add(g, std::memory_order_relaxed);
     });
-    cold_rows_ -= gone.load();
+    for (size_t b = 0; b < nb; ++b)
+      for (size_t c = 0; c < nch; ++c) {
+        const uint32_t g = ix_gone_[b * nch + c];
+        cold_[c].live -= g;
+        cold_rows_ -= g;
+      }
     return true;
   }
 
@@ -1314,7 +1320,7 @@ class SessionCore {
   uint32_t next_seq_ = 1, seq_lo_ = 1;
   std::vector<int32_t> seq_pos_;  // chunk seq - seq_lo_ -> position in cold_ (-1: gone)
   std::vector<uint64_t> ix_hit_, ix_want_;  // take_indexed scratch (kept between calls)
-  std::vector<uint32_t> ix_run_;
+  std::vector<uint32_t> ix_run_, ix_gone_;
   IndexStats ixs_;
   std::vector<size_t> ix_kept_;
   std::vector<uint64_t> pending_released_;

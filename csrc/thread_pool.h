@@ -30,6 +30,7 @@ class WorkerPool {
     cv_.notify_all();
     for (auto& t : th_) t.join();
   }
+  int workers() const { return (int)th_.size(); }
   void run(int n, const std::function<void(int)>& f) {
     if (n <= 0) return;
     if (th_.empty() || n == 1) {
