@@ -7,7 +7,8 @@
 # `timeout -k 10 seconds`, output in gpurun_out/TAG_name.log; the first failing step ends the
 # run (a fault, abort or time limit leaves the GPU alone after it). The last line of each log
 # is echoed so the gpurun tail carries the results. A command that starts with "prof:" runs
-# under `rocprofv3 --kernel-trace --stats` from /tmp, output in gpurun_out/TAG_name/.
+# under `rocprofv3 --kernel-trace --stats` from /tmp, output in gpurun_out/TAG_name/ ("pmem:"
+# adds --memory-copy-trace).
 #
 # Shortcuts for STEP: "tests" (all GPU tests), "bench" (bench.py 24/6),
 # "cfgN" (bench_configs --config N, default steps), "profN" (kernel profile of config N).
@@ -36,10 +37,13 @@ for raw in "$@"; do
   cmd=${rest#*|}
   log="$ROOT/gpurun_out/${TAG}_${name}.log"
   t0=$(date +%s)
-  if [[ $cmd == prof:* ]]; then
+  if [[ $cmd == prof:* || $cmd == pmem:* ]]; then
+    trace="--kernel-trace --stats"
+    [[ $cmd == pmem:* ]] && trace="--kernel-trace --memory-copy-trace --stats"
     cmd=${cmd#prof:}
+    cmd=${cmd#pmem:}
     (cd /tmp && export TMPDIR=/tmp &&
-      timeout -k 10 "$secs" rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/${TAG}_${name}" \
+      timeout -k 10 "$secs" rocprofv3 $trace -d "$ROOT/gpurun_out/${TAG}_${name}" \
         -o prof -- $cmd > "$log" 2>&1)
   else
     timeout -k 10 "$secs" bash -c "$cmd" > "$log" 2>&1
