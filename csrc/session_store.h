@@ -232,7 +232,7 @@ class SessionCore {
     ColdPlan p;
     insert_hot(K, S, E, A, C, F, n, cold, p);
     if (cold) {
-      build_cold(K, S, E, A, C, n, p);
+      build_cold_parallel(K, S, E, A, C, n, p);
       index_cold(p);
       publish_cold(p);
     }
@@ -304,6 +304,46 @@ class SessionCore {
       m_[key].push_back(Session{S[i], E[i], (uint64_t)A[i], (uint32_t)C[i], (uint32_t)F[i]});
       mark_hot(key);
       schedule(key);
+    }
+  }
+  // build_cold with the common all-cold copy split into row blocks on the store's pool (the
+  // spill worker's build phase: ~12 MB of column copies per eviction, mostly first-touch page
+  // faults of the chunk's fresh columns). Reads the store's pool only: outside the lock.
+  void build_cold_parallel(const int64_t* K, const int64_t* S, const int64_t* E, const int64_t* A,
+                           const int64_t* C, int64_t n, ColdPlan& p) {
+    constexpr int64_t kBlk = 65536;
+    if (p.nc != n || n < 2 * kBlk) return build_cold(K, S, E, A, C, n, p);
+    if (!pool_) {
+      unsigned hw = std::thread::hardware_concurrency();
+      pool_.reset(new WorkerPool(std::max(0, std::min<int>(hw ? (int)hw : 1, max_threads_) - 1)));
+    }
+    ColdChunk& ch = p.ch;
+    ch.key.resize(n);
+    ch.start.resize(n);
+    ch.end.resize(n);
+    ch.acc.resize(n);
+    ch.cnt.resize(n);
+    const int nb = (int)((n + kBlk - 1) / kBlk);
+    std::vector<uint64_t> lo((size_t)nb, ~0ull), hi((size_t)nb, 0);
+    pool_->run(nb, [&](int b) {
+      const int64_t a = (int64_t)b * kBlk, m = std::min(n, a + kBlk) - a;
+      std::memcpy(ch.key.data() + a, K + a, (size_t)m * 8);
+      std::memcpy(ch.start.data() + a, S + a, (size_t)m * 8);
+      std::memcpy(ch.end.data() + a, E + a, (size_t)m * 8);
+      std::memcpy(ch.acc.data() + a, A + a, (size_t)m * 8);
+      uint64_t l = ~0ull, h = 0;
+      for (int64_t i = a; i < a + m; ++i) {
+        ch.cnt[i] = (uint32_t)C[i];
+        const uint64_t k = (uint64_t)K[i];
+        l = k < l ? k : l;
+        h = k > h ? k : h;
+      }
+      lo[(size_t)b] = l;
+      hi[(size_t)b] = h;
+    });
+    for (int b = 0; b < nb; ++b) {
+      ch.kmin = std::min(ch.kmin, lo[(size_t)b]);
+      ch.kmax = std::max(ch.kmax, hi[(size_t)b]);
     }
   }
   // The classified cold rows into p.ch (touches no store state: runs outside the store lock).

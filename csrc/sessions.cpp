@@ -455,7 +455,7 @@ class SessionStore {
         }
         dcv_.notify_all();
         const auto t2 = clk::now();
-        if (one && nr) sess::SessionCore::build_cold(col[0], col[1], col[2], col[3], col[4], nr, plan);
+        if (one && nr) one->build_cold_parallel(col[0], col[1], col[2], col[3], col[4], nr, plan);
         const auto t2b = clk::now();
         // The cold-row index entries of the new chunk, still outside the lock: every other user
         // of the index (extract, promote, expiry) joins this worker first.

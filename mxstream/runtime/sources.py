@@ -321,6 +321,7 @@ class TextFileSource(Source):
         from ..ops.native import load
 
         chunk = max(1 << 20, self.batch * 48)
+        self._dcap = (chunk + (2 << 20) - 1) & ~((2 << 20) - 1)  # device chunk buffers
         self._pin = torch.cuda.is_available()
         threads = min(16, max(1, __import__("os").cpu_count() or 1))
         self._cstream = None
@@ -411,7 +412,15 @@ class TextFileSource(Source):
                 t.ready(wait=True)
             if self._pre is not None:
                 self._pre[0].token.ready(wait=True)
-            self._ring.close()
+            if self._mapped:
+                # every copy out of the mapping has completed: its segments are unlocked and
+                # unmapped on a helper thread (~6 ms for 768 MB, no GIL held) after the job
+                import threading
+
+                threading.Thread(target=self._ring.close, name="mxs-ring-close",
+                                 daemon=True).start()
+            else:
+                self._ring.close()
             self._ring = None
             _give_slots(self._slots, self._pin)
             self._slots = []
@@ -431,7 +440,9 @@ class TextFileSource(Source):
             import torch
 
             with torch.cuda.stream(self._cstream):
-                dev = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self._dev)
+                # one allocation size for every chunk: the caching allocator hands the freed
+                # buffers back instead of going to the driver per chunk size
+                dev = torch.empty(self._dcap, dtype=torch.uint8, device=self._dev)
                 off = int(ptr) - self._ring.map_base
                 cut = min(int(nbytes), (off // self._seg + 1) * self._seg - off)
                 for a, b in ((0, cut), (cut, int(nbytes))):  # one copy per page-locked segment
@@ -471,7 +482,8 @@ class TextFileSource(Source):
                         raise RuntimeError(f"text upload: hip error {rc}")
                     dev = dev[:nbytes]
                 else:
-                    dev = tb.data.to(self._dev, non_blocking=True)
+                    dev = torch.empty(self._dcap, dtype=torch.uint8, device=self._dev)[:nbytes]
+                    dev.copy_(tb.data, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self._cstream)
             tok.uploaded(ev)
