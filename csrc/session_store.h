@@ -448,13 +448,17 @@ class SessionCore {
         e = ((uint64_t)cur << 32) | (uint64_t)r;
       }
     };
+    // One task: on the box a 300K-row eviction indexes in ~1.0 ms on one core and ~1.5 ms on
+    // 8 or 16 key-range tasks (each re-reads the key column; scripts/native/store_bench.cpp,
+    // profiles/r5_store_bench.json). The range split stays for much larger evictions.
+    constexpr size_t kRowsPerTask = (size_t)1 << 21;
     int T = 1;
-    if (n >= 65536) {
+    if (n >= 2 * kRowsPerTask) {
       if (!pool_) {
         unsigned hw = std::thread::hardware_concurrency();
         pool_.reset(new WorkerPool(std::max(0, std::min<int>(hw ? (int)hw : 1, max_threads_) - 1)));
       }
-      T = std::max(1, std::min<int>(pool_->workers() + 1, (int)(n / 32768)));
+      T = std::max(1, std::min<int>(pool_->workers() + 1, (int)(n / kRowsPerTask)));
     }
     if (T == 1) {
       task(0, kspan);
