@@ -424,47 +424,54 @@ class SessionCore {
       return;
     }
     ch.seq = next_seq_++;
-    // Tasks own disjoint key ranges of the chunk's span (every task reads the key column, a
-    // sequential 8 bytes a row, and writes only its own keys' entries): plain stores, so the
-    // random index writes overlap -- atomic read-modify-writes would serialize each miss.
+    // Row blocks on the pool, two passes of relaxed (plain) stores -- atomic read-modify-writes
+    // serialize every cache miss, key-range tasks re-read the key column per task:
+    //  1. every run's first row stores its entry, or kMultiLoc over a live entry of another row;
+    //  2. every run's first row reads its entry back: another row's entry there means a second
+    //     run of the key in this chunk (its writer lost the race) -> kMultiLoc.
     const uint32_t cur = ch.seq;
     const size_t n = ch.key.size();
-    const uint64_t klo = ch.kmin, kspan = ch.kmax - ch.kmin + 1;
-    auto task = [&](uint64_t a, uint64_t b) {  // keys [klo + a, klo + b)
-      for (size_t r = 0; r < n; ++r) {
+    auto entry = [&](uint64_t k) { return loc_ + (k - loc_base_); };
+    auto first_of_run = [&](size_t r) { return r == 0 || ch.key[r - 1] != ch.key[r]; };
+    auto pass1 = [&](size_t lo, size_t hi) {
+      for (size_t r = lo; r < hi; ++r) {
+        if (!first_of_run(r)) continue;  // a run's later rows: reached from its first
         const uint64_t k = ch.key[r];
-        if (k - klo < a || k - klo >= b) continue;
-        if (r && ch.key[r - 1] == k) continue;  // a run's later rows: reached from its first
-        uint64_t& e = loc_[k - loc_base_];
-        if (e == kMultiLoc) continue;
-        if (e != kNoLoc) {
-          const uint32_t es = (uint32_t)(e >> 32), er = (uint32_t)e;
-          const bool live = es == cur ? (er < n && ch.key[er] == k && ch.cnt[er]) : live_loc(e, k);
-          if (live) {
-            e = kMultiLoc;
-            continue;
-          }
+        uint64_t* e = entry(k);
+        const uint64_t old = __atomic_load_n(e, __ATOMIC_RELAXED);
+        if (old == kMultiLoc) continue;
+        uint64_t want = ((uint64_t)cur << 32) | (uint64_t)r;
+        if (old != kNoLoc) {
+          const uint32_t es = (uint32_t)(old >> 32), er = (uint32_t)old;
+          const bool live = es == cur ? (er < n && er != r && ch.key[er] == k && ch.cnt[er])
+                                      : live_loc(old, k);
+          if (live) want = kMultiLoc;
         }
-        e = ((uint64_t)cur << 32) | (uint64_t)r;
+        __atomic_store_n(e, want, __ATOMIC_RELAXED);
       }
     };
-    // One task: on the box a 300K-row eviction indexes in ~1.0 ms on one core and ~1.5 ms on
-    // 8 or 16 key-range tasks (each re-reads the key column; scripts/native/store_bench.cpp,
-    // profiles/r5_store_bench.json). The range split stays for much larger evictions.
-    constexpr size_t kRowsPerTask = (size_t)1 << 21;
-    int T = 1;
-    if (n >= 2 * kRowsPerTask) {
-      if (!pool_) {
-        unsigned hw = std::thread::hardware_concurrency();
-        pool_.reset(new WorkerPool(std::max(0, std::min<int>(hw ? (int)hw : 1, max_threads_) - 1)));
+    auto pass2 = [&](size_t lo, size_t hi) {
+      for (size_t r = lo; r < hi; ++r) {
+        if (!first_of_run(r)) continue;
+        uint64_t* e = entry(ch.key[r]);
+        const uint64_t v = __atomic_load_n(e, __ATOMIC_RELAXED);
+        if (v != kMultiLoc && v != (((uint64_t)cur << 32) | (uint64_t)r))
+          __atomic_store_n(e, kMultiLoc, __ATOMIC_RELAXED);
       }
-      T = std::max(1, std::min<int>(pool_->workers() + 1, (int)(n / kRowsPerTask)));
+    };
+    constexpr size_t kBlk = 32768;
+    const int nb = (int)((n + kBlk - 1) / kBlk);
+    if (nb <= 1) {
+      pass1(0, n);
+      pass2(0, n);
+      return;
     }
-    if (T == 1) {
-      task(0, kspan);
-    } else {
-      pool_->run(T, [&](int t) { task(kspan * (uint64_t)t / T, kspan * (uint64_t)(t + 1) / T); });
+    if (!pool_) {
+      unsigned hw = std::thread::hardware_concurrency();
+      pool_.reset(new WorkerPool(std::max(0, std::min<int>(hw ? (int)hw : 1, max_threads_) - 1)));
     }
+    pool_->run(nb, [&](int b) { pass1((size_t)b * kBlk, std::min(n, (size_t)(b + 1) * kBlk)); });
+    pool_->run(nb, [&](int b) { pass2((size_t)b * kBlk, std::min(n, (size_t)(b + 1) * kBlk)); });
   }
   ~SessionCore() { drop_index(); }
 

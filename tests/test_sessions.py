@@ -339,6 +339,34 @@ def test_store_extract_rows_into_multi_and_hot_keys():
     _extract_both(stores[0], stores[1], w2, 0)
 
 
+def test_store_index_duplicate_keys_in_one_chunk():
+    """The cold-row index of a large chunk is built by parallel row blocks: a key whose rows sit
+    in two blocks of one chunk (not adjacent) must end as a multi-place key (the extract scans
+    and returns both sessions); an adjacent run is one entry; keys re-evicted while an older
+    row lives are multi too."""
+    from mxstream.ops.native import load
+
+    st = load().SessionStore(100, 10**9, K.AGG_SUM_I64)
+    n = 200_000
+    keys = np.arange(1000, 1000 + n, dtype=np.int64)
+    keys[150_000] = 5  # key 5: rows 10 and 150_000 (different row blocks)
+    keys[10] = 5
+    keys[20], keys[21] = 6, 6  # key 6: an adjacent run
+    start = np.arange(n, dtype=np.int64) * 1000
+    one = np.ones(n, np.int64)
+    st.insert(keys, start, start + 100, keys, one, one, True)
+    ex = st.extract(np.array([5, 6, 1030], np.int64), 0, 4)
+    got = sorted(zip(ex["key"].tolist(), ex["start"].tolist()))
+    assert got == [(5, 10_000), (5, 150_000_000), (6, 20_000), (6, 21_000), (1030, 30_000)]
+    assert st.index_stats()["multi_aborts"] >= 1
+    # an older live row + a new chunk's row of the same key: multi
+    k = np.array([2000, 2001], np.int64)
+    st.insert(k, np.array([5, 6], np.int64) * 10**7, np.array([5, 6], np.int64) * 10**7 + 100, k,
+              np.ones(2, np.int64), np.ones(2, np.int64), True)
+    ex = st.extract(np.array([2000], np.int64), 0, 4)
+    assert sorted(ex["start"].tolist()) == [1000 * 1000, 5 * 10**7]
+
+
 @pytest.mark.parametrize("shards", [2, 8])
 def test_sharded_store_equals_one_store(shards):
     """Key shards worked by the pool (csrc/session_shards.h) give the single store's results:
