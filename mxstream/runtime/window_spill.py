@@ -25,6 +25,10 @@ from ..ops import expr as E
 from ..ops import kernels as K
 
 _F64 = (K.AGG_SUM_F64, K.AGG_AVG_F64, K.AGG_MIN_F64, K.AGG_MAX_F64)
+# Reserve the next, larger export slab on a background thread ("1"; off by default: the
+# background page-locking slowed the exports beside it 7x on the box, config 4-spill 1.43 G vs
+# 1.80 G without it, profiles/r5_c4s_reserve_ab.md).
+_PIN_RESERVE = __import__("os").environ.get("MXS_PIN_RESERVE", "0") == "1"
 _MIN = (K.AGG_MIN_I64, K.AGG_MIN_F64)
 _MAX = (K.AGG_MAX_I64, K.AGG_MAX_F64)
 
@@ -163,13 +167,14 @@ class HostWindowTier:
         if bound == 0:
             return None
         if torch.device(device).type == "cuda":
-            # Slab for 1.5x the tier's rows: the tier grows between firings, and every larger
-            # pinned slab is a fresh page-locked allocation (~12 ms at 256 MB on the box).
-            bound = bound * 3 // 2
+            # Slab for 3x the tier's rows: the tier grows between firings, and every larger
+            # pinned slab is a fresh page-locked allocation (~12 ms at 256 MB, ~34 ms at 1 GB on
+            # the box) -- the headroom moves the growth into the warm-up.
+            bound = bound * 3
             a8 = (bound * 8 + 255) & ~255
             need = 2 * a8 + bound * 4 + 256
             t, arr = pool.take(need)
-            if t.numel() < 2 * need and hasattr(pool, "reserve_async"):
+            if _PIN_RESERVE and t.numel() < 2 * need and hasattr(pool, "reserve_async"):
                 pool.reserve_async(2 * need)  # the tier grows: the next slab, off the step
             base = t.data_ptr()
             n = int(self._t.export_rows(int(p0), int(p1), base, base + a8, base + 2 * a8, bound))
