@@ -179,6 +179,22 @@ class TextRingCore {
     int64_t cap;
   };
 
+  void touch_pages(const char* p, int64_t len) {
+    const int T = (int)std::min<int64_t>(threads_, std::max<int64_t>(1, len >> 22));
+    auto piece = [&](int t) {
+      const int64_t a = (len * t / T) & ~(int64_t)4095, b = len * (t + 1) / T;
+      unsigned s = 0;
+      for (int64_t o = a; o < b; o += 4096) s += (unsigned char)((volatile const char*)p)[o];
+      touched_.fetch_add(s, std::memory_order_relaxed);  // keeps the reads
+    };
+    if (T == 1 || !pool_) {
+      for (int t = 0; t < T; ++t) piece(t);
+    } else {
+      pool_->run(T, piece);
+    }
+  }
+  std::atomic<unsigned> touched_{0};
+
   // Mapped mode: the newlines of [off, off + len) counted from the mapping by the parallel
   // readers (the first touch of each page happens here, off the consumer's thread).
   void count_mapped(int64_t off, int64_t len, int64_t* newlines) {
@@ -250,6 +266,10 @@ class TextRingCore {
         bool seg_ok = true;
         while (seg_done_ < off + want && seg_done_ < (int64_t)map_len_) {
           const int64_t len = std::min<int64_t>(seg_, (int64_t)map_len_ - seg_done_);
+          // Fault the segment's pages into the page table first (parallel page-stride reads):
+          // page-locking resident pages takes microseconds, while page-locking absent ones
+          // faults them in under the runtime's lock, stalling every HIP call of the consumer.
+          touch_pages(map_ + seg_done_, len);
           const int rc = seg_fn_(reinterpret_cast<intptr_t>(map_ + seg_done_), len);
           if (rc) {
             err = "page-locking the file mapping failed (error " + std::to_string(rc) + ")";

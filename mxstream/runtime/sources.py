@@ -218,10 +218,13 @@ _H2D_BLOCKS = int(__import__("os").environ.get("MXS_H2D_BLOCKS", "512"))
 _RING_SLOTS = max(3, int(__import__("os").environ.get("MXS_RING_SLOTS", "8")))
 # Slots are page-locked pageable buffers (hipHostRegister) instead of pinned allocations.
 _SLOT_REGISTER = __import__("os").environ.get("MXS_SLOT_REGISTER", "0") == "1"
-# Device ingest reads the file through its mapping (csrc/text_ring.h mapped mode): the mapping is
-# page-locked read-only once and every chunk goes page cache -> HBM in one DMA, no host memcpy.
-# "0": the pread reader into pinned slots.
-_TEXT_MMAP = __import__("os").environ.get("MXS_TEXT_MMAP", "1") != "0"
+# "1": device ingest reads the file through its mapping (csrc/text_ring.h mapped mode): the
+# mapping is page-locked read-only segment by segment and every chunk goes page cache -> HBM in
+# one DMA, no host memcpy. Off by default: page-locking page-cache pages the first time costs
+# more than copying them (7.5 GB/s on the box, against 26 GB/s for the parallel pread into pinned
+# slots; 39-56 GB/s once the pages were locked before), so it only pays for a file read again
+# and again (profiles/r5_text_reader.md).
+_TEXT_MMAP = __import__("os").environ.get("MXS_TEXT_MMAP", "0") == "1"
 _HIP_REGISTER_READONLY = 0x08
 _TEXT_SEG = 64 << 20  # page-locked segment of the mapped reader (bytes; raised to the chunk size)
 
