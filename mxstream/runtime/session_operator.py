@@ -348,7 +348,10 @@ class KeyedSessionOperator:
                 self.red[2:3].fill_(I64_MAX)
             self.comm.allreduce_min_(self.red[:8])
             if self.world > 1:
-                self.comm.all_to_all(self.recv, self.send)
+                # the per-rank chunks are nsub * bucket_cap records of rec_w words: the prefix of
+                # the buffers (sized for 24-byte records) -- 16-byte steps send 2/3 of it
+                words = self.nbuckets * self.bucket_cap * self.rec_w
+                self.comm.all_to_all(self.recv[:words], self.send[:words])
                 self.comm.all_to_all(self.recv_counts, self.cursor)
             folded = None
             if spec:
