@@ -177,16 +177,21 @@ class ShardedCore {
     return t;
   }
   // The promote path's extract as promote rows (SessionCore::extract_rows_into).
-  std::pair<int64_t, int64_t> extract_rows_into(const int64_t* keys, int64_t n, int64_t wm,
-                                                int64_t max_sess, int64_t gap, int64_t* rows,
-                                                int64_t cap, int64_t* moved_out,
-                                                int64_t moved_cap) {
+  std::tuple<int64_t, int64_t, int64_t> extract_rows_into(const int64_t* keys, int64_t n,
+                                                          int64_t wm, int64_t max_sess,
+                                                          int64_t gap, int64_t* rows, int64_t cap,
+                                                          int64_t* moved_out,
+                                                          int64_t moved_cap) {
     if (shards() == 1)
       return sh_[0]->extract_rows_into(keys, n, wm, max_sess, gap, rows, cap, moved_out,
                                        moved_cap);
+    std::vector<uint64_t> want, bits;
+    SessionCore::sort_unique_keys(keys, n, want, bits);
     std::vector<int64_t> moved;
-    const Columns c = extract(keys, n, wm, max_sess, &moved);
-    return SessionCore::promote_rows(c, moved, gap, rows, cap, moved_out, moved_cap);
+    const Columns c = extract((const int64_t*)want.data(), (int64_t)want.size(), wm, max_sess,
+                              &moved);
+    const auto r = SessionCore::promote_rows(c, moved, gap, rows, cap, moved_out, moved_cap);
+    return {r.first, r.second, (int64_t)want.size()};
   }
   void fire(int64_t wm, const ExprProg& mp, const ExprProg& fp, SessionCore::FireOut& o,
             bool expire_cold = true) {

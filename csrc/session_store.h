@@ -13,6 +13,7 @@
 #include <sys/mman.h>
 #include <stdexcept>
 #include <thread>
+#include <tuple>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
@@ -734,21 +735,53 @@ class SessionCore {
   // key, sessions of the key}; rows of a key are adjacent, position 0 first. `moved` receives
   // the keys that left the store. Returns {rows, moved}.
   static constexpr int kPromoteRow = 8;
-  std::pair<int64_t, int64_t> extract_rows_into(const int64_t* keys, int64_t n, int64_t wm,
-                                                int64_t max_sess, int64_t gap, int64_t* rows,
-                                                int64_t cap, int64_t* moved_out,
-                                                int64_t moved_cap) {
-    // No hot sessions among the wanted keys and one cold row per key (the revisit shape): the
-    // rows go from the chunks straight into `rows`, no intermediate columns.
-    if (max_sess >= 1 && index_usable() && n > 0) {
-      std::vector<uint64_t>& want = ix_want_;
-      want.assign((const uint64_t*)keys, (const uint64_t*)keys + n);
-      bool sorted = true;
-      for (int64_t i = 1; i < n && sorted; ++i) sorted = want[i - 1] < want[i];
-      if (!sorted) {
-        std::sort(want.begin(), want.end());
-        want.erase(std::unique(want.begin(), want.end()), want.end());
+  // The keys ascending without duplicates: a copy when they already are, a bitmap over their
+  // span for dense ids (the promote path passes a step's diverted record keys as they come,
+  // ~10^5 with repeats), a sort otherwise.
+  static void sort_unique_keys(const int64_t* keys, int64_t n, std::vector<uint64_t>& out,
+                               std::vector<uint64_t>& bits) {
+    const uint64_t* k = (const uint64_t*)keys;
+    out.clear();
+    if (n <= 0) return;
+    bool sorted = true;
+    uint64_t lo = k[0], hi = k[0];
+    for (int64_t i = 1; i < n; ++i) {
+      sorted = sorted && k[i - 1] < k[i];
+      lo = k[i] < lo ? k[i] : lo;
+      hi = k[i] > hi ? k[i] : hi;
+    }
+    if (sorted) {
+      out.assign(k, k + n);
+      return;
+    }
+    const uint64_t span = hi - lo + 1;
+    if (span != 0 && span <= ((uint64_t)1 << 28) && span / 64 <= (uint64_t)n * 4) {
+      bits.assign((size_t)((span + 63) / 64), 0);
+      for (int64_t i = 0; i < n; ++i) {
+        const uint64_t o = k[i] - lo;
+        bits[o >> 6] |= 1ull << (o & 63);
       }
+      for (size_t w = 0; w < bits.size(); ++w)
+        for (uint64_t b = bits[w]; b; b &= b - 1)
+          out.push_back(lo + (w << 6) + (uint64_t)__builtin_ctzll(b));
+      return;
+    }
+    out.assign(k, k + n);
+    std::sort(out.begin(), out.end());
+    out.erase(std::unique(out.begin(), out.end()), out.end());
+  }
+  // Returns {rows, moved keys, distinct wanted keys}; `keys` may repeat and come in any order.
+  std::tuple<int64_t, int64_t, int64_t> extract_rows_into(const int64_t* keys, int64_t n,
+                                                          int64_t wm, int64_t max_sess,
+                                                          int64_t gap, int64_t* rows, int64_t cap,
+                                                          int64_t* moved_out,
+                                                          int64_t moved_cap) {
+    std::vector<uint64_t>& want = ix_want_;
+    sort_unique_keys(keys, n, want, ix_bits_);
+    const int64_t nu = (int64_t)want.size();
+    // No hot sessions among the wanted keys and at most max_sess cold rows per key in one
+    // place (the revisit shape): the rows go from the chunks straight into `rows`.
+    if (max_sess >= 1 && index_usable() && nu > 0) {
       if ((int64_t)want.size() > moved_cap)
         throw std::length_error("extract_rows_into: moved capacity");
       int64_t nk = 0;
@@ -772,12 +805,14 @@ class SessionCore {
           });
       if (ok) {
         std::memcpy(moved_out, want.data(), want.size() * sizeof(int64_t));
-        return {nk, (int64_t)want.size()};
+        return {nk, nu, nu};
       }
     }
     std::vector<int64_t> moved;
-    const Columns c = extract(keys, n, wm, max_sess, &moved);
-    return promote_rows(c, moved, gap, rows, cap, moved_out, moved_cap);
+    const std::vector<uint64_t> uniq(want);  // (extract reuses the scratch)
+    const Columns c = extract((const int64_t*)uniq.data(), nu, wm, max_sess, &moved);
+    const auto r = promote_rows(c, moved, gap, rows, cap, moved_out, moved_cap);
+    return {r.first, r.second, nu};
   }
   // extract()'s output (keys grouped, ascending) as promote rows + the moved keys.
   static std::pair<int64_t, int64_t> promote_rows(const Columns& c,
@@ -1370,7 +1405,7 @@ class SessionCore {
   bool loc_off_ = false;
   uint32_t next_seq_ = 1, seq_lo_ = 1;
   std::vector<int32_t> seq_pos_;  // chunk seq - seq_lo_ -> position in cold_ (-1: gone)
-  std::vector<uint64_t> ix_hit_, ix_want_;  // take_indexed scratch (kept between calls)
+  std::vector<uint64_t> ix_hit_, ix_want_, ix_bits_;  // take_indexed scratch (kept between calls)
   std::vector<uint32_t> ix_run_, ix_gone_;
   IndexStats ixs_;
   std::vector<size_t> ix_kept_;

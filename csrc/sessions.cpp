@@ -183,11 +183,11 @@ class SessionStore {
   }
   // The promote path's extract straight into caller memory (pinned, reused): promote rows of
   // 8 int64 (csrc/session_store.h extract_rows_into) at `rows` (cap rows) and the keys that left
-  // the store at `moved` (moved_cap). Returns (rows, moved).
-  std::pair<int64_t, int64_t> extract_rows_into_np(const I64Array& keys, int64_t wm,
-                                                   int64_t max_sess, int64_t gap, intptr_t rows,
-                                                   int64_t cap, intptr_t moved,
-                                                   int64_t moved_cap) {
+  // the store at `moved` (moved_cap); `keys` may repeat. Returns (rows, moved, distinct keys).
+  std::tuple<int64_t, int64_t, int64_t> extract_rows_into_np(const I64Array& keys, int64_t wm,
+                                                             int64_t max_sess, int64_t gap,
+                                                             intptr_t rows, int64_t cap,
+                                                             intptr_t moved, int64_t moved_cap) {
     py::gil_scoped_release nogil;
     join_all();
     std::lock_guard<std::mutex> g(mu_);
@@ -196,7 +196,7 @@ class SessionStore {
                                         reinterpret_cast<int64_t*>(moved), moved_cap);
     // the promote kernel writes record `position` of a slot: never past the slot's kSess
     const int64_t* w = reinterpret_cast<const int64_t*>(rows);
-    for (int64_t i = 0; i < r.first; ++i)
+    for (int64_t i = 0; i < std::get<0>(r); ++i)
       if (w[i * 8 + 7] > max_sess || w[i * 8 + 6] >= w[i * 8 + 7])
         throw std::logic_error("extract_rows_into: session position out of range");
     return r;

@@ -648,11 +648,20 @@ class KeyedSessionOperator:
             dk, dt, dv = (x.clone(memory_format=torch.contiguous_format)
                           for x in self._diverted(n_host, tbase))
             dev = self.device
-            uk = torch.unique(dk)
-            ukh = uk.cpu().numpy()
             if _PROMOTE_ROWS:
-                n_moved = self._promote_rows(uk, ukh, wm)
+                # the diverted keys as they are (repeats included): the store dedups them (a
+                # bitmap over dense ids) -- no device unique and no second round trip
+                with self._phase("promote.keys"):
+                    if getattr(self, "_pk_host", None) is None or self._pk_host.numel() < n_host:
+                        self._pk_host = torch.empty(max(1024, 1 << (n_host - 1).bit_length()),
+                                                    dtype=torch.int64, pin_memory=True)
+                    hk = self._pk_host[:n_host]
+                    hk.copy_(dk, non_blocking=True)
+                    torch.cuda.current_stream(dev).synchronize()
+                n_moved = self._promote_rows(dk, hk.numpy(), wm)
             else:
+                with self._phase("promote.unique"):
+                    ukh = torch.unique(dk).cpu().numpy()
                 n_moved = self._promote_packed(ukh, wm)
             self.metrics.promoted_keys += n_moved
             # Re-partition the diverted records (local sub-tables only) and fold them.
@@ -660,6 +669,7 @@ class KeyedSessionOperator:
             # same size on every rank, so they are never regrown locally).
             per = n_host / self.nsub
             cap = (int(per * 1.5 + 6 * math.sqrt(max(per, 1.0)) + 64) + 8 * 16 + 7) & ~7
+            t_part = time.perf_counter()
             while True:
                 words = self.nsub * cap * K.REC_WORDS
                 if getattr(self, "_rf_send", None) is None or self._rf_send.numel() < words:
@@ -675,13 +685,16 @@ class KeyedSessionOperator:
                 if int(self._rf_cursor.max()) <= cap:
                     break
                 cap *= 2  # a bucket overflowed (skewed keys): larger buckets, partition again
-            h, total = self._fold_recs(self._rf_send, self._rf_cursor, 1, tbase, wm, tbits, cap)
+            self.phase_s["promote.partition"] += time.perf_counter() - t_part
+            with self._phase("promote.fold"):
+                h, total = self._fold_recs(self._rf_send, self._rf_cursor, 1, tbase, wm, tbits,
+                                           cap)
             self.metrics.records_promoted += n_host - h[2]
             late = h[6] if total else 0
             late += self._overflow_runs(h, wm)
             return h[2], late
 
-    def _promote_rows(self, uk, ukh, wm: int) -> int:
+    def _promote_rows(self, dk, hk, wm: int) -> int:
         """The promote path's host side in one C++ call and one copy: the store writes the
         revisited keys' sessions as promote rows {key, start, end, acc, cnt | flags << 32, last
         activity, position, sessions of the key} straight into a reused pinned buffer
@@ -689,9 +702,10 @@ class KeyedSessionOperator:
         instead of a scan of every cold row; the general extract otherwise), plus the keys that
         left the store. ONE copy takes the rows to HBM and session_promote_rows (two launches:
         slot insert + record 0, then further positions) writes the slots. The keys leave the
-        device spill set from the device copy of the unique keys when all of them moved (no
-        upload). Returns the number of keys that left the store."""
-        n = len(ukh)
+        device spill set from the device copy of the diverted keys when all of them moved (no
+        upload; repeats are harmless). dk / hk: the diverted keys on the device / in pinned
+        memory. Returns the number of keys that left the store."""
+        n = len(hk)
         if n == 0:
             return 0
         rows_cap = n * K_SESS
@@ -705,18 +719,18 @@ class KeyedSessionOperator:
             self._pd_copied.synchronize()  # the previous upload has left the pinned buffers
         hrows, hmoved = self._pd_host, self._pd_moved
         with self._phase("promote.extract"):
-            nk, nm = self.store.extract_rows_into(ukh, wm, K_SESS, self.gap, hrows.data_ptr(),
-                                                  hrows.shape[0], hmoved.data_ptr(),
-                                                  hmoved.numel())
+            nk, nm, nu = self.store.extract_rows_into(hk, wm, K_SESS, self.gap, hrows.data_ptr(),
+                                                      hrows.shape[0], hmoved.data_ptr(),
+                                                      hmoved.numel())
         st = self._st()
         with self._phase("promote.scatter"):
-            if nm == n:
-                mt = uk  # every wanted key left the store
+            if nm == nu:
+                mt = dk  # every wanted key left the store
             else:
                 mt = hmoved[:nm].to(self.device, non_blocking=True)
             if nm:
                 self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
-                                          mt.data_ptr(), nm, st)
+                                          mt.data_ptr(), mt.numel(), st)
             if nk:
                 self._pd_dev[:nk].copy_(hrows[:nk], non_blocking=True)
             if getattr(self, "_pd_copied", None) is None:

@@ -279,8 +279,9 @@ def _packed_by_key(ex):
 def _extract_both(a, b, want, wm):
     rows = np.zeros((want.size * 4, 8), np.int64)
     moved = np.zeros(want.size, np.int64)
-    nk, nm = a.extract_rows_into(want, wm, 4, 100, rows.ctypes.data, rows.shape[0],
-                                 moved.ctypes.data, moved.size)
+    nk, nm, nu = a.extract_rows_into(want, wm, 4, 100, rows.ctypes.data, rows.shape[0],
+                                     moved.ctypes.data, moved.size)
+    assert nu == np.unique(want).size
     ex = b.extract_packed(want, wm, 4, 100)
     assert _rows_by_key(rows, nk) == _packed_by_key(ex)
     assert np.array_equal(np.sort(moved[:nm]), np.sort(ex["moved"]))
@@ -330,7 +331,7 @@ def test_store_extract_rows_into_multi_and_hot_keys():
             st_.process(np.array([30], np.int64), np.array([200_000 + t * 1000], np.int64),
                         np.array([1], np.int64), 0)
         stores.append(st_)
-    want = np.array([21, 8, 7, 20, 30, 999_999, 3, 4, 5], np.int64)
+    want = np.array([21, 8, 7, 20, 30, 999_999, 3, 4, 5, 7, 21], np.int64)  # unsorted, repeats
     nk, nm = _extract_both(stores[0], stores[1], want, 0)
     assert nm == want.size - 1  # key 30 stays
     assert stores[0].num_keys() == stores[1].num_keys()
