@@ -333,7 +333,7 @@ def test_store_extract_rows_into_multi_and_hot_keys():
         stores.append(st_)
     want = np.array([21, 8, 7, 20, 30, 999_999, 3, 4, 5, 7, 21], np.int64)  # unsorted, repeats
     nk, nm = _extract_both(stores[0], stores[1], want, 0)
-    assert nm == want.size - 1  # key 30 stays
+    assert nm == np.unique(want).size - 1  # key 30 stays
     assert stores[0].num_keys() == stores[1].num_keys()
     # the multi keys' entries are cleared: the next extract takes the indexed path again
     w2 = np.arange(100, 200, dtype=np.int64)
