@@ -331,6 +331,7 @@ def _timed_profile():
         st = pstats.Stats(prof, stream=s)
         st.sort_stats("tottime").print_stats(30)
         st.print_callers("empty|absorb|export")
+        st.sort_stats("cumulative").print_stats(40)
         with open(out, "w") as f:
             f.write(s.getvalue())
 
@@ -423,6 +424,7 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
     vt = torch.empty_like(kt)
     step_i = [0]
     lat = []
+    rev = [None, None]  # revisit keys / scratch
 
     def step():
         t_in = time.perf_counter()
@@ -431,9 +433,17 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
                      ts_base=i * span, ts_span=span, disorder=1_000, val_lo=0, val_span=10_000)
         kt.add_(i * drift)
         if revisit > 0 and i >= 12:
+            # every stride-th event goes to a key of the drift window 10 steps back: its own
+            # uniform draw over that window (gen_events), written over the strided events
+            # (torch's int64 remainder_ on the strided view cost ~6 ms of host time per step)
             stride = max(2, round(1.0 / revisit))
             old = kt[::stride]
-            old.sub_(10 * drift + i * drift).remainder_(drift).add_((i - 10) * drift)
+            if rev[0] is None or rev[0].numel() != old.numel():
+                rev[0] = torch.empty(old.numel(), dtype=torch.int64, device=dev)
+                rev[1] = torch.empty_like(rev[0])
+            K.gen_events(rev[0], rev[1], rev[1], seed=55, stream_id=1, idx0=i * old.numel(),
+                         nkeys=drift, ts_base=0, ts_span=1, disorder=0, val_lo=0, val_span=1)
+            old.copy_(rev[0].add_((i - 10) * drift))
         rows = op.process(kt, tt, vt)
         step_i[0] += 1
         if len(rows):
@@ -449,9 +459,10 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
     m0 = dict(op.metrics.__dict__)
     t0 = time.perf_counter()
     alerts = 0
-    for _ in range(steps):
-        alerts += step()
-    _sync(dev)
+    with _timed_profile():
+        for _ in range(steps):
+            alerts += step()
+        _sync(dev)
     dt = time.perf_counter() - t0
     mt = op.metrics
     return {"config": 5, "metric": "events/sec (session-window alert + host-DRAM spill)",
