@@ -442,7 +442,7 @@ class KeyedRollingOperator:
             # (the copy kernel reads the row count itself) and ONE wait -- instead of a flag read
             # plus three pageable D2H copies, each its own sync. The rows are copied out of the
             # slab (callers may keep them), so the slab is free again at once.
-            from .window_operator import CountedHostRows, PinnedSlabPool
+            from .host_rows import CountedHostRows, PinnedSlabPool
 
             if getattr(self, "_emit_pool", None) is None:
                 self._emit_pool = PinnedSlabPool(max_slabs=4)

@@ -220,7 +220,7 @@ class KeyedSessionOperator:
             self._occ_pending = None  # event of an in-flight occupancy count (_occ_launch)
             # Fired rows: the device-counted copy into a pinned slab (one wait per firing);
             # more rows than the slab column holds take the synchronous copy.
-            from .window_operator import PinnedSlabPool
+            from .host_rows import PinnedSlabPool
 
             self._pool = PinnedSlabPool()
             self._fire_rows_async = min(self.ocap, 1 << 20)
@@ -840,7 +840,7 @@ class KeyedSessionOperator:
                            self.out_start.data_ptr(), self.out_end.data_ptr(),
                            self.out_val.data_ptr(), self.out_raw.data_ptr(),
                            self.out_cnt.data_ptr(), c[6:7].data_ptr(), self.ocap, st)
-        from .window_operator import CountedHostRows
+        from .host_rows import CountedHostRows
 
         ka = self._fire_rows_async
         cols = [t[:ka] for t in (self.out_key, self.out_start, self.out_end, self.out_val,
@@ -943,7 +943,7 @@ class KeyedSessionOperator:
         a job for the store's persistent C++ worker (csrc/sessions.cpp SessionStore.spill_submit):
         it waits for the copy's HIP event, inserts the rows and expires dead cold chunks with no
         GIL and no Python thread. Its results are applied when polled (_apply_spill_results)."""
-        from .window_operator import CountedHostRows
+        from .host_rows import CountedHostRows
 
         if getattr(self, "_spill_stream", None) is None:
             self._spill_stream = torch.cuda.Stream(self.device)

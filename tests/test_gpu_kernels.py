@@ -421,9 +421,9 @@ def test_spill_tier_gpu_matches_unbounded_cpu(gpu_device, pane_sort, monkeypatch
     unbounded C++-twin table."""
     import sys
 
-    from mxstream.runtime import window_operator as W
+    from mxstream.runtime import window_tiering as WT
 
-    monkeypatch.setattr(W, "_EVICT_PANE_SORT", pane_sort)
+    monkeypatch.setattr(WT, "_EVICT_PANE_SORT", pane_sort)
 
     sys.path.insert(0, __import__("os").path.dirname(__file__))
     from test_window_operator_cpu import _drift_batches, _run_windows
