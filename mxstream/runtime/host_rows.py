@@ -73,7 +73,10 @@ class PinnedSlabPool:
         self.allocs += 1
         self.slabs.append((t, t.numpy()))
 
-    def take(self, nbytes: int) -> tuple[torch.Tensor, np.ndarray]:
+    def take(self, nbytes: int, twins: bool = False) -> tuple[torch.Tensor, np.ndarray]:
+        """A free slab of at least nbytes. twins: when a new slab must be allocated, allocate a
+        second one of the same size with it -- a caller that holds one slab while it fills the
+        next (the tier export) would otherwise page-lock the second at a later, busier call."""
         if getattr(self, "_reserving", None) is not None:
             # a reserve in flight that this take needs is waited for (not allocated twice)
             self._land_reserve(block=not any(s[0].numel() >= nbytes and self._free(i)
@@ -86,10 +89,20 @@ class PinnedSlabPool:
             free = [i for i in range(len(self.slabs)) if self._free(i)]
             if free:
                 self.slabs.pop(min(free, key=lambda i: self.slabs[i][0].numel()))
-        t = torch.empty(_next_pow2(max(nbytes, 1 << 16)), dtype=torch.uint8, pin_memory=self.pin)
+        size = _next_pow2(max(nbytes, 1 << 16))
+        t = torch.empty(size, dtype=torch.uint8, pin_memory=self.pin)
         self.allocs += 1
         slab = (t, t.numpy())
         self.slabs.append(slab)
+        if twins and len(self.slabs) < self.max_slabs + 1:
+            if len(self.slabs) > self.max_slabs:  # make room: the smallest free other slab
+                free = [i for i in range(len(self.slabs) - 1) if self._free(i)]
+                if free:
+                    self.slabs.pop(min(free, key=lambda i: self.slabs[i][0].numel()))
+            if len(self.slabs) < self.max_slabs:
+                t2 = torch.empty(size, dtype=torch.uint8, pin_memory=self.pin)
+                self.allocs += 1
+                self.slabs.append((t2, t2.numpy()))
         return slab
 
 

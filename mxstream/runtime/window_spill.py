@@ -173,7 +173,7 @@ class HostWindowTier:
             bound = bound * 3
             a8 = (bound * 8 + 255) & ~255
             need = 2 * a8 + bound * 4 + 256
-            t, arr = pool.take(need)
+            t, arr = pool.take(need, twins=True) if hasattr(pool, "slabs") else pool.take(need)
             if _PIN_RESERVE and t.numel() < 2 * need and hasattr(pool, "reserve_async"):
                 pool.reserve_async(2 * need)  # the tier grows: the next slab, off the step
             base = t.data_ptr()

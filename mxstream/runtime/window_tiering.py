@@ -258,7 +258,7 @@ class _TierMixin:
             ev.synchronize()  # (long done: a previous firing's copy) -- the slab may be reused
         self._tier_h2d = []
         if self._tier_pool is None and cuda:
-            self._tier_pool = PinnedSlabPool(max_slabs=2)
+            self._tier_pool = PinnedSlabPool(max_slabs=3)  # two current + one draining
         ex = self.host_tier.export(p0, p1, dev, self._tier_pool)
         if cuda and ex is not None:
             ev = torch.cuda.Event()
