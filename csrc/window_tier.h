@@ -253,8 +253,15 @@ class WindowTierCore {
   // Pane-sorted chunks contribute one contiguous segment each (copied by threads in equal row
   // shares); other chunks are filtered row by row (counted in parallel, then copied to their
   // prefix offsets). Row order is unspecified.
+  // Window form: only output rows [r_begin, r_begin + cap) are written (to k[o - r_begin]...),
+  // so a large export can go through a ring of fixed pinned slabs piece by piece; the returned
+  // total is the whole export's row count. The output order is the same for every window.
   size_t export_rows(int64_t p0, int64_t p1, uint64_t* k, uint64_t* a, uint32_t* c,
                      size_t cap) const {
+    return export_window(p0, p1, k, a, c, 0, cap, false);
+  }
+  size_t export_window(int64_t p0, int64_t p1, uint64_t* k, uint64_t* a, uint32_t* c,
+                       size_t r_begin, size_t cap, bool partial) const {
     struct Seg {
       const Chunk* ch;
       size_t lo, hi, out;
@@ -292,32 +299,41 @@ class WindowTierCore {
     std::vector<size_t> off(src.size() + 1, nseg);
     for (size_t j = 0; j < src.size(); ++j) off[j + 1] = off[j] + cnt[j];
     const size_t total = off.back();
-    if (total > cap || total == 0) return total;
-    // sorted segments: thread t copies output rows [nseg * t / T, nseg * (t + 1) / T)
-    const size_t T = host_threads(nseg);
-    if (nseg)
+    if (total == 0 || (!partial && total > cap)) return total;
+    // the output window [wb, we) of the row order
+    const size_t wb = std::min(r_begin, total), we = std::min(total, r_begin + cap);
+    if (wb >= we) return total;
+    // sorted segments: thread t copies output rows [wb + n * t / T, wb + n * (t + 1) / T) of the
+    // window's part that falls in the segments [0, nseg)
+    const size_t sb = wb, se = std::min(we, nseg);
+    const size_t nwin = se > sb ? se - sb : 0;
+    const size_t T = host_threads(nwin);
+    if (nwin)
       run_threads(T, [&](size_t t) {
-        const size_t r0 = nseg * t / T, r1 = nseg * (t + 1) / T;
+        const size_t r0 = sb + nwin * t / T, r1 = sb + nwin * (t + 1) / T;
         for (const Seg& s : segs) {
           const size_t o0 = std::max(r0, s.out), o1 = std::min(r1, s.out + (s.hi - s.lo));
           if (o0 >= o1) continue;
           const size_t i0 = s.lo + (o0 - s.out), m = o1 - o0;
-          std::memcpy(k + o0, s.ch->key.data() + i0, m * 8);
-          std::memcpy(a + o0, s.ch->acc.data() + i0, m * 8);
+          std::memcpy(k + (o0 - wb), s.ch->key.data() + i0, m * 8);
+          std::memcpy(a + (o0 - wb), s.ch->acc.data() + i0, m * 8);
           const int64_t* cs = s.ch->cnt.data() + i0;
-          for (size_t q = 0; q < m; ++q) c[o0 + q] = (uint32_t)cs[q];
+          for (size_t q = 0; q < m; ++q) c[o0 - wb + q] = (uint32_t)cs[q];
         }
       });
-    if (!src.empty())
+    if (!src.empty() && we > nseg)
       run_threads(Tu, [&](size_t t) {
         for (size_t j = t; j < src.size(); j += Tu) {
+          if (off[j + 1] <= wb || off[j] >= we) continue;
           const Chunk& ch = *src[j];
           size_t o = off[j];
-          for (size_t i = 0; i < ch.size(); ++i) {
+          for (size_t i = 0; i < ch.size() && o < we; ++i) {
             if (!keep(ch, i)) continue;
-            k[o] = ch.key[i];
-            a[o] = (uint64_t)ch.acc[i];
-            c[o] = (uint32_t)ch.cnt[i];
+            if (o >= wb) {
+              k[o - wb] = ch.key[i];
+              a[o - wb] = (uint64_t)ch.acc[i];
+              c[o - wb] = (uint32_t)ch.cnt[i];
+            }
             ++o;
           }
         }

@@ -65,6 +65,13 @@ void bind_window_tier(py::module_& m) {
         return t.export_rows(p0, p1, reinterpret_cast<uint64_t*>(k), reinterpret_cast<uint64_t*>(a),
                              reinterpret_cast<uint32_t*>(c), cap);
       })
+      .def("export_window", [](const WindowTierCore& t, int64_t p0, int64_t p1, intptr_t k,
+                               intptr_t a, intptr_t c, size_t r_begin, size_t cap) {
+        py::gil_scoped_release nogil;
+        return t.export_window(p0, p1, reinterpret_cast<uint64_t*>(k),
+                               reinterpret_cast<uint64_t*>(a), reinterpret_cast<uint32_t*>(c),
+                               r_begin, cap, true);
+      })
       .def("part", [](const WindowTierCore& t, int64_t p0, int64_t p1) {
         std::vector<uint64_t> k;
         std::vector<int64_t> a, c;

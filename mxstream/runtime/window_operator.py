@@ -347,7 +347,6 @@ class KeyedWindowOperator(_AggMixin, _FireMixin, _TierMixin, _StateMixin):
         self._evict_pending = None   # asynchronous eviction rows on their way to host DRAM
         self._evict_busy = None      # event: the eviction copy stopped reading the device rows
         self._evict_pool = None
-        self._tier_pool = None       # pinned slabs of the tier's rows for device-merged firings
         self._tier_h2d: list = []    # (event, slab) of tier rows still being copied H2D
         self._tier_tab = None        # the device-merged firing's combine table + outputs
         self._tout_busy = None

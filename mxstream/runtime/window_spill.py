@@ -25,10 +25,6 @@ from ..ops import expr as E
 from ..ops import kernels as K
 
 _F64 = (K.AGG_SUM_F64, K.AGG_AVG_F64, K.AGG_MIN_F64, K.AGG_MAX_F64)
-# Reserve the next, larger export slab on a background thread ("1"; off by default: the
-# background page-locking slowed the exports beside it 7x on the box, config 4-spill 1.43 G vs
-# 1.80 G without it, profiles/r5_c4s_reserve_ab.md).
-_PIN_RESERVE = __import__("os").environ.get("MXS_PIN_RESERVE", "0") == "1"
 _MIN = (K.AGG_MIN_I64, K.AGG_MIN_F64)
 _MAX = (K.AGG_MAX_I64, K.AGG_MAX_F64)
 
@@ -156,10 +152,10 @@ class HostWindowTier:
         return r is not None and r[0] <= p1 and r[1] >= p0
 
     def export(self, p0: int, p1: int, device, pool=None):
-        """Live rows of panes [p0, p1], uncombined, as (keys int64, acc int64, cnt int32, n) on
-        `device` (the device-merged tiered firing). GPU: the threaded C++ export writes a pinned
-        slab, the columns go H2D on the current stream (asynchronous); the slab's numpy array is
-        returned as a fifth element -- hold it until the copy has completed. None: no rows."""
+        """Live rows of panes [p0, p1], uncombined, as (keys int64, acc int64, cnt int32, n,
+        None) on `device` (the device-merged tiered firing). GPU: piece by piece through the
+        ring of page-locked slabs (_export_ring), the copies asynchronous on the current stream.
+        None: no rows. (`pool`: unused, kept for callers.)"""
         import torch
 
         self._join()
@@ -167,25 +163,7 @@ class HostWindowTier:
         if bound == 0:
             return None
         if torch.device(device).type == "cuda":
-            # Slab for 3x the tier's rows: the tier grows between firings, and every larger
-            # pinned slab is a fresh page-locked allocation (~12 ms at 256 MB, ~34 ms at 1 GB on
-            # the box) -- the headroom moves the growth into the warm-up.
-            bound = bound * 3
-            a8 = (bound * 8 + 255) & ~255
-            need = 2 * a8 + bound * 4 + 256
-            t, arr = pool.take(need, twins=True) if hasattr(pool, "slabs") else pool.take(need)
-            if _PIN_RESERVE and t.numel() < 2 * need and hasattr(pool, "reserve_async"):
-                pool.reserve_async(2 * need)  # the tier grows: the next slab, off the step
-            base = t.data_ptr()
-            n = int(self._t.export_rows(int(p0), int(p1), base, base + a8, base + 2 * a8, bound))
-            if n > bound:  # export_rows writes nothing past `bound` and returns the total
-                raise RuntimeError(f"tier export: {n} live rows exceed the {bound}-row slab")
-            if n == 0:
-                return None
-            k = t[:n * 8].view(torch.int64).to(device, non_blocking=True)
-            a = t[a8:a8 + n * 8].view(torch.int64).to(device, non_blocking=True)
-            c = t[2 * a8:2 * a8 + n * 4].view(torch.int32).to(device, non_blocking=True)
-            return k, a, c, n, arr
+            return self._export_ring(p0, p1, device)
         k = np.empty(bound, np.int64)
         a = np.empty(bound, np.int64)
         c = np.empty(bound, np.int32)
@@ -197,6 +175,54 @@ class HostWindowTier:
             return None
         return (torch.from_numpy(k[:n]), torch.from_numpy(a[:n]), torch.from_numpy(c[:n]), n,
                 None)
+
+    # Ring of fixed page-locked slabs for the device export: a large export goes piece by piece
+    # (C++ export_window writes rows [r, r + piece) of the export's row order), each piece's H2D
+    # on the current stream, a slab reused once its earlier copy has completed. The pinned
+    # memory never grows with the tier (a growing single slab was re-page-locked inside the
+    # stream: 44-88 ms per growth on the box).
+    _RING_SLABS = 4
+    _RING_ROWS = 1 << 22  # rows per piece: 80 MB per slab (8 + 8 + 4 bytes a row)
+
+    def _export_ring(self, p0: int, p1: int, device):
+        import torch
+
+        if getattr(self, "_ring", None) is None:
+            pr = self._RING_ROWS
+            self._ring = [[torch.empty(pr * 20, dtype=torch.uint8, pin_memory=True), None]
+                          for _ in range(self._RING_SLABS)]
+        pr = self._RING_ROWS
+        total = None
+        dk = da = dc = None
+        r, i = 0, 0
+        while total is None or r < total:
+            slot = self._ring[i % len(self._ring)]
+            if slot[1] is not None:
+                slot[1].synchronize()  # this slab's previous piece has reached the device
+                slot[1] = None
+            t = slot[0]
+            base = t.data_ptr()
+            n = int(self._t.export_window(int(p0), int(p1), base, base + 8 * pr, base + 16 * pr,
+                                          r, pr))
+            if total is None:
+                if n == 0:
+                    return None
+                total = n
+                dk = torch.empty(total, dtype=torch.int64, device=device)
+                da = torch.empty(total, dtype=torch.int64, device=device)
+                dc = torch.empty(total, dtype=torch.int32, device=device)
+            elif n != total:
+                raise RuntimeError("tier export: the tier changed between pieces (internal error)")
+            m = min(pr, total - r)
+            dk[r:r + m].copy_(t[:8 * m].view(torch.int64), non_blocking=True)
+            da[r:r + m].copy_(t[8 * pr:8 * pr + 8 * m].view(torch.int64), non_blocking=True)
+            dc[r:r + m].copy_(t[16 * pr:16 * pr + 4 * m].view(torch.int32), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(device))
+            slot[1] = ev
+            r += m
+            i += 1
+        return dk, da, dc, total, None
 
     def part(self, p0: int, p1: int):
         """This tier's share of the window over panes [p0, p1]: (keys, acc, cnt) per key."""

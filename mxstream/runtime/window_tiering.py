@@ -257,9 +257,7 @@ class _TierMixin:
         for ev, _arr in self._tier_h2d:
             ev.synchronize()  # (long done: a previous firing's copy) -- the slab may be reused
         self._tier_h2d = []
-        if self._tier_pool is None and cuda:
-            self._tier_pool = PinnedSlabPool(max_slabs=3)  # two current + one draining
-        ex = self.host_tier.export(p0, p1, dev, self._tier_pool)
+        ex = self.host_tier.export(p0, p1, dev)
         if cuda and ex is not None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(dev))

@@ -616,6 +616,43 @@ def test_cxx_window_tier_equals_numpy_combine(n):
     assert int(r["cnt"].sum()) == int(cols["cnt"][cols["pane"] >= 15].sum())
 
 
+@pytest.mark.parametrize("piece", [1, 777, 40_000, 10**6])
+def test_cxx_window_tier_export_window_pieces(piece):
+    """export_window (the GPU export's pieces through a ring of fixed pinned slabs) concatenated
+    over [0, total) equals export_rows in the same order -- pane-sorted chunks and a chunk whose
+    pane span is too wide to sort (filtered row by row), with a purged (dead) prefix."""
+    from mxstream.ops.native import load
+
+    rng = np.random.default_rng(9)
+    t = load().WindowTier(K.AGG_SUM_I64)
+    for _ in range(3):
+        n = 30_000
+        t.absorb(rng.integers(0, 50_000, n).astype(np.uint64), rng.integers(10, 20, n),
+                 rng.integers(-9, 9, n), rng.integers(1, 4, n), np.zeros(n, np.uint8))
+    n = 5_000  # pane span >= 2^20: kept unsorted
+    pane = rng.integers(10, 20, n)
+    pane[0] = 10 + (1 << 21)
+    t.absorb(rng.integers(0, 50_000, n).astype(np.uint64), pane, rng.integers(-9, 9, n),
+             rng.integers(1, 4, n), np.zeros(n, np.uint8))
+    t.purge(12)
+    cap = t.nrows
+    k, a, c = np.empty(cap, np.uint64), np.empty(cap, np.int64), np.empty(cap, np.uint32)
+    total = t.export_rows(12, 17, k.ctypes.data, a.ctypes.data, c.ctypes.data, cap)
+    assert 0 < total <= cap
+    parts = [[], [], []]
+    r = 0
+    while r < total:
+        pk, pa, pc = np.empty(piece, np.uint64), np.empty(piece, np.int64), np.empty(piece, np.uint32)
+        assert t.export_window(12, 17, pk.ctypes.data, pa.ctypes.data, pc.ctypes.data, r,
+                               piece) == total
+        m = min(piece, total - r)
+        for lst, arr in zip(parts, (pk, pa, pc)):
+            lst.append(arr[:m])
+        r += m
+    for whole, lst in zip((k, a, c), parts):
+        assert np.array_equal(whole[:total], np.concatenate(lst))
+
+
 def test_cxx_window_tier_purge_never_rewinds():
     """A purge with a cutoff below an earlier purge's (15, then 12) leaves the tier as the first
     purge left it: dead rows stay dead, counts do not wrap (csrc/window_tier.h purge)."""
