@@ -380,10 +380,14 @@ PYBIND11_MODULE(_mxs_native, m) {
   m.def("gpu_gen_events", [](intptr_t keys, intptr_t ts, intptr_t vals, int64_t n, uint64_t seed,
                              uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                              int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
-                             int32_t val_f64, double zipf_s, intptr_t stream) {
+                             int32_t val_f64, double zipf_s, intptr_t stream, uint64_t key_base) {
     gpu::gen_events(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), n, seed, stream_id, idx0,
-                    nkeys, ts_base, ts_span, disorder, val_lo, val_span, val_f64, zipf_s, stream);
-  });
+                    nkeys, ts_base, ts_span, disorder, val_lo, val_span, val_f64, zipf_s, stream,
+                    key_base);
+  }, py::arg("keys"), py::arg("ts"), py::arg("vals"), py::arg("n"), py::arg("seed"),
+     py::arg("stream_id"), py::arg("idx0"), py::arg("nkeys"), py::arg("ts_base"),
+     py::arg("ts_span"), py::arg("disorder"), py::arg("val_lo"), py::arg("val_span"),
+     py::arg("val_f64"), py::arg("zipf_s"), py::arg("stream"), py::arg("key_base") = 0);
   m.def("gpu_partition", [](intptr_t keys, intptr_t ts, intptr_t vals, intptr_t jhash, int64_t n,
                             py::dict plan, intptr_t kg_dest, intptr_t cursor, intptr_t out,
                             intptr_t stats, intptr_t late_idx, uint32_t late_cap, intptr_t stream) {
@@ -1124,11 +1128,14 @@ PYBIND11_MODULE(_mxs_native, m) {
   m.def("cpu_gen_events", [](intptr_t keys, intptr_t ts, intptr_t vals, int64_t n, uint64_t seed,
                              uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                              int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
-                             int32_t val_f64, double zipf_s) {
+                             int32_t val_f64, double zipf_s, uint64_t key_base) {
     py::gil_scoped_release nogil;
     cpu::gen_events(P<uint64_t>(keys), P<int64_t>(ts), P<uint64_t>(vals), n, seed, stream_id, idx0,
-                    nkeys, ts_base, ts_span, disorder, val_lo, val_span, val_f64, zipf_s);
-  });
+                    nkeys, ts_base, ts_span, disorder, val_lo, val_span, val_f64, zipf_s, key_base);
+  }, py::arg("keys"), py::arg("ts"), py::arg("vals"), py::arg("n"), py::arg("seed"),
+     py::arg("stream_id"), py::arg("idx0"), py::arg("nkeys"), py::arg("ts_base"),
+     py::arg("ts_span"), py::arg("disorder"), py::arg("val_lo"), py::arg("val_span"),
+     py::arg("val_f64"), py::arg("zipf_s"), py::arg("key_base") = 0);
   m.def("cpu_partition", [](intptr_t keys, intptr_t ts, intptr_t vals, intptr_t jhash, int64_t n,
                             py::dict plan, intptr_t kg_dest, intptr_t cursor, intptr_t out,
                             intptr_t stats, intptr_t late_idx, uint32_t late_cap) {

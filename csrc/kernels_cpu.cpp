@@ -39,7 +39,7 @@ static Rec load_any(const Rec* base, size_t idx, int rec_words) {
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
-                int32_t val_f64, double zipf_s) {
+                int32_t val_f64, double zipf_s, uint64_t key_base) {
   auto mulhi = [](uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); };
   const double span_per_event = (double)ts_span / (double)n;
   const uint64_t disorder_p1 = (uint64_t)(disorder + 1);
@@ -47,7 +47,7 @@ void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t
     const uint64_t r = rng64(seed, stream_id, idx0 + (uint64_t)i);
     const uint64_t r2 = mix64(r);
     const uint64_t r3 = mix64(r2);
-    const uint64_t key = zipf_s > 0.0 ? zipf_key(r, nkeys, zipf_s) : mulhi(r, nkeys);
+    const uint64_t key = (zipf_s > 0.0 ? zipf_key(r, nkeys, zipf_s) : mulhi(r, nkeys)) + key_base;
     if (val_f64 & 2) reinterpret_cast<int32_t*>(keys)[i] = (int32_t)key;
     else keys[i] = key;
     int64_t t = ts_base + (int64_t)((double)i * span_per_event);

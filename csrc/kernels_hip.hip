@@ -103,7 +103,7 @@ __global__ __launch_bounds__(256) void gen_events_kernel(
     uint64_t* __restrict__ keys, int64_t* __restrict__ ts, uint64_t* __restrict__ vals,
     int64_t n, uint64_t seed, uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
     double span_per_event, uint64_t disorder_p1, int64_t val_lo, uint64_t val_span,
-    int32_t mode, double zipf_s) {
+    int32_t mode, double zipf_s, uint64_t key_base) {
   // mode bit 0: values as f64 bits; bit 1: int32 key ids (the columnar sources' dictionary ids)
   // zipf_s > 0: skewed keys (key_of_draw: power law, rank 0 hottest); 0: uniform.
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -116,6 +116,8 @@ __global__ __launch_bounds__(256) void gen_events_kernel(
             val_lo, val_span, mode, zipf_s, k0, t0, v0);
     gen_one(seed, stream_id, idx0 + (uint64_t)i + 1, i + 1, nkeys, ts_base, span_per_event,
             disorder_p1, val_lo, val_span, mode, zipf_s, k1, t1, v1);
+    k0 += key_base;  // (a drifting key window: no separate add pass over the column)
+    k1 += key_base;
     if (mode & 4) {  // a column not 16-byte aligned (a sliced tensor): scalar stores
       if (mode & 2) {
         reinterpret_cast<int32_t*>(keys)[i] = (int32_t)k0;
@@ -144,6 +146,7 @@ __global__ __launch_bounds__(256) void gen_events_kernel(
     int64_t t;
     gen_one(seed, stream_id, idx0 + (uint64_t)i, i, nkeys, ts_base, span_per_event, disorder_p1,
             val_lo, val_span, mode, zipf_s, k, t, v);
+    k += key_base;
     if (mode & 2) reinterpret_cast<int32_t*>(keys)[i] = (int32_t)k;
     else keys[i] = k;
     ts[i] = t;
@@ -4170,7 +4173,7 @@ int device_count() {
 void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t seed,
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
-                int32_t val_f64, double zipf_s, intptr_t stream) {
+                int32_t val_f64, double zipf_s, intptr_t stream, uint64_t key_base) {
   if (n <= 0) return;
   // mode bit 2: scalar stores (a column that is not 16-byte aligned; int32 keys need 8 bytes)
   const uintptr_t kmis = (uintptr_t)keys & ((val_f64 & 2) ? 7 : 15);
@@ -4178,7 +4181,7 @@ void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t
   hipLaunchKernelGGL(gen_events_kernel, dim3(grid_for((n + 1) / 2, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, keys, ts, vals, n, seed, stream_id, idx0, nkeys, ts_base,
                      (double)ts_span / (double)n, (uint64_t)(disorder + 1), val_lo,
-                     (uint64_t)val_span, mode, zipf_s);
+                     (uint64_t)val_span, mode, zipf_s, key_base);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -186,15 +186,23 @@ def config2_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 5
     vt = torch.empty_like(kt)
     step_i = [0]
     stride = max(2, round(1.0 / revisit)) if revisit > 0 else 0
+    rev = [None, None]
 
     def step():
         i = step_i[0]
         K.gen_events(kt, tt, vt, seed=2, stream_id=0, idx0=i * batch, nkeys=active, ts_base=0,
-                     ts_span=1000, disorder=0, val_lo=0, val_span=100)
-        kt.add_(i * drift)
+                     ts_span=1000, disorder=0, val_lo=0, val_span=100, key_base=i * drift)
         if stride and i >= 12:
+            # every stride-th event: a key of the drift window 10 steps back (its own draw; a
+            # strided int64 remainder_ cost milliseconds of host time per step)
             old = kt[::stride]
-            old.sub_(i * drift).remainder_(drift).add_((i - 10) * drift)
+            if rev[0] is None or rev[0].numel() != old.numel():
+                rev[0] = torch.empty(old.numel(), dtype=torch.int64, device=dev)
+                rev[1] = torch.empty_like(rev[0])
+            K.gen_events(rev[0], rev[1], rev[1], seed=22, stream_id=1, idx0=i * old.numel(),
+                         nkeys=drift, ts_base=0, ts_span=1, disorder=0, val_lo=0, val_span=1,
+                         key_base=(i - 10) * drift)
+            old.copy_(rev[0])
         rows = op.process(kt, vt)
         step_i[0] += 1
         return len(rows.keys)
@@ -364,8 +372,8 @@ def config4_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 1
     def step():
         i = step_i[0]
         K.gen_events(kt, tt, vt, seed=41, stream_id=0, idx0=i * batch, nkeys=active,
-                     ts_base=i * span, ts_span=span, disorder=2_000, val_lo=0, val_span=20_000)
-        kt.add_(i * drift)
+                     ts_base=i * span, ts_span=span, disorder=2_000, val_lo=0, val_span=20_000,
+                     key_base=i * drift)
         fired = op.process(kt, tt, vt)
         step_i[0] += 1
         return sum(len(r.keys) for r in fired)
@@ -430,8 +438,8 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
         t_in = time.perf_counter()
         i = step_i[0]
         K.gen_events(kt, tt, vt, seed=5, stream_id=0, idx0=i * batch, nkeys=active,
-                     ts_base=i * span, ts_span=span, disorder=1_000, val_lo=0, val_span=10_000)
-        kt.add_(i * drift)
+                     ts_base=i * span, ts_span=span, disorder=1_000, val_lo=0, val_span=10_000,
+                     key_base=i * drift)
         if revisit > 0 and i >= 12:
             # every stride-th event goes to a key of the drift window 10 steps back: its own
             # uniform draw over that window (gen_events), written over the strided events
@@ -442,8 +450,9 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
                 rev[0] = torch.empty(old.numel(), dtype=torch.int64, device=dev)
                 rev[1] = torch.empty_like(rev[0])
             K.gen_events(rev[0], rev[1], rev[1], seed=55, stream_id=1, idx0=i * old.numel(),
-                         nkeys=drift, ts_base=0, ts_span=1, disorder=0, val_lo=0, val_span=1)
-            old.copy_(rev[0].add_((i - 10) * drift))
+                         nkeys=drift, ts_base=0, ts_span=1, disorder=0, val_lo=0, val_span=1,
+                         key_base=(i - 10) * drift)
+            old.copy_(rev[0])
         rows = op.process(kt, tt, vt)
         step_i[0] += 1
         if len(rows):

@@ -75,9 +75,10 @@ def reset_stats(s: torch.Tensor) -> None:
 
 def gen_events(keys, ts, vals, *, seed: int, stream_id: int, idx0: int, nkeys: int,
                ts_base: int, ts_span: int, disorder: int, val_lo: int, val_span: int,
-               val_f64: bool = False, zipf: float = 0.0) -> None:
+               val_f64: bool = False, zipf: float = 0.0, key_base: int = 0) -> None:
     """keys: int64, or int32 (dictionary ids, nkeys < 2^31). zipf > 0: power-law skewed keys
-    with that exponent (key 0 hottest; csrc/mxs_common.h zipf_key), 0: uniform."""
+    with that exponent (key 0 hottest; csrc/mxs_common.h zipf_key), 0: uniform. key_base: added
+    to every key (a drifting key window without a separate pass)."""
     n = keys.numel()
     dev = keys.device
     key32 = keys.dtype == torch.int32
@@ -92,10 +93,12 @@ def gen_events(keys, ts, vals, *, seed: int, stream_id: int, idx0: int, nkeys: i
             float(zipf))
     if zipf < 0:
         raise ValueError("zipf exponent must be >= 0")
+    if key_base < 0:
+        raise ValueError("key_base must be >= 0")
     if _is_gpu(keys):
-        m.gpu_gen_events(*args, _stream(keys))
+        m.gpu_gen_events(*args, _stream(keys), key_base)
     else:
-        m.cpu_gen_events(*args)
+        m.cpu_gen_events(*args, key_base)
 
 
 @dataclass
