@@ -425,6 +425,14 @@ class SessionCore {
       return;
     }
     ch.seq = next_seq_++;
+    // Entries of ids never seen before sit on fresh pages: map them in one call
+    // (MADV_POPULATE_WRITE, Linux 5.14+; an error just leaves them to the faults below) instead
+    // of one page fault per 4 KB from the store passes, which the mm lock serialises.
+    {
+      const uintptr_t a = reinterpret_cast<uintptr_t>(loc_ + (ch.kmin - loc_base_)) & ~(uintptr_t)4095;
+      const uintptr_t b = reinterpret_cast<uintptr_t>(loc_ + (ch.kmax - loc_base_) + 1);
+      (void)::madvise(reinterpret_cast<void*>(a), b - a, 23 /* MADV_POPULATE_WRITE */);
+    }
     // Row blocks on the pool, two passes of relaxed (plain) stores -- atomic read-modify-writes
     // serialize every cache miss, key-range tasks re-read the key column per task:
     //  1. every run's first row stores its entry, or kMultiLoc over a live entry of another row;
