@@ -153,7 +153,9 @@ AggPlan make_agg(py::dict d) {
     p.dcnt = reinterpret_cast<uint32_t*>(d["dcnt"].cast<intptr_t>());
     if (!p.dcnt || !p.dlist) throw std::invalid_argument("delta ring needs dcnt and the slot list");
   }
-  if (p.split < 1 || p.split > 1024) throw std::invalid_argument("agg split out of range");
+  // < 0: forced split of every sub-table over -split workgroups (window_agg_kernel)
+  if (p.split == 0 || p.split > 1024 || p.split < -64)
+    throw std::invalid_argument("agg split out of range");
   p.pmask = d.contains("pmask") ? d["pmask"].cast<uint32_t>() : 0u;
   if (p.pmask && !(p.pmask >> 31) && __builtin_popcount(p.pmask) != p.np_step)
     throw std::invalid_argument("sparse panes: np_step must equal popcount(pmask)");

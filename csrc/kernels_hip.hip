@@ -1282,8 +1282,11 @@ __device__ __forceinline__ uint32_t pk_cnt(uint64_t p) {
 // DENSE: directly addressed dense key ids (AggPlan.dense_bits): no LDS key table, no probe.
 constexpr uint32_t kAggSliceMin = 131072;  // records per workgroup of a split sub-table
 
-template <int AGG, int RW, bool PK = false, bool DENSE = false, bool DET = false>
-__global__ __launch_bounds__(1024) void window_agg_kernel(
+// V (8-byte packed path only, A/B via MXS_AGG_V): bit 0 = eight record loads in flight per
+// thread instead of four; bit 1 = at most 64 VGPRs (launch bounds of eight waves per SIMD), so two
+// 1024-thread workgroups fit one CU when their LDS images do.
+template <int AGG, int RW, bool PK = false, bool DENSE = false, bool DET = false, int V = 0>
+__global__ __launch_bounds__(1024, (V & 2) ? 8 : 1) void window_agg_kernel(
     const void* __restrict__ recs, const uint32_t* __restrict__ counts, AggPlan p,
     uint64_t* __restrict__ keys_g, uint64_t* __restrict__ acc_g, uint32_t* __restrict__ cnt_g,
     uint8_t* __restrict__ dirty_g, uint32_t* __restrict__ occupancy, uint32_t* __restrict__ flags) {
@@ -1293,14 +1296,15 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
   // Split sub-tables (AggPlan.split, hot keys): workgroup `slice` of `split` takes an equal
   // share of the sub-table's records; the shares merge into the state with atomic adds.
   if (p.skip && *p.skip) return;  // incomplete exchange: redone by the host (AggPlan.skip)
-  const int split = p.split;  // launcher guarantees 1 unless the layout/aggregate allows it
+  // split < 0: every sub-table over -split workgroups (forced, AggPlan.split).
+  const int split = p.split < 0 ? -p.split : p.split;  // launcher: 1 unless the layout allows it
   const int sub = split > 1 ? (int)blockIdx.x / split : (int)blockIdx.x;
   const int slice = split > 1 ? (int)blockIdx.x % split : 0;
   int nact = 1;
   if (split > 1) {
     uint32_t ca = counts[sub];
     ca = ca < p.bucket_cap ? ca : p.bucket_cap;
-    nact = (int)((ca + kAggSliceMin - 1) / kAggSliceMin);
+    nact = p.split < 0 ? split : (int)((ca + kAggSliceMin - 1) / kAggSliceMin);
     nact = nact < 1 ? 1 : nact > split ? split : nact;
     if (slice >= nact) return;  // workgroup-uniform: before any barrier
   }
@@ -1360,11 +1364,12 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
       // This workgroup's share [e_lo, c) of the segment (all of it unless split).
       const uint32_t e_lo = shared_sub ? (uint32_t)((uint64_t)c * slice / nact) : 0u;
       if (shared_sub) c = (uint32_t)((uint64_t)c * (slice + 1) / nact);
-      // kAggU independent record loads in flight per thread before the LDS work.
-      for (uint32_t e0 = e_lo + threadIdx.x; e0 < c; e0 += blockDim.x * kAggU) {
-        Rec rr[kAggU];
+      // kU independent record loads in flight per thread before the LDS work.
+      constexpr int kU = (V & 1) ? 8 : kAggU;
+      for (uint32_t e0 = e_lo + threadIdx.x; e0 < c; e0 += blockDim.x * kU) {
+        Rec rr[kU];
 #pragma unroll
-        for (int u = 0; u < kAggU; ++u) {
+        for (int u = 0; u < kU; ++u) {
           const uint32_t e = e0 + u * blockDim.x;
           // Branch-free: a load under `if (e < c)` made the compiler wait for each load at the
           // branch join (s_waitcnt vmcnt(0) after every load: no loads in flight at all).
@@ -1372,9 +1377,9 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
           rr[u] = load_rec<RW>(recs, seg0 + (e < c ? e : c - 1));
         }
 #pragma unroll
-        for (int u = 0; u < kAggU; ++u) pin_rec<RW>(rr[u]);
+        for (int u = 0; u < kU; ++u) pin_rec<RW>(rr[u]);
 #pragma unroll
-        for (int u = 0; u < kAggU; ++u) {
+        for (int u = 0; u < kU; ++u) {
           const uint32_t e = e0 + u * blockDim.x;
           if (e >= c) break;
           const Rec& r = rr[u];
@@ -1423,7 +1428,7 @@ __global__ __launch_bounds__(1024) void window_agg_kernel(
     // kWB slots per thread per batch: all their state loads are issued before the first
     // combine, so the read-modify-write costs one memory latency per batch instead of one per
     // slot (a slot-at-a-time loop serialised 8 dependent HBM round trips per thread).
-    constexpr int kWB = 8;
+    constexpr int kWB = (V & 2) ? 4 : 8;  // V bit 1: fewer registers (64-VGPR variant)
     const uint32_t nrow = (uint32_t)npg * cap;
     for (uint32_t i0 = threadIdx.x; i0 < nrow; i0 += blockDim.x * kWB) {
       uint32_t dc[kWB], oc[kWB];
@@ -4600,11 +4605,16 @@ static bool agg_pack_ok(const AggPlan& p) {
     const char* e = std::getenv("MXS_AGG_PACK");
     return !(e && e[0] == '0');
   }();
+  // records one workgroup folds: a forced split (AggPlan.split < 0, dense ids, one source, no
+  // touched-slot list: the launcher's split condition) gives each a 1/-split share
+  uint64_t per_wg = (uint64_t)p.nsrc * p.bucket_cap;
+  if (p.split < -1 && p.dense_bits && p.nsrc == 1 && !p.dlist)
+    per_wg = (p.bucket_cap + (uint64_t)(-p.split) - 1) / (uint64_t)(-p.split);
   return enabled && (p.agg == AGG_SUM_I64 || p.agg == AGG_AVG_I64) && p.rec_words <= 2 &&
-         !p.combined && (uint64_t)p.nsrc * p.bucket_cap < 65536;
+         !p.combined && per_wg < 65536;
 }
 
-template <int AGG, int RW, bool PK, bool DENSE, bool DET = false>
+template <int AGG, int RW, bool PK, bool DENSE, bool DET = false, int V = 0>
 static void launch_agg_v(const Rec* recs, const uint32_t* counts, const AggPlan& p,
                          uint64_t* keys_g, uint64_t* acc_g, uint32_t* cnt_g, uint8_t* dirty_g,
                          uint32_t* occ, uint32_t* flags, size_t lds, hipStream_t s) {
@@ -4613,7 +4623,7 @@ static void launch_agg_v(const Rec* recs, const uint32_t* counts, const AggPlan&
   if (lds > kAggDynMax) throw std::runtime_error("window_agg: LDS image exceeds 160 KiB");
   static bool attr = false;
   if (!attr) {
-    HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, RW, PK, DENSE, DET>,
+    HIP_CHECK(hipFuncSetAttribute((const void*)window_agg_kernel<AGG, RW, PK, DENSE, DET, V>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)kAggDynMax));
     attr = true;
   }
@@ -4622,8 +4632,9 @@ static void launch_agg_v(const Rec* recs, const uint32_t* counts, const AggPlan&
   AggPlan q = p;
   const bool split_ok = DENSE && p.nsrc == 1 && !p.dlist &&
                         (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64 || AGG == AGG_COUNT);
-  q.split = split_ok && p.split > 1 ? p.split : 1;
-  hipLaunchKernelGGL((window_agg_kernel<AGG, RW, PK, DENSE, DET>), dim3(p.nsub * q.split), dim3(1024),
+  q.split = split_ok && (p.split > 1 || p.split < -1) ? p.split : 1;
+  const int nsplit = q.split < 0 ? -q.split : q.split;
+  hipLaunchKernelGGL((window_agg_kernel<AGG, RW, PK, DENSE, DET, V>), dim3(p.nsub * nsplit), dim3(1024),
                      lds, s, (const void*)recs, counts, q, keys_g, acc_g, cnt_g, dirty_g, occ,
                      flags);
 }
@@ -4647,10 +4658,23 @@ static void launch_agg_d(const Rec* recs, const uint32_t* counts, const AggPlan&
   if constexpr (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) {
     if (agg_pack_ok(p)) {
       const size_t lds_pk = keys_lds + (size_t)p.pg * cap * 8 + 16 + list_lds;
-      if (p.rec_words == 1)
-        launch_agg_v<AGG, 1, true, DENSE>(recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ,
-                                          flags, lds_pk, s);
-      else
+      // default 2: the 64-VGPR build (two workgroups per CU: hashed 1M-key step 135 -> 119 us)
+      static const int v = [] {
+        const char* e = std::getenv("MXS_AGG_V");
+        return e ? std::atoi(e) & 3 : 2;
+      }();
+      if (p.rec_words == 1) {
+        switch (v) {
+          case 1: launch_agg_v<AGG, 1, true, DENSE, false, 1>(recs, counts, p, keys_g, acc_g, cnt_g,
+                                                              dirty_g, occ, flags, lds_pk, s); break;
+          case 2: launch_agg_v<AGG, 1, true, DENSE, false, 2>(recs, counts, p, keys_g, acc_g, cnt_g,
+                                                              dirty_g, occ, flags, lds_pk, s); break;
+          case 3: launch_agg_v<AGG, 1, true, DENSE, false, 3>(recs, counts, p, keys_g, acc_g, cnt_g,
+                                                              dirty_g, occ, flags, lds_pk, s); break;
+          default: launch_agg_v<AGG, 1, true, DENSE>(recs, counts, p, keys_g, acc_g, cnt_g, dirty_g,
+                                                     occ, flags, lds_pk, s);
+        }
+      } else
         launch_agg_v<AGG, 2, true, DENSE>(recs, counts, p, keys_g, acc_g, cnt_g, dirty_g, occ,
                                           flags, lds_pk, s);
       return;

@@ -415,7 +415,7 @@ class SessionCore {
         loc_off_ = true;
         return;
       }
-      (void)::madvise(m, kMaxLocSpan * sizeof(uint64_t), MADV_HUGEPAGE);
+      if (env_flag("MXS_INDEX_THP", true)) (void)::madvise(m, kMaxLocSpan * sizeof(uint64_t), MADV_HUGEPAGE);
       loc_ = static_cast<uint64_t*>(m);
       // room below the first keys for ids a little older than them
       loc_base_ = ch.kmin > kMaxLocSpan / 8 ? ch.kmin - kMaxLocSpan / 8 : 0;
@@ -428,7 +428,7 @@ class SessionCore {
     // Entries of ids never seen before sit on fresh pages: map them in one call
     // (MADV_POPULATE_WRITE, Linux 5.14+; an error just leaves them to the faults below) instead
     // of one page fault per 4 KB from the store passes, which the mm lock serialises.
-    {
+    if (env_flag("MXS_INDEX_POPULATE", true)) {
       const uintptr_t a = reinterpret_cast<uintptr_t>(loc_ + (ch.kmin - loc_base_)) & ~(uintptr_t)4095;
       const uintptr_t b = reinterpret_cast<uintptr_t>(loc_ + (ch.kmax - loc_base_) + 1);
       (void)::madvise(reinterpret_cast<void*>(a), b - a, 23 /* MADV_POPULATE_WRITE */);
@@ -1323,7 +1323,18 @@ class SessionCore {
 
   int64_t gap_, late_;
  public:
-  int max_threads_ = 16;  // extract's chunk-scan threads (1 inside a sharded store)
+  // extract's chunk-scan / worker-phase threads (1 inside a sharded store); MXS_STORE_THREADS
+  // caps it (the pool shares the process's CPU quota with the stepping thread)
+  int max_threads_ = default_threads();
+  static bool env_flag(const char* name, bool dflt) {
+    const char* e = std::getenv(name);
+    return e ? e[0] != '0' : dflt;
+  }
+  static int default_threads() {
+    const char* e = std::getenv("MXS_STORE_THREADS");
+    const int v = e ? std::atoi(e) : 0;
+    return v > 0 ? std::min(v, 64) : 16;
+  }
   std::unique_ptr<WorkerPool> pool_;  // indexed extract's key blocks (created on first use)
  private:
   int agg_;

@@ -317,13 +317,43 @@ def _gc_settle() -> None:
         __import__("sys").setswitchinterval(float(os.environ["MXS_SWITCH_INTERVAL"]))
 
 
+def _cgroup_cpu_stat() -> dict:
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f if ln.strip())}
+    except (OSError, ValueError):
+        return {}
+
+
+@__import__("contextlib").contextmanager
+def _cpu_accounting():
+    """Process CPU time and cgroup CPU throttling over the timed region, on stderr: a CPU quota
+    exhausted by the process's threads stalls the stepping thread at arbitrary points."""
+    import resource
+    import sys
+    import threading
+
+    r0, c0, t0 = resource.getrusage(resource.RUSAGE_SELF), _cgroup_cpu_stat(), time.perf_counter()
+    try:
+        yield
+    finally:
+        r1, c1, dt = resource.getrusage(resource.RUSAGE_SELF), _cgroup_cpu_stat(), \
+            time.perf_counter() - t0
+        cpu = (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)
+        d = {k: c1[k] - c0.get(k, 0) for k in c1}
+        print(f"timed region {dt * 1e3:.1f} ms: process cpu {cpu * 1e3:.1f} ms "
+              f"({cpu / max(dt, 1e-9):.2f} cpus), py threads {threading.active_count()}, "
+              f"cgroup {d}", file=sys.stderr)
+
+
 @__import__("contextlib").contextmanager
 def _timed_profile():
     """MXS_BENCH_PROFILE=<file>: cProfile of the timed region only (host hot spots without the
     warmup's one-time allocations), top entries by own time written to <file>."""
     out = __import__("os").environ.get("MXS_BENCH_PROFILE")
     if not out:
-        yield
+        with _cpu_accounting():
+            yield
         return
     import cProfile
     import io
@@ -493,6 +523,7 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
             "host_phase_ms_per_step": {k: round(v * 1e3 / steps, 2)
                                        for k, v in sorted(op.phase_s.items())},
             "spill_slab_allocs": op.metrics.extra.get("spill_slab_allocs", 0),
+            "promote_bad_keys": op.metrics.extra.get("promote_bad_keys", 0),
             "store_index": op.store.index_stats() if hasattr(op.store, "index_stats") else None}
 
 

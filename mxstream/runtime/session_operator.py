@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os as _os
 import time
 from collections import defaultdict
 from dataclasses import dataclass, field
@@ -628,6 +629,34 @@ class KeyedSessionOperator:
         r = self.host_recs[: n_host * K.REC_WORDS].view(-1, K.REC_WORDS)
         return r[:, 0], (r[:, 2] & 0xFFFFFFFF) + tbase, r[:, 1]
 
+    def _diverted_cols(self, n_host: int, tbase: int):
+        """The diverted records as three contiguous columns in a reused device buffer (fresh
+        clones per step reached the caching allocator's slow path: 3.7 ms/step measured in the
+        revisit config, profiles/r5_cfg5r_final.json)."""
+        buf = getattr(self, "_dv_buf", None)
+        if buf is None or buf.shape[1] < n_host:
+            buf = self._dv_buf = torch.empty((3, max(1 << 16, 1 << (n_host - 1).bit_length())),
+                                             dtype=torch.int64, device=self.device)
+        r = self.host_recs[: n_host * K.REC_WORDS].view(-1, K.REC_WORDS)
+        dk, dt, dv = buf[0, :n_host], buf[1, :n_host], buf[2, :n_host]
+        with self._phase("promote.clone.presync"):
+            if _os.environ.get("MXS_DBG_PRESYNC") == "1":
+                torch.cuda.current_stream(self.device).synchronize()
+        with self._phase("promote.clone.k"):
+            dk.copy_(r[:, 0])
+        with self._phase("promote.clone.and"):
+            if _os.environ.get("MXS_DBG_MASKT") == "1":
+                if getattr(self, "_mask32", None) is None:
+                    self._mask32 = torch.tensor(0xFFFFFFFF, dtype=torch.int64, device=self.device)
+                torch.bitwise_and(r[:, 2], self._mask32, out=dt)
+            else:
+                torch.bitwise_and(r[:, 2], 0xFFFFFFFF, out=dt)
+        with self._phase("promote.clone.add"):
+            dt.add_(tbase)
+        with self._phase("promote.clone.v"):
+            dv.copy_(r[:, 1])
+        return dk, dt, dv
+
     def _host_fold(self, n_host: int, tbase: int, wm: int) -> None:
         """Records of keys that live in host DRAM: folded by the host store."""
         k, t, v = (x.cpu().numpy() for x in self._diverted(n_host, tbase))
@@ -645,8 +674,8 @@ class KeyedSessionOperator:
         sessions than a slot holds, or whose sub-table is full, stay on the host path.
         Returns (records still for the host tier, late-dropped)."""
         with self._phase("promote"):
-            dk, dt, dv = (x.clone(memory_format=torch.contiguous_format)
-                          for x in self._diverted(n_host, tbase))
+            with self._phase("promote.clone"):
+                dk, dt, dv = self._diverted_cols(n_host, tbase)
             dev = self.device
             if _PROMOTE_ROWS:
                 # the diverted keys as they are (repeats included): the store dedups them (a
@@ -691,7 +720,8 @@ class KeyedSessionOperator:
                                            cap)
             self.metrics.records_promoted += n_host - h[2]
             late = h[6] if total else 0
-            late += self._overflow_runs(h, wm)
+            with self._phase("promote.overflow"):
+                late += self._overflow_runs(h, wm)
             return h[2], late
 
     def _promote_rows(self, dk, hk, wm: int) -> int:
@@ -716,7 +746,8 @@ class KeyedSessionOperator:
             self._pd_dev = torch.empty((cap, 8), dtype=torch.int64, device=self.device)
             self._pd_slots = torch.empty(cap, dtype=torch.int64, device=self.device)
         if getattr(self, "_pd_copied", None) is not None:
-            self._pd_copied.synchronize()  # the previous upload has left the pinned buffers
+            with self._phase("promote.wait_upload"):
+                self._pd_copied.synchronize()  # the previous upload has left the pinned buffers
         hrows, hmoved = self._pd_host, self._pd_moved
         with self._phase("promote.extract"):
             nk, nm, nu = self.store.extract_rows_into(hk, wm, K_SESS, self.gap, hrows.data_ptr(),
@@ -749,6 +780,8 @@ class KeyedSessionOperator:
             ins, n_bad = self.ctr[3:5].tolist()
             self._live_estimate += ins
         if n_bad:  # sub-table full (rare): those keys' sessions go back to the store
+            ex = self.metrics.extra
+            ex["promote_bad_keys"] = ex.get("promote_bad_keys", 0) + n_bad
             bad = (self._pd_slots[:nk] < 0).cpu().numpy()
             r = hrows[:nk].numpy()[bad]
             self.store.insert(np.ascontiguousarray(r[:, 0]), np.ascontiguousarray(r[:, 1]),

@@ -20,6 +20,12 @@ I64_MIN = K.I64_MIN
 I64_MAX = K.I64_MAX
 
 
+
+# > 1: every sub-table's records split over this many workgroups even when none is hot (dense
+# ids, additive aggregates: partial sums merge with atomic adds) -- more workgroups than CUs
+# (A/B, MXS_AGG_FORCE_SPLIT).
+_FORCE_SPLIT = int(_os.environ.get("MXS_AGG_FORCE_SPLIT", "0"))
+
 class _AggMixin:
     """Methods of KeyedWindowOperator (mixed in; state lives on the operator)."""
 
@@ -247,9 +253,11 @@ class _AggMixin:
         """Mirror of the launcher's packed (sum, count) LDS accumulator condition (8 bytes per
         slot and pane instead of 12): integer sums of 8/16-byte own records, < 65536 records
         per sub-table."""
+        per_wg = self._part_ranks * self.bucket_cap
+        if _FORCE_SPLIT > 1 and self.dense_bits and self._part_ranks == 1 and self.dlist is None:
+            per_wg = -(-self.bucket_cap // _FORCE_SPLIT)  # forced split: a share per workgroup
         return (self.agg in (K.AGG_SUM_I64, K.AGG_AVG_I64) and rw <= 2 and not self.combine
-                and self._part_ranks * self.bucket_cap < 65536
-                and _os.environ.get("MXS_AGG_PACK", "1") != "0")
+                and per_wg < 65536 and _os.environ.get("MXS_AGG_PACK", "1") != "0")
 
     def _zero_pane(self, so: int, k: int = 1) -> None:
         """Reset k consecutive pane slabs starting at slot index `so` (pane-major state)."""
