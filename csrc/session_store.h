@@ -415,23 +415,39 @@ class SessionCore {
         loc_off_ = true;
         return;
       }
-      if (env_flag("MXS_INDEX_THP", true)) (void)::madvise(m, kMaxLocSpan * sizeof(uint64_t), MADV_HUGEPAGE);
+      // 4 KB pages: huge pages (MADV_HUGEPAGE) populated here stalled the stepping thread by
+      // ~3 ms per step in config 5 with revisits (profiles/r5_index_paging.md); opt-in
+      if (env_flag("MXS_INDEX_THP", false)) (void)::madvise(m, kMaxLocSpan * sizeof(uint64_t), MADV_HUGEPAGE);
       loc_ = static_cast<uint64_t*>(m);
       // room below the first keys for ids a little older than them
       loc_base_ = ch.kmin > kMaxLocSpan / 8 ? ch.kmin - kMaxLocSpan / 8 : 0;
+      pop_lo_ = ch.kmin - loc_base_;
+      pop_hi_.store(pop_lo_);
     }
     if (ch.kmin < loc_base_ || ch.kmax - loc_base_ >= kMaxLocSpan) {
       drop_index();
       return;
     }
     ch.seq = next_seq_++;
-    // Entries of ids never seen before sit on fresh pages: map them in one call
+    // Entries of ids never seen before sit on fresh pages: mapped in one call
     // (MADV_POPULATE_WRITE, Linux 5.14+; an error just leaves them to the faults below) instead
-    // of one page fault per 4 KB from the store passes, which the mm lock serialises.
+    // of one page fault per 4 KB from the store passes, which the mm lock serialises -- and,
+    // for ids above the mapped range (drifting key spaces), ahead of need on a background
+    // thread, so the worker's index phase finds its pages mapped.
     if (env_flag("MXS_INDEX_POPULATE", true)) {
-      const uintptr_t a = reinterpret_cast<uintptr_t>(loc_ + (ch.kmin - loc_base_)) & ~(uintptr_t)4095;
-      const uintptr_t b = reinterpret_cast<uintptr_t>(loc_ + (ch.kmax - loc_base_) + 1);
-      (void)::madvise(reinterpret_cast<void*>(a), b - a, 23 /* MADV_POPULATE_WRITE */);
+      const size_t lo = ch.kmin - loc_base_, hi = ch.kmax - loc_base_ + 1;
+      if (lo < pop_lo_) {
+        populate(lo, pop_lo_);
+        pop_lo_ = lo;
+      }
+      const size_t ph = pop_hi_.load();
+      if (hi > ph) {
+        populate(ph, hi);
+        size_t cur = pop_hi_.load();
+        while (cur < hi && !pop_hi_.compare_exchange_weak(cur, hi)) {
+        }
+      }
+      populate_ahead(hi);
     }
     // Row blocks on the pool, two passes of relaxed (plain) stores -- atomic read-modify-writes
     // serialize every cache miss, key-range tasks re-read the key column per task:
@@ -919,32 +935,20 @@ class SessionCore {
   // hot sessions leave the store (appended to `released`). Emits no rows, so the GPU operator
   // runs it on its spill worker, off the step's critical path.
   void expire_cold(int64_t wm, std::vector<int64_t>& released) {
+    std::vector<ColdChunk> gone;
+    detach_expired(wm, gone);
+    released_of(gone, released);
+    recycle(gone);
+  }  // the chunks not kept as spares are freed here
+  // The three steps of expire_cold, so that the spill worker holds the store lock only for the
+  // first and the last (config 5 at steady state: expiry under the lock stalled the step's host
+  // fire by ~2 ms). 1. Under the lock: chunks past cleanup at `wm` leave cold_ for `gone`.
+  void detach_expired(int64_t wm, std::vector<ColdChunk>& gone) {
     bool erased = false;
     for (auto it = cold_.begin(); it != cold_.end();) {
       if (it->max_due <= wm) {
-        // (a key whose cold row expires leaves unless it also has hot sessions; with no hot keys
-        // -- the common case, hot state is overflow only -- no per-row map probe)
-        released.reserve(released.size() + it->key.size());
-        const bool no_hot = m_.empty();
-        for (size_t r = 0; r < it->key.size(); ++r)
-          if (it->cnt[r] && (no_hot || !is_hot(it->key[r])))
-            released.push_back((int64_t)it->key[r]);
         cold_rows_ -= it->live;
-        if (spare_.size() < 4) {  // keep the columns' memory for the next eviction's chunk
-          ColdChunk sp = std::move(*it);
-          sp.key.clear();
-          sp.start.clear();
-          sp.end.clear();
-          sp.acc.clear();
-          sp.cnt.clear();
-          sp.by_key.clear();
-          sp.max_due = INT64_MIN;
-          sp.live = 0;
-          sp.kmin = ~0ull;
-          sp.kmax = 0;
-          sp.seq = 0;
-          spare_.push_back(std::move(sp));
-        }
+        gone.push_back(std::move(*it));
         it = cold_.erase(it);
         erased = true;
       } else {
@@ -952,6 +956,38 @@ class SessionCore {
       }
     }
     if (erased) reindex_chunks();
+  }
+  // 2. The keys of the detached chunks' live rows that leave the store: a key with hot sessions
+  // stays (under the lock unless hot_free(), i.e. no hot state -- the common case, hot state is
+  // overflow only -- which makes it a pure function of the detached chunks).
+  void released_of(const std::vector<ColdChunk>& gone, std::vector<int64_t>& released) const {
+    const bool no_hot = m_.empty();
+    for (const ColdChunk& ch : gone) {
+      released.reserve(released.size() + ch.key.size());
+      for (size_t r = 0; r < ch.key.size(); ++r)
+        if (ch.cnt[r] && (no_hot || !is_hot(ch.key[r]))) released.push_back((int64_t)ch.key[r]);
+    }
+  }
+  bool hot_free() const { return m_.empty(); }
+  // 3. Under the lock: the detached chunks' column memory back to the spare list (at most 4
+  // kept for the next evictions' chunks); the caller frees the rest (`gone`) after the lock.
+  void recycle(std::vector<ColdChunk>& gone) {
+    for (ColdChunk& sp : gone) {
+      if (spare_.size() >= 4) break;
+      if (!sp.key.capacity()) continue;
+      sp.key.clear();
+      sp.start.clear();
+      sp.end.clear();
+      sp.acc.clear();
+      sp.cnt.clear();
+      sp.by_key.clear();
+      sp.max_due = INT64_MIN;
+      sp.live = 0;
+      sp.kmin = ~0ull;
+      sp.kmax = 0;
+      sp.seq = 0;
+      spare_.push_back(std::move(sp));
+    }
   }
 
   // Device spill set (open addressing on mix64(key) >> 32, linear probing, empty = ~0) holding
@@ -1079,7 +1115,32 @@ class SessionCore {
     return r < ch.key.size() && ch.key[r] == key && ch.cnt[r];
   }
   bool index_usable() const { return !loc_off_ && loc_ != nullptr; }
+  // Map the index pages of entries [a, b) (whole pages).
+  void populate(size_t a, size_t b) const {
+    if (b <= a) return;
+    const uintptr_t x = reinterpret_cast<uintptr_t>(loc_ + a) & ~(uintptr_t)4095;
+    const uintptr_t y = reinterpret_cast<uintptr_t>(loc_ + b);
+    (void)::madvise(reinterpret_cast<void*>(x), y - x, 23 /* MADV_POPULATE_WRITE */);
+  }
+  // Entries up to `need`: when the mapped range ends less than kPopAhead / 2 above it, one
+  // background thread maps the next kPopAhead entries (one at a time; joined before the next).
+  static constexpr size_t kPopAhead = (size_t)1 << 22;  // 32 MB of entries
+  void populate_ahead(size_t need) {
+    const size_t ph = pop_hi_.load();
+    if (need + kPopAhead / 2 <= ph || ph >= kMaxLocSpan || pop_busy_.load()) return;
+    if (pop_thread_.joinable()) pop_thread_.join();
+    const size_t end = std::min(kMaxLocSpan, ph + kPopAhead);
+    pop_busy_.store(true);
+    pop_thread_ = std::thread([this, ph, end] {
+      populate(ph, end);
+      size_t cur = pop_hi_.load();
+      while (cur < end && !pop_hi_.compare_exchange_weak(cur, end)) {
+      }
+      pop_busy_.store(false);
+    });
+  }
   void drop_index() {
+    if (pop_thread_.joinable()) pop_thread_.join();
     if (loc_) ::munmap(loc_, kMaxLocSpan * sizeof(uint64_t));
     loc_ = nullptr;
     loc_off_ = true;
@@ -1420,6 +1481,10 @@ class SessionCore {
   std::vector<ColdChunk> spare_;  // emptied chunks whose column capacity is reused
   size_t cold_rows_ = 0;
   uint64_t* loc_ = nullptr;  // dense cold-row index (index_cold): kMaxLocSpan reserved entries
+  size_t pop_lo_ = 0;                 // entries [pop_lo_, pop_hi_) have their pages mapped
+  std::atomic<size_t> pop_hi_{0};
+  std::atomic<bool> pop_busy_{false};
+  std::thread pop_thread_;            // the read-ahead mapping (populate_ahead)
   uint64_t loc_base_ = 0;
   bool loc_off_ = false;
   uint32_t next_seq_ = 1, seq_lo_ = 1;

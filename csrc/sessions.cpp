@@ -91,7 +91,7 @@ struct SpillDone {
   uint64_t id = 0;
   int64_t nr = 0, ne = 0, nk = 0;
   std::vector<int64_t> released;
-  double t_wait = 0, t_hot = 0, t_build = 0, t_index = 0, t_publish = 0;  // seconds per phase
+  double t_wait = 0, t_hot = 0, t_build = 0, t_index = 0, t_publish = 0, t_expire = 0;  // s
   std::exception_ptr err;
 };
 
@@ -394,6 +394,7 @@ class SessionStore {
       r["t_build"] = d.t_build;
       r["t_index"] = d.t_index;
       r["t_publish"] = d.t_publish;
+      r["t_expire"] = d.t_expire;
       out.append(r);
     }
     if (err) std::rethrow_exception(err);
@@ -461,17 +462,39 @@ class SessionStore {
         // of the index (extract, promote, expiry) joins this worker first.
         if (one && nr) one->index_cold(plan);
         const auto t3 = clk::now();
+        // Expiry: a single store detaches its expired chunks under the lock and reads their keys
+        // and frees their memory outside it (the step's host fire waits for this lock).
+        std::vector<sess::ColdChunk> gone;
+        bool gather_outside = false;
         {
           std::lock_guard<std::mutex> g(mu_);
           if (one && nr) one->publish_cold(plan);
-          if (j.expire) c_.expire_cold(j.expire_wm, d.released);
+          if (j.expire) {
+            if (one) {
+              one->detach_expired(j.expire_wm, gone);
+              gather_outside = one->hot_free();
+              if (!gather_outside) one->released_of(gone, d.released);
+            } else {
+              c_.expire_cold(j.expire_wm, d.released);
+            }
+          }
         }
         const auto t4 = clk::now();
+        if (!gone.empty()) {
+          if (gather_outside) one->released_of(gone, d.released);
+          {
+            std::lock_guard<std::mutex> g(mu_);
+            one->recycle(gone);  // up to the spare limit; the rest stays in `gone`
+          }
+          gone.clear();  // frees the remaining chunks' memory outside the lock
+        }
+        const auto t5 = clk::now();
         d.t_wait = sec(t0, t1);
         d.t_hot = sec(t1, t2);
         d.t_build = sec(t2, t2b);
         d.t_index = sec(t2b, t3);
         d.t_publish = sec(t3, t4);
+        d.t_expire = sec(t4, t5);
       } catch (...) {
         d.err = std::current_exception();
       }

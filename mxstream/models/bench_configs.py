@@ -333,10 +333,27 @@ def _cpu_accounting():
     import sys
     import threading
 
+    import gc
+
+    gcs = {"n": [0, 0, 0], "ms": [0.0, 0.0, 0.0], "t": 0.0}
+
+    def on_gc(phase, info):
+        if phase == "start":
+            gcs["t"] = time.perf_counter()
+        else:
+            g = info["generation"]
+            gcs["n"][g] += 1
+            gcs["ms"][g] += (time.perf_counter() - gcs["t"]) * 1e3
+
+    gc.callbacks.append(on_gc)
     r0, c0, t0 = resource.getrusage(resource.RUSAGE_SELF), _cgroup_cpu_stat(), time.perf_counter()
     try:
         yield
     finally:
+        gc.callbacks.remove(on_gc)
+        print(f"gc in timed region: collections per generation {gcs['n']}, ms "
+              f"{[round(x, 2) for x in gcs['ms']]}, tracked objects {len(gc.get_objects())}",
+              file=sys.stderr)
         r1, c1, dt = resource.getrusage(resource.RUSAGE_SELF), _cgroup_cpu_stat(), \
             time.perf_counter() - t0
         cpu = (r1.ru_utime - r0.ru_utime) + (r1.ru_stime - r0.ru_stime)

@@ -32,7 +32,6 @@ from __future__ import annotations
 
 import contextlib
 import math
-import os as _os
 import time
 from collections import defaultdict
 from dataclasses import dataclass, field
@@ -229,6 +228,17 @@ class KeyedSessionOperator:
             self._hlate = torch.zeros(1, dtype=torch.int64, pin_memory=True)
             self._hred = torch.zeros(K.RED_WORDS, dtype=torch.int64, pin_memory=True)
             self.spill_any = False
+            self._warm_promote_ops()
+
+    def _warm_promote_ops(self) -> None:
+        """The first launch of a PyTorch kernel in a process loads its code object (tens of ms
+        on a fresh box, measured as a 60 ms stall inside the first promotion of config 5 with
+        revisits, which the warm-up steps never reach): the promote path's own tensor ops run
+        once here, on dummy rows, so no step pays it."""
+        self._diverted_cols(1, 0)
+        cur = torch.zeros(self.nsub, dtype=torch.int32, device=self.device)
+        int(cur.max())
+        torch.cuda.current_stream(self.device).synchronize()
 
     # ---- buffers ----------------------------------------------------------------------------
     def _alloc(self, batch_capacity: int, slack: float = 1.5) -> None:
@@ -485,7 +495,7 @@ class KeyedSessionOperator:
         rel = d["released"]
         if self.gpu and len(rel) and self.spill_any:
             # Keys that left the host store leave the device spill set (tombstoned).
-            kt = torch.from_numpy(rel).to(self.device)
+            kt = self._keys_to_device(rel)
             self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
                                       kt.data_ptr(), kt.numel(), self._st())
         return SessionRows(d["keys"].view(np.uint64), d["start"], d["end"], d["values"], d["raw"],
@@ -630,31 +640,17 @@ class KeyedSessionOperator:
         return r[:, 0], (r[:, 2] & 0xFFFFFFFF) + tbase, r[:, 1]
 
     def _diverted_cols(self, n_host: int, tbase: int):
-        """The diverted records as three contiguous columns in a reused device buffer (fresh
-        clones per step reached the caching allocator's slow path: 3.7 ms/step measured in the
-        revisit config, profiles/r5_cfg5r_final.json)."""
+        """The diverted records as three contiguous columns in a reused device buffer."""
         buf = getattr(self, "_dv_buf", None)
         if buf is None or buf.shape[1] < n_host:
             buf = self._dv_buf = torch.empty((3, max(1 << 16, 1 << (n_host - 1).bit_length())),
                                              dtype=torch.int64, device=self.device)
         r = self.host_recs[: n_host * K.REC_WORDS].view(-1, K.REC_WORDS)
         dk, dt, dv = buf[0, :n_host], buf[1, :n_host], buf[2, :n_host]
-        with self._phase("promote.clone.presync"):
-            if _os.environ.get("MXS_DBG_PRESYNC") == "1":
-                torch.cuda.current_stream(self.device).synchronize()
-        with self._phase("promote.clone.k"):
-            dk.copy_(r[:, 0])
-        with self._phase("promote.clone.and"):
-            if _os.environ.get("MXS_DBG_MASKT") == "1":
-                if getattr(self, "_mask32", None) is None:
-                    self._mask32 = torch.tensor(0xFFFFFFFF, dtype=torch.int64, device=self.device)
-                torch.bitwise_and(r[:, 2], self._mask32, out=dt)
-            else:
-                torch.bitwise_and(r[:, 2], 0xFFFFFFFF, out=dt)
-        with self._phase("promote.clone.add"):
-            dt.add_(tbase)
-        with self._phase("promote.clone.v"):
-            dv.copy_(r[:, 1])
+        dk.copy_(r[:, 0])
+        torch.bitwise_and(r[:, 2], 0xFFFFFFFF, out=dt)
+        dt.add_(tbase)
+        dv.copy_(r[:, 1])
         return dk, dt, dv
 
     def _host_fold(self, n_host: int, tbase: int, wm: int) -> None:
@@ -1024,12 +1020,31 @@ class KeyedSessionOperator:
         if self.gpu and self.store.spill_submitted():
             self._apply_spill_results(self.store.spill_poll())
 
+    def _keys_to_device(self, keys: np.ndarray) -> torch.Tensor:
+        """Host key ids on the device through a reused page-locked buffer and an asynchronous
+        copy on the current stream (a pageable copy of the ~3 MB released per expired chunk
+        cost ~0.9 ms per step at steady state). Valid for kernels enqueued on the same stream."""
+        n = len(keys)
+        buf = getattr(self, "_kh_buf", None)
+        if buf is None or buf[0].numel() < n:
+            cap = max(1 << 16, 1 << (n - 1).bit_length())
+            buf = self._kh_buf = (torch.empty(cap, dtype=torch.int64, pin_memory=True),
+                                  torch.empty(cap, dtype=torch.int64, device=self.device),
+                                  torch.cuda.Event())
+            buf[2].record(torch.cuda.current_stream(self.device))
+        host, dev, ev = buf
+        ev.synchronize()  # the previous copy has left the pinned buffer
+        host[:n].numpy()[:] = keys
+        dev[:n].copy_(host[:n], non_blocking=True)
+        ev.record(torch.cuda.current_stream(self.device))
+        return dev[:n]
+
     def _apply_spill_results(self, res: list) -> None:
         for r in res:
             rel = r["released"]
             if len(rel) and self.spill_any:
                 # keys of expired cold chunks leave the device spill set
-                kt = torch.from_numpy(rel).to(self.device)
+                kt = self._keys_to_device(rel)
                 self.native.gpu_set_erase(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
                                           kt.data_ptr(), kt.numel(), self._st())
             self._live_estimate -= r["ne"]
@@ -1037,7 +1052,7 @@ class KeyedSessionOperator:
             self.set_used += r["nr"]
             self.metrics.freed_slots += r["ne"]
             self.metrics.spilled_keys += r["nk"]
-            for k in ("wait", "hot", "build", "index", "publish"):  # the worker's own phase times
+            for k in ("wait", "hot", "build", "index", "publish", "expire"):  # worker phase times
                 self.phase_s[f"spill.worker.{k}"] += r[f"t_{k}"]
 
     def _ensure_spill_capacity(self, extra: int) -> None:

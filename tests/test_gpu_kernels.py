@@ -727,3 +727,31 @@ def test_window_rows_pane_sort(gpu_device):
         a = got[off[j]:off[j + 1]]
         b = src[pane[:n].numpy() == p_lo + j]
         assert np.array_equal(a[np.lexsort(a.T[::-1])], b[np.lexsort(b.T[::-1])])
+
+
+def test_hashed_narrow_steps_over_wide_table_keys_equal_cpu(gpu_device):
+    """8-byte records fold against 32-bit LDS keys; a sub-table holding a key >= 2^32 - 1
+    (restored from a checkpoint written by 16-byte steps) keeps 64-bit keys. Steps 1.. run
+    narrow on a table restored with wide keys in most sub-tables: results equal the CPU twin's."""
+    res = {}
+    for d in (gpu_device, torch.device("cpu")):
+        def op_for():
+            return KeyedWindowOperator(size=2000, agg=K.AGG_SUM_I64, device=d, max_keys=20_000,
+                                       batch_capacity=1 << 16, ooo_bound=300, cap_log2=9)
+        op = op_for()
+        keys, ts, vals = _gen(d, 1 << 16, 20_000, span=2500, disorder=300, seed=11)
+        wide = torch.arange(keys.numel(), device=d) % 16 == 0
+        keys = torch.where(wide, keys + (1 << 33), keys)  # ~4K wide keys: most sub-tables
+        out = op.process(keys, ts, vals)
+        snap = op.snapshot_state()
+        op = op_for()
+        op.restore_state(snap.columns, snap.meta)
+        if d.type == "cuda":
+            assert op.rec_w == 1  # the restored operator runs 8-byte records again
+        for step in range(1, 5):
+            keys, ts, vals = _gen(d, 1 << 16, 20_000, span=2500, disorder=300, seed=11 + step)
+            ts += step * 2500
+            out += op.process(keys, ts, vals)
+        out += op.finish()
+        res[d.type] = _results(out)
+    assert res["cuda"] == res["cpu"]
