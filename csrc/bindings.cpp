@@ -240,6 +240,7 @@ IngestOut make_ingest_out(py::dict d) {
   o.shash = P<uint64_t>(d["shash"].cast<intptr_t>());
   o.nflag = P<uint32_t>(d["nflag"].cast<intptr_t>());
   o.maxts = P<int64_t>(d["maxts"].cast<intptr_t>());
+  o.tile_max = d.contains("tile_max") ? P<int64_t>(d["tile_max"].cast<intptr_t>()) : nullptr;
   return o;
 }
 

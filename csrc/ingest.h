@@ -56,6 +56,9 @@ struct IngestOut {
   uint64_t* shash;    // [n * S] content hash (never 0)
   uint32_t* nflag;    // flagged lines (device counter)
   int64_t* maxts;     // max of column ts_col over the unflagged lines (device, atomic max)
+  // [tiles] per-tile maxima reduced by one workgroup after the parse (nullptr: one atomic max
+  // per workgroup -- same-address atomics from every workgroup serialise across the XCDs)
+  int64_t* tile_max = nullptr;
 };
 
 // Device string dictionary: id <-> bytes, plus the Java hash of every id.

@@ -45,6 +45,114 @@ __device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
   return v;
 }
 
+// The device twin of ingest.h ingest_line with one copy of each field parser: the output
+// columns are visited in a loop that is not unrolled, each finding its split field from a
+// cursor over the line (one forward scan when the columns ask for ascending split indices,
+// a rescan from the line start otherwise). ingest_line's unrolled per-column copies of every
+// parser made a 34K-instruction kernel whose instruction fetch, not its work, set its time.
+// Same results as ingest_line (Java String.split semantics: trailing empty fields dropped, ""
+// splits to [""]).
+template <class Text>
+__device__ uint8_t ingest_line_dev(Text text, int64_t a, int64_t b, int64_t li, int64_t n,
+                                   const IngestSpec& sp, const IngestOut& o, int64_t* ts_val) {
+  const char sep = (char)sp.sep;
+  uint8_t st = 0;
+  int idx = 0;       // split index of the field starting at `cur`
+  int64_t cur = a;
+#pragma unroll 1
+  for (int f = 0; f < sp.nfields; ++f) {
+    const int want = sp.field[f];
+    if (want < idx) {
+      idx = 0;
+      cur = a;
+    }
+    bool exists = true;
+    while (idx < want) {  // skip to the start of field `want`
+      int64_t p = cur;
+      while (p < b && text[p] != sep) ++p;
+      if (p >= b) {
+        exists = false;
+        break;
+      }
+      cur = p + 1;
+      ++idx;
+    }
+    int64_t fe = cur;
+    bool present = false;
+    if (exists) {
+      while (fe < b && text[fe] != sep) ++fe;
+      if (fe > cur) {
+        present = true;
+      } else if (a == b) {
+        present = want == 0;
+      } else {  // an empty field counts only when a later field is not empty
+        for (int64_t p = fe; p < b; ++p)
+          if (text[p] != sep) {
+            present = true;
+            break;
+          }
+      }
+    }
+    const int32_t kind = sp.kind[f];
+    if (kind == IK_STR) {
+      const int64_t p = li * sp.nstr + sp.sidx[f];
+      if (!present) {
+        o.slen[p] = -1;
+        st = 1;  // ArrayIndexOutOfBounds: the host reports it
+        continue;
+      }
+      const char* q = text_at(text, cur);
+      const int64_t len = fe - cur;
+      o.spos[p] = cur;
+      o.slen[p] = (int32_t)len;
+      o.sjh[p] = java_hash_utf8(q, len);
+      o.shash[p] = text_hash64(q, len);
+      continue;
+    }
+    if (!present) {
+      st = 1;
+      continue;
+    }
+    const char* q = text_at(text, cur);
+    const int64_t len = fe - cur;
+    int64_t v = 0;
+    bool ok = true;
+    switch (kind) {
+      case IK_DOUBLE: {
+        double d;
+        ok = fast_parse_double(q, len, &d);
+        v = (int64_t)f64_bits(d);
+        break;
+      }
+      case IK_LONG:
+      case IK_RAW_LONG:
+        ok = parse_long_ascii(q, len, INT64_MIN, INT64_MAX, &v) == 0;
+        break;
+      case IK_INT:
+        ok = parse_long_ascii(q, len, INT32_MIN, INT32_MAX, &v) == 0;
+        break;
+      case IK_TS_INTSEC:
+      case IK_TS_MS:
+      case IK_ISO_SEC: {
+        int64_t es = 0, ms = 0;
+        ok = iso_local_datetime(q, len, sp.offset_s, &es, &ms);
+        v = kind == IK_TS_MS ? es * 1000 + ms
+            : kind == IK_ISO_SEC ? (int64_t)(int32_t)(uint32_t)(uint64_t)es
+                                 : (int64_t)(int32_t)(uint32_t)(uint64_t)es * 1000;  // (int) quirk
+        break;
+      }
+      default: ok = false;
+    }
+    if (!ok) {
+      st = 1;
+      continue;
+    }
+    o.cols[(int64_t)f * n + li] = v;
+    if (f == sp.ts_col) *ts_val = v;
+  }
+  return st;
+}
+
 // One workgroup per tile of 256 lines: the tile's bytes are staged into LDS (line_tile.h), every
 // thread splits and parses its line there, then probes the dictionary for its string fields.
 template <class Text>
@@ -60,7 +168,7 @@ __device__ __forceinline__ void ingest_one_line(Text text, const char* __restric
   if (b > a && text[b - 1] == '\n') --b;  // the last line of a batch ending in '\n'
   if (b > a && text[b - 1] == '\r') --b;  // SocketTextStreamFunction strips a trailing '\r'
   int64_t ts = INT64_MIN;
-  const uint8_t st = ingest_line(text, a, b, li, n, sp, o, &ts);
+  const uint8_t st = ingest_line_dev(text, a, b, li, n, sp, o, &ts);
   o.status[li] = st;
   *local_flag += st;
   if (!st && ts > *local_max) *local_max = ts;
@@ -73,8 +181,10 @@ __device__ __forceinline__ void ingest_one_line(Text text, const char* __restric
       const uint64_t h = o.shash[p];
       uint32_t q = dict_home(h, d.mask);
       for (uint32_t i = 0; i <= d.mask; ++i) {
-        const uint64_t k = __hip_atomic_load(&d.tab_h[q], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
+        // A plain (L1-cacheable) load: slots only go 0 -> hash, so a stale 0 just sends this
+        // thread to the CAS below, which returns the slot's hash; an agent-scope load went to
+        // L2 for every string of every line.
+        const uint64_t k = d.tab_h[q];
         if (k == h) {
           slot = (int32_t)q;
           break;
@@ -99,10 +209,18 @@ __device__ __forceinline__ void ingest_one_line(Text text, const char* __restric
   }
 }
 
+// 16 KB tiles (256 lines of up to ~60 bytes): eight 256-thread workgroups per CU, the 32-wave
+// limit, where the 24 KB tile of line_tile.h allows six. Longer lines go to the global kernel.
+constexpr int kIngestTileBytes = 16 * 1024;
+
+// GLOBAL = false: tiles whose bytes fit the LDS tile, parsed there (the other tiles' workgroups
+// return at once); GLOBAL = true: the launch after it parses only the tiles that did not fit,
+// from global memory. Two kernels instead of both paths in one keep each one's code small.
+template <bool GLOBAL>
 __global__ __launch_bounds__(256) void ingest_parse_kernel(
     const char* __restrict__ text, int64_t text_len, const int64_t* __restrict__ starts,
     int64_t n, IngestSpec sp, IngestOut o, DictState d) {
-  __shared__ __attribute__((aligned(16))) char tile[kTileLdsBytes];
+  __shared__ __attribute__((aligned(16))) char tile[GLOBAL ? 16 : kIngestTileBytes];
   int64_t local_max = INT64_MIN;
   uint32_t local_flag = 0;
   const int64_t l0 = (int64_t)blockIdx.x * kTileLines;
@@ -110,22 +228,54 @@ __global__ __launch_bounds__(256) void ingest_parse_kernel(
   const int64_t lo = starts[l0];
   int64_t hi = l1 < n ? starts[l1] : text_len;
   if (hi > text_len) hi = text_len;
-  const LdsText lt = stage_line_tile(text, lo, hi, tile, kTileLdsBytes);
+  if (tile_fits_lds(text, lo, hi, kIngestTileBytes) == GLOBAL) return;  // workgroup-uniform
   const int64_t li = l0 + threadIdx.x;
-  if (li < l1) {
-    if (lt.p != nullptr)
-      ingest_one_line(lt, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag);
-    else
-      ingest_one_line(text, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag);
+  if constexpr (GLOBAL) {
+    if (li < l1) ingest_one_line(text, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag);
+  } else {
+    const LdsText lt = stage_line_tile(text, lo, hi, tile, kIngestTileBytes);
+    if (li < l1) ingest_one_line(lt, text, text_len, starts, n, li, sp, o, d, &local_max, &local_flag);
   }
-  // One atomic per wave for the flag count and the max timestamp.
+  // The workgroup's flag count and max timestamp: the max goes to its tile slot (reduced by
+  // tile_max_reduce_kernel), the flag count -- rare -- straight to the counter.
+  __shared__ int64_t s_max[kTileLines / 64];
+  __shared__ uint32_t s_fl[kTileLines / 64];
   local_max = wave_max_i64(local_max);
   uint32_t fl = local_flag;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) fl += __shfl_xor(fl, off, 64);
   if ((threadIdx.x & 63) == 0) {
-    if (fl) atomicAdd(o.nflag, fl);
-    if (local_max != INT64_MIN) atomicMax((long long*)o.maxts, (long long)local_max);
+    s_max[threadIdx.x >> 6] = local_max;
+    s_fl[threadIdx.x >> 6] = fl;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t m = INT64_MIN;
+    uint32_t f = 0;
+    for (int w = 0; w < kTileLines / 64; ++w) {
+      m = s_max[w] > m ? s_max[w] : m;
+      f += s_fl[w];
+    }
+    if (f) atomicAdd(o.nflag, f);
+    if (o.tile_max)
+      o.tile_max[blockIdx.x] = m;
+    else if (m != INT64_MIN)
+      atomicMax((long long*)o.maxts, (long long)m);
+  }
+}
+
+// Max of the per-tile maxima into the batch maximum (one workgroup, one atomic).
+__global__ __launch_bounds__(1024) void tile_max_reduce_kernel(const int64_t* __restrict__ tile_max,
+                                                               int64_t tiles, int64_t* maxts) {
+  __shared__ int64_t s_w[16];
+  int64_t m = INT64_MIN;
+  for (int64_t t = threadIdx.x; t < tiles; t += blockDim.x) m = tile_max[t] > m ? tile_max[t] : m;
+  m = wave_max_i64(m);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 0; w < 16; ++w) m = s_w[w] > m ? s_w[w] : m;
+    if (m != INT64_MIN) atomicMax((long long*)maxts, (long long)m);
   }
 }
 
@@ -371,9 +521,17 @@ void ingest_parse(const char* text, int64_t text_len, const int64_t* starts, int
   if (sp.nfields < 1 || sp.nfields > kIngestMaxFields) throw std::invalid_argument("ingest: fields");
   const int64_t tiles = (n + kTileLines - 1) / kTileLines;
   if (tiles > INT32_MAX) throw std::invalid_argument("ingest: batch too large");
-  hipLaunchKernelGGL(ingest_parse_kernel, dim3((uint32_t)tiles), dim3(kTileLines), 0,
+  hipLaunchKernelGGL(ingest_parse_kernel<false>, dim3((uint32_t)tiles), dim3(kTileLines), 0,
                      (hipStream_t)stream, text, text_len, starts, n, sp, o, d);
   ING_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(ingest_parse_kernel<true>, dim3((uint32_t)tiles), dim3(kTileLines), 0,
+                     (hipStream_t)stream, text, text_len, starts, n, sp, o, d);
+  ING_CHECK(hipGetLastError());
+  if (o.tile_max) {
+    hipLaunchKernelGGL(tile_max_reduce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream,
+                       o.tile_max, tiles, o.maxts);
+    ING_CHECK(hipGetLastError());
+  }
 }
 
 void dict_find_new(int64_t n, int32_t nstr, const IngestOut& o, const DictState& d,

@@ -26,6 +26,13 @@ struct LdsText {
 };
 __device__ __forceinline__ const char* text_at(const LdsText& t, int64_t i) { return t.p + (i - t.base); }
 
+// Bytes [lo, hi) of `text` fit an LDS tile of `cap` bytes (stage_line_tile's condition).
+__device__ __forceinline__ bool tile_fits_lds(const char* text, int64_t lo, int64_t hi, int cap) {
+  const int64_t nb = hi - lo;
+  const int pad = (int)((uintptr_t)(text + lo) & 15);
+  return nb > 0 && nb + pad <= cap;
+}
+
 // Stage bytes [lo, hi) of `text` into `lds` (16-byte aligned, cap bytes): unaligned head and
 // tail bytes one per thread, the aligned body as 16-byte loads/stores. Returns the LdsText view,
 // or p == nullptr when the range does not fit (the caller parses from global memory). Every

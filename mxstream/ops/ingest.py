@@ -380,7 +380,8 @@ class TextIngest:
                "sjh": self._buf("sjh", np_, torch.int32).data_ptr(),
                "sslot": self._buf("sslot", np_, torch.int32).data_ptr(),
                "shash": self._buf("shash", np_, torch.int64).data_ptr(),
-               "nflag": ctl[0:1].data_ptr(), "maxts": ctl[1:2].data_ptr()}
+               "nflag": ctl[0:1].data_ptr(), "maxts": ctl[1:2].data_ptr(),
+               "tile_max": self._buf("tilemax", (n + 255) // 256, torch.int64).data_ptr()}
         ds = self.dict.state()
         m.ingest_parse(self.cuda, buf.data_ptr(), nbytes, starts.data_ptr(), n, self._spec, out,
                        ds, st)
