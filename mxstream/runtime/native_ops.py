@@ -97,7 +97,10 @@ class _ColumnInput:
                 raise TypeError("mixed key types")
             if cb.strings is not self.dict:
                 known = self.dict.strings() if len(self.dict) else []
-                if not self.templates and cb.strings.strings()[:len(known)] == known:
+                # (an empty dictionary needs no comparison: reading the parser's names back
+                # would wait for the device -- a 7 ms stall in the first step of config 7)
+                if not self.templates and (not known
+                                           or cb.strings.strings()[:len(known)] == known):
                     # the parser's dictionary (after a restore: the same strings, same ids)
                     self.dict = cb.strings
                 else:
