@@ -36,7 +36,8 @@ from ..parallel.comm import Comm, LocalComm
 # The operator's halves (mixins) and the names other modules import from here.
 from .host_rows import (CountedHostRows, PinnedSlabPool, _event_spin, _host_wait,  # noqa: F401
                         _next_pow2, to_host_arrays)
-from .window_agg import _FORCE_SPLIT, _AggMixin
+from . import window_agg as _wa
+from .window_agg import _AggMixin
 from .window_fire import _FireMixin
 from .window_state import _StateMixin
 from .window_tiering import _TierMixin
@@ -729,8 +730,8 @@ class KeyedWindowOperator(_AggMixin, _FireMixin, _TierMixin, _StateMixin):
                 # Hot keys: a sub-table holding more than AGG_SLICE records is shared by several
                 # workgroups (the launcher applies it where the atomic merge is exact).
                 aplan.split = min(64, max(1, -(-b.maxb // K.AGG_SLICE))) if not combined else 1
-                if _FORCE_SPLIT > 1 and aplan.split == 1 and not combined:
-                    aplan.split = -_FORCE_SPLIT  # every sub-table over this many workgroups (A/B)
+                if _wa._FORCE_SPLIT > 1 and aplan.split == 1 and not combined:
+                    aplan.split = -_wa._FORCE_SPLIT  # every sub-table over n workgroups (A/B)
                 if self.dlist is not None:
                     aplan.dlist, aplan.dlist_n = self.dlist.data_ptr(), self.dlist_n.data_ptr()
                     aplan.slot_mark = self.slot_mark.data_ptr()

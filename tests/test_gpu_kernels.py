@@ -755,3 +755,27 @@ def test_hashed_narrow_steps_over_wide_table_keys_equal_cpu(gpu_device):
         out += op.finish()
         res[d.type] = _results(out)
     assert res["cuda"] == res["cpu"]
+
+
+@pytest.mark.parametrize("split", [2, 4])
+def test_forced_agg_split_equals_default(gpu_device, split, monkeypatch):
+    """MXS_AGG_FORCE_SPLIT (A/B knob): every dense sub-table folded by `split` workgroups whose
+    partial sums merge with atomics (and the packed accumulators each share allows) gives the
+    same windows as one workgroup per sub-table."""
+    import mxstream.runtime.window_agg as WA
+
+    res = {}
+    for n_split in (0, split):
+        monkeypatch.setattr(WA, "_FORCE_SPLIT", n_split)
+        op = KeyedWindowOperator(size=2000, agg=K.AGG_SUM_I64, device=gpu_device,
+                                 max_keys=1 << 16, batch_capacity=1 << 18, ooo_bound=300,
+                                 dense_keys=True)
+        out = []
+        for step in range(4):
+            keys, ts, vals = _gen(gpu_device, 1 << 18, 1 << 16, span=2500, disorder=300,
+                                  seed=21 + step)
+            ts += step * 2500
+            out += op.process(keys, ts, vals)
+        out += op.finish()
+        res[n_split] = _results(out)
+    assert res[0] == res[split]
