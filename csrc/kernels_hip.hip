@@ -4677,11 +4677,14 @@ static void launch_agg_d(const Rec* recs, const uint32_t* counts, const AggPlan&
   if constexpr (AGG == AGG_SUM_I64 || AGG == AGG_AVG_I64) {
     if (agg_pack_ok(p)) {
       const size_t lds_pk = keys_lds + (size_t)p.pg * cap * 8 + 16 + list_lds;
-      // default 2: the 64-VGPR build (two workgroups per CU: hashed 1M-key step 135 -> 119 us)
-      static const int v = [] {
+      // Default: the 64-VGPR build (V = 2) when two workgroups' LDS images fit a CU -- that is
+      // what its register cap buys (hashed 1M-key step 135 -> 119 us); otherwise the default
+      // build (its larger write-back batches). MXS_AGG_V forces a variant (A/B).
+      static const int v_env = [] {
         const char* e = std::getenv("MXS_AGG_V");
-        return e ? std::atoi(e) & 3 : 2;
+        return e ? std::atoi(e) & 3 : -1;
       }();
+      const int v = v_env >= 0 ? v_env : (2 * (lds_pk + 512) <= 160 * 1024 ? 2 : 0);
       if (p.rec_words == 1) {
         switch (v) {
           case 1: launch_agg_v<AGG, 1, true, DENSE, false, 1>(recs, counts, p, keys_g, acc_g, cnt_g,

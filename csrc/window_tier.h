@@ -764,12 +764,13 @@ class WindowTierCore {
     c.dirty.clear();
     spare_.push_back(std::move(c));
   }
-  // After an absorb of n rows: unless a spare already holds 1.25 n rows, a background thread
-  // maps and touches the columns of the next one (the next eviction is of similar size), so the
-  // page faults run beside the stream's next steps instead of inside the next absorb.
+  // After an absorb of n rows: unless a spare already holds 2 n rows, a background thread maps
+  // and touches the columns of the next one, so the page faults run beside the stream's next
+  // steps instead of inside the next absorb. Evictions grow with the key space: a 1.25 n spare
+  // was outgrown often enough to leave 10 ms absorbs in config 4-spill.
   void prefault_async(size_t n) {
     if (!prefault_) return;
-    const size_t want = n + n / 4;
+    const size_t want = 2 * n;
     {
       std::lock_guard<std::mutex> g(sp_mu_);
       for (auto& sp : spare_)
