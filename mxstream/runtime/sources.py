@@ -327,6 +327,7 @@ class TextFileSource(Source):
         self._dcap = (chunk + (2 << 20) - 1) & ~((2 << 20) - 1)  # device chunk buffers
         self._pin = torch.cuda.is_available()
         threads = min(16, max(1, __import__("os").cpu_count() or 1))
+        threads = int(__import__("os").environ.get("MXS_READ_THREADS", threads))  # (A/B)
         self._cstream = None
         if self.ring_device is not None and str(self.ring_device).startswith("cuda") \
                 and torch.cuda.is_available():
