@@ -224,6 +224,12 @@ class ShardedCore {
   }
   bool contains(uint64_t key) const { return sh_[shard_of(key)]->contains(key); }
   bool hot(uint64_t key) const { return sh_[shard_of(key)]->hot(key); }
+  // No shard holds hot (in-memory, not cold-chunk) sessions.
+  bool hot_free() const {
+    for (auto& s : sh_)
+      if (!s->hot_free()) return false;
+    return true;
+  }
   size_t num_keys() const {
     size_t t = 0;
     for (auto& s : sh_) t += s->num_keys();

@@ -50,6 +50,14 @@ template <class T>
 py::array_t<T> to_np(const std::vector<T>& v) {
   return py::array_t<T>((py::ssize_t)v.size(), v.data());
 }
+// The vector's buffer handed to NumPy without a copy (the array owns it through a capsule).
+template <class T>
+py::array_t<T> to_np_move(std::vector<T>&& v) {
+  if (v.empty()) return py::array_t<T>(0);
+  auto* h = new std::vector<T>(std::move(v));
+  py::capsule own(h, [](void* p) { delete static_cast<std::vector<T>*>(p); });
+  return py::array_t<T>((py::ssize_t)h->size(), h->data(), own);
+}
 
 py::dict columns_dict(const sess::Columns& c) {
   py::dict d;
@@ -372,12 +380,13 @@ class SessionStore {
       // the device spill set: dropped from the list here, under the store lock.
       py::gil_scoped_release nogil;
       std::lock_guard<std::mutex> g(mu_);
-      for (auto& d : done) {
-        size_t w = 0;
-        for (int64_t k : d.released)
-          if (!c_.hot((uint64_t)k)) d.released[w++] = k;
-        d.released.resize(w);
-      }
+      if (!c_.hot_free())  // (no hot sessions at all -- the common case: nothing to drop)
+        for (auto& d : done) {
+          size_t w = 0;
+          for (int64_t k : d.released)
+            if (!c_.hot((uint64_t)k)) d.released[w++] = k;
+          d.released.resize(w);
+        }
     }
     py::list out;
     std::exception_ptr err;
@@ -388,7 +397,7 @@ class SessionStore {
       r["nr"] = d.nr;
       r["ne"] = d.ne;
       r["nk"] = d.nk;
-      r["released"] = to_np(d.released);
+      r["released"] = to_np_move(std::move(d.released));
       r["t_wait"] = d.t_wait;
       r["t_hot"] = d.t_hot;
       r["t_build"] = d.t_build;
