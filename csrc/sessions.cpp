@@ -238,15 +238,15 @@ class SessionStore {
       c_.fire(wm, sess::SessionCore::prog(map_code.data(), map_code.size(), map_consts.data(), map_consts.size()),
            sess::SessionCore::prog(f_code.data(), f_code.size(), f_consts.data(), f_consts.size()), o, expire);
     }
-    py::dict d;
-    d["keys"] = to_np(o.okey);
-    d["start"] = to_np(o.ostart);
-    d["end"] = to_np(o.oend);
-    d["values"] = to_np(o.oval);
-    d["raw"] = to_np(o.oraw);
-    d["counts"] = to_np(o.ocnt);
-    d["refire"] = to_np(o.oref);
-    d["released"] = to_np(o.released);
+    py::dict d;  // the columns' buffers handed over, not copied
+    d["keys"] = to_np_move(std::move(o.okey));
+    d["start"] = to_np_move(std::move(o.ostart));
+    d["end"] = to_np_move(std::move(o.oend));
+    d["values"] = to_np_move(std::move(o.oval));
+    d["raw"] = to_np_move(std::move(o.oraw));
+    d["counts"] = to_np_move(std::move(o.ocnt));
+    d["refire"] = to_np_move(std::move(o.oref));
+    d["released"] = to_np_move(std::move(o.released));
     return d;
   }
   // Cold-chunk expiry alone (GIL released).
