@@ -62,6 +62,10 @@ def main() -> int:
                          "aggregation (partial accumulators cross one all-to-all per fired "
                          "window), records = every step's (key, pane)-combined records cross the "
                          "all-to-all to the key's owner (hashed state); auto = partials")
+    ap.add_argument("--device-warmup-ms", type=float, default=0.0,
+                    help="before the warm-up steps: keep the GPU busy with the synthetic source "
+                         "for this long, so its clocks are at their sustained level when the "
+                         "warm-up steps start (reported in the JSON)")
     ap.add_argument("--no-records-figure", action="store_true",
                     help="G > 1: skip the per-event-exchange (records) run reported next to it")
     a = ap.parse_args()
@@ -109,8 +113,13 @@ def main() -> int:
         if device.type == "cuda":
             torch.cuda.synchronize(device)
 
+    dev_warm = bench.device_warmup(a.device_warmup_ms) if a.device_warmup_ms > 0 else 0.0
     for _ in range(a.warmup):
         bench.step()
+    # The warm-up steps complete before the clock starts: the pipelined operator's pending state
+    # half of the last warm-up step is applied here, so the timed region holds exactly K
+    # partitions and K state halves (the last one drained below).
+    bench.drain()
     sync()
     comm.barrier()
     sync()
@@ -137,7 +146,7 @@ def main() -> int:
         if wd is not None:
             wd.beat()
     # Pipelined: the last step's state half (aggregation, firing) runs inside the timed region
-    # too, so K timed steps = K partitions + K+1 state halves (never less work than K steps).
+    # too, so K timed steps = K partitions + K state halves.
     bench.drain()
     if step_t is not None:
         step_t.append(time.perf_counter())
@@ -197,6 +206,7 @@ def main() -> int:
         xb = TumblingWindowBench(xcfg, comm, device)
         for _ in range(a.warmup):
             xb.step()
+        xb.drain()
         sync()
         comm.barrier()
         sync()
@@ -255,6 +265,7 @@ def main() -> int:
             "firings_for_latency": int(lt[2].item()),
             "alerts": int(al.item()),
             "late_dropped": op_metrics.num_late_records_dropped,
+            "device_warmup_ms": round(dev_warm, 1),
             # untimed extra runs, NOT the headline: the same job on hashed keyed state, and
             # (G > 1) with the per-event records exchange instead of local-global partials
             **(hashed or {}),

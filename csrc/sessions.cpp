@@ -23,6 +23,7 @@
 // Micro-batch semantics (shared with the GPU kernels): a batch's elements of one key are merged
 // in timestamp order; a run of elements closer than `gap` becomes one candidate session, which
 // is dropped as late only if it is late on its own and merges with no live session.
+#include <cstdio>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -202,11 +203,19 @@ class SessionStore {
     const auto r = c_.extract_rows_into(keys.data(), keys.size(), wm, max_sess, gap,
                                         reinterpret_cast<int64_t*>(rows), cap,
                                         reinterpret_cast<int64_t*>(moved), moved_cap);
-    // the promote kernel writes record `position` of a slot: never past the slot's kSess
+    // The promote kernel writes record `position` of a slot: never past the slot's kSess. Both
+    // extract paths bound a key's sessions by max_sess BEFORE the key leaves the store
+    // (take_indexed_with's limit; extract() keeps a key with more on the host), so this is an
+    // invariant: a violation means the store is already inconsistent, and the keys are gone --
+    // no exception could hand the state back, so it stops the process (an assertion).
     const int64_t* w = reinterpret_cast<const int64_t*>(rows);
     for (int64_t i = 0; i < std::get<0>(r); ++i)
-      if (w[i * 8 + 7] > max_sess || w[i * 8 + 6] >= w[i * 8 + 7])
-        throw std::logic_error("extract_rows_into: session position out of range");
+      if (w[i * 8 + 7] > max_sess || w[i * 8 + 6] >= w[i * 8 + 7]) {
+        std::fprintf(stderr, "mxstream: extract_rows_into: session position out of range "
+                             "(row %lld: %lld of %lld, max %lld)\n", (long long)i,
+                     (long long)w[i * 8 + 6], (long long)w[i * 8 + 7], (long long)max_sess);
+        std::abort();
+      }
     return r;
   }
   // The dense cold-row index's counters (csrc/session_store.h IndexStats) summed over shards.
@@ -318,8 +327,11 @@ class SessionStore {
       if (!j.ev && hipEventCreateWithFlags(&j.ev, hipEventDisableTiming | hipEventBlockingSync) !=
                        hipSuccess)
         throw std::runtime_error("spill_submit: hipEventCreate failed");
-      if (hipEventRecord(j.ev, reinterpret_cast<hipStream_t>(stream)) != hipSuccess)
+      if (hipEventRecord(j.ev, reinterpret_cast<hipStream_t>(stream)) != hipSuccess) {
+        std::lock_guard<std::mutex> g(qmu_);
+        free_ev_.push_back(j.ev);  // the event goes back to the pool, not leaked
         throw std::runtime_error("spill_submit: hipEventRecord failed");
+      }
     }
     std::lock_guard<std::mutex> g(qmu_);
     if (!th_.joinable()) th_ = std::thread([this] { worker(); });

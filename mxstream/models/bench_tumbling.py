@@ -112,6 +112,23 @@ class TumblingWindowBench:
         self.step_idx += 1
         return self._account(fired)
 
+    def device_warmup(self, ms: float) -> float:
+        """Keep the GPU busy with the synthetic source's kernel (no operator state touched) for
+        `ms` milliseconds of wall time, so clocks reach their sustained level before the
+        warm-up steps; returns the time spent (ms)."""
+        if self.device.type != "cuda":
+            return 0.0
+        cfg = self.cfg
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < ms:
+            for _ in range(4):
+                K.gen_events(self.keys, self.ts, self.vals, seed=cfg.seed + 1,
+                             stream_id=self.comm.rank, idx0=0, nkeys=cfg.keys, ts_base=0,
+                             ts_span=cfg.step_span_ms, disorder=cfg.disorder_ms, val_lo=0,
+                             val_span=cfg.val_max, zipf=cfg.zipf)
+            torch.cuda.synchronize(self.device)
+        return (time.perf_counter() - t0) * 1e3
+
     def drain(self) -> int:
         """Run the pending state half (pipelined mode) and collect every queued firing."""
         return self._account(self.op.flush())

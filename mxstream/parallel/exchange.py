@@ -55,11 +55,14 @@ def exchange_rows(comm, dest: torch.Tensor, cols: list[torch.Tensor]) -> list[to
                           flags.data_ptr(), st)
     else:
         m.cpu_xrows_count(dest.data_ptr(), n, world, counts.data_ptr(), flags.data_ptr())
-    mx = counts.max().to(torch.int64).reshape(1)
+    # [largest per-destination count, bad-destination flag]: one MAX all-reduce, so a bad
+    # destination on any rank is seen by every rank before the payload exchange (all raise
+    # together instead of the others blocking in the all-to-all).
+    mx = torch.stack([counts.max().to(torch.int64), flags[0].to(torch.int64)])
     comm.allreduce_max_(mx)
     rc = torch.empty_like(counts)
     comm.all_to_all(rc, counts)
-    h = torch.cat([mx, flags.to(torch.int64), rc.to(torch.int64)]).cpu().tolist()  # one read
+    h = torch.cat([mx, rc.to(torch.int64)]).cpu().tolist()  # one read
     if h[1]:
         raise ValueError("exchange_rows: a destination rank outside [0, world)")
     cap = int(h[0])

@@ -460,11 +460,17 @@ def write_host_checkpoint(d: Path, *, job_id: str, checkpoint_id: int, states: d
 
 
 def read_host_checkpoint(path: str | os.PathLike, rank: int = 0, world: int = 1,
-                         parallelism: int | None = None,
-                         max_parallelism: int = 128) -> tuple[dict, dict[str, dict]]:
+                         parallelism: int | None = None, max_parallelism: int = 128,
+                         node_parallelism: dict[str, int] | None = None
+                         ) -> tuple[dict, dict[str, dict]]:
     """Metadata (with this rank's ``extra``) and this rank's operator states. At the world size
     that wrote the checkpoint every rank reads its own files; at another world size every rank
-    reads all of them and keeps the key groups it now owns (rescale_host_state)."""
+    reads all of them and keeps the key groups it now owns (rescale_host_state).
+
+    node_parallelism: uid -> the operator's own parallelism where it differs from the
+    environment's (``set_parallelism``): the executor routes a key with the parallelism of its
+    node (executor.py ``_exchange``), so each operator's owned key-group range is computed with
+    that node's parallelism, not one range for every operator."""
     from .statecodec import read_state
 
     d = Path(path)
@@ -480,8 +486,13 @@ def read_host_checkpoint(path: str | os.PathLike, rank: int = 0, world: int = 1,
         states = {nid: read_state(d / name) for nid, name in per_rank[rank].items()}
         return dict(meta, extra=extras[rank]), states
     old = [{nid: read_state(d / name) for nid, name in files.items()} for files in per_rank]
-    lo, hi = owned_key_groups(rank, world, parallelism or world, max_parallelism)
-    states = {nid: rescale_host_state([o[nid] for o in old], rank, world, (lo, hi),
+    node_parallelism = node_parallelism or {}
+
+    def kg_range(nid: str) -> tuple[int, int]:
+        return owned_key_groups(rank, world, node_parallelism.get(nid) or parallelism or world,
+                                max_parallelism)
+
+    states = {nid: rescale_host_state([o[nid] for o in old], rank, world, kg_range(nid),
                                       max_parallelism)
               for nid in per_rank[0]}
     return dict(meta, extra=rescale_extra(extras, rank, world)), states

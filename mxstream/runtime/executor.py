@@ -480,8 +480,10 @@ class Executor:
         from .checkpoint import read_host_checkpoint
 
         rank, world = (self.comm.rank, self.comm.world) if self.comm is not None else (0, 1)
-        meta, states = read_host_checkpoint(path, rank, world, self.env.parallelism,
-                                            self.env.max_parallelism)
+        meta, states = read_host_checkpoint(
+            path, rank, world, self.env.parallelism, self.env.max_parallelism,
+            node_parallelism={self._uid(nd): nd.parallelism for nd in self.nodes
+                              if nd.parallelism})
         names = meta["extra"]["nodes"]
         for nd in self.nodes:
             key = self._uid(nd)

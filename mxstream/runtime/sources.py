@@ -42,6 +42,14 @@ class Source:
 
     # Replayable sources report their read position in checkpoints and seek back to it on
     # restore (Flink's source offsets). Non-replayable ones (socket) return {}.
+    #
+    # Rank-strided sources (global item i on rank i % G) keep, after a restore at another world
+    # size, the old layout's positions they were re-split from (`_prior`): a later checkpoint
+    # stores them next to its own positions, so the set of items emitted before it is exact
+    # after any number of rescales -- a same-size restore re-applies the filter, a further
+    # rescale chains it.
+    _prior: list | None = None
+
     def snapshot(self) -> dict:
         pos = getattr(self, "pos", None)
         return {} if pos is None else {"pos": pos, "rescale": self._rescale_info()}
@@ -50,10 +58,14 @@ class Source:
         if "rescaled" in snap:
             self.restore_rescaled(snap["rescaled"])
         elif "pos" in snap:
+            prior = snap.get("rescale", {}).get("prior")
+            if prior is not None:
+                self.restore_rescaled(prior)  # the re-split layout the positions index into
             self.pos = snap["pos"]
 
     def _rescale_info(self) -> dict:
-        return {"rank": self.rank, "world": self.world, "pos": getattr(self, "pos", None)}
+        return {"rank": self.rank, "world": self.world, "pos": getattr(self, "pos", None),
+                "prior": self._prior}
 
     def restore_rescaled(self, old: list[dict]) -> None:
         """Resume from a checkpoint written at another world size: `old` = every old rank's
@@ -61,13 +73,19 @@ class Source:
         raise ValueError(f"{self.name}: no restore at a different world size")
 
     @staticmethod
-    def _consumed(old: list[dict]):
-        """Global index i of a rank-strided source (index i on rank i % G at position i // G)
-        was emitted before the checkpoint iff i // G < pos of that old rank."""
+    def _consumed(old: list[dict], n_items: int):
+        """Predicate over global item indices: emitted before the checkpoint whose ranks'
+        positions are `old`. Old rank r's items were the indices i = r (mod G) that its own
+        prior layout had not emitted, in order; it emitted the first `pos` of them."""
         g = len(old)
-        pos = [o["pos"] for o in sorted(old, key=lambda o: o["rank"])]
-        return lambda i: i // g < pos[i % g]
-
+        old = sorted(old, key=lambda o: o["rank"])
+        prior = [o.get("prior") for o in old]
+        before = Source._consumed(prior[0], n_items) if prior[0] is not None else None
+        bound = []
+        for r, o in enumerate(old):
+            idx = [i for i in range(r, n_items, g) if before is None or not before(i)]
+            bound.append(idx[o["pos"]] if o["pos"] < len(idx) else n_items)
+        return lambda i: (before is not None and before(i)) or i < bound[i % g]
 
 class CollectionSource(Source):
     name = "Collection Source"
@@ -89,13 +107,14 @@ class CollectionSource(Source):
             self.timestamps = [self.timestamps[i] for i in idx]
 
     def restore_rescaled(self, old):
-        done = self._consumed(old)
         values, ts = self._all
+        done = self._consumed(old, len(values))
         idx = [i for i in range(self.rank, len(values), self.world) if not done(i)]
         self.values = [values[i] for i in idx]
         if ts is not None:
             self.timestamps = [ts[i] for i in idx]
         self.pos = 0
+        self._prior = old
 
     def poll(self, now):
         if self.pos >= len(self.values):
@@ -391,14 +410,15 @@ class TextFileSource(Source):
         if self.columnar or self.lines is None:
             raise ValueError("text file source: the columnar reader's byte ranges cannot be "
                              "re-split at another world size")
-        done = self._consumed(old)
         with open(self.path, "r", encoding="utf-8") as f:
             lines = f.read().split("\n")
         if lines and lines[-1] == "":
             lines.pop()
         lines = [l[:-1] if l.endswith("\r") else l for l in lines]
+        done = self._consumed(old, len(lines))
         self.lines = [lines[i] for i in range(self.rank, len(lines), self.world) if not done(i)]
         self.pos = 0
+        self._prior = old
 
     def restore(self, snap: dict) -> None:
         if self.columnar and "bpos" in snap:
@@ -566,19 +586,29 @@ class SequenceSource(Source):
 
     def snapshot(self) -> dict:
         return {"cur": self.cur, "rescale": {"rank": self.rank, "world": self.world,
-                                             "cur": self.cur}}
+                                             "cur": self.cur, "prior": self._prior}}
 
     def restore(self, snap: dict) -> None:
         if "rescaled" in snap:
             self.restore_rescaled(snap["rescaled"])
         else:
+            prior = snap.get("rescale", {}).get("prior")
+            if prior is not None:
+                self.restore_rescaled(prior)  # keep skipping what the older layout emitted
             self.cur = snap.get("cur", self.cur)
 
-    def restore_rescaled(self, old):
-        # old rank r emitted start + r, start + r + G, ... below its cursor
+    def _emitted(self, old: list[dict]):
+        """Predicate: value x was emitted under the layout `old` (old rank r emitted its values
+        start + r, start + r + G, ... below its cursor, except those its prior layout had)."""
         g = len(old)
-        cur = [o["cur"] for o in sorted(old, key=lambda o: o["rank"])]
-        self._skip = lambda x: x < cur[(x - self.start) % g]
+        old = sorted(old, key=lambda o: o["rank"])
+        cur = [o["cur"] for o in old]
+        before = self._emitted(old[0]["prior"]) if old[0].get("prior") is not None else None
+        return lambda x: (before is not None and before(x)) or x < cur[(x - self.start) % g]
+
+    def restore_rescaled(self, old):
+        self._skip = self._emitted(old)
+        self._prior = old
         self.cur = self.start + self.rank
 
     def poll(self, now):

@@ -311,3 +311,81 @@ def test_host_checkpoint_restores_at_another_world_size(tmp_path, old_world, new
     assert 0 < len(after) < len(ref)
     assert len(c_ref) > 20 and set(c_got) == set(c_ref)
     assert all(c_got[k] >= v for k, v in c_ref.items())
+
+
+def _drain_source(src, k):
+    """Poll up to k items (k=None: all) from a source; returns the values."""
+    got = []
+    while k is None or len(got) < k:
+        items, done = src.poll(0)
+        got.extend(r.value for r in items)
+        if done:
+            break
+    return got
+
+
+@pytest.mark.parametrize("kind", ["collection", "sequence"])
+def test_source_rescale_survives_later_checkpoints(kind):
+    """A rescale restore's re-split is kept in later snapshots: world 2 -> 3 (rescale) ->
+    checkpoint -> restore at 3 (same size) -> checkpoint -> restore at 2 (rescale again). Every
+    item is emitted exactly once over the four runs (no replays folded twice into state)."""
+    from mxstream.runtime.checkpoint import rescale_host_state
+    from mxstream.runtime.sources import CollectionSource, SequenceSource
+
+    n = 97
+
+    def make():
+        return (CollectionSource(list(range(n)), batch_size=3) if kind == "collection"
+                else SequenceSource(0, n - 1, batch_size=3))
+
+    def run(world, snaps, take):
+        out, new = [], []
+        for r in range(world):
+            s = make()
+            s.open(r, world, None)
+            if snaps is not None:
+                old_world = len(snaps)
+                snap = (snaps[r] if old_world == world
+                        else rescale_host_state(snaps, r, world, (0, 127), 128))
+                s.restore(snap)
+            out += _drain_source(s, take[r] if isinstance(take, list) else take)
+            new.append(s.snapshot())
+        return out, new
+
+    emitted, snaps = run(2, None, [30, 2])  # uneven: the re-split leaves gaps to skip
+    for world, take in ((3, 3), (3, 3), (2, None)):
+        got, snaps = run(world, snaps, take)
+        emitted += got
+    assert sorted(emitted) == list(range(n)), Counter(emitted).most_common(3)
+
+
+def test_rescale_uses_each_operators_own_parallelism(tmp_path):
+    """A keyed operator with its own parallelism (set_parallelism(1): the executor routes every
+    key to rank 0) is re-split at another world size with ITS key-group ranges, not the
+    environment's: all of its state lands on rank 0, where its keys now arrive; an operator at
+    the environment's parallelism is spread by the usual ranges."""
+    from mxstream.runtime.checkpoint import (owned_key_groups, read_host_checkpoint,
+                                             write_host_checkpoint, write_host_states)
+    from mxstream.utils.hashing import key_group
+
+    keys = [f"k{i}" for i in range(40)]
+    ranks = []
+    for r in range(2):  # the old job: world 2, both operators keyed
+        mine = [k for k in keys if owned_key_groups(r, 2, 4, 128)[0] <= key_group(k, 128)
+                <= owned_key_groups(r, 2, 4, 128)[1]]
+        keyed = {}
+        for k in mine:
+            keyed.setdefault(key_group(k, 128), {}).setdefault("v", {})[k] = 1
+        states = {"p1": {"keyed": keyed}, "p4": {"keyed": keyed}}
+        files = write_host_states(tmp_path, states, r)
+        ranks.append({"host_operators": files, "extra": {"clock": None}})
+    write_host_checkpoint(tmp_path, job_id="j", checkpoint_id=1, states={}, extra={}, ranks=ranks)
+
+    got = {}
+    for r in range(4):
+        _, st = read_host_checkpoint(tmp_path, r, 4, 4, 128, node_parallelism={"p1": 1})
+        got[r] = {nid: sorted(k for t in s.get("keyed", {}).values() for k in t["v"])
+                  for nid, s in st.items()}
+    assert got[0]["p1"] == sorted(keys) and all(not got[r]["p1"] for r in (1, 2, 3))
+    assert sorted(k for r in range(4) for k in got[r]["p4"]) == sorted(keys)
+    assert sum(1 for r in range(4) if got[r]["p4"]) > 1
