@@ -265,6 +265,14 @@ DictState make_dict(py::dict d) {
 
 }  // namespace
 
+namespace mxs {
+// The validated expression program, for the other binding units (window_step_bindings.cpp).
+ExprProg expr_program(const std::vector<int32_t>& code, const std::vector<double>& consts) {
+  return make_prog(code, consts);
+}
+}  // namespace mxs
+void bind_window_step(py::module_& m);
+
 PYBIND11_MODULE(_mxs_native, m) {
   m.doc() = "mxstream native engine: gfx950 HIP kernels, C++ CPU twins and host runtime";
   m.attr("REC_BYTES") = (int)sizeof(Rec);
@@ -1216,4 +1224,5 @@ PYBIND11_MODULE(_mxs_native, m) {
   bind_listwin(m);
   bind_window_tier(m);
   bind_window_control(m);
+  bind_window_step(m);
 }

@@ -135,14 +135,14 @@ void step_begin(uint32_t* cursor, int nb, int64_t* stats) {
 }
 
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
-                 int64_t proc_now, int64_t* red, const uint32_t* flags) {
+                 int64_t proc_now, int64_t* red, const uint32_t* flags, int32_t idle) {
   int64_t lm = std::max(local_maxts[0], stats[kStatMaxTs]);
   local_maxts[0] = lm;
   const int64_t wm = event_mode ? (lm == INT64_MIN ? INT64_MIN : lm - bound) : proc_now;
   const int64_t qmax = stats[kStatMaxPane];
   red[0] = qmax == INT64_MIN ? INT64_MAX : -qmax;
   red[1] = stats[kStatMinPane];
-  red[2] = wm;
+  red[2] = idle ? INT64_MAX : wm;
   red[3] = -(stats[kStatOverflow] & 1);
   red[4] = -((stats[kStatOverflow] >> 1) & 1);
   // Record width a value needs: -2 = 24-byte records, -1 = 16-byte records, 0 = as planned.

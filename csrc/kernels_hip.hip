@@ -1089,24 +1089,67 @@ __global__ __launch_bounds__(256) void step_begin_kernel(uint32_t* __restrict__ 
 // a copy of the raw stats for the host (red[8..15]).
 __global__ void step_finish_kernel(const int64_t* __restrict__ stats, int64_t* __restrict__ local_maxts,
                                    int64_t bound, int32_t event_mode, int64_t proc_now,
-                                   int64_t* __restrict__ red, const uint32_t* __restrict__ flags) {
-  if (threadIdx.x != 0) return;
+                                   int64_t* __restrict__ red, const uint32_t* __restrict__ flags,
+                                   int32_t idle, int64_t* __restrict__ host_red) {
+  // One lane per word of the reduced vector (16 words).
+  const int j = threadIdx.x;
+  if (j >= 16) return;
   int64_t lm = local_maxts[0];
   const int64_t bm = stats[kStatMaxTs];
   lm = bm > lm ? bm : lm;
-  local_maxts[0] = lm;
+  if (j == 0) local_maxts[0] = lm;
   const int64_t wm = event_mode ? (lm == INT64_MIN ? INT64_MIN : lm - bound) : proc_now;
-  const int64_t qmax = stats[kStatMaxPane];
-  red[0] = qmax == INT64_MIN ? INT64_MAX : -qmax;
-  red[1] = stats[kStatMinPane];
-  red[2] = wm;
-  red[3] = -(stats[kStatOverflow] & 1);
-  red[4] = -((stats[kStatOverflow] >> 1) & 1);
-  // Record width a value needs: -2 = 24-byte records, -1 = 16-byte records, 0 = as planned.
-  red[5] = (stats[kStatOverflow] & 4) ? -2 : (stats[kStatOverflow] & 16) ? -1 : 0;
-  red[6] = flags ? -(int64_t)(flags[0] & 1u) : 0;  // a key found no slot (table full), sticky
-  red[7] = -((stats[kStatOverflow] >> 3) & 1);  // the reserved key id ~0 occurred
-  for (int j = 0; j < kStatCount; ++j) red[8 + j] = stats[j];
+  const int64_t ovf = stats[kStatOverflow];
+  int64_t v;
+  switch (j) {
+    case 0: {
+      const int64_t qmax = stats[kStatMaxPane];
+      v = qmax == INT64_MIN ? INT64_MAX : -qmax;
+      break;
+    }
+    case 1: v = stats[kStatMinPane]; break;
+    case 2: v = idle ? INT64_MAX : wm; break;  // an idle partition has no say in the MIN
+    case 3: v = -(ovf & 1); break;
+    case 4: v = -((ovf >> 1) & 1); break;
+    // Record width a value needs: -2 = 24-byte records, -1 = 16-byte records, 0 = as planned.
+    case 5: v = (ovf & 4) ? -2 : (ovf & 16) ? -1 : 0; break;
+    case 6: v = flags ? -(int64_t)(flags[0] & 1u) : 0; break;  // a key found no slot, sticky
+    case 7: v = -((ovf >> 3) & 1); break;  // the reserved key id ~0 occurred
+    default: v = stats[j - 8]; break;
+  }
+  red[j] = v;
+  if (host_red) host_red[j] = v;  // vector store into the mapped pinned buffer
+}
+
+__global__ __launch_bounds__(256) void combine_check_kernel(const uint32_t* __restrict__ flags,
+                                                            const uint32_t* __restrict__ counts,
+                                                            int nb, int64_t* __restrict__ chk) {
+  __shared__ uint32_t mx[256];
+  uint32_t m = 0;
+  for (int i = threadIdx.x; i < nb; i += 256) m = counts[i] > m ? counts[i] : m;
+  mx[threadIdx.x] = m;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s && mx[threadIdx.x + s] > mx[threadIdx.x]) mx[threadIdx.x] = mx[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    chk[0] = -(int64_t)(flags[0] & 2u);
+    chk[1] = -(int64_t)mx[0];
+  }
+}
+
+__global__ __launch_bounds__(256) void widen_i32_kernel(const int32_t* __restrict__ in, int64_t n,
+                                                        int64_t* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (int64_t)in[i];
+}
+
+__global__ __launch_bounds__(256) void fill_u64_kernel(uint64_t* __restrict__ p, int64_t n, uint64_t v) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -4216,9 +4259,33 @@ void step_begin(uint32_t* cursor, int nb, int64_t* stats, intptr_t stream) {
 }
 
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
-                 int64_t proc_now, int64_t* red, const uint32_t* flags, intptr_t stream) {
+                 int64_t proc_now, int64_t* red, const uint32_t* flags, intptr_t stream,
+                 int32_t idle, int64_t* host_red) {
   hipLaunchKernelGGL(step_finish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, stats,
-                     local_maxts, bound, event_mode, proc_now, red, flags);
+                     local_maxts, bound, event_mode, proc_now, red, flags, idle, host_red);
+  HIP_CHECK(hipGetLastError());
+}
+
+void combine_check(const uint32_t* flags, const uint32_t* counts, int nb, int64_t* chk,
+                   intptr_t stream) {
+  hipLaunchKernelGGL(combine_check_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, flags,
+                     counts, nb, chk);
+  HIP_CHECK(hipGetLastError());
+}
+
+void widen_i32(const int32_t* in, int64_t n, int64_t* out, intptr_t stream) {
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>(8192, (n + 255) / 256);
+  hipLaunchKernelGGL(widen_i32_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, in,
+                     n, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void fill_u64(uint64_t* p, int64_t n, uint64_t v, intptr_t stream) {
+  if (n <= 0) return;
+  const int64_t blocks = std::min<int64_t>(4096, (n + 255) / 256);
+  hipLaunchKernelGGL(fill_u64_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, p,
+                     n, v);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -391,8 +391,19 @@ void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_
                   const ExprProg& filt, uint64_t* out_key, uint64_t* out_val, int64_t* out_tag,
                   uint32_t* out_n, uint32_t out_cap, int abits, int shift, intptr_t stream,
                   uint32_t count_n = 0);
+// idle: this partition is idle (red[2] = +inf: no say in the MIN watermark); host_red: also
+// store the reduced vector into this pinned host buffer (one rank: no all-reduce in between, so
+// the step's host read needs no separate copy).
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
-                 int64_t proc_now, int64_t* red, const uint32_t* flags, intptr_t stream);
+                 int64_t proc_now, int64_t* red, const uint32_t* flags, intptr_t stream,
+                 int32_t idle = 0, int64_t* host_red = nullptr);
+// The combiner's overflow check as a MIN all-reduce operand: chk = [-(flags[0] & 2),
+// -max(counts[0..nb))].
+void combine_check(const uint32_t* flags, const uint32_t* counts, int nb, int64_t* chk,
+                   intptr_t stream);
+void fill_u64(uint64_t* p, int64_t n, uint64_t v, intptr_t stream);
+// Sign-extend int32 key ids to int64 (paths that do not read an int32 key column).
+void widen_i32(const int32_t* in, int64_t n, int64_t* out, intptr_t stream);
 void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt,
                       const uint32_t* n_in, const ScatPlan& plan, const int32_t* jhash,
                       const int32_t* kg_dest, uint32_t* cursor, Rec* out, uint32_t* flags,
@@ -480,7 +491,7 @@ void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, u
                   uint32_t* flags, const ExprProg& filt, uint64_t* out_key, uint64_t* out_val,
                   int64_t* out_tag, uint32_t* out_n, uint32_t out_cap, uint32_t count_n = 0);
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
-                 int64_t proc_now, int64_t* red, const uint32_t* flags);
+                 int64_t proc_now, int64_t* red, const uint32_t* flags, int32_t idle = 0);
 void keygroups(const uint64_t* keys, int64_t n, int hash_mode, const int32_t* jhash, int max_par,
                int32_t* kg);
 void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,

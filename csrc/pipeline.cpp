@@ -1,14 +1,13 @@
 // mxstream — native keyed event-time window pipeline + C ABI (mxs_c.h).
 //
-// The per-rank micro-batch control loop of runtime/window_operator.py (KeyedWindowOperator,
-// G = 1) in C++, so a host without Python (a JNI binding of the Java DataStream API, a C/C++
-// service) can run the reference's BandwidthMonitorWithEventTime shape
-// (chapter3/src/main/java/me/zjy/BandwidthMonitorWithEventTime.java:30-55): Flink window
-// assignment (TimeWindow.getWindowStartWithOffset), bounded-out-of-orderness watermark, late drop
-// (maxTs + allowedLateness <= wm), re-firing of late-but-allowed data, purge after cleanup time,
-// Long.MAX_VALUE watermark at end of input. Same kernels as the Python operator: gfx950
-// (device = 1) or the C++ twins (device = 0); tests/test_capi.py checks the two agree and
-// replays the chapter3 README golden stream through the C ABI.
+// A host without Python (a JNI binding of the Java DataStream API, a C/C++ service) runs the
+// reference's BandwidthMonitorWithEventTime shape
+// (chapter3/src/main/java/me/zjy/BandwidthMonitorWithEventTime.java:30-55) through the SAME
+// native window step as the Python operator (csrc/window_step.h WindowStep: Flink window
+// assignment, bounded-out-of-orderness watermark, late drop, re-firing of late-but-allowed data,
+// purge after cleanup time, Long.MAX_VALUE watermark at end of input), on gfx950 (device = 1) or
+// the C++ twins (device = 0). tests/test_capi.py replays the chapter3 README golden stream through
+// the C ABI. Also here: the rolling-aggregate and session loops of the C ABI.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -22,7 +21,7 @@
 #include <vector>
 
 #include "mxs_c.h"
-#include "window_control.h"
+#include "window_step.h"
 #include "mxs_check.h"
 #include "mxs_kernels.h"
 #include "session_store.h"
@@ -30,32 +29,19 @@
 namespace mxs {
 namespace {
 
-using i128 = __int128;
-constexpr int64_t kMin = INT64_MIN, kMax = INT64_MAX;
-
 thread_local std::string g_err;
 
 void hip_ok(hipError_t e, const char* what) {
   if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
 }
 
-i128 fdiv128(i128 a, i128 b) {
-  i128 q = a / b;
-  if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
-  return q;
-}
-i128 java_rem(i128 a, i128 b) {  // Java's % on long: sign of the dividend
-  const i128 r = (a < 0 ? -a : a) % (b < 0 ? -b : b);
-  return a < 0 ? -r : r;
-}
-int64_t clamp64(i128 v) { return v > kMax ? kMax : v < kMin ? kMin : (int64_t)v; }
 int64_t next_pow2(int64_t x) {
   int64_t p = 1;
   while (p < x) p <<= 1;
   return p;
 }
 
-// Device-or-host buffers of one pipeline.
+// Device-or-host buffers of one pipeline (the rolling loop below).
 struct Mem {
   bool gpu = false;
   hipStream_t stream = nullptr;
@@ -95,10 +81,6 @@ struct Mem {
       std::memcpy(dst, src, bytes);
     }
   }
-  void dev_copy(void* dst, const void* src, size_t bytes) {
-    if (gpu) hip_ok(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream), "D2D");
-    else std::memmove(dst, src, bytes);
-  }
   ~Mem() {
     for (void* p : owned) {
       if (gpu) (void)hipFree(p);
@@ -107,7 +89,7 @@ struct Mem {
   }
 };
 
-// runtime/geometry.py state_geometry(max_keys, world = 1)
+// runtime/geometry.py state_geometry(max_keys, world = 1) (the rolling loop's tables)
 void state_geometry(int64_t max_keys, int* nsub_out, int* cap_log2_out) {
   const double per_rank = (double)max_keys + 64;
   const double load = 0.7;
@@ -124,313 +106,86 @@ void state_geometry(int64_t max_keys, int* nsub_out, int* cap_log2_out) {
 
 }  // namespace
 
+// The C ABI's window pipeline: the SAME native step the Python operator runs
+// (csrc/window_step.h WindowStep, one rank, unpipelined), fed from host arrays.
 class WindowPipeline {
  public:
-  explicit WindowPipeline(const mxs_window_config& c)
-      : cfg_(c), ctl_(c.size_ms, c.slide_ms, c.offset_ms, c.lateness_ms) {
-    if (c.size_ms <= 0 || c.slide_ms <= 0) throw std::invalid_argument("window size and slide must be positive");
-    if (c.agg < AGG_SUM_I64 || c.agg > AGG_AVG_I64) throw std::invalid_argument("unknown aggregate");
+  explicit WindowPipeline(const mxs_window_config& c) : gpu_(c.device != 0) {
     if (c.lateness_ms < 0 || c.ooo_bound_ms < 0) throw std::invalid_argument("negative lateness / bound");
-    mem_.gpu = c.device != 0;
-    if (mem_.gpu) {
+    WindowStepConfig w;
+    w.size = c.size_ms;
+    w.slide = c.slide_ms;
+    w.offset = c.offset_ms;
+    w.lateness = c.lateness_ms;
+    w.agg = c.agg;
+    w.gpu = gpu_;
+    w.device_index = c.device_index;
+    w.max_parallelism = c.max_parallelism > 0 ? c.max_parallelism : 128;
+    w.max_keys = std::max<int64_t>(c.max_keys, 1);
+    w.batch_capacity = std::max<int64_t>(c.batch_capacity, 1024);
+    w.ooo_bound = c.ooo_bound_ms;
+    struct One : StepComm {
+      void allreduce_min_i64(int64_t*, int, intptr_t) override {}
+      void all_to_all(void* r, const void* s, int64_t b, int, intptr_t) override {
+        if (r != s) std::memmove(r, s, (size_t)b);
+      }
+    };
+    if (gpu_) {
       hip_ok(hipSetDevice(c.device_index), "hipSetDevice");
-      hip_ok(hipStreamCreateWithFlags(&mem_.stream, hipStreamNonBlocking), "hipStreamCreate");
+      hip_ok(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "hipStreamCreate");
     }
-    ooo_ = c.ooo_bound_ms;
-    max_par_ = c.max_parallelism > 0 ? c.max_parallelism : 128;
-    const int64_t pane = ctl_.pane(), slide = c.slide_ms, lateness = c.lateness_ms;
-    state_geometry(std::max<int64_t>(c.max_keys, 1), &nsub_, &cap_log2_);
-    nsub_log2_ = 0;
-    while ((1 << nsub_log2_) < nsub_) ++nsub_log2_;
-    nslots_ = (int64_t)nsub_ << cap_log2_;
-    ring_ = std::max<int64_t>(4, next_pow2(ctl_.panes_per_window() + 2 + (lateness + pane - 1) / pane +
-                                           (std::max(ooo_, slide) + pane - 1) / pane));
-    const bool int_agg = c.agg == AGG_SUM_I64 || c.agg == AGG_MIN_I64 || c.agg == AGG_MAX_I64 ||
-                         c.agg == AGG_COUNT || c.agg == AGG_AVG_I64;
-    compact_ = mem_.gpu && int_agg;
-    keys_g_ = (uint64_t*)mem_.alloc(nslots_ * 8);
-    mem_.fill(keys_g_, 0xFF, nslots_ * 8);
-    alloc_state(ring_);
-    occ_ = (uint32_t*)mem_.alloc(nsub_ * 4);
-    flags_ = (uint32_t*)mem_.alloc(16);
-    kg_dest_ = (int32_t*)mem_.alloc(max_par_ * 4);  // all key groups on this rank (zeros)
-    stats_ = (int64_t*)mem_.alloc(kStatCount * 8);
-    red_ = (int64_t*)mem_.alloc(16 * 8);
-    local_maxts_ = (int64_t*)mem_.alloc(8);
-    mem_.to_dev(local_maxts_, &kMin, 8);
-    minbuf_ = (int64_t*)mem_.alloc(8);
-    out_keys_ = (uint64_t*)mem_.alloc(nslots_ * 8);
-    out_vals_ = (double*)mem_.alloc(nslots_ * 8);
-    out_raw_ = (uint64_t*)mem_.alloc(nslots_ * 8);
-    out_cnt_ = (uint32_t*)mem_.alloc(nslots_ * 4);
-    out_n_ = (uint32_t*)mem_.alloc(4);
-    alloc_buckets(std::max<int64_t>(c.batch_capacity, 1024), 1.5);
+    step_.reset(new WindowStep(w, std::make_shared<One>()));
   }
-
   ~WindowPipeline() {
-    if (mem_.gpu && mem_.stream) {
-      (void)hipStreamSynchronize(mem_.stream);
-      (void)hipStreamDestroy(mem_.stream);
-    }
+    step_.reset();
+    if (gpu_ && stream_) (void)hipStreamDestroy(stream_);
+    for (void* p : in_) (void)hipFree(p);  // device copies of the host batches (GPU only)
   }
 
   void process(const uint64_t* keys_h, const int64_t* ts_h, const int64_t* vals_h, int64_t n) {
     if (n < 0) throw std::invalid_argument("negative batch size");
-    if (n > batch_capacity_) alloc_buckets(n, slack_);
-    if (n > in_cap_) {
-      mem_.release(in_keys_);
-      mem_.release(in_ts_);
-      mem_.release(in_vals_);
-      in_cap_ = n;
-      in_keys_ = (uint64_t*)mem_.alloc(n * 8);
-      in_ts_ = (int64_t*)mem_.alloc(n * 8);
-      in_vals_ = (uint64_t*)mem_.alloc(n * 8);
-    }
-    if (n) {
-      mem_.to_dev(in_keys_, keys_h, n * 8);
-      mem_.to_dev(in_ts_, ts_h, n * 8);
-      mem_.to_dev(in_vals_, vals_h, n * 8);
-    }
-    const int64_t old_wm = wm_;
-    const int64_t pane_base = pane_base_of(n);
-    int64_t host[16];
-    for (;;) {
-      if (mem_.gpu) gpu::step_begin(cursor_, nb(), stats_, (intptr_t)mem_.stream);
-      else cpu::step_begin(cursor_, nb(), stats_);
-      PartPlan pp;
-      std::memset(&pp, 0, sizeof(pp));
-      pp.max_parallelism = max_par_;
-      pp.nsub_log2 = nsub_log2_;
-      pp.nranks = 1;
-      pp.window_mode = 1;
-      pp.drop_late = 1;
-      pp.hash_mode = 0;
-      pp.bucket_cap = (uint32_t)bucket_cap_;
-      pp.late_ts = ctl_.late_ts(old_wm);
-      pp.tbase = ctl_.pane_start(pane_base);
-      pp.pane = ctl_.pane();
-      pp.inv_pane = 1.0 / (double)ctl_.pane();
-      pp.rec_words = compact_ ? 2 : 3;
-      if (n) {
-        if (mem_.gpu)
-          gpu::partition(in_keys_, in_ts_, in_vals_, nullptr, n, pp, kg_dest_, cursor_, send_,
-                         stats_, nullptr, 0, (intptr_t)mem_.stream);
-        else
-          cpu::partition(in_keys_, in_ts_, in_vals_, nullptr, n, pp, kg_dest_, cursor_, send_,
-                         stats_, nullptr, 0);
+    const void *k = keys_h, *t = ts_h, *v = vals_h;
+    if (gpu_ && n) {
+      if (n > in_cap_) {
+        for (void* p : in_) (void)hipFree(p);
+        in_.assign(3, nullptr);
+        for (auto& p : in_) hip_ok(hipMalloc(&p, (size_t)n * 8), "hipMalloc");
+        in_cap_ = n;
       }
-      if (mem_.gpu)
-        gpu::step_finish(stats_, local_maxts_, ooo_, 1, 0, red_, nullptr, (intptr_t)mem_.stream);
-      else
-        cpu::step_finish(stats_, local_maxts_, ooo_, 1, 0, red_, nullptr);
-      mem_.to_host(host, red_, sizeof(host));  // the step's single host sync
-      if (host[4]) throw std::runtime_error("event timestamp outside the representable pane range");
-      if (host[5]) {
-        compact_ = false;  // a value does not fit the 16-byte record
-        continue;
-      }
-      if (host[3]) {
-        alloc_buckets(batch_capacity_, slack_ * 2);
-        continue;
-      }
-      break;
+      hip_ok(hipMemcpyAsync(in_[0], keys_h, n * 8, hipMemcpyHostToDevice, stream_), "H2D");
+      hip_ok(hipMemcpyAsync(in_[1], ts_h, n * 8, hipMemcpyHostToDevice, stream_), "H2D");
+      hip_ok(hipMemcpyAsync(in_[2], vals_h, n * 8, hipMemcpyHostToDevice, stream_), "H2D");
+      k = in_[0];
+      t = in_[1];
+      v = in_[2];
     }
-    const int64_t qmax = -host[0], qmin = host[1], wm_global = host[2];
-    records_in_ += n;
-    late_dropped_ += host[8 + kStatLate];
-    if (qmin <= qmax) {
-      const int64_t gmin = pane_base + qmin, gmax = pane_base + qmax;
-      const int64_t span = ctl_.live_span_with(gmin, gmax);
-      if (span > ring_) grow_ring(span);
-      ctl_.observe(gmin, gmax, old_wm);
-      const int64_t fhi = ctl_.fired_hi();
-      const int64_t cap = (int64_t)1 << cap_log2_;
-      const int64_t np = gmax - gmin + 1;
-      const int64_t pg = std::max<int64_t>(1, std::min<int64_t>(np, (150 * 1024 - cap * 8) / (cap * 12)));
-      AggPlan ap;
-      std::memset(&ap, 0, sizeof(ap));
-      ap.cap_log2 = cap_log2_;
-      ap.nsub = nsub_;
-      ap.ring = (int32_t)ring_;
-      ap.agg = cfg_.agg;
-      ap.nsrc = 1;
-      ap.bucket_cap = (uint32_t)bucket_cap_;
-      ap.np_step = (int32_t)np;
-      ap.pg = (int32_t)pg;
-      ap.pane_base = pane_base;
-      ap.p_lo = qmin;
-      ap.fired_hi = fhi;
-      ap.rec_words = compact_ ? 2 : 3;
-      if (mem_.gpu)
-        gpu::window_agg(send_, cursor_, ap, keys_g_, acc_g_, cnt_g_, dirty_g_, occ_, flags_,
-                        (intptr_t)mem_.stream);
-      else
-        cpu::window_agg(send_, cursor_, ap, keys_g_, acc_g_, cnt_g_, dirty_g_, occ_, flags_);
-      if (gmin <= fhi) refire(gmin, std::min(gmax, fhi), old_wm);
-    }
-    ++steps_;
-    const int64_t new_wm = std::max(old_wm, wm_global);
-    wm_ = new_wm;
-    fire_ready(new_wm);
-    purge(new_wm);
+    step_->process(k, false, (const int64_t*)t, v, n, (intptr_t)stream_);
+    collect();
   }
 
   void finish() {
-    if (wm_ >= kMax) return;
-    wm_ = kMax;
-    fire_ready(kMax);
-    purge(kMax);
+    step_->finish((intptr_t)stream_);
+    collect();
   }
 
-  int64_t watermark() const { return wm_; }
-  int64_t late_dropped() const { return late_dropped_; }
-  int64_t records_in() const { return records_in_; }
+  int64_t watermark() const { return step_->wm(); }
+  int64_t late_dropped() const { return step_->metrics().num_late_records_dropped; }
+  int64_t records_in() const { return step_->metrics().num_records_in; }
   std::deque<mxs_window_result> results;
 
  private:
-  int nb() const { return 1 << nsub_log2_; }
-
-  void alloc_state(int64_t ring) {
-    acc_g_ = (uint64_t*)mem_.alloc(ring * nslots_ * 8);
-    cnt_g_ = (uint32_t*)mem_.alloc(ring * nslots_ * 4);
-    dirty_g_ = (uint8_t*)mem_.alloc(ring * nslots_);
-    mem_.fill(acc_g_, 0, ring * nslots_ * 8);
-    mem_.fill(cnt_g_, 0, ring * nslots_ * 4);
-    mem_.fill(dirty_g_, 0, ring * nslots_);
+  void collect() {
+    for (const FireRows& r : step_->take(true))
+      for (int64_t i = 0; i < r.n; ++i)
+        results.push_back({r.start, r.end, ((const uint64_t*)r.keys)[i], r.vals[i], r.raw[i],
+                           (uint32_t)r.cnt[i], r.refire ? 1 : 0});
   }
 
-  void alloc_buckets(int64_t capacity, double slack) {
-    batch_capacity_ = capacity;
-    slack_ = slack;
-    const double per = (double)capacity / nb();
-    const int64_t nblk = std::min<int64_t>(1024, std::max<int64_t>(1, (capacity + 65535) / 65536));
-    int64_t cap = (int64_t)(per * slack + 6 * std::sqrt(std::max(per, 1.0)) + 64) + 8 * nblk;
-    bucket_cap_ = (cap + 7) & ~(int64_t)7;
-    mem_.release(send_);
-    mem_.release(cursor_);
-    send_ = (Rec*)mem_.alloc((size_t)nb() * bucket_cap_ * sizeof(Rec));
-    cursor_ = (uint32_t*)mem_.alloc(nb() * 4);
-  }
-
-  void grow_ring(int64_t need) {
-    const int64_t nr = next_pow2(need), old = ring_;
-    uint64_t* oacc = acc_g_;
-    uint32_t* ocnt = cnt_g_;
-    uint8_t* odirty = dirty_g_;
-    alloc_state(nr);
-    if (ctl_.has_live())
-      for (int64_t p = ctl_.min_live(); p <= ctl_.max_seen(); ++p) {
-        const int64_t so = (p & (old - 1)) * nslots_, sn = (p & (nr - 1)) * nslots_;
-        mem_.dev_copy(acc_g_ + sn, oacc + so, nslots_ * 8);
-        mem_.dev_copy(cnt_g_ + sn, ocnt + so, nslots_ * 4);
-        mem_.dev_copy(dirty_g_ + sn, odirty + so, nslots_);
-      }
-    if (mem_.gpu) hip_ok(hipStreamSynchronize(mem_.stream), "sync");
-    mem_.release(oacc);
-    mem_.release(ocnt);
-    mem_.release(odirty);
-    ring_ = nr;
-  }
-
-  // The step's base pane: from the watermark once there is one (every non-late element has
-  // ts >= wm - size - lateness + 1), else the batch's minimum timestamp.
-  int64_t pane_base_of(int64_t n) {
-    if (wm_ > kMin) return ctl_.pane_base_from_wm(wm_);
-    int64_t m = kMax;
-    if (n) {
-      if (mem_.gpu) {
-        mem_.to_dev(minbuf_, &kMax, 8);
-        gpu::min_i64(in_ts_, n, minbuf_, (intptr_t)mem_.stream);
-        mem_.to_host(&m, minbuf_, 8);
-      } else {
-        for (int64_t i = 0; i < n; ++i) m = std::min(m, in_ts_[i]);
-      }
-    }
-    int64_t base = m != kMax ? ctl_.pane_of(m) : 0;
-    if (ctl_.has_live()) base = std::min(base, ctl_.min_live());
-    return base;
-  }
-
-  void fire_window(int64_t s, bool only_dirty) {
-    const auto pr = ctl_.window_panes(s);
-    const int64_t p0 = pr.first, p1 = pr.second;
-    if (p1 < p0) return;
-    const uint32_t zero = 0;
-    mem_.to_dev(out_n_, &zero, 4);
-    FirePlan fp;
-    std::memset(&fp, 0, sizeof(fp));
-    fp.agg = cfg_.agg;
-    fp.npanes = (int32_t)(p1 - p0 + 1);
-    fp.ring = (int32_t)ring_;
-    fp.only_dirty = only_dirty ? 1 : 0;
-    fp.nslots = nslots_;
-    fp.p0 = p0;
-    fp.wstart = (double)s;
-    fp.wend = (double)s + (double)ctl_.size();
-    fp.out_cap = (uint32_t)nslots_;
-    if (mem_.gpu)
-      gpu::window_fire(keys_g_, acc_g_, cnt_g_, dirty_g_, fp, out_keys_, out_vals_, out_raw_,
-                       out_cnt_, out_n_, (intptr_t)mem_.stream);
-    else
-      cpu::window_fire(keys_g_, acc_g_, cnt_g_, dirty_g_, fp, out_keys_, out_vals_, out_raw_,
-                       out_cnt_, out_n_);
-    uint32_t n = 0;
-    mem_.to_host(&n, out_n_, 4);
-    n = (uint32_t)std::min<int64_t>(n, nslots_);
-    if (!n) return;
-    std::vector<uint64_t> k(n), raw(n);
-    std::vector<double> v(n);
-    std::vector<uint32_t> c(n);
-    mem_.to_host(k.data(), out_keys_, n * 8);
-    mem_.to_host(v.data(), out_vals_, n * 8);
-    mem_.to_host(raw.data(), out_raw_, n * 8);
-    mem_.to_host(c.data(), out_cnt_, n * 4);
-    for (uint32_t i = 0; i < n; ++i)
-      results.push_back({s, clamp64((i128)s + ctl_.size()), k[i], v[i], (int64_t)raw[i], c[i],
-                         only_dirty ? 1 : 0});
-  }
-
-  void fire_ready(int64_t wm) {
-    for (int64_t s : ctl_.take_due(wm)) fire_window(s, false);
-  }
-
-  void refire(int64_t pmin, int64_t pmax, int64_t old_wm) {
-    for (int64_t s : ctl_.refire_windows(pmin, pmax, old_wm)) fire_window(s, true);
-    for (int64_t p = pmin; p <= pmax; ++p)
-      mem_.fill(dirty_g_ + (p & (ring_ - 1)) * nslots_, 0, nslots_);
-  }
-
-  void purge(int64_t wm) {
-    const auto r = ctl_.purge_range(wm, ring_);
-    for (int64_t p = r.from; p < r.stop; ++p) {
-      const int64_t so = (p & (ring_ - 1)) * nslots_;
-      mem_.fill(acc_g_ + so, 0, nslots_ * 8);
-      mem_.fill(cnt_g_ + so, 0, nslots_ * 4);
-      mem_.fill(dirty_g_ + so, 0, nslots_);
-    }
-    ctl_.commit_purge(r.keep_from);
-  }
-
-  mxs_window_config cfg_;
-  WindowControl ctl_;  // window arithmetic + firing bookkeeping (shared with the Python operator)
-  Mem mem_;
-  int64_t ooo_, ring_, nslots_;
-  int max_par_, nsub_, cap_log2_, nsub_log2_;
-  bool compact_ = false;
-  int64_t batch_capacity_ = 0, bucket_cap_ = 0, in_cap_ = 0;
-  double slack_ = 1.5;
-  uint64_t *keys_g_ = nullptr, *acc_g_ = nullptr, *out_keys_ = nullptr, *out_raw_ = nullptr;
-  uint64_t *in_keys_ = nullptr, *in_vals_ = nullptr;
-  int64_t *in_ts_ = nullptr, *stats_ = nullptr, *red_ = nullptr, *local_maxts_ = nullptr,
-          *minbuf_ = nullptr;
-  uint32_t *cnt_g_ = nullptr, *occ_ = nullptr, *flags_ = nullptr, *cursor_ = nullptr,
-           *out_cnt_ = nullptr, *out_n_ = nullptr;
-  uint8_t* dirty_g_ = nullptr;
-  int32_t* kg_dest_ = nullptr;
-  double* out_vals_ = nullptr;
-  Rec* send_ = nullptr;
-  int64_t wm_ = kMin;
-  int64_t records_in_ = 0, late_dropped_ = 0, steps_ = 0;
+  bool gpu_;
+  hipStream_t stream_ = nullptr;
+  std::unique_ptr<WindowStep> step_;
+  std::vector<void*> in_;
+  int64_t in_cap_ = 0;
 };
 
 }  // namespace mxs

@@ -30,7 +30,7 @@ HIP_SOURCES = ["kernels_hip.hip", "sort_hip.hip", "parse_hip.hip", "vector_hip.h
 CXX_SOURCES = ["kernels_cpu.cpp", "ingest_cpu.cpp", "runtime.cpp", "sessions.cpp", "vector_cpu.cpp",
                "vector_bindings.cpp", "trace.cpp", "check_cpu.cpp", "reader.cpp", "format.cpp", "listwin_cpu.cpp",
                "listwin_bindings.cpp", "window_tier_bindings.cpp", "window_control_bindings.cpp",
-               "bindings.cpp"]
+               "window_step.cpp", "window_step_bindings.cpp", "bindings.cpp"]
 # roctx ranges (csrc/trace.cpp) come from the ROCm profiler SDK's marker library.
 LINK_LIBS = ["-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
 
@@ -167,7 +167,8 @@ def build_tsan(verbose: bool = False) -> Path:
 
 
 CAPI_SOURCES = ["kernels_hip.hip", "check_hip.hip", "sort_hip.hip", "rolling_hist_hip.hip",
-                "kernels_cpu.cpp", "pipeline.cpp"]
+                "vector_hip.hip", "kernels_cpu.cpp", "vector_cpu.cpp", "window_step.cpp",
+                "pipeline.cpp"]
 
 
 def capi_path() -> Path:

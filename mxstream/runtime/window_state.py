@@ -1,6 +1,7 @@
 """Checkpoint half of the keyed window operator (runtime/window_operator.py): state sizes,
-synchronous and asynchronous snapshots (device tables copied on a side stream, the host tier
-frozen), restore with key-group filtering (rescaling), and the merge-ring rebuild.
+synchronous and asynchronous snapshots (device tables cloned on the stream, the host tier and the
+firing bookkeeping frozen), restore with key-group filtering (rescaling), and the merge-ring
+rebuild. The tables are the native step's memory (csrc/window_step.h), seen as tensors.
 
 Reference: chapter3/README.md:454-456 (checkpointed state survives failures).
 """
@@ -18,7 +19,7 @@ I64_MAX = K.I64_MAX
 
 
 class _StateMixin:
-    """Methods of KeyedWindowOperator (mixed in; state lives on the operator)."""
+    """Methods of KeyedWindowOperator (mixed in; state lives in the native step)."""
 
     # ---- introspection ---------------------------------------------------------------------
     def state_bytes(self) -> int:
@@ -29,7 +30,7 @@ class _StateMixin:
         """Bytes of keyed state in the host-DRAM tier (0 without spill)."""
         if self.host_tier is None:
             return 0
-        self._land_evictions()
+        self._sync_state()
         return self.host_tier.nbytes
 
     def num_keys(self) -> int:
@@ -38,13 +39,17 @@ class _StateMixin:
             return int((self.cnt_g.view(self.ring, self.nslots) > 0).any(0).sum().item())
         return int(self.occ.sum().item())
 
-    def _sync_state(self) -> None:
-        """Make the state tables current for a host reader: the pending step must be applied
-        (its fired rows are kept for the next process()/flush() caller) and S1 drained."""
-        if self._pending is not None:
-            self._carry.extend(self.flush())
-        self._drain()
-        self._land_evictions()  # evicted rows still in flight belong to the tier's state
+    def _book(self) -> dict:
+        """Firing bookkeeping as of now (or as of the freeze, for a frozen copy)."""
+        b = self.__dict__.get("_frozen_book")
+        if b is not None:
+            return b
+        m = self.metrics
+        return {"wm": self.wm, "next_fire_start": self.next_fire_start,
+                "min_live_pane": self.min_live_pane, "max_seen_pane": self.max_seen_pane,
+                "ring": self.ring,
+                "metrics": {k: getattr(m, k) for k in ("num_records_in", "num_late_records_dropped",
+                                                       "num_records_out", "num_fires", "steps")}}
 
     # ---- checkpoint / restore (runtime/checkpoint.py) --------------------------------------
     def owned_key_groups(self) -> tuple[int, int]:
@@ -59,46 +64,58 @@ class _StateMixin:
                                  f"{getattr(self, k)!r}")
 
     def snapshot_state_async(self):
-        """Freeze the state now (D2D copies), export it later: see checkpoint.freeze_operator."""
+        """Freeze the state now (D2D clones, bookkeeping and host tier copied), export it later:
+        see checkpoint.freeze_operator."""
         from .checkpoint import freeze_operator
 
         self._sync_state()
+        book = self._book()
 
-        def private_tier(frozen):
-            # The export reads the spill tier from a worker thread while the step loop keeps
-            # absorbing / purging the live one: the frozen copy gets its own tier as of now, so
-            # keys evicted after the freeze are neither lost nor exported twice.
+        def private(frozen):
+            # The export runs on a worker thread while the step loop keeps going: the frozen copy
+            # gets its own bookkeeping and its own tier as of now.
+            frozen._frozen_book = book
             if self.host_tier is not None:
-                frozen.host_tier = self.host_tier.copy()
+                frozen._frozen_tier = self.host_tier.copy()
 
-        return freeze_operator(self, self._state_tensors, post=private_tier)
+        return freeze_operator(self, self._state_tensors, post=private)
+
+    def _snapshot_tier(self):
+        t = self.__dict__.get("_frozen_tier")
+        return t if t is not None else self.host_tier
 
     def snapshot_state(self):
         """Live (key, pane) accumulators grouped by key group, plus the firing bookkeeping."""
         from .checkpoint import OperatorSnapshot
 
-        self._sync_state()
-        live = torch.nonzero(self.keys_g != -1).flatten()
+        if "_frozen_book" not in self.__dict__:
+            self._sync_state()
+        book = self._book()
+        keys_g, cnt_g, acc_g, dirty_g = self.keys_g, self.cnt_g, self.acc_g, self.dirty_g
+        ring, nslots = book["ring"], self.nslots
+        live = torch.nonzero(keys_g != -1).flatten()
         cols = {"key": np.zeros(0, np.int64), "pane": np.zeros(0, np.int64),
                 "acc": np.zeros(0, np.int64), "cnt": np.zeros(0, np.int32),
                 "dirty": np.zeros(0, np.uint8)}
         kg = np.zeros(0, np.int32)
-        if self.min_live_pane is not None and live.numel():
-            panes = torch.arange(self.min_live_pane, self.max_seen_pane + 1, device=self.device)
-            idx = ((panes & (self.ring - 1)) * self.nslots)[:, None] + live[None, :]
-            cnt = self.cnt_g[idx]
+        lo, hi = book["min_live_pane"], book["max_seen_pane"]
+        if lo is not None and live.numel():
+            panes = torch.arange(lo, hi + 1, device=keys_g.device)
+            idx = ((panes & (ring - 1)) * nslots)[:, None] + live[None, :]
+            cnt = cnt_g[idx]
             sel = cnt > 0
-            keys = self.keys_g[live][None, :].expand_as(idx)[sel].contiguous()
+            keys = keys_g[live][None, :].expand_as(idx)[sel].contiguous()
             kg = K.keygroups(keys, max_parallelism=self.max_parallelism, hash_mode=self.hash_mode,
                              jhash=self.jhash).cpu().numpy()
             cols = {"key": keys.cpu().numpy(),
                     "pane": panes[:, None].expand_as(idx)[sel].cpu().numpy(),
-                    "acc": self.acc_g[idx][sel].cpu().numpy(),
+                    "acc": acc_g[idx][sel].cpu().numpy(),
                     "cnt": cnt[sel].cpu().numpy(),
-                    "dirty": self.dirty_g[idx][sel].cpu().numpy()}
-        if self.host_tier is not None and self.host_tier.nrows:
+                    "dirty": dirty_g[idx][sel].cpu().numpy()}
+        tier = self._snapshot_tier()
+        if tier is not None and tier.nrows:
             # Spilled state travels in the same rows (restore folds duplicate (key, pane) rows).
-            h = self.host_tier.rows()
+            h = tier.rows()
             hk = torch.from_numpy(h["key"].view(np.int64))
             kg = np.concatenate([kg, K.keygroups(hk, max_parallelism=self.max_parallelism,
                                                  hash_mode=self.hash_mode,
@@ -111,50 +128,33 @@ class _StateMixin:
                     "dirty": np.concatenate([cols["dirty"], h["dirty"]])}
         meta = {"kind": "window", "size": self.size, "slide": self.slide, "offset": self.offset,
                 "lateness": self.lateness, "agg": self.agg, "time_mode": self.time_mode,
-                "wm": self.wm, "next_fire_start": self.next_fire_start,
-                "min_live_pane": self.min_live_pane, "max_seen_pane": self.max_seen_pane,
-                "metrics": {"num_records_in": self.metrics.num_records_in,
-                            "num_late_records_dropped": self.metrics.num_late_records_dropped,
-                            "num_records_out": self.metrics.num_records_out,
-                            "num_fires": self.metrics.num_fires, "steps": self.metrics.steps}}
+                "wm": book["wm"], "next_fire_start": book["next_fire_start"],
+                "min_live_pane": lo, "max_seen_pane": hi, "metrics": book["metrics"]}
         return OperatorSnapshot(kg, cols, meta)
+
+    def _restore_book(self, meta: dict) -> None:
+        """Bookkeeping of a restore; the ring is re-laid (zeroed) to hold the live panes."""
+        lo, hi = meta["min_live_pane"], meta["max_seen_pane"]
+        ring = self.ring
+        if lo is not None and hi - lo + 1 > ring:
+            ring = _next_pow2(hi - lo + 1)
+        self._s.reset_state(ring)
+        self.wm = meta["wm"]
+        self.next_fire_start = meta["next_fire_start"]
+        self._set_live(lo, hi)
+        for k, v in meta.get("metrics", {}).items():
+            setattr(self.metrics, k, v)
 
     def restore_state(self, rows: dict, meta: dict) -> None:
         """Rebuild the tables from checkpoint rows (this rank's key groups only)."""
         self._check_ckpt_meta(meta)
-        if self.host_tier is not None:
-            self._evict_pending = None  # rows of the replaced state
-            self.host_tier.clear()
-        self._pending, self._carry = None, []
-        self._drain()
+        self._restore_book(meta)
         dev = self.device
-        self.wm = meta["wm"]
-        self.metrics.current_watermark = self.wm
-        self.next_fire_start = meta["next_fire_start"]
-        self.min_live_pane, self.max_seen_pane = meta["min_live_pane"], meta["max_seen_pane"]
-        for k, v in meta.get("metrics", {}).items():
-            setattr(self.metrics, k, v)
-        if self.min_live_pane is not None and self.max_seen_pane - self.min_live_pane + 1 > self.ring:
-            self.ring = _next_pow2(self.max_seen_pane - self.min_live_pane + 1)
-            self.acc_g = torch.zeros(self.ring * self.nslots, dtype=torch.int64, device=dev)
-            self.cnt_g = torch.zeros(self.ring * self.nslots, dtype=torch.int32, device=dev)
-            self.dirty_g = torch.zeros(self.ring * self.nslots, dtype=torch.uint8, device=dev)
-        if not self.dense_bits:
-            self.keys_g.fill_(-1)
-        if self.dlist is not None:
-            self.dlist_n.zero_()
-            self.slot_mark.zero_()
-        self.acc_g.zero_()
-        self.cnt_g.zero_()
-        self.dirty_g.zero_()
-        self.occ.zero_()
-        if self.local_global and self.lateness > 0:
-            self.dacc_g = torch.zeros(self.ring * self.nslots, dtype=torch.int64, device=dev)
-            self.dcnt_g = torch.zeros(self.ring * self.nslots, dtype=torch.int32, device=dev)
         if not len(rows["key"]):
             if self.local_global:
-                self._rebuild_merge_ring()
+                self._s.rebuild_merge_ring(self._stream())
             return
+        keys_g, acc_g, cnt_g, dirty_g = self.keys_g, self.acc_g, self.cnt_g, self.dirty_g
         keys = torch.from_numpy(np.ascontiguousarray(rows["key"])).to(dev)
         pane = torch.from_numpy(np.ascontiguousarray(rows["pane"])).to(dev)
         acc = torch.from_numpy(np.ascontiguousarray(rows["acc"])).to(dev)
@@ -179,7 +179,7 @@ class _StateMixin:
             slots_u = torch.full((uniq.numel(),), -1, dtype=torch.int64, device=dev)
             hot = torch.nonzero(~to_tier).flatten()
             if hot.numel():
-                slots_u[hot] = K.table_insert(uniq[hot].contiguous(), self.keys_g,
+                slots_u[hot] = K.table_insert(uniq[hot].contiguous(), keys_g,
                                               nsub_log2=self.nsub_log2, cap_log2=self.cap_log2)
             row_tier = (slots_u < 0)[inv]
             occ_slots = slots_u[slots_u >= 0]
@@ -193,7 +193,7 @@ class _StateMixin:
                 inv = inv[sel]
                 slots_u = torch.where(slots_u < 0, torch.zeros_like(slots_u), slots_u)
         else:
-            slots_u = K.table_insert(uniq.contiguous(), self.keys_g, nsub_log2=self.nsub_log2,
+            slots_u = K.table_insert(uniq.contiguous(), keys_g, nsub_log2=self.nsub_log2,
                                      cap_log2=self.cap_log2)
         if bool((slots_u < 0).any()):
             raise RuntimeError("restore: keyed state does not fit the table (raise max_keys)")
@@ -201,18 +201,16 @@ class _StateMixin:
         idx = (pane & (self.ring - 1)) * self.nslots + slot
         u, inv = torch.unique(idx, return_inverse=True)
         if u.numel() == idx.numel():
-            self.acc_g[idx], self.cnt_g[idx], self.dirty_g[idx] = acc, cnt, dirty
+            acc_g[idx], cnt_g[idx], dirty_g[idx] = acc, cnt, dirty
         else:
             # Several rows per (key, pane): partial accumulators of a local-global checkpoint
             # (every rank held a partial of every key) -- fold them with the aggregate.
-            self.acc_g[u] = combine_partials(self.agg, acc, inv, u.numel())
-            self.cnt_g[u] = torch.zeros(u.numel(), dtype=torch.int32, device=dev).index_add_(
-                0, inv, cnt)
-            self.dirty_g[u] = torch.zeros(u.numel(), dtype=torch.int32, device=dev).scatter_reduce_(
+            acc_g[u] = combine_partials(self.agg, acc, inv, u.numel())
+            cnt_g[u] = torch.zeros(u.numel(), dtype=torch.int32, device=dev).index_add_(0, inv, cnt)
+            dirty_g[u] = torch.zeros(u.numel(), dtype=torch.int32, device=dev).scatter_reduce_(
                 0, inv, dirty.to(torch.int32), "amax").to(torch.uint8)
         if self.dlist is not None:
             # Rebuild the touched-slot list from the restored dirty bytes.
-            self.slot_mark.zero_()
             ds = torch.unique(slot[dirty != 0]).to(torch.int32)
             self.dlist[:ds.numel()] = ds
             self.dlist_n.fill_(ds.numel())
@@ -221,26 +219,4 @@ class _StateMixin:
         self.occ.copy_(torch.bincount(occ_slots >> self.cap_log2, minlength=self.nsub)
                        .to(torch.int32))
         if self.local_global:
-            self._rebuild_merge_ring()
-
-    def _rebuild_merge_ring(self) -> None:
-        """Local-global with allowed lateness, after a restore: the owners' merged values of the
-        windows that fired but are not cleaned (a late re-firing adds deltas to them) are
-        recomputed from the restored state -- the same collective exchange as a fire, without
-        the emit. Every rank runs the same window sequence (identical restored bookkeeping)."""
-        self.keys_m.fill_(-1)
-        self.acc_m.zero_()
-        self.cnt_m.zero_()
-        self.dirty_m.zero_()
-        self.occ_m.zero_()
-        if (self.lateness <= 0 or self.next_fire_start is None or self.min_live_pane is None
-                or self.wm == I64_MIN):
-            return
-        s = max(self._align_up(self.wm - self.size - self.lateness + 2),
-                self.first_start_containing(self.pane_start(self.min_live_pane)))
-        while s < self.next_fire_start:
-            p0 = max(self.pane_of(s), self.min_live_pane)
-            p1 = min(self.pane_of(s) + self.panes_per_window - 1, self.max_seen_pane)
-            if p1 >= p0:
-                self._fire_window_partials(s, p0, p1, only_dirty=False, emit=False)
-            s += self.slide
+            self._s.rebuild_merge_ring(self._stream())

@@ -1,5 +1,5 @@
-"""Result and plan records of the keyed window operator (runtime/window_operator.py) and the
-aggregate helpers shared by its halves (window_fire.py, window_tiering.py, window_state.py).
+"""Result records of the keyed window operator (runtime/window_operator.py) and the aggregate
+helpers of its checkpoint half (window_state.py).
 """
 from __future__ import annotations
 
@@ -54,62 +54,6 @@ class FireResult:
     refire: bool = False
     seq: int = 0            # the operator's batch count when the firing was triggered (1-based
                             # process() call; latency accounting of deferred results)
-
-
-@dataclass
-class _PendingFire:
-    """A firing whose rows are on their way to the host (CountedHostRows): stands in the output
-    list at its place until resolved (KeyedWindowOperator._resolve)."""
-    rows: "CountedHostRows"
-    wins: list              # window starts of the group, in firing order
-    kv: bool                # compact (key id, value) rows
-    only_dirty: bool
-    bounds: bool            # per-window cumulative counts in fixed(1); else the count is flags[2]
-    seq: int = 0
-
-
-@dataclass
-class _Front:
-    """One batch whose partition has been enqueued (S0) and whose reduced vector is on its way
-    to pinned host memory."""
-    keys: torch.Tensor
-    ts: torch.Tensor
-    vals: torch.Tensor
-    n: int
-    par: int
-    old_wm: int
-    pane_base: int
-    proc_now: int
-    rw: int = 3
-    ev: object = None
-    idle: bool = False
-
-
-@dataclass
-class _Back:
-    """The state half of one step, planned on the host after its sync."""
-    par: int
-    n: int
-    old_wm: int
-    rw: int
-    pane_base: int
-    has_data: bool = False
-    qmin: int = 0
-    np_step: int = 0
-    pg: int = 1
-    gmin: int = 0
-    gmax: int = -1
-    fired_hi: int = I64_MIN
-    new_wm: int | None = None
-    ccap: int = 0
-    hard: int = 0
-    chk_ev: object = None
-    chk_dev: object = None  # all-reduced combiner check on the device (AggPlan.skip)
-    aplan: object = None    # the step's aggregation plan (redo after a combiner overflow)
-    maxb: int = 0  # largest bucket fill of the step's partition (0: not reported)
-    pmask: int = 0  # relative panes with records (GPU partition, one rank's own records)
-    np_act: int = 0  # panes the aggregation visits (popcount(pmask), else np_step)
-    seq: int = 0   # metrics.steps after this batch (FireResult.seq of what it fires)
 
 
 @dataclass

@@ -261,6 +261,10 @@ class StageTimer:
 
         return _Ctx()
 
+    def add(self, name: str, ms: float) -> None:
+        """A stage time measured elsewhere (the native window step's own stage clocks)."""
+        self.registry.histogram(f"{self.scope}.step_ms.{name}").update(ms)
+
     def flush(self) -> None:
         """Resolve recorded GPU events (call after a sync point)."""
         from . import trace

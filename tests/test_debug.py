@@ -62,17 +62,22 @@ def test_corruptions_are_detected():
 
 
 def test_debug_mode_checks_every_step(monkeypatch):
+    """MXS_DEBUG: the native step checks the table invariants after every aggregation; a corrupted
+    table (a key moved to another sub-table) stops the next step with the step number."""
     monkeypatch.setenv("MXS_DEBUG", "1")
-    calls = []
-    orig = D.assert_table_ok
-
-    def spy(*a, **kw):
-        calls.append(kw.get("where"))
-        return orig(*a, **kw)
-
-    monkeypatch.setattr(D, "assert_table_ok", spy)
-    _populated_op("cpu")
-    assert calls and calls[0].startswith("after step")
+    op = _populated_op("cpu")  # clean steps pass the check
+    keys = op.keys_g
+    live = torch.nonzero(keys != -1).flatten()
+    cap = 1 << op.cap_log2
+    s0 = int(live[0])
+    other = (s0 // cap + 1) % op.nsub
+    free = (keys[other * cap:(other + 1) * cap] == -1).nonzero().flatten()
+    keys[other * cap + int(free[0])] = keys[s0]
+    keys[s0] = -1
+    k = torch.full((16,), 7, dtype=torch.int64)
+    t = torch.full((16,), 500, dtype=torch.int64)
+    with pytest.raises(RuntimeError, match="invariant violated after step 2"):
+        op.process(k, t, torch.ones(16, dtype=torch.int64))
 
 
 def test_host_sanitizer_harness():

@@ -421,9 +421,7 @@ def test_spill_tier_gpu_matches_unbounded_cpu(gpu_device, pane_sort, monkeypatch
     unbounded C++-twin table."""
     import sys
 
-    from mxstream.runtime import window_tiering as WT
-
-    monkeypatch.setattr(WT, "_EVICT_PANE_SORT", pane_sort)
+    monkeypatch.setenv("MXS_EVICT_PANE_SORT", "1" if pane_sort else "0")
 
     sys.path.insert(0, __import__("os").path.dirname(__file__))
     from test_window_operator_cpu import _drift_batches, _run_windows
@@ -568,7 +566,7 @@ def test_async_fire_equals_sync_fire(gpu_device, emit, pipeline, monkeypatch):
         op = KeyedWindowOperator(size=6000, slide=1000, lateness=3000, agg=K.AGG_SUM_I64,
                                  device=gpu_device, max_keys=100_000, batch_capacity=200_000,
                                  ooo_bound=500, dense_keys=True, emit=emit, pipeline=pipeline)
-        assert op._async_fire == async_fire
+        assert op.async_fire == async_fire
         rows, tags = [], []
         for step in range(16):
             k = torch.empty(200_000, dtype=torch.int64, device=gpu_device)
@@ -670,7 +668,7 @@ def test_two_level_partition_equals_plain(gpu_device, key_dtype, monkeypatch):
         op = KeyedWindowOperator(size=4000, slide=1000, lateness=2000, agg=K.AGG_SUM_I64,
                                  device=gpu_device, max_keys=3_000_000, batch_capacity=1 << 20,
                                  ooo_bound=300, dense_keys=True, narrow=True)
-        assert op.nbuckets > 512 and (op._scratch is not None) == two_level
+        assert op.nbuckets > 512 and op.two_level == two_level
         rows = []
         for step in range(9):
             k = torch.empty(1 << 20, dtype=key_dtype, device=gpu_device)
@@ -762,11 +760,9 @@ def test_forced_agg_split_equals_default(gpu_device, split, monkeypatch):
     """MXS_AGG_FORCE_SPLIT (A/B knob): every dense sub-table folded by `split` workgroups whose
     partial sums merge with atomics (and the packed accumulators each share allows) gives the
     same windows as one workgroup per sub-table."""
-    import mxstream.runtime.window_agg as WA
-
     res = {}
     for n_split in (0, split):
-        monkeypatch.setattr(WA, "_FORCE_SPLIT", n_split)
+        monkeypatch.setenv("MXS_AGG_FORCE_SPLIT", str(n_split))
         op = KeyedWindowOperator(size=2000, agg=K.AGG_SUM_I64, device=gpu_device,
                                  max_keys=1 << 16, batch_capacity=1 << 18, ooo_bound=300,
                                  dense_keys=True)

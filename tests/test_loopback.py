@@ -553,7 +553,7 @@ def test_combiner_overflow_redone_after_the_exchange(dev, pipeline, lateness):
         op = make(comm, per, pipeline)
         out = []
         for step in range(STEPS):
-            op._ccap_hint = 64  # force an overflow of the combined buckets
+            op.set_combine_hint(64)  # force an overflow of the combined buckets
             out += op.process(*_batch(dev, comm.rank, step, per, nkeys, late=late))
         out += op.finish()
         return _collect_seq(out), op.metrics.extra.get("combine_regrows", 0)
