@@ -135,7 +135,8 @@ void step_begin(uint32_t* cursor, int nb, int64_t* stats) {
 }
 
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
-                 int64_t proc_now, int64_t* red, const uint32_t* flags, int32_t idle) {
+                 int64_t proc_now, int64_t* red, const uint32_t* flags, int32_t idle,
+                 int32_t fill_word, const uint32_t* cursor, int nb) {
   int64_t lm = std::max(local_maxts[0], stats[kStatMaxTs]);
   local_maxts[0] = lm;
   const int64_t wm = event_mode ? (lm == INT64_MIN ? INT64_MIN : lm - bound) : proc_now;
@@ -144,6 +145,11 @@ void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int3
   red[1] = stats[kStatMinPane];
   red[2] = idle ? INT64_MAX : wm;
   red[3] = -(stats[kStatOverflow] & 1);
+  if (fill_word && cursor) {
+    uint32_t m = 0;
+    for (int i = 0; i < nb; ++i) m = std::max(m, cursor[i]);
+    red[3] = (stats[kStatOverflow] & 1) ? -((int64_t)1 << 40) : -(int64_t)m;
+  }
   red[4] = -((stats[kStatOverflow] >> 1) & 1);
   // Record width a value needs: -2 = 24-byte records, -1 = 16-byte records, 0 = as planned.
   red[5] = (stats[kStatOverflow] & 4) ? -2 : (stats[kStatOverflow] & 16) ? -1 : 0;
@@ -683,6 +689,17 @@ void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t*
     r.t = 0;
     r.aux = cnt[i];
   }
+}
+
+void bucket_repack(const uint64_t* src, const uint32_t* counts, int nb, uint32_t src_cap,
+                   uint32_t dst_cap, int words, uint64_t* dst, uint64_t* xstat) {
+  for (int b = 0; b < nb; ++b) {
+    const uint32_t c = std::min(counts[b], dst_cap);
+    std::memcpy(dst + (size_t)b * dst_cap * words, src + (size_t)b * src_cap * words,
+                (size_t)c * words * 8);
+    if (xstat) xstat[1] += (uint64_t)c * words * 8;
+  }
+  if (xstat) xstat[0] += (uint64_t)nb * dst_cap * words * 8;
 }
 
 void tier_merge(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt, int64_t n,

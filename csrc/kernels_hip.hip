@@ -1090,7 +1090,21 @@ __global__ __launch_bounds__(256) void step_begin_kernel(uint32_t* __restrict__ 
 __global__ void step_finish_kernel(const int64_t* __restrict__ stats, int64_t* __restrict__ local_maxts,
                                    int64_t bound, int32_t event_mode, int64_t proc_now,
                                    int64_t* __restrict__ red, const uint32_t* __restrict__ flags,
-                                   int32_t idle, int64_t* __restrict__ host_red) {
+                                   int32_t idle, int64_t* __restrict__ host_red, int32_t fill_word,
+                                   const uint32_t* __restrict__ cursor, int nb) {
+  // fill_word: the largest bucket fill, from the cursors (every partition variant fills them)
+  __shared__ uint32_t fmax[64];
+  if (fill_word) {
+    uint32_t m = 0;
+    for (int i = threadIdx.x; i < nb; i += 64) m = cursor[i] > m ? cursor[i] : m;
+    fmax[threadIdx.x] = m;
+    __syncthreads();
+    for (int s = 32; s > 0; s >>= 1) {
+      if ((int)threadIdx.x < s && fmax[threadIdx.x + s] > fmax[threadIdx.x])
+        fmax[threadIdx.x] = fmax[threadIdx.x + s];
+      __syncthreads();
+    }
+  }
   // One lane per word of the reduced vector (16 words).
   const int j = threadIdx.x;
   if (j >= 16) return;
@@ -1109,7 +1123,9 @@ __global__ void step_finish_kernel(const int64_t* __restrict__ stats, int64_t* _
     }
     case 1: v = stats[kStatMinPane]; break;
     case 2: v = idle ? INT64_MAX : wm; break;  // an idle partition has no say in the MIN
-    case 3: v = -(ovf & 1); break;
+    case 3:
+      v = !fill_word ? -(ovf & 1) : (ovf & 1) ? -((int64_t)1 << 40) : -(int64_t)fmax[0];
+      break;
     case 4: v = -((ovf >> 1) & 1); break;
     // Record width a value needs: -2 = 24-byte records, -1 = 16-byte records, 0 = as planned.
     case 5: v = (ovf & 4) ? -2 : (ovf & 16) ? -1 : 0; break;
@@ -1125,6 +1141,60 @@ __global__ __launch_bounds__(256) void combine_check_kernel(const uint32_t* __re
                                                             const uint32_t* __restrict__ counts,
                                                             int nb, int64_t* __restrict__ chk) {
   __shared__ uint32_t mx[256];
+  __shared__ uint64_t sm[256];
+  uint32_t m = 0;
+  uint64_t sum = 0;
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    m = counts[i] > m ? counts[i] : m;
+    sum += counts[i];
+  }
+  mx[threadIdx.x] = m;
+  sm[threadIdx.x] = sum;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      if (mx[threadIdx.x + s] > mx[threadIdx.x]) mx[threadIdx.x] = mx[threadIdx.x + s];
+      sm[threadIdx.x] += sm[threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    chk[0] = -(int64_t)(flags[0] & 2u);
+    chk[1] = -(int64_t)mx[0];
+    chk[2] = (int64_t)sm[0];  // records combined on this rank (payload accounting; not reduced)
+  }
+}
+
+// One workgroup per bucket: the bucket's records (words u64 each) copied as 16-byte vectors where
+// the whole run is 16-byte aligned (rec words even or stride-aligned), else word by word.
+__global__ __launch_bounds__(256) void bucket_repack_kernel(const uint64_t* __restrict__ src,
+                                                            const uint32_t* __restrict__ counts,
+                                                            uint32_t src_cap, uint32_t dst_cap,
+                                                            int words, uint64_t* __restrict__ dst,
+                                                            unsigned long long* __restrict__ xstat) {
+  const int b = blockIdx.x;
+  const uint32_t c = counts[b] < dst_cap ? counts[b] : dst_cap;
+  const uint64_t* s = src + (size_t)b * src_cap * words;
+  uint64_t* d = dst + (size_t)b * dst_cap * words;
+  const size_t nw = (size_t)c * words;
+  if (!(((uintptr_t)s | (uintptr_t)d) & 15)) {
+    const size_t nv = nw / 2;
+    const uint4* s4 = (const uint4*)s;
+    uint4* d4 = (uint4*)d;
+    for (size_t i = threadIdx.x; i < nv; i += blockDim.x) d4[i] = s4[i];
+    if ((nw & 1) && threadIdx.x == 0) d[nw - 1] = s[nw - 1];
+  } else {
+    for (size_t i = threadIdx.x; i < nw; i += blockDim.x) d[i] = s[i];
+  }
+  if (xstat && threadIdx.x == 0) {
+    atomicAdd(&xstat[1], (unsigned long long)nw * 8ull);
+    atomicAdd(&xstat[0], (unsigned long long)dst_cap * words * 8ull);
+  }
+}
+
+__global__ __launch_bounds__(256) void neg_max_u32_kernel(const uint32_t* __restrict__ counts, int nb,
+                                                          int64_t* __restrict__ out) {
+  __shared__ uint32_t mx[256];
   uint32_t m = 0;
   for (int i = threadIdx.x; i < nb; i += 256) m = counts[i] > m ? counts[i] : m;
   mx[threadIdx.x] = m;
@@ -1133,10 +1203,7 @@ __global__ __launch_bounds__(256) void combine_check_kernel(const uint32_t* __re
     if ((int)threadIdx.x < s && mx[threadIdx.x + s] > mx[threadIdx.x]) mx[threadIdx.x] = mx[threadIdx.x + s];
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    chk[0] = -(int64_t)(flags[0] & 2u);
-    chk[1] = -(int64_t)mx[0];
-  }
+  if (threadIdx.x == 0) out[0] = -(int64_t)mx[0];
 }
 
 __global__ __launch_bounds__(256) void widen_i32_kernel(const int32_t* __restrict__ in, int64_t n,
@@ -4260,9 +4327,11 @@ void step_begin(uint32_t* cursor, int nb, int64_t* stats, intptr_t stream) {
 
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
                  int64_t proc_now, int64_t* red, const uint32_t* flags, intptr_t stream,
-                 int32_t idle, int64_t* host_red) {
+                 int32_t idle, int64_t* host_red, int32_t fill_word, const uint32_t* cursor,
+                 int nb) {
   hipLaunchKernelGGL(step_finish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, stats,
-                     local_maxts, bound, event_mode, proc_now, red, flags, idle, host_red);
+                     local_maxts, bound, event_mode, proc_now, red, flags, idle, host_red,
+                     fill_word && cursor ? 1 : 0, cursor, nb);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -4270,6 +4339,20 @@ void combine_check(const uint32_t* flags, const uint32_t* counts, int nb, int64_
                    intptr_t stream) {
   hipLaunchKernelGGL(combine_check_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, flags,
                      counts, nb, chk);
+  HIP_CHECK(hipGetLastError());
+}
+
+void bucket_repack(const uint64_t* src, const uint32_t* counts, int nb, uint32_t src_cap,
+                   uint32_t dst_cap, int words, uint64_t* dst, uint64_t* xstat, intptr_t stream) {
+  if (nb <= 0) return;
+  hipLaunchKernelGGL(bucket_repack_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, src,
+                     counts, src_cap, dst_cap, words, dst, (unsigned long long*)xstat);
+  HIP_CHECK(hipGetLastError());
+}
+
+void neg_max_u32(const uint32_t* counts, int nb, int64_t* out, intptr_t stream) {
+  hipLaunchKernelGGL(neg_max_u32_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, counts, nb,
+                     out);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -394,14 +394,26 @@ void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_
 // idle: this partition is idle (red[2] = +inf: no say in the MIN watermark); host_red: also
 // store the reduced vector into this pinned host buffer (one rank: no all-reduce in between, so
 // the step's host read needs no separate copy).
+// fill_word (with the bucket cursors): red[3] carries -(largest bucket fill) instead of
+// -(overflow bit) (an overflow is -2^40): the MIN all-reduce then gives every rank the global
+// fill that sizes the exchange.
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
                  int64_t proc_now, int64_t* red, const uint32_t* flags, intptr_t stream,
-                 int32_t idle = 0, int64_t* host_red = nullptr);
+                 int32_t idle = 0, int64_t* host_red = nullptr, int32_t fill_word = 0,
+                 const uint32_t* cursor = nullptr, int nb = 0);
 // The combiner's overflow check as a MIN all-reduce operand: chk = [-(flags[0] & 2),
-// -max(counts[0..nb))].
+// -max(counts[0..nb))], and chk[2] = sum(counts) (this rank's combined records).
 void combine_check(const uint32_t* flags, const uint32_t* counts, int nb, int64_t* chk,
                    intptr_t stream);
 void fill_u64(uint64_t* p, int64_t n, uint64_t v, intptr_t stream);
+// Exchange repack (keyBy all-to-all without padding): bucket b's first min(counts[b], dst_cap)
+// records (`words` u64 words each) from stride src_cap to stride dst_cap, so the equal-split
+// all-to-all moves dst_cap-record slices sized to the largest fill over all ranks instead of the
+// fixed partition capacity. xstat (optional): += [dst bytes, payload bytes] of this repack.
+void bucket_repack(const uint64_t* src, const uint32_t* counts, int nb, uint32_t src_cap,
+                   uint32_t dst_cap, int words, uint64_t* dst, uint64_t* xstat, intptr_t stream);
+// -max(counts[0..nb)) into *out (a MIN all-reduce operand: the largest fill over the ranks).
+void neg_max_u32(const uint32_t* counts, int nb, int64_t* out, intptr_t stream);
 // Sign-extend int32 key ids to int64 (paths that do not read an int32 key column).
 void widen_i32(const int32_t* in, int64_t n, int64_t* out, intptr_t stream);
 void scatter_partials(const uint64_t* keys, const uint64_t* acc, const uint32_t* cnt,
@@ -491,7 +503,10 @@ void rolling_rows(const Rec* recs, const uint32_t* counts, int nsrc, int nsub, u
                   uint32_t* flags, const ExprProg& filt, uint64_t* out_key, uint64_t* out_val,
                   int64_t* out_tag, uint32_t* out_n, uint32_t out_cap, uint32_t count_n = 0);
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
-                 int64_t proc_now, int64_t* red, const uint32_t* flags, int32_t idle = 0);
+                 int64_t proc_now, int64_t* red, const uint32_t* flags, int32_t idle = 0,
+                 int32_t fill_word = 0, const uint32_t* cursor = nullptr, int nb = 0);
+void bucket_repack(const uint64_t* src, const uint32_t* counts, int nb, uint32_t src_cap,
+                   uint32_t dst_cap, int words, uint64_t* dst, uint64_t* xstat);
 void keygroups(const uint64_t* keys, int64_t n, int hash_mode, const int32_t* jhash, int max_par,
                int32_t* kg);
 void table_insert(const uint64_t* keys, int64_t n, int nsub_log2, int cap_log2, uint64_t* keys_g,

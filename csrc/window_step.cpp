@@ -372,6 +372,8 @@ void WindowStep::init_owner_tables(int64_t max_keys) {
   fbcap_ = (int64_t)1 << cap_log2_o_;
   const int64_t nbf = (int64_t)world_ << nsub_o_log2_;
   fsend_ = mem_alloc(nbf * fbcap_ * 24, dk, false);
+  fxsend_ = mem_alloc(nbf * fbcap_ * 24, dk, false);
+  fmax_ = mem_alloc(16, dk);
   frecv_ = mem_alloc(nbf * fbcap_ * 24, dk, false);
   fcursor_ = mem_alloc(nbf * 4, dk);
   frecv_counts_ = mem_alloc(nbf * 4, dk);
@@ -402,6 +404,7 @@ void WindowStep::alloc_buckets(int64_t capacity, double slack) {
   recv_ = exchanging_ && !combine_ ? mem_alloc(words * 8, dk, false) : nullptr;
   recv_counts_ = exchanging_ ? mem_alloc(nbuckets_ * 4, dk) : nullptr;
   scratch_ = scratch_cursor_ = nullptr;
+  xsend_ = nullptr;  // the exchange's repack buffer follows the bucket capacity
   if (two_level_ok()) {
     scratch_ = mem_alloc((size_t)nbuckets_ * bucket_cap_ * 8, dk, false);
     scratch_cursor_ = mem_alloc(512 * 4, dk);
@@ -459,7 +462,6 @@ void WindowStep::reset_state(int64_t ring) {
   }
   memset_async(occ_, 0, 0, occ_->bytes);
   pending_.reset();
-  unverified_.reset();
   evict_pending_.reset();
   queue_.clear();
   done_.clear();
@@ -589,7 +591,6 @@ void WindowStep::process(const void* keys, bool key32, const int64_t* ts, const 
                          int64_t n, intptr_t stream, const float* vecs) {
   cur_ = s0_ = (hipStream_t)stream;
   block_hint_ = !pipeline_;
-  verify_combine();
   if (!pipeline_) {
     Front f = front(keys, key32, ts, vals, vecs, n);
     Back b = settle(f);
@@ -624,7 +625,6 @@ void WindowStep::process(const void* keys, bool key32, const int64_t* ts, const 
 
 void WindowStep::flush(intptr_t stream) {
   cur_ = s0_ = (hipStream_t)stream;
-  verify_combine();
   std::unique_ptr<Back> prev = std::move(pending_);
   if (prev) {
     {
@@ -633,7 +633,6 @@ void WindowStep::flush(intptr_t stream) {
     }
     back_finish(*prev);
   }
-  verify_combine();
 }
 
 void WindowStep::advance_watermark(int64_t wm, intptr_t stream) {
@@ -772,7 +771,7 @@ void WindowStep::launch_front(Front& f) {
                      pplan_, P<int32_t>(kg_dest_), cur, send, stats, li, lcap, s);
     gpu::step_finish(stats, P<int64_t>(local_maxts_), bound, ev, f.proc_now, red,
                      P<uint32_t>(flags_), s, f.idle ? 1 : 0,
-                     world_ == 1 ? P<int64_t>(hred_[p]) : nullptr);
+                     world_ == 1 ? P<int64_t>(hred_[p]) : nullptr, exchanging_ ? 1 : 0, cur, nb);
   } else {
     cpu::step_begin(cur, nb, stats);
     std::vector<uint64_t> wide;
@@ -787,7 +786,7 @@ void WindowStep::launch_front(Front& f) {
       cpu::partition((const uint64_t*)keys, f.ts, (const uint64_t*)f.vals, cfg_.jhash, f.n, pplan_,
                      P<int32_t>(kg_dest_), cur, send, stats, li, lcap);
     cpu::step_finish(stats, P<int64_t>(local_maxts_), bound, ev, f.proc_now, red,
-                     P<uint32_t>(flags_), f.idle ? 1 : 0);
+                     P<uint32_t>(flags_), f.idle ? 1 : 0, exchanging_ ? 1 : 0, cur, nb);
   }
   // Watermark valve + pane range + every overflow flag: ONE MIN all-reduce per step.
   if (world_ > 1) comm_->allreduce_min_i64(red, 8, (intptr_t)cur_);
@@ -819,8 +818,9 @@ WindowStep::Back WindowStep::settle(Front& f) {
       // A record does not fit the format: wider records from now on.
       rec_w_ = need_rw;
       ++m_.compact_fallbacks;
-    } else if (host[3]) {
-      // A bucket overflowed somewhere: grow the fixed bucket capacity and redo the step.
+    } else if (exchanging_ ? -host[3] >= ((int64_t)1 << 40) : host[3] != 0) {
+      // A bucket overflowed somewhere: grow the fixed bucket capacity and redo the step. (With
+      // the records exchange the word carries the largest fill over the ranks instead.)
       ++m_.bucket_regrows;
       alloc_buckets(batch_capacity_, slack_ * 2);
     } else {
@@ -848,6 +848,8 @@ WindowStep::Back WindowStep::settle(Front& f) {
   b.rw = f.rw;
   b.pane_base = f.pane_base;
   b.maxb = stv[kStatMaxBucket];
+  b.fill = exchanging_ ? -host[3] : stv[kStatMaxBucket];
+  b.accepted = stv[kStatAccepted];
   b.seq = m_.steps + 1;
   b.vecs = f.vecs;
   if (qmin <= qmax) {
@@ -916,7 +918,7 @@ void WindowStep::back_finish(Back& b) {
       combined = 1;
     } else if (exchanging_) {
       Stage stage(this, "all_to_all");
-      exchange_records(b);
+      exchange_records(b, &bcap);
     }
     if (gpu_ && exchanging_) {
       if (!ev_consumed_[b.par]) ev_consumed_[b.par] = new_event();
@@ -954,15 +956,9 @@ void WindowStep::back_finish(Back& b) {
       ap.dacc = P<uint64_t>(dacc_g_);
       ap.dcnt = P<uint32_t>(dcnt_g_);
     }
-    if (combined) ap.skip = P<int64_t>(chk_);
     {
       Stage stage(this, "window_agg");
       aggregate(recs, counts, ap, &b);
-    }
-    if (combined) {
-      b.aplan = ap;
-      b.aplan_set = true;
-      unverified_.reset(new Back(b));
     }
     if (gpu_ && !exchanging_) {
       if (!ev_consumed_[b.par]) ev_consumed_[b.par] = new_event();
@@ -1029,35 +1025,48 @@ void WindowStep::aggregate(const Rec* recs, const uint32_t* counts, AggPlan& ap,
                     P<uint8_t>(dirty_g_), P<uint32_t>(occ_), P<uint32_t>(flags_));
 }
 
-void WindowStep::exchange_records(Back& b) {
-  // G > 1 without the combiner: the equal-split all-to-all of the bucket ranges. Buckets hold
-  // records of rw words (8-byte RecN: rw 1), so each rank's chunk is a prefix share.
-  const int64_t words = (int64_t)nbuckets_ * bucket_cap_ * b.rw;
+void WindowStep::exchange_records(Back& b, uint32_t* xcap_out) {
+  // G > 1 without the combiner: the buckets are repacked to a stride of the largest fill over
+  // all ranks (all-reduced with the step's MIN vector), then ONE equal-split all-to-all moves
+  // nbuckets x that stride records of rw words -- not the partition's fixed capacity (which
+  // carries 1.5x slack): no padding crosses xGMI beyond the fill spread between buckets.
+  const int rw = b.rw;
+  const uint32_t xcap = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(b.fill, bucket_cap_));
+  if (!xsend_) xsend_ = mem_alloc((size_t)nbuckets_ * bucket_cap_ * 24, gpu_ ? 1 : 0, false);
+  if (gpu_)
+    gpu::bucket_repack(P<uint64_t>(send_[b.par]), P<uint32_t>(cursor_[b.par]), nbuckets_,
+                       (uint32_t)bucket_cap_, xcap, rw, P<uint64_t>(xsend_), nullptr, (intptr_t)cur_);
+  else
+    cpu::bucket_repack(P<uint64_t>(send_[b.par]), P<uint32_t>(cursor_[b.par]), nbuckets_,
+                       (uint32_t)bucket_cap_, xcap, rw, P<uint64_t>(xsend_), nullptr);
+  const int64_t words = (int64_t)nbuckets_ * xcap * rw;
   if (cfg_.dim > 0) {
-    const int64_t need = (int64_t)nbuckets_ * bucket_cap_ * cfg_.dim;
+    const int64_t need = (int64_t)nbuckets_ * xcap * cfg_.dim;
     if (!send_vec_ || (int64_t)send_vec_->bytes < need * 4) {
       send_vec_ = mem_alloc(need * 4, gpu_ ? 1 : 0);
       recv_vec_ = mem_alloc(need * 4, gpu_ ? 1 : 0);
     }
     if (gpu_)
-      gpu::vec_gather(send_[b.par]->p, b.rw, P<uint32_t>(cursor_[b.par]), nbuckets_,
-                      (uint32_t)bucket_cap_, b.vecs, cfg_.dim, P<float>(send_vec_), (intptr_t)cur_);
+      gpu::vec_gather(xsend_->p, rw, P<uint32_t>(cursor_[b.par]), nbuckets_, xcap, b.vecs,
+                      cfg_.dim, P<float>(send_vec_), (intptr_t)cur_);
     else
-      cpu::vec_gather(send_[b.par]->p, b.rw, P<uint32_t>(cursor_[b.par]), nbuckets_,
-                      (uint32_t)bucket_cap_, b.vecs, cfg_.dim, P<float>(send_vec_));
+      cpu::vec_gather(xsend_->p, rw, P<uint32_t>(cursor_[b.par]), nbuckets_, xcap, b.vecs,
+                      cfg_.dim, P<float>(send_vec_));
     comm_->all_to_all(recv_vec_->p, send_vec_->p, need * 4, 4, (intptr_t)cur_);
     m_.a2a_bytes += need * 4;
+    m_.payload_bytes += b.accepted * cfg_.dim * 4;
   }
-  comm_->all_to_all(recv_->p, send_[b.par]->p, words * 8, 8, (intptr_t)cur_);
+  comm_->all_to_all(recv_->p, xsend_->p, words * 8, 8, (intptr_t)cur_);
   comm_->all_to_all(recv_counts_->p, cursor_[b.par]->p, (int64_t)nbuckets_ * 4, 4, (intptr_t)cur_);
   m_.a2a_bytes += words * 8;
-  m_.payload_bytes += b.n * 8 * b.rw;
+  m_.payload_bytes += b.accepted * rw * 8;
+  *xcap_out = xcap;
 }
 
 // ---- records exchange with the sender-side combiner -------------------------------------------
 void WindowStep::combine_begin(Back& b) {
   // Pre-aggregate every send bucket to one record per (key, pane); the global overflow flag and
-  // largest fill go through one small MIN all-reduce into pinned memory (read by verify_combine).
+  // largest fill go through one small MIN all-reduce into pinned memory (read by combine_finish).
   const int64_t cap = (int64_t)1 << cap_log2_;
   const int64_t hard = std::min<int64_t>(bucket_cap_, cap * b.np_step);
   const int64_t ccap = std::min<int64_t>(hard, std::max<int64_t>(64, ((int64_t)ccap_hint_ + 7) & ~7));
@@ -1094,67 +1103,62 @@ void WindowStep::combine_begin(Back& b) {
     const uint32_t* cc = P<uint32_t>(comb_counts_);
     uint32_t mx = 0;
     for (int i = 0; i < nbuckets_; ++i) mx = std::max(mx, cc[i]);
+    int64_t sum = 0;
+    for (int i = 0; i < nbuckets_; ++i) sum += cc[i];
     P<int64_t>(chk_)[0] = -(int64_t)(P<uint32_t>(flags_)[1] & 2u);
     P<int64_t>(chk_)[1] = -(int64_t)mx;
+    P<int64_t>(chk_)[2] = sum;
   }
   if (world_ > 1) comm_->allreduce_min_i64(P<int64_t>(chk_), 2, (intptr_t)cur_);
   b.ccap = (uint32_t)ccap;
   b.hard = (uint32_t)hard;
   if (gpu_) {
-    hip_ok(hipMemcpyAsync(hchk_->p, chk_->p, 16, hipMemcpyDeviceToHost, cur_), "D2H");
+    hip_ok(hipMemcpyAsync(hchk_->p, chk_->p, 24, hipMemcpyDeviceToHost, cur_), "D2H");
     if (!b.chk_ev) b.chk_ev = new_event();
     record(b.chk_ev, cur_);
   } else {
-    std::memcpy(hchk_->p, chk_->p, 16);
+    std::memcpy(hchk_->p, chk_->p, 24);
     b.chk_ev = nullptr;
   }
 }
 
 void WindowStep::combine_finish(Back& b, const Rec** recs, const uint32_t** counts, uint32_t* bcap) {
-  // The all-to-all of the combined buckets, without waiting for the overflow check: the step's
-  // aggregation skips itself on the device when the all-reduced check reports an overflow
-  // (AggPlan.skip), and verify_combine redoes the exchange with larger buckets later.
-  const int64_t bytes = (int64_t)nbuckets_ * b.ccap * 24;
-  comm_->all_to_all(comb_recv_->p, comb_send_->p, bytes, 8, (intptr_t)cur_);
-  comm_->all_to_all(recv_counts_->p, comb_counts_->p, (int64_t)nbuckets_ * 4, 4, (intptr_t)cur_);
-  m_.a2a_bytes += bytes;
-  m_.payload_bytes += b.n * 8 * b.rw;
-  *recs = P<Rec>(comb_recv_);
-  *counts = P<uint32_t>(recv_counts_);
-  *bcap = b.ccap;
-}
-
-void WindowStep::verify_combine() {
-  // Read the overflow check of the last combined exchange; on overflow (every rank sees the same
-  // all-reduced check) recombine the step's send buckets with twice the capacity, exchange again
-  // and aggregate. Called before anything reads or replaces the state.
-  std::unique_ptr<Back> b = std::move(unverified_);
-  if (!b) return;
-  StreamScope sc(this, true);
-  bool redo = false;
+  // The combined buckets cross ONE all-to-all at a stride of the largest combined fill over all
+  // ranks: the all-reduced check (overflow bit, largest fill) is read first -- a short host wait
+  // on the combine, while the next batch's partition keeps the GPU busy -- an overflow is redone
+  // with twice the capacity right here, and the buckets are repacked to the fill (no padding
+  // crosses xGMI beyond the fill spread between buckets).
   int64_t ovf = 0, fill = 0;
   for (;;) {
-    if (b->chk_ev) host_wait(b->chk_ev);
+    if (b.chk_ev) host_wait(b.chk_ev);
     ovf = -P<int64_t>(hchk_)[0];
     fill = -P<int64_t>(hchk_)[1];
     if (!ovf) break;
-    if (b->ccap >= b->hard)
+    if (b.ccap >= b.hard)
       throw std::runtime_error("window_combine: a send bucket exceeds its sub-table capacity");
-    ccap_hint_ = b->ccap * 2;
+    ccap_hint_ = b.ccap * 2;
     ++m_.combine_regrows;
-    combine_begin(*b);
-    redo = true;
+    combine_begin(b);
   }
-  ccap_hint_ = (uint32_t)std::max<int64_t>(64, (int64_t)(fill * 1.25) + 8);
-  if (redo) {
-    const Rec* recs = nullptr;
-    const uint32_t* counts = nullptr;
-    uint32_t bcap = 0;
-    combine_finish(*b, &recs, &counts, &bcap);
-    b->aplan.bucket_cap = bcap;
-    b->aplan.skip = nullptr;
-    aggregate(recs, counts, b->aplan, b.get());
-  }
+  m_.payload_bytes += P<int64_t>(hchk_)[2] * 24;
+  // next step's combined capacity: this step's global fill + 10 % (an overflow is redone above)
+  ccap_hint_ = (uint32_t)std::max<int64_t>(64, (int64_t)(fill * 1.10) + 16);
+  const uint32_t x = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(fill, b.ccap));
+  if (!comb_x_ || comb_x_->bytes < (size_t)nbuckets_ * x * 24)
+    comb_x_ = mem_alloc((size_t)nbuckets_ * b.ccap * 24, gpu_ ? 1 : 0, false);
+  if (gpu_)
+    gpu::bucket_repack(P<uint64_t>(comb_send_), P<uint32_t>(comb_counts_), nbuckets_, b.ccap, x, 3,
+                       P<uint64_t>(comb_x_), nullptr, (intptr_t)cur_);
+  else
+    cpu::bucket_repack(P<uint64_t>(comb_send_), P<uint32_t>(comb_counts_), nbuckets_, b.ccap, x, 3,
+                       P<uint64_t>(comb_x_), nullptr);
+  const int64_t bytes = (int64_t)nbuckets_ * x * 24;
+  comm_->all_to_all(comb_recv_->p, comb_x_->p, bytes, 8, (intptr_t)cur_);
+  comm_->all_to_all(recv_counts_->p, comb_counts_->p, (int64_t)nbuckets_ * 4, 4, (intptr_t)cur_);
+  m_.a2a_bytes += bytes;
+  *recs = P<Rec>(comb_recv_);
+  *counts = P<uint32_t>(recv_counts_);
+  *bcap = x;
 }
 
 // ---- firing --------------------------------------------------------------------------------
@@ -1177,7 +1181,6 @@ void WindowStep::fire_ready(int64_t wm, int64_t seq) {
 }
 
 void WindowStep::refire(int64_t pmin, int64_t pmax, int64_t old_wm, int64_t seq) {
-  verify_combine();
   fire_list(ctl_.refire_windows(pmin, pmax, old_wm), true, seq);
   if (dlist_) {
     if (gpu_)
@@ -1197,7 +1200,6 @@ void WindowStep::refire(int64_t pmin, int64_t pmax, int64_t old_wm, int64_t seq)
 }
 
 void WindowStep::fire_list(const std::vector<int64_t>& starts, bool only_dirty, int64_t seq) {
-  if (!starts.empty()) verify_combine();
   const bool batched = !local_global_ && !tier_ && cfg_.dim == 0;
   if (starts.size() > 1 && batched) {
     fire_many(starts, only_dirty, seq);
@@ -1652,10 +1654,34 @@ void WindowStep::fire_window_partials(int64_t s, int64_t p0, int64_t p1, bool on
   else
     cpu::scatter_partials(pk, pa, pc, P<uint32_t>(part_n_), sp, cfg_.jhash, P<int32_t>(kg_dest_),
                           P<uint32_t>(fcursor_), P<Rec>(fsend_), P<uint32_t>(flags_));
-  const int64_t nbf = (int64_t)world_ << nsub_o_log2_;
-  comm_->all_to_all(frecv_->p, fsend_->p, nbf * fbcap_ * 24, 8, (intptr_t)cur_);
-  comm_->all_to_all(frecv_counts_->p, fcursor_->p, nbf * 4, 4, (intptr_t)cur_);
-  m_.a2a_bytes += nbf * fbcap_ * 24;
+  // The owners' buckets hold at most one row per key of an owner sub-table (fbcap = its slot
+  // count); the all-to-all moves a stride of the largest fill over the ranks instead (one
+  // 1-word MIN all-reduce and a host read per fired window), repacked on the device.
+  const int nbf = world_ << nsub_o_log2_;
+  if (gpu_) {
+    gpu::neg_max_u32(P<uint32_t>(fcursor_), nbf, P<int64_t>(fmax_), (intptr_t)cur_);
+    hip_ok(hipMemcpyAsync(P<int64_t>(fmax_) + 1, part_n_->p, 4, hipMemcpyDeviceToDevice, cur_), "D2D");
+  } else {
+    const uint32_t* fc = P<uint32_t>(fcursor_);
+    uint32_t mx = 0;
+    for (int i = 0; i < nbf; ++i) mx = std::max(mx, fc[i]);
+    P<int64_t>(fmax_)[0] = -(int64_t)mx;
+    P<int64_t>(fmax_)[1] = *P<uint32_t>(part_n_);
+  }
+  comm_->allreduce_min_i64(P<int64_t>(fmax_), 1, (intptr_t)cur_);
+  int64_t hx[2];
+  to_host_sync(hx, fmax_->p, 16);
+  const uint32_t fx = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(-hx[0], fbcap_));
+  if (gpu_)
+    gpu::bucket_repack(P<uint64_t>(fsend_), P<uint32_t>(fcursor_), nbf, (uint32_t)fbcap_, fx, 3,
+                       P<uint64_t>(fxsend_), nullptr, (intptr_t)cur_);
+  else
+    cpu::bucket_repack(P<uint64_t>(fsend_), P<uint32_t>(fcursor_), nbf, (uint32_t)fbcap_, fx, 3,
+                       P<uint64_t>(fxsend_), nullptr);
+  comm_->all_to_all(frecv_->p, fxsend_->p, (int64_t)nbf * fx * 24, 8, (intptr_t)cur_);
+  comm_->all_to_all(frecv_counts_->p, fcursor_->p, (int64_t)nbf * 4, 4, (intptr_t)cur_);
+  m_.a2a_bytes += (int64_t)nbf * fx * 24;
+  m_.payload_bytes += (hx[1] & 0xFFFFFFFF) * 24;
   const int64_t widx = WindowControl::fdiv((__int128)s - cfg_.offset, cfg_.slide);
   const int64_t so = (widx & (ring_m_ - 1)) * nslots_o_;
   if (!only_dirty) {  // the slice's previous window is cleaned: reuse it
@@ -1670,7 +1696,7 @@ void WindowStep::fire_window_partials(int64_t s, int64_t p0, int64_t p1, bool on
   mp.ring = (int32_t)ring_m_;
   mp.agg = cfg_.agg;
   mp.nsrc = world_;
-  mp.bucket_cap = (uint32_t)fbcap_;
+  mp.bucket_cap = fx;
   mp.np_step = 1;
   mp.pg = 1;
   mp.pane_base = widx;
@@ -1846,7 +1872,6 @@ void WindowStep::purge(int64_t wm) {
   }
   int64_t p = r.from;
   const int64_t stop = r.stop;
-  if (p < stop) verify_combine();  // a redo must not land in a zeroed pane
   while (p < stop) {  // at most two runs of consecutive ring positions (wrap-around)
     const int64_t rp = p & (ring_ - 1);
     const int64_t k = std::min(stop - p, ring_ - rp);
@@ -1858,7 +1883,6 @@ void WindowStep::purge(int64_t wm) {
 
 // ---- host-DRAM spill tier ------------------------------------------------------------------------
 void WindowStep::maybe_spill() {
-  verify_combine();  // the occupancy must include a redone combined step's inserts
   const int64_t cap = (int64_t)1 << cap_log2_;
   std::vector<uint32_t> occ((size_t)nsub_);
   to_host_sync(occ.data(), occ_->p, (size_t)nsub_ * 4);
@@ -1881,7 +1905,6 @@ std::vector<int64_t> WindowStep::compact_state(bool has_cutoff, int64_t cutoff_p
   // rows go to a pinned slab by the counted copy kernel on the copy stream, with no host sync;
   // the tier absorbs them at the next point that reads it (land_evictions).
   if (stream) cur_ = (hipStream_t)stream;
-  verify_combine();
   if (dense_bits_) return {0, 0, 0};
   if (has_cutoff && !tier_) throw std::invalid_argument("evicting keys needs the spill tier (spill=True)");
   land_evictions();

@@ -262,9 +262,9 @@ class WindowStep {
     int64_t new_wm = 0;
     uint32_t ccap = 0, hard = 0;
     hipEvent_t chk_ev = nullptr;
-    AggPlan aplan{};
-    bool aplan_set = false;
     int64_t maxb = 0;
+    int64_t fill = 0;      // largest bucket fill (over all ranks with the records exchange)
+    int64_t accepted = 0;  // records this rank's partition kept
     uint32_t pmask = 0;
     int64_t np_act = 0, seq = 0;
     const float* vecs = nullptr;
@@ -290,8 +290,7 @@ class WindowStep {
   // combine (records exchange with the sender-side combiner)
   void combine_begin(Back& b);
   void combine_finish(Back& b, const Rec** recs, const uint32_t** counts, uint32_t* bcap);
-  void verify_combine();
-  void exchange_records(Back& b);
+  void exchange_records(Back& b, uint32_t* xcap_out);
   void aggregate(const Rec* recs, const uint32_t* counts, AggPlan& ap, const Back* b);
   bool agg_pack_ok(int rw) const;
   // firing
@@ -378,6 +377,7 @@ class WindowStep {
   int nsub_o_ = 0, nsub_o_log2_ = 0, cap_log2_o_ = 0;
   int64_t nslots_o_ = 0, ring_m_ = 1, fbcap_ = 0, mfires_ = 0;
   Buf keys_m_, acc_m_, cnt_m_, dirty_m_, occ_m_, fsend_, frecv_, fcursor_, frecv_counts_, part_n_;
+  Buf fxsend_, fmax_, xsend_, comb_x_;
   // plan caches
   PartPlan pplan_{};
   bool pplan_ok_ = false;
@@ -388,7 +388,6 @@ class WindowStep {
   hipEvent_t ready_ev_ = nullptr;
   Buf evict_slab_;
   std::unique_ptr<Back> pending_;
-  std::unique_ptr<Back> unverified_;
   hipEvent_t out_busy_ = nullptr, rout_busy_ = nullptr, tout_busy_ = nullptr;
   std::deque<FireBatch> queue_;   // firings whose rows may still be in flight, in order
   std::deque<FireRows> done_;

@@ -29,10 +29,9 @@ I64_MAX = (1 << 63) - 1
 FK_ISO_SEC = 7
 
 
-
 def _spin(ev) -> None:
-    """hipEventQuery polled in C++ with the GIL released (runtime/window_operator._event_spin)."""
-    from ..runtime.window_operator import _event_spin
+    """hipEventQuery polled in C++ with the GIL released (runtime/host_rows._event_spin)."""
+    from ..runtime.host_rows import _event_spin
 
     _event_spin(ev)
 

@@ -1,6 +1,9 @@
-"""Undefined-global check for Python modules (no linter in this image): reports names a function
-reads that are bound neither in the function (any scope inside it), nor at module level, nor as
-builtins -- the NameErrors a module split would leave for a code path no test reaches.
+"""Lint for Python modules (no linter in this image):
+
+* undefined globals: names a function reads that are bound neither in the function (any scope
+  inside it), nor at module level, nor as builtins -- the NameErrors a module split would leave
+  for a code path no test reaches;
+* blank-line debris: runs of three or more blank lines (what a mechanical split leaves behind).
 
     python scripts/check_names.py mxstream/runtime/window_operator.py [...]
 """
@@ -68,7 +71,21 @@ def check(path: str) -> list[str]:
     return sorted(set(bad))
 
 
+def blank_runs(path: str, limit: int = 3) -> list[str]:
+    """Runs of `limit` or more consecutive blank lines."""
+    bad, run = [], 0
+    lines = open(path).read().split("\n")
+    for i, line in enumerate(lines + ["x"], 1):
+        if line.strip() == "" and i <= len(lines):
+            run += 1
+            continue
+        if run >= limit and i <= len(lines):
+            bad.append(f"{path}:{i - run}: {run} blank lines in a row")
+        run = 0
+    return bad
+
+
 if __name__ == "__main__":
-    problems = [p for f in sys.argv[1:] for p in check(f)]
+    problems = [p for f in sys.argv[1:] for p in check(f) + blank_runs(f)]
     print("\n".join(problems) if problems else "ok")
     sys.exit(1 if problems else 0)
