@@ -30,9 +30,16 @@ def _words(c: torch.Tensor) -> int:
     return per // 4
 
 
-def exchange_rows(comm, dest: torch.Tensor, cols: list[torch.Tensor]) -> list[torch.Tensor]:
+class NotExchangeable(RuntimeError):
+    """Some rank flagged its rows as not encodable: every rank raises it, before any payload
+    moved (the caller switches every rank to its fallback together)."""
+
+
+def exchange_rows(comm, dest: torch.Tensor, cols: list[torch.Tensor],
+                  abort: bool = False) -> list[torch.Tensor]:
     """Rows to their destination ranks; returns the received columns (same dtypes and trailing
-    shapes). Collective: every rank calls it, with or without rows."""
+    shapes). Collective: every rank calls it, with or without rows. abort=True on any rank: every
+    rank raises NotExchangeable after the first (small) collective."""
     from ..ops.native import load
 
     world = comm.world
@@ -58,13 +65,17 @@ def exchange_rows(comm, dest: torch.Tensor, cols: list[torch.Tensor]) -> list[to
     # [largest per-destination count, bad-destination flag]: one MAX all-reduce, so a bad
     # destination on any rank is seen by every rank before the payload exchange (all raise
     # together instead of the others blocking in the all-to-all).
-    mx = torch.stack([counts.max().to(torch.int64), flags[0].to(torch.int64)])
+    mx = torch.stack([counts.max().to(torch.int64), flags[0].to(torch.int64),
+                      torch.tensor(int(abort), dtype=torch.int64, device=dev)])
     comm.allreduce_max_(mx)
     rc = torch.empty_like(counts)
     comm.all_to_all(rc, counts)
     h = torch.cat([mx, rc.to(torch.int64)]).cpu().tolist()  # one read
     if h[1]:
         raise ValueError("exchange_rows: a destination rank outside [0, world)")
+    if h[2]:
+        raise NotExchangeable("exchange_rows: a rank's rows are not encodable")
+    h = h[:2] + h[3:]
     cap = int(h[0])
     if cap == 0:
         return [c[:0] for c in cols]
@@ -87,6 +98,64 @@ def exchange_rows(comm, dest: torch.Tensor, cols: list[torch.Tensor]) -> list[to
     else:
         m.cpu_xrows_unpack(recv.data_ptr(), rc.data_ptr(), world, cap, spec_recv)
     return outs
+
+
+def exchange_records(comm, outs: list[list], last_wm: int | None):
+    """The keyBy edge of host (Python) operators: ``outs[r]`` = this rank's records (``Rec``)
+    for rank r. Records travel code-free and typed (runtime/statecodec.py JSON of each
+    destination's (value, timestamp) list, no pickle) as 32-bit words through ONE exchange_rows
+    call -- a destination receives only its own records, O(N) bytes per pass instead of every
+    rank's records on every rank. Returns (received records in source-rank order, every rank's
+    last watermark). Raises NotExchangeable on every rank when a value has no typed encoding on
+    some rank (the caller falls back to the object collective on every rank together)."""
+    import numpy as np
+
+    from ..runtime.operators import LONG_MIN, Rec
+    from ..runtime.statecodec import _Enc, decode
+
+    world = comm.world
+    blobs, abort = [], False
+    for r in range(world):
+        try:
+            enc = _Enc()
+            tree = [[enc.enc(it.value), it.ts] for it in outs[r]]
+            if enc.arrays:
+                raise TypeError("numpy arrays inside records")
+            import json
+
+            blobs.append(json.dumps(tree, allow_nan=False, separators=(",", ":")).encode()
+                         if outs[r] else b"")
+        except TypeError:
+            abort, blobs = True, [b""] * world
+            break
+    # one blob per destination: [nbytes u32][bytes padded to 4]; every word tagged with its rank
+    words, dest = [], []
+    for r, b in enumerate(blobs):
+        if not b:
+            continue
+        pad = (-len(b)) % 4
+        w = np.frombuffer(len(b).to_bytes(4, "little") + b + b"\0" * pad, dtype=np.int32)
+        words.append(w)
+        dest.append(np.full(len(w), r, dtype=np.int64))
+    # (RCCL moves device tensors: the words go through the GPU exchange kernels there)
+    dev = (torch.device("cuda", torch.cuda.current_device())
+           if getattr(comm, "backend", "") == "nccl" else torch.device("cpu"))
+    wv = torch.from_numpy(np.concatenate(words)) if words else torch.empty(0, dtype=torch.int32)
+    dv = torch.from_numpy(np.concatenate(dest)) if dest else torch.empty(0, dtype=torch.int64)
+    # every rank's last watermark: one all-to-all of world int64 (rank r sends its value to all)
+    wm = torch.full((world,), LONG_MIN if last_wm is None else int(last_wm), dtype=torch.int64,
+                    device=dev)
+    all_wm = torch.empty_like(wm)
+    comm.all_to_all(all_wm, wm)
+    got = exchange_rows(comm, dv.to(dev), [wv.to(dev)], abort=abort)[0].cpu().numpy()
+    got = got.view(np.uint8).tobytes()
+    recv, o = [], 0
+    while o < len(got):
+        nb = int.from_bytes(got[o:o + 4], "little")
+        for v, ts in decode(got[o + 4:o + 4 + nb].decode()):
+            recv.append(Rec(v, ts))
+        o += 4 + nb + ((-nb) % 4)
+    return recv, [None if w == LONG_MIN else w for w in all_wm.tolist()]
 
 
 def gather_rows(comm, cols: list[torch.Tensor]) -> list[torch.Tensor]:

@@ -334,6 +334,16 @@ class Executor:
         except Exception as e:  # noqa: BLE001 -- a user key selector failed: agreed in _control
             self._record_failure(e)
             outs, last_wm = [[] for _ in range(world)], None
+        from ..parallel.exchange import NotExchangeable, exchange_records
+
+        # Typed, code-free columnar exchange (statecodec words through exchange_rows): each rank
+        # receives only its own records. Values without a typed encoding (arbitrary user objects)
+        # make every rank fall back to the object collective together.
+        try:
+            recv, wms = exchange_records(self.comm, outs, last_wm)
+            return recv + self._merge_watermarks(n, last_wm, wms)
+        except NotExchangeable:
+            self.metrics["objectExchangeFallbacks"] = self.metrics.get("objectExchangeFallbacks", 0) + 1
         got = self.comm.all_gather_object((outs, last_wm))
         recv: list = []
         for r_outs, _ in got:

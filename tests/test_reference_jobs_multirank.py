@@ -86,12 +86,12 @@ KEYED = {"ComputeCpuMax", "ComputeCpuAvg", "ComputeCpuMiddle", "BandwidthMonitor
          "BandwidthMonitorWithEventTime", "Sessions"}
 
 
-def _run(name, comm=None, device="cpu"):
+def _run(name, comm=None, device="cpu", native="auto"):
     build, gen, timed = JOBS[name]
     lines = gen()
     out = []
     env = StreamExecutionEnvironment(4, clock=ManualClock(0)).set_output(out.append)
-    env.config.native = "auto"
+    env.config.native = native
     env.config.device = device
     env.config.text_ingest = "device"
     env._comm = comm
@@ -234,7 +234,7 @@ def test_control_plane_has_no_object_collectives(name, world):
         _steady_state_quiet(per_pass)
 
 
-def _gloo_worker(rank, world, port, name, q):
+def _gloo_worker(rank, world, port, name, q, native="auto"):
     import os
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -256,7 +256,7 @@ def _gloo_worker(rank, world, port, name, q):
         from mxstream.parallel.comm import TorchComm
 
         passes, _ = _object_spy(TorchComm, X.Executor)
-        out, _, _ = _run(name)
+        out, _, _ = _run(name, native=native)
         seen["passes"] = next(iter(passes.values()), [])
         q.put((rank, out, seen, None))
     except Exception:  # noqa: BLE001
@@ -365,3 +365,60 @@ def test_dictionary_beyond_dense_budget_moves_to_hashed_tier(world, monkeypatch)
     assert ops and all(o.op.host_tier is not None and not o.op.dense_bits for o in ops)
     assert sum(o.op.metrics.extra.get("spilled_keys", 0) for o in ops) > 0  # keys left HBM
     assert Counter(got) == Counter(ref)
+
+
+HOST_KEYED = ["ComputeCpuMiddle", "BandwidthMonitorWithEventTime"]
+
+
+@pytest.mark.parametrize("name", HOST_KEYED)
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_host_keyed_edge_has_no_object_collectives(name, world):
+    """Host (Python) operators on a keyed edge -- the planner does not lower them (native off):
+    the executor's keyBy moves the records as typed, code-free words through the hand-written
+    row exchange (parallel/exchange.exchange_records), each rank receiving only its own records;
+    no pickled all_gather_object per pass once the job runs, and the output equals one process."""
+    from mxstream.parallel.comm import LoopbackComm, run_loopback
+    from mxstream.runtime import executor as X
+
+    passes, undo = _object_spy(LoopbackComm, X.Executor)
+    try:
+        res = run_loopback(world, lambda comm: _run(name, comm, native="off"))
+    finally:
+        undo()
+    ref, _, _ = _run(name, native="off")
+    got = [l for out, _, _ in res for l in out]
+    assert Counter(_strip(got)) == Counter(_strip(ref))
+    assert all(r.metrics.get("objectExchangeFallbacks", 0) == 0 for _, r, _ in res)
+    for per_pass in passes.values():
+        assert sum(per_pass) == 0, per_pass
+
+
+def test_host_keyed_edge_gloo_processes():
+    """The same host keyed edge over two gloo processes (TorchComm)."""
+    import os
+    import socket
+
+    import torch.multiprocessing as mp
+
+    name = "ComputeCpuMiddle"
+    for k in ("RANK", "WORLD_SIZE"):
+        os.environ.pop(k, None)
+    ref, _, _ = _run(name, native="off")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, 2, port, name, q, "off")) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [e for *_, e in res if e]
+    assert not errs, errs
+    got = [l for _, lines, _, _ in res for l in lines]
+    assert Counter(_strip(got)) == Counter(_strip(ref))
+    for _, _, seen, _ in res:
+        assert sum(seen["passes"]) == 0, seen["passes"]
