@@ -1213,6 +1213,19 @@ __global__ __launch_bounds__(256) void widen_i32_kernel(const int32_t* __restric
     out[i] = (int64_t)in[i];
 }
 
+// Grid-stride zeroing of three byte ranges in one launch (the purge of a run of pane slabs).
+__global__ __launch_bounds__(256) void zero3_kernel(uint4* __restrict__ a, int64_t na,
+                                                    uint4* __restrict__ b, int64_t nb,
+                                                    uint4* __restrict__ c, int64_t nc) {
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na + nb + nc; i += stride) {
+    if (i < na) a[i] = z;
+    else if (i < na + nb) b[i - na] = z;
+    else c[i - na - nb] = z;
+  }
+}
+
 __global__ __launch_bounds__(256) void fill_u64_kernel(uint64_t* __restrict__ p, int64_t n, uint64_t v) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -4361,6 +4374,27 @@ void widen_i32(const int32_t* in, int64_t n, int64_t* out, intptr_t stream) {
   const int64_t blocks = std::min<int64_t>(8192, (n + 255) / 256);
   hipLaunchKernelGGL(widen_i32_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, in,
                      n, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void zero_panes(void* acc, int acc_bytes, uint32_t* cnt, uint8_t* dirty, int64_t so, int64_t n,
+                intptr_t stream) {
+  if (n <= 0) return;
+  // slabs are nslots-multiples of 64 slots: every range below is a whole number of 16 bytes
+  uint8_t* a = (uint8_t*)acc + so * acc_bytes;
+  uint8_t* b = (uint8_t*)(cnt + so);
+  uint8_t* c = dirty + so;
+  const int64_t na = n * acc_bytes / 16, nb = n * 4 / 16, nc = n / 16;
+  if ((((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) & 15) || (n & 15)) {
+    HIP_CHECK(hipMemsetAsync(a, 0, n * acc_bytes, (hipStream_t)stream));
+    HIP_CHECK(hipMemsetAsync(b, 0, n * 4, (hipStream_t)stream));
+    HIP_CHECK(hipMemsetAsync(c, 0, n, (hipStream_t)stream));
+    return;
+  }
+  const int64_t tot = na + nb + nc;
+  const int64_t blocks = std::min<int64_t>(2048, (tot + 255) / 256);
+  hipLaunchKernelGGL(zero3_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
+                     (uint4*)a, na, (uint4*)b, nb, (uint4*)c, nc);
   HIP_CHECK(hipGetLastError());
 }
 

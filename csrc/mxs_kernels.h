@@ -406,6 +406,10 @@ void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int3
 void combine_check(const uint32_t* flags, const uint32_t* counts, int nb, int64_t* chk,
                    intptr_t stream);
 void fill_u64(uint64_t* p, int64_t n, uint64_t v, intptr_t stream);
+// Purge of consecutive pane slabs: zero acc (acc_bytes per slot: 8, or 4 x dim for vectors),
+// cnt and dirty of slots [so, so + n) in one launch (16-byte stores).
+void zero_panes(void* acc, int acc_bytes, uint32_t* cnt, uint8_t* dirty, int64_t so, int64_t n,
+                intptr_t stream);
 // Exchange repack (keyBy all-to-all without padding): bucket b's first min(counts[b], dst_cap)
 // records (`words` u64 words each) from stride src_cap to stride dst_cap, so the equal-split
 // all-to-all moves dst_cap-record slices sized to the largest fill over all ranks instead of the

@@ -1855,6 +1855,11 @@ void WindowStep::fire_window_vector(int64_t s, int64_t p0, int64_t p1, bool only
 void WindowStep::zero_panes(int64_t r, int64_t k) {
   // Reset k consecutive pane slabs starting at ring position r (pane-major state).
   const size_t so = (size_t)(r * nslots_), ns = (size_t)(k * nslots_);
+  if (gpu_) {  // one launch for the three slabs
+    if (cfg_.dim > 0) gpu::zero_panes(vacc_g_->p, cfg_.dim * 4, P<uint32_t>(cnt_g_), P<uint8_t>(dirty_g_), so, ns, (intptr_t)cur_);
+    else gpu::zero_panes(acc_g_->p, 8, P<uint32_t>(cnt_g_), P<uint8_t>(dirty_g_), so, ns, (intptr_t)cur_);
+    return;
+  }
   if (cfg_.dim > 0) memset_async(vacc_g_, 0, so * cfg_.dim * 4, ns * cfg_.dim * 4);
   else memset_async(acc_g_, 0, so * 8, ns * 8);
   memset_async(cnt_g_, 0, so * 4, ns * 4);
