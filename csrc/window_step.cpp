@@ -555,6 +555,15 @@ void WindowStep::host_wait(hipEvent_t ev) {
   }
 }
 
+void WindowStep::claim_flags() {
+  // Every counted copy in flight reads the flags words (row count, overflow bits) when it runs
+  // on the copy stream: whatever fire resets them next waits for all of them first, whichever
+  // output columns they copy (plain, re-firing or tiered).
+  claim(&out_busy_);
+  claim(&rout_busy_);
+  claim(&tout_busy_);
+}
+
 void WindowStep::claim(hipEvent_t* ev) {
   if (*ev) {
     hip_ok(hipStreamWaitEvent(cur_, *ev, 0), "hipStreamWaitEvent");
@@ -1340,7 +1349,7 @@ std::vector<FireRows> WindowStep::take(bool block) {
 void WindowStep::fire_window(int64_t s, bool only_dirty, int64_t seq) {
   // Only panes inside the live span exist in the ring; older / newer panes of the window never
   // held data and their ring slots belong to other panes (aliasing).
-  if (gpu_) claim(&out_busy_);
+  if (gpu_) claim_flags();
   const auto pr = ctl_.window_panes(s);
   const int64_t p0 = pr.first, p1 = pr.second;
   if (p1 < p0) return;
@@ -1447,7 +1456,7 @@ void WindowStep::fire_many(const std::vector<int64_t>& starts, bool only_dirty, 
     stage_[3] = mem_alloc(n * 4, 1, false);
     stage_[4] = mem_alloc(std::max(fire_group_, 32) * 4, 1);
   }
-  if (gpu_) claim(&out_busy_);
+  if (gpu_) claim_flags();
   const int g = fire_group_;
   for (size_t i = 0; i < wins.size(); i += g) {
     const int k = (int)std::min<size_t>(g, wins.size() - i);
@@ -1455,7 +1464,7 @@ void WindowStep::fire_many(const std::vector<int64_t>& starts, bool only_dirty, 
     uint32_t* on = P<uint32_t>(flags_) + 2;
     uint32_t* bounds = P<uint32_t>(fire_bounds_);
     if (gpu_) {
-      claim(&out_busy_);  // the previous chunk's copy may still read out_*
+      claim_flags();  // the previous chunk's copy may still read out_* and the flags
       FireStage st{P<uint64_t>(stage_[0]), P<double>(stage_[1]),
                    kv ? nullptr : P<uint64_t>(stage_[2]), kv ? nullptr : P<uint32_t>(stage_[3]),
                    P<uint32_t>(stage_[4]), (uint32_t)nslots_};
@@ -1518,7 +1527,7 @@ bool WindowStep::refire_fused(const std::vector<int64_t>& starts, const std::vec
   const bool kv = cfg_.emit_kv && dense_bits_;
   const int64_t region = ((int64_t)n_list + 3) & ~(int64_t)3;
   const int64_t rows_cap = k * region;
-  claim(&rout_busy_);  // the previous re-firing's copy reads the staging / columns
+  claim_flags();  // earlier copies read the staging / columns and the flags
   if (!rout_[0] || rout_cap_ < rows_cap || rout_kv_ != kv) {
     const int64_t cap = std::max<int64_t>(rows_cap, 1 << 16);
     for (int j = 0; j < 2; ++j) {
@@ -2201,7 +2210,7 @@ void WindowStep::fire_window_tiered(int64_t s, int64_t p0, int64_t p1, bool only
   //  3. tier_merge combines both per key into a transient table (a re-firing marks the
   //     device's dirty keys and folds tier rows of those keys only);
   //  4. window_fire over the table (one pane) with the fused map/filter epilogue.
-  if (gpu_) claim(&out_busy_);
+  if (gpu_) claim_flags();
   memset_async(flags_, 0, 8, 4);
   FirePlan fp;
   std::memset(&fp, 0, sizeof(fp));

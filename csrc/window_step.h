@@ -318,6 +318,7 @@ class WindowStep {
   void check_fire_flags(const uint32_t* hf);
   Buf take_slab(size_t bytes);
   void claim(hipEvent_t* ev);
+  void claim_flags();
   // spill tier
   void maybe_spill();
   void land_evictions();
