@@ -43,6 +43,7 @@ from ..ops import expr as E
 from ..ops import kernels as K
 from ..ops.native import load
 from ..parallel.comm import Comm, LocalComm
+from .host_rows import _event_spin
 
 I64_MIN, I64_MAX = K.I64_MIN, K.I64_MAX
 K_SESS = 4                # resident sessions per key slot (csrc/kernels_hip.hip kSess)
@@ -129,7 +130,11 @@ class KeyedSessionOperator:
                  spill_rows: int = 1 << 20, emit_capacity: int | None = None,
                  external_watermark: bool = False, host_budget_bytes: int | None = None,
                  idle_timeout_steps: int | None = None, spill_set_log2: int = 16,
-                 sub_table_log2: int | None = None):
+                 sub_table_log2: int | None = None, pipeline: bool = False):
+        """pipeline (GPU): the host half of step i -- the fold's counters, the host store's fire,
+        the fired rows' collection, the spill -- runs while the GPU works on step i+1's
+        partition and fold; process() then returns the sessions fired by the PREVIOUS batch
+        (flush() / finish() drain). GPU order stays fold(i) -> fire(i) -> fold(i+1)."""
         if gap <= 0:
             raise ValueError("session gap must be positive")
         self.device = K.resolve_device(device)
@@ -149,6 +154,10 @@ class KeyedSessionOperator:
         self.host_budget_bytes = host_budget_bytes
         self.idle_spill_ms = int(idle_spill_ms if idle_spill_ms is not None else 4 * gap)
         self.metrics = SessionMetrics()
+        self.pipeline = bool(pipeline)
+        self._pend: dict | None = None   # pipelined: the step whose host half is pending
+        self._rehash_due = False
+        self._carry: list = []           # rows a state reader's flush fired (returned next)
         self.late_side: list = []  # late records are dropped (no side output on this path)
         self.phase_s: dict[str, float] = defaultdict(float)  # host wall time per phase
         self.native = load()
@@ -299,6 +308,7 @@ class KeyedSessionOperator:
         self.slot_last.fill_(I64_MIN)
 
     def state_bytes(self) -> int:
+        self._sync_pending()
         if self.gpu:
             self._join_spill()
         hbm = 0
@@ -321,6 +331,17 @@ class KeyedSessionOperator:
 
     # ---- main entry -------------------------------------------------------------------------
     def process(self, keys: torch.Tensor, ts: torch.Tensor, vals: torch.Tensor) -> SessionRows:
+        if (self.pipeline and self.gpu and self.wm != I64_MIN and _SESSION_SORT == "lds"
+                and self.nslots.bit_length() + 32 <= 62 and keys.numel() <= self.batch_capacity):
+            return self._process_pipelined(keys, ts, vals)
+        pre = self.flush() if self._pend is not None or self._carry else None
+        out = self._process_sync(keys, ts, vals)
+        return out if pre is None else SessionRows.concat([pre, out])
+
+    def _process_sync(self, keys: torch.Tensor, ts: torch.Tensor, vals: torch.Tensor,
+                      fire: bool = True, exact: bool = False) -> SessionRows | None:
+        """One unpipelined step. fire=False: the step stops before its fire (the watermark is
+        set; the pipelined path fires it later); exact: start with the exact time base."""
         n = keys.numel()
         if n > self.batch_capacity:
             self._alloc(n, self.slack)
@@ -332,7 +353,7 @@ class KeyedSessionOperator:
         # base 2^30 ms (12 days) below it -- identical on every rank, no MIN all-reduce and no
         # host sync -- and a step with an older record is redone with the exact minimum (the
         # partition flags it like an unrepresentable span).
-        exact = self.wm == I64_MIN
+        exact = exact or self.wm == I64_MIN
         if exact:
             tbase = self._exact_tbase(ts, n)
         else:
@@ -343,27 +364,9 @@ class KeyedSessionOperator:
         spec = (self.gpu and _SESSION_SORT == "lds"
                 and self.nslots.bit_length() + 32 <= 62)
         while True:
-            K.step_begin(self.cursor, self.stats)
-            plan = K.PartitionPlan(max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2,
-                                   nranks=self.world, window_mode=1, drop_late=0, hash_mode=0,
-                                   bucket_cap=self.bucket_cap, late_ts=I64_MIN, tbase=tbase, pane=1,
-                                   rec_words=self.rec_w)
-            if self._scratch is not None and (self.rec_w == 2 or self._two_level24):
-                plan.scratch = self._scratch.data_ptr()
-                plan.scratch_cursor = self._scratch_cursor.data_ptr()
-            if n:
-                K.partition(keys, ts, vals, plan, self.kg_dest, self.cursor, self.send, self.stats)
-            K.step_finish(self.stats, self.local_maxts, self.red, bound=self.ooo_bound,
-                          event_mode=True, proc_now=0)
-            if idle:
-                self.red[2:3].fill_(I64_MAX)
-            self.comm.allreduce_min_(self.red[:8])
-            if self.world > 1:
-                # the per-rank chunks are nsub * bucket_cap records of rec_w words: the prefix of
-                # the buffers (sized for 24-byte records) -- 16-byte steps send 2/3 of it
-                words = self.nbuckets * self.bucket_cap * self.rec_w
-                self.comm.all_to_all(self.recv[:words], self.send[:words])
-                self.comm.all_to_all(self.recv_counts, self.cursor)
+            # (the per-rank chunks of the all-to-all are nsub * bucket_cap records of rec_w words:
+            # the prefix of the buffers, sized for 24-byte records)
+            self._launch_front(keys, ts, vals, n, tbase, idle)
             folded = None
             if spec:
                 with self._phase("fold_gpu"):
@@ -409,7 +412,146 @@ class KeyedSessionOperator:
         # Sessions that late data re-opened fire even when the watermark did not move
         # (EventTimeTrigger.onElement: maxTimestamp <= currentWatermark -> FIRE).
         wm = old_wm if self.external_watermark else max(old_wm, wm_global)
+        if not fire:
+            self.wm = wm
+            self.metrics.current_watermark = wm
+            return None
         return self._fire_at(wm)
+
+    def _launch_front(self, keys, ts, vals, n: int, tbase: int, idle: bool) -> None:
+        """step_begin + partition + step_finish, the watermark valve's MIN all-reduce and (G > 1)
+        the records all-to-all, all enqueued (no host wait)."""
+        K.step_begin(self.cursor, self.stats)
+        plan = K.PartitionPlan(max_parallelism=self.max_parallelism, nsub_log2=self.nsub_log2,
+                               nranks=self.world, window_mode=1, drop_late=0, hash_mode=0,
+                               bucket_cap=self.bucket_cap, late_ts=I64_MIN, tbase=tbase, pane=1,
+                               rec_words=self.rec_w)
+        if self._scratch is not None and (self.rec_w == 2 or self._two_level24):
+            plan.scratch = self._scratch.data_ptr()
+            plan.scratch_cursor = self._scratch_cursor.data_ptr()
+        if n:
+            K.partition(keys, ts, vals, plan, self.kg_dest, self.cursor, self.send, self.stats)
+        K.step_finish(self.stats, self.local_maxts, self.red, bound=self.ooo_bound,
+                      event_mode=True, proc_now=0)
+        if idle:
+            self.red[2:3].fill_(I64_MAX)
+        self.comm.allreduce_min_(self.red[:8])
+        if self.world > 1:
+            words = self.nbuckets * self.bucket_cap * self.rec_w
+            self.comm.all_to_all(self.recv[:words], self.send[:words])
+            self.comm.all_to_all(self.recv_counts, self.cursor)
+
+    def _counters_launch(self):
+        """The fold's counters and late count on their way to pinned memory (an event, no wait)."""
+        self._hctr.copy_(self.ctr, non_blocking=True)
+        self._hlate.copy_(self.late_cnt, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        return ev
+
+    def _counters_read(self, ev) -> list[int]:
+        with self._phase("fold_gpu.sync"):
+            _event_spin(ev)
+            h = self._hctr[:6].tolist() + [int(self._hlate[0])]
+        self._live_estimate += h[3]
+        return h
+
+    def _process_pipelined(self, keys, ts, vals) -> SessionRows:
+        """One pipelined step (GPU, LDS fold): returns what the PREVIOUS batch fired.
+
+        GPU stream:  ... fold(i-1) | partition(i) | fire(i-1) | fold(i) | spill(i-1) ...
+        host:        wait fold(i-1)'s counters -> its host fold work -> launch fire(i-1) ->
+                     launch fold(i) (skips itself on the device if step i must be redone) ->
+                     host fire(i-1), collect its rows, spill(i-1) -> read step i's flags.
+        Late data of batch i merges after fire(i-1) exactly as unpipelined."""
+        n = keys.numel()
+        old_wm = self.wm
+        empty0 = self._empty_steps
+        self._empty_steps = self._empty_steps + 1 if n == 0 else 0
+        idle = self._idle_marked or (self.idle_timeout_steps is not None
+                                     and self._empty_steps >= self.idle_timeout_steps)
+        tbase = old_wm - (1 << 30)
+        with self._phase("front"):
+            self._launch_front(keys, ts, vals, n, tbase, idle)
+            self._hred.copy_(self.red, non_blocking=True)
+            ev_red = torch.cuda.Event()
+            ev_red.record(torch.cuda.current_stream(self.device))
+        P, self._pend = self._pend, None
+        fire_rows = None
+        if P is not None:
+            if not P["done"]:
+                h = self._counters_read(P["ev"])
+                with self._phase("fold_gpu"):
+                    self._fold_finish(h, h[0], P["tbase"], P["old_wm"], 32)
+            self._rehash_if_due()
+            with self._phase("fire_gpu"):
+                fire_rows = self._fire_gpu_launch(P["wm"])
+        with self._phase("fold_gpu"):
+            self._fold_prepare()
+            launched = self._fold_launch(self.recv, self.recv_counts, self.world, tbase, old_wm,
+                                         32, self.bucket_cap, skip=self.red, rw=self.rec_w)
+            ev_fold = self._counters_launch() if launched else None
+        out = (self._fire_complete(P["wm"], fire_rows, inflight=launched) if P is not None
+               else SessionRows.concat([]))
+        with self._phase("front.sync"):
+            _event_spin(ev_red)
+            host = self._hred.tolist()
+        if host[7]:
+            raise ValueError("key ids -1 and -2 are reserved (the state tables' markers)")
+        redo = host[4] or host[3] or (host[5] and self.rec_w < 3)
+        if redo or not launched:
+            # The speculative fold skipped itself on the device (or the LDS fold does not apply):
+            # this batch takes the synchronous path (cause fixed first), its fire stays pending.
+            exact = bool(host[4])
+            ex = self.metrics.extra
+            if exact:
+                ex["tbase_redos"] = ex.get("tbase_redos", 0) + 1
+            if host[5] and self.rec_w < 3:
+                self.rec_w = 3
+                ex["record_widenings"] = ex.get("record_widenings", 0) + 1
+            if host[3]:
+                self._alloc(self.batch_capacity, self.slack * 2)
+            self._rehash_if_due()
+            self._empty_steps = empty0
+            self._process_sync(keys, ts, vals, fire=False, exact=exact)
+            self._pend = {"tbase": 0, "old_wm": old_wm, "wm": self.wm, "ev": None, "done": True}
+            return out
+        wm_global = host[2]
+        if wm_global == I64_MAX:
+            wm_global = old_wm
+        self.metrics.num_records_in += n
+        self.metrics.steps += 1
+        wm = old_wm if self.external_watermark else max(old_wm, wm_global)
+        self.wm = wm
+        self.metrics.current_watermark = wm
+        self._pend = {"tbase": tbase, "old_wm": old_wm, "wm": wm, "ev": ev_fold, "done": False}
+        return out
+
+    def flush(self) -> SessionRows:
+        """Pipelined: the pending step's host half (counters, host fold work, fire, spill) and
+        any rows a state reader's flush left behind."""
+        out, self._carry = self._carry, []
+        P, self._pend = self._pend, None
+        if P is not None:
+            if not P["done"]:
+                h = self._counters_read(P["ev"])
+                self._fold_finish(h, h[0], P["tbase"], P["old_wm"], 32)
+            self._rehash_if_due()
+            out.append(self._fire_at(P["wm"]))
+        return SessionRows.concat(out)
+
+    def _rehash_if_due(self) -> None:
+        """A rehash the spill check deferred while a fold was in flight (it moves slots, and the
+        in-flight fold's overflow slots are read afterwards): done with no fold pending."""
+        if self._rehash_due:
+            self._rehash_due = False
+            self._rehash()
+            self._tombs_bound = 0
+
+    def _sync_pending(self) -> None:
+        """Before a state reader: apply the pending step; its rows wait for the next call."""
+        if self._pend is not None:
+            self._carry.append(self.flush())
 
     def _exact_tbase(self, ts: torch.Tensor, n: int) -> int:
         """The step's minimum timestamp over all ranks (one MIN all-reduce + host read)."""
@@ -424,22 +566,28 @@ class KeyedSessionOperator:
 
     def advance_watermark(self, wm: int) -> SessionRows:
         wm = int(wm)
+        pre = self.flush()
         if wm <= self.wm:
-            return SessionRows.concat([])
-        return self._fire_at(wm)
+            return pre
+        return SessionRows.concat([pre, self._fire_at(wm)])
 
     def _fire_at(self, wm: int) -> SessionRows:
         self.wm = wm
         self.metrics.current_watermark = wm
         if wm == I64_MIN:
             return SessionRows.concat([])
-        parts = []
         pending = None
         if self.gpu:
             # The GPU firing is launched first; the host store fires while it runs and its rows
             # come back.
             with self._phase("fire_gpu"):
                 pending = self._fire_gpu_launch(wm)
+        return self._fire_complete(wm, pending)
+
+    def _fire_complete(self, wm: int, pending, inflight: bool = False) -> SessionRows:
+        """The host store's fire at `wm`, the launched GPU fire's rows, the spill check
+        (inflight: the next batch's fold is already enqueued -- see _maybe_spill)."""
+        parts = []
         with self._phase("fire_host"):
             # (the store's fire waits for the hot phase of queued eviction jobs itself)
             host_rows = self._fire_host(wm)
@@ -451,7 +599,7 @@ class KeyedSessionOperator:
         self.metrics.num_records_out += len(out)
         if self.gpu:
             with self._phase("spill"):
-                self._maybe_spill(wm)
+                self._maybe_spill(wm, inflight)
         if self.host_budget_bytes is not None and self.steps_since_budget_check() and \
                 self.host_bytes() > self.host_budget_bytes:
             raise MemoryError(f"host-DRAM session state {self.host_bytes()} B exceeds the budget "
@@ -1132,7 +1280,11 @@ class KeyedSessionOperator:
         live, occupied = self._occ_pin.tolist()
         return int(live), int(occupied)
 
-    def _maybe_spill(self, wm: int) -> None:
+    def _maybe_spill(self, wm: int, inflight: bool = False) -> None:
+        """inflight (pipelined step): the next batch's fold, at lateness watermark `wm`, is
+        enqueued ahead of this check -- a due rehash waits for the next step (it moves slots the
+        fold's overflow list names), and idle eviction spares every slot that fold can have
+        overflowed (last event time > wm - gap - lateness; see the kernel's sess_merge)."""
         # Live keys come from the kernels' insert / evict counters; the table is scanned only
         # after a restore and when the tombstone bound suggests a rehash.
         # Rehash (drop tombstones) once live + tombstones pass 0.8 of the slots with at least 8 %
@@ -1145,11 +1297,19 @@ class KeyedSessionOperator:
         self._poll_spill()
         t_occ = time.perf_counter()
 
-        if self._occ_exact:
-            live, occupied = self._count_occupancy()
-            if due(live, occupied):
+        def rehash():
+            if inflight:
+                self._rehash_due = True
+            else:
                 self._rehash()
                 self._tombs_bound = 0
+
+        if self._rehash_due:
+            live = self._live_estimate  # a rehash is already queued for the next step
+        elif self._occ_exact:
+            live, occupied = self._count_occupancy()
+            if due(live, occupied):
+                rehash()
         else:
             # The tombstone bound only grows (new keys reuse tombstones unseen), so the exact
             # counts are taken without a host wait: launched when the bound suggests a rehash and
@@ -1157,8 +1317,7 @@ class KeyedSessionOperator:
             live = self._live_estimate
             stale = self._occ_poll()
             if stale is not None and due(*stale):
-                self._rehash()
-                self._tombs_bound = 0
+                rehash()
             elif stale is not None:
                 # Not due: tighten the estimates from the exact counts (plus the inserts and
                 # evictions counted since the launch), so the bound stops re-launching the scan
@@ -1173,7 +1332,10 @@ class KeyedSessionOperator:
         if live > self.max_load * self.nslots and wm > I64_MIN:
             # LRU by last event time: keys idle for idle_spill_ms move to host DRAM (keys with no
             # live session are simply freed).
-            self._evict(idle_before=wm - self.idle_spill_ms)
+            idle_before = wm - self.idle_spill_ms
+            if inflight:
+                idle_before = min(idle_before, wm - self.gap - self.lateness)
+            self._evict(idle_before=idle_before)
         # Store empty again: clear the device set (drops its tombstones) and skip set probes.
         if (self.spill_any and self.store.spill_completed() == self.store.spill_submitted()
                 and self.store.num_keys() == 0):
@@ -1183,13 +1345,17 @@ class KeyedSessionOperator:
 
     # ---- inspection -------------------------------------------------------------------------
     def resident_keys(self) -> int:
+        self._sync_pending()
         if not self.gpu:
             return 0
         k = self.keys_g
         return int(((k != EMPTY_KEY) & (k != TOMB_KEY)).sum().item())
 
     def snapshot(self) -> dict:
-        """All live sessions (both tiers) as host columns key/start/end/acc/cnt/flags."""
+        """All live sessions (both tiers) as host columns key/start/end/acc/cnt/flags. Pipelined:
+        the pending step is applied first (its fired rows come with the next call -- a caller
+        that checkpoints calls flush() before and emits them)."""
+        self._sync_pending()
         if self.gpu:
             self._join_spill()
         parts = [self.store.snapshot()]
@@ -1232,6 +1398,7 @@ class KeyedSessionOperator:
         for k in ("gap", "agg"):
             if meta[k] != getattr(self, k):
                 raise ValueError(f"checkpoint {k} does not match the operator")
+        self._pend, self._carry, self._rehash_due = None, [], False
         self.wm = meta["wm"]
         for k, v in meta.get("metrics", {}).items():
             setattr(self.metrics, k, v)

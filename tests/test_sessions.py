@@ -683,3 +683,84 @@ def test_store_extract_hands_back_sessions():
     assert st.contains(3) and not st.contains(1) and not st.contains(4)
     snap = st.snapshot()
     assert sorted(snap["key"].tolist()) == [3, 3, 3, 3]
+
+
+# ------------------------------------------------------------------ pipelined step (GPU)
+@pytest.mark.gpu
+@settings(max_examples=8, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(seed=st.integers(0, 10_000), gap=st.sampled_from([5, 100, 400]),
+       batch=st.sampled_from([64, 1000]), lateness=st.sampled_from([0, 300]))
+def test_gpu_pipelined_sessions_equal_cpu(seed, gap, batch, lateness):
+    """The pipelined step (a batch's fire and spill run after the next batch's fold is enqueued)
+    fires exactly the sessions of the CPU store."""
+    rng = np.random.default_rng(seed)
+    n = 3000
+    ts = np.sort(rng.integers(0, 30_000, n)) + rng.integers(-400, 400, n)
+    events = [(int(k), int(t), int(v)) for k, t, v in
+              zip(rng.integers(0, 50, n), ts, rng.integers(0, 100, n))]
+    a, _ = engine(events, gap, 100, lateness, device="cpu", batch=batch)
+    b, op = engine(events, gap, 100, lateness, device="cuda", batch=batch, pipeline=True)
+    assert a == b
+    assert op._pend is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("promote", [True, False])
+def test_gpu_pipelined_overflow_spill_promote(promote):
+    """Overflow runs, idle eviction into the host store, rehash and promotion with the pipelined
+    step: equal to the CPU store."""
+    rng = np.random.default_rng(3)
+    n = 20_000
+    ts = np.sort(rng.integers(0, 200_000, n))
+    keys = rng.integers(0, 3000, n)
+    events = [(int(k), int(t), int(v)) for k, t, v in zip(keys, ts, rng.integers(0, 9, n))]
+    b, op = engine_with(events, 50, 30_000, 5_000, promote=promote, device="cuda", batch=2000,
+                        max_load=0.05, idle_spill_ms=2_000, cap_log2=6, pipeline=True)
+    a2, _ = engine(events, 50, 30_000, 5_000, device="cpu", batch=2000)
+    assert a2 == b
+    assert op.metrics.spilled_keys > 0 or op.metrics.overflow_keys > 0
+
+
+@pytest.mark.gpu
+def test_gpu_pipelined_redo_steps():
+    """Steps the speculative fold must skip (a record far older than the provisional time base,
+    a value that needs 24-byte records) take the synchronous path inside the pipeline."""
+    rng = np.random.default_rng(8)
+    events = []
+    for step in range(12):
+        for _ in range(300):
+            events.append((int(rng.integers(0, 40)), 10_000_000_000 + step * 1000
+                           + int(rng.integers(0, 900)), int(rng.integers(0, 9))))
+    events[5 * 300 + 7] = (3, 10_000_000_000 - (1 << 31), 4)  # older than wm - 2^30
+    events[8 * 300 + 9] = (4, 10_000_008_100, 1 << 40)        # outside int32
+    a, _ = engine(events, 200, 100, 1 << 33, device="cpu", batch=300)
+    b, op = engine(events, 200, 100, 1 << 33, device="cuda", batch=300, pipeline=True)
+    assert a == b
+    assert op.metrics.extra.get("tbase_redos", 0) >= 1
+    assert op.metrics.extra.get("record_widenings", 0) == 1
+
+
+@pytest.mark.gpu
+def test_gpu_pipelined_snapshot_flushes_pending():
+    """A snapshot between steps applies the pending step: the same sessions as the unpipelined
+    operator, and the pending fire's rows come with the next call."""
+    rng = np.random.default_rng(4)
+    ops = [KeyedSessionOperator(gap=100, lateness=0, agg=K.AGG_SUM_I64, device="cuda",
+                                max_keys=1 << 10, batch_capacity=512, ooo_bound=50, pipeline=p)
+           for p in (False, True)]
+    fired = [Counter(), Counter()]
+    for step in range(6):
+        k = torch.from_numpy(rng.integers(0, 30, 500)).cuda()
+        t = torch.from_numpy(np.sort(rng.integers(step * 400, step * 400 + 400, 500))).cuda()
+        v = torch.from_numpy(rng.integers(0, 9, 500)).cuda()
+        for i, op in enumerate(ops):
+            r = op.process(k, t, v)
+            fired[i].update(zip(r.keys.tolist(), r.start.tolist(), r.raw.tolist()))
+        if step == 3:
+            s0, s1 = (sorted(zip(*(op.snapshot()[f].tolist() for f in ("key", "start", "acc"))))
+                      for op in ops)
+            assert s0 == s1
+    for i, op in enumerate(ops):
+        r = op.finish()
+        fired[i].update(zip(r.keys.tolist(), r.start.tolist(), r.raw.tolist()))
+    assert fired[0] == fired[1] and sum(fired[0].values()) > 0
