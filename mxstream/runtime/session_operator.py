@@ -551,7 +551,8 @@ class KeyedSessionOperator:
     def _sync_pending(self) -> None:
         """Before a state reader: apply the pending step; its rows wait for the next call."""
         if self._pend is not None:
-            self._carry.append(self.flush())
+            rows = self.flush()  # (flush swaps self._carry: read it after the call)
+            self._carry.append(rows)
 
     def _exact_tbase(self, ts: torch.Tensor, n: int) -> int:
         """The step's minimum timestamp over all ranks (one MIN all-reduce + host read)."""
