@@ -156,7 +156,6 @@ class KeyedSessionOperator:
         self.metrics = SessionMetrics()
         self.pipeline = bool(pipeline)
         self._pend: dict | None = None   # pipelined: the step whose host half is pending
-        self._rehash_due = False
         self._carry: list = []           # rows a state reader's flush fired (returned next)
         self.late_side: list = []  # late records are dropped (no side output on this path)
         self.phase_s: dict[str, float] = defaultdict(float)  # host wall time per phase
@@ -459,11 +458,14 @@ class KeyedSessionOperator:
     def _process_pipelined(self, keys, ts, vals) -> SessionRows:
         """One pipelined step (GPU, LDS fold): returns what the PREVIOUS batch fired.
 
-        GPU stream:  ... fold(i-1) | partition(i) | fire(i-1) | fold(i) | spill(i-1) ...
-        host:        wait fold(i-1)'s counters -> its host fold work -> launch fire(i-1) ->
+        GPU stream:  ... fold(i-1) | partition(i) | spill(i-1) | fire(i-1) | fold(i) ...
+        host:        wait fold(i-1)'s counters -> its host fold work -> spill check (no fold in
+                     flight: evictions and rehashes see a settled table) -> launch fire(i-1) ->
                      launch fold(i) (skips itself on the device if step i must be redone) ->
-                     host fire(i-1), collect its rows, spill(i-1) -> read step i's flags.
-        Late data of batch i merges after fire(i-1) exactly as unpipelined."""
+                     host fire(i-1), collect its rows -> read step i's flags.
+        Late data of batch i merges after fire(i-1) exactly as unpipelined; the spill check runs
+        before the fire instead of after it (an eviction only moves sessions between the tiers,
+        and the host store fires what the GPU does not)."""
         n = keys.numel()
         old_wm = self.wm
         empty0 = self._empty_steps
@@ -483,7 +485,8 @@ class KeyedSessionOperator:
                 h = self._counters_read(P["ev"])
                 with self._phase("fold_gpu"):
                     self._fold_finish(h, h[0], P["tbase"], P["old_wm"], 32)
-            self._rehash_if_due()
+            with self._phase("spill"):
+                self._maybe_spill(P["wm"])
             with self._phase("fire_gpu"):
                 fire_rows = self._fire_gpu_launch(P["wm"])
         with self._phase("fold_gpu"):
@@ -491,7 +494,7 @@ class KeyedSessionOperator:
             launched = self._fold_launch(self.recv, self.recv_counts, self.world, tbase, old_wm,
                                          32, self.bucket_cap, skip=self.red, rw=self.rec_w)
             ev_fold = self._counters_launch() if launched else None
-        out = (self._fire_complete(P["wm"], fire_rows, inflight=launched) if P is not None
+        out = (self._fire_complete(P["wm"], fire_rows, spill=False) if P is not None
                else SessionRows.concat([]))
         with self._phase("front.sync"):
             _event_spin(ev_red)
@@ -511,7 +514,6 @@ class KeyedSessionOperator:
                 ex["record_widenings"] = ex.get("record_widenings", 0) + 1
             if host[3]:
                 self._alloc(self.batch_capacity, self.slack * 2)
-            self._rehash_if_due()
             self._empty_steps = empty0
             self._process_sync(keys, ts, vals, fire=False, exact=exact)
             self._pend = {"tbase": 0, "old_wm": old_wm, "wm": self.wm, "ev": None, "done": True}
@@ -536,17 +538,8 @@ class KeyedSessionOperator:
             if not P["done"]:
                 h = self._counters_read(P["ev"])
                 self._fold_finish(h, h[0], P["tbase"], P["old_wm"], 32)
-            self._rehash_if_due()
             out.append(self._fire_at(P["wm"]))
         return SessionRows.concat(out)
-
-    def _rehash_if_due(self) -> None:
-        """A rehash the spill check deferred while a fold was in flight (it moves slots, and the
-        in-flight fold's overflow slots are read afterwards): done with no fold pending."""
-        if self._rehash_due:
-            self._rehash_due = False
-            self._rehash()
-            self._tombs_bound = 0
 
     def _sync_pending(self) -> None:
         """Before a state reader: apply the pending step; its rows wait for the next call."""
@@ -585,9 +578,9 @@ class KeyedSessionOperator:
                 pending = self._fire_gpu_launch(wm)
         return self._fire_complete(wm, pending)
 
-    def _fire_complete(self, wm: int, pending, inflight: bool = False) -> SessionRows:
-        """The host store's fire at `wm`, the launched GPU fire's rows, the spill check
-        (inflight: the next batch's fold is already enqueued -- see _maybe_spill)."""
+    def _fire_complete(self, wm: int, pending, spill: bool = True) -> SessionRows:
+        """The host store's fire at `wm`, the launched GPU fire's rows, the spill check (the
+        pipelined step runs that before the fire: spill=False)."""
         parts = []
         with self._phase("fire_host"):
             # (the store's fire waits for the hot phase of queued eviction jobs itself)
@@ -598,9 +591,9 @@ class KeyedSessionOperator:
         parts.append(host_rows)
         out = SessionRows.concat(parts)
         self.metrics.num_records_out += len(out)
-        if self.gpu:
+        if self.gpu and spill:
             with self._phase("spill"):
-                self._maybe_spill(wm, inflight)
+                self._maybe_spill(wm)
         if self.host_budget_bytes is not None and self.steps_since_budget_check() and \
                 self.host_bytes() > self.host_budget_bytes:
             raise MemoryError(f"host-DRAM session state {self.host_bytes()} B exceeds the budget "
@@ -1281,11 +1274,7 @@ class KeyedSessionOperator:
         live, occupied = self._occ_pin.tolist()
         return int(live), int(occupied)
 
-    def _maybe_spill(self, wm: int, inflight: bool = False) -> None:
-        """inflight (pipelined step): the next batch's fold, at lateness watermark `wm`, is
-        enqueued ahead of this check -- a due rehash waits for the next step (it moves slots the
-        fold's overflow list names), and idle eviction spares every slot that fold can have
-        overflowed (last event time > wm - gap - lateness; see the kernel's sess_merge)."""
+    def _maybe_spill(self, wm: int) -> None:
         # Live keys come from the kernels' insert / evict counters; the table is scanned only
         # after a restore and when the tombstone bound suggests a rehash.
         # Rehash (drop tombstones) once live + tombstones pass 0.8 of the slots with at least 8 %
@@ -1299,15 +1288,10 @@ class KeyedSessionOperator:
         t_occ = time.perf_counter()
 
         def rehash():
-            if inflight:
-                self._rehash_due = True
-            else:
-                self._rehash()
-                self._tombs_bound = 0
+            self._rehash()
+            self._tombs_bound = 0
 
-        if self._rehash_due:
-            live = self._live_estimate  # a rehash is already queued for the next step
-        elif self._occ_exact:
+        if self._occ_exact:
             live, occupied = self._count_occupancy()
             if due(live, occupied):
                 rehash()
@@ -1333,10 +1317,7 @@ class KeyedSessionOperator:
         if live > self.max_load * self.nslots and wm > I64_MIN:
             # LRU by last event time: keys idle for idle_spill_ms move to host DRAM (keys with no
             # live session are simply freed).
-            idle_before = wm - self.idle_spill_ms
-            if inflight:
-                idle_before = min(idle_before, wm - self.gap - self.lateness)
-            self._evict(idle_before=idle_before)
+            self._evict(idle_before=wm - self.idle_spill_ms)
         # Store empty again: clear the device set (drops its tombstones) and skip set probes.
         if (self.spill_any and self.store.spill_completed() == self.store.spill_submitted()
                 and self.store.num_keys() == 0):
@@ -1399,7 +1380,7 @@ class KeyedSessionOperator:
         for k in ("gap", "agg"):
             if meta[k] != getattr(self, k):
                 raise ValueError(f"checkpoint {k} does not match the operator")
-        self._pend, self._carry, self._rehash_due = None, [], False
+        self._pend, self._carry = None, []
         self.wm = meta["wm"]
         for k, v in meta.get("metrics", {}).items():
             setattr(self.metrics, k, v)
