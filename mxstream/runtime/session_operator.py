@@ -458,14 +458,14 @@ class KeyedSessionOperator:
     def _process_pipelined(self, keys, ts, vals) -> SessionRows:
         """One pipelined step (GPU, LDS fold): returns what the PREVIOUS batch fired.
 
-        GPU stream:  ... fold(i-1) | partition(i) | spill(i-1) | fire(i-1) | fold(i) ...
-        host:        wait fold(i-1)'s counters -> its host fold work -> spill check (no fold in
-                     flight: evictions and rehashes see a settled table) -> launch fire(i-1) ->
-                     launch fold(i) (skips itself on the device if step i must be redone) ->
-                     host fire(i-1), collect its rows -> read step i's flags.
-        Late data of batch i merges after fire(i-1) exactly as unpipelined; the spill check runs
-        before the fire instead of after it (an eviction only moves sessions between the tiers,
-        and the host store fires what the GPU does not)."""
+        GPU stream:  ... fold(i-1) | partition(i) | fire(i-1) | spill(i-1) | fold(i) ...
+        host:        wait fold(i-1)'s counters -> its host fold work -> launch fire(i-1) ->
+                     host store fire(i-1) -> spill check -> launch fold(i) (skips itself on the
+                     device if step i must be redone) -> collect fire(i-1)'s rows -> read step
+                     i's flags.
+        The GPU order is the unpipelined one (late data of batch i merges after fire(i-1)); the
+        spill check still runs with no fold in flight (evictions and rehashes move slots the
+        fold's overflow list names), and the host fire waits only for earlier evictions."""
         n = keys.numel()
         old_wm = self.wm
         empty0 = self._empty_steps
@@ -485,16 +485,18 @@ class KeyedSessionOperator:
                 h = self._counters_read(P["ev"])
                 with self._phase("fold_gpu"):
                     self._fold_finish(h, h[0], P["tbase"], P["old_wm"], 32)
-            with self._phase("spill"):
-                self._maybe_spill(P["wm"])
             with self._phase("fire_gpu"):
                 fire_rows = self._fire_gpu_launch(P["wm"])
+            with self._phase("fire_host"):
+                host_rows = self._fire_host(P["wm"])
+            with self._phase("spill"):
+                self._maybe_spill(P["wm"])
         with self._phase("fold_gpu"):
             self._fold_prepare()
             launched = self._fold_launch(self.recv, self.recv_counts, self.world, tbase, old_wm,
                                          32, self.bucket_cap, skip=self.red, rw=self.rec_w)
             ev_fold = self._counters_launch() if launched else None
-        out = (self._fire_complete(P["wm"], fire_rows, spill=False) if P is not None
+        out = (self._fire_rows(P["wm"], fire_rows, host_rows) if P is not None
                else SessionRows.concat([]))
         with self._phase("front.sync"):
             _event_spin(ev_red)
@@ -578,22 +580,27 @@ class KeyedSessionOperator:
                 pending = self._fire_gpu_launch(wm)
         return self._fire_complete(wm, pending)
 
-    def _fire_complete(self, wm: int, pending, spill: bool = True) -> SessionRows:
-        """The host store's fire at `wm`, the launched GPU fire's rows, the spill check (the
-        pipelined step runs that before the fire: spill=False)."""
-        parts = []
+    def _fire_complete(self, wm: int, pending) -> SessionRows:
+        """The host store's fire at `wm`, the launched GPU fire's rows, the spill check."""
         with self._phase("fire_host"):
             # (the store's fire waits for the hot phase of queued eviction jobs itself)
             host_rows = self._fire_host(wm)
+        if self.gpu:
+            with self._phase("spill"):
+                self._maybe_spill(wm)
+        return self._fire_rows(wm, pending, host_rows)
+
+    def _fire_rows(self, wm: int, pending, host_rows: SessionRows) -> SessionRows:
+        """The launched GPU fire's rows (the spill check's eviction kernel runs after the fire
+        kernel: the rows are those of the table before it) with the host store's, and the
+        host-DRAM budget check."""
+        parts = []
         if pending is not None:
             with self._phase("fire_gpu"):
                 parts.append(self._fire_gpu_collect(pending))
         parts.append(host_rows)
         out = SessionRows.concat(parts)
         self.metrics.num_records_out += len(out)
-        if self.gpu and spill:
-            with self._phase("spill"):
-                self._maybe_spill(wm)
         if self.host_budget_bytes is not None and self.steps_since_budget_check() and \
                 self.host_bytes() > self.host_budget_bytes:
             raise MemoryError(f"host-DRAM session state {self.host_bytes()} B exceeds the budget "
