@@ -235,14 +235,16 @@ class SessionStore {
     return d;
   }
   // Fire / clean up everything the watermark allows. Returns columns of emitted rows plus the
-  // keys that left the store ("released"). Waits only for the hot phase of queued evictions.
+  // keys that left the store ("released"). Waits only for the hot phase of queued evictions --
+  // of jobs up to `hot_upto` when >= 0 (later ones evicted sessions the GPU fire already saw).
   py::dict fire_np(int64_t wm, std::vector<int32_t> map_code, std::vector<double> map_consts,
-                   std::vector<int32_t> f_code, std::vector<double> f_consts, bool expire) {
+                   std::vector<int32_t> f_code, std::vector<double> f_consts, bool expire,
+                   int64_t hot_upto) {
     sess::SessionCore::FireOut o;
     {
       py::gil_scoped_release nogil;
       if (expire) join_all();
-      else wait_hot();
+      else wait_hot(hot_upto);
       std::lock_guard<std::mutex> g(mu_);
       c_.fire(wm, sess::SessionCore::prog(map_code.data(), map_code.size(), map_consts.data(), map_consts.size()),
            sess::SessionCore::prog(f_code.data(), f_code.size(), f_consts.data(), f_consts.size()), o, expire);
@@ -377,9 +379,9 @@ class SessionStore {
     std::unique_lock<std::mutex> lk(qmu_);
     dcv_.wait(lk, [&] { return completed_ == submitted_; });
   }
-  void wait_hot() {
+  void wait_hot(int64_t upto = -1) {  // jobs finish their hot phase in id order
     std::unique_lock<std::mutex> lk(qmu_);
-    dcv_.wait(lk, [&] { return hot_done_ == submitted_; });
+    dcv_.wait(lk, [&] { return hot_done_ >= (upto < 0 ? submitted_ : (uint64_t)upto); });
   }
   py::list take_results() {
     std::deque<SpillDone> done;
@@ -564,7 +566,7 @@ void bind_sessions(py::module_& m) {
       .def("index_stats", &SessionStore::index_stats)
       .def("fire", &SessionStore::fire_np, py::arg("wm"), py::arg("map_code"),
            py::arg("map_consts"), py::arg("f_code"), py::arg("f_consts"),
-           py::arg("expire_cold") = true)
+           py::arg("expire_cold") = true, py::arg("hot_upto") = -1)
       .def("expire_cold", &SessionStore::expire_cold_np)
       .def("spill_set", &SessionStore::spill_set_np)
       .def("contains", &SessionStore::contains)

@@ -460,12 +460,15 @@ class KeyedSessionOperator:
 
         GPU stream:  ... fold(i-1) | partition(i) | fire(i-1) | spill(i-1) | fold(i) ...
         host:        wait fold(i-1)'s counters -> its host fold work -> launch fire(i-1) ->
-                     host store fire(i-1) -> spill check -> launch fold(i) (skips itself on the
-                     device if step i must be redone) -> collect fire(i-1)'s rows -> read step
+                     spill check -> launch fold(i) (skips itself on the device if step i must be
+                     redone) -> host store fire(i-1) -> collect fire(i-1)'s rows -> read step
                      i's flags.
-        The GPU order is the unpipelined one (late data of batch i merges after fire(i-1)); the
-        spill check still runs with no fold in flight (evictions and rehashes move slots the
-        fold's overflow list names), and the host fire waits only for earlier evictions."""
+        The GPU order is the unpipelined one (late data of batch i merges after fire(i-1)). The
+        spill check runs with no fold in flight (evictions and rehashes move slots the fold's
+        overflow list names); the host fire overlaps fold(i) and waits only for evictions
+        before fire(i-1) (later ones moved sessions the GPU fire saw). Keys the host fire
+        releases leave the device spill set behind fold(i), which still diverted their records
+        to the host tier: _host_fold puts such keys back in the set."""
         n = keys.numel()
         old_wm = self.wm
         empty0 = self._empty_steps
@@ -487,8 +490,7 @@ class KeyedSessionOperator:
                     self._fold_finish(h, h[0], P["tbase"], P["old_wm"], 32)
             with self._phase("fire_gpu"):
                 fire_rows = self._fire_gpu_launch(P["wm"])
-            with self._phase("fire_host"):
-                host_rows = self._fire_host(P["wm"])
+            jobs = self.store.spill_submitted()
             with self._phase("spill"):
                 self._maybe_spill(P["wm"])
         with self._phase("fold_gpu"):
@@ -496,8 +498,11 @@ class KeyedSessionOperator:
             launched = self._fold_launch(self.recv, self.recv_counts, self.world, tbase, old_wm,
                                          32, self.bucket_cap, skip=self.red, rw=self.rec_w)
             ev_fold = self._counters_launch() if launched else None
-        out = (self._fire_rows(P["wm"], fire_rows, host_rows) if P is not None
-               else SessionRows.concat([]))
+        out = SessionRows.concat([])
+        if P is not None:
+            with self._phase("fire_host"):
+                host_rows = self._fire_host(P["wm"], jobs)
+            out = self._fire_rows(P["wm"], fire_rows, host_rows)
         with self._phase("front.sync"):
             _event_spin(ev_red)
             host = self._hred.tolist()
@@ -632,13 +637,15 @@ class KeyedSessionOperator:
         if len(k):
             self.metrics.num_late_records_dropped += int(self.store.process(k, t, v, wm))
 
-    def _fire_host(self, wm: int) -> SessionRows:
+    def _fire_host(self, wm: int, hot_upto: int = -1) -> SessionRows:
+        """hot_upto >= 0: wait only for eviction jobs up to that id (the pipelined step fires
+        after the next spill check: its evictions were in HBM for the GPU fire)."""
         mc, mk = self.map_prog.as_args()
         fc, fk = self.filter_prog.as_args()
         # GPU: cold-chunk expiry (no rows, only released keys) runs on the spill worker after
         # its insert, except at end of input.
         defer = self.gpu and wm != I64_MAX
-        d = self.store.fire(wm, mc, mk, fc, fk, not defer)
+        d = self.store.fire(wm, mc, mk, fc, fk, not defer, hot_upto)
         if defer:
             self._expire_wm = wm
         rel = d["released"]
@@ -804,7 +811,14 @@ class KeyedSessionOperator:
 
     def _host_fold(self, n_host: int, tbase: int, wm: int) -> None:
         """Records of keys that live in host DRAM: folded by the host store."""
-        k, t, v = (x.cpu().numpy() for x in self._diverted(n_host, tbase))
+        dk, t, v = self._diverted(n_host, tbase)
+        if self.pipeline:
+            # (pipelined: a key released by the host fire that ran behind this fold's launch was
+            # erased from the set after its records were diverted -- it holds sessions again)
+            dk = dk.contiguous()
+            self.native.gpu_set_insert(self.spill_set.data_ptr(), self.spill_set.numel() - 1,
+                                       dk.data_ptr(), dk.numel(), self._st())
+        k, t, v = (x.cpu().numpy() for x in (dk, t, v))
         self.metrics.num_late_records_dropped += int(self.store.process(k.copy(), t, v.copy(), wm))
         self.metrics.records_to_host += n_host
         self.set_used += n_host  # upper bound on keys the lookup added (full sub-tables)
