@@ -605,13 +605,14 @@ PYBIND11_MODULE(_mxs_native, m) {
                                 intptr_t n_long, int64_t n_cap, int tbits, int64_t gap,
                                 int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
                                 int64_t nslots, intptr_t sess, intptr_t slot_due,
-                                intptr_t slot_last, intptr_t late_cnt, intptr_t ovf_slots,
-                                intptr_t n_ovf, intptr_t ovf_rows, intptr_t n_ovf_runs,
-                                uint32_t ovf_cap, intptr_t stream) {
+                                intptr_t slot_last, intptr_t late_cnt, intptr_t keys_g,
+                                intptr_t ovf_slots, intptr_t n_ovf, intptr_t ovf_rows,
+                                intptr_t n_ovf_runs, uint32_t ovf_cap, intptr_t stream) {
     gpu::session_merge(P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_in),
                        P<uint32_t>(long_heads), P<uint32_t>(n_long), n_cap, tbits, gap, lateness,
                        wm, tbase, agg, cap_log2, nslots, P<int64_t>(sess), P<int64_t>(slot_due),
-                       P<int64_t>(slot_last), P<uint64_t>(late_cnt), P<int64_t>(ovf_slots),
+                       P<int64_t>(slot_last), P<uint64_t>(late_cnt), P<uint64_t>(keys_g),
+                       P<int64_t>(ovf_slots),
                        P<uint32_t>(n_ovf), P<int64_t>(ovf_rows), P<uint32_t>(n_ovf_runs), ovf_cap,
                        stream);
   });
@@ -620,21 +621,23 @@ PYBIND11_MODULE(_mxs_native, m) {
                                       intptr_t n_long, int tbits, int64_t gap, int64_t lateness,
                                       int64_t wm, int64_t tbase, int agg, int cap_log2,
                                       int64_t nslots, intptr_t sess, intptr_t slot_due,
-                                      intptr_t slot_last, intptr_t late_cnt, intptr_t ovf_slots,
-                                      intptr_t n_ovf, intptr_t ovf_rows, intptr_t n_ovf_runs,
-                                      uint32_t ovf_cap, intptr_t stream, int pair) {
+                                      intptr_t slot_last, intptr_t late_cnt, intptr_t keys_g,
+                                      intptr_t ovf_slots, intptr_t n_ovf, intptr_t ovf_rows,
+                                      intptr_t n_ovf_runs, uint32_t ovf_cap, intptr_t stream,
+                                      int pair) {
     gpu::session_merge_heads(P<int64_t>(sk), P<uint64_t>(vals), P<uint32_t>(n_in),
                              P<uint64_t>(heads), P<uint32_t>(n_heads), head_cap,
                              P<uint32_t>(long_heads), P<uint32_t>(n_long), tbits, gap, lateness,
                              wm, tbase, agg, cap_log2, nslots, P<int64_t>(sess),
                              P<int64_t>(slot_due), P<int64_t>(slot_last), P<uint64_t>(late_cnt),
-                             P<int64_t>(ovf_slots), P<uint32_t>(n_ovf), P<int64_t>(ovf_rows),
+                             P<uint64_t>(keys_g), P<int64_t>(ovf_slots), P<uint32_t>(n_ovf), P<int64_t>(ovf_rows),
                              P<uint32_t>(n_ovf_runs), ovf_cap, stream, pair);
   }, py::arg("sk"), py::arg("vals"), py::arg("n_in"), py::arg("heads"), py::arg("n_heads"),
      py::arg("head_cap"), py::arg("long_heads"), py::arg("n_long"), py::arg("tbits"),
      py::arg("gap"), py::arg("lateness"), py::arg("wm"), py::arg("tbase"), py::arg("agg"),
      py::arg("cap_log2"), py::arg("nslots"), py::arg("sess"), py::arg("slot_due"),
-     py::arg("slot_last"), py::arg("late_cnt"), py::arg("ovf_slots"), py::arg("n_ovf"),
+     py::arg("slot_last"), py::arg("late_cnt"), py::arg("keys_g"), py::arg("ovf_slots"),
+     py::arg("n_ovf"),
      py::arg("ovf_rows"), py::arg("n_ovf_runs"), py::arg("ovf_cap"), py::arg("stream"),
      py::arg("pair") = 0);
   m.def("gpu_session_fire", [](int64_t gap, int64_t lateness, int64_t wm, int agg, int cap_log2,

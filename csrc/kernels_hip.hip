@@ -3490,7 +3490,8 @@ struct SessOut {
   int64_t* slot_due;
   int64_t* slot_last;
   uint64_t* late_cnt;
-  int64_t* ovf_slots;
+  const uint64_t* keys;  // the slot table's keys (read for the overflow list)
+  int64_t* ovf_slots;    // (slot, key) pairs
   uint32_t* n_ovf;
   int64_t* ovf_rows;
   uint32_t* n_ovf_runs;
@@ -3529,8 +3530,11 @@ __device__ __forceinline__ void sess_finish(const SessState& st, int64_t slot, i
   *meta = make_longlong2(sess_due(st, a.lateness), last_ts > prev_last ? last_ts : prev_last);
   if (late) atomicAdd((unsigned long long*)o.late_cnt, (unsigned long long)late);
   if (overflow) {
+    // The host evicts these keys and re-merges their overflow runs. The key rides along: a
+    // pipelined step may evict the slot (idle) before the host reads the list.
     const uint32_t q = atomicAdd(o.n_ovf, 1u);
-    o.ovf_slots[q] = slot;  // host evicts these keys and re-merges their overflow runs
+    o.ovf_slots[2 * (size_t)q] = slot;
+    o.ovf_slots[2 * (size_t)q + 1] = (int64_t)o.keys[slot];
   }
 }
 
@@ -5422,10 +5426,11 @@ void session_merge(const int64_t* sk, const uint64_t* vals, const uint32_t* n_in
                    uint32_t* long_heads, uint32_t* n_long, int64_t n_cap, int tbits, int64_t gap,
                    int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
                    int64_t nslots, int64_t* sess, int64_t* slot_due, int64_t* slot_last,
-                   uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf, int64_t* ovf_rows,
-                   uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream) {
+                   uint64_t* late_cnt, const uint64_t* keys_g, int64_t* ovf_slots,
+                   uint32_t* n_ovf, int64_t* ovf_rows, uint32_t* n_ovf_runs, uint32_t ovf_cap,
+                   intptr_t stream) {
   const SessArgs a = make_sess_args(gap, lateness, wm, tbase, agg, cap_log2, nslots, tbits);
-  const SessOut o{reinterpret_cast<SessRec*>(sess), slot_due, slot_last, late_cnt,
+  const SessOut o{reinterpret_cast<SessRec*>(sess), slot_due, slot_last, late_cnt, keys_g,
                   ovf_slots, n_ovf, ovf_rows, n_ovf_runs, ovf_cap};
   hipLaunchKernelGGL(session_merge_small_kernel, dim3(grid_for(n_cap, 256, 16384)), dim3(256), 0,
                      (hipStream_t)stream, sk, vals, n_in, a, o, long_heads, n_long);
@@ -5441,13 +5446,14 @@ void session_merge_heads(const int64_t* sk, const uint64_t* vals, const uint32_t
                          uint32_t* long_heads, uint32_t* n_long, int tbits, int64_t gap,
                          int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
                          int64_t nslots, int64_t* sess, int64_t* slot_due, int64_t* slot_last,
-                         uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf, int64_t* ovf_rows,
-                         uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream, int pair) {
+                         uint64_t* late_cnt, const uint64_t* keys_g, int64_t* ovf_slots,
+                         uint32_t* n_ovf, int64_t* ovf_rows, uint32_t* n_ovf_runs,
+                         uint32_t ovf_cap, intptr_t stream, int pair) {
   // pair: session_lookup_sort wrote interleaved (sort key, value) pairs at sk (vals unused)
   const SessArgs a = make_sess_args(gap, lateness, wm, tbase, agg, cap_log2, nslots, tbits,
                                     pair ? 2 : 1);
   if (pair) vals = reinterpret_cast<const uint64_t*>(sk) + 1;
-  const SessOut o{reinterpret_cast<SessRec*>(sess), slot_due, slot_last, late_cnt,
+  const SessOut o{reinterpret_cast<SessRec*>(sess), slot_due, slot_last, late_cnt, keys_g,
                   ovf_slots, n_ovf, ovf_rows, n_ovf_runs, ovf_cap};
   hipLaunchKernelGGL(session_merge_heads_kernel, dim3(grid_for(head_cap, 256, 16384)), dim3(256),
                      0, (hipStream_t)stream, sk, vals, heads, n_heads, a, o, long_heads, n_long);

@@ -322,16 +322,18 @@ void session_merge(const int64_t* sk, const uint64_t* vals, const uint32_t* n_in
                    uint32_t* long_heads, uint32_t* n_long, int64_t n_cap, int tbits, int64_t gap,
                    int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
                    int64_t nslots, int64_t* sess, int64_t* slot_due, int64_t* slot_last,
-                   uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf, int64_t* ovf_rows,
-                   uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream);
+                   uint64_t* late_cnt, const uint64_t* keys_g, int64_t* ovf_slots,
+                   uint32_t* n_ovf, int64_t* ovf_rows, uint32_t* n_ovf_runs, uint32_t ovf_cap,
+                   intptr_t stream);
 // session_merge over the segment list of session_lookup_sort (position | length << 32).
 void session_merge_heads(const int64_t* sk, const uint64_t* vals, const uint32_t* n_in,
                          const uint64_t* heads, const uint32_t* n_heads, int64_t head_cap,
                          uint32_t* long_heads, uint32_t* n_long, int tbits, int64_t gap,
                          int64_t lateness, int64_t wm, int64_t tbase, int agg, int cap_log2,
                          int64_t nslots, int64_t* sess, int64_t* slot_due, int64_t* slot_last,
-                         uint64_t* late_cnt, int64_t* ovf_slots, uint32_t* n_ovf, int64_t* ovf_rows,
-                         uint32_t* n_ovf_runs, uint32_t ovf_cap, intptr_t stream, int pair = 0);
+                         uint64_t* late_cnt, const uint64_t* keys_g, int64_t* ovf_slots,
+                         uint32_t* n_ovf, int64_t* ovf_rows, uint32_t* n_ovf_runs,
+                         uint32_t ovf_cap, intptr_t stream, int pair = 0);
 void session_fire(int64_t gap, int64_t lateness, int64_t wm, int agg, int cap_log2,
                   int64_t nslots, const uint64_t* keys_g, int64_t* sess, int64_t* slot_due,
                   const ExprProg& map, const ExprProg& filt, uint64_t* out_key, int64_t* out_start,

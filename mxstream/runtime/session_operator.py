@@ -156,6 +156,7 @@ class KeyedSessionOperator:
         self.metrics = SessionMetrics()
         self.pipeline = bool(pipeline)
         self._pend: dict | None = None   # pipelined: the step whose host half is pending
+        self._rehash_due = False
         self._carry: list = []           # rows a state reader's flush fired (returned next)
         self.late_side: list = []  # late records are dropped (no side output on this path)
         self.phase_s: dict[str, float] = defaultdict(float)  # host wall time per phase
@@ -292,7 +293,7 @@ class KeyedSessionOperator:
             # holds the worst case: every received record a run of its own.
             self.ovf_cap = max(1 << 12, total)
             self.ovf_rows = torch.empty(5 * self.ovf_cap, dtype=torch.int64, device=dev)
-            self.ovf_slots = torch.empty(total, dtype=torch.int64, device=dev)
+            self.ovf_slots = torch.empty(2 * total, dtype=torch.int64, device=dev)  # (slot, key)
 
     def _alloc_state(self) -> None:
         dev, n = self.device, self.nslots
@@ -458,17 +459,19 @@ class KeyedSessionOperator:
     def _process_pipelined(self, keys, ts, vals) -> SessionRows:
         """One pipelined step (GPU, LDS fold): returns what the PREVIOUS batch fired.
 
-        GPU stream:  ... fold(i-1) | partition(i) | fire(i-1) | spill(i-1) | fold(i) ...
+        GPU stream:  ... fold(i-1) | partition(i) | fire(i-1) | fold(i) | evict(i-1) ...
         host:        wait fold(i-1)'s counters -> its host fold work -> launch fire(i-1) ->
-                     spill check -> launch fold(i) (skips itself on the device if step i must be
-                     redone) -> host store fire(i-1) -> collect fire(i-1)'s rows -> read step
-                     i's flags.
-        The GPU order is the unpipelined one (late data of batch i merges after fire(i-1)). The
-        spill check runs with no fold in flight (evictions and rehashes move slots the fold's
-        overflow list names); the host fire overlaps fold(i) and waits only for evictions
-        before fire(i-1) (later ones moved sessions the GPU fire saw). Keys the host fire
-        releases leave the device spill set behind fold(i), which still diverted their records
-        to the host tier: _host_fold puts such keys back in the set."""
+                     launch fold(i) (skips itself on the device if step i must be redone) ->
+                     spill check at fire(i-1)'s watermark -> host store fire(i-1) -> collect
+                     fire(i-1)'s rows -> read step i's flags.
+        Late data of batch i merges after fire(i-1) as unpipelined; the spill check and the host
+        fire overlap fold(i). An eviction behind fold(i) moves that fold's merges with the
+        sessions (the overflow list carries each slot's key, so an overflowed slot may be
+        evicted before the host reads the list); a due rehash, which moves slots, waits for the
+        next step's window with no fold in flight. The host fire waits only for evictions
+        before fire(i-1) (later ones moved sessions the GPU fire saw). Keys the host fire or the
+        spill worker release leave the device spill set behind fold(i), which still diverted
+        their records to the host tier: _host_fold puts such keys back in the set."""
         n = keys.numel()
         old_wm = self.wm
         empty0 = self._empty_steps
@@ -488,11 +491,9 @@ class KeyedSessionOperator:
                 h = self._counters_read(P["ev"])
                 with self._phase("fold_gpu"):
                     self._fold_finish(h, h[0], P["tbase"], P["old_wm"], 32)
+            self._rehash_if_due()
             with self._phase("fire_gpu"):
                 fire_rows = self._fire_gpu_launch(P["wm"])
-            jobs = self.store.spill_submitted()
-            with self._phase("spill"):
-                self._maybe_spill(P["wm"])
         with self._phase("fold_gpu"):
             self._fold_prepare()
             launched = self._fold_launch(self.recv, self.recv_counts, self.world, tbase, old_wm,
@@ -500,6 +501,9 @@ class KeyedSessionOperator:
             ev_fold = self._counters_launch() if launched else None
         out = SessionRows.concat([])
         if P is not None:
+            jobs = self.store.spill_submitted()
+            with self._phase("spill"):
+                self._maybe_spill(P["wm"], inflight=launched)
             with self._phase("fire_host"):
                 host_rows = self._fire_host(P["wm"], jobs)
             out = self._fire_rows(P["wm"], fire_rows, host_rows)
@@ -521,6 +525,7 @@ class KeyedSessionOperator:
                 ex["record_widenings"] = ex.get("record_widenings", 0) + 1
             if host[3]:
                 self._alloc(self.batch_capacity, self.slack * 2)
+            self._rehash_if_due()
             self._empty_steps = empty0
             self._process_sync(keys, ts, vals, fire=False, exact=exact)
             self._pend = {"tbase": 0, "old_wm": old_wm, "wm": self.wm, "ev": None, "done": True}
@@ -545,8 +550,17 @@ class KeyedSessionOperator:
             if not P["done"]:
                 h = self._counters_read(P["ev"])
                 self._fold_finish(h, h[0], P["tbase"], P["old_wm"], 32)
+            self._rehash_if_due()
             out.append(self._fire_at(P["wm"]))
         return SessionRows.concat(out)
+
+    def _rehash_if_due(self) -> None:
+        """A rehash the spill check deferred while a fold was in flight (it moves slots; the
+        fold's overflow list and counters are read afterwards): done with no fold pending."""
+        if self._rehash_due:
+            self._rehash_due = False
+            self._rehash()
+            self._tombs_bound = 0
 
     def _sync_pending(self) -> None:
         """Before a state reader: apply the pending step; its rows wait for the next call."""
@@ -729,8 +743,9 @@ class KeyedSessionOperator:
                                 self.agg, self.cap_log2, self.nslots, self.sess.data_ptr(),
                                 self.slot_due.data_ptr(),
                                 self.slot_last.data_ptr(), self.late_cnt.data_ptr(),
-                                self.ovf_slots.data_ptr(), c[4:5].data_ptr(),
-                                self.ovf_rows.data_ptr(), c[5:6].data_ptr(), self.ovf_cap, st)
+                                self.keys_g.data_ptr(), self.ovf_slots.data_ptr(),
+                                c[4:5].data_ptr(), self.ovf_rows.data_ptr(), c[5:6].data_ptr(),
+                                self.ovf_cap, st)
         h = self._fold_counters()
         if h[2] > self.host_cap:
             raise RuntimeError("host diversion buffer overflow")
@@ -772,9 +787,9 @@ class KeyedSessionOperator:
                                   self.lateness, wm, tbase, self.agg, self.cap_log2, self.nslots,
                                   self.sess.data_ptr(), self.slot_due.data_ptr(),
                                   self.slot_last.data_ptr(), self.late_cnt.data_ptr(),
-                                  self.ovf_slots.data_ptr(), c[4:5].data_ptr(),
-                                  self.ovf_rows.data_ptr(), c[5:6].data_ptr(), self.ovf_cap, st,
-                                  _SESSION_PAIR)
+                                  self.keys_g.data_ptr(), self.ovf_slots.data_ptr(),
+                                  c[4:5].data_ptr(), self.ovf_rows.data_ptr(), c[5:6].data_ptr(),
+                                  self.ovf_cap, st, _SESSION_PAIR)
         return True
 
     def _fold_counters(self, with_red: bool = False) -> list[int]:
@@ -1006,9 +1021,12 @@ class KeyedSessionOperator:
             return 0
         if n_runs > self.ovf_cap:
             raise RuntimeError("session overflow-run buffer too small")
-        slots = self.ovf_slots[:n_ovf]
-        okeys = self.keys_g[slots].cpu().numpy()
-        sl = slots.cpu().numpy()
+        pairs = self.ovf_slots[:2 * n_ovf].view(n_ovf, 2)
+        slots = pairs[:, 0].contiguous()
+        # (the merge recorded each slot's key: a pipelined step's idle eviction may have
+        # tombstoned the slot since -- _evict skips it, its sessions are in the store already)
+        hp = pairs.cpu().numpy()
+        sl, okeys = hp[:, 0].copy(), hp[:, 1].copy()
         self._evict(slots=slots)
         rows = self.ovf_rows.view(5, self.ovf_cap)[:, :n_runs].cpu().numpy()
         # key of every run's slot (vectorised: sorted slots + searchsorted)
@@ -1295,7 +1313,9 @@ class KeyedSessionOperator:
         live, occupied = self._occ_pin.tolist()
         return int(live), int(occupied)
 
-    def _maybe_spill(self, wm: int) -> None:
+    def _maybe_spill(self, wm: int, inflight: bool = False) -> None:
+        """inflight: a fold is enqueued ahead of this check (pipelined step) -- a due rehash
+        waits for the next step (_rehash_if_due)."""
         # Live keys come from the kernels' insert / evict counters; the table is scanned only
         # after a restore and when the tombstone bound suggests a rehash.
         # Rehash (drop tombstones) once live + tombstones pass 0.8 of the slots with at least 8 %
@@ -1309,10 +1329,15 @@ class KeyedSessionOperator:
         t_occ = time.perf_counter()
 
         def rehash():
-            self._rehash()
-            self._tombs_bound = 0
+            if inflight:
+                self._rehash_due = True
+            else:
+                self._rehash()
+                self._tombs_bound = 0
 
-        if self._occ_exact:
+        if self._rehash_due:
+            live = self._live_estimate  # a rehash is already queued for the next step
+        elif self._occ_exact:
             live, occupied = self._count_occupancy()
             if due(live, occupied):
                 rehash()
@@ -1401,7 +1426,7 @@ class KeyedSessionOperator:
         for k in ("gap", "agg"):
             if meta[k] != getattr(self, k):
                 raise ValueError(f"checkpoint {k} does not match the operator")
-        self._pend, self._carry = None, []
+        self._pend, self._carry, self._rehash_due = None, [], False
         self.wm = meta["wm"]
         for k, v in meta.get("metrics", {}).items():
             setattr(self.metrics, k, v)
