@@ -284,6 +284,15 @@ class SessionCore {
       }
       return true;
     };
+    if (cold && no_hot && first_hot.empty()) {
+      // The common eviction (config 5): no hot state and every row fired unmodified -- every
+      // row is cold, no per-row classification (build_cold reads isc only when nc < n).
+      int64_t em = INT64_MIN;
+      for (int64_t i = 0; i < n; ++i) em = E[i] > em ? E[i] : em;
+      p.nc = n;
+      p.emax = em;
+      return;
+    }
     if (cold) {
       p.isc.resize((size_t)n);
       int64_t c = 0, em = INT64_MIN;
@@ -962,6 +971,35 @@ class SessionCore {
   // overflow only -- which makes it a pure function of the detached chunks).
   void released_of(const std::vector<ColdChunk>& gone, std::vector<int64_t>& released) const {
     const bool no_hot = m_.empty();
+    size_t rows = 0;
+    for (const ColdChunk& ch : gone) rows += ch.key.size();
+    if (no_hot && pool_ && rows >= 262144) {
+      // Row blocks on the store's pool: count the live rows per block, then each block writes
+      // its keys at its offset (the order of the serial loop).
+      constexpr size_t kBlk = 65536;
+      std::vector<std::pair<const ColdChunk*, size_t>> blocks;
+      for (const ColdChunk& ch : gone)
+        for (size_t a = 0; a < ch.key.size(); a += kBlk) blocks.push_back({&ch, a});
+      std::vector<size_t> cnt(blocks.size() + 1, 0);
+      pool_->run((int)blocks.size(), [&](int b) {
+        const ColdChunk& ch = *blocks[(size_t)b].first;
+        const size_t a = blocks[(size_t)b].second, e = std::min(ch.key.size(), a + kBlk);
+        size_t c = 0;
+        for (size_t r = a; r < e; ++r) c += ch.cnt[r] != 0;
+        cnt[(size_t)b + 1] = c;
+      });
+      for (size_t b = 0; b < blocks.size(); ++b) cnt[b + 1] += cnt[b];
+      const size_t base = released.size();
+      released.resize(base + cnt.back());
+      pool_->run((int)blocks.size(), [&](int b) {
+        const ColdChunk& ch = *blocks[(size_t)b].first;
+        const size_t a = blocks[(size_t)b].second, e = std::min(ch.key.size(), a + kBlk);
+        int64_t* o = released.data() + base + cnt[(size_t)b];
+        for (size_t r = a; r < e; ++r)
+          if (ch.cnt[r]) *o++ = (int64_t)ch.key[r];
+      });
+      return;
+    }
     for (const ColdChunk& ch : gone) {
       released.reserve(released.size() + ch.key.size());
       for (size_t r = 0; r < ch.key.size(); ++r)

@@ -764,3 +764,25 @@ def test_gpu_pipelined_snapshot_flushes_pending():
         r = op.finish()
         fired[i].update(zip(r.keys.tolist(), r.start.tolist(), r.raw.tolist()))
     assert fired[0] == fired[1] and sum(fired[0].values()) > 0
+
+
+def test_store_worker_expiry_releases_large_chunks():
+    """The worker's expiry of big cold chunks (the parallel released-key gather, >= 256K rows)
+    releases exactly the keys of the live rows, in row order."""
+    from mxstream.ops.native import load
+
+    m = load()
+    st_ = m.SessionStore(100, 1_000, K.AGG_SUM_I64)
+    n = 300_000
+    k = np.arange(n, dtype=np.int64) * 3 + 7
+    one = np.ones_like(k)
+    cnt = np.where(np.arange(n) % 5 == 0, 0, 1).astype(np.int64)  # some rows already taken
+    buf, offs = _slab([k, k % 1000, k % 1000 + 50, k % 11, cnt, one], n)
+    st_.spill_submit(-1, buf.ctypes.data, 0, offs, n)
+    st_.spill_join()
+    buf2, offs2 = _slab([k[:1] + 1, k[:1], k[:1], k[:1], one[:1], one[:1]], 1)
+    st_.spill_submit(-1, buf2.ctypes.data, 0, offs2, 1, 10 ** 9)  # expiry at a late watermark
+    res = st_.spill_join()
+    rel = np.concatenate([r["released"] for r in res])
+    live = k[cnt != 0]
+    assert np.array_equal(rel[:len(live)], live)
