@@ -107,14 +107,14 @@ void java_split(std::string_view line, char sep, std::vector<std::string_view>& 
     out.push_back(line);
     return;
   }
-  size_t start = 0;
-  for (size_t i = 0; i < line.size(); ++i) {
-    if (line[i] == sep) {
-      out.push_back(line.substr(start, i - start));
-      start = i + 1;
-    }
+  const char* const b = line.data();
+  const char* const e = b + line.size();
+  const char* start = b;
+  for (const char* q; (q = static_cast<const char*>(std::memchr(start, sep, (size_t)(e - start))));) {
+    out.push_back(std::string_view(start, (size_t)(q - start)));
+    start = q + 1;
   }
-  out.push_back(line.substr(start));
+  out.push_back(std::string_view(start, (size_t)(e - start)));
   while (!out.empty() && out.back().empty()) out.pop_back();
 }
 
@@ -234,16 +234,52 @@ enum FieldKind : int {
 
 // Parse one line's fields into row `li` of the columns. String fields get a thread-local id
 // (remapped to the dictionary's ids afterwards). Throws ParseError.
+// Open addressing over (hash, id) words with linear probing: field values are short (host
+// names, "cpuN"), a lookup is one hash of <= a few words and, on a hit, one compare.
 struct LocalDict {
-  std::unordered_map<std::string_view, uint32_t> ids;
   std::vector<std::string_view> strs;
+  std::vector<uint64_t> tab = std::vector<uint64_t>(1024, 0);  // (hash hi 32 | id + 1), 0 = empty
+  static uint64_t hash(std::string_view v) {
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)v.size();
+    size_t i = 0;
+    for (; i + 8 <= v.size(); i += 8) {
+      uint64_t w;
+      std::memcpy(&w, v.data() + i, 8);
+      h = mix64(h ^ w);
+    }
+    if (i < v.size()) {
+      uint64_t w = 0;
+      std::memcpy(&w, v.data() + i, v.size() - i);
+      h = mix64(h ^ w);
+    }
+    return h;
+  }
+  void grow() {
+    std::vector<uint64_t> t(tab.size() * 2, 0);
+    const size_t mask = t.size() - 1;
+    for (uint64_t x : tab) {
+      if (!x) continue;
+      size_t j = (size_t)(hash(strs[(uint32_t)x - 1]) & mask);
+      while (t[j]) j = (j + 1) & mask;
+      t[j] = x;
+    }
+    tab.swap(t);
+  }
   uint32_t intern(std::string_view v) {
-    auto it = ids.find(v);
-    if (it != ids.end()) return it->second;
-    const uint32_t id = (uint32_t)strs.size();
-    strs.push_back(v);
-    ids.emplace(v, id);
-    return id;
+    const uint64_t h = hash(v);
+    const uint64_t tag = h >> 32 << 32;
+    const size_t mask = tab.size() - 1;
+    for (size_t j = (size_t)(h & mask);; j = (j + 1) & mask) {
+      const uint64_t x = tab[j];
+      if (!x) {
+        const uint32_t id = (uint32_t)strs.size();
+        strs.push_back(v);
+        tab[j] = tag | (uint64_t)(id + 1);
+        if (2 * strs.size() > tab.size()) grow();
+        return id;
+      }
+      if ((x >> 32 << 32) == tag && strs[(uint32_t)x - 1] == v) return (uint32_t)x - 1;
+    }
   }
 };
 
@@ -290,13 +326,14 @@ static void parse_line_into(std::string_view line, char sep,
 // newline does not start a line.
 static void find_lines(std::string_view all, size_t a, size_t b, std::vector<std::string_view>& out) {
   size_t start = a;
-  for (size_t i = a; i < b; ++i) {
-    if (all[i] == '\n') {
-      std::string_view l = all.substr(start, i - start);
-      if (!l.empty() && l.back() == '\r') l.remove_suffix(1);
-      out.push_back(l);
-      start = i + 1;
-    }
+  out.reserve(out.size() + (b - a) / 24 + 16);
+  for (const char* q; start < b &&
+                      (q = static_cast<const char*>(std::memchr(all.data() + start, '\n', b - start)));) {
+    const size_t i = (size_t)(q - all.data());
+    std::string_view l = all.substr(start, i - start);
+    if (!l.empty() && l.back() == '\r') l.remove_suffix(1);
+    out.push_back(l);
+    start = i + 1;
   }
   if (start < b) {
     std::string_view l = all.substr(start, b - start);
