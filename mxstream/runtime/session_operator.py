@@ -204,11 +204,12 @@ class KeyedSessionOperator:
             # counters: [0] n_out [1] n_heads [2] n_host [3] n_inserted(step) [4] n_ovf
             #           [5] n_ovf_runs [6] fire n_out [7] evict rows [8] evicted [9] rehash ins
             self.ctr = torch.zeros(16, dtype=torch.int32, device=dev)
-            # The two pinned slabs of the asynchronous eviction copy, at their final size now
-            # (page-locking ~100 MB costs ~15 ms: never inside a step).
+            # The pinned slabs of the asynchronous eviction copy, at their final size now
+            # (page-locking ~100 MB costs ~15 ms: never inside a step) -- a third one with the
+            # pipelined step, whose evictions trail a fold, so the store worker may lag a step.
             nb = ((self.ctr.numel() * 4 + 255) & ~255) + 6 * ((self.spill_rows * 8 + 255) & ~255)
             self._spill_slabs = []
-            for _ in range(2):
+            for _ in range(3 if self.pipeline else 2):
                 t = torch.empty(_next_pow2(nb), dtype=torch.uint8, pin_memory=True)
                 self._spill_slabs.append([t, t.numpy(), 0])  # tensor, array, job id
             self._spill_turn = 0
@@ -1158,7 +1159,7 @@ class KeyedSessionOperator:
         if getattr(self, "_spill_stream", None) is None:
             self._spill_stream = torch.cuda.Stream(self.device)
         slab = self._spill_slabs[self._spill_turn]
-        self._spill_turn ^= 1
+        self._spill_turn = (self._spill_turn + 1) % len(self._spill_slabs)
         if slab[2] > self.store.spill_completed():
             self._join_spill()  # that slab's rows are still being read by the worker
 
