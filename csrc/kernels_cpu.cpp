@@ -40,20 +40,18 @@ void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
                 int32_t val_f64, double zipf_s, uint64_t key_base) {
-  auto mulhi = [](uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); };
   const double span_per_event = (double)ts_span / (double)n;
   const uint64_t disorder_p1 = (uint64_t)(disorder + 1);
+  const uint64_t base = mix64(seed ^ (stream_id * 0xd1b54a32d192ed03ull));
   for (int64_t i = 0; i < n; ++i) {
-    const uint64_t r = rng64(seed, stream_id, idx0 + (uint64_t)i);
-    const uint64_t r2 = mix64(r);
-    const uint64_t r3 = mix64(r2);
-    const uint64_t key = (zipf_s > 0.0 ? zipf_key(r, nkeys, zipf_s) : mulhi(r, nkeys)) + key_base;
+    uint64_t key;
+    int64_t t, v;
+    gen_event(base, idx0 + (uint64_t)i, i, nkeys, ts_base, span_per_event, disorder_p1, val_lo,
+              val_span > 0 ? (uint64_t)val_span : 0, zipf_s, key, t, v);
+    key += key_base;
     if (val_f64 & 2) reinterpret_cast<int32_t*>(keys)[i] = (int32_t)key;
     else keys[i] = key;
-    int64_t t = ts_base + (int64_t)((double)i * span_per_event);
-    if (disorder_p1 > 1) t -= (int64_t)mulhi(r2, disorder_p1);
     ts[i] = t;
-    const int64_t v = val_lo + (val_span > 0 ? (int64_t)mulhi(r3, (uint64_t)val_span) : 0);
     vals[i] = (val_f64 & 1) ? f64_bits((double)v) : (uint64_t)v;
   }
 }

@@ -81,18 +81,14 @@ __device__ __forceinline__ uint64_t f64_unord(int64_t o) {
 // Synthetic source: SoA (key, ts, val) batch from a counter-based RNG (device-side so the
 // benchmark measures the engine, not PCIe).
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void gen_one(uint64_t seed, uint64_t stream_id, uint64_t idx,
-                                        int64_t i, uint64_t nkeys, int64_t ts_base,
-                                        double span_per_event, uint64_t disorder_p1,
-                                        int64_t val_lo, uint64_t val_span, int32_t mode,
-                                        double zipf_s, uint64_t& key, int64_t& t, uint64_t& v) {
-  const uint64_t r = rng64(seed, stream_id, idx);
-  const uint64_t r2 = mix64(r);
-  const uint64_t r3 = mix64(r2);
-  key = zipf_s > 0.0 ? zipf_key(r, nkeys, zipf_s) : __umul64hi(r, nkeys);  // multiply-shift
-  t = ts_base + (int64_t)((double)i * span_per_event);
-  if (disorder_p1 > 1) t -= (int64_t)__umul64hi(r2, disorder_p1);
-  const int64_t x = val_lo + (val_span ? (int64_t)__umul64hi(r3, val_span) : 0);
+__device__ __forceinline__ void gen_one(uint64_t base, uint64_t idx, int64_t i, uint64_t nkeys,
+                                        int64_t ts_base, double span_per_event,
+                                        uint64_t disorder_p1, int64_t val_lo, uint64_t val_span,
+                                        int32_t mode, double zipf_s, uint64_t& key, int64_t& t,
+                                        uint64_t& v) {
+  int64_t x;
+  gen_event(base, idx, i, nkeys, ts_base, span_per_event, disorder_p1, val_lo, val_span, zipf_s,
+            key, t, x);
   v = (mode & 1) ? f64_bits((double)x) : (uint64_t)x;
 }
 
@@ -108,14 +104,15 @@ __global__ __launch_bounds__(256) void gen_events_kernel(
   // zipf_s > 0: skewed keys (key_of_draw: power law, rank 0 hottest); 0: uniform.
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t npairs = n >> 1;
+  const uint64_t base = mix64(seed ^ (stream_id * 0xd1b54a32d192ed03ull));  // rng64's stream word
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < npairs; p += stride) {
     const int64_t i = 2 * p;
     uint64_t k0, k1, v0, v1;
     int64_t t0, t1;
-    gen_one(seed, stream_id, idx0 + (uint64_t)i, i, nkeys, ts_base, span_per_event, disorder_p1,
-            val_lo, val_span, mode, zipf_s, k0, t0, v0);
-    gen_one(seed, stream_id, idx0 + (uint64_t)i + 1, i + 1, nkeys, ts_base, span_per_event,
-            disorder_p1, val_lo, val_span, mode, zipf_s, k1, t1, v1);
+    gen_one(base, idx0 + (uint64_t)i, i, nkeys, ts_base, span_per_event, disorder_p1, val_lo,
+            val_span, mode, zipf_s, k0, t0, v0);
+    gen_one(base, idx0 + (uint64_t)i + 1, i + 1, nkeys, ts_base, span_per_event, disorder_p1,
+            val_lo, val_span, mode, zipf_s, k1, t1, v1);
     k0 += key_base;  // (a drifting key window: no separate add pass over the column)
     k1 += key_base;
     if (mode & 4) {  // a column not 16-byte aligned (a sliced tensor): scalar stores
@@ -144,8 +141,8 @@ __global__ __launch_bounds__(256) void gen_events_kernel(
     const int64_t i = n - 1;
     uint64_t k, v;
     int64_t t;
-    gen_one(seed, stream_id, idx0 + (uint64_t)i, i, nkeys, ts_base, span_per_event, disorder_p1,
-            val_lo, val_span, mode, zipf_s, k, t, v);
+    gen_one(mix64(seed ^ (stream_id * 0xd1b54a32d192ed03ull)), idx0 + (uint64_t)i, i, nkeys,
+            ts_base, span_per_event, disorder_p1, val_lo, val_span, mode, zipf_s, k, t, v);
     k += key_base;
     if (mode & 2) reinterpret_cast<int32_t*>(keys)[i] = (int32_t)k;
     else keys[i] = k;
@@ -4332,7 +4329,7 @@ void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t
   hipLaunchKernelGGL(gen_events_kernel, dim3(grid_for((n + 1) / 2, 256, 8192)), dim3(256), 0,
                      (hipStream_t)stream, keys, ts, vals, n, seed, stream_id, idx0, nkeys, ts_base,
                      (double)ts_span / (double)n, (uint64_t)(disorder + 1), val_lo,
-                     (uint64_t)val_span, mode, zipf_s, key_base);
+                     (uint64_t)(val_span > 0 ? val_span : 0), mode, zipf_s, key_base);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -149,6 +149,39 @@ MXS_HD uint64_t rng64(uint64_t seed, uint64_t stream, uint64_t idx) {
   return mix64(mix64(seed ^ (stream * 0xd1b54a32d192ed03ull)) + idx * 0x9e3779b97f4a7c15ull);
 }
 
+MXS_HD uint64_t mulhi_u64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(a, b);
+#else
+  return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+
+// r * n >> 32 for n <= 2^32: a uniform draw in [0, n) from 32 random bits (one 32x32 -> 64
+// multiply on the device instead of the four of a 64-bit high product).
+MXS_HD uint64_t draw32(uint32_t r, uint64_t n) { return ((uint64_t)r * n) >> 32; }
+
+// One synthetic event (the source of the benchmarks and tests; CPU and GPU bit-identical except
+// with zipf_s > 0): two splitmix64 words per event -- the key from the high half of the first
+// (all of it for key spaces beyond 2^32 or the power law), the disorder from the low half of
+// the second and the value from its high half (32-bit draws whenever the range fits).
+// `base` = rng64's per-(seed, stream) word mix64(seed ^ stream * C), hoisted by the caller.
+MXS_HD void gen_event(uint64_t base, uint64_t idx, int64_t i, uint64_t nkeys, int64_t ts_base,
+                      double span_per_event, uint64_t disorder_p1, int64_t val_lo,
+                      uint64_t val_span, double zipf_s, uint64_t& key, int64_t& t, int64_t& v) {
+  const uint64_t r = mix64(base + idx * 0x9e3779b97f4a7c15ull);
+  const uint64_t r2 = mix64(r);
+  key = zipf_s > 0.0 ? zipf_key(r, nkeys, zipf_s)
+                     : (nkeys <= (1ull << 32) ? draw32((uint32_t)(r >> 32), nkeys) : mulhi_u64(r, nkeys));
+  t = ts_base + (int64_t)((double)i * span_per_event);
+  if (disorder_p1 > 1)
+    t -= (int64_t)(disorder_p1 <= (1ull << 32) ? draw32((uint32_t)r2, disorder_p1)
+                                               : mulhi_u64(r2, disorder_p1));
+  v = val_lo + (int64_t)(val_span == 0 ? 0
+                         : val_span <= (1ull << 32) ? draw32((uint32_t)(r2 >> 32), val_span)
+                                                    : mulhi_u64(mix64(r2), val_span));
+}
+
 // ---------------------------------------------------------------------------------------------
 // Window math (Flink 1.8 TimeWindow semantics, Java '%' = truncated remainder)
 // ---------------------------------------------------------------------------------------------
