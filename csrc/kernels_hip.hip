@@ -1088,7 +1088,18 @@ __global__ void step_finish_kernel(const int64_t* __restrict__ stats, int64_t* _
                                    int64_t bound, int32_t event_mode, int64_t proc_now,
                                    int64_t* __restrict__ red, const uint32_t* __restrict__ flags,
                                    int32_t idle, int64_t* __restrict__ host_red, int32_t fill_word,
-                                   const uint32_t* __restrict__ cursor, int nb) {
+                                   const uint32_t* __restrict__ cursor, int nb,
+                                   uint32_t* __restrict__ next_cursor,
+                                   int64_t* __restrict__ next_stats) {
+  // A later step's cursors and stats (distinct buffers): step_begin's work, in this launch.
+  if (next_cursor) {
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) next_cursor[i] = 0;
+    if (threadIdx.x < kStatCount) {
+      const int j = threadIdx.x;
+      next_stats[j] = j == kStatMaxTs ? INT64_MIN : j == kStatMinPane ? INT64_MAX
+                    : j == kStatMaxPane ? INT64_MIN : 0;
+    }
+  }
   // fill_word: the largest bucket fill, from the cursors (every partition variant fills them)
   __shared__ uint32_t fmax[64];
   if (fill_word) {
@@ -4342,10 +4353,11 @@ void step_begin(uint32_t* cursor, int nb, int64_t* stats, intptr_t stream) {
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
                  int64_t proc_now, int64_t* red, const uint32_t* flags, intptr_t stream,
                  int32_t idle, int64_t* host_red, int32_t fill_word, const uint32_t* cursor,
-                 int nb) {
+                 int nb, uint32_t* next_cursor, int64_t* next_stats) {
   hipLaunchKernelGGL(step_finish_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, stats,
                      local_maxts, bound, event_mode, proc_now, red, flags, idle, host_red,
-                     fill_word && cursor ? 1 : 0, cursor, nb);
+                     fill_word && cursor ? 1 : 0, cursor, nb, next_stats ? next_cursor : nullptr,
+                     next_cursor ? next_stats : nullptr);
   HIP_CHECK(hipGetLastError());
 }
 

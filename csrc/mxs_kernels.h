@@ -399,10 +399,14 @@ void rolling_scan(int agg, const int64_t* sk, const int64_t* perm, const uint64_
 // fill_word (with the bucket cursors): red[3] carries -(largest bucket fill) instead of
 // -(overflow bit) (an overflow is -2^40): the MIN all-reduce then gives every rank the global
 // fill that sizes the exchange.
+// next_cursor / next_stats (both or neither): the buffers of a later step, zeroed and reset
+// here as step_begin would -- that step then skips its step_begin launch (WindowStep rotates
+// three cursor / stats sets, so the set reset here is no longer read by anything queued).
 void step_finish(const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
                  int64_t proc_now, int64_t* red, const uint32_t* flags, intptr_t stream,
                  int32_t idle = 0, int64_t* host_red = nullptr, int32_t fill_word = 0,
-                 const uint32_t* cursor = nullptr, int nb = 0);
+                 const uint32_t* cursor = nullptr, int nb = 0, uint32_t* next_cursor = nullptr,
+                 int64_t* next_stats = nullptr);
 // The combiner's overflow check as a MIN all-reduce operand: chk = [-(flags[0] & 2),
 // -max(counts[0..nb))], and chk[2] = sum(counts) (this rank's combined records).
 void combine_check(const uint32_t* flags, const uint32_t* counts, int nb, int64_t* chk,

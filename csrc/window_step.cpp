@@ -253,9 +253,11 @@ WindowStep::WindowStep(const WindowStepConfig& c, std::shared_ptr<StepComm> comm
   slack_ = c.bucket_slack;
   alloc_buckets(c.batch_capacity, c.bucket_slack);
   for (int p = 0; p < (pipeline_ ? 2 : 1); ++p) {
-    stats_[p] = mem_alloc(kStatCount * 8, dk);
     red_[p] = mem_alloc(kRedWords * 8, dk);
     hred_[p] = mem_alloc(kRedWords * 8, gpu_ ? 2 : 0);
+  }
+  for (int p = 0; p < 3; ++p) {
+    stats_[p] = mem_alloc(kStatCount * 8, dk);
     const int64_t init[kStatCount] = {INT64_MIN, INT64_MAX, INT64_MIN, 0, 0, 0, 0, 0};
     if (gpu_) hip_ok(hipMemcpy(stats_[p]->p, init, sizeof(init), hipMemcpyHostToDevice), "H2D");
     else std::memcpy(stats_[p]->p, init, sizeof(init));
@@ -397,9 +399,10 @@ void WindowStep::alloc_buckets(int64_t capacity, double slack) {
   bucket_cap_ = (cap + 7) & ~(int64_t)7;
   const size_t words = (size_t)nbuckets_ * bucket_cap_ * 3;
   const int dk = gpu_ ? 1 : 0;
-  for (int p = 0; p < (pipeline_ ? 2 : 1); ++p) {
-    send_[p] = mem_alloc(words * 8, dk, false);
+  for (int p = 0; p < (pipeline_ ? 2 : 1); ++p) send_[p] = mem_alloc(words * 8, dk, false);
+  for (int p = 0; p < 3; ++p) {
     cursor_[p] = mem_alloc(nbuckets_ * 4, dk);
+    cready_[p] = false;  // (fresh buffers: the next front runs its step_begin)
   }
   recv_ = exchanging_ && !combine_ ? mem_alloc(words * 8, dk, false) : nullptr;
   recv_counts_ = exchanging_ ? mem_alloc(nbuckets_ * 4, dk) : nullptr;
@@ -700,6 +703,8 @@ WindowStep::Front WindowStep::front(const void* keys, bool key32, const int64_t*
   Front f;
   f.par = par_;
   if (pipeline_) par_ ^= 1;
+  f.cpar = cpar_;
+  cpar_ = (cpar_ + 1) % 3;
   empty_steps_ = n == 0 ? empty_steps_ + 1 : 0;
   f.keys = keys;
   f.key32 = key32;
@@ -763,9 +768,10 @@ void WindowStep::launch_front(Front& f) {
   pplan_.tbase = ctl_.pane_start(f.pane_base);
   if (f.n >= ((int64_t)1 << 32)) throw std::invalid_argument("batch too large (2^32 events)");
   const int nb = nbuckets_;
-  uint32_t* cur = P<uint32_t>(cursor_[p]);
+  const int cp = f.cpar, cn = (f.cpar + 1) % 3;
+  uint32_t* cur = P<uint32_t>(cursor_[cp]);
   Rec* send = P<Rec>(send_[p]);
-  int64_t* stats = P<int64_t>(stats_[p]);
+  int64_t* stats = P<int64_t>(stats_[cp]);
   int64_t* red = P<int64_t>(red_[p]);
   uint32_t* li = P<uint32_t>(late_idx_);
   const uint32_t lcap = late_idx_ ? (uint32_t)cfg_.late_capacity : 0u;
@@ -774,13 +780,16 @@ void WindowStep::launch_front(Front& f) {
   Stage stage(this, "partition");
   if (gpu_) {
     const intptr_t s = (intptr_t)cur_;
-    gpu::step_begin(cur, nb, stats, s);
+    if (!cready_[cp]) gpu::step_begin(cur, nb, stats, s);  // (else reset by the last step_finish)
+    cready_[cp] = false;  // a redo of this step resets them again
     if (f.n)
       gpu::partition((const uint64_t*)keys_in, f.ts, (const uint64_t*)f.vals, cfg_.jhash, f.n,
                      pplan_, P<int32_t>(kg_dest_), cur, send, stats, li, lcap, s);
     gpu::step_finish(stats, P<int64_t>(local_maxts_), bound, ev, f.proc_now, red,
                      P<uint32_t>(flags_), s, f.idle ? 1 : 0,
-                     world_ == 1 ? P<int64_t>(hred_[p]) : nullptr, exchanging_ ? 1 : 0, cur, nb);
+                     world_ == 1 ? P<int64_t>(hred_[p]) : nullptr, exchanging_ ? 1 : 0, cur, nb,
+                     P<uint32_t>(cursor_[cn]), P<int64_t>(stats_[cn]));
+    cready_[cn] = true;
   } else {
     cpu::step_begin(cur, nb, stats);
     std::vector<uint64_t> wide;
@@ -852,6 +861,7 @@ WindowStep::Back WindowStep::settle(Front& f) {
   }
   Back b;
   b.par = f.par;
+  b.cpar = f.cpar;
   b.n = f.n;
   b.old_wm = f.old_wm;
   b.rw = f.rw;
@@ -918,7 +928,7 @@ void WindowStep::back_finish(Back& b) {
   StreamScope sc(this, true);
   if (b.has_data) {
     const Rec* recs = exchanging_ ? P<Rec>(recv_) : P<Rec>(send_[b.par]);
-    const uint32_t* counts = exchanging_ ? P<uint32_t>(recv_counts_) : P<uint32_t>(cursor_[b.par]);
+    const uint32_t* counts = exchanging_ ? P<uint32_t>(recv_counts_) : P<uint32_t>(cursor_[b.cpar]);
     uint32_t bcap = (uint32_t)bucket_cap_;
     int combined = 0;
     if (combine_) {
@@ -1043,10 +1053,10 @@ void WindowStep::exchange_records(Back& b, uint32_t* xcap_out) {
   const uint32_t xcap = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(b.fill, bucket_cap_));
   if (!xsend_) xsend_ = mem_alloc((size_t)nbuckets_ * bucket_cap_ * 24, gpu_ ? 1 : 0, false);
   if (gpu_)
-    gpu::bucket_repack(P<uint64_t>(send_[b.par]), P<uint32_t>(cursor_[b.par]), nbuckets_,
+    gpu::bucket_repack(P<uint64_t>(send_[b.par]), P<uint32_t>(cursor_[b.cpar]), nbuckets_,
                        (uint32_t)bucket_cap_, xcap, rw, P<uint64_t>(xsend_), nullptr, (intptr_t)cur_);
   else
-    cpu::bucket_repack(P<uint64_t>(send_[b.par]), P<uint32_t>(cursor_[b.par]), nbuckets_,
+    cpu::bucket_repack(P<uint64_t>(send_[b.par]), P<uint32_t>(cursor_[b.cpar]), nbuckets_,
                        (uint32_t)bucket_cap_, xcap, rw, P<uint64_t>(xsend_), nullptr);
   const int64_t words = (int64_t)nbuckets_ * xcap * rw;
   if (cfg_.dim > 0) {
@@ -1056,17 +1066,17 @@ void WindowStep::exchange_records(Back& b, uint32_t* xcap_out) {
       recv_vec_ = mem_alloc(need * 4, gpu_ ? 1 : 0);
     }
     if (gpu_)
-      gpu::vec_gather(xsend_->p, rw, P<uint32_t>(cursor_[b.par]), nbuckets_, xcap, b.vecs,
+      gpu::vec_gather(xsend_->p, rw, P<uint32_t>(cursor_[b.cpar]), nbuckets_, xcap, b.vecs,
                       cfg_.dim, P<float>(send_vec_), (intptr_t)cur_);
     else
-      cpu::vec_gather(xsend_->p, rw, P<uint32_t>(cursor_[b.par]), nbuckets_, xcap, b.vecs,
+      cpu::vec_gather(xsend_->p, rw, P<uint32_t>(cursor_[b.cpar]), nbuckets_, xcap, b.vecs,
                       cfg_.dim, P<float>(send_vec_));
     comm_->all_to_all(recv_vec_->p, send_vec_->p, need * 4, 4, (intptr_t)cur_);
     m_.a2a_bytes += need * 4;
     m_.payload_bytes += b.accepted * cfg_.dim * 4;
   }
   comm_->all_to_all(recv_->p, xsend_->p, words * 8, 8, (intptr_t)cur_);
-  comm_->all_to_all(recv_counts_->p, cursor_[b.par]->p, (int64_t)nbuckets_ * 4, 4, (intptr_t)cur_);
+  comm_->all_to_all(recv_counts_->p, cursor_[b.cpar]->p, (int64_t)nbuckets_ * 4, 4, (intptr_t)cur_);
   m_.a2a_bytes += words * 8;
   m_.payload_bytes += b.accepted * rw * 8;
   *xcap_out = xcap;
@@ -1100,13 +1110,13 @@ void WindowStep::combine_begin(Back& b) {
   cp.split = 1;
   // chk = [-(overflow bit), -(largest combined bucket)] (window_combine writes both)
   if (gpu_) {
-    gpu::window_combine(P<Rec>(send_[b.par]), P<uint32_t>(cursor_[b.par]), nbuckets_, cp,
+    gpu::window_combine(P<Rec>(send_[b.par]), P<uint32_t>(cursor_[b.cpar]), nbuckets_, cp,
                         P<Rec>(comb_send_), (uint32_t)ccap, P<uint32_t>(comb_counts_),
                         P<uint32_t>(flags_) + 1, (intptr_t)cur_);
     gpu::combine_check(P<uint32_t>(flags_) + 1, P<uint32_t>(comb_counts_), nbuckets_,
                        P<int64_t>(chk_), (intptr_t)cur_);
   } else {
-    cpu::window_combine(P<Rec>(send_[b.par]), P<uint32_t>(cursor_[b.par]), nbuckets_, cp,
+    cpu::window_combine(P<Rec>(send_[b.par]), P<uint32_t>(cursor_[b.cpar]), nbuckets_, cp,
                         P<Rec>(comb_send_), (uint32_t)ccap, P<uint32_t>(comb_counts_),
                         P<uint32_t>(flags_) + 1);
     const uint32_t* cc = P<uint32_t>(comb_counts_);

@@ -246,14 +246,14 @@ class WindowStep {
     const void* vals = nullptr;
     const float* vecs = nullptr;
     int64_t n = 0;
-    int par = 0;
+    int par = 0, cpar = 0;
     int64_t old_wm = INT64_MIN, pane_base = 0, proc_now = 0;
     int rw = 3;
     bool idle = false;
     hipEvent_t ev = nullptr;
   };
   struct Back {
-    int par = 0;
+    int par = 0, cpar = 0;
     int64_t n = 0, old_wm = INT64_MIN, pane_base = 0;
     int rw = 3;
     bool has_data = false;
@@ -365,7 +365,13 @@ class WindowStep {
   Buf keys_g_, acc_g_, cnt_g_, dirty_g_, dacc_g_, dcnt_g_, vacc_g_, occ_, flags_, kg_dest_;
   Buf local_maxts_, dlist_, dlist_n_, slot_mark_, late_idx_, minbuf_, hflags_, wide_;
   bool block_hint_ = true;
-  Buf send_[2], cursor_[2], stats_[2], red_[2], hred_[2];
+  Buf send_[2], red_[2], hred_[2];
+  // Bucket cursors and partition stats rotate over three sets (cpar): a step's step_finish
+  // resets the next step's set, last read by the state half of the step two before (queued
+  // ahead, or waited for through ev_consumed_) -- the next step launches no step_begin.
+  Buf cursor_[3], stats_[3];
+  int cpar_ = 0;
+  bool cready_[3] = {false, false, false};
   Buf recv_, recv_counts_, scratch_, scratch_cursor_, comb_send_, comb_recv_, comb_counts_;
   Buf chk_, hchk_;
   Buf out_keys_, out_vals_, out_raw_, out_cnt_, fire_bounds_, hbounds_, out_vec_;
