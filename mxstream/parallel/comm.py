@@ -17,6 +17,10 @@ import os
 import torch
 import torch.distributed as dist
 
+from ..utils.log import get_logger
+
+log = get_logger(__name__)
+
 
 class Comm:
     """Interface; LocalComm is the G=1 case, TorchComm the multi-process one."""
@@ -276,9 +280,13 @@ def run_loopback(world: int, fn, *args, device: torch.device | None = None,
         t.start()
     for t in ths:
         t.join()
-    first = next((e for e in errs if e is not None and not isinstance(e, threading.BrokenBarrierError)),
+    first = next((e for e in errs if e is not None and not isinstance(e, threading.BrokenBarrierError)
+                  and not isinstance(e.__cause__, threading.BrokenBarrierError)),
                  next((e for e in errs if e is not None), None))
     if first is not None:
+        for r, e in enumerate(errs):  # the other ranks' errors, for the log
+            if e is not None and e is not first:
+                log.warning("loopback rank %d also failed: %s: %s", r, type(e).__name__, e)
         raise first
     return res
 
