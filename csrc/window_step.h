@@ -371,6 +371,9 @@ class WindowStep {
   // ahead, or waited for through ev_consumed_) -- the next step launches no step_begin.
   Buf cursor_[3], stats_[3];
   int cpar_ = 0;
+  // Device bytes the fused re-firing's staging may take to skip its list-length read
+  // (MXS_REFIRE_STAGE_MB, default 8 GiB of the 288 GB HBM).
+  int64_t refire_stage_budget_ = (int64_t)8192 << 20;
   bool cready_[3] = {false, false, false};
   Buf recv_, recv_counts_, scratch_, scratch_cursor_, comb_send_, comb_recv_, comb_counts_;
   Buf chk_, hchk_;
