@@ -11,8 +11,10 @@ concurrently, so it is per-link bound and never the bottleneck at micro-batch si
 """
 from __future__ import annotations
 
+import collections
 import datetime
 import os
+import sys
 
 import torch
 import torch.distributed as dist
@@ -94,6 +96,11 @@ class LoopbackGroup:
         self._barrier = threading.Barrier(world, timeout=timeout_s)
         self._slots: list = [None] * world
         self._events: list = [None] * world
+        # every collective's kind per rank, checked at its first barrier (a rank that enters a
+        # different collective than its peers fails loudly instead of mixing buffers), and the
+        # last few kinds with their callers, for that error message
+        self._kinds: list = [None] * world
+        self._hist: list = [collections.deque(maxlen=12) for _ in range(world)]
         self._done: list = [[None] * world for _ in range(world)]
         self.a2a_bytes = 0
 
@@ -132,11 +139,24 @@ class LoopbackComm(Comm):
 
     # Collective skeleton: deposit -> barrier -> read peers -> barrier (peers done reading) ->
     # the owner's stream waits for the readers' events before it reuses its buffer.
-    def _deposit(self, t) -> None:
+    def _enter(self, kind: str, slot) -> None:
+        """Deposit this rank's slot, wait for the peers, check they entered the same collective."""
         g = self.group_obj
-        g._slots[self.rank] = t
-        g._events[self.rank] = _record_event(t) if isinstance(t, torch.Tensor) else None
+        if isinstance(slot, torch.Tensor):
+            kind = f"{kind}[{slot.device.type},{str(slot.dtype)[6:]}]"
+        f = sys._getframe(2)
+        g._hist[self.rank].append(f"{kind} <- {f.f_code.co_name}:{f.f_lineno} "
+                                  f"<- {f.f_back.f_code.co_name if f.f_back else '?'}")
+        g._kinds[self.rank] = kind
+        g._slots[self.rank] = slot
+        g._events[self.rank] = _record_event(slot) if isinstance(slot, torch.Tensor) else None
         g.wait()
+        if any(k != kind for k in g._kinds):
+            hist = "\n".join(f"  rank {r}: " + " | ".join(list(h)[-4:]) for r, h in enumerate(g._hist))
+            raise RuntimeError(f"loopback collective mismatch: ranks entered {g._kinds}\n{hist}")
+
+    def _deposit(self, t, kind: str = "collective") -> None:
+        self._enter(kind, t)
 
     def _finish(self, t) -> None:
         g = self.group_obj
@@ -160,7 +180,7 @@ class LoopbackComm(Comm):
         if self.world == 1:
             LocalComm.all_to_all(self, out, inp)
             return
-        self._deposit(inp)
+        self._deposit(inp, "all_to_all")
         c = inp.numel() // self.world
         for src in range(self.world):
             peer = self._read(src, out)
@@ -174,7 +194,7 @@ class LoopbackComm(Comm):
     def _allreduce(self, t, op) -> None:
         if self.world == 1:
             return
-        self._deposit(t)
+        self._deposit(t, f"allreduce_{op.__name__}")
         acc = t.clone()
         for src in range(self.world):
             if src == self.rank:
@@ -203,12 +223,12 @@ class LoopbackComm(Comm):
 
     def barrier(self):
         if self.world > 1:
-            self.group_obj.wait()
+            self._enter("barrier", None)
 
     def broadcast_(self, t, src: int = 0):
         if self.world == 1:
             return
-        self._deposit(t)
+        self._deposit(t, f"broadcast_{src}")
         if self.rank != src:
             peer = self._read(src, t)
             t.copy_(peer)
@@ -219,8 +239,7 @@ class LoopbackComm(Comm):
         if self.world == 1:
             return obj
         g = self.group_obj
-        g._slots[self.rank] = obj
-        g.wait()
+        self._enter(f"broadcast_object_{src}", obj)
         v = g._slots[src]
         g.wait()
         return v
@@ -229,8 +248,7 @@ class LoopbackComm(Comm):
         if self.world == 1:
             return [obj]
         g = self.group_obj
-        g._slots[self.rank] = obj
-        g.wait()
+        self._enter("all_gather_object", obj)
         v = list(g._slots)
         g.wait()
         return v
