@@ -604,6 +604,10 @@ void WindowStep::process(const void* keys, bool key32, const int64_t* ts, const 
                          int64_t n, intptr_t stream, const float* vecs) {
   cur_ = s0_ = (hipStream_t)stream;
   block_hint_ = !pipeline_;
+  if (n > batch_capacity_ && world_ == 1 && pending_) {
+    // The buffers are reallocated for this batch: the queued state half reads the old ones.
+    flush(stream);
+  }
   if (!pipeline_) {
     Front f = front(keys, key32, ts, vals, vecs, n);
     Back b = settle(f);
@@ -697,7 +701,9 @@ int64_t WindowStep::pane_base(const int64_t* ts, int64_t n) {
 
 WindowStep::Front WindowStep::front(const void* keys, bool key32, const int64_t* ts,
                                     const void* vals, const float* vecs, int64_t n) {
-  if (n > batch_capacity_) {
+  // A batch past the capacity: one rank regrows alone (process() drained the pending state
+  // half first); with peers the regrow is agreed through the step's reduced vector (settle).
+  if (n > batch_capacity_ && world_ == 1) {
     flush((intptr_t)cur_);
     alloc_buckets(n, slack_);
   }
@@ -770,6 +776,9 @@ void WindowStep::launch_front(Front& f) {
   if (f.n >= ((int64_t)1 << 32)) throw std::invalid_argument("batch too large (2^32 events)");
   const int nb = nbuckets_;
   const int cp = f.cpar, cn = (f.cpar + 1) % 3;
+  // (G > 1) a batch past the capacity is not partitioned: red[4] = -(n << 1) asks every rank to
+  // regrow to n and redo the step (settle), so the bucket geometry stays the same on all ranks.
+  const bool over = f.n > batch_capacity_;
   uint32_t* cur = P<uint32_t>(cursor_[cp]);
   Rec* send = P<Rec>(send_[p]);
   int64_t* stats = P<int64_t>(stats_[cp]);
@@ -783,7 +792,7 @@ void WindowStep::launch_front(Front& f) {
     const intptr_t s = (intptr_t)cur_;
     if (!cready_[cp]) gpu::step_begin(cur, nb, stats, s);  // (else reset by the last step_finish)
     cready_[cp] = false;  // a redo of this step resets them again
-    if (f.n)
+    if (f.n && !over)
       gpu::partition((const uint64_t*)keys_in, f.ts, (const uint64_t*)f.vals, cfg_.jhash, f.n,
                      pplan_, P<int32_t>(kg_dest_), cur, send, stats, li, lcap, s);
     gpu::step_finish(stats, P<int64_t>(local_maxts_), bound, ev, f.proc_now, red,
@@ -791,6 +800,7 @@ void WindowStep::launch_front(Front& f) {
                      world_ == 1 ? P<int64_t>(hred_[p]) : nullptr, exchanging_ ? 1 : 0, cur, nb,
                      P<uint32_t>(cursor_[cn]), P<int64_t>(stats_[cn]));
     cready_[cn] = true;
+    if (over) gpu::fill_u64((uint64_t*)(red + 4), 1, (uint64_t)(-(f.n << 1)), s);
   } else {
     cpu::step_begin(cur, nb, stats);
     std::vector<uint64_t> wide;
@@ -801,11 +811,12 @@ void WindowStep::launch_front(Front& f) {
       for (int64_t i = 0; i < f.n; ++i) wide[(size_t)i] = (uint64_t)(int64_t)k32[i];
       keys = wide.data();
     }
-    if (f.n)
+    if (f.n && !over)
       cpu::partition((const uint64_t*)keys, f.ts, (const uint64_t*)f.vals, cfg_.jhash, f.n, pplan_,
                      P<int32_t>(kg_dest_), cur, send, stats, li, lcap);
     cpu::step_finish(stats, P<int64_t>(local_maxts_), bound, ev, f.proc_now, red,
                      P<uint32_t>(flags_), f.idle ? 1 : 0, exchanging_ ? 1 : 0, cur, nb);
+    if (over) red[4] = -(f.n << 1);
   }
   // Watermark valve + pane range + every overflow flag: ONE MIN all-reduce per step.
   if (world_ > 1) comm_->allreduce_min_i64(red, 8, (intptr_t)cur_);
@@ -827,13 +838,18 @@ WindowStep::Back WindowStep::settle(Front& f) {
   for (;;) {
     if (f.ev) host_wait(f.ev);
     host = P<int64_t>(hred_[f.par]);
-    if (host[4])
+    if (host[4] == -1)
       throw std::runtime_error("event timestamp outside the representable pane range "
                                "(more than 2^32 panes ahead of the watermark)");
     if (host[6]) throw std::runtime_error("keyed state table full: a key found no free slot (raise max_keys)");
     if (host[7]) throw std::invalid_argument("key ids -1 and -2 are reserved (the state tables' markers)");
     const int need_rw = -host[5] == 1 ? 2 : -host[5] == 2 ? 3 : rec_w_;
-    if (need_rw > rec_w_) {
+    if (host[4] < -1) {
+      // Some rank's batch exceeds the capacity (word 4 = -(largest such batch << 1)): every
+      // rank regrows to it -- the same bucket geometry everywhere -- and redoes the step.
+      ++m_.bucket_regrows;
+      alloc_buckets(std::max<int64_t>(batch_capacity_, (-host[4]) >> 1), slack_);
+    } else if (need_rw > rec_w_) {
       // A record does not fit the format: wider records from now on.
       rec_w_ = need_rw;
       ++m_.compact_fallbacks;

@@ -596,3 +596,53 @@ def test_exchange_bytes_close_to_payload_at_g8(exchange, combine):
     res = run_loopback(W, rank)
     a2a, payload = sum(r[0] for r in res), sum(r[1] for r in res)
     assert payload > 0 and a2a / payload <= 1.2, (a2a, payload)
+
+
+@pytest.mark.parametrize("dev", _devices())
+@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("exchange", ["records", "partials"])
+@pytest.mark.parametrize("pipeline", [False, "stream"])
+def test_window_batches_outgrow_capacity_unevenly(dev, world, exchange, pipeline):
+    """Ranks' batches pass the (small) batch capacity at different steps: the regrow is agreed
+    through the step's reduced vector (every rank regrows to the largest batch and redoes the
+    step), so the ranks keep one bucket geometry and one collective sequence; a single rank
+    drains its queued state half before its buffers are reallocated. Equal to one process."""
+    _skip_no_gpu(dev)
+    per, nkeys, cap_log2 = _sizes(dev)
+    sizes = [[per // 8 * (1 + ((s + r) % 4) * (r + 1)) for s in range(STEPS)] for r in range(world)]
+
+    def make(comm, pipe=pipeline):
+        return KeyedWindowOperator(size=3000, slide=1000, lateness=1500, agg=K.AGG_SUM_I64,
+                                   device=dev, comm=comm, max_keys=nkeys, batch_capacity=per // 8,
+                                   ooo_bound=500, cap_log2=cap_log2, pipeline=pipe,
+                                   exchange=exchange)
+
+    def batch(rank, step):
+        k, t, v = _batch(dev, rank, step, per, nkeys, late=2000)
+        n = sizes[rank][step]
+        t = t[:n].contiguous()
+        t[-1] = step * 2000 + 2000  # every rank's batch ends at the same event time (see _batch)
+        return k[:n].contiguous(), t, v[:n].contiguous()
+
+    def rank_fn(comm):
+        op = make(comm)
+        out = []
+        for step in range(STEPS):
+            out += op.process(*batch(comm.rank, step))
+        out += op.finish()
+        return _collect(out), op.metrics.num_late_records_dropped
+
+    res = run_loopback(world, rank_fn, device=torch.device(dev))
+    merged, late = {}, 0
+    for d, nl in res:
+        merged.update(d)
+        late += nl
+    ref_op = make(None, pipe=False)
+    out = []
+    for step in range(STEPS):
+        parts = [batch(r, step) for r in range(world)]
+        out += ref_op.process(*[torch.cat([p[i] for p in parts]) for i in range(3)])
+    out += ref_op.finish()
+    assert len(_collect(out)) > 0
+    assert merged == _collect(out)
+    assert late == ref_op.metrics.num_late_records_dropped
