@@ -315,6 +315,7 @@ WindowStep::WindowStep(const WindowStepConfig& c, std::shared_ptr<StepComm> comm
   agg_pack_env_ = env_on("MXS_AGG_PACK", true);
   force_split_ = env_int("MXS_AGG_FORCE_SPLIT", 0);
   refire_stage_budget_ = (int64_t)env_int("MXS_REFIRE_STAGE_MB", 8192) << 20;
+  fused_reset_ = env_on("MXS_STEP_RESET", true);
   evict_pane_sort_ = env_on("MXS_EVICT_PANE_SORT", true);
   if (c.spill) {
     if (dense_bits_ || vec) throw std::invalid_argument("spill needs hashed keys and a plain reduce");
@@ -798,8 +799,9 @@ void WindowStep::launch_front(Front& f) {
     gpu::step_finish(stats, P<int64_t>(local_maxts_), bound, ev, f.proc_now, red,
                      P<uint32_t>(flags_), s, f.idle ? 1 : 0,
                      world_ == 1 ? P<int64_t>(hred_[p]) : nullptr, exchanging_ ? 1 : 0, cur, nb,
-                     P<uint32_t>(cursor_[cn]), P<int64_t>(stats_[cn]));
-    cready_[cn] = true;
+                     fused_reset_ ? P<uint32_t>(cursor_[cn]) : nullptr,
+                     fused_reset_ ? P<int64_t>(stats_[cn]) : nullptr);
+    cready_[cn] = fused_reset_;
     if (over) gpu::fill_u64((uint64_t*)(red + 4), 1, (uint64_t)(-(f.n << 1)), s);
   } else {
     cpu::step_begin(cur, nb, stats);

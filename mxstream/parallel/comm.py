@@ -224,6 +224,7 @@ class LoopbackComm(Comm):
     def barrier(self):
         if self.world > 1:
             self._enter("barrier", None)
+            self.group_obj.wait()  # (every rank checked the kinds before any enters the next)
 
     def broadcast_(self, t, src: int = 0):
         if self.world == 1:
