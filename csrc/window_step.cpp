@@ -316,6 +316,7 @@ WindowStep::WindowStep(const WindowStepConfig& c, std::shared_ptr<StepComm> comm
   force_split_ = env_int("MXS_AGG_FORCE_SPLIT", 0);
   refire_stage_budget_ = (int64_t)env_int("MXS_REFIRE_STAGE_MB", 8192) << 20;
   fused_reset_ = env_on("MXS_STEP_RESET", true);
+  debug_exchange_ = env_on("MXS_DEBUG_EXCHANGE", false);
   evict_pane_sort_ = env_on("MXS_EVICT_PANE_SORT", true);
   if (c.spill) {
     if (dense_bits_ || vec) throw std::invalid_argument("spill needs hashed keys and a plain reduce");
@@ -1078,6 +1079,10 @@ void WindowStep::exchange_records(Back& b, uint32_t* xcap_out) {
     cpu::bucket_repack(P<uint64_t>(send_[b.par]), P<uint32_t>(cursor_[b.cpar]), nbuckets_,
                        (uint32_t)bucket_cap_, xcap, rw, P<uint64_t>(xsend_), nullptr);
   const int64_t words = (int64_t)nbuckets_ * xcap * rw;
+  if (debug_exchange_)
+    std::fprintf(stderr, "[mxs exchange] rank %d step %lld rw %d fill %lld bucket_cap %lld xcap %u "
+                 "nbuckets %d words %lld\n", rank_, (long long)m_.steps, rw, (long long)b.fill,
+                 (long long)bucket_cap_, xcap, nbuckets_, (long long)words);
   if (cfg_.dim > 0) {
     const int64_t need = (int64_t)nbuckets_ * xcap * cfg_.dim;
     if (!send_vec_ || (int64_t)send_vec_->bytes < need * 4) {

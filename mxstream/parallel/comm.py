@@ -180,7 +180,7 @@ class LoopbackComm(Comm):
         if self.world == 1:
             LocalComm.all_to_all(self, out, inp)
             return
-        self._deposit(inp, "all_to_all")
+        self._deposit(inp, f"all_to_all_{inp.numel()}")
         c = inp.numel() // self.world
         for src in range(self.world):
             peer = self._read(src, out)
