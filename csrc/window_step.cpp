@@ -822,7 +822,20 @@ void WindowStep::launch_front(Front& f) {
     if (over) red[4] = -(f.n << 1);
   }
   // Watermark valve + pane range + every overflow flag: ONE MIN all-reduce per step.
+  int64_t dbg_before[8] = {0};
+  if (debug_exchange_ && gpu_) {
+    hip_ok(hipStreamSynchronize(cur_), "sync");
+    hip_ok(hipMemcpy(dbg_before, red, 64, hipMemcpyDeviceToHost), "D2H");
+  }
   if (world_ > 1) comm_->allreduce_min_i64(red, 8, (intptr_t)cur_);
+  if (debug_exchange_ && gpu_) {
+    int64_t after[8];
+    hip_ok(hipStreamSynchronize(cur_), "sync");
+    hip_ok(hipMemcpy(after, red, 64, hipMemcpyDeviceToHost), "D2H");
+    std::fprintf(stderr, "[mxs front] rank %d world %d stream %p red3 %lld -> %lld red2 %lld -> %lld\n",
+                 rank_, world_, (void*)cur_, (long long)dbg_before[3], (long long)after[3],
+                 (long long)dbg_before[2], (long long)after[2]);
+  }
   if (gpu_) {
     if (world_ > 1)
       hip_ok(hipMemcpyAsync(hred_[p]->p, red, kRedWords * 8, hipMemcpyDeviceToHost, cur_), "D2H");

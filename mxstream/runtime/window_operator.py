@@ -49,6 +49,9 @@ I64_MAX = K.I64_MAX
 _DTYPES = {"i8": torch.int64, "i4": torch.int32, "u1": torch.uint8}
 
 
+_SYNC_COLL = __import__("os").environ.get("MXS_DEBUG_SYNC_COLL") == "1"  # (debug A/B)
+
+
 class _StepCommAdapter:
     """The native step's collectives over the rank's comm (torch.distributed: RCCL over xGMI or
     gloo; a LoopbackComm of virtual ranks). Buffers are the step's own memory, wrapped as
@@ -79,6 +82,8 @@ class _StepCommAdapter:
     def allreduce_min(self, ptr: int, n: int, stream: int) -> None:
         with self._stream(stream):
             self.comm.allreduce_min_(self._t(ptr, n, "i8"))
+            if _SYNC_COLL:
+                torch.cuda.synchronize(self.device)
 
     def all_to_all(self, recv: int, send: int, nbytes: int, elem: int, stream: int) -> None:
         code = {8: "i8", 4: "i4"}.get(elem, "u1")
