@@ -49,9 +49,6 @@ I64_MAX = K.I64_MAX
 _DTYPES = {"i8": torch.int64, "i4": torch.int32, "u1": torch.uint8}
 
 
-_SYNC_COLL = __import__("os").environ.get("MXS_DEBUG_SYNC_COLL") == "1"  # (debug A/B)
-
-
 class _StepCommAdapter:
     """The native step's collectives over the rank's comm (torch.distributed: RCCL over xGMI or
     gloo; a LoopbackComm of virtual ranks). Buffers are the step's own memory, wrapped as
@@ -77,13 +74,17 @@ class _StepCommAdapter:
 
         if self.device.type != "cuda":
             return contextlib.nullcontext()
+        if stream == 0:
+            # The step runs on the legacy default stream (torch's default stream hands out
+            # handle 0). ExternalStream(0) is NOT that stream here: torch maps a null handle to
+            # some other stream, and the collective raced the step's kernels (loopback ranks
+            # read each other's vectors before step_finish had written them).
+            return torch.cuda.stream(torch.cuda.default_stream(self.device))
         return torch.cuda.stream(torch.cuda.ExternalStream(stream, device=self.device))
 
     def allreduce_min(self, ptr: int, n: int, stream: int) -> None:
         with self._stream(stream):
             self.comm.allreduce_min_(self._t(ptr, n, "i8"))
-            if _SYNC_COLL:
-                torch.cuda.synchronize(self.device)
 
     def all_to_all(self, recv: int, send: int, nbytes: int, elem: int, stream: int) -> None:
         code = {8: "i8", 4: "i4"}.get(elem, "u1")

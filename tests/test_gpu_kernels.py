@@ -775,3 +775,20 @@ def test_forced_agg_split_equals_default(gpu_device, split, monkeypatch):
         out += op.finish()
         res[n_split] = _results(out)
     assert res[0] == res[split]
+
+
+@pytest.mark.gpu
+def test_step_comm_stream_is_the_steps_stream():
+    """The native step's collectives run on the step's own stream: for the legacy default stream
+    (handle 0) that is torch's default stream, not whatever torch makes of ExternalStream(0)."""
+    from mxstream.parallel.comm import LocalComm
+    from mxstream.runtime.window_operator import _StepCommAdapter
+
+    dev = torch.device("cuda", 0)
+    ad = _StepCommAdapter(LocalComm(), dev)
+    with ad._stream(0):
+        assert torch.cuda.current_stream(dev).cuda_stream == \
+            torch.cuda.default_stream(dev).cuda_stream
+    s = torch.cuda.Stream(dev)
+    with ad._stream(s.cuda_stream):
+        assert torch.cuda.current_stream(dev).cuda_stream == s.cuda_stream
