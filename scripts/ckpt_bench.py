@@ -32,10 +32,11 @@ def main() -> int:
     ap.add_argument("--at", type=int, default=3)
     ap.add_argument("--dir", default="/tmp/mxs_ckpt")
     ap.add_argument("--batch", type=int, default=1 << 24)
+    ap.add_argument("--keys", type=int, default=1_000_000, help="key space (10M: BASELINE scale)")
     a = ap.parse_args()
     dev = torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
     shutil.rmtree(a.dir, ignore_errors=True)
-    b = TumblingWindowBench(TumblingBenchConfig(batch=a.batch), LocalComm(), dev)
+    b = TumblingWindowBench(TumblingBenchConfig(batch=a.batch, keys=a.keys), LocalComm(), dev)
     coord = CheckpointCoordinator(CheckpointStorage(a.dir, job_id="e" * 32), {"window": b.op})
     times, marks = [], {}
     for s in range(a.steps):
@@ -66,7 +67,7 @@ def main() -> int:
         "sync_ckpt_ms": round(sync_st["ms"], 3), "async_freeze_ms": round(async_st["sync_ms"], 3),
         "async_end_to_end_ms": round(async_st["ms"], 3),
         "async_export_ms": round(async_st["export_ms"], 3), "bytes": sync_st["bytes"],
-        "device": str(dev)}))
+        "keys": a.keys, "device": str(dev)}))
     shutil.rmtree(a.dir, ignore_errors=True)
     return 0
 
