@@ -454,7 +454,7 @@ def config4_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 1
 
 def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_000,
             drift: int = 400_000, table_keys: int = 4_000_000, device: str = "cuda",
-            revisit: float = 0.0, promote: bool = True, pipeline: bool = True) -> dict:
+            revisit: float = 0.0, promote: bool = True, pipeline: bool | None = None) -> dict:
     """Session windows (gap 5 s, 30 s allowed lateness) over a drifting active key set: each step
     draws events from `active` consecutive key ids whose window advances by `drift` ids, so keys
     go idle and their sessions close. The HBM slot table holds `table_keys` keys; idle keys whose
@@ -464,8 +464,12 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
     ~10 drift windows ago -- spilled keys whose records take the host-DRAM store path.
     pipeline: the operator's pipelined step (a batch's fire/spill host work overlaps the next
     batch's fold); its alerts come out one step later and their latency counts from the arrival
-    of the batch that fired them; the timed loop ends with the drain (op.flush())."""
+    of the batch that fired them; the timed loop ends with the drain (op.flush()). Default: on
+    without revisits; with revisits the promotions join the spill worker every step and the
+    unpipelined step is faster (profiles/r6_cfg5r.json)."""
     dev = torch.device(device)
+    if pipeline is None:
+        pipeline = revisit == 0
     span, gap = 2_000, 5_000
     per_key_step = batch / active
     # A key is active for active/drift steps; its session spans that time.
@@ -928,7 +932,7 @@ def main(argv=None) -> int:
                     mfma=not a.valu, zipf=a.zipf)
     else:
         r = config5(a.steps, a.warmup, a.batch or (1 << 24), device=a.device, revisit=a.revisit,
-                    promote=not a.host_fold, pipeline=not a.no_pipeline)
+                    promote=not a.host_fold, pipeline=False if a.no_pipeline else None)
     print(json.dumps(r), flush=True)
     return 0
 
