@@ -316,7 +316,7 @@ WindowStep::WindowStep(const WindowStepConfig& c, std::shared_ptr<StepComm> comm
   force_split_ = env_int("MXS_AGG_FORCE_SPLIT", 0);
   refire_stage_budget_ = (int64_t)env_int("MXS_REFIRE_STAGE_MB", 8192) << 20;
   fused_reset_ = env_on("MXS_STEP_RESET", true);
-  fused_finish_ = env_on("MXS_FUSED_FINISH", true);
+  fused_finish_ = env_on("MXS_FUSED_FINISH", false);
   debug_exchange_ = env_on("MXS_DEBUG_EXCHANGE", false);
   evict_pane_sort_ = env_on("MXS_EVICT_PANE_SORT", true);
   if (c.spill) {
