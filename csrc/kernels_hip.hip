@@ -743,108 +743,6 @@ constexpr size_t compact_lds_rb(int cu, int rb) {
 }
 static_assert(compact_lds_rb(8, 8) <= 160 * 1024, "8K-record RecN rounds exceed 160 KiB");
 
-// Step epilogue: fold this batch into the source partition's watermark and build the vector
-// the watermark valve all-reduces (MIN): [-max pane, min pane, wm, -bucket ovf, -pane ovf] plus
-// a copy of the raw stats for the host (red[8..15]). Every thread of the block calls it (block
-// barriers inside); COH: stats and cursors written by other workgroups of the SAME launch (the
-// partition's last workgroup) -- read with agent-scope atomic loads, past the non-coherent
-// caches of this XCD.
-template <bool COH>
-__device__ __forceinline__ void step_finish_body(
-    const int64_t* stats, int64_t* local_maxts, int64_t bound, int32_t event_mode,
-    int64_t proc_now, int64_t* red, const uint32_t* flags, int32_t idle, int64_t* host_red,
-    int32_t fill_word, const uint32_t* cursor, int nb, uint32_t* next_cursor, int64_t* next_stats,
-    uint32_t* fmax /* LDS [64] */) {
-  auto st = [&](int j) -> int64_t {
-    if constexpr (COH)
-      return __hip_atomic_load(stats + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      return stats[j];
-  };
-  // A later step's cursors and stats (distinct buffers): step_begin's work, in this launch.
-  if (next_cursor) {
-    for (int i = threadIdx.x; i < nb; i += blockDim.x) next_cursor[i] = 0;
-    if (threadIdx.x < kStatCount) {
-      const int j = threadIdx.x;
-      next_stats[j] = j == kStatMaxTs ? INT64_MIN : j == kStatMinPane ? INT64_MAX
-                    : j == kStatMaxPane ? INT64_MIN : 0;
-    }
-  }
-  // fill_word: the largest bucket fill, from the cursors (every partition variant fills them)
-  if (fill_word) {
-    if (threadIdx.x < 64) {
-      uint32_t m = 0;
-      for (int i = threadIdx.x; i < nb; i += 64) {
-        uint32_t c;
-        if constexpr (COH)
-          c = __hip_atomic_load(cursor + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-          c = cursor[i];
-        m = c > m ? c : m;
-      }
-      fmax[threadIdx.x] = m;
-    }
-    __syncthreads();
-    for (int s = 32; s > 0; s >>= 1) {
-      if ((int)threadIdx.x < s && fmax[threadIdx.x + s] > fmax[threadIdx.x])
-        fmax[threadIdx.x] = fmax[threadIdx.x + s];
-      __syncthreads();
-    }
-  }
-  // One lane per word of the reduced vector (16 words).
-  const int j = threadIdx.x;
-  if (j >= 16) return;
-  int64_t lm = local_maxts[0];
-  const int64_t bm = st(kStatMaxTs);
-  lm = bm > lm ? bm : lm;
-  if (j == 0) local_maxts[0] = lm;
-  const int64_t wm = event_mode ? (lm == INT64_MIN ? INT64_MIN : lm - bound) : proc_now;
-  const int64_t ovf = st(kStatOverflow);
-  int64_t v;
-  switch (j) {
-    case 0: {
-      const int64_t qmax = st(kStatMaxPane);
-      v = qmax == INT64_MIN ? INT64_MAX : -qmax;
-      break;
-    }
-    case 1: v = st(kStatMinPane); break;
-    case 2: v = idle ? INT64_MAX : wm; break;  // an idle partition has no say in the MIN
-    case 3:
-      v = !fill_word ? -(ovf & 1) : (ovf & 1) ? -((int64_t)1 << 40) : -(int64_t)fmax[0];
-      break;
-    case 4: v = -((ovf >> 1) & 1); break;
-    // Record width a value needs: -2 = 24-byte records, -1 = 16-byte records, 0 = as planned.
-    case 5: v = (ovf & 4) ? -2 : (ovf & 16) ? -1 : 0; break;
-    case 6: v = flags ? -(int64_t)(flags[0] & 1u) : 0; break;  // a key found no slot, sticky
-    case 7: v = -((ovf >> 3) & 1); break;  // the reserved key id ~0 occurred
-    default: v = st(j - 8); break;
-  }
-  red[j] = v;
-  if (host_red) host_red[j] = v;  // vector store into the mapped pinned buffer
-}
-
-// The partition's last workgroup runs the step epilogue (plan.fin): one launch fewer per step.
-// Every workgroup bumps the ticket once after its stats / cursor atomics (acq_rel at agent
-// scope); the one that sees gridDim.x - 1 has every other group's atomics visible.
-__device__ __forceinline__ void partition_fused_finish(const PartPlan& plan,
-                                                       const int64_t* stats,
-                                                       const uint32_t* cursor) {
-  const StepFin& f = plan.fin;
-  if (!f.ticket) return;
-  __shared__ uint32_t last;
-  __shared__ uint32_t fmax[64];
-  __syncthreads();
-  if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(f.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-           gridDim.x - 1;
-  __syncthreads();
-  if (!last) return;
-  step_finish_body<true>(stats, f.local_maxts, f.bound, f.event_mode, f.proc_now, f.red, f.flags,
-                         f.idle, f.host_red, f.fill_word, cursor, f.nb, f.next_cursor,
-                         f.next_stats, fmax);
-  if (threadIdx.x == 0) *f.ticket = 0;  // for the next step's launch
-}
-
 // RB = 16: RecC records; RB = 8: RecN records (one destination, see RecN).
 template <int V, int CU = kCU, bool ONE = false, int RB = 16, bool K32 = false, bool PAIR = false>
 __global__ __launch_bounds__(1024) void partition_compact_kernel(
@@ -1168,7 +1066,6 @@ __global__ __launch_bounds__(1024) void partition_compact_kernel(
     if (!late_idx && nlate) atomicAdd((unsigned long long*)&stats[kStatLate], (unsigned long long)nlate);
     if (flags) atomicOr((unsigned long long*)&stats[kStatOverflow], (unsigned long long)flags);
   }
-  partition_fused_finish(plan, stats, cursor);  // (the last workgroup: the step epilogue)
 }
 
 // Step prologue: zero the bucket cursors and reset the stats block (one launch instead of two
@@ -1184,6 +1081,9 @@ __global__ __launch_bounds__(256) void step_begin_kernel(uint32_t* __restrict__ 
   }
 }
 
+// Step epilogue: fold this batch into the source partition's watermark and build the vector
+// the watermark valve all-reduces (MIN): [-max pane, min pane, wm, -bucket ovf, -pane ovf] plus
+// a copy of the raw stats for the host (red[8..15]).
 __global__ void step_finish_kernel(const int64_t* __restrict__ stats, int64_t* __restrict__ local_maxts,
                                    int64_t bound, int32_t event_mode, int64_t proc_now,
                                    int64_t* __restrict__ red, const uint32_t* __restrict__ flags,
@@ -1191,9 +1091,58 @@ __global__ void step_finish_kernel(const int64_t* __restrict__ stats, int64_t* _
                                    const uint32_t* __restrict__ cursor, int nb,
                                    uint32_t* __restrict__ next_cursor,
                                    int64_t* __restrict__ next_stats) {
+  // A later step's cursors and stats (distinct buffers): step_begin's work, in this launch.
+  if (next_cursor) {
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) next_cursor[i] = 0;
+    if (threadIdx.x < kStatCount) {
+      const int j = threadIdx.x;
+      next_stats[j] = j == kStatMaxTs ? INT64_MIN : j == kStatMinPane ? INT64_MAX
+                    : j == kStatMaxPane ? INT64_MIN : 0;
+    }
+  }
+  // fill_word: the largest bucket fill, from the cursors (every partition variant fills them)
   __shared__ uint32_t fmax[64];
-  step_finish_body<false>(stats, local_maxts, bound, event_mode, proc_now, red, flags, idle,
-                          host_red, fill_word, cursor, nb, next_cursor, next_stats, fmax);
+  if (fill_word) {
+    uint32_t m = 0;
+    for (int i = threadIdx.x; i < nb; i += 64) m = cursor[i] > m ? cursor[i] : m;
+    fmax[threadIdx.x] = m;
+    __syncthreads();
+    for (int s = 32; s > 0; s >>= 1) {
+      if ((int)threadIdx.x < s && fmax[threadIdx.x + s] > fmax[threadIdx.x])
+        fmax[threadIdx.x] = fmax[threadIdx.x + s];
+      __syncthreads();
+    }
+  }
+  // One lane per word of the reduced vector (16 words).
+  const int j = threadIdx.x;
+  if (j >= 16) return;
+  int64_t lm = local_maxts[0];
+  const int64_t bm = stats[kStatMaxTs];
+  lm = bm > lm ? bm : lm;
+  if (j == 0) local_maxts[0] = lm;
+  const int64_t wm = event_mode ? (lm == INT64_MIN ? INT64_MIN : lm - bound) : proc_now;
+  const int64_t ovf = stats[kStatOverflow];
+  int64_t v;
+  switch (j) {
+    case 0: {
+      const int64_t qmax = stats[kStatMaxPane];
+      v = qmax == INT64_MIN ? INT64_MAX : -qmax;
+      break;
+    }
+    case 1: v = stats[kStatMinPane]; break;
+    case 2: v = idle ? INT64_MAX : wm; break;  // an idle partition has no say in the MIN
+    case 3:
+      v = !fill_word ? -(ovf & 1) : (ovf & 1) ? -((int64_t)1 << 40) : -(int64_t)fmax[0];
+      break;
+    case 4: v = -((ovf >> 1) & 1); break;
+    // Record width a value needs: -2 = 24-byte records, -1 = 16-byte records, 0 = as planned.
+    case 5: v = (ovf & 4) ? -2 : (ovf & 16) ? -1 : 0; break;
+    case 6: v = flags ? -(int64_t)(flags[0] & 1u) : 0; break;  // a key found no slot, sticky
+    case 7: v = -((ovf >> 3) & 1); break;  // the reserved key id ~0 occurred
+    default: v = stats[j - 8]; break;
+  }
+  red[j] = v;
+  if (host_red) host_red[j] = v;  // vector store into the mapped pinned buffer
 }
 
 __global__ __launch_bounds__(256) void combine_check_kernel(const uint32_t* __restrict__ flags,
@@ -4677,15 +4626,10 @@ void dispatch_compact(const uint64_t* keys, const int64_t* ts, const uint64_t* v
 #undef MXS_COMPACT
 }
 
-bool partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
-               const int32_t* jhash_tab, int64_t n, const PartPlan& plan_in, const int32_t* kg_dest,
+void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
+               const int32_t* jhash_tab, int64_t n, const PartPlan& plan, const int32_t* kg_dest,
                uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap,
                intptr_t stream) {
-  // The fused step epilogue rides only on the single-launch compact paths (plan_in.fin); every
-  // other path runs with it off and the caller launches step_finish.
-  PartPlan plan = plan_in;
-  plan.fin.ticket = nullptr;
-  const bool fuse = plan_in.fin.ticket != nullptr;
   const int nb = plan.nranks << plan.nsub_log2;
   if (plan.rec_words == 1) {
     // Narrow 8-byte records. Up to 512 buckets the LDS-staged compact kernel; more (e.g. 4096
@@ -4697,12 +4641,12 @@ bool partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
     if (plan.nranks != 1) {
       if (nb > kCMaxNb)
         throw std::invalid_argument("partition: 8-byte records to several ranks need <= 512 buckets");
-      if (n <= 0) return false;
-      dispatch_compact<false, 8>(keys, ts, vals, jhash_tab, n, plan_in, kg_dest, cursor, out, stats,
+      if (n <= 0) return;
+      dispatch_compact<false, 8>(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats,
                                  late_idx, late_cap, stream);
-      return fuse;
+      return;
     }
-    if (n <= 0) return false;
+    if (n <= 0) return;
     if (nb > kCMaxNb && plan.scratch && plan.scratch_cursor && nb <= kCMaxNb * 32) {
       // Two-level: compact staged partition into 512 coarse buckets, then the split kernel.
       int L = 0;
@@ -4718,25 +4662,25 @@ bool partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                          (const void*)plan.scratch, plan.scratch_cursor, pc.bucket_cap, plan, L,
                          cursor, (void*)out, stats);
       HIP_CHECK(hipGetLastError());
-      return false;
+      return;
     }
     if (nb > kCMaxNb) {
       if (plan.key32)
         throw std::invalid_argument("partition: int32 keys need <= 512 buckets");
       partition_variant(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats,
                         late_idx, late_cap, stream, 1);
-      return false;
+      return;
     }
-    dispatch_compact<true, 8>(keys, ts, vals, jhash_tab, n, plan_in, kg_dest, cursor, out, stats,
+    dispatch_compact<true, 8>(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats,
                               late_idx, late_cap, stream);
-    return fuse;
+    return;
   }
   if (plan.rec_words == 2 && nb > kCMaxNb && plan.scratch && plan.scratch_cursor &&
       nb <= kCMaxNb * 32 && (uint64_t)nb * plan.bucket_cap < (1ull << 32)) {
     // Two-level 16-byte partition (session records, more than 512 buckets): the compact staged
     // kernel into 512 coarse buckets (one LDS counting sort per 4096-record round, contiguous
     // run writes), then one workgroup per coarse bucket splits it into its 2^L fine buckets.
-    if (n <= 0) return false;
+    if (n <= 0) return;
     int L = 0;
     while ((nb >> L) > kCMaxNb) ++L;
     PartPlan pc = plan;
@@ -4755,17 +4699,17 @@ bool partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                        (const void*)plan.scratch, plan.scratch_cursor, pc.bucket_cap, plan, L,
                        cursor, (void*)out, stats);
     HIP_CHECK(hipGetLastError());
-    return false;
+    return;
   }
   if (plan.rec_words == 2 && nb <= kCMaxNb && (uint64_t)nb * plan.bucket_cap < (1ull << 32)) {
-    if (n <= 0) return false;
+    if (n <= 0) return;
     if (plan.nranks == 1)
-      dispatch_compact<true, 16>(keys, ts, vals, jhash_tab, n, plan_in, kg_dest, cursor, out,
-                                 stats, late_idx, late_cap, stream);
+      dispatch_compact<true, 16>(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats,
+                                 late_idx, late_cap, stream);
     else
-      dispatch_compact<false, 16>(keys, ts, vals, jhash_tab, n, plan_in, kg_dest, cursor, out,
-                                  stats, late_idx, late_cap, stream);
-    return fuse;
+      dispatch_compact<false, 16>(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats,
+                                  late_idx, late_cap, stream);
+    return;
   }
   if (plan.key32)
     throw std::invalid_argument("partition: int32 keys need compact records (<= 512 buckets)");
@@ -4773,7 +4717,7 @@ bool partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
       nb <= kStageMaxNb * 32 && (uint64_t)nb * plan.bucket_cap < (1ull << 32)) {
     // Two-level 24-byte partition (session / generic records): the write-combined staged
     // kernel into 512 coarse buckets, then the split kernel into the fine buckets.
-    if (n <= 0) return false;
+    if (n <= 0) return;
     int L = 0;
     while ((nb >> L) > kStageMaxNb) ++L;
     PartPlan pc = plan;
@@ -4788,13 +4732,12 @@ bool partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                        (const void*)plan.scratch, plan.scratch_cursor, pc.bucket_cap, plan, L,
                        cursor, (void*)out, stats);
     HIP_CHECK(hipGetLastError());
-    return false;
+    return;
   }
   // Write-combined staged scatter when the LDS carry buffers fit (<= 512 buckets); otherwise
   // the plain scatter. Both stream their inputs with non-temporal loads (kbench A/B).
   partition_variant(keys, ts, vals, jhash_tab, n, plan, kg_dest, cursor, out, stats, late_idx,
                     late_cap, stream, nb <= kStageMaxNb ? 5 : 1);
-  return false;
 }
 
 void partition_variant(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,

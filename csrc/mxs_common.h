@@ -533,20 +533,6 @@ MXS_HD int64_t fast_floor_div_pos(int64_t t_rel, int64_t d, double inv_d) {
 // ---------------------------------------------------------------------------------------------
 // Partition plan (keyBy + window assignment + late check) shared by CPU and GPU.
 // ---------------------------------------------------------------------------------------------
-// The step epilogue (step_finish) run by the partition's last workgroup (GPU, single-launch
-// partitions): ticket == nullptr -> off (the caller launches step_finish itself).
-struct StepFin {
-  uint32_t* ticket;          // workgroups done (reset to 0 by the last one)
-  int64_t* local_maxts;
-  int64_t* red;
-  const uint32_t* flags;
-  int64_t* host_red;
-  uint32_t* next_cursor;     // (with next_stats) the next step's set, reset here
-  int64_t* next_stats;
-  int64_t bound, proc_now;
-  int32_t event_mode, idle, fill_word, nb;
-};
-
 struct PartPlan {
   int32_t max_parallelism;   // Flink maxParallelism (128 by default)
   int32_t nsub_log2;         // sub-tables per rank = 1 << nsub_log2
@@ -571,7 +557,6 @@ struct PartPlan {
   // then a split kernel per coarse bucket into its 2^L fine buckets. 0: the plain scatter.
   uint64_t* scratch;
   uint32_t* scratch_cursor;  // [512] coarse fills
-  StepFin fin;               // GPU: fused step epilogue (fin.ticket == nullptr: off)
 };
 
 // Sub-table of a key: a 32-bit multiplicative hash of both key halves (3 32-bit multiplies).

@@ -213,9 +213,7 @@ void gen_events(uint64_t* keys, int64_t* ts, uint64_t* vals, int64_t n, uint64_t
                 uint64_t stream_id, uint64_t idx0, uint64_t nkeys, int64_t ts_base,
                 int64_t ts_span, int64_t disorder, int64_t val_lo, int64_t val_span,
                 int32_t val_f64, double zipf_s, intptr_t stream, uint64_t key_base = 0);
-// Returns true when plan.fin ran inside the partition (single-launch paths only); false: the
-// caller launches step_finish (plan.fin ignored, nothing launched for n <= 0).
-bool partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
+void partition(const uint64_t* keys, const int64_t* ts, const uint64_t* vals,
                const int32_t* jhash_tab, int64_t n, const PartPlan& plan, const int32_t* kg_dest,
                uint32_t* cursor, Rec* out, int64_t* stats, uint32_t* late_idx, uint32_t late_cap,
                intptr_t stream);

@@ -316,7 +316,6 @@ WindowStep::WindowStep(const WindowStepConfig& c, std::shared_ptr<StepComm> comm
   force_split_ = env_int("MXS_AGG_FORCE_SPLIT", 0);
   refire_stage_budget_ = (int64_t)env_int("MXS_REFIRE_STAGE_MB", 8192) << 20;
   fused_reset_ = env_on("MXS_STEP_RESET", true);
-  fused_finish_ = env_on("MXS_FUSED_FINISH", false);
   debug_exchange_ = env_on("MXS_DEBUG_EXCHANGE", false);
   evict_pane_sort_ = env_on("MXS_EVICT_PANE_SORT", true);
   if (c.spill) {
@@ -795,28 +794,14 @@ void WindowStep::launch_front(Front& f) {
     const intptr_t s = (intptr_t)cur_;
     if (!cready_[cp]) gpu::step_begin(cur, nb, stats, s);  // (else reset by the last step_finish)
     cready_[cp] = false;  // a redo of this step resets them again
-    int64_t* hr = world_ == 1 ? P<int64_t>(hred_[p]) : nullptr;
-    uint32_t* ncur = fused_reset_ ? P<uint32_t>(cursor_[cn]) : nullptr;
-    int64_t* nst = fused_reset_ ? P<int64_t>(stats_[cn]) : nullptr;
-    // The step epilogue in the partition's last workgroup (single-launch partitions): no
-    // step_finish launch. MXS_FUSED_FINISH=0: the separate launch (A/B).
-    StepFin& fin = pplan_.fin;
-    std::memset(&fin, 0, sizeof(fin));
-    if (fused_finish_) {
-      if (!fin_ticket_) fin_ticket_ = mem_alloc(16, 1);
-      fin = StepFin{P<uint32_t>(fin_ticket_), P<int64_t>(local_maxts_), red, P<uint32_t>(flags_),
-                    hr, ncur, nst, bound, f.proc_now, ev, f.idle ? 1 : 0, exchanging_ ? 1 : 0,
-                    nb};
-    }
-    bool fused = false;
     if (f.n && !over)
-      fused = gpu::partition((const uint64_t*)keys_in, f.ts, (const uint64_t*)f.vals, cfg_.jhash,
-                             f.n, pplan_, P<int32_t>(kg_dest_), cur, send, stats, li, lcap, s);
-    fin.ticket = nullptr;
-    if (!fused)
-      gpu::step_finish(stats, P<int64_t>(local_maxts_), bound, ev, f.proc_now, red,
-                       P<uint32_t>(flags_), s, f.idle ? 1 : 0, hr, exchanging_ ? 1 : 0, cur, nb,
-                       ncur, nst);
+      gpu::partition((const uint64_t*)keys_in, f.ts, (const uint64_t*)f.vals, cfg_.jhash, f.n,
+                     pplan_, P<int32_t>(kg_dest_), cur, send, stats, li, lcap, s);
+    gpu::step_finish(stats, P<int64_t>(local_maxts_), bound, ev, f.proc_now, red,
+                     P<uint32_t>(flags_), s, f.idle ? 1 : 0,
+                     world_ == 1 ? P<int64_t>(hred_[p]) : nullptr, exchanging_ ? 1 : 0, cur, nb,
+                     fused_reset_ ? P<uint32_t>(cursor_[cn]) : nullptr,
+                     fused_reset_ ? P<int64_t>(stats_[cn]) : nullptr);
     cready_[cn] = fused_reset_;
     if (over) gpu::fill_u64((uint64_t*)(red + 4), 1, (uint64_t)(-(f.n << 1)), s);
   } else {

@@ -375,8 +375,6 @@ class WindowStep {
   // (MXS_REFIRE_STAGE_MB, default 8 GiB of the 288 GB HBM).
   int64_t refire_stage_budget_ = (int64_t)8192 << 20;
   bool fused_reset_ = true;  // MXS_STEP_RESET=0: a step_begin launch per step (A/B)
-  bool fused_finish_ = false;  // MXS_FUSED_FINISH=1: the step epilogue in the partition
-  Buf fin_ticket_;            // the partition's workgroup ticket (StepFin)
   bool debug_exchange_ = false;  // MXS_DEBUG_EXCHANGE=1: one stderr line per records exchange
   bool cready_[3] = {false, false, false};
   Buf recv_, recv_counts_, scratch_, scratch_cursor_, comb_send_, comb_recv_, comb_counts_;
