@@ -1160,14 +1160,19 @@ class SessionCore {
     const uintptr_t y = reinterpret_cast<uintptr_t>(loc_ + b);
     (void)::madvise(reinterpret_cast<void*>(x), y - x, 23 /* MADV_POPULATE_WRITE */);
   }
-  // Entries up to `need`: when the mapped range ends less than kPopAhead / 2 above it, one
-  // background thread maps the next kPopAhead entries (one at a time; joined before the next).
-  static constexpr size_t kPopAhead = (size_t)1 << 22;  // 32 MB of entries
+  // Entries up to `need`: when the mapped range ends less than pop_ahead_ / 2 above it, one
+  // background thread maps the next pop_ahead_ entries (one at a time; joined before the next).
+  // (MXS_INDEX_AHEAD_MB: the read-ahead in MB of entries, default 32)
+  const size_t pop_ahead_ = (size_t)std::max(1, env_int_("MXS_INDEX_AHEAD_MB", 32)) << 17;
+  static int env_int_(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e && *e ? std::atoi(e) : dflt;
+  }
   void populate_ahead(size_t need) {
     const size_t ph = pop_hi_.load();
-    if (need + kPopAhead / 2 <= ph || ph >= kMaxLocSpan || pop_busy_.load()) return;
+    if (need + pop_ahead_ / 2 <= ph || ph >= kMaxLocSpan || pop_busy_.load()) return;
     if (pop_thread_.joinable()) pop_thread_.join();
-    const size_t end = std::min(kMaxLocSpan, ph + kPopAhead);
+    const size_t end = std::min(kMaxLocSpan, ph + pop_ahead_);
     pop_busy_.store(true);
     pop_thread_ = std::thread([this, ph, end] {
       populate(ph, end);
