@@ -1203,23 +1203,51 @@ class KeyedSessionOperator:
             self._apply_spill_results(self.store.spill_poll())
 
     def _keys_to_device(self, keys: np.ndarray) -> torch.Tensor:
-        """Host key ids on the device through a reused page-locked buffer and an asynchronous
-        copy on the current stream (a pageable copy of the ~3 MB released per expired chunk
-        cost ~0.9 ms per step at steady state). Valid for kernels enqueued on the same stream."""
+        """Host key ids on the device for a kernel the caller enqueues next on the current stream
+        (a pageable copy of the ~3 MB released per expired chunk cost ~0.9 ms per step).
+
+        A ring of four pinned / device buffer pairs; the copy runs on a side stream and the
+        current stream waits for it. The host reuses a pinned buffer after ITS copy (side stream,
+        not queued behind the step's kernels) -- copying on the current stream made the second
+        call of a pipelined step wait for the fold queued ahead of it. A device buffer is
+        rewritten only after the current stream's use of it (an event recorded at the next call,
+        once the caller's kernel is enqueued)."""
         n = len(keys)
-        buf = getattr(self, "_kh_buf", None)
-        if buf is None or buf[0].numel() < n:
-            cap = max(1 << 16, 1 << (n - 1).bit_length())
-            buf = self._kh_buf = (torch.empty(cap, dtype=torch.int64, pin_memory=True),
-                                  torch.empty(cap, dtype=torch.int64, device=self.device),
-                                  torch.cuda.Event())
-            buf[2].record(torch.cuda.current_stream(self.device))
-        host, dev, ev = buf
-        ev.synchronize()  # the previous copy has left the pinned buffer
-        host[:n].numpy()[:] = keys
-        dev[:n].copy_(host[:n], non_blocking=True)
-        ev.record(torch.cuda.current_stream(self.device))
-        return dev[:n]
+        dev = self.device
+        ring = getattr(self, "_kh_ring", None)
+        if ring is None:
+            ring = self._kh_ring = [{"cap": 0, "host": None, "dev": None, "copied": None,
+                                     "used": None} for _ in range(4)]
+            self._kh_i = 0
+            self._kh_last = None
+            self._kh_side = torch.cuda.Stream(dev)
+        cur = torch.cuda.current_stream(dev)
+        if self._kh_last is not None:  # the previous call's kernel is enqueued by now
+            ev = torch.cuda.Event()
+            ev.record(cur)
+            self._kh_last["used"] = ev
+        slot = ring[self._kh_i]
+        self._kh_i = (self._kh_i + 1) % len(ring)
+        if slot["cap"] < n:
+            cap = max(1 << 16, 1 << (max(n, 1) - 1).bit_length())
+            if slot["copied"] is not None:
+                slot["copied"].synchronize()
+            slot.update(cap=cap, host=torch.empty(cap, dtype=torch.int64, pin_memory=True),
+                        dev=torch.empty(cap, dtype=torch.int64, device=dev), copied=None)
+        elif slot["copied"] is not None:
+            slot["copied"].synchronize()  # its last copy has left the pinned buffer
+        slot["host"][:n].numpy()[:] = keys
+        side = self._kh_side
+        if slot["used"] is not None:
+            side.wait_event(slot["used"])  # the device buffer's last reader is done
+        with torch.cuda.stream(side):
+            slot["dev"][:n].copy_(slot["host"][:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        slot["copied"] = ev
+        cur.wait_event(ev)
+        self._kh_last = slot
+        return slot["dev"][:n]
 
     def _apply_spill_results(self, res: list) -> None:
         for r in res:
