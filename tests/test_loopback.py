@@ -646,3 +646,34 @@ def test_window_batches_outgrow_capacity_unevenly(dev, world, exchange, pipeline
     assert len(_collect(out)) > 0
     assert merged == _collect(out)
     assert late == ref_op.metrics.num_late_records_dropped
+
+
+def test_loopback_collective_mismatch_is_reported():
+    """A rank that enters a different collective than its peers fails every rank with a message
+    naming what each rank entered (instead of pairing unrelated buffers or hanging)."""
+    def fn(comm):
+        t = torch.zeros(4, dtype=torch.int64)
+        if comm.rank == 0:
+            comm.allreduce_min_(t)
+        else:
+            comm.all_to_all(torch.empty_like(t), t)
+
+    with pytest.raises(RuntimeError, match="loopback collective mismatch"):
+        run_loopback(2, fn, timeout_s=30)
+
+
+def test_loopback_collectives_match_in_order():
+    """Equal collective sequences pass the check (including barriers and object gathers)."""
+    def fn(comm):
+        t = torch.full((4,), comm.rank, dtype=torch.int64)
+        comm.allreduce_min_(t)
+        comm.barrier()
+        got = comm.all_gather_object(comm.rank)
+        inp = torch.full((4,), comm.rank, dtype=torch.int64)
+        out = torch.empty_like(inp)
+        comm.all_to_all(out, inp)
+        return int(t[0]), got, out.tolist()
+
+    res = run_loopback(2, fn, timeout_s=30)
+    assert res[0][0] == res[1][0] == 0 and res[0][1] == [0, 1]
+    assert res[1][2] == [0, 0, 1, 1]
