@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -226,6 +227,7 @@ class SessionCore {
     ColdChunk ch;
     std::vector<uint8_t> isc;  // per row: 1 = goes to the cold chunk
     int64_t nc = 0, emax = INT64_MIN;
+    double t_populate = 0;  // s: index_cold's synchronous page population (spill worker timers)
     bool indexed = false;  // index_cold() ran (the spill worker runs it outside the lock)
   };
   void insert(const int64_t* K, const int64_t* S, const int64_t* E, const int64_t* A,
@@ -444,6 +446,7 @@ class SessionCore {
     // for ids above the mapped range (drifting key spaces), ahead of need on a background
     // thread, so the worker's index phase finds its pages mapped.
     if (env_flag("MXS_INDEX_POPULATE", true)) {
+      const auto tp0 = std::chrono::steady_clock::now();
       const size_t lo = ch.kmin - loc_base_, hi = ch.kmax - loc_base_ + 1;
       if (lo < pop_lo_) {
         populate(lo, pop_lo_);
@@ -457,6 +460,7 @@ class SessionCore {
         }
       }
       populate_ahead(hi);
+      p.t_populate += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp0).count();
     }
     // Row blocks on the pool, two passes of relaxed (plain) stores -- atomic read-modify-writes
     // serialize every cache miss, key-range tasks re-read the key column per task:

@@ -99,6 +99,9 @@ struct SpillJob {
 struct SpillDone {
   uint64_t id = 0;
   int64_t nr = 0, ne = 0, nk = 0;
+  int64_t n_hot = 0;       // rows that went to the hot map (not fired-unmodified or key hot)
+  int64_t hot_keys = 0;    // hot map size after the insert (0: the all-cold fast path applies)
+  double t_populate = 0;   // s: of t_index, the synchronous index page population
   std::vector<int64_t> released;
   double t_wait = 0, t_hot = 0, t_build = 0, t_index = 0, t_publish = 0, t_expire = 0;  // s
   std::exception_ptr err;
@@ -418,6 +421,9 @@ class SessionStore {
       r["t_index"] = d.t_index;
       r["t_publish"] = d.t_publish;
       r["t_expire"] = d.t_expire;
+      r["n_hot"] = d.n_hot;
+      r["t_populate"] = d.t_populate;
+      r["hot_keys"] = d.hot_keys;
       out.append(r);
     }
     if (err) std::rethrow_exception(err);
@@ -470,6 +476,10 @@ class SessionStore {
           if (nr) {
             if (one) one->insert_hot(col[0], col[1], col[2], col[3], col[4], col[5], nr, true, plan);
             else c_.insert(col[0], col[1], col[2], col[3], col[4], col[5], nr, true);
+            if (one) {
+              d.n_hot = nr - plan.nc;
+              d.hot_keys = one->hot_free() ? 0 : 1;
+            }
           }
         }
         {
@@ -518,6 +528,7 @@ class SessionStore {
         d.t_index = sec(t2b, t3);
         d.t_publish = sec(t3, t4);
         d.t_expire = sec(t4, t5);
+        d.t_populate = plan.t_populate;
       } catch (...) {
         d.err = std::current_exception();
       }

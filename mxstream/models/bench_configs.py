@@ -552,6 +552,9 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
                                        for k, v in sorted(op.phase_s.items())},
             "spill_slab_allocs": op.metrics.extra.get("spill_slab_allocs", 0),
             "promote_bad_keys": op.metrics.extra.get("promote_bad_keys", 0),
+            "spill_hot_rows": op.metrics.extra.get("spill_hot_rows", 0),
+            "spill_jobs_with_hot_map": op.metrics.extra.get("spill_jobs_with_hot_map", 0),
+            "spill_jobs": op.metrics.extra.get("spill_jobs", 0),
             "store_index": op.store.index_stats() if hasattr(op.store, "index_stats") else None}
 
 

@@ -1264,6 +1264,10 @@ class KeyedSessionOperator:
             self.metrics.spilled_keys += r["nk"]
             for k in ("wait", "hot", "build", "index", "publish", "expire"):  # worker phase times
                 self.phase_s[f"spill.worker.{k}"] += r[f"t_{k}"]
+            self.phase_s["spill.worker.index.populate"] += r["t_populate"]
+            ex = self.metrics.extra  # rows the worker could not take the all-cold path for
+            ex["spill_hot_rows"] = ex.get("spill_hot_rows", 0) + r["n_hot"]
+            ex["spill_jobs_with_hot_map"] = ex.get("spill_jobs_with_hot_map", 0) + r["hot_keys"]
 
     def _ensure_spill_capacity(self, extra: int) -> None:
         """Keep the device spill set (live keys + tombstones) at most half full after `extra`
