@@ -228,6 +228,8 @@ class SessionCore {
     std::vector<uint8_t> isc;  // per row: 1 = goes to the cold chunk
     int64_t nc = 0, emax = INT64_MIN;
     double t_populate = 0;  // s: index_cold's synchronous page population (spill worker timers)
+    bool emax_pending = false;  // all-cold fast path: emax (and nkeys) computed by the build
+    int64_t nkeys = -1;         // distinct keys of the rows (runs of equal keys), from the build
     bool indexed = false;  // index_cold() ran (the spill worker runs it outside the lock)
   };
   void insert(const int64_t* K, const int64_t* S, const int64_t* E, const int64_t* A,
@@ -240,8 +242,10 @@ class SessionCore {
       publish_cold(p);
     }
   }
+  // all_fired: the caller checked (outside the store lock) that every row has F == 1.
   void insert_hot(const int64_t* K, const int64_t* S, const int64_t* E, const int64_t* A,
-                  const int64_t* C, const int64_t* F, int64_t n, bool cold, ColdPlan& p) {
+                  const int64_t* C, const int64_t* F, int64_t n, bool cold, ColdPlan& p,
+                  bool all_fired = false) {
     refresh_hot_filter();
     if (cold && !spare_.empty()) {
       // A dropped chunk's columns: capacity whose pages are already mapped. Fresh columns of a
@@ -250,6 +254,13 @@ class SessionCore {
       spare_.pop_back();
     }
     const bool no_hot = m_.empty();
+    if (cold && no_hot && all_fired) {
+      // The common eviction (config 5) with the rows pre-checked: every row is cold. O(1)
+      // under the store lock -- the build (outside it, on the pool) takes emax and the keys.
+      p.nc = n;
+      p.emax_pending = true;
+      return;
+    }
     // Row i goes to the cold chunk iff it fired unmodified (F == 1) and its key is not hot --
     // hot already at the call, or made hot by an EARLIER row of this call (the serial rule).
     // (key, first row) of the rows that turn keys hot, sorted by key, behind a bit filter: a
@@ -337,6 +348,7 @@ class SessionCore {
     ch.cnt.resize(n);
     const int nb = (int)((n + kBlk - 1) / kBlk);
     std::vector<uint64_t> lo((size_t)nb, ~0ull), hi((size_t)nb, 0);
+    std::vector<int64_t> em((size_t)nb, INT64_MIN), runs((size_t)nb, 0);
     pool_->run(nb, [&](int b) {
       const int64_t a = (int64_t)b * kBlk, m = std::min(n, a + kBlk) - a;
       std::memcpy(ch.key.data() + a, K + a, (size_t)m * 8);
@@ -344,24 +356,43 @@ class SessionCore {
       std::memcpy(ch.end.data() + a, E + a, (size_t)m * 8);
       std::memcpy(ch.acc.data() + a, A + a, (size_t)m * 8);
       uint64_t l = ~0ull, h = 0;
+      int64_t e = INT64_MIN, r = 0;
       for (int64_t i = a; i < a + m; ++i) {
         ch.cnt[i] = (uint32_t)C[i];
         const uint64_t k = (uint64_t)K[i];
         l = k < l ? k : l;
         h = k > h ? k : h;
+        e = E[i] > e ? E[i] : e;
+        r += i == 0 || K[i] != K[i - 1];  // a new run of equal keys starts here
       }
       lo[(size_t)b] = l;
       hi[(size_t)b] = h;
+      em[(size_t)b] = e;
+      runs[(size_t)b] = r;
     });
+    int64_t e = INT64_MIN, r = 0;
     for (int b = 0; b < nb; ++b) {
       ch.kmin = std::min(ch.kmin, lo[(size_t)b]);
       ch.kmax = std::max(ch.kmax, hi[(size_t)b]);
+      e = std::max(e, em[(size_t)b]);
+      r += runs[(size_t)b];
     }
+    if (p.emax_pending) {
+      p.emax = e;
+      p.emax_pending = false;
+    }
+    p.nkeys = r;
   }
   // The classified cold rows into p.ch (touches no store state: runs outside the store lock).
   static void build_cold(const int64_t* K, const int64_t* S, const int64_t* E, const int64_t* A,
                          const int64_t* C, int64_t n, ColdPlan& p) {
     ColdChunk& ch = p.ch;
+    if (p.emax_pending) {  // (all-cold fast path: every row is cold)
+      int64_t e = INT64_MIN;
+      for (int64_t i = 0; i < n; ++i) e = E[i] > e ? E[i] : e;
+      p.emax = e;
+      p.emax_pending = false;
+    }
     const int64_t nc = p.nc;
     ch.key.resize(nc);
     ch.start.resize(nc);

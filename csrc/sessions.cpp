@@ -466,15 +466,17 @@ class SessionStore {
           nr = (int64_t)tmp[0].size();
         }
         d.nr = nr;
-        int64_t nk = nr ? 1 : 0;
-        for (int64_t i = 1; i < nr; ++i) nk += col[0][i] != col[0][i - 1];
-        d.nk = nk;
         sess::SessionCore::ColdPlan plan;
         sess::SessionCore* one = c_.single();
+        // Outside the store lock: every row fired unmodified? (then the insert under the lock
+        // is O(1) and the build takes emax and the key count on the pool)
+        bool all_fired = one != nullptr;
+        for (int64_t i = 0; all_fired && i < nr; ++i) all_fired = col[5][i] == 1;
         {
           std::lock_guard<std::mutex> g(mu_);
           if (nr) {
-            if (one) one->insert_hot(col[0], col[1], col[2], col[3], col[4], col[5], nr, true, plan);
+            if (one) one->insert_hot(col[0], col[1], col[2], col[3], col[4], col[5], nr, true, plan,
+                                     all_fired);
             else c_.insert(col[0], col[1], col[2], col[3], col[4], col[5], nr, true);
             if (one) {
               d.n_hot = nr - plan.nc;
@@ -491,6 +493,13 @@ class SessionStore {
         const auto t2 = clk::now();
         if (one && nr) one->build_cold_parallel(col[0], col[1], col[2], col[3], col[4], nr, plan);
         const auto t2b = clk::now();
+        if (plan.nkeys >= 0) {
+          d.nk = plan.nkeys;
+        } else {
+          int64_t nk = nr ? 1 : 0;
+          for (int64_t i = 1; i < nr; ++i) nk += col[0][i] != col[0][i - 1];
+          d.nk = nk;
+        }
         // The cold-row index entries of the new chunk, still outside the lock: every other user
         // of the index (extract, promote, expiry) joins this worker first.
         if (one && nr) one->index_cold(plan);
