@@ -73,6 +73,10 @@ _REC16 = __import__("os").environ.get("MXS_SESSION_REC16", "1") != "0"
 # Promotion of revisited spilled keys through promote rows (SessionStore.extract_rows_into +
 # session_promote_rows); "0": the previous extract_packed path (A/B).
 _PROMOTE_ROWS = __import__("os").environ.get("MXS_PROMOTE_ROWS", "1") != "0"
+# Slot-table rehash trigger (drop tombstones): occupied fraction above _REHASH_OCC with at least
+# _REHASH_TOMBS of the slots tombstoned (MXS_SESSION_REHASH="occ,tombs").
+_REHASH_OCC, _REHASH_TOMBS = (float(x) for x in
+                              __import__("os").environ.get("MXS_SESSION_REHASH", "0.8,0.08").split(","))
 
 
 def _next_pow2(x: int) -> int:
@@ -1356,7 +1360,8 @@ class KeyedSessionOperator:
         # LDS probes of the fold (a missing key scans to the first empty slot) grow with the
         # occupied fraction, not with the live one.
         def due(live, occupied):
-            return occupied > 0.8 * self.nslots and occupied - live > 0.08 * self.nslots
+            return (occupied > _REHASH_OCC * self.nslots
+                    and occupied - live > _REHASH_TOMBS * self.nslots)
 
         self._poll_spill()
         t_occ = time.perf_counter()
