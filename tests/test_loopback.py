@@ -239,17 +239,20 @@ def _collect_sessions(rows):
 
 @pytest.mark.parametrize("dev", _devices())
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_sessions_invariant_to_world(dev, world):
+@pytest.mark.parametrize("pipeline", [False, True])
+def test_sessions_invariant_to_world(dev, world, pipeline):
+    """pipeline=True (GPU): the pipelined session step at G ranks (its fires come one call
+    later; the union over ranks and calls is the same)."""
     from mxstream.runtime.session_operator import KeyedSessionOperator
 
     _skip_no_gpu(dev)
     per = 3000 if dev == "cpu" else 60_000
     nkeys = 5000 if dev == "cpu" else 40_000
 
-    def make(comm, cap):
+    def make(comm, cap, pipe=pipeline):
         return KeyedSessionOperator(gap=40, lateness=300, agg=K.AGG_SUM_I64, device=dev,
                                     comm=comm, max_keys=nkeys, batch_capacity=cap, ooo_bound=500,
-                                    cap_log2=8 if dev == "cpu" else None)
+                                    cap_log2=8 if dev == "cpu" else None, pipeline=pipe)
 
     def rank_fn(comm):
         op = make(comm, per)
@@ -264,7 +267,7 @@ def test_sessions_invariant_to_world(dev, world):
         assert not (set(d) & set(merged)), "a session fired on two ranks"
         merged.update(d)
         late += nl
-    op = make(None, per * world)
+    op = make(None, per * world, pipe=False)
     ref = {}
     for step in range(STEPS):
         ref.update(_collect_sessions(op.process(*_concat(dev, world, step, per, nkeys))))
