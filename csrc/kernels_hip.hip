@@ -2205,7 +2205,7 @@ constexpr int kRefireThreads = 256;
 
 __global__ __launch_bounds__(kRefireThreads) void window_refire_multi_kernel(
     const uint64_t* __restrict__ keys_g, const uint64_t* __restrict__ acc_g,
-    const uint32_t* __restrict__ cnt_g, const uint8_t* __restrict__ dirty_g, FirePlan p,
+    const uint32_t* __restrict__ cnt_g, uint8_t* __restrict__ dirty_g, FirePlan p,
     FireWinPack pack, int64_t u0, int nu, uint32_t dmask, FireStage st) {
   extern __shared__ __attribute__((aligned(16))) double fsm[];
   constexpr int T = kRefireThreads;
@@ -2304,6 +2304,14 @@ __global__ __launch_bounds__(kRefireThreads) void window_refire_multi_kernel(
           if (st.cnt) st.cnt[o + q] = cnt;
         }
       }
+    }
+    if (p.clear_mark && live) {
+      // dirty_clear's work for this slot, by the thread that just read its dirty bytes: the
+      // panes that held them (dmask panes with a count; dirty bytes are set only with data)
+#pragma unroll
+      for (int q = 0; q < kRefireP; ++q)
+        if (dirt >> q & 1u) dirty_g[(size_t)((u0 + q) & (p.ring - 1)) * nslots + s] = 0;
+      p.clear_mark[s] = 0u;
     }
   }
 }
@@ -5103,7 +5111,8 @@ bool window_refire_many(const uint64_t* keys_g, const uint64_t* acc_g, const uin
   // The list length stays on the device: a grid for the list's capacity (nslots), rounds of
   // 256 slots per workgroup; workgroups past the list end exit at once.
   hipLaunchKernelGGL(window_refire_multi_kernel, dim3(grid_for(base.nslots, kRefireThreads * 4, 2048)),
-                     dim3(kRefireThreads), lds, s, keys_g, acc_g, cnt_g, dirty_g, base, pack, u0,
+                     dim3(kRefireThreads), lds, s, keys_g, acc_g, cnt_g,
+                     const_cast<uint8_t*>(dirty_g), base, pack, u0,
                      (int)(u1 - u0), dmask, st);
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(fire_pack_kernel, dim3(grid_for(base.nslots / k, 256 * 4, 64), k), dim3(256),

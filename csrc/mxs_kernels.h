@@ -81,6 +81,9 @@ struct FirePlan {
   // else: keys written as uint32 (dense ids) into the key column's first 4*n bytes; a null
   // out_raw / out_cnt column is not written.
   int32_t key32;
+  // Fused re-firing only: clear each listed slot's dirty bytes and touched mark once its
+  // windows are evaluated (dirty_clear's work, same thread; non-null = on).
+  uint32_t* clear_mark;
 };
 
 // One window of a batched firing (window_fire_many): the per-window fields of FirePlan.

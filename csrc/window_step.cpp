@@ -1237,8 +1237,11 @@ void WindowStep::fire_ready(int64_t wm, int64_t seq) {
 }
 
 void WindowStep::refire(int64_t pmin, int64_t pmax, int64_t old_wm, int64_t seq) {
+  refire_cleared_ = false;
   fire_list(ctl_.refire_windows(pmin, pmax, old_wm), true, seq);
-  if (dlist_) {
+  if (dlist_ && refire_cleared_) {
+    memset_async(dlist_n_, 0, 0, 4);  // the fused re-firing cleared the slots itself
+  } else if (dlist_) {
     if (gpu_)
       gpu::dirty_clear(P<uint32_t>(dlist_), P<uint32_t>(dlist_n_), (uint32_t)nslots_, (int)ring_,
                        nslots_, P<uint8_t>(dirty_g_), P<uint32_t>(slot_mark_), pmin,
@@ -1609,7 +1612,9 @@ bool WindowStep::refire_fused(const std::vector<int64_t>& starts, const std::vec
   base.key32 = kv ? 1 : 0;
   base.list = P<uint32_t>(dlist_);
   base.list_n = P<uint32_t>(dlist_n_);
-  FireStage st{P<uint64_t>(rout_[0]), P<double>(rout_[1]), P<uint64_t>(rout_[2]),
+  // The re-firing clears the listed slots' dirty bytes and marks itself (no dirty_clear launch;
+  // the fused path runs only without the local-global delta ring, which dirty_clear also resets)
+  base.clear_mark = dacc_g_ ? nullptr : P<uint32_t>(slot_mark_);
                P<uint32_t>(rout_[3]), P<uint32_t>(rout_[8]), (uint32_t)region};
   uint32_t* bnd = P<uint32_t>(rout_[9]);
   memset_async(flags_, 0, 12, 4);
@@ -1619,6 +1624,7 @@ bool WindowStep::refire_fused(const std::vector<int64_t>& starts, const std::vec
       P<uint32_t>(rout_[7]), bnd + 32, bnd, P<uint32_t>(flags_) + 3, (intptr_t)cur_, dirty_lo_,
       dirty_mask_);
   if (!ok) return false;
+  refire_cleared_ = base.clear_mark != nullptr;
   FireBatch fb;
   fb.wins = starts;
   fb.kv = kv;

@@ -371,6 +371,7 @@ class WindowStep {
   // ahead, or waited for through ev_consumed_) -- the next step launches no step_begin.
   Buf cursor_[3], stats_[3];
   int cpar_ = 0;
+  bool refire_cleared_ = false;  // the last refire()'s fused kernel cleared its listed slots
   // Device bytes the fused re-firing's staging may take to skip its list-length read
   // (MXS_REFIRE_STAGE_MB, default 8 GiB of the 288 GB HBM).
   int64_t refire_stage_budget_ = (int64_t)8192 << 20;
