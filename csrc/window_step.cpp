@@ -1615,6 +1615,7 @@ bool WindowStep::refire_fused(const std::vector<int64_t>& starts, const std::vec
   // The re-firing clears the listed slots' dirty bytes and marks itself (no dirty_clear launch;
   // the fused path runs only without the local-global delta ring, which dirty_clear also resets)
   base.clear_mark = dacc_g_ ? nullptr : P<uint32_t>(slot_mark_);
+  FireStage st{P<uint64_t>(rout_[0]), P<double>(rout_[1]), P<uint64_t>(rout_[2]),
                P<uint32_t>(rout_[3]), P<uint32_t>(rout_[8]), (uint32_t)region};
   uint32_t* bnd = P<uint32_t>(rout_[9]);
   memset_async(flags_, 0, 12, 4);
