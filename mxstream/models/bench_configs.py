@@ -466,7 +466,8 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
     batch's fold); its alerts come out one step later and their latency counts from the arrival
     of the batch that fired them; the timed loop ends with the drain (op.flush()). Default: on
     without revisits; with revisits the promotions join the spill worker every step and the
-    unpipelined step is faster (profiles/r6_cfg5r.json)."""
+    unpipelined step is faster (1.86 G against 1.02 G: profiles/r6_cfg5r_unpipelined.json,
+    profiles/r6_cfg5r.json)."""
     dev = torch.device(device)
     if pipeline is None:
         pipeline = revisit == 0
