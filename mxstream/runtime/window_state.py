@@ -18,6 +18,20 @@ I64_MIN = K.I64_MIN
 I64_MAX = K.I64_MAX
 
 
+def _to_host(ts: list[torch.Tensor]) -> list[np.ndarray]:
+    """Device columns -> numpy: page-locked destinations (torch's caching host allocator reuses
+    them from one snapshot to the next), every copy queued on the current stream, one wait."""
+    if not ts or not ts[0].is_cuda:
+        return [t.cpu().numpy() for t in ts]
+    out = []
+    for t in ts:
+        h = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        h.copy_(t, non_blocking=True)
+        out.append(h)
+    torch.cuda.current_stream(ts[0].device).synchronize()
+    return [h.numpy() for h in out]
+
+
 class _StateMixin:
     """Methods of KeyedWindowOperator (mixed in; state lives in the native step)."""
 
@@ -105,13 +119,15 @@ class _StateMixin:
             cnt = cnt_g[idx]
             sel = cnt > 0
             keys = keys_g[live][None, :].expand_as(idx)[sel].contiguous()
-            kg = K.keygroups(keys, max_parallelism=self.max_parallelism, hash_mode=self.hash_mode,
-                             jhash=self.jhash).cpu().numpy()
-            cols = {"key": keys.cpu().numpy(),
-                    "pane": panes[:, None].expand_as(idx)[sel].cpu().numpy(),
-                    "acc": acc_g[idx][sel].cpu().numpy(),
-                    "cnt": cnt[sel].cpu().numpy(),
-                    "dirty": dirty_g[idx][sel].cpu().numpy()}
+            kgd = K.keygroups(keys, max_parallelism=self.max_parallelism, hash_mode=self.hash_mode,
+                              jhash=self.jhash)
+            # Rows in file order (key group, stable) before they leave the device: the state file
+            # writer then writes the columns as they are (csrc/kg_file.h).
+            kgd, order = torch.sort(kgd, stable=True)
+            at = idx[sel][order]
+            kg, *vals = _to_host([kgd, keys[order], panes[:, None].expand_as(idx)[sel][order],
+                                  acc_g[at], cnt[sel][order], dirty_g[at]])
+            cols = dict(zip(("key", "pane", "acc", "cnt", "dirty"), vals))
         tier = self._snapshot_tier()
         if tier is not None and tier.nrows:
             # Spilled state travels in the same rows (restore folds duplicate (key, pane) rows).

@@ -43,6 +43,34 @@ def _fires(out):
                   for r in out for k, a, c in zip(r.keys, r.raw, r.counts))
 
 
+@pytest.mark.parametrize("n", [1000, 2_500_000])  # 2.5M 8-byte rows: several 16 MB pieces
+def test_kg_file_sorted_and_unsorted_rows_write_the_same_file(tmp_path, n):
+    """The state file writer (csrc/kg_file.h) writes kg-sorted input as it is and permutes any
+    other input (stable counting sort, threaded gather): both give the same file, and a key-group
+    range read returns exactly that range's rows in input order."""
+    from pathlib import Path
+
+    from mxstream.runtime.checkpoint import (OperatorSnapshot, read_operator_rows,
+                                             write_operator_file)
+
+    rng = np.random.default_rng(3)
+    kg = rng.integers(0, 128, n).astype(np.int32)
+    cols = {"key": rng.integers(0, 1 << 40, n), "cnt": rng.integers(0, 99, n).astype(np.int32),
+            "dirty": rng.integers(0, 2, n).astype(np.uint8)}
+    order = np.argsort(kg, kind="stable")
+    d1, d2 = Path(tmp_path / "u"), Path(tmp_path / "s")
+    d1.mkdir()
+    d2.mkdir()
+    f1 = write_operator_file(d1, "w", 0, OperatorSnapshot(kg, cols), 128)
+    f2 = write_operator_file(d2, "w", 0, OperatorSnapshot(kg[order], {c: v[order] for c, v in
+                                                                        cols.items()}), 128)
+    assert (d1 / f1).read_bytes() == (d2 / f2).read_bytes()
+    got = read_operator_rows(d1, [f1], 40, 70)
+    sel = order[(kg[order] >= 40) & (kg[order] <= 70)]
+    for c, v in cols.items():
+        assert np.array_equal(got[c], v[sel]), c
+
+
 def test_window_checkpoint_restore_equals_uninterrupted(tmp_path):
     op = _win()
     storage = CheckpointStorage(tmp_path, job_id="a" * 32)
