@@ -153,9 +153,12 @@ def read_operator_rows(directory: Path, files: list[str], kg_lo: int, kg_hi: int
         sizes = [np.dtype(dt).itemsize for _, dt in cols]
         head, _lo, _hi, _offs, raw, nrows = m.read_kg_file(str(path), sizes, kg_lo, kg_hi)
         for (cname, dt), buf in zip(cols, raw):
-            parts.setdefault(cname, []).append(np.frombuffer(bytes(buf), dtype=np.dtype(dt)))
-    return {c: (np.concatenate(parts[c]) if parts.get(c) else np.zeros(0, np.dtype(dt)))
-            for c, dt in order}
+            parts.setdefault(cname, []).append(np.asarray(buf).view(np.dtype(dt)))
+    def join(c, dt):
+        p = parts.get(c)
+        return np.zeros(0, np.dtype(dt)) if not p else p[0] if len(p) == 1 else np.concatenate(p)
+
+    return {c: join(c, dt) for c, dt in order}
 
 
 def _atomic_write_json(path: Path, obj: dict) -> None:

@@ -1,5 +1,6 @@
 """Where a synchronous window checkpoint's time goes at BASELINE scale (10M keys): the operator's
-snapshot (device gather + D2H) and the key-group file write, timed separately.
+snapshot (device gather + D2H) and the key-group file write, timed separately; then the restore
+(file read, and the rebuild of a fresh operator's tables).
 
   python scripts/ckpt_breakdown.py --keys 10000000 --steps 4
 """
@@ -19,7 +20,7 @@ import torch  # noqa: E402
 
 from mxstream.models.bench_tumbling import TumblingBenchConfig, TumblingWindowBench  # noqa: E402
 from mxstream.parallel.comm import LocalComm  # noqa: E402
-from mxstream.runtime.checkpoint import write_operator_file  # noqa: E402
+from mxstream.runtime.checkpoint import read_operator_rows, write_operator_file  # noqa: E402
 
 
 def main() -> int:
@@ -48,6 +49,18 @@ def main() -> int:
             out["write_ms"].append(round((t2 - t1) * 1e3, 2))
             out["rows"] = int(len(snap.kg))
             out["bytes"] = int(sum(v.nbytes for v in snap.columns.values()))
+        fresh = TumblingWindowBench(TumblingBenchConfig(batch=a.batch, keys=a.keys), LocalComm(),
+                                    dev)
+        out["read_ms"], out["restore_ms"] = [], []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            rows = read_operator_rows(Path(d), ["window-0.kg"], 0, b.op.max_parallelism - 1)
+            t1 = time.perf_counter()
+            fresh.op.restore_state(rows, snap.meta)
+            sync()
+            t2 = time.perf_counter()
+            out["read_ms"].append(round((t1 - t0) * 1e3, 2))
+            out["restore_ms"].append(round((t2 - t1) * 1e3, 2))
     print(json.dumps(out))
     return 0
 
