@@ -10,7 +10,7 @@
 # under `rocprofv3 --kernel-trace --stats` from /tmp, output in gpurun_out/TAG_name/ ("pmem:"
 # adds --memory-copy-trace).
 #
-# Shortcuts for STEP: "tests" (all GPU tests), "bench" (bench.py 24/6),
+# Shortcuts for STEP: "tests" (all GPU tests), "bench" (bench.py 24/6), "smoke" (__graft_entry__.smoke),
 # "cfgN" (bench_configs --config N, default steps), "profN" (kernel profile of config N).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -24,6 +24,7 @@ expand() {
   case "$1" in
     tests) echo "tests|900|python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" ;;
     bench) echo "bench|300|python bench.py --steps 24 --warmup 6" ;;
+    smoke) echo "smoke|200|python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" ;;
     cfg[0-9]*) echo "${1}|400|python -m mxstream.models.bench_configs --config ${1#cfg}" ;;
     prof[0-9]*) echo "${1}|400|prof:python3 -m mxstream.models.bench_configs --config ${1#prof} --steps 10 --warmup 6" ;;
     *) echo "$1" ;;
