@@ -71,7 +71,7 @@ inline void gather(char* dst, const char* src, size_t isz, const uint64_t* perm,
 inline void write_kg_columns(const std::string& path, const std::string& header, uint32_t kg_lo,
                              uint32_t kg_hi, const int32_t* kgp, size_t n,
                              const std::vector<std::pair<const char*, size_t>>& cols,
-                             int threads = 8) {
+                             int threads = 8, size_t piece_bytes = (size_t)16 << 20) {
   const uint32_t ngroups = kg_hi - kg_lo + 1;
   std::vector<uint64_t> off(ngroups + 1, 0);
   bool sorted = true;
@@ -110,8 +110,8 @@ inline void write_kg_columns(const std::string& path, const std::string& header,
   if (fd < 0) throw std::runtime_error("cannot open " + tmp + ": " + std::strerror(errno));
   try {
     kgf::pwrite_all(fd, pre.data(), pre.size(), 0);
-    // Pieces of <= 16 MB of one column each; workers take them in order.
-    constexpr size_t kPiece = (size_t)16 << 20;
+    // Pieces of <= piece_bytes (16 MB) of one column each; workers take them in order.
+    const size_t kPiece = std::max<size_t>(1, piece_bytes);
     struct Piece {
       size_t col, r0, r1;
     };

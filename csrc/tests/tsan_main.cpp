@@ -16,11 +16,13 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <iterator>
 #include <string>
 #include <thread>
 #include <vector>
@@ -234,19 +236,40 @@ static int test_kg_writers() {
   std::vector<std::thread> th;
   std::vector<std::string> paths;
   for (int w = 0; w < 4; ++w) paths.push_back(tmp_path(("kg" + std::to_string(w)).c_str()));
+  // kg-sorted copy: the writer's no-permutation path
+  std::vector<int32_t> kgs(kg);
+  std::vector<int64_t> cols_s(n);
+  {
+    std::vector<size_t> ord(n);
+    for (size_t i = 0; i < n; ++i) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return kg[a] < kg[b]; });
+    for (size_t i = 0; i < n; ++i) {
+      kgs[i] = kg[ord[i]];
+      cols_s[i] = col[ord[i]];
+    }
+  }
+  // Writers 0/1: unsorted input (threaded gather), writers 2/3: sorted input; 64 KB pieces so
+  // each file is written by the writer's own pool of 4 threads.
   for (int w = 0; w < 4; ++w)
     th.emplace_back([&, w] {
-      write_kg_columns(paths[w], "{\"rank\": " + std::to_string(w) + "}", 0, 127, kg.data(), n,
-                       {{(const char*)col.data(), 8}});
+      const bool srt = w >= 2;
+      write_kg_columns(paths[w], "{\"rank\": " + std::to_string(w % 2) + "}", 0, 127,
+                       srt ? kgs.data() : kg.data(), n,
+                       {{(const char*)(srt ? cols_s.data() : col.data()), 8},
+                        {(const char*)(srt ? kgs.data() : kg.data()), 4}},
+                       4, (size_t)64 << 10);
     });
   for (auto& x : th) x.join();
+  std::vector<std::string> body;
   for (auto& p : paths) {
     std::ifstream f(p, std::ios::binary);
-    char magic[8];
-    f.read(magic, 8);
-    if (!f || std::memcmp(magic, "MXSKG001", 8) != 0) return fail("kg file: " + p);
+    std::string b((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    if (b.size() < 8 || std::memcmp(b.data(), "MXSKG001", 8) != 0) return fail("kg file: " + p);
+    body.push_back(std::move(b));
     std::remove(p.c_str());
   }
+  // sorted and unsorted input of the same rows give the same file
+  if (body[0] != body[2] || body[1] != body[3]) return fail("kg file: sorted != unsorted input");
   return 0;
 }
 
