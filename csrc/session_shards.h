@@ -259,6 +259,13 @@ class ShardedCore {
     std::sort(k.begin(), k.end());
     return k;
   }
+  // snapshot() of every shard, built by the shards in parallel (shard order, as snapshot()).
+  std::vector<Columns> snapshot_parts() {
+    std::vector<Columns> part(sh_.size());
+    each([&](int s) { part[s] = sh_[s]->snapshot(); });
+    return part;
+  }
+
   Columns snapshot() const {
     Columns out;
     for (auto& s : sh_) {

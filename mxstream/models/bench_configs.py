@@ -454,7 +454,8 @@ def config4_spill(steps: int, warmup: int, batch: int = 1 << 22, active: int = 1
 
 def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_000,
             drift: int = 400_000, table_keys: int = 4_000_000, device: str = "cuda",
-            revisit: float = 0.0, promote: bool = True, pipeline: bool | None = None) -> dict:
+            revisit: float = 0.0, promote: bool = True, pipeline: bool | None = None,
+            ckpt: bool = False) -> dict:
     """Session windows (gap 5 s, 30 s allowed lateness) over a drifting active key set: each step
     draws events from `active` consecutive key ids whose window advances by `drift` ids, so keys
     go idle and their sessions close. The HBM slot table holds `table_keys` keys; idle keys whose
@@ -533,7 +534,39 @@ def config5(steps: int, warmup: int, batch: int = 1 << 24, active: int = 4_000_0
         _sync(dev)
         dt = time.perf_counter() - t0
     mt = op.metrics
-    return {"config": 5, "pipeline": op.pipeline, "metric": "events/sec (session-window alert + host-DRAM spill)",
+    ck = None
+    if ckpt:  # after the timed loop: one synchronous checkpoint of both tiers (untimed above)
+        import tempfile
+        from pathlib import Path
+
+        from ..runtime.checkpoint import write_operator_file
+
+        ck = {"snapshot_ms": [], "write_ms": []}
+        with tempfile.TemporaryDirectory() as d:
+            for _ in range(2):
+                _sync(dev)
+                c0 = time.perf_counter()
+                snap = op.snapshot_state()
+                c1 = time.perf_counter()
+                write_operator_file(Path(d), "session", 0, snap, op.max_parallelism)
+                c2 = time.perf_counter()
+                ck["snapshot_ms"].append(round((c1 - c0) * 1e3, 2))
+                ck["write_ms"].append(round((c2 - c1) * 1e3, 2))
+            # split of the snapshot: the two tiers' rows, then the key groups on the host
+            from ..ops import kernels as KK
+
+            _sync(dev)
+            c0 = time.perf_counter()
+            rows = op.snapshot()
+            c1 = time.perf_counter()
+            KK.keygroups(torch.from_numpy(np.ascontiguousarray(rows["key"], dtype=np.int64)),
+                         max_parallelism=op.max_parallelism)
+            c2 = time.perf_counter()
+            ck["rows_ms"] = round((c1 - c0) * 1e3, 2)
+            ck["keygroups_ms"] = round((c2 - c1) * 1e3, 2)
+            ck["rows"] = int(len(snap.kg))
+            ck["bytes"] = int(sum(v.nbytes for v in snap.columns.values()))
+    return {"config": 5, "pipeline": op.pipeline, "checkpoint": ck, "metric": "events/sec (session-window alert + host-DRAM spill)",
             "value": batch * steps / dt, "unit": "events/s", "ms_per_step": dt / steps * 1e3,
             "p50_alert_latency_ms": statistics.median(lat) if lat else None,
             "p99_alert_latency_ms": (sorted(lat)[min(len(lat) - 1, int(0.99 * len(lat)))]
@@ -885,6 +918,8 @@ def main(argv=None) -> int:
                     help="config 5: fold records of spilled keys in host DRAM (no promotion to HBM)")
     ap.add_argument("--spill", action="store_true",
                     help="configs 2/4: key space outgrowing the HBM table (host-DRAM tier)")
+    ap.add_argument("--ckpt", action="store_true",
+                    help="config 5: time one synchronous checkpoint after the timed loop")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="config 5: the unpipelined session step")
     ap.add_argument("--revisit", type=float, default=0.0,
@@ -936,7 +971,8 @@ def main(argv=None) -> int:
                     mfma=not a.valu, zipf=a.zipf)
     else:
         r = config5(a.steps, a.warmup, a.batch or (1 << 24), device=a.device, revisit=a.revisit,
-                    promote=not a.host_fold, pipeline=False if a.no_pipeline else None)
+                    promote=not a.host_fold, pipeline=False if a.no_pipeline else None,
+                    ckpt=a.ckpt)
     print(json.dumps(r), flush=True)
     return 0
 

@@ -1426,15 +1426,20 @@ class KeyedSessionOperator:
             self._join_spill()
         parts = [self.store.snapshot()]
         if self.gpu:
-            keys = self.keys_g.cpu().numpy()
-            rec = self.sess.view(self.nslots, K_SESS, 4).cpu().numpy()
-            cnt = rec[:, :, 3] & 0xFFFFFFFF
-            live = (keys != EMPTY_KEY) & (keys != TOMB_KEY)
-            for j in range(K_SESS):
-                sel = live & (cnt[:, j] > 0)
-                parts.append({"key": keys[sel], "start": rec[sel, j, 0], "end": rec[sel, j, 1],
-                              "acc": rec[sel, j, 2], "cnt": cnt[sel, j],
-                              "flags": rec[sel, j, 3] >> 32})
+            # Live sessions selected on the device (session-index-major, then slot), so only
+            # their rows cross to the host, into page-locked buffers.
+            from .window_state import _to_host
+
+            keys = self.keys_g
+            rec = self.sess.view(self.nslots, K_SESS, 4)
+            w3 = rec[:, :, 3]
+            live = ((keys != EMPTY_KEY) & (keys != TOMB_KEY))[None, :] & \
+                ((w3 & 0xFFFFFFFF) > 0).t()
+            j, s = live.nonzero(as_tuple=True)
+            r = rec[s, j]
+            cols = _to_host([keys[s], r[:, 0], r[:, 1], r[:, 2], r[:, 3] & 0xFFFFFFFF,
+                             r[:, 3] >> 32])
+            parts.append(dict(zip(("key", "start", "end", "acc", "cnt", "flags"), cols)))
         return {f: np.concatenate([p[f] for p in parts]) for f in
                 ("key", "start", "end", "acc", "cnt", "flags")}
 
