@@ -282,7 +282,10 @@ class SessionStore {
     auto g = joined();
     return to_np(c_.key_list());
   }
-  py::dict snapshot_np() {
+  // extra > 0: every column gets `extra` more rows after the store's, left for the caller to
+  // fill (the HBM tier's rows: no concatenation afterwards).
+  py::dict snapshot_np(int64_t extra) {
+    if (extra < 0) throw std::invalid_argument("extra < 0");
     auto g = joined();
     // The shards build their rows in parallel, then copy them into the numpy columns in
     // parallel, without the GIL (one thread concatenating the shards' vectors and a second copy
@@ -298,7 +301,7 @@ class SessionStore {
     py::dict d;
     int64_t* cols[6];
     for (int c = 0; c < 6; ++c) {
-      I64Array a((py::ssize_t)offs.back());
+      I64Array a((py::ssize_t)(offs.back() + (size_t)extra));
       cols[c] = a.mutable_data();
       d[names[c]] = a;
     }
@@ -623,7 +626,7 @@ void bind_sessions(py::module_& m) {
       .def("num_cold_rows", &SessionStore::num_cold_rows)
       .def("bytes", &SessionStore::bytes)
       .def("key_list", &SessionStore::key_list_np)
-      .def("snapshot", &SessionStore::snapshot_np)
+      .def("snapshot", &SessionStore::snapshot_np, py::arg("extra") = 0)
       .def("spill_submit", &SessionStore::spill_submit, py::arg("stream"), py::arg("slab"),
            py::arg("ctr_off"), py::arg("col_off"), py::arg("rows"), py::arg("expire_wm") = py::none())
       .def("spill_submitted", &SessionStore::spill_submitted)

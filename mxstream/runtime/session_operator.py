@@ -1424,24 +1424,26 @@ class KeyedSessionOperator:
         self._sync_pending()
         if self.gpu:
             self._join_spill()
-        parts = [self.store.snapshot()]
-        if self.gpu:
-            # Live sessions selected on the device (session-index-major, then slot), so only
-            # their rows cross to the host, into page-locked buffers.
-            from .window_state import _to_host
-
-            keys = self.keys_g
-            rec = self.sess.view(self.nslots, K_SESS, 4)
-            w3 = rec[:, :, 3]
-            live = ((keys != EMPTY_KEY) & (keys != TOMB_KEY))[None, :] & \
-                ((w3 & 0xFFFFFFFF) > 0).t()
-            j, s = live.nonzero(as_tuple=True)
+        names = ("key", "start", "end", "acc", "cnt", "flags")
+        if not self.gpu:
+            return self.store.snapshot()
+        # Live HBM sessions selected on the device (session-index-major, then slot); only their
+        # rows cross to the host, straight into the tail of the store's snapshot columns.
+        keys = self.keys_g
+        rec = self.sess.view(self.nslots, K_SESS, 4)
+        live = ((keys != EMPTY_KEY) & (keys != TOMB_KEY))[None, :] & \
+            ((rec[:, :, 3] & 0xFFFFFFFF) > 0).t()
+        j, s = live.nonzero(as_tuple=True)
+        n_dev = int(s.numel())
+        out = self.store.snapshot(n_dev)
+        if n_dev:
+            n0 = len(out["key"]) - n_dev
             r = rec[s, j]
-            cols = _to_host([keys[s], r[:, 0], r[:, 1], r[:, 2], r[:, 3] & 0xFFFFFFFF,
-                             r[:, 3] >> 32])
-            parts.append(dict(zip(("key", "start", "end", "acc", "cnt", "flags"), cols)))
-        return {f: np.concatenate([p[f] for p in parts]) for f in
-                ("key", "start", "end", "acc", "cnt", "flags")}
+            cols = (keys[s], r[:, 0], r[:, 1], r[:, 2], r[:, 3] & 0xFFFFFFFF, r[:, 3] >> 32)
+            for f, t in zip(names, cols):
+                torch.from_numpy(out[f][n0:]).copy_(t, non_blocking=True)
+            torch.cuda.current_stream(keys.device).synchronize()
+        return out
 
     # ---- checkpoint / restore (runtime/checkpoint.py) --------------------------------------
     def owned_key_groups(self) -> tuple[int, int]:
